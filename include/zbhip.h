@@ -1,0 +1,314 @@
+/*
+ * zbhip.h — C ABI of libzbhip.so, the MI355X batch executor for Zeebe's BPMN
+ * element-lifecycle hot path.
+ *
+ * The library replaces, for one partition, everything from
+ * `Engine.process` (engine/src/main/java/io/camunda/zeebe/engine/Engine.java:99-131)
+ * down to the zb-db column-family mutations, for the supported element subset
+ * (process, none start/end event, service task, exclusive gateway, parallel
+ * gateway).  It is meant to sit behind the stream-platform `RecordProcessor`
+ * API (stream-platform/src/main/java/io/camunda/zeebe/stream/api/RecordProcessor.java:17-108):
+ * a Java host adapter buffers a window of hot-path commands from the log,
+ * submits them, runs them to quiescence and re-emits the drained records per
+ * source command through `ProcessingResultBuilder`.
+ *
+ * Conventions:
+ *  - a handle is one partition; every call on one handle is single-threaded
+ *    (mirrors the partition actor); different handles may run concurrently;
+ *  - errors are negative ZBHIP_E* codes, nothing throws across the ABI;
+ *  - device memory is owned by the handle, host buffers by the caller;
+ *  - keys are generated on the device as per-instance ordinals and relabelled
+ *    by zbhip_drain to the reference's keys, `Protocol.encodePartitionId(p, n)`
+ *    (protocol/src/main/java/io/camunda/zeebe/protocol/Protocol.java:98-100),
+ *    n advancing in submission (log) order exactly as `DbKeyGenerator.nextKey`
+ *    (stream-platform/.../state/DbKeyGenerator.java:39-42) would.
+ *
+ * Element indexing (shared contract with the CPU oracle): element index 0 is
+ * the process itself; the process's flow nodes and sequence flows follow in
+ * XML document order.
+ */
+#ifndef ZBHIP_H
+#define ZBHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZBHIP_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define ZBHIP_OK 0
+#define ZBHIP_EINVAL -1     /* bad argument */
+#define ZBHIP_ENOMEM -2     /* capacity exhausted (instances, records, documents) */
+#define ZBHIP_EDEVICE -3    /* HIP runtime error */
+#define ZBHIP_EPARSE -4     /* BPMN/FEEL outside the supported subset */
+#define ZBHIP_EUNSUPP -5    /* construct outside the supported subset */
+#define ZBHIP_ESTATE -6     /* call out of order (e.g. drain before run) */
+#define ZBHIP_ENODEV -7     /* no usable gfx950 device */
+
+/* ---- protocol enums (protocol/src/main/resources/protocol.xml:23-72) ---- */
+enum zbhip_record_type { ZBHIP_RT_EVENT = 0, ZBHIP_RT_COMMAND = 1, ZBHIP_RT_REJECTION = 2 };
+enum zbhip_value_type {
+  ZBHIP_VT_JOB = 0,
+  ZBHIP_VT_PROCESS_INSTANCE = 5,
+  ZBHIP_VT_MESSAGE = 10,
+  ZBHIP_VT_MESSAGE_SUBSCRIPTION = 11,
+  ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION = 12,
+  ZBHIP_VT_VARIABLE = 17,
+  ZBHIP_VT_PROCESS_INSTANCE_CREATION = 19,
+  ZBHIP_VT_PROCESS_EVENT = 24
+};
+enum zbhip_rejection_type {
+  ZBHIP_REJ_INVALID_ARGUMENT = 0,
+  ZBHIP_REJ_NOT_FOUND = 1,
+  ZBHIP_REJ_ALREADY_EXISTS = 2,
+  ZBHIP_REJ_INVALID_STATE = 3,
+  ZBHIP_REJ_PROCESSING_ERROR = 4,
+  ZBHIP_REJ_NONE = 255
+};
+/* ProcessInstanceIntent (protocol/.../intent/ProcessInstanceIntent.java:22-35) */
+enum zbhip_pi_intent {
+  ZBHIP_PI_SEQUENCE_FLOW_TAKEN = 1,
+  ZBHIP_PI_ELEMENT_ACTIVATING = 2,
+  ZBHIP_PI_ELEMENT_ACTIVATED = 3,
+  ZBHIP_PI_ELEMENT_COMPLETING = 4,
+  ZBHIP_PI_ELEMENT_COMPLETED = 5,
+  ZBHIP_PI_ELEMENT_TERMINATING = 6,
+  ZBHIP_PI_ELEMENT_TERMINATED = 7,
+  ZBHIP_PI_ACTIVATE_ELEMENT = 8,
+  ZBHIP_PI_COMPLETE_ELEMENT = 9,
+  ZBHIP_PI_TERMINATE_ELEMENT = 10
+};
+/* JobIntent CREATED=0 COMPLETE=1 COMPLETED=2; VariableIntent CREATED=0 UPDATED=1;
+ * ProcessEventIntent TRIGGERING=0; ProcessInstanceCreationIntent CREATE=0 CREATED=1 */
+enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2 };
+enum { ZBHIP_VAR_CREATED = 0, ZBHIP_VAR_UPDATED = 1 };
+enum { ZBHIP_PE_TRIGGERING = 0 };
+enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
+
+/* BpmnElementType / BpmnEventType ordinals (protocol/.../value/BpmnElementType.java:24-58,
+ * BpmnEventType.java:24-35) */
+enum zbhip_element_type {
+  ZBHIP_EL_UNSPECIFIED = 0,
+  ZBHIP_EL_PROCESS = 1,
+  ZBHIP_EL_SUB_PROCESS = 2,
+  ZBHIP_EL_EVENT_SUB_PROCESS = 3,
+  ZBHIP_EL_START_EVENT = 4,
+  ZBHIP_EL_INTERMEDIATE_CATCH_EVENT = 5,
+  ZBHIP_EL_INTERMEDIATE_THROW_EVENT = 6,
+  ZBHIP_EL_BOUNDARY_EVENT = 7,
+  ZBHIP_EL_END_EVENT = 8,
+  ZBHIP_EL_SERVICE_TASK = 9,
+  ZBHIP_EL_RECEIVE_TASK = 10,
+  ZBHIP_EL_USER_TASK = 11,
+  ZBHIP_EL_MANUAL_TASK = 12,
+  ZBHIP_EL_TASK = 13,
+  ZBHIP_EL_EXCLUSIVE_GATEWAY = 14,
+  ZBHIP_EL_PARALLEL_GATEWAY = 15,
+  ZBHIP_EL_EVENT_BASED_GATEWAY = 16,
+  ZBHIP_EL_INCLUSIVE_GATEWAY = 17,
+  ZBHIP_EL_SEQUENCE_FLOW = 18
+};
+enum zbhip_event_type {
+  ZBHIP_EV_UNSPECIFIED = 0,
+  ZBHIP_EV_CONDITIONAL = 1,
+  ZBHIP_EV_ERROR = 2,
+  ZBHIP_EV_ESCALATION = 3,
+  ZBHIP_EV_LINK = 4,
+  ZBHIP_EV_MESSAGE = 5,
+  ZBHIP_EV_NONE = 6,
+  ZBHIP_EV_SIGNAL = 7,
+  ZBHIP_EV_TERMINATE = 8,
+  ZBHIP_EV_TIMER = 9
+};
+
+/* ---- compiled process (deploy-time CSR tables) -------- */
+#define ZBHIP_NONE16 0xFFFFu
+
+typedef struct zbhip_element {
+  uint8_t element_type;  /* zbhip_element_type */
+  uint8_t event_type;    /* zbhip_event_type */
+  uint16_t out_begin;    /* outgoing flows: out_flow[out_begin .. out_begin+out_count) in getOutgoing() order */
+  uint16_t out_count;
+  uint16_t in_count;     /* incoming arity (parallel-gateway join arity) */
+  uint16_t flow_source;  /* sequence flow: source node; else ZBHIP_NONE16 */
+  uint16_t flow_target;  /* sequence flow: target node; else ZBHIP_NONE16 */
+  uint16_t condition;    /* sequence flow: condition index; ZBHIP_NONE16 = no condition */
+  uint16_t default_flow; /* exclusive gateway: default flow element; else ZBHIP_NONE16 */
+  uint16_t job_type;     /* service task: string-table index of the job type */
+  uint16_t job_retries;  /* service task: static retries */
+  uint16_t join_slot;    /* sequence flow into a parallel gateway: its taken-counter slot; else NONE */
+  uint16_t id;           /* string-table index of the element id */
+} zbhip_element;
+
+/* FEEL condition bytecode (subset of feel-scala 1.17.0 boolean expressions,
+ * SURVEY §8a row 16).  Stack machine over {NUMBER(scaled int64), BOOLEAN, NULL}. */
+enum zbhip_op {
+  ZBHIP_OP_END = 0,
+  ZBHIP_OP_PUSH_VAR = 1,   /* arg = variable-name id */
+  ZBHIP_OP_PUSH_NUM = 2,   /* literal = value * 10^ZBHIP_DEC_SCALE */
+  ZBHIP_OP_PUSH_BOOL = 3,  /* arg = 0/1 */
+  ZBHIP_OP_PUSH_NULL = 4,
+  ZBHIP_OP_LT = 5, ZBHIP_OP_LE = 6, ZBHIP_OP_GT = 7, ZBHIP_OP_GE = 8,
+  ZBHIP_OP_EQ = 9, ZBHIP_OP_NE = 10,
+  ZBHIP_OP_AND = 11, ZBHIP_OP_OR = 12, ZBHIP_OP_NOT = 13
+};
+#define ZBHIP_DEC_SCALE 6   /* fixed decimal scale of NUMBER values on the device */
+
+typedef struct zbhip_insn {
+  uint8_t op;
+  uint8_t pad[3];
+  uint32_t arg;
+  int64_t literal;
+} zbhip_insn;
+
+typedef struct zbhip_process_csr {
+  uint32_t n_elements;           /* elements[0] is the process */
+  const zbhip_element* elements;
+  uint32_t n_out;
+  const uint16_t* out_flow;      /* CSR targets of out_begin/out_count */
+  uint32_t n_conditions;
+  const uint32_t* cond_begin;    /* condition c: code[cond_begin[c] .. cond_begin[c+1]) */
+  uint32_t n_code;
+  const zbhip_insn* code;
+  uint32_t n_strings;
+  const char* const* strings;    /* ids, job types, variable names (NUL-terminated) */
+  uint16_t none_start;           /* element index of the none start event (NONE = none) */
+  uint16_t n_join_slots;         /* taken-sequence-flow counters per instance */
+  int64_t process_definition_key;
+  int32_t version;
+  uint16_t bpmn_process_id;      /* string index */
+  uint16_t pad;
+} zbhip_process_csr;
+
+/* Host-side compiler: BPMN XML -> CSR (engine/.../deployment/model/transformation/BpmnTransformer.java:109-127).
+ * Returns ZBHIP_OK or ZBHIP_EPARSE/ZBHIP_EUNSUPP with a message in err. */
+int zbhip_compile_bpmn(const char* xml, size_t len, int64_t process_definition_key, int32_t version,
+                       zbhip_process_csr** out, char* err, size_t err_cap);
+void zbhip_free_csr(zbhip_process_csr* csr);
+
+/* ---- partition handle -------------------------------------------------- */
+typedef struct zbhip_config {
+  int32_t partition_id;          /* 1-based, as in Zeebe */
+  int32_t partition_count;
+  int32_t device;                /* HIP device ordinal */
+  int32_t max_commands_in_batch; /* StreamProcessorContext.DEFAULT_MAX_COMMANDS_IN_BATCH = 100 */
+  uint32_t max_instances;        /* instance slots in HBM */
+  uint32_t max_commands;         /* commands per submitted window */
+  uint32_t max_records_per_batch;/* record slots per command (0 = derive from deployed processes) */
+  uint32_t max_doc_entries;      /* variable-document entries per window */
+  int64_t initial_key;           /* last key already generated in the partition (0 = fresh) */
+  void* stream;                  /* hipStream_t to launch on (NULL = handle-owned stream) */
+} zbhip_config;
+
+typedef struct zbhip_handle zbhip_handle;
+
+int zbhip_open(const zbhip_config* cfg, zbhip_handle** out);
+void zbhip_close(zbhip_handle* h);
+int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* process_idx_out);
+/* Interns a variable name for this partition; returns its id (>=0) or an error. */
+int zbhip_intern(zbhip_handle* h, const char* name);
+const char* zbhip_string(zbhip_handle* h, uint32_t process_idx, uint32_t string_idx);
+const char* zbhip_name(zbhip_handle* h, uint32_t name_id);
+
+/* ---- commands ------------------------------------------------------------ */
+enum zbhip_command_kind {
+  ZBHIP_CMD_CREATE = 1,        /* PROCESS_INSTANCE_CREATION:CREATE (CreateProcessInstanceProcessor.java:129-158) */
+  ZBHIP_CMD_JOB_COMPLETE = 2   /* JOB:COMPLETE (JobCompleteProcessor.java:47-92) */
+};
+
+enum zbhip_doc_type { ZBHIP_DOC_NIL = 0, ZBHIP_DOC_BOOL = 1, ZBHIP_DOC_INT = 2, ZBHIP_DOC_DEC = 3,
+                      ZBHIP_DOC_OTHER = 4 };
+
+/* One entry of a variable document (a msgpack map entry on the reference side).
+ * DEC values are value * 10^ZBHIP_DEC_SCALE (exact decimal). */
+typedef struct zbhip_doc_entry {
+  uint32_t name_id;
+  uint8_t type;
+  uint8_t pad[3];
+  int64_t value;
+} zbhip_doc_entry;
+
+typedef struct zbhip_command {
+  uint32_t instance;    /* instance slot; CREATE: the slot to create the instance in */
+  uint8_t kind;         /* zbhip_command_kind */
+  uint8_t doc_count;    /* entries of the variable document (0 = empty document) */
+  uint16_t ref;         /* CREATE: process index; JOB_COMPLETE: job key ordinal in the instance */
+  uint32_t doc_begin;   /* first entry in the window's document array */
+  uint32_t pad;
+} zbhip_command;
+
+/* Submits a window of commands in log order.  Host buffers are copied. */
+int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs,
+                 size_t n_docs);
+/* Same, from device-resident arrays already in HBM (no copy; must stay valid until run returns). */
+int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,
+                        const zbhip_doc_entry* dev_docs, size_t n_docs);
+
+#define ZBHIP_RUN_NO_RESULTS 1u  /* skip the D2H copy of results (benchmarking) */
+#define ZBHIP_RUN_TIMED 2u       /* record HIP events around each kernel */
+/* Processes the submitted window to quiescence.  Returns #commands processed or <0. */
+int zbhip_run(zbhip_handle* h, uint32_t flags);
+
+/* ---- results ------------------------------------------------------------- */
+/* Drained record (one per follow-up record of a batch), ordered by (source, ordinal). */
+typedef struct zbhip_record {
+  int64_t key;                  /* relabelled to the reference key */
+  int64_t scope_key;            /* PI: flowScopeKey; JOB: elementInstanceKey; VARIABLE/PROCESS_EVENT:
+                                   scopeKey; PI_CREATION: processInstanceKey */
+  int64_t process_instance_key;
+  int64_t source_index;         /* index of the batch's initial command in submission order */
+  int32_t process_idx;
+  int32_t element_idx;          /* element/flow index; VARIABLE: variable-name id; -1 none */
+  uint8_t record_type;
+  uint8_t value_type;
+  uint8_t intent;
+  uint8_t rejection_type;       /* ZBHIP_REJ_NONE unless record_type == REJECTION */
+  uint32_t ordinal;             /* position within the batch */
+  int64_t aux;                  /* VARIABLE: document entry index; JOB:COMPLETED: source doc; else -1 */
+} zbhip_record;
+
+int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out);
+/* Number of records the last run produced (before draining). */
+int64_t zbhip_pending_records(zbhip_handle* h);
+
+typedef struct zbhip_stats {
+  uint64_t commands;            /* commands processed by the last run */
+  uint64_t records;             /* records emitted */
+  uint64_t transitions;         /* PI events with element-lifecycle/SFT intents */
+  uint64_t completed_instances; /* PROCESS ELEMENT_COMPLETED */
+  uint64_t keys;                /* keys generated */
+  uint64_t fallback;            /* batches flagged for the fallback path */
+  double step_ms;               /* device time of the lifecycle kernel(s), ZBHIP_RUN_TIMED */
+  double compact_ms;            /* device time of the compaction kernel(s) */
+  uint32_t rounds;              /* per-instance serialisation rounds of the window */
+  uint32_t launches;
+} zbhip_stats;
+int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out);
+
+/* Exports the partition state as canonical text rows, one per zb-db column-family
+ * entry ("CF|key parts|value fields"), keys relabelled; the sink is called per row. */
+typedef void (*zbhip_state_sink)(void* ctx, const char* row);
+int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx);
+
+/* Instances whose last batch needs the fallback path (incident, FEEL outside the
+ * subset, batch-limit overflow, capacity).  Their state was left untouched. */
+int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_out);
+
+/* Maps a drained (relabelled) key back to (instance, key ordinal) for building
+ * follow-up commands (e.g. JOB:COMPLETE).  Returns ZBHIP_EINVAL if unknown. */
+int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal);
+
+/* Rejection reason text exactly as the reference writes it. */
+int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, size_t cap);
+
+/* Library build information ("gfx950 …"). */
+const char* zbhip_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZBHIP_H */

@@ -1,0 +1,151 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU oracle (oracle/zb_oracle.cpp).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module; the product (zeebe_amd) never does.  Parity is pinned by the
+golden vectors in tests/golden/ (the Java reference cannot run in this image).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from zeebe_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "zb_oracle.cpp")):
+            build()
+        L = C.CDLL(LIB)
+        L.zbo_new.restype = C.c_void_p
+        L.zbo_new.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64]
+        L.zbo_free.argtypes = [C.c_void_p]
+        L.zbo_last_error.restype = C.c_char_p
+        L.zbo_last_error.argtypes = [C.c_void_p]
+        L.zbo_deploy_xml.argtypes = [C.c_void_p, C.c_char_p, C.c_int64, C.c_int]
+        L.zbo_intern.argtypes = [C.c_void_p, C.c_char_p]
+        L.zbo_name.restype = C.c_char_p
+        L.zbo_name.argtypes = [C.c_void_p, C.c_int]
+        L.zbo_n_elements.argtypes = [C.c_void_p, C.c_int]
+        L.zbo_element_id.restype = C.c_char_p
+        L.zbo_element_id.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.zbo_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.zbo_run.argtypes = [C.c_void_p]
+        L.zbo_n_records.restype = C.c_size_t
+        L.zbo_n_records.argtypes = [C.c_void_p]
+        L.zbo_records.restype = C.c_size_t
+        L.zbo_records.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.zbo_reason.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        L.zbo_clear_records.argtypes = [C.c_void_p]
+        L.zbo_resolve.restype = C.c_int64
+        L.zbo_resolve.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.zbo_state.restype = C.c_size_t
+        L.zbo_state.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        L.zbo_fallback.restype = C.c_size_t
+        L.zbo_fallback.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.zbo_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint64)]
+        L.zbo_bench.restype = C.c_double
+        L.zbo_bench.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        _lib = L
+    return _lib
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+class Oracle:
+    """One partition of the CPU restatement (EngineRule.singlePartition analogue)."""
+
+    def __init__(self, partition_id=1, partition_count=1, max_commands_in_batch=100, initial_key=0):
+        self.L = lib()
+        self.h = self.L.zbo_new(partition_id, partition_count, max_commands_in_batch, initial_key)
+        self.partition_id = partition_id
+
+    def close(self):
+        if self.h:
+            self.L.zbo_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def deploy(self, xml, process_definition_key=2251799813685249, version=1):
+        if isinstance(xml, str):
+            xml = xml.encode()
+        r = self.L.zbo_deploy_xml(self.h, xml, process_definition_key, version)
+        if r < 0:
+            raise OracleError(self.L.zbo_last_error(self.h).decode())
+        return r
+
+    def intern(self, name):
+        return self.L.zbo_intern(self.h, name.encode())
+
+    def name(self, nid):
+        return self.L.zbo_name(self.h, nid).decode()
+
+    def element_id(self, proc, elem):
+        return self.L.zbo_element_id(self.h, proc, elem).decode()
+
+    def submit(self, cmds, docs=None):
+        cmds = np.ascontiguousarray(cmds, dtype=abi.COMMAND_DTYPE)
+        docs = np.ascontiguousarray(docs if docs is not None else abi.make_docs(0), dtype=abi.DOC_DTYPE)
+        self.L.zbo_submit(self.h, cmds.ctypes.data, len(cmds), docs.ctypes.data, len(docs))
+
+    def run(self):
+        r = self.L.zbo_run(self.h)
+        if r < 0:
+            raise OracleError(self.L.zbo_last_error(self.h).decode())
+        return r
+
+    def records(self):
+        n = self.L.zbo_n_records(self.h)
+        out = np.zeros(n, dtype=abi.RECORD_DTYPE)
+        self.L.zbo_records(self.h, out.ctypes.data, n)
+        return out
+
+    def reason(self, idx):
+        buf = C.create_string_buffer(1024)
+        self.L.zbo_reason(self.h, idx, buf, 1024)
+        return buf.value.decode()
+
+    def clear_records(self):
+        self.L.zbo_clear_records(self.h)
+
+    def resolve(self, instance, ordinal):
+        return self.L.zbo_resolve(self.h, instance, ordinal)
+
+    def state(self):
+        n = self.L.zbo_state(self.h, None, 0)
+        buf = C.create_string_buffer(n)
+        self.L.zbo_state(self.h, buf, n)
+        return [r for r in buf.value.decode().split("\n") if r]
+
+    def counters(self):
+        t, c, m = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self.L.zbo_counters(self.h, C.byref(t), C.byref(c), C.byref(m))
+        return {"transitions": t.value, "completed_instances": c.value, "commands": m.value}
+
+
+def bench(xml, threads, n_instances, phases, with_amount=False, seed=0x5EED03):
+    """CPU baseline: `threads` partitions, one per core (returns seconds, transitions, completed)."""
+    if isinstance(xml, str):
+        xml = xml.encode()
+    t, c = C.c_uint64(), C.c_uint64()
+    sec = lib().zbo_bench(xml, threads, n_instances, phases, 1 if with_amount else 0, seed, C.byref(t), C.byref(c))
+    if sec < 0:
+        raise OracleError("bench deploy failed")
+    return sec, t.value, c.value

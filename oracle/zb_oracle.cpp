@@ -1,0 +1,1537 @@
+// ============================================================================
+// zb_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of Zeebe's BPMN element-lifecycle hot path (reference:
+// honlyc/zeebe 8.4.0-SNAPSHOT, read-only at /root/reference).  It is the checker
+// the GPU executor is parity-tested against and the "port" CPU baseline timed by
+// bench.py.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+// may load it; the product (zeebe_amd/, libzbhip.so) never links or calls it.
+//
+// Parity pinning: the reference is Java 21 + Maven and cannot be built or run in
+// this image (no JDK); the oracle is pinned against golden vectors transcribed
+// from the reference's own tests and code-derived sequences,
+// see tests/golden/ and tests/test_oracle_golden.py.
+//
+// Every function cites the reference file:line it restates.  Paths are relative
+// to /root/reference/engine/src/main/java/io/camunda/zeebe/engine/ unless they
+// start with another module name.
+// ============================================================================
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "../include/zbhip.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Minimal XML reader (enough for BPMN 2.0 files written by the modeler or the
+// fluent builder).  Namespace prefixes are stripped.
+// ---------------------------------------------------------------------------
+struct XNode {
+  std::string name;
+  std::map<std::string, std::string> attrs;
+  std::string text;
+  std::vector<std::unique_ptr<XNode>> kids;
+  const XNode* child(const std::string& n) const {
+    for (auto& k : kids)
+      if (k->name == n) return k.get();
+    return nullptr;
+  }
+  std::string attr(const std::string& n, const std::string& dflt = "") const {
+    auto it = attrs.find(n);
+    return it == attrs.end() ? dflt : it->second;
+  }
+};
+
+static std::string strip_ns(const std::string& s) {
+  auto p = s.find(':');
+  return p == std::string::npos ? s : s.substr(p + 1);
+}
+
+static std::string xml_unescape(const std::string& s) {
+  std::string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '&') {
+      auto e = s.find(';', i);
+      if (e == std::string::npos) { o += s[i]; continue; }
+      std::string ent = s.substr(i + 1, e - i - 1);
+      if (ent == "lt") o += '<';
+      else if (ent == "gt") o += '>';
+      else if (ent == "amp") o += '&';
+      else if (ent == "quot") o += '"';
+      else if (ent == "apos") o += '\'';
+      else if (!ent.empty() && ent[0] == '#') {
+        long cp = ent.size() > 1 && ent[1] == 'x' ? strtol(ent.c_str() + 2, nullptr, 16)
+                                                  : strtol(ent.c_str() + 1, nullptr, 10);
+        if (cp < 128) o += (char)cp;
+      }
+      i = e;
+    } else {
+      o += s[i];
+    }
+  }
+  return o;
+}
+
+struct XmlParser {
+  const std::string& s;
+  size_t i = 0;
+  std::string err;
+  explicit XmlParser(const std::string& src) : s(src) {}
+  void skip_ws() { while (i < s.size() && isspace((unsigned char)s[i])) ++i; }
+  bool parse_misc() {  // comments, PIs, doctype
+    for (;;) {
+      skip_ws();
+      if (s.compare(i, 4, "<!--") == 0) {
+        auto e = s.find("-->", i);
+        if (e == std::string::npos) return false;
+        i = e + 3;
+      } else if (s.compare(i, 2, "<?") == 0) {
+        auto e = s.find("?>", i);
+        if (e == std::string::npos) return false;
+        i = e + 2;
+      } else if (s.compare(i, 2, "<!") == 0) {
+        auto e = s.find('>', i);
+        if (e == std::string::npos) return false;
+        i = e + 1;
+      } else {
+        return true;
+      }
+    }
+  }
+  std::unique_ptr<XNode> parse_element() {
+    if (!parse_misc() || i >= s.size() || s[i] != '<') { err = "expected element"; return nullptr; }
+    ++i;
+    auto n = std::make_unique<XNode>();
+    size_t st = i;
+    while (i < s.size() && !isspace((unsigned char)s[i]) && s[i] != '>' && s[i] != '/') ++i;
+    n->name = strip_ns(s.substr(st, i - st));
+    for (;;) {
+      skip_ws();
+      if (i >= s.size()) { err = "eof in tag"; return nullptr; }
+      if (s[i] == '/') {
+        if (s.compare(i, 2, "/>") != 0) { err = "bad tag end"; return nullptr; }
+        i += 2;
+        return n;
+      }
+      if (s[i] == '>') { ++i; break; }
+      size_t as = i;
+      while (i < s.size() && s[i] != '=' && !isspace((unsigned char)s[i])) ++i;
+      std::string an = s.substr(as, i - as);
+      skip_ws();
+      if (i >= s.size() || s[i] != '=') { err = "bad attribute"; return nullptr; }
+      ++i;
+      skip_ws();
+      char q = s[i];
+      if (q != '"' && q != '\'') { err = "bad attribute quote"; return nullptr; }
+      auto e = s.find(q, i + 1);
+      if (e == std::string::npos) { err = "eof in attribute"; return nullptr; }
+      n->attrs[strip_ns(an)] = xml_unescape(s.substr(i + 1, e - i - 1));
+      i = e + 1;
+    }
+    // content
+    for (;;) {
+      if (i >= s.size()) { err = "eof in content"; return nullptr; }
+      if (s.compare(i, 2, "</") == 0) {
+        auto e = s.find('>', i);
+        if (e == std::string::npos) { err = "eof in end tag"; return nullptr; }
+        i = e + 1;
+        return n;
+      }
+      if (s.compare(i, 9, "<![CDATA[") == 0) {
+        auto e = s.find("]]>", i);
+        if (e == std::string::npos) { err = "eof in cdata"; return nullptr; }
+        n->text += s.substr(i + 9, e - i - 9);
+        i = e + 3;
+        continue;
+      }
+      if (s.compare(i, 4, "<!--") == 0 || s.compare(i, 2, "<?") == 0) {
+        if (!parse_misc()) { err = "bad misc"; return nullptr; }
+        continue;
+      }
+      if (s[i] == '<') {
+        auto k = parse_element();
+        if (!k) return nullptr;
+        n->kids.push_back(std::move(k));
+        continue;
+      }
+      auto e = s.find('<', i);
+      if (e == std::string::npos) e = s.size();
+      n->text += xml_unescape(s.substr(i, e - i));
+      i = e;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// FEEL subset: boolean conditions over numbers/booleans/null
+// (feel-scala 1.17.0 is a third-party dependency absent from the tree:
+// parent/pom.xml:93,925-927).  Numbers are exact decimals (BigDecimal in
+// feel-scala, feel/.../MessagePackValueMapper.scala:41-71); held here as
+// __int128 scaled by 10^18.
+// ---------------------------------------------------------------------------
+enum VKind { V_NULL, V_BOOL, V_NUM, V_ERR };
+struct FVal {
+  VKind k = V_NULL;
+  __int128 n = 0;
+  bool b = false;
+};
+static const __int128 kScale18 = (__int128)1000000000000000000LL;
+
+struct FExpr {
+  enum Op { NUM, BOOL, NUL, VAR, CMP, AND, OR, NOT } op;
+  std::string cmp;  // "<" "<=" ">" ">=" "=" "!="
+  __int128 num = 0;
+  bool b = false;
+  std::string var;
+  std::unique_ptr<FExpr> l, r;
+};
+
+struct FeelParser {
+  std::string s;
+  size_t i = 0;
+  bool ok = true;
+  explicit FeelParser(std::string src) : s(std::move(src)) {}
+  void ws() { while (i < s.size() && isspace((unsigned char)s[i])) ++i; }
+  bool kw(const char* w) {
+    ws();
+    size_t n = strlen(w);
+    if (s.compare(i, n, w) == 0 && (i + n >= s.size() || !(isalnum((unsigned char)s[i + n]) || s[i + n] == '_'))) {
+      i += n;
+      return true;
+    }
+    return false;
+  }
+  std::unique_ptr<FExpr> parse_or() {
+    auto l = parse_and();
+    while (ok && kw("or")) {
+      auto e = std::make_unique<FExpr>();
+      e->op = FExpr::OR;
+      e->l = std::move(l);
+      e->r = parse_and();
+      l = std::move(e);
+    }
+    return l;
+  }
+  std::unique_ptr<FExpr> parse_and() {
+    auto l = parse_cmp();
+    while (ok && kw("and")) {
+      auto e = std::make_unique<FExpr>();
+      e->op = FExpr::AND;
+      e->l = std::move(l);
+      e->r = parse_cmp();
+      l = std::move(e);
+    }
+    return l;
+  }
+  std::unique_ptr<FExpr> parse_cmp() {
+    auto l = parse_atom();
+    ws();
+    static const char* ops[] = {"<=", ">=", "!=", "<", ">", "="};
+    for (auto o : ops) {
+      size_t n = strlen(o);
+      if (s.compare(i, n, o) == 0) {
+        i += n;
+        auto e = std::make_unique<FExpr>();
+        e->op = FExpr::CMP;
+        e->cmp = o;
+        e->l = std::move(l);
+        e->r = parse_atom();
+        return e;
+      }
+    }
+    return l;
+  }
+  std::unique_ptr<FExpr> parse_atom() {
+    ws();
+    auto e = std::make_unique<FExpr>();
+    if (i >= s.size()) { ok = false; return e; }
+    if (s[i] == '(') {
+      ++i;
+      auto in = parse_or();
+      ws();
+      if (i >= s.size() || s[i] != ')') ok = false;
+      else ++i;
+      return in;
+    }
+    if (kw("not")) {
+      ws();
+      if (i >= s.size() || s[i] != '(') { ok = false; return e; }
+      ++i;
+      e->op = FExpr::NOT;
+      e->l = parse_or();
+      ws();
+      if (i >= s.size() || s[i] != ')') ok = false;
+      else ++i;
+      return e;
+    }
+    if (kw("true")) { e->op = FExpr::BOOL; e->b = true; return e; }
+    if (kw("false")) { e->op = FExpr::BOOL; e->b = false; return e; }
+    if (kw("null")) { e->op = FExpr::NUL; return e; }
+    bool neg = false;
+    if (s[i] == '-') { neg = true; ++i; }
+    if (i < s.size() && (isdigit((unsigned char)s[i]) || s[i] == '.')) {
+      __int128 ip = 0, fp = 0, fs = 1;
+      while (i < s.size() && isdigit((unsigned char)s[i])) ip = ip * 10 + (s[i++] - '0');
+      if (i < s.size() && s[i] == '.') {
+        ++i;
+        int digits = 0;
+        while (i < s.size() && isdigit((unsigned char)s[i])) {
+          if (digits < 18) { fp = fp * 10 + (s[i] - '0'); fs *= 10; }
+          ++digits;
+          ++i;
+        }
+        if (digits > 18) ok = false;
+      }
+      e->op = FExpr::NUM;
+      e->num = ip * kScale18 + fp * (kScale18 / fs);
+      if (neg) e->num = -e->num;
+      return e;
+    }
+    if (neg) { ok = false; return e; }
+    if (isalpha((unsigned char)s[i]) || s[i] == '_') {
+      size_t st = i;
+      while (i < s.size() && (isalnum((unsigned char)s[i]) || s[i] == '_')) ++i;
+      e->op = FExpr::VAR;
+      e->var = s.substr(st, i - st);
+      ws();
+      if (i < s.size() && (s[i] == '.' || s[i] == '[' || s[i] == '(')) ok = false;  // paths/calls: outside subset
+      return e;
+    }
+    ok = false;
+    return e;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Process model (ExecutableProcess / ExecutableFlowNode / ExecutableSequenceFlow)
+// ---------------------------------------------------------------------------
+struct OEl {
+  std::string id;
+  int type = ZBHIP_EL_UNSPECIFIED;
+  int event = ZBHIP_EV_UNSPECIFIED;
+  std::vector<int> out, in, out_with_cond;
+  int src = -1, tgt = -1;
+  bool has_cond = false;
+  std::unique_ptr<FExpr> cond;
+  int default_flow = -1;
+  std::string job_type;
+  int retries = 3;
+};
+
+struct OProc {
+  std::string bpmn_id;
+  int64_t def_key = 0;
+  int version = 1;
+  std::vector<OEl> els;  // [0] = process
+  int none_start = -1;
+};
+
+// BpmnTransformer.transformDefinitions (deployment/model/transformation/BpmnTransformer.java:109-127)
+// with ModelWalker.walk (bpmn-model/.../traversal/ModelWalker.java:60-81): siblings are
+// pushed with addFirst, so sequence flows are connected in reverse document order
+// (SequenceFlowTransformer.connectWithFlowNodes), which fixes getOutgoing() order.
+static bool build_process(const XNode& proc, OProc& P, std::string& err) {
+  P.bpmn_id = proc.attr("id");
+  P.els.clear();
+  OEl pe;
+  pe.id = P.bpmn_id;
+  pe.type = ZBHIP_EL_PROCESS;
+  P.els.push_back(std::move(pe));
+  std::unordered_map<std::string, int> idx;
+  idx[P.bpmn_id] = 0;
+  std::vector<const XNode*> flows;
+  for (auto& k : proc.kids) {
+    const std::string& n = k->name;
+    OEl e;
+    e.id = k->attr("id");
+    if (n == "startEvent") {
+      e.type = ZBHIP_EL_START_EVENT;
+      // StartEventTransformer.java:40 — event type from the event definition
+      if (k->child("messageEventDefinition") || k->child("timerEventDefinition") ||
+          k->child("signalEventDefinition") || k->child("errorEventDefinition") ||
+          k->child("escalationEventDefinition") || k->child("conditionalEventDefinition")) {
+        err = "start event with event definition outside the supported subset";
+        return false;
+      }
+      e.event = ZBHIP_EV_NONE;
+    } else if (n == "endEvent") {
+      e.type = ZBHIP_EL_END_EVENT;
+      if (k->child("terminateEventDefinition") || k->child("errorEventDefinition") ||
+          k->child("messageEventDefinition") || k->child("escalationEventDefinition") ||
+          k->child("signalEventDefinition")) {
+        err = "end event with event definition outside the supported subset";
+        return false;
+      }
+      e.event = ZBHIP_EV_NONE;  // EndEventTransformer.java:37
+    } else if (n == "serviceTask") {
+      e.type = ZBHIP_EL_SERVICE_TASK;
+      const XNode* ext = k->child("extensionElements");
+      const XNode* td = ext ? ext->child("taskDefinition") : nullptr;
+      if (!td) { err = "service task without zeebe:taskDefinition"; return false; }
+      e.job_type = td->attr("type");
+      std::string r = td->attr("retries", "3");
+      if (e.job_type.empty() || e.job_type[0] == '=' || r.empty() || r[0] == '=') {
+        err = "job type/retries expressions outside the supported subset";
+        return false;
+      }
+      e.retries = atoi(r.c_str());
+      if (ext && (ext->child("ioMapping") || ext->child("taskHeaders"))) {
+        err = "io mappings / task headers outside the supported subset";
+        return false;
+      }
+    } else if (n == "exclusiveGateway") {
+      e.type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
+    } else if (n == "parallelGateway") {
+      e.type = ZBHIP_EL_PARALLEL_GATEWAY;
+    } else if (n == "sequenceFlow") {
+      e.type = ZBHIP_EL_SEQUENCE_FLOW;
+      flows.push_back(k.get());
+    } else if (n == "extensionElements" || n == "documentation" || n == "textAnnotation" ||
+               n == "association") {
+      continue;
+    } else {
+      err = "element <" + n + "> outside the supported subset";
+      return false;
+    }
+    if (e.id.empty()) { err = "element without id"; return false; }
+    idx[e.id] = (int)P.els.size();
+    P.els.push_back(std::move(e));
+  }
+  // gateway default flows (ExclusiveGatewayTransformer.transformDefaultFlow)
+  for (auto& k : proc.kids) {
+    if (k->name == "exclusiveGateway" && !k->attr("default").empty()) {
+      auto it = idx.find(k->attr("default"));
+      if (it == idx.end()) { err = "unknown default flow"; return false; }
+      P.els[idx[k->attr("id")]].default_flow = it->second;
+    }
+  }
+  // step 2 walk: reverse document order (ModelWalker.java:75-79)
+  for (auto it = flows.rbegin(); it != flows.rend(); ++it) {
+    const XNode* f = *it;
+    int fi = idx[f->attr("id")];
+    auto s = idx.find(f->attr("sourceRef"));
+    auto t = idx.find(f->attr("targetRef"));
+    if (s == idx.end() || t == idx.end()) { err = "flow with unknown source/target"; return false; }
+    OEl& fe = P.els[fi];
+    fe.src = s->second;
+    fe.tgt = t->second;
+    // SequenceFlowTransformer.parseCondition: runs before connectWithFlowNodes
+    if (const XNode* c = f->child("conditionExpression")) {
+      std::string txt = c->text;
+      size_t a = txt.find_first_not_of(" \t\r\n");
+      size_t b = txt.find_last_not_of(" \t\r\n");
+      txt = a == std::string::npos ? "" : txt.substr(a, b - a + 1);
+      fe.has_cond = true;
+      if (txt.empty() || txt[0] != '=') { err = "static (non-FEEL) condition outside the subset"; return false; }
+      FeelParser fp(txt.substr(1));
+      fe.cond = fp.parse_or();
+      fp.ws();
+      if (!fp.ok || fp.i != fp.s.size()) { err = "FEEL condition outside the subset: " + txt; return false; }
+    }
+    P.els[fe.src].out.push_back(fi);  // ExecutableFlowNode.addOutgoing
+    if (P.els[fe.src].type == ZBHIP_EL_EXCLUSIVE_GATEWAY && fe.has_cond)
+      P.els[fe.src].out_with_cond.push_back(fi);  // ExecutableExclusiveGateway.addOutgoing
+    P.els[fe.tgt].in.push_back(fi);
+  }
+  for (size_t i = 1; i < P.els.size(); ++i)
+    if (P.els[i].type == ZBHIP_EL_START_EVENT && P.els[i].event == ZBHIP_EV_NONE) P.none_start = (int)i;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Engine state (zb-db column families, protocol/.../ZbColumnFamilies.java)
+// ---------------------------------------------------------------------------
+struct PiValue {  // ProcessInstanceRecord (protocol-impl/.../ProcessInstanceRecord.java:36-72)
+  int proc = -1;
+  int elem = -1;
+  int64_t flowScopeKey = -1;
+  int64_t piKey = -1;
+};
+
+struct ElementInstance {  // state/instance/ElementInstance.java:23-54
+  int64_t key = -1;
+  int64_t parentKey = -1;
+  int childCount = 0;
+  int64_t jobKey = 0;
+  int state = 0;
+  PiValue value;
+  int activeSequenceFlows = 0;
+};
+
+struct Doc {  // a variable document (msgpack map) as a list of entries
+  uint32_t begin = 0;
+  uint32_t count = 0;
+};
+
+struct JobRow {  // JobRecord without variables (DbJobState.createJobRecord)
+  PiValue pi;
+  int64_t elementInstanceKey = -1;
+  std::string type;
+  int retries = 3;
+};
+
+struct EventTrigger {  // state/instance/EventTrigger.java
+  int elem = -1;
+  int proc = -1;
+  Doc vars;
+  int64_t piKey = -1;
+};
+
+struct VarRow {
+  int64_t key;
+  uint8_t type;
+  int64_t value;
+  uint32_t doc_index;
+};
+
+// A command or event in flight (TypedRecord)
+struct ORecord {
+  zbhip_record r;
+  PiValue pi;          // for PI records
+  Doc doc;             // variables carried (CREATE/JOB_COMPLETE/ VARIABLE entry)
+  std::string reason;  // rejection reason
+  uint32_t instance = 0;
+  int16_t job_ord = -1;
+};
+
+struct Unsupported {
+  std::string what;
+};
+
+class Oracle {
+ public:
+  Oracle(int partition, int partition_count, int max_cmds, int64_t initial_key)
+      : partition_(partition), partition_count_(partition_count), max_cmds_(max_cmds) {
+    key_counter_ = initial_key;
+  }
+
+  std::vector<OProc> procs;
+  std::vector<std::string> names;
+  std::unordered_map<std::string, int> name_ids;
+  std::vector<zbhip_doc_entry> docs;  // all submitted document entries (global index)
+  std::string last_error;
+
+  int intern(const std::string& n) {
+    auto it = name_ids.find(n);
+    if (it != name_ids.end()) return it->second;
+    int id = (int)names.size();
+    names.push_back(n);
+    name_ids[n] = id;
+    return id;
+  }
+
+  int deploy(const std::string& xml, int64_t def_key, int version) {
+    XmlParser xp(xml);
+    auto root = xp.parse_element();
+    if (!root) { last_error = "xml: " + xp.err; return ZBHIP_EPARSE; }
+    const XNode* proc = nullptr;
+    for (auto& k : root->kids)
+      if (k->name == "process" && k->attr("isExecutable", "true") != "false") { proc = k.get(); break; }
+    if (!proc) { last_error = "no executable process"; return ZBHIP_EPARSE; }
+    OProc P;
+    if (!build_process(*proc, P, last_error)) return ZBHIP_EUNSUPP;
+    P.def_key = def_key;
+    P.version = version;
+    // intern condition variable names now so ids match the product's deploy order
+    for (auto& e : P.els) intern_vars(e.cond.get());
+    procs.push_back(std::move(P));
+    return (int)procs.size() - 1;
+  }
+
+  void intern_vars(const FExpr* e) {
+    if (!e) return;
+    if (e->op == FExpr::VAR) intern(e->var);
+    intern_vars(e->l.get());
+    intern_vars(e->r.get());
+  }
+
+  // Writes external commands to the log (the client side of EngineRule).
+  void submit(const zbhip_command* cmds, size_t n, const zbhip_doc_entry* d, size_t nd) {
+    uint32_t doc_base = (uint32_t)docs.size();
+    docs.insert(docs.end(), d, d + nd);
+    for (size_t i = 0; i < n; ++i) {
+      const zbhip_command& c = cmds[i];
+      ORecord rec{};
+      std::memset(&rec.r, 0, sizeof(rec.r));
+      rec.r.record_type = ZBHIP_RT_COMMAND;
+      rec.r.rejection_type = ZBHIP_REJ_NONE;
+      rec.instance = c.instance;
+      rec.doc = Doc{doc_base + c.doc_begin, c.doc_count};
+      rec.r.process_idx = -1;
+      rec.r.element_idx = -1;
+      rec.r.scope_key = -1;
+      rec.r.process_instance_key = -1;
+      rec.r.aux = c.doc_count ? (int64_t)(doc_base + c.doc_begin) : -1;
+      if (c.kind == ZBHIP_CMD_CREATE) {
+        rec.r.process_idx = c.ref;
+        rec.r.value_type = ZBHIP_VT_PROCESS_INSTANCE_CREATION;
+        rec.r.intent = ZBHIP_PIC_CREATE;
+        rec.r.key = -1;
+      } else {
+        rec.r.value_type = ZBHIP_VT_JOB;
+        rec.r.intent = ZBHIP_JOB_COMPLETE;
+        rec.r.key = resolve(c.instance, c.ref);
+        rec.job_ord = (int16_t)c.ref;
+      }
+      rec.r.source_index = next_source_++;
+      log_.push_back(std::move(rec));
+    }
+  }
+
+  // StreamProcessor / ProcessingStateMachine: read the log and process each command as a batch.
+  int run() {
+    int processed = 0;
+    while (!log_.empty()) {
+      ORecord cmd = std::move(log_.front());
+      log_.pop_front();
+      try {
+        batch_processing(cmd);
+      } catch (const Unsupported& u) {
+        last_error = "unsupported at source " + std::to_string(cmd.r.source_index) + ": " + u.what;
+        fallback_.push_back(cmd.instance);
+        return ZBHIP_EUNSUPP;
+      }
+      ++processed;
+    }
+    return processed;
+  }
+
+  std::vector<ORecord> out;  // every follow-up record, in log order
+  std::vector<uint32_t> fallback_;
+
+  // key ordinal lookup: per instance slot, every key generated in its batches
+  std::unordered_map<uint32_t, std::vector<int64_t>> inst_keys;
+
+  int64_t resolve(uint32_t inst, uint32_t ord) {
+    auto it = inst_keys.find(inst);
+    if (it == inst_keys.end() || ord >= it->second.size()) return -1;
+    return it->second[ord];
+  }
+
+  std::string dump_state() const;
+  uint64_t transitions = 0, completed_instances = 0, commands_processed = 0;
+
+ private:
+  int partition_, partition_count_, max_cmds_;
+  int64_t key_counter_ = 0;
+  int64_t next_source_ = 0;
+  std::deque<ORecord> log_;
+
+  // --- state (zb-db column families) ---
+  std::map<int64_t, ElementInstance> ei_;                       // ELEMENT_INSTANCE_KEY
+  std::set<std::pair<int64_t, int64_t>> parent_child_;          // ELEMENT_INSTANCE_PARENT_CHILD
+  std::map<int64_t, int64_t> child_parent_;                     // ELEMENT_INSTANCE_CHILD_PARENT
+  std::map<std::tuple<int64_t, int, int>, int> taken_;          // NUMBER_OF_TAKEN_SEQUENCE_FLOWS (proc-local ids)
+  std::set<std::pair<int64_t, int64_t>> pi_by_def_;             // PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY
+  std::map<std::pair<int64_t, int>, VarRow> vars_;              // VARIABLES (scope, name id)
+  std::set<int64_t> event_scope_;                               // EVENT_SCOPE (accepting, not interrupted)
+  std::map<std::pair<int64_t, int64_t>, EventTrigger> triggers_;// EVENT_TRIGGER
+  std::map<int64_t, JobRow> jobs_;                              // JOBS (+ JOB_STATES = ACTIVATABLE)
+  std::set<std::tuple<std::string, std::string, int64_t>> activatable_;  // JOB_ACTIVATABLE
+
+  // --- batch context ---
+  std::vector<ORecord>* batch_ = nullptr;
+  uint32_t cur_instance_ = 0;
+  int64_t cur_source_ = 0;
+
+  // DbKeyGenerator.nextKey (stream-platform/.../state/DbKeyGenerator.java:39-42) with
+  // Protocol.encodePartitionId (protocol/.../Protocol.java:98-100)
+  int64_t next_key() {
+    ++key_counter_;
+    int64_t k = ((int64_t)partition_ << 51) + key_counter_;
+    inst_keys[cur_instance_].push_back(k);
+    return k;
+  }
+
+  const OProc& P(int proc) const { return procs[proc]; }
+  const OEl& E(const PiValue& v) const { return procs[v.proc].els[v.elem]; }
+
+  ORecord& append(int rt, int vt, int intent, int64_t key) {
+    ORecord rec{};
+    std::memset(&rec.r, 0, sizeof(rec.r));
+    rec.r.record_type = (uint8_t)rt;
+    rec.r.value_type = (uint8_t)vt;
+    rec.r.intent = (uint8_t)intent;
+    rec.r.key = key;
+    rec.r.rejection_type = ZBHIP_REJ_NONE;
+    rec.r.source_index = cur_source_;
+    rec.r.ordinal = (uint32_t)batch_->size();
+    rec.r.aux = -1;
+    rec.r.process_idx = -1;
+    rec.r.element_idx = -1;
+    rec.r.scope_key = -1;
+    rec.r.process_instance_key = -1;
+    rec.instance = cur_instance_;
+    batch_->push_back(std::move(rec));
+    return batch_->back();
+  }
+
+  void fill_pi(ORecord& rec, const PiValue& v) {
+    rec.pi = v;
+    rec.r.process_idx = v.proc;
+    rec.r.element_idx = v.elem;
+    rec.r.scope_key = v.flowScopeKey;
+    rec.r.process_instance_key = v.piKey;
+  }
+
+  // ResultBuilderBackedEventApplyingStateWriter.appendFollowUpEvent
+  // (processing/streamprocessor/writers/ResultBuilderBackedEventApplyingStateWriter.java:45-57):
+  // append the record, then apply it immediately.
+  void pi_event(int64_t key, int intent, const PiValue& v) {
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_INSTANCE, intent, key);
+    fill_pi(rec, v);
+    ++transitions;
+    if (intent == ZBHIP_PI_ELEMENT_COMPLETED && P(v.proc).els[v.elem].type == ZBHIP_EL_PROCESS)
+      ++completed_instances;
+    apply_pi(key, intent, v);
+  }
+
+  // ResultBuilderBackedTypedCommandWriter.appendFollowUpCommand
+  void pi_command(int64_t key, int intent, const PiValue& v) {
+    ORecord& rec = append(ZBHIP_RT_COMMAND, ZBHIP_VT_PROCESS_INSTANCE, intent, key);
+    fill_pi(rec, v);
+  }
+
+  // TypedRejectionWriter.appendRejection: key and value of the command
+  void reject(const ORecord& cmd, int type, const std::string& reason) {
+    ORecord& rec = append(ZBHIP_RT_REJECTION, cmd.r.value_type, cmd.r.intent, cmd.r.key);
+    rec.r.rejection_type = (uint8_t)type;
+    rec.r.process_idx = cmd.r.process_idx;
+    rec.r.element_idx = cmd.r.element_idx;
+    rec.r.scope_key = cmd.r.scope_key;
+    rec.r.process_instance_key = cmd.r.process_instance_key;
+    rec.r.aux = cmd.r.aux;
+    rec.pi = cmd.pi;
+    rec.doc = cmd.doc;
+    rec.reason = reason;
+  }
+
+  // ---------------------------------------------------------------------
+  // ProcessingStateMachine.batchProcessing / collectBatchProcessingStepResult
+  // (stream-platform/.../stream/impl/ProcessingStateMachine.java:328-417)
+  // ---------------------------------------------------------------------
+  void batch_processing(ORecord& initial) {
+    std::vector<ORecord> batch;
+    batch_ = &batch;
+    cur_instance_ = initial.instance;
+    cur_source_ = initial.r.source_index;
+    std::deque<ORecord> pending;
+    pending.push_back(initial);
+    int processed = 0;
+    size_t last_size = 0;
+    while (!pending.empty() && processed < max_cmds_) {
+      ORecord cmd = std::move(pending.front());
+      pending.pop_front();
+      process(cmd);
+      ++commands_processed;
+      int current_batch_size = (int)pending.size() + processed + 1;
+      int to_process = 0;
+      for (size_t i = last_size; i < batch.size(); ++i) {
+        if (batch[i].r.record_type == ZBHIP_RT_COMMAND) {
+          if (current_batch_size + to_process < max_cmds_) {
+            pending.push_back(batch[i]);
+            ++to_process;
+          } else {
+            // written to the log unprocessed: processed later as its own batch
+            ORecord later = batch[i];
+            later.r.source_index = next_source_++;
+            log_.push_back(later);
+          }
+        }
+      }
+      last_size = batch.size();
+      ++processed;
+    }
+    for (auto& r : batch) out.push_back(std::move(r));
+    batch_ = nullptr;
+  }
+
+  // Engine.process (Engine.java:99-131) -> RecordProcessorMap dispatch
+  void process(ORecord& cmd) {
+    if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION)
+      create_process_instance(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_JOB)
+      complete_job(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE)
+      bpmn_process_record(cmd);
+    else
+      throw Unsupported{"value type"};
+  }
+
+  // ---------------------------------------------------------------------
+  // CreateProcessInstanceProcessor (processing/processinstance/CreateProcessInstanceProcessor.java:100-158,319-330)
+  // wrapped by CommandProcessorImpl.processRecord (processing/streamprocessor/CommandProcessorImpl.java:65-103)
+  // ---------------------------------------------------------------------
+  void create_process_instance(ORecord& cmd) {
+    int proc = cmd.r.process_idx;
+    if (proc < 0 || proc >= (int)procs.size()) {
+      reject(cmd, ZBHIP_REJ_NOT_FOUND, "Expected to find process definition with key '" +
+                                           std::to_string(proc) + "', but none found");
+      return;
+    }
+    const OProc& p = P(proc);
+    if (p.none_start < 0) {
+      reject(cmd, ZBHIP_REJ_INVALID_STATE,
+             "Expected to create instance of process with none start event, but there is no such event");
+      return;
+    }
+    int64_t piKey = next_key();
+    // setVariablesFromDocument -> VariableBehavior.mergeLocalDocument (processing/variable/VariableBehavior.java:60-82)
+    merge_local_document(piKey, proc, piKey, cmd.doc);
+    PiValue v;  // initProcessInstanceRecord
+    v.proc = proc;
+    v.elem = 0;
+    v.flowScopeKey = -1;
+    v.piKey = piKey;
+    pi_command(piKey, ZBHIP_PI_ACTIVATE_ELEMENT, v);
+    // controller.accept(CREATED) -> entityKey = nextKey (command key is -1)
+    int64_t createdKey = next_key();
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_INSTANCE_CREATION, ZBHIP_PIC_CREATED, createdKey);
+    rec.r.process_idx = proc;
+    rec.r.element_idx = 0;
+    rec.r.scope_key = piKey;
+    rec.r.process_instance_key = piKey;
+    rec.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
+    rec.doc = cmd.doc;
+  }
+
+  // VariableBehavior.mergeLocalDocument + setLocalVariable (VariableBehavior.java:60-82,191-200).
+  // Documents with more than one entry iterate in agrona Int2IntHashMap order
+  // (IndexedDocument.java:44-63, third-party agrona 1.19.2): parity unpinned, rejected here.
+  void merge_local_document(int64_t scopeKey, int proc, int64_t piKey, const Doc& d) {
+    if (d.count == 0) return;
+    if (d.count > 1) throw Unsupported{"multi-entry variable document (agrona iteration order unpinned)"};
+    for (uint32_t j = 0; j < d.count; ++j) set_local_variable(scopeKey, proc, piKey, d.begin + j);
+  }
+
+  void set_local_variable(int64_t scopeKey, int proc, int64_t piKey, uint32_t entry) {
+    const zbhip_doc_entry& de = docs[entry];
+    auto it = vars_.find({scopeKey, (int)de.name_id});
+    if (it == vars_.end()) {
+      int64_t key = next_key();
+      var_event(key, ZBHIP_VAR_CREATED, scopeKey, proc, piKey, entry);
+    } else if (!(it->second.type == de.type && it->second.value == de.value)) {
+      var_event(it->second.key, ZBHIP_VAR_UPDATED, scopeKey, proc, piKey, entry);
+    }
+  }
+
+  void var_event(int64_t key, int intent, int64_t scopeKey, int proc, int64_t piKey, uint32_t entry) {
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_VARIABLE, intent, key);
+    rec.r.process_idx = proc;
+    rec.r.element_idx = (int32_t)docs[entry].name_id;
+    rec.r.scope_key = scopeKey;
+    rec.r.process_instance_key = piKey;
+    rec.r.aux = entry;
+    // VariableApplier.applyState -> DbVariableState.setVariableLocal
+    vars_[{scopeKey, (int)docs[entry].name_id}] = VarRow{key, docs[entry].type, docs[entry].value, entry};
+  }
+
+  // VariableBehavior.mergeDocument (VariableBehavior.java:105-150)
+  void merge_document(int64_t scopeKey, int proc, int64_t piKey, const Doc& d) {
+    if (d.count == 0) return;
+    if (d.count > 1) throw Unsupported{"multi-entry variable document (agrona iteration order unpinned)"};
+    std::vector<uint32_t> entries;
+    for (uint32_t j = 0; j < d.count; ++j) entries.push_back(d.begin + j);
+    int64_t current = scopeKey;
+    for (;;) {
+      auto pit = child_parent_.find(current);
+      int64_t parent = pit == child_parent_.end() ? -1 : pit->second;
+      if (parent <= 0) break;
+      for (auto e = entries.begin(); e != entries.end();) {
+        const zbhip_doc_entry& de = docs[*e];
+        auto vit = vars_.find({current, (int)de.name_id});
+        if (vit != vars_.end() && !(vit->second.type == de.type && vit->second.value == de.value)) {
+          var_event(vit->second.key, ZBHIP_VAR_UPDATED, current, proc, piKey, *e);
+          e = entries.erase(e);
+        } else {
+          ++e;
+        }
+      }
+      current = parent;
+    }
+    for (uint32_t e : entries) set_local_variable(current, proc, piKey, e);
+  }
+
+  // ---------------------------------------------------------------------
+  // JobCompleteProcessor (processing/job/JobCompleteProcessor.java:47-92) with
+  // DefaultJobCommandPreconditionGuard (processing/job/DefaultJobCommandPreconditionGuard.java:26-46)
+  // ---------------------------------------------------------------------
+  void complete_job(ORecord& cmd) {
+    int64_t jobKey = cmd.r.key;
+    auto jit = jobs_.find(jobKey);
+    if (jit == jobs_.end()) {
+      // JobCommandPreconditionChecker.check: NOT_FOUND
+      reject(cmd, ZBHIP_REJ_NOT_FOUND,
+             "Expected to complete job with key '" + std::to_string(jobKey) + "', but no such job was found");
+      return;
+    }
+    JobRow job = jit->second;
+    // accept(COMPLETED, job with command variables) -> event, JobCompletedApplier
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_COMPLETED, jobKey);
+    rec.r.process_idx = job.pi.proc;
+    rec.r.element_idx = job.pi.elem;
+    rec.r.scope_key = job.elementInstanceKey;
+    rec.r.process_instance_key = job.pi.piKey;
+    rec.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
+    rec.doc = cmd.doc;
+    apply_job_completed(jobKey, job);
+    // afterAccept
+    auto sit = ei_.find(job.elementInstanceKey);
+    if (sit != ei_.end()) {
+      ElementInstance task = sit->second;
+      auto fit = ei_.find(task.value.flowScopeKey);
+      if (fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED) {
+        // EventHandle.triggeringProcessEvent(JobRecord) (processing/common/EventHandle.java:151-158)
+        // -> EventTriggerBehavior.triggeringProcessEvent (processing/common/EventTriggerBehavior.java:148-166)
+        int64_t eventKey = next_key();
+        ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
+        pe.r.process_idx = job.pi.proc;
+        pe.r.element_idx = job.pi.elem;
+        pe.r.scope_key = job.elementInstanceKey;
+        pe.r.process_instance_key = job.pi.piKey;
+        pe.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
+        pe.doc = cmd.doc;
+        // ProcessEventTriggeringApplier (state/appliers/ProcessEventTriggeringApplier.java:35-56)
+        // -> DbEventScopeInstanceState.triggerEvent (only if the scope accepts)
+        if (event_scope_.count(job.elementInstanceKey))
+          triggers_[{job.elementInstanceKey, eventKey}] = EventTrigger{job.pi.elem, job.pi.proc, cmd.doc, job.pi.piKey};
+        pi_command(job.elementInstanceKey, ZBHIP_PI_COMPLETE_ELEMENT, task.value);
+      }
+    }
+  }
+
+  // JobCreatedApplier (state/appliers/JobCreatedApplier.java:28-41) / DbJobState.create
+  void apply_job_created(int64_t jobKey, const JobRow& job) {
+    jobs_[jobKey] = job;
+    activatable_.insert({job.type, "<default>", jobKey});
+    auto it = ei_.find(job.elementInstanceKey);
+    if (it != ei_.end()) it->second.jobKey = jobKey;
+  }
+
+  // JobCompletedApplier (state/appliers/JobCompletedApplier.java:28-45) / DbJobState.delete (:175-188)
+  void apply_job_completed(int64_t jobKey, const JobRow& job) {
+    jobs_.erase(jobKey);
+    activatable_.erase({job.type, "<default>", jobKey});
+    auto it = ei_.find(job.elementInstanceKey);
+    if (it != ei_.end()) {
+      auto fit = ei_.find(it->second.value.flowScopeKey);
+      if (fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED) it->second.jobKey = -1;
+    }
+  }
+
+  // ---------------------------------------------------------------------
+  // BpmnStreamProcessor.processRecord (processing/bpmn/BpmnStreamProcessor.java:74-162)
+  // ---------------------------------------------------------------------
+  void bpmn_process_record(ORecord& cmd) {
+    std::string violation;
+    if (!check_state_transition(cmd, violation)) {
+      reject(cmd, ZBHIP_REJ_INVALID_STATE, violation);
+      return;
+    }
+    const OEl& el = E(cmd.pi);
+    if (cmd.r.intent == ZBHIP_PI_ACTIVATE_ELEMENT) {
+      // BpmnStateTransitionBehavior.transitionToActivating (behavior/BpmnStateTransitionBehavior.java:72-100)
+      if (ei_.count(cmd.r.key)) throw Unsupported{"re-activation (incident resolution)"};
+      int64_t key = cmd.r.key == -1 ? next_key() : cmd.r.key;
+      pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATING, cmd.pi);
+      // onElementActivating -> container.onChildActivating: ProcessProcessor default (right)
+      on_activate(el, key, cmd.pi);
+    } else if (cmd.r.intent == ZBHIP_PI_COMPLETE_ELEMENT) {
+      // transitionToCompleting (:116-130)
+      if (ei_.at(cmd.r.key).state == ZBHIP_PI_ELEMENT_COMPLETING) throw Unsupported{"re-completion (incident resolution)"};
+      pi_event(cmd.r.key, ZBHIP_PI_ELEMENT_COMPLETING, cmd.pi);
+      on_complete(el, cmd.r.key, cmd.pi);
+    } else {
+      throw Unsupported{"terminate"};
+    }
+  }
+
+  // ProcessInstanceStateTransitionGuard.checkStateTransition (processing/bpmn/ProcessInstanceStateTransitionGuard.java:47-186)
+  static const char* state_name(int s) {
+    switch (s) {
+      case ZBHIP_PI_ELEMENT_ACTIVATING: return "ELEMENT_ACTIVATING";
+      case ZBHIP_PI_ELEMENT_ACTIVATED: return "ELEMENT_ACTIVATED";
+      case ZBHIP_PI_ELEMENT_COMPLETING: return "ELEMENT_COMPLETING";
+      case ZBHIP_PI_ELEMENT_COMPLETED: return "ELEMENT_COMPLETED";
+      case ZBHIP_PI_ELEMENT_TERMINATING: return "ELEMENT_TERMINATING";
+      case ZBHIP_PI_ELEMENT_TERMINATED: return "ELEMENT_TERMINATED";
+      default: return "?";
+    }
+  }
+
+  bool has_active_flow_scope(const ORecord& cmd, std::string& v) {
+    const OEl& el = E(cmd.pi);
+    if (el.type == ZBHIP_EL_PROCESS) return true;
+    auto it = ei_.find(cmd.pi.flowScopeKey);
+    if (it == ei_.end()) {
+      v = "Expected flow scope instance with key '" + std::to_string(cmd.pi.flowScopeKey) +
+          "' to be present in state but not found.";
+      return false;
+    }
+    if (it->second.state != ZBHIP_PI_ELEMENT_ACTIVATED) {
+      v = std::string("Expected flow scope instance to be in state 'ELEMENT_ACTIVATED' but was '") +
+          state_name(it->second.state) + "'.";
+      return false;
+    }
+    return true;  // never interrupted in the supported subset
+  }
+
+  bool check_state_transition(const ORecord& cmd, std::string& v) {
+    if (cmd.r.intent == ZBHIP_PI_ACTIVATE_ELEMENT) {
+      if (!has_active_flow_scope(cmd, v)) return false;
+      const OEl& el = E(cmd.pi);
+      if (el.type == ZBHIP_EL_PARALLEL_GATEWAY) {  // canActivateParallelGateway (:169-186)
+        int taken = number_of_taken_flows(cmd.pi.flowScopeKey, cmd.pi.proc, cmd.pi.elem);
+        if (taken < (int)el.in.size()) {
+          v = "Expected to be able to activate parallel gateway '" + el.id +
+              "', but not all sequence flows have been taken.";
+          return false;
+        }
+      }
+      return true;
+    }
+    if (cmd.r.intent == ZBHIP_PI_COMPLETE_ELEMENT) {
+      auto it = ei_.find(cmd.r.key);
+      if (it == ei_.end()) {
+        v = "Expected element instance with key '" + std::to_string(cmd.r.key) +
+            "' to be present in state but not found.";
+        return false;
+      }
+      int s = it->second.state;
+      if (s != ZBHIP_PI_ELEMENT_ACTIVATED && s != ZBHIP_PI_ELEMENT_COMPLETING) {
+        v = std::string("Expected element instance to be in state 'ELEMENT_ACTIVATED' or one of "
+                        "'[ELEMENT_COMPLETING]' but was '") + state_name(s) + "'.";
+        return false;
+      }
+      return has_active_flow_scope(cmd, v);
+    }
+    throw Unsupported{"intent"};
+  }
+
+  // DbElementInstanceState.getNumberOfTakenSequenceFlows (state/instance/DbElementInstanceState.java:330-344):
+  // counts DISTINCT flows with a counter row under (flowScopeKey, gatewayId)
+  int number_of_taken_flows(int64_t fs, int proc, int gw) {
+    int n = 0;
+    for (auto it = taken_.lower_bound({fs, gw, -1}); it != taken_.end(); ++it) {
+      if (std::get<0>(it->first) != fs || std::get<1>(it->first) != gw) break;
+      ++n;
+    }
+    (void)proc;
+    return n;
+  }
+
+  // ---------------------------------------------------------------------
+  // element processors: onActivate / onComplete
+  // ---------------------------------------------------------------------
+  void on_activate(const OEl& el, int64_t key, const PiValue& v) {
+    switch (el.type) {
+      case ZBHIP_EL_PROCESS: {  // ProcessProcessor.onActivate (processing/bpmn/container/ProcessProcessor.java:55-61,119-128)
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        const OProc& p = P(v.proc);
+        PiValue c = v;  // activateChildInstance (BpmnStateTransitionBehavior.java:279-290)
+        c.flowScopeKey = key;
+        c.elem = p.none_start;
+        pi_command(-1, ZBHIP_PI_ACTIVATE_ELEMENT, c);
+        break;
+      }
+      case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onActivate (processing/bpmn/event/StartEventProcessor.java:45-50)
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        pi_command(key, ZBHIP_PI_COMPLETE_ELEMENT, v);
+        break;
+      case ZBHIP_EL_END_EVENT:  // EndEventProcessor.NoneEndEventBehavior.onActivate (processing/bpmn/event/EndEventProcessor.java:110-134)
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        pi_event(key, ZBHIP_PI_ELEMENT_COMPLETING, v);
+        complete_and_take(el, key, v, /*output_mappings=*/true);
+        break;
+      case ZBHIP_EL_SERVICE_TASK: {  // JobWorkerTaskProcessor.onActivate (processing/bpmn/task/JobWorkerTaskProcessor.java:49-61)
+        // BpmnJobBehavior.createNewJob -> writeJobCreatedEvent (behavior/BpmnJobBehavior.java:113-119,194-218)
+        JobRow job;
+        job.pi = v;
+        job.elementInstanceKey = key;
+        job.type = el.job_type;
+        job.retries = el.retries;
+        int64_t jobKey = next_key();
+        ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_CREATED, jobKey);
+        rec.r.process_idx = v.proc;
+        rec.r.element_idx = v.elem;
+        rec.r.scope_key = key;
+        rec.r.process_instance_key = v.piKey;
+        apply_job_created(jobKey, job);
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        break;
+      }
+      case ZBHIP_EL_EXCLUSIVE_GATEWAY: {  // ExclusiveGatewayProcessor.onActivate (processing/bpmn/gateway/ExclusiveGatewayProcessor.java:47-66)
+        int flow = find_sequence_flow_to_take(el, key, v.proc);
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        pi_event(key, ZBHIP_PI_ELEMENT_COMPLETING, v);
+        transition_to_completed(el, key, v);
+        if (flow >= 0) take_sequence_flow(key, v, flow);
+        break;
+      }
+      case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (processing/bpmn/gateway/ParallelGatewayProcessor.java:34-50)
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        pi_event(key, ZBHIP_PI_ELEMENT_COMPLETING, v);
+        transition_to_completed(el, key, v);
+        for (int f : el.out) take_sequence_flow(key, v, f);
+        break;
+      default:
+        throw Unsupported{"element type"};
+    }
+  }
+
+  void on_complete(const OEl& el, int64_t key, const PiValue& v) {
+    switch (el.type) {
+      case ZBHIP_EL_PROCESS:  // ProcessProcessor.onComplete (:63-76): never end of path
+        pi_event(key, ZBHIP_PI_ELEMENT_COMPLETED, v);
+        break;
+      case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onComplete (:52-67)
+        complete_and_take(el, key, v, true);
+        break;
+      case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onComplete (:63-75)
+        complete_and_take(el, key, v, true);
+        break;
+      default:
+        throw Unsupported{"complete of element without wait state"};
+    }
+  }
+
+  // applyOutputMappings (behavior/BpmnVariableMappingBehavior.java:86-156) ->
+  // transitionToCompleted -> takeOutgoingSequenceFlows (BpmnStateTransitionBehavior.java:365-369)
+  void complete_and_take(const OEl& el, int64_t key, const PiValue& v, bool output_mappings) {
+    if (output_mappings) {
+      const EventTrigger* trig = nullptr;  // peekEventTrigger(elementInstanceKey)
+      auto it = triggers_.lower_bound({key, INT64_MIN});
+      if (it != triggers_.end() && it->first.first == key) trig = &it->second;
+      if (trig && trig->vars.count > 0) merge_document(key, v.proc, v.piKey, trig->vars);
+      // START_EVENT without trigger: local variables of the start event are empty.
+    }
+    transition_to_completed(el, key, v);
+    for (int f : el.out) take_sequence_flow(key, v, f);
+  }
+
+  // BpmnStateTransitionBehavior.transitionToCompleted (:158-191) and afterExecutionPathCompleted (:404-417)
+  void transition_to_completed(const OEl& el, int64_t key, const PiValue& v) {
+    bool end_of_path = el.type != ZBHIP_EL_PROCESS && el.out.empty();
+    pi_event(key, ZBHIP_PI_ELEMENT_COMPLETED, v);
+    if (end_of_path) {
+      // ProcessProcessor.afterExecutionPathCompleted (:130-140) -> BpmnStateBehavior.canBeCompleted (behavior/BpmnStateBehavior.java:76-95)
+      auto fit = ei_.find(v.flowScopeKey);
+      if (fit != ei_.end()) {
+        const ElementInstance& fs = fit->second;
+        if ((int64_t)fs.childCount + fs.activeSequenceFlows == 0) {
+          pi_command(fs.key, ZBHIP_PI_COMPLETE_ELEMENT, fs.value);
+        }
+      }
+    }
+  }
+
+  // takeSequenceFlow (:243-263) + activateElementInstanceInFlowScope (:326-339)
+  void take_sequence_flow(int64_t /*from*/, const PiValue& v, int flow) {
+    const OEl& f = P(v.proc).els[flow];
+    PiValue sv = v;
+    sv.elem = flow;
+    int64_t sfKey = next_key();
+    pi_event(sfKey, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sv);
+    PiValue tv = v;
+    tv.elem = f.tgt;
+    int64_t k = next_key();
+    pi_command(k, ZBHIP_PI_ACTIVATE_ELEMENT, tv);
+  }
+
+  // ExclusiveGatewayProcessor.findSequenceFlowToTake (:86-126)
+  int find_sequence_flow_to_take(const OEl& el, int64_t gwKey, int proc) {
+    const OProc& p = P(proc);
+    if (el.out.empty()) return -1;  // implicit end of the flow scope
+    if (el.out.size() == 1 && !p.els[el.out[0]].has_cond) return el.out[0];
+    for (int f : el.out_with_cond) {
+      if (el.default_flow == f) continue;  // the default flow's condition is never evaluated
+      // ExpressionProcessor.evaluateBooleanExpression (processing/common/ExpressionProcessor.java:126-131,356-368)
+      FVal r = eval(p.els[f].cond.get(), gwKey);
+      if (r.k != V_BOOL) throw Unsupported{"condition did not evaluate to a boolean (incident)"};
+      if (r.b) return f;
+    }
+    if (el.default_flow >= 0) return el.default_flow;
+    throw Unsupported{"no outgoing flow chosen (incident CONDITION_ERROR)"};
+  }
+
+  // DbVariableState.getVariable walks the scope chain (state/variable/DbVariableState.java:174-200)
+  const VarRow* lookup_var(int64_t scope, int name) {
+    int64_t s = scope;
+    while (s > 0) {
+      auto it = vars_.find({s, name});
+      if (it != vars_.end()) return &it->second;
+      auto pit = child_parent_.find(s);
+      if (pit == child_parent_.end()) break;
+      s = pit->second;
+    }
+    return nullptr;
+  }
+
+  FVal eval(const FExpr* e, int64_t scope) {
+    FVal r;
+    switch (e->op) {
+      case FExpr::NUM: r.k = V_NUM; r.n = e->num; return r;
+      case FExpr::BOOL: r.k = V_BOOL; r.b = e->b; return r;
+      case FExpr::NUL: r.k = V_NULL; return r;
+      case FExpr::VAR: {
+        auto it = name_ids.find(e->var);
+        const VarRow* vr = it == name_ids.end() ? nullptr : lookup_var(scope, it->second);
+        if (!vr || vr->type == ZBHIP_DOC_NIL) { r.k = V_NULL; return r; }
+        if (vr->type == ZBHIP_DOC_BOOL) { r.k = V_BOOL; r.b = vr->value != 0; return r; }
+        if (vr->type == ZBHIP_DOC_INT) { r.k = V_NUM; r.n = (__int128)vr->value * kScale18; return r; }
+        if (vr->type == ZBHIP_DOC_DEC) { r.k = V_NUM; r.n = (__int128)vr->value * (kScale18 / 1000000); return r; }
+        r.k = V_ERR;
+        return r;
+      }
+      case FExpr::NOT: {
+        FVal a = eval(e->l.get(), scope);
+        if (a.k != V_BOOL) throw Unsupported{"not() of non-boolean"};
+        r.k = V_BOOL; r.b = !a.b; return r;
+      }
+      case FExpr::AND:
+      case FExpr::OR: {
+        FVal a = eval(e->l.get(), scope), b = eval(e->r.get(), scope);
+        if (a.k != V_BOOL || b.k != V_BOOL) throw Unsupported{"and/or over non-booleans"};
+        r.k = V_BOOL;
+        r.b = e->op == FExpr::AND ? (a.b && b.b) : (a.b || b.b);
+        return r;
+      }
+      case FExpr::CMP: {
+        FVal a = eval(e->l.get(), scope), b = eval(e->r.get(), scope);
+        if (a.k == V_ERR || b.k == V_ERR) throw Unsupported{"value type outside the subset"};
+        const std::string& c = e->cmp;
+        if (c == "=" || c == "!=") {
+          bool eq;
+          if (a.k == V_NULL || b.k == V_NULL) eq = a.k == b.k;
+          else if (a.k != b.k) throw Unsupported{"comparison of mixed types"};
+          else eq = a.k == V_NUM ? a.n == b.n : a.b == b.b;
+          r.k = V_BOOL;
+          r.b = c == "=" ? eq : !eq;
+          return r;
+        }
+        if (a.k != V_NUM || b.k != V_NUM) throw Unsupported{"ordering comparison with non-number"};
+        r.k = V_BOOL;
+        if (c == "<") r.b = a.n < b.n;
+        else if (c == "<=") r.b = a.n <= b.n;
+        else if (c == ">") r.b = a.n > b.n;
+        else r.b = a.n >= b.n;
+        return r;
+      }
+    }
+    throw Unsupported{"expr"};
+  }
+
+  // ---------------------------------------------------------------------
+  // event appliers for PROCESS_INSTANCE (state/appliers/EventAppliers.java:121-157)
+  // ---------------------------------------------------------------------
+  void apply_pi(int64_t key, int intent, const PiValue& v) {
+    const OEl& el = E(v);
+    switch (intent) {
+      case ZBHIP_PI_ELEMENT_ACTIVATING: {  // ProcessInstanceElementActivatingApplier.applyState (:48-77)
+        // createEventScope (:255-289): job worker elements get an event scope
+        if (el.type == ZBHIP_EL_SERVICE_TASK) event_scope_.insert(key);
+        // cleanupSequenceFlowsTaken (:79-98): Tetris decrement of (flowScope, gateway)
+        if (el.type == ZBHIP_EL_PARALLEL_GATEWAY) {
+          for (auto it = taken_.lower_bound({v.flowScopeKey, v.elem, -1}); it != taken_.end();) {
+            if (std::get<0>(it->first) != v.flowScopeKey || std::get<1>(it->first) != v.elem) break;
+            if (--it->second > 0) ++it;
+            else it = taken_.erase(it);
+          }
+        }
+        auto fit = ei_.find(v.flowScopeKey);
+        // DbElementInstanceState.newInstance/createInstance (state/instance/DbElementInstanceState.java:141-210)
+        ElementInstance inst;
+        inst.key = key;
+        inst.state = ZBHIP_PI_ELEMENT_ACTIVATING;
+        inst.value = v;
+        if (fit != ei_.end()) {
+          inst.parentKey = fit->second.key;
+          fit->second.childCount += 1;
+        }
+        ei_[key] = inst;
+        parent_child_.insert({inst.parentKey, key});
+        child_parent_[key] = inst.parentKey;  // DbVariableState.createScope
+        if (el.type == ZBHIP_EL_PROCESS) pi_by_def_.insert({P(v.proc).def_key, key});
+        if (fit == ei_.end()) return;  // root process (applyRootProcessState: no parent)
+        // decrementActiveSequenceFlow (:130-204); decrementActiveSequenceFlows clamps at 0 (ElementInstance.java:203-213)
+        ElementInstance& fs = fit->second;
+        auto dec = [&fs]() { if (fs.activeSequenceFlows > 0) fs.activeSequenceFlows--; };
+        switch (el.type) {
+          case ZBHIP_EL_START_EVENT:
+          case ZBHIP_EL_BOUNDARY_EVENT:
+            break;
+          case ZBHIP_EL_PARALLEL_GATEWAY:
+            for (size_t i = 0; i < el.in.size(); ++i) dec();
+            break;
+          default:
+            dec();
+        }
+        break;
+      }
+      case ZBHIP_PI_ELEMENT_ACTIVATED:  // ProcessInstanceElementActivatedApplier
+        ei_.at(key).state = ZBHIP_PI_ELEMENT_ACTIVATED;
+        break;
+      case ZBHIP_PI_ELEMENT_COMPLETING:  // ProcessInstanceElementCompletingApplier
+        ei_.at(key).state = ZBHIP_PI_ELEMENT_COMPLETING;
+        break;
+      case ZBHIP_PI_ELEMENT_COMPLETED: {  // ProcessInstanceElementCompletedApplier (:45-73)
+        // eventScopeInstanceState.deleteInstance: triggers then the scope
+        for (auto it = triggers_.lower_bound({key, INT64_MIN}); it != triggers_.end() && it->first.first == key;)
+          it = triggers_.erase(it);
+        event_scope_.erase(key);
+        // DbElementInstanceState.removeInstance (:160-193)
+        auto it = ei_.find(key);
+        if (it == ei_.end()) break;
+        int64_t parent = it->second.parentKey;
+        parent_child_.erase({parent, key});
+        ei_.erase(it);
+        // variableState.removeScope: variables of the scope + child->parent row
+        for (auto vit = vars_.lower_bound({key, INT32_MIN}); vit != vars_.end() && vit->first.first == key;)
+          vit = vars_.erase(vit);
+        child_parent_.erase(key);
+        for (auto tit = taken_.lower_bound({key, INT32_MIN, INT32_MIN}); tit != taken_.end() && std::get<0>(tit->first) == key;)
+          tit = taken_.erase(tit);
+        if (el.type == ZBHIP_EL_PROCESS) pi_by_def_.erase({P(v.proc).def_key, key});
+        if (parent > 0) ei_.at(parent).childCount -= 1;
+        break;
+      }
+      case ZBHIP_PI_SEQUENCE_FLOW_TAKEN: {  // ProcessInstanceSequenceFlowTakenApplier (:32-69)
+        ElementInstance& fs = ei_.at(v.flowScopeKey);
+        fs.activeSequenceFlows += 1;
+        const OEl& tgt = P(v.proc).els[el.tgt];
+        if (tgt.type == ZBHIP_EL_PARALLEL_GATEWAY) taken_[{v.flowScopeKey, el.tgt, v.elem}] += 1;
+        break;
+      }
+      default:
+        break;
+    }
+  }
+};
+
+std::string Oracle::dump_state() const {
+  std::vector<std::string> rows;
+  char buf[512];
+  auto pid = [this](const PiValue& v, int e) -> const std::string& { return procs[v.proc].els[e].id; };
+  snprintf(buf, sizeof buf, "KEY|latestKey|%lld", (long long)(((int64_t)partition_ << 51) + key_counter_));
+  rows.push_back(buf);
+  for (auto& [k, e] : ei_) {
+    const OEl& el = procs[e.value.proc].els[e.value.elem];
+    snprintf(buf, sizeof buf,
+             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%d,childActivatedCount=0,childCompletedCount=0,"
+             "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=0,interruptingElementId=,"
+             "calledChildInstanceKey=-1,state=%d,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
+             "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%d",
+             (long long)k, (long long)e.parentKey, e.childCount, (long long)e.jobKey, e.state, el.id.c_str(), el.type,
+             el.event, (long long)e.value.flowScopeKey, (long long)e.value.piKey,
+             (long long)procs[e.value.proc].def_key, e.activeSequenceFlows);
+    rows.push_back(buf);
+  }
+  for (auto& [p, c] : parent_child_) {
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", (long long)p, (long long)c);
+    rows.push_back(buf);
+  }
+  for (auto& [c, p] : child_parent_) {
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", (long long)c, (long long)p);
+    rows.push_back(buf);
+  }
+  for (auto& [k, n] : taken_) {
+    // gateway/flow ids need the process: find it via any element instance is not possible here;
+    // ids are process-local indices resolved through the first process that has them
+    int gw = std::get<1>(k), fl = std::get<2>(k);
+    const OProc* proc = nullptr;
+    auto eit = ei_.find(std::get<0>(k));
+    if (eit != ei_.end()) proc = &procs[eit->second.value.proc];
+    snprintf(buf, sizeof buf, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS|%lld|%s|%s|%d", (long long)std::get<0>(k),
+             proc ? proc->els[gw].id.c_str() : "?", proc ? proc->els[fl].id.c_str() : "?", n);
+    rows.push_back(buf);
+  }
+  for (auto& [d, p] : pi_by_def_) {
+    snprintf(buf, sizeof buf, "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY|%lld|%lld", (long long)d, (long long)p);
+    rows.push_back(buf);
+  }
+  for (auto& [k, vr] : vars_) {
+    snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%d,value=%lld", (long long)k.first,
+             names[k.second].c_str(), (long long)vr.key, vr.type, (long long)vr.value);
+    rows.push_back(buf);
+  }
+  for (auto k : event_scope_) {
+    snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", (long long)k);
+    rows.push_back(buf);
+  }
+  for (auto& [k, t] : triggers_) {
+    PiValue pv;
+    pv.proc = t.proc;
+    snprintf(buf, sizeof buf, "EVENT_TRIGGER|%lld|%lld|elementId=%s,processInstanceKey=%lld,vars=%u:%u",
+             (long long)k.first, (long long)k.second, pid(pv, t.elem).c_str(), (long long)t.piKey, t.vars.begin,
+             t.vars.count);
+    rows.push_back(buf);
+  }
+  for (auto& [k, j] : jobs_) {
+    const OProc& p = procs[j.pi.proc];
+    snprintf(buf, sizeof buf,
+             "JOBS|%lld|type=%s,retries=%d,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
+             "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>",
+             (long long)k, j.type.c_str(), j.retries, p.els[j.pi.elem].id.c_str(), (long long)j.elementInstanceKey,
+             (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version);
+    rows.push_back(buf);
+    snprintf(buf, sizeof buf, "JOB_STATES|%lld|ACTIVATABLE", (long long)k);
+    rows.push_back(buf);
+  }
+  for (auto& [t, ten, k] : activatable_) {
+    snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|%s|%lld", t.c_str(), ten.c_str(), (long long)k);
+    rows.push_back(buf);
+  }
+  std::sort(rows.begin(), rows.end());
+  std::string s;
+  for (auto& r : rows) { s += r; s += '\n'; }
+  return s;
+}
+
+}  // namespace
+
+// ============================================================================
+// C API (ctypes) — test infrastructure only
+// ============================================================================
+extern "C" {
+
+void* zbo_new(int partition_id, int partition_count, int max_commands_in_batch, int64_t initial_key) {
+  return new Oracle(partition_id, partition_count, max_commands_in_batch, initial_key);
+}
+void zbo_free(void* o) { delete static_cast<Oracle*>(o); }
+const char* zbo_last_error(void* o) { return static_cast<Oracle*>(o)->last_error.c_str(); }
+
+int zbo_deploy_xml(void* o, const char* xml, int64_t def_key, int version) {
+  return static_cast<Oracle*>(o)->deploy(std::string(xml), def_key, version);
+}
+int zbo_intern(void* o, const char* name) { return static_cast<Oracle*>(o)->intern(name); }
+const char* zbo_name(void* o, int id) {
+  auto* O = static_cast<Oracle*>(o);
+  return id >= 0 && id < (int)O->names.size() ? O->names[id].c_str() : "";
+}
+int zbo_n_elements(void* o, int proc) { return (int)static_cast<Oracle*>(o)->procs.at(proc).els.size(); }
+const char* zbo_element_id(void* o, int proc, int elem) {
+  return static_cast<Oracle*>(o)->procs.at(proc).els.at(elem).id.c_str();
+}
+
+int zbo_submit(void* o, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs, size_t nd) {
+  static_cast<Oracle*>(o)->submit(cmds, n, docs, nd);
+  return 0;
+}
+int zbo_run(void* o) { return static_cast<Oracle*>(o)->run(); }
+
+size_t zbo_n_records(void* o) { return static_cast<Oracle*>(o)->out.size(); }
+size_t zbo_records(void* o, zbhip_record* out, size_t cap) {
+  auto* O = static_cast<Oracle*>(o);
+  size_t n = std::min(cap, O->out.size());
+  for (size_t i = 0; i < n; ++i) out[i] = O->out[i].r;
+  return O->out.size();
+}
+int zbo_reason(void* o, size_t idx, char* buf, size_t cap) {
+  auto* O = static_cast<Oracle*>(o);
+  if (idx >= O->out.size()) return -1;
+  snprintf(buf, cap, "%s", O->out[idx].reason.c_str());
+  return (int)O->out[idx].reason.size();
+}
+void zbo_clear_records(void* o) { static_cast<Oracle*>(o)->out.clear(); }
+int64_t zbo_resolve(void* o, uint32_t instance, uint32_t ord) { return static_cast<Oracle*>(o)->resolve(instance, ord); }
+
+size_t zbo_state(void* o, char* buf, size_t cap) {
+  std::string s = static_cast<Oracle*>(o)->dump_state();
+  if (buf && cap) snprintf(buf, cap, "%s", s.c_str());
+  return s.size() + 1;
+}
+size_t zbo_fallback(void* o, uint32_t* out, size_t cap) {
+  auto* O = static_cast<Oracle*>(o);
+  size_t n = std::min(cap, O->fallback_.size());
+  for (size_t i = 0; i < n; ++i) out[i] = O->fallback_[i];
+  return O->fallback_.size();
+}
+void zbo_counters(void* o, uint64_t* transitions, uint64_t* completed, uint64_t* commands) {
+  auto* O = static_cast<Oracle*>(o);
+  *transitions = O->transitions;
+  *completed = O->completed_instances;
+  *commands = O->commands_processed;
+}
+
+// CPU baseline: `threads` independent partitions (one per host core, as Zeebe runs one
+// actor per partition), each processing `n_instances` CREATE commands and then `phases`
+// windows of JOB:COMPLETE (one per instance, completing the job created in the previous
+// phase).  Returns wall seconds of the processing loop; process compilation excluded.
+double zbo_bench(const char* xml, int threads, int n_instances, int phases, int var_name_kind,
+                 uint64_t seed, uint64_t* transitions_out, uint64_t* completed_out) {
+  std::vector<std::unique_ptr<Oracle>> os;
+  std::vector<std::vector<zbhip_command>> creates(threads);
+  std::vector<std::vector<zbhip_doc_entry>> docs(threads);
+  for (int t = 0; t < threads; ++t) {
+    os.emplace_back(new Oracle(t + 1, threads, 100, 0));
+    if (os.back()->deploy(xml, 2251799813685249LL, 1) < 0) return -1.0;
+    int name = os.back()->intern("amount");
+    uint64_t s = seed + (uint64_t)t * 0x9E3779B97F4A7C15ULL;
+    for (int i = 0; i < n_instances; ++i) {
+      zbhip_command c{};
+      c.instance = (uint32_t)i;
+      c.kind = ZBHIP_CMD_CREATE;
+      c.ref = 0;
+      if (var_name_kind) {
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        zbhip_doc_entry d{};
+        d.name_id = (uint32_t)name;
+        d.type = ZBHIP_DOC_INT;
+        d.value = (int64_t)(s % 2001);
+        c.doc_begin = (uint32_t)docs[t].size();
+        c.doc_count = 1;
+        docs[t].push_back(d);
+      }
+      creates[t].push_back(c);
+    }
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t) {
+    th.emplace_back([&, t]() {
+      Oracle& O = *os[t];
+      O.submit(creates[t].data(), creates[t].size(), docs[t].data(), docs[t].size());
+      O.run();
+      O.out.clear();
+      for (int ph = 0; ph < phases; ++ph) {
+        // complete the job each instance is waiting on (the last JOB:CREATED of the instance)
+        std::vector<zbhip_command> cs;
+        cs.reserve(n_instances);
+        for (int i = 0; i < n_instances; ++i) {
+          auto& ks = O.inst_keys[(uint32_t)i];
+          zbhip_command c{};
+          c.instance = (uint32_t)i;
+          c.kind = ZBHIP_CMD_JOB_COMPLETE;
+          c.ref = (uint16_t)(ks.size() - 1);  // the job key is the last key of the activating batch
+          cs.push_back(c);
+        }
+        O.submit(cs.data(), cs.size(), nullptr, 0);
+        O.run();
+        O.out.clear();
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t tr = 0, cp = 0;
+  for (auto& o : os) { tr += o->transitions; cp += o->completed_instances; }
+  *transitions_out = tr;
+  *completed_out = cp;
+  return sec;
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+"""ctypes / numpy mirror of ``include/zbhip.h`` (the libzbhip.so C ABI).
+
+The layouts here must match the header byte for byte; ``tests/test_abi.py``
+checks the sizes against the compiled library.
+"""
+import ctypes as C
+
+import numpy as np
+
+# ---- protocol enums (protocol/src/main/resources/protocol.xml:23-72) ----
+RT_EVENT, RT_COMMAND, RT_REJECTION = 0, 1, 2
+VT_JOB = 0
+VT_PROCESS_INSTANCE = 5
+VT_MESSAGE = 10
+VT_MESSAGE_SUBSCRIPTION = 11
+VT_PROCESS_MESSAGE_SUBSCRIPTION = 12
+VT_VARIABLE = 17
+VT_PROCESS_INSTANCE_CREATION = 19
+VT_PROCESS_EVENT = 24
+
+REJ_INVALID_ARGUMENT, REJ_NOT_FOUND, REJ_ALREADY_EXISTS, REJ_INVALID_STATE = 0, 1, 2, 3
+REJ_PROCESSING_ERROR, REJ_NONE = 4, 255
+
+# ProcessInstanceIntent (protocol/.../intent/ProcessInstanceIntent.java:22-35)
+PI_INTENTS = {
+    1: "SEQUENCE_FLOW_TAKEN", 2: "ELEMENT_ACTIVATING", 3: "ELEMENT_ACTIVATED",
+    4: "ELEMENT_COMPLETING", 5: "ELEMENT_COMPLETED", 6: "ELEMENT_TERMINATING",
+    7: "ELEMENT_TERMINATED", 8: "ACTIVATE_ELEMENT", 9: "COMPLETE_ELEMENT", 10: "TERMINATE_ELEMENT",
+}
+PI_INTENT_IDS = {v: k for k, v in PI_INTENTS.items()}
+JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED"}
+VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
+PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
+PIC_INTENTS = {0: "CREATE", 1: "CREATED"}
+VALUE_TYPES = {0: "JOB", 5: "PROCESS_INSTANCE", 10: "MESSAGE", 11: "MESSAGE_SUBSCRIPTION",
+               12: "PROCESS_MESSAGE_SUBSCRIPTION", 17: "VARIABLE", 19: "PROCESS_INSTANCE_CREATION",
+               24: "PROCESS_EVENT"}
+RECORD_TYPES = {0: "EVENT", 1: "COMMAND", 2: "COMMAND_REJECTION"}
+REJECTION_TYPES = {0: "INVALID_ARGUMENT", 1: "NOT_FOUND", 2: "ALREADY_EXISTS", 3: "INVALID_STATE",
+                   4: "PROCESSING_ERROR", 255: "NULL_VAL"}
+ELEMENT_TYPES = ["UNSPECIFIED", "PROCESS", "SUB_PROCESS", "EVENT_SUB_PROCESS", "START_EVENT",
+                 "INTERMEDIATE_CATCH_EVENT", "INTERMEDIATE_THROW_EVENT", "BOUNDARY_EVENT", "END_EVENT",
+                 "SERVICE_TASK", "RECEIVE_TASK", "USER_TASK", "MANUAL_TASK", "TASK", "EXCLUSIVE_GATEWAY",
+                 "PARALLEL_GATEWAY", "EVENT_BASED_GATEWAY", "INCLUSIVE_GATEWAY", "SEQUENCE_FLOW"]
+EVENT_TYPES = ["UNSPECIFIED", "CONDITIONAL", "ERROR", "ESCALATION", "LINK", "MESSAGE", "NONE",
+               "SIGNAL", "TERMINATE", "TIMER"]
+
+
+def intent_name(value_type, intent):
+    table = {VT_PROCESS_INSTANCE: PI_INTENTS, VT_JOB: JOB_INTENTS, VT_VARIABLE: VAR_INTENTS,
+             VT_PROCESS_EVENT: PE_INTENTS, VT_PROCESS_INSTANCE_CREATION: PIC_INTENTS}.get(value_type, {})
+    return table.get(intent, str(intent))
+
+
+CMD_CREATE = 1
+CMD_JOB_COMPLETE = 2
+DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER = 0, 1, 2, 3, 4
+DEC_SCALE = 6
+
+RUN_NO_RESULTS = 1
+RUN_TIMED = 2
+
+
+class DocEntry(C.Structure):
+    _fields_ = [("name_id", C.c_uint32), ("type", C.c_uint8), ("pad", C.c_uint8 * 3), ("value", C.c_int64)]
+
+
+class Command(C.Structure):
+    _fields_ = [("instance", C.c_uint32), ("kind", C.c_uint8), ("doc_count", C.c_uint8),
+                ("ref", C.c_uint16), ("doc_begin", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Record(C.Structure):
+    _fields_ = [("key", C.c_int64), ("scope_key", C.c_int64), ("process_instance_key", C.c_int64),
+                ("source_index", C.c_int64), ("process_idx", C.c_int32), ("element_idx", C.c_int32),
+                ("record_type", C.c_uint8), ("value_type", C.c_uint8), ("intent", C.c_uint8),
+                ("rejection_type", C.c_uint8), ("ordinal", C.c_uint32), ("aux", C.c_int64)]
+
+
+class Config(C.Structure):
+    _fields_ = [("partition_id", C.c_int32), ("partition_count", C.c_int32), ("device", C.c_int32),
+                ("max_commands_in_batch", C.c_int32), ("max_instances", C.c_uint32),
+                ("max_commands", C.c_uint32), ("max_records_per_batch", C.c_uint32),
+                ("max_doc_entries", C.c_uint32), ("initial_key", C.c_int64), ("stream", C.c_void_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("commands", C.c_uint64), ("records", C.c_uint64), ("transitions", C.c_uint64),
+                ("completed_instances", C.c_uint64), ("keys", C.c_uint64), ("fallback", C.c_uint64),
+                ("step_ms", C.c_double), ("compact_ms", C.c_double), ("rounds", C.c_uint32),
+                ("launches", C.c_uint32)]
+
+
+COMMAND_DTYPE = np.dtype([("instance", "<u4"), ("kind", "u1"), ("doc_count", "u1"), ("ref", "<u2"),
+                          ("doc_begin", "<u4"), ("pad", "<u4")])
+DOC_DTYPE = np.dtype([("name_id", "<u4"), ("type", "u1"), ("pad", "u1", (3,)), ("value", "<i8")])
+RECORD_DTYPE = np.dtype([("key", "<i8"), ("scope_key", "<i8"), ("process_instance_key", "<i8"),
+                         ("source_index", "<i8"), ("process_idx", "<i4"), ("element_idx", "<i4"),
+                         ("record_type", "u1"), ("value_type", "u1"), ("intent", "u1"),
+                         ("rejection_type", "u1"), ("ordinal", "<u4"), ("aux", "<i8")])
+
+assert COMMAND_DTYPE.itemsize == C.sizeof(Command) == 16
+assert DOC_DTYPE.itemsize == C.sizeof(DocEntry) == 16
+assert RECORD_DTYPE.itemsize == C.sizeof(Record) == 56
+
+
+def make_commands(n):
+    return np.zeros(n, dtype=COMMAND_DTYPE)
+
+
+def make_docs(n):
+    return np.zeros(n, dtype=DOC_DTYPE)
+
+
+def record_tuple(r, element_id=None, name=None):
+    """Canonical comparable tuple of one drained record (numpy row or ctypes Record)."""
+    return (int(r["source_index"]), int(r["ordinal"]), int(r["record_type"]), int(r["value_type"]),
+            int(r["intent"]), int(r["rejection_type"]), int(r["key"]), int(r["scope_key"]),
+            int(r["process_instance_key"]), int(r["process_idx"]), int(r["element_idx"]), int(r["aux"]))

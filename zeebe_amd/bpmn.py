@@ -1,0 +1,201 @@
+"""A small fluent BPMN builder producing the same XML document order as the
+reference's model API (bpmn-model/src/main/java/io/camunda/zeebe/model/bpmn/builder/
+AbstractFlowNodeBuilder.java:92-179): ``createTarget`` appends the target node
+first and then the connecting sequence flow, unless ``sequenceFlowId`` /
+``condition`` created the flow earlier.  Document order matters: the engine
+connects sequence flows in reverse document order (ModelWalker.java:75-79),
+which fixes every ``getOutgoing()`` order.
+
+Usage mirrors ``Bpmn.createExecutableProcess(id).startEvent()...done()``.
+"""
+from xml.sax.saxutils import escape, quoteattr
+
+BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
+ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
+
+
+class _Node:
+    def __init__(self, kind, id_, **attrs):
+        self.kind = kind
+        self.id = id_
+        self.attrs = attrs
+        self.job_type = None
+        self.retries = None
+        self.default = None
+        self.condition = None
+        self.source = None
+        self.target = None
+
+
+class ProcessBuilder:
+    def __init__(self, process_id):
+        self.process_id = process_id
+        self.children = []  # document order
+        self.nodes = {}
+        self.current = None
+        self._pending_flow = None
+        self._counter = 0
+
+    # ---- helpers ----
+    def _gen_id(self, kind):
+        self._counter += 1
+        return "%s_%d" % (kind, self._counter)
+
+    def _flow(self):
+        if self._pending_flow is None:
+            f = _Node("sequenceFlow", self._gen_id("sequenceFlow"))
+            self.children.append(f)
+            self._pending_flow = f
+        return self._pending_flow
+
+    def _add_node(self, kind, id_):
+        id_ = id_ or self._gen_id(kind)
+        n = _Node(kind, id_)
+        self.children.append(n)
+        self.nodes[id_] = n
+        if self.current is not None:
+            self._connect(n)
+        self.current = n
+        return n
+
+    def _connect(self, target):
+        f = self._flow()
+        f.source = self.current.id
+        f.target = target.id
+        self._pending_flow = None
+
+    # ---- fluent API ----
+    def startEvent(self, id_=None):
+        self._add_node("startEvent", id_)
+        return self
+
+    def endEvent(self, id_=None):
+        self._add_node("endEvent", id_)
+        return self
+
+    def serviceTask(self, id_=None, job_type=None, retries=None):
+        n = self._add_node("serviceTask", id_)
+        n.job_type = job_type if job_type is not None else "task"
+        n.retries = retries
+        return self
+
+    def zeebeJobType(self, t):
+        self.current.job_type = t
+        return self
+
+    def exclusiveGateway(self, id_=None):
+        self._add_node("exclusiveGateway", id_)
+        return self
+
+    def parallelGateway(self, id_=None):
+        self._add_node("parallelGateway", id_)
+        return self
+
+    def sequenceFlowId(self, id_):
+        f = self._flow()
+        f.id = id_
+        return self
+
+    def conditionExpression(self, expr):
+        # AbstractFlowNodeBuilder.conditionExpression -> asZeebeExpression: "=" prefix
+        self._flow().condition = expr if expr.startswith("=") else "=" + expr
+        return self
+
+    def condition(self, expr):
+        self._flow().condition = expr
+        return self
+
+    def defaultFlow(self):
+        # AbstractExclusiveGatewayBuilder.defaultFlow: the current flow is created now
+        self.current.default = self._flow()
+        return self
+
+    def moveToLastExclusiveGateway(self):
+        for c in reversed(self.children):
+            if c.kind == "exclusiveGateway":
+                self.current = c
+                return self
+        raise ValueError("no exclusive gateway")
+
+    def moveToLastGateway(self):
+        # AbstractFlowNodeBuilder.findLastGateway: walk unique predecessors from the current node
+        node = self.current
+        while True:
+            prev = [c.source for c in self.children if c.kind == "sequenceFlow" and c.target == node.id]
+            if len(prev) != 1:
+                raise ValueError("Unable to determine an unique previous gateway of " + node.id)
+            node = self.nodes[prev[0]]
+            if node.kind in ("exclusiveGateway", "parallelGateway"):
+                self.current = node
+                return self
+
+    def moveToNode(self, id_):
+        self.current = self.nodes[id_]
+        return self
+
+    def connectTo(self, id_):
+        self._connect(self.nodes[id_])
+        self.current = self.nodes[id_]
+        return self
+
+    def done(self):
+        out = ['<?xml version="1.0" encoding="UTF-8" standalone="no"?>',
+               '<definitions xmlns="%s" xmlns:zeebe="%s" id="definitions" targetNamespace="%s">'
+               % (BPMN_NS, ZEEBE_NS, BPMN_NS),
+               '  <process id=%s isExecutable="true">' % quoteattr(self.process_id)]
+        for c in self.children:
+            if c.kind == "sequenceFlow":
+                attrs = 'id=%s sourceRef=%s targetRef=%s' % (quoteattr(c.id), quoteattr(c.source), quoteattr(c.target))
+                if c.condition is None:
+                    out.append("    <sequenceFlow %s/>" % attrs)
+                else:
+                    out.append("    <sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
+                               % (attrs, escape(c.condition)))
+            elif c.kind == "serviceTask":
+                retries = ' retries="%s"' % c.retries if c.retries is not None else ""
+                out.append('    <serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
+                           '</extensionElements></serviceTask>' % (quoteattr(c.id), quoteattr(c.job_type), retries))
+            elif c.kind == "exclusiveGateway" and c.default:
+                out.append("    <exclusiveGateway id=%s default=%s/>" % (quoteattr(c.id), quoteattr(c.default.id)))
+            else:
+                out.append("    <%s id=%s/>" % (c.kind, quoteattr(c.id)))
+        out.append("  </process>")
+        out.append("</definitions>")
+        return "\n".join(out) + "\n"
+
+
+def createExecutableProcess(process_id):
+    return ProcessBuilder(process_id)
+
+
+# ---- the BASELINE.json workloads -------------------------------------------------------------
+
+def linear_process(n_tasks=10, process_id="linear", job_type="benchmark-task"):
+    """Config 2: start -> task1 .. taskN -> end."""
+    b = createExecutableProcess(process_id).startEvent("start")
+    for i in range(1, n_tasks + 1):
+        b.serviceTask("task%d" % i, job_type)
+    return b.endEvent("end").done()
+
+
+def xor_process(process_id="xor", condition="= amount > 1000"):
+    """Config 3: start -> xor -> [high: condition -> endHigh] [default -> endLow]."""
+    return (createExecutableProcess(process_id).startEvent("start").exclusiveGateway("xor")
+            .sequenceFlowId("high").conditionExpression(condition).endEvent("endHigh")
+            .moveToNode("xor").sequenceFlowId("low").defaultFlow().endEvent("endLow").done())
+
+
+def fork_join_process(branches=8, process_id="forkjoin", tasks=False, job_type="branch"):
+    """Config 4: start -> fork(parallel, N out) -> N flows [-> task_i] -> join(parallel, N in) -> end."""
+    b = createExecutableProcess(process_id).startEvent("start").parallelGateway("fork")
+    for i in range(1, branches + 1):
+        b.moveToNode("fork").sequenceFlowId("f%d" % i)
+        if tasks:
+            b.serviceTask("t%d" % i, job_type)
+            b.sequenceFlowId("j%d" % i)
+        if i == 1:
+            b.parallelGateway("join")
+        else:
+            b.connectTo("join")
+    b.moveToNode("join").sequenceFlowId("toEnd").endEvent("end")
+    return b.done()
