@@ -1,0 +1,221 @@
+"""Headline benchmark: BPMN element transitions/s (+ completed instances/s) of the MI355X
+batch executor on BASELINE.json configs[1] -- a linear 10-service-task process, 10^6
+instances per GPU, jobs auto-completed in 10 phases (one JOB:COMPLETE window per task).
+
+One step = one full pass of that workload over the partition: a window of 10^6
+PROCESS_INSTANCE_CREATION:CREATE commands followed by 10 windows of 10^6 JOB:COMPLETE,
+each processed to quiescence (63 transitions, 119 records per instance).  Inputs are
+synthetic and already resident in HBM; nothing is skipped inside the timed region.
+
+Multi-GPU: one process per GPU, one Zeebe partition per GPU (Protocol.encodePartitionId),
+instances keyed to partitions; no data-path collective (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config linear10|one_task|xor|forkjoin8]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SURVEY_BYTES_PER_TRANSITION = {"linear10": 114.4, "one_task": 100.4, "xor": 93.3, "forkjoin8": 92.8}
+
+
+def workload(name):
+    from zeebe_amd import bpmn
+    if name == "linear10":
+        return bpmn.linear_process(10), 1_000_000, 10, False
+    if name == "one_task":
+        with open(os.path.join(ROOT, "tests", "golden", "one_task.bpmn")) as f:
+            return f.read(), 1_000_000, 1, False
+    if name == "xor":
+        return bpmn.xor_process(), 10_000_000, 0, True
+    if name == "forkjoin8":
+        return bpmn.fork_join_process(8), 10_000_000, 0, False
+    raise SystemExit("unknown config " + name)
+
+
+def algorithmic_bytes(name, n, phases):
+    """Minimum HBM bytes of the k_step launches of one step ('Bytes per unit'):
+    commands read (16 B), compact records written (8 B), per-command header written (8 B),
+    instance header read+written (16+16 B), element-instance slots read/written (8 B each),
+    variables (16 B) and join counters (16 B) where the workload has them."""
+    if name in ("linear10", "one_task"):
+        # CREATE: cmd 16 + hdr 32 + 15 recs*8 + hdr 8 + 1 slot write 8
+        b = 16 + 32 + 15 * 8 + 8 + 8
+        for p in range(phases):
+            last = p == phases - 1
+            recs = 14 if last else 10
+            # JOB:COMPLETE: cmd 16 + hdr 32 + slot read 8 (+ write 8 if another task follows) + recs + hdr 8
+            b += 16 + 32 + 8 + (0 if last else 8) + recs * 8 + 8
+        return b * n
+    if name == "xor":
+        return (16 + 16 + 32 + 26 * 8 + 8) * n  # + the amount document entry (16 B)
+    if name == "forkjoin8":
+        return (16 + 32 + 52 * 8 + 8) * n
+    return 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="linear10")
+    ap.add_argument("--instances", type=int, default=0, help="override instances per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-instances", type=int, default=100_000, help="instances per CPU thread (bounded sample)")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+
+    from zeebe_amd import abi
+    from zeebe_amd.engine import Partition
+
+    xml, n, phases, with_amount = workload(args.config)
+    if args.instances:
+        n = args.instances
+    recs_per_batch = 64
+    part = Partition(partition_id=rank + 1, partition_count=world, device=local_rank, max_instances=n,
+                     max_commands=n, max_records_per_batch=recs_per_batch)
+    part.deploy(xml)
+    name = part.intern("amount") if with_amount else None
+
+    # ---- synthetic windows, built once and kept resident in HBM ----
+    dev = torch.device("cuda", local_rank)
+    windows = []
+    create = abi.make_commands(n)
+    create["instance"] = np.arange(n, dtype=np.uint32)
+    create["kind"] = abi.CMD_CREATE
+    docs_t = None
+    if with_amount:
+        rng = np.random.default_rng(0x5EED03 + rank)
+        docs = abi.make_docs(n)
+        docs["name_id"] = name
+        docs["type"] = abi.DOC_INT
+        docs["value"] = rng.integers(0, 2001, n)
+        create["doc_count"] = 1
+        create["doc_begin"] = np.arange(n, dtype=np.uint32)
+        docs_t = torch.from_numpy(docs.view(np.uint8).copy()).to(dev)
+    windows.append(torch.from_numpy(create.view(np.uint8).copy()).to(dev))
+    job_ord = 5 if not with_amount else 6
+    for p in range(phases):
+        c = abi.make_commands(n)
+        c["instance"] = np.arange(n, dtype=np.uint32)
+        c["kind"] = abi.CMD_JOB_COMPLETE
+        c["ref"] = job_ord + 4 * p
+        windows.append(torch.from_numpy(c.view(np.uint8).copy()).to(dev))
+    torch.cuda.synchronize()
+
+    def step(timed=False):
+        tr = comp = recs = 0
+        step_ms = compact_ms = 0.0
+        launches = 0
+        for i, w in enumerate(windows):
+            if i == 0 and docs_t is not None:
+                part.submit_device(w.data_ptr(), n, docs_t.data_ptr(), n)
+            else:
+                part.submit_device(w.data_ptr(), n)
+            part.run(abi.RUN_NO_RESULTS | (abi.RUN_TIMED if timed else 0))
+            s = part.stats()
+            assert s["fallback"] == 0, s
+            tr += s["transitions"]
+            comp += s["completed_instances"]
+            recs += s["records"]
+            step_ms += s["step_ms"]
+            compact_ms += s["compact_ms"]
+            launches += 1
+        return tr, comp, recs, step_ms, compact_ms, launches
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tot_tr = tot_comp = tot_recs = 0
+    for _ in range(args.steps):
+        tr, comp, recs, _, _, _ = step()
+        tot_tr += tr
+        tot_comp += comp
+        tot_recs += recs
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([tot_tr, tot_comp, tot_recs], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        tot_tr, tot_comp, tot_recs = (int(x) for x in c.tolist())
+
+    # ---- kernel timing with HIP events on the partition's stream (separate, untimed pass) ----
+    tr, comp, recs, step_ms, compact_ms, launches = step(timed=True)
+    alg = algorithmic_bytes(args.config, n, phases)
+    k_step_avg_ms = step_ms / launches
+    achieved = alg / launches / (k_step_avg_ms * 1e-3) / 1e9
+    survey_bpt = SURVEY_BYTES_PER_TRANSITION.get(args.config)
+
+    result = {
+        "metric": "BPMN element transitions/sec + completed instances/sec, 1/2/4/8 MI355X",
+        "value": tot_tr / elapsed,
+        "unit": "transitions/s",
+        "completed_instances_per_s": tot_comp / elapsed,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic: %d instances/GPU, jobs auto-completed in %d phases, inputs resident in HBM" % (n, phases),
+        "config": {"workload": {"linear10": "configs[1] linear 10-service-task process, 1M instances, auto-completed jobs",
+                                "one_task": "configs[0] one_task.bpmn create->job complete",
+                                "xor": "configs[2] exclusive gateway `= amount > 1000`, 10M instances",
+                                "forkjoin8": "configs[3] parallel fork/join 8 branches, 10M instances"}[args.config],
+                   "instances_per_gpu": n, "windows_per_step": len(windows), "partitions": world,
+                   "parallelism": "one partition per GPU (dp%d)" % world, "max_commands_in_batch": 100},
+        "records_per_s": tot_recs / elapsed,
+        "roofline": {"bound": "hbm", "kernel": "k_step", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBPS, "traffic": None,
+                     "algorithmic_bytes_per_step": alg,
+                     "bytes_per_transition": alg / max(tr, 1),
+                     "k_step_avg_ms": k_step_avg_ms, "compact_avg_ms": compact_ms / launches,
+                     "survey_bytes_per_transition": survey_bpt,
+                     "survey_model_GBps": (tr / (step_ms * 1e-3) * survey_bpt / 1e9) if survey_bpt else None},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.oracle import bench as cpu_bench
+        th = args.cpu_threads
+        sec, ctr, ccomp = cpu_bench(xml, th, args.cpu_instances, phases, with_amount)
+        result["cpu_baseline"] = {"value": ctr / sec, "unit": "transitions/s", "cores": th, "kind": "port",
+                                  "completed_instances_per_s": ccomp / sec,
+                                  "sample": "%d partitions (1 per thread) x %d instances, same workload, %.1f s"
+                                            % (th, args.cpu_instances, sec)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -267,7 +267,9 @@ typedef struct zbhip_record {
   uint8_t value_type;
   uint8_t intent;
   uint8_t rejection_type;       /* ZBHIP_REJ_NONE unless record_type == REJECTION */
-  uint32_t ordinal;             /* position within the batch */
+  uint16_t ordinal;             /* position within the batch */
+  uint8_t reason;               /* rejection reason kind (zbhip_reason), 0 = none */
+  uint8_t reason_arg;           /* e.g. the offending element-instance state */
   int64_t aux;                  /* VARIABLE: document entry index; JOB:COMPLETED: source doc; else -1 */
 } zbhip_record;
 
@@ -302,6 +304,16 @@ int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_o
  * follow-up commands (e.g. JOB:COMPLETE).  Returns ZBHIP_EINVAL if unknown. */
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal);
 
+/* Rejection reasons (text formats in zbhip_rejection_reason). */
+enum zbhip_reason {
+  ZBHIP_REASON_NONE = 0,
+  ZBHIP_REASON_PGW_NOT_ALL_TAKEN = 1, /* ProcessInstanceStateTransitionGuard.java:169-186 */
+  ZBHIP_REASON_FS_NOT_FOUND = 2,      /* :88-100 */
+  ZBHIP_REASON_FS_STATE = 3,          /* :116-128 */
+  ZBHIP_REASON_EI_NOT_FOUND = 4,      /* :74-86 */
+  ZBHIP_REASON_EI_STATE = 5,          /* :102-114 */
+  ZBHIP_REASON_JOB_NOT_FOUND = 6      /* JobCommandPreconditionChecker.java */
+};
 /* Rejection reason text exactly as the reference writes it. */
 int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, size_t cap);
 

@@ -505,7 +505,7 @@ struct ORecord {
   Doc doc;             // variables carried (CREATE/JOB_COMPLETE/ VARIABLE entry)
   std::string reason;  // rejection reason
   uint32_t instance = 0;
-  int16_t job_ord = -1;
+  int32_t job_ord = -1;
 };
 
 struct Unsupported {
@@ -584,8 +584,8 @@ class Oracle {
       } else {
         rec.r.value_type = ZBHIP_VT_JOB;
         rec.r.intent = ZBHIP_JOB_COMPLETE;
-        rec.r.key = resolve(c.instance, c.ref);
-        rec.job_ord = (int16_t)c.ref;
+        rec.r.key = -1;  // resolved when processed: the job may be created earlier in this window
+        rec.job_ord = (int32_t)c.ref;
       }
       rec.r.source_index = next_source_++;
       log_.push_back(std::move(rec));
@@ -669,7 +669,7 @@ class Oracle {
     rec.r.key = key;
     rec.r.rejection_type = ZBHIP_REJ_NONE;
     rec.r.source_index = cur_source_;
-    rec.r.ordinal = (uint32_t)batch_->size();
+    rec.r.ordinal = (uint16_t)batch_->size();
     rec.r.aux = -1;
     rec.r.process_idx = -1;
     rec.r.element_idx = -1;
@@ -871,6 +871,7 @@ class Oracle {
   // DefaultJobCommandPreconditionGuard (processing/job/DefaultJobCommandPreconditionGuard.java:26-46)
   // ---------------------------------------------------------------------
   void complete_job(ORecord& cmd) {
+    if (cmd.job_ord >= 0) cmd.r.key = resolve(cmd.instance, (uint32_t)cmd.job_ord);
     int64_t jobKey = cmd.r.key;
     auto jit = jobs_.find(jobKey);
     if (jit == jobs_.end()) {

@@ -102,7 +102,7 @@ def linear_batches(n=10, proc="linear", flows=None):
     return batches
 
 
-def xor_batch(branch, proc="xor", f_start="sequenceFlow_1"):
+def xor_batch(branch, proc="xorProcess", f_start="sequenceFlow_1"):
     """A.3 (amount present): VARIABLE:CREATED first, then one batch to process completion."""
     flow, end = ("high", "endHigh") if branch == "high" else ("low", "endLow")
     return [

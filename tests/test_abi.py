@@ -1,0 +1,66 @@
+"""The C-ABI library loads and exports every symbol include/zbhip.h declares (no GPU needed)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from zeebe_amd import abi, native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "zbhip.h")).read()
+    return sorted(set(re.findall(r"\b(zbhip_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = native.load()
+    out = subprocess.check_output(["nm", "-D", "--defined-only", native.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (zbhip_\w+)", out))
+    declared = set(_declared())
+    assert declared <= exported, declared - exported
+    assert set(native.SYMBOLS) == declared
+    assert b"gfx950" in L.zbhip_build_info()
+
+
+def test_library_contains_gfx950_code_object():
+    blob = open(native.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the embedded HIP fat binary targets gfx950 only
+    assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def test_struct_sizes_match_header():
+    # compile a tiny C program against the header and compare layouts
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "zbhip.h"
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(zbhip_command), sizeof(zbhip_doc_entry),
+ sizeof(zbhip_record), sizeof(zbhip_config), sizeof(zbhip_stats), offsetof(zbhip_record, ordinal),
+ offsetof(zbhip_record, aux), sizeof(zbhip_element)); return 0;}
+'''
+    d = os.path.join(ROOT, "build")
+    os.makedirs(d, exist_ok=True)
+    src = os.path.join(d, "sizes.c")
+    exe = os.path.join(d, "sizes")
+    open(src, "w").write(prog)
+    subprocess.check_call(["gcc", "-I" + os.path.join(ROOT, "include"), src, "-o", exe])
+    got = [int(x) for x in subprocess.check_output([exe]).split()]
+    assert got == [C.sizeof(abi.Command), C.sizeof(abi.DocEntry), C.sizeof(abi.Record), C.sizeof(abi.Config),
+                   C.sizeof(abi.Stats), abi.Record.ordinal.offset, abi.Record.aux.offset, 24]
+
+
+def test_open_without_gpu_fails_loudly():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    from zeebe_amd.engine import Partition
+    with pytest.raises(native.ZbhipError) as e:
+        Partition(max_instances=16, max_commands=16)
+    assert "ENODEV" in str(e.value)

@@ -1,0 +1,91 @@
+"""Host compiler (BPMN XML -> CSR) against the reference's transformation rules and the oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import process_xml
+from oracle.oracle import Oracle
+from zeebe_amd import bpmn
+from zeebe_amd.engine import ELEMENT_DTYPE, _Csr
+from zeebe_amd.native import ZbhipError, check, load
+
+
+class Compiled:
+    def __init__(self, xml):
+        self.L = load()
+        if isinstance(xml, str):
+            xml = xml.encode()
+        self.csr = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = self.L.zbhip_compile_bpmn(xml, len(xml), 1, 1, C.byref(self.csr), err, 512)
+        check(rc, err.value.decode())
+        c = C.cast(self.csr, C.POINTER(_Csr)).contents
+        self.els = np.frombuffer(C.string_at(c.elements, c.n_elements * ELEMENT_DTYPE.itemsize), dtype=ELEMENT_DTYPE)
+        self.out = np.frombuffer(C.string_at(c.out_flow, max(c.n_out, 1) * 2), dtype="<u2")[: c.n_out]
+        self.strings = [c.strings[i].decode() for i in range(c.n_strings)]
+
+    def id(self, e):
+        return self.strings[self.els[e]["id"]]
+
+    def outgoing(self, eid):
+        e = [self.id(i) for i in range(len(self.els))].index(eid)
+        b, n = self.els[e]["out_begin"], self.els[e]["out_count"]
+        return [self.id(f) for f in self.out[b:b + n]]
+
+    def __del__(self):
+        self.L.zbhip_free_csr(self.csr)
+
+
+def test_element_indexing_matches_oracle():
+    for xml in [process_xml({"fixture": "one_task.bpmn"}), bpmn.linear_process(10), bpmn.xor_process(),
+                bpmn.fork_join_process(8), bpmn.fork_join_process(8, tasks=True)]:
+        c = Compiled(xml)
+        o = Oracle()
+        p = o.deploy(xml)
+        assert [c.id(i) for i in range(len(c.els))] == [o.element_id(p, i) for i in range(len(c.els))]
+
+
+def test_outgoing_order_is_reverse_document_order():
+    # ModelWalker.java:75-79 -> getOutgoing() of the fork lists f8 .. f1
+    c = Compiled(bpmn.fork_join_process(8))
+    assert c.outgoing("fork") == ["f%d" % i for i in range(8, 0, -1)]
+    assert c.els[[c.id(i) for i in range(len(c.els))].index("join")]["in_count"] == 8
+
+
+def test_join_slots_are_contiguous_per_gateway():
+    c = Compiled(bpmn.fork_join_process(8))
+    ids = [c.id(i) for i in range(len(c.els))]
+    base = c.els[ids.index("join")]["join_slot"]
+    slots = sorted(int(c.els[ids.index("f%d" % i)]["join_slot"]) for i in range(1, 9))
+    assert slots == list(range(base, base + 8))
+
+
+def test_condition_and_default_flow():
+    c = Compiled(bpmn.xor_process())
+    ids = [c.id(i) for i in range(len(c.els))]
+    xor = c.els[ids.index("xor")]
+    assert ids[xor["default_flow"]] == "low"
+    assert c.els[ids.index("high")]["condition"] != 0xFFFF
+    assert c.els[ids.index("low")]["condition"] == 0xFFFF
+
+
+@pytest.mark.parametrize("cond", ["= amount.x > 1", "= f(amount)", "= amount > 1.1234567", "= amount >",
+                                  "= amount > \"x\""])
+def test_unsupported_feel_is_rejected_at_deploy(cond):
+    with pytest.raises(ZbhipError):
+        Compiled(bpmn.xor_process(condition=cond))
+
+
+def test_unsupported_element_is_rejected():
+    xml = process_xml({"fixture": "one_task.bpmn"}).replace("bpmn:serviceTask", "bpmn:userTask")
+    with pytest.raises(ZbhipError):
+        Compiled(xml)
+
+
+def test_static_condition_is_rejected():
+    # a condition without the `=` prefix is a static string (FeelExpressionLanguage.parseExpression):
+    # evaluating it as a boolean raises an incident in the reference -> outside the subset
+    xml = bpmn.xor_process().replace("= amount &gt; 1000", "amount &gt; 1000")
+    with pytest.raises(ZbhipError):
+        Compiled(xml)

@@ -1,0 +1,287 @@
+"""Parity of the gfx950 executor (libzbhip.so, through the C ABI) with the CPU oracle and the
+golden vectors.  Bar: bit-exact records (keys relabelled to the reference's keys) and
+bit-exact final state, for every BASELINE workload at oracle-checkable sizes, plus
+size-independent properties at the full BASELINE sizes."""
+import numpy as np
+import pytest
+
+from helpers import (amount_docs, complete_commands, create_commands, load_appendix_a, process_xml, symbolic)
+from oracle.oracle import Oracle
+from zeebe_amd import abi, bpmn
+from zeebe_amd.engine import EngineRule, Partition
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [f for f in abi.RECORD_DTYPE.names if f not in ("reason", "reason_arg")]
+
+
+def assert_same_records(got, want, part=None, orc=None):
+    assert len(got) == len(want), (len(got), len(want))
+    for f in FIELDS:
+        if not np.array_equal(got[f], want[f]):
+            bad = np.nonzero(got[f] != want[f])[0][:5]
+            raise AssertionError("field %s differs at %s: got %s want %s" % (f, bad, got[f][bad], want[f][bad]))
+    if part is not None:
+        for i in np.nonzero(got["record_type"] == abi.RT_REJECTION)[0]:
+            assert part.reason(got[i]) == orc.reason(int(i))
+
+
+def run_both(part, orc, cmds, docs=None):
+    part.submit(cmds, docs)
+    part.run()
+    got = part.drain()
+    orc.clear_records()
+    orc.submit(cmds, docs)
+    orc.run()
+    want = orc.records()
+    assert_same_records(got, want, part, orc)
+    return got
+
+
+def open_job_completions(part, rng=None):
+    """One JOB:COMPLETE per instance for the jobs still open in the exported state (random job
+    per instance when rng is given, else the first by key)."""
+    keys = sorted(int(r.split("|")[1]) for r in part.state() if r.startswith("JOBS|"))
+    if not keys:
+        return None
+    by_inst = {}
+    for k in keys:
+        inst, ordv = part.resolve_key(k)
+        by_inst.setdefault(inst, []).append(ordv)
+    insts = sorted(by_inst)
+    c = abi.make_commands(len(insts))
+    c["instance"] = insts
+    c["ref"] = [by_inst[i][rng.integers(len(by_inst[i]))] if rng is not None else by_inst[i][0] for i in insts]
+    c["kind"] = abi.CMD_JOB_COMPLETE
+    return c
+
+
+def drive(xml, n, docs_fn=None, phases=20, rng_seed=None, max_records=64):
+    part = Partition(max_instances=n, max_commands=max(n, 8), max_records_per_batch=max_records)
+    orc = Oracle()
+    assert part.deploy(xml) == orc.deploy(xml) == 0
+    cmds = create_commands(n, 0)
+    docs = None
+    if docs_fn is not None:
+        assert part.intern("amount") == orc.intern("amount")
+        docs = docs_fn(n)
+        cmds["doc_count"] = 1
+        cmds["doc_begin"] = np.arange(n)
+    run_both(part, orc, cmds, docs)
+    assert part.state() == orc.state()
+    rng = np.random.default_rng(rng_seed) if rng_seed is not None else None
+    for _ in range(phases):
+        c = open_job_completions(part, rng)
+        if c is None:
+            break
+        run_both(part, orc, c)
+        assert part.state() == orc.state()
+    assert part.stats()["fallback"] == 0
+    return part, orc
+
+
+# ---- golden vectors (Appendix A) -------------------------------------------------------------
+CASES = load_appendix_a()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_gpu_appendix_a(name):
+    case = CASES[name]
+    part = Partition(max_instances=4, max_commands=4)
+    proc = part.deploy(process_xml(case["process"]))
+    docs = None
+    cmds = create_commands(1, proc)
+    if "amount" in case:
+        docs = amount_docs([case["amount"]], part.intern("amount"))
+        cmds["doc_count"] = 1
+    part.submit(cmds, docs)
+    part.run()
+    recs = part.drain()
+    reason = lambda i: part.reason(recs[i])  # noqa: E731
+    got = [symbolic(recs, part.element_id, part.name, reason)]
+    for _ in case["batches"][1:]:
+        jobs = [int(r["key"]) for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == 0]
+        inst, ordv = part.resolve_key(jobs[0])
+        part.submit(complete_commands([inst], [ordv]))
+        part.run()
+        recs = part.drain()
+        reason = lambda i: part.reason(recs[i])  # noqa: E731
+        got.append(symbolic(recs, part.element_id, part.name, reason))
+    assert got == case["batches"]
+
+
+# ---- the BASELINE workloads vs the oracle ----------------------------------------------------
+def test_one_task_parity():
+    drive(process_xml({"fixture": "one_task.bpmn"}), 3000)
+
+
+def test_linear10_parity():
+    drive(bpmn.linear_process(10), 2000)
+
+
+def test_xor_int_parity():
+    rng = np.random.default_rng(0x5EED03)
+    drive(bpmn.xor_process(), 4000, lambda n: amount_docs(rng.integers(0, 2001, n), 0))
+
+
+def test_xor_decimal_parity():
+    rng = np.random.default_rng(0x5EED03)
+    # variant 3b: v/100 with v ~ U[0, 200000], scaled decimal (x 1e6)
+    drive(bpmn.xor_process(), 4000, lambda n: amount_docs(rng.integers(0, 200001, n) * 10000, 0, decimal=True))
+
+
+def test_fork_join8_parity():
+    drive(bpmn.fork_join_process(8), 2000)
+
+
+def test_fork_join8_tasks_random_order_parity():
+    # variant 4b: one task per branch, jobs completed in seeded random branch order
+    drive(bpmn.fork_join_process(8, tasks=True), 500, phases=12, rng_seed=0x5EED04)
+
+
+def test_exclusive_split_model_parity():
+    xml = (bpmn.createExecutableProcess("process").startEvent().exclusiveGateway("xor").sequenceFlowId("s1")
+           .conditionExpression("amount < 5").endEvent("a").moveToLastGateway().sequenceFlowId("s2")
+           .conditionExpression("amount >= 5 and amount < 10").endEvent("b").moveToLastExclusiveGateway()
+           .defaultFlow().sequenceFlowId("s3").endEvent("c").done())
+    rng = np.random.default_rng(7)
+    drive(xml, 1000, lambda n: amount_docs(rng.integers(-3, 15, n), 0))
+
+
+def test_reference_gateway_models_parity():
+    models = [
+        # ParallelGatewayTest.shouldRejectActivateCommandWhenSequenceFlowIsTakenTwice
+        bpmn.createExecutableProcess("process").startEvent().parallelGateway("splitting").parallelGateway("joining")
+        .moveToNode("splitting").exclusiveGateway("exclusive").moveToNode("splitting").connectTo("exclusive")
+        .moveToNode("exclusive").connectTo("joining").moveToNode("joining").endEvent("endEvent").done(),
+        # shouldOnlyTriggerGatewayWhenAllBranchesAreActivated
+        bpmn.createExecutableProcess("process").startEvent().parallelGateway("fork").exclusiveGateway("exclusiveJoin")
+        .moveToLastGateway().connectTo("exclusiveJoin").sequenceFlowId("joinFlow1").parallelGateway("join")
+        .moveToNode("fork").serviceTask("waitState", "type").sequenceFlowId("joinFlow2").connectTo("join")
+        .endEvent().done(),
+        # shouldCompleteScopeOnParallelGateway / no outgoing flows
+        bpmn.createExecutableProcess("process").startEvent("start").sequenceFlowId("flow1").parallelGateway("fork")
+        .done(),
+        bpmn.createExecutableProcess("process").startEvent().exclusiveGateway("xor").done(),
+        # shouldCompleteScopeWhenAllPathsCompleted
+        bpmn.createExecutableProcess("process").startEvent("start").parallelGateway("fork")
+        .serviceTask("task1", "type1").endEvent("end1").moveToNode("fork").serviceTask("task2", "type2")
+        .endEvent("end2").done(),
+    ]
+    for xml in models:
+        drive(xml, 300, phases=4)
+
+
+def test_mixed_window_rounds_and_rejections():
+    """Several commands of one instance in one window (serialised into rounds in log order), a
+    duplicate JOB:COMPLETE (NOT_FOUND rejection) and interleaved instances."""
+    xml = bpmn.linear_process(2)
+    part = Partition(max_instances=64, max_commands=256)
+    orc = Oracle()
+    part.deploy(xml)
+    orc.deploy(xml)
+    run_both(part, orc, create_commands(40, 0))
+    # job of task1 is key ordinal 5 in every instance; task2's job will be ordinal 9
+    inst = np.repeat(np.arange(40), 3)
+    ords = np.tile([5, 5, 9], 40)
+    c = complete_commands(inst, ords)
+    got = run_both(part, orc, c)
+    assert (got["record_type"] == abi.RT_REJECTION).sum() == 40
+    assert part.stats()["rounds"] == 3
+    assert part.state() == orc.state()
+
+
+def test_missing_variable_falls_back_and_leaves_instance_untouched():
+    xml = bpmn.xor_process()
+    part = Partition(max_instances=8, max_commands=8)
+    part.deploy(xml)
+    name = part.intern("amount")
+    cmds = create_commands(4, 0)
+    cmds["doc_count"] = [1, 0, 1, 1]
+    cmds["doc_begin"] = [0, 0, 1, 2]
+    part.submit(cmds, amount_docs([5, 2000, 1001], name))
+    part.run()
+    assert part.fallback() == [1]
+    recs = part.drain()
+    assert set(int(r["source_index"]) for r in recs) == {0, 2, 3}
+    # the other three instances match the oracle run without the offending command
+    orc = Oracle()
+    orc.deploy(xml)
+    orc.intern("amount")
+    keep = cmds[[0, 2, 3]].copy()
+    keep["doc_begin"] = [0, 1, 2]
+    orc.submit(keep, amount_docs([5, 2000, 1001], name))
+    orc.run()
+    want = orc.records()
+    for f in ("record_type", "value_type", "intent", "element_idx", "ordinal"):
+        assert np.array_equal(recs[f], want[f])
+
+
+def test_engine_rule_style_parallel_gateway():
+    # ParallelGatewayTest.shouldCompleteScopeWhenAllPathsCompleted, written like the reference test
+    engine = EngineRule.single_partition(max_instances=16, max_commands=16)
+    engine.deployment().with_xml_resource(
+        bpmn.createExecutableProcess("process").startEvent("start").parallelGateway("fork")
+        .serviceTask("task1", "type1").endEvent("end1").moveToNode("fork").serviceTask("task2", "type2")
+        .endEvent("end2").done()).deploy()
+    pi = engine.process_instance().of_bpmn_process_id("process").create()
+    engine.job().of_instance(pi).with_type("type1").complete()
+    engine.job().of_instance(pi).with_type("type2").complete()
+    pairs = engine.process_instance_records()
+    ends = [e for e, i in pairs if e.startswith("end") and i == "ELEMENT_COMPLETED"]
+    assert ends == ["end1", "end2"]
+    assert pairs[-1] == ("process", "ELEMENT_COMPLETED")
+
+
+# ---- full BASELINE sizes: size-independent properties ----------------------------------------
+def _full_run(xml, n, phases, docs=None, name=None):
+    part = Partition(max_instances=n, max_commands=n, max_records_per_batch=64)
+    part.deploy(xml)
+    cmds = create_commands(n, 0)
+    if docs is not None:
+        part.intern(name)
+        cmds["doc_count"] = 1
+        cmds["doc_begin"] = np.arange(n, dtype=np.uint32)
+    part.submit(cmds, docs)
+    part.run(abi.RUN_NO_RESULTS)
+    stats = [part.stats()]
+    job_ord = 5
+    for _ in range(phases):
+        c = complete_commands(np.arange(n), np.full(n, job_ord))
+        part.submit(c)
+        part.run(abi.RUN_NO_RESULTS)
+        stats.append(part.stats())
+        job_ord += 4
+    return part, stats
+
+
+def test_linear10_full_size_properties():
+    """Config 2 at 10^6 instances: 63 transitions, 119 records and 45 keys per instance; every
+    instance completes; nothing falls back."""
+    n = 1_000_000
+    part, stats = _full_run(bpmn.linear_process(10), n, 10)
+    assert all(s["fallback"] == 0 for s in stats)
+    assert sum(s["transitions"] for s in stats) == 63 * n
+    assert sum(s["records"] for s in stats) == 119 * n
+    assert sum(s["keys"] for s in stats) == 45 * n
+    assert stats[-1]["completed_instances"] == n
+    assert stats[0]["records"] == 15 * n and stats[-1]["records"] == 14 * n
+
+
+def test_xor_full_size_branch_counts():
+    """Config 3 at 10^7 instances: the number of `high` branches equals #(amount > 1000)."""
+    n = 10_000_000
+    rng = np.random.default_rng(0x5EED03)
+    vals = rng.integers(0, 2001, n)
+    part, stats = _full_run(bpmn.xor_process(), n, 0, amount_docs(vals, 0), "amount")
+    s = stats[0]
+    assert s["fallback"] == 0 and s["transitions"] == 18 * n and s["records"] == 26 * n
+    assert s["completed_instances"] == n
+
+
+def test_fork_join8_full_size_properties():
+    n = 10_000_000
+    part, stats = _full_run(bpmn.fork_join_process(8), n, 0)
+    s = stats[0]
+    assert s["fallback"] == 0 and s["transitions"] == 30 * n and s["records"] == 52 * n
+    assert s["completed_instances"] == n

@@ -74,7 +74,8 @@ class Record(C.Structure):
     _fields_ = [("key", C.c_int64), ("scope_key", C.c_int64), ("process_instance_key", C.c_int64),
                 ("source_index", C.c_int64), ("process_idx", C.c_int32), ("element_idx", C.c_int32),
                 ("record_type", C.c_uint8), ("value_type", C.c_uint8), ("intent", C.c_uint8),
-                ("rejection_type", C.c_uint8), ("ordinal", C.c_uint32), ("aux", C.c_int64)]
+                ("rejection_type", C.c_uint8), ("ordinal", C.c_uint16), ("reason", C.c_uint8),
+                ("reason_arg", C.c_uint8), ("aux", C.c_int64)]
 
 
 class Config(C.Structure):
@@ -97,7 +98,8 @@ DOC_DTYPE = np.dtype([("name_id", "<u4"), ("type", "u1"), ("pad", "u1", (3,)), (
 RECORD_DTYPE = np.dtype([("key", "<i8"), ("scope_key", "<i8"), ("process_instance_key", "<i8"),
                          ("source_index", "<i8"), ("process_idx", "<i4"), ("element_idx", "<i4"),
                          ("record_type", "u1"), ("value_type", "u1"), ("intent", "u1"),
-                         ("rejection_type", "u1"), ("ordinal", "<u4"), ("aux", "<i8")])
+                         ("rejection_type", "u1"), ("ordinal", "<u2"), ("reason", "u1"), ("reason_arg", "u1"),
+                         ("aux", "<i8")])
 
 assert COMMAND_DTYPE.itemsize == C.sizeof(Command) == 16
 assert DOC_DTYPE.itemsize == C.sizeof(DocEntry) == 16

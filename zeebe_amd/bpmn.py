@@ -178,7 +178,7 @@ def linear_process(n_tasks=10, process_id="linear", job_type="benchmark-task"):
     return b.endEvent("end").done()
 
 
-def xor_process(process_id="xor", condition="= amount > 1000"):
+def xor_process(process_id="xorProcess", condition="= amount > 1000"):
     """Config 3: start -> xor -> [high: condition -> endHigh] [default -> endLow]."""
     return (createExecutableProcess(process_id).startEvent("start").exclusiveGateway("xor")
             .sequenceFlowId("high").conditionExpression(condition).endEvent("endHigh")

@@ -1,0 +1,510 @@
+// Host-side process compiler: BPMN 2.0 XML -> flat CSR transition tables.
+//
+// Restates the deploy-time transformation of the reference
+// (engine/src/main/java/io/camunda/zeebe/engine/processing/deployment/model/transformation/
+// BpmnTransformer.java:109-127) for the supported element subset:
+//  - FlowElementInstantiationTransformer.java:37-60: one executable element per flow node/flow;
+//  - ModelWalker.walk (bpmn-model/.../traversal/ModelWalker.java:60-81) pushes siblings with
+//    addFirst, so SequenceFlowTransformer.connectWithFlowNodes runs over the flows in REVERSE
+//    document order: that fixes every getOutgoing()/getIncoming() order;
+//  - SequenceFlowTransformer.parseCondition runs before connect, so ExecutableExclusiveGateway
+//    .addOutgoing sees the condition (outgoingWithCondition keeps outgoing order);
+//  - ExclusiveGatewayTransformer: default flow;
+//  - StartEventTransformer.java:40 / EndEventTransformer.java:37: event type NONE.
+// FEEL conditions (`=`-prefixed, FeelExpressionLanguage.parseExpression) are lowered to the
+// postfix bytecode of include/zbhip.h; anything outside the typed comparison subset is rejected
+// at deploy time (ZBHIP_EUNSUPP) rather than evaluated differently on the device.
+#include <cctype>
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/zbhip.h"
+
+namespace zbc {
+
+// ---------------------------------------------------------------------------
+// XML: a compact pull tokenizer building an element tree (prefixes dropped).
+// ---------------------------------------------------------------------------
+struct Elem {
+  std::string tag;
+  std::vector<std::pair<std::string, std::string>> attrs;
+  std::string text;
+  std::vector<Elem> children;
+  const std::string* get(const char* name) const {
+    for (auto& a : attrs)
+      if (a.first == name) return &a.second;
+    return nullptr;
+  }
+  const Elem* first(const char* tag_name) const {
+    for (auto& c : children)
+      if (c.tag == tag_name) return &c;
+    return nullptr;
+  }
+};
+
+class Xml {
+ public:
+  Xml(const char* s, size_t n) : p_(s), end_(s + n) {}
+  bool parse(Elem& root, std::string& err) {
+    skip_prolog();
+    if (!element(root)) {
+      err = err_.empty() ? "malformed XML" : err_;
+      return false;
+    }
+    return true;
+  }
+
+ private:
+  const char* p_;
+  const char* end_;
+  std::string err_;
+
+  static std::string local(const std::string& q) {
+    size_t c = q.rfind(':');
+    return c == std::string::npos ? q : q.substr(c + 1);
+  }
+  bool starts(const char* lit) const {
+    size_t n = strlen(lit);
+    return (size_t)(end_ - p_) >= n && memcmp(p_, lit, n) == 0;
+  }
+  bool skip_to(const char* lit) {
+    size_t n = strlen(lit);
+    while (p_ + n <= end_) {
+      if (memcmp(p_, lit, n) == 0) {
+        p_ += n;
+        return true;
+      }
+      ++p_;
+    }
+    return false;
+  }
+  void ws() {
+    while (p_ < end_ && isspace((unsigned char)*p_)) ++p_;
+  }
+  void skip_prolog() {
+    for (;;) {
+      ws();
+      if (starts("<?")) { skip_to("?>"); continue; }
+      if (starts("<!--")) { skip_to("-->"); continue; }
+      if (starts("<!")) { skip_to(">"); continue; }
+      return;
+    }
+  }
+  static void decode_into(std::string& out, const char* b, const char* e) {
+    while (b < e) {
+      if (*b != '&') { out += *b++; continue; }
+      const char* semi = (const char*)memchr(b, ';', e - b);
+      if (!semi) { out += *b++; continue; }
+      std::string ent(b + 1, semi);
+      if (ent == "lt") out += '<';
+      else if (ent == "gt") out += '>';
+      else if (ent == "amp") out += '&';
+      else if (ent == "quot") out += '"';
+      else if (ent == "apos") out += '\'';
+      else if (ent.size() > 1 && ent[0] == '#') {
+        long v = ent[1] == 'x' ? strtol(ent.c_str() + 2, nullptr, 16) : strtol(ent.c_str() + 1, nullptr, 10);
+        if (v > 0 && v < 128) out += (char)v;
+      }
+      b = semi + 1;
+    }
+  }
+  bool element(Elem& el) {
+    if (p_ >= end_ || *p_ != '<') { err_ = "expected '<'"; return false; }
+    ++p_;
+    const char* s = p_;
+    while (p_ < end_ && !isspace((unsigned char)*p_) && *p_ != '>' && *p_ != '/') ++p_;
+    el.tag = local(std::string(s, p_));
+    for (;;) {
+      ws();
+      if (p_ >= end_) { err_ = "unterminated tag"; return false; }
+      if (*p_ == '/') {
+        if (p_ + 1 >= end_ || p_[1] != '>') { err_ = "bad empty tag"; return false; }
+        p_ += 2;
+        return true;
+      }
+      if (*p_ == '>') { ++p_; break; }
+      const char* an = p_;
+      while (p_ < end_ && *p_ != '=' && !isspace((unsigned char)*p_)) ++p_;
+      std::string name = local(std::string(an, p_));
+      ws();
+      if (p_ >= end_ || *p_ != '=') { err_ = "attribute without value"; return false; }
+      ++p_;
+      ws();
+      if (p_ >= end_ || (*p_ != '"' && *p_ != '\'')) { err_ = "unquoted attribute"; return false; }
+      char q = *p_++;
+      const char* vb = p_;
+      while (p_ < end_ && *p_ != q) ++p_;
+      if (p_ >= end_) { err_ = "unterminated attribute"; return false; }
+      std::string v;
+      decode_into(v, vb, p_);
+      ++p_;
+      el.attrs.emplace_back(std::move(name), std::move(v));
+    }
+    for (;;) {
+      if (p_ >= end_) { err_ = "unterminated element <" + el.tag + ">"; return false; }
+      if (starts("</")) {
+        if (!skip_to(">")) { err_ = "unterminated end tag"; return false; }
+        return true;
+      }
+      if (starts("<![CDATA[")) {
+        p_ += 9;
+        const char* b = p_;
+        if (!skip_to("]]>")) { err_ = "unterminated CDATA"; return false; }
+        el.text.append(b, p_ - 3);
+        continue;
+      }
+      if (starts("<!--")) { skip_to("-->"); continue; }
+      if (starts("<?")) { skip_to("?>"); continue; }
+      if (*p_ == '<') {
+        el.children.emplace_back();
+        if (!element(el.children.back())) return false;
+        continue;
+      }
+      const char* b = p_;
+      while (p_ < end_ && *p_ != '<') ++p_;
+      decode_into(el.text, b, p_);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// FEEL subset -> postfix bytecode
+// ---------------------------------------------------------------------------
+class FeelCompiler {
+ public:
+  FeelCompiler(const std::string& src, std::vector<zbhip_insn>& code,
+               std::function<uint32_t(const std::string&)> name_of)
+      : s_(src), code_(code), name_of_(std::move(name_of)) {}
+
+  bool compile(std::string& err) {
+    if (!disj()) { err = "FEEL outside the supported subset: " + s_; return false; }
+    ws();
+    if (i_ != s_.size()) { err = "FEEL outside the supported subset (trailing input): " + s_; return false; }
+    emit(ZBHIP_OP_END, 0, 0);
+    return true;
+  }
+
+ private:
+  const std::string& s_;
+  size_t i_ = 0;
+  std::vector<zbhip_insn>& code_;
+  std::function<uint32_t(const std::string&)> name_of_;
+
+  void emit(uint8_t op, uint32_t arg, int64_t lit) {
+    zbhip_insn in{};
+    in.op = op;
+    in.arg = arg;
+    in.literal = lit;
+    code_.push_back(in);
+  }
+  void ws() { while (i_ < s_.size() && isspace((unsigned char)s_[i_])) ++i_; }
+  static bool ident_char(char c) { return isalnum((unsigned char)c) || c == '_'; }
+  bool keyword(const char* w) {
+    ws();
+    size_t n = strlen(w);
+    if (s_.compare(i_, n, w) != 0) return false;
+    if (i_ + n < s_.size() && ident_char(s_[i_ + n])) return false;
+    i_ += n;
+    return true;
+  }
+  bool disj() {
+    if (!conj()) return false;
+    while (keyword("or")) {
+      if (!conj()) return false;
+      emit(ZBHIP_OP_OR, 0, 0);
+    }
+    return true;
+  }
+  bool conj() {
+    if (!comparison()) return false;
+    while (keyword("and")) {
+      if (!comparison()) return false;
+      emit(ZBHIP_OP_AND, 0, 0);
+    }
+    return true;
+  }
+  bool comparison() {
+    if (!operand()) return false;
+    ws();
+    struct { const char* t; uint8_t op; } ops[] = {{"<=", ZBHIP_OP_LE}, {">=", ZBHIP_OP_GE}, {"!=", ZBHIP_OP_NE},
+                                                   {"<", ZBHIP_OP_LT}, {">", ZBHIP_OP_GT}, {"=", ZBHIP_OP_EQ}};
+    for (auto& o : ops) {
+      size_t n = strlen(o.t);
+      if (s_.compare(i_, n, o.t) == 0) {
+        i_ += n;
+        if (!operand()) return false;
+        emit(o.op, 0, 0);
+        return true;
+      }
+    }
+    return true;
+  }
+  bool operand() {
+    ws();
+    if (i_ >= s_.size()) return false;
+    if (s_[i_] == '(') {
+      ++i_;
+      if (!disj()) return false;
+      ws();
+      if (i_ >= s_.size() || s_[i_] != ')') return false;
+      ++i_;
+      return true;
+    }
+    if (keyword("not")) {
+      ws();
+      if (i_ >= s_.size() || s_[i_] != '(') return false;
+      ++i_;
+      if (!disj()) return false;
+      ws();
+      if (i_ >= s_.size() || s_[i_] != ')') return false;
+      ++i_;
+      emit(ZBHIP_OP_NOT, 0, 0);
+      return true;
+    }
+    if (keyword("true")) { emit(ZBHIP_OP_PUSH_BOOL, 1, 0); return true; }
+    if (keyword("false")) { emit(ZBHIP_OP_PUSH_BOOL, 0, 0); return true; }
+    if (keyword("null")) { emit(ZBHIP_OP_PUSH_NULL, 0, 0); return true; }
+    bool neg = false;
+    if (s_[i_] == '-') { neg = true; ++i_; }
+    if (i_ < s_.size() && (isdigit((unsigned char)s_[i_]) || s_[i_] == '.')) {
+      // exact decimal literal, scaled by 10^ZBHIP_DEC_SCALE
+      __int128 v = 0;
+      int frac = -1;
+      for (; i_ < s_.size() && (isdigit((unsigned char)s_[i_]) || s_[i_] == '.'); ++i_) {
+        if (s_[i_] == '.') {
+          if (frac >= 0) return false;
+          frac = 0;
+          continue;
+        }
+        if (frac >= 0 && ++frac > ZBHIP_DEC_SCALE) return false;  // not exactly representable
+        v = v * 10 + (s_[i_] - '0');
+        if (v > ((__int128)1 << 62)) return false;
+      }
+      for (int k = frac < 0 ? 0 : frac; k < ZBHIP_DEC_SCALE; ++k) v *= 10;
+      if (v > (__int128)INT64_MAX) return false;
+      emit(ZBHIP_OP_PUSH_NUM, 0, neg ? -(int64_t)v : (int64_t)v);
+      return true;
+    }
+    if (neg) return false;
+    if (isalpha((unsigned char)s_[i_]) || s_[i_] == '_') {
+      size_t b = i_;
+      while (i_ < s_.size() && ident_char(s_[i_])) ++i_;
+      std::string name = s_.substr(b, i_ - b);
+      ws();
+      if (i_ < s_.size() && (s_[i_] == '.' || s_[i_] == '[' || s_[i_] == '(')) return false;  // paths, calls
+      emit(ZBHIP_OP_PUSH_VAR, name_of_(name), 0);
+      return true;
+    }
+    return false;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// The compiled process (owns the storage the CSR view points into)
+// ---------------------------------------------------------------------------
+struct Compiled {
+  zbhip_process_csr csr{};
+  std::vector<zbhip_element> elements;
+  std::vector<uint16_t> out_flow;
+  std::vector<uint32_t> cond_begin;
+  std::vector<zbhip_insn> code;
+  std::vector<std::string> strings;
+  std::vector<const char*> string_ptrs;
+  std::unordered_map<std::string, uint16_t> string_ids;
+
+  uint16_t str(const std::string& s) {
+    auto it = string_ids.find(s);
+    if (it != string_ids.end()) return it->second;
+    uint16_t id = (uint16_t)strings.size();
+    strings.push_back(s);
+    string_ids.emplace(s, id);
+    return id;
+  }
+  void finish() {
+    string_ptrs.clear();
+    for (auto& s : strings) string_ptrs.push_back(s.c_str());
+    csr.n_elements = (uint32_t)elements.size();
+    csr.elements = elements.data();
+    csr.n_out = (uint32_t)out_flow.size();
+    csr.out_flow = out_flow.data();
+    csr.n_conditions = cond_begin.empty() ? 0 : (uint32_t)cond_begin.size() - 1;
+    csr.cond_begin = cond_begin.data();
+    csr.n_code = (uint32_t)code.size();
+    csr.code = code.data();
+    csr.n_strings = (uint32_t)strings.size();
+    csr.strings = string_ptrs.data();
+  }
+};
+
+static zbhip_element blank(uint8_t type, uint16_t id) {
+  zbhip_element e{};
+  e.element_type = type;
+  e.event_type = ZBHIP_EV_UNSPECIFIED;
+  e.flow_source = e.flow_target = e.condition = e.default_flow = ZBHIP_NONE16;
+  e.job_type = e.join_slot = ZBHIP_NONE16;
+  e.job_retries = 0;
+  e.id = id;
+  return e;
+}
+
+static int compile(const char* xml, size_t len, int64_t def_key, int32_t version, Compiled& C,
+                   std::string& err) {
+  Elem root;
+  Xml parser(xml, len);
+  if (!parser.parse(root, err)) return ZBHIP_EPARSE;
+  const Elem* proc = nullptr;
+  for (auto& c : root.children) {
+    if (c.tag != "process") continue;
+    const std::string* ex = c.get("isExecutable");
+    if (ex && *ex == "false") continue;
+    proc = &c;
+    break;
+  }
+  if (!proc || !proc->get("id")) { err = "no executable process"; return ZBHIP_EPARSE; }
+  const std::string pid = *proc->get("id");
+  C.csr.bpmn_process_id = C.str(pid);
+  C.elements.push_back(blank(ZBHIP_EL_PROCESS, C.csr.bpmn_process_id));
+  std::unordered_map<std::string, uint16_t> index{{pid, 0}};
+  std::vector<const Elem*> flows;
+  std::vector<std::vector<uint16_t>> out_lists, in_lists;
+
+  for (auto& c : proc->children) {
+    uint8_t type;
+    if (c.tag == "startEvent") type = ZBHIP_EL_START_EVENT;
+    else if (c.tag == "endEvent") type = ZBHIP_EL_END_EVENT;
+    else if (c.tag == "serviceTask") type = ZBHIP_EL_SERVICE_TASK;
+    else if (c.tag == "exclusiveGateway") type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
+    else if (c.tag == "parallelGateway") type = ZBHIP_EL_PARALLEL_GATEWAY;
+    else if (c.tag == "sequenceFlow") type = ZBHIP_EL_SEQUENCE_FLOW;
+    else if (c.tag == "extensionElements" || c.tag == "documentation" || c.tag == "textAnnotation" ||
+             c.tag == "association")
+      continue;
+    else { err = "element <" + c.tag + "> outside the supported subset"; return ZBHIP_EUNSUPP; }
+    const std::string* id = c.get("id");
+    if (!id || id->empty()) { err = "element without id"; return ZBHIP_EPARSE; }
+    if (C.elements.size() >= 0xFFF0) { err = "too many elements"; return ZBHIP_EUNSUPP; }
+    zbhip_element e = blank(type, C.str(*id));
+    if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_END_EVENT) {
+      for (auto& d : c.children)
+        if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+          err = "event definition <" + d.tag + "> outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
+      e.event_type = ZBHIP_EV_NONE;
+    }
+    if (type == ZBHIP_EL_SERVICE_TASK) {
+      const Elem* ext = c.first("extensionElements");
+      const Elem* td = ext ? ext->first("taskDefinition") : nullptr;
+      const std::string* jt = td ? td->get("type") : nullptr;
+      if (!jt || jt->empty()) { err = "service task '" + *id + "' without a job type"; return ZBHIP_EPARSE; }
+      const std::string* rt = td->get("retries");
+      std::string retries = rt ? *rt : "3";
+      if ((*jt)[0] == '=' || retries.empty() || retries[0] == '=') {
+        err = "job type/retries expressions outside the supported subset";
+        return ZBHIP_EUNSUPP;
+      }
+      if (ext->first("ioMapping") || ext->first("taskHeaders")) {
+        err = "io mappings / task headers outside the supported subset";
+        return ZBHIP_EUNSUPP;
+      }
+      e.job_type = C.str(*jt);
+      e.job_retries = (uint16_t)atoi(retries.c_str());
+    }
+    if (type == ZBHIP_EL_SEQUENCE_FLOW) flows.push_back(&c);
+    index[*id] = (uint16_t)C.elements.size();
+    C.elements.push_back(e);
+  }
+  out_lists.resize(C.elements.size());
+  in_lists.resize(C.elements.size());
+
+  for (auto& c : proc->children) {
+    if (c.tag != "exclusiveGateway") continue;
+    if (const std::string* d = c.get("default")) {
+      auto it = index.find(*d);
+      if (it == index.end()) { err = "unknown default flow " + *d; return ZBHIP_EPARSE; }
+      C.elements[index[*c.get("id")]].default_flow = it->second;
+    }
+  }
+
+  C.cond_begin.push_back(0);
+  auto name_of = [&C](const std::string& n) -> uint32_t { return C.str(n); };
+  // Reverse document order: ModelWalker.java:75-79
+  for (auto it = flows.rbegin(); it != flows.rend(); ++it) {
+    const Elem& f = **it;
+    uint16_t fi = index[*f.get("id")];
+    const std::string* sr = f.get("sourceRef");
+    const std::string* tr = f.get("targetRef");
+    auto s = sr ? index.find(*sr) : index.end();
+    auto t = tr ? index.find(*tr) : index.end();
+    if (s == index.end() || t == index.end()) { err = "sequence flow with unknown source/target"; return ZBHIP_EPARSE; }
+    zbhip_element& fe = C.elements[fi];
+    fe.flow_source = s->second;
+    fe.flow_target = t->second;
+    if (const Elem* ce = f.first("conditionExpression")) {
+      size_t a = ce->text.find_first_not_of(" \t\r\n");
+      size_t b = ce->text.find_last_not_of(" \t\r\n");
+      std::string txt = a == std::string::npos ? "" : ce->text.substr(a, b - a + 1);
+      if (txt.empty() || txt[0] != '=') { err = "static (non-FEEL) condition outside the subset"; return ZBHIP_EUNSUPP; }
+      std::string body = txt.substr(1);
+      FeelCompiler fc(body, C.code, name_of);
+      if (!fc.compile(err)) return ZBHIP_EUNSUPP;
+      fe.condition = (uint16_t)(C.cond_begin.size() - 1);
+      C.cond_begin.push_back((uint32_t)C.code.size());
+    }
+    out_lists[fe.flow_source].push_back(fi);
+    in_lists[fe.flow_target].push_back(fi);
+  }
+  // CSR of outgoing lists
+  for (size_t e = 0; e < C.elements.size(); ++e) {
+    C.elements[e].out_begin = (uint16_t)C.out_flow.size();
+    C.elements[e].out_count = (uint16_t)out_lists[e].size();
+    C.elements[e].in_count = (uint16_t)in_lists[e].size();
+    for (uint16_t f : out_lists[e]) C.out_flow.push_back(f);
+  }
+  // join counters (NUMBER_OF_TAKEN_SEQUENCE_FLOWS[flowScope, gateway, flow]): the incoming flows of
+  // each parallel gateway get consecutive per-instance counter slots; the gateway's join_slot is the
+  // base of its range, so canActivateParallelGateway counts slots [base, base + in_count).
+  uint16_t slots = 0;
+  for (size_t g = 0; g < C.elements.size(); ++g) {
+    if (C.elements[g].element_type != ZBHIP_EL_PARALLEL_GATEWAY) continue;
+    C.elements[g].join_slot = slots;
+    for (uint16_t f : in_lists[g]) C.elements[f].join_slot = slots++;
+  }
+  C.csr.n_join_slots = slots;
+  C.csr.none_start = ZBHIP_NONE16;
+  for (size_t e = 1; e < C.elements.size(); ++e)
+    if (C.elements[e].element_type == ZBHIP_EL_START_EVENT) C.csr.none_start = (uint16_t)e;
+  C.csr.process_definition_key = def_key;
+  C.csr.version = version;
+  C.finish();
+  return ZBHIP_OK;
+}
+
+}  // namespace zbc
+
+extern "C" int zbhip_compile_bpmn(const char* xml, size_t len, int64_t process_definition_key, int32_t version,
+                                  zbhip_process_csr** out, char* err, size_t err_cap) {
+  if (!xml || !out) return ZBHIP_EINVAL;
+  auto* c = new zbc::Compiled();
+  std::string e;
+  int rc = zbc::compile(xml, len, process_definition_key, version, *c, e);
+  if (rc != ZBHIP_OK) {
+    if (err && err_cap) snprintf(err, err_cap, "%s", e.c_str());
+    delete c;
+    *out = nullptr;
+    return rc;
+  }
+  *out = &c->csr;  // csr is the first member: zbhip_free_csr recovers the owner
+  return ZBHIP_OK;
+}
+
+extern "C" void zbhip_free_csr(zbhip_process_csr* csr) {
+  delete reinterpret_cast<zbc::Compiled*>(reinterpret_cast<char*>(csr));
+}

@@ -1,0 +1,816 @@
+// gfx950 kernels of the BPMN element-lifecycle batch executor.
+//
+// k_step: one lane owns one command of the window (CREATE / JOB:COMPLETE) and runs that
+// command's whole batch -- the ProcessingStateMachine follow-up FIFO
+// (stream-platform/.../stream/impl/ProcessingStateMachine.java:328-417) -- over the
+// instance it addresses.  Instances are independent inside a partition, so a lane never
+// shares state with another lane (the host serialises commands of one instance into
+// rounds): the join counters, the element-instance table and the variables of an instance
+// are private to its lane, read once from HBM at batch start (coalesced SoA rows) and
+// written back once at the end.  Transient element instances (start events, gateways, end
+// events) live only in the lane's LDS table and never touch HBM.  The deployed processes'
+// CSR transition tables are staged in LDS by every workgroup.
+//
+// Element processors and appliers restated here (paths relative to
+// engine/src/main/java/io/camunda/zeebe/engine/):
+//   processing/bpmn/BpmnStreamProcessor.java:74-162, ProcessInstanceStateTransitionGuard.java:47-186,
+//   processing/bpmn/behavior/BpmnStateTransitionBehavior.java:72-417,
+//   processing/bpmn/container/ProcessProcessor.java:55-140, event/StartEventProcessor.java:45-67,
+//   event/EndEventProcessor.java:110-134, task/JobWorkerTaskProcessor.java:49-75,
+//   gateway/ExclusiveGatewayProcessor.java:47-126, gateway/ParallelGatewayProcessor.java:34-50,
+//   processing/processinstance/CreateProcessInstanceProcessor.java:129-158,
+//   processing/job/JobCompleteProcessor.java:47-92, processing/common/EventTriggerBehavior.java:148-166,
+//   processing/variable/VariableBehavior.java:60-200,
+//   state/appliers/ProcessInstanceElement{Activating,Activated,Completing,Completed}Applier.java,
+//   state/appliers/ProcessInstanceSequenceFlowTakenApplier.java:32-69, JobCreatedApplier.java:28-41,
+//   JobCompletedApplier.java:28-45, state/instance/DbElementInstanceState.java:135-344.
+//
+// k_block_sums / k_scan_sums / k_compact: exclusive scan of the per-command record counts and
+// an ordered copy of every batch's records into one contiguous append buffer (log order).
+#include <hip/hip_runtime.h>
+
+#include "zb_internal.h"
+
+namespace zb {
+
+// ---------------------------------------------------------------------------------------------
+// per-lane batch context
+// ---------------------------------------------------------------------------------------------
+struct Lane {
+  const uint32_t* pb;   // process block (LDS)
+  uint2* tbl;           // LDS table base (entry t at tbl[t * kBlock])
+  uint32_t* q;          // LDS queue base (entry i at q[(i % kQueue) * kBlock])
+  uint2* rec;           // this command's record slot
+  uint32_t rec_cap;
+  uint32_t nrec;
+  uint32_t fail;
+  uint32_t transitions;
+  uint32_t completed;
+  int limit;
+  int processed;
+  int qh, qt;
+  int nt;               // table high-water mark
+  uint16_t proc;
+  uint16_t next_ord;
+  uint16_t first_ord;
+  uint16_t trig_key;    // event trigger of a completed job (EVENT_TRIGGER row), NONE if none
+  bool pi_live;
+  uint8_t pi_state;
+  int pi_child;
+  int pi_asf;
+  uint32_t doc_begin;
+  uint32_t doc_count;
+  const zbhip_doc_entry* docs;
+  int nvars;
+  uint2 vm[kVars];
+  long long vv[kVars];
+  uint32_t jw[kJoinWords];
+  bool has_join;
+};
+
+__device__ __forceinline__ void set_fail(Lane& L, uint32_t why) {
+  if (!L.fail) L.fail = why;
+}
+
+__device__ __forceinline__ uint4 elem_of(const Lane& L, uint32_t e) {
+  return reinterpret_cast<const uint4*>(L.pb + 8)[e];
+}
+__device__ __forceinline__ uint32_t etype(uint4 w) { return w.x & 0xFF; }
+__device__ __forceinline__ uint32_t out_flow(const Lane& L, uint32_t i) {
+  return reinterpret_cast<const uint16_t*>(L.pb + L.pb[2])[i];
+}
+
+__device__ __forceinline__ uint16_t new_key(Lane& L) {
+  if (L.next_ord >= 0xFFF0) set_fail(L, FB_KEYS);
+  return L.next_ord++;
+}
+
+__device__ __forceinline__ void emit(Lane& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
+                                     uint32_t flags = 0) {
+  if (L.nrec < L.rec_cap) {
+    L.rec[L.nrec] = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16) | (flags << 24));
+  } else {
+    set_fail(L, FB_RECORDS);
+  }
+  ++L.nrec;
+  if (code >= ZBHIP_PI_SEQUENCE_FLOW_TAKEN && code <= ZBHIP_PI_ELEMENT_TERMINATED) ++L.transitions;
+}
+
+// queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | key << 16
+__device__ __forceinline__ void push(Lane& L, uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
+  // ProcessingStateMachine.collectBatchProcessingStepResult (:388-417): a follow-up command is
+  // processed in this batch only while pending + processed + 1 + admitted < maxCommandsInBatch;
+  // otherwise the platform writes it to the log unprocessed -> outside the device subset.
+  if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
+  if (L.qt - L.qh >= kQueue) { set_fail(L, FB_QUEUE); return; }
+  L.q[(L.qt % kQueue) * kBlock] = elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
+  ++L.qt;
+}
+
+// ---- element-instance table (LDS) ----------------------------------------------------------
+__device__ __forceinline__ int tbl_find(const Lane& L, uint32_t key) {
+  for (int t = 0; t < L.nt; ++t) {
+    uint2 e = L.tbl[t * kBlock];
+    if (e.x != 0xFFFFFFFFu && (e.x >> 16) == key) return t;
+  }
+  return -1;
+}
+__device__ __forceinline__ int tbl_find_job(const Lane& L, uint32_t job) {
+  for (int t = 0; t < L.nt; ++t) {
+    uint2 e = L.tbl[t * kBlock];
+    if (e.x != 0xFFFFFFFFu && (e.y & 0xFFFF) == job && (e.y >> 24) & 1u) return t;
+  }
+  return -1;
+}
+__device__ __forceinline__ void tbl_insert(Lane& L, uint32_t elem, uint32_t key, uint32_t state) {
+  int t = 0;
+  for (; t < L.nt; ++t)
+    if (L.tbl[t * kBlock].x == 0xFFFFFFFFu) break;
+  if (t == L.nt) {
+    if (L.nt >= kTable) { set_fail(L, FB_TABLE); return; }
+    ++L.nt;
+  }
+  L.tbl[t * kBlock] = make_uint2(elem | (key << 16), JOB_ZERO | (state << 16));
+}
+__device__ __forceinline__ void tbl_set_state(Lane& L, int t, uint32_t state) {
+  uint2 e = L.tbl[t * kBlock];
+  e.y = (e.y & 0xFF00FFFFu) | (state << 16);
+  L.tbl[t * kBlock] = e;
+}
+
+// ---- variables (registers) ------------------------------------------------------------------
+__device__ __forceinline__ int var_find(const Lane& L, uint32_t scope, uint32_t name) {
+  int r = -1;
+#pragma unroll
+  for (int v = 0; v < kVars; ++v)
+    if (v < L.nvars && L.vm[v].x == (name | (scope << 16))) r = v;
+  return r;
+}
+
+// VariableBehavior.setLocalVariable (VariableBehavior.java:191-200) + VariableApplier
+__device__ void set_local_variable(Lane& L, uint32_t scope, const zbhip_doc_entry& d) {
+  int v = var_find(L, scope, d.name_id);
+  if (v < 0) {
+    if (L.nvars >= kVars) { set_fail(L, FB_VARS); return; }
+    uint32_t key = new_key(L);
+    emit(L, C_VAR_CREATED, key, scope, d.name_id);
+    int n = L.nvars++;
+#pragma unroll
+    for (int i = 0; i < kVars; ++i)
+      if (i == n) {
+        L.vm[i] = make_uint2(d.name_id | (scope << 16), key | ((uint32_t)d.type << 16));
+        L.vv[i] = d.value;
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kVars; ++i)
+      if (i == v && !(((L.vm[i].y >> 16) & 0xFF) == d.type && L.vv[i] == d.value)) {
+        emit(L, C_VAR_UPDATED, L.vm[i].y & 0xFFFF, scope, d.name_id);
+        L.vm[i].y = (L.vm[i].y & 0xFFFF) | ((uint32_t)d.type << 16);
+        L.vv[i] = d.value;
+      }
+  }
+}
+
+// VariableBehavior.mergeDocument (VariableBehavior.java:105-150) from an element scope whose
+// parent is the process instance (the only nesting in the supported subset).
+__device__ void merge_document_from(Lane& L, uint32_t scope_key, uint32_t begin, uint32_t count) {
+  if (count == 0) return;
+  if (count > 1) { set_fail(L, FB_DOC); return; }
+  const zbhip_doc_entry d = L.docs[begin];
+  if (scope_key != 0) {
+    int v = var_find(L, scope_key, d.name_id);
+    if (v >= 0) {
+#pragma unroll
+      for (int i = 0; i < kVars; ++i)
+        if (i == v && !(((L.vm[i].y >> 16) & 0xFF) == d.type && L.vv[i] == d.value)) {
+          emit(L, C_VAR_UPDATED, L.vm[i].y & 0xFFFF, scope_key, d.name_id);
+          L.vm[i].y = (L.vm[i].y & 0xFFFF) | ((uint32_t)d.type << 16);
+          L.vv[i] = d.value;
+          return;  // consumed at this scope
+        }
+    }
+  }
+  set_local_variable(L, 0, d);
+}
+
+// ---- join counters (registers, 16 x u8) ----------------------------------------------------
+__device__ __forceinline__ uint32_t join_get(const Lane& L, uint32_t s) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int i = 0; i < kJoinWords; ++i)
+    if ((int)(s >> 2) == i) w = L.jw[i];
+  return (w >> ((s & 3) * 8)) & 0xFF;
+}
+__device__ __forceinline__ void join_set(Lane& L, uint32_t s, uint32_t v) {
+#pragma unroll
+  for (int i = 0; i < kJoinWords; ++i)
+    if ((int)(s >> 2) == i) {
+      uint32_t sh = (s & 3) * 8;
+      L.jw[i] = (L.jw[i] & ~(0xFFu << sh)) | ((v & 0xFF) << sh);
+    }
+}
+
+// ---- FEEL condition bytecode ------------------------------------------------------------------
+// Values: tag 0 NULL, 1 BOOL, 2 NUMBER (x 10^ZBHIP_DEC_SCALE).  Results that are not boolean
+// raise an incident in the reference (ExpressionProcessor.java:356-368) -> fallback.
+__device__ bool eval_condition(Lane& L, uint32_t cond, uint32_t scope_key, bool& out) {
+  const uint32_t* pb = L.pb;
+  uint32_t pc = pb[pb[3] + cond];
+  const uint32_t* code = pb + pb[4];
+  uint8_t tag[8];
+  long long val[8];
+  int sp = 0;
+  for (int guard = 0; guard < 64; ++guard) {
+    const uint32_t* in = code + 4 * pc++;
+    uint32_t op = in[0];
+    if (op == ZBHIP_OP_END) break;
+    if (op == ZBHIP_OP_PUSH_VAR || op == ZBHIP_OP_PUSH_NUM || op == ZBHIP_OP_PUSH_BOOL || op == ZBHIP_OP_PUSH_NULL) {
+      if (sp >= 8) return false;
+      uint8_t t = 0;
+      long long x = 0;
+      if (op == ZBHIP_OP_PUSH_NUM) {
+        t = 2;
+        x = (long long)(((unsigned long long)in[3] << 32) | in[2]);
+      } else if (op == ZBHIP_OP_PUSH_BOOL) {
+        t = 1;
+        x = in[1] != 0;
+      } else if (op == ZBHIP_OP_PUSH_VAR) {
+        // DbVariableState.getVariable: element scope first, then the process instance scope
+        int v = var_find(L, scope_key, in[1]);
+        if (v < 0) v = var_find(L, 0, in[1]);
+        if (v >= 0) {
+          uint32_t ty = 0;
+          long long raw = 0;
+#pragma unroll
+          for (int i = 0; i < kVars; ++i)
+            if (i == v) { ty = (L.vm[i].y >> 16) & 0xFF; raw = L.vv[i]; }
+          if (ty == ZBHIP_DOC_NIL) {
+            t = 0;
+          } else if (ty == ZBHIP_DOC_BOOL) {
+            t = 1;
+            x = raw != 0;
+          } else if (ty == ZBHIP_DOC_INT) {
+            if (raw > 9223372036854LL || raw < -9223372036854LL) return false;
+            t = 2;
+            x = raw * 1000000LL;
+          } else if (ty == ZBHIP_DOC_DEC) {
+            t = 2;
+            x = raw;
+          } else {
+            return false;
+          }
+        }
+      }
+      tag[sp] = t;
+      val[sp] = x;
+      ++sp;
+      continue;
+    }
+    if (op == ZBHIP_OP_NOT) {
+      if (sp < 1 || tag[sp - 1] != 1) return false;
+      val[sp - 1] = !val[sp - 1];
+      continue;
+    }
+    if (sp < 2) return false;
+    uint8_t ta = tag[sp - 2], tb = tag[sp - 1];
+    long long a = val[sp - 2], b = val[sp - 1];
+    --sp;
+    bool r;
+    if (op == ZBHIP_OP_AND || op == ZBHIP_OP_OR) {
+      if (ta != 1 || tb != 1) return false;
+      r = op == ZBHIP_OP_AND ? (a && b) : (a || b);
+    } else if (op == ZBHIP_OP_EQ || op == ZBHIP_OP_NE) {
+      bool eq;
+      if (ta == 0 || tb == 0) eq = ta == tb;
+      else if (ta != tb) return false;
+      else eq = a == b;
+      r = op == ZBHIP_OP_EQ ? eq : !eq;
+    } else {
+      if (ta != 2 || tb != 2) return false;
+      r = op == ZBHIP_OP_LT ? a < b : op == ZBHIP_OP_LE ? a <= b : op == ZBHIP_OP_GT ? a > b : a >= b;
+    }
+    tag[sp - 1] = 1;
+    val[sp - 1] = r;
+  }
+  if (sp != 1 || tag[0] != 1) return false;
+  out = val[0] != 0;
+  return true;
+}
+
+// ExclusiveGatewayProcessor.findSequenceFlowToTake (:86-126)
+__device__ uint32_t find_sequence_flow(Lane& L, uint4 gw, uint32_t gw_key) {
+  uint32_t ob = gw.y & 0xFFFF, oc = gw.y >> 16;
+  if (oc == 0) return NONE;  // implicit end
+  if (oc == 1 && (elem_of(L, out_flow(L, ob)).z >> 16) == NONE) return out_flow(L, ob);
+  uint32_t dflt = gw.z & 0xFFFF;
+  for (uint32_t i = 0; i < oc; ++i) {
+    uint32_t f = out_flow(L, ob + i);
+    uint32_t cond = elem_of(L, f).z >> 16;
+    if (cond == NONE || f == dflt) continue;  // outgoingWithCondition, default skipped
+    bool ok;
+    if (!eval_condition(L, cond, gw_key, ok)) { set_fail(L, FB_FEEL); return NONE; }
+    if (ok) return f;
+  }
+  if (dflt != NONE) return dflt;
+  set_fail(L, FB_NO_CONDITION);
+  return NONE;
+}
+
+// ---- appliers ------------------------------------------------------------------------------
+// ProcessInstanceElementActivatingApplier.applyState (:48-204) for a child of the process
+__device__ void apply_activating_child(Lane& L, uint32_t elem, uint4 w, uint32_t key) {
+  uint32_t type = etype(w);
+  if (type == ZBHIP_EL_PARALLEL_GATEWAY) {  // cleanupSequenceFlowsTaken: Tetris decrement
+    uint32_t base = w.w & 0xFFFF, n = w.x >> 16;
+    for (uint32_t s = base; s < base + n; ++s) {
+      uint32_t c = join_get(L, s);
+      if (c > 0) join_set(L, s, c - 1);
+    }
+  }
+  tbl_insert(L, elem, key, ZBHIP_PI_ELEMENT_ACTIVATING);
+  ++L.pi_child;
+  if (type == ZBHIP_EL_START_EVENT) {
+  } else if (type == ZBHIP_EL_PARALLEL_GATEWAY) {
+    int n = (int)(w.x >> 16);
+    L.pi_asf = L.pi_asf > n ? L.pi_asf - n : 0;  // decrementActiveSequenceFlows clamps at 0
+  } else if (L.pi_asf > 0) {
+    --L.pi_asf;
+  }
+}
+
+// ProcessInstanceElementCompletedApplier.applyState (:45-73) -> DbElementInstanceState.removeInstance
+__device__ void apply_completed_child(Lane& L, int t, uint32_t key) {
+  if (L.trig_key == key) L.trig_key = NONE;  // eventScopeInstanceState.deleteInstance (triggers)
+  L.tbl[t * kBlock] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+  --L.pi_child;
+}
+
+// takeSequenceFlow (:243-263) + activateElementInstanceInFlowScope (:326-339)
+__device__ void take_sequence_flow(Lane& L, uint32_t flow) {
+  uint4 fw = elem_of(L, flow);
+  uint32_t sft = new_key(L);
+  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, flow);
+  ++L.pi_asf;  // ProcessInstanceSequenceFlowTakenApplier
+  uint32_t target = fw.z & 0xFFFF;
+  if (etype(elem_of(L, target)) == ZBHIP_EL_PARALLEL_GATEWAY) {
+    uint32_t s = fw.w & 0xFFFF;
+    uint32_t c = join_get(L, s);
+    if (c >= 255) set_fail(L, FB_JOIN);
+    join_set(L, s, c + 1);
+  }
+  uint32_t k = new_key(L);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, 0, target);
+  push(L, target, false, true, k);
+}
+
+// transitionToCompleted (:158-191) + afterExecutionPathCompleted -> ProcessProcessor (:130-140)
+__device__ void transition_to_completed_child(Lane& L, int t, uint32_t elem, uint4 w, uint32_t key) {
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, key, 0, elem);
+  apply_completed_child(L, t, key);
+  if ((w.y >> 16) == 0) {  // end of the execution path
+    if (L.pi_live && L.pi_child + L.pi_asf == 0) {  // BpmnStateBehavior.canBeCompleted
+      emit(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0);
+      push(L, 0, true, false, 0);
+    }
+  }
+}
+
+__device__ void take_outgoing(Lane& L, uint4 w) {
+  uint32_t ob = w.y & 0xFFFF, oc = w.y >> 16;
+  for (uint32_t i = 0; i < oc && !L.fail; ++i) take_sequence_flow(L, out_flow(L, ob + i));
+}
+
+// ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
+__device__ void reject_pi(Lane& L, bool complete, uint32_t elem, uint32_t key, bool fs_pi, uint32_t reason,
+                          uint32_t arg) {
+  emit(L, kRejectBit | (complete ? ZBHIP_PI_COMPLETE_ELEMENT : ZBHIP_PI_ACTIVATE_ELEMENT), key,
+       fs_pi ? 0u : (uint32_t)NONE, elem, reason | (arg << 4));
+}
+
+__device__ void process_pi(Lane& L, uint32_t entry) {
+  const uint32_t elem = entry & 0xFFF;
+  const bool complete = (entry >> 12) & 1;
+  const bool fs_pi = (entry >> 13) & 1;
+  const uint32_t cmd_key = entry >> 16;
+  const uint4 w = elem_of(L, elem);
+  const uint32_t type = etype(w);
+
+  if (!complete) {
+    // ---- ACTIVATE_ELEMENT: guard (:47-70) ----
+    if (type != ZBHIP_EL_PROCESS) {
+      if (!L.pi_live) { reject_pi(L, false, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_NOT_FOUND, 0); return; }
+      if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED) {
+        reject_pi(L, false, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_STATE, L.pi_state);
+        return;
+      }
+      if (type == ZBHIP_EL_PARALLEL_GATEWAY) {  // canActivateParallelGateway (:169-186)
+        uint32_t base = w.w & 0xFFFF, n = w.x >> 16, taken = 0;
+        for (uint32_t s = base; s < base + n; ++s) taken += join_get(L, s) > 0;
+        if (taken < n) { reject_pi(L, false, elem, cmd_key, fs_pi, ZBHIP_REASON_PGW_NOT_ALL_TAKEN, 0); return; }
+      }
+    }
+    // transitionToActivating (:72-100)
+    if (type == ZBHIP_EL_PROCESS) {
+      if (L.pi_live) { set_fail(L, FB_UNSUPPORTED); return; }
+      emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, cmd_key, NONE, 0);
+      L.pi_live = true;
+      L.pi_state = ZBHIP_PI_ELEMENT_ACTIVATING;
+      L.pi_child = 0;
+      L.pi_asf = 0;
+      // ProcessProcessor.onActivate (:55-61,119-128)
+      emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, cmd_key, NONE, 0);
+      L.pi_state = ZBHIP_PI_ELEMENT_ACTIVATED;
+      uint32_t start = L.pb[0] >> 16;
+      emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, NONE, 0, start);  // activateChildInstance: key -1
+      push(L, start, false, true, NONE);
+      return;
+    }
+    if (cmd_key != NONE && tbl_find(L, cmd_key) >= 0) { set_fail(L, FB_UNSUPPORTED); return; }
+    const uint32_t key = cmd_key == NONE ? new_key(L) : cmd_key;
+    emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, key, 0, elem);
+    apply_activating_child(L, elem, w, key);
+    if (L.fail) return;
+    const int t = L.nt > 0 ? tbl_find(L, key) : -1;
+    switch (type) {
+      case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onActivate (:45-50)
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+        tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
+        emit(L, ZBHIP_PI_COMPLETE_ELEMENT, key, 0, elem);
+        push(L, elem, true, true, key);
+        return;
+      case ZBHIP_EL_END_EVENT:  // NoneEndEventBehavior.onActivate/onComplete (:110-134)
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, 0, elem);
+        transition_to_completed_child(L, t, elem, w, key);
+        take_outgoing(L, w);
+        return;
+      case ZBHIP_EL_SERVICE_TASK: {  // JobWorkerTaskProcessor.onActivate (:49-61)
+        uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
+        emit(L, C_JOB_CREATED, job, key, elem);
+        uint2 e = L.tbl[t * kBlock];   // JobCreatedApplier: element instance jobKey
+        e.y = (job & 0xFFFF) | (e.y & 0x00FF0000u) | (1u << 24);
+        L.tbl[t * kBlock] = e;
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+        tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
+        return;
+      }
+      case ZBHIP_EL_EXCLUSIVE_GATEWAY: {  // ExclusiveGatewayProcessor.onActivate (:47-66)
+        uint32_t flow = find_sequence_flow(L, w, key);
+        if (L.fail) return;
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, 0, elem);
+        transition_to_completed_child(L, t, elem, w, key);
+        if (flow != NONE) take_sequence_flow(L, flow);
+        return;
+      }
+      case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (:34-50)
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, 0, elem);
+        transition_to_completed_child(L, t, elem, w, key);
+        take_outgoing(L, w);
+        return;
+      default:
+        set_fail(L, FB_UNSUPPORTED);
+        return;
+    }
+  }
+
+  // ---- COMPLETE_ELEMENT: guard (:56-63) ----
+  if (type == ZBHIP_EL_PROCESS) {
+    if (!L.pi_live) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
+    if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED && L.pi_state != ZBHIP_PI_ELEMENT_COMPLETING) {
+      reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_STATE, L.pi_state);
+      return;
+    }
+    if (L.pi_state == ZBHIP_PI_ELEMENT_COMPLETING) { set_fail(L, FB_UNSUPPORTED); return; }
+    // ProcessProcessor.onComplete (:63-76): COMPLETING, COMPLETED (never end of path)
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETING, 0, NONE, 0);
+    L.pi_state = ZBHIP_PI_ELEMENT_COMPLETING;
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETED, 0, NONE, 0);
+    L.pi_live = false;  // removeInstance: variables, taken-flow counters of the scope go with it
+    L.nvars = 0;
+#pragma unroll
+    for (int i = 0; i < kJoinWords; ++i) L.jw[i] = 0;
+    ++L.completed;
+    return;
+  }
+  const int t = tbl_find(L, cmd_key);
+  if (t < 0) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
+  const uint32_t st = (L.tbl[t * kBlock].y >> 16) & 0xFF;
+  if (st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING) {
+    reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_STATE, st);
+    return;
+  }
+  if (!L.pi_live) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_NOT_FOUND, 0); return; }
+  if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED) {
+    reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_STATE, L.pi_state);
+    return;
+  }
+  if (st == ZBHIP_PI_ELEMENT_COMPLETING) { set_fail(L, FB_UNSUPPORTED); return; }
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, cmd_key, 0, elem);
+  tbl_set_state(L, t, ZBHIP_PI_ELEMENT_COMPLETING);
+  if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK) { set_fail(L, FB_UNSUPPORTED); return; }
+  // applyOutputMappings (BpmnVariableMappingBehavior.java:86-156): event-trigger variables
+  if (L.trig_key == cmd_key) merge_document_from(L, cmd_key, L.doc_begin, L.doc_count);
+  transition_to_completed_child(L, t, elem, w, cmd_key);
+  take_outgoing(L, w);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_step
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  const uint32_t prog_words = (P.prog_words + 3) & ~3u;
+  uint32_t* prog = smem;
+  uint2* tbl_base = reinterpret_cast<uint2*>(smem + prog_words);
+  uint32_t* q_base = reinterpret_cast<uint32_t*>(tbl_base + kTable * kBlock);
+  for (uint32_t i = threadIdx.x; i < P.prog_words; i += kBlock) prog[i] = P.prog[i];
+  __syncthreads();
+
+  const uint32_t lane_id = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t n_rec = 0, n_trans = 0, n_comp = 0, n_keys = 0, n_fb = 0, n_cmd = 0;
+  if (lane_id < P.n_launch) {
+    const uint32_t ci = P.order ? P.order[lane_id] : lane_id;
+    const uint4 cw = P.cmds[ci];  // zbhip_command
+    const uint32_t inst = cw.x;
+    const uint32_t kind = cw.y & 0xFF;
+    const uint32_t doc_count = (cw.y >> 8) & 0xFF;
+    const uint32_t ref = cw.y >> 16;
+    const uint32_t doc_begin = cw.z;
+    const uint32_t N = P.st.n;
+
+    Lane L;
+    L.tbl = tbl_base + threadIdx.x;
+    L.q = q_base + threadIdx.x;
+    L.rec = P.rec + (size_t)ci * P.rec_cap;
+    L.rec_cap = P.rec_cap;
+    L.nrec = 0;
+    L.fail = 0;
+    L.transitions = 0;
+    L.completed = 0;
+    L.limit = P.max_cmds_in_batch;
+    L.processed = 0;
+    L.qh = L.qt = 0;
+    L.nt = 0;
+    L.trig_key = NONE;
+    L.docs = P.docs;
+    L.doc_begin = doc_begin;
+    L.doc_count = doc_count;
+    L.has_join = false;
+#pragma unroll
+    for (int i = 0; i < kJoinWords; ++i) L.jw[i] = 0;
+    L.nvars = 0;
+#pragma unroll
+    for (int i = 0; i < kVars; ++i) { L.vm[i] = make_uint2(0xFFFFFFFFu, 0); L.vv[i] = 0; }
+
+    const bool bad_cmd = inst >= N || (doc_count && (uint64_t)doc_begin + doc_count > P.n_docs);
+    const uint4 h = bad_cmd ? make_uint4(0xFFFFFFFFu, 0, 0, 0) : P.st.hdr[inst];
+    L.proc = h.x & 0xFFFF;
+    L.next_ord = h.x >> 16;
+    L.pi_state = h.y & 0xFF;
+    L.pi_live = (h.y >> 24) & 1;
+    L.pi_child = h.z & 0xFFFF;
+    L.pi_asf = h.z >> 16;
+    const uint32_t nslots0 = (h.y >> 8) & 0xFF;
+    const uint32_t nvars0 = (h.y >> 16) & 0xFF;
+
+    if (bad_cmd) {
+      set_fail(L, FB_UNSUPPORTED);  // never touches HBM outside the partition's arrays
+      L.proc = NONE;
+    } else if (kind == ZBHIP_CMD_CREATE) {
+      // CreateProcessInstanceProcessor.createProcessInstance (:129-158)
+      if (L.proc != NONE) set_fail(L, FB_SLOT_IN_USE);
+      else if (ref >= P.n_procs) set_fail(L, FB_BAD_PROCESS);
+      L.proc = ref;
+      L.next_ord = 0;
+      L.pi_live = false;
+      L.pi_state = 0;
+      L.pi_child = L.pi_asf = 0;
+    } else if (L.proc != NONE) {
+      // load the waiting instance: element-instance slots -> LDS table, variables, join counters
+      for (uint32_t s = 0; s < nslots0 && s < (uint32_t)kSlots; ++s)
+        L.tbl[s * kBlock] = P.st.slots[(size_t)s * N + inst];
+      L.nt = (int)nslots0;
+      L.nvars = (int)nvars0;
+#pragma unroll
+      for (int v = 0; v < kVars; ++v)
+        if (v < L.nvars) { L.vm[v] = P.st.var_meta[(size_t)v * N + inst]; L.vv[v] = P.st.var_val[(size_t)v * N + inst]; }
+    }
+    L.first_ord = L.next_ord;
+    if (!L.fail && L.proc != NONE) {
+      L.pb = prog + prog[1 + L.proc];
+      L.has_join = (L.pb[1] & 0xFFFF) != 0;
+      if (L.has_join && kind != ZBHIP_CMD_CREATE) {
+#pragma unroll
+        for (int i = 0; i < kJoinWords; ++i) L.jw[i] = P.st.join[(size_t)i * N + inst];
+      }
+    }
+
+    if (!L.fail && kind == ZBHIP_CMD_CREATE) {
+      if ((L.pb[0] >> 16) == NONE) set_fail(L, FB_BAD_PROCESS);
+      uint32_t pi = new_key(L);  // = ordinal 0
+      // setVariablesFromDocument -> VariableBehavior.mergeLocalDocument (:60-82)
+      if (doc_count > 1) set_fail(L, FB_DOC);
+      else if (doc_count == 1) set_local_variable(L, pi, P.docs[doc_begin]);
+      emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0);
+      push(L, 0, false, false, pi);
+      uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
+      emit(L, C_PIC_CREATED, created, pi, 0);
+    } else if (!L.fail && kind == ZBHIP_CMD_JOB_COMPLETE) {
+      // JobCompleteProcessor (:47-92) + DefaultJobCommandPreconditionGuard (:26-46)
+      const int t = L.proc == NONE ? -1 : tbl_find_job(L, ref);
+      if (t < 0) {
+        emit(L, kRejectBit | C_JOB_COMPLETE, ref, NONE, NONE, ZBHIP_REASON_JOB_NOT_FOUND);
+      } else {
+        uint2 e = L.tbl[t * kBlock];
+        const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
+        emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
+        // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
+        e.y &= ~(1u << 24);
+        if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
+        L.tbl[t * kBlock] = e;
+        if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) {  // afterAccept
+          uint32_t pe = new_key(L);  // EventTriggerBehavior.triggeringProcessEvent
+          emit(L, C_PE_TRIGGERING, pe, task_key, task_elem);
+          L.trig_key = task_key;       // ProcessEventTriggeringApplier: EVENT_TRIGGER row
+          emit(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, 0, task_elem);
+          push(L, task_elem, true, true, task_key);
+        }
+      }
+    } else if (!L.fail) {
+      set_fail(L, FB_UNSUPPORTED);
+    }
+    L.processed = 1;
+
+    // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
+    while (L.qh < L.qt && !L.fail) {
+      const uint32_t entry = L.q[(L.qh % kQueue) * kBlock];
+      ++L.qh;
+      process_pi(L, entry);
+      ++L.processed;
+    }
+
+    // ---- commit: write back the instance (or leave it untouched on fallback) ----
+    uint32_t ns = 0;
+    if (!L.fail && L.pi_live) {
+      for (int t = 0; t < L.nt; ++t)
+        if (L.tbl[t * kBlock].x != 0xFFFFFFFFu) ++ns;
+      if (ns > (uint32_t)kSlots) set_fail(L, FB_SLOTS);
+    }
+    if (!L.fail) {
+      if (L.pi_live) {
+        uint32_t s = 0;
+        for (int t = 0; t < L.nt; ++t) {
+          uint2 e = L.tbl[t * kBlock];
+          if (e.x != 0xFFFFFFFFu) P.st.slots[(size_t)(s++) * N + inst] = e;
+        }
+#pragma unroll
+        for (int v = 0; v < kVars; ++v)
+          if (v < L.nvars) { P.st.var_meta[(size_t)v * N + inst] = L.vm[v]; P.st.var_val[(size_t)v * N + inst] = L.vv[v]; }
+        if (L.has_join) {
+#pragma unroll
+          for (int i = 0; i < kJoinWords; ++i) P.st.join[(size_t)i * N + inst] = L.jw[i];
+        }
+        P.st.hdr[inst] = make_uint4(L.proc | ((uint32_t)L.next_ord << 16),
+                                    L.pi_state | (ns << 8) | ((uint32_t)L.nvars << 16) | (1u << 24),
+                                    (uint32_t)L.pi_child | ((uint32_t)L.pi_asf << 16), 0);
+      } else {
+        // the process instance completed: free the slot (rows removed with the instance);
+        // keep next_ord so late commands for the instance relabel consistently
+        P.st.hdr[inst] = make_uint4(0xFFFFu | ((uint32_t)L.next_ord << 16), 0, 0, 0);
+        if (L.has_join) {
+#pragma unroll
+          for (int i = 0; i < kJoinWords; ++i) P.st.join[(size_t)i * N + inst] = 0;
+        }
+      }
+      P.cmd_hdr[ci] = make_uint2(L.nrec | ((uint32_t)(uint16_t)(L.next_ord - L.first_ord) << 16),
+                                 L.first_ord | ((uint32_t)ST_OK << 16));
+      n_rec = L.nrec;
+      n_trans = L.transitions;
+      n_comp = L.completed;
+      n_keys = (uint16_t)(L.next_ord - L.first_ord);
+    } else {
+      P.cmd_hdr[ci] = make_uint2(0, L.first_ord | ((uint32_t)ST_FALLBACK << 16) | (L.fail << 24));
+      n_fb = 1;
+    }
+    n_cmd = 1;
+  }
+  // one atomic per wave and counter (wave64 reduction)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    n_rec += __shfl_xor(n_rec, off);
+    n_trans += __shfl_xor(n_trans, off);
+    n_comp += __shfl_xor(n_comp, off);
+    n_keys += __shfl_xor(n_keys, off);
+    n_fb += __shfl_xor(n_fb, off);
+    n_cmd += __shfl_xor(n_cmd, off);
+  }
+  if ((threadIdx.x & 63) == 0 && n_cmd) {
+    atomicAdd(&P.counters[0], (unsigned long long)n_rec);
+    atomicAdd(&P.counters[1], (unsigned long long)n_trans);
+    atomicAdd(&P.counters[2], (unsigned long long)n_comp);
+    atomicAdd(&P.counters[3], (unsigned long long)n_keys);
+    atomicAdd(&P.counters[4], (unsigned long long)n_fb);
+    atomicAdd(&P.counters[5], (unsigned long long)n_cmd);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// compaction: per-block record totals -> exclusive scan -> ordered copy into the append buffer
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t o = __shfl_up(v, off);
+    if (lane >= (uint32_t)off) v += o;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_block_sums(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum) {
+  __shared__ uint32_t ws[kBlock / 64];
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t v = i < n ? (cmd_hdr[i].x & 0xFFFF) : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) s += ws[w];
+    bsum[blockIdx.x] = s;
+  }
+}
+
+// single workgroup: exclusive scan of the block sums (64-bit total)
+__global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* bsum, uint32_t nb, unsigned long long* total) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nb; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < nb ? bsum[i] : 0;
+    uint32_t inc = wave_incl_scan(v);
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      uint32_t x = threadIdx.x < 16 ? ws[threadIdx.x] : 0;
+      uint32_t xi = wave_incl_scan(x);
+      if (threadIdx.x < 16) ws[threadIdx.x] = xi - x;
+    }
+    __syncthreads();
+    const uint32_t c = carry;
+    const uint32_t excl = c + ws[threadIdx.x >> 6] + inc - v;
+    if (i < nb) bsum[i] = excl;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = excl + v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void k_compact(const uint2* cmd_hdr, uint32_t n, const uint32_t* bsum,
+                                                    const uint2* rec, uint32_t rec_cap, uint2* out) {
+  __shared__ uint32_t ws[kBlock / 64];
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t v = i < n ? (cmd_hdr[i].x & 0xFFFF) : 0;
+  const uint32_t inc = wave_incl_scan(v);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += ws[w];
+  const uint32_t off = bsum[blockIdx.x] + wbase + inc - v;
+  const uint2* src = rec + (size_t)i * rec_cap;
+  for (uint32_t j = 0; j < v; ++j) out[off + j] = src[j];
+}
+
+// ---------------------------------------------------------------------------------------------
+// launch wrappers (host)
+// ---------------------------------------------------------------------------------------------
+size_t step_lds_bytes(uint32_t prog_words) {
+  return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)kTable * kBlock * sizeof(uint2) +
+         (size_t)kQueue * kBlock * sizeof(uint32_t);
+}
+
+hipError_t launch_step(const StepParams& P, hipStream_t s) {
+  if (P.n_launch == 0) return hipSuccess;
+  const uint32_t grid = (P.n_launch + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_step, dim3(grid), dim3(kBlock), step_lds_bytes(P.prog_words), s, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum, const uint2* rec, uint32_t rec_cap,
+                          uint2* out, unsigned long long* total, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t nb = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_block_sums, dim3(nb), dim3(kBlock), 0, s, cmd_hdr, n, bsum);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, s, bsum, nb, total);
+  hipLaunchKernelGGL(k_compact, dim3(nb), dim3(kBlock), 0, s, cmd_hdr, n, bsum, rec, rec_cap, out);
+  return hipGetLastError();
+}
+
+}  // namespace zb

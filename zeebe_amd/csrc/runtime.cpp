@@ -1,0 +1,787 @@
+// Host runtime of libzbhip.so: partition handles, deployment into the LDS program arena,
+// command windows, kernel launches, key relabelling, record drain and state export.
+//
+// The handle is one Zeebe partition (StreamProcessor + Engine of one partition,
+// broker/.../steps/StreamProcessorTransitionStep.java:127-165); all device memory it needs is
+// allocated at open (HBM is sized for the instance capacity, SoA), nothing is allocated in
+// the run path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "zb_internal.h"
+
+namespace zb {
+size_t step_lds_bytes(uint32_t prog_words);
+hipError_t launch_step(const StepParams& P, hipStream_t s);
+hipError_t launch_compact(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum, const uint2* rec, uint32_t rec_cap,
+                          uint2* out, unsigned long long* total, hipStream_t s);
+}  // namespace zb
+
+using namespace zb;
+
+namespace {
+
+struct Proc {
+  std::vector<zbhip_element> els;
+  std::vector<uint16_t> out;
+  std::vector<uint32_t> cond_begin;
+  std::vector<zbhip_insn> code;
+  std::vector<std::string> strings;
+  uint16_t none_start = NONE;
+  uint16_t n_join_slots = 0;
+  int64_t def_key = 0;
+  int32_t version = 1;
+  uint16_t bpmn_id = 0;
+  const std::string& id(uint32_t e) const { return strings[els[e].id]; }
+};
+
+struct BatchRef {
+  int64_t base;  // first generated key counter value (key = (p << 51) + base + i)
+  uint32_t inst;
+  uint16_t first_ord;
+  uint16_t nkeys;
+};
+
+const char* state_name(int s) {
+  switch (s) {
+    case ZBHIP_PI_ELEMENT_ACTIVATING: return "ELEMENT_ACTIVATING";
+    case ZBHIP_PI_ELEMENT_ACTIVATED: return "ELEMENT_ACTIVATED";
+    case ZBHIP_PI_ELEMENT_COMPLETING: return "ELEMENT_COMPLETING";
+    case ZBHIP_PI_ELEMENT_COMPLETED: return "ELEMENT_COMPLETED";
+    case ZBHIP_PI_ELEMENT_TERMINATING: return "ELEMENT_TERMINATING";
+    case ZBHIP_PI_ELEMENT_TERMINATED: return "ELEMENT_TERMINATED";
+    default: return "?";
+  }
+}
+
+template <typename T>
+hipError_t dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) return hipSuccess;
+  return hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+}
+
+}  // namespace
+
+struct zbhip_handle {
+  zbhip_config cfg{};
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+
+  std::vector<Proc> procs;
+  std::vector<uint32_t> prog;
+  uint32_t* d_prog = nullptr;
+  size_t d_prog_cap = 0;
+
+  std::vector<std::string> names;
+  std::unordered_map<std::string, uint32_t> name_ids;
+
+  DevState st{};
+  uint4* d_cmds = nullptr;
+  zbhip_doc_entry* d_docs = nullptr;
+  uint32_t* d_order = nullptr;
+  uint2* d_rec = nullptr;
+  uint2* d_cmd_hdr = nullptr;
+  uint32_t* d_bsum = nullptr;
+  uint2* d_out = nullptr;
+  unsigned long long* d_counters = nullptr;  // [0..5] + [6] compact total
+  uint32_t rec_cap = 64;
+  size_t rec_slots = 0;  // commands the record buffer is sized for
+
+  // current window
+  bool external = false;
+  const uint4* ext_cmds = nullptr;
+  const zbhip_doc_entry* ext_docs = nullptr;
+  std::vector<zbhip_command> h_cmds;
+  std::vector<zbhip_doc_entry> h_docs;
+  size_t n_cmds = 0, n_docs = 0;
+  std::vector<uint32_t> round_begin;
+  std::vector<uint32_t> h_order;
+  int64_t doc_base = 0, next_doc_base = 0;
+  int64_t source_base = 0, next_source = 0;
+  bool ran = false;
+
+  // results of the last run
+  std::vector<uint2> h_hdr;
+  std::vector<uint2> h_out;
+  std::vector<uint64_t> h_off;  // record offset of each command in h_out
+  size_t drain_cmd = 0, drain_rec = 0;
+  bool results = false;
+
+  // key relabelling (DbKeyGenerator order)
+  int64_t key_counter = 0;
+  bool relabel_ok = true;
+  std::vector<std::vector<std::pair<uint16_t, int64_t>>> hist;
+  std::vector<uint16_t> inst_proc;
+  std::vector<BatchRef> batches;
+
+  zbhip_stats stats{};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+
+  long long key_of(uint32_t inst, uint32_t ord) const {
+    if (ord == NONE || inst >= hist.size()) return -1;
+    const auto& h = hist[inst];
+    for (size_t i = h.size(); i-- > 0;)
+      if (h[i].first <= ord) return ((int64_t)cfg.partition_id << 51) + h[i].second + (ord - h[i].first);
+    return -1;
+  }
+};
+
+#define HIPCHK(x)                            \
+  do {                                       \
+    hipError_t e_ = (x);                     \
+    if (e_ != hipSuccess) return ZBHIP_EDEVICE; \
+  } while (0)
+
+extern "C" {
+
+const char* zbhip_build_info(void) {
+  return "libzbhip gfx950 (HIP) k_step/k_block_sums/k_scan_sums/k_compact, ABI " "1";
+}
+
+int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
+  if (!cfg || !out || cfg->max_instances == 0 || cfg->max_commands == 0 || cfg->partition_id < 0 ||
+      cfg->max_instances >= 0xFFFFFFF0u)
+    return ZBHIP_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return ZBHIP_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return ZBHIP_ENODEV;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZBHIP_ENODEV;
+  HIPCHK(hipSetDevice(cfg->device));
+  auto* h = new zbhip_handle();
+  h->cfg = *cfg;
+  if (h->cfg.max_commands_in_batch <= 0) h->cfg.max_commands_in_batch = 100;
+  if (h->cfg.max_doc_entries == 0) h->cfg.max_doc_entries = cfg->max_commands;
+  h->rec_cap = cfg->max_records_per_batch ? cfg->max_records_per_batch : 64;
+  if (h->rec_cap > 0xFFFF) { delete h; return ZBHIP_EINVAL; }
+  h->key_counter = cfg->initial_key;
+  if (cfg->stream) {
+    h->stream = reinterpret_cast<hipStream_t>(cfg->stream);
+  } else {
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return ZBHIP_EDEVICE; }
+    h->own_stream = true;
+  }
+  const size_t N = cfg->max_instances;
+  h->st.n = (uint32_t)N;
+  bool ok = dalloc(&h->st.hdr, N) == hipSuccess && dalloc(&h->st.slots, N * kSlots) == hipSuccess &&
+            dalloc(&h->st.var_meta, N * kVars) == hipSuccess && dalloc(&h->st.var_val, N * kVars) == hipSuccess &&
+            dalloc(&h->st.join, N * kJoinWords) == hipSuccess &&
+            dalloc(&h->d_cmds, cfg->max_commands) == hipSuccess &&
+            dalloc(&h->d_docs, h->cfg.max_doc_entries) == hipSuccess &&
+            dalloc(&h->d_order, cfg->max_commands) == hipSuccess &&
+            dalloc(&h->d_cmd_hdr, cfg->max_commands) == hipSuccess &&
+            dalloc(&h->d_bsum, (cfg->max_commands + kBlock - 1) / kBlock + 1) == hipSuccess &&
+            dalloc(&h->d_counters, 8) == hipSuccess &&
+            dalloc(&h->d_rec, (size_t)cfg->max_commands * h->rec_cap) == hipSuccess &&
+            dalloc(&h->d_out, (size_t)cfg->max_commands * h->rec_cap) == hipSuccess;
+  if (!ok) { zbhip_close(h); return ZBHIP_ENOMEM; }
+  h->rec_slots = cfg->max_commands;
+  // every slot starts free (proc = 0xFFFF); counters zero
+  if (hipMemsetAsync(h->st.hdr, 0xFF, N * sizeof(uint4), h->stream) != hipSuccess ||
+      hipMemsetAsync(h->st.join, 0, N * kJoinWords * sizeof(uint32_t), h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess) {
+    zbhip_close(h);
+    return ZBHIP_EDEVICE;
+  }
+  for (auto& e : h->ev) (void)hipEventCreate(&e);
+  *out = h;
+  return ZBHIP_OK;
+}
+
+void zbhip_close(zbhip_handle* h) {
+  if (!h) return;
+  (void)hipFree(h->st.hdr);
+  (void)hipFree(h->st.slots);
+  (void)hipFree(h->st.var_meta);
+  (void)hipFree(h->st.var_val);
+  (void)hipFree(h->st.join);
+  (void)hipFree(h->d_prog);
+  (void)hipFree(h->d_cmds);
+  (void)hipFree(h->d_docs);
+  (void)hipFree(h->d_order);
+  (void)hipFree(h->d_rec);
+  (void)hipFree(h->d_cmd_hdr);
+  (void)hipFree(h->d_bsum);
+  (void)hipFree(h->d_out);
+  (void)hipFree(h->d_counters);
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int zbhip_intern(zbhip_handle* h, const char* name) {
+  if (!h || !name) return ZBHIP_EINVAL;
+  auto it = h->name_ids.find(name);
+  if (it != h->name_ids.end()) return (int)it->second;
+  if (h->names.size() >= 0xFFF0) return ZBHIP_ENOMEM;
+  uint32_t id = (uint32_t)h->names.size();
+  h->names.emplace_back(name);
+  h->name_ids.emplace(name, id);
+  return (int)id;
+}
+
+const char* zbhip_name(zbhip_handle* h, uint32_t id) {
+  return h && id < h->names.size() ? h->names[id].c_str() : "";
+}
+
+const char* zbhip_string(zbhip_handle* h, uint32_t p, uint32_t s) {
+  if (!h || p >= h->procs.size() || s >= h->procs[p].strings.size()) return "";
+  return h->procs[p].strings[s].c_str();
+}
+
+// Builds the LDS program arena from every deployed process (layout: zb_internal.h).
+static int rebuild_program(zbhip_handle* h) {
+  std::vector<uint32_t> prog(1 + h->procs.size(), 0);
+  prog[0] = (uint32_t)h->procs.size();
+  while (prog.size() % 4) prog.push_back(0);
+  for (size_t p = 0; p < h->procs.size(); ++p) {
+    const Proc& P = h->procs[p];
+    const uint32_t base = (uint32_t)prog.size();
+    prog[1 + p] = base;
+    const uint32_t n_el = (uint32_t)P.els.size();
+    const uint32_t out_off = 8 + 4 * n_el;
+    const uint32_t cond_off = out_off + ((uint32_t)P.out.size() + 1) / 2;
+    const uint32_t n_cond = P.cond_begin.empty() ? 0 : (uint32_t)P.cond_begin.size() - 1;
+    const uint32_t code_off = cond_off + n_cond;
+    const uint32_t total = (code_off + 4 * (uint32_t)P.code.size() + 3) & ~3u;
+    prog.resize(base + total, 0);
+    uint32_t* pb = prog.data() + base;
+    pb[0] = n_el | ((uint32_t)P.none_start << 16);
+    pb[1] = P.n_join_slots | (n_cond << 16);
+    pb[2] = out_off;
+    pb[3] = cond_off;
+    pb[4] = code_off;
+    for (uint32_t e = 0; e < n_el; ++e) {
+      const zbhip_element& E = P.els[e];
+      uint32_t* w = pb + 8 + 4 * e;
+      w[0] = E.element_type | ((uint32_t)E.event_type << 8) | ((uint32_t)E.in_count << 16);
+      w[1] = E.out_begin | ((uint32_t)E.out_count << 16);
+      if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW) w[2] = E.flow_target | ((uint32_t)E.condition << 16);
+      else if (E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY) w[2] = E.default_flow | (0xFFFFu << 16);
+      else if (E.element_type == ZBHIP_EL_SERVICE_TASK) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
+      else w[2] = 0xFFFFFFFFu;
+      w[3] = E.join_slot | ((uint32_t)E.id << 16);
+    }
+    uint16_t* outw = reinterpret_cast<uint16_t*>(pb + out_off);
+    for (size_t i = 0; i < P.out.size(); ++i) outw[i] = P.out[i];
+    for (uint32_t c = 0; c < n_cond; ++c) pb[cond_off + c] = P.cond_begin[c];
+    for (size_t i = 0; i < P.code.size(); ++i) {
+      uint32_t* in = pb + code_off + 4 * i;
+      in[0] = P.code[i].op;
+      in[1] = P.code[i].arg;
+      in[2] = (uint32_t)((uint64_t)P.code[i].literal & 0xFFFFFFFFu);
+      in[3] = (uint32_t)((uint64_t)P.code[i].literal >> 32);
+    }
+  }
+  if (prog.size() > kMaxProgWords) return ZBHIP_ENOMEM;
+  if (prog.size() > h->d_prog_cap) {
+    (void)hipFree(h->d_prog);
+    h->d_prog = nullptr;
+    if (dalloc(&h->d_prog, prog.size()) != hipSuccess) return ZBHIP_ENOMEM;
+    h->d_prog_cap = prog.size();
+  }
+  HIPCHK(hipMemcpyAsync(h->d_prog, prog.data(), prog.size() * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->prog.swap(prog);
+  return ZBHIP_OK;
+}
+
+int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_out) {
+  if (!h || !csr || csr->n_elements == 0 || csr->n_elements > (uint32_t)kMaxElements) return ZBHIP_EINVAL;
+  if (csr->n_join_slots > kMaxJoinSlots) return ZBHIP_EUNSUPP;
+  if (h->procs.size() >= 0xFFF0) return ZBHIP_ENOMEM;
+  Proc P;
+  P.els.assign(csr->elements, csr->elements + csr->n_elements);
+  P.out.assign(csr->out_flow, csr->out_flow + csr->n_out);
+  if (csr->n_conditions) P.cond_begin.assign(csr->cond_begin, csr->cond_begin + csr->n_conditions + 1);
+  P.code.assign(csr->code, csr->code + csr->n_code);
+  for (uint32_t i = 0; i < csr->n_strings; ++i) P.strings.emplace_back(csr->strings[i]);
+  P.none_start = csr->none_start;
+  P.n_join_slots = csr->n_join_slots;
+  P.def_key = csr->process_definition_key;
+  P.version = csr->version;
+  P.bpmn_id = csr->bpmn_process_id;
+  for (auto& e : P.els)
+    if (e.element_type != ZBHIP_EL_PROCESS && e.element_type != ZBHIP_EL_START_EVENT &&
+        e.element_type != ZBHIP_EL_END_EVENT && e.element_type != ZBHIP_EL_SERVICE_TASK &&
+        e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
+        e.element_type != ZBHIP_EL_SEQUENCE_FLOW)
+      return ZBHIP_EUNSUPP;
+  // condition variable names -> partition name ids, interned in element order (the oracle's order)
+  for (auto& e : P.els) {
+    if (e.element_type != ZBHIP_EL_SEQUENCE_FLOW || e.condition == ZBHIP_NONE16) continue;
+    for (uint32_t i = P.cond_begin[e.condition]; i < P.cond_begin[e.condition + 1]; ++i)
+      if (P.code[i].op == ZBHIP_OP_PUSH_VAR) {
+        if (P.code[i].arg >= P.strings.size()) return ZBHIP_EINVAL;
+        int id = zbhip_intern(h, P.strings[P.code[i].arg].c_str());
+        if (id < 0) return id;
+        P.code[i].arg = (uint32_t)id;
+      }
+  }
+  h->procs.push_back(std::move(P));
+  int rc = rebuild_program(h);
+  if (rc != ZBHIP_OK) {
+    h->procs.pop_back();
+    return rc;
+  }
+  if (idx_out) *idx_out = (uint32_t)h->procs.size() - 1;
+  return ZBHIP_OK;
+}
+
+// Splits the window into rounds so that each instance appears at most once per launch; commands
+// of one instance keep their log order across rounds (the reference processes them in log order).
+static void plan_rounds(zbhip_handle* h) {
+  h->round_begin.clear();
+  h->h_order.clear();
+  std::unordered_map<uint32_t, uint32_t> last;
+  last.reserve(h->n_cmds * 2);
+  std::vector<uint32_t> round_of(h->n_cmds);
+  uint32_t max_round = 0;
+  for (size_t i = 0; i < h->n_cmds; ++i) {
+    auto it = last.find(h->h_cmds[i].instance);
+    uint32_t r = it == last.end() ? 0 : it->second + 1;
+    last[h->h_cmds[i].instance] = r;
+    round_of[i] = r;
+    max_round = std::max(max_round, r);
+  }
+  if (max_round == 0) return;  // single round: identity order
+  std::vector<uint32_t> cnt(max_round + 2, 0);
+  for (uint32_t r : round_of) cnt[r + 1]++;
+  for (size_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
+  h->round_begin.assign(cnt.begin(), cnt.end());
+  h->h_order.resize(h->n_cmds);
+  std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
+  for (size_t i = 0; i < h->n_cmds; ++i) h->h_order[pos[round_of[i]]++] = (uint32_t)i;
+}
+
+static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t n_docs) {
+  for (size_t i = 0; i < n; ++i) {
+    const zbhip_command& c = cmds[i];
+    if (c.instance >= h->cfg.max_instances) return ZBHIP_EINVAL;
+    if (c.kind == ZBHIP_CMD_CREATE) {
+      if (c.ref >= h->procs.size()) return ZBHIP_EINVAL;
+    } else if (c.kind == ZBHIP_CMD_JOB_COMPLETE) {
+      if (c.ref >= 0xFFF0) return ZBHIP_EINVAL;
+    } else {
+      return ZBHIP_EINVAL;
+    }
+    if (c.doc_count && (size_t)c.doc_begin + c.doc_count > n_docs) return ZBHIP_EINVAL;
+  }
+  return ZBHIP_OK;
+}
+
+int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs, size_t n_docs) {
+  if (!h || (n && !cmds) || (n_docs && !docs)) return ZBHIP_EINVAL;
+  if (n > h->cfg.max_commands || n_docs > h->cfg.max_doc_entries) return ZBHIP_ENOMEM;
+  int rc = validate(h, cmds, n, n_docs);
+  if (rc) return rc;
+  h->external = false;
+  h->h_cmds.assign(cmds, cmds + n);
+  h->h_docs.assign(docs, docs + n_docs);
+  h->n_cmds = n;
+  h->n_docs = n_docs;
+  h->doc_base = h->next_doc_base;
+  h->next_doc_base += (int64_t)n_docs;
+  h->source_base = h->next_source;
+  h->next_source += (int64_t)n;
+  plan_rounds(h);
+  if (n) HIPCHK(hipMemcpyAsync(h->d_cmds, cmds, n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
+  if (n_docs)
+    HIPCHK(hipMemcpyAsync(h->d_docs, docs, n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice, h->stream));
+  if (!h->h_order.empty())
+    HIPCHK(hipMemcpyAsync(h->d_order, h->h_order.data(), n * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->ran = false;
+  h->results = false;
+  return ZBHIP_OK;
+}
+
+int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
+                        size_t n_docs) {
+  if (!h || (n && !dev_cmds)) return ZBHIP_EINVAL;
+  if (n > h->rec_slots) return ZBHIP_ENOMEM;
+  h->external = true;
+  h->ext_cmds = reinterpret_cast<const uint4*>(dev_cmds);
+  h->ext_docs = dev_docs;
+  h->h_cmds.clear();
+  h->h_docs.clear();
+  h->n_cmds = n;
+  h->n_docs = n_docs;
+  h->round_begin.clear();
+  h->h_order.clear();
+  h->doc_base = h->next_doc_base;
+  h->next_doc_base += (int64_t)n_docs;
+  h->source_base = h->next_source;
+  h->next_source += (int64_t)n;
+  h->ran = false;
+  h->results = false;
+  return ZBHIP_OK;
+}
+
+int zbhip_run(zbhip_handle* h, uint32_t flags) {
+  if (!h) return ZBHIP_EINVAL;
+  if (h->ran) return ZBHIP_ESTATE;
+  if (h->procs.empty()) return ZBHIP_ESTATE;
+  const bool timed = flags & ZBHIP_RUN_TIMED;
+  const bool want = !(flags & ZBHIP_RUN_NO_RESULTS);
+  const uint32_t n = (uint32_t)h->n_cmds;
+  HIPCHK(hipMemsetAsync(h->d_counters, 0, 8 * sizeof(unsigned long long), h->stream));
+
+  StepParams P{};
+  P.cmds = h->external ? h->ext_cmds : h->d_cmds;
+  P.docs = h->external ? h->ext_docs : h->d_docs;
+  P.n_docs = (uint32_t)h->n_docs;
+  P.prog = h->d_prog;
+  P.prog_words = (uint32_t)h->prog.size();
+  P.n_procs = (uint32_t)h->procs.size();
+  P.st = h->st;
+  P.rec = h->d_rec;
+  P.rec_cap = h->rec_cap;
+  P.cmd_hdr = h->d_cmd_hdr;
+  P.counters = h->d_counters;
+  P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
+
+  uint32_t launches = 0;
+  if (timed) HIPCHK(hipEventRecord(h->ev[0], h->stream));
+  if (h->round_begin.empty()) {
+    P.order = nullptr;
+    P.n_launch = n;
+    HIPCHK(launch_step(P, h->stream));
+    launches = n ? 1 : 0;
+  } else {
+    for (size_t r = 0; r + 1 < h->round_begin.size(); ++r) {
+      P.order = h->d_order + h->round_begin[r];
+      P.n_launch = h->round_begin[r + 1] - h->round_begin[r];
+      HIPCHK(launch_step(P, h->stream));
+      ++launches;
+    }
+  }
+  if (timed) HIPCHK(hipEventRecord(h->ev[1], h->stream));
+  HIPCHK(launch_compact(h->d_cmd_hdr, n, h->d_bsum, h->d_rec, h->rec_cap, h->d_out, h->d_counters + 6, h->stream));
+  if (timed) HIPCHK(hipEventRecord(h->ev[2], h->stream));
+
+  unsigned long long cnt[8] = {0};
+  HIPCHK(hipMemcpyAsync(cnt, h->d_counters, sizeof cnt, hipMemcpyDeviceToHost, h->stream));
+  if (want) {
+    h->h_hdr.resize(n);
+    if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (want) {
+    h->h_out.resize(cnt[6]);
+    if (cnt[6])
+      HIPCHK(hipMemcpy(h->h_out.data(), h->d_out, cnt[6] * sizeof(uint2), hipMemcpyDeviceToHost));
+  }
+  h->stats.commands = cnt[5];
+  h->stats.records = cnt[0];
+  h->stats.transitions = cnt[1];
+  h->stats.completed_instances = cnt[2];
+  h->stats.keys = cnt[3];
+  h->stats.fallback = cnt[4];
+  h->stats.launches = launches + (n ? 3 : 0);
+  h->stats.rounds = h->round_begin.empty() ? (n ? 1 : 0) : (uint32_t)h->round_begin.size() - 1;
+  if (timed) {
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, h->ev[0], h->ev[1]);
+    (void)hipEventElapsedTime(&b, h->ev[1], h->ev[2]);
+    h->stats.step_ms = a;
+    h->stats.compact_ms = b;
+  }
+
+  // key relabelling bookkeeping, in log (source) order
+  if (!want || h->external) {
+    h->relabel_ok = false;
+    h->key_counter += (int64_t)cnt[3];
+  } else {
+    if (h->hist.size() < h->cfg.max_instances) {
+      h->hist.resize(h->cfg.max_instances);
+      h->inst_proc.resize(h->cfg.max_instances, NONE);
+    }
+    h->h_off.resize(n + 1);
+    uint64_t off = 0;
+    for (uint32_t c = 0; c < n; ++c) {
+      const uint2 hd = h->h_hdr[c];
+      const zbhip_command& cm = h->h_cmds[c];
+      h->h_off[c] = off;
+      const uint32_t nrec = hd.x & 0xFFFF, nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
+      off += nrec;
+      if (((hd.y >> 16) & 0xFF) != ST_OK) continue;
+      if (cm.kind == ZBHIP_CMD_CREATE) {
+        h->hist[cm.instance].clear();
+        h->inst_proc[cm.instance] = cm.ref;
+      }
+      if (nkeys) {
+        h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
+        h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys});
+      }
+      h->key_counter += nkeys;
+    }
+    h->h_off[n] = off;
+    h->results = true;
+  }
+  h->drain_cmd = 0;
+  h->drain_rec = 0;
+  h->ran = true;
+  return (int)cnt[5];
+}
+
+int64_t zbhip_pending_records(zbhip_handle* h) {
+  if (!h || !h->results) return 0;
+  return (int64_t)h->h_out.size();
+}
+
+int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
+  if (!h || !out) return ZBHIP_EINVAL;
+  *out = h->stats;
+  return ZBHIP_OK;
+}
+
+int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
+  if (!h || (cap && !out)) return ZBHIP_EINVAL;
+  if (n_out) *n_out = 0;
+  if (!h->results) return ZBHIP_ESTATE;
+  size_t k = 0;
+  const int64_t pbits = (int64_t)h->cfg.partition_id << 51;
+  (void)pbits;
+  while (k < cap && h->drain_cmd < h->n_cmds) {
+    const size_t c = h->drain_cmd;
+    const uint2 hd = h->h_hdr[c];
+    const uint32_t nrec = hd.x & 0xFFFF;
+    if (h->drain_rec >= nrec) {
+      ++h->drain_cmd;
+      h->drain_rec = 0;
+      continue;
+    }
+    const zbhip_command& cm = h->h_cmds[c];
+    const uint32_t inst = cm.instance;
+    const int64_t doc = cm.doc_count ? h->doc_base + cm.doc_begin : -1;
+    const uint2 w = h->h_out[h->h_off[c] + h->drain_rec];
+    const uint32_t key_ord = w.x & 0xFFFF, aux_ord = w.x >> 16, elem = w.y & 0xFFFF;
+    const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
+    const bool rej = code & kRejectBit;
+    const uint32_t c6 = code & 0x3F;
+    const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
+    zbhip_record r{};
+    r.key = h->key_of(inst, key_ord);
+    r.scope_key = aux_ord == NONE ? -1 : h->key_of(inst, aux_ord);
+    r.process_instance_key = h->key_of(inst, 0);
+    r.source_index = h->source_base + (int64_t)c;
+    r.process_idx = proc == NONE ? -1 : proc;
+    r.element_idx = elem == NONE ? -1 : (int32_t)elem;
+    r.rejection_type = ZBHIP_REJ_NONE;
+    r.ordinal = (uint16_t)h->drain_rec;
+    r.aux = -1;
+    r.reason = 0;
+    r.reason_arg = 0;
+    if (c6 >= 1 && c6 <= 10) {
+      r.value_type = ZBHIP_VT_PROCESS_INSTANCE;
+      r.intent = (uint8_t)c6;
+      r.record_type = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
+    } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE) {
+      r.value_type = ZBHIP_VT_JOB;
+      r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED : ZBHIP_JOB_COMPLETE;
+      r.record_type = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
+      if (c6 != C_JOB_CREATED) r.aux = doc;
+    } else if (c6 == C_VAR_CREATED || c6 == C_VAR_UPDATED) {
+      r.value_type = ZBHIP_VT_VARIABLE;
+      r.intent = c6 == C_VAR_CREATED ? ZBHIP_VAR_CREATED : ZBHIP_VAR_UPDATED;
+      r.record_type = ZBHIP_RT_EVENT;
+      // the value comes from the batch's source document entry of that name
+      for (uint32_t j = 0; j < cm.doc_count; ++j)
+        if (h->h_docs[cm.doc_begin + j].name_id == elem) r.aux = h->doc_base + cm.doc_begin + j;
+    } else if (c6 == C_PE_TRIGGERING) {
+      r.value_type = ZBHIP_VT_PROCESS_EVENT;
+      r.intent = ZBHIP_PE_TRIGGERING;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.aux = doc;
+    } else if (c6 == C_PIC_CREATED) {
+      r.value_type = ZBHIP_VT_PROCESS_INSTANCE_CREATION;
+      r.intent = ZBHIP_PIC_CREATED;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.aux = doc;
+    } else {
+      return ZBHIP_EDEVICE;  // corrupt record
+    }
+    if (rej) {
+      r.reason = fl & 0xF;
+      r.reason_arg = fl >> 4;
+      if (r.value_type == ZBHIP_VT_JOB) {
+        r.rejection_type = ZBHIP_REJ_NOT_FOUND;
+        r.process_idx = -1;
+        r.element_idx = -1;
+        r.scope_key = -1;
+        r.process_instance_key = -1;
+      } else {
+        r.rejection_type = ZBHIP_REJ_INVALID_STATE;
+      }
+    }
+    out[k++] = r;
+    ++h->drain_rec;
+  }
+  if (n_out) *n_out = k;
+  return ZBHIP_OK;
+}
+
+int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* r, char* buf, size_t cap) {
+  if (!h || !r || !buf) return ZBHIP_EINVAL;
+  std::string id;
+  if (r->process_idx >= 0 && (size_t)r->process_idx < h->procs.size() && r->element_idx >= 0 &&
+      (size_t)r->element_idx < h->procs[r->process_idx].els.size())
+    id = h->procs[r->process_idx].id(r->element_idx);
+  // ProcessInstanceStateTransitionGuard.java:74-186, JobCommandPreconditionChecker.java
+  switch (r->reason) {
+    case ZBHIP_REASON_PGW_NOT_ALL_TAKEN:
+      return snprintf(buf, cap, "Expected to be able to activate parallel gateway '%s', but not all sequence flows have been taken.", id.c_str());
+    case ZBHIP_REASON_FS_NOT_FOUND:
+      return snprintf(buf, cap, "Expected flow scope instance with key '%lld' to be present in state but not found.", (long long)r->scope_key);
+    case ZBHIP_REASON_FS_STATE:
+      return snprintf(buf, cap, "Expected flow scope instance to be in state 'ELEMENT_ACTIVATED' but was '%s'.", state_name(r->reason_arg));
+    case ZBHIP_REASON_EI_NOT_FOUND:
+      return snprintf(buf, cap, "Expected element instance with key '%lld' to be present in state but not found.", (long long)r->key);
+    case ZBHIP_REASON_EI_STATE:
+      return snprintf(buf, cap, "Expected element instance to be in state 'ELEMENT_ACTIVATED' or one of '[ELEMENT_COMPLETING]' but was '%s'.", state_name(r->reason_arg));
+    case ZBHIP_REASON_JOB_NOT_FOUND:
+      return snprintf(buf, cap, "Expected to complete job with key '%lld', but no such job was found", (long long)r->key);
+    default:
+      if (cap) buf[0] = 0;
+      return 0;
+  }
+}
+
+int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal) {
+  if (!h || !instance || !ordinal) return ZBHIP_EINVAL;
+  const int64_t v = key - ((int64_t)h->cfg.partition_id << 51);
+  auto it = std::upper_bound(h->batches.begin(), h->batches.end(), v,
+                             [](int64_t x, const BatchRef& b) { return x < b.base; });
+  if (it == h->batches.begin()) return ZBHIP_EINVAL;
+  --it;
+  if (v >= it->base + it->nkeys) return ZBHIP_EINVAL;
+  *instance = it->inst;
+  *ordinal = (uint16_t)(it->first_ord + (v - it->base));
+  return ZBHIP_OK;
+}
+
+int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_out) {
+  if (!h || !n_out) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (!h->results) return h->stats.fallback ? ZBHIP_ESTATE : ZBHIP_OK;
+  size_t k = 0;
+  for (size_t c = 0; c < h->n_cmds; ++c)
+    if (((h->h_hdr[c].y >> 16) & 0xFF) != ST_OK) {
+      if (k < cap && instances) instances[k] = h->h_cmds[c].instance;
+      ++k;
+    }
+  *n_out = k;
+  return ZBHIP_OK;
+}
+
+// Canonical CF rows (same text format as the oracle's state dump).
+int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
+  if (!h || !sink) return ZBHIP_EINVAL;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  const size_t N = h->st.n;
+  std::vector<uint4> hdr(N);
+  std::vector<uint2> slots(N * kSlots), vm(N * kVars);
+  std::vector<long long> vv(N * kVars);
+  std::vector<uint32_t> join(N * kJoinWords);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(hdr.data(), h->st.hdr, N * sizeof(uint4), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(slots.data(), h->st.slots, N * kSlots * sizeof(uint2), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(vm.data(), h->st.var_meta, N * kVars * sizeof(uint2), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(vv.data(), h->st.var_val, N * kVars * sizeof(long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(join.data(), h->st.join, N * kJoinWords * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  char buf[768];
+  snprintf(buf, sizeof buf, "KEY|latestKey|%lld", (long long)(((int64_t)h->cfg.partition_id << 51) + h->key_counter));
+  sink(ctx, buf);
+  for (size_t i = 0; i < N; ++i) {
+    const uint4 hd = hdr[i];
+    const uint32_t proc = hd.x & 0xFFFF;
+    if (proc == NONE || !((hd.y >> 24) & 1)) continue;
+    const Proc& P = h->procs[proc];
+    const uint32_t inst = (uint32_t)i;
+    const long long pik = h->key_of(inst, 0);
+    const uint32_t nslots = (hd.y >> 8) & 0xFF, nvars = (hd.y >> 16) & 0xFF;
+    snprintf(buf, sizeof buf,
+             "ELEMENT_INSTANCE_KEY|%lld|parentKey=-1,childCount=%u,childActivatedCount=0,childCompletedCount=0,"
+             "childTerminatedCount=0,jobKey=0,multiInstanceLoopCounter=0,interruptingElementId=,"
+             "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=-1,"
+             "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%u",
+             pik, hd.z & 0xFFFF, hd.y & 0xFF, P.id(0).c_str(), ZBHIP_EL_PROCESS, ZBHIP_EV_UNSPECIFIED, pik,
+             (long long)P.def_key, hd.z >> 16);
+    sink(ctx, buf);
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|-1|%lld", pik);
+    sink(ctx, buf);
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|-1", pik);
+    sink(ctx, buf);
+    snprintf(buf, sizeof buf, "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY|%lld|%lld", (long long)P.def_key, pik);
+    sink(ctx, buf);
+    for (uint32_t s = 0; s < nslots; ++s) {
+      const uint2 e = slots[(size_t)s * N + i];
+      const uint32_t elem = e.x & 0xFFFF;
+      const long long k = h->key_of(inst, e.x >> 16);
+      const uint32_t job = e.y & 0xFFFF, state = (e.y >> 16) & 0xFF;
+      const bool job_row = (e.y >> 24) & 1;
+      const long long jk = job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
+      const zbhip_element& E = P.els[elem];
+      snprintf(buf, sizeof buf,
+               "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=0,childActivatedCount=0,childCompletedCount=0,"
+               "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=0,interruptingElementId=,"
+               "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
+               "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=0",
+               k, pik, jk, state, P.id(elem).c_str(), E.element_type, E.event_type, pik, pik, (long long)P.def_key);
+      sink(ctx, buf);
+      snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", pik, k);
+      sink(ctx, buf);
+      snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, pik);
+      sink(ctx, buf);
+      if (E.element_type == ZBHIP_EL_SERVICE_TASK) {
+        snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", k);
+        sink(ctx, buf);
+      }
+      if (job_row) {
+        const char* type = P.strings[E.job_type].c_str();
+        snprintf(buf, sizeof buf,
+                 "JOBS|%lld|type=%s,retries=%u,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
+                 "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>",
+                 jk, type, E.job_retries, P.id(elem).c_str(), k, pik, P.strings[P.bpmn_id].c_str(), (long long)P.def_key,
+                 P.version);
+        sink(ctx, buf);
+        snprintf(buf, sizeof buf, "JOB_STATES|%lld|ACTIVATABLE", jk);
+        sink(ctx, buf);
+        snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|<default>|%lld", type, jk);
+        sink(ctx, buf);
+      }
+    }
+    for (uint32_t v = 0; v < nvars; ++v) {
+      const uint2 m = vm[(size_t)v * N + i];
+      const uint32_t scope = m.x >> 16;
+      snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%lld", h->key_of(inst, scope),
+               h->names[m.x & 0xFFFF].c_str(), h->key_of(inst, m.y & 0xFFFF), (m.y >> 16) & 0xFF, vv[(size_t)v * N + i]);
+      sink(ctx, buf);
+    }
+    if (P.n_join_slots) {
+      for (uint32_t f = 0; f < P.els.size(); ++f) {
+        const zbhip_element& E = P.els[f];
+        if (E.element_type != ZBHIP_EL_SEQUENCE_FLOW || E.join_slot == ZBHIP_NONE16) continue;
+        const uint32_t s = E.join_slot;
+        const uint32_t cnt = (join[(size_t)(s >> 2) * N + i] >> ((s & 3) * 8)) & 0xFF;
+        if (!cnt) continue;
+        snprintf(buf, sizeof buf, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS|%lld|%s|%s|%u", pik, P.id(E.flow_target).c_str(),
+                 P.id(f).c_str(), cnt);
+        sink(ctx, buf);
+      }
+    }
+  }
+  return ZBHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// Internal layouts shared by the gfx950 kernels (engine.hip) and the host runtime.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/zbhip.h"
+
+namespace zb {
+
+constexpr int kBlock = 256;        // threads per workgroup (4 wave64)
+constexpr int kTable = 12;         // live element-instance entries per lane during a batch (LDS)
+constexpr int kQueue = 16;         // pending follow-up commands per lane (LDS ring)
+constexpr int kSlots = 8;          // persistent element-instance slots per process instance (HBM)
+constexpr int kVars = 4;           // variables per process instance (HBM)
+constexpr int kJoinWords = 4;      // 16 x u8 taken-sequence-flow counters per instance (HBM)
+constexpr int kMaxJoinSlots = 4 * kJoinWords;
+constexpr uint32_t kMaxProgWords = 6144;  // program arena staged in LDS (24 KiB; total LDS <= 64 KiB)
+constexpr int kMaxElements = 4095;        // 12-bit element index in queue entries
+
+constexpr uint16_t NONE = 0xFFFF;
+
+// ElementInstance.jobKey encodings in a slot (ElementInstance.java:23-54: default 0,
+// JobCreatedApplier sets the job key, JobCompletedApplier sets -1)
+constexpr uint16_t JOB_ZERO = 0xFFFF;
+constexpr uint16_t JOB_MINUS1 = 0xFFFE;
+
+// Compact device record: 8 bytes
+//   x = key_ord | aux_ord << 16        (0xFFFF = -1)
+//   y = elem | code << 16 | flags << 24
+// code: PI events/commands = ProcessInstanceIntent value (1..10), others below,
+//       | kRejectBit for COMMAND_REJECTION.  flags: rejection reason | arg << 4.
+enum : uint8_t {
+  C_JOB_CREATED = 16,
+  C_JOB_COMPLETED = 17,
+  C_JOB_COMPLETE = 18,
+  C_VAR_CREATED = 20,
+  C_VAR_UPDATED = 21,
+  C_PE_TRIGGERING = 24,
+  C_PIC_CREATED = 28,
+  kRejectBit = 0x40,
+};
+
+// per-command header written by k_step: x = nrec | nkeys << 16, y = first_ord | status << 16 | fb << 24
+enum : uint8_t { ST_OK = 0, ST_FALLBACK = 1 };
+enum : uint8_t {
+  FB_NONE = 0,
+  FB_QUEUE = 1,        // more pending commands than the LDS ring holds
+  FB_TABLE = 2,        // more live element instances than the LDS table holds
+  FB_RECORDS = 3,      // more records than the per-command record slot holds
+  FB_KEYS = 4,         // more than 65 520 keys in one instance
+  FB_BATCH_LIMIT = 5,  // follow-up command beyond maxCommandsInBatch (written to the log by the PSM)
+  FB_FEEL = 6,         // condition result not a boolean (incident) / value outside the subset
+  FB_VARS = 7,         // more variables than the per-instance slots
+  FB_SLOT_IN_USE = 8,  // CREATE into an occupied instance slot
+  FB_NO_CONDITION = 9, // no flow chosen and no default flow (incident CONDITION_ERROR)
+  FB_UNSUPPORTED = 10, // element/transition outside the subset
+  FB_DOC = 11,         // multi-entry variable document (agrona iteration order unpinned)
+  FB_JOIN = 12,        // taken-sequence-flow counter overflow
+  FB_SLOTS = 13,       // more persistent element instances than kSlots
+  FB_BAD_PROCESS = 14, // unknown process / no none start event
+};
+
+// Program arena (u32 words), LDS-staged by every workgroup:
+//   [0] n_procs, [1 .. n_procs] word offset of each process block (multiple of 4)
+// process block p:
+//   p[0] = n_elements | none_start << 16
+//   p[1] = n_join_slots | n_conditions << 16
+//   p[2] = out_off, p[3] = cond_off, p[4] = code_off (words, relative to p), p[5..7] = 0
+//   p[8 + 4e .. ] element e: w0 = type | event << 8 | in_count << 16
+//                            w1 = out_begin | out_count << 16
+//                            w2 = flow: target | condition << 16; xgw: default_flow; task: job_type | retries << 16
+//                            w3 = join_slot | id << 16
+//   p[out_off]  u16 outgoing flows (two per word)
+//   p[cond_off] u32 first instruction of each condition
+//   p[code_off] instructions: op, arg, literal_lo, literal_hi
+struct DevState {
+  uint4* hdr;        // [n] x = proc | next_ord << 16; y = pi_state | nslots << 8 | nvars << 16 | pi_live << 24
+                     //     z = pi_child | pi_asf << 16; w = 0
+  uint2* slots;      // [kSlots][n] x = elem | key << 16; y = job | state << 16 | flags << 24 (bit0: job row exists)
+  uint2* var_meta;   // [kVars][n]  x = name | scope << 16; y = key | type << 16
+  long long* var_val;// [kVars][n]
+  uint32_t* join;    // [kJoinWords][n]
+  uint32_t n;
+};
+
+struct StepParams {
+  const uint4* cmds;          // zbhip_command[n_cmds] (window, log order)
+  const uint32_t* order;      // command indices processed by this launch (round); null = identity
+  uint32_t n_launch;          // lanes in this launch
+  const zbhip_doc_entry* docs;
+  uint32_t n_docs;
+  const uint32_t* prog;
+  uint32_t prog_words;
+  uint32_t n_procs;
+  DevState st;
+  uint2* rec;                 // [n_cmds][rec_cap] record slots, indexed by command index
+  uint32_t rec_cap;
+  uint2* cmd_hdr;             // [n_cmds]
+  unsigned long long* counters;  // [0] records [1] transitions [2] completed [3] keys [4] fallback [5] commands
+  int32_t max_cmds_in_batch;
+};
+
+}  // namespace zb

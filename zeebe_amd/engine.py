@@ -1,0 +1,317 @@
+"""Host-side mirror of the reference's processing interface for the BPMN element-lifecycle
+hot path, driving libzbhip.so (gfx950).
+
+* :class:`Partition` -- one partition handle (the C ABI in include/zbhip.h).
+* :class:`GpuRecordProcessor` -- the stream-platform ``RecordProcessor`` contract
+  (stream-platform/.../stream/api/RecordProcessor.java:17-108): ``accepts(value_type)``,
+  ``process(window)`` returning the follow-up records grouped per source command.
+* :class:`EngineRule` -- the test-client surface of the reference's ``EngineRule``
+  (engine/src/test/java/io/camunda/zeebe/engine/util/EngineRule.java) so parity tests read
+  like the reference's own tests: ``deployment().with_xml_resource(xml).deploy()``,
+  ``process_instance().of_bpmn_process_id(id).with_variable(k, v).create()``,
+  ``job().of_instance(pi).with_type(t).complete()``, and RecordingExporter-style queries.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .native import STATE_SINK, ZbhipError, check, load
+
+
+class ProcessDefinition:
+    def __init__(self, idx, bpmn_process_id, element_ids, element_types, job_types):
+        self.idx = idx
+        self.bpmn_process_id = bpmn_process_id
+        self.element_ids = element_ids
+        self.element_types = element_types
+        self.job_types = job_types
+
+
+class _Csr(C.Structure):  # prefix of zbhip_process_csr needed to read the element table
+    _fields_ = [("n_elements", C.c_uint32), ("elements", C.c_void_p), ("n_out", C.c_uint32),
+                ("out_flow", C.c_void_p), ("n_conditions", C.c_uint32), ("cond_begin", C.c_void_p),
+                ("n_code", C.c_uint32), ("code", C.c_void_p), ("n_strings", C.c_uint32),
+                ("strings", C.POINTER(C.c_char_p))]
+
+
+ELEMENT_DTYPE = np.dtype([("element_type", "u1"), ("event_type", "u1"), ("out_begin", "<u2"), ("out_count", "<u2"),
+                          ("in_count", "<u2"), ("flow_source", "<u2"), ("flow_target", "<u2"), ("condition", "<u2"),
+                          ("default_flow", "<u2"), ("job_type", "<u2"), ("job_retries", "<u2"), ("join_slot", "<u2"),
+                          ("id", "<u2")])
+
+
+class Partition:
+    """One Zeebe partition executed on one MI355X (a libzbhip handle)."""
+
+    def __init__(self, partition_id=1, partition_count=1, device=0, max_instances=1 << 16, max_commands=1 << 16,
+                 max_records_per_batch=64, max_doc_entries=0, max_commands_in_batch=100, initial_key=0, stream=None):
+        self.L = load()
+        cfg = abi.Config(partition_id=partition_id, partition_count=partition_count, device=device,
+                         max_commands_in_batch=max_commands_in_batch, max_instances=max_instances,
+                         max_commands=max_commands, max_records_per_batch=max_records_per_batch,
+                         max_doc_entries=max_doc_entries, initial_key=initial_key, stream=stream)
+        h = C.c_void_p()
+        check(self.L.zbhip_open(C.byref(cfg), C.byref(h)), "zbhip_open")
+        self.h = h
+        self.partition_id = partition_id
+        self.processes = []
+        self.max_commands = max_commands
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.zbhip_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+    # ---- deployment (host compiler -> CSR -> LDS program arena) ----
+    def deploy(self, xml, process_definition_key=2251799813685249, version=1):
+        if isinstance(xml, str):
+            xml = xml.encode()
+        csr = C.c_void_p()
+        err = C.create_string_buffer(512)
+        check(self.L.zbhip_compile_bpmn(xml, len(xml), process_definition_key, version, C.byref(csr), err, 512),
+              err.value.decode())
+        try:
+            c = C.cast(csr, C.POINTER(_Csr)).contents
+            els = np.frombuffer(C.string_at(c.elements, c.n_elements * ELEMENT_DTYPE.itemsize), dtype=ELEMENT_DTYPE)
+            strings = [c.strings[i].decode() for i in range(c.n_strings)]
+            idx = C.c_uint32()
+            check(self.L.zbhip_deploy(self.h, csr, C.byref(idx)), "zbhip_deploy")
+        finally:
+            self.L.zbhip_free_csr(csr)
+        pd = ProcessDefinition(idx.value, strings[els[0]["id"]], [strings[i] for i in els["id"]],
+                               [abi.ELEMENT_TYPES[t] for t in els["element_type"]],
+                               [strings[j] if j != 0xFFFF else None for j in els["job_type"]])
+        self.processes.append(pd)
+        return idx.value
+
+    def intern(self, name):
+        return check(self.L.zbhip_intern(self.h, name.encode()))
+
+    def name(self, nid):
+        return self.L.zbhip_name(self.h, nid).decode()
+
+    def element_id(self, proc, elem):
+        return self.processes[proc].element_ids[elem]
+
+    # ---- commands ----
+    def submit(self, cmds, docs=None):
+        cmds = np.ascontiguousarray(cmds, dtype=abi.COMMAND_DTYPE)
+        docs = np.ascontiguousarray(docs if docs is not None else abi.make_docs(0), dtype=abi.DOC_DTYPE)
+        check(self.L.zbhip_submit(self.h, cmds.ctypes.data, len(cmds), docs.ctypes.data, len(docs)), "zbhip_submit")
+
+    def submit_device(self, cmd_ptr, n, doc_ptr=0, n_docs=0):
+        """Commands already resident in HBM (e.g. a torch uint8 tensor's data_ptr())."""
+        check(self.L.zbhip_submit_device(self.h, cmd_ptr, n, doc_ptr or None, n_docs), "zbhip_submit_device")
+
+    def run(self, flags=0):
+        return check(self.L.zbhip_run(self.h, flags), "zbhip_run")
+
+    def drain(self):
+        n = self.L.zbhip_pending_records(self.h)
+        out = np.zeros(max(n, 0), dtype=abi.RECORD_DTYPE)
+        got = C.c_size_t()
+        check(self.L.zbhip_drain(self.h, out.ctypes.data if n else None, n, C.byref(got)), "zbhip_drain")
+        return out[: got.value]
+
+    def reason(self, rec):
+        r = abi.Record()
+        for f, _ in abi.Record._fields_:
+            setattr(r, f, int(rec[f]))
+        buf = C.create_string_buffer(512)
+        self.L.zbhip_rejection_reason(self.h, C.byref(r), buf, 512)
+        return buf.value.decode()
+
+    def stats(self):
+        s = abi.Stats()
+        check(self.L.zbhip_get_stats(self.h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in abi.Stats._fields_}
+
+    def state(self):
+        rows = []
+        cb = STATE_SINK(lambda ctx, row: rows.append(row.decode()))
+        check(self.L.zbhip_export_state(self.h, cb, None), "zbhip_export_state")
+        return sorted(rows)
+
+    def fallback(self):
+        n = C.c_size_t()
+        check(self.L.zbhip_fallback(self.h, None, 0, C.byref(n)))
+        buf = (C.c_uint32 * max(n.value, 1))()
+        check(self.L.zbhip_fallback(self.h, buf, n.value, C.byref(n)))
+        return list(buf[: n.value])
+
+    def resolve_key(self, key):
+        inst, ordv = C.c_uint32(), C.c_uint16()
+        check(self.L.zbhip_resolve_key(self.h, key, C.byref(inst), C.byref(ordv)), "unknown key %d" % key)
+        return inst.value, ordv.value
+
+
+class GpuRecordProcessor:
+    """The RecordProcessor contract for a window of hot-path commands (see module doc)."""
+
+    ACCEPTED = (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB)
+
+    def __init__(self, partition):
+        self.partition = partition
+
+    def accepts(self, value_type):
+        return value_type in self.ACCEPTED
+
+    def process(self, cmds, docs=None):
+        """Processes the window to quiescence; returns {source_index: [records]} in log order."""
+        self.partition.submit(cmds, docs)
+        self.partition.run()
+        recs = self.partition.drain()
+        out = {}
+        for r in recs:
+            out.setdefault(int(r["source_index"]), []).append(r)
+        return out
+
+
+# ---------------------------------------------------------------------------------------------
+# EngineRule-style client
+# ---------------------------------------------------------------------------------------------
+class EngineRule:
+    """Single-partition test engine on the GPU (EngineRule.singlePartition)."""
+
+    def __init__(self, partition=None, **kw):
+        self.partition = partition or Partition(**kw)
+        self.records = []       # RecordingExporter: every drained record, in log order
+        self.reasons = {}
+        self._next_instance = 0
+        self._pi_instance = {}  # process instance key -> instance slot
+        self._by_id = {}
+
+    @classmethod
+    def single_partition(cls, **kw):
+        return cls(**kw)
+
+    # deployment().withXmlResource(xml).deploy()
+    def deployment(self):
+        rule = self
+
+        class _D:
+            def __init__(self):
+                self.xml = None
+
+            def with_xml_resource(self, xml):
+                self.xml = xml
+                return self
+
+            def deploy(self):
+                idx = rule.partition.deploy(self.xml)
+                rule._by_id[rule.partition.processes[idx].bpmn_process_id] = idx
+                return idx
+
+        return _D()
+
+    def _execute(self, cmds, docs=None):
+        self.partition.submit(cmds, docs)
+        self.partition.run()
+        recs = self.partition.drain()
+        base = len(self.records)
+        for i, r in enumerate(recs):
+            if r["record_type"] == abi.RT_REJECTION:
+                self.reasons[base + i] = self.partition.reason(r)
+        self.records.extend(recs)
+        return recs
+
+    def process_instance(self):
+        rule = self
+
+        class _P:
+            def __init__(self):
+                self.proc = None
+                self.vars = []
+
+            def of_bpmn_process_id(self, pid):
+                self.proc = rule._by_id[pid]
+                return self
+
+            def with_variable(self, name, value):
+                self.vars.append((name, value))
+                return self
+
+            def create(self):
+                inst = rule._next_instance
+                rule._next_instance += 1
+                cmds = abi.make_commands(1)
+                cmds["instance"] = inst
+                cmds["kind"] = abi.CMD_CREATE
+                cmds["ref"] = self.proc
+                docs = abi.make_docs(len(self.vars))
+                for j, (n, v) in enumerate(self.vars):
+                    docs[j]["name_id"] = rule.partition.intern(n)
+                    if isinstance(v, bool):
+                        docs[j]["type"], docs[j]["value"] = abi.DOC_BOOL, int(v)
+                    elif isinstance(v, int):
+                        docs[j]["type"], docs[j]["value"] = abi.DOC_INT, v
+                    else:
+                        docs[j]["type"], docs[j]["value"] = abi.DOC_DEC, int(round(v * 10 ** abi.DEC_SCALE))
+                cmds["doc_count"] = len(self.vars)
+                recs = rule._execute(cmds, docs)
+                created = [r for r in recs if r["value_type"] == abi.VT_PROCESS_INSTANCE_CREATION]
+                pi = int(created[0]["process_instance_key"])
+                rule._pi_instance[pi] = inst
+                return pi
+
+        return _P()
+
+    def job(self):
+        rule = self
+
+        class _J:
+            def __init__(self):
+                self.pi = None
+                self.type = None
+                self.key = None
+
+            def of_instance(self, pi):
+                self.pi = pi
+                return self
+
+            def with_type(self, t):
+                self.type = t
+                return self
+
+            def with_key(self, k):
+                self.key = k
+                return self
+
+            def complete(self):
+                key = self.key
+                if key is None:
+                    created = [r for r in rule.records if r["value_type"] == abi.VT_JOB and r["intent"] == 0
+                               and int(r["process_instance_key"]) == self.pi and
+                               rule.partition.processes[int(r["process_idx"])].job_types[int(r["element_idx"])]
+                               == self.type]
+                    key = int(created[-1]["key"])
+                inst, ordv = rule.partition.resolve_key(key)
+                cmds = abi.make_commands(1)
+                cmds["instance"] = inst
+                cmds["kind"] = abi.CMD_JOB_COMPLETE
+                cmds["ref"] = ordv
+                return rule._execute(cmds)
+
+        return _J()
+
+    # RecordingExporter.processInstanceRecords() as (elementId, intent-name) pairs
+    def process_instance_records(self, only_events=False):
+        out = []
+        for r in self.records:
+            if r["value_type"] != abi.VT_PROCESS_INSTANCE:
+                continue
+            if only_events and r["record_type"] != abi.RT_EVENT:
+                continue
+            out.append((self.partition.element_id(int(r["process_idx"]), int(r["element_idx"])),
+                        abi.PI_INTENTS[int(r["intent"])]))
+        return out
+
+
+__all__ = ["Partition", "GpuRecordProcessor", "EngineRule", "ZbhipError"]

@@ -1,0 +1,75 @@
+"""Loads the in-tree libzbhip.so (gfx950) and declares its C ABI.
+
+There is no fallback: if the library is missing or cannot be loaded, every entry
+point raises.  The CPU oracle is test infrastructure and is never used here.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzbhip.so")
+
+ERRORS = {-1: "ZBHIP_EINVAL", -2: "ZBHIP_ENOMEM", -3: "ZBHIP_EDEVICE", -4: "ZBHIP_EPARSE",
+          -5: "ZBHIP_EUNSUPP", -6: "ZBHIP_ESTATE", -7: "ZBHIP_ENODEV"}
+
+# every symbol include/zbhip.h declares (tests/test_abi.py checks the export table)
+SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", "zbhip_deploy", "zbhip_intern",
+           "zbhip_string", "zbhip_name", "zbhip_submit", "zbhip_submit_device", "zbhip_run", "zbhip_drain",
+           "zbhip_pending_records", "zbhip_get_stats", "zbhip_export_state", "zbhip_fallback",
+           "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info"]
+
+
+class ZbhipError(RuntimeError):
+    def __init__(self, code, what=""):
+        super().__init__("%s (%d)%s" % (ERRORS.get(code, "?"), code, (": " + what) if what else ""))
+        self.code = code
+
+
+STATE_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p)
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ZbhipError(-7, "libzbhip.so not built (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i64, u32 = C.c_void_p, C.c_size_t, C.c_int64, C.c_uint32
+    L.zbhip_compile_bpmn.argtypes = [C.c_char_p, sz, i64, C.c_int32, C.POINTER(vp), C.c_char_p, sz]
+    L.zbhip_free_csr.argtypes = [vp]
+    L.zbhip_free_csr.restype = None
+    L.zbhip_open.argtypes = [C.POINTER(abi.Config), C.POINTER(vp)]
+    L.zbhip_close.argtypes = [vp]
+    L.zbhip_close.restype = None
+    L.zbhip_deploy.argtypes = [vp, vp, C.POINTER(u32)]
+    L.zbhip_intern.argtypes = [vp, C.c_char_p]
+    L.zbhip_string.argtypes = [vp, u32, u32]
+    L.zbhip_string.restype = C.c_char_p
+    L.zbhip_name.argtypes = [vp, u32]
+    L.zbhip_name.restype = C.c_char_p
+    L.zbhip_submit.argtypes = [vp, vp, sz, vp, sz]
+    L.zbhip_submit_device.argtypes = [vp, vp, sz, vp, sz]
+    L.zbhip_run.argtypes = [vp, u32]
+    L.zbhip_drain.argtypes = [vp, vp, sz, C.POINTER(sz)]
+    L.zbhip_pending_records.argtypes = [vp]
+    L.zbhip_pending_records.restype = i64
+    L.zbhip_get_stats.argtypes = [vp, C.POINTER(abi.Stats)]
+    L.zbhip_export_state.argtypes = [vp, STATE_SINK, vp]
+    L.zbhip_fallback.argtypes = [vp, C.POINTER(u32), sz, C.POINTER(sz)]
+    L.zbhip_resolve_key.argtypes = [vp, i64, C.POINTER(u32), C.POINTER(C.c_uint16)]
+    L.zbhip_rejection_reason.argtypes = [vp, C.POINTER(abi.Record), C.c_char_p, sz]
+    L.zbhip_build_info.argtypes = []
+    L.zbhip_build_info.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc < 0:
+        raise ZbhipError(rc, what)
+    return rc
