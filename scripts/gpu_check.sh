@@ -26,8 +26,8 @@ fi
 if [[ $STEPS == *prof* ]]; then
   run prof
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline \
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-} \
     > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
-  find gpurun_out/prof -name "*kernel_stats.csv" | head -3
+  find gpurun_out/prof -name "*stats.csv" | head -5; cat $(find gpurun_out/prof -name "*kernel_stats.csv" | head -1) | cut -c1-220
 fi
 echo "=== done"

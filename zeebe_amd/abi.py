@@ -29,6 +29,7 @@ PI_INTENTS = {
 }
 PI_INTENT_IDS = {v: k for k, v in PI_INTENTS.items()}
 JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED"}
+JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED = 0, 1, 2
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
 PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
 PIC_INTENTS = {0: "CREATE", 1: "CREATED"}

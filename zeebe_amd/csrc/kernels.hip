@@ -62,11 +62,47 @@ struct Lane {
   uint32_t doc_count;
   const zbhip_doc_entry* docs;
   int nvars;
-  uint2 vm[kVars];
-  long long vv[kVars];
-  uint32_t jw[kJoinWords];
+  // variables and join counters are explicit scalars (not arrays): an array member indexed at
+  // run time would force the whole context into scratch memory
+  uint32_t vx0, vx1, vx2, vx3;  // name | scope << 16
+  uint32_t vy0, vy1, vy2, vy3;  // key | type << 16
+  long long vv0, vv1, vv2, vv3;
+  uint32_t jw0, jw1, jw2, jw3;
   bool has_join;
 };
+static_assert(kVars == 4 && kJoinWords == 4, "scalarised tables");
+
+__device__ __forceinline__ uint32_t var_x(const Lane& L, int i) {
+  return i == 0 ? L.vx0 : i == 1 ? L.vx1 : i == 2 ? L.vx2 : L.vx3;
+}
+__device__ __forceinline__ uint32_t var_y(const Lane& L, int i) {
+  return i == 0 ? L.vy0 : i == 1 ? L.vy1 : i == 2 ? L.vy2 : L.vy3;
+}
+__device__ __forceinline__ long long var_v(const Lane& L, int i) {
+  const long long v0 = L.vv0, v1 = L.vv1, v2 = L.vv2, v3 = L.vv3;
+  long long r = v3;
+  r = i == 2 ? v2 : r;
+  r = i == 1 ? v1 : r;
+  r = i == 0 ? v0 : r;
+  return r;
+}
+// branch-free updates: a store per field keeps every field a plain SSA value (an if/else chain
+// is merged by the optimiser into one store through a selected pointer -> scratch)
+__device__ __forceinline__ void var_put(Lane& L, int i, uint32_t x, uint32_t y, long long v) {
+  L.vx0 = i == 0 ? x : L.vx0; L.vy0 = i == 0 ? y : L.vy0; L.vv0 = i == 0 ? v : L.vv0;
+  L.vx1 = i == 1 ? x : L.vx1; L.vy1 = i == 1 ? y : L.vy1; L.vv1 = i == 1 ? v : L.vv1;
+  L.vx2 = i == 2 ? x : L.vx2; L.vy2 = i == 2 ? y : L.vy2; L.vv2 = i == 2 ? v : L.vv2;
+  L.vx3 = i == 3 ? x : L.vx3; L.vy3 = i == 3 ? y : L.vy3; L.vv3 = i == 3 ? v : L.vv3;
+}
+__device__ __forceinline__ uint32_t jw_get(const Lane& L, int i) {
+  return i == 0 ? L.jw0 : i == 1 ? L.jw1 : i == 2 ? L.jw2 : L.jw3;
+}
+__device__ __forceinline__ void jw_put(Lane& L, int i, uint32_t w) {
+  L.jw0 = i == 0 ? w : L.jw0;
+  L.jw1 = i == 1 ? w : L.jw1;
+  L.jw2 = i == 2 ? w : L.jw2;
+  L.jw3 = i == 3 ? w : L.jw3;
+}
 
 __device__ __forceinline__ void set_fail(Lane& L, uint32_t why) {
   if (!L.fail) L.fail = why;
@@ -140,55 +176,47 @@ __device__ __forceinline__ void tbl_set_state(Lane& L, int t, uint32_t state) {
 
 // ---- variables (registers) ------------------------------------------------------------------
 __device__ __forceinline__ int var_find(const Lane& L, uint32_t scope, uint32_t name) {
+  const uint32_t want = name | (scope << 16);
   int r = -1;
-#pragma unroll
-  for (int v = 0; v < kVars; ++v)
-    if (v < L.nvars && L.vm[v].x == (name | (scope << 16))) r = v;
+  if (L.nvars > 3 && L.vx3 == want) r = 3;
+  if (L.nvars > 2 && L.vx2 == want) r = 2;
+  if (L.nvars > 1 && L.vx1 == want) r = 1;
+  if (L.nvars > 0 && L.vx0 == want) r = 0;
   return r;
 }
 
 // VariableBehavior.setLocalVariable (VariableBehavior.java:191-200) + VariableApplier
-__device__ void set_local_variable(Lane& L, uint32_t scope, const zbhip_doc_entry& d) {
+__device__ __forceinline__ void set_local_variable(Lane& L, uint32_t scope, const zbhip_doc_entry& d) {
   int v = var_find(L, scope, d.name_id);
   if (v < 0) {
     if (L.nvars >= kVars) { set_fail(L, FB_VARS); return; }
     uint32_t key = new_key(L);
     emit(L, C_VAR_CREATED, key, scope, d.name_id);
-    int n = L.nvars++;
-#pragma unroll
-    for (int i = 0; i < kVars; ++i)
-      if (i == n) {
-        L.vm[i] = make_uint2(d.name_id | (scope << 16), key | ((uint32_t)d.type << 16));
-        L.vv[i] = d.value;
-      }
+    var_put(L, L.nvars++, d.name_id | (scope << 16), key | ((uint32_t)d.type << 16), d.value);
   } else {
-#pragma unroll
-    for (int i = 0; i < kVars; ++i)
-      if (i == v && !(((L.vm[i].y >> 16) & 0xFF) == d.type && L.vv[i] == d.value)) {
-        emit(L, C_VAR_UPDATED, L.vm[i].y & 0xFFFF, scope, d.name_id);
-        L.vm[i].y = (L.vm[i].y & 0xFFFF) | ((uint32_t)d.type << 16);
-        L.vv[i] = d.value;
-      }
+    const uint32_t y = var_y(L, v);
+    if (!(((y >> 16) & 0xFF) == d.type && var_v(L, v) == d.value)) {
+      emit(L, C_VAR_UPDATED, y & 0xFFFF, scope, d.name_id);
+      var_put(L, v, var_x(L, v), (y & 0xFFFF) | ((uint32_t)d.type << 16), d.value);
+    }
   }
 }
 
 // VariableBehavior.mergeDocument (VariableBehavior.java:105-150) from an element scope whose
 // parent is the process instance (the only nesting in the supported subset).
-__device__ void merge_document_from(Lane& L, uint32_t scope_key, uint32_t begin, uint32_t count) {
+__device__ __forceinline__ void merge_document_from(Lane& L, uint32_t scope_key, uint32_t begin, uint32_t count) {
   if (count == 0) return;
   if (count > 1) { set_fail(L, FB_DOC); return; }
   const zbhip_doc_entry d = L.docs[begin];
   if (scope_key != 0) {
     int v = var_find(L, scope_key, d.name_id);
     if (v >= 0) {
-#pragma unroll
-      for (int i = 0; i < kVars; ++i)
-        if (i == v && !(((L.vm[i].y >> 16) & 0xFF) == d.type && L.vv[i] == d.value)) {
-          emit(L, C_VAR_UPDATED, L.vm[i].y & 0xFFFF, scope_key, d.name_id);
-          L.vm[i].y = (L.vm[i].y & 0xFFFF) | ((uint32_t)d.type << 16);
-          L.vv[i] = d.value;
-          return;  // consumed at this scope
-        }
+      const uint32_t y = var_y(L, v);
+      if (!(((y >> 16) & 0xFF) == d.type && var_v(L, v) == d.value)) {
+        emit(L, C_VAR_UPDATED, y & 0xFFFF, scope_key, d.name_id);
+        var_put(L, v, var_x(L, v), (y & 0xFFFF) | ((uint32_t)d.type << 16), d.value);
+        return;  // consumed at this scope
+      }
     }
   }
   set_local_variable(L, 0, d);
@@ -196,86 +224,71 @@ __device__ void merge_document_from(Lane& L, uint32_t scope_key, uint32_t begin,
 
 // ---- join counters (registers, 16 x u8) ----------------------------------------------------
 __device__ __forceinline__ uint32_t join_get(const Lane& L, uint32_t s) {
-  uint32_t w = 0;
-#pragma unroll
-  for (int i = 0; i < kJoinWords; ++i)
-    if ((int)(s >> 2) == i) w = L.jw[i];
-  return (w >> ((s & 3) * 8)) & 0xFF;
+  return (jw_get(L, (int)(s >> 2)) >> ((s & 3) * 8)) & 0xFF;
 }
 __device__ __forceinline__ void join_set(Lane& L, uint32_t s, uint32_t v) {
-#pragma unroll
-  for (int i = 0; i < kJoinWords; ++i)
-    if ((int)(s >> 2) == i) {
-      uint32_t sh = (s & 3) * 8;
-      L.jw[i] = (L.jw[i] & ~(0xFFu << sh)) | ((v & 0xFF) << sh);
-    }
+  const uint32_t sh = (s & 3) * 8;
+  const int i = (int)(s >> 2);
+  jw_put(L, i, (jw_get(L, i) & ~(0xFFu << sh)) | ((v & 0xFF) << sh));
 }
 
 // ---- FEEL condition bytecode ------------------------------------------------------------------
 // Values: tag 0 NULL, 1 BOOL, 2 NUMBER (x 10^ZBHIP_DEC_SCALE).  Results that are not boolean
 // raise an incident in the reference (ExpressionProcessor.java:356-368) -> fallback.
-__device__ bool eval_condition(Lane& L, uint32_t cond, uint32_t scope_key, bool& out) {
+// The operand stack is four registers, top first (the compiler bounds the depth to 4).
+__device__ __forceinline__ bool load_var(const Lane& L, uint32_t name, uint32_t scope_key, uint32_t& t,
+                                         long long& x) {
+  // DbVariableState.getVariable: element scope first, then the process instance scope
+  int v = var_find(L, scope_key, name);
+  if (v < 0) v = var_find(L, 0, name);
+  t = 0;
+  x = 0;
+  if (v < 0) return true;  // missing -> null
+  const uint32_t ty = (var_y(L, v) >> 16) & 0xFF;
+  const long long raw = var_v(L, v);
+  if (ty == ZBHIP_DOC_NIL) return true;
+  if (ty == ZBHIP_DOC_BOOL) { t = 1; x = raw != 0; return true; }
+  if (ty == ZBHIP_DOC_INT) {
+    if (raw > 9223372036854LL || raw < -9223372036854LL) return false;
+    t = 2;
+    x = raw * 1000000LL;
+    return true;
+  }
+  if (ty == ZBHIP_DOC_DEC) { t = 2; x = raw; return true; }
+  return false;
+}
+
+__device__ __forceinline__ bool eval_condition(Lane& L, uint32_t cond, uint32_t scope_key, bool& out) {
   const uint32_t* pb = L.pb;
   uint32_t pc = pb[pb[3] + cond];
   const uint32_t* code = pb + pb[4];
-  uint8_t tag[8];
-  long long val[8];
+  uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   int sp = 0;
-  for (int guard = 0; guard < 64; ++guard) {
-    const uint32_t* in = code + 4 * pc++;
-    uint32_t op = in[0];
+  for (int guard = 0; guard < 32; ++guard) {
+    const uint4 in = *reinterpret_cast<const uint4*>(code + 4 * pc++);
+    const uint32_t op = in.x;
     if (op == ZBHIP_OP_END) break;
-    if (op == ZBHIP_OP_PUSH_VAR || op == ZBHIP_OP_PUSH_NUM || op == ZBHIP_OP_PUSH_BOOL || op == ZBHIP_OP_PUSH_NULL) {
-      if (sp >= 8) return false;
-      uint8_t t = 0;
+    if (op <= ZBHIP_OP_PUSH_NULL) {
+      uint32_t t = 0;
       long long x = 0;
-      if (op == ZBHIP_OP_PUSH_NUM) {
-        t = 2;
-        x = (long long)(((unsigned long long)in[3] << 32) | in[2]);
-      } else if (op == ZBHIP_OP_PUSH_BOOL) {
-        t = 1;
-        x = in[1] != 0;
-      } else if (op == ZBHIP_OP_PUSH_VAR) {
-        // DbVariableState.getVariable: element scope first, then the process instance scope
-        int v = var_find(L, scope_key, in[1]);
-        if (v < 0) v = var_find(L, 0, in[1]);
-        if (v >= 0) {
-          uint32_t ty = 0;
-          long long raw = 0;
-#pragma unroll
-          for (int i = 0; i < kVars; ++i)
-            if (i == v) { ty = (L.vm[i].y >> 16) & 0xFF; raw = L.vv[i]; }
-          if (ty == ZBHIP_DOC_NIL) {
-            t = 0;
-          } else if (ty == ZBHIP_DOC_BOOL) {
-            t = 1;
-            x = raw != 0;
-          } else if (ty == ZBHIP_DOC_INT) {
-            if (raw > 9223372036854LL || raw < -9223372036854LL) return false;
-            t = 2;
-            x = raw * 1000000LL;
-          } else if (ty == ZBHIP_DOC_DEC) {
-            t = 2;
-            x = raw;
-          } else {
-            return false;
-          }
-        }
-      }
-      tag[sp] = t;
-      val[sp] = x;
+      if (op == ZBHIP_OP_PUSH_NUM) { t = 2; x = (long long)(((unsigned long long)in.w << 32) | in.z); }
+      else if (op == ZBHIP_OP_PUSH_BOOL) { t = 1; x = in.y != 0; }
+      else if (op == ZBHIP_OP_PUSH_VAR) { if (!load_var(L, in.y, scope_key, t, x)) return false; }
+      if (sp >= 4) return false;
+      t3 = t2; a3 = a2; t2 = t1; a2 = a1; t1 = t0; a1 = a0; t0 = t; a0 = x;
       ++sp;
       continue;
     }
     if (op == ZBHIP_OP_NOT) {
-      if (sp < 1 || tag[sp - 1] != 1) return false;
-      val[sp - 1] = !val[sp - 1];
+      if (sp < 1 || t0 != 1) return false;
+      a0 = !a0;
       continue;
     }
     if (sp < 2) return false;
-    uint8_t ta = tag[sp - 2], tb = tag[sp - 1];
-    long long a = val[sp - 2], b = val[sp - 1];
-    --sp;
+    // binary: a = second, b = top
+    const uint32_t ta = t1, tb = t0;
+    const long long a = a1, b = a0;
     bool r;
     if (op == ZBHIP_OP_AND || op == ZBHIP_OP_OR) {
       if (ta != 1 || tb != 1) return false;
@@ -290,16 +303,17 @@ __device__ bool eval_condition(Lane& L, uint32_t cond, uint32_t scope_key, bool&
       if (ta != 2 || tb != 2) return false;
       r = op == ZBHIP_OP_LT ? a < b : op == ZBHIP_OP_LE ? a <= b : op == ZBHIP_OP_GT ? a > b : a >= b;
     }
-    tag[sp - 1] = 1;
-    val[sp - 1] = r;
+    t0 = 1; a0 = r;
+    t1 = t2; a1 = a2; t2 = t3; a2 = a3;
+    --sp;
   }
-  if (sp != 1 || tag[0] != 1) return false;
-  out = val[0] != 0;
+  if (sp != 1 || t0 != 1) return false;
+  out = a0 != 0;
   return true;
 }
 
 // ExclusiveGatewayProcessor.findSequenceFlowToTake (:86-126)
-__device__ uint32_t find_sequence_flow(Lane& L, uint4 gw, uint32_t gw_key) {
+__device__ __forceinline__ uint32_t find_sequence_flow(Lane& L, uint4 gw, uint32_t gw_key) {
   uint32_t ob = gw.y & 0xFFFF, oc = gw.y >> 16;
   if (oc == 0) return NONE;  // implicit end
   if (oc == 1 && (elem_of(L, out_flow(L, ob)).z >> 16) == NONE) return out_flow(L, ob);
@@ -319,7 +333,7 @@ __device__ uint32_t find_sequence_flow(Lane& L, uint4 gw, uint32_t gw_key) {
 
 // ---- appliers ------------------------------------------------------------------------------
 // ProcessInstanceElementActivatingApplier.applyState (:48-204) for a child of the process
-__device__ void apply_activating_child(Lane& L, uint32_t elem, uint4 w, uint32_t key) {
+__device__ __forceinline__ void apply_activating_child(Lane& L, uint32_t elem, uint4 w, uint32_t key) {
   uint32_t type = etype(w);
   if (type == ZBHIP_EL_PARALLEL_GATEWAY) {  // cleanupSequenceFlowsTaken: Tetris decrement
     uint32_t base = w.w & 0xFFFF, n = w.x >> 16;
@@ -340,14 +354,14 @@ __device__ void apply_activating_child(Lane& L, uint32_t elem, uint4 w, uint32_t
 }
 
 // ProcessInstanceElementCompletedApplier.applyState (:45-73) -> DbElementInstanceState.removeInstance
-__device__ void apply_completed_child(Lane& L, int t, uint32_t key) {
+__device__ __forceinline__ void apply_completed_child(Lane& L, int t, uint32_t key) {
   if (L.trig_key == key) L.trig_key = NONE;  // eventScopeInstanceState.deleteInstance (triggers)
   L.tbl[t * kBlock] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   --L.pi_child;
 }
 
 // takeSequenceFlow (:243-263) + activateElementInstanceInFlowScope (:326-339)
-__device__ void take_sequence_flow(Lane& L, uint32_t flow) {
+__device__ __forceinline__ void take_sequence_flow(Lane& L, uint32_t flow) {
   uint4 fw = elem_of(L, flow);
   uint32_t sft = new_key(L);
   emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, flow);
@@ -365,7 +379,7 @@ __device__ void take_sequence_flow(Lane& L, uint32_t flow) {
 }
 
 // transitionToCompleted (:158-191) + afterExecutionPathCompleted -> ProcessProcessor (:130-140)
-__device__ void transition_to_completed_child(Lane& L, int t, uint32_t elem, uint4 w, uint32_t key) {
+__device__ __forceinline__ void transition_to_completed_child(Lane& L, int t, uint32_t elem, uint4 w, uint32_t key) {
   emit(L, ZBHIP_PI_ELEMENT_COMPLETED, key, 0, elem);
   apply_completed_child(L, t, key);
   if ((w.y >> 16) == 0) {  // end of the execution path
@@ -376,19 +390,19 @@ __device__ void transition_to_completed_child(Lane& L, int t, uint32_t elem, uin
   }
 }
 
-__device__ void take_outgoing(Lane& L, uint4 w) {
+__device__ __forceinline__ void take_outgoing(Lane& L, uint4 w) {
   uint32_t ob = w.y & 0xFFFF, oc = w.y >> 16;
   for (uint32_t i = 0; i < oc && !L.fail; ++i) take_sequence_flow(L, out_flow(L, ob + i));
 }
 
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
-__device__ void reject_pi(Lane& L, bool complete, uint32_t elem, uint32_t key, bool fs_pi, uint32_t reason,
+__device__ __forceinline__ void reject_pi(Lane& L, bool complete, uint32_t elem, uint32_t key, bool fs_pi, uint32_t reason,
                           uint32_t arg) {
   emit(L, kRejectBit | (complete ? ZBHIP_PI_COMPLETE_ELEMENT : ZBHIP_PI_ACTIVATE_ELEMENT), key,
        fs_pi ? 0u : (uint32_t)NONE, elem, reason | (arg << 4));
 }
 
-__device__ void process_pi(Lane& L, uint32_t entry) {
+__device__ __forceinline__ void process_pi(Lane& L, uint32_t entry) {
   const uint32_t elem = entry & 0xFFF;
   const bool complete = (entry >> 12) & 1;
   const bool fs_pi = (entry >> 13) & 1;
@@ -490,8 +504,7 @@ __device__ void process_pi(Lane& L, uint32_t entry) {
     emit(L, ZBHIP_PI_ELEMENT_COMPLETED, 0, NONE, 0);
     L.pi_live = false;  // removeInstance: variables, taken-flow counters of the scope go with it
     L.nvars = 0;
-#pragma unroll
-    for (int i = 0; i < kJoinWords; ++i) L.jw[i] = 0;
+    L.jw0 = L.jw1 = L.jw2 = L.jw3 = 0;
     ++L.completed;
     return;
   }
@@ -559,11 +572,11 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     L.doc_begin = doc_begin;
     L.doc_count = doc_count;
     L.has_join = false;
-#pragma unroll
-    for (int i = 0; i < kJoinWords; ++i) L.jw[i] = 0;
+    L.jw0 = L.jw1 = L.jw2 = L.jw3 = 0;
     L.nvars = 0;
-#pragma unroll
-    for (int i = 0; i < kVars; ++i) { L.vm[i] = make_uint2(0xFFFFFFFFu, 0); L.vv[i] = 0; }
+    L.vx0 = L.vx1 = L.vx2 = L.vx3 = 0xFFFFFFFFu;
+    L.vy0 = L.vy1 = L.vy2 = L.vy3 = 0;
+    L.vv0 = L.vv1 = L.vv2 = L.vv3 = 0;
 
     const bool bad_cmd = inst >= N || (doc_count && (uint64_t)doc_begin + doc_count > P.n_docs);
     const uint4 h = bad_cmd ? make_uint4(0xFFFFFFFFu, 0, 0, 0) : P.st.hdr[inst];
@@ -596,15 +609,20 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
       L.nvars = (int)nvars0;
 #pragma unroll
       for (int v = 0; v < kVars; ++v)
-        if (v < L.nvars) { L.vm[v] = P.st.var_meta[(size_t)v * N + inst]; L.vv[v] = P.st.var_val[(size_t)v * N + inst]; }
+        if (v < L.nvars) {
+          const uint2 m = P.st.var_meta[(size_t)v * N + inst];
+          var_put(L, v, m.x, m.y, P.st.var_val[(size_t)v * N + inst]);
+        }
     }
     L.first_ord = L.next_ord;
     if (!L.fail && L.proc != NONE) {
       L.pb = prog + prog[1 + L.proc];
       L.has_join = (L.pb[1] & 0xFFFF) != 0;
       if (L.has_join && kind != ZBHIP_CMD_CREATE) {
-#pragma unroll
-        for (int i = 0; i < kJoinWords; ++i) L.jw[i] = P.st.join[(size_t)i * N + inst];
+        L.jw0 = P.st.join[inst];
+        L.jw1 = P.st.join[(size_t)N + inst];
+        L.jw2 = P.st.join[(size_t)2 * N + inst];
+        L.jw3 = P.st.join[(size_t)3 * N + inst];
       }
     }
 
@@ -668,10 +686,15 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
         }
 #pragma unroll
         for (int v = 0; v < kVars; ++v)
-          if (v < L.nvars) { P.st.var_meta[(size_t)v * N + inst] = L.vm[v]; P.st.var_val[(size_t)v * N + inst] = L.vv[v]; }
+          if (v < L.nvars) {
+            P.st.var_meta[(size_t)v * N + inst] = make_uint2(var_x(L, v), var_y(L, v));
+            P.st.var_val[(size_t)v * N + inst] = var_v(L, v);
+          }
         if (L.has_join) {
-#pragma unroll
-          for (int i = 0; i < kJoinWords; ++i) P.st.join[(size_t)i * N + inst] = L.jw[i];
+          P.st.join[inst] = L.jw0;
+          P.st.join[(size_t)N + inst] = L.jw1;
+          P.st.join[(size_t)2 * N + inst] = L.jw2;
+          P.st.join[(size_t)3 * N + inst] = L.jw3;
         }
         P.st.hdr[inst] = make_uint4(L.proc | ((uint32_t)L.next_ord << 16),
                                     L.pi_state | (ns << 8) | ((uint32_t)L.nvars << 16) | (1u << 24),
@@ -773,9 +796,14 @@ __global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* bsum, uint32_t nb,
   if (threadIdx.x == 0) *total = carry;
 }
 
+// Block b owns commands [256 b, 256 b + 256): it scans their record counts into LDS and then all
+// 256 lanes copy the block's records together, lane l taking output records l, l + 256, ...
+// (binary search over the LDS prefix finds the source command): every store is coalesced and
+// the loads walk each command's slot contiguously.
 __global__ __launch_bounds__(kBlock) void k_compact(const uint2* cmd_hdr, uint32_t n, const uint32_t* bsum,
                                                     const uint2* rec, uint32_t rec_cap, uint2* out) {
   __shared__ uint32_t ws[kBlock / 64];
+  __shared__ uint32_t pre[kBlock + 1];
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t v = i < n ? (cmd_hdr[i].x & 0xFFFF) : 0;
   const uint32_t inc = wave_incl_scan(v);
@@ -783,9 +811,21 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint2* cmd_hdr, uint32
   __syncthreads();
   uint32_t wbase = 0;
   for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += ws[w];
-  const uint32_t off = bsum[blockIdx.x] + wbase + inc - v;
-  const uint2* src = rec + (size_t)i * rec_cap;
-  for (uint32_t j = 0; j < v; ++j) out[off + j] = src[j];
+  pre[threadIdx.x] = wbase + inc - v;
+  if (threadIdx.x == kBlock - 1) pre[kBlock] = wbase + inc;
+  __syncthreads();
+  const uint32_t total = pre[kBlock];
+  const uint32_t base = bsum[blockIdx.x];
+  const uint2* src = rec + (size_t)blockIdx.x * kBlock * rec_cap;
+  for (uint32_t o = threadIdx.x; o < total; o += kBlock) {
+    uint32_t lo = 0, hi = kBlock;  // largest c with pre[c] <= o
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= o) lo = mid;
+      else hi = mid;
+    }
+    out[base + o] = src[(size_t)lo * rec_cap + (o - pre[lo])];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
