@@ -40,7 +40,7 @@ struct Lane {
   const uint32_t* pb;   // process block (LDS)
   uint2* tbl;           // LDS table base (entry t at tbl[t * kBlock])
   uint32_t* q;          // LDS queue base (entry i at q[(i % kQueue) * kBlock])
-  uint2* rec;           // this command's record slot
+  uint2* rec;           // this command's record slot: record j at rec[j * 64] (wave-interleaved)
   uint32_t rec_cap;
   uint32_t nrec;
   uint32_t fail;
@@ -124,7 +124,7 @@ __device__ __forceinline__ uint16_t new_key(Lane& L) {
 __device__ __forceinline__ void emit(Lane& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
                                      uint32_t flags = 0) {
   if (L.nrec < L.rec_cap) {
-    L.rec[L.nrec] = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16) | (flags << 24));
+    L.rec[(size_t)L.nrec * 64] = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16) | (flags << 24));
   } else {
     set_fail(L, FB_RECORDS);
   }
@@ -557,7 +557,9 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     Lane L;
     L.tbl = tbl_base + threadIdx.x;
     L.q = q_base + threadIdx.x;
-    L.rec = P.rec + (size_t)ci * P.rec_cap;
+    // wave-interleaved record slots: the 64 commands of a group of 64 write record j side by side,
+    // so each emit of a wave is one coalesced 512-byte store
+    L.rec = P.rec + ((size_t)(ci >> 6) * P.rec_cap << 6) + (ci & 63);
     L.rec_cap = P.rec_cap;
     L.nrec = 0;
     L.fail = 0;
@@ -720,7 +722,9 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     }
     n_cmd = 1;
   }
-  // one atomic per wave and counter (wave64 reduction)
+  // per-workgroup statistics: wave64 reduction, then the 4 waves through LDS; one plain add per
+  // counter into this workgroup's own row (no global-atomic hot spot: rows are reduced by
+  // k_scan_sums).
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     n_rec += __shfl_xor(n_rec, off);
@@ -730,13 +734,17 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     n_fb += __shfl_xor(n_fb, off);
     n_cmd += __shfl_xor(n_cmd, off);
   }
-  if ((threadIdx.x & 63) == 0 && n_cmd) {
-    atomicAdd(&P.counters[0], (unsigned long long)n_rec);
-    atomicAdd(&P.counters[1], (unsigned long long)n_trans);
-    atomicAdd(&P.counters[2], (unsigned long long)n_comp);
-    atomicAdd(&P.counters[3], (unsigned long long)n_keys);
-    atomicAdd(&P.counters[4], (unsigned long long)n_fb);
-    atomicAdd(&P.counters[5], (unsigned long long)n_cmd);
+  __shared__ uint32_t wstat[kBlock / 64][8];
+  if ((threadIdx.x & 63) == 0) {
+    uint32_t* w = wstat[threadIdx.x >> 6];
+    w[0] = n_rec; w[1] = n_trans; w[2] = n_comp; w[3] = n_keys; w[4] = n_fb; w[5] = n_cmd;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) sum += wstat[w][threadIdx.x];
+    if (sum) atomicAdd(&P.blk_stats[(size_t)blockIdx.x * 8 + threadIdx.x], sum);  // own row: uncontended
   }
 }
 
@@ -769,9 +777,30 @@ __global__ __launch_bounds__(kBlock) void k_block_sums(const uint2* cmd_hdr, uin
 }
 
 // single workgroup: exclusive scan of the block sums (64-bit total)
-__global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* bsum, uint32_t nb, unsigned long long* total) {
+__global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* bsum, uint32_t nb, unsigned long long* total,
+                                                   const uint32_t* blk_stats, uint32_t n_blk,
+                                                   unsigned long long* counters) {
   __shared__ uint32_t ws[16];
   __shared__ uint32_t carry;
+  __shared__ unsigned long long cs[16][6];
+  {  // reduce the per-workgroup statistics rows of k_step
+    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t b = threadIdx.x; b < n_blk; b += 1024)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) c[k] += blk_stats[(size_t)b * 8 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) c[k] += __shfl_xor(c[k], off);
+      if ((threadIdx.x & 63) == 0) cs[threadIdx.x >> 6][k] = c[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      unsigned long long t = 0;
+      for (int w = 0; w < 16; ++w) t += cs[w][threadIdx.x];
+      counters[threadIdx.x] = t;
+    }
+  }
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   for (uint32_t base = 0; base < nb; base += 1024) {
@@ -816,7 +845,7 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint2* cmd_hdr, uint32
   __syncthreads();
   const uint32_t total = pre[kBlock];
   const uint32_t base = bsum[blockIdx.x];
-  const uint2* src = rec + (size_t)blockIdx.x * kBlock * rec_cap;
+  const uint2* src = rec + (size_t)blockIdx.x * kBlock * rec_cap;  // 4 groups of 64 commands
   for (uint32_t o = threadIdx.x; o < total; o += kBlock) {
     uint32_t lo = 0, hi = kBlock;  // largest c with pre[c] <= o
     while (hi - lo > 1) {
@@ -824,7 +853,8 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint2* cmd_hdr, uint32
       if (pre[mid] <= o) lo = mid;
       else hi = mid;
     }
-    out[base + o] = src[(size_t)lo * rec_cap + (o - pre[lo])];
+    const uint32_t j = o - pre[lo];
+    out[base + o] = src[(((size_t)(lo >> 6) * rec_cap + j) << 6) + (lo & 63)];
   }
 }
 
@@ -844,11 +874,12 @@ hipError_t launch_step(const StepParams& P, hipStream_t s) {
 }
 
 hipError_t launch_compact(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum, const uint2* rec, uint32_t rec_cap,
-                          uint2* out, unsigned long long* total, hipStream_t s) {
-  if (n == 0) return hipSuccess;
+                          uint2* out, unsigned long long* total, const uint32_t* blk_stats, uint32_t n_blk,
+                          unsigned long long* counters, hipStream_t s) {
   const uint32_t nb = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_block_sums, dim3(nb), dim3(kBlock), 0, s, cmd_hdr, n, bsum);
-  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, s, bsum, nb, total);
+  if (n) hipLaunchKernelGGL(k_block_sums, dim3(nb), dim3(kBlock), 0, s, cmd_hdr, n, bsum);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, s, bsum, nb, total, blk_stats, n_blk, counters);
+  if (n == 0) return hipGetLastError();
   hipLaunchKernelGGL(k_compact, dim3(nb), dim3(kBlock), 0, s, cmd_hdr, n, bsum, rec, rec_cap, out);
   return hipGetLastError();
 }

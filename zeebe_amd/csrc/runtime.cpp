@@ -20,7 +20,8 @@ namespace zb {
 size_t step_lds_bytes(uint32_t prog_words);
 hipError_t launch_step(const StepParams& P, hipStream_t s);
 hipError_t launch_compact(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum, const uint2* rec, uint32_t rec_cap,
-                          uint2* out, unsigned long long* total, hipStream_t s);
+                          uint2* out, unsigned long long* total, const uint32_t* blk_stats, uint32_t n_blk,
+                          unsigned long long* counters, hipStream_t s);
 }  // namespace zb
 
 using namespace zb;
@@ -91,6 +92,7 @@ struct zbhip_handle {
   uint32_t* d_bsum = nullptr;
   uint2* d_out = nullptr;
   unsigned long long* d_counters = nullptr;  // [0..5] + [6] compact total
+  uint32_t* d_blk_stats = nullptr;           // [max grid][8]
   uint32_t rec_cap = 64;
   size_t rec_slots = 0;  // commands the record buffer is sized for
 
@@ -180,6 +182,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
             dalloc(&h->d_cmd_hdr, cfg->max_commands) == hipSuccess &&
             dalloc(&h->d_bsum, (cfg->max_commands + kBlock - 1) / kBlock + 1) == hipSuccess &&
             dalloc(&h->d_counters, 8) == hipSuccess &&
+            dalloc(&h->d_blk_stats, ((size_t)(cfg->max_commands + kBlock - 1) / kBlock) * 8) == hipSuccess &&
             dalloc(&h->d_rec, (size_t)cfg->max_commands * h->rec_cap) == hipSuccess &&
             dalloc(&h->d_out, (size_t)cfg->max_commands * h->rec_cap) == hipSuccess;
   if (!ok) { zbhip_close(h); return ZBHIP_ENOMEM; }
@@ -212,6 +215,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_bsum);
   (void)hipFree(h->d_out);
   (void)hipFree(h->d_counters);
+  (void)hipFree(h->d_blk_stats);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -434,7 +438,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   const bool timed = flags & ZBHIP_RUN_TIMED;
   const bool want = !(flags & ZBHIP_RUN_NO_RESULTS);
   const uint32_t n = (uint32_t)h->n_cmds;
-  HIPCHK(hipMemsetAsync(h->d_counters, 0, 8 * sizeof(unsigned long long), h->stream));
+  const uint32_t n_blk = (n + kBlock - 1) / kBlock;
+  if (n_blk) HIPCHK(hipMemsetAsync(h->d_blk_stats, 0, (size_t)n_blk * 8 * sizeof(uint32_t), h->stream));
 
   StepParams P{};
   P.cmds = h->external ? h->ext_cmds : h->d_cmds;
@@ -447,7 +452,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.rec = h->d_rec;
   P.rec_cap = h->rec_cap;
   P.cmd_hdr = h->d_cmd_hdr;
-  P.counters = h->d_counters;
+  P.blk_stats = h->d_blk_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
 
   uint32_t launches = 0;
@@ -466,7 +471,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     }
   }
   if (timed) HIPCHK(hipEventRecord(h->ev[1], h->stream));
-  HIPCHK(launch_compact(h->d_cmd_hdr, n, h->d_bsum, h->d_rec, h->rec_cap, h->d_out, h->d_counters + 6, h->stream));
+  HIPCHK(launch_compact(h->d_cmd_hdr, n, h->d_bsum, h->d_rec, h->rec_cap, h->d_out, h->d_counters + 6,
+                        h->d_blk_stats, n_blk, h->d_counters, h->stream));
   if (timed) HIPCHK(hipEventRecord(h->ev[2], h->stream));
 
   unsigned long long cnt[8] = {0};

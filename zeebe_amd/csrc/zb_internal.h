@@ -95,7 +95,7 @@ struct StepParams {
   uint2* rec;                 // [n_cmds][rec_cap] record slots, indexed by command index
   uint32_t rec_cap;
   uint2* cmd_hdr;             // [n_cmds]
-  unsigned long long* counters;  // [0] records [1] transitions [2] completed [3] keys [4] fallback [5] commands
+  uint32_t* blk_stats;        // [grid][8] per-workgroup: records, transitions, completed, keys, fallback, commands
   int32_t max_cmds_in_batch;
 };
 
