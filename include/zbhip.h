@@ -248,8 +248,9 @@ int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbh
 int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,
                         const zbhip_doc_entry* dev_docs, size_t n_docs);
 
-#define ZBHIP_RUN_NO_RESULTS 1u  /* skip the D2H copy of results (benchmarking) */
-#define ZBHIP_RUN_TIMED 2u       /* record HIP events around each kernel */
+#define ZBHIP_RUN_NO_RESULTS 1u  /* benchmarking: no D2H copy, no host wait, no key relabelling */
+#define ZBHIP_RUN_TIMED 2u       /* record HIP events around the lifecycle kernel launches */
+#define ZBHIP_RUN_ACCUMULATE 4u  /* keep accumulating statistics/timings of the previous runs */
 /* Processes the submitted window to quiescence.  Returns #commands processed or <0. */
 int zbhip_run(zbhip_handle* h, uint32_t flags);
 
@@ -284,8 +285,8 @@ typedef struct zbhip_stats {
   uint64_t completed_instances; /* PROCESS ELEMENT_COMPLETED */
   uint64_t keys;                /* keys generated */
   uint64_t fallback;            /* batches flagged for the fallback path */
-  double step_ms;               /* device time of the lifecycle kernel(s), ZBHIP_RUN_TIMED */
-  double compact_ms;            /* device time of the compaction kernel(s) */
+  double step_ms;               /* device time of the lifecycle kernel launches (ZBHIP_RUN_TIMED runs) */
+  double compact_ms;            /* 0: record compaction is fused into the lifecycle kernel */
   uint32_t rounds;              /* per-instance serialisation rounds of the window */
   uint32_t launches;
 } zbhip_stats;

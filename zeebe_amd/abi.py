@@ -60,6 +60,7 @@ DEC_SCALE = 6
 
 RUN_NO_RESULTS = 1
 RUN_TIMED = 2
+RUN_ACCUMULATE = 4
 
 
 class DocEntry(C.Structure):

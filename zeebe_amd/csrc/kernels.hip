@@ -36,11 +36,22 @@ namespace zb {
 // ---------------------------------------------------------------------------------------------
 // per-lane batch context
 // ---------------------------------------------------------------------------------------------
+// Kernel configuration: workgroup size B, LDS element-instance table entries T, LDS queue
+// entries Q, records staged in LDS per lane R (rows j >= R go to the global overflow rows).
+template <int B_, int T_, int Q_, int R_>
+struct KCfg {
+  static constexpr int B = B_, T = T_, Q = Q_, R = R_;
+};
+using KSimple = KCfg<128, 4, 4, 32>;    // processes without parallel gateways / multi-outgoing nodes
+using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
+
+template <class K>
 struct Lane {
   const uint32_t* pb;   // process block (LDS)
-  uint2* tbl;           // LDS table base (entry t at tbl[t * kBlock])
-  uint32_t* q;          // LDS queue base (entry i at q[(i % kQueue) * kBlock])
-  uint2* rec;           // this command's record slot: record j at rec[j * 64] (wave-interleaved)
+  uint2* tbl;           // LDS table base (entry t at tbl[t * K::B])
+  uint32_t* q;          // LDS queue base (entry i at q[(i % K::Q) * K::B])
+  uint2* stage;         // LDS record rows of this lane: record j < R at stage[j * K::B]
+  uint2* rec;           // global overflow rows of this command: record j >= R at rec[j * 64]
   uint32_t rec_cap;
   uint32_t nrec;
   uint32_t fail;
@@ -72,13 +83,16 @@ struct Lane {
 };
 static_assert(kVars == 4 && kJoinWords == 4, "scalarised tables");
 
-__device__ __forceinline__ uint32_t var_x(const Lane& L, int i) {
+template <class K>
+__device__ __forceinline__ uint32_t var_x(const Lane<K>& L, int i) {
   return i == 0 ? L.vx0 : i == 1 ? L.vx1 : i == 2 ? L.vx2 : L.vx3;
 }
-__device__ __forceinline__ uint32_t var_y(const Lane& L, int i) {
+template <class K>
+__device__ __forceinline__ uint32_t var_y(const Lane<K>& L, int i) {
   return i == 0 ? L.vy0 : i == 1 ? L.vy1 : i == 2 ? L.vy2 : L.vy3;
 }
-__device__ __forceinline__ long long var_v(const Lane& L, int i) {
+template <class K>
+__device__ __forceinline__ long long var_v(const Lane<K>& L, int i) {
   const long long v0 = L.vv0, v1 = L.vv1, v2 = L.vv2, v3 = L.vv3;
   long long r = v3;
   r = i == 2 ? v2 : r;
@@ -88,43 +102,53 @@ __device__ __forceinline__ long long var_v(const Lane& L, int i) {
 }
 // branch-free updates: a store per field keeps every field a plain SSA value (an if/else chain
 // is merged by the optimiser into one store through a selected pointer -> scratch)
-__device__ __forceinline__ void var_put(Lane& L, int i, uint32_t x, uint32_t y, long long v) {
+template <class K>
+__device__ __forceinline__ void var_put(Lane<K>& L, int i, uint32_t x, uint32_t y, long long v) {
   L.vx0 = i == 0 ? x : L.vx0; L.vy0 = i == 0 ? y : L.vy0; L.vv0 = i == 0 ? v : L.vv0;
   L.vx1 = i == 1 ? x : L.vx1; L.vy1 = i == 1 ? y : L.vy1; L.vv1 = i == 1 ? v : L.vv1;
   L.vx2 = i == 2 ? x : L.vx2; L.vy2 = i == 2 ? y : L.vy2; L.vv2 = i == 2 ? v : L.vv2;
   L.vx3 = i == 3 ? x : L.vx3; L.vy3 = i == 3 ? y : L.vy3; L.vv3 = i == 3 ? v : L.vv3;
 }
-__device__ __forceinline__ uint32_t jw_get(const Lane& L, int i) {
+template <class K>
+__device__ __forceinline__ uint32_t jw_get(const Lane<K>& L, int i) {
   return i == 0 ? L.jw0 : i == 1 ? L.jw1 : i == 2 ? L.jw2 : L.jw3;
 }
-__device__ __forceinline__ void jw_put(Lane& L, int i, uint32_t w) {
+template <class K>
+__device__ __forceinline__ void jw_put(Lane<K>& L, int i, uint32_t w) {
   L.jw0 = i == 0 ? w : L.jw0;
   L.jw1 = i == 1 ? w : L.jw1;
   L.jw2 = i == 2 ? w : L.jw2;
   L.jw3 = i == 3 ? w : L.jw3;
 }
 
-__device__ __forceinline__ void set_fail(Lane& L, uint32_t why) {
+template <class K>
+__device__ __forceinline__ void set_fail(Lane<K>& L, uint32_t why) {
   if (!L.fail) L.fail = why;
 }
 
-__device__ __forceinline__ uint4 elem_of(const Lane& L, uint32_t e) {
+template <class K>
+__device__ __forceinline__ uint4 elem_of(const Lane<K>& L, uint32_t e) {
   return reinterpret_cast<const uint4*>(L.pb + 8)[e];
 }
 __device__ __forceinline__ uint32_t etype(uint4 w) { return w.x & 0xFF; }
-__device__ __forceinline__ uint32_t out_flow(const Lane& L, uint32_t i) {
+template <class K>
+__device__ __forceinline__ uint32_t out_flow(const Lane<K>& L, uint32_t i) {
   return reinterpret_cast<const uint16_t*>(L.pb + L.pb[2])[i];
 }
 
-__device__ __forceinline__ uint16_t new_key(Lane& L) {
+template <class K>
+__device__ __forceinline__ uint16_t new_key(Lane<K>& L) {
   if (L.next_ord >= 0xFFF0) set_fail(L, FB_KEYS);
   return L.next_ord++;
 }
 
-__device__ __forceinline__ void emit(Lane& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
+template <class K>
+__device__ __forceinline__ void emit(Lane<K>& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
                                      uint32_t flags = 0) {
   if (L.nrec < L.rec_cap) {
-    L.rec[(size_t)L.nrec * 64] = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16) | (flags << 24));
+    const uint2 r = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16) | (flags << 24));
+    if (L.nrec < (uint32_t)K::R) L.stage[L.nrec * K::B] = r;
+    else L.rec[(size_t)L.nrec * 64] = r;
   } else {
     set_fail(L, FB_RECORDS);
   }
@@ -133,49 +157,55 @@ __device__ __forceinline__ void emit(Lane& L, uint32_t code, uint32_t key, uint3
 }
 
 // queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | key << 16
-__device__ __forceinline__ void push(Lane& L, uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
+template <class K>
+__device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
   // ProcessingStateMachine.collectBatchProcessingStepResult (:388-417): a follow-up command is
   // processed in this batch only while pending + processed + 1 + admitted < maxCommandsInBatch;
   // otherwise the platform writes it to the log unprocessed -> outside the device subset.
   if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
-  if (L.qt - L.qh >= kQueue) { set_fail(L, FB_QUEUE); return; }
-  L.q[(L.qt % kQueue) * kBlock] = elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
+  if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
+  L.q[(L.qt % kQueue) * K::B] = elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
   ++L.qt;
 }
 
 // ---- element-instance table (LDS) ----------------------------------------------------------
-__device__ __forceinline__ int tbl_find(const Lane& L, uint32_t key) {
+template <class K>
+__device__ __forceinline__ int tbl_find(const Lane<K>& L, uint32_t key) {
   for (int t = 0; t < L.nt; ++t) {
-    uint2 e = L.tbl[t * kBlock];
+    uint2 e = L.tbl[t * K::B];
     if (e.x != 0xFFFFFFFFu && (e.x >> 16) == key) return t;
   }
   return -1;
 }
-__device__ __forceinline__ int tbl_find_job(const Lane& L, uint32_t job) {
+template <class K>
+__device__ __forceinline__ int tbl_find_job(const Lane<K>& L, uint32_t job) {
   for (int t = 0; t < L.nt; ++t) {
-    uint2 e = L.tbl[t * kBlock];
+    uint2 e = L.tbl[t * K::B];
     if (e.x != 0xFFFFFFFFu && (e.y & 0xFFFF) == job && (e.y >> 24) & 1u) return t;
   }
   return -1;
 }
-__device__ __forceinline__ void tbl_insert(Lane& L, uint32_t elem, uint32_t key, uint32_t state) {
+template <class K>
+__device__ __forceinline__ void tbl_insert(Lane<K>& L, uint32_t elem, uint32_t key, uint32_t state) {
   int t = 0;
   for (; t < L.nt; ++t)
-    if (L.tbl[t * kBlock].x == 0xFFFFFFFFu) break;
+    if (L.tbl[t * K::B].x == 0xFFFFFFFFu) break;
   if (t == L.nt) {
-    if (L.nt >= kTable) { set_fail(L, FB_TABLE); return; }
+    if (L.nt >= K::T) { set_fail(L, FB_TABLE); return; }
     ++L.nt;
   }
-  L.tbl[t * kBlock] = make_uint2(elem | (key << 16), JOB_ZERO | (state << 16));
+  L.tbl[t * K::B] = make_uint2(elem | (key << 16), JOB_ZERO | (state << 16));
 }
-__device__ __forceinline__ void tbl_set_state(Lane& L, int t, uint32_t state) {
-  uint2 e = L.tbl[t * kBlock];
+template <class K>
+__device__ __forceinline__ void tbl_set_state(Lane<K>& L, int t, uint32_t state) {
+  uint2 e = L.tbl[t * K::B];
   e.y = (e.y & 0xFF00FFFFu) | (state << 16);
-  L.tbl[t * kBlock] = e;
+  L.tbl[t * K::B] = e;
 }
 
 // ---- variables (registers) ------------------------------------------------------------------
-__device__ __forceinline__ int var_find(const Lane& L, uint32_t scope, uint32_t name) {
+template <class K>
+__device__ __forceinline__ int var_find(const Lane<K>& L, uint32_t scope, uint32_t name) {
   const uint32_t want = name | (scope << 16);
   int r = -1;
   if (L.nvars > 3 && L.vx3 == want) r = 3;
@@ -186,7 +216,8 @@ __device__ __forceinline__ int var_find(const Lane& L, uint32_t scope, uint32_t 
 }
 
 // VariableBehavior.setLocalVariable (VariableBehavior.java:191-200) + VariableApplier
-__device__ __forceinline__ void set_local_variable(Lane& L, uint32_t scope, const zbhip_doc_entry& d) {
+template <class K>
+__device__ __forceinline__ void set_local_variable(Lane<K>& L, uint32_t scope, const zbhip_doc_entry& d) {
   int v = var_find(L, scope, d.name_id);
   if (v < 0) {
     if (L.nvars >= kVars) { set_fail(L, FB_VARS); return; }
@@ -204,7 +235,8 @@ __device__ __forceinline__ void set_local_variable(Lane& L, uint32_t scope, cons
 
 // VariableBehavior.mergeDocument (VariableBehavior.java:105-150) from an element scope whose
 // parent is the process instance (the only nesting in the supported subset).
-__device__ __forceinline__ void merge_document_from(Lane& L, uint32_t scope_key, uint32_t begin, uint32_t count) {
+template <class K>
+__device__ __forceinline__ void merge_document_from(Lane<K>& L, uint32_t scope_key, uint32_t begin, uint32_t count) {
   if (count == 0) return;
   if (count > 1) { set_fail(L, FB_DOC); return; }
   const zbhip_doc_entry d = L.docs[begin];
@@ -223,10 +255,12 @@ __device__ __forceinline__ void merge_document_from(Lane& L, uint32_t scope_key,
 }
 
 // ---- join counters (registers, 16 x u8) ----------------------------------------------------
-__device__ __forceinline__ uint32_t join_get(const Lane& L, uint32_t s) {
+template <class K>
+__device__ __forceinline__ uint32_t join_get(const Lane<K>& L, uint32_t s) {
   return (jw_get(L, (int)(s >> 2)) >> ((s & 3) * 8)) & 0xFF;
 }
-__device__ __forceinline__ void join_set(Lane& L, uint32_t s, uint32_t v) {
+template <class K>
+__device__ __forceinline__ void join_set(Lane<K>& L, uint32_t s, uint32_t v) {
   const uint32_t sh = (s & 3) * 8;
   const int i = (int)(s >> 2);
   jw_put(L, i, (jw_get(L, i) & ~(0xFFu << sh)) | ((v & 0xFF) << sh));
@@ -236,7 +270,8 @@ __device__ __forceinline__ void join_set(Lane& L, uint32_t s, uint32_t v) {
 // Values: tag 0 NULL, 1 BOOL, 2 NUMBER (x 10^ZBHIP_DEC_SCALE).  Results that are not boolean
 // raise an incident in the reference (ExpressionProcessor.java:356-368) -> fallback.
 // The operand stack is four registers, top first (the compiler bounds the depth to 4).
-__device__ __forceinline__ bool load_var(const Lane& L, uint32_t name, uint32_t scope_key, uint32_t& t,
+template <class K>
+__device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32_t scope_key, uint32_t& t,
                                          long long& x) {
   // DbVariableState.getVariable: element scope first, then the process instance scope
   int v = var_find(L, scope_key, name);
@@ -258,7 +293,8 @@ __device__ __forceinline__ bool load_var(const Lane& L, uint32_t name, uint32_t 
   return false;
 }
 
-__device__ __forceinline__ bool eval_condition(Lane& L, uint32_t cond, uint32_t scope_key, bool& out) {
+template <class K>
+__device__ __forceinline__ bool eval_condition(Lane<K>& L, uint32_t cond, uint32_t scope_key, bool& out) {
   const uint32_t* pb = L.pb;
   uint32_t pc = pb[pb[3] + cond];
   const uint32_t* code = pb + pb[4];
@@ -313,7 +349,8 @@ __device__ __forceinline__ bool eval_condition(Lane& L, uint32_t cond, uint32_t 
 }
 
 // ExclusiveGatewayProcessor.findSequenceFlowToTake (:86-126)
-__device__ __forceinline__ uint32_t find_sequence_flow(Lane& L, uint4 gw, uint32_t gw_key) {
+template <class K>
+__device__ __forceinline__ uint32_t find_sequence_flow(Lane<K>& L, uint4 gw, uint32_t gw_key) {
   uint32_t ob = gw.y & 0xFFFF, oc = gw.y >> 16;
   if (oc == 0) return NONE;  // implicit end
   if (oc == 1 && (elem_of(L, out_flow(L, ob)).z >> 16) == NONE) return out_flow(L, ob);
@@ -333,7 +370,8 @@ __device__ __forceinline__ uint32_t find_sequence_flow(Lane& L, uint4 gw, uint32
 
 // ---- appliers ------------------------------------------------------------------------------
 // ProcessInstanceElementActivatingApplier.applyState (:48-204) for a child of the process
-__device__ __forceinline__ void apply_activating_child(Lane& L, uint32_t elem, uint4 w, uint32_t key) {
+template <class K>
+__device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem, uint4 w, uint32_t key) {
   uint32_t type = etype(w);
   if (type == ZBHIP_EL_PARALLEL_GATEWAY) {  // cleanupSequenceFlowsTaken: Tetris decrement
     uint32_t base = w.w & 0xFFFF, n = w.x >> 16;
@@ -354,14 +392,16 @@ __device__ __forceinline__ void apply_activating_child(Lane& L, uint32_t elem, u
 }
 
 // ProcessInstanceElementCompletedApplier.applyState (:45-73) -> DbElementInstanceState.removeInstance
-__device__ __forceinline__ void apply_completed_child(Lane& L, int t, uint32_t key) {
+template <class K>
+__device__ __forceinline__ void apply_completed_child(Lane<K>& L, int t, uint32_t key) {
   if (L.trig_key == key) L.trig_key = NONE;  // eventScopeInstanceState.deleteInstance (triggers)
-  L.tbl[t * kBlock] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+  L.tbl[t * K::B] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   --L.pi_child;
 }
 
 // takeSequenceFlow (:243-263) + activateElementInstanceInFlowScope (:326-339)
-__device__ __forceinline__ void take_sequence_flow(Lane& L, uint32_t flow) {
+template <class K>
+__device__ __forceinline__ void take_sequence_flow(Lane<K>& L, uint32_t flow) {
   uint4 fw = elem_of(L, flow);
   uint32_t sft = new_key(L);
   emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, flow);
@@ -379,7 +419,8 @@ __device__ __forceinline__ void take_sequence_flow(Lane& L, uint32_t flow) {
 }
 
 // transitionToCompleted (:158-191) + afterExecutionPathCompleted -> ProcessProcessor (:130-140)
-__device__ __forceinline__ void transition_to_completed_child(Lane& L, int t, uint32_t elem, uint4 w, uint32_t key) {
+template <class K>
+__device__ __forceinline__ void transition_to_completed_child(Lane<K>& L, int t, uint32_t elem, uint4 w, uint32_t key) {
   emit(L, ZBHIP_PI_ELEMENT_COMPLETED, key, 0, elem);
   apply_completed_child(L, t, key);
   if ((w.y >> 16) == 0) {  // end of the execution path
@@ -390,19 +431,22 @@ __device__ __forceinline__ void transition_to_completed_child(Lane& L, int t, ui
   }
 }
 
-__device__ __forceinline__ void take_outgoing(Lane& L, uint4 w) {
+template <class K>
+__device__ __forceinline__ void take_outgoing(Lane<K>& L, uint4 w) {
   uint32_t ob = w.y & 0xFFFF, oc = w.y >> 16;
   for (uint32_t i = 0; i < oc && !L.fail; ++i) take_sequence_flow(L, out_flow(L, ob + i));
 }
 
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
-__device__ __forceinline__ void reject_pi(Lane& L, bool complete, uint32_t elem, uint32_t key, bool fs_pi, uint32_t reason,
+template <class K>
+__device__ __forceinline__ void reject_pi(Lane<K>& L, bool complete, uint32_t elem, uint32_t key, bool fs_pi, uint32_t reason,
                           uint32_t arg) {
   emit(L, kRejectBit | (complete ? ZBHIP_PI_COMPLETE_ELEMENT : ZBHIP_PI_ACTIVATE_ELEMENT), key,
        fs_pi ? 0u : (uint32_t)NONE, elem, reason | (arg << 4));
 }
 
-__device__ __forceinline__ void process_pi(Lane& L, uint32_t entry) {
+template <class K>
+__device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   const uint32_t elem = entry & 0xFFF;
   const bool complete = (entry >> 12) & 1;
   const bool fs_pi = (entry >> 13) & 1;
@@ -462,9 +506,9 @@ __device__ __forceinline__ void process_pi(Lane& L, uint32_t entry) {
       case ZBHIP_EL_SERVICE_TASK: {  // JobWorkerTaskProcessor.onActivate (:49-61)
         uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
         emit(L, C_JOB_CREATED, job, key, elem);
-        uint2 e = L.tbl[t * kBlock];   // JobCreatedApplier: element instance jobKey
+        uint2 e = L.tbl[t * K::B];   // JobCreatedApplier: element instance jobKey
         e.y = (job & 0xFFFF) | (e.y & 0x00FF0000u) | (1u << 24);
-        L.tbl[t * kBlock] = e;
+        L.tbl[t * K::B] = e;
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
         return;
@@ -510,7 +554,7 @@ __device__ __forceinline__ void process_pi(Lane& L, uint32_t entry) {
   }
   const int t = tbl_find(L, cmd_key);
   if (t < 0) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
-  const uint32_t st = (L.tbl[t * kBlock].y >> 16) & 0xFF;
+  const uint32_t st = (L.tbl[t * K::B].y >> 16) & 0xFF;
   if (st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING) {
     reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_STATE, st);
     return;
@@ -533,16 +577,21 @@ __device__ __forceinline__ void process_pi(Lane& L, uint32_t entry) {
 // ---------------------------------------------------------------------------------------------
 // k_step
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
+template <class K>
+__global__ __launch_bounds__(K::B) void k_step(StepParams P) {
   extern __shared__ __align__(16) uint32_t smem[];
   const uint32_t prog_words = (P.prog_words + 3) & ~3u;
   uint32_t* prog = smem;
   uint2* tbl_base = reinterpret_cast<uint2*>(smem + prog_words);
-  uint32_t* q_base = reinterpret_cast<uint32_t*>(tbl_base + kTable * kBlock);
-  for (uint32_t i = threadIdx.x; i < P.prog_words; i += kBlock) prog[i] = P.prog[i];
+  uint2* stage_base = tbl_base + K::T * K::B;
+  uint32_t* q_base = reinterpret_cast<uint32_t*>(stage_base + K::R * K::B);
+  uint32_t* pre = q_base + K::Q * K::B;  // [B + 1] record offsets of the lanes in the block
+  uint32_t* cis = pre + K::B + 1;        // [B] command index of each lane
+  for (uint32_t i = threadIdx.x; i < P.prog_words; i += K::B) prog[i] = P.prog[i];
   __syncthreads();
 
-  const uint32_t lane_id = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t my_nrec = 0, my_ci = 0;
+  const uint32_t lane_id = blockIdx.x * K::B + threadIdx.x;
   uint32_t n_rec = 0, n_trans = 0, n_comp = 0, n_keys = 0, n_fb = 0, n_cmd = 0;
   if (lane_id < P.n_launch) {
     const uint32_t ci = P.order ? P.order[lane_id] : lane_id;
@@ -554,12 +603,14 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     const uint32_t doc_begin = cw.z;
     const uint32_t N = P.st.n;
 
-    Lane L;
+    Lane<K> L;
     L.tbl = tbl_base + threadIdx.x;
     L.q = q_base + threadIdx.x;
-    // wave-interleaved record slots: the 64 commands of a group of 64 write record j side by side,
-    // so each emit of a wave is one coalesced 512-byte store
+    L.stage = stage_base + threadIdx.x;
+    // overflow rows (j >= R) are wave-interleaved by command: each emit of a wave is one
+    // coalesced 512-byte store
     L.rec = P.rec + ((size_t)(ci >> 6) * P.rec_cap << 6) + (ci & 63);
+    my_ci = ci;
     L.rec_cap = P.rec_cap;
     L.nrec = 0;
     L.fail = 0;
@@ -605,8 +656,9 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
       L.pi_child = L.pi_asf = 0;
     } else if (L.proc != NONE) {
       // load the waiting instance: element-instance slots -> LDS table, variables, join counters
-      for (uint32_t s = 0; s < nslots0 && s < (uint32_t)kSlots; ++s)
-        L.tbl[s * kBlock] = P.st.slots[(size_t)s * N + inst];
+      if (nslots0 > (uint32_t)K::T) set_fail(L, FB_TABLE);
+      for (uint32_t s = 0; s < nslots0 && s < (uint32_t)K::T; ++s)
+        L.tbl[s * K::B] = P.st.slots[(size_t)s * N + inst];
       L.nt = (int)nslots0;
       L.nvars = (int)nvars0;
 #pragma unroll
@@ -644,13 +696,13 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
       if (t < 0) {
         emit(L, kRejectBit | C_JOB_COMPLETE, ref, NONE, NONE, ZBHIP_REASON_JOB_NOT_FOUND);
       } else {
-        uint2 e = L.tbl[t * kBlock];
+        uint2 e = L.tbl[t * K::B];
         const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
         emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
         // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
         e.y &= ~(1u << 24);
         if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
-        L.tbl[t * kBlock] = e;
+        L.tbl[t * K::B] = e;
         if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) {  // afterAccept
           uint32_t pe = new_key(L);  // EventTriggerBehavior.triggeringProcessEvent
           emit(L, C_PE_TRIGGERING, pe, task_key, task_elem);
@@ -666,7 +718,7 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
 
     // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
     while (L.qh < L.qt && !L.fail) {
-      const uint32_t entry = L.q[(L.qh % kQueue) * kBlock];
+      const uint32_t entry = L.q[(L.qh % K::Q) * K::B];
       ++L.qh;
       process_pi(L, entry);
       ++L.processed;
@@ -676,14 +728,14 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     uint32_t ns = 0;
     if (!L.fail && L.pi_live) {
       for (int t = 0; t < L.nt; ++t)
-        if (L.tbl[t * kBlock].x != 0xFFFFFFFFu) ++ns;
+        if (L.tbl[t * K::B].x != 0xFFFFFFFFu) ++ns;
       if (ns > (uint32_t)kSlots) set_fail(L, FB_SLOTS);
     }
     if (!L.fail) {
       if (L.pi_live) {
         uint32_t s = 0;
         for (int t = 0; t < L.nt; ++t) {
-          uint2 e = L.tbl[t * kBlock];
+          uint2 e = L.tbl[t * K::B];
           if (e.x != 0xFFFFFFFFu) P.st.slots[(size_t)(s++) * N + inst] = e;
         }
 #pragma unroll
@@ -713,6 +765,7 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
       P.cmd_hdr[ci] = make_uint2(L.nrec | ((uint32_t)(uint16_t)(L.next_ord - L.first_ord) << 16),
                                  L.first_ord | ((uint32_t)ST_OK << 16));
       n_rec = L.nrec;
+      my_nrec = L.nrec;
       n_trans = L.transitions;
       n_comp = L.completed;
       n_keys = (uint16_t)(L.next_ord - L.first_ord);
@@ -722,9 +775,48 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     }
     n_cmd = 1;
   }
-  // per-workgroup statistics: wave64 reduction, then the 4 waves through LDS; one plain add per
-  // counter into this workgroup's own row (no global-atomic hot spot: rows are reduced by
-  // k_scan_sums).
+  // ---- wavefront scan compaction: the block's records go out contiguously, once ----
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t inc = my_nrec;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(inc, off);
+    if (lane >= (uint32_t)off) inc += o;
+  }
+  __shared__ uint32_t wsum[K::B / 64];
+  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+  cis[threadIdx.x] = my_ci;
+  __syncthreads();
+  uint32_t wbase = 0;
+#pragma unroll
+  for (int w = 0; w < K::B / 64; ++w)
+    if (w < (int)(threadIdx.x >> 6)) wbase += wsum[w];
+  pre[threadIdx.x] = wbase + inc - my_nrec;
+  if (threadIdx.x == K::B - 1) pre[K::B] = wbase + inc;
+  __syncthreads();
+  const uint32_t total = pre[K::B];
+  uint2* out = P.out + (size_t)(P.region_base + blockIdx.x) * K::B * P.rec_cap;
+  for (uint32_t o = threadIdx.x; o < total; o += K::B) {
+    uint32_t lo = 0, hi = K::B;  // the lane whose records cover o: largest l with pre[l] <= o
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= o) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t j = o - pre[lo];
+    uint2 r;
+    if (j < (uint32_t)K::R) {
+      r = stage_base[j * K::B + lo];
+    } else {
+      const uint32_t c = cis[lo];
+      r = P.rec[(((size_t)(c >> 6) * P.rec_cap + j) << 6) + (c & 63)];
+    }
+    out[o] = r;
+  }
+  if (threadIdx.x == 0) P.region_total[P.region_base + blockIdx.x] = total;
+
+  // ---- statistics: wave64 reduction, waves through LDS, one add per counter into one of 64
+  // spread rows (non-returning atomics, no hot line) ----
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     n_rec += __shfl_xor(n_rec, off);
@@ -734,8 +826,8 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
     n_fb += __shfl_xor(n_fb, off);
     n_cmd += __shfl_xor(n_cmd, off);
   }
-  __shared__ uint32_t wstat[kBlock / 64][8];
-  if ((threadIdx.x & 63) == 0) {
+  __shared__ uint32_t wstat[K::B / 64][8];
+  if (lane == 0) {
     uint32_t* w = wstat[threadIdx.x >> 6];
     w[0] = n_rec; w[1] = n_trans; w[2] = n_comp; w[3] = n_keys; w[4] = n_fb; w[5] = n_cmd;
   }
@@ -743,13 +835,13 @@ __global__ __launch_bounds__(kBlock) void k_step(StepParams P) {
   if (threadIdx.x < 6) {
     uint32_t sum = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) sum += wstat[w][threadIdx.x];
-    if (sum) atomicAdd(&P.blk_stats[(size_t)blockIdx.x * 8 + threadIdx.x], sum);  // own row: uncontended
+    for (int w = 0; w < K::B / 64; ++w) sum += wstat[w][threadIdx.x];
+    if (sum) atomicAdd(&P.stats[(blockIdx.x & 63) * 8 + threadIdx.x], (unsigned long long)sum);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// compaction: per-block record totals -> exclusive scan -> ordered copy into the append buffer
+// drain path (not in the hot loop): gather the workgroup regions into one contiguous buffer
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const uint32_t lane = threadIdx.x & 63;
@@ -761,126 +853,73 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(kBlock) void k_block_sums(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum) {
-  __shared__ uint32_t ws[kBlock / 64];
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t v = i < n ? (cmd_hdr[i].x & 0xFFFF) : 0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t s = 0;
-    for (int w = 0; w < kBlock / 64; ++w) s += ws[w];
-    bsum[blockIdx.x] = s;
-  }
-}
-
-// single workgroup: exclusive scan of the block sums (64-bit total)
-__global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* bsum, uint32_t nb, unsigned long long* total,
-                                                   const uint32_t* blk_stats, uint32_t n_blk,
-                                                   unsigned long long* counters) {
-  __shared__ uint32_t ws[16];
-  __shared__ uint32_t carry;
-  __shared__ unsigned long long cs[16][6];
-  {  // reduce the per-workgroup statistics rows of k_step
-    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
-    for (uint32_t b = threadIdx.x; b < n_blk; b += 1024)
-#pragma unroll
-      for (int k = 0; k < 6; ++k) c[k] += blk_stats[(size_t)b * 8 + k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) c[k] += __shfl_xor(c[k], off);
-      if ((threadIdx.x & 63) == 0) cs[threadIdx.x >> 6][k] = c[k];
-    }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-      unsigned long long t = 0;
-      for (int w = 0; w < 16; ++w) t += cs[w][threadIdx.x];
-      counters[threadIdx.x] = t;
-    }
-  }
+// single workgroup: exclusive scan of the region totals (64-bit total)
+__global__ __launch_bounds__(1024) void k_scan_regions(const uint32_t* tot, uint32_t nr, unsigned long long* off,
+                                                      unsigned long long* total) {
+  __shared__ unsigned long long ws[16];
+  __shared__ unsigned long long carry;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
-  for (uint32_t base = 0; base < nb; base += 1024) {
+  for (uint32_t base = 0; base < nr; base += 1024) {
     const uint32_t i = base + threadIdx.x;
-    const uint32_t v = i < nb ? bsum[i] : 0;
-    uint32_t inc = wave_incl_scan(v);
+    const uint32_t v = i < nr ? tot[i] : 0;
+    const uint32_t inc = wave_incl_scan(v);
     if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
     __syncthreads();
-    if (threadIdx.x < 64) {
-      uint32_t x = threadIdx.x < 16 ? ws[threadIdx.x] : 0;
-      uint32_t xi = wave_incl_scan(x);
-      if (threadIdx.x < 16) ws[threadIdx.x] = xi - x;
-    }
+    unsigned long long wb = 0;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wb += ws[w];
+    const unsigned long long c = carry;
+    if (i < nr) off[i] = c + wb + inc - v;
     __syncthreads();
-    const uint32_t c = carry;
-    const uint32_t excl = c + ws[threadIdx.x >> 6] + inc - v;
-    if (i < nb) bsum[i] = excl;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry = excl + v;
+    if (threadIdx.x == 1023) carry = c + wb + inc;
     __syncthreads();
   }
   if (threadIdx.x == 0) *total = carry;
 }
 
-// Block b owns commands [256 b, 256 b + 256): it scans their record counts into LDS and then all
-// 256 lanes copy the block's records together, lane l taking output records l, l + 256, ...
-// (binary search over the LDS prefix finds the source command): every store is coalesced and
-// the loads walk each command's slot contiguously.
-__global__ __launch_bounds__(kBlock) void k_compact(const uint2* cmd_hdr, uint32_t n, const uint32_t* bsum,
-                                                    const uint2* rec, uint32_t rec_cap, uint2* out) {
-  __shared__ uint32_t ws[kBlock / 64];
-  __shared__ uint32_t pre[kBlock + 1];
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t v = i < n ? (cmd_hdr[i].x & 0xFFFF) : 0;
-  const uint32_t inc = wave_incl_scan(v);
-  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
-  __syncthreads();
-  uint32_t wbase = 0;
-  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += ws[w];
-  pre[threadIdx.x] = wbase + inc - v;
-  if (threadIdx.x == kBlock - 1) pre[kBlock] = wbase + inc;
-  __syncthreads();
-  const uint32_t total = pre[kBlock];
-  const uint32_t base = bsum[blockIdx.x];
-  const uint2* src = rec + (size_t)blockIdx.x * kBlock * rec_cap;  // 4 groups of 64 commands
-  for (uint32_t o = threadIdx.x; o < total; o += kBlock) {
-    uint32_t lo = 0, hi = kBlock;  // largest c with pre[c] <= o
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (pre[mid] <= o) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t j = o - pre[lo];
-    out[base + o] = src[(((size_t)(lo >> 6) * rec_cap + j) << 6) + (lo & 63)];
-  }
+template <int B>
+__global__ __launch_bounds__(256) void k_gather(const uint2* regions, const uint32_t* tot,
+                                                const unsigned long long* off, uint32_t rec_cap, uint2* out) {
+  const uint32_t g = blockIdx.x;
+  const uint32_t n = tot[g];
+  const uint2* src = regions + (size_t)g * B * rec_cap;
+  uint2* dst = out + off[g];
+  for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------------------------
 // launch wrappers (host)
 // ---------------------------------------------------------------------------------------------
-size_t step_lds_bytes(uint32_t prog_words) {
-  return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)kTable * kBlock * sizeof(uint2) +
-         (size_t)kQueue * kBlock * sizeof(uint32_t);
+template <class K>
+static size_t lds_bytes(uint32_t prog_words) {
+  return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::T * K::B * sizeof(uint2) +
+         (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t) +
+         (size_t)(2 * K::B + 1) * sizeof(uint32_t);
 }
 
-hipError_t launch_step(const StepParams& P, hipStream_t s) {
+uint32_t step_block(int variant) { return variant ? KGeneric::B : KSimple::B; }
+
+size_t step_lds_bytes(int variant, uint32_t prog_words) {
+  return variant ? lds_bytes<KGeneric>(prog_words) : lds_bytes<KSimple>(prog_words);
+}
+
+hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
   if (P.n_launch == 0) return hipSuccess;
-  const uint32_t grid = (P.n_launch + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_step, dim3(grid), dim3(kBlock), step_lds_bytes(P.prog_words), s, P);
+  if (variant) {
+    const uint32_t grid = (P.n_launch + KGeneric::B - 1) / KGeneric::B;
+    hipLaunchKernelGGL(k_step<KGeneric>, dim3(grid), dim3(KGeneric::B), lds_bytes<KGeneric>(P.prog_words), s, P);
+  } else {
+    const uint32_t grid = (P.n_launch + KSimple::B - 1) / KSimple::B;
+    hipLaunchKernelGGL(k_step<KSimple>, dim3(grid), dim3(KSimple::B), lds_bytes<KSimple>(P.prog_words), s, P);
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_compact(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum, const uint2* rec, uint32_t rec_cap,
-                          uint2* out, unsigned long long* total, const uint32_t* blk_stats, uint32_t n_blk,
-                          unsigned long long* counters, hipStream_t s) {
-  const uint32_t nb = (n + kBlock - 1) / kBlock;
-  if (n) hipLaunchKernelGGL(k_block_sums, dim3(nb), dim3(kBlock), 0, s, cmd_hdr, n, bsum);
-  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, s, bsum, nb, total, blk_stats, n_blk, counters);
-  if (n == 0) return hipGetLastError();
-  hipLaunchKernelGGL(k_compact, dim3(nb), dim3(kBlock), 0, s, cmd_hdr, n, bsum, rec, rec_cap, out);
+hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
+                         uint32_t rec_cap, uint2* out, unsigned long long* total, hipStream_t s) {
+  static_assert(KSimple::B == KGeneric::B, "one region geometry");
+  hipLaunchKernelGGL(k_scan_regions, dim3(1), dim3(1024), 0, s, tot, n_regions, off, total);
+  if (n_regions) hipLaunchKernelGGL(k_gather<KSimple::B>, dim3(n_regions), dim3(256), 0, s, regions, tot, off, rec_cap, out);
   return hipGetLastError();
 }
 

@@ -17,11 +17,13 @@
 #include "zb_internal.h"
 
 namespace zb {
-size_t step_lds_bytes(uint32_t prog_words);
-hipError_t launch_step(const StepParams& P, hipStream_t s);
-hipError_t launch_compact(const uint2* cmd_hdr, uint32_t n, uint32_t* bsum, const uint2* rec, uint32_t rec_cap,
-                          uint2* out, unsigned long long* total, const uint32_t* blk_stats, uint32_t n_blk,
-                          unsigned long long* counters, hipStream_t s);
+uint32_t step_block(int variant);
+size_t step_lds_bytes(int variant, uint32_t prog_words);
+hipError_t launch_step(int variant, const StepParams& P, hipStream_t s);
+hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
+                         uint32_t rec_cap, uint2* out, unsigned long long* total, hipStream_t s);
+constexpr uint32_t kRegionBlock = 128;  // k_step workgroup size of both variants
+constexpr uint32_t kExtraRegions = 64;  // regions for the extra workgroups of multi-round windows
 }  // namespace zb
 
 using namespace zb;
@@ -89,10 +91,15 @@ struct zbhip_handle {
   uint32_t* d_order = nullptr;
   uint2* d_rec = nullptr;
   uint2* d_cmd_hdr = nullptr;
-  uint32_t* d_bsum = nullptr;
-  uint2* d_out = nullptr;
-  unsigned long long* d_counters = nullptr;  // [0..5] + [6] compact total
-  uint32_t* d_blk_stats = nullptr;           // [max grid][8]
+  uint2* d_regions = nullptr;                // [regions][128 * rec_cap] per-workgroup record regions
+  uint32_t* d_region_total = nullptr;        // [regions]
+  unsigned long long* d_region_off = nullptr;// [regions] (drain path)
+  unsigned long long* d_stats = nullptr;     // [64][8] spread accumulators + [512] gather total
+  uint32_t regions_cap = 0;
+  int variant = 0;                           // 0 = KSimple, 1 = KGeneric
+  std::vector<std::pair<uint32_t, uint32_t>> launches;  // (region_base, first position in order) per launch
+  std::vector<hipEvent_t> tev;               // timing events (pairs) since the last stats reset
+  size_t tev_used = 0;
   uint32_t rec_cap = 64;
   size_t rec_slots = 0;  // commands the record buffer is sized for
 
@@ -124,6 +131,9 @@ struct zbhip_handle {
   std::vector<BatchRef> batches;
 
   zbhip_stats stats{};
+  bool stats_dirty = false;
+  uint32_t n_regions = 0;
+  unsigned long long key_counter_approx = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 
   long long key_of(uint32_t inst, uint32_t ord) const {
@@ -180,16 +190,18 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
             dalloc(&h->d_docs, h->cfg.max_doc_entries) == hipSuccess &&
             dalloc(&h->d_order, cfg->max_commands) == hipSuccess &&
             dalloc(&h->d_cmd_hdr, cfg->max_commands) == hipSuccess &&
-            dalloc(&h->d_bsum, (cfg->max_commands + kBlock - 1) / kBlock + 1) == hipSuccess &&
-            dalloc(&h->d_counters, 8) == hipSuccess &&
-            dalloc(&h->d_blk_stats, ((size_t)(cfg->max_commands + kBlock - 1) / kBlock) * 8) == hipSuccess &&
-            dalloc(&h->d_rec, (size_t)cfg->max_commands * h->rec_cap) == hipSuccess &&
-            dalloc(&h->d_out, (size_t)cfg->max_commands * h->rec_cap) == hipSuccess;
+            dalloc(&h->d_stats, 64 * 8 + 8) == hipSuccess &&
+            dalloc(&h->d_rec, ((size_t)cfg->max_commands + 64) * h->rec_cap) == hipSuccess;
+  h->regions_cap = (cfg->max_commands + kRegionBlock - 1) / kRegionBlock + kExtraRegions;
+  ok = ok && dalloc(&h->d_regions, (size_t)h->regions_cap * kRegionBlock * h->rec_cap) == hipSuccess &&
+       dalloc(&h->d_region_total, h->regions_cap) == hipSuccess &&
+       dalloc(&h->d_region_off, h->regions_cap) == hipSuccess;
   if (!ok) { zbhip_close(h); return ZBHIP_ENOMEM; }
   h->rec_slots = cfg->max_commands;
   // every slot starts free (proc = 0xFFFF); counters zero
   if (hipMemsetAsync(h->st.hdr, 0xFF, N * sizeof(uint4), h->stream) != hipSuccess ||
       hipMemsetAsync(h->st.join, 0, N * kJoinWords * sizeof(uint32_t), h->stream) != hipSuccess ||
+      hipMemsetAsync(h->d_stats, 0, (64 * 8 + 8) * sizeof(unsigned long long), h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
     zbhip_close(h);
     return ZBHIP_EDEVICE;
@@ -212,10 +224,11 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_order);
   (void)hipFree(h->d_rec);
   (void)hipFree(h->d_cmd_hdr);
-  (void)hipFree(h->d_bsum);
-  (void)hipFree(h->d_out);
-  (void)hipFree(h->d_counters);
-  (void)hipFree(h->d_blk_stats);
+  (void)hipFree(h->d_regions);
+  (void)hipFree(h->d_region_total);
+  (void)hipFree(h->d_region_off);
+  (void)hipFree(h->d_stats);
+  for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -331,10 +344,21 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         P.code[i].arg = (uint32_t)id;
       }
   }
+  // kernel variant: one token per instance at a time (no parallel gateway, no multi-outgoing
+  // node other than an exclusive gateway) fits the small register/LDS configuration
+  bool generic = false;
+  for (auto& e : P.els) {
+    if (e.element_type == ZBHIP_EL_PARALLEL_GATEWAY) generic = true;
+    if (e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.out_count > 1)
+      generic = true;
+  }
+  const int old_variant = h->variant;
+  if (generic) h->variant = 1;
   h->procs.push_back(std::move(P));
   int rc = rebuild_program(h);
   if (rc != ZBHIP_OK) {
     h->procs.pop_back();
+    h->variant = old_variant;
     return rc;
   }
   if (idx_out) *idx_out = (uint32_t)h->procs.size() - 1;
@@ -431,15 +455,28 @@ int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n
   return ZBHIP_OK;
 }
 
+static hipEvent_t next_event(zbhip_handle* h) {
+  if (h->tev_used == h->tev.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    h->tev.push_back(e);
+  }
+  return h->tev[h->tev_used++];
+}
+
 int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (!h) return ZBHIP_EINVAL;
   if (h->ran) return ZBHIP_ESTATE;
   if (h->procs.empty()) return ZBHIP_ESTATE;
   const bool timed = flags & ZBHIP_RUN_TIMED;
   const bool want = !(flags & ZBHIP_RUN_NO_RESULTS);
+  const bool accumulate = flags & ZBHIP_RUN_ACCUMULATE;
   const uint32_t n = (uint32_t)h->n_cmds;
-  const uint32_t n_blk = (n + kBlock - 1) / kBlock;
-  if (n_blk) HIPCHK(hipMemsetAsync(h->d_blk_stats, 0, (size_t)n_blk * 8 * sizeof(uint32_t), h->stream));
+  const uint32_t B = step_block(h->variant);
+  if (!accumulate) {
+    HIPCHK(hipMemsetAsync(h->d_stats, 0, 64 * 8 * sizeof(unsigned long long), h->stream));
+    h->tev_used = 0;
+  }
 
   StepParams P{};
   P.cmds = h->external ? h->ext_cmds : h->d_cmds;
@@ -451,93 +488,101 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.st = h->st;
   P.rec = h->d_rec;
   P.rec_cap = h->rec_cap;
+  P.out = h->d_regions;
+  P.region_total = h->d_region_total;
   P.cmd_hdr = h->d_cmd_hdr;
-  P.blk_stats = h->d_blk_stats;
+  P.stats = h->d_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
 
-  uint32_t launches = 0;
-  if (timed) HIPCHK(hipEventRecord(h->ev[0], h->stream));
+  // launches: one per round (commands of one instance are serialised in log order)
+  h->launches.clear();
+  std::vector<std::pair<uint32_t, uint32_t>> spans;  // (first position, count)
   if (h->round_begin.empty()) {
-    P.order = nullptr;
-    P.n_launch = n;
-    HIPCHK(launch_step(P, h->stream));
-    launches = n ? 1 : 0;
+    if (n) spans.push_back({0, n});
   } else {
-    for (size_t r = 0; r + 1 < h->round_begin.size(); ++r) {
-      P.order = h->d_order + h->round_begin[r];
-      P.n_launch = h->round_begin[r + 1] - h->round_begin[r];
-      HIPCHK(launch_step(P, h->stream));
-      ++launches;
-    }
+    for (size_t r = 0; r + 1 < h->round_begin.size(); ++r)
+      spans.push_back({h->round_begin[r], h->round_begin[r + 1] - h->round_begin[r]});
   }
-  if (timed) HIPCHK(hipEventRecord(h->ev[1], h->stream));
-  HIPCHK(launch_compact(h->d_cmd_hdr, n, h->d_bsum, h->d_rec, h->rec_cap, h->d_out, h->d_counters + 6,
-                        h->d_blk_stats, n_blk, h->d_counters, h->stream));
-  if (timed) HIPCHK(hipEventRecord(h->ev[2], h->stream));
-
-  unsigned long long cnt[8] = {0};
-  HIPCHK(hipMemcpyAsync(cnt, h->d_counters, sizeof cnt, hipMemcpyDeviceToHost, h->stream));
-  if (want) {
-    h->h_hdr.resize(n);
-    if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
+  uint32_t region = 0;
+  for (auto& sp : spans) {
+    h->launches.push_back({region, sp.first});
+    region += (sp.second + B - 1) / B;
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
-  if (want) {
-    h->h_out.resize(cnt[6]);
-    if (cnt[6])
-      HIPCHK(hipMemcpy(h->h_out.data(), h->d_out, cnt[6] * sizeof(uint2), hipMemcpyDeviceToHost));
-  }
-  h->stats.commands = cnt[5];
-  h->stats.records = cnt[0];
-  h->stats.transitions = cnt[1];
-  h->stats.completed_instances = cnt[2];
-  h->stats.keys = cnt[3];
-  h->stats.fallback = cnt[4];
-  h->stats.launches = launches + (n ? 3 : 0);
-  h->stats.rounds = h->round_begin.empty() ? (n ? 1 : 0) : (uint32_t)h->round_begin.size() - 1;
+  if (region > h->regions_cap) return ZBHIP_ENOMEM;  // too many rounds for the region pool
+  hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timed) {
-    float a = 0, b = 0;
-    (void)hipEventElapsedTime(&a, h->ev[0], h->ev[1]);
-    (void)hipEventElapsedTime(&b, h->ev[1], h->ev[2]);
-    h->stats.step_ms = a;
-    h->stats.compact_ms = b;
+    e0 = next_event(h);
+    e1 = next_event(h);
+    if (!e0 || !e1) return ZBHIP_EDEVICE;
+    HIPCHK(hipEventRecord(e0, h->stream));
   }
-
-  // key relabelling bookkeeping, in log (source) order
-  if (!want || h->external) {
-    h->relabel_ok = false;
-    h->key_counter += (int64_t)cnt[3];
-  } else {
-    if (h->hist.size() < h->cfg.max_instances) {
-      h->hist.resize(h->cfg.max_instances);
-      h->inst_proc.resize(h->cfg.max_instances, NONE);
-    }
-    h->h_off.resize(n + 1);
-    uint64_t off = 0;
-    for (uint32_t c = 0; c < n; ++c) {
-      const uint2 hd = h->h_hdr[c];
-      const zbhip_command& cm = h->h_cmds[c];
-      h->h_off[c] = off;
-      const uint32_t nrec = hd.x & 0xFFFF, nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
-      off += nrec;
-      if (((hd.y >> 16) & 0xFF) != ST_OK) continue;
-      if (cm.kind == ZBHIP_CMD_CREATE) {
-        h->hist[cm.instance].clear();
-        h->inst_proc[cm.instance] = cm.ref;
-      }
-      if (nkeys) {
-        h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
-        h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys});
-      }
-      h->key_counter += nkeys;
-    }
-    h->h_off[n] = off;
-    h->results = true;
+  for (size_t l = 0; l < spans.size(); ++l) {
+    P.order = h->round_begin.empty() ? nullptr : h->d_order + spans[l].first;
+    P.n_launch = spans[l].second;
+    P.region_base = h->launches[l].first;
+    HIPCHK(launch_step(h->variant, P, h->stream));
   }
+  if (timed) HIPCHK(hipEventRecord(e1, h->stream));
+  h->stats.launches = (uint32_t)spans.size();
+  h->stats.rounds = (uint32_t)spans.size();
+  h->n_regions = region;
+  h->ran = true;
   h->drain_cmd = 0;
   h->drain_rec = 0;
-  h->ran = true;
-  return (int)cnt[5];
+  h->results = false;
+
+  if (!want || h->external) {
+    // benchmarking mode: nothing is copied back and nothing waits; keys are not relabelled
+    h->relabel_ok = false;
+    h->stats_dirty = true;
+    return (int)n;
+  }
+
+  // ---- results: headers + records gathered into log order (drain path, off the hot loop) ----
+  h->h_hdr.resize(n);
+  if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(launch_gather(h->d_regions, h->d_region_total, region, h->d_region_off, h->rec_cap, h->d_rec,
+                       h->d_stats + 64 * 8, h->stream));
+  unsigned long long total = 0;
+  HIPCHK(hipMemcpyAsync(&total, h->d_stats + 64 * 8, sizeof total, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->h_out.resize(total);
+  if (total) HIPCHK(hipMemcpy(h->h_out.data(), h->d_rec, total * sizeof(uint2), hipMemcpyDeviceToHost));
+  h->stats_dirty = true;
+
+  // record offset of every command: regions follow launch order, lanes follow the launch order
+  h->h_off.assign(n + 1, 0);
+  uint64_t off = 0;
+  for (auto& sp : spans)
+    for (uint32_t k = 0; k < sp.second; ++k) {
+      const uint32_t c = h->round_begin.empty() ? sp.first + k : h->h_order[sp.first + k];
+      h->h_off[c] = off;
+      off += h->h_hdr[c].x & 0xFFFF;
+    }
+  if (off != total) return ZBHIP_EDEVICE;
+
+  // key relabelling bookkeeping, in log (source) order
+  if (h->hist.size() < h->cfg.max_instances) {
+    h->hist.resize(h->cfg.max_instances);
+    h->inst_proc.resize(h->cfg.max_instances, NONE);
+  }
+  for (uint32_t c = 0; c < n; ++c) {
+    const uint2 hd = h->h_hdr[c];
+    const zbhip_command& cm = h->h_cmds[c];
+    const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
+    if (((hd.y >> 16) & 0xFF) != ST_OK) continue;
+    if (cm.kind == ZBHIP_CMD_CREATE) {
+      h->hist[cm.instance].clear();
+      h->inst_proc[cm.instance] = cm.ref;
+    }
+    if (nkeys) {
+      h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
+      h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys});
+    }
+    h->key_counter += nkeys;
+  }
+  h->results = true;
+  return (int)n;
 }
 
 int64_t zbhip_pending_records(zbhip_handle* h) {
@@ -547,6 +592,29 @@ int64_t zbhip_pending_records(zbhip_handle* h) {
 
 int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
   if (!h || !out) return ZBHIP_EINVAL;
+  if (h->stats_dirty) {
+    unsigned long long rows[64 * 8];
+    HIPCHK(hipMemcpyAsync(rows, h->d_stats, sizeof rows, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    unsigned long long c[8] = {0};
+    for (int r = 0; r < 64; ++r)
+      for (int k = 0; k < 8; ++k) c[k] += rows[r * 8 + k];
+    h->stats.records = c[0];
+    h->stats.transitions = c[1];
+    h->stats.completed_instances = c[2];
+    h->stats.keys = c[3];
+    h->stats.fallback = c[4];
+    h->stats.commands = c[5];
+    double ms = 0;
+    for (size_t i = 0; i + 1 < h->tev_used; i += 2) {
+      float a = 0;
+      if (hipEventElapsedTime(&a, h->tev[i], h->tev[i + 1]) == hipSuccess) ms += a;
+    }
+    h->stats.step_ms = ms;
+    h->stats.compact_ms = 0;  // compaction is fused into k_step
+    if (!h->relabel_ok) h->key_counter_approx = c[3];
+    h->stats_dirty = false;
+  }
   *out = h->stats;
   return ZBHIP_OK;
 }

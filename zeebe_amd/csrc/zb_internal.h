@@ -92,10 +92,14 @@ struct StepParams {
   uint32_t prog_words;
   uint32_t n_procs;
   DevState st;
-  uint2* rec;                 // [n_cmds][rec_cap] record slots, indexed by command index
-  uint32_t rec_cap;
+  uint2* rec;                 // overflow record rows (j >= R), wave-interleaved by command index
+  uint32_t rec_cap;           // max records per batch
+  uint2* out;                 // workgroup regions: region g holds its block's records contiguously
+  uint32_t region_base;       // region of this launch's workgroup 0
+  uint32_t* region_total;     // [regions] records in each region
   uint2* cmd_hdr;             // [n_cmds]
-  uint32_t* blk_stats;        // [grid][8] per-workgroup: records, transitions, completed, keys, fallback, commands
+  unsigned long long* stats;  // [64][8] spread accumulators: records, transitions, completed, keys,
+                              // fallback, commands
   int32_t max_cmds_in_batch;
 };
 
