@@ -268,7 +268,7 @@ static int rebuild_program(zbhip_handle* h) {
     const uint32_t out_off = 8 + 4 * n_el;
     const uint32_t cond_off = out_off + ((uint32_t)P.out.size() + 1) / 2;
     const uint32_t n_cond = P.cond_begin.empty() ? 0 : (uint32_t)P.cond_begin.size() - 1;
-    const uint32_t code_off = cond_off + n_cond;
+    const uint32_t code_off = (cond_off + n_cond + 3) & ~3u;  // 16-byte aligned instructions (uint4 loads)
     const uint32_t total = (code_off + 4 * (uint32_t)P.code.size() + 3) & ~3u;
     prog.resize(base + total, 0);
     uint32_t* pb = prog.data() + base;

@@ -71,7 +71,7 @@ enum : uint8_t {
 //                            w3 = join_slot | id << 16
 //   p[out_off]  u16 outgoing flows (two per word)
 //   p[cond_off] u32 first instruction of each condition
-//   p[code_off] instructions: op, arg, literal_lo, literal_hi
+//   p[code_off] instructions (16-byte aligned): op, arg, literal_lo, literal_hi
 struct DevState {
   uint4* hdr;        // [n] x = proc | next_ord << 16; y = pi_state | nslots << 8 | nvars << 16 | pi_live << 24
                      //     z = pi_child | pi_asf << 16; w = 0
