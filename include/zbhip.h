@@ -301,6 +301,10 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx);
  * subset, batch-limit overflow, capacity).  Their state was left untouched. */
 int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_out);
 
+/* Status of command i of the last run: 0 = processed, 1 = needs the fallback path; *reason is
+ * the device fallback code (FB_* in zeebe_amd/csrc/zb_internal.h), 0 when processed. */
+int zbhip_command_status(zbhip_handle* h, size_t i, uint32_t* status, uint32_t* reason);
+
 /* Maps a drained (relabelled) key back to (instance, key ordinal) for building
  * follow-up commands (e.g. JOB:COMPLETE).  Returns ZBHIP_EINVAL if unknown. */
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal);

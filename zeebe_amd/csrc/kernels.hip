@@ -164,7 +164,7 @@ __device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, b
   // otherwise the platform writes it to the log unprocessed -> outside the device subset.
   if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
   if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
-  L.q[(L.qt % kQueue) * K::B] = elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
+  L.q[(L.qt % K::Q) * K::B] = elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
   ++L.qt;
 }
 

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -354,6 +355,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   }
   const int old_variant = h->variant;
   if (generic) h->variant = 1;
+  if (const char* fv = getenv("ZBHIP_FORCE_VARIANT")) h->variant = atoi(fv) ? 1 : 0;
   h->procs.push_back(std::move(P));
   int rc = rebuild_program(h);
   if (rc != ZBHIP_OK) {
@@ -741,6 +743,15 @@ int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t
   if (v >= it->base + it->nkeys) return ZBHIP_EINVAL;
   *instance = it->inst;
   *ordinal = (uint16_t)(it->first_ord + (v - it->base));
+  return ZBHIP_OK;
+}
+
+int zbhip_command_status(zbhip_handle* h, size_t i, uint32_t* status, uint32_t* reason) {
+  if (!h || !status || !reason) return ZBHIP_EINVAL;
+  if (!h->results) return ZBHIP_ESTATE;
+  if (i >= h->n_cmds) return ZBHIP_EINVAL;
+  *status = (h->h_hdr[i].y >> 16) & 0xFF;
+  *reason = h->h_hdr[i].y >> 24;
   return ZBHIP_OK;
 }
 

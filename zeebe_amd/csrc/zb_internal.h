@@ -6,9 +6,7 @@
 
 namespace zb {
 
-constexpr int kBlock = 256;        // threads per workgroup (4 wave64)
-constexpr int kTable = 12;         // live element-instance entries per lane during a batch (LDS)
-constexpr int kQueue = 16;         // pending follow-up commands per lane (LDS ring)
+// workgroup size and per-lane LDS capacities are per kernel variant (KCfg in kernels.hip)
 constexpr int kSlots = 8;          // persistent element-instance slots per process instance (HBM)
 constexpr int kVars = 4;           // variables per process instance (HBM)
 constexpr int kJoinWords = 4;      // 16 x u8 taken-sequence-flow counters per instance (HBM)

@@ -146,6 +146,15 @@ class Partition:
         check(self.L.zbhip_fallback(self.h, buf, n.value, C.byref(n)))
         return list(buf[: n.value])
 
+    FALLBACK_REASONS = {1: "queue", 2: "table", 3: "records", 4: "keys", 5: "batch-limit", 6: "feel", 7: "vars",
+                        8: "slot-in-use", 9: "no-condition", 10: "unsupported", 11: "doc", 12: "join",
+                        13: "slots", 14: "bad-process"}
+
+    def command_status(self, i):
+        st, rs = C.c_uint32(), C.c_uint32()
+        check(self.L.zbhip_command_status(self.h, i, C.byref(st), C.byref(rs)))
+        return st.value, self.FALLBACK_REASONS.get(rs.value, rs.value)
+
     def resolve_key(self, key):
         inst, ordv = C.c_uint32(), C.c_uint16()
         check(self.L.zbhip_resolve_key(self.h, key, C.byref(inst), C.byref(ordv)), "unknown key %d" % key)

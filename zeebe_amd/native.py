@@ -18,7 +18,7 @@ ERRORS = {-1: "ZBHIP_EINVAL", -2: "ZBHIP_ENOMEM", -3: "ZBHIP_EDEVICE", -4: "ZBHI
 SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", "zbhip_deploy", "zbhip_intern",
            "zbhip_string", "zbhip_name", "zbhip_submit", "zbhip_submit_device", "zbhip_run", "zbhip_drain",
            "zbhip_pending_records", "zbhip_get_stats", "zbhip_export_state", "zbhip_fallback",
-           "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info"]
+           "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info", "zbhip_command_status"]
 
 
 class ZbhipError(RuntimeError):
@@ -63,6 +63,7 @@ def load():
     L.zbhip_fallback.argtypes = [vp, C.POINTER(u32), sz, C.POINTER(sz)]
     L.zbhip_resolve_key.argtypes = [vp, i64, C.POINTER(u32), C.POINTER(C.c_uint16)]
     L.zbhip_rejection_reason.argtypes = [vp, C.POINTER(abi.Record), C.c_char_p, sz]
+    L.zbhip_command_status.argtypes = [vp, sz, C.POINTER(u32), C.POINTER(u32)]
     L.zbhip_build_info.argtypes = []
     L.zbhip_build_info.restype = C.c_char_p
     _lib = L
