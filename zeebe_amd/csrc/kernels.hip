@@ -29,6 +29,8 @@
 // an ordered copy of every batch's records into one contiguous append buffer (log order).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "zb_internal.h"
 
 namespace zb {
@@ -38,12 +40,15 @@ namespace zb {
 // ---------------------------------------------------------------------------------------------
 // Kernel configuration: workgroup size B, LDS element-instance table entries T, LDS queue
 // entries Q, records staged in LDS per lane R (rows j >= R go to the global overflow rows).
-template <int B_, int T_, int Q_, int R_>
+// F selects the flush: 0 = the workgroup's lanes copy output record o = l, l + B, ... (binary
+// search of the lane prefix in LDS, coalesced stores); 1 = every lane stores its own records at
+// its prefix (no search; the workgroup region's lines are completed within a few stores).
+template <int B_, int T_, int Q_, int R_, int F_>
 struct KCfg {
-  static constexpr int B = B_, T = T_, Q = Q_, R = R_;
+  static constexpr int B = B_, T = T_, Q = Q_, R = R_, F = F_;
 };
-using KSimple = KCfg<128, 4, 4, 32>;    // processes without parallel gateways / multi-outgoing nodes
-using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
+using KSimple = KCfg<128, 4, 4, 16, 1>;   // processes without parallel gateways / multi-outgoing nodes
+using KGeneric = KCfg<128, 12, 16, 16, 1>; // everything else in the subset
 
 template <class K>
 struct Lane {
@@ -787,31 +792,41 @@ __global__ __launch_bounds__(K::B) void k_step(StepParams P) {
   if (lane == 63) wsum[threadIdx.x >> 6] = inc;
   cis[threadIdx.x] = my_ci;
   __syncthreads();
-  uint32_t wbase = 0;
+  uint32_t wbase = 0, total = 0;
 #pragma unroll
-  for (int w = 0; w < K::B / 64; ++w)
+  for (int w = 0; w < K::B / 64; ++w) {
     if (w < (int)(threadIdx.x >> 6)) wbase += wsum[w];
-  pre[threadIdx.x] = wbase + inc - my_nrec;
-  if (threadIdx.x == K::B - 1) pre[K::B] = wbase + inc;
-  __syncthreads();
-  const uint32_t total = pre[K::B];
+    total += wsum[w];
+  }
   uint2* out = P.out + (size_t)(P.region_base + blockIdx.x) * K::B * P.rec_cap;
-  for (uint32_t o = threadIdx.x; o < total; o += K::B) {
-    uint32_t lo = 0, hi = K::B;  // the lane whose records cover o: largest l with pre[l] <= o
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (pre[mid] <= o) lo = mid;
-      else hi = mid;
+  if constexpr (K::F == 1) {
+    const uint32_t my_off = wbase + inc - my_nrec;
+    for (uint32_t j = 0; j < my_nrec; ++j) {
+      const uint2 r = j < (uint32_t)K::R ? stage_base[j * K::B + threadIdx.x]
+                                         : P.rec[(((size_t)(my_ci >> 6) * P.rec_cap + j) << 6) + (my_ci & 63)];
+      out[my_off + j] = r;
     }
-    const uint32_t j = o - pre[lo];
-    uint2 r;
-    if (j < (uint32_t)K::R) {
-      r = stage_base[j * K::B + lo];
-    } else {
-      const uint32_t c = cis[lo];
-      r = P.rec[(((size_t)(c >> 6) * P.rec_cap + j) << 6) + (c & 63)];
+  } else {
+    pre[threadIdx.x] = wbase + inc - my_nrec;
+    if (threadIdx.x == K::B - 1) pre[K::B] = wbase + inc;
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < total; o += K::B) {
+      uint32_t lo = 0, hi = K::B;  // the lane whose records cover o: largest l with pre[l] <= o
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= o) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t j = o - pre[lo];
+      uint2 r;
+      if (j < (uint32_t)K::R) {
+        r = stage_base[j * K::B + lo];
+      } else {
+        const uint32_t c = cis[lo];
+        r = P.rec[(((size_t)(c >> 6) * P.rec_cap + j) << 6) + (c & 63)];
+      }
+      out[o] = r;
     }
-    out[o] = r;
   }
   if (threadIdx.x == 0) P.region_total[P.region_base + blockIdx.x] = total;
 
@@ -877,12 +892,12 @@ __global__ __launch_bounds__(1024) void k_scan_regions(const uint32_t* tot, uint
   if (threadIdx.x == 0) *total = carry;
 }
 
-template <int B>
+// region g starts at g * region_stride records (the workgroup size of the run x rec_cap)
 __global__ __launch_bounds__(256) void k_gather(const uint2* regions, const uint32_t* tot,
-                                                const unsigned long long* off, uint32_t rec_cap, uint2* out) {
+                                                const unsigned long long* off, size_t region_stride, uint2* out) {
   const uint32_t g = blockIdx.x;
   const uint32_t n = tot[g];
-  const uint2* src = regions + (size_t)g * B * rec_cap;
+  const uint2* src = regions + (size_t)g * region_stride;
   uint2* dst = out + off[g];
   for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
 }
@@ -897,7 +912,39 @@ static size_t lds_bytes(uint32_t prog_words) {
          (size_t)(2 * K::B + 1) * sizeof(uint32_t);
 }
 
-uint32_t step_block(int variant) { return variant ? KGeneric::B : KSimple::B; }
+// Tuning table: ZBHIP_KCFG=<i> selects an alternative configuration for the small variant.
+using KTune0 = KCfg<128, 4, 4, 32, 0>;
+using KTune1 = KCfg<128, 4, 4, 16, 0>;
+using KTune2 = KCfg<256, 4, 4, 16, 1>;
+using KTune3 = KCfg<64, 4, 4, 16, 1>;
+using KTune4 = KCfg<128, 4, 4, 8, 1>;
+
+static int tune_cfg() {
+  static int v = [] {
+    const char* e = getenv("ZBHIP_KCFG");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
+template <class K>
+static hipError_t launch_k(const StepParams& P, hipStream_t s) {
+  const uint32_t grid = (P.n_launch + K::B - 1) / K::B;
+  hipLaunchKernelGGL(k_step<K>, dim3(grid), dim3(K::B), lds_bytes<K>(P.prog_words), s, P);
+  return hipGetLastError();
+}
+
+uint32_t step_block(int variant) {
+  if (!variant) switch (tune_cfg()) {
+      case 0: return KTune0::B;
+      case 1: return KTune1::B;
+      case 2: return KTune2::B;
+      case 3: return KTune3::B;
+      case 4: return KTune4::B;
+      default: break;
+    }
+  return variant ? KGeneric::B : KSimple::B;
+}
 
 size_t step_lds_bytes(int variant, uint32_t prog_words) {
   return variant ? lds_bytes<KGeneric>(prog_words) : lds_bytes<KSimple>(prog_words);
@@ -905,21 +952,21 @@ size_t step_lds_bytes(int variant, uint32_t prog_words) {
 
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
   if (P.n_launch == 0) return hipSuccess;
-  if (variant) {
-    const uint32_t grid = (P.n_launch + KGeneric::B - 1) / KGeneric::B;
-    hipLaunchKernelGGL(k_step<KGeneric>, dim3(grid), dim3(KGeneric::B), lds_bytes<KGeneric>(P.prog_words), s, P);
-  } else {
-    const uint32_t grid = (P.n_launch + KSimple::B - 1) / KSimple::B;
-    hipLaunchKernelGGL(k_step<KSimple>, dim3(grid), dim3(KSimple::B), lds_bytes<KSimple>(P.prog_words), s, P);
+  if (variant) return launch_k<KGeneric>(P, s);
+  switch (tune_cfg()) {
+    case 0: return launch_k<KTune0>(P, s);
+    case 1: return launch_k<KTune1>(P, s);
+    case 2: return launch_k<KTune2>(P, s);
+    case 3: return launch_k<KTune3>(P, s);
+    case 4: return launch_k<KTune4>(P, s);
+    default: return launch_k<KSimple>(P, s);
   }
-  return hipGetLastError();
 }
 
 hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
-                         uint32_t rec_cap, uint2* out, unsigned long long* total, hipStream_t s) {
-  static_assert(KSimple::B == KGeneric::B, "one region geometry");
+                         size_t region_stride, uint2* out, unsigned long long* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_regions, dim3(1), dim3(1024), 0, s, tot, n_regions, off, total);
-  if (n_regions) hipLaunchKernelGGL(k_gather<KSimple::B>, dim3(n_regions), dim3(256), 0, s, regions, tot, off, rec_cap, out);
+  if (n_regions) hipLaunchKernelGGL(k_gather, dim3(n_regions), dim3(256), 0, s, regions, tot, off, region_stride, out);
   return hipGetLastError();
 }
 

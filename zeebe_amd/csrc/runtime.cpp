@@ -22,8 +22,7 @@ uint32_t step_block(int variant);
 size_t step_lds_bytes(int variant, uint32_t prog_words);
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s);
 hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
-                         uint32_t rec_cap, uint2* out, unsigned long long* total, hipStream_t s);
-constexpr uint32_t kRegionBlock = 128;  // k_step workgroup size of both variants
+                         size_t region_stride, uint2* out, unsigned long long* total, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;  // regions for the extra workgroups of multi-round windows
 }  // namespace zb
 
@@ -97,6 +96,7 @@ struct zbhip_handle {
   unsigned long long* d_region_off = nullptr;// [regions] (drain path)
   unsigned long long* d_stats = nullptr;     // [64][8] spread accumulators + [512] gather total
   uint32_t regions_cap = 0;
+  size_t region_records = 0;
   int variant = 0;                           // 0 = KSimple, 1 = KGeneric
   std::vector<std::pair<uint32_t, uint32_t>> launches;  // (region_base, first position in order) per launch
   std::vector<hipEvent_t> tev;               // timing events (pairs) since the last stats reset
@@ -193,8 +193,11 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
             dalloc(&h->d_cmd_hdr, cfg->max_commands) == hipSuccess &&
             dalloc(&h->d_stats, 64 * 8 + 8) == hipSuccess &&
             dalloc(&h->d_rec, ((size_t)cfg->max_commands + 64) * h->rec_cap) == hipSuccess;
-  h->regions_cap = (cfg->max_commands + kRegionBlock - 1) / kRegionBlock + kExtraRegions;
-  ok = ok && dalloc(&h->d_regions, (size_t)h->regions_cap * kRegionBlock * h->rec_cap) == hipSuccess &&
+  // region pool: every workgroup of a run owns (workgroup size) * rec_cap records; sized for a
+  // full window plus kExtraRegions partly filled workgroups of extra rounds (<= 256 lanes each)
+  h->region_records = ((size_t)cfg->max_commands + (size_t)kExtraRegions * 256) * h->rec_cap;
+  h->regions_cap = (cfg->max_commands + 63) / 64 + kExtraRegions;
+  ok = ok && dalloc(&h->d_regions, h->region_records) == hipSuccess &&
        dalloc(&h->d_region_total, h->regions_cap) == hipSuccess &&
        dalloc(&h->d_region_off, h->regions_cap) == hipSuccess;
   if (!ok) { zbhip_close(h); return ZBHIP_ENOMEM; }
@@ -510,7 +513,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     h->launches.push_back({region, sp.first});
     region += (sp.second + B - 1) / B;
   }
-  if (region > h->regions_cap) return ZBHIP_ENOMEM;  // too many rounds for the region pool
+  if (region > h->regions_cap || (size_t)region * B * h->rec_cap > h->region_records)
+    return ZBHIP_ENOMEM;  // too many rounds for the region pool
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timed) {
     e0 = next_event(h);
@@ -543,7 +547,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   // ---- results: headers + records gathered into log order (drain path, off the hot loop) ----
   h->h_hdr.resize(n);
   if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(launch_gather(h->d_regions, h->d_region_total, region, h->d_region_off, h->rec_cap, h->d_rec,
+  HIPCHK(launch_gather(h->d_regions, h->d_region_total, region, h->d_region_off, (size_t)B * h->rec_cap, h->d_rec,
                        h->d_stats + 64 * 8, h->stream));
   unsigned long long total = 0;
   HIPCHK(hipMemcpyAsync(&total, h->d_stats + 64 * 8, sizeof total, hipMemcpyDeviceToHost, h->stream));

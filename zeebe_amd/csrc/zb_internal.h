@@ -6,7 +6,8 @@
 
 namespace zb {
 
-// workgroup size and per-lane LDS capacities are per kernel variant (KCfg in kernels.hip)
+// workgroup size and per-lane LDS capacities are per kernel variant (KCfg in kernels.hip);
+// every workgroup owns one output region of (workgroup size) * rec_cap records
 constexpr int kSlots = 8;          // persistent element-instance slots per process instance (HBM)
 constexpr int kVars = 4;           // variables per process instance (HBM)
 constexpr int kJoinWords = 4;      // 16 x u8 taken-sequence-flow counters per instance (HBM)
