@@ -69,7 +69,7 @@ def main():
     ap.add_argument("--instances", type=int, default=0, help="override instances per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-instances", type=int, default=100_000, help="instances per CPU thread (bounded sample)")
+    ap.add_argument("--cpu-instances", type=int, default=300_000, help="instances per CPU thread (bounded sample)")
     args = ap.parse_args()
 
     import numpy as np
