@@ -25,10 +25,11 @@
 //   state/appliers/ProcessInstanceSequenceFlowTakenApplier.java:32-69, JobCreatedApplier.java:28-41,
 //   JobCompletedApplier.java:28-45, state/instance/DbElementInstanceState.java:135-344.
 //
-// k_block_sums / k_scan_sums / k_compact: exclusive scan of the per-command record counts and
-// an ordered copy of every batch's records into one contiguous append buffer (log order).
+// k_scan_regions / k_gather (drain path only): exclusive scan of the per-chunk record totals and
+// an ordered copy of every chunk's records into one contiguous append buffer.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 
 #include "zb_internal.h"
@@ -40,15 +41,17 @@ namespace zb {
 // ---------------------------------------------------------------------------------------------
 // Kernel configuration: workgroup size B, LDS element-instance table entries T, LDS queue
 // entries Q, records staged in LDS per lane R (rows j >= R go to the global overflow rows).
-// F selects the flush: 0 = the workgroup's lanes copy output record o = l, l + B, ... (binary
-// search of the lane prefix in LDS, coalesced stores); 1 = every lane stores its own records at
-// its prefix (no search; the workgroup region's lines are completed within a few stores).
-template <int B_, int T_, int Q_, int R_, int F_>
+// After the chunk's wavefront scan an owner map in LDS lets the workgroup store the chunk's
+// records contiguously with coalesced 16-byte writes.  (Measured alternatives, linear-10: every
+// lane storing its own records at its prefix scatters each store over ~40 cache lines; a
+// binary search of the lane prefix per record was slower still; B = 64 / 256 and R = 8 / 32
+// were 2-10 % slower.)
+template <int B_, int T_, int Q_, int R_>
 struct KCfg {
-  static constexpr int B = B_, T = T_, Q = Q_, R = R_, F = F_;
+  static constexpr int B = B_, T = T_, Q = Q_, R = R_;
 };
-using KSimple = KCfg<128, 4, 4, 16, 1>;   // processes without parallel gateways / multi-outgoing nodes
-using KGeneric = KCfg<128, 12, 16, 16, 1>; // everything else in the subset
+using KSimple = KCfg<128, 4, 4, 16>;   // processes without parallel gateways / multi-outgoing nodes
+using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
 
 template <class K>
 struct Lane {
@@ -582,6 +585,236 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
 // ---------------------------------------------------------------------------------------------
 // k_step
 // ---------------------------------------------------------------------------------------------
+// ---- instance rows of one command, fetched ahead of its chunk --------------------------------
+constexpr uint32_t kNoCmd = 0xFFFFFFFFu;
+
+template <class K>
+__device__ __forceinline__ uint32_t cmd_index(const StepParams& P, uint32_t chunk) {
+  const uint32_t lane_id = chunk * K::B + threadIdx.x;
+  if (lane_id >= P.n_launch) return kNoCmd;
+  return P.order ? P.order[lane_id] : lane_id;
+}
+__device__ __forceinline__ uint4 load_cmd(const StepParams& P, uint32_t ci) {
+  return ci != kNoCmd ? P.cmds[ci] : make_uint4(0, 0, 0, 0);
+}
+// header row, and the first element-instance slot of a waiting instance (a CREATE reads none)
+__device__ __forceinline__ void load_rows(const StepParams& P, uint32_t ci, const uint4& cw, uint4& h, uint2& s0) {
+  h = make_uint4(0xFFFFFFFFu, 0, 0, 0);
+  s0 = make_uint2(0xFFFFFFFFu, 0);
+  if (ci != kNoCmd && cw.x < P.st.n) {
+    h = P.st.hdr[cw.x];
+    if ((cw.y & 0xFF) != ZBHIP_CMD_CREATE) s0 = P.st.slots[cw.x];
+  }
+}
+
+// record j >= R of command ci: the wave-interleaved global overflow rows
+__device__ __forceinline__ uint2 overflow_row(const StepParams& P, uint32_t ci, uint32_t j) {
+  return P.rec[(((size_t)(ci >> 6) * P.rec_cap + j) << 6) + (ci & 63)];
+}
+
+struct Counters {
+  uint32_t rec, trans, comp, keys, fb, cmd;
+};
+
+// One command's whole batch on one lane; returns the number of records it staged.
+template <class K>
+__device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint32_t* prog, uint2* tbl_base,
+                                                uint2* stage_base, uint32_t* q_base, uint32_t ci, uint4 cw,
+                                                uint4 h, uint2 s0, Counters& acc) {
+  const uint32_t inst = cw.x;
+  const uint32_t kind = cw.y & 0xFF;
+  const uint32_t doc_count = (cw.y >> 8) & 0xFF;
+  const uint32_t ref = cw.y >> 16;
+  const uint32_t doc_begin = cw.z;
+  const uint32_t N = P.st.n;
+
+  Lane<K> L;
+  L.tbl = tbl_base + threadIdx.x;
+  L.q = q_base + threadIdx.x;
+  L.stage = stage_base + threadIdx.x;
+  // overflow rows (j >= R) are wave-interleaved by command: each emit of a wave is one
+  // coalesced 512-byte store
+  L.rec = P.rec + ((size_t)(ci >> 6) * P.rec_cap << 6) + (ci & 63);
+  L.rec_cap = P.rec_cap;
+  L.nrec = 0;
+  L.fail = 0;
+  L.transitions = 0;
+  L.completed = 0;
+  L.limit = P.max_cmds_in_batch;
+  L.processed = 0;
+  L.qh = L.qt = 0;
+  L.nt = 0;
+  L.trig_key = NONE;
+  L.docs = P.docs;
+  L.doc_begin = doc_begin;
+  L.doc_count = doc_count;
+  L.has_join = false;
+  L.jw0 = L.jw1 = L.jw2 = L.jw3 = 0;
+  L.nvars = 0;
+  L.vx0 = L.vx1 = L.vx2 = L.vx3 = 0xFFFFFFFFu;
+  L.vy0 = L.vy1 = L.vy2 = L.vy3 = 0;
+  L.vv0 = L.vv1 = L.vv2 = L.vv3 = 0;
+
+  const bool bad_cmd = inst >= N || (doc_count && (uint64_t)doc_begin + doc_count > P.n_docs);
+  if (bad_cmd) h = make_uint4(0xFFFFFFFFu, 0, 0, 0);
+  L.proc = h.x & 0xFFFF;
+  L.next_ord = h.x >> 16;
+  L.pi_state = h.y & 0xFF;
+  L.pi_live = (h.y >> 24) & 1;
+  L.pi_child = h.z & 0xFFFF;
+  L.pi_asf = h.z >> 16;
+  const uint32_t nslots0 = (h.y >> 8) & 0xFF;
+  const uint32_t nvars0 = (h.y >> 16) & 0xFF;
+
+  if (bad_cmd) {
+    set_fail(L, FB_UNSUPPORTED);  // never touches HBM outside the partition's arrays
+    L.proc = NONE;
+  } else if (kind == ZBHIP_CMD_CREATE) {
+    // CreateProcessInstanceProcessor.createProcessInstance (:129-158)
+    if (L.proc != NONE) set_fail(L, FB_SLOT_IN_USE);
+    else if (ref >= P.n_procs) set_fail(L, FB_BAD_PROCESS);
+    L.proc = ref;
+    L.next_ord = 0;
+    L.pi_live = false;
+    L.pi_state = 0;
+    L.pi_child = L.pi_asf = 0;
+  } else if (L.proc != NONE) {
+    // load the waiting instance: element-instance slots -> LDS table, variables, join counters
+    if (nslots0 > (uint32_t)K::T) set_fail(L, FB_TABLE);
+    if (nslots0 > 0) L.tbl[0] = s0;
+    for (uint32_t s = 1; s < nslots0 && s < (uint32_t)K::T; ++s)
+      L.tbl[s * K::B] = P.st.slots[(size_t)s * N + inst];
+    L.nt = (int)nslots0;
+    L.nvars = (int)nvars0;
+#pragma unroll
+    for (int v = 0; v < kVars; ++v)
+      if (v < L.nvars) {
+        const uint2 m = P.st.var_meta[(size_t)v * N + inst];
+        var_put(L, v, m.x, m.y, P.st.var_val[(size_t)v * N + inst]);
+      }
+  }
+  L.first_ord = L.next_ord;
+  if (!L.fail && L.proc != NONE) {
+    L.pb = prog + prog[1 + L.proc];
+    L.has_join = (L.pb[1] & 0xFFFF) != 0;
+    if (L.has_join && kind != ZBHIP_CMD_CREATE) {
+      L.jw0 = P.st.join[inst];
+      L.jw1 = P.st.join[(size_t)N + inst];
+      L.jw2 = P.st.join[(size_t)2 * N + inst];
+      L.jw3 = P.st.join[(size_t)3 * N + inst];
+    }
+  }
+
+  if (!L.fail && kind == ZBHIP_CMD_CREATE) {
+    if ((L.pb[0] >> 16) == NONE) set_fail(L, FB_BAD_PROCESS);
+    uint32_t pi = new_key(L);  // = ordinal 0
+    // setVariablesFromDocument -> VariableBehavior.mergeLocalDocument (:60-82)
+    if (doc_count > 1) set_fail(L, FB_DOC);
+    else if (doc_count == 1) set_local_variable(L, pi, P.docs[doc_begin]);
+    emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0);
+    push(L, 0, false, false, pi);
+    uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
+    emit(L, C_PIC_CREATED, created, pi, 0);
+  } else if (!L.fail && kind == ZBHIP_CMD_JOB_COMPLETE) {
+    // JobCompleteProcessor (:47-92) + DefaultJobCommandPreconditionGuard (:26-46)
+    const int t = L.proc == NONE ? -1 : tbl_find_job(L, ref);
+    if (t < 0) {
+      emit(L, kRejectBit | C_JOB_COMPLETE, ref, NONE, NONE, ZBHIP_REASON_JOB_NOT_FOUND);
+    } else {
+      uint2 e = L.tbl[t * K::B];
+      const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
+      emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
+      // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
+      e.y &= ~(1u << 24);
+      if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
+      L.tbl[t * K::B] = e;
+      if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) {  // afterAccept
+        uint32_t pe = new_key(L);  // EventTriggerBehavior.triggeringProcessEvent
+        emit(L, C_PE_TRIGGERING, pe, task_key, task_elem);
+        L.trig_key = task_key;       // ProcessEventTriggeringApplier: EVENT_TRIGGER row
+        emit(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, 0, task_elem);
+        push(L, task_elem, true, true, task_key);
+      }
+    }
+  } else if (!L.fail) {
+    set_fail(L, FB_UNSUPPORTED);
+  }
+  L.processed = 1;
+
+  // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
+  while (L.qh < L.qt && !L.fail) {
+    const uint32_t entry = L.q[(L.qh % K::Q) * K::B];
+    ++L.qh;
+    process_pi(L, entry);
+    ++L.processed;
+  }
+
+  // ---- commit: write back the instance (or leave it untouched on fallback) ----
+  uint32_t ns = 0;
+  if (!L.fail && L.pi_live) {
+    for (int t = 0; t < L.nt; ++t)
+      if (L.tbl[t * K::B].x != 0xFFFFFFFFu) ++ns;
+    if (ns > (uint32_t)kSlots) set_fail(L, FB_SLOTS);
+  }
+  // the counters are updated branch-free: per-branch updates are merged by the optimiser into a
+  // store through a selected pointer, which puts the whole accumulator in scratch
+  const bool ok = !L.fail;
+  if (ok && L.pi_live) {
+    uint32_t s = 0;
+    for (int t = 0; t < L.nt; ++t) {
+      uint2 e = L.tbl[t * K::B];
+      if (e.x != 0xFFFFFFFFu) P.st.slots[(size_t)(s++) * N + inst] = e;
+    }
+#pragma unroll
+    for (int v = 0; v < kVars; ++v)
+      if (v < L.nvars) {
+        P.st.var_meta[(size_t)v * N + inst] = make_uint2(var_x(L, v), var_y(L, v));
+        P.st.var_val[(size_t)v * N + inst] = var_v(L, v);
+      }
+  }
+  if (ok && L.has_join) {
+    const bool live = L.pi_live;  // a completed instance's counters are removed with it
+    P.st.join[inst] = live ? L.jw0 : 0u;
+    P.st.join[(size_t)N + inst] = live ? L.jw1 : 0u;
+    P.st.join[(size_t)2 * N + inst] = live ? L.jw2 : 0u;
+    P.st.join[(size_t)3 * N + inst] = live ? L.jw3 : 0u;
+  }
+  if (ok) {
+    // a completed instance frees its slot (rows removed with the instance) but keeps next_ord,
+    // so late commands for the instance relabel consistently
+    const bool live = L.pi_live;
+    P.st.hdr[inst] = live ? make_uint4(L.proc | ((uint32_t)L.next_ord << 16),
+                                       L.pi_state | (ns << 8) | ((uint32_t)L.nvars << 16) | (1u << 24),
+                                       (uint32_t)L.pi_child | ((uint32_t)L.pi_asf << 16), 0)
+                          : make_uint4(0xFFFFu | ((uint32_t)L.next_ord << 16), 0, 0, 0);
+  }
+  const uint32_t nkeys = ok ? (uint16_t)(L.next_ord - L.first_ord) : 0u;
+  const uint32_t nrec = ok ? L.nrec : 0u;
+  P.cmd_hdr[ci] = make_uint2(nrec | (nkeys << 16),
+                             L.first_ord | ((uint32_t)(ok ? ST_OK : ST_FALLBACK) << 16) | (L.fail << 24));
+  acc.cmd += 1;
+  acc.fb += ok ? 0u : 1u;
+  acc.rec += nrec;
+  acc.trans += ok ? L.transitions : 0u;
+  acc.comp += ok ? L.completed : 0u;
+  acc.keys += nkeys;
+  return nrec;
+}
+
+#ifdef ZB_STAMPS
+// cycle stamps per phase (summed over waves): [0] top-of-chunk wait, [1] run_command,
+// [2] scan + barrier, [3] flush issue, [4] chunks, [5] prologue (program staging + first loads)
+__device__ unsigned long long g_stamps[8];
+#define ZB_STAMP(v) const unsigned long long v = clock64()
+#else
+#define ZB_STAMP(v)
+#endif
+
+// k_step: workgroup g processes chunks g, g + G, g + 2G, ... of B commands (G = grid size,
+// sized by the host to the resident workgroups).  The rows of a command are fetched two chunks
+// ahead (command index three, command word two, header + first slot one chunk ahead), so the
+// dependent load chain command -> instance rows overlaps the previous chunk's processing.
+// Chunk c's records are compacted by a wavefront scan into output region region_base + c.
 template <class K>
 __global__ __launch_bounds__(K::B) void k_step(StepParams P) {
   extern __shared__ __align__(16) uint32_t smem[];
@@ -590,261 +823,126 @@ __global__ __launch_bounds__(K::B) void k_step(StepParams P) {
   uint2* tbl_base = reinterpret_cast<uint2*>(smem + prog_words);
   uint2* stage_base = tbl_base + K::T * K::B;
   uint32_t* q_base = reinterpret_cast<uint32_t*>(stage_base + K::R * K::B);
-  uint32_t* pre = q_base + K::Q * K::B;  // [B + 1] record offsets of the lanes in the block
-  uint32_t* cis = pre + K::B + 1;        // [B] command index of each lane
+  uint32_t* pre = q_base + K::Q * K::B;  // [B] first output record of each lane in the chunk
+  uint32_t* cis = pre + K::B;            // [B] command index of each lane
+  uint8_t* own = reinterpret_cast<uint8_t*>(cis + K::B);  // [B * R] lane owning output record o
+  static_assert(K::B <= 256, "owner map holds lane ids in bytes");
+  __shared__ uint32_t wsum[2][K::B / 64];
+  ZB_STAMP(t_start);
+#ifdef ZB_STAMPS
+  unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0};
+#endif
   for (uint32_t i = threadIdx.x; i < P.prog_words; i += K::B) prog[i] = P.prog[i];
   __syncthreads();
 
-  uint32_t my_nrec = 0, my_ci = 0;
-  const uint32_t lane_id = blockIdx.x * K::B + threadIdx.x;
-  uint32_t n_rec = 0, n_trans = 0, n_comp = 0, n_keys = 0, n_fb = 0, n_cmd = 0;
-  if (lane_id < P.n_launch) {
-    const uint32_t ci = P.order ? P.order[lane_id] : lane_id;
-    const uint4 cw = P.cmds[ci];  // zbhip_command
-    const uint32_t inst = cw.x;
-    const uint32_t kind = cw.y & 0xFF;
-    const uint32_t doc_count = (cw.y >> 8) & 0xFF;
-    const uint32_t ref = cw.y >> 16;
-    const uint32_t doc_begin = cw.z;
-    const uint32_t N = P.st.n;
-
-    Lane<K> L;
-    L.tbl = tbl_base + threadIdx.x;
-    L.q = q_base + threadIdx.x;
-    L.stage = stage_base + threadIdx.x;
-    // overflow rows (j >= R) are wave-interleaved by command: each emit of a wave is one
-    // coalesced 512-byte store
-    L.rec = P.rec + ((size_t)(ci >> 6) * P.rec_cap << 6) + (ci & 63);
-    my_ci = ci;
-    L.rec_cap = P.rec_cap;
-    L.nrec = 0;
-    L.fail = 0;
-    L.transitions = 0;
-    L.completed = 0;
-    L.limit = P.max_cmds_in_batch;
-    L.processed = 0;
-    L.qh = L.qt = 0;
-    L.nt = 0;
-    L.trig_key = NONE;
-    L.docs = P.docs;
-    L.doc_begin = doc_begin;
-    L.doc_count = doc_count;
-    L.has_join = false;
-    L.jw0 = L.jw1 = L.jw2 = L.jw3 = 0;
-    L.nvars = 0;
-    L.vx0 = L.vx1 = L.vx2 = L.vx3 = 0xFFFFFFFFu;
-    L.vy0 = L.vy1 = L.vy2 = L.vy3 = 0;
-    L.vv0 = L.vv1 = L.vv2 = L.vv3 = 0;
-
-    const bool bad_cmd = inst >= N || (doc_count && (uint64_t)doc_begin + doc_count > P.n_docs);
-    const uint4 h = bad_cmd ? make_uint4(0xFFFFFFFFu, 0, 0, 0) : P.st.hdr[inst];
-    L.proc = h.x & 0xFFFF;
-    L.next_ord = h.x >> 16;
-    L.pi_state = h.y & 0xFF;
-    L.pi_live = (h.y >> 24) & 1;
-    L.pi_child = h.z & 0xFFFF;
-    L.pi_asf = h.z >> 16;
-    const uint32_t nslots0 = (h.y >> 8) & 0xFF;
-    const uint32_t nvars0 = (h.y >> 16) & 0xFF;
-
-    if (bad_cmd) {
-      set_fail(L, FB_UNSUPPORTED);  // never touches HBM outside the partition's arrays
-      L.proc = NONE;
-    } else if (kind == ZBHIP_CMD_CREATE) {
-      // CreateProcessInstanceProcessor.createProcessInstance (:129-158)
-      if (L.proc != NONE) set_fail(L, FB_SLOT_IN_USE);
-      else if (ref >= P.n_procs) set_fail(L, FB_BAD_PROCESS);
-      L.proc = ref;
-      L.next_ord = 0;
-      L.pi_live = false;
-      L.pi_state = 0;
-      L.pi_child = L.pi_asf = 0;
-    } else if (L.proc != NONE) {
-      // load the waiting instance: element-instance slots -> LDS table, variables, join counters
-      if (nslots0 > (uint32_t)K::T) set_fail(L, FB_TABLE);
-      for (uint32_t s = 0; s < nslots0 && s < (uint32_t)K::T; ++s)
-        L.tbl[s * K::B] = P.st.slots[(size_t)s * N + inst];
-      L.nt = (int)nslots0;
-      L.nvars = (int)nvars0;
-#pragma unroll
-      for (int v = 0; v < kVars; ++v)
-        if (v < L.nvars) {
-          const uint2 m = P.st.var_meta[(size_t)v * N + inst];
-          var_put(L, v, m.x, m.y, P.st.var_val[(size_t)v * N + inst]);
-        }
-    }
-    L.first_ord = L.next_ord;
-    if (!L.fail && L.proc != NONE) {
-      L.pb = prog + prog[1 + L.proc];
-      L.has_join = (L.pb[1] & 0xFFFF) != 0;
-      if (L.has_join && kind != ZBHIP_CMD_CREATE) {
-        L.jw0 = P.st.join[inst];
-        L.jw1 = P.st.join[(size_t)N + inst];
-        L.jw2 = P.st.join[(size_t)2 * N + inst];
-        L.jw3 = P.st.join[(size_t)3 * N + inst];
-      }
-    }
-
-    if (!L.fail && kind == ZBHIP_CMD_CREATE) {
-      if ((L.pb[0] >> 16) == NONE) set_fail(L, FB_BAD_PROCESS);
-      uint32_t pi = new_key(L);  // = ordinal 0
-      // setVariablesFromDocument -> VariableBehavior.mergeLocalDocument (:60-82)
-      if (doc_count > 1) set_fail(L, FB_DOC);
-      else if (doc_count == 1) set_local_variable(L, pi, P.docs[doc_begin]);
-      emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0);
-      push(L, 0, false, false, pi);
-      uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
-      emit(L, C_PIC_CREATED, created, pi, 0);
-    } else if (!L.fail && kind == ZBHIP_CMD_JOB_COMPLETE) {
-      // JobCompleteProcessor (:47-92) + DefaultJobCommandPreconditionGuard (:26-46)
-      const int t = L.proc == NONE ? -1 : tbl_find_job(L, ref);
-      if (t < 0) {
-        emit(L, kRejectBit | C_JOB_COMPLETE, ref, NONE, NONE, ZBHIP_REASON_JOB_NOT_FOUND);
-      } else {
-        uint2 e = L.tbl[t * K::B];
-        const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
-        emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
-        // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
-        e.y &= ~(1u << 24);
-        if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
-        L.tbl[t * K::B] = e;
-        if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) {  // afterAccept
-          uint32_t pe = new_key(L);  // EventTriggerBehavior.triggeringProcessEvent
-          emit(L, C_PE_TRIGGERING, pe, task_key, task_elem);
-          L.trig_key = task_key;       // ProcessEventTriggeringApplier: EVENT_TRIGGER row
-          emit(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, 0, task_elem);
-          push(L, task_elem, true, true, task_key);
-        }
-      }
-    } else if (!L.fail) {
-      set_fail(L, FB_UNSUPPORTED);
-    }
-    L.processed = 1;
-
-    // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
-    while (L.qh < L.qt && !L.fail) {
-      const uint32_t entry = L.q[(L.qh % K::Q) * K::B];
-      ++L.qh;
-      process_pi(L, entry);
-      ++L.processed;
-    }
-
-    // ---- commit: write back the instance (or leave it untouched on fallback) ----
-    uint32_t ns = 0;
-    if (!L.fail && L.pi_live) {
-      for (int t = 0; t < L.nt; ++t)
-        if (L.tbl[t * K::B].x != 0xFFFFFFFFu) ++ns;
-      if (ns > (uint32_t)kSlots) set_fail(L, FB_SLOTS);
-    }
-    if (!L.fail) {
-      if (L.pi_live) {
-        uint32_t s = 0;
-        for (int t = 0; t < L.nt; ++t) {
-          uint2 e = L.tbl[t * K::B];
-          if (e.x != 0xFFFFFFFFu) P.st.slots[(size_t)(s++) * N + inst] = e;
-        }
-#pragma unroll
-        for (int v = 0; v < kVars; ++v)
-          if (v < L.nvars) {
-            P.st.var_meta[(size_t)v * N + inst] = make_uint2(var_x(L, v), var_y(L, v));
-            P.st.var_val[(size_t)v * N + inst] = var_v(L, v);
-          }
-        if (L.has_join) {
-          P.st.join[inst] = L.jw0;
-          P.st.join[(size_t)N + inst] = L.jw1;
-          P.st.join[(size_t)2 * N + inst] = L.jw2;
-          P.st.join[(size_t)3 * N + inst] = L.jw3;
-        }
-        P.st.hdr[inst] = make_uint4(L.proc | ((uint32_t)L.next_ord << 16),
-                                    L.pi_state | (ns << 8) | ((uint32_t)L.nvars << 16) | (1u << 24),
-                                    (uint32_t)L.pi_child | ((uint32_t)L.pi_asf << 16), 0);
-      } else {
-        // the process instance completed: free the slot (rows removed with the instance);
-        // keep next_ord so late commands for the instance relabel consistently
-        P.st.hdr[inst] = make_uint4(0xFFFFu | ((uint32_t)L.next_ord << 16), 0, 0, 0);
-        if (L.has_join) {
-#pragma unroll
-          for (int i = 0; i < kJoinWords; ++i) P.st.join[(size_t)i * N + inst] = 0;
-        }
-      }
-      P.cmd_hdr[ci] = make_uint2(L.nrec | ((uint32_t)(uint16_t)(L.next_ord - L.first_ord) << 16),
-                                 L.first_ord | ((uint32_t)ST_OK << 16));
-      n_rec = L.nrec;
-      my_nrec = L.nrec;
-      n_trans = L.transitions;
-      n_comp = L.completed;
-      n_keys = (uint16_t)(L.next_ord - L.first_ord);
-    } else {
-      P.cmd_hdr[ci] = make_uint2(0, L.first_ord | ((uint32_t)ST_FALLBACK << 16) | (L.fail << 24));
-      n_fb = 1;
-    }
-    n_cmd = 1;
-  }
-  // ---- wavefront scan compaction: the block's records go out contiguously, once ----
+  const uint32_t n_chunks = (P.n_launch + K::B - 1) / K::B;
+  const uint32_t G = gridDim.x;
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t inc = my_nrec;
+  Counters acc = {0, 0, 0, 0, 0, 0};
+
+  uint32_t c = blockIdx.x;
+  uint32_t ci1 = cmd_index<K>(P, c);
+  uint4 cw1 = load_cmd(P, ci1);
+  uint4 h1;
+  uint2 s1;
+  load_rows(P, ci1, cw1, h1, s1);
+  uint32_t ci2 = cmd_index<K>(P, c + G);
+  uint4 cw2 = load_cmd(P, ci2);
+  uint32_t ci3 = cmd_index<K>(P, c + 2 * G);
+#ifdef ZB_STAMPS
+  { const uint32_t u = __builtin_amdgcn_readfirstlane(cw1.x + h1.x + s1.x);
+    ZB_STAMP(t_pro); acc_t[5] += t_pro - t_start + (u == 0x12345678u); }
+#endif
+
+  for (uint32_t it = 0; c < n_chunks; c += G, ++it) {
+    ZB_STAMP(t0);
+    const uint32_t ci = ci1;
+    const uint4 cw = cw1, h = h1;
+    const uint2 s0 = s1;
+    // advance the pipeline before touching the current command
+    ci1 = ci2;
+    cw1 = cw2;
+    load_rows(P, ci1, cw1, h1, s1);
+    ci2 = ci3;
+    cw2 = load_cmd(P, ci2);
+    ci3 = cmd_index<K>(P, c + 3 * G);
+    ZB_STAMP(t1);
+
+    uint32_t my_nrec = 0;
+    if (ci != kNoCmd) my_nrec = run_command<K>(P, prog, tbl_base, stage_base, q_base, ci, cw, h, s0, acc);
+    ZB_STAMP(t2);
+
+    // ---- wavefront scan compaction: the chunk's records go out contiguously, once ----
+    uint32_t inc = my_nrec;
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t o = __shfl_up(inc, off);
-    if (lane >= (uint32_t)off) inc += o;
-  }
-  __shared__ uint32_t wsum[K::B / 64];
-  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
-  cis[threadIdx.x] = my_ci;
-  __syncthreads();
-  uint32_t wbase = 0, total = 0;
-#pragma unroll
-  for (int w = 0; w < K::B / 64; ++w) {
-    if (w < (int)(threadIdx.x >> 6)) wbase += wsum[w];
-    total += wsum[w];
-  }
-  uint2* out = P.out + (size_t)(P.region_base + blockIdx.x) * K::B * P.rec_cap;
-  if constexpr (K::F == 1) {
-    const uint32_t my_off = wbase + inc - my_nrec;
-    for (uint32_t j = 0; j < my_nrec; ++j) {
-      const uint2 r = j < (uint32_t)K::R ? stage_base[j * K::B + threadIdx.x]
-                                         : P.rec[(((size_t)(my_ci >> 6) * P.rec_cap + j) << 6) + (my_ci & 63)];
-      out[my_off + j] = r;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(inc, off);
+      if (lane >= (uint32_t)off) inc += o;
     }
-  } else {
-    pre[threadIdx.x] = wbase + inc - my_nrec;
-    if (threadIdx.x == K::B - 1) pre[K::B] = wbase + inc;
+    uint32_t* ws = wsum[it & 1];  // double-buffered: one barrier per chunk
+    if (lane == 63) ws[threadIdx.x >> 6] = inc;
     __syncthreads();
-    for (uint32_t o = threadIdx.x; o < total; o += K::B) {
-      uint32_t lo = 0, hi = K::B;  // the lane whose records cover o: largest l with pre[l] <= o
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= o) lo = mid;
-        else hi = mid;
-      }
-      const uint32_t j = o - pre[lo];
-      uint2 r;
-      if (j < (uint32_t)K::R) {
-        r = stage_base[j * K::B + lo];
-      } else {
-        const uint32_t c = cis[lo];
-        r = P.rec[(((size_t)(c >> 6) * P.rec_cap + j) << 6) + (c & 63)];
-      }
-      out[o] = r;
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < K::B / 64; ++w) {
+      if (w < (int)(threadIdx.x >> 6)) wbase += ws[w];
+      total += ws[w];
     }
+    ZB_STAMP(t3);
+    uint2* out = P.out + (size_t)(P.region_base + c) * K::B * P.rec_cap;
+    const uint32_t my_off = wbase + inc - my_nrec;
+    if (total <= (uint32_t)(K::B * K::R)) {
+      // packed copy: an owner map in LDS turns the lanes' columns into one contiguous run that
+      // the workgroup stores with 16-byte, fully coalesced writes (2 records per lane)
+      pre[threadIdx.x] = my_off;
+      cis[threadIdx.x] = ci;
+      for (uint32_t j = 0; j < my_nrec; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
+      __syncthreads();
+      for (uint32_t o = 2 * threadIdx.x; o < total; o += 2 * K::B) {
+        const uint32_t l0 = own[o];
+        const uint32_t j0 = o - pre[l0];
+        const uint2 r0 = j0 < (uint32_t)K::R ? stage_base[j0 * K::B + l0] : overflow_row(P, cis[l0], j0);
+        if (o + 1 < total) {
+          const uint32_t l1 = own[o + 1];
+          const uint32_t j1 = o + 1 - pre[l1];
+          const uint2 r1 = j1 < (uint32_t)K::R ? stage_base[j1 * K::B + l1] : overflow_row(P, cis[l1], j1);
+          *reinterpret_cast<uint4*>(out + o) = make_uint4(r0.x, r0.y, r1.x, r1.y);
+        } else {
+          out[o] = r0;
+        }
+      }
+      __syncthreads();  // the next chunk reuses the stage columns and the owner map
+    } else {
+      // more records than the owner map covers: every lane stores its own records
+      for (uint32_t j = 0; j < my_nrec; ++j)
+        out[my_off + j] = j < (uint32_t)K::R ? stage_base[j * K::B + threadIdx.x] : overflow_row(P, ci, j);
+    }
+    if (threadIdx.x == 0) P.region_total[P.region_base + c] = total;
+#ifdef ZB_STAMPS
+    ZB_STAMP(t4);
+    acc_t[0] += t1 - t0; acc_t[1] += t2 - t1; acc_t[2] += t3 - t2; acc_t[3] += t4 - t3; acc_t[4] += 1;
+#endif
   }
-  if (threadIdx.x == 0) P.region_total[P.region_base + blockIdx.x] = total;
+#ifdef ZB_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_stamps[k], acc_t[k]);
+#endif
 
   // ---- statistics: wave64 reduction, waves through LDS, one add per counter into one of 64
   // spread rows (non-returning atomics, no hot line) ----
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    n_rec += __shfl_xor(n_rec, off);
-    n_trans += __shfl_xor(n_trans, off);
-    n_comp += __shfl_xor(n_comp, off);
-    n_keys += __shfl_xor(n_keys, off);
-    n_fb += __shfl_xor(n_fb, off);
-    n_cmd += __shfl_xor(n_cmd, off);
+    acc.rec += __shfl_xor(acc.rec, off);
+    acc.trans += __shfl_xor(acc.trans, off);
+    acc.comp += __shfl_xor(acc.comp, off);
+    acc.keys += __shfl_xor(acc.keys, off);
+    acc.fb += __shfl_xor(acc.fb, off);
+    acc.cmd += __shfl_xor(acc.cmd, off);
   }
   __shared__ uint32_t wstat[K::B / 64][8];
   if (lane == 0) {
     uint32_t* w = wstat[threadIdx.x >> 6];
-    w[0] = n_rec; w[1] = n_trans; w[2] = n_comp; w[3] = n_keys; w[4] = n_fb; w[5] = n_cmd;
+    w[0] = acc.rec; w[1] = acc.trans; w[2] = acc.comp; w[3] = acc.keys; w[4] = acc.fb; w[5] = acc.cmd;
   }
   __syncthreads();
   if (threadIdx.x < 6) {
@@ -909,58 +1007,67 @@ template <class K>
 static size_t lds_bytes(uint32_t prog_words) {
   return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::T * K::B * sizeof(uint2) +
          (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t) +
-         (size_t)(2 * K::B + 1) * sizeof(uint32_t);
+         (size_t)2 * K::B * sizeof(uint32_t) + (size_t)K::B * K::R;
 }
 
-// Tuning table: ZBHIP_KCFG=<i> selects an alternative configuration for the small variant.
-using KTune0 = KCfg<128, 4, 4, 32, 0>;
-using KTune1 = KCfg<128, 4, 4, 16, 0>;
-using KTune2 = KCfg<256, 4, 4, 16, 1>;
-using KTune3 = KCfg<64, 4, 4, 16, 1>;
-using KTune4 = KCfg<128, 4, 4, 8, 1>;
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 
-static int tune_cfg() {
-  static int v = [] {
-    const char* e = getenv("ZBHIP_KCFG");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
+// Grid of a launch: as many workgroups as are resident at once (occupancy x CUs), each looping
+// over an equal share of the chunks; ZBHIP_CHUNKS_PER_WG=k instead gives every workgroup k chunks.
+template <class K>
+static uint32_t grid_for(uint32_t n_chunks, size_t lds) {
+  static int cus = 0;
+  static size_t cached_lds = ~(size_t)0;
+  static int per_cu = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  if (lds != cached_lds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step<K>, K::B, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
+    cached_lds = lds;
+  }
+  const int fixed = env_int("ZBHIP_CHUNKS_PER_WG", 0);
+  if (fixed > 0) return (n_chunks + fixed - 1) / fixed;
+  const uint32_t resident = (uint32_t)(per_cu * cus);
+  if (n_chunks <= resident) return n_chunks;
+  const uint32_t per_wg = (n_chunks + resident - 1) / resident;
+  return (n_chunks + per_wg - 1) / per_wg;
 }
 
 template <class K>
 static hipError_t launch_k(const StepParams& P, hipStream_t s) {
-  const uint32_t grid = (P.n_launch + K::B - 1) / K::B;
-  hipLaunchKernelGGL(k_step<K>, dim3(grid), dim3(K::B), lds_bytes<K>(P.prog_words), s, P);
+  const uint32_t n_chunks = (P.n_launch + K::B - 1) / K::B;
+  const size_t lds = lds_bytes<K>(P.prog_words);
+  hipLaunchKernelGGL(k_step<K>, dim3(grid_for<K>(n_chunks, lds)), dim3(K::B), lds, s, P);
   return hipGetLastError();
 }
 
-uint32_t step_block(int variant) {
-  if (!variant) switch (tune_cfg()) {
-      case 0: return KTune0::B;
-      case 1: return KTune1::B;
-      case 2: return KTune2::B;
-      case 3: return KTune3::B;
-      case 4: return KTune4::B;
-      default: break;
-    }
-  return variant ? KGeneric::B : KSimple::B;
-}
+uint32_t step_block(int variant) { return variant ? KGeneric::B : KSimple::B; }
 
 size_t step_lds_bytes(int variant, uint32_t prog_words) {
   return variant ? lds_bytes<KGeneric>(prog_words) : lds_bytes<KSimple>(prog_words);
 }
 
+void dump_stamps() {
+#ifdef ZB_STAMPS
+  unsigned long long h[8] = {};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof h) != hipSuccess) return;
+  const double waves = 1.0;  // sums are per wave (lane 0)
+  fprintf(stderr, "[stamps] chunks %llu | per chunk cycles: top-wait %.0f run %.0f scan+barrier %.0f flush %.0f | prologue sum %.3g\n",
+          h[4], h[0] / (double)h[4] * waves, h[1] / (double)h[4], h[2] / (double)h[4], h[3] / (double)h[4], (double)h[5]);
+  const unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z);
+#endif
+}
+
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
   if (P.n_launch == 0) return hipSuccess;
-  if (variant) return launch_k<KGeneric>(P, s);
-  switch (tune_cfg()) {
-    case 0: return launch_k<KTune0>(P, s);
-    case 1: return launch_k<KTune1>(P, s);
-    case 2: return launch_k<KTune2>(P, s);
-    case 3: return launch_k<KTune3>(P, s);
-    case 4: return launch_k<KTune4>(P, s);
-    default: return launch_k<KSimple>(P, s);
-  }
+  return variant ? launch_k<KGeneric>(P, s) : launch_k<KSimple>(P, s);
 }
 
 hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,

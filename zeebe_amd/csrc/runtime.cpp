@@ -21,6 +21,7 @@ namespace zb {
 uint32_t step_block(int variant);
 size_t step_lds_bytes(int variant, uint32_t prog_words);
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s);
+void dump_stamps();
 hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
                          size_t region_stride, uint2* out, unsigned long long* total, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;  // regions for the extra workgroups of multi-round windows
@@ -597,6 +598,7 @@ int64_t zbhip_pending_records(zbhip_handle* h) {
 }
 
 int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
+  if (getenv("ZBHIP_STAMPS")) dump_stamps();
   if (!h || !out) return ZBHIP_EINVAL;
   if (h->stats_dirty) {
     unsigned long long rows[64 * 8];

@@ -9,7 +9,8 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzbhip.so")
+# ZBHIP_LIB selects an alternative in-tree build (e.g. the instrumented libzbhip_stamps.so)
+LIB_PATH = os.path.join(HERE, os.environ.get("ZBHIP_LIB", "libzbhip.so"))
 
 ERRORS = {-1: "ZBHIP_EINVAL", -2: "ZBHIP_ENOMEM", -3: "ZBHIP_EDEVICE", -4: "ZBHIP_EPARSE",
           -5: "ZBHIP_EUNSUPP", -6: "ZBHIP_ESTATE", -7: "ZBHIP_ENODEV"}
