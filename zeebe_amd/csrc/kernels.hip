@@ -211,6 +211,12 @@ __device__ __forceinline__ void tbl_set_state(Lane<K>& L, int t, uint32_t state)
   L.tbl[t * K::B] = e;
 }
 
+// Complete every outstanding vector-memory operation inside the branch that issued a conditional
+// load (s_waitcnt vmcnt(0); gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  The wait-count pass
+// is conservative at control-flow joins: without this it waits at the join on every path, and
+// that wait would also cover the next chunk's rows prefetched at the top of the chunk loop.
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // ---- variables (registers) ------------------------------------------------------------------
 template <class K>
 __device__ __forceinline__ int var_find(const Lane<K>& L, uint32_t scope, uint32_t name) {
@@ -248,6 +254,7 @@ __device__ __forceinline__ void merge_document_from(Lane<K>& L, uint32_t scope_k
   if (count == 0) return;
   if (count > 1) { set_fail(L, FB_DOC); return; }
   const zbhip_doc_entry d = L.docs[begin];
+  vm_drain();
   if (scope_key != 0) {
     int v = var_find(L, scope_key, d.name_id);
     if (v >= 0) {
@@ -682,16 +689,22 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     // load the waiting instance: element-instance slots -> LDS table, variables, join counters
     if (nslots0 > (uint32_t)K::T) set_fail(L, FB_TABLE);
     if (nslots0 > 0) L.tbl[0] = s0;
-    for (uint32_t s = 1; s < nslots0 && s < (uint32_t)K::T; ++s)
-      L.tbl[s * K::B] = P.st.slots[(size_t)s * N + inst];
+    if (nslots0 > 1) {
+      for (uint32_t s = 1; s < nslots0 && s < (uint32_t)K::T; ++s)
+        L.tbl[s * K::B] = P.st.slots[(size_t)s * N + inst];
+      vm_drain();
+    }
     L.nt = (int)nslots0;
     L.nvars = (int)nvars0;
+    if (L.nvars > 0) {
 #pragma unroll
-    for (int v = 0; v < kVars; ++v)
-      if (v < L.nvars) {
-        const uint2 m = P.st.var_meta[(size_t)v * N + inst];
-        var_put(L, v, m.x, m.y, P.st.var_val[(size_t)v * N + inst]);
-      }
+      for (int v = 0; v < kVars; ++v)
+        if (v < L.nvars) {
+          const uint2 m = P.st.var_meta[(size_t)v * N + inst];
+          var_put(L, v, m.x, m.y, P.st.var_val[(size_t)v * N + inst]);
+        }
+      vm_drain();
+    }
   }
   L.first_ord = L.next_ord;
   if (!L.fail && L.proc != NONE) {
@@ -702,6 +715,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       L.jw1 = P.st.join[(size_t)N + inst];
       L.jw2 = P.st.join[(size_t)2 * N + inst];
       L.jw3 = P.st.join[(size_t)3 * N + inst];
+      vm_drain();
     }
   }
 
@@ -710,7 +724,11 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     uint32_t pi = new_key(L);  // = ordinal 0
     // setVariablesFromDocument -> VariableBehavior.mergeLocalDocument (:60-82)
     if (doc_count > 1) set_fail(L, FB_DOC);
-    else if (doc_count == 1) set_local_variable(L, pi, P.docs[doc_begin]);
+    else if (doc_count == 1) {
+      const zbhip_doc_entry d = P.docs[doc_begin];
+      vm_drain();
+      set_local_variable(L, pi, d);
+    }
     emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0);
     push(L, 0, false, false, pi);
     uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
@@ -824,8 +842,7 @@ __global__ __launch_bounds__(K::B) void k_step(StepParams P) {
   uint2* stage_base = tbl_base + K::T * K::B;
   uint32_t* q_base = reinterpret_cast<uint32_t*>(stage_base + K::R * K::B);
   uint32_t* pre = q_base + K::Q * K::B;  // [B] first output record of each lane in the chunk
-  uint32_t* cis = pre + K::B;            // [B] command index of each lane
-  uint8_t* own = reinterpret_cast<uint8_t*>(cis + K::B);  // [B * R] lane owning output record o
+  uint8_t* own = reinterpret_cast<uint8_t*>(pre + K::B);  // [B * R] lane owning output record o
   static_assert(K::B <= 256, "owner map holds lane ids in bytes");
   __shared__ uint32_t wsum[2][K::B / 64];
   ZB_STAMP(t_start);
@@ -880,32 +897,35 @@ __global__ __launch_bounds__(K::B) void k_step(StepParams P) {
       if (lane >= (uint32_t)off) inc += o;
     }
     uint32_t* ws = wsum[it & 1];  // double-buffered: one barrier per chunk
-    if (lane == 63) ws[threadIdx.x >> 6] = inc;
+    const bool wave_ovf = __ballot(my_nrec > (uint32_t)K::R) != 0;
+    if (lane == 63) ws[threadIdx.x >> 6] = inc | (wave_ovf ? 0x80000000u : 0u);
     __syncthreads();
     uint32_t wbase = 0, total = 0;
+    bool ovf = false;
 #pragma unroll
     for (int w = 0; w < K::B / 64; ++w) {
-      if (w < (int)(threadIdx.x >> 6)) wbase += ws[w];
-      total += ws[w];
+      const uint32_t v = ws[w] & 0x7FFFFFFFu;
+      if (w < (int)(threadIdx.x >> 6)) wbase += v;
+      total += v;
+      ovf |= (ws[w] >> 31) != 0;
     }
     ZB_STAMP(t3);
     uint2* out = P.out + (size_t)(P.region_base + c) * K::B * P.rec_cap;
     const uint32_t my_off = wbase + inc - my_nrec;
-    if (total <= (uint32_t)(K::B * K::R)) {
+    if (!ovf && total <= (uint32_t)(K::B * K::R)) {
       // packed copy: an owner map in LDS turns the lanes' columns into one contiguous run that
-      // the workgroup stores with 16-byte, fully coalesced writes (2 records per lane)
+      // the workgroup stores with 16-byte, fully coalesced writes (2 records per lane).  Only
+      // chunks without overflow rows take it, so the copy reads LDS alone and its stores never
+      // wait on vector memory.
       pre[threadIdx.x] = my_off;
-      cis[threadIdx.x] = ci;
       for (uint32_t j = 0; j < my_nrec; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
       __syncthreads();
       for (uint32_t o = 2 * threadIdx.x; o < total; o += 2 * K::B) {
         const uint32_t l0 = own[o];
-        const uint32_t j0 = o - pre[l0];
-        const uint2 r0 = j0 < (uint32_t)K::R ? stage_base[j0 * K::B + l0] : overflow_row(P, cis[l0], j0);
+        const uint2 r0 = stage_base[(o - pre[l0]) * K::B + l0];
         if (o + 1 < total) {
           const uint32_t l1 = own[o + 1];
-          const uint32_t j1 = o + 1 - pre[l1];
-          const uint2 r1 = j1 < (uint32_t)K::R ? stage_base[j1 * K::B + l1] : overflow_row(P, cis[l1], j1);
+          const uint2 r1 = stage_base[(o + 1 - pre[l1]) * K::B + l1];
           *reinterpret_cast<uint4*>(out + o) = make_uint4(r0.x, r0.y, r1.x, r1.y);
         } else {
           out[o] = r0;
@@ -913,7 +933,7 @@ __global__ __launch_bounds__(K::B) void k_step(StepParams P) {
       }
       __syncthreads();  // the next chunk reuses the stage columns and the owner map
     } else {
-      // more records than the owner map covers: every lane stores its own records
+      // records in overflow rows, or more than the owner map covers: every lane stores its own
       for (uint32_t j = 0; j < my_nrec; ++j)
         out[my_off + j] = j < (uint32_t)K::R ? stage_base[j * K::B + threadIdx.x] : overflow_row(P, ci, j);
     }
@@ -1007,7 +1027,7 @@ template <class K>
 static size_t lds_bytes(uint32_t prog_words) {
   return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::T * K::B * sizeof(uint2) +
          (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t) +
-         (size_t)2 * K::B * sizeof(uint32_t) + (size_t)K::B * K::R;
+         (size_t)K::B * sizeof(uint32_t) + (size_t)K::B * K::R;
 }
 
 static int env_int(const char* name, int dflt) {
