@@ -169,6 +169,14 @@ def main():
     k_step_avg_ms = step_ms / launches
     achieved = alg / launches / (k_step_avg_ms * 1e-3) / 1e9
     survey_bpt = SURVEY_BYTES_PER_TRANSITION.get(args.config)
+    # HBM traffic per launch from the PMC passes of this build (scripts/pmc.sh + scripts/pmc_traffic.py,
+    # FETCH_SIZE x2 gfx950 correction); null when no summary for this workload is committed
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
+    if os.path.exists(tpath) and not args.instances:
+        with open(tpath) as f:
+            traffic = json.load(f)["traffic_bytes_per_launch"]
+        traffic_src = os.path.relpath(tpath, ROOT)
 
     result = {
         "metric": "BPMN element transitions/sec + completed instances/sec, 1/2/4/8 MI355X",
@@ -192,7 +200,8 @@ def main():
                    "parallelism": "one partition per GPU (dp%d)" % world, "max_commands_in_batch": 100},
         "records_per_s": tot_recs / elapsed,
         "roofline": {"bound": "hbm", "kernel": "k_step", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBPS, "traffic": None,
+                     "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": alg / launches,
                      "algorithmic_bytes_per_step": alg,
                      "bytes_per_transition": alg / max(tr, 1),
                      "k_step_avg_ms": k_step_avg_ms, "compaction": "fused into k_step (wavefront scan)",
