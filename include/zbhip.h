@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 1
+#define ZBHIP_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -88,6 +88,15 @@ enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2 };
 enum { ZBHIP_VAR_CREATED = 0, ZBHIP_VAR_UPDATED = 1 };
 enum { ZBHIP_PE_TRIGGERING = 0 };
 enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
+/* MessageIntent, MessageSubscriptionIntent, ProcessMessageSubscriptionIntent
+ * (protocol/.../intent/MessageIntent.java:19-23, MessageSubscriptionIntent.java:19-30,
+ * ProcessMessageSubscriptionIntent.java:19-28) */
+enum { ZBHIP_MSG_PUBLISH = 0, ZBHIP_MSG_PUBLISHED = 1, ZBHIP_MSG_EXPIRE = 2, ZBHIP_MSG_EXPIRED = 3 };
+enum { ZBHIP_MS_CREATE = 0, ZBHIP_MS_CREATED = 1, ZBHIP_MS_CORRELATE = 2, ZBHIP_MS_CORRELATED = 3,
+       ZBHIP_MS_REJECT = 4, ZBHIP_MS_REJECTED = 5, ZBHIP_MS_DELETE = 6, ZBHIP_MS_DELETED = 7,
+       ZBHIP_MS_CORRELATING = 8 };
+enum { ZBHIP_PMS_CREATING = 0, ZBHIP_PMS_CREATE = 1, ZBHIP_PMS_CREATED = 2, ZBHIP_PMS_CORRELATE = 3,
+       ZBHIP_PMS_CORRELATED = 4, ZBHIP_PMS_DELETING = 5, ZBHIP_PMS_DELETE = 6, ZBHIP_PMS_DELETED = 7 };
 
 /* BpmnElementType / BpmnEventType ordinals (protocol/.../value/BpmnElementType.java:24-58,
  * BpmnEventType.java:24-35) */
@@ -142,6 +151,8 @@ typedef struct zbhip_element {
   uint16_t job_retries;  /* service task: static retries */
   uint16_t join_slot;    /* sequence flow into a parallel gateway: its taken-counter slot; else NONE */
   uint16_t id;           /* string-table index of the element id */
+  uint16_t message_name; /* message catch event: string-table index of the static message name; else NONE */
+  uint16_t correlation_var; /* message catch event: string-table index of the variable of `= var` */
 } zbhip_element;
 
 /* FEEL condition bytecode (subset of feel-scala 1.17.0 boolean expressions,
@@ -201,6 +212,8 @@ typedef struct zbhip_config {
   uint32_t max_records_per_batch;/* record slots per command (0 = derive from deployed processes) */
   uint32_t max_doc_entries;      /* variable-document entries per window */
   int64_t initial_key;           /* last key already generated in the partition (0 = fresh) */
+  uint32_t max_correlation_keys; /* correlation slots of this message partition (0 = no messages) */
+  uint32_t pad;
   void* stream;                  /* hipStream_t to launch on (NULL = handle-owned stream) */
 } zbhip_config;
 
@@ -217,11 +230,25 @@ const char* zbhip_name(zbhip_handle* h, uint32_t name_id);
 /* ---- commands ------------------------------------------------------------ */
 enum zbhip_command_kind {
   ZBHIP_CMD_CREATE = 1,        /* PROCESS_INSTANCE_CREATION:CREATE (CreateProcessInstanceProcessor.java:129-158) */
-  ZBHIP_CMD_JOB_COMPLETE = 2   /* JOB:COMPLETE (JobCompleteProcessor.java:47-92) */
+  ZBHIP_CMD_JOB_COMPLETE = 2,  /* JOB:COMPLETE (JobCompleteProcessor.java:47-92) */
+  /* MESSAGE:PUBLISH with timeToLive <= 0, no messageId and no variables (MessagePublishProcessor.java
+   * handleNewMessage): instance = correlation-key string id (the correlation slot of this message
+   * partition), ref = message-name id (zbhip_intern).  Other publishes belong to the CPU engine. */
+  ZBHIP_CMD_PUBLISH = 3,
+  /* Cross-partition subscription commands (SubscriptionCommandSender.java:54-338) received from
+   * another partition's outbox: doc_begin = index into the window's zbhip_xpart_cmd array.
+   * instance = the command's subject: the PI instance slot (xpart.instance) for
+   * PROCESS_MESSAGE_SUBSCRIPTION commands, the correlation slot (xpart.correlation_key) for
+   * MESSAGE_SUBSCRIPTION commands. */
+  ZBHIP_CMD_MSG_SUB_CREATE = 4,    /* MessageSubscriptionCreateProcessor.java:83-104 */
+  ZBHIP_CMD_PMS_CREATE = 5,        /* ProcessMessageSubscriptionCreateProcessor */
+  ZBHIP_CMD_PMS_CORRELATE = 6,     /* ProcessMessageSubscriptionCorrelateProcessor */
+  ZBHIP_CMD_MSG_SUB_CORRELATE = 7  /* MessageSubscriptionCorrelateProcessor */
 };
 
+/* STR values are string ids of the partition's value dictionary (zbhip_intern_string). */
 enum zbhip_doc_type { ZBHIP_DOC_NIL = 0, ZBHIP_DOC_BOOL = 1, ZBHIP_DOC_INT = 2, ZBHIP_DOC_DEC = 3,
-                      ZBHIP_DOC_OTHER = 4 };
+                      ZBHIP_DOC_OTHER = 4, ZBHIP_DOC_STR = 5 };
 
 /* One entry of a variable document (a msgpack map entry on the reference side).
  * DEC values are value * 10^ZBHIP_DEC_SCALE (exact decimal). */
@@ -241,12 +268,54 @@ typedef struct zbhip_command {
   uint32_t pad;
 } zbhip_command;
 
+/* A cross-partition subscription command (the compact form of the MessageSubscriptionRecord /
+ * ProcessMessageSubscriptionRecord that SubscriptionCommandSender.java:54-338 sends with
+ * InterPartitionCommandSender; the exchange between partitions moves these, 48 bytes each).
+ * Keys are the reference's (relabelled) keys; (instance, element_ord) is the routing handle of the
+ * subscribing element instance on its PI partition.  Name ids (message name, bpmnProcessId) and
+ * string ids (correlation key) are valid on every partition when deployments and interning are
+ * replicated in the same order on all partitions (the host adapter's duty, like deployment
+ * distribution). */
+typedef struct zbhip_xpart_cmd {
+  int64_t element_instance_key;
+  int64_t process_instance_key;
+  int64_t message_key;       /* -1 unset */
+  uint32_t correlation_key;  /* string id (routing: also set where the record value has none) */
+  uint32_t instance;         /* PI instance slot on the PI partition */
+  uint16_t element_ord;      /* key ordinal of the subscribing element instance in that instance */
+  uint16_t message_name;     /* name id */
+  uint16_t bpmn_process_id;  /* name id */
+  uint8_t kind;              /* ZBHIP_CMD_MSG_SUB_CREATE .. ZBHIP_CMD_MSG_SUB_CORRELATE */
+  uint8_t interrupting;
+  int16_t source_partition;
+  int16_t target_partition;
+  uint32_t pad;
+} zbhip_xpart_cmd;
+
 /* Submits a window of commands in log order.  Host buffers are copied. */
 int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs,
                  size_t n_docs);
-/* Same, from device-resident arrays already in HBM (no copy; must stay valid until run returns). */
+/* Same, with the window's received cross-partition commands (referenced by doc_begin). */
+int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs,
+                    size_t n_docs, const zbhip_xpart_cmd* xparts, size_t n_xparts);
+/* Same, from device-resident arrays already in HBM (no copy; must stay valid until run returns).
+ * The caller guarantees that every subject (instance slot / correlation slot) appears at most once
+ * in the window (no round planning). */
 int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,
                         const zbhip_doc_entry* dev_docs, size_t n_docs);
+int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,
+                           const zbhip_doc_entry* dev_docs, size_t n_docs,
+                           const zbhip_xpart_cmd* dev_xparts, size_t n_xparts);
+
+/* Value dictionary (correlation keys and other string variable values): returns the id (>= 0) of
+ * the string, interning it if new, or an error.  The device holds each string's Java hashCode
+ * (SubscriptionUtil.getSubscriptionHashCode, signed bytes) for subscription routing. */
+int64_t zbhip_intern_string(zbhip_handle* h, const char* bytes, size_t len);
+/* Bulk form: n strings, string i = bytes[offsets[i] .. offsets[i+1]); ids_out may be NULL. */
+int zbhip_intern_strings(zbhip_handle* h, const char* bytes, const uint64_t* offsets, size_t n, uint32_t* ids_out);
+const char* zbhip_string_value(zbhip_handle* h, uint32_t id, size_t* len);
+/* SubscriptionUtil.getSubscriptionPartitionId (protocol-impl/.../SubscriptionUtil.java:22-44). */
+int32_t zbhip_subscription_partition(const char* bytes, size_t len, int32_t partition_count);
 
 #define ZBHIP_RUN_NO_RESULTS 1u  /* benchmarking: no D2H copy, no host wait, no key relabelling */
 #define ZBHIP_RUN_TIMED 2u       /* record HIP events around the lifecycle kernel launches */
@@ -272,7 +341,16 @@ typedef struct zbhip_record {
   uint8_t reason;               /* rejection reason kind (zbhip_reason), 0 = none */
   uint8_t reason_arg;           /* e.g. the offending element-instance state */
   int64_t aux;                  /* VARIABLE: document entry index; JOB:COMPLETED: source doc; else -1 */
+  /* message value fields (MESSAGE / MESSAGE_SUBSCRIPTION / PROCESS_MESSAGE_SUBSCRIPTION) */
+  int64_t message_key;          /* messageKey, -1 unset */
+  uint32_t correlation_key;     /* string id, ZBHIP_NO_STRING = empty */
+  uint16_t message_name;        /* name id, 0xFFFF = empty */
+  uint16_t bpmn_process_id;     /* name id, 0xFFFF = empty */
+  int32_t partition;            /* PMS: subscriptionPartitionId; else 0 */
+  uint8_t interrupting;
+  uint8_t pad[3];
 } zbhip_record;
+#define ZBHIP_NO_STRING 0xFFFFFFFFu
 
 int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out);
 /* Number of records the last run produced (before draining). */
@@ -297,6 +375,14 @@ int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out);
 typedef void (*zbhip_state_sink)(void* ctx, const char* row);
 int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx);
 
+/* Cross-partition commands the last run sent (post-commit side effects of its batches, in log
+ * order, keys relabelled); the host routes them to their target partitions (drain mode). */
+int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_out);
+/* Device form: after zbhip_run (any mode) the outbox bucketed by target partition, stable in log
+ * order, with device-computed keys; counts[t] = entries for partition t + 1 (partition_count
+ * entries).  The pointer stays valid until the next run.  This is what the RCCL all-to-all sends. */
+int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32_t* counts);
+
 /* Instances whose last batch needs the fallback path (incident, FEEL outside the
  * subset, batch-limit overflow, capacity).  Their state was left untouched. */
 int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_out);
@@ -317,7 +403,13 @@ enum zbhip_reason {
   ZBHIP_REASON_FS_STATE = 3,          /* :116-128 */
   ZBHIP_REASON_EI_NOT_FOUND = 4,      /* :74-86 */
   ZBHIP_REASON_EI_STATE = 5,          /* :102-114 */
-  ZBHIP_REASON_JOB_NOT_FOUND = 6      /* JobCommandPreconditionChecker.java */
+  ZBHIP_REASON_JOB_NOT_FOUND = 6,     /* JobCommandPreconditionChecker.java */
+  ZBHIP_REASON_MS_ALREADY_OPEN = 7,   /* MessageSubscriptionCreateProcessor SUBSCRIPTION_ALREADY_OPENED_MESSAGE */
+  ZBHIP_REASON_PMS_CREATE_NOT_FOUND = 8, /* ProcessMessageSubscriptionCreateProcessor NO_SUBSCRIPTION_FOUND */
+  ZBHIP_REASON_PMS_CREATE_NOT_OPENING = 9, /* ... NOT_OPENING_MSG ("opened"/"closing") */
+  ZBHIP_REASON_PMS_CORR_NOT_FOUND = 10, /* ProcessMessageSubscriptionCorrelateProcessor NO_SUBSCRIPTION_FOUND */
+  ZBHIP_REASON_PMS_CORR_NO_EVENT = 11,  /* ... NO_EVENT_OCCURRED_MESSAGE */
+  ZBHIP_REASON_MS_CORR_NOT_FOUND = 12   /* MessageSubscriptionCorrelateProcessor NO_SUBSCRIPTION_FOUND */
 };
 /* Rejection reason text exactly as the reference writes it. */
 int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, size_t cap);

@@ -57,6 +57,16 @@ def lib():
         L.zbo_fallback.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.zbo_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                    C.POINTER(C.c_uint64)]
+        L.zbo_submit_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
+                                    C.c_size_t]
+        L.zbo_intern_string.restype = C.c_int64
+        L.zbo_intern_string.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        L.zbo_outbox.restype = C.c_size_t
+        L.zbo_outbox.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.zbo_clear_outbox.argtypes = [C.c_void_p]
+        L.zbo_subscription_partition.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
+        L.zbo_java_hash.restype = C.c_int32
+        L.zbo_java_hash.argtypes = [C.c_char_p, C.c_size_t]
         L.zbo_bench.restype = C.c_double
         L.zbo_bench.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
@@ -100,10 +110,24 @@ class Oracle:
     def element_id(self, proc, elem):
         return self.L.zbo_element_id(self.h, proc, elem).decode()
 
-    def submit(self, cmds, docs=None):
+    def submit(self, cmds, docs=None, xparts=None):
         cmds = np.ascontiguousarray(cmds, dtype=abi.COMMAND_DTYPE)
         docs = np.ascontiguousarray(docs if docs is not None else abi.make_docs(0), dtype=abi.DOC_DTYPE)
-        self.L.zbo_submit(self.h, cmds.ctypes.data, len(cmds), docs.ctypes.data, len(docs))
+        xp = np.ascontiguousarray(xparts if xparts is not None else abi.make_xparts(0), dtype=abi.XPART_DTYPE)
+        self.L.zbo_submit_ex(self.h, cmds.ctypes.data, len(cmds), docs.ctypes.data, len(docs), xp.ctypes.data,
+                             len(xp))
+
+    def intern_string(self, value):
+        b = value.encode() if isinstance(value, str) else value
+        return self.L.zbo_intern_string(self.h, b, len(b))
+
+    def outbox(self, clear=True):
+        n = self.L.zbo_outbox(self.h, None, 0)
+        out = abi.make_xparts(n)
+        self.L.zbo_outbox(self.h, out.ctypes.data, n)
+        if clear:
+            self.L.zbo_clear_outbox(self.h)
+        return out
 
     def run(self):
         r = self.L.zbo_run(self.h)
@@ -138,6 +162,16 @@ class Oracle:
         t, c, m = C.c_uint64(), C.c_uint64(), C.c_uint64()
         self.L.zbo_counters(self.h, C.byref(t), C.byref(c), C.byref(m))
         return {"transitions": t.value, "completed_instances": c.value, "commands": m.value}
+
+
+def subscription_partition(correlation_key, partition_count):
+    b = correlation_key.encode() if isinstance(correlation_key, str) else correlation_key
+    return lib().zbo_subscription_partition(b, len(b), partition_count)
+
+
+def java_hash(value):
+    b = value.encode() if isinstance(value, str) else value
+    return lib().zbo_java_hash(b, len(b))
 
 
 def bench(xml, threads, n_instances, phases, with_amount=False, seed=0x5EED03):

@@ -330,6 +330,7 @@ struct OEl {
   int default_flow = -1;
   std::string job_type;
   int retries = 3;
+  std::string msg_name, corr_var;  // message catch event (MessageTransformer.java:30-60)
 };
 
 struct OProc {
@@ -344,7 +345,9 @@ struct OProc {
 // with ModelWalker.walk (bpmn-model/.../traversal/ModelWalker.java:60-81): siblings are
 // pushed with addFirst, so sequence flows are connected in reverse document order
 // (SequenceFlowTransformer.connectWithFlowNodes), which fixes getOutgoing() order.
-static bool build_process(const XNode& proc, OProc& P, std::string& err) {
+using MessageDefs = std::unordered_map<std::string, std::pair<std::string, std::string>>;  // id -> (name, corr var)
+
+static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, std::string& err) {
   P.bpmn_id = proc.attr("id");
   P.els.clear();
   OEl pe;
@@ -393,6 +396,23 @@ static bool build_process(const XNode& proc, OProc& P, std::string& err) {
         err = "io mappings / task headers outside the supported subset";
         return false;
       }
+    } else if (n == "intermediateCatchEvent") {
+      // CatchEventTransformer.transformMessageEventDefinition (transformer/CatchEventTransformer.java:88-100)
+      e.type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
+      const XNode* med = k->child("messageEventDefinition");
+      if (!med || k->child("timerEventDefinition") || k->child("signalEventDefinition") ||
+          k->child("linkEventDefinition") || k->child("conditionalEventDefinition")) {
+        err = "intermediate catch event outside the supported subset (message only)";
+        return false;
+      }
+      auto mi = msgs.find(med->attr("messageRef"));
+      if (mi == msgs.end() || mi->second.first.empty() || mi->second.second.empty()) {
+        err = "message outside the supported subset (static name, `= variable` correlation key)";
+        return false;
+      }
+      e.event = ZBHIP_EV_MESSAGE;
+      e.msg_name = mi->second.first;
+      e.corr_var = mi->second.second;
     } else if (n == "exclusiveGateway") {
       e.type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
     } else if (n == "parallelGateway") {
@@ -498,15 +518,93 @@ struct VarRow {
   uint32_t doc_index;
 };
 
+// Message values (MessageSubscriptionRecord / ProcessMessageSubscriptionRecord / MessageRecord,
+// protocol-impl/.../record/value/message/*.java) in compact form, plus the routing handle of the
+// subscribing element instance (instance slot, key ordinal) that the cross-partition commands carry.
+struct MsgVal {
+  int64_t pik = -1, eik = -1, msg_key = -1;
+  uint32_t corr = ZBHIP_NO_STRING;
+  uint16_t name = 0xFFFF, bpmn = 0xFFFF;
+  int32_t partition = 0;
+  uint8_t interrupting = 0;
+  int proc = -1, elem = -1;  // PMS records that carry the elementId
+  uint32_t inst = 0;
+  uint16_t eord = 0;
+};
+
 // A command or event in flight (TypedRecord)
 struct ORecord {
   zbhip_record r;
+  MsgVal m;
   PiValue pi;          // for PI records
   Doc doc;             // variables carried (CREATE/JOB_COMPLETE/ VARIABLE entry)
   std::string reason;  // rejection reason
   uint32_t instance = 0;
   int32_t job_ord = -1;
+  bool slot = false;   // subject is the correlation slot `instance` (MESSAGE / MESSAGE_SUBSCRIPTION commands)
 };
+
+static void fill_msg(ORecord& rec, const MsgVal& m) {
+  rec.m = m;
+  rec.r.scope_key = m.eik;
+  rec.r.process_instance_key = m.pik;
+  rec.r.message_key = m.msg_key;
+  rec.r.correlation_key = m.corr;
+  rec.r.message_name = m.name;
+  rec.r.bpmn_process_id = m.bpmn;
+  rec.r.partition = m.partition;
+  rec.r.interrupting = m.interrupting;
+  rec.r.process_idx = m.proc;
+  rec.r.element_idx = m.elem;
+}
+
+static void xpart_kind(int kind, int& vt, int& intent) {
+  switch (kind) {
+    case ZBHIP_CMD_MSG_SUB_CREATE: vt = ZBHIP_VT_MESSAGE_SUBSCRIPTION; intent = ZBHIP_MS_CREATE; return;
+    case ZBHIP_CMD_MSG_SUB_CORRELATE: vt = ZBHIP_VT_MESSAGE_SUBSCRIPTION; intent = ZBHIP_MS_CORRELATE; return;
+    case ZBHIP_CMD_PMS_CREATE: vt = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; intent = ZBHIP_PMS_CREATE; return;
+    default: vt = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; intent = ZBHIP_PMS_CORRELATE; return;
+  }
+}
+
+// The record value each SubscriptionCommandSender method writes (SubscriptionCommandSender.java:54-338):
+// openMessageSubscription: pik, eik, bpmnProcessId, messageKey -1, name, correlationKey, interrupting;
+// openProcessMessageSubscription: subscriptionPartitionId = sender, pik, eik, messageKey -1, name, interrupting;
+// correlateProcessMessageSubscription: subscriptionPartitionId = sender, pik, eik, bpmnProcessId, messageKey,
+//   name, variables, correlationKey;  correlateMessageSubscription: pik, eik, bpmnProcessId, messageKey -1, name.
+static MsgVal command_value(int kind, const MsgVal& in, int sender) {
+  MsgVal m;
+  m.pik = in.pik;
+  m.eik = in.eik;
+  m.name = in.name;
+  m.inst = in.inst;
+  m.eord = in.eord;
+  switch (kind) {
+    case ZBHIP_CMD_MSG_SUB_CREATE:
+      m.bpmn = in.bpmn; m.corr = in.corr; m.interrupting = in.interrupting; break;
+    case ZBHIP_CMD_PMS_CREATE:
+      m.partition = sender; m.interrupting = in.interrupting; break;
+    case ZBHIP_CMD_PMS_CORRELATE:
+      m.partition = sender; m.bpmn = in.bpmn; m.msg_key = in.msg_key; m.corr = in.corr; break;
+    default:  // MSG_SUB_CORRELATE
+      m.bpmn = in.bpmn; break;
+  }
+  return m;
+}
+
+// SubscriptionUtil.getSubscriptionHashCode / getSubscriptionPartitionId
+// (protocol-impl/.../SubscriptionUtil.java:22-44): String#hashCode over SIGNED bytes, Java int
+// overflow, then abs(hash % partitionCount) + START_PARTITION_ID.
+static int32_t java_hash(const std::string& b) {
+  uint32_t h = 0;
+  for (char c : b) h = 31u * h + (uint32_t)(int32_t)(int8_t)c;
+  return (int32_t)h;
+}
+static int subscription_partition(const std::string& b, int partition_count) {
+  int32_t h = java_hash(b);
+  int32_t r = h % partition_count;
+  return (r < 0 ? -r : r) + 1;
+}
 
 struct Unsupported {
   std::string what;
@@ -523,7 +621,21 @@ class Oracle {
   std::vector<std::string> names;
   std::unordered_map<std::string, int> name_ids;
   std::vector<zbhip_doc_entry> docs;  // all submitted document entries (global index)
+  std::vector<zbhip_xpart_cmd> xdocs;  // all received cross-partition commands (global index)
+  std::vector<zbhip_xpart_cmd> outbox;  // sent cross-partition commands (post-commit side effects)
   std::string last_error;
+
+  // value dictionary (zbhip_intern_string)
+  std::vector<std::string> strs;
+  std::unordered_map<std::string, uint32_t> str_ids;
+  uint32_t intern_string(const std::string& v) {
+    auto it = str_ids.find(v);
+    if (it != str_ids.end()) return it->second;
+    uint32_t id = (uint32_t)strs.size();
+    strs.push_back(v);
+    str_ids.emplace(v, id);
+    return id;
+  }
 
   int intern(const std::string& n) {
     auto it = name_ids.find(n);
@@ -542,12 +654,45 @@ class Oracle {
     for (auto& k : root->kids)
       if (k->name == "process" && k->attr("isExecutable", "true") != "false") { proc = k.get(); break; }
     if (!proc) { last_error = "no executable process"; return ZBHIP_EPARSE; }
+    // <message> definitions: static name, correlation key `= variable` (MessageTransformer.java:30-60)
+    MessageDefs msgs;
+    for (auto& k : root->kids) {
+      if (k->name != "message") continue;
+      std::string nm = k->attr("name"), ck;
+      const XNode* ext = k->child("extensionElements");
+      const XNode* sub = ext ? ext->child("subscription") : nullptr;
+      if (sub) ck = sub->attr("correlationKey");
+      auto trim = [](std::string t) {
+        size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+        return a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+      };
+      ck = trim(ck);
+      std::string var;
+      if (ck.size() >= 2 && ck[0] == '=') {
+        var = trim(ck.substr(1));
+        bool ident = !var.empty() && (isalpha((unsigned char)var[0]) || var[0] == '_');
+        for (char ch : var) ident = ident && (isalnum((unsigned char)ch) || ch == '_');
+        if (!ident) var.clear();
+      }
+      if (!nm.empty() && nm[0] == '=') nm.clear();
+      msgs[k->attr("id")] = {nm, var};
+    }
     OProc P;
-    if (!build_process(*proc, P, last_error)) return ZBHIP_EUNSUPP;
+    if (!build_process(*proc, msgs, P, last_error)) return ZBHIP_EUNSUPP;
     P.def_key = def_key;
     P.version = version;
     // intern condition variable names now so ids match the product's deploy order
     for (auto& e : P.els) intern_vars(e.cond.get());
+    // message names, correlation variables and the bpmnProcessId of processes with message catch
+    // events go into the same name dictionary (the product's zbhip_deploy interns in this order)
+    bool has_msg = false;
+    for (auto& e : P.els)
+      if (e.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+        intern(e.msg_name);
+        intern(e.corr_var);
+        has_msg = true;
+      }
+    if (has_msg) intern(P.bpmn_id);
     procs.push_back(std::move(P));
     return (int)procs.size() - 1;
   }
@@ -560,9 +705,12 @@ class Oracle {
   }
 
   // Writes external commands to the log (the client side of EngineRule).
-  void submit(const zbhip_command* cmds, size_t n, const zbhip_doc_entry* d, size_t nd) {
+  void submit(const zbhip_command* cmds, size_t n, const zbhip_doc_entry* d, size_t nd,
+              const zbhip_xpart_cmd* xp = nullptr, size_t nx = 0) {
     uint32_t doc_base = (uint32_t)docs.size();
     docs.insert(docs.end(), d, d + nd);
+    uint32_t x_base = (uint32_t)xdocs.size();
+    if (nx) xdocs.insert(xdocs.end(), xp, xp + nx);
     for (size_t i = 0; i < n; ++i) {
       const zbhip_command& c = cmds[i];
       ORecord rec{};
@@ -576,11 +724,48 @@ class Oracle {
       rec.r.scope_key = -1;
       rec.r.process_instance_key = -1;
       rec.r.aux = c.doc_count ? (int64_t)(doc_base + c.doc_begin) : -1;
+      rec.r.message_key = -1;
+      rec.r.correlation_key = ZBHIP_NO_STRING;
+      rec.r.message_name = 0xFFFF;
+      rec.r.bpmn_process_id = 0xFFFF;
       if (c.kind == ZBHIP_CMD_CREATE) {
         rec.r.process_idx = c.ref;
         rec.r.value_type = ZBHIP_VT_PROCESS_INSTANCE_CREATION;
         rec.r.intent = ZBHIP_PIC_CREATE;
         rec.r.key = -1;
+      } else if (c.kind == ZBHIP_CMD_PUBLISH) {
+        // MessageRecord: name, correlationKey, timeToLive 0, no variables, no messageId
+        rec.doc = Doc{0, 0};
+        rec.r.aux = -1;
+        rec.r.value_type = ZBHIP_VT_MESSAGE;
+        rec.r.intent = ZBHIP_MSG_PUBLISH;
+        rec.r.key = -1;
+        rec.m.corr = c.instance;
+        rec.m.name = c.ref;
+        fill_msg(rec, rec.m);
+        rec.slot = true;
+      } else if (c.kind >= ZBHIP_CMD_MSG_SUB_CREATE && c.kind <= ZBHIP_CMD_MSG_SUB_CORRELATE) {
+        const zbhip_xpart_cmd& x = xdocs[x_base + c.doc_begin];
+        rec.doc = Doc{0, 0};
+        rec.r.aux = -1;
+        rec.r.key = -1;
+        MsgVal m;
+        m.eik = x.element_instance_key;
+        m.pik = x.process_instance_key;
+        m.msg_key = x.message_key;
+        m.corr = x.correlation_key;
+        m.name = x.message_name;
+        m.bpmn = x.bpmn_process_id;
+        m.interrupting = x.interrupting;
+        m.inst = x.instance;
+        m.eord = x.element_ord;
+        int vt, it;
+        xpart_kind(c.kind, vt, it);
+        rec.r.value_type = (uint8_t)vt;
+        rec.r.intent = (uint8_t)it;
+        rec.m = command_value(c.kind, m, x.source_partition);
+        fill_msg(rec, rec.m);
+        rec.slot = c.kind == ZBHIP_CMD_MSG_SUB_CREATE || c.kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
       } else {
         rec.r.value_type = ZBHIP_VT_JOB;
         rec.r.intent = ZBHIP_JOB_COMPLETE;
@@ -615,6 +800,7 @@ class Oracle {
 
   // key ordinal lookup: per instance slot, every key generated in its batches
   std::unordered_map<uint32_t, std::vector<int64_t>> inst_keys;
+  std::unordered_map<uint32_t, std::vector<int64_t>> slot_keys;  // keys generated by correlation slots
 
   int64_t resolve(uint32_t inst, uint32_t ord) {
     auto it = inst_keys.find(inst);
@@ -643,9 +829,19 @@ class Oracle {
   std::map<int64_t, JobRow> jobs_;                              // JOBS (+ JOB_STATES = ACTIVATABLE)
   std::set<std::tuple<std::string, std::string, int64_t>> activatable_;  // JOB_ACTIVATABLE
 
+  // --- message state (ZbColumnFamilies PROCESS_SUBSCRIPTION_BY_KEY, MESSAGE_SUBSCRIPTION_BY_KEY,
+  // MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY, MESSAGE_STATS) ---
+  struct PmsRow { int64_t key; bool opened; MsgVal rec; };
+  struct MsgSub { int64_t key; bool correlating; MsgVal rec; };
+  std::map<std::pair<int64_t, int>, PmsRow> pms_;                        // [eik, name]
+  std::map<std::pair<int64_t, int>, MsgSub> msub_;                       // [eik, name]
+  std::set<std::tuple<int, uint32_t, int64_t>> msub_by_corr_;           // [name, corr, eik]
+  bool msg_stats_ = false;                                               // messagesDeadlineCount row
+
   // --- batch context ---
   std::vector<ORecord>* batch_ = nullptr;
   uint32_t cur_instance_ = 0;
+  bool cur_slot_ = false;   // keys of the batch so far belong to the correlation slot cur_instance_
   int64_t cur_source_ = 0;
 
   // DbKeyGenerator.nextKey (stream-platform/.../state/DbKeyGenerator.java:39-42) with
@@ -653,8 +849,20 @@ class Oracle {
   int64_t next_key() {
     ++key_counter_;
     int64_t k = ((int64_t)partition_ << 51) + key_counter_;
-    inst_keys[cur_instance_].push_back(k);
+    (cur_slot_ ? slot_keys : inst_keys)[cur_instance_].push_back(k);
     return k;
+  }
+  // key ordinal of `key` within the instance slot `inst` (routing handle of the xpart commands)
+  uint16_t ord_of(uint32_t inst, int64_t key) {
+    auto& v = inst_keys[inst];
+    for (size_t i = v.size(); i-- > 0;)
+      if (v[i] == key) return (uint16_t)i;
+    throw Unsupported{"routing handle of an unknown key"};
+  }
+  // switches the batch to the subject instance `inst` (a PI command inside a message batch)
+  void enter_instance(uint32_t inst) {
+    cur_slot_ = false;
+    cur_instance_ = inst;
   }
 
   const OProc& P(int proc) const { return procs[proc]; }
@@ -675,7 +883,12 @@ class Oracle {
     rec.r.element_idx = -1;
     rec.r.scope_key = -1;
     rec.r.process_instance_key = -1;
+    rec.r.message_key = -1;
+    rec.r.correlation_key = ZBHIP_NO_STRING;
+    rec.r.message_name = 0xFFFF;
+    rec.r.bpmn_process_id = 0xFFFF;
     rec.instance = cur_instance_;
+    rec.slot = cur_slot_;
     batch_->push_back(std::move(rec));
     return batch_->back();
   }
@@ -715,6 +928,13 @@ class Oracle {
     rec.r.scope_key = cmd.r.scope_key;
     rec.r.process_instance_key = cmd.r.process_instance_key;
     rec.r.aux = cmd.r.aux;
+    rec.r.message_key = cmd.r.message_key;
+    rec.r.correlation_key = cmd.r.correlation_key;
+    rec.r.message_name = cmd.r.message_name;
+    rec.r.bpmn_process_id = cmd.r.bpmn_process_id;
+    rec.r.partition = cmd.r.partition;
+    rec.r.interrupting = cmd.r.interrupting;
+    rec.m = cmd.m;
     rec.pi = cmd.pi;
     rec.doc = cmd.doc;
     rec.reason = reason;
@@ -728,6 +948,7 @@ class Oracle {
     std::vector<ORecord> batch;
     batch_ = &batch;
     cur_instance_ = initial.instance;
+    cur_slot_ = initial.slot;
     cur_source_ = initial.r.source_index;
     std::deque<ORecord> pending;
     pending.push_back(initial);
@@ -768,8 +989,209 @@ class Oracle {
       complete_job(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE)
       bpmn_process_record(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_MESSAGE && cmd.r.intent == ZBHIP_MSG_PUBLISH)
+      publish_message(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_MS_CREATE)
+      message_subscription_create(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_MS_CORRELATE)
+      message_subscription_correlate(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_PMS_CREATE)
+      process_message_subscription_create(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_PMS_CORRELATE)
+      process_message_subscription_correlate(cmd);
     else
       throw Unsupported{"value type"};
+  }
+
+  // =====================================================================
+  // Message correlation
+  // =====================================================================
+  ORecord& msg_record(int rt, int vt, int intent, int64_t key, const MsgVal& m) {
+    ORecord& r = append(rt, vt, intent, key);
+    fill_msg(r, m);
+    return r;
+  }
+
+  // SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition (:304-320): the receiver's own
+  // partition -> a follow-up command in this batch (key -1); another partition -> a post-commit side
+  // effect (InterPartitionCommandSender.sendCommand), collected in the outbox in batch order.
+  void send_command(int target, int kind, const MsgVal& in) {
+    MsgVal v = command_value(kind, in, partition_);
+    int vt, it;
+    xpart_kind(kind, vt, it);
+    if (target == partition_) {
+      ORecord& r = msg_record(ZBHIP_RT_COMMAND, vt, it, -1, v);
+      r.slot = false;
+      return;
+    }
+    zbhip_xpart_cmd x{};
+    x.element_instance_key = in.eik;
+    x.process_instance_key = in.pik;
+    x.message_key = v.msg_key;
+    x.correlation_key = in.corr;  // routing: the correlation slot on the message partition
+    x.instance = in.inst;
+    x.element_ord = in.eord;
+    x.message_name = in.name;
+    x.bpmn_process_id = in.bpmn;
+    x.kind = (uint8_t)kind;
+    x.interrupting = in.interrupting;
+    x.source_partition = (int16_t)partition_;
+    x.target_partition = (int16_t)target;
+    outbox.push_back(x);
+  }
+
+  static int partition_of_key(int64_t key) { return (int)(key >> 51); }  // Protocol.decodePartitionId
+
+  // CatchEventBehavior.subscribeToEvents -> subscribeToMessageEvent (processing/common/CatchEventBehavior.java:111-125,248-283)
+  void subscribe_to_message(const OEl& el, int64_t key, const PiValue& v) {
+    // evaluateCorrelationKey (:155-178) -> ExpressionProcessor.evaluateMessageCorrelationKeyExpression
+    // (processing/common/ExpressionProcessor.java:309-337): STRING or NUMBER, else incident
+    auto nit = name_ids.find(el.corr_var);
+    const VarRow* vr = nit == name_ids.end() ? nullptr : lookup_var(key, nit->second);
+    if (!vr || vr->type != ZBHIP_DOC_STR)
+      throw Unsupported{"correlation key is not a string (incident, or a NUMBER outside the subset)"};
+    MsgVal m;
+    m.corr = (uint32_t)vr->value;
+    m.name = (uint16_t)intern(el.msg_name);
+    m.bpmn = (uint16_t)intern(P(v.proc).bpmn_id);
+    m.pik = v.piKey;
+    m.eik = key;
+    m.partition = subscription_partition(strs.at(m.corr), partition_count_);
+    m.interrupting = 1;  // intermediate catch events interrupt (ExecutableCatchEvent.java:36-38)
+    m.proc = v.proc;
+    m.elem = v.elem;
+    m.inst = cur_instance_;
+    m.eord = ord_of(cur_instance_, key);
+    for (auto& [k2, row] : pms_)
+      if (row.rec.inst == cur_instance_) throw Unsupported{"second open message subscription of an instance"};
+    int64_t subKey = next_key();
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_CREATING, subKey, m);
+    pms_[{key, (int)m.name}] = PmsRow{subKey, false, m};  // ProcessMessageSubscriptionCreatingApplier
+    send_command(m.partition, ZBHIP_CMD_MSG_SUB_CREATE, m);
+  }
+
+  // MessageSubscriptionCreateProcessor.processRecord (processing/message/MessageSubscriptionCreateProcessor.java:66-104)
+  void message_subscription_create(ORecord& cmd) {
+    const MsgVal c = cmd.m;
+    MsgVal ack = c;
+    if (msub_.count({c.eik, (int)c.name})) {
+      send_command(partition_of_key(c.pik), ZBHIP_CMD_PMS_CREATE, ack);
+      reject(cmd, ZBHIP_REJ_INVALID_STATE,
+             "Expected to open a new message subscription for element with key '" + std::to_string(c.eik) +
+                 "' and message name '" + names.at(c.name) +
+                 "', but there is already a message subscription for that element key and message name opened");
+      return;
+    }
+    int64_t k = next_key();
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_CREATED, k, c);
+    msub_[{c.eik, (int)c.name}] = MsgSub{k, false, c};  // MessageSubscriptionCreatedApplier
+    msub_by_corr_.insert({(int)c.name, c.corr, c.eik});
+    // MessageCorrelator.correlateNextMessage: a message outlives its PUBLISH batch only with a
+    // positive time-to-live, which the subset excludes -> nothing buffered to correlate
+    send_command(partition_of_key(c.pik), ZBHIP_CMD_PMS_CREATE, ack);
+  }
+
+  // ProcessMessageSubscriptionCreateProcessor.processRecord
+  void process_message_subscription_create(ORecord& cmd) {
+    if (cmd.r.record_type == ZBHIP_RT_COMMAND && cur_slot_) enter_instance(cmd.m.inst);
+    const MsgVal c = cmd.m;
+    auto it = pms_.find({c.eik, (int)c.name});
+    if (it != pms_.end() && !it->second.opened) {
+      msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_CREATED, it->second.key, it->second.rec);
+      it->second.opened = true;  // ProcessMessageSubscriptionCreatedApplier.updateToOpenedState
+      return;
+    }
+    const std::string base = "Expected to create process message subscription with element key '" +
+                             std::to_string(c.eik) + "' and message name '" + names.at(c.name) + "', but ";
+    if (it == pms_.end()) reject(cmd, ZBHIP_REJ_NOT_FOUND, base + "no such subscription was found");
+    else reject(cmd, ZBHIP_REJ_INVALID_STATE, base + "it is already opened");
+  }
+
+  // MessagePublishProcessor.processRecord / handleNewMessage (processing/message/MessagePublishProcessor.java)
+  void publish_message(ORecord& cmd) {
+    const MsgVal c = cmd.m;  // name, correlationKey (no messageId, TTL 0, no variables)
+    int64_t msgKey = next_key();
+    MsgVal mv;
+    mv.name = c.name;
+    mv.corr = c.corr;
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE, ZBHIP_MSG_PUBLISHED, msgKey, mv);
+    msg_stats_ = true;  // MessagePublishedApplier -> DbMessageState.put: messagesDeadlineCount upsert
+    // correlateToSubscriptions: visit [tenant, name, correlationKey, *] in element-instance-key order
+    std::vector<MsgVal> correlating;
+    std::set<int> bpmn_seen;
+    for (auto it = msub_by_corr_.lower_bound({(int)c.name, c.corr, INT64_MIN}); it != msub_by_corr_.end(); ++it) {
+      if (std::get<0>(*it) != (int)c.name || std::get<1>(*it) != c.corr) break;
+      MsgSub& sub = msub_.at({std::get<2>(*it), (int)c.name});
+      if (sub.correlating || bpmn_seen.count(sub.rec.bpmn)) continue;
+      sub.rec.msg_key = msgKey;
+      msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_CORRELATING, sub.key, sub.rec);
+      sub.correlating = true;  // MessageSubscriptionCorrelatingApplier (+ transient message correlation)
+      bpmn_seen.insert(sub.rec.bpmn);
+      correlating.push_back(sub.rec);
+    }
+    // sendCorrelateCommand: correlateProcessMessageSubscription with the message's name and key
+    for (MsgVal m : correlating) {
+      m.msg_key = msgKey;
+      m.name = c.name;
+      m.corr = c.corr;
+      send_command(partition_of_key(m.pik), ZBHIP_CMD_PMS_CORRELATE, m);
+    }
+    // timeToLive <= 0: EXPIRED in the same batch; MessageExpiredApplier removes the message and its
+    // MESSAGE_CORRELATED rows (DbMessageState.remove :314-349)
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE, ZBHIP_MSG_EXPIRED, msgKey, mv);
+  }
+
+  // ProcessMessageSubscriptionCorrelateProcessor.processRecord
+  void process_message_subscription_correlate(ORecord& cmd) {
+    if (cur_slot_) enter_instance(cmd.m.inst);
+    const MsgVal c = cmd.m;
+    auto it = pms_.find({c.eik, (int)c.name});
+    if (it == pms_.end()) throw Unsupported{"PMS correlate rejection (MESSAGE_SUBSCRIPTION:REJECT outside the subset)"};
+    auto eit = ei_.find(c.eik);
+    // EventHandle.canTriggerElement: active instance, event scope accepting, flow scope not interrupted
+    if (eit == ei_.end() || eit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED || !event_scope_.count(c.eik))
+      throw Unsupported{"PMS correlate rejection (no event occurred)"};
+    MsgVal m = c;  // record.setElementId(subscription elementId).setInterrupting(...)
+    m.interrupting = it->second.rec.interrupting;
+    m.proc = it->second.rec.proc;
+    m.elem = it->second.rec.elem;
+    const int64_t subKey = it->second.key;
+    const bool interrupting = it->second.rec.interrupting;
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_CORRELATED, subKey, m);
+    if (interrupting) pms_.erase(it);  // ProcessMessageSubscriptionCorrelatedApplier
+    else throw Unsupported{"non-interrupting subscription"};
+    // EventHandle.activateElement (processing/common/EventHandle.java:109-150)
+    const ElementInstance inst = eit->second;
+    int64_t eventKey = next_key();
+    ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
+    pe.r.process_idx = inst.value.proc;
+    pe.r.element_idx = inst.value.elem;
+    pe.r.scope_key = c.eik;
+    pe.r.process_instance_key = inst.value.piKey;
+    if (event_scope_.count(c.eik))  // ProcessEventTriggeringApplier: trigger with the message variables (none)
+      triggers_[{c.eik, eventKey}] = EventTrigger{inst.value.elem, inst.value.proc, Doc{0, 0}, inst.value.piKey};
+    pi_command(c.eik, ZBHIP_PI_COMPLETE_ELEMENT, inst.value);  // isElementActivated: intermediate catch
+    // sendAcknowledgeCommand -> correlateMessageSubscription(record.subscriptionPartitionId, ...)
+    MsgVal ack = c;
+    ack.corr = it == pms_.end() ? c.corr : c.corr;
+    send_command(c.partition, ZBHIP_CMD_MSG_SUB_CORRELATE, ack);
+  }
+
+  // MessageSubscriptionCorrelateProcessor.processRecord
+  void message_subscription_correlate(ORecord& cmd) {
+    const MsgVal c = cmd.m;
+    auto it = msub_.find({c.eik, (int)c.name});
+    if (it == msub_.end()) {
+      reject(cmd, ZBHIP_REJ_NOT_FOUND,
+             "Expected to correlate subscription for element with key '" + std::to_string(c.eik) +
+                 "' and message name '" + names.at(c.name) + "', but no such message subscription exists");
+      return;
+    }
+    const MsgSub sub = it->second;
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_CORRELATED, sub.key, sub.rec);
+    if (!sub.rec.interrupting) throw Unsupported{"non-interrupting message subscription"};
+    msub_by_corr_.erase({(int)sub.rec.name, sub.rec.corr, sub.rec.eik});  // MessageSubscriptionCorrelatedApplier
+    msub_.erase(it);
   }
 
   // ---------------------------------------------------------------------
@@ -1083,6 +1505,12 @@ class Oracle {
         if (flow >= 0) take_sequence_flow(key, v, flow);
         break;
       }
+      case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT:
+        // IntermediateCatchEventProcessor.DefaultIntermediateCatchEventBehavior.onActivate
+        // (processing/bpmn/event/IntermediateCatchEventProcessor.java): subscribeToEvents, then ACTIVATED
+        subscribe_to_message(el, key, v);
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        break;
       case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (processing/bpmn/gateway/ParallelGatewayProcessor.java:34-50)
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         pi_event(key, ZBHIP_PI_ELEMENT_COMPLETING, v);
@@ -1105,6 +1533,15 @@ class Oracle {
       case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onComplete (:63-75)
         complete_and_take(el, key, v, true);
         break;
+      case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT: {
+        // IntermediateCatchEventProcessor.onComplete: applyOutputMappings, unsubscribeFromEvents
+        // (CatchEventBehavior.unsubscribeFromMessageEvents visits the element's remaining process
+        // message subscriptions: none after an interrupting correlation), transitionToCompleted
+        for (auto& [k2, row] : pms_)
+          if (k2.first == key) throw Unsupported{"unsubscribe (PROCESS_MESSAGE_SUBSCRIPTION:DELETING)"};
+        complete_and_take(el, key, v, true);
+        break;
+      }
       default:
         throw Unsupported{"complete of element without wait state"};
     }
@@ -1244,7 +1681,7 @@ class Oracle {
     switch (intent) {
       case ZBHIP_PI_ELEMENT_ACTIVATING: {  // ProcessInstanceElementActivatingApplier.applyState (:48-77)
         // createEventScope (:255-289): job worker elements get an event scope
-        if (el.type == ZBHIP_EL_SERVICE_TASK) event_scope_.insert(key);
+        if (el.type == ZBHIP_EL_SERVICE_TASK || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) event_scope_.insert(key);
         // cleanupSequenceFlowsTaken (:79-98): Tetris decrement of (flowScope, gateway)
         if (el.type == ZBHIP_EL_PARALLEL_GATEWAY) {
           for (auto it = taken_.lower_bound({v.flowScopeKey, v.elem, -1}); it != taken_.end();) {
@@ -1396,6 +1833,33 @@ std::string Oracle::dump_state() const {
     snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|%s|%lld", t.c_str(), ten.c_str(), (long long)k);
     rows.push_back(buf);
   }
+  auto nm = [this](int id) -> const char* { return id >= 0 && id < (int)names.size() ? names[id].c_str() : ""; };
+  auto sv = [this](uint32_t id) -> const char* { return id < strs.size() ? strs[id].c_str() : ""; };
+  for (auto& [k, row] : pms_) {
+    const MsgVal& m = row.rec;
+    snprintf(buf, sizeof buf,
+             "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%d,processInstanceKey=%lld,"
+             "bpmnProcessId=%s,messageKey=%lld,correlationKey=%s,elementId=%s,interrupting=%d",
+             (long long)k.first, nm(k.second), (long long)row.key, row.opened ? "OPENED" : "OPENING", m.partition,
+             (long long)m.pik, nm(m.bpmn), (long long)m.msg_key, sv(m.corr), procs[m.proc].els[m.elem].id.c_str(),
+             m.interrupting);
+    rows.push_back(buf);
+  }
+  for (auto& [k, sub] : msub_) {
+    const MsgVal& m = sub.rec;
+    snprintf(buf, sizeof buf,
+             "MESSAGE_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,correlating=%d,processInstanceKey=%lld,bpmnProcessId=%s,"
+             "messageKey=%lld,correlationKey=%s,interrupting=%d",
+             (long long)k.first, nm(k.second), (long long)sub.key, sub.correlating ? 1 : 0, (long long)m.pik,
+             nm(m.bpmn), (long long)m.msg_key, sv(m.corr), m.interrupting);
+    rows.push_back(buf);
+  }
+  for (auto& [n, c, e] : msub_by_corr_) {
+    snprintf(buf, sizeof buf, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY|<default>|%s|%s|%lld", nm(n), sv(c),
+             (long long)e);
+    rows.push_back(buf);
+  }
+  if (msg_stats_) rows.push_back("MESSAGE_STATS|messagesDeadlineCount|0");
   std::sort(rows.begin(), rows.end());
   std::string s;
   for (auto& r : rows) { s += r; s += '\n'; }
@@ -1432,6 +1896,25 @@ int zbo_submit(void* o, const zbhip_command* cmds, size_t n, const zbhip_doc_ent
   static_cast<Oracle*>(o)->submit(cmds, n, docs, nd);
   return 0;
 }
+int zbo_submit_ex(void* o, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs, size_t nd,
+                  const zbhip_xpart_cmd* xp, size_t nx) {
+  static_cast<Oracle*>(o)->submit(cmds, n, docs, nd, xp, nx);
+  return 0;
+}
+int64_t zbo_intern_string(void* o, const char* b, size_t len) {
+  return static_cast<Oracle*>(o)->intern_string(std::string(b, len));
+}
+size_t zbo_outbox(void* o, zbhip_xpart_cmd* out, size_t cap) {
+  auto* O = static_cast<Oracle*>(o);
+  size_t n = std::min(cap, O->outbox.size());
+  for (size_t i = 0; i < n; ++i) out[i] = O->outbox[i];
+  return O->outbox.size();
+}
+void zbo_clear_outbox(void* o) { static_cast<Oracle*>(o)->outbox.clear(); }
+int zbo_subscription_partition(const char* b, size_t len, int partition_count) {
+  return subscription_partition(std::string(b, len), partition_count);
+}
+int32_t zbo_java_hash(const char* b, size_t len) { return java_hash(std::string(b, len)); }
 int zbo_run(void* o) { return static_cast<Oracle*>(o)->run(); }
 
 size_t zbo_n_records(void* o) { return static_cast<Oracle*>(o)->out.size(); }

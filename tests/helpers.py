@@ -10,7 +10,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = os.path.join(HERE, "golden")
 
 VT_SHORT = {abi.VT_PROCESS_INSTANCE: "PI", abi.VT_PROCESS_INSTANCE_CREATION: "PIC", abi.VT_JOB: "JOB",
-            abi.VT_VARIABLE: "VAR", abi.VT_PROCESS_EVENT: "PE"}
+            abi.VT_VARIABLE: "VAR", abi.VT_PROCESS_EVENT: "PE", abi.VT_MESSAGE: "MSG",
+            abi.VT_MESSAGE_SUBSCRIPTION: "MS", abi.VT_PROCESS_MESSAGE_SUBSCRIPTION: "PMS"}
 RT_SHORT = {abi.RT_EVENT: "E", abi.RT_COMMAND: "C", abi.RT_REJECTION: "R"}
 
 
@@ -29,6 +30,9 @@ def process_xml(spec):
 def sym_key(k, partition=1):
     if k < 0:
         return -1
+    p = k >> 51
+    if p != partition:
+        return "p%dk%d" % (p, k - (p << 51))
     return "k%d" % (k - (partition << 51))
 
 
@@ -85,3 +89,115 @@ def amount_docs(values, name_id, decimal=False):
     d["type"] = abi.DOC_DEC if decimal else abi.DOC_INT
     d["value"] = np.asarray(values, dtype=np.int64)
     return d
+
+
+def load_appendix_a5():
+    with open(os.path.join(GOLDEN, "appendix_a5.json")) as f:
+        return json.load(f)
+
+
+def string_docs(name_id, string_ids):
+    d = abi.make_docs(len(string_ids))
+    d["name_id"] = name_id
+    d["type"] = abi.DOC_STR
+    d["value"] = np.asarray(string_ids, dtype=np.int64)
+    return d
+
+
+def publish_commands(string_ids, name_id):
+    c = abi.make_commands(len(string_ids))
+    c["instance"] = np.asarray(string_ids, dtype=np.uint32)
+    c["kind"] = abi.CMD_PUBLISH
+    c["ref"] = name_id
+    return c
+
+
+class MessageCluster:
+    """Config 5 driver over P partitions (oracles or GPU partitions, same interface through
+    `adapter`): create instances, run the subscription exchange to quiescence, publish one
+    message per correlation key on its message partition, exchange again.  Every window's
+    records and outbox are logged per partition in order, so two clusters fed the same inputs
+    can be compared step by step."""
+
+    def __init__(self, parts, adapter, xml, message_name="msg", var="key"):
+        self.parts = parts
+        self.P = len(parts)
+        self.ad = adapter
+        for p in parts:
+            adapter.deploy(p, xml)
+        self.name_id = adapter.intern(parts[0], message_name)
+        self.var_id = adapter.intern(parts[0], var)
+        for p in parts:
+            assert adapter.intern(p, message_name) == self.name_id and adapter.intern(p, var) == self.var_id
+        self.log = []  # (phase, partition, records, outbox)
+
+    def intern_keys(self, keys):
+        ids = None
+        for p in self.parts:
+            got = [self.ad.intern_string(p, k) for k in keys]
+            assert ids is None or got == ids  # replicated dictionary
+            ids = got
+        return ids
+
+    def _run(self, phase, p, cmds, docs=None, xparts=None):
+        recs, ob = self.ad.window(self.parts[p - 1], cmds, docs, xparts)
+        self.log.append((phase, p, recs, ob))
+        return ob
+
+    def exchange(self, phase, outboxes):
+        from zeebe_amd.exchange import route, window_from_xparts
+        rounds = 0
+        while any(len(o) for o in outboxes):
+            inbox = route(outboxes, self.P)
+            outboxes = [abi.make_xparts(0) for _ in range(self.P)]
+            for t in range(1, self.P + 1):
+                if len(inbox[t - 1]):
+                    cmds, xp = window_from_xparts(inbox[t - 1])
+                    outboxes[t - 1] = self._run(phase, t, cmds, None, xp)
+            rounds += 1
+            assert rounds < 8
+        return rounds
+
+    def create(self, instances_per_partition, keys):
+        """keys[p-1][i] = correlation key string of instance i on partition p."""
+        outboxes = []
+        for p in range(1, self.P + 1):
+            n = instances_per_partition
+            ids = keys[p - 1]
+            cmds = create_commands(n)
+            cmds["doc_count"] = 1
+            cmds["doc_begin"] = np.arange(n, dtype=np.uint32)
+            outboxes.append(self._run("create", p, cmds, string_docs(self.var_id, ids)))
+        self.exchange("subscribe", outboxes)
+
+    def publish(self, key_ids, key_partition):
+        """key_partition[i] = message partition of key_ids[i] (SubscriptionUtil)."""
+        outboxes = []
+        for p in range(1, self.P + 1):
+            mine = [k for k, q in zip(key_ids, key_partition) if q == p]
+            if mine:
+                outboxes.append(self._run("publish", p, publish_commands(mine, self.name_id)))
+            else:
+                outboxes.append(abi.make_xparts(0))
+        self.exchange("correlate", outboxes)
+
+
+class OracleAdapter:
+    @staticmethod
+    def deploy(p, xml):
+        return p.deploy(xml)
+
+    @staticmethod
+    def intern(p, name):
+        return p.intern(name)
+
+    @staticmethod
+    def intern_string(p, s):
+        return p.intern_string(s)
+
+    @staticmethod
+    def window(p, cmds, docs, xparts):
+        p.clear_records()
+        p.submit(cmds, docs, xparts)
+        p.run()
+        return p.records(), p.outbox()

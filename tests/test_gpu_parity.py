@@ -12,7 +12,7 @@ from zeebe_amd.engine import EngineRule, Partition
 
 pytestmark = pytest.mark.gpu
 
-FIELDS = [f for f in abi.RECORD_DTYPE.names if f not in ("reason", "reason_arg")]
+FIELDS = abi.PARITY_FIELDS
 
 
 def assert_same_records(got, want, part=None, orc=None):

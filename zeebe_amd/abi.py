@@ -33,6 +33,15 @@ JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED = 0, 1, 2
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
 PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
 PIC_INTENTS = {0: "CREATE", 1: "CREATED"}
+# MessageIntent / MessageSubscriptionIntent / ProcessMessageSubscriptionIntent
+MSG_INTENTS = {0: "PUBLISH", 1: "PUBLISHED", 2: "EXPIRE", 3: "EXPIRED"}
+MS_INTENTS = {0: "CREATE", 1: "CREATED", 2: "CORRELATE", 3: "CORRELATED", 4: "REJECT", 5: "REJECTED",
+              6: "DELETE", 7: "DELETED", 8: "CORRELATING"}
+PMS_INTENTS = {0: "CREATING", 1: "CREATE", 2: "CREATED", 3: "CORRELATE", 4: "CORRELATED", 5: "DELETING",
+               6: "DELETE", 7: "DELETED"}
+MSG_PUBLISH, MSG_PUBLISHED, MSG_EXPIRED = 0, 1, 3
+MS_CREATE, MS_CREATED, MS_CORRELATE, MS_CORRELATED, MS_CORRELATING = 0, 1, 2, 3, 8
+PMS_CREATING, PMS_CREATE, PMS_CREATED, PMS_CORRELATE, PMS_CORRELATED = 0, 1, 2, 3, 4
 VALUE_TYPES = {0: "JOB", 5: "PROCESS_INSTANCE", 10: "MESSAGE", 11: "MESSAGE_SUBSCRIPTION",
                12: "PROCESS_MESSAGE_SUBSCRIPTION", 17: "VARIABLE", 19: "PROCESS_INSTANCE_CREATION",
                24: "PROCESS_EVENT"}
@@ -49,13 +58,18 @@ EVENT_TYPES = ["UNSPECIFIED", "CONDITIONAL", "ERROR", "ESCALATION", "LINK", "MES
 
 def intent_name(value_type, intent):
     table = {VT_PROCESS_INSTANCE: PI_INTENTS, VT_JOB: JOB_INTENTS, VT_VARIABLE: VAR_INTENTS,
-             VT_PROCESS_EVENT: PE_INTENTS, VT_PROCESS_INSTANCE_CREATION: PIC_INTENTS}.get(value_type, {})
+             VT_PROCESS_EVENT: PE_INTENTS, VT_PROCESS_INSTANCE_CREATION: PIC_INTENTS, VT_MESSAGE: MSG_INTENTS,
+             VT_MESSAGE_SUBSCRIPTION: MS_INTENTS, VT_PROCESS_MESSAGE_SUBSCRIPTION: PMS_INTENTS}.get(value_type, {})
     return table.get(intent, str(intent))
 
 
 CMD_CREATE = 1
 CMD_JOB_COMPLETE = 2
-DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER = 0, 1, 2, 3, 4
+CMD_PUBLISH = 3
+CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE = 4, 5, 6, 7
+XPART_KINDS = (CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE)
+DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR = 0, 1, 2, 3, 4, 5
+NO_STRING = 0xFFFFFFFF
 DEC_SCALE = 6
 
 RUN_NO_RESULTS = 1
@@ -77,14 +91,25 @@ class Record(C.Structure):
                 ("source_index", C.c_int64), ("process_idx", C.c_int32), ("element_idx", C.c_int32),
                 ("record_type", C.c_uint8), ("value_type", C.c_uint8), ("intent", C.c_uint8),
                 ("rejection_type", C.c_uint8), ("ordinal", C.c_uint16), ("reason", C.c_uint8),
-                ("reason_arg", C.c_uint8), ("aux", C.c_int64)]
+                ("reason_arg", C.c_uint8), ("aux", C.c_int64), ("message_key", C.c_int64),
+                ("correlation_key", C.c_uint32), ("message_name", C.c_uint16), ("bpmn_process_id", C.c_uint16),
+                ("partition", C.c_int32), ("interrupting", C.c_uint8), ("pad", C.c_uint8 * 3)]
+
+
+class XpartCmd(C.Structure):
+    _fields_ = [("element_instance_key", C.c_int64), ("process_instance_key", C.c_int64),
+                ("message_key", C.c_int64), ("correlation_key", C.c_uint32), ("instance", C.c_uint32),
+                ("element_ord", C.c_uint16), ("message_name", C.c_uint16), ("bpmn_process_id", C.c_uint16),
+                ("kind", C.c_uint8), ("interrupting", C.c_uint8), ("source_partition", C.c_int16),
+                ("target_partition", C.c_int16), ("pad", C.c_uint32)]
 
 
 class Config(C.Structure):
     _fields_ = [("partition_id", C.c_int32), ("partition_count", C.c_int32), ("device", C.c_int32),
                 ("max_commands_in_batch", C.c_int32), ("max_instances", C.c_uint32),
                 ("max_commands", C.c_uint32), ("max_records_per_batch", C.c_uint32),
-                ("max_doc_entries", C.c_uint32), ("initial_key", C.c_int64), ("stream", C.c_void_p)]
+                ("max_doc_entries", C.c_uint32), ("initial_key", C.c_int64), ("max_correlation_keys", C.c_uint32),
+                ("pad", C.c_uint32), ("stream", C.c_void_p)]
 
 
 class Stats(C.Structure):
@@ -101,11 +126,22 @@ RECORD_DTYPE = np.dtype([("key", "<i8"), ("scope_key", "<i8"), ("process_instanc
                          ("source_index", "<i8"), ("process_idx", "<i4"), ("element_idx", "<i4"),
                          ("record_type", "u1"), ("value_type", "u1"), ("intent", "u1"),
                          ("rejection_type", "u1"), ("ordinal", "<u2"), ("reason", "u1"), ("reason_arg", "u1"),
-                         ("aux", "<i8")])
+                         ("aux", "<i8"), ("message_key", "<i8"), ("correlation_key", "<u4"),
+                         ("message_name", "<u2"), ("bpmn_process_id", "<u2"), ("partition", "<i4"),
+                         ("interrupting", "u1"), ("pad", "u1", (3,))])
+XPART_DTYPE = np.dtype([("element_instance_key", "<i8"), ("process_instance_key", "<i8"), ("message_key", "<i8"),
+                        ("correlation_key", "<u4"), ("instance", "<u4"), ("element_ord", "<u2"),
+                        ("message_name", "<u2"), ("bpmn_process_id", "<u2"), ("kind", "u1"),
+                        ("interrupting", "u1"), ("source_partition", "<i2"), ("target_partition", "<i2"),
+                        ("pad", "<u4")])
 
 assert COMMAND_DTYPE.itemsize == C.sizeof(Command) == 16
 assert DOC_DTYPE.itemsize == C.sizeof(DocEntry) == 16
-assert RECORD_DTYPE.itemsize == C.sizeof(Record) == 56
+assert RECORD_DTYPE.itemsize == C.sizeof(Record) == 80
+assert XPART_DTYPE.itemsize == C.sizeof(XpartCmd) == 48
+
+# fields compared between the GPU path and the oracle (the rejection reason is compared as text)
+PARITY_FIELDS = [f for f in RECORD_DTYPE.names if f not in ("reason", "reason_arg", "pad")]
 
 
 def make_commands(n):
@@ -116,8 +152,14 @@ def make_docs(n):
     return np.zeros(n, dtype=DOC_DTYPE)
 
 
+def make_xparts(n):
+    return np.zeros(n, dtype=XPART_DTYPE)
+
+
 def record_tuple(r, element_id=None, name=None):
     """Canonical comparable tuple of one drained record (numpy row or ctypes Record)."""
     return (int(r["source_index"]), int(r["ordinal"]), int(r["record_type"]), int(r["value_type"]),
             int(r["intent"]), int(r["rejection_type"]), int(r["key"]), int(r["scope_key"]),
-            int(r["process_instance_key"]), int(r["process_idx"]), int(r["element_idx"]), int(r["aux"]))
+            int(r["process_instance_key"]), int(r["process_idx"]), int(r["element_idx"]), int(r["aux"]),
+            int(r["message_key"]), int(r["correlation_key"]), int(r["message_name"]), int(r["bpmn_process_id"]),
+            int(r["partition"]), int(r["interrupting"]))

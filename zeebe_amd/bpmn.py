@@ -25,6 +25,7 @@ class _Node:
         self.condition = None
         self.source = None
         self.target = None
+        self.message = None  # (message id, name, correlation key expression) of a message catch event
 
 
 class ProcessBuilder:
@@ -81,6 +82,17 @@ class ProcessBuilder:
 
     def zeebeJobType(self, t):
         self.current.job_type = t
+        return self
+
+    def intermediateCatchEvent(self, id_=None):
+        self._add_node("intermediateCatchEvent", id_)
+        return self
+
+    def message(self, name, correlation_key):
+        """IntermediateCatchEventBuilder.message(m -> m.name(name).zeebeCorrelationKeyExpression(key)):
+        a <message> with a zeebe:subscription under the definitions (ZeebeExpression: "=" prefix)."""
+        expr = correlation_key if correlation_key.startswith("=") else "=" + correlation_key
+        self.current.message = ("Message_%s" % self.current.id, name, expr)
         return self
 
     def exclusiveGateway(self, id_=None):
@@ -155,11 +167,19 @@ class ProcessBuilder:
                 retries = ' retries="%s"' % c.retries if c.retries is not None else ""
                 out.append('    <serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
                            '</extensionElements></serviceTask>' % (quoteattr(c.id), quoteattr(c.job_type), retries))
+            elif c.kind == "intermediateCatchEvent" and c.message:
+                out.append('    <intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
+                           '</intermediateCatchEvent>' % (quoteattr(c.id), quoteattr(c.id + "_med"),
+                                                          quoteattr(c.message[0])))
             elif c.kind == "exclusiveGateway" and c.default:
                 out.append("    <exclusiveGateway id=%s default=%s/>" % (quoteattr(c.id), quoteattr(c.default.id)))
             else:
                 out.append("    <%s id=%s/>" % (c.kind, quoteattr(c.id)))
         out.append("  </process>")
+        for c in self.children:
+            if c.kind == "intermediateCatchEvent" and c.message:
+                out.append('  <message id=%s name=%s><extensionElements><zeebe:subscription correlationKey=%s/>'
+                           '</extensionElements></message>' % tuple(quoteattr(x) for x in c.message))
         out.append("</definitions>")
         return "\n".join(out) + "\n"
 
@@ -199,3 +219,10 @@ def fork_join_process(branches=8, process_id="forkjoin", tasks=False, job_type="
             b.connectTo("join")
     b.moveToNode("join").sequenceFlowId("toEnd").endEvent("end")
     return b.done()
+
+
+def message_catch_process(process_id="process", message_name="msg", correlation_key="key", catch_id="catch"):
+    """Config 5: start -> message catch (name, `= correlation_key`) -> end
+    (MessageCorrelationMultiplePartitionsTest.java:43-49 shape)."""
+    return (createExecutableProcess(process_id).startEvent("start").intermediateCatchEvent(catch_id)
+            .message(message_name, correlation_key).endEvent("end").done())

@@ -349,6 +349,7 @@ static zbhip_element blank(uint8_t type, uint16_t id) {
   e.event_type = ZBHIP_EV_UNSPECIFIED;
   e.flow_source = e.flow_target = e.condition = e.default_flow = ZBHIP_NONE16;
   e.job_type = e.join_slot = ZBHIP_NONE16;
+  e.message_name = e.correlation_var = ZBHIP_NONE16;
   e.job_retries = 0;
   e.id = id;
   return e;
@@ -369,6 +370,34 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
   }
   if (!proc || !proc->get("id")) { err = "no executable process"; return ZBHIP_EPARSE; }
   const std::string pid = *proc->get("id");
+  // <message> elements of the definitions (MessageTransformer.java:30-60): static names and
+  // `= variable` correlation keys only
+  struct Msg { std::string name, corr; bool ok; std::string why; };
+  std::unordered_map<std::string, Msg> messages;
+  for (auto& c : root.children) {
+    if (c.tag != "message" || !c.get("id")) continue;
+    Msg m{"", "", true, ""};
+    const std::string* nm = c.get("name");
+    if (!nm || nm->empty() || (*nm)[0] == '=') { m.ok = false; m.why = "message name expression outside the subset"; }
+    else m.name = *nm;
+    const Elem* ext = c.first("extensionElements");
+    const Elem* sub = ext ? ext->first("subscription") : nullptr;
+    const std::string* ck = sub ? sub->get("correlationKey") : nullptr;
+    std::string t = ck ? *ck : "";
+    size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+    t = a == std::string::npos ? "" : t.substr(a, b - a + 1);
+    if (t.size() < 2 || t[0] != '=') { m.ok = false; m.why = "correlation key must be a `= variable` expression"; }
+    else {
+      std::string v = t.substr(1);
+      size_t va = v.find_first_not_of(" \t\r\n"), vb = v.find_last_not_of(" \t\r\n");
+      v = va == std::string::npos ? "" : v.substr(va, vb - va + 1);
+      bool ident = !v.empty() && (isalpha((unsigned char)v[0]) || v[0] == '_');
+      for (char ch : v) ident = ident && (isalnum((unsigned char)ch) || ch == '_');
+      if (!ident) { m.ok = false; m.why = "correlation key expression outside the subset (`= variable` only)"; }
+      m.corr = v;
+    }
+    messages[*c.get("id")] = m;
+  }
   C.csr.bpmn_process_id = C.str(pid);
   C.elements.push_back(blank(ZBHIP_EL_PROCESS, C.csr.bpmn_process_id));
   std::unordered_map<std::string, uint16_t> index{{pid, 0}};
@@ -383,6 +412,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     else if (c.tag == "exclusiveGateway") type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
     else if (c.tag == "parallelGateway") type = ZBHIP_EL_PARALLEL_GATEWAY;
     else if (c.tag == "sequenceFlow") type = ZBHIP_EL_SEQUENCE_FLOW;
+    else if (c.tag == "intermediateCatchEvent") type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
     else if (c.tag == "extensionElements" || c.tag == "documentation" || c.tag == "textAnnotation" ||
              c.tag == "association")
       continue;
@@ -398,6 +428,24 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           return ZBHIP_EUNSUPP;
         }
       e.event_type = ZBHIP_EV_NONE;
+    }
+    if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+      // CatchEventTransformer.transformMessageEventDefinition: message catch events only
+      const Elem* med = c.first("messageEventDefinition");
+      for (auto& d : c.children)
+        if (&d != med && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+          err = "event definition <" + d.tag + "> outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
+      if (!med || !med->get("messageRef")) { err = "intermediate catch event without a message"; return ZBHIP_EUNSUPP; }
+      auto mi = messages.find(*med->get("messageRef"));
+      if (mi == messages.end()) { err = "unknown message " + *med->get("messageRef"); return ZBHIP_EPARSE; }
+      if (!mi->second.ok) { err = mi->second.why; return ZBHIP_EUNSUPP; }
+      if (const Elem* ext = c.first("extensionElements"))
+        if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+      e.event_type = ZBHIP_EV_MESSAGE;
+      e.message_name = C.str(mi->second.name);
+      e.correlation_var = C.str(mi->second.corr);
     }
     if (type == ZBHIP_EL_SERVICE_TASK) {
       const Elem* ext = c.first("extensionElements");
