@@ -572,6 +572,8 @@ static void xpart_kind(int kind, int& vt, int& intent) {
 // openProcessMessageSubscription: subscriptionPartitionId = sender, pik, eik, messageKey -1, name, interrupting;
 // correlateProcessMessageSubscription: subscriptionPartitionId = sender, pik, eik, bpmnProcessId, messageKey,
 //   name, variables, correlationKey;  correlateMessageSubscription: pik, eik, bpmnProcessId, messageKey -1, name.
+// Properties not set keep their declared defaults: interrupting = true (MessageSubscriptionRecord.java:33,
+// ProcessMessageSubscriptionRecord.java:37), strings "", messageKey -1.
 static MsgVal command_value(int kind, const MsgVal& in, int sender) {
   MsgVal m;
   m.pik = in.pik;
@@ -584,10 +586,10 @@ static MsgVal command_value(int kind, const MsgVal& in, int sender) {
       m.bpmn = in.bpmn; m.corr = in.corr; m.interrupting = in.interrupting; break;
     case ZBHIP_CMD_PMS_CREATE:
       m.partition = sender; m.interrupting = in.interrupting; break;
-    case ZBHIP_CMD_PMS_CORRELATE:
-      m.partition = sender; m.bpmn = in.bpmn; m.msg_key = in.msg_key; m.corr = in.corr; break;
-    default:  // MSG_SUB_CORRELATE
-      m.bpmn = in.bpmn; break;
+    case ZBHIP_CMD_PMS_CORRELATE:  // interrupting keeps its default (true)
+      m.partition = sender; m.bpmn = in.bpmn; m.msg_key = in.msg_key; m.corr = in.corr; m.interrupting = 1; break;
+    default:  // MSG_SUB_CORRELATE; interrupting keeps its default (true)
+      m.bpmn = in.bpmn; m.interrupting = 1; break;
   }
   return m;
 }

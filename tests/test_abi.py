@@ -38,9 +38,10 @@ def test_struct_sizes_match_header():
 #include <stdio.h>
 #include <stddef.h>
 #include "zbhip.h"
-int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(zbhip_command), sizeof(zbhip_doc_entry),
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(zbhip_command), sizeof(zbhip_doc_entry),
  sizeof(zbhip_record), sizeof(zbhip_config), sizeof(zbhip_stats), offsetof(zbhip_record, ordinal),
- offsetof(zbhip_record, aux), sizeof(zbhip_element)); return 0;}
+ offsetof(zbhip_record, aux), sizeof(zbhip_element), sizeof(zbhip_xpart_cmd), offsetof(zbhip_record, partition),
+ offsetof(zbhip_xpart_cmd, kind)); return 0;}
 '''
     d = os.path.join(ROOT, "build")
     os.makedirs(d, exist_ok=True)
@@ -50,7 +51,8 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(zbhip_command)
     subprocess.check_call(["gcc", "-I" + os.path.join(ROOT, "include"), src, "-o", exe])
     got = [int(x) for x in subprocess.check_output([exe]).split()]
     assert got == [C.sizeof(abi.Command), C.sizeof(abi.DocEntry), C.sizeof(abi.Record), C.sizeof(abi.Config),
-                   C.sizeof(abi.Stats), abi.Record.ordinal.offset, abi.Record.aux.offset, 24]
+                   C.sizeof(abi.Stats), abi.Record.ordinal.offset, abi.Record.aux.offset, 28,
+                   C.sizeof(abi.XpartCmd), abi.Record.partition.offset, abi.XpartCmd.kind.offset]
 
 
 def test_open_without_gpu_fails_loudly():

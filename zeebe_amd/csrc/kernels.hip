@@ -46,12 +46,14 @@ namespace zb {
 // lane storing its own records at its prefix scatters each store over ~40 cache lines; a
 // binary search of the lane prefix per record was slower still; B = 64 / 256 and R = 8 / 32
 // were 2-10 % slower.)
-template <int B_, int T_, int Q_, int R_>
+template <int B_, int T_, int Q_, int R_, bool M_ = false>
 struct KCfg {
   static constexpr int B = B_, T = T_, Q = Q_, R = R_;
+  static constexpr bool M = M_;  // message correlation (catch events, subscription commands)
 };
 using KSimple = KCfg<128, 4, 4, 16>;   // processes without parallel gateways / multi-outgoing nodes
 using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
+using KMsg = KCfg<128, 12, 16, 16, true>;  // partitions with message catch events (config 5)
 
 template <class K>
 struct Lane {
@@ -88,7 +90,37 @@ struct Lane {
   long long vv0, vv1, vv2, vv3;
   uint32_t jw0, jw1, jw2, jw3;
   bool has_join;
+  // ---- message correlation (K::M only) ----
+  uint32_t ci;              // window index of the command (outbox, key references)
+  uint32_t inst;            // instance whose rows are loaded (kNoInst: none, a slot lane before a
+                            // local PROCESS_MESSAGE_SUBSCRIPTION command)
+  uint32_t pm_x, pm_y, pm_z;// PROCESS_SUBSCRIPTION row of the loaded instance
+  long long pik;            // real process-instance key of the loaded instance, or a reference
+  bool slot_lane;           // primary subject is the correlation slot `slot`
+  uint32_t slot;
+  uint16_t s_next_ord;      // correlation-slot key space
+  uint16_t i_first_ord;     // first instance-space ordinal of this batch
+  uint32_t n_out, n_pay;
+  // pending local commands (SubscriptionCommandSender follow-ups on this partition)
+  uint32_t lq_slot;         // correlation slot of a local MESSAGE_SUBSCRIPTION command
+  uint32_t lq_row;          // slot row of a local PROCESS_MESSAGE_SUBSCRIPTION:CORRELATE
+  long long lq_msg;         // its message key (reference)
+  uint32_t lq_name_bpmn;    // message name | bpmnProcessId << 16 of the pending command
+  uint32_t lq_corr;         // correlation key of the pending command
+  long long lq_eik, lq_pik; // element / process instance keys of the pending command (references)
+  uint32_t lq_eord;         // routing handle ordinal of the pending command
+  // deferred correlation-slot row operations, applied at commit
+  bool op_ins;              // insert a row into slot op_slot
+  uint32_t op_slot;
+  uint4 ins_a;
+  long long ins_eik, ins_pik;
+  uint32_t op_corr_mask, op_rm_mask, op_rm_slot;
+  long long op_corr_msg, ins_key;
+  const StepParams* sp;
+  const uint32_t* prog;     // LDS program arena (mid-batch instance loads)
+  uint16_t s_first_ord;
 };
+constexpr uint32_t kNoInst = 0xFFFFFFFFu;
 static_assert(kVars == 4 && kJoinWords == 4, "scalarised tables");
 
 template <class K>
@@ -164,6 +196,44 @@ __device__ __forceinline__ void emit(Lane<K>& L, uint32_t code, uint32_t key, ui
   if (code >= ZBHIP_PI_SEQUENCE_FLOW_TAKEN && code <= ZBHIP_PI_ELEMENT_TERMINATED) ++L.transitions;
 }
 
+// ---- message records: a header row and kPayloadRows payload rows ---------------------------
+template <class K>
+__device__ __forceinline__ void emit_row(Lane<K>& L, uint2 r) {
+  if (L.nrec < L.rec_cap) {
+    if (L.nrec < (uint32_t)K::R) L.stage[L.nrec * K::B] = r;
+    else L.rec[(size_t)L.nrec * 64] = r;
+  } else {
+    set_fail(L, FB_RECORDS);
+  }
+  ++L.nrec;
+}
+__device__ __forceinline__ uint2 split64(long long v) {
+  return make_uint2((uint32_t)((unsigned long long)v & 0xFFFFFFFFu), (uint32_t)((unsigned long long)v >> 32));
+}
+// Record values of MESSAGE / MESSAGE_SUBSCRIPTION / PROCESS_MESSAGE_SUBSCRIPTION records
+// (protocol-impl/.../value/message/*Record.java): keys as references, resolved on drain.
+template <class K>
+__device__ __forceinline__ void emit_msg(Lane<K>& L, uint32_t code, long long key, long long eik, long long pik,
+                                         long long msg, uint32_t corr, uint32_t name_bpmn, uint32_t part,
+                                         uint32_t intr, uint32_t elem, uint32_t flags = 0) {
+  emit_row(L, make_uint2(0xFFFFFFFFu, (elem & 0xFFF) | kPayloadBit | (code << 16) | (flags << 24)));
+  emit_row(L, make_uint2(corr, name_bpmn));
+  emit_row(L, split64(key));
+  emit_row(L, split64(eik));
+  emit_row(L, split64(pik));
+  emit_row(L, split64(msg));
+  emit_row(L, make_uint2(part | (intr << 16), 0));
+  L.n_pay += kPayloadRows;
+}
+// key references (zb_internal.h): a subject's ordinal (resolved by the host drain through the
+// subject's key history) or a key of window command ci (resolved by the device key scan)
+__device__ __forceinline__ long long ref_subj(bool is_slot, uint32_t subject, uint32_t ord) {
+  return -2 - (long long)((1ull << 62) | ((unsigned long long)is_slot << 61) | ((unsigned long long)subject << 16) | ord);
+}
+__device__ __forceinline__ long long ref_cmd(uint32_t ci, bool sec, uint32_t ord) {
+  return -2 - (long long)(((unsigned long long)ci << 17) | ((unsigned long long)sec << 16) | ord);
+}
+
 // queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | key << 16
 template <class K>
 __device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
@@ -173,6 +243,17 @@ __device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, b
   if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
   if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
   L.q[(L.qt % K::Q) * K::B] = elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
+  ++L.qt;
+}
+
+// local subscription commands (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition,
+// :304-320: receiver == this partition -> follow-up command of the batch): bit 14 + kind
+enum : uint32_t { LQ_BIT = 1u << 14, LQ_MS_CREATE = 1, LQ_PMS_CREATE = 2, LQ_PMS_CORRELATE = 3, LQ_MS_CORRELATE = 4 };
+template <class K>
+__device__ __forceinline__ void push_local(Lane<K>& L, uint32_t kind) {
+  if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
+  if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
+  L.q[(L.qt % K::Q) * K::B] = LQ_BIT | kind;
   ++L.qt;
 }
 
@@ -452,6 +533,302 @@ __device__ __forceinline__ void take_outgoing(Lane<K>& L, uint4 w) {
   for (uint32_t i = 0; i < oc && !L.fail; ++i) take_sequence_flow(L, out_flow(L, ob + i));
 }
 
+
+// =============================================================================================
+// Message correlation (K::M variant only)
+// =============================================================================================
+// Partition of a correlation key: SubscriptionUtil.getSubscriptionPartitionId
+// (protocol-impl/.../SubscriptionUtil.java:22-44) over the host-computed Java hashCode.
+__device__ __forceinline__ uint32_t subscription_partition(int32_t h, int32_t partitions) {
+  const int32_t r = h % partitions;
+  return (uint32_t)((r < 0 ? -r : r) + 1);
+}
+
+template <class K>
+__device__ __forceinline__ uint16_t new_slot_key(Lane<K>& L) {
+  if (L.s_next_ord >= 0xFFF0) set_fail(L, FB_KEYS);
+  return L.s_next_ord++;
+}
+
+// payload references of the loaded instance's keys / of the lane's correlation slot keys
+template <class K>
+__device__ __forceinline__ long long iref(const Lane<K>& L, uint32_t ord) { return ref_subj(false, L.inst, ord); }
+template <class K>
+__device__ __forceinline__ long long sref(const Lane<K>& L, uint32_t ord) { return ref_subj(true, L.slot, ord); }
+// device-resolved reference of a key the loaded instance generated in this batch
+template <class K>
+__device__ __forceinline__ long long cref_inst(const Lane<K>& L, uint32_t ord) { return ref_cmd(L.ci, L.slot_lane, ord); }
+
+// one cross-partition send (post-commit side effect: InterPartitionCommandSender.sendCommand)
+template <class K>
+__device__ __forceinline__ void send_xpart(Lane<K>& L, uint32_t kind, uint32_t target, long long eik, long long pik,
+                                           long long msg, uint32_t corr, uint32_t inst, uint32_t eord,
+                                           uint32_t name_bpmn, uint32_t intr) {
+  if (L.n_out >= (uint32_t)kOut - 1) { set_fail(L, FB_MESSAGE); return; }  // one entry kept for a row patch
+  zbhip_xpart_cmd x;
+  x.element_instance_key = eik;
+  x.process_instance_key = pik;
+  x.message_key = msg;
+  x.correlation_key = corr;
+  x.instance = inst;
+  x.element_ord = (uint16_t)eord;
+  x.message_name = (uint16_t)(name_bpmn & 0xFFFF);
+  x.bpmn_process_id = (uint16_t)(name_bpmn >> 16);
+  x.kind = (uint8_t)kind;
+  x.interrupting = (uint8_t)intr;
+  x.source_partition = (int16_t)L.sp->partition_id;
+  x.target_partition = (int16_t)target;
+  x.pad = 0;
+  L.sp->xout[(size_t)L.ci * kOut + L.n_out++] = x;
+}
+
+// CatchEventBehavior.subscribeToEvents -> subscribeToMessageEvent (processing/common/
+// CatchEventBehavior.java:111-125,155-178,248-283): correlation key `= var` (STRING), the
+// PROCESS_MESSAGE_SUBSCRIPTION:CREATING event (+key), then MESSAGE_SUBSCRIPTION:CREATE to the
+// subscription partition -- a follow-up command here, or an outbox entry for another partition.
+template <class K>
+__device__ __forceinline__ void subscribe_message(Lane<K>& L, uint32_t elem, uint4 w, uint32_t key) {
+  const StepParams& P = *L.sp;
+  const uint32_t name = w.z & 0xFFFF, var = w.z >> 16;
+  int v = var_find(L, key, var);  // DbVariableState.getVariable: element scope, then the process
+  if (v < 0) v = var_find(L, 0, var);
+  // ExpressionProcessor.evaluateMessageCorrelationKeyExpression: STRING (NUMBER / null -> outside)
+  if (v < 0 || ((var_y(L, v) >> 16) & 0xFF) != ZBHIP_DOC_STR || L.slot_lane) { set_fail(L, FB_MESSAGE); return; }
+  const long long sv = var_v(L, v);
+  if (sv < 0 || sv >= (long long)P.n_strs || ((L.pm_x >> 12) & 3) != 0) { set_fail(L, FB_MESSAGE); return; }
+  const uint32_t corr = (uint32_t)sv;
+  const uint32_t part = subscription_partition((int32_t)P.str_hash[corr], P.partition_count);
+  const uint32_t nb = name | ((L.pb[5] & 0xFFFF) << 16);
+  const uint32_t sub = new_key(L);
+  L.pm_x = elem | (1u << 12) | (1u << 14) | (part << 16);  // ProcessMessageSubscriptionCreatingApplier
+  L.pm_y = key | (sub << 16);
+  L.pm_z = corr;
+  emit_msg(L, C_PMS_CREATING, iref(L, sub), iref(L, key), iref(L, 0), -1, corr, nb, part, 1, elem);
+  if ((int32_t)part == P.partition_id) {
+    emit_msg(L, C_MS_CREATE, -1, iref(L, key), iref(L, 0), -1, corr, nb, 0, 1, kNoElem);
+    L.lq_slot = corr;
+    L.lq_corr = corr;
+    L.lq_name_bpmn = nb;
+    L.lq_eord = key;
+    L.lq_eik = cref_inst(L, key);
+    L.lq_pik = L.pik;
+    push_local(L, LQ_MS_CREATE);
+  } else {
+    send_xpart(L, ZBHIP_CMD_MSG_SUB_CREATE, part, cref_inst(L, key), L.pik, -1, corr, L.inst, key, nb, 1);
+  }
+}
+
+// a row of correlation slot `slot`: state != free, same subscriber (PI partition, instance, ord), same name
+template <class K>
+__device__ __forceinline__ int find_row(const Lane<K>& L, uint32_t slot, uint32_t pi_part, uint32_t inst, uint32_t eord,
+                                        uint32_t name) {
+  const StepParams& P = *L.sp;
+  int found = -1;
+  for (int r = kSubs - 1; r >= 0; --r) {
+    const uint4 a = P.st.sub_a[(size_t)r * P.st.n_slots + slot];
+    if (((a.x & 0xFF) == 1 || (a.x & 0xFF) == 2) && (a.x >> 16) == pi_part && a.z == inst && (a.w & 0xFFFF) == eord && (a.y & 0xFFFF) == name)
+      found = r;
+  }
+  if (L.op_ins && L.op_slot == slot && (L.ins_a.x >> 16) == pi_part && L.ins_a.z == inst &&
+      (L.ins_a.w & 0xFFFF) == eord && (L.ins_a.y & 0xFFFF) == name)
+    found = kSubs;  // inserted by this batch
+  return found;
+}
+
+// MessageSubscriptionCreateProcessor.processRecord (processing/message/MessageSubscriptionCreateProcessor.java:66-104)
+// values: eik / pik references as received, routing handle (pi_part, inst, eord)
+template <class K>
+__device__ __forceinline__ void ms_create(Lane<K>& L, uint32_t slot, uint32_t corr, uint32_t nb, uint32_t intr,
+                                          uint32_t pi_part, uint32_t inst, uint32_t eord, long long eik,
+                                          long long pik, long long eik_p, long long pik_p) {
+  const StepParams& P = *L.sp;
+  if (slot >= P.st.n_slots) { set_fail(L, FB_MESSAGE); return; }
+  const bool dup = find_row(L, slot, pi_part, inst, eord, nb & 0xFFFF) >= 0;
+  uint32_t key = NONE;
+  if (!dup) {
+    key = L.slot_lane ? new_slot_key(L) : new_key(L);
+    const long long kp = L.slot_lane ? sref(L, key) : iref(L, key);
+    emit_msg(L, C_MS_CREATED, kp, eik_p, pik_p, -1, corr, nb, 0, intr, kNoElem);
+    if (L.op_ins) { set_fail(L, FB_MESSAGE); return; }
+    // MessageSubscriptionCreatedApplier -> DbMessageSubscriptionState.put (row written at commit)
+    L.op_ins = true;
+    L.op_slot = slot;
+    L.ins_a = make_uint4(1u | (intr << 8) | ((L.slot_lane ? 0u : 1u) << 9) | (pi_part << 16), nb, inst,
+                         eord | (key << 16));
+    L.ins_eik = eik;
+    L.ins_pik = pik;
+    L.ins_key = ref_cmd(L.ci, false, key);  // the batch's primary key space (instance or slot)
+  }
+  // MessageCorrelator.correlateNextMessage: no message outlives its PUBLISH batch in the subset
+  // (time-to-live 0) -> acknowledge: SubscriptionCommandSender.openProcessMessageSubscription
+  if ((int32_t)pi_part == P.partition_id) {
+    emit_msg(L, C_PMS_CREATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING,
+             (nb & 0xFFFF) | 0xFFFF0000u, (uint32_t)P.partition_id, intr, kNoElem);
+    L.lq_eord = eord;
+    L.lq_name_bpmn = nb;
+    L.lq_eik = eik;
+    L.lq_pik = pik;
+    L.lq_row = inst;  // the instance to load in a slot lane
+    push_local(L, LQ_PMS_CREATE);
+  } else {
+    send_xpart(L, ZBHIP_CMD_PMS_CREATE, pi_part, eik, pik, -1, corr, inst, eord, nb, intr);
+  }
+  if (dup)
+    emit_msg(L, kRejectBit | C_MS_CREATE, -1, eik_p, pik_p, -1, corr, nb, 0, intr, kNoElem, ZBHIP_REASON_MS_ALREADY_OPEN);
+}
+
+// ProcessMessageSubscriptionCreateProcessor.processRecord: OPENING -> CREATED (subscription key)
+template <class K>
+__device__ __forceinline__ void pms_create(Lane<K>& L, uint32_t eord, uint32_t name, long long eik_p, long long pik_p,
+                                           uint32_t part, uint32_t intr) {
+  const uint32_t st = (L.pm_x >> 12) & 3;
+  const uint32_t pm_elem = L.pm_x & 0xFFF;
+  const bool match = st != 0 && (L.pm_y & 0xFFFF) == eord && (elem_of(L, pm_elem).z & 0xFFFF) == name;
+  if (match && st == 1) {
+    const uint32_t nb = name | ((L.pb[5] & 0xFFFF) << 16);
+    emit_msg(L, C_PMS_CREATED, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, L.pm_z, nb, L.pm_x >> 16,
+             (L.pm_x >> 14) & 1, pm_elem);
+    L.pm_x = (L.pm_x & ~(3u << 12)) | (2u << 12);  // ProcessMessageSubscriptionCreatedApplier: OPENED
+    return;
+  }
+  emit_msg(L, kRejectBit | C_PMS_CREATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, name | 0xFFFF0000u, part, intr,
+           kNoElem, match ? (ZBHIP_REASON_PMS_CREATE_NOT_OPENING | (1u << 4)) : ZBHIP_REASON_PMS_CREATE_NOT_FOUND);
+}
+
+// ProcessMessageSubscriptionCorrelateProcessor.processRecord: CORRELATED, EventHandle.activateElement
+// (processing/common/EventHandle.java:109-150: PROCESS_EVENT:TRIGGERING +key, COMPLETE_ELEMENT),
+// then the acknowledgement MESSAGE_SUBSCRIPTION:CORRELATE to the message partition
+template <class K>
+__device__ __forceinline__ void pms_correlate(Lane<K>& L, uint32_t eord, uint32_t nb, long long eik_p, long long pik_p,
+                                              long long msg_p, uint32_t corr, uint32_t part, long long eik,
+                                              long long pik) {
+  const uint32_t st = (L.pm_x >> 12) & 3;
+  const uint32_t elem = L.pm_x & 0xFFF;
+  const uint32_t name = nb & 0xFFFF;
+  // no subscription / rejection -> MESSAGE_SUBSCRIPTION:REJECT (outside the subset)
+  if (st == 0 || (L.pm_y & 0xFFFF) != eord || (elem_of(L, elem).z & 0xFFFF) != name) { set_fail(L, FB_MESSAGE); return; }
+  const int t = tbl_find(L, eord);  // canTriggerElement: the catch event is ACTIVATED with its event scope
+  if (t < 0 || ((L.tbl[t * K::B].y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED) { set_fail(L, FB_MESSAGE); return; }
+  const uint32_t intr = (L.pm_x >> 14) & 1;
+  emit_msg(L, C_PMS_CORRELATED, iref(L, L.pm_y >> 16), eik_p, pik_p, msg_p, corr, nb, part, intr, elem);
+  L.pm_x = L.pm_y = L.pm_z = 0;  // ProcessMessageSubscriptionCorrelatedApplier: interrupting -> removed
+  const uint32_t pe = new_key(L);
+  emit(L, C_PE_TRIGGERING, pe, eord, elem);
+  L.trig_key = (uint16_t)eord;
+  emit(L, ZBHIP_PI_COMPLETE_ELEMENT, eord, 0, elem);
+  push(L, elem, true, true, eord);
+  // sendAcknowledgeCommand -> SubscriptionCommandSender.correlateMessageSubscription (sender partition)
+  if ((int32_t)part == L.sp->partition_id) {
+    emit_msg(L, C_MS_CORRELATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, nb, 0, 1, kNoElem);
+    L.lq_slot = corr;
+    L.lq_eord = eord;
+    L.lq_name_bpmn = nb;
+    L.lq_eik = eik_p;
+    L.lq_pik = pik_p;
+    L.lq_row = L.inst;
+    push_local(L, LQ_MS_CORRELATE);
+  } else {
+    send_xpart(L, ZBHIP_CMD_MSG_SUB_CORRELATE, part, eik, pik, -1, corr, L.inst, eord, nb, 1);
+  }
+}
+
+// MessageSubscriptionCorrelateProcessor.processRecord: CORRELATED (the stored record) or NOT_FOUND
+template <class K>
+__device__ __forceinline__ void ms_correlate(Lane<K>& L, uint32_t slot, uint32_t pi_part, uint32_t inst, uint32_t eord,
+                                             uint32_t nb, long long eik_p, long long pik_p) {
+  const StepParams& P = *L.sp;
+  const int r = slot < P.st.n_slots ? find_row(L, slot, pi_part, inst, eord, nb & 0xFFFF) : -1;
+  if (r < 0) {
+    emit_msg(L, kRejectBit | C_MS_CORRELATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, nb, 0, 1, kNoElem,
+             ZBHIP_REASON_MS_CORR_NOT_FOUND);
+    return;
+  }
+  if (r == kSubs) { set_fail(L, FB_MESSAGE); return; }  // correlate of a row opened in this very batch
+  const size_t ri = (size_t)r * P.st.n_slots + slot;
+  const uint4 a = P.st.sub_a[ri];
+  const longlong2 b = P.st.sub_b[ri];
+  const longlong2 k = P.st.sub_k[ri];
+  const long long msg = (L.op_corr_mask >> r) & 1 ? L.op_corr_msg : k.y;
+  if (!((a.x >> 8) & 1)) { set_fail(L, FB_MESSAGE); return; }  // non-interrupting: correlateNextMessage
+  emit_msg(L, C_MS_CORRELATED, k.x, b.x, b.y, msg, slot, a.y, 0, 1, kNoElem);
+  // MessageSubscriptionCorrelatedApplier: interrupting -> removed (at commit)
+  if (L.op_rm_mask && L.op_rm_slot != slot) { set_fail(L, FB_MESSAGE); return; }
+  L.op_rm_mask |= 1u << r;
+  L.op_rm_slot = slot;
+}
+
+// sort key of a subscription's element instance key for the visit order of
+// MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY [tenant, name, correlationKey, elementInstanceKey]:
+// (partition, pending-in-this-window, key or (command, ordinal)) -- a key this window generated is
+// newer than every real key of its partition
+__device__ __forceinline__ unsigned long long eik_order(long long eik, uint32_t part) {
+  if (eik >= 0) return (unsigned long long)eik;
+  const unsigned long long v = (unsigned long long)(-2 - eik);
+  return ((unsigned long long)part << 51) | (1ull << 50) | (v & ((1ull << 50) - 1));
+}
+
+// MessagePublishProcessor.handleNewMessage (processing/message/MessagePublishProcessor.java):
+// PUBLISHED (+key), CORRELATING per open subscription (first per bpmnProcessId, element instance
+// key order), PROCESS_MESSAGE_SUBSCRIPTION:CORRELATE sends, EXPIRED (time-to-live 0)
+template <class K>
+__device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint32_t name) {
+  const StepParams& P = *L.sp;
+  if (slot >= P.st.n_slots) { set_fail(L, FB_MESSAGE); return; }
+  const uint32_t msg = new_slot_key(L);
+  const uint32_t nb_msg = name | 0xFFFF0000u;
+  emit_msg(L, C_MSG_PUBLISHED, sref(L, msg), -1, -1, -1, slot, nb_msg, 0, 0, kNoElem);
+  const long long msg_ref = ref_cmd(L.ci, false, msg);
+  // selection sort of the slot's open rows by element instance key
+  uint32_t done = 0, chosen[kSubs], nch = 0, bpmn_seen[kSubs];
+  for (int it = 0; it < kSubs; ++it) {
+    int best = -1;
+    unsigned long long bk = ~0ull;
+    for (int r = 0; r < kSubs; ++r) {
+      if ((done >> r) & 1) continue;
+      const size_t ri = (size_t)r * P.st.n_slots + slot;
+      const uint4 a = P.st.sub_a[ri];
+      if (!((a.x & 0xFF) == 1 || (a.x & 0xFF) == 2) || (a.y & 0xFFFF) != name) { done |= 1u << r; continue; }
+      const unsigned long long o = eik_order(P.st.sub_b[ri].x, a.x >> 16);
+      if (o < bk) { bk = o; best = r; }
+    }
+    if (best < 0) break;
+    done |= 1u << best;
+    const size_t ri = (size_t)best * P.st.n_slots + slot;
+    const uint4 a = P.st.sub_a[ri];
+    bool seen = false;
+    for (uint32_t j = 0; j < nch; ++j) seen |= bpmn_seen[j] == (a.y >> 16);
+    if ((a.x & 0xFF) == 2 || seen) continue;  // correlating, or this process already correlates
+    const longlong2 b = P.st.sub_b[ri];
+    emit_msg(L, C_MS_CORRELATING, P.st.sub_k[ri].x, b.x, b.y, sref(L, msg), slot, a.y, 0, (a.x >> 8) & 1, kNoElem);
+    bpmn_seen[nch] = a.y >> 16;
+    chosen[nch++] = (uint32_t)best;
+    L.op_corr_mask |= 1u << best;  // MessageSubscriptionCorrelatingApplier (at commit)
+  }
+  L.op_corr_msg = msg_ref;
+  // sendCorrelateCommand: SubscriptionCommandSender.correlateProcessMessageSubscription
+  for (uint32_t j = 0; j < nch; ++j) {
+    const size_t ri = (size_t)chosen[j] * P.st.n_slots + slot;
+    const uint4 a = P.st.sub_a[ri];
+    const longlong2 b = P.st.sub_b[ri];
+    const uint32_t target = a.x >> 16;
+    if ((int32_t)target == P.partition_id) {
+      emit_msg(L, C_PMS_CORRELATE, -1, b.x, b.y, sref(L, msg), slot, a.y, (uint32_t)P.partition_id, 1, kNoElem);
+      if (L.lq_row != kNoInst) { set_fail(L, FB_MESSAGE); return; }  // one local instance per batch
+      L.lq_row = a.z;
+      L.lq_eord = a.w & 0xFFFF;
+      L.lq_name_bpmn = a.y;
+      L.lq_eik = b.x;
+      L.lq_pik = b.y;
+      L.lq_msg = sref(L, msg);
+      L.lq_corr = slot;
+      push_local(L, LQ_PMS_CORRELATE);
+    } else {
+      send_xpart(L, ZBHIP_CMD_PMS_CORRELATE, target, b.x, b.y, msg_ref, slot, a.z, a.w & 0xFFFF, a.y, (a.x >> 8) & 1);
+    }
+  }
+  emit_msg(L, C_MSG_EXPIRED, sref(L, msg), -1, -1, -1, slot, nb_msg, 0, 0, kNoElem);
+}
+
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
 template <class K>
 __device__ __forceinline__ void reject_pi(Lane<K>& L, bool complete, uint32_t elem, uint32_t key, bool fs_pi, uint32_t reason,
@@ -537,6 +914,16 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         if (flow != NONE) take_sequence_flow(L, flow);
         return;
       }
+      case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT:  // IntermediateCatchEventProcessor.onActivate
+        if constexpr (K::M) {
+          subscribe_message(L, elem, w, key);
+          if (L.fail) return;
+          emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+          tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
+        } else {
+          set_fail(L, FB_UNSUPPORTED);
+        }
+        return;
       case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (:34-50)
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
         emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, 0, elem);
@@ -582,7 +969,19 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   if (st == ZBHIP_PI_ELEMENT_COMPLETING) { set_fail(L, FB_UNSUPPORTED); return; }
   emit(L, ZBHIP_PI_ELEMENT_COMPLETING, cmd_key, 0, elem);
   tbl_set_state(L, t, ZBHIP_PI_ELEMENT_COMPLETING);
-  if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK) { set_fail(L, FB_UNSUPPORTED); return; }
+  if constexpr (K::M) {
+    if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+      // IntermediateCatchEventProcessor.onComplete -> unsubscribeFromEvents: a subscription still
+      // open here would write PROCESS_MESSAGE_SUBSCRIPTION:DELETING (outside the subset)
+      if (((L.pm_x >> 12) & 3) != 0 && (L.pm_y & 0xFFFF) == cmd_key) { set_fail(L, FB_MESSAGE); return; }
+    } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK) {
+      set_fail(L, FB_UNSUPPORTED);
+      return;
+    }
+  } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK) {
+    set_fail(L, FB_UNSUPPORTED);
+    return;
+  }
   // applyOutputMappings (BpmnVariableMappingBehavior.java:86-156): event-trigger variables
   if (L.trig_key == cmd_key) merge_document_from(L, cmd_key, L.doc_begin, L.doc_count);
   transition_to_completed_child(L, t, elem, w, cmd_key);
@@ -623,6 +1022,162 @@ struct Counters {
   uint32_t rec, trans, comp, keys, fb, cmd;
 };
 
+
+// ---- message path: instance loaded in the middle of a batch (a slot lane's local
+// PROCESS_MESSAGE_SUBSCRIPTION command for an instance of this partition) --------------------
+template <class K>
+__device__ __forceinline__ void load_instance_mid(Lane<K>& L, uint32_t inst) {
+  const StepParams& P = *L.sp;
+  const uint32_t N = P.st.n;
+  if (L.inst != kNoInst) { if (L.inst != inst) set_fail(L, FB_MESSAGE); return; }
+  if (inst >= N) { set_fail(L, FB_MESSAGE); return; }
+  const uint4 h = P.st.hdr[inst];
+  const uint32_t proc = h.x & 0xFFFF;
+  if (proc == NONE || !((h.y >> 24) & 1) || proc >= P.n_procs) { set_fail(L, FB_MESSAGE); return; }
+  const uint32_t nslots = (h.y >> 8) & 0xFF, nvars = (h.y >> 16) & 0xFF;
+  if (nslots > (uint32_t)K::T) { set_fail(L, FB_TABLE); return; }
+  L.inst = inst;
+  L.proc = (uint16_t)proc;
+  L.next_ord = h.x >> 16;
+  L.i_first_ord = L.next_ord;
+  L.pi_state = h.y & 0xFF;
+  L.pi_live = true;
+  L.pi_child = h.z & 0xFFFF;
+  L.pi_asf = h.z >> 16;
+  for (uint32_t sl = 0; sl < nslots; ++sl) L.tbl[sl * K::B] = P.st.slots[(size_t)sl * N + inst];
+  L.nt = (int)nslots;
+  L.nvars = (int)nvars;
+#pragma unroll
+  for (int v = 0; v < kVars; ++v)
+    if (v < L.nvars) {
+      const uint2 m = P.st.var_meta[(size_t)v * N + inst];
+      var_put(L, v, m.x, m.y, P.st.var_val[(size_t)v * N + inst]);
+    }
+  L.pb = L.prog + L.prog[1 + proc];
+  L.has_join = (L.pb[1] & 0xFFFF) != 0;
+  if (L.has_join) {
+    L.jw0 = P.st.join[inst];
+    L.jw1 = P.st.join[(size_t)N + inst];
+    L.jw2 = P.st.join[(size_t)2 * N + inst];
+    L.jw3 = P.st.join[(size_t)3 * N + inst];
+  }
+  const uint4 pm = P.st.pms[inst];
+  L.pm_x = pm.x;
+  L.pm_y = pm.y;
+  L.pm_z = pm.z;
+  L.pik = P.st.pi_key[inst];
+  vm_drain();
+}
+
+// a follow-up subscription command of this partition (queue entry LQ_BIT | kind)
+template <class K>
+__device__ __forceinline__ void process_local(Lane<K>& L, uint32_t kind) {
+  const uint32_t own = (uint32_t)L.sp->partition_id;
+  switch (kind) {
+    case LQ_MS_CREATE:  // from a catch event of the loaded instance
+      ms_create(L, L.lq_slot, L.lq_corr, L.lq_name_bpmn, 1, own, L.inst, L.lq_eord, L.lq_eik, L.lq_pik,
+                iref(L, L.lq_eord), iref(L, 0));
+      return;
+    case LQ_PMS_CREATE: {  // acknowledgement of a subscription this partition opened
+      const bool was_loaded = L.inst != kNoInst;
+      load_instance_mid(L, L.lq_row);
+      if (L.fail) return;
+      const long long eik_p = was_loaded && !L.slot_lane ? iref(L, L.lq_eord) : L.lq_eik;
+      const long long pik_p = was_loaded && !L.slot_lane ? iref(L, 0) : L.lq_pik;
+      pms_create(L, L.lq_eord, L.lq_name_bpmn & 0xFFFF, eik_p, pik_p, own, 1);
+      return;
+    }
+    case LQ_PMS_CORRELATE:  // a message published on this partition for one of its instances
+      load_instance_mid(L, L.lq_row);
+      if (L.fail) return;
+      pms_correlate(L, L.lq_eord, L.lq_name_bpmn, L.lq_eik, L.lq_pik, L.lq_msg, L.lq_corr, own, L.lq_eik, L.lq_pik);
+      return;
+    case LQ_MS_CORRELATE:
+      ms_correlate(L, L.lq_slot, own, L.lq_row, L.lq_eord, L.lq_name_bpmn, L.lq_eik, L.lq_pik);
+      return;
+    default:
+      set_fail(L, FB_UNSUPPORTED);
+  }
+}
+
+// the initial command of a batch that is a message / subscription command
+template <class K>
+__device__ __forceinline__ void message_command(Lane<K>& L, uint32_t kind, uint32_t subject, uint32_t ref, uint32_t xi) {
+  const StepParams& P = *L.sp;
+  if (kind == ZBHIP_CMD_PUBLISH) { publish_message(L, subject, ref); return; }
+  if (xi >= P.n_xparts) { set_fail(L, FB_UNSUPPORTED); return; }
+  const zbhip_xpart_cmd x = P.xparts[xi];
+  const uint32_t nb = (uint32_t)x.message_name | ((uint32_t)x.bpmn_process_id << 16);
+  const uint32_t src = (uint32_t)x.source_partition;
+  switch (kind) {
+    case ZBHIP_CMD_MSG_SUB_CREATE:
+      ms_create(L, subject, x.correlation_key, nb, x.interrupting, src, x.instance, x.element_ord,
+                x.element_instance_key, x.process_instance_key, x.element_instance_key, x.process_instance_key);
+      return;
+    case ZBHIP_CMD_MSG_SUB_CORRELATE:
+      ms_correlate(L, subject, src, x.instance, x.element_ord, nb, x.element_instance_key, x.process_instance_key);
+      return;
+    case ZBHIP_CMD_PMS_CREATE:
+      pms_create(L, x.element_ord, x.message_name, x.element_instance_key, x.process_instance_key, src, x.interrupting);
+      return;
+    case ZBHIP_CMD_PMS_CORRELATE:
+      if (L.proc == NONE) { set_fail(L, FB_MESSAGE); return; }
+      pms_correlate(L, x.element_ord, nb, x.element_instance_key, x.process_instance_key, x.message_key,
+                    x.correlation_key, src, x.element_instance_key, x.process_instance_key);
+      return;
+    default:
+      set_fail(L, FB_UNSUPPORTED);
+  }
+}
+
+// deferred correlation-slot row writes (DbMessageSubscriptionState put / updateToCorrelatingState /
+// remove).  Rows are claimed with a CAS so lanes of one launch inserting into the same slot never
+// collide; readers only see states 1 (open) and 2 (correlating), never a row being written (3).
+template <class K>
+__device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
+  const StepParams& P = *L.sp;
+  const uint32_t S = P.st.n_slots;
+  uint32_t patch_mask = 0, patch_slot = L.op_slot;
+  if (L.op_ins) {
+    int got = -1;
+    for (int r = 0; r < kSubs && got < 0; ++r)
+      if (atomicCAS(&P.st.sub_a[(size_t)r * S + L.op_slot].x, 0u, 3u) == 0u) got = r;
+    if (got < 0) { set_fail(L, FB_MESSAGE); return; }  // correlation slot full
+    const size_t ri = (size_t)got * S + L.op_slot;
+    P.st.sub_b[ri] = make_longlong2(L.ins_eik, L.ins_pik);
+    P.st.sub_k[ri] = make_longlong2(L.ins_key, -1);
+    uint4 a = L.ins_a;
+    P.st.sub_a[ri] = make_uint4(3u, a.y, a.z, a.w);
+    __threadfence();
+    atomicExch(&P.st.sub_a[ri].x, a.x);
+    patch_mask |= 1u << got;
+  }
+  if (L.op_corr_mask) {
+    for (int r = 0; r < kSubs; ++r)
+      if ((L.op_corr_mask >> r) & 1) {
+        const size_t ri = (size_t)r * S + L.slot;
+        P.st.sub_k[ri].y = L.op_corr_msg;
+        uint4 a = P.st.sub_a[ri];
+        P.st.sub_a[ri].x = (a.x & ~0xFFu) | 2u;
+      }
+    patch_mask |= L.op_corr_mask;
+    patch_slot = L.slot;
+  }
+  if (L.op_rm_mask) {
+    for (int r = 0; r < kSubs; ++r)
+      if ((L.op_rm_mask >> r) & 1) atomicExch(&P.st.sub_a[(size_t)r * S + L.op_rm_slot].x, 0u);
+    patch_mask &= ~(L.op_rm_slot == patch_slot ? L.op_rm_mask : 0u);
+  }
+  if (patch_mask) {  // the key scan replaces this window's key references in these rows
+    zbhip_xpart_cmd x = {};
+    x.kind = XK_PATCH;
+    x.correlation_key = patch_slot;
+    x.instance = patch_mask;
+    P.xout[(size_t)L.ci * kOut + L.n_out++] = x;
+  }
+  if (L.slot_lane) P.st.slot_hdr[L.slot].x = L.s_next_ord;
+}
+
 // One command's whole batch on one lane; returns the number of records it staged.
 template <class K>
 __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint32_t* prog, uint2* tbl_base,
@@ -661,8 +1216,33 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.vx0 = L.vx1 = L.vx2 = L.vx3 = 0xFFFFFFFFu;
   L.vy0 = L.vy1 = L.vy2 = L.vy3 = 0;
   L.vv0 = L.vv1 = L.vv2 = L.vv3 = 0;
+  bool slot_kind = false;
+  if constexpr (K::M) {
+    L.sp = &P;
+    L.prog = prog;
+    L.ci = ci;
+    L.inst = inst;
+    L.pm_x = L.pm_y = L.pm_z = 0;
+    L.pik = -1;
+    L.slot_lane = false;
+    L.slot = 0;
+    L.s_next_ord = L.s_first_ord = 0;
+    L.n_out = L.n_pay = 0;
+    L.lq_slot = L.lq_corr = L.lq_name_bpmn = L.lq_eord = 0;
+    L.lq_row = kNoInst;
+    L.lq_msg = L.lq_eik = L.lq_pik = -1;
+    L.op_ins = false;
+    L.op_slot = 0;
+    L.ins_a = make_uint4(0, 0, 0, 0);
+    L.ins_eik = L.ins_pik = L.ins_key = -1;
+    L.op_corr_mask = L.op_rm_mask = L.op_rm_slot = 0;
+    L.op_corr_msg = -1;
+    slot_kind = kind == ZBHIP_CMD_PUBLISH || kind == ZBHIP_CMD_MSG_SUB_CREATE || kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
+  }
 
-  const bool bad_cmd = inst >= N || (doc_count && (uint64_t)doc_begin + doc_count > P.n_docs);
+  const bool bad_cmd = (slot_kind ? inst >= P.st.n_slots : inst >= N) ||
+                       (doc_count && (uint64_t)doc_begin + doc_count > P.n_docs);
+  if (slot_kind) h = make_uint4(0xFFFFFFFFu, 0, 0, 0);
   if (bad_cmd) h = make_uint4(0xFFFFFFFFu, 0, 0, 0);
   L.proc = h.x & 0xFFFF;
   L.next_ord = h.x >> 16;
@@ -676,6 +1256,14 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if (bad_cmd) {
     set_fail(L, FB_UNSUPPORTED);  // never touches HBM outside the partition's arrays
     L.proc = NONE;
+  } else if (slot_kind) {
+    if constexpr (K::M) {  // a correlation slot: its rows are read on demand, instance loaded later
+      L.slot_lane = true;
+      L.slot = inst;
+      L.inst = kNoInst;
+      L.s_next_ord = L.s_first_ord = (uint16_t)P.st.slot_hdr[inst].x;
+      L.proc = NONE;
+    }
   } else if (kind == ZBHIP_CMD_CREATE) {
     // CreateProcessInstanceProcessor.createProcessInstance (:129-158)
     if (L.proc != NONE) set_fail(L, FB_SLOT_IN_USE);
@@ -707,6 +1295,21 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     }
   }
   L.first_ord = L.next_ord;
+  if constexpr (K::M) {
+    L.i_first_ord = L.next_ord;
+    if (!bad_cmd && !slot_kind) {
+      if (kind == ZBHIP_CMD_CREATE) {
+        L.pik = ref_cmd(ci, false, 0);
+      } else if (L.proc != NONE) {
+        const uint4 pm = P.st.pms[inst];
+        L.pm_x = pm.x;
+        L.pm_y = pm.y;
+        L.pm_z = pm.z;
+        L.pik = P.st.pi_key[inst];
+        vm_drain();
+      }
+    }
+  }
   if (!L.fail && L.proc != NONE) {
     L.pb = prog + prog[1 + L.proc];
     L.has_join = (L.pb[1] & 0xFFFF) != 0;
@@ -755,7 +1358,8 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       }
     }
   } else if (!L.fail) {
-    set_fail(L, FB_UNSUPPORTED);
+    if constexpr (K::M) message_command(L, kind, inst, ref, doc_begin);
+    else set_fail(L, FB_UNSUPPORTED);
   }
   L.processed = 1;
 
@@ -763,6 +1367,13 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   while (L.qh < L.qt && !L.fail) {
     const uint32_t entry = L.q[(L.qh % K::Q) * K::B];
     ++L.qh;
+    if constexpr (K::M) {
+      if (entry & LQ_BIT) {
+        process_local(L, entry & 0xF);
+        ++L.processed;
+        continue;
+      }
+    }
     process_pi(L, entry);
     ++L.processed;
   }
@@ -774,45 +1385,65 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       if (L.tbl[t * K::B].x != 0xFFFFFFFFu) ++ns;
     if (ns > (uint32_t)kSlots) set_fail(L, FB_SLOTS);
   }
+  uint32_t winst = inst;
+  if constexpr (K::M) {
+    winst = L.inst;
+    if (!L.fail) commit_slot_rows(L);
+  }
   // the counters are updated branch-free: per-branch updates are merged by the optimiser into a
   // store through a selected pointer, which puts the whole accumulator in scratch
   const bool ok = !L.fail;
-  if (ok && L.pi_live) {
+  if (ok && L.pi_live && winst != kNoInst) {
     uint32_t s = 0;
     for (int t = 0; t < L.nt; ++t) {
       uint2 e = L.tbl[t * K::B];
-      if (e.x != 0xFFFFFFFFu) P.st.slots[(size_t)(s++) * N + inst] = e;
+      if (e.x != 0xFFFFFFFFu) P.st.slots[(size_t)(s++) * N + winst] = e;
     }
 #pragma unroll
     for (int v = 0; v < kVars; ++v)
       if (v < L.nvars) {
-        P.st.var_meta[(size_t)v * N + inst] = make_uint2(var_x(L, v), var_y(L, v));
-        P.st.var_val[(size_t)v * N + inst] = var_v(L, v);
+        P.st.var_meta[(size_t)v * N + winst] = make_uint2(var_x(L, v), var_y(L, v));
+        P.st.var_val[(size_t)v * N + winst] = var_v(L, v);
       }
   }
-  if (ok && L.has_join) {
+  if (ok && L.has_join && winst != kNoInst) {
     const bool live = L.pi_live;  // a completed instance's counters are removed with it
-    P.st.join[inst] = live ? L.jw0 : 0u;
-    P.st.join[(size_t)N + inst] = live ? L.jw1 : 0u;
-    P.st.join[(size_t)2 * N + inst] = live ? L.jw2 : 0u;
-    P.st.join[(size_t)3 * N + inst] = live ? L.jw3 : 0u;
+    P.st.join[winst] = live ? L.jw0 : 0u;
+    P.st.join[(size_t)N + winst] = live ? L.jw1 : 0u;
+    P.st.join[(size_t)2 * N + winst] = live ? L.jw2 : 0u;
+    P.st.join[(size_t)3 * N + winst] = live ? L.jw3 : 0u;
   }
-  if (ok) {
+  if constexpr (K::M) {
+    if (ok && winst != kNoInst) P.st.pms[winst] = make_uint4(L.pi_live ? L.pm_x : 0u, L.pi_live ? L.pm_y : 0u,
+                                                             L.pi_live ? L.pm_z : 0u, 0u);
+  }
+  if (ok && winst != kNoInst) {
     // a completed instance frees its slot (rows removed with the instance) but keeps next_ord,
     // so late commands for the instance relabel consistently
     const bool live = L.pi_live;
-    P.st.hdr[inst] = live ? make_uint4(L.proc | ((uint32_t)L.next_ord << 16),
+    P.st.hdr[winst] = live ? make_uint4(L.proc | ((uint32_t)L.next_ord << 16),
                                        L.pi_state | (ns << 8) | ((uint32_t)L.nvars << 16) | (1u << 24),
                                        (uint32_t)L.pi_child | ((uint32_t)L.pi_asf << 16), 0)
                           : make_uint4(0xFFFFu | ((uint32_t)L.next_ord << 16), 0, 0, 0);
   }
-  const uint32_t nkeys = ok ? (uint16_t)(L.next_ord - L.first_ord) : 0u;
+  uint32_t nkeys = ok ? (uint16_t)(L.next_ord - L.first_ord) : 0u;
+  uint32_t first = L.first_ord, npay = 0;
+  if constexpr (K::M) {
+    // slot lanes: the slot's keys first, then the instance loaded in the middle of the batch
+    const uint32_t nsec = ok && L.slot_lane && L.inst != kNoInst ? (uint16_t)(L.next_ord - L.i_first_ord) : 0u;
+    if (L.slot_lane) {
+      nkeys = ok ? (uint16_t)(L.s_next_ord - L.s_first_ord) + nsec : 0u;
+      first = L.s_first_ord;
+    }
+    npay = ok ? L.n_pay : 0u;
+    P.cmd_hdr2[ci] = make_uint4(L.inst, L.i_first_ord | (nsec << 16), ok ? L.n_out : 0u, npay);
+  }
   const uint32_t nrec = ok ? L.nrec : 0u;
   P.cmd_hdr[ci] = make_uint2(nrec | (nkeys << 16),
-                             L.first_ord | ((uint32_t)(ok ? ST_OK : ST_FALLBACK) << 16) | (L.fail << 24));
+                             first | ((uint32_t)(ok ? ST_OK : ST_FALLBACK) << 16) | (L.fail << 24));
   acc.cmd += 1;
   acc.fb += ok ? 0u : 1u;
-  acc.rec += nrec;
+  acc.rec += nrec - npay;
   acc.trans += ok ? L.transitions : 0u;
   acc.comp += ok ? L.completed : 0u;
   acc.keys += nkeys;
@@ -986,6 +1617,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan_u(uint32_t v) { return wave_incl_scan(v); }
+
 // single workgroup: exclusive scan of the region totals (64-bit total)
 __global__ __launch_bounds__(1024) void k_scan_regions(const uint32_t* tot, uint32_t nr, unsigned long long* off,
                                                       unsigned long long* total) {
@@ -1018,6 +1651,213 @@ __global__ __launch_bounds__(256) void k_gather(const uint2* regions, const uint
   const uint2* src = regions + (size_t)g * region_stride;
   uint2* dst = out + off[g];
   for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// message path, after the k_step launches of a window (KMsg partitions only)
+// ---------------------------------------------------------------------------------------------
+// Key scan: DbKeyGenerator hands out keys in log order, so command c's keys start at
+// counter + sum_{c' < c} nkeys(c') (exclusive scan over the window, 64-bit).  With the bases the
+// device resolves the window's key references in the outbox and in the correlation-slot rows,
+// writes each created instance's real process-instance key, and advances the counter -- so the
+// cross-partition exchange never needs the host.
+struct KeyScanParams {
+  const uint2* cmd_hdr;
+  const uint4* cmd_hdr2;
+  const uint4* cmds;
+  uint32_t n;
+  unsigned long long* block_sum;  // [blocks]
+  unsigned long long* base;       // [n] key counter value before command c's first key
+  unsigned long long* counter;    // [1] the partition's key counter (last generated value)
+  zbhip_xpart_cmd* xout;
+  long long* pi_key;
+  uint32_t n_inst;
+  uint4* sub_a;
+  longlong2* sub_b;
+  longlong2* sub_k;
+  uint32_t n_slots;
+  long long pbits;
+};
+
+constexpr int kScanB = 1024;
+
+__global__ __launch_bounds__(kScanB) void k_key_block_sums(KeyScanParams K) {
+  const uint32_t i = blockIdx.x * kScanB + threadIdx.x;
+  uint32_t v = i < K.n ? K.cmd_hdr[i].x >> 16 : 0u;
+  v = wave_incl_scan_u(v);
+  __shared__ uint32_t ws[kScanB / 64];
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kScanB / 64; ++w) t += ws[w];
+    K.block_sum[blockIdx.x] = t;
+  }
+}
+
+// single workgroup: exclusive scan of the block sums (in place), counter advanced at the end
+__global__ __launch_bounds__(1024) void k_key_scan_sums(KeyScanParams K, uint32_t nb) {
+  __shared__ unsigned long long ws[16];
+  __shared__ unsigned long long carry;
+  if (threadIdx.x == 0) carry = *K.counter;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+    const uint32_t i = b0 + threadIdx.x;
+    const unsigned long long v = i < nb ? K.block_sum[i] : 0ull;
+    unsigned long long inc = v;
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned long long o = __shfl_up(inc, off);
+      if (lane >= (uint32_t)off) inc += o;
+    }
+    if (lane == 63) ws[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    unsigned long long wb = 0;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wb += ws[w];
+    const unsigned long long c = carry;
+    if (i < nb) K.block_sum[i] = c + wb + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = c + wb + inc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *K.counter = carry;
+}
+
+__device__ __forceinline__ long long resolve_cmd_ref(const KeyScanParams& K, long long ref) {
+  if (ref >= -1) return ref;
+  const unsigned long long v = (unsigned long long)(-2 - ref);
+  if ((v >> 62) & 1) return ref;  // a subject ordinal: resolved by the host drain
+  const uint32_t c = (uint32_t)(v >> 17), sec = (v >> 16) & 1, ord = v & 0xFFFF;
+  if (c >= K.n) return ref;
+  const uint2 h = K.cmd_hdr[c];
+  const uint4 h2 = K.cmd_hdr2[c];
+  const uint32_t nsec = h2.y >> 16;
+  const uint32_t nprim = (h.x >> 16) - nsec;
+  const unsigned long long off = sec ? nprim + (uint16_t)(ord - (h2.y & 0xFFFF)) : (uint16_t)(ord - (h.y & 0xFFFF));
+  return K.pbits + (long long)(K.base[c] + 1 + off);
+}
+
+__global__ __launch_bounds__(kScanB) void k_key_apply(KeyScanParams K) {
+  const uint32_t i = blockIdx.x * kScanB + threadIdx.x;
+  const uint32_t v = i < K.n ? K.cmd_hdr[i].x >> 16 : 0u;
+  const uint32_t inc = wave_incl_scan_u(v);
+  __shared__ uint32_t ws[kScanB / 64];
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  unsigned long long b = K.block_sum[blockIdx.x];
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) b += ws[w];
+  if (i < K.n) K.base[i] = b + inc - v;
+}
+
+// second pass (all bases known): patch references that may point at any command of the window
+__global__ __launch_bounds__(256) void k_key_patch(KeyScanParams K) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= K.n) return;
+  const uint2 h = K.cmd_hdr[c];
+  if (((h.y >> 16) & 0xFF) != ST_OK) return;
+  const uint4 cw = K.cmds[c];
+  if ((cw.y & 0xFF) == ZBHIP_CMD_CREATE && cw.x < K.n_inst)  // ordinal 0 of the CREATE batch
+    K.pi_key[cw.x] = K.pbits + (long long)(K.base[c] + 1 + (uint16_t)(0 - (h.y & 0xFFFF)));
+  const uint32_t nout = K.cmd_hdr2[c].z;
+  for (uint32_t j = 0; j < nout && j < (uint32_t)kOut; ++j) {
+    zbhip_xpart_cmd& x = K.xout[(size_t)c * kOut + j];
+    if (x.kind == XK_PATCH) {
+      const uint32_t slot = x.correlation_key;
+      if (slot >= K.n_slots) continue;
+      for (int r = 0; r < kSubs; ++r)
+        if ((x.instance >> r) & 1) {
+          const size_t ri = (size_t)r * K.n_slots + slot;
+          longlong2 bb = K.sub_b[ri], kk = K.sub_k[ri];
+          K.sub_b[ri] = make_longlong2(resolve_cmd_ref(K, bb.x), resolve_cmd_ref(K, bb.y));
+          K.sub_k[ri] = make_longlong2(resolve_cmd_ref(K, kk.x), resolve_cmd_ref(K, kk.y));
+        }
+      continue;
+    }
+    x.element_instance_key = resolve_cmd_ref(K, x.element_instance_key);
+    x.process_instance_key = resolve_cmd_ref(K, x.process_instance_key);
+    x.message_key = resolve_cmd_ref(K, x.message_key);
+  }
+}
+
+// Outbox buckets by target partition, stable in log order (what the all-to-all sends):
+// per-block counts, a scan (target-major), then a scatter that keeps each block's order.
+struct BucketParams {
+  const uint2* cmd_hdr;
+  const uint4* cmd_hdr2;
+  const zbhip_xpart_cmd* xout;
+  uint32_t n;
+  uint32_t parts;
+  uint32_t* blk_cnt;     // [blocks][parts] -> exclusive offsets
+  uint32_t* counts;      // [parts]
+  zbhip_xpart_cmd* out;
+};
+constexpr int kBucketB = 256;
+
+__device__ __forceinline__ uint32_t entries_to(const BucketParams& Q, uint32_t c, uint32_t t) {
+  if (c >= Q.n || ((Q.cmd_hdr[c].y >> 16) & 0xFF) != ST_OK) return 0;
+  const uint32_t nout = min(Q.cmd_hdr2[c].z, (uint32_t)kOut);
+  uint32_t k = 0;
+  for (uint32_t j = 0; j < nout; ++j) {
+    const zbhip_xpart_cmd& x = Q.xout[(size_t)c * kOut + j];
+    k += x.kind != XK_PATCH && (uint32_t)x.target_partition == t + 1;
+  }
+  return k;
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t& total) {
+  __shared__ uint32_t ws[kBucketB / 64];
+  const uint32_t inc = wave_incl_scan_u(v);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t b = 0;
+  total = 0;
+  for (int w = 0; w < kBucketB / 64; ++w) {
+    if (w < (int)(threadIdx.x >> 6)) b += ws[w];
+    total += ws[w];
+  }
+  __syncthreads();
+  return b + inc - v;
+}
+
+__global__ __launch_bounds__(kBucketB) void k_bucket_count(BucketParams Q) {
+  const uint32_t c = blockIdx.x * kBucketB + threadIdx.x;
+  for (uint32_t t = 0; t < Q.parts; ++t) {
+    uint32_t tot;
+    (void)block_excl_scan(entries_to(Q, c, t), tot);
+    if (threadIdx.x == 0) Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] = tot;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_bucket_scan(BucketParams Q, uint32_t nb) {
+  if (threadIdx.x != 0) return;
+  uint32_t off = 0;
+  for (uint32_t t = 0; t < Q.parts; ++t) {
+    const uint32_t start = off;
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint32_t v = Q.blk_cnt[(size_t)b * Q.parts + t];
+      Q.blk_cnt[(size_t)b * Q.parts + t] = off;
+      off += v;
+    }
+    Q.counts[t] = off - start;
+  }
+}
+
+__global__ __launch_bounds__(kBucketB) void k_bucket_scatter(BucketParams Q) {
+  const uint32_t c = blockIdx.x * kBucketB + threadIdx.x;
+  for (uint32_t t = 0; t < Q.parts; ++t) {
+    uint32_t tot;
+    const uint32_t mine = entries_to(Q, c, t);
+    uint32_t o = Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] + block_excl_scan(mine, tot);
+    if (mine) {
+      const uint32_t nout = min(Q.cmd_hdr2[c].z, (uint32_t)kOut);
+      for (uint32_t j = 0; j < nout; ++j) {
+        const zbhip_xpart_cmd& x = Q.xout[(size_t)c * kOut + j];
+        if (x.kind != XK_PATCH && (uint32_t)x.target_partition == t + 1) Q.out[o++] = x;
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1067,10 +1907,35 @@ static hipError_t launch_k(const StepParams& P, hipStream_t s) {
   return hipGetLastError();
 }
 
-uint32_t step_block(int variant) { return variant ? KGeneric::B : KSimple::B; }
+uint32_t step_block(int variant) { return variant == 2 ? KMsg::B : variant ? KGeneric::B : KSimple::B; }
 
 size_t step_lds_bytes(int variant, uint32_t prog_words) {
-  return variant ? lds_bytes<KGeneric>(prog_words) : lds_bytes<KSimple>(prog_words);
+  return variant == 2 ? lds_bytes<KMsg>(prog_words)
+                      : variant ? lds_bytes<KGeneric>(prog_words) : lds_bytes<KSimple>(prog_words);
+}
+
+hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uint4* cmds, uint32_t n,
+                          unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
+                          zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  KeyScanParams K{cmd_hdr, cmd_hdr2, cmds, n, block_sum, base, counter, xout, st.pi_key, st.n,
+                  st.sub_a, st.sub_b, st.sub_k, st.n_slots, pbits};
+  const uint32_t nb = (n + kScanB - 1) / kScanB;
+  hipLaunchKernelGGL(k_key_block_sums, dim3(nb), dim3(kScanB), 0, s, K);
+  hipLaunchKernelGGL(k_key_scan_sums, dim3(1), dim3(1024), 0, s, K, nb);
+  hipLaunchKernelGGL(k_key_apply, dim3(nb), dim3(kScanB), 0, s, K);
+  hipLaunchKernelGGL(k_key_patch, dim3((n + 255) / 256), dim3(256), 0, s, K);
+  return hipGetLastError();
+}
+
+hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
+                         uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s) {
+  BucketParams Q{cmd_hdr, cmd_hdr2, xout, n, parts, blk_cnt, counts, out};
+  const uint32_t nb = (n + kBucketB - 1) / kBucketB;
+  if (nb) hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBucketB), 0, s, Q);
+  hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(64), 0, s, Q, nb);
+  if (nb) hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBucketB), 0, s, Q);
+  return hipGetLastError();
 }
 
 void dump_stamps() {
@@ -1087,7 +1952,7 @@ void dump_stamps() {
 
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
   if (P.n_launch == 0) return hipSuccess;
-  return variant ? launch_k<KGeneric>(P, s) : launch_k<KSimple>(P, s);
+  return variant == 2 ? launch_k<KMsg>(P, s) : variant ? launch_k<KGeneric>(P, s) : launch_k<KSimple>(P, s);
 }
 
 hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,

@@ -24,6 +24,11 @@ hipError_t launch_step(int variant, const StepParams& P, hipStream_t s);
 void dump_stamps();
 hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
                          size_t region_stride, uint2* out, unsigned long long* total, hipStream_t s);
+hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uint4* cmds, uint32_t n,
+                          unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
+                          zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s);
+hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
+                         uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;  // regions for the extra workgroups of multi-round windows
 }  // namespace zb
 
@@ -42,8 +47,17 @@ struct Proc {
   int64_t def_key = 0;
   int32_t version = 1;
   uint16_t bpmn_id = 0;
+  uint16_t bpmn_name = NONE;  // name id of the bpmnProcessId (processes with message catch events)
+  bool has_msg = false;
   const std::string& id(uint32_t e) const { return strings[els[e].id]; }
 };
+
+// Java String#hashCode over signed bytes (SubscriptionUtil.getSubscriptionHashCode, :22-30)
+int32_t java_hash(const char* b, size_t n) {
+  uint32_t h = 0;
+  for (size_t i = 0; i < n; ++i) h = 31u * h + (uint32_t)(int32_t)(int8_t)b[i];
+  return (int32_t)h;
+}
 
 struct BatchRef {
   int64_t base;  // first generated key counter value (key = (p << 51) + base + i)
@@ -122,7 +136,7 @@ struct zbhip_handle {
   std::vector<uint2> h_hdr;
   std::vector<uint2> h_out;
   std::vector<uint64_t> h_off;  // record offset of each command in h_out
-  size_t drain_cmd = 0, drain_rec = 0;
+  size_t drain_cmd = 0, drain_rec = 0, drain_ord = 0;
   bool results = false;
 
   // key relabelling (DbKeyGenerator order)
@@ -132,11 +146,55 @@ struct zbhip_handle {
   std::vector<uint16_t> inst_proc;
   std::vector<BatchRef> batches;
 
+  // ---- message correlation (variant 2) ----
+  std::vector<std::string> strs;               // value dictionary
+  std::unordered_map<std::string, uint32_t> str_ids;
+  std::vector<uint32_t> str_hash;
+  uint32_t* d_str_hash = nullptr;
+  size_t d_str_cap = 0, d_str_n = 0;
+  zbhip_xpart_cmd* d_xparts = nullptr;         // host-submitted window xparts
+  const zbhip_xpart_cmd* ext_xparts = nullptr;
+  std::vector<zbhip_xpart_cmd> h_xparts;
+  size_t n_xparts = 0;
+  uint4* d_cmd_hdr2 = nullptr;
+  zbhip_xpart_cmd* d_xout = nullptr;
+  zbhip_xpart_cmd* d_xbucket = nullptr;
+  uint32_t* d_blk_cnt = nullptr;
+  uint32_t* d_xcount = nullptr;
+  unsigned long long* d_key_counter = nullptr;
+  unsigned long long* d_key_base = nullptr;
+  unsigned long long* d_key_blk = nullptr;
+  bool bucketed = false;
+  bool published = false;                      // a publish ran: MESSAGE_STATS row exists
+  std::vector<uint4> h_hdr2;
+  std::vector<int64_t> h_base;                 // key counter before each command's first key
+  std::vector<zbhip_xpart_cmd> h_xout;
+  bool msg() const { return variant == 2; }
+
   zbhip_stats stats{};
   bool stats_dirty = false;
   uint32_t n_regions = 0;
   unsigned long long key_counter_approx = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+
+  // subjects of the key history: instance slots [0, n), correlation slots [n, n + S)
+  uint32_t slot_subject(uint32_t slot) const { return cfg.max_instances + slot; }
+  // a key reference of a payload row / row (zb_internal.h) -> the reference's key
+  long long resolve_ref(long long ref) const {
+    if (ref >= -1) return ref;
+    const unsigned long long v = (unsigned long long)(-2 - ref);
+    const uint32_t ord = v & 0xFFFF;
+    if ((v >> 62) & 1) {
+      const bool is_slot = (v >> 61) & 1;
+      const uint32_t subj = (uint32_t)((v >> 16) & 0xFFFFFFFFull);
+      return key_of(is_slot ? slot_subject(subj) : subj, ord);
+    }
+    const uint32_t c = (uint32_t)(v >> 17), sec = (v >> 16) & 1;
+    if (c >= h_base.size() || c >= h_hdr.size()) return -1;
+    const uint32_t nsec = h_hdr2[c].y >> 16, nprim = (h_hdr[c].x >> 16) - nsec;
+    const uint32_t off = sec ? nprim + (uint16_t)(ord - (h_hdr2[c].y & 0xFFFF)) : (uint16_t)(ord - (h_hdr[c].y & 0xFFFF));
+    return ((int64_t)cfg.partition_id << 51) + h_base[c] + 1 + off;
+  }
 
   long long key_of(uint32_t inst, uint32_t ord) const {
     if (ord == NONE || inst >= hist.size()) return -1;
@@ -201,7 +259,35 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   ok = ok && dalloc(&h->d_regions, h->region_records) == hipSuccess &&
        dalloc(&h->d_region_total, h->regions_cap) == hipSuccess &&
        dalloc(&h->d_region_off, h->regions_cap) == hipSuccess;
+  // message correlation state (config 5): PROCESS_SUBSCRIPTION rows per instance, correlation slots
+  const size_t S = cfg->max_correlation_keys;
+  h->st.n_slots = (uint32_t)S;
+  if (S) {
+    ok = ok && dalloc(&h->st.pms, N) == hipSuccess && dalloc(&h->st.pi_key, N) == hipSuccess &&
+         dalloc(&h->st.slot_hdr, S) == hipSuccess && dalloc(&h->st.sub_a, S * kSubs) == hipSuccess &&
+         dalloc(&h->st.sub_b, S * kSubs) == hipSuccess && dalloc(&h->st.sub_k, S * kSubs) == hipSuccess;
+  }
+  ok = ok && dalloc(&h->d_cmd_hdr2, cfg->max_commands) == hipSuccess &&
+       dalloc(&h->d_xparts, cfg->max_commands) == hipSuccess &&
+       dalloc(&h->d_key_counter, 1) == hipSuccess && dalloc(&h->d_key_base, cfg->max_commands) == hipSuccess &&
+       dalloc(&h->d_key_blk, (cfg->max_commands + 1023) / 1024 + 1) == hipSuccess && dalloc(&h->d_xcount, 1024) == hipSuccess;
+  if (S) {
+    ok = ok && dalloc(&h->d_xout, (size_t)cfg->max_commands * kOut) == hipSuccess &&
+         dalloc(&h->d_xbucket, (size_t)cfg->max_commands * kOut) == hipSuccess &&
+         dalloc(&h->d_blk_cnt, ((size_t)cfg->max_commands / 256 + 1) * (size_t)std::max(1, cfg->partition_count)) == hipSuccess;
+  }
   if (!ok) { zbhip_close(h); return ZBHIP_ENOMEM; }
+  if (S) {
+    const unsigned long long kc = (unsigned long long)cfg->initial_key;
+    if (hipMemsetAsync(h->st.pms, 0, N * sizeof(uint4), h->stream) != hipSuccess ||
+        hipMemsetAsync(h->st.pi_key, 0xFF, N * sizeof(long long), h->stream) != hipSuccess ||
+        hipMemsetAsync(h->st.slot_hdr, 0, S * sizeof(uint2), h->stream) != hipSuccess ||
+        hipMemsetAsync(h->st.sub_a, 0, S * kSubs * sizeof(uint4), h->stream) != hipSuccess ||
+        hipMemcpyAsync(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice, h->stream) != hipSuccess) {
+      zbhip_close(h);
+      return ZBHIP_EDEVICE;
+    }
+  }
   h->rec_slots = cfg->max_commands;
   // every slot starts free (proc = 0xFFFF); counters zero
   if (hipMemsetAsync(h->st.hdr, 0xFF, N * sizeof(uint4), h->stream) != hipSuccess ||
@@ -233,6 +319,22 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_region_total);
   (void)hipFree(h->d_region_off);
   (void)hipFree(h->d_stats);
+  (void)hipFree(h->st.pms);
+  (void)hipFree(h->st.pi_key);
+  (void)hipFree(h->st.slot_hdr);
+  (void)hipFree(h->st.sub_a);
+  (void)hipFree(h->st.sub_b);
+  (void)hipFree(h->st.sub_k);
+  (void)hipFree(h->d_str_hash);
+  (void)hipFree(h->d_xparts);
+  (void)hipFree(h->d_cmd_hdr2);
+  (void)hipFree(h->d_xout);
+  (void)hipFree(h->d_xbucket);
+  (void)hipFree(h->d_blk_cnt);
+  (void)hipFree(h->d_xcount);
+  (void)hipFree(h->d_key_counter);
+  (void)hipFree(h->d_key_base);
+  (void)hipFree(h->d_key_blk);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -282,6 +384,7 @@ static int rebuild_program(zbhip_handle* h) {
     pb[2] = out_off;
     pb[3] = cond_off;
     pb[4] = code_off;
+    pb[5] = P.bpmn_name;  // name id of the bpmnProcessId (message records)
     for (uint32_t e = 0; e < n_el; ++e) {
       const zbhip_element& E = P.els[e];
       uint32_t* w = pb + 8 + 4 * e;
@@ -290,6 +393,8 @@ static int rebuild_program(zbhip_handle* h) {
       if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW) w[2] = E.flow_target | ((uint32_t)E.condition << 16);
       else if (E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY) w[2] = E.default_flow | (0xFFFFu << 16);
       else if (E.element_type == ZBHIP_EL_SERVICE_TASK) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
+      else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
+        w[2] = E.message_name | ((uint32_t)E.correlation_var << 16);  // name ids (zbhip_deploy)
       else w[2] = 0xFFFFFFFFu;
       w[3] = E.join_slot | ((uint32_t)E.id << 16);
     }
@@ -336,8 +441,14 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if (e.element_type != ZBHIP_EL_PROCESS && e.element_type != ZBHIP_EL_START_EVENT &&
         e.element_type != ZBHIP_EL_END_EVENT && e.element_type != ZBHIP_EL_SERVICE_TASK &&
         e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
-        e.element_type != ZBHIP_EL_SEQUENCE_FLOW)
+        e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
       return ZBHIP_EUNSUPP;
+  for (auto& e : P.els)
+    if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+      if (!h->st.n_slots) return ZBHIP_EUNSUPP;  // the handle was opened without message state
+      if (e.message_name >= P.strings.size() || e.correlation_var >= P.strings.size()) return ZBHIP_EINVAL;
+      P.has_msg = true;
+    }
   // condition variable names -> partition name ids, interned in element order (the oracle's order)
   for (auto& e : P.els) {
     if (e.element_type != ZBHIP_EL_SEQUENCE_FLOW || e.condition == ZBHIP_NONE16) continue;
@@ -349,6 +460,21 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         P.code[i].arg = (uint32_t)id;
       }
   }
+  // message names and correlation variables, then the bpmnProcessId, in element order (the
+  // oracle's order): the name dictionary is replicated across partitions by deploy order
+  if (P.has_msg) {
+    for (auto& e : P.els) {
+      if (e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) continue;
+      int mn = zbhip_intern(h, P.strings[e.message_name].c_str());
+      int cv = zbhip_intern(h, P.strings[e.correlation_var].c_str());
+      if (mn < 0 || cv < 0) return ZBHIP_ENOMEM;
+      e.message_name = (uint16_t)mn;
+      e.correlation_var = (uint16_t)cv;
+    }
+    int bn = zbhip_intern(h, P.strings[P.bpmn_id].c_str());
+    if (bn < 0) return ZBHIP_ENOMEM;
+    P.bpmn_name = (uint16_t)bn;
+  }
   // kernel variant: one token per instance at a time (no parallel gateway, no multi-outgoing
   // node other than an exclusive gateway) fits the small register/LDS configuration
   bool generic = false;
@@ -358,8 +484,9 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       generic = true;
   }
   const int old_variant = h->variant;
-  if (generic) h->variant = 1;
-  if (const char* fv = getenv("ZBHIP_FORCE_VARIANT")) h->variant = atoi(fv) ? 1 : 0;
+  if (generic && h->variant < 1) h->variant = 1;
+  if (P.has_msg) h->variant = 2;  // KMsg: message catch events, subscription commands, key scan
+  if (const char* fv = getenv("ZBHIP_FORCE_VARIANT")) h->variant = std::max(h->variant == 2 ? 2 : 0, atoi(fv) ? 1 : 0);
   h->procs.push_back(std::move(P));
   int rc = rebuild_program(h);
   if (rc != ZBHIP_OK) {
@@ -371,19 +498,34 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   return ZBHIP_OK;
 }
 
-// Splits the window into rounds so that each instance appears at most once per launch; commands
-// of one instance keep their log order across rounds (the reference processes them in log order).
+static bool slot_kind(uint8_t k) {
+  return k == ZBHIP_CMD_PUBLISH || k == ZBHIP_CMD_MSG_SUB_CREATE || k == ZBHIP_CMD_MSG_SUB_CORRELATE;
+}
+
+// Splits the window into rounds so that each subject (instance slot; correlation slot for message
+// commands) appears at most once per launch; commands of one subject keep their log order across
+// rounds (the reference processes them in log order).  Message commands may touch an instance of
+// this partition and instance commands a correlation slot, so a change between the two classes
+// starts a new epoch: every later command goes to a round after all earlier ones.
 static void plan_rounds(zbhip_handle* h) {
   h->round_begin.clear();
   h->h_order.clear();
-  std::unordered_map<uint32_t, uint32_t> last;
+  std::unordered_map<uint64_t, uint32_t> last;
   last.reserve(h->n_cmds * 2);
   std::vector<uint32_t> round_of(h->n_cmds);
-  uint32_t max_round = 0;
+  uint32_t max_round = 0, epoch = 0;
+  int cls = -1;
   for (size_t i = 0; i < h->n_cmds; ++i) {
-    auto it = last.find(h->h_cmds[i].instance);
-    uint32_t r = it == last.end() ? 0 : it->second + 1;
-    last[h->h_cmds[i].instance] = r;
+    const bool sk = slot_kind(h->h_cmds[i].kind);
+    if (h->msg() && cls >= 0 && (int)sk != cls && i > 0) {
+      epoch = max_round + 1;
+      last.clear();
+    }
+    cls = (int)sk;
+    const uint64_t subj = ((uint64_t)sk << 32) | h->h_cmds[i].instance;
+    auto it = last.find(subj);
+    uint32_t r = it == last.end() ? epoch : it->second + 1;
+    last[subj] = r;
     round_of[i] = r;
     max_round = std::max(max_round, r);
   }
@@ -397,9 +539,21 @@ static void plan_rounds(zbhip_handle* h) {
   for (size_t i = 0; i < h->n_cmds; ++i) h->h_order[pos[round_of[i]]++] = (uint32_t)i;
 }
 
-static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t n_docs) {
+static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t n_docs,
+                    const zbhip_xpart_cmd* xp, size_t n_xp) {
   for (size_t i = 0; i < n; ++i) {
     const zbhip_command& c = cmds[i];
+    if (slot_kind(c.kind) || c.kind == ZBHIP_CMD_PMS_CREATE || c.kind == ZBHIP_CMD_PMS_CORRELATE) {
+      if (!h->msg()) return ZBHIP_EUNSUPP;
+      if (c.doc_count) return ZBHIP_EINVAL;
+      if (slot_kind(c.kind) ? c.instance >= h->st.n_slots : c.instance >= h->cfg.max_instances) return ZBHIP_EINVAL;
+      if (c.kind == ZBHIP_CMD_PUBLISH) {
+        if (c.ref >= h->names.size() || c.instance >= h->strs.size()) return ZBHIP_EINVAL;
+      } else {
+        if (c.doc_begin >= n_xp || xp[c.doc_begin].kind != c.kind) return ZBHIP_EINVAL;
+      }
+      continue;
+    }
     if (c.instance >= h->cfg.max_instances) return ZBHIP_EINVAL;
     if (c.kind == ZBHIP_CMD_CREATE) {
       if (c.ref >= h->procs.size()) return ZBHIP_EINVAL;
@@ -413,14 +567,45 @@ static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t
   return ZBHIP_OK;
 }
 
+// uploads the Java hashCodes of strings interned since the last run
+static int sync_strings(zbhip_handle* h) {
+  if (h->d_str_n == h->strs.size()) return ZBHIP_OK;
+  if (h->strs.size() > h->d_str_cap) {
+    size_t cap = std::max<size_t>(1024, h->strs.size() * 2);
+    uint32_t* d = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&d), cap * sizeof(uint32_t)) != hipSuccess) return ZBHIP_ENOMEM;
+    if (h->d_str_n)
+      HIPCHK(hipMemcpyAsync(d, h->d_str_hash, h->d_str_n * sizeof(uint32_t), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    (void)hipFree(h->d_str_hash);
+    h->d_str_hash = d;
+    h->d_str_cap = cap;
+  }
+  HIPCHK(hipMemcpyAsync(h->d_str_hash + h->d_str_n, h->str_hash.data() + h->d_str_n,
+                        (h->strs.size() - h->d_str_n) * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->d_str_n = h->strs.size();
+  return ZBHIP_OK;
+}
+
 int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs, size_t n_docs) {
-  if (!h || (n && !cmds) || (n_docs && !docs)) return ZBHIP_EINVAL;
-  if (n > h->cfg.max_commands || n_docs > h->cfg.max_doc_entries) return ZBHIP_ENOMEM;
-  int rc = validate(h, cmds, n, n_docs);
+  return zbhip_submit_ex(h, cmds, n, docs, n_docs, nullptr, 0);
+}
+
+int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs, size_t n_docs,
+                    const zbhip_xpart_cmd* xparts, size_t n_xparts) {
+  if (!h || (n && !cmds) || (n_docs && !docs) || (n_xparts && !xparts)) return ZBHIP_EINVAL;
+  if (n > h->cfg.max_commands || n_docs > h->cfg.max_doc_entries || n_xparts > h->cfg.max_commands) return ZBHIP_ENOMEM;
+  int rc = validate(h, cmds, n, n_docs, xparts, n_xparts);
   if (rc) return rc;
   h->external = false;
   h->h_cmds.assign(cmds, cmds + n);
   h->h_docs.assign(docs, docs + n_docs);
+  h->h_xparts.assign(xparts, xparts + n_xparts);
+  h->n_xparts = n_xparts;
+  h->ext_xparts = nullptr;
+  if (n_xparts)
+    HIPCHK(hipMemcpyAsync(h->d_xparts, xparts, n_xparts * sizeof(zbhip_xpart_cmd), hipMemcpyHostToDevice, h->stream));
   h->n_cmds = n;
   h->n_docs = n_docs;
   h->doc_base = h->next_doc_base;
@@ -441,9 +626,17 @@ int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbh
 
 int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
                         size_t n_docs) {
+  return zbhip_submit_device_ex(h, dev_cmds, n, dev_docs, n_docs, nullptr, 0);
+}
+
+int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
+                           size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts) {
   if (!h || (n && !dev_cmds)) return ZBHIP_EINVAL;
   if (n > h->rec_slots) return ZBHIP_ENOMEM;
   h->external = true;
+  h->ext_xparts = dev_xparts;
+  h->n_xparts = n_xparts;
+  h->h_xparts.clear();
   h->ext_cmds = reinterpret_cast<const uint4*>(dev_cmds);
   h->ext_docs = dev_docs;
   h->h_cmds.clear();
@@ -499,6 +692,18 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.cmd_hdr = h->d_cmd_hdr;
   P.stats = h->d_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
+  if (h->msg()) {
+    int rc = sync_strings(h);
+    if (rc) return rc;
+    P.xparts = h->external ? h->ext_xparts : h->d_xparts;
+    P.n_xparts = (uint32_t)h->n_xparts;
+    P.str_hash = h->d_str_hash;
+    P.n_strs = (uint32_t)h->d_str_n;
+    P.cmd_hdr2 = h->d_cmd_hdr2;
+    P.xout = h->d_xout;
+    P.partition_id = h->cfg.partition_id;
+    P.partition_count = std::max(1, h->cfg.partition_count);
+  }
 
   // launches: one per round (commands of one instance are serialised in log order)
   h->launches.clear();
@@ -529,6 +734,13 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     P.region_base = h->launches[l].first;
     HIPCHK(launch_step(h->variant, P, h->stream));
   }
+  if (h->msg()) {
+    // keys of the window in log order: real process-instance keys, outbox and slot-row references
+    HIPCHK(launch_keyscan(h->d_cmd_hdr, h->d_cmd_hdr2, P.cmds, n, h->d_key_blk, h->d_key_base, h->d_key_counter,
+                          h->d_xout, h->st, (long long)h->cfg.partition_id << 51, h->stream));
+    h->bucketed = false;
+    for (auto& c : h->h_cmds) h->published |= c.kind == ZBHIP_CMD_PUBLISH;
+  }
   if (timed) HIPCHK(hipEventRecord(e1, h->stream));
   h->stats.launches = (uint32_t)spans.size();
   h->stats.rounds = (uint32_t)spans.size();
@@ -536,6 +748,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   h->ran = true;
   h->drain_cmd = 0;
   h->drain_rec = 0;
+  h->drain_ord = 0;
   h->results = false;
 
   if (!want || h->external) {
@@ -548,6 +761,9 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   // ---- results: headers + records gathered into log order (drain path, off the hot loop) ----
   h->h_hdr.resize(n);
   if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
+  h->h_hdr2.assign(n, make_uint4(0, 0, 0, 0));
+  if (n && h->msg())
+    HIPCHK(hipMemcpyAsync(h->h_hdr2.data(), h->d_cmd_hdr2, n * sizeof(uint4), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(launch_gather(h->d_regions, h->d_region_total, region, h->d_region_off, (size_t)B * h->rec_cap, h->d_rec,
                        h->d_stats + 64 * 8, h->stream));
   unsigned long long total = 0;
@@ -569,15 +785,34 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (off != total) return ZBHIP_EDEVICE;
 
   // key relabelling bookkeeping, in log (source) order
-  if (h->hist.size() < h->cfg.max_instances) {
-    h->hist.resize(h->cfg.max_instances);
+  const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
+  if (h->hist.size() < subjects) {
+    h->hist.resize(subjects);
     h->inst_proc.resize(h->cfg.max_instances, NONE);
   }
+  h->h_base.assign(n, 0);
   for (uint32_t c = 0; c < n; ++c) {
     const uint2 hd = h->h_hdr[c];
     const zbhip_command& cm = h->h_cmds[c];
     const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
+    h->h_base[c] = h->key_counter;
     if (((hd.y >> 16) & 0xFF) != ST_OK) continue;
+    if (h->msg() && slot_kind(cm.kind)) {
+      // the correlation slot's keys first, then the instance a local command loaded
+      const uint4 h2 = h->h_hdr2[c];
+      const uint32_t nsec = h2.y >> 16, nprim = nkeys - nsec;
+      const uint32_t subj = h->slot_subject(cm.instance);
+      if (nprim) {
+        h->hist[subj].push_back({(uint16_t)first, h->key_counter + 1});
+        h->batches.push_back({h->key_counter + 1, subj, (uint16_t)first, (uint16_t)nprim});
+      }
+      if (nsec) {
+        h->hist[h2.x].push_back({(uint16_t)(h2.y & 0xFFFF), h->key_counter + 1 + nprim});
+        h->batches.push_back({h->key_counter + 1 + nprim, h2.x, (uint16_t)(h2.y & 0xFFFF), (uint16_t)nsec});
+      }
+      h->key_counter += nkeys;
+      continue;
+    }
     if (cm.kind == ZBHIP_CMD_CREATE) {
       h->hist[cm.instance].clear();
       h->inst_proc[cm.instance] = cm.ref;
@@ -594,7 +829,9 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
 
 int64_t zbhip_pending_records(zbhip_handle* h) {
   if (!h || !h->results) return 0;
-  return (int64_t)h->h_out.size();
+  int64_t pay = 0;
+  for (auto& x : h->h_hdr2) pay += x.w;  // payload rows of message records
+  return (int64_t)h->h_out.size() - pay;
 }
 
 int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
@@ -627,13 +864,42 @@ int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
   return ZBHIP_OK;
 }
 
+// message record codes -> (record type, value type, intent)
+static bool message_code(uint32_t c6, zbhip_record& r) {
+  switch (c6) {
+    case C_PMS_CREATING: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_CREATING; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_PMS_CREATE: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_CREATE; r.record_type = ZBHIP_RT_COMMAND; return true;
+    case C_PMS_CREATED: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_CREATED; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_PMS_CORRELATE: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_CORRELATE; r.record_type = ZBHIP_RT_COMMAND; return true;
+    case C_PMS_CORRELATED: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_CORRELATED; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_MS_CREATE: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CREATE; r.record_type = ZBHIP_RT_COMMAND; return true;
+    case C_MS_CREATED: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CREATED; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_MS_CORRELATING: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CORRELATING; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_MS_CORRELATE: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CORRELATE; r.record_type = ZBHIP_RT_COMMAND; return true;
+    case C_MS_CORRELATED: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CORRELATED; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_MSG_PUBLISHED: r.value_type = ZBHIP_VT_MESSAGE; r.intent = ZBHIP_MSG_PUBLISHED; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_MSG_EXPIRED: r.value_type = ZBHIP_VT_MESSAGE; r.intent = ZBHIP_MSG_EXPIRED; r.record_type = ZBHIP_RT_EVENT; return true;
+    default: return false;
+  }
+}
+
+static uint8_t rejection_type_of(uint32_t reason) {
+  switch (reason) {
+    case ZBHIP_REASON_JOB_NOT_FOUND:
+    case ZBHIP_REASON_PMS_CREATE_NOT_FOUND:
+    case ZBHIP_REASON_PMS_CORR_NOT_FOUND:
+    case ZBHIP_REASON_MS_CORR_NOT_FOUND:
+      return ZBHIP_REJ_NOT_FOUND;
+    default:
+      return ZBHIP_REJ_INVALID_STATE;
+  }
+}
+
 int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
   if (!h || (cap && !out)) return ZBHIP_EINVAL;
   if (n_out) *n_out = 0;
   if (!h->results) return ZBHIP_ESTATE;
   size_t k = 0;
-  const int64_t pbits = (int64_t)h->cfg.partition_id << 51;
-  (void)pbits;
   while (k < cap && h->drain_cmd < h->n_cmds) {
     const size_t c = h->drain_cmd;
     const uint2 hd = h->h_hdr[c];
@@ -641,27 +907,63 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
     if (h->drain_rec >= nrec) {
       ++h->drain_cmd;
       h->drain_rec = 0;
+      h->drain_ord = 0;
       continue;
     }
     const zbhip_command& cm = h->h_cmds[c];
-    const uint32_t inst = cm.instance;
+    // the instance the records refer to: the command's, or the one a message batch loaded
+    const uint32_t inst = h->msg() && slot_kind(cm.kind) ? h->h_hdr2[c].x : cm.instance;
     const int64_t doc = cm.doc_count ? h->doc_base + cm.doc_begin : -1;
-    const uint2 w = h->h_out[h->h_off[c] + h->drain_rec];
+    const uint2* rows = h->h_out.data() + h->h_off[c];
+    const uint2 w = rows[h->drain_rec];
     const uint32_t key_ord = w.x & 0xFFFF, aux_ord = w.x >> 16, elem = w.y & 0xFFFF;
     const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
     const bool rej = code & kRejectBit;
     const uint32_t c6 = code & 0x3F;
     const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
     zbhip_record r{};
+    r.source_index = h->source_base + (int64_t)c;
+    r.rejection_type = ZBHIP_REJ_NONE;
+    r.ordinal = (uint16_t)h->drain_ord;
+    r.aux = -1;
+    r.message_key = -1;
+    r.correlation_key = ZBHIP_NO_STRING;
+    r.message_name = 0xFFFF;
+    r.bpmn_process_id = 0xFFFF;
+    if (h->msg() && elem != NONE && (elem & kPayloadBit)) {
+      // message record: 6 payload rows (kernels.hip emit_msg)
+      if (h->drain_rec + kPayloadRows >= nrec) return ZBHIP_EDEVICE;
+      const uint2* pl = rows + h->drain_rec + 1;
+      auto ll = [](uint2 v) { return (long long)(((unsigned long long)v.y << 32) | v.x); };
+      if (!message_code(c6, r)) return ZBHIP_EDEVICE;
+      const uint32_t el = elem & 0xFFF;
+      r.correlation_key = pl[0].x;
+      r.message_name = (uint16_t)(pl[0].y & 0xFFFF);
+      r.bpmn_process_id = (uint16_t)(pl[0].y >> 16);
+      r.key = h->resolve_ref(ll(pl[1]));
+      r.scope_key = h->resolve_ref(ll(pl[2]));
+      r.process_instance_key = h->resolve_ref(ll(pl[3]));
+      r.message_key = h->resolve_ref(ll(pl[4]));
+      r.partition = (int32_t)(pl[5].x & 0xFFFF);
+      r.interrupting = (uint8_t)(pl[5].x >> 16);
+      r.element_idx = el == kNoElem ? -1 : (int32_t)el;
+      r.process_idx = el == kNoElem || proc == NONE ? -1 : proc;
+      if (rej) {
+        r.record_type = ZBHIP_RT_REJECTION;
+        r.reason = fl & 0xF;
+        r.reason_arg = fl >> 4;
+        r.rejection_type = rejection_type_of(r.reason);
+      }
+      out[k++] = r;
+      h->drain_rec += 1 + kPayloadRows;
+      ++h->drain_ord;
+      continue;
+    }
     r.key = h->key_of(inst, key_ord);
     r.scope_key = aux_ord == NONE ? -1 : h->key_of(inst, aux_ord);
     r.process_instance_key = h->key_of(inst, 0);
-    r.source_index = h->source_base + (int64_t)c;
     r.process_idx = proc == NONE ? -1 : proc;
     r.element_idx = elem == NONE ? -1 : (int32_t)elem;
-    r.rejection_type = ZBHIP_REJ_NONE;
-    r.ordinal = (uint16_t)h->drain_rec;
-    r.aux = -1;
     r.reason = 0;
     r.reason_arg = 0;
     if (c6 >= 1 && c6 <= 10) {
@@ -708,6 +1010,7 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
     }
     out[k++] = r;
     ++h->drain_rec;
+    ++h->drain_ord;
   }
   if (n_out) *n_out = k;
   return ZBHIP_OK;
@@ -733,6 +1036,21 @@ int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* r, char* buf, si
       return snprintf(buf, cap, "Expected element instance to be in state 'ELEMENT_ACTIVATED' or one of '[ELEMENT_COMPLETING]' but was '%s'.", state_name(r->reason_arg));
     case ZBHIP_REASON_JOB_NOT_FOUND:
       return snprintf(buf, cap, "Expected to complete job with key '%lld', but no such job was found", (long long)r->key);
+    // processing/message/*Processor.java rejection texts
+    case ZBHIP_REASON_MS_ALREADY_OPEN:
+      return snprintf(buf, cap, "Expected to open a new message subscription for element with key '%lld' and message "
+                      "name '%s', but there is already a message subscription for that element key and message name opened",
+                      (long long)r->scope_key, zbhip_name(h, r->message_name));
+    case ZBHIP_REASON_PMS_CREATE_NOT_FOUND:
+      return snprintf(buf, cap, "Expected to create process message subscription with element key '%lld' and message "
+                      "name '%s', but no such subscription was found", (long long)r->scope_key, zbhip_name(h, r->message_name));
+    case ZBHIP_REASON_PMS_CREATE_NOT_OPENING:
+      return snprintf(buf, cap, "Expected to create process message subscription with element key '%lld' and message "
+                      "name '%s', but it is already %s", (long long)r->scope_key, zbhip_name(h, r->message_name),
+                      r->reason_arg ? "opened" : "closing");
+    case ZBHIP_REASON_MS_CORR_NOT_FOUND:
+      return snprintf(buf, cap, "Expected to correlate subscription for element with key '%lld' and message name '%s', "
+                      "but no such message subscription exists", (long long)r->scope_key, zbhip_name(h, r->message_name));
     default:
       if (cap) buf[0] = 0;
       return 0;
@@ -749,6 +1067,91 @@ int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t
   if (v >= it->base + it->nkeys) return ZBHIP_EINVAL;
   *instance = it->inst;
   *ordinal = (uint16_t)(it->first_ord + (v - it->base));
+  return ZBHIP_OK;
+}
+
+// ---- value dictionary ------------------------------------------------------------------------
+int64_t zbhip_intern_string(zbhip_handle* h, const char* bytes, size_t len) {
+  if (!h || (len && !bytes)) return ZBHIP_EINVAL;
+  std::string v(bytes ? bytes : "", len);
+  auto it = h->str_ids.find(v);
+  if (it != h->str_ids.end()) return it->second;
+  if (h->strs.size() >= 0xFFFFFFF0u) return ZBHIP_ENOMEM;
+  const uint32_t id = (uint32_t)h->strs.size();
+  h->str_hash.push_back((uint32_t)java_hash(v.data(), v.size()));
+  h->strs.push_back(std::move(v));
+  h->str_ids.emplace(h->strs.back(), id);
+  return id;
+}
+
+int zbhip_intern_strings(zbhip_handle* h, const char* bytes, const uint64_t* offsets, size_t n, uint32_t* ids_out) {
+  if (!h || (n && (!bytes || !offsets))) return ZBHIP_EINVAL;
+  h->strs.reserve(h->strs.size() + n);
+  h->str_hash.reserve(h->str_hash.size() + n);
+  for (size_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i]) return ZBHIP_EINVAL;
+    int64_t id = zbhip_intern_string(h, bytes + offsets[i], offsets[i + 1] - offsets[i]);
+    if (id < 0) return (int)id;
+    if (ids_out) ids_out[i] = (uint32_t)id;
+  }
+  return ZBHIP_OK;
+}
+
+const char* zbhip_string_value(zbhip_handle* h, uint32_t id, size_t* len) {
+  if (!h || id >= h->strs.size()) {
+    if (len) *len = 0;
+    return "";
+  }
+  if (len) *len = h->strs[id].size();
+  return h->strs[id].c_str();
+}
+
+int32_t zbhip_subscription_partition(const char* bytes, size_t len, int32_t partition_count) {
+  if (partition_count <= 0) return ZBHIP_EINVAL;
+  const int32_t r = java_hash(bytes, len) % partition_count;
+  return (r < 0 ? -r : r) + 1;
+}
+
+// ---- outbox --------------------------------------------------------------------------------------
+int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_out) {
+  if (!h || !n_out) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (!h->results) return h->msg() ? ZBHIP_ESTATE : ZBHIP_OK;
+  if (!h->msg()) return ZBHIP_OK;
+  const size_t n = h->n_cmds;
+  h->h_xout.resize(n * kOut);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(h->h_xout.data(), h->d_xout, n * kOut * sizeof(zbhip_xpart_cmd), hipMemcpyDeviceToHost,
+                          h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  size_t k = 0;
+  for (size_t c = 0; c < n; ++c) {
+    if (((h->h_hdr[c].y >> 16) & 0xFF) != ST_OK) continue;
+    for (uint32_t j = 0; j < h->h_hdr2[c].z && j < (uint32_t)kOut; ++j) {
+      const zbhip_xpart_cmd& x = h->h_xout[c * kOut + j];
+      if (x.kind == XK_PATCH) continue;
+      if (out && k < cap) out[k] = x;
+      ++k;
+    }
+  }
+  *n_out = k;
+  return ZBHIP_OK;
+}
+
+int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32_t* counts) {
+  if (!h || !dev_out || !counts) return ZBHIP_EINVAL;
+  if (!h->msg() || !h->ran) return ZBHIP_ESTATE;
+  const uint32_t parts = (uint32_t)std::max(1, h->cfg.partition_count);
+  if (parts > 1024) return ZBHIP_EINVAL;
+  if (!h->bucketed) {
+    HIPCHK(launch_bucket(h->d_cmd_hdr, h->d_cmd_hdr2, h->d_xout, (uint32_t)h->n_cmds, parts, h->d_blk_cnt,
+                         h->d_xcount, h->d_xbucket, h->stream));
+    h->bucketed = true;
+  }
+  HIPCHK(hipMemcpyAsync(counts, h->d_xcount, parts * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  *dev_out = h->d_xbucket;
   return ZBHIP_OK;
 }
 
@@ -784,7 +1187,16 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   std::vector<uint2> slots(N * kSlots), vm(N * kVars);
   std::vector<long long> vv(N * kVars);
   std::vector<uint32_t> join(N * kJoinWords);
+  const size_t S = h->st.n_slots;
+  std::vector<uint4> pms(S ? N : 0), sub_a(S * kSubs);
+  std::vector<longlong2> sub_b(S * kSubs), sub_k(S * kSubs);
   HIPCHK(hipStreamSynchronize(h->stream));
+  if (S) {
+    HIPCHK(hipMemcpy(pms.data(), h->st.pms, N * sizeof(uint4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(sub_a.data(), h->st.sub_a, S * kSubs * sizeof(uint4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(sub_b.data(), h->st.sub_b, S * kSubs * sizeof(longlong2), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(sub_k.data(), h->st.sub_k, S * kSubs * sizeof(longlong2), hipMemcpyDeviceToHost));
+  }
   HIPCHK(hipMemcpy(hdr.data(), h->st.hdr, N * sizeof(uint4), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(slots.data(), h->st.slots, N * kSlots * sizeof(uint2), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(vm.data(), h->st.var_meta, N * kVars * sizeof(uint2), hipMemcpyDeviceToHost));
@@ -834,7 +1246,7 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
       sink(ctx, buf);
       snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, pik);
       sink(ctx, buf);
-      if (E.element_type == ZBHIP_EL_SERVICE_TASK) {
+      if (E.element_type == ZBHIP_EL_SERVICE_TASK || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
         snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", k);
         sink(ctx, buf);
       }
@@ -859,6 +1271,18 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
                h->names[m.x & 0xFFFF].c_str(), h->key_of(inst, m.y & 0xFFFF), (m.y >> 16) & 0xFF, vv[(size_t)v * N + i]);
       sink(ctx, buf);
     }
+    if (S && ((pms[i].x >> 12) & 3)) {  // PROCESS_SUBSCRIPTION_BY_KEY [eik, name] (DbProcessMessageSubscriptionState)
+      const uint4 m = pms[i];
+      const uint32_t el = m.x & 0xFFF;
+      const zbhip_element& E = P.els[el];
+      snprintf(buf, sizeof buf,
+               "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%u,processInstanceKey=%lld,"
+               "bpmnProcessId=%s,messageKey=-1,correlationKey=%s,elementId=%s,interrupting=%u",
+               h->key_of(inst, m.y & 0xFFFF), zbhip_name(h, E.message_name), h->key_of(inst, m.y >> 16),
+               ((m.x >> 12) & 3) == 1 ? "OPENING" : "OPENED", m.x >> 16, pik, zbhip_name(h, P.bpmn_name),
+               zbhip_string_value(h, m.z, nullptr), P.id(el).c_str(), (m.x >> 14) & 1);
+      sink(ctx, buf);
+    }
     if (P.n_join_slots) {
       for (uint32_t f = 0; f < P.els.size(); ++f) {
         const zbhip_element& E = P.els[f];
@@ -872,6 +1296,27 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
       }
     }
   }
+  // MESSAGE_SUBSCRIPTION_BY_KEY [eik, name] and MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY
+  // [tenant, name, correlationKey, eik] of this (message) partition (DbMessageSubscriptionState)
+  for (size_t slot = 0; slot < S; ++slot)
+    for (int r = 0; r < kSubs; ++r) {
+      const size_t ri = (size_t)r * S + slot;
+      const uint4 a = sub_a[ri];
+      const uint32_t st = a.x & 0xFF;
+      if (st != 1 && st != 2) continue;
+      const char* name = zbhip_name(h, a.y & 0xFFFF);
+      const char* corr = zbhip_string_value(h, (uint32_t)slot, nullptr);
+      snprintf(buf, sizeof buf,
+               "MESSAGE_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,correlating=%d,processInstanceKey=%lld,bpmnProcessId=%s,"
+               "messageKey=%lld,correlationKey=%s,interrupting=%u",
+               (long long)sub_b[ri].x, name, (long long)sub_k[ri].x, st == 2 ? 1 : 0, (long long)sub_b[ri].y,
+               zbhip_name(h, a.y >> 16), (long long)sub_k[ri].y, corr, (a.x >> 8) & 1);
+      sink(ctx, buf);
+      snprintf(buf, sizeof buf, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY|<default>|%s|%s|%lld", name, corr,
+               (long long)sub_b[ri].x);
+      sink(ctx, buf);
+    }
+  if (h->published) sink(ctx, "MESSAGE_STATS|messagesDeadlineCount|0");
   return ZBHIP_OK;
 }
 

@@ -17,6 +17,18 @@ constexpr int kMaxElements = 4095;        // 12-bit element index in queue entri
 
 constexpr uint16_t NONE = 0xFFFF;
 
+// ---- message correlation (config 5; kernel variant KMsg) ----
+constexpr int kSubs = 4;           // message-subscription rows per correlation slot (HBM)
+constexpr int kOut = 6;            // outbox entries per command (sends + local-row key patches)
+constexpr uint8_t XK_PATCH = 0xFF; // outbox entry kind: patch the real keys of a locally inserted row
+constexpr uint32_t kNoElem = 0xFFF;       // element field of records without an element
+constexpr uint32_t kPayloadBit = 1u << 14; // record followed by kPayloadRows payload rows
+constexpr int kPayloadRows = 6;
+// 64-bit key references inside payload rows and outbox entries: >= 0 a real key, -1 none,
+// <= -2 an ordinal: v = -2 - ref, space = v >> 16 (0: the lane's instance, 1: the lane's
+// correlation slot), ord = v & 0xFFFF.  The device key scan / the host drain resolve them.
+enum : uint32_t { KS_INST = 0, KS_SLOT = 1 };
+
 // ElementInstance.jobKey encodings in a slot (ElementInstance.java:23-54: default 0,
 // JobCreatedApplier sets the job key, JobCompletedApplier sets -1)
 constexpr uint16_t JOB_ZERO = 0xFFFF;
@@ -35,6 +47,18 @@ enum : uint8_t {
   C_VAR_UPDATED = 21,
   C_PE_TRIGGERING = 24,
   C_PIC_CREATED = 28,
+  C_PMS_CREATING = 32,
+  C_PMS_CREATE = 33,
+  C_PMS_CREATED = 34,
+  C_PMS_CORRELATE = 35,
+  C_PMS_CORRELATED = 36,
+  C_MS_CREATE = 40,
+  C_MS_CREATED = 41,
+  C_MS_CORRELATING = 42,
+  C_MS_CORRELATE = 43,
+  C_MS_CORRELATED = 44,
+  C_MSG_PUBLISHED = 49,
+  C_MSG_EXPIRED = 50,
   kRejectBit = 0x40,
 };
 
@@ -56,6 +80,8 @@ enum : uint8_t {
   FB_JOIN = 12,        // taken-sequence-flow counter overflow
   FB_SLOTS = 13,       // more persistent element instances than kSlots
   FB_BAD_PROCESS = 14, // unknown process / no none start event
+  FB_MESSAGE = 15,     // message path outside the subset (NUMBER correlation key, second open
+                       // subscription, rejected correlation, full correlation slot, outbox overflow)
 };
 
 // Program arena (u32 words), LDS-staged by every workgroup:
@@ -79,6 +105,18 @@ struct DevState {
   long long* var_val;// [kVars][n]
   uint32_t* join;    // [kJoinWords][n]
   uint32_t n;
+  // message correlation (allocated when max_correlation_keys > 0)
+  uint4* pms;        // [n] PROCESS_SUBSCRIPTION row of the instance's waiting catch event:
+                     //     x = elem | state << 12 (0 none, 1 opening, 2 opened) | interrupting << 14 | subpart << 16
+                     //     y = eik ord | subscription key ord << 16; z = correlation key id; w = 0
+  long long* pi_key; // [n] real process-instance key (written by the device key scan)
+  uint2* slot_hdr;   // [S] x = next key ordinal of the correlation slot; y = 0
+  uint4* sub_a;      // [kSubs][S] MESSAGE_SUBSCRIPTION rows: x = state (0 free, 1 open, 2 correlating)
+                     //   | interrupting << 8 | key-in-instance-space << 9 | PI partition << 16;
+                     //   y = message name | bpmnProcessId << 16; z = PI instance slot; w = eik ord | key ord << 16
+  longlong2* sub_b;  // [kSubs][S] x = element instance key, y = process instance key (real)
+  longlong2* sub_k;  // [kSubs][S] x = subscription key, y = message key while correlating (-1 else)
+  uint32_t n_slots;
 };
 
 struct StepParams {
@@ -100,6 +138,15 @@ struct StepParams {
   unsigned long long* stats;  // [64][8] spread accumulators: records, transitions, completed, keys,
                               // fallback, commands
   int32_t max_cmds_in_batch;
+  // message correlation (KMsg)
+  const zbhip_xpart_cmd* xparts;
+  uint32_t n_xparts;
+  const uint32_t* str_hash;   // [n_strs] Java hashCode of each value-dictionary string
+  uint32_t n_strs;
+  uint4* cmd_hdr2;            // [n_cmds] x = secondary instance, y = first ord | nkeys << 16 (secondary
+                              // space), z = outbox entries, w = payload rows
+  zbhip_xpart_cmd* xout;      // [n_cmds * kOut]
+  int32_t partition_id, partition_count;
 };
 
 }  // namespace zb

@@ -45,16 +45,19 @@ class Partition:
     """One Zeebe partition executed on one MI355X (a libzbhip handle)."""
 
     def __init__(self, partition_id=1, partition_count=1, device=0, max_instances=1 << 16, max_commands=1 << 16,
-                 max_records_per_batch=64, max_doc_entries=0, max_commands_in_batch=100, initial_key=0, stream=None):
+                 max_records_per_batch=64, max_doc_entries=0, max_commands_in_batch=100, initial_key=0, stream=None,
+                 max_correlation_keys=0):
         self.L = load()
         cfg = abi.Config(partition_id=partition_id, partition_count=partition_count, device=device,
                          max_commands_in_batch=max_commands_in_batch, max_instances=max_instances,
                          max_commands=max_commands, max_records_per_batch=max_records_per_batch,
-                         max_doc_entries=max_doc_entries, initial_key=initial_key, stream=stream)
+                         max_doc_entries=max_doc_entries, initial_key=initial_key, stream=stream,
+                         max_correlation_keys=max_correlation_keys)
         h = C.c_void_p()
         check(self.L.zbhip_open(C.byref(cfg), C.byref(h)), "zbhip_open")
         self.h = h
         self.partition_id = partition_id
+        self.partition_count = partition_count
         self.processes = []
         self.max_commands = max_commands
 
@@ -101,14 +104,50 @@ class Partition:
         return self.processes[proc].element_ids[elem]
 
     # ---- commands ----
-    def submit(self, cmds, docs=None):
+    def submit(self, cmds, docs=None, xparts=None):
         cmds = np.ascontiguousarray(cmds, dtype=abi.COMMAND_DTYPE)
         docs = np.ascontiguousarray(docs if docs is not None else abi.make_docs(0), dtype=abi.DOC_DTYPE)
-        check(self.L.zbhip_submit(self.h, cmds.ctypes.data, len(cmds), docs.ctypes.data, len(docs)), "zbhip_submit")
+        xp = np.ascontiguousarray(xparts if xparts is not None else abi.make_xparts(0), dtype=abi.XPART_DTYPE)
+        check(self.L.zbhip_submit_ex(self.h, cmds.ctypes.data, len(cmds), docs.ctypes.data, len(docs),
+                                     xp.ctypes.data if len(xp) else None, len(xp)), "zbhip_submit")
 
-    def submit_device(self, cmd_ptr, n, doc_ptr=0, n_docs=0):
+    def submit_device(self, cmd_ptr, n, doc_ptr=0, n_docs=0, xpart_ptr=0, n_xparts=0):
         """Commands already resident in HBM (e.g. a torch uint8 tensor's data_ptr())."""
-        check(self.L.zbhip_submit_device(self.h, cmd_ptr, n, doc_ptr or None, n_docs), "zbhip_submit_device")
+        check(self.L.zbhip_submit_device_ex(self.h, cmd_ptr, n, doc_ptr or None, n_docs, xpart_ptr or None, n_xparts),
+              "zbhip_submit_device")
+
+    # ---- value dictionary (correlation keys) ----
+    def intern_string(self, value):
+        b = value.encode() if isinstance(value, str) else value
+        return check(self.L.zbhip_intern_string(self.h, b, len(b)), "zbhip_intern_string")
+
+    def intern_strings(self, values):
+        bs = [v.encode() if isinstance(v, str) else v for v in values]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs])
+        blob = b"".join(bs)
+        ids = np.zeros(len(bs), dtype=np.uint32)
+        check(self.L.zbhip_intern_strings(self.h, blob, off.ctypes.data, len(bs), ids.ctypes.data), "intern_strings")
+        return ids
+
+    def string_value(self, sid):
+        return self.L.zbhip_string_value(self.h, sid, None).decode()
+
+    # ---- cross-partition outbox (SubscriptionCommandSender sends) ----
+    def outbox(self):
+        n = C.c_size_t()
+        check(self.L.zbhip_outbox(self.h, None, 0, C.byref(n)), "zbhip_outbox")
+        out = abi.make_xparts(n.value)
+        if n.value:
+            check(self.L.zbhip_outbox(self.h, out.ctypes.data, n.value, C.byref(n)), "zbhip_outbox")
+        return out
+
+    def outbox_device(self):
+        """(device pointer, per-target counts) of the outbox bucketed by target partition."""
+        ptr = C.c_void_p()
+        counts = np.zeros(max(1, self.partition_count), dtype=np.uint32)
+        check(self.L.zbhip_outbox_device(self.h, C.byref(ptr), counts.ctypes.data), "zbhip_outbox_device")
+        return ptr.value or 0, counts
 
     def run(self, flags=0):
         return check(self.L.zbhip_run(self.h, flags), "zbhip_run")
@@ -123,7 +162,8 @@ class Partition:
     def reason(self, rec):
         r = abi.Record()
         for f, _ in abi.Record._fields_:
-            setattr(r, f, int(rec[f]))
+            if f != "pad":
+                setattr(r, f, int(rec[f]))
         buf = C.create_string_buffer(512)
         self.L.zbhip_rejection_reason(self.h, C.byref(r), buf, 512)
         return buf.value.decode()
@@ -148,7 +188,7 @@ class Partition:
 
     FALLBACK_REASONS = {1: "queue", 2: "table", 3: "records", 4: "keys", 5: "batch-limit", 6: "feel", 7: "vars",
                         8: "slot-in-use", 9: "no-condition", 10: "unsupported", 11: "doc", 12: "join",
-                        13: "slots", 14: "bad-process"}
+                        13: "slots", 14: "bad-process", 15: "message"}
 
     def command_status(self, i):
         st, rs = C.c_uint32(), C.c_uint32()

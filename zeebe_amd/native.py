@@ -19,7 +19,9 @@ ERRORS = {-1: "ZBHIP_EINVAL", -2: "ZBHIP_ENOMEM", -3: "ZBHIP_EDEVICE", -4: "ZBHI
 SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", "zbhip_deploy", "zbhip_intern",
            "zbhip_string", "zbhip_name", "zbhip_submit", "zbhip_submit_device", "zbhip_run", "zbhip_drain",
            "zbhip_pending_records", "zbhip_get_stats", "zbhip_export_state", "zbhip_fallback",
-           "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info", "zbhip_command_status"]
+           "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info", "zbhip_command_status",
+           "zbhip_submit_ex", "zbhip_submit_device_ex", "zbhip_intern_string", "zbhip_intern_strings",
+           "zbhip_string_value", "zbhip_subscription_partition", "zbhip_outbox", "zbhip_outbox_device"]
 
 
 class ZbhipError(RuntimeError):
@@ -65,6 +67,17 @@ def load():
     L.zbhip_resolve_key.argtypes = [vp, i64, C.POINTER(u32), C.POINTER(C.c_uint16)]
     L.zbhip_rejection_reason.argtypes = [vp, C.POINTER(abi.Record), C.c_char_p, sz]
     L.zbhip_command_status.argtypes = [vp, sz, C.POINTER(u32), C.POINTER(u32)]
+    L.zbhip_submit_ex.argtypes = [vp, vp, sz, vp, sz, vp, sz]
+    L.zbhip_submit_device_ex.argtypes = [vp, vp, sz, vp, sz, vp, sz]
+    L.zbhip_intern_string.argtypes = [vp, C.c_char_p, sz]
+    L.zbhip_intern_string.restype = i64
+    L.zbhip_intern_strings.argtypes = [vp, C.c_char_p, vp, sz, vp]
+    L.zbhip_string_value.argtypes = [vp, u32, C.POINTER(sz)]
+    L.zbhip_string_value.restype = C.c_char_p
+    L.zbhip_subscription_partition.argtypes = [C.c_char_p, sz, C.c_int32]
+    L.zbhip_subscription_partition.restype = C.c_int32
+    L.zbhip_outbox.argtypes = [vp, vp, sz, C.POINTER(sz)]
+    L.zbhip_outbox_device.argtypes = [vp, C.POINTER(vp), vp]
     L.zbhip_build_info.argtypes = []
     L.zbhip_build_info.restype = C.c_char_p
     _lib = L
