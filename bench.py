@@ -10,7 +10,11 @@ synthetic and already resident in HBM; nothing is skipped inside the timed regio
 Multi-GPU: one process per GPU, one Zeebe partition per GPU (Protocol.encodePartitionId),
 instances keyed to partitions; no data-path collective (weak scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config linear10|one_task|xor|forkjoin8]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config linear10|one_task|xor|forkjoin8|msg]
+
+--config msg is configs[4]: a message catch event correlated across partitions (one partition per
+GPU; the subscription commands between partitions go through RCCL all-to-all over xGMI, or, with
+--virtual-partitions P on one GPU, through device-to-device copies between P partitions).
 """
 import argparse
 import json
@@ -60,6 +64,166 @@ def algorithmic_bytes(name, n, phases):
     return 0
 
 
+def run_msg(args, world, rank, local_rank, dist):
+    """configs[4]: start -> message catch (`= key`) -> end, n instances per partition, one message per
+    correlation key published on its message partition (SubscriptionUtil), time-to-live 0.  One step:
+    CREATE windows -> exchange (MESSAGE_SUBSCRIPTION:CREATE, PROCESS_MESSAGE_SUBSCRIPTION:CREATE) ->
+    PUBLISH windows -> exchange (PROCESS_MESSAGE_SUBSCRIPTION:CORRELATE, MESSAGE_SUBSCRIPTION:CORRELATE),
+    every window run to quiescence on the device; inputs resident in HBM."""
+    import numpy as np
+    import torch
+
+    from zeebe_amd import abi, bpmn
+    from zeebe_amd.engine import Partition
+    from zeebe_amd.exchange import XPART_BYTES, DeviceExchange, LocalExchange
+
+    dev = torch.device("cuda", local_rank)
+    vp = args.virtual_partitions if world == 1 else 1
+    P = world * vp  # partitions in the cluster
+    n = args.instances or 1_000_000
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    my_parts = list(range(rank * vp + 1, rank * vp + vp + 1))
+    parts = [Partition(partition_id=p, partition_count=P, device=local_rank, max_instances=n, max_commands=4 * n,
+                       max_correlation_keys=n * P, max_records_per_batch=128, stream=stream) for p in my_parts]
+    xml = bpmn.message_catch_process()
+    t_setup = time.perf_counter()
+    blob_parts, offs = [], [0]
+    for p in range(1, P + 1):
+        for i in range(n):
+            b = b"k-%d-%d" % (p, i)
+            blob_parts.append(b)
+            offs.append(offs[-1] + len(b))
+    blob = b"".join(blob_parts)
+    offsets = np.asarray(offs, dtype=np.uint64)
+    import ctypes as C
+    ids = None
+    for part in parts:
+        part.deploy(xml)
+        got = np.zeros(n * P, dtype=np.uint32)
+        from zeebe_amd.native import check
+        check(part.L.zbhip_intern_strings(part.h, blob, offsets.ctypes.data, n * P, got.ctypes.data))
+        assert ids is None or np.array_equal(ids, got)  # replicated dictionary
+        ids = got
+    var_id, name_id = parts[0].intern("key"), parts[0].intern("msg")
+    owner = parts[0].string_partitions(ids, P)  # message partition of every key
+    windows = []
+    for p, part in zip(my_parts, parts):
+        create = abi.make_commands(n)
+        create["instance"] = np.arange(n, dtype=np.uint32)
+        create["kind"] = abi.CMD_CREATE
+        create["doc_count"] = 1
+        create["doc_begin"] = np.arange(n, dtype=np.uint32)
+        docs = abi.make_docs(n)
+        docs["name_id"] = var_id
+        docs["type"] = abi.DOC_STR
+        docs["value"] = ids[(p - 1) * n:p * n]
+        mine = ids[owner == p]
+        pub = abi.make_commands(len(mine))
+        pub["instance"] = mine
+        pub["kind"] = abi.CMD_PUBLISH
+        pub["ref"] = name_id
+        windows.append(tuple(torch.from_numpy(a.view(np.uint8).copy()).to(dev) for a in (create, docs, pub)) +
+                       (len(mine),))
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+    exch = LocalExchange(parts, 4 * n, dev) if world == 1 else DeviceExchange()
+    staging = torch.empty(4 * n * XPART_BYTES, dtype=torch.uint8, device=dev) if world > 1 else None
+
+    def exchange_until_quiet(flags):
+        rounds = 0
+        while rounds < 6:
+            if world == 1:
+                if sum(exch.step()) == 0:
+                    break
+                exch.deliver(flags)
+            else:
+                _, total = exch.exchange_partition(parts[0], staging, flags)
+                if total == 0:
+                    break
+            rounds += 1
+        return rounds
+
+    def step(first, timed=False):
+        flags = abi.RUN_NO_RESULTS | (abi.RUN_TIMED if timed else 0)
+        for k, (part, (cw, dw, pw, npub)) in enumerate(zip(parts, windows)):
+            part.submit_device(cw.data_ptr(), n, dw.data_ptr(), n)
+            part.run(flags | (0 if first else abi.RUN_ACCUMULATE))
+        r1 = exchange_until_quiet(flags | abi.RUN_ACCUMULATE)
+        for part, (cw, dw, pw, npub) in zip(parts, windows):
+            part.submit_device(pw.data_ptr(), npub)
+            part.run(flags | abi.RUN_ACCUMULATE)
+        r2 = exchange_until_quiet(flags | abi.RUN_ACCUMULATE)
+        return r1, r2
+
+    for k in range(args.warmup):
+        step(first=(k == 0))
+    for part in parts:
+        s = part.stats()
+        assert s["fallback"] == 0, s
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rounds = None
+    for k in range(args.steps):
+        rounds = step(first=(k == 0))
+    st = [part.stats() for part in parts]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    assert all(s["fallback"] == 0 for s in st), st
+    tr = sum(s["transitions"] for s in st)
+    comp = sum(s["completed_instances"] for s in st)
+    recs = sum(s["records"] for s in st)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([tr, comp, recs], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        tr, comp, recs = (int(x) for x in c.tolist())
+    assert comp == n * P * args.steps, (comp, n * P * args.steps)
+    # device time of the lifecycle kernel launches + key scans (untimed pass)
+    step(first=True, timed=True)
+    st = [part.stats() for part in parts]
+    dev_ms = sum(s["step_ms"] for s in st)
+    # bytes per instance over both partitions (DESIGN.md §3, config 5): commands 16 B x 4 windows,
+    # records 8 B x rows, instance rows 16+8+16 B read+written per PI window, slot rows 48 B written
+    # and read, 48-byte subscription commands written, bucketed, exchanged and read (x4)
+    rows = sum(s["records"] for s in st) / max(1, n * P)
+    alg_per_inst = 16 * 6 + 8 * (rows + 6 * 10) + 2 * 40 * 3 + 2 * 48 * 3 + 4 * 48 * 4
+    alg = alg_per_inst * n * P
+    result = {
+        "metric": "BPMN element transitions/sec + completed instances/sec, 1/2/4/8 MI355X",
+        "value": tr / elapsed,
+        "unit": "transitions/s",
+        "completed_instances_per_s": comp / elapsed,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic: %d instances/partition, correlation keys k-<p>-<i>, one message per key (TTL 0)" % n,
+        "config": {"workload": "configs[4] message catch event correlated across partitions",
+                   "instances_per_partition": n, "partitions": P, "partitions_per_gpu": vp,
+                   "exchange": "rccl all_to_all_single" if world > 1 else ("device copies" if P > 1 else "none (local)"),
+                   "exchange_rounds": rounds, "parallelism": "one partition per GPU (dp%d)" % world},
+        "records_per_s": recs / elapsed,
+        "setup_s": setup_s,
+        "roofline": {"bound": "hbm", "kernel": "k_step<KMsg> + key scan", "achieved": alg / (dev_ms * 1e-3) / 1e9 / world,
+                     "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": alg / (dev_ms * 1e-3) / 1e9 / world / PEAK_HBM_GBPS,
+                     "traffic": None, "algorithmic_bytes_per_instance": alg_per_inst, "device_ms_per_step": dev_ms},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,6 +234,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-instances", type=int, default=300_000, help="instances per CPU thread (bounded sample)")
+    ap.add_argument("--virtual-partitions", type=int, default=1,
+                    help="--config msg on one GPU: partitions hosted by this process (exchange by device copies)")
     args = ap.parse_args()
 
     import numpy as np
@@ -84,6 +250,8 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
+    if args.config == "msg":
+        return run_msg(args, world, rank, local_rank, dist)
 
     from zeebe_amd import abi
     from zeebe_amd.engine import Partition

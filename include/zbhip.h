@@ -380,8 +380,20 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx);
 int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_out);
 /* Device form: after zbhip_run (any mode) the outbox bucketed by target partition, stable in log
  * order, with device-computed keys; counts[t] = entries for partition t + 1 (partition_count
- * entries).  The pointer stays valid until the next run.  This is what the RCCL all-to-all sends. */
+ * entries).  The pointer stays valid until the next run.  This is what the RCCL all-to-all sends.
+ * The outbox is handed out once: later calls before the next run report zero counts. */
 int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32_t* counts);
+
+/* Copies bucketed outbox entries [first, first + count) (zbhip_outbox_device order) to dev_dst,
+ * asynchronously on the handle's stream. */
+int zbhip_outbox_copy(zbhip_handle* h, void* dev_dst, size_t first, size_t count);
+/* Receiving side of the exchange: submits the n received commands at dev_xparts (device memory,
+ * arrival order) as the next window, building its commands on the device (subject = the PI
+ * instance slot for PROCESS_MESSAGE_SUBSCRIPTION commands, the correlation slot otherwise).
+ * dev_xparts must stay valid until zbhip_run returns. */
+int zbhip_submit_xparts_device(zbhip_handle* h, const zbhip_xpart_cmd* dev_xparts, size_t n);
+/* SubscriptionUtil.getSubscriptionPartitionId of n interned strings (out[i] in 1..partition_count). */
+int zbhip_string_partitions(zbhip_handle* h, const uint32_t* ids, size_t n, int32_t partition_count, int32_t* out);
 
 /* Instances whose last batch needs the fallback path (incident, FEEL outside the
  * subset, batch-limit overflow, capacity).  Their state was left untouched. */

@@ -166,3 +166,68 @@ def test_gpu_outbox_device_buckets():
     for f in XPART_FIELDS:
         assert np.array_equal(got[f], want[f]), f
     assert [int(x) for x in counts] == [int(np.sum(host["target_partition"] == t)) for t in range(1, P + 1)]
+
+
+@pytest.mark.parametrize("P", [1, 4])
+def test_gpu_device_exchange_runs_the_protocol(P):
+    """The bench path: device-resident windows, device outbox buckets, device-to-device exchange
+    between P partitions on one GPU (no host relabelling): every instance completes, the
+    per-partition record/transition counts equal the oracle cluster's."""
+    import torch
+    from zeebe_amd.exchange import LocalExchange
+    n = 512
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    parts = [Partition(partition_id=p, partition_count=P, max_instances=n, max_commands=4 * n,
+                       max_correlation_keys=n * P, max_records_per_batch=128, stream=stream) for p in range(1, P + 1)]
+    keys = ["k-%d-%d" % (p, i) for p in range(1, P + 1) for i in range(n)]
+    for part in parts:
+        part.deploy(XML)
+        ids = part.intern_strings(keys)
+    var_id, name_id = parts[0].intern("key"), parts[0].intern("msg")
+    owner = parts[0].string_partitions(ids, P)
+    flags = abi.RUN_NO_RESULTS
+    bufs = []
+    for p, part in enumerate(parts, 1):
+        c = create_commands(n)
+        c["doc_count"] = 1
+        c["doc_begin"] = np.arange(n)
+        d = string_docs(var_id, ids[(p - 1) * n:p * n])
+        tc = torch.from_numpy(c.view(np.uint8).copy()).to(dev)
+        td = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        bufs += [tc, td]
+        part.submit_device(tc.data_ptr(), n, td.data_ptr(), n)
+        part.run(flags)
+    ex = LocalExchange(parts, 4 * n, dev)
+    for _ in range(4):
+        if sum(ex.step()) == 0:
+            break
+        ex.deliver(flags | abi.RUN_ACCUMULATE)
+    for p, part in enumerate(parts, 1):
+        mine = ids[owner == p]
+        pub = abi.make_commands(len(mine))
+        pub["instance"] = mine
+        pub["kind"] = abi.CMD_PUBLISH
+        pub["ref"] = name_id
+        tp = torch.from_numpy(pub.view(np.uint8).copy()).to(dev)
+        bufs.append(tp)
+        part.submit_device(tp.data_ptr(), len(mine))
+        part.run(flags | abi.RUN_ACCUMULATE)
+    for _ in range(4):
+        if sum(ex.step()) == 0:
+            break
+        ex.deliver(flags | abi.RUN_ACCUMULATE)
+    torch.cuda.synchronize()
+    st = [part.stats() for part in parts]
+    assert all(s["fallback"] == 0 for s in st), st
+    assert sum(s["completed_instances"] for s in st) == n * P
+    # the oracle cluster on the same inputs
+    orc = MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], OracleAdapter, XML)
+    oids = orc.intern_keys(keys)
+    orc.create(n, [oids[(p - 1) * n:p * n] for p in range(1, P + 1)])
+    orc.publish(oids, [int(x) for x in owner])
+    for s, o in zip(st, orc.parts):
+        c = o.counters()
+        assert s["transitions"] == c["transitions"] and s["completed_instances"] == c["completed_instances"]
+    # records of every partition (device stats) = the oracle's
+    assert sum(s["records"] for s in st) == sum(len(r) for _, _, r, _ in orc.log)

@@ -1860,6 +1860,15 @@ __global__ __launch_bounds__(kBucketB) void k_bucket_scatter(BucketParams Q) {
   }
 }
 
+// window of received cross-partition commands (exchange receiving side): one command per entry
+__global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const zbhip_xpart_cmd x = xp[i];
+  const bool pms = x.kind == ZBHIP_CMD_PMS_CREATE || x.kind == ZBHIP_CMD_PMS_CORRELATE;
+  cmds[i] = make_uint4(pms ? x.instance : x.correlation_key, x.kind, i, 0);  // zbhip_command layout
+}
+
 // ---------------------------------------------------------------------------------------------
 // launch wrappers (host)
 // ---------------------------------------------------------------------------------------------
@@ -1925,6 +1934,11 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
   hipLaunchKernelGGL(k_key_scan_sums, dim3(1), dim3(1024), 0, s, K, nb);
   hipLaunchKernelGGL(k_key_apply, dim3(nb), dim3(kScanB), 0, s, K);
   hipLaunchKernelGGL(k_key_patch, dim3((n + 255) / 256), dim3(256), 0, s, K);
+  return hipGetLastError();
+}
+
+hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_xpart_window, dim3((n + 255) / 256), dim3(256), 0, s, xp, n, cmds);
   return hipGetLastError();
 }
 

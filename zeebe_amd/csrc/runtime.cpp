@@ -27,6 +27,7 @@ hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_r
 hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uint4* cmds, uint32_t n,
                           unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
                           zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s);
+hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s);
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
                          uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;  // regions for the extra workgroups of multi-round windows
@@ -165,6 +166,7 @@ struct zbhip_handle {
   unsigned long long* d_key_base = nullptr;
   unsigned long long* d_key_blk = nullptr;
   bool bucketed = false;
+  bool outbox_taken = false;  // zbhip_outbox_device already handed out the last run's outbox
   bool published = false;                      // a publish ran: MESSAGE_STATS row exists
   std::vector<uint4> h_hdr2;
   std::vector<int64_t> h_base;                 // key counter before each command's first key
@@ -739,6 +741,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     HIPCHK(launch_keyscan(h->d_cmd_hdr, h->d_cmd_hdr2, P.cmds, n, h->d_key_blk, h->d_key_base, h->d_key_counter,
                           h->d_xout, h->st, (long long)h->cfg.partition_id << 51, h->stream));
     h->bucketed = false;
+    h->outbox_taken = false;
     for (auto& c : h->h_cmds) h->published |= c.kind == ZBHIP_CMD_PUBLISH;
   }
   if (timed) HIPCHK(hipEventRecord(e1, h->stream));
@@ -1149,9 +1152,42 @@ int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32
                          h->d_xcount, h->d_xbucket, h->stream));
     h->bucketed = true;
   }
+  *dev_out = h->d_xbucket;
+  if (h->outbox_taken) {  // sent already: nothing new until the next run
+    memset(counts, 0, parts * sizeof(uint32_t));
+    return ZBHIP_OK;
+  }
   HIPCHK(hipMemcpyAsync(counts, h->d_xcount, parts * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  *dev_out = h->d_xbucket;
+  h->outbox_taken = true;
+  return ZBHIP_OK;
+}
+
+int zbhip_outbox_copy(zbhip_handle* h, void* dev_dst, size_t first, size_t count) {
+  if (!h || (count && !dev_dst)) return ZBHIP_EINVAL;
+  if (!h->msg() || !h->bucketed) return ZBHIP_ESTATE;
+  if (first + count > h->n_cmds * kOut) return ZBHIP_EINVAL;
+  if (count)
+    HIPCHK(hipMemcpyAsync(dev_dst, h->d_xbucket + first, count * sizeof(zbhip_xpart_cmd), hipMemcpyDeviceToDevice,
+                          h->stream));
+  return ZBHIP_OK;
+}
+
+int zbhip_submit_xparts_device(zbhip_handle* h, const zbhip_xpart_cmd* dev_xparts, size_t n) {
+  if (!h || (n && !dev_xparts)) return ZBHIP_EINVAL;
+  if (!h->msg()) return ZBHIP_EUNSUPP;
+  if (n > h->cfg.max_commands) return ZBHIP_ENOMEM;
+  HIPCHK(launch_xpart_window(dev_xparts, (uint32_t)n, h->d_cmds, h->stream));
+  return zbhip_submit_device_ex(h, reinterpret_cast<const zbhip_command*>(h->d_cmds), n, nullptr, 0, dev_xparts, n);
+}
+
+int zbhip_string_partitions(zbhip_handle* h, const uint32_t* ids, size_t n, int32_t partition_count, int32_t* out) {
+  if (!h || partition_count <= 0 || (n && (!ids || !out))) return ZBHIP_EINVAL;
+  for (size_t i = 0; i < n; ++i) {
+    if (ids[i] >= h->str_hash.size()) return ZBHIP_EINVAL;
+    const int32_t r = (int32_t)h->str_hash[ids[i]] % partition_count;
+    out[i] = (r < 0 ? -r : r) + 1;
+  }
   return ZBHIP_OK;
 }
 

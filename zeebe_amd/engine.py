@@ -142,6 +142,19 @@ class Partition:
             check(self.L.zbhip_outbox(self.h, out.ctypes.data, n.value, C.byref(n)), "zbhip_outbox")
         return out
 
+    def outbox_copy(self, dev_dst, first, count):
+        check(self.L.zbhip_outbox_copy(self.h, dev_dst, first, count), "zbhip_outbox_copy")
+
+    def submit_xparts_device(self, dev_xparts, n):
+        """The exchange's receiving side: a window of n received commands already in HBM."""
+        check(self.L.zbhip_submit_xparts_device(self.h, dev_xparts or None, n), "zbhip_submit_xparts_device")
+
+    def string_partitions(self, ids, partition_count):
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        out = np.zeros(len(ids), dtype=np.int32)
+        check(self.L.zbhip_string_partitions(self.h, ids.ctypes.data, len(ids), partition_count, out.ctypes.data))
+        return out
+
     def outbox_device(self):
         """(device pointer, per-target counts) of the outbox bucketed by target partition."""
         ptr = C.c_void_p()

@@ -47,6 +47,45 @@ def route(outboxes, partition_count):
     return [np.concatenate(x) if x else abi.make_xparts(0) for x in inbox]
 
 
+XPART_BYTES = abi.XPART_DTYPE.itemsize
+
+
+class LocalExchange:
+    """Several partitions hosted by one process on one GPU (all on one stream): every target's
+    inbox is the concatenation, in source-partition order, of the sources' device buckets for it,
+    assembled with device-to-device copies.  ``step()`` returns the inbox sizes; ``deliver()``
+    submits each non-empty inbox as the target's next window."""
+
+    def __init__(self, parts, max_entries, device):
+        import torch
+        self.parts = parts
+        self.inbox = [torch.empty(max_entries * XPART_BYTES, dtype=torch.uint8, device=device) for _ in parts]
+        self.sizes = [0] * len(parts)
+
+    def step(self):
+        P = len(self.parts)
+        buckets = [p.outbox_device()[1] for p in self.parts]
+        for t in range(P):
+            off = 0
+            for s_, counts in enumerate(buckets):
+                c = int(counts[t])
+                if c:
+                    first = int(counts[:t].sum())
+                    self.parts[s_].outbox_copy(self.inbox[t].data_ptr() + off * XPART_BYTES, first, c)
+                    off += c
+            self.sizes[t] = off
+        return list(self.sizes)
+
+    def deliver(self, flags=0):
+        ran = 0
+        for t, part in enumerate(self.parts):
+            if self.sizes[t]:
+                part.submit_xparts_device(self.inbox[t].data_ptr(), self.sizes[t])
+                part.run(flags)
+                ran += 1
+        return ran
+
+
 class DeviceExchange:
     """All-to-all of device-resident outboxes between the ranks of a process group (rank r =
     partition r + 1).  ``send`` takes the outbox as a uint8 device tensor already bucketed by
@@ -60,6 +99,23 @@ class DeviceExchange:
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
+
+    def exchange_partition(self, part, staging, flags=0):
+        """One exchange step for this rank's partition: send its device outbox, receive its inbox
+        (into ``staging``, a uint8 device tensor), submit and run it.  Returns (received, total
+        received over all ranks); every rank calls it the same number of times."""
+        import torch
+        ptr, counts = part.outbox_device()
+        n = int(counts.sum())
+        if n:
+            part.outbox_copy(staging.data_ptr(), 0, n)
+        inbox, got = self.send(staging, counts)
+        total = torch.tensor([got], dtype=torch.int64, device=staging.device)
+        self.dist.all_reduce(total, group=self.group)
+        if got:
+            part.submit_xparts_device(inbox.data_ptr(), got)
+            part.run(flags)
+        return got, int(total.item())
 
     def send(self, outbox_bytes, counts):
         import torch

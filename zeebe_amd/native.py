@@ -21,7 +21,8 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_pending_records", "zbhip_get_stats", "zbhip_export_state", "zbhip_fallback",
            "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info", "zbhip_command_status",
            "zbhip_submit_ex", "zbhip_submit_device_ex", "zbhip_intern_string", "zbhip_intern_strings",
-           "zbhip_string_value", "zbhip_subscription_partition", "zbhip_outbox", "zbhip_outbox_device"]
+           "zbhip_string_value", "zbhip_subscription_partition", "zbhip_outbox", "zbhip_outbox_device",
+           "zbhip_outbox_copy", "zbhip_submit_xparts_device", "zbhip_string_partitions"]
 
 
 class ZbhipError(RuntimeError):
@@ -78,6 +79,9 @@ def load():
     L.zbhip_subscription_partition.restype = C.c_int32
     L.zbhip_outbox.argtypes = [vp, vp, sz, C.POINTER(sz)]
     L.zbhip_outbox_device.argtypes = [vp, C.POINTER(vp), vp]
+    L.zbhip_outbox_copy.argtypes = [vp, vp, sz, sz]
+    L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
+    L.zbhip_string_partitions.argtypes = [vp, vp, sz, C.c_int32, vp]
     L.zbhip_build_info.argtypes = []
     L.zbhip_build_info.restype = C.c_char_p
     _lib = L
