@@ -46,12 +46,20 @@ namespace zb {
 // lane storing its own records at its prefix scatters each store over ~40 cache lines; a
 // binary search of the lane prefix per record was slower still; B = 64 / 256 and R = 8 / 32
 // were 2-10 % slower.)
-template <int B_, int T_, int Q_, int R_, bool M_ = false>
+template <int B_, int T_, int Q_, int R_, bool M_ = false, bool J_ = true, bool X_ = true, int W_ = 0>
 struct KCfg {
   static constexpr int B = B_, T = T_, Q = Q_, R = R_;
+  static constexpr int W = W_;   // waves per SIMD the register allocation targets (0 = compiler default)
   static constexpr bool M = M_;  // message correlation (catch events, subscription commands)
+  static constexpr bool J = J_;  // parallel-gateway join counters
+  static constexpr bool X = X_;  // exclusive gateways (FEEL condition evaluation)
 };
-using KSimple = KCfg<128, 4, 4, 16>;   // processes without parallel gateways / multi-outgoing nodes
+using KSimple = KCfg<128, 4, 4, 16, false, false>;  // no parallel gateways / multi-outgoing nodes: no join counters
+// Linear chains (every node <= 1 outgoing flow, no gateways, no catch events): at most two element
+// instances are alive in a batch, no FEEL evaluator, no join counters.  T = 2 and R = 15 keep the
+// workgroup at <= 20 KiB of LDS and the register target at 128 VGPRs, so 4 waves per SIMD are
+// resident (KSimple: 3).
+using KLinear = KCfg<128, 2, 4, 15, false, false, false, 4>;
 using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
 using KMsg = KCfg<128, 12, 16, 16, true>;  // partitions with message catch events (config 5)
 
@@ -906,6 +914,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         return;
       }
       case ZBHIP_EL_EXCLUSIVE_GATEWAY: {  // ExclusiveGatewayProcessor.onActivate (:47-66)
+        if constexpr (!K::X) { set_fail(L, FB_UNSUPPORTED); return; }
         uint32_t flow = find_sequence_flow(L, w, key);
         if (L.fail) return;
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
@@ -1054,7 +1063,7 @@ __device__ __forceinline__ void load_instance_mid(Lane<K>& L, uint32_t inst) {
       var_put(L, v, m.x, m.y, P.st.var_val[(size_t)v * N + inst]);
     }
   L.pb = L.prog + L.prog[1 + proc];
-  L.has_join = (L.pb[1] & 0xFFFF) != 0;
+  L.has_join = K::J && (L.pb[1] & 0xFFFF) != 0;
   if (L.has_join) {
     L.jw0 = P.st.join[inst];
     L.jw1 = P.st.join[(size_t)N + inst];
@@ -1312,7 +1321,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   }
   if (!L.fail && L.proc != NONE) {
     L.pb = prog + prog[1 + L.proc];
-    L.has_join = (L.pb[1] & 0xFFFF) != 0;
+    L.has_join = K::J && (L.pb[1] & 0xFFFF) != 0;
     if (L.has_join && kind != ZBHIP_CMD_CREATE) {
       L.jw0 = P.st.join[inst];
       L.jw1 = P.st.join[(size_t)N + inst];
@@ -1465,16 +1474,18 @@ __device__ unsigned long long g_stamps[8];
 // dependent load chain command -> instance rows overlaps the previous chunk's processing.
 // Chunk c's records are compacted by a wavefront scan into output region region_base + c.
 template <class K>
-__global__ __launch_bounds__(K::B) void k_step(StepParams P) {
+__global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::W : 1))) void k_step(StepParams P) {
   extern __shared__ __align__(16) uint32_t smem[];
   const uint32_t prog_words = (P.prog_words + 3) & ~3u;
   uint32_t* prog = smem;
   uint2* tbl_base = reinterpret_cast<uint2*>(smem + prog_words);
   uint2* stage_base = tbl_base + K::T * K::B;
   uint32_t* q_base = reinterpret_cast<uint32_t*>(stage_base + K::R * K::B);
-  uint32_t* pre = q_base + K::Q * K::B;  // [B] first output record of each lane in the chunk
-  uint8_t* own = reinterpret_cast<uint8_t*>(pre + K::B);  // [B * R] lane owning output record o
+  // the flush's prefix array and owner map alias the FIFO and the element table, idle by then
+  uint32_t* pre = q_base;                                   // [B] first output record of each lane
+  uint8_t* own = reinterpret_cast<uint8_t*>(tbl_base);      // [B * R] lane owning output record o
   static_assert(K::B <= 256, "owner map holds lane ids in bytes");
+  static_assert(K::T * 8 >= K::R && K::Q >= 1, "flush scratch fits the table / FIFO regions");
   __shared__ uint32_t wsum[2][K::B / 64];
   ZB_STAMP(t_start);
 #ifdef ZB_STAMPS
@@ -1551,15 +1562,28 @@ __global__ __launch_bounds__(K::B) void k_step(StepParams P) {
       pre[threadIdx.x] = my_off;
       for (uint32_t j = 0; j < my_nrec; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
       __syncthreads();
-      for (uint32_t o = 2 * threadIdx.x; o < total; o += 2 * K::B) {
-        const uint32_t l0 = own[o];
-        const uint2 r0 = stage_base[(o - pre[l0]) * K::B + l0];
-        if (o + 1 < total) {
-          const uint32_t l1 = own[o + 1];
-          const uint2 r1 = stage_base[(o + 1 - pre[l1]) * K::B + l1];
+      // four output records per thread and iteration: one 4-byte owner read, then four
+      // independent prefix reads and four independent row reads (no dependent LDS chain per
+      // record), two 16-byte stores
+      for (uint32_t o = 4 * threadIdx.x; o < total; o += 4 * K::B) {
+        const uint32_t ow = *reinterpret_cast<const uint32_t*>(own + o);
+        const uint32_t n4 = total - o;  // >= 1
+        const uint32_t l0 = ow & 0xFF;
+        const uint32_t l1 = n4 > 1 ? (ow >> 8) & 0xFF : l0;
+        const uint32_t l2 = n4 > 2 ? (ow >> 16) & 0xFF : l0;
+        const uint32_t l3 = n4 > 3 ? ow >> 24 : l0;
+        const uint32_t p0 = pre[l0], p1 = pre[l1], p2 = pre[l2], p3 = pre[l3];
+        const uint2 r0 = stage_base[(o - p0) * K::B + l0];
+        const uint2 r1 = stage_base[(n4 > 1 ? o + 1 - p1 : o - p0) * K::B + l1];
+        const uint2 r2 = stage_base[(n4 > 2 ? o + 2 - p2 : o - p0) * K::B + l2];
+        const uint2 r3 = stage_base[(n4 > 3 ? o + 3 - p3 : o - p0) * K::B + l3];
+        if (n4 >= 4) {
           *reinterpret_cast<uint4*>(out + o) = make_uint4(r0.x, r0.y, r1.x, r1.y);
+          *reinterpret_cast<uint4*>(out + o + 2) = make_uint4(r2.x, r2.y, r3.x, r3.y);
         } else {
           out[o] = r0;
+          if (n4 > 1) out[o + 1] = r1;
+          if (n4 > 2) out[o + 2] = r2;
         }
       }
       __syncthreads();  // the next chunk reuses the stage columns and the owner map
@@ -1875,8 +1899,7 @@ __global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp,
 template <class K>
 static size_t lds_bytes(uint32_t prog_words) {
   return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::T * K::B * sizeof(uint2) +
-         (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t) +
-         (size_t)K::B * sizeof(uint32_t) + (size_t)K::B * K::R;
+         (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -1916,11 +1939,16 @@ static hipError_t launch_k(const StepParams& P, hipStream_t s) {
   return hipGetLastError();
 }
 
-uint32_t step_block(int variant) { return variant == 2 ? KMsg::B : variant ? KGeneric::B : KSimple::B; }
+// variants: 0 KSimple, 1 KGeneric, 2 KMsg, 3 KLinear
+uint32_t step_block(int variant) {
+  return variant == 3 ? KLinear::B : variant == 2 ? KMsg::B : variant ? KGeneric::B : KSimple::B;
+}
 
 size_t step_lds_bytes(int variant, uint32_t prog_words) {
-  return variant == 2 ? lds_bytes<KMsg>(prog_words)
-                      : variant ? lds_bytes<KGeneric>(prog_words) : lds_bytes<KSimple>(prog_words);
+  return variant == 3   ? lds_bytes<KLinear>(prog_words)
+         : variant == 2 ? lds_bytes<KMsg>(prog_words)
+         : variant      ? lds_bytes<KGeneric>(prog_words)
+                        : lds_bytes<KSimple>(prog_words);
 }
 
 hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uint4* cmds, uint32_t n,
@@ -1966,7 +1994,12 @@ void dump_stamps() {
 
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
   if (P.n_launch == 0) return hipSuccess;
-  return variant == 2 ? launch_k<KMsg>(P, s) : variant ? launch_k<KGeneric>(P, s) : launch_k<KSimple>(P, s);
+  switch (variant) {
+    case 3: return launch_k<KLinear>(P, s);
+    case 2: return launch_k<KMsg>(P, s);
+    case 1: return launch_k<KGeneric>(P, s);
+    default: return launch_k<KSimple>(P, s);
+  }
 }
 
 hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,

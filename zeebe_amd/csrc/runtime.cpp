@@ -113,7 +113,7 @@ struct zbhip_handle {
   unsigned long long* d_stats = nullptr;     // [64][8] spread accumulators + [512] gather total
   uint32_t regions_cap = 0;
   size_t region_records = 0;
-  int variant = 0;                           // 0 = KSimple, 1 = KGeneric
+  int variant = 3;                           // kernel variant (zbhip_deploy): 3 KLinear, 0 KSimple, 1 KGeneric, 2 KMsg
   std::vector<std::pair<uint32_t, uint32_t>> launches;  // (region_base, first position in order) per launch
   std::vector<hipEvent_t> tev;               // timing events (pairs) since the last stats reset
   size_t tev_used = 0;
@@ -477,18 +477,26 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if (bn < 0) return ZBHIP_ENOMEM;
     P.bpmn_name = (uint16_t)bn;
   }
-  // kernel variant: one token per instance at a time (no parallel gateway, no multi-outgoing
-  // node other than an exclusive gateway) fits the small register/LDS configuration
-  bool generic = false;
+  // kernel variant, the smallest that covers every deployed process (kernels.hip KCfg):
+  //   3 KLinear  -- linear chains: every node <= 1 outgoing flow, no gateways (4 waves/SIMD)
+  //   0 KSimple  -- one token per instance (no parallel gateway / multi-outgoing node but an XOR)
+  //   1 KGeneric -- everything else in the subset
+  //   2 KMsg     -- message catch events and subscription commands (config 5)
+  int cls = 3;
   for (auto& e : P.els) {
-    if (e.element_type == ZBHIP_EL_PARALLEL_GATEWAY) generic = true;
+    if (e.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY && cls == 3) cls = 0;
+    if (e.element_type == ZBHIP_EL_PARALLEL_GATEWAY) cls = 1;
     if (e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.out_count > 1)
-      generic = true;
+      cls = 1;
   }
+  if (P.has_msg) cls = 2;
+  auto rank = [](int v) { return v == 3 ? 0 : v == 0 ? 1 : v == 1 ? 2 : 3; };
   const int old_variant = h->variant;
-  if (generic && h->variant < 1) h->variant = 1;
-  if (P.has_msg) h->variant = 2;  // KMsg: message catch events, subscription commands, key scan
-  if (const char* fv = getenv("ZBHIP_FORCE_VARIANT")) h->variant = std::max(h->variant == 2 ? 2 : 0, atoi(fv) ? 1 : 0);
+  if (h->procs.empty() || rank(cls) > rank(h->variant)) h->variant = cls;
+  if (const char* fv = getenv("ZBHIP_FORCE_VARIANT")) {  // experiments: never below what the processes need
+    const int f = atoi(fv);
+    if (rank(f) >= rank(h->variant)) h->variant = f;
+  }
   h->procs.push_back(std::move(P));
   int rc = rebuild_program(h);
   if (rc != ZBHIP_OK) {
