@@ -46,10 +46,12 @@ namespace zb {
 // lane storing its own records at its prefix scatters each store over ~40 cache lines; a
 // binary search of the lane prefix per record was slower still; B = 64 / 256 and R = 8 / 32
 // were 2-10 % slower.)
-template <int B_, int T_, int Q_, int R_, bool M_ = false, bool J_ = true, bool X_ = true, int W_ = 0>
+template <int B_, int T_, int Q_, int R_, bool M_ = false, bool J_ = true, bool X_ = true, int W_ = 0,
+          bool REG_ = false>
 struct KCfg {
   static constexpr int B = B_, T = T_, Q = Q_, R = R_;
   static constexpr int W = W_;   // waves per SIMD the register allocation targets (0 = compiler default)
+  static constexpr bool REG = REG_;  // element table and FIFO in registers (T == Q == 2), not LDS
   static constexpr bool M = M_;  // message correlation (catch events, subscription commands)
   static constexpr bool J = J_;  // parallel-gateway join counters
   static constexpr bool X = X_;  // exclusive gateways (FEEL condition evaluation)
@@ -58,8 +60,9 @@ using KSimple = KCfg<128, 4, 4, 16, false, false>;  // no parallel gateways / mu
 // Linear chains (every node <= 1 outgoing flow, no gateways, no catch events): at most two element
 // instances are alive in a batch, no FEEL evaluator, no join counters.  T = 2 and R = 15 keep the
 // workgroup at <= 20 KiB of LDS and the register target at 128 VGPRs, so 4 waves per SIMD are
-// resident (KSimple: 3).
-using KLinear = KCfg<128, 2, 4, 15, false, false, false, 4>;
+// resident (KSimple: 3).  The FIFO never holds more than one entry there and the table two, so both
+// live in registers: the batch logic issues no dependent LDS round trips, only the record stage.
+using KLinear = KCfg<128, 2, 2, 15, false, false, false, 4, true>;
 using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
 using KMsg = KCfg<128, 12, 16, 16, true>;  // partitions with message catch events (config 5)
 
@@ -98,6 +101,8 @@ struct Lane {
   long long vv0, vv1, vv2, vv3;
   uint32_t jw0, jw1, jw2, jw3;
   bool has_join;
+  uint2 r_t0, r_t1;         // K::REG: element table entries
+  uint32_t r_q0, r_q1;      // K::REG: FIFO entries
   // ---- message correlation (K::M only) ----
   uint32_t ci;              // window index of the command (outbox, key references)
   uint32_t inst;            // instance whose rows are loaded (kNoInst: none, a slot lane before a
@@ -193,6 +198,11 @@ __device__ __forceinline__ uint16_t new_key(Lane<K>& L) {
 template <class K>
 __device__ __forceinline__ void emit(Lane<K>& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
                                      uint32_t flags = 0) {
+#ifdef ZB_EXP_NOEMIT  // diagnostic build: records counted, never staged
+  ++L.nrec;
+  if (code >= ZBHIP_PI_SEQUENCE_FLOW_TAKEN && code <= ZBHIP_PI_ELEMENT_TERMINATED) ++L.transitions;
+  return;
+#endif
   if (L.nrec < L.rec_cap) {
     const uint2 r = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16) | (flags << 24));
     if (L.nrec < (uint32_t)K::R) L.stage[L.nrec * K::B] = r;
@@ -242,6 +252,41 @@ __device__ __forceinline__ long long ref_cmd(uint32_t ci, bool sec, uint32_t ord
   return -2 - (long long)(((unsigned long long)ci << 17) | ((unsigned long long)sec << 16) | ord);
 }
 
+// element table / FIFO storage: LDS columns, or registers for K::REG (branch-free selects keep
+// every field a plain SSA value, as for the variables)
+template <class K>
+__device__ __forceinline__ uint2 tget(const Lane<K>& L, int t) {
+  if constexpr (K::REG) {
+    static_assert(K::T == 2 && K::Q == 2, "register table / FIFO");
+    return t == 0 ? L.r_t0 : L.r_t1;
+  } else {
+    return L.tbl[t * K::B];
+  }
+}
+template <class K>
+__device__ __forceinline__ void tput(Lane<K>& L, int t, uint2 v) {
+  if constexpr (K::REG) {
+    L.r_t0.x = t == 0 ? v.x : L.r_t0.x; L.r_t0.y = t == 0 ? v.y : L.r_t0.y;
+    L.r_t1.x = t == 1 ? v.x : L.r_t1.x; L.r_t1.y = t == 1 ? v.y : L.r_t1.y;
+  } else {
+    L.tbl[t * K::B] = v;
+  }
+}
+template <class K>
+__device__ __forceinline__ uint32_t qget(const Lane<K>& L, int i) {
+  if constexpr (K::REG) return (i & 1) ? L.r_q1 : L.r_q0;
+  else return L.q[(i % K::Q) * K::B];
+}
+template <class K>
+__device__ __forceinline__ void qput(Lane<K>& L, int i, uint32_t v) {
+  if constexpr (K::REG) {
+    L.r_q0 = (i & 1) ? L.r_q0 : v;
+    L.r_q1 = (i & 1) ? v : L.r_q1;
+  } else {
+    L.q[(i % K::Q) * K::B] = v;
+  }
+}
+
 // queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | key << 16
 template <class K>
 __device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
@@ -250,7 +295,7 @@ __device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, b
   // otherwise the platform writes it to the log unprocessed -> outside the device subset.
   if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
   if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
-  L.q[(L.qt % K::Q) * K::B] = elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
+  qput(L, L.qt, elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16));
   ++L.qt;
 }
 
@@ -261,7 +306,7 @@ template <class K>
 __device__ __forceinline__ void push_local(Lane<K>& L, uint32_t kind) {
   if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
   if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
-  L.q[(L.qt % K::Q) * K::B] = LQ_BIT | kind;
+  qput(L, L.qt, LQ_BIT | kind);
   ++L.qt;
 }
 
@@ -269,7 +314,7 @@ __device__ __forceinline__ void push_local(Lane<K>& L, uint32_t kind) {
 template <class K>
 __device__ __forceinline__ int tbl_find(const Lane<K>& L, uint32_t key) {
   for (int t = 0; t < L.nt; ++t) {
-    uint2 e = L.tbl[t * K::B];
+    uint2 e = tget(L, t);
     if (e.x != 0xFFFFFFFFu && (e.x >> 16) == key) return t;
   }
   return -1;
@@ -277,7 +322,7 @@ __device__ __forceinline__ int tbl_find(const Lane<K>& L, uint32_t key) {
 template <class K>
 __device__ __forceinline__ int tbl_find_job(const Lane<K>& L, uint32_t job) {
   for (int t = 0; t < L.nt; ++t) {
-    uint2 e = L.tbl[t * K::B];
+    uint2 e = tget(L, t);
     if (e.x != 0xFFFFFFFFu && (e.y & 0xFFFF) == job && (e.y >> 24) & 1u) return t;
   }
   return -1;
@@ -286,18 +331,18 @@ template <class K>
 __device__ __forceinline__ void tbl_insert(Lane<K>& L, uint32_t elem, uint32_t key, uint32_t state) {
   int t = 0;
   for (; t < L.nt; ++t)
-    if (L.tbl[t * K::B].x == 0xFFFFFFFFu) break;
+    if (tget(L, t).x == 0xFFFFFFFFu) break;
   if (t == L.nt) {
     if (L.nt >= K::T) { set_fail(L, FB_TABLE); return; }
     ++L.nt;
   }
-  L.tbl[t * K::B] = make_uint2(elem | (key << 16), JOB_ZERO | (state << 16));
+  tput(L, t, make_uint2(elem | (key << 16), JOB_ZERO | (state << 16)));
 }
 template <class K>
 __device__ __forceinline__ void tbl_set_state(Lane<K>& L, int t, uint32_t state) {
-  uint2 e = L.tbl[t * K::B];
+  uint2 e = tget(L, t);
   e.y = (e.y & 0xFF00FFFFu) | (state << 16);
-  L.tbl[t * K::B] = e;
+  tput(L, t, e);
 }
 
 // Complete every outstanding vector-memory operation inside the branch that issued a conditional
@@ -499,7 +544,7 @@ __device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem
 template <class K>
 __device__ __forceinline__ void apply_completed_child(Lane<K>& L, int t, uint32_t key) {
   if (L.trig_key == key) L.trig_key = NONE;  // eventScopeInstanceState.deleteInstance (triggers)
-  L.tbl[t * K::B] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+  tput(L, t, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
   --L.pi_child;
 }
 
@@ -716,7 +761,7 @@ __device__ __forceinline__ void pms_correlate(Lane<K>& L, uint32_t eord, uint32_
   // no subscription / rejection -> MESSAGE_SUBSCRIPTION:REJECT (outside the subset)
   if (st == 0 || (L.pm_y & 0xFFFF) != eord || (elem_of(L, elem).z & 0xFFFF) != name) { set_fail(L, FB_MESSAGE); return; }
   const int t = tbl_find(L, eord);  // canTriggerElement: the catch event is ACTIVATED with its event scope
-  if (t < 0 || ((L.tbl[t * K::B].y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED) { set_fail(L, FB_MESSAGE); return; }
+  if (t < 0 || ((tget(L, t).y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED) { set_fail(L, FB_MESSAGE); return; }
   const uint32_t intr = (L.pm_x >> 14) & 1;
   emit_msg(L, C_PMS_CORRELATED, iref(L, L.pm_y >> 16), eik_p, pik_p, msg_p, corr, nb, part, intr, elem);
   L.pm_x = L.pm_y = L.pm_z = 0;  // ProcessMessageSubscriptionCorrelatedApplier: interrupting -> removed
@@ -906,9 +951,9 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       case ZBHIP_EL_SERVICE_TASK: {  // JobWorkerTaskProcessor.onActivate (:49-61)
         uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
         emit(L, C_JOB_CREATED, job, key, elem);
-        uint2 e = L.tbl[t * K::B];   // JobCreatedApplier: element instance jobKey
+        uint2 e = tget(L, t);   // JobCreatedApplier: element instance jobKey
         e.y = (job & 0xFFFF) | (e.y & 0x00FF0000u) | (1u << 24);
-        L.tbl[t * K::B] = e;
+        tput(L, t, e);
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
         return;
@@ -965,7 +1010,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   }
   const int t = tbl_find(L, cmd_key);
   if (t < 0) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
-  const uint32_t st = (L.tbl[t * K::B].y >> 16) & 0xFF;
+  const uint32_t st = (tget(L, t).y >> 16) & 0xFF;
   if (st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING) {
     reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_STATE, st);
     return;
@@ -1053,7 +1098,7 @@ __device__ __forceinline__ void load_instance_mid(Lane<K>& L, uint32_t inst) {
   L.pi_live = true;
   L.pi_child = h.z & 0xFFFF;
   L.pi_asf = h.z >> 16;
-  for (uint32_t sl = 0; sl < nslots; ++sl) L.tbl[sl * K::B] = P.st.slots[(size_t)sl * N + inst];
+  for (uint32_t sl = 0; sl < nslots; ++sl) tput(L, (int)sl, P.st.slots[(size_t)sl * N + inst]);
   L.nt = (int)nslots;
   L.nvars = (int)nvars;
 #pragma unroll
@@ -1202,6 +1247,8 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   Lane<K> L;
   L.tbl = tbl_base + threadIdx.x;
   L.q = q_base + threadIdx.x;
+  L.r_t0 = L.r_t1 = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+  L.r_q0 = L.r_q1 = 0;
   L.stage = stage_base + threadIdx.x;
   // overflow rows (j >= R) are wave-interleaved by command: each emit of a wave is one
   // coalesced 512-byte store
@@ -1285,10 +1332,10 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   } else if (L.proc != NONE) {
     // load the waiting instance: element-instance slots -> LDS table, variables, join counters
     if (nslots0 > (uint32_t)K::T) set_fail(L, FB_TABLE);
-    if (nslots0 > 0) L.tbl[0] = s0;
+    if (nslots0 > 0) tput(L, 0, s0);
     if (nslots0 > 1) {
       for (uint32_t s = 1; s < nslots0 && s < (uint32_t)K::T; ++s)
-        L.tbl[s * K::B] = P.st.slots[(size_t)s * N + inst];
+        tput(L, (int)s, P.st.slots[(size_t)s * N + inst]);
       vm_drain();
     }
     L.nt = (int)nslots0;
@@ -1351,13 +1398,13 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     if (t < 0) {
       emit(L, kRejectBit | C_JOB_COMPLETE, ref, NONE, NONE, ZBHIP_REASON_JOB_NOT_FOUND);
     } else {
-      uint2 e = L.tbl[t * K::B];
+      uint2 e = tget(L, t);
       const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
       emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
       // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
       e.y &= ~(1u << 24);
       if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
-      L.tbl[t * K::B] = e;
+      tput(L, t, e);
       if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) {  // afterAccept
         uint32_t pe = new_key(L);  // EventTriggerBehavior.triggeringProcessEvent
         emit(L, C_PE_TRIGGERING, pe, task_key, task_elem);
@@ -1374,7 +1421,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
 
   // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
   while (L.qh < L.qt && !L.fail) {
-    const uint32_t entry = L.q[(L.qh % K::Q) * K::B];
+    const uint32_t entry = qget(L, L.qh);
     ++L.qh;
     if constexpr (K::M) {
       if (entry & LQ_BIT) {
@@ -1391,7 +1438,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   uint32_t ns = 0;
   if (!L.fail && L.pi_live) {
     for (int t = 0; t < L.nt; ++t)
-      if (L.tbl[t * K::B].x != 0xFFFFFFFFu) ++ns;
+      if (tget(L, t).x != 0xFFFFFFFFu) ++ns;
     if (ns > (uint32_t)kSlots) set_fail(L, FB_SLOTS);
   }
   uint32_t winst = inst;
@@ -1405,7 +1452,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if (ok && L.pi_live && winst != kNoInst) {
     uint32_t s = 0;
     for (int t = 0; t < L.nt; ++t) {
-      uint2 e = L.tbl[t * K::B];
+      uint2 e = tget(L, t);
       if (e.x != 0xFFFFFFFFu) P.st.slots[(size_t)(s++) * N + winst] = e;
     }
 #pragma unroll
@@ -1479,13 +1526,14 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
   const uint32_t prog_words = (P.prog_words + 3) & ~3u;
   uint32_t* prog = smem;
   uint2* tbl_base = reinterpret_cast<uint2*>(smem + prog_words);
-  uint2* stage_base = tbl_base + K::T * K::B;
+  uint2* stage_base = tbl_base + (K::REG ? 0 : K::T * K::B);
   uint32_t* q_base = reinterpret_cast<uint32_t*>(stage_base + K::R * K::B);
   // the flush's prefix array and owner map alias the FIFO and the element table, idle by then
+  // (K::REG: table and FIFO are registers; the flush scratch follows the stage)
   uint32_t* pre = q_base;                                   // [B] first output record of each lane
-  uint8_t* own = reinterpret_cast<uint8_t*>(tbl_base);      // [B * R] lane owning output record o
+  uint8_t* own = K::REG ? reinterpret_cast<uint8_t*>(q_base + K::B) : reinterpret_cast<uint8_t*>(tbl_base);
   static_assert(K::B <= 256, "owner map holds lane ids in bytes");
-  static_assert(K::T * 8 >= K::R && K::Q >= 1, "flush scratch fits the table / FIFO regions");
+  static_assert(K::REG || (K::T * 8 >= K::R && K::Q >= 1), "flush scratch fits the table / FIFO regions");
   __shared__ uint32_t wsum[2][K::B / 64];
   ZB_STAMP(t_start);
 #ifdef ZB_STAMPS
@@ -1565,6 +1613,9 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
       // four output records per thread and iteration: one 4-byte owner read, then four
       // independent prefix reads and four independent row reads (no dependent LDS chain per
       // record), two 16-byte stores
+#ifdef ZB_EXP_NOFLUSH  // diagnostic build: records staged but never copied out
+      if (total == 0xFFFFFFFFu)
+#endif
       for (uint32_t o = 4 * threadIdx.x; o < total; o += 4 * K::B) {
         const uint32_t ow = *reinterpret_cast<const uint32_t*>(own + o);
         const uint32_t n4 = total - o;  // >= 1
@@ -1898,6 +1949,9 @@ __global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp,
 // ---------------------------------------------------------------------------------------------
 template <class K>
 static size_t lds_bytes(uint32_t prog_words) {
+  if (K::REG)  // program | stage | flush prefix array + owner map
+    return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::B * 4 +
+           (((size_t)K::B * K::R + 3) & ~(size_t)3);
   return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::T * K::B * sizeof(uint2) +
          (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t);
 }
