@@ -218,6 +218,15 @@ def run_msg(args, world, rank, local_rank, dist):
                      "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": alg / (dev_ms * 1e-3) / 1e9 / world / PEAK_HBM_GBPS,
                      "traffic": None, "algorithmic_bytes_per_instance": alg_per_inst, "device_ms_per_step": dev_ms},
     }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.oracle import bench_msg
+        th = args.cpu_threads
+        n_cpu = max(1000, args.cpu_instances // 6)
+        sec, ctr, ccomp = bench_msg(xml, th, n_cpu)
+        result["cpu_baseline"] = {"value": ctr / sec, "unit": "transitions/s", "cores": th, "kind": "port",
+                                  "completed_instances_per_s": ccomp / sec,
+                                  "sample": "%d partitions (1 per thread) x %d instances, cross-partition exchange "
+                                            "between phases on the calling thread, %.1f s" % (th, n_cpu, sec)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

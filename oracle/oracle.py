@@ -67,6 +67,8 @@ def lib():
         L.zbo_subscription_partition.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
         L.zbo_java_hash.restype = C.c_int32
         L.zbo_java_hash.argtypes = [C.c_char_p, C.c_size_t]
+        L.zbo_bench_msg.restype = C.c_double
+        L.zbo_bench_msg.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.zbo_bench.restype = C.c_double
         L.zbo_bench.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
@@ -180,6 +182,17 @@ def bench(xml, threads, n_instances, phases, with_amount=False, seed=0x5EED03):
         xml = xml.encode()
     t, c = C.c_uint64(), C.c_uint64()
     sec = lib().zbo_bench(xml, threads, n_instances, phases, 1 if with_amount else 0, seed, C.byref(t), C.byref(c))
+    if sec < 0:
+        raise OracleError("bench deploy failed")
+    return sec, t.value, c.value
+
+
+def bench_msg(xml, partitions, n_instances):
+    """CPU baseline of config 5: `partitions` partitions (one thread each), n instances each."""
+    if isinstance(xml, str):
+        xml = xml.encode()
+    t, c = C.c_uint64(), C.c_uint64()
+    sec = lib().zbo_bench_msg(xml, partitions, n_instances, C.byref(t), C.byref(c))
     if sec < 0:
         raise OracleError("bench deploy failed")
     return sec, t.value, c.value

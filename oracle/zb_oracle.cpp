@@ -630,6 +630,8 @@ class Oracle {
   // value dictionary (zbhip_intern_string)
   std::vector<std::string> strs;
   std::unordered_map<std::string, uint32_t> str_ids;
+  const std::vector<std::string>* shared_strs = nullptr;  // bench: one dictionary for all partitions
+  const std::string& str(uint32_t id) const { return shared_strs ? shared_strs->at(id) : strs.at(id); }
   uint32_t intern_string(const std::string& v) {
     auto it = str_ids.find(v);
     if (it != str_ids.end()) return it->second;
@@ -836,6 +838,7 @@ class Oracle {
   struct PmsRow { int64_t key; bool opened; MsgVal rec; };
   struct MsgSub { int64_t key; bool correlating; MsgVal rec; };
   std::map<std::pair<int64_t, int>, PmsRow> pms_;                        // [eik, name]
+  std::unordered_map<uint32_t, int> pms_inst_;                           // open subscriptions per instance slot
   std::map<std::pair<int64_t, int>, MsgSub> msub_;                       // [eik, name]
   std::set<std::tuple<int, uint32_t, int64_t>> msub_by_corr_;           // [name, corr, eik]
   bool msg_stats_ = false;                                               // messagesDeadlineCount row
@@ -1058,17 +1061,17 @@ class Oracle {
     m.bpmn = (uint16_t)intern(P(v.proc).bpmn_id);
     m.pik = v.piKey;
     m.eik = key;
-    m.partition = subscription_partition(strs.at(m.corr), partition_count_);
+    m.partition = subscription_partition(str(m.corr), partition_count_);
     m.interrupting = 1;  // intermediate catch events interrupt (ExecutableCatchEvent.java:36-38)
     m.proc = v.proc;
     m.elem = v.elem;
     m.inst = cur_instance_;
     m.eord = ord_of(cur_instance_, key);
-    for (auto& [k2, row] : pms_)
-      if (row.rec.inst == cur_instance_) throw Unsupported{"second open message subscription of an instance"};
+    if (pms_inst_[cur_instance_] > 0) throw Unsupported{"second open message subscription of an instance"};
     int64_t subKey = next_key();
     msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_CREATING, subKey, m);
     pms_[{key, (int)m.name}] = PmsRow{subKey, false, m};  // ProcessMessageSubscriptionCreatingApplier
+    ++pms_inst_[cur_instance_];
     send_command(m.partition, ZBHIP_CMD_MSG_SUB_CREATE, m);
   }
 
@@ -1160,7 +1163,10 @@ class Oracle {
     const int64_t subKey = it->second.key;
     const bool interrupting = it->second.rec.interrupting;
     msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_CORRELATED, subKey, m);
-    if (interrupting) pms_.erase(it);  // ProcessMessageSubscriptionCorrelatedApplier
+    if (interrupting) {  // ProcessMessageSubscriptionCorrelatedApplier
+      --pms_inst_[it->second.rec.inst];
+      pms_.erase(it);
+    }
     else throw Unsupported{"non-interrupting subscription"};
     // EventHandle.activateElement (processing/common/EventHandle.java:109-150)
     const ElementInstance inst = eit->second;
@@ -1539,8 +1545,9 @@ class Oracle {
         // IntermediateCatchEventProcessor.onComplete: applyOutputMappings, unsubscribeFromEvents
         // (CatchEventBehavior.unsubscribeFromMessageEvents visits the element's remaining process
         // message subscriptions: none after an interrupting correlation), transitionToCompleted
-        for (auto& [k2, row] : pms_)
-          if (k2.first == key) throw Unsupported{"unsubscribe (PROCESS_MESSAGE_SUBSCRIPTION:DELETING)"};
+        auto pit = pms_.lower_bound({key, INT32_MIN});
+        if (pit != pms_.end() && pit->first.first == key)
+          throw Unsupported{"unsubscribe (PROCESS_MESSAGE_SUBSCRIPTION:DELETING)"};
         complete_and_take(el, key, v, true);
         break;
       }
@@ -1957,6 +1964,96 @@ void zbo_counters(void* o, uint64_t* transitions, uint64_t* completed, uint64_t*
 // actor per partition), each processing `n_instances` CREATE commands and then `phases`
 // windows of JOB:COMPLETE (one per instance, completing the job created in the previous
 // phase).  Returns wall seconds of the processing loop; process compilation excluded.
+// CPU baseline of config 5: P partitions (one thread each) run the message-correlation protocol
+// on n instances each; the exchange between the phases (route by target partition, sources in
+// partition order) runs on the calling thread.  Returns wall seconds of processing + exchange.
+double zbo_bench_msg(const char* xml, int P, int n, uint64_t* transitions_out, uint64_t* completed_out) {
+  std::vector<std::string> dict;
+  dict.reserve((size_t)P * n);
+  for (int p = 1; p <= P; ++p)
+    for (int i = 0; i < n; ++i) dict.push_back("k-" + std::to_string(p) + "-" + std::to_string(i));
+  std::vector<std::unique_ptr<Oracle>> os;
+  for (int p = 1; p <= P; ++p) {
+    os.emplace_back(new Oracle(p, P, 100, 0));
+    if (os.back()->deploy(xml, 2251799813685249LL, 1) < 0) return -1.0;
+    os.back()->shared_strs = &dict;
+  }
+  const int var = os[0]->intern("key"), name = os[0]->intern("msg");
+  std::vector<std::vector<zbhip_command>> cmd(P), pub(P);
+  std::vector<std::vector<zbhip_doc_entry>> docs(P);
+  for (int p = 0; p < P; ++p)
+    for (int i = 0; i < n; ++i) {
+      zbhip_command c{};
+      c.instance = (uint32_t)i;
+      c.kind = ZBHIP_CMD_CREATE;
+      c.doc_count = 1;
+      c.doc_begin = (uint32_t)i;
+      cmd[p].push_back(c);
+      zbhip_doc_entry d{};
+      d.name_id = (uint32_t)var;
+      d.type = ZBHIP_DOC_STR;
+      d.value = (int64_t)p * n + i;
+      docs[p].push_back(d);
+    }
+  for (uint32_t id = 0; id < (uint32_t)dict.size(); ++id) {
+    zbhip_command c{};
+    c.instance = id;
+    c.kind = ZBHIP_CMD_PUBLISH;
+    c.ref = (uint16_t)name;
+    pub[subscription_partition(dict[id], P) - 1].push_back(c);
+  }
+  auto parallel = [&](auto fn) {
+    std::vector<std::thread> th;
+    for (int p = 0; p < P; ++p) th.emplace_back([&, p]() { fn(p); });
+    for (auto& t : th) t.join();
+  };
+  auto exchange = [&]() {
+    for (int round = 0; round < 8; ++round) {
+      std::vector<std::vector<zbhip_xpart_cmd>> inbox(P);
+      size_t total = 0;
+      for (int s = 0; s < P; ++s) {
+        for (auto& x : os[s]->outbox) inbox[x.target_partition - 1].push_back(x);
+        total += os[s]->outbox.size();
+        os[s]->outbox.clear();
+      }
+      if (!total) return;
+      parallel([&](int t) {
+        std::vector<zbhip_command> cs(inbox[t].size());
+        for (size_t i = 0; i < inbox[t].size(); ++i) {
+          const zbhip_xpart_cmd& x = inbox[t][i];
+          const bool pms = x.kind == ZBHIP_CMD_PMS_CREATE || x.kind == ZBHIP_CMD_PMS_CORRELATE;
+          cs[i] = zbhip_command{};
+          cs[i].instance = pms ? x.instance : x.correlation_key;
+          cs[i].kind = x.kind;
+          cs[i].doc_begin = (uint32_t)i;
+        }
+        os[t]->submit(cs.data(), cs.size(), nullptr, 0, inbox[t].data(), inbox[t].size());
+        os[t]->run();
+        os[t]->out.clear();
+      });
+    }
+  };
+  auto t0 = std::chrono::steady_clock::now();
+  parallel([&](int p) {
+    os[p]->submit(cmd[p].data(), cmd[p].size(), docs[p].data(), docs[p].size());
+    os[p]->run();
+    os[p]->out.clear();
+  });
+  exchange();
+  parallel([&](int p) {
+    os[p]->submit(pub[p].data(), pub[p].size(), nullptr, 0);
+    os[p]->run();
+    os[p]->out.clear();
+  });
+  exchange();
+  double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t tr = 0, cp = 0;
+  for (auto& o : os) { tr += o->transitions; cp += o->completed_instances; }
+  *transitions_out = tr;
+  *completed_out = cp;
+  return sec;
+}
+
 double zbo_bench(const char* xml, int threads, int n_instances, int phases, int var_name_kind,
                  uint64_t seed, uint64_t* transitions_out, uint64_t* completed_out) {
   std::vector<std::unique_ptr<Oracle>> os;
