@@ -1,0 +1,138 @@
+"""Random structured BPMN processes inside the executor's subset (the idea of the reference's
+test-util/.../bpmn/random generator: blocks of tasks, exclusive split/merge and parallel fork/join,
+nested).  Used to drive the GPU executor and the CPU oracle with the same inputs.
+
+Bounds keep every process inside the device limits (<= 8 waiting elements per instance, <= 16
+join counters, a default flow on every exclusive split so no incident is raised)."""
+from xml.sax.saxutils import escape, quoteattr
+
+BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
+ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
+
+
+class _Gen:
+    def __init__(self, rng, max_depth, max_blocks, messages):
+        self.rng = rng
+        self.max_depth = max_depth
+        self.max_blocks = max_blocks
+        self.messages = messages
+        self.nodes = []   # (kind, id, extra)
+        self.flows = []   # [id, src, tgt, condition or None]
+        self.defaults = {}
+        self.n = 0
+        self.join_slots = 0
+        self.catches = 0
+
+    def _id(self, kind):
+        self.n += 1
+        return "%s_%d" % (kind, self.n)
+
+    def node(self, kind, **extra):
+        nid = self._id(kind)
+        self.nodes.append((kind, nid, extra))
+        return nid
+
+    def flow(self, src, tgt, cond=None):
+        fid = self._id("flow")
+        self.flows.append([fid, src, tgt, cond])
+        return fid
+
+    def condition(self):
+        r = self.rng
+        a = int(r.integers(0, 1000))
+        kind = int(r.integers(0, 4))
+        if kind == 0:
+            return "= amount > %d" % a
+        if kind == 1:
+            return "= amount <= %d" % a
+        if kind == 2:
+            b = int(r.integers(a, 1001))
+            return "= amount >= %d and amount < %d" % (a, b)
+        return "= amount = %d or amount > %d" % (a, int(r.integers(500, 1000)))
+
+    def sequence(self, cur, depth, width):
+        for _ in range(int(self.rng.integers(0, self.max_blocks + 1))):
+            cur = self.block(cur, depth, width)
+        return cur
+
+    def block(self, cur, depth, width):
+        r = self.rng
+        choices = ["task", "task"]
+        if depth < self.max_depth:
+            choices += ["xor", "xor"]
+            if width * 2 <= 8 and self.join_slots + 3 <= 16:
+                choices.append("par")
+        if self.messages and self.catches < 1 and width == 1:
+            choices.append("catch")
+        c = choices[int(r.integers(0, len(choices)))]
+        if c == "task":
+            t = self.node("serviceTask", job_type="job%d" % int(r.integers(0, 3)))
+            self.flow(cur, t)
+            return t
+        if c == "catch":
+            self.catches += 1
+            e = self.node("intermediateCatchEvent")
+            self.flow(cur, e)
+            return e
+        if c == "xor":
+            split = self.node("exclusiveGateway")
+            self.flow(cur, split)
+            merge = self.node("exclusiveGateway")
+            k = int(r.integers(2, 4))
+            dflt = int(r.integers(0, k))
+            for b in range(k):
+                first = len(self.flows)
+                end = self.sequence(split, depth + 1, width)
+                if end == split:  # empty branch: direct flow to the merge
+                    fid = self.flow(split, merge, None if b == dflt else self.condition())
+                else:
+                    fid = self.flows[first][0]  # the branch's first flow leaves the split
+                    self.flows[first][3] = None if b == dflt else self.condition()
+                    self.flow(end, merge)
+                if b == dflt:
+                    self.defaults[split] = fid
+            return merge
+        fork = self.node("parallelGateway")
+        self.flow(cur, fork)
+        join = self.node("parallelGateway")
+        k = int(r.integers(2, 4)) if width * 3 <= 8 and self.join_slots + 3 <= 16 else 2
+        self.join_slots += k
+        for _ in range(k):
+            end = self.sequence(fork, depth + 1, width * k)
+            self.flow(end, join)
+        return join
+
+
+def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False):
+    g = _Gen(rng, max_depth, max_blocks, messages)
+    start = g.node("startEvent")
+    cur = g.sequence(start, 0, 1)
+    end = g.node("endEvent")
+    g.flow(cur, end)
+    out = ['<?xml version="1.0" encoding="UTF-8"?>',
+           '<definitions xmlns="%s" xmlns:zeebe="%s" id="d" targetNamespace="%s">' % (BPMN_NS, ZEEBE_NS, BPMN_NS),
+           '  <process id=%s isExecutable="true">' % quoteattr(process_id)]
+    for kind, nid, extra in g.nodes:
+        if kind == "serviceTask":
+            out.append('    <serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s/>'
+                       '</extensionElements></serviceTask>' % (quoteattr(nid), quoteattr(extra["job_type"])))
+        elif kind == "exclusiveGateway" and nid in g.defaults:
+            out.append('    <exclusiveGateway id=%s default=%s/>' % (quoteattr(nid), quoteattr(g.defaults[nid])))
+        elif kind == "intermediateCatchEvent":
+            out.append('    <intermediateCatchEvent id=%s><messageEventDefinition messageRef="msg_def"/>'
+                       '</intermediateCatchEvent>' % quoteattr(nid))
+        else:
+            out.append("    <%s id=%s/>" % (kind, quoteattr(nid)))
+    for fid, src, tgt, cond in g.flows:
+        attrs = "id=%s sourceRef=%s targetRef=%s" % (quoteattr(fid), quoteattr(src), quoteattr(tgt))
+        if cond is None:
+            out.append("    <sequenceFlow %s/>" % attrs)
+        else:
+            out.append("    <sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
+                       % (attrs, escape(cond)))
+    out.append("  </process>")
+    if messages:
+        out.append('  <message id="msg_def" name="msg"><extensionElements>'
+                   '<zeebe:subscription correlationKey="= key"/></extensionElements></message>')
+    out.append("</definitions>")
+    return "\n".join(out) + "\n"

@@ -89,3 +89,14 @@ def test_static_condition_is_rejected():
     xml = bpmn.xor_process().replace("= amount &gt; 1000", "amount &gt; 1000")
     with pytest.raises(ZbhipError):
         Compiled(xml)
+
+
+def test_random_processes_compile_like_the_oracle():
+    # tests/random_bpmn.py processes: the host compiler and the oracle agree on element indexing
+    from random_bpmn import random_process
+    for seed in range(30):
+        xml = random_process(np.random.default_rng(1000 + seed))
+        c = Compiled(xml)
+        o = Oracle()
+        assert o.deploy(xml) == 0
+        assert [c.id(i) for i in range(len(c.els))] == [o.element_id(0, i) for i in range(len(c.els))]
