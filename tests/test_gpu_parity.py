@@ -191,6 +191,45 @@ def test_mixed_window_rounds_and_rejections():
     assert part.state() == orc.state()
 
 
+def test_linear_segments_mixed_with_general_path():
+    """KLinear's deploy-time straight-line segments (kernels.hip fast_command) next to the general
+    path in the same chunks: CREATEs with and without a variable document, a start event that
+    leads straight into an end event, JOB:COMPLETEs with a document, stale job references
+    (NOT_FOUND rejections) next to canonical completions."""
+    rng = np.random.default_rng(0x5E6)
+    n = 300
+    part = Partition(max_instances=n, max_commands=2 * n, max_records_per_batch=64)
+    orc = Oracle()
+    lin = bpmn.linear_process(3)
+    short = bpmn.createExecutableProcess("short").startEvent("s").endEvent("e").done()
+    for i, xml in enumerate((lin, short)):
+        assert part.deploy(xml, 2251799813685249 + i) == orc.deploy(xml, 2251799813685249 + i) == i
+    name = part.intern("amount")
+    assert orc.intern("amount") == name
+    cmds = create_commands(n, 0)
+    cmds["ref"] = np.where(np.arange(n) % 7 == 6, 1, 0)
+    with_doc = np.arange(n) % 3 == 0
+    cmds["doc_count"] = with_doc
+    cmds["doc_begin"] = np.cumsum(with_doc) - with_doc
+    docs = amount_docs(rng.integers(0, 100, int(with_doc.sum())), name)
+    run_both(part, orc, cmds, docs)
+    assert part.state() == orc.state()
+    for phase in range(6):
+        c = open_job_completions(part)
+        if c is None:
+            break
+        m = len(c)
+        d = rng.random(m) < 0.3
+        c["doc_count"] = d
+        c["doc_begin"] = np.cumsum(d) - d
+        stale = c[rng.random(m) < 0.2].copy()   # the same job completed twice in one window
+        stale["doc_count"] = 0
+        both = np.concatenate([c, stale])
+        run_both(part, orc, both, amount_docs(rng.integers(0, 100, int(d.sum())), name))
+        assert part.state() == orc.state()
+    assert phase >= 3
+
+
 def test_missing_variable_falls_back_and_leaves_instance_untouched():
     xml = bpmn.xor_process()
     part = Partition(max_instances=8, max_commands=8)

@@ -45,7 +45,9 @@ namespace zb {
 // records contiguously with coalesced 16-byte writes.  (Measured alternatives, linear-10: every
 // lane storing its own records at its prefix scatters each store over ~40 cache lines; a
 // binary search of the lane prefix per record was slower still; B = 64 / 256 and R = 8 / 32
-// were 2-10 % slower.)
+// were 2-10 % slower; for the single-wave KLinear, compacting through registers (each lane reads
+// its column, then writes it at its prefix) spilled and was ~2 % slower, and an owner map of stage
+// indices (one dependent LDS level fewer) ~4 % slower.)
 template <int B_, int T_, int Q_, int R_, bool M_ = false, bool J_ = true, bool X_ = true, int W_ = 0,
           bool REG_ = false>
 struct KCfg {
@@ -350,6 +352,15 @@ __device__ __forceinline__ void tbl_set_state(Lane<K>& L, int t, uint32_t state)
 // is conservative at control-flow joins: without this it waits at the join on every path, and
 // that wait would also cover the next chunk's rows prefetched at the top of the chunk loop.
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// Retire: an empty asm reading the registers of a prefetch load.  The compiler's waitcnt pass
+// waits for a load at its first use; vmcnt retires in issue order, so a first use that falls
+// after stores (the next iteration's top, after the flush) would also wait for every store ack.
+// Consuming the registers at a chosen point, before any store, moves that wait there.  (The
+// preheader loads are consumed before the loop for the same reason: the loop header merges the
+// preheader's pending loads with the back edge's pending stores.)
+__device__ __forceinline__ void consume(uint32_t v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void consume(uint2 v) { asm volatile("" ::"v"(v.x), "v"(v.y)); }
+__device__ __forceinline__ void consume(uint4 v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
 
 // ---- variables (registers) ------------------------------------------------------------------
 template <class K>
@@ -1042,6 +1053,114 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   take_outgoing(L, w);
 }
 
+// ---- straight-line segments of linear chains (K::REG) --------------------------------------
+// The arena's segment word of a start event or service task (runtime.cpp rebuild_program) says
+// that leaving it is deterministic: one unconditional outgoing flow `f` into a service task or a
+// none end event `n` without outgoing flows.  From the canonical waiting state (the scope
+// ACTIVATED with that one child) the whole batch of a JOB:COMPLETE -- and of a CREATE whose start
+// event leads into a task -- is then a fixed record sequence: exactly what the general path
+// (JobCompleteProcessor, the FIFO over BpmnStreamProcessor, ProcessProcessor, the appliers)
+// emits, written here with static stage rows and no FIFO, element table or guard dispatch.  Any
+// other state, a variable document, a tight batch limit or record capacity takes the general path.
+constexpr uint32_t SEG_VALID = 1u << 31, SEG_FROM_TASK = 1u << 30, SEG_TO_END = 1u << 24;
+
+template <class K>
+__device__ __forceinline__ void put(Lane<K>& L, int j, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem) {
+  L.stage[j * K::B] = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16));
+}
+
+// records of the segment tail from the flow's SFT on (row j0 onwards), keys from ordinal k;
+// ProcessInstanceSequenceFlowTakenApplier, then ACTIVATE_ELEMENT(n) processed as in process_pi
+template <class K>
+__device__ __forceinline__ void seg_enter(Lane<K>& L, int j0, uint32_t sg, uint32_t k) {
+  const uint32_t f = sg & 0xFFF, n = (sg >> 12) & 0xFFF;
+  put(L, j0, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, k, 0, f);
+  put(L, j0 + 1, ZBHIP_PI_ACTIVATE_ELEMENT, k + 1, 0, n);
+  put(L, j0 + 2, ZBHIP_PI_ELEMENT_ACTIVATING, k + 1, 0, n);
+}
+
+template <class K>
+__device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t ref, uint32_t doc_count) {
+  if (L.fail || L.proc == NONE || doc_count != 0 || L.limit <= 4 || L.rec_cap < 16 || L.next_ord >= 0xFFE0)
+    return false;
+  const uint32_t* seg = L.pb + L.pb[6];
+  if (kind == ZBHIP_CMD_JOB_COMPLETE) {
+    if (!(L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED && L.nt == 1 && L.pi_child == 1 && L.pi_asf == 0))
+      return false;
+    const uint2 e = L.r_t0;
+    if (e.x == 0xFFFFFFFFu || (e.y & 0xFFFF) != ref || !((e.y >> 24) & 1u) ||
+        ((e.y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED)
+      return false;
+    const uint32_t te = e.x & 0xFFFF, tk = e.x >> 16;
+    const uint32_t sg = seg[te];
+    if ((sg & (SEG_VALID | SEG_FROM_TASK)) != (SEG_VALID | SEG_FROM_TASK)) return false;
+    const uint32_t k = L.next_ord, n = (sg >> 12) & 0xFFF;
+    // JobCompleteProcessor + EventTriggerBehavior.triggeringProcessEvent, then COMPLETE_ELEMENT(task)
+    put(L, 0, C_JOB_COMPLETED, ref, tk, te);
+    put(L, 1, C_PE_TRIGGERING, k, tk, te);
+    put(L, 2, ZBHIP_PI_COMPLETE_ELEMENT, tk, 0, te);
+    put(L, 3, ZBHIP_PI_ELEMENT_COMPLETING, tk, 0, te);
+    put(L, 4, ZBHIP_PI_ELEMENT_COMPLETED, tk, 0, te);
+    seg_enter(L, 5, sg, k + 1);
+    if (!(sg & SEG_TO_END)) {  // JobWorkerTaskProcessor.onActivate: the next wait state
+      put(L, 8, C_JOB_CREATED, k + 3, k + 2, n);
+      put(L, 9, ZBHIP_PI_ELEMENT_ACTIVATED, k + 2, 0, n);
+      L.r_t0 = make_uint2(n | ((k + 2) << 16), ((k + 3) & 0xFFFF) | (ZBHIP_PI_ELEMENT_ACTIVATED << 16) | (1u << 24));
+      L.next_ord = (uint16_t)(k + 4);
+      L.nrec = 10;
+      L.transitions = 5;
+    } else {  // NoneEndEventBehavior, end of the path -> ProcessProcessor.onComplete
+      put(L, 8, ZBHIP_PI_ELEMENT_ACTIVATED, k + 2, 0, n);
+      put(L, 9, ZBHIP_PI_ELEMENT_COMPLETING, k + 2, 0, n);
+      put(L, 10, ZBHIP_PI_ELEMENT_COMPLETED, k + 2, 0, n);
+      put(L, 11, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0);
+      put(L, 12, ZBHIP_PI_ELEMENT_COMPLETING, 0, NONE, 0);
+      put(L, 13, ZBHIP_PI_ELEMENT_COMPLETED, 0, NONE, 0);
+      L.r_t0 = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+      L.next_ord = (uint16_t)(k + 3);
+      L.pi_child = 0;
+      L.pi_live = false;
+      L.pi_state = ZBHIP_PI_ELEMENT_COMPLETING;
+      L.nvars = 0;
+      L.nrec = 14;
+      L.transitions = 9;
+      L.completed = 1;
+    }
+    return true;
+  }
+  if (kind == ZBHIP_CMD_CREATE) {  // CreateProcessInstanceProcessor, ProcessProcessor, StartEventProcessor
+    const uint32_t start = L.pb[0] >> 16;
+    if (start == NONE) return false;
+    const uint32_t sg = seg[start];
+    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END)) != SEG_VALID) return false;
+    const uint32_t n = (sg >> 12) & 0xFFF;
+    put(L, 0, ZBHIP_PI_ACTIVATE_ELEMENT, 0, NONE, 0);
+    put(L, 1, C_PIC_CREATED, 1, 0, 0);
+    put(L, 2, ZBHIP_PI_ELEMENT_ACTIVATING, 0, NONE, 0);
+    put(L, 3, ZBHIP_PI_ELEMENT_ACTIVATED, 0, NONE, 0);
+    put(L, 4, ZBHIP_PI_ACTIVATE_ELEMENT, NONE, 0, start);
+    put(L, 5, ZBHIP_PI_ELEMENT_ACTIVATING, 2, 0, start);
+    put(L, 6, ZBHIP_PI_ELEMENT_ACTIVATED, 2, 0, start);
+    put(L, 7, ZBHIP_PI_COMPLETE_ELEMENT, 2, 0, start);
+    put(L, 8, ZBHIP_PI_ELEMENT_COMPLETING, 2, 0, start);
+    put(L, 9, ZBHIP_PI_ELEMENT_COMPLETED, 2, 0, start);
+    seg_enter(L, 10, sg, 3);
+    put(L, 13, C_JOB_CREATED, 5, 4, n);
+    put(L, 14, ZBHIP_PI_ELEMENT_ACTIVATED, 4, 0, n);
+    L.r_t0 = make_uint2(n | (4u << 16), 5u | (ZBHIP_PI_ELEMENT_ACTIVATED << 16) | (1u << 24));
+    L.nt = 1;
+    L.next_ord = 6;
+    L.pi_live = true;
+    L.pi_state = ZBHIP_PI_ELEMENT_ACTIVATED;
+    L.pi_child = 1;
+    L.pi_asf = 0;
+    L.nrec = 15;
+    L.transitions = 9;
+    return true;
+  }
+  return false;
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_step
 // ---------------------------------------------------------------------------------------------
@@ -1233,10 +1352,10 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
 }
 
 // One command's whole batch on one lane; returns the number of records it staged.
-template <class K>
+template <class K, class Retire>
 __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint32_t* prog, uint2* tbl_base,
                                                 uint2* stage_base, uint32_t* q_base, uint32_t ci, uint4 cw,
-                                                uint4 h, uint2 s0, Counters& acc) {
+                                                uint4 h, uint2 s0, Counters& acc, const Retire& retire) {
   const uint32_t inst = cw.x;
   const uint32_t kind = cw.y & 0xFF;
   const uint32_t doc_count = (cw.y >> 8) & 0xFF;
@@ -1378,7 +1497,12 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     }
   }
 
-  if (!L.fail && kind == ZBHIP_CMD_CREATE) {
+  // deploy-time compiled straight-line segments (linear chains): the batch is emitted without
+  // the FIFO; anything outside the canonical states takes the general path below
+  bool fast = false;
+  if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
+  if (fast) {
+  } else if (!L.fail && kind == ZBHIP_CMD_CREATE) {
     if ((L.pb[0] >> 16) == NONE) set_fail(L, FB_BAD_PROCESS);
     uint32_t pi = new_key(L);  // = ordinal 0
     // setVariablesFromDocument -> VariableBehavior.mergeLocalDocument (:60-82)
@@ -1420,7 +1544,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.processed = 1;
 
   // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
-  while (L.qh < L.qt && !L.fail) {
+  while (!fast && L.qh < L.qt && !L.fail) {
     const uint32_t entry = qget(L, L.qh);
     ++L.qh;
     if constexpr (K::M) {
@@ -1434,6 +1558,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     ++L.processed;
   }
 
+  retire();  // the caller's prefetch loads: retired before the first store of the commit
   // ---- commit: write back the instance (or leave it untouched on fallback) ----
   uint32_t ns = 0;
   if (!L.fail && L.pi_live) {
@@ -1556,6 +1681,7 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
   uint32_t ci2 = cmd_index<K>(P, c + G);
   uint4 cw2 = load_cmd(P, ci2);
   uint32_t ci3 = cmd_index<K>(P, c + 2 * G);
+  consume(ci1); consume(cw1); consume(h1); consume(s1); consume(cw2); consume(ci3);
 #ifdef ZB_STAMPS
   { const uint32_t u = __builtin_amdgcn_readfirstlane(cw1.x + h1.x + s1.x);
     ZB_STAMP(t_pro); acc_t[5] += t_pro - t_start + (u == 0x12345678u); }
@@ -1576,7 +1702,12 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
     ZB_STAMP(t1);
 
     uint32_t my_nrec = 0;
-    if (ci != kNoCmd) my_nrec = run_command<K>(P, prog, tbl_base, stage_base, q_base, ci, cw, h, s0, acc);
+    // The prefetch loads just issued are retired inside run_command, right before its commit stores
+    // (see Retire): by then they have had the whole batch logic to arrive, and no store is ahead of
+    // them in the vmcnt queue.
+    const auto retire = [&]() { consume(h1); consume(s1); consume(cw2); consume(ci3); };
+    if (ci != kNoCmd) my_nrec = run_command<K>(P, prog, tbl_base, stage_base, q_base, ci, cw, h, s0, acc, retire);
+    else retire();
     ZB_STAMP(t2);
 
     // ---- wavefront scan compaction: the chunk's records go out contiguously, once ----

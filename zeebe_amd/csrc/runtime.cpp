@@ -378,7 +378,8 @@ static int rebuild_program(zbhip_handle* h) {
     const uint32_t cond_off = out_off + ((uint32_t)P.out.size() + 1) / 2;
     const uint32_t n_cond = P.cond_begin.empty() ? 0 : (uint32_t)P.cond_begin.size() - 1;
     const uint32_t code_off = (cond_off + n_cond + 3) & ~3u;  // 16-byte aligned instructions (uint4 loads)
-    const uint32_t total = (code_off + 4 * (uint32_t)P.code.size() + 3) & ~3u;
+    const uint32_t seg_off = code_off + 4 * (uint32_t)P.code.size();
+    const uint32_t total = (seg_off + n_el + 3) & ~3u;
     prog.resize(base + total, 0);
     uint32_t* pb = prog.data() + base;
     pb[0] = n_el | ((uint32_t)P.none_start << 16);
@@ -387,6 +388,27 @@ static int rebuild_program(zbhip_handle* h) {
     pb[3] = cond_off;
     pb[4] = code_off;
     pb[5] = P.bpmn_name;  // name id of the bpmnProcessId (message records)
+    pb[6] = seg_off;
+    // straight-line segment words (kernels.hip fast_command): a start event or service task with
+    // one unconditional outgoing flow into a service task or a none end event without outgoing flows
+    for (uint32_t e = 0; e < n_el; ++e) {
+      const zbhip_element& E = P.els[e];
+      uint32_t sg = 0;
+      if ((E.element_type == ZBHIP_EL_START_EVENT || E.element_type == ZBHIP_EL_SERVICE_TASK) && E.out_count == 1) {
+        const uint32_t f = P.out[E.out_begin];
+        const zbhip_element& F = P.els[f];
+        const uint32_t n = F.flow_target;
+        if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.condition == ZBHIP_NONE16 && n < n_el && f < 0xFFF && n < 0xFFF) {
+          const zbhip_element& N = P.els[n];
+          const bool task = N.element_type == ZBHIP_EL_SERVICE_TASK;
+          const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
+          if (task || end)
+            sg = (1u << 31) | (E.element_type == ZBHIP_EL_SERVICE_TASK ? 1u << 30 : 0u) | (end ? 1u << 24 : 0u) |
+                 (n << 12) | f;
+        }
+      }
+      pb[seg_off + e] = sg;
+    }
     for (uint32_t e = 0; e < n_el; ++e) {
       const zbhip_element& E = P.els[e];
       uint32_t* w = pb + 8 + 4 * e;

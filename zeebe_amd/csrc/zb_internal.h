@@ -89,7 +89,8 @@ enum : uint8_t {
 // process block p:
 //   p[0] = n_elements | none_start << 16
 //   p[1] = n_join_slots | n_conditions << 16
-//   p[2] = out_off, p[3] = cond_off, p[4] = code_off (words, relative to p), p[5..7] = 0
+//   p[2] = out_off, p[3] = cond_off, p[4] = code_off (words, relative to p), p[5] = bpmnProcessId
+//   name id, p[6] = seg_off, p[7] = 0
 //   p[8 + 4e .. ] element e: w0 = type | event << 8 | in_count << 16
 //                            w1 = out_begin | out_count << 16
 //                            w2 = flow: target | condition << 16; xgw: default_flow; task: job_type | retries << 16
@@ -97,6 +98,8 @@ enum : uint8_t {
 //   p[out_off]  u16 outgoing flows (two per word)
 //   p[cond_off] u32 first instruction of each condition
 //   p[code_off] instructions (16-byte aligned): op, arg, literal_lo, literal_hi
+//   p[seg_off]  u32 straight-line segment word per element (kernels.hip fast_command):
+//               valid << 31 | from_task << 30 | to_end << 24 | target << 12 | flow, or 0
 struct DevState {
   uint4* hdr;        // [n] x = proc | next_ord << 16; y = pi_state | nslots << 8 | nvars << 16 | pi_live << 24
                      //     z = pi_child | pi_asf << 16; w = 0
