@@ -426,6 +426,46 @@ enum zbhip_reason {
 /* Rejection reason text exactly as the reference writes it. */
 int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, size_t cap);
 
+/* ---- log serialisation --------------------------------------------------
+ * Drained records -> the bytes the reference's log stream holds for them: per source command one
+ * sequenced batch (SequencedBatchSerializer.java:33-67) of 8-aligned entries, each = dispatcher
+ * frame (DataFrameDescriptor.java, 12 bytes) + LogEntryDescriptor header (40 bytes: flags with
+ * skipProcessing for processed follow-up commands, position, sourcePosition, key, timestamp,
+ * metadata length) + SBE RecordMetadata (protocol.xml:137-152, schema version 4) + msgpack record
+ * value (ObjectValue.java:78-84; ProcessInstanceRecord, JobRecord, VariableRecord,
+ * ProcessEventRecord, ProcessInstanceCreationRecord).  Host code (no device work).
+ * A serializer holds the deployment's constant msgpack runs and the name / value dictionaries; a
+ * handle owns one kept in step with zbhip_deploy / zbhip_intern / zbhip_intern_string
+ * (zbhip_handle_serializer), a standalone one is built with the same calls in the same order. */
+typedef struct zbhip_serializer zbhip_serializer;
+int zbhip_serializer_new(zbhip_serializer** out);
+void zbhip_serializer_free(zbhip_serializer* s);
+int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, uint32_t* process_idx_out);
+int zbhip_serializer_intern(zbhip_serializer* s, const char* name);
+int64_t zbhip_serializer_intern_string(zbhip_serializer* s, const char* bytes, size_t len);
+/* RecordMetadata.brokerVersion written into every entry (default 8.4.0, the reference build). */
+int zbhip_serializer_set_broker_version(zbhip_serializer* s, int32_t major, int32_t minor, int32_t patch);
+int zbhip_serializer_rejection_reason(zbhip_serializer* s, const zbhip_record* rec, char* buf, size_t cap);
+zbhip_serializer* zbhip_handle_serializer(zbhip_handle* h);
+
+/* The window the records were drained from, and the log positions of its batches. */
+typedef struct zbhip_log_window {
+  const zbhip_command* cmds;       /* the submitted window (record.source_index - source_base) */
+  size_t n_cmds;
+  int64_t source_base;             /* source_index of cmds[0] */
+  const zbhip_doc_entry* docs;     /* its document entries (record.aux - doc_base for VARIABLE) */
+  size_t n_docs;
+  int64_t doc_base;
+  const int64_t* source_positions; /* log position of each command of the window (sourcePosition) */
+  int64_t first_position;          /* position of the first serialised record (the sequencer's next) */
+  int64_t timestamp;               /* the batches' timestamp (ms) */
+} zbhip_log_window;
+
+/* Serialises n drained records (in drain order) into out.  *used = bytes needed; ZBHIP_ENOMEM if
+ * cap is short (out == NULL: size query).  Message records: ZBHIP_EUNSUPP. */
+int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n, const zbhip_log_window* w,
+                        uint8_t* out, size_t cap, size_t* used);
+
 /* Library build information ("gfx950 …"). */
 const char* zbhip_build_info(void);
 

@@ -37,6 +37,16 @@ def lib():
         L.zbo_deploy_xml.argtypes = [C.c_void_p, C.c_char_p, C.c_int64, C.c_int]
         L.zbo_intern.argtypes = [C.c_void_p, C.c_char_p]
         L.zbo_name.restype = C.c_char_p
+        L.zbo_element_job_type.restype = C.c_char_p
+        L.zbo_element_job_type.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.zbo_process_info.restype = C.c_char_p
+        L.zbo_process_info.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.zbo_element_info.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.zbo_n_names.argtypes = [C.c_void_p]
+        L.zbo_n_strings.argtypes = [C.c_void_p]
+        L.zbo_string_value.restype = C.c_void_p
+        L.zbo_string_value.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]
+        L.zbo_n_processes.argtypes = [C.c_void_p]
         L.zbo_name.argtypes = [C.c_void_p, C.c_int]
         L.zbo_n_elements.argtypes = [C.c_void_p, C.c_int]
         L.zbo_element_id.restype = C.c_char_p
@@ -111,6 +121,33 @@ class Oracle:
 
     def element_id(self, proc, elem):
         return self.L.zbo_element_id(self.h, proc, elem).decode()
+
+    def string_value(self, sid):
+        n = C.c_size_t()
+        p = self.L.zbo_string_value(self.h, sid, C.byref(n))
+        return C.string_at(p, n.value)
+
+    def strings(self):
+        return [self.string_value(i) for i in range(self.L.zbo_n_strings(self.h))]
+
+    def names(self):
+        return [self.name(i) for i in range(self.L.zbo_n_names(self.h))]
+
+    def process_tables(self):
+        """Deployment tables for oracle/logserial.py: per process bpmn_process_id, version, key and
+        elements (type, event_type, id, job_type, retries)."""
+        out = []
+        for p in range(self.L.zbo_n_processes(self.h)):
+            key, ver = C.c_int64(), C.c_int()
+            bid = self.L.zbo_process_info(self.h, p, C.byref(key), C.byref(ver)).decode()
+            els = []
+            for e in range(self.L.zbo_n_elements(self.h, p)):
+                t, ev, r = C.c_int(), C.c_int(), C.c_int()
+                self.L.zbo_element_info(self.h, p, e, C.byref(t), C.byref(ev), C.byref(r))
+                els.append((t.value, ev.value, self.element_id(p, e),
+                            self.L.zbo_element_job_type(self.h, p, e).decode(), r.value))
+            out.append({"bpmn_process_id": bid, "version": ver.value, "key": key.value, "elements": els})
+        return out
 
     def submit(self, cmds, docs=None, xparts=None):
         cmds = np.ascontiguousarray(cmds, dtype=abi.COMMAND_DTYPE)

@@ -1901,6 +1901,32 @@ const char* zbo_element_id(void* o, int proc, int elem) {
   return static_cast<Oracle*>(o)->procs.at(proc).els.at(elem).id.c_str();
 }
 
+// deployment tables for the log-serialisation checker (oracle/logserial.py)
+int zbo_element_info(void* o, int proc, int elem, int* type, int* event, int* retries) {
+  const OEl& e = static_cast<Oracle*>(o)->procs.at(proc).els.at(elem);
+  *type = e.type;
+  *event = e.event;
+  *retries = e.retries;
+  return 0;
+}
+const char* zbo_element_job_type(void* o, int proc, int elem) {
+  return static_cast<Oracle*>(o)->procs.at(proc).els.at(elem).job_type.c_str();
+}
+const char* zbo_process_info(void* o, int proc, int64_t* def_key, int* version) {
+  const OProc& P = static_cast<Oracle*>(o)->procs.at(proc);
+  *def_key = P.def_key;
+  *version = P.version;
+  return P.bpmn_id.c_str();
+}
+const char* zbo_string_value(void* o, int id, size_t* len) {
+  const std::string& v = static_cast<Oracle*>(o)->str((uint32_t)id);
+  *len = v.size();
+  return v.data();
+}
+int zbo_n_strings(void* o) { return (int)static_cast<Oracle*>(o)->strs.size(); }
+int zbo_n_names(void* o) { return (int)static_cast<Oracle*>(o)->names.size(); }
+int zbo_n_processes(void* o) { return (int)static_cast<Oracle*>(o)->procs.size(); }
+
 int zbo_submit(void* o, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs, size_t nd) {
   static_cast<Oracle*>(o)->submit(cmds, n, docs, nd);
   return 0;

@@ -1,0 +1,242 @@
+"""Log serialisation: the oracle restatement (oracle/logserial.py) against the
+reference's golden vectors, and the product serializer (libzbhip.so zbhip_serialize_log, host code,
+runs here without a GPU) against the oracle, byte for byte, on the CPU engine's records of every
+BASELINE workload at small sizes.  The msgpack library (an independent implementation) decodes
+the values for the golden comparisons."""
+import json
+import os
+import struct
+
+import msgpack
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, amount_docs, complete_commands, create_commands, process_xml
+from oracle import logserial as LS
+from oracle.oracle import Oracle
+from zeebe_amd import abi, bpmn
+from zeebe_amd.logwriter import LogSerializer, split_entries
+
+
+# ---- the oracle against the reference's vectors --------------------------------------------------
+def test_msgpack_writer_golden_vectors():
+    d = json.load(open(os.path.join(GOLDEN, "msgpack_writer.json")))
+    for name, op, arg, want in d["vectors"]:
+        w = LS.MsgPackWriter()
+        if op == "binary":
+            w.binary(arg.encode())
+        elif arg is None:
+            getattr(w, op)()
+        else:
+            getattr(w, op)(arg)
+        assert bytes(w.b).hex() == want, name
+
+
+def _pack_inputs(v):
+    if isinstance(v, dict) and "__msgpack__" in v:
+        return msgpack.packb(v["__msgpack__"])
+    if isinstance(v, list):
+        return [_pack_inputs(x) for x in v]
+    return v
+
+
+def test_record_values_match_reference_json():
+    d = json.load(open(os.path.join(GOLDEN, "record_json.json")))
+    for case in d["cases"]:
+        schema = getattr(LS, case["schema"])
+        values = {k: _pack_inputs(v) for k, v in case["values"].items()}
+        raw = LS.write_object(schema, values)
+        got = msgpack.unpackb(raw, raw=False)
+        assert list(got) == [p[0] for p in schema], case["name"]  # declaration order
+        kinds = {p[0]: p[1] for p in schema}
+        for k, want in case["expected"].items():
+            v = got[k]
+            if kinds[k] == "bin":
+                v = msgpack.unpackb(v, raw=False)
+            if isinstance(want, str) and not isinstance(v, str):
+                v = json.dumps(v)  # VariableRecord.getValue(): the value's JSON
+            assert v == want, (case["name"], k, v, want)
+        assert set(got) - set(case["expected"]) <= set(case.get("json_hidden", [])), case["name"]
+
+
+def test_metadata_block_layout():
+    md = LS.record_metadata(LS.RT_REJECTION, LS.VT_PI, 8, 3, b"why")
+    block, template, schema, version = struct.unpack_from("<HHHH", md)
+    assert (block, template, schema, version) == (32, 200, 0, 4)
+    rt, stream, req, proto, vt, intent = struct.unpack_from("<BiQHBB", md, 8)
+    assert (rt, stream, req, proto, vt, intent) == (2, -(1 << 31), (1 << 64) - 1, 4, 5, 8)
+    major, minor, patch, rv, rej = struct.unpack_from("<iiiHB", md, 25)
+    assert (major, minor, patch, rv, rej) == (8, 4, 0, 1, 3)
+    n = struct.unpack_from("<I", md, 40)[0]
+    assert md[44:44 + n] == b"why"
+    m = struct.unpack_from("<I", md, 44 + n)[0]
+    assert msgpack.unpackb(md[48 + n:48 + n + m], raw=False) == {"format": "UNKNOWN", "authData": ""}
+    assert len(md) == 48 + n + m
+
+
+# ---- the product serializer against the oracle ------------------------------------------------------
+STATES = {"ELEMENT_ACTIVATING": 2, "ELEMENT_ACTIVATED": 3, "ELEMENT_COMPLETING": 4, "ELEMENT_COMPLETED": 5,
+          "ELEMENT_TERMINATING": 6, "ELEMENT_TERMINATED": 7}
+REASONS = [("Expected to be able to activate parallel gateway", 1),
+           ("Expected flow scope instance with key", 2), ("Expected flow scope instance to be in state", 3),
+           ("Expected element instance with key", 4), ("Expected element instance to be in state", 5),
+           ("Expected to complete job with key", 6)]
+
+
+def with_reason_codes(recs, orc):
+    """The CPU engine keeps rejection texts only; the drained records carry (reason, arg) codes
+    that the serializer formats.  Classify the oracle's texts into codes so the product formats
+    them itself (a wrong code or format shows up as a byte mismatch)."""
+    recs = recs.copy()
+    for i in np.nonzero(recs["record_type"] == abi.RT_REJECTION)[0]:
+        text = orc.reason(int(i))
+        code = [c for prefix, c in REASONS if text.startswith(prefix)]
+        assert code, text
+        recs[i]["reason"] = code[0]
+        recs[i]["reason_arg"] = STATES.get(text.rsplit("'", 2)[-2], 0) if code[0] in (3, 5) else 0
+    return recs
+
+
+class Run:
+    """Drives the CPU engine window by window and serialises every window's records with both."""
+
+    def __init__(self, xmls, names=(), strings=()):
+        self.orc = Oracle()
+        self.ser = LogSerializer()
+        for i, xml in enumerate(xmls):
+            key = 2251799813685249 + i
+            assert self.orc.deploy(xml, key) == self.ser.deploy(xml, key) == i
+        for n in names:
+            assert self.orc.intern(n) == self.ser.intern(n)
+        for s in strings:
+            assert self.orc.intern_string(s) == self.ser.intern_string(s)
+        self.source_base = self.doc_base = 0
+        self.position = 1000
+        self.total = 0
+
+    def window(self, cmds, docs=None):
+        docs = docs if docs is not None else abi.make_docs(0)
+        self.orc.clear_records()
+        self.orc.submit(cmds, docs)
+        self.orc.run()
+        recs = with_reason_codes(self.orc.records(), self.orc)
+        pos = self.position + 10 * np.arange(len(cmds), dtype=np.int64)
+        first = int(pos[-1]) + 1 if len(cmds) else self.position
+        got = self.ser.serialize(recs, cmds, docs, self.source_base, self.doc_base, pos, first, 1700000000123)
+        names, strings = self.orc.names(), self.orc.strings()
+        tables = LS.Tables(self.orc.process_tables(), lambda i: names[i], lambda i: strings[i])
+        sb, db = self.source_base, self.doc_base
+
+        def docs_of_source(si):
+            c = cmds[si - sb]
+            return docs[int(c["doc_begin"]):int(c["doc_begin"]) + int(c["doc_count"])]
+
+        want = LS.serialize(recs, tables, docs_of_source, lambda a: docs[a - db], self.orc.reason, first,
+                            lambda si: int(pos[si - sb]), 1700000000123)
+        assert got == want
+        check_entries(got, recs, first, pos, sb)
+        self.source_base += len(cmds)
+        self.doc_base += len(docs)
+        self.position = first + len(recs)
+        self.total += len(recs)
+        return recs
+
+
+def check_entries(buf, recs, first, pos, sb):
+    """Independent walk over the bytes: framing, header fields, metadata, msgpack values."""
+    entries = list(split_entries(buf))
+    assert len(entries) == len(recs)
+    for i, ((off, framed), r) in enumerate(zip(entries, recs)):
+        assert off % 8 == 0
+        e = buf[off + 12:off + framed]
+        _, flags, _, p, sp, key, ts, mlen, _ = struct.unpack_from("<HBBqqqqHH", e)
+        assert (p, sp, key, ts) == (first + i, int(pos[int(r["source_index"]) - sb]), int(r["key"]), 1700000000123)
+        assert flags == (1 if r["record_type"] == abi.RT_COMMAND else 0)
+        rt, vt, intent = struct.unpack_from("<B", e, 48)[0], e[40 + 8 + 15], e[40 + 8 + 16]
+        assert (rt, vt, intent) == (r["record_type"], r["value_type"], r["intent"])
+        value = msgpack.unpackb(e[40 + mlen:], raw=False)
+        assert value["tenantId"] == "<default>"
+        if r["value_type"] == abi.VT_PROCESS_INSTANCE:
+            assert value["processInstanceKey"] == r["process_instance_key"]
+            assert value["flowScopeKey"] == r["scope_key"]
+
+
+@pytest.mark.parametrize("workload", ["one_task", "linear3", "fork_join4"])
+def test_serializer_matches_oracle(workload):
+    xml = {"one_task": process_xml({"fixture": "one_task.bpmn"}), "linear3": bpmn.linear_process(3),
+           "fork_join4": bpmn.fork_join_process(4, tasks=True)}[workload]
+    run = Run([xml])
+    _drive_simple(run, 40)
+    assert run.total > 40
+
+
+def _key_map(orc, n):
+    """(key -> (instance, ordinal)) of the oracle's instances 0..n-1."""
+    m = {}
+    for i in range(n):
+        o = 0
+        while True:
+            k = orc.resolve(i, o)
+            if k < 0:
+                break
+            m[k] = (i, o)
+            o += 1
+    return m
+
+
+def _drive_simple(run, n, docs=None, mutate=None, first=0):
+    cmds = create_commands(n, 0, first)
+    if docs is not None:
+        cmds["doc_count"] = 1
+        cmds["doc_begin"] = np.arange(n)
+    recs = run.window(cmds, docs)
+    for _ in range(20):
+        jobs = [int(r["key"]) for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+        if not jobs:
+            break
+        km = _key_map(run.orc, first + n)
+        c = complete_commands([km[k][0] for k in jobs], [km[k][1] for k in jobs])
+        d = None
+        if mutate is not None:
+            c, d = mutate(c)
+        recs = run.window(c, d)
+    return run
+
+
+def test_serializer_variables_and_decimals():
+    """Config 3 (int and scaled-decimal `amount`), VARIABLE records and documents."""
+    rng = np.random.default_rng(0x5EED03)
+    run = Run([bpmn.xor_process()], names=["amount"])
+    _drive_simple(run, 30, amount_docs(rng.integers(0, 2001, 30), 0))
+    _drive_simple(run, 30, amount_docs(rng.integers(0, 200001, 30) * 10000, 0, decimal=True), first=30)
+
+
+def test_serializer_job_documents_strings_and_rejections():
+    """JOB:COMPLETE with variable documents (bool, nil, string, int) on the job path, stale jobs
+    (NOT_FOUND rejections with their text) and the PROCESS_EVENT / JOB:COMPLETED documents."""
+    run = Run([bpmn.linear_process(2)], names=["x", "s"], strings=["hello", "k-" + "z" * 40])
+    kinds = [(abi.DOC_INT, 7), (abi.DOC_BOOL, 1), (abi.DOC_NIL, 0), (abi.DOC_STR, 1), (abi.DOC_INT, -70000)]
+
+    def mutate(c):
+        m = len(c)
+        d = abi.make_docs(m)
+        for i in range(m):
+            t, v = kinds[i % len(kinds)]
+            d[i]["name_id"] = i % 2
+            d[i]["type"], d[i]["value"] = t, v
+        c["doc_count"] = np.arange(m) % 3 != 0
+        c["doc_begin"] = np.arange(m)
+        stale = c[: m // 4].copy()
+        stale["doc_count"] = 0
+        return np.concatenate([c, stale]), d
+
+    _drive_simple(run, 24, mutate=mutate)
+
+
+def test_serializer_rejects_message_records():
+    run = Run([bpmn.linear_process(1)])
+    recs = run.window(create_commands(1, 0))
+    bad = recs[:1].copy()
+    bad["value_type"] = abi.VT_MESSAGE
+    with pytest.raises(Exception):
+        run.ser.serialize(bad, create_commands(1, 0), source_base=run.source_base - 1)

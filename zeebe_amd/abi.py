@@ -104,6 +104,12 @@ class XpartCmd(C.Structure):
                 ("target_partition", C.c_int16), ("pad", C.c_uint32)]
 
 
+class LogWindow(C.Structure):  # zbhip_log_window
+    _fields_ = [("cmds", C.c_void_p), ("n_cmds", C.c_size_t), ("source_base", C.c_int64), ("docs", C.c_void_p),
+                ("n_docs", C.c_size_t), ("doc_base", C.c_int64), ("source_positions", C.c_void_p),
+                ("first_position", C.c_int64), ("timestamp", C.c_int64)]
+
+
 class Config(C.Structure):
     _fields_ = [("partition_id", C.c_int32), ("partition_count", C.c_int32), ("device", C.c_int32),
                 ("max_commands_in_batch", C.c_int32), ("max_instances", C.c_uint32),

@@ -64,7 +64,10 @@ using KSimple = KCfg<128, 4, 4, 16, false, false>;  // no parallel gateways / mu
 // workgroup at <= 20 KiB of LDS and the register target at 128 VGPRs, so 4 waves per SIMD are
 // resident (KSimple: 3).  The FIFO never holds more than one entry there and the table two, so both
 // live in registers: the batch logic issues no dependent LDS round trips, only the record stage.
-using KLinear = KCfg<64, 2, 2, 15, false, false, false, 4, true>;
+#ifndef ZB_KLINEAR_W
+#define ZB_KLINEAR_W 4
+#endif
+using KLinear = KCfg<64, 2, 2, 15, false, false, false, ZB_KLINEAR_W, true>;
 using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
 using KMsg = KCfg<128, 12, 16, 16, true>;  // partitions with message catch events (config 5)
 

@@ -1,0 +1,496 @@
+// Log serialiser of libzbhip.so: drained records -> the bytes the reference's log stream holds
+// for them.  Host code, no device work: it turns the compact records of a
+// window into sequenced batches of log entries -- dispatcher framing, the LogEntryDescriptor
+// header, the SBE RecordMetadata and the msgpack record value -- exactly as
+//   SequencedBatchSerializer.java:33-67, LogAppendEntrySerializer.java:40-111,
+//   LogEntryDescriptor.java (static block), DataFrameDescriptor.java,
+//   RecordMetadata.java write/reset + protocol.xml:137-152 (schema version 4, protocol/pom.xml:28),
+//   ObjectValue.java:78-84 + MsgPackWriter.java:62-316
+// write them.  Record values follow the engine's writers: ProcessInstanceRecord.java:62-74 with
+// BpmnStateTransitionBehavior.java:243-339 / CreateProcessInstanceProcessor.java:319-330,
+// JobRecord.java:39-83 with BpmnJobBehavior.java:194-218 and JobCompleteProcessor.java:75-92,
+// VariableRecord.java:25-41, ProcessEventRecord.java:25-42 with EventTriggerBehavior.java:148-166,
+// ProcessInstanceCreationRecord.java:32-55 with CreateProcessInstanceProcessor.java:129-158, and a
+// rejection carries its command's value (ResultBuilderBackedRejectionWriter.java:25-38).
+//
+// Deploy time compiles, per element, the constant msgpack runs of its records (everything but
+// the keys), so a record costs a few memcpys and the variable-length key integers.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/zbhip.h"
+
+namespace {
+
+using Bytes = std::string;
+
+// ---- MsgPackWriter (MsgPackWriter.java:62-316) ------------------------------------------------
+void be16(Bytes& b, uint16_t v) { b.push_back((char)(v >> 8)); b.push_back((char)v); }
+void be32(Bytes& b, uint32_t v) { be16(b, (uint16_t)(v >> 16)); be16(b, (uint16_t)v); }
+void be64(Bytes& b, uint64_t v) { be32(b, (uint32_t)(v >> 32)); be32(b, (uint32_t)v); }
+
+void mp_map(Bytes& b, uint32_t n) {
+  if (n < 16) b.push_back((char)(0x80 | n));
+  else if (n < 65536) { b.push_back((char)0xde); be16(b, (uint16_t)n); }
+  else { b.push_back((char)0xdf); be32(b, n); }
+}
+void mp_array(Bytes& b, uint32_t n) {
+  if (n < 16) b.push_back((char)(0x90 | n));
+  else if (n < 65536) { b.push_back((char)0xdc); be16(b, (uint16_t)n); }
+  else { b.push_back((char)0xdd); be32(b, n); }
+}
+void mp_int(Bytes& b, int64_t v) {
+  if (v < -(1LL << 5)) {
+    if (v < -(1LL << 15)) {
+      if (v < -(1LL << 31)) { b.push_back((char)0xd3); be64(b, (uint64_t)v); }
+      else { b.push_back((char)0xd2); be32(b, (uint32_t)v); }
+    } else if (v < -(1LL << 7)) { b.push_back((char)0xd1); be16(b, (uint16_t)v); }
+    else { b.push_back((char)0xd0); b.push_back((char)v); }
+  } else if (v < (1LL << 7)) {
+    b.push_back((char)v);
+  } else if (v < (1LL << 16)) {
+    if (v < (1LL << 8)) { b.push_back((char)0xcc); b.push_back((char)v); }
+    else { b.push_back((char)0xcd); be16(b, (uint16_t)v); }
+  } else if (v < (1LL << 32)) { b.push_back((char)0xce); be32(b, (uint32_t)v); }
+  else { b.push_back((char)0xcf); be64(b, (uint64_t)v); }
+}
+void mp_str(Bytes& b, const char* s, size_t n) {
+  if (n < 32) b.push_back((char)(0xa0 | n));
+  else if (n < 256) { b.push_back((char)0xd9); b.push_back((char)n); }
+  else if (n < 65536) { b.push_back((char)0xda); be16(b, (uint16_t)n); }
+  else { b.push_back((char)0xdb); be32(b, (uint32_t)n); }
+  b.append(s, n);
+}
+void mp_str(Bytes& b, const std::string& s) { mp_str(b, s.data(), s.size()); }
+void mp_bin(Bytes& b, const Bytes& v) {
+  const size_t n = v.size();
+  if (n < 256) { b.push_back((char)0xc4); b.push_back((char)n); }
+  else if (n < 65536) { b.push_back((char)0xc5); be16(b, (uint16_t)n); }
+  else { b.push_back((char)0xc6); be32(b, (uint32_t)n); }
+  b.append(v);
+}
+void key(Bytes& b, const char* k) { mp_str(b, k, strlen(k)); }
+
+const char* element_type_name(uint32_t t) {
+  static const char* n[] = {"UNSPECIFIED", "PROCESS", "SUB_PROCESS", "EVENT_SUB_PROCESS", "START_EVENT",
+                            "INTERMEDIATE_CATCH_EVENT", "INTERMEDIATE_THROW_EVENT", "BOUNDARY_EVENT", "END_EVENT",
+                            "SERVICE_TASK", "RECEIVE_TASK", "USER_TASK", "MANUAL_TASK", "TASK", "EXCLUSIVE_GATEWAY",
+                            "PARALLEL_GATEWAY", "EVENT_BASED_GATEWAY", "INCLUSIVE_GATEWAY", "SEQUENCE_FLOW"};
+  return t < sizeof(n) / sizeof(n[0]) ? n[t] : "UNSPECIFIED";
+}
+const char* event_type_name(uint32_t t) {
+  static const char* n[] = {"UNSPECIFIED", "CONDITIONAL", "ERROR", "ESCALATION", "LINK", "MESSAGE", "NONE",
+                            "SIGNAL", "TERMINATE", "TIMER"};
+  return t < sizeof(n) / sizeof(n[0]) ? n[t] : "UNSPECIFIED";
+}
+const char* state_text(int s) {
+  switch (s) {
+    case ZBHIP_PI_ELEMENT_ACTIVATING: return "ELEMENT_ACTIVATING";
+    case ZBHIP_PI_ELEMENT_ACTIVATED: return "ELEMENT_ACTIVATED";
+    case ZBHIP_PI_ELEMENT_COMPLETING: return "ELEMENT_COMPLETING";
+    case ZBHIP_PI_ELEMENT_COMPLETED: return "ELEMENT_COMPLETED";
+    case ZBHIP_PI_ELEMENT_TERMINATING: return "ELEMENT_TERMINATING";
+    case ZBHIP_PI_ELEMENT_TERMINATED: return "ELEMENT_TERMINATED";
+    default: return "?";
+  }
+}
+
+const char* kTenant = "<default>";  // TenantOwned.DEFAULT_TENANT_IDENTIFIER
+const Bytes kEmptyDoc("\x80", 1);   // MsgPackHelper.EMTPY_OBJECT (DocumentValue.EMPTY_DOCUMENT, JobRecord.NO_HEADERS)
+
+// deploy-time constant runs of one element's records
+struct SerElement {
+  uint8_t type = 0, event = 0;
+  std::string id;
+  // ProcessInstanceRecord: [map, bpmnElementType .. processDefinitionKey, "processInstanceKey"] key
+  // ["flowScopeKey"] key [bpmnEventType .. tenantId]
+  Bytes pi_head, pi_tail;
+  // JobRecord of a service task: [map .. customHeaders, "variables"] bin(doc) [errorMessage ..
+  // processDefinitionKey, "processInstanceKey"] key ["elementId" .. "elementInstanceKey"] key [tenantId]
+  Bytes job_head, job_mid, job_tail;
+};
+struct SerProcess {
+  std::string bpmn_id;
+  int32_t version = 1;
+  int64_t def_key = 0;
+  std::vector<SerElement> els;
+};
+
+}  // namespace
+
+struct zbhip_serializer {
+  std::vector<SerProcess> procs;
+  std::vector<std::string> names;
+  std::unordered_map<std::string, uint32_t> name_ids;
+  std::vector<std::string> strs;
+  std::unordered_map<std::string, uint32_t> str_ids;
+  int32_t broker[3] = {8, 4, 0};  // RecordMetadata.CURRENT_BROKER_VERSION of the reference build (8.4.0-SNAPSHOT)
+  Bytes auth;                     // empty AuthInfo (format UNKNOWN, authData "")
+};
+
+extern "C" {
+
+int zbhip_serializer_new(zbhip_serializer** out) {
+  if (!out) return ZBHIP_EINVAL;
+  auto* s = new zbhip_serializer();
+  mp_map(s->auth, 2);  // AuthInfo.java: declareProperty(formatProp).declareProperty(authDataProp)
+  key(s->auth, "format");
+  key(s->auth, "UNKNOWN");
+  key(s->auth, "authData");
+  key(s->auth, "");
+  *out = s;
+  return ZBHIP_OK;
+}
+
+void zbhip_serializer_free(zbhip_serializer* s) { delete s; }
+
+int zbhip_serializer_set_broker_version(zbhip_serializer* s, int32_t major, int32_t minor, int32_t patch) {
+  if (!s) return ZBHIP_EINVAL;
+  s->broker[0] = major;
+  s->broker[1] = minor;
+  s->broker[2] = patch;
+  return ZBHIP_OK;
+}
+
+int zbhip_serializer_intern(zbhip_serializer* s, const char* name) {
+  if (!s || !name) return ZBHIP_EINVAL;
+  auto it = s->name_ids.find(name);
+  if (it != s->name_ids.end()) return (int)it->second;
+  const uint32_t id = (uint32_t)s->names.size();
+  s->names.emplace_back(name);
+  s->name_ids.emplace(name, id);
+  return (int)id;
+}
+
+int64_t zbhip_serializer_intern_string(zbhip_serializer* s, const char* bytes, size_t len) {
+  if (!s || (len && !bytes)) return ZBHIP_EINVAL;
+  std::string v(bytes ? bytes : "", len);
+  auto it = s->str_ids.find(v);
+  if (it != s->str_ids.end()) return it->second;
+  const uint32_t id = (uint32_t)s->strs.size();
+  s->strs.push_back(v);
+  s->str_ids.emplace(std::move(v), id);
+  return id;
+}
+
+int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, uint32_t* idx_out) {
+  if (!s || !csr || csr->n_elements == 0) return ZBHIP_EINVAL;
+  SerProcess P;
+  auto str = [&](uint16_t i) -> std::string { return i < csr->n_strings ? csr->strings[i] : ""; };
+  P.bpmn_id = str(csr->bpmn_process_id);
+  P.version = csr->version;
+  P.def_key = csr->process_definition_key;
+  P.els.resize(csr->n_elements);
+  for (uint32_t e = 0; e < csr->n_elements; ++e) {
+    const zbhip_element& E = csr->elements[e];
+    SerElement& S = P.els[e];
+    S.type = E.element_type;
+    S.event = E.element_type == ZBHIP_EL_PROCESS ? ZBHIP_EV_UNSPECIFIED : E.event_type;
+    S.id = str(E.id);
+    // ProcessInstanceRecord (declaration order ProcessInstanceRecord.java:63-73)
+    mp_map(S.pi_head, 11);
+    key(S.pi_head, "bpmnElementType");
+    key(S.pi_head, element_type_name(S.type));
+    key(S.pi_head, "elementId");
+    mp_str(S.pi_head, S.id);
+    key(S.pi_head, "bpmnProcessId");
+    mp_str(S.pi_head, P.bpmn_id);
+    key(S.pi_head, "version");
+    mp_int(S.pi_head, P.version);
+    key(S.pi_head, "processDefinitionKey");
+    mp_int(S.pi_head, P.def_key);
+    key(S.pi_head, "processInstanceKey");
+    key(S.pi_tail, "bpmnEventType");
+    key(S.pi_tail, event_type_name(S.event));
+    key(S.pi_tail, "parentProcessInstanceKey");
+    mp_int(S.pi_tail, -1);
+    key(S.pi_tail, "parentElementInstanceKey");
+    mp_int(S.pi_tail, -1);
+    key(S.pi_tail, "tenantId");
+    key(S.pi_tail, kTenant);
+    if (E.element_type == ZBHIP_EL_SERVICE_TASK) {
+      // JobRecord (JobRecord.java:67-83) as BpmnJobBehavior.writeJobCreatedEvent fills it
+      mp_map(S.job_head, 17);
+      key(S.job_head, "deadline");
+      mp_int(S.job_head, -1);
+      key(S.job_head, "worker");
+      key(S.job_head, "");
+      key(S.job_head, "retries");
+      mp_int(S.job_head, (int32_t)E.job_retries);
+      key(S.job_head, "retryBackoff");
+      mp_int(S.job_head, 0);
+      key(S.job_head, "recurringTime");
+      mp_int(S.job_head, -1);
+      key(S.job_head, "type");
+      mp_str(S.job_head, str(E.job_type));
+      key(S.job_head, "customHeaders");
+      S.job_head += kEmptyDoc;  // no task headers: NO_HEADERS (BpmnJobBehavior.java:365-367)
+      key(S.job_head, "variables");
+      key(S.job_mid, "errorMessage");
+      key(S.job_mid, "");
+      key(S.job_mid, "errorCode");
+      key(S.job_mid, "");
+      key(S.job_mid, "bpmnProcessId");
+      mp_str(S.job_mid, P.bpmn_id);
+      key(S.job_mid, "processDefinitionVersion");
+      mp_int(S.job_mid, P.version);
+      key(S.job_mid, "processDefinitionKey");
+      mp_int(S.job_mid, P.def_key);
+      key(S.job_mid, "processInstanceKey");
+      key(S.job_tail, "elementId");
+      mp_str(S.job_tail, S.id);
+      key(S.job_tail, "elementInstanceKey");
+    }
+  }
+  if (idx_out) *idx_out = (uint32_t)s->procs.size();
+  s->procs.push_back(std::move(P));
+  return ZBHIP_OK;
+}
+
+const char* zbhip_serializer_name(zbhip_serializer* s, uint32_t id) {
+  return s && id < s->names.size() ? s->names[id].c_str() : "";
+}
+
+// Rejection reason text exactly as the reference writes it (ProcessInstanceStateTransitionGuard.java
+// :74-186, JobCommandPreconditionChecker, processing/message/*Processor.java).
+int zbhip_serializer_rejection_reason(zbhip_serializer* s, const zbhip_record* r, char* buf, size_t cap) {
+  if (!s || !r || !buf) return ZBHIP_EINVAL;
+  std::string id;
+  if (r->process_idx >= 0 && (size_t)r->process_idx < s->procs.size() && r->element_idx >= 0 &&
+      (size_t)r->element_idx < s->procs[r->process_idx].els.size())
+    id = s->procs[r->process_idx].els[r->element_idx].id;
+  const char* mname = zbhip_serializer_name(s, r->message_name);
+  switch (r->reason) {
+    case ZBHIP_REASON_PGW_NOT_ALL_TAKEN:
+      return snprintf(buf, cap, "Expected to be able to activate parallel gateway '%s', but not all sequence flows have been taken.", id.c_str());
+    case ZBHIP_REASON_FS_NOT_FOUND:
+      return snprintf(buf, cap, "Expected flow scope instance with key '%lld' to be present in state but not found.", (long long)r->scope_key);
+    case ZBHIP_REASON_FS_STATE:
+      return snprintf(buf, cap, "Expected flow scope instance to be in state 'ELEMENT_ACTIVATED' but was '%s'.", state_text(r->reason_arg));
+    case ZBHIP_REASON_EI_NOT_FOUND:
+      return snprintf(buf, cap, "Expected element instance with key '%lld' to be present in state but not found.", (long long)r->key);
+    case ZBHIP_REASON_EI_STATE:
+      return snprintf(buf, cap, "Expected element instance to be in state 'ELEMENT_ACTIVATED' or one of '[ELEMENT_COMPLETING]' but was '%s'.", state_text(r->reason_arg));
+    case ZBHIP_REASON_JOB_NOT_FOUND:
+      return snprintf(buf, cap, "Expected to complete job with key '%lld', but no such job was found", (long long)r->key);
+    case ZBHIP_REASON_MS_ALREADY_OPEN:
+      return snprintf(buf, cap, "Expected to open a new message subscription for element with key '%lld' and message "
+                      "name '%s', but there is already a message subscription for that element key and message name opened",
+                      (long long)r->scope_key, mname);
+    case ZBHIP_REASON_PMS_CREATE_NOT_FOUND:
+      return snprintf(buf, cap, "Expected to create process message subscription with element key '%lld' and message "
+                      "name '%s', but no such subscription was found", (long long)r->scope_key, mname);
+    case ZBHIP_REASON_PMS_CREATE_NOT_OPENING:
+      return snprintf(buf, cap, "Expected to create process message subscription with element key '%lld' and message "
+                      "name '%s', but it is already %s", (long long)r->scope_key, mname, r->reason_arg ? "opened" : "closing");
+    case ZBHIP_REASON_MS_CORR_NOT_FOUND:
+      return snprintf(buf, cap, "Expected to correlate subscription for element with key '%lld' and message name '%s', "
+                      "but no such message subscription exists", (long long)r->scope_key, mname);
+    default:
+      if (cap) buf[0] = 0;
+      return 0;
+  }
+}
+
+}  // extern "C"
+
+namespace {
+
+// msgpack of one document value, canonical client encoding (compact ints, float64 decimals = v / 10^6)
+bool doc_value(const zbhip_serializer* s, const zbhip_doc_entry& d, Bytes& b) {
+  switch (d.type) {
+    case ZBHIP_DOC_NIL: b.push_back((char)0xc0); return true;
+    case ZBHIP_DOC_BOOL: b.push_back((char)(d.value ? 0xc3 : 0xc2)); return true;
+    case ZBHIP_DOC_INT: mp_int(b, d.value); return true;
+    case ZBHIP_DOC_DEC: {
+      const double v = (double)d.value / 1e6;
+      uint64_t u;
+      memcpy(&u, &v, 8);
+      b.push_back((char)0xcb);
+      be64(b, u);
+      return true;
+    }
+    case ZBHIP_DOC_STR:
+      if ((uint64_t)d.value >= s->strs.size()) return false;
+      mp_str(b, s->strs[(size_t)d.value]);
+      return true;
+    default: return false;
+  }
+}
+
+bool document(const zbhip_serializer* s, const zbhip_doc_entry* e, size_t n, Bytes& b) {
+  if (n == 0) { b = kEmptyDoc; return true; }  // DocumentValue.wrap: empty / nil -> EMPTY_DOCUMENT
+  b.clear();
+  mp_map(b, (uint32_t)n);
+  for (size_t i = 0; i < n; ++i) {
+    if (e[i].name_id >= s->names.size()) return false;
+    mp_str(b, s->names[e[i].name_id]);
+    if (!doc_value(s, e[i], b)) return false;
+  }
+  return true;
+}
+
+void le16(Bytes& b, uint16_t v) { b.push_back((char)v); b.push_back((char)(v >> 8)); }
+void le32(Bytes& b, uint32_t v) { le16(b, (uint16_t)v); le16(b, (uint16_t)(v >> 16)); }
+void le64(Bytes& b, uint64_t v) { le32(b, (uint32_t)v); le32(b, (uint32_t)(v >> 32)); }
+
+}  // namespace
+
+extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n, const zbhip_log_window* w,
+                                   uint8_t* out, size_t cap, size_t* used) {
+  if (!s || !w || (n && !recs) || !used) return ZBHIP_EINVAL;
+  *used = 0;
+  Bytes value, md, doc, entry;
+  char reason[512];
+  size_t off = 0;
+  int64_t last_src = -1;
+  Bytes src_doc;
+  for (size_t i = 0; i < n; ++i) {
+    const zbhip_record& r = recs[i];
+    const int64_t ci = r.source_index - w->source_base;
+    if (ci < 0 || (size_t)ci >= w->n_cmds) return ZBHIP_EINVAL;
+    const zbhip_command& cm = w->cmds[ci];
+    if (r.source_index != last_src) {  // the source command's variable document
+      if (cm.doc_count && ((uint64_t)cm.doc_begin + cm.doc_count > w->n_docs || !w->docs)) return ZBHIP_EINVAL;
+      if (!document(s, cm.doc_count ? w->docs + cm.doc_begin : nullptr, cm.doc_count, src_doc)) return ZBHIP_EUNSUPP;
+      last_src = r.source_index;
+    }
+    const SerProcess* P = r.process_idx >= 0 && (size_t)r.process_idx < s->procs.size() ? &s->procs[r.process_idx] : nullptr;
+    const SerElement* E = P && r.element_idx >= 0 && (size_t)r.element_idx < P->els.size() ? &P->els[r.element_idx] : nullptr;
+    value.clear();
+    switch (r.value_type) {
+      case ZBHIP_VT_PROCESS_INSTANCE:
+        if (!E) return ZBHIP_EINVAL;
+        value += E->pi_head;
+        mp_int(value, r.process_instance_key);
+        key(value, "flowScopeKey");
+        mp_int(value, r.scope_key);
+        value += E->pi_tail;
+        break;
+      case ZBHIP_VT_JOB:
+        if (r.record_type == ZBHIP_RT_REJECTION) {  // the JOB:COMPLETE command's value
+          mp_map(value, 17);
+          key(value, "deadline"); mp_int(value, -1);
+          key(value, "worker"); key(value, "");
+          key(value, "retries"); mp_int(value, -1);
+          key(value, "retryBackoff"); mp_int(value, 0);
+          key(value, "recurringTime"); mp_int(value, -1);
+          key(value, "type"); key(value, "");
+          key(value, "customHeaders"); value += kEmptyDoc;
+          key(value, "variables"); mp_bin(value, src_doc);
+          key(value, "errorMessage"); key(value, "");
+          key(value, "errorCode"); key(value, "");
+          key(value, "bpmnProcessId"); key(value, "");
+          key(value, "processDefinitionVersion"); mp_int(value, -1);
+          key(value, "processDefinitionKey"); mp_int(value, -1);
+          key(value, "processInstanceKey"); mp_int(value, -1);
+          key(value, "elementId"); key(value, "");
+          key(value, "elementInstanceKey"); mp_int(value, -1);
+          key(value, "tenantId"); key(value, kTenant);
+        } else {
+          if (!E || E->job_head.empty()) return ZBHIP_EINVAL;
+          value += E->job_head;
+          mp_bin(value, r.intent == ZBHIP_JOB_COMPLETED ? src_doc : kEmptyDoc);
+          value += E->job_mid;
+          mp_int(value, r.process_instance_key);
+          value += E->job_tail;
+          mp_int(value, r.scope_key);
+          key(value, "tenantId");
+          key(value, kTenant);
+        }
+        break;
+      case ZBHIP_VT_VARIABLE: {
+        if (!P || r.element_idx < 0 || (size_t)r.element_idx >= s->names.size()) return ZBHIP_EINVAL;
+        const int64_t di = r.aux - w->doc_base;
+        if (!w->docs || di < 0 || (size_t)di >= w->n_docs) return ZBHIP_EINVAL;
+        doc.clear();
+        if (!doc_value(s, w->docs[di], doc)) return ZBHIP_EUNSUPP;
+        mp_map(value, 7);  // VariableRecord.java:35-41
+        key(value, "name"); mp_str(value, s->names[r.element_idx]);
+        key(value, "value"); mp_bin(value, doc);
+        key(value, "scopeKey"); mp_int(value, r.scope_key);
+        key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+        key(value, "processDefinitionKey"); mp_int(value, P->def_key);
+        key(value, "bpmnProcessId"); mp_str(value, P->bpmn_id);
+        key(value, "tenantId"); key(value, kTenant);
+        break;
+      }
+      case ZBHIP_VT_PROCESS_EVENT:
+        if (!E || !P) return ZBHIP_EINVAL;
+        mp_map(value, 6);  // ProcessEventRecord.java:37-42
+        key(value, "scopeKey"); mp_int(value, r.scope_key);
+        key(value, "targetElementId"); mp_str(value, E->id);
+        key(value, "variables"); mp_bin(value, src_doc);
+        key(value, "processDefinitionKey"); mp_int(value, P->def_key);
+        key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+        key(value, "tenantId"); key(value, kTenant);
+        break;
+      case ZBHIP_VT_PROCESS_INSTANCE_CREATION:
+        if (!P) return ZBHIP_EINVAL;
+        mp_map(value, 8);  // ProcessInstanceCreationRecord.java:48-55
+        key(value, "bpmnProcessId"); mp_str(value, P->bpmn_id);
+        key(value, "processDefinitionKey"); mp_int(value, P->def_key);
+        key(value, "processInstanceKey"); mp_int(value, r.scope_key);
+        key(value, "version"); mp_int(value, P->version);
+        key(value, "variables"); mp_bin(value, src_doc);
+        key(value, "fetchVariables"); mp_array(value, 0);
+        key(value, "startInstructions"); mp_array(value, 0);
+        key(value, "tenantId"); key(value, kTenant);
+        break;
+      default:
+        return ZBHIP_EUNSUPP;  // message records: not serialised yet
+    }
+    // ---- SBE RecordMetadata (messageHeader + 32-byte block + 2 var-data fields) ----
+    md.clear();
+    le16(md, 32); le16(md, 200); le16(md, 0); le16(md, 4);   // blockLength, templateId, schemaId, version
+    md.push_back((char)r.record_type);
+    le32(md, 0x80000000u);                                   // requestStreamId: int32 null
+    le64(md, ~0ull);                                         // requestId: uint64 null
+    le16(md, 4);                                             // protocolVersion = Protocol.PROTOCOL_VERSION
+    md.push_back((char)r.value_type);
+    md.push_back((char)r.intent);
+    le32(md, (uint32_t)s->broker[0]); le32(md, (uint32_t)s->broker[1]); le32(md, (uint32_t)s->broker[2]);
+    le16(md, 1);                                             // recordVersion: latest applier version / default
+    const bool rej = r.record_type == ZBHIP_RT_REJECTION;
+    md.push_back((char)(rej ? r.rejection_type : 255));     // RejectionType.NULL_VAL
+    size_t rl = 0;
+    if (rej) {
+      const int k = zbhip_serializer_rejection_reason(s, &r, reason, sizeof reason);
+      rl = k > 0 ? std::min((size_t)k, sizeof reason - 1) : 0;
+    }
+    le32(md, (uint32_t)rl);
+    md.append(reason, rl);
+    le32(md, (uint32_t)s->auth.size());
+    md += s->auth;
+    // ---- dispatcher frame + LogEntryDescriptor header + metadata + value, 8-aligned ----
+    const size_t body = 40 + md.size() + value.size();
+    const size_t framed = 12 + body;
+    const size_t aligned = (framed + 7) & ~(size_t)7;
+    const size_t ci_pos = (size_t)ci;
+    const int64_t src_pos = w->source_positions ? w->source_positions[ci_pos] : -1;
+    if (out && off + aligned <= cap) {
+      uint8_t* p = out + off;
+      memset(p, 0, aligned);
+      const uint32_t fl = (uint32_t)framed;
+      memcpy(p, &fl, 4);
+      uint8_t* e = p + 12;
+      e[2] = r.record_type == ZBHIP_RT_COMMAND ? 1 : 0;  // skipProcessing: processed follow-up command
+      const int64_t pos = w->first_position + (int64_t)i;
+      memcpy(e + 4, &pos, 8);
+      memcpy(e + 12, &src_pos, 8);
+      memcpy(e + 20, &r.key, 8);
+      memcpy(e + 28, &w->timestamp, 8);
+      const uint16_t ml = (uint16_t)md.size();
+      memcpy(e + 36, &ml, 2);
+      memcpy(e + 40, md.data(), md.size());
+      memcpy(e + 40 + md.size(), value.data(), value.size());
+    }
+    off += aligned;
+  }
+  *used = off;
+  return off <= cap || !out ? ZBHIP_OK : ZBHIP_ENOMEM;
+}

@@ -90,6 +90,7 @@ hipError_t dalloc(T** p, size_t count) {
 
 struct zbhip_handle {
   zbhip_config cfg{};
+  zbhip_serializer* ser = nullptr;  // log serialiser, kept in step with deploy / intern (logwriter.cpp)
   hipStream_t stream = nullptr;
   bool own_stream = false;
 
@@ -232,6 +233,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   HIPCHK(hipSetDevice(cfg->device));
   auto* h = new zbhip_handle();
   h->cfg = *cfg;
+  zbhip_serializer_new(&h->ser);
   if (h->cfg.max_commands_in_batch <= 0) h->cfg.max_commands_in_batch = 100;
   if (h->cfg.max_doc_entries == 0) h->cfg.max_doc_entries = cfg->max_commands;
   h->rec_cap = cfg->max_records_per_batch ? cfg->max_records_per_batch : 64;
@@ -341,6 +343,7 @@ void zbhip_close(zbhip_handle* h) {
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  zbhip_serializer_free(h->ser);
   delete h;
 }
 
@@ -352,6 +355,7 @@ int zbhip_intern(zbhip_handle* h, const char* name) {
   uint32_t id = (uint32_t)h->names.size();
   h->names.emplace_back(name);
   h->name_ids.emplace(name, id);
+  if (h->ser) zbhip_serializer_intern(h->ser, name);
   return (int)id;
 }
 
@@ -526,6 +530,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     h->variant = old_variant;
     return rc;
   }
+  zbhip_serializer_deploy(h->ser, csr, nullptr);  // same index: both append in deploy order
   if (idx_out) *idx_out = (uint32_t)h->procs.size() - 1;
   return ZBHIP_OK;
 }
@@ -1051,44 +1056,10 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
 
 int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* r, char* buf, size_t cap) {
   if (!h || !r || !buf) return ZBHIP_EINVAL;
-  std::string id;
-  if (r->process_idx >= 0 && (size_t)r->process_idx < h->procs.size() && r->element_idx >= 0 &&
-      (size_t)r->element_idx < h->procs[r->process_idx].els.size())
-    id = h->procs[r->process_idx].id(r->element_idx);
-  // ProcessInstanceStateTransitionGuard.java:74-186, JobCommandPreconditionChecker.java
-  switch (r->reason) {
-    case ZBHIP_REASON_PGW_NOT_ALL_TAKEN:
-      return snprintf(buf, cap, "Expected to be able to activate parallel gateway '%s', but not all sequence flows have been taken.", id.c_str());
-    case ZBHIP_REASON_FS_NOT_FOUND:
-      return snprintf(buf, cap, "Expected flow scope instance with key '%lld' to be present in state but not found.", (long long)r->scope_key);
-    case ZBHIP_REASON_FS_STATE:
-      return snprintf(buf, cap, "Expected flow scope instance to be in state 'ELEMENT_ACTIVATED' but was '%s'.", state_name(r->reason_arg));
-    case ZBHIP_REASON_EI_NOT_FOUND:
-      return snprintf(buf, cap, "Expected element instance with key '%lld' to be present in state but not found.", (long long)r->key);
-    case ZBHIP_REASON_EI_STATE:
-      return snprintf(buf, cap, "Expected element instance to be in state 'ELEMENT_ACTIVATED' or one of '[ELEMENT_COMPLETING]' but was '%s'.", state_name(r->reason_arg));
-    case ZBHIP_REASON_JOB_NOT_FOUND:
-      return snprintf(buf, cap, "Expected to complete job with key '%lld', but no such job was found", (long long)r->key);
-    // processing/message/*Processor.java rejection texts
-    case ZBHIP_REASON_MS_ALREADY_OPEN:
-      return snprintf(buf, cap, "Expected to open a new message subscription for element with key '%lld' and message "
-                      "name '%s', but there is already a message subscription for that element key and message name opened",
-                      (long long)r->scope_key, zbhip_name(h, r->message_name));
-    case ZBHIP_REASON_PMS_CREATE_NOT_FOUND:
-      return snprintf(buf, cap, "Expected to create process message subscription with element key '%lld' and message "
-                      "name '%s', but no such subscription was found", (long long)r->scope_key, zbhip_name(h, r->message_name));
-    case ZBHIP_REASON_PMS_CREATE_NOT_OPENING:
-      return snprintf(buf, cap, "Expected to create process message subscription with element key '%lld' and message "
-                      "name '%s', but it is already %s", (long long)r->scope_key, zbhip_name(h, r->message_name),
-                      r->reason_arg ? "opened" : "closing");
-    case ZBHIP_REASON_MS_CORR_NOT_FOUND:
-      return snprintf(buf, cap, "Expected to correlate subscription for element with key '%lld' and message name '%s', "
-                      "but no such message subscription exists", (long long)r->scope_key, zbhip_name(h, r->message_name));
-    default:
-      if (cap) buf[0] = 0;
-      return 0;
-  }
+  return zbhip_serializer_rejection_reason(h->ser, r, buf, cap);
 }
+
+zbhip_serializer* zbhip_handle_serializer(zbhip_handle* h) { return h ? h->ser : nullptr; }
 
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal) {
   if (!h || !instance || !ordinal) return ZBHIP_EINVAL;
@@ -1111,6 +1082,7 @@ int64_t zbhip_intern_string(zbhip_handle* h, const char* bytes, size_t len) {
   if (it != h->str_ids.end()) return it->second;
   if (h->strs.size() >= 0xFFFFFFF0u) return ZBHIP_ENOMEM;
   const uint32_t id = (uint32_t)h->strs.size();
+  if (h->ser) zbhip_serializer_intern_string(h->ser, v.data(), v.size());
   h->str_hash.push_back((uint32_t)java_hash(v.data(), v.size()));
   h->strs.push_back(std::move(v));
   h->str_ids.emplace(h->strs.back(), id);

@@ -97,6 +97,11 @@ class Partition:
     def intern(self, name):
         return check(self.L.zbhip_intern(self.h, name.encode()))
 
+    def log_serializer(self):
+        """The partition's log serialiser (follows its deployments and dictionaries)."""
+        from .logwriter import LogSerializer
+        return LogSerializer(self)
+
     def name(self, nid):
         return self.L.zbhip_name(self.h, nid).decode()
 

@@ -22,7 +22,10 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info", "zbhip_command_status",
            "zbhip_submit_ex", "zbhip_submit_device_ex", "zbhip_intern_string", "zbhip_intern_strings",
            "zbhip_string_value", "zbhip_subscription_partition", "zbhip_outbox", "zbhip_outbox_device",
-           "zbhip_outbox_copy", "zbhip_submit_xparts_device", "zbhip_string_partitions"]
+           "zbhip_outbox_copy", "zbhip_submit_xparts_device", "zbhip_string_partitions",
+           "zbhip_serializer_new", "zbhip_serializer_free", "zbhip_serializer_deploy", "zbhip_serializer_intern",
+           "zbhip_serializer_intern_string", "zbhip_serializer_set_broker_version",
+           "zbhip_serializer_rejection_reason", "zbhip_handle_serializer", "zbhip_serialize_log"]
 
 
 class ZbhipError(RuntimeError):
@@ -82,6 +85,18 @@ def load():
     L.zbhip_outbox_copy.argtypes = [vp, vp, sz, sz]
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
     L.zbhip_string_partitions.argtypes = [vp, vp, sz, C.c_int32, vp]
+    L.zbhip_serializer_new.argtypes = [C.POINTER(vp)]
+    L.zbhip_serializer_free.argtypes = [vp]
+    L.zbhip_serializer_free.restype = None
+    L.zbhip_serializer_deploy.argtypes = [vp, vp, C.POINTER(u32)]
+    L.zbhip_serializer_intern.argtypes = [vp, C.c_char_p]
+    L.zbhip_serializer_intern_string.argtypes = [vp, C.c_char_p, sz]
+    L.zbhip_serializer_intern_string.restype = i64
+    L.zbhip_serializer_set_broker_version.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32]
+    L.zbhip_serializer_rejection_reason.argtypes = [vp, C.POINTER(abi.Record), C.c_char_p, sz]
+    L.zbhip_handle_serializer.argtypes = [vp]
+    L.zbhip_handle_serializer.restype = vp
+    L.zbhip_serialize_log.argtypes = [vp, vp, sz, C.POINTER(abi.LogWindow), vp, sz, C.POINTER(sz)]
     L.zbhip_build_info.argtypes = []
     L.zbhip_build_info.restype = C.c_char_p
     _lib = L
