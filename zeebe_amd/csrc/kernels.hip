@@ -1505,6 +1505,10 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   bool fast = false;
   if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
   if (fast) {
+#ifdef ZB_EXP_FASTONLY  // diagnostic build: the general path compiled out (its commands fall back)
+  } else if (K::REG) {
+    set_fail(L, FB_UNSUPPORTED);
+#endif
   } else if (!L.fail && kind == ZBHIP_CMD_CREATE) {
     if ((L.pb[0] >> 16) == NONE) set_fail(L, FB_BAD_PROCESS);
     uint32_t pi = new_key(L);  // = ordinal 0
@@ -1547,6 +1551,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.processed = 1;
 
   // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
+#ifdef ZB_EXP_FASTONLY
+  if (K::REG) fast = true;
+#endif
   while (!fast && L.qh < L.qt && !L.fail) {
     const uint32_t entry = qget(L, L.qh);
     ++L.qh;
@@ -1736,7 +1743,22 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
     ZB_STAMP(t3);
     uint2* out = P.out + (size_t)(P.region_base + c) * K::B * P.rec_cap;
     const uint32_t my_off = wbase + inc - my_nrec;
-    if (!ovf && total <= (uint32_t)(K::B * K::R)) {
+    // homogeneous single-wave chunk (every lane emitted the same n records -- a window of one
+    // command kind at one element, the common case of straight-line segments): record o of the
+    // run is row o % n of lane o / n, so the copy needs no owner map; o / n by a 16-bit
+    // reciprocal, exact for o < 2^16 / n
+    const uint32_t n0 = __builtin_amdgcn_readfirstlane(my_nrec);
+    if (K::REG && !ovf && n0 > 0 && __ballot(my_nrec != n0) == 0 && total == K::B * n0) {
+      const uint32_t m = (65536u + n0 - 1) / n0;
+      for (uint32_t o = 2 * threadIdx.x; o < total; o += 2 * K::B) {
+        const uint32_t l0 = (o * m) >> 16, j0 = o - l0 * n0;
+        const uint32_t l1 = j0 + 1 == n0 ? l0 + 1 : l0, j1 = j0 + 1 == n0 ? 0 : j0 + 1;
+        const uint2 r0 = stage_base[j0 * K::B + l0];
+        const uint2 r1 = stage_base[j1 * K::B + l1];
+        *reinterpret_cast<uint4*>(out + o) = make_uint4(r0.x, r0.y, r1.x, r1.y);
+      }
+      __builtin_amdgcn_wave_barrier();  // the next chunk reuses the stage
+    } else if (!ovf && total <= (uint32_t)(K::B * K::R)) {
       // packed copy: an owner map in LDS turns the lanes' columns into one contiguous run that
       // the workgroup stores with 16-byte, fully coalesced writes (2 records per lane).  Only
       // chunks without overflow rows take it, so the copy reads LDS alone and its stores never
