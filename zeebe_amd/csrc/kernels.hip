@@ -58,7 +58,15 @@ struct KCfg {
   static constexpr bool J = J_;  // parallel-gateway join counters
   static constexpr bool X = X_;  // exclusive gateways (FEEL condition evaluation)
 };
-using KSimple = KCfg<128, 4, 4, 16, false, false>;  // no parallel gateways / multi-outgoing nodes: no join counters
+// One token per instance (exclusive gateways, no parallel gateways / multi-outgoing nodes: no join
+// counters).  64-lane workgroups with 28 stage rows hold a whole config-3 CREATE batch (26 records)
+// in LDS: with 16 rows every chunk spilled 10 rows per lane to the global overflow rows and took
+// the per-lane flush -- 1.9x slower (A/B on config 3: 0.83 -> 1.59 x 10^11 transitions/s).
+#ifndef ZB_KSIMPLE_B
+#define ZB_KSIMPLE_B 64
+#define ZB_KSIMPLE_R 28
+#endif
+using KSimple = KCfg<ZB_KSIMPLE_B, 4, 4, ZB_KSIMPLE_R, false, false>;
 // Linear chains (every node <= 1 outgoing flow, no gateways, no catch events): at most two element
 // instances are alive in a batch, no FEEL evaluator, no join counters.  T = 2 and R = 15 keep the
 // workgroup at <= 20 KiB of LDS and the register target at 128 VGPRs, so 4 waves per SIMD are
@@ -68,7 +76,11 @@ using KSimple = KCfg<128, 4, 4, 16, false, false>;  // no parallel gateways / mu
 #define ZB_KLINEAR_W 4
 #endif
 using KLinear = KCfg<64, 2, 2, 15, false, false, false, ZB_KLINEAR_W, true>;
-using KGeneric = KCfg<128, 12, 16, 16>; // everything else in the subset
+#ifndef ZB_KGENERIC_B
+#define ZB_KGENERIC_B 128
+#define ZB_KGENERIC_R 16
+#endif
+using KGeneric = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R>; // everything else in the subset
 using KMsg = KCfg<128, 12, 16, 16, true>;  // partitions with message catch events (config 5)
 
 template <class K>
@@ -1674,23 +1686,24 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
 #ifdef ZB_STAMPS
   unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0};
 #endif
-  for (uint32_t i = threadIdx.x; i < P.prog_words; i += K::B) prog[i] = P.prog[i];
-  __syncthreads();
-
   const uint32_t n_chunks = (P.n_launch + K::B - 1) / K::B;
   const uint32_t G = gridDim.x;
   const uint32_t lane = threadIdx.x & 63;
   Counters acc = {0, 0, 0, 0, 0, 0};
 
+  // the first commands are requested before the program is staged, so the two latencies overlap
+  // (the chain program -> command -> instance rows becomes max(program, command) -> rows)
   uint32_t c = blockIdx.x;
   uint32_t ci1 = cmd_index<K>(P, c);
   uint4 cw1 = load_cmd(P, ci1);
-  uint4 h1;
-  uint2 s1;
-  load_rows(P, ci1, cw1, h1, s1);
   uint32_t ci2 = cmd_index<K>(P, c + G);
   uint4 cw2 = load_cmd(P, ci2);
   uint32_t ci3 = cmd_index<K>(P, c + 2 * G);
+  for (uint32_t i = threadIdx.x; i < P.prog_words; i += K::B) prog[i] = P.prog[i];
+  uint4 h1;
+  uint2 s1;
+  load_rows(P, ci1, cw1, h1, s1);
+  __syncthreads();
   consume(ci1); consume(cw1); consume(h1); consume(s1); consume(cw2); consume(ci3);
 #ifdef ZB_STAMPS
   { const uint32_t u = __builtin_amdgcn_readfirstlane(cw1.x + h1.x + s1.x);
