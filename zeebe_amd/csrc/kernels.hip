@@ -1807,6 +1807,23 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
         }
       }
       __syncthreads();  // the next chunk reuses the stage columns and the owner map
+    } else if (!K::REG && !K::M && total <= (uint32_t)(K::T * K::B * 8)) {
+      // long batches (rows j >= R in the global overflow rows): the same owner map over the whole
+      // run, one record per thread and iteration, rows j >= R fetched from the overflow rows
+      // (L2-resident, just written); the stores stay contiguous
+      uint32_t* lci = q_base + K::B;  // FIFO region, idle: window index of each lane's command
+      pre[threadIdx.x] = my_off;
+      lci[threadIdx.x] = ci;
+      for (uint32_t j = 0; j < my_nrec; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
+      __syncthreads();
+      for (uint32_t o = threadIdx.x; o < total; o += K::B) {
+        const uint32_t l = own[o], j = o - pre[l];
+        uint2 r;
+        if (j < (uint32_t)K::R) r = stage_base[j * K::B + l];
+        else r = overflow_row(P, lci[l], j);
+        out[o] = r;
+      }
+      __syncthreads();
     } else {
       // records in overflow rows, or more than the owner map covers: every lane stores its own
       for (uint32_t j = 0; j < my_nrec; ++j)
