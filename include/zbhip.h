@@ -466,6 +466,17 @@ typedef struct zbhip_log_window {
 int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n, const zbhip_log_window* w,
                         uint8_t* out, size_t cap, size_t* used);
 
+/* ---- zb-db byte encoding of the state ---------------------------------------
+ * The partition state as RocksDB entries: key = 8-byte big-endian ZbColumnFamilies ordinal +
+ * DbLong / DbString / DbInt parts, value = DbNil / DbLong / DbInt or the msgpack of the state
+ * object (ElementInstance, VariableInstance, EventScopeInstance, JobRecordValue, JobStateValue,
+ * NextValue).  Message-correlation column families are not encoded yet (skipped). */
+typedef void (*zbhip_db_sink)(void* ctx, uint32_t column_family, const uint8_t* key, size_t key_len,
+                              const uint8_t* value, size_t value_len);
+int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx);
+/* One canonical row of zbhip_export_state -> its entry; 1 = emitted, 0 = column family not encoded. */
+int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char* row, zbhip_db_sink sink, void* ctx);
+
 /* Library build information ("gfx950 …"). */
 const char* zbhip_build_info(void);
 

@@ -138,6 +138,8 @@ def write_object(schema, values, w=None):
             w.integer(v)
         elif kind == "bin":
             w.binary(v)
+        elif kind == "bool":
+            w.boolean(v)
         elif kind == "raw":
             w.b += v
         elif kind == "array":

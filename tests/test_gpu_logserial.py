@@ -1,11 +1,13 @@
 """Log bytes of the GPU path: records drained from libzbhip.so, serialised by the partition's own
 serializer (zbhip_handle_serializer), equal byte for byte to the oracle's serialisation
-(oracle/logserial.py) of the CPU engine's records for the same windows."""
+(oracle/logserial.py) of the CPU engine's records for the same windows; and the zb-db bytes of the
+GPU-held state (zbhip_export_state_db) equal to oracle/statedb.py's encoding of the CPU engine's."""
 import numpy as np
 import pytest
 
 from helpers import amount_docs, complete_commands, create_commands, process_xml
 from oracle import logserial as LS
+from oracle import statedb as SD
 from oracle.oracle import Oracle
 from test_logserial import check_entries, with_reason_codes
 from zeebe_amd import abi, bpmn
@@ -55,6 +57,10 @@ class Pair:
         codes = with_reason_codes(want_recs, self.orc)
         assert np.array_equal(codes["reason"], got_recs["reason"])
         assert np.array_equal(codes["reason_arg"], got_recs["reason_arg"])
+        # zb-db bytes of the state the GPU holds == the oracle's encoding of the CPU engine's state
+        strings = self.orc.strings()
+        assert self.part.state_db() == SD.encode_rows(self.orc.state(), self.orc.process_tables(),
+                                                      lambda i: strings[i])
         self.source_base += len(cmds)
         self.doc_base += len(docs)
         self.position = first + len(got_recs)

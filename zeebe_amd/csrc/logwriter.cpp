@@ -494,3 +494,172 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
   *used = off;
   return off <= cap || !out ? ZBHIP_OK : ZBHIP_ENOMEM;
 }
+
+// ---- zb-db byte encoding of the exported state ----------------------------
+// One canonical state row of zbhip_export_state -> its RocksDB entry: key = 8-byte big-endian
+// column-family ordinal (ColumnFamilyContext.writeKey; ordinals = ZbColumnFamilies.java positions)
+// + DbLong / DbString / DbInt parts (zb-db/.../impl/DbLong.java, DbString.java, DbInt.java: big
+// endian, strings with a 4-byte length), value = DbNil (0xFF), DbLong / DbInt or the msgpack of the
+// state's UnpackedObject (ElementInstance.java:23-55 + IndexedRecord.java:22-29, VariableInstance,
+// EventScopeInstance, JobRecordValue, JobStateValue, NextValue).
+namespace {
+
+void dbl(Bytes& b, int64_t v) { be64(b, (uint64_t)v); }
+void dbs(Bytes& b, const std::string& s) { be32(b, (uint32_t)s.size()); b.append(s); }
+void cf_prefix(Bytes& b, uint32_t cf) { be64(b, cf); }
+
+std::vector<std::string> split(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  size_t a = 0;
+  for (;;) {
+    const size_t p = s.find(sep, a);
+    out.push_back(s.substr(a, p == std::string::npos ? std::string::npos : p - a));
+    if (p == std::string::npos) return out;
+    a = p + 1;
+  }
+}
+std::unordered_map<std::string, std::string> fields_of(const std::string& s) {
+  std::unordered_map<std::string, std::string> m;
+  for (auto& kv : split(s, ',')) {
+    const size_t e = kv.find('=');
+    m[kv.substr(0, e)] = e == std::string::npos ? "" : kv.substr(e + 1);
+  }
+  return m;
+}
+int64_t ll(const std::string& s) { return strtoll(s.c_str(), nullptr, 10); }
+
+const char* pi_intent_name(int s) {
+  switch (s) {
+    case ZBHIP_PI_SEQUENCE_FLOW_TAKEN: return "SEQUENCE_FLOW_TAKEN";
+    default: return state_text(s);
+  }
+}
+
+}  // namespace
+
+extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char* row, zbhip_db_sink sink, void* ctx) {
+  if (!s || !row || !sink) return ZBHIP_EINVAL;
+  const std::vector<std::string> p = split(row, '|');
+  const std::string& cf = p[0];
+  Bytes k, v;
+  uint32_t ord = 0;
+  auto need = [&](size_t n) { return p.size() >= n; };
+  if (cf == "KEY" && need(3)) {  // NextValueManager: DbString "latestKey" -> NextValue
+    ord = 1;
+    cf_prefix(k, ord); dbs(k, p[1]);
+    mp_map(v, 1); key(v, "nextValue"); mp_int(v, ll(p[2]));
+  } else if (cf == "ELEMENT_INSTANCE_KEY" && need(3)) {
+    ord = 7;
+    auto f = fields_of(p[2]);
+    const int64_t def = ll(f["processDefinitionKey"]);
+    const SerProcess* P = nullptr;
+    for (auto& q : s->procs)
+      if (q.def_key == def) { P = &q; break; }
+    if (!P) return ZBHIP_EINVAL;
+    const int64_t ek = ll(p[1]);
+    cf_prefix(k, ord); dbl(k, ek);
+    mp_map(v, 11);  // ElementInstance.java:44-54
+    key(v, "parentKey"); mp_int(v, ll(f["parentKey"]));
+    key(v, "childCount"); mp_int(v, ll(f["childCount"]));
+    key(v, "childActivatedCount"); mp_int(v, ll(f["childActivatedCount"]));
+    key(v, "childCompletedCount"); mp_int(v, ll(f["childCompletedCount"]));
+    key(v, "childTerminatedCount"); mp_int(v, ll(f["childTerminatedCount"]));
+    key(v, "jobKey"); mp_int(v, ll(f["jobKey"]));
+    key(v, "multiInstanceLoopCounter"); mp_int(v, ll(f["multiInstanceLoopCounter"]));
+    key(v, "interruptingElementId"); mp_str(v, f["interruptingElementId"]);
+    key(v, "calledChildInstanceKey"); mp_int(v, ll(f["calledChildInstanceKey"]));
+    key(v, "elementRecord");
+    mp_map(v, 3);  // IndexedRecord.java:29
+    key(v, "key"); mp_int(v, ek);
+    key(v, "state"); key(v, pi_intent_name((int)ll(f["state"])));
+    key(v, "processInstanceRecord");
+    mp_map(v, 11);  // ProcessInstanceRecord.java:63-73
+    key(v, "bpmnElementType"); key(v, element_type_name((uint32_t)ll(f["bpmnElementType"])));
+    key(v, "elementId"); mp_str(v, f["elementId"]);
+    key(v, "bpmnProcessId"); mp_str(v, P->bpmn_id);
+    key(v, "version"); mp_int(v, P->version);
+    key(v, "processDefinitionKey"); mp_int(v, P->def_key);
+    key(v, "processInstanceKey"); mp_int(v, ll(f["processInstanceKey"]));
+    key(v, "flowScopeKey"); mp_int(v, ll(f["flowScopeKey"]));
+    key(v, "bpmnEventType"); key(v, event_type_name((uint32_t)ll(f["bpmnEventType"])));
+    key(v, "parentProcessInstanceKey"); mp_int(v, -1);
+    key(v, "parentElementInstanceKey"); mp_int(v, -1);
+    key(v, "tenantId"); key(v, kTenant);
+    key(v, "activeSequenceFlows"); mp_int(v, ll(f["activeSequenceFlows"]));
+  } else if (cf == "ELEMENT_INSTANCE_PARENT_CHILD" && need(3)) {
+    ord = 6;
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbl(k, ll(p[2]));
+    v.push_back((char)0xff);
+  } else if (cf == "ELEMENT_INSTANCE_CHILD_PARENT" && need(3)) {
+    ord = 9;
+    cf_prefix(k, ord); dbl(k, ll(p[1]));
+    dbl(v, ll(p[2]));
+  } else if (cf == "NUMBER_OF_TAKEN_SEQUENCE_FLOWS" && need(5)) {
+    ord = 8;
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbs(k, p[2]); dbs(k, p[3]);
+    be32(v, (uint32_t)ll(p[4]));
+  } else if (cf == "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY" && need(3)) {
+    ord = 55;
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbl(k, ll(p[2]));
+    v.push_back((char)0xff);
+  } else if (cf == "VARIABLES" && need(4)) {
+    ord = 10;
+    auto f = fields_of(p[3]);
+    zbhip_doc_entry d{};
+    d.type = (uint8_t)ll(f["type"]);
+    d.value = ll(f["value"]);
+    Bytes val;
+    if (!doc_value(s, d, val)) return ZBHIP_EUNSUPP;
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbs(k, p[2]);
+    mp_map(v, 2);  // VariableInstance.java:22
+    key(v, "key"); mp_int(v, ll(f["key"]));
+    key(v, "value"); mp_bin(v, val);
+  } else if (cf == "EVENT_SCOPE" && need(3)) {
+    ord = 37;
+    auto f = fields_of(p[2]);
+    cf_prefix(k, ord); dbl(k, ll(p[1]));
+    mp_map(v, 4);  // EventScopeInstance.java:32-35
+    key(v, "accepting"); v.push_back((char)(f["accepting"] == "1" ? 0xc3 : 0xc2));
+    key(v, "interrupting"); mp_array(v, 0);
+    key(v, "boundaryElementIds"); mp_array(v, 0);
+    key(v, "interrupted"); v.push_back((char)(f["interrupted"] == "1" ? 0xc3 : 0xc2));
+  } else if (cf == "JOBS" && need(3)) {
+    ord = 16;
+    auto f = fields_of(p[2]);
+    cf_prefix(k, ord); dbl(k, ll(p[1]));
+    mp_map(v, 1);  // JobRecordValue.java:21 -> JobRecord stored without variables (DbJobState.create)
+    key(v, "jobRecord");
+    mp_map(v, 17);
+    key(v, "deadline"); mp_int(v, -1);
+    key(v, "worker"); key(v, "");
+    key(v, "retries"); mp_int(v, ll(f["retries"]));
+    key(v, "retryBackoff"); mp_int(v, 0);
+    key(v, "recurringTime"); mp_int(v, -1);
+    key(v, "type"); mp_str(v, f["type"]);
+    key(v, "customHeaders"); v += kEmptyDoc;
+    key(v, "variables"); mp_bin(v, kEmptyDoc);
+    key(v, "errorMessage"); key(v, "");
+    key(v, "errorCode"); key(v, "");
+    key(v, "bpmnProcessId"); mp_str(v, f["bpmnProcessId"]);
+    key(v, "processDefinitionVersion"); mp_int(v, ll(f["processDefinitionVersion"]));
+    key(v, "processDefinitionKey"); mp_int(v, ll(f["processDefinitionKey"]));
+    key(v, "processInstanceKey"); mp_int(v, ll(f["processInstanceKey"]));
+    key(v, "elementId"); mp_str(v, f["elementId"]);
+    key(v, "elementInstanceKey"); mp_int(v, ll(f["elementInstanceKey"]));
+    key(v, "tenantId"); mp_str(v, f["tenantId"]);
+  } else if (cf == "JOB_STATES" && need(3)) {
+    ord = 17;
+    cf_prefix(k, ord); dbl(k, ll(p[1]));
+    mp_map(v, 1);  // JobStateValue.java:21
+    key(v, "jobState"); mp_str(v, p[2]);
+  } else if (cf == "JOB_ACTIVATABLE" && need(4)) {
+    ord = 76;  // DbTenantAwareKey(tenant, [type, jobKey], SUFFIX)
+    cf_prefix(k, ord); dbs(k, p[1]); dbl(k, ll(p[3])); dbs(k, p[2]);
+    v.push_back((char)0xff);
+  } else {
+    return 0;  // message-correlation column families: not encoded yet
+  }
+  sink(ctx, ord, reinterpret_cast<const uint8_t*>(k.data()), k.size(), reinterpret_cast<const uint8_t*>(v.data()),
+       v.size());
+  return 1;
+}

@@ -1061,6 +1061,27 @@ int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* r, char* buf, si
 
 zbhip_serializer* zbhip_handle_serializer(zbhip_handle* h) { return h ? h->ser : nullptr; }
 
+namespace {
+struct DbExport {
+  zbhip_serializer* ser;
+  zbhip_db_sink sink;
+  void* ctx;
+  int rc;
+};
+void db_row(void* c, const char* row) {
+  auto* e = static_cast<DbExport*>(c);
+  const int r = zbhip_serializer_encode_state_row(e->ser, row, e->sink, e->ctx);
+  if (r < 0 && e->rc == ZBHIP_OK) e->rc = r;
+}
+}  // namespace
+
+int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx) {
+  if (!h || !sink) return ZBHIP_EINVAL;
+  DbExport e{h->ser, sink, ctx, ZBHIP_OK};
+  const int rc = zbhip_export_state(h, db_row, &e);
+  return rc < 0 ? rc : e.rc;
+}
+
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal) {
   if (!h || !instance || !ordinal) return ZBHIP_EINVAL;
   const int64_t v = key - ((int64_t)h->cfg.partition_id << 51);

@@ -97,6 +97,13 @@ class Partition:
     def intern(self, name):
         return check(self.L.zbhip_intern(self.h, name.encode()))
 
+    def state_db(self):
+        """The partition state as zb-db entries (column family ordinal, key bytes, value bytes)."""
+        from .logwriter import _db_collector
+        out, cb = _db_collector()
+        check(self.L.zbhip_export_state_db(self.h, cb, None), "zbhip_export_state_db")
+        return sorted(out)
+
     def log_serializer(self):
         """The partition's log serialiser (follows its deployments and dictionaries)."""
         from .logwriter import LogSerializer

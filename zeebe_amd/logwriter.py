@@ -12,7 +12,16 @@ import ctypes as C
 import numpy as np
 
 from . import abi
-from .native import check, load
+from .native import DB_SINK, check, load
+
+
+def _db_collector():
+    rows = []
+
+    def sink(_ctx, cf, k, kn, v, vn):
+        rows.append((cf, C.string_at(k, kn), C.string_at(v, vn)))
+
+    return rows, DB_SINK(sink)
 
 
 class LogSerializer:
@@ -58,6 +67,13 @@ class LogSerializer:
     def intern_string(self, value):
         b = value.encode() if isinstance(value, str) else bytes(value)
         return check(self.L.zbhip_serializer_intern_string(self.s, b, len(b)))
+
+    def encode_state_rows(self, rows):
+        """zb-db entries (column family ordinal, key bytes, value bytes) of canonical state rows."""
+        out, cb = _db_collector()
+        for r in rows:
+            check(self.L.zbhip_serializer_encode_state_row(self.s, r.encode(), cb, None), "encode_state_row")
+        return sorted(out)
 
     def set_broker_version(self, major, minor, patch):
         check(self.L.zbhip_serializer_set_broker_version(self.s, major, minor, patch))

@@ -25,7 +25,8 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_outbox_copy", "zbhip_submit_xparts_device", "zbhip_string_partitions",
            "zbhip_serializer_new", "zbhip_serializer_free", "zbhip_serializer_deploy", "zbhip_serializer_intern",
            "zbhip_serializer_intern_string", "zbhip_serializer_set_broker_version",
-           "zbhip_serializer_rejection_reason", "zbhip_handle_serializer", "zbhip_serialize_log"]
+           "zbhip_serializer_rejection_reason", "zbhip_handle_serializer", "zbhip_serialize_log",
+           "zbhip_export_state_db", "zbhip_serializer_encode_state_row"]
 
 
 class ZbhipError(RuntimeError):
@@ -35,6 +36,8 @@ class ZbhipError(RuntimeError):
 
 
 STATE_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p)
+DB_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_uint8),
+                      C.c_size_t)
 
 _lib = None
 
@@ -97,6 +100,8 @@ def load():
     L.zbhip_handle_serializer.argtypes = [vp]
     L.zbhip_handle_serializer.restype = vp
     L.zbhip_serialize_log.argtypes = [vp, vp, sz, C.POINTER(abi.LogWindow), vp, sz, C.POINTER(sz)]
+    L.zbhip_export_state_db.argtypes = [vp, DB_SINK, vp]
+    L.zbhip_serializer_encode_state_row.argtypes = [vp, C.c_char_p, DB_SINK, vp]
     L.zbhip_build_info.argtypes = []
     L.zbhip_build_info.restype = C.c_char_p
     _lib = L
