@@ -68,3 +68,20 @@ def test_state_bytes_fork_join_counters():
 
     _drive_simple(run, 20, mutate=one_branch_per_window)
     assert SD.CF["NUMBER_OF_TAKEN_SEQUENCE_FLOWS"] in run.cfs
+
+
+def test_key_encodings_golden():
+    import json
+    import os
+    from helpers import GOLDEN
+    d = json.load(open(os.path.join(GOLDEN, "zbdb_keys.json")))
+    for name, op, arg, want in d["vectors"]:
+        if op == "dbstr":
+            got = SD.dbstr(arg)
+        elif op == "dblong":
+            got = SD.dblong(arg)
+        elif op == "tenant_prefix":
+            got = SD.dbstr(arg[0]) + SD.dbstr(arg[1])
+        else:
+            got = SD.dbstr(arg[1]) + SD.dbstr(arg[0])
+        assert got.hex() == want, name
