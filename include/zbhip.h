@@ -433,7 +433,8 @@ int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, 
  * skipProcessing for processed follow-up commands, position, sourcePosition, key, timestamp,
  * metadata length) + SBE RecordMetadata (protocol.xml:137-152, schema version 4) + msgpack record
  * value (ObjectValue.java:78-84; ProcessInstanceRecord, JobRecord, VariableRecord,
- * ProcessEventRecord, ProcessInstanceCreationRecord).  Host code (no device work).
+ * ProcessEventRecord, ProcessInstanceCreationRecord, MessageRecord, MessageSubscriptionRecord,
+ * ProcessMessageSubscriptionRecord).  Host code (no device work).
  * A serializer holds the deployment's constant msgpack runs and the name / value dictionaries; a
  * handle owns one kept in step with zbhip_deploy / zbhip_intern / zbhip_intern_string
  * (zbhip_handle_serializer), a standalone one is built with the same calls in the same order. */
@@ -459,10 +460,12 @@ typedef struct zbhip_log_window {
   const int64_t* source_positions; /* log position of each command of the window (sourcePosition) */
   int64_t first_position;          /* position of the first serialised record (the sequencer's next) */
   int64_t timestamp;               /* the batches' timestamp (ms) */
+  const int64_t* source_timestamps;/* timestamp of each window command (MESSAGE deadline =
+                                      PUBLISH timestamp + timeToLive); NULL = timestamp */
 } zbhip_log_window;
 
 /* Serialises n drained records (in drain order) into out.  *used = bytes needed; ZBHIP_ENOMEM if
- * cap is short (out == NULL: size query).  Message records: ZBHIP_EUNSUPP. */
+ * cap is short (out == NULL: size query). */
 int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n, const zbhip_log_window* w,
                         uint8_t* out, size_t cap, size_t* used);
 

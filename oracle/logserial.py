@@ -10,7 +10,8 @@ Only tests/ may import this module.  It restates, in plain Python:
     (PackedValue.java:28-30), ArrayValue -> array header + items (ArrayValue.java:31-35);
   * the record values the engine writes for the path (protocol-impl/.../record/value/...):
     ProcessInstanceRecord.java:62-74, JobRecord.java:39-83, VariableRecord.java:25-41,
-    ProcessEventRecord.java:25-42, ProcessInstanceCreationRecord.java:32-55, with the field values
+    ProcessEventRecord.java:25-42, ProcessInstanceCreationRecord.java:32-55, MessageRecord.java:37-43,
+    MessageSubscriptionRecord.java:40-48, ProcessMessageSubscriptionRecord.java:44-54, with the field values
     of BpmnStateTransitionBehavior.java:243-339, CreateProcessInstanceProcessor.java:129-158,319-330,
     BpmnJobBehavior.java:194-218,359-400 (jobRecord reused, variables EMPTY_DOCUMENT, NO_HEADERS),
     JobCompleteProcessor.java:75-92, EventTriggerBehavior.java:148-166, EventHandle.java:151-158,
@@ -180,6 +181,22 @@ PROCESS_INSTANCE_CREATION = [
     ("bpmnProcessId", "str", ""), ("processDefinitionKey", "long", -1), ("processInstanceKey", "long", -1),
     ("version", "int", -1), ("variables", "bin", EMPTY_DOCUMENT), ("fetchVariables", "array", []),
     ("startInstructions", "array", []), ("tenantId", "str", "<default>")]
+# MessageRecord.java:37-43 (name, correlationKey, timeToLive have no default)
+MESSAGE = [
+    ("name", "str", NO_DEFAULT), ("correlationKey", "str", NO_DEFAULT), ("timeToLive", "long", NO_DEFAULT),
+    ("variables", "bin", EMPTY_DOCUMENT), ("messageId", "str", ""), ("deadline", "long", -1),
+    ("tenantId", "str", "<default>")]
+# MessageSubscriptionRecord.java:40-48
+MESSAGE_SUBSCRIPTION = [
+    ("processInstanceKey", "long", NO_DEFAULT), ("elementInstanceKey", "long", NO_DEFAULT), ("messageKey", "long", -1),
+    ("messageName", "str", ""), ("correlationKey", "str", ""), ("interrupting", "bool", True),
+    ("bpmnProcessId", "str", ""), ("variables", "bin", EMPTY_DOCUMENT), ("tenantId", "str", "<default>")]
+# ProcessMessageSubscriptionRecord.java:44-54
+PROCESS_MESSAGE_SUBSCRIPTION = [
+    ("subscriptionPartitionId", "int", NO_DEFAULT), ("processInstanceKey", "long", NO_DEFAULT),
+    ("elementInstanceKey", "long", NO_DEFAULT), ("messageKey", "long", -1), ("messageName", "str", ""),
+    ("variables", "bin", EMPTY_DOCUMENT), ("interrupting", "bool", True), ("bpmnProcessId", "str", ""),
+    ("correlationKey", "str", ""), ("elementId", "str", ""), ("tenantId", "str", "<default>")]
 # AuthInfo.java: format (enum, UNKNOWN), authData ("")
 AUTH_INFO = [("format", "enum", "UNKNOWN"), ("authData", "str", "")]
 
@@ -266,6 +283,8 @@ def log_entry(key, metadata, value, position, source_position, timestamp, proces
 # ---- the path's records -----------------------------------------------------------------------------
 RT_EVENT, RT_COMMAND, RT_REJECTION = 0, 1, 2
 VT_JOB, VT_PI, VT_VARIABLE, VT_PIC, VT_PE = 0, 5, 17, 19, 24
+VT_MESSAGE, VT_MS, VT_PMS = 10, 11, 12
+NO_STRING, NO_NAME = 0xFFFFFFFF, 0xFFFF
 
 
 class Tables:
@@ -277,9 +296,33 @@ class Tables:
         self.processes, self.name, self.string_value = processes, name, string_value
 
 
-def record_value(r, tables, docs_of_source, doc_entry):
+def _message_value(r, vt, tables, timestamp):
+    """Values of the message-correlation records (the drained record carries every field the
+    reference record holds: MessagePublishProcessor.java:100-125 deadline = the PUBLISH command's
+    timestamp + timeToLive (0 in the subset), SubscriptionCommandSender / the subscription
+    processors for the others; message variables are empty in the subset)."""
+    name = lambda i: tables.name(i) if i != NO_NAME else ""  # noqa: E731
+    corr = int(r["correlation_key"])
+    corr_s = tables.string_value(corr) if corr != NO_STRING else b""
+    if vt == VT_MESSAGE:
+        return write_object(MESSAGE, dict(name=name(int(r["message_name"])), correlationKey=corr_s, timeToLive=0,
+                                          deadline=timestamp))
+    common = dict(processInstanceKey=int(r["process_instance_key"]), elementInstanceKey=int(r["scope_key"]),
+                  messageKey=int(r["message_key"]), messageName=name(int(r["message_name"])), correlationKey=corr_s,
+                  interrupting=bool(r["interrupting"]), bpmnProcessId=name(int(r["bpmn_process_id"])))
+    if vt == VT_MS:
+        return write_object(MESSAGE_SUBSCRIPTION, common)
+    p, e = int(r["process_idx"]), int(r["element_idx"])
+    elem = tables.processes[p]["elements"][e][2] if p >= 0 and e >= 0 else ""
+    return write_object(PROCESS_MESSAGE_SUBSCRIPTION, dict(common, subscriptionPartitionId=int(r["partition"]),
+                                                           elementId=elem))
+
+
+def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
     """msgpack record value of one drained record (fields of zbhip_record)."""
     vt, rt = int(r["value_type"]), int(r["record_type"])
+    if vt in (VT_MESSAGE, VT_MS, VT_PMS):
+        return _message_value(r, vt, tables, timestamp)
     p = tables.processes[int(r["process_idx"])] if int(r["process_idx"]) >= 0 else None
     el = p["elements"][int(r["element_idx"])] if p is not None and int(r["element_idx"]) >= 0 else None
     src_doc = document_bytes(docs_of_source(int(r["source_index"])), tables.name, tables.string_value)
@@ -317,7 +360,7 @@ def record_value(r, tables, docs_of_source, doc_entry):
 
 
 def serialize(records, tables, docs_of_source, doc_entry, reason_text, first_position, source_position, timestamp,
-              broker_version=(8, 4, 0)):
+              broker_version=(8, 4, 0), source_timestamp=None):
     """The log bytes of the records' batches: records of one source command form one sequenced
     batch (sourcePosition = that command's position), positions consecutive from first_position."""
     out = bytearray()
@@ -326,7 +369,9 @@ def serialize(records, tables, docs_of_source, doc_entry, reason_text, first_pos
         rej = int(r["rejection_type"]) if rt == RT_REJECTION else REJECTION_NULL
         reason = reason_text(i).encode() if rt == RT_REJECTION else b""
         md = record_metadata(rt, int(r["value_type"]), int(r["intent"]), rej, reason, broker_version)
-        value = record_value(r, tables, docs_of_source, doc_entry)
+        si = int(r["source_index"])
+        value = record_value(r, tables, docs_of_source, doc_entry,
+                             source_timestamp(si) if source_timestamp else timestamp)
         out += log_entry(int(r["key"]), md, value, first_position + i, source_position(int(r["source_index"])),
                          timestamp, rt == RT_COMMAND)
     return bytes(out)

@@ -80,7 +80,8 @@ STATES = {"ELEMENT_ACTIVATING": 2, "ELEMENT_ACTIVATED": 3, "ELEMENT_COMPLETING":
 REASONS = [("Expected to be able to activate parallel gateway", 1),
            ("Expected flow scope instance with key", 2), ("Expected flow scope instance to be in state", 3),
            ("Expected element instance with key", 4), ("Expected element instance to be in state", 5),
-           ("Expected to complete job with key", 6)]
+           ("Expected to complete job with key", 6), ("Expected to open a new message subscription", 7),
+           ("Expected to correlate subscription for element", 12)]
 
 
 def with_reason_codes(recs, orc):
@@ -233,10 +234,91 @@ def test_serializer_job_documents_strings_and_rejections():
     _drive_simple(run, 24, mutate=mutate)
 
 
-def test_serializer_rejects_message_records():
+def test_serializer_rejects_unknown_value_types():
     run = Run([bpmn.linear_process(1)])
     recs = run.window(create_commands(1, 0))
     bad = recs[:1].copy()
-    bad["value_type"] = abi.VT_MESSAGE
+    bad["value_type"] = 4  # DEPLOYMENT: outside the path
     with pytest.raises(Exception):
         run.ser.serialize(bad, create_commands(1, 0), source_base=run.source_base - 1)
+
+
+# ---- config 5: message-correlation records -------------------------------------------------------
+class SerializingOracleAdapter:
+    """OracleAdapter that also serialises every window of every partition with a standalone
+    product serializer and with the oracle restatement, and compares the bytes."""
+
+    def __init__(self):
+        from helpers import OracleAdapter
+        self.base = OracleAdapter
+        self.ser = {}
+        self.windows = 0
+
+    def _s(self, p):
+        if id(p) not in self.ser:
+            self.ser[id(p)] = [LogSerializer(), 0, 0, 1]
+        return self.ser[id(p)]
+
+    def _sync_names(self, p):
+        s = self._s(p)[0]
+        for n in p.names():
+            s.intern(n)
+
+    def deploy(self, p, xml):
+        r = self.base.deploy(p, xml)
+        assert self._s(p)[0].deploy(xml) == r
+        self._sync_names(p)
+        return r
+
+    def intern(self, p, name):
+        r = self.base.intern(p, name)
+        self._sync_names(p)
+        return r
+
+    def intern_string(self, p, v):
+        r = self.base.intern_string(p, v)
+        assert self._s(p)[0].intern_string(v) == r
+        return r
+
+    def window(self, p, cmds, docs, xparts):
+        recs, ob = self.base.window(p, cmds, docs, xparts)
+        st = self._s(p)
+        ser, sb, db, position = st
+        docs = docs if docs is not None else abi.make_docs(0)
+        recs_c = with_reason_codes(recs, p)
+        pos = position + 2 * np.arange(len(cmds), dtype=np.int64)
+        ts = 1700000000000 + 7 * np.arange(len(cmds), dtype=np.int64)
+        first = int(pos[-1]) + 1
+        got = ser.serialize(recs_c, cmds, docs, sb, db, pos, first, 1700000000123, ts)
+        names, strings = p.names(), p.strings()
+        tables = LS.Tables(p.process_tables(), lambda i: names[i], lambda i: strings[i])
+
+        def docs_of_source(si):
+            c = cmds[si - sb]
+            return docs[int(c["doc_begin"]):int(c["doc_begin"]) + int(c["doc_count"])] if len(docs) else docs[:0]
+
+        want = LS.serialize(recs_c, tables, docs_of_source, lambda a: docs[a - db], p.reason, first,
+                            lambda si: int(pos[si - sb]), 1700000000123, source_timestamp=lambda si: int(ts[si - sb]))
+        assert got == want
+        check_entries(got, recs_c, first, pos, sb)
+        st[1], st[2], st[3] = sb + len(cmds), db + len(docs), first + len(recs)
+        self.windows += 1
+        return recs, ob
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_serializer_message_correlation(P):
+    from helpers import MessageCluster
+    from oracle.oracle import subscription_partition
+    ad = SerializingOracleAdapter()
+    cl = MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], ad,
+                        bpmn.message_catch_process())
+    n = 12
+    keys = [["k-%d-%d" % (p, i) for i in range(n)] for p in range(1, P + 1)]
+    flat = [k for ks in keys for k in ks]
+    ids = cl.intern_keys(flat)
+    cl.create(n, [ids[(p - 1) * n:p * n] for p in range(1, P + 1)])
+    cl.publish(ids, [subscription_partition(k, P) for k in flat])
+    kinds = {int(v) for _, _, recs, _ in cl.log for v in recs["value_type"]}
+    assert {abi.VT_MESSAGE, abi.VT_MESSAGE_SUBSCRIPTION, abi.VT_PROCESS_MESSAGE_SUBSCRIPTION} <= kinds
+    assert ad.windows >= 2 * P

@@ -107,7 +107,7 @@ class XpartCmd(C.Structure):
 class LogWindow(C.Structure):  # zbhip_log_window
     _fields_ = [("cmds", C.c_void_p), ("n_cmds", C.c_size_t), ("source_base", C.c_int64), ("docs", C.c_void_p),
                 ("n_docs", C.c_size_t), ("doc_base", C.c_int64), ("source_positions", C.c_void_p),
-                ("first_position", C.c_int64), ("timestamp", C.c_int64)]
+                ("first_position", C.c_int64), ("timestamp", C.c_int64), ("source_timestamps", C.c_void_p)]
 
 
 class Config(C.Structure):

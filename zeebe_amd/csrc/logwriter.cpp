@@ -441,8 +441,58 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         key(value, "startInstructions"); mp_array(value, 0);
         key(value, "tenantId"); key(value, kTenant);
         break;
+      case ZBHIP_VT_MESSAGE:
+      case ZBHIP_VT_MESSAGE_SUBSCRIPTION:
+      case ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION: {
+        // the drained record carries every field of the reference record; message variables are
+        // empty in the subset; MESSAGE deadline = the PUBLISH command's timestamp + timeToLive (0)
+        // (MessagePublishProcessor.java:100-125)
+        auto name = [&](uint32_t id) -> const std::string& {
+          static const std::string empty;
+          return id != 0xFFFF && id < s->names.size() ? s->names[id] : empty;
+        };
+        static const std::string empty_s;
+        const std::string& corr =
+            r.correlation_key != ZBHIP_NO_STRING && r.correlation_key < s->strs.size() ? s->strs[r.correlation_key] : empty_s;
+        if (r.value_type == ZBHIP_VT_MESSAGE) {
+          const int64_t ts = w->source_timestamps ? w->source_timestamps[ci] : w->timestamp;
+          mp_map(value, 7);  // MessageRecord.java:37-43
+          key(value, "name"); mp_str(value, name(r.message_name));
+          key(value, "correlationKey"); mp_str(value, corr);
+          key(value, "timeToLive"); mp_int(value, 0);
+          key(value, "variables"); mp_bin(value, kEmptyDoc);
+          key(value, "messageId"); key(value, "");
+          key(value, "deadline"); mp_int(value, ts);
+          key(value, "tenantId"); key(value, kTenant);
+        } else if (r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION) {
+          mp_map(value, 9);  // MessageSubscriptionRecord.java:40-48
+          key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+          key(value, "elementInstanceKey"); mp_int(value, r.scope_key);
+          key(value, "messageKey"); mp_int(value, r.message_key);
+          key(value, "messageName"); mp_str(value, name(r.message_name));
+          key(value, "correlationKey"); mp_str(value, corr);
+          key(value, "interrupting"); value.push_back((char)(r.interrupting ? 0xc3 : 0xc2));
+          key(value, "bpmnProcessId"); mp_str(value, name(r.bpmn_process_id));
+          key(value, "variables"); mp_bin(value, kEmptyDoc);
+          key(value, "tenantId"); key(value, kTenant);
+        } else {
+          mp_map(value, 11);  // ProcessMessageSubscriptionRecord.java:44-54
+          key(value, "subscriptionPartitionId"); mp_int(value, r.partition);
+          key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+          key(value, "elementInstanceKey"); mp_int(value, r.scope_key);
+          key(value, "messageKey"); mp_int(value, r.message_key);
+          key(value, "messageName"); mp_str(value, name(r.message_name));
+          key(value, "variables"); mp_bin(value, kEmptyDoc);
+          key(value, "interrupting"); value.push_back((char)(r.interrupting ? 0xc3 : 0xc2));
+          key(value, "bpmnProcessId"); mp_str(value, name(r.bpmn_process_id));
+          key(value, "correlationKey"); mp_str(value, corr);
+          key(value, "elementId"); mp_str(value, E ? E->id : empty_s);
+          key(value, "tenantId"); key(value, kTenant);
+        }
+        break;
+      }
       default:
-        return ZBHIP_EUNSUPP;  // message records: not serialised yet
+        return ZBHIP_EUNSUPP;
     }
     // ---- SBE RecordMetadata (messageHeader + 32-byte block + 2 var-data fields) ----
     md.clear();
