@@ -473,7 +473,7 @@ int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n,
  * The partition state as RocksDB entries: key = 8-byte big-endian ZbColumnFamilies ordinal +
  * DbLong / DbString / DbInt parts, value = DbNil / DbLong / DbInt or the msgpack of the state
  * object (ElementInstance, VariableInstance, EventScopeInstance, JobRecordValue, JobStateValue,
- * NextValue).  Message-correlation column families are not encoded yet (skipped). */
+ * NextValue, MessageSubscription, ProcessMessageSubscription) -- the 15 column families of the path. */
 typedef void (*zbhip_db_sink)(void* ctx, uint32_t column_family, const uint8_t* key, size_t key_len,
                               const uint8_t* value, size_t value_len);
 int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx);

@@ -27,7 +27,11 @@ bytes, value bytes) as RocksDB holds them:
       JOB_ACTIVATABLE [[type, jobKey], tenant] -> DbNil (:87-95, PlacementType.SUFFIX);
       KEY "latestKey" -> NextValue{nextValue} (stream-platform/.../state/NextValueManager.java:32-34,
                             DbKeyGenerator.java:21).
-Message-correlation column families (config 5) are not encoded yet.  Parity of the values is
+      MESSAGE_SUBSCRIPTION_BY_KEY [eik, name] -> MessageSubscription{record, key, correlating};
+      MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY [[tenant, [name, correlationKey]], eik] -> DbNil;
+      PROCESS_SUBSCRIPTION_BY_KEY [eik, [tenant, name]] -> ProcessMessageSubscription{record, state, key};
+      MESSAGE_STATS "deadline_message_count" -> DbLong (DbMessageState.java:165-175).
+Parity of the values is
 restated from the code (no reference fixture holds zb-db bytes): "parity unpinned" beyond the
 msgpack primitives oracle/logserial.py is pinned on.
 """
@@ -37,7 +41,8 @@ from oracle import logserial as LS
 
 CF = {"KEY": 1, "ELEMENT_INSTANCE_PARENT_CHILD": 6, "ELEMENT_INSTANCE_KEY": 7, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS": 8,
       "ELEMENT_INSTANCE_CHILD_PARENT": 9, "VARIABLES": 10, "JOBS": 16, "JOB_STATES": 17, "EVENT_SCOPE": 37,
-      "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY": 55, "JOB_ACTIVATABLE": 76}
+      "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY": 55, "JOB_ACTIVATABLE": 76, "MESSAGE_SUBSCRIPTION_BY_KEY": 27,
+      "MESSAGE_STATS": 54, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY": 74, "PROCESS_SUBSCRIPTION_BY_KEY": 75}
 NIL = b"\xff"
 PI_INTENT = {1: "SEQUENCE_FLOW_TAKEN", 2: "ELEMENT_ACTIVATING", 3: "ELEMENT_ACTIVATED", 4: "ELEMENT_COMPLETING",
              5: "ELEMENT_COMPLETED", 6: "ELEMENT_TERMINATING", 7: "ELEMENT_TERMINATED"}
@@ -84,7 +89,7 @@ def encode_rows(rows, processes, string_value):
         parts = row.split("|")
         name = parts[0]
         if name not in CF:
-            continue  # message-correlation column families: not encoded yet
+            continue  # not a column family of the path
         prefix = struct.pack(">q", CF[name])
         if name == "KEY":
             out.append((CF[name], prefix + dbstr(parts[1]), LS.write_object(NEXT_VALUE, {"nextValue": int(parts[2])})))
@@ -134,6 +139,30 @@ def encode_rows(rows, processes, string_value):
         elif name == "JOB_STATES":
             out.append((CF[name], prefix + dblong(int(parts[1])),
                         LS.write_object([("jobState", "enum", LS.NO_DEFAULT)], {"jobState": parts[2]})))
+        elif name == "MESSAGE_SUBSCRIPTION_BY_KEY":  # DbMessageSubscriptionState.java:64-73, MessageSubscription.java
+            f = fields(parts[3])
+            rec = LS.write_object(LS.MESSAGE_SUBSCRIPTION, dict(
+                processInstanceKey=int(f["processInstanceKey"]), elementInstanceKey=int(parts[1]),
+                messageKey=int(f["messageKey"]), messageName=parts[2], correlationKey=f["correlationKey"],
+                interrupting=f["interrupting"] == "1", bpmnProcessId=f["bpmnProcessId"]))
+            val = LS.write_object([("record", "raw", None), ("key", "long", LS.NO_DEFAULT), ("correlating", "bool", False)],
+                                  {"record": rec, "key": int(f["key"]), "correlating": f["correlating"] == "1"})
+            out.append((CF[name], prefix + dblong(int(parts[1])) + dbstr(parts[2]), val))
+        elif name == "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY":  # :75-86, tenant PREFIX
+            out.append((CF[name], prefix + dbstr(parts[1]) + dbstr(parts[2]) + dbstr(parts[3]) + dblong(int(parts[4])),
+                        NIL))
+        elif name == "PROCESS_SUBSCRIPTION_BY_KEY":  # DbProcessMessageSubscriptionState.java:53-66
+            f = fields(parts[3])
+            rec = LS.write_object(LS.PROCESS_MESSAGE_SUBSCRIPTION, dict(
+                subscriptionPartitionId=int(f["subscriptionPartitionId"]), processInstanceKey=int(f["processInstanceKey"]),
+                elementInstanceKey=int(parts[1]), messageKey=int(f["messageKey"]), messageName=parts[2],
+                interrupting=f["interrupting"] == "1", bpmnProcessId=f["bpmnProcessId"],
+                correlationKey=f["correlationKey"], elementId=f["elementId"]))
+            val = LS.write_object([("record", "raw", None), ("state", "enum", "STATE_OPENING"), ("key", "long", LS.NO_DEFAULT)],
+                                  {"record": rec, "state": "STATE_" + f["state"], "key": int(f["key"])})
+            out.append((CF[name], prefix + dblong(int(parts[1])) + dbstr("<default>") + dbstr(parts[2]), val))
+        elif name == "MESSAGE_STATS":  # DbMessageState.java:165-175
+            out.append((CF[name], prefix + dbstr("deadline_message_count"), dblong(int(parts[2]))))
         elif name == "JOB_ACTIVATABLE":
             out.append((CF[name], prefix + dbstr(parts[1]) + dblong(int(parts[3])) + dbstr(parts[2]), NIL))
     return sorted(out)

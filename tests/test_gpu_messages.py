@@ -65,9 +65,12 @@ def assert_same_logs(gpu, orc):
 
 
 def assert_same_state(gpu, orc):
+    from oracle import statedb as SD
     for g, o in zip(gpu.parts, orc.parts):
         gs, os_ = g.state(), o.state()
         assert gs == os_, (sorted(set(gs) ^ set(os_)))[:6]
+        strings = o.strings()
+        assert g.state_db() == SD.encode_rows(os_, o.process_tables(), lambda i: strings[i])
 
 
 @pytest.mark.parametrize("case", ["remote", "local"])

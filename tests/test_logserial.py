@@ -253,6 +253,7 @@ class SerializingOracleAdapter:
         self.base = OracleAdapter
         self.ser = {}
         self.windows = 0
+        self.state_cfs = set()
 
     def _s(self, p):
         if id(p) not in self.ser:
@@ -302,6 +303,11 @@ class SerializingOracleAdapter:
         assert got == want
         check_entries(got, recs_c, first, pos, sb)
         st[1], st[2], st[3] = sb + len(cmds), db + len(docs), first + len(recs)
+        # zb-db bytes of the partition state, message column families included
+        from oracle import statedb as SD
+        rows = p.state()
+        assert ser.encode_state_rows(rows) == SD.encode_rows(rows, p.process_tables(), lambda i: strings[i])
+        self.state_cfs |= {r.split("|")[0] for r in rows}
         self.windows += 1
         return recs, ob
 
@@ -322,3 +328,4 @@ def test_serializer_message_correlation(P):
     kinds = {int(v) for _, _, recs, _ in cl.log for v in recs["value_type"]}
     assert {abi.VT_MESSAGE, abi.VT_MESSAGE_SUBSCRIPTION, abi.VT_PROCESS_MESSAGE_SUBSCRIPTION} <= kinds
     assert ad.windows >= 2 * P
+    assert {"PROCESS_SUBSCRIPTION_BY_KEY", "MESSAGE_STATS"} <= ad.state_cfs or P == 1

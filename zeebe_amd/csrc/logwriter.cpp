@@ -551,7 +551,9 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
 // + DbLong / DbString / DbInt parts (zb-db/.../impl/DbLong.java, DbString.java, DbInt.java: big
 // endian, strings with a 4-byte length), value = DbNil (0xFF), DbLong / DbInt or the msgpack of the
 // state's UnpackedObject (ElementInstance.java:23-55 + IndexedRecord.java:22-29, VariableInstance,
-// EventScopeInstance, JobRecordValue, JobStateValue, NextValue).
+// EventScopeInstance, JobRecordValue, JobStateValue, NextValue, MessageSubscription,
+// ProcessMessageSubscription).  Rows are split at '|' and ',': correlation keys / names holding
+// those characters are outside what this encoder reads back.
 namespace {
 
 void dbl(Bytes& b, int64_t v) { be64(b, (uint64_t)v); }
@@ -706,8 +708,54 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     ord = 76;  // DbTenantAwareKey(tenant, [type, jobKey], SUFFIX)
     cf_prefix(k, ord); dbs(k, p[1]); dbl(k, ll(p[3])); dbs(k, p[2]);
     v.push_back((char)0xff);
+  } else if (cf == "MESSAGE_SUBSCRIPTION_BY_KEY" && need(4)) {
+    ord = 27;  // [eik, messageName] -> MessageSubscription{record, key, correlating} (DbMessageSubscriptionState.java:64-73)
+    auto f = fields_of(p[3]);
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbs(k, p[2]);
+    mp_map(v, 3);
+    key(v, "record");
+    mp_map(v, 9);  // MessageSubscriptionRecord.java:40-48
+    key(v, "processInstanceKey"); mp_int(v, ll(f["processInstanceKey"]));
+    key(v, "elementInstanceKey"); mp_int(v, ll(p[1]));
+    key(v, "messageKey"); mp_int(v, ll(f["messageKey"]));
+    key(v, "messageName"); mp_str(v, p[2]);
+    key(v, "correlationKey"); mp_str(v, f["correlationKey"]);
+    key(v, "interrupting"); v.push_back((char)(f["interrupting"] == "1" ? 0xc3 : 0xc2));
+    key(v, "bpmnProcessId"); mp_str(v, f["bpmnProcessId"]);
+    key(v, "variables"); mp_bin(v, kEmptyDoc);
+    key(v, "tenantId"); key(v, kTenant);
+    key(v, "key"); mp_int(v, ll(f["key"]));
+    key(v, "correlating"); v.push_back((char)(f["correlating"] == "1" ? 0xc3 : 0xc2));
+  } else if (cf == "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY" && need(5)) {
+    ord = 74;  // [[tenant, [name, correlationKey]] PREFIX, eik] -> DbNil (:75-86)
+    cf_prefix(k, ord); dbs(k, p[1]); dbs(k, p[2]); dbs(k, p[3]); dbl(k, ll(p[4]));
+    v.push_back((char)0xff);
+  } else if (cf == "PROCESS_SUBSCRIPTION_BY_KEY" && need(4)) {
+    ord = 75;  // [eik, [tenant, messageName] PREFIX] -> ProcessMessageSubscription{record, state, key}
+    auto f = fields_of(p[3]);  // (DbProcessMessageSubscriptionState.java:53-66, ProcessMessageSubscription.java:19-26)
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbs(k, kTenant); dbs(k, p[2]);
+    mp_map(v, 3);
+    key(v, "record");
+    mp_map(v, 11);  // ProcessMessageSubscriptionRecord.java:44-54
+    key(v, "subscriptionPartitionId"); mp_int(v, ll(f["subscriptionPartitionId"]));
+    key(v, "processInstanceKey"); mp_int(v, ll(f["processInstanceKey"]));
+    key(v, "elementInstanceKey"); mp_int(v, ll(p[1]));
+    key(v, "messageKey"); mp_int(v, ll(f["messageKey"]));
+    key(v, "messageName"); mp_str(v, p[2]);
+    key(v, "variables"); mp_bin(v, kEmptyDoc);
+    key(v, "interrupting"); v.push_back((char)(f["interrupting"] == "1" ? 0xc3 : 0xc2));
+    key(v, "bpmnProcessId"); mp_str(v, f["bpmnProcessId"]);
+    key(v, "correlationKey"); mp_str(v, f["correlationKey"]);
+    key(v, "elementId"); mp_str(v, f["elementId"]);
+    key(v, "tenantId"); key(v, kTenant);
+    key(v, "state"); mp_str(v, "STATE_" + f["state"]);
+    key(v, "key"); mp_int(v, ll(f["key"]));
+  } else if (cf == "MESSAGE_STATS" && need(3)) {
+    ord = 54;  // DbMessageState.java:165-175: DbString "deadline_message_count" -> DbLong
+    cf_prefix(k, ord); dbs(k, "deadline_message_count");
+    dbl(v, ll(p[2]));
   } else {
-    return 0;  // message-correlation column families: not encoded yet
+    return 0;  // not a column family of the path
   }
   sink(ctx, ord, reinterpret_cast<const uint8_t*>(k.data()), k.size(), reinterpret_cast<const uint8_t*>(v.data()),
        v.size());
