@@ -1816,12 +1816,27 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
       lci[threadIdx.x] = ci;
       for (uint32_t j = 0; j < my_nrec; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
       __syncthreads();
-      for (uint32_t o = threadIdx.x; o < total; o += K::B) {
-        const uint32_t l = own[o], j = o - pre[l];
-        uint2 r;
-        if (j < (uint32_t)K::R) r = stage_base[j * K::B + l];
-        else r = overflow_row(P, lci[l], j);
-        out[o] = r;
+      // four records per thread and iteration (independent chains: the overflow rows' L2 latency
+      // is paid once per four records, not per record)
+      for (uint32_t o0 = threadIdx.x; o0 < total; o0 += 4 * K::B) {
+        uint32_t l[4], j[4];
+        uint2 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t o = o0 + u * K::B;
+          l[u] = o < total ? own[o] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) j[u] = o0 + u * K::B - pre[l[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (o0 + u * K::B >= total) continue;
+          if (j[u] < (uint32_t)K::R) r[u] = stage_base[j[u] * K::B + l[u]];
+          else r[u] = overflow_row(P, lci[l[u]], j[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (o0 + u * K::B < total) out[o0 + u * K::B] = r[u];
       }
       __syncthreads();
     } else {
