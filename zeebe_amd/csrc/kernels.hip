@@ -40,7 +40,8 @@ namespace zb {
 // per-lane batch context
 // ---------------------------------------------------------------------------------------------
 // Kernel configuration: workgroup size B, LDS element-instance table entries T, LDS queue
-// entries Q, records staged in LDS per lane R (rows j >= R go to the global overflow rows).
+// entries Q, records staged in LDS per lane R (rows j >= R are written straight into the chunk's
+// output region, above its packed run, and interleaved into order by the drain gather).
 // After the chunk's wavefront scan an owner map in LDS lets the workgroup store the chunk's
 // records contiguously with coalesced 16-byte writes.  (Measured alternatives, linear-10: every
 // lane storing its own records at its prefix scatters each store over ~40 cache lines; a
@@ -60,8 +61,8 @@ struct KCfg {
 };
 // One token per instance (exclusive gateways, no parallel gateways / multi-outgoing nodes: no join
 // counters).  64-lane workgroups with 28 stage rows hold a whole config-3 CREATE batch (26 records)
-// in LDS: with 16 rows every chunk spilled 10 rows per lane to the global overflow rows and took
-// the per-lane flush -- 1.9x slower (A/B on config 3: 0.83 -> 1.59 x 10^11 transitions/s).
+// in LDS: with 16 rows every chunk spilled 10 rows per lane out of LDS and took the per-lane
+// flush -- 1.9x slower (A/B on config 3: 0.83 -> 1.59 x 10^11 transitions/s).
 #ifndef ZB_KSIMPLE_B
 #define ZB_KSIMPLE_B 64
 #define ZB_KSIMPLE_R 28
@@ -89,7 +90,7 @@ struct Lane {
   uint2* tbl;           // LDS table base (entry t at tbl[t * K::B])
   uint32_t* q;          // LDS queue base (entry i at q[(i % K::Q) * K::B])
   uint2* stage;         // LDS record rows of this lane: record j < R at stage[j * K::B]
-  uint2* rec;           // global overflow rows of this command: record j >= R at rec[j * 64]
+  uint2* rec;           // rows j >= R of this command: rec[j * B] (its chunk's output region)
   uint32_t rec_cap;
   uint32_t nrec;
   uint32_t fail;
@@ -223,7 +224,7 @@ __device__ __forceinline__ void emit(Lane<K>& L, uint32_t code, uint32_t key, ui
   if (L.nrec < L.rec_cap) {
     const uint2 r = make_uint2((key & 0xFFFF) | (aux << 16), (elem & 0xFFFF) | (code << 16) | (flags << 24));
     if (L.nrec < (uint32_t)K::R) L.stage[L.nrec * K::B] = r;
-    else L.rec[(size_t)L.nrec * 64] = r;
+    else L.rec[(size_t)L.nrec * K::B] = r;
   } else {
     set_fail(L, FB_RECORDS);
   }
@@ -236,7 +237,7 @@ template <class K>
 __device__ __forceinline__ void emit_row(Lane<K>& L, uint2 r) {
   if (L.nrec < L.rec_cap) {
     if (L.nrec < (uint32_t)K::R) L.stage[L.nrec * K::B] = r;
-    else L.rec[(size_t)L.nrec * 64] = r;
+    else L.rec[(size_t)L.nrec * K::B] = r;
   } else {
     set_fail(L, FB_RECORDS);
   }
@@ -1201,11 +1202,6 @@ __device__ __forceinline__ void load_rows(const StepParams& P, uint32_t ci, cons
   }
 }
 
-// record j >= R of command ci: the wave-interleaved global overflow rows
-__device__ __forceinline__ uint2 overflow_row(const StepParams& P, uint32_t ci, uint32_t j) {
-  return P.rec[(((size_t)(ci >> 6) * P.rec_cap + j) << 6) + (ci & 63)];
-}
-
 struct Counters {
   uint32_t rec, trans, comp, keys, fb, cmd;
 };
@@ -1369,8 +1365,8 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
 // One command's whole batch on one lane; returns the number of records it staged.
 template <class K, class Retire>
 __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint32_t* prog, uint2* tbl_base,
-                                                uint2* stage_base, uint32_t* q_base, uint32_t ci, uint4 cw,
-                                                uint4 h, uint2 s0, Counters& acc, const Retire& retire) {
+                                                uint2* stage_base, uint32_t* q_base, uint2* region, uint32_t ci,
+                                                uint4 cw, uint4 h, uint2 s0, Counters& acc, const Retire& retire) {
   const uint32_t inst = cw.x;
   const uint32_t kind = cw.y & 0xFF;
   const uint32_t doc_count = (cw.y >> 8) & 0xFF;
@@ -1384,9 +1380,10 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.r_t0 = L.r_t1 = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   L.r_q0 = L.r_q1 = 0;
   L.stage = stage_base + threadIdx.x;
-  // overflow rows (j >= R) are wave-interleaved by command: each emit of a wave is one
-  // coalesced 512-byte store
-  L.rec = P.rec + ((size_t)(ci >> 6) * P.rec_cap << 6) + (ci & 63);
+  // rows j >= R go straight to the chunk's output region, at j * B + lane (above the packed
+  // rows, which never exceed B * R): each emit of a wave is one coalesced 512-byte store, and
+  // the drain gather puts them in order
+  L.rec = region + threadIdx.x;
   L.rec_cap = P.rec_cap;
   L.nrec = 0;
   L.fail = 0;
@@ -1724,17 +1721,21 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
     ci3 = cmd_index<K>(P, c + 3 * G);
     ZB_STAMP(t1);
 
+    uint2* out = P.out + (size_t)(P.region_base + c) * K::B * P.rec_cap;
     uint32_t my_nrec = 0;
     // The prefetch loads just issued are retired inside run_command, right before its commit stores
     // (see Retire): by then they have had the whole batch logic to arrive, and no store is ahead of
     // them in the vmcnt queue.
     const auto retire = [&]() { consume(h1); consume(s1); consume(cw2); consume(ci3); };
-    if (ci != kNoCmd) my_nrec = run_command<K>(P, prog, tbl_base, stage_base, q_base, ci, cw, h, s0, acc, retire);
+    if (ci != kNoCmd)
+      my_nrec = run_command<K>(P, prog, tbl_base, stage_base, q_base, out, ci, cw, h, s0, acc, retire);
     else retire();
     ZB_STAMP(t2);
 
-    // ---- wavefront scan compaction: the chunk's records go out contiguously, once ----
-    uint32_t inc = my_nrec;
+    // ---- wavefront scan compaction: the chunk's staged rows (j < R) go out contiguously, once;
+    // rows j >= R are already in the region, above the packed run ----
+    const uint32_t mc = min(my_nrec, (uint32_t)K::R);
+    uint32_t inc = mc;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t o = __shfl_up(inc, off);
@@ -1754,14 +1755,13 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
       ovf |= (ws[w] >> 31) != 0;
     }
     ZB_STAMP(t3);
-    uint2* out = P.out + (size_t)(P.region_base + c) * K::B * P.rec_cap;
-    const uint32_t my_off = wbase + inc - my_nrec;
-    // homogeneous single-wave chunk (every lane emitted the same n records -- a window of one
+    const uint32_t my_off = wbase + inc - mc;
+    // homogeneous single-wave chunk (every lane staged the same n rows -- a window of one
     // command kind at one element, the common case of straight-line segments): record o of the
     // run is row o % n of lane o / n, so the copy needs no owner map; o / n by a 16-bit
     // reciprocal, exact for o < 2^16 / n
-    const uint32_t n0 = __builtin_amdgcn_readfirstlane(my_nrec);
-    if (K::REG && !ovf && n0 > 0 && __ballot(my_nrec != n0) == 0 && total == K::B * n0) {
+    const uint32_t n0 = __builtin_amdgcn_readfirstlane(mc);
+    if (K::REG && n0 > 0 && __ballot(mc != n0) == 0 && total == K::B * n0) {
       const uint32_t m = (65536u + n0 - 1) / n0;
       for (uint32_t o = 2 * threadIdx.x; o < total; o += 2 * K::B) {
         const uint32_t l0 = (o * m) >> 16, j0 = o - l0 * n0;
@@ -1771,13 +1771,12 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
         *reinterpret_cast<uint4*>(out + o) = make_uint4(r0.x, r0.y, r1.x, r1.y);
       }
       __builtin_amdgcn_wave_barrier();  // the next chunk reuses the stage
-    } else if (!ovf && total <= (uint32_t)(K::B * K::R)) {
-      // packed copy: an owner map in LDS turns the lanes' columns into one contiguous run that
-      // the workgroup stores with 16-byte, fully coalesced writes (2 records per lane).  Only
-      // chunks without overflow rows take it, so the copy reads LDS alone and its stores never
-      // wait on vector memory.
+    } else {
+      // packed copy: an owner map in LDS turns the lanes' columns into one contiguous run
+      // (at most B * R rows) that the workgroup stores with 16-byte, fully coalesced writes.
+      // The copy reads LDS alone, so its stores never wait on vector memory.
       pre[threadIdx.x] = my_off;
-      for (uint32_t j = 0; j < my_nrec; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
+      for (uint32_t j = 0; j < mc; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
       __syncthreads();
       // four output records per thread and iteration: one 4-byte owner read, then four
       // independent prefix reads and four independent row reads (no dependent LDS chain per
@@ -1807,44 +1806,11 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
         }
       }
       __syncthreads();  // the next chunk reuses the stage columns and the owner map
-    } else if (!K::REG && !K::M && total <= (uint32_t)(K::T * K::B * 8)) {
-      // long batches (rows j >= R in the global overflow rows): the same owner map over the whole
-      // run, one record per thread and iteration, rows j >= R fetched from the overflow rows
-      // (L2-resident, just written); the stores stay contiguous
-      uint32_t* lci = q_base + K::B;  // FIFO region, idle: window index of each lane's command
-      pre[threadIdx.x] = my_off;
-      lci[threadIdx.x] = ci;
-      for (uint32_t j = 0; j < my_nrec; ++j) own[my_off + j] = (uint8_t)threadIdx.x;
-      __syncthreads();
-      // four records per thread and iteration (independent chains: the overflow rows' L2 latency
-      // is paid once per four records, not per record)
-      for (uint32_t o0 = threadIdx.x; o0 < total; o0 += 4 * K::B) {
-        uint32_t l[4], j[4];
-        uint2 r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t o = o0 + u * K::B;
-          l[u] = o < total ? own[o] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) j[u] = o0 + u * K::B - pre[l[u]];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (o0 + u * K::B >= total) continue;
-          if (j[u] < (uint32_t)K::R) r[u] = stage_base[j[u] * K::B + l[u]];
-          else r[u] = overflow_row(P, lci[l[u]], j[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (o0 + u * K::B < total) out[o0 + u * K::B] = r[u];
-      }
-      __syncthreads();
-    } else {
-      // records in overflow rows, or more than the owner map covers: every lane stores its own
-      for (uint32_t j = 0; j < my_nrec; ++j)
-        out[my_off + j] = j < (uint32_t)K::R ? stage_base[j * K::B + threadIdx.x] : overflow_row(P, ci, j);
     }
-    if (threadIdx.x == 0) P.region_total[P.region_base + c] = total;
+    // region total; a region holding rows j >= R is flagged instead (bit 31) and leaves its lanes'
+    // record counts for the drain path to total and interleave
+    if (ovf) P.region_lanes[(size_t)(P.region_base + c) * K::B + threadIdx.x] = (uint16_t)my_nrec;
+    if (threadIdx.x == 0) P.region_total[P.region_base + c] = ovf ? 0x80000000u : total;
 #ifdef ZB_STAMPS
     ZB_STAMP(t4);
     acc_t[0] += t1 - t0; acc_t[1] += t2 - t1; acc_t[2] += t3 - t2; acc_t[3] += t4 - t3; acc_t[4] += 1;
@@ -1895,8 +1861,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 
 __device__ __forceinline__ uint32_t wave_incl_scan_u(uint32_t v) { return wave_incl_scan(v); }
 
-// single workgroup: exclusive scan of the region totals (64-bit total)
-__global__ __launch_bounds__(1024) void k_scan_regions(const uint32_t* tot, uint32_t nr, unsigned long long* off,
+// single workgroup: exclusive scan of the region totals (64-bit total); a flagged region's total
+// is the sum of its B lane counts
+__global__ __launch_bounds__(1024) void k_scan_regions(const uint32_t* tot, const uint16_t* lanes, uint32_t B,
+                                                      uint32_t nr, unsigned long long* off,
                                                       unsigned long long* total) {
   __shared__ unsigned long long ws[16];
   __shared__ unsigned long long carry;
@@ -1904,7 +1872,11 @@ __global__ __launch_bounds__(1024) void k_scan_regions(const uint32_t* tot, uint
   __syncthreads();
   for (uint32_t base = 0; base < nr; base += 1024) {
     const uint32_t i = base + threadIdx.x;
-    const uint32_t v = i < nr ? tot[i] : 0;
+    uint32_t v = i < nr ? tot[i] : 0;
+    if (v >> 31) {
+      v = 0;
+      for (uint32_t l = 0; l < B; ++l) v += lanes[(size_t)i * B + l];
+    }
     const uint32_t inc = wave_incl_scan(v);
     if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
     __syncthreads();
@@ -1919,14 +1891,38 @@ __global__ __launch_bounds__(1024) void k_scan_regions(const uint32_t* tot, uint
   if (threadIdx.x == 0) *total = carry;
 }
 
-// region g starts at g * region_stride records (the workgroup size of the run x rec_cap)
-__global__ __launch_bounds__(256) void k_gather(const uint2* regions, const uint32_t* tot,
-                                                const unsigned long long* off, size_t region_stride, uint2* out) {
+// region g starts at g * region_stride records (the workgroup size B of the run x rec_cap).  A
+// region without rows j >= R is one packed run; one with them (bit 31 of its total) holds the
+// lanes' first R rows packed at the front and row j >= R of lane l at j * B + l, and the lanes'
+// record counts in lanes[g * B ..]: each lane's records are copied in order (drain path only).
+__global__ __launch_bounds__(256) void k_gather(const uint2* regions, const uint32_t* tot, const uint16_t* lanes,
+                                                const unsigned long long* off, size_t region_stride, uint32_t B,
+                                                uint32_t R, uint2* out) {
   const uint32_t g = blockIdx.x;
-  const uint32_t n = tot[g];
+  const uint32_t t = tot[g];
   const uint2* src = regions + (size_t)g * region_stride;
   uint2* dst = out + off[g];
-  for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+  if (!(t >> 31)) {
+    for (uint32_t i = threadIdx.x; i < t; i += 256) dst[i] = src[i];
+    return;
+  }
+  __shared__ uint32_t wc[4], wn[4];
+  const uint32_t l = threadIdx.x;
+  const uint32_t n = l < B ? lanes[(size_t)g * B + l] : 0u;
+  const uint32_t c = min(n, R);
+  const uint32_t ic = wave_incl_scan(c), in = wave_incl_scan(n);
+  if ((l & 63) == 63) {
+    wc[l >> 6] = ic;
+    wn[l >> 6] = in;
+  }
+  __syncthreads();
+  uint32_t bc = 0, bn = 0;
+  for (uint32_t w = 0; w < (l >> 6); ++w) {
+    bc += wc[w];
+    bn += wn[w];
+  }
+  const uint32_t cp = bc + ic - c, fp = bn + in - n;
+  for (uint32_t j = 0; j < n; ++j) dst[fp + j] = j < R ? src[cp + j] : src[(size_t)j * B + l];
 }
 
 
@@ -2257,10 +2253,18 @@ hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
   }
 }
 
-hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
-                         size_t region_stride, uint2* out, unsigned long long* total, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan_regions, dim3(1), dim3(1024), 0, s, tot, n_regions, off, total);
-  if (n_regions) hipLaunchKernelGGL(k_gather, dim3(n_regions), dim3(256), 0, s, regions, tot, off, region_stride, out);
+uint32_t step_rows(int variant) {
+  return variant == 3 ? KLinear::R : variant == 2 ? KMsg::R : variant ? KGeneric::R : KSimple::R;
+}
+
+hipError_t launch_gather(const uint2* regions, const uint32_t* tot, const uint16_t* lanes, uint32_t n_regions,
+                         unsigned long long* off, size_t region_stride, uint32_t B, uint32_t R, uint2* out,
+                         unsigned long long* total, hipStream_t s) {
+  if (B > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_scan_regions, dim3(1), dim3(1024), 0, s, tot, lanes, B, n_regions, off, total);
+  if (n_regions)
+    hipLaunchKernelGGL(k_gather, dim3(n_regions), dim3(256), 0, s, regions, tot, lanes, off, region_stride, B, R,
+                       out);
   return hipGetLastError();
 }
 

@@ -22,8 +22,10 @@ uint32_t step_block(int variant);
 size_t step_lds_bytes(int variant, uint32_t prog_words);
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s);
 void dump_stamps();
-hipError_t launch_gather(const uint2* regions, const uint32_t* tot, uint32_t n_regions, unsigned long long* off,
-                         size_t region_stride, uint2* out, unsigned long long* total, hipStream_t s);
+uint32_t step_rows(int variant);
+hipError_t launch_gather(const uint2* regions, const uint32_t* tot, const uint16_t* lanes, uint32_t n_regions,
+                         unsigned long long* off, size_t region_stride, uint32_t B, uint32_t R, uint2* out,
+                         unsigned long long* total, hipStream_t s);
 hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uint4* cmds, uint32_t n,
                           unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
                           zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s);
@@ -110,6 +112,7 @@ struct zbhip_handle {
   uint2* d_cmd_hdr = nullptr;
   uint2* d_regions = nullptr;                // [regions][128 * rec_cap] per-workgroup record regions
   uint32_t* d_region_total = nullptr;        // [regions]
+  uint16_t* d_region_lanes = nullptr;        // [regions][128] lane record counts (regions with rows j >= R)
   unsigned long long* d_region_off = nullptr;// [regions] (drain path)
   unsigned long long* d_stats = nullptr;     // [64][8] spread accumulators + [512] gather total
   uint32_t regions_cap = 0;
@@ -262,6 +265,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   h->regions_cap = (cfg->max_commands + 63) / 64 + kExtraRegions;
   ok = ok && dalloc(&h->d_regions, h->region_records) == hipSuccess &&
        dalloc(&h->d_region_total, h->regions_cap) == hipSuccess &&
+       dalloc(&h->d_region_lanes, (size_t)h->regions_cap * 128) == hipSuccess &&
        dalloc(&h->d_region_off, h->regions_cap) == hipSuccess;
   // message correlation state (config 5): PROCESS_SUBSCRIPTION rows per instance, correlation slots
   const size_t S = cfg->max_correlation_keys;
@@ -321,6 +325,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_cmd_hdr);
   (void)hipFree(h->d_regions);
   (void)hipFree(h->d_region_total);
+  (void)hipFree(h->d_region_lanes);
   (void)hipFree(h->d_region_off);
   (void)hipFree(h->d_stats);
   (void)hipFree(h->st.pms);
@@ -722,10 +727,10 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.prog_words = (uint32_t)h->prog.size();
   P.n_procs = (uint32_t)h->procs.size();
   P.st = h->st;
-  P.rec = h->d_rec;
   P.rec_cap = h->rec_cap;
   P.out = h->d_regions;
   P.region_total = h->d_region_total;
+  P.region_lanes = h->d_region_lanes;
   P.cmd_hdr = h->d_cmd_hdr;
   P.stats = h->d_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
@@ -802,8 +807,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   h->h_hdr2.assign(n, make_uint4(0, 0, 0, 0));
   if (n && h->msg())
     HIPCHK(hipMemcpyAsync(h->h_hdr2.data(), h->d_cmd_hdr2, n * sizeof(uint4), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(launch_gather(h->d_regions, h->d_region_total, region, h->d_region_off, (size_t)B * h->rec_cap, h->d_rec,
-                       h->d_stats + 64 * 8, h->stream));
+  HIPCHK(launch_gather(h->d_regions, h->d_region_total, h->d_region_lanes, region, h->d_region_off,
+                       (size_t)B * h->rec_cap, B, step_rows(h->variant), h->d_rec, h->d_stats + 64 * 8, h->stream));
   unsigned long long total = 0;
   HIPCHK(hipMemcpyAsync(&total, h->d_stats + 64 * 8, sizeof total, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));

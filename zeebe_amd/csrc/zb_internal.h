@@ -132,11 +132,11 @@ struct StepParams {
   uint32_t prog_words;
   uint32_t n_procs;
   DevState st;
-  uint2* rec;                 // overflow record rows (j >= R), wave-interleaved by command index
   uint32_t rec_cap;           // max records per batch
   uint2* out;                 // workgroup regions: region g holds its block's records contiguously
   uint32_t region_base;       // region of this launch's workgroup 0
-  uint32_t* region_total;     // [regions] records in each region
+  uint32_t* region_total;     // [regions] records in each region (bit 31: holds rows j >= R)
+  uint16_t* region_lanes;     // [regions][B] record counts of the lanes of a region with rows j >= R
   uint2* cmd_hdr;             // [n_cmds]
   unsigned long long* stats;  // [64][8] spread accumulators: records, transitions, completed, keys,
                               // fallback, commands
