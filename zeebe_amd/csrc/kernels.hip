@@ -29,6 +29,7 @@
 // an ordered copy of every chunk's records into one contiguous append buffer.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -60,29 +61,43 @@ struct KCfg {
   static constexpr bool X = X_;  // exclusive gateways (FEEL condition evaluation)
 };
 // One token per instance (exclusive gateways, no parallel gateways / multi-outgoing nodes: no join
-// counters).  64-lane workgroups with 28 stage rows hold a whole config-3 CREATE batch (26 records)
-// in LDS: with 16 rows every chunk spilled 10 rows per lane out of LDS and took the per-lane
-// flush -- 1.9x slower (A/B on config 3: 0.83 -> 1.59 x 10^11 transitions/s).
+// counters).  Only R = 4 stage rows: rows j >= R go straight to the output region (one coalesced
+// wave store per row), so LDS no longer limits residency (5 KiB per workgroup) and the register
+// file does (3 waves per SIMD).  Measured on config 3 (exclusive gateway, 26-record CREATE
+// batches): R = 28 (the whole batch in LDS, 9 workgroups per CU) 1.57, R = 8 2.11, R = 4
+// 2.22 x 10^11 transitions/s.
 #ifndef ZB_KSIMPLE_B
 #define ZB_KSIMPLE_B 64
-#define ZB_KSIMPLE_R 28
+#define ZB_KSIMPLE_R 4
 #endif
-using KSimple = KCfg<ZB_KSIMPLE_B, 4, 4, ZB_KSIMPLE_R, false, false>;
+#ifndef ZB_KSIMPLE_W
+#define ZB_KSIMPLE_W 0
+#endif
+using KSimple = KCfg<ZB_KSIMPLE_B, 4, 4, ZB_KSIMPLE_R, false, false, true, ZB_KSIMPLE_W>;
 // Linear chains (every node <= 1 outgoing flow, no gateways, no catch events): at most two element
 // instances are alive in a batch, no FEEL evaluator, no join counters.  T = 2 and R = 15 keep the
 // workgroup at <= 20 KiB of LDS and the register target at 128 VGPRs, so 4 waves per SIMD are
 // resident (KSimple: 3).  The FIFO never holds more than one entry there and the table two, so both
 // live in registers: the batch logic issues no dependent LDS round trips, only the record stage.
+// R = 15 holds every straight-line segment's fixed record sequence (fast_command's static rows).
 #ifndef ZB_KLINEAR_W
 #define ZB_KLINEAR_W 4
 #endif
 using KLinear = KCfg<64, 2, 2, 15, false, false, false, ZB_KLINEAR_W, true>;
+// Everything else in the subset (parallel gateways: join counters).  R = 4 as for KSimple: config
+// 4 (fork/join 8, ~60-record CREATE batches) R = 16 1.44, R = 8 1.63, R = 4 1.93 x 10^11.
 #ifndef ZB_KGENERIC_B
 #define ZB_KGENERIC_B 128
-#define ZB_KGENERIC_R 16
+#define ZB_KGENERIC_R 4
 #endif
-using KGeneric = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R>; // everything else in the subset
-using KMsg = KCfg<128, 12, 16, 16, true>;  // partitions with message catch events (config 5)
+#ifndef ZB_KGENERIC_W
+#define ZB_KGENERIC_W 0
+#endif
+using KGeneric = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, ZB_KGENERIC_W>;
+#ifndef ZB_KMSG_R
+#define ZB_KMSG_R 4
+#endif
+using KMsg = KCfg<128, 12, 16, ZB_KMSG_R, true>;  // partitions with message catch events (config 5)
 
 template <class K>
 struct Lane {
@@ -1721,7 +1736,7 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
     ci3 = cmd_index<K>(P, c + 3 * G);
     ZB_STAMP(t1);
 
-    uint2* out = P.out + (size_t)(P.region_base + c) * K::B * P.rec_cap;
+    uint2* out = P.out + (size_t)(P.region_base + c) * P.region_stride;
     uint32_t my_nrec = 0;
     // The prefetch loads just issued are retired inside run_command, right before its commit stores
     // (see Retire): by then they have had the whole batch logic to arrive, and no store is ahead of
@@ -2160,6 +2175,9 @@ static int env_int(const char* name, int dflt) {
 
 // Grid of a launch: as many workgroups as are resident at once (occupancy x CUs), each looping
 // over an equal share of the chunks; ZBHIP_CHUNKS_PER_WG=k instead gives every workgroup k chunks.
+constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr size_t kLdsGranule = 1280;  // 160 KB / 128
+
 template <class K>
 static uint32_t grid_for(uint32_t n_chunks, size_t lds) {
   static int cus = 0;
@@ -2172,6 +2190,14 @@ static uint32_t grid_for(uint32_t n_chunks, size_t lds) {
   }
   if (lds != cached_lds) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step<K>, K::B, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
+    // the occupancy query counts LDS in bytes; the CU allocates it in kLdsGranule blocks, so near
+    // the limit it promises one workgroup more than fits (measured: 13 600 B x 12 and
+    // 27 008 B x 6 workgroups ran as 11 and 5) and the grid's last workgroups ran after the rest
+    const size_t granted = (lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule;
+    if (granted) per_cu = std::max(1, std::min(per_cu, (int)(kLdsPerCu / granted)));
+    const int forced = env_int("ZBHIP_WG_PER_CU", 0);
+    if (forced > 0) per_cu = forced;
+    if (env_int("ZBHIP_DEBUG", 0)) fprintf(stderr, "[zbhip] k_step B=%d R=%d lds=%zu per_cu=%d\n", K::B, K::R, lds, per_cu);
     cached_lds = lds;
   }
   const int fixed = env_int("ZBHIP_CHUNKS_PER_WG", 0);

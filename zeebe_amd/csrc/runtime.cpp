@@ -32,7 +32,8 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s);
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
                          uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s);
-constexpr uint32_t kExtraRegions = 64;  // regions for the extra workgroups of multi-round windows
+constexpr uint32_t kExtraRegions = 64;
+constexpr uint32_t kRegionPad = 0;  // regions for the extra workgroups of multi-round windows
 }  // namespace zb
 
 using namespace zb;
@@ -117,6 +118,7 @@ struct zbhip_handle {
   unsigned long long* d_stats = nullptr;     // [64][8] spread accumulators + [512] gather total
   uint32_t regions_cap = 0;
   size_t region_records = 0;
+  uint32_t region_pad = 0;  // records between consecutive regions (region stride B * rec_cap + pad)
   int variant = 3;                           // kernel variant (zbhip_deploy): 3 KLinear, 0 KSimple, 1 KGeneric, 2 KMsg
   std::vector<std::pair<uint32_t, uint32_t>> launches;  // (region_base, first position in order) per launch
   std::vector<hipEvent_t> tev;               // timing events (pairs) since the last stats reset
@@ -261,8 +263,13 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
             dalloc(&h->d_rec, ((size_t)cfg->max_commands + 64) * h->rec_cap) == hipSuccess;
   // region pool: every workgroup of a run owns (workgroup size) * rec_cap records; sized for a
   // full window plus kExtraRegions partly filled workgroups of extra rounds (<= 256 lanes each)
-  h->region_records = ((size_t)cfg->max_commands + (size_t)kExtraRegions * 256) * h->rec_cap;
   h->regions_cap = (cfg->max_commands + 63) / 64 + kExtraRegions;
+  {
+    const char* e = getenv("ZBHIP_REGION_PAD");
+    h->region_pad = e ? (uint32_t)atoi(e) : kRegionPad;
+  }
+  h->region_records = ((size_t)cfg->max_commands + (size_t)kExtraRegions * 256) * h->rec_cap +
+                      (size_t)h->regions_cap * h->region_pad;
   ok = ok && dalloc(&h->d_regions, h->region_records) == hipSuccess &&
        dalloc(&h->d_region_total, h->regions_cap) == hipSuccess &&
        dalloc(&h->d_region_lanes, (size_t)h->regions_cap * 128) == hipSuccess &&
@@ -728,6 +735,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.n_procs = (uint32_t)h->procs.size();
   P.st = h->st;
   P.rec_cap = h->rec_cap;
+  P.region_stride = B * h->rec_cap + h->region_pad;
   P.out = h->d_regions;
   P.region_total = h->d_region_total;
   P.region_lanes = h->d_region_lanes;
@@ -761,7 +769,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     h->launches.push_back({region, sp.first});
     region += (sp.second + B - 1) / B;
   }
-  if (region > h->regions_cap || (size_t)region * B * h->rec_cap > h->region_records)
+  if (region > h->regions_cap || (size_t)region * P.region_stride > h->region_records)
     return ZBHIP_ENOMEM;  // too many rounds for the region pool
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timed) {
@@ -808,7 +816,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (n && h->msg())
     HIPCHK(hipMemcpyAsync(h->h_hdr2.data(), h->d_cmd_hdr2, n * sizeof(uint4), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(launch_gather(h->d_regions, h->d_region_total, h->d_region_lanes, region, h->d_region_off,
-                       (size_t)B * h->rec_cap, B, step_rows(h->variant), h->d_rec, h->d_stats + 64 * 8, h->stream));
+                       P.region_stride, B, step_rows(h->variant), h->d_rec, h->d_stats + 64 * 8, h->stream));
   unsigned long long total = 0;
   HIPCHK(hipMemcpyAsync(&total, h->d_stats + 64 * 8, sizeof total, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));

@@ -133,6 +133,7 @@ struct StepParams {
   uint32_t n_procs;
   DevState st;
   uint32_t rec_cap;           // max records per batch
+  uint32_t region_stride;     // records from one output region to the next (>= B * rec_cap)
   uint2* out;                 // workgroup regions: region g holds its block's records contiguously
   uint32_t region_base;       // region of this launch's workgroup 0
   uint32_t* region_total;     // [regions] records in each region (bit 31: holds rows j >= R)
