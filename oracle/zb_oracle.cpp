@@ -413,6 +413,23 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       e.event = ZBHIP_EV_MESSAGE;
       e.msg_name = mi->second.first;
       e.corr_var = mi->second.second;
+    } else if (n == "task" || n == "manualTask") {
+      // undefined / manual tasks (BpmnElementProcessors.java:65-68 -> UndefinedTaskProcessor):
+      // activities without behaviour, event type UNSPECIFIED
+      e.type = n == "task" ? ZBHIP_EL_TASK : ZBHIP_EL_MANUAL_TASK;
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+    } else if (n == "intermediateThrowEvent") {
+      // IntermediateThrowEventProcessor.NoneIntermediateThrowEventBehavior (:113-138): none events only
+      e.type = ZBHIP_EL_INTERMEDIATE_THROW_EVENT;
+      for (auto& d : k->kids)
+        if (d->name.size() > 15 && d->name.compare(d->name.size() - 15, 15, "EventDefinition") == 0) {
+          err = "intermediate throw event with event definition outside the supported subset";
+          return false;
+        }
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+      e.event = ZBHIP_EV_NONE;
     } else if (n == "exclusiveGateway") {
       e.type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
     } else if (n == "parallelGateway") {
@@ -1480,6 +1497,9 @@ class Oracle {
         break;
       }
       case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onActivate (processing/bpmn/event/StartEventProcessor.java:45-50)
+      case ZBHIP_EL_TASK:         // UndefinedTaskProcessor.onActivate (processing/bpmn/task/UndefinedTaskProcessor.java:37-42)
+      case ZBHIP_EL_MANUAL_TASK:  // ManualTaskProcessor extends UndefinedTaskProcessor
+      case ZBHIP_EL_INTERMEDIATE_THROW_EVENT:  // NoneIntermediateThrowEventBehavior.onActivate (:120-126)
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         pi_command(key, ZBHIP_PI_COMPLETE_ELEMENT, v);
         break;
@@ -1539,7 +1559,12 @@ class Oracle {
         complete_and_take(el, key, v, true);
         break;
       case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onComplete (:63-75)
+      case ZBHIP_EL_INTERMEDIATE_THROW_EVENT:  // NoneIntermediateThrowEventBehavior.onComplete (:128-137)
         complete_and_take(el, key, v, true);
+        break;
+      case ZBHIP_EL_TASK:  // UndefinedTaskProcessor.onComplete (:44-51): no output mappings
+      case ZBHIP_EL_MANUAL_TASK:
+        complete_and_take(el, key, v, false);
         break;
       case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT: {
         // IntermediateCatchEventProcessor.onComplete: applyOutputMappings, unsubscribeFromEvents

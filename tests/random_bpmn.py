@@ -11,8 +11,9 @@ ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
 
 
 class _Gen:
-    def __init__(self, rng, max_depth, max_blocks, messages):
+    def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False):
         self.rng = rng
+        self.pass_through = pass_through
         self.max_depth = max_depth
         self.max_blocks = max_blocks
         self.messages = messages
@@ -64,7 +65,13 @@ class _Gen:
                 choices.append("par")
         if self.messages and self.catches < 1 and width == 1:
             choices.append("catch")
+        if self.pass_through:
+            choices.append("pass")
         c = choices[int(r.integers(0, len(choices)))]
+        if c == "pass":  # elements without behaviour: undefined / manual task, none throw event
+            t = self.node(("task", "manualTask", "intermediateThrowEvent")[int(r.integers(0, 3))])
+            self.flow(cur, t)
+            return t
         if c == "task":
             t = self.node("serviceTask", job_type="job%d" % int(r.integers(0, 3)))
             self.flow(cur, t)
@@ -103,8 +110,8 @@ class _Gen:
         return join
 
 
-def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False):
-    g = _Gen(rng, max_depth, max_blocks, messages)
+def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False):
+    g = _Gen(rng, max_depth, max_blocks, messages, pass_through)
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")

@@ -100,3 +100,28 @@ def test_random_processes_compile_like_the_oracle():
         o = Oracle()
         assert o.deploy(xml) == 0
         assert [c.id(i) for i in range(len(c.els))] == [o.element_id(0, i) for i in range(len(c.els))]
+
+
+def test_pass_through_elements_compile_like_the_oracle():
+    # undefined task, manual task, none intermediate throw event: element type and event type as
+    # the oracle's transformation (UNSPECIFIED for tasks, NONE for the throw event)
+    from random_bpmn import random_process
+    for seed in range(20):
+        xml = random_process(np.random.default_rng(2000 + seed), pass_through=True)
+        c = Compiled(xml)
+        o = Oracle()
+        assert o.deploy(xml) == 0
+        tables = o.process_tables()[0]["elements"]
+        assert [(c.id(i), int(c.els[i]["element_type"]), int(c.els[i]["event_type"])) for i in range(len(c.els))] == \
+            [(t[2], t[0], t[1]) for t in tables]
+
+
+@pytest.mark.parametrize("definition", ["messageEventDefinition", "signalEventDefinition", "linkEventDefinition"])
+def test_throw_event_with_definition_is_rejected(definition):
+    xml = (bpmn.createExecutableProcess("p").startEvent("s").intermediateThrowEvent("t").endEvent("e").done()
+           .replace('<intermediateThrowEvent id="t"/>',
+                    '<intermediateThrowEvent id="t"><%s id="d"/></intermediateThrowEvent>' % definition))
+    with pytest.raises(ZbhipError):
+        Compiled(xml)
+    with pytest.raises(Exception):
+        Oracle().deploy(xml)

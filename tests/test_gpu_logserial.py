@@ -81,10 +81,12 @@ def drive(pair, n, docs=None):
         recs = pair.window(complete_commands([r[0] for r in res], [r[1] for r in res]))
 
 
-@pytest.mark.parametrize("workload", ["one_task", "linear10", "fork_join8", "fork_join8_tasks"])
+@pytest.mark.parametrize("workload", ["one_task", "linear10", "fork_join8", "fork_join8_tasks", "pass_through"])
 def test_gpu_log_bytes_match_oracle(workload):
+    from test_logserial import PASS_THROUGH_XML
     xml = {"one_task": process_xml({"fixture": "one_task.bpmn"}), "linear10": bpmn.linear_process(10),
-           "fork_join8": bpmn.fork_join_process(8), "fork_join8_tasks": bpmn.fork_join_process(8, tasks=True)}[workload]
+           "fork_join8": bpmn.fork_join_process(8), "fork_join8_tasks": bpmn.fork_join_process(8, tasks=True),
+           "pass_through": PASS_THROUGH_XML}[workload]
     drive(Pair(xml, 200), 200)
 
 

@@ -324,3 +324,16 @@ def test_fork_join8_full_size_properties():
     s = stats[0]
     assert s["fallback"] == 0 and s["transitions"] == 30 * n and s["records"] == 52 * n
     assert s["completed_instances"] == n
+
+
+@pytest.mark.parametrize("kind", ["task", "manualTask", "intermediateThrowEvent"])
+def test_pass_through_element_parity(kind):
+    # BpmnElementTypeTest / BpmnEventTypeTest models (start -> X -> end, and start -> X -> task ->
+    # X -> end): linear chains take KLinear, records and state equal to the oracle's
+    b = bpmn.createExecutableProcess("process").startEvent("start")
+    drive(getattr(b, kind)("elem").endEvent("end").done(), 200)
+    b = bpmn.createExecutableProcess("process").startEvent("start")
+    xml = getattr(getattr(b, kind)("a").serviceTask("t", "job"), kind)("b").endEvent("end").done()
+    drive(xml, 200)
+    b = bpmn.createExecutableProcess("process").startEvent("start")
+    drive(getattr(b, kind)("elem").done(), 50)  # the element ends the execution path

@@ -21,3 +21,13 @@ def test_random_process_parity(seed):
     assert part.state() == orc.state()
     # every instance ran to completion: only the key counter row is left
     assert [r for r in part.state() if not r.startswith("KEY|")] == []
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_process_with_pass_through_elements_parity(seed):
+    # undefined / manual tasks and none throw events among the random blocks
+    rng = np.random.default_rng(2000 + seed)
+    xml = random_process(rng, pass_through=True)
+    part, orc = drive(xml, 96, lambda n: amount_docs(rng.integers(0, 1000, n), 0), phases=60,
+                      rng_seed=seed, max_records=256)
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []

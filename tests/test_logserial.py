@@ -162,10 +162,14 @@ def check_entries(buf, recs, first, pos, sb):
             assert value["flowScopeKey"] == r["scope_key"]
 
 
-@pytest.mark.parametrize("workload", ["one_task", "linear3", "fork_join4"])
+PASS_THROUGH_XML = (bpmn.createExecutableProcess("process").startEvent("start").task("t").manualTask("m")
+                    .intermediateThrowEvent("e").serviceTask("s", "job").endEvent("end").done())
+
+
+@pytest.mark.parametrize("workload", ["one_task", "linear3", "fork_join4", "pass_through"])
 def test_serializer_matches_oracle(workload):
     xml = {"one_task": process_xml({"fixture": "one_task.bpmn"}), "linear3": bpmn.linear_process(3),
-           "fork_join4": bpmn.fork_join_process(4, tasks=True)}[workload]
+           "fork_join4": bpmn.fork_join_process(4, tasks=True), "pass_through": PASS_THROUGH_XML}[workload]
     run = Run([xml])
     _drive_simple(run, 40)
     assert run.total > 40

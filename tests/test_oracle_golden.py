@@ -303,3 +303,68 @@ def test_many_instances_are_independent():
     assert len(shapes) == 1
     keys = [int(recs[b[0]]["key"]) - BASE for b in batches]
     assert keys == [1 + 6 * i for i in range(50)]
+
+
+# ---- elements without behaviour: undefined task, manual task, none
+# intermediate throw event -- UndefinedTaskProcessor / ManualTaskProcessor (task/*.java) and
+# IntermediateThrowEventProcessor.NoneIntermediateThrowEventBehavior (event/*.java:113-138)
+
+PASS_THROUGH = {"task": ("TASK", "UNSPECIFIED"), "manualTask": ("MANUAL_TASK", "UNSPECIFIED"),
+                "intermediateThrowEvent": ("INTERMEDIATE_THROW_EVENT", "NONE")}
+
+
+def _types(o, recs, elem_id):
+    from oracle import logserial as LS
+    tables = o.process_tables()
+    out = set()
+    for r in recs:
+        if r["value_type"] != abi.VT_PROCESS_INSTANCE:
+            continue
+        p, e = int(r["process_idx"]), int(r["element_idx"])
+        if o.element_id(p, e) == elem_id:
+            el = tables[p]["elements"][e]
+            out.add((LS.ELEMENT_TYPE[el[0]], LS.EVENT_TYPE[el[1]]))
+    return out
+
+
+@pytest.mark.parametrize("kind", sorted(PASS_THROUGH))
+def test_pass_through_element_types(kind):
+    # BpmnElementTypeTest (:367-396): every record of the element carries its element type;
+    # BpmnEventTypeTest (:54-62, :415-424): NONE for the none throw event, UNSPECIFIED for tasks
+    b = bpmn.createExecutableProcess("process").startEvent("start")
+    xml = getattr(b, kind)("elem").endEvent("end").done()
+    o = Oracle()
+    recs = _run_single(o, create_commands(1, o.deploy(xml)))
+    assert _types(o, recs, "elem") == {PASS_THROUGH[kind]}
+    p = _pairs(o, recs)
+    assert _contains_sequence(p, [
+        ("elem", "ACTIVATE_ELEMENT"), ("elem", "ELEMENT_ACTIVATING"), ("elem", "ELEMENT_ACTIVATED"),
+        ("elem", "COMPLETE_ELEMENT"), ("elem", "ELEMENT_COMPLETING"), ("elem", "ELEMENT_COMPLETED")])
+    assert p[-1] == ("process", "ELEMENT_COMPLETED")
+    assert o.state() == ["KEY|latestKey|%d" % (BASE + 7)]
+
+
+def test_none_throw_event_ends_the_path():
+    # BpmnEventTypeTest "None Throw Event" model: start -> throw, no end event; the throw event's
+    # completion ends the execution path and completes the process
+    xml = bpmn.createExecutableProcess("process").startEvent("start").intermediateThrowEvent("elem").done()
+    o = Oracle()
+    p = _pairs(o, _run_single(o, create_commands(1, o.deploy(xml))), only_events=True)
+    assert p[-4:] == [("elem", "ELEMENT_COMPLETING"), ("elem", "ELEMENT_COMPLETED"),
+                      ("process", "ELEMENT_COMPLETING"), ("process", "ELEMENT_COMPLETED")]
+
+
+def test_pass_through_elements_mixed_with_jobs_and_gateways():
+    xml = (bpmn.createExecutableProcess("process").startEvent("start").task("t1")
+           .parallelGateway("fork").manualTask("m1").serviceTask("s1", "job").parallelGateway("join")
+           .moveToNode("fork").intermediateThrowEvent("e1").connectTo("join")
+           .moveToNode("join").endEvent("end").done())
+    o = Oracle()
+    recs = _run_single(o, create_commands(1, o.deploy(xml)))
+    jobs = [int(r["key"]) for r in recs if r["value_type"] == abi.VT_JOB]
+    assert len(jobs) == 1
+    p = _pairs(o, recs, only_events=True)
+    assert ("e1", "ELEMENT_COMPLETED") in p and ("m1", "ELEMENT_COMPLETED") in p and ("t1", "ELEMENT_COMPLETED") in p
+    assert ("process", "ELEMENT_COMPLETED") not in p
+    recs = _run_single(o, complete_commands([0], [jobs[0] - BASE - 1]))
+    assert _pairs(o, recs, only_events=True)[-1] == ("process", "ELEMENT_COMPLETED")

@@ -84,6 +84,18 @@ class ProcessBuilder:
         self.current.job_type = t
         return self
 
+    def task(self, id_=None):
+        self._add_node("task", id_)
+        return self
+
+    def manualTask(self, id_=None):
+        self._add_node("manualTask", id_)
+        return self
+
+    def intermediateThrowEvent(self, id_=None):
+        self._add_node("intermediateThrowEvent", id_)
+        return self
+
     def intermediateCatchEvent(self, id_=None):
         self._add_node("intermediateCatchEvent", id_)
         return self

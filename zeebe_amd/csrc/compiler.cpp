@@ -413,6 +413,9 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     else if (c.tag == "parallelGateway") type = ZBHIP_EL_PARALLEL_GATEWAY;
     else if (c.tag == "sequenceFlow") type = ZBHIP_EL_SEQUENCE_FLOW;
     else if (c.tag == "intermediateCatchEvent") type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
+    else if (c.tag == "intermediateThrowEvent") type = ZBHIP_EL_INTERMEDIATE_THROW_EVENT;
+    else if (c.tag == "task") type = ZBHIP_EL_TASK;
+    else if (c.tag == "manualTask") type = ZBHIP_EL_MANUAL_TASK;
     else if (c.tag == "extensionElements" || c.tag == "documentation" || c.tag == "textAnnotation" ||
              c.tag == "association")
       continue;
@@ -428,6 +431,18 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           return ZBHIP_EUNSUPP;
         }
       e.event_type = ZBHIP_EV_NONE;
+    }
+    if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT || type == ZBHIP_EL_TASK || type == ZBHIP_EL_MANUAL_TASK) {
+      // activities / events without behaviour (UndefinedTaskProcessor, ManualTaskProcessor,
+      // IntermediateThrowEventProcessor.NoneIntermediateThrowEventBehavior): none events only
+      for (auto& d : c.children)
+        if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+          err = "event definition <" + d.tag + "> outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
+      if (const Elem* ext = c.first("extensionElements"))
+        if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+      if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT) e.event_type = ZBHIP_EV_NONE;
     }
     if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
       // CatchEventTransformer.transformMessageEventDefinition: message catch events only

@@ -979,6 +979,9 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     const int t = L.nt > 0 ? tbl_find(L, key) : -1;
     switch (type) {
       case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onActivate (:45-50)
+      case ZBHIP_EL_TASK:         // UndefinedTaskProcessor.onActivate (task/UndefinedTaskProcessor.java:37-42)
+      case ZBHIP_EL_MANUAL_TASK:  // ManualTaskProcessor extends UndefinedTaskProcessor
+      case ZBHIP_EL_INTERMEDIATE_THROW_EVENT:  // NoneIntermediateThrowEventBehavior.onActivate (:120-126)
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
         emit(L, ZBHIP_PI_COMPLETE_ELEMENT, key, 0, elem);
@@ -1070,11 +1073,11 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       // IntermediateCatchEventProcessor.onComplete -> unsubscribeFromEvents: a subscription still
       // open here would write PROCESS_MESSAGE_SUBSCRIPTION:DELETING (outside the subset)
       if (((L.pm_x >> 12) & 3) != 0 && (L.pm_y & 0xFFFF) == cmd_key) { set_fail(L, FB_MESSAGE); return; }
-    } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK) {
+    } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK && !pass_through(type)) {
       set_fail(L, FB_UNSUPPORTED);
       return;
     }
-  } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK) {
+  } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK && !pass_through(type)) {
     set_fail(L, FB_UNSUPPORTED);
     return;
   }

@@ -481,7 +481,8 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if (e.element_type != ZBHIP_EL_PROCESS && e.element_type != ZBHIP_EL_START_EVENT &&
         e.element_type != ZBHIP_EL_END_EVENT && e.element_type != ZBHIP_EL_SERVICE_TASK &&
         e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
-        e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
+        e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT &&
+        !pass_through(e.element_type))
       return ZBHIP_EUNSUPP;
   for (auto& e : P.els)
     if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {

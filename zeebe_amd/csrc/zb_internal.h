@@ -122,6 +122,12 @@ struct DevState {
   uint32_t n_slots;
 };
 
+// elements without behaviour: ACTIVATING, ACTIVATED, COMPLETE_ELEMENT, COMPLETING, COMPLETED, then
+// the outgoing flows (UndefinedTaskProcessor / ManualTaskProcessor, NoneIntermediateThrowEventBehavior)
+__host__ __device__ inline bool pass_through(uint32_t type) {
+  return type == ZBHIP_EL_TASK || type == ZBHIP_EL_MANUAL_TASK || type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT;
+}
+
 struct StepParams {
   const uint4* cmds;          // zbhip_command[n_cmds] (window, log order)
   const uint32_t* order;      // command indices processed by this launch (round); null = identity
