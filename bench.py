@@ -233,6 +233,38 @@ def run_msg(args, world, rank, local_rank, dist):
         dist.destroy_process_group()
 
 
+def host_io_pass(args, xml, n, host_windows, local_rank, recs_per_batch):
+    """The boundary as a host adapter uses it (zbhip_submit from host memory, zbhip_run with results,
+    zbhip_drain into host memory): every window crosses PCIe in (16 B per command) and out (the
+    compact records), and the host expands them to 80-byte zbhip_record with keys relabelled in
+    DbKeyGenerator order.  A fresh partition; one untimed pass, then one timed pass.  Never `value`."""
+    import time
+
+    from zeebe_amd.engine import Partition
+
+    part = Partition(partition_id=1, partition_count=1, device=local_rank, max_instances=n, max_commands=n,
+                     max_records_per_batch=recs_per_batch)
+    part.deploy(xml)
+    if host_windows[0][1] is not None:
+        part.intern("amount")
+    res = None
+    for timed in (False, True):
+        t0 = time.perf_counter()
+        recs = trans = 0
+        for cmds, docs in host_windows:
+            part.submit(cmds, docs)
+            part.run(0)
+            out = part.drain()
+            recs += len(out)
+        sec = time.perf_counter() - t0
+        trans = part.stats()["transitions"]
+        if timed:
+            res = {"value": trans / sec, "unit": "transitions/s", "records_per_s": recs / sec,
+                   "ms_per_step": sec * 1e3, "records_per_step": recs,
+                   "path": "zbhip_submit (host buffers) + zbhip_run + zbhip_drain (80-B records, relabelled keys)"}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -243,6 +275,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-instances", type=int, default=300_000, help="instances per CPU thread (bounded sample)")
+    ap.add_argument("--host-io", action="store_true",
+                    help="also time one pass with host command buffers and drained records (PCIe + host relabel)")
     ap.add_argument("--virtual-partitions", type=int, default=1,
                     help="--config msg on one GPU: partitions hosted by this process (exchange by device copies)")
     args = ap.parse_args()
@@ -279,6 +313,7 @@ def main():
     # ---- synthetic windows, built once and kept resident in HBM ----
     dev = torch.device("cuda", local_rank)
     windows = []
+    host_windows = []  # the same windows as host buffers, for the PCIe-inclusive pass (--host-io)
     create = abi.make_commands(n)
     create["instance"] = np.arange(n, dtype=np.uint32)
     create["kind"] = abi.CMD_CREATE
@@ -293,6 +328,7 @@ def main():
         create["doc_begin"] = np.arange(n, dtype=np.uint32)
         docs_t = torch.from_numpy(docs.view(np.uint8).copy()).to(dev)
     windows.append(torch.from_numpy(create.view(np.uint8).copy()).to(dev))
+    host_windows.append((create, docs if with_amount else None))
     job_ord = 5 if not with_amount else 6
     for p in range(phases):
         c = abi.make_commands(n)
@@ -300,6 +336,7 @@ def main():
         c["kind"] = abi.CMD_JOB_COMPLETE
         c["ref"] = job_ord + 4 * p
         windows.append(torch.from_numpy(c.view(np.uint8).copy()).to(dev))
+        host_windows.append((c, None))
     torch.cuda.synchronize()
 
     def step(first, timed=False):
@@ -399,6 +436,8 @@ def main():
                      "survey_bytes_per_transition": survey_bpt,
                      "survey_model_GBps": (tr / (k_step_avg_ms * launches * 1e-3) * survey_bpt / 1e9) if survey_bpt else None},
     }
+    if args.host_io and rank == 0:
+        result["host_io"] = host_io_pass(args, xml, n, host_windows, local_rank, recs_per_batch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle import bench as cpu_bench
         th = args.cpu_threads
