@@ -5,8 +5,9 @@
  * The library replaces, for one partition, everything from
  * `Engine.process` (engine/src/main/java/io/camunda/zeebe/engine/Engine.java:99-131)
  * down to the zb-db column-family mutations, for the supported element subset
- * (process, none start/end event, service task, exclusive gateway, parallel
- * gateway).  It is meant to sit behind the stream-platform `RecordProcessor`
+ * (process, none start/end event, service task, undefined and manual task,
+ * none intermediate throw event, message intermediate catch event, exclusive
+ * gateway, parallel gateway).  It is meant to sit behind the stream-platform `RecordProcessor`
  * API (stream-platform/src/main/java/io/camunda/zeebe/stream/api/RecordProcessor.java:17-108):
  * a Java host adapter buffers a window of hot-path commands from the log,
  * submits them, runs them to quiescence and re-emits the drained records per
