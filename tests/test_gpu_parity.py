@@ -115,6 +115,13 @@ def test_one_task_parity():
     drive(process_xml({"fixture": "one_task.bpmn"}), 3000)
 
 
+def test_bulk_drain_parity():
+    # windows above kBulkDrainMin (65 536 records) drain on host threads, command ranges split by
+    # record count (runtime.cpp zbhip_drain); same records as the oracle, in log order
+    part, _ = drive(bpmn.linear_process(3), 12000, phases=4)
+    assert part.stats()["records"] >= 1 << 16
+
+
 def test_linear10_parity():
     drive(bpmn.linear_process(10), 2000)
 

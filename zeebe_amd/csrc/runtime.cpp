@@ -8,10 +8,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -33,6 +35,7 @@ hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmd
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
                          uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;
+constexpr size_t kBulkDrainMin = 1 << 16;  // records: below this the drain stays on the calling thread
 constexpr uint32_t kRegionPad = 0;  // regions for the extra workgroups of multi-round windows
 }  // namespace zb
 
@@ -947,70 +950,26 @@ static uint8_t rejection_type_of(uint32_t reason) {
   }
 }
 
-int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
-  if (!h || (cap && !out)) return ZBHIP_EINVAL;
-  if (n_out) *n_out = 0;
-  if (!h->results) return ZBHIP_ESTATE;
-  size_t k = 0;
-  while (k < cap && h->drain_cmd < h->n_cmds) {
-    const size_t c = h->drain_cmd;
-    const uint2 hd = h->h_hdr[c];
-    const uint32_t nrec = hd.x & 0xFFFF;
-    if (h->drain_rec >= nrec) {
-      ++h->drain_cmd;
-      h->drain_rec = 0;
-      h->drain_ord = 0;
-      continue;
-    }
-    const zbhip_command& cm = h->h_cmds[c];
-    // the instance the records refer to: the command's, or the one a message batch loaded
-    const uint32_t inst = h->msg() && slot_kind(cm.kind) ? h->h_hdr2[c].x : cm.instance;
-    const int64_t doc = cm.doc_count ? h->doc_base + cm.doc_begin : -1;
-    const uint2* rows = h->h_out.data() + h->h_off[c];
-    const uint2 w = rows[h->drain_rec];
-    const uint32_t key_ord = w.x & 0xFFFF, aux_ord = w.x >> 16, elem = w.y & 0xFFFF;
-    const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
-    const bool rej = code & kRejectBit;
-    const uint32_t c6 = code & 0x3F;
-    const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
-    zbhip_record r{};
-    r.source_index = h->source_base + (int64_t)c;
-    r.rejection_type = ZBHIP_REJ_NONE;
-    r.ordinal = (uint16_t)h->drain_ord;
-    r.aux = -1;
-    r.message_key = -1;
-    r.correlation_key = ZBHIP_NO_STRING;
-    r.message_name = 0xFFFF;
-    r.bpmn_process_id = 0xFFFF;
-    if (h->msg() && elem != NONE && (elem & kPayloadBit)) {
-      // message record: 6 payload rows (kernels.hip emit_msg)
-      if (h->drain_rec + kPayloadRows >= nrec) return ZBHIP_EDEVICE;
-      const uint2* pl = rows + h->drain_rec + 1;
-      auto ll = [](uint2 v) { return (long long)(((unsigned long long)v.y << 32) | v.x); };
-      if (!message_code(c6, r)) return ZBHIP_EDEVICE;
-      const uint32_t el = elem & 0xFFF;
-      r.correlation_key = pl[0].x;
-      r.message_name = (uint16_t)(pl[0].y & 0xFFFF);
-      r.bpmn_process_id = (uint16_t)(pl[0].y >> 16);
-      r.key = h->resolve_ref(ll(pl[1]));
-      r.scope_key = h->resolve_ref(ll(pl[2]));
-      r.process_instance_key = h->resolve_ref(ll(pl[3]));
-      r.message_key = h->resolve_ref(ll(pl[4]));
-      r.partition = (int32_t)(pl[5].x & 0xFFFF);
-      r.interrupting = (uint8_t)(pl[5].x >> 16);
-      r.element_idx = el == kNoElem ? -1 : (int32_t)el;
-      r.process_idx = el == kNoElem || proc == NONE ? -1 : proc;
-      if (rej) {
-        r.record_type = ZBHIP_RT_REJECTION;
-        r.reason = fl & 0xF;
-        r.reason_arg = fl >> 4;
-        r.rejection_type = rejection_type_of(r.reason);
-      }
-      out[k++] = r;
-      h->drain_rec += 1 + kPayloadRows;
-      ++h->drain_ord;
-      continue;
-    }
+// One compact row of a plain (non-message) record -> zbhip_record: relabelled keys, record /
+// value type and intent from the row code, document references.  Read-only on the handle, so the
+// bulk drain runs it from several threads.
+static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w, uint32_t ord, zbhip_record& r) {
+  const zbhip_command& cm = h->h_cmds[c];
+  const int64_t doc = cm.doc_count ? h->doc_base + cm.doc_begin : -1;
+  const uint32_t key_ord = w.x & 0xFFFF, aux_ord = w.x >> 16, elem = w.y & 0xFFFF;
+  const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
+  const bool rej = code & kRejectBit;
+  const uint32_t c6 = code & 0x3F;
+  const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
+  r = zbhip_record{};
+  r.source_index = h->source_base + (int64_t)c;
+  r.rejection_type = ZBHIP_REJ_NONE;
+  r.ordinal = (uint16_t)ord;
+  r.aux = -1;
+  r.message_key = -1;
+  r.correlation_key = ZBHIP_NO_STRING;
+  r.message_name = 0xFFFF;
+  r.bpmn_process_id = 0xFFFF;
     r.key = h->key_of(inst, key_ord);
     r.scope_key = aux_ord == NONE ? -1 : h->key_of(inst, aux_ord);
     r.process_instance_key = h->key_of(inst, 0);
@@ -1059,6 +1018,107 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
       } else {
         r.rejection_type = ZBHIP_REJ_INVALID_STATE;
       }
+    }
+  return ZBHIP_OK;
+}
+
+int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
+  if (!h || (cap && !out)) return ZBHIP_EINVAL;
+  if (n_out) *n_out = 0;
+  if (!h->results) return ZBHIP_ESTATE;
+  if (!h->msg() && h->drain_cmd == 0 && h->drain_rec == 0 && h->h_out.size() >= kBulkDrainMin &&
+      cap >= h->h_out.size()) {
+    // whole window at once: record i of command c goes to out[first(c) + i] (one row per record
+    // without message payloads), so command ranges expand independently on host threads
+    const size_t n = h->n_cmds;
+    std::vector<size_t> first(n + 1, 0);
+    for (size_t c = 0; c < n; ++c) first[c + 1] = first[c] + (h->h_hdr[c].x & 0xFFFF);
+    if (first[n] != h->h_out.size()) return ZBHIP_EDEVICE;
+    const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::atomic<int> err{0};
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < T; ++t)
+      pool.emplace_back([&, t]() {
+        // commands split by record count, so every thread expands about total / T records
+        const size_t lo = std::lower_bound(first.begin(), first.end(), first[n] * t / T) - first.begin();
+        const size_t hi = std::lower_bound(first.begin(), first.end(), first[n] * (t + 1) / T) - first.begin();
+        for (size_t c = lo; c < hi && c < n; ++c) {
+          const uint2* rows = h->h_out.data() + h->h_off[c];
+          const uint32_t nrec = h->h_hdr[c].x & 0xFFFF;
+          for (uint32_t i = 0; i < nrec; ++i) {
+            const int rc = expand_plain(h, c, h->h_cmds[c].instance, rows[i], i, out[first[c] + i]);
+            if (rc) { err.store(rc); return; }
+          }
+        }
+      });
+    for (auto& th : pool) th.join();
+    if (err.load()) return err.load();
+    h->drain_cmd = n;
+    if (n_out) *n_out = first[n];
+    return ZBHIP_OK;
+  }
+  size_t k = 0;
+  while (k < cap && h->drain_cmd < h->n_cmds) {
+    const size_t c = h->drain_cmd;
+    const uint2 hd = h->h_hdr[c];
+    const uint32_t nrec = hd.x & 0xFFFF;
+    if (h->drain_rec >= nrec) {
+      ++h->drain_cmd;
+      h->drain_rec = 0;
+      h->drain_ord = 0;
+      continue;
+    }
+    const zbhip_command& cm = h->h_cmds[c];
+    // the instance the records refer to: the command's, or the one a message batch loaded
+    const uint32_t inst = h->msg() && slot_kind(cm.kind) ? h->h_hdr2[c].x : cm.instance;
+    const uint2* rows = h->h_out.data() + h->h_off[c];
+    const uint2 w = rows[h->drain_rec];
+    const uint32_t elem = w.y & 0xFFFF;
+    const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
+    const bool rej = code & kRejectBit;
+    const uint32_t c6 = code & 0x3F;
+    const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
+    zbhip_record r{};
+    r.source_index = h->source_base + (int64_t)c;
+    r.rejection_type = ZBHIP_REJ_NONE;
+    r.ordinal = (uint16_t)h->drain_ord;
+    r.aux = -1;
+    r.message_key = -1;
+    r.correlation_key = ZBHIP_NO_STRING;
+    r.message_name = 0xFFFF;
+    r.bpmn_process_id = 0xFFFF;
+    if (h->msg() && elem != NONE && (elem & kPayloadBit)) {
+      // message record: 6 payload rows (kernels.hip emit_msg)
+      if (h->drain_rec + kPayloadRows >= nrec) return ZBHIP_EDEVICE;
+      const uint2* pl = rows + h->drain_rec + 1;
+      auto ll = [](uint2 v) { return (long long)(((unsigned long long)v.y << 32) | v.x); };
+      if (!message_code(c6, r)) return ZBHIP_EDEVICE;
+      const uint32_t el = elem & 0xFFF;
+      r.correlation_key = pl[0].x;
+      r.message_name = (uint16_t)(pl[0].y & 0xFFFF);
+      r.bpmn_process_id = (uint16_t)(pl[0].y >> 16);
+      r.key = h->resolve_ref(ll(pl[1]));
+      r.scope_key = h->resolve_ref(ll(pl[2]));
+      r.process_instance_key = h->resolve_ref(ll(pl[3]));
+      r.message_key = h->resolve_ref(ll(pl[4]));
+      r.partition = (int32_t)(pl[5].x & 0xFFFF);
+      r.interrupting = (uint8_t)(pl[5].x >> 16);
+      r.element_idx = el == kNoElem ? -1 : (int32_t)el;
+      r.process_idx = el == kNoElem || proc == NONE ? -1 : proc;
+      if (rej) {
+        r.record_type = ZBHIP_RT_REJECTION;
+        r.reason = fl & 0xF;
+        r.reason_arg = fl >> 4;
+        r.rejection_type = rejection_type_of(r.reason);
+      }
+      out[k++] = r;
+      h->drain_rec += 1 + kPayloadRows;
+      ++h->drain_ord;
+      continue;
+    }
+    {
+      const int rc = expand_plain(h, c, inst, w, h->drain_ord, r);
+      if (rc) return rc;
     }
     out[k++] = r;
     ++h->drain_rec;
