@@ -152,6 +152,9 @@ struct zbhip_handle {
   // key relabelling (DbKeyGenerator order)
   int64_t key_counter = 0;
   bool relabel_ok = true;
+  // plan_rounds: (stamp, last round) per subject
+  std::vector<std::pair<uint32_t, uint32_t>> plan_last;
+  uint32_t plan_stamp = 0;
   std::vector<std::vector<std::pair<uint16_t, int64_t>>> hist;
   std::vector<uint16_t> inst_proc;
   std::vector<BatchRef> batches;
@@ -563,8 +566,18 @@ static bool slot_kind(uint8_t k) {
 static void plan_rounds(zbhip_handle* h) {
   h->round_begin.clear();
   h->h_order.clear();
-  std::unordered_map<uint64_t, uint32_t> last;
-  last.reserve(h->n_cmds * 2);
+  // last round per subject in a flat table (instances, then correlation slots), valid where its
+  // stamp is the current one: no hashing and no clearing per window
+  const size_t n_inst = h->cfg.max_instances;
+  if (h->plan_last.size() < n_inst + h->st.n_slots) h->plan_last.assign(n_inst + h->st.n_slots, {0u, 0u});
+  auto next_stamp = [h]() {
+    if (++h->plan_stamp == 0) {  // wrapped: forget every entry
+      std::fill(h->plan_last.begin(), h->plan_last.end(), std::make_pair(0u, 0u));
+      h->plan_stamp = 1;
+    }
+    return h->plan_stamp;
+  };
+  uint32_t stamp = next_stamp();
   std::vector<uint32_t> round_of(h->n_cmds);
   uint32_t max_round = 0, epoch = 0;
   int cls = -1;
@@ -572,13 +585,12 @@ static void plan_rounds(zbhip_handle* h) {
     const bool sk = slot_kind(h->h_cmds[i].kind);
     if (h->msg() && cls >= 0 && (int)sk != cls && i > 0) {
       epoch = max_round + 1;
-      last.clear();
+      stamp = next_stamp();
     }
     cls = (int)sk;
-    const uint64_t subj = ((uint64_t)sk << 32) | h->h_cmds[i].instance;
-    auto it = last.find(subj);
-    uint32_t r = it == last.end() ? epoch : it->second + 1;
-    last[subj] = r;
+    auto& e = h->plan_last[(sk ? n_inst : 0) + h->h_cmds[i].instance];  // bounds: validate()
+    const uint32_t r = e.first == stamp ? e.second + 1 : epoch;
+    e = {stamp, r};
     round_of[i] = r;
     max_round = std::max(max_round, r);
   }
