@@ -126,7 +126,7 @@ def run_msg(args, world, rank, local_rank, dist):
                        (len(mine),))
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
-    exch = LocalExchange(parts, 4 * n, dev) if world == 1 else DeviceExchange()
+    exch = LocalExchange(parts, 4 * n, dev) if world == 1 else DeviceExchange(max_entries=4 * n, device=dev)
     staging = torch.empty(4 * n * XPART_BYTES, dtype=torch.uint8, device=dev) if world > 1 else None
 
     def exchange_until_quiet(flags):
@@ -293,7 +293,34 @@ def main():
     ap.add_argument("--virtual-partitions", type=int, default=1,
                     help="--config msg on one GPU: partitions hosted by this process (exchange by device copies)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` without a launcher: start one rank per GPU (spawned interpreters; this
+        # process never touches the GPU) and exit with the ranks' status
+        import torch.multiprocessing as mp
+        port = _free_port()
+        ctx = mp.start_processes(_spawned_rank, args=(args.gpus, port, sys.argv[1:]), nprocs=args.gpus,
+                                 join=True, start_method="spawn")
+        return ctx
+    run_rank(args)
 
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawned_rank(rank, world, port, argv):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.argv = [sys.argv[0]] + list(argv)
+    main()
+
+
+def run_rank(args):
     import numpy as np
     import torch
 
@@ -305,6 +332,8 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # one partition per GPU: the ranks the launcher started are the GPUs measured
+        assert dist.get_world_size() == world and (args.gpus in (1, world)), (dist.get_world_size(), args.gpus)
     torch.cuda.set_device(local_rank)
     if args.config == "msg":
         return run_msg(args, world, rank, local_rank, dist)

@@ -385,6 +385,11 @@ int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_ou
  * The outbox is handed out once: later calls before the next run report zero counts. */
 int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32_t* counts);
 
+/* Same without a host wait: the per-target counts (uint32[partition_count]) are copied to dev_counts
+ * (device memory) asynchronously on the handle's stream -- what a device-resident all-to-all
+ * exchange feeds to its count collective, so an exchange round needs a single host sync. */
+int zbhip_outbox_device_async(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, void* dev_counts);
+
 /* Copies bucketed outbox entries [first, first + count) (zbhip_outbox_device order) to dev_dst,
  * asynchronously on the handle's stream. */
 int zbhip_outbox_copy(zbhip_handle* h, void* dev_dst, size_t first, size_t count);

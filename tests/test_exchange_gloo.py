@@ -1,8 +1,9 @@
 """The N>1 exchange path on CPU: two processes (gloo, world size 2), one partition each (the CPU
 oracle stands in for the device partition), outboxes bucketed by target partition and exchanged
-with DeviceExchange.send (all_to_all_single of counts, then of the 48-byte commands: the same calls
-RCCL runs on the GPUs).  The result must equal the single-process cluster driven by
-exchange.route()."""
+with DeviceExchange (the count all_gather and the all_to_all_single of the 48-byte commands: the
+same calls RCCL runs on the GPUs).  The result must equal the single-process cluster driven by
+exchange.route().  The GPU twin (libzbhip partitions in every rank) is
+tests/test_gpu_multiprocess.py."""
 import json
 import os
 import socket
@@ -31,6 +32,41 @@ def _bucket(ob):
     return ob[order], counts
 
 
+class _OraclePartition:
+    """The partition surface DeviceExchange.exchange_partition drives (outbox_device_async,
+    outbox_copy, submit_xparts_device, run) over the CPU oracle; "device" buffers are host memory
+    (CPU tensors of the gloo path)."""
+
+    def __init__(self, o, on_window):
+        self.o = o
+        self.on_window = on_window
+        self.ob = abi.make_xparts(0)
+        self.pending = None
+
+    def outbox_device_async(self, counts_ptr):
+        import ctypes
+        self.bucketed, counts = _bucket(self.ob)
+        self.ob = abi.make_xparts(0)  # handed out once
+        c = np.asarray(counts, dtype=np.int32)
+        ctypes.memmove(counts_ptr, c.ctypes.data, c.nbytes)
+        return 0
+
+    def outbox_copy(self, dst, first, count):
+        import ctypes
+        src = np.ascontiguousarray(self.bucketed[first:first + count])
+        ctypes.memmove(dst, src.ctypes.data, src.nbytes)
+
+    def submit_xparts_device(self, ptr, n):
+        import ctypes
+        buf = (ctypes.c_uint8 * (n * abi.XPART_DTYPE.itemsize)).from_address(ptr)
+        self.pending = np.frombuffer(bytes(buf), dtype=abi.XPART_DTYPE)
+
+    def run(self, flags=0):
+        from zeebe_amd.exchange import window_from_xparts
+        cmds, xp = window_from_xparts(self.pending)
+        self.ob = self.on_window(cmds, xp)
+
+
 def _rank_main(rank, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -50,20 +86,15 @@ def _rank_main(rank, port, out_dir):
         log.append([phase, [abi.record_tuple(r) for r in recs]])
         return ob
 
+    staging = torch.empty(64 * N * abi.XPART_DTYPE.itemsize, dtype=torch.uint8)
+
     def exchange(phase, ob):
+        part = _OraclePartition(o, lambda cmds, xp: window(phase, cmds, None, xp))
+        part.ob = ob
         for _ in range(6):
-            bucketed, counts = _bucket(ob)
-            payload = torch.from_numpy(bucketed.view(np.uint8).copy())
-            inbox, got = ex.send(payload, counts)
-            total = torch.tensor([got])
-            dist.all_reduce(total)
-            if int(total) == 0:
+            got, total = ex.exchange_partition(part, staging)
+            if total == 0:
                 return
-            ob = abi.make_xparts(0)
-            if got:
-                xp = np.frombuffer(inbox.numpy().tobytes(), dtype=abi.XPART_DTYPE)
-                cmds, xp = window_from_xparts(xp)
-                ob = window(phase, cmds, None, xp)
 
     c = create_commands(N)
     c["doc_count"] = 1

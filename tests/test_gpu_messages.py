@@ -98,7 +98,7 @@ def test_gpu_appendix_a5(case):
     assert_same_state(gpu, orc)
 
 
-@pytest.mark.parametrize("P", [1, 2, 3])
+@pytest.mark.parametrize("P", [1, 2, 3, 8])
 def test_gpu_cluster_parity(P):
     n = 48
     gpu, orc = clusters(P, n)

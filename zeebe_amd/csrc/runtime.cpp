@@ -806,7 +806,6 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
                           h->d_xout, h->st, (long long)h->cfg.partition_id << 51, h->stream));
     h->bucketed = false;
     h->outbox_taken = false;
-    for (auto& c : h->h_cmds) h->published |= c.kind == ZBHIP_CMD_PUBLISH;
   }
   if (timed) HIPCHK(hipEventRecord(e1, h->stream));
   h->stats.launches = (uint32_t)spans.size();
@@ -818,11 +817,28 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   h->drain_ord = 0;
   h->results = false;
 
-  if (!want || h->external) {
+  if (!want) {
     // benchmarking mode: nothing is copied back and nothing waits; keys are not relabelled
     h->relabel_ok = false;
     h->stats_dirty = true;
     return (int)n;
+  }
+  if (h->external) {
+    // a device-resident window with results (e.g. an exchange inbox in drain mode): the host
+    // bookkeeping below reads the window's commands, documents and received commands
+    h->h_cmds.resize(n);
+    h->h_docs.resize(h->n_docs);
+    h->h_xparts.resize(h->n_xparts);
+    if (n) HIPCHK(hipMemcpyAsync(h->h_cmds.data(), P.cmds, n * sizeof(zbhip_command), hipMemcpyDeviceToHost, h->stream));
+    if (h->n_docs && P.docs)
+      HIPCHK(hipMemcpyAsync(h->h_docs.data(), P.docs, h->n_docs * sizeof(zbhip_doc_entry), hipMemcpyDeviceToHost, h->stream));
+    if (h->n_xparts && h->ext_xparts)
+      HIPCHK(hipMemcpyAsync(h->h_xparts.data(), h->ext_xparts, h->n_xparts * sizeof(zbhip_xpart_cmd),
+                            hipMemcpyDeviceToHost, h->stream));
+  }
+  if (h->msg()) {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    for (auto& c : h->h_cmds) h->published |= c.kind == ZBHIP_CMD_PUBLISH;
   }
 
   // ---- results: headers + records gathered into log order (drain path, off the hot loop) ----
@@ -1269,6 +1285,26 @@ int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32
   HIPCHK(hipMemcpyAsync(counts, h->d_xcount, parts * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->outbox_taken = true;
+  return ZBHIP_OK;
+}
+
+int zbhip_outbox_device_async(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, void* dev_counts) {
+  if (!h || !dev_out || !dev_counts) return ZBHIP_EINVAL;
+  if (!h->msg() || !h->ran) return ZBHIP_ESTATE;
+  const uint32_t parts = (uint32_t)std::max(1, h->cfg.partition_count);
+  if (parts > 1024) return ZBHIP_EINVAL;
+  if (!h->bucketed) {
+    HIPCHK(launch_bucket(h->d_cmd_hdr, h->d_cmd_hdr2, h->d_xout, (uint32_t)h->n_cmds, parts, h->d_blk_cnt,
+                         h->d_xcount, h->d_xbucket, h->stream));
+    h->bucketed = true;
+  }
+  *dev_out = h->d_xbucket;
+  if (h->outbox_taken) {
+    HIPCHK(hipMemsetAsync(dev_counts, 0, parts * sizeof(uint32_t), h->stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(dev_counts, h->d_xcount, parts * sizeof(uint32_t), hipMemcpyDeviceToDevice, h->stream));
+    h->outbox_taken = true;
+  }
   return ZBHIP_OK;
 }
 

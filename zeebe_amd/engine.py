@@ -174,6 +174,13 @@ class Partition:
         check(self.L.zbhip_outbox_device(self.h, C.byref(ptr), counts.ctypes.data), "zbhip_outbox_device")
         return ptr.value or 0, counts
 
+    def outbox_device_async(self, dev_counts):
+        """Device pointer of the bucketed outbox; the per-target counts (uint32) are copied to the
+        device buffer dev_counts on the partition's stream (no host wait)."""
+        ptr = C.c_void_p()
+        check(self.L.zbhip_outbox_device_async(self.h, C.byref(ptr), dev_counts), "zbhip_outbox_device_async")
+        return ptr.value or 0
+
     def run(self, flags=0):
         return check(self.L.zbhip_run(self.h, flags), "zbhip_run")
 

@@ -63,14 +63,18 @@ class LocalExchange:
         self.sizes = [0] * len(parts)
 
     def step(self):
+        import torch
         P = len(self.parts)
-        buckets = [p.outbox_device()[1] for p in self.parts]
+        mat = torch.zeros((P, P), dtype=torch.int32, device=self.inbox[0].device)
+        for s_, p in enumerate(self.parts):  # counts to the device, one host wait for all of them
+            p.outbox_device_async(mat[s_].data_ptr())
+        buckets = mat.cpu().numpy().astype(np.int64)
         for t in range(P):
             off = 0
-            for s_, counts in enumerate(buckets):
-                c = int(counts[t])
+            for s_ in range(P):
+                c = int(buckets[s_, t])
                 if c:
-                    first = int(counts[:t].sum())
+                    first = int(buckets[s_, :t].sum())
                     self.parts[s_].outbox_copy(self.inbox[t].data_ptr() + off * XPART_BYTES, first, c)
                     off += c
             self.sizes[t] = off
@@ -88,36 +92,89 @@ class LocalExchange:
 
 class DeviceExchange:
     """All-to-all of device-resident outboxes between the ranks of a process group (rank r =
-    partition r + 1).  ``send`` takes the outbox as a uint8 device tensor already bucketed by
-    target (``zbhip_outbox_device``) and the per-target counts; it returns the received bucket
-    concatenation (uint8 tensor of 48-byte commands, sources in rank order) and its length."""
+    partition r + 1), one exchange round per call of :meth:`exchange_partition`:
+
+    1. the partition buckets its outbox by target on the device and copies the per-target counts
+       into a device buffer (``zbhip_outbox_device_async``, no host wait);
+    2. one ``all_gather`` of the counts: every rank learns the whole P x P send matrix, i.e. its
+       receive splits and the global total (the round's termination test) -- the round's only
+       host synchronisation;
+    3. one ``all_to_all_single`` of the 48-byte commands with those splits.  With the ``nccl``
+       backend this is RCCL over xGMI (each GPU pair on its own link, no ring);
+    4. the received commands (sources in rank order, each in send order: the order the oracle
+       cluster uses) become the partition's next window, built on the device
+       (``zbhip_submit_xparts_device``), and run.
+
+    With the ``gloo`` backend (CPU collectives: the multi-process tests, several ranks sharing one
+    GPU) the counts and commands are staged through host memory; the partition side is the same.
+    """
 
     XPART_BYTES = abi.XPART_DTYPE.itemsize
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, max_entries=0, device=None):
+        import torch
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.host = dist.get_backend(group) == "gloo"
+        self.device = device
+        self.max_entries = max_entries
+        self.inbox = None
+        if max_entries and device is not None:
+            self.inbox = torch.empty(max_entries * self.XPART_BYTES, dtype=torch.uint8, device=device)
+        self.rounds = 0
+        self.sent = 0
+
+    def _inbox(self, n, device):
+        import torch
+        if self.inbox is None or self.inbox.numel() < n * self.XPART_BYTES:
+            self.inbox = torch.empty(max(n, self.max_entries) * self.XPART_BYTES, dtype=torch.uint8, device=device)
+        return self.inbox
 
     def exchange_partition(self, part, staging, flags=0):
-        """One exchange step for this rank's partition: send its device outbox, receive its inbox
-        (into ``staging``, a uint8 device tensor), submit and run it.  Returns (received, total
-        received over all ranks); every rank calls it the same number of times."""
+        """One exchange round for this rank's partition: send its device outbox, receive its inbox,
+        submit and run it.  ``staging`` is a uint8 device tensor of at least the outbox's bytes.
+        Returns (received, total sent over all ranks); every rank calls it the same number of
+        times, and a round with total 0 ends the exchange."""
         import torch
-        ptr, counts = part.outbox_device()
-        n = int(counts.sum())
-        if n:
-            part.outbox_copy(staging.data_ptr(), 0, n)
-        inbox, got = self.send(staging, counts)
-        total = torch.tensor([got], dtype=torch.int64, device=staging.device)
-        self.dist.all_reduce(total, group=self.group)
-        if got:
-            part.submit_xparts_device(inbox.data_ptr(), got)
+        dist, P, B = self.dist, self.world, self.XPART_BYTES
+        dev = staging.device
+        cnt = torch.zeros(P, dtype=torch.int32, device=dev)
+        part.outbox_device_async(cnt.data_ptr())
+        if self.host:
+            cnt = cnt.cpu()
+        rows = [torch.empty_like(cnt) for _ in range(P)]
+        dist.all_gather(rows, cnt, group=self.group)
+        mat = torch.stack(rows).cpu().numpy().astype(np.int64)  # [source][target]
+        total = int(mat.sum())
+        if total == 0:
+            return 0, 0
+        send = [int(x) for x in mat[self.rank]]
+        recv = [int(x) for x in mat[:, self.rank]]
+        n_send, n_recv = sum(send), sum(recv)
+        if n_send:
+            part.outbox_copy(staging.data_ptr(), 0, n_send)
+        src = staging[: n_send * B]
+        if self.host:
+            src = src.cpu()
+            out = torch.empty(n_recv * B, dtype=torch.uint8)
+        else:
+            out = self._inbox(n_recv, dev)[: n_recv * B]
+        dist.all_to_all_single(out, src, [r * B for r in recv], [s * B for s in send], group=self.group)
+        if self.host and n_recv:
+            out = self._inbox(n_recv, dev)[: n_recv * B].copy_(out)
+        self.rounds += 1
+        self.sent += n_send
+        if n_recv:
+            part.submit_xparts_device(out.data_ptr(), n_recv)
             part.run(flags)
-        return got, int(total.item())
+        return n_recv, total
 
     def send(self, outbox_bytes, counts):
+        """Host-driven form (CPU tests): ``outbox_bytes`` already bucketed by target, ``counts`` per
+        target; returns the received bucket concatenation and its length."""
         import torch
         dist = self.dist
         dev = outbox_bytes.device
