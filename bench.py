@@ -81,7 +81,7 @@ def run_msg(args, world, rank, local_rank, dist):
     vp = args.virtual_partitions if world == 1 else 1
     P = world * vp  # partitions in the cluster
     n = args.instances or 1_000_000
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = torch.cuda.Stream(device=dev).cuda_stream  # one stream shared by the partitions (exchange order)
     my_parts = list(range(rank * vp + 1, rank * vp + vp + 1))
     parts = [Partition(partition_id=p, partition_count=P, device=local_rank, max_instances=n, max_commands=4 * n,
                        max_correlation_keys=n * P, max_records_per_batch=128, stream=stream) for p in my_parts]

@@ -390,6 +390,10 @@ int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32
  * exchange feeds to its count collective, so an exchange round needs a single host sync. */
 int zbhip_outbox_device_async(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, void* dev_counts);
 
+/* The hipStream_t the handle launches on (the configured stream, or the handle's own): callers that
+ * order their own device work against the handle's (an exchange's collectives) use this stream. */
+void* zbhip_stream(zbhip_handle* h);
+
 /* Copies bucketed outbox entries [first, first + count) (zbhip_outbox_device order) to dev_dst,
  * asynchronously on the handle's stream. */
 int zbhip_outbox_copy(zbhip_handle* h, void* dev_dst, size_t first, size_t count);

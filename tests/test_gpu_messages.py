@@ -180,7 +180,7 @@ def test_gpu_device_exchange_runs_the_protocol(P):
     from zeebe_amd.exchange import LocalExchange
     n = 512
     dev = torch.device("cuda", 0)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = torch.cuda.Stream(device=dev).cuda_stream  # one stream shared by the partitions (exchange order)
     parts = [Partition(partition_id=p, partition_count=P, max_instances=n, max_commands=4 * n,
                        max_correlation_keys=n * P, max_records_per_batch=128, stream=stream) for p in range(1, P + 1)]
     keys = ["k-%d-%d" % (p, i) for p in range(1, P + 1) for i in range(n)]

@@ -41,7 +41,7 @@ def _rank_main(rank, P, port, out_dir):
     from zeebe_amd.exchange import XPART_BYTES, DeviceExchange
     dist.init_process_group("gloo", rank=rank, world_size=P)
     dev = torch.device("cuda", 0)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = torch.cuda.Stream(device=dev).cuda_stream  # one stream shared by the partitions (exchange order)
     part = Partition(partition_id=rank + 1, partition_count=P, max_instances=N, max_commands=4 * N * P,
                      max_correlation_keys=N * P, max_records_per_batch=256, stream=stream)
     part.deploy(XML)

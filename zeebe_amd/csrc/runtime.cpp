@@ -1288,6 +1288,8 @@ int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32
   return ZBHIP_OK;
 }
 
+void* zbhip_stream(zbhip_handle* h) { return h ? reinterpret_cast<void*>(h->stream) : nullptr; }
+
 int zbhip_outbox_device_async(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, void* dev_counts) {
   if (!h || !dev_out || !dev_counts) return ZBHIP_EINVAL;
   if (!h->msg() || !h->ran) return ZBHIP_ESTATE;

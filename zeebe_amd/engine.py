@@ -58,6 +58,7 @@ class Partition:
         self.h = h
         self.partition_id = partition_id
         self.partition_count = partition_count
+        self.device = device
         self.processes = []
         self.max_commands = max_commands
 
@@ -173,6 +174,14 @@ class Partition:
         counts = np.zeros(max(1, self.partition_count), dtype=np.uint32)
         check(self.L.zbhip_outbox_device(self.h, C.byref(ptr), counts.ctypes.data), "zbhip_outbox_device")
         return ptr.value or 0, counts
+
+    def torch_stream(self):
+        """The partition's HIP stream as a torch stream: device work that must be ordered with the
+        partition's launches (exchange buffers, collectives) is issued on it."""
+        import torch
+        if getattr(self, "_tstream", None) is None:
+            self._tstream = torch.cuda.ExternalStream(self.L.zbhip_stream(self.h), device=torch.device("cuda", self.device))
+        return self._tstream
 
     def outbox_device_async(self, dev_counts):
         """Device pointer of the bucketed outbox; the per-target counts (uint32) are copied to the

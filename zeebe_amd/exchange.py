@@ -64,6 +64,14 @@ class LocalExchange:
 
     def step(self):
         import torch
+        streams = {p.L.zbhip_stream(p.h) for p in self.parts}
+        if len(streams) != 1:  # the copies between partitions are ordered by one stream
+            raise ValueError("LocalExchange: the partitions must launch on one stream")
+        with torch.cuda.stream(self.parts[0].torch_stream()):
+            return self._step()
+
+    def _step(self):
+        import torch
         P = len(self.parts)
         mat = torch.zeros((P, P), dtype=torch.int32, device=self.inbox[0].device)
         for s_, p in enumerate(self.parts):  # counts to the device, one host wait for all of them
@@ -138,6 +146,13 @@ class DeviceExchange:
         submit and run it.  ``staging`` is a uint8 device tensor of at least the outbox's bytes.
         Returns (received, total sent over all ranks); every rank calls it the same number of
         times, and a round with total 0 ends the exchange."""
+        import torch
+        if staging.device.type != "cuda":  # host-only partitions (CPU tests)
+            return self._exchange(part, staging, flags)
+        with torch.cuda.stream(part.torch_stream()):  # ordered with the partition's launches
+            return self._exchange(part, staging, flags)
+
+    def _exchange(self, part, staging, flags):
         import torch
         dist, P, B = self.dist, self.world, self.XPART_BYTES
         dev = staging.device
