@@ -84,7 +84,8 @@ def run_msg(args, world, rank, local_rank, dist):
     stream = torch.cuda.Stream(device=dev).cuda_stream  # one stream shared by the partitions (exchange order)
     my_parts = list(range(rank * vp + 1, rank * vp + vp + 1))
     parts = [Partition(partition_id=p, partition_count=P, device=local_rank, max_instances=n, max_commands=4 * n,
-                       max_correlation_keys=n * P, max_records_per_batch=128, stream=stream) for p in my_parts]
+                       max_correlation_keys=n * P, max_records_per_batch=128, stream=stream,
+                       trusted_device_windows=True) for p in my_parts]
     xml = bpmn.message_catch_process()
     t_setup = time.perf_counter()
     blob_parts, offs = [], [0]
@@ -348,7 +349,8 @@ def run_rank(args):
     # the partition launches on a torch stream, so torch.cuda.Event brackets its kernels directly
     pstream = torch.cuda.Stream(device=torch.device("cuda", local_rank))
     part = Partition(partition_id=rank + 1, partition_count=world, device=local_rank, max_instances=n,
-                     max_commands=n, max_records_per_batch=recs_per_batch, stream=pstream.cuda_stream)
+                     max_commands=n, max_records_per_batch=recs_per_batch, stream=pstream.cuda_stream,
+                     trusted_device_windows=True)  # one command per instance per window, by construction
     part.deploy(xml)
     name = part.intern("amount") if with_amount else None
 

@@ -214,9 +214,13 @@ typedef struct zbhip_config {
   uint32_t max_doc_entries;      /* variable-document entries per window */
   int64_t initial_key;           /* last key already generated in the partition (0 = fresh) */
   uint32_t max_correlation_keys; /* correlation slots of this message partition (0 = no messages) */
-  uint32_t pad;
+  uint32_t flags;                /* ZBHIP_OPEN_* */
   void* stream;                  /* hipStream_t to launch on (NULL = handle-owned stream) */
 } zbhip_config;
+
+/* The caller guarantees that a device-resident window (zbhip_submit_device*) addresses every subject
+ * at most once; without this flag every device window's subjects are checked on the device first. */
+#define ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS 1u
 
 typedef struct zbhip_handle zbhip_handle;
 
@@ -293,15 +297,21 @@ typedef struct zbhip_xpart_cmd {
   uint32_t pad;
 } zbhip_xpart_cmd;
 
-/* Submits a window of commands in log order.  Host buffers are copied. */
+/* Submits a window of commands in log order.  Host buffers are copied.  Commands of one subject run
+ * in log order (the window is split into launches); a CREATE into an instance slot that an earlier
+ * command of the same window addresses is refused (ZBHIP_EINVAL): a slot is reused only after the
+ * window that ended its instance was drained. */
 int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs,
                  size_t n_docs);
 /* Same, with the window's received cross-partition commands (referenced by doc_begin). */
 int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs,
                     size_t n_docs, const zbhip_xpart_cmd* xparts, size_t n_xparts);
 /* Same, from device-resident arrays already in HBM (no copy; must stay valid until run returns).
- * The caller guarantees that every subject (instance slot / correlation slot) appears at most once
- * in the window (no round planning). */
+ * The window's subjects are checked on the device (one small kernel and a host wait): a window that
+ * addresses a subject (instance slot / correlation slot) more than once is copied to the host and
+ * planned into rounds like a host window; a subject out of range returns ZBHIP_EINVAL.  Handles
+ * opened with ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS skip the check: the caller then guarantees one
+ * command per subject (the benchmark's windows, by construction). */
 int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,
                         const zbhip_doc_entry* dev_docs, size_t n_docs);
 int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,
@@ -414,7 +424,9 @@ int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_o
 int zbhip_command_status(zbhip_handle* h, size_t i, uint32_t* status, uint32_t* reason);
 
 /* Maps a drained (relabelled) key back to (instance, key ordinal) for building
- * follow-up commands (e.g. JOB:COMPLETE).  Returns ZBHIP_EINVAL if unknown. */
+ * follow-up commands (e.g. JOB:COMPLETE).  Returns ZBHIP_EINVAL if unknown or if the instance that
+ * generated it has ended (its slot may hold a new instance): the adapter hands such a command to the
+ * CPU engine, which rejects it (NOT_FOUND) as the reference does. */
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal);
 
 /* Rejection reasons (text formats in zbhip_rejection_reason). */
@@ -489,6 +501,24 @@ typedef void (*zbhip_db_sink)(void* ctx, uint32_t column_family, const uint8_t* 
 int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx);
 /* One canonical row of zbhip_export_state -> its entry; 1 = emitted, 0 = column family not encoded. */
 int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char* row, zbhip_db_sink sink, void* ctx);
+
+/* ---- fallback hand-off (Engine.java:134 onProcessingError, ProcessingStateMachine.java:276-310) --
+ * A command the device did not process (zbhip_command_status != 0) goes to the CPU engine, in log
+ * order.  Every later command of the same subject in the window falls back too (FB_FENCED), so the
+ * CPU engine sees the subject's commands in log order against the state they were left in.  For
+ * each fallback command the adapter
+ *   1. moves the instance to the CPU engine once: zbhip_export_instances_db (its zb-db entries, to
+ *      be written into RocksDB) + zbhip_evict_instances (the slot is freed, its keys stop resolving);
+ *   2. sets DbKeyGenerator to zbhip_key_before(h, i) and runs engine.process(command);
+ *   3. declares the keys that generated: zbhip_set_external_keys(h, i, n).
+ * Keys of the window's later device-processed commands follow those (relabelled at the first
+ * drain / export / resolve, which fixes the window's keys).  Config 5 windows: declared keys must
+ * be 0 (the device already fixed their keys for the exchange). */
+int zbhip_export_instances(zbhip_handle* h, const uint32_t* instances, size_t n, zbhip_state_sink sink, void* ctx);
+int zbhip_export_instances_db(zbhip_handle* h, const uint32_t* instances, size_t n, zbhip_db_sink sink, void* ctx);
+int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n);
+int zbhip_key_before(zbhip_handle* h, size_t i, int64_t* key);
+int zbhip_set_external_keys(zbhip_handle* h, size_t i, uint32_t nkeys);
 
 /* Library build information ("gfx950 …"). */
 const char* zbhip_build_info(void);

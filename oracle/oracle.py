@@ -53,6 +53,9 @@ def lib():
         L.zbo_element_id.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.zbo_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
         L.zbo_run.argtypes = [C.c_void_p]
+        L.zbo_key_counter.restype = C.c_int64
+        L.zbo_key_counter.argtypes = [C.c_void_p]
+        L.zbo_set_key_counter.argtypes = [C.c_void_p, C.c_int64]
         L.zbo_n_records.restype = C.c_size_t
         L.zbo_n_records.argtypes = [C.c_void_p]
         L.zbo_records.restype = C.c_size_t
@@ -167,6 +170,13 @@ class Oracle:
         if clear:
             self.L.zbo_clear_outbox(self.h)
         return out
+
+    def key_counter(self):
+        """DbKeyGenerator's current value (the counter, without the partition bits)."""
+        return self.L.zbo_key_counter(self.h)
+
+    def set_key_counter(self, v):
+        self.L.zbo_set_key_counter(self.h, v)
 
     def run(self):
         r = self.L.zbo_run(self.h)

@@ -830,6 +830,9 @@ class Oracle {
   }
 
   std::string dump_state() const;
+  // DbKeyGenerator's current value (the CPU engine of a fallback hand-off is set to the device's)
+  int64_t key_counter() const { return key_counter_; }
+  void set_key_counter(int64_t v) { key_counter_ = v; }
   uint64_t transitions = 0, completed_instances = 0, commands_processed = 0;
 
  private:
@@ -1976,6 +1979,8 @@ int zbo_subscription_partition(const char* b, size_t len, int partition_count) {
 }
 int32_t zbo_java_hash(const char* b, size_t len) { return java_hash(std::string(b, len)); }
 int zbo_run(void* o) { return static_cast<Oracle*>(o)->run(); }
+int64_t zbo_key_counter(void* o) { return static_cast<Oracle*>(o)->key_counter(); }
+void zbo_set_key_counter(void* o, int64_t v) { static_cast<Oracle*>(o)->set_key_counter(v); }
 
 size_t zbo_n_records(void* o) { return static_cast<Oracle*>(o)->out.size(); }
 size_t zbo_records(void* o, zbhip_record* out, size_t cap) {

@@ -8,11 +8,12 @@ OUT=${OUT:-gpurun_out/ev}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-for spec in ${CONFIGS:-linear10 linear10@10000000 one_task xor forkjoin8 msg}; do
+for spec in ${CONFIGS:-linear10 linear10@10000000 one_task xor forkjoin8 msg msg8}; do
   cfg=${spec%@*}
   args="--config $cfg"
   tag=$cfg
   if [[ $spec == *@* ]]; then args="$args --instances ${spec#*@}"; tag="${cfg}_${spec#*@}"; fi
+  if [[ $spec == msg8 ]]; then args="--config msg --virtual-partitions 8"; fi
   echo "=== bench $tag"
   timeout -k 10 600 python -u bench.py $args --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err \
     || { tail -20 $OUT/bench_$tag.err; exit 1; }

@@ -17,4 +17,10 @@ cat $O/bench.json
 echo "=== bench msg"
 timeout -k 10 600 python -u bench.py --config msg --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_msg.json 2> $O/bench_msg.err || { tail -30 $O/bench_msg.err; exit 1; }
 cat $O/bench_msg.json
+
+if [[ -n "$MSG8" ]]; then
+echo "=== bench msg 8 virtual partitions"
+timeout -k 10 600 python -u bench.py --config msg --virtual-partitions 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_msg8.json 2> $O/bench_msg8.err || { tail -30 $O/bench_msg8.err; exit 1; }
+cat $O/bench_msg8.json
+fi
 echo "=== done"

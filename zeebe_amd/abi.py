@@ -110,12 +110,15 @@ class LogWindow(C.Structure):  # zbhip_log_window
                 ("first_position", C.c_int64), ("timestamp", C.c_int64), ("source_timestamps", C.c_void_p)]
 
 
+OPEN_TRUSTED_DEVICE_WINDOWS = 1
+
+
 class Config(C.Structure):
     _fields_ = [("partition_id", C.c_int32), ("partition_count", C.c_int32), ("device", C.c_int32),
                 ("max_commands_in_batch", C.c_int32), ("max_instances", C.c_uint32),
                 ("max_commands", C.c_uint32), ("max_records_per_batch", C.c_uint32),
                 ("max_doc_entries", C.c_uint32), ("initial_key", C.c_int64), ("max_correlation_keys", C.c_uint32),
-                ("pad", C.c_uint32), ("stream", C.c_void_p)]
+                ("flags", C.c_uint32), ("stream", C.c_void_p)]
 
 
 class Stats(C.Structure):

@@ -1235,6 +1235,7 @@ __device__ __forceinline__ void load_instance_mid(Lane<K>& L, uint32_t inst) {
   if (inst >= N) { set_fail(L, FB_MESSAGE); return; }
   const uint4 h = P.st.hdr[inst];
   const uint32_t proc = h.x & 0xFFFF;
+  if (h.w == P.stamp) { set_fail(L, FB_FENCED); return; }
   if (proc == NONE || !((h.y >> 24) & 1) || proc >= P.n_procs) { set_fail(L, FB_MESSAGE); return; }
   const uint32_t nslots = (h.y >> 8) & 0xFF, nvars = (h.y >> 16) & 0xFF;
   if (nslots > (uint32_t)K::T) { set_fail(L, FB_TABLE); return; }
@@ -1447,6 +1448,14 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
 
   const bool bad_cmd = (slot_kind ? inst >= P.st.n_slots : inst >= N) ||
                        (doc_count && (uint64_t)doc_begin + doc_count > P.n_docs);
+  // fence: an earlier command of this subject in the window fell back (its state was left as it
+  // was), so this one must follow it on the CPU engine in log order
+  uint2 slot_row = make_uint2(0, 0);
+  if constexpr (K::M) {
+    if (slot_kind && !bad_cmd) slot_row = P.st.slot_hdr[inst];
+  }
+  const bool fenced = !bad_cmd && (slot_kind ? slot_row.y == P.stamp : h.w == P.stamp);
+  if (fenced) set_fail(L, FB_FENCED);
   if (slot_kind) h = make_uint4(0xFFFFFFFFu, 0, 0, 0);
   if (bad_cmd) h = make_uint4(0xFFFFFFFFu, 0, 0, 0);
   L.proc = h.x & 0xFFFF;
@@ -1466,7 +1475,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       L.slot_lane = true;
       L.slot = inst;
       L.inst = kNoInst;
-      L.s_next_ord = L.s_first_ord = (uint16_t)P.st.slot_hdr[inst].x;
+      L.s_next_ord = L.s_first_ord = (uint16_t)slot_row.x;
       L.proc = NONE;
     }
   } else if (kind == ZBHIP_CMD_CREATE) {
@@ -1656,9 +1665,21 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     npay = ok ? L.n_pay : 0u;
     P.cmd_hdr2[ci] = make_uint4(L.inst, L.i_first_ord | (nsec << 16), ok ? L.n_out : 0u, npay);
   }
+  if (!ok && !bad_cmd) {  // fence the subject(s) for the rest of the window
+    if (slot_kind) {
+      if constexpr (K::M) P.st.slot_hdr[inst].y = P.stamp;
+    } else {
+      P.st.hdr[inst].w = P.stamp;
+    }
+    if constexpr (K::M) {
+      if (slot_kind && L.inst != kNoInst && L.inst < N) P.st.hdr[L.inst].w = P.stamp;
+    }
+  }
+  const bool ended = ok && !L.pi_live && winst != kNoInst && L.proc != NONE;
   const uint32_t nrec = ok ? L.nrec : 0u;
   P.cmd_hdr[ci] = make_uint2(nrec | (nkeys << 16),
-                             first | ((uint32_t)(ok ? ST_OK : ST_FALLBACK) << 16) | (L.fail << 24));
+                             first | ((uint32_t)(ok ? ST_OK : ST_FALLBACK) << 16) | (L.fail << 24) |
+                                 (ended ? HDR_ENDED : 0u));
   acc.cmd += 1;
   acc.fb += ok ? 0u : 1u;
   acc.rec += nrec - npay;
@@ -2120,26 +2141,50 @@ __global__ __launch_bounds__(kBucketB) void k_bucket_count(BucketParams Q) {
   }
 }
 
-__global__ __launch_bounds__(64) void k_bucket_scan(BucketParams Q, uint32_t nb) {
+// The scan of the per-block counts, target-major (bucket t after buckets 0..t-1, blocks in order):
+// k_bucket_scan_groups scans groups of 1024 block counts per target in parallel (local offsets,
+// group totals), k_bucket_scan_bases turns the few group totals into group bases and the counts.
+constexpr int kScanG = 1024;
+__global__ __launch_bounds__(kScanG) void k_bucket_scan_groups(BucketParams Q, uint32_t nb, uint32_t* grp) {
+  const uint32_t b = blockIdx.x * kScanG + threadIdx.x;
+  __shared__ uint32_t ws[kScanG / 64];
+  for (uint32_t t = 0; t < Q.parts; ++t) {
+    const uint32_t v = b < nb ? Q.blk_cnt[(size_t)b * Q.parts + t] : 0u;
+    const uint32_t inc = wave_incl_scan_u(v);
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (int w = 0; w < kScanG / 64; ++w) {
+      if (w < (int)(threadIdx.x >> 6)) base += ws[w];
+      total += ws[w];
+    }
+    if (b < nb) Q.blk_cnt[(size_t)b * Q.parts + t] = base + inc - v;
+    if (threadIdx.x == 0) grp[(size_t)blockIdx.x * Q.parts + t] = total;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_bucket_scan_bases(BucketParams Q, uint32_t ng, uint32_t* grp) {
   if (threadIdx.x != 0) return;
   uint32_t off = 0;
   for (uint32_t t = 0; t < Q.parts; ++t) {
     const uint32_t start = off;
-    for (uint32_t b = 0; b < nb; ++b) {
-      const uint32_t v = Q.blk_cnt[(size_t)b * Q.parts + t];
-      Q.blk_cnt[(size_t)b * Q.parts + t] = off;
+    for (uint32_t g = 0; g < ng; ++g) {
+      const uint32_t v = grp[(size_t)g * Q.parts + t];
+      grp[(size_t)g * Q.parts + t] = off;
       off += v;
     }
     Q.counts[t] = off - start;
   }
 }
 
-__global__ __launch_bounds__(kBucketB) void k_bucket_scatter(BucketParams Q) {
+__global__ __launch_bounds__(kBucketB) void k_bucket_scatter(BucketParams Q, const uint32_t* grp) {
   const uint32_t c = blockIdx.x * kBucketB + threadIdx.x;
+  const uint32_t g = blockIdx.x / kScanG;
   for (uint32_t t = 0; t < Q.parts; ++t) {
     uint32_t tot;
     const uint32_t mine = entries_to(Q, c, t);
-    uint32_t o = Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] + block_excl_scan(mine, tot);
+    uint32_t o = grp[(size_t)g * Q.parts + t] + Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] + block_excl_scan(mine, tot);
     if (mine) {
       const uint32_t nout = min(Q.cmd_hdr2[c].z, (uint32_t)kOut);
       for (uint32_t j = 0; j < nout; ++j) {
@@ -2157,6 +2202,27 @@ __global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp,
   const zbhip_xpart_cmd x = xp[i];
   const bool pms = x.kind == ZBHIP_CMD_PMS_CREATE || x.kind == ZBHIP_CMD_PMS_CORRELATE;
   cmds[i] = make_uint4(pms ? x.instance : x.correlation_key, x.kind, i, 0);  // zbhip_command layout
+}
+
+// Subject check of a device-resident window (zbhip_submit_device*): every command claims its
+// subject (instance slot, or correlation slot for MESSAGE / MESSAGE_SUBSCRIPTION commands) with the
+// window's stamp; a second claim in the window flags a duplicate (bit 0), a subject out of range or
+// an unknown kind bit 1.  The host then plans the window into rounds (or refuses it).
+__global__ __launch_bounds__(256) void k_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots,
+                                                       uint32_t* seen, uint32_t stamp, uint32_t* flag) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  uint32_t f = 0;
+  if (i < n) {
+    const uint4 c = cmds[i];
+    const uint32_t kind = c.y & 0xFF;
+    const bool sk = kind == ZBHIP_CMD_PUBLISH || kind == ZBHIP_CMD_MSG_SUB_CREATE || kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
+    if (kind < ZBHIP_CMD_CREATE || kind > ZBHIP_CMD_MSG_SUB_CORRELATE || (sk ? c.x >= n_slots : c.x >= n_inst)) {
+      f = 2;
+    } else if (atomicExch(&seen[(sk ? n_inst : 0u) + c.x], stamp) == stamp) {
+      f = 1;
+    }
+  }
+  if (f) atomicOr(flag, f);  // rare: a faulty window
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2245,6 +2311,13 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
   return hipGetLastError();
 }
 
+hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
+                                uint32_t stamp, uint32_t* flag, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_subject_check, dim3((n + 255) / 256), dim3(256), 0, s, cmds, n, n_inst, n_slots, seen, stamp,
+                            flag);
+  return hipGetLastError();
+}
+
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_xpart_window, dim3((n + 255) / 256), dim3(256), 0, s, xp, n, cmds);
   return hipGetLastError();
@@ -2254,9 +2327,12 @@ hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhi
                          uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s) {
   BucketParams Q{cmd_hdr, cmd_hdr2, xout, n, parts, blk_cnt, counts, out};
   const uint32_t nb = (n + kBucketB - 1) / kBucketB;
+  const uint32_t ng = (nb + kScanG - 1) / kScanG;
+  uint32_t* grp = blk_cnt + (size_t)std::max(nb, 1u) * parts;  // [ng][parts] after the block counts
   if (nb) hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBucketB), 0, s, Q);
-  hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(64), 0, s, Q, nb);
-  if (nb) hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBucketB), 0, s, Q);
+  if (nb) hipLaunchKernelGGL(k_bucket_scan_groups, dim3(ng), dim3(kScanG), 0, s, Q, nb, grp);
+  hipLaunchKernelGGL(k_bucket_scan_bases, dim3(1), dim3(64), 0, s, Q, ng, grp);
+  if (nb) hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBucketB), 0, s, Q, grp);
   return hipGetLastError();
 }
 

@@ -32,6 +32,8 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
                           unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
                           zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s);
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s);
+hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
+                                uint32_t stamp, uint32_t* flag, hipStream_t s);
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
                          uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;
@@ -71,6 +73,7 @@ struct BatchRef {
   uint32_t inst;
   uint16_t first_ord;
   uint16_t nkeys;
+  uint32_t gen;  // generation of the subject when the keys were generated (inst_gen)
 };
 
 const char* state_name(int s) {
@@ -152,9 +155,23 @@ struct zbhip_handle {
   // key relabelling (DbKeyGenerator order)
   int64_t key_counter = 0;
   bool relabel_ok = true;
-  // plan_rounds: (stamp, last round) per subject
+  bool finalized = true;           // the last run's key bookkeeping is done (finalize)
+  std::vector<uint32_t> ext_keys;  // keys the CPU engine generated for the window's fallback commands
+  // plan_rounds: (stamp, last round) per subject; window of the last command per instance slot
   std::vector<std::pair<uint32_t, uint32_t>> plan_last;
   uint32_t plan_stamp = 0;
+  std::vector<uint32_t> plan_seen;
+  uint32_t plan_window = 0;
+  // fence stamps of the device windows (StepParams.stamp; hdr.w / slot_hdr.y of a fallen-back subject)
+  uint32_t window_stamp = 0;
+  // device-window subject check (k_subject_check)
+  uint32_t* d_seen = nullptr;
+  uint32_t* d_check_flag = nullptr;
+  uint32_t check_stamp = 0;
+  // resolve_key: the generation of every subject (bumped when an instance is created or ends, so
+  // keys of an earlier instance in a reused slot never resolve); stale entries are compacted away
+  std::vector<uint32_t> inst_gen;
+  size_t batches_compacted = 0;
   std::vector<std::vector<std::pair<uint16_t, int64_t>>> hist;
   std::vector<uint16_t> inst_proc;
   std::vector<BatchRef> batches;
@@ -225,6 +242,8 @@ struct zbhip_handle {
     if (e_ != hipSuccess) return ZBHIP_EDEVICE; \
   } while (0)
 
+static int finalize(zbhip_handle* h);
+
 extern "C" {
 
 const char* zbhip_build_info(void) {
@@ -291,11 +310,13 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   ok = ok && dalloc(&h->d_cmd_hdr2, cfg->max_commands) == hipSuccess &&
        dalloc(&h->d_xparts, cfg->max_commands) == hipSuccess &&
        dalloc(&h->d_key_counter, 1) == hipSuccess && dalloc(&h->d_key_base, cfg->max_commands) == hipSuccess &&
-       dalloc(&h->d_key_blk, (cfg->max_commands + 1023) / 1024 + 1) == hipSuccess && dalloc(&h->d_xcount, 1024) == hipSuccess;
+       dalloc(&h->d_key_blk, (cfg->max_commands + 1023) / 1024 + 1) == hipSuccess && dalloc(&h->d_xcount, 1024) == hipSuccess &&
+       dalloc(&h->d_seen, N + S) == hipSuccess && dalloc(&h->d_check_flag, 1) == hipSuccess;
   if (S) {
     ok = ok && dalloc(&h->d_xout, (size_t)cfg->max_commands * kOut) == hipSuccess &&
          dalloc(&h->d_xbucket, (size_t)cfg->max_commands * kOut) == hipSuccess &&
-         dalloc(&h->d_blk_cnt, ((size_t)cfg->max_commands / 256 + 1) * (size_t)std::max(1, cfg->partition_count)) == hipSuccess;
+         dalloc(&h->d_blk_cnt, ((size_t)cfg->max_commands / 256 + 1 + (size_t)cfg->max_commands / (256 * 1024) + 1) *
+                                   (size_t)std::max(1, cfg->partition_count)) == hipSuccess;
   }
   if (!ok) { zbhip_close(h); return ZBHIP_ENOMEM; }
   if (S) {
@@ -313,6 +334,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   // every slot starts free (proc = 0xFFFF); counters zero
   if (hipMemsetAsync(h->st.hdr, 0xFF, N * sizeof(uint4), h->stream) != hipSuccess ||
       hipMemsetAsync(h->st.join, 0, N * kJoinWords * sizeof(uint32_t), h->stream) != hipSuccess ||
+      hipMemsetAsync(h->d_seen, 0, (N + S) * sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_stats, 0, (64 * 8 + 8) * sizeof(unsigned long long), h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
     zbhip_close(h);
@@ -357,6 +379,8 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_key_counter);
   (void)hipFree(h->d_key_base);
   (void)hipFree(h->d_key_blk);
+  (void)hipFree(h->d_seen);
+  (void)hipFree(h->d_check_flag);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -563,9 +587,24 @@ static bool slot_kind(uint8_t k) {
 // rounds (the reference processes them in log order).  Message commands may touch an instance of
 // this partition and instance commands a correlation slot, so a change between the two classes
 // starts a new epoch: every later command goes to a round after all earlier ones.
-static void plan_rounds(zbhip_handle* h) {
+static int plan_rounds(zbhip_handle* h) {
   h->round_begin.clear();
   h->h_order.clear();
+  // a CREATE into an instance slot that an earlier command of the same window addressed is refused:
+  // the adapter reuses a slot only after the window that ended its instance was drained (records of
+  // both instances would otherwise share the slot's key history)
+  const size_t n_inst0 = h->cfg.max_instances;
+  if (h->plan_seen.size() < n_inst0) h->plan_seen.assign(n_inst0, 0u);
+  if (++h->plan_window == 0) {
+    std::fill(h->plan_seen.begin(), h->plan_seen.end(), 0u);
+    h->plan_window = 1;
+  }
+  for (size_t i = 0; i < h->n_cmds; ++i) {
+    const zbhip_command& c = h->h_cmds[i];
+    if (slot_kind(c.kind)) continue;
+    if (c.kind == ZBHIP_CMD_CREATE && h->plan_seen[c.instance] == h->plan_window) return ZBHIP_EINVAL;
+    h->plan_seen[c.instance] = h->plan_window;
+  }
   // last round per subject in a flat table (instances, then correlation slots), valid where its
   // stamp is the current one: no hashing and no clearing per window
   const size_t n_inst = h->cfg.max_instances;
@@ -594,7 +633,7 @@ static void plan_rounds(zbhip_handle* h) {
     round_of[i] = r;
     max_round = std::max(max_round, r);
   }
-  if (max_round == 0) return;  // single round: identity order
+  if (max_round == 0) return ZBHIP_OK;  // single round: identity order
   std::vector<uint32_t> cnt(max_round + 2, 0);
   for (uint32_t r : round_of) cnt[r + 1]++;
   for (size_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
@@ -602,6 +641,7 @@ static void plan_rounds(zbhip_handle* h) {
   h->h_order.resize(h->n_cmds);
   std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
   for (size_t i = 0; i < h->n_cmds; ++i) h->h_order[pos[round_of[i]]++] = (uint32_t)i;
+  return ZBHIP_OK;
 }
 
 static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t n_docs,
@@ -661,7 +701,9 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
                     const zbhip_xpart_cmd* xparts, size_t n_xparts) {
   if (!h || (n && !cmds) || (n_docs && !docs) || (n_xparts && !xparts)) return ZBHIP_EINVAL;
   if (n > h->cfg.max_commands || n_docs > h->cfg.max_doc_entries || n_xparts > h->cfg.max_commands) return ZBHIP_ENOMEM;
-  int rc = validate(h, cmds, n, n_docs, xparts, n_xparts);
+  int rc = finalize(h);  // the previous window's keys are fixed before its commands are replaced
+  if (rc) return rc;
+  rc = validate(h, cmds, n, n_docs, xparts, n_xparts);
   if (rc) return rc;
   h->external = false;
   h->h_cmds.assign(cmds, cmds + n);
@@ -673,11 +715,15 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
     HIPCHK(hipMemcpyAsync(h->d_xparts, xparts, n_xparts * sizeof(zbhip_xpart_cmd), hipMemcpyHostToDevice, h->stream));
   h->n_cmds = n;
   h->n_docs = n_docs;
+  rc = plan_rounds(h);
+  if (rc) {
+    h->n_cmds = h->n_docs = h->n_xparts = 0;
+    return rc;
+  }
   h->doc_base = h->next_doc_base;
   h->next_doc_base += (int64_t)n_docs;
   h->source_base = h->next_source;
   h->next_source += (int64_t)n;
-  plan_rounds(h);
   if (n) HIPCHK(hipMemcpyAsync(h->d_cmds, cmds, n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
   if (n_docs)
     HIPCHK(hipMemcpyAsync(h->d_docs, docs, n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice, h->stream));
@@ -694,10 +740,44 @@ int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n
   return zbhip_submit_device_ex(h, dev_cmds, n, dev_docs, n_docs, nullptr, 0);
 }
 
+// A device window's subjects are checked on the device (k_subject_check): a window that addresses
+// one subject twice is copied to the host and planned into rounds like a host window (so it runs
+// in log order per subject); a subject out of range refuses the window.  Handles opened with
+// ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS skip the check (the caller guarantees one command per subject).
+static int check_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
+                               size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts, bool* replanned) {
+  *replanned = false;
+  if ((h->cfg.flags & ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS) || n == 0) return ZBHIP_OK;
+  if (++h->check_stamp == 0) {
+    HIPCHK(hipMemsetAsync(h->d_seen, 0, ((size_t)h->cfg.max_instances + h->st.n_slots) * sizeof(uint32_t), h->stream));
+    h->check_stamp = 1;
+  }
+  uint32_t flag = 0;
+  HIPCHK(hipMemsetAsync(h->d_check_flag, 0, sizeof(uint32_t), h->stream));
+  HIPCHK(launch_subject_check(reinterpret_cast<const uint4*>(dev_cmds), (uint32_t)n, h->cfg.max_instances, h->st.n_slots,
+                              h->d_seen, h->check_stamp, h->d_check_flag, h->stream));
+  HIPCHK(hipMemcpyAsync(&flag, h->d_check_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (flag & 2) return ZBHIP_EINVAL;
+  if (!(flag & 1)) return ZBHIP_OK;
+  std::vector<zbhip_command> c(n);
+  std::vector<zbhip_doc_entry> d(n_docs);
+  std::vector<zbhip_xpart_cmd> x(n_xparts);
+  HIPCHK(hipMemcpy(c.data(), dev_cmds, n * sizeof(zbhip_command), hipMemcpyDeviceToHost));
+  if (n_docs) HIPCHK(hipMemcpy(d.data(), dev_docs, n_docs * sizeof(zbhip_doc_entry), hipMemcpyDeviceToHost));
+  if (n_xparts) HIPCHK(hipMemcpy(x.data(), dev_xparts, n_xparts * sizeof(zbhip_xpart_cmd), hipMemcpyDeviceToHost));
+  *replanned = true;
+  return zbhip_submit_ex(h, c.data(), n, d.data(), n_docs, x.data(), n_xparts);
+}
+
 int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
                            size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts) {
   if (!h || (n && !dev_cmds)) return ZBHIP_EINVAL;
   if (n > h->rec_slots) return ZBHIP_ENOMEM;
+  if (int rc0 = finalize(h)) return rc0;
+  bool replanned = false;
+  const int rc = check_device_window(h, dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, &replanned);
+  if (rc || replanned) return rc;
   h->external = true;
   h->ext_xparts = dev_xparts;
   h->n_xparts = n_xparts;
@@ -728,6 +808,69 @@ static hipEvent_t next_event(zbhip_handle* h) {
   return h->tev[h->tev_used++];
 }
 
+// Key relabelling bookkeeping of the last run, in log (source) order: each command's first key
+// (DbKeyGenerator order), the subjects' key histories and the resolve_key table.  Deferred until the
+// window's results are first used, so that the adapter can declare the keys its CPU engine generated
+// for the window's fallback commands (zbhip_set_external_keys) before the keys after them are fixed.
+static int finalize(zbhip_handle* h) {
+  if (!h->results || h->finalized) return ZBHIP_OK;
+  h->finalized = true;
+  const uint32_t n = (uint32_t)h->n_cmds;
+  const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
+  if (h->hist.size() < subjects) {
+    h->hist.resize(subjects);
+    h->inst_proc.resize(h->cfg.max_instances, NONE);
+    h->inst_gen.resize(subjects, 0);
+  }
+  h->h_base.assign(n, 0);
+  for (uint32_t c = 0; c < n; ++c) {
+    const uint2 hd = h->h_hdr[c];
+    const zbhip_command& cm = h->h_cmds[c];
+    const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
+    h->h_base[c] = h->key_counter;
+    if (((hd.y >> 16) & 0xFF) != ST_OK) {  // processed by the CPU engine: the keys it declared
+      h->key_counter += h->ext_keys[c];
+      continue;
+    }
+    if (h->msg() && slot_kind(cm.kind)) {
+      // the correlation slot's keys first, then the instance a local command loaded
+      const uint4 h2 = h->h_hdr2[c];
+      const uint32_t nsec = h2.y >> 16, nprim = nkeys - nsec;
+      const uint32_t subj = h->slot_subject(cm.instance);
+      if (nprim) {
+        h->hist[subj].push_back({(uint16_t)first, h->key_counter + 1});
+        h->batches.push_back({h->key_counter + 1, subj, (uint16_t)first, (uint16_t)nprim, h->inst_gen[subj]});
+      }
+      if (nsec) {
+        h->hist[h2.x].push_back({(uint16_t)(h2.y & 0xFFFF), h->key_counter + 1 + nprim});
+        h->batches.push_back({h->key_counter + 1 + nprim, h2.x, (uint16_t)(h2.y & 0xFFFF), (uint16_t)nsec, h->inst_gen[h2.x]});
+      }
+      if ((hd.y & HDR_ENDED) && h2.x < h->cfg.max_instances) ++h->inst_gen[h2.x];
+      h->key_counter += nkeys;
+      continue;
+    }
+    if (cm.kind == ZBHIP_CMD_CREATE) {  // a new instance in the slot: its own key history
+      h->hist[cm.instance].clear();
+      h->inst_proc[cm.instance] = cm.ref;
+      ++h->inst_gen[cm.instance];
+    }
+    if (nkeys) {
+      h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
+      h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[cm.instance]});
+    }
+    if (hd.y & HDR_ENDED) ++h->inst_gen[cm.instance];  // completed: its job keys no longer resolve
+    h->key_counter += nkeys;
+  }
+  // drop the key-table entries of ended / replaced instances once they outnumber the rest
+  if (h->batches.size() >= 2 * h->batches_compacted + (1u << 20)) {
+    auto live = [h](const BatchRef& b) { return b.gen == h->inst_gen[b.inst]; };
+    h->batches.erase(std::remove_if(h->batches.begin(), h->batches.end(), [&](const BatchRef& b) { return !live(b); }),
+                     h->batches.end());
+    h->batches_compacted = h->batches.size();
+  }
+  return ZBHIP_OK;
+}
+
 int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (!h) return ZBHIP_EINVAL;
   if (h->ran) return ZBHIP_ESTATE;
@@ -737,6 +880,14 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   const bool accumulate = flags & ZBHIP_RUN_ACCUMULATE;
   const uint32_t n = (uint32_t)h->n_cmds;
   const uint32_t B = step_block(h->variant);
+  // fence stamp of this window (0 and 0xFFFFFFFF are never stamps: open-time values of hdr.w and
+  // slot_hdr.y); on wrap-around every stale stamp is cleared first
+  if (++h->window_stamp == 0xFFFFFFFFu) {
+    HIPCHK(hipMemset2DAsync(reinterpret_cast<char*>(h->st.hdr) + 12, sizeof(uint4), 0, 4, h->st.n, h->stream));
+    if (h->st.n_slots)
+      HIPCHK(hipMemset2DAsync(reinterpret_cast<char*>(h->st.slot_hdr) + 4, sizeof(uint2), 0, 4, h->st.n_slots, h->stream));
+    h->window_stamp = 1;
+  }
   if (!accumulate) {
     HIPCHK(hipMemsetAsync(h->d_stats, 0, 64 * 8 * sizeof(unsigned long long), h->stream));
     h->tev_used = 0;
@@ -758,6 +909,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.cmd_hdr = h->d_cmd_hdr;
   P.stats = h->d_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
+  P.stamp = h->window_stamp;
   if (h->msg()) {
     int rc = sync_strings(h);
     if (rc) return rc;
@@ -867,45 +1019,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     }
   if (off != total) return ZBHIP_EDEVICE;
 
-  // key relabelling bookkeeping, in log (source) order
-  const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
-  if (h->hist.size() < subjects) {
-    h->hist.resize(subjects);
-    h->inst_proc.resize(h->cfg.max_instances, NONE);
-  }
-  h->h_base.assign(n, 0);
-  for (uint32_t c = 0; c < n; ++c) {
-    const uint2 hd = h->h_hdr[c];
-    const zbhip_command& cm = h->h_cmds[c];
-    const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
-    h->h_base[c] = h->key_counter;
-    if (((hd.y >> 16) & 0xFF) != ST_OK) continue;
-    if (h->msg() && slot_kind(cm.kind)) {
-      // the correlation slot's keys first, then the instance a local command loaded
-      const uint4 h2 = h->h_hdr2[c];
-      const uint32_t nsec = h2.y >> 16, nprim = nkeys - nsec;
-      const uint32_t subj = h->slot_subject(cm.instance);
-      if (nprim) {
-        h->hist[subj].push_back({(uint16_t)first, h->key_counter + 1});
-        h->batches.push_back({h->key_counter + 1, subj, (uint16_t)first, (uint16_t)nprim});
-      }
-      if (nsec) {
-        h->hist[h2.x].push_back({(uint16_t)(h2.y & 0xFFFF), h->key_counter + 1 + nprim});
-        h->batches.push_back({h->key_counter + 1 + nprim, h2.x, (uint16_t)(h2.y & 0xFFFF), (uint16_t)nsec});
-      }
-      h->key_counter += nkeys;
-      continue;
-    }
-    if (cm.kind == ZBHIP_CMD_CREATE) {
-      h->hist[cm.instance].clear();
-      h->inst_proc[cm.instance] = cm.ref;
-    }
-    if (nkeys) {
-      h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
-      h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys});
-    }
-    h->key_counter += nkeys;
-  }
+  h->ext_keys.assign(n, 0);
+  h->finalized = false;
   h->results = true;
   return (int)n;
 }
@@ -1054,6 +1169,7 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
   if (!h || (cap && !out)) return ZBHIP_EINVAL;
   if (n_out) *n_out = 0;
   if (!h->results) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
   if (!h->msg() && h->drain_cmd == 0 && h->drain_rec == 0 && h->h_out.size() >= kBulkDrainMin &&
       cap >= h->h_out.size()) {
     // whole window at once: record i of command c goes to out[first(c) + i] (one row per record
@@ -1186,12 +1302,14 @@ int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx) {
 
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal) {
   if (!h || !instance || !ordinal) return ZBHIP_EINVAL;
+  if (int rc = finalize(h)) return rc;
   const int64_t v = key - ((int64_t)h->cfg.partition_id << 51);
   auto it = std::upper_bound(h->batches.begin(), h->batches.end(), v,
                              [](int64_t x, const BatchRef& b) { return x < b.base; });
   if (it == h->batches.begin()) return ZBHIP_EINVAL;
   --it;
   if (v >= it->base + it->nkeys) return ZBHIP_EINVAL;
+  if (it->inst < h->inst_gen.size() && it->gen != h->inst_gen[it->inst]) return ZBHIP_EINVAL;  // instance ended
   *instance = it->inst;
   *ordinal = (uint16_t)(it->first_ord + (v - it->base));
   return ZBHIP_OK;
@@ -1246,6 +1364,7 @@ int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_ou
   *n_out = 0;
   if (!h->results) return h->msg() ? ZBHIP_ESTATE : ZBHIP_OK;
   if (!h->msg()) return ZBHIP_OK;
+  if (int rc = finalize(h)) return rc;
   const size_t n = h->n_cmds;
   h->h_xout.resize(n * kOut);
   if (n) {
@@ -1343,7 +1462,7 @@ int zbhip_command_status(zbhip_handle* h, size_t i, uint32_t* status, uint32_t* 
   if (!h->results) return ZBHIP_ESTATE;
   if (i >= h->n_cmds) return ZBHIP_EINVAL;
   *status = (h->h_hdr[i].y >> 16) & 0xFF;
-  *reason = h->h_hdr[i].y >> 24;
+  *reason = (h->h_hdr[i].y >> 24) & 0x7F;
   return ZBHIP_OK;
 }
 
@@ -1362,9 +1481,134 @@ int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_o
 }
 
 // Canonical CF rows (same text format as the oracle's state dump).
+namespace {
+struct InstRows {  // the SoA rows of one instance slot
+  uint4 hdr;
+  uint2 slots[kSlots];
+  uint2 vm[kVars];
+  long long vv[kVars];
+  uint32_t join[kJoinWords];
+  uint4 pms;
+  bool has_pms;
+};
+}  // namespace
+
+// the rows of one process instance (ELEMENT_INSTANCE_KEY ... NUMBER_OF_TAKEN_SEQUENCE_FLOWS,
+// PROCESS_SUBSCRIPTION_BY_KEY); nothing for a free slot
+static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbhip_state_sink sink, void* ctx) {
+  char buf[768];
+  const uint4 hd = R.hdr;
+  const uint32_t proc = hd.x & 0xFFFF;
+  if (proc == NONE || !((hd.y >> 24) & 1) || proc >= h->procs.size()) return;
+  const Proc& P = h->procs[proc];
+  const long long pik = h->key_of(inst, 0);
+  const uint32_t nslots = (hd.y >> 8) & 0xFF, nvars = (hd.y >> 16) & 0xFF;
+  snprintf(buf, sizeof buf,
+           "ELEMENT_INSTANCE_KEY|%lld|parentKey=-1,childCount=%u,childActivatedCount=0,childCompletedCount=0,"
+           "childTerminatedCount=0,jobKey=0,multiInstanceLoopCounter=0,interruptingElementId=,"
+           "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=-1,"
+           "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%u",
+           pik, hd.z & 0xFFFF, hd.y & 0xFF, P.id(0).c_str(), ZBHIP_EL_PROCESS, ZBHIP_EV_UNSPECIFIED, pik,
+           (long long)P.def_key, hd.z >> 16);
+  sink(ctx, buf);
+  snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|-1|%lld", pik);
+  sink(ctx, buf);
+  snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|-1", pik);
+  sink(ctx, buf);
+  snprintf(buf, sizeof buf, "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY|%lld|%lld", (long long)P.def_key, pik);
+  sink(ctx, buf);
+  for (uint32_t s = 0; s < nslots; ++s) {
+    const uint2 e = R.slots[s];
+    const uint32_t elem = e.x & 0xFFFF;
+    const long long k = h->key_of(inst, e.x >> 16);
+    const uint32_t job = e.y & 0xFFFF, state = (e.y >> 16) & 0xFF;
+    const bool job_row = (e.y >> 24) & 1;
+    const long long jk = job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
+    const zbhip_element& E = P.els[elem];
+    snprintf(buf, sizeof buf,
+             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=0,childActivatedCount=0,childCompletedCount=0,"
+             "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=0,interruptingElementId=,"
+             "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
+             "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=0",
+             k, pik, jk, state, P.id(elem).c_str(), E.element_type, E.event_type, pik, pik, (long long)P.def_key);
+    sink(ctx, buf);
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", pik, k);
+    sink(ctx, buf);
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, pik);
+    sink(ctx, buf);
+    if (E.element_type == ZBHIP_EL_SERVICE_TASK || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+      snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", k);
+      sink(ctx, buf);
+    }
+    if (job_row) {
+      const char* type = P.strings[E.job_type].c_str();
+      snprintf(buf, sizeof buf,
+               "JOBS|%lld|type=%s,retries=%u,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
+               "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>",
+               jk, type, E.job_retries, P.id(elem).c_str(), k, pik, P.strings[P.bpmn_id].c_str(), (long long)P.def_key,
+               P.version);
+      sink(ctx, buf);
+      snprintf(buf, sizeof buf, "JOB_STATES|%lld|ACTIVATABLE", jk);
+      sink(ctx, buf);
+      snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|<default>|%lld", type, jk);
+      sink(ctx, buf);
+    }
+  }
+  for (uint32_t v = 0; v < nvars; ++v) {
+    const uint2 m = R.vm[v];
+    const uint32_t scope = m.x >> 16;
+    snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%lld", h->key_of(inst, scope),
+             h->names[m.x & 0xFFFF].c_str(), h->key_of(inst, m.y & 0xFFFF), (m.y >> 16) & 0xFF, R.vv[v]);
+    sink(ctx, buf);
+  }
+  if (R.has_pms && ((R.pms.x >> 12) & 3)) {  // PROCESS_SUBSCRIPTION_BY_KEY [eik, name] (DbProcessMessageSubscriptionState)
+    const uint4 m = R.pms;
+    const uint32_t el = m.x & 0xFFF;
+    const zbhip_element& E = P.els[el];
+    snprintf(buf, sizeof buf,
+             "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%u,processInstanceKey=%lld,"
+             "bpmnProcessId=%s,messageKey=-1,correlationKey=%s,elementId=%s,interrupting=%u",
+             h->key_of(inst, m.y & 0xFFFF), zbhip_name(h, E.message_name), h->key_of(inst, m.y >> 16),
+             ((m.x >> 12) & 3) == 1 ? "OPENING" : "OPENED", m.x >> 16, pik, zbhip_name(h, P.bpmn_name),
+             zbhip_string_value(h, m.z, nullptr), P.id(el).c_str(), (m.x >> 14) & 1);
+    sink(ctx, buf);
+  }
+  if (P.n_join_slots) {
+    for (uint32_t f = 0; f < P.els.size(); ++f) {
+      const zbhip_element& E = P.els[f];
+      if (E.element_type != ZBHIP_EL_SEQUENCE_FLOW || E.join_slot == ZBHIP_NONE16) continue;
+      const uint32_t s = E.join_slot;
+      const uint32_t cnt = (R.join[s >> 2] >> ((s & 3) * 8)) & 0xFF;
+      if (!cnt) continue;
+      snprintf(buf, sizeof buf, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS|%lld|%s|%s|%u", pik, P.id(E.flow_target).c_str(),
+               P.id(f).c_str(), cnt);
+      sink(ctx, buf);
+    }
+  }
+}
+
+// one instance's rows gathered from HBM (small copies: the hand-off path of a few instances)
+static int gather_instance(zbhip_handle* h, uint32_t i, InstRows& R) {
+  const size_t N = h->st.n;
+  HIPCHK(hipMemcpy(&R.hdr, h->st.hdr + i, sizeof(uint4), hipMemcpyDeviceToHost));
+  const uint32_t nslots = (R.hdr.y >> 8) & 0xFF, nvars = (R.hdr.y >> 16) & 0xFF;
+  for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s)
+    HIPCHK(hipMemcpy(&R.slots[s], h->st.slots + s * N + i, sizeof(uint2), hipMemcpyDeviceToHost));
+  for (uint32_t v = 0; v < nvars && v < (uint32_t)kVars; ++v) {
+    HIPCHK(hipMemcpy(&R.vm[v], h->st.var_meta + v * N + i, sizeof(uint2), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&R.vv[v], h->st.var_val + v * N + i, sizeof(long long), hipMemcpyDeviceToHost));
+  }
+  for (int w = 0; w < kJoinWords; ++w)
+    HIPCHK(hipMemcpy(&R.join[w], h->st.join + w * N + i, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  R.has_pms = h->st.n_slots != 0;
+  if (R.has_pms) HIPCHK(hipMemcpy(&R.pms, h->st.pms + i, sizeof(uint4), hipMemcpyDeviceToHost));
+  return ZBHIP_OK;
+}
+
 int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   if (!h || !sink) return ZBHIP_EINVAL;
   if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
   const size_t N = h->st.n;
   std::vector<uint4> hdr(N);
   std::vector<uint2> slots(N * kSlots), vm(N * kVars);
@@ -1388,96 +1632,20 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   char buf[768];
   snprintf(buf, sizeof buf, "KEY|latestKey|%lld", (long long)(((int64_t)h->cfg.partition_id << 51) + h->key_counter));
   sink(ctx, buf);
+  InstRows R{};
   for (size_t i = 0; i < N; ++i) {
-    const uint4 hd = hdr[i];
-    const uint32_t proc = hd.x & 0xFFFF;
-    if (proc == NONE || !((hd.y >> 24) & 1)) continue;
-    const Proc& P = h->procs[proc];
-    const uint32_t inst = (uint32_t)i;
-    const long long pik = h->key_of(inst, 0);
-    const uint32_t nslots = (hd.y >> 8) & 0xFF, nvars = (hd.y >> 16) & 0xFF;
-    snprintf(buf, sizeof buf,
-             "ELEMENT_INSTANCE_KEY|%lld|parentKey=-1,childCount=%u,childActivatedCount=0,childCompletedCount=0,"
-             "childTerminatedCount=0,jobKey=0,multiInstanceLoopCounter=0,interruptingElementId=,"
-             "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=-1,"
-             "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%u",
-             pik, hd.z & 0xFFFF, hd.y & 0xFF, P.id(0).c_str(), ZBHIP_EL_PROCESS, ZBHIP_EV_UNSPECIFIED, pik,
-             (long long)P.def_key, hd.z >> 16);
-    sink(ctx, buf);
-    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|-1|%lld", pik);
-    sink(ctx, buf);
-    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|-1", pik);
-    sink(ctx, buf);
-    snprintf(buf, sizeof buf, "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY|%lld|%lld", (long long)P.def_key, pik);
-    sink(ctx, buf);
-    for (uint32_t s = 0; s < nslots; ++s) {
-      const uint2 e = slots[(size_t)s * N + i];
-      const uint32_t elem = e.x & 0xFFFF;
-      const long long k = h->key_of(inst, e.x >> 16);
-      const uint32_t job = e.y & 0xFFFF, state = (e.y >> 16) & 0xFF;
-      const bool job_row = (e.y >> 24) & 1;
-      const long long jk = job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
-      const zbhip_element& E = P.els[elem];
-      snprintf(buf, sizeof buf,
-               "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=0,childActivatedCount=0,childCompletedCount=0,"
-               "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=0,interruptingElementId=,"
-               "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
-               "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=0",
-               k, pik, jk, state, P.id(elem).c_str(), E.element_type, E.event_type, pik, pik, (long long)P.def_key);
-      sink(ctx, buf);
-      snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", pik, k);
-      sink(ctx, buf);
-      snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, pik);
-      sink(ctx, buf);
-      if (E.element_type == ZBHIP_EL_SERVICE_TASK || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
-        snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", k);
-        sink(ctx, buf);
-      }
-      if (job_row) {
-        const char* type = P.strings[E.job_type].c_str();
-        snprintf(buf, sizeof buf,
-                 "JOBS|%lld|type=%s,retries=%u,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
-                 "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>",
-                 jk, type, E.job_retries, P.id(elem).c_str(), k, pik, P.strings[P.bpmn_id].c_str(), (long long)P.def_key,
-                 P.version);
-        sink(ctx, buf);
-        snprintf(buf, sizeof buf, "JOB_STATES|%lld|ACTIVATABLE", jk);
-        sink(ctx, buf);
-        snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|<default>|%lld", type, jk);
-        sink(ctx, buf);
-      }
+    R.hdr = hdr[i];
+    const uint32_t proc = R.hdr.x & 0xFFFF;
+    if (proc == NONE || !((R.hdr.y >> 24) & 1)) continue;
+    for (int k = 0; k < kSlots; ++k) R.slots[k] = slots[(size_t)k * N + i];
+    for (int k = 0; k < kVars; ++k) {
+      R.vm[k] = vm[(size_t)k * N + i];
+      R.vv[k] = vv[(size_t)k * N + i];
     }
-    for (uint32_t v = 0; v < nvars; ++v) {
-      const uint2 m = vm[(size_t)v * N + i];
-      const uint32_t scope = m.x >> 16;
-      snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%lld", h->key_of(inst, scope),
-               h->names[m.x & 0xFFFF].c_str(), h->key_of(inst, m.y & 0xFFFF), (m.y >> 16) & 0xFF, vv[(size_t)v * N + i]);
-      sink(ctx, buf);
-    }
-    if (S && ((pms[i].x >> 12) & 3)) {  // PROCESS_SUBSCRIPTION_BY_KEY [eik, name] (DbProcessMessageSubscriptionState)
-      const uint4 m = pms[i];
-      const uint32_t el = m.x & 0xFFF;
-      const zbhip_element& E = P.els[el];
-      snprintf(buf, sizeof buf,
-               "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%u,processInstanceKey=%lld,"
-               "bpmnProcessId=%s,messageKey=-1,correlationKey=%s,elementId=%s,interrupting=%u",
-               h->key_of(inst, m.y & 0xFFFF), zbhip_name(h, E.message_name), h->key_of(inst, m.y >> 16),
-               ((m.x >> 12) & 3) == 1 ? "OPENING" : "OPENED", m.x >> 16, pik, zbhip_name(h, P.bpmn_name),
-               zbhip_string_value(h, m.z, nullptr), P.id(el).c_str(), (m.x >> 14) & 1);
-      sink(ctx, buf);
-    }
-    if (P.n_join_slots) {
-      for (uint32_t f = 0; f < P.els.size(); ++f) {
-        const zbhip_element& E = P.els[f];
-        if (E.element_type != ZBHIP_EL_SEQUENCE_FLOW || E.join_slot == ZBHIP_NONE16) continue;
-        const uint32_t s = E.join_slot;
-        const uint32_t cnt = (join[(size_t)(s >> 2) * N + i] >> ((s & 3) * 8)) & 0xFF;
-        if (!cnt) continue;
-        snprintf(buf, sizeof buf, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS|%lld|%s|%s|%u", pik, P.id(E.flow_target).c_str(),
-                 P.id(f).c_str(), cnt);
-        sink(ctx, buf);
-      }
-    }
+    for (int k = 0; k < kJoinWords; ++k) R.join[k] = join[(size_t)k * N + i];
+    R.has_pms = S != 0;
+    if (S) R.pms = pms[i];
+    emit_instance(h, (uint32_t)i, R, sink, ctx);
   }
   // MESSAGE_SUBSCRIPTION_BY_KEY [eik, name] and MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY
   // [tenant, name, correlationKey, eik] of this (message) partition (DbMessageSubscriptionState)
@@ -1500,6 +1668,81 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
       sink(ctx, buf);
     }
   if (h->published) sink(ctx, "MESSAGE_STATS|messagesDeadlineCount|0");
+  return ZBHIP_OK;
+}
+
+int zbhip_export_instances_db(zbhip_handle* h, const uint32_t* instances, size_t n, zbhip_db_sink sink, void* ctx) {
+  if (!h || !sink) return ZBHIP_EINVAL;
+  DbExport e{h->ser, sink, ctx, ZBHIP_OK};
+  const int rc = zbhip_export_instances(h, instances, n, db_row, &e);
+  return rc < 0 ? rc : e.rc;
+}
+
+// Hand-off of instances to the CPU engine: their slots are freed on the device (as a completed
+// instance's: rows gone, the key ordinal kept) and their keys no longer resolve.
+int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n) {
+  if (!h || (n && !instances)) return ZBHIP_EINVAL;
+  if (int rc = finalize(h)) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (size_t k = 0; k < n; ++k) {
+    const uint32_t i = instances[k];
+    if (i >= h->st.n) return ZBHIP_EINVAL;
+    uint4 hd;
+    HIPCHK(hipMemcpy(&hd, h->st.hdr + i, sizeof hd, hipMemcpyDeviceToHost));
+    const uint4 freed = make_uint4(0xFFFFu | (hd.x & 0xFFFF0000u), 0, 0, hd.w);  // the fence stays
+    HIPCHK(hipMemcpy(h->st.hdr + i, &freed, sizeof freed, hipMemcpyHostToDevice));
+    const uint32_t zero[kJoinWords] = {0, 0, 0, 0};
+    for (int w = 0; w < kJoinWords; ++w)
+      HIPCHK(hipMemcpy(h->st.join + (size_t)w * h->st.n + i, &zero[w], sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (h->st.n_slots) {
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      HIPCHK(hipMemcpy(h->st.pms + i, &z, sizeof z, hipMemcpyHostToDevice));
+    }
+    if (i < h->inst_gen.size()) ++h->inst_gen[i];
+  }
+  return ZBHIP_OK;
+}
+
+// DbKeyGenerator's value before window command i: the keys of the commands before it, the CPU
+// engine's declared ones included
+int zbhip_key_before(zbhip_handle* h, size_t i, int64_t* key) {
+  if (!h || !key) return ZBHIP_EINVAL;
+  if (!h->results) return ZBHIP_ESTATE;
+  if (i > h->n_cmds) return ZBHIP_EINVAL;
+  if (h->finalized) {
+    *key = ((int64_t)h->cfg.partition_id << 51) + (i < h->n_cmds ? h->h_base[i] : h->key_counter);
+    return ZBHIP_OK;
+  }
+  int64_t c = h->key_counter;
+  for (size_t k = 0; k < i; ++k) {
+    const uint2 hd = h->h_hdr[k];
+    c += ((hd.y >> 16) & 0xFF) == ST_OK ? (int64_t)(hd.x >> 16) : (int64_t)h->ext_keys[k];
+  }
+  *key = ((int64_t)h->cfg.partition_id << 51) + c;
+  return ZBHIP_OK;
+}
+
+int zbhip_set_external_keys(zbhip_handle* h, size_t i, uint32_t nkeys) {
+  if (!h) return ZBHIP_EINVAL;
+  if (!h->results || h->finalized) return ZBHIP_ESTATE;
+  if (i >= h->n_cmds || ((h->h_hdr[i].y >> 16) & 0xFF) == ST_OK) return ZBHIP_EINVAL;
+  // config 5: the device key scan fixed this window's keys already (outbox, slot rows)
+  if (h->msg() && nkeys) return ZBHIP_EUNSUPP;
+  h->ext_keys[i] = nkeys;
+  return ZBHIP_OK;
+}
+
+int zbhip_export_instances(zbhip_handle* h, const uint32_t* instances, size_t n, zbhip_state_sink sink, void* ctx) {
+  if (!h || !sink || (n && !instances)) return ZBHIP_EINVAL;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (size_t k = 0; k < n; ++k) {
+    if (instances[k] >= h->st.n) return ZBHIP_EINVAL;
+    InstRows R{};
+    if (int rc = gather_instance(h, instances[k], R)) return rc;
+    emit_instance(h, instances[k], R, sink, ctx);
+  }
   return ZBHIP_OK;
 }
 

@@ -82,7 +82,12 @@ enum : uint8_t {
   FB_BAD_PROCESS = 14, // unknown process / no none start event
   FB_MESSAGE = 15,     // message path outside the subset (NUMBER correlation key, second open
                        // subscription, rejected correlation, full correlation slot, outbox overflow)
+  FB_FENCED = 16,      // an earlier command of the same subject in this window fell back: the CPU
+                       // engine must process this one after it (log order), so it is not run here
+  FB_DUPLICATE = 17,   // (device windows) a second command for one subject in one launch
 };
+// cmd_hdr.y bit 31: the batch ended its process instance (completed; the slot is free)
+constexpr uint32_t HDR_ENDED = 1u << 31;
 
 // Program arena (u32 words), LDS-staged by every workgroup:
 //   [0] n_procs, [1 .. n_procs] word offset of each process block (multiple of 4)
@@ -102,7 +107,7 @@ enum : uint8_t {
 //               valid << 31 | from_task << 30 | to_end << 24 | target << 12 | flow, or 0
 struct DevState {
   uint4* hdr;        // [n] x = proc | next_ord << 16; y = pi_state | nslots << 8 | nvars << 16 | pi_live << 24
-                     //     z = pi_child | pi_asf << 16; w = 0
+                     //     z = pi_child | pi_asf << 16; w = fence: the window stamp of a fallen-back command
   uint2* slots;      // [kSlots][n] x = elem | key << 16; y = job | state << 16 | flags << 24 (bit0: job row exists)
   uint2* var_meta;   // [kVars][n]  x = name | scope << 16; y = key | type << 16
   long long* var_val;// [kVars][n]
@@ -113,7 +118,7 @@ struct DevState {
                      //     x = elem | state << 12 (0 none, 1 opening, 2 opened) | interrupting << 14 | subpart << 16
                      //     y = eik ord | subscription key ord << 16; z = correlation key id; w = 0
   long long* pi_key; // [n] real process-instance key (written by the device key scan)
-  uint2* slot_hdr;   // [S] x = next key ordinal of the correlation slot; y = 0
+  uint2* slot_hdr;   // [S] x = next key ordinal of the correlation slot; y = fence stamp (as hdr.w)
   uint4* sub_a;      // [kSubs][S] MESSAGE_SUBSCRIPTION rows: x = state (0 free, 1 open, 2 correlating)
                      //   | interrupting << 8 | key-in-instance-space << 9 | PI partition << 16;
                      //   y = message name | bpmnProcessId << 16; z = PI instance slot; w = eik ord | key ord << 16
@@ -157,6 +162,7 @@ struct StepParams {
                               // space), z = outbox entries, w = payload rows
   zbhip_xpart_cmd* xout;      // [n_cmds * kOut]
   int32_t partition_id, partition_count;
+  uint32_t stamp;             // window stamp: hdr.w / slot_hdr.y of a subject whose command fell back
 };
 
 }  // namespace zb

@@ -46,13 +46,14 @@ class Partition:
 
     def __init__(self, partition_id=1, partition_count=1, device=0, max_instances=1 << 16, max_commands=1 << 16,
                  max_records_per_batch=64, max_doc_entries=0, max_commands_in_batch=100, initial_key=0, stream=None,
-                 max_correlation_keys=0):
+                 max_correlation_keys=0, trusted_device_windows=False):
         self.L = load()
         cfg = abi.Config(partition_id=partition_id, partition_count=partition_count, device=device,
                          max_commands_in_batch=max_commands_in_batch, max_instances=max_instances,
                          max_commands=max_commands, max_records_per_batch=max_records_per_batch,
                          max_doc_entries=max_doc_entries, initial_key=initial_key, stream=stream,
-                         max_correlation_keys=max_correlation_keys)
+                         max_correlation_keys=max_correlation_keys,
+                         flags=abi.OPEN_TRUSTED_DEVICE_WINDOWS if trusted_device_windows else 0)
         h = C.c_void_p()
         check(self.L.zbhip_open(C.byref(cfg), C.byref(h)), "zbhip_open")
         self.h = h
@@ -225,6 +226,33 @@ class Partition:
         check(self.L.zbhip_export_state(self.h, cb, None), "zbhip_export_state")
         return sorted(rows)
 
+    # ---- fallback hand-off to the CPU engine (include/zbhip.h) ----
+    def export_instances(self, instances):
+        rows = []
+        cb = STATE_SINK(lambda ctx, row: rows.append(row.decode()))
+        ids = np.ascontiguousarray(instances, dtype=np.uint32)
+        check(self.L.zbhip_export_instances(self.h, ids.ctypes.data, len(ids), cb, None), "zbhip_export_instances")
+        return sorted(rows)
+
+    def export_instances_db(self, instances):
+        from .logwriter import _db_collector
+        out, cb = _db_collector()
+        ids = np.ascontiguousarray(instances, dtype=np.uint32)
+        check(self.L.zbhip_export_instances_db(self.h, ids.ctypes.data, len(ids), cb, None), "zbhip_export_instances_db")
+        return sorted(out)
+
+    def evict_instances(self, instances):
+        ids = np.ascontiguousarray(instances, dtype=np.uint32)
+        check(self.L.zbhip_evict_instances(self.h, ids.ctypes.data, len(ids)), "zbhip_evict_instances")
+
+    def key_before(self, i):
+        k = C.c_int64()
+        check(self.L.zbhip_key_before(self.h, i, C.byref(k)), "zbhip_key_before")
+        return k.value
+
+    def set_external_keys(self, i, nkeys):
+        check(self.L.zbhip_set_external_keys(self.h, i, nkeys), "zbhip_set_external_keys")
+
     def fallback(self):
         n = C.c_size_t()
         check(self.L.zbhip_fallback(self.h, None, 0, C.byref(n)))
@@ -234,7 +262,7 @@ class Partition:
 
     FALLBACK_REASONS = {1: "queue", 2: "table", 3: "records", 4: "keys", 5: "batch-limit", 6: "feel", 7: "vars",
                         8: "slot-in-use", 9: "no-condition", 10: "unsupported", 11: "doc", 12: "join",
-                        13: "slots", 14: "bad-process", 15: "message"}
+                        13: "slots", 14: "bad-process", 15: "message", 16: "fenced", 17: "duplicate"}
 
     def command_status(self, i):
         st, rs = C.c_uint32(), C.c_uint32()

@@ -26,7 +26,9 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_serializer_new", "zbhip_serializer_free", "zbhip_serializer_deploy", "zbhip_serializer_intern",
            "zbhip_serializer_intern_string", "zbhip_serializer_set_broker_version",
            "zbhip_serializer_rejection_reason", "zbhip_handle_serializer", "zbhip_serialize_log",
-           "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream"]
+           "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream",
+           "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
+           "zbhip_set_external_keys"]
 
 
 class ZbhipError(RuntimeError):
@@ -87,6 +89,11 @@ def load():
     L.zbhip_outbox_device.argtypes = [vp, C.POINTER(vp), vp]
     L.zbhip_outbox_copy.argtypes = [vp, vp, sz, sz]
     L.zbhip_outbox_device_async.argtypes = [vp, C.POINTER(vp), vp]
+    L.zbhip_export_instances.argtypes = [vp, vp, sz, STATE_SINK, vp]
+    L.zbhip_export_instances_db.argtypes = [vp, vp, sz, DB_SINK, vp]
+    L.zbhip_evict_instances.argtypes = [vp, vp, sz]
+    L.zbhip_key_before.argtypes = [vp, sz, C.POINTER(i64)]
+    L.zbhip_set_external_keys.argtypes = [vp, sz, u32]
     L.zbhip_stream.argtypes = [vp]
     L.zbhip_stream.restype = vp
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
