@@ -155,8 +155,9 @@ struct zbhip_handle {
   // key relabelling (DbKeyGenerator order)
   int64_t key_counter = 0;
   bool relabel_ok = true;
-  bool finalized = true;           // the last run's key bookkeeping is done (finalize)
+  size_t fin_next = 0;             // the last run's key bookkeeping is done for commands < fin_next (advance)
   std::vector<uint32_t> ext_keys;  // keys the CPU engine generated for the window's fallback commands
+  std::vector<uint8_t> declared;   // ... declared by the adapter (zbhip_set_external_keys)
   // plan_rounds: (stamp, last round) per subject; window of the last command per instance slot
   std::vector<std::pair<uint32_t, uint32_t>> plan_last;
   uint32_t plan_stamp = 0;
@@ -809,29 +810,33 @@ static hipEvent_t next_event(zbhip_handle* h) {
 }
 
 // Key relabelling bookkeeping of the last run, in log (source) order: each command's first key
-// (DbKeyGenerator order), the subjects' key histories and the resolve_key table.  Deferred until the
-// window's results are first used, so that the adapter can declare the keys its CPU engine generated
-// for the window's fallback commands (zbhip_set_external_keys) before the keys after them are fixed.
-static int finalize(zbhip_handle* h) {
-  if (!h->results || h->finalized) return ZBHIP_OK;
-  h->finalized = true;
-  const uint32_t n = (uint32_t)h->n_cmds;
+// (DbKeyGenerator order), the subjects' key histories and the resolve_key table.  It advances
+// lazily, command by command: up to `limit`, and never past a fallback command whose CPU-engine keys
+// were not declared yet (zbhip_set_external_keys), unless `force` (then it generated none) -- so the
+// adapter can hand a fallback instance over (its earlier commands' keys are fixed) and declare the
+// keys the CPU engine generated before the keys of the window's later commands are fixed.
+static int advance(zbhip_handle* h, size_t limit, bool force) {
+  if (!h->results || h->fin_next >= h->n_cmds) return ZBHIP_OK;
   const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
   if (h->hist.size() < subjects) {
     h->hist.resize(subjects);
     h->inst_proc.resize(h->cfg.max_instances, NONE);
     h->inst_gen.resize(subjects, 0);
   }
-  h->h_base.assign(n, 0);
-  for (uint32_t c = 0; c < n; ++c) {
+  const size_t n = std::min(limit, h->n_cmds);
+  for (size_t c = h->fin_next; c < n; ++c) {
     const uint2 hd = h->h_hdr[c];
     const zbhip_command& cm = h->h_cmds[c];
     const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
-    h->h_base[c] = h->key_counter;
     if (((hd.y >> 16) & 0xFF) != ST_OK) {  // processed by the CPU engine: the keys it declared
+      if (!h->declared[c] && !force) return ZBHIP_OK;
+      h->h_base[c] = h->key_counter;
       h->key_counter += h->ext_keys[c];
+      h->fin_next = c + 1;
       continue;
     }
+    h->h_base[c] = h->key_counter;
+    h->fin_next = c + 1;
     if (h->msg() && slot_kind(cm.kind)) {
       // the correlation slot's keys first, then the instance a local command loaded
       const uint4 h2 = h->h_hdr2[c];
@@ -861,7 +866,8 @@ static int finalize(zbhip_handle* h) {
     if (hd.y & HDR_ENDED) ++h->inst_gen[cm.instance];  // completed: its job keys no longer resolve
     h->key_counter += nkeys;
   }
-  // drop the key-table entries of ended / replaced instances once they outnumber the rest
+  if (h->fin_next < h->n_cmds) return ZBHIP_OK;
+  // window done: drop the key-table entries of ended / replaced instances once they outnumber the rest
   if (h->batches.size() >= 2 * h->batches_compacted + (1u << 20)) {
     auto live = [h](const BatchRef& b) { return b.gen == h->inst_gen[b.inst]; };
     h->batches.erase(std::remove_if(h->batches.begin(), h->batches.end(), [&](const BatchRef& b) { return !live(b); }),
@@ -870,6 +876,9 @@ static int finalize(zbhip_handle* h) {
   }
   return ZBHIP_OK;
 }
+
+// the whole window (undeclared fallback commands generated no keys)
+static int finalize(zbhip_handle* h) { return advance(h, ~(size_t)0, true); }
 
 int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (!h) return ZBHIP_EINVAL;
@@ -1020,7 +1029,9 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (off != total) return ZBHIP_EDEVICE;
 
   h->ext_keys.assign(n, 0);
-  h->finalized = false;
+  h->declared.assign(n, 0);
+  h->h_base.assign(n, 0);
+  h->fin_next = 0;
   h->results = true;
   return (int)n;
 }
@@ -1302,7 +1313,9 @@ int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx) {
 
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal) {
   if (!h || !instance || !ordinal) return ZBHIP_EINVAL;
-  if (int rc = finalize(h)) return rc;
+  // keys of commands after a fallback command whose CPU-engine keys are not declared yet resolve
+  // once the window is drained
+  if (int rc = advance(h, ~(size_t)0, false)) return rc;
   const int64_t v = key - ((int64_t)h->cfg.partition_id << 51);
   auto it = std::upper_bound(h->batches.begin(), h->batches.end(), v,
                              [](int64_t x, const BatchRef& b) { return x < b.base; });
@@ -1682,7 +1695,7 @@ int zbhip_export_instances_db(zbhip_handle* h, const uint32_t* instances, size_t
 // instance's: rows gone, the key ordinal kept) and their keys no longer resolve.
 int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n) {
   if (!h || (n && !instances)) return ZBHIP_EINVAL;
-  if (int rc = finalize(h)) return rc;
+  if (int rc = advance(h, ~(size_t)0, false)) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   for (size_t k = 0; k < n; ++k) {
     const uint32_t i = instances[k];
@@ -1709,12 +1722,13 @@ int zbhip_key_before(zbhip_handle* h, size_t i, int64_t* key) {
   if (!h || !key) return ZBHIP_EINVAL;
   if (!h->results) return ZBHIP_ESTATE;
   if (i > h->n_cmds) return ZBHIP_EINVAL;
-  if (h->finalized) {
-    *key = ((int64_t)h->cfg.partition_id << 51) + (i < h->n_cmds ? h->h_base[i] : h->key_counter);
+  if (int rc = advance(h, i, false)) return rc;
+  if (i < h->fin_next) {
+    *key = ((int64_t)h->cfg.partition_id << 51) + h->h_base[i];
     return ZBHIP_OK;
   }
-  int64_t c = h->key_counter;
-  for (size_t k = 0; k < i; ++k) {
+  int64_t c = h->key_counter;  // after commands < fin_next
+  for (size_t k = h->fin_next; k < i; ++k) {
     const uint2 hd = h->h_hdr[k];
     c += ((hd.y >> 16) & 0xFF) == ST_OK ? (int64_t)(hd.x >> 16) : (int64_t)h->ext_keys[k];
   }
@@ -1724,18 +1738,22 @@ int zbhip_key_before(zbhip_handle* h, size_t i, int64_t* key) {
 
 int zbhip_set_external_keys(zbhip_handle* h, size_t i, uint32_t nkeys) {
   if (!h) return ZBHIP_EINVAL;
-  if (!h->results || h->finalized) return ZBHIP_ESTATE;
+  if (!h->results) return ZBHIP_ESTATE;
   if (i >= h->n_cmds || ((h->h_hdr[i].y >> 16) & 0xFF) == ST_OK) return ZBHIP_EINVAL;
+  if (i < h->fin_next) return ZBHIP_ESTATE;  // the keys after it are fixed already
   // config 5: the device key scan fixed this window's keys already (outbox, slot rows)
   if (h->msg() && nkeys) return ZBHIP_EUNSUPP;
   h->ext_keys[i] = nkeys;
+  h->declared[i] = 1;
   return ZBHIP_OK;
 }
 
 int zbhip_export_instances(zbhip_handle* h, const uint32_t* instances, size_t n, zbhip_state_sink sink, void* ctx) {
   if (!h || !sink || (n && !instances)) return ZBHIP_EINVAL;
   if (!h->relabel_ok) return ZBHIP_ESTATE;
-  if (int rc = finalize(h)) return rc;
+  // the keys up to the first undeclared fallback command (a fallback instance's own history ends
+  // before its fallback command: later commands of it are fenced)
+  if (int rc = advance(h, ~(size_t)0, false)) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   for (size_t k = 0; k < n; ++k) {
     if (instances[k] >= h->st.n) return ZBHIP_EINVAL;
