@@ -359,7 +359,10 @@ typedef struct zbhip_record {
   uint16_t bpmn_process_id;     /* name id, 0xFFFF = empty */
   int32_t partition;            /* PMS: subscriptionPartitionId; else 0 */
   uint8_t interrupting;
-  uint8_t pad[3];
+  uint8_t unprocessed;          /* a follow-up COMMAND written to the log unprocessed (past
+                                   maxCommandsInBatch, ProcessingStateMachine.java:388-417): it
+                                   starts a batch of its own later (no skipProcessing flag) */
+  uint8_t pad[2];
 } zbhip_record;
 #define ZBHIP_NO_STRING 0xFFFFFFFFu
 

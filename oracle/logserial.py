@@ -373,5 +373,5 @@ def serialize(records, tables, docs_of_source, doc_entry, reason_text, first_pos
         value = record_value(r, tables, docs_of_source, doc_entry,
                              source_timestamp(si) if source_timestamp else timestamp)
         out += log_entry(int(r["key"]), md, value, first_position + i, source_position(int(r["source_index"])),
-                         timestamp, rt == RT_COMMAND)
+                         timestamp, rt == RT_COMMAND and not int(r["unprocessed"]))
     return bytes(out)

@@ -993,7 +993,9 @@ class Oracle {
             ++to_process;
           } else {
             // written to the log unprocessed: processed later as its own batch
+            batch[i].r.unprocessed = 1;
             ORecord later = batch[i];
+            later.r.unprocessed = 0;
             later.r.source_index = next_source_++;
             log_.push_back(later);
           }

@@ -93,7 +93,8 @@ class Record(C.Structure):
                 ("rejection_type", C.c_uint8), ("ordinal", C.c_uint16), ("reason", C.c_uint8),
                 ("reason_arg", C.c_uint8), ("aux", C.c_int64), ("message_key", C.c_int64),
                 ("correlation_key", C.c_uint32), ("message_name", C.c_uint16), ("bpmn_process_id", C.c_uint16),
-                ("partition", C.c_int32), ("interrupting", C.c_uint8), ("pad", C.c_uint8 * 3)]
+                ("partition", C.c_int32), ("interrupting", C.c_uint8), ("unprocessed", C.c_uint8),
+                ("pad", C.c_uint8 * 2)]
 
 
 class XpartCmd(C.Structure):
@@ -137,7 +138,7 @@ RECORD_DTYPE = np.dtype([("key", "<i8"), ("scope_key", "<i8"), ("process_instanc
                          ("rejection_type", "u1"), ("ordinal", "<u2"), ("reason", "u1"), ("reason_arg", "u1"),
                          ("aux", "<i8"), ("message_key", "<i8"), ("correlation_key", "<u4"),
                          ("message_name", "<u2"), ("bpmn_process_id", "<u2"), ("partition", "<i4"),
-                         ("interrupting", "u1"), ("pad", "u1", (3,))])
+                         ("interrupting", "u1"), ("unprocessed", "u1"), ("pad", "u1", (2,))])
 XPART_DTYPE = np.dtype([("element_instance_key", "<i8"), ("process_instance_key", "<i8"), ("message_key", "<i8"),
                         ("correlation_key", "<u4"), ("instance", "<u4"), ("element_ord", "<u2"),
                         ("message_name", "<u2"), ("bpmn_process_id", "<u2"), ("kind", "u1"),

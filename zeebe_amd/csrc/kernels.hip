@@ -71,7 +71,7 @@ struct KCfg {
 #define ZB_KSIMPLE_R 4
 #endif
 #ifndef ZB_KSIMPLE_W
-#define ZB_KSIMPLE_W 0
+#define ZB_KSIMPLE_W 3  // 168 VGPRs, no spill: the register allocator is held to 3 waves per SIMD
 #endif
 using KSimple = KCfg<ZB_KSIMPLE_B, 4, 4, ZB_KSIMPLE_R, false, false, true, ZB_KSIMPLE_W>;
 // Linear chains (every node <= 1 outgoing flow, no gateways, no catch events): at most two element
@@ -91,7 +91,7 @@ using KLinear = KCfg<64, 2, 2, 15, false, false, false, ZB_KLINEAR_W, true>;
 #define ZB_KGENERIC_R 4
 #endif
 #ifndef ZB_KGENERIC_W
-#define ZB_KGENERIC_W 0
+#define ZB_KGENERIC_W 3
 #endif
 using KGeneric = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, ZB_KGENERIC_W>;
 #ifndef ZB_KMSG_R
@@ -113,7 +113,10 @@ struct Lane {
   uint32_t completed;
   int limit;
   int processed;
-  int qh, qt;
+  int qh, qt;          // LDS ring (register pair for K::REG)
+  uint32_t g;           // the lane's global FIFO behind the ring (entries beyond K::Q pending):
+                        // head | tail << 16, entries in StepParams.qspill
+  uint32_t ci;          // window index of the command (overflow entries, outbox, key references)
   int nt;               // table high-water mark
   uint16_t proc;
   uint16_t next_ord;
@@ -137,7 +140,6 @@ struct Lane {
   uint2 r_t0, r_t1;         // K::REG: element table entries
   uint32_t r_q0, r_q1;      // K::REG: FIFO entries
   // ---- message correlation (K::M only) ----
-  uint32_t ci;              // window index of the command (outbox, key references)
   uint32_t inst;            // instance whose rows are loaded (kNoInst: none, a slot lane before a
                             // local PROCESS_MESSAGE_SUBSCRIPTION command)
   uint32_t pm_x, pm_y, pm_z;// PROCESS_SUBSCRIPTION row of the loaded instance
@@ -321,15 +323,73 @@ __device__ __forceinline__ void qput(Lane<K>& L, int i, uint32_t v) {
 }
 
 // queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | key << 16
+__device__ __forceinline__ uint32_t qentry(uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
+  return elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
+}
 template <class K>
-__device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
-  // ProcessingStateMachine.collectBatchProcessingStepResult (:388-417): a follow-up command is
-  // processed in this batch only while pending + processed + 1 + admitted < maxCommandsInBatch;
-  // otherwise the platform writes it to the log unprocessed -> outside the device subset.
-  if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
-  if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
-  qput(L, L.qt, elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16));
-  ++L.qt;
+__device__ __forceinline__ int pending(const Lane<K>& L) {
+  return (L.qt - L.qh) + (int)((L.g >> 16) - (L.g & 0xFFFF));
+}
+// entry i of the lane's global FIFO (resident lanes of the grid are interleaved: coalesced rows)
+__device__ __forceinline__ uint32_t* spill_at(const StepParams& P, uint32_t i) {
+  return P.qspill + ((size_t)(i % P.qspill_cap) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+}
+// the batch FIFO: the oldest K::Q pending entries in the LDS ring, newer ones (a large fan-out,
+// e.g. a fork with more branches than K::Q) in the lane's global FIFO, moved into the ring as it drains
+template <class K>
+__device__ __forceinline__ void enqueue(Lane<K>& L, uint32_t entry) {
+  const uint32_t gh = L.g & 0xFFFF, gt = L.g >> 16;
+  if (L.qt - L.qh < K::Q && gt == gh) {
+    qput(L, L.qt, entry);
+    ++L.qt;
+    return;
+  }
+  if constexpr (K::REG) {
+    set_fail(L, FB_QUEUE);
+  } else {
+    if (gt - gh >= L.sp->qspill_cap || gt >= 0xFFFF) { set_fail(L, FB_QUEUE); return; }
+    *spill_at(*L.sp, gt) = entry;
+    L.g += 1u << 16;
+  }
+}
+template <class K>
+__device__ __forceinline__ uint32_t dequeue(Lane<K>& L) {
+  const uint32_t entry = qget(L, L.qh);
+  ++L.qh;
+  if constexpr (!K::REG) {
+    const uint32_t gh = L.g & 0xFFFF;
+    if ((L.g >> 16) > gh) {
+      qput(L, L.qt, *spill_at(*L.sp, gh));
+      ++L.qt;
+      ++L.g;
+    }
+  }
+  return entry;
+}
+
+// ProcessingStateMachine.collectBatchProcessingStepResult (:388-417): a follow-up command is
+// processed in this batch only while pending + processed + 1 + admitted < maxCommandsInBatch;
+// otherwise the platform writes it to the log unprocessed and processes it later as a batch of its
+// own (after the window's commands, in the order written): the record is flagged and the command
+// kept in the overflow list for the runtime's continuation launches.
+template <class K>
+__device__ __forceinline__ void overflow(Lane<K>& L, uint32_t entry) {
+  const StepParams& P = *L.sp;
+  if (!P.ovf) { set_fail(L, FB_BATCH_LIMIT); return; }
+  const uint32_t slot = atomicAdd(P.ovf_count, 1u);
+  if (slot >= P.ovf_cap) { set_fail(L, FB_BATCH_LIMIT); return; }
+  P.ovf[slot] = make_uint4(L.ci, entry, L.nrec - 1, 0u);
+}
+
+// a follow-up command of the batch: its COMMAND record, then the FIFO (or the overflow list)
+template <class K>
+__device__ __forceinline__ void follow_up(Lane<K>& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
+                                          bool complete, bool fs_pi, uint32_t qkey) {
+  const bool admit = pending(L) + L.processed + 1 < L.limit;
+  emit(L, code, key, aux, elem, admit ? 0u : F_UNPROCESSED);
+  const uint32_t entry = qentry(elem, complete, fs_pi, qkey);
+  if (admit) enqueue(L, entry);
+  else overflow(L, entry);
 }
 
 // local subscription commands (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition,
@@ -337,10 +397,10 @@ __device__ __forceinline__ void push(Lane<K>& L, uint32_t elem, bool complete, b
 enum : uint32_t { LQ_BIT = 1u << 14, LQ_MS_CREATE = 1, LQ_PMS_CREATE = 2, LQ_PMS_CORRELATE = 3, LQ_MS_CORRELATE = 4 };
 template <class K>
 __device__ __forceinline__ void push_local(Lane<K>& L, uint32_t kind) {
-  if ((L.qt - L.qh) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
-  if (L.qt - L.qh >= K::Q) { set_fail(L, FB_QUEUE); return; }
-  qput(L, L.qt, LQ_BIT | kind);
-  ++L.qt;
+  // past the batch limit a local subscription command would need its pending context written to
+  // the log: outside the device subset
+  if (pending(L) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
+  enqueue(L, LQ_BIT | kind);
 }
 
 // ---- element-instance table (LDS) ----------------------------------------------------------
@@ -605,8 +665,7 @@ __device__ __forceinline__ void take_sequence_flow(Lane<K>& L, uint32_t flow) {
     join_set(L, s, c + 1);
   }
   uint32_t k = new_key(L);
-  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, 0, target);
-  push(L, target, false, true, k);
+  follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, 0, target, false, true, k);
 }
 
 // transitionToCompleted (:158-191) + afterExecutionPathCompleted -> ProcessProcessor (:130-140)
@@ -616,8 +675,7 @@ __device__ __forceinline__ void transition_to_completed_child(Lane<K>& L, int t,
   apply_completed_child(L, t, key);
   if ((w.y >> 16) == 0) {  // end of the execution path
     if (L.pi_live && L.pi_child + L.pi_asf == 0) {  // BpmnStateBehavior.canBeCompleted
-      emit(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0);
-      push(L, 0, true, false, 0);
+      follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0, true, false, 0);
     }
   }
 }
@@ -810,8 +868,7 @@ __device__ __forceinline__ void pms_correlate(Lane<K>& L, uint32_t eord, uint32_
   const uint32_t pe = new_key(L);
   emit(L, C_PE_TRIGGERING, pe, eord, elem);
   L.trig_key = (uint16_t)eord;
-  emit(L, ZBHIP_PI_COMPLETE_ELEMENT, eord, 0, elem);
-  push(L, elem, true, true, eord);
+  follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, eord, 0, elem, true, true, eord);
   // sendAcknowledgeCommand -> SubscriptionCommandSender.correlateMessageSubscription (sender partition)
   if ((int32_t)part == L.sp->partition_id) {
     emit_msg(L, C_MS_CORRELATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, nb, 0, 1, kNoElem);
@@ -967,8 +1024,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, cmd_key, NONE, 0);
       L.pi_state = ZBHIP_PI_ELEMENT_ACTIVATED;
       uint32_t start = L.pb[0] >> 16;
-      emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, NONE, 0, start);  // activateChildInstance: key -1
-      push(L, start, false, true, NONE);
+      follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, NONE, 0, start, false, true, NONE);  // activateChildInstance: key -1
       return;
     }
     if (cmd_key != NONE && tbl_find(L, cmd_key) >= 0) { set_fail(L, FB_UNSUPPORTED); return; }
@@ -984,8 +1040,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       case ZBHIP_EL_INTERMEDIATE_THROW_EVENT:  // NoneIntermediateThrowEventBehavior.onActivate (:120-126)
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
-        emit(L, ZBHIP_PI_COMPLETE_ELEMENT, key, 0, elem);
-        push(L, elem, true, true, key);
+        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, key, 0, elem, true, true, key);
         return;
       case ZBHIP_EL_END_EVENT:  // NoneEndEventBehavior.onActivate/onComplete (:110-134)
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
@@ -1208,7 +1263,7 @@ __device__ __forceinline__ uint32_t cmd_index(const StepParams& P, uint32_t chun
   return P.order ? P.order[lane_id] : lane_id;
 }
 __device__ __forceinline__ uint4 load_cmd(const StepParams& P, uint32_t ci) {
-  return ci != kNoCmd ? P.cmds[ci] : make_uint4(0, 0, 0, 0);
+  return ci != kNoCmd ? P.cmds[ci - P.cmd_base] : make_uint4(0, 0, 0, 0);
 }
 // header row, and the first element-instance slot of a waiting instance (a CREATE reads none)
 __device__ __forceinline__ void load_rows(const StepParams& P, uint32_t ci, const uint4& cw, uint4& h, uint2& s0) {
@@ -1411,6 +1466,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.limit = P.max_cmds_in_batch;
   L.processed = 0;
   L.qh = L.qt = 0;
+  L.g = 0;
+  L.ci = ci;
+  L.sp = &P;
   L.nt = 0;
   L.trig_key = NONE;
   L.docs = P.docs;
@@ -1424,9 +1482,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.vv0 = L.vv1 = L.vv2 = L.vv3 = 0;
   bool slot_kind = false;
   if constexpr (K::M) {
-    L.sp = &P;
     L.prog = prog;
-    L.ci = ci;
     L.inst = inst;
     L.pm_x = L.pm_y = L.pm_z = 0;
     L.pik = -1;
@@ -1478,6 +1534,11 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       L.s_next_ord = L.s_first_ord = (uint16_t)slot_row.x;
       L.proc = NONE;
     }
+  } else if (kind == CMD_FOLLOWUP && L.proc == NONE) {
+    // a follow-up command read back from the log after its instance ended: the guard rejects it
+    if (ref >= P.n_procs) set_fail(L, FB_BAD_PROCESS);
+    L.proc = ref;
+    L.pi_live = false;
   } else if (kind == ZBHIP_CMD_CREATE) {
     // CreateProcessInstanceProcessor.createProcessInstance (:129-158)
     if (L.proc != NONE) set_fail(L, FB_SLOT_IN_USE);
@@ -1555,8 +1616,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       vm_drain();
       set_local_variable(L, pi, d);
     }
-    emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0);
-    push(L, 0, false, false, pi);
+    follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0, false, false, pi);
     uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
     emit(L, C_PIC_CREATED, created, pi, 0);
   } else if (!L.fail && kind == ZBHIP_CMD_JOB_COMPLETE) {
@@ -1576,23 +1636,24 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
         uint32_t pe = new_key(L);  // EventTriggerBehavior.triggeringProcessEvent
         emit(L, C_PE_TRIGGERING, pe, task_key, task_elem);
         L.trig_key = task_key;       // ProcessEventTriggeringApplier: EVENT_TRIGGER row
-        emit(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, 0, task_elem);
-        push(L, task_elem, true, true, task_key);
+        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, 0, task_elem, true, true, task_key);
       }
     }
+  } else if (!L.fail && kind == CMD_FOLLOWUP) {
+    // written to the log past the batch limit: the command is this batch's initial command
+    enqueue(L, doc_begin);
   } else if (!L.fail) {
     if constexpr (K::M) message_command(L, kind, inst, ref, doc_begin);
     else set_fail(L, FB_UNSUPPORTED);
   }
-  L.processed = 1;
+  L.processed = kind == CMD_FOLLOWUP ? 0 : 1;
 
   // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
 #ifdef ZB_EXP_FASTONLY
   if (K::REG) fast = true;
 #endif
   while (!fast && L.qh < L.qt && !L.fail) {
-    const uint32_t entry = qget(L, L.qh);
-    ++L.qh;
+    const uint32_t entry = dequeue(L);
     if constexpr (K::M) {
       if (entry & LQ_BIT) {
         process_local(L, entry & 0xF);
@@ -2248,7 +2309,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr size_t kLdsGranule = 1280;  // 160 KB / 128
 
 template <class K>
-static uint32_t grid_for(uint32_t n_chunks, size_t lds) {
+static uint32_t resident_for(size_t lds) {
   static int cus = 0;
   static size_t cached_lds = ~(size_t)0;
   static int per_cu = 0;
@@ -2269,9 +2330,14 @@ static uint32_t grid_for(uint32_t n_chunks, size_t lds) {
     if (env_int("ZBHIP_DEBUG", 0)) fprintf(stderr, "[zbhip] k_step B=%d R=%d lds=%zu per_cu=%d\n", K::B, K::R, lds, per_cu);
     cached_lds = lds;
   }
+  return (uint32_t)(per_cu * cus);
+}
+
+template <class K>
+static uint32_t grid_for(uint32_t n_chunks, size_t lds) {
   const int fixed = env_int("ZBHIP_CHUNKS_PER_WG", 0);
   if (fixed > 0) return (n_chunks + fixed - 1) / fixed;
-  const uint32_t resident = (uint32_t)(per_cu * cus);
+  const uint32_t resident = resident_for<K>(lds);
   if (n_chunks <= resident) return n_chunks;
   const uint32_t per_wg = (n_chunks + resident - 1) / resident;
   return (n_chunks + per_wg - 1) / per_wg;
@@ -2283,6 +2349,17 @@ static hipError_t launch_k(const StepParams& P, hipStream_t s) {
   const size_t lds = lds_bytes<K>(P.prog_words);
   hipLaunchKernelGGL(k_step<K>, dim3(grid_for<K>(n_chunks, lds)), dim3(K::B), lds, s, P);
   return hipGetLastError();
+}
+
+// the largest grid of a k_step launch (its resident workgroups; ZBHIP_CHUNKS_PER_WG aside)
+uint32_t step_resident(int variant, uint32_t prog_words) {
+  return variant == 3   ? resident_for<KLinear>(lds_bytes<KLinear>(prog_words))
+         : variant == 2 ? resident_for<KMsg>(lds_bytes<KMsg>(prog_words))
+         : variant      ? resident_for<KGeneric>(lds_bytes<KGeneric>(prog_words))
+                        : resident_for<KSimple>(lds_bytes<KSimple>(prog_words));
+}
+uint32_t step_queue(int variant) {
+  return variant == 3 ? KLinear::Q : variant == 2 ? KMsg::Q : variant ? KGeneric::Q : KSimple::Q;
 }
 
 // variants: 0 KSimple, 1 KGeneric, 2 KMsg, 3 KLinear

@@ -528,7 +528,8 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
       const uint32_t fl = (uint32_t)framed;
       memcpy(p, &fl, 4);
       uint8_t* e = p + 12;
-      e[2] = r.record_type == ZBHIP_RT_COMMAND ? 1 : 0;  // skipProcessing: processed follow-up command
+      // skipProcessing: a follow-up command processed in its batch (not one written unprocessed)
+      e[2] = r.record_type == ZBHIP_RT_COMMAND && !r.unprocessed ? 1 : 0;
       const int64_t pos = w->first_position + (int64_t)i;
       memcpy(e + 4, &pos, 8);
       memcpy(e + 12, &src_pos, 8);

@@ -6,6 +6,7 @@
 // allocated at open (HBM is sized for the instance capacity, SoA), nothing is allocated in
 // the run path.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -21,6 +22,8 @@
 
 namespace zb {
 uint32_t step_block(int variant);
+uint32_t step_resident(int variant, uint32_t prog_words);
+uint32_t step_queue(int variant);
 size_t step_lds_bytes(int variant, uint32_t prog_words);
 hipError_t launch_step(int variant, const StepParams& P, hipStream_t s);
 void dump_stamps();
@@ -60,6 +63,34 @@ struct Proc {
   bool has_msg = false;
   const std::string& id(uint32_t e) const { return strings[els[e].id]; }
 };
+
+// Host threads a bulk host pass may use: the CPUs this process may run on (affinity mask, which
+// honours taskset / cgroup cpusets), at most 16.
+unsigned host_threads() {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int n = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+  return (unsigned)std::max(1, std::min(16, n));
+}
+
+// fn(t, T) for t in [0, T) on up to T threads; a thread that cannot be started runs its share on
+// the calling thread (no exception leaves the C ABI, no joinable thread is destroyed)
+template <class F>
+void parallel_for(unsigned T, const F& fn) {
+  std::vector<std::thread> pool;
+  pool.reserve(T);
+  unsigned t = 1;
+  for (; t < T; ++t) {
+    try {
+      pool.emplace_back(fn, t, T);
+    } catch (...) {
+      break;
+    }
+  }
+  for (unsigned u = t; u < T; ++u) fn(u, T);
+  fn(0u, T);
+  for (auto& th : pool) th.join();
+}
 
 // Java String#hashCode over signed bytes (SubscriptionUtil.getSubscriptionHashCode, :22-30)
 int32_t java_hash(const char* b, size_t n) {
@@ -126,7 +157,26 @@ struct zbhip_handle {
   size_t region_records = 0;
   uint32_t region_pad = 0;  // records between consecutive regions (region stride B * rec_cap + pad)
   int variant = 3;                           // kernel variant (zbhip_deploy): 3 KLinear, 0 KSimple, 1 KGeneric, 2 KMsg
-  std::vector<std::pair<uint32_t, uint32_t>> launches;  // (region_base, first position in order) per launch
+  // launches of the last run: region base, lane count, and the window index of each lane (the
+  // main window's rounds: identity or h_order; continuation batches: cont_order)
+  struct Launch {
+    uint32_t region, first, count;
+    uint8_t src;  // 0 identity, 1 h_order[first + k], 2 cont_order[first + k]
+  };
+  std::vector<Launch> launches;
+  // follow-up commands written to the log past maxCommandsInBatch, read back as batches of their own
+  // after the window (kernels.hip overflow / CMD_FOLLOWUP)
+  bool may_overflow = false;           // a deployed process can exceed the batch limit (deploy-time bound)
+  uint32_t max_pending = 0;            // deploy-time bound of pending follow-ups in one batch
+  uint4* d_ovf = nullptr;
+  uint32_t* d_ovf_count = nullptr;
+  zbhip_command* d_cont = nullptr;     // continuation commands (window indices n ..)
+  uint32_t* d_cont_order = nullptr;
+  std::vector<zbhip_command> cont_cmds;
+  std::vector<uint32_t> cont_order;
+  uint32_t* d_qspill = nullptr;        // batch FIFO entries beyond the LDS ring (kernels.hip enqueue)
+  size_t qspill_words = 0;
+  uint32_t qspill_cap = 0;
   std::vector<hipEvent_t> tev;               // timing events (pairs) since the last stats reset
   size_t tev_used = 0;
   uint32_t rec_cap = 64;
@@ -312,7 +362,9 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
        dalloc(&h->d_xparts, cfg->max_commands) == hipSuccess &&
        dalloc(&h->d_key_counter, 1) == hipSuccess && dalloc(&h->d_key_base, cfg->max_commands) == hipSuccess &&
        dalloc(&h->d_key_blk, (cfg->max_commands + 1023) / 1024 + 1) == hipSuccess && dalloc(&h->d_xcount, 1024) == hipSuccess &&
-       dalloc(&h->d_seen, N + S) == hipSuccess && dalloc(&h->d_check_flag, 1) == hipSuccess;
+       dalloc(&h->d_seen, N + S) == hipSuccess && dalloc(&h->d_check_flag, 1) == hipSuccess &&
+       dalloc(&h->d_ovf, cfg->max_commands) == hipSuccess && dalloc(&h->d_ovf_count, 1) == hipSuccess &&
+       dalloc(&h->d_cont, cfg->max_commands) == hipSuccess && dalloc(&h->d_cont_order, cfg->max_commands) == hipSuccess;
   if (S) {
     ok = ok && dalloc(&h->d_xout, (size_t)cfg->max_commands * kOut) == hipSuccess &&
          dalloc(&h->d_xbucket, (size_t)cfg->max_commands * kOut) == hipSuccess &&
@@ -336,6 +388,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   if (hipMemsetAsync(h->st.hdr, 0xFF, N * sizeof(uint4), h->stream) != hipSuccess ||
       hipMemsetAsync(h->st.join, 0, N * kJoinWords * sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_seen, 0, (N + S) * sizeof(uint32_t), h->stream) != hipSuccess ||
+      hipMemsetAsync(h->d_ovf_count, 0, sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_stats, 0, (64 * 8 + 8) * sizeof(unsigned long long), h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
     zbhip_close(h);
@@ -381,6 +434,11 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_key_base);
   (void)hipFree(h->d_key_blk);
   (void)hipFree(h->d_seen);
+  (void)hipFree(h->d_ovf);
+  (void)hipFree(h->d_ovf_count);
+  (void)hipFree(h->d_cont);
+  (void)hipFree(h->d_cont_order);
+  (void)hipFree(h->d_qspill);
   (void)hipFree(h->d_check_flag);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
@@ -409,6 +467,44 @@ const char* zbhip_name(zbhip_handle* h, uint32_t id) {
 const char* zbhip_string(zbhip_handle* h, uint32_t p, uint32_t s) {
   if (!h || p >= h->procs.size() || s >= h->procs[p].strings.size()) return "";
   return h->procs[p].strings[s].c_str();
+}
+
+// Deploy-time bound of the commands one batch of the process can hold (ProcessingStateMachine's
+// FIFO): every token reaching a node costs at most its ACTIVATE and COMPLETE commands, a token
+// count per node summed over the incoming flows (joins and exclusive gateways over-counted), plus the
+// initial command, the process's ACTIVATE and COMPLETE.  A cycle has no bound.
+static uint64_t batch_bound(const Proc& P) {
+  const size_t E = P.els.size();
+  std::vector<uint64_t> tok(E, 0);
+  std::vector<uint32_t> indeg(E, 0);
+  auto is_node = [&](size_t e) { return e > 0 && P.els[e].element_type != ZBHIP_EL_SEQUENCE_FLOW; };
+  for (size_t f = 0; f < E; ++f)
+    if (P.els[f].element_type == ZBHIP_EL_SEQUENCE_FLOW && P.els[f].flow_target < E) ++indeg[P.els[f].flow_target];
+  std::vector<uint32_t> ready;
+  for (size_t e = 0; e < E; ++e)
+    if (is_node(e) && indeg[e] == 0) {
+      tok[e] = 1;
+      ready.push_back((uint32_t)e);
+    }
+  size_t seen = 0, nodes = 0;
+  for (size_t e = 0; e < E; ++e) nodes += is_node(e);
+  uint64_t total = 3;
+  while (!ready.empty()) {
+    const uint32_t e = ready.back();
+    ready.pop_back();
+    ++seen;
+    total += 2 * tok[e];
+    const zbhip_element& N = P.els[e];
+    for (uint32_t i = 0; i < N.out_count; ++i) {
+      const uint32_t f = P.out[N.out_begin + i];
+      const uint32_t t = P.els[f].flow_target;
+      if (t >= E) continue;
+      tok[t] += tok[e];
+      if (tok[t] > (1u << 20)) return ~0ull;
+      if (--indeg[t] == 0) ready.push_back(t);
+    }
+  }
+  return seen == nodes ? total : ~0ull;  // nodes never reached: a cycle
 }
 
 // Builds the LDS program arena from every deployed process (layout: zb_internal.h).
@@ -568,6 +664,18 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if (rank(f) >= rank(h->variant)) h->variant = f;
   }
   h->procs.push_back(std::move(P));
+  {
+    const uint64_t limit = (uint64_t)h->cfg.max_commands_in_batch;
+    bool over = false;
+    uint64_t pend = 0;
+    for (const Proc& Q : h->procs) {
+      const uint64_t b = batch_bound(Q);
+      over |= b >= limit;
+      pend = std::max(pend, std::min(b, limit));
+    }
+    h->may_overflow = over;
+    h->max_pending = (uint32_t)pend;
+  }
   int rc = rebuild_program(h);
   if (rc != ZBHIP_OK) {
     h->procs.pop_back();
@@ -934,20 +1042,41 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
 
   // launches: one per round (commands of one instance are serialised in log order)
   h->launches.clear();
-  std::vector<std::pair<uint32_t, uint32_t>> spans;  // (first position, count)
+  uint32_t region = 0;
+  auto add_launch = [&](uint32_t first, uint32_t count, uint8_t src) {
+    h->launches.push_back({region, first, count, src});
+    region += (count + B - 1) / B;
+  };
   if (h->round_begin.empty()) {
-    if (n) spans.push_back({0, n});
+    if (n) add_launch(0, n, 0);
   } else {
     for (size_t r = 0; r + 1 < h->round_begin.size(); ++r)
-      spans.push_back({h->round_begin[r], h->round_begin[r + 1] - h->round_begin[r]});
-  }
-  uint32_t region = 0;
-  for (auto& sp : spans) {
-    h->launches.push_back({region, sp.first});
-    region += (sp.second + B - 1) / B;
+      add_launch(h->round_begin[r], h->round_begin[r + 1] - h->round_begin[r], 1);
   }
   if (region > h->regions_cap || (size_t)region * P.region_stride > h->region_records)
     return ZBHIP_ENOMEM;  // too many rounds for the region pool
+  // follow-up commands past the batch limit (not for message partitions: their local commands
+  // carry context the log entry would need -> FB_BATCH_LIMIT); batch FIFO spill for fan-outs
+  // larger than the LDS ring
+  const bool overflow = h->may_overflow && !h->msg();
+  if (overflow) {
+    P.ovf = h->d_ovf;
+    P.ovf_count = h->d_ovf_count;
+    P.ovf_cap = h->cfg.max_commands;
+  }
+  if (h->max_pending > step_queue(h->variant) && h->variant != 3 && !getenv("ZBHIP_CHUNKS_PER_WG")) {
+    const uint32_t cap = h->max_pending;
+    const size_t words = (size_t)step_resident(h->variant, P.prog_words) * B * cap;
+    if (words > h->qspill_words) {
+      (void)hipFree(h->d_qspill);
+      h->d_qspill = nullptr;
+      h->qspill_words = 0;
+      if (dalloc(&h->d_qspill, words) != hipSuccess) return ZBHIP_ENOMEM;
+      h->qspill_words = words;
+    }
+    P.qspill = h->d_qspill;
+    P.qspill_cap = cap;
+  }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timed) {
     e0 = next_event(h);
@@ -955,12 +1084,76 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     if (!e0 || !e1) return ZBHIP_EDEVICE;
     HIPCHK(hipEventRecord(e0, h->stream));
   }
-  for (size_t l = 0; l < spans.size(); ++l) {
-    P.order = h->round_begin.empty() ? nullptr : h->d_order + spans[l].first;
-    P.n_launch = spans[l].second;
-    P.region_base = h->launches[l].first;
+  for (const auto& l : h->launches) {
+    P.order = l.src == 0 ? nullptr : h->d_order + l.first;
+    P.n_launch = l.count;
+    P.region_base = l.region;
     HIPCHK(launch_step(h->variant, P, h->stream));
   }
+  // continuation: the follow-up commands written to the log unprocessed become batches of their
+  // own after the window, in the order written (source command, then record ordinal); theirs may
+  // overflow again
+  uint32_t n_all = n;
+  h->cont_cmds.clear();
+  h->cont_order.clear();
+  std::vector<uint2> hdr_tmp;
+  while (overflow) {
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpyAsync(&cnt, h->d_ovf_count, sizeof cnt, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (cnt == 0) break;
+    if (cnt > h->cfg.max_commands) return ZBHIP_ENOMEM;
+    std::vector<uint4> ov(cnt);
+    HIPCHK(hipMemcpy(ov.data(), h->d_ovf, cnt * sizeof(uint4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemsetAsync(h->d_ovf_count, 0, sizeof(uint32_t), h->stream));
+    hdr_tmp.resize(n_all);
+    HIPCHK(hipMemcpy(hdr_tmp.data(), h->d_cmd_hdr, n_all * sizeof(uint2), hipMemcpyDeviceToHost));
+    // entries of batches that fell back are void (their records were dropped)
+    ov.erase(std::remove_if(ov.begin(), ov.end(), [&](const uint4& e) {
+               return e.x >= n_all || ((hdr_tmp[e.x].y >> 16) & 0xFF) != ST_OK;
+             }), ov.end());
+    if (ov.empty()) break;
+    std::sort(ov.begin(), ov.end(), [](const uint4& a, const uint4& b) {
+      return a.x != b.x ? a.x < b.x : (a.z & 0xFFFF) < (b.z & 0xFFFF);
+    });
+    if ((size_t)n_all + ov.size() > h->cfg.max_commands) return ZBHIP_ENOMEM;
+    // the continuation window: rounds so that an instance appears once per launch, in order
+    const uint32_t first_new = (uint32_t)h->cont_cmds.size();
+    std::unordered_map<uint32_t, uint32_t> rounds_of;
+    std::vector<uint32_t> round(ov.size());
+    uint32_t max_round = 0;
+    for (size_t k = 0; k < ov.size(); ++k) {
+      zbhip_command c{};
+      c.instance = ov[k].w;
+      c.kind = CMD_FOLLOWUP;
+      c.ref = (uint16_t)(ov[k].z >> 16);
+      c.doc_begin = ov[k].y;
+      h->cont_cmds.push_back(c);
+      round[k] = rounds_of[c.instance]++;
+      max_round = std::max(max_round, round[k]);
+    }
+    HIPCHK(hipMemcpyAsync(h->d_cont + first_new, h->cont_cmds.data() + first_new, ov.size() * sizeof(zbhip_command),
+                          hipMemcpyHostToDevice, h->stream));
+    for (uint32_t r = 0; r <= max_round; ++r) {
+      const uint32_t begin = (uint32_t)h->cont_order.size();
+      for (size_t k = 0; k < ov.size(); ++k)
+        if (round[k] == r) h->cont_order.push_back(n_all + (uint32_t)k);
+      add_launch(begin, (uint32_t)h->cont_order.size() - begin, 2);
+    }
+    if (region > h->regions_cap || (size_t)region * P.region_stride > h->region_records) return ZBHIP_ENOMEM;
+    HIPCHK(hipMemcpyAsync(h->d_cont_order, h->cont_order.data(), h->cont_order.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, h->stream));
+    P.cmds = reinterpret_cast<const uint4*>(h->d_cont);
+    P.cmd_base = n;
+    for (size_t l = h->launches.size() - (max_round + 1); l < h->launches.size(); ++l) {
+      P.order = h->d_cont_order + h->launches[l].first;
+      P.n_launch = h->launches[l].count;
+      P.region_base = h->launches[l].region;
+      HIPCHK(launch_step(h->variant, P, h->stream));
+    }
+    n_all += (uint32_t)ov.size();
+  }
+  h->next_source += (int64_t)(n_all - n);  // the continuation batches' log positions follow
   if (h->msg()) {
     // keys of the window in log order: real process-instance keys, outbox and slot-row references
     HIPCHK(launch_keyscan(h->d_cmd_hdr, h->d_cmd_hdr2, P.cmds, n, h->d_key_blk, h->d_key_base, h->d_key_counter,
@@ -969,8 +1162,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     h->outbox_taken = false;
   }
   if (timed) HIPCHK(hipEventRecord(e1, h->stream));
-  h->stats.launches = (uint32_t)spans.size();
-  h->stats.rounds = (uint32_t)spans.size();
+  h->stats.launches = (uint32_t)h->launches.size();
+  h->stats.rounds = (uint32_t)h->launches.size();
   h->n_regions = region;
   h->ran = true;
   h->drain_cmd = 0;
@@ -982,7 +1175,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     // benchmarking mode: nothing is copied back and nothing waits; keys are not relabelled
     h->relabel_ok = false;
     h->stats_dirty = true;
-    return (int)n;
+    h->n_cmds = n_all;
+    return (int)n_all;
   }
   if (h->external) {
     // a device-resident window with results (e.g. an exchange inbox in drain mode): the host
@@ -1001,6 +1195,11 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     HIPCHK(hipStreamSynchronize(h->stream));
     for (auto& c : h->h_cmds) h->published |= c.kind == ZBHIP_CMD_PUBLISH;
   }
+  h->h_cmds.resize(n);
+  h->h_cmds.insert(h->h_cmds.end(), h->cont_cmds.begin(), h->cont_cmds.end());
+  h->n_cmds = n_all;
+  {
+  const uint32_t n = n_all;  // the window and its continuation batches
 
   // ---- results: headers + records gathered into log order (drain path, off the hot loop) ----
   h->h_hdr.resize(n);
@@ -1020,9 +1219,9 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   // record offset of every command: regions follow launch order, lanes follow the launch order
   h->h_off.assign(n + 1, 0);
   uint64_t off = 0;
-  for (auto& sp : spans)
-    for (uint32_t k = 0; k < sp.second; ++k) {
-      const uint32_t c = h->round_begin.empty() ? sp.first + k : h->h_order[sp.first + k];
+  for (const auto& l : h->launches)
+    for (uint32_t k = 0; k < l.count; ++k) {
+      const uint32_t c = l.src == 0 ? l.first + k : l.src == 1 ? h->h_order[l.first + k] : h->cont_order[l.first + k];
       h->h_off[c] = off;
       off += h->h_hdr[c].x & 0xFFFF;
     }
@@ -1033,7 +1232,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   h->h_base.assign(n, 0);
   h->fin_next = 0;
   h->results = true;
-  return (int)n;
+  }
+  return (int)n_all;
 }
 
 int64_t zbhip_pending_records(zbhip_handle* h) {
@@ -1135,6 +1335,7 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.value_type = ZBHIP_VT_PROCESS_INSTANCE;
       r.intent = (uint8_t)c6;
       r.record_type = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
+      r.unprocessed = !rej && c6 >= 8 && (fl & F_UNPROCESSED) ? 1 : 0;
     } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE) {
       r.value_type = ZBHIP_VT_JOB;
       r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED : ZBHIP_JOB_COMPLETE;
@@ -1189,24 +1390,20 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
     std::vector<size_t> first(n + 1, 0);
     for (size_t c = 0; c < n; ++c) first[c + 1] = first[c] + (h->h_hdr[c].x & 0xFFFF);
     if (first[n] != h->h_out.size()) return ZBHIP_EDEVICE;
-    const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::atomic<int> err{0};
-    std::vector<std::thread> pool;
-    for (unsigned t = 0; t < T; ++t)
-      pool.emplace_back([&, t]() {
-        // commands split by record count, so every thread expands about total / T records
-        const size_t lo = std::lower_bound(first.begin(), first.end(), first[n] * t / T) - first.begin();
-        const size_t hi = std::lower_bound(first.begin(), first.end(), first[n] * (t + 1) / T) - first.begin();
-        for (size_t c = lo; c < hi && c < n; ++c) {
-          const uint2* rows = h->h_out.data() + h->h_off[c];
-          const uint32_t nrec = h->h_hdr[c].x & 0xFFFF;
-          for (uint32_t i = 0; i < nrec; ++i) {
-            const int rc = expand_plain(h, c, h->h_cmds[c].instance, rows[i], i, out[first[c] + i]);
-            if (rc) { err.store(rc); return; }
-          }
+    parallel_for(host_threads(), [&](unsigned t, unsigned T) {
+      // commands split by record count, so every thread expands about total / T records
+      const size_t lo = std::lower_bound(first.begin(), first.end(), first[n] * t / T) - first.begin();
+      const size_t hi = std::lower_bound(first.begin(), first.end(), first[n] * (t + 1) / T) - first.begin();
+      for (size_t c = lo; c < hi && c < n; ++c) {
+        const uint2* rows = h->h_out.data() + h->h_off[c];
+        const uint32_t nrec = h->h_hdr[c].x & 0xFFFF;
+        for (uint32_t i = 0; i < nrec; ++i) {
+          const int rc = expand_plain(h, c, h->h_cmds[c].instance, rows[i], i, out[first[c] + i]);
+          if (rc) { err.store(rc); return; }
         }
-      });
-    for (auto& th : pool) th.join();
+      }
+    });
     if (err.load()) return err.load();
     h->drain_cmd = n;
     if (n_out) *n_out = first[n];

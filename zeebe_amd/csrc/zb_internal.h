@@ -88,6 +88,12 @@ enum : uint8_t {
 };
 // cmd_hdr.y bit 31: the batch ended its process instance (completed; the slot is free)
 constexpr uint32_t HDR_ENDED = 1u << 31;
+// compact record flags (bits 24..31 of y) of a follow-up command the PSM wrote to the log
+// unprocessed (past maxCommandsInBatch, ProcessingStateMachine.java:388-417)
+constexpr uint32_t F_UNPROCESSED = 0x80;
+// internal command kind: such a follow-up command read back from the log as a batch of its own
+// (instance = its instance slot, ref = its process, doc_begin = its queue entry)
+constexpr uint8_t CMD_FOLLOWUP = 0x20;
 
 // Program arena (u32 words), LDS-staged by every workgroup:
 //   [0] n_procs, [1 .. n_procs] word offset of each process block (multiple of 4)
@@ -163,6 +169,15 @@ struct StepParams {
   zbhip_xpart_cmd* xout;      // [n_cmds * kOut]
   int32_t partition_id, partition_count;
   uint32_t stamp;             // window stamp: hdr.w / slot_hdr.y of a subject whose command fell back
+  uint32_t cmd_base;          // window index of cmds[0] (continuation launches of follow-up batches)
+  // batch FIFO entries beyond the LDS ring (large fan-outs): per resident lane, qspill_cap entries
+  // strided by gridDim.x * B
+  uint32_t* qspill;
+  uint32_t qspill_cap;
+  // follow-up commands past maxCommandsInBatch: {window index, queue entry, record ordinal, 0}
+  uint4* ovf;
+  uint32_t* ovf_count;
+  uint32_t ovf_cap;
 };
 
 }  // namespace zb

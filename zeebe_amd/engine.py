@@ -196,7 +196,9 @@ class Partition:
 
     def drain(self, out=None):
         """The window's records in log order; `out` (a RECORD_DTYPE array) is reused when it is
-        large enough, so a host loop over windows does not fault in fresh pages every time."""
+        large enough, so a host loop over windows does not fault in fresh pages every time.  The
+        result is then a view of `out`: it is only valid until the next drain into the same buffer
+        (callers that keep records, like EngineRule, copy them)."""
         n = self.L.zbhip_pending_records(self.h)
         # every field of a drained record is written by zbhip_drain: no zero fill (a window of
         # 10^6 linear-10 commands drains ~0.9 GB)
