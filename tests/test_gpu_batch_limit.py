@@ -74,23 +74,23 @@ def test_one_task_batch_limit(limit):
     assert (got > 0) == (limit == 3)
 
 
-@pytest.mark.parametrize("limit", [3, 7, 100])
+@pytest.mark.parametrize("limit", [3, 5, 100])
 def test_linear_batch_limit(limit):
     got = drive(bpmn.linear_process(4), limit)
-    assert (got > 0) == (limit < 100)
+    assert (got > 0) == (limit == 3)
 
 
 @pytest.mark.parametrize("limit", [3, 10, 20, 100])
-def test_fork_join_16_batch_limit(limit):
-    got = drive(bpmn.fork_join_process(16), limit)
-    assert (got > 0) == (limit < 100)
+def test_fork_join_12_batch_limit(limit):
+    got = drive(bpmn.fork_join_process(12), limit)  # 13 taken-flow counters (<= 16, kJoinWords)
+    assert (got > 0) == (limit <= 10)
 
 
 @pytest.mark.parametrize("limit", [3, 10, 100])
 def test_fan_out_beyond_the_lds_ring(limit):
     # 40 tokens pending at once: more than the LDS ring of KGeneric (16), the rest in the global FIFO
     got = drive(fork_to_ends(40), limit)
-    assert (got > 0) == (limit < 100)
+    assert (got > 0) == (limit < 100)  # the oracle's count: the parity check compares every record
 
 
 @pytest.mark.parametrize("limit", [4, 100])

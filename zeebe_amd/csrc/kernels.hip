@@ -378,7 +378,8 @@ __device__ __forceinline__ void overflow(Lane<K>& L, uint32_t entry) {
   if (!P.ovf) { set_fail(L, FB_BATCH_LIMIT); return; }
   const uint32_t slot = atomicAdd(P.ovf_count, 1u);
   if (slot >= P.ovf_cap) { set_fail(L, FB_BATCH_LIMIT); return; }
-  P.ovf[slot] = make_uint4(L.ci, entry, L.nrec - 1, 0u);
+  // {window index, queue entry, record ordinal | process << 16, instance slot}
+  P.ovf[slot] = make_uint4(L.ci, entry, (L.nrec - 1) | ((uint32_t)L.proc << 16), P.cmds[L.ci - P.cmd_base].x);
 }
 
 // a follow-up command of the batch: its COMMAND record, then the FIFO (or the overflow list)

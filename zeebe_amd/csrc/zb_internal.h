@@ -174,7 +174,8 @@ struct StepParams {
   // strided by gridDim.x * B
   uint32_t* qspill;
   uint32_t qspill_cap;
-  // follow-up commands past maxCommandsInBatch: {window index, queue entry, record ordinal, 0}
+  // follow-up commands past maxCommandsInBatch: {window index, queue entry, record ordinal |
+  // process << 16, instance slot}
   uint4* ovf;
   uint32_t* ovf_count;
   uint32_t ovf_cap;
