@@ -523,6 +523,29 @@ int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n);
 int zbhip_key_before(zbhip_handle* h, size_t i, int64_t* key);
 int zbhip_set_external_keys(zbhip_handle* h, size_t i, uint32_t nkeys);
 
+/* ---- zb-db bytes back into HBM (restart / hand-back; the reference's
+ * replay-equivalence property, ReplayStateRandomizedPropertyTest.java:74-140) ----------------------
+ * One zb-db entry -> its canonical state row (the inverse of zbhip_serializer_encode_state_row);
+ * string variable values are interned through `intern` (NULL: refused).  Returns the row's length,
+ * 0 for a column family outside the path, or an error. */
+typedef int64_t (*zbhip_string_interner)(void* ctx, const char* bytes, size_t len);
+int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t column_family, const uint8_t* key, size_t key_len,
+                                        const uint8_t* value, size_t value_len, zbhip_string_interner intern,
+                                        void* ictx, char* row, size_t cap);
+/* Loads process instances into free instance slots from their zb-db entries (a flat buffer of
+ * entries, each: uint32 column family, uint32 key length, uint32 value length, key bytes, value bytes
+ * -- the entries zbhip_export_state_db / zbhip_export_instances_db produce, e.g. a RocksDB
+ * snapshot's).  The deployments (same definition keys) must be deployed first.  The instances take
+ * the slots first_slot, first_slot + 1, ... in process-instance-key order; every key keeps its value
+ * (zbhip_resolve_key resolves their job keys and process-instance keys), and the key counter moves
+ * to KEY latestKey if that is larger.  *n_instances = instances loaded.  Column families of the
+ * message partition side (MESSAGE_SUBSCRIPTION_*) are refused (ZBHIP_EUNSUPP): their routing handles
+ * to the subscribers' instance slots are not in the reference's state. */
+int zbhip_import_state_db(zbhip_handle* h, const uint8_t* entries, size_t len, uint32_t first_slot,
+                          uint32_t* n_instances);
+/* The same from canonical state rows (zbhip_export_state's format), '\n'-separated. */
+int zbhip_import_state(zbhip_handle* h, const char* rows, size_t len, uint32_t first_slot, uint32_t* n_instances);
+
 /* Library build information ("gfx950 …"). */
 const char* zbhip_build_info(void);
 

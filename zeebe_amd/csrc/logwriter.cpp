@@ -16,6 +16,7 @@
 // Deploy time compiles, per element, the constant msgpack runs of its records (everything but
 // the keys), so a record costs a few memcpys and the variable-length key integers.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -761,4 +762,355 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
   sink(ctx, ord, reinterpret_cast<const uint8_t*>(k.data()), k.size(), reinterpret_cast<const uint8_t*>(v.data()),
        v.size());
   return 1;
+}
+
+// ---- zb-db entry -> canonical state row (the inverse of zbhip_serializer_encode_state_row) ------
+// The importer's front end (zbhip_import_state_db): RocksDB keys and the msgpack of the state
+// objects read back exactly as the encoder above writes them (MsgPackReader.java semantics for the
+// value types the path stores).
+namespace {
+
+struct MpNode {
+  enum Kind { NIL, BOOL, INT, FLOAT, STR, BIN, MAP, ARR } k = NIL;
+  int64_t i = 0;
+  double f = 0;
+  std::string s;                                   // STR / BIN bytes
+  std::vector<std::pair<std::string, MpNode>> kv;  // MAP (string keys)
+  std::vector<MpNode> arr;
+  const MpNode* get(const char* name) const {
+    for (auto& e : kv)
+      if (e.first == name) return &e.second;
+    return nullptr;
+  }
+};
+
+struct MpReader {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool need(size_t n) const { return (size_t)(e - p) >= n; }
+  uint64_t be(int n) {
+    uint64_t v = 0;
+    for (int k = 0; k < n; ++k) v = (v << 8) | *p++;
+    return v;
+  }
+  bool parse(MpNode& o, int depth = 0) {
+    if (depth > 8 || !need(1)) return false;
+    const uint8_t t = *p++;
+    auto bytes = [&](uint32_t n, MpNode::Kind k) {
+      if (!need(n)) return false;
+      o.k = k;
+      o.s.assign(reinterpret_cast<const char*>(p), n);
+      p += n;
+      return true;
+    };
+    auto map = [&](uint32_t n) {
+      o.k = MpNode::MAP;
+      for (uint32_t j = 0; j < n; ++j) {
+        MpNode key, v;
+        if (!parse(key, depth + 1) || key.k != MpNode::STR || !parse(v, depth + 1)) return false;
+        o.kv.emplace_back(std::move(key.s), std::move(v));
+      }
+      return true;
+    };
+    auto arr = [&](uint32_t n) {
+      o.k = MpNode::ARR;
+      o.arr.resize(n);
+      for (uint32_t j = 0; j < n; ++j)
+        if (!parse(o.arr[j], depth + 1)) return false;
+      return true;
+    };
+    if (t <= 0x7f) { o.k = MpNode::INT; o.i = t; return true; }
+    if (t >= 0xe0) { o.k = MpNode::INT; o.i = (int8_t)t; return true; }
+    if ((t & 0xf0) == 0x80) return map(t & 0x0f);
+    if ((t & 0xf0) == 0x90) return arr(t & 0x0f);
+    if ((t & 0xe0) == 0xa0) return bytes(t & 0x1f, MpNode::STR);
+    switch (t) {
+      case 0xc0: o.k = MpNode::NIL; return true;
+      case 0xc2: case 0xc3: o.k = MpNode::BOOL; o.i = t == 0xc3; return true;
+      case 0xc4: return need(1) && bytes((uint32_t)be(1), MpNode::BIN);
+      case 0xc5: return need(2) && bytes((uint32_t)be(2), MpNode::BIN);
+      case 0xc6: return need(4) && bytes((uint32_t)be(4), MpNode::BIN);
+      case 0xcb: {
+        if (!need(8)) return false;
+        const uint64_t u = be(8);
+        o.k = MpNode::FLOAT;
+        memcpy(&o.f, &u, 8);
+        return true;
+      }
+      case 0xcc: if (!need(1)) return false; o.k = MpNode::INT; o.i = (int64_t)be(1); return true;
+      case 0xcd: if (!need(2)) return false; o.k = MpNode::INT; o.i = (int64_t)be(2); return true;
+      case 0xce: if (!need(4)) return false; o.k = MpNode::INT; o.i = (int64_t)be(4); return true;
+      case 0xcf: if (!need(8)) return false; o.k = MpNode::INT; o.i = (int64_t)be(8); return true;
+      case 0xd0: if (!need(1)) return false; o.k = MpNode::INT; o.i = (int8_t)be(1); return true;
+      case 0xd1: if (!need(2)) return false; o.k = MpNode::INT; o.i = (int16_t)be(2); return true;
+      case 0xd2: if (!need(4)) return false; o.k = MpNode::INT; o.i = (int32_t)be(4); return true;
+      case 0xd3: if (!need(8)) return false; o.k = MpNode::INT; o.i = (int64_t)be(8); return true;
+      case 0xd9: return need(1) && bytes((uint32_t)be(1), MpNode::STR);
+      case 0xda: return need(2) && bytes((uint32_t)be(2), MpNode::STR);
+      case 0xdb: return need(4) && bytes((uint32_t)be(4), MpNode::STR);
+      case 0xdc: return need(2) && arr((uint32_t)be(2));
+      case 0xdd: return need(4) && arr((uint32_t)be(4));
+      case 0xde: return need(2) && map((uint32_t)be(2));
+      case 0xdf: return need(4) && map((uint32_t)be(4));
+      default: return false;
+    }
+  }
+};
+
+bool mp_read(const uint8_t* v, size_t n, MpNode& out) {
+  MpReader r{v, v + n};
+  return r.parse(out) && r.p == r.e;
+}
+
+// key parts: DbLong / DbInt / DbString (big-endian, DbString 4-byte length)
+struct KeyReader {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool ok = true;
+  int64_t dblong() {
+    if (e - p < 8) { ok = false; return 0; }
+    uint64_t v = 0;
+    for (int k = 0; k < 8; ++k) v = (v << 8) | *p++;
+    return (int64_t)v;
+  }
+  int32_t dbint() {
+    if (e - p < 4) { ok = false; return 0; }
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k) v = (v << 8) | *p++;
+    return (int32_t)v;
+  }
+  std::string dbstr() {
+    const int32_t n = dbint();
+    if (!ok || n < 0 || e - p < n) { ok = false; return std::string(); }
+    std::string s(reinterpret_cast<const char*>(p), (size_t)n);
+    p += n;
+    return s;
+  }
+};
+
+int enum_index(const char* (*name)(uint32_t), uint32_t count, const std::string& s) {
+  for (uint32_t t = 0; t < count; ++t)
+    if (s == name(t)) return (int)t;
+  return -1;
+}
+int state_index(const std::string& s) {
+  for (int t = ZBHIP_PI_ELEMENT_ACTIVATING; t <= ZBHIP_PI_ELEMENT_TERMINATED; ++t)
+    if (s == state_text(t)) return t;
+  return -1;
+}
+int64_t mi(const MpNode* n) { return n && n->k == MpNode::INT ? n->i : 0; }
+std::string ms(const MpNode* n) { return n && n->k == MpNode::STR ? n->s : std::string(); }
+int mb(const MpNode* n) { return n && n->k == MpNode::BOOL && n->i ? 1 : 0; }
+
+}  // namespace
+
+extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t cf, const uint8_t* key, size_t klen,
+                                                   const uint8_t* val, size_t vlen, zbhip_string_interner intern,
+                                                   void* ictx, char* row, size_t cap) {
+  if (!s || (!key && klen) || (!val && vlen) || !row || cap == 0) return ZBHIP_EINVAL;
+  KeyReader K{key, key + klen};
+  if (K.dblong() != (int64_t)cf || !K.ok) return ZBHIP_EINVAL;
+  std::string out;
+  char b[512];
+  MpNode v;
+  auto value = [&]() { return mp_read(val, vlen, v) && v.k == MpNode::MAP; };
+  auto be_long = [&](const uint8_t* p, size_t n, int64_t& o) {
+    if (n != 8) return false;
+    uint64_t x = 0;
+    for (int k = 0; k < 8; ++k) x = (x << 8) | p[k];
+    o = (int64_t)x;
+    return true;
+  };
+  switch (cf) {
+    case 1: {  // KEY
+      const std::string name = K.dbstr();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "KEY|%s|%lld", name.c_str(), (long long)mi(v.get("nextValue")));
+      out = b;
+      break;
+    }
+    case 7: {  // ELEMENT_INSTANCE_KEY
+      const int64_t ek = K.dblong();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      const MpNode* rec = v.get("elementRecord");
+      const MpNode* pir = rec ? rec->get("processInstanceRecord") : nullptr;
+      if (!rec || !pir) return ZBHIP_EINVAL;
+      const int state = state_index(ms(rec->get("state")));
+      const int et = enum_index(element_type_name, 19, ms(pir->get("bpmnElementType")));
+      const int ev = enum_index(event_type_name, 10, ms(pir->get("bpmnEventType")));
+      if (state < 0 || et < 0 || ev < 0) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b,
+               "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%lld,childActivatedCount=%lld,childCompletedCount=%lld,"
+               "childTerminatedCount=%lld,jobKey=%lld,multiInstanceLoopCounter=%lld,interruptingElementId=%s,"
+               "calledChildInstanceKey=%lld,state=%d,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
+               "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%lld",
+               (long long)ek, (long long)mi(v.get("parentKey")), (long long)mi(v.get("childCount")),
+               (long long)mi(v.get("childActivatedCount")), (long long)mi(v.get("childCompletedCount")),
+               (long long)mi(v.get("childTerminatedCount")), (long long)mi(v.get("jobKey")),
+               (long long)mi(v.get("multiInstanceLoopCounter")), ms(v.get("interruptingElementId")).c_str(),
+               (long long)mi(v.get("calledChildInstanceKey")), state, ms(pir->get("elementId")).c_str(), et, ev,
+               (long long)mi(pir->get("flowScopeKey")), (long long)mi(pir->get("processInstanceKey")),
+               (long long)mi(pir->get("processDefinitionKey")), (long long)mi(v.get("activeSequenceFlows")));
+      out = b;
+      break;
+    }
+    case 6: case 55: {  // ELEMENT_INSTANCE_PARENT_CHILD, PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY -> DbNil
+      const int64_t a = K.dblong(), c = K.dblong();
+      if (!K.ok) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "%s|%lld|%lld", cf == 6 ? "ELEMENT_INSTANCE_PARENT_CHILD" : "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY",
+               (long long)a, (long long)c);
+      out = b;
+      break;
+    }
+    case 9: {  // ELEMENT_INSTANCE_CHILD_PARENT -> DbLong
+      const int64_t c = K.dblong();
+      int64_t parent = 0;
+      if (!K.ok || !be_long(val, vlen, parent)) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", (long long)c, (long long)parent);
+      out = b;
+      break;
+    }
+    case 8: {  // NUMBER_OF_TAKEN_SEQUENCE_FLOWS -> DbInt
+      const int64_t scope = K.dblong();
+      const std::string gw = K.dbstr(), flow = K.dbstr();
+      if (!K.ok || vlen != 4) return ZBHIP_EINVAL;
+      const int32_t n = (int32_t)(((uint32_t)val[0] << 24) | ((uint32_t)val[1] << 16) | ((uint32_t)val[2] << 8) | val[3]);
+      snprintf(b, sizeof b, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS|%lld|%s|%s|%d", (long long)scope, gw.c_str(), flow.c_str(), n);
+      out = b;
+      break;
+    }
+    case 10: {  // VARIABLES
+      const int64_t scope = K.dblong();
+      const std::string name = K.dbstr();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      const MpNode* bin = v.get("value");
+      MpNode x;
+      if (!bin || bin->k != MpNode::BIN ||
+          !mp_read(reinterpret_cast<const uint8_t*>(bin->s.data()), bin->s.size(), x))
+        return ZBHIP_EINVAL;
+      int type;
+      long long dv = 0;
+      switch (x.k) {
+        case MpNode::NIL: type = ZBHIP_DOC_NIL; break;
+        case MpNode::BOOL: type = ZBHIP_DOC_BOOL; dv = x.i; break;
+        case MpNode::INT: type = ZBHIP_DOC_INT; dv = x.i; break;
+        case MpNode::FLOAT: {  // exact 6-digit scaled decimals only (the device's DEC)
+          type = ZBHIP_DOC_DEC;
+          const double sc = x.f * 1e6;
+          if (!(sc > -9.2e18 && sc < 9.2e18)) return ZBHIP_EUNSUPP;
+          dv = llround(sc);
+          if ((double)dv / 1e6 != x.f) return ZBHIP_EUNSUPP;
+          break;
+        }
+        case MpNode::STR: {
+          if (!intern) return ZBHIP_EUNSUPP;
+          const int64_t id = intern(ictx, x.s.data(), x.s.size());
+          if (id < 0) return (int)id;
+          type = ZBHIP_DOC_STR;
+          dv = id;
+          break;
+        }
+        default: return ZBHIP_EUNSUPP;  // documents / arrays: outside the device's variables
+      }
+      snprintf(b, sizeof b, "VARIABLES|%lld|%s|key=%lld,type=%d,value=%lld", (long long)scope, name.c_str(),
+               (long long)mi(v.get("key")), type, dv);
+      out = b;
+      break;
+    }
+    case 37: {  // EVENT_SCOPE
+      const int64_t k = K.dblong();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "EVENT_SCOPE|%lld|accepting=%d,interrupted=%d", (long long)k, mb(v.get("accepting")),
+               mb(v.get("interrupted")));
+      out = b;
+      break;
+    }
+    case 16: {  // JOBS
+      const int64_t k = K.dblong();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      const MpNode* j = v.get("jobRecord");
+      if (!j) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b,
+               "JOBS|%lld|type=%s,retries=%lld,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
+               "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%lld,tenantId=%s",
+               (long long)k, ms(j->get("type")).c_str(), (long long)mi(j->get("retries")), ms(j->get("elementId")).c_str(),
+               (long long)mi(j->get("elementInstanceKey")), (long long)mi(j->get("processInstanceKey")),
+               ms(j->get("bpmnProcessId")).c_str(), (long long)mi(j->get("processDefinitionKey")),
+               (long long)mi(j->get("processDefinitionVersion")), ms(j->get("tenantId")).c_str());
+      out = b;
+      break;
+    }
+    case 17: {  // JOB_STATES
+      const int64_t k = K.dblong();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "JOB_STATES|%lld|%s", (long long)k, ms(v.get("jobState")).c_str());
+      out = b;
+      break;
+    }
+    case 76: {  // JOB_ACTIVATABLE [[type, jobKey], tenant]
+      const std::string type = K.dbstr();
+      const int64_t k = K.dblong();
+      const std::string tenant = K.dbstr();
+      if (!K.ok) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "JOB_ACTIVATABLE|%s|%s|%lld", type.c_str(), tenant.c_str(), (long long)k);
+      out = b;
+      break;
+    }
+    case 75: {  // PROCESS_SUBSCRIPTION_BY_KEY [eik, [tenant, name]]
+      const int64_t eik = K.dblong();
+      const std::string tenant = K.dbstr(), name = K.dbstr();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      const MpNode* r = v.get("record");
+      if (!r) return ZBHIP_EINVAL;
+      std::string st = ms(v.get("state"));
+      if (st.rfind("STATE_", 0) == 0) st = st.substr(6);
+      snprintf(b, sizeof b,
+               "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%lld,processInstanceKey=%lld,"
+               "bpmnProcessId=%s,messageKey=%lld,correlationKey=%s,elementId=%s,interrupting=%d",
+               (long long)eik, name.c_str(), (long long)mi(v.get("key")), st.c_str(),
+               (long long)mi(r->get("subscriptionPartitionId")), (long long)mi(r->get("processInstanceKey")),
+               ms(r->get("bpmnProcessId")).c_str(), (long long)mi(r->get("messageKey")),
+               ms(r->get("correlationKey")).c_str(), ms(r->get("elementId")).c_str(), mb(r->get("interrupting")));
+      out = b;
+      break;
+    }
+    case 27: {  // MESSAGE_SUBSCRIPTION_BY_KEY [eik, name]
+      const int64_t eik = K.dblong();
+      const std::string name = K.dbstr();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      const MpNode* r = v.get("record");
+      if (!r) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b,
+               "MESSAGE_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,correlating=%d,processInstanceKey=%lld,bpmnProcessId=%s,"
+               "messageKey=%lld,correlationKey=%s,interrupting=%d",
+               (long long)eik, name.c_str(), (long long)mi(v.get("key")), mb(v.get("correlating")),
+               (long long)mi(r->get("processInstanceKey")), ms(r->get("bpmnProcessId")).c_str(),
+               (long long)mi(r->get("messageKey")), ms(r->get("correlationKey")).c_str(), mb(r->get("interrupting")));
+      out = b;
+      break;
+    }
+    case 74: {  // MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY
+      const std::string tenant = K.dbstr(), name = K.dbstr(), corr = K.dbstr();
+      const int64_t eik = K.dblong();
+      if (!K.ok) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY|%s|%s|%s|%lld", tenant.c_str(), name.c_str(),
+               corr.c_str(), (long long)eik);
+      out = b;
+      break;
+    }
+    case 54: {  // MESSAGE_STATS
+      const std::string name = K.dbstr();
+      int64_t n = 0;
+      if (!K.ok || !be_long(val, vlen, n)) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "MESSAGE_STATS|messagesDeadlineCount|%lld", (long long)n);
+      out = b;
+      break;
+    }
+    default:
+      return 0;  // not a column family of the path
+  }
+  if (K.p != K.e) return ZBHIP_EINVAL;  // trailing key bytes
+  if (out.size() + 1 > cap) return ZBHIP_ENOMEM;
+  memcpy(row, out.c_str(), out.size() + 1);
+  return (int)out.size();
 }

@@ -13,6 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <set>
+#include <tuple>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -1962,3 +1965,294 @@ int zbhip_export_instances(zbhip_handle* h, const uint32_t* instances, size_t n,
 }
 
 }  // extern "C"
+
+// ---- import: canonical rows / zb-db entries -> SoA rows ---------------------
+namespace {
+std::vector<std::string> split_row(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  size_t a = 0;
+  for (;;) {
+    const size_t b = s.find(sep, a);
+    out.push_back(s.substr(a, b == std::string::npos ? std::string::npos : b - a));
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  return out;
+}
+std::unordered_map<std::string, std::string> row_fields(const std::string& s) {
+  std::unordered_map<std::string, std::string> f;
+  for (const auto& kv : split_row(s, ',')) {
+    const size_t e = kv.find('=');
+    if (e != std::string::npos) f[kv.substr(0, e)] = kv.substr(e + 1);
+  }
+  return f;
+}
+int64_t to_ll(const std::string& s) { return strtoll(s.c_str(), nullptr, 10); }
+
+struct ImpElement {
+  int64_t key = 0, job = 0, pik = 0, fs = 0, def = 0, child_count = 0, asf = 0;
+  uint32_t state = 0, type = 0;
+  std::string id;
+};
+struct ImpVar {
+  int64_t scope = 0, key = 0, value = 0;
+  std::string name;
+  uint32_t type = 0;
+};
+struct ImpPms {
+  int64_t eik = 0, key = 0;
+  std::string name, corr, elem_id;
+  uint32_t state = 0, part = 0, intr = 0;
+};
+int64_t string_interner(void* ctx, const char* b, size_t n) {
+  return zbhip_intern_string(static_cast<zbhip_handle*>(ctx), b, n);
+}
+}  // namespace
+
+extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len, uint32_t first_slot,
+                                  uint32_t* n_instances) {
+  if (!h || (len && !text)) return ZBHIP_EINVAL;
+  if (n_instances) *n_instances = 0;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  std::map<int64_t, ImpElement> els;
+  std::vector<ImpVar> vars;
+  std::vector<std::tuple<int64_t, std::string, std::string, uint32_t>> taken;
+  std::set<int64_t> job_rows;
+  std::vector<ImpPms> pms;
+  int64_t latest = -1;
+  bool stats_row = false;
+  for (const std::string& row : split_row(std::string(text, len), '\n')) {
+    if (row.empty()) continue;
+    const auto p = split_row(row, '|');
+    const std::string& cf = p[0];
+    if (cf == "KEY" && p.size() >= 3) {
+      latest = to_ll(p[2]);
+    } else if (cf == "ELEMENT_INSTANCE_KEY" && p.size() >= 3) {
+      auto f = row_fields(p[2]);
+      ImpElement e;
+      e.key = to_ll(p[1]);
+      e.job = to_ll(f["jobKey"]);
+      e.pik = to_ll(f["processInstanceKey"]);
+      e.fs = to_ll(f["flowScopeKey"]);
+      e.def = to_ll(f["processDefinitionKey"]);
+      e.child_count = to_ll(f["childCount"]);
+      e.asf = to_ll(f["activeSequenceFlows"]);
+      e.state = (uint32_t)to_ll(f["state"]);
+      e.type = (uint32_t)to_ll(f["bpmnElementType"]);
+      e.id = f["elementId"];
+      els[e.key] = e;
+    } else if (cf == "VARIABLES" && p.size() >= 4) {
+      auto f = row_fields(p[3]);
+      vars.push_back({to_ll(p[1]), to_ll(f["key"]), to_ll(f["value"]), p[2], (uint32_t)to_ll(f["type"])});
+    } else if (cf == "NUMBER_OF_TAKEN_SEQUENCE_FLOWS" && p.size() >= 5) {
+      taken.emplace_back(to_ll(p[1]), p[2], p[3], (uint32_t)to_ll(p[4]));
+    } else if (cf == "JOBS" && p.size() >= 3) {
+      job_rows.insert(to_ll(p[1]));
+    } else if (cf == "PROCESS_SUBSCRIPTION_BY_KEY" && p.size() >= 4) {
+      auto f = row_fields(p[3]);
+      ImpPms m;
+      m.eik = to_ll(p[1]);
+      m.name = p[2];
+      m.key = to_ll(f["key"]);
+      m.state = f["state"] == "OPENING" ? 1u : 2u;
+      m.part = (uint32_t)to_ll(f["subscriptionPartitionId"]);
+      m.corr = f["correlationKey"];
+      m.elem_id = f["elementId"];
+      m.intr = (uint32_t)to_ll(f["interrupting"]);
+      pms.push_back(m);
+    } else if (cf == "MESSAGE_SUBSCRIPTION_BY_KEY" || cf == "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY") {
+      return ZBHIP_EUNSUPP;  // message-partition rows: no routing handle to the subscriber's slot
+    } else if (cf == "MESSAGE_STATS") {
+      stats_row = true;
+    }
+    // ELEMENT_INSTANCE_PARENT_CHILD / _CHILD_PARENT, PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY,
+    // EVENT_SCOPE, JOB_STATES, JOB_ACTIVATABLE follow from the rows above
+  }
+  if (!pms.empty() && !h->st.n_slots) return ZBHIP_EUNSUPP;
+  std::vector<int64_t> piks;
+  for (const auto& kv : els)
+    if (kv.second.type == ZBHIP_EL_PROCESS) piks.push_back(kv.first);  // map order: key order
+  const size_t N = h->st.n;
+  if ((size_t)first_slot + piks.size() > N) return ZBHIP_ENOMEM;
+  if (piks.empty() && latest < 0) return ZBHIP_OK;
+
+  // the partition's SoA rows, edited on the host and written back once
+  std::vector<uint4> hdr(N);
+  std::vector<uint2> slots(N * kSlots), vm(N * kVars);
+  std::vector<long long> vv(N * kVars);
+  std::vector<uint32_t> join(N * kJoinWords);
+  std::vector<uint4> pmsrow(h->st.n_slots ? N : 0);
+  std::vector<long long> pikrow(h->st.n_slots ? N : 0);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(hdr.data(), h->st.hdr, N * sizeof(uint4), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(slots.data(), h->st.slots, N * kSlots * sizeof(uint2), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(vm.data(), h->st.var_meta, N * kVars * sizeof(uint2), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(vv.data(), h->st.var_val, N * kVars * sizeof(long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(join.data(), h->st.join, N * kJoinWords * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (h->st.n_slots) {
+    HIPCHK(hipMemcpy(pmsrow.data(), h->st.pms, N * sizeof(uint4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pikrow.data(), h->st.pi_key, N * sizeof(long long), hipMemcpyDeviceToHost));
+  }
+  const int64_t pbits = (int64_t)h->cfg.partition_id << 51;
+  const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
+  if (h->hist.size() < subjects) {
+    h->hist.resize(subjects);
+    h->inst_proc.resize(h->cfg.max_instances, NONE);
+    h->inst_gen.resize(subjects, 0);
+  }
+  struct Done {
+    uint32_t slot;
+    std::vector<int64_t> keys;
+  };
+  std::vector<Done> done;
+  for (size_t k = 0; k < piks.size(); ++k) {
+    const uint32_t inst = first_slot + (uint32_t)k;
+    const ImpElement& pe = els[piks[k]];
+    if ((hdr[inst].x & 0xFFFF) != NONE) return ZBHIP_EINVAL;  // the slot holds an instance
+    int proc = -1;
+    for (size_t q = 0; q < h->procs.size(); ++q)
+      if (h->procs[q].def_key == pe.def) proc = (int)q;
+    if (proc < 0) return ZBHIP_EINVAL;  // not deployed
+    const Proc& P = h->procs[proc];
+    auto elem_of_id = [&](const std::string& id) -> int {
+      for (size_t e = 0; e < P.els.size(); ++e)
+        if (P.els[e].element_type != ZBHIP_EL_SEQUENCE_FLOW && P.id((uint32_t)e) == id) return (int)e;
+      return -1;
+    };
+    // keys of the instance: ordinal 0 the instance, then every other key in key order
+    std::vector<const ImpElement*> children;
+    std::vector<int64_t> keys;
+    for (const auto& kv : els) {
+      const ImpElement& e = kv.second;
+      if (e.pik != pe.key || e.key == pe.key) continue;
+      if (e.fs != pe.key) return ZBHIP_EUNSUPP;  // nested scopes: outside the subset
+      children.push_back(&e);
+      keys.push_back(e.key);
+      if (e.job > 0) keys.push_back(e.job);
+    }
+    std::vector<const ImpVar*> ivars;
+    auto scope_of = [&](int64_t s) { return s == pe.key || std::any_of(children.begin(), children.end(), [&](const ImpElement* c) { return c->key == s; }); };
+    for (const auto& v : vars)
+      if (scope_of(v.scope)) {
+        ivars.push_back(&v);
+        keys.push_back(v.key);
+      }
+    const ImpPms* sub = nullptr;
+    for (const auto& m : pms)
+      if (std::any_of(children.begin(), children.end(), [&](const ImpElement* c) { return c->key == m.eik; })) {
+        if (sub) return ZBHIP_EUNSUPP;  // one open subscription per instance
+        sub = &m;
+        keys.push_back(m.key);
+      }
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    keys.erase(std::remove(keys.begin(), keys.end(), pe.key), keys.end());
+    keys.insert(keys.begin(), pe.key);
+    if (keys.size() >= 0xFFF0) return ZBHIP_ENOMEM;
+    auto ord = [&](int64_t key) -> uint32_t {
+      return (uint32_t)(std::lower_bound(keys.begin() + 1, keys.end(), key) - keys.begin());
+    };
+    if (children.size() > (size_t)kSlots || ivars.size() > (size_t)kVars) return ZBHIP_ENOMEM;
+    for (size_t c = 0; c < children.size(); ++c) {
+      const ImpElement& e = *children[c];
+      const int el = elem_of_id(e.id);
+      if (el < 0 || P.els[el].element_type != e.type) return ZBHIP_EINVAL;
+      const uint32_t job = e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
+      const uint32_t row = e.job > 0 && job_rows.count(e.job) ? 1u : 0u;
+      slots[c * N + inst] = make_uint2((uint32_t)el | (ord(e.key) << 16), job | (e.state << 16) | (row << 24));
+    }
+    for (size_t v = 0; v < ivars.size(); ++v) {
+      const ImpVar& x = *ivars[v];
+      const int name = zbhip_intern(h, x.name.c_str());
+      if (name < 0) return name;
+      const uint32_t scope = x.scope == pe.key ? 0u : ord(x.scope);
+      vm[v * N + inst] = make_uint2((uint32_t)name | (scope << 16), ord(x.key) | (x.type << 16));
+      vv[v * N + inst] = x.value;
+    }
+    for (int w = 0; w < kJoinWords; ++w) join[(size_t)w * N + inst] = 0;
+    for (const auto& t : taken) {
+      if (std::get<0>(t) != pe.key) continue;
+      int slot = -1;
+      for (size_t f = 0; f < P.els.size(); ++f) {
+        const zbhip_element& F = P.els[f];
+        if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && P.id((uint32_t)f) == std::get<2>(t) && F.flow_target < P.els.size() &&
+            P.id(F.flow_target) == std::get<1>(t))
+          slot = F.join_slot == ZBHIP_NONE16 ? -1 : F.join_slot;
+      }
+      if (slot < 0 || std::get<3>(t) > 255) return ZBHIP_EUNSUPP;
+      join[(size_t)(slot >> 2) * N + inst] |= std::get<3>(t) << ((slot & 3) * 8);
+    }
+    if (h->st.n_slots) {
+      pmsrow[inst] = make_uint4(0, 0, 0, 0);
+      pikrow[inst] = pe.key;
+      if (sub) {
+        const int el = elem_of_id(sub->elem_id);
+        if (el < 0) return ZBHIP_EINVAL;
+        const int64_t corr = zbhip_intern_string(h, sub->corr.data(), sub->corr.size());
+        if (corr < 0) return (int)corr;
+        pmsrow[inst] = make_uint4((uint32_t)el | (sub->state << 12) | (sub->intr << 14) | (sub->part << 16),
+                                  ord(sub->eik) | (ord(sub->key) << 16), (uint32_t)corr, 0);
+      }
+    } else if (sub) {
+      return ZBHIP_EUNSUPP;
+    }
+    hdr[inst] = make_uint4((uint32_t)proc | ((uint32_t)keys.size() << 16),
+                           pe.state | ((uint32_t)children.size() << 8) | ((uint32_t)ivars.size() << 16) | (1u << 24),
+                           (uint32_t)pe.child_count | ((uint32_t)pe.asf << 16), 0);
+    done.push_back({inst, std::move(keys)});
+  }
+  HIPCHK(hipMemcpy(h->st.hdr, hdr.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->st.slots, slots.data(), N * kSlots * sizeof(uint2), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->st.var_meta, vm.data(), N * kVars * sizeof(uint2), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->st.var_val, vv.data(), N * kVars * sizeof(long long), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->st.join, join.data(), N * kJoinWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (h->st.n_slots) {
+    HIPCHK(hipMemcpy(h->st.pms, pmsrow.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->st.pi_key, pikrow.data(), N * sizeof(long long), hipMemcpyHostToDevice));
+  }
+  // key histories and the resolve_key table: one entry per imported key
+  for (const Done& d : done) {
+    auto& hs = h->hist[d.slot];
+    hs.clear();
+    ++h->inst_gen[d.slot];
+    h->inst_proc[d.slot] = (uint16_t)(hdr[d.slot].x & 0xFFFF);
+    for (size_t o = 0; o < d.keys.size(); ++o) {
+      hs.push_back({(uint16_t)o, d.keys[o] - pbits});
+      h->batches.push_back({d.keys[o] - pbits, d.slot, (uint16_t)o, 1, h->inst_gen[d.slot]});
+    }
+  }
+  std::sort(h->batches.begin(), h->batches.end(), [](const BatchRef& a, const BatchRef& b) { return a.base < b.base; });
+  if (latest >= 0 && latest - pbits > h->key_counter) h->key_counter = latest - pbits;
+  if (h->st.n_slots) {
+    const unsigned long long kc = (unsigned long long)h->key_counter;
+    HIPCHK(hipMemcpy(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice));
+  }
+  h->published |= stats_row;
+  if (n_instances) *n_instances = (uint32_t)done.size();
+  return ZBHIP_OK;
+}
+
+extern "C" int zbhip_import_state_db(zbhip_handle* h, const uint8_t* entries, size_t len, uint32_t first_slot,
+                                     uint32_t* n_instances) {
+  if (!h || (len && !entries)) return ZBHIP_EINVAL;
+  std::string rows;
+  std::vector<char> row(4096);
+  size_t off = 0;
+  while (off < len) {
+    if (len - off < 12) return ZBHIP_EINVAL;
+    uint32_t hd[3];
+    memcpy(hd, entries + off, 12);
+    off += 12;
+    if (len - off < (size_t)hd[1] + hd[2]) return ZBHIP_EINVAL;
+    const int n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
+                                                      string_interner, h, row.data(), row.size());
+    if (n < 0) return n;
+    if (n > 0) {
+      rows.append(row.data(), (size_t)n);
+      rows.push_back('\n');
+    }
+    off += (size_t)hd[1] + hd[2];
+  }
+  return zbhip_import_state(h, rows.data(), rows.size(), first_slot, n_instances);
+}

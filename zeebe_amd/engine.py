@@ -247,6 +247,21 @@ class Partition:
         ids = np.ascontiguousarray(instances, dtype=np.uint32)
         check(self.L.zbhip_evict_instances(self.h, ids.ctypes.data, len(ids)), "zbhip_evict_instances")
 
+    def import_state_db(self, entries, first_slot=0):
+        """Loads process instances from zb-db entries [(column family, key, value)] into free slots
+        first_slot, ... (process-instance-key order); returns the number of instances."""
+        import struct
+        blob = b"".join(struct.pack("<III", cf, len(k), len(v)) + bytes(k) + bytes(v) for cf, k, v in entries)
+        n = C.c_uint32()
+        check(self.L.zbhip_import_state_db(self.h, blob, len(blob), first_slot, C.byref(n)), "zbhip_import_state_db")
+        return n.value
+
+    def import_state(self, rows, first_slot=0):
+        text = "\n".join(rows).encode()
+        n = C.c_uint32()
+        check(self.L.zbhip_import_state(self.h, text, len(text), first_slot, C.byref(n)), "zbhip_import_state")
+        return n.value
+
     def key_before(self, i):
         k = C.c_int64()
         check(self.L.zbhip_key_before(self.h, i, C.byref(k)), "zbhip_key_before")

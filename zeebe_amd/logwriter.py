@@ -75,6 +75,22 @@ class LogSerializer:
             check(self.L.zbhip_serializer_encode_state_row(self.s, r.encode(), cb, None), "encode_state_row")
         return sorted(out)
 
+    def decode_state_entries(self, entries, intern=None):
+        """zb-db entries -> canonical state rows (the inverse of encode_state_rows); intern(bytes) -> id
+        maps string variable values to value-dictionary ids."""
+        import ctypes as C
+
+        from .native import INTERNER
+        cb = INTERNER((lambda ctx, b, n: intern(C.string_at(b, n))) if intern else (lambda ctx, b, n: -5))
+        buf = C.create_string_buffer(8192)
+        rows = []
+        for cf, k, v in entries:
+            n = check(self.L.zbhip_serializer_decode_state_entry(self.s, cf, k, len(k), v, len(v), cb, None, buf, 8192),
+                      "decode_state_entry")
+            if n:
+                rows.append(buf.value.decode())
+        return sorted(rows)
+
     def set_broker_version(self, major, minor, patch):
         check(self.L.zbhip_serializer_set_broker_version(self.s, major, minor, patch))
 

@@ -28,7 +28,8 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_serializer_rejection_reason", "zbhip_handle_serializer", "zbhip_serialize_log",
            "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream",
            "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
-           "zbhip_set_external_keys"]
+           "zbhip_set_external_keys", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
+           "zbhip_import_state"]
 
 
 class ZbhipError(RuntimeError):
@@ -40,6 +41,7 @@ class ZbhipError(RuntimeError):
 STATE_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p)
 DB_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_uint8),
                       C.c_size_t)
+INTERNER = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.c_void_p, C.c_size_t)
 
 _lib = None
 
@@ -94,6 +96,10 @@ def load():
     L.zbhip_evict_instances.argtypes = [vp, vp, sz]
     L.zbhip_key_before.argtypes = [vp, sz, C.POINTER(i64)]
     L.zbhip_set_external_keys.argtypes = [vp, sz, u32]
+    L.zbhip_serializer_decode_state_entry.argtypes = [vp, u32, C.c_char_p, sz, C.c_char_p, sz, INTERNER, vp,
+                                                      C.c_char_p, sz]
+    L.zbhip_import_state_db.argtypes = [vp, C.c_char_p, sz, u32, C.POINTER(u32)]
+    L.zbhip_import_state.argtypes = [vp, C.c_char_p, sz, u32, C.POINTER(u32)]
     L.zbhip_stream.argtypes = [vp]
     L.zbhip_stream.restype = vp
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
