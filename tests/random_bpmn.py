@@ -61,7 +61,7 @@ class _Gen:
         choices = ["task", "task"]
         if depth < self.max_depth:
             choices += ["xor", "xor"]
-            if width * 2 <= 8 and self.join_slots + 3 <= 16:
+            if width * 2 <= 8 and self.join_slots + 4 <= 16:
                 choices.append("par")
         if self.messages and self.catches < 1 and width == 1:
             choices.append("catch")
@@ -102,8 +102,8 @@ class _Gen:
         fork = self.node("parallelGateway")
         self.flow(cur, fork)
         join = self.node("parallelGateway")
-        k = int(r.integers(2, 4)) if width * 3 <= 8 and self.join_slots + 3 <= 16 else 2
-        self.join_slots += k
+        k = int(r.integers(2, 4)) if width * 3 <= 8 and self.join_slots + 4 <= 16 else 2
+        self.join_slots += k + 1  # the flows into the join and the one into the fork
         for _ in range(k):
             end = self.sequence(fork, depth + 1, width * k)
             self.flow(end, join)
