@@ -505,6 +505,57 @@ int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx);
 /* One canonical row of zbhip_export_state -> its entry; 1 = emitted, 0 = column family not encoded. */
 int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char* row, zbhip_db_sink sink, void* ctx);
 
+/* ---- job activation ----------------------------------------------------------
+ * JOB_BATCH:ACTIVATE (JobBatchActivateProcessor.java:60-143, JobBatchCollector.java:67-123,
+ * JobBatchActivatedApplier.java:27-37, DbJobState.activate :118-133): the activatable jobs of a type
+ * in JOB_ACTIVATABLE order (job key) up to maxJobsToActivate, each with deadline = the command's
+ * timestamp + timeout, the worker, and the variables visible from its element instance
+ * (JobVariablesCollector / DbVariableState.getVariablesAsDocument: the element's scope, then the
+ * process instance's, names in DbString order -- length, then bytes -- each name once, filtered by
+ * the requested names if any); the jobs become ACTIVATED (JOB_STATES, JOB_DEADLINES, out of
+ * JOB_ACTIVATABLE).  The batch key is the partition's next key.  A command is processed between
+ * windows, in log order.  The size-based truncation of the reference (4 MB records) is not modelled:
+ * at most `cap` jobs are returned. */
+typedef struct zbhip_job_activation {
+  const char* type;            /* job type (UTF-8) */
+  size_t type_len;
+  const char* worker;
+  size_t worker_len;
+  int64_t timeout;             /* ms */
+  int32_t max_jobs;            /* maxJobsToActivate */
+  int32_t pad;
+  int64_t timestamp;           /* the command's timestamp (ms) */
+  const uint32_t* variables;   /* requested variable name ids (zbhip_intern); none = every variable */
+  size_t n_variables;
+} zbhip_job_activation;
+
+typedef struct zbhip_activated_job {
+  int64_t key;                   /* job key */
+  int64_t element_instance_key;
+  int64_t process_instance_key;
+  int64_t deadline;
+  uint32_t instance;             /* instance slot */
+  int32_t process_idx;
+  int32_t element_idx;
+  uint16_t retries;
+  uint16_t n_variables;
+  zbhip_doc_entry variables[4];  /* the job's variables document, in document order */
+} zbhip_activated_job;
+
+typedef struct zbhip_job_batch {
+  int64_t key;                   /* JOB_BATCH:ACTIVATED key; -1 when rejected */
+  uint32_t n_jobs;
+  uint8_t rejection_type;        /* ZBHIP_REJ_INVALID_ARGUMENT or ZBHIP_REJ_NONE */
+  uint8_t reason;                /* 1 max jobs, 2 timeout, 3 type (JobBatchActivateProcessor.rejectCommand) */
+  uint8_t truncated;
+  uint8_t pad;
+} zbhip_job_batch;
+
+int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* cmd, zbhip_activated_job* jobs, size_t cap,
+                        zbhip_job_batch* result);
+/* The rejection reason of a refused JOB_BATCH:ACTIVATE, exactly as JobBatchActivateProcessor writes it. */
+int zbhip_job_batch_rejection_reason(const zbhip_job_activation* cmd, const zbhip_job_batch* result, char* buf, size_t cap);
+
 /* ---- fallback hand-off (Engine.java:134 onProcessingError, ProcessingStateMachine.java:276-310) --
  * A command the device did not process (zbhip_command_status != 0) goes to the CPU engine, in log
  * order.  Every later command of the same subject in the window falls back too (FB_FENCED), so the

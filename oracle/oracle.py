@@ -53,6 +53,9 @@ def lib():
         L.zbo_element_id.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.zbo_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
         L.zbo_run.argtypes = [C.c_void_p]
+        L.zbo_activate_jobs.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int64, C.c_int, C.c_int64, C.c_char_p,
+                                        C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                        C.POINTER(C.c_int64)]
         L.zbo_key_counter.restype = C.c_int64
         L.zbo_key_counter.argtypes = [C.c_void_p]
         L.zbo_set_key_counter.argtypes = [C.c_void_p, C.c_int64]
@@ -170,6 +173,17 @@ class Oracle:
         if clear:
             self.L.zbo_clear_outbox(self.h)
         return out
+
+    def activate_jobs(self, job_type, worker="worker", timeout=300000, max_jobs=10, timestamp=0, variables=()):
+        """JOB_BATCH:ACTIVATE on the oracle: (batch key, activated jobs, rejection reason)."""
+        import numpy as np
+        from zeebe_amd import abi
+        out = np.zeros(max(max_jobs, 1) + 1, dtype=abi.ACTIVATED_JOB_DTYPE)
+        n, key = C.c_size_t(), C.c_int64()
+        blob = b"".join(v.encode() + b"\0" for v in variables)
+        reason = self.L.zbo_activate_jobs(self.h, job_type.encode(), worker.encode(), timeout, max_jobs, timestamp, blob,
+                                          len(variables), out.ctypes.data, len(out), C.byref(n), C.byref(key))
+        return key.value, out[: n.value], reason
 
     def key_counter(self):
         """DbKeyGenerator's current value (the counter, without the partition bits)."""

@@ -25,6 +25,7 @@ bytes, value bytes) as RocksDB holds them:
       JOBS key -> JobRecordValue{jobRecord} stored without variables (DbJobState.java:77-81);
       JOB_STATES key -> JobStateValue{jobState: ACTIVATABLE} (:84-85);
       JOB_ACTIVATABLE [[type, jobKey], tenant] -> DbNil (:87-95, PlacementType.SUFFIX);
+      JOB_DEADLINES [deadline, jobKey] -> DbNil (:100-102; activated jobs);
       KEY "latestKey" -> NextValue{nextValue} (stream-platform/.../state/NextValueManager.java:32-34,
                             DbKeyGenerator.java:21).
       MESSAGE_SUBSCRIPTION_BY_KEY [eik, name] -> MessageSubscription{record, key, correlating};
@@ -42,7 +43,8 @@ from oracle import logserial as LS
 CF = {"KEY": 1, "ELEMENT_INSTANCE_PARENT_CHILD": 6, "ELEMENT_INSTANCE_KEY": 7, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS": 8,
       "ELEMENT_INSTANCE_CHILD_PARENT": 9, "VARIABLES": 10, "JOBS": 16, "JOB_STATES": 17, "EVENT_SCOPE": 37,
       "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY": 55, "JOB_ACTIVATABLE": 76, "MESSAGE_SUBSCRIPTION_BY_KEY": 27,
-      "MESSAGE_STATS": 54, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY": 74, "PROCESS_SUBSCRIPTION_BY_KEY": 75}
+      "MESSAGE_STATS": 54, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY": 74, "PROCESS_SUBSCRIPTION_BY_KEY": 75,
+      "JOB_DEADLINES": 18}
 NIL = b"\xff"
 PI_INTENT = {1: "SEQUENCE_FLOW_TAKEN", 2: "ELEMENT_ACTIVATING", 3: "ELEMENT_ACTIVATED", 4: "ELEMENT_COMPLETING",
              5: "ELEMENT_COMPLETED", 6: "ELEMENT_TERMINATING", 7: "ELEMENT_TERMINATED"}
@@ -131,6 +133,7 @@ def encode_rows(rows, processes, string_value):
         elif name == "JOBS":
             key, f = int(parts[1]), fields(parts[2])
             job = LS.write_object(LS.JOB, dict(
+                deadline=int(f.get("deadline", -1)), worker=f.get("worker", ""),
                 retries=int(f["retries"]), type=f["type"], bpmnProcessId=f["bpmnProcessId"],
                 processDefinitionVersion=int(f["processDefinitionVersion"]),
                 processDefinitionKey=int(f["processDefinitionKey"]), processInstanceKey=int(f["processInstanceKey"]),
@@ -163,6 +166,8 @@ def encode_rows(rows, processes, string_value):
             out.append((CF[name], prefix + dblong(int(parts[1])) + dbstr("<default>") + dbstr(parts[2]), val))
         elif name == "MESSAGE_STATS":  # DbMessageState.java:165-175
             out.append((CF[name], prefix + dbstr("deadline_message_count"), dblong(int(parts[2]))))
+        elif name == "JOB_DEADLINES":  # DbJobState.java:100-102: [deadline, jobKey] -> DbNil
+            out.append((CF[name], prefix + dblong(int(parts[1])) + dblong(int(parts[2])), NIL))
         elif name == "JOB_ACTIVATABLE":
             out.append((CF[name], prefix + dbstr(parts[1]) + dblong(int(parts[3])) + dbstr(parts[2]), NIL))
     return sorted(out)

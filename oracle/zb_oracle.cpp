@@ -519,6 +519,9 @@ struct JobRow {  // JobRecord without variables (DbJobState.createJobRecord)
   int64_t elementInstanceKey = -1;
   std::string type;
   int retries = 3;
+  bool activated = false;  // JOB_STATES ACTIVATED (DbJobState.activate :118-133)
+  int64_t deadline = -1;
+  std::string worker;
 };
 
 struct EventTrigger {  // state/instance/EventTrigger.java
@@ -830,6 +833,71 @@ class Oracle {
   }
 
   std::string dump_state() const;
+  // JOB_BATCH:ACTIVATE (processing/job/JobBatchActivateProcessor.java:60-143, JobBatchCollector.java
+  // :67-123): jobs of `type` in JOB_ACTIVATABLE order ([[type, jobKey], tenant]), deadline, worker,
+  // variables (JobVariablesCollector -> DbVariableState.getVariablesAsDocument :193-247: the element
+  // scope, then its flow scope; names in DbString key order (length, bytes), each once), then
+  // JobBatchActivatedApplier -> DbJobState.activate.  Returns the rejection reason (0 accepted).
+  struct Activated {
+    int64_t key, eik, pik, deadline;
+    int proc, elem, retries;
+    std::vector<std::pair<int, VarRow>> vars;  // (name id, row)
+  };
+  int activate_jobs(const std::string& type, const std::string& worker, int64_t timeout, int max_jobs,
+                    int64_t timestamp, const std::vector<std::string>& requested, std::vector<Activated>& out,
+                    int64_t& batch_key) {
+    out.clear();
+    batch_key = -1;
+    if (max_jobs < 1) return 1;
+    if (timeout < 1) return 2;
+    if (type.empty()) return 3;
+    batch_key = ((int64_t)partition_ << 51) + ++key_counter_;  // keyGenerator.nextKey, no instance's
+    std::vector<int64_t> keys;
+    for (auto it = activatable_.lower_bound({type, "<default>", INT64_MIN});
+         it != activatable_.end() && std::get<0>(*it) == type && std::get<1>(*it) == "<default>" &&
+         (int)keys.size() < max_jobs;
+         ++it)
+      keys.push_back(std::get<2>(*it));
+    auto name_less = [this](int a, int b) {  // DbString: 4-byte big-endian length, then the bytes
+      const std::string& x = names[a];
+      const std::string& y = names[b];
+      return x.size() != y.size() ? x.size() < y.size() : x < y;
+    };
+    for (int64_t k : keys) {
+      JobRow& j = jobs_.at(k);
+      Activated a;
+      a.key = k;
+      a.eik = j.elementInstanceKey;
+      a.pik = j.pi.piKey;
+      a.deadline = timestamp + timeout;
+      a.proc = j.pi.proc;
+      a.elem = j.pi.elem;
+      a.retries = j.retries;
+      std::vector<int64_t> scopes{j.elementInstanceKey};
+      auto eit = ei_.find(j.elementInstanceKey);
+      if (eit != ei_.end() && eit->second.value.flowScopeKey >= 0) scopes.push_back(eit->second.value.flowScopeKey);
+      std::set<int> seen;
+      for (int64_t scope : scopes) {
+        std::vector<int> local;
+        for (auto& [sk, row] : vars_)
+          if (sk.first == scope) local.push_back(sk.second);
+        std::sort(local.begin(), local.end(), name_less);
+        for (int nid : local) {
+          if (seen.count(nid)) continue;
+          if (!requested.empty() && std::find(requested.begin(), requested.end(), names[nid]) == requested.end()) continue;
+          seen.insert(nid);
+          a.vars.push_back({nid, vars_.at({scope, nid})});
+        }
+      }
+      j.activated = true;
+      j.deadline = a.deadline;
+      j.worker = worker;
+      activatable_.erase({j.type, "<default>", k});
+      out.push_back(std::move(a));
+    }
+    return 0;
+  }
+
   // DbKeyGenerator's current value (the CPU engine of a fallback hand-off is set to the device's)
   int64_t key_counter() const { return key_counter_; }
   void set_key_counter(int64_t v) { key_counter_ = v; }
@@ -1861,12 +1929,18 @@ std::string Oracle::dump_state() const {
     const OProc& p = procs[j.pi.proc];
     snprintf(buf, sizeof buf,
              "JOBS|%lld|type=%s,retries=%d,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
-             "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>",
+             "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
+             "deadline=%lld,worker=%s",
              (long long)k, j.type.c_str(), j.retries, p.els[j.pi.elem].id.c_str(), (long long)j.elementInstanceKey,
-             (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version);
+             (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version, (long long)j.deadline,
+             j.worker.c_str());
     rows.push_back(buf);
-    snprintf(buf, sizeof buf, "JOB_STATES|%lld|ACTIVATABLE", (long long)k);
+    snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", (long long)k, j.activated ? "ACTIVATED" : "ACTIVATABLE");
     rows.push_back(buf);
+    if (j.activated) {  // JOB_DEADLINES [deadline, jobKey] -> DbNil
+      snprintf(buf, sizeof buf, "JOB_DEADLINES|%lld|%lld", (long long)j.deadline, (long long)k);
+      rows.push_back(buf);
+    }
   }
   for (auto& [t, ten, k] : activatable_) {
     snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|%s|%lld", t.c_str(), ten.c_str(), (long long)k);
@@ -1982,6 +2056,38 @@ int zbo_subscription_partition(const char* b, size_t len, int partition_count) {
 int32_t zbo_java_hash(const char* b, size_t len) { return java_hash(std::string(b, len)); }
 int zbo_run(void* o) { return static_cast<Oracle*>(o)->run(); }
 int64_t zbo_key_counter(void* o) { return static_cast<Oracle*>(o)->key_counter(); }
+// names: requested variable names, NUL-separated (n of them)
+int zbo_activate_jobs(void* o, const char* type, const char* worker, int64_t timeout, int max_jobs, int64_t timestamp,
+                      const char* names, size_t n_names, zbhip_activated_job* out, size_t cap, size_t* n_out,
+                      int64_t* batch_key) {
+  auto* O = static_cast<Oracle*>(o);
+  std::vector<std::string> req;
+  for (size_t i = 0; i < n_names; ++i) {
+    req.emplace_back(names);
+    names += req.back().size() + 1;
+  }
+  std::vector<Oracle::Activated> got;
+  const int reason = O->activate_jobs(type, worker, timeout, max_jobs, timestamp, req, got, *batch_key);
+  *n_out = got.size();
+  for (size_t i = 0; i < got.size() && i < cap; ++i) {
+    zbhip_activated_job& j = out[i];
+    memset(&j, 0, sizeof j);
+    j.key = got[i].key;
+    j.element_instance_key = got[i].eik;
+    j.process_instance_key = got[i].pik;
+    j.deadline = got[i].deadline;
+    j.process_idx = got[i].proc;
+    j.element_idx = got[i].elem;
+    j.retries = (uint16_t)got[i].retries;
+    j.n_variables = (uint16_t)got[i].vars.size();
+    for (size_t v = 0; v < got[i].vars.size() && v < 4; ++v) {
+      j.variables[v].name_id = (uint32_t)got[i].vars[v].first;
+      j.variables[v].type = got[i].vars[v].second.type;
+      j.variables[v].value = got[i].vars[v].second.value;
+    }
+  }
+  return reason;
+}
 void zbo_set_key_counter(void* o, int64_t v) { static_cast<Oracle*>(o)->set_key_counter(v); }
 
 size_t zbo_n_records(void* o) { return static_cast<Oracle*>(o)->out.size(); }

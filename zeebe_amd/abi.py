@@ -114,6 +114,17 @@ class LogWindow(C.Structure):  # zbhip_log_window
 OPEN_TRUSTED_DEVICE_WINDOWS = 1
 
 
+class JobActivation(C.Structure):  # zbhip_job_activation (JOB_BATCH:ACTIVATE)
+    _fields_ = [("type", C.c_char_p), ("type_len", C.c_size_t), ("worker", C.c_char_p), ("worker_len", C.c_size_t),
+                ("timeout", C.c_int64), ("max_jobs", C.c_int32), ("pad", C.c_int32), ("timestamp", C.c_int64),
+                ("variables", C.c_void_p), ("n_variables", C.c_size_t)]
+
+
+class JobBatch(C.Structure):  # zbhip_job_batch
+    _fields_ = [("key", C.c_int64), ("n_jobs", C.c_uint32), ("rejection_type", C.c_uint8), ("reason", C.c_uint8),
+                ("truncated", C.c_uint8), ("pad", C.c_uint8)]
+
+
 class Config(C.Structure):
     _fields_ = [("partition_id", C.c_int32), ("partition_count", C.c_int32), ("device", C.c_int32),
                 ("max_commands_in_batch", C.c_int32), ("max_instances", C.c_uint32),
@@ -132,6 +143,11 @@ class Stats(C.Structure):
 COMMAND_DTYPE = np.dtype([("instance", "<u4"), ("kind", "u1"), ("doc_count", "u1"), ("ref", "<u2"),
                           ("doc_begin", "<u4"), ("pad", "<u4")])
 DOC_DTYPE = np.dtype([("name_id", "<u4"), ("type", "u1"), ("pad", "u1", (3,)), ("value", "<i8")])
+# zbhip_activated_job
+ACTIVATED_JOB_DTYPE = np.dtype([("key", "<i8"), ("element_instance_key", "<i8"), ("process_instance_key", "<i8"),
+                                ("deadline", "<i8"), ("instance", "<u4"), ("process_idx", "<i4"),
+                                ("element_idx", "<i4"), ("retries", "<u2"), ("n_variables", "<u2"),
+                                ("variables", DOC_DTYPE, (4,))])
 RECORD_DTYPE = np.dtype([("key", "<i8"), ("scope_key", "<i8"), ("process_instance_key", "<i8"),
                          ("source_index", "<i8"), ("process_idx", "<i4"), ("element_idx", "<i4"),
                          ("record_type", "u1"), ("value_type", "u1"), ("intent", "u1"),

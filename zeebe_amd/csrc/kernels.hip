@@ -1630,7 +1630,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
       emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
       // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
-      e.y &= ~(1u << 24);
+      e.y &= ~(3u << 24);  // the job row (and its ACTIVATED state) is deleted
       if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
       tput(L, t, e);
       if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) {  // afterAccept
@@ -2286,6 +2286,46 @@ __global__ __launch_bounds__(256) void k_subject_check(const uint4* cmds, uint32
   }
   if (f) atomicOr(flag, f);  // rare: a faulty window
 }
+
+// JOB_BATCH:ACTIVATE on the device (JobBatchActivatedApplier -> DbJobState.activate): the jobs the
+// host picked from its JOB_ACTIVATABLE index are marked ACTIVATED in their element-instance slot
+// (flags bit 1), and each job's element-instance slot word, process, and the instance's variables
+// (JobVariablesCollector's input) are gathered for the JOB_BATCH:ACTIVATED record.
+struct ActivatedOut {
+  uint4 a;             // x = slot word (elem | key ord << 16), y = hdr.x, z = hdr.y, w = 1 found
+  uint2 meta[kVars];
+  long long val[kVars];
+};
+__global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2* jobs, uint32_t n, ActivatedOut* out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t inst = jobs[i].x, ord = jobs[i].y;
+  ActivatedOut o = {};
+  if (inst < st.n) {
+    const uint4 h = st.hdr[inst];
+    const uint32_t nslots = (h.y >> 8) & 0xFF, nvars = (h.y >> 16) & 0xFF;
+    for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s) {
+      uint2 e = st.slots[(size_t)s * st.n + inst];
+      if ((e.y & 0xFFFF) == ord && ((e.y >> 24) & 3u) == 1u) {
+        e.y |= 2u << 24;
+        st.slots[(size_t)s * st.n + inst] = e;
+        o.a = make_uint4(e.x, h.x, h.y, 1u);
+      }
+    }
+    for (uint32_t v = 0; v < nvars && v < (uint32_t)kVars; ++v) {
+      o.meta[v] = st.var_meta[(size_t)v * st.n + inst];
+      o.val[v] = st.var_val[(size_t)v * st.n + inst];
+    }
+  }
+  out[i] = o;
+}
+
+hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_activate_jobs, dim3((n + 255) / 256), dim3(256), 0, s, st, jobs, n,
+                            static_cast<ActivatedOut*>(out));
+  return hipGetLastError();
+}
+size_t activated_out_bytes() { return sizeof(ActivatedOut); }
 
 // ---------------------------------------------------------------------------------------------
 // launch wrappers (host)

@@ -684,8 +684,8 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     mp_map(v, 1);  // JobRecordValue.java:21 -> JobRecord stored without variables (DbJobState.create)
     key(v, "jobRecord");
     mp_map(v, 17);
-    key(v, "deadline"); mp_int(v, -1);
-    key(v, "worker"); key(v, "");
+    key(v, "deadline"); mp_int(v, f.count("deadline") ? ll(f["deadline"]) : -1);
+    key(v, "worker"); mp_str(v, f["worker"]);
     key(v, "retries"); mp_int(v, ll(f["retries"]));
     key(v, "retryBackoff"); mp_int(v, 0);
     key(v, "recurringTime"); mp_int(v, -1);
@@ -706,6 +706,10 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     cf_prefix(k, ord); dbl(k, ll(p[1]));
     mp_map(v, 1);  // JobStateValue.java:21
     key(v, "jobState"); mp_str(v, p[2]);
+  } else if (cf == "JOB_DEADLINES" && need(3)) {
+    ord = 18;  // DbJobState.java:100-102: [deadline, jobKey] -> DbNil
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbl(k, ll(p[2]));
+    v.push_back((char)0xff);
   } else if (cf == "JOB_ACTIVATABLE" && need(4)) {
     ord = 76;  // DbTenantAwareKey(tenant, [type, jobKey], SUFFIX)
     cf_prefix(k, ord); dbs(k, p[1]); dbl(k, ll(p[3])); dbs(k, p[2]);
@@ -1032,11 +1036,13 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
       if (!j) return ZBHIP_EINVAL;
       snprintf(b, sizeof b,
                "JOBS|%lld|type=%s,retries=%lld,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
-               "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%lld,tenantId=%s",
+               "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%lld,tenantId=%s,deadline=%lld,"
+               "worker=%s",
                (long long)k, ms(j->get("type")).c_str(), (long long)mi(j->get("retries")), ms(j->get("elementId")).c_str(),
                (long long)mi(j->get("elementInstanceKey")), (long long)mi(j->get("processInstanceKey")),
                ms(j->get("bpmnProcessId")).c_str(), (long long)mi(j->get("processDefinitionKey")),
-               (long long)mi(j->get("processDefinitionVersion")), ms(j->get("tenantId")).c_str());
+               (long long)mi(j->get("processDefinitionVersion")), ms(j->get("tenantId")).c_str(),
+               (long long)mi(j->get("deadline")), ms(j->get("worker")).c_str());
       out = b;
       break;
     }
@@ -1044,6 +1050,13 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
       const int64_t k = K.dblong();
       if (!K.ok || !value()) return ZBHIP_EINVAL;
       snprintf(b, sizeof b, "JOB_STATES|%lld|%s", (long long)k, ms(v.get("jobState")).c_str());
+      out = b;
+      break;
+    }
+    case 18: {  // JOB_DEADLINES [deadline, jobKey] -> DbNil
+      const int64_t d = K.dblong(), k = K.dblong();
+      if (!K.ok) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "JOB_DEADLINES|%lld|%lld", (long long)d, (long long)k);
       out = b;
       break;
     }

@@ -38,6 +38,8 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
                           unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
                           zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s);
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s);
+hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, hipStream_t s);
+size_t activated_out_bytes();
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
                                 uint32_t stamp, uint32_t* flag, hipStream_t s);
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
@@ -64,6 +66,7 @@ struct Proc {
   uint16_t bpmn_id = 0;
   uint16_t bpmn_name = NONE;  // name id of the bpmnProcessId (processes with message catch events)
   bool has_msg = false;
+  std::vector<uint32_t> job_type_id;  // per element: id of its job type (service tasks), else ~0
   const std::string& id(uint32_t e) const { return strings[els[e].id]; }
 };
 
@@ -229,6 +232,27 @@ struct zbhip_handle {
   std::vector<std::vector<std::pair<uint16_t, int64_t>>> hist;
   std::vector<uint16_t> inst_proc;
   std::vector<BatchRef> batches;
+
+  // ---- job activation (zbhip_activate_jobs) ----
+  // JOB_ACTIVATABLE of the GPU-resident jobs, [type, job key] -> (instance, job key ordinal): built
+  // from the device rows at the first activation, then kept by the key bookkeeping (advance)
+  bool job_index_on = false;
+  std::map<std::pair<uint32_t, int64_t>, std::pair<uint32_t, uint16_t>> job_index;
+  std::unordered_map<std::string, uint32_t> job_type_ids;
+  struct Activation {
+    int64_t deadline;
+    std::string worker;
+    uint32_t inst;
+  };
+  std::unordered_map<int64_t, Activation> activated;  // ACTIVATED jobs: deadline, worker
+  std::vector<int64_t> completed_activated;           // completed in the last window (dropped next)
+  uint32_t job_type(const std::string& t) {
+    auto it = job_type_ids.find(t);
+    if (it != job_type_ids.end()) return it->second;
+    const uint32_t id = (uint32_t)job_type_ids.size();
+    job_type_ids.emplace(t, id);
+    return id;
+  }
 
   // ---- message correlation (variant 2) ----
   std::vector<std::string> strs;               // value dictionary
@@ -666,6 +690,10 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     const int f = atoi(fv);
     if (rank(f) >= rank(h->variant)) h->variant = f;
   }
+  P.job_type_id.assign(P.els.size(), ~0u);
+  for (size_t e = 0; e < P.els.size(); ++e)
+    if (P.els[e].element_type == ZBHIP_EL_SERVICE_TASK && P.els[e].job_type < P.strings.size())
+      P.job_type_id[e] = h->job_type(P.strings[P.els[e].job_type]);
   h->procs.push_back(std::move(P));
   {
     const uint64_t limit = (uint64_t)h->cfg.max_commands_in_batch;
@@ -920,6 +948,33 @@ static hipEvent_t next_event(zbhip_handle* h) {
   return h->tev[h->tev_used++];
 }
 
+// JOB_ACTIVATABLE bookkeeping of one processed command from its records: JOB:CREATED adds a job,
+// JOB:COMPLETED removes it (its ACTIVATED entry is dropped at the next window)
+static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
+  const uint32_t nrec = h->h_hdr[c].x & 0xFFFF;
+  const uint2* rows = h->h_out.data() + h->h_off[c];
+  const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
+  if (proc == NONE || proc >= h->procs.size()) return;
+  const Proc& P = h->procs[proc];
+  for (uint32_t i = 0; i < nrec; ++i) {
+    const uint2 w = rows[i];
+    const uint32_t elem = w.y & 0xFFFF, code = (w.y >> 16) & 0x3F;
+    if (h->msg() && elem != NONE && (elem & kPayloadBit)) {  // message record + payload rows
+      i += kPayloadRows;
+      continue;
+    }
+    if (((w.y >> 16) & kRejectBit) || (code != C_JOB_CREATED && code != C_JOB_COMPLETED) || elem >= P.els.size()) continue;
+    const uint32_t tid = P.job_type_id[elem];
+    const int64_t key = h->key_of(inst, w.x & 0xFFFF);
+    if (code == C_JOB_CREATED) {
+      h->job_index[{tid, key}] = {inst, (uint16_t)(w.x & 0xFFFF)};
+    } else {
+      h->job_index.erase({tid, key});
+      if (h->activated.count(key)) h->completed_activated.push_back(key);
+    }
+  }
+}
+
 // Key relabelling bookkeeping of the last run, in log (source) order: each command's first key
 // (DbKeyGenerator order), the subjects' key histories and the resolve_key table.  It advances
 // lazily, command by command: up to `limit`, and never past a fallback command whose CPU-engine keys
@@ -928,6 +983,10 @@ static hipEvent_t next_event(zbhip_handle* h) {
 // keys the CPU engine generated before the keys of the window's later commands are fixed.
 static int advance(zbhip_handle* h, size_t limit, bool force) {
   if (!h->results || h->fin_next >= h->n_cmds) return ZBHIP_OK;
+  if (h->fin_next == 0) {  // a new window: jobs completed in the previous one are gone
+    for (int64_t k : h->completed_activated) h->activated.erase(k);
+    h->completed_activated.clear();
+  }
   const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
   if (h->hist.size() < subjects) {
     h->hist.resize(subjects);
@@ -961,6 +1020,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
         h->hist[h2.x].push_back({(uint16_t)(h2.y & 0xFFFF), h->key_counter + 1 + nprim});
         h->batches.push_back({h->key_counter + 1 + nprim, h2.x, (uint16_t)(h2.y & 0xFFFF), (uint16_t)nsec, h->inst_gen[h2.x]});
       }
+      if (h->job_index_on && h2.x < h->cfg.max_instances) track_jobs(h, c, h2.x);
       if ((hd.y & HDR_ENDED) && h2.x < h->cfg.max_instances) ++h->inst_gen[h2.x];
       h->key_counter += nkeys;
       continue;
@@ -974,6 +1034,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
       h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
       h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[cm.instance]});
     }
+    if (h->job_index_on) track_jobs(h, c, cm.instance);
     if (hd.y & HDR_ENDED) ++h->inst_gen[cm.instance];  // completed: its job keys no longer resolve
     h->key_counter += nkeys;
   }
@@ -1755,15 +1816,23 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     }
     if (job_row) {
       const char* type = P.strings[E.job_type].c_str();
+      const bool act = (e.y >> 25) & 1;  // ACTIVATED (zbhip_activate_jobs): deadline and worker on the host
+      const auto ait = act ? h->activated.find(jk) : h->activated.end();
+      const long long deadline = ait != h->activated.end() ? (long long)ait->second.deadline : -1;
       snprintf(buf, sizeof buf,
                "JOBS|%lld|type=%s,retries=%u,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
-               "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>",
+               "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
+               "deadline=%lld,worker=%s",
                jk, type, E.job_retries, P.id(elem).c_str(), k, pik, P.strings[P.bpmn_id].c_str(), (long long)P.def_key,
-               P.version);
+               P.version, deadline, ait != h->activated.end() ? ait->second.worker.c_str() : "");
       sink(ctx, buf);
-      snprintf(buf, sizeof buf, "JOB_STATES|%lld|ACTIVATABLE", jk);
+      snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", jk, act ? "ACTIVATED" : "ACTIVATABLE");
       sink(ctx, buf);
-      snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|<default>|%lld", type, jk);
+      if (act) {
+        snprintf(buf, sizeof buf, "JOB_DEADLINES|%lld|%lld", deadline, jk);
+      } else {
+        snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|<default>|%lld", type, jk);
+      }
       sink(ctx, buf);
     }
   }
@@ -1912,6 +1981,10 @@ int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n) 
       HIPCHK(hipMemcpy(h->st.pms + i, &z, sizeof z, hipMemcpyHostToDevice));
     }
     if (i < h->inst_gen.size()) ++h->inst_gen[i];
+    for (auto it = h->job_index.begin(); it != h->job_index.end();)
+      it = it->second.first == i ? h->job_index.erase(it) : std::next(it);
+    for (auto it = h->activated.begin(); it != h->activated.end();)
+      it = it->second.inst == i ? h->activated.erase(it) : std::next(it);
   }
   return ZBHIP_OK;
 }
@@ -2019,6 +2092,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   std::vector<ImpVar> vars;
   std::vector<std::tuple<int64_t, std::string, std::string, uint32_t>> taken;
   std::set<int64_t> job_rows;
+  std::map<int64_t, std::pair<int64_t, std::string>> job_act;  // ACTIVATED jobs: deadline, worker
+  std::set<int64_t> job_activated_state;
   std::vector<ImpPms> pms;
   int64_t latest = -1;
   bool stats_row = false;
@@ -2049,6 +2124,11 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       taken.emplace_back(to_ll(p[1]), p[2], p[3], (uint32_t)to_ll(p[4]));
     } else if (cf == "JOBS" && p.size() >= 3) {
       job_rows.insert(to_ll(p[1]));
+      auto f = row_fields(p[2]);
+      job_act[to_ll(p[1])] = {f.count("deadline") ? to_ll(f["deadline"]) : -1, f["worker"]};
+    } else if (cf == "JOB_STATES" && p.size() >= 3) {
+      if (p[2] == "ACTIVATED") job_activated_state.insert(to_ll(p[1]));
+      else if (p[2] != "ACTIVATABLE") return ZBHIP_EUNSUPP;  // failed / error-thrown jobs: outside the subset
     } else if (cf == "PROCESS_SUBSCRIPTION_BY_KEY" && p.size() >= 4) {
       auto f = row_fields(p[3]);
       ImpPms m;
@@ -2159,7 +2239,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       const int el = elem_of_id(e.id);
       if (el < 0 || P.els[el].element_type != e.type) return ZBHIP_EINVAL;
       const uint32_t job = e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
-      const uint32_t row = e.job > 0 && job_rows.count(e.job) ? 1u : 0u;
+      const uint32_t row = e.job > 0 && job_rows.count(e.job) ? (job_activated_state.count(e.job) ? 3u : 1u) : 0u;
       slots[c * N + inst] = make_uint2((uint32_t)el | (ord(e.key) << 16), job | (e.state << 16) | (row << 24));
     }
     for (size_t v = 0; v < ivars.size(); ++v) {
@@ -2229,6 +2309,10 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     HIPCHK(hipMemcpy(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice));
   }
   h->published |= stats_row;
+  for (const Done& d : done)
+    for (int64_t k : d.keys)
+      if (job_activated_state.count(k)) h->activated[k] = {job_act[k].first, job_act[k].second, d.slot};
+  h->job_index_on = false;  // rebuilt from the device rows at the next activation
   if (n_instances) *n_instances = (uint32_t)done.size();
   return ZBHIP_OK;
 }
@@ -2255,4 +2339,162 @@ extern "C" int zbhip_import_state_db(zbhip_handle* h, const uint8_t* entries, si
     off += (size_t)hd[1] + hd[2];
   }
   return zbhip_import_state(h, rows.data(), rows.size(), first_slot, n_instances);
+}
+
+// ---- job activation ----------------------------------------------------------
+// JOB_BATCH:ACTIVATE: the host's JOB_ACTIVATABLE index picks the jobs (type, then job key), the device
+// marks them ACTIVATED and gathers their element instances and variables (k_activate_jobs).
+static int build_job_index(zbhip_handle* h) {
+  const size_t N = h->st.n;
+  std::vector<uint4> hdr(N);
+  std::vector<uint2> slots(N * kSlots);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(hdr.data(), h->st.hdr, N * sizeof(uint4), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(slots.data(), h->st.slots, N * kSlots * sizeof(uint2), hipMemcpyDeviceToHost));
+  h->job_index.clear();
+  for (size_t i = 0; i < N; ++i) {
+    const uint32_t proc = hdr[i].x & 0xFFFF;
+    if (proc == NONE || proc >= h->procs.size() || !((hdr[i].y >> 24) & 1)) continue;
+    const Proc& P = h->procs[proc];
+    const uint32_t ns = (hdr[i].y >> 8) & 0xFF;
+    for (uint32_t s = 0; s < ns && s < (uint32_t)kSlots; ++s) {
+      const uint2 e = slots[s * N + i];
+      const uint32_t elem = e.x & 0xFFFF, job = e.y & 0xFFFF, fl = e.y >> 24;
+      if ((fl & 3u) != 1u || elem >= P.els.size()) continue;  // a job row, not activated
+      h->job_index[{P.job_type_id[elem], h->key_of((uint32_t)i, job)}] = {(uint32_t)i, (uint16_t)job};
+    }
+  }
+  h->job_index_on = true;
+  return ZBHIP_OK;
+}
+
+extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* cmd, zbhip_activated_job* jobs,
+                                   size_t cap, zbhip_job_batch* res) {
+  if (!h || !cmd || !res || (cap && !jobs) || (cmd->type_len && !cmd->type) || (cmd->worker_len && !cmd->worker) ||
+      (cmd->n_variables && !cmd->variables))
+    return ZBHIP_EINVAL;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  *res = zbhip_job_batch{};
+  res->key = -1;
+  res->rejection_type = ZBHIP_REJ_NONE;
+  // JobBatchActivateProcessor.isValid / rejectCommand (:68-118): INVALID_ARGUMENT, no key
+  const uint8_t reason = cmd->max_jobs < 1 ? 1 : cmd->timeout < 1 ? 2 : cmd->type_len == 0 ? 3 : 0;
+  if (reason) {
+    res->rejection_type = ZBHIP_REJ_INVALID_ARGUMENT;
+    res->reason = reason;
+    return ZBHIP_OK;
+  }
+  if (!h->job_index_on)
+    if (int rc = build_job_index(h)) return rc;
+  res->key = ((int64_t)h->cfg.partition_id << 51) + ++h->key_counter;  // keyGenerator.nextKey
+  if (h->st.n_slots) {
+    const unsigned long long kc = (unsigned long long)h->key_counter;
+    HIPCHK(hipMemcpy(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice));
+  }
+  const std::string type(cmd->type, cmd->type_len), worker(cmd->worker ? cmd->worker : "", cmd->worker_len);
+  auto tit = h->job_type_ids.find(type);
+  std::vector<std::pair<int64_t, std::pair<uint32_t, uint16_t>>> pick;
+  if (tit != h->job_type_ids.end()) {
+    const size_t want = std::min<size_t>((size_t)cmd->max_jobs, cap);
+    for (auto it = h->job_index.lower_bound({tit->second, INT64_MIN});
+         it != h->job_index.end() && it->first.first == tit->second && pick.size() < want; ++it)
+      pick.push_back({it->first.second, it->second});
+    if (!pick.empty() && pick.size() == cap && cap < (size_t)cmd->max_jobs) {  // the caller's buffer was the limit
+      const auto nx = h->job_index.upper_bound({tit->second, pick.back().first});
+      res->truncated = nx != h->job_index.end() && nx->first.first == tit->second;
+    }
+  }
+  res->n_jobs = (uint32_t)pick.size();
+  if (pick.empty()) return ZBHIP_OK;
+  const size_t n = pick.size(), ob = activated_out_bytes();
+  std::vector<uint2> list(n);
+  for (size_t i = 0; i < n; ++i) list[i] = make_uint2(pick[i].second.first, pick[i].second.second);
+  uint2* d_list = nullptr;
+  void* d_out = nullptr;
+  std::vector<uint8_t> outb(n * ob);
+  if (hipMalloc(reinterpret_cast<void**>(&d_list), n * sizeof(uint2)) != hipSuccess) return ZBHIP_ENOMEM;
+  if (hipMalloc(&d_out, n * ob) != hipSuccess) {
+    (void)hipFree(d_list);
+    return ZBHIP_ENOMEM;
+  }
+  hipError_t e = hipMemcpyAsync(d_list, list.data(), n * sizeof(uint2), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = launch_activate_jobs(h->st, d_list, (uint32_t)n, d_out, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(outb.data(), d_out, n * ob, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d_list);
+  (void)hipFree(d_out);
+  if (e != hipSuccess) return ZBHIP_EDEVICE;
+  std::vector<uint32_t> requested(cmd->variables, cmd->variables + cmd->n_variables);
+  auto name_less = [h](uint32_t a, uint32_t b) {  // DbString order: length, then bytes
+    const std::string& x = h->names[a];
+    const std::string& y = h->names[b];
+    return x.size() != y.size() ? x.size() < y.size() : x < y;
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t* o = outb.data() + i * ob;
+    uint4 a;
+    uint2 meta[kVars];
+    long long val[kVars];
+    memcpy(&a, o, sizeof a);
+    memcpy(meta, o + sizeof(uint4), sizeof meta);
+    memcpy(val, o + sizeof(uint4) + sizeof meta, sizeof val);
+    const uint32_t inst = pick[i].second.first;
+    if (!a.w) return ZBHIP_EDEVICE;  // the index and the device rows disagree
+    const uint32_t proc = a.y & 0xFFFF, elem = a.x & 0xFFFF, eord = a.x >> 16;
+    zbhip_activated_job& j = jobs[i];
+    j = zbhip_activated_job{};
+    j.key = pick[i].first;
+    j.element_instance_key = h->key_of(inst, eord);
+    j.process_instance_key = h->key_of(inst, 0);
+    j.deadline = cmd->timestamp + cmd->timeout;
+    j.instance = inst;
+    j.process_idx = (int32_t)proc;
+    j.element_idx = (int32_t)elem;
+    j.retries = proc < h->procs.size() && elem < h->procs[proc].els.size() ? h->procs[proc].els[elem].job_retries : 0;
+    // DbVariableState.visitVariables: the element's scope, then the process instance's
+    const uint32_t nv = std::min<uint32_t>((a.z >> 16) & 0xFF, (uint32_t)kVars);
+    std::vector<uint32_t> taken;
+    for (uint32_t scope : {eord, 0u}) {
+      std::vector<uint32_t> local;
+      for (uint32_t v = 0; v < nv; ++v)
+        if ((meta[v].x >> 16) == scope) local.push_back(v);
+      std::sort(local.begin(), local.end(),
+                [&](uint32_t p, uint32_t q) { return name_less(meta[p].x & 0xFFFF, meta[q].x & 0xFFFF); });
+      for (uint32_t v : local) {
+        const uint32_t name = meta[v].x & 0xFFFF;
+        if (std::find(taken.begin(), taken.end(), name) != taken.end()) continue;
+        if (!requested.empty() && std::find(requested.begin(), requested.end(), name) == requested.end()) continue;
+        taken.push_back(name);
+        zbhip_doc_entry& d = j.variables[j.n_variables++];
+        d.name_id = name;
+        d.type = (uint8_t)((meta[v].y >> 16) & 0xFF);
+        d.value = val[v];
+      }
+    }
+    // JobBatchActivatedApplier -> DbJobState.activate: ACTIVATED, out of JOB_ACTIVATABLE, deadline
+    h->job_index.erase({tit->second, j.key});
+    h->activated[j.key] = {j.deadline, worker, inst};
+  }
+  return ZBHIP_OK;
+}
+
+extern "C" int zbhip_job_batch_rejection_reason(const zbhip_job_activation* cmd, const zbhip_job_batch* res, char* buf,
+                                               size_t cap) {
+  if (!cmd || !res || !buf || !cap) return ZBHIP_EINVAL;
+  const char* f = "Expected to activate job batch with %s to be %s, but it was %s";  // rejectCommand (:91-118)
+  char v[64];
+  switch (res->reason) {
+    case 1:
+      snprintf(v, sizeof v, "'%d'", cmd->max_jobs);
+      snprintf(buf, cap, f, "max jobs to activate", "greater than zero", v);
+      break;
+    case 2:
+      snprintf(v, sizeof v, "'%lld'", (long long)cmd->timeout);
+      snprintf(buf, cap, f, "timeout", "greater than zero", v);
+      break;
+    case 3: snprintf(buf, cap, f, "type", "present", "blank"); break;
+    default: buf[0] = 0;
+  }
+  return ZBHIP_OK;
 }

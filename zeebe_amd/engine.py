@@ -262,6 +262,21 @@ class Partition:
         check(self.L.zbhip_import_state(self.h, text, len(text), first_slot, C.byref(n)), "zbhip_import_state")
         return n.value
 
+    def activate_jobs(self, job_type, worker="worker", timeout=300000, max_jobs=10, timestamp=0, variables=(),
+                      cap=None):
+        """JOB_BATCH:ACTIVATE (JobBatchActivateProcessor): (batch key, activated jobs, rejection reason);
+        the key is -1 and the reason 1/2/3 for an invalid command."""
+        t, w = job_type.encode(), worker.encode()
+        names = np.asarray([self.intern(v) for v in variables], dtype=np.uint32)
+        cap = max_jobs if cap is None else cap
+        out = np.zeros(max(cap, 1), dtype=abi.ACTIVATED_JOB_DTYPE)
+        cmd = abi.JobActivation(type=t, type_len=len(t), worker=w, worker_len=len(w), timeout=timeout,
+                                max_jobs=max_jobs, timestamp=timestamp,
+                                variables=names.ctypes.data if len(names) else None, n_variables=len(names))
+        res = abi.JobBatch()
+        check(self.L.zbhip_activate_jobs(self.h, C.byref(cmd), out.ctypes.data, cap, C.byref(res)), "zbhip_activate_jobs")
+        return res.key, out[: res.n_jobs], res.reason
+
     def key_before(self, i):
         k = C.c_int64()
         check(self.L.zbhip_key_before(self.h, i, C.byref(k)), "zbhip_key_before")

@@ -29,7 +29,7 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream",
            "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
            "zbhip_set_external_keys", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
-           "zbhip_import_state"]
+           "zbhip_import_state", "zbhip_activate_jobs", "zbhip_job_batch_rejection_reason"]
 
 
 class ZbhipError(RuntimeError):
@@ -100,6 +100,8 @@ def load():
                                                       C.c_char_p, sz]
     L.zbhip_import_state_db.argtypes = [vp, C.c_char_p, sz, u32, C.POINTER(u32)]
     L.zbhip_import_state.argtypes = [vp, C.c_char_p, sz, u32, C.POINTER(u32)]
+    L.zbhip_activate_jobs.argtypes = [vp, C.POINTER(abi.JobActivation), vp, sz, C.POINTER(abi.JobBatch)]
+    L.zbhip_job_batch_rejection_reason.argtypes = [C.POINTER(abi.JobActivation), C.POINTER(abi.JobBatch), C.c_char_p, sz]
     L.zbhip_stream.argtypes = [vp]
     L.zbhip_stream.restype = vp
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
