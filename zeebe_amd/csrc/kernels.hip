@@ -97,7 +97,10 @@ using KGeneric = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, Z
 #ifndef ZB_KMSG_R
 #define ZB_KMSG_R 4
 #endif
-using KMsg = KCfg<128, 12, 16, ZB_KMSG_R, true>;  // partitions with message catch events (config 5)
+#ifndef ZB_KMSG_W
+#define ZB_KMSG_W 2  // 256 VGPRs, no AGPR or scratch spill: 2 waves per SIMD (compiler default: 260 -> 1)
+#endif
+using KMsg = KCfg<128, 12, 16, ZB_KMSG_R, true, true, true, ZB_KMSG_W>;  // message catch events (config 5)
 
 template <class K>
 struct Lane {
@@ -1405,10 +1408,13 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
     const size_t ri = (size_t)got * S + L.op_slot;
     P.st.sub_b[ri] = make_longlong2(L.ins_eik, L.ins_pik);
     P.st.sub_k[ri] = make_longlong2(L.ins_key, -1);
-    uint4 a = L.ins_a;
-    P.st.sub_a[ri] = make_uint4(3u, a.y, a.z, a.w);
-    __threadfence();
-    atomicExch(&P.st.sub_a[ri].x, a.x);
+    // the row in one 16-byte store, state included.  No release fence: on gfx950 an agent-scope
+    // fence writes back the XCD's whole L2 (buffer_wbl2), once per wave -- and nothing needs it.
+    // Rows are read by later launches (kernel boundaries order them); a lane of this launch that
+    // reads the slot meanwhile (another subscriber's duplicate check) matches only its own
+    // (partition, instance, element) triple, which no concurrent insert carries, and removed rows
+    // are zeroed, so even a torn read of a row being written matches nothing.
+    P.st.sub_a[ri] = L.ins_a;
     patch_mask |= 1u << got;
   }
   if (L.op_corr_mask) {
@@ -1424,7 +1430,7 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
   }
   if (L.op_rm_mask) {
     for (int r = 0; r < kSubs; ++r)
-      if ((L.op_rm_mask >> r) & 1) atomicExch(&P.st.sub_a[(size_t)r * S + L.op_rm_slot].x, 0u);
+      if ((L.op_rm_mask >> r) & 1) P.st.sub_a[(size_t)r * S + L.op_rm_slot] = make_uint4(0, 0, 0, 0);
     patch_mask &= ~(L.op_rm_slot == patch_slot ? L.op_rm_mask : 0u);
   }
   if (patch_mask) {  // the key scan replaces this window's key references in these rows
@@ -1437,6 +1443,15 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
   if (L.slot_lane) P.st.slot_hdr[L.slot].x = L.s_next_ord;
 }
 
+#ifdef ZB_STAMPS
+// run_command phases (summed over waves, cycles): [0] row loads, [1] initial command,
+// [2] FIFO: PI entries, [3] FIFO: local subscription entries, [4] commit, [5] FIFO entries
+__device__ unsigned long long g_stamps_run[8];
+#define ZB_RSTAMP(v) const unsigned long long v = clock64()
+#else
+#define ZB_RSTAMP(v)
+#endif
+
 // One command's whole batch on one lane; returns the number of records it staged.
 template <class K, class Retire>
 __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint32_t* prog, uint2* tbl_base,
@@ -1448,6 +1463,10 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   const uint32_t ref = cw.y >> 16;
   const uint32_t doc_begin = cw.z;
   const uint32_t N = P.st.n;
+  ZB_RSTAMP(r0);
+#ifdef ZB_STAMPS
+  unsigned long long r_pi = 0, r_lq = 0, r_n = 0;
+#endif
 
   Lane<K> L;
   L.tbl = tbl_base + threadIdx.x;
@@ -1598,6 +1617,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     }
   }
 
+  ZB_RSTAMP(r1);
   // deploy-time compiled straight-line segments (linear chains): the batch is emitted without
   // the FIFO; anything outside the canonical states takes the general path below
   bool fast = false;
@@ -1648,6 +1668,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     else set_fail(L, FB_UNSUPPORTED);
   }
   L.processed = kind == CMD_FOLLOWUP ? 0 : 1;
+  ZB_RSTAMP(r2);
 
   // ---- the batch FIFO (ProcessingStateMachine.batchProcessing :328-374) ----
 #ifdef ZB_EXP_FASTONLY
@@ -1655,16 +1676,28 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
 #endif
   while (!fast && L.qh < L.qt && !L.fail) {
     const uint32_t entry = dequeue(L);
+#ifdef ZB_STAMPS
+    ++r_n;
+#endif
     if constexpr (K::M) {
       if (entry & LQ_BIT) {
+        ZB_RSTAMP(q0);
         process_local(L, entry & 0xF);
         ++L.processed;
+#ifdef ZB_STAMPS
+        ZB_RSTAMP(q1); r_lq += q1 - q0;
+#endif
         continue;
       }
     }
+    ZB_RSTAMP(p0);
     process_pi(L, entry);
     ++L.processed;
+#ifdef ZB_STAMPS
+    ZB_RSTAMP(p1); r_pi += p1 - p0;
+#endif
   }
+  ZB_RSTAMP(r3);
 
   retire();  // the caller's prefetch loads: retired before the first store of the commit
   // ---- commit: write back the instance (or leave it untouched on fallback) ----
@@ -1744,6 +1777,15 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
                                  (ended ? HDR_ENDED : 0u));
   acc.cmd += 1;
   acc.fb += ok ? 0u : 1u;
+#ifdef ZB_STAMPS
+  {
+    ZB_RSTAMP(r4);
+    if ((threadIdx.x & 63) == 0) {
+      const unsigned long long v[6] = {r1 - r0, r2 - r1, r_pi, r_lq, r4 - r3, r_n};
+      for (int k = 0; k < 6; ++k) atomicAdd(&g_stamps_run[k], v[k]);
+    }
+  }
+#endif
   acc.rec += nrec - npay;
   acc.trans += ok ? L.transitions : 0u;
   acc.comp += ok ? L.completed : 0u;
@@ -2168,14 +2210,26 @@ struct BucketParams {
 };
 constexpr int kBucketB = 256;
 
-__device__ __forceinline__ uint32_t entries_to(const BucketParams& Q, uint32_t c, uint32_t t) {
-  if (c >= Q.n || ((Q.cmd_hdr[c].y >> 16) & 0xFF) != ST_OK) return 0;
-  const uint32_t nout = min(Q.cmd_hdr2[c].z, (uint32_t)kOut);
-  uint32_t k = 0;
-  for (uint32_t j = 0; j < nout; ++j) {
-    const zbhip_xpart_cmd& x = Q.xout[(size_t)c * kOut + j];
-    k += x.kind != XK_PATCH && (uint32_t)x.target_partition == t + 1;
+// The targets (1-based partition ids, 0 = none) of command c's sent entries, read once: the
+// bpmn_process_id/kind/interrupting word (bytes 36..39) and the source/target word (40..43).
+__device__ __forceinline__ void load_targets(const BucketParams& Q, uint32_t c, uint32_t (&tg)[kOut]) {
+  uint32_t nout = 0;
+  if (c < Q.n && ((Q.cmd_hdr[c].y >> 16) & 0xFF) == ST_OK) nout = min(Q.cmd_hdr2[c].z, (uint32_t)kOut);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(Q.xout + (size_t)c * kOut);
+#pragma unroll
+  for (int j = 0; j < kOut; ++j) {
+    tg[j] = 0;
+    if ((uint32_t)j < nout) {
+      const uint32_t kw = w[j * (sizeof(zbhip_xpart_cmd) / 4) + 9], tw = w[j * (sizeof(zbhip_xpart_cmd) / 4) + 10];
+      if (((kw >> 16) & 0xFF) != XK_PATCH) tg[j] = (uint32_t)(int32_t)(int16_t)(tw >> 16);
+    }
   }
+}
+
+__device__ __forceinline__ uint32_t count_to(const uint32_t (&tg)[kOut], uint32_t t) {
+  uint32_t k = 0;
+#pragma unroll
+  for (int j = 0; j < kOut; ++j) k += tg[j] == t + 1;
   return k;
 }
 
@@ -2194,13 +2248,19 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t& total)
   return b + inc - v;
 }
 
+// per-block counts by target: an LDS histogram (one pass over the outbox, any partition count)
+constexpr uint32_t kMaxParts = 1024;
 __global__ __launch_bounds__(kBucketB) void k_bucket_count(BucketParams Q) {
-  const uint32_t c = blockIdx.x * kBucketB + threadIdx.x;
-  for (uint32_t t = 0; t < Q.parts; ++t) {
-    uint32_t tot;
-    (void)block_excl_scan(entries_to(Q, c, t), tot);
-    if (threadIdx.x == 0) Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] = tot;
-  }
+  __shared__ uint32_t hist[kMaxParts];
+  for (uint32_t t = threadIdx.x; t < Q.parts; t += kBucketB) hist[t] = 0;
+  __syncthreads();
+  uint32_t tg[kOut];
+  load_targets(Q, blockIdx.x * kBucketB + threadIdx.x, tg);
+#pragma unroll
+  for (int j = 0; j < kOut; ++j)
+    if (tg[j] - 1u < Q.parts) atomicAdd(&hist[tg[j] - 1], 1u);
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < Q.parts; t += kBucketB) Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] = hist[t];
 }
 
 // The scan of the per-block counts, target-major (bucket t after buckets 0..t-1, blocks in order):
@@ -2240,18 +2300,32 @@ __global__ __launch_bounds__(64) void k_bucket_scan_bases(BucketParams Q, uint32
   }
 }
 
+// the scatter visits only the targets present in the block (an LDS bit set), in target order; the
+// block scan per target keeps log order (command, then entry) inside each bucket
 __global__ __launch_bounds__(kBucketB) void k_bucket_scatter(BucketParams Q, const uint32_t* grp) {
+  __shared__ uint32_t present[kMaxParts / 32];
+  for (uint32_t t = threadIdx.x; t < kMaxParts / 32; t += kBucketB) present[t] = 0;
+  __syncthreads();
   const uint32_t c = blockIdx.x * kBucketB + threadIdx.x;
   const uint32_t g = blockIdx.x / kScanG;
-  for (uint32_t t = 0; t < Q.parts; ++t) {
-    uint32_t tot;
-    const uint32_t mine = entries_to(Q, c, t);
-    uint32_t o = grp[(size_t)g * Q.parts + t] + Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] + block_excl_scan(mine, tot);
-    if (mine) {
-      const uint32_t nout = min(Q.cmd_hdr2[c].z, (uint32_t)kOut);
-      for (uint32_t j = 0; j < nout; ++j) {
-        const zbhip_xpart_cmd& x = Q.xout[(size_t)c * kOut + j];
-        if (x.kind != XK_PATCH && (uint32_t)x.target_partition == t + 1) Q.out[o++] = x;
+  uint32_t tg[kOut];
+  load_targets(Q, c, tg);
+#pragma unroll
+  for (int j = 0; j < kOut; ++j)
+    if (tg[j] - 1u < Q.parts) atomicOr(&present[(tg[j] - 1) >> 5], 1u << ((tg[j] - 1) & 31));
+  __syncthreads();
+  for (uint32_t wi = 0; wi < (Q.parts + 31) / 32; ++wi) {
+    uint32_t bits = present[wi];  // the same for every thread: uniform loop
+    while (bits) {
+      const uint32_t t = wi * 32 + __builtin_ctz(bits);
+      bits &= bits - 1;
+      uint32_t tot;
+      const uint32_t mine = count_to(tg, t);
+      uint32_t o = grp[(size_t)g * Q.parts + t] + Q.blk_cnt[(size_t)blockIdx.x * Q.parts + t] + block_excl_scan(mine, tot);
+      if (mine) {
+#pragma unroll
+        for (int j = 0; j < kOut; ++j)
+          if (tg[j] == t + 1) Q.out[o++] = Q.xout[(size_t)c * kOut + j];
       }
     }
   }
@@ -2458,11 +2532,17 @@ void dump_stamps() {
 #ifdef ZB_STAMPS
   unsigned long long h[8] = {};
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof h) != hipSuccess) return;
+  const unsigned long long z8[8] = {};
   const double waves = 1.0;  // sums are per wave (lane 0)
+  unsigned long long q[8] = {};
+  if (hipMemcpyFromSymbol(q, HIP_SYMBOL(g_stamps_run), sizeof q) == hipSuccess && h[4])
+    fprintf(stderr, "[stamps] run_command per chunk: loads %.0f initial %.0f fifo-pi %.0f fifo-local %.0f commit %.0f | entries/lane0 %.2f\n",
+            q[0] / (double)h[4], q[1] / (double)h[4], q[2] / (double)h[4], q[3] / (double)h[4], q[4] / (double)h[4],
+            q[5] / (double)h[4]);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_run), z8, sizeof z8);
   fprintf(stderr, "[stamps] chunks %llu | per chunk cycles: top-wait %.0f run %.0f scan+barrier %.0f flush %.0f | prologue sum %.3g\n",
           h[4], h[0] / (double)h[4] * waves, h[1] / (double)h[4], h[2] / (double)h[4], h[3] / (double)h[4], (double)h[5]);
-  const unsigned long long z[8] = {};
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z8, sizeof z8);
 #endif
 }
 
