@@ -152,6 +152,7 @@ struct Lane {
   uint16_t s_next_ord;      // correlation-slot key space
   uint16_t i_first_ord;     // first instance-space ordinal of this batch
   uint32_t n_out, n_pay;
+  uint32_t x_sum;           // sends: count (bits 0..3) | their target if one (8..23) | mixed (31)
   // pending local commands (SubscriptionCommandSender follow-ups on this partition)
   uint32_t lq_slot;         // correlation slot of a local MESSAGE_SUBSCRIPTION command
   uint32_t lq_row;          // slot row of a local PROCESS_MESSAGE_SUBSCRIPTION:CORRELATE
@@ -721,7 +722,8 @@ template <class K>
 __device__ __forceinline__ void send_xpart(Lane<K>& L, uint32_t kind, uint32_t target, long long eik, long long pik,
                                            long long msg, uint32_t corr, uint32_t inst, uint32_t eord,
                                            uint32_t name_bpmn, uint32_t intr) {
-  if (L.n_out >= (uint32_t)kOut - 1) { set_fail(L, FB_MESSAGE); return; }  // one entry kept for a row patch
+  // one entry kept for a row patch; continuation batches (ci past the window) never send
+  if (L.n_out >= (uint32_t)kOut - 1 || L.ci >= L.sp->xcap) { set_fail(L, FB_MESSAGE); return; }
   zbhip_xpart_cmd x;
   x.element_instance_key = eik;
   x.process_instance_key = pik;
@@ -736,7 +738,10 @@ __device__ __forceinline__ void send_xpart(Lane<K>& L, uint32_t kind, uint32_t t
   x.source_partition = (int16_t)L.sp->partition_id;
   x.target_partition = (int16_t)target;
   x.pad = 0;
-  L.sp->xout[(size_t)L.ci * kOut + L.n_out++] = x;
+  L.sp->xout[(size_t)L.n_out++ * L.sp->xcap + L.ci] = x;
+  const uint32_t ns = L.x_sum & 0xF, t0 = (L.x_sum >> 8) & 0xFFFF;
+  const bool mixed = (L.x_sum >> 31) || (ns && t0 != (target & 0xFFFF));
+  L.x_sum = (ns + 1) | ((ns ? t0 : target & 0xFFFF) << 8) | (mixed ? 0x80000000u : 0u);
 }
 
 // CatchEventBehavior.subscribeToEvents -> subscribeToMessageEvent (processing/common/
@@ -1399,7 +1404,7 @@ template <class K>
 __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
   const StepParams& P = *L.sp;
   const uint32_t S = P.st.n_slots;
-  uint32_t patch_mask = 0, patch_slot = L.op_slot;
+  uint32_t patch_mask = 0, patch_slot = L.op_slot, patch_what = 0;  // bit 0: sub_b, bit 1: sub_k
   if (L.op_ins) {
     int got = -1;
     for (int r = 0; r < kSubs && got < 0; ++r)
@@ -1416,6 +1421,9 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
     // are zeroed, so even a torn read of a row being written matches nothing.
     P.st.sub_a[ri] = L.ins_a;
     patch_mask |= 1u << got;
+    // the subscription key is always a reference of this window; the element / process instance
+    // keys only when this window generated them (a received command carries real keys)
+    patch_what |= 2u | (L.ins_eik < -1 || L.ins_pik < -1 ? 1u : 0u);
   }
   if (L.op_corr_mask) {
     for (int r = 0; r < kSubs; ++r)
@@ -1427,18 +1435,21 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
       }
     patch_mask |= L.op_corr_mask;
     patch_slot = L.slot;
+    patch_what |= 2u;  // the correlating message key
   }
   if (L.op_rm_mask) {
     for (int r = 0; r < kSubs; ++r)
       if ((L.op_rm_mask >> r) & 1) P.st.sub_a[(size_t)r * S + L.op_rm_slot] = make_uint4(0, 0, 0, 0);
     patch_mask &= ~(L.op_rm_slot == patch_slot ? L.op_rm_mask : 0u);
   }
+  if (patch_mask && L.ci >= P.xcap) { set_fail(L, FB_MESSAGE); return; }
   if (patch_mask) {  // the key scan replaces this window's key references in these rows
     zbhip_xpart_cmd x = {};
     x.kind = XK_PATCH;
     x.correlation_key = patch_slot;
     x.instance = patch_mask;
-    P.xout[(size_t)L.ci * kOut + L.n_out++] = x;
+    x.element_ord = (uint16_t)patch_what;
+    P.xout[(size_t)L.n_out++ * P.xcap + L.ci] = x;
   }
   if (L.slot_lane) P.st.slot_hdr[L.slot].x = L.s_next_ord;
 }
@@ -1510,6 +1521,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     L.slot = 0;
     L.s_next_ord = L.s_first_ord = 0;
     L.n_out = L.n_pay = 0;
+    L.x_sum = 0;
     L.lq_slot = L.lq_corr = L.lq_name_bpmn = L.lq_eord = 0;
     L.lq_row = kNoInst;
     L.lq_msg = L.lq_eik = L.lq_pik = -1;
@@ -1758,7 +1770,10 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       first = L.s_first_ord;
     }
     npay = ok ? L.n_pay : 0u;
-    P.cmd_hdr2[ci] = make_uint4(L.inst, L.i_first_ord | (nsec << 16), ok ? L.n_out : 0u, npay);
+    // z: outbox entries (bits 0..3; sends first, a row patch last), sends (4..7), their common
+    // target (8..23) unless mixed (31) -- the bucketing reads the outbox only for mixed targets
+    P.cmd_hdr2[ci] = make_uint4(L.inst, L.i_first_ord | (nsec << 16),
+                                ok ? L.n_out | ((L.x_sum & 0xF) << 4) | (L.x_sum & 0xFFFFFF00u) : 0u, npay);
   }
   if (!ok && !bad_cmd) {  // fence the subject(s) for the rest of the window
     if (slot_kind) {
@@ -2086,6 +2101,7 @@ struct KeyScanParams {
   unsigned long long* base;       // [n] key counter value before command c's first key
   unsigned long long* counter;    // [1] the partition's key counter (last generated value)
   zbhip_xpart_cmd* xout;
+  uint32_t xcap;
   long long* pi_key;
   uint32_t n_inst;
   uint4* sub_a;
@@ -2140,18 +2156,35 @@ __global__ __launch_bounds__(1024) void k_key_scan_sums(KeyScanParams K, uint32_
   if (threadIdx.x == 0) *K.counter = carry;
 }
 
+// a key reference of window command rc, given that command's headers and key base
+__device__ __forceinline__ long long resolve_with(unsigned long long v, uint2 h, uint4 h2, unsigned long long base,
+                                                  long long pbits) {
+  const uint32_t sec = (v >> 16) & 1, ord = v & 0xFFFF;
+  const uint32_t nsec = h2.y >> 16;
+  const uint32_t nprim = (h.x >> 16) - nsec;
+  const unsigned long long off = sec ? nprim + (uint16_t)(ord - (h2.y & 0xFFFF)) : (uint16_t)(ord - (h.y & 0xFFFF));
+  return pbits + (long long)(base + 1 + off);
+}
+
 __device__ __forceinline__ long long resolve_cmd_ref(const KeyScanParams& K, long long ref) {
   if (ref >= -1) return ref;
   const unsigned long long v = (unsigned long long)(-2 - ref);
   if ((v >> 62) & 1) return ref;  // a subject ordinal: resolved by the host drain
-  const uint32_t c = (uint32_t)(v >> 17), sec = (v >> 16) & 1, ord = v & 0xFFFF;
+  const uint32_t c = (uint32_t)(v >> 17);
   if (c >= K.n) return ref;
-  const uint2 h = K.cmd_hdr[c];
-  const uint4 h2 = K.cmd_hdr2[c];
-  const uint32_t nsec = h2.y >> 16;
-  const uint32_t nprim = (h.x >> 16) - nsec;
-  const unsigned long long off = sec ? nprim + (uint16_t)(ord - (h2.y & 0xFFFF)) : (uint16_t)(ord - (h.y & 0xFFFF));
-  return K.pbits + (long long)(K.base[c] + 1 + off);
+  return resolve_with(v, K.cmd_hdr[c], K.cmd_hdr2[c], K.base[c], K.pbits);
+}
+
+// the common case: a reference of the patching command itself, from the registers holding its
+// headers (every reference k_step writes names its own command; another command's only when a
+// lane copied a row that a concurrent lane of the launch had just inserted)
+__device__ __forceinline__ long long resolve_own(const KeyScanParams& K, long long ref, uint32_t c, uint2 h, uint4 h2,
+                                                 unsigned long long base) {
+  if (ref >= -1) return ref;
+  const unsigned long long v = (unsigned long long)(-2 - ref);
+  if ((v >> 62) & 1) return ref;
+  if ((uint32_t)(v >> 17) != c) return resolve_cmd_ref(K, ref);
+  return resolve_with(v, h, h2, base, K.pbits);
 }
 
 __global__ __launch_bounds__(kScanB) void k_key_apply(KeyScanParams K) {
@@ -2166,33 +2199,55 @@ __global__ __launch_bounds__(kScanB) void k_key_apply(KeyScanParams K) {
   if (i < K.n) K.base[i] = b + inc - v;
 }
 
-// second pass (all bases known): patch references that may point at any command of the window
+__device__ __forceinline__ long long ll_of(uint32_t lo, uint32_t hi) {
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// second pass (all bases known): patch references that may point at any command of the window.
+// Every load of a command is issued before its first store (an outbox entry as three 16-byte
+// loads), so a thread waits for one round of loads, not for a chain through its own stores.
 __global__ __launch_bounds__(256) void k_key_patch(KeyScanParams K) {
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= K.n) return;
   const uint2 h = K.cmd_hdr[c];
-  if (((h.y >> 16) & 0xFF) != ST_OK) return;
+  const uint4 h2 = K.cmd_hdr2[c];
   const uint4 cw = K.cmds[c];
+  const unsigned long long base = K.base[c];
+  if (((h.y >> 16) & 0xFF) != ST_OK) return;
   if ((cw.y & 0xFF) == ZBHIP_CMD_CREATE && cw.x < K.n_inst)  // ordinal 0 of the CREATE batch
-    K.pi_key[cw.x] = K.pbits + (long long)(K.base[c] + 1 + (uint16_t)(0 - (h.y & 0xFFFF)));
-  const uint32_t nout = K.cmd_hdr2[c].z;
-  for (uint32_t j = 0; j < nout && j < (uint32_t)kOut; ++j) {
-    zbhip_xpart_cmd& x = K.xout[(size_t)c * kOut + j];
-    if (x.kind == XK_PATCH) {
-      const uint32_t slot = x.correlation_key;
+    K.pi_key[cw.x] = K.pbits + (long long)(base + 1 + (uint16_t)(0 - (h.y & 0xFFFF)));
+  const uint32_t nout = min(h2.z & 0xF, (uint32_t)kOut);
+  for (uint32_t j = 0; j < nout; ++j) {
+    uint4* xp = reinterpret_cast<uint4*>(K.xout + (size_t)j * K.xcap + c);
+    const uint4 q0 = xp[0];  // element / process instance keys
+    const uint4 q1 = xp[1];  // message key, correlation key (row patch: slot), instance (row mask)
+    const uint4 q2 = xp[2];  // element_ord (row patch: fields), name, bpmn process id, kind, ...
+    if (((q2.y >> 16) & 0xFF) == XK_PATCH) {
+      const uint32_t slot = q1.z, mask = q1.w, what = q2.x & 0xFFFF;
       if (slot >= K.n_slots) continue;
+      // only the row fields that may hold references of this window: random rows, so every
+      // array left alone saves a read-modify-write of a line
       for (int r = 0; r < kSubs; ++r)
-        if ((x.instance >> r) & 1) {
+        if ((mask >> r) & 1) {
           const size_t ri = (size_t)r * K.n_slots + slot;
-          longlong2 bb = K.sub_b[ri], kk = K.sub_k[ri];
-          K.sub_b[ri] = make_longlong2(resolve_cmd_ref(K, bb.x), resolve_cmd_ref(K, bb.y));
-          K.sub_k[ri] = make_longlong2(resolve_cmd_ref(K, kk.x), resolve_cmd_ref(K, kk.y));
+          if (what & 1) {
+            const longlong2 bb = K.sub_b[ri];
+            K.sub_b[ri] = make_longlong2(resolve_own(K, bb.x, c, h, h2, base), resolve_own(K, bb.y, c, h, h2, base));
+          }
+          if (what & 2) {
+            const longlong2 kk = K.sub_k[ri];
+            K.sub_k[ri] = make_longlong2(resolve_own(K, kk.x, c, h, h2, base), resolve_own(K, kk.y, c, h, h2, base));
+          }
         }
       continue;
     }
-    x.element_instance_key = resolve_cmd_ref(K, x.element_instance_key);
-    x.process_instance_key = resolve_cmd_ref(K, x.process_instance_key);
-    x.message_key = resolve_cmd_ref(K, x.message_key);
+    const long long eik = ll_of(q0.x, q0.y), pik = ll_of(q0.z, q0.w), msg = ll_of(q1.x, q1.y);
+    const long long e2 = resolve_own(K, eik, c, h, h2, base), p2 = resolve_own(K, pik, c, h, h2, base),
+                    m2 = resolve_own(K, msg, c, h, h2, base);
+    if (e2 != eik || p2 != pik)
+      xp[0] = make_uint4((uint32_t)e2, (uint32_t)((unsigned long long)e2 >> 32), (uint32_t)p2,
+                         (uint32_t)((unsigned long long)p2 >> 32));
+    if (m2 != msg) reinterpret_cast<long long*>(xp + 1)[0] = m2;
   }
 }
 
@@ -2202,6 +2257,7 @@ struct BucketParams {
   const uint2* cmd_hdr;
   const uint4* cmd_hdr2;
   const zbhip_xpart_cmd* xout;
+  uint32_t xcap;
   uint32_t n;
   uint32_t parts;
   uint32_t* blk_cnt;     // [blocks][parts] -> exclusive offsets
@@ -2210,17 +2266,21 @@ struct BucketParams {
 };
 constexpr int kBucketB = 256;
 
-// The targets (1-based partition ids, 0 = none) of command c's sent entries, read once: the
-// bpmn_process_id/kind/interrupting word (bytes 36..39) and the source/target word (40..43).
+// The targets (1-based partition ids, 0 = none) of command c's sent entries.  The command header
+// summarises them (count and common target); only a command whose sends go to several partitions
+// has its outbox read: the bpmn_process_id/kind/interrupting word (bytes 36..39) and the
+// source/target word (40..43) of each entry.
 __device__ __forceinline__ void load_targets(const BucketParams& Q, uint32_t c, uint32_t (&tg)[kOut]) {
-  uint32_t nout = 0;
-  if (c < Q.n && ((Q.cmd_hdr[c].y >> 16) & 0xFF) == ST_OK) nout = min(Q.cmd_hdr2[c].z, (uint32_t)kOut);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(Q.xout + (size_t)c * kOut);
+  uint32_t z = 0;
+  if (c < Q.n && ((Q.cmd_hdr[c].y >> 16) & 0xFF) == ST_OK) z = Q.cmd_hdr2[c].z;
+  const uint32_t nout = min(z & 0xF, (uint32_t)kOut), nsend = (z >> 4) & 0xF, tgt = (z >> 8) & 0xFFFF;
+  const bool mixed = z >> 31;
 #pragma unroll
   for (int j = 0; j < kOut; ++j) {
-    tg[j] = 0;
-    if ((uint32_t)j < nout) {
-      const uint32_t kw = w[j * (sizeof(zbhip_xpart_cmd) / 4) + 9], tw = w[j * (sizeof(zbhip_xpart_cmd) / 4) + 10];
+    tg[j] = !mixed && (uint32_t)j < nsend ? tgt : 0u;
+    if (mixed && (uint32_t)j < nout) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(Q.xout + (size_t)j * Q.xcap + c);
+      const uint32_t kw = w[9], tw = w[10];
       if (((kw >> 16) & 0xFF) != XK_PATCH) tg[j] = (uint32_t)(int32_t)(int16_t)(tw >> 16);
     }
   }
@@ -2325,7 +2385,7 @@ __global__ __launch_bounds__(kBucketB) void k_bucket_scatter(BucketParams Q, con
       if (mine) {
 #pragma unroll
         for (int j = 0; j < kOut; ++j)
-          if (tg[j] == t + 1) Q.out[o++] = Q.xout[(size_t)c * kOut + j];
+          if (tg[j] == t + 1) Q.out[o++] = Q.xout[(size_t)j * Q.xcap + c];
       }
     }
   }
@@ -2491,9 +2551,9 @@ size_t step_lds_bytes(int variant, uint32_t prog_words) {
 
 hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uint4* cmds, uint32_t n,
                           unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
-                          zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s) {
+                          zbhip_xpart_cmd* xout, uint32_t xcap, const DevState& st, long long pbits, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  KeyScanParams K{cmd_hdr, cmd_hdr2, cmds, n, block_sum, base, counter, xout, st.pi_key, st.n,
+  KeyScanParams K{cmd_hdr, cmd_hdr2, cmds, n, block_sum, base, counter, xout, xcap, st.pi_key, st.n,
                   st.sub_a, st.sub_b, st.sub_k, st.n_slots, pbits};
   const uint32_t nb = (n + kScanB - 1) / kScanB;
   hipLaunchKernelGGL(k_key_block_sums, dim3(nb), dim3(kScanB), 0, s, K);
@@ -2515,9 +2575,10 @@ hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmd
   return hipGetLastError();
 }
 
-hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
-                         uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s) {
-  BucketParams Q{cmd_hdr, cmd_hdr2, xout, n, parts, blk_cnt, counts, out};
+hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t xcap,
+                         uint32_t n, uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out,
+                         hipStream_t s) {
+  BucketParams Q{cmd_hdr, cmd_hdr2, xout, xcap, n, parts, blk_cnt, counts, out};
   const uint32_t nb = (n + kBucketB - 1) / kBucketB;
   const uint32_t ng = (nb + kScanG - 1) / kScanG;
   uint32_t* grp = blk_cnt + (size_t)std::max(nb, 1u) * parts;  // [ng][parts] after the block counts

@@ -36,14 +36,15 @@ hipError_t launch_gather(const uint2* regions, const uint32_t* tot, const uint16
                          unsigned long long* total, hipStream_t s);
 hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uint4* cmds, uint32_t n,
                           unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
-                          zbhip_xpart_cmd* xout, const DevState& st, long long pbits, hipStream_t s);
+                          zbhip_xpart_cmd* xout, uint32_t xcap, const DevState& st, long long pbits, hipStream_t s);
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s);
 hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, hipStream_t s);
 size_t activated_out_bytes();
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
                                 uint32_t stamp, uint32_t* flag, hipStream_t s);
-hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t n,
-                         uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out, hipStream_t s);
+hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t xcap,
+                         uint32_t n, uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out,
+                         hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;
 constexpr size_t kBulkDrainMin = 1 << 16;  // records: below this the drain stays on the calling thread
 constexpr uint32_t kRegionPad = 0;  // regions for the extra workgroups of multi-round windows
@@ -1100,6 +1101,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     P.n_strs = (uint32_t)h->d_str_n;
     P.cmd_hdr2 = h->d_cmd_hdr2;
     P.xout = h->d_xout;
+    P.xcap = (uint32_t)h->cfg.max_commands;
     P.partition_id = h->cfg.partition_id;
     P.partition_count = std::max(1, h->cfg.partition_count);
   }
@@ -1221,7 +1223,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (h->msg()) {
     // keys of the window in log order: real process-instance keys, outbox and slot-row references
     HIPCHK(launch_keyscan(h->d_cmd_hdr, h->d_cmd_hdr2, P.cmds, n, h->d_key_blk, h->d_key_base, h->d_key_counter,
-                          h->d_xout, h->st, (long long)h->cfg.partition_id << 51, h->stream));
+                          h->d_xout, (uint32_t)h->cfg.max_commands, h->st, (long long)h->cfg.partition_id << 51,
+                          h->stream));
     h->bucketed = false;
     h->outbox_taken = false;
   }
@@ -1641,16 +1644,17 @@ int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_ou
   if (int rc = finalize(h)) return rc;
   const size_t n = h->n_cmds;
   h->h_xout.resize(n * kOut);
-  if (n) {
-    HIPCHK(hipMemcpyAsync(h->h_xout.data(), h->d_xout, n * kOut * sizeof(zbhip_xpart_cmd), hipMemcpyDeviceToHost,
-                          h->stream));
+  if (n) {  // entry-major on the device (entry j of command c at j * max_commands + c)
+    HIPCHK(hipMemcpy2DAsync(h->h_xout.data(), n * sizeof(zbhip_xpart_cmd), h->d_xout,
+                            (size_t)h->cfg.max_commands * sizeof(zbhip_xpart_cmd), n * sizeof(zbhip_xpart_cmd), kOut,
+                            hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
   }
   size_t k = 0;
   for (size_t c = 0; c < n; ++c) {
     if (((h->h_hdr[c].y >> 16) & 0xFF) != ST_OK) continue;
-    for (uint32_t j = 0; j < h->h_hdr2[c].z && j < (uint32_t)kOut; ++j) {
-      const zbhip_xpart_cmd& x = h->h_xout[c * kOut + j];
+    for (uint32_t j = 0; j < (h->h_hdr2[c].z & 0xF) && j < (uint32_t)kOut; ++j) {
+      const zbhip_xpart_cmd& x = h->h_xout[j * n + c];
       if (x.kind == XK_PATCH) continue;
       if (out && k < cap) out[k] = x;
       ++k;
@@ -1666,7 +1670,7 @@ int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32
   const uint32_t parts = (uint32_t)std::max(1, h->cfg.partition_count);
   if (parts > 1024) return ZBHIP_EINVAL;
   if (!h->bucketed) {
-    HIPCHK(launch_bucket(h->d_cmd_hdr, h->d_cmd_hdr2, h->d_xout, (uint32_t)h->n_cmds, parts, h->d_blk_cnt,
+    HIPCHK(launch_bucket(h->d_cmd_hdr, h->d_cmd_hdr2, h->d_xout, (uint32_t)h->cfg.max_commands, (uint32_t)h->n_cmds, parts, h->d_blk_cnt,
                          h->d_xcount, h->d_xbucket, h->stream));
     h->bucketed = true;
   }
@@ -1689,7 +1693,7 @@ int zbhip_outbox_device_async(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, 
   const uint32_t parts = (uint32_t)std::max(1, h->cfg.partition_count);
   if (parts > 1024) return ZBHIP_EINVAL;
   if (!h->bucketed) {
-    HIPCHK(launch_bucket(h->d_cmd_hdr, h->d_cmd_hdr2, h->d_xout, (uint32_t)h->n_cmds, parts, h->d_blk_cnt,
+    HIPCHK(launch_bucket(h->d_cmd_hdr, h->d_cmd_hdr2, h->d_xout, (uint32_t)h->cfg.max_commands, (uint32_t)h->n_cmds, parts, h->d_blk_cnt,
                          h->d_xcount, h->d_xbucket, h->stream));
     h->bucketed = true;
   }

@@ -166,7 +166,9 @@ struct StepParams {
   uint32_t n_strs;
   uint4* cmd_hdr2;            // [n_cmds] x = secondary instance, y = first ord | nkeys << 16 (secondary
                               // space), z = outbox entries, w = payload rows
-  zbhip_xpart_cmd* xout;      // [n_cmds * kOut]
+  zbhip_xpart_cmd* xout;      // [kOut][xcap]: entry j of command c at j * xcap + c (entry 0 of
+                              // consecutive commands contiguous: coalesced writes and reads)
+  uint32_t xcap;              // the outbox's command capacity (config.max_commands)
   int32_t partition_id, partition_count;
   uint32_t stamp;             // window stamp: hdr.w / slot_hdr.y of a subject whose command fell back
   uint32_t cmd_base;          // window index of cmds[0] (continuation launches of follow-up batches)
