@@ -13,7 +13,8 @@ import numpy as np
 from zeebe_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+# ORACLE_LIB selects another build of the same sources (scripts/sanitize.sh: the ASan build)
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 
 def build():
