@@ -410,6 +410,7 @@ def run_rank(args):
         step(first=(k == 0))
     ev1.record(pstream)
     s = part.stats()  # waits for the partition's stream
+    tpl_timed = s["template_batches"]
     torch.cuda.synchronize()
     span_ms = ev0.elapsed_time(ev1)  # device time of the timed region: the k_step launches back to back
     if dist:
@@ -469,6 +470,8 @@ def run_rank(args):
                    "instances_per_gpu": n, "windows_per_step": len(windows), "partitions": world,
                    "parallelism": "one partition per GPU (dp%d)" % world, "max_commands_in_batch": 100},
         "records_per_s": tot_recs / elapsed,
+        # CREATE batches copied from a template the general path recorded (kernels.hip tpl_create)
+        "template_batches_per_step": tpl_timed / max(1, args.steps),
         "roofline": {"bound": "hbm", "kernel": "k_step", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "bytes/launch",
                      "traffic_source": traffic_src, "algorithmic_bytes_per_launch": alg / launches,

@@ -381,6 +381,7 @@ typedef struct zbhip_stats {
   double compact_ms;            /* 0: record compaction is fused into the lifecycle kernel */
   uint32_t rounds;              /* per-instance serialisation rounds of the window */
   uint32_t launches;
+  uint64_t template_batches;    /* CREATE batches copied from a recorded template (kernels.hip tpl_create) */
 } zbhip_stats;
 int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out);
 

@@ -137,7 +137,7 @@ class Stats(C.Structure):
     _fields_ = [("commands", C.c_uint64), ("records", C.c_uint64), ("transitions", C.c_uint64),
                 ("completed_instances", C.c_uint64), ("keys", C.c_uint64), ("fallback", C.c_uint64),
                 ("step_ms", C.c_double), ("compact_ms", C.c_double), ("rounds", C.c_uint32),
-                ("launches", C.c_uint32)]
+                ("launches", C.c_uint32), ("template_batches", C.c_uint64)]
 
 
 COMMAND_DTYPE = np.dtype([("instance", "<u4"), ("kind", "u1"), ("doc_count", "u1"), ("ref", "<u2"),

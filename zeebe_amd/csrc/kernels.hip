@@ -1259,6 +1259,101 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
   return false;
 }
 
+// ---- CREATE batch templates (non-register variants) -------------------------------------------
+// A process whose CREATE batch never waits (runtime.cpp create_template_word: every element
+// reachable from the none start event is an event without wait state, a flow or a gateway; at most
+// one exclusive gateway, right behind the start event) completes the instance inside the batch, and
+// the batch's compact records depend only on the process, the name of the document's variable and
+// the flow that gateway takes: key ordinals restart at 0 for a CREATE, and variable values never
+// appear in the compact rows.  The first lane of a launch that runs such a batch through the general
+// path (BpmnStreamProcessor FIFO) records its rows as the template of (process, variant); from the
+// next launch on, a CREATE with the same variant only evaluates the gateway's condition and copies
+// the rows.  A template written in the running launch is never read in it (launch_seq), so no
+// fence is needed: launches are ordered by the stream.
+constexpr int kTplReplayed = 0x7FFF;
+
+template <class K>
+__device__ __forceinline__ uint2* tpl_at(const StepParams& P, uint32_t proc, uint32_t v) {
+  return P.tpl + ((size_t)proc * kTplVar + v) * kTplWords;
+}
+
+// -> kTplReplayed (the batch is in the lane), a variant to record after the general path, or -1
+template <class K>
+__device__ __forceinline__ int tpl_create(Lane<K>& L, uint32_t doc_count, uint32_t doc_begin, uint32_t& name) {
+  const StepParams& P = *L.sp;
+  const uint32_t tw = L.pb[7];
+  name = 0xFFFF;
+  if (!(tw & TPL_OK) || doc_count > 1 || L.limit <= 0 || L.limit > 0xFFFF || L.proc >= P.n_procs) return -1;
+  uint32_t v = 0;
+  const uint32_t gw = tw & 0xFFF;
+  if (doc_count == 1) {
+    const zbhip_doc_entry d = P.docs[doc_begin];
+    vm_drain();
+    name = d.name_id;
+    // the variable as set_local_variable puts it (process scope, key ordinal 1): the condition's input
+    L.vx0 = d.name_id;
+    L.vy0 = 1u | ((uint32_t)d.type << 16);
+    L.vv0 = d.value;
+    L.nvars = 1;
+  }
+  if (gw != 0xFFF) {
+    const uint4 w = elem_of(L, gw);
+    const uint32_t f = find_sequence_flow(L, w, NONE);  // ExclusiveGatewayProcessor.findSequenceFlowToTake
+    const uint32_t ob = w.y & 0xFFFF, oc = w.y >> 16;
+    v = kTplVar;
+    for (uint32_t i = 0; i < oc && i < (uint32_t)kTplVar; ++i)
+      if (out_flow(L, ob + i) == f) v = i;
+  }
+  L.nvars = 0;
+  L.vx0 = 0xFFFFFFFFu;
+  L.vy0 = 0;
+  L.vv0 = 0;
+  if (L.fail || v >= (uint32_t)kTplVar) {  // an incident or no flow: the general path decides
+    L.fail = 0;
+    return -1;
+  }
+  const uint2* t = tpl_at<K>(P, L.proc, v);
+  const uint4 hd = *reinterpret_cast<const uint4*>(t);
+  // hd.x = state (2 valid) | variable name << 16, hd.y = launch it was recorded in,
+  // hd.z = records | keys << 16, hd.w = transitions | batch limit << 16
+  const uint32_t n = hd.z & 0xFFFF;
+  if (hd.x != (2u | (name << 16)) || hd.y == P.launch_seq || (hd.w >> 16) != (uint32_t)L.limit || n > L.rec_cap ||
+      n > (uint32_t)kTplRec)
+    return (int)v;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint2 r = t[2 + j];
+    if (j < (uint32_t)K::R) L.stage[j * K::B] = r;
+    else L.rec[(size_t)j * K::B] = r;
+  }
+  L.nrec = n;
+  L.transitions = hd.w & 0xFFFF;
+  L.completed = 1;
+  L.next_ord = (uint16_t)(hd.z >> 16);
+  L.pi_live = false;
+  L.pi_state = ZBHIP_PI_ELEMENT_COMPLETING;
+  L.pi_child = L.pi_asf = 0;
+  L.nt = 0;
+  return kTplReplayed;
+}
+
+// after the general path: the batch's rows become the template of variant v, if it completed the
+// instance and nothing was left for later batches (no row written unprocessed)
+template <class K>
+__device__ __forceinline__ void tpl_record(Lane<K>& L, uint32_t v, uint32_t name) {
+  const StepParams& P = *L.sp;
+  if (L.fail || L.pi_live || !L.completed || L.nrec > (uint32_t)kTplRec || L.nrec > L.rec_cap) return;
+  uint2* t = tpl_at<K>(P, L.proc, v);
+  if (atomicCAS(reinterpret_cast<uint32_t*>(t), 0u, 1u) != 0u) return;  // recorded (or claimed) already
+  bool clean = true;
+  for (uint32_t j = 0; j < L.nrec; ++j) {
+    const uint2 r = j < (uint32_t)K::R ? L.stage[j * K::B] : L.rec[(size_t)j * K::B];
+    clean &= ((r.y >> 24) & F_UNPROCESSED) == 0;
+    t[2 + j] = r;
+  }
+  t[1] = make_uint2(L.nrec | ((uint32_t)L.next_ord << 16), L.transitions | ((uint32_t)L.limit << 16));
+  t[0] = make_uint2(clean ? 2u | (name << 16) : 3u, P.launch_seq);  // state and launch: one 8-byte store
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_step
 // ---------------------------------------------------------------------------------------------
@@ -1285,7 +1380,7 @@ __device__ __forceinline__ void load_rows(const StepParams& P, uint32_t ci, cons
 }
 
 struct Counters {
-  uint32_t rec, trans, comp, keys, fb, cmd;
+  uint32_t rec, trans, comp, keys, fb, cmd, tpl;
 };
 
 
@@ -1634,6 +1729,19 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   // the FIFO; anything outside the canonical states takes the general path below
   bool fast = false;
   if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
+  int tpl_v = -1;
+  uint32_t tpl_name = 0xFFFF;
+  bool tpl_hit = false;
+  if constexpr (!K::REG && !K::M) {
+    if (P.tpl && !L.fail && kind == ZBHIP_CMD_CREATE && L.proc != NONE) {
+      tpl_v = tpl_create(L, doc_count, doc_begin, tpl_name);
+      if (tpl_v == kTplReplayed) {
+        fast = true;
+        tpl_v = -1;
+        tpl_hit = true;
+      }
+    }
+  }
   if (fast) {
 #ifdef ZB_EXP_FASTONLY  // diagnostic build: the general path compiled out (its commands fall back)
   } else if (K::REG) {
@@ -1710,6 +1818,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
 #endif
   }
   ZB_RSTAMP(r3);
+  if constexpr (!K::REG && !K::M) {
+    if (tpl_v >= 0) tpl_record(L, (uint32_t)tpl_v, tpl_name);
+  }
 
   retire();  // the caller's prefetch loads: retired before the first store of the commit
   // ---- commit: write back the instance (or leave it untouched on fallback) ----
@@ -1792,6 +1903,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
                                  (ended ? HDR_ENDED : 0u));
   acc.cmd += 1;
   acc.fb += ok ? 0u : 1u;
+  acc.tpl += tpl_hit && ok ? 1u : 0u;
 #ifdef ZB_STAMPS
   {
     ZB_RSTAMP(r4);
@@ -1844,7 +1956,7 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
   const uint32_t n_chunks = (P.n_launch + K::B - 1) / K::B;
   const uint32_t G = gridDim.x;
   const uint32_t lane = threadIdx.x & 63;
-  Counters acc = {0, 0, 0, 0, 0, 0};
+  Counters acc = {0, 0, 0, 0, 0, 0, 0};
 
   // the first commands are requested before the program is staged, so the two latencies overlap
   // (the chain program -> command -> instance rows becomes max(program, command) -> rows)
@@ -1989,14 +2101,16 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
     acc.keys += __shfl_xor(acc.keys, off);
     acc.fb += __shfl_xor(acc.fb, off);
     acc.cmd += __shfl_xor(acc.cmd, off);
+    acc.tpl += __shfl_xor(acc.tpl, off);
   }
   __shared__ uint32_t wstat[K::B / 64][8];
   if (lane == 0) {
     uint32_t* w = wstat[threadIdx.x >> 6];
     w[0] = acc.rec; w[1] = acc.trans; w[2] = acc.comp; w[3] = acc.keys; w[4] = acc.fb; w[5] = acc.cmd;
+    w[6] = acc.tpl;
   }
   __syncthreads();
-  if (threadIdx.x < 6) {
+  if (threadIdx.x < 7) {
     uint32_t sum = 0;
 #pragma unroll
     for (int w = 0; w < K::B / 64; ++w) sum += wstat[w][threadIdx.x];

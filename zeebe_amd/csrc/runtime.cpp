@@ -145,6 +145,9 @@ struct zbhip_handle {
   std::vector<uint32_t> prog;
   uint32_t* d_prog = nullptr;
   size_t d_prog_cap = 0;
+  uint2* d_tpl = nullptr;        // CREATE batch templates [procs][kTplVar][kTplWords] (kernels.hip)
+  size_t tpl_procs = 0;          // processes the template table holds
+  uint32_t launch_seq = 0;       // k_step launches so far (StepParams.launch_seq)
 
   std::vector<std::string> names;
   std::unordered_map<std::string, uint32_t> name_ids;
@@ -467,6 +470,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_cont);
   (void)hipFree(h->d_cont_order);
   (void)hipFree(h->d_qspill);
+  (void)hipFree(h->d_tpl);
   (void)hipFree(h->d_check_flag);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
@@ -536,6 +540,55 @@ static uint64_t batch_bound(const Proc& P) {
 }
 
 // Builds the LDS program arena from every deployed process (layout: zb_internal.h).
+// CREATE batch templates (kernels.hip tpl_create): the template word of a process whose CREATE
+// batch never waits -- every element reachable from the none start event is a none start or end
+// event, a sequence flow or a gateway -- so the batch completes the instance, and whose rows
+// depend on at most one decision: one exclusive gateway, entered only from the start event's one
+// flow (one token reaches it, once).  Anything else: 0 (no template, the general path as always).
+static uint32_t create_template_word(const Proc& P) {
+  const uint32_t n_el = (uint32_t)P.els.size();
+  if (P.none_start == NONE || P.none_start >= n_el) return 0;
+  std::vector<char> seen(n_el, 0);
+  std::vector<uint32_t> todo{P.none_start};
+  uint32_t xgw = 0xFFF, n_xgw = 0;
+  while (!todo.empty()) {
+    const uint32_t e = todo.back();
+    todo.pop_back();
+    if (e >= n_el) return 0;
+    if (seen[e]) continue;
+    seen[e] = 1;
+    const zbhip_element& E = P.els[e];
+    switch (E.element_type) {
+      case ZBHIP_EL_SEQUENCE_FLOW:
+        todo.push_back(E.flow_target);
+        continue;
+      case ZBHIP_EL_START_EVENT:
+        if (E.event_type != ZBHIP_EV_NONE) return 0;
+        break;
+      case ZBHIP_EL_END_EVENT:
+        if (E.event_type != ZBHIP_EV_NONE || E.out_count) return 0;
+        break;
+      case ZBHIP_EL_PARALLEL_GATEWAY:
+        break;
+      case ZBHIP_EL_EXCLUSIVE_GATEWAY:
+        ++n_xgw;
+        xgw = e;
+        break;
+      default:
+        return 0;  // a wait state (task, catch event) or an element outside the subset
+    }
+    for (uint32_t i = 0; i < E.out_count; ++i) todo.push_back(P.out[E.out_begin + i]);
+  }
+  if (n_xgw > 1) return 0;
+  if (n_xgw == 1) {
+    const zbhip_element& S = P.els[P.none_start];
+    if (S.out_count != 1 || xgw >= 0xFFF || P.els[xgw].in_count != 1) return 0;
+    const uint32_t f = P.out[S.out_begin];
+    if (f >= n_el || P.els[f].flow_target != xgw) return 0;
+  }
+  return TPL_OK | xgw;
+}
+
 static int rebuild_program(zbhip_handle* h) {
   std::vector<uint32_t> prog(1 + h->procs.size(), 0);
   prog[0] = (uint32_t)h->procs.size();
@@ -560,6 +613,7 @@ static int rebuild_program(zbhip_handle* h) {
     pb[4] = code_off;
     pb[5] = P.bpmn_name;  // name id of the bpmnProcessId (message records)
     pb[6] = seg_off;
+    pb[7] = create_template_word(P);
     // straight-line segment words (kernels.hip fast_command): a start event or service task with
     // one unconditional outgoing flow into a service task or a none end event without outgoing flows
     for (uint32_t e = 0; e < n_el; ++e) {
@@ -610,6 +664,17 @@ static int rebuild_program(zbhip_handle* h) {
     h->d_prog = nullptr;
     if (dalloc(&h->d_prog, prog.size()) != hipSuccess) return ZBHIP_ENOMEM;
     h->d_prog_cap = prog.size();
+  }
+  if (h->procs.size() > h->tpl_procs && h->variant != 2 && h->variant != 3) {
+    // a larger template table (templates are relearned: the next launches record them again)
+    (void)hipFree(h->d_tpl);
+    h->d_tpl = nullptr;
+    h->tpl_procs = 0;
+    const size_t cap = std::max<size_t>(16, h->procs.size() * 2);
+    const size_t words = cap * kTplVar * kTplWords;
+    if (dalloc(&h->d_tpl, words) != hipSuccess) return ZBHIP_ENOMEM;
+    HIPCHK(hipMemsetAsync(h->d_tpl, 0, words * sizeof(uint2), h->stream));
+    h->tpl_procs = cap;
   }
   HIPCHK(hipMemcpyAsync(h->d_prog, prog.data(), prog.size() * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1092,6 +1157,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.stats = h->d_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
   P.stamp = h->window_stamp;
+  P.tpl = (h->variant == 0 || h->variant == 1) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
   if (h->msg()) {
     int rc = sync_strings(h);
     if (rc) return rc;
@@ -1154,6 +1220,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     P.order = l.src == 0 ? nullptr : h->d_order + l.first;
     P.n_launch = l.count;
     P.region_base = l.region;
+    P.launch_seq = ++h->launch_seq;
     HIPCHK(launch_step(h->variant, P, h->stream));
   }
   // continuation: the follow-up commands written to the log unprocessed become batches of their
@@ -1215,6 +1282,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
       P.order = h->d_cont_order + h->launches[l].first;
       P.n_launch = h->launches[l].count;
       P.region_base = h->launches[l].region;
+      P.launch_seq = ++h->launch_seq;
       HIPCHK(launch_step(h->variant, P, h->stream));
     }
     n_all += (uint32_t)ov.size();
@@ -1326,6 +1394,7 @@ int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
     h->stats.keys = c[3];
     h->stats.fallback = c[4];
     h->stats.commands = c[5];
+    h->stats.template_batches = c[6];
     double ms = 0;
     for (size_t i = 0; i + 1 < h->tev_used; i += 2) {
       float a = 0;

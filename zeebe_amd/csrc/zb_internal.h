@@ -19,6 +19,12 @@ constexpr uint16_t NONE = 0xFFFF;
 
 // ---- message correlation (config 5; kernel variant KMsg) ----
 constexpr int kSubs = 4;           // message-subscription rows per correlation slot (HBM)
+// CREATE batch templates (kernels.hip tpl_create): per process kTplVar variants (the outcome of
+// its one exclusive gateway), each a header (2 uint2) and up to kTplRec compact records
+constexpr int kTplVar = 4;
+constexpr int kTplRec = 126;
+constexpr uint32_t kTplWords = kTplRec + 2;  // uint2 per variant
+constexpr uint32_t TPL_OK = 1u << 31;        // program header word 7: bit 31 eligible, bits 0..11 gateway
 constexpr int kOut = 6;            // outbox entries per command (sends + local-row key patches)
 constexpr uint8_t XK_PATCH = 0xFF; // outbox entry kind: patch the real keys of a locally inserted row
 constexpr uint32_t kNoElem = 0xFFF;       // element field of records without an element
@@ -101,7 +107,7 @@ constexpr uint8_t CMD_FOLLOWUP = 0x20;
 //   p[0] = n_elements | none_start << 16
 //   p[1] = n_join_slots | n_conditions << 16
 //   p[2] = out_off, p[3] = cond_off, p[4] = code_off (words, relative to p), p[5] = bpmnProcessId
-//   name id, p[6] = seg_off, p[7] = 0
+//   name id, p[6] = seg_off, p[7] = CREATE template word (TPL_OK | exclusive gateway or 0xFFF; 0 = none)
 //   p[8 + 4e .. ] element e: w0 = type | event << 8 | in_count << 16
 //                            w1 = out_begin | out_count << 16
 //                            w2 = flow: target | condition << 16; xgw: default_flow; task: job_type | retries << 16
@@ -181,6 +187,10 @@ struct StepParams {
   uint4* ovf;
   uint32_t* ovf_count;
   uint32_t ovf_cap;
+  // CREATE batch templates [n_procs][kTplVar][kTplWords] (null: off) and this launch's sequence
+  // number (a template recorded in the running launch is not used before the next one)
+  uint2* tpl;
+  uint32_t launch_seq;
 };
 
 }  // namespace zb
