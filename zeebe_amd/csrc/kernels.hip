@@ -1276,10 +1276,17 @@ template <class K>
 __device__ __forceinline__ uint2* tpl_at(const StepParams& P, uint32_t proc, uint32_t v) {
   return P.tpl + ((size_t)proc * kTplVar + v) * kTplWords;
 }
+template <class K>
+constexpr bool kTplOn = !K::REG && !K::M;
+template <class K>
+constexpr size_t tpl_lds_bytes() {
+  return kTplOn<K> ? (size_t)kTplLdsProcs * kTplVar * kTplLdsWords * sizeof(uint2) : 0;
+}
 
 // -> kTplReplayed (the batch is in the lane), a variant to record after the general path, or -1
 template <class K>
-__device__ __forceinline__ int tpl_create(Lane<K>& L, uint32_t doc_count, uint32_t doc_begin, uint32_t& name) {
+__device__ __forceinline__ int tpl_create(Lane<K>& L, uint32_t doc_count, uint32_t doc_begin, uint32_t& name,
+                                          const uint2* tpl_lds) {
   const StepParams& P = *L.sp;
   const uint32_t tw = L.pb[7];
   name = 0xFFFF;
@@ -1312,16 +1319,21 @@ __device__ __forceinline__ int tpl_create(Lane<K>& L, uint32_t doc_count, uint32
     L.fail = 0;
     return -1;
   }
+  // the workgroup's LDS copy (taken at kernel start: templates of earlier launches, complete) for
+  // the first processes, HBM otherwise or for rows past the copy
+  const bool in_lds = L.proc < (uint32_t)kTplLdsProcs;
+  const uint2* tl = tpl_lds + ((size_t)L.proc * kTplVar + v) * kTplLdsWords;
   const uint2* t = tpl_at<K>(P, L.proc, v);
-  const uint4 hd = *reinterpret_cast<const uint4*>(t);
+  const uint4 hd = *reinterpret_cast<const uint4*>(in_lds ? tl : t);
   // hd.x = state (2 valid) | variable name << 16, hd.y = launch it was recorded in,
   // hd.z = records | keys << 16, hd.w = transitions | batch limit << 16
   const uint32_t n = hd.z & 0xFFFF;
   if (hd.x != (2u | (name << 16)) || hd.y == P.launch_seq || (hd.w >> 16) != (uint32_t)L.limit || n > L.rec_cap ||
       n > (uint32_t)kTplRec)
     return (int)v;
+  const uint2* rows = in_lds && n + 2 <= kTplLdsWords ? tl : t;
   for (uint32_t j = 0; j < n; ++j) {
-    const uint2 r = t[2 + j];
+    const uint2 r = rows[2 + j];
     if (j < (uint32_t)K::R) L.stage[j * K::B] = r;
     else L.rec[(size_t)j * K::B] = r;
   }
@@ -1369,7 +1381,9 @@ __device__ __forceinline__ uint32_t cmd_index(const StepParams& P, uint32_t chun
 __device__ __forceinline__ uint4 load_cmd(const StepParams& P, uint32_t ci) {
   return ci != kNoCmd ? P.cmds[ci - P.cmd_base] : make_uint4(0, 0, 0, 0);
 }
-// header row, and the first element-instance slot of a waiting instance (a CREATE reads none)
+// header row, and the first element-instance slot of a waiting instance (a CREATE reads none).
+// (Prefetching a CREATE's document entry here too was measured: -11 % on configs[2], the wider
+// pipeline registers cost more than the dependent load they save.)
 __device__ __forceinline__ void load_rows(const StepParams& P, uint32_t ci, const uint4& cw, uint4& h, uint2& s0) {
   h = make_uint4(0xFFFFFFFFu, 0, 0, 0);
   s0 = make_uint2(0xFFFFFFFFu, 0);
@@ -1562,7 +1576,8 @@ __device__ unsigned long long g_stamps_run[8];
 template <class K, class Retire>
 __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint32_t* prog, uint2* tbl_base,
                                                 uint2* stage_base, uint32_t* q_base, uint2* region, uint32_t ci,
-                                                uint4 cw, uint4 h, uint2 s0, Counters& acc, const Retire& retire) {
+                                                uint4 cw, uint4 h, uint2 s0, Counters& acc, const Retire& retire,
+                                                const uint2* tpl_lds) {
   const uint32_t inst = cw.x;
   const uint32_t kind = cw.y & 0xFF;
   const uint32_t doc_count = (cw.y >> 8) & 0xFF;
@@ -1734,7 +1749,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   bool tpl_hit = false;
   if constexpr (!K::REG && !K::M) {
     if (P.tpl && !L.fail && kind == ZBHIP_CMD_CREATE && L.proc != NONE) {
-      tpl_v = tpl_create(L, doc_count, doc_begin, tpl_name);
+      tpl_v = tpl_create(L, doc_count, doc_begin, tpl_name, tpl_lds);
       if (tpl_v == kTplReplayed) {
         fast = true;
         tpl_v = -1;
@@ -1967,6 +1982,15 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
   uint4 cw2 = load_cmd(P, ci2);
   uint32_t ci3 = cmd_index<K>(P, c + 2 * G);
   for (uint32_t i = threadIdx.x; i < P.prog_words; i += K::B) prog[i] = P.prog[i];
+  // CREATE templates of the first processes (after the FIFO; alias nothing)
+  uint2* tpl_lds = reinterpret_cast<uint2*>(q_base + (K::REG ? 0 : K::Q * K::B));
+  if constexpr (kTplOn<K>) {
+    constexpr uint32_t words = (uint32_t)kTplLdsProcs * kTplVar * kTplLdsWords;
+    for (uint32_t i = threadIdx.x; i < words; i += K::B) {
+      const uint32_t pv = i / kTplLdsWords, w = i % kTplLdsWords;
+      tpl_lds[i] = P.tpl && pv / kTplVar < P.n_procs ? P.tpl[(size_t)pv * kTplWords + w] : make_uint2(0, 0);
+    }
+  }
   uint4 h1;
   uint2 s1;
   load_rows(P, ci1, cw1, h1, s1);
@@ -1998,7 +2022,7 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
     // them in the vmcnt queue.
     const auto retire = [&]() { consume(h1); consume(s1); consume(cw2); consume(ci3); };
     if (ci != kNoCmd)
-      my_nrec = run_command<K>(P, prog, tbl_base, stage_base, q_base, out, ci, cw, h, s0, acc, retire);
+      my_nrec = run_command<K>(P, prog, tbl_base, stage_base, q_base, out, ci, cw, h, s0, acc, retire, tpl_lds);
     else retire();
     ZB_STAMP(t2);
 
@@ -2584,7 +2608,7 @@ static size_t lds_bytes(uint32_t prog_words) {
     return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::B * 4 +
            (((size_t)K::B * K::R + 3) & ~(size_t)3);
   return (size_t)((prog_words + 3) & ~3u) * 4 + (size_t)K::T * K::B * sizeof(uint2) +
-         (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t);
+         (size_t)K::R * K::B * sizeof(uint2) + (size_t)K::Q * K::B * sizeof(uint32_t) + tpl_lds_bytes<K>();
 }
 
 static int env_int(const char* name, int dflt) {

@@ -24,6 +24,10 @@ constexpr int kSubs = 4;           // message-subscription rows per correlation 
 constexpr int kTplVar = 4;
 constexpr int kTplRec = 126;
 constexpr uint32_t kTplWords = kTplRec + 2;  // uint2 per variant
+// the templates of processes 0 .. kTplLdsProcs-1 (their first kTplLdsWords words) are staged in LDS
+// by every workgroup at kernel start
+constexpr int kTplLdsProcs = 2;
+constexpr uint32_t kTplLdsWords = 64;
 constexpr uint32_t TPL_OK = 1u << 31;        // program header word 7: bit 31 eligible, bits 0..11 gateway
 constexpr int kOut = 6;            // outbox entries per command (sends + local-row key patches)
 constexpr uint8_t XK_PATCH = 0xFF; // outbox entry kind: patch the real keys of a locally inserted row
