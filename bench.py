@@ -195,6 +195,14 @@ def run_msg(args, world, rank, local_rank, dist):
     rows = sum(s["records"] for s in st) / max(1, n * P)
     alg_per_inst = 16 * 6 + 8 * (rows + 6 * 10) + 2 * 40 * 3 + 2 * 48 * 3 + 4 * 48 * 4
     alg = alg_per_inst * n * P
+    # HBM traffic per step of the config-5 kernels (k_step, key scan, bucketing) from the PMC passes
+    # of this build (scripts/evidence.sh: pmc_traffic.py "zb::" <steps>); null without a summary
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "pmc_%s.json" % ("msg" if vp == 1 else "msg%d" % vp))
+    if os.path.exists(tpath) and not args.instances and world == 1:
+        with open(tpath) as f:
+            traffic = json.load(f).get("traffic_bytes_per_step")
+        traffic_src = os.path.relpath(tpath, ROOT)
     result = {
         "metric": "BPMN element transitions/sec + completed instances/sec, 1/2/4/8 MI355X",
         "value": tr / elapsed,
@@ -217,7 +225,9 @@ def run_msg(args, world, rank, local_rank, dist):
         "setup_s": setup_s,
         "roofline": {"bound": "hbm", "kernel": "k_step<KMsg> + key scan", "achieved": alg / (dev_ms * 1e-3) / 1e9 / world,
                      "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": alg / (dev_ms * 1e-3) / 1e9 / world / PEAK_HBM_GBPS,
-                     "traffic": None, "algorithmic_bytes_per_instance": alg_per_inst, "device_ms_per_step": dev_ms},
+                     "traffic": traffic, "traffic_unit": "bytes/step (all zb:: kernels)", "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_step": alg, "algorithmic_bytes_per_instance": alg_per_inst,
+                     "device_ms_per_step": dev_ms},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle import bench_msg
