@@ -495,6 +495,19 @@ typedef struct zbhip_log_window {
 int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n, const zbhip_log_window* w,
                         uint8_t* out, size_t cap, size_t* used);
 
+/* Device form (configs 1-4): after zbhip_run with results, every record of the window serialised
+ * into device memory (owned by the handle, valid until the next call) -- the same bytes as
+ * zbhip_drain + zbhip_serialize_log(zbhip_handle_serializer(h), ...) with this window description
+ * (w->cmds / w->docs / bases are taken from the handle; w->source_positions, first_position,
+ * timestamp are used).  Keys are relabelled on the device: ordinals of the batch from its key base,
+ * older ones from a per-instance ring of the last 16 ordinals in HBM, which holds every key only if
+ * every window of the handle comes through here.  ZBHIP_EUNSUPP (use the host serialiser for this
+ * window and the later ones): message partitions, continuation batches, imported state, string
+ * variables, a key older than the ring, or a window that skipped this call. */
+int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_window* w, const void** dev_bytes, size_t* used);
+/* Copies n bytes of the last zbhip_serialize_log_device output into host memory. */
+int zbhip_log_device_copy(zbhip_handle* h, void* dst, size_t n);
+
 /* ---- zb-db byte encoding of the state ---------------------------------------
  * The partition state as RocksDB entries: key = 8-byte big-endian ZbColumnFamilies ordinal +
  * DbLong / DbString / DbInt parts, value = DbNil / DbLong / DbInt or the msgpack of the state

@@ -1,0 +1,125 @@
+"""Log bytes written on the device (zbhip_serialize_log_device, logdev.hip): for every window, the
+bytes equal the host serialiser's (zbhip_serialize_log over the drained records -- itself equal to
+the oracle's, tests/test_gpu_logserial.py) byte for byte: frames, LogEntryDescriptor headers, SBE
+RecordMetadata with rejection texts, msgpack values with documents; keys relabelled on the device
+(batch key bases, the previous command of the instance in the window, the per-instance key ring).
+
+SequencedBatchSerializer.java:33-67, LogAppendEntrySerializer.java:40-111, protocol.xml:137-152."""
+import numpy as np
+import pytest
+
+from helpers import amount_docs, create_commands
+from zeebe_amd import abi, bpmn
+from zeebe_amd.engine import Partition
+from zeebe_amd.native import ZbhipError
+
+pytestmark = pytest.mark.gpu
+
+TS = 1700000000123
+
+
+class Log:
+    def __init__(self, xml, n, names=(), max_records=128, **kw):
+        self.part = Partition(max_instances=n, max_commands=16 * n, max_records_per_batch=max_records, **kw)
+        assert self.part.deploy(xml) == 0
+        self.names = [self.part.intern(x) for x in names]
+        self.ser = self.part.log_serializer()
+        self.source_base = self.doc_base = 0
+        self.position = 100
+        self.windows = 0
+
+    def window(self, cmds, docs=None, device=True):
+        docs = docs if docs is not None else abi.make_docs(0)
+        self.part.submit(cmds, docs)
+        self.part.run()
+        pos = self.position + 2 * np.arange(len(cmds), dtype=np.int64)
+        first = int(pos[-1]) + 1 if len(cmds) else self.position
+        dev = self.part.serialize_log_device(pos, first, TS) if device else None
+        recs = self.part.drain()
+        host = self.ser.serialize(recs, cmds, docs, self.source_base, self.doc_base, pos, first, TS)
+        if device:
+            assert len(dev) == len(host)
+            if dev != host:
+                bad = next(i for i in range(len(host)) if dev[i] != host[i])
+                raise AssertionError("byte %d of %d differs: device %r host %r" % (bad, len(host), dev[bad - 8:bad + 24],
+                                                                                 host[bad - 8:bad + 24]))
+        self.source_base += len(cmds)
+        self.doc_base += len(docs)
+        self.position = first + len(recs)
+        self.windows += 1
+        return recs
+
+
+def job_completions(recs, part, rng=None, limit=None):
+    jobs = [int(r["key"]) for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+    if rng is not None:
+        rng.shuffle(jobs)
+    jobs = jobs[:limit] if limit else jobs
+    c = abi.make_commands(len(jobs))
+    for i, k in enumerate(jobs):
+        c[i]["instance"], c[i]["ref"] = part.resolve_key(k)
+    c["kind"] = abi.CMD_JOB_COMPLETE
+    return c
+
+
+@pytest.mark.parametrize("tasks", [1, 5])
+def test_linear_windows(tasks):
+    n = 300
+    log = Log(bpmn.linear_process(tasks), n)
+    recs = log.window(create_commands(n))
+    for _ in range(tasks):
+        recs = log.window(job_completions(recs, log.part))
+    assert log.windows == tasks + 1
+
+
+def test_exclusive_gateway_documents():
+    # int, decimal, bool and nil values, both outcomes, and the template path on later windows
+    n = 256
+    log = Log(bpmn.xor_process(), n, names=("amount",))
+    rng = np.random.default_rng(3)
+    for w in range(4):
+        c = create_commands(n)
+        c["doc_count"] = 1
+        c["doc_begin"] = np.arange(n)
+        if w == 0:
+            d = amount_docs(rng.integers(0, 2000, n), log.names[0])
+        elif w == 1:
+            d = amount_docs(rng.integers(0, 200000, n) / 100.0, log.names[0], decimal=True)
+        else:
+            d = amount_docs(rng.integers(-5000, 5000000000, n), log.names[0])
+        log.window(c, d)
+
+
+def test_fork_join_rejections_and_tasks():
+    # join rejections (reason texts with element ids); branch tasks completed in random order, several
+    # jobs of an instance in one window (rounds: the previous-command chain)
+    n = 64
+    log = Log(bpmn.fork_join_process(8), n)
+    for _ in range(3):
+        log.window(create_commands(n))
+    log2 = Log(bpmn.fork_join_process(4, tasks=True), n)
+    recs = log2.window(create_commands(n))
+    rng = np.random.default_rng(9)
+    for _ in range(6):
+        c = job_completions(recs, log2.part, rng)
+        if len(c) == 0:
+            break
+        recs = log2.window(c)
+
+
+def test_stale_job_complete_rejection():
+    # JOB:COMPLETE of a job completed in an earlier window: NOT_FOUND rejection with the job key
+    n = 32
+    log = Log(bpmn.linear_process(2), n)
+    recs = log.window(create_commands(n))
+    c = job_completions(recs, log.part)
+    log.window(c)
+    log.window(c)  # the same commands again: every one rejected
+
+
+def test_a_skipped_window_turns_the_device_path_off():
+    n = 16
+    log = Log(bpmn.linear_process(2), n)
+    recs = log.window(create_commands(n), device=False)
+    with pytest.raises(ZbhipError, match="EUNSUPP"):
+        log.window(job_completions(recs, log.part))

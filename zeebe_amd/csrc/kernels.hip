@@ -1349,12 +1349,23 @@ __device__ __forceinline__ int tpl_create(Lane<K>& L, uint32_t doc_count, uint32
 }
 
 // after the general path: the batch's rows become the template of variant v, if it completed the
-// instance and nothing was left for later batches (no row written unprocessed)
+// instance and nothing was left for later batches (no row written unprocessed).  At most one lane
+// per wave and chunk tries, and a workgroup tries a template once (its LDS copy's header marks the
+// attempt): a first window of 10^7 CREATEs would otherwise send 10^7 CAS to one address (measured:
+// the recording launch 20x slower than a replaying one).
 template <class K>
-__device__ __forceinline__ void tpl_record(Lane<K>& L, uint32_t v, uint32_t name) {
+__device__ __forceinline__ void tpl_record(Lane<K>& L, uint32_t v, uint32_t name, uint2* tpl_lds) {
   const StepParams& P = *L.sp;
-  if (L.fail || L.pi_live || !L.completed || L.nrec > (uint32_t)kTplRec || L.nrec > L.rec_cap) return;
+  const bool want = !(L.fail || L.pi_live || !L.completed || L.nrec > (uint32_t)kTplRec || L.nrec > L.rec_cap);
+  const unsigned long long m = __ballot(want);
+  if (!want || (threadIdx.x & 63) != (uint32_t)__builtin_ctzll(m)) return;
+  if (L.proc < (uint32_t)kTplLdsProcs) {
+    uint2* tl = tpl_lds + ((size_t)L.proc * kTplVar + v) * kTplLdsWords;
+    if (tl[0].x != 0) return;  // this workgroup saw it recorded, or tried already
+    tl[0].x = 1;
+  }
   uint2* t = tpl_at<K>(P, L.proc, v);
+  if (*reinterpret_cast<volatile uint32_t*>(t) != 0u) return;
   if (atomicCAS(reinterpret_cast<uint32_t*>(t), 0u, 1u) != 0u) return;  // recorded (or claimed) already
   bool clean = true;
   for (uint32_t j = 0; j < L.nrec; ++j) {
@@ -1577,7 +1588,7 @@ template <class K, class Retire>
 __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint32_t* prog, uint2* tbl_base,
                                                 uint2* stage_base, uint32_t* q_base, uint2* region, uint32_t ci,
                                                 uint4 cw, uint4 h, uint2 s0, Counters& acc, const Retire& retire,
-                                                const uint2* tpl_lds) {
+                                                uint2* tpl_lds) {
   const uint32_t inst = cw.x;
   const uint32_t kind = cw.y & 0xFF;
   const uint32_t doc_count = (cw.y >> 8) & 0xFF;
@@ -1834,7 +1845,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   }
   ZB_RSTAMP(r3);
   if constexpr (!K::REG && !K::M) {
-    if (tpl_v >= 0) tpl_record(L, (uint32_t)tpl_v, tpl_name);
+    if (tpl_v >= 0) tpl_record(L, (uint32_t)tpl_v, tpl_name, tpl_lds);
   }
 
   retire();  // the caller's prefetch loads: retired before the first store of the commit

@@ -1,0 +1,542 @@
+// Log bytes on the device: the window's compact records -> the bytes the reference's log stream
+// holds for them, written into HBM.  The same format as the host serialiser (logwriter.cpp:
+// SequencedBatchSerializer.java:33-67, LogAppendEntrySerializer.java:40-111, LogEntryDescriptor,
+// RecordMetadata + protocol.xml:137-152, MsgPackWriter.java:62-316, the record values of
+// ProcessInstanceRecord / JobRecord / VariableRecord / ProcessEventRecord /
+// ProcessInstanceCreationRecord) for configs 1-4; the host builds the constant byte runs at deploy
+// time (zb::log_device_tables) and the per-command table of the window (key base, positions).
+//
+// Keys.  A record names keys by (instance, ordinal).  Ordinals of the command's own batch resolve
+// from its key base; older ordinals from an earlier command of the same instance in this window
+// (`prev` chain) or from the instance's key ring in HBM: the last kRing ordinals of every instance,
+// each entry tagged with its ordinal (ordinal << 48 | key counter), filled after each window, plus
+// the process-instance key (ordinal 0).  An ordinal the ring no longer holds flags the window, and
+// the host serialiser takes it instead.
+//
+// Passes: k_log_sizes (one thread per command: entry sizes) -> u64 scan over commands -> k_log_write
+// (one thread per command writes its entries, 8-byte stores) -> k_ring_fill (CREATEs reset their
+// instance's ring, then every command adds its ordinals).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "zb_internal.h"
+
+namespace zb {
+
+constexpr uint32_t kRing = 16;
+
+// global byte runs of the device tables (logwriter.cpp log_device_tables builds them in this order)
+enum LogRun : uint32_t {
+  G_AUTH, G_TENANT, G_FLOWSCOPE, G_EMPTY_BIN, G_JREJ_HEAD, G_JREJ_TAIL, G_VAR_A, G_VAR_VALUE, G_VAR_SCOPE,
+  G_K_PIK, G_K_DEF, G_K_BPMN, G_PE_A, G_PE_TARGET, G_K_VARS, G_PIC_A, G_K_VERSION, G_PIC_TAIL,
+  G_RS_PGW_A, G_RS_PGW_B, G_RS_FSNF_A, G_RS_NF_B, G_RS_FSST_A, G_RS_Q, G_RS_EINF_A, G_RS_EIST_A, G_RS_JOB_A,
+  G_RS_JOB_B, G_ST0, G_COUNT = G_ST0 + 16
+};
+// element runs (proc block word 6 + 14 e)
+enum ElRun : uint32_t { E_PI_HEAD, E_PI_TAIL, E_JOB_HEAD, E_JOB_MID, E_JOB_TAIL, E_ID_STR, E_ID_RAW, E_COUNT };
+
+struct LogParams {
+  const uint2* rows;            // gathered compact rows (launch order)
+  const LogCmd* cmds;           // [n]
+  uint32_t n;
+  const uint8_t* arena;         // byte runs, each 4-aligned
+  const uint32_t* idx;          // run table (see log_device_tables)
+  const zbhip_doc_entry* docs;  // the window's document entries
+  uint32_t n_docs;
+  const uint16_t* inst_proc;    // [n_inst] process of each instance slot (NONE: free)
+  unsigned long long* ring;     // [kRing][n_inst]
+  unsigned long long* kpi;      // [n_inst] bit 63 | key counter of ordinal 0
+  uint32_t n_inst;
+  long long pbits;              // partition_id << 51
+  long long first_position, timestamp;
+  int32_t broker[3];
+  unsigned long long* bytes;    // [n] entry bytes of each command, then (scanned) byte offsets
+  uint64_t* out;                // log bytes (8-byte aligned entries)
+  uint32_t* flag;               // bit 0: an unresolved key / unsupported value (host serialiser instead)
+};
+
+__device__ __forceinline__ uint2 run(const LogParams& L, uint32_t i) {
+  return make_uint2(L.idx[2 * i], L.idx[2 * i + 1]);
+}
+__device__ __forceinline__ uint32_t proc_block(const LogParams& L, uint32_t p) {
+  const uint32_t p0 = 2 * G_COUNT + 1 + 2 * L.idx[2 * G_COUNT];
+  return p < L.idx[p0] ? L.idx[p0 + 1 + p] : 0u;
+}
+__device__ __forceinline__ uint2 el_run(const LogParams& L, uint32_t pb, uint32_t e, uint32_t k) {
+  const uint32_t w = pb + 6 + E_COUNT * 2 * e + 2 * k;
+  return make_uint2(L.idx[w], L.idx[w + 1]);
+}
+__device__ __forceinline__ uint2 name_run(const LogParams& L, uint32_t id) {
+  const uint32_t nn = L.idx[2 * G_COUNT];
+  return id < nn ? make_uint2(L.idx[2 * G_COUNT + 1 + 2 * id], L.idx[2 * G_COUNT + 2 + 2 * id]) : make_uint2(0, 0);
+}
+
+// ---- byte sinks: a counter, or 8-byte little-endian stores ---------------------------------
+struct Count {
+  unsigned long long n = 0;
+  __device__ __forceinline__ void b(uint32_t) { ++n; }
+  __device__ __forceinline__ void bytes(const LogParams&, uint2 r) { n += r.y; }
+  __device__ __forceinline__ void zeros(uint32_t k) { n += k; }
+};
+struct Write {
+  uint64_t* p;
+  uint64_t acc = 0;
+  uint32_t nb = 0;
+  __device__ __forceinline__ void b(uint32_t x) {
+    acc |= (uint64_t)(x & 0xFFu) << (8 * nb);
+    if (++nb == 8) {
+      *p++ = acc;
+      acc = 0;
+      nb = 0;
+    }
+  }
+  __device__ __forceinline__ void bytes(const LogParams& L, uint2 r) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(L.arena + r.x);
+    for (uint32_t i = 0; i < r.y; i += 4) {
+      const uint32_t v = w[i >> 2];
+      const uint32_t k = r.y - i < 4 ? r.y - i : 4;
+      for (uint32_t j = 0; j < k; ++j) b(v >> (8 * j));
+    }
+  }
+  __device__ __forceinline__ void zeros(uint32_t k) {
+    for (uint32_t i = 0; i < k; ++i) b(0);
+  }
+};
+
+template <class S>
+__device__ __forceinline__ void le(S& s, unsigned long long v, int n) {
+  for (int i = 0; i < n; ++i) s.b((uint32_t)(v >> (8 * i)));
+}
+template <class S>
+__device__ __forceinline__ void be(S& s, unsigned long long v, int n) {
+  for (int i = n - 1; i >= 0; --i) s.b((uint32_t)(v >> (8 * i)));
+}
+
+// MsgPackWriter.writeInteger (:154-212): the smallest encoding
+template <class S>
+__device__ __forceinline__ void mp_int(S& s, long long v) {
+  if (v < -(1LL << 5)) {
+    if (v < -(1LL << 15)) {
+      if (v < -(1LL << 31)) { s.b(0xd3); be(s, (unsigned long long)v, 8); }
+      else { s.b(0xd2); be(s, (unsigned long long)v, 4); }
+    } else if (v < -(1LL << 7)) { s.b(0xd1); be(s, (unsigned long long)v, 2); }
+    else { s.b(0xd0); s.b((uint32_t)v); }
+  } else if (v < (1LL << 7)) {
+    s.b((uint32_t)v);
+  } else if (v < (1LL << 16)) {
+    if (v < (1LL << 8)) { s.b(0xcc); s.b((uint32_t)v); }
+    else { s.b(0xcd); be(s, (unsigned long long)v, 2); }
+  } else if (v < (1LL << 32)) { s.b(0xce); be(s, (unsigned long long)v, 4); }
+  else { s.b(0xcf); be(s, (unsigned long long)v, 8); }
+}
+__device__ __forceinline__ uint32_t mp_int_len(long long v) {
+  if (v < -(1LL << 5)) return v < -(1LL << 31) ? 9 : v < -(1LL << 15) ? 5 : v < -(1LL << 7) ? 3 : 2;
+  if (v < (1LL << 7)) return 1;
+  return v < (1LL << 8) ? 2 : v < (1LL << 16) ? 3 : v < (1LL << 32) ? 5 : 9;
+}
+
+// decimal text of a signed 64-bit integer (the "%lld" of the reason texts)
+template <class S>
+__device__ __forceinline__ void dec(S& s, long long v) {
+  char d[20];
+  int n = 0;
+  unsigned long long u = v < 0 ? 0ull - (unsigned long long)v : (unsigned long long)v;
+  do { d[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+  if (v < 0) s.b('-');
+  while (n) s.b((uint32_t)d[--n]);
+}
+
+// ---- one record -------------------------------------------------------------------------------
+struct Rec {
+  long long key, scope, pik;
+  uint32_t proc, elem;      // NONE when not applicable
+  uint8_t rt, vt, intent, rej_type, reason, reason_arg, skip;
+};
+
+// key of ordinal `ord` of instance `inst` as seen by command c (see the header comment)
+__device__ __forceinline__ bool key_of(const LogParams& L, uint32_t c, uint32_t inst, uint32_t ord, long long& key) {
+  if (ord == NONE) { key = -1; return true; }
+  for (int hop = 0; hop < 64 && c != 0xFFFFFFFFu; ++hop) {
+    const LogCmd& m = L.cmds[c];
+    if (ord >= m.first_ord && m.nkeys) {  // this batch (ordinals grow within an instance generation)
+      key = L.pbits + (long long)(m.key0 + (uint16_t)(ord - m.first_ord));
+      return true;
+    }
+    if (m.first_ord == 0) break;  // a CREATE: nothing older in this generation
+    c = m.prev;
+  }
+  if (inst >= L.n_inst) return false;
+  if (ord == 0) {
+    const unsigned long long k = L.kpi[inst];
+    if (!(k >> 63)) return false;
+    key = L.pbits + (long long)(k & ((1ull << 63) - 1));
+    return true;
+  }
+  const unsigned long long e = L.ring[(size_t)(ord % kRing) * L.n_inst + inst];
+  if ((e >> 48) != ord) return false;
+  key = L.pbits + (long long)(e & ((1ull << 48) - 1));
+  return true;
+}
+
+__device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const LogCmd& m, uint2 w, Rec& r) {
+  const uint32_t key_ord = w.x & 0xFFFF, aux_ord = w.x >> 16, elem = w.y & 0xFFFF;
+  const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
+  const bool rej = code & kRejectBit;
+  const uint32_t c6 = code & 0x3F;
+  const uint32_t inst = m.instance;
+  r.proc = inst < L.n_inst ? L.inst_proc[inst] : NONE;
+  r.elem = elem;
+  if (!key_of(L, c, inst, key_ord, r.key) || !key_of(L, c, inst, aux_ord, r.scope) || !key_of(L, c, inst, 0, r.pik))
+    return false;
+  r.rej_type = ZBHIP_REJ_NONE;
+  r.reason = r.reason_arg = 0;
+  r.skip = 0;
+  if (c6 >= 1 && c6 <= 10) {
+    r.vt = ZBHIP_VT_PROCESS_INSTANCE;
+    r.intent = (uint8_t)c6;
+    r.rt = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
+    r.skip = !rej && c6 >= 8 && !(fl & F_UNPROCESSED) ? 1 : 0;  // a follow-up command processed in its batch
+  } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE) {
+    r.vt = ZBHIP_VT_JOB;
+    r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED : ZBHIP_JOB_COMPLETE;
+    r.rt = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
+  } else if (c6 == C_VAR_CREATED || c6 == C_VAR_UPDATED) {
+    r.vt = ZBHIP_VT_VARIABLE;
+    r.intent = c6 == C_VAR_CREATED ? ZBHIP_VAR_CREATED : ZBHIP_VAR_UPDATED;
+    r.rt = ZBHIP_RT_EVENT;
+  } else if (c6 == C_PE_TRIGGERING) {
+    r.vt = ZBHIP_VT_PROCESS_EVENT;
+    r.intent = ZBHIP_PE_TRIGGERING;
+    r.rt = ZBHIP_RT_EVENT;
+  } else if (c6 == C_PIC_CREATED) {
+    r.vt = ZBHIP_VT_PROCESS_INSTANCE_CREATION;
+    r.intent = ZBHIP_PIC_CREATED;
+    r.rt = ZBHIP_RT_EVENT;
+  } else {
+    return false;  // a message record or a corrupt row: the host serialiser
+  }
+  if (rej) {
+    r.reason = fl & 0xF;
+    r.reason_arg = fl >> 4;
+    if (r.vt == ZBHIP_VT_JOB) {
+      r.rej_type = ZBHIP_REJ_NOT_FOUND;
+      r.proc = NONE;
+      r.elem = NONE;
+      r.scope = -1;
+      r.pik = -1;
+    } else {
+      r.rej_type = ZBHIP_REJ_INVALID_STATE;
+    }
+  }
+  return true;
+}
+
+// msgpack of one document value (logwriter.cpp doc_value); strings are not on the device
+template <class S>
+__device__ __forceinline__ bool doc_value(S& s, const zbhip_doc_entry& d) {
+  switch (d.type) {
+    case ZBHIP_DOC_NIL: s.b(0xc0); return true;
+    case ZBHIP_DOC_BOOL: s.b(d.value ? 0xc3 : 0xc2); return true;
+    case ZBHIP_DOC_INT: mp_int(s, d.value); return true;
+    case ZBHIP_DOC_DEC: {
+      const double v = (double)d.value / 1e6;
+      s.b(0xcb);
+      be(s, (unsigned long long)__double_as_longlong(v), 8);
+      return true;
+    }
+    default: return false;
+  }
+}
+__device__ __forceinline__ uint32_t doc_value_len(const zbhip_doc_entry& d) {
+  return d.type == ZBHIP_DOC_INT ? mp_int_len(d.value) : d.type == ZBHIP_DOC_DEC ? 9u : 1u;
+}
+__device__ __forceinline__ bool doc_ok(const zbhip_doc_entry& d) {
+  return d.type == ZBHIP_DOC_NIL || d.type == ZBHIP_DOC_BOOL || d.type == ZBHIP_DOC_INT || d.type == ZBHIP_DOC_DEC;
+}
+
+// mp_bin of the command's document (DocumentValue: empty -> EMPTY_DOCUMENT; one entry -> a map)
+template <class S>
+__device__ __forceinline__ void src_doc_bin(S& s, const LogParams& L, const LogCmd& m) {
+  if (m.doc_count == 0) { s.bytes(L, run(L, G_EMPTY_BIN)); return; }
+  const zbhip_doc_entry d = L.docs[m.doc_begin];
+  const uint2 nr = name_run(L, d.name_id);
+  const uint32_t len = 1 + nr.y + doc_value_len(d);
+  s.b(0xc4);  // < 256 bytes: a name and a scalar
+  s.b(len);
+  s.b(0x81);
+  s.bytes(L, nr);
+  doc_value(s, d);
+}
+
+template <class S>
+__device__ __forceinline__ void reason_text(S& s, const LogParams& L, const Rec& r, uint32_t pb) {
+  switch (r.reason) {
+    case ZBHIP_REASON_PGW_NOT_ALL_TAKEN:
+      s.bytes(L, run(L, G_RS_PGW_A));
+      if (pb && r.elem != NONE) s.bytes(L, el_run(L, pb, r.elem, E_ID_RAW));
+      s.bytes(L, run(L, G_RS_PGW_B));
+      return;
+    case ZBHIP_REASON_FS_NOT_FOUND:
+      s.bytes(L, run(L, G_RS_FSNF_A)); dec(s, r.scope); s.bytes(L, run(L, G_RS_NF_B));
+      return;
+    case ZBHIP_REASON_FS_STATE:
+      s.bytes(L, run(L, G_RS_FSST_A)); s.bytes(L, run(L, G_ST0 + (r.reason_arg & 15))); s.bytes(L, run(L, G_RS_Q));
+      return;
+    case ZBHIP_REASON_EI_NOT_FOUND:
+      s.bytes(L, run(L, G_RS_EINF_A)); dec(s, r.key); s.bytes(L, run(L, G_RS_NF_B));
+      return;
+    case ZBHIP_REASON_EI_STATE:
+      s.bytes(L, run(L, G_RS_EIST_A)); s.bytes(L, run(L, G_ST0 + (r.reason_arg & 15))); s.bytes(L, run(L, G_RS_Q));
+      return;
+    case ZBHIP_REASON_JOB_NOT_FOUND:
+      s.bytes(L, run(L, G_RS_JOB_A)); dec(s, r.key); s.bytes(L, run(L, G_RS_JOB_B));
+      return;
+    default:
+      return;
+  }
+}
+
+// the record value (msgpack); false: outside what the device writes
+template <class S>
+__device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m, const Rec& r, uint32_t pb) {
+  const bool has_el = pb && r.elem != NONE && r.elem < L.idx[pb + 5];
+  switch (r.vt) {
+    case ZBHIP_VT_PROCESS_INSTANCE:
+      if (!has_el) return false;
+      s.bytes(L, el_run(L, pb, r.elem, E_PI_HEAD));
+      mp_int(s, r.pik);
+      s.bytes(L, run(L, G_FLOWSCOPE));
+      mp_int(s, r.scope);
+      s.bytes(L, el_run(L, pb, r.elem, E_PI_TAIL));
+      return true;
+    case ZBHIP_VT_JOB:
+      if (r.rt == ZBHIP_RT_REJECTION) {
+        s.bytes(L, run(L, G_JREJ_HEAD));
+        src_doc_bin(s, L, m);
+        s.bytes(L, run(L, G_JREJ_TAIL));
+        return true;
+      }
+      if (!has_el || el_run(L, pb, r.elem, E_JOB_HEAD).y == 0) return false;
+      s.bytes(L, el_run(L, pb, r.elem, E_JOB_HEAD));
+      if (r.intent == ZBHIP_JOB_COMPLETED) src_doc_bin(s, L, m);
+      else s.bytes(L, run(L, G_EMPTY_BIN));
+      s.bytes(L, el_run(L, pb, r.elem, E_JOB_MID));
+      mp_int(s, r.pik);
+      s.bytes(L, el_run(L, pb, r.elem, E_JOB_TAIL));
+      mp_int(s, r.scope);
+      s.bytes(L, run(L, G_TENANT));
+      return true;
+    case ZBHIP_VT_VARIABLE: {
+      // the batch's source document entry of that name (VariableRecord.java:35-41)
+      if (!pb || m.doc_count != 1) return false;
+      const zbhip_doc_entry d = L.docs[m.doc_begin];
+      if (d.name_id != r.elem) return false;
+      const uint2 nr = name_run(L, r.elem);
+      s.bytes(L, run(L, G_VAR_A));
+      s.bytes(L, nr);
+      s.bytes(L, run(L, G_VAR_VALUE));
+      s.b(0xc4);
+      s.b(doc_value_len(d));
+      doc_value(s, d);
+      s.bytes(L, run(L, G_VAR_SCOPE));
+      mp_int(s, r.scope);
+      s.bytes(L, run(L, G_K_PIK));
+      mp_int(s, r.pik);
+      s.bytes(L, run(L, G_K_DEF));
+      mp_int(s, (long long)(((unsigned long long)L.idx[pb + 3] << 32) | L.idx[pb + 2]));
+      s.bytes(L, run(L, G_K_BPMN));
+      s.bytes(L, make_uint2(L.idx[pb], L.idx[pb + 1]));
+      s.bytes(L, run(L, G_TENANT));
+      return true;
+    }
+    case ZBHIP_VT_PROCESS_EVENT:
+      if (!has_el) return false;
+      s.bytes(L, run(L, G_PE_A));
+      mp_int(s, r.scope);
+      s.bytes(L, run(L, G_PE_TARGET));
+      s.bytes(L, el_run(L, pb, r.elem, E_ID_STR));
+      s.bytes(L, run(L, G_K_VARS));
+      src_doc_bin(s, L, m);
+      s.bytes(L, run(L, G_K_DEF));
+      mp_int(s, (long long)(((unsigned long long)L.idx[pb + 3] << 32) | L.idx[pb + 2]));
+      s.bytes(L, run(L, G_K_PIK));
+      mp_int(s, r.pik);
+      s.bytes(L, run(L, G_TENANT));
+      return true;
+    case ZBHIP_VT_PROCESS_INSTANCE_CREATION:
+      if (!pb) return false;
+      s.bytes(L, run(L, G_PIC_A));
+      s.bytes(L, make_uint2(L.idx[pb], L.idx[pb + 1]));
+      s.bytes(L, run(L, G_K_DEF));
+      mp_int(s, (long long)(((unsigned long long)L.idx[pb + 3] << 32) | L.idx[pb + 2]));
+      s.bytes(L, run(L, G_K_PIK));
+      mp_int(s, r.scope);
+      s.bytes(L, run(L, G_K_VERSION));
+      mp_int(s, (long long)(int32_t)L.idx[pb + 4]);
+      s.bytes(L, run(L, G_K_VARS));
+      src_doc_bin(s, L, m);
+      s.bytes(L, run(L, G_PIC_TAIL));
+      s.bytes(L, run(L, G_TENANT));
+      return true;
+    default:
+      return false;
+  }
+}
+
+// one log entry: dispatcher frame + LogEntryDescriptor header + SBE RecordMetadata + value, 8-aligned
+// (logwriter.cpp zbhip_serialize_log); `S` counts in the first pass and writes in the second.
+template <class S>
+__device__ __forceinline__ bool entry(S& s, const LogParams& L, const LogCmd& m, const Rec& r, long long pos) {
+  const uint32_t pb = r.proc != NONE ? proc_block(L, r.proc) : 0u;
+  Count vc, rc;
+  if (!value(vc, L, m, r, pb)) return false;
+  const bool rej = r.rt == ZBHIP_RT_REJECTION;
+  if (rej) reason_text(rc, L, r, pb);
+  const uint2 auth = run(L, G_AUTH);  // le32 length + AuthInfo msgpack
+  const uint32_t md = 8 + 32 + 4 + (uint32_t)rc.n + auth.y;
+  const uint32_t framed = 12 + 40 + md + (uint32_t)vc.n;
+  const uint32_t aligned = (framed + 7) & ~7u;
+  le(s, framed, 4);
+  s.zeros(8);
+  s.b(0); s.b(0); s.b(r.skip); s.b(0);
+  le(s, (unsigned long long)pos, 8);
+  le(s, (unsigned long long)m.src_pos, 8);
+  le(s, (unsigned long long)r.key, 8);
+  le(s, (unsigned long long)L.timestamp, 8);
+  le(s, md, 2);
+  s.zeros(2);
+  // RecordMetadata: messageHeader (blockLength 32, templateId 200, schemaId 0, version 4) + block
+  le(s, 32, 2); le(s, 200, 2); le(s, 0, 2); le(s, 4, 2);
+  s.b(r.rt);
+  le(s, 0x80000000u, 4);          // requestStreamId: null
+  le(s, ~0ull, 8);                // requestId: null
+  le(s, 4, 2);                    // protocolVersion
+  s.b(r.vt);
+  s.b(r.intent);
+  le(s, (uint32_t)L.broker[0], 4); le(s, (uint32_t)L.broker[1], 4); le(s, (uint32_t)L.broker[2], 4);
+  le(s, 1, 2);                    // recordVersion
+  s.b(rej ? r.rej_type : 255);
+  le(s, rc.n, 4);
+  if (rej) reason_text(s, L, r, pb);
+  s.bytes(L, auth);
+  value(s, L, m, r, pb);
+  s.zeros(aligned - framed);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= L.n) return;
+  const LogCmd m = L.cmds[c];
+  Count s;
+  for (uint32_t j = 0; j < m.nrec; ++j) {
+    Rec r;
+    if (!decode(L, c, m, L.rows[m.rec_off + j], r) || !entry(s, L, m, r, 0)) {
+      atomicOr(L.flag, 1u);
+      break;
+    }
+  }
+  L.bytes[c] = s.n;
+}
+
+__global__ __launch_bounds__(256) void k_log_write(LogParams L) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= L.n) return;
+  const LogCmd m = L.cmds[c];
+  Write s;
+  s.p = L.out + (L.bytes[c] >> 3);
+  for (uint32_t j = 0; j < m.nrec; ++j) {
+    Rec r;
+    if (!decode(L, c, m, L.rows[m.rec_off + j], r)) return;
+    entry(s, L, m, r, L.first_position + (long long)(m.out_rec + j));
+  }
+}
+
+// exclusive scan of the per-command byte counts (in place), total at bytes[n]
+constexpr int kLogScanB = 1024;
+__global__ __launch_bounds__(kLogScanB) void k_log_block_sums(unsigned long long* v, uint32_t n, unsigned long long* bs) {
+  const uint32_t i = blockIdx.x * kLogScanB + threadIdx.x;
+  __shared__ unsigned long long ws[kLogScanB / 64];
+  unsigned long long x = i < n ? v[i] : 0ull;
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(x, off);
+    if ((threadIdx.x & 63) >= (uint32_t)off) x += y;
+  }
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kLogScanB / 64; ++w) t += ws[w];
+    bs[blockIdx.x] = t;
+  }
+}
+__global__ __launch_bounds__(64) void k_log_scan_sums(unsigned long long* bs, uint32_t nb, unsigned long long* total) {
+  if (threadIdx.x != 0) return;
+  unsigned long long acc = 0;
+  for (uint32_t b = 0; b < nb; ++b) {
+    const unsigned long long x = bs[b];
+    bs[b] = acc;
+    acc += x;
+  }
+  *total = acc;
+}
+__global__ __launch_bounds__(kLogScanB) void k_log_apply(unsigned long long* v, uint32_t n, const unsigned long long* bs) {
+  const uint32_t i = blockIdx.x * kLogScanB + threadIdx.x;
+  __shared__ unsigned long long ws[kLogScanB / 64];
+  const unsigned long long x0 = i < n ? v[i] : 0ull;
+  unsigned long long x = x0;
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(x, off);
+    if ((threadIdx.x & 63) >= (uint32_t)off) x += y;
+  }
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  unsigned long long b = bs[blockIdx.x];
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) b += ws[w];
+  if (i < n) v[i] = b + x - x0;
+}
+
+// ring fill after the window: CREATEs reset their instance (a new generation), then every command
+// adds its batch's ordinals (atomicMax: a later batch of the instance carries larger ordinals)
+__global__ __launch_bounds__(256) void k_ring_create(LogParams L) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= L.n) return;
+  const LogCmd m = L.cmds[c];
+  if (!m.nkeys || m.first_ord != 0 || m.instance >= L.n_inst) return;
+  for (uint32_t s = 0; s < kRing; ++s) L.ring[(size_t)s * L.n_inst + m.instance] = 0ull;
+  L.kpi[m.instance] = (1ull << 63) | (unsigned long long)m.key0;
+}
+__global__ __launch_bounds__(256) void k_ring_add(LogParams L) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= L.n) return;
+  const LogCmd m = L.cmds[c];
+  if (!m.nkeys || m.instance >= L.n_inst) return;
+  const uint32_t k0 = m.nkeys > kRing ? m.nkeys - kRing : 0u;  // the last kRing ordinals of the batch
+  for (uint32_t k = k0; k < m.nkeys; ++k) {
+    const uint32_t ord = (uint16_t)(m.first_ord + k);
+    const unsigned long long e = ((unsigned long long)ord << 48) | (unsigned long long)(m.key0 + k);
+    atomicMax(&L.ring[(size_t)(ord % kRing) * L.n_inst + m.instance], e);
+  }
+}
+
+hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
+  LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.docs, a.n_docs, a.inst_proc, a.ring, a.kpi, a.n_inst, a.pbits,
+              a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]}, a.bytes, a.out, a.flag};
+  const uint32_t g = (a.n + 255) / 256;
+  if (a.phase == 0) {  // sizes and byte offsets
+    if (a.n) hipLaunchKernelGGL(k_log_sizes, dim3(g), dim3(256), 0, s, L);
+    const uint32_t nb = (a.n + kLogScanB - 1) / kLogScanB;
+    if (a.n) hipLaunchKernelGGL(k_log_block_sums, dim3(nb), dim3(kLogScanB), 0, s, a.bytes, a.n, a.block_sums);
+    hipLaunchKernelGGL(k_log_scan_sums, dim3(1), dim3(64), 0, s, a.block_sums, nb, a.bytes + a.n);
+    if (a.n) hipLaunchKernelGGL(k_log_apply, dim3(nb), dim3(kLogScanB), 0, s, a.bytes, a.n, a.block_sums);
+  } else if (a.phase == 1) {
+    if (a.n) hipLaunchKernelGGL(k_log_write, dim3(g), dim3(256), 0, s, L);
+  } else {
+    if (a.n) hipLaunchKernelGGL(k_ring_create, dim3(g), dim3(256), 0, s, L);
+    if (a.n) hipLaunchKernelGGL(k_ring_add, dim3(g), dim3(256), 0, s, L);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace zb

@@ -1127,3 +1127,113 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
   memcpy(row, out.c_str(), out.size() + 1);
   return (int)out.size();
 }
+
+// ---- device tables of the serialiser (logdev.hip) ------------------------------------------------
+// The constant byte runs of zbhip_serialize_log, laid out for the device writer: a byte arena (runs
+// 4-aligned) and a u32 table -- the global runs in logdev.hip's LogRun order (offset, length), the
+// names (msgpack strings), then per process: bpmnProcessId (msgpack string), definition key (lo,
+// hi), version, element count, and per element its ProcessInstanceRecord / JobRecord runs, its id as
+// a msgpack string and raw (the reason texts).
+namespace zb {
+void serializer_broker(const zbhip_serializer* s, int32_t out[3]) {
+  for (int i = 0; i < 3; ++i) out[i] = s ? s->broker[i] : 0;
+}
+int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, std::vector<uint32_t>& idx) {
+  if (!s) return ZBHIP_EINVAL;
+  arena.clear();
+  idx.clear();
+  auto push = [&](const Bytes& b) {
+    while (arena.size() % 4) arena.push_back(0);
+    idx.push_back((uint32_t)arena.size());
+    idx.push_back((uint32_t)b.size());
+    arena.insert(arena.end(), b.begin(), b.end());
+  };
+  auto k = [](std::initializer_list<const char*> keys) {
+    Bytes b;
+    for (const char* x : keys) key(b, x);
+    return b;
+  };
+  Bytes b;
+  le32(b, (uint32_t)s->auth.size());  // G_AUTH: the metadata's authorization var-data
+  b += s->auth;
+  push(b);
+  b.clear(); key(b, "tenantId"); key(b, kTenant); push(b);           // G_TENANT
+  push(k({"flowScopeKey"}));                                          // G_FLOWSCOPE
+  b.clear(); mp_bin(b, kEmptyDoc); push(b);                           // G_EMPTY_BIN
+  b.clear();                                                          // G_JREJ_HEAD (JOB:COMPLETE value)
+  mp_map(b, 17);
+  key(b, "deadline"); mp_int(b, -1);
+  key(b, "worker"); key(b, "");
+  key(b, "retries"); mp_int(b, -1);
+  key(b, "retryBackoff"); mp_int(b, 0);
+  key(b, "recurringTime"); mp_int(b, -1);
+  key(b, "type"); key(b, "");
+  key(b, "customHeaders"); b += kEmptyDoc;
+  key(b, "variables");
+  push(b);
+  b.clear();                                                          // G_JREJ_TAIL
+  key(b, "errorMessage"); key(b, "");
+  key(b, "errorCode"); key(b, "");
+  key(b, "bpmnProcessId"); key(b, "");
+  key(b, "processDefinitionVersion"); mp_int(b, -1);
+  key(b, "processDefinitionKey"); mp_int(b, -1);
+  key(b, "processInstanceKey"); mp_int(b, -1);
+  key(b, "elementId"); key(b, "");
+  key(b, "elementInstanceKey"); mp_int(b, -1);
+  key(b, "tenantId"); key(b, kTenant);
+  push(b);
+  b.clear(); mp_map(b, 7); key(b, "name"); push(b);                   // G_VAR_A
+  push(k({"value"}));                                                 // G_VAR_VALUE
+  push(k({"scopeKey"}));                                              // G_VAR_SCOPE
+  push(k({"processInstanceKey"}));                                    // G_K_PIK
+  push(k({"processDefinitionKey"}));                                  // G_K_DEF
+  push(k({"bpmnProcessId"}));                                         // G_K_BPMN
+  b.clear(); mp_map(b, 6); key(b, "scopeKey"); push(b);               // G_PE_A
+  push(k({"targetElementId"}));                                       // G_PE_TARGET
+  push(k({"variables"}));                                             // G_K_VARS
+  b.clear(); mp_map(b, 8); key(b, "bpmnProcessId"); push(b);          // G_PIC_A
+  push(k({"version"}));                                               // G_K_VERSION
+  b.clear(); key(b, "fetchVariables"); mp_array(b, 0); key(b, "startInstructions"); mp_array(b, 0); push(b);  // G_PIC_TAIL
+  for (const char* t : {"Expected to be able to activate parallel gateway '", "', but not all sequence flows have been taken.",
+                        "Expected flow scope instance with key '", "' to be present in state but not found.",
+                        "Expected flow scope instance to be in state 'ELEMENT_ACTIVATED' but was '", "'.",
+                        "Expected element instance with key '",
+                        "Expected element instance to be in state 'ELEMENT_ACTIVATED' or one of '[ELEMENT_COMPLETING]' but was '",
+                        "Expected to complete job with key '", "', but no such job was found"})
+    push(Bytes(t));                                                   // G_RS_*
+  for (int st = 0; st < 16; ++st) push(Bytes(state_text(st)));       // G_ST0 ..
+  idx.push_back((uint32_t)s->names.size());
+  for (const std::string& nm : s->names) {
+    b.clear();
+    mp_str(b, nm);
+    push(b);
+  }
+  const size_t p0 = idx.size();
+  idx.push_back((uint32_t)s->procs.size());
+  idx.resize(idx.size() + s->procs.size(), 0);
+  for (size_t p = 0; p < s->procs.size(); ++p) {
+    const SerProcess& P = s->procs[p];
+    idx[p0 + 1 + p] = (uint32_t)idx.size();
+    b.clear();
+    mp_str(b, P.bpmn_id);
+    push(b);
+    idx.push_back((uint32_t)((uint64_t)P.def_key & 0xFFFFFFFFu));
+    idx.push_back((uint32_t)((uint64_t)P.def_key >> 32));
+    idx.push_back((uint32_t)P.version);
+    idx.push_back((uint32_t)P.els.size());
+    for (const SerElement& E : P.els) {
+      push(E.pi_head);
+      push(E.pi_tail);
+      push(E.job_head);
+      push(E.job_mid);
+      push(E.job_tail);
+      b.clear();
+      mp_str(b, E.id);
+      push(b);
+      push(E.id);
+    }
+  }
+  while (arena.size() % 4) arena.push_back(0);
+  return ZBHIP_OK;
+}
+}  // namespace zb

@@ -39,6 +39,9 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
                           zbhip_xpart_cmd* xout, uint32_t xcap, const DevState& st, long long pbits, hipStream_t s);
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s);
 hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, hipStream_t s);
+hipError_t launch_log_device(const LogLaunch& a, hipStream_t s);
+int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, std::vector<uint32_t>& idx);
+void serializer_broker(const zbhip_serializer* s, int32_t out[3]);
 size_t activated_out_bytes();
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
                                 uint32_t stamp, uint32_t* flag, hipStream_t s);
@@ -236,6 +239,24 @@ struct zbhip_handle {
   std::vector<std::vector<std::pair<uint16_t, int64_t>>> hist;
   std::vector<uint16_t> inst_proc;
   std::vector<BatchRef> batches;
+
+  // ---- log bytes on the device (zbhip_serialize_log_device, logdev.hip) ----
+  uint8_t* d_log_arena = nullptr;   // the serialiser's constant byte runs
+  uint32_t* d_log_idx = nullptr;
+  size_t log_arena_cap = 0, log_idx_cap = 0;
+  size_t log_tables_procs = ~(size_t)0, log_tables_names = ~(size_t)0;
+  unsigned long long* d_ring = nullptr;  // [16][max_instances] key ring + [max_instances] PI keys
+  uint16_t* d_inst_proc = nullptr;
+  LogCmd* d_logcmd = nullptr;
+  unsigned long long* d_log_bytes = nullptr;  // [max_commands + 1 + scan blocks]
+  uint64_t* d_log_out = nullptr;
+  size_t log_out_cap = 0;
+  uint32_t* d_log_flag = nullptr;
+  std::vector<LogCmd> h_logcmd;
+  std::vector<uint64_t> log_prev;   // per instance: window | last command of the window (prev chain)
+  uint64_t windows_run = 0;         // zbhip_run calls
+  uint64_t ring_filled = 0;         // windows whose keys are in the ring (all of them, or the path is off)
+  bool ring_ok = true;              // false once a window's keys missed the ring (or state was imported)
 
   // ---- job activation (zbhip_activate_jobs) ----
   // JOB_ACTIVATABLE of the GPU-resident jobs, [type, job key] -> (instance, job key ordinal): built
@@ -471,6 +492,14 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_cont_order);
   (void)hipFree(h->d_qspill);
   (void)hipFree(h->d_tpl);
+  (void)hipFree(h->d_log_arena);
+  (void)hipFree(h->d_log_idx);
+  (void)hipFree(h->d_ring);
+  (void)hipFree(h->d_inst_proc);
+  (void)hipFree(h->d_logcmd);
+  (void)hipFree(h->d_log_bytes);
+  (void)hipFree(h->d_log_out);
+  (void)hipFree(h->d_log_flag);
   (void)hipFree(h->d_check_flag);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
@@ -1122,6 +1151,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (!h) return ZBHIP_EINVAL;
   if (h->ran) return ZBHIP_ESTATE;
   if (h->procs.empty()) return ZBHIP_ESTATE;
+  if (h->ring_filled != h->windows_run) h->ring_ok = false;  // the previous window's keys are not in the ring
+  ++h->windows_run;
   const bool timed = flags & ZBHIP_RUN_TIMED;
   const bool want = !(flags & ZBHIP_RUN_NO_RESULTS);
   const bool accumulate = flags & ZBHIP_RUN_ACCUMULATE;
@@ -2161,6 +2192,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   if (n_instances) *n_instances = 0;
   if (!h->relabel_ok) return ZBHIP_ESTATE;
   if (int rc = finalize(h)) return rc;
+  h->ring_ok = false;  // imported keys are not in the device key ring: the host serialiser from now on
   std::map<int64_t, ImpElement> els;
   std::vector<ImpVar> vars;
   std::vector<std::tuple<int64_t, std::string, std::string, uint32_t>> taken;
@@ -2569,5 +2601,150 @@ extern "C" int zbhip_job_batch_rejection_reason(const zbhip_job_activation* cmd,
     case 3: snprintf(buf, cap, f, "type", "present", "blank"); break;
     default: buf[0] = 0;
   }
+  return ZBHIP_OK;
+}
+
+// ---- log bytes on the device (logdev.hip) ----------------------------------------------------------
+// After zbhip_run with results: every record of the window serialised in HBM, in drain order, the
+// same bytes zbhip_serialize_log writes for the drained records.  The window's keys then go into
+// the device key ring, which is why every window has to come through here for the path to stay on:
+// a window that did not (or imported state, message partitions, continuation batches, string
+// variables, a key older than the ring) makes this return ZBHIP_EUNSUPP -- the host serialiser
+// (zbhip_drain + zbhip_serialize_log) is then the path for that window and the ones after it.
+extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_window* w, const void** dev_bytes,
+                                          size_t* used) {
+  if (!h || !w || !dev_bytes || !used) return ZBHIP_EINVAL;
+  *dev_bytes = nullptr;
+  *used = 0;
+  if (!h->results) return ZBHIP_ESTATE;
+  const bool fill = h->ring_filled + 1 == h->windows_run;  // every earlier window's keys are in the ring
+  if (!fill) h->ring_ok = false;
+  h->ring_filled = h->windows_run;  // this window is accounted for, whether or not it is written here
+  if (h->msg() || !h->cont_cmds.empty() || h->external) h->ring_ok = false;
+  if (!h->ring_ok) return ZBHIP_EUNSUPP;
+  if (int rc = finalize(h)) return rc;
+  const size_t n = h->n_cmds;
+  const size_t N = h->cfg.max_instances;
+  if (w->n_cmds != n) return ZBHIP_EINVAL;
+  // tables of the serialiser (deployments / names changed since the last upload)
+  if (h->log_tables_procs != h->procs.size() || h->log_tables_names != h->names.size()) {
+    std::vector<uint8_t> arena;
+    std::vector<uint32_t> idx;
+    if (int rc = log_device_tables(h->ser, arena, idx)) return rc;
+    if (arena.size() > h->log_arena_cap) {
+      (void)hipFree(h->d_log_arena);
+      h->d_log_arena = nullptr;
+      if (dalloc(&h->d_log_arena, arena.size() * 2) != hipSuccess) return ZBHIP_ENOMEM;
+      h->log_arena_cap = arena.size() * 2;
+    }
+    if (idx.size() > h->log_idx_cap) {
+      (void)hipFree(h->d_log_idx);
+      h->d_log_idx = nullptr;
+      if (dalloc(&h->d_log_idx, idx.size() * 2) != hipSuccess) return ZBHIP_ENOMEM;
+      h->log_idx_cap = idx.size() * 2;
+    }
+    HIPCHK(hipMemcpyAsync(h->d_log_arena, arena.data(), arena.size(), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d_log_idx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->log_tables_procs = h->procs.size();
+    h->log_tables_names = h->names.size();
+  }
+  if (!h->d_ring) {
+    const size_t words = (size_t)16 * N + N;  // logdev.hip kRing = 16
+    if (dalloc(&h->d_ring, words) != hipSuccess || dalloc(&h->d_inst_proc, N) != hipSuccess ||
+        dalloc(&h->d_logcmd, (size_t)h->cfg.max_commands) != hipSuccess ||
+        dalloc(&h->d_log_bytes, (size_t)h->cfg.max_commands + 1 + ((size_t)h->cfg.max_commands + 1023) / 1024 + 1) != hipSuccess ||
+        dalloc(&h->d_log_flag, 1) != hipSuccess)
+      return ZBHIP_ENOMEM;
+    HIPCHK(hipMemsetAsync(h->d_ring, 0, words * sizeof(unsigned long long), h->stream));
+  }
+  // the window's command table: rows, record positions, key bases, the prev chain per instance
+  h->h_logcmd.resize(n);
+  if (h->log_prev.size() < N) h->log_prev.assign(N, ~0ull);
+  const uint64_t win = h->windows_run;
+  uint64_t out_rec = 0;
+  for (size_t c = 0; c < n; ++c) {
+    const uint2 hd = h->h_hdr[c];
+    const zbhip_command& cm = h->h_cmds[c];
+    const bool ok = ((hd.y >> 16) & 0xFF) == ST_OK;
+    LogCmd& m = h->h_logcmd[c];
+    m.rec_off = h->h_off[c];
+    m.out_rec = out_rec;
+    m.key0 = (unsigned long long)(h->h_base[c] + 1);
+    m.src_pos = w->source_positions ? w->source_positions[c] : -1;
+    m.instance = cm.instance;
+    m.first_ord = (uint16_t)(hd.y & 0xFFFF);
+    m.nkeys = ok ? (uint16_t)(hd.x >> 16) : 0;
+    m.nrec = (uint16_t)(hd.x & 0xFFFF);
+    m.doc_count = cm.doc_count;
+    m.doc_begin = cm.doc_begin;
+    m.pad = 0;
+    m.prev = ~0u;
+    if (cm.instance < N) {
+      const uint64_t lp = h->log_prev[cm.instance];
+      if ((lp >> 32) == (win & 0xFFFFFFFFu)) m.prev = (uint32_t)lp;
+      h->log_prev[cm.instance] = ((win & 0xFFFFFFFFu) << 32) | (uint32_t)c;
+    }
+    out_rec += m.nrec;
+  }
+  if (n) HIPCHK(hipMemcpyAsync(h->d_logcmd, h->h_logcmd.data(), n * sizeof(LogCmd), hipMemcpyHostToDevice, h->stream));
+  if (h->inst_proc.size() >= N)
+    HIPCHK(hipMemcpyAsync(h->d_inst_proc, h->inst_proc.data(), N * sizeof(uint16_t), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemsetAsync(h->d_log_flag, 0, sizeof(uint32_t), h->stream));
+  LogLaunch a{};
+  a.rows = h->d_rec;
+  a.cmds = h->d_logcmd;
+  a.n = (uint32_t)n;
+  a.arena = h->d_log_arena;
+  a.idx = h->d_log_idx;
+  a.docs = h->d_docs;
+  a.n_docs = (uint32_t)h->n_docs;
+  a.inst_proc = h->d_inst_proc;
+  a.ring = h->d_ring;
+  a.kpi = h->d_ring + (size_t)16 * N;
+  a.n_inst = (uint32_t)N;
+  a.pbits = (long long)h->cfg.partition_id << 51;
+  a.first_position = w->first_position;
+  a.timestamp = w->timestamp;
+  serializer_broker(h->ser, a.broker);
+  a.bytes = h->d_log_bytes;
+  a.block_sums = h->d_log_bytes + n + 1;
+  a.flag = h->d_log_flag;
+  a.phase = 0;
+  HIPCHK(launch_log_device(a, h->stream));
+  unsigned long long total = 0;
+  uint32_t flag = 0;
+  HIPCHK(hipMemcpyAsync(&total, h->d_log_bytes + n, sizeof total, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(&flag, h->d_log_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  int rc = ZBHIP_OK;
+  if (flag) {
+    rc = ZBHIP_EUNSUPP;  // a key the ring does not hold, or a value outside the device writer
+  } else {
+    if (total > h->log_out_cap) {
+      (void)hipFree(h->d_log_out);
+      h->d_log_out = nullptr;
+      h->log_out_cap = 0;
+      const size_t cap = std::max<size_t>(total + total / 4, 1 << 20);
+      if (dalloc(&h->d_log_out, cap / 8) != hipSuccess) return ZBHIP_ENOMEM;
+      h->log_out_cap = cap / 8 * 8;
+    }
+    a.out = h->d_log_out;
+    a.phase = 1;
+    HIPCHK(launch_log_device(a, h->stream));
+    *dev_bytes = h->d_log_out;
+    *used = total;
+  }
+  a.phase = 2;  // the window's keys into the ring, in any case
+  HIPCHK(launch_log_device(a, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return rc;
+}
+
+extern "C" int zbhip_log_device_copy(zbhip_handle* h, void* dst, size_t n) {
+  if (!h || (n && !dst)) return ZBHIP_EINVAL;
+  if (n > h->log_out_cap || (n && !h->d_log_out)) return ZBHIP_EINVAL;
+  if (n) HIPCHK(hipMemcpyAsync(dst, h->d_log_out, n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
   return ZBHIP_OK;
 }

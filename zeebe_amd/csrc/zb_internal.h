@@ -197,4 +197,38 @@ struct StepParams {
   uint32_t launch_seq;
 };
 
+// ---- log bytes on the device (logdev.hip) ----
+struct LogCmd {
+  unsigned long long rec_off;  // first gathered row of the command
+  unsigned long long out_rec;  // log-order index of its first record in the window
+  unsigned long long key0;     // key counter of its first new key: key = pbits + key0 + (ord - first_ord)
+  long long src_pos;           // sourcePosition of its records
+  uint32_t instance;
+  uint32_t prev;               // previous command of the same instance in the window, or ~0
+  uint16_t first_ord, nkeys, nrec, doc_count;
+  uint32_t doc_begin;
+  uint32_t pad;
+};
+struct LogLaunch {
+  int phase;                   // 0 sizes + offsets, 1 write, 2 key ring
+  const uint2* rows;
+  const LogCmd* cmds;
+  uint32_t n;
+  const uint8_t* arena;
+  const uint32_t* idx;
+  const zbhip_doc_entry* docs;
+  uint32_t n_docs;
+  const uint16_t* inst_proc;
+  unsigned long long* ring;
+  unsigned long long* kpi;
+  uint32_t n_inst;
+  long long pbits;
+  long long first_position, timestamp;
+  int32_t broker[3];
+  unsigned long long* bytes;   // [n + 1]
+  unsigned long long* block_sums;
+  uint64_t* out;
+  uint32_t* flag;
+};
+
 }  // namespace zb

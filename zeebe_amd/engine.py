@@ -106,6 +106,23 @@ class Partition:
         check(self.L.zbhip_export_state_db(self.h, cb, None), "zbhip_export_state_db")
         return sorted(out)
 
+    def serialize_log_device(self, source_positions=None, first_position=1, timestamp=0, copy=True):
+        """Log bytes of the last run's window written on the device (zbhip_serialize_log_device):
+        the bytes `log_serializer().serialize(drain(), ...)` gives for the same window.  Returns the
+        bytes (copy=True) or (device pointer, size); raises ZbhipError(ZBHIP_EUNSUPP) when the window
+        needs the host serialiser."""
+        pos = np.ascontiguousarray(source_positions if source_positions is not None
+                                   else np.arange(1, self._n_cmds + 1), dtype=np.int64)
+        w = abi.LogWindow(None, self._n_cmds, 0, None, 0, 0, pos.ctypes.data, first_position, timestamp, None)
+        ptr, used = C.c_void_p(), C.c_size_t()
+        check(self.L.zbhip_serialize_log_device(self.h, C.byref(w), C.byref(ptr), C.byref(used)),
+              "zbhip_serialize_log_device")
+        if not copy:
+            return ptr.value, used.value
+        out = C.create_string_buffer(max(used.value, 1))
+        check(self.L.zbhip_log_device_copy(self.h, out, used.value), "zbhip_log_device_copy")
+        return out.raw[:used.value]
+
     def log_serializer(self):
         """The partition's log serialiser (follows its deployments and dictionaries)."""
         from .logwriter import LogSerializer
@@ -124,11 +141,13 @@ class Partition:
         xp = np.ascontiguousarray(xparts if xparts is not None else abi.make_xparts(0), dtype=abi.XPART_DTYPE)
         check(self.L.zbhip_submit_ex(self.h, cmds.ctypes.data, len(cmds), docs.ctypes.data, len(docs),
                                      xp.ctypes.data if len(xp) else None, len(xp)), "zbhip_submit")
+        self._n_cmds = len(cmds)
 
     def submit_device(self, cmd_ptr, n, doc_ptr=0, n_docs=0, xpart_ptr=0, n_xparts=0):
         """Commands already resident in HBM (e.g. a torch uint8 tensor's data_ptr())."""
         check(self.L.zbhip_submit_device_ex(self.h, cmd_ptr, n, doc_ptr or None, n_docs, xpart_ptr or None, n_xparts),
               "zbhip_submit_device")
+        self._n_cmds = n
 
     # ---- value dictionary (correlation keys) ----
     def intern_string(self, value):

@@ -29,7 +29,8 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream",
            "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
            "zbhip_set_external_keys", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
-           "zbhip_import_state", "zbhip_activate_jobs", "zbhip_job_batch_rejection_reason"]
+           "zbhip_import_state", "zbhip_activate_jobs", "zbhip_job_batch_rejection_reason",
+           "zbhip_serialize_log_device", "zbhip_log_device_copy"]
 
 
 class ZbhipError(RuntimeError):
@@ -118,6 +119,8 @@ def load():
     L.zbhip_handle_serializer.argtypes = [vp]
     L.zbhip_handle_serializer.restype = vp
     L.zbhip_serialize_log.argtypes = [vp, vp, sz, C.POINTER(abi.LogWindow), vp, sz, C.POINTER(sz)]
+    L.zbhip_serialize_log_device.argtypes = [vp, C.POINTER(abi.LogWindow), C.POINTER(vp), C.POINTER(sz)]
+    L.zbhip_log_device_copy.argtypes = [vp, vp, sz]
     L.zbhip_export_state_db.argtypes = [vp, DB_SINK, vp]
     L.zbhip_serializer_encode_state_row.argtypes = [vp, C.c_char_p, DB_SINK, vp]
     L.zbhip_build_info.argtypes = []
