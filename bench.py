@@ -286,6 +286,61 @@ def host_io_pass(args, xml, n, host_windows, local_rank, recs_per_batch):
                    "ms_per_step": sec * 1e3, "records_per_step": recs,
                    "submit_ms": split[0] * 1e3, "run_ms": split[1] * 1e3, "drain_ms": split[2] * 1e3,
                    "path": "zbhip_submit (host buffers) + zbhip_run + zbhip_drain (80-B records, relabelled keys)"}
+    res["log_bytes"] = log_device_pass(xml, n, host_windows, local_rank, recs_per_batch)
+    return res
+
+
+def log_device_pass(xml, n, host_windows, local_rank, recs_per_batch):
+    """Submit -> log bytes: the same windows from host buffers, run with the records left in HBM
+    (ZBHIP_RUN_DEVICE_RECORDS) and serialised there (zbhip_serialize_log_device: the reference's
+    log entries, keys relabelled on the device); then once more with the bytes copied to host memory
+    (PCIe-inclusive).  A fresh partition; one untimed pass, then the timed passes."""
+    import ctypes as C
+    import time
+
+    import numpy as np
+
+    from zeebe_amd import abi
+    from zeebe_amd.engine import Partition
+
+    part = Partition(partition_id=1, partition_count=1, device=local_rank, max_instances=n, max_commands=n,
+                     max_records_per_batch=recs_per_batch)
+    part.deploy(xml)
+    if host_windows[0][1] is not None:
+        part.intern("amount")
+    pos = [np.arange(len(c), dtype=np.int64) * 2 + 1 for c, _ in host_windows]
+    host_buf = None
+    res = {}
+    for mode in ("warm", "hbm", "host"):
+        t0 = time.perf_counter()
+        total = 0
+        split = [0.0, 0.0, 0.0, 0.0]  # submit / run / serialise / copy
+        first = 1
+        for w, (cmds, docs) in enumerate(host_windows):
+            ta = time.perf_counter()
+            part.submit(cmds, docs)
+            tb = time.perf_counter()
+            part.run(abi.RUN_DEVICE_RECORDS | (abi.RUN_ACCUMULATE if w else 0))
+            tc = time.perf_counter()
+            ptr, used = part.serialize_log_device(pos[w], first, 1700000000123, copy=False)
+            td = time.perf_counter()
+            if mode == "host":
+                if host_buf is None or len(host_buf) < used:
+                    host_buf = C.create_string_buffer(int(used * 1.25) + 1)
+                part.L.zbhip_log_device_copy(part.h, host_buf, used)
+            te = time.perf_counter()
+            first += int(part.L.zbhip_pending_records(part.h))
+            total += used
+            for k, dt in enumerate((tb - ta, tc - tb, td - tc, te - td)):
+                split[k] += dt
+        sec = time.perf_counter() - t0
+        if mode != "warm":
+            trans = part.stats()["transitions"]
+            res[mode] = {"value": trans / sec, "unit": "transitions/s", "log_bytes_per_step": total,
+                         "log_GBps": total / sec / 1e9, "ms_per_step": sec * 1e3, "submit_ms": split[0] * 1e3,
+                         "run_ms": split[1] * 1e3, "serialize_ms": split[2] * 1e3, "copy_ms": split[3] * 1e3}
+    res["path"] = ("zbhip_submit (host buffers) + zbhip_run(DEVICE_RECORDS) + zbhip_serialize_log_device "
+                   "(log entries in HBM); 'host' adds zbhip_log_device_copy into host memory")
     return res
 
 

@@ -331,6 +331,8 @@ int32_t zbhip_subscription_partition(const char* bytes, size_t len, int32_t part
 #define ZBHIP_RUN_NO_RESULTS 1u  /* benchmarking: no D2H copy, no host wait, no key relabelling */
 #define ZBHIP_RUN_TIMED 2u       /* record HIP events around the lifecycle kernel launches */
 #define ZBHIP_RUN_ACCUMULATE 4u  /* keep accumulating statistics/timings of the previous runs */
+#define ZBHIP_RUN_DEVICE_RECORDS 8u /* results mode, but the records stay in HBM until a drain needs them
+                                       (zbhip_serialize_log_device reads them there) */
 /* Processes the submitted window to quiescence.  Returns #commands processed or <0. */
 int zbhip_run(zbhip_handle* h, uint32_t flags);
 

@@ -28,10 +28,10 @@ class Log:
         self.position = 100
         self.windows = 0
 
-    def window(self, cmds, docs=None, device=True):
+    def window(self, cmds, docs=None, device=True, flags=0):
         docs = docs if docs is not None else abi.make_docs(0)
         self.part.submit(cmds, docs)
-        self.part.run()
+        self.part.run(flags)
         pos = self.position + 2 * np.arange(len(cmds), dtype=np.int64)
         first = int(pos[-1]) + 1 if len(cmds) else self.position
         dev = self.part.serialize_log_device(pos, first, TS) if device else None
@@ -123,3 +123,24 @@ def test_a_skipped_window_turns_the_device_path_off():
     recs = log.window(create_commands(n), device=False)
     with pytest.raises(ZbhipError, match="EUNSUPP"):
         log.window(job_completions(recs, log.part))
+
+
+def test_records_left_in_hbm_and_device_windows():
+    # ZBHIP_RUN_DEVICE_RECORDS: the records stay in HBM for the device writer; a later drain copies
+    # them (the bytes and the drained records agree with the host path); windows submitted from
+    # device memory take the same path
+    import torch
+
+    n = 200
+    log = Log(bpmn.linear_process(3), n)
+    recs = log.window(create_commands(n), flags=abi.RUN_DEVICE_RECORDS)
+    recs = log.window(job_completions(recs, log.part), flags=abi.RUN_DEVICE_RECORDS)
+    c = job_completions(recs, log.part)
+    dev = torch.from_numpy(c.view(np.uint8).copy()).cuda()
+    log.part.submit_device(dev.data_ptr(), len(c))
+    log.part.run(abi.RUN_DEVICE_RECORDS)
+    pos = log.position + 2 * np.arange(len(c), dtype=np.int64)
+    first = int(pos[-1]) + 1
+    got = log.part.serialize_log_device(pos, first, TS)
+    recs = log.part.drain()
+    assert got == log.ser.serialize(recs, c, abi.make_docs(0), log.source_base, log.doc_base, pos, first, TS)

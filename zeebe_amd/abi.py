@@ -75,6 +75,7 @@ DEC_SCALE = 6
 RUN_NO_RESULTS = 1
 RUN_TIMED = 2
 RUN_ACCUMULATE = 4
+RUN_DEVICE_RECORDS = 8
 
 
 class DocEntry(C.Structure):

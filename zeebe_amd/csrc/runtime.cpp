@@ -212,6 +212,8 @@ struct zbhip_handle {
   std::vector<uint2> h_hdr;
   std::vector<uint2> h_out;
   std::vector<uint64_t> h_off;  // record offset of each command in h_out
+  size_t out_total = 0;         // records of the last run (in d_rec; in h_out once out_host)
+  bool out_host = false;
   size_t drain_cmd = 0, drain_rec = 0, drain_ord = 0;
   bool results = false;
 
@@ -1043,6 +1045,16 @@ static hipEvent_t next_event(zbhip_handle* h) {
   return h->tev[h->tev_used++];
 }
 
+// the last run's records in host memory (ZBHIP_RUN_DEVICE_RECORDS left them in HBM)
+static int ensure_out(zbhip_handle* h) {
+  if (h->out_host) return ZBHIP_OK;
+  h->h_out.resize(h->out_total);
+  if (h->out_total)
+    HIPCHK(hipMemcpy(h->h_out.data(), h->d_rec, h->out_total * sizeof(uint2), hipMemcpyDeviceToHost));
+  h->out_host = true;
+  return ZBHIP_OK;
+}
+
 // JOB_ACTIVATABLE bookkeeping of one processed command from its records: JOB:CREATED adds a job,
 // JOB:COMPLETED removes it (its ACTIVATED entry is dropped at the next window)
 static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
@@ -1082,6 +1094,8 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
     for (int64_t k : h->completed_activated) h->activated.erase(k);
     h->completed_activated.clear();
   }
+  if (h->job_index_on)
+    if (int rc = ensure_out(h)) return rc;
   const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
   if (h->hist.size() < subjects) {
     h->hist.resize(subjects);
@@ -1378,8 +1392,14 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   unsigned long long total = 0;
   HIPCHK(hipMemcpyAsync(&total, h->d_stats + 64 * 8, sizeof total, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  h->h_out.resize(total);
-  if (total) HIPCHK(hipMemcpy(h->h_out.data(), h->d_rec, total * sizeof(uint2), hipMemcpyDeviceToHost));
+  h->out_total = total;
+  h->out_host = false;
+  h->h_out.clear();
+  if (!(flags & ZBHIP_RUN_DEVICE_RECORDS)) {
+    h->h_out.resize(total);
+    if (total) HIPCHK(hipMemcpy(h->h_out.data(), h->d_rec, total * sizeof(uint2), hipMemcpyDeviceToHost));
+    h->out_host = true;
+  }
   h->stats_dirty = true;
 
   // record offset of every command: regions follow launch order, lanes follow the launch order
@@ -1406,7 +1426,7 @@ int64_t zbhip_pending_records(zbhip_handle* h) {
   if (!h || !h->results) return 0;
   int64_t pay = 0;
   for (auto& x : h->h_hdr2) pay += x.w;  // payload rows of message records
-  return (int64_t)h->h_out.size() - pay;
+  return (int64_t)h->out_total - pay;
 }
 
 int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
@@ -1549,6 +1569,7 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
   if (n_out) *n_out = 0;
   if (!h->results) return ZBHIP_ESTATE;
   if (int rc = finalize(h)) return rc;
+  if (int rc = ensure_out(h)) return rc;
   if (!h->msg() && h->drain_cmd == 0 && h->drain_rec == 0 && h->h_out.size() >= kBulkDrainMin &&
       cap >= h->h_out.size()) {
     // whole window at once: record i of command c goes to out[first(c) + i] (one row per record
@@ -2620,7 +2641,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   const bool fill = h->ring_filled + 1 == h->windows_run;  // every earlier window's keys are in the ring
   if (!fill) h->ring_ok = false;
   h->ring_filled = h->windows_run;  // this window is accounted for, whether or not it is written here
-  if (h->msg() || !h->cont_cmds.empty() || h->external) h->ring_ok = false;
+  if (h->msg() || !h->cont_cmds.empty()) h->ring_ok = false;
   if (!h->ring_ok) return ZBHIP_EUNSUPP;
   if (int rc = finalize(h)) return rc;
   const size_t n = h->n_cmds;
@@ -2697,7 +2718,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   a.n = (uint32_t)n;
   a.arena = h->d_log_arena;
   a.idx = h->d_log_idx;
-  a.docs = h->d_docs;
+  a.docs = h->external ? h->ext_docs : h->d_docs;
   a.n_docs = (uint32_t)h->n_docs;
   a.inst_proc = h->d_inst_proc;
   a.ring = h->d_ring;
