@@ -42,6 +42,7 @@ struct LogParams {
   uint32_t n;
   const uint8_t* arena;         // byte runs, each 4-aligned
   const uint32_t* idx;          // run table (see log_device_tables)
+  uint32_t arena_words, idx_words;  // sizes (the kernels stage both in LDS when they fit)
   const zbhip_doc_entry* docs;  // the window's document entries
   uint32_t n_docs;
   const uint16_t* inst_proc;    // [n_inst] process of each instance slot (NONE: free)
@@ -75,42 +76,47 @@ __device__ __forceinline__ uint2 name_run(const LogParams& L, uint32_t id) {
 // ---- byte sinks: a counter, or 8-byte little-endian stores ---------------------------------
 struct Count {
   unsigned long long n = 0;
+  __device__ __forceinline__ void put(uint32_t, uint32_t k) { n += k; }
   __device__ __forceinline__ void b(uint32_t) { ++n; }
   __device__ __forceinline__ void bytes(const LogParams&, uint2 r) { n += r.y; }
   __device__ __forceinline__ void zeros(uint32_t k) { n += k; }
 };
+// appends up to four bytes at a time into a 64-bit accumulator, stored when it fills
 struct Write {
   uint64_t* p;
   uint64_t acc = 0;
   uint32_t nb = 0;
-  __device__ __forceinline__ void b(uint32_t x) {
-    acc |= (uint64_t)(x & 0xFFu) << (8 * nb);
-    if (++nb == 8) {
+  __device__ __forceinline__ void put(uint32_t v, uint32_t k) {  // the k (1..4) low bytes of v
+    const uint64_t x = k == 4 ? (uint64_t)v : (uint64_t)(v & ((1u << (8 * k)) - 1));
+    acc |= x << (8 * nb);
+    nb += k;
+    if (nb >= 8) {
       *p++ = acc;
-      acc = 0;
-      nb = 0;
+      nb -= 8;
+      acc = nb ? x >> (8 * (k - nb)) : 0;
     }
   }
+  __device__ __forceinline__ void b(uint32_t x) { put(x, 1); }
   __device__ __forceinline__ void bytes(const LogParams& L, uint2 r) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(L.arena + r.x);
-    for (uint32_t i = 0; i < r.y; i += 4) {
-      const uint32_t v = w[i >> 2];
-      const uint32_t k = r.y - i < 4 ? r.y - i : 4;
-      for (uint32_t j = 0; j < k; ++j) b(v >> (8 * j));
-    }
+    for (uint32_t i = 0; i < r.y; i += 4) put(w[i >> 2], r.y - i < 4 ? r.y - i : 4);
   }
   __device__ __forceinline__ void zeros(uint32_t k) {
-    for (uint32_t i = 0; i < k; ++i) b(0);
+    for (uint32_t i = 0; i < k; i += 4) put(0, k - i < 4 ? k - i : 4);
   }
 };
 
 template <class S>
 __device__ __forceinline__ void le(S& s, unsigned long long v, int n) {
-  for (int i = 0; i < n; ++i) s.b((uint32_t)(v >> (8 * i)));
+  if (n == 8) { s.put((uint32_t)v, 4); s.put((uint32_t)(v >> 32), 4); }
+  else s.put((uint32_t)v, (uint32_t)n);
 }
 template <class S>
 __device__ __forceinline__ void be(S& s, unsigned long long v, int n) {
-  for (int i = n - 1; i >= 0; --i) s.b((uint32_t)(v >> (8 * i)));
+  if (n == 8) { s.put(__builtin_bswap32((uint32_t)(v >> 32)), 4); s.put(__builtin_bswap32((uint32_t)v), 4); }
+  else if (n == 4) s.put(__builtin_bswap32((uint32_t)v), 4);
+  else if (n == 2) s.put(((uint32_t)(v >> 8) & 0xFF) | (((uint32_t)v & 0xFF) << 8), 2);
+  else s.put((uint32_t)v, 1);
 }
 
 // MsgPackWriter.writeInteger (:154-212): the smallest encoding
@@ -425,7 +431,21 @@ __device__ __forceinline__ bool entry(S& s, const LogParams& L, const LogCmd& m,
   return true;
 }
 
+// the tables in LDS (every run is read byte by byte; from HBM each word is a dependent round trip)
+constexpr uint32_t kLdsTableWords = 12 * 1024;  // 48 KB
+__device__ __forceinline__ void stage_tables(LogParams& L, uint32_t* lds) {
+  if (L.arena_words + L.idx_words > kLdsTableWords) return;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(L.arena);
+  for (uint32_t i = threadIdx.x; i < L.arena_words; i += blockDim.x) lds[i] = a[i];
+  for (uint32_t i = threadIdx.x; i < L.idx_words; i += blockDim.x) lds[L.arena_words + i] = L.idx[i];
+  __syncthreads();
+  L.arena = reinterpret_cast<const uint8_t*>(lds);
+  L.idx = lds + L.arena_words;
+}
+
 __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
+  extern __shared__ uint32_t tables[];
+  stage_tables(L, tables);
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= L.n) return;
   const LogCmd m = L.cmds[c];
@@ -441,6 +461,8 @@ __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
 }
 
 __global__ __launch_bounds__(256) void k_log_write(LogParams L) {
+  extern __shared__ uint32_t tables[];
+  stage_tables(L, tables);
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= L.n) return;
   const LogCmd m = L.cmds[c];
@@ -521,17 +543,19 @@ __global__ __launch_bounds__(256) void k_ring_add(LogParams L) {
 }
 
 hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
-  LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.docs, a.n_docs, a.inst_proc, a.ring, a.kpi, a.n_inst, a.pbits,
-              a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]}, a.bytes, a.out, a.flag};
+  LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.arena_words, a.idx_words, a.docs, a.n_docs, a.inst_proc, a.ring,
+              a.kpi, a.n_inst, a.pbits, a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]},
+              a.bytes, a.out, a.flag};
   const uint32_t g = (a.n + 255) / 256;
+  const size_t lds = a.arena_words + a.idx_words <= kLdsTableWords ? (size_t)(a.arena_words + a.idx_words) * 4 : 0;
   if (a.phase == 0) {  // sizes and byte offsets
-    if (a.n) hipLaunchKernelGGL(k_log_sizes, dim3(g), dim3(256), 0, s, L);
+    if (a.n) hipLaunchKernelGGL(k_log_sizes, dim3(g), dim3(256), lds, s, L);
     const uint32_t nb = (a.n + kLogScanB - 1) / kLogScanB;
     if (a.n) hipLaunchKernelGGL(k_log_block_sums, dim3(nb), dim3(kLogScanB), 0, s, a.bytes, a.n, a.block_sums);
     hipLaunchKernelGGL(k_log_scan_sums, dim3(1), dim3(64), 0, s, a.block_sums, nb, a.bytes + a.n);
     if (a.n) hipLaunchKernelGGL(k_log_apply, dim3(nb), dim3(kLogScanB), 0, s, a.bytes, a.n, a.block_sums);
   } else if (a.phase == 1) {
-    if (a.n) hipLaunchKernelGGL(k_log_write, dim3(g), dim3(256), 0, s, L);
+    if (a.n) hipLaunchKernelGGL(k_log_write, dim3(g), dim3(256), lds, s, L);
   } else {
     if (a.n) hipLaunchKernelGGL(k_ring_create, dim3(g), dim3(256), 0, s, L);
     if (a.n) hipLaunchKernelGGL(k_ring_add, dim3(g), dim3(256), 0, s, L);

@@ -9,6 +9,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -247,6 +248,7 @@ struct zbhip_handle {
   uint32_t* d_log_idx = nullptr;
   size_t log_arena_cap = 0, log_idx_cap = 0;
   size_t log_tables_procs = ~(size_t)0, log_tables_names = ~(size_t)0;
+  uint32_t log_arena_words = 0, log_idx_words = 0;
   unsigned long long* d_ring = nullptr;  // [16][max_instances] key ring + [max_instances] PI keys
   uint16_t* d_inst_proc = nullptr;
   LogCmd* d_logcmd = nullptr;
@@ -1082,6 +1084,53 @@ static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
   }
 }
 
+// The whole bookkeeping of a plain window at once (no message subjects, no job index): key bases
+// in log order (a sequential prefix), then the per-instance histories, processes and generations on
+// host threads -- each thread owns the instances i % T == t and walks the window in log order, so
+// every instance sees its commands in order -- and the resolve table filled at precomputed places.
+static void advance_window_parallel(zbhip_handle* h) {
+  const size_t n = h->n_cmds;
+  std::vector<uint32_t> bpos(n, ~0u);
+  int64_t kc = h->key_counter;
+  size_t nb = 0;
+  for (size_t c = 0; c < n; ++c) {
+    const uint2 hd = h->h_hdr[c];
+    h->h_base[c] = kc;
+    if (((hd.y >> 16) & 0xFF) == ST_OK) {
+      const uint32_t nk = hd.x >> 16;
+      if (nk) bpos[c] = (uint32_t)nb++;
+      kc += nk;
+    } else {
+      kc += h->ext_keys[c];
+    }
+  }
+  const size_t b0 = h->batches.size();
+  h->batches.resize(b0 + nb);
+  const uint32_t N = h->cfg.max_instances;
+  parallel_for(host_threads(), [&](unsigned t, unsigned T) {
+    for (size_t c = 0; c < n; ++c) {
+      const zbhip_command& cm = h->h_cmds[c];
+      const uint32_t inst = cm.instance;
+      if (inst >= N || inst % T != t) continue;
+      const uint2 hd = h->h_hdr[c];
+      if (((hd.y >> 16) & 0xFF) != ST_OK) continue;
+      const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
+      if (cm.kind == ZBHIP_CMD_CREATE) {  // a new instance in the slot: its own key history
+        h->hist[inst].clear();
+        h->inst_proc[inst] = cm.ref;
+        ++h->inst_gen[inst];
+      }
+      if (nkeys) {
+        h->hist[inst].push_back({(uint16_t)first, h->h_base[c] + 1});
+        h->batches[b0 + bpos[c]] = {h->h_base[c] + 1, inst, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[inst]};
+      }
+      if (hd.y & HDR_ENDED) ++h->inst_gen[inst];  // completed: its job keys no longer resolve
+    }
+  });
+  h->key_counter = kc;
+  h->fin_next = n;
+}
+
 // Key relabelling bookkeeping of the last run, in log (source) order: each command's first key
 // (DbKeyGenerator order), the subjects' key histories and the resolve_key table.  It advances
 // lazily, command by command: up to `limit`, and never past a fallback command whose CPU-engine keys
@@ -1103,6 +1152,13 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
     h->inst_gen.resize(subjects, 0);
   }
   const size_t n = std::min(limit, h->n_cmds);
+  if (h->fin_next == 0 && n == h->n_cmds && !h->msg() && !h->job_index_on && n >= (1u << 16)) {
+    bool all_declared = true;  // the whole window can be done now (fallback keys declared, or forced)
+    if (!force)
+      for (size_t c = 0; c < n && all_declared; ++c)
+        all_declared = ((h->h_hdr[c].y >> 16) & 0xFF) == ST_OK || h->declared[c];
+    if (all_declared) advance_window_parallel(h);
+  }
   for (size_t c = h->fin_next; c < n; ++c) {
     const uint2 hd = h->h_hdr[c];
     const zbhip_command& cm = h->h_cmds[c];
@@ -2643,7 +2699,11 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   h->ring_filled = h->windows_run;  // this window is accounted for, whether or not it is written here
   if (h->msg() || !h->cont_cmds.empty()) h->ring_ok = false;
   if (!h->ring_ok) return ZBHIP_EUNSUPP;
+  const bool dbg = getenv("ZBHIP_DEBUG") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  const auto t0 = now();
   if (int rc = finalize(h)) return rc;
+  const auto t1 = now();
   const size_t n = h->n_cmds;
   const size_t N = h->cfg.max_instances;
   if (w->n_cmds != n) return ZBHIP_EINVAL;
@@ -2669,6 +2729,8 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     HIPCHK(hipStreamSynchronize(h->stream));
     h->log_tables_procs = h->procs.size();
     h->log_tables_names = h->names.size();
+    h->log_arena_words = (uint32_t)(arena.size() / 4);
+    h->log_idx_words = (uint32_t)idx.size();
   }
   if (!h->d_ring) {
     const size_t words = (size_t)16 * N + N;  // logdev.hip kRing = 16
@@ -2680,11 +2742,12 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     HIPCHK(hipMemsetAsync(h->d_ring, 0, words * sizeof(unsigned long long), h->stream));
   }
   // the window's command table: rows, record positions, key bases, the prev chain per instance
+  // (a window of one round has one command per instance: no chain, and it is filled on host threads)
   h->h_logcmd.resize(n);
   if (h->log_prev.size() < N) h->log_prev.assign(N, ~0ull);
   const uint64_t win = h->windows_run;
-  uint64_t out_rec = 0;
-  for (size_t c = 0; c < n; ++c) {
+  const bool one_round = h->round_begin.empty();
+  auto fill_cmd = [&](size_t c, uint64_t out_rec) {
     const uint2 hd = h->h_hdr[c];
     const zbhip_command& cm = h->h_cmds[c];
     const bool ok = ((hd.y >> 16) & 0xFF) == ST_OK;
@@ -2701,13 +2764,34 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     m.doc_begin = cm.doc_begin;
     m.pad = 0;
     m.prev = ~0u;
-    if (cm.instance < N) {
-      const uint64_t lp = h->log_prev[cm.instance];
-      if ((lp >> 32) == (win & 0xFFFFFFFFu)) m.prev = (uint32_t)lp;
-      h->log_prev[cm.instance] = ((win & 0xFFFFFFFFu) << 32) | (uint32_t)c;
+    return (uint64_t)m.nrec;
+  };
+  if (one_round) {
+    const unsigned T = host_threads();
+    std::vector<uint64_t> part(T + 1, 0);
+    parallel_for(T, [&](unsigned t, unsigned TT) {  // records per thread range, then each range from its base
+      uint64_t s = 0;
+      for (size_t c = n * t / TT; c < n * (t + 1) / TT; ++c) s += h->h_hdr[c].x & 0xFFFF;
+      part[t + 1] = s;
+    });
+    for (unsigned t = 0; t < T; ++t) part[t + 1] += part[t];
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      uint64_t out_rec = part[t];
+      for (size_t c = n * t / TT; c < n * (t + 1) / TT; ++c) out_rec += fill_cmd(c, out_rec);
+    });
+  } else {
+    uint64_t out_rec = 0;
+    for (size_t c = 0; c < n; ++c) {
+      out_rec += fill_cmd(c, out_rec);
+      const uint32_t inst = h->h_cmds[c].instance;
+      if (inst < N) {
+        const uint64_t lp = h->log_prev[inst];
+        if ((lp >> 32) == (win & 0xFFFFFFFFu)) h->h_logcmd[c].prev = (uint32_t)lp;
+        h->log_prev[inst] = ((win & 0xFFFFFFFFu) << 32) | (uint32_t)c;
+      }
     }
-    out_rec += m.nrec;
   }
+  const auto t2 = now();
   if (n) HIPCHK(hipMemcpyAsync(h->d_logcmd, h->h_logcmd.data(), n * sizeof(LogCmd), hipMemcpyHostToDevice, h->stream));
   if (h->inst_proc.size() >= N)
     HIPCHK(hipMemcpyAsync(h->d_inst_proc, h->inst_proc.data(), N * sizeof(uint16_t), hipMemcpyHostToDevice, h->stream));
@@ -2718,6 +2802,8 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   a.n = (uint32_t)n;
   a.arena = h->d_log_arena;
   a.idx = h->d_log_idx;
+  a.arena_words = h->log_arena_words;
+  a.idx_words = h->log_idx_words;
   a.docs = h->external ? h->ext_docs : h->d_docs;
   a.n_docs = (uint32_t)h->n_docs;
   a.inst_proc = h->d_inst_proc;
@@ -2738,6 +2824,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   HIPCHK(hipMemcpyAsync(&total, h->d_log_bytes + n, sizeof total, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(&flag, h->d_log_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  const auto t3 = now();
   int rc = ZBHIP_OK;
   if (flag) {
     rc = ZBHIP_EUNSUPP;  // a key the ring does not hold, or a value outside the device writer
@@ -2759,6 +2846,12 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   a.phase = 2;  // the window's keys into the ring, in any case
   HIPCHK(launch_log_device(a, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  if (dbg) {
+    const auto t4 = now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[zbhip] serialize_log_device n=%zu: finalize %.2f ms, table %.2f ms, upload+sizes %.2f ms, write+ring %.2f ms\n",
+            n, ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
+  }
   return rc;
 }
 

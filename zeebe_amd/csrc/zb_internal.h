@@ -216,6 +216,7 @@ struct LogLaunch {
   uint32_t n;
   const uint8_t* arena;
   const uint32_t* idx;
+  uint32_t arena_words, idx_words;
   const zbhip_doc_entry* docs;
   uint32_t n_docs;
   const uint16_t* inst_proc;
