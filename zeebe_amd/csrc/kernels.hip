@@ -787,7 +787,7 @@ __device__ __forceinline__ int find_row(const Lane<K>& L, uint32_t slot, uint32_
   const StepParams& P = *L.sp;
   int found = -1;
   for (int r = kSubs - 1; r >= 0; --r) {
-    const uint4 a = P.st.sub_a[(size_t)r * P.st.n_slots + slot];
+    const uint4 a = P.st.sub_a[sub_ri(r, slot)];
     if (((a.x & 0xFF) == 1 || (a.x & 0xFF) == 2) && (a.x >> 16) == pi_part && a.z == inst && (a.w & 0xFFFF) == eord && (a.y & 0xFFFF) == name)
       found = r;
   }
@@ -905,7 +905,7 @@ __device__ __forceinline__ void ms_correlate(Lane<K>& L, uint32_t slot, uint32_t
     return;
   }
   if (r == kSubs) { set_fail(L, FB_MESSAGE); return; }  // correlate of a row opened in this very batch
-  const size_t ri = (size_t)r * P.st.n_slots + slot;
+  const size_t ri = sub_ri(r, slot);
   const uint4 a = P.st.sub_a[ri];
   const longlong2 b = P.st.sub_b[ri];
   const longlong2 k = P.st.sub_k[ri];
@@ -946,7 +946,7 @@ __device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint3
     unsigned long long bk = ~0ull;
     for (int r = 0; r < kSubs; ++r) {
       if ((done >> r) & 1) continue;
-      const size_t ri = (size_t)r * P.st.n_slots + slot;
+      const size_t ri = sub_ri(r, slot);
       const uint4 a = P.st.sub_a[ri];
       if (!((a.x & 0xFF) == 1 || (a.x & 0xFF) == 2) || (a.y & 0xFFFF) != name) { done |= 1u << r; continue; }
       const unsigned long long o = eik_order(P.st.sub_b[ri].x, a.x >> 16);
@@ -954,7 +954,7 @@ __device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint3
     }
     if (best < 0) break;
     done |= 1u << best;
-    const size_t ri = (size_t)best * P.st.n_slots + slot;
+    const size_t ri = sub_ri(best, slot);
     const uint4 a = P.st.sub_a[ri];
     bool seen = false;
     for (uint32_t j = 0; j < nch; ++j) seen |= bpmn_seen[j] == (a.y >> 16);
@@ -968,7 +968,7 @@ __device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint3
   L.op_corr_msg = msg_ref;
   // sendCorrelateCommand: SubscriptionCommandSender.correlateProcessMessageSubscription
   for (uint32_t j = 0; j < nch; ++j) {
-    const size_t ri = (size_t)chosen[j] * P.st.n_slots + slot;
+    const size_t ri = sub_ri(chosen[j], slot);
     const uint4 a = P.st.sub_a[ri];
     const longlong2 b = P.st.sub_b[ri];
     const uint32_t target = a.x >> 16;
@@ -1523,14 +1523,13 @@ __device__ __forceinline__ void message_command(Lane<K>& L, uint32_t kind, uint3
 template <class K>
 __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
   const StepParams& P = *L.sp;
-  const uint32_t S = P.st.n_slots;
   uint32_t patch_mask = 0, patch_slot = L.op_slot, patch_what = 0;  // bit 0: sub_b, bit 1: sub_k
   if (L.op_ins) {
     int got = -1;
     for (int r = 0; r < kSubs && got < 0; ++r)
-      if (atomicCAS(&P.st.sub_a[(size_t)r * S + L.op_slot].x, 0u, 3u) == 0u) got = r;
+      if (atomicCAS(&P.st.sub_a[sub_ri(r, L.op_slot)].x, 0u, 3u) == 0u) got = r;
     if (got < 0) { set_fail(L, FB_MESSAGE); return; }  // correlation slot full
-    const size_t ri = (size_t)got * S + L.op_slot;
+    const size_t ri = sub_ri(got, L.op_slot);
     P.st.sub_b[ri] = make_longlong2(L.ins_eik, L.ins_pik);
     P.st.sub_k[ri] = make_longlong2(L.ins_key, -1);
     // the row in one 16-byte store, state included.  No release fence: on gfx950 an agent-scope
@@ -1548,7 +1547,7 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
   if (L.op_corr_mask) {
     for (int r = 0; r < kSubs; ++r)
       if ((L.op_corr_mask >> r) & 1) {
-        const size_t ri = (size_t)r * S + L.slot;
+        const size_t ri = sub_ri(r, L.slot);
         P.st.sub_k[ri].y = L.op_corr_msg;
         uint4 a = P.st.sub_a[ri];
         P.st.sub_a[ri].x = (a.x & ~0xFFu) | 2u;
@@ -1559,7 +1558,7 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
   }
   if (L.op_rm_mask) {
     for (int r = 0; r < kSubs; ++r)
-      if ((L.op_rm_mask >> r) & 1) P.st.sub_a[(size_t)r * S + L.op_rm_slot] = make_uint4(0, 0, 0, 0);
+      if ((L.op_rm_mask >> r) & 1) P.st.sub_a[sub_ri(r, L.op_rm_slot)] = make_uint4(0, 0, 0, 0);
     patch_mask &= ~(L.op_rm_slot == patch_slot ? L.op_rm_mask : 0u);
   }
   if (patch_mask && L.ci >= P.xcap) { set_fail(L, FB_MESSAGE); return; }
@@ -2378,7 +2377,7 @@ __global__ __launch_bounds__(256) void k_key_patch(KeyScanParams K) {
       // array left alone saves a read-modify-write of a line
       for (int r = 0; r < kSubs; ++r)
         if ((mask >> r) & 1) {
-          const size_t ri = (size_t)r * K.n_slots + slot;
+          const size_t ri = sub_ri(r, slot);
           if (what & 1) {
             const longlong2 bb = K.sub_b[ri];
             K.sub_b[ri] = make_longlong2(resolve_own(K, bb.x, c, h, h2, base), resolve_own(K, bb.y, c, h, h2, base));

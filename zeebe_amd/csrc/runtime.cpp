@@ -2114,7 +2114,7 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   // [tenant, name, correlationKey, eik] of this (message) partition (DbMessageSubscriptionState)
   for (size_t slot = 0; slot < S; ++slot)
     for (int r = 0; r < kSubs; ++r) {
-      const size_t ri = (size_t)r * S + slot;
+      const size_t ri = sub_ri(r, slot);
       const uint4 a = sub_a[ri];
       const uint32_t st = a.x & 0xFF;
       if (st != 1 && st != 2) continue;

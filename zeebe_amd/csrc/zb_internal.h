@@ -29,6 +29,9 @@ constexpr uint32_t kTplWords = kTplRec + 2;  // uint2 per variant
 constexpr int kTplLdsProcs = 2;
 constexpr uint32_t kTplLdsWords = 64;
 constexpr uint32_t TPL_OK = 1u << 31;        // program header word 7: bit 31 eligible, bits 0..11 gateway
+// row r of correlation slot s in sub_a / sub_b / sub_k: slot-major, so a slot's kSubs rows share
+// one cache line per array (a lookup reads 3 lines, not 3 * kSubs)
+__host__ __device__ inline size_t sub_ri(uint32_t r, size_t slot) { return slot * kSubs + r; }
 constexpr int kOut = 6;            // outbox entries per command (sends + local-row key patches)
 constexpr uint8_t XK_PATCH = 0xFF; // outbox entry kind: patch the real keys of a locally inserted row
 constexpr uint32_t kNoElem = 0xFFF;       // element field of records without an element
