@@ -112,3 +112,25 @@ def test_batch_limit_disables_the_template():
     assert part.deploy(xml) == orc.deploy(xml) == 0
     used = windows(part, orc, [(create_commands(n), None) for _ in range(3)])
     assert used == [0, 0, 0]
+
+
+def test_interleaved_processes_in_every_wave():
+    # two template processes (and both outcomes of the gateway) side by side in every wave: each
+    # (process, outcome) gets recorded, so the second window is served from templates entirely
+    n = 512
+    part, orc = Partition(max_instances=n, max_commands=n, max_records_per_batch=128), Oracle()
+    for e in (part, orc):
+        e.deploy(bpmn.fork_join_process(3), process_definition_key=2251799813685249)
+        e.deploy(bpmn.xor_process(), process_definition_key=2251799813685250)
+    name = part.intern("amount")
+    assert orc.intern("amount") == name
+    rng = np.random.default_rng(17)
+    batches = []
+    for _ in range(3):
+        c = create_commands(n)
+        c["ref"] = np.arange(n) % 2
+        c["doc_count"] = np.arange(n) % 2
+        c["doc_begin"] = np.arange(n)
+        batches.append((c, amount_docs(rng.integers(0, 2000, n), name)))
+    used = windows(part, orc, batches)
+    assert used[1] == n and used[2] == n

@@ -1356,16 +1356,14 @@ __device__ __forceinline__ int tpl_create(Lane<K>& L, uint32_t doc_count, uint32
 template <class K>
 __device__ __forceinline__ void tpl_record(Lane<K>& L, uint32_t v, uint32_t name, uint2* tpl_lds) {
   const StepParams& P = *L.sp;
-  const bool want = !(L.fail || L.pi_live || !L.completed || L.nrec > (uint32_t)kTplRec || L.nrec > L.rec_cap);
+  uint2* t = tpl_at<K>(P, L.proc, v);
+  uint2* tl = L.proc < (uint32_t)kTplLdsProcs ? tpl_lds + ((size_t)L.proc * kTplVar + v) * kTplLdsWords : nullptr;
+  // candidates: a recordable batch whose template this workgroup has not seen recorded or tried
+  const bool want = !(L.fail || L.pi_live || !L.completed || L.nrec > (uint32_t)kTplRec || L.nrec > L.rec_cap) &&
+                    (!tl || tl[0].x == 0) && *reinterpret_cast<volatile uint32_t*>(t) == 0u;
   const unsigned long long m = __ballot(want);
   if (!want || (threadIdx.x & 63) != (uint32_t)__builtin_ctzll(m)) return;
-  if (L.proc < (uint32_t)kTplLdsProcs) {
-    uint2* tl = tpl_lds + ((size_t)L.proc * kTplVar + v) * kTplLdsWords;
-    if (tl[0].x != 0) return;  // this workgroup saw it recorded, or tried already
-    tl[0].x = 1;
-  }
-  uint2* t = tpl_at<K>(P, L.proc, v);
-  if (*reinterpret_cast<volatile uint32_t*>(t) != 0u) return;
+  if (tl) tl[0].x = 1;  // tried by this workgroup
   if (atomicCAS(reinterpret_cast<uint32_t*>(t), 0u, 1u) != 0u) return;  // recorded (or claimed) already
   bool clean = true;
   for (uint32_t j = 0; j < L.nrec; ++j) {
