@@ -11,8 +11,9 @@ ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
 
 
 class _Gen:
-    def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False):
+    def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True):
         self.rng = rng
+        self.tasks = tasks
         self.pass_through = pass_through
         self.max_depth = max_depth
         self.max_blocks = max_blocks
@@ -58,7 +59,7 @@ class _Gen:
 
     def block(self, cur, depth, width):
         r = self.rng
-        choices = ["task", "task"]
+        choices = ["task", "task"] if self.tasks else ["pass"]
         if depth < self.max_depth:
             choices += ["xor", "xor"]
             if width * 2 <= 8 and self.join_slots + 4 <= 16:
@@ -110,8 +111,10 @@ class _Gen:
         return join
 
 
-def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False):
-    g = _Gen(rng, max_depth, max_blocks, messages, pass_through)
+def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False,
+                   tasks=True):
+    """tasks=False: no wait states (the CREATE batch runs the instance to its end)."""
+    g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks)
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")

@@ -134,3 +134,40 @@ def test_interleaved_processes_in_every_wave():
         batches.append((c, amount_docs(rng.integers(0, 2000, n), name)))
     used = windows(part, orc, batches)
     assert used[1] == n and used[2] == n
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_straight_through_processes(seed):
+    # random processes without wait states (gateways, pass-through elements, nested): three CREATE
+    # windows with documents; records and state equal to the oracle's, and every window's device log
+    # bytes equal to the host serialiser's
+    from random_bpmn import random_process
+
+    rng = np.random.default_rng(4000 + seed)
+    xml = random_process(rng, tasks=False)
+    n = 128
+    # a straight-through batch of these processes can run to a few hundred records
+    part, orc = Partition(max_instances=n, max_commands=n, max_records_per_batch=1024), Oracle()
+    assert part.deploy(xml) == orc.deploy(xml) == 0
+    name = part.intern("amount")
+    assert orc.intern("amount") == name
+    ser = part.log_serializer()
+    base = 0
+    for w in range(3):
+        c = create_commands(n)
+        c["doc_count"] = 1
+        c["doc_begin"] = np.arange(n)
+        d = amount_docs(rng.integers(0, 1000, n), name)
+        part.submit(c, d)
+        part.run()
+        pos = 1 + 2 * np.arange(n, dtype=np.int64)
+        dev = part.serialize_log_device(pos, 2 * n + 1, 1700000000123)
+        got = part.drain()
+        assert dev == ser.serialize(got, c, d, base, base, pos, 2 * n + 1, 1700000000123)
+        base += n
+        orc.clear_records()
+        orc.submit(c, d)
+        orc.run()
+        assert_same_records(got, orc.records(), part, orc)
+        assert part.fallback() == []
+        assert part.state() == orc.state()
