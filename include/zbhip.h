@@ -154,6 +154,10 @@ typedef struct zbhip_element {
   uint16_t id;           /* string-table index of the element id */
   uint16_t message_name; /* message catch event: string-table index of the static message name; else NONE */
   uint16_t correlation_var; /* message catch event: string-table index of the variable of `= var` */
+  uint16_t flow_scope;   /* the element's container: 0 = the process, else the embedded sub-process
+                          * element (ExecutableFlowElement.getFlowScope, FlowElementInstantiationTransformer) */
+  uint16_t start_event;  /* process / embedded sub-process: its none start event
+                          * (ExecutableFlowElementContainer.getNoneStartEvent); else ZBHIP_NONE16 */
 } zbhip_element;
 
 /* FEEL condition bytecode (subset of feel-scala 1.17.0 boolean expressions,

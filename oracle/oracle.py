@@ -129,6 +129,11 @@ class Oracle:
     def element_id(self, proc, elem):
         return self.L.zbo_element_id(self.h, proc, elem).decode()
 
+    def element_type(self, proc, elem):
+        t, ev, r = C.c_int(), C.c_int(), C.c_int()
+        self.L.zbo_element_info(self.h, proc, elem, C.byref(t), C.byref(ev), C.byref(r))
+        return t.value
+
     def string_value(self, sid):
         n = C.c_size_t()
         p = self.L.zbo_string_value(self.h, sid, C.byref(n))

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <set>
@@ -331,6 +332,8 @@ struct OEl {
   std::string job_type;
   int retries = 3;
   std::string msg_name, corr_var;  // message catch event (MessageTransformer.java:30-60)
+  int scope = 0;                   // flow scope element (ExecutableFlowElement.getFlowScope): 0 = process
+  int start = -1;                  // process / sub-process: getNoneStartEvent
 };
 
 struct OProc {
@@ -356,11 +359,15 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
   P.els.push_back(std::move(pe));
   std::unordered_map<std::string, int> idx;
   idx[P.bpmn_id] = 0;
-  std::vector<const XNode*> flows;
-  for (auto& k : proc.kids) {
+  std::vector<const XNode*> flows, xgws;
+  // FlowElementInstantiationTransformer over every container (the process and its embedded
+  // sub-processes, SubProcessTransformer): elements numbered in document pre-order
+  std::function<bool(const XNode&, int)> walk = [&](const XNode& parent, int scope) -> bool {
+  for (auto& k : parent.kids) {
     const std::string& n = k->name;
     OEl e;
     e.id = k->attr("id");
+    e.scope = scope;
     if (n == "startEvent") {
       e.type = ZBHIP_EL_START_EVENT;
       // StartEventTransformer.java:40 — event type from the event definition
@@ -430,27 +437,49 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_NONE;
+    } else if (n == "subProcess") {
+      // embedded sub-process only (SubProcessProcessor): no event sub-process, no loop, no mappings
+      e.type = ZBHIP_EL_SUB_PROCESS;
+      if (k->attr("triggeredByEvent") == "true") { err = "event sub-process outside the supported subset"; return false; }
+      if (k->child("multiInstanceLoopCharacteristics") || k->child("standardLoopCharacteristics")) {
+        err = "multi-instance outside the supported subset";
+        return false;
+      }
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
     } else if (n == "exclusiveGateway") {
       e.type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
+      xgws.push_back(k.get());
     } else if (n == "parallelGateway") {
       e.type = ZBHIP_EL_PARALLEL_GATEWAY;
     } else if (n == "sequenceFlow") {
       e.type = ZBHIP_EL_SEQUENCE_FLOW;
       flows.push_back(k.get());
     } else if (n == "extensionElements" || n == "documentation" || n == "textAnnotation" ||
-               n == "association") {
+               n == "association" || n == "incoming" || n == "outgoing") {
       continue;
     } else {
       err = "element <" + n + "> outside the supported subset";
       return false;
     }
     if (e.id.empty()) { err = "element without id"; return false; }
-    idx[e.id] = (int)P.els.size();
+    const int self = (int)P.els.size();
+    const int type = e.type, event = e.event;
+    idx[e.id] = self;
     P.els.push_back(std::move(e));
+    if (type == ZBHIP_EL_SUB_PROCESS) {
+      if (!walk(*k, self)) return false;
+      if (P.els[self].start < 0) { err = "sub-process without a none start event"; return false; }
+    } else if (type == ZBHIP_EL_START_EVENT && event == ZBHIP_EV_NONE) {
+      P.els[scope].start = self;
+    }
   }
+  return true;
+  };
+  if (!walk(proc, 0)) return false;
   // gateway default flows (ExclusiveGatewayTransformer.transformDefaultFlow)
-  for (auto& k : proc.kids) {
-    if (k->name == "exclusiveGateway" && !k->attr("default").empty()) {
+  for (const XNode* k : xgws) {
+    if (!k->attr("default").empty()) {
       auto it = idx.find(k->attr("default"));
       if (it == idx.end()) { err = "unknown default flow"; return false; }
       P.els[idx[k->attr("id")]].default_flow = it->second;
@@ -464,6 +493,10 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
     auto t = idx.find(f->attr("targetRef"));
     if (s == idx.end() || t == idx.end()) { err = "flow with unknown source/target"; return false; }
     OEl& fe = P.els[fi];
+    if (P.els[s->second].scope != fe.scope || P.els[t->second].scope != fe.scope) {
+      err = "sequence flow crossing a sub-process boundary";
+      return false;
+    }
     fe.src = s->second;
     fe.tgt = t->second;
     // SequenceFlowTransformer.parseCondition: runs before connectWithFlowNodes
@@ -484,8 +517,7 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       P.els[fe.src].out_with_cond.push_back(fi);  // ExecutableExclusiveGateway.addOutgoing
     P.els[fe.tgt].in.push_back(fi);
   }
-  for (size_t i = 1; i < P.els.size(); ++i)
-    if (P.els[i].type == ZBHIP_EL_START_EVENT && P.els[i].event == ZBHIP_EV_NONE) P.none_start = (int)i;
+  P.none_start = P.els[0].start;
   return true;
 }
 
@@ -1569,6 +1601,15 @@ class Oracle {
         pi_command(-1, ZBHIP_PI_ACTIVATE_ELEMENT, c);
         break;
       }
+      case ZBHIP_EL_SUB_PROCESS: {  // SubProcessProcessor.onActivate (processing/bpmn/container/SubProcessProcessor.java:49-66)
+        // applyInputMappings (none in the subset), transitionToActivated, activateChildInstance(none start)
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        PiValue c = v;
+        c.flowScopeKey = key;
+        c.elem = el.start;
+        pi_command(-1, ZBHIP_PI_ACTIVATE_ELEMENT, c);
+        break;
+      }
       case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onActivate (processing/bpmn/event/StartEventProcessor.java:45-50)
       case ZBHIP_EL_TASK:         // UndefinedTaskProcessor.onActivate (processing/bpmn/task/UndefinedTaskProcessor.java:37-42)
       case ZBHIP_EL_MANUAL_TASK:  // ManualTaskProcessor extends UndefinedTaskProcessor
@@ -1629,6 +1670,10 @@ class Oracle {
         pi_event(key, ZBHIP_PI_ELEMENT_COMPLETED, v);
         break;
       case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onComplete (:52-67)
+        complete_and_take(el, key, v, true);
+        break;
+      case ZBHIP_EL_SUB_PROCESS:  // SubProcessProcessor.onComplete (:68-82): applyOutputMappings,
+        // unsubscribeFromEvents (no subscriptions in the subset), transitionToCompleted, take flows
         complete_and_take(el, key, v, true);
         break;
       case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onComplete (:63-75)

@@ -3,7 +3,9 @@ test-util/.../bpmn/random generator: blocks of tasks, exclusive split/merge and 
 nested).  Used to drive the GPU executor and the CPU oracle with the same inputs.
 
 Bounds keep every process inside the device limits (<= 8 waiting elements per instance, <= 16
-join counters, a default flow on every exclusive split so no incident is raised)."""
+join counters, a default flow on every exclusive split so no incident is raised).  With
+``sub_processes`` a block can be an embedded sub-process holding a nested sequence (start ->
+blocks -> end), never inside a parallel branch (one active instance per sub-process element)."""
 from xml.sax.saxutils import escape, quoteattr
 
 BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
@@ -11,8 +13,11 @@ ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
 
 
 class _Gen:
-    def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True):
+    def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True, sub_processes=False):
         self.rng = rng
+        self.sub_processes = sub_processes
+        self.scope = None  # the sub-process being filled (None: the process)
+        self.subs = 0
         self.tasks = tasks
         self.pass_through = pass_through
         self.max_depth = max_depth
@@ -31,12 +36,12 @@ class _Gen:
 
     def node(self, kind, **extra):
         nid = self._id(kind)
-        self.nodes.append((kind, nid, extra))
+        self.nodes.append((kind, nid, dict(extra, scope=self.scope)))
         return nid
 
     def flow(self, src, tgt, cond=None):
         fid = self._id("flow")
-        self.flows.append([fid, src, tgt, cond])
+        self.flows.append([fid, src, tgt, cond, self.scope])
         return fid
 
     def condition(self):
@@ -68,7 +73,20 @@ class _Gen:
             choices.append("catch")
         if self.pass_through:
             choices.append("pass")
+        if self.sub_processes and width == 1 and depth < self.max_depth and self.subs < 3:
+            choices.append("sub")
         c = choices[int(r.integers(0, len(choices)))]
+        if c == "sub":  # embedded sub-process: start -> blocks -> end inside, one persistent slot
+            self.subs += 1
+            sp = self.node("subProcess")
+            self.flow(cur, sp)
+            outer, self.scope = self.scope, sp
+            st = self.node("startEvent")
+            end = self.sequence(st, depth + 1, width)
+            en = self.node("endEvent")
+            self.flow(end, en)
+            self.scope = outer
+            return sp
         if c == "pass":  # elements without behaviour: undefined / manual task, none throw event
             t = self.node(("task", "manualTask", "intermediateThrowEvent")[int(r.integers(0, 3))])
             self.flow(cur, t)
@@ -94,8 +112,8 @@ class _Gen:
                 if end == split:  # empty branch: direct flow to the merge
                     fid = self.flow(split, merge, None if b == dflt else self.condition())
                 else:
-                    fid = self.flows[first][0]  # the branch's first flow leaves the split
-                    self.flows[first][3] = None if b == dflt else self.condition()
+                    fid = next(f[0] for f in self.flows[first:] if f[1] == split)  # the branch's first flow
+                    next(f for f in self.flows[first:] if f[1] == split)[3] = None if b == dflt else self.condition()
                     self.flow(end, merge)
                 if b == dflt:
                     self.defaults[split] = fid
@@ -112,9 +130,9 @@ class _Gen:
 
 
 def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False,
-                   tasks=True):
+                   tasks=True, sub_processes=False):
     """tasks=False: no wait states (the CREATE batch runs the instance to its end)."""
-    g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks)
+    g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes)
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")
@@ -122,24 +140,35 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
     out = ['<?xml version="1.0" encoding="UTF-8"?>',
            '<definitions xmlns="%s" xmlns:zeebe="%s" id="d" targetNamespace="%s">' % (BPMN_NS, ZEEBE_NS, BPMN_NS),
            '  <process id=%s isExecutable="true">' % quoteattr(process_id)]
-    for kind, nid, extra in g.nodes:
-        if kind == "serviceTask":
-            out.append('    <serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s/>'
-                       '</extensionElements></serviceTask>' % (quoteattr(nid), quoteattr(extra["job_type"])))
-        elif kind == "exclusiveGateway" and nid in g.defaults:
-            out.append('    <exclusiveGateway id=%s default=%s/>' % (quoteattr(nid), quoteattr(g.defaults[nid])))
-        elif kind == "intermediateCatchEvent":
-            out.append('    <intermediateCatchEvent id=%s><messageEventDefinition messageRef="msg_def"/>'
-                       '</intermediateCatchEvent>' % quoteattr(nid))
-        else:
-            out.append("    <%s id=%s/>" % (kind, quoteattr(nid)))
-    for fid, src, tgt, cond in g.flows:
-        attrs = "id=%s sourceRef=%s targetRef=%s" % (quoteattr(fid), quoteattr(src), quoteattr(tgt))
-        if cond is None:
-            out.append("    <sequenceFlow %s/>" % attrs)
-        else:
-            out.append("    <sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
-                       % (attrs, escape(cond)))
+    def render(scope, ind):
+        for kind, nid, extra in g.nodes:
+            if extra["scope"] != scope:
+                continue
+            if kind == "serviceTask":
+                out.append('%s<serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s/>'
+                           '</extensionElements></serviceTask>' % (ind, quoteattr(nid), quoteattr(extra["job_type"])))
+            elif kind == "exclusiveGateway" and nid in g.defaults:
+                out.append('%s<exclusiveGateway id=%s default=%s/>' % (ind, quoteattr(nid), quoteattr(g.defaults[nid])))
+            elif kind == "intermediateCatchEvent":
+                out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition messageRef="msg_def"/>'
+                           '</intermediateCatchEvent>' % (ind, quoteattr(nid)))
+            elif kind == "subProcess":
+                out.append("%s<subProcess id=%s>" % (ind, quoteattr(nid)))
+                render(nid, ind + "  ")
+                out.append("%s</subProcess>" % ind)
+            else:
+                out.append("%s<%s id=%s/>" % (ind, kind, quoteattr(nid)))
+        for fid, src, tgt, cond, fscope in g.flows:
+            if fscope != scope:
+                continue
+            attrs = "id=%s sourceRef=%s targetRef=%s" % (quoteattr(fid), quoteattr(src), quoteattr(tgt))
+            if cond is None:
+                out.append("%s<sequenceFlow %s/>" % (ind, attrs))
+            else:
+                out.append("%s<sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
+                           % (ind, attrs, escape(cond)))
+
+    render(None, "    ")
     out.append("  </process>")
     if messages:
         out.append('  <message id="msg_def" name="msg"><extensionElements>'

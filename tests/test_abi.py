@@ -7,6 +7,7 @@ import subprocess
 import pytest
 
 from zeebe_amd import abi, native
+from zeebe_amd.engine import ELEMENT_DTYPE
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -51,7 +52,7 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(zb
     subprocess.check_call(["gcc", "-I" + os.path.join(ROOT, "include"), src, "-o", exe])
     got = [int(x) for x in subprocess.check_output([exe]).split()]
     assert got == [C.sizeof(abi.Command), C.sizeof(abi.DocEntry), C.sizeof(abi.Record), C.sizeof(abi.Config),
-                   C.sizeof(abi.Stats), abi.Record.ordinal.offset, abi.Record.aux.offset, 28,
+                   C.sizeof(abi.Stats), abi.Record.ordinal.offset, abi.Record.aux.offset, ELEMENT_DTYPE.itemsize,
                    C.sizeof(abi.XpartCmd), abi.Record.partition.offset, abi.XpartCmd.kind.offset]
 
 

@@ -31,8 +31,11 @@ class _Node:
 class ProcessBuilder:
     def __init__(self, process_id):
         self.process_id = process_id
-        self.children = []  # document order
+        self.root = []       # the process's children, document order
+        self.children = self.root  # the container being built (the process or an embedded sub-process)
         self.nodes = {}
+        self._container_of = {}  # node id -> the children list it lives in
+        self._stack = []     # enclosing containers while building a sub-process
         self.current = None
         self._pending_flow = None
         self._counter = 0
@@ -54,6 +57,7 @@ class ProcessBuilder:
         n = _Node(kind, id_)
         self.children.append(n)
         self.nodes[id_] = n
+        self._container_of[id_] = self.children
         if self.current is not None:
             self._connect(n)
         self.current = n
@@ -107,6 +111,24 @@ class ProcessBuilder:
         self.current.message = ("Message_%s" % self.current.id, name, expr)
         return self
 
+    def subProcess(self, id_=None):
+        """AbstractFlowNodeBuilder.subProcess(id).embeddedSubProcess(): the sub-process node and its
+        incoming flow in the current container, then its children inside it (startEvent() there
+        starts a new path); ``subProcessDone()`` continues after the sub-process."""
+        n = self._add_node("subProcess", id_)
+        n.children = []
+        self._stack.append((self.children, n))
+        self.children = n.children
+        self.current = None
+        self._pending_flow = None
+        return self
+
+    def subProcessDone(self):
+        self.children, n = self._stack.pop()
+        self.current = n
+        self._pending_flow = None
+        return self
+
     def exclusiveGateway(self, id_=None):
         self._add_node("exclusiveGateway", id_)
         return self
@@ -145,7 +167,7 @@ class ProcessBuilder:
         # AbstractFlowNodeBuilder.findLastGateway: walk unique predecessors from the current node
         node = self.current
         while True:
-            prev = [c.source for c in self.children if c.kind == "sequenceFlow" and c.target == node.id]
+            prev = [c.source for c in self._container_of[node.id] if c.kind == "sequenceFlow" and c.target == node.id]
             if len(prev) != 1:
                 raise ValueError("Unable to determine an unique previous gateway of " + node.id)
             node = self.nodes[prev[0]]
@@ -155,6 +177,7 @@ class ProcessBuilder:
 
     def moveToNode(self, id_):
         self.current = self.nodes[id_]
+        self.children = self._container_of[id_]
         return self
 
     def connectTo(self, id_):
@@ -167,31 +190,40 @@ class ProcessBuilder:
                '<definitions xmlns="%s" xmlns:zeebe="%s" id="definitions" targetNamespace="%s">'
                % (BPMN_NS, ZEEBE_NS, BPMN_NS),
                '  <process id=%s isExecutable="true">' % quoteattr(self.process_id)]
-        for c in self.children:
-            if c.kind == "sequenceFlow":
-                attrs = 'id=%s sourceRef=%s targetRef=%s' % (quoteattr(c.id), quoteattr(c.source), quoteattr(c.target))
-                if c.condition is None:
-                    out.append("    <sequenceFlow %s/>" % attrs)
+        catches = []
+
+        def render(children, ind):
+            for c in children:
+                if c.kind == "sequenceFlow":
+                    attrs = 'id=%s sourceRef=%s targetRef=%s' % (quoteattr(c.id), quoteattr(c.source), quoteattr(c.target))
+                    if c.condition is None:
+                        out.append("%s<sequenceFlow %s/>" % (ind, attrs))
+                    else:
+                        out.append("%s<sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
+                                   % (ind, attrs, escape(c.condition)))
+                elif c.kind == "serviceTask":
+                    retries = ' retries="%s"' % c.retries if c.retries is not None else ""
+                    out.append('%s<serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
+                               '</extensionElements></serviceTask>' % (ind, quoteattr(c.id), quoteattr(c.job_type), retries))
+                elif c.kind == "intermediateCatchEvent" and c.message:
+                    catches.append(c)
+                    out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
+                               '</intermediateCatchEvent>' % (ind, quoteattr(c.id), quoteattr(c.id + "_med"),
+                                                              quoteattr(c.message[0])))
+                elif c.kind == "exclusiveGateway" and c.default:
+                    out.append("%s<exclusiveGateway id=%s default=%s/>" % (ind, quoteattr(c.id), quoteattr(c.default.id)))
+                elif c.kind == "subProcess":
+                    out.append("%s<subProcess id=%s>" % (ind, quoteattr(c.id)))
+                    render(c.children, ind + "  ")
+                    out.append("%s</subProcess>" % ind)
                 else:
-                    out.append("    <sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
-                               % (attrs, escape(c.condition)))
-            elif c.kind == "serviceTask":
-                retries = ' retries="%s"' % c.retries if c.retries is not None else ""
-                out.append('    <serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
-                           '</extensionElements></serviceTask>' % (quoteattr(c.id), quoteattr(c.job_type), retries))
-            elif c.kind == "intermediateCatchEvent" and c.message:
-                out.append('    <intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
-                           '</intermediateCatchEvent>' % (quoteattr(c.id), quoteattr(c.id + "_med"),
-                                                          quoteattr(c.message[0])))
-            elif c.kind == "exclusiveGateway" and c.default:
-                out.append("    <exclusiveGateway id=%s default=%s/>" % (quoteattr(c.id), quoteattr(c.default.id)))
-            else:
-                out.append("    <%s id=%s/>" % (c.kind, quoteattr(c.id)))
+                    out.append("%s<%s id=%s/>" % (ind, c.kind, quoteattr(c.id)))
+
+        render(self.root, "    ")
         out.append("  </process>")
-        for c in self.children:
-            if c.kind == "intermediateCatchEvent" and c.message:
-                out.append('  <message id=%s name=%s><extensionElements><zeebe:subscription correlationKey=%s/>'
-                           '</extensionElements></message>' % tuple(quoteattr(x) for x in c.message))
+        for c in catches:
+            out.append('  <message id=%s name=%s><extensionElements><zeebe:subscription correlationKey=%s/>'
+                       '</extensionElements></message>' % tuple(quoteattr(x) for x in c.message))
         out.append("</definitions>")
         return "\n".join(out) + "\n"
 
@@ -231,6 +263,22 @@ def fork_join_process(branches=8, process_id="forkjoin", tasks=False, job_type="
             b.connectTo("join")
     b.moveToNode("join").sequenceFlowId("toEnd").endEvent("end")
     return b.done()
+
+
+def sub_process_process(inner="task", process_id="process", job_type="task"):
+    """EmbeddedSubProcessTest.java:41-80 shapes: start -> sub-process(start -> [inner] -> end) -> end.
+    inner: "none" (NO_TASK_SUB_PROCESS), "task" (ONE_TASK_SUB_PROCESS), "parallel"
+    (PARALLEL_TASKS_SUB_PROCESS: fork -> task-1 / task-2 -> join), "nested" (a nested sub-process)."""
+    b = createExecutableProcess(process_id).startEvent().subProcess("sub-process").startEvent()
+    if inner == "task":
+        b.serviceTask("task", job_type)
+    elif inner == "parallel":
+        (b.parallelGateway("fork").serviceTask("task-1", "task-1").sequenceFlowId("join-1").parallelGateway("join")
+         .moveToNode("fork").serviceTask("task-2", "task-2").sequenceFlowId("join-2").connectTo("join"))
+    elif inner == "nested":
+        b.subProcess("nestedSubProcess").startEvent().endEvent().subProcessDone()
+    b.endEvent().subProcessDone()
+    return b.endEvent().done()
 
 
 def message_catch_process(process_id="process", message_name="msg", correlation_key="key", catch_id="catch"):

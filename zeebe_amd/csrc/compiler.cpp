@@ -349,6 +349,8 @@ static zbhip_element blank(uint8_t type, uint16_t id) {
   e.event_type = ZBHIP_EV_UNSPECIFIED;
   e.flow_source = e.flow_target = e.condition = e.default_flow = ZBHIP_NONE16;
   e.job_type = e.join_slot = ZBHIP_NONE16;
+  e.flow_scope = 0;
+  e.start_event = ZBHIP_NONE16;
   e.message_name = e.correlation_var = ZBHIP_NONE16;
   e.job_retries = 0;
   e.id = id;
@@ -400,99 +402,135 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
   }
   C.csr.bpmn_process_id = C.str(pid);
   C.elements.push_back(blank(ZBHIP_EL_PROCESS, C.csr.bpmn_process_id));
+  C.elements[0].flow_scope = 0;
   std::unordered_map<std::string, uint16_t> index{{pid, 0}};
   std::vector<const Elem*> flows;
   std::vector<std::vector<uint16_t>> out_lists, in_lists;
+  std::vector<const Elem*> xgws;
 
-  for (auto& c : proc->children) {
-    uint8_t type;
-    if (c.tag == "startEvent") type = ZBHIP_EL_START_EVENT;
-    else if (c.tag == "endEvent") type = ZBHIP_EL_END_EVENT;
-    else if (c.tag == "serviceTask") type = ZBHIP_EL_SERVICE_TASK;
-    else if (c.tag == "exclusiveGateway") type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
-    else if (c.tag == "parallelGateway") type = ZBHIP_EL_PARALLEL_GATEWAY;
-    else if (c.tag == "sequenceFlow") type = ZBHIP_EL_SEQUENCE_FLOW;
-    else if (c.tag == "intermediateCatchEvent") type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
-    else if (c.tag == "intermediateThrowEvent") type = ZBHIP_EL_INTERMEDIATE_THROW_EVENT;
-    else if (c.tag == "task") type = ZBHIP_EL_TASK;
-    else if (c.tag == "manualTask") type = ZBHIP_EL_MANUAL_TASK;
-    else if (c.tag == "extensionElements" || c.tag == "documentation" || c.tag == "textAnnotation" ||
-             c.tag == "association")
-      continue;
-    else { err = "element <" + c.tag + "> outside the supported subset"; return ZBHIP_EUNSUPP; }
-    const std::string* id = c.get("id");
-    if (!id || id->empty()) { err = "element without id"; return ZBHIP_EPARSE; }
-    if (C.elements.size() >= 0xFFF0) { err = "too many elements"; return ZBHIP_EUNSUPP; }
-    zbhip_element e = blank(type, C.str(*id));
-    if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_END_EVENT) {
-      for (auto& d : c.children)
-        if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
-          err = "event definition <" + d.tag + "> outside the supported subset";
-          return ZBHIP_EUNSUPP;
-        }
-      e.event_type = ZBHIP_EV_NONE;
-    }
-    if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT || type == ZBHIP_EL_TASK || type == ZBHIP_EL_MANUAL_TASK) {
-      // activities / events without behaviour (UndefinedTaskProcessor, ManualTaskProcessor,
-      // IntermediateThrowEventProcessor.NoneIntermediateThrowEventBehavior): none events only
-      for (auto& d : c.children)
-        if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
-          err = "event definition <" + d.tag + "> outside the supported subset";
-          return ZBHIP_EUNSUPP;
-        }
-      if (const Elem* ext = c.first("extensionElements"))
-        if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
-      if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT) e.event_type = ZBHIP_EV_NONE;
-    }
-    if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
-      // CatchEventTransformer.transformMessageEventDefinition: message catch events only
-      const Elem* med = c.first("messageEventDefinition");
-      for (auto& d : c.children)
-        if (&d != med && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
-          err = "event definition <" + d.tag + "> outside the supported subset";
-          return ZBHIP_EUNSUPP;
-        }
-      if (!med || !med->get("messageRef")) { err = "intermediate catch event without a message"; return ZBHIP_EUNSUPP; }
-      auto mi = messages.find(*med->get("messageRef"));
-      if (mi == messages.end()) { err = "unknown message " + *med->get("messageRef"); return ZBHIP_EPARSE; }
-      if (!mi->second.ok) { err = mi->second.why; return ZBHIP_EUNSUPP; }
-      if (const Elem* ext = c.first("extensionElements"))
-        if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
-      e.event_type = ZBHIP_EV_MESSAGE;
-      e.message_name = C.str(mi->second.name);
-      e.correlation_var = C.str(mi->second.corr);
-    }
-    if (type == ZBHIP_EL_SERVICE_TASK) {
-      const Elem* ext = c.first("extensionElements");
-      const Elem* td = ext ? ext->first("taskDefinition") : nullptr;
-      const std::string* jt = td ? td->get("type") : nullptr;
-      if (!jt || jt->empty()) { err = "service task '" + *id + "' without a job type"; return ZBHIP_EPARSE; }
-      const std::string* rt = td->get("retries");
-      std::string retries = rt ? *rt : "3";
-      if ((*jt)[0] == '=' || retries.empty() || retries[0] == '=') {
-        err = "job type/retries expressions outside the supported subset";
-        return ZBHIP_EUNSUPP;
+  // Elements in document pre-order: an embedded sub-process, then its children, then its next
+  // sibling (the oracle numbers them the same way).  Every sequence flow connects two nodes of one
+  // container, so the flows' reverse document order per container is the walker's order.
+  std::function<int(const Elem&, uint16_t)> container = [&](const Elem& parent, uint16_t scope) -> int {
+    for (auto& c : parent.children) {
+      uint8_t type;
+      if (c.tag == "startEvent") type = ZBHIP_EL_START_EVENT;
+      else if (c.tag == "endEvent") type = ZBHIP_EL_END_EVENT;
+      else if (c.tag == "serviceTask") type = ZBHIP_EL_SERVICE_TASK;
+      else if (c.tag == "exclusiveGateway") type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
+      else if (c.tag == "parallelGateway") type = ZBHIP_EL_PARALLEL_GATEWAY;
+      else if (c.tag == "sequenceFlow") type = ZBHIP_EL_SEQUENCE_FLOW;
+      else if (c.tag == "intermediateCatchEvent") type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
+      else if (c.tag == "intermediateThrowEvent") type = ZBHIP_EL_INTERMEDIATE_THROW_EVENT;
+      else if (c.tag == "task") type = ZBHIP_EL_TASK;
+      else if (c.tag == "manualTask") type = ZBHIP_EL_MANUAL_TASK;
+      else if (c.tag == "subProcess") type = ZBHIP_EL_SUB_PROCESS;
+      else if (c.tag == "extensionElements" || c.tag == "documentation" || c.tag == "textAnnotation" ||
+               c.tag == "association" || c.tag == "incoming" || c.tag == "outgoing")
+        continue;
+      else { err = "element <" + c.tag + "> outside the supported subset"; return ZBHIP_EUNSUPP; }
+      const std::string* id = c.get("id");
+      if (!id || id->empty()) { err = "element without id"; return ZBHIP_EPARSE; }
+      if (C.elements.size() >= 0xFF0) { err = "too many elements"; return ZBHIP_EUNSUPP; }
+      zbhip_element e = blank(type, C.str(*id));
+      e.flow_scope = scope;
+      if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_END_EVENT) {
+        for (auto& d : c.children)
+          if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+            err = "event definition <" + d.tag + "> outside the supported subset";
+            return ZBHIP_EUNSUPP;
+          }
+        e.event_type = ZBHIP_EV_NONE;
       }
-      if (ext->first("ioMapping") || ext->first("taskHeaders")) {
-        err = "io mappings / task headers outside the supported subset";
-        return ZBHIP_EUNSUPP;
+      if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT || type == ZBHIP_EL_TASK || type == ZBHIP_EL_MANUAL_TASK) {
+        // activities / events without behaviour (UndefinedTaskProcessor, ManualTaskProcessor,
+        // IntermediateThrowEventProcessor.NoneIntermediateThrowEventBehavior): none events only
+        for (auto& d : c.children)
+          if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+            err = "event definition <" + d.tag + "> outside the supported subset";
+            return ZBHIP_EUNSUPP;
+          }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT) e.event_type = ZBHIP_EV_NONE;
       }
-      e.job_type = C.str(*jt);
-      e.job_retries = (uint16_t)atoi(retries.c_str());
+      if (type == ZBHIP_EL_SUB_PROCESS) {
+        // embedded sub-process (SubProcessTransformer / SubProcessProcessor): no event
+        // sub-process, no multi-instance, no io mappings
+        const std::string* tbe = c.get("triggeredByEvent");
+        if (tbe && *tbe == "true") { err = "event sub-process outside the supported subset"; return ZBHIP_EUNSUPP; }
+        if (c.first("multiInstanceLoopCharacteristics") || c.first("standardLoopCharacteristics")) {
+          err = "multi-instance sub-process outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+      }
+      if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+        // CatchEventTransformer.transformMessageEventDefinition: message catch events only
+        const Elem* med = c.first("messageEventDefinition");
+        for (auto& d : c.children)
+          if (&d != med && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+            err = "event definition <" + d.tag + "> outside the supported subset";
+            return ZBHIP_EUNSUPP;
+          }
+        if (!med || !med->get("messageRef")) { err = "intermediate catch event without a message"; return ZBHIP_EUNSUPP; }
+        auto mi = messages.find(*med->get("messageRef"));
+        if (mi == messages.end()) { err = "unknown message " + *med->get("messageRef"); return ZBHIP_EPARSE; }
+        if (!mi->second.ok) { err = mi->second.why; return ZBHIP_EUNSUPP; }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        e.event_type = ZBHIP_EV_MESSAGE;
+        e.message_name = C.str(mi->second.name);
+        e.correlation_var = C.str(mi->second.corr);
+      }
+      if (type == ZBHIP_EL_SERVICE_TASK) {
+        const Elem* ext = c.first("extensionElements");
+        const Elem* td = ext ? ext->first("taskDefinition") : nullptr;
+        const std::string* jt = td ? td->get("type") : nullptr;
+        if (!jt || jt->empty()) { err = "service task '" + *id + "' without a job type"; return ZBHIP_EPARSE; }
+        const std::string* rt = td->get("retries");
+        std::string retries = rt ? *rt : "3";
+        if ((*jt)[0] == '=' || retries.empty() || retries[0] == '=') {
+          err = "job type/retries expressions outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
+        if (ext->first("ioMapping") || ext->first("taskHeaders")) {
+          err = "io mappings / task headers outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
+        e.job_type = C.str(*jt);
+        e.job_retries = (uint16_t)atoi(retries.c_str());
+      }
+      if (type == ZBHIP_EL_SEQUENCE_FLOW) flows.push_back(&c);
+      if (type == ZBHIP_EL_EXCLUSIVE_GATEWAY) xgws.push_back(&c);
+      if (index.count(*id)) { err = "duplicate element id " + *id; return ZBHIP_EPARSE; }
+      const uint16_t self = (uint16_t)C.elements.size();
+      index[*id] = self;
+      C.elements.push_back(e);
+      if (type == ZBHIP_EL_SUB_PROCESS) {
+        if (int rc = container(c, self)) return rc;
+      } else if (type == ZBHIP_EL_START_EVENT) {
+        // getNoneStartEvent of the container (the last none start event in document order)
+        C.elements[scope].start_event = self;
+      }
     }
-    if (type == ZBHIP_EL_SEQUENCE_FLOW) flows.push_back(&c);
-    index[*id] = (uint16_t)C.elements.size();
-    C.elements.push_back(e);
-  }
+    return ZBHIP_OK;
+  };
+  if (int rc = container(*proc, 0)) return rc;
+  for (size_t e = 1; e < C.elements.size(); ++e)
+    if (C.elements[e].element_type == ZBHIP_EL_SUB_PROCESS && C.elements[e].start_event == ZBHIP_NONE16) {
+      err = "sub-process without a none start event";
+      return ZBHIP_EUNSUPP;
+    }
   out_lists.resize(C.elements.size());
   in_lists.resize(C.elements.size());
 
-  for (auto& c : proc->children) {
-    if (c.tag != "exclusiveGateway") continue;
-    if (const std::string* d = c.get("default")) {
+  for (const Elem* c : xgws) {
+    if (const std::string* d = c->get("default")) {
       auto it = index.find(*d);
       if (it == index.end()) { err = "unknown default flow " + *d; return ZBHIP_EPARSE; }
-      C.elements[index[*c.get("id")]].default_flow = it->second;
+      C.elements[index[*c->get("id")]].default_flow = it->second;
     }
   }
 
@@ -508,6 +546,10 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     auto t = tr ? index.find(*tr) : index.end();
     if (s == index.end() || t == index.end()) { err = "sequence flow with unknown source/target"; return ZBHIP_EPARSE; }
     zbhip_element& fe = C.elements[fi];
+    if (C.elements[s->second].flow_scope != fe.flow_scope || C.elements[t->second].flow_scope != fe.flow_scope) {
+      err = "sequence flow crossing a sub-process boundary";
+      return ZBHIP_EPARSE;
+    }
     fe.flow_source = s->second;
     fe.flow_target = t->second;
     if (const Elem* ce = f.first("conditionExpression")) {
@@ -541,9 +583,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     for (uint16_t f : in_lists[g]) C.elements[f].join_slot = slots++;
   }
   C.csr.n_join_slots = slots;
-  C.csr.none_start = ZBHIP_NONE16;
-  for (size_t e = 1; e < C.elements.size(); ++e)
-    if (C.elements[e].element_type == ZBHIP_EL_START_EVENT) C.csr.none_start = (uint16_t)e;
+  C.csr.none_start = C.elements[0].start_event;
   C.csr.process_definition_key = def_key;
   C.csr.version = version;
   C.finish();

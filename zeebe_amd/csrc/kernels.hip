@@ -51,7 +51,7 @@ namespace zb {
 // its column, then writes it at its prefix) spilled and was ~2 % slower, and an owner map of stage
 // indices (one dependent LDS level fewer) ~4 % slower.)
 template <int B_, int T_, int Q_, int R_, bool M_ = false, bool J_ = true, bool X_ = true, int W_ = 0,
-          bool REG_ = false>
+          bool REG_ = false, bool S_ = false>
 struct KCfg {
   static constexpr int B = B_, T = T_, Q = Q_, R = R_;
   static constexpr int W = W_;   // waves per SIMD the register allocation targets (0 = compiler default)
@@ -59,6 +59,7 @@ struct KCfg {
   static constexpr bool M = M_;  // message correlation (catch events, subscription commands)
   static constexpr bool J = J_;  // parallel-gateway join counters
   static constexpr bool X = X_;  // exclusive gateways (FEEL condition evaluation)
+  static constexpr bool S = S_;  // flow scopes below the process (embedded sub-processes)
 };
 // One token per instance (exclusive gateways, no parallel gateways / multi-outgoing nodes: no join
 // counters).  Only R = 4 stage rows: rows j >= R go straight to the output region (one coalesced
@@ -101,6 +102,9 @@ using KGeneric = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, Z
 #define ZB_KMSG_W 2  // 256 VGPRs, no AGPR or scratch spill: 2 waves per SIMD (compiler default: 260 -> 1)
 #endif
 using KMsg = KCfg<128, 12, 16, ZB_KMSG_R, true, true, true, ZB_KMSG_W>;  // message catch events (config 5)
+// Embedded sub-processes: KGeneric plus flow scopes (a sub-process instance is an element-table
+// entry whose job field counts its children and active sequence flows)
+using KScope = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, ZB_KGENERIC_W, false, true>;
 
 template <class K>
 struct Lane {
@@ -426,20 +430,66 @@ __device__ __forceinline__ int tbl_find_job(const Lane<K>& L, uint32_t job) {
   return -1;
 }
 template <class K>
-__device__ __forceinline__ void tbl_insert(Lane<K>& L, uint32_t elem, uint32_t key, uint32_t state) {
+__device__ __forceinline__ int tbl_insert(Lane<K>& L, uint32_t elem, uint32_t key, uint32_t state) {
   int t = 0;
   for (; t < L.nt; ++t)
     if (tget(L, t).x == 0xFFFFFFFFu) break;
   if (t == L.nt) {
-    if (L.nt >= K::T) { set_fail(L, FB_TABLE); return; }
+    if (L.nt >= K::T) { set_fail(L, FB_TABLE); return -1; }
     ++L.nt;
   }
   tput(L, t, make_uint2(elem | (key << 16), JOB_ZERO | (state << 16)));
+  return t;
 }
 template <class K>
 __device__ __forceinline__ void tbl_set_state(Lane<K>& L, int t, uint32_t state) {
   uint2 e = tget(L, t);
   e.y = (e.y & 0xFF00FFFFu) | (state << 16);
+  tput(L, t, e);
+}
+
+// ---- flow scopes (K::S: embedded sub-processes) ----------------------------------------------
+// An element's container is the high half of its word 3 (0: the process).  A sub-process instance
+// is an element-table entry like any other (one active instance per sub-process element; a second
+// concurrent one falls back) whose job field holds childCount | activeSequenceFlows << 8
+// (ElementInstance.java:23-54); the process scope keeps its counters in pi_child / pi_asf.
+template <class K>
+__device__ __forceinline__ uint32_t scope_of(uint4 w) {
+  if constexpr (K::S) return w.w >> 16;
+  else return 0;
+}
+template <class K>
+__device__ __forceinline__ int scope_find(const Lane<K>& L, uint32_t c) {
+  for (int t = 0; t < L.nt; ++t) {
+    const uint2 e = tget(L, t);
+    if (e.x != 0xFFFFFFFFu && (e.x & 0xFFFF) == c) return t;
+  }
+  return -1;
+}
+// key ordinal of the flow scope instance of container c (the process instance: ordinal 0)
+template <class K>
+__device__ __forceinline__ uint32_t scope_key(Lane<K>& L, uint32_t c) {
+  if (c == 0) return 0;
+  const int t = scope_find(L, c);
+  if (t < 0) { set_fail(L, FB_UNSUPPORTED); return 0; }
+  return tget(L, t).x >> 16;
+}
+// childCount += dc, activeSequenceFlows += da; decrements clamp at 0 (ElementInstance.java:203-213)
+template <class K>
+__device__ __forceinline__ void scope_adjust(Lane<K>& L, uint32_t c, int dc, int da) {
+  if (c == 0) {
+    L.pi_child += dc;
+    L.pi_asf = L.pi_asf + da < 0 ? 0 : L.pi_asf + da;
+    return;
+  }
+  const int t = scope_find(L, c);
+  if (t < 0) { set_fail(L, FB_UNSUPPORTED); return; }
+  uint2 e = tget(L, t);
+  const int child = (int)(e.y & 0xFF) + dc;
+  int asf = (int)((e.y >> 8) & 0xFF) + da;
+  if (asf < 0) asf = 0;
+  if (child < 0 || child > 255 || asf > 255) { set_fail(L, FB_TABLE); return; }
+  e.y = (e.y & 0xFFFF0000u) | (uint32_t)child | ((uint32_t)asf << 8);
   tput(L, t, e);
 }
 
@@ -636,6 +686,17 @@ __device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem
       if (c > 0) join_set(L, s, c - 1);
     }
   }
+  if constexpr (K::S) {
+    // a second active instance of one sub-process element: outside the device subset
+    if (type == ZBHIP_EL_SUB_PROCESS && scope_find(L, elem) >= 0) { set_fail(L, FB_UNSUPPORTED); return; }
+    const int t = tbl_insert(L, elem, key, ZBHIP_PI_ELEMENT_ACTIVATING);
+    if (t < 0) return;
+    if (type == ZBHIP_EL_SUB_PROCESS)  // jobKey 0; no children, no active flows yet
+      tput(L, t, make_uint2(elem | (key << 16), (uint32_t)ZBHIP_PI_ELEMENT_ACTIVATING << 16));
+    const int da = type == ZBHIP_EL_START_EVENT ? 0 : type == ZBHIP_EL_PARALLEL_GATEWAY ? -(int)(w.x >> 16) : -1;
+    scope_adjust(L, scope_of<K>(w), 1, da);
+    return;
+  }
   tbl_insert(L, elem, key, ZBHIP_PI_ELEMENT_ACTIVATING);
   ++L.pi_child;
   if (type == ZBHIP_EL_START_EVENT) {
@@ -651,6 +712,17 @@ __device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem
 template <class K>
 __device__ __forceinline__ void apply_completed_child(Lane<K>& L, int t, uint32_t key) {
   if (L.trig_key == key) L.trig_key = NONE;  // eventScopeInstanceState.deleteInstance (triggers)
+  if constexpr (K::S) {
+    const uint4 w = elem_of(L, tget(L, t).x & 0xFFFF);
+    tput(L, t, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+    if (etype(w) == ZBHIP_EL_SUB_PROCESS) {  // its taken-flow counters go with it (removeInstance)
+      const uint32_t m = w.z >> 16;
+      for (uint32_t s = 0; s < (uint32_t)kMaxJoinSlots; ++s)
+        if ((m >> s) & 1u) join_set(L, s, 0);
+    }
+    scope_adjust(L, scope_of<K>(w), -1, 0);
+    return;
+  }
   tput(L, t, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
   --L.pi_child;
 }
@@ -659,9 +731,12 @@ __device__ __forceinline__ void apply_completed_child(Lane<K>& L, int t, uint32_
 template <class K>
 __device__ __forceinline__ void take_sequence_flow(Lane<K>& L, uint32_t flow) {
   uint4 fw = elem_of(L, flow);
+  const uint32_t c = scope_of<K>(fw);
+  const uint32_t fsk = K::S ? scope_key(L, c) : 0u;
   uint32_t sft = new_key(L);
-  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, flow);
-  ++L.pi_asf;  // ProcessInstanceSequenceFlowTakenApplier
+  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, fsk, flow);
+  if constexpr (K::S) scope_adjust(L, c, 0, 1);  // ProcessInstanceSequenceFlowTakenApplier
+  else ++L.pi_asf;
   uint32_t target = fw.z & 0xFFFF;
   if (etype(elem_of(L, target)) == ZBHIP_EL_PARALLEL_GATEWAY) {
     uint32_t s = fw.w & 0xFFFF;
@@ -670,17 +745,29 @@ __device__ __forceinline__ void take_sequence_flow(Lane<K>& L, uint32_t flow) {
     join_set(L, s, c + 1);
   }
   uint32_t k = new_key(L);
-  follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, 0, target, false, true, k);
+  follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, fsk, target, false, true, k);
 }
 
 // transitionToCompleted (:158-191) + afterExecutionPathCompleted -> ProcessProcessor (:130-140)
 template <class K>
 __device__ __forceinline__ void transition_to_completed_child(Lane<K>& L, int t, uint32_t elem, uint4 w, uint32_t key) {
-  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, key, 0, elem);
+  const uint32_t c = scope_of<K>(w);
+  const uint32_t fsk = K::S ? scope_key(L, c) : 0u;
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, key, fsk, elem);
   apply_completed_child(L, t, key);
   if ((w.y >> 16) == 0) {  // end of the execution path
-    if (L.pi_live && L.pi_child + L.pi_asf == 0) {  // BpmnStateBehavior.canBeCompleted
-      follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0, true, false, 0);
+    if (c == 0) {
+      if (L.pi_live && L.pi_child + L.pi_asf == 0) {  // BpmnStateBehavior.canBeCompleted
+        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0, true, false, 0);
+      }
+    } else if constexpr (K::S) {
+      // SubProcessProcessor.afterExecutionPathCompleted (:97-106): completeElement(flow scope)
+      const int ts = scope_find(L, c);
+      if (ts >= 0 && (tget(L, ts).y & 0xFFFF) == 0) {
+        const uint32_t sk = tget(L, ts).x >> 16;
+        const uint32_t pc = scope_of<K>(elem_of(L, c));
+        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, sk, scope_key(L, pc), c, true, pc == 0, sk);
+      }
     }
   }
 }
@@ -992,10 +1079,10 @@ __device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint3
 
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
 template <class K>
-__device__ __forceinline__ void reject_pi(Lane<K>& L, bool complete, uint32_t elem, uint32_t key, bool fs_pi, uint32_t reason,
-                          uint32_t arg) {
-  emit(L, kRejectBit | (complete ? ZBHIP_PI_COMPLETE_ELEMENT : ZBHIP_PI_ACTIVATE_ELEMENT), key,
-       fs_pi ? 0u : (uint32_t)NONE, elem, reason | (arg << 4));
+__device__ __forceinline__ void reject_pi(Lane<K>& L, bool complete, uint32_t elem, uint32_t key, uint32_t aux,
+                                          uint32_t reason, uint32_t arg) {
+  emit(L, kRejectBit | (complete ? ZBHIP_PI_COMPLETE_ELEMENT : ZBHIP_PI_ACTIVATE_ELEMENT), key, aux, elem,
+       reason | (arg << 4));
 }
 
 template <class K>
@@ -1006,19 +1093,35 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   const uint32_t cmd_key = entry >> 16;
   const uint4 w = elem_of(L, elem);
   const uint32_t type = etype(w);
+  // flowScopeKey of the element's records and rejections: the process's children 0 (K::S: the
+  // instance of the element's container), the process itself -1
+  const uint32_t c = scope_of<K>(w);
+  uint32_t fsa = 0, raux = fs_pi ? 0u : (uint32_t)NONE;
+  if constexpr (K::S) {
+    if (type != ZBHIP_EL_PROCESS) {
+      fsa = scope_key(L, c);  // a container without an instance (never in the subset): fallback
+      if (L.fail) return;
+      raux = fsa;
+    }
+  }
 
   if (!complete) {
     // ---- ACTIVATE_ELEMENT: guard (:47-70) ----
     if (type != ZBHIP_EL_PROCESS) {
-      if (!L.pi_live) { reject_pi(L, false, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_NOT_FOUND, 0); return; }
-      if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED) {
-        reject_pi(L, false, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_STATE, L.pi_state);
+      if (c != 0) {  // K::S: the flow scope is a sub-process instance (found by scope_key)
+        const uint32_t fst = (tget(L, scope_find(L, c)).y >> 16) & 0xFF;
+        if (fst != ZBHIP_PI_ELEMENT_ACTIVATED) { reject_pi(L, false, elem, cmd_key, raux, ZBHIP_REASON_FS_STATE, fst); return; }
+      } else if (!L.pi_live) {
+        reject_pi(L, false, elem, cmd_key, raux, ZBHIP_REASON_FS_NOT_FOUND, 0);
+        return;
+      } else if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED) {
+        reject_pi(L, false, elem, cmd_key, raux, ZBHIP_REASON_FS_STATE, L.pi_state);
         return;
       }
       if (type == ZBHIP_EL_PARALLEL_GATEWAY) {  // canActivateParallelGateway (:169-186)
         uint32_t base = w.w & 0xFFFF, n = w.x >> 16, taken = 0;
         for (uint32_t s = base; s < base + n; ++s) taken += join_get(L, s) > 0;
-        if (taken < n) { reject_pi(L, false, elem, cmd_key, fs_pi, ZBHIP_REASON_PGW_NOT_ALL_TAKEN, 0); return; }
+        if (taken < n) { reject_pi(L, false, elem, cmd_key, raux, ZBHIP_REASON_PGW_NOT_ALL_TAKEN, 0); return; }
       }
     }
     // transitionToActivating (:72-100)
@@ -1038,7 +1141,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     }
     if (cmd_key != NONE && tbl_find(L, cmd_key) >= 0) { set_fail(L, FB_UNSUPPORTED); return; }
     const uint32_t key = cmd_key == NONE ? new_key(L) : cmd_key;
-    emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, key, 0, elem);
+    emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, key, fsa, elem);
     apply_activating_child(L, elem, w, key);
     if (L.fail) return;
     const int t = L.nt > 0 ? tbl_find(L, key) : -1;
@@ -1047,13 +1150,13 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       case ZBHIP_EL_TASK:         // UndefinedTaskProcessor.onActivate (task/UndefinedTaskProcessor.java:37-42)
       case ZBHIP_EL_MANUAL_TASK:  // ManualTaskProcessor extends UndefinedTaskProcessor
       case ZBHIP_EL_INTERMEDIATE_THROW_EVENT:  // NoneIntermediateThrowEventBehavior.onActivate (:120-126)
-        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
-        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, key, 0, elem, true, true, key);
+        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, key, fsa, elem, true, true, key);
         return;
       case ZBHIP_EL_END_EVENT:  // NoneEndEventBehavior.onActivate/onComplete (:110-134)
-        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
-        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
+        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, fsa, elem);
         transition_to_completed_child(L, t, elem, w, key);
         take_outgoing(L, w);
         return;
@@ -1063,7 +1166,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         uint2 e = tget(L, t);   // JobCreatedApplier: element instance jobKey
         e.y = (job & 0xFFFF) | (e.y & 0x00FF0000u) | (1u << 24);
         tput(L, t, e);
-        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
         return;
       }
@@ -1071,8 +1174,8 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         if constexpr (!K::X) { set_fail(L, FB_UNSUPPORTED); return; }
         uint32_t flow = find_sequence_flow(L, w, key);
         if (L.fail) return;
-        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
-        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
+        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, fsa, elem);
         transition_to_completed_child(L, t, elem, w, key);
         if (flow != NONE) take_sequence_flow(L, flow);
         return;
@@ -1081,15 +1184,25 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         if constexpr (K::M) {
           subscribe_message(L, elem, w, key);
           if (L.fail) return;
-          emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
+          emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
           tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
         } else {
           set_fail(L, FB_UNSUPPORTED);
         }
         return;
+      case ZBHIP_EL_SUB_PROCESS:  // SubProcessProcessor.onActivate (container/SubProcessProcessor.java:49-66)
+        if constexpr (K::S) {
+          emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
+          tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
+          // activateChildInstance: the none start event, key -1, flow scope = this instance
+          follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, NONE, key, w.z & 0xFFFF, false, false, NONE);
+        } else {
+          set_fail(L, FB_UNSUPPORTED);
+        }
+        return;
       case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (:34-50)
-        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, 0, elem);
-        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, 0, elem);
+        emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
+        emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, fsa, elem);
         transition_to_completed_child(L, t, elem, w, key);
         take_outgoing(L, w);
         return;
@@ -1101,9 +1214,9 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
 
   // ---- COMPLETE_ELEMENT: guard (:56-63) ----
   if (type == ZBHIP_EL_PROCESS) {
-    if (!L.pi_live) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
+    if (!L.pi_live) { reject_pi(L, true, elem, cmd_key, raux, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
     if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED && L.pi_state != ZBHIP_PI_ELEMENT_COMPLETING) {
-      reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_STATE, L.pi_state);
+      reject_pi(L, true, elem, cmd_key, raux, ZBHIP_REASON_EI_STATE, L.pi_state);
       return;
     }
     if (L.pi_state == ZBHIP_PI_ELEMENT_COMPLETING) { set_fail(L, FB_UNSUPPORTED); return; }
@@ -1118,19 +1231,24 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     return;
   }
   const int t = tbl_find(L, cmd_key);
-  if (t < 0) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
+  if (t < 0) { reject_pi(L, true, elem, cmd_key, raux, ZBHIP_REASON_EI_NOT_FOUND, 0); return; }
   const uint32_t st = (tget(L, t).y >> 16) & 0xFF;
   if (st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING) {
-    reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_EI_STATE, st);
+    reject_pi(L, true, elem, cmd_key, raux, ZBHIP_REASON_EI_STATE, st);
     return;
   }
-  if (!L.pi_live) { reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_NOT_FOUND, 0); return; }
-  if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED) {
-    reject_pi(L, true, elem, cmd_key, fs_pi, ZBHIP_REASON_FS_STATE, L.pi_state);
+  if (c != 0) {  // K::S: the flow scope is a sub-process instance
+    const uint32_t fst = (tget(L, scope_find(L, c)).y >> 16) & 0xFF;
+    if (fst != ZBHIP_PI_ELEMENT_ACTIVATED) { reject_pi(L, true, elem, cmd_key, raux, ZBHIP_REASON_FS_STATE, fst); return; }
+  } else if (!L.pi_live) {
+    reject_pi(L, true, elem, cmd_key, raux, ZBHIP_REASON_FS_NOT_FOUND, 0);
+    return;
+  } else if (L.pi_state != ZBHIP_PI_ELEMENT_ACTIVATED) {
+    reject_pi(L, true, elem, cmd_key, raux, ZBHIP_REASON_FS_STATE, L.pi_state);
     return;
   }
   if (st == ZBHIP_PI_ELEMENT_COMPLETING) { set_fail(L, FB_UNSUPPORTED); return; }
-  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, cmd_key, 0, elem);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, cmd_key, fsa, elem);
   tbl_set_state(L, t, ZBHIP_PI_ELEMENT_COMPLETING);
   if constexpr (K::M) {
     if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
@@ -1141,7 +1259,9 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       set_fail(L, FB_UNSUPPORTED);
       return;
     }
-  } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK && !pass_through(type)) {
+  } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK && !pass_through(type) &&
+             !(K::S && type == ZBHIP_EL_SUB_PROCESS)) {
+    // SubProcessProcessor.onComplete (:68-82): no output mappings or subscriptions in the subset
     set_fail(L, FB_UNSUPPORTED);
     return;
   }
@@ -1792,15 +1912,26 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       uint2 e = tget(L, t);
       const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
       emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
+      // the task's flow scope: the process instance, or (K::S) the sub-process instance around it
+      bool fs_active = L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED;
+      uint32_t fsk = 0;
+      if constexpr (K::S) {
+        const uint32_t c = scope_of<K>(elem_of(L, task_elem));
+        if (c != 0) {
+          const int ts = scope_find(L, c);
+          fs_active = ts >= 0 && ((tget(L, ts).y >> 16) & 0xFF) == ZBHIP_PI_ELEMENT_ACTIVATED;
+          fsk = ts >= 0 ? tget(L, ts).x >> 16 : 0u;
+        }
+      }
       // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
       e.y &= ~(3u << 24);  // the job row (and its ACTIVATED state) is deleted
-      if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
+      if (fs_active) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
       tput(L, t, e);
-      if (L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED) {  // afterAccept
+      if (fs_active) {  // afterAccept
         uint32_t pe = new_key(L);  // EventTriggerBehavior.triggeringProcessEvent
         emit(L, C_PE_TRIGGERING, pe, task_key, task_elem);
         L.trig_key = task_key;       // ProcessEventTriggeringApplier: EVENT_TRIGGER row
-        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, 0, task_elem, true, true, task_key);
+        follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, fsk, task_elem, true, true, task_key);
       }
     }
   } else if (!L.fail && kind == CMD_FOLLOWUP) {
@@ -2676,6 +2807,7 @@ static hipError_t launch_k(const StepParams& P, hipStream_t s) {
 uint32_t step_resident(int variant, uint32_t prog_words) {
   return variant == 3   ? resident_for<KLinear>(lds_bytes<KLinear>(prog_words))
          : variant == 2 ? resident_for<KMsg>(lds_bytes<KMsg>(prog_words))
+         : variant == 4 ? resident_for<KScope>(lds_bytes<KScope>(prog_words))
          : variant      ? resident_for<KGeneric>(lds_bytes<KGeneric>(prog_words))
                         : resident_for<KSimple>(lds_bytes<KSimple>(prog_words));
 }
@@ -2683,7 +2815,8 @@ uint32_t step_queue(int variant) {
   return variant == 3 ? KLinear::Q : variant == 2 ? KMsg::Q : variant ? KGeneric::Q : KSimple::Q;
 }
 
-// variants: 0 KSimple, 1 KGeneric, 2 KMsg, 3 KLinear
+// variants: 0 KSimple, 1 KGeneric, 2 KMsg, 3 KLinear, 4 KScope (KGeneric's B, T, Q, R)
+static_assert(KScope::B == KGeneric::B && KScope::Q == KGeneric::Q && KScope::R == KGeneric::R, "KScope shapes");
 uint32_t step_block(int variant) {
   return variant == 3 ? KLinear::B : variant == 2 ? KMsg::B : variant ? KGeneric::B : KSimple::B;
 }
@@ -2691,6 +2824,7 @@ uint32_t step_block(int variant) {
 size_t step_lds_bytes(int variant, uint32_t prog_words) {
   return variant == 3   ? lds_bytes<KLinear>(prog_words)
          : variant == 2 ? lds_bytes<KMsg>(prog_words)
+         : variant == 4 ? lds_bytes<KScope>(prog_words)
          : variant      ? lds_bytes<KGeneric>(prog_words)
                         : lds_bytes<KSimple>(prog_words);
 }
@@ -2759,6 +2893,7 @@ hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
     case 3: return launch_k<KLinear>(P, s);
     case 2: return launch_k<KMsg>(P, s);
     case 1: return launch_k<KGeneric>(P, s);
+    case 4: return launch_k<KScope>(P, s);
     default: return launch_k<KSimple>(P, s);
   }
 }

@@ -170,7 +170,7 @@ struct zbhip_handle {
   uint32_t regions_cap = 0;
   size_t region_records = 0;
   uint32_t region_pad = 0;  // records between consecutive regions (region stride B * rec_cap + pad)
-  int variant = 3;                           // kernel variant (zbhip_deploy): 3 KLinear, 0 KSimple, 1 KGeneric, 2 KMsg
+  int variant = 3;                           // kernel variant (zbhip_deploy): 3 KLinear, 0 KSimple, 1 KGeneric, 2 KMsg, 4 KScope
   // launches of the last run: region base, lane count, and the window index of each lane (the
   // main window's rounds: identity or h_order; continuation batches: cont_order)
   struct Launch {
@@ -545,6 +545,9 @@ static uint64_t batch_bound(const Proc& P) {
   auto is_node = [&](size_t e) { return e > 0 && P.els[e].element_type != ZBHIP_EL_SEQUENCE_FLOW; };
   for (size_t f = 0; f < E; ++f)
     if (P.els[f].element_type == ZBHIP_EL_SEQUENCE_FLOW && P.els[f].flow_target < E) ++indeg[P.els[f].flow_target];
+  // a sub-process activates its none start event once per token that reaches it
+  for (size_t e = 1; e < E; ++e)
+    if (P.els[e].element_type == ZBHIP_EL_SUB_PROCESS && P.els[e].start_event < E) ++indeg[P.els[e].start_event];
   std::vector<uint32_t> ready;
   for (size_t e = 0; e < E; ++e)
     if (is_node(e) && indeg[e] == 0) {
@@ -560,6 +563,10 @@ static uint64_t batch_bound(const Proc& P) {
     ++seen;
     total += 2 * tok[e];
     const zbhip_element& N = P.els[e];
+    if (N.element_type == ZBHIP_EL_SUB_PROCESS && N.start_event < E) {
+      tok[N.start_event] += tok[e];
+      if (--indeg[N.start_event] == 0) ready.push_back(N.start_event);
+    }
     for (uint32_t i = 0; i < N.out_count; ++i) {
       const uint32_t f = P.out[N.out_begin + i];
       const uint32_t t = P.els[f].flow_target;
@@ -652,7 +659,8 @@ static int rebuild_program(zbhip_handle* h) {
     for (uint32_t e = 0; e < n_el; ++e) {
       const zbhip_element& E = P.els[e];
       uint32_t sg = 0;
-      if ((E.element_type == ZBHIP_EL_START_EVENT || E.element_type == ZBHIP_EL_SERVICE_TASK) && E.out_count == 1) {
+      if ((E.element_type == ZBHIP_EL_START_EVENT || E.element_type == ZBHIP_EL_SERVICE_TASK) && E.out_count == 1 &&
+          E.flow_scope == 0) {
         const uint32_t f = P.out[E.out_begin];
         const zbhip_element& F = P.els[f];
         const uint32_t n = F.flow_target;
@@ -667,6 +675,14 @@ static int rebuild_program(zbhip_handle* h) {
       }
       pb[seg_off + e] = sg;
     }
+    // NUMBER_OF_TAKEN_SEQUENCE_FLOWS rows of a sub-process's own gateways: removed with the
+    // sub-process instance (DbElementInstanceState.removeInstance)
+    std::vector<uint32_t> join_mask(n_el, 0);
+    for (uint32_t f = 0; f < n_el; ++f) {
+      const zbhip_element& F = P.els[f];
+      if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.join_slot < 16 && F.flow_scope)
+        join_mask[F.flow_scope] |= 1u << F.join_slot;
+    }
     for (uint32_t e = 0; e < n_el; ++e) {
       const zbhip_element& E = P.els[e];
       uint32_t* w = pb + 8 + 4 * e;
@@ -677,8 +693,9 @@ static int rebuild_program(zbhip_handle* h) {
       else if (E.element_type == ZBHIP_EL_SERVICE_TASK) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
       else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
         w[2] = E.message_name | ((uint32_t)E.correlation_var << 16);  // name ids (zbhip_deploy)
+      else if (E.element_type == ZBHIP_EL_SUB_PROCESS) w[2] = E.start_event | (join_mask[e] << 16);
       else w[2] = 0xFFFFFFFFu;
-      w[3] = E.join_slot | ((uint32_t)E.id << 16);
+      w[3] = E.join_slot | ((uint32_t)E.flow_scope << 16);
     }
     uint16_t* outw = reinterpret_cast<uint16_t*>(pb + out_off);
     for (size_t i = 0; i < P.out.size(); ++i) outw[i] = P.out[i];
@@ -735,8 +752,16 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         e.element_type != ZBHIP_EL_END_EVENT && e.element_type != ZBHIP_EL_SERVICE_TASK &&
         e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
         e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT &&
-        !pass_through(e.element_type))
+        e.element_type != ZBHIP_EL_SUB_PROCESS && !pass_through(e.element_type))
       return ZBHIP_EUNSUPP;
+  for (size_t e = 0; e < P.els.size(); ++e) {  // containers: a sub-process element, before its children
+    const zbhip_element& E = P.els[e];
+    if (e > 0 && (E.flow_scope >= e || (E.flow_scope && P.els[E.flow_scope].element_type != ZBHIP_EL_SUB_PROCESS)))
+      return ZBHIP_EINVAL;
+    if (E.element_type == ZBHIP_EL_SUB_PROCESS &&
+        (E.start_event >= P.els.size() || P.els[E.start_event].flow_scope != e))
+      return ZBHIP_EINVAL;
+  }
   for (auto& e : P.els)
     if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
       if (!h->st.n_slots) return ZBHIP_EUNSUPP;  // the handle was opened without message state
@@ -773,16 +798,21 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   //   3 KLinear  -- linear chains: every node <= 1 outgoing flow, no gateways (4 waves/SIMD)
   //   0 KSimple  -- one token per instance (no parallel gateway / multi-outgoing node but an XOR)
   //   1 KGeneric -- everything else in the subset
-  //   2 KMsg     -- message catch events and subscription commands (config 5)
+  //   4 KScope   -- embedded sub-processes (flow scopes below the process)
+  //   2 KMsg     -- message catch events and subscription commands (config 5); a sub-process
+  //                 deployed next to them falls back (KMsg has no flow scopes)
   int cls = 3;
+  bool scopes = false;
   for (auto& e : P.els) {
     if (e.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY && cls == 3) cls = 0;
     if (e.element_type == ZBHIP_EL_PARALLEL_GATEWAY) cls = 1;
     if (e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.out_count > 1)
       cls = 1;
+    scopes |= e.element_type == ZBHIP_EL_SUB_PROCESS;
   }
+  if (scopes) cls = 4;
   if (P.has_msg) cls = 2;
-  auto rank = [](int v) { return v == 3 ? 0 : v == 0 ? 1 : v == 1 ? 2 : 3; };
+  auto rank = [](int v) { return v == 3 ? 0 : v == 0 ? 1 : v == 1 ? 2 : v == 4 ? 3 : 4; };
   const int old_variant = h->variant;
   if (h->procs.empty() || rank(cls) > rank(h->variant)) h->variant = cls;
   if (const char* fv = getenv("ZBHIP_FORCE_VARIANT")) {  // experiments: never below what the processes need
@@ -1258,7 +1288,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.stats = h->d_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
   P.stamp = h->window_stamp;
-  P.tpl = (h->variant == 0 || h->variant == 1) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
+  P.tpl = (h->variant == 0 || h->variant == 1 || h->variant == 4) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
   if (h->msg()) {
     int rc = sync_strings(h);
     if (rc) return rc;
@@ -1972,24 +2002,35 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
   sink(ctx, buf);
   snprintf(buf, sizeof buf, "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY|%lld|%lld", (long long)P.def_key, pik);
   sink(ctx, buf);
+  // the key of the instance of container c (an element's flow scope): the process instance, or the
+  // slot of the sub-process element c (one active instance per sub-process element)
+  auto scope_key = [&](uint32_t c) -> long long {
+    if (c == 0) return pik;
+    for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s)
+      if ((R.slots[s].x & 0xFFFF) == c) return h->key_of(inst, R.slots[s].x >> 16);
+    return pik;
+  };
   for (uint32_t s = 0; s < nslots; ++s) {
     const uint2 e = R.slots[s];
     const uint32_t elem = e.x & 0xFFFF;
     const long long k = h->key_of(inst, e.x >> 16);
     const uint32_t job = e.y & 0xFFFF, state = (e.y >> 16) & 0xFF;
     const bool job_row = (e.y >> 24) & 1;
-    const long long jk = job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
     const zbhip_element& E = P.els[elem];
+    const bool sub = E.element_type == ZBHIP_EL_SUB_PROCESS;  // job field: childCount | activeSequenceFlows << 8
+    const long long jk = sub ? 0 : job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
+    const long long fs = scope_key(E.flow_scope);
     snprintf(buf, sizeof buf,
-             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=0,childActivatedCount=0,childCompletedCount=0,"
+             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%u,childActivatedCount=0,childCompletedCount=0,"
              "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=0,interruptingElementId=,"
              "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
-             "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=0",
-             k, pik, jk, state, P.id(elem).c_str(), E.element_type, E.event_type, pik, pik, (long long)P.def_key);
+             "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%u",
+             k, fs, sub ? job & 0xFF : 0u, jk, state, P.id(elem).c_str(), E.element_type, E.event_type, fs, pik,
+             (long long)P.def_key, sub ? (job >> 8) & 0xFF : 0u);
     sink(ctx, buf);
-    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", pik, k);
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", fs, k);
     sink(ctx, buf);
-    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, pik);
+    snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, fs);
     sink(ctx, buf);
     if (E.element_type == ZBHIP_EL_SERVICE_TASK || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
       snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", k);
@@ -2043,8 +2084,8 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       const uint32_t s = E.join_slot;
       const uint32_t cnt = (R.join[s >> 2] >> ((s & 3) * 8)) & 0xFF;
       if (!cnt) continue;
-      snprintf(buf, sizeof buf, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS|%lld|%s|%s|%u", pik, P.id(E.flow_target).c_str(),
-               P.id(f).c_str(), cnt);
+      snprintf(buf, sizeof buf, "NUMBER_OF_TAKEN_SEQUENCE_FLOWS|%lld|%s|%s|%u", scope_key(E.flow_scope),
+               P.id(E.flow_target).c_str(), P.id(f).c_str(), cnt);
       sink(ctx, buf);
     }
   }

@@ -38,7 +38,8 @@ class _Csr(C.Structure):  # prefix of zbhip_process_csr needed to read the eleme
 ELEMENT_DTYPE = np.dtype([("element_type", "u1"), ("event_type", "u1"), ("out_begin", "<u2"), ("out_count", "<u2"),
                           ("in_count", "<u2"), ("flow_source", "<u2"), ("flow_target", "<u2"), ("condition", "<u2"),
                           ("default_flow", "<u2"), ("job_type", "<u2"), ("job_retries", "<u2"), ("join_slot", "<u2"),
-                          ("id", "<u2"), ("message_name", "<u2"), ("correlation_var", "<u2")])
+                          ("id", "<u2"), ("message_name", "<u2"), ("correlation_var", "<u2"),
+                          ("flow_scope", "<u2"), ("start_event", "<u2")])
 
 
 class Partition:
