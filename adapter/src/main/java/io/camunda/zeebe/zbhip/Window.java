@@ -1,0 +1,337 @@
+/*
+ * One read-ahead window of the adapter: the zbhip_command rows and variable-document entries of
+ * consecutive hot-path commands, their log positions, and after zbhip_run the drained records
+ * (zbhip_record, ordered by source command then ordinal) rebuilt into the reference's record values
+ * and metadata for ProcessingResultBuilder.appendRecord (ProcessingResultBuilder.java:30-54).
+ *
+ * Not compiled in this image (no JDK).  Record values follow ProcessInstanceRecord.java:61-72,
+ * JobRecord.java, VariableRecord.java, ProcessEventRecord.java and
+ * ProcessInstanceCreationRecord.java; the document entries follow the msgpack value mapping of
+ * include/zbhip.h (int64, 6-digit scaled decimals, booleans, nil, value-dictionary strings).
+ */
+package io.camunda.zeebe.zbhip;
+
+import static java.lang.foreign.ValueLayout.JAVA_BYTE;
+import static java.lang.foreign.ValueLayout.JAVA_INT;
+import static java.lang.foreign.ValueLayout.JAVA_LONG;
+import static java.lang.foreign.ValueLayout.JAVA_SHORT;
+
+import io.camunda.zeebe.msgpack.spec.MsgPackReader;
+import io.camunda.zeebe.msgpack.spec.MsgPackToken;
+import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
+import io.camunda.zeebe.protocol.impl.record.UnifiedRecordValue;
+import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessEventRecord;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceRecord;
+import io.camunda.zeebe.protocol.impl.record.value.variable.VariableRecord;
+import io.camunda.zeebe.protocol.record.RecordType;
+import io.camunda.zeebe.protocol.record.RejectionType;
+import io.camunda.zeebe.protocol.record.ValueType;
+import io.camunda.zeebe.protocol.record.intent.Intent;
+import io.camunda.zeebe.protocol.record.intent.JobIntent;
+import io.camunda.zeebe.protocol.record.intent.ProcessEventIntent;
+import io.camunda.zeebe.protocol.record.intent.ProcessInstanceCreationIntent;
+import io.camunda.zeebe.protocol.record.intent.ProcessInstanceIntent;
+import io.camunda.zeebe.protocol.record.intent.VariableIntent;
+import io.camunda.zeebe.protocol.record.value.BpmnElementType;
+import io.camunda.zeebe.protocol.record.value.BpmnEventType;
+import io.camunda.zeebe.stream.api.ProcessingResultBuilder;
+import java.lang.foreign.Arena;
+import java.lang.foreign.MemorySegment;
+import java.util.ArrayList;
+import java.util.Arrays;
+import java.util.List;
+import java.util.function.IntConsumer;
+import org.agrona.DirectBuffer;
+import org.agrona.concurrent.UnsafeBuffer;
+
+final class Window {
+
+  private static final String TENANT = "<default>"; // TenantOwned.DEFAULT_TENANT_IDENTIFIER
+  private static final byte DOC_NIL = 0, DOC_BOOL = 1, DOC_INT = 2, DOC_DEC = 3, DOC_STR = 5; // zbhip_doc_type
+  private static final int MAX = 1 << 16;
+  private static final int MAX_DOCS = 16 * MAX;
+
+  private MemorySegment cmds;
+  private MemorySegment docs;
+  private MemorySegment recs;
+  private long recCap;
+  private int n;
+  private int nDocs;
+  private long nRecs;
+  private long sourceBase; // zbhip_record.source_index of this window's first command (submission order)
+  private final long[] positions = new long[MAX];
+  private final int[] instances = new int[MAX];
+  private int[] recBegin = new int[MAX + 1];
+  // the command's msgpack variable document and each entry's msgpack value (VARIABLE records)
+  private final DirectBuffer[] documents = new DirectBuffer[MAX];
+  private final List<DirectBuffer> entryValues = new ArrayList<>();
+  private final MsgPackReader msgpack = new MsgPackReader();
+
+  void init(final Arena arena) {
+    cmds = arena.allocate(ZbHip.COMMAND.byteSize() * MAX, 16);
+    docs = arena.allocate(ZbHip.DOC_ENTRY.byteSize() * MAX_DOCS, 16);
+  }
+
+  void reset(final long firstPosition) {
+    sourceBase += n;
+    n = 0;
+    nDocs = 0;
+    nRecs = 0;
+    entryValues.clear();
+    Arrays.fill(documents, null);
+  }
+
+  int size() {
+    return n;
+  }
+
+  boolean covers(final long position) {
+    return n > 0 && position >= positions[0] && position <= positions[n - 1];
+  }
+
+  int indexOf(final long position) {
+    final int i = Arrays.binarySearch(positions, 0, n, position);
+    return i >= 0 ? i : -1;
+  }
+
+  int instanceOf(final int i) {
+    return instances[i];
+  }
+
+  /** PROCESS_INSTANCE_CREATION:CREATE -> ZBHIP_CMD_CREATE into instance slot {@code slot}. */
+  boolean addCreate(
+      final long position, final int process, final int slot, final DirectBuffer variables, final GpuBatchProcessor p) {
+    final int first = nDocs;
+    final int count = decodeDocument(variables, p);
+    if (count < 0) {
+      return false;
+    }
+    put(position, slot, ZbHip.CMD_CREATE, count, process, first, variables);
+    return true;
+  }
+
+  /** JOB:COMPLETE -> ZBHIP_CMD_JOB_COMPLETE; ref = zbhip_resolve_key's (slot << 16 | ordinal). */
+  boolean addJobComplete(final long position, final long ref, final DirectBuffer variables, final GpuBatchProcessor p) {
+    final int first = nDocs;
+    final int count = decodeDocument(variables, p);
+    if (count < 0) {
+      return false;
+    }
+    put(position, (int) (ref >>> 16), ZbHip.CMD_JOB_COMPLETE, count, (int) (ref & 0xFFFF), first, variables);
+    return true;
+  }
+
+  private void put(
+      final long position, final int instance, final byte kind, final int docCount, final int ref, final int docBegin,
+      final DirectBuffer variables) {
+    final long o = ZbHip.COMMAND.byteSize() * n;
+    cmds.set(JAVA_INT, o, instance);
+    cmds.set(JAVA_BYTE, o + 4, kind);
+    cmds.set(JAVA_BYTE, o + 5, (byte) docCount);
+    cmds.set(JAVA_SHORT, o + 6, (short) ref);
+    cmds.set(JAVA_INT, o + 8, docBegin);
+    cmds.set(JAVA_INT, o + 12, 0);
+    positions[n] = position;
+    instances[n] = instance;
+    documents[n] = copy(variables, 0, variables.capacity());
+    n++;
+  }
+
+  /**
+   * The command's variable document as zbhip_doc_entry rows (IndexedDocument.java:44-63 order);
+   * -1 when an entry is outside the device's value subset (the command stays on the CPU engine).
+   */
+  private int decodeDocument(final DirectBuffer doc, final GpuBatchProcessor p) {
+    if (doc.capacity() == 0) {
+      return 0;
+    }
+    msgpack.wrap(doc, 0, doc.capacity());
+    final int size = msgpack.readMapHeader();
+    if (size > 255 || nDocs + size > MAX_DOCS) {
+      return -1;
+    }
+    for (int e = 0; e < size; e++) {
+      final MsgPackToken name = msgpack.readToken();
+      final String nameStr = name.getValueBuffer().getStringWithoutLengthUtf8(0, name.getValueBuffer().capacity());
+      final int valueStart = msgpack.getOffset();
+      final MsgPackToken v = msgpack.readToken();
+      final byte type;
+      final long value;
+      switch (v.getType()) {
+        case NIL -> { type = DOC_NIL; value = 0; }
+        case BOOLEAN -> { type = DOC_BOOL; value = v.getBooleanValue() ? 1 : 0; }
+        case INTEGER -> { type = DOC_INT; value = v.getIntegerValue(); }
+        case FLOAT -> {
+          final double d = v.getFloatValue();
+          final long scaled = Math.round(d * 1_000_000d);
+          if ((double) scaled / 1_000_000d != d) {
+            return -1; // not exactly a 6-digit decimal: FEEL over it is outside the subset
+          }
+          type = DOC_DEC;
+          value = scaled;
+        }
+        case STRING -> {
+          final DirectBuffer s = v.getValueBuffer();
+          final byte[] b = new byte[s.capacity()];
+          s.getBytes(0, b);
+          type = DOC_STR;
+          value = p.internString(b);
+        }
+        default -> { return -1; } // arrays, maps, binaries: outside the subset
+      }
+      final long o = ZbHip.DOC_ENTRY.byteSize() * nDocs;
+      docs.set(JAVA_INT, o, p.internName(nameStr));
+      docs.set(JAVA_BYTE, o + 4, type);
+      docs.set(JAVA_LONG, o + 8, value);
+      entryValues.add(copy(doc, valueStart, msgpack.getOffset() - valueStart));
+      nDocs++;
+    }
+    return size;
+  }
+
+  private static DirectBuffer copy(final DirectBuffer src, final int offset, final int length) {
+    final byte[] b = new byte[length];
+    src.getBytes(offset, b);
+    return new UnsafeBuffer(b);
+  }
+
+  /** zbhip_submit + zbhip_run + zbhip_drain; recBegin[i] = first record of window command i. */
+  void submitRunDrain(final MemorySegment handle) {
+    ZbHip.submit(handle, cmds, n, docs, nDocs);
+    ZbHip.run(handle, 0);
+    final long pending = ZbHip.pendingRecords(handle);
+    if (pending > recCap) {
+      recCap = Math.max(pending, 2 * recCap);
+      recs = Arena.ofAuto().allocate(ZbHip.RECORD.byteSize() * recCap, 16);
+    }
+    nRecs = ZbHip.drain(handle, recs, recCap);
+    if (recBegin.length < n + 1) {
+      recBegin = new int[n + 1];
+    }
+    Arrays.fill(recBegin, 0, n + 1, 0);
+    for (long r = 0; r < nRecs; r++) {
+      recBegin[(int) (recs.get(JAVA_LONG, r * 80 + 24) - sourceBase) + 1]++; // records are ordered by source
+    }
+    for (int i = 0; i < n; i++) {
+      recBegin[i + 1] += recBegin[i];
+    }
+  }
+
+  /** Slots of process instances completed by the window (PROCESS ELEMENT_COMPLETED records). */
+  void forEachEndedInstance(final IntConsumer slot) {
+    for (long r = 0; r < nRecs; r++) {
+      final long o = r * 80;
+      if (recs.get(JAVA_BYTE, o + 41) == ValueType.PROCESS_INSTANCE.value()
+          && recs.get(JAVA_BYTE, o + 42) == ProcessInstanceIntent.ELEMENT_COMPLETED.value()
+          && recs.get(JAVA_INT, o + 36) == 0) {
+        slot.accept(instances[(int) (recs.get(JAVA_LONG, o + 24) - sourceBase)]);
+      }
+    }
+  }
+
+  /** Appends window command i's records to the builder, as the reference's processors would. */
+  void emit(final int i, final ProcessingResultBuilder out, final GpuBatchProcessor p) {
+    final RecordMetadata meta = new RecordMetadata();
+    for (int r = recBegin[i]; r < recBegin[i + 1]; r++) {
+      final MemorySegment rec = recs.asSlice(80L * r, 80);
+      final long key = rec.get(JAVA_LONG, 0);
+      final byte recordType = rec.get(JAVA_BYTE, 40);
+      final byte valueType = rec.get(JAVA_BYTE, 41);
+      final byte intent = rec.get(JAVA_BYTE, 42);
+      final int rejection = rec.get(JAVA_BYTE, 43) & 0xFF;
+      meta.reset()
+          .recordType(RecordType.values()[recordType])
+          .valueType(ValueType.get((short) valueType))
+          .intent(intent(valueType, intent));
+      if (rejection != 0xFF) {
+        meta.rejectionType(RejectionType.get((short) rejection)).rejectionReason(p.rejectionReason(rec));
+      }
+      out.appendRecord(key, value(rec, i, p), meta);
+    }
+  }
+
+  private static Intent intent(final byte valueType, final byte intent) {
+    return Intent.fromProtocolValue(ValueType.get((short) valueType), (short) intent);
+  }
+
+  private UnifiedRecordValue value(final MemorySegment r, final int i, final GpuBatchProcessor p) {
+    final ZbHip.Deployed d = p.process(r.get(JAVA_INT, 32) < 0 ? 0 : r.get(JAVA_INT, 32));
+    final int elem = r.get(JAVA_INT, 36);
+    final long scope = r.get(JAVA_LONG, 8);
+    final long pik = r.get(JAVA_LONG, 16);
+    final long aux = r.get(JAVA_LONG, 48);
+    final ValueType vt = ValueType.get((short) r.get(JAVA_BYTE, 41));
+    switch (vt) {
+      case PROCESS_INSTANCE -> {
+        final ProcessInstanceRecord v = new ProcessInstanceRecord();
+        v.setBpmnElementType(BpmnElementType.values()[d.elementTypes()[elem]])
+            .setBpmnEventType(BpmnEventType.values()[d.eventTypes()[elem]])
+            .setElementId(d.elementIds()[elem])
+            .setBpmnProcessId(d.bpmnProcessId())
+            .setVersion(d.version())
+            .setProcessDefinitionKey(d.definitionKey())
+            .setProcessInstanceKey(pik)
+            .setFlowScopeKey(scope)
+            .setParentProcessInstanceKey(-1)
+            .setParentElementInstanceKey(-1)
+            .setTenantId(TENANT);
+        return v;
+      }
+      case JOB -> {
+        final JobRecord v = new JobRecord();
+        if (elem >= 0) {
+          v.setType(d.jobTypes()[elem])
+              .setRetries(d.retries()[elem])
+              .setElementId(d.elementIds()[elem])
+              .setElementInstanceKey(scope)
+              .setProcessInstanceKey(pik)
+              .setBpmnProcessId(d.bpmnProcessId())
+              .setProcessDefinitionVersion(d.version())
+              .setProcessDefinitionKey(d.definitionKey());
+        }
+        if (aux >= 0) {
+          v.setVariables(documents[i]); // JOB:COMPLETED / COMPLETE rejection: the command's variables
+        }
+        return v.setTenantId(TENANT);
+      }
+      case VARIABLE -> {
+        final VariableRecord v = new VariableRecord();
+        v.setName(new UnsafeBuffer(p.name(elem).getBytes()))
+            .setValue(entryValues.get((int) aux))
+            .setScopeKey(scope)
+            .setProcessInstanceKey(pik)
+            .setProcessDefinitionKey(d.definitionKey())
+            .setBpmnProcessId(new UnsafeBuffer(d.bpmnProcessId().getBytes()));
+        return v.setTenantId(TENANT);
+      }
+      case PROCESS_EVENT -> {
+        final ProcessEventRecord v = new ProcessEventRecord();
+        v.setScopeKey(scope)
+            .setTargetElementIdBuffer(new UnsafeBuffer(d.elementIds()[elem].getBytes()))
+            .setVariablesBuffer(documents[i])
+            .setProcessDefinitionKey(d.definitionKey())
+            .setProcessInstanceKey(pik);
+        return v.setTenantId(TENANT);
+      }
+      case PROCESS_INSTANCE_CREATION -> {
+        final ProcessInstanceCreationRecord v = new ProcessInstanceCreationRecord();
+        v.setBpmnProcessId(d.bpmnProcessId())
+            .setProcessDefinitionKey(d.definitionKey())
+            .setVersion(d.version())
+            .setProcessInstanceKey(scope)
+            .setVariables(documents[i]);
+        return v.setTenantId(TENANT);
+      }
+      default -> throw new IllegalStateException("value type outside configs 1-4: " + vt
+          + " (config 5 windows write their log bytes with zbhip_serialize_log)");
+    }
+  }
+
+  static {
+    // record kinds the device emits for configs 1-4 (zbhip.h enums) map onto these reference intents
+    assert JobIntent.CREATED.value() == 0 && VariableIntent.CREATED.value() == 0
+        && ProcessEventIntent.TRIGGERING.value() == 0 && ProcessInstanceCreationIntent.CREATED.value() == 1;
+  }
+}

@@ -5,9 +5,9 @@
  * The library replaces, for one partition, everything from
  * `Engine.process` (engine/src/main/java/io/camunda/zeebe/engine/Engine.java:99-131)
  * down to the zb-db column-family mutations, for the supported element subset
- * (process, none start/end event, service task, undefined and manual task,
- * none intermediate throw event, message intermediate catch event, exclusive
- * gateway, parallel gateway).  It is meant to sit behind the stream-platform `RecordProcessor`
+ * (process, embedded sub-process, none start/end event, service task, undefined
+ * and manual task, none intermediate throw event, message intermediate catch
+ * event, exclusive gateway, parallel gateway).  It is meant to sit behind the stream-platform `RecordProcessor`
  * API (stream-platform/src/main/java/io/camunda/zeebe/stream/api/RecordProcessor.java:17-108):
  * a Java host adapter buffers a window of hot-path commands from the log,
  * submits them, runs them to quiescence and re-emits the drained records per
@@ -25,8 +25,8 @@
  *    (stream-platform/.../state/DbKeyGenerator.java:39-42) would.
  *
  * Element indexing (shared contract with the CPU oracle): element index 0 is
- * the process itself; the process's flow nodes and sequence flows follow in
- * XML document order.
+ * the process itself; the flow nodes and sequence flows follow in XML document
+ * pre-order (an embedded sub-process, then its children, then its next sibling).
  */
 #ifndef ZBHIP_H
 #define ZBHIP_H
@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 2
+#define ZBHIP_ABI_VERSION 3  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes) */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0

@@ -67,3 +67,20 @@ def test_open_without_gpu_fails_loudly():
     with pytest.raises(native.ZbhipError) as e:
         Partition(max_instances=16, max_commands=16)
     assert "ENODEV" in str(e.value)
+
+
+def test_java_adapter_binds_exported_symbols():
+    # adapter/src/main/java/.../ZbHip.java (the Panama FFM binding; no JDK in this image): every
+    # downcall names a function declared in include/zbhip.h and exported by libzbhip.so
+    src = open(os.path.join(ROOT, "adapter", "src", "main", "java", "io", "camunda", "zeebe", "zbhip",
+                            "ZbHip.java")).read()
+    names = re.findall(r'fn\(\s*"(zbhip_[a-z_]+)"', src)
+    assert len(names) >= 20
+    header = open(os.path.join(ROOT, "include", "zbhip.h")).read()
+    lib = native.load()
+    for n in names:
+        assert re.search(r"\b%s\(" % n, header), n
+        assert hasattr(lib, n), n
+    # the struct sizes the binding documents
+    assert C.sizeof(abi.Command) == 16 and C.sizeof(abi.DocEntry) == 16
+    assert C.sizeof(abi.Record) == 80 and C.sizeof(abi.XpartCmd) == 48

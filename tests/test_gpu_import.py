@@ -84,7 +84,7 @@ def _continue(parts, orc, rng, phases):
             assert p.state() == orc.state()
 
 
-@pytest.mark.parametrize("case", ["linear", "fork_join_tasks", "xor_then_tasks"])
+@pytest.mark.parametrize("case", ["linear", "fork_join_tasks", "xor_then_tasks", "sub_parallel", "sub_chain"])
 def test_export_import_continue(case):
     n = 64
     rng = np.random.default_rng(7)
@@ -94,6 +94,11 @@ def test_export_import_continue(case):
         xml = bpmn.linear_process(5)
     elif case == "fork_join_tasks":
         xml = bpmn.fork_join_process(4, tasks=True)
+    elif case == "sub_parallel":  # a sub-process instance with its join counter rows in the state
+        xml = bpmn.sub_process_process("parallel")
+    elif case == "sub_chain":  # nested sub-process instances (flow scopes two levels down)
+        from test_gpu_subprocess import _sub_then_task_then_sub
+        xml = _sub_then_task_then_sub()
     else:  # variables in the state (amount), a gateway behind a task
         xml = (bpmn.createExecutableProcess("p").startEvent("s").serviceTask("t1", "a").exclusiveGateway("x")
                .sequenceFlowId("hi").conditionExpression("= amount > 500").serviceTask("t2", "b").endEvent("e1")
@@ -136,13 +141,13 @@ def test_export_import_continue(case):
     assert [r for r in fresh.state() if not r.startswith("KEY|")] == []
 
 
-@pytest.mark.parametrize("seed", range(8))
-def test_random_processes_restart_equivalence(seed):
+@pytest.mark.parametrize("seed,subs", [(s, False) for s in range(8)] + [(s, True) for s in (1, 3, 4, 7, 19, 22)])
+def test_random_processes_restart_equivalence(seed, subs):
     # ReplayStateRandomizedPropertyTest in the device's terms: random processes, a restart (export
     # -> import into a fresh handle) at a random phase, and the state after every later window
-    # equal to the uninterrupted partition's and the oracle's
+    # equal to the uninterrupted partition's and the oracle's (subs: with embedded sub-processes)
     rng = np.random.default_rng(3000 + seed)
-    xml = random_process(rng)
+    xml = random_process(rng, sub_processes=subs)
     n = 48
     part = Partition(max_instances=n, max_commands=n, max_records_per_batch=256)
     orc = Oracle()

@@ -2426,18 +2426,27 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     // keys of the instance: ordinal 0 the instance, then every other key in key order
     std::vector<const ImpElement*> children;
     std::vector<int64_t> keys;
+    std::set<int64_t> subs;  // embedded sub-process instances of this process instance
     for (const auto& kv : els) {
       const ImpElement& e = kv.second;
       if (e.pik != pe.key || e.key == pe.key) continue;
-      if (e.fs != pe.key) return ZBHIP_EUNSUPP;  // nested scopes: outside the subset
       children.push_back(&e);
       keys.push_back(e.key);
-      if (e.job > 0) keys.push_back(e.job);
+      if (e.type == ZBHIP_EL_SUB_PROCESS) subs.insert(e.key);
+      else if (e.job > 0) keys.push_back(e.job);
+    }
+    // flow scopes: the process instance or one of its sub-process instances (KScope slots); a
+    // sub-process instance's counters live in its slot's job field
+    for (const ImpElement* c : children) {
+      if (c->fs != pe.key && !subs.count(c->fs)) return ZBHIP_EUNSUPP;
+      if (c->type == ZBHIP_EL_SUB_PROCESS && (c->child_count < 0 || c->child_count > 255 || c->asf < 0 || c->asf > 255))
+        return ZBHIP_EUNSUPP;
     }
     std::vector<const ImpVar*> ivars;
     auto scope_of = [&](int64_t s) { return s == pe.key || std::any_of(children.begin(), children.end(), [&](const ImpElement* c) { return c->key == s; }); };
     for (const auto& v : vars)
       if (scope_of(v.scope)) {
+        if (subs.count(v.scope)) return ZBHIP_EUNSUPP;  // sub-process-local variables: outside the subset
         ivars.push_back(&v);
         keys.push_back(v.key);
       }
@@ -2461,8 +2470,13 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       const ImpElement& e = *children[c];
       const int el = elem_of_id(e.id);
       if (el < 0 || P.els[el].element_type != e.type) return ZBHIP_EINVAL;
-      const uint32_t job = e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
-      const uint32_t row = e.job > 0 && job_rows.count(e.job) ? (job_activated_state.count(e.job) ? 3u : 1u) : 0u;
+      if (P.els[el].flow_scope != (e.fs == pe.key ? 0u : els[e.fs].type == ZBHIP_EL_SUB_PROCESS
+                                                              ? (uint32_t)elem_of_id(els[e.fs].id) : ~0u))
+        return ZBHIP_EINVAL;  // the flow scope instance is not the element's container
+      const bool sub_el = e.type == ZBHIP_EL_SUB_PROCESS;
+      const uint32_t job = sub_el ? (uint32_t)e.child_count | ((uint32_t)e.asf << 8)
+                                  : e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
+      const uint32_t row = !sub_el && e.job > 0 && job_rows.count(e.job) ? (job_activated_state.count(e.job) ? 3u : 1u) : 0u;
       slots[c * N + inst] = make_uint2((uint32_t)el | (ord(e.key) << 16), job | (e.state << 16) | (row << 24));
     }
     for (size_t v = 0; v < ivars.size(); ++v) {
@@ -2475,7 +2489,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     }
     for (int w = 0; w < kJoinWords; ++w) join[(size_t)w * N + inst] = 0;
     for (const auto& t : taken) {
-      if (std::get<0>(t) != pe.key) continue;
+      if (std::get<0>(t) != pe.key && !subs.count(std::get<0>(t))) continue;
       int slot = -1;
       for (size_t f = 0; f < P.els.size(); ++f) {
         const zbhip_element& F = P.els[f];
