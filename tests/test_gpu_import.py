@@ -118,7 +118,7 @@ def test_export_import_continue(case):
     part.run()
     _same(part.drain(), (orc.submit(cmds, docs), orc.run(), orc.records())[2])
     # a few completions, one job per instance per window (joins left waiting, tasks open)
-    for _ in range(1 if case == "xor_then_tasks" else 2):
+    for _ in range(1 if case in ("xor_then_tasks", "sub_parallel") else 2):
         c = open_job_completions(part, rng)
         if c is None:
             break
