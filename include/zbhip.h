@@ -120,8 +120,18 @@ enum zbhip_element_type {
   ZBHIP_EL_PARALLEL_GATEWAY = 15,
   ZBHIP_EL_EVENT_BASED_GATEWAY = 16,
   ZBHIP_EL_INCLUSIVE_GATEWAY = 17,
-  ZBHIP_EL_SEQUENCE_FLOW = 18
+  ZBHIP_EL_SEQUENCE_FLOW = 18,
+  ZBHIP_EL_MULTI_INSTANCE_BODY = 19,
+  ZBHIP_EL_CALL_ACTIVITY = 20,
+  ZBHIP_EL_BUSINESS_RULE_TASK = 21,
+  ZBHIP_EL_SCRIPT_TASK = 22,
+  ZBHIP_EL_SEND_TASK = 23
 };
+/* job worker tasks (BpmnElementProcessors.java:46-60 -> JobWorkerTaskProcessor): service and send
+ * tasks, script / business-rule tasks with a zeebe:taskDefinition (no zeebe:script /
+ * zeebe:calledDecision) */
+#define ZBHIP_IS_JOB_WORKER(t) ((t) == ZBHIP_EL_SERVICE_TASK || (t) == ZBHIP_EL_SEND_TASK || \
+                                (t) == ZBHIP_EL_SCRIPT_TASK || (t) == ZBHIP_EL_BUSINESS_RULE_TASK)
 enum zbhip_event_type {
   ZBHIP_EV_UNSPECIFIED = 0,
   ZBHIP_EV_CONDITIONAL = 1,

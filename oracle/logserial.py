@@ -204,7 +204,8 @@ ELEMENT_TYPE = {0: "UNSPECIFIED", 1: "PROCESS", 2: "SUB_PROCESS", 3: "EVENT_SUB_
                 5: "INTERMEDIATE_CATCH_EVENT", 6: "INTERMEDIATE_THROW_EVENT", 7: "BOUNDARY_EVENT", 8: "END_EVENT",
                 9: "SERVICE_TASK", 10: "RECEIVE_TASK", 11: "USER_TASK", 12: "MANUAL_TASK", 13: "TASK",
                 14: "EXCLUSIVE_GATEWAY", 15: "PARALLEL_GATEWAY", 16: "EVENT_BASED_GATEWAY", 17: "INCLUSIVE_GATEWAY",
-                18: "SEQUENCE_FLOW"}
+                18: "SEQUENCE_FLOW", 19: "MULTI_INSTANCE_BODY", 20: "CALL_ACTIVITY", 21: "BUSINESS_RULE_TASK",
+                22: "SCRIPT_TASK", 23: "SEND_TASK"}
 EVENT_TYPE = {0: "UNSPECIFIED", 1: "CONDITIONAL", 2: "ERROR", 3: "ESCALATION", 4: "LINK", 5: "MESSAGE", 6: "NONE",
               7: "SIGNAL", 8: "TERMINATE", 9: "TIMER"}
 

@@ -387,9 +387,16 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
         return false;
       }
       e.event = ZBHIP_EV_NONE;  // EndEventTransformer.java:37
-    } else if (n == "serviceTask") {
-      e.type = ZBHIP_EL_SERVICE_TASK;
+    } else if (n == "serviceTask" || n == "sendTask" || n == "scriptTask" || n == "businessRuleTask") {
+      // job worker tasks (BpmnElementProcessors.java:46-60): JobWorkerTaskProcessor, or the job
+      // behaviour of ScriptTaskProcessor / BusinessRuleTaskProcessor (a zeebe:taskDefinition)
+      e.type = n == "serviceTask" ? ZBHIP_EL_SERVICE_TASK : n == "sendTask" ? ZBHIP_EL_SEND_TASK
+               : n == "scriptTask" ? ZBHIP_EL_SCRIPT_TASK : ZBHIP_EL_BUSINESS_RULE_TASK;
       const XNode* ext = k->child("extensionElements");
+      if (ext && (ext->child("script") || ext->child("calledDecision"))) {
+        err = "script / decision task without a job outside the supported subset";
+        return false;
+      }
       const XNode* td = ext ? ext->child("taskDefinition") : nullptr;
       if (!td) { err = "service task without zeebe:taskDefinition"; return false; }
       e.job_type = td->attr("type");
@@ -1622,7 +1629,10 @@ class Oracle {
         pi_event(key, ZBHIP_PI_ELEMENT_COMPLETING, v);
         complete_and_take(el, key, v, /*output_mappings=*/true);
         break;
-      case ZBHIP_EL_SERVICE_TASK: {  // JobWorkerTaskProcessor.onActivate (processing/bpmn/task/JobWorkerTaskProcessor.java:49-61)
+      case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onActivate (processing/bpmn/task/JobWorkerTaskProcessor.java:49-61)
+      case ZBHIP_EL_SEND_TASK:
+      case ZBHIP_EL_SCRIPT_TASK:
+      case ZBHIP_EL_BUSINESS_RULE_TASK: {
         // BpmnJobBehavior.createNewJob -> writeJobCreatedEvent (behavior/BpmnJobBehavior.java:113-119,194-218)
         JobRow job;
         job.pi = v;
@@ -1677,6 +1687,9 @@ class Oracle {
         complete_and_take(el, key, v, true);
         break;
       case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onComplete (:63-75)
+      case ZBHIP_EL_SEND_TASK:
+      case ZBHIP_EL_SCRIPT_TASK:
+      case ZBHIP_EL_BUSINESS_RULE_TASK:
       case ZBHIP_EL_INTERMEDIATE_THROW_EVENT:  // NoneIntermediateThrowEventBehavior.onComplete (:128-137)
         complete_and_take(el, key, v, true);
         break;
@@ -1833,7 +1846,7 @@ class Oracle {
     switch (intent) {
       case ZBHIP_PI_ELEMENT_ACTIVATING: {  // ProcessInstanceElementActivatingApplier.applyState (:48-77)
         // createEventScope (:255-289): job worker elements get an event scope
-        if (el.type == ZBHIP_EL_SERVICE_TASK || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) event_scope_.insert(key);
+        if (ZBHIP_IS_JOB_WORKER(el.type) || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) event_scope_.insert(key);
         // cleanupSequenceFlowsTaken (:79-98): Tetris decrement of (flowScope, gateway)
         if (el.type == ZBHIP_EL_PARALLEL_GATEWAY) {
           for (auto it = taken_.lower_bound({v.flowScopeKey, v.elem, -1}); it != taken_.end();) {

@@ -13,8 +13,10 @@ ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
 
 
 class _Gen:
-    def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True, sub_processes=False):
+    def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True, sub_processes=False,
+                 task_kinds=False):
         self.rng = rng
+        self.task_kinds = task_kinds
         self.sub_processes = sub_processes
         self.scope = None  # the sub-process being filled (None: the process)
         self.subs = 0
@@ -92,7 +94,10 @@ class _Gen:
             self.flow(cur, t)
             return t
         if c == "task":
-            t = self.node("serviceTask", job_type="job%d" % int(r.integers(0, 3)))
+            kind = "serviceTask"
+            if self.task_kinds:  # the job worker tasks (JobWorkerTaskBlockBuilder's choices)
+                kind = ("serviceTask", "sendTask", "scriptTask", "businessRuleTask")[int(r.integers(0, 4))]
+            t = self.node(kind, job_type="job%d" % int(r.integers(0, 3)))
             self.flow(cur, t)
             return t
         if c == "catch":
@@ -130,9 +135,10 @@ class _Gen:
 
 
 def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False,
-                   tasks=True, sub_processes=False):
-    """tasks=False: no wait states (the CREATE batch runs the instance to its end)."""
-    g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes)
+                   tasks=True, sub_processes=False, task_kinds=False):
+    """tasks=False: no wait states (the CREATE batch runs the instance to its end); task_kinds: job
+    worker tasks among service / send / script / business-rule tasks."""
+    g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes, task_kinds)
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")
@@ -144,9 +150,9 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
         for kind, nid, extra in g.nodes:
             if extra["scope"] != scope:
                 continue
-            if kind == "serviceTask":
-                out.append('%s<serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s/>'
-                           '</extensionElements></serviceTask>' % (ind, quoteattr(nid), quoteattr(extra["job_type"])))
+            if kind in ("serviceTask", "sendTask", "scriptTask", "businessRuleTask"):
+                out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s/>'
+                           '</extensionElements></%s>' % (ind, kind, quoteattr(nid), quoteattr(extra["job_type"]), kind))
             elif kind == "exclusiveGateway" and nid in g.defaults:
                 out.append('%s<exclusiveGateway id=%s default=%s/>' % (ind, quoteattr(nid), quoteattr(g.defaults[nid])))
             elif kind == "intermediateCatchEvent":

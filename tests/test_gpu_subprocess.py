@@ -3,7 +3,8 @@ row 4) against the CPU oracle: records (flowScopeKey of every element inside a s
 sub-process instance's key), exported state (the sub-process's childCount / activeSequenceFlows,
 parent-child rows, taken-flow counters keyed by the sub-process instance), log bytes (host and
 device serialisers) and zb-db bytes.  Shapes from EmbeddedSubProcessTest.java:41-62,386-467 and
-random structured processes with nested sub-processes (tests/random_bpmn.py)."""
+random structured processes with nested sub-processes (tests/random_bpmn.py).  Also the other job
+worker tasks (send / script / business-rule tasks with a zeebe:taskDefinition)."""
 import numpy as np
 import pytest
 
@@ -12,7 +13,7 @@ from random_bpmn import random_process
 from test_gpu_logdev import Log, job_completions
 from test_gpu_logserial import Pair
 from test_gpu_logserial import drive as drive_log
-from test_gpu_parity import drive, run_both
+from test_gpu_parity import drive
 from oracle.oracle import Oracle
 from zeebe_amd import abi, bpmn
 from zeebe_amd.engine import Partition
@@ -137,3 +138,25 @@ def test_gpu_second_active_instance_of_a_sub_process_falls_back():
     subs = [r for r in o.records() if r["value_type"] == abi.VT_PROCESS_INSTANCE and r["intent"] == 3
             and o.element_type(0, int(r["element_idx"])) == ET["SUB_PROCESS"]]
     assert len(subs) == 2
+
+
+# ---- job worker tasks: send / script / business-rule tasks with a zeebe:taskDefinition ----------
+def test_gpu_job_worker_task_kinds_linear():
+    # a linear chain of the four job worker kinds: KLinear's straight-line segments cover them
+    from test_oracle_subprocess import _job_worker_chain
+    part, orc = drive(_job_worker_chain(), 500, phases=6)
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []
+
+
+def test_gpu_job_worker_task_kinds_log_bytes():
+    from test_oracle_subprocess import _job_worker_chain
+    drive_log(Pair(_job_worker_chain(), 100), 100)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_random_job_worker_kinds_with_sub_processes(seed):
+    rng = np.random.default_rng(4000 + seed)
+    xml = random_process(rng, sub_processes=True, task_kinds=True)
+    part, orc = drive(xml, 96, lambda n: amount_docs(rng.integers(0, 1000, n), 0), phases=60, rng_seed=seed,
+                      max_records=256)
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []

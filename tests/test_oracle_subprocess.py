@@ -186,3 +186,39 @@ def test_sub_processes_outside_the_subset_are_refused(inner):
         Compiled(xml)
     with pytest.raises(OracleError):
         Oracle().deploy(xml)
+
+
+def _job_worker_chain():
+    b = bpmn.createExecutableProcess("process").startEvent("start")
+    for kind in ("serviceTask", "sendTask", "scriptTask", "businessRuleTask"):
+        b.jobWorkerTask(kind, kind + "-1", kind)
+    return b.endEvent("end").done()
+
+
+def test_job_worker_tasks_create_jobs():
+    # BpmnElementProcessors.java:46-60: send tasks and script / business-rule tasks with a
+    # zeebe:taskDefinition run JobWorkerTaskProcessor -- JOB:CREATED with the element's type and id
+    o = Oracle()
+    recs = list(_create(o, _job_worker_chain()))
+    kinds = ["SERVICE_TASK", "SEND_TASK", "SCRIPT_TASK", "BUSINESS_RULE_TASK"]
+    for step, kind in enumerate(kinds):
+        job = [r for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED][-1]
+        assert abi.ELEMENT_TYPES[o.element_type(0, int(job["element_idx"]))] == kind
+        assert ("JOBS|%d|type=%s," % (int(job["key"]), o.element_id(0, int(job["element_idx"])).split("-")[0])
+                in "\n".join(o.state()))
+        recs = list(_run(o, complete_commands([0], [int(job["key"]) - BASE - 1])))
+    assert ("PROCESS", "ELEMENT_COMPLETED") in _types(o, recs)
+
+
+@pytest.mark.parametrize("ext", ['<zeebe:script expression="=1" resultVariable="x"/>',
+                                 '<zeebe:calledDecision decisionId="d" resultVariable="x"/>'])
+def test_script_and_decision_tasks_without_a_job_are_refused(ext):
+    tag = "scriptTask" if "script" in ext else "businessRuleTask"
+    xml = ('<definitions xmlns="http://www.omg.org/spec/BPMN/20100524/MODEL" xmlns:zeebe="http://camunda.org/schema/zeebe/1.0">'
+           '<process id="p" isExecutable="true"><startEvent id="a"/><%s id="t"><extensionElements>%s'
+           '</extensionElements></%s><sequenceFlow id="f" sourceRef="a" targetRef="t"/></process></definitions>'
+           % (tag, ext, tag))
+    with pytest.raises(ZbhipError):
+        Compiled(xml)
+    with pytest.raises(OracleError):
+        Oracle().deploy(xml)

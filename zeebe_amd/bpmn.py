@@ -84,6 +84,14 @@ class ProcessBuilder:
         n.retries = retries
         return self
 
+    def jobWorkerTask(self, kind, id_=None, job_type=None, retries=None):
+        """sendTask / scriptTask / businessRuleTask with a zeebe:taskDefinition (job workers, like
+        serviceTask: BpmnElementProcessors.java:46-60)."""
+        n = self._add_node(kind, id_)
+        n.job_type = job_type if job_type is not None else "task"
+        n.retries = retries
+        return self
+
     def zeebeJobType(self, t):
         self.current.job_type = t
         return self
@@ -201,10 +209,11 @@ class ProcessBuilder:
                     else:
                         out.append("%s<sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
                                    % (ind, attrs, escape(c.condition)))
-                elif c.kind == "serviceTask":
+                elif c.kind in ("serviceTask", "sendTask", "scriptTask", "businessRuleTask"):
                     retries = ' retries="%s"' % c.retries if c.retries is not None else ""
-                    out.append('%s<serviceTask id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
-                               '</extensionElements></serviceTask>' % (ind, quoteattr(c.id), quoteattr(c.job_type), retries))
+                    out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
+                               '</extensionElements></%s>' % (ind, c.kind, quoteattr(c.id), quoteattr(c.job_type), retries,
+                                                             c.kind))
                 elif c.kind == "intermediateCatchEvent" and c.message:
                     catches.append(c)
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'

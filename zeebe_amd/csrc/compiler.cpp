@@ -417,6 +417,9 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       if (c.tag == "startEvent") type = ZBHIP_EL_START_EVENT;
       else if (c.tag == "endEvent") type = ZBHIP_EL_END_EVENT;
       else if (c.tag == "serviceTask") type = ZBHIP_EL_SERVICE_TASK;
+      else if (c.tag == "sendTask") type = ZBHIP_EL_SEND_TASK;
+      else if (c.tag == "scriptTask") type = ZBHIP_EL_SCRIPT_TASK;
+      else if (c.tag == "businessRuleTask") type = ZBHIP_EL_BUSINESS_RULE_TASK;
       else if (c.tag == "exclusiveGateway") type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
       else if (c.tag == "parallelGateway") type = ZBHIP_EL_PARALLEL_GATEWAY;
       else if (c.tag == "sequenceFlow") type = ZBHIP_EL_SEQUENCE_FLOW;
@@ -484,8 +487,14 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         e.message_name = C.str(mi->second.name);
         e.correlation_var = C.str(mi->second.corr);
       }
-      if (type == ZBHIP_EL_SERVICE_TASK) {
+      if (ZBHIP_IS_JOB_WORKER(type)) {
+        // job worker tasks: a zeebe:taskDefinition (a zeebe:script / zeebe:calledDecision is
+        // ScriptTaskProcessor's / BusinessRuleTaskProcessor's non-job behaviour: outside the subset)
         const Elem* ext = c.first("extensionElements");
+        if (ext && (ext->first("script") || ext->first("calledDecision"))) {
+          err = "script / decision tasks without a job outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
         const Elem* td = ext ? ext->first("taskDefinition") : nullptr;
         const std::string* jt = td ? td->get("type") : nullptr;
         if (!jt || jt->empty()) { err = "service task '" + *id + "' without a job type"; return ZBHIP_EPARSE; }

@@ -1160,7 +1160,10 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         transition_to_completed_child(L, t, elem, w, key);
         take_outgoing(L, w);
         return;
-      case ZBHIP_EL_SERVICE_TASK: {  // JobWorkerTaskProcessor.onActivate (:49-61)
+      case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onActivate (:49-61); the job worker
+      case ZBHIP_EL_SEND_TASK:     // send / script / business-rule tasks (BpmnElementProcessors.java:46-60)
+      case ZBHIP_EL_SCRIPT_TASK:
+      case ZBHIP_EL_BUSINESS_RULE_TASK: {
         uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
         emit(L, C_JOB_CREATED, job, key, elem);
         uint2 e = tget(L, t);   // JobCreatedApplier: element instance jobKey
@@ -1255,11 +1258,11 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       // IntermediateCatchEventProcessor.onComplete -> unsubscribeFromEvents: a subscription still
       // open here would write PROCESS_MESSAGE_SUBSCRIPTION:DELETING (outside the subset)
       if (((L.pm_x >> 12) & 3) != 0 && (L.pm_y & 0xFFFF) == cmd_key) { set_fail(L, FB_MESSAGE); return; }
-    } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK && !pass_through(type)) {
+    } else if (type != ZBHIP_EL_START_EVENT && !ZBHIP_IS_JOB_WORKER(type) && !pass_through(type)) {
       set_fail(L, FB_UNSUPPORTED);
       return;
     }
-  } else if (type != ZBHIP_EL_START_EVENT && type != ZBHIP_EL_SERVICE_TASK && !pass_through(type) &&
+  } else if (type != ZBHIP_EL_START_EVENT && !ZBHIP_IS_JOB_WORKER(type) && !pass_through(type) &&
              !(K::S && type == ZBHIP_EL_SUB_PROCESS)) {
     // SubProcessProcessor.onComplete (:68-82): no output mappings or subscriptions in the subset
     set_fail(L, FB_UNSUPPORTED);

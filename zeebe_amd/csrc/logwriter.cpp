@@ -80,7 +80,8 @@ const char* element_type_name(uint32_t t) {
   static const char* n[] = {"UNSPECIFIED", "PROCESS", "SUB_PROCESS", "EVENT_SUB_PROCESS", "START_EVENT",
                             "INTERMEDIATE_CATCH_EVENT", "INTERMEDIATE_THROW_EVENT", "BOUNDARY_EVENT", "END_EVENT",
                             "SERVICE_TASK", "RECEIVE_TASK", "USER_TASK", "MANUAL_TASK", "TASK", "EXCLUSIVE_GATEWAY",
-                            "PARALLEL_GATEWAY", "EVENT_BASED_GATEWAY", "INCLUSIVE_GATEWAY", "SEQUENCE_FLOW"};
+                            "PARALLEL_GATEWAY", "EVENT_BASED_GATEWAY", "INCLUSIVE_GATEWAY", "SEQUENCE_FLOW",
+                            "MULTI_INSTANCE_BODY", "CALL_ACTIVITY", "BUSINESS_RULE_TASK", "SCRIPT_TASK", "SEND_TASK"};
   return t < sizeof(n) / sizeof(n[0]) ? n[t] : "UNSPECIFIED";
 }
 const char* event_type_name(uint32_t t) {
@@ -213,7 +214,7 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
     mp_int(S.pi_tail, -1);
     key(S.pi_tail, "tenantId");
     key(S.pi_tail, kTenant);
-    if (E.element_type == ZBHIP_EL_SERVICE_TASK) {
+    if (ZBHIP_IS_JOB_WORKER(E.element_type)) {
       // JobRecord (JobRecord.java:67-83) as BpmnJobBehavior.writeJobCreatedEvent fills it
       mp_map(S.job_head, 17);
       key(S.job_head, "deadline");

@@ -659,17 +659,17 @@ static int rebuild_program(zbhip_handle* h) {
     for (uint32_t e = 0; e < n_el; ++e) {
       const zbhip_element& E = P.els[e];
       uint32_t sg = 0;
-      if ((E.element_type == ZBHIP_EL_START_EVENT || E.element_type == ZBHIP_EL_SERVICE_TASK) && E.out_count == 1 &&
+      if ((E.element_type == ZBHIP_EL_START_EVENT || ZBHIP_IS_JOB_WORKER(E.element_type)) && E.out_count == 1 &&
           E.flow_scope == 0) {
         const uint32_t f = P.out[E.out_begin];
         const zbhip_element& F = P.els[f];
         const uint32_t n = F.flow_target;
         if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.condition == ZBHIP_NONE16 && n < n_el && f < 0xFFF && n < 0xFFF) {
           const zbhip_element& N = P.els[n];
-          const bool task = N.element_type == ZBHIP_EL_SERVICE_TASK;
+          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type);
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
           if (task || end)
-            sg = (1u << 31) | (E.element_type == ZBHIP_EL_SERVICE_TASK ? 1u << 30 : 0u) | (end ? 1u << 24 : 0u) |
+            sg = (1u << 31) | (ZBHIP_IS_JOB_WORKER(E.element_type) ? 1u << 30 : 0u) | (end ? 1u << 24 : 0u) |
                  (n << 12) | f;
         }
       }
@@ -690,7 +690,7 @@ static int rebuild_program(zbhip_handle* h) {
       w[1] = E.out_begin | ((uint32_t)E.out_count << 16);
       if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW) w[2] = E.flow_target | ((uint32_t)E.condition << 16);
       else if (E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY) w[2] = E.default_flow | (0xFFFFu << 16);
-      else if (E.element_type == ZBHIP_EL_SERVICE_TASK) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
+      else if (ZBHIP_IS_JOB_WORKER(E.element_type)) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
       else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
         w[2] = E.message_name | ((uint32_t)E.correlation_var << 16);  // name ids (zbhip_deploy)
       else if (E.element_type == ZBHIP_EL_SUB_PROCESS) w[2] = E.start_event | (join_mask[e] << 16);
@@ -749,7 +749,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   P.bpmn_id = csr->bpmn_process_id;
   for (auto& e : P.els)
     if (e.element_type != ZBHIP_EL_PROCESS && e.element_type != ZBHIP_EL_START_EVENT &&
-        e.element_type != ZBHIP_EL_END_EVENT && e.element_type != ZBHIP_EL_SERVICE_TASK &&
+        e.element_type != ZBHIP_EL_END_EVENT && !ZBHIP_IS_JOB_WORKER(e.element_type) &&
         e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
         e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT &&
         e.element_type != ZBHIP_EL_SUB_PROCESS && !pass_through(e.element_type))
@@ -821,7 +821,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   }
   P.job_type_id.assign(P.els.size(), ~0u);
   for (size_t e = 0; e < P.els.size(); ++e)
-    if (P.els[e].element_type == ZBHIP_EL_SERVICE_TASK && P.els[e].job_type < P.strings.size())
+    if (ZBHIP_IS_JOB_WORKER(P.els[e].element_type) && P.els[e].job_type < P.strings.size())
       P.job_type_id[e] = h->job_type(P.strings[P.els[e].job_type]);
   h->procs.push_back(std::move(P));
   {
@@ -2032,7 +2032,7 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     sink(ctx, buf);
     snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, fs);
     sink(ctx, buf);
-    if (E.element_type == ZBHIP_EL_SERVICE_TASK || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+    if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
       snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", k);
       sink(ctx, buf);
     }
