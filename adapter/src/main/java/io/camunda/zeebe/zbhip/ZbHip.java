@@ -254,7 +254,7 @@ public final class ZbHip {
   /**
    * zbhip_compile_bpmn + zbhip_deploy: the deployment, or null when the process uses a construct
    * outside the GPU subset (ZBHIP_EUNSUPP: its commands stay on the CPU engine).  The element table
-   * is read from the compiled CSR (zbhip_process_csr / zbhip_element, 32-byte elements).
+   * is read from the compiled CSR (zbhip_process_csr / zbhip_element, 36-byte elements).
    */
   public static Deployed deploy(final MemorySegment h, final byte[] bpmnXml, final long definitionKey, final int version) {
     try (Arena a = Arena.ofConfined()) {
@@ -275,7 +275,7 @@ public final class ZbHip {
         }
         check(d, "zbhip_deploy");
         final int n = c.get(JAVA_INT, 0);
-        final MemorySegment els = c.get(ADDRESS, 8).reinterpret(32L * n);
+        final MemorySegment els = c.get(ADDRESS, 8).reinterpret(36L * n);
         final int nStrings = c.get(JAVA_INT, 64);
         final MemorySegment strs = c.get(ADDRESS, 72).reinterpret(8L * nStrings);
         final String[] strings = new String[nStrings];
@@ -288,7 +288,7 @@ public final class ZbHip {
         final byte[] events = new byte[n];
         final int[] retries = new int[n];
         for (int e = 0; e < n; e++) {
-          final long o = 32L * e;
+          final long o = 36L * e;
           types[e] = els.get(JAVA_BYTE, o);
           events[e] = els.get(JAVA_BYTE, o + 1);
           final int jt = els.get(JAVA_SHORT, o + 16) & 0xFFFF;

@@ -60,7 +60,8 @@ enum zbhip_value_type {
   ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION = 12,
   ZBHIP_VT_VARIABLE = 17,
   ZBHIP_VT_PROCESS_INSTANCE_CREATION = 19,
-  ZBHIP_VT_PROCESS_EVENT = 24
+  ZBHIP_VT_PROCESS_EVENT = 24,
+  ZBHIP_VT_TIMER = 15
 };
 enum zbhip_rejection_type {
   ZBHIP_REJ_INVALID_ARGUMENT = 0,
@@ -89,6 +90,8 @@ enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2 };
 enum { ZBHIP_VAR_CREATED = 0, ZBHIP_VAR_UPDATED = 1 };
 enum { ZBHIP_PE_TRIGGERING = 0 };
 enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
+/* TimerIntent (protocol/.../intent/TimerIntent.java:19-30) */
+enum { ZBHIP_TIMER_CREATED = 0, ZBHIP_TIMER_TRIGGER = 1, ZBHIP_TIMER_TRIGGERED = 2 };
 /* MessageIntent, MessageSubscriptionIntent, ProcessMessageSubscriptionIntent
  * (protocol/.../intent/MessageIntent.java:19-23, MessageSubscriptionIntent.java:19-30,
  * ProcessMessageSubscriptionIntent.java:19-28) */
@@ -168,6 +171,7 @@ typedef struct zbhip_element {
                           * element (ExecutableFlowElement.getFlowScope, FlowElementInstantiationTransformer) */
   uint16_t start_event;  /* process / embedded sub-process: its none start event
                           * (ExecutableFlowElementContainer.getNoneStartEvent); else ZBHIP_NONE16 */
+  uint32_t duration_ms;  /* timer catch event: the static timeDuration in ms (Interval.parse); else 0 */
 } zbhip_element;
 
 /* FEEL condition bytecode (subset of feel-scala 1.17.0 boolean expressions,
@@ -262,7 +266,11 @@ enum zbhip_command_kind {
   ZBHIP_CMD_MSG_SUB_CREATE = 4,    /* MessageSubscriptionCreateProcessor.java:83-104 */
   ZBHIP_CMD_PMS_CREATE = 5,        /* ProcessMessageSubscriptionCreateProcessor */
   ZBHIP_CMD_PMS_CORRELATE = 6,     /* ProcessMessageSubscriptionCorrelateProcessor */
-  ZBHIP_CMD_MSG_SUB_CORRELATE = 7  /* MessageSubscriptionCorrelateProcessor */
+  ZBHIP_CMD_MSG_SUB_CORRELATE = 7, /* MessageSubscriptionCorrelateProcessor */
+  /* TIMER:TRIGGER (TriggerTimerProcessor.java:81-114, written by DueDateTimerChecker for a due
+   * timer): instance = the instance slot, ref = the timer key's ordinal in the instance,
+   * (doc_begin | pad << 32) = the timer's dueDate (the command's TimerRecord.dueDate) */
+  ZBHIP_CMD_TIMER_TRIGGER = 8
 };
 
 /* STR values are string ids of the partition's value dictionary (zbhip_intern_string). */
@@ -349,6 +357,9 @@ int32_t zbhip_subscription_partition(const char* bytes, size_t len, int32_t part
                                        (zbhip_serialize_log_device reads them there) */
 /* Processes the submitted window to quiescence.  Returns #commands processed or <0. */
 int zbhip_run(zbhip_handle* h, uint32_t flags);
+/* ActorClock.currentTimeMillis() for the next runs: timer catch events get dueDate = now + their
+ * duration (CatchEventBehavior.subscribeToTimerEvent, CatchEventBehavior.java:303-330). */
+int zbhip_set_clock(zbhip_handle* h, int64_t now_ms);
 
 /* ---- results ------------------------------------------------------------- */
 /* Drained record (one per follow-up record of a batch), ordered by (source, ordinal). */
@@ -463,7 +474,9 @@ enum zbhip_reason {
   ZBHIP_REASON_PMS_CREATE_NOT_OPENING = 9, /* ... NOT_OPENING_MSG ("opened"/"closing") */
   ZBHIP_REASON_PMS_CORR_NOT_FOUND = 10, /* ProcessMessageSubscriptionCorrelateProcessor NO_SUBSCRIPTION_FOUND */
   ZBHIP_REASON_PMS_CORR_NO_EVENT = 11,  /* ... NO_EVENT_OCCURRED_MESSAGE */
-  ZBHIP_REASON_MS_CORR_NOT_FOUND = 12   /* MessageSubscriptionCorrelateProcessor NO_SUBSCRIPTION_FOUND */
+  ZBHIP_REASON_MS_CORR_NOT_FOUND = 12,  /* MessageSubscriptionCorrelateProcessor NO_SUBSCRIPTION_FOUND */
+  ZBHIP_REASON_TIMER_NOT_FOUND = 13,    /* TriggerTimerProcessor NO_TIMER_FOUND_MESSAGE */
+  ZBHIP_REASON_TIMER_NOT_ACTIVE = 14    /* TriggerTimerProcessor NO_ACTIVE_TIMER_MESSAGE */
 };
 /* Rejection reason text exactly as the reference writes it. */
 int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, size_t cap);

@@ -176,6 +176,11 @@ VARIABLE = [
 PROCESS_EVENT = [
     ("scopeKey", "long", NO_DEFAULT), ("targetElementId", "str", NO_DEFAULT), ("variables", "bin", EMPTY_DOCUMENT),
     ("processDefinitionKey", "long", -1), ("processInstanceKey", "long", -1), ("tenantId", "str", "<default>")]
+# TimerRecord.java:24-40 (every property written by CatchEventBehavior.subscribeToTimerEvent)
+TIMER = [
+    ("elementInstanceKey", "long", NO_DEFAULT), ("processInstanceKey", "long", NO_DEFAULT),
+    ("dueDate", "long", NO_DEFAULT), ("targetElementId", "str", NO_DEFAULT), ("repetitions", "int", NO_DEFAULT),
+    ("processDefinitionKey", "long", NO_DEFAULT), ("tenantId", "str", "<default>")]
 # ProcessInstanceCreationRecord.java:32-55 (ArrayProperty is always set, ArrayProperty.java)
 PROCESS_INSTANCE_CREATION = [
     ("bpmnProcessId", "str", ""), ("processDefinitionKey", "long", -1), ("processInstanceKey", "long", -1),
@@ -285,6 +290,7 @@ def log_entry(key, metadata, value, position, source_position, timestamp, proces
 RT_EVENT, RT_COMMAND, RT_REJECTION = 0, 1, 2
 VT_JOB, VT_PI, VT_VARIABLE, VT_PIC, VT_PE = 0, 5, 17, 19, 24
 VT_MESSAGE, VT_MS, VT_PMS = 10, 11, 12
+VT_TIMER = 15
 NO_STRING, NO_NAME = 0xFFFFFFFF, 0xFFFF
 
 
@@ -353,6 +359,11 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
         return write_object(PROCESS_EVENT, dict(scopeKey=int(r["scope_key"]), targetElementId=el[2], variables=src_doc,
                                                 processDefinitionKey=p["key"],
                                                 processInstanceKey=int(r["process_instance_key"])))
+    if vt == VT_TIMER:  # a rejected TIMER:TRIGGER: the command's key and dueDate (the window's view of it)
+        return write_object(TIMER, dict(elementInstanceKey=int(r["scope_key"]),
+                                        processInstanceKey=int(r["process_instance_key"]), dueDate=int(r["aux"]),
+                                        targetElementId=el[2] if el is not None else "", repetitions=1,
+                                        processDefinitionKey=p["key"] if p is not None else -1))
     if vt == VT_PIC:
         return write_object(PROCESS_INSTANCE_CREATION, dict(
             bpmnProcessId=p["bpmn_process_id"], processDefinitionKey=p["key"],

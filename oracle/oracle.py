@@ -65,6 +65,8 @@ def lib():
         L.zbo_records.restype = C.c_size_t
         L.zbo_records.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.zbo_reason.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        L.zbo_set_clock.argtypes = [C.c_void_p, C.c_int64]
+        L.zbo_set_clock.restype = None
         L.zbo_clear_records.argtypes = [C.c_void_p]
         L.zbo_resolve.restype = C.c_int64
         L.zbo_resolve.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
@@ -128,6 +130,10 @@ class Oracle:
 
     def element_id(self, proc, elem):
         return self.L.zbo_element_id(self.h, proc, elem).decode()
+
+    def set_clock(self, now_ms):
+        """ActorClock.currentTimeMillis() for the next windows (timer due dates)."""
+        self.L.zbo_set_clock(self.h, int(now_ms))
 
     def element_type(self, proc, elem):
         t, ev, r = C.c_int(), C.c_int(), C.c_int()

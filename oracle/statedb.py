@@ -44,7 +44,12 @@ CF = {"KEY": 1, "ELEMENT_INSTANCE_PARENT_CHILD": 6, "ELEMENT_INSTANCE_KEY": 7, "
       "ELEMENT_INSTANCE_CHILD_PARENT": 9, "VARIABLES": 10, "JOBS": 16, "JOB_STATES": 17, "EVENT_SCOPE": 37,
       "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY": 55, "JOB_ACTIVATABLE": 76, "MESSAGE_SUBSCRIPTION_BY_KEY": 27,
       "MESSAGE_STATS": 54, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY": 74, "PROCESS_SUBSCRIPTION_BY_KEY": 75,
-      "JOB_DEADLINES": 18}
+      "JOB_DEADLINES": 18, "TIMERS": 12, "TIMER_DUE_DATES": 13}
+# TimerInstance.java:25-43 (declaration order)
+TIMER_INSTANCE = [
+    ("handlerNodeId", "str", ""), ("processDefinitionKey", "long", 0), ("key", "long", 0),
+    ("elementInstanceKey", "long", 0), ("processInstanceKey", "long", 0), ("dueDate", "long", 0),
+    ("repetitions", "int", 0), ("tenantId", "str", "<default>")]
 NIL = b"\xff"
 PI_INTENT = {1: "SEQUENCE_FLOW_TAKEN", 2: "ELEMENT_ACTIVATING", 3: "ELEMENT_ACTIVATED", 4: "ELEMENT_COMPLETING",
              5: "ELEMENT_COMPLETED", 6: "ELEMENT_TERMINATING", 7: "ELEMENT_TERMINATED"}
@@ -166,6 +171,15 @@ def encode_rows(rows, processes, string_value):
             out.append((CF[name], prefix + dblong(int(parts[1])) + dbstr("<default>") + dbstr(parts[2]), val))
         elif name == "MESSAGE_STATS":  # DbMessageState.java:165-175
             out.append((CF[name], prefix + dbstr("deadline_message_count"), dblong(int(parts[2]))))
+        elif name == "TIMERS":  # DbTimerInstanceState: [elementInstanceKey, timerKey] -> TimerInstance
+            f = fields(parts[3])
+            val = LS.write_object(TIMER_INSTANCE, dict(
+                handlerNodeId=f["handlerNodeId"], processDefinitionKey=int(f["processDefinitionKey"]), key=int(f["key"]),
+                elementInstanceKey=int(f["elementInstanceKey"]), processInstanceKey=int(f["processInstanceKey"]),
+                dueDate=int(f["dueDate"]), repetitions=int(f["repetitions"]), tenantId=f["tenantId"]))
+            out.append((CF[name], prefix + dblong(int(parts[1])) + dblong(int(parts[2])), val))
+        elif name == "TIMER_DUE_DATES":  # [dueDate, [elementInstanceKey, timerKey]] -> DbNil
+            out.append((CF[name], prefix + dblong(int(parts[1])) + dblong(int(parts[2])) + dblong(int(parts[3])), NIL))
         elif name == "JOB_DEADLINES":  # DbJobState.java:100-102: [deadline, jobKey] -> DbNil
             out.append((CF[name], prefix + dblong(int(parts[1])) + dblong(int(parts[2])), NIL))
         elif name == "JOB_ACTIVATABLE":

@@ -332,6 +332,7 @@ struct OEl {
   std::string job_type;
   int retries = 3;
   std::string msg_name, corr_var;  // message catch event (MessageTransformer.java:30-60)
+  int64_t timer_ms = -1;           // timer catch event: the static timeDuration in ms (TimerTransformer)
   int scope = 0;                   // flow scope element (ExecutableFlowElement.getFlowScope): 0 = process
   int start = -1;                  // process / sub-process: getNoneStartEvent
 };
@@ -349,6 +350,39 @@ struct OProc {
 // pushed with addFirst, so sequence flows are connected in reverse document order
 // (SequenceFlowTransformer.connectWithFlowNodes), which fixes getOutgoing() order.
 using MessageDefs = std::unordered_map<std::string, std::pair<std::string, std::string>>;  // id -> (name, corr var)
+
+// Interval.parse (bpmn-model/.../util/time/Interval.java) for static durations: "P[nD][T[nH][nM][n[.f]S]]"
+// -- days are 24 h in UTC, so the due date is now + a fixed number of ms.  Years / months / weeks,
+// negative parts and expressions (`=`) are outside the subset: -1.
+static int64_t parse_duration_ms(std::string t) {
+  size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+  if (a == std::string::npos) return -1;
+  t = t.substr(a, b - a + 1);
+  if (t.size() < 3 || t[0] != 'P') return -1;
+  int64_t ms = 0;
+  bool time = false, any = false;
+  size_t i = 1;
+  while (i < t.size()) {
+    if (t[i] == 'T') { if (time) return -1; time = true; ++i; continue; }
+    int64_t whole = 0, frac = 0, fdig = 0;
+    size_t s = i;
+    while (i < t.size() && isdigit((unsigned char)t[i])) { whole = whole * 10 + (t[i] - '0'); if (whole > (1LL << 40)) return -1; ++i; }
+    if (i < t.size() && t[i] == '.') {
+      ++i;
+      while (i < t.size() && isdigit((unsigned char)t[i])) { if (fdig < 3) { frac = frac * 10 + (t[i] - '0'); ++fdig; } ++i; }
+      while (fdig < 3) { frac *= 10; ++fdig; }
+    }
+    if (i == s || i >= t.size()) return -1;
+    const char u = t[i++];
+    any = true;
+    if (!time && u == 'D' && !frac) ms += whole * 86400000LL;
+    else if (time && u == 'H' && !frac) ms += whole * 3600000LL;
+    else if (time && u == 'M' && !frac) ms += whole * 60000LL;
+    else if (time && u == 'S') ms += whole * 1000LL + frac;
+    else return -1;
+  }
+  return any ? ms : -1;
+}
 
 static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, std::string& err) {
   P.bpmn_id = proc.attr("id");
@@ -410,6 +444,21 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
         err = "io mappings / task headers outside the supported subset";
         return false;
       }
+    } else if (n == "intermediateCatchEvent" && k->child("timerEventDefinition")) {
+      // CatchEventTransformer.transformTimerEventDefinition: timeDuration (a static ISO-8601
+      // duration, Interval.parse) only; timeDate / timeCycle / expressions outside the subset
+      e.type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
+      const XNode* ted = k->child("timerEventDefinition");
+      const XNode* td = ted->child("timeDuration");
+      if (!td || k->child("messageEventDefinition") || k->child("signalEventDefinition")) {
+        err = "timer catch event outside the supported subset (timeDuration only)";
+        return false;
+      }
+      e.timer_ms = parse_duration_ms(td->text);
+      if (e.timer_ms < 0 || e.timer_ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return false; }
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+      e.event = ZBHIP_EV_TIMER;
     } else if (n == "intermediateCatchEvent") {
       // CatchEventTransformer.transformMessageEventDefinition (transformer/CatchEventTransformer.java:88-100)
       e.type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
@@ -750,7 +799,7 @@ class Oracle {
     // events go into the same name dictionary (the product's zbhip_deploy interns in this order)
     bool has_msg = false;
     for (auto& e : P.els)
-      if (e.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+      if (e.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && e.event == ZBHIP_EV_MESSAGE) {
         intern(e.msg_name);
         intern(e.corr_var);
         has_msg = true;
@@ -829,6 +878,13 @@ class Oracle {
         rec.m = command_value(c.kind, m, x.source_partition);
         fill_msg(rec, rec.m);
         rec.slot = c.kind == ZBHIP_CMD_MSG_SUB_CREATE || c.kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
+      } else if (c.kind == ZBHIP_CMD_TIMER_TRIGGER) {
+        rec.doc = Doc{0, 0};
+        rec.r.aux = (int64_t)((uint64_t)c.doc_begin | ((uint64_t)c.pad << 32));  // the command's dueDate
+        rec.r.value_type = ZBHIP_VT_TIMER;
+        rec.r.intent = ZBHIP_TIMER_TRIGGER;
+        rec.r.key = -1;
+        rec.job_ord = (int32_t)c.ref;
       } else {
         rec.r.value_type = ZBHIP_VT_JOB;
         rec.r.intent = ZBHIP_JOB_COMPLETE;
@@ -957,6 +1013,14 @@ class Oracle {
   std::map<std::pair<int64_t, int>, VarRow> vars_;              // VARIABLES (scope, name id)
   std::set<int64_t> event_scope_;                               // EVENT_SCOPE (accepting, not interrupted)
   std::map<std::pair<int64_t, int64_t>, EventTrigger> triggers_;// EVENT_TRIGGER
+  struct TimerRow {  // TimerInstance (state/instance/TimerInstance.java:23-44)
+    PiValue pi;      // process, handler element, process instance key
+    int64_t dueDate = 0;
+  };
+  std::map<std::pair<int64_t, int64_t>, TimerRow> timers_;     // TIMERS [elementInstanceKey, timerKey]
+ public:
+  int64_t now_ms = 0;  // ActorClock.currentTimeMillis() of the window's processing (zbo_set_clock)
+ private:
   std::map<int64_t, JobRow> jobs_;                              // JOBS (+ JOB_STATES = ACTIVATABLE)
   std::set<std::tuple<std::string, std::string, int64_t>> activatable_;  // JOB_ACTIVATABLE
 
@@ -1121,6 +1185,8 @@ class Oracle {
       create_process_instance(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_JOB)
       complete_job(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_TIMER && cmd.r.intent == ZBHIP_TIMER_TRIGGER)
+      trigger_timer(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE)
       bpmn_process_record(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_MESSAGE && cmd.r.intent == ZBHIP_MSG_PUBLISH)
@@ -1177,6 +1243,64 @@ class Oracle {
   static int partition_of_key(int64_t key) { return (int)(key >> 51); }  // Protocol.decodePartitionId
 
   // CatchEventBehavior.subscribeToEvents -> subscribeToMessageEvent (processing/common/CatchEventBehavior.java:111-125,248-283)
+  // CatchEventBehavior.subscribeToTimerEvent (processing/common/CatchEventBehavior.java:303-330):
+  // dueDate = now + duration, TIMER:CREATED (+key); TimerCreatedApplier stores the TimerInstance
+  void subscribe_to_timer(const OEl& el, int64_t key, const PiValue& v) {
+    const int64_t due = now_ms + el.timer_ms;
+    const int64_t tk = next_key();
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_TIMER, ZBHIP_TIMER_CREATED, tk);
+    rec.r.process_idx = v.proc;
+    rec.r.element_idx = v.elem;
+    rec.r.scope_key = key;
+    rec.r.process_instance_key = v.piKey;
+    rec.r.aux = due;
+    TimerRow t;
+    t.pi = v;
+    t.dueDate = due;
+    timers_[{key, tk}] = t;
+  }
+
+  // TriggerTimerProcessor.processRecord (processing/timer/TriggerTimerProcessor.java:81-114) for a
+  // timer of an intermediate catch event: TIMER:TRIGGERED (the command's key and value), then
+  // EventHandle.activateElement (EventHandle.java:104-131): PROCESS_EVENT:TRIGGERING (+key, no
+  // variables) and COMPLETE_ELEMENT for the catch event
+  void trigger_timer(ORecord& cmd) {
+    cmd.r.key = resolve(cmd.instance, (uint32_t)cmd.job_ord);
+    const int64_t tk = cmd.r.key;
+    auto it = timers_.begin();
+    for (; it != timers_.end(); ++it)
+      if (it->first.second == tk) break;
+    if (it == timers_.end()) {
+      reject(cmd, ZBHIP_REJ_NOT_FOUND,
+             "Expected to trigger timer with key '" + std::to_string(tk) + "', but no such timer was found");
+      return;
+    }
+    const int64_t eik = it->first.first;
+    const TimerRow t = it->second;
+    auto eit = ei_.find(eik);
+    if (eit == ei_.end() || eit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED || !event_scope_.count(eik)) {
+      reject(cmd, ZBHIP_REJ_INVALID_STATE,
+             "Expected to trigger a timer with key '" + std::to_string(tk) + "', but the timer is not active anymore");
+      return;
+    }
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_TIMER, ZBHIP_TIMER_TRIGGERED, tk);
+    rec.r.process_idx = t.pi.proc;
+    rec.r.element_idx = t.pi.elem;
+    rec.r.scope_key = eik;
+    rec.r.process_instance_key = t.pi.piKey;
+    rec.r.aux = t.dueDate;
+    timers_.erase(it);  // TimerTriggeredApplier
+    const int64_t eventKey = next_key();
+    ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
+    pe.r.process_idx = t.pi.proc;
+    pe.r.element_idx = t.pi.elem;
+    pe.r.scope_key = eik;
+    pe.r.process_instance_key = t.pi.piKey;
+    pe.r.aux = -1;
+    triggers_[{eik, eventKey}] = EventTrigger{t.pi.elem, t.pi.proc, Doc{0, 0}, t.pi.piKey};
+    pi_command(eik, ZBHIP_PI_COMPLETE_ELEMENT, eit->second.value);
+  }
+
   void subscribe_to_message(const OEl& el, int64_t key, const PiValue& v) {
     // evaluateCorrelationKey (:155-178) -> ExpressionProcessor.evaluateMessageCorrelationKeyExpression
     // (processing/common/ExpressionProcessor.java:309-337): STRING or NUMBER, else incident
@@ -1660,7 +1784,8 @@ class Oracle {
       case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT:
         // IntermediateCatchEventProcessor.DefaultIntermediateCatchEventBehavior.onActivate
         // (processing/bpmn/event/IntermediateCatchEventProcessor.java): subscribeToEvents, then ACTIVATED
-        subscribe_to_message(el, key, v);
+        if (el.event == ZBHIP_EV_TIMER) subscribe_to_timer(el, key, v);
+        else subscribe_to_message(el, key, v);
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         break;
       case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (processing/bpmn/gateway/ParallelGatewayProcessor.java:34-50)
@@ -1704,6 +1829,8 @@ class Oracle {
         auto pit = pms_.lower_bound({key, INT32_MIN});
         if (pit != pms_.end() && pit->first.first == key)
           throw Unsupported{"unsubscribe (PROCESS_MESSAGE_SUBSCRIPTION:DELETING)"};
+        auto tit = timers_.lower_bound({key, INT64_MIN});  // unsubscribeFromTimerEvents: TIMER:CANCELED
+        if (tit != timers_.end() && tit->first.first == key) throw Unsupported{"unsubscribe (TIMER:CANCEL)"};
         complete_and_take(el, key, v, true);
         break;
       }
@@ -1983,6 +2110,18 @@ std::string Oracle::dump_state() const {
              t.vars.count);
     rows.push_back(buf);
   }
+  for (auto& [k, t] : timers_) {
+    const OProc& p = procs[t.pi.proc];
+    snprintf(buf, sizeof buf,
+             "TIMERS|%lld|%lld|handlerNodeId=%s,processDefinitionKey=%lld,key=%lld,elementInstanceKey=%lld,"
+             "processInstanceKey=%lld,dueDate=%lld,repetitions=1,tenantId=<default>",
+             (long long)k.first, (long long)k.second, p.els[t.pi.elem].id.c_str(), (long long)p.def_key,
+             (long long)k.second, (long long)k.first, (long long)t.pi.piKey, (long long)t.dueDate);
+    rows.push_back(buf);
+    snprintf(buf, sizeof buf, "TIMER_DUE_DATES|%lld|%lld|%lld", (long long)t.dueDate, (long long)k.first,
+             (long long)k.second);
+    rows.push_back(buf);
+  }
   for (auto& [k, j] : jobs_) {
     const OProc& p = procs[j.pi.proc];
     snprintf(buf, sizeof buf,
@@ -2162,6 +2301,7 @@ int zbo_reason(void* o, size_t idx, char* buf, size_t cap) {
   return (int)O->out[idx].reason.size();
 }
 void zbo_clear_records(void* o) { static_cast<Oracle*>(o)->out.clear(); }
+void zbo_set_clock(void* o, int64_t now_ms) { static_cast<Oracle*>(o)->now_ms = now_ms; }
 int64_t zbo_resolve(void* o, uint32_t instance, uint32_t ord) { return static_cast<Oracle*>(o)->resolve(instance, ord); }
 
 size_t zbo_state(void* o, char* buf, size_t cap) {

@@ -81,7 +81,8 @@ REASONS = [("Expected to be able to activate parallel gateway", 1),
            ("Expected flow scope instance with key", 2), ("Expected flow scope instance to be in state", 3),
            ("Expected element instance with key", 4), ("Expected element instance to be in state", 5),
            ("Expected to complete job with key", 6), ("Expected to open a new message subscription", 7),
-           ("Expected to correlate subscription for element", 12)]
+           ("Expected to correlate subscription for element", 12), ("Expected to trigger timer with key", 13),
+           ("Expected to trigger a timer with key", 14)]
 
 
 def with_reason_codes(recs, orc):

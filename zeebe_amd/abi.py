@@ -17,6 +17,7 @@ VT_PROCESS_MESSAGE_SUBSCRIPTION = 12
 VT_VARIABLE = 17
 VT_PROCESS_INSTANCE_CREATION = 19
 VT_PROCESS_EVENT = 24
+VT_TIMER = 15
 
 REJ_INVALID_ARGUMENT, REJ_NOT_FOUND, REJ_ALREADY_EXISTS, REJ_INVALID_STATE = 0, 1, 2, 3
 REJ_PROCESSING_ERROR, REJ_NONE = 4, 255
@@ -33,6 +34,8 @@ JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED = 0, 1, 2
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
 PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
 PIC_INTENTS = {0: "CREATE", 1: "CREATED"}
+TIMER_INTENTS = {0: "CREATED", 1: "TRIGGER", 2: "TRIGGERED", 3: "CANCEL", 4: "CANCELED"}
+TIMER_CREATED, TIMER_TRIGGER, TIMER_TRIGGERED = 0, 1, 2
 # MessageIntent / MessageSubscriptionIntent / ProcessMessageSubscriptionIntent
 MSG_INTENTS = {0: "PUBLISH", 1: "PUBLISHED", 2: "EXPIRE", 3: "EXPIRED"}
 MS_INTENTS = {0: "CREATE", 1: "CREATED", 2: "CORRELATE", 3: "CORRELATED", 4: "REJECT", 5: "REJECTED",
@@ -44,7 +47,7 @@ MS_CREATE, MS_CREATED, MS_CORRELATE, MS_CORRELATED, MS_CORRELATING = 0, 1, 2, 3,
 PMS_CREATING, PMS_CREATE, PMS_CREATED, PMS_CORRELATE, PMS_CORRELATED = 0, 1, 2, 3, 4
 VALUE_TYPES = {0: "JOB", 5: "PROCESS_INSTANCE", 10: "MESSAGE", 11: "MESSAGE_SUBSCRIPTION",
                12: "PROCESS_MESSAGE_SUBSCRIPTION", 17: "VARIABLE", 19: "PROCESS_INSTANCE_CREATION",
-               24: "PROCESS_EVENT"}
+               24: "PROCESS_EVENT", 15: "TIMER"}
 RECORD_TYPES = {0: "EVENT", 1: "COMMAND", 2: "COMMAND_REJECTION"}
 REJECTION_TYPES = {0: "INVALID_ARGUMENT", 1: "NOT_FOUND", 2: "ALREADY_EXISTS", 3: "INVALID_STATE",
                    4: "PROCESSING_ERROR", 255: "NULL_VAL"}
@@ -60,7 +63,8 @@ EVENT_TYPES = ["UNSPECIFIED", "CONDITIONAL", "ERROR", "ESCALATION", "LINK", "MES
 def intent_name(value_type, intent):
     table = {VT_PROCESS_INSTANCE: PI_INTENTS, VT_JOB: JOB_INTENTS, VT_VARIABLE: VAR_INTENTS,
              VT_PROCESS_EVENT: PE_INTENTS, VT_PROCESS_INSTANCE_CREATION: PIC_INTENTS, VT_MESSAGE: MSG_INTENTS,
-             VT_MESSAGE_SUBSCRIPTION: MS_INTENTS, VT_PROCESS_MESSAGE_SUBSCRIPTION: PMS_INTENTS}.get(value_type, {})
+             VT_MESSAGE_SUBSCRIPTION: MS_INTENTS, VT_PROCESS_MESSAGE_SUBSCRIPTION: PMS_INTENTS,
+             VT_TIMER: TIMER_INTENTS}.get(value_type, {})
     return table.get(intent, str(intent))
 
 
@@ -68,6 +72,7 @@ CMD_CREATE = 1
 CMD_JOB_COMPLETE = 2
 CMD_PUBLISH = 3
 CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE = 4, 5, 6, 7
+CMD_TIMER_TRIGGER = 8  # ref = timer key ordinal, doc_begin | pad << 32 = the timer's dueDate
 XPART_KINDS = (CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE)
 DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR = 0, 1, 2, 3, 4, 5
 NO_STRING = 0xFFFFFFFF

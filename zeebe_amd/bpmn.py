@@ -26,6 +26,7 @@ class _Node:
         self.source = None
         self.target = None
         self.message = None  # (message id, name, correlation key expression) of a message catch event
+        self.timer = None    # timeDuration of a timer catch event
 
 
 class ProcessBuilder:
@@ -137,6 +138,11 @@ class ProcessBuilder:
         self._pending_flow = None
         return self
 
+    def timerWithDuration(self, duration):
+        """IntermediateCatchEventBuilder.timerWithDuration: <timerEventDefinition><timeDuration>."""
+        self.current.timer = duration
+        return self
+
     def exclusiveGateway(self, id_=None):
         self._add_node("exclusiveGateway", id_)
         return self
@@ -219,6 +225,10 @@ class ProcessBuilder:
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
                                '</intermediateCatchEvent>' % (ind, quoteattr(c.id), quoteattr(c.id + "_med"),
                                                               quoteattr(c.message[0])))
+                elif c.kind == "intermediateCatchEvent" and c.timer:
+                    out.append('%s<intermediateCatchEvent id=%s><timerEventDefinition id=%s><timeDuration>%s'
+                               '</timeDuration></timerEventDefinition></intermediateCatchEvent>'
+                               % (ind, quoteattr(c.id), quoteattr(c.id + "_ted"), escape(c.timer)))
                 elif c.kind == "exclusiveGateway" and c.default:
                     out.append("%s<exclusiveGateway id=%s default=%s/>" % (ind, quoteattr(c.id), quoteattr(c.default.id)))
                 elif c.kind == "subProcess":

@@ -343,6 +343,50 @@ struct Compiled {
   }
 };
 
+// Interval.parse (bpmn-model/.../util/time/Interval.java) of a static duration
+// "P[nD][T[nH][nM][n[.f]S]]": days are 24 h in UTC, so due = now + a fixed number of ms.  Years,
+// months, weeks, negative parts and `=` expressions: -1 (outside the subset).
+static int64_t duration_ms(const std::string& text) {
+  size_t a = text.find_first_not_of(" \t\r\n"), b = text.find_last_not_of(" \t\r\n");
+  if (a == std::string::npos) return -1;
+  const std::string t = text.substr(a, b - a + 1);
+  if (t.size() < 3 || t[0] != 'P') return -1;
+  int64_t ms = 0;
+  bool in_time = false, any = false;
+  for (size_t i = 1; i < t.size();) {
+    if (t[i] == 'T') {
+      if (in_time) return -1;
+      in_time = true;
+      ++i;
+      continue;
+    }
+    const size_t s = i;
+    int64_t whole = 0, frac = 0;
+    int digits = 0;
+    while (i < t.size() && isdigit((unsigned char)t[i])) {
+      whole = whole * 10 + (t[i++] - '0');
+      if (whole > (1LL << 40)) return -1;
+    }
+    if (i < t.size() && t[i] == '.') {
+      ++i;
+      while (i < t.size() && isdigit((unsigned char)t[i])) {
+        if (digits < 3) { frac = frac * 10 + (t[i] - '0'); ++digits; }
+        ++i;
+      }
+      for (; digits < 3; ++digits) frac *= 10;
+    }
+    if (i == s || i >= t.size()) return -1;
+    const char u = t[i++];
+    any = true;
+    if (!in_time && u == 'D' && !frac) ms += whole * 86400000LL;
+    else if (in_time && u == 'H' && !frac) ms += whole * 3600000LL;
+    else if (in_time && u == 'M' && !frac) ms += whole * 60000LL;
+    else if (in_time && u == 'S') ms += whole * 1000LL + frac;
+    else return -1;
+  }
+  return any ? ms : -1;
+}
+
 static zbhip_element blank(uint8_t type, uint16_t id) {
   zbhip_element e{};
   e.element_type = type;
@@ -351,6 +395,7 @@ static zbhip_element blank(uint8_t type, uint16_t id) {
   e.job_type = e.join_slot = ZBHIP_NONE16;
   e.flow_scope = 0;
   e.start_event = ZBHIP_NONE16;
+  e.duration_ms = 0;
   e.message_name = e.correlation_var = ZBHIP_NONE16;
   e.job_retries = 0;
   e.id = id;
@@ -469,7 +514,21 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         if (const Elem* ext = c.first("extensionElements"))
           if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
       }
-      if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+      if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && c.first("timerEventDefinition")) {
+        // CatchEventTransformer.transformTimerEventDefinition: a static timeDuration only
+        const Elem* ted = c.first("timerEventDefinition");
+        const Elem* td = ted->first("timeDuration");
+        if (!td || c.first("messageEventDefinition") || c.first("signalEventDefinition")) {
+          err = "timer catch event outside the supported subset (timeDuration only)";
+          return ZBHIP_EUNSUPP;
+        }
+        const int64_t ms = duration_ms(td->text);
+        if (ms < 0 || ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return ZBHIP_EUNSUPP; }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        e.event_type = ZBHIP_EV_TIMER;
+        e.duration_ms = (uint32_t)ms;
+      } else if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
         // CatchEventTransformer.transformMessageEventDefinition: message catch events only
         const Elem* med = c.first("messageEventDefinition");
         for (auto& d : c.children)

@@ -175,6 +175,10 @@ struct Lane {
   const StepParams* sp;
   const uint32_t* prog;     // LDS program arena (mid-batch instance loads)
   uint16_t s_first_ord;
+  // ---- the instance's timer (K::S, processes with timer catch events; DevState.tmr) ----
+  bool has_tmr;
+  uint32_t tm_x, tm_y;      // catch element | timer ordinal << 16; element-instance ordinal | live << 31
+  long long tm_due;
 };
 constexpr uint32_t kNoInst = 0xFFFFFFFFu;
 static_assert(kVars == 4 && kJoinWords == 4, "scalarised tables");
@@ -1077,6 +1081,33 @@ __device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint3
   emit_msg(L, C_MSG_EXPIRED, sref(L, msg), -1, -1, -1, slot, nb_msg, 0, 0, kNoElem);
 }
 
+// ---- TIMER:TRIGGER (K::S) --------------------------------------------------------------------
+// TriggerTimerProcessor.processRecord (processing/timer/TriggerTimerProcessor.java:81-114) for the
+// instance's timer: NOT_FOUND / INVALID_STATE rejections, TIMER:TRIGGERED (the command's key),
+// TimerTriggeredApplier (the row removed), then EventHandle.activateElement (EventHandle.java:104-131):
+// PROCESS_EVENT:TRIGGERING (+key, no variables) and COMPLETE_ELEMENT for the catch event
+template <class K>
+__device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord) {
+  if (L.proc == NONE || !L.pi_live || !(L.tm_y >> 31) || (L.tm_x >> 16) != tord) {
+    emit(L, kRejectBit | C_TIMER_TRIGGER, tord, NONE, NONE, ZBHIP_REASON_TIMER_NOT_FOUND);
+    return;
+  }
+  const uint32_t eord = L.tm_y & 0xFFFF, elem = L.tm_x & 0xFFF;
+  const int t = tbl_find(L, eord);  // canTriggerElement: the catch event is ACTIVATED, its scope accepting
+  if (t < 0 || ((tget(L, t).y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED) {
+    emit(L, kRejectBit | C_TIMER_TRIGGER, tord, NONE, NONE, ZBHIP_REASON_TIMER_NOT_ACTIVE);
+    return;
+  }
+  emit(L, C_TIMER_TRIGGERED, tord, eord, elem);
+  L.tm_x = L.tm_y = 0;
+  L.tm_due = 0;
+  const uint32_t pe = new_key(L);
+  emit(L, C_PE_TRIGGERING, pe, eord, elem);
+  L.trig_key = (uint16_t)eord;  // ProcessEventTriggeringApplier: EVENT_TRIGGER row (no variables)
+  const uint32_t c = scope_of<K>(elem_of(L, elem));
+  follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, eord, scope_key(L, c), elem, true, c == 0, eord);
+}
+
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
 template <class K>
 __device__ __forceinline__ void reject_pi(Lane<K>& L, bool complete, uint32_t elem, uint32_t key, uint32_t aux,
@@ -1189,6 +1220,18 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
           if (L.fail) return;
           emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
           tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
+        } else if constexpr (K::S) {
+          // timer: CatchEventBehavior.subscribeToTimerEvent (CatchEventBehavior.java:303-330):
+          // dueDate = now + duration, TIMER:CREATED (+key), TimerCreatedApplier; one timer per
+          // instance on the device (a second one falls back)
+          if (((w.x >> 8) & 0xFF) != ZBHIP_EV_TIMER || !L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
+          const uint32_t tk = new_key(L);
+          L.tm_x = elem | (tk << 16);
+          L.tm_y = key | (1u << 31);
+          L.tm_due = L.sp->now_ms + (long long)w.z;
+          emit(L, C_TIMER_CREATED, tk, key, elem);
+          emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
+          tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
         } else {
           set_fail(L, FB_UNSUPPORTED);
         }
@@ -1262,6 +1305,10 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       set_fail(L, FB_UNSUPPORTED);
       return;
     }
+  } else if (K::S && type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+    // IntermediateCatchEventProcessor.onComplete -> unsubscribeFromEvents: a timer still open here
+    // would be canceled (TIMER:CANCELED, outside the subset)
+    if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) { set_fail(L, FB_UNSUPPORTED); return; }
   } else if (type != ZBHIP_EL_START_EVENT && !ZBHIP_IS_JOB_WORKER(type) && !pass_through(type) &&
              !(K::S && type == ZBHIP_EL_SUB_PROCESS)) {
     // SubProcessProcessor.onComplete (:68-82): no output mappings or subscriptions in the subset
@@ -1752,6 +1799,11 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.vx0 = L.vx1 = L.vx2 = L.vx3 = 0xFFFFFFFFu;
   L.vy0 = L.vy1 = L.vy2 = L.vy3 = 0;
   L.vv0 = L.vv1 = L.vv2 = L.vv3 = 0;
+  if constexpr (K::S) {
+    L.has_tmr = false;
+    L.tm_x = L.tm_y = 0;
+    L.tm_due = 0;
+  }
   bool slot_kind = false;
   if constexpr (K::M) {
     L.prog = prog;
@@ -1861,6 +1913,16 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if (!L.fail && L.proc != NONE) {
     L.pb = prog + prog[1 + L.proc];
     L.has_join = K::J && (L.pb[1] & 0xFFFF) != 0;
+    if constexpr (K::S) {
+      L.has_tmr = (L.pb[5] >> 16) & 1;
+      if (L.has_tmr && kind != ZBHIP_CMD_CREATE) {
+        const uint4 tr = P.st.tmr[inst];
+        L.tm_x = tr.x;
+        L.tm_y = tr.y;
+        L.tm_due = (long long)(((unsigned long long)tr.w << 32) | tr.z);
+        vm_drain();
+      }
+    }
     if (L.has_join && kind != ZBHIP_CMD_CREATE) {
       L.jw0 = P.st.join[inst];
       L.jw1 = P.st.join[(size_t)N + inst];
@@ -1937,6 +1999,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
         follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, task_key, fsk, task_elem, true, true, task_key);
       }
     }
+  } else if (!L.fail && kind == ZBHIP_CMD_TIMER_TRIGGER) {
+    if constexpr (K::S) trigger_timer(L, ref);
+    else set_fail(L, FB_UNSUPPORTED);
   } else if (!L.fail && kind == CMD_FOLLOWUP) {
     // written to the log past the batch limit: the command is this batch's initial command
     enqueue(L, doc_begin);
@@ -2018,6 +2083,13 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if constexpr (K::M) {
     if (ok && winst != kNoInst) P.st.pms[winst] = make_uint4(L.pi_live ? L.pm_x : 0u, L.pi_live ? L.pm_y : 0u,
                                                              L.pi_live ? L.pm_z : 0u, 0u);
+  }
+  if constexpr (K::S) {
+    if (ok && winst != kNoInst && L.has_tmr) {
+      const bool keep = L.pi_live && (L.tm_y >> 31);
+      const unsigned long long d = (unsigned long long)L.tm_due;
+      P.st.tmr[winst] = keep ? make_uint4(L.tm_x, L.tm_y, (uint32_t)d, (uint32_t)(d >> 32)) : make_uint4(0, 0, 0, 0);
+    }
   }
   if (ok && winst != kNoInst) {
     // a completed instance frees its slot (rows removed with the instance) but keeps next_ord,

@@ -292,6 +292,11 @@ int zbhip_serializer_rejection_reason(zbhip_serializer* s, const zbhip_record* r
     case ZBHIP_REASON_MS_CORR_NOT_FOUND:
       return snprintf(buf, cap, "Expected to correlate subscription for element with key '%lld' and message name '%s', "
                       "but no such message subscription exists", (long long)r->scope_key, mname);
+    case ZBHIP_REASON_TIMER_NOT_FOUND:  // TriggerTimerProcessor.java:40-41
+      return snprintf(buf, cap, "Expected to trigger timer with key '%lld', but no such timer was found", (long long)r->key);
+    case ZBHIP_REASON_TIMER_NOT_ACTIVE:  // TriggerTimerProcessor.java:42-43
+      return snprintf(buf, cap, "Expected to trigger a timer with key '%lld', but the timer is not active anymore",
+                      (long long)r->key);
     default:
       if (cap) buf[0] = 0;
       return 0;
@@ -429,6 +434,18 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         key(value, "variables"); mp_bin(value, src_doc);
         key(value, "processDefinitionKey"); mp_int(value, P->def_key);
         key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+        key(value, "tenantId"); key(value, kTenant);
+        break;
+      case ZBHIP_VT_TIMER:
+        // TimerRecord.java:24-40 (CREATED / TRIGGERED: CatchEventBehavior.java:311-319; a rejected
+        // TIMER:TRIGGER: the command's value as far as the window holds it -- its key and dueDate)
+        mp_map(value, 7);
+        key(value, "elementInstanceKey"); mp_int(value, r.scope_key);
+        key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+        key(value, "dueDate"); mp_int(value, r.aux);
+        key(value, "targetElementId"); mp_str(value, E ? E->id : std::string());
+        key(value, "repetitions"); mp_int(value, 1);
+        key(value, "processDefinitionKey"); mp_int(value, P ? P->def_key : -1);
         key(value, "tenantId"); key(value, kTenant);
         break;
       case ZBHIP_VT_PROCESS_INSTANCE_CREATION:
@@ -702,6 +719,23 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     key(v, "elementId"); mp_str(v, f["elementId"]);
     key(v, "elementInstanceKey"); mp_int(v, ll(f["elementInstanceKey"]));
     key(v, "tenantId"); mp_str(v, f["tenantId"]);
+  } else if (cf == "TIMERS" && need(4)) {
+    ord = 12;  // DbTimerInstanceState: [elementInstanceKey, timerKey] -> TimerInstance (TimerInstance.java:36-43)
+    auto f = fields_of(p[3]);
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbl(k, ll(p[2]));
+    mp_map(v, 8);
+    key(v, "handlerNodeId"); mp_str(v, f["handlerNodeId"]);
+    key(v, "processDefinitionKey"); mp_int(v, ll(f["processDefinitionKey"]));
+    key(v, "key"); mp_int(v, ll(f["key"]));
+    key(v, "elementInstanceKey"); mp_int(v, ll(f["elementInstanceKey"]));
+    key(v, "processInstanceKey"); mp_int(v, ll(f["processInstanceKey"]));
+    key(v, "dueDate"); mp_int(v, ll(f["dueDate"]));
+    key(v, "repetitions"); mp_int(v, ll(f["repetitions"]));
+    key(v, "tenantId"); mp_str(v, f["tenantId"]);
+  } else if (cf == "TIMER_DUE_DATES" && need(4)) {
+    ord = 13;  // [dueDate, [elementInstanceKey, timerKey]] -> DbNil
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbl(k, ll(p[2])); dbl(k, ll(p[3]));
+    v.push_back((char)0xff);
   } else if (cf == "JOB_STATES" && need(3)) {
     ord = 17;
     cf_prefix(k, ord); dbl(k, ll(p[1]));
@@ -1051,6 +1085,26 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
       const int64_t k = K.dblong();
       if (!K.ok || !value()) return ZBHIP_EINVAL;
       snprintf(b, sizeof b, "JOB_STATES|%lld|%s", (long long)k, ms(v.get("jobState")).c_str());
+      out = b;
+      break;
+    }
+    case 12: {  // TIMERS [eik, timerKey] -> TimerInstance
+      const int64_t e = K.dblong(), t = K.dblong();
+      if (!K.ok || !value()) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b,
+               "TIMERS|%lld|%lld|handlerNodeId=%s,processDefinitionKey=%lld,key=%lld,elementInstanceKey=%lld,"
+               "processInstanceKey=%lld,dueDate=%lld,repetitions=%lld,tenantId=%s",
+               (long long)e, (long long)t, ms(v.get("handlerNodeId")).c_str(), (long long)mi(v.get("processDefinitionKey")),
+               (long long)mi(v.get("key")), (long long)mi(v.get("elementInstanceKey")),
+               (long long)mi(v.get("processInstanceKey")), (long long)mi(v.get("dueDate")),
+               (long long)mi(v.get("repetitions")), ms(v.get("tenantId")).c_str());
+      out = b;
+      break;
+    }
+    case 13: {  // TIMER_DUE_DATES [dueDate, eik, timerKey] -> DbNil
+      const int64_t d = K.dblong(), e = K.dblong(), t = K.dblong();
+      if (!K.ok) return ZBHIP_EINVAL;
+      snprintf(b, sizeof b, "TIMER_DUE_DATES|%lld|%lld|%lld", (long long)d, (long long)e, (long long)t);
       out = b;
       break;
     }

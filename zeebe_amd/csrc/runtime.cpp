@@ -71,6 +71,7 @@ struct Proc {
   uint16_t bpmn_id = 0;
   uint16_t bpmn_name = NONE;  // name id of the bpmnProcessId (processes with message catch events)
   bool has_msg = false;
+  bool has_timer = false;     // timer catch events (KScope, the instance timer row)
   std::vector<uint32_t> job_type_id;  // per element: id of its job type (service tasks), else ~0
   const std::string& id(uint32_t e) const { return strings[els[e].id]; }
 };
@@ -220,6 +221,8 @@ struct zbhip_handle {
 
   // key relabelling (DbKeyGenerator order)
   int64_t key_counter = 0;
+  int64_t clock_ms = 0;       // zbhip_set_clock: the clock of the next runs (timer due dates)
+  int64_t run_clock_ms = 0;   // the clock of the last run (drained TIMER:CREATED dueDates)
   bool relabel_ok = true;
   size_t fin_next = 0;             // the last run's key bookkeeping is done for commands < fin_next (advance)
   std::vector<uint32_t> ext_keys;  // keys the CPU engine generated for the window's fallback commands
@@ -406,6 +409,8 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
        dalloc(&h->d_region_total, h->regions_cap) == hipSuccess &&
        dalloc(&h->d_region_lanes, (size_t)h->regions_cap * 128) == hipSuccess &&
        dalloc(&h->d_region_off, h->regions_cap) == hipSuccess;
+  // timer rows (KScope timer catch events): one per instance
+  ok = ok && dalloc(&h->st.tmr, N) == hipSuccess;
   // message correlation state (config 5): PROCESS_SUBSCRIPTION rows per instance, correlation slots
   const size_t S = cfg->max_correlation_keys;
   h->st.n_slots = (uint32_t)S;
@@ -442,6 +447,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   h->rec_slots = cfg->max_commands;
   // every slot starts free (proc = 0xFFFF); counters zero
   if (hipMemsetAsync(h->st.hdr, 0xFF, N * sizeof(uint4), h->stream) != hipSuccess ||
+      hipMemsetAsync(h->st.tmr, 0, N * sizeof(uint4), h->stream) != hipSuccess ||
       hipMemsetAsync(h->st.join, 0, N * kJoinWords * sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_seen, 0, (N + S) * sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_ovf_count, 0, sizeof(uint32_t), h->stream) != hipSuccess ||
@@ -474,6 +480,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_region_off);
   (void)hipFree(h->d_stats);
   (void)hipFree(h->st.pms);
+  (void)hipFree(h->st.tmr);
   (void)hipFree(h->st.pi_key);
   (void)hipFree(h->st.slot_hdr);
   (void)hipFree(h->st.sub_a);
@@ -651,7 +658,7 @@ static int rebuild_program(zbhip_handle* h) {
     pb[2] = out_off;
     pb[3] = cond_off;
     pb[4] = code_off;
-    pb[5] = P.bpmn_name;  // name id of the bpmnProcessId (message records)
+    pb[5] = P.bpmn_name | (P.has_timer ? 1u << 16 : 0u);  // name id of the bpmnProcessId (message records)
     pb[6] = seg_off;
     pb[7] = create_template_word(P);
     // straight-line segment words (kernels.hip fast_command): a start event or service task with
@@ -691,6 +698,8 @@ static int rebuild_program(zbhip_handle* h) {
       if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW) w[2] = E.flow_target | ((uint32_t)E.condition << 16);
       else if (E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY) w[2] = E.default_flow | (0xFFFFu << 16);
       else if (ZBHIP_IS_JOB_WORKER(E.element_type)) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
+      else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && E.event_type == ZBHIP_EV_TIMER)
+        w[2] = E.duration_ms;
       else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
         w[2] = E.message_name | ((uint32_t)E.correlation_var << 16);  // name ids (zbhip_deploy)
       else if (E.element_type == ZBHIP_EL_SUB_PROCESS) w[2] = E.start_event | (join_mask[e] << 16);
@@ -763,7 +772,9 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       return ZBHIP_EINVAL;
   }
   for (auto& e : P.els)
-    if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+    if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && e.event_type == ZBHIP_EV_TIMER) {
+      P.has_timer = true;
+    } else if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
       if (!h->st.n_slots) return ZBHIP_EUNSUPP;  // the handle was opened without message state
       if (e.message_name >= P.strings.size() || e.correlation_var >= P.strings.size()) return ZBHIP_EINVAL;
       P.has_msg = true;
@@ -783,7 +794,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   // oracle's order): the name dictionary is replicated across partitions by deploy order
   if (P.has_msg) {
     for (auto& e : P.els) {
-      if (e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) continue;
+      if (e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || e.event_type != ZBHIP_EV_MESSAGE) continue;
       int mn = zbhip_intern(h, P.strings[e.message_name].c_str());
       int cv = zbhip_intern(h, P.strings[e.correlation_var].c_str());
       if (mn < 0 || cv < 0) return ZBHIP_ENOMEM;
@@ -810,7 +821,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       cls = 1;
     scopes |= e.element_type == ZBHIP_EL_SUB_PROCESS;
   }
-  if (scopes) cls = 4;
+  if (scopes || P.has_timer) cls = 4;  // timer catch events: KScope as well (the instance's timer row)
   if (P.has_msg) cls = 2;
   auto rank = [](int v) { return v == 3 ? 0 : v == 0 ? 1 : v == 1 ? 2 : v == 4 ? 3 : 4; };
   const int old_variant = h->variant;
@@ -933,6 +944,9 @@ static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t
       if (c.ref >= h->procs.size()) return ZBHIP_EINVAL;
     } else if (c.kind == ZBHIP_CMD_JOB_COMPLETE) {
       if (c.ref >= 0xFFF0) return ZBHIP_EINVAL;
+    } else if (c.kind == ZBHIP_CMD_TIMER_TRIGGER) {
+      if (c.ref >= 0xFFF0 || c.doc_count) return ZBHIP_EINVAL;  // doc_begin | pad << 32 = dueDate
+      continue;
     } else {
       return ZBHIP_EINVAL;
     }
@@ -1247,6 +1261,12 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
 // the whole window (undeclared fallback commands generated no keys)
 static int finalize(zbhip_handle* h) { return advance(h, ~(size_t)0, true); }
 
+int zbhip_set_clock(zbhip_handle* h, int64_t now_ms) {
+  if (!h) return ZBHIP_EINVAL;
+  h->clock_ms = now_ms;
+  return ZBHIP_OK;
+}
+
 int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (!h) return ZBHIP_EINVAL;
   if (h->ran) return ZBHIP_ESTATE;
@@ -1288,6 +1308,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.stats = h->d_stats;
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
   P.stamp = h->window_stamp;
+  P.now_ms = h->clock_ms;
+  h->run_clock_ms = h->clock_ms;
   P.tpl = (h->variant == 0 || h->variant == 1 || h->variant == 4) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
   if (h->msg()) {
     int rc = sync_strings(h);
@@ -1571,6 +1593,7 @@ static uint8_t rejection_type_of(uint32_t reason) {
     case ZBHIP_REASON_PMS_CREATE_NOT_FOUND:
     case ZBHIP_REASON_PMS_CORR_NOT_FOUND:
     case ZBHIP_REASON_MS_CORR_NOT_FOUND:
+    case ZBHIP_REASON_TIMER_NOT_FOUND:
       return ZBHIP_REJ_NOT_FOUND;
     default:
       return ZBHIP_REJ_INVALID_STATE;
@@ -1631,13 +1654,30 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.intent = ZBHIP_PIC_CREATED;
       r.record_type = ZBHIP_RT_EVENT;
       r.aux = doc;
+    } else if (c6 == C_TIMER_CREATED || c6 == C_TIMER_TRIGGERED || c6 == C_TIMER_TRIGGER) {
+      // TimerRecord: elementInstanceKey (scope_key), dueDate in aux -- CREATED: the run's clock plus
+      // the element's duration (CatchEventBehavior.java:310); TRIGGERED / a rejected TRIGGER: the
+      // command's TimerRecord (TriggerTimerProcessor.java:108: the TIMER:TRIGGER value)
+      r.value_type = ZBHIP_VT_TIMER;
+      r.intent = c6 == C_TIMER_CREATED ? ZBHIP_TIMER_CREATED : c6 == C_TIMER_TRIGGERED ? ZBHIP_TIMER_TRIGGERED
+                                                                                      : ZBHIP_TIMER_TRIGGER;
+      r.record_type = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
+      const int64_t cmd_due = (int64_t)((uint64_t)cm.doc_begin | ((uint64_t)cm.pad << 32));
+      const zbhip_element* E = proc != NONE && elem < h->procs[proc].els.size() ? &h->procs[proc].els[elem] : nullptr;
+      r.aux = c6 == C_TIMER_CREATED ? h->run_clock_ms + (E ? (int64_t)E->duration_ms : 0) : cmd_due;
     } else {
       return ZBHIP_EDEVICE;  // corrupt record
     }
     if (rej) {
       r.reason = fl & 0xF;
       r.reason_arg = fl >> 4;
-      if (r.value_type == ZBHIP_VT_JOB) {
+      if (r.value_type == ZBHIP_VT_TIMER) {  // the TIMER:TRIGGER command's value
+        r.rejection_type = rejection_type_of(r.reason);
+        r.process_idx = -1;
+        r.element_idx = -1;
+        r.scope_key = -1;
+        r.process_instance_key = -1;
+      } else if (r.value_type == ZBHIP_VT_JOB) {
         r.rejection_type = ZBHIP_REJ_NOT_FOUND;
         r.process_idx = -1;
         r.element_idx = -1;
@@ -1975,6 +2015,7 @@ struct InstRows {  // the SoA rows of one instance slot
   uint32_t join[kJoinWords];
   uint4 pms;
   bool has_pms;
+  uint4 tmr;  // the instance's timer row (DevState.tmr)
 };
 }  // namespace
 
@@ -2065,6 +2106,17 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
              h->names[m.x & 0xFFFF].c_str(), h->key_of(inst, m.y & 0xFFFF), (m.y >> 16) & 0xFF, R.vv[v]);
     sink(ctx, buf);
   }
+  if (R.tmr.y >> 31) {  // TIMERS [eik, timerKey] -> TimerInstance, TIMER_DUE_DATES [dueDate, eik, timerKey] (DbTimerInstanceState)
+    const long long eik = h->key_of(inst, R.tmr.y & 0xFFFF), tk = h->key_of(inst, R.tmr.x >> 16);
+    const long long due = (long long)(((unsigned long long)R.tmr.w << 32) | R.tmr.z);
+    snprintf(buf, sizeof buf,
+             "TIMERS|%lld|%lld|handlerNodeId=%s,processDefinitionKey=%lld,key=%lld,elementInstanceKey=%lld,"
+             "processInstanceKey=%lld,dueDate=%lld,repetitions=1,tenantId=<default>",
+             eik, tk, P.id(R.tmr.x & 0xFFF).c_str(), (long long)P.def_key, tk, eik, pik, due);
+    sink(ctx, buf);
+    snprintf(buf, sizeof buf, "TIMER_DUE_DATES|%lld|%lld|%lld", due, eik, tk);
+    sink(ctx, buf);
+  }
   if (R.has_pms && ((R.pms.x >> 12) & 3)) {  // PROCESS_SUBSCRIPTION_BY_KEY [eik, name] (DbProcessMessageSubscriptionState)
     const uint4 m = R.pms;
     const uint32_t el = m.x & 0xFFF;
@@ -2106,6 +2158,7 @@ static int gather_instance(zbhip_handle* h, uint32_t i, InstRows& R) {
     HIPCHK(hipMemcpy(&R.join[w], h->st.join + w * N + i, sizeof(uint32_t), hipMemcpyDeviceToHost));
   R.has_pms = h->st.n_slots != 0;
   if (R.has_pms) HIPCHK(hipMemcpy(&R.pms, h->st.pms + i, sizeof(uint4), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&R.tmr, h->st.tmr + i, sizeof(uint4), hipMemcpyDeviceToHost));
   return ZBHIP_OK;
 }
 
@@ -2118,6 +2171,7 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   std::vector<uint2> slots(N * kSlots), vm(N * kVars);
   std::vector<long long> vv(N * kVars);
   std::vector<uint32_t> join(N * kJoinWords);
+  std::vector<uint4> tmr(N);
   const size_t S = h->st.n_slots;
   std::vector<uint4> pms(S ? N : 0), sub_a(S * kSubs);
   std::vector<longlong2> sub_b(S * kSubs), sub_k(S * kSubs);
@@ -2133,6 +2187,7 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   HIPCHK(hipMemcpy(vm.data(), h->st.var_meta, N * kVars * sizeof(uint2), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(vv.data(), h->st.var_val, N * kVars * sizeof(long long), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(join.data(), h->st.join, N * kJoinWords * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(tmr.data(), h->st.tmr, N * sizeof(uint4), hipMemcpyDeviceToHost));
   char buf[768];
   snprintf(buf, sizeof buf, "KEY|latestKey|%lld", (long long)(((int64_t)h->cfg.partition_id << 51) + h->key_counter));
   sink(ctx, buf);
@@ -2149,6 +2204,7 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
     for (int k = 0; k < kJoinWords; ++k) R.join[k] = join[(size_t)k * N + i];
     R.has_pms = S != 0;
     if (S) R.pms = pms[i];
+    R.tmr = tmr[i];
     emit_instance(h, (uint32_t)i, R, sink, ctx);
   }
   // MESSAGE_SUBSCRIPTION_BY_KEY [eik, name] and MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY
@@ -2198,10 +2254,9 @@ int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n) 
     const uint32_t zero[kJoinWords] = {0, 0, 0, 0};
     for (int w = 0; w < kJoinWords; ++w)
       HIPCHK(hipMemcpy(h->st.join + (size_t)w * h->st.n + i, &zero[w], sizeof(uint32_t), hipMemcpyHostToDevice));
-    if (h->st.n_slots) {
-      const uint4 z = make_uint4(0, 0, 0, 0);
-      HIPCHK(hipMemcpy(h->st.pms + i, &z, sizeof z, hipMemcpyHostToDevice));
-    }
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    if (h->st.n_slots) HIPCHK(hipMemcpy(h->st.pms + i, &z, sizeof z, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->st.tmr + i, &z, sizeof z, hipMemcpyHostToDevice));
     if (i < h->inst_gen.size()) ++h->inst_gen[i];
     for (auto it = h->job_index.begin(); it != h->job_index.end();)
       it = it->second.first == i ? h->job_index.erase(it) : std::next(it);
@@ -2294,6 +2349,10 @@ struct ImpVar {
   std::string name;
   uint32_t type = 0;
 };
+struct ImpTimer {
+  int64_t eik = 0, key = 0, due = 0;
+  std::string handler;
+};
 struct ImpPms {
   int64_t eik = 0, key = 0;
   std::string name, corr, elem_id;
@@ -2318,6 +2377,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   std::map<int64_t, std::pair<int64_t, std::string>> job_act;  // ACTIVATED jobs: deadline, worker
   std::set<int64_t> job_activated_state;
   std::vector<ImpPms> pms;
+  std::vector<ImpTimer> timers;
   int64_t latest = -1;
   bool stats_row = false;
   for (const std::string& row : split_row(std::string(text, len), '\n')) {
@@ -2364,6 +2424,10 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       m.elem_id = f["elementId"];
       m.intr = (uint32_t)to_ll(f["interrupting"]);
       pms.push_back(m);
+    } else if (cf == "TIMERS" && p.size() >= 4) {
+      auto f = row_fields(p[3]);
+      if (to_ll(f["repetitions"]) != 1) return ZBHIP_EUNSUPP;  // cycles: outside the subset
+      timers.push_back({to_ll(p[1]), to_ll(p[2]), to_ll(f["dueDate"]), f["handlerNodeId"]});
     } else if (cf == "MESSAGE_SUBSCRIPTION_BY_KEY" || cf == "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY") {
       return ZBHIP_EUNSUPP;  // message-partition rows: no routing handle to the subscriber's slot
     } else if (cf == "MESSAGE_STATS") {
@@ -2387,12 +2451,14 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   std::vector<uint32_t> join(N * kJoinWords);
   std::vector<uint4> pmsrow(h->st.n_slots ? N : 0);
   std::vector<long long> pikrow(h->st.n_slots ? N : 0);
+  std::vector<uint4> tmrrow(N);
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(hdr.data(), h->st.hdr, N * sizeof(uint4), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(slots.data(), h->st.slots, N * kSlots * sizeof(uint2), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(vm.data(), h->st.var_meta, N * kVars * sizeof(uint2), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(vv.data(), h->st.var_val, N * kVars * sizeof(long long), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(join.data(), h->st.join, N * kJoinWords * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(tmrrow.data(), h->st.tmr, N * sizeof(uint4), hipMemcpyDeviceToHost));
   if (h->st.n_slots) {
     HIPCHK(hipMemcpy(pmsrow.data(), h->st.pms, N * sizeof(uint4), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(pikrow.data(), h->st.pi_key, N * sizeof(long long), hipMemcpyDeviceToHost));
@@ -2449,6 +2515,13 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
         if (subs.count(v.scope)) return ZBHIP_EUNSUPP;  // sub-process-local variables: outside the subset
         ivars.push_back(&v);
         keys.push_back(v.key);
+      }
+    const ImpTimer* tmr = nullptr;  // the instance's timer (one per instance on the device)
+    for (const auto& t : timers)
+      if (std::any_of(children.begin(), children.end(), [&](const ImpElement* c) { return c->key == t.eik; })) {
+        if (tmr) return ZBHIP_EUNSUPP;
+        tmr = &t;
+        keys.push_back(t.key);
       }
     const ImpPms* sub = nullptr;
     for (const auto& m : pms)
@@ -2514,6 +2587,13 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     } else if (sub) {
       return ZBHIP_EUNSUPP;
     }
+    tmrrow[inst] = make_uint4(0, 0, 0, 0);
+    if (tmr) {
+      const int el = elem_of_id(tmr->handler);
+      if (el < 0 || !P.has_timer) return ZBHIP_EINVAL;
+      tmrrow[inst] = make_uint4((uint32_t)el | (ord(tmr->key) << 16), ord(tmr->eik) | (1u << 31),
+                                (uint32_t)(uint64_t)tmr->due, (uint32_t)((uint64_t)tmr->due >> 32));
+    }
     hdr[inst] = make_uint4((uint32_t)proc | ((uint32_t)keys.size() << 16),
                            pe.state | ((uint32_t)children.size() << 8) | ((uint32_t)ivars.size() << 16) | (1u << 24),
                            (uint32_t)pe.child_count | ((uint32_t)pe.asf << 16), 0);
@@ -2524,6 +2604,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   HIPCHK(hipMemcpy(h->st.var_meta, vm.data(), N * kVars * sizeof(uint2), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->st.var_val, vv.data(), N * kVars * sizeof(long long), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->st.join, join.data(), N * kJoinWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->st.tmr, tmrrow.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
   if (h->st.n_slots) {
     HIPCHK(hipMemcpy(h->st.pms, pmsrow.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->st.pi_key, pikrow.data(), N * sizeof(long long), hipMemcpyHostToDevice));

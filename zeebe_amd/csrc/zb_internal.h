@@ -72,6 +72,9 @@ enum : uint8_t {
   C_MS_CORRELATED = 44,
   C_MSG_PUBLISHED = 49,
   C_MSG_EXPIRED = 50,
+  C_TIMER_CREATED = 52,   // key = timer, aux = element instance (TimerRecord, CatchEventBehavior.java:303-330)
+  C_TIMER_TRIGGER = 53,   // (rejections of TIMER:TRIGGER)
+  C_TIMER_TRIGGERED = 54,
   kRejectBit = 0x40,
 };
 
@@ -114,11 +117,14 @@ constexpr uint8_t CMD_FOLLOWUP = 0x20;
 //   p[0] = n_elements | none_start << 16
 //   p[1] = n_join_slots | n_conditions << 16
 //   p[2] = out_off, p[3] = cond_off, p[4] = code_off (words, relative to p), p[5] = bpmnProcessId
-//   name id, p[6] = seg_off, p[7] = CREATE template word (TPL_OK | exclusive gateway or 0xFFF; 0 = none)
+//   name id | has timer catch events << 16, p[6] = seg_off, p[7] = CREATE template word (TPL_OK |
+//   exclusive gateway or 0xFFF; 0 = none)
 //   p[8 + 4e .. ] element e: w0 = type | event << 8 | in_count << 16
 //                            w1 = out_begin | out_count << 16
-//                            w2 = flow: target | condition << 16; xgw: default_flow; task: job_type | retries << 16
-//                            w3 = join_slot | id << 16
+//                            w2 = flow: target | condition << 16; xgw: default_flow; task: job_type | retries << 16;
+//                                 message catch: name | correlation variable << 16; timer catch: duration ms;
+//                                 sub-process: none start event | join slots of its gateways << 16
+//                            w3 = join_slot | container (flow scope element; 0 = the process) << 16
 //   p[out_off]  u16 outgoing flows (two per word)
 //   p[cond_off] u32 first instruction of each condition
 //   p[code_off] instructions (16-byte aligned): op, arg, literal_lo, literal_hi
@@ -144,6 +150,8 @@ struct DevState {
   longlong2* sub_b;  // [kSubs][S] x = element instance key, y = process instance key (real)
   longlong2* sub_k;  // [kSubs][S] x = subscription key, y = message key while correlating (-1 else)
   uint32_t n_slots;
+  uint4* tmr;        // [n] the instance's timer (KScope; one per instance): x = catch element | timer key
+                     //     ordinal << 16, y = element-instance ordinal | live << 31, z/w = dueDate lo/hi
 };
 
 // elements without behaviour: ACTIVATING, ACTIVATED, COMPLETE_ELEMENT, COMPLETING, COMPLETED, then
@@ -198,6 +206,7 @@ struct StepParams {
   // number (a template recorded in the running launch is not used before the next one)
   uint2* tpl;
   uint32_t launch_seq;
+  long long now_ms;           // zbhip_set_clock: ActorClock.currentTimeMillis() of this window
 };
 
 // ---- log bytes on the device (logdev.hip) ----

@@ -39,7 +39,7 @@ ELEMENT_DTYPE = np.dtype([("element_type", "u1"), ("event_type", "u1"), ("out_be
                           ("in_count", "<u2"), ("flow_source", "<u2"), ("flow_target", "<u2"), ("condition", "<u2"),
                           ("default_flow", "<u2"), ("job_type", "<u2"), ("job_retries", "<u2"), ("join_slot", "<u2"),
                           ("id", "<u2"), ("message_name", "<u2"), ("correlation_var", "<u2"),
-                          ("flow_scope", "<u2"), ("start_event", "<u2")])
+                          ("flow_scope", "<u2"), ("start_event", "<u2"), ("duration_ms", "<u4")])
 
 
 class Partition:
@@ -213,6 +213,10 @@ class Partition:
 
     def run(self, flags=0):
         return check(self.L.zbhip_run(self.h, flags), "zbhip_run")
+
+    def set_clock(self, now_ms):
+        """ActorClock.currentTimeMillis() for the next runs (timer catch events' due dates)."""
+        check(self.L.zbhip_set_clock(self.h, int(now_ms)), "zbhip_set_clock")
 
     def drain(self, out=None):
         """The window's records in log order; `out` (a RECORD_DTYPE array) is reused when it is

@@ -17,7 +17,7 @@ ERRORS = {-1: "ZBHIP_EINVAL", -2: "ZBHIP_ENOMEM", -3: "ZBHIP_EDEVICE", -4: "ZBHI
 
 # every symbol include/zbhip.h declares (tests/test_abi.py checks the export table)
 SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", "zbhip_deploy", "zbhip_intern",
-           "zbhip_string", "zbhip_name", "zbhip_submit", "zbhip_submit_device", "zbhip_run", "zbhip_drain",
+           "zbhip_string", "zbhip_name", "zbhip_submit", "zbhip_submit_device", "zbhip_run", "zbhip_set_clock", "zbhip_drain",
            "zbhip_pending_records", "zbhip_get_stats", "zbhip_export_state", "zbhip_fallback",
            "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info", "zbhip_command_status",
            "zbhip_submit_ex", "zbhip_submit_device_ex", "zbhip_intern_string", "zbhip_intern_strings",
@@ -70,6 +70,7 @@ def load():
     L.zbhip_submit.argtypes = [vp, vp, sz, vp, sz]
     L.zbhip_submit_device.argtypes = [vp, vp, sz, vp, sz]
     L.zbhip_run.argtypes = [vp, u32]
+    L.zbhip_set_clock.argtypes = [vp, C.c_int64]
     L.zbhip_drain.argtypes = [vp, vp, sz, C.POINTER(sz)]
     L.zbhip_pending_records.argtypes = [vp]
     L.zbhip_pending_records.restype = i64
