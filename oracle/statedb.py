@@ -132,8 +132,17 @@ def encode_rows(rows, processes, string_value):
             out.append((CF[name], prefix + dblong(int(parts[1])) + dbstr(parts[2]), val))
         elif name == "EVENT_SCOPE":
             f = fields(parts[2])
+            def ids(v):  # ';'-separated element ids -> ArrayProperty<StringValue> items
+                out = []
+                for x in (v.split(";") if v else []):
+                    w = LS.MsgPackWriter()
+                    w.string(x)
+                    out.append(bytes(w.b))
+                return out
             val = LS.write_object(EVENT_SCOPE_INSTANCE, {"accepting": f["accepting"] == "1",
-                                                      "interrupted": f["interrupted"] == "1"})
+                                                      "interrupted": f["interrupted"] == "1",
+                                                      "interrupting": ids(f.get("interrupting", "")),
+                                                      "boundaryElementIds": ids(f.get("boundaryElementIds", ""))})
             out.append((CF[name], prefix + dblong(int(parts[1])), val))
         elif name == "JOBS":
             key, f = int(parts[1]), fields(parts[2])

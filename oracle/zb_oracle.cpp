@@ -2099,7 +2099,14 @@ std::string Oracle::dump_state() const {
     rows.push_back(buf);
   }
   for (auto k : event_scope_) {
-    snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", (long long)k);
+    // EventScopeInstance (state/instance/EventScopeInstance.java:25-35): the interrupting ids of a
+    // catch event are its own id (ExecutableCatchEventElement.java:124-127), an activity's those of
+    // its interrupting boundary events (none in the subset); boundaryElementIds empty
+    auto eit = ei_.find(k);
+    const OEl* el = eit == ei_.end() ? nullptr : &procs[eit->second.value.proc].els[eit->second.value.elem];
+    const std::string intr = el && el->type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ? el->id : "";
+    snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=",
+             (long long)k, intr.c_str());
     rows.push_back(buf);
   }
   for (auto& [k, t] : triggers_) {

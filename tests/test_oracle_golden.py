@@ -57,7 +57,7 @@ def test_one_task_final_state_is_empty_after_completion():
     assert any(r.startswith("JOBS|%d|type=benchmark-task,retries=3" % (BASE + 6)) for r in st)
     assert "JOB_STATES|%d|ACTIVATABLE" % (BASE + 6) in st
     assert "JOB_ACTIVATABLE|benchmark-task|<default>|%d" % (BASE + 6) in st
-    assert "EVENT_SCOPE|%d|accepting=1,interrupted=0" % (BASE + 5) in st
+    assert "EVENT_SCOPE|%d|accepting=1,interrupted=0,interrupting=,boundaryElementIds=" % (BASE + 5) in st
     assert "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY|2251799813685249|%d" % (BASE + 1) in st
     _run_single(o, complete_commands([0], [5]))
     # everything removed on completion; only the key generator remains

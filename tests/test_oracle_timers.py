@@ -82,7 +82,7 @@ def test_should_create_timer():
     assert int(created["aux"]) == NOW + 10000
     st = o.state()
     assert "TIMER_DUE_DATES|%d|%d|%d" % (NOW + 10000, int(activated["key"]), int(created["key"])) in st
-    assert "EVENT_SCOPE|%d|accepting=1,interrupted=0" % int(activated["key"]) in st
+    assert "EVENT_SCOPE|%d|accepting=1,interrupted=0,interrupting=timer,boundaryElementIds=" % int(activated["key"]) in st
 
 
 def test_should_trigger_and_complete_timer_event():

@@ -691,9 +691,15 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     auto f = fields_of(p[2]);
     cf_prefix(k, ord); dbl(k, ll(p[1]));
     mp_map(v, 4);  // EventScopeInstance.java:32-35
+    auto ids = [&](const std::string& list) {  // ';'-separated element ids -> ArrayProperty<StringValue>
+      std::vector<std::string> out;
+      if (!list.empty()) out = split(list, ';');
+      mp_array(v, (uint32_t)out.size());
+      for (auto& id : out) mp_str(v, id);
+    };
     key(v, "accepting"); v.push_back((char)(f["accepting"] == "1" ? 0xc3 : 0xc2));
-    key(v, "interrupting"); mp_array(v, 0);
-    key(v, "boundaryElementIds"); mp_array(v, 0);
+    key(v, "interrupting"); ids(f["interrupting"]);
+    key(v, "boundaryElementIds"); ids(f["boundaryElementIds"]);
     key(v, "interrupted"); v.push_back((char)(f["interrupted"] == "1" ? 0xc3 : 0xc2));
   } else if (cf == "JOBS" && need(3)) {
     ord = 16;
@@ -1059,8 +1065,15 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
     case 37: {  // EVENT_SCOPE
       const int64_t k = K.dblong();
       if (!K.ok || !value()) return ZBHIP_EINVAL;
-      snprintf(b, sizeof b, "EVENT_SCOPE|%lld|accepting=%d,interrupted=%d", (long long)k, mb(v.get("accepting")),
-               mb(v.get("interrupted")));
+      auto ids = [&](const char* name) {
+        std::string out;
+        if (const MpNode* a = v.get(name))
+          for (const auto& it : a->arr) out += (out.empty() ? "" : ";") + ms(&it);
+        return out;
+      };
+      snprintf(b, sizeof b, "EVENT_SCOPE|%lld|accepting=%d,interrupted=%d,interrupting=%s,boundaryElementIds=%s",
+               (long long)k, mb(v.get("accepting")), mb(v.get("interrupted")), ids("interrupting").c_str(),
+               ids("boundaryElementIds").c_str());
       out = b;
       break;
     }

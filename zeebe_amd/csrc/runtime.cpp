@@ -2074,7 +2074,11 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, fs);
     sink(ctx, buf);
     if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
-      snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0", k);
+      // EventScopeInstance.java:25-35: a catch event's interrupting ids are its own id
+      // (ExecutableCatchEventElement.java:124-127), a job worker's those of its interrupting
+      // boundary events (none in the subset)
+      snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=", k,
+               E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ? P.id(elem).c_str() : "");
       sink(ctx, buf);
     }
     if (job_row) {
