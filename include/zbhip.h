@@ -84,14 +84,15 @@ enum zbhip_pi_intent {
   ZBHIP_PI_COMPLETE_ELEMENT = 9,
   ZBHIP_PI_TERMINATE_ELEMENT = 10
 };
-/* JobIntent CREATED=0 COMPLETE=1 COMPLETED=2; VariableIntent CREATED=0 UPDATED=1;
- * ProcessEventIntent TRIGGERING=0; ProcessInstanceCreationIntent CREATE=0 CREATED=1 */
-enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2 };
+/* JobIntent CREATED=0 COMPLETE=1 COMPLETED=2 CANCELED=10 (JobIntent.java:19-45); VariableIntent
+ * CREATED=0 UPDATED=1; ProcessEventIntent TRIGGERING=0 TRIGGERED=1; ProcessInstanceCreationIntent
+ * CREATE=0 CREATED=1 */
+enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2, ZBHIP_JOB_CANCELED = 10 };
 enum { ZBHIP_VAR_CREATED = 0, ZBHIP_VAR_UPDATED = 1 };
-enum { ZBHIP_PE_TRIGGERING = 0 };
+enum { ZBHIP_PE_TRIGGERING = 0, ZBHIP_PE_TRIGGERED = 1 };
 enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
 /* TimerIntent (protocol/.../intent/TimerIntent.java:19-30) */
-enum { ZBHIP_TIMER_CREATED = 0, ZBHIP_TIMER_TRIGGER = 1, ZBHIP_TIMER_TRIGGERED = 2 };
+enum { ZBHIP_TIMER_CREATED = 0, ZBHIP_TIMER_TRIGGER = 1, ZBHIP_TIMER_TRIGGERED = 2, ZBHIP_TIMER_CANCELED = 4 };
 /* MessageIntent, MessageSubscriptionIntent, ProcessMessageSubscriptionIntent
  * (protocol/.../intent/MessageIntent.java:19-23, MessageSubscriptionIntent.java:19-30,
  * ProcessMessageSubscriptionIntent.java:19-28) */
@@ -157,7 +158,8 @@ typedef struct zbhip_element {
   uint16_t out_begin;    /* outgoing flows: out_flow[out_begin .. out_begin+out_count) in getOutgoing() order */
   uint16_t out_count;
   uint16_t in_count;     /* incoming arity (parallel-gateway join arity) */
-  uint16_t flow_source;  /* sequence flow: source node; else ZBHIP_NONE16 */
+  uint16_t flow_source;  /* sequence flow: source node; boundary event: the activity it is attached to
+                          * (attachedToRef, ExecutableActivity.attach); else ZBHIP_NONE16 */
   uint16_t flow_target;  /* sequence flow: target node; else ZBHIP_NONE16 */
   uint16_t condition;    /* sequence flow: condition index; ZBHIP_NONE16 = no condition */
   uint16_t default_flow; /* exclusive gateway: default flow element; else ZBHIP_NONE16 */
@@ -170,8 +172,9 @@ typedef struct zbhip_element {
   uint16_t flow_scope;   /* the element's container: 0 = the process, else the embedded sub-process
                           * element (ExecutableFlowElement.getFlowScope, FlowElementInstantiationTransformer) */
   uint16_t start_event;  /* process / embedded sub-process: its none start event
-                          * (ExecutableFlowElementContainer.getNoneStartEvent); else ZBHIP_NONE16 */
-  uint32_t duration_ms;  /* timer catch event: the static timeDuration in ms (Interval.parse); else 0 */
+                          * (ExecutableFlowElementContainer.getNoneStartEvent); job worker task: its
+                          * (one, interrupting timer) boundary event; else ZBHIP_NONE16 */
+  uint32_t duration_ms;  /* timer catch / boundary event: the static timeDuration in ms (Interval.parse); else 0 */
 } zbhip_element;
 
 /* FEEL condition bytecode (subset of feel-scala 1.17.0 boolean expressions,

@@ -356,7 +356,9 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
                                            processInstanceKey=int(r["process_instance_key"]),
                                            processDefinitionKey=p["key"], bpmnProcessId=p["bpmn_process_id"]))
     if vt == VT_PE:
-        return write_object(PROCESS_EVENT, dict(scopeKey=int(r["scope_key"]), targetElementId=el[2], variables=src_doc,
+        # TRIGGERED: EventTriggerBehavior.processEventTriggered resets the record (no variables)
+        pe_vars = EMPTY_DOCUMENT if int(r["intent"]) == 1 else src_doc
+        return write_object(PROCESS_EVENT, dict(scopeKey=int(r["scope_key"]), targetElementId=el[2], variables=pe_vars,
                                                 processDefinitionKey=p["key"],
                                                 processInstanceKey=int(r["process_instance_key"])))
     if vt == VT_TIMER:  # a rejected TIMER:TRIGGER: the command's key and dueDate (the window's view of it)

@@ -335,6 +335,8 @@ struct OEl {
   int64_t timer_ms = -1;           // timer catch event: the static timeDuration in ms (TimerTransformer)
   int scope = 0;                   // flow scope element (ExecutableFlowElement.getFlowScope): 0 = process
   int start = -1;                  // process / sub-process: getNoneStartEvent
+  int attached = -1;               // boundary event: the activity it is attached to (attachedToRef)
+  int boundary = -1;               // activity: its (one, interrupting) boundary event (ExecutableActivity.attach)
 };
 
 struct OProc {
@@ -394,6 +396,7 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
   std::unordered_map<std::string, int> idx;
   idx[P.bpmn_id] = 0;
   std::vector<const XNode*> flows, xgws;
+  std::vector<std::pair<int, std::string>> boundaries;  // (boundary event, attachedToRef)
   // FlowElementInstantiationTransformer over every container (the process and its embedded
   // sub-processes, SubProcessTransformer): elements numbered in document pre-order
   std::function<bool(const XNode&, int)> walk = [&](const XNode& parent, int scope) -> bool {
@@ -459,6 +462,25 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_TIMER;
+    } else if (n == "boundaryEvent") {
+      // BoundaryEventTransformer (deployment/model/transformer/BoundaryEventTransformer.java):
+      // interrupting timer boundary events with a static timeDuration on job worker tasks only
+      e.type = ZBHIP_EL_BOUNDARY_EVENT;
+      if (k->attr("cancelActivity") == "false") { err = "non-interrupting boundary event outside the supported subset"; return false; }
+      const XNode* ted = k->child("timerEventDefinition");
+      const XNode* td = ted ? ted->child("timeDuration") : nullptr;
+      if (!td || k->child("messageEventDefinition") || k->child("errorEventDefinition") ||
+          k->child("signalEventDefinition") || k->child("escalationEventDefinition") ||
+          k->child("compensateEventDefinition") || k->child("conditionalEventDefinition")) {
+        err = "boundary event outside the supported subset (timer timeDuration only)";
+        return false;
+      }
+      e.timer_ms = parse_duration_ms(td->text);
+      if (e.timer_ms < 0 || e.timer_ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return false; }
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+      e.event = ZBHIP_EV_TIMER;
+      boundaries.push_back({(int)P.els.size(), k->attr("attachedToRef")});
     } else if (n == "intermediateCatchEvent") {
       // CatchEventTransformer.transformMessageEventDefinition (transformer/CatchEventTransformer.java:88-100)
       e.type = ZBHIP_EL_INTERMEDIATE_CATCH_EVENT;
@@ -533,6 +555,19 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
   return true;
   };
   if (!walk(proc, 0)) return false;
+  // BoundaryEventTransformer: attach to the activity (ExecutableActivity.attach, ExecutableActivity.java:28-38)
+  for (auto& [b, ref] : boundaries) {
+    auto it = idx.find(ref);
+    if (it == idx.end()) { err = "boundary event attached to an unknown element"; return false; }
+    OEl& a = P.els[it->second];
+    if (!ZBHIP_IS_JOB_WORKER(a.type) || a.scope != P.els[b].scope) {
+      err = "boundary event on an element outside the supported subset (job worker tasks only)";
+      return false;
+    }
+    if (a.boundary >= 0) { err = "more than one boundary event on an activity outside the supported subset"; return false; }
+    a.boundary = b;
+    P.els[b].attached = it->second;
+  }
   // gateway default flows (ExclusiveGatewayTransformer.transformDefaultFlow)
   for (const XNode* k : xgws) {
     if (!k->attr("default").empty()) {
@@ -1011,7 +1046,8 @@ class Oracle {
   std::map<std::tuple<int64_t, int, int>, int> taken_;          // NUMBER_OF_TAKEN_SEQUENCE_FLOWS (proc-local ids)
   std::set<std::pair<int64_t, int64_t>> pi_by_def_;             // PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY
   std::map<std::pair<int64_t, int>, VarRow> vars_;              // VARIABLES (scope, name id)
-  std::set<int64_t> event_scope_;                               // EVENT_SCOPE (accepting, not interrupted)
+  std::set<int64_t> event_scope_;                               // EVENT_SCOPE
+  std::set<int64_t> es_interrupted_, es_closed_;                // EventScopeInstance.interrupted / !accepting
   std::map<std::pair<int64_t, int64_t>, EventTrigger> triggers_;// EVENT_TRIGGER
   struct TimerRow {  // TimerInstance (state/instance/TimerInstance.java:23-44)
     PiValue pi;      // process, handler element, process instance key
@@ -1278,7 +1314,7 @@ class Oracle {
     const int64_t eik = it->first.first;
     const TimerRow t = it->second;
     auto eit = ei_.find(eik);
-    if (eit == ei_.end() || eit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED || !event_scope_.count(eik)) {
+    if (eit == ei_.end() || eit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED || !can_trigger(eik, t.pi.elem, t.pi.proc)) {
       reject(cmd, ZBHIP_REJ_INVALID_STATE,
              "Expected to trigger a timer with key '" + std::to_string(tk) + "', but the timer is not active anymore");
       return;
@@ -1297,8 +1333,51 @@ class Oracle {
     pe.r.scope_key = eik;
     pe.r.process_instance_key = t.pi.piKey;
     pe.r.aux = -1;
-    triggers_[{eik, eventKey}] = EventTrigger{t.pi.elem, t.pi.proc, Doc{0, 0}, t.pi.piKey};
-    pi_command(eik, ZBHIP_PI_COMPLETE_ELEMENT, eit->second.value);
+    trigger_event(eik, eventKey, t.pi.elem, t.pi.proc, Doc{0, 0}, t.pi.piKey);
+    if (E(t.pi).type == ZBHIP_EL_BOUNDARY_EVENT)  // isInterrupting: terminate the activity first
+      pi_command(eik, ZBHIP_PI_TERMINATE_ELEMENT, eit->second.value);
+    else                                          // isElementActivated (catch event)
+      pi_command(eik, ZBHIP_PI_COMPLETE_ELEMENT, eit->second.value);
+  }
+
+  // DbEventScopeInstanceState.canTriggerEvent (state/instance/DbEventScopeInstanceState.java:178-182):
+  // accepting, and not interrupted unless the element is one of the scope's boundary events
+  bool can_trigger(int64_t scope, int elem, int proc) const {
+    if (!event_scope_.count(scope) || es_closed_.count(scope)) return false;
+    if (!es_interrupted_.count(scope)) return true;
+    const OEl& e = procs[proc].els[elem];
+    return e.type == ZBHIP_EL_BOUNDARY_EVENT;
+  }
+
+  // DbEventScopeInstanceState.triggerEvent (:100-124): an interrupting element id interrupts the
+  // scope, an interrupting boundary event also closes it; then the EVENT_TRIGGER row
+  void trigger_event(int64_t scope, int64_t eventKey, int elem, int proc, Doc vars, int64_t piKey) {
+    if (!can_trigger(scope, elem, proc)) return;
+    auto sit = ei_.find(scope);
+    if (sit != ei_.end()) {
+      const OEl& owner = procs[sit->second.value.proc].els[sit->second.value.elem];
+      const bool interrupting = owner.id == procs[proc].els[elem].id ? owner.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
+                                                                           owner.type == ZBHIP_EL_BOUNDARY_EVENT
+                                                                     : owner.boundary == elem;
+      if (interrupting) es_interrupted_.insert(scope);
+      if (interrupting && owner.boundary == elem) es_closed_.insert(scope);
+    }
+    triggers_[{scope, eventKey}] = EventTrigger{elem, proc, vars, piKey};
+  }
+
+  // CatchEventBehavior.unsubscribeFromTimerEvents (processing/common/CatchEventBehavior.java:369-392):
+  // TIMER:CANCELED (the timer's key and stored value) per timer of the element instance; TimerCancelledApplier
+  void unsubscribe_timers(int64_t eik) {
+    for (auto it = timers_.lower_bound({eik, INT64_MIN}); it != timers_.end() && it->first.first == eik;) {
+      const TimerRow& t = it->second;
+      ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_TIMER, ZBHIP_TIMER_CANCELED, it->first.second);
+      rec.r.process_idx = t.pi.proc;
+      rec.r.element_idx = t.pi.elem;
+      rec.r.scope_key = eik;
+      rec.r.process_instance_key = t.pi.piKey;
+      rec.r.aux = t.dueDate;
+      it = timers_.erase(it);
+    }
   }
 
   void subscribe_to_message(const OEl& el, int64_t key, const PiValue& v) {
@@ -1591,8 +1670,7 @@ class Oracle {
         pe.doc = cmd.doc;
         // ProcessEventTriggeringApplier (state/appliers/ProcessEventTriggeringApplier.java:35-56)
         // -> DbEventScopeInstanceState.triggerEvent (only if the scope accepts)
-        if (event_scope_.count(job.elementInstanceKey))
-          triggers_[{job.elementInstanceKey, eventKey}] = EventTrigger{job.pi.elem, job.pi.proc, cmd.doc, job.pi.piKey};
+        trigger_event(job.elementInstanceKey, eventKey, job.pi.elem, job.pi.proc, cmd.doc, job.pi.piKey);
         pi_command(job.elementInstanceKey, ZBHIP_PI_COMPLETE_ELEMENT, task.value);
       }
     }
@@ -1615,6 +1693,12 @@ class Oracle {
       auto fit = ei_.find(it->second.value.flowScopeKey);
       if (fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED) it->second.jobKey = -1;
     }
+  }
+
+  // JobCanceledApplier (state/appliers/JobCanceledApplier.java:28-30) -> DbJobState.cancel -> delete
+  void apply_job_canceled(int64_t jobKey, const JobRow& job) {
+    jobs_.erase(jobKey);
+    activatable_.erase({job.type, "<default>", jobKey});
   }
 
   // ---------------------------------------------------------------------
@@ -1640,7 +1724,9 @@ class Oracle {
       pi_event(cmd.r.key, ZBHIP_PI_ELEMENT_COMPLETING, cmd.pi);
       on_complete(el, cmd.r.key, cmd.pi);
     } else {
-      throw Unsupported{"terminate"};
+      // TERMINATE_ELEMENT: transitionToTerminating, then the processor's onTerminate (:151-154)
+      pi_event(cmd.r.key, ZBHIP_PI_ELEMENT_TERMINATING, cmd.pi);
+      on_terminate(el, cmd.r.key, cmd.pi);
     }
   }
 
@@ -1703,6 +1789,21 @@ class Oracle {
       }
       return has_active_flow_scope(cmd, v);
     }
+    if (cmd.r.intent == ZBHIP_PI_TERMINATE_ELEMENT) {  // hasElementInstanceWithState (:60-64)
+      auto it = ei_.find(cmd.r.key);
+      if (it == ei_.end()) {
+        v = "Expected element instance with key '" + std::to_string(cmd.r.key) +
+            "' to be present in state but not found.";
+        return false;
+      }
+      int s = it->second.state;
+      if (s != ZBHIP_PI_ELEMENT_ACTIVATING && s != ZBHIP_PI_ELEMENT_ACTIVATED && s != ZBHIP_PI_ELEMENT_COMPLETING) {
+        v = std::string("Expected element instance to be in state 'ELEMENT_ACTIVATING' or one of "
+                        "'[ELEMENT_ACTIVATED, ELEMENT_COMPLETING]' but was '") + state_name(s) + "'.";
+        return false;
+      }
+      return true;
+    }
     throw Unsupported{"intent"};
   }
 
@@ -1757,6 +1858,12 @@ class Oracle {
       case ZBHIP_EL_SEND_TASK:
       case ZBHIP_EL_SCRIPT_TASK:
       case ZBHIP_EL_BUSINESS_RULE_TASK: {
+        // eventSubscriptionBehavior.subscribeToEvents: the attached boundary event's timer first
+        if (el.boundary >= 0) {
+          PiValue bv = v;
+          bv.elem = el.boundary;
+          subscribe_to_timer(P(v.proc).els[el.boundary], key, bv);
+        }
         // BpmnJobBehavior.createNewJob -> writeJobCreatedEvent (behavior/BpmnJobBehavior.java:113-119,194-218)
         JobRow job;
         job.pi = v;
@@ -1815,6 +1922,11 @@ class Oracle {
       case ZBHIP_EL_SEND_TASK:
       case ZBHIP_EL_SCRIPT_TASK:
       case ZBHIP_EL_BUSINESS_RULE_TASK:
+        // applyOutputMappings, unsubscribeFromEvents (the boundary event's timer: TIMER:CANCELED),
+        // transitionToCompleted, takeOutgoingSequenceFlows
+        complete_and_take(el, key, v, true, /*unsubscribe=*/true);
+        break;
+      case ZBHIP_EL_BOUNDARY_EVENT:  // BoundaryEventProcessor.onComplete (processing/bpmn/event/BoundaryEventProcessor.java:47-56)
       case ZBHIP_EL_INTERMEDIATE_THROW_EVENT:  // NoneIntermediateThrowEventBehavior.onComplete (:128-137)
         complete_and_take(el, key, v, true);
         break;
@@ -1839,9 +1951,58 @@ class Oracle {
     }
   }
 
+  // JobWorkerTaskProcessor.onTerminate (processing/bpmn/task/JobWorkerTaskProcessor.java:77-104)
+  void on_terminate(const OEl& el, int64_t key, const PiValue& v) {
+    if (!ZBHIP_IS_JOB_WORKER(el.type)) throw Unsupported{"terminate of a non job worker element"};
+    // jobBehavior.cancelJob (behavior/BpmnJobBehavior.java:251-274): JOB:CANCELED with the stored job
+    const int64_t jobKey = ei_.at(key).jobKey;
+    auto jit = jobKey > 0 ? jobs_.find(jobKey) : jobs_.end();
+    if (jit != jobs_.end()) {
+      const JobRow job = jit->second;
+      ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_CANCELED, jobKey);
+      rec.r.process_idx = job.pi.proc;
+      rec.r.element_idx = job.pi.elem;
+      rec.r.scope_key = job.elementInstanceKey;
+      rec.r.process_instance_key = job.pi.piKey;
+      apply_job_canceled(jobKey, job);
+    }
+    unsubscribe_timers(key);
+    // findEventTrigger (BpmnEventSubscriptionBehavior.java:63-70): the scope's first trigger, unless
+    // it is the element's own
+    auto tit = triggers_.lower_bound({key, INT64_MIN});
+    const bool found = tit != triggers_.end() && tit->first.first == key && tit->second.elem != v.elem;
+    auto fit = ei_.find(v.flowScopeKey);
+    if (!found || fit == ei_.end() || fit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED)
+      throw Unsupported{"termination without an event trigger (onElementTerminated)"};
+    const int64_t eventKey = tit->first.second;
+    const int target = tit->second.elem;
+    pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);  // transitionToTerminated
+    activate_triggered_event(eventKey, target, key, v.flowScopeKey, v);
+  }
+
+  // EventTriggerBehavior.activateTriggeredEvent (processing/common/EventTriggerBehavior.java:191-244):
+  // PROCESS_EVENT:TRIGGERED (the trigger's key), ACTIVATING + ACTIVATED of the triggered event
+  // (+key, flow scope = the given one), COMPLETE_ELEMENT
+  void activate_triggered_event(int64_t eventKey, int target, int64_t scope, int64_t flowScopeKey, const PiValue& v) {
+    ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERED, eventKey);
+    pe.r.process_idx = v.proc;
+    pe.r.element_idx = target;
+    pe.r.scope_key = scope;
+    pe.r.process_instance_key = v.piKey;
+    pe.r.aux = -1;
+    triggers_.erase({scope, eventKey});  // ProcessEventTriggeredApplier: deleteTrigger (if it exists)
+    PiValue bv = v;
+    bv.elem = target;
+    bv.flowScopeKey = flowScopeKey;
+    const int64_t bk = next_key();
+    pi_event(bk, ZBHIP_PI_ELEMENT_ACTIVATING, bv);
+    pi_event(bk, ZBHIP_PI_ELEMENT_ACTIVATED, bv);
+    pi_command(bk, ZBHIP_PI_COMPLETE_ELEMENT, bv);
+  }
+
   // applyOutputMappings (behavior/BpmnVariableMappingBehavior.java:86-156) ->
   // transitionToCompleted -> takeOutgoingSequenceFlows (BpmnStateTransitionBehavior.java:365-369)
-  void complete_and_take(const OEl& el, int64_t key, const PiValue& v, bool output_mappings) {
+  void complete_and_take(const OEl& el, int64_t key, const PiValue& v, bool output_mappings, bool unsubscribe = false) {
     if (output_mappings) {
       const EventTrigger* trig = nullptr;  // peekEventTrigger(elementInstanceKey)
       auto it = triggers_.lower_bound({key, INT64_MIN});
@@ -1849,6 +2010,7 @@ class Oracle {
       if (trig && trig->vars.count > 0) merge_document(key, v.proc, v.piKey, trig->vars);
       // START_EVENT without trigger: local variables of the start event are empty.
     }
+    if (unsubscribe) unsubscribe_timers(key);
     transition_to_completed(el, key, v);
     for (int f : el.out) take_sequence_flow(key, v, f);
   }
@@ -1973,7 +2135,9 @@ class Oracle {
     switch (intent) {
       case ZBHIP_PI_ELEMENT_ACTIVATING: {  // ProcessInstanceElementActivatingApplier.applyState (:48-77)
         // createEventScope (:255-289): job worker elements get an event scope
-        if (ZBHIP_IS_JOB_WORKER(el.type) || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) event_scope_.insert(key);
+        if (ZBHIP_IS_JOB_WORKER(el.type) || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
+            el.type == ZBHIP_EL_BOUNDARY_EVENT)
+          event_scope_.insert(key);
         // cleanupSequenceFlowsTaken (:79-98): Tetris decrement of (flowScope, gateway)
         if (el.type == ZBHIP_EL_PARALLEL_GATEWAY) {
           for (auto it = taken_.lower_bound({v.flowScopeKey, v.elem, -1}); it != taken_.end();) {
@@ -2018,11 +2182,17 @@ class Oracle {
       case ZBHIP_PI_ELEMENT_COMPLETING:  // ProcessInstanceElementCompletingApplier
         ei_.at(key).state = ZBHIP_PI_ELEMENT_COMPLETING;
         break;
+      case ZBHIP_PI_ELEMENT_TERMINATING:  // ProcessInstanceElementTerminatingApplier
+        ei_.at(key).state = ZBHIP_PI_ELEMENT_TERMINATING;
+        break;
+      case ZBHIP_PI_ELEMENT_TERMINATED:  // ProcessInstanceElementTerminatedApplier (:38-55): the same removal
       case ZBHIP_PI_ELEMENT_COMPLETED: {  // ProcessInstanceElementCompletedApplier (:45-73)
         // eventScopeInstanceState.deleteInstance: triggers then the scope
         for (auto it = triggers_.lower_bound({key, INT64_MIN}); it != triggers_.end() && it->first.first == key;)
           it = triggers_.erase(it);
         event_scope_.erase(key);
+        es_interrupted_.erase(key);
+        es_closed_.erase(key);
         // DbElementInstanceState.removeInstance (:160-193)
         auto it = ei_.find(key);
         if (it == ei_.end()) break;
@@ -2100,13 +2270,17 @@ std::string Oracle::dump_state() const {
   }
   for (auto k : event_scope_) {
     // EventScopeInstance (state/instance/EventScopeInstance.java:25-35): the interrupting ids of a
-    // catch event are its own id (ExecutableCatchEventElement.java:124-127), an activity's those of
-    // its interrupting boundary events (none in the subset); boundaryElementIds empty
+    // catch / boundary event are its own id (ExecutableCatchEventElement.java:124-132), an activity's
+    // those of its interrupting boundary events, which are also its boundaryElementIds
+    // (ExecutableActivity.java:28-38)
     auto eit = ei_.find(k);
-    const OEl* el = eit == ei_.end() ? nullptr : &procs[eit->second.value.proc].els[eit->second.value.elem];
-    const std::string intr = el && el->type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ? el->id : "";
-    snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=",
-             (long long)k, intr.c_str());
+    const OProc* op = eit == ei_.end() ? nullptr : &procs[eit->second.value.proc];
+    const OEl* el = op ? &op->els[eit->second.value.elem] : nullptr;
+    std::string intr, bnd;
+    if (el && (el->type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || el->type == ZBHIP_EL_BOUNDARY_EVENT)) intr = el->id;
+    if (el && el->boundary >= 0) intr = bnd = op->els[el->boundary].id;
+    snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=%d,interrupted=%d,interrupting=%s,boundaryElementIds=%s",
+             (long long)k, es_closed_.count(k) ? 0 : 1, es_interrupted_.count(k) ? 1 : 0, intr.c_str(), bnd.c_str());
     rows.push_back(buf);
   }
   for (auto& [k, t] : triggers_) {

@@ -6,7 +6,7 @@ O=${OUT:-gpurun_out/tmr}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 echo "=== timer + sub-process tests"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_timers.py tests/test_gpu_subprocess.py -x -v -m gpu --timeout 120 \
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_timers.py tests/test_gpu_subprocess.py} -x -v -m gpu --timeout 120 \
   --timeout-method thread > $O/pytest_new.log 2>&1 || { tail -80 $O/pytest_new.log; exit 1; }
 tail -3 $O/pytest_new.log
 if [[ -n "$FULL" ]]; then

@@ -1,0 +1,146 @@
+"""Interrupting timer boundary events on the gfx950 path (KScope) against the CPU oracle with the same
+clock: the boundary timer created with the task (before its job), canceled when the job completes
+first (TIMER:CANCELED with the stored dueDate), or triggered first -- TERMINATE_ELEMENT of the task,
+JOB:CANCELED, ELEMENT_TERMINATED, PROCESS_EVENT:TRIGGERED and the boundary event's activation and
+outgoing flows; each instance's open job or timer is chosen at random every round.  Records, state,
+host log bytes, zb-db bytes and restart through zb-db bytes.  Reference: BoundaryEventTest.java:48-139,
+ActivityTest.java:150-199, JobWorkerTaskProcessor.java:77-104, EventTriggerBehavior.java:191-244."""
+import pytest
+
+from test_gpu_logserial import Pair
+from test_gpu_timers import _open_work, drive_timers, part_key
+from test_oracle_boundary import multiple_sequence_flows
+from test_oracle_timers import NOW
+from zeebe_amd import abi, bpmn
+from zeebe_amd.engine import Partition
+from helpers import create_commands
+import numpy as np
+
+pytestmark = pytest.mark.gpu
+
+
+def _linear_with_boundary():
+    # a -> b, a's timer escalates to c
+    b = bpmn.createExecutableProcess("process").startEvent("s").serviceTask("a", "a").boundaryEvent("late")
+    b.timerWithDuration("PT5M").serviceTask("c", "c").endEvent("ce").moveToActivity("a").serviceTask("b", "b")
+    return b.endEvent("e").done()
+
+
+def _boundary_in_sub_process():
+    b = bpmn.createExecutableProcess("process").startEvent().parallelGateway("fork").subProcess("sub").startEvent()
+    b.serviceTask("inner", "inner").boundaryEvent("late").timerWithDuration("PT1M").endEvent("lateEnd")
+    b.moveToActivity("inner").endEvent().subProcessDone().parallelGateway("join").moveToNode("fork")
+    b.serviceTask("other", "other").connectTo("join")
+    return b.endEvent("e").done()
+
+
+def _boundary_then_catch():
+    # the boundary timer's row is reused by the catch event after the task (one timer at a time)
+    b = bpmn.createExecutableProcess("process").startEvent("s").jobWorkerTask("scriptTask", "a", "a")
+    b.boundaryEvent("late").timerWithDuration("PT2H").endEvent("le").moveToActivity("a")
+    b.intermediateCatchEvent("wait").timerWithDuration("PT1S").serviceTask("z", "z")
+    return b.endEvent("e").done()
+
+
+def _boundary_to_gateway():
+    # the boundary event leaves through a parallel gateway into two tasks
+    b = bpmn.createExecutableProcess("process").startEvent("s").serviceTask("a", "a").boundaryEvent("late")
+    b.timerWithDuration("PT10S").parallelGateway("fork").serviceTask("x", "x").parallelGateway("join")
+    b.moveToNode("fork").serviceTask("y", "y").connectTo("join").endEvent("je").moveToActivity("a")
+    return b.endEvent("e").done()
+
+
+SHAPES = {"multiple_sequence_flows": lambda: multiple_sequence_flows("PT30S"), "linear": _linear_with_boundary,
+          "in_sub_process": _boundary_in_sub_process, "then_catch": _boundary_then_catch,
+          "to_gateway": _boundary_to_gateway}
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("seed", [3, 8])
+def test_gpu_boundary_parity(shape, seed):
+    part, orc = drive_timers(SHAPES[shape](), 200, seed=seed)
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []
+
+
+def test_gpu_boundary_both_outcomes():
+    # every instance's first move: even instances complete the job, odd ones fire the timer
+    xml = multiple_sequence_flows("PT30S")
+    n = 64
+    part = Partition(max_instances=n, max_commands=n, max_records_per_batch=128)
+    from oracle.oracle import Oracle
+    from test_gpu_parity import run_both
+    orc = Oracle()
+    assert part.deploy(xml) == orc.deploy(xml) == 0
+    for e in (part, orc):
+        e.set_clock(NOW)
+    run_both(part, orc, create_commands(n, 0))
+    rows = part.state()
+    c = abi.make_commands(n)
+    for r in rows:
+        p = r.split("|")
+        if r.startswith("JOBS|"):
+            inst, ordv = part.resolve_key(int(p[1]))
+            if inst % 2 == 0:
+                c[inst]["instance"], c[inst]["kind"], c[inst]["ref"] = inst, abi.CMD_JOB_COMPLETE, ordv
+        elif r.startswith("TIMERS|"):
+            inst, ordv = part.resolve_key(int(p[2]))
+            due = int(dict(kv.split("=") for kv in p[3].split(","))["dueDate"])
+            if inst % 2 == 1:
+                c[inst]["instance"], c[inst]["kind"], c[inst]["ref"] = inst, abi.CMD_TIMER_TRIGGER, ordv
+                c[inst]["doc_begin"], c[inst]["pad"] = due & 0xFFFFFFFF, due >> 32
+    for e in (part, orc):
+        e.set_clock(NOW + 30000)
+    got = run_both(part, orc, c)
+    assert part.state() == orc.state() == [r for r in part.state() if r.startswith("KEY|")]
+    assert (got["value_type"] == abi.VT_TIMER).sum() == n  # CANCELED for even, TRIGGERED for odd
+    assert ((got["value_type"] == abi.VT_JOB) & (got["intent"] == abi.JOB_CANCELED)).sum() == n // 2
+    assert part.stats()["fallback"] == 0
+
+
+@pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch"])
+def test_gpu_boundary_log_and_db_bytes(shape):
+    pair = Pair(SHAPES[shape](), 100)
+    for e in (pair.part, pair.orc):
+        e.set_clock(NOW)
+    pair.window(create_commands(100, 0))
+    rng = np.random.default_rng(5)
+    for step in range(8):
+        c = _open_work(pair.part, rng)
+        if c is None:
+            break
+        for e in (pair.part, pair.orc):
+            e.set_clock(NOW + 1000 * (step + 1))
+        pair.window(c)
+
+
+@pytest.mark.parametrize("shape", ["linear", "in_sub_process"])
+def test_gpu_boundary_restart_equivalence(shape):
+    xml = SHAPES[shape]()
+    n = 48
+    part, orc = drive_timers(xml, n, phases=1)
+    fresh = Partition(max_instances=n, max_commands=n, max_records_per_batch=128)
+    assert fresh.deploy(xml) == 0
+    entries = part.state_db()
+    fresh.import_state_db(entries)
+    assert fresh.state() == part.state() and fresh.state_db() == entries
+    rng = np.random.default_rng(11)
+    clock = NOW + 100000
+    for _ in range(10):
+        c = _open_work(part, rng)
+        if c is None:
+            break
+        clock += 1000
+        c2 = c.copy()
+        for j, cmd in enumerate(c):
+            c2[j]["instance"], c2[j]["ref"] = fresh.resolve_key(part_key(part, int(cmd["instance"]), int(cmd["ref"])))
+        for p, cc in ((part, c), (fresh, c2)):
+            p.set_clock(clock)
+            p.submit(cc)
+            p.run()
+            p.drain()
+        orc.set_clock(clock)
+        orc.clear_records()
+        orc.submit(c)
+        orc.run()
+        assert part.state() == orc.state() == fresh.state()
+    assert [r for r in fresh.state() if not r.startswith("KEY|")] == []

@@ -1,0 +1,248 @@
+"""Interrupting timer boundary events on job worker tasks on the CPU oracle,
+pinned by the reference's BoundaryEventTest (engine/src/test/java/io/camunda/zeebe/engine/processing/
+bpmn/boundary/BoundaryEventTest.java:48-139) and ActivityTest (processing/bpmn/activity/ActivityTest.java:
+150-199, 260-280; its WITH_BOUNDARY_EVENTS model has two timers on one task, the device subset one --
+the assertions are the same per timer); the model subset shared by oracle and product compiler; the
+product's log serializer and zb-db encoder against the oracle restatements on boundary windows."""
+import numpy as np
+import pytest
+
+from helpers import create_commands
+from oracle.oracle import Oracle, OracleError
+from test_compiler import Compiled
+from test_logserial import Run
+from test_oracle_timers import BASE, NOW, _run, trigger_commands
+from zeebe_amd import abi, bpmn
+from zeebe_amd.native import ZbhipError
+
+
+def multiple_sequence_flows(duration="PT0.1S", job_type="type"):
+    """BoundaryEventTest.MULTIPLE_SEQUENCE_FLOWS (:48-60) with the static duration its expression
+    evaluates to: the boundary timer leaves through two flows, the task through one."""
+    return (bpmn.createExecutableProcess("process").startEvent().serviceTask("task", job_type).boundaryEvent("timer")
+            .cancelActivity(True).timerWithDuration(duration).endEvent("end1").moveToNode("timer").endEvent("end2")
+            .moveToActivity("task").endEvent("taskEnd").done())
+
+
+def with_boundary_event():
+    """ActivityTest.WITH_BOUNDARY_EVENTS (:49-61) with its first timer."""
+    return (bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "type").boundaryEvent("timer1")
+            .timerWithDuration("PT10S").endEvent().moveToActivity("task").endEvent("taskEnd").done())
+
+
+def _eid(o, r):
+    e = int(r["element_idx"])
+    return o.element_id(0, e) if e >= 0 else None
+
+
+def _tuple(o, r):
+    return abi.VALUE_TYPES.get(int(r["value_type"]), int(r["value_type"])), \
+        abi.intent_name(int(r["value_type"]), int(r["intent"])), _eid(o, r)
+
+
+def _between(o, recs, start, stop):
+    """RecordingExporter.records().between(task `start`, task `stop`) as (value type, intent, element)."""
+    out, on = [], False
+    for r in recs:
+        t = _tuple(o, r)
+        if t == ("PROCESS_INSTANCE", start, "task"):
+            on = True
+        if on:
+            out.append(t)
+        if on and t == ("PROCESS_INSTANCE", stop, "task"):
+            break
+    return out
+
+
+def _trigger_all(o, recs):
+    created = [r for r in recs if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CREATED]
+    return _run(o, trigger_commands([0] * len(created), [int(r["key"]) - BASE - 1 for r in created],
+                                    [int(r["aux"]) for r in created]))
+
+
+def _complete_jobs(o, recs):
+    jobs = [r for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+    c = abi.make_commands(len(jobs))
+    c["kind"] = abi.CMD_JOB_COMPLETE
+    c["ref"] = [int(r["key"]) - BASE - 1 for r in jobs]
+    return _run(o, c)
+
+
+def _started(xml):
+    o = Oracle()
+    o.set_clock(NOW)
+    o.deploy(xml)
+    return o, _run(o, create_commands(1, 0))
+
+
+def test_subscribe_on_activation():
+    # ActivityTest.shouldSubscribeToBoundaryEventTriggersOnReady (:150-180): the boundary timer is
+    # created between the task's ACTIVATING and ACTIVATED, before the job
+    o, recs = _started(with_boundary_event())
+    assert [t[1] for t in _between(o, recs, "ELEMENT_ACTIVATING", "ELEMENT_ACTIVATED")] == [
+        "ELEMENT_ACTIVATING", "CREATED", "CREATED", "ELEMENT_ACTIVATED"]
+    seq = _between(o, recs, "ELEMENT_ACTIVATING", "ELEMENT_ACTIVATED")
+    assert seq[1] == ("TIMER", "CREATED", "timer1") and seq[2] == ("JOB", "CREATED", "task")
+    timer = [r for r in recs if r["value_type"] == abi.VT_TIMER][0]
+    assert int(timer["aux"]) == NOW + 10000
+    task_key = [r for r in recs if _tuple(o, r) == ("PROCESS_INSTANCE", "ELEMENT_ACTIVATED", "task")][0]["key"]
+    assert int(timer["scope_key"]) == int(task_key)  # elementInstanceKey = the activity's instance
+    st = o.state()
+    assert "EVENT_SCOPE|%d|accepting=1,interrupted=0,interrupting=timer1,boundaryElementIds=timer1" % int(task_key) in st
+    assert any(r.startswith("TIMERS|%d|" % int(task_key)) and "handlerNodeId=timer1" in r for r in st)
+
+
+def test_unsubscribe_on_completing():
+    # ActivityTest.shouldUnsubscribeFromBoundaryEventTriggersOnCompleting (:184-199, :260-280):
+    # TIMER:CANCELED between the task's COMPLETING and COMPLETED, with the timer's key and value
+    o, recs = _started(with_boundary_event())
+    created = [r for r in recs if r["value_type"] == abi.VT_TIMER][0]
+    done = _complete_jobs(o, recs)
+    seq = _between(o, done, "ELEMENT_COMPLETING", "ELEMENT_COMPLETED")
+    assert seq[0][1] == "ELEMENT_COMPLETING" and seq[-1][1] == "ELEMENT_COMPLETED"
+    assert ("TIMER", "CANCELED", "timer1") in seq
+    canceled = [r for r in done if r["value_type"] == abi.VT_TIMER][0]
+    for f in ("key", "scope_key", "process_instance_key", "aux", "element_idx"):
+        assert canceled[f] == created[f], f
+    assert [r for r in o.state() if not r.startswith("KEY|")] == []
+    # the canceled timer can no longer be triggered (TriggerTimerProcessor.java:86-90)
+    again = _run(o, trigger_commands([0], [int(created["key"]) - BASE - 1], [int(created["aux"])]))
+    assert len(again) == 1 and again[0]["record_type"] == abi.RT_REJECTION
+    assert again[0]["rejection_type"] == abi.REJ_NOT_FOUND
+
+
+def test_activate_boundary_event_when_triggered():
+    # BoundaryEventTest.shouldActivateBoundaryEventWhenEventTriggered (:100-139): containsSubsequence
+    # TIMER TRIGGERED, task ELEMENT_TERMINATING, JOB CANCELED, task ELEMENT_TERMINATED, timer ACTIVATING
+    o, recs = _started(multiple_sequence_flows())
+    fired = _trigger_all(o, recs)
+    seq = [_tuple(o, r) for r in fired]
+    want = [("TIMER", "TRIGGERED", "timer"), ("PROCESS_INSTANCE", "ELEMENT_TERMINATING", "task"),
+            ("JOB", "CANCELED", "task"), ("PROCESS_INSTANCE", "ELEMENT_TERMINATED", "task"),
+            ("PROCESS_INSTANCE", "ELEMENT_ACTIVATING", "timer")]
+    it = iter(seq)
+    assert all(w in it for w in want), seq
+    # the full batch head (EventHandle.activateElement, JobWorkerTaskProcessor.onTerminate,
+    # EventTriggerBehavior.activateTriggeredEvent)
+    assert seq[:10] == [
+        ("TIMER", "TRIGGERED", "timer"), ("PROCESS_EVENT", "TRIGGERING", "timer"),
+        ("PROCESS_INSTANCE", "TERMINATE_ELEMENT", "task"), ("PROCESS_INSTANCE", "ELEMENT_TERMINATING", "task"),
+        ("JOB", "CANCELED", "task"), ("PROCESS_INSTANCE", "ELEMENT_TERMINATED", "task"),
+        ("PROCESS_EVENT", "TRIGGERED", "timer"), ("PROCESS_INSTANCE", "ELEMENT_ACTIVATING", "timer"),
+        ("PROCESS_INSTANCE", "ELEMENT_ACTIVATED", "timer"), ("PROCESS_INSTANCE", "COMPLETE_ELEMENT", "timer")]
+    pe = [r for r in fired if r["value_type"] == abi.VT_PROCESS_EVENT]
+    assert pe[0]["key"] == pe[1]["key"]  # TRIGGERED under the trigger's key
+    task = [r for r in fired if _tuple(o, r)[2] == "task" and r["value_type"] == abi.VT_PROCESS_INSTANCE][0]
+    act = [r for r in fired if _tuple(o, r) == ("PROCESS_INSTANCE", "ELEMENT_ACTIVATING", "timer")][0]
+    assert int(act["scope_key"]) == int(task["scope_key"])  # the boundary event's flow scope: the task's
+    assert int(act["key"]) > int(pe[0]["key"])
+
+
+def test_take_all_outgoing_sequence_flows_if_triggered():
+    # BoundaryEventTest.shouldTakeAllOutgoingSequenceFlowsIfTriggered (:75-98)
+    o, recs = _started(multiple_sequence_flows())
+    fired = _trigger_all(o, recs)
+    ends = [_eid(o, r) for r in fired if r["value_type"] == abi.VT_PROCESS_INSTANCE and
+            abi.PI_INTENTS[int(r["intent"])] == "ELEMENT_COMPLETED" and _eid(o, r) in ("end1", "end2", "taskEnd")]
+    assert sorted(ends) == ["end1", "end2"]
+    assert [r for r in o.state() if not r.startswith("KEY|")] == []
+
+
+def test_job_of_a_terminated_task_is_not_found():
+    o, recs = _started(multiple_sequence_flows())
+    _trigger_all(o, recs)
+    rej = _complete_jobs(o, recs)
+    assert len(rej) == 1 and rej[0]["record_type"] == abi.RT_REJECTION
+    assert rej[0]["rejection_type"] == abi.REJ_NOT_FOUND
+
+
+def test_boundary_in_sub_process_and_parallel_branch():
+    # the timer-or-job race inside a sub-process, next to a plain job in a parallel branch
+    b = bpmn.createExecutableProcess("process").startEvent().parallelGateway("fork").subProcess("sub").startEvent()
+    b.serviceTask("inner", "inner").boundaryEvent("late").timerWithDuration("PT1M").endEvent("lateEnd")
+    b.moveToActivity("inner").endEvent().subProcessDone().parallelGateway("join").moveToNode("fork")
+    b.serviceTask("other", "other").connectTo("join")
+    o, recs = _started(b.endEvent("e").done())
+    fired = _trigger_all(o, recs)
+    assert ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "late") in [_tuple(o, r) for r in fired]
+    _complete_jobs(o, recs)  # inner: NOT_FOUND; other: completes the join
+    assert [r for r in o.state() if not r.startswith("KEY|")] == []
+
+
+def _boundary_model(attrs="", body=None, on="serviceTask"):
+    body = body if body is not None else ('<timerEventDefinition id="t"><timeDuration>PT1S</timeDuration>'
+                                          '</timerEventDefinition>')
+    task = ('<serviceTask id="a"><extensionElements><zeebe:taskDefinition type="a"/></extensionElements></serviceTask>'
+            if on == "serviceTask" else '<task id="a"/>')
+    return ('<?xml version="1.0" encoding="UTF-8"?><definitions xmlns="http://www.omg.org/spec/BPMN/20100524/MODEL" '
+            'xmlns:zeebe="http://camunda.org/schema/zeebe/1.0" id="d" targetNamespace="x"><process id="p" '
+            'isExecutable="true"><startEvent id="s"/>%s<sequenceFlow id="f1" sourceRef="s" targetRef="a"/>'
+            '<boundaryEvent id="b" attachedToRef="a"%s>%s</boundaryEvent><endEvent id="e"/>'
+            '<sequenceFlow id="f2" sourceRef="b" targetRef="e"/></process></definitions>' % (task, attrs, body))
+
+
+def test_boundary_model_subset():
+    for xml in (_boundary_model(), multiple_sequence_flows(), with_boundary_event()):
+        Compiled(xml)
+        Oracle().deploy(xml)
+    refused = [_boundary_model(' cancelActivity="false"'),
+               _boundary_model(body='<messageEventDefinition id="m" messageRef="x"/>'),
+               _boundary_model(body='<timerEventDefinition id="t"><timeCycle>R3/PT1S</timeCycle></timerEventDefinition>'),
+               _boundary_model(on="task"),
+               (bpmn.createExecutableProcess("p").startEvent().serviceTask("a", "a").boundaryEvent("b1")
+                .timerWithDuration("PT1S").endEvent().moveToActivity("a").boundaryEvent("b2").timerWithDuration("PT2S")
+                .endEvent().moveToActivity("a").endEvent().done())]
+    for xml in refused:
+        with pytest.raises(ZbhipError):
+            Compiled(xml)
+        with pytest.raises(OracleError):
+            Oracle().deploy(xml)
+    c = Compiled(multiple_sequence_flows("PT2M"))
+    ids = [c.id(i) for i in range(len(c.els))]
+    task, timer = ids.index("task"), ids.index("timer")
+    assert int(c.els[timer]["element_type"]) == abi.ELEMENT_TYPES.index("BOUNDARY_EVENT")
+    assert int(c.els[timer]["flow_source"]) == task and int(c.els[task]["start_event"]) == timer
+    assert int(c.els[timer]["duration_ms"]) == 120000
+
+
+def test_product_serializer_and_state_encoder_on_boundary_records():
+    # the product's host log serializer and zb-db encoder (+ decoder) over the CPU engine's boundary
+    # windows equal the oracle restatements byte for byte: TIMER:CREATED / CANCELED / TRIGGERED,
+    # JOB:CANCELED, PROCESS_EVENT:TRIGGERED, TERMINATE_ELEMENT / ELEMENT_TERMINATING / TERMINATED,
+    # EVENT_SCOPE rows with boundary ids
+    from oracle import statedb as SD
+    from test_statedb import _check_state
+    run = Run([multiple_sequence_flows("PT30S")])
+    run.orc.set_clock(NOW)
+    recs = run.window(create_commands(6, 0))
+    encoded = _check_state(run)
+    assert {SD.CF["TIMERS"], SD.CF["EVENT_SCOPE"]} <= encoded
+    entries = run.ser.encode_state_rows(run.orc.state())
+    assert sorted(run.ser.decode_state_entries(entries)) == sorted(
+        r for r in run.orc.state() if r.split("|")[0] in SD.CF)
+    # instances 0..2: the job completes (TIMER:CANCELED); 3..5: the timer fires (termination)
+    jobs = [r for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+    timers = [r for r in recs if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CREATED]
+    c = abi.make_commands(6)
+    for i in range(6):
+        c[i]["instance"] = i
+        if i < 3:
+            c[i]["kind"], c[i]["ref"] = abi.CMD_JOB_COMPLETE, _ord(run.orc, i, int(jobs[i]["key"]))
+        else:
+            due = int(timers[i]["aux"])
+            c[i]["kind"], c[i]["ref"] = abi.CMD_TIMER_TRIGGER, _ord(run.orc, i, int(timers[i]["key"]))
+            c[i]["doc_begin"], c[i]["pad"] = due & 0xFFFFFFFF, due >> 32
+    run.orc.set_clock(NOW + 30000)
+    out = run.window(c)
+    kinds = {(int(r["value_type"]), int(r["intent"])) for r in out}
+    assert {(abi.VT_TIMER, abi.TIMER_CANCELED), (abi.VT_JOB, abi.JOB_CANCELED),
+            (abi.VT_PROCESS_EVENT, abi.PE_TRIGGERED)} <= kinds
+    _check_state(run)
+    assert [r for r in run.orc.state() if not r.startswith("KEY|")] == []
+
+
+def _ord(o, instance, key):
+    for i in range(64):
+        if o.resolve(instance, i) == key:
+            return i
+    raise KeyError(key)

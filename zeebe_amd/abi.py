@@ -29,13 +29,14 @@ PI_INTENTS = {
     7: "ELEMENT_TERMINATED", 8: "ACTIVATE_ELEMENT", 9: "COMPLETE_ELEMENT", 10: "TERMINATE_ELEMENT",
 }
 PI_INTENT_IDS = {v: k for k, v in PI_INTENTS.items()}
-JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED"}
-JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED = 0, 1, 2
+JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED", 10: "CANCELED"}
+JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED, JOB_CANCELED = 0, 1, 2, 10
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
 PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
 PIC_INTENTS = {0: "CREATE", 1: "CREATED"}
 TIMER_INTENTS = {0: "CREATED", 1: "TRIGGER", 2: "TRIGGERED", 3: "CANCEL", 4: "CANCELED"}
-TIMER_CREATED, TIMER_TRIGGER, TIMER_TRIGGERED = 0, 1, 2
+TIMER_CREATED, TIMER_TRIGGER, TIMER_TRIGGERED, TIMER_CANCELED = 0, 1, 2, 4
+PE_TRIGGERING, PE_TRIGGERED = 0, 1
 # MessageIntent / MessageSubscriptionIntent / ProcessMessageSubscriptionIntent
 MSG_INTENTS = {0: "PUBLISH", 1: "PUBLISHED", 2: "EXPIRE", 3: "EXPIRED"}
 MS_INTENTS = {0: "CREATE", 1: "CREATED", 2: "CORRELATE", 3: "CORRELATED", 4: "REJECT", 5: "REJECTED",

@@ -27,6 +27,8 @@ class _Node:
         self.target = None
         self.message = None  # (message id, name, correlation key expression) of a message catch event
         self.timer = None    # timeDuration of a timer catch event
+        self.attached_to = None     # boundary event: the activity it is attached to
+        self.cancel_activity = True  # boundary event: interrupting (BoundaryEvent default)
 
 
 class ProcessBuilder:
@@ -138,6 +140,28 @@ class ProcessBuilder:
         self._pending_flow = None
         return self
 
+    def boundaryEvent(self, id_=None):
+        """AbstractActivityBuilder.boundaryEvent(id): a boundaryEvent sibling of the current activity
+        appended to its container (no connecting flow), attachedToRef = the activity; the builder
+        continues from the boundary event."""
+        activity = self.current
+        id_ = id_ or self._gen_id("boundaryEvent")
+        n = _Node("boundaryEvent", id_)
+        n.attached_to = activity.id
+        self.children.append(n)
+        self.nodes[id_] = n
+        self._container_of[id_] = self.children
+        self.current = n
+        self._pending_flow = None
+        return self
+
+    def cancelActivity(self, cancel):
+        self.current.cancel_activity = bool(cancel)
+        return self
+
+    def moveToActivity(self, id_):
+        return self.moveToNode(id_)
+
     def timerWithDuration(self, duration):
         """IntermediateCatchEventBuilder.timerWithDuration: <timerEventDefinition><timeDuration>."""
         self.current.timer = duration
@@ -229,6 +253,14 @@ class ProcessBuilder:
                     out.append('%s<intermediateCatchEvent id=%s><timerEventDefinition id=%s><timeDuration>%s'
                                '</timeDuration></timerEventDefinition></intermediateCatchEvent>'
                                % (ind, quoteattr(c.id), quoteattr(c.id + "_ted"), escape(c.timer)))
+                elif c.kind == "boundaryEvent":
+                    cancel = "" if c.cancel_activity else ' cancelActivity="false"'
+                    body = ""
+                    if c.timer:
+                        body = ('<timerEventDefinition id=%s><timeDuration>%s</timeDuration></timerEventDefinition>'
+                                % (quoteattr(c.id + "_ted"), escape(c.timer)))
+                    out.append('%s<boundaryEvent id=%s attachedToRef=%s%s>%s</boundaryEvent>'
+                               % (ind, quoteattr(c.id), quoteattr(c.attached_to), cancel, body))
                 elif c.kind == "exclusiveGateway" and c.default:
                     out.append("%s<exclusiveGateway id=%s default=%s/>" % (ind, quoteattr(c.id), quoteattr(c.default.id)))
                 elif c.kind == "subProcess":

@@ -452,6 +452,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
   std::vector<const Elem*> flows;
   std::vector<std::vector<uint16_t>> out_lists, in_lists;
   std::vector<const Elem*> xgws;
+  std::vector<std::pair<uint16_t, std::string>> boundaries;  // (boundary event, attachedToRef)
 
   // Elements in document pre-order: an embedded sub-process, then its children, then its next
   // sibling (the oracle numbers them the same way).  Every sequence flow connects two nodes of one
@@ -473,6 +474,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       else if (c.tag == "task") type = ZBHIP_EL_TASK;
       else if (c.tag == "manualTask") type = ZBHIP_EL_MANUAL_TASK;
       else if (c.tag == "subProcess") type = ZBHIP_EL_SUB_PROCESS;
+      else if (c.tag == "boundaryEvent") type = ZBHIP_EL_BOUNDARY_EVENT;
       else if (c.tag == "extensionElements" || c.tag == "documentation" || c.tag == "textAnnotation" ||
                c.tag == "association" || c.tag == "incoming" || c.tag == "outgoing")
         continue;
@@ -513,6 +515,26 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         }
         if (const Elem* ext = c.first("extensionElements"))
           if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+      }
+      if (type == ZBHIP_EL_BOUNDARY_EVENT) {
+        // BoundaryEventTransformer: interrupting timer boundary events (a static timeDuration) on
+        // job worker tasks; attached after the walk
+        const std::string* ca = c.get("cancelActivity");
+        if (ca && *ca == "false") { err = "non-interrupting boundary event outside the supported subset"; return ZBHIP_EUNSUPP; }
+        const Elem* ted = c.first("timerEventDefinition");
+        const Elem* td = ted ? ted->first("timeDuration") : nullptr;
+        for (auto& d : c.children)
+          if (&d != ted && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) td = nullptr;
+        if (!td) { err = "boundary event outside the supported subset (timer timeDuration only)"; return ZBHIP_EUNSUPP; }
+        const int64_t ms = duration_ms(td->text);
+        if (ms < 0 || ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return ZBHIP_EUNSUPP; }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        const std::string* at = c.get("attachedToRef");
+        if (!at) { err = "boundary event without attachedToRef"; return ZBHIP_EPARSE; }
+        e.event_type = ZBHIP_EV_TIMER;
+        e.duration_ms = (uint32_t)ms;
+        boundaries.push_back({(uint16_t)C.elements.size(), *at});
       }
       if (type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && c.first("timerEventDefinition")) {
         // CatchEventTransformer.transformTimerEventDefinition: a static timeDuration only
@@ -586,6 +608,20 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     return ZBHIP_OK;
   };
   if (int rc = container(*proc, 0)) return rc;
+  // ExecutableActivity.attach (ExecutableActivity.java:28-38): one boundary event per job worker
+  // task of the same container
+  for (auto& [b, ref] : boundaries) {
+    auto it = index.find(ref);
+    if (it == index.end()) { err = "boundary event attached to an unknown element " + ref; return ZBHIP_EPARSE; }
+    zbhip_element& A = C.elements[it->second];
+    if (!ZBHIP_IS_JOB_WORKER(A.element_type) || A.flow_scope != C.elements[b].flow_scope) {
+      err = "boundary event on an element outside the supported subset (job worker tasks only)";
+      return ZBHIP_EUNSUPP;
+    }
+    if (A.start_event != ZBHIP_NONE16) { err = "more than one boundary event on an activity outside the supported subset"; return ZBHIP_EUNSUPP; }
+    A.start_event = b;
+    C.elements[b].flow_source = it->second;
+  }
   for (size_t e = 1; e < C.elements.size(); ++e)
     if (C.elements[e].element_type == ZBHIP_EL_SUB_PROCESS && C.elements[e].start_event == ZBHIP_NONE16) {
       err = "sub-process without a none start event";

@@ -129,6 +129,7 @@ struct Lane {
   uint16_t next_ord;
   uint16_t first_ord;
   uint16_t trig_key;    // event trigger of a completed job (EVENT_TRIGGER row), NONE if none
+  uint16_t trig_evt;    // K::S: the PROCESS_EVENT key ordinal of a boundary event's trigger on trig_key
   bool pi_live;
   uint8_t pi_state;
   int pi_child;
@@ -334,7 +335,9 @@ __device__ __forceinline__ void qput(Lane<K>& L, int i, uint32_t v) {
   }
 }
 
-// queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | key << 16
+// queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | (K::M local command) << 14 |
+// terminate (K::S TERMINATE_ELEMENT) << 15 | key << 16
+constexpr uint32_t Q_TERM = 1u << 15;
 __device__ __forceinline__ uint32_t qentry(uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
   return elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
 }
@@ -397,10 +400,10 @@ __device__ __forceinline__ void overflow(Lane<K>& L, uint32_t entry) {
 // a follow-up command of the batch: its COMMAND record, then the FIFO (or the overflow list)
 template <class K>
 __device__ __forceinline__ void follow_up(Lane<K>& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
-                                          bool complete, bool fs_pi, uint32_t qkey) {
+                                          bool complete, bool fs_pi, uint32_t qkey, uint32_t qflags = 0) {
   const bool admit = pending(L) + L.processed + 1 < L.limit;
   emit(L, code, key, aux, elem, admit ? 0u : F_UNPROCESSED);
-  const uint32_t entry = qentry(elem, complete, fs_pi, qkey);
+  const uint32_t entry = qentry(elem, complete, fs_pi, qkey) | qflags;
   if (admit) enqueue(L, entry);
   else overflow(L, entry);
 }
@@ -697,7 +700,8 @@ __device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem
     if (t < 0) return;
     if (type == ZBHIP_EL_SUB_PROCESS)  // jobKey 0; no children, no active flows yet
       tput(L, t, make_uint2(elem | (key << 16), (uint32_t)ZBHIP_PI_ELEMENT_ACTIVATING << 16));
-    const int da = type == ZBHIP_EL_START_EVENT ? 0 : type == ZBHIP_EL_PARALLEL_GATEWAY ? -(int)(w.x >> 16) : -1;
+    const int da = type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_BOUNDARY_EVENT ? 0
+                   : type == ZBHIP_EL_PARALLEL_GATEWAY ? -(int)(w.x >> 16) : -1;
     scope_adjust(L, scope_of<K>(w), 1, da);
     return;
   }
@@ -1104,8 +1108,75 @@ __device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord) {
   const uint32_t pe = new_key(L);
   emit(L, C_PE_TRIGGERING, pe, eord, elem);
   L.trig_key = (uint16_t)eord;  // ProcessEventTriggeringApplier: EVENT_TRIGGER row (no variables)
+  if (etype(elem_of(L, elem)) == ZBHIP_EL_BOUNDARY_EVENT) {
+    // an interrupting boundary event: TERMINATE_ELEMENT of the activity it is attached to (the
+    // activation of the boundary event follows its termination, terminate_pi); the trigger's
+    // PROCESS_EVENT key travels with the EVENT_TRIGGER row.  Past the batch limit the command
+    // would be written unprocessed with that context: outside the device subset.
+    if (pending(L) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
+    L.trig_evt = (uint16_t)pe;
+    const uint32_t task = tget(L, t).x & 0xFFFF;
+    const uint32_t c = scope_of<K>(elem_of(L, task));
+    follow_up(L, ZBHIP_PI_TERMINATE_ELEMENT, eord, scope_key(L, c), task, false, c == 0, eord, Q_TERM);
+    return;
+  }
   const uint32_t c = scope_of<K>(elem_of(L, elem));
   follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, eord, scope_key(L, c), elem, true, c == 0, eord);
+}
+
+// CatchEventBehavior.unsubscribeFromTimerEvent (processing/common/CatchEventBehavior.java:380-392):
+// TIMER:CANCELED with the timer's key and stored value (its dueDate goes to the command's cmd_due
+// entry: at most one timer is canceled per batch); TimerCancelledApplier removes the row
+template <class K>
+__device__ __forceinline__ void cancel_timer(Lane<K>& L) {
+  emit(L, C_TIMER_CANCELED, L.tm_x >> 16, L.tm_y & 0xFFFF, L.tm_x & 0xFFF);
+  L.sp->cmd_due[L.ci] = L.tm_due;
+  L.tm_x = L.tm_y = 0;
+  L.tm_due = 0;
+}
+
+// TERMINATE_ELEMENT of a job worker task whose interrupting boundary event was triggered:
+// ProcessInstanceStateTransitionGuard (:60-64), transitionToTerminating, then
+// JobWorkerTaskProcessor.onTerminate (task/JobWorkerTaskProcessor.java:77-104): cancelJob
+// (JOB:CANCELED, BpmnJobBehavior.java:251-274), unsubscribeFromEvents, findEventTrigger ->
+// transitionToTerminated (ProcessInstanceElementTerminatedApplier: the instance removed like a
+// completed one) and EventTriggerBehavior.activateTriggeredEvent (EventTriggerBehavior.java:191-244):
+// PROCESS_EVENT:TRIGGERED, the boundary event ACTIVATING + ACTIVATED (+key, flow scope = the
+// activity's), COMPLETE_ELEMENT
+template <class K>
+__device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w, uint32_t key, uint32_t fsa) {
+  const int t = tbl_find(L, key);
+  const uint32_t st = t < 0 ? 0u : (tget(L, t).y >> 16) & 0xFF;
+  if (t < 0 || !ZBHIP_IS_JOB_WORKER(etype(w)) ||
+      (st != ZBHIP_PI_ELEMENT_ACTIVATING && st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING)) {
+    set_fail(L, FB_UNSUPPORTED);
+    return;
+  }
+  emit(L, ZBHIP_PI_ELEMENT_TERMINATING, key, fsa, elem);
+  tbl_set_state(L, t, ZBHIP_PI_ELEMENT_TERMINATING);
+  const uint2 e = tget(L, t);
+  const uint32_t job = e.y & 0xFFFF;
+  if (((e.y >> 24) & 1u) && job != JOB_ZERO && job != JOB_MINUS1) emit(L, C_JOB_CANCELED, job, key, elem);
+  if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == key) cancel_timer(L);
+  const uint32_t c = scope_of<K>(w);
+  const uint32_t fst = c == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, c)).y >> 16) & 0xFF;
+  const uint32_t target = w.w & 0xFFFF;  // the activity's boundary event
+  if (L.trig_key != key || L.trig_evt == NONE || fst != ZBHIP_PI_ELEMENT_ACTIVATED || target == 0xFFFF) {
+    set_fail(L, FB_UNSUPPORTED);  // a termination without an event trigger (onElementTerminated)
+    return;
+  }
+  const uint32_t pe = L.trig_evt;
+  emit(L, ZBHIP_PI_ELEMENT_TERMINATED, key, fsa, elem);
+  apply_completed_child(L, t, key);  // removeInstance; the event scope with its trigger
+  L.trig_evt = NONE;
+  emit(L, C_PE_TRIGGERED, pe, key, target);
+  const uint32_t bk = new_key(L);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, bk, fsa, target);
+  apply_activating_child(L, target, elem_of(L, target), bk);
+  if (L.fail) return;
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, bk, fsa, target);
+  tbl_set_state(L, tbl_find(L, bk), ZBHIP_PI_ELEMENT_ACTIVATED);
+  follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, bk, fsa, target, true, true, bk);
 }
 
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
@@ -1133,6 +1204,10 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       fsa = scope_key(L, c);  // a container without an instance (never in the subset): fallback
       if (L.fail) return;
       raux = fsa;
+    }
+    if (entry & Q_TERM) {
+      terminate_pi(L, elem, w, cmd_key, fsa);
+      return;
     }
   }
 
@@ -1195,6 +1270,19 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       case ZBHIP_EL_SEND_TASK:     // send / script / business-rule tasks (BpmnElementProcessors.java:46-60)
       case ZBHIP_EL_SCRIPT_TASK:
       case ZBHIP_EL_BUSINESS_RULE_TASK: {
+        if constexpr (K::S) {
+          // eventSubscriptionBehavior.subscribeToEvents: the attached boundary event's timer
+          // (CatchEventBehavior.subscribeToTimerEvent) before the job; one timer per instance
+          const uint32_t b = w.w & 0xFFFF;
+          if (b != 0xFFFF) {
+            if (!L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
+            const uint32_t tk = new_key(L);
+            L.tm_x = b | (tk << 16);
+            L.tm_y = key | (1u << 31);
+            L.tm_due = L.sp->now_ms + (long long)elem_of(L, b).z;
+            emit(L, C_TIMER_CREATED, tk, key, b);
+          }
+        }
         uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
         emit(L, C_JOB_CREATED, job, key, elem);
         uint2 e = tget(L, t);   // JobCreatedApplier: element instance jobKey
@@ -1310,13 +1398,18 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     // would be canceled (TIMER:CANCELED, outside the subset)
     if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) { set_fail(L, FB_UNSUPPORTED); return; }
   } else if (type != ZBHIP_EL_START_EVENT && !ZBHIP_IS_JOB_WORKER(type) && !pass_through(type) &&
-             !(K::S && type == ZBHIP_EL_SUB_PROCESS)) {
-    // SubProcessProcessor.onComplete (:68-82): no output mappings or subscriptions in the subset
+             !(K::S && (type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_BOUNDARY_EVENT))) {
+    // SubProcessProcessor.onComplete (:68-82): no output mappings or subscriptions in the subset;
+    // BoundaryEventProcessor.onComplete (event/BoundaryEventProcessor.java:47-56): no mappings
     set_fail(L, FB_UNSUPPORTED);
     return;
   }
   // applyOutputMappings (BpmnVariableMappingBehavior.java:86-156): event-trigger variables
   if (L.trig_key == cmd_key) merge_document_from(L, cmd_key, L.doc_begin, L.doc_count);
+  if constexpr (K::S) {
+    // JobWorkerTaskProcessor.onComplete (:63-75): unsubscribeFromEvents -- the boundary event's timer
+    if (ZBHIP_IS_JOB_WORKER(type) && (L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) cancel_timer(L);
+  }
   transition_to_completed_child(L, t, elem, w, cmd_key);
   take_outgoing(L, w);
 }
@@ -1790,6 +1883,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.sp = &P;
   L.nt = 0;
   L.trig_key = NONE;
+  L.trig_evt = NONE;
   L.docs = P.docs;
   L.doc_begin = doc_begin;
   L.doc_count = doc_count;

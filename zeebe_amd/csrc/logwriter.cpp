@@ -431,7 +431,8 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         mp_map(value, 6);  // ProcessEventRecord.java:37-42
         key(value, "scopeKey"); mp_int(value, r.scope_key);
         key(value, "targetElementId"); mp_str(value, E->id);
-        key(value, "variables"); mp_bin(value, src_doc);
+        // TRIGGERED: EventTriggerBehavior.processEventTriggered resets the record (no variables)
+        key(value, "variables"); mp_bin(value, r.intent == ZBHIP_PE_TRIGGERED ? kEmptyDoc : src_doc);
         key(value, "processDefinitionKey"); mp_int(value, P->def_key);
         key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
         key(value, "tenantId"); key(value, kTenant);

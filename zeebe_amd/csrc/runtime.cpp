@@ -297,6 +297,8 @@ struct zbhip_handle {
   std::vector<zbhip_xpart_cmd> h_xparts;
   size_t n_xparts = 0;
   uint4* d_cmd_hdr2 = nullptr;
+  long long* d_cmd_due = nullptr;       // (KScope) dueDate of the timer each batch canceled
+  std::vector<long long> h_cmd_due;
   zbhip_xpart_cmd* d_xout = nullptr;
   zbhip_xpart_cmd* d_xbucket = nullptr;
   uint32_t* d_blk_cnt = nullptr;
@@ -410,7 +412,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
        dalloc(&h->d_region_lanes, (size_t)h->regions_cap * 128) == hipSuccess &&
        dalloc(&h->d_region_off, h->regions_cap) == hipSuccess;
   // timer rows (KScope timer catch events): one per instance
-  ok = ok && dalloc(&h->st.tmr, N) == hipSuccess;
+  ok = ok && dalloc(&h->st.tmr, N) == hipSuccess && dalloc(&h->d_cmd_due, cfg->max_commands) == hipSuccess;
   // message correlation state (config 5): PROCESS_SUBSCRIPTION rows per instance, correlation slots
   const size_t S = cfg->max_correlation_keys;
   h->st.n_slots = (uint32_t)S;
@@ -481,6 +483,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_stats);
   (void)hipFree(h->st.pms);
   (void)hipFree(h->st.tmr);
+  (void)hipFree(h->d_cmd_due);
   (void)hipFree(h->st.pi_key);
   (void)hipFree(h->st.slot_hdr);
   (void)hipFree(h->st.sub_a);
@@ -667,13 +670,13 @@ static int rebuild_program(zbhip_handle* h) {
       const zbhip_element& E = P.els[e];
       uint32_t sg = 0;
       if ((E.element_type == ZBHIP_EL_START_EVENT || ZBHIP_IS_JOB_WORKER(E.element_type)) && E.out_count == 1 &&
-          E.flow_scope == 0) {
+          E.flow_scope == 0 && !(ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16)) {
         const uint32_t f = P.out[E.out_begin];
         const zbhip_element& F = P.els[f];
         const uint32_t n = F.flow_target;
         if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.condition == ZBHIP_NONE16 && n < n_el && f < 0xFFF && n < 0xFFF) {
           const zbhip_element& N = P.els[n];
-          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type);
+          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && N.start_event == ZBHIP_NONE16;
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
           if (task || end)
             sg = (1u << 31) | (ZBHIP_IS_JOB_WORKER(E.element_type) ? 1u << 30 : 0u) | (end ? 1u << 24 : 0u) |
@@ -698,13 +701,15 @@ static int rebuild_program(zbhip_handle* h) {
       if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW) w[2] = E.flow_target | ((uint32_t)E.condition << 16);
       else if (E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY) w[2] = E.default_flow | (0xFFFFu << 16);
       else if (ZBHIP_IS_JOB_WORKER(E.element_type)) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
-      else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && E.event_type == ZBHIP_EV_TIMER)
+      else if ((E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && E.event_type == ZBHIP_EV_TIMER) ||
+               E.element_type == ZBHIP_EL_BOUNDARY_EVENT)
         w[2] = E.duration_ms;
       else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
         w[2] = E.message_name | ((uint32_t)E.correlation_var << 16);  // name ids (zbhip_deploy)
       else if (E.element_type == ZBHIP_EL_SUB_PROCESS) w[2] = E.start_event | (join_mask[e] << 16);
       else w[2] = 0xFFFFFFFFu;
-      w[3] = E.join_slot | ((uint32_t)E.flow_scope << 16);
+      // a job worker's join_slot half: its boundary event (zbhip_element.start_event), 0xFFFF if none
+      w[3] = (ZBHIP_IS_JOB_WORKER(E.element_type) ? E.start_event : E.join_slot) | ((uint32_t)E.flow_scope << 16);
     }
     uint16_t* outw = reinterpret_cast<uint16_t*>(pb + out_off);
     for (size_t i = 0; i < P.out.size(); ++i) outw[i] = P.out[i];
@@ -761,8 +766,20 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         e.element_type != ZBHIP_EL_END_EVENT && !ZBHIP_IS_JOB_WORKER(e.element_type) &&
         e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
         e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT &&
-        e.element_type != ZBHIP_EL_SUB_PROCESS && !pass_through(e.element_type))
+        e.element_type != ZBHIP_EL_SUB_PROCESS && e.element_type != ZBHIP_EL_BOUNDARY_EVENT &&
+        !pass_through(e.element_type))
       return ZBHIP_EUNSUPP;
+  // interrupting timer boundary events: one per job worker task, in the task's container
+  for (size_t e = 0; e < P.els.size(); ++e) {
+    const zbhip_element& E = P.els[e];
+    if (E.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
+      if (E.event_type != ZBHIP_EV_TIMER || E.flow_source >= P.els.size()) return ZBHIP_EUNSUPP;
+      const zbhip_element& A = P.els[E.flow_source];
+      if (!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e || A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
+    } else if (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) {
+      if (E.start_event >= P.els.size() || P.els[E.start_event].element_type != ZBHIP_EL_BOUNDARY_EVENT) return ZBHIP_EINVAL;
+    }
+  }
   for (size_t e = 0; e < P.els.size(); ++e) {  // containers: a sub-process element, before its children
     const zbhip_element& E = P.els[e];
     if (e > 0 && (E.flow_scope >= e || (E.flow_scope && P.els[E.flow_scope].element_type != ZBHIP_EL_SUB_PROCESS)))
@@ -772,7 +789,8 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       return ZBHIP_EINVAL;
   }
   for (auto& e : P.els)
-    if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && e.event_type == ZBHIP_EV_TIMER) {
+    if ((e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && e.event_type == ZBHIP_EV_TIMER) ||
+        e.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
       P.has_timer = true;
     } else if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
       if (!h->st.n_slots) return ZBHIP_EUNSUPP;  // the handle was opened without message state
@@ -1116,7 +1134,9 @@ static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
       i += kPayloadRows;
       continue;
     }
-    if (((w.y >> 16) & kRejectBit) || (code != C_JOB_CREATED && code != C_JOB_COMPLETED) || elem >= P.els.size()) continue;
+    if (((w.y >> 16) & kRejectBit) || (code != C_JOB_CREATED && code != C_JOB_COMPLETED && code != C_JOB_CANCELED) ||
+        elem >= P.els.size())
+      continue;
     const uint32_t tid = P.job_type_id[elem];
     const int64_t key = h->key_of(inst, w.x & 0xFFFF);
     if (code == C_JOB_CREATED) {
@@ -1309,6 +1329,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
   P.stamp = h->window_stamp;
   P.now_ms = h->clock_ms;
+  P.cmd_due = h->d_cmd_due;
   h->run_clock_ms = h->clock_ms;
   P.tpl = (h->variant == 0 || h->variant == 1 || h->variant == 4) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
   if (h->msg()) {
@@ -1493,6 +1514,10 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   h->h_hdr.resize(n);
   if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
   h->h_hdr2.assign(n, make_uint4(0, 0, 0, 0));
+  if (n && h->variant == 4) {  // dueDates of canceled timers (TIMER:CANCELED values)
+    h->h_cmd_due.resize(n);
+    HIPCHK(hipMemcpyAsync(h->h_cmd_due.data(), h->d_cmd_due, n * sizeof(long long), hipMemcpyDeviceToHost, h->stream));
+  }
   if (n && h->msg())
     HIPCHK(hipMemcpyAsync(h->h_hdr2.data(), h->d_cmd_hdr2, n * sizeof(uint4), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(launch_gather(h->d_regions, h->d_region_total, h->d_region_lanes, region, h->d_region_off,
@@ -1632,11 +1657,12 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.intent = (uint8_t)c6;
       r.record_type = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
       r.unprocessed = !rej && c6 >= 8 && (fl & F_UNPROCESSED) ? 1 : 0;
-    } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE) {
+    } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE || c6 == C_JOB_CANCELED) {
       r.value_type = ZBHIP_VT_JOB;
-      r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED : ZBHIP_JOB_COMPLETE;
+      r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED
+                 : c6 == C_JOB_CANCELED ? ZBHIP_JOB_CANCELED : ZBHIP_JOB_COMPLETE;
       r.record_type = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
-      if (c6 != C_JOB_CREATED) r.aux = doc;
+      if (c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE) r.aux = doc;
     } else if (c6 == C_VAR_CREATED || c6 == C_VAR_UPDATED) {
       r.value_type = ZBHIP_VT_VARIABLE;
       r.intent = c6 == C_VAR_CREATED ? ZBHIP_VAR_CREATED : ZBHIP_VAR_UPDATED;
@@ -1644,16 +1670,22 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       // the value comes from the batch's source document entry of that name
       for (uint32_t j = 0; j < cm.doc_count; ++j)
         if (h->h_docs[cm.doc_begin + j].name_id == elem) r.aux = h->doc_base + cm.doc_begin + j;
-    } else if (c6 == C_PE_TRIGGERING) {
+    } else if (c6 == C_PE_TRIGGERING || c6 == C_PE_TRIGGERED) {
       r.value_type = ZBHIP_VT_PROCESS_EVENT;
-      r.intent = ZBHIP_PE_TRIGGERING;
+      r.intent = c6 == C_PE_TRIGGERING ? ZBHIP_PE_TRIGGERING : ZBHIP_PE_TRIGGERED;
       r.record_type = ZBHIP_RT_EVENT;
-      r.aux = doc;
+      r.aux = c6 == C_PE_TRIGGERING ? doc : -1;
     } else if (c6 == C_PIC_CREATED) {
       r.value_type = ZBHIP_VT_PROCESS_INSTANCE_CREATION;
       r.intent = ZBHIP_PIC_CREATED;
       r.record_type = ZBHIP_RT_EVENT;
       r.aux = doc;
+    } else if (c6 == C_TIMER_CANCELED) {
+      // CatchEventBehavior.unsubscribeFromTimerEvent: the stored timer's dueDate (cmd_due)
+      r.value_type = ZBHIP_VT_TIMER;
+      r.intent = ZBHIP_TIMER_CANCELED;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.aux = c < h->h_cmd_due.size() ? h->h_cmd_due[c] : -1;
     } else if (c6 == C_TIMER_CREATED || c6 == C_TIMER_TRIGGERED || c6 == C_TIMER_TRIGGER) {
       // TimerRecord: elementInstanceKey (scope_key), dueDate in aux -- CREATED: the run's clock plus
       // the element's duration (CatchEventBehavior.java:310); TRIGGERED / a rejected TRIGGER: the
@@ -2073,12 +2105,16 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     sink(ctx, buf);
     snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, fs);
     sink(ctx, buf);
-    if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
-      // EventScopeInstance.java:25-35: a catch event's interrupting ids are its own id
-      // (ExecutableCatchEventElement.java:124-127), a job worker's those of its interrupting
-      // boundary events (none in the subset)
-      snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=", k,
-               E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ? P.id(elem).c_str() : "");
+    if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
+        E.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
+      // EventScopeInstance.java:25-35: a catch / boundary event's interrupting ids are its own id
+      // (ExecutableCatchEventElement.java:124-132), a job worker's those of its interrupting
+      // boundary event, which is also its boundaryElementIds (ExecutableActivity.java:28-38)
+      const bool own = E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT;
+      const bool bnd = ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16;
+      const std::string ids = own ? P.id(elem) : bnd ? P.id(E.start_event) : std::string();
+      snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=%s", k,
+               ids.c_str(), bnd ? ids.c_str() : "");
       sink(ctx, buf);
     }
     if (job_row) {

@@ -56,9 +56,11 @@ enum : uint8_t {
   C_JOB_CREATED = 16,
   C_JOB_COMPLETED = 17,
   C_JOB_COMPLETE = 18,
+  C_JOB_CANCELED = 19,    // BpmnJobBehavior.cancelJob (JOB:CANCELED, the stored job)
   C_VAR_CREATED = 20,
   C_VAR_UPDATED = 21,
   C_PE_TRIGGERING = 24,
+  C_PE_TRIGGERED = 25,    // EventTriggerBehavior.processEventTriggered
   C_PIC_CREATED = 28,
   C_PMS_CREATING = 32,
   C_PMS_CREATE = 33,
@@ -75,6 +77,7 @@ enum : uint8_t {
   C_TIMER_CREATED = 52,   // key = timer, aux = element instance (TimerRecord, CatchEventBehavior.java:303-330)
   C_TIMER_TRIGGER = 53,   // (rejections of TIMER:TRIGGER)
   C_TIMER_TRIGGERED = 54,
+  C_TIMER_CANCELED = 55,  // CatchEventBehavior.unsubscribeFromTimerEvent; dueDate in StepParams.cmd_due
   kRejectBit = 0x40,
 };
 
@@ -122,9 +125,11 @@ constexpr uint8_t CMD_FOLLOWUP = 0x20;
 //   p[8 + 4e .. ] element e: w0 = type | event << 8 | in_count << 16
 //                            w1 = out_begin | out_count << 16
 //                            w2 = flow: target | condition << 16; xgw: default_flow; task: job_type | retries << 16;
-//                                 message catch: name | correlation variable << 16; timer catch: duration ms;
-//                                 sub-process: none start event | join slots of its gateways << 16
-//                            w3 = join_slot | container (flow scope element; 0 = the process) << 16
+//                                 message catch: name | correlation variable << 16; timer catch / boundary
+//                                 event: duration ms; sub-process: none start event | join slots of its
+//                                 gateways << 16
+//                            w3 = join_slot (job worker: its boundary event or 0xFFFF) | container
+//                                 (flow scope element; 0 = the process) << 16
 //   p[out_off]  u16 outgoing flows (two per word)
 //   p[cond_off] u32 first instruction of each condition
 //   p[code_off] instructions (16-byte aligned): op, arg, literal_lo, literal_hi
@@ -150,8 +155,9 @@ struct DevState {
   longlong2* sub_b;  // [kSubs][S] x = element instance key, y = process instance key (real)
   longlong2* sub_k;  // [kSubs][S] x = subscription key, y = message key while correlating (-1 else)
   uint32_t n_slots;
-  uint4* tmr;        // [n] the instance's timer (KScope; one per instance): x = catch element | timer key
-                     //     ordinal << 16, y = element-instance ordinal | live << 31, z/w = dueDate lo/hi
+  uint4* tmr;        // [n] the instance's timer (KScope; one per instance): x = catch / boundary element |
+                     //     timer key ordinal << 16, y = element-instance ordinal (the catch event's, or the
+                     //     activity's a boundary event is attached to) | live << 31, z/w = dueDate lo/hi
 };
 
 // elements without behaviour: ACTIVATING, ACTIVATED, COMPLETE_ELEMENT, COMPLETING, COMPLETED, then
@@ -207,6 +213,7 @@ struct StepParams {
   uint2* tpl;
   uint32_t launch_seq;
   long long now_ms;           // zbhip_set_clock: ActorClock.currentTimeMillis() of this window
+  long long* cmd_due;         // [n_cmds] (KScope) dueDate of the timer a batch canceled (at most one)
 };
 
 // ---- log bytes on the device (logdev.hip) ----
