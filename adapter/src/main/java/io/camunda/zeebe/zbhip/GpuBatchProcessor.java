@@ -20,10 +20,13 @@ import io.camunda.zeebe.logstreams.log.LoggedEvent;
 import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
+import io.camunda.zeebe.protocol.impl.record.value.timer.TimerRecord;
 import io.camunda.zeebe.protocol.record.RecordType;
 import io.camunda.zeebe.protocol.record.ValueType;
 import io.camunda.zeebe.protocol.record.intent.JobIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessInstanceCreationIntent;
+import io.camunda.zeebe.protocol.record.intent.TimerIntent;
+import io.camunda.zeebe.scheduler.clock.ActorClock;
 import io.camunda.zeebe.stream.api.ProcessingResult;
 import io.camunda.zeebe.stream.api.ProcessingResultBuilder;
 import io.camunda.zeebe.stream.api.RecordProcessor;
@@ -117,7 +120,8 @@ public final class GpuBatchProcessor implements RecordProcessor {
 
   @Override
   public boolean accepts(final ValueType valueType) {
-    return valueType == ValueType.PROCESS_INSTANCE_CREATION || valueType == ValueType.JOB || engine.accepts(valueType);
+    return valueType == ValueType.PROCESS_INSTANCE_CREATION || valueType == ValueType.JOB
+        || valueType == ValueType.TIMER || engine.accepts(valueType);
   }
 
   @Override
@@ -161,7 +165,9 @@ public final class GpuBatchProcessor implements RecordProcessor {
     if (record.getValueType() == ValueType.PROCESS_INSTANCE_CREATION) {
       return record.getIntent() == ProcessInstanceCreationIntent.CREATE;
     }
-    return record.getValueType() == ValueType.JOB && record.getIntent() == JobIntent.COMPLETE
+    // JOB:COMPLETE of a device job; TIMER:TRIGGER (DueDateTimerChecker's command) of a device timer
+    return ((record.getValueType() == ValueType.JOB && record.getIntent() == JobIntent.COMPLETE)
+            || (record.getValueType() == ValueType.TIMER && record.getIntent() == TimerIntent.TRIGGER))
         && ZbHip.resolveKey(handle, record.getKey()) >= 0;
   }
 
@@ -176,6 +182,7 @@ public final class GpuBatchProcessor implements RecordProcessor {
     final RecordMetadata meta = new RecordMetadata();
     final ProcessInstanceCreationRecord create = new ProcessInstanceCreationRecord();
     final JobRecord job = new JobRecord();
+    final TimerRecord timer = new TimerRecord();
     while (reader.hasNext() && window.size() < WINDOW) {
       final LoggedEvent event = reader.next();
       event.readMetadata(meta);
@@ -198,10 +205,19 @@ public final class GpuBatchProcessor implements RecordProcessor {
         if (ref < 0 || !window.addJobComplete(event.getPosition(), ref, job.getVariablesBuffer(), this)) {
           break; // a job of a CPU-resident instance
         }
+      } else if (meta.getValueType() == ValueType.TIMER && meta.getIntent() == TimerIntent.TRIGGER) {
+        event.readValue(timer);
+        final long ref = ZbHip.resolveKey(handle, event.getKey());
+        if (ref < 0) {
+          break; // a timer of a CPU-resident instance
+        }
+        window.addTimerTrigger(event.getPosition(), ref, timer.getDueDate());
       } else {
         break; // any other command ends the window
       }
     }
+    // the window's clock: TIMER:CREATED dueDates (CatchEventBehavior.java:310, ActorClock)
+    ZbHip.setClock(handle, ActorClock.currentTimeMillis());
     window.submitRunDrain(handle);
     // instances that ended in this window free their slots for later CREATEs
     window.forEachEndedInstance(slot -> usedSlots.clear(slot));

@@ -24,6 +24,7 @@ import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessEventRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceRecord;
+import io.camunda.zeebe.protocol.impl.record.value.timer.TimerRecord;
 import io.camunda.zeebe.protocol.impl.record.value.variable.VariableRecord;
 import io.camunda.zeebe.protocol.record.RecordType;
 import io.camunda.zeebe.protocol.record.RejectionType;
@@ -122,6 +123,17 @@ final class Window {
     put(position, (int) (ref >>> 16), ZbHip.CMD_JOB_COMPLETE, count, (int) (ref & 0xFFFF), first, variables);
     return true;
   }
+
+  /**
+   * TIMER:TRIGGER -> ZBHIP_CMD_TIMER_TRIGGER; ref = zbhip_resolve_key's (slot << 16 | ordinal) of the
+   * timer key, the command's dueDate in doc_begin (low) and pad (high).
+   */
+  void addTimerTrigger(final long position, final long ref, final long dueDate) {
+    put(position, (int) (ref >>> 16), ZbHip.CMD_TIMER_TRIGGER, 0, (int) (ref & 0xFFFF), (int) dueDate, EMPTY);
+    cmds.set(JAVA_INT, ZbHip.COMMAND.byteSize() * (n - 1) + 12, (int) (dueDate >>> 32)); // pad: dueDate high word
+  }
+
+  private static final DirectBuffer EMPTY = new UnsafeBuffer(new byte[0]);
 
   private void put(
       final long position, final int instance, final byte kind, final int docCount, final int ref, final int docBegin,
@@ -309,10 +321,25 @@ final class Window {
       case PROCESS_EVENT -> {
         final ProcessEventRecord v = new ProcessEventRecord();
         v.setScopeKey(scope)
-            .setTargetElementIdBuffer(new UnsafeBuffer(d.elementIds()[elem].getBytes()))
-            .setVariablesBuffer(documents[i])
+            .setTargetElementIdBuffer(new UnsafeBuffer(d.elementIds()[elem].getBytes()));
+        if (r.get(JAVA_BYTE, 42) == ProcessEventIntent.TRIGGERING.value()) {
+          v.setVariablesBuffer(documents[i]); // TRIGGERED: processEventTriggered resets the record
+        }
+        v
             .setProcessDefinitionKey(d.definitionKey())
             .setProcessInstanceKey(pik);
+        return v.setTenantId(TENANT);
+      }
+      case TIMER -> {
+        // TimerRecord (CatchEventBehavior.java:311-319): CREATED / CANCELED / TRIGGERED carry the
+        // timer's value, a rejected TRIGGER the command's key and dueDate
+        final TimerRecord v = new TimerRecord();
+        v.setElementInstanceKey(scope)
+            .setProcessInstanceKey(pik)
+            .setDueDate(aux)
+            .setRepetitions(1)
+            .setTargetElementId(new UnsafeBuffer(elem >= 0 ? d.elementIds()[elem].getBytes() : new byte[0]))
+            .setProcessDefinitionKey(elem >= 0 ? d.definitionKey() : -1);
         return v.setTenantId(TENANT);
       }
       case PROCESS_INSTANCE_CREATION -> {

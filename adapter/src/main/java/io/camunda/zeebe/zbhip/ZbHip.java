@@ -39,6 +39,7 @@ public final class ZbHip {
   // ---- command kinds (zbhip_command_kind) ----
   public static final byte CMD_CREATE = 1; // PROCESS_INSTANCE_CREATION:CREATE
   public static final byte CMD_JOB_COMPLETE = 2; // JOB:COMPLETE
+  public static final byte CMD_TIMER_TRIGGER = 8; // TIMER:TRIGGER (the due-date checker's command)
   public static final byte CMD_PUBLISH = 3; // MESSAGE:PUBLISH (config 5)
   public static final byte CMD_MSG_SUB_CREATE = 4;
   public static final byte CMD_PMS_CREATE = 5;
@@ -157,6 +158,7 @@ public final class ZbHip {
   private static final MethodHandle SUBMIT_EX =
       fn("zbhip_submit_ex", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG));
   private static final MethodHandle RUN = fn("zbhip_run", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
+  private static final MethodHandle SET_CLOCK = fn("zbhip_set_clock", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG));
   private static final MethodHandle PENDING = fn("zbhip_pending_records", FunctionDescriptor.of(JAVA_LONG, ADDRESS));
   private static final MethodHandle DRAIN = fn("zbhip_drain", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle OUTBOX = fn("zbhip_outbox", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
@@ -338,6 +340,11 @@ public final class ZbHip {
 
   public static int run(final MemorySegment h, final int flags) {
     return check((int) call(RUN, h, flags), "zbhip_run");
+  }
+
+  /** ActorClock.currentTimeMillis() of the next window (timer dueDates: CatchEventBehavior.java:310). */
+  public static void setClock(final MemorySegment h, final long nowMillis) {
+    check((int) call(SET_CLOCK, h, nowMillis), "zbhip_set_clock");
   }
 
   public static long pendingRecords(final MemorySegment h) {
