@@ -5,7 +5,9 @@ nested).  Used to drive the GPU executor and the CPU oracle with the same inputs
 Bounds keep every process inside the device limits (<= 8 waiting elements per instance, <= 16
 join counters, a default flow on every exclusive split so no incident is raised).  With
 ``sub_processes`` a block can be an embedded sub-process holding a nested sequence (start ->
-blocks -> end), never inside a parallel branch (one active instance per sub-process element)."""
+blocks -> end), never inside a parallel branch (one active instance per sub-process element).
+With ``boundaries`` a task outside parallel branches may carry an interrupting timer boundary event
+whose path ends in an end event or merges back after the task (one timer per instance at a time)."""
 from xml.sax.saxutils import escape, quoteattr
 
 BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
@@ -14,8 +16,9 @@ ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
 
 class _Gen:
     def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True, sub_processes=False,
-                 task_kinds=False):
+                 task_kinds=False, boundaries=False):
         self.rng = rng
+        self.boundaries = boundaries
         self.task_kinds = task_kinds
         self.sub_processes = sub_processes
         self.scope = None  # the sub-process being filled (None: the process)
@@ -99,6 +102,16 @@ class _Gen:
                 kind = ("serviceTask", "sendTask", "scriptTask", "businessRuleTask")[int(r.integers(0, 4))]
             t = self.node(kind, job_type="job%d" % int(r.integers(0, 3)))
             self.flow(cur, t)
+            if self.boundaries and width == 1 and int(r.integers(0, 2)):
+                # an interrupting timer boundary event: its own end, or back through an XOR merge
+                b = self.node("boundaryEvent", attached=t, duration="PT%dS" % int(r.integers(1, 120)))
+                if int(r.integers(0, 2)):
+                    self.flow(b, self.node("endEvent"))
+                    return t
+                merge = self.node("exclusiveGateway")
+                self.flow(t, merge)
+                self.flow(b, merge)
+                return merge
             return t
         if c == "catch":
             self.catches += 1
@@ -135,10 +148,11 @@ class _Gen:
 
 
 def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False,
-                   tasks=True, sub_processes=False, task_kinds=False):
+                   tasks=True, sub_processes=False, task_kinds=False, boundaries=False):
     """tasks=False: no wait states (the CREATE batch runs the instance to its end); task_kinds: job
     worker tasks among service / send / script / business-rule tasks."""
-    g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes, task_kinds)
+    g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes, task_kinds,
+             boundaries)
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")
@@ -158,6 +172,10 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
             elif kind == "intermediateCatchEvent":
                 out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition messageRef="msg_def"/>'
                            '</intermediateCatchEvent>' % (ind, quoteattr(nid)))
+            elif kind == "boundaryEvent":
+                out.append('%s<boundaryEvent id=%s attachedToRef=%s><timerEventDefinition><timeDuration>%s'
+                           '</timeDuration></timerEventDefinition></boundaryEvent>'
+                           % (ind, quoteattr(nid), quoteattr(extra["attached"]), extra["duration"]))
             elif kind == "subProcess":
                 out.append("%s<subProcess id=%s>" % (ind, quoteattr(nid)))
                 render(nid, ind + "  ")

@@ -97,6 +97,20 @@ def test_gpu_boundary_both_outcomes():
     assert part.stats()["fallback"] == 0
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_random_processes_with_boundary_events(seed):
+    # tests/random_bpmn.py: random structured processes (sub-processes, job worker kinds) whose
+    # tasks outside parallel branches may carry a timer boundary event; each round completes a job
+    # or fires a timer per instance at random
+    from helpers import amount_docs
+    from random_bpmn import random_process
+    rng = np.random.default_rng(6000 + seed)
+    xml = random_process(rng, sub_processes=True, task_kinds=True, boundaries=True)
+    part, orc = drive_timers(xml, 96, seed=seed, phases=60, max_records=256,
+                             docs_fn=lambda n: amount_docs(rng.integers(0, 1000, n), 0))
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []
+
+
 @pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch"])
 def test_gpu_boundary_log_and_db_bytes(shape):
     pair = Pair(SHAPES[shape](), 100)

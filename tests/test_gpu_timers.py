@@ -45,14 +45,20 @@ def _open_work(part, rng):
     return c
 
 
-def drive_timers(xml, n, seed=0, phases=30):
-    part = Partition(max_instances=n, max_commands=max(n, 8), max_records_per_batch=128)
+def drive_timers(xml, n, seed=0, phases=30, docs_fn=None, max_records=128):
+    part = Partition(max_instances=n, max_commands=max(n, 8), max_records_per_batch=max_records)
     orc = Oracle()
     assert part.deploy(xml) == orc.deploy(xml) == 0
     clock = NOW
     for e in (part, orc):
         e.set_clock(clock)
-    run_both(part, orc, create_commands(n, 0))
+    cmds, docs = create_commands(n, 0), None
+    if docs_fn is not None:  # an `amount` per instance (random processes' conditions)
+        assert part.intern("amount") == orc.intern("amount")
+        docs = docs_fn(n)
+        cmds["doc_count"] = 1
+        cmds["doc_begin"] = np.arange(n)
+    run_both(part, orc, cmds, docs)
     assert part.state() == orc.state()
     rng = np.random.default_rng(seed)
     for _ in range(phases):
