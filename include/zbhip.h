@@ -164,7 +164,7 @@ typedef struct zbhip_element {
   uint16_t condition;    /* sequence flow: condition index; ZBHIP_NONE16 = no condition */
   uint16_t default_flow; /* exclusive gateway: default flow element; else ZBHIP_NONE16 */
   uint16_t job_type;     /* service task: string-table index of the job type */
-  uint16_t job_retries;  /* service task: static retries */
+  uint16_t job_retries;  /* service task: static retries; boundary event: 1 interrupting (cancelActivity), 0 not */
   uint16_t join_slot;    /* sequence flow into a parallel gateway: its taken-counter slot; else NONE */
   uint16_t id;           /* string-table index of the element id */
   uint16_t message_name; /* message catch event: string-table index of the static message name; else NONE */
@@ -173,7 +173,7 @@ typedef struct zbhip_element {
                           * element (ExecutableFlowElement.getFlowScope, FlowElementInstantiationTransformer) */
   uint16_t start_event;  /* process / embedded sub-process: its none start event
                           * (ExecutableFlowElementContainer.getNoneStartEvent); job worker task: its
-                          * (one, interrupting timer) boundary event; else ZBHIP_NONE16 */
+                          * (one, timer) boundary event; else ZBHIP_NONE16 */
   uint32_t duration_ms;  /* timer catch / boundary event: the static timeDuration in ms (Interval.parse); else 0 */
 } zbhip_element;
 

@@ -336,7 +336,8 @@ struct OEl {
   int scope = 0;                   // flow scope element (ExecutableFlowElement.getFlowScope): 0 = process
   int start = -1;                  // process / sub-process: getNoneStartEvent
   int attached = -1;               // boundary event: the activity it is attached to (attachedToRef)
-  int boundary = -1;               // activity: its (one, interrupting) boundary event (ExecutableActivity.attach)
+  int boundary = -1;               // activity: its (one) boundary event (ExecutableActivity.attach)
+  bool interrupting = true;        // boundary event: cancelActivity (ExecutableBoundaryEvent.interrupting)
 };
 
 struct OProc {
@@ -464,9 +465,9 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       e.event = ZBHIP_EV_TIMER;
     } else if (n == "boundaryEvent") {
       // BoundaryEventTransformer (deployment/model/transformer/BoundaryEventTransformer.java):
-      // interrupting timer boundary events with a static timeDuration on job worker tasks only
+      // timer boundary events (interrupting or not) with a static timeDuration on job worker tasks only
       e.type = ZBHIP_EL_BOUNDARY_EVENT;
-      if (k->attr("cancelActivity") == "false") { err = "non-interrupting boundary event outside the supported subset"; return false; }
+      e.interrupting = k->attr("cancelActivity") != "false";
       const XNode* ted = k->child("timerEventDefinition");
       const XNode* td = ted ? ted->child("timeDuration") : nullptr;
       if (!td || k->child("messageEventDefinition") || k->child("errorEventDefinition") ||
@@ -1334,9 +1335,12 @@ class Oracle {
     pe.r.process_instance_key = t.pi.piKey;
     pe.r.aux = -1;
     trigger_event(eik, eventKey, t.pi.elem, t.pi.proc, Doc{0, 0}, t.pi.piKey);
-    if (E(t.pi).type == ZBHIP_EL_BOUNDARY_EVENT)  // isInterrupting: terminate the activity first
+    const OEl& target = E(t.pi);
+    if (target.type == ZBHIP_EL_BOUNDARY_EVENT && target.interrupting)  // terminate the activity first
       pi_command(eik, ZBHIP_PI_TERMINATE_ELEMENT, eit->second.value);
-    else                                          // isElementActivated (catch event)
+    else if (target.type == ZBHIP_EL_BOUNDARY_EVENT)  // non-interrupting: activateTriggeredEvent now
+      activate_triggered_event(eventKey, t.pi.elem, eik, eit->second.value.flowScopeKey, eit->second.value);
+    else                                              // isElementActivated (catch event)
       pi_command(eik, ZBHIP_PI_COMPLETE_ELEMENT, eit->second.value);
   }
 
@@ -1358,7 +1362,7 @@ class Oracle {
       const OEl& owner = procs[sit->second.value.proc].els[sit->second.value.elem];
       const bool interrupting = owner.id == procs[proc].els[elem].id ? owner.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
                                                                            owner.type == ZBHIP_EL_BOUNDARY_EVENT
-                                                                     : owner.boundary == elem;
+                                                                     : owner.boundary == elem && procs[proc].els[elem].interrupting;
       if (interrupting) es_interrupted_.insert(scope);
       if (interrupting && owner.boundary == elem) es_closed_.insert(scope);
     }
@@ -2278,7 +2282,10 @@ std::string Oracle::dump_state() const {
     const OEl* el = op ? &op->els[eit->second.value.elem] : nullptr;
     std::string intr, bnd;
     if (el && (el->type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || el->type == ZBHIP_EL_BOUNDARY_EVENT)) intr = el->id;
-    if (el && el->boundary >= 0) intr = bnd = op->els[el->boundary].id;
+    if (el && el->boundary >= 0) {  // interruptingIds only for cancelActivity boundary events
+      bnd = op->els[el->boundary].id;
+      if (op->els[el->boundary].interrupting) intr = bnd;
+    }
     snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=%d,interrupted=%d,interrupting=%s,boundaryElementIds=%s",
              (long long)k, es_closed_.count(k) ? 0 : 1, es_interrupted_.count(k) ? 1 : 0, intr.c_str(), bnd.c_str());
     rows.push_back(buf);

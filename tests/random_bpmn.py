@@ -6,8 +6,9 @@ Bounds keep every process inside the device limits (<= 8 waiting elements per in
 join counters, a default flow on every exclusive split so no incident is raised).  With
 ``sub_processes`` a block can be an embedded sub-process holding a nested sequence (start ->
 blocks -> end), never inside a parallel branch (one active instance per sub-process element).
-With ``boundaries`` a task outside parallel branches may carry an interrupting timer boundary event
-whose path ends in an end event or merges back after the task (one timer per instance at a time)."""
+With ``boundaries`` a task outside parallel branches may carry a timer boundary event whose path
+ends in an end event or (interrupting ones) merges back after the task (one timer per instance at a
+time)."""
 from xml.sax.saxutils import escape, quoteattr
 
 BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
@@ -104,8 +105,10 @@ class _Gen:
             self.flow(cur, t)
             if self.boundaries and width == 1 and int(r.integers(0, 2)):
                 # an interrupting timer boundary event: its own end, or back through an XOR merge
-                b = self.node("boundaryEvent", attached=t, duration="PT%dS" % int(r.integers(1, 120)))
-                if int(r.integers(0, 2)):
+                b = self.node("boundaryEvent", attached=t, duration="PT%dS" % int(r.integers(1, 120)),
+                              cancel=bool(int(r.integers(0, 3))))
+                # a non-interrupting one always ends on its own (merging back would double the token)
+                if int(r.integers(0, 2)) or not self.nodes[-1][2]["cancel"]:
                     self.flow(b, self.node("endEvent"))
                     return t
                 merge = self.node("exclusiveGateway")
@@ -173,9 +176,10 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
                 out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition messageRef="msg_def"/>'
                            '</intermediateCatchEvent>' % (ind, quoteattr(nid)))
             elif kind == "boundaryEvent":
-                out.append('%s<boundaryEvent id=%s attachedToRef=%s><timerEventDefinition><timeDuration>%s'
+                out.append('%s<boundaryEvent id=%s attachedToRef=%s%s><timerEventDefinition><timeDuration>%s'
                            '</timeDuration></timerEventDefinition></boundaryEvent>'
-                           % (ind, quoteattr(nid), quoteattr(extra["attached"]), extra["duration"]))
+                           % (ind, quoteattr(nid), quoteattr(extra["attached"]),
+                              "" if extra["cancel"] else ' cancelActivity="false"', extra["duration"]))
             elif kind == "subProcess":
                 out.append("%s<subProcess id=%s>" % (ind, quoteattr(nid)))
                 render(nid, ind + "  ")

@@ -9,7 +9,7 @@ import pytest
 
 from test_gpu_logserial import Pair
 from test_gpu_timers import _open_work, drive_timers, part_key
-from test_oracle_boundary import multiple_sequence_flows
+from test_oracle_boundary import multiple_sequence_flows, non_interrupting_process
 from test_oracle_timers import NOW
 from zeebe_amd import abi, bpmn
 from zeebe_amd.engine import Partition
@@ -50,7 +50,16 @@ def _boundary_to_gateway():
     return b.endEvent("e").done()
 
 
+def _non_interrupting_escalation():
+    # a non-interrupting reminder that runs a task of its own while the activity waits
+    b = bpmn.createExecutableProcess("process").startEvent("s").serviceTask("a", "a").boundaryEvent("remind")
+    b.cancelActivity(False).timerWithDuration("PT1H").serviceTask("r", "r").endEvent("re").moveToActivity("a")
+    return b.serviceTask("b", "b").endEvent("e").done()
+
+
 SHAPES = {"multiple_sequence_flows": lambda: multiple_sequence_flows("PT30S"), "linear": _linear_with_boundary,
+          "non_interrupting": lambda: non_interrupting_process("PT30S"),
+          "non_interrupting_escalation": _non_interrupting_escalation,
           "in_sub_process": _boundary_in_sub_process, "then_catch": _boundary_then_catch,
           "to_gateway": _boundary_to_gateway}
 
@@ -111,7 +120,7 @@ def test_gpu_random_processes_with_boundary_events(seed):
     assert [r for r in part.state() if not r.startswith("KEY|")] == []
 
 
-@pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch"])
+@pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch", "non_interrupting_escalation"])
 def test_gpu_boundary_log_and_db_bytes(shape):
     pair = Pair(SHAPES[shape](), 100)
     for e in (pair.part, pair.orc):
@@ -127,7 +136,7 @@ def test_gpu_boundary_log_and_db_bytes(shape):
         pair.window(c)
 
 
-@pytest.mark.parametrize("shape", ["linear", "in_sub_process"])
+@pytest.mark.parametrize("shape", ["linear", "in_sub_process", "non_interrupting_escalation"])
 def test_gpu_boundary_restart_equivalence(shape):
     xml = SHAPES[shape]()
     n = 48

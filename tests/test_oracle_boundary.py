@@ -30,6 +30,14 @@ def with_boundary_event():
             .timerWithDuration("PT10S").endEvent().moveToActivity("task").endEvent("taskEnd").done())
 
 
+def non_interrupting_process(duration="PT1S"):
+    """BoundaryEventTest.NON_INTERRUPTING_PROCESS (:61-69) with a static timeDuration in place of
+    its cycle expression (one trigger, no reschedule)."""
+    return (bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "type").boundaryEvent("event")
+            .cancelActivity(False).timerWithDuration(duration).endEvent("eventEnd").moveToActivity("task")
+            .endEvent("taskEnd").done())
+
+
 def _eid(o, r):
     e = int(r["element_idx"])
     return o.element_id(0, e) if e >= 0 else None
@@ -148,6 +156,34 @@ def test_take_all_outgoing_sequence_flows_if_triggered():
     assert [r for r in o.state() if not r.startswith("KEY|")] == []
 
 
+def test_non_interrupting_boundary_keeps_the_activity():
+    # BoundaryEventTest.shouldNotTerminateActivityForNonInterruptingBoundaryEvents (:274-313): the
+    # subsequence TIMER TRIGGERED ... JOB COMPLETED, task COMPLETING, task COMPLETED (its cycle's
+    # re-created timer and the CANCELED of it do not occur for a duration); the boundary event's
+    # path runs while the task stays ACTIVATED (EventHandle.activateElement, not interrupting)
+    o, recs = _started(non_interrupting_process())
+    task_key = [r for r in recs if _tuple(o, r) == ("PROCESS_INSTANCE", "ELEMENT_ACTIVATED", "task")][0]["key"]
+    st = o.state()
+    assert "EVENT_SCOPE|%d|accepting=1,interrupted=0,interrupting=,boundaryElementIds=event" % int(task_key) in st
+    fired = _trigger_all(o, recs)
+    seq = [_tuple(o, r) for r in fired]
+    assert seq[:7] == [
+        ("TIMER", "TRIGGERED", "event"), ("PROCESS_EVENT", "TRIGGERING", "event"),
+        ("PROCESS_EVENT", "TRIGGERED", "event"), ("PROCESS_INSTANCE", "ELEMENT_ACTIVATING", "event"),
+        ("PROCESS_INSTANCE", "ELEMENT_ACTIVATED", "event"), ("PROCESS_INSTANCE", "COMPLETE_ELEMENT", "event"),
+        ("PROCESS_INSTANCE", "ELEMENT_COMPLETING", "event")]
+    assert not any(t[1].startswith(("TERMINATE", "ELEMENT_TERMINAT")) or t[1] == "CANCELED" for t in seq)
+    assert ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "eventEnd") in seq
+    assert any(r.startswith("ELEMENT_INSTANCE_KEY|%d|" % int(task_key)) and "state=3" in r for r in o.state())
+    done = _complete_jobs(o, recs)
+    it = iter([_tuple(o, r) for r in recs + fired + done])
+    want = [("TIMER", "TRIGGERED", "event"), ("JOB", "COMPLETED", "task"),
+            ("PROCESS_INSTANCE", "ELEMENT_COMPLETING", "task"), ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "task")]
+    assert all(w in it for w in want)
+    assert not any(_tuple(o, r) == ("TIMER", "CANCELED", "event") for r in done)
+    assert [r for r in o.state() if not r.startswith("KEY|")] == []
+
+
 def test_job_of_a_terminated_task_is_not_found():
     o, recs = _started(multiple_sequence_flows())
     _trigger_all(o, recs)
@@ -182,11 +218,11 @@ def _boundary_model(attrs="", body=None, on="serviceTask"):
 
 
 def test_boundary_model_subset():
-    for xml in (_boundary_model(), multiple_sequence_flows(), with_boundary_event()):
+    for xml in (_boundary_model(), _boundary_model(' cancelActivity="false"'), multiple_sequence_flows(),
+                with_boundary_event(), non_interrupting_process()):
         Compiled(xml)
         Oracle().deploy(xml)
-    refused = [_boundary_model(' cancelActivity="false"'),
-               _boundary_model(body='<messageEventDefinition id="m" messageRef="x"/>'),
+    refused = [_boundary_model(body='<messageEventDefinition id="m" messageRef="x"/>'),
                _boundary_model(body='<timerEventDefinition id="t"><timeCycle>R3/PT1S</timeCycle></timerEventDefinition>'),
                _boundary_model(on="task"),
                (bpmn.createExecutableProcess("p").startEvent().serviceTask("a", "a").boundaryEvent("b1")
@@ -202,7 +238,10 @@ def test_boundary_model_subset():
     task, timer = ids.index("task"), ids.index("timer")
     assert int(c.els[timer]["element_type"]) == abi.ELEMENT_TYPES.index("BOUNDARY_EVENT")
     assert int(c.els[timer]["flow_source"]) == task and int(c.els[task]["start_event"]) == timer
-    assert int(c.els[timer]["duration_ms"]) == 120000
+    assert int(c.els[timer]["duration_ms"]) == 120000 and int(c.els[timer]["job_retries"]) == 1
+    c = Compiled(non_interrupting_process())
+    ids = [c.id(i) for i in range(len(c.els))]
+    assert int(c.els[ids.index("event")]["job_retries"]) == 0  # cancelActivity="false"
 
 
 def test_product_serializer_and_state_encoder_on_boundary_records():

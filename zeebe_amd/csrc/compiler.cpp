@@ -517,10 +517,10 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
       }
       if (type == ZBHIP_EL_BOUNDARY_EVENT) {
-        // BoundaryEventTransformer: interrupting timer boundary events (a static timeDuration) on
-        // job worker tasks; attached after the walk
-        const std::string* ca = c.get("cancelActivity");
-        if (ca && *ca == "false") { err = "non-interrupting boundary event outside the supported subset"; return ZBHIP_EUNSUPP; }
+        // BoundaryEventTransformer: timer boundary events (a static timeDuration; interrupting or not)
+        // on job worker tasks; attached after the walk
+        const std::string* ca = c.get("cancelActivity");  // BoundaryEvent default: interrupting
+        e.job_retries = ca && *ca == "false" ? 0 : 1;
         const Elem* ted = c.first("timerEventDefinition");
         const Elem* td = ted ? ted->first("timeDuration") : nullptr;
         for (auto& d : c.children)

@@ -1086,6 +1086,22 @@ __device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint3
 }
 
 // ---- TIMER:TRIGGER (K::S) --------------------------------------------------------------------
+// EventTriggerBehavior.activateTriggeredEvent (processing/common/EventTriggerBehavior.java:191-244):
+// PROCESS_EVENT:TRIGGERED under the trigger's key (aux: its event scope), the triggered event's
+// ACTIVATING + ACTIVATED (+key, flow scope fsa) and its COMPLETE_ELEMENT
+template <class K>
+__device__ __forceinline__ void activate_triggered_event(Lane<K>& L, uint32_t pe, uint32_t scope, uint32_t target,
+                                                         uint32_t fsa) {
+  emit(L, C_PE_TRIGGERED, pe, scope, target);
+  const uint32_t bk = new_key(L);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, bk, fsa, target);
+  apply_activating_child(L, target, elem_of(L, target), bk);
+  if (L.fail) return;
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, bk, fsa, target);
+  tbl_set_state(L, tbl_find(L, bk), ZBHIP_PI_ELEMENT_ACTIVATED);
+  follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, bk, fsa, target, true, true, bk);
+}
+
 // TriggerTimerProcessor.processRecord (processing/timer/TriggerTimerProcessor.java:81-114) for the
 // instance's timer: NOT_FOUND / INVALID_STATE rejections, TIMER:TRIGGERED (the command's key),
 // TimerTriggeredApplier (the row removed), then EventHandle.activateElement (EventHandle.java:104-131):
@@ -1108,7 +1124,17 @@ __device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord) {
   const uint32_t pe = new_key(L);
   emit(L, C_PE_TRIGGERING, pe, eord, elem);
   L.trig_key = (uint16_t)eord;  // ProcessEventTriggeringApplier: EVENT_TRIGGER row (no variables)
-  if (etype(elem_of(L, elem)) == ZBHIP_EL_BOUNDARY_EVENT) {
+  const uint4 bw = elem_of(L, elem);
+  if (etype(bw) == ZBHIP_EL_BOUNDARY_EVENT && (bw.w & 0xFFFF) == 0) {
+    // a non-interrupting boundary event: EventHandle.activateElement -> activateTriggeredEvent in
+    // this batch; the activity stays active (its EVENT_TRIGGER row is deleted by TRIGGERED)
+    L.trig_key = NONE;
+    const uint32_t task = tget(L, t).x & 0xFFFF;
+    const uint32_t c = scope_of<K>(elem_of(L, task));
+    activate_triggered_event(L, pe, eord, elem, scope_key(L, c));
+    return;
+  }
+  if (etype(bw) == ZBHIP_EL_BOUNDARY_EVENT) {
     // an interrupting boundary event: TERMINATE_ELEMENT of the activity it is attached to (the
     // activation of the boundary event follows its termination, terminate_pi); the trigger's
     // PROCESS_EVENT key travels with the EVENT_TRIGGER row.  Past the batch limit the command
@@ -1169,14 +1195,7 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
   emit(L, ZBHIP_PI_ELEMENT_TERMINATED, key, fsa, elem);
   apply_completed_child(L, t, key);  // removeInstance; the event scope with its trigger
   L.trig_evt = NONE;
-  emit(L, C_PE_TRIGGERED, pe, key, target);
-  const uint32_t bk = new_key(L);
-  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, bk, fsa, target);
-  apply_activating_child(L, target, elem_of(L, target), bk);
-  if (L.fail) return;
-  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, bk, fsa, target);
-  tbl_set_state(L, tbl_find(L, bk), ZBHIP_PI_ELEMENT_ACTIVATED);
-  follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, bk, fsa, target, true, true, bk);
+  activate_triggered_event(L, pe, key, target, fsa);
 }
 
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------

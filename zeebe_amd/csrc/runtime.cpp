@@ -709,7 +709,10 @@ static int rebuild_program(zbhip_handle* h) {
       else if (E.element_type == ZBHIP_EL_SUB_PROCESS) w[2] = E.start_event | (join_mask[e] << 16);
       else w[2] = 0xFFFFFFFFu;
       // a job worker's join_slot half: its boundary event (zbhip_element.start_event), 0xFFFF if none
-      w[3] = (ZBHIP_IS_JOB_WORKER(E.element_type) ? E.start_event : E.join_slot) | ((uint32_t)E.flow_scope << 16);
+      // a boundary event's: 1 if interrupting (zbhip_element.job_retries)
+      const uint32_t low = ZBHIP_IS_JOB_WORKER(E.element_type) ? E.start_event
+                           : E.element_type == ZBHIP_EL_BOUNDARY_EVENT ? E.job_retries : E.join_slot;
+      w[3] = low | ((uint32_t)E.flow_scope << 16);
     }
     uint16_t* outw = reinterpret_cast<uint16_t*>(pb + out_off);
     for (size_t i = 0; i < P.out.size(); ++i) outw[i] = P.out[i];
@@ -2113,8 +2116,9 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       const bool own = E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT;
       const bool bnd = ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16;
       const std::string ids = own ? P.id(elem) : bnd ? P.id(E.start_event) : std::string();
+      const bool intr = own || (bnd && P.els[E.start_event].job_retries);  // cancelActivity boundary events only
       snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=%s", k,
-               ids.c_str(), bnd ? ids.c_str() : "");
+               intr ? ids.c_str() : "", bnd ? ids.c_str() : "");
       sink(ctx, buf);
     }
     if (job_row) {

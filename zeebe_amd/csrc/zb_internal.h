@@ -128,7 +128,8 @@ constexpr uint8_t CMD_FOLLOWUP = 0x20;
 //                                 message catch: name | correlation variable << 16; timer catch / boundary
 //                                 event: duration ms; sub-process: none start event | join slots of its
 //                                 gateways << 16
-//                            w3 = join_slot (job worker: its boundary event or 0xFFFF) | container
+//                            w3 = join_slot (job worker: its boundary event or 0xFFFF; boundary event:
+//                                 1 interrupting, 0 not) | container
 //                                 (flow scope element; 0 = the process) << 16
 //   p[out_off]  u16 outgoing flows (two per word)
 //   p[cond_off] u32 first instruction of each condition
