@@ -119,6 +119,58 @@ struct BatchRef {
   uint32_t gen;  // generation of the subject when the keys were generated (inst_gen)
 };
 
+// The resolve_key table: BatchRefs in key order, in segments (one per plain window, or appended
+// entries), so appending 10^6 entries never moves the older ones and a compaction runs segment by
+// segment on host threads.  Lookup: the segment by its first key, then within it.
+struct KeyTable {
+  std::vector<std::vector<BatchRef>> seg;
+  size_t count = 0;
+  size_t size() const { return count; }
+  // a new segment of n entries, filled by the caller (indexes 0 .. n-1, from any thread)
+  BatchRef* append_segment(size_t n) {
+    if (n == 0) return nullptr;
+    seg.emplace_back(n);
+    count += n;
+    return seg.back().data();
+  }
+  void push_back(const BatchRef& b) {
+    if (seg.empty() || seg.back().size() >= (1u << 20)) {
+      seg.emplace_back();
+      seg.back().reserve(1024);
+    }
+    seg.back().push_back(b);
+    ++count;
+  }
+  const BatchRef* find(int64_t v) const {  // the last entry with base <= v
+    auto s = std::upper_bound(seg.begin(), seg.end(), v,
+                              [](int64_t x, const std::vector<BatchRef>& g) { return x < g.front().base; });
+    if (s == seg.begin()) return nullptr;
+    --s;
+    auto it = std::upper_bound(s->begin(), s->end(), v, [](int64_t x, const BatchRef& b) { return x < b.base; });
+    return it == s->begin() ? nullptr : &*(it - 1);
+  }
+  template <class Live>
+  void compact(const Live& live) {
+    parallel_for(host_threads(), [&](unsigned t, unsigned T) {
+      for (size_t i = t; i < seg.size(); i += T)
+        seg[i].erase(std::remove_if(seg[i].begin(), seg[i].end(), [&](const BatchRef& b) { return !live(b); }),
+                     seg[i].end());
+    });
+    seg.erase(std::remove_if(seg.begin(), seg.end(), [](const std::vector<BatchRef>& g) { return g.empty(); }),
+              seg.end());
+    count = 0;
+    for (auto& g : seg) count += g.size();
+  }
+  void sort_all() {  // (imports: one segment again)
+    std::vector<BatchRef> all;
+    all.reserve(count);
+    for (auto& g : seg) all.insert(all.end(), g.begin(), g.end());
+    std::sort(all.begin(), all.end(), [](const BatchRef& a, const BatchRef& b) { return a.base < b.base; });
+    seg.clear();
+    if (!all.empty()) seg.push_back(std::move(all));
+  }
+};
+
 const char* state_name(int s) {
   switch (s) {
     case ZBHIP_PI_ELEMENT_ACTIVATING: return "ELEMENT_ACTIVATING";
@@ -231,6 +283,7 @@ struct zbhip_handle {
   std::vector<std::pair<uint32_t, uint32_t>> plan_last;
   uint32_t plan_stamp = 0;
   std::vector<uint32_t> plan_seen;
+  std::vector<uint32_t> plan_round;  // round of each command of the window being planned
   uint32_t plan_window = 0;
   // fence stamps of the device windows (StepParams.stamp; hdr.w / slot_hdr.y of a fallen-back subject)
   uint32_t window_stamp = 0;
@@ -242,9 +295,10 @@ struct zbhip_handle {
   // keys of an earlier instance in a reused slot never resolve); stale entries are compacted away
   std::vector<uint32_t> inst_gen;
   size_t batches_compacted = 0;
+  std::atomic<size_t> batches_dead{0};  // entries of ended instances since the last compaction
   std::vector<std::vector<std::pair<uint16_t, int64_t>>> hist;
   std::vector<uint16_t> inst_proc;
-  std::vector<BatchRef> batches;
+  KeyTable batches;
 
   // ---- log bytes on the device (zbhip_serialize_log_device, logdev.hip) ----
   uint8_t* d_log_arena = nullptr;   // the serialiser's constant byte runs
@@ -298,6 +352,7 @@ struct zbhip_handle {
   size_t n_xparts = 0;
   uint4* d_cmd_hdr2 = nullptr;
   long long* d_cmd_due = nullptr;       // (KScope) dueDate of the timer each batch canceled
+  bool debug = getenv("ZBHIP_DEBUG") != nullptr;  // per-call host timing lines on stderr
   std::vector<long long> h_cmd_due;
   zbhip_xpart_cmd* d_xout = nullptr;
   zbhip_xpart_cmd* d_xbucket = nullptr;
@@ -894,17 +949,22 @@ static int plan_rounds(zbhip_handle* h) {
   // a CREATE into an instance slot that an earlier command of the same window addressed is refused:
   // the adapter reuses a slot only after the window that ended its instance was drained (records of
   // both instances would otherwise share the slot's key history)
-  const size_t n_inst0 = h->cfg.max_instances;
-  if (h->plan_seen.size() < n_inst0) h->plan_seen.assign(n_inst0, 0u);
-  if (++h->plan_window == 0) {
-    std::fill(h->plan_seen.begin(), h->plan_seen.end(), 0u);
-    h->plan_window = 1;
-  }
-  for (size_t i = 0; i < h->n_cmds; ++i) {
-    const zbhip_command& c = h->h_cmds[i];
-    if (slot_kind(c.kind)) continue;
-    if (c.kind == ZBHIP_CMD_CREATE && h->plan_seen[c.instance] == h->plan_window) return ZBHIP_EINVAL;
-    h->plan_seen[c.instance] = h->plan_window;
+  // (message partitions: a window-wide stamp table, the round stamps below restart per epoch;
+  // otherwise the round table's own stamp says "addressed earlier in this window")
+  const bool msg = h->msg();
+  if (msg) {
+    const size_t n_inst0 = h->cfg.max_instances;
+    if (h->plan_seen.size() < n_inst0) h->plan_seen.assign(n_inst0, 0u);
+    if (++h->plan_window == 0) {
+      std::fill(h->plan_seen.begin(), h->plan_seen.end(), 0u);
+      h->plan_window = 1;
+    }
+    for (size_t i = 0; i < h->n_cmds; ++i) {
+      const zbhip_command& c = h->h_cmds[i];
+      if (slot_kind(c.kind)) continue;
+      if (c.kind == ZBHIP_CMD_CREATE && h->plan_seen[c.instance] == h->plan_window) return ZBHIP_EINVAL;
+      h->plan_seen[c.instance] = h->plan_window;
+    }
   }
   // last round per subject in a flat table (instances, then correlation slots), valid where its
   // stamp is the current one: no hashing and no clearing per window
@@ -918,17 +978,19 @@ static int plan_rounds(zbhip_handle* h) {
     return h->plan_stamp;
   };
   uint32_t stamp = next_stamp();
-  std::vector<uint32_t> round_of(h->n_cmds);
+  std::vector<uint32_t>& round_of = h->plan_round;
+  if (round_of.size() < h->n_cmds) round_of.resize(h->n_cmds);
   uint32_t max_round = 0, epoch = 0;
   int cls = -1;
   for (size_t i = 0; i < h->n_cmds; ++i) {
     const bool sk = slot_kind(h->h_cmds[i].kind);
-    if (h->msg() && cls >= 0 && (int)sk != cls && i > 0) {
+    if (msg && cls >= 0 && (int)sk != cls && i > 0) {
       epoch = max_round + 1;
       stamp = next_stamp();
     }
     cls = (int)sk;
     auto& e = h->plan_last[(sk ? n_inst : 0) + h->h_cmds[i].instance];  // bounds: validate()
+    if (!msg && e.first == stamp && h->h_cmds[i].kind == ZBHIP_CMD_CREATE) return ZBHIP_EINVAL;
     const uint32_t r = e.first == stamp ? e.second + 1 : epoch;
     e = {stamp, r};
     round_of[i] = r;
@@ -936,7 +998,7 @@ static int plan_rounds(zbhip_handle* h) {
   }
   if (max_round == 0) return ZBHIP_OK;  // single round: identity order
   std::vector<uint32_t> cnt(max_round + 2, 0);
-  for (uint32_t r : round_of) cnt[r + 1]++;
+  for (size_t i = 0; i < h->n_cmds; ++i) cnt[round_of[i] + 1]++;
   for (size_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
   h->round_begin.assign(cnt.begin(), cnt.end());
   h->h_order.resize(h->n_cmds);
@@ -1005,8 +1067,12 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
                     const zbhip_xpart_cmd* xparts, size_t n_xparts) {
   if (!h || (n && !cmds) || (n_docs && !docs) || (n_xparts && !xparts)) return ZBHIP_EINVAL;
   if (n > h->cfg.max_commands || n_docs > h->cfg.max_doc_entries || n_xparts > h->cfg.max_commands) return ZBHIP_ENOMEM;
+  const bool dbg = h->debug;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  const auto t0 = now();
   int rc = finalize(h);  // the previous window's keys are fixed before its commands are replaced
   if (rc) return rc;
+  const auto t1 = now();
   rc = validate(h, cmds, n, n_docs, xparts, n_xparts);
   if (rc) return rc;
   h->external = false;
@@ -1019,11 +1085,13 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
     HIPCHK(hipMemcpyAsync(h->d_xparts, xparts, n_xparts * sizeof(zbhip_xpart_cmd), hipMemcpyHostToDevice, h->stream));
   h->n_cmds = n;
   h->n_docs = n_docs;
+  const auto t2 = now();
   rc = plan_rounds(h);
   if (rc) {
     h->n_cmds = h->n_docs = h->n_xparts = 0;
     return rc;
   }
+  const auto t3 = now();
   h->doc_base = h->next_doc_base;
   h->next_doc_base += (int64_t)n_docs;
   h->source_base = h->next_source;
@@ -1036,6 +1104,11 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   HIPCHK(hipStreamSynchronize(h->stream));
   h->ran = false;
   h->results = false;
+  if (dbg) {
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[zbhip] submit n=%zu: finalize %.2f ms, validate+copy %.2f ms, plan %.2f ms, upload %.2f ms\n", n,
+            ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, now()));
+  }
   return ZBHIP_OK;
 }
 
@@ -1157,44 +1230,89 @@ static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
 // every instance sees its commands in order -- and the resolve table filled at precomputed places.
 static void advance_window_parallel(zbhip_handle* h) {
   const size_t n = h->n_cmds;
-  std::vector<uint32_t> bpos(n, ~0u);
-  int64_t kc = h->key_counter;
-  size_t nb = 0;
-  for (size_t c = 0; c < n; ++c) {
-    const uint2 hd = h->h_hdr[c];
-    h->h_base[c] = kc;
-    if (((hd.y >> 16) & 0xFF) == ST_OK) {
-      const uint32_t nk = hd.x >> 16;
-      if (nk) bpos[c] = (uint32_t)nb++;
-      kc += nk;
-    } else {
-      kc += h->ext_keys[c];
-    }
-  }
-  const size_t b0 = h->batches.size();
-  h->batches.resize(b0 + nb);
-  const uint32_t N = h->cfg.max_instances;
-  parallel_for(host_threads(), [&](unsigned t, unsigned T) {
-    for (size_t c = 0; c < n; ++c) {
-      const zbhip_command& cm = h->h_cmds[c];
-      const uint32_t inst = cm.instance;
-      if (inst >= N || inst % T != t) continue;
+  const unsigned T = host_threads();
+  // key bases and resolve-table positions in log order: per-range sums, then each range from its base
+  std::vector<int64_t> kbase(T + 1, 0);
+  std::vector<size_t> bbase(T + 1, 0);
+  auto range = [n](unsigned t, unsigned TT) { return std::make_pair(n * t / TT, n * (t + 1) / TT); };
+  parallel_for(T, [&](unsigned t, unsigned TT) {
+    int64_t k = 0;
+    size_t b = 0;
+    const auto [lo, hi] = range(t, TT);
+    for (size_t c = lo; c < hi; ++c) {
       const uint2 hd = h->h_hdr[c];
-      if (((hd.y >> 16) & 0xFF) != ST_OK) continue;
-      const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
-      if (cm.kind == ZBHIP_CMD_CREATE) {  // a new instance in the slot: its own key history
-        h->hist[inst].clear();
-        h->inst_proc[inst] = cm.ref;
-        ++h->inst_gen[inst];
+      if (((hd.y >> 16) & 0xFF) == ST_OK) {
+        k += hd.x >> 16;
+        b += (hd.x >> 16) != 0;
+      } else {
+        k += h->ext_keys[c];
       }
-      if (nkeys) {
-        h->hist[inst].push_back({(uint16_t)first, h->h_base[c] + 1});
-        h->batches[b0 + bpos[c]] = {h->h_base[c] + 1, inst, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[inst]};
-      }
-      if (hd.y & HDR_ENDED) ++h->inst_gen[inst];  // completed: its job keys no longer resolve
     }
+    kbase[t + 1] = k;
+    bbase[t + 1] = b;
   });
-  h->key_counter = kc;
+  kbase[0] = h->key_counter;
+  for (unsigned t = 0; t < T; ++t) {
+    kbase[t + 1] += kbase[t];
+    bbase[t + 1] += bbase[t];
+  }
+  BatchRef* const tbl = h->batches.append_segment(bbase[T]);
+  const uint32_t N = h->cfg.max_instances;
+  // one subject per command in a one-round window: every range updates its own instances; with
+  // rounds, each thread owns the instances i % T == t and walks the window in log order
+  const bool one_round = h->round_begin.empty() && h->cont_cmds.empty();
+  auto apply = [&](size_t c, size_t bpos, size_t& dead) {
+    const zbhip_command& cm = h->h_cmds[c];
+    const uint32_t inst = cm.instance;
+    const uint2 hd = h->h_hdr[c];
+    const uint32_t nkeys = hd.x >> 16, first = hd.y & 0xFFFF;
+    if (cm.kind == ZBHIP_CMD_CREATE) {  // a new instance in the slot: its own key history
+      h->hist[inst].clear();
+      h->inst_proc[inst] = cm.ref;
+      ++h->inst_gen[inst];
+    }
+    if (nkeys) {
+      h->hist[inst].push_back({(uint16_t)first, h->h_base[c] + 1});
+      tbl[bpos] = {h->h_base[c] + 1, inst, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[inst]};
+    }
+    if (hd.y & HDR_ENDED) {  // completed: its job keys no longer resolve
+      ++h->inst_gen[inst];
+      dead += h->hist[inst].size();  // (summed per thread: no shared counter in the loop)
+    }
+  };
+  std::vector<uint32_t> bpos(one_round ? 0 : n, ~0u);
+  parallel_for(T, [&](unsigned t, unsigned TT) {
+    int64_t kc = kbase[t];
+    size_t nb = bbase[t], dead = 0;
+    const auto [lo, hi] = range(t, TT);
+    for (size_t c = lo; c < hi; ++c) {
+      const uint2 hd = h->h_hdr[c];
+      h->h_base[c] = kc;
+      const bool ok = ((hd.y >> 16) & 0xFF) == ST_OK;
+      kc += ok ? (int64_t)(hd.x >> 16) : h->ext_keys[c];
+      if (!ok) continue;
+      const size_t here = nb;
+      nb += (hd.x >> 16) != 0;
+      if (!one_round) {
+        bpos[c] = (uint32_t)here;
+      } else if (h->h_cmds[c].instance < N) {
+        apply(c, here, dead);
+      }
+    }
+    h->batches_dead.fetch_add(dead, std::memory_order_relaxed);
+  });
+  if (!one_round) {
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      size_t dead = 0;
+      for (size_t c = 0; c < n; ++c) {
+        const uint32_t inst = h->h_cmds[c].instance;
+        if (inst >= N || inst % TT != t || bpos[c] == ~0u) continue;
+        apply(c, bpos[c], dead);
+      }
+      h->batches_dead.fetch_add(dead, std::memory_order_relaxed);
+    });
+  }
+  h->key_counter = kbase[T];
   h->fin_next = n;
 }
 
@@ -1253,7 +1371,10 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
         h->batches.push_back({h->key_counter + 1 + nprim, h2.x, (uint16_t)(h2.y & 0xFFFF), (uint16_t)nsec, h->inst_gen[h2.x]});
       }
       if (h->job_index_on && h2.x < h->cfg.max_instances) track_jobs(h, c, h2.x);
-      if ((hd.y & HDR_ENDED) && h2.x < h->cfg.max_instances) ++h->inst_gen[h2.x];
+      if ((hd.y & HDR_ENDED) && h2.x < h->cfg.max_instances) {
+        ++h->inst_gen[h2.x];
+        h->batches_dead.fetch_add(h->hist[h2.x].size(), std::memory_order_relaxed);
+      }
       h->key_counter += nkeys;
       continue;
     }
@@ -1267,16 +1388,19 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
       h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[cm.instance]});
     }
     if (h->job_index_on) track_jobs(h, c, cm.instance);
-    if (hd.y & HDR_ENDED) ++h->inst_gen[cm.instance];  // completed: its job keys no longer resolve
+    if (hd.y & HDR_ENDED) {  // completed: its job keys no longer resolve
+      ++h->inst_gen[cm.instance];
+      h->batches_dead.fetch_add(h->hist[cm.instance].size(), std::memory_order_relaxed);
+    }
     h->key_counter += nkeys;
   }
   if (h->fin_next < h->n_cmds) return ZBHIP_OK;
   // window done: drop the key-table entries of ended / replaced instances once they outnumber the rest
-  if (h->batches.size() >= 2 * h->batches_compacted + (1u << 20)) {
-    auto live = [h](const BatchRef& b) { return b.gen == h->inst_gen[b.inst]; };
-    h->batches.erase(std::remove_if(h->batches.begin(), h->batches.end(), [&](const BatchRef& b) { return !live(b); }),
-                     h->batches.end());
+  // (once ended instances' entries are a third of the table: a scan that finds nothing is not paid for)
+  if (h->batches.size() >= 2 * h->batches_compacted + (1u << 20) && 3 * h->batches_dead.load() >= h->batches.size()) {
+    h->batches.compact([h](const BatchRef& b) { return b.gen == h->inst_gen[b.inst]; });
     h->batches_compacted = h->batches.size();
+    h->batches_dead = 0;
   }
   return ZBHIP_OK;
 }
@@ -1514,6 +1638,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   const uint32_t n = n_all;  // the window and its continuation batches
 
   // ---- results: headers + records gathered into log order (drain path, off the hot loop) ----
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  const auto t0 = now();
   h->h_hdr.resize(n);
   if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
   h->h_hdr2.assign(n, make_uint4(0, 0, 0, 0));
@@ -1528,6 +1654,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   unsigned long long total = 0;
   HIPCHK(hipMemcpyAsync(&total, h->d_stats + 64 * 8, sizeof total, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  const auto t1 = now();
   h->out_total = total;
   h->out_host = false;
   h->h_out.clear();
@@ -1539,15 +1666,41 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   h->stats_dirty = true;
 
   // record offset of every command: regions follow launch order, lanes follow the launch order
-  h->h_off.assign(n + 1, 0);
+  h->h_off.resize(n + 1);
   uint64_t off = 0;
-  for (const auto& l : h->launches)
-    for (uint32_t k = 0; k < l.count; ++k) {
-      const uint32_t c = l.src == 0 ? l.first + k : l.src == 1 ? h->h_order[l.first + k] : h->cont_order[l.first + k];
-      h->h_off[c] = off;
-      off += h->h_hdr[c].x & 0xFFFF;
-    }
+  if (h->launches.size() == 1 && h->launches[0].src == 0 && n >= (1u << 16)) {
+    // one launch in log order: a prefix sum of the record counts, by ranges on host threads
+    const unsigned T = host_threads();
+    std::vector<uint64_t> part(T + 1, 0);
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      uint64_t sum = 0;
+      for (size_t c = (size_t)n * t / TT; c < (size_t)n * (t + 1) / TT; ++c) sum += h->h_hdr[c].x & 0xFFFF;
+      part[t + 1] = sum;
+    });
+    for (unsigned t = 0; t < T; ++t) part[t + 1] += part[t];
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      uint64_t o = part[t];
+      for (size_t c = (size_t)n * t / TT; c < (size_t)n * (t + 1) / TT; ++c) {
+        h->h_off[c] = o;
+        o += h->h_hdr[c].x & 0xFFFF;
+      }
+    });
+    off = part[T];
+  } else {
+    for (const auto& l : h->launches)
+      for (uint32_t k = 0; k < l.count; ++k) {
+        const uint32_t c = l.src == 0 ? l.first + k : l.src == 1 ? h->h_order[l.first + k] : h->cont_order[l.first + k];
+        h->h_off[c] = off;
+        off += h->h_hdr[c].x & 0xFFFF;
+      }
+  }
+  h->h_off[n] = 0;
   if (off != total) return ZBHIP_EDEVICE;
+  if (h->debug) {
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[zbhip] run n=%u: kernels + headers + gather %.2f ms, records copy + offsets %.2f ms\n", n,
+            ms(t0, t1), ms(t1, now()));
+  }
 
   h->ext_keys.assign(n, 0);
   h->declared.assign(n, 0);
@@ -1863,10 +2016,8 @@ int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t
   // once the window is drained
   if (int rc = advance(h, ~(size_t)0, false)) return rc;
   const int64_t v = key - ((int64_t)h->cfg.partition_id << 51);
-  auto it = std::upper_bound(h->batches.begin(), h->batches.end(), v,
-                             [](int64_t x, const BatchRef& b) { return x < b.base; });
-  if (it == h->batches.begin()) return ZBHIP_EINVAL;
-  --it;
+  const BatchRef* it = h->batches.find(v);
+  if (!it) return ZBHIP_EINVAL;
   if (v >= it->base + it->nkeys) return ZBHIP_EINVAL;
   if (it->inst < h->inst_gen.size() && it->gen != h->inst_gen[it->inst]) return ZBHIP_EINVAL;  // instance ended
   *instance = it->inst;
@@ -2664,7 +2815,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       h->batches.push_back({d.keys[o] - pbits, d.slot, (uint16_t)o, 1, h->inst_gen[d.slot]});
     }
   }
-  std::sort(h->batches.begin(), h->batches.end(), [](const BatchRef& a, const BatchRef& b) { return a.base < b.base; });
+  h->batches.sort_all();
   if (latest >= 0 && latest - pbits > h->key_counter) h->key_counter = latest - pbits;
   if (h->st.n_slots) {
     const unsigned long long kc = (unsigned long long)h->key_counter;
