@@ -81,20 +81,46 @@ struct Count {
   __device__ __forceinline__ void bytes(const LogParams&, uint2 r) { n += r.y; }
   __device__ __forceinline__ void zeros(uint32_t k) { n += k; }
 };
-// appends up to four bytes at a time into a 64-bit accumulator, stored when it fills
+// appends up to four bytes at a time into a 128-bit accumulator, stored with one 16-byte store
+// when it fills (a lane writes its own command's bytes: every store is a separate transaction, so
+// fewer, wider stores); a command's bytes start 8-byte aligned, so the first store may be 8 bytes
 struct Write {
   uint64_t* p;
-  uint64_t acc = 0;
+  uint64_t a0 = 0, a1 = 0;  // pending bytes 0..7 and 8..15
   uint32_t nb = 0;
+  uint32_t cap = 16;        // 8 until p is 16-byte aligned
+  __device__ __forceinline__ void start(uint64_t* q) {
+    p = q;
+    cap = (reinterpret_cast<uintptr_t>(q) & 15) ? 8u : 16u;
+  }
   __device__ __forceinline__ void put(uint32_t v, uint32_t k) {  // the k (1..4) low bytes of v
     const uint64_t x = k == 4 ? (uint64_t)v : (uint64_t)(v & ((1u << (8 * k)) - 1));
-    acc |= x << (8 * nb);
-    nb += k;
-    if (nb >= 8) {
-      *p++ = acc;
-      nb -= 8;
-      acc = nb ? x >> (8 * (k - nb)) : 0;
+    if (nb < 8) {
+      a0 |= x << (8 * nb);
+      if (nb + k > 8) a1 |= x >> (8 * (8 - nb));
+    } else {
+      a1 |= x << (8 * (nb - 8));
     }
+    nb += k;
+    if (nb < cap) return;
+    if (cap == 16) {
+      *reinterpret_cast<ulonglong2*>(p) = make_ulonglong2(a0, a1);
+      p += 2;
+      nb -= 16;
+      a0 = nb ? x >> (8 * (k - nb)) : 0;
+      a1 = 0;
+    } else {
+      *p++ = a0;
+      nb -= 8;
+      a0 = a1;
+      a1 = 0;
+      cap = 16;
+    }
+  }
+  __device__ __forceinline__ void finish() {  // entries end 8-byte aligned: at most one word pending
+    if (nb) *p++ = a0;
+    nb = 0;
+    a0 = a1 = 0;
   }
   __device__ __forceinline__ void b(uint32_t x) { put(x, 1); }
   __device__ __forceinline__ void bytes(const LogParams& L, uint2 r) {
@@ -467,12 +493,13 @@ __global__ __launch_bounds__(256) void k_log_write(LogParams L) {
   if (c >= L.n) return;
   const LogCmd m = L.cmds[c];
   Write s;
-  s.p = L.out + (L.bytes[c] >> 3);
+  s.start(L.out + (L.bytes[c] >> 3));
   for (uint32_t j = 0; j < m.nrec; ++j) {
     Rec r;
     if (!decode(L, c, m, L.rows[m.rec_off + j], r)) return;
     entry(s, L, m, r, L.first_position + (long long)(m.out_rec + j));
   }
+  s.finish();
 }
 
 // exclusive scan of the per-command byte counts (in place), total at bytes[n]
