@@ -27,6 +27,10 @@ for cfg in one_task xor forkjoin8 msg; do
     || { tail -20 $O/bench_$cfg.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/bench_$cfg.json'));print('%.4e'%d['value'], d['unit'], 'frac %.3f'%d['roofline']['frac'])"
 done
+echo "=== host boundary (--host-io) with kernel trace"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_hio -o hio -- python3 bench.py --host-io --steps 2 --warmup 1 --no-cpu-baseline \
+  > $O/bench_hostio.json 2> $O/bench_hostio.err || { tail -20 $O/bench_hostio.err; exit 1; }
+cat $(find $O/prof_hio -name "*kernel_stats.csv" | head -1) | cut -c1-160 | head -8
 echo "=== bench msg 8 virtual partitions"
 timeout -k 10 600 python -u bench.py --config msg --virtual-partitions 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_msg_p8.json 2> $O/bench_msg_p8.err \
   || { tail -20 $O/bench_msg_p8.err; exit 1; }
