@@ -337,7 +337,8 @@ final class Window {
         v.setElementInstanceKey(scope)
             .setProcessInstanceKey(pik)
             .setDueDate(aux)
-            .setRepetitions(1)
+            // zbhip_record.partition: the TimerRecord's repetitions (-1 infinite); a rejection: 1
+            .setRepetitions(r.get(JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value() ? 1 : r.get(JAVA_INT, 72))
             .setTargetElementId(new UnsafeBuffer(elem >= 0 ? d.elementIds()[elem].getBytes() : new byte[0]))
             .setProcessDefinitionKey(elem >= 0 ? d.definitionKey() : -1);
         return v.setTenantId(TENANT);

@@ -164,7 +164,8 @@ typedef struct zbhip_element {
   uint16_t condition;    /* sequence flow: condition index; ZBHIP_NONE16 = no condition */
   uint16_t default_flow; /* exclusive gateway: default flow element; else ZBHIP_NONE16 */
   uint16_t job_type;     /* service task: string-table index of the job type */
-  uint16_t job_retries;  /* service task: static retries; boundary event: 1 interrupting (cancelActivity), 0 not */
+  uint16_t job_retries;  /* service task: static retries; boundary event: bit 0 interrupting (cancelActivity),
+                          * bits 8..15 the timer's repetitions (1 a duration, n of "Rn/", 255 "R/" infinite) */
   uint16_t join_slot;    /* sequence flow into a parallel gateway: its taken-counter slot; else NONE */
   uint16_t id;           /* string-table index of the element id */
   uint16_t message_name; /* message catch event: string-table index of the static message name; else NONE */
@@ -387,7 +388,7 @@ typedef struct zbhip_record {
   uint32_t correlation_key;     /* string id, ZBHIP_NO_STRING = empty */
   uint16_t message_name;        /* name id, 0xFFFF = empty */
   uint16_t bpmn_process_id;     /* name id, 0xFFFF = empty */
-  int32_t partition;            /* PMS: subscriptionPartitionId; else 0 */
+  int32_t partition;            /* PMS: subscriptionPartitionId; TIMER events: repetitions (-1 infinite); else 0 */
   uint8_t interrupting;
   uint8_t unprocessed;          /* a follow-up COMMAND written to the log unprocessed (past
                                    maxCommandsInBatch, ProcessingStateMachine.java:388-417): it

@@ -361,10 +361,12 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
         return write_object(PROCESS_EVENT, dict(scopeKey=int(r["scope_key"]), targetElementId=el[2], variables=pe_vars,
                                                 processDefinitionKey=p["key"],
                                                 processInstanceKey=int(r["process_instance_key"])))
-    if vt == VT_TIMER:  # a rejected TIMER:TRIGGER: the command's key and dueDate (the window's view of it)
+    if vt == VT_TIMER:  # events: the timer's value (repetitions in `partition`); a rejected TIMER:TRIGGER:
+        # the command's key and dueDate (the window's view of it)
+        reps = 1 if rt == RT_REJECTION else int(r["partition"])
         return write_object(TIMER, dict(elementInstanceKey=int(r["scope_key"]),
                                         processInstanceKey=int(r["process_instance_key"]), dueDate=int(r["aux"]),
-                                        targetElementId=el[2] if el is not None else "", repetitions=1,
+                                        targetElementId=el[2] if el is not None else "", repetitions=reps,
                                         processDefinitionKey=p["key"] if p is not None else -1))
     if vt == VT_PIC:
         return write_object(PROCESS_INSTANCE_CREATION, dict(

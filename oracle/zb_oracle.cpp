@@ -338,6 +338,7 @@ struct OEl {
   int attached = -1;               // boundary event: the activity it is attached to (attachedToRef)
   int boundary = -1;               // activity: its (one) boundary event (ExecutableActivity.attach)
   bool interrupting = true;        // boundary event: cancelActivity (ExecutableBoundaryEvent.interrupting)
+  int reps = 1;                    // timer: repetitions (RepeatingInterval; 1 a duration, -1 infinite)
 };
 
 struct OProc {
@@ -470,14 +471,33 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       e.interrupting = k->attr("cancelActivity") != "false";
       const XNode* ted = k->child("timerEventDefinition");
       const XNode* td = ted ? ted->child("timeDuration") : nullptr;
-      if (!td || k->child("messageEventDefinition") || k->child("errorEventDefinition") ||
+      const XNode* tc = ted && !td && !e.interrupting ? ted->child("timeCycle") : nullptr;
+      if ((!td && !tc) || k->child("messageEventDefinition") || k->child("errorEventDefinition") ||
           k->child("signalEventDefinition") || k->child("escalationEventDefinition") ||
           k->child("compensateEventDefinition") || k->child("conditionalEventDefinition")) {
-        err = "boundary event outside the supported subset (timer timeDuration only)";
+        err = "boundary event outside the supported subset (timer timeDuration, or timeCycle when non-interrupting)";
         return false;
       }
-      e.timer_ms = parse_duration_ms(td->text);
-      if (e.timer_ms < 0 || e.timer_ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return false; }
+      std::string dtext = td ? td->text : "";
+      if (tc) {  // RepeatingInterval.parse (bpmn-model/.../util/time/RepeatingInterval.java): "R[n]/interval"
+        std::string t = tc->text;
+        size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+        t = a == std::string::npos ? "" : t.substr(a, b - a + 1);
+        const size_t slash = t.find('/');
+        bool ok = t.size() > 2 && t[0] == 'R' && slash != std::string::npos && t.find('/', slash + 1) == std::string::npos;
+        if (ok && slash == 1) {
+          e.reps = -1;  // RepeatingInterval.INFINITE
+        } else if (ok) {
+          const std::string n = t.substr(1, slash - 1);
+          ok = n.size() <= 3 && n.find_first_not_of("0123456789") == std::string::npos;
+          e.reps = ok ? atoi(n.c_str()) : 0;
+          ok = ok && e.reps >= 1 && e.reps <= 254;
+        }
+        if (!ok) { err = "timer cycle outside the supported subset: " + tc->text; return false; }
+        dtext = t.substr(slash + 1);
+      }
+      e.timer_ms = parse_duration_ms(dtext);
+      if (e.timer_ms < 0 || e.timer_ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + dtext; return false; }
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_TIMER;
@@ -1053,6 +1073,7 @@ class Oracle {
   struct TimerRow {  // TimerInstance (state/instance/TimerInstance.java:23-44)
     PiValue pi;      // process, handler element, process instance key
     int64_t dueDate = 0;
+    int reps = 1;    // repetitions (-1 infinite)
   };
   std::map<std::pair<int64_t, int64_t>, TimerRow> timers_;     // TIMERS [elementInstanceKey, timerKey]
  public:
@@ -1282,8 +1303,8 @@ class Oracle {
   // CatchEventBehavior.subscribeToEvents -> subscribeToMessageEvent (processing/common/CatchEventBehavior.java:111-125,248-283)
   // CatchEventBehavior.subscribeToTimerEvent (processing/common/CatchEventBehavior.java:303-330):
   // dueDate = now + duration, TIMER:CREATED (+key); TimerCreatedApplier stores the TimerInstance
-  void subscribe_to_timer(const OEl& el, int64_t key, const PiValue& v) {
-    const int64_t due = now_ms + el.timer_ms;
+  void subscribe_to_timer(const OEl& el, int64_t key, const PiValue& v) { subscribe_timer_at(key, v, now_ms + el.timer_ms, el.reps); }
+  void subscribe_timer_at(int64_t key, const PiValue& v, int64_t due, int reps) {
     const int64_t tk = next_key();
     ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_TIMER, ZBHIP_TIMER_CREATED, tk);
     rec.r.process_idx = v.proc;
@@ -1291,9 +1312,11 @@ class Oracle {
     rec.r.scope_key = key;
     rec.r.process_instance_key = v.piKey;
     rec.r.aux = due;
+    rec.r.partition = reps;  // TimerRecord.repetitions
     TimerRow t;
     t.pi = v;
     t.dueDate = due;
+    t.reps = reps;
     timers_[{key, tk}] = t;
   }
 
@@ -1326,6 +1349,7 @@ class Oracle {
     rec.r.scope_key = eik;
     rec.r.process_instance_key = t.pi.piKey;
     rec.r.aux = t.dueDate;
+    rec.r.partition = t.reps;
     timers_.erase(it);  // TimerTriggeredApplier
     const int64_t eventKey = next_key();
     ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
@@ -1342,6 +1366,10 @@ class Oracle {
       activate_triggered_event(eventKey, t.pi.elem, eik, eit->second.value.flowScopeKey, eit->second.value);
     else                                              // isElementActivated (catch event)
       pi_command(eik, ZBHIP_PI_COMPLETE_ELEMENT, eit->second.value);
+    // shouldReschedule / rescheduleTimer (TriggerTimerProcessor.java:116-160): a cycle's next timer
+    // from the last dueDate (refreshTimer: Interval.withStart(dueDate)), one repetition fewer
+    if (t.reps == -1 || t.reps > 1)
+      subscribe_timer_at(eik, t.pi, t.dueDate + target.timer_ms, t.reps == -1 ? -1 : t.reps - 1);
   }
 
   // DbEventScopeInstanceState.canTriggerEvent (state/instance/DbEventScopeInstanceState.java:178-182):
@@ -1380,6 +1408,7 @@ class Oracle {
       rec.r.scope_key = eik;
       rec.r.process_instance_key = t.pi.piKey;
       rec.r.aux = t.dueDate;
+      rec.r.partition = t.reps;
       it = timers_.erase(it);
     }
   }
@@ -2302,9 +2331,9 @@ std::string Oracle::dump_state() const {
     const OProc& p = procs[t.pi.proc];
     snprintf(buf, sizeof buf,
              "TIMERS|%lld|%lld|handlerNodeId=%s,processDefinitionKey=%lld,key=%lld,elementInstanceKey=%lld,"
-             "processInstanceKey=%lld,dueDate=%lld,repetitions=1,tenantId=<default>",
+             "processInstanceKey=%lld,dueDate=%lld,repetitions=%d,tenantId=<default>",
              (long long)k.first, (long long)k.second, p.els[t.pi.elem].id.c_str(), (long long)p.def_key,
-             (long long)k.second, (long long)k.first, (long long)t.pi.piKey, (long long)t.dueDate);
+             (long long)k.second, (long long)k.first, (long long)t.pi.piKey, (long long)t.dueDate, t.reps);
     rows.push_back(buf);
     snprintf(buf, sizeof buf, "TIMER_DUE_DATES|%lld|%lld|%lld", (long long)t.dueDate, (long long)k.first,
              (long long)k.second);

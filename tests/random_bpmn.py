@@ -105,8 +105,11 @@ class _Gen:
             self.flow(cur, t)
             if self.boundaries and width == 1 and int(r.integers(0, 2)):
                 # an interrupting timer boundary event: its own end, or back through an XOR merge
-                b = self.node("boundaryEvent", attached=t, duration="PT%dS" % int(r.integers(1, 120)),
-                              cancel=bool(int(r.integers(0, 3))))
+                cancel = bool(int(r.integers(0, 3)))
+                timer = "PT%dS" % int(r.integers(1, 120))
+                if not cancel and int(r.integers(0, 2)):  # a cycle (non-interrupting only)
+                    timer = ("R/" if int(r.integers(0, 2)) else "R%d/" % int(r.integers(1, 4))) + timer
+                b = self.node("boundaryEvent", attached=t, duration=timer, cancel=cancel)
                 # a non-interrupting one always ends on its own (merging back would double the token)
                 if int(r.integers(0, 2)) or not self.nodes[-1][2]["cancel"]:
                     self.flow(b, self.node("endEvent"))
@@ -176,10 +179,11 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
                 out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition messageRef="msg_def"/>'
                            '</intermediateCatchEvent>' % (ind, quoteattr(nid)))
             elif kind == "boundaryEvent":
-                out.append('%s<boundaryEvent id=%s attachedToRef=%s%s><timerEventDefinition><timeDuration>%s'
-                           '</timeDuration></timerEventDefinition></boundaryEvent>'
+                tag = "timeCycle" if extra["duration"].startswith("R") else "timeDuration"
+                out.append('%s<boundaryEvent id=%s attachedToRef=%s%s><timerEventDefinition><%s>%s'
+                           '</%s></timerEventDefinition></boundaryEvent>'
                            % (ind, quoteattr(nid), quoteattr(extra["attached"]),
-                              "" if extra["cancel"] else ' cancelActivity="false"', extra["duration"]))
+                              "" if extra["cancel"] else ' cancelActivity="false"', tag, extra["duration"], tag))
             elif kind == "subProcess":
                 out.append("%s<subProcess id=%s>" % (ind, quoteattr(nid)))
                 render(nid, ind + "  ")

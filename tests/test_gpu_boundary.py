@@ -9,7 +9,7 @@ import pytest
 
 from test_gpu_logserial import Pair
 from test_gpu_timers import _open_work, drive_timers, part_key
-from test_oracle_boundary import multiple_sequence_flows, non_interrupting_process
+from test_oracle_boundary import cycle_process, multiple_sequence_flows, non_interrupting_process
 from test_oracle_timers import NOW
 from zeebe_amd import abi, bpmn
 from zeebe_amd.engine import Partition
@@ -60,6 +60,7 @@ def _non_interrupting_escalation():
 SHAPES = {"multiple_sequence_flows": lambda: multiple_sequence_flows("PT30S"), "linear": _linear_with_boundary,
           "non_interrupting": lambda: non_interrupting_process("PT30S"),
           "non_interrupting_escalation": _non_interrupting_escalation,
+          "cycle_infinite": lambda: cycle_process("R/PT30S"), "cycle_r3": lambda: cycle_process("R3/PT10S"),
           "in_sub_process": _boundary_in_sub_process, "then_catch": _boundary_then_catch,
           "to_gateway": _boundary_to_gateway}
 
@@ -120,7 +121,8 @@ def test_gpu_random_processes_with_boundary_events(seed):
     assert [r for r in part.state() if not r.startswith("KEY|")] == []
 
 
-@pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch", "non_interrupting_escalation"])
+@pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch", "non_interrupting_escalation",
+                                   "cycle_r3"])
 def test_gpu_boundary_log_and_db_bytes(shape):
     pair = Pair(SHAPES[shape](), 100)
     for e in (pair.part, pair.orc):
@@ -136,7 +138,7 @@ def test_gpu_boundary_log_and_db_bytes(shape):
         pair.window(c)
 
 
-@pytest.mark.parametrize("shape", ["linear", "in_sub_process", "non_interrupting_escalation"])
+@pytest.mark.parametrize("shape", ["linear", "in_sub_process", "non_interrupting_escalation", "cycle_infinite"])
 def test_gpu_boundary_restart_equivalence(shape):
     xml = SHAPES[shape]()
     n = 48

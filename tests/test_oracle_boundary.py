@@ -238,10 +238,77 @@ def test_boundary_model_subset():
     task, timer = ids.index("task"), ids.index("timer")
     assert int(c.els[timer]["element_type"]) == abi.ELEMENT_TYPES.index("BOUNDARY_EVENT")
     assert int(c.els[timer]["flow_source"]) == task and int(c.els[task]["start_event"]) == timer
-    assert int(c.els[timer]["duration_ms"]) == 120000 and int(c.els[timer]["job_retries"]) == 1
+    # job_retries of a boundary event: interrupting | repetitions << 8
+    assert int(c.els[timer]["duration_ms"]) == 120000 and int(c.els[timer]["job_retries"]) == 1 | (1 << 8)
     c = Compiled(non_interrupting_process())
     ids = [c.id(i) for i in range(len(c.els))]
-    assert int(c.els[ids.index("event")]["job_retries"]) == 0  # cancelActivity="false"
+    assert int(c.els[ids.index("event")]["job_retries"]) == 0 | (1 << 8)  # cancelActivity="false"
+    for cycle, reps in (("R/PT1S", 255), ("R3/PT2M", 3), ("R254/PT1S", 254)):
+        c = Compiled(_boundary_model(' cancelActivity="false"', _cycle(cycle)))
+        ids = [c.id(i) for i in range(len(c.els))]
+        assert int(c.els[ids.index("b")]["job_retries"]) == reps << 8, cycle
+        Oracle().deploy(_boundary_model(' cancelActivity="false"', _cycle(cycle)))
+    for xml in (_boundary_model("", _cycle("R/PT1S")), _boundary_model(' cancelActivity="false"', _cycle("R0/PT1S")),
+                _boundary_model(' cancelActivity="false"', _cycle("R255/PT1S")),
+                _boundary_model(' cancelActivity="false"', _cycle("R/2024-01-01T00:00:00Z/PT1S"))):
+        with pytest.raises(ZbhipError):
+            Compiled(xml)
+        with pytest.raises(OracleError):
+            Oracle().deploy(xml)
+
+
+def _cycle(text):
+    return '<timerEventDefinition id="t"><timeCycle>%s</timeCycle></timerEventDefinition>' % text
+
+
+def cycle_process(cycle="R/PT1S"):
+    """BoundaryEventTest.NON_INTERRUPTING_PROCESS (:61-69) with the static cycle its
+    `cycle(duration("PT1S"))` expression evaluates to (R/PT1S: infinite repetitions)."""
+    b = bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "type").boundaryEvent("event")
+    b.cancelActivity(False).timerWithCycle(cycle).endEvent("eventEnd").moveToActivity("task")
+    return b.endEvent("taskEnd").done()
+
+
+def test_non_interrupting_cycle_reschedules():
+    # BoundaryEventTest.shouldNotTerminateActivityForNonInterruptingBoundaryEvents (:274-313), exactly:
+    # TIMER TRIGGERED, TIMER CREATED (the cycle's next), JOB COMPLETED, task COMPLETING,
+    # TIMER CANCELED, task COMPLETED
+    o, recs = _started(cycle_process())
+    created = [r for r in recs if r["value_type"] == abi.VT_TIMER][0]
+    assert int(created["partition"]) == -1  # TimerRecord.repetitions: RepeatingInterval.INFINITE
+    fired = _trigger_all(o, recs)
+    timers = [r for r in fired if r["value_type"] == abi.VT_TIMER]
+    assert [abi.TIMER_INTENTS[int(r["intent"])] for r in timers] == ["TRIGGERED", "CREATED"]
+    nxt = timers[1]
+    assert int(nxt["aux"]) == int(created["aux"]) + 1000 and int(nxt["key"]) > int(created["key"])
+    assert int(nxt["scope_key"]) == int(created["scope_key"]) and int(nxt["partition"]) == -1
+    # the rescheduled CREATED follows the boundary event's activation (TriggerTimerProcessor.java:109-116)
+    seq = [_tuple(o, r) for r in fired]
+    assert seq.index(("TIMER", "CREATED", "event")) > seq.index(("PROCESS_INSTANCE", "COMPLETE_ELEMENT", "event"))
+    done = _complete_jobs(o, recs)
+    it = iter([_tuple(o, r) for r in recs + fired + done])
+    want = [("TIMER", "TRIGGERED", "event"), ("TIMER", "CREATED", "event"), ("JOB", "COMPLETED", "task"),
+            ("PROCESS_INSTANCE", "ELEMENT_COMPLETING", "task"), ("TIMER", "CANCELED", "event"),
+            ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "task")]
+    assert all(w in it for w in want)
+    assert [r for r in o.state() if not r.startswith("KEY|")] == []
+
+
+def test_cycle_with_repetitions_stops():
+    # R3: three triggers (repetitions 3, 2, 1 in the records), then no timer is left
+    o, recs = _started(cycle_process("R3/PT10S"))
+    seen = []
+    for _ in range(4):
+        open_timers = [r for r in o.state() if r.startswith("TIMERS|")]
+        if not open_timers:
+            break
+        created = [r for r in recs if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CREATED][-1:]
+        fired = _trigger_all(o, created)
+        seen += [(abi.TIMER_INTENTS[int(r["intent"])], int(r["partition"])) for r in fired
+                 if r["value_type"] == abi.VT_TIMER]
+        recs = fired
+    assert seen == [("TRIGGERED", 3), ("CREATED", 2), ("TRIGGERED", 2), ("CREATED", 1), ("TRIGGERED", 1)]
+    assert any(r.startswith("JOBS|") for r in o.state())  # the activity is still waiting
 
 
 def test_product_serializer_and_state_encoder_on_boundary_records():

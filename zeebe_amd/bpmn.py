@@ -162,6 +162,11 @@ class ProcessBuilder:
     def moveToActivity(self, id_):
         return self.moveToNode(id_)
 
+    def timerWithCycle(self, cycle):
+        """BoundaryEventBuilder.timerWithCycle: <timerEventDefinition><timeCycle>."""
+        self.current.timer = ("cycle", cycle)
+        return self
+
     def timerWithDuration(self, duration):
         """IntermediateCatchEventBuilder.timerWithDuration: <timerEventDefinition><timeDuration>."""
         self.current.timer = duration
@@ -256,7 +261,10 @@ class ProcessBuilder:
                 elif c.kind == "boundaryEvent":
                     cancel = "" if c.cancel_activity else ' cancelActivity="false"'
                     body = ""
-                    if c.timer:
+                    if isinstance(c.timer, tuple):
+                        body = ('<timerEventDefinition id=%s><timeCycle>%s</timeCycle></timerEventDefinition>'
+                                % (quoteattr(c.id + "_ted"), escape(c.timer[1])))
+                    elif c.timer:
                         body = ('<timerEventDefinition id=%s><timeDuration>%s</timeDuration></timerEventDefinition>'
                                 % (quoteattr(c.id + "_ted"), escape(c.timer)))
                     out.append('%s<boundaryEvent id=%s attachedToRef=%s%s>%s</boundaryEvent>'

@@ -520,14 +520,39 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         // BoundaryEventTransformer: timer boundary events (a static timeDuration; interrupting or not)
         // on job worker tasks; attached after the walk
         const std::string* ca = c.get("cancelActivity");  // BoundaryEvent default: interrupting
-        e.job_retries = ca && *ca == "false" ? 0 : 1;
+        const bool interrupting = !(ca && *ca == "false");
         const Elem* ted = c.first("timerEventDefinition");
         const Elem* td = ted ? ted->first("timeDuration") : nullptr;
+        const Elem* tc = ted && !td ? ted->first("timeCycle") : nullptr;
         for (auto& d : c.children)
-          if (&d != ted && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) td = nullptr;
-        if (!td) { err = "boundary event outside the supported subset (timer timeDuration only)"; return ZBHIP_EUNSUPP; }
-        const int64_t ms = duration_ms(td->text);
-        if (ms < 0 || ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return ZBHIP_EUNSUPP; }
+          if (&d != ted && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) td = tc = nullptr;
+        // a static timeCycle "R[n]/duration" (RepeatingInterval.parse) on a non-interrupting
+        // boundary event: repetitions n (1..254) or infinite (255); a duration: 1
+        uint32_t reps = 1;
+        std::string dtext = td ? td->text : "";
+        if (tc && !interrupting) {
+          std::string t = tc->text;
+          const size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+          t = a == std::string::npos ? "" : t.substr(a, b - a + 1);
+          const size_t slash = t.find('/');
+          bool ok = t.size() > 2 && t[0] == 'R' && slash != std::string::npos && t.find('/', slash + 1) == std::string::npos;
+          if (ok && slash == 1) {
+            reps = 255;
+          } else if (ok) {
+            const std::string n = t.substr(1, slash - 1);
+            ok = n.size() <= 3 && n.find_first_not_of("0123456789") == std::string::npos;
+            reps = ok ? (uint32_t)atoi(n.c_str()) : 0;
+            ok = ok && reps >= 1 && reps <= 254;
+          }
+          if (!ok) { err = "timer cycle outside the supported subset: " + tc->text; return ZBHIP_EUNSUPP; }
+          dtext = t.substr(slash + 1);
+        } else if (!td) {
+          err = "boundary event outside the supported subset (timer timeDuration, or timeCycle when non-interrupting)";
+          return ZBHIP_EUNSUPP;
+        }
+        e.job_retries = (uint16_t)((interrupting ? 1u : 0u) | (reps << 8));
+        const int64_t ms = duration_ms(dtext);
+        if (ms < 0 || ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + dtext; return ZBHIP_EUNSUPP; }
         if (const Elem* ext = c.first("extensionElements"))
           if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
         const std::string* at = c.get("attachedToRef");

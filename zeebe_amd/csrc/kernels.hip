@@ -1107,7 +1107,7 @@ __device__ __forceinline__ void activate_triggered_event(Lane<K>& L, uint32_t pe
 // TimerTriggeredApplier (the row removed), then EventHandle.activateElement (EventHandle.java:104-131):
 // PROCESS_EVENT:TRIGGERING (+key, no variables) and COMPLETE_ELEMENT for the catch event
 template <class K>
-__device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord) {
+__device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord, long long cmd_due) {
   if (L.proc == NONE || !L.pi_live || !(L.tm_y >> 31) || (L.tm_x >> 16) != tord) {
     emit(L, kRejectBit | C_TIMER_TRIGGER, tord, NONE, NONE, ZBHIP_REASON_TIMER_NOT_FOUND);
     return;
@@ -1118,20 +1118,31 @@ __device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord) {
     emit(L, kRejectBit | C_TIMER_TRIGGER, tord, NONE, NONE, ZBHIP_REASON_TIMER_NOT_ACTIVE);
     return;
   }
-  emit(L, C_TIMER_TRIGGERED, tord, eord, elem);
+  const uint32_t reps = (L.tm_y >> 16) & 0xFF;  // TimerRecord.repetitions (255: infinite)
+  emit(L, C_TIMER_TRIGGERED, tord, eord, elem, reps);
   L.tm_x = L.tm_y = 0;
   L.tm_due = 0;
   const uint32_t pe = new_key(L);
   emit(L, C_PE_TRIGGERING, pe, eord, elem);
   L.trig_key = (uint16_t)eord;  // ProcessEventTriggeringApplier: EVENT_TRIGGER row (no variables)
   const uint4 bw = elem_of(L, elem);
-  if (etype(bw) == ZBHIP_EL_BOUNDARY_EVENT && (bw.w & 0xFFFF) == 0) {
+  if (etype(bw) == ZBHIP_EL_BOUNDARY_EVENT && (bw.w & 1) == 0) {
     // a non-interrupting boundary event: EventHandle.activateElement -> activateTriggeredEvent in
     // this batch; the activity stays active (its EVENT_TRIGGER row is deleted by TRIGGERED)
     L.trig_key = NONE;
     const uint32_t task = tget(L, t).x & 0xFFFF;
     const uint32_t c = scope_of<K>(elem_of(L, task));
     activate_triggered_event(L, pe, eord, elem, scope_key(L, c));
+    // shouldReschedule / rescheduleTimer (TriggerTimerProcessor.java:116-160): a cycle's next timer
+    // from the command's dueDate (refreshTimer), one repetition fewer
+    if (reps == 255 || reps > 1) {
+      const uint32_t nr = reps == 255 ? 255u : reps - 1;
+      const uint32_t tk = new_key(L);
+      L.tm_x = elem | (tk << 16);
+      L.tm_y = eord | (nr << 16) | (1u << 31);
+      L.tm_due = cmd_due + (long long)bw.z;
+      emit(L, C_TIMER_NEXT, tk, eord, elem, nr);
+    }
     return;
   }
   if (etype(bw) == ZBHIP_EL_BOUNDARY_EVENT) {
@@ -1155,7 +1166,7 @@ __device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord) {
 // entry: at most one timer is canceled per batch); TimerCancelledApplier removes the row
 template <class K>
 __device__ __forceinline__ void cancel_timer(Lane<K>& L) {
-  emit(L, C_TIMER_CANCELED, L.tm_x >> 16, L.tm_y & 0xFFFF, L.tm_x & 0xFFF);
+  emit(L, C_TIMER_CANCELED, L.tm_x >> 16, L.tm_y & 0xFFFF, L.tm_x & 0xFFF, (L.tm_y >> 16) & 0xFF);
   L.sp->cmd_due[L.ci] = L.tm_due;
   L.tm_x = L.tm_y = 0;
   L.tm_due = 0;
@@ -1295,11 +1306,13 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
           const uint32_t b = w.w & 0xFFFF;
           if (b != 0xFFFF) {
             if (!L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
+            const uint4 bw = elem_of(L, b);
+            const uint32_t reps = (bw.w >> 8) & 0xFF;  // 1 a duration, a cycle's count, 255 infinite
             const uint32_t tk = new_key(L);
             L.tm_x = b | (tk << 16);
-            L.tm_y = key | (1u << 31);
-            L.tm_due = L.sp->now_ms + (long long)elem_of(L, b).z;
-            emit(L, C_TIMER_CREATED, tk, key, b);
+            L.tm_y = key | (reps << 16) | (1u << 31);
+            L.tm_due = L.sp->now_ms + (long long)bw.z;
+            emit(L, C_TIMER_CREATED, tk, key, b, reps);
           }
         }
         uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
@@ -1334,9 +1347,9 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
           if (((w.x >> 8) & 0xFF) != ZBHIP_EV_TIMER || !L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
           const uint32_t tk = new_key(L);
           L.tm_x = elem | (tk << 16);
-          L.tm_y = key | (1u << 31);
+          L.tm_y = key | (1u << 16) | (1u << 31);  // one repetition (a duration)
           L.tm_due = L.sp->now_ms + (long long)w.z;
-          emit(L, C_TIMER_CREATED, tk, key, elem);
+          emit(L, C_TIMER_CREATED, tk, key, elem, 1);
           emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
           tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
         } else {
@@ -2113,7 +2126,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       }
     }
   } else if (!L.fail && kind == ZBHIP_CMD_TIMER_TRIGGER) {
-    if constexpr (K::S) trigger_timer(L, ref);
+    if constexpr (K::S) trigger_timer(L, ref, (long long)(((unsigned long long)cw.w << 32) | cw.z));
     else set_fail(L, FB_UNSUPPORTED);
   } else if (!L.fail && kind == CMD_FOLLOWUP) {
     // written to the log past the batch limit: the command is this batch's initial command

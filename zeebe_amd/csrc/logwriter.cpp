@@ -445,7 +445,7 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
         key(value, "dueDate"); mp_int(value, r.aux);
         key(value, "targetElementId"); mp_str(value, E ? E->id : std::string());
-        key(value, "repetitions"); mp_int(value, 1);
+        key(value, "repetitions"); mp_int(value, r.record_type == ZBHIP_RT_REJECTION ? 1 : r.partition);
         key(value, "processDefinitionKey"); mp_int(value, P ? P->def_key : -1);
         key(value, "tenantId"); key(value, kTenant);
         break;

@@ -1842,17 +1842,21 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.intent = ZBHIP_TIMER_CANCELED;
       r.record_type = ZBHIP_RT_EVENT;
       r.aux = c < h->h_cmd_due.size() ? h->h_cmd_due[c] : -1;
-    } else if (c6 == C_TIMER_CREATED || c6 == C_TIMER_TRIGGERED || c6 == C_TIMER_TRIGGER) {
+      r.partition = fl == 255 ? -1 : (int32_t)fl;  // TimerRecord.repetitions
+    } else if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT || c6 == C_TIMER_TRIGGERED || c6 == C_TIMER_TRIGGER) {
       // TimerRecord: elementInstanceKey (scope_key), dueDate in aux -- CREATED: the run's clock plus
       // the element's duration (CatchEventBehavior.java:310); TRIGGERED / a rejected TRIGGER: the
       // command's TimerRecord (TriggerTimerProcessor.java:108: the TIMER:TRIGGER value)
       r.value_type = ZBHIP_VT_TIMER;
-      r.intent = c6 == C_TIMER_CREATED ? ZBHIP_TIMER_CREATED : c6 == C_TIMER_TRIGGERED ? ZBHIP_TIMER_TRIGGERED
-                                                                                      : ZBHIP_TIMER_TRIGGER;
+      r.intent = c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT ? ZBHIP_TIMER_CREATED
+                 : c6 == C_TIMER_TRIGGERED ? ZBHIP_TIMER_TRIGGERED : ZBHIP_TIMER_TRIGGER;
       r.record_type = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
       const int64_t cmd_due = (int64_t)((uint64_t)cm.doc_begin | ((uint64_t)cm.pad << 32));
       const zbhip_element* E = proc != NONE && elem < h->procs[proc].els.size() ? &h->procs[proc].els[elem] : nullptr;
-      r.aux = c6 == C_TIMER_CREATED ? h->run_clock_ms + (E ? (int64_t)E->duration_ms : 0) : cmd_due;
+      // a cycle's next timer counts from the TRIGGER command's dueDate (refreshTimer), others from the clock
+      const int64_t dur = E ? (int64_t)E->duration_ms : 0;
+      r.aux = c6 == C_TIMER_CREATED ? h->run_clock_ms + dur : c6 == C_TIMER_NEXT ? cmd_due + dur : cmd_due;
+      if (!rej) r.partition = fl == 255 ? -1 : (int32_t)fl;  // TimerRecord.repetitions
     } else {
       return ZBHIP_EDEVICE;  // corrupt record
     }
@@ -2267,7 +2271,7 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       const bool own = E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT;
       const bool bnd = ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16;
       const std::string ids = own ? P.id(elem) : bnd ? P.id(E.start_event) : std::string();
-      const bool intr = own || (bnd && P.els[E.start_event].job_retries);  // cancelActivity boundary events only
+      const bool intr = own || (bnd && (P.els[E.start_event].job_retries & 1));  // cancelActivity boundary events only
       snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=%s", k,
                intr ? ids.c_str() : "", bnd ? ids.c_str() : "");
       sink(ctx, buf);
@@ -2306,8 +2310,9 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     const long long due = (long long)(((unsigned long long)R.tmr.w << 32) | R.tmr.z);
     snprintf(buf, sizeof buf,
              "TIMERS|%lld|%lld|handlerNodeId=%s,processDefinitionKey=%lld,key=%lld,elementInstanceKey=%lld,"
-             "processInstanceKey=%lld,dueDate=%lld,repetitions=1,tenantId=<default>",
-             eik, tk, P.id(R.tmr.x & 0xFFF).c_str(), (long long)P.def_key, tk, eik, pik, due);
+             "processInstanceKey=%lld,dueDate=%lld,repetitions=%d,tenantId=<default>",
+             eik, tk, P.id(R.tmr.x & 0xFFF).c_str(), (long long)P.def_key, tk, eik, pik, due,
+             ((R.tmr.y >> 16) & 0xFF) == 255 ? -1 : (int)((R.tmr.y >> 16) & 0xFF));
     sink(ctx, buf);
     snprintf(buf, sizeof buf, "TIMER_DUE_DATES|%lld|%lld|%lld", due, eik, tk);
     sink(ctx, buf);
@@ -2547,6 +2552,7 @@ struct ImpVar {
 struct ImpTimer {
   int64_t eik = 0, key = 0, due = 0;
   std::string handler;
+  uint32_t reps = 1;  // repetitions as the timer row holds them (255 infinite)
 };
 struct ImpPms {
   int64_t eik = 0, key = 0;
@@ -2621,8 +2627,9 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       pms.push_back(m);
     } else if (cf == "TIMERS" && p.size() >= 4) {
       auto f = row_fields(p[3]);
-      if (to_ll(f["repetitions"]) != 1) return ZBHIP_EUNSUPP;  // cycles: outside the subset
-      timers.push_back({to_ll(p[1]), to_ll(p[2]), to_ll(f["dueDate"]), f["handlerNodeId"]});
+      const int64_t reps = to_ll(f["repetitions"]);  // -1 (infinite) or 1..254 on the device
+      if (reps != -1 && (reps < 1 || reps > 254)) return ZBHIP_EUNSUPP;
+      timers.push_back({to_ll(p[1]), to_ll(p[2]), to_ll(f["dueDate"]), f["handlerNodeId"], reps == -1 ? 255u : (uint32_t)reps});
     } else if (cf == "MESSAGE_SUBSCRIPTION_BY_KEY" || cf == "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY") {
       return ZBHIP_EUNSUPP;  // message-partition rows: no routing handle to the subscriber's slot
     } else if (cf == "MESSAGE_STATS") {
@@ -2786,7 +2793,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     if (tmr) {
       const int el = elem_of_id(tmr->handler);
       if (el < 0 || !P.has_timer) return ZBHIP_EINVAL;
-      tmrrow[inst] = make_uint4((uint32_t)el | (ord(tmr->key) << 16), ord(tmr->eik) | (1u << 31),
+      tmrrow[inst] = make_uint4((uint32_t)el | (ord(tmr->key) << 16), ord(tmr->eik) | (tmr->reps << 16) | (1u << 31),
                                 (uint32_t)(uint64_t)tmr->due, (uint32_t)((uint64_t)tmr->due >> 32));
     }
     hdr[inst] = make_uint4((uint32_t)proc | ((uint32_t)keys.size() << 16),

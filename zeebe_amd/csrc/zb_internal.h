@@ -74,10 +74,13 @@ enum : uint8_t {
   C_MS_CORRELATED = 44,
   C_MSG_PUBLISHED = 49,
   C_MSG_EXPIRED = 50,
-  C_TIMER_CREATED = 52,   // key = timer, aux = element instance (TimerRecord, CatchEventBehavior.java:303-330)
+  C_TIMER_CREATED = 52,   // key = timer, aux = element instance, flags = repetitions (255 infinite)
+                          // (TimerRecord, CatchEventBehavior.java:303-330)
   C_TIMER_TRIGGER = 53,   // (rejections of TIMER:TRIGGER)
   C_TIMER_TRIGGERED = 54,
   C_TIMER_CANCELED = 55,  // CatchEventBehavior.unsubscribeFromTimerEvent; dueDate in StepParams.cmd_due
+  C_TIMER_NEXT = 56,      // TIMER:CREATED of a cycle's next timer (rescheduleTimer): dueDate from the
+                          // TRIGGER command's, not the run's clock
   kRejectBit = 0x40,
 };
 
@@ -129,7 +132,7 @@ constexpr uint8_t CMD_FOLLOWUP = 0x20;
 //                                 event: duration ms; sub-process: none start event | join slots of its
 //                                 gateways << 16
 //                            w3 = join_slot (job worker: its boundary event or 0xFFFF; boundary event:
-//                                 1 interrupting, 0 not) | container
+//                                 interrupting | repetitions << 8) | container
 //                                 (flow scope element; 0 = the process) << 16
 //   p[out_off]  u16 outgoing flows (two per word)
 //   p[cond_off] u32 first instruction of each condition
@@ -158,7 +161,8 @@ struct DevState {
   uint32_t n_slots;
   uint4* tmr;        // [n] the instance's timer (KScope; one per instance): x = catch / boundary element |
                      //     timer key ordinal << 16, y = element-instance ordinal (the catch event's, or the
-                     //     activity's a boundary event is attached to) | live << 31, z/w = dueDate lo/hi
+                     //     activity's a boundary event is attached to) | repetitions << 16 (255 infinite)
+                     //     | live << 31, z/w = dueDate lo/hi
 };
 
 // elements without behaviour: ACTIVATING, ACTIVATED, COMPLETE_ELEMENT, COMPLETING, COMPLETED, then
