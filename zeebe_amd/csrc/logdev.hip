@@ -31,10 +31,11 @@ enum LogRun : uint32_t {
   G_AUTH, G_TENANT, G_FLOWSCOPE, G_EMPTY_BIN, G_JREJ_HEAD, G_JREJ_TAIL, G_VAR_A, G_VAR_VALUE, G_VAR_SCOPE,
   G_K_PIK, G_K_DEF, G_K_BPMN, G_PE_A, G_PE_TARGET, G_K_VARS, G_PIC_A, G_K_VERSION, G_PIC_TAIL,
   G_RS_PGW_A, G_RS_PGW_B, G_RS_FSNF_A, G_RS_NF_B, G_RS_FSST_A, G_RS_Q, G_RS_EINF_A, G_RS_EIST_A, G_RS_JOB_A,
-  G_RS_JOB_B, G_ST0, G_COUNT = G_ST0 + 16
+  G_RS_JOB_B, G_RS_TNF_A, G_RS_TNF_B, G_RS_TNA_A, G_RS_TNA_B, G_TIMER_A, G_TIMER_DUE, G_TIMER_REPS, G_ST0,
+  G_COUNT = G_ST0 + 16
 };
-// element runs (proc block word 6 + 14 e)
-enum ElRun : uint32_t { E_PI_HEAD, E_PI_TAIL, E_JOB_HEAD, E_JOB_MID, E_JOB_TAIL, E_ID_STR, E_ID_RAW, E_COUNT };
+// element runs (proc block word 6 + 16 e); E_DUR is the timer duration in ms (.x), not a byte run
+enum ElRun : uint32_t { E_PI_HEAD, E_PI_TAIL, E_JOB_HEAD, E_JOB_MID, E_JOB_TAIL, E_ID_STR, E_ID_RAW, E_DUR, E_COUNT };
 
 struct LogParams {
   const uint2* rows;            // gathered compact rows (launch order)
@@ -55,6 +56,8 @@ struct LogParams {
   unsigned long long* bytes;    // [n] entry bytes of each command, then (scanned) byte offsets
   uint64_t* out;                // log bytes (8-byte aligned entries)
   uint32_t* flag;               // bit 0: an unresolved key / unsupported value (host serialiser instead)
+  long long now_ms;             // the run's clock: TIMER:CREATED dueDate = clock + duration
+  const long long* cmd_due;     // [n] dueDate of the timer each batch canceled
 };
 
 __device__ __forceinline__ uint2 run(const LogParams& L, uint32_t i) {
@@ -182,6 +185,8 @@ __device__ __forceinline__ void dec(S& s, long long v) {
 // ---- one record -------------------------------------------------------------------------------
 struct Rec {
   long long key, scope, pik;
+  long long due;            // TIMER: dueDate
+  int reps;                 // TIMER: repetitions (-1 infinite)
   uint32_t proc, elem;      // NONE when not applicable
   uint8_t rt, vt, intent, rej_type, reason, reason_arg, skip;
 };
@@ -229,18 +234,38 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
     r.intent = (uint8_t)c6;
     r.rt = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
     r.skip = !rej && c6 >= 8 && !(fl & F_UNPROCESSED) ? 1 : 0;  // a follow-up command processed in its batch
-  } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE) {
+  } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE || c6 == C_JOB_CANCELED) {
     r.vt = ZBHIP_VT_JOB;
-    r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED : ZBHIP_JOB_COMPLETE;
+    r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED
+               : c6 == C_JOB_CANCELED ? ZBHIP_JOB_CANCELED : ZBHIP_JOB_COMPLETE;
     r.rt = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
   } else if (c6 == C_VAR_CREATED || c6 == C_VAR_UPDATED) {
     r.vt = ZBHIP_VT_VARIABLE;
     r.intent = c6 == C_VAR_CREATED ? ZBHIP_VAR_CREATED : ZBHIP_VAR_UPDATED;
     r.rt = ZBHIP_RT_EVENT;
-  } else if (c6 == C_PE_TRIGGERING) {
+  } else if (c6 == C_PE_TRIGGERING || c6 == C_PE_TRIGGERED) {
     r.vt = ZBHIP_VT_PROCESS_EVENT;
-    r.intent = ZBHIP_PE_TRIGGERING;
+    r.intent = c6 == C_PE_TRIGGERING ? ZBHIP_PE_TRIGGERING : ZBHIP_PE_TRIGGERED;
     r.rt = ZBHIP_RT_EVENT;
+  } else if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT || c6 == C_TIMER_TRIGGERED || c6 == C_TIMER_TRIGGER ||
+             c6 == C_TIMER_CANCELED) {
+    // TimerRecord (runtime.cpp expand_plain): CREATED from the clock, a cycle's next timer from the
+    // TRIGGER command's dueDate, TRIGGERED / a rejected TRIGGER the command's, CANCELED the stored one
+    r.vt = ZBHIP_VT_TIMER;
+    r.intent = c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT ? ZBHIP_TIMER_CREATED
+               : c6 == C_TIMER_TRIGGERED ? ZBHIP_TIMER_TRIGGERED : c6 == C_TIMER_CANCELED ? ZBHIP_TIMER_CANCELED
+               : ZBHIP_TIMER_TRIGGER;
+    r.rt = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
+    const long long cmd = (long long)(((unsigned long long)m.pad << 32) | m.doc_begin);
+    long long dur = 0;
+    if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT) {
+      const uint32_t pb = r.proc != NONE ? proc_block(L, r.proc) : 0u;
+      if (!pb || elem >= L.idx[pb + 5]) return false;
+      dur = (long long)el_run(L, pb, elem, E_DUR).x;
+    }
+    r.due = c6 == C_TIMER_CREATED ? L.now_ms + dur : c6 == C_TIMER_NEXT ? cmd + dur
+            : c6 == C_TIMER_CANCELED ? L.cmd_due[c] : cmd;
+    r.reps = rej ? 1 : fl == 255 ? -1 : (int)fl;
   } else if (c6 == C_PIC_CREATED) {
     r.vt = ZBHIP_VT_PROCESS_INSTANCE_CREATION;
     r.intent = ZBHIP_PIC_CREATED;
@@ -253,6 +278,12 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
     r.reason_arg = fl >> 4;
     if (r.vt == ZBHIP_VT_JOB) {
       r.rej_type = ZBHIP_REJ_NOT_FOUND;
+      r.proc = NONE;
+      r.elem = NONE;
+      r.scope = -1;
+      r.pik = -1;
+    } else if (r.vt == ZBHIP_VT_TIMER) {  // the TIMER:TRIGGER command's value
+      r.rej_type = r.reason == ZBHIP_REASON_TIMER_NOT_FOUND ? ZBHIP_REJ_NOT_FOUND : ZBHIP_REJ_INVALID_STATE;
       r.proc = NONE;
       r.elem = NONE;
       r.scope = -1;
@@ -324,6 +355,12 @@ __device__ __forceinline__ void reason_text(S& s, const LogParams& L, const Rec&
     case ZBHIP_REASON_JOB_NOT_FOUND:
       s.bytes(L, run(L, G_RS_JOB_A)); dec(s, r.key); s.bytes(L, run(L, G_RS_JOB_B));
       return;
+    case ZBHIP_REASON_TIMER_NOT_FOUND:
+      s.bytes(L, run(L, G_RS_TNF_A)); dec(s, r.key); s.bytes(L, run(L, G_RS_TNF_B));
+      return;
+    case ZBHIP_REASON_TIMER_NOT_ACTIVE:
+      s.bytes(L, run(L, G_RS_TNA_A)); dec(s, r.key); s.bytes(L, run(L, G_RS_TNA_B));
+      return;
     default:
       return;
   }
@@ -389,11 +426,29 @@ __device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m,
       s.bytes(L, run(L, G_PE_TARGET));
       s.bytes(L, el_run(L, pb, r.elem, E_ID_STR));
       s.bytes(L, run(L, G_K_VARS));
-      src_doc_bin(s, L, m);
+      if (r.intent == ZBHIP_PE_TRIGGERED) s.bytes(L, run(L, G_EMPTY_BIN));  // processEventTriggered: reset record
+      else src_doc_bin(s, L, m);
       s.bytes(L, run(L, G_K_DEF));
       mp_int(s, (long long)(((unsigned long long)L.idx[pb + 3] << 32) | L.idx[pb + 2]));
       s.bytes(L, run(L, G_K_PIK));
       mp_int(s, r.pik);
+      s.bytes(L, run(L, G_TENANT));
+      return true;
+    case ZBHIP_VT_TIMER:  // TimerRecord.java:24-40
+      if (r.rt != ZBHIP_RT_REJECTION && !has_el) return false;
+      s.bytes(L, run(L, G_TIMER_A));
+      mp_int(s, r.scope);
+      s.bytes(L, run(L, G_K_PIK));
+      mp_int(s, r.pik);
+      s.bytes(L, run(L, G_TIMER_DUE));
+      mp_int(s, r.due);
+      s.bytes(L, run(L, G_PE_TARGET));
+      if (has_el) s.bytes(L, el_run(L, pb, r.elem, E_ID_STR));
+      else s.b(0xa0);  // ""
+      s.bytes(L, run(L, G_TIMER_REPS));
+      mp_int(s, r.reps);
+      s.bytes(L, run(L, G_K_DEF));
+      mp_int(s, has_el ? (long long)(((unsigned long long)L.idx[pb + 3] << 32) | L.idx[pb + 2]) : -1LL);
       s.bytes(L, run(L, G_TENANT));
       return true;
     case ZBHIP_VT_PROCESS_INSTANCE_CREATION:
@@ -572,7 +627,7 @@ __global__ __launch_bounds__(256) void k_ring_add(LogParams L) {
 hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
   LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.arena_words, a.idx_words, a.docs, a.n_docs, a.inst_proc, a.ring,
               a.kpi, a.n_inst, a.pbits, a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]},
-              a.bytes, a.out, a.flag};
+              a.bytes, a.out, a.flag, a.now_ms, a.cmd_due};
   const uint32_t g = (a.n + 255) / 256;
   const size_t lds = a.arena_words + a.idx_words <= kLdsTableWords ? (size_t)(a.arena_words + a.idx_words) * 4 : 0;
   if (a.phase == 0) {  // sizes and byte offsets

@@ -108,6 +108,7 @@ const Bytes kEmptyDoc("\x80", 1);   // MsgPackHelper.EMTPY_OBJECT (DocumentValue
 struct SerElement {
   uint8_t type = 0, event = 0;
   std::string id;
+  uint32_t duration_ms = 0;  // timer catch / boundary event (the device log path's TIMER dueDates)
   // ProcessInstanceRecord: [map, bpmnElementType .. processDefinitionKey, "processInstanceKey"] key
   // ["flowScopeKey"] key [bpmnEventType .. tenantId]
   Bytes pi_head, pi_tail;
@@ -193,6 +194,7 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
     S.type = E.element_type;
     S.event = E.element_type == ZBHIP_EL_PROCESS ? ZBHIP_EV_UNSPECIFIED : E.event_type;
     S.id = str(E.id);
+    S.duration_ms = E.duration_ms;
     // ProcessInstanceRecord (declaration order ProcessInstanceRecord.java:63-73)
     mp_map(S.pi_head, 11);
     key(S.pi_head, "bpmnElementType");
@@ -1268,8 +1270,13 @@ int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, st
                         "Expected flow scope instance to be in state 'ELEMENT_ACTIVATED' but was '", "'.",
                         "Expected element instance with key '",
                         "Expected element instance to be in state 'ELEMENT_ACTIVATED' or one of '[ELEMENT_COMPLETING]' but was '",
-                        "Expected to complete job with key '", "', but no such job was found"})
+                        "Expected to complete job with key '", "', but no such job was found",
+                        "Expected to trigger timer with key '", "', but no such timer was found",
+                        "Expected to trigger a timer with key '", "', but the timer is not active anymore"})
     push(Bytes(t));                                                   // G_RS_*
+  b.clear(); mp_map(b, 7); key(b, "elementInstanceKey"); push(b);     // G_TIMER_A (TimerRecord.java:24-40)
+  push(k({"dueDate"}));                                               // G_TIMER_DUE
+  push(k({"repetitions"}));                                           // G_TIMER_REPS
   for (int st = 0; st < 16; ++st) push(Bytes(state_text(st)));       // G_ST0 ..
   idx.push_back((uint32_t)s->names.size());
   for (const std::string& nm : s->names) {
@@ -1300,6 +1307,8 @@ int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, st
       mp_str(b, E.id);
       push(b);
       push(E.id);
+      idx.push_back(E.duration_ms);  // E_DUR: not a byte run, the element's timer duration
+      idx.push_back(0);
     }
   }
   while (arena.size() % 4) arena.push_back(0);

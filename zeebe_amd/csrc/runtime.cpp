@@ -3100,7 +3100,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     m.nrec = (uint16_t)(hd.x & 0xFFFF);
     m.doc_count = cm.doc_count;
     m.doc_begin = cm.doc_begin;
-    m.pad = 0;
+    m.pad = cm.pad;
     m.prev = ~0u;
     return (uint64_t)m.nrec;
   };
@@ -3155,6 +3155,8 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   a.bytes = h->d_log_bytes;
   a.block_sums = h->d_log_bytes + n + 1;
   a.flag = h->d_log_flag;
+  a.now_ms = h->run_clock_ms;
+  a.cmd_due = h->d_cmd_due;
   a.phase = 0;
   HIPCHK(launch_log_device(a, h->stream));
   unsigned long long total = 0;

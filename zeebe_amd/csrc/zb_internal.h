@@ -231,7 +231,7 @@ struct LogCmd {
   uint32_t prev;               // previous command of the same instance in the window, or ~0
   uint16_t first_ord, nkeys, nrec, doc_count;
   uint32_t doc_begin;
-  uint32_t pad;
+  uint32_t pad;                // the command's pad (TIMER:TRIGGER: dueDate high word)
 };
 struct LogLaunch {
   int phase;                   // 0 sizes + offsets, 1 write, 2 key ring
@@ -254,6 +254,8 @@ struct LogLaunch {
   unsigned long long* block_sums;
   uint64_t* out;
   uint32_t* flag;
+  long long now_ms;            // the run's clock (TIMER:CREATED dueDates)
+  const long long* cmd_due;    // [n] dueDate of the timer each batch canceled (KScope)
 };
 
 }  // namespace zb
