@@ -10,7 +10,7 @@ synthetic and already resident in HBM; nothing is skipped inside the timed regio
 Multi-GPU: one process per GPU, one Zeebe partition per GPU (Protocol.encodePartitionId),
 instances keyed to partitions; no data-path collective (weak scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config linear10|one_task|xor|forkjoin8|msg]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config linear10|one_task|xor|forkjoin8|boundary10|msg]
 
 --config msg is configs[4]: a message catch event correlated across partitions (one partition per
 GPU; the subscription commands between partitions go through RCCL all-to-all over xGMI, or, with
@@ -40,7 +40,18 @@ def workload(name):
         return bpmn.xor_process(), 10_000_000, 0, True
     if name == "forkjoin8":
         return bpmn.fork_join_process(8), 10_000_000, 0, False
+    if name == "boundary10":  # linear-10 with an interrupting timer boundary event on every task (KScope)
+        b = bpmn.createExecutableProcess("boundary10").startEvent("start")
+        for i in range(10):
+            b.serviceTask("task%d" % i, "benchmark-task").boundaryEvent("late%d" % i).timerWithDuration("PT1H")
+            b.endEvent("lateEnd%d" % i).moveToActivity("task%d" % i)
+        return b.endEvent("end").done(), 1_000_000, 10, False
     raise SystemExit("unknown config " + name)
+
+
+# first job key ordinal and ordinals per phase of the JOB:COMPLETE windows (kernels.hip key order:
+# per task SFT, ACTIVATE, [the boundary's timer,] job; per completion PROCESS_EVENT + those)
+JOB_ORDINALS = {"boundary10": (6, 5)}
 
 
 def algorithmic_bytes(name, n, phases):
@@ -61,6 +72,15 @@ def algorithmic_bytes(name, n, phases):
         return (16 + 16 + 32 + 26 * 8 + 8) * n  # + the amount document entry (16 B)
     if name == "forkjoin8":
         return (16 + 32 + 52 * 8 + 8) * n
+    if name == "boundary10":
+        # linear-10's rows plus the timer: CREATE 16 records + the timer row written (16 B); each
+        # JOB:COMPLETE 12 records (TIMER:CANCELED, the next TIMER:CREATED), the timer row read and
+        # written, the canceled dueDate (8 B); the last one 15 records
+        b = 16 + 32 + 16 * 8 + 8 + 8 + 16
+        for p in range(phases):
+            last = p == phases - 1
+            b += 16 + 32 + 8 + (0 if last else 8) + (15 if last else 12) * 8 + 8 + 16 + 16 + 8
+        return b * n
     return 0
 
 
@@ -438,12 +458,12 @@ def run_rank(args):
         docs_t = torch.from_numpy(docs.view(np.uint8).copy()).to(dev)
     windows.append(torch.from_numpy(create.view(np.uint8).copy()).to(dev))
     host_windows.append((create, docs if with_amount else None))
-    job_ord = 5 if not with_amount else 6
+    job_ord, per_phase = JOB_ORDINALS.get(args.config, (5 if not with_amount else 6, 4))
     for p in range(phases):
         c = abi.make_commands(n)
         c["instance"] = np.arange(n, dtype=np.uint32)
         c["kind"] = abi.CMD_JOB_COMPLETE
-        c["ref"] = job_ord + 4 * p
+        c["ref"] = job_ord + per_phase * p
         windows.append(torch.from_numpy(c.view(np.uint8).copy()).to(dev))
         host_windows.append((c, None))
     torch.cuda.synchronize()
@@ -531,7 +551,9 @@ def run_rank(args):
         "config": {"workload": {"linear10": "configs[1] linear 10-service-task process, 1M instances, auto-completed jobs",
                                 "one_task": "configs[0] one_task.bpmn create->job complete",
                                 "xor": "configs[2] exclusive gateway `= amount > 1000`, 10M instances",
-                                "forkjoin8": "configs[3] parallel fork/join 8 branches, 10M instances"}[args.config],
+                                "forkjoin8": "configs[3] parallel fork/join 8 branches, 10M instances",
+                                "boundary10": "linear 10 service tasks, each with an interrupting timer boundary "
+                                              "event (timers created and canceled), 1M instances"}[args.config],
                    "instances_per_gpu": n, "windows_per_step": len(windows), "partitions": world,
                    "parallelism": "one partition per GPU (dp%d)" % world, "max_commands_in_batch": 100},
         "records_per_s": tot_recs / elapsed,
