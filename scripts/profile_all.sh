@@ -21,7 +21,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 cat $(find $O/prof -name "*kernel_stats.csv" | head -1) | cut -c1-200
 echo "=== pmc"
 rm -rf gpurun_out/pmc && bash scripts/pmc.sh || exit 1
-for cfg in one_task xor forkjoin8 msg; do
+for cfg in one_task xor forkjoin8 boundary10 msg; do
   echo "=== bench $cfg"
   timeout -k 10 600 python -u bench.py --config $cfg --steps 3 --warmup 1 > $O/bench_$cfg.json 2> $O/bench_$cfg.err \
     || { tail -20 $O/bench_$cfg.err; exit 1; }
