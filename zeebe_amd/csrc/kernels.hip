@@ -104,7 +104,10 @@ using KGeneric = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, Z
 using KMsg = KCfg<128, 12, 16, ZB_KMSG_R, true, true, true, ZB_KMSG_W>;  // message catch events (config 5)
 // Embedded sub-processes: KGeneric plus flow scopes (a sub-process instance is an element-table
 // entry whose job field counts its children and active sequence flows)
-using KScope = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, ZB_KGENERIC_W, false, true>;
+#ifndef ZB_KSCOPE_W
+#define ZB_KSCOPE_W ZB_KGENERIC_W
+#endif
+using KScope = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, ZB_KSCOPE_W, false, true>;
 
 template <class K>
 struct Lane {
