@@ -1642,7 +1642,9 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   const auto t0 = now();
   h->h_hdr.resize(n);
   if (n) HIPCHK(hipMemcpyAsync(h->h_hdr.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost, h->stream));
-  h->h_hdr2.assign(n, make_uint4(0, 0, 0, 0));
+  // secondary headers: message partitions only (slot batches, outbox counts, payload rows)
+  if (h->msg()) h->h_hdr2.assign(n, make_uint4(0, 0, 0, 0));
+  else h->h_hdr2.clear();
   if (n && h->variant == 4) {  // dueDates of canceled timers (TIMER:CANCELED values)
     h->h_cmd_due.resize(n);
     HIPCHK(hipMemcpyAsync(h->h_cmd_due.data(), h->d_cmd_due, n * sizeof(long long), hipMemcpyDeviceToHost, h->stream));
