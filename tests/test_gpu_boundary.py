@@ -169,3 +169,35 @@ def test_gpu_boundary_restart_equivalence(shape):
         orc.run()
         assert part.state() == orc.state() == fresh.state()
     assert [r for r in fresh.state() if not r.startswith("KEY|")] == []
+
+
+@pytest.mark.parametrize("shape", ["multiple_sequence_flows", "non_interrupting_escalation", "cycle_r3", "to_gateway"])
+def test_gpu_boundary_batch_limit(shape):
+    # maxCommandsInBatch = 3: the boundary event's follow-ups (its COMPLETE_ELEMENT, the flows'
+    # ACTIVATEs) are written to the log unprocessed and run as continuation batches
+    # (ProcessingStateMachine.java:388-417), records (`unprocessed` flags included) and state equal
+    from oracle.oracle import Oracle
+    from test_gpu_parity import run_both
+    n = 32
+    part = Partition(max_instances=n, max_commands=64 * n, max_records_per_batch=256, max_commands_in_batch=3)
+    orc = Oracle(max_commands_in_batch=3)
+    xml = SHAPES[shape]()
+    assert part.deploy(xml) == orc.deploy(xml) == 0
+    clock = NOW
+    for e in (part, orc):
+        e.set_clock(clock)
+    run_both(part, orc, create_commands(n, 0))
+    rng = np.random.default_rng(12)
+    unprocessed = 0
+    for _ in range(20):
+        c = _open_work(part, rng)
+        if c is None:
+            break
+        clock += 1000
+        for e in (part, orc):
+            e.set_clock(clock)
+        got = run_both(part, orc, c)
+        unprocessed += int(got["unprocessed"].sum())
+        assert part.state() == orc.state()
+    assert part.stats()["fallback"] == 0 and unprocessed > 0
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []
