@@ -117,6 +117,9 @@ struct BatchRef {
   uint16_t first_ord;
   uint16_t nkeys;
   uint32_t gen;  // generation of the subject when the keys were generated (inst_gen)
+  // not zero-filled when a window's segment of 10^6 entries is allocated (every entry is written)
+  BatchRef() {}
+  BatchRef(int64_t b, uint32_t i, uint16_t f, uint16_t n, uint32_t g) : base(b), inst(i), first_ord(f), nkeys(n), gen(g) {}
 };
 
 // The resolve_key table: BatchRefs in key order, in segments (one per plain window, or appended
