@@ -38,7 +38,10 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 3  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes) */
+#define ZBHIP_ABI_VERSION 4  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+                               4: timer boundary events (start_event / flow_source / job_retries of job
+                                  workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
+                                  PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
