@@ -1707,9 +1707,20 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
             ms(t0, t1), ms(t1, now()));
   }
 
-  h->ext_keys.assign(n, 0);
-  h->declared.assign(n, 0);
-  h->h_base.assign(n, 0);
+  // fallback key declarations start empty; key bases are written by advance() before any read
+  h->ext_keys.resize(n);
+  h->declared.resize(n);
+  h->h_base.resize(n);
+  if (n >= (1u << 16)) {
+    parallel_for(host_threads(), [&](unsigned t, unsigned T) {
+      const size_t lo = (size_t)n * t / T, hi = (size_t)n * (t + 1) / T;
+      std::fill(h->ext_keys.begin() + lo, h->ext_keys.begin() + hi, 0);
+      std::fill(h->declared.begin() + lo, h->declared.begin() + hi, 0);
+    });
+  } else {
+    std::fill(h->ext_keys.begin(), h->ext_keys.end(), 0);
+    std::fill(h->declared.begin(), h->declared.end(), 0);
+  }
   h->fin_next = 0;
   h->results = true;
   }
