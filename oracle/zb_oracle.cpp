@@ -355,9 +355,9 @@ struct OProc {
 // (SequenceFlowTransformer.connectWithFlowNodes), which fixes getOutgoing() order.
 using MessageDefs = std::unordered_map<std::string, std::pair<std::string, std::string>>;  // id -> (name, corr var)
 
-// Interval.parse (bpmn-model/.../util/time/Interval.java) for static durations: "P[nD][T[nH][nM][n[.f]S]]"
-// -- days are 24 h in UTC, so the due date is now + a fixed number of ms.  Years / months / weeks,
-// negative parts and expressions (`=`) are outside the subset: -1.
+// Interval.parse (bpmn-model/.../util/time/Interval.java) for static durations: "P[0D][T[nH][nM][n[.f]S]]"
+// -- a Duration, so the due date is now + a fixed number of ms.  Days (a Period: calendar-based in the
+// system zone), years / months / weeks, negative parts and expressions (`=`) are outside the subset: -1.
 static int64_t parse_duration_ms(std::string t) {
   size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
   if (a == std::string::npos) return -1;
@@ -379,7 +379,9 @@ static int64_t parse_duration_ms(std::string t) {
     if (i == s || i >= t.size()) return -1;
     const char u = t[i++];
     any = true;
-    if (!time && u == 'D' && !frac) ms += whole * 86400000LL;
+    // a non-zero day count makes the interval calendar-based (Interval.isCalendarBased,
+    // Interval.java:77-93: ZonedDateTime.plus in the system zone): outside the subset
+    if (!time && u == 'D' && !frac && whole == 0) continue;
     else if (time && u == 'H' && !frac) ms += whole * 3600000LL;
     else if (time && u == 'M' && !frac) ms += whole * 60000LL;
     else if (time && u == 'S') ms += whole * 1000LL + frac;
@@ -1367,9 +1369,13 @@ class Oracle {
     else                                              // isElementActivated (catch event)
       pi_command(eik, ZBHIP_PI_COMPLETE_ELEMENT, eit->second.value);
     // shouldReschedule / rescheduleTimer (TriggerTimerProcessor.java:116-160): a cycle's next timer
-    // from the last dueDate (refreshTimer: Interval.withStart(dueDate)), one repetition fewer
-    if (t.reps == -1 || t.reps > 1)
-      subscribe_timer_at(eik, t.pi, t.dueDate + target.timer_ms, t.reps == -1 ? -1 : t.reps - 1);
+    // from the last dueDate (refreshTimer: Interval.withStart(dueDate) starts at dueDate + interval),
+    // one repetition fewer; subscribeToTimerEvent takes timer.getDueDate(now) = Interval.toEpochMilli
+    // (Interval.java:77-93): that start, or now + interval when the start is not after now
+    if (t.reps == -1 || t.reps > 1) {
+      const int64_t start = t.dueDate + target.timer_ms;
+      subscribe_timer_at(eik, t.pi, start <= now_ms ? now_ms + target.timer_ms : start, t.reps == -1 ? -1 : t.reps - 1);
+    }
   }
 
   // DbEventScopeInstanceState.canTriggerEvent (state/instance/DbEventScopeInstanceState.java:178-182):

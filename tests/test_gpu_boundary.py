@@ -201,3 +201,48 @@ def test_gpu_boundary_batch_limit(shape):
         assert part.state() == orc.state()
     assert part.stats()["fallback"] == 0 and unprocessed > 0
     assert [r for r in part.state() if not r.startswith("KEY|")] == []
+
+
+def test_gpu_late_cycle_triggers():
+    # TriggerTimerProcessor.refreshTimer + Interval.toEpochMilli (Interval.java:77-93): the next
+    # timer of a cycle starts at dueDate + interval unless that is not after the clock, then clock +
+    # interval.  Four groups of instances are triggered in four windows, each later past its dueDate
+    # (0, 999, 1000 and 2500 ms late, PT1S cycle); records and state equal the oracle's and the device
+    # log bytes equal the host serialiser's
+    from oracle.oracle import Oracle
+    from test_gpu_logdev import Log
+    from test_gpu_parity import assert_same_records
+    xml = cycle_process("R/PT1S")
+    n = 4 * 64
+    log = Log(xml, n)
+    orc = Oracle()
+    assert orc.deploy(xml) == 0
+    for e in (log.part, orc):
+        e.set_clock(NOW)
+    orc.submit(create_commands(n, 0))
+    orc.run()
+    assert_same_records(log.window(create_commands(n, 0)), orc.records())
+    timers = {}
+    for r in log.part.state():
+        if r.startswith("TIMERS|"):
+            p = r.split("|")
+            timers[log.part.resolve_key(int(p[2]))] = int(dict(kv.split("=") for kv in p[3].split(","))["dueDate"])
+    assert len(timers) == n
+    for g, late in enumerate((0, 999, 1000, 2500)):
+        mine = [(i, o) for (i, o) in sorted(timers) if i // 64 == g]
+        c = abi.make_commands(len(mine))
+        for j, (i, o) in enumerate(mine):
+            due = timers[(i, o)]
+            c[j]["instance"], c[j]["kind"], c[j]["ref"] = i, abi.CMD_TIMER_TRIGGER, o
+            c[j]["doc_begin"], c[j]["pad"] = due & 0xFFFFFFFF, due >> 32
+        for e in (log.part, orc):
+            e.set_clock(NOW + 1000 + late)
+        orc.clear_records()
+        orc.submit(c)
+        orc.run()
+        got = log.window(c)
+        assert_same_records(got, orc.records())
+        nxt = got[(got["value_type"] == abi.VT_TIMER) & (got["intent"] == abi.TIMER_CREATED)]
+        want_due = NOW + 2000 if late < 1000 else NOW + 1000 + late + 1000
+        assert len(nxt) == 64 and (nxt["aux"] == want_due).all()
+        assert log.part.state() == orc.state()

@@ -315,14 +315,40 @@ def test_linear10_full_size_properties():
 
 
 def test_xor_full_size_branch_counts():
-    """Config 3 at 10^7 instances: the number of `high` branches equals #(amount > 1000)."""
+    """Config 3 at 10^7 instances: the number of SEQUENCE_FLOW_TAKEN records on the `high` flow
+    equals #(amount > 1000), on `low` the rest, and every instance ends on its own branch's end
+    event (records drained in chunks, counted per element)."""
     n = 10_000_000
     rng = np.random.default_rng(0x5EED03)
     vals = rng.integers(0, 2001, n)
-    part, stats = _full_run(bpmn.xor_process(), n, 0, amount_docs(vals, 0), "amount")
-    s = stats[0]
+    xml = bpmn.xor_process()
+    part = Partition(max_instances=n, max_commands=n, max_records_per_batch=64)
+    part.deploy(xml)
+    assert part.intern("amount") == 0
+    cmds = create_commands(n, 0)
+    cmds["doc_count"] = 1
+    cmds["doc_begin"] = np.arange(n, dtype=np.uint32)
+    part.submit(cmds, amount_docs(vals, 0))
+    part.run()
+    s = part.stats()
     assert s["fallback"] == 0 and s["transitions"] == 18 * n and s["records"] == 26 * n
     assert s["completed_instances"] == n
+    ids = part.processes[0].element_ids
+    high, low, end_high = ids.index("high"), ids.index("low"), ids.index("endHigh")
+    taken = {high: 0, low: 0}
+    ended_high = 0
+    total = 0
+    for recs in part.drain_chunks():
+        total += len(recs)
+        pi = recs[recs["value_type"] == abi.VT_PROCESS_INSTANCE]
+        sft = pi[(pi["intent"] == abi.PI_INTENT_IDS["SEQUENCE_FLOW_TAKEN"]) & (pi["record_type"] == abi.RT_EVENT)]
+        for f in taken:
+            taken[f] += int((sft["element_idx"] == f).sum())
+        ended_high += int(((pi["intent"] == abi.PI_INTENT_IDS["ELEMENT_COMPLETED"]) & (pi["element_idx"] == end_high)).sum())
+    want_high = int((vals > 1000).sum())
+    assert total == 26 * n
+    assert taken[high] == want_high and taken[low] == n - want_high
+    assert ended_high == want_high
 
 
 def test_fork_join8_full_size_properties():

@@ -294,6 +294,23 @@ def test_non_interrupting_cycle_reschedules():
     assert [r for r in o.state() if not r.startswith("KEY|")] == []
 
 
+@pytest.mark.parametrize("late_ms,next_due", [(0, NOW + 2000), (999, NOW + 2000), (1000, NOW + 1000 + 1000 + 1000),
+                                              (2500, NOW + 1000 + 2500 + 1000)])
+def test_late_cycle_trigger_counts_from_the_clock(late_ms, next_due):
+    # TriggerTimerProcessor.refreshTimer (:161-175): Interval.withStart(dueDate) starts at dueDate +
+    # interval; subscribeToTimerEvent takes Interval.toEpochMilli(now) (Interval.java:77-93), which is
+    # that start unless start <= now, then now + interval -- a trigger processed a period or more late
+    # does not schedule a dueDate in the past
+    o, recs = _started(cycle_process("R/PT1S"))
+    created = [r for r in recs if r["value_type"] == abi.VT_TIMER][0]
+    assert int(created["aux"]) == NOW + 1000
+    o.set_clock(NOW + 1000 + late_ms)
+    fired = _trigger_all(o, recs)
+    nxt = [r for r in fired if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CREATED][0]
+    assert int(nxt["aux"]) == next_due
+    assert any(r.startswith("TIMER_DUE_DATES|%d|" % next_due) for r in o.state())
+
+
 def test_cycle_with_repetitions_stops():
     # R3: three triggers (repetitions 3, 2, 1 in the records), then no timer is left
     o, recs = _started(cycle_process("R3/PT10S"))

@@ -344,8 +344,9 @@ struct Compiled {
 };
 
 // Interval.parse (bpmn-model/.../util/time/Interval.java) of a static duration
-// "P[nD][T[nH][nM][n[.f]S]]": days are 24 h in UTC, so due = now + a fixed number of ms.  Years,
-// months, weeks, negative parts and `=` expressions: -1 (outside the subset).
+// "P[0D][T[nH][nM][n[.f]S]]": a Duration, so due = now + a fixed number of ms.  Days (a Period, which
+// Interval.toEpochMilli adds in the broker's system zone), years, months, weeks, negative parts and
+// `=` expressions: -1 (outside the subset).
 static int64_t duration_ms(const std::string& text) {
   size_t a = text.find_first_not_of(" \t\r\n"), b = text.find_last_not_of(" \t\r\n");
   if (a == std::string::npos) return -1;
@@ -378,7 +379,9 @@ static int64_t duration_ms(const std::string& text) {
     if (i == s || i >= t.size()) return -1;
     const char u = t[i++];
     any = true;
-    if (!in_time && u == 'D' && !frac) ms += whole * 86400000LL;
+    // days make the interval calendar-based (Interval.isCalendarBased): ZonedDateTime.plus in the
+    // broker's system zone, so a DST change moves the due date by an hour -- outside the subset
+    if (!in_time && u == 'D' && !frac && whole == 0) continue;
     else if (in_time && u == 'H' && !frac) ms += whole * 3600000LL;
     else if (in_time && u == 'M' && !frac) ms += whole * 60000LL;
     else if (in_time && u == 'S') ms += whole * 1000LL + frac;

@@ -1137,13 +1137,14 @@ __device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord, long lo
     const uint32_t c = scope_of<K>(elem_of(L, task));
     activate_triggered_event(L, pe, eord, elem, scope_key(L, c));
     // shouldReschedule / rescheduleTimer (TriggerTimerProcessor.java:116-160): a cycle's next timer
-    // from the command's dueDate (refreshTimer), one repetition fewer
+    // from the command's dueDate (refreshTimer: Interval.withStart), one repetition fewer; a start
+    // already past counts from the clock instead (Interval.toEpochMilli, Interval.java:77-93)
     if (reps == 255 || reps > 1) {
       const uint32_t nr = reps == 255 ? 255u : reps - 1;
       const uint32_t tk = new_key(L);
       L.tm_x = elem | (tk << 16);
       L.tm_y = eord | (nr << 16) | (1u << 31);
-      L.tm_due = cmd_due + (long long)bw.z;
+      L.tm_due = next_cycle_due(cmd_due, (long long)bw.z, L.sp->now_ms);
       emit(L, C_TIMER_NEXT, tk, eord, elem, nr);
     }
     return;

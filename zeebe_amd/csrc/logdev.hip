@@ -263,7 +263,7 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
       if (!pb || elem >= L.idx[pb + 5]) return false;
       dur = (long long)el_run(L, pb, elem, E_DUR).x;
     }
-    r.due = c6 == C_TIMER_CREATED ? L.now_ms + dur : c6 == C_TIMER_NEXT ? cmd + dur
+    r.due = c6 == C_TIMER_CREATED ? L.now_ms + dur : c6 == C_TIMER_NEXT ? next_cycle_due(cmd, dur, L.now_ms)
             : c6 == C_TIMER_CANCELED ? L.cmd_due[c] : cmd;
     r.reps = rej ? 1 : fl == 255 ? -1 : (int)fl;
   } else if (c6 == C_PIC_CREATED) {

@@ -1238,6 +1238,10 @@ static void advance_window_parallel(zbhip_handle* h) {
   std::vector<int64_t> kbase(T + 1, 0);
   std::vector<size_t> bbase(T + 1, 0);
   auto range = [n](unsigned t, unsigned TT) { return std::make_pair(n * t / TT, n * (t + 1) / TT); };
+  const uint32_t N = h->cfg.max_instances;
+  // a resolve-table entry for every processed command with keys whose subject is an instance slot
+  // (the entries are written at these places below; none is left unwritten)
+  auto has_entry = [h, N](size_t c, uint2 hd) { return (hd.x >> 16) != 0 && h->h_cmds[c].instance < N; };
   parallel_for(T, [&](unsigned t, unsigned TT) {
     int64_t k = 0;
     size_t b = 0;
@@ -1246,7 +1250,7 @@ static void advance_window_parallel(zbhip_handle* h) {
       const uint2 hd = h->h_hdr[c];
       if (((hd.y >> 16) & 0xFF) == ST_OK) {
         k += hd.x >> 16;
-        b += (hd.x >> 16) != 0;
+        b += has_entry(c, hd);
       } else {
         k += h->ext_keys[c];
       }
@@ -1260,7 +1264,6 @@ static void advance_window_parallel(zbhip_handle* h) {
     bbase[t + 1] += bbase[t];
   }
   BatchRef* const tbl = h->batches.append_segment(bbase[T]);
-  const uint32_t N = h->cfg.max_instances;
   // one subject per command in a one-round window: every range updates its own instances; with
   // rounds, each thread owns the instances i % T == t and walks the window in log order
   const bool one_round = h->round_begin.empty() && h->cont_cmds.empty();
@@ -1294,11 +1297,12 @@ static void advance_window_parallel(zbhip_handle* h) {
       const bool ok = ((hd.y >> 16) & 0xFF) == ST_OK;
       kc += ok ? (int64_t)(hd.x >> 16) : h->ext_keys[c];
       if (!ok) continue;
+      if (h->h_cmds[c].instance >= N) continue;
       const size_t here = nb;
-      nb += (hd.x >> 16) != 0;
+      nb += has_entry(c, hd);
       if (!one_round) {
         bpos[c] = (uint32_t)here;
-      } else if (h->h_cmds[c].instance < N) {
+      } else {
         apply(c, here, dead);
       }
     }
@@ -1871,7 +1875,8 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       const zbhip_element* E = proc != NONE && elem < h->procs[proc].els.size() ? &h->procs[proc].els[elem] : nullptr;
       // a cycle's next timer counts from the TRIGGER command's dueDate (refreshTimer), others from the clock
       const int64_t dur = E ? (int64_t)E->duration_ms : 0;
-      r.aux = c6 == C_TIMER_CREATED ? h->run_clock_ms + dur : c6 == C_TIMER_NEXT ? cmd_due + dur : cmd_due;
+      r.aux = c6 == C_TIMER_CREATED ? h->run_clock_ms + dur
+               : c6 == C_TIMER_NEXT ? next_cycle_due(cmd_due, dur, h->run_clock_ms) : cmd_due;
       if (!rej) r.partition = fl == 255 ? -1 : (int32_t)fl;  // TimerRecord.repetitions
     } else {
       return ZBHIP_EDEVICE;  // corrupt record

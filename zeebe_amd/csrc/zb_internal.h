@@ -42,6 +42,14 @@ constexpr int kPayloadRows = 6;
 // correlation slot), ord = v & 0xFFFF.  The device key scan / the host drain resolve them.
 enum : uint32_t { KS_INST = 0, KS_SLOT = 1 };
 
+// The dueDate of a timer cycle's next timer (TriggerTimerProcessor.refreshTimer, :161-175):
+// Interval.withStart(the TRIGGER command's dueDate) starts at dueDate + interval, and
+// Interval.toEpochMilli(now) (Interval.java:77-93) returns that start unless it is not after now,
+// then now + interval (a trigger processed a period or more late does not schedule a past dueDate).
+__host__ __device__ inline long long next_cycle_due(long long due, long long interval, long long now) {
+  return due + interval <= now ? now + interval : due + interval;
+}
+
 // ElementInstance.jobKey encodings in a slot (ElementInstance.java:23-54: default 0,
 // JobCreatedApplier sets the job key, JobCompletedApplier sets -1)
 constexpr uint16_t JOB_ZERO = 0xFFFF;

@@ -232,6 +232,17 @@ class Partition:
         check(self.L.zbhip_drain(self.h, out.ctypes.data if n else None, n, C.byref(got)), "zbhip_drain")
         return out[: got.value]
 
+    def drain_chunks(self, chunk=1 << 22):
+        """The window's records in log order, `chunk` at a time (bounded host memory for windows of
+        10^7 commands); every yielded view is overwritten by the next one."""
+        out = np.empty(chunk, dtype=abi.RECORD_DTYPE)
+        got = C.c_size_t()
+        while True:
+            check(self.L.zbhip_drain(self.h, out.ctypes.data, chunk, C.byref(got)), "zbhip_drain")
+            if got.value == 0:
+                return
+            yield out[: got.value]
+
     def reason(self, rec):
         r = abi.Record()
         for f, _ in abi.Record._fields_:
