@@ -4,11 +4,31 @@
  * that answers the hot-path commands from libzbhip.so and hands everything else -- and every
  * command the device falls back on -- to the unchanged engine.
  *
+ * Inside ProcessingStateMachine.batchProcessing / collectBatchProcessingStepResult
+ * (stream-platform/.../stream/impl/ProcessingStateMachine.java:328-417) it behaves as the engine:
+ *  - a device batch is appended whole when the platform processes its initial command; the
+ *    follow-up commands the platform then feeds back (UnwrittenRecord) were already processed on the
+ *    device and return the builder unchanged (out.build(), never EmptyProcessingResult: the platform
+ *    skips the builder's entries by their count);
+ *  - follow-ups written unprocessed past maxCommandsInBatch are device continuations
+ *    (ZBHIP_OPEN_DEFER_CONTINUATIONS): they run when the platform reads them back, at their own log
+ *    position (ZBHIP_CMD_CONTINUE), after whatever the log holds before them;
+ *  - one key generator: after each device command DbKeyGenerator.setKeyIfHigher(device keys),
+ *    before each window zbhip_set_key_if_higher(DbKeyGenerator's key);
+ *  - the fallback hand-off declares the engine's keys after its batch (a post-commit task);
+ *  - JOB_BATCH:ACTIVATE of job types only device instances hold goes to zbhip_activate_jobs;
+ *  - after recovery the instances of device processes move from RocksDB into HBM (onRecovered).
+ * The Python mirror zeebe_amd/adapter.py is this class line for line in behaviour; tests/test_gpu_psm.py
+ * runs it inside a restatement of ProcessingStateMachine against the engine alone.
+ *
  * Not compiled in this image (no JDK); written against the reference's interfaces:
  *   RecordProcessor                stream-platform/.../stream/api/RecordProcessor.java:17-108
  *   ProcessingResultBuilder        stream-platform/.../stream/api/ProcessingResultBuilder.java:22-80
  *   RecordProcessorContext         stream-platform/.../stream/api/RecordProcessorContext.java:18-32
- *   KeyGeneratorControls           stream-platform/.../stream/impl/state/DbKeyGenerator.java:40-60
+ *   KeyGeneratorControls           stream-platform/.../stream/api/state/KeyGeneratorControls.java:11-19
+ *   DbKeyGenerator                 stream-platform/.../stream/impl/state/DbKeyGenerator.java:17-61
+ *   UnwrittenRecord                stream-platform/.../stream/impl/records/UnwrittenRecord.java:19-40
+ *   StreamProcessorLifecycleAware  stream-platform/.../stream/api/StreamProcessorLifecycleAware.java:13
  *   LogStreamReader / LoggedEvent  logstreams/.../log/LogStreamReader.java, LoggedEvent.java
  * See INTEGRATION.md for the contract of every zbhip call used here.
  */
@@ -18,32 +38,41 @@ import io.camunda.zeebe.engine.Engine;
 import io.camunda.zeebe.logstreams.log.LogStreamReader;
 import io.camunda.zeebe.logstreams.log.LoggedEvent;
 import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
+import io.camunda.zeebe.protocol.impl.record.value.job.JobBatchRecord;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceRecord;
 import io.camunda.zeebe.protocol.impl.record.value.timer.TimerRecord;
 import io.camunda.zeebe.protocol.record.RecordType;
 import io.camunda.zeebe.protocol.record.ValueType;
+import io.camunda.zeebe.protocol.record.intent.JobBatchIntent;
 import io.camunda.zeebe.protocol.record.intent.JobIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessInstanceCreationIntent;
+import io.camunda.zeebe.protocol.record.intent.ProcessInstanceIntent;
 import io.camunda.zeebe.protocol.record.intent.TimerIntent;
 import io.camunda.zeebe.scheduler.clock.ActorClock;
 import io.camunda.zeebe.stream.api.ProcessingResult;
 import io.camunda.zeebe.stream.api.ProcessingResultBuilder;
+import io.camunda.zeebe.stream.api.ReadonlyStreamProcessorContext;
 import io.camunda.zeebe.stream.api.RecordProcessor;
 import io.camunda.zeebe.stream.api.RecordProcessorContext;
+import io.camunda.zeebe.stream.api.StreamProcessorLifecycleAware;
 import io.camunda.zeebe.stream.api.records.TypedRecord;
-import io.camunda.zeebe.stream.impl.state.KeyGeneratorControls;
+import io.camunda.zeebe.stream.impl.records.UnwrittenRecord;
+import io.camunda.zeebe.stream.impl.state.DbKeyGenerator;
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
+import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.BitSet;
 import java.util.HashMap;
 import java.util.HashSet;
+import java.util.Iterator;
 import java.util.List;
 import java.util.Map;
 import java.util.Set;
 
-public final class GpuBatchProcessor implements RecordProcessor {
+public final class GpuBatchProcessor implements RecordProcessor, StreamProcessorLifecycleAware {
 
   /** Deployed processes the adapter knows: bpmnProcessId (latest version) / definition key. */
   public interface Deployments {
@@ -53,34 +82,62 @@ public final class GpuBatchProcessor implements RecordProcessor {
     record DeployedResource(long definitionKey, String bpmnProcessId, int version, byte[] xml) {}
   }
 
+  /** Raw column-family access of a hand-off and of recovery; the broker binds it to its ZeebeDb transaction. */
+  public interface RawDb {
+    void upsert(int columnFamily, byte[] key, byte[] value);
+
+    void delete(int columnFamily, byte[] key);
+
+    /** Every entry of the hot-path column families (ZbColumnFamilies ordinals), in key order. */
+    void forEach(Entry consumer);
+
+    interface Entry {
+      void entry(int columnFamily, byte[] key, byte[] value);
+    }
+  }
+
+  /** A follow-up a device batch wrote unprocessed: matched against the log in the order written. */
+  record Continuation(long id, int slot, long key, int intent, String elementId, long flowScopeKey, long piKey) {
+    boolean matches(final TypedRecord record) {
+      final ProcessInstanceRecord v = (ProcessInstanceRecord) record.getValue();
+      return record.getKey() == key && record.getIntent().value() == intent && v.getElementId().equals(elementId)
+          && v.getFlowScopeKey() == flowScopeKey && v.getProcessInstanceKey() == piKey;
+    }
+  }
+
   private static final int WINDOW = 1 << 16; // commands per submitted window (zbhip_config.max_commands)
   private static final int INSTANCES = 1 << 22; // instance slots in HBM (288 GB holds ~2.5e9)
 
   private final Engine engine;
   private final LogStreamReader reader;
   private final Deployments deployments;
-  private final RawDbWriter zeebeDb;
+  private final RawDb zeebeDb;
   private final int partitionCount;
   private final int device;
+  private int partitionId;
 
   private final Arena arena = Arena.ofShared();
   private MemorySegment handle;
-  private KeyGeneratorControls keyGenerator;
+  private DbKeyGenerator keyGenerator;
   private final Map<Long, ZbHip.Deployed> byKey = new HashMap<>();
   private final Map<String, ZbHip.Deployed> latestById = new HashMap<>();
   private final List<ZbHip.Deployed> byIndex = new ArrayList<>();
+  private final Set<String> engineJobTypes = new HashSet<>();
   private final BitSet usedSlots = new BitSet(INSTANCES);
+  private final Set<Integer> ended = new HashSet<>(); // ended instances whose continuations still wait
   private int nextFreeSlot;
 
   // the window read ahead from the log
   private final Window window = new Window();
   private final Set<Integer> handedOff = new HashSet<>();
+  private final ArrayDeque<Continuation> continuations = new ArrayDeque<>();
+  private int followUps; // follow-ups of the current device batch the platform feeds back
 
   public GpuBatchProcessor(
       final Engine engine,
       final LogStreamReader reader,
       final Deployments deployments,
-      final RawDbWriter zeebeDb,
+      final RawDb zeebeDb,
       final int partitionCount,
       final int device) {
     this.engine = engine;
@@ -94,21 +151,28 @@ public final class GpuBatchProcessor implements RecordProcessor {
   @Override
   public void init(final RecordProcessorContext ctx) {
     engine.init(ctx);
-    keyGenerator = (KeyGeneratorControls) ctx.getKeyGenerator();
+    // the platform's key generator is the DbKeyGenerator (StreamProcessor.java:368)
+    keyGenerator = (DbKeyGenerator) ctx.getKeyGenerator();
+    partitionId = ctx.getPartitionId();
+    final long partitionBits = (long) partitionId << 51;
     handle =
         ZbHip.open(
             arena, ctx.getPartitionId(), partitionCount, device, /* maxCommandsInBatch */ 100, INSTANCES, WINDOW,
-            keyGenerator.getCurrentKey(), /* correlation slots: config 5 only */ 0);
+            keyGenerator.getCurrentKey() - partitionBits, /* correlation slots: config 5 only */ 0,
+            ZbHip.OPEN_DEFER_CONTINUATIONS);
     for (final var d : deployments.all()) {
       deploy(d);
     }
     window.init(arena);
+    ctx.addLifecycleListeners(List.of(this));
   }
 
   private void deploy(final Deployments.DeployedResource d) {
     final ZbHip.Deployed p = ZbHip.deploy(handle, d.xml(), d.definitionKey(), d.version());
     if (p == null) {
-      return; // outside the device subset: its instances run on the CPU engine
+      // outside the device subset: its instances (and their job types) stay on the CPU engine
+      engineJobTypes.addAll(JobTypes.of(d.xml()));
+      return;
     }
     byKey.put(d.definitionKey(), p);
     byIndex.add(p);
@@ -121,32 +185,66 @@ public final class GpuBatchProcessor implements RecordProcessor {
   @Override
   public boolean accepts(final ValueType valueType) {
     return valueType == ValueType.PROCESS_INSTANCE_CREATION || valueType == ValueType.JOB
-        || valueType == ValueType.TIMER || engine.accepts(valueType);
+        || valueType == ValueType.TIMER || valueType == ValueType.JOB_BATCH || engine.accepts(valueType);
   }
 
   @Override
   public void replay(final TypedRecord record) {
-    // events only; the appliers write RocksDB.  Instances restored this way are loaded into HBM
-    // after recovery with ZbHip.importStateDb over the hot-path column families.
+    // events only; the appliers write RocksDB.  Instances restored this way move into HBM in onRecovered
     engine.replay(record);
+  }
+
+  /**
+   * After replay the engine's state holds every instance: those of device processes move into HBM
+   * (zbhip_import_state_db) and leave RocksDB, except instances a command still waiting in the log
+   * addresses by its own record (a follow-up written unprocessed before the restart).
+   */
+  @Override
+  public void onRecovered(final ReadonlyStreamProcessorContext context) {
+    final RecoveredState state = RecoveredState.collect(handle, zeebeDb, reader);
+    if (state.size() > 0) {
+      final int first = nextFreeSlot;
+      final int n = ZbHip.importStateDb(handle, state.entries(arena), state.bytes(), first);
+      usedSlots.set(first, first + n);
+      nextFreeSlot = first + n;
+      state.forEachMoved(zeebeDb::delete);
+    }
+    ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
   }
 
   @Override
   public ProcessingResult process(final TypedRecord record, final ProcessingResultBuilder out) {
-    if (!isHotPath(record)) {
+    if (record instanceof UnwrittenRecord) {
+      // a follow-up command the platform feeds back within the current batch
+      if (followUps > 0) {
+        followUps--;
+        return out.build(); // already processed on the device: its records are in the builder
+      }
       return engine.process(record, out);
     }
-    if (!window.covers(record.getPosition())) {
-      fillWindow(record);
+    followUps = 0;
+    if (record.getValueType() == ValueType.JOB_BATCH && record.getIntent() == JobBatchIntent.ACTIVATE) {
+      final JobBatchRecord batch = (JobBatchRecord) record.getValue();
+      return engineJobTypes.contains(batch.getType()) ? engine.process(record, out) : activateJobs(record, batch, out);
     }
-    final int i = window.indexOf(record.getPosition());
+    int i = window.covers(record.getPosition()) ? window.indexOf(record.getPosition()) : -1;
     if (i < 0) {
-      return engine.process(record, out); // the read-ahead stopped before it (e.g. a CPU-resident instance)
+      if (!isHotPath(record, continuations.iterator())) {
+        return engine.process(record, out);
+      }
+      fillWindow(record);
+      i = window.indexOf(record.getPosition());
+      if (i < 0) {
+        return engine.process(record, out); // the read-ahead stopped before it
+      }
     }
     if (ZbHip.commandStatus(handle, i) != 0) {
       return fallBack(i, record, out);
     }
-    window.emit(i, out, this);
+    followUps = window.emit(i, record, out, this);
+    // DbKeyGenerator after this command: the device's keys so far (the engine's next command, a
+    // fallback in this window or whatever follows the window, continues after them)
+    keyGenerator.setKeyIfHigher(ZbHip.keyBefore(handle, i + 1));
     return out.build();
   }
 
@@ -158,17 +256,37 @@ public final class GpuBatchProcessor implements RecordProcessor {
 
   // ---- the window ------------------------------------------------------------------------------
 
-  private boolean isHotPath(final TypedRecord record) {
+  private ZbHip.Deployed createTarget(final ProcessInstanceCreationRecord create) {
+    return create.getProcessDefinitionKey() > 0
+        ? byKey.get(create.getProcessDefinitionKey())
+        : latestById.get(create.getBpmnProcessId());
+  }
+
+  /**
+   * Would the device take this log command?  {@code next}: the continuations not yet claimed by the
+   * read-ahead (a log PI command is one when it is the next one written).
+   */
+  private boolean isHotPath(final TypedRecord record, final Iterator<Continuation> next) {
     if (record.getRecordType() != RecordType.COMMAND) {
       return false;
     }
-    if (record.getValueType() == ValueType.PROCESS_INSTANCE_CREATION) {
-      return record.getIntent() == ProcessInstanceCreationIntent.CREATE;
+    final ValueType vt = record.getValueType();
+    if (vt == ValueType.PROCESS_INSTANCE_CREATION) {
+      return record.getIntent() == ProcessInstanceCreationIntent.CREATE
+          && createTarget((ProcessInstanceCreationRecord) record.getValue()) != null;
     }
-    // JOB:COMPLETE of a device job; TIMER:TRIGGER (DueDateTimerChecker's command) of a device timer
-    return ((record.getValueType() == ValueType.JOB && record.getIntent() == JobIntent.COMPLETE)
-            || (record.getValueType() == ValueType.TIMER && record.getIntent() == TimerIntent.TRIGGER))
-        && ZbHip.resolveKey(handle, record.getKey()) >= 0;
+    if ((vt == ValueType.JOB && record.getIntent() == JobIntent.COMPLETE)
+        || (vt == ValueType.TIMER && record.getIntent() == TimerIntent.TRIGGER)) {
+      // JOB:COMPLETE of a device job; TIMER:TRIGGER (DueDateTimerChecker's command) of a device timer
+      return ZbHip.resolveKey(handle, record.getKey()) >= 0;
+    }
+    if (vt == ValueType.PROCESS_INSTANCE
+        && (record.getIntent() == ProcessInstanceIntent.ACTIVATE_ELEMENT
+            || record.getIntent() == ProcessInstanceIntent.COMPLETE_ELEMENT
+            || record.getIntent() == ProcessInstanceIntent.TERMINATE_ELEMENT)) {
+      return next.hasNext() && next.next().matches(record);
+    }
+    return false;
   }
 
   /**
@@ -177,50 +295,75 @@ public final class GpuBatchProcessor implements RecordProcessor {
    * window's records (keys relabelled to DbKeyGenerator's, ordered by source command).
    */
   private void fillWindow(final TypedRecord first) {
+    freeEndedSlots();
     window.reset(first.getPosition());
     reader.seek(first.getPosition());
     final RecordMetadata meta = new RecordMetadata();
-    final ProcessInstanceCreationRecord create = new ProcessInstanceCreationRecord();
-    final JobRecord job = new JobRecord();
-    final TimerRecord timer = new TimerRecord();
+    final Iterator<Continuation> next = continuations.iterator();
+    int claimed = 0;
     while (reader.hasNext() && window.size() < WINDOW) {
       final LoggedEvent event = reader.next();
       event.readMetadata(meta);
-      if (meta.getRecordType() != RecordType.COMMAND) {
-        continue; // follow-up events of earlier batches between the commands
+      if (meta.getRecordType() != RecordType.COMMAND || event.shouldSkipProcessing()) {
+        continue; // follow-up events and processed follow-up commands of earlier batches
       }
-      if (meta.getValueType() == ValueType.PROCESS_INSTANCE_CREATION
-          && meta.getIntent() == ProcessInstanceCreationIntent.CREATE) {
-        event.readValue(create);
-        final ZbHip.Deployed p =
-            create.getProcessDefinitionKey() > 0
-                ? byKey.get(create.getProcessDefinitionKey())
-                : latestById.get(create.getBpmnProcessId());
-        if (p == null || !window.addCreate(event.getPosition(), p.index(), takeSlot(), create.getVariablesBuffer(), this)) {
-          break; // a process on the CPU engine: the window ends before it (log order is kept)
+      final TypedRecord rec = Window.typed(event, meta, partitionId);
+      final Iterator<Continuation> peek = continuations.stream().skip(claimed).iterator();
+      if (!isHotPath(rec, peek)) {
+        break; // the engine's: the window ends before it (log order is kept)
+      }
+      final ValueType vt = meta.getValueType();
+      if (vt == ValueType.PROCESS_INSTANCE_CREATION) {
+        final ProcessInstanceCreationRecord create = (ProcessInstanceCreationRecord) rec.getValue();
+        final int slot = takeSlot();
+        if (slot < 0 || !window.addCreate(event.getPosition(), rec, createTarget(create).index(), slot, this)) {
+          if (slot >= 0) {
+            usedSlots.clear(slot); // the document is outside the subset: the slot stays free
+          }
+          break; // the engine takes this CREATE
         }
-      } else if (meta.getValueType() == ValueType.JOB && meta.getIntent() == JobIntent.COMPLETE) {
-        event.readValue(job);
+      } else if (vt == ValueType.JOB) {
         final long ref = ZbHip.resolveKey(handle, event.getKey());
-        if (ref < 0 || !window.addJobComplete(event.getPosition(), ref, job.getVariablesBuffer(), this)) {
-          break; // a job of a CPU-resident instance
+        if (!window.addJobComplete(event.getPosition(), rec, ref, this)) {
+          break;
         }
-      } else if (meta.getValueType() == ValueType.TIMER && meta.getIntent() == TimerIntent.TRIGGER) {
-        event.readValue(timer);
+      } else if (vt == ValueType.TIMER) {
         final long ref = ZbHip.resolveKey(handle, event.getKey());
-        if (ref < 0) {
-          break; // a timer of a CPU-resident instance
-        }
-        window.addTimerTrigger(event.getPosition(), ref, timer.getDueDate());
+        window.addTimerTrigger(event.getPosition(), rec, ref, ((TimerRecord) rec.getValue()).getDueDate());
       } else {
-        break; // any other command ends the window
+        final Continuation c = next.next();
+        claimed++;
+        window.addContinuation(event.getPosition(), rec, c.slot(), c.id());
       }
     }
+    for (int k = 0; k < claimed; k++) {
+      continuations.removeFirst();
+    }
+    // keys the engine generated since the last window come first (setKeyIfHigher)
+    ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
     // the window's clock: TIMER:CREATED dueDates (CatchEventBehavior.java:310, ActorClock)
     ZbHip.setClock(handle, ActorClock.currentTimeMillis());
-    window.submitRunDrain(handle);
-    // instances that ended in this window free their slots for later CREATEs
-    window.forEachEndedInstance(slot -> usedSlots.clear(slot));
+    window.submitRun(handle);
+  }
+
+  /** A process instance completed (Window.emit): its slot is free once its continuations ran. */
+  void instanceEnded(final int slot) {
+    ended.add(slot);
+  }
+
+  private void freeEndedSlots() {
+    for (final Iterator<Integer> it = ended.iterator(); it.hasNext(); ) {
+      final int slot = it.next();
+      if (ZbHip.pendingContinuations(handle, slot) == 0) {
+        usedSlots.clear(slot);
+        it.remove();
+      }
+    }
+  }
+
+  /** A continuation the window's command i wrote unprocessed (Window.emit, in log order). */
+  void expectContinuation(final Continuation c) {
+    continuations.addLast(c);
   }
 
   int internName(final String name) {
@@ -236,6 +379,12 @@ public final class GpuBatchProcessor implements RecordProcessor {
     if (s >= INSTANCES) {
       s = usedSlots.nextClearBit(0);
     }
+    while (s < INSTANCES && window.addresses(s)) {
+      s = usedSlots.nextClearBit(s + 1);
+    }
+    if (s >= INSTANCES) {
+      return -1;
+    }
     usedSlots.set(s);
     nextFreeSlot = s + 1;
     return s;
@@ -243,6 +392,11 @@ public final class GpuBatchProcessor implements RecordProcessor {
 
   ZbHip.Deployed process(final int index) {
     return byIndex.get(index);
+  }
+
+  /** A value-dictionary string (string variables). */
+  byte[] stringValue(final long id) {
+    return ZbHip.stringValue(handle, id);
   }
 
   /** The partition's name dictionary (variable names of VARIABLE records). */
@@ -260,19 +414,39 @@ public final class GpuBatchProcessor implements RecordProcessor {
     final int instance = window.instanceOf(i);
     if (handedOff.add(instance)) {
       // the instance's zb-db entries into RocksDB (the platform's transaction), then off the device
-      ZbHip.handOff(handle, instance, zeebeDb::upsert);
+      // with its waiting continuations (the engine reads them back from the log)
+      ZbHip.handOff(handle, instance, (cf, key, value) -> {
+        if (cf == JobTypes.JOBS_COLUMN_FAMILY) {
+          engineJobTypes.add(JobTypes.typeOfJobsValue(value));
+        }
+        zeebeDb.upsert(cf, key, value);
+      });
+      continuations.removeIf(c -> c.slot() == instance);
       usedSlots.clear(instance);
+      ended.remove(instance);
     }
     final long before = ZbHip.keyBefore(handle, i);
     keyGenerator.setKeyIfHigher(before);
-    final ProcessingResult result = engine.process(record, out);
-    ZbHip.setExternalKeys(handle, i, (int) (keyGenerator.getCurrentKey() - before));
-    return result;
+    // the keys the engine's batch generates (follow-ups included) are declared after it
+    out.appendPostCommitTask(() -> {
+      ZbHip.setExternalKeys(handle, i, (int) (keyGenerator.getCurrentKey() - before));
+      return true;
+    });
+    return engine.process(record, out);
   }
 
-  /** Raw column-family writes of a hand-off; the broker binds this to its ZeebeDb transaction. */
-  public interface RawDbWriter {
-    void upsert(int columnFamily, byte[] key, byte[] value);
+  // ---- job activation (JobBatchActivateProcessor.java:60-143) --------------------------------------
+
+  private ProcessingResult activateJobs(
+      final TypedRecord record, final JobBatchRecord batch, final ProcessingResultBuilder out) {
+    ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
+    final JobActivation activation = JobActivation.of(arena, batch, record.getTimestamp(), this);
+    ZbHip.activateJobs(handle, activation.command(), activation.jobs(), activation.capacity(), activation.result());
+    activation.emit(record, out, this);
+    if (activation.key() >= 0) {
+      keyGenerator.setKeyIfHigher(activation.key());
+    }
+    return out.build();
   }
 
   public void close() {

@@ -1,0 +1,112 @@
+/*
+ * Recovery hand-back (StreamProcessorLifecycleAware.onRecovered): after replay RocksDB holds every
+ * instance; the entries of the instances the device takes over (processes deployed on it, minus
+ * instances a command still waiting in the log addresses by its own record) are selected natively
+ * (zbhip_select_instances_db), imported into HBM (zbhip_import_state_db) and deleted from RocksDB.
+ * The Python mirror is GpuBatchProcessor.on_recovered in zeebe_amd/adapter.py.  Not compiled in this
+ * image (no JDK).
+ */
+package io.camunda.zeebe.zbhip;
+
+import io.camunda.zeebe.logstreams.log.LogStreamReader;
+import io.camunda.zeebe.logstreams.log.LoggedEvent;
+import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceRecord;
+import io.camunda.zeebe.protocol.record.RecordType;
+import io.camunda.zeebe.protocol.record.ValueType;
+import java.lang.foreign.Arena;
+import java.lang.foreign.MemorySegment;
+import java.lang.foreign.ValueLayout;
+import java.util.ArrayList;
+import java.util.List;
+import java.util.Set;
+import java.util.TreeSet;
+
+final class RecoveredState {
+  private record Entry(int columnFamily, byte[] key, byte[] value) {}
+
+  private final List<Entry> moved;
+  private final long bytes;
+
+  private RecoveredState(final List<Entry> moved) {
+    this.moved = moved;
+    long b = 0;
+    for (final Entry e : moved) {
+      b += 12L + e.key().length + e.value().length;
+    }
+    bytes = b;
+  }
+
+  static RecoveredState collect(final MemorySegment handle, final GpuBatchProcessor.RawDb db, final LogStreamReader reader) {
+    final List<Entry> all = new ArrayList<>();
+    db.forEach((cf, key, value) -> all.add(new Entry(cf, key, value)));
+    // process instances an unprocessed command in the rest of the log addresses (the reader stands
+    // at the first record after the last processed one)
+    final Set<Long> waiting = new TreeSet<>();
+    final RecordMetadata meta = new RecordMetadata();
+    final ProcessInstanceRecord pi = new ProcessInstanceRecord();
+    while (reader.hasNext()) {
+      final LoggedEvent event = reader.next();
+      event.readMetadata(meta);
+      if (meta.getRecordType() == RecordType.COMMAND && !event.shouldSkipProcessing()
+          && meta.getValueType() == ValueType.PROCESS_INSTANCE) {
+        event.readValue(pi);
+        waiting.add(pi.getProcessInstanceKey());
+      }
+    }
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment blob = serialize(a, all);
+      final MemorySegment exclude = a.allocateArray(ValueLayout.JAVA_LONG, waiting.stream().mapToLong(Long::longValue).toArray());
+      final MemorySegment take = a.allocate(Math.max(1, all.size()));
+      ZbHip.selectInstancesDb(handle, blob, blob.byteSize(), exclude, waiting.size(), take, all.size());
+      final List<Entry> moved = new ArrayList<>();
+      for (int i = 0; i < all.size(); i++) {
+        if (take.get(ValueLayout.JAVA_BYTE, i) != 0) {
+          moved.add(all.get(i));
+        }
+      }
+      return new RecoveredState(moved);
+    }
+  }
+
+  int size() {
+    return moved.size();
+  }
+
+  long bytes() {
+    return bytes;
+  }
+
+  /** The moved entries as zbhip_import_state_db's flat buffer. */
+  MemorySegment entries(final Arena arena) {
+    return serialize(arena, moved);
+  }
+
+  void forEachMoved(final Deleter d) {
+    for (final Entry e : moved) {
+      d.delete(e.columnFamily(), e.key());
+    }
+  }
+
+  interface Deleter {
+    void delete(int columnFamily, byte[] key);
+  }
+
+  private static MemorySegment serialize(final Arena arena, final List<Entry> entries) {
+    long n = 0;
+    for (final Entry e : entries) {
+      n += 12L + e.key().length + e.value().length;
+    }
+    final MemorySegment out = arena.allocate(Math.max(1, n), 8);
+    long o = 0;
+    for (final Entry e : entries) {
+      out.set(ValueLayout.JAVA_INT_UNALIGNED, o, e.columnFamily());
+      out.set(ValueLayout.JAVA_INT_UNALIGNED, o + 4, e.key().length);
+      out.set(ValueLayout.JAVA_INT_UNALIGNED, o + 8, e.value().length);
+      MemorySegment.copy(e.key(), 0, out, ValueLayout.JAVA_BYTE, o + 12, e.key().length);
+      MemorySegment.copy(e.value(), 0, out, ValueLayout.JAVA_BYTE, o + 12 + e.key().length, e.value().length);
+      o += 12L + e.key().length + e.value().length;
+    }
+    return out.asSlice(0, n);
+  }
+}

@@ -37,13 +37,17 @@ import io.camunda.zeebe.protocol.record.intent.ProcessInstanceIntent;
 import io.camunda.zeebe.protocol.record.intent.VariableIntent;
 import io.camunda.zeebe.protocol.record.value.BpmnElementType;
 import io.camunda.zeebe.protocol.record.value.BpmnEventType;
+import io.camunda.zeebe.logstreams.log.LoggedEvent;
 import io.camunda.zeebe.stream.api.ProcessingResultBuilder;
+import io.camunda.zeebe.stream.api.records.TypedRecord;
+import io.camunda.zeebe.stream.impl.records.RecordValues;
+import io.camunda.zeebe.stream.impl.records.TypedRecordImpl;
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
 import java.util.ArrayList;
 import java.util.Arrays;
+import java.util.BitSet;
 import java.util.List;
-import java.util.function.IntConsumer;
 import org.agrona.DirectBuffer;
 import org.agrona.concurrent.UnsafeBuffer;
 
@@ -54,17 +58,18 @@ final class Window {
   private static final int MAX = 1 << 16;
   private static final int MAX_DOCS = 16 * MAX;
 
+  private MemorySegment handle;
   private MemorySegment cmds;
   private MemorySegment docs;
   private MemorySegment recs;
   private long recCap;
   private int n;
   private int nDocs;
-  private long nRecs;
   private long sourceBase; // zbhip_record.source_index of this window's first command (submission order)
   private final long[] positions = new long[MAX];
   private final int[] instances = new int[MAX];
-  private int[] recBegin = new int[MAX + 1];
+  private final BitSet addressed = new BitSet(); // instance slots the window's commands address
+  private static final RecordValues RECORD_VALUES = new RecordValues();
   // the command's msgpack variable document and each entry's msgpack value (VARIABLE records)
   private final DirectBuffer[] documents = new DirectBuffer[MAX];
   private final List<DirectBuffer> entryValues = new ArrayList<>();
@@ -78,8 +83,8 @@ final class Window {
   void reset(final long firstPosition) {
     sourceBase += n;
     n = 0;
+    addressed.clear();
     nDocs = 0;
-    nRecs = 0;
     entryValues.clear();
     Arrays.fill(documents, null);
   }
@@ -101,26 +106,53 @@ final class Window {
     return instances[i];
   }
 
+  boolean addresses(final int slot) {
+    return addressed.get(slot);
+  }
+
+  /**
+   * A log command read ahead, as the platform's TypedRecord: metadata copied, the value read into a
+   * fresh object (RecordValues reuses its instances), so it stays valid while the reader moves on.
+   */
+  static TypedRecord typed(final LoggedEvent event, final RecordMetadata meta, final int partitionId) {
+    final TypedRecordImpl r = new TypedRecordImpl(partitionId);
+    final RecordMetadata copy = new RecordMetadata();
+    copy.wrap(meta);
+    final UnifiedRecordValue value =
+        switch (meta.getValueType()) {
+          case PROCESS_INSTANCE_CREATION -> new ProcessInstanceCreationRecord();
+          case JOB -> new JobRecord();
+          case TIMER -> new TimerRecord();
+          case PROCESS_INSTANCE -> new ProcessInstanceRecord();
+          default -> RECORD_VALUES.readRecordValue(event, meta.getValueType());
+        };
+    event.readValue(value);
+    r.wrap(event, copy, value);
+    return r;
+  }
+
   /** PROCESS_INSTANCE_CREATION:CREATE -> ZBHIP_CMD_CREATE into instance slot {@code slot}. */
   boolean addCreate(
-      final long position, final int process, final int slot, final DirectBuffer variables, final GpuBatchProcessor p) {
+      final long position, final TypedRecord command, final int process, final int slot, final GpuBatchProcessor p) {
+    final DirectBuffer variables = ((ProcessInstanceCreationRecord) command.getValue()).getVariablesBuffer();
     final int first = nDocs;
     final int count = decodeDocument(variables, p);
     if (count < 0) {
       return false;
     }
-    put(position, slot, ZbHip.CMD_CREATE, count, process, first, variables);
+    put(position, command, slot, ZbHip.CMD_CREATE, count, process, first, variables);
     return true;
   }
 
   /** JOB:COMPLETE -> ZBHIP_CMD_JOB_COMPLETE; ref = zbhip_resolve_key's (slot << 16 | ordinal). */
-  boolean addJobComplete(final long position, final long ref, final DirectBuffer variables, final GpuBatchProcessor p) {
+  boolean addJobComplete(final long position, final TypedRecord command, final long ref, final GpuBatchProcessor p) {
+    final DirectBuffer variables = ((JobRecord) command.getValue()).getVariablesBuffer();
     final int first = nDocs;
     final int count = decodeDocument(variables, p);
     if (count < 0) {
       return false;
     }
-    put(position, (int) (ref >>> 16), ZbHip.CMD_JOB_COMPLETE, count, (int) (ref & 0xFFFF), first, variables);
+    put(position, command, (int) (ref >>> 16), ZbHip.CMD_JOB_COMPLETE, count, (int) (ref & 0xFFFF), first, variables);
     return true;
   }
 
@@ -128,15 +160,30 @@ final class Window {
    * TIMER:TRIGGER -> ZBHIP_CMD_TIMER_TRIGGER; ref = zbhip_resolve_key's (slot << 16 | ordinal) of the
    * timer key, the command's dueDate in doc_begin (low) and pad (high).
    */
-  void addTimerTrigger(final long position, final long ref, final long dueDate) {
-    put(position, (int) (ref >>> 16), ZbHip.CMD_TIMER_TRIGGER, 0, (int) (ref & 0xFFFF), (int) dueDate, EMPTY);
+  void addTimerTrigger(final long position, final TypedRecord command, final long ref, final long dueDate) {
+    put(position, command, (int) (ref >>> 16), ZbHip.CMD_TIMER_TRIGGER, 0, (int) (ref & 0xFFFF), (int) dueDate, EMPTY);
     cmds.set(JAVA_INT, ZbHip.COMMAND.byteSize() * (n - 1) + 12, (int) (dueDate >>> 32)); // pad: dueDate high word
+  }
+
+  /**
+   * A follow-up an earlier device batch wrote unprocessed, read back at its log position ->
+   * ZBHIP_CMD_CONTINUE with its continuation id in doc_begin (low) and pad (high).
+   */
+  void addContinuation(final long position, final TypedRecord command, final int slot, final long id) {
+    put(position, command, slot, ZbHip.CMD_CONTINUE, 0, 0, (int) id, EMPTY);
+    cmds.set(JAVA_INT, ZbHip.COMMAND.byteSize() * (n - 1) + 12, (int) (id >>> 32));
   }
 
   private static final DirectBuffer EMPTY = new UnsafeBuffer(new byte[0]);
 
   private void put(
-      final long position, final int instance, final byte kind, final int docCount, final int ref, final int docBegin,
+      final long position,
+      final TypedRecord command,
+      final int instance,
+      final byte kind,
+      final int docCount,
+      final int ref,
+      final int docBegin,
       final DirectBuffer variables) {
     final long o = ZbHip.COMMAND.byteSize() * n;
     cmds.set(JAVA_INT, o, instance);
@@ -147,6 +194,7 @@ final class Window {
     cmds.set(JAVA_INT, o + 12, 0);
     positions[n] = position;
     instances[n] = instance;
+    addressed.set(instance);
     documents[n] = copy(variables, 0, variables.capacity());
     n++;
   }
@@ -209,50 +257,37 @@ final class Window {
     return new UnsafeBuffer(b);
   }
 
-  /** zbhip_submit + zbhip_run + zbhip_drain; recBegin[i] = first record of window command i. */
-  void submitRunDrain(final MemorySegment handle) {
+  /**
+   * zbhip_submit + zbhip_run.  The records are drained command by command when the platform reaches
+   * each (zbhip_drain_command): the keys of commands after a fallback command are fixed only once the
+   * CPU engine's keys for it are declared.
+   */
+  void submitRun(final MemorySegment handle) {
+    this.handle = handle;
     ZbHip.submit(handle, cmds, n, docs, nDocs);
     ZbHip.run(handle, 0);
-    final long pending = ZbHip.pendingRecords(handle);
-    if (pending > recCap) {
-      recCap = Math.max(pending, 2 * recCap);
-      recs = Arena.ofAuto().allocate(ZbHip.RECORD.byteSize() * recCap, 16);
-    }
-    nRecs = ZbHip.drain(handle, recs, recCap);
-    if (recBegin.length < n + 1) {
-      recBegin = new int[n + 1];
-    }
-    Arrays.fill(recBegin, 0, n + 1, 0);
-    for (long r = 0; r < nRecs; r++) {
-      recBegin[(int) (recs.get(JAVA_LONG, r * 80 + 24) - sourceBase) + 1]++; // records are ordered by source
-    }
-    for (int i = 0; i < n; i++) {
-      recBegin[i + 1] += recBegin[i];
-    }
   }
 
-  /** Slots of process instances completed by the window (PROCESS ELEMENT_COMPLETED records). */
-  void forEachEndedInstance(final IntConsumer slot) {
-    for (long r = 0; r < nRecs; r++) {
-      final long o = r * 80;
-      if (recs.get(JAVA_BYTE, o + 41) == ValueType.PROCESS_INSTANCE.value()
-          && recs.get(JAVA_BYTE, o + 42) == ProcessInstanceIntent.ELEMENT_COMPLETED.value()
-          && recs.get(JAVA_INT, o + 36) == 0) {
-        slot.accept(instances[(int) (recs.get(JAVA_LONG, o + 24) - sourceBase)]);
-      }
-    }
-  }
-
-  /** Appends window command i's records to the builder, as the reference's processors would. */
-  void emit(final int i, final ProcessingResultBuilder out, final GpuBatchProcessor p) {
+  /**
+   * Appends window command i's records to the builder, as the reference's processors would, and
+   * returns how many follow-up commands the platform will feed back (the ones not written
+   * unprocessed).  A rejection of the command itself carries the command's value
+   * (TypedRejectionWriter.appendRejection: TimerRecord, JobRecord, ... as the log holds them);
+   * every follow-up written unprocessed is expected back from the log as a continuation (its id in
+   * the record's aux); a process instance that completed frees its slot once its continuations ran.
+   */
+  int emit(final int i, final TypedRecord command, final ProcessingResultBuilder out, final GpuBatchProcessor p) {
+    final long nr = ZbHip.drainCommand(handle, i, this::ofAtLeast);
     final RecordMetadata meta = new RecordMetadata();
-    for (int r = recBegin[i]; r < recBegin[i + 1]; r++) {
+    int admitted = 0;
+    for (long r = 0; r < nr; r++) {
       final MemorySegment rec = recs.asSlice(80L * r, 80);
       final long key = rec.get(JAVA_LONG, 0);
       final byte recordType = rec.get(JAVA_BYTE, 40);
       final byte valueType = rec.get(JAVA_BYTE, 41);
       final byte intent = rec.get(JAVA_BYTE, 42);
       final int rejection = rec.get(JAVA_BYTE, 43) & 0xFF;
+      final int ordinal = rec.get(JAVA_SHORT, 44) & 0xFFFF;
       meta.reset()
           .recordType(RecordType.values()[recordType])
           .valueType(ValueType.get((short) valueType))
@@ -260,8 +295,34 @@ final class Window {
       if (rejection != 0xFF) {
         meta.rejectionType(RejectionType.get((short) rejection)).rejectionReason(p.rejectionReason(rec));
       }
-      out.appendRecord(key, value(rec, i, p), meta);
+      final boolean ofCommand = recordType == RecordType.COMMAND_REJECTION.value() && ordinal == 0
+          && valueType == command.getValueType().value() && intent == command.getIntent().value();
+      final UnifiedRecordValue value = ofCommand ? (UnifiedRecordValue) command.getValue() : value(rec, i, p);
+      out.appendRecord(key, value, meta);
+      if (recordType == RecordType.COMMAND.value()) {
+        if (rec.get(JAVA_BYTE, 77) != 0) { // zbhip_record.unprocessed: a continuation, its id in aux
+          final ProcessInstanceRecord v = (ProcessInstanceRecord) value;
+          p.expectContinuation(new GpuBatchProcessor.Continuation(
+              rec.get(JAVA_LONG, 48), instances[i], key, intent, v.getElementId(), v.getFlowScopeKey(),
+              v.getProcessInstanceKey()));
+        } else {
+          admitted++;
+        }
+      } else if (valueType == ValueType.PROCESS_INSTANCE.value()
+          && intent == ProcessInstanceIntent.ELEMENT_COMPLETED.value() && rec.get(JAVA_INT, 36) == 0) {
+        p.instanceEnded(instances[i]); // the process element (index 0) completed
+      }
     }
+    return admitted;
+  }
+
+  /** A record buffer of at least {@code n} rows (zbhip_drain_command's output). */
+  private MemorySegment ofAtLeast(final long n) {
+    if (n > recCap) {
+      recCap = Math.max(n, 2 * recCap);
+      recs = Arena.ofAuto().allocate(ZbHip.RECORD.byteSize() * recCap, 16);
+    }
+    return recs;
   }
 
   private static Intent intent(final byte valueType, final byte intent) {

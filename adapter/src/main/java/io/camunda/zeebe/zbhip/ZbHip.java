@@ -35,11 +35,14 @@ public final class ZbHip {
   // ---- error codes (zbhip.h zbhip_status) ----
   public static final int OK = 0;
   public static final int EUNSUPP = -5;
+  public static final int ENOMEM = -2;
 
   // ---- command kinds (zbhip_command_kind) ----
   public static final byte CMD_CREATE = 1; // PROCESS_INSTANCE_CREATION:CREATE
   public static final byte CMD_JOB_COMPLETE = 2; // JOB:COMPLETE
   public static final byte CMD_TIMER_TRIGGER = 8; // TIMER:TRIGGER (the due-date checker's command)
+  public static final byte CMD_CONTINUE = 9; // a deferred continuation read back from the log
+  public static final int OPEN_DEFER_CONTINUATIONS = 2; // zbhip_config.flags
   public static final byte CMD_PUBLISH = 3; // MESSAGE:PUBLISH (config 5)
   public static final byte CMD_MSG_SUB_CREATE = 4;
   public static final byte CMD_PMS_CREATE = 5;
@@ -173,6 +176,22 @@ public final class ZbHip {
       fn("zbhip_export_instances_db", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle EVICT = fn("zbhip_evict_instances", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG));
   private static final MethodHandle KEY_BEFORE = fn("zbhip_key_before", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
+  private static final MethodHandle CONTINUATIONS =
+      fn("zbhip_continuations", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
+  private static final MethodHandle PENDING_CONTINUATIONS =
+      fn("zbhip_pending_continuations", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
+  private static final MethodHandle CURRENT_KEY = fn("zbhip_current_key", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
+  private static final MethodHandle SET_KEY_IF_HIGHER =
+      fn("zbhip_set_key_if_higher", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG));
+  private static final MethodHandle ACTIVATE_JOBS =
+      fn("zbhip_activate_jobs", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
+  private static final MethodHandle DRAIN_COMMAND =
+      fn("zbhip_drain_command", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
+  private static final MethodHandle STRING_VALUE =
+      fn("zbhip_string_value", FunctionDescriptor.of(ADDRESS, ADDRESS, JAVA_INT, ADDRESS));
+  private static final MethodHandle SELECT_INSTANCES_DB =
+      fn("zbhip_select_instances_db",
+          FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle EXTERNAL_KEYS =
       fn("zbhip_set_external_keys", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, JAVA_INT));
   private static final MethodHandle IMPORT_DB =
@@ -218,7 +237,8 @@ public final class ZbHip {
       final int maxInstances,
       final int maxCommands,
       final long initialKey,
-      final int maxCorrelationKeys) {
+      final int maxCorrelationKeys,
+      final int flags) {
     final MemorySegment cfg = arena.allocate(CONFIG);
     cfg.set(JAVA_INT, 0, partitionId);
     cfg.set(JAVA_INT, 4, partitionCount);
@@ -230,7 +250,7 @@ public final class ZbHip {
     cfg.set(JAVA_INT, 28, 16 * maxCommands);
     cfg.set(JAVA_LONG, 32, initialKey);
     cfg.set(JAVA_INT, 40, maxCorrelationKeys);
-    cfg.set(JAVA_INT, 44, 0);
+    cfg.set(JAVA_INT, 44, flags);
     cfg.set(ADDRESS, 48, MemorySegment.NULL);
     final MemorySegment out = arena.allocate(ADDRESS);
     check((int) call(OPEN, cfg, out), "zbhip_open");
@@ -423,6 +443,88 @@ public final class ZbHip {
       final MemorySegment k = a.allocate(JAVA_LONG);
       check((int) call(KEY_BEFORE, h, i, k), "zbhip_key_before");
       return k.get(JAVA_LONG, 0);
+    }
+  }
+
+  /** zbhip_continuations: [first id, count] the last run deferred, in drain order of its unprocessed records. */
+  public static long[] continuations(final MemorySegment h) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment first = a.allocate(JAVA_LONG);
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      check((int) call(CONTINUATIONS, h, first, n), "zbhip_continuations");
+      return new long[] {first.get(JAVA_LONG, 0), n.get(JAVA_LONG, 0)};
+    }
+  }
+
+  public static int pendingContinuations(final MemorySegment h, final int instance) {
+    return check((int) call(PENDING_CONTINUATIONS, h, instance), "zbhip_pending_continuations");
+  }
+
+  /** DbKeyGenerator's last key on the device (the last window's keys and the declared CPU-engine keys). */
+  public static long currentKey(final MemorySegment h) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment k = a.allocate(JAVA_LONG);
+      check((int) call(CURRENT_KEY, h, k), "zbhip_current_key");
+      return k.get(JAVA_LONG, 0);
+    }
+  }
+
+  /** KeyGeneratorControls.setKeyIfHigher on the device: keys the CPU engine generated between windows. */
+  public static void setKeyIfHigher(final MemorySegment h, final long key) {
+    check((int) call(SET_KEY_IF_HIGHER, h, key), "zbhip_set_key_if_higher");
+  }
+
+  /**
+   * zbhip_activate_jobs (JOB_BATCH:ACTIVATE): {@code cmd} a zbhip_job_activation, {@code jobs} room
+   * for {@code cap} zbhip_activated_job rows, {@code result} a zbhip_job_batch.
+   */
+  public static void activateJobs(
+      final MemorySegment h, final MemorySegment cmd, final MemorySegment jobs, final long cap, final MemorySegment result) {
+    check((int) call(ACTIVATE_JOBS, h, cmd, jobs, cap, result), "zbhip_activate_jobs");
+  }
+
+  /** Room for the records of one command: returns a buffer of at least n RECORD rows. */
+  public interface RecordBuffer {
+    MemorySegment ofAtLeast(long n);
+  }
+
+  /** zbhip_drain_command: the records of window command i into {@code buffer}; returns their number. */
+  public static long drainCommand(final MemorySegment h, final long i, final RecordBuffer buffer) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      MemorySegment out = buffer.ofAtLeast(256);
+      int rc = (int) call(DRAIN_COMMAND, h, i, out, out.byteSize() / 80, n);
+      if (rc == ENOMEM) { // more records than the buffer: n holds how many
+        out = buffer.ofAtLeast(n.get(JAVA_LONG, 0));
+        rc = (int) call(DRAIN_COMMAND, h, i, out, out.byteSize() / 80, n);
+      }
+      check(rc, "zbhip_drain_command");
+      return n.get(JAVA_LONG, 0);
+    }
+  }
+
+  /** zbhip_string_value: the bytes of value-dictionary string {@code id}. */
+  public static byte[] stringValue(final MemorySegment h, final long id) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment len = a.allocate(JAVA_LONG);
+      final MemorySegment p = (MemorySegment) call(STRING_VALUE, h, (int) id, len);
+      return p.reinterpret(len.get(JAVA_LONG, 0)).toArray(JAVA_BYTE);
+    }
+  }
+
+  /** zbhip_select_instances_db: marks in {@code take} the entries of the instances the device takes over. */
+  public static int selectInstancesDb(
+      final MemorySegment h,
+      final MemorySegment entries,
+      final long len,
+      final MemorySegment exclude,
+      final long nExclude,
+      final MemorySegment take,
+      final long nTake) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      return check((int) call(SELECT_INSTANCES_DB, h, entries, len, exclude, nExclude, take, nTake, n),
+          "zbhip_select_instances_db");
     }
   }
 

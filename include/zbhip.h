@@ -38,10 +38,13 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 4  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+#define ZBHIP_ABI_VERSION 5  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
                                4: timer boundary events (start_event / flow_source / job_retries of job
                                   workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
-                                  PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions */
+                                  PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions;
+                               5: ZBHIP_OPEN_DEFER_CONTINUATIONS / ZBHIP_CMD_CONTINUE,
+                                  zbhip_continuations, zbhip_pending_continuations, zbhip_current_key,
+                                  zbhip_set_key_if_higher */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -246,6 +249,13 @@ typedef struct zbhip_config {
 /* The caller guarantees that a device-resident window (zbhip_submit_device*) addresses every subject
  * at most once; without this flag every device window's subjects are checked on the device first. */
 #define ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS 1u
+/* Follow-up commands written to the log unprocessed (past maxCommandsInBatch) are not run after
+ * their window: each waits as a continuation until the log reader submits it at its own log
+ * position (ZBHIP_CMD_CONTINUE), so commands the log holds between the two -- other hot-path
+ * commands, the CPU engine's -- come first, as in the reference.  Without the flag zbhip_run runs
+ * them right after the window (a log that holds nothing in between: the benches, the oracle's
+ * window model). */
+#define ZBHIP_OPEN_DEFER_CONTINUATIONS 2u
 
 typedef struct zbhip_handle zbhip_handle;
 
@@ -277,7 +287,12 @@ enum zbhip_command_kind {
   /* TIMER:TRIGGER (TriggerTimerProcessor.java:81-114, written by DueDateTimerChecker for a due
    * timer): instance = the instance slot, ref = the timer key's ordinal in the instance,
    * (doc_begin | pad << 32) = the timer's dueDate (the command's TimerRecord.dueDate) */
-  ZBHIP_CMD_TIMER_TRIGGER = 8
+  ZBHIP_CMD_TIMER_TRIGGER = 8,
+  /* A follow-up command an earlier batch wrote to the log unprocessed (past maxCommandsInBatch,
+   * ProcessingStateMachine.java:388-417) and the platform now reads back as a batch of its own, on a
+   * handle opened with ZBHIP_OPEN_DEFER_CONTINUATIONS: instance = its instance slot,
+   * doc_begin | pad << 32 = its continuation id (zbhip_continuations).  Host windows only. */
+  ZBHIP_CMD_CONTINUE = 9
 };
 
 /* STR values are string ids of the partition's value dictionary (zbhip_intern_string). */
@@ -401,6 +416,14 @@ typedef struct zbhip_record {
 #define ZBHIP_NO_STRING 0xFFFFFFFFu
 
 int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out);
+/* The records of window command i only (plain windows; ZBHIP_EUNSUPP for message partitions): what a
+ * host adapter emits when the platform reaches command i.  Keys of the commands after a fallback
+ * command are fixed once the CPU engine's keys for it are declared (zbhip_set_external_keys), so a
+ * command after an undeclared fallback returns ZBHIP_ESTATE; zbhip_drain, by contrast, fixes the
+ * whole window (undeclared fallbacks generated no keys).  cap too small: ZBHIP_ENOMEM with *n_out =
+ * the records needed.  With ZBHIP_OPEN_DEFER_CONTINUATIONS a record written unprocessed carries its
+ * continuation id in aux. */
+int zbhip_drain_command(zbhip_handle* h, size_t i, zbhip_record* out, size_t cap, size_t* n_out);
 /* Number of records the last run produced (before draining). */
 int64_t zbhip_pending_records(zbhip_handle* h);
 
@@ -456,6 +479,21 @@ int zbhip_string_partitions(zbhip_handle* h, const uint32_t* ids, size_t n, int3
 /* Instances whose last batch needs the fallback path (incident, FEEL outside the
  * subset, batch-limit overflow, capacity).  Their state was left untouched. */
 int zbhip_fallback(zbhip_handle* h, uint32_t* instances, size_t cap, size_t* n_out);
+
+/* ZBHIP_OPEN_DEFER_CONTINUATIONS: the continuation ids the last run handed out, [first, first + n),
+ * one per drained record with `unprocessed` set, in drain order. */
+int zbhip_continuations(zbhip_handle* h, uint64_t* first_id, uint64_t* n);
+/* Continuations of the instance in slot `instance` still waiting to be read back: its slot is not
+ * free for a CREATE until they ran (or the instance was evicted, which drops them). */
+int zbhip_pending_continuations(zbhip_handle* h, uint32_t instance);
+
+/* DbKeyGenerator between windows (stream-platform/.../state/DbKeyGenerator.java:39-61).  The
+ * partition has one key generator: the host keeps the reference's (the CPU engine's, in RocksDB)
+ * level with the device's.  zbhip_current_key: the last key generated so far (the last window's keys
+ * and the CPU engine's declared ones); zbhip_set_key_if_higher: keys the CPU engine generated
+ * between windows (KeyGeneratorControls.setKeyIfHigher), the next window's follow them. */
+int zbhip_current_key(zbhip_handle* h, int64_t* key);
+int zbhip_set_key_if_higher(zbhip_handle* h, int64_t key);
 
 /* Status of command i of the last run: 0 = processed, 1 = needs the fallback path; *reason is
  * the device fallback code (FB_* in zeebe_amd/csrc/zb_internal.h), 0 when processed. */
@@ -633,6 +671,13 @@ typedef int64_t (*zbhip_string_interner)(void* ctx, const char* bytes, size_t le
 int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t column_family, const uint8_t* key, size_t key_len,
                                         const uint8_t* value, size_t value_len, zbhip_string_interner intern,
                                         void* ictx, char* row, size_t cap);
+/* Recovery hand-back (StreamProcessorLifecycleAware.onRecovered): of the entries (the format below) of
+ * the engine's state, marks in take[i] those of the process instances the handle can take over --
+ * instances of processes deployed on it, minus the process instance keys in `exclude` (instances a
+ * command still waiting in the log addresses by its own record).  *n_entries = entries read (take
+ * needs that many bytes, else ZBHIP_ENOMEM).  Returns the number of instances selected. */
+int zbhip_select_instances_db(zbhip_handle* h, const uint8_t* entries, size_t len, const int64_t* exclude,
+                              size_t n_exclude, uint8_t* take, size_t n_take, size_t* n_entries);
 /* Loads process instances into free instance slots from their zb-db entries (a flat buffer of
  * entries, each: uint32 column family, uint32 key length, uint32 value length, key bytes, value bytes
  * -- the entries zbhip_export_state_db / zbhip_export_instances_db produce, e.g. a RocksDB

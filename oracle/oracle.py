@@ -60,6 +60,10 @@ def lib():
         L.zbo_key_counter.restype = C.c_int64
         L.zbo_key_counter.argtypes = [C.c_void_p]
         L.zbo_set_key_counter.argtypes = [C.c_void_p, C.c_int64]
+        L.zbo_process_one.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_int64, C.c_int]
+        L.zbo_import_rows.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        L.zbo_ordinal_of.restype = C.c_int64
+        L.zbo_ordinal_of.argtypes = [C.c_void_p, C.c_uint32, C.c_int64]
         L.zbo_n_records.restype = C.c_size_t
         L.zbo_n_records.argtypes = [C.c_void_p]
         L.zbo_records.restype = C.c_size_t
@@ -232,6 +236,28 @@ class Oracle:
         buf = C.create_string_buffer(n)
         self.L.zbo_state(self.h, buf, n)
         return [r for r in buf.value.decode().split("\n") if r]
+
+    def process_one(self, rec, instance, docs=None, source=0, first_ordinal=0):
+        """Engine.process for exactly one command (a RECORD_DTYPE row, see zb_oracle.cpp
+        process_one): its records are appended to records(); returns how many."""
+        r = np.ascontiguousarray(np.asarray(rec, dtype=abi.RECORD_DTYPE).reshape(1))
+        d = np.ascontiguousarray(docs if docs is not None else abi.make_docs(0), dtype=abi.DOC_DTYPE)
+        n = self.L.zbo_process_one(self.h, r.ctypes.data, instance, d.ctypes.data, len(d), source, first_ordinal)
+        if n < 0:
+            raise OracleError(self.L.zbo_last_error(self.h).decode())
+        return n
+
+    def ordinal_of(self, instance, key):
+        """The key's ordinal among the keys instance slot `instance` generated (-1 unknown)."""
+        return self.L.zbo_ordinal_of(self.h, instance, key)
+
+    def import_rows(self, rows):
+        """Column-family rows (the dump_state / zbhip_export_instances text) into this engine's state."""
+        text = "\n".join(rows).encode()
+        n = self.L.zbo_import_rows(self.h, text, len(text))
+        if n < 0:
+            raise OracleError(self.L.zbo_last_error(self.h).decode())
+        return n
 
     def counters(self):
         t, c, m = C.c_uint64(), C.c_uint64(), C.c_uint64()

@@ -986,6 +986,198 @@ class Oracle {
   }
 
   std::string dump_state() const;
+
+  // ---- one command at a time (tests/psm.py restates ProcessingStateMachine around this) ----------
+  // Engine.process (Engine.java:99-131) for exactly one command: its records are appended to `out`
+  // (ordinals from first_ordinal, source index `source`) and nothing else runs -- the caller's batch
+  // FIFO feeds the follow-up commands back.  The command comes as a record: value type, intent, key
+  // (JOB:COMPLETE: the job key; TIMER:TRIGGER: the timer key, dueDate in aux; PROCESS_INSTANCE
+  // commands: the element instance key or -1), process / element indices, flowScopeKey (scope_key),
+  // processInstanceKey; `instance` is its subject slot (key bookkeeping), `d` its variable document.
+  int process_one(const zbhip_record& r, uint32_t instance, const zbhip_doc_entry* d, size_t nd, int64_t source,
+                  int first_ordinal) {
+    ORecord rec{};
+    rec.r = r;
+    rec.r.record_type = ZBHIP_RT_COMMAND;
+    rec.r.unprocessed = 0;
+    rec.instance = instance;
+    rec.job_ord = -1;
+    const uint32_t base = (uint32_t)docs.size();
+    docs.insert(docs.end(), d, d + nd);
+    rec.doc = Doc{base, (uint32_t)nd};
+    rec.r.aux = r.value_type == ZBHIP_VT_TIMER ? r.aux : nd ? (int64_t)base : -1;
+    rec.pi.proc = r.process_idx;
+    rec.pi.elem = r.element_idx;
+    rec.pi.flowScopeKey = r.scope_key;
+    rec.pi.piKey = r.process_instance_key;
+    const bool known = (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION && r.intent == ZBHIP_PIC_CREATE) ||
+                       (r.value_type == ZBHIP_VT_JOB && r.intent == ZBHIP_JOB_COMPLETE) ||
+                       (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
+                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT);
+    if (!known) { last_error = "process_one: command outside the restated subset"; return ZBHIP_EUNSUPP; }
+    if (r.value_type == ZBHIP_VT_PROCESS_INSTANCE || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION)
+      if (r.process_idx < 0 || r.process_idx >= (int)procs.size() ||
+          (r.value_type == ZBHIP_VT_PROCESS_INSTANCE &&
+           (r.element_idx < 0 || r.element_idx >= (int)procs[r.process_idx].els.size()))) {
+        last_error = "process_one: unknown process or element";
+        return ZBHIP_EINVAL;
+      }
+    std::vector<ORecord> batch;
+    batch_ = &batch;
+    cur_instance_ = instance;
+    cur_slot_ = false;
+    cur_source_ = source;
+    try {
+      process(rec);
+    } catch (const Unsupported& u) {
+      batch_ = nullptr;
+      last_error = "unsupported: " + u.what;
+      return ZBHIP_EUNSUPP;
+    }
+    ++commands_processed;
+    batch_ = nullptr;
+    for (auto& x : batch) {
+      x.r.ordinal = (uint16_t)(x.r.ordinal + first_ordinal);
+      out.push_back(std::move(x));
+    }
+    return (int)batch.size();
+  }
+
+  // The zb-db rows of a hand-off (the device's zbhip_export_instances text, the dump_state format) into
+  // this engine's column families: what the host adapter's RawDbWriter puts into RocksDB before the
+  // CPU engine processes the instance's commands (fallback hand-off).  Returns the
+  // number of rows read, or < 0 (last_error) for a row outside the restated families.
+  int import_rows(const std::string& text) {
+    std::vector<std::vector<std::string>> rows;
+    size_t a = 0;
+    while (a < text.size()) {
+      size_t b = text.find('\n', a);
+      if (b == std::string::npos) b = text.size();
+      if (b > a) {
+        std::vector<std::string> parts;
+        size_t s = a;
+        for (size_t i = a; i <= b; ++i)
+          if (i == b || text[i] == '|') { parts.push_back(text.substr(s, i - s)); s = i + 1; }
+        rows.push_back(std::move(parts));
+      }
+      a = b + 1;
+    }
+    auto fields = [](const std::string& f) {
+      std::map<std::string, std::string> m;
+      size_t s = 0;
+      while (s <= f.size()) {
+        size_t e = f.find(',', s);
+        if (e == std::string::npos) e = f.size();
+        const std::string kv = f.substr(s, e - s);
+        const size_t q = kv.find('=');
+        if (q != std::string::npos) m[kv.substr(0, q)] = kv.substr(q + 1);
+        s = e + 1;
+      }
+      return m;
+    };
+    auto L = [](const std::string& v) { return (int64_t)std::stoll(v); };
+    auto find_proc = [this](int64_t def_key, const std::string& elem_id, int& proc, int& elem) {
+      for (size_t p = 0; p < procs.size(); ++p) {
+        if (procs[p].def_key != def_key) continue;
+        for (size_t e = 0; e < procs[p].els.size(); ++e)
+          if (procs[p].els[e].id == elem_id) { proc = (int)p; elem = (int)e; return true; }
+      }
+      return false;
+    };
+    int n = 0;
+    try {
+      // element instances first (the other families find their process through them), job states
+      // last (after their JOBS rows)
+      for (int pass = 0; pass < 3; ++pass)
+        for (auto& r : rows) {
+          const std::string& cf = r[0];
+          const bool first = cf == "ELEMENT_INSTANCE_KEY";
+          if ((first ? 0 : cf == "JOB_STATES" ? 2 : 1) != pass) continue;
+          ++n;
+          if (cf == "KEY" || cf == "TIMER_DUE_DATES" || cf == "JOB_ACTIVATABLE" || cf == "JOB_DEADLINES") continue;
+          if (first) {
+            auto f = fields(r.at(2));
+            ElementInstance ei;
+            ei.key = L(r.at(1));
+            ei.parentKey = L(f.at("parentKey"));
+            ei.childCount = (int)L(f.at("childCount"));
+            ei.jobKey = L(f.at("jobKey"));
+            ei.state = (int)L(f.at("state"));
+            ei.activeSequenceFlows = (int)L(f.at("activeSequenceFlows"));
+            ei.value.flowScopeKey = L(f.at("flowScopeKey"));
+            ei.value.piKey = L(f.at("processInstanceKey"));
+            if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), ei.value.proc, ei.value.elem))
+              throw Unsupported{"element " + f.at("elementId")};
+            ei_[ei.key] = ei;
+          } else if (cf == "ELEMENT_INSTANCE_PARENT_CHILD") {
+            parent_child_.insert({L(r.at(1)), L(r.at(2))});
+          } else if (cf == "ELEMENT_INSTANCE_CHILD_PARENT") {
+            child_parent_[L(r.at(1))] = L(r.at(2));
+          } else if (cf == "NUMBER_OF_TAKEN_SEQUENCE_FLOWS") {
+            const int64_t scope = L(r.at(1));
+            const OProc& pr = procs[ei_.at(scope).value.proc];
+            int gw = -1, fl = -1;
+            for (size_t e = 0; e < pr.els.size(); ++e) {
+              if (pr.els[e].id == r.at(2)) gw = (int)e;
+              if (pr.els[e].id == r.at(3)) fl = (int)e;
+            }
+            if (gw < 0 || fl < 0) throw Unsupported{"taken flow " + r.at(2) + "/" + r.at(3)};
+            taken_[{scope, gw, fl}] = (int)L(r.at(4));
+          } else if (cf == "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY") {
+            pi_by_def_.insert({L(r.at(1)), L(r.at(2))});
+          } else if (cf == "VARIABLES") {
+            auto f = fields(r.at(3));
+            vars_[{L(r.at(1)), intern(r.at(2))}] = VarRow{L(f.at("key")), (uint8_t)L(f.at("type")), L(f.at("value")), 0};
+          } else if (cf == "EVENT_SCOPE") {
+            auto f = fields(r.at(2));
+            const int64_t k = L(r.at(1));
+            event_scope_.insert(k);
+            if (f.at("accepting") == "0") es_closed_.insert(k);
+            if (f.at("interrupted") == "1") es_interrupted_.insert(k);
+          } else if (cf == "TIMERS") {
+            auto f = fields(r.at(3));
+            TimerRow t;
+            const int64_t eik = L(r.at(1));
+            if (!find_proc(L(f.at("processDefinitionKey")), f.at("handlerNodeId"), t.pi.proc, t.pi.elem))
+              throw Unsupported{"timer handler " + f.at("handlerNodeId")};
+            t.pi.piKey = L(f.at("processInstanceKey"));
+            auto eit = ei_.find(eik);
+            if (eit != ei_.end()) t.pi.flowScopeKey = eit->second.value.flowScopeKey;
+            t.dueDate = L(f.at("dueDate"));
+            t.reps = (int)L(f.at("repetitions"));
+            timers_[{eik, L(r.at(2))}] = t;
+          } else if (cf == "JOBS") {
+            auto f = fields(r.at(2));
+            JobRow j;
+            if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), j.pi.proc, j.pi.elem))
+              throw Unsupported{"job element " + f.at("elementId")};
+            j.pi.piKey = L(f.at("processInstanceKey"));
+            j.elementInstanceKey = L(f.at("elementInstanceKey"));
+            auto eit = ei_.find(j.elementInstanceKey);
+            if (eit != ei_.end()) j.pi.flowScopeKey = eit->second.value.flowScopeKey;
+            j.type = f.at("type");
+            j.retries = (int)L(f.at("retries"));
+            j.deadline = L(f.at("deadline"));
+            j.worker = f.at("worker");
+            jobs_[L(r.at(1))] = j;
+          } else if (cf == "JOB_STATES") {
+            const int64_t k = L(r.at(1));
+            JobRow& j = jobs_.at(k);
+            j.activated = r.at(2) == "ACTIVATED";
+            if (!j.activated) activatable_.insert({j.type, "<default>", k});
+          } else {
+            throw Unsupported{"column family " + cf};
+          }
+        }
+    } catch (const Unsupported& u) {
+      last_error = "import: " + u.what;
+      return ZBHIP_EUNSUPP;
+    } catch (const std::exception& e) {
+      last_error = std::string("import: malformed row (") + e.what() + ")";
+      return ZBHIP_EINVAL;
+    }
+    return n;
+  }
   // JOB_BATCH:ACTIVATE (processing/job/JobBatchActivateProcessor.java:60-143, JobBatchCollector.java
   // :67-123): jobs of `type` in JOB_ACTIVATABLE order ([[type, jobKey], tenant]), deadline, worker,
   // variables (JobVariablesCollector -> DbVariableState.getVariablesAsDocument :193-247: the element
@@ -1327,7 +1519,7 @@ class Oracle {
   // EventHandle.activateElement (EventHandle.java:104-131): PROCESS_EVENT:TRIGGERING (+key, no
   // variables) and COMPLETE_ELEMENT for the catch event
   void trigger_timer(ORecord& cmd) {
-    cmd.r.key = resolve(cmd.instance, (uint32_t)cmd.job_ord);
+    if (cmd.job_ord >= 0) cmd.r.key = resolve(cmd.instance, (uint32_t)cmd.job_ord);
     const int64_t tk = cmd.r.key;
     auto it = timers_.begin();
     for (; it != timers_.end(); ++it)
@@ -2511,6 +2703,21 @@ int zbo_activate_jobs(void* o, const char* type, const char* worker, int64_t tim
 void zbo_set_key_counter(void* o, int64_t v) { static_cast<Oracle*>(o)->set_key_counter(v); }
 
 size_t zbo_n_records(void* o) { return static_cast<Oracle*>(o)->out.size(); }
+int zbo_process_one(void* o, const zbhip_record* r, uint32_t instance, const zbhip_doc_entry* docs, size_t nd,
+                    int64_t source, int first_ordinal) {
+  return static_cast<Oracle*>(o)->process_one(*r, instance, docs, nd, source, first_ordinal);
+}
+int64_t zbo_ordinal_of(void* o, uint32_t instance, int64_t key) {
+  auto& m = static_cast<Oracle*>(o)->inst_keys;
+  auto it = m.find(instance);
+  if (it == m.end()) return -1;
+  for (size_t i = 0; i < it->second.size(); ++i)
+    if (it->second[i] == key) return (int64_t)i;
+  return -1;
+}
+int zbo_import_rows(void* o, const char* text, size_t len) {
+  return static_cast<Oracle*>(o)->import_rows(std::string(text, len));
+}
 size_t zbo_records(void* o, zbhip_record* out, size_t cap) {
   auto* O = static_cast<Oracle*>(o);
   size_t n = std::min(cap, O->out.size());

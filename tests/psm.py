@@ -1,0 +1,329 @@
+"""TEST INFRASTRUCTURE -- a restatement of stream-platform's processing loop over an in-memory log, the
+harness the reference's own platform tests use (stream-platform/src/test/.../StreamPlatform.java:63-85:
+ListLogStorage + SyncLogStream, a mocked RecordProcessor), with the CPU oracle as the engine behind
+the RecordProcessor interface.
+
+* :class:`Log` / :class:`Reader` -- the log stream: entries with positions, source positions and the
+  processed flag (LogAppendEntry.ofProcessed, LogEntryDescriptor skipProcessing).
+* :class:`StreamProcessor` -- ProcessingStateMachine.processCommand / batchProcessing /
+  collectBatchProcessingStepResult (stream-platform/.../stream/impl/ProcessingStateMachine.java:
+  247-417): one batch per unprocessed command read from the log, a FIFO of follow-up commands fed back
+  as UnwrittenRecords while pending + processed + new < maxCommandsInBatch, the rest written
+  unprocessed; the batch is appended to the log with sourceRecordPosition = the initial command's
+  position, then its post-commit tasks run (executeSideEffects, :546-590).
+* :class:`OracleEngine` -- the reference engine (oracle/zb_oracle.cpp process_one: Engine.process for
+  one command) as a RecordProcessor, with the partition's key generator (DbKeyGenerator) and the
+  RawDbWriter of a hand-off (import_rows).
+* :class:`Client` -- the EngineRule test clients writing commands to the log.
+
+Only tests use this module (it loads the oracle)."""
+import numpy as np
+
+from oracle.oracle import Oracle
+from zeebe_amd import abi
+from zeebe_amd.adapter import (JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED, VT_JOB_BATCH, RecordValues, doc_entries,
+                               typed_value)
+from zeebe_amd.engine import ProcessDefinition
+
+
+class Rec:
+    """A logged record (LoggedEvent + TypedRecord); position None = UnwrittenRecord."""
+    __slots__ = ("position", "source_position", "record_type", "value_type", "intent", "key", "rejection_type",
+                 "rejection_reason", "value", "processed", "timestamp")
+
+    def __init__(self, record_type, value_type, intent, key, value, rejection_type=abi.REJ_NONE, rejection_reason="",
+                 position=None, source_position=-1, processed=False, timestamp=0):
+        self.record_type, self.value_type, self.intent, self.key = record_type, value_type, intent, key
+        self.value, self.rejection_type, self.rejection_reason = value, rejection_type, rejection_reason
+        self.position, self.source_position, self.processed, self.timestamp = position, source_position, processed, timestamp
+
+    def canonical(self):
+        return (self.position, self.source_position, self.record_type, self.value_type, self.intent, self.key,
+                self.rejection_type, self.rejection_reason, self.processed, _canon(self.value))
+
+    def __repr__(self):
+        return "Rec(%s)" % (self.canonical(),)
+
+
+def _canon(v):
+    if isinstance(v, dict):
+        return tuple(sorted((k, _canon(x)) for k, x in v.items()))
+    if isinstance(v, (list, tuple)):
+        return tuple(_canon(x) for x in v)
+    return v
+
+
+class Log:
+    def __init__(self):
+        self.entries = []
+
+    def append(self, recs, source_position=-1):
+        for r in recs:
+            r.position = len(self.entries) + 1
+            r.source_position = source_position
+            self.entries.append(r)
+
+    def reader(self):
+        return Reader(self)
+
+    def canonical(self):
+        return [r.canonical() for r in self.entries]
+
+
+class Reader:
+    def __init__(self, log):
+        self.log = log
+        self.i = 0
+
+    def seek(self, position):
+        self.i = position - 1
+
+    def has_next(self):
+        return self.i < len(self.log.entries)
+
+    def next(self):
+        r = self.log.entries[self.i]
+        self.i += 1
+        return r
+
+
+class Builder:
+    """BufferedProcessingResultBuilder (+ the ProcessingResult it builds)."""
+
+    def __init__(self):
+        self.entries = []
+        self.post_commit = []
+
+    def append_record(self, key, record_type, value_type, intent, rejection_type, rejection_reason, value):
+        self.entries.append(Rec(record_type, value_type, intent, key, value, rejection_type, rejection_reason))
+
+    def append_post_commit_task(self, task):
+        self.post_commit.append(task)
+
+    def build(self):
+        return self
+
+
+class StreamProcessor:
+    """ProcessingStateMachine (stream-platform/.../stream/impl/ProcessingStateMachine.java:247-417)."""
+
+    def __init__(self, log, processors, max_commands_in_batch=100):
+        self.log = log
+        self.processors = processors
+        self.limit = max_commands_in_batch
+        self.read = 0
+        self.batches = 0
+
+    def run(self):
+        """Processes the log to its end (readNextRecord -> processCommand, :199-310)."""
+        while self.read < len(self.log.entries):
+            rec = self.log.entries[self.read]
+            self.read += 1
+            if rec.record_type == abi.RT_COMMAND and not rec.processed:
+                self._process_command(rec)
+
+    def _process_command(self, initial):
+        builder = Builder()
+        pending, writes = [initial], []
+        processed = last_size = 0
+        while pending and processed < self.limit:
+            command = pending.pop(0)
+            proc = next((p for p in self.processors if p.accepts(command.value_type)), None)
+            if proc is not None:
+                result = proc.process(command, builder)
+                # collectBatchProcessingStepResult (:388-417)
+                to_process = []
+                current = len(pending) + processed + 1
+                for e in result.entries[last_size:]:
+                    w = Rec(e.record_type, e.value_type, e.intent, e.key, e.value, e.rejection_type, e.rejection_reason)
+                    if e.record_type == abi.RT_COMMAND and current + len(to_process) < self.limit:
+                        to_process.append(Rec(e.record_type, e.value_type, e.intent, e.key, e.value))
+                        w.processed = True  # LogAppendEntry.ofProcessed
+                    writes.append(w)
+                pending.extend(to_process)
+                last_size = len(result.entries)
+            processed += 1
+        self.log.append(writes, initial.position)
+        self.batches += 1
+        for task in builder.post_commit:  # executeSideEffects: post-commit tasks after the write
+            task()
+
+
+def oracle_tables(o):
+    """The oracle's deployments as ProcessDefinitions (the adapter's RecordValues input)."""
+    out = []
+    for i, t in enumerate(o.process_tables()):
+        els = t["elements"]
+        out.append(ProcessDefinition(i, t["bpmn_process_id"], [e[2] for e in els], [abi.ELEMENT_TYPES[e[0]] for e in els],
+                                     [e[3] or None for e in els], [abi.EVENT_TYPES[e[1]] for e in els],
+                                     [e[4] for e in els], t["version"], t["key"]))
+    return out
+
+
+class OracleEngine:
+    """The reference engine as a RecordProcessor (Engine.java:71-131), one command per process call;
+    also the partition's DbKeyGenerator (KeyGeneratorControls) and the RawDbWriter of a hand-off."""
+
+    ACCEPTS = (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, abi.VT_PROCESS_INSTANCE, VT_JOB_BATCH)
+
+    def __init__(self, partition_id=1, max_commands_in_batch=100, clock=0):
+        self.o = Oracle(partition_id=partition_id, max_commands_in_batch=max_commands_in_batch)
+        self.o.set_clock(clock)
+        self.pbits = partition_id << 51
+        self.slot_of = {}
+        self.next_slot = 0
+        self.doc_values = []  # client value of every document entry the oracle holds (its doc indices)
+        self.values = None
+        self.tables = []
+
+    def deploy(self, xml, key, version=1):
+        idx = self.o.deploy(xml, key, version)
+        self.tables = oracle_tables(self.o)
+        self.values = RecordValues(self.tables, self.o.name)
+        return idx
+
+    def set_clock(self, now):
+        self.o.set_clock(now)
+
+    # KeyGeneratorControls
+    def current_key(self):
+        return self.pbits + self.o.key_counter()
+
+    def set_key_if_higher(self, key):
+        if key - self.pbits > self.o.key_counter():
+            self.o.set_key_counter(key - self.pbits)
+
+    # RawDbWriter
+    def upsert(self, rows):
+        self.o.import_rows(rows)
+
+    def state(self):
+        return self.o.state()
+
+    def accepts(self, vt):
+        return vt in self.ACCEPTS
+
+    def replay(self, record):
+        pass
+
+    def _proc_index(self, v):
+        pdk = v.get("processDefinitionKey", -1)
+        best = -1
+        for i, p in enumerate(self.tables):
+            if pdk is not None and pdk > 0:
+                if p.definition_key == pdk:
+                    return i
+            elif p.bpmn_process_id == v.get("bpmnProcessId") and (best < 0 or p.version > self.tables[best].version):
+                best = i
+        return best
+
+    def process(self, record, out):
+        vt, it, v = record.value_type, record.intent, record.value
+        if vt == VT_JOB_BATCH:
+            return self._activate(record, out)
+        r = np.zeros(1, dtype=abi.RECORD_DTYPE)[0]
+        r["record_type"], r["value_type"], r["intent"], r["key"] = abi.RT_COMMAND, vt, it, record.key
+        r["process_idx"] = r["element_idx"] = -1
+        r["scope_key"] = r["process_instance_key"] = r["aux"] = r["message_key"] = -1
+        r["correlation_key"], r["message_name"], r["bpmn_process_id"] = abi.NO_STRING, 0xFFFF, 0xFFFF
+        r["rejection_type"] = abi.REJ_NONE
+        slot = 0xFFFFFF
+        variables = tuple(v.get("variables", ())) if isinstance(v, dict) else ()
+        if vt == abi.VT_PROCESS_INSTANCE_CREATION:
+            r["process_idx"] = self._proc_index(v)
+            slot = self.next_slot
+            self.next_slot += 1
+        elif vt == abi.VT_TIMER:
+            r["aux"] = v["dueDate"]
+        elif vt == abi.VT_PROCESS_INSTANCE:
+            p = self._proc_index(v)
+            r["process_idx"] = p
+            r["element_idx"] = self.tables[p].element_ids.index(v["elementId"])
+            r["scope_key"], r["process_instance_key"] = v["flowScopeKey"], v["processInstanceKey"]
+            slot = self.slot_of.setdefault(v["processInstanceKey"], 0xFFFFF0 - len(self.slot_of))
+        docs = doc_entries(variables, self.o.intern, self.o.intern_string)
+        base = len(self.doc_values)
+        self.doc_values.extend(val for _, val in variables)
+        self.o.clear_records()
+        self.o.process_one(r, slot, docs, record.position or 0, len(out.entries))
+        recs = self.o.records()
+        for k, x in enumerate(recs):
+            rt, xvt, xit = int(x["record_type"]), int(x["value_type"]), int(x["intent"])
+            if rt == abi.RT_REJECTION and k == 0 and xvt == vt and xit == it:
+                value = dict(v)  # TypedRejectionWriter: the command's value
+            else:
+                value = self.values.value(x, variables, lambda aux: self.doc_values[aux])
+            if xvt == abi.VT_PROCESS_INSTANCE_CREATION:
+                self.slot_of[int(x["scope_key"])] = slot
+            out.append_record(int(x["key"]), rt, xvt, xit, int(x["rejection_type"]),
+                              self.o.reason(k) if rt == abi.RT_REJECTION else "", value)
+        return out.build()
+
+    def _activate(self, record, out):
+        v = record.value
+        key, jobs, reason = self.o.activate_jobs(v["type"], v["worker"], v["timeout"], v["maxJobsToActivate"],
+                                                 v.get("timestamp", 0))
+        if key < 0:
+            out.append_record(record.key, abi.RT_REJECTION, VT_JOB_BATCH, JOB_BATCH_ACTIVATE,
+                              abi.REJ_INVALID_ARGUMENT, "reason %d" % reason, dict(v))
+            return out.build()
+        strings = self.o.strings()
+        out.append_record(key, abi.RT_EVENT, VT_JOB_BATCH, JOB_BATCH_ACTIVATED, abi.REJ_NONE, "",
+                          self.values.job_batch(v, key, jobs, self.o.name, lambda i: strings[i].decode()))
+        return out.build()
+
+
+class Client:
+    """EngineRule's test clients (util/client/*Client.java): commands written to the log."""
+
+    def __init__(self, *logs):
+        self.logs = logs
+
+    def write(self, *recs):
+        for log in self.logs:
+            log.append([Rec(r.record_type, r.value_type, r.intent, r.key, r.value) for r in recs])
+
+    @staticmethod
+    def create(bpmn_process_id, variables=(), key=-1):
+        return Rec(abi.RT_COMMAND, abi.VT_PROCESS_INSTANCE_CREATION, 0, -1,
+                   {"bpmnProcessId": bpmn_process_id, "processDefinitionKey": key, "version": -1,
+                    "variables": tuple(variables), "tenantId": "<default>"})
+
+    @staticmethod
+    def complete_job(key, variables=()):
+        return Rec(abi.RT_COMMAND, abi.VT_JOB, abi.JOB_COMPLETE, key, {"variables": tuple(variables),
+                                                                       "tenantId": "<default>"})
+
+    @staticmethod
+    def trigger_timer(created):
+        """DueDateTimerChecker's TIMER:TRIGGER: the timer's TimerRecord (DueDateTimerChecker.java:118-125)."""
+        return Rec(abi.RT_COMMAND, abi.VT_TIMER, abi.TIMER_TRIGGER, created.key, dict(created.value))
+
+    @staticmethod
+    def activate_jobs(job_type, worker="w", timeout=300000, max_jobs=10, timestamp=0):
+        return Rec(abi.RT_COMMAND, VT_JOB_BATCH, JOB_BATCH_ACTIVATE, -1,
+                   {"type": job_type, "worker": worker, "timeout": timeout, "maxJobsToActivate": max_jobs,
+                    "timestamp": timestamp})
+
+
+def open_jobs(log):
+    """Job keys created and not completed / canceled so far (RecordingExporter over the log)."""
+    alive = {}
+    for r in log.entries:
+        if r.value_type == abi.VT_JOB and r.record_type == abi.RT_EVENT:
+            if r.intent == abi.JOB_CREATED:
+                alive[r.key] = r
+            elif r.intent in (abi.JOB_COMPLETED, abi.JOB_CANCELED):
+                alive.pop(r.key, None)
+    return alive
+
+
+def open_timers(log):
+    alive = {}
+    for r in log.entries:
+        if r.value_type == abi.VT_TIMER and r.record_type == abi.RT_EVENT:
+            if r.intent == abi.TIMER_CREATED:
+                alive[r.key] = r
+            elif r.intent in (abi.TIMER_TRIGGERED, abi.TIMER_CANCELED):
+                alive.pop(r.key, None)
+    return alive

@@ -74,6 +74,7 @@ CMD_JOB_COMPLETE = 2
 CMD_PUBLISH = 3
 CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE = 4, 5, 6, 7
 CMD_TIMER_TRIGGER = 8  # ref = timer key ordinal, doc_begin | pad << 32 = the timer's dueDate
+CMD_CONTINUE = 9  # a deferred continuation read back from the log: doc_begin | pad << 32 = its id
 XPART_KINDS = (CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE)
 DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR = 0, 1, 2, 3, 4, 5
 NO_STRING = 0xFFFFFFFF
@@ -120,6 +121,7 @@ class LogWindow(C.Structure):  # zbhip_log_window
 
 
 OPEN_TRUSTED_DEVICE_WINDOWS = 1
+OPEN_DEFER_CONTINUATIONS = 2
 
 
 class JobActivation(C.Structure):  # zbhip_job_activation (JOB_BATCH:ACTIVATE)

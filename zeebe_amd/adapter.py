@@ -1,0 +1,512 @@
+"""Python mirror of the reference-side host adapter (adapter/src/main/java/io/camunda/zeebe/zbhip/
+GpuBatchProcessor.java + Window.java), line for line in behaviour: a stream-platform
+``RecordProcessor`` (stream-platform/.../stream/api/RecordProcessor.java:17-108) placed before the
+engine (StreamProcessorTransitionStep.java:135-147: ``List.of(gpu, engine, checkpointProcessor)``) that
+answers the hot-path commands from libzbhip.so and hands everything else to the engine.  It behaves
+inside ``ProcessingStateMachine.batchProcessing`` / ``collectBatchProcessingStepResult``
+(stream-platform/.../stream/impl/ProcessingStateMachine.java:328-417) as the engine would:
+
+* A device batch is emitted whole when the platform processes its initial command.  The follow-up
+  commands the platform then feeds back (``UnwrittenRecord``) were already processed on the device,
+  so they return the builder unchanged -- ``out.build()``, not an empty result: the platform skips
+  the builder's entries it has seen by their count (``lastProcessingResultSize``).
+* Follow-ups the platform writes to the log unprocessed (past ``maxCommandsInBatch``) are device
+  continuations (``ZBHIP_OPEN_DEFER_CONTINUATIONS``): they run when the platform reads them back,
+  at their own log position (``ZBHIP_CMD_CONTINUE``), after whatever the log holds before them.
+* The partition has one key generator (``DbKeyGenerator``): after every device command the engine's
+  generator is moved past the device's keys (``KeyGeneratorControls.setKeyIfHigher``), before every
+  window the device's past the engine's (``zbhip_set_key_if_higher``).
+* A command the device falls back on hands its instance to the engine (zb-db rows through the
+  platform's transaction, then evicted) and the engine's keys are declared once its batch is done.
+* ``JOB_BATCH:ACTIVATE`` of a job type only device instances hold goes to ``zbhip_activate_jobs``
+  (JobBatchActivateProcessor.java:60-143).
+* After recovery, instances of device processes move from the engine's state into HBM
+  (``on_recovered`` -> ``zbhip_import_state``), as StreamProcessorLifecycleAware.onRecovered would.
+
+Record values are dicts keyed by the reference's property names (ProcessInstanceRecord.java:61-72,
+JobRecord, VariableRecord, ProcessEventRecord, TimerRecord, ProcessInstanceCreationRecord,
+JobBatchRecord); variable documents are tuples of (name, value) in document order.
+
+Platform objects used (duck-typed like the Java interfaces):
+  record  -- TypedRecord: record_type, value_type, intent, key, value, position (None for an
+             UnwrittenRecord), timestamp
+  out     -- ProcessingResultBuilder: append_record(key, record_type, value_type, intent,
+             rejection_type, rejection_reason, value); build()
+  reader  -- LogStreamReader: seek(position), has_next(), next() (records with .processed)
+  engine  -- the engine's RecordProcessor (accepts / process / replay / on_processing_error)
+  zeebe_db-- RawDbWriter: upsert(rows) of a hand-off (the zb-db rows of the instance)
+  key_generator -- DbKeyGenerator: current_key(), set_key_if_higher(key)
+"""
+from . import abi
+from .engine import Partition
+
+VT_JOB_BATCH = 1
+JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED = 0, 1
+PI_COMMAND_INTENTS = (8, 9, 10)  # ACTIVATE_ELEMENT, COMPLETE_ELEMENT, TERMINATE_ELEMENT
+TENANT = "<default>"  # TenantOwned.DEFAULT_TENANT_IDENTIFIER
+
+
+def doc_entries(variables, intern_name, intern_string):
+    """A client's variable document [(name, value)] as zbhip_doc_entry rows, or None when a value is
+    outside the device subset (Window.decodeDocument: arrays, maps, inexact decimals)."""
+    d = abi.make_docs(len(variables))
+    for j, (name, v) in enumerate(variables):
+        d[j]["name_id"] = intern_name(name)
+        if v is None:
+            d[j]["type"] = abi.DOC_NIL
+        elif isinstance(v, bool):
+            d[j]["type"], d[j]["value"] = abi.DOC_BOOL, int(v)
+        elif isinstance(v, int):
+            d[j]["type"], d[j]["value"] = abi.DOC_INT, v
+        elif isinstance(v, float):
+            scaled = round(v * 10 ** abi.DEC_SCALE)
+            if scaled / 10 ** abi.DEC_SCALE != v:
+                return None
+            d[j]["type"], d[j]["value"] = abi.DOC_DEC, scaled
+        elif isinstance(v, str):
+            d[j]["type"], d[j]["value"] = abi.DOC_STR, intern_string(v)
+        else:
+            return None
+    return d
+
+
+def typed_value(t, v, string_value):
+    """A stored variable (zbhip_doc_type, value) as the client's value."""
+    return (None if t == abi.DOC_NIL else bool(v) if t == abi.DOC_BOOL else int(v) if t == abi.DOC_INT
+            else int(v) / 10 ** abi.DEC_SCALE if t == abi.DOC_DEC else string_value(int(v)) if t == abi.DOC_STR
+            else ("other", int(v)))
+
+
+class RecordValues:
+    """zbhip_record rows -> the reference's record values (Window.value).  `procs` are the
+    deployment's ProcessDefinitions (by process index), `name` the variable-name dictionary."""
+
+    def __init__(self, procs, name):
+        self.procs = procs
+        self.name = name
+
+    def value(self, r, command_doc=(), entry_value=None):
+        vt = int(r["value_type"])
+        p = self.procs[max(int(r["process_idx"]), 0)] if self.procs else None
+        elem = int(r["element_idx"])
+        scope, pik, aux = int(r["scope_key"]), int(r["process_instance_key"]), int(r["aux"])
+        if vt == abi.VT_PROCESS_INSTANCE:
+            return {"bpmnElementType": p.element_types[elem], "elementId": p.element_ids[elem],
+                    "bpmnProcessId": p.bpmn_process_id, "version": p.version,
+                    "processDefinitionKey": p.definition_key, "processInstanceKey": pik, "flowScopeKey": scope,
+                    "bpmnEventType": p.event_types[elem], "parentProcessInstanceKey": -1,
+                    "parentElementInstanceKey": -1, "tenantId": TENANT}
+        if vt == abi.VT_JOB:
+            v = {"tenantId": TENANT, "variables": tuple(command_doc) if aux >= 0 else ()}
+            if elem >= 0:
+                v.update({"type": p.job_types[elem], "retries": p.retries[elem], "elementId": p.element_ids[elem],
+                          "elementInstanceKey": scope, "processInstanceKey": pik, "bpmnProcessId": p.bpmn_process_id,
+                          "processDefinitionVersion": p.version, "processDefinitionKey": p.definition_key})
+            return v
+        if vt == abi.VT_VARIABLE:
+            return {"name": self.name(elem), "value": entry_value(aux), "scopeKey": scope, "processInstanceKey": pik,
+                    "processDefinitionKey": p.definition_key, "bpmnProcessId": p.bpmn_process_id, "tenantId": TENANT}
+        if vt == abi.VT_PROCESS_EVENT:
+            return {"scopeKey": scope, "targetElementId": p.element_ids[elem],
+                    "variables": tuple(command_doc) if int(r["intent"]) == abi.PE_TRIGGERING else (),
+                    "processDefinitionKey": p.definition_key, "processInstanceKey": pik, "tenantId": TENANT}
+        if vt == abi.VT_TIMER:
+            return {"elementInstanceKey": scope, "processInstanceKey": pik, "dueDate": aux,
+                    "repetitions": int(r["partition"]), "targetElementId": p.element_ids[elem] if elem >= 0 else "",
+                    "processDefinitionKey": p.definition_key if elem >= 0 else -1, "tenantId": TENANT}
+        if vt == abi.VT_PROCESS_INSTANCE_CREATION:
+            return {"bpmnProcessId": p.bpmn_process_id, "processDefinitionKey": p.definition_key,
+                    "version": p.version, "processInstanceKey": scope, "variables": tuple(command_doc),
+                    "tenantId": TENANT}
+        raise ValueError("value type outside the adapter's subset: %d" % vt)
+
+    def job_batch(self, command, key, jobs, name, string_value):
+        """JobBatchRecord of an accepted JOB_BATCH:ACTIVATE (JobBatchActivateProcessor.java:120-143)."""
+        v = dict(command)
+        out = []
+        for j in jobs:
+            p = self.procs[int(j["process_idx"])]
+            e = int(j["element_idx"])
+            out.append({"type": command["type"], "worker": command["worker"], "deadline": int(j["deadline"]),
+                        "retries": int(j["retries"]), "elementId": p.element_ids[e],
+                        "elementInstanceKey": int(j["element_instance_key"]),
+                        "processInstanceKey": int(j["process_instance_key"]), "bpmnProcessId": p.bpmn_process_id,
+                        "processDefinitionKey": p.definition_key, "processDefinitionVersion": p.version,
+                        "variables": tuple((name(int(x["name_id"])), typed_value(int(x["type"]), x["value"], string_value))
+                                           for x in j["variables"][:int(j["n_variables"])]),
+                        "tenantId": TENANT})
+        v.update({"jobKeys": tuple(int(j["key"]) for j in jobs), "jobs": tuple(out), "truncated": False})
+        return v
+
+
+class Window:
+    """One read-ahead window (Window.java): the zbhip_command rows and documents of consecutive
+    hot-path commands and their log positions."""
+
+    def __init__(self):
+        self.cmds = []       # zbhip_command rows (dicts)
+        self.docs = []       # zbhip_doc_entry rows
+        self.doc_values = []  # the client value of each entry (VARIABLE records)
+        self.positions = []
+        self.instances = []
+        self.doc_base = 0    # zbhip doc index of this window's first entry
+
+    def reset(self, doc_base):
+        self.__init__()
+        self.doc_base = doc_base
+
+    def size(self):
+        return len(self.cmds)
+
+    def covers(self, position):
+        return bool(self.positions) and self.positions[0] <= position <= self.positions[-1]
+
+    def index_of(self, position):
+        try:
+            return self.positions.index(position)
+        except ValueError:
+            return -1
+
+    def put(self, record, instance, kind, ref, docs=None, values=(), doc_begin=None, pad=0):
+        c = {"instance": instance, "kind": kind, "ref": ref, "doc_count": 0, "doc_begin": 0, "pad": pad}
+        if docs is not None and len(docs):
+            c["doc_count"], c["doc_begin"] = len(docs), len(self.docs)
+            self.docs.extend(docs)
+            self.doc_values.extend(values)
+        if doc_begin is not None:
+            c["doc_begin"] = doc_begin
+        self.cmds.append(c)
+        self.positions.append(record.position)
+        self.instances.append(instance)
+
+    def arrays(self):
+        cmds = abi.make_commands(len(self.cmds))
+        for i, c in enumerate(self.cmds):
+            for f, v in c.items():
+                cmds[i][f] = v
+        docs = abi.make_docs(len(self.docs))
+        for j, d in enumerate(self.docs):
+            docs[j] = d
+        return cmds, docs
+
+
+class GpuBatchProcessor:
+    """The adapter (GpuBatchProcessor.java).  `deployments`: [(bpmn xml, definition key, version)]
+    in deployment order; processes the device compiler refuses stay with the engine, as do
+    `engine_deployments` (processes the host keeps on the engine, e.g. deployed after start-up).
+    JOB_BATCH:ACTIVATE goes to the device only for job types no engine process declares: the
+    reference activates jobs of a type across all instances in key order, and the engine's
+    JOB_ACTIVATABLE rows are not visible here."""
+
+    WINDOW = 1 << 16
+
+    def __init__(self, engine, reader, deployments, zeebe_db, key_generator, partition_id=1, partition_count=1,
+                 device=0, instances=1 << 16, window=None, max_commands_in_batch=100, max_records_per_batch=256,
+                 clock=None, engine_deployments=()):
+        self.engine = engine
+        self.reader = reader
+        self.deployments = deployments
+        self.zeebe_db = zeebe_db
+        self.key_generator = key_generator
+        self.partition_id = partition_id
+        self.partition_count = partition_count
+        self.device = device
+        self.instances = instances
+        self.window_size = window or self.WINDOW
+        self.limit = max_commands_in_batch
+        self.max_records = max_records_per_batch
+        self.clock = clock or (lambda: 0)  # ActorClock.currentTimeMillis
+        self.part = None
+        self.by_key, self.latest_by_id, self.by_index = {}, {}, []
+        self.engine_job_types = set()  # job types the engine's processes (or handed-off instances) hold
+        from .bpmn import job_types_of
+        for xml, _, _ in engine_deployments:
+            self.engine_job_types.update(job_types_of(xml))
+        self.used_slots = set()
+        self.ended = set()             # ended instances whose slot waits for their continuations
+        self.next_free = 0
+        self.window = Window()
+        self.handed_off = set()
+        self.followups = 0             # follow-ups of the current device batch the platform feeds back
+        self.engine_batch = False      # the current batch's initial command went to the engine
+        self.pending_declaration = None  # (window index, key before) of a fallback command
+        self.continuations = []        # expected continuations, in log order: (id, slot, match key)
+        self.doc_total = 0             # document entries submitted so far (zbhip doc indices)
+        self.values = None
+        # what went where (tests read these)
+        self.counts = {"windows": 0, "device_commands": 0, "continuations": 0, "fallbacks": 0, "activations": 0,
+                       "engine_commands": 0, "followups_answered": 0}
+
+    # ---- RecordProcessor ----------------------------------------------------------------------
+    def init(self):
+        pbits = self.partition_id << 51
+        self.part = Partition(partition_id=self.partition_id, partition_count=self.partition_count,
+                              device=self.device, max_instances=self.instances, max_commands=self.window_size,
+                              max_records_per_batch=self.max_records, max_doc_entries=16 * self.window_size,
+                              max_commands_in_batch=self.limit,
+                              initial_key=self.key_generator.current_key() - pbits, defer_continuations=True)
+        for xml, key, version in self.deployments:
+            self.deploy(xml, key, version)
+        self.values = RecordValues(self.part.processes, self.part.name)
+
+    def deploy(self, xml, key, version):
+        from .native import ZbhipError
+        try:
+            idx = self.part.deploy(xml, key, version)
+        except ZbhipError:
+            # outside the device subset: its instances (and job types) run on the CPU engine
+            from .bpmn import job_types_of
+            self.engine_job_types.update(job_types_of(xml))
+            self.by_index.append(None)
+            return None
+        p = self.part.processes[idx]
+        self.by_key[key] = p
+        self.by_index.append(p)
+        prev = self.latest_by_id.get(p.bpmn_process_id)
+        if prev is None or prev.version < version:
+            self.latest_by_id[p.bpmn_process_id] = p
+        return p
+
+    def accepts(self, value_type):
+        return value_type in (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, VT_JOB_BATCH) \
+            or self.engine.accepts(value_type)
+
+    def replay(self, record):
+        # events only; the appliers write the engine's state.  Instances restored this way move
+        # into HBM after recovery (on_recovered)
+        self.engine.replay(record)
+
+    def on_recovered(self, entries, resume_position=None):
+        """StreamProcessorLifecycleAware.onRecovered: instances of device processes move from the
+        engine's state (its zb-db entries [(column family, key, value)], RocksDB after replay) into HBM
+        (zbhip_select_instances_db + zbhip_import_state_db).  Instances that a command still waiting in
+        the log addresses by its own record (a follow-up written unprocessed before the restart) stay
+        with the engine.  Returns the mask of the entries moved (the caller deletes them)."""
+        waiting = set()
+        if resume_position is not None:
+            self.reader.seek(resume_position)
+            while self.reader.has_next():
+                rec = self.reader.next()
+                if rec.record_type == abi.RT_COMMAND and not rec.processed and rec.value_type == abi.VT_PROCESS_INSTANCE:
+                    waiting.add(rec.value.get("processInstanceKey"))
+        take, n = self.part.select_instances_db(entries, sorted(waiting))
+        if n:
+            first = self.next_free
+            got = self.part.import_state_db([e for e, t in zip(entries, take) if t], first_slot=first)
+            self.used_slots.update(range(first, first + got))
+            self.next_free = first + got
+        self.part.set_key_if_higher(self.key_generator.current_key())
+        return take
+
+    def process(self, record, out):
+        if record.position is None:
+            # a follow-up command the platform feeds back within the current batch
+            if self.followups > 0:
+                self.followups -= 1
+                self.counts["followups_answered"] += 1
+                return out.build()  # already processed on the device, its records are in the builder
+            return self.engine.process(record, out)
+        self._batch_done()
+        self.followups = 0
+        self.engine_batch = False
+        if record.value_type == VT_JOB_BATCH and record.intent == JOB_BATCH_ACTIVATE \
+                and record.value["type"] not in self.engine_job_types:
+            return self._activate_jobs(record, out)
+        i = self.window.index_of(record.position) if self.window.covers(record.position) else -1
+        if i < 0:
+            if not self._hot(record, 0):
+                self.engine_batch = True
+                self.counts["engine_commands"] += 1
+                return self.engine.process(record, out)
+            self._fill_window(record)
+            i = self.window.index_of(record.position)
+        if i < 0:
+            self.engine_batch = True
+            return self.engine.process(record, out)
+        st, _ = self.part.command_status(i)
+        if st != 0:
+            self.counts["fallbacks"] += 1
+            return self._fall_back(i, record, out)
+        self.counts["device_commands"] += 1
+        self.counts["continuations"] += self.window.cmds[i]["kind"] == abi.CMD_CONTINUE
+        self._emit(i, record, out)
+        # DbKeyGenerator after this command: the device's keys so far (the engine's next command, a
+        # fallback in this window or whatever follows the window, continues after them)
+        self.key_generator.set_key_if_higher(self.part.key_before(i + 1))
+        return out.build()
+
+    def on_processing_error(self, error, record, out):
+        return self.engine.on_processing_error(error, record, out)
+
+    # ---- the window -----------------------------------------------------------------------------
+    def _create_target(self, v):
+        pdk = v.get("processDefinitionKey", -1)
+        return self.by_key.get(pdk) if pdk is not None and pdk > 0 else self.latest_by_id.get(v.get("bpmnProcessId"))
+
+    def _resolve(self, key):
+        from .native import ZbhipError
+        try:
+            return self.part.resolve_key(key)
+        except ZbhipError:
+            return None
+
+    def _continuation_match(self, record):
+        v = record.value
+        return (record.key, record.intent, v.get("elementId"), v.get("flowScopeKey"), v.get("processInstanceKey"))
+
+    def _hot(self, record, k):
+        """Would the device take this log command?  k: continuations already claimed by the read-ahead."""
+        if record.record_type != abi.RT_COMMAND:
+            return False
+        vt, it = record.value_type, record.intent
+        if vt == abi.VT_PROCESS_INSTANCE_CREATION:
+            return it == 0 and self._create_target(record.value) is not None
+        if vt == abi.VT_JOB and it == abi.JOB_COMPLETE or vt == abi.VT_TIMER and it == abi.TIMER_TRIGGER:
+            return self._resolve(record.key) is not None
+        if vt == abi.VT_PROCESS_INSTANCE and it in PI_COMMAND_INTENTS:
+            # a follow-up a device batch wrote unprocessed, read back in the order written
+            return k < len(self.continuations) and self.continuations[k][2] == self._continuation_match(record)
+        return False
+
+    def _fill_window(self, first):
+        """Reads consecutive hot-path commands from the log starting at `first` (GpuBatchProcessor
+        .fillWindow) and submits and runs them once."""
+        self._free_ended()
+        self.window.reset(self.doc_total)
+        self.reader.seek(first.position)
+        claimed = 0
+        while self.reader.has_next() and self.window.size() < self.window_size:
+            rec = self.reader.next()
+            if rec.record_type != abi.RT_COMMAND or rec.processed:
+                continue  # events and processed follow-ups of earlier batches between the commands
+            if not self._hot(rec, claimed):
+                break  # the engine's: the window ends before it (log order is kept)
+            vt = rec.value_type
+            if vt == abi.VT_PROCESS_INSTANCE_CREATION:
+                v = rec.value
+                docs = doc_entries(v.get("variables", ()), self.part.intern, self.part.intern_string)
+                if docs is None:
+                    break  # a document outside the subset: the engine takes this CREATE
+                slot = self._take_slot()
+                if slot is None:
+                    break
+                self.window.put(rec, slot, abi.CMD_CREATE, self._create_target(v).idx, docs,
+                                [val for _, val in v.get("variables", ())])
+            elif vt == abi.VT_JOB:
+                docs = doc_entries(rec.value.get("variables", ()), self.part.intern, self.part.intern_string)
+                if docs is None:
+                    break
+                inst, ordv = self._resolve(rec.key)
+                self.window.put(rec, inst, abi.CMD_JOB_COMPLETE, ordv, docs,
+                                [val for _, val in rec.value.get("variables", ())])
+            elif vt == abi.VT_TIMER:
+                inst, ordv = self._resolve(rec.key)
+                due = rec.value["dueDate"]
+                self.window.put(rec, inst, abi.CMD_TIMER_TRIGGER, ordv, doc_begin=due & 0xFFFFFFFF, pad=due >> 32)
+            else:
+                cid, slot, _ = self.continuations[claimed]
+                claimed += 1
+                self.window.put(rec, slot, abi.CMD_CONTINUE, 0, doc_begin=cid & 0xFFFFFFFF, pad=cid >> 32)
+        del self.continuations[:claimed]
+        # keys the engine generated since the last window come first (setKeyIfHigher)
+        self.part.set_key_if_higher(self.key_generator.current_key())
+        # the window's clock: TIMER:CREATED dueDates (CatchEventBehavior.java:310, ActorClock)
+        self.part.set_clock(self.clock())
+        cmds, docs = self.window.arrays()
+        self.counts["windows"] += 1
+        self.part.submit(cmds, docs)
+        self.doc_total += len(docs)
+        self.part.run()
+        # the records are drained command by command as the platform reaches them
+        # (zbhip_drain_command): a fallback command's CPU-engine keys come before the later ones
+
+    def _free_ended(self):
+        for s in list(self.ended):
+            if self.part.pending_continuations(s) == 0:
+                self.ended.discard(s)
+                self.used_slots.discard(s)
+
+    def _take_slot(self):
+        for _ in range(self.instances):
+            s = self.next_free % self.instances
+            self.next_free = s + 1
+            if s not in self.used_slots and s not in self.window.instances:
+                self.used_slots.add(s)
+                return s
+        return None
+
+    def _emit(self, i, record, out):
+        """Window command i's records into the builder as the reference's processors write them
+        (Window.emit).  A rejection of the command itself carries the command's value
+        (TypedRejectionWriter.appendRejection)."""
+        cmd_doc = tuple(record.value.get("variables", ())) if isinstance(record.value, dict) else ()
+        win = self.window
+        admitted = 0
+        for r in self.part.drain_command(i):
+            rt, vt, it = int(r["record_type"]), int(r["value_type"]), int(r["intent"])
+            if rt == abi.RT_REJECTION and int(r["ordinal"]) == 0 and vt == record.value_type and it == record.intent:
+                value = dict(record.value)
+            else:
+                value = self.values.value(r, cmd_doc, lambda aux: win.doc_values[aux - win.doc_base])
+            reason = self.part.reason(r) if rt == abi.RT_REJECTION else ""
+            out.append_record(int(r["key"]), rt, vt, it, int(r["rejection_type"]), reason, value)
+            if rt == abi.RT_COMMAND:
+                if r["unprocessed"]:
+                    # a continuation (its id in aux): expected back from the log in the order written
+                    self.continuations.append((int(r["aux"]), win.instances[i],
+                                               (int(r["key"]), it, value.get("elementId"), value.get("flowScopeKey"),
+                                                value.get("processInstanceKey"))))
+                else:
+                    admitted += 1
+            elif vt == abi.VT_PROCESS_INSTANCE and it == 5 and value.get("bpmnElementType") == "PROCESS":
+                self.ended.add(win.instances[i])  # its slot is free once its continuations ran
+        self.followups = admitted
+
+    # ---- keys ------------------------------------------------------------------------------------
+    def _batch_done(self):
+        """The previous batch ended: the keys a fallback command's engine batch generated are declared
+        (zbhip_set_external_keys) before the window's later commands fix theirs."""
+        if self.pending_declaration is not None:
+            i, before = self.pending_declaration
+            self.pending_declaration = None
+            self.part.set_external_keys(i, self.key_generator.current_key() - before)
+
+    # ---- fallback hand-off (Engine.java:134, ProcessingStateMachine.java:276-310) ----
+    def _fall_back(self, i, record, out):
+        inst = self.window.instances[i]
+        if inst not in self.handed_off:
+            # the instance's zb-db rows into the engine's state (the platform's transaction), then off
+            # the device with its waiting continuations (the engine reads them back from the log)
+            self.handed_off.add(inst)
+            rows = self.part.export_instances([inst])
+            # its jobs are the engine's now: activations of their types go there too
+            self.engine_job_types.update(r.split("|")[2].split(",")[0][len("type="):] for r in rows
+                                         if r.startswith("JOBS|"))
+            self.zeebe_db.upsert(rows)
+            self.part.evict_instances([inst])
+            self.continuations = [c for c in self.continuations if c[1] != inst]
+            self.used_slots.discard(inst)
+            self.ended.discard(inst)
+        before = self.part.key_before(i)
+        self.key_generator.set_key_if_higher(before)
+        self.engine_batch = True
+        self.pending_declaration = (i, before)
+        # the engine's keys are declared when its batch (follow-ups included) is done
+        out.append_post_commit_task(self._batch_done)
+        return self.engine.process(record, out)
+
+    # ---- job activation (JobBatchActivateProcessor.java:60-143) ------------------------------------
+    def _activate_jobs(self, record, out):
+        v = record.value
+        self.part.set_key_if_higher(self.key_generator.current_key())
+        self.counts["activations"] += 1
+        key, jobs, reason = self.part.activate_jobs(v["type"], v["worker"], v["timeout"], v["maxJobsToActivate"],
+                                                    v.get("timestamp", 0))
+        if key < 0:
+            out.append_record(record.key, abi.RT_REJECTION, VT_JOB_BATCH, JOB_BATCH_ACTIVATE,
+                              abi.REJ_INVALID_ARGUMENT, "reason %d" % reason, dict(v))
+            return out.build()
+        self.key_generator.set_key_if_higher(key)
+        out.append_record(key, abi.RT_EVENT, VT_JOB_BATCH, JOB_BATCH_ACTIVATED, abi.REJ_NONE, "",
+                          self.values.job_batch(v, key, jobs, self.part.name, self.part.string_value))
+        return out.build()

@@ -345,3 +345,11 @@ def message_catch_process(process_id="process", message_name="msg", correlation_
     (MessageCorrelationMultiplePartitionsTest.java:43-49 shape)."""
     return (createExecutableProcess(process_id).startEvent("start").intermediateCatchEvent(catch_id)
             .message(message_name, correlation_key).endEvent("end").done())
+
+
+def job_types_of(xml):
+    """Static job types (zeebe:taskDefinition type) a BPMN XML declares."""
+    import re
+    if isinstance(xml, bytes):
+        xml = xml.decode()
+    return set(m for m in re.findall(r'taskDefinition[^>]*?\stype="([^"=][^"]*)"', xml))

@@ -20,6 +20,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "zb_internal.h"
@@ -240,10 +241,21 @@ struct zbhip_handle {
   uint32_t max_pending = 0;            // deploy-time bound of pending follow-ups in one batch
   uint4* d_ovf = nullptr;
   uint32_t* d_ovf_count = nullptr;
+  uint32_t ovf_cap = 0;                // overflow entries per run (a batch past it falls back: FB_BATCH_LIMIT)
   zbhip_command* d_cont = nullptr;     // continuation commands (window indices n ..)
   uint32_t* d_cont_order = nullptr;
   std::vector<zbhip_command> cont_cmds;
   std::vector<uint32_t> cont_order;
+  // ZBHIP_OPEN_DEFER_CONTINUATIONS: a follow-up written unprocessed is not run after the window; it
+  // waits here (id -> its CMD_FOLLOWUP command) until the log reader submits it (ZBHIP_CMD_CONTINUE)
+  // at its own log position.  Ids follow the drain order of the unprocessed records.
+  std::unordered_map<uint64_t, zbhip_command> deferred;
+  std::unordered_map<uint32_t, uint32_t> deferred_per_inst;  // pending continuations per instance slot
+  uint64_t next_cont_id = 1;
+  uint64_t last_cont_first = 0, last_cont_n = 0;             // ids the last run deferred
+  std::unordered_map<uint64_t, uint64_t> cont_ids;           // (window command << 16 | record ordinal) -> id
+  bool window_continues = false;                             // the window runs deferred continuations
+  bool defer() const { return cfg.flags & ZBHIP_OPEN_DEFER_CONTINUATIONS; }
   uint32_t* d_qspill = nullptr;        // batch FIFO entries beyond the LDS ring (kernels.hip enqueue)
   size_t qspill_words = 0;
   uint32_t qspill_cap = 0;
@@ -484,7 +496,8 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
        dalloc(&h->d_key_counter, 1) == hipSuccess && dalloc(&h->d_key_base, cfg->max_commands) == hipSuccess &&
        dalloc(&h->d_key_blk, (cfg->max_commands + 1023) / 1024 + 1) == hipSuccess && dalloc(&h->d_xcount, 1024) == hipSuccess &&
        dalloc(&h->d_seen, N + S) == hipSuccess && dalloc(&h->d_check_flag, 1) == hipSuccess &&
-       dalloc(&h->d_ovf, cfg->max_commands) == hipSuccess && dalloc(&h->d_ovf_count, 1) == hipSuccess &&
+       dalloc(&h->d_ovf, h->ovf_cap = std::max<uint32_t>(4096u, 4u * cfg->max_commands)) == hipSuccess &&
+       dalloc(&h->d_ovf_count, 1) == hipSuccess &&
        dalloc(&h->d_cont, cfg->max_commands) == hipSuccess && dalloc(&h->d_cont_order, cfg->max_commands) == hipSuccess;
   if (S) {
     ok = ok && dalloc(&h->d_xout, (size_t)cfg->max_commands * kOut) == hipSuccess &&
@@ -1028,10 +1041,18 @@ static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t
     if (c.instance >= h->cfg.max_instances) return ZBHIP_EINVAL;
     if (c.kind == ZBHIP_CMD_CREATE) {
       if (c.ref >= h->procs.size()) return ZBHIP_EINVAL;
+      // the slot's instance still has follow-ups waiting in the log: it is not free yet
+      if (!h->deferred_per_inst.empty() && h->deferred_per_inst.count(c.instance)) return ZBHIP_EINVAL;
     } else if (c.kind == ZBHIP_CMD_JOB_COMPLETE) {
       if (c.ref >= 0xFFF0) return ZBHIP_EINVAL;
     } else if (c.kind == ZBHIP_CMD_TIMER_TRIGGER) {
       if (c.ref >= 0xFFF0 || c.doc_count) return ZBHIP_EINVAL;  // doc_begin | pad << 32 = dueDate
+      continue;
+    } else if (c.kind == ZBHIP_CMD_CONTINUE) {
+      // a deferred continuation read back from the log: known id, its own instance, no document
+      if (!h->defer() || c.doc_count) return ZBHIP_EINVAL;
+      auto it = h->deferred.find((uint64_t)c.doc_begin | ((uint64_t)c.pad << 32));
+      if (it == h->deferred.end() || it->second.instance != c.instance) return ZBHIP_EINVAL;
       continue;
     } else {
       return ZBHIP_EINVAL;
@@ -1080,6 +1101,14 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   if (rc) return rc;
   h->external = false;
   h->h_cmds.assign(cmds, cmds + n);
+  bool continues = false;
+  for (const auto& c : h->h_cmds) continues |= c.kind == ZBHIP_CMD_CONTINUE;
+  if (continues) {
+    // duplicates of one id in a window are refused before anything is consumed
+    std::unordered_map<uint64_t, int> seen;
+    for (const auto& c : h->h_cmds)
+      if (c.kind == ZBHIP_CMD_CONTINUE && seen[(uint64_t)c.doc_begin | ((uint64_t)c.pad << 32)]++) return ZBHIP_EINVAL;
+  }
   h->h_docs.assign(docs, docs + n_docs);
   h->h_xparts.assign(xparts, xparts + n_xparts);
   h->n_xparts = n_xparts;
@@ -1099,6 +1128,21 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   h->next_doc_base += (int64_t)n_docs;
   h->source_base = h->next_source;
   h->next_source += (int64_t)n;
+  if (continues) {
+    // each continuation becomes the CMD_FOLLOWUP batch it was deferred as (the kernel runs it
+    // against the instance's state at this log position, as the reference does when it reads the
+    // command back)
+    for (auto& c : h->h_cmds) {
+      if (c.kind != ZBHIP_CMD_CONTINUE) continue;
+      auto it = h->deferred.find((uint64_t)c.doc_begin | ((uint64_t)c.pad << 32));
+      c = it->second;
+      h->deferred.erase(it);
+      auto pi = h->deferred_per_inst.find(c.instance);
+      if (pi != h->deferred_per_inst.end() && --pi->second == 0) h->deferred_per_inst.erase(pi);
+    }
+    cmds = h->h_cmds.data();
+  }
+  h->window_continues = continues;
   if (n) HIPCHK(hipMemcpyAsync(h->d_cmds, cmds, n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
   if (n_docs)
     HIPCHK(hipMemcpyAsync(h->d_docs, docs, n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice, h->stream));
@@ -1159,6 +1203,7 @@ int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_
   const int rc = check_device_window(h, dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, &replanned);
   if (rc || replanned) return rc;
   h->external = true;
+  h->window_continues = false;  // (ZBHIP_CMD_CONTINUE is a host-window command)
   h->ext_xparts = dev_xparts;
   h->n_xparts = n_xparts;
   h->h_xparts.clear();
@@ -1502,7 +1547,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (overflow) {
     P.ovf = h->d_ovf;
     P.ovf_count = h->d_ovf_count;
-    P.ovf_cap = h->cfg.max_commands;
+    P.ovf_cap = h->ovf_cap;
   }
   if (h->max_pending > step_queue(h->variant) && h->variant != 3 && !getenv("ZBHIP_CHUNKS_PER_WG")) {
     const uint32_t cap = h->max_pending;
@@ -1537,13 +1582,48 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   uint32_t n_all = n;
   h->cont_cmds.clear();
   h->cont_order.clear();
+  h->last_cont_first = h->next_cont_id;
+  h->last_cont_n = 0;
+  h->cont_ids.clear();
   std::vector<uint2> hdr_tmp;
-  while (overflow) {
+  if (overflow && h->defer()) {
+    // deferred: the follow-ups written unprocessed wait for their own log positions
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpyAsync(&cnt, h->d_ovf_count, sizeof cnt, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    // entries past the list's capacity were not written: their batches fell back (FB_BATCH_LIMIT)
+    cnt = std::min(cnt, h->ovf_cap);
+    if (cnt) {
+      std::vector<uint4> ov(cnt);
+      HIPCHK(hipMemcpy(ov.data(), h->d_ovf, cnt * sizeof(uint4), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemsetAsync(h->d_ovf_count, 0, sizeof(uint32_t), h->stream));
+      hdr_tmp.resize(n);
+      HIPCHK(hipMemcpy(hdr_tmp.data(), h->d_cmd_hdr, n * sizeof(uint2), hipMemcpyDeviceToHost));
+      ov.erase(std::remove_if(ov.begin(), ov.end(), [&](const uint4& e) {
+                 return e.x >= n || ((hdr_tmp[e.x].y >> 16) & 0xFF) != ST_OK;
+               }), ov.end());
+      std::sort(ov.begin(), ov.end(), [](const uint4& a, const uint4& b) {
+        return a.x != b.x ? a.x < b.x : (a.z & 0xFFFF) < (b.z & 0xFFFF);
+      });
+      for (const uint4& e : ov) {
+        zbhip_command c{};
+        c.instance = e.w;
+        c.kind = CMD_FOLLOWUP;
+        c.ref = (uint16_t)(e.z >> 16);
+        c.doc_begin = e.y;
+        h->cont_ids.emplace(((uint64_t)e.x << 16) | (e.z & 0xFFFF), h->next_cont_id);
+        h->deferred.emplace(h->next_cont_id++, c);
+        ++h->deferred_per_inst[c.instance];
+      }
+      h->last_cont_n = ov.size();
+    }
+  }
+  while (overflow && !h->defer()) {
     uint32_t cnt = 0;
     HIPCHK(hipMemcpyAsync(&cnt, h->d_ovf_count, sizeof cnt, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     if (cnt == 0) break;
-    if (cnt > h->cfg.max_commands) return ZBHIP_ENOMEM;
+    cnt = std::min(cnt, h->ovf_cap);  // past the capacity: those batches fell back
     std::vector<uint4> ov(cnt);
     HIPCHK(hipMemcpy(ov.data(), h->d_ovf, cnt * sizeof(uint4), hipMemcpyDeviceToHost));
     HIPCHK(hipMemsetAsync(h->d_ovf_count, 0, sizeof(uint32_t), h->stream));
@@ -1833,6 +1913,10 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.intent = (uint8_t)c6;
       r.record_type = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
       r.unprocessed = !rej && c6 >= 8 && (fl & F_UNPROCESSED) ? 1 : 0;
+      if (r.unprocessed && !h->cont_ids.empty()) {  // deferred: the continuation's id
+        auto it = h->cont_ids.find(((uint64_t)c << 16) | ord);
+        if (it != h->cont_ids.end()) r.aux = (int64_t)it->second;
+      }
     } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE || c6 == C_JOB_CANCELED) {
       r.value_type = ZBHIP_VT_JOB;
       r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED
@@ -2033,6 +2117,31 @@ int zbhip_export_state_db(zbhip_handle* h, zbhip_db_sink sink, void* ctx) {
   DbExport e{h->ser, sink, ctx, ZBHIP_OK};
   const int rc = zbhip_export_state(h, db_row, &e);
   return rc < 0 ? rc : e.rc;
+}
+
+// The records of window command i only (a plain window: no message payloads), keys relabelled: the
+// adapter emits a window command's batch when the platform reaches it, and keys of commands after a
+// fallback command are fixed only once the CPU engine's keys for it are declared -- so this advances
+// the key bookkeeping up to i without forcing (ZBHIP_ESTATE while an earlier fallback is undeclared).
+int zbhip_drain_command(zbhip_handle* h, size_t i, zbhip_record* out, size_t cap, size_t* n_out) {
+  if (!h || (cap && !out) || !n_out) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (!h->results) return ZBHIP_ESTATE;
+  if (h->msg()) return ZBHIP_EUNSUPP;
+  if (i >= h->n_cmds) return ZBHIP_EINVAL;
+  if (int rc = advance(h, i + 1, false)) return rc;
+  if (h->fin_next <= i) return ZBHIP_ESTATE;
+  if (int rc = ensure_out(h)) return rc;
+  const uint32_t nrec = h->h_hdr[i].x & 0xFFFF;
+  if (cap < nrec) {
+    *n_out = nrec;
+    return ZBHIP_ENOMEM;
+  }
+  const uint2* rows = h->h_out.data() + h->h_off[i];
+  for (uint32_t k = 0; k < nrec; ++k)
+    if (int rc = expand_plain(h, i, h->h_cmds[i].instance, rows[k], k, out[k])) return rc;
+  *n_out = nrec;
+  return ZBHIP_OK;
 }
 
 int zbhip_resolve_key(zbhip_handle* h, int64_t key, uint32_t* instance, uint16_t* ordinal) {
@@ -2483,6 +2592,50 @@ int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n) 
       it = it->second.first == i ? h->job_index.erase(it) : std::next(it);
     for (auto it = h->activated.begin(); it != h->activated.end();)
       it = it->second.inst == i ? h->activated.erase(it) : std::next(it);
+    // its follow-ups still waiting in the log now belong to the CPU engine, which reads them back
+    if (h->deferred_per_inst.erase(i))
+      for (auto it = h->deferred.begin(); it != h->deferred.end();)
+        it = it->second.instance == i ? h->deferred.erase(it) : std::next(it);
+  }
+  return ZBHIP_OK;
+}
+
+int zbhip_continuations(zbhip_handle* h, uint64_t* first_id, uint64_t* n) {
+  if (!h || !first_id || !n) return ZBHIP_EINVAL;
+  *first_id = h->last_cont_first;
+  *n = h->last_cont_n;
+  return ZBHIP_OK;
+}
+
+int zbhip_pending_continuations(zbhip_handle* h, uint32_t instance) {
+  if (!h) return ZBHIP_EINVAL;
+  auto it = h->deferred_per_inst.find(instance);
+  return it == h->deferred_per_inst.end() ? 0 : (int)it->second;
+}
+
+// DbKeyGenerator's current key after the last window (its key bookkeeping finished: the CPU
+// engine's declared keys included, undeclared fallbacks counted as none)
+int zbhip_current_key(zbhip_handle* h, int64_t* key) {
+  if (!h || !key) return ZBHIP_EINVAL;
+  if (h->ran && !h->results) return ZBHIP_ESTATE;  // a benchmarking run: keys were not counted
+  if (int rc = finalize(h)) return rc;
+  *key = ((int64_t)h->cfg.partition_id << 51) + h->key_counter;
+  return ZBHIP_OK;
+}
+
+// KeyGeneratorControls.setKeyIfHigher (stream-platform/.../state/DbKeyGenerator.java:54-61): keys the
+// CPU engine generated between two windows; the next window's keys follow them
+int zbhip_set_key_if_higher(zbhip_handle* h, int64_t key) {
+  if (!h) return ZBHIP_EINVAL;
+  if (h->ran && !h->results) return ZBHIP_ESTATE;
+  const int64_t pbits = (int64_t)h->cfg.partition_id << 51;
+  if (key < pbits || key - pbits >= (1LL << 51)) return ZBHIP_EINVAL;  // another partition's key
+  if (int rc = finalize(h)) return rc;
+  if (key - pbits > h->key_counter) {
+    h->key_counter = key - pbits;
+    const unsigned long long kc = (unsigned long long)h->key_counter;
+    HIPCHK(hipMemcpyAsync(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
   }
   return ZBHIP_OK;
 }
@@ -2882,6 +3035,94 @@ extern "C" int zbhip_import_state_db(zbhip_handle* h, const uint8_t* entries, si
   return zbhip_import_state(h, rows.data(), rows.size(), first_slot, n_instances);
 }
 
+// After recovery (StreamProcessorLifecycleAware.onRecovered) the engine's state holds every instance:
+// this marks the entries of the instances the handle can take over -- process instances of processes
+// deployed on the handle, minus `exclude` (instances a command still waiting in the log addresses) --
+// so the adapter imports exactly those (zbhip_import_state_db) and deletes them from RocksDB.  An
+// entry belongs to the instance of its element instance / job / scope (the column families' keys).
+extern "C" int zbhip_select_instances_db(zbhip_handle* h, const uint8_t* entries, size_t len, const int64_t* exclude,
+                                         size_t n_exclude, uint8_t* take, size_t n_take, size_t* n_entries) {
+  if (!h || (len && !entries) || (n_exclude && !exclude) || (n_take && !take)) return ZBHIP_EINVAL;
+  std::vector<std::string> rows;
+  std::vector<char> row(4096);
+  size_t off = 0;
+  while (off < len) {
+    if (len - off < 12) return ZBHIP_EINVAL;
+    uint32_t hd[3];
+    memcpy(hd, entries + off, 12);
+    off += 12;
+    if (len - off < (size_t)hd[1] + hd[2]) return ZBHIP_EINVAL;
+    const int n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
+                                                      string_interner, h, row.data(), row.size());
+    if (n < 0) return n;
+    rows.emplace_back(row.data(), (size_t)n);
+    off += (size_t)hd[1] + hd[2];
+  }
+  if (n_entries) *n_entries = rows.size();
+  if (n_take < rows.size()) return ZBHIP_ENOMEM;
+  auto split = [](const std::string& r) {
+    std::vector<std::string> p;
+    size_t s = 0;
+    for (size_t i = 0; i <= r.size(); ++i)
+      if (i == r.size() || r[i] == '|') { p.push_back(r.substr(s, i - s)); s = i + 1; }
+    return p;
+  };
+  auto field = [](const std::string& f, const char* name) -> std::string {
+    const std::string k = std::string(name) + "=";
+    size_t a = 0;
+    while (a < f.size()) {
+      size_t e = f.find(',', a);
+      if (e == std::string::npos) e = f.size();
+      if (f.compare(a, k.size(), k) == 0) return f.substr(a + k.size(), e - a - k.size());
+      a = e + 1;
+    }
+    return std::string();
+  };
+  std::unordered_set<int64_t> device_keys, excluded(exclude, exclude + n_exclude), eligible;
+  for (const Proc& p : h->procs) device_keys.insert(p.def_key);
+  std::unordered_map<int64_t, int64_t> ei, jobs;  // element instance / job key -> process instance key
+  std::vector<std::vector<std::string>> parts(rows.size());
+  for (size_t i = 0; i < rows.size(); ++i) {
+    if (rows[i].empty()) continue;
+    parts[i] = split(rows[i]);
+    const auto& p = parts[i];
+    if (p[0] == "ELEMENT_INSTANCE_KEY" && p.size() > 2) {
+      const int64_t pik = std::stoll(field(p[2], "processInstanceKey"));
+      ei[std::stoll(p[1])] = pik;
+      if (field(p[2], "bpmnElementType") == "1" && device_keys.count(std::stoll(field(p[2], "processDefinitionKey"))) &&
+          !excluded.count(pik))
+        eligible.insert(pik);
+    } else if (p[0] == "JOBS" && p.size() > 2) {
+      jobs[std::stoll(p[1])] = std::stoll(field(p[2], "processInstanceKey"));
+    }
+  }
+  auto owner = [&](const std::vector<std::string>& p) -> int64_t {
+    auto in = [](const std::unordered_map<int64_t, int64_t>& m, const std::string& k) -> int64_t {
+      auto it = m.find(std::stoll(k));
+      return it == m.end() ? -1 : it->second;
+    };
+    const std::string& cf = p[0];
+    if (p.size() < 2) return -1;
+    if (cf == "ELEMENT_INSTANCE_KEY" || cf == "ELEMENT_INSTANCE_CHILD_PARENT" || cf == "NUMBER_OF_TAKEN_SEQUENCE_FLOWS" ||
+        cf == "VARIABLES" || cf == "EVENT_SCOPE" || cf == "EVENT_TRIGGER" || cf == "TIMERS")
+      return in(ei, p[1]);
+    if (cf == "ELEMENT_INSTANCE_PARENT_CHILD" && p.size() > 2) return in(ei, p[2]);  // [parent, child]: the child's
+    if (cf == "TIMER_DUE_DATES" && p.size() > 2) return in(ei, p[2]);
+    if (cf == "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY" && p.size() > 2) return std::stoll(p[2]);
+    if (cf == "JOBS" || cf == "JOB_STATES") return in(jobs, p[1]);
+    if (cf == "JOB_ACTIVATABLE" && p.size() > 3) return in(jobs, p[3]);
+    if (cf == "JOB_DEADLINES" && p.size() > 2) return in(jobs, p[2]);
+    return -1;
+  };
+  try {
+    for (size_t i = 0; i < rows.size(); ++i)
+      take[i] = !parts[i].empty() && eligible.count(owner(parts[i])) ? 1 : 0;
+  } catch (const std::exception&) {
+    return ZBHIP_EINVAL;
+  }
+  return (int)eligible.size();
+}
+
 // ---- job activation ----------------------------------------------------------
 // JOB_BATCH:ACTIVATE: the host's JOB_ACTIVATABLE index picks the jobs (type, then job key), the device
 // marks them ACTIVATED and gathers their element instances and variables (k_activate_jobs).
@@ -3056,7 +3297,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   const bool fill = h->ring_filled + 1 == h->windows_run;  // every earlier window's keys are in the ring
   if (!fill) h->ring_ok = false;
   h->ring_filled = h->windows_run;  // this window is accounted for, whether or not it is written here
-  if (h->msg() || !h->cont_cmds.empty()) h->ring_ok = false;
+  if (h->msg() || !h->cont_cmds.empty() || h->window_continues) h->ring_ok = false;
   if (!h->ring_ok) return ZBHIP_EUNSUPP;
   const bool dbg = getenv("ZBHIP_DEBUG") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };

@@ -20,12 +20,17 @@ from .native import STATE_SINK, ZbhipError, check, load
 
 
 class ProcessDefinition:
-    def __init__(self, idx, bpmn_process_id, element_ids, element_types, job_types):
+    def __init__(self, idx, bpmn_process_id, element_ids, element_types, job_types, event_types=None, retries=None,
+                 version=1, definition_key=-1):
         self.idx = idx
         self.bpmn_process_id = bpmn_process_id
         self.element_ids = element_ids
         self.element_types = element_types
         self.job_types = job_types
+        self.event_types = event_types       # BpmnEventType names
+        self.retries = retries               # job retries of job worker elements
+        self.version = version
+        self.definition_key = definition_key
 
 
 class _Csr(C.Structure):  # prefix of zbhip_process_csr needed to read the element table
@@ -47,14 +52,15 @@ class Partition:
 
     def __init__(self, partition_id=1, partition_count=1, device=0, max_instances=1 << 16, max_commands=1 << 16,
                  max_records_per_batch=64, max_doc_entries=0, max_commands_in_batch=100, initial_key=0, stream=None,
-                 max_correlation_keys=0, trusted_device_windows=False):
+                 max_correlation_keys=0, trusted_device_windows=False, defer_continuations=False):
         self.L = load()
         cfg = abi.Config(partition_id=partition_id, partition_count=partition_count, device=device,
                          max_commands_in_batch=max_commands_in_batch, max_instances=max_instances,
                          max_commands=max_commands, max_records_per_batch=max_records_per_batch,
                          max_doc_entries=max_doc_entries, initial_key=initial_key, stream=stream,
                          max_correlation_keys=max_correlation_keys,
-                         flags=abi.OPEN_TRUSTED_DEVICE_WINDOWS if trusted_device_windows else 0)
+                         flags=(abi.OPEN_TRUSTED_DEVICE_WINDOWS if trusted_device_windows else 0)
+                         | (abi.OPEN_DEFER_CONTINUATIONS if defer_continuations else 0))
         h = C.c_void_p()
         check(self.L.zbhip_open(C.byref(cfg), C.byref(h)), "zbhip_open")
         self.h = h
@@ -93,7 +99,10 @@ class Partition:
             self.L.zbhip_free_csr(csr)
         pd = ProcessDefinition(idx.value, strings[els[0]["id"]], [strings[i] for i in els["id"]],
                                [abi.ELEMENT_TYPES[t] for t in els["element_type"]],
-                               [strings[j] if j != 0xFFFF else None for j in els["job_type"]])
+                               [strings[j] if j != 0xFFFF else None for j in els["job_type"]],
+                               [abi.EVENT_TYPES[t] for t in els["event_type"]],
+                               [int(r) if j != 0xFFFF else None for r, j in zip(els["job_retries"], els["job_type"])],
+                               version, process_definition_key)
         self.processes.append(pd)
         return idx.value
 
@@ -232,6 +241,16 @@ class Partition:
         check(self.L.zbhip_drain(self.h, out.ctypes.data if n else None, n, C.byref(got)), "zbhip_drain")
         return out[: got.value]
 
+    def drain_command(self, i, cap=256):
+        """The records of window command i (zbhip_drain_command)."""
+        out = np.empty(cap, dtype=abi.RECORD_DTYPE)
+        n = C.c_size_t()
+        rc = self.L.zbhip_drain_command(self.h, i, out.ctypes.data, cap, C.byref(n))
+        if rc == -2 and n.value > cap:
+            return self.drain_command(i, n.value)
+        check(rc, "zbhip_drain_command")
+        return out[: n.value]
+
     def drain_chunks(self, chunk=1 << 22):
         """The window's records in log order, `chunk` at a time (bounded host memory for windows of
         10^7 commands); every yielded view is overwritten by the next one."""
@@ -291,6 +310,18 @@ class Partition:
         check(self.L.zbhip_import_state_db(self.h, blob, len(blob), first_slot, C.byref(n)), "zbhip_import_state_db")
         return n.value
 
+    def select_instances_db(self, entries, exclude=()):
+        """zbhip_select_instances_db: which of the zb-db entries [(column family, key, value)] belong to
+        process instances this partition can take over (recovery); returns (mask, instances)."""
+        import struct
+        blob = b"".join(struct.pack("<III", cf, len(k), len(v)) + bytes(k) + bytes(v) for cf, k, v in entries)
+        ex = np.ascontiguousarray(list(exclude), dtype=np.int64)
+        take = np.zeros(max(len(entries), 1), dtype=np.uint8)
+        n = C.c_size_t()
+        rc = check(self.L.zbhip_select_instances_db(self.h, blob, len(blob), ex.ctypes.data if len(ex) else None, len(ex),
+                                                    take.ctypes.data, len(take), C.byref(n)), "zbhip_select_instances_db")
+        return take[: n.value].astype(bool), rc
+
     def import_state(self, rows, first_slot=0):
         text = "\n".join(rows).encode()
         n = C.c_uint32()
@@ -316,6 +347,23 @@ class Partition:
         k = C.c_int64()
         check(self.L.zbhip_key_before(self.h, i, C.byref(k)), "zbhip_key_before")
         return k.value
+
+    def continuations(self):
+        """Ids of the continuations the last run deferred, in drain order of the unprocessed records."""
+        first, n = C.c_uint64(), C.c_uint64()
+        check(self.L.zbhip_continuations(self.h, C.byref(first), C.byref(n)), "zbhip_continuations")
+        return range(first.value, first.value + n.value)
+
+    def pending_continuations(self, instance):
+        return check(self.L.zbhip_pending_continuations(self.h, instance), "zbhip_pending_continuations")
+
+    def current_key(self):
+        k = C.c_int64()
+        check(self.L.zbhip_current_key(self.h, C.byref(k)), "zbhip_current_key")
+        return k.value
+
+    def set_key_if_higher(self, key):
+        check(self.L.zbhip_set_key_if_higher(self.h, key), "zbhip_set_key_if_higher")
 
     def set_external_keys(self, i, nkeys):
         check(self.L.zbhip_set_external_keys(self.h, i, nkeys), "zbhip_set_external_keys")

@@ -30,7 +30,9 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
            "zbhip_set_external_keys", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
            "zbhip_import_state", "zbhip_activate_jobs", "zbhip_job_batch_rejection_reason",
-           "zbhip_serialize_log_device", "zbhip_log_device_copy"]
+           "zbhip_serialize_log_device", "zbhip_log_device_copy", "zbhip_continuations",
+           "zbhip_pending_continuations", "zbhip_current_key", "zbhip_set_key_if_higher",
+           "zbhip_select_instances_db", "zbhip_drain_command"]
 
 
 class ZbhipError(RuntimeError):
@@ -97,6 +99,12 @@ def load():
     L.zbhip_export_instances_db.argtypes = [vp, vp, sz, DB_SINK, vp]
     L.zbhip_evict_instances.argtypes = [vp, vp, sz]
     L.zbhip_key_before.argtypes = [vp, sz, C.POINTER(i64)]
+    L.zbhip_continuations.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.zbhip_pending_continuations.argtypes = [vp, u32]
+    L.zbhip_current_key.argtypes = [vp, C.POINTER(i64)]
+    L.zbhip_set_key_if_higher.argtypes = [vp, i64]
+    L.zbhip_drain_command.argtypes = [vp, sz, vp, sz, C.POINTER(sz)]
+    L.zbhip_select_instances_db.argtypes = [vp, vp, sz, vp, sz, vp, sz, C.POINTER(sz)]
     L.zbhip_set_external_keys.argtypes = [vp, sz, u32]
     L.zbhip_serializer_decode_state_entry.argtypes = [vp, u32, C.c_char_p, sz, C.c_char_p, sz, INTERNER, vp,
                                                       C.c_char_p, sz]
