@@ -26,7 +26,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-SURVEY_BYTES_PER_TRANSITION = {"linear10": 114.4, "one_task": 100.4, "xor": 93.3, "forkjoin8": 92.8}
+SURVEY_BYTES_PER_TRANSITION = {"linear10": 114.4, "one_task": 100.4, "xor": 93.3, "forkjoin8": 92.8,
+                               "forkjoin8_tasks": 92.8}
 
 
 def workload(name):
@@ -40,6 +41,8 @@ def workload(name):
         return bpmn.xor_process(), 10_000_000, 0, True
     if name == "forkjoin8":
         return bpmn.fork_join_process(8), 10_000_000, 0, False
+    if name == "forkjoin8_tasks":  # variant 4b: a service task per branch, jobs completed in random branch order
+        return bpmn.fork_join_process(8, tasks=True), 10_000_000, 8, False
     if name == "boundary10":  # linear-10 with an interrupting timer boundary event on every task (KScope)
         b = bpmn.createExecutableProcess("boundary10").startEvent("start")
         for i in range(10):
@@ -52,6 +55,10 @@ def workload(name):
 # first job key ordinal and ordinals per phase of the JOB:COMPLETE windows (kernels.hip key order:
 # per task SFT, ACTIVATE, [the boundary's timer,] job; per completion PROCESS_EVENT + those)
 JOB_ORDINALS = {"boundary10": (6, 5)}
+# forkjoin8_tasks records per window (SURVEY App. A.4 variant 4b): CREATE 63 (start, fork, 8 x
+# [SFT, ACTIVATE, ACTIVATING, JOB:CREATED, ACTIVATED]); completions 1..7 9 each (JOB:COMPLETED,
+# PROCESS_EVENT, COMPLETE, COMPLETING, COMPLETED, SFT, ACTIVATE(join), the join's rejection... )
+FJ8T_RECORDS = None  # measured by the bench's probe (records of one instance per window)
 
 
 def algorithmic_bytes(name, n, phases):
@@ -72,6 +79,17 @@ def algorithmic_bytes(name, n, phases):
         return (16 + 16 + 32 + 26 * 8 + 8) * n  # + the amount document entry (16 B)
     if name == "forkjoin8":
         return (16 + 32 + 52 * 8 + 8) * n
+    if name == "forkjoin8_tasks":
+        # CREATE: cmd 16 + hdr 32 + records (start .. 8 branches activated, 8 jobs) + hdr 8 + 8 slots
+        # written (8 B each) + join words 16; each JOB:COMPLETE: cmd 16 + hdr 32 + the 8 slots read
+        # (the lane loads the instance's table) + the remaining ones written + join words read and
+        # written 32 + records + hdr 8.  Records per window: see records_forkjoin8_tasks
+        recs = FJ8T_RECORDS
+        b = 16 + 32 + recs[0] * 8 + 8 + 8 * 8 + 16
+        for p in range(phases):
+            left = 8 - p - 1
+            b += 16 + 32 + (8 - p) * 8 + left * 8 + 32 + recs[p + 1] * 8 + 8
+        return b * n
     if name == "boundary10":
         # linear-10's rows plus the timer: CREATE 16 records + the timer row written (16 B); each
         # JOB:COMPLETE 12 records (TIMER:CANCELED, the next TIMER:CREATED), the timer row read and
@@ -372,6 +390,8 @@ def main():
     ap.add_argument("--config", default="linear10")
     ap.add_argument("--instances", type=int, default=0, help="override instances per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-templates", action="store_true",
+                    help="general path only: CREATE batch templates off (ZBHIP_NO_TEMPLATES)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-instances", type=int, default=300_000, help="instances per CPU thread (bounded sample)")
     ap.add_argument("--host-io", action="store_true",
@@ -406,6 +426,35 @@ def _spawned_rank(rank, world, port, argv):
     main()
 
 
+def probe_fork_join_tasks(xml, local_rank):
+    """One instance of variant 4b in results mode: the key ordinal of each branch's job (JOB:CREATED
+    of task t<b> in the CREATE batch) and the records of each window (CREATE, then 8 completions)."""
+    import numpy as np
+    from zeebe_amd import abi
+    from zeebe_amd.engine import Partition
+    part = Partition(max_instances=1, max_commands=1, max_records_per_batch=64, device=local_rank)
+    part.deploy(xml)
+    c = abi.make_commands(1)
+    c["kind"] = abi.CMD_CREATE
+    part.submit(c)
+    part.run()
+    recs = part.drain()
+    counts = [len(recs)]
+    ids = part.processes[0].element_ids
+    ords = np.zeros(8, dtype=np.uint16)
+    for r in recs:
+        if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED:
+            ords[int(ids[int(r["element_idx"])][1:]) - 1] = part.resolve_key(int(r["key"]))[1]
+    for b in range(8):
+        c = abi.make_commands(1)
+        c["kind"], c["ref"] = abi.CMD_JOB_COMPLETE, ords[b]
+        part.submit(c)
+        part.run()
+        counts.append(len(part.drain()))
+    part.close()
+    return ords, counts
+
+
 def run_rank(args):
     import numpy as np
     import torch
@@ -427,6 +476,8 @@ def run_rank(args):
     from zeebe_amd import abi
     from zeebe_amd.engine import Partition
 
+    if args.no_templates:
+        os.environ["ZBHIP_NO_TEMPLATES"] = "1"  # read by zbhip_run at every launch
     xml, n, phases, with_amount = workload(args.config)
     if args.instances:
         n = args.instances
@@ -459,11 +510,20 @@ def run_rank(args):
     windows.append(torch.from_numpy(create.view(np.uint8).copy()).to(dev))
     host_windows.append((create, docs if with_amount else None))
     job_ord, per_phase = JOB_ORDINALS.get(args.config, (5 if not with_amount else 6, 4))
+    branch_ord = None
+    if args.config == "forkjoin8_tasks":
+        # variant 4b: every instance completes its 8 branch jobs in its own seeded random order
+        # (seed 0x5EED04); the job key ordinals and records per window come from a probe
+        branch_ord, recs = probe_fork_join_tasks(xml, local_rank)
+        global FJ8T_RECORDS
+        FJ8T_RECORDS = recs
+        rng = np.random.default_rng(0x5EED04 + rank)
+        order = np.argsort(rng.random((n, 8)), axis=1).astype(np.uint16)  # a permutation per instance
     for p in range(phases):
         c = abi.make_commands(n)
         c["instance"] = np.arange(n, dtype=np.uint32)
         c["kind"] = abi.CMD_JOB_COMPLETE
-        c["ref"] = job_ord + per_phase * p
+        c["ref"] = job_ord + per_phase * p if branch_ord is None else branch_ord[order[:, p]]
         windows.append(torch.from_numpy(c.view(np.uint8).copy()).to(dev))
         host_windows.append((c, None))
     torch.cuda.synchronize()
@@ -552,10 +612,13 @@ def run_rank(args):
                                 "one_task": "configs[0] one_task.bpmn create->job complete",
                                 "xor": "configs[2] exclusive gateway `= amount > 1000`, 10M instances",
                                 "forkjoin8": "configs[3] parallel fork/join 8 branches, 10M instances",
+                                "forkjoin8_tasks": "configs[3] variant 4b: fork/join 8 branches with a service task "
+                                                   "each, jobs completed in random branch order, 10M instances",
                                 "boundary10": "linear 10 service tasks, each with an interrupting timer boundary "
                                               "event (timers created and canceled), 1M instances"}[args.config],
                    "instances_per_gpu": n, "windows_per_step": len(windows), "partitions": world,
-                   "parallelism": "one partition per GPU (dp%d)" % world, "max_commands_in_batch": 100},
+                   "parallelism": "one partition per GPU (dp%d)" % world, "max_commands_in_batch": 100,
+                   "templates": not args.no_templates},
         "records_per_s": tot_recs / elapsed,
         # CREATE batches copied from a template the general path recorded (kernels.hip tpl_create)
         "template_batches_per_step": tpl_timed / max(1, args.steps),
@@ -573,9 +636,12 @@ def run_rank(args):
     if args.host_io and rank == 0:
         result["host_io"] = host_io_pass(args, xml, n, host_windows, local_rank, recs_per_batch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle.oracle import bench as cpu_bench
+        from oracle.oracle import bench as cpu_bench, bench_jobs
         th = args.cpu_threads
-        sec, ctr, ccomp = cpu_bench(xml, th, args.cpu_instances, phases, with_amount)
+        if branch_ord is not None:
+            sec, ctr, ccomp = bench_jobs(xml, th, args.cpu_instances, branch_ord)
+        else:
+            sec, ctr, ccomp = cpu_bench(xml, th, args.cpu_instances, phases, with_amount)
         result["cpu_baseline"] = {"value": ctr / sec, "unit": "transitions/s", "cores": th, "kind": "port",
                                   "completed_instances_per_s": ccomp / sec,
                                   "sample": "%d partitions (1 per thread) x %d instances, same workload, %.1f s"

@@ -92,6 +92,9 @@ def lib():
         L.zbo_java_hash.argtypes = [C.c_char_p, C.c_size_t]
         L.zbo_bench_msg.restype = C.c_double
         L.zbo_bench_msg.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.zbo_bench_jobs.restype = C.c_double
+        L.zbo_bench_jobs.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_uint64,
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.zbo_bench.restype = C.c_double
         L.zbo_bench.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
@@ -281,6 +284,20 @@ def bench(xml, threads, n_instances, phases, with_amount=False, seed=0x5EED03):
         xml = xml.encode()
     t, c = C.c_uint64(), C.c_uint64()
     sec = lib().zbo_bench(xml, threads, n_instances, phases, 1 if with_amount else 0, seed, C.byref(t), C.byref(c))
+    if sec < 0:
+        raise OracleError("bench deploy failed")
+    return sec, t.value, c.value
+
+
+def bench_jobs(xml, threads, n_instances, job_ords, seed=0x5EED04):
+    """CPU baseline of variant 4b: each instance completes its jobs (key ordinals job_ords) in its
+    own random order, one per phase; returns seconds, transitions, completed."""
+    import numpy as np
+    if isinstance(xml, str):
+        xml = xml.encode()
+    o = np.ascontiguousarray(job_ords, dtype=np.uint16)
+    t, c = C.c_uint64(), C.c_uint64()
+    sec = lib().zbo_bench_jobs(xml, threads, n_instances, o.ctypes.data, len(o), seed, C.byref(t), C.byref(c))
     if sec < 0:
         raise OracleError("bench deploy failed")
     return sec, t.value, c.value

@@ -2846,8 +2846,23 @@ double zbo_bench_msg(const char* xml, int P, int n, uint64_t* transitions_out, u
   return sec;
 }
 
+static double bench_impl(const char* xml, int threads, int n_instances, int phases, int var_name_kind, uint64_t seed,
+                         const uint16_t* job_ords, int n_ords, uint64_t* transitions_out, uint64_t* completed_out);
+
 double zbo_bench(const char* xml, int threads, int n_instances, int phases, int var_name_kind,
                  uint64_t seed, uint64_t* transitions_out, uint64_t* completed_out) {
+  return bench_impl(xml, threads, n_instances, phases, var_name_kind, seed, nullptr, 0, transitions_out, completed_out);
+}
+
+// Variant 4b: every instance waits on n_ords jobs at once (their key ordinals in the
+// CREATE batch) and completes them in its own random order, one per phase.
+double zbo_bench_jobs(const char* xml, int threads, int n_instances, const uint16_t* job_ords, int n_ords,
+                      uint64_t seed, uint64_t* transitions_out, uint64_t* completed_out) {
+  return bench_impl(xml, threads, n_instances, n_ords, 0, seed, job_ords, n_ords, transitions_out, completed_out);
+}
+
+static double bench_impl(const char* xml, int threads, int n_instances, int phases, int var_name_kind, uint64_t seed,
+                         const uint16_t* job_ords, int n_ords, uint64_t* transitions_out, uint64_t* completed_out) {
   std::vector<std::unique_ptr<Oracle>> os;
   std::vector<std::vector<zbhip_command>> creates(threads);
   std::vector<std::vector<zbhip_doc_entry>> docs(threads);
@@ -2874,6 +2889,21 @@ double zbo_bench(const char* xml, int threads, int n_instances, int phases, int 
       creates[t].push_back(c);
     }
   }
+  // per instance a random order of its jobs (variant 4b)
+  std::vector<std::vector<uint16_t>> order(threads);
+  if (job_ords)
+    for (int t = 0; t < threads; ++t) {
+      uint64_t s = seed * 0x2545F4914F6CDD1DULL + (uint64_t)t + 1;
+      order[t].resize((size_t)n_instances * n_ords);
+      for (int i = 0; i < n_instances; ++i) {
+        uint16_t* o = &order[t][(size_t)i * n_ords];
+        for (int k = 0; k < n_ords; ++k) o[k] = (uint16_t)k;
+        for (int k = n_ords - 1; k > 0; --k) {
+          s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+          std::swap(o[k], o[s % (uint64_t)(k + 1)]);
+        }
+      }
+    }
   auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
   for (int t = 0; t < threads; ++t) {
@@ -2892,6 +2922,7 @@ double zbo_bench(const char* xml, int threads, int n_instances, int phases, int 
           c.instance = (uint32_t)i;
           c.kind = ZBHIP_CMD_JOB_COMPLETE;
           c.ref = (uint16_t)(ks.size() - 1);  // the job key is the last key of the activating batch
+          if (job_ords) c.ref = job_ords[order[t][(size_t)i * n_ords + ph]];
           cs.push_back(c);
         }
         O.submit(cs.data(), cs.size(), nullptr, 0);
