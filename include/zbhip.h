@@ -38,13 +38,17 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 5  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+#define ZBHIP_ABI_VERSION 6  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
                                4: timer boundary events (start_event / flow_source / job_retries of job
                                   workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
                                   PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions;
                                5: ZBHIP_OPEN_DEFER_CONTINUATIONS / ZBHIP_CMD_CONTINUE,
                                   zbhip_continuations, zbhip_pending_continuations, zbhip_current_key,
-                                  zbhip_set_key_if_higher */
+                                  zbhip_set_key_if_higher;
+                               6: multi-instance bodies (ZBHIP_EL_MULTI_INSTANCE_BODY elements,
+                                  ZBHIP_OP_ITEM collections), PROCESS_INSTANCE_BATCH records, VARIABLE
+                                  records with inline values (ZBHIP_AUX_INLINE), six variables per
+                                  activated job */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -67,7 +71,8 @@ enum zbhip_value_type {
   ZBHIP_VT_VARIABLE = 17,
   ZBHIP_VT_PROCESS_INSTANCE_CREATION = 19,
   ZBHIP_VT_PROCESS_EVENT = 24,
-  ZBHIP_VT_TIMER = 15
+  ZBHIP_VT_TIMER = 15,
+  ZBHIP_VT_PROCESS_INSTANCE_BATCH = 34
 };
 enum zbhip_rejection_type {
   ZBHIP_REJ_INVALID_ARGUMENT = 0,
@@ -99,6 +104,8 @@ enum { ZBHIP_PE_TRIGGERING = 0, ZBHIP_PE_TRIGGERED = 1 };
 enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
 /* TimerIntent (protocol/.../intent/TimerIntent.java:19-30) */
 enum { ZBHIP_TIMER_CREATED = 0, ZBHIP_TIMER_TRIGGER = 1, ZBHIP_TIMER_TRIGGERED = 2, ZBHIP_TIMER_CANCELED = 4 };
+/* ProcessInstanceBatchIntent (protocol/.../intent/ProcessInstanceBatchIntent.java:18-20) */
+enum { ZBHIP_PIB_TERMINATE = 0, ZBHIP_PIB_ACTIVATE = 1 };
 /* MessageIntent, MessageSubscriptionIntent, ProcessMessageSubscriptionIntent
  * (protocol/.../intent/MessageIntent.java:19-23, MessageSubscriptionIntent.java:19-30,
  * ProcessMessageSubscriptionIntent.java:19-28) */
@@ -167,20 +174,27 @@ typedef struct zbhip_element {
   uint16_t flow_source;  /* sequence flow: source node; boundary event: the activity it is attached to
                           * (attachedToRef, ExecutableActivity.attach); else ZBHIP_NONE16 */
   uint16_t flow_target;  /* sequence flow: target node; else ZBHIP_NONE16 */
-  uint16_t condition;    /* sequence flow: condition index; ZBHIP_NONE16 = no condition */
+  uint16_t condition;    /* sequence flow: condition index; ZBHIP_NONE16 = no condition;
+                          * multi-instance body: the index of its static inputCollection (ZBHIP_OP_ITEM
+                          * instructions, one per item, then ZBHIP_OP_END) */
   uint16_t default_flow; /* exclusive gateway: default flow element; else ZBHIP_NONE16 */
   uint16_t job_type;     /* service task: string-table index of the job type */
   uint16_t job_retries;  /* service task: static retries; boundary event: bit 0 interrupting (cancelActivity),
-                          * bits 8..15 the timer's repetitions (1 a duration, n of "Rn/", 255 "R/" infinite) */
+                          * bits 8..15 the timer's repetitions (1 a duration, n of "Rn/", 255 "R/" infinite);
+                          * multi-instance body: bit 0 isSequential */
   uint16_t join_slot;    /* sequence flow into a parallel gateway: its taken-counter slot; else NONE */
   uint16_t id;           /* string-table index of the element id */
-  uint16_t message_name; /* message catch event: string-table index of the static message name; else NONE */
+  uint16_t message_name; /* message catch event: string-table index of the static message name;
+                          * multi-instance body: string-table index of its inputElement; else NONE */
   uint16_t correlation_var; /* message catch event: string-table index of the variable of `= var` */
   uint16_t flow_scope;   /* the element's container: 0 = the process, else the embedded sub-process
-                          * element (ExecutableFlowElement.getFlowScope, FlowElementInstantiationTransformer) */
+                          * element (ExecutableFlowElement.getFlowScope, FlowElementInstantiationTransformer)
+                          * or the multi-instance body of an inner activity (MultiInstanceActivityTransformer) */
   uint16_t start_event;  /* process / embedded sub-process: its none start event
                           * (ExecutableFlowElementContainer.getNoneStartEvent); job worker task: its
-                          * (one, timer) boundary event; else ZBHIP_NONE16 */
+                          * (one, timer) boundary event; multi-instance body: its inner activity
+                          * (ExecutableMultiInstanceBody.getInnerActivity), which shares its id; else
+                          * ZBHIP_NONE16 */
   uint32_t duration_ms;  /* timer catch / boundary event: the static timeDuration in ms (Interval.parse); else 0 */
 } zbhip_element;
 
@@ -194,7 +208,10 @@ enum zbhip_op {
   ZBHIP_OP_PUSH_NULL = 4,
   ZBHIP_OP_LT = 5, ZBHIP_OP_LE = 6, ZBHIP_OP_GT = 7, ZBHIP_OP_GE = 8,
   ZBHIP_OP_EQ = 9, ZBHIP_OP_NE = 10,
-  ZBHIP_OP_AND = 11, ZBHIP_OP_OR = 12, ZBHIP_OP_NOT = 13
+  ZBHIP_OP_AND = 11, ZBHIP_OP_OR = 12, ZBHIP_OP_NOT = 13,
+  ZBHIP_OP_ITEM = 14       /* an inputCollection item: arg = its zbhip_doc_type -- INT, BOOL, NIL or STR;
+                            * literal = the value (STR: string-table index; zbhip_deploy interns it
+                            * into the value dictionary) */
 };
 #define ZBHIP_DEC_SCALE 6   /* fixed decimal scale of NUMBER values on the device */
 
@@ -388,7 +405,8 @@ int zbhip_set_clock(zbhip_handle* h, int64_t now_ms);
 typedef struct zbhip_record {
   int64_t key;                  /* relabelled to the reference key */
   int64_t scope_key;            /* PI: flowScopeKey; JOB: elementInstanceKey; VARIABLE/PROCESS_EVENT:
-                                   scopeKey; PI_CREATION: processInstanceKey */
+                                   scopeKey; PI_CREATION: processInstanceKey;
+                                   PROCESS_INSTANCE_BATCH: batchElementInstanceKey */
   int64_t process_instance_key;
   int64_t source_index;         /* index of the batch's initial command in submission order */
   int32_t process_idx;
@@ -400,7 +418,10 @@ typedef struct zbhip_record {
   uint16_t ordinal;             /* position within the batch */
   uint8_t reason;               /* rejection reason kind (zbhip_reason), 0 = none */
   uint8_t reason_arg;           /* e.g. the offending element-instance state */
-  int64_t aux;                  /* VARIABLE: document entry index; JOB:COMPLETED: source doc; else -1 */
+  int64_t aux;                  /* VARIABLE: document entry index, or ZBHIP_AUX_INLINE (the value in
+                                   message_key, its zbhip_doc_type in partition: multi-instance
+                                   loopCounter / input element); JOB:COMPLETED: source doc;
+                                   PROCESS_INSTANCE_BATCH: index (children still to activate); else -1 */
   /* message value fields (MESSAGE / MESSAGE_SUBSCRIPTION / PROCESS_MESSAGE_SUBSCRIPTION) */
   int64_t message_key;          /* messageKey, -1 unset */
   uint32_t correlation_key;     /* string id, ZBHIP_NO_STRING = empty */
@@ -414,6 +435,7 @@ typedef struct zbhip_record {
   uint8_t pad[2];
 } zbhip_record;
 #define ZBHIP_NO_STRING 0xFFFFFFFFu
+#define ZBHIP_AUX_INLINE (-2)
 
 int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out);
 /* The records of window command i only (plain windows; ZBHIP_EUNSUPP for message partitions): what a
@@ -627,7 +649,7 @@ typedef struct zbhip_activated_job {
   int32_t element_idx;
   uint16_t retries;
   uint16_t n_variables;
-  zbhip_doc_entry variables[4];  /* the job's variables document, in document order */
+  zbhip_doc_entry variables[6];  /* the job's variables document, in document order */
 } zbhip_activated_job;
 
 typedef struct zbhip_job_batch {

@@ -339,6 +339,16 @@ struct OEl {
   int boundary = -1;               // activity: its (one) boundary event (ExecutableActivity.attach)
   bool interrupting = true;        // boundary event: cancelActivity (ExecutableBoundaryEvent.interrupting)
   int reps = 1;                    // timer: repetitions (RepeatingInterval; 1 a duration, -1 infinite)
+  // multi-instance body (ExecutableMultiInstanceBody / ExecutableLoopCharacteristics): its inner
+  // activity (the next element, same id, flow scope = the body), isSequential, the static
+  // inputCollection's items (zbhip_doc_type, value; strings as text until deploy interns them) and the
+  // inputElement variable name ("" none)
+  int inner = -1;
+  bool mi_seq = false;
+  std::vector<std::pair<uint8_t, int64_t>> mi_items;
+  std::vector<std::string> mi_item_text;
+  std::string mi_input;
+  int mi_input_id = -1, mi_loop_id = -1;
 };
 
 struct OProc {
@@ -388,6 +398,81 @@ static int64_t parse_duration_ms(std::string t) {
     else return -1;
   }
   return any ? ms : -1;
+}
+
+// MultiInstanceActivityTransformer.transformLoopCharacteristics
+// (deployment/model/transformer/MultiInstanceActivityTransformer.java:80-122) for the subset: the
+// inputCollection a static FEEL list literal (`= [10, 20, 30]`, `= ["a", "b"]`: integer, string,
+// boolean and null items -- FeelToMessagePackTransformer writes a whole number as a msgpack integer),
+// an optional inputElement; a completionCondition, outputCollection or outputElement is outside it.
+static bool parse_multi_instance(const XNode& mil, OEl& body, std::string& err) {
+  body.mi_seq = mil.attr("isSequential") == "true";
+  const XNode* cc = mil.child("completionCondition");
+  if (cc && cc->text.find_first_not_of(" \t\r\n") != std::string::npos) {
+    err = "multi-instance completionCondition outside the supported subset";
+    return false;
+  }
+  const XNode* ext = mil.child("extensionElements");
+  const XNode* lc = ext ? ext->child("loopCharacteristics") : nullptr;
+  if (!lc) { err = "multi-instance without zeebe:loopCharacteristics"; return false; }
+  if (!lc->attr("outputCollection").empty() || !lc->attr("outputElement").empty()) {
+    err = "multi-instance outputCollection / outputElement outside the supported subset";
+    return false;
+  }
+  body.mi_input = lc->attr("inputElement");
+  std::string t = lc->attr("inputCollection");
+  size_t i = t.find_first_not_of(" \t\r\n");
+  auto bad = [&err, &t]() { err = "multi-instance inputCollection outside the supported subset (a static list): " + t; return false; };
+  if (i == std::string::npos || t[i] != '=') return bad();
+  auto ws = [&]() { while (i < t.size() && isspace((unsigned char)t[i])) ++i; };
+  ++i;
+  ws();
+  if (i >= t.size() || t[i] != '[') return bad();
+  ++i;
+  ws();
+  if (i < t.size() && t[i] == ']') {
+    ++i;
+  } else {
+    for (;;) {
+      ws();
+      if (i >= t.size()) return bad();
+      if (t[i] == '"') {
+        size_t e = t.find('"', i + 1);
+        if (e == std::string::npos) return bad();
+        const std::string v = t.substr(i + 1, e - i - 1);
+        if (v.find('\\') != std::string::npos) return bad();
+        body.mi_items.push_back({ZBHIP_DOC_STR, 0});
+        body.mi_item_text.push_back(v);
+        i = e + 1;
+      } else if (t.compare(i, 4, "true") == 0 || t.compare(i, 5, "false") == 0 || t.compare(i, 4, "null") == 0) {
+        const bool n = t[i] == 'n', tr = t[i] == 't';
+        body.mi_items.push_back({n ? ZBHIP_DOC_NIL : ZBHIP_DOC_BOOL, tr ? 1 : 0});
+        body.mi_item_text.emplace_back();
+        i += t[i] == 'f' ? 5 : 4;
+      } else {
+        const bool neg = t[i] == '-';
+        if (neg) ++i;
+        const size_t s0 = i;
+        unsigned long long v = 0;
+        while (i < t.size() && isdigit((unsigned char)t[i])) {
+          if (v > 922337203685477580ULL) return bad();
+          v = v * 10 + (unsigned)(t[i] - '0');
+          ++i;
+        }
+        if (i == s0 || v > 9223372036854775807ULL || (i < t.size() && (t[i] == '.' || isalpha((unsigned char)t[i]))))
+          return bad();
+        body.mi_items.push_back({ZBHIP_DOC_INT, neg ? -(int64_t)v : (int64_t)v});
+        body.mi_item_text.emplace_back();
+      }
+      ws();
+      if (i < t.size() && t[i] == ',') { ++i; continue; }
+      if (i < t.size() && t[i] == ']') { ++i; break; }
+      return bad();
+    }
+  }
+  ws();
+  if (i != t.size() || body.mi_items.size() > 65535) return bad();
+  return true;
 }
 
 static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, std::string& err) {
@@ -564,6 +649,27 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       return false;
     }
     if (e.id.empty()) { err = "element without id"; return false; }
+    if (k->child("standardLoopCharacteristics")) { err = "standard loop outside the supported subset"; return false; }
+    if (const XNode* mil = k->child("multiInstanceLoopCharacteristics")) {
+      // MultiInstanceActivityTransformer.transform (:35-78): the body takes the activity's id, flow
+      // scope and sequence flows; the inner activity's flow scope is the body
+      if (!ZBHIP_IS_JOB_WORKER(e.type) && e.type != ZBHIP_EL_TASK && e.type != ZBHIP_EL_MANUAL_TASK) {
+        err = "multi-instance " + n + " outside the supported subset (job worker and undefined tasks)";
+        return false;
+      }
+      OEl b;
+      b.id = e.id;
+      b.type = ZBHIP_EL_MULTI_INSTANCE_BODY;
+      b.scope = scope;
+      if (!parse_multi_instance(*mil, b, err)) return false;
+      const int bi = (int)P.els.size();
+      b.inner = bi + 1;
+      idx[e.id] = bi;
+      P.els.push_back(std::move(b));
+      e.scope = bi;
+      P.els.push_back(std::move(e));
+      continue;
+    }
     const int self = (int)P.els.size();
     const int type = e.type, event = e.event;
     idx[e.id] = self;
@@ -653,6 +759,7 @@ struct ElementInstance {  // state/instance/ElementInstance.java:23-54
   int state = 0;
   PiValue value;
   int activeSequenceFlows = 0;
+  int childActivated = 0, childCompleted = 0, loopCounter = 0;  // multi-instance (ElementInstance.java:25-33)
 };
 
 struct Doc {  // a variable document (msgpack map) as a list of entries
@@ -863,6 +970,15 @@ class Oracle {
         has_msg = true;
       }
     if (has_msg) intern(P.bpmn_id);
+    // multi-instance bodies, in element order: the inputElement and loopCounter names, then the string
+    // items into the value dictionary (the product's zbhip_deploy interns in this order)
+    for (auto& e : P.els) {
+      if (e.type != ZBHIP_EL_MULTI_INSTANCE_BODY) continue;
+      if (!e.mi_input.empty()) e.mi_input_id = intern(e.mi_input);
+      e.mi_loop_id = intern("loopCounter");
+      for (size_t j = 0; j < e.mi_items.size(); ++j)
+        if (e.mi_items[j].first == ZBHIP_DOC_STR) e.mi_items[j].second = intern_string(e.mi_item_text[j]);
+    }
     procs.push_back(std::move(P));
     return (int)procs.size() - 1;
   }
@@ -1005,7 +1121,8 @@ class Oracle {
     const uint32_t base = (uint32_t)docs.size();
     docs.insert(docs.end(), d, d + nd);
     rec.doc = Doc{base, (uint32_t)nd};
-    rec.r.aux = r.value_type == ZBHIP_VT_TIMER ? r.aux : nd ? (int64_t)base : -1;
+    rec.r.aux = r.value_type == ZBHIP_VT_TIMER || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH ? r.aux
+                : nd ? (int64_t)base : -1;
     rec.pi.proc = r.process_idx;
     rec.pi.elem = r.element_idx;
     rec.pi.flowScopeKey = r.scope_key;
@@ -1013,11 +1130,13 @@ class Oracle {
     const bool known = (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION && r.intent == ZBHIP_PIC_CREATE) ||
                        (r.value_type == ZBHIP_VT_JOB && r.intent == ZBHIP_JOB_COMPLETE) ||
                        (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
-                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT);
+                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT) ||
+                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && r.intent == ZBHIP_PIB_ACTIVATE);
     if (!known) { last_error = "process_one: command outside the restated subset"; return ZBHIP_EUNSUPP; }
-    if (r.value_type == ZBHIP_VT_PROCESS_INSTANCE || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION)
+    if (r.value_type == ZBHIP_VT_PROCESS_INSTANCE || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION ||
+        r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH)
       if (r.process_idx < 0 || r.process_idx >= (int)procs.size() ||
-          (r.value_type == ZBHIP_VT_PROCESS_INSTANCE &&
+          (r.value_type != ZBHIP_VT_PROCESS_INSTANCE_CREATION &&
            (r.element_idx < 0 || r.element_idx >= (int)procs[r.process_idx].els.size()))) {
         last_error = "process_one: unknown process or element";
         return ZBHIP_EINVAL;
@@ -1104,6 +1223,10 @@ class Oracle {
             ei.jobKey = L(f.at("jobKey"));
             ei.state = (int)L(f.at("state"));
             ei.activeSequenceFlows = (int)L(f.at("activeSequenceFlows"));
+            ei.childActivated = (int)L(f.at("childActivatedCount"));
+            ei.childCompleted = (int)L(f.at("childCompletedCount"));
+            ei.loopCounter = (int)L(f.at("multiInstanceLoopCounter"));
+            if (L(f.at("childTerminatedCount")) != 0) throw Unsupported{"terminated children"};
             ei.value.flowScopeKey = L(f.at("flowScopeKey"));
             ei.value.piKey = L(f.at("processInstanceKey"));
             if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), ei.value.proc, ei.value.elem))
@@ -1218,9 +1341,12 @@ class Oracle {
       a.proc = j.pi.proc;
       a.elem = j.pi.elem;
       a.retries = j.retries;
+      // the element scope, then every scope above it (a multi-instance inner activity: its loop
+      // variables, the body, the process instance)
       std::vector<int64_t> scopes{j.elementInstanceKey};
-      auto eit = ei_.find(j.elementInstanceKey);
-      if (eit != ei_.end() && eit->second.value.flowScopeKey >= 0) scopes.push_back(eit->second.value.flowScopeKey);
+      for (auto pit = child_parent_.find(j.elementInstanceKey); pit != child_parent_.end() && pit->second > 0;
+           pit = child_parent_.find(pit->second))
+        scopes.push_back(pit->second);
       std::set<int> seen;
       for (int64_t scope : scopes) {
         std::vector<int> local;
@@ -1441,6 +1567,8 @@ class Oracle {
       trigger_timer(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE)
       bpmn_process_record(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && cmd.r.intent == ZBHIP_PIB_ACTIVATE)
+      activate_batch(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_MESSAGE && cmd.r.intent == ZBHIP_MSG_PUBLISH)
       publish_message(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_MS_CREATE)
@@ -1932,6 +2060,56 @@ class Oracle {
     activatable_.erase({job.type, "<default>", jobKey});
   }
 
+  // ActivateProcessInstanceBatchProcessor.processRecord (processing/processinstance/
+  // ActivateProcessInstanceBatchProcessor.java:44-60): `index` ACTIVATE_ELEMENT commands of the inner
+  // activity, each with a new key, the body's record value with flow scope = the body
+  // (createChildInstanceRecord :62-84).  The size-based split into a follow-up batch command
+  // (canWriteCommands, ~4 MB batches) never happens at these record sizes.
+  void activate_batch(ORecord& cmd) {
+    auto it = ei_.find(cmd.r.scope_key);
+    if (it == ei_.end()) throw Unsupported{"batch activation without its body instance"};
+    PiValue c = it->second.value;
+    c.flowScopeKey = it->second.key;
+    c.elem = E(it->second.value).inner;
+    for (int64_t n = cmd.r.aux; n > 0; --n) pi_command(next_key(), ZBHIP_PI_ACTIVATE_ELEMENT, c);
+  }
+
+  // MultiInstanceBodyProcessor.onChildActivating (:129-158) -> setLoopVariables (:270-305): the item at
+  // loopCounter - 1 as the inputElement (if any), then loopCounter, local to the inner instance
+  void on_child_activating(const OEl& body, int64_t key, const PiValue& v) {
+    const int loop = ei_.at(key).loopCounter;
+    if (loop < 1 || loop > (int)body.mi_items.size()) throw Unsupported{"loop counter past the input collection (incident)"};
+    const auto& item = body.mi_items[loop - 1];
+    if (body.mi_input_id >= 0) set_local_inline(key, v.proc, v.piKey, body.mi_input_id, item.first, item.second);
+    set_local_inline(key, v.proc, v.piKey, body.mi_loop_id, ZBHIP_DOC_INT, loop);
+  }
+
+  // VariableBehavior.setLocalVariable (VariableBehavior.java:191-200) of a value the engine computed
+  // (not a command document entry): the record carries it inline (zbhip_record.aux = ZBHIP_AUX_INLINE)
+  void set_local_inline(int64_t scopeKey, int proc, int64_t piKey, int name, uint8_t type, int64_t value) {
+    auto it = vars_.find({scopeKey, name});
+    int64_t key;
+    int intent;
+    if (it == vars_.end()) {
+      key = next_key();
+      intent = ZBHIP_VAR_CREATED;
+    } else if (!(it->second.type == type && it->second.value == value)) {
+      key = it->second.key;
+      intent = ZBHIP_VAR_UPDATED;
+    } else {
+      return;
+    }
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_VARIABLE, intent, key);
+    rec.r.process_idx = proc;
+    rec.r.element_idx = name;
+    rec.r.scope_key = scopeKey;
+    rec.r.process_instance_key = piKey;
+    rec.r.aux = ZBHIP_AUX_INLINE;
+    rec.r.message_key = value;
+    rec.r.partition = type;
+    vars_[{scopeKey, name}] = VarRow{key, type, value, UINT32_MAX};
+  }
+
   // ---------------------------------------------------------------------
   // BpmnStreamProcessor.processRecord (processing/bpmn/BpmnStreamProcessor.java:74-162)
   // ---------------------------------------------------------------------
@@ -1947,7 +2125,10 @@ class Oracle {
       if (ei_.count(cmd.r.key)) throw Unsupported{"re-activation (incident resolution)"};
       int64_t key = cmd.r.key == -1 ? next_key() : cmd.r.key;
       pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATING, cmd.pi);
-      // onElementActivating -> container.onChildActivating: ProcessProcessor default (right)
+      // onElementActivating -> container.onChildActivating: ProcessProcessor / SubProcessProcessor
+      // default (right); a multi-instance body sets the inner instance's loop variables
+      if (el.scope > 0 && P(cmd.pi.proc).els[el.scope].type == ZBHIP_EL_MULTI_INSTANCE_BODY)
+        on_child_activating(P(cmd.pi.proc).els[el.scope], key, cmd.pi);
       on_activate(el, key, cmd.pi);
     } else if (cmd.r.intent == ZBHIP_PI_COMPLETE_ELEMENT) {
       // transitionToCompleting (:116-130)
@@ -2073,6 +2254,34 @@ class Oracle {
         pi_command(-1, ZBHIP_PI_ACTIVATE_ELEMENT, c);
         break;
       }
+      case ZBHIP_EL_MULTI_INSTANCE_BODY: {
+        // MultiInstanceBodyProcessor.onActivate (processing/bpmn/container/MultiInstanceBodyProcessor.java:83-98):
+        // the static inputCollection always evaluates, no event subscriptions; activate (:229-252):
+        // ACTIVATED, then an empty collection completes the body, a sequential body activates its
+        // first inner instance (activateChildInstanceWithKey, BpmnStateTransitionBehavior.java:292-307),
+        // a parallel one writes PROCESS_INSTANCE_BATCH:ACTIVATE (activateChildInstancesInBatches :315-324)
+        pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+        if (el.mi_items.empty()) {
+          pi_command(key, ZBHIP_PI_COMPLETE_ELEMENT, v);
+          break;
+        }
+        PiValue c = v;
+        c.flowScopeKey = key;
+        c.elem = el.inner;
+        if (el.mi_seq) {
+          pi_command(next_key(), ZBHIP_PI_ACTIVATE_ELEMENT, c);
+        } else {
+          const int64_t bk = next_key();
+          ORecord& rec = append(ZBHIP_RT_COMMAND, ZBHIP_VT_PROCESS_INSTANCE_BATCH, ZBHIP_PIB_ACTIVATE, bk);
+          rec.r.process_idx = v.proc;
+          rec.r.element_idx = v.elem;
+          rec.r.scope_key = key;  // batchElementInstanceKey
+          rec.r.process_instance_key = v.piKey;
+          rec.r.aux = (int64_t)el.mi_items.size();  // index: the children to activate
+          rec.pi = v;
+        }
+        break;
+      }
       case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onActivate (processing/bpmn/event/StartEventProcessor.java:45-50)
       case ZBHIP_EL_TASK:         // UndefinedTaskProcessor.onActivate (processing/bpmn/task/UndefinedTaskProcessor.java:37-42)
       case ZBHIP_EL_MANUAL_TASK:  // ManualTaskProcessor extends UndefinedTaskProcessor
@@ -2165,6 +2374,11 @@ class Oracle {
       case ZBHIP_EL_MANUAL_TASK:
         complete_and_take(el, key, v, false);
         break;
+      case ZBHIP_EL_MULTI_INSTANCE_BODY:
+        // MultiInstanceBodyProcessor.onComplete (:100-114): unsubscribeFromEvents (none), no output
+        // collection to propagate, transitionToCompleted, takeOutgoingSequenceFlows
+        complete_and_take(el, key, v, false);
+        break;
       case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT: {
         // IntermediateCatchEventProcessor.onComplete: applyOutputMappings, unsubscribeFromEvents
         // (CatchEventBehavior.unsubscribeFromMessageEvents visits the element's remaining process
@@ -2253,7 +2467,21 @@ class Oracle {
     if (end_of_path) {
       // ProcessProcessor.afterExecutionPathCompleted (:130-140) -> BpmnStateBehavior.canBeCompleted (behavior/BpmnStateBehavior.java:76-95)
       auto fit = ei_.find(v.flowScopeKey);
-      if (fit != ei_.end()) {
+      if (fit != ei_.end() && E(fit->second.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+        // MultiInstanceBodyProcessor.beforeExecutionPathCompleted (:160-191): no output collection, no
+        // completion condition (false); afterExecutionPathCompleted (:193-230): a sequential body
+        // creates its next inner instance while items are left, else completes once no child is active
+        const ElementInstance& body = fit->second;
+        const OEl& b = E(body.value);
+        if (b.mi_seq && body.loopCounter < (int)b.mi_items.size()) {
+          PiValue c = body.value;
+          c.flowScopeKey = body.key;
+          c.elem = b.inner;
+          pi_command(next_key(), ZBHIP_PI_ACTIVATE_ELEMENT, c);
+        } else if ((int64_t)body.childCount + body.activeSequenceFlows == 0) {
+          pi_command(body.key, ZBHIP_PI_COMPLETE_ELEMENT, body.value);
+        }
+      } else if (fit != ei_.end()) {
         const ElementInstance& fs = fit->second;
         if ((int64_t)fs.childCount + fs.activeSequenceFlows == 0) {
           pi_command(fs.key, ZBHIP_PI_COMPLETE_ELEMENT, fs.value);
@@ -2387,6 +2615,13 @@ class Oracle {
           inst.parentKey = fit->second.key;
           fit->second.childCount += 1;
         }
+        if (fit != ei_.end() && E(fit->second.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+          // manageMultiInstance (:237-253): the body's loop counter and childActivatedCount, the
+          // inner instance's loop counter
+          fit->second.loopCounter += 1;
+          fit->second.childActivated += 1;
+          inst.loopCounter = fit->second.loopCounter;
+        }
         ei_[key] = inst;
         parent_child_.insert({inst.parentKey, key});
         child_parent_[key] = inst.parentKey;  // DbVariableState.createScope
@@ -2437,7 +2672,14 @@ class Oracle {
         for (auto tit = taken_.lower_bound({key, INT32_MIN, INT32_MIN}); tit != taken_.end() && std::get<0>(tit->first) == key;)
           tit = taken_.erase(tit);
         if (el.type == ZBHIP_EL_PROCESS) pi_by_def_.erase({P(v.proc).def_key, key});
-        if (parent > 0) ei_.at(parent).childCount -= 1;
+        if (parent > 0) {
+          ElementInstance& pe = ei_.at(parent);
+          pe.childCount -= 1;
+          if (E(pe.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {  // manageMultiInstance (Completed :104-110)
+            if (intent == ZBHIP_PI_ELEMENT_TERMINATED) throw Unsupported{"terminated multi-instance child"};
+            pe.childCompleted += 1;
+          }
+        }
         break;
       }
       case ZBHIP_PI_SEQUENCE_FLOW_TAKEN: {  // ProcessInstanceSequenceFlowTakenApplier (:32-69)
@@ -2462,11 +2704,12 @@ std::string Oracle::dump_state() const {
   for (auto& [k, e] : ei_) {
     const OEl& el = procs[e.value.proc].els[e.value.elem];
     snprintf(buf, sizeof buf,
-             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%d,childActivatedCount=0,childCompletedCount=0,"
-             "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=0,interruptingElementId=,"
+             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%d,childActivatedCount=%d,childCompletedCount=%d,"
+             "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=%d,interruptingElementId=,"
              "calledChildInstanceKey=-1,state=%d,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
              "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%d",
-             (long long)k, (long long)e.parentKey, e.childCount, (long long)e.jobKey, e.state, el.id.c_str(), el.type,
+             (long long)k, (long long)e.parentKey, e.childCount, e.childActivated, e.childCompleted,
+             (long long)e.jobKey, e.loopCounter, e.state, el.id.c_str(), el.type,
              el.event, (long long)e.value.flowScopeKey, (long long)e.value.piKey,
              (long long)procs[e.value.proc].def_key, e.activeSequenceFlows);
     rows.push_back(buf);
@@ -2692,7 +2935,7 @@ int zbo_activate_jobs(void* o, const char* type, const char* worker, int64_t tim
     j.element_idx = got[i].elem;
     j.retries = (uint16_t)got[i].retries;
     j.n_variables = (uint16_t)got[i].vars.size();
-    for (size_t v = 0; v < got[i].vars.size() && v < 4; ++v) {
+    for (size_t v = 0; v < got[i].vars.size() && v < 6; ++v) {
       j.variables[v].name_id = (uint32_t)got[i].vars[v].first;
       j.variables[v].type = got[i].vars[v].second.type;
       j.variables[v].value = got[i].vars[v].second.value;

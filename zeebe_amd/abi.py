@@ -18,6 +18,7 @@ VT_VARIABLE = 17
 VT_PROCESS_INSTANCE_CREATION = 19
 VT_PROCESS_EVENT = 24
 VT_TIMER = 15
+VT_PROCESS_INSTANCE_BATCH = 34
 
 REJ_INVALID_ARGUMENT, REJ_NOT_FOUND, REJ_ALREADY_EXISTS, REJ_INVALID_STATE = 0, 1, 2, 3
 REJ_PROCESSING_ERROR, REJ_NONE = 4, 255
@@ -35,6 +36,9 @@ VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
 PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
 PIC_INTENTS = {0: "CREATE", 1: "CREATED"}
 TIMER_INTENTS = {0: "CREATED", 1: "TRIGGER", 2: "TRIGGERED", 3: "CANCEL", 4: "CANCELED"}
+PIB_INTENTS = {0: "TERMINATE", 1: "ACTIVATE"}
+PIB_ACTIVATE = 1
+AUX_INLINE = -2  # VARIABLE record with its value inline (message_key, doc type in partition)
 TIMER_CREATED, TIMER_TRIGGER, TIMER_TRIGGERED, TIMER_CANCELED = 0, 1, 2, 4
 PE_TRIGGERING, PE_TRIGGERED = 0, 1
 # MessageIntent / MessageSubscriptionIntent / ProcessMessageSubscriptionIntent
@@ -65,7 +69,7 @@ def intent_name(value_type, intent):
     table = {VT_PROCESS_INSTANCE: PI_INTENTS, VT_JOB: JOB_INTENTS, VT_VARIABLE: VAR_INTENTS,
              VT_PROCESS_EVENT: PE_INTENTS, VT_PROCESS_INSTANCE_CREATION: PIC_INTENTS, VT_MESSAGE: MSG_INTENTS,
              VT_MESSAGE_SUBSCRIPTION: MS_INTENTS, VT_PROCESS_MESSAGE_SUBSCRIPTION: PMS_INTENTS,
-             VT_TIMER: TIMER_INTENTS}.get(value_type, {})
+             VT_TIMER: TIMER_INTENTS, VT_PROCESS_INSTANCE_BATCH: PIB_INTENTS}.get(value_type, {})
     return table.get(intent, str(intent))
 
 
@@ -157,7 +161,7 @@ DOC_DTYPE = np.dtype([("name_id", "<u4"), ("type", "u1"), ("pad", "u1", (3,)), (
 ACTIVATED_JOB_DTYPE = np.dtype([("key", "<i8"), ("element_instance_key", "<i8"), ("process_instance_key", "<i8"),
                                 ("deadline", "<i8"), ("instance", "<u4"), ("process_idx", "<i4"),
                                 ("element_idx", "<i4"), ("retries", "<u2"), ("n_variables", "<u2"),
-                                ("variables", DOC_DTYPE, (4,))])
+                                ("variables", DOC_DTYPE, (6,))])
 RECORD_DTYPE = np.dtype([("key", "<i8"), ("scope_key", "<i8"), ("process_instance_key", "<i8"),
                          ("source_index", "<i8"), ("process_idx", "<i4"), ("element_idx", "<i4"),
                          ("record_type", "u1"), ("value_type", "u1"), ("intent", "u1"),

@@ -29,6 +29,7 @@ class _Node:
         self.timer = None    # timeDuration of a timer catch event
         self.attached_to = None     # boundary event: the activity it is attached to
         self.cancel_activity = True  # boundary event: interrupting (BoundaryEvent default)
+        self.multi = None    # activity: (isSequential, inputCollection, inputElement, extra attrs)
 
 
 class ProcessBuilder:
@@ -155,6 +156,15 @@ class ProcessBuilder:
         self._pending_flow = None
         return self
 
+    def multiInstance(self, input_collection, input_element=None, sequential=False, **extra):
+        """AbstractActivityBuilder.multiInstance(b -> b.zeebeInputCollectionExpression(..)
+        .zeebeInputElement(..).sequential()/.parallel()): a <multiInstanceLoopCharacteristics> with a
+        zeebe:loopCharacteristics (MultiInstanceLoopCharacteristicsBuilder); `extra` adds attributes
+        (outputCollection, outputElement) or a completionCondition."""
+        expr = input_collection if input_collection.startswith("=") else "=" + input_collection
+        self.current.multi = (bool(sequential), expr, input_element, extra)
+        return self
+
     def cancelActivity(self, cancel):
         self.current.cancel_activity = bool(cancel)
         return self
@@ -247,8 +257,8 @@ class ProcessBuilder:
                 elif c.kind in ("serviceTask", "sendTask", "scriptTask", "businessRuleTask"):
                     retries = ' retries="%s"' % c.retries if c.retries is not None else ""
                     out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
-                               '</extensionElements></%s>' % (ind, c.kind, quoteattr(c.id), quoteattr(c.job_type), retries,
-                                                             c.kind))
+                               '</extensionElements>%s</%s>' % (ind, c.kind, quoteattr(c.id), quoteattr(c.job_type),
+                                                               retries, loop(c), c.kind))
                 elif c.kind == "intermediateCatchEvent" and c.message:
                     catches.append(c)
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
@@ -275,8 +285,26 @@ class ProcessBuilder:
                     out.append("%s<subProcess id=%s>" % (ind, quoteattr(c.id)))
                     render(c.children, ind + "  ")
                     out.append("%s</subProcess>" % ind)
+                elif c.multi:
+                    out.append("%s<%s id=%s>%s</%s>" % (ind, c.kind, quoteattr(c.id), loop(c), c.kind))
                 else:
                     out.append("%s<%s id=%s/>" % (ind, c.kind, quoteattr(c.id)))
+
+        def loop(c):
+            if not c.multi:
+                return ""
+            seq, coll, elem, extra = c.multi
+            attrs = 'inputCollection=%s' % quoteattr(coll)
+            if elem:
+                attrs += ' inputElement=%s' % quoteattr(elem)
+            for k in ("outputCollection", "outputElement"):
+                if k in extra:
+                    attrs += ' %s=%s' % (k, quoteattr(extra[k]))
+            cc = ('<completionCondition>%s</completionCondition>' % escape(extra["completionCondition"])
+                  if "completionCondition" in extra else "")
+            return ('<multiInstanceLoopCharacteristics isSequential="%s">%s<extensionElements>'
+                    '<zeebe:loopCharacteristics %s/></extensionElements></multiInstanceLoopCharacteristics>'
+                    % ("true" if seq else "false", cc, attrs))
 
         render(self.root, "    ")
         out.append("  </process>")
@@ -345,6 +373,26 @@ def message_catch_process(process_id="process", message_name="msg", correlation_
     (MessageCorrelationMultiplePartitionsTest.java:43-49 shape)."""
     return (createExecutableProcess(process_id).startEvent("start").intermediateCatchEvent(catch_id)
             .message(message_name, correlation_key).endEvent("end").done())
+
+
+def multi_instance_process(items=(10, 20, 30), sequential=False, input_element="item", process_id="process",
+                           element_id="task", job_type="task", inner="serviceTask", after=None):
+    """MultiInstanceActivityTest.process (engine/src/test/.../multiinstance/MultiInstanceActivityTest.java:
+    98-108): start -> a multi-instance activity over a static collection -> [after: a service task] ->
+    end.  `items` is the FEEL list (a sequence of ints / strings, or the literal text)."""
+    if isinstance(items, str):
+        coll = items
+    else:
+        coll = "= [" + ", ".join('"%s"' % v if isinstance(v, str) else str(v) for v in items) + "]"
+    b = createExecutableProcess(process_id).startEvent("start")
+    if inner == "serviceTask":
+        b.serviceTask(element_id, job_type)
+    else:
+        getattr(b, inner)(element_id)
+    b.multiInstance(coll, input_element, sequential)
+    if after:
+        b.serviceTask(after, after)
+    return b.endEvent("end").done()
 
 
 def job_types_of(xml):
