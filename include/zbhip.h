@@ -420,14 +420,15 @@ typedef struct zbhip_record {
   uint8_t reason_arg;           /* e.g. the offending element-instance state */
   int64_t aux;                  /* VARIABLE: document entry index, or ZBHIP_AUX_INLINE (the value in
                                    message_key, its zbhip_doc_type in partition: multi-instance
-                                   loopCounter / input element); JOB:COMPLETED: source doc;
-                                   PROCESS_INSTANCE_BATCH: index (children still to activate); else -1 */
+                                   loopCounter / input element); JOB:COMPLETED: source doc; else -1 */
   /* message value fields (MESSAGE / MESSAGE_SUBSCRIPTION / PROCESS_MESSAGE_SUBSCRIPTION) */
   int64_t message_key;          /* messageKey, -1 unset */
   uint32_t correlation_key;     /* string id, ZBHIP_NO_STRING = empty */
   uint16_t message_name;        /* name id, 0xFFFF = empty */
   uint16_t bpmn_process_id;     /* name id, 0xFFFF = empty */
-  int32_t partition;            /* PMS: subscriptionPartitionId; TIMER events: repetitions (-1 infinite); else 0 */
+  int32_t partition;            /* PMS: subscriptionPartitionId; TIMER events: repetitions (-1 infinite);
+                                   PROCESS_INSTANCE_BATCH: index (the children still to activate);
+                                   VARIABLE with aux == ZBHIP_AUX_INLINE: the value's zbhip_doc_type; else 0 */
   uint8_t interrupting;
   uint8_t unprocessed;          /* a follow-up COMMAND written to the log unprocessed (past
                                    maxCommandsInBatch, ProcessingStateMachine.java:388-417): it

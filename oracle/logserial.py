@@ -181,6 +181,10 @@ TIMER = [
     ("elementInstanceKey", "long", NO_DEFAULT), ("processInstanceKey", "long", NO_DEFAULT),
     ("dueDate", "long", NO_DEFAULT), ("targetElementId", "str", NO_DEFAULT), ("repetitions", "int", NO_DEFAULT),
     ("processDefinitionKey", "long", NO_DEFAULT), ("tenantId", "str", "<default>")]
+# ProcessInstanceBatchRecord.java:18-40 (no tenantId)
+PROCESS_INSTANCE_BATCH = [
+    ("processInstanceKey", "long", NO_DEFAULT), ("batchElementInstanceKey", "long", NO_DEFAULT),
+    ("index", "long", -1)]
 # ProcessInstanceCreationRecord.java:32-55 (ArrayProperty is always set, ArrayProperty.java)
 PROCESS_INSTANCE_CREATION = [
     ("bpmnProcessId", "str", ""), ("processDefinitionKey", "long", -1), ("processInstanceKey", "long", -1),
@@ -291,6 +295,8 @@ RT_EVENT, RT_COMMAND, RT_REJECTION = 0, 1, 2
 VT_JOB, VT_PI, VT_VARIABLE, VT_PIC, VT_PE = 0, 5, 17, 19, 24
 VT_MESSAGE, VT_MS, VT_PMS = 10, 11, 12
 VT_TIMER = 15
+VT_PIB = 34
+AUX_INLINE = -2
 NO_STRING, NO_NAME = 0xFFFFFFFF, 0xFFFF
 
 
@@ -350,7 +356,10 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
             fields["variables"] = src_doc
         return write_object(JOB, fields)
     if vt == VT_VARIABLE:
-        e = doc_entry(int(r["aux"]))
+        if int(r["aux"]) == AUX_INLINE:  # a value the engine computed (multi-instance loop variables)
+            e = {"name_id": int(r["element_idx"]), "type": int(r["partition"]), "value": int(r["message_key"])}
+        else:
+            e = doc_entry(int(r["aux"]))
         return write_object(VARIABLE, dict(name=tables.name(int(r["element_idx"])),
                                            value=value_bytes(e, tables.string_value), scopeKey=int(r["scope_key"]),
                                            processInstanceKey=int(r["process_instance_key"]),
@@ -368,6 +377,10 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
                                         processInstanceKey=int(r["process_instance_key"]), dueDate=int(r["aux"]),
                                         targetElementId=el[2] if el is not None else "", repetitions=reps,
                                         processDefinitionKey=p["key"] if p is not None else -1))
+    if vt == VT_PIB:
+        return write_object(PROCESS_INSTANCE_BATCH, dict(processInstanceKey=int(r["process_instance_key"]),
+                                                         batchElementInstanceKey=int(r["scope_key"]),
+                                                         index=int(r["partition"])))
     if vt == VT_PIC:
         return write_object(PROCESS_INSTANCE_CREATION, dict(
             bpmnProcessId=p["bpmn_process_id"], processDefinitionKey=p["key"],

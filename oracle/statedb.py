@@ -113,6 +113,9 @@ def encode_rows(rows, processes, string_value):
                                                    "processInstanceRecord": pir})
             val = LS.write_object(ELEMENT_INSTANCE, dict(
                 parentKey=int(f["parentKey"]), childCount=int(f["childCount"]), jobKey=int(f["jobKey"]),
+                childActivatedCount=int(f["childActivatedCount"]), childCompletedCount=int(f["childCompletedCount"]),
+                childTerminatedCount=int(f["childTerminatedCount"]),
+                multiInstanceLoopCounter=int(f["multiInstanceLoopCounter"]),
                 interruptingElementId=f["interruptingElementId"], calledChildInstanceKey=int(f["calledChildInstanceKey"]),
                 elementRecord=rec, activeSequenceFlows=int(f["activeSequenceFlows"])))
             out.append((CF[name], prefix + dblong(key), val))

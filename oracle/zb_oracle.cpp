@@ -1121,8 +1121,7 @@ class Oracle {
     const uint32_t base = (uint32_t)docs.size();
     docs.insert(docs.end(), d, d + nd);
     rec.doc = Doc{base, (uint32_t)nd};
-    rec.r.aux = r.value_type == ZBHIP_VT_TIMER || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH ? r.aux
-                : nd ? (int64_t)base : -1;
+    rec.r.aux = r.value_type == ZBHIP_VT_TIMER ? r.aux : nd ? (int64_t)base : -1;
     rec.pi.proc = r.process_idx;
     rec.pi.elem = r.element_idx;
     rec.pi.flowScopeKey = r.scope_key;
@@ -2071,7 +2070,7 @@ class Oracle {
     PiValue c = it->second.value;
     c.flowScopeKey = it->second.key;
     c.elem = E(it->second.value).inner;
-    for (int64_t n = cmd.r.aux; n > 0; --n) pi_command(next_key(), ZBHIP_PI_ACTIVATE_ELEMENT, c);
+    for (int32_t n = cmd.r.partition; n > 0; --n) pi_command(next_key(), ZBHIP_PI_ACTIVATE_ELEMENT, c);
   }
 
   // MultiInstanceBodyProcessor.onChildActivating (:129-158) -> setLoopVariables (:270-305): the item at
@@ -2277,7 +2276,7 @@ class Oracle {
           rec.r.element_idx = v.elem;
           rec.r.scope_key = key;  // batchElementInstanceKey
           rec.r.process_instance_key = v.piKey;
-          rec.r.aux = (int64_t)el.mi_items.size();  // index: the children to activate
+          rec.r.partition = (int32_t)el.mi_items.size();  // index: the children to activate
           rec.pi = v;
         }
         break;

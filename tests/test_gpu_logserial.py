@@ -42,7 +42,7 @@ class Pair:
         first = int(pos[-1]) + 1
         got = self.ser.serialize(got_recs, cmds, docs, self.source_base, self.doc_base, pos, first, TS)
         names = self.orc.names()
-        tables = LS.Tables(self.orc.process_tables(), lambda i: names[i], lambda i: b"")
+        tables = LS.Tables(self.orc.process_tables(), lambda i: names[i], self.orc.string_value)
         sb, db = self.source_base, self.doc_base
 
         def docs_of_source(si):

@@ -157,7 +157,11 @@ def check_entries(buf, recs, first, pos, sb):
         rt, vt, intent = struct.unpack_from("<B", e, 48)[0], e[40 + 8 + 15], e[40 + 8 + 16]
         assert (rt, vt, intent) == (r["record_type"], r["value_type"], r["intent"])
         value = msgpack.unpackb(e[40 + mlen:], raw=False)
-        assert value["tenantId"] == "<default>"
+        if r["value_type"] == abi.VT_PROCESS_INSTANCE_BATCH:  # ProcessInstanceBatchRecord: no tenantId
+            assert value == {"processInstanceKey": r["process_instance_key"],
+                             "batchElementInstanceKey": r["scope_key"], "index": r["partition"]}
+        else:
+            assert value["tenantId"] == "<default>"
         if r["value_type"] == abi.VT_PROCESS_INSTANCE:
             assert value["processInstanceKey"] == r["process_instance_key"]
             assert value["flowScopeKey"] == r["scope_key"]

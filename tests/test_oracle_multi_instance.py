@@ -197,7 +197,7 @@ def test_parallel_batch_command_and_counters():
     body_key = int([r for r in recs if r["value_type"] == abi.VT_PROCESS_INSTANCE and
                     r["intent"] == abi.PI_INTENT_IDS["ELEMENT_ACTIVATED"] and
                     o.element_type(0, int(r["element_idx"])) == abi.ELEMENT_TYPES.index("MULTI_INSTANCE_BODY")][0]["key"])
-    assert int(pib[0]["scope_key"]) == body_key and int(pib[0]["aux"]) == 3
+    assert int(pib[0]["scope_key"]) == body_key and int(pib[0]["partition"]) == 3
     i = list(recs).index(pib[0])
     acts = [r for r in recs[i + 1:] if r["record_type"] == abi.RT_COMMAND and r["value_type"] == abi.VT_PROCESS_INSTANCE]
     assert [int(r["key"]) for r in acts[:3]] == [int(pib[0]["key"]) + 1 + k for k in range(3)]
@@ -247,3 +247,27 @@ def test_undefined_task_inner(seq):
     t = _types(o, recs, "task")
     assert t.count(("TASK", "ELEMENT_COMPLETED")) == 3 and t[-1] == ("MULTI_INSTANCE_BODY", "ELEMENT_COMPLETED")
     assert o.state() == ["KEY|latestKey|%d" % (BASE + o.key_counter())]
+
+
+def test_zb_db_round_trip():
+    # the state rows of waiting multi-instance bodies / inner instances (counters, loop variables
+    # with an interned string item) through the product's zb-db encoder and decoder (host code)
+    from zeebe_amd.logwriter import LogSerializer
+    xml = bpmn.multi_instance_process((10, "twenty", 30), after="after")
+    o = Oracle()
+    o.deploy(xml)
+    _run(o, create_commands(2))
+    rows = sorted(r for r in o.state() if not r.startswith("KEY|"))
+    assert any("bpmnElementType=19," in r and "childActivatedCount=3" in r for r in rows)
+    s = LogSerializer()
+    s.deploy(xml)
+    for n in o.names():
+        s.intern(n)
+    for v in o.strings():
+        s.intern_string(v)
+    back = s.decode_state_entries(s.encode_state_rows(rows), intern=lambda b: s.intern_string(b))
+    assert back == rows
+    # and the product encoder's bytes are oracle/statedb.py's
+    from oracle import statedb as SD
+    strings = o.strings()
+    assert s.encode_state_rows(rows) == SD.encode_rows(rows, o.process_tables(), lambda i: strings[i])

@@ -383,7 +383,9 @@ def multi_instance_process(items=(10, 20, 30), sequential=False, input_element="
     if isinstance(items, str):
         coll = items
     else:
-        coll = "= [" + ", ".join('"%s"' % v if isinstance(v, str) else str(v) for v in items) + "]"
+        lit = lambda v: ('"%s"' % v if isinstance(v, str) else "null" if v is None  # noqa: E731
+                         else ("true" if v else "false") if isinstance(v, bool) else str(v))
+        coll = "= [" + ", ".join(lit(v) for v in items) + "]"
     b = createExecutableProcess(process_id).startEvent("start")
     if inner == "serviceTask":
         b.serviceTask(element_id, job_type)

@@ -390,6 +390,85 @@ static int64_t duration_ms(const std::string& text) {
   return any ? ms : -1;
 }
 
+// A multi-instance activity's loop characteristics (MultiInstanceActivityTransformer
+// .transformLoopCharacteristics, deployment/model/transformer/MultiInstanceActivityTransformer.java:
+// 80-122) in the subset: the inputCollection a static FEEL list literal of integer, string, boolean and
+// null items (FeelToMessagePackTransformer writes a whole number as a msgpack integer), an optional
+// inputElement; a completionCondition, outputCollection or outputElement is outside it.
+struct MiItem { uint8_t type; int64_t value; std::string text; };
+static bool parse_loop(const Elem& mil, bool& seq, std::string& input, std::vector<MiItem>& items, std::string& err) {
+  const std::string* sq = mil.get("isSequential");
+  seq = sq && *sq == "true";
+  if (const Elem* cc = mil.first("completionCondition"))
+    if (cc->text.find_first_not_of(" \t\r\n") != std::string::npos) {
+      err = "multi-instance completionCondition outside the supported subset";
+      return false;
+    }
+  const Elem* ext = mil.first("extensionElements");
+  const Elem* lc = ext ? ext->first("loopCharacteristics") : nullptr;
+  if (!lc) { err = "multi-instance without zeebe:loopCharacteristics"; return false; }
+  const std::string* oc = lc->get("outputCollection");
+  const std::string* oe = lc->get("outputElement");
+  if ((oc && !oc->empty()) || (oe && !oe->empty())) {
+    err = "multi-instance outputCollection / outputElement outside the supported subset";
+    return false;
+  }
+  const std::string* ie = lc->get("inputElement");
+  input = ie ? *ie : "";
+  const std::string* ic = lc->get("inputCollection");
+  const std::string t = ic ? *ic : "";
+  auto bad = [&]() { err = "multi-instance inputCollection outside the supported subset (a static list): " + t; return false; };
+  size_t i = t.find_first_not_of(" \t\r\n");
+  auto ws = [&]() { while (i < t.size() && isspace((unsigned char)t[i])) ++i; };
+  if (i == std::string::npos || t[i] != '=') return bad();
+  ++i;
+  ws();
+  if (i >= t.size() || t[i] != '[') return bad();
+  ++i;
+  ws();
+  if (i < t.size() && t[i] == ']') {
+    ++i;
+  } else {
+    for (;;) {
+      ws();
+      if (i >= t.size()) return bad();
+      MiItem it{ZBHIP_DOC_INT, 0, ""};
+      if (t[i] == '"') {
+        const size_t e = t.find('"', i + 1);
+        if (e == std::string::npos) return bad();
+        it.type = ZBHIP_DOC_STR;
+        it.text = t.substr(i + 1, e - i - 1);
+        if (it.text.find('\\') != std::string::npos) return bad();
+        i = e + 1;
+      } else if (t.compare(i, 4, "true") == 0 || t.compare(i, 4, "null") == 0 || t.compare(i, 5, "false") == 0) {
+        it.type = t[i] == 'n' ? ZBHIP_DOC_NIL : ZBHIP_DOC_BOOL;
+        it.value = t[i] == 't';
+        i += t[i] == 'f' ? 5 : 4;
+      } else {
+        const bool neg = t[i] == '-';
+        if (neg) ++i;
+        const size_t s0 = i;
+        unsigned long long v = 0;
+        for (; i < t.size() && isdigit((unsigned char)t[i]); ++i) {
+          if (v > 922337203685477580ULL) return bad();
+          v = v * 10 + (unsigned)(t[i] - '0');
+        }
+        if (i == s0 || v > 9223372036854775807ULL || (i < t.size() && (t[i] == '.' || isalpha((unsigned char)t[i]))))
+          return bad();
+        it.value = neg ? -(int64_t)v : (int64_t)v;
+      }
+      items.push_back(it);
+      ws();
+      if (i < t.size() && t[i] == ',') { ++i; continue; }
+      if (i < t.size() && t[i] == ']') { ++i; break; }
+      return bad();
+    }
+  }
+  ws();
+  if (i != t.size() || items.size() > 65535) return bad();
+  return true;
+}
+
 static zbhip_element blank(uint8_t type, uint16_t id) {
   zbhip_element e{};
   e.element_type = type;
@@ -456,6 +535,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
   std::vector<std::vector<uint16_t>> out_lists, in_lists;
   std::vector<const Elem*> xgws;
   std::vector<std::pair<uint16_t, std::string>> boundaries;  // (boundary event, attachedToRef)
+  std::vector<std::pair<uint16_t, std::vector<MiItem>>> collections;  // (multi-instance body, its items)
 
   // Elements in document pre-order: an embedded sub-process, then its children, then its next
   // sibling (the oracle numbers them the same way).  Every sequence flow connects two nodes of one
@@ -623,6 +703,32 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       if (type == ZBHIP_EL_SEQUENCE_FLOW) flows.push_back(&c);
       if (type == ZBHIP_EL_EXCLUSIVE_GATEWAY) xgws.push_back(&c);
       if (index.count(*id)) { err = "duplicate element id " + *id; return ZBHIP_EPARSE; }
+      if (c.first("standardLoopCharacteristics")) { err = "standard loops outside the supported subset"; return ZBHIP_EUNSUPP; }
+      if (const Elem* mil = c.first("multiInstanceLoopCharacteristics")) {
+        // MultiInstanceActivityTransformer.transform (:35-78): the body takes the activity's id, flow
+        // scope and sequence flows (its index answers the id); the inner activity follows it, its flow
+        // scope the body
+        if (!ZBHIP_IS_JOB_WORKER(type) && type != ZBHIP_EL_TASK && type != ZBHIP_EL_MANUAL_TASK) {
+          err = "multi-instance <" + c.tag + "> outside the supported subset (job worker and undefined tasks)";
+          return ZBHIP_EUNSUPP;
+        }
+        bool seq = false;
+        std::string input;
+        std::vector<MiItem> items;
+        if (!parse_loop(*mil, seq, input, items, err)) return ZBHIP_EUNSUPP;
+        zbhip_element b = blank(ZBHIP_EL_MULTI_INSTANCE_BODY, e.id);
+        b.flow_scope = scope;
+        b.job_retries = seq ? 1 : 0;
+        b.message_name = input.empty() ? ZBHIP_NONE16 : C.str(input);
+        const uint16_t bi = (uint16_t)C.elements.size();
+        b.start_event = (uint16_t)(bi + 1);
+        index[*id] = bi;
+        C.elements.push_back(b);
+        collections.push_back({bi, std::move(items)});
+        e.flow_scope = bi;
+        C.elements.push_back(e);
+        continue;
+      }
       const uint16_t self = (uint16_t)C.elements.size();
       index[*id] = self;
       C.elements.push_back(e);
@@ -697,6 +803,21 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     }
     out_lists[fe.flow_source].push_back(fi);
     in_lists[fe.flow_target].push_back(fi);
+  }
+  // the bodies' inputCollections after the flows' conditions (condition indices of flows unchanged)
+  for (auto& [b, items] : collections) {
+    C.elements[b].condition = (uint16_t)(C.cond_begin.size() - 1);
+    for (const MiItem& it : items) {
+      zbhip_insn in{};
+      in.op = ZBHIP_OP_ITEM;
+      in.arg = it.type;
+      in.literal = it.type == ZBHIP_DOC_STR ? (int64_t)C.str(it.text) : it.value;
+      C.code.push_back(in);
+    }
+    zbhip_insn end{};
+    end.op = ZBHIP_OP_END;
+    C.code.push_back(end);
+    C.cond_begin.push_back((uint32_t)C.code.size());
   }
   // CSR of outgoing lists
   for (size_t e = 0; e < C.elements.size(); ++e) {

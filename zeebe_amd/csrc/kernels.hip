@@ -496,7 +496,10 @@ __device__ __forceinline__ void scope_adjust(Lane<K>& L, uint32_t c, int dc, int
   if (t < 0) { set_fail(L, FB_UNSUPPORTED); return; }
   uint2 e = tget(L, t);
   const int child = (int)(e.y & 0xFF) + dc;
-  int asf = (int)((e.y >> 8) & 0xFF) + da;
+  // a multi-instance body's second byte is its loop counter: its inner instances take no sequence
+  // flows, so its activeSequenceFlows stays 0 (the activation's decrement clamps at 0)
+  const bool mi = etype(elem_of(L, c)) == ZBHIP_EL_MULTI_INSTANCE_BODY;
+  int asf = mi ? (int)((e.y >> 8) & 0xFF) : (int)((e.y >> 8) & 0xFF) + da;
   if (asf < 0) asf = 0;
   if (child < 0 || child > 255 || asf > 255) { set_fail(L, FB_TABLE); return; }
   e.y = (e.y & 0xFFFF0000u) | (uint32_t)child | ((uint32_t)asf << 8);
@@ -697,15 +700,30 @@ __device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem
     }
   }
   if constexpr (K::S) {
-    // a second active instance of one sub-process element: outside the device subset
-    if (type == ZBHIP_EL_SUB_PROCESS && scope_find(L, elem) >= 0) { set_fail(L, FB_UNSUPPORTED); return; }
+    // a second active instance of one container element: outside the device subset
+    const bool container = type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_MULTI_INSTANCE_BODY;
+    if (container && scope_find(L, elem) >= 0) { set_fail(L, FB_UNSUPPORTED); return; }
     const int t = tbl_insert(L, elem, key, ZBHIP_PI_ELEMENT_ACTIVATING);
     if (t < 0) return;
-    if (type == ZBHIP_EL_SUB_PROCESS)  // jobKey 0; no children, no active flows yet
+    if (container)  // jobKey 0; no children, no active flows (a body: loop counter 0) yet
       tput(L, t, make_uint2(elem | (key << 16), (uint32_t)ZBHIP_PI_ELEMENT_ACTIVATING << 16));
     const int da = type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_BOUNDARY_EVENT ? 0
                    : type == ZBHIP_EL_PARALLEL_GATEWAY ? -(int)(w.x >> 16) : -1;
-    scope_adjust(L, scope_of<K>(w), 1, da);
+    const uint32_t c = scope_of<K>(w);
+    scope_adjust(L, c, 1, da);
+    if (c != 0 && !L.fail && etype(elem_of(L, c)) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      // manageMultiInstance (ProcessInstanceElementActivatingApplier.java:237-253): the body's loop
+      // counter (= childActivatedCount) + 1, the inner instance's loop counter set to it
+      const int tb = scope_find(L, c);
+      uint2 b = tget(L, tb);
+      const uint32_t loop = ((b.y >> 8) & 0xFF) + 1;
+      if (loop > 63) { set_fail(L, FB_UNSUPPORTED); return; }
+      b.y = (b.y & 0xFFFF00FFu) | (loop << 8);
+      tput(L, tb, b);
+      uint2 e = tget(L, t);
+      e.y = (e.y & 0x03FFFFFFu) | (loop << 26);
+      tput(L, t, e);
+    }
     return;
   }
   tbl_insert(L, elem, key, ZBHIP_PI_ELEMENT_ACTIVATING);
@@ -772,8 +790,25 @@ __device__ __forceinline__ void transition_to_completed_child(Lane<K>& L, int t,
         follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0, true, false, 0);
       }
     } else if constexpr (K::S) {
-      // SubProcessProcessor.afterExecutionPathCompleted (:97-106): completeElement(flow scope)
       const int ts = scope_find(L, c);
+      const uint4 cw = elem_of(L, c);
+      if (etype(cw) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+        // MultiInstanceBodyProcessor.beforeExecutionPathCompleted (:160-191): no output collection, no
+        // completion condition; afterExecutionPathCompleted (:193-230): a sequential body activates its
+        // next inner instance while items are left, else the body completes once no child is active
+        if (ts < 0) { set_fail(L, FB_UNSUPPORTED); return; }
+        const uint2 be = tget(L, ts);
+        const uint32_t sk = be.x >> 16, loop = (be.y >> 8) & 0xFF;
+        if (((cw.z >> 20) & 1u) && loop < ((cw.z >> 12) & 0xFF)) {
+          const uint32_t k = new_key(L);  // createInnerInstance -> activateChildInstanceWithKey
+          follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, sk, cw.z & 0xFFF, false, false, k);
+        } else if ((be.y & 0xFF) == 0) {
+          const uint32_t pc = scope_of<K>(cw);
+          follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, sk, scope_key(L, pc), c, true, pc == 0, sk);
+        }
+        return;
+      }
+      // SubProcessProcessor.afterExecutionPathCompleted (:97-106): completeElement(flow scope)
       if (ts >= 0 && (tget(L, ts).y & 0xFFFF) == 0) {
         const uint32_t sk = tget(L, ts).x >> 16;
         const uint32_t pc = scope_of<K>(elem_of(L, c));
@@ -1213,6 +1248,21 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
   activate_triggered_event(L, pe, key, target, fsa);
 }
 
+// ActivateProcessInstanceBatchProcessor.processRecord (processing/processinstance/
+// ActivateProcessInstanceBatchProcessor.java:44-60): an ACTIVATE_ELEMENT of the inner activity per
+// child still to activate, each with a new key, flow scope = the body (createChildInstanceRecord
+// :62-84); never split into a follow-up batch command at these record sizes (canWriteCommands)
+template <class K>
+__device__ __forceinline__ void activate_batch(Lane<K>& L, uint32_t body, uint4 w) {
+  const int tb = scope_find(L, body);
+  if (tb < 0) { set_fail(L, FB_UNSUPPORTED); return; }
+  const uint32_t bk = tget(L, tb).x >> 16, inner = w.z & 0xFFF, n = (w.z >> 12) & 0xFF;
+  for (uint32_t i = 0; i < n && !L.fail; ++i) {
+    const uint32_t k = new_key(L);
+    follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, bk, inner, false, false, k);
+  }
+}
+
 // ---- BpmnStreamProcessor.processRecord for one PI command ----------------------------------
 template <class K>
 __device__ __forceinline__ void reject_pi(Lane<K>& L, bool complete, uint32_t elem, uint32_t key, uint32_t aux,
@@ -1240,7 +1290,8 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       raux = fsa;
     }
     if (entry & Q_TERM) {
-      terminate_pi(L, elem, w, cmd_key, fsa);
+      if (complete) activate_batch(L, elem, w);  // PROCESS_INSTANCE_BATCH:ACTIVATE of a body
+      else terminate_pi(L, elem, w, cmd_key, fsa);
       return;
     }
   }
@@ -1285,6 +1336,26 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     apply_activating_child(L, elem, w, key);
     if (L.fail) return;
     const int t = L.nt > 0 ? tbl_find(L, key) : -1;
+    if constexpr (K::S) {
+      const uint4 bw = elem_of(L, c);
+      if (c != 0 && etype(bw) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+        // onElementActivating -> MultiInstanceBodyProcessor.onChildActivating (:129-158) ->
+        // setLoopVariables (:270-305): the item at loopCounter - 1 as the inputElement (if any), then
+        // loopCounter, local to the inner instance (VARIABLE:CREATED, values from the program)
+        const uint32_t loop = tget(L, t).y >> 26;
+        if ((bw.x >> 16) != 0xFFFFu) {
+          const uint32_t ki = new_key(L);
+          emit(L, C_MI_ITEM, ki, key, c, loop);
+        }
+        const uint32_t kl = new_key(L);
+        emit(L, C_MI_LOOP, kl, key, c, loop);
+        if (!ZBHIP_IS_JOB_WORKER(type)) {  // no job: the job field keeps the variables' key
+          uint2 e = tget(L, t);
+          e.y = (e.y & 0xFFFF0000u) | kl;
+          tput(L, t, e);
+        }
+      }
+    }
     switch (type) {
       case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onActivate (:45-50)
       case ZBHIP_EL_TASK:         // UndefinedTaskProcessor.onActivate (task/UndefinedTaskProcessor.java:37-42)
@@ -1322,7 +1393,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
         emit(L, C_JOB_CREATED, job, key, elem);
         uint2 e = tget(L, t);   // JobCreatedApplier: element instance jobKey
-        e.y = (job & 0xFFFF) | (e.y & 0x00FF0000u) | (1u << 24);
+        e.y = (job & 0xFFFF) | (e.y & 0xFCFF0000u) | (1u << 24);  // (a multi-instance loop counter stays)
         tput(L, t, e);
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
@@ -1356,6 +1427,25 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
           emit(L, C_TIMER_CREATED, tk, key, elem, 1);
           emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
           tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
+        } else {
+          set_fail(L, FB_UNSUPPORTED);
+        }
+        return;
+      case ZBHIP_EL_MULTI_INSTANCE_BODY:  // MultiInstanceBodyProcessor.onActivate (:83-98) -> activate (:229-252)
+        if constexpr (K::S) {
+          // the static inputCollection always evaluates; no event subscriptions on the body
+          emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
+          tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
+          const uint32_t n = (w.z >> 12) & 0xFF;
+          if (n == 0) {  // an empty collection: completeElement
+            follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, key, fsa, elem, true, true, key);
+          } else if ((w.z >> 20) & 1u) {  // createInnerInstance -> activateChildInstanceWithKey (:292-307)
+            const uint32_t k = new_key(L);
+            follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, key, w.z & 0xFFF, false, false, k);
+          } else {  // activateChildInstancesInBatches (:315-324): PROCESS_INSTANCE_BATCH:ACTIVATE
+            const uint32_t kb = new_key(L);
+            follow_up(L, C_PIB_ACTIVATE, kb, key, elem, true, false, kb, Q_TERM);
+          }
         } else {
           set_fail(L, FB_UNSUPPORTED);
         }
@@ -1434,14 +1524,27 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     // would be canceled (TIMER:CANCELED, outside the subset)
     if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) { set_fail(L, FB_UNSUPPORTED); return; }
   } else if (type != ZBHIP_EL_START_EVENT && !ZBHIP_IS_JOB_WORKER(type) && !pass_through(type) &&
-             !(K::S && (type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_BOUNDARY_EVENT))) {
+             !(K::S && (type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_BOUNDARY_EVENT ||
+                        type == ZBHIP_EL_MULTI_INSTANCE_BODY))) {
     // SubProcessProcessor.onComplete (:68-82): no output mappings or subscriptions in the subset;
     // BoundaryEventProcessor.onComplete (event/BoundaryEventProcessor.java:47-56): no mappings
     set_fail(L, FB_UNSUPPORTED);
     return;
   }
   // applyOutputMappings (BpmnVariableMappingBehavior.java:86-156): event-trigger variables
-  if (L.trig_key == cmd_key) merge_document_from(L, cmd_key, L.doc_begin, L.doc_count);
+  if (L.trig_key == cmd_key) {
+    if constexpr (K::S) {
+      // an inner instance's own loop variables would be updated in its scope (mergeDocument): they
+      // are not in the variable table (derived from the slot), so such a document falls back
+      const uint4 bw = elem_of(L, c);
+      if (c != 0 && L.doc_count == 1 && etype(bw) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+        const uint32_t name = L.docs[L.doc_begin].name_id;
+        vm_drain();
+        if (name == (bw.x >> 16) || name == (bw.w & 0xFFFF)) { set_fail(L, FB_DOC); return; }
+      }
+    }
+    merge_document_from(L, cmd_key, L.doc_begin, L.doc_count);
+  }
   if constexpr (K::S) {
     // JobWorkerTaskProcessor.onComplete (:63-75): unsubscribeFromEvents -- the boundary event's timer
     if (ZBHIP_IS_JOB_WORKER(type) && (L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) cancel_timer(L);
@@ -2116,6 +2219,10 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
           const int ts = scope_find(L, c);
           fs_active = ts >= 0 && ((tget(L, ts).y >> 16) & 0xFF) == ZBHIP_PI_ELEMENT_ACTIVATED;
           fsk = ts >= 0 ? tget(L, ts).x >> 16 : 0u;
+          // a multi-instance inner instance whose COMPLETE_ELEMENT would be written unprocessed
+          // would wait with jobKey -1 and no key of its loop variables left in its slot: fallback
+          if (etype(elem_of(L, c)) == ZBHIP_EL_MULTI_INSTANCE_BODY && pending(L) + L.processed + 1 >= L.limit)
+            set_fail(L, FB_BATCH_LIMIT);
         }
       }
       // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
@@ -2925,7 +3032,7 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
       if ((e.y & 0xFFFF) == ord && ((e.y >> 24) & 3u) == 1u) {
         e.y |= 2u << 24;
         st.slots[(size_t)s * st.n + inst] = e;
-        o.a = make_uint4(e.x, h.x, h.y, 1u);
+        o.a = make_uint4(e.x, h.x, h.y, e.y);  // (e.y != 0: its state; a multi-instance loop counter)
       }
     }
     for (uint32_t v = 0; v < nvars && v < (uint32_t)kVars; ++v) {

@@ -414,10 +414,18 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         break;
       case ZBHIP_VT_VARIABLE: {
         if (!P || r.element_idx < 0 || (size_t)r.element_idx >= s->names.size()) return ZBHIP_EINVAL;
-        const int64_t di = r.aux - w->doc_base;
-        if (!w->docs || di < 0 || (size_t)di >= w->n_docs) return ZBHIP_EINVAL;
         doc.clear();
-        if (!doc_value(s, w->docs[di], doc)) return ZBHIP_EUNSUPP;
+        if (r.aux == ZBHIP_AUX_INLINE) {  // a value the engine computed (multi-instance loop variables)
+          zbhip_doc_entry d{};
+          d.name_id = (uint32_t)r.element_idx;
+          d.type = (uint8_t)r.partition;
+          d.value = r.message_key;
+          if (!doc_value(s, d, doc)) return ZBHIP_EUNSUPP;
+        } else {
+          const int64_t di = r.aux - w->doc_base;
+          if (!w->docs || di < 0 || (size_t)di >= w->n_docs) return ZBHIP_EINVAL;
+          if (!doc_value(s, w->docs[di], doc)) return ZBHIP_EUNSUPP;
+        }
         mp_map(value, 7);  // VariableRecord.java:35-41
         key(value, "name"); mp_str(value, s->names[r.element_idx]);
         key(value, "value"); mp_bin(value, doc);
@@ -450,6 +458,12 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         key(value, "repetitions"); mp_int(value, r.record_type == ZBHIP_RT_REJECTION ? 1 : r.partition);
         key(value, "processDefinitionKey"); mp_int(value, P ? P->def_key : -1);
         key(value, "tenantId"); key(value, kTenant);
+        break;
+      case ZBHIP_VT_PROCESS_INSTANCE_BATCH:
+        mp_map(value, 3);  // ProcessInstanceBatchRecord.java:38-40
+        key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+        key(value, "batchElementInstanceKey"); mp_int(value, r.scope_key);
+        key(value, "index"); mp_int(value, r.partition);
         break;
       case ZBHIP_VT_PROCESS_INSTANCE_CREATION:
         if (!P) return ZBHIP_EINVAL;
@@ -984,7 +998,7 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
       const MpNode* pir = rec ? rec->get("processInstanceRecord") : nullptr;
       if (!rec || !pir) return ZBHIP_EINVAL;
       const int state = state_index(ms(rec->get("state")));
-      const int et = enum_index(element_type_name, 19, ms(pir->get("bpmnElementType")));
+      const int et = enum_index(element_type_name, 24, ms(pir->get("bpmnElementType")));
       const int ev = enum_index(event_type_name, 10, ms(pir->get("bpmnEventType")));
       if (state < 0 || et < 0 || ev < 0) return ZBHIP_EINVAL;
       snprintf(b, sizeof b,

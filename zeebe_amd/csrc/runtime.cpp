@@ -74,8 +74,28 @@ struct Proc {
   bool has_msg = false;
   bool has_timer = false;     // timer catch events (KScope, the instance timer row)
   std::vector<uint32_t> job_type_id;  // per element: id of its job type (service tasks), else ~0
+  // multi-instance bodies (ExecutableMultiInstanceBody): the inner activity, isSequential, the
+  // inputElement's name id (NONE: none), the loopCounter name id, the static inputCollection
+  // (zbhip_doc_type, value; strings as value-dictionary ids)
+  struct Mi {
+    uint16_t body, inner;
+    bool seq;
+    uint16_t input_name, loop_name;
+    std::vector<std::pair<uint8_t, int64_t>> items;
+  };
+  std::vector<Mi> mi;
+  std::vector<int16_t> mi_of;  // per element: its body's index in `mi` (the body and its inner activity), -1
+  const Mi* mi_body(uint32_t e) const { return e < mi_of.size() && mi_of[e] >= 0 ? &mi[mi_of[e]] : nullptr; }
+  // the body around inner activity e (nullptr: e is not an inner activity)
+  const Mi* mi_inner(uint32_t e) const {
+    const Mi* m = mi_body(e);
+    return m && m->inner == e ? m : nullptr;
+  }
   const std::string& id(uint32_t e) const { return strings[els[e].id]; }
 };
+// device limit of a multi-instance body: loop counters live in 6 bits of the inner instance's slot
+// (kernels.hip apply_activating_child), children in 8 bits of the body's
+constexpr size_t kMaxMiItems = 63;
 
 // Host threads a bulk host pass may use: the CPUs this process may run on (affinity mask, which
 // honours taskset / cgroup cpusets), at most 16.
@@ -620,6 +640,7 @@ const char* zbhip_string(zbhip_handle* h, uint32_t p, uint32_t s) {
 // count per node summed over the incoming flows (joins and exclusive gateways over-counted), plus the
 // initial command, the process's ACTIVATE and COMPLETE.  A cycle has no bound.
 static uint64_t batch_bound(const Proc& P) {
+  if (!P.mi.empty()) return ~0ull;  // a parallel body's children: up to its collection's size per token
   const size_t E = P.els.size();
   std::vector<uint64_t> tok(E, 0);
   std::vector<uint32_t> indeg(E, 0);
@@ -784,6 +805,13 @@ static int rebuild_program(zbhip_handle* h) {
       const uint32_t low = ZBHIP_IS_JOB_WORKER(E.element_type) ? E.start_event
                            : E.element_type == ZBHIP_EL_BOUNDARY_EVENT ? E.job_retries : E.join_slot;
       w[3] = low | ((uint32_t)E.flow_scope << 16);
+      if (const Proc::Mi* m = E.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY ? P.mi_body(e) : nullptr) {
+        // a multi-instance body: w0 high half its inputElement's name id, w2 inner activity |
+        // collection size << 12 | isSequential << 20, w3 low half the loopCounter name id
+        w[0] = E.element_type | ((uint32_t)E.event_type << 8) | ((uint32_t)m->input_name << 16);
+        w[2] = m->inner | ((uint32_t)m->items.size() << 12) | (m->seq ? 1u << 20 : 0u);
+        w[3] = m->loop_name | ((uint32_t)E.flow_scope << 16);
+      }
     }
     uint16_t* outw = reinterpret_cast<uint16_t*>(pb + out_off);
     for (size_t i = 0; i < P.out.size(); ++i) outw[i] = P.out[i];
@@ -841,7 +869,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
         e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT &&
         e.element_type != ZBHIP_EL_SUB_PROCESS && e.element_type != ZBHIP_EL_BOUNDARY_EVENT &&
-        !pass_through(e.element_type))
+        e.element_type != ZBHIP_EL_MULTI_INSTANCE_BODY && !pass_through(e.element_type))
       return ZBHIP_EUNSUPP;
   // interrupting timer boundary events: one per job worker task, in the task's container
   for (size_t e = 0; e < P.els.size(); ++e) {
@@ -856,8 +884,12 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   }
   for (size_t e = 0; e < P.els.size(); ++e) {  // containers: a sub-process element, before its children
     const zbhip_element& E = P.els[e];
-    if (e > 0 && (E.flow_scope >= e || (E.flow_scope && P.els[E.flow_scope].element_type != ZBHIP_EL_SUB_PROCESS)))
+    if (e > 0 && (E.flow_scope >= e || (E.flow_scope && P.els[E.flow_scope].element_type != ZBHIP_EL_SUB_PROCESS &&
+                                        P.els[E.flow_scope].element_type != ZBHIP_EL_MULTI_INSTANCE_BODY)))
       return ZBHIP_EINVAL;
+    if (E.flow_scope && P.els[E.flow_scope].element_type == ZBHIP_EL_MULTI_INSTANCE_BODY &&
+        P.els[E.flow_scope].start_event != e)
+      return ZBHIP_EINVAL;  // a body contains exactly its inner activity
     if (E.element_type == ZBHIP_EL_SUB_PROCESS &&
         (E.start_event >= P.els.size() || P.els[E.start_event].flow_scope != e))
       return ZBHIP_EINVAL;
@@ -871,6 +903,40 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       if (e.message_name >= P.strings.size() || e.correlation_var >= P.strings.size()) return ZBHIP_EINVAL;
       P.has_msg = true;
     }
+  // multi-instance bodies (MultiInstanceActivityTransformer): the inner activity right behind the body,
+  // a job worker (no boundary event: those attach to the body, outside the subset) or an undefined
+  // task; a static collection of at most kMaxMiItems items (ZBHIP_OP_ITEM, then ZBHIP_OP_END)
+  P.mi_of.assign(P.els.size(), -1);
+  for (size_t e = 0; e < P.els.size(); ++e) {
+    const zbhip_element& E = P.els[e];
+    if (E.element_type != ZBHIP_EL_MULTI_INSTANCE_BODY) continue;
+    if (E.start_event != e + 1 || e + 1 >= P.els.size() || e >= 0xFFF) return ZBHIP_EINVAL;
+    const zbhip_element& I = P.els[e + 1];
+    if (I.flow_scope != e || I.out_count || I.in_count) return ZBHIP_EINVAL;
+    if (!(ZBHIP_IS_JOB_WORKER(I.element_type) && I.start_event == ZBHIP_NONE16) && I.element_type != ZBHIP_EL_TASK &&
+        I.element_type != ZBHIP_EL_MANUAL_TASK)
+      return ZBHIP_EUNSUPP;
+    if (E.condition == ZBHIP_NONE16 || (size_t)E.condition + 1 >= P.cond_begin.size()) return ZBHIP_EINVAL;
+    Proc::Mi m;
+    m.body = (uint16_t)e;
+    m.inner = (uint16_t)(e + 1);
+    m.seq = E.job_retries & 1;
+    m.input_name = m.loop_name = NONE;
+    const uint32_t b0 = P.cond_begin[E.condition], b1 = P.cond_begin[E.condition + 1];
+    if (b1 <= b0 || b1 > P.code.size() || P.code[b1 - 1].op != ZBHIP_OP_END) return ZBHIP_EINVAL;
+    for (uint32_t i = b0; i + 1 < b1; ++i) {
+      const zbhip_insn& in = P.code[i];
+      if (in.op != ZBHIP_OP_ITEM) return ZBHIP_EINVAL;
+      if (in.arg != ZBHIP_DOC_INT && in.arg != ZBHIP_DOC_BOOL && in.arg != ZBHIP_DOC_NIL && in.arg != ZBHIP_DOC_STR)
+        return ZBHIP_EUNSUPP;
+      if (in.arg == ZBHIP_DOC_STR && (in.literal < 0 || (size_t)in.literal >= P.strings.size())) return ZBHIP_EINVAL;
+      m.items.push_back({(uint8_t)in.arg, in.literal});
+    }
+    if (m.items.size() > kMaxMiItems) return ZBHIP_EUNSUPP;
+    if (E.message_name != ZBHIP_NONE16 && E.message_name >= P.strings.size()) return ZBHIP_EINVAL;
+    P.mi_of[e] = P.mi_of[e + 1] = (int16_t)P.mi.size();
+    P.mi.push_back(std::move(m));
+  }
   // condition variable names -> partition name ids, interned in element order (the oracle's order)
   for (auto& e : P.els) {
     if (e.element_type != ZBHIP_EL_SEQUENCE_FLOW || e.condition == ZBHIP_NONE16) continue;
@@ -897,6 +963,26 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if (bn < 0) return ZBHIP_ENOMEM;
     P.bpmn_name = (uint16_t)bn;
   }
+  // multi-instance bodies, in element order: the inputElement and loopCounter names, then the string
+  // items into the value dictionary (the oracle's deploy order)
+  for (Proc::Mi& m : P.mi) {
+    const zbhip_element& E = P.els[m.body];
+    if (E.message_name != ZBHIP_NONE16) {
+      const int in = zbhip_intern(h, P.strings[E.message_name].c_str());
+      if (in < 0) return in;
+      m.input_name = (uint16_t)in;
+    }
+    const int ln = zbhip_intern(h, "loopCounter");
+    if (ln < 0) return ln;
+    m.loop_name = (uint16_t)ln;
+    for (auto& it : m.items)
+      if (it.first == ZBHIP_DOC_STR) {
+        const std::string& t = P.strings[(size_t)it.second];
+        const int64_t sid = zbhip_intern_string(h, t.data(), t.size());
+        if (sid < 0) return (int)sid;
+        it.second = sid;
+      }
+  }
   // kernel variant, the smallest that covers every deployed process (kernels.hip KCfg):
   //   3 KLinear  -- linear chains: every node <= 1 outgoing flow, no gateways (4 waves/SIMD)
   //   0 KSimple  -- one token per instance (no parallel gateway / multi-outgoing node but an XOR)
@@ -911,7 +997,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if (e.element_type == ZBHIP_EL_PARALLEL_GATEWAY) cls = 1;
     if (e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.out_count > 1)
       cls = 1;
-    scopes |= e.element_type == ZBHIP_EL_SUB_PROCESS;
+    scopes |= e.element_type == ZBHIP_EL_SUB_PROCESS || e.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY;
   }
   if (scopes || P.has_timer) cls = 4;  // timer catch events: KScope as well (the instance's timer row)
   if (P.has_msg) cls = 2;
@@ -1930,6 +2016,32 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       // the value comes from the batch's source document entry of that name
       for (uint32_t j = 0; j < cm.doc_count; ++j)
         if (h->h_docs[cm.doc_begin + j].name_id == elem) r.aux = h->doc_base + cm.doc_begin + j;
+    } else if (c6 == C_MI_ITEM || c6 == C_MI_LOOP) {
+      // MultiInstanceBodyProcessor.setLoopVariables: VARIABLE:CREATED in the inner instance's scope,
+      // the value inline -- the body's item at loopCounter - 1, or loopCounter itself
+      const Proc::Mi* m = proc != NONE ? h->procs[proc].mi_body(elem) : nullptr;
+      if (!m || fl < 1 || fl > m->items.size()) return ZBHIP_EDEVICE;
+      r.value_type = ZBHIP_VT_VARIABLE;
+      r.intent = ZBHIP_VAR_CREATED;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.element_idx = c6 == C_MI_ITEM ? m->input_name : m->loop_name;
+      r.aux = ZBHIP_AUX_INLINE;
+      r.partition = c6 == C_MI_ITEM ? m->items[fl - 1].first : ZBHIP_DOC_INT;
+      r.message_key = c6 == C_MI_ITEM ? m->items[fl - 1].second : (int64_t)fl;
+    } else if (c6 == C_PIB_ACTIVATE) {
+      // PROCESS_INSTANCE_BATCH:ACTIVATE (activateChildInstancesInBatches): batchElementInstanceKey =
+      // the body (scope_key), index = its collection's size
+      const Proc::Mi* m = proc != NONE ? h->procs[proc].mi_body(elem) : nullptr;
+      if (!m) return ZBHIP_EDEVICE;
+      r.value_type = ZBHIP_VT_PROCESS_INSTANCE_BATCH;
+      r.intent = ZBHIP_PIB_ACTIVATE;
+      r.record_type = ZBHIP_RT_COMMAND;
+      r.partition = (int32_t)m->items.size();
+      r.unprocessed = (fl & F_UNPROCESSED) ? 1 : 0;
+      if (r.unprocessed && !h->cont_ids.empty()) {
+        auto it = h->cont_ids.find(((uint64_t)c << 16) | ord);
+        if (it != h->cont_ids.end()) r.aux = (int64_t)it->second;
+      }
     } else if (c6 == C_PE_TRIGGERING || c6 == C_PE_TRIGGERED) {
       r.value_type = ZBHIP_VT_PROCESS_EVENT;
       r.intent = c6 == C_PE_TRIGGERING ? ZBHIP_PE_TRIGGERING : ZBHIP_PE_TRIGGERED;
@@ -2379,16 +2491,33 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     const bool job_row = (e.y >> 24) & 1;
     const zbhip_element& E = P.els[elem];
     const bool sub = E.element_type == ZBHIP_EL_SUB_PROCESS;  // job field: childCount | activeSequenceFlows << 8
-    const long long jk = sub ? 0 : job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
+    const bool body = E.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY;  // childCount | loop counter << 8
+    const Proc::Mi* im = P.mi_inner(elem);  // a multi-instance inner instance: its loop counter in the flags
+    const bool jw = ZBHIP_IS_JOB_WORKER(E.element_type);
+    const long long jk = sub || body || (im && !jw) ? 0 : job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
     const long long fs = scope_key(E.flow_scope);
+    const uint32_t child = sub || body ? job & 0xFF : 0u, loop = body ? (job >> 8) & 0xFF : im ? e.y >> 26 : 0u;
     snprintf(buf, sizeof buf,
-             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%u,childActivatedCount=0,childCompletedCount=0,"
-             "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=0,interruptingElementId=,"
+             "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%u,childActivatedCount=%u,childCompletedCount=%u,"
+             "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=%u,interruptingElementId=,"
              "calledChildInstanceKey=-1,state=%u,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
              "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%u",
-             k, fs, sub ? job & 0xFF : 0u, jk, state, P.id(elem).c_str(), E.element_type, E.event_type, fs, pik,
-             (long long)P.def_key, sub ? (job >> 8) & 0xFF : 0u);
+             k, fs, child, body ? loop : 0u, body ? loop - child : 0u, jk, loop, state, P.id(elem).c_str(),
+             E.element_type, E.event_type, fs, pik, (long long)P.def_key, sub ? (job >> 8) & 0xFF : 0u);
     sink(ctx, buf);
+    if (im && loop >= 1 && loop <= im->items.size() && (jw ? job_row : job != JOB_ZERO)) {
+      // the inner instance's loop variables (setLoopVariables): keys right before its job's (a job
+      // worker) or the loopCounter key in its job field (an undefined task), values from the program
+      const uint32_t kl = jw ? job - 1 : job;
+      if (im->input_name != NONE) {
+        snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%lld", k, h->names[im->input_name].c_str(),
+                 h->key_of(inst, kl - 1), (unsigned)im->items[loop - 1].first, (long long)im->items[loop - 1].second);
+        sink(ctx, buf);
+      }
+      snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%u", k, h->names[im->loop_name].c_str(),
+               h->key_of(inst, kl), (unsigned)ZBHIP_DOC_INT, loop);
+      sink(ctx, buf);
+    }
     snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", fs, k);
     sink(ctx, buf);
     snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, fs);
@@ -2715,6 +2844,7 @@ int64_t to_ll(const std::string& s) { return strtoll(s.c_str(), nullptr, 10); }
 
 struct ImpElement {
   int64_t key = 0, job = 0, pik = 0, fs = 0, def = 0, child_count = 0, asf = 0;
+  int64_t activated = 0, completed = 0, terminated = 0, loop = 0;  // multi-instance counters
   uint32_t state = 0, type = 0;
   std::string id;
 };
@@ -2771,6 +2901,10 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       e.def = to_ll(f["processDefinitionKey"]);
       e.child_count = to_ll(f["childCount"]);
       e.asf = to_ll(f["activeSequenceFlows"]);
+      e.activated = to_ll(f["childActivatedCount"]);
+      e.completed = to_ll(f["childCompletedCount"]);
+      e.terminated = to_ll(f["childTerminatedCount"]);
+      e.loop = to_ll(f["multiInstanceLoopCounter"]);
       e.state = (uint32_t)to_ll(f["state"]);
       e.type = (uint32_t)to_ll(f["bpmnElementType"]);
       e.id = f["elementId"];
@@ -2860,9 +2994,12 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       if (h->procs[q].def_key == pe.def) proc = (int)q;
     if (proc < 0) return ZBHIP_EINVAL;  // not deployed
     const Proc& P = h->procs[proc];
-    auto elem_of_id = [&](const std::string& id) -> int {
+    // an element by id and type (a multi-instance body and its inner activity share the id)
+    auto elem_of_id = [&](const std::string& id, uint32_t type = ~0u) -> int {
       for (size_t e = 0; e < P.els.size(); ++e)
-        if (P.els[e].element_type != ZBHIP_EL_SEQUENCE_FLOW && P.id((uint32_t)e) == id) return (int)e;
+        if (P.els[e].element_type != ZBHIP_EL_SEQUENCE_FLOW && P.id((uint32_t)e) == id &&
+            (type == ~0u || P.els[e].element_type == type))
+          return (int)e;
       return -1;
     };
     // keys of the instance: ordinal 0 the instance, then every other key in key order
@@ -2874,23 +3011,41 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       if (e.pik != pe.key || e.key == pe.key) continue;
       children.push_back(&e);
       keys.push_back(e.key);
-      if (e.type == ZBHIP_EL_SUB_PROCESS) subs.insert(e.key);
+      if (e.type == ZBHIP_EL_SUB_PROCESS || e.type == ZBHIP_EL_MULTI_INSTANCE_BODY) subs.insert(e.key);
       else if (e.job > 0) keys.push_back(e.job);
     }
-    // flow scopes: the process instance or one of its sub-process instances (KScope slots); a
-    // sub-process instance's counters live in its slot's job field
+    // flow scopes: the process instance or one of its sub-process / multi-instance body instances
+    // (KScope slots); a container's counters live in its slot's job field
     for (const ImpElement* c : children) {
       if (c->fs != pe.key && !subs.count(c->fs)) return ZBHIP_EUNSUPP;
       if (c->type == ZBHIP_EL_SUB_PROCESS && (c->child_count < 0 || c->child_count > 255 || c->asf < 0 || c->asf > 255))
         return ZBHIP_EUNSUPP;
+      if (c->terminated != 0) return ZBHIP_EUNSUPP;
+      if (c->type == ZBHIP_EL_MULTI_INSTANCE_BODY &&  // childActivatedCount = loop, completed = loop - active
+          (c->loop < 0 || c->loop > (int64_t)kMaxMiItems || c->asf != 0 || c->activated != c->loop ||
+           c->child_count < 0 || c->completed != c->loop - c->child_count))
+        return ZBHIP_EUNSUPP;
+      if (c->type != ZBHIP_EL_MULTI_INSTANCE_BODY && c->loop != 0 &&
+          !(subs.count(c->fs) && els[c->fs].type == ZBHIP_EL_MULTI_INSTANCE_BODY))
+        return ZBHIP_EUNSUPP;
     }
     std::vector<const ImpVar*> ivars;
     auto scope_of = [&](int64_t s) { return s == pe.key || std::any_of(children.begin(), children.end(), [&](const ImpElement* c) { return c->key == s; }); };
+    // a multi-instance inner instance's own variables: its loop variables, derived from its slot on
+    // the device (checked against the program below); their keys take ordinals like any other
+    std::map<int64_t, std::map<std::string, const ImpVar*>> loop_vars;
     for (const auto& v : vars)
       if (scope_of(v.scope)) {
-        if (subs.count(v.scope)) return ZBHIP_EUNSUPP;  // sub-process-local variables: outside the subset
-        ivars.push_back(&v);
+        if (subs.count(v.scope)) return ZBHIP_EUNSUPP;  // container-local variables: outside the subset
         keys.push_back(v.key);
+        if (v.scope != pe.key) {
+          const ImpElement& se = els[v.scope];
+          if (subs.count(se.fs) && els[se.fs].type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+            loop_vars[v.scope][v.name] = &v;
+            continue;
+          }
+        }
+        ivars.push_back(&v);
       }
     const ImpTimer* tmr = nullptr;  // the instance's timer (one per instance on the device)
     for (const auto& t : timers)
@@ -2917,15 +3072,40 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     if (children.size() > (size_t)kSlots || ivars.size() > (size_t)kVars) return ZBHIP_ENOMEM;
     for (size_t c = 0; c < children.size(); ++c) {
       const ImpElement& e = *children[c];
-      const int el = elem_of_id(e.id);
+      const int el = elem_of_id(e.id, e.type);
       if (el < 0 || P.els[el].element_type != e.type) return ZBHIP_EINVAL;
-      if (P.els[el].flow_scope != (e.fs == pe.key ? 0u : els[e.fs].type == ZBHIP_EL_SUB_PROCESS
-                                                              ? (uint32_t)elem_of_id(els[e.fs].id) : ~0u))
+      const bool in_container = e.fs != pe.key && (els[e.fs].type == ZBHIP_EL_SUB_PROCESS ||
+                                                   els[e.fs].type == ZBHIP_EL_MULTI_INSTANCE_BODY);
+      if (P.els[el].flow_scope != (e.fs == pe.key ? 0u : in_container ? (uint32_t)elem_of_id(els[e.fs].id, els[e.fs].type)
+                                                                      : ~0u))
         return ZBHIP_EINVAL;  // the flow scope instance is not the element's container
-      const bool sub_el = e.type == ZBHIP_EL_SUB_PROCESS;
-      const uint32_t job = sub_el ? (uint32_t)e.child_count | ((uint32_t)e.asf << 8)
-                                  : e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
-      const uint32_t row = !sub_el && e.job > 0 && job_rows.count(e.job) ? (job_activated_state.count(e.job) ? 3u : 1u) : 0u;
+      const bool sub_el = e.type == ZBHIP_EL_SUB_PROCESS, body = e.type == ZBHIP_EL_MULTI_INSTANCE_BODY;
+      uint32_t job = sub_el ? (uint32_t)e.child_count | ((uint32_t)e.asf << 8)
+                     : body ? (uint32_t)e.child_count | ((uint32_t)e.loop << 8)
+                     : e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
+      uint32_t row = !sub_el && !body && e.job > 0 && job_rows.count(e.job) ? (job_activated_state.count(e.job) ? 3u : 1u) : 0u;
+      if (const Proc::Mi* m = P.mi_inner((uint32_t)el)) {
+        // the loop counter in the flags; its loop variables exactly what setLoopVariables wrote,
+        // keyed right below the job's key (a job worker) or kept in the job field (an undefined task)
+        if (e.loop < 1 || e.loop > (int64_t)m->items.size()) return ZBHIP_EUNSUPP;
+        const auto lv = loop_vars.find(e.key);
+        if (lv == loop_vars.end() || lv->second.size() != (m->input_name != NONE ? 2u : 1u)) return ZBHIP_EUNSUPP;
+        const auto li = lv->second.find(h->names[m->loop_name]);
+        if (li == lv->second.end() || li->second->type != ZBHIP_DOC_INT || li->second->value != e.loop) return ZBHIP_EUNSUPP;
+        const uint32_t kl = ord(li->second->key);
+        if (m->input_name != NONE) {
+          const auto ii = lv->second.find(h->names[m->input_name]);
+          const auto& item = m->items[(size_t)e.loop - 1];
+          if (ii == lv->second.end() || ii->second->type != item.first || ii->second->value != item.second ||
+              ord(ii->second->key) + 1 != kl)
+            return ZBHIP_EUNSUPP;
+        }
+        if (ZBHIP_IS_JOB_WORKER(e.type) ? !(row & 1) || job != kl + 1 : e.job != 0) return ZBHIP_EUNSUPP;
+        if (!ZBHIP_IS_JOB_WORKER(e.type)) job = kl;
+        row |= (uint32_t)e.loop << 2;
+      } else if (!loop_vars.empty() && loop_vars.count(e.key)) {
+        return ZBHIP_EUNSUPP;
+      }
       slots[c * N + inst] = make_uint2((uint32_t)el | (ord(e.key) << 16), job | (e.state << 16) | (row << 24));
     }
     for (size_t v = 0; v < ivars.size(); ++v) {
@@ -3237,6 +3417,23 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     // DbVariableState.visitVariables: the element's scope, then the process instance's
     const uint32_t nv = std::min<uint32_t>((a.z >> 16) & 0xFF, (uint32_t)kVars);
     std::vector<uint32_t> taken;
+    const Proc::Mi* m = proc < h->procs.size() ? h->procs[proc].mi_inner(elem) : nullptr;
+    const uint32_t loop = a.w >> 26;
+    if (m && loop >= 1 && loop <= m->items.size()) {
+      // a multi-instance inner instance's scope: its loop variables (setLoopVariables), then the
+      // body's (none), then the process instance's
+      std::vector<zbhip_doc_entry> local;
+      if (m->input_name != NONE)
+        local.push_back({m->input_name, m->items[loop - 1].first, {0, 0, 0}, m->items[loop - 1].second});
+      local.push_back({m->loop_name, (uint8_t)ZBHIP_DOC_INT, {0, 0, 0}, (int64_t)loop});
+      std::sort(local.begin(), local.end(),
+                [&](const zbhip_doc_entry& p, const zbhip_doc_entry& q) { return name_less(p.name_id, q.name_id); });
+      for (const zbhip_doc_entry& d : local) {
+        if (!requested.empty() && std::find(requested.begin(), requested.end(), d.name_id) == requested.end()) continue;
+        taken.push_back(d.name_id);
+        j.variables[j.n_variables++] = d;
+      }
+    }
     for (uint32_t scope : {eord, 0u}) {
       std::vector<uint32_t> local;
       for (uint32_t v = 0; v < nv; ++v)

@@ -67,6 +67,10 @@ enum : uint8_t {
   C_JOB_CANCELED = 19,    // BpmnJobBehavior.cancelJob (JOB:CANCELED, the stored job)
   C_VAR_CREATED = 20,
   C_VAR_UPDATED = 21,
+  C_MI_ITEM = 22,         // VARIABLE:CREATED of a multi-instance inner instance's inputElement / its
+  C_MI_LOOP = 23,         // loopCounter (MultiInstanceBodyProcessor.setLoopVariables): key = the variable,
+                          // aux = the inner instance, elem = the body, flags = the loop counter
+  C_PIB_ACTIVATE = 26,    // PROCESS_INSTANCE_BATCH:ACTIVATE (command): aux = the body, elem = the body
   C_PE_TRIGGERING = 24,
   C_PE_TRIGGERED = 25,    // EventTriggerBehavior.processEventTriggered
   C_PIC_CREATED = 28,
@@ -142,6 +146,9 @@ constexpr uint8_t CMD_FOLLOWUP = 0x20;
 //                            w3 = join_slot (job worker: its boundary event or 0xFFFF; boundary event:
 //                                 interrupting | repetitions << 8) | container
 //                                 (flow scope element; 0 = the process) << 16
+//                            multi-instance body: w0 high half = its inputElement's name id (0xFFFF
+//                                 none), w2 = inner activity | items << 12 | isSequential << 20, w3 low
+//                                 half = the loopCounter name id
 //   p[out_off]  u16 outgoing flows (two per word)
 //   p[cond_off] u32 first instruction of each condition
 //   p[code_off] instructions (16-byte aligned): op, arg, literal_lo, literal_hi
@@ -150,7 +157,12 @@ constexpr uint8_t CMD_FOLLOWUP = 0x20;
 struct DevState {
   uint4* hdr;        // [n] x = proc | next_ord << 16; y = pi_state | nslots << 8 | nvars << 16 | pi_live << 24
                      //     z = pi_child | pi_asf << 16; w = fence: the window stamp of a fallen-back command
-  uint2* slots;      // [kSlots][n] x = elem | key << 16; y = job | state << 16 | flags << 24 (bit0: job row exists)
+  uint2* slots;      // [kSlots][n] x = elem | key << 16; y = job | state << 16 | flags << 24 (bit0: job row
+                     // exists, bit1: its job ACTIVATED, bits 2..7: a multi-instance inner instance's loop
+                     // counter).  Containers use the job field for childCount | activeSequenceFlows << 8
+                     // (sub-process) or childCount | multiInstanceLoopCounter << 8 (multi-instance body:
+                     // childActivatedCount = the loop counter, childCompletedCount = loop - childCount);
+                     // an undefined-task inner instance for its loopCounter variable's key ordinal
   uint2* var_meta;   // [kVars][n]  x = name | scope << 16; y = key | type << 16
   long long* var_val;// [kVars][n]
   uint32_t* join;    // [kJoinWords][n]
