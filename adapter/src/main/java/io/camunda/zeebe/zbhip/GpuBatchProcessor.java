@@ -41,7 +41,9 @@ import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobBatchRecord;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceBatchRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceRecord;
+import io.camunda.zeebe.protocol.record.intent.ProcessInstanceBatchIntent;
 import io.camunda.zeebe.protocol.impl.record.value.timer.TimerRecord;
 import io.camunda.zeebe.protocol.record.RecordType;
 import io.camunda.zeebe.protocol.record.ValueType;
@@ -96,12 +98,22 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     }
   }
 
-  /** A follow-up a device batch wrote unprocessed: matched against the log in the order written. */
-  record Continuation(long id, int slot, long key, int intent, String elementId, long flowScopeKey, long piKey) {
+  /**
+   * A follow-up a device batch wrote unprocessed (a PROCESS_INSTANCE command or a multi-instance
+   * body's PROCESS_INSTANCE_BATCH:ACTIVATE): matched against the log in the order written.
+   */
+  record Continuation(long id, int slot, long key, int valueType, int intent, String elementId, long flowScopeKey,
+      long batchElementInstanceKey, long piKey) {
     boolean matches(final TypedRecord record) {
-      final ProcessInstanceRecord v = (ProcessInstanceRecord) record.getValue();
-      return record.getKey() == key && record.getIntent().value() == intent && v.getElementId().equals(elementId)
-          && v.getFlowScopeKey() == flowScopeKey && v.getProcessInstanceKey() == piKey;
+      if (record.getKey() != key || record.getValueType().value() != valueType || record.getIntent().value() != intent) {
+        return false;
+      }
+      if (record.getValue() instanceof final ProcessInstanceRecord v) {
+        return v.getElementId().equals(elementId) && v.getFlowScopeKey() == flowScopeKey
+            && v.getProcessInstanceKey() == piKey;
+      }
+      return record.getValue() instanceof final ProcessInstanceBatchRecord v
+          && v.getBatchElementInstanceKey() == batchElementInstanceKey && v.getProcessInstanceKey() == piKey;
     }
   }
 
@@ -280,10 +292,11 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       // JOB:COMPLETE of a device job; TIMER:TRIGGER (DueDateTimerChecker's command) of a device timer
       return ZbHip.resolveKey(handle, record.getKey()) >= 0;
     }
-    if (vt == ValueType.PROCESS_INSTANCE
-        && (record.getIntent() == ProcessInstanceIntent.ACTIVATE_ELEMENT
-            || record.getIntent() == ProcessInstanceIntent.COMPLETE_ELEMENT
-            || record.getIntent() == ProcessInstanceIntent.TERMINATE_ELEMENT)) {
+    if ((vt == ValueType.PROCESS_INSTANCE
+            && (record.getIntent() == ProcessInstanceIntent.ACTIVATE_ELEMENT
+                || record.getIntent() == ProcessInstanceIntent.COMPLETE_ELEMENT
+                || record.getIntent() == ProcessInstanceIntent.TERMINATE_ELEMENT))
+        || (vt == ValueType.PROCESS_INSTANCE_BATCH && record.getIntent() == ProcessInstanceBatchIntent.ACTIVATE)) {
       return next.hasNext() && next.next().matches(record);
     }
     return false;

@@ -3,7 +3,7 @@
  * command, room for the activated jobs, and the JOB_BATCH:ACTIVATED event (or the INVALID_ARGUMENT
  * rejection) the adapter appends -- JobBatchRecord with jobKeys and jobs (JobRecord with deadline,
  * worker and the collected variables, JobBatchCollector.java:67-123).  Struct layouts: include/zbhip.h
- * (zbhip_job_activation 72 B, zbhip_job_batch 16 B, zbhip_activated_job 112 B).  Not compiled in this
+ * (zbhip_job_activation 72 B, zbhip_job_batch 16 B, zbhip_activated_job 144 B).  Not compiled in this
  * image (no JDK).
  */
 package io.camunda.zeebe.zbhip;
@@ -31,7 +31,7 @@ import org.agrona.concurrent.UnsafeBuffer;
 
 record JobActivation(MemorySegment command, MemorySegment jobs, long capacity, MemorySegment result, JobBatchRecord batch) {
   private static final byte DOC_NIL = 0, DOC_BOOL = 1, DOC_INT = 2, DOC_DEC = 3, DOC_STR = 5;
-  private static final int JOB_BYTES = 112;
+  private static final int JOB_BYTES = 144;
 
   static JobActivation of(final Arena arena, final JobBatchRecord batch, final long timestamp, final GpuBatchProcessor p) {
     final byte[] type = batch.getType().getBytes(StandardCharsets.UTF_8);

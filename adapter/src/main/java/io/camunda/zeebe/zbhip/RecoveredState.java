@@ -11,6 +11,7 @@ package io.camunda.zeebe.zbhip;
 import io.camunda.zeebe.logstreams.log.LogStreamReader;
 import io.camunda.zeebe.logstreams.log.LoggedEvent;
 import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceBatchRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceRecord;
 import io.camunda.zeebe.protocol.record.RecordType;
 import io.camunda.zeebe.protocol.record.ValueType;
@@ -45,6 +46,7 @@ final class RecoveredState {
     final Set<Long> waiting = new TreeSet<>();
     final RecordMetadata meta = new RecordMetadata();
     final ProcessInstanceRecord pi = new ProcessInstanceRecord();
+    final ProcessInstanceBatchRecord batch = new ProcessInstanceBatchRecord();
     while (reader.hasNext()) {
       final LoggedEvent event = reader.next();
       event.readMetadata(meta);
@@ -52,6 +54,10 @@ final class RecoveredState {
           && meta.getValueType() == ValueType.PROCESS_INSTANCE) {
         event.readValue(pi);
         waiting.add(pi.getProcessInstanceKey());
+      } else if (meta.getRecordType() == RecordType.COMMAND && !event.shouldSkipProcessing()
+          && meta.getValueType() == ValueType.PROCESS_INSTANCE_BATCH) {
+        event.readValue(batch);
+        waiting.add(batch.getProcessInstanceKey());
       }
     }
     try (Arena a = Arena.ofConfined()) {

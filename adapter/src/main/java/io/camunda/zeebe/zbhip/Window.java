@@ -18,11 +18,14 @@ import static java.lang.foreign.ValueLayout.JAVA_SHORT;
 
 import io.camunda.zeebe.msgpack.spec.MsgPackReader;
 import io.camunda.zeebe.msgpack.spec.MsgPackToken;
+import io.camunda.zeebe.msgpack.spec.MsgPackWriter;
+import org.agrona.ExpandableArrayBuffer;
 import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
 import io.camunda.zeebe.protocol.impl.record.UnifiedRecordValue;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessEventRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
+import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceBatchRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceRecord;
 import io.camunda.zeebe.protocol.impl.record.value.timer.TimerRecord;
 import io.camunda.zeebe.protocol.impl.record.value.variable.VariableRecord;
@@ -124,6 +127,7 @@ final class Window {
           case JOB -> new JobRecord();
           case TIMER -> new TimerRecord();
           case PROCESS_INSTANCE -> new ProcessInstanceRecord();
+          case PROCESS_INSTANCE_BATCH -> new ProcessInstanceBatchRecord();
           default -> RECORD_VALUES.readRecordValue(event, meta.getValueType());
         };
     event.readValue(value);
@@ -301,10 +305,16 @@ final class Window {
       out.appendRecord(key, value, meta);
       if (recordType == RecordType.COMMAND.value()) {
         if (rec.get(JAVA_BYTE, 77) != 0) { // zbhip_record.unprocessed: a continuation, its id in aux
-          final ProcessInstanceRecord v = (ProcessInstanceRecord) value;
-          p.expectContinuation(new GpuBatchProcessor.Continuation(
-              rec.get(JAVA_LONG, 48), instances[i], key, intent, v.getElementId(), v.getFlowScopeKey(),
-              v.getProcessInstanceKey()));
+          if (value instanceof final ProcessInstanceRecord v) {
+            p.expectContinuation(new GpuBatchProcessor.Continuation(
+                rec.get(JAVA_LONG, 48), instances[i], key, valueType, intent, v.getElementId(), v.getFlowScopeKey(),
+                -1, v.getProcessInstanceKey()));
+          } else {
+            final ProcessInstanceBatchRecord v = (ProcessInstanceBatchRecord) value;
+            p.expectContinuation(new GpuBatchProcessor.Continuation(
+                rec.get(JAVA_LONG, 48), instances[i], key, valueType, intent, null, -1,
+                v.getBatchElementInstanceKey(), v.getProcessInstanceKey()));
+          }
         } else {
           admitted++;
         }
@@ -371,8 +381,10 @@ final class Window {
       }
       case VARIABLE -> {
         final VariableRecord v = new VariableRecord();
+        // aux == ZBHIP_AUX_INLINE: a value the engine computed (a multi-instance loop variable), its
+        // zbhip_doc_type in zbhip_record.partition and the value in message_key
         v.setName(new UnsafeBuffer(p.name(elem).getBytes()))
-            .setValue(entryValues.get((int) aux))
+            .setValue(aux == -2 ? inline(r.get(JAVA_INT, 72), r.get(JAVA_LONG, 56), p) : entryValues.get((int) aux))
             .setScopeKey(scope)
             .setProcessInstanceKey(pik)
             .setProcessDefinitionKey(d.definitionKey())
@@ -404,6 +416,11 @@ final class Window {
             .setProcessDefinitionKey(elem >= 0 ? d.definitionKey() : -1);
         return v.setTenantId(TENANT);
       }
+      case PROCESS_INSTANCE_BATCH -> {
+        // a multi-instance body's activateChildInstancesInBatches (index in zbhip_record.partition)
+        final ProcessInstanceBatchRecord v = new ProcessInstanceBatchRecord();
+        return v.setProcessInstanceKey(pik).setBatchElementInstanceKey(scope).setIndex(r.get(JAVA_INT, 72));
+      }
       case PROCESS_INSTANCE_CREATION -> {
         final ProcessInstanceCreationRecord v = new ProcessInstanceCreationRecord();
         v.setBpmnProcessId(d.bpmnProcessId())
@@ -416,6 +433,20 @@ final class Window {
       default -> throw new IllegalStateException("value type outside configs 1-4: " + vt
           + " (config 5 windows write their log bytes with zbhip_serialize_log)");
     }
+  }
+
+  /** One msgpack value of a zbhip_doc_type (FeelToMessagePackTransformer's encoding of an item). */
+  private static DirectBuffer inline(final int type, final long value, final GpuBatchProcessor p) {
+    final ExpandableArrayBuffer buf = new ExpandableArrayBuffer(16);
+    final MsgPackWriter w = new MsgPackWriter().wrap(buf, 0);
+    switch (type) {
+      case DOC_BOOL -> w.writeBoolean(value != 0);
+      case DOC_INT -> w.writeInteger(value);
+      case DOC_DEC -> w.writeFloat(value / 1_000_000d);
+      case DOC_STR -> w.writeString(new UnsafeBuffer(p.stringValue(value)));
+      default -> w.writeNil();
+    }
+    return new UnsafeBuffer(buf, 0, w.getOffset());
   }
 
   static {

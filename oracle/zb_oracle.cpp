@@ -1132,10 +1132,9 @@ class Oracle {
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && r.intent == ZBHIP_PIB_ACTIVATE);
     if (!known) { last_error = "process_one: command outside the restated subset"; return ZBHIP_EUNSUPP; }
-    if (r.value_type == ZBHIP_VT_PROCESS_INSTANCE || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION ||
-        r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH)
+    if (r.value_type == ZBHIP_VT_PROCESS_INSTANCE || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION)
       if (r.process_idx < 0 || r.process_idx >= (int)procs.size() ||
-          (r.value_type != ZBHIP_VT_PROCESS_INSTANCE_CREATION &&
+          (r.value_type == ZBHIP_VT_PROCESS_INSTANCE &&
            (r.element_idx < 0 || r.element_idx >= (int)procs[r.process_idx].els.size()))) {
         last_error = "process_one: unknown process or element";
         return ZBHIP_EINVAL;

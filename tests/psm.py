@@ -164,7 +164,8 @@ class OracleEngine:
     """The reference engine as a RecordProcessor (Engine.java:71-131), one command per process call;
     also the partition's DbKeyGenerator (KeyGeneratorControls) and the RawDbWriter of a hand-off."""
 
-    ACCEPTS = (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, abi.VT_PROCESS_INSTANCE, VT_JOB_BATCH)
+    ACCEPTS = (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, abi.VT_PROCESS_INSTANCE, VT_JOB_BATCH,
+               abi.VT_PROCESS_INSTANCE_BATCH)
 
     def __init__(self, partition_id=1, max_commands_in_batch=100, clock=0):
         self.o = Oracle(partition_id=partition_id, max_commands_in_batch=max_commands_in_batch)
@@ -179,7 +180,7 @@ class OracleEngine:
     def deploy(self, xml, key, version=1):
         idx = self.o.deploy(xml, key, version)
         self.tables = oracle_tables(self.o)
-        self.values = RecordValues(self.tables, self.o.name)
+        self.values = RecordValues(self.tables, self.o.name, lambda i: self.o.string_value(i).decode())
         return idx
 
     def set_clock(self, now):
@@ -238,8 +239,14 @@ class OracleEngine:
         elif vt == abi.VT_PROCESS_INSTANCE:
             p = self._proc_index(v)
             r["process_idx"] = p
-            r["element_idx"] = self.tables[p].element_ids.index(v["elementId"])
+            t = self.tables[p]  # by id and type: a multi-instance body and its inner activity share the id
+            r["element_idx"] = next(e for e, (i, ty) in enumerate(zip(t.element_ids, t.element_types))
+                                    if i == v["elementId"] and ty == v["bpmnElementType"])
             r["scope_key"], r["process_instance_key"] = v["flowScopeKey"], v["processInstanceKey"]
+            slot = self.slot_of.setdefault(v["processInstanceKey"], 0xFFFFF0 - len(self.slot_of))
+        elif vt == abi.VT_PROCESS_INSTANCE_BATCH:
+            r["scope_key"], r["process_instance_key"] = v["batchElementInstanceKey"], v["processInstanceKey"]
+            r["partition"] = v["index"]
             slot = self.slot_of.setdefault(v["processInstanceKey"], 0xFFFFF0 - len(self.slot_of))
         docs = doc_entries(variables, self.o.intern, self.o.intern_string)
         base = len(self.doc_values)

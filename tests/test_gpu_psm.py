@@ -206,3 +206,27 @@ def test_restart_imports_device_instances():
             break
         phase(ref, mixed, recs)
     assert not open_jobs(ref.log)
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_multi_instance_in_the_processing_loop(limit):
+    # parallel and sequential bodies behind the adapter: PROCESS_INSTANCE_BATCH:ACTIVATE and the inner
+    # activations as follow-ups answered from the builder or, past a limit of 3, continuations read
+    # back from the log (matched by key, value type, intent and value); job activations carry the
+    # loop variables
+    a = bpmn.multi_instance_process((1, "two", 3), process_id="par", job_type="mi-par", after="after")
+    b = bpmn.multi_instance_process((4, 5), sequential=True, process_id="seq", job_type="mi-seq")
+    deps = [(a, KEY_A, 1), (b, KEY_B, 1)]
+    ref, mixed = Ref(deps, limit), Mixed(deps, deps, limit)
+    phase(ref, mixed, [Client.create("par") for _ in range(8)] + [Client.create("seq") for _ in range(8)])
+    rng = np.random.default_rng(17 + limit)
+    for p in range(12):
+        recs = completions(ref, rng, lambda k: (("r", int(k) % 5),) if k % 2 else ())
+        if not recs:
+            break
+        extra = [Client.activate_jobs("mi-par", max_jobs=3)] if p % 2 == 0 else []
+        phase(ref, mixed, recs + extra)
+    c = mixed.adapter.counts
+    assert c["fallbacks"] == 0 and c["device_commands"] > 40
+    assert (c["continuations"] > 0) == (limit == 3)
+    assert not open_jobs(ref.log)

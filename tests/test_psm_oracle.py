@@ -19,7 +19,7 @@ KEY = 2251799813685249
 
 def _native_batches(o, recs, doc_values):
     from psm import oracle_tables
-    vals = RecordValues(oracle_tables(o), o.name)
+    vals = RecordValues(oracle_tables(o), o.name, lambda i: o.string_value(i).decode())
     batches = []
     last = None
     for k, r in enumerate(recs):
@@ -156,3 +156,11 @@ def test_oracle_import_rows_round_trip():
         StreamProcessor(out, [eng]).run()
     assert out_a.canonical() == out_b.canonical()
     assert a.state() == b.state()
+
+
+@pytest.mark.parametrize("seq", [False, True])
+@pytest.mark.parametrize("limit", [3, 100])
+def test_psm_multi_instance(seq, limit):
+    # PROCESS_INSTANCE_BATCH:ACTIVATE and the inner activations through the PSM restatement, past the
+    # limit too; loop-variable records carry their values inline
+    drive(bpmn.multi_instance_process((10, "b", 30), sequential=seq, after="after"), limit, with_docs=True)

@@ -81,9 +81,10 @@ class RecordValues:
     """zbhip_record rows -> the reference's record values (Window.value).  `procs` are the
     deployment's ProcessDefinitions (by process index), `name` the variable-name dictionary."""
 
-    def __init__(self, procs, name):
+    def __init__(self, procs, name, string_value=None):
         self.procs = procs
         self.name = name
+        self.string_value = string_value  # value-dictionary id -> str (inline STR values)
 
     def value(self, r, command_doc=(), entry_value=None):
         vt = int(r["value_type"])
@@ -104,7 +105,10 @@ class RecordValues:
                           "processDefinitionVersion": p.version, "processDefinitionKey": p.definition_key})
             return v
         if vt == abi.VT_VARIABLE:
-            return {"name": self.name(elem), "value": entry_value(aux), "scopeKey": scope, "processInstanceKey": pik,
+            # ZBHIP_AUX_INLINE: a value the engine computed (multi-instance loop variables)
+            val = typed_value(int(r["partition"]), int(r["message_key"]), self.string_value) \
+                if aux == abi.AUX_INLINE else entry_value(aux)
+            return {"name": self.name(elem), "value": val, "scopeKey": scope, "processInstanceKey": pik,
                     "processDefinitionKey": p.definition_key, "bpmnProcessId": p.bpmn_process_id, "tenantId": TENANT}
         if vt == abi.VT_PROCESS_EVENT:
             return {"scopeKey": scope, "targetElementId": p.element_ids[elem],
@@ -114,6 +118,8 @@ class RecordValues:
             return {"elementInstanceKey": scope, "processInstanceKey": pik, "dueDate": aux,
                     "repetitions": int(r["partition"]), "targetElementId": p.element_ids[elem] if elem >= 0 else "",
                     "processDefinitionKey": p.definition_key if elem >= 0 else -1, "tenantId": TENANT}
+        if vt == abi.VT_PROCESS_INSTANCE_BATCH:  # ProcessInstanceBatchRecord.java:18-40
+            return {"processInstanceKey": pik, "batchElementInstanceKey": scope, "index": int(r["partition"])}
         if vt == abi.VT_PROCESS_INSTANCE_CREATION:
             return {"bpmnProcessId": p.bpmn_process_id, "processDefinitionKey": p.definition_key,
                     "version": p.version, "processInstanceKey": scope, "variables": tuple(command_doc),
@@ -247,7 +253,7 @@ class GpuBatchProcessor:
                               initial_key=self.key_generator.current_key() - pbits, defer_continuations=True)
         for xml, key, version in self.deployments:
             self.deploy(xml, key, version)
-        self.values = RecordValues(self.part.processes, self.part.name)
+        self.values = RecordValues(self.part.processes, self.part.name, self.part.string_value)
 
     def deploy(self, xml, key, version):
         from .native import ZbhipError
@@ -287,7 +293,8 @@ class GpuBatchProcessor:
             self.reader.seek(resume_position)
             while self.reader.has_next():
                 rec = self.reader.next()
-                if rec.record_type == abi.RT_COMMAND and not rec.processed and rec.value_type == abi.VT_PROCESS_INSTANCE:
+                if rec.record_type == abi.RT_COMMAND and not rec.processed and \
+                        rec.value_type in (abi.VT_PROCESS_INSTANCE, abi.VT_PROCESS_INSTANCE_BATCH):
                     waiting.add(rec.value.get("processInstanceKey"))
         take, n = self.part.select_instances_db(entries, sorted(waiting))
         if n:
@@ -350,9 +357,14 @@ class GpuBatchProcessor:
         except ZbhipError:
             return None
 
+    @staticmethod
+    def _match(key, vt, it, v):
+        """What identifies a follow-up command written unprocessed when it comes back from the log."""
+        return (key, vt, it, v.get("elementId"), v.get("flowScopeKey"), v.get("batchElementInstanceKey"),
+                v.get("processInstanceKey"))
+
     def _continuation_match(self, record):
-        v = record.value
-        return (record.key, record.intent, v.get("elementId"), v.get("flowScopeKey"), v.get("processInstanceKey"))
+        return self._match(record.key, record.value_type, record.intent, record.value)
 
     def _hot(self, record, k):
         """Would the device take this log command?  k: continuations already claimed by the read-ahead."""
@@ -363,7 +375,8 @@ class GpuBatchProcessor:
             return it == 0 and self._create_target(record.value) is not None
         if vt == abi.VT_JOB and it == abi.JOB_COMPLETE or vt == abi.VT_TIMER and it == abi.TIMER_TRIGGER:
             return self._resolve(record.key) is not None
-        if vt == abi.VT_PROCESS_INSTANCE and it in PI_COMMAND_INTENTS:
+        if (vt == abi.VT_PROCESS_INSTANCE and it in PI_COMMAND_INTENTS) or \
+                (vt == abi.VT_PROCESS_INSTANCE_BATCH and it == abi.PIB_ACTIVATE):
             # a follow-up a device batch wrote unprocessed, read back in the order written
             return k < len(self.continuations) and self.continuations[k][2] == self._continuation_match(record)
         return False
@@ -453,9 +466,7 @@ class GpuBatchProcessor:
             if rt == abi.RT_COMMAND:
                 if r["unprocessed"]:
                     # a continuation (its id in aux): expected back from the log in the order written
-                    self.continuations.append((int(r["aux"]), win.instances[i],
-                                               (int(r["key"]), it, value.get("elementId"), value.get("flowScopeKey"),
-                                                value.get("processInstanceKey"))))
+                    self.continuations.append((int(r["aux"]), win.instances[i], self._match(int(r["key"]), vt, it, value)))
                 else:
                     admitted += 1
             elif vt == abi.VT_PROCESS_INSTANCE and it == 5 and value.get("bpmnElementType") == "PROCESS":
