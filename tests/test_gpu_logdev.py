@@ -189,3 +189,29 @@ def test_timer_and_boundary_windows(shape):
             assert recs[0]["record_type"] == abi.RT_REJECTION
             stale_done = True
     assert log.declined < log.windows - 1  # the device wrote the timer windows
+
+
+def test_window_past_two_gigabytes():
+    # a CREATE window of linear-10 whose log bytes pass 2^31 (byte offsets in 64 bits end to end: the
+    # wave-cooperative writer reads every entry's offset across lanes); the tail's bytes equal the host
+    # serialiser's for the tail's records
+    n = 450_000
+    part = Partition(max_instances=n, max_commands=n, max_records_per_batch=64)
+    assert part.deploy(bpmn.linear_process(10)) == 0
+    ser = part.log_serializer()
+    cmds = create_commands(n)
+    part.submit(cmds)
+    part.run()
+    pos = 100 + 2 * np.arange(n, dtype=np.int64)
+    first = int(pos[-1]) + 1
+    ptr, used = part.serialize_log_device(pos, first, TS, copy=False)
+    assert used > (1 << 31)
+    recs = part.drain()
+    k = 64  # the last k commands' records
+    tail_src = n - k
+    at = int(np.searchsorted(recs["source_index"], tail_src))
+    host = ser.serialize(recs[at:], cmds[tail_src:], abi.make_docs(0), tail_src, 0, pos[tail_src:], first + at, TS)
+    import ctypes as C
+    buf = C.create_string_buffer(used)
+    part.L.zbhip_log_device_copy(part.h, buf, used)
+    assert buf.raw[used - len(host):used] == host

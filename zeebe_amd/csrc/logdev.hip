@@ -13,9 +13,18 @@
 // the process-instance key (ordinal 0).  An ordinal the ring no longer holds flags the window, and
 // the host serialiser takes it instead.
 //
+// Entry templates.  Most entries of the path have a fixed layout once their keys are fixed-width
+// (PROCESS_INSTANCE events and commands, JOB:CREATED, document-less JOB:COMPLETED / PROCESS_EVENT /
+// PROCESS_INSTANCE_CREATION:CREATED; keys >= 2^32 always take msgpack's 9-byte form): the host
+// serialises each (process, element, kind) once with sentinel keys (logwriter.cpp
+// log_device_templates), and the device copies the template and patches the header's position,
+// sourcePosition, key and timestamp and the value's big-endian processInstanceKey / scope key.
+//
 // Passes: k_log_sizes (one thread per command: entry sizes) -> u64 scan over commands -> k_log_write
-// (one thread per command writes its entries, 8-byte stores) -> k_ring_fill (CREATEs reset their
-// instance's ring, then every command adds its ordinals).
+// (one lane per command resolves its next record; a templated entry is then copied by half a wave,
+// 16 B per lane, two entries per store instruction, so the stores cover whole consecutive lines and
+// no lane composes bytes; other entries are composed by their lane directly) -> k_ring_fill
+// (CREATEs reset their instance's ring, then every command adds its ordinals).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -58,7 +67,12 @@ struct LogParams {
   uint32_t* flag;               // bit 0: an unresolved key / unsupported value (host serialiser instead)
   long long now_ms;             // the run's clock: TIMER:CREATED dueDate = clock + duration
   const long long* cmd_due;     // [n] dueDate of the timer each batch canceled
+  const uint8_t* tpl;           // entry templates (logwriter.cpp log_device_templates)
+  const uint4* tpl_desc;
+  const uint32_t* tpl_idx;
+  uint32_t* rinfo;              // [rows] per record: template id << 16 | entry bytes, or kSlow | bytes
 };
+constexpr uint32_t kSlow = 1u << 31;
 
 __device__ __forceinline__ uint2 run(const LogParams& L, uint32_t i) {
   return make_uint2(L.idx[2 * i], L.idx[2 * i + 1]);
@@ -524,37 +538,202 @@ __device__ __forceinline__ void stage_tables(LogParams& L, uint32_t* lds) {
   L.idx = lds + L.arena_words;
 }
 
+// the record's entry template (id + 1, 0: composed instead): its kind (zb_internal.h kLogTplKinds),
+// the keys the template can take (patched in its 9-byte msgpack form, or a process element's -1
+// flowScopeKey that is part of the template)
+__device__ __forceinline__ uint32_t tpl_of(const LogParams& L, const LogCmd& m, const Rec& r, uint4& d) {
+  if (r.rt == ZBHIP_RT_REJECTION || r.proc >= L.tpl_idx[0] || L.pbits < (1LL << 32)) return 0;
+  uint32_t k;
+  switch (r.vt) {
+    case ZBHIP_VT_PROCESS_INSTANCE: k = r.skip ? 10u + r.intent - 8u : r.intent - 1u; break;
+    case ZBHIP_VT_JOB:
+      k = r.intent == ZBHIP_JOB_CREATED ? 13u : r.intent == ZBHIP_JOB_COMPLETED && !m.doc_count ? 17u : NONE;
+      break;
+    case ZBHIP_VT_PROCESS_EVENT:
+      k = r.intent == ZBHIP_PE_TRIGGERED ? 15u : r.intent == ZBHIP_PE_TRIGGERING && !m.doc_count ? 14u : NONE;
+      break;
+    case ZBHIP_VT_PROCESS_INSTANCE_CREATION: k = m.doc_count ? NONE : 16u; break;
+    default: return 0;
+  }
+  if (k >= kLogTplKinds) return 0;
+  const uint32_t pb = proc_block(L, r.proc);
+  if (!pb || r.elem >= L.idx[pb + 5]) return 0;
+  const uint32_t id = L.tpl_idx[L.tpl_idx[1 + r.proc] + r.elem * kLogTplKinds + k];
+  if (!id) return 0;
+  d = L.tpl_desc[id - 1];
+  const long long big = 1LL << 32;
+  if ((d.y >> 16) && r.pik < big) return 0;
+  if (d.z ? r.scope < big : (r.vt != ZBHIP_VT_PROCESS_INSTANCE || r.scope != -1)) return 0;
+  return id;
+}
+
+// pass 1: entry sizes per command, and per record its template or kSlow (flag bit 1: some record is
+// composed, k_log_compose runs; bit 0: a key or value outside the device writer)
 __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
   extern __shared__ uint32_t tables[];
   stage_tables(L, tables);
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= L.n) return;
-  const LogCmd m = L.cmds[c];
-  Count s;
-  for (uint32_t j = 0; j < m.nrec; ++j) {
-    Rec r;
-    if (!decode(L, c, m, L.rows[m.rec_off + j], r) || !entry(s, L, m, r, 0)) {
-      atomicOr(L.flag, 1u);
-      break;
+  bool slow = false;
+  if (c < L.n) {
+    const LogCmd m = L.cmds[c];
+    Count s;
+    for (uint32_t j = 0; j < m.nrec; ++j) {
+      Rec r;
+      uint4 d;
+      if (!decode(L, c, m, L.rows[m.rec_off + j], r)) {
+        atomicOr(L.flag, 1u);
+        break;
+      }
+      const uint32_t id = tpl_of(L, m, r, d);
+      if (id && id < 0x8000u) {
+        s.n += d.y & 0xFFFF;
+        L.rinfo[m.rec_off + j] = id << 16 | (d.y & 0xFFFF);
+      } else {
+        Count e;
+        if (!entry(e, L, m, r, 0) || e.n >= 0x10000) {
+          atomicOr(L.flag, 1u);
+          break;
+        }
+        s.n += e.n;
+        L.rinfo[m.rec_off + j] = kSlow | (uint32_t)e.n;
+        slow = true;
+      }
     }
+    L.bytes[c] = s.n;
   }
-  L.bytes[c] = s.n;
+  const unsigned long long b = __ballot(slow);
+  if (b && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(b)) atomicOr(L.flag, 2u);
 }
 
-__global__ __launch_bounds__(256) void k_log_write(LogParams L) {
+// x (8 bytes in memory order) placed at byte d of a 16-byte chunk (lo = bytes 0..7, hi = 8..15)
+__device__ __forceinline__ void patch8(unsigned long long& lo, unsigned long long& hi, unsigned long long x, int d) {
+  const unsigned long long M = ~0ull;
+  if (d <= -8 || d >= 16) return;
+  if (d < 0) {
+    const int sh = -8 * d;
+    lo = (lo & ~(M >> sh)) | (x >> sh);
+  } else if (d < 8) {
+    const int sh = 8 * d;
+    lo = (lo & ~(M << sh)) | (x << sh);
+    if (sh) hi = (hi & ~(M >> (64 - sh))) | (x >> (64 - sh));
+  } else {
+    const int sh = 8 * (d - 8);
+    hi = (hi & ~(M << sh)) | (x << sh);
+  }
+}
+
+// a templated entry, handed from the lane that resolved its keys to the half wave that copies it
+struct TplEnt {
+  unsigned long long dst;
+  long long key, scope, pik, lpos, src;
+  uint32_t off, size, pa, sa;
+};
+constexpr uint32_t kLogWriteB = 256;
+constexpr uint32_t kWaveEnts = 128;  // hand-over slots per wave (flushed once 64 are pending)
+
+// one 16-byte chunk (o16) of a templated entry: template bytes + header fields + value keys
+__device__ __forceinline__ void tpl_chunk(const LogParams& L, uint8_t* out, const TplEnt& e, uint32_t o16,
+                                          unsigned long long ts, ulonglong2 t) {
+  unsigned long long lo = t.x, hi = t.y;
+  if (o16 == 16) { lo = (unsigned long long)e.lpos; hi = (unsigned long long)e.src; }
+  if (o16 == 32) { lo = (unsigned long long)e.key; hi = ts; }
+  if (e.pa) patch8(lo, hi, __builtin_bswap64((unsigned long long)e.pik), (int)e.pa - (int)o16);
+  if (e.sa) patch8(lo, hi, __builtin_bswap64((unsigned long long)e.scope), (int)e.sa - (int)o16);
+  uint8_t* const q = out + e.dst + o16;
+  if (o16 + 16 <= e.size) *reinterpret_cast<ulonglong2*>(q) = make_ulonglong2(lo, hi);
+  else *reinterpret_cast<unsigned long long*>(q) = lo;
+}
+
+// pass 2: the templated entries.  Each lane walks its command's records and resolves the keys of
+// the templated ones into the wave's hand-over slots; whenever 64 are pending the wave copies them,
+// two entries per store instruction (lanes 0-31 one, 32-63 the next, 16 B per lane), four in flight.
+__global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t table_words) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  TplEnt* const ents = reinterpret_cast<TplEnt*>(smem + ((table_words + 3) & ~3u));
+  if (table_words) stage_tables(L, smem);  // (0: they do not fit, read from HBM)
+  const uint32_t lane = threadIdx.x & 63;
+  TplEnt* const wents = ents + (threadIdx.x >> 6) * kWaveEnts;
+  const uint32_t c = blockIdx.x * kLogWriteB + threadIdx.x;
+  const bool live = c < L.n;
+  LogCmd m{};
+  if (live) m = L.cmds[c];
+  unsigned long long pos = live ? L.bytes[c] : 0ull;  // byte offset of the lane's next entry
+  const uint32_t nrec = live ? m.nrec : 0u;
+  uint32_t rounds = nrec;  // the wave's largest record count
+  for (int o = 32; o; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
+  uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
+  const unsigned long long ts = (unsigned long long)L.timestamp;
+  const uint32_t half = lane >> 5, o16 = (lane & 31) * 16;
+  const unsigned long long below = (1ull << lane) - 1;
+  uint32_t cnt = 0;  // pending slots (wave-uniform)
+  for (uint32_t j = 0; j <= rounds; ++j) {
+    if (j < rounds) {
+      bool tpl = false;
+      TplEnt e;
+      if (j < nrec) {
+        const uint32_t info = L.rinfo[m.rec_off + j];
+        if (!(info & kSlow)) {
+          const uint2 w = L.rows[m.rec_off + j];
+          const uint32_t inst = m.instance;
+          tpl = key_of(L, c, inst, w.x & 0xFFFF, e.key) && key_of(L, c, inst, w.x >> 16, e.scope) &&
+                key_of(L, c, inst, 0, e.pik);
+          const uint4 d = L.tpl_desc[(info >> 16) - 1];
+          e.dst = pos;
+          e.lpos = L.first_position + (long long)(m.out_rec + j);
+          e.src = m.src_pos;
+          e.off = d.x;
+          e.size = d.y & 0xFFFF;
+          e.pa = d.y >> 16;
+          e.sa = d.z;
+        }
+        pos += info & 0xFFFF;
+      }
+      const unsigned long long mask = __ballot(tpl);
+      if (tpl) wents[cnt + (uint32_t)__popcll(mask & below)] = e;
+      cnt += (uint32_t)__popcll(mask);
+      if (cnt < 64 && j + 1 < rounds) continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t i = 0; i < cnt; i += 4) {
+      const uint32_t i0 = i + half, i1 = i + 2 + half;
+      const bool v0 = i0 < cnt, v1 = i1 < cnt;
+      TplEnt e0, e1;
+      if (v0) e0 = wents[i0];
+      if (v1) e1 = wents[i1];
+      const bool w0 = v0 && o16 < e0.size, w1 = v1 && o16 < e1.size;
+      ulonglong2 t0 = make_ulonglong2(0, 0), t1 = make_ulonglong2(0, 0);
+      if (w0) t0 = *reinterpret_cast<const ulonglong2*>(L.tpl + e0.off + o16);
+      if (w1) t1 = *reinterpret_cast<const ulonglong2*>(L.tpl + e1.off + o16);
+      if (w0) tpl_chunk(L, out, e0, o16, ts, t0);
+      if (w1) tpl_chunk(L, out, e1, o16, ts, t1);
+    }
+    cnt = 0;
+    __builtin_amdgcn_wave_barrier();  // the slots are rewritten next
+  }
+}
+
+// pass 2b (flag bit 1 only): the entries without a template, composed by their command's lane
+__global__ __launch_bounds__(256) void k_log_compose(LogParams L) {
   extern __shared__ uint32_t tables[];
   stage_tables(L, tables);
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= L.n) return;
   const LogCmd m = L.cmds[c];
-  Write s;
-  s.start(L.out + (L.bytes[c] >> 3));
+  unsigned long long pos = L.bytes[c];
   for (uint32_t j = 0; j < m.nrec; ++j) {
-    Rec r;
-    if (!decode(L, c, m, L.rows[m.rec_off + j], r)) return;
-    entry(s, L, m, r, L.first_position + (long long)(m.out_rec + j));
+    const uint32_t info = L.rinfo[m.rec_off + j];
+    if (info & kSlow) {
+      Rec r;
+      if (!decode(L, c, m, L.rows[m.rec_off + j], r)) return;
+      Write w;
+      w.start(L.out + (pos >> 3));
+      entry(w, L, m, r, L.first_position + (long long)(m.out_rec + j));
+      w.finish();
+    }
+    pos += info & 0xFFFF;
   }
-  s.finish();
 }
 
 // exclusive scan of the per-command byte counts (in place), total at bytes[n]
@@ -575,15 +754,30 @@ __global__ __launch_bounds__(kLogScanB) void k_log_block_sums(unsigned long long
     bs[blockIdx.x] = t;
   }
 }
-__global__ __launch_bounds__(64) void k_log_scan_sums(unsigned long long* bs, uint32_t nb, unsigned long long* total) {
-  if (threadIdx.x != 0) return;
-  unsigned long long acc = 0;
-  for (uint32_t b = 0; b < nb; ++b) {
-    const unsigned long long x = bs[b];
-    bs[b] = acc;
-    acc += x;
+// exclusive scan of the block sums in place (one workgroup, kLogScanB at a time), total at *total
+__global__ __launch_bounds__(kLogScanB) void k_log_scan_sums(unsigned long long* bs, uint32_t nb, unsigned long long* total) {
+  __shared__ unsigned long long ws[kLogScanB / 64];
+  __shared__ unsigned long long carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nb; base += kLogScanB) {
+    const uint32_t i = base + threadIdx.x;
+    const unsigned long long x0 = i < nb ? bs[i] : 0ull;
+    unsigned long long x = x0;
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned long long y = __shfl_up(x, off);
+      if ((threadIdx.x & 63) >= (uint32_t)off) x += y;
+    }
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+    __syncthreads();
+    unsigned long long b = carry;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) b += ws[w];
+    if (i < nb) bs[i] = b + x - x0;
+    __syncthreads();
+    if (threadIdx.x == kLogScanB - 1) carry = b + x;
+    __syncthreads();
   }
-  *total = acc;
+  if (threadIdx.x == 0) *total = carry;
 }
 __global__ __launch_bounds__(kLogScanB) void k_log_apply(unsigned long long* v, uint32_t n, const unsigned long long* bs) {
   const uint32_t i = blockIdx.x * kLogScanB + threadIdx.x;
@@ -599,6 +793,65 @@ __global__ __launch_bounds__(kLogScanB) void k_log_apply(unsigned long long* v, 
   unsigned long long b = bs[blockIdx.x];
   for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) b += ws[w];
   if (i < n) v[i] = b + x - x0;
+}
+
+// The command table of a one-round window whose rows were gathered in log order, on the device:
+// rec_off = out_rec = the exclusive scan of the record counts, key0 = the key counter + 1 + the
+// exclusive scan of the key counts (runtime.cpp builds the same on the host for other windows).
+// Block sums pack records (low half) and keys (high half): neither passes 2^32 in a window.
+__global__ __launch_bounds__(kLogScanB) void k_table_block_sums(const uint2* hdr, uint32_t n, unsigned long long* bs) {
+  const uint32_t i = blockIdx.x * kLogScanB + threadIdx.x;
+  __shared__ unsigned long long ws[kLogScanB / 64];
+  const uint2 h = i < n ? hdr[i] : make_uint2(0, 0);
+  unsigned long long x = (unsigned long long)(h.x & 0xFFFF) | ((unsigned long long)(h.x >> 16) << 32);
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(x, off);
+    if ((threadIdx.x & 63) >= (uint32_t)off) x += y;
+  }
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kLogScanB / 64; ++w) t += ws[w];
+    bs[blockIdx.x] = t;
+  }
+}
+__global__ __launch_bounds__(kLogScanB) void k_table_build(LogParams L, const uint2* hdr, const zbhip_command* cmds,
+                                                          const long long* src_pos, unsigned long long key_base,
+                                                          const unsigned long long* bs, LogCmd* out,
+                                                          uint16_t* inst_proc) {
+  const uint32_t i = blockIdx.x * kLogScanB + threadIdx.x;
+  __shared__ unsigned long long ws[kLogScanB / 64];
+  const uint2 h = i < L.n ? hdr[i] : make_uint2(0, 0);
+  const unsigned long long x0 = (unsigned long long)(h.x & 0xFFFF) | ((unsigned long long)(h.x >> 16) << 32);
+  unsigned long long x = x0;
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(x, off);
+    if ((threadIdx.x & 63) >= (uint32_t)off) x += y;
+  }
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  unsigned long long b = bs[blockIdx.x];
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) b += ws[w];
+  if (i >= L.n) return;
+  const unsigned long long ex = b + x - x0;  // records before | keys before << 32
+  const zbhip_command cm = cmds[i];
+  LogCmd m;
+  m.rec_off = ex & 0xFFFFFFFFull;
+  m.out_rec = m.rec_off;
+  m.key0 = key_base + 1 + (ex >> 32);
+  m.src_pos = src_pos ? src_pos[i] : -1;
+  m.instance = cm.instance;
+  m.prev = ~0u;
+  m.first_ord = (uint16_t)(h.y & 0xFFFF);
+  m.nkeys = ((h.y >> 16) & 0xFF) == ST_OK ? (uint16_t)(h.x >> 16) : (uint16_t)0;
+  m.nrec = (uint16_t)(h.x & 0xFFFF);
+  m.doc_count = cm.doc_count;
+  m.doc_begin = cm.doc_begin;
+  m.pad = cm.pad;
+  out[i] = m;
+  // a CREATE starts its slot's instance (one command per instance in a one-round window)
+  if (cm.kind == ZBHIP_CMD_CREATE && cm.instance < L.n_inst) inst_proc[cm.instance] = cm.ref;
 }
 
 // ring fill after the window: CREATEs reset their instance (a new generation), then every command
@@ -627,17 +880,29 @@ __global__ __launch_bounds__(256) void k_ring_add(LogParams L) {
 hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
   LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.arena_words, a.idx_words, a.docs, a.n_docs, a.inst_proc, a.ring,
               a.kpi, a.n_inst, a.pbits, a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]},
-              a.bytes, a.out, a.flag, a.now_ms, a.cmd_due};
+              a.bytes, a.out, a.flag, a.now_ms, a.cmd_due, a.tpl, a.tpl_desc, a.tpl_idx, a.rinfo};
   const uint32_t g = (a.n + 255) / 256;
   const size_t lds = a.arena_words + a.idx_words <= kLdsTableWords ? (size_t)(a.arena_words + a.idx_words) * 4 : 0;
   if (a.phase == 0) {  // sizes and byte offsets
     if (a.n) hipLaunchKernelGGL(k_log_sizes, dim3(g), dim3(256), lds, s, L);
     const uint32_t nb = (a.n + kLogScanB - 1) / kLogScanB;
     if (a.n) hipLaunchKernelGGL(k_log_block_sums, dim3(nb), dim3(kLogScanB), 0, s, a.bytes, a.n, a.block_sums);
-    hipLaunchKernelGGL(k_log_scan_sums, dim3(1), dim3(64), 0, s, a.block_sums, nb, a.bytes + a.n);
+    hipLaunchKernelGGL(k_log_scan_sums, dim3(1), dim3(kLogScanB), 0, s, a.block_sums, nb, a.bytes + a.n);
     if (a.n) hipLaunchKernelGGL(k_log_apply, dim3(nb), dim3(kLogScanB), 0, s, a.bytes, a.n, a.block_sums);
+  } else if (a.phase == 3) {  // the command table (block sums, their scan, the rows)
+    const uint32_t nb = (a.n + kLogScanB - 1) / kLogScanB;
+    if (a.n) hipLaunchKernelGGL(k_table_block_sums, dim3(nb), dim3(kLogScanB), 0, s, a.hdr, a.n, a.table_sums);
+    hipLaunchKernelGGL(k_log_scan_sums, dim3(1), dim3(kLogScanB), 0, s, a.table_sums, nb, a.table_sums + nb);
+    if (a.n)
+      hipLaunchKernelGGL(k_table_build, dim3(nb), dim3(kLogScanB), 0, s, L, a.hdr, a.wcmds, a.src_pos, a.key_base,
+                         a.table_sums, a.table, a.inst_proc_w);
   } else if (a.phase == 1) {
-    if (a.n) hipLaunchKernelGGL(k_log_write, dim3(g), dim3(256), lds, s, L);
+    // the tables (when they fit), then the waves' template hand-over slots
+    const uint32_t tw = (uint32_t)(lds / 4);
+    if (a.n)
+      hipLaunchKernelGGL(k_log_write, dim3((a.n + kLogWriteB - 1) / kLogWriteB), dim3(kLogWriteB),
+                         (size_t)((tw + 3) & ~3u) * 4 + (kLogWriteB / 64) * kWaveEnts * sizeof(TplEnt), s, L, tw);
+    if (a.n && a.compose) hipLaunchKernelGGL(k_log_compose, dim3(g), dim3(256), lds, s, L);
   } else {
     if (a.n) hipLaunchKernelGGL(k_ring_create, dim3(g), dim3(256), 0, s, L);
     if (a.n) hipLaunchKernelGGL(k_ring_add, dim3(g), dim3(256), 0, s, L);

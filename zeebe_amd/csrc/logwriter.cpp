@@ -1223,6 +1223,114 @@ namespace zb {
 void serializer_broker(const zbhip_serializer* s, int32_t out[3]) {
   for (int i = 0; i < 3; ++i) out[i] = s ? s->broker[i] : 0;
 }
+// Entry templates for the device writer (logdev.hip k_log_write): every record kind whose log entry
+// has a fixed layout once its keys are fixed-width -- PROCESS_INSTANCE events and commands,
+// JOB:CREATED, JOB:COMPLETED / PROCESS_EVENT / PROCESS_INSTANCE_CREATION:CREATED without a document --
+// serialised here once per (process, element, kind) with sentinel keys, positions and timestamp.
+// The device copies a template and patches the header's position / sourcePosition / key / timestamp
+// (8-byte little-endian at 16 / 24 / 32 / 40) and the value's processInstanceKey and scope key
+// (msgpack uint64, big-endian, at the offsets found here).  Keys >= 2^32 always take the 9-byte msgpack
+// form, and every key of the path is >= 2^51; a process element's flowScopeKey is -1 (its own template).
+// desc (uint4 per template): x = byte offset (16-aligned), y = size | (pik value offset << 16), z =
+// scope value offset (value offsets: the first byte after 0xcf, 0 = none); idx: [0] process count,
+// [1 + p] the base of process p's [element][kLogTplKinds] table of template id + 1 (0: none).
+constexpr uint32_t kLogTplKinds = 18;  // = zb_internal.h
+int log_device_templates(zbhip_serializer* s, std::vector<uint8_t>& bytes, std::vector<uint32_t>& desc,
+                         std::vector<uint32_t>& idx) {
+  if (!s) return ZBHIP_EINVAL;
+  bytes.clear();
+  desc.clear();
+  idx.clear();
+  const int64_t KEY = 0x0F1E2D3C4B5A6978LL, PIK = 0x1A2B3C4D5E6F7081LL, SCOPE = 0x2B3C4D5E6F708192LL;
+  const int64_t POS = 0x3C4D5E6F708192A3LL, SRC = 0x4D5E6F708192A3B4LL, TS = 0x5E6F708192A3B4C5LL;
+  zbhip_command cmd{};
+  const int64_t src = SRC;
+  zbhip_log_window w{};
+  w.cmds = &cmd;
+  w.n_cmds = 1;
+  w.source_positions = &src;
+  w.first_position = POS;
+  w.timestamp = TS;
+  std::vector<uint8_t> out(4096);
+  auto be_bytes = [](int64_t v) {
+    std::string b(9, '\0');
+    b[0] = (char)0xcf;
+    for (int i = 0; i < 8; ++i) b[1 + i] = (char)((uint64_t)v >> (56 - 8 * i));
+    return b;
+  };
+  const std::string pik_be = be_bytes(PIK), scope_be = be_bytes(SCOPE);
+  idx.push_back((uint32_t)s->procs.size());
+  idx.resize(1 + s->procs.size(), 0);
+  for (size_t p = 0; p < s->procs.size(); ++p) {
+    idx[1 + p] = (uint32_t)idx.size();
+    const size_t ne = s->procs[p].els.size();
+    const size_t base = idx.size();
+    idx.resize(base + ne * kLogTplKinds, 0);
+    for (size_t e = 0; e < ne; ++e) {
+      for (uint32_t k = 0; k < kLogTplKinds; ++k) {
+        zbhip_record r{};
+        r.key = KEY;
+        r.process_instance_key = PIK;
+        r.scope_key = SCOPE;
+        r.process_idx = (int32_t)p;
+        r.element_idx = (int32_t)e;
+        r.rejection_type = ZBHIP_REJ_NONE;
+        r.aux = -1;
+        r.message_key = -1;
+        r.correlation_key = ZBHIP_NO_STRING;
+        r.message_name = r.bpmn_process_id = 0xFFFF;
+        if (k < 13) {  // PROCESS_INSTANCE: events 1..7, unprocessed commands 8..10, processed ones (10 + ...)
+          const uint32_t intent = k < 10 ? k + 1 : k - 2;
+          r.value_type = ZBHIP_VT_PROCESS_INSTANCE;
+          r.intent = (uint8_t)intent;
+          r.record_type = intent >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT;
+          r.unprocessed = intent >= 8 && k < 10 ? 1 : 0;
+          if (e == 0) r.scope_key = -1;  // the process: flowScopeKey -1
+        } else if (k == 13 || k == 17) {
+          if (!ZBHIP_IS_JOB_WORKER(s->procs[p].els[e].type)) continue;
+          r.value_type = ZBHIP_VT_JOB;
+          r.intent = k == 13 ? ZBHIP_JOB_CREATED : ZBHIP_JOB_COMPLETED;
+          r.record_type = ZBHIP_RT_EVENT;
+        } else if (k == 14 || k == 15) {
+          r.value_type = ZBHIP_VT_PROCESS_EVENT;
+          r.intent = k == 14 ? ZBHIP_PE_TRIGGERING : ZBHIP_PE_TRIGGERED;
+          r.record_type = ZBHIP_RT_EVENT;
+        } else {  // 16
+          if (e != 0) continue;
+          r.value_type = ZBHIP_VT_PROCESS_INSTANCE_CREATION;
+          r.intent = ZBHIP_PIC_CREATED;
+          r.record_type = ZBHIP_RT_EVENT;
+        }
+        size_t used = 0;
+        if (zbhip_serialize_log(s, &r, 1, &w, out.data(), out.size(), &used) != ZBHIP_OK || used > 512 || used % 8)
+          continue;
+        const std::string b(reinterpret_cast<const char*>(out.data()), used);
+        auto le_at = [&b](size_t o) {
+          uint64_t v = 0;
+          for (int i = 7; i >= 0; --i) v = (v << 8) | (uint8_t)b[o + i];
+          return (int64_t)v;
+        };
+        if (le_at(16) != POS || le_at(24) != SRC || le_at(32) != KEY || le_at(40) != TS) continue;
+        if (b.find(be_bytes(KEY)) != std::string::npos) continue;  // the record key inside the value
+        const size_t a = b.find(pik_be), c = b.find(scope_be);
+        if ((a != std::string::npos && b.find(pik_be, a + 1) != std::string::npos) ||
+            (c != std::string::npos && b.find(scope_be, c + 1) != std::string::npos))
+          continue;  // a sentinel twice: not a fixed layout
+        const size_t off = bytes.size();
+        bytes.insert(bytes.end(), b.begin(), b.end());
+        bytes.resize((bytes.size() + 15) & ~(size_t)15, 0);
+        const uint32_t id = (uint32_t)(desc.size() / 4);
+        desc.push_back((uint32_t)off);
+        desc.push_back((uint32_t)used | ((a == std::string::npos ? 0u : (uint32_t)a + 1) << 16));
+        desc.push_back(c == std::string::npos ? 0u : (uint32_t)c + 1);
+        desc.push_back(0);
+        idx[base + e * kLogTplKinds + k] = id + 1;
+      }
+    }
+  }
+  return ZBHIP_OK;
+}
+
 int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, std::vector<uint32_t>& idx) {
   if (!s) return ZBHIP_EINVAL;
   arena.clear();

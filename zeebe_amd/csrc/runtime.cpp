@@ -43,6 +43,8 @@ hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmd
 hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, hipStream_t s);
 hipError_t launch_log_device(const LogLaunch& a, hipStream_t s);
 int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, std::vector<uint32_t>& idx);
+int log_device_templates(zbhip_serializer* s, std::vector<uint8_t>& bytes, std::vector<uint32_t>& desc,
+                         std::vector<uint32_t>& idx);
 void serializer_broker(const zbhip_serializer* s, int32_t out[3]);
 size_t activated_out_bytes();
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
@@ -341,13 +343,19 @@ struct zbhip_handle {
   size_t log_arena_cap = 0, log_idx_cap = 0;
   size_t log_tables_procs = ~(size_t)0, log_tables_names = ~(size_t)0;
   uint32_t log_arena_words = 0, log_idx_words = 0;
+  uint8_t* d_log_tpl = nullptr;     // entry templates | their descriptors (16-aligned) | the index
+  size_t log_tpl_cap = 0, log_tpl_desc_off = 0, log_tpl_idx_off = 0;
   unsigned long long* d_ring = nullptr;  // [16][max_instances] key ring + [max_instances] PI keys
   uint16_t* d_inst_proc = nullptr;
   LogCmd* d_logcmd = nullptr;
   unsigned long long* d_log_bytes = nullptr;  // [max_commands + 1 + scan blocks]
+  long long* d_src_pos = nullptr;             // [max_commands] source positions (device-built command table)
+  std::vector<uint16_t> inst_proc_stage;      // inst_proc as uploaded for that table
+  unsigned long long* d_tbl_sums = nullptr;   // scan blocks of the device-built command table
   uint64_t* d_log_out = nullptr;
   size_t log_out_cap = 0;
   uint32_t* d_log_flag = nullptr;
+  uint32_t* d_log_rinfo = nullptr;  // [rows] per record: template / composed, entry bytes
   std::vector<LogCmd> h_logcmd;
   std::vector<uint64_t> log_prev;   // per instance: window | last command of the window (prev chain)
   uint64_t windows_run = 0;         // zbhip_run calls
@@ -438,10 +446,13 @@ struct zbhip_handle {
   }
 };
 
-#define HIPCHK(x)                            \
-  do {                                       \
-    hipError_t e_ = (x);                     \
-    if (e_ != hipSuccess) return ZBHIP_EDEVICE; \
+#define HIPCHK(x)                                                                                \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess) {                                                                      \
+      if (getenv("ZBHIP_DEBUG")) fprintf(stderr, "[zbhip] %s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return ZBHIP_EDEVICE;                                                                      \
+    }                                                                                            \
   } while (0)
 
 static int finalize(zbhip_handle* h);
@@ -599,12 +610,16 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_tpl);
   (void)hipFree(h->d_log_arena);
   (void)hipFree(h->d_log_idx);
+  (void)hipFree(h->d_log_tpl);
   (void)hipFree(h->d_ring);
   (void)hipFree(h->d_inst_proc);
   (void)hipFree(h->d_logcmd);
   (void)hipFree(h->d_log_bytes);
+  (void)hipFree(h->d_src_pos);
+  (void)hipFree(h->d_tbl_sums);
   (void)hipFree(h->d_log_out);
   (void)hipFree(h->d_log_flag);
+  (void)hipFree(h->d_log_rinfo);
   (void)hipFree(h->d_check_flag);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
@@ -3499,11 +3514,27 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   const bool dbg = getenv("ZBHIP_DEBUG") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };
   const auto t0 = now();
-  if (int rc = finalize(h)) return rc;
-  const auto t1 = now();
   const size_t n = h->n_cmds;
   const size_t N = h->cfg.max_instances;
   if (w->n_cmds != n) return ZBHIP_EINVAL;
+  // The command table on the device (logdev.hip k_table_build) when the window is one round of
+  // device-processed commands gathered in log order and its key bookkeeping has not started: the
+  // host's key relabelling bookkeeping (finalize) then runs while the device builds the table and
+  // sizes the entries.  Otherwise the host builds the table after finalize.
+  bool dev_table = n > 0 && h->round_begin.empty() && h->fin_next == 0 && h->launches.size() == 1 &&
+                   h->launches[0].src == 0 && h->launches[0].count == n && !getenv("ZBHIP_HOST_LOG_TABLE");
+  if (dev_table) {
+    std::atomic<bool> all_ok{true};
+    parallel_for(host_threads(), [&](unsigned t, unsigned TT) {
+      for (size_t c = n * t / TT; c < n * (t + 1) / TT && all_ok.load(std::memory_order_relaxed); ++c)
+        if (((h->h_hdr[c].y >> 16) & 0xFF) != ST_OK) all_ok = false;
+    });
+    dev_table = all_ok;
+  }
+  const unsigned long long key_base = (unsigned long long)h->key_counter;  // (fin_next == 0: the window's base)
+  if (!dev_table)
+    if (int rc = finalize(h)) return rc;
+  const auto t1 = now();
   // tables of the serialiser (deployments / names changed since the last upload)
   if (h->log_tables_procs != h->procs.size() || h->log_tables_names != h->names.size()) {
     std::vector<uint8_t> arena;
@@ -3517,12 +3548,30 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     }
     if (idx.size() > h->log_idx_cap) {
       (void)hipFree(h->d_log_idx);
+  (void)hipFree(h->d_log_tpl);
       h->d_log_idx = nullptr;
       if (dalloc(&h->d_log_idx, idx.size() * 2) != hipSuccess) return ZBHIP_ENOMEM;
       h->log_idx_cap = idx.size() * 2;
     }
     HIPCHK(hipMemcpyAsync(h->d_log_arena, arena.data(), arena.size(), hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d_log_idx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, h->stream));
+    std::vector<uint8_t> tpl;
+    std::vector<uint32_t> desc, tidx;
+    if (int rc = log_device_templates(h->ser, tpl, desc, tidx)) return rc;
+    const size_t desc_off = (tpl.size() + 15) & ~(size_t)15, idx_off = desc_off + desc.size() * 4;
+    const size_t tpl_bytes = idx_off + tidx.size() * 4;
+    if (tpl_bytes > h->log_tpl_cap) {
+      (void)hipFree(h->d_log_tpl);
+      h->d_log_tpl = nullptr;
+      if (dalloc(&h->d_log_tpl, tpl_bytes * 2) != hipSuccess) return ZBHIP_ENOMEM;
+      h->log_tpl_cap = tpl_bytes * 2;
+    }
+    tpl.resize(tpl_bytes, 0);
+    memcpy(tpl.data() + desc_off, desc.data(), desc.size() * 4);
+    memcpy(tpl.data() + idx_off, tidx.data(), tidx.size() * 4);
+    HIPCHK(hipMemcpyAsync(h->d_log_tpl, tpl.data(), tpl_bytes, hipMemcpyHostToDevice, h->stream));
+    h->log_tpl_desc_off = desc_off;
+    h->log_tpl_idx_off = idx_off;
     HIPCHK(hipStreamSynchronize(h->stream));
     h->log_tables_procs = h->procs.size();
     h->log_tables_names = h->names.size();
@@ -3534,12 +3583,77 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     if (dalloc(&h->d_ring, words) != hipSuccess || dalloc(&h->d_inst_proc, N) != hipSuccess ||
         dalloc(&h->d_logcmd, (size_t)h->cfg.max_commands) != hipSuccess ||
         dalloc(&h->d_log_bytes, (size_t)h->cfg.max_commands + 1 + ((size_t)h->cfg.max_commands + 1023) / 1024 + 1) != hipSuccess ||
-        dalloc(&h->d_log_flag, 1) != hipSuccess)
+        dalloc(&h->d_log_flag, 1) != hipSuccess || dalloc(&h->d_src_pos, (size_t)h->cfg.max_commands) != hipSuccess ||
+        dalloc(&h->d_tbl_sums, ((size_t)h->cfg.max_commands + 1023) / 1024 + 2) != hipSuccess ||
+        dalloc(&h->d_log_rinfo, ((size_t)h->cfg.max_commands + 64) * h->rec_cap) != hipSuccess)
       return ZBHIP_ENOMEM;
     HIPCHK(hipMemsetAsync(h->d_ring, 0, words * sizeof(unsigned long long), h->stream));
   }
+  LogLaunch a{};
+  a.rows = h->d_rec;
+  a.cmds = h->d_logcmd;
+  a.n = (uint32_t)n;
+  a.arena = h->d_log_arena;
+  a.idx = h->d_log_idx;
+  a.arena_words = h->log_arena_words;
+  a.idx_words = h->log_idx_words;
+  a.tpl = h->d_log_tpl;
+  a.tpl_desc = reinterpret_cast<const uint4*>(h->d_log_tpl + h->log_tpl_desc_off);
+  a.tpl_idx = reinterpret_cast<const uint32_t*>(h->d_log_tpl + h->log_tpl_idx_off);
+  a.docs = h->external ? h->ext_docs : h->d_docs;
+  a.n_docs = (uint32_t)h->n_docs;
+  a.inst_proc = h->d_inst_proc;
+  a.ring = h->d_ring;
+  a.kpi = h->d_ring + (size_t)16 * N;
+  a.n_inst = (uint32_t)N;
+  a.pbits = (long long)h->cfg.partition_id << 51;
+  a.first_position = w->first_position;
+  a.timestamp = w->timestamp;
+  serializer_broker(h->ser, a.broker);
+  a.bytes = h->d_log_bytes;
+  a.block_sums = h->d_log_bytes + n + 1;
+  a.flag = h->d_log_flag;
+  a.now_ms = h->run_clock_ms;
+  a.cmd_due = h->d_cmd_due;
+  a.rinfo = h->d_log_rinfo;
+  unsigned long long total = 0;
+  uint32_t flag = 0;
+  if (dev_table) {
+    // the instances' processes before this window (the table kernel adds this window's CREATEs);
+    // a copy, since finalize updates inst_proc while the upload may still read it
+    if (h->inst_proc.size() >= N) {
+      h->inst_proc_stage.assign(h->inst_proc.begin(), h->inst_proc.begin() + N);
+      HIPCHK(hipMemcpyAsync(h->d_inst_proc, h->inst_proc_stage.data(), N * sizeof(uint16_t), hipMemcpyHostToDevice,
+                            h->stream));
+    }
+    if (w->source_positions)
+      HIPCHK(hipMemcpyAsync(h->d_src_pos, w->source_positions, n * sizeof(long long), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(h->d_log_flag, 0, sizeof(uint32_t), h->stream));
+    a.hdr = h->d_cmd_hdr;
+    a.wcmds = reinterpret_cast<const zbhip_command*>(h->external ? h->ext_cmds : h->d_cmds);
+    a.src_pos = w->source_positions ? h->d_src_pos : nullptr;
+    a.key_base = key_base;
+    a.table = h->d_logcmd;
+    a.table_sums = h->d_tbl_sums;
+    a.inst_proc_w = h->d_inst_proc;
+    a.phase = 3;
+    HIPCHK(launch_log_device(a, h->stream));
+    a.phase = 0;
+    HIPCHK(launch_log_device(a, h->stream));
+    HIPCHK(hipMemcpyAsync(&total, h->d_log_bytes + n, sizeof total, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(&flag, h->d_log_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
+    // meanwhile on the host: the window's key relabelling bookkeeping (the same key bases)
+    if (int rc = finalize(h)) {
+      (void)hipStreamSynchronize(h->stream);
+      return rc;
+    }
+    if (h->h_base[0] + 1 != (int64_t)key_base + 1 || h->key_counter < (int64_t)key_base) return ZBHIP_EDEVICE;
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  const auto t2 = now();
   // the window's command table: rows, record positions, key bases, the prev chain per instance
   // (a window of one round has one command per instance: no chain, and it is filled on host threads)
+  if (!dev_table) {
   h->h_logcmd.resize(n);
   if (h->log_prev.size() < N) h->log_prev.assign(N, ~0ull);
   const uint64_t win = h->windows_run;
@@ -3588,44 +3702,19 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
       }
     }
   }
-  const auto t2 = now();
   if (n) HIPCHK(hipMemcpyAsync(h->d_logcmd, h->h_logcmd.data(), n * sizeof(LogCmd), hipMemcpyHostToDevice, h->stream));
   if (h->inst_proc.size() >= N)
     HIPCHK(hipMemcpyAsync(h->d_inst_proc, h->inst_proc.data(), N * sizeof(uint16_t), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemsetAsync(h->d_log_flag, 0, sizeof(uint32_t), h->stream));
-  LogLaunch a{};
-  a.rows = h->d_rec;
-  a.cmds = h->d_logcmd;
-  a.n = (uint32_t)n;
-  a.arena = h->d_log_arena;
-  a.idx = h->d_log_idx;
-  a.arena_words = h->log_arena_words;
-  a.idx_words = h->log_idx_words;
-  a.docs = h->external ? h->ext_docs : h->d_docs;
-  a.n_docs = (uint32_t)h->n_docs;
-  a.inst_proc = h->d_inst_proc;
-  a.ring = h->d_ring;
-  a.kpi = h->d_ring + (size_t)16 * N;
-  a.n_inst = (uint32_t)N;
-  a.pbits = (long long)h->cfg.partition_id << 51;
-  a.first_position = w->first_position;
-  a.timestamp = w->timestamp;
-  serializer_broker(h->ser, a.broker);
-  a.bytes = h->d_log_bytes;
-  a.block_sums = h->d_log_bytes + n + 1;
-  a.flag = h->d_log_flag;
-  a.now_ms = h->run_clock_ms;
-  a.cmd_due = h->d_cmd_due;
   a.phase = 0;
   HIPCHK(launch_log_device(a, h->stream));
-  unsigned long long total = 0;
-  uint32_t flag = 0;
   HIPCHK(hipMemcpyAsync(&total, h->d_log_bytes + n, sizeof total, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(&flag, h->d_log_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  }
   const auto t3 = now();
   int rc = ZBHIP_OK;
-  if (flag) {
+  if (flag & 1u) {
     rc = ZBHIP_EUNSUPP;  // a key the ring does not hold, or a value outside the device writer
   } else {
     if (total > h->log_out_cap) {
@@ -3637,6 +3726,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
       h->log_out_cap = cap / 8 * 8;
     }
     a.out = h->d_log_out;
+    a.compose = (flag & 2u) ? 1 : 0;
     a.phase = 1;
     HIPCHK(launch_log_device(a, h->stream));
     *dev_bytes = h->d_log_out;
@@ -3648,8 +3738,8 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   if (dbg) {
     const auto t4 = now();
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    fprintf(stderr, "[zbhip] serialize_log_device n=%zu: finalize %.2f ms, table %.2f ms, upload+sizes %.2f ms, write+ring %.2f ms\n",
-            n, ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
+    fprintf(stderr, "[zbhip] serialize_log_device n=%zu (%s table): finalize %.2f ms, table %.2f ms, upload+sizes %.2f ms, "
+            "write+ring %.2f ms\n", n, dev_table ? "device" : "host", ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
   }
   return rc;
 }

@@ -242,6 +242,12 @@ struct StepParams {
 };
 
 // ---- log bytes on the device (logdev.hip) ----
+// entry templates of the device log writer (logwriter.cpp log_device_templates): PROCESS_INSTANCE
+// intents 1..10 (commands unprocessed), 10..12 the commands processed in their batch, 13 JOB:CREATED,
+// 14 / 15 PROCESS_EVENT TRIGGERING / TRIGGERED, 16 PROCESS_INSTANCE_CREATION:CREATED, 17
+// JOB:COMPLETED (the last four without a document)
+constexpr uint32_t kLogTplKinds = 18;
+
 struct LogCmd {
   unsigned long long rec_off;  // first gathered row of the command
   unsigned long long out_rec;  // log-order index of its first record in the window
@@ -254,7 +260,7 @@ struct LogCmd {
   uint32_t pad;                // the command's pad (TIMER:TRIGGER: dueDate high word)
 };
 struct LogLaunch {
-  int phase;                   // 0 sizes + offsets, 1 write, 2 key ring
+  int phase;                   // 0 sizes + offsets, 1 write, 2 key ring, 3 command table
   const uint2* rows;
   const LogCmd* cmds;
   uint32_t n;
@@ -276,6 +282,19 @@ struct LogLaunch {
   uint32_t* flag;
   long long now_ms;            // the run's clock (TIMER:CREATED dueDates)
   const long long* cmd_due;    // [n] dueDate of the timer each batch canceled (KScope)
+  // phase 3: the command table built on the device (a one-round window gathered in log order)
+  const uint2* hdr;            // [n] per-command headers of the run (nrec | nkeys << 16, first_ord)
+  const zbhip_command* wcmds;  // [n] the window's commands
+  const long long* src_pos;    // [n] sourcePosition of each command (NULL: -1)
+  unsigned long long key_base; // key counter before the window's first key
+  LogCmd* table;               // [n] out
+  unsigned long long* table_sums;  // scan blocks + 1
+  uint16_t* inst_proc_w;       // the window's CREATEs set their slot's process here
+  const uint8_t* tpl;          // entry templates (16-aligned)
+  const uint4* tpl_desc;       // per template: offset, size | pik offset + 1 << 16, scope offset + 1
+  const uint32_t* tpl_idx;     // [0] n procs, [1 + p] base of process p's [element][kLogTplKinds] ids + 1
+  uint32_t* rinfo;             // [rows] per record: its template or composed, and its entry bytes
+  int compose;                 // phase 1: entries without a template exist (the size pass's flag bit 1)
 };
 
 }  // namespace zb
