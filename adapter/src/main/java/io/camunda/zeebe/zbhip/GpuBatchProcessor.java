@@ -39,6 +39,7 @@ import io.camunda.zeebe.logstreams.log.LogStreamReader;
 import io.camunda.zeebe.logstreams.log.LoggedEvent;
 import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobBatchRecord;
+import io.camunda.zeebe.protocol.impl.record.value.incident.IncidentRecord;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceBatchRecord;
@@ -242,6 +243,13 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     int i = window.covers(record.getPosition()) ? window.indexOf(record.getPosition()) : -1;
     if (i < 0) {
       if (!isHotPath(record, continuations.iterator())) {
+        // a command the device does not run for an instance it holds (INCIDENT:RESOLVE of a gateway's
+        // incident, PROCESS_INSTANCE:CANCEL, ...): the instance moves to RocksDB first
+        final int held = heldInstance(record);
+        if (held >= 0) {
+          handOff(held);
+          keyGenerator.setKeyIfHigher(ZbHip.currentKey(handle));
+        }
         return engine.process(record, out);
       }
       fillWindow(record);
@@ -417,14 +425,28 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     return ZbHip.name(handle, id);
   }
 
+  String incidentMessage(final MemorySegment rec) {
+    return ZbHip.incidentMessage(handle, rec);
+  }
+
   String rejectionReason(final MemorySegment rec) {
     return ZbHip.rejectionReason(handle, rec);
   }
 
   // ---- fallback hand-off (INTEGRATION.md §8; Engine.java:134, ProcessingStateMachine.java:276-310) ----
 
-  private ProcessingResult fallBack(final int i, final TypedRecord record, final ProcessingResultBuilder out) {
-    final int instance = window.instanceOf(i);
+  /** The device instance slot a non-hot-path command addresses by its key or its value's process instance, or -1. */
+  private int heldInstance(final TypedRecord record) {
+    long ref = record.getKey() >= 0 ? ZbHip.resolveKey(handle, record.getKey()) : -1;
+    if (ref < 0) {
+      final long pik = record.getValue() instanceof final ProcessInstanceRecord v ? v.getProcessInstanceKey()
+          : record.getValue() instanceof final IncidentRecord v ? v.getProcessInstanceKey() : -1;
+      ref = pik >= 0 ? ZbHip.resolveKey(handle, pik) : -1;
+    }
+    return ref < 0 ? -1 : (int) (ref >>> 16);
+  }
+
+  private void handOff(final int instance) {
     if (handedOff.add(instance)) {
       // the instance's zb-db entries into RocksDB (the platform's transaction), then off the device
       // with its waiting continuations (the engine reads them back from the log)
@@ -438,6 +460,11 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       usedSlots.clear(instance);
       ended.remove(instance);
     }
+  }
+
+  private ProcessingResult fallBack(final int i, final TypedRecord record, final ProcessingResultBuilder out) {
+    final int instance = window.instanceOf(i);
+    handOff(instance);
     final long before = ZbHip.keyBefore(handle, i);
     keyGenerator.setKeyIfHigher(before);
     // the keys the engine's batch generates (follow-ups included) are declared after it

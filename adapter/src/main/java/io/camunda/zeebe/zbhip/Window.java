@@ -22,6 +22,7 @@ import io.camunda.zeebe.msgpack.spec.MsgPackWriter;
 import org.agrona.ExpandableArrayBuffer;
 import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
 import io.camunda.zeebe.protocol.impl.record.UnifiedRecordValue;
+import io.camunda.zeebe.protocol.impl.record.value.incident.IncidentRecord;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessEventRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
@@ -40,6 +41,7 @@ import io.camunda.zeebe.protocol.record.intent.ProcessInstanceIntent;
 import io.camunda.zeebe.protocol.record.intent.VariableIntent;
 import io.camunda.zeebe.protocol.record.value.BpmnElementType;
 import io.camunda.zeebe.protocol.record.value.BpmnEventType;
+import io.camunda.zeebe.protocol.record.value.ErrorType;
 import io.camunda.zeebe.logstreams.log.LoggedEvent;
 import io.camunda.zeebe.stream.api.ProcessingResultBuilder;
 import io.camunda.zeebe.stream.api.records.TypedRecord;
@@ -414,6 +416,20 @@ final class Window {
             .setRepetitions(r.get(JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value() ? 1 : r.get(JAVA_INT, 72))
             .setTargetElementId(new UnsafeBuffer(elem >= 0 ? d.elementIds()[elem].getBytes() : new byte[0]))
             .setProcessDefinitionKey(elem >= 0 ? d.definitionKey() : -1);
+        return v.setTenantId(TENANT);
+      }
+      case INCIDENT -> {
+        // BpmnIncidentBehavior.createIncident (:51-71) of an exclusive gateway: the ErrorType ordinal
+        // in zbhip_record.partition, the message composed by the library (zbhip_incident_message)
+        final IncidentRecord v = new IncidentRecord();
+        v.setErrorType(ErrorType.values()[r.get(JAVA_INT, 72)])
+            .setErrorMessage(p.incidentMessage(r))
+            .setBpmnProcessId(new UnsafeBuffer(d.bpmnProcessId().getBytes()))
+            .setProcessDefinitionKey(d.definitionKey())
+            .setProcessInstanceKey(pik)
+            .setElementId(new UnsafeBuffer(d.elementIds()[elem].getBytes()))
+            .setElementInstanceKey(scope)
+            .setVariableScopeKey(scope);
         return v.setTenantId(TENANT);
       }
       case PROCESS_INSTANCE_BATCH -> {

@@ -172,6 +172,8 @@ public final class ZbHip {
       fn("zbhip_resolve_key", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle REASON =
       fn("zbhip_rejection_reason", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG));
+  private static final MethodHandle INCIDENT_MESSAGE =
+      fn("zbhip_incident_message", FunctionDescriptor.of(JAVA_LONG, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG));
   private static final MethodHandle EXPORT_INSTANCES_DB =
       fn("zbhip_export_instances_db", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle EVICT = fn("zbhip_evict_instances", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG));
@@ -416,6 +418,17 @@ public final class ZbHip {
       final MemorySegment buf = a.allocate(1024);
       check((int) call(REASON, h, record, buf, 1024L), "zbhip_rejection_reason");
       return buf.getUtf8String(0);
+    }
+  }
+
+  /** The errorMessage of a drained INCIDENT record (zbhip_incident_message). */
+  public static String incidentMessage(final MemorySegment h, final MemorySegment record) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment buf = a.allocate(4096);
+      final long n = (long) call(INCIDENT_MESSAGE, h, record, buf, 4096L);
+      check(n < 0 ? (int) n : 0, "zbhip_incident_message");
+      final byte[] b = buf.asSlice(0, Math.min(n, 4096L)).toArray(JAVA_BYTE);
+      return new String(b, java.nio.charset.StandardCharsets.UTF_8);
     }
   }
 

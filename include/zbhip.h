@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 6  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+#define ZBHIP_ABI_VERSION 7  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
                                4: timer boundary events (start_event / flow_source / job_retries of job
                                   workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
                                   PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions;
@@ -48,7 +48,9 @@ extern "C" {
                                6: multi-instance bodies (ZBHIP_EL_MULTI_INSTANCE_BODY elements,
                                   ZBHIP_OP_ITEM collections), PROCESS_INSTANCE_BATCH records, VARIABLE
                                   records with inline values (ZBHIP_AUX_INLINE), six variables per
-                                  activated job */
+                                  activated job;
+                               7: INCIDENT:CREATED records of exclusive gateways (ZBHIP_VT_INCIDENT,
+                                  zbhip_incident_message), zbhip_process_csr.cond_text */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -65,6 +67,7 @@ enum zbhip_record_type { ZBHIP_RT_EVENT = 0, ZBHIP_RT_COMMAND = 1, ZBHIP_RT_REJE
 enum zbhip_value_type {
   ZBHIP_VT_JOB = 0,
   ZBHIP_VT_PROCESS_INSTANCE = 5,
+  ZBHIP_VT_INCIDENT = 6,
   ZBHIP_VT_MESSAGE = 10,
   ZBHIP_VT_MESSAGE_SUBSCRIPTION = 11,
   ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION = 12,
@@ -104,6 +107,12 @@ enum { ZBHIP_PE_TRIGGERING = 0, ZBHIP_PE_TRIGGERED = 1 };
 enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
 /* TimerIntent (protocol/.../intent/TimerIntent.java:19-30) */
 enum { ZBHIP_TIMER_CREATED = 0, ZBHIP_TIMER_TRIGGER = 1, ZBHIP_TIMER_TRIGGERED = 2, ZBHIP_TIMER_CANCELED = 4 };
+/* IncidentIntent CREATED=0 RESOLVE=1 RESOLVED=2 (protocol/.../intent/IncidentIntent.java:19-22) */
+enum { ZBHIP_INCIDENT_CREATED = 0 };
+/* ErrorType ordinals (protocol/.../record/value/ErrorType.java) of the device's incidents */
+enum { ZBHIP_ERR_CONDITION_ERROR = 3, ZBHIP_ERR_EXTRACT_VALUE_ERROR = 4 };
+/* the type of a condition's non-boolean result (ResultType names in the incident message) */
+enum { ZBHIP_FEEL_NULL = 0, ZBHIP_FEEL_NUMBER = 1, ZBHIP_FEEL_STRING = 2 };
 /* ProcessInstanceBatchIntent (protocol/.../intent/ProcessInstanceBatchIntent.java:18-20) */
 enum { ZBHIP_PIB_TERMINATE = 0, ZBHIP_PIB_ACTIVATE = 1 };
 /* MessageIntent, MessageSubscriptionIntent, ProcessMessageSubscriptionIntent
@@ -239,6 +248,8 @@ typedef struct zbhip_process_csr {
   int32_t version;
   uint16_t bpmn_process_id;      /* string index */
   uint16_t pad;
+  const char* const* cond_text;  /* condition c's FEEL text after '=' (ParsedExpression.text: the incident
+                                    message); "" for a multi-instance collection */
 } zbhip_process_csr;
 
 /* Host-side compiler: BPMN XML -> CSR (engine/.../deployment/model/transformation/BpmnTransformer.java:109-127).
@@ -420,13 +431,15 @@ typedef struct zbhip_record {
   uint8_t reason_arg;           /* e.g. the offending element-instance state */
   int64_t aux;                  /* VARIABLE: document entry index, or ZBHIP_AUX_INLINE (the value in
                                    message_key, its zbhip_doc_type in partition: multi-instance
-                                   loopCounter / input element); JOB:COMPLETED: source doc; else -1 */
+                                   loopCounter / input element); JOB:COMPLETED: source doc; INCIDENT: the
+                                   sequence flow whose condition was not a boolean (-1: none chosen); else -1 */
   /* message value fields (MESSAGE / MESSAGE_SUBSCRIPTION / PROCESS_MESSAGE_SUBSCRIPTION) */
   int64_t message_key;          /* messageKey, -1 unset */
   uint32_t correlation_key;     /* string id, ZBHIP_NO_STRING = empty */
   uint16_t message_name;        /* name id, 0xFFFF = empty */
   uint16_t bpmn_process_id;     /* name id, 0xFFFF = empty */
   int32_t partition;            /* PMS: subscriptionPartitionId; TIMER events: repetitions (-1 infinite);
+                                   INCIDENT: the ErrorType ordinal (reason_arg: the ZBHIP_FEEL_* result);
                                    PROCESS_INSTANCE_BATCH: index (the children still to activate);
                                    VARIABLE with aux == ZBHIP_AUX_INLINE: the value's zbhip_doc_type; else 0 */
   uint8_t interrupting;
@@ -439,6 +452,12 @@ typedef struct zbhip_record {
 #define ZBHIP_AUX_INLINE (-2)
 
 int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out);
+/* The errorMessage of a drained INCIDENT record (BpmnIncidentBehavior.createIncident's Failure):
+ * CONDITION_ERROR "Expected at least one condition to evaluate to true, or to have a default flow"
+ * (ExclusiveGatewayProcessor.java:121-125), EXTRACT_VALUE_ERROR "Expected result of the expression
+ * '<text>' to be 'BOOLEAN', but was '<NULL|NUMBER|STRING>'." (ExpressionProcessor.java:356-368).
+ * Writes at most cap bytes (no NUL) and returns the full length, or < 0. */
+int64_t zbhip_incident_message(zbhip_handle* h, const zbhip_record* r, char* out, size_t cap);
 /* The records of window command i only (plain windows; ZBHIP_EUNSUPP for message partitions): what a
  * host adapter emits when the platform reaches command i.  Keys of the commands after a fallback
  * command are fixed once the CPU engine's keys for it are declared (zbhip_set_external_keys), so a
@@ -570,6 +589,8 @@ int64_t zbhip_serializer_intern_string(zbhip_serializer* s, const char* bytes, s
 /* RecordMetadata.brokerVersion written into every entry (default 8.4.0, the reference build). */
 int zbhip_serializer_set_broker_version(zbhip_serializer* s, int32_t major, int32_t minor, int32_t patch);
 int zbhip_serializer_rejection_reason(zbhip_serializer* s, const zbhip_record* rec, char* buf, size_t cap);
+/* zbhip_incident_message on a serializer's deployments. */
+int64_t zbhip_serializer_incident_message(zbhip_serializer* s, const zbhip_record* rec, char* buf, size_t cap);
 zbhip_serializer* zbhip_handle_serializer(zbhip_handle* h);
 
 /* The window the records were drained from, and the log positions of its batches. */

@@ -181,6 +181,25 @@ TIMER = [
     ("elementInstanceKey", "long", NO_DEFAULT), ("processInstanceKey", "long", NO_DEFAULT),
     ("dueDate", "long", NO_DEFAULT), ("targetElementId", "str", NO_DEFAULT), ("repetitions", "int", NO_DEFAULT),
     ("processDefinitionKey", "long", NO_DEFAULT), ("tenantId", "str", "<default>")]
+# IncidentRecord.java:20-47
+INCIDENT = [
+    ("errorType", "enum", "UNKNOWN"), ("errorMessage", "str", ""), ("bpmnProcessId", "str", ""),
+    ("processDefinitionKey", "long", -1), ("processInstanceKey", "long", -1), ("elementId", "str", ""),
+    ("elementInstanceKey", "long", -1), ("jobKey", "long", -1), ("variableScopeKey", "long", -1),
+    ("tenantId", "str", "<default>")]
+ERROR_TYPE = {3: "CONDITION_ERROR", 4: "EXTRACT_VALUE_ERROR"}  # ErrorType.java ordinals
+FEEL_RESULT = {0: "NULL", 1: "NUMBER", 2: "STRING"}
+
+
+def incident_message(p, error_type, flow, result):
+    """errorMessage of an exclusive gateway's incident: ExclusiveGatewayProcessor.java:121-125
+    (CONDITION_ERROR) or ExpressionProcessor.typeCheck (:356-368, EXTRACT_VALUE_ERROR)."""
+    if error_type == 3:
+        return "Expected at least one condition to evaluate to true, or to have a default flow"
+    return "Expected result of the expression '%s' to be 'BOOLEAN', but was '%s'." % (
+        p["cond_text"][flow], FEEL_RESULT[result])
+
+
 # ProcessInstanceBatchRecord.java:18-40 (no tenantId)
 PROCESS_INSTANCE_BATCH = [
     ("processInstanceKey", "long", NO_DEFAULT), ("batchElementInstanceKey", "long", NO_DEFAULT),
@@ -296,6 +315,7 @@ VT_JOB, VT_PI, VT_VARIABLE, VT_PIC, VT_PE = 0, 5, 17, 19, 24
 VT_MESSAGE, VT_MS, VT_PMS = 10, 11, 12
 VT_TIMER = 15
 VT_PIB = 34
+VT_INCIDENT = 6
 AUX_INLINE = -2
 NO_STRING, NO_NAME = 0xFFFFFFFF, 0xFFFF
 
@@ -377,6 +397,13 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
                                         processInstanceKey=int(r["process_instance_key"]), dueDate=int(r["aux"]),
                                         targetElementId=el[2] if el is not None else "", repetitions=reps,
                                         processDefinitionKey=p["key"] if p is not None else -1))
+    if vt == VT_INCIDENT:  # BpmnIncidentBehavior.createIncident (:51-71)
+        et = int(r["partition"])
+        return write_object(INCIDENT, dict(
+            errorType=ERROR_TYPE[et], errorMessage=incident_message(p, et, int(r["aux"]), int(r["reason_arg"])),
+            bpmnProcessId=p["bpmn_process_id"], processDefinitionKey=p["key"],
+            processInstanceKey=int(r["process_instance_key"]), elementId=el[2],
+            elementInstanceKey=int(r["scope_key"]), variableScopeKey=int(r["scope_key"])))
     if vt == VT_PIB:
         return write_object(PROCESS_INSTANCE_BATCH, dict(processInstanceKey=int(r["process_instance_key"]),
                                                          batchElementInstanceKey=int(r["scope_key"]),

@@ -40,6 +40,8 @@ def lib():
         L.zbo_name.restype = C.c_char_p
         L.zbo_element_job_type.restype = C.c_char_p
         L.zbo_element_job_type.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.zbo_element_cond_text.restype = C.c_char_p
+        L.zbo_element_cond_text.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.zbo_process_info.restype = C.c_char_p
         L.zbo_process_info.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.zbo_element_info.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -171,7 +173,9 @@ class Oracle:
                 self.L.zbo_element_info(self.h, p, e, C.byref(t), C.byref(ev), C.byref(r))
                 els.append((t.value, ev.value, self.element_id(p, e),
                             self.L.zbo_element_job_type(self.h, p, e).decode(), r.value))
-            out.append({"bpmn_process_id": bid, "version": ver.value, "key": key.value, "elements": els})
+            conds = [self.L.zbo_element_cond_text(self.h, p, e).decode() for e in range(len(els))]
+            out.append({"bpmn_process_id": bid, "version": ver.value, "key": key.value, "elements": els,
+                        "cond_text": conds})
         return out
 
     def submit(self, cmds, docs=None, xparts=None):

@@ -184,7 +184,7 @@ struct XmlParser {
 // feel-scala, feel/.../MessagePackValueMapper.scala:41-71); held here as
 // __int128 scaled by 10^18.
 // ---------------------------------------------------------------------------
-enum VKind { V_NULL, V_BOOL, V_NUM, V_ERR };
+enum VKind { V_NULL, V_BOOL, V_NUM, V_ERR, V_STR };
 struct FVal {
   VKind k = V_NULL;
   __int128 n = 0;
@@ -328,6 +328,7 @@ struct OEl {
   int src = -1, tgt = -1;
   bool has_cond = false;
   std::unique_ptr<FExpr> cond;
+  std::string cond_text;           // the FEEL expression's text after '=' (ParsedExpression.text)
   int default_flow = -1;
   std::string job_type;
   int retries = 3;
@@ -727,6 +728,7 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       txt = a == std::string::npos ? "" : txt.substr(a, b - a + 1);
       fe.has_cond = true;
       if (txt.empty() || txt[0] != '=') { err = "static (non-FEEL) condition outside the subset"; return false; }
+      fe.cond_text = txt.substr(1);
       FeelParser fp(txt.substr(1));
       fe.cond = fp.parse_or();
       fp.ws();
@@ -1398,6 +1400,13 @@ class Oracle {
   int64_t now_ms = 0;  // ActorClock.currentTimeMillis() of the window's processing (zbo_set_clock)
  private:
   std::map<int64_t, JobRow> jobs_;                              // JOBS (+ JOB_STATES = ACTIVATABLE)
+  struct IncidentRow {  // IncidentRecord (protocol-impl/.../incident/IncidentRecord.java:20-48)
+    PiValue pi;         // process, element, process instance key
+    int64_t eik = -1;   // elementInstanceKey = variableScopeKey
+    int error_type = 0, flow = -1, result = 0;  // the message: zbhip_incident_message
+  };
+  std::map<int64_t, IncidentRow> incidents_;                    // INCIDENTS
+  std::map<int64_t, int64_t> incident_pi_;                      // INCIDENT_PROCESS_INSTANCES [eik -> incident]
   std::set<std::tuple<std::string, std::string, int64_t>> activatable_;  // JOB_ACTIVATABLE
 
   // --- message state (ZbColumnFamilies PROCESS_SUBSCRIPTION_BY_KEY, MESSAGE_SUBSCRIPTION_BY_KEY,
@@ -2319,7 +2328,12 @@ class Oracle {
         break;
       }
       case ZBHIP_EL_EXCLUSIVE_GATEWAY: {  // ExclusiveGatewayProcessor.onActivate (processing/bpmn/gateway/ExclusiveGatewayProcessor.java:47-66)
-        int flow = find_sequence_flow_to_take(el, key, v.proc);
+        FlowFailure fail;
+        int flow = find_sequence_flow_to_take(el, key, v.proc, fail);
+        if (flow == -2) {  // incidentBehavior.createIncident(failure, activating)
+          create_incident(fail, key, v);
+          break;
+        }
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         pi_event(key, ZBHIP_PI_ELEMENT_COMPLETING, v);
         transition_to_completed(el, key, v);
@@ -2502,19 +2516,55 @@ class Oracle {
   }
 
   // ExclusiveGatewayProcessor.findSequenceFlowToTake (:86-126)
-  int find_sequence_flow_to_take(const OEl& el, int64_t gwKey, int proc) {
+  // A failure (Either.left) is returned as -2 with `fail`: the error type, the flow whose condition
+  // did not evaluate to a boolean (-1: none chosen) and that result's type.
+  struct FlowFailure { int error_type = 0, flow = -1, result = 0; };
+  int find_sequence_flow_to_take(const OEl& el, int64_t gwKey, int proc, FlowFailure& fail) {
     const OProc& p = P(proc);
     if (el.out.empty()) return -1;  // implicit end of the flow scope
     if (el.out.size() == 1 && !p.els[el.out[0]].has_cond) return el.out[0];
     for (int f : el.out_with_cond) {
       if (el.default_flow == f) continue;  // the default flow's condition is never evaluated
-      // ExpressionProcessor.evaluateBooleanExpression (processing/common/ExpressionProcessor.java:126-131,356-368)
+      // ExpressionProcessor.evaluateBooleanExpression (processing/common/ExpressionProcessor.java:126-131,356-368):
+      // typeCheck -> EXTRACT_VALUE_ERROR "Expected result of the expression '%s' to be 'BOOLEAN', but was '%s'."
       FVal r = eval(p.els[f].cond.get(), gwKey);
-      if (r.k != V_BOOL) throw Unsupported{"condition did not evaluate to a boolean (incident)"};
+      if (r.k != V_BOOL) {
+        if (r.k == V_ERR) throw Unsupported{"condition value outside the subset"};
+        fail.error_type = ZBHIP_ERR_EXTRACT_VALUE_ERROR;
+        fail.flow = f;
+        fail.result = r.k == V_NULL ? ZBHIP_FEEL_NULL : r.k == V_NUM ? ZBHIP_FEEL_NUMBER : ZBHIP_FEEL_STRING;
+        return -2;
+      }
       if (r.b) return f;
     }
     if (el.default_flow >= 0) return el.default_flow;
-    throw Unsupported{"no outgoing flow chosen (incident CONDITION_ERROR)"};
+    // (:121-125) NO_OUTGOING_FLOW_CHOSEN_ERROR, CONDITION_ERROR
+    fail.error_type = ZBHIP_ERR_CONDITION_ERROR;
+    return -2;
+  }
+
+  // BpmnIncidentBehavior.createIncident (processing/bpmn/behavior/BpmnIncidentBehavior.java:51-71):
+  // INCIDENT:CREATED (key = nextKey) for the element instance, variable scope = the element instance
+  // (the failure's scope key is the gateway's); IncidentCreatedApplier -> DbIncidentState.createIncident
+  // (INCIDENTS, INCIDENT_PROCESS_INSTANCES).  The element instance stays where the failure left it.
+  void create_incident(const FlowFailure& f, int64_t eik, const PiValue& v) {
+    const int64_t key = next_key();
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_INCIDENT, ZBHIP_INCIDENT_CREATED, key);
+    rec.r.process_idx = v.proc;
+    rec.r.element_idx = v.elem;
+    rec.r.scope_key = eik;
+    rec.r.process_instance_key = v.piKey;
+    rec.r.partition = f.error_type;
+    rec.r.aux = f.flow;
+    rec.r.reason_arg = (uint8_t)f.result;
+    IncidentRow row;
+    row.pi = v;
+    row.eik = eik;
+    row.error_type = f.error_type;
+    row.flow = f.flow;
+    row.result = f.result;
+    incidents_[key] = row;
+    incident_pi_[eik] = key;
   }
 
   // DbVariableState.getVariable walks the scope chain (state/variable/DbVariableState.java:174-200)
@@ -2543,6 +2593,7 @@ class Oracle {
         if (vr->type == ZBHIP_DOC_BOOL) { r.k = V_BOOL; r.b = vr->value != 0; return r; }
         if (vr->type == ZBHIP_DOC_INT) { r.k = V_NUM; r.n = (__int128)vr->value * kScale18; return r; }
         if (vr->type == ZBHIP_DOC_DEC) { r.k = V_NUM; r.n = (__int128)vr->value * (kScale18 / 1000000); return r; }
+        if (vr->type == ZBHIP_DOC_STR) { r.k = V_STR; return r; }  // (the text is never compared)
         r.k = V_ERR;
         return r;
       }
@@ -2565,11 +2616,19 @@ class Oracle {
         const std::string& c = e->cmp;
         if (c == "=" || c == "!=") {
           bool eq;
+          if (a.k == V_STR || b.k == V_STR) throw Unsupported{"string equality"};
           if (a.k == V_NULL || b.k == V_NULL) eq = a.k == b.k;
           else if (a.k != b.k) throw Unsupported{"comparison of mixed types"};
           else eq = a.k == V_NUM ? a.n == b.n : a.b == b.b;
           r.k = V_BOOL;
           r.b = c == "=" ? eq : !eq;
+          return r;
+        }
+        // feel-scala 1.17: an ordering comparison with null, or of a string with a number, is null
+        // (ConditionIncidentTest.shouldCreateIncidentIfConditionFailsToEvaluate: `foo > 10` with
+        // foo = "bar" was 'NULL')
+        if (a.k == V_NULL || b.k == V_NULL || (a.k == V_STR && b.k == V_NUM) || (a.k == V_NUM && b.k == V_STR)) {
+          r.k = V_NULL;
           return r;
         }
         if (a.k != V_NUM || b.k != V_NUM) throw Unsupported{"ordering comparison with non-number"};
@@ -2795,6 +2854,19 @@ std::string Oracle::dump_state() const {
       rows.push_back(buf);
     }
   }
+  for (auto& [k, in] : incidents_) {  // INCIDENTS (DbIncidentState.createIncident)
+    const OProc& p = procs[in.pi.proc];
+    snprintf(buf, sizeof buf,
+             "INCIDENTS|%lld|errorType=%d,flow=%d,result=%d,processDefinitionKey=%lld,processInstanceKey=%lld,"
+             "elementId=%s,elementInstanceKey=%lld",
+             (long long)k, in.error_type, in.flow, in.result, (long long)p.def_key, (long long)in.pi.piKey,
+             p.els[in.pi.elem].id.c_str(), (long long)in.eik);
+    rows.push_back(buf);
+  }
+  for (auto& [e, k] : incident_pi_) {
+    snprintf(buf, sizeof buf, "INCIDENT_PROCESS_INSTANCES|%lld|%lld", (long long)e, (long long)k);
+    rows.push_back(buf);
+  }
   for (auto& [t, ten, k] : activatable_) {
     snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|%s|%lld", t.c_str(), ten.c_str(), (long long)k);
     rows.push_back(buf);
@@ -2866,6 +2938,12 @@ int zbo_element_info(void* o, int proc, int elem, int* type, int* event, int* re
   *retries = e.retries;
   return 0;
 }
+const char* zbo_element_cond_text(void* o, int proc, int elem) {
+  auto* z = static_cast<Oracle*>(o);
+  if (proc < 0 || (size_t)proc >= z->procs.size() || elem < 0 || (size_t)elem >= z->procs[proc].els.size()) return "";
+  return z->procs[proc].els[elem].cond_text.c_str();
+}
+
 const char* zbo_element_job_type(void* o, int proc, int elem) {
   return static_cast<Oracle*>(o)->procs.at(proc).els.at(elem).job_type.c_str();
 }

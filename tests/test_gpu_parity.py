@@ -237,15 +237,19 @@ def test_linear_segments_mixed_with_general_path():
     assert phase >= 3
 
 
-def test_missing_variable_falls_back_and_leaves_instance_untouched():
+def test_condition_outside_the_subset_falls_back_and_leaves_instance_untouched():
+    # `amount > 1000` over a boolean: outside the device's FEEL subset (a missing amount is NULL and
+    # raises an incident on the device, tests/test_gpu_incidents.py)
     xml = bpmn.xor_process()
     part = Partition(max_instances=8, max_commands=8)
     part.deploy(xml)
     name = part.intern("amount")
     cmds = create_commands(4, 0)
-    cmds["doc_count"] = [1, 0, 1, 1]
-    cmds["doc_begin"] = [0, 0, 1, 2]
-    part.submit(cmds, amount_docs([5, 2000, 1001], name))
+    cmds["doc_count"] = [1, 1, 1, 1]
+    cmds["doc_begin"] = [0, 3, 1, 2]
+    docs = amount_docs([5, 2000, 1001, 1], name)
+    docs[3]["type"] = abi.DOC_BOOL
+    part.submit(cmds, docs)
     part.run()
     assert part.fallback() == [1]
     recs = part.drain()

@@ -233,14 +233,15 @@ def test_exclusive_gateway_decimal_and_boundaries():
     assert taken == ["high", "low", "low"]
 
 
-def test_exclusive_gateway_missing_variable_is_unsupported():
-    # a null operand of `>` makes the result non-boolean -> incident in the reference
-    # (ExpressionProcessor.java:356-368): outside the supported subset, flagged
+def test_exclusive_gateway_missing_variable_raises_an_incident():
+    # a null operand of `>` makes the result NULL, not a boolean -> incident EXTRACT_VALUE_ERROR
+    # (ExpressionProcessor.java:356-368; tests/test_oracle_incidents.py pins the records)
     o = Oracle()
     proc = o.deploy(bpmn.xor_process())
     o.submit(create_commands(1, proc))
-    with pytest.raises(OracleError):
-        o.run()
+    o.run()
+    recs = o.records()
+    assert int(recs[-1]["value_type"]) == abi.VT_INCIDENT and int(recs[-1]["partition"]) == abi.ERR_EXTRACT_VALUE_ERROR
 
 
 def test_exclusive_gateway_no_outgoing_flow_completes_scope():

@@ -19,6 +19,10 @@ VT_PROCESS_INSTANCE_CREATION = 19
 VT_PROCESS_EVENT = 24
 VT_TIMER = 15
 VT_PROCESS_INSTANCE_BATCH = 34
+VT_INCIDENT = 6
+INCIDENT_CREATED = 0
+ERR_CONDITION_ERROR, ERR_EXTRACT_VALUE_ERROR = 3, 4  # ErrorType ordinals
+FEEL_NULL, FEEL_NUMBER, FEEL_STRING = 0, 1, 2       # zbhip_record.reason_arg of an INCIDENT
 
 REJ_INVALID_ARGUMENT, REJ_NOT_FOUND, REJ_ALREADY_EXISTS, REJ_INVALID_STATE = 0, 1, 2, 3
 REJ_PROCESSING_ERROR, REJ_NONE = 4, 255
@@ -30,6 +34,7 @@ PI_INTENTS = {
     7: "ELEMENT_TERMINATED", 8: "ACTIVATE_ELEMENT", 9: "COMPLETE_ELEMENT", 10: "TERMINATE_ELEMENT",
 }
 PI_INTENT_IDS = {v: k for k, v in PI_INTENTS.items()}
+PI_SEQUENCE_FLOW_TAKEN, PI_ELEMENT_ACTIVATING, PI_ELEMENT_ACTIVATED = 1, 2, 3
 JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED", 10: "CANCELED"}
 JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED, JOB_CANCELED = 0, 1, 2, 10
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}

@@ -322,6 +322,12 @@ class GpuBatchProcessor:
         i = self.window.index_of(record.position) if self.window.covers(record.position) else -1
         if i < 0:
             if not self._hot(record, 0):
+                # a command the device does not run for an instance it holds (INCIDENT:RESOLVE of a
+                # gateway's incident, PROCESS_INSTANCE:CANCEL, ...): the instance moves to the engine first
+                held = self._held_instance(record)
+                if held is not None:
+                    self._hand_off(held)
+                    self.key_generator.set_key_if_higher(self.part.current_key())
                 self.engine_batch = True
                 self.counts["engine_commands"] += 1
                 return self.engine.process(record, out)
@@ -483,8 +489,28 @@ class GpuBatchProcessor:
             self.part.set_external_keys(i, self.key_generator.current_key() - before)
 
     # ---- fallback hand-off (Engine.java:134, ProcessingStateMachine.java:276-310) ----
+    def _held_instance(self, record):
+        """the device instance slot a non-hot-path command addresses by its key or its value's
+        processInstanceKey, or None"""
+        for k in (record.key, (record.value or {}).get("processInstanceKey", -1)):
+            if k is not None and k >= 0:
+                ref = self._resolve(k)
+                if ref is not None:
+                    return ref[0]
+        return None
+
     def _fall_back(self, i, record, out):
         inst = self.window.instances[i]
+        self._hand_off(inst)
+        before = self.part.key_before(i)
+        self.key_generator.set_key_if_higher(before)
+        self.engine_batch = True
+        self.pending_declaration = (i, before)
+        # the engine's keys are declared when its batch (follow-ups included) is done
+        out.append_post_commit_task(self._batch_done)
+        return self.engine.process(record, out)
+
+    def _hand_off(self, inst):
         if inst not in self.handed_off:
             # the instance's zb-db rows into the engine's state (the platform's transaction), then off
             # the device with its waiting continuations (the engine reads them back from the log)
@@ -498,13 +524,6 @@ class GpuBatchProcessor:
             self.continuations = [c for c in self.continuations if c[1] != inst]
             self.used_slots.discard(inst)
             self.ended.discard(inst)
-        before = self.part.key_before(i)
-        self.key_generator.set_key_if_higher(before)
-        self.engine_batch = True
-        self.pending_declaration = (i, before)
-        # the engine's keys are declared when its batch (follow-ups included) is done
-        out.append_post_commit_task(self._batch_done)
-        return self.engine.process(record, out)
 
     # ---- job activation (JobBatchActivateProcessor.java:60-143) ------------------------------------
     def _activate_jobs(self, record, out):

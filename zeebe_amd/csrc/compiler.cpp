@@ -314,6 +314,8 @@ struct Compiled {
   std::vector<zbhip_element> elements;
   std::vector<uint16_t> out_flow;
   std::vector<uint32_t> cond_begin;
+  std::vector<std::string> cond_texts;
+  std::vector<const char*> cond_ptrs;
   std::vector<zbhip_insn> code;
   std::vector<std::string> strings;
   std::vector<const char*> string_ptrs;
@@ -336,6 +338,9 @@ struct Compiled {
     csr.out_flow = out_flow.data();
     csr.n_conditions = cond_begin.empty() ? 0 : (uint32_t)cond_begin.size() - 1;
     csr.cond_begin = cond_begin.data();
+    cond_ptrs.clear();
+    for (auto& t : cond_texts) cond_ptrs.push_back(t.c_str());
+    csr.cond_text = cond_ptrs.data();
     csr.n_code = (uint32_t)code.size();
     csr.code = code.data();
     csr.n_strings = (uint32_t)strings.size();
@@ -800,6 +805,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       if (!fc.compile(err)) return ZBHIP_EUNSUPP;
       fe.condition = (uint16_t)(C.cond_begin.size() - 1);
       C.cond_begin.push_back((uint32_t)C.code.size());
+      C.cond_texts.push_back(body);  // FeelExpressionLanguage.parseExpression: group(1) of "\\=(.+)"
     }
     out_lists[fe.flow_source].push_back(fi);
     in_lists[fe.flow_target].push_back(fi);
@@ -818,6 +824,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     end.op = ZBHIP_OP_END;
     C.code.push_back(end);
     C.cond_begin.push_back((uint32_t)C.code.size());
+    C.cond_texts.emplace_back();
   }
   // CSR of outgoing lists
   for (size_t e = 0; e < C.elements.size(); ++e) {

@@ -133,6 +133,7 @@ struct Lane {
   uint16_t first_ord;
   uint16_t trig_key;    // event trigger of a completed job (EVENT_TRIGGER row), NONE if none
   uint16_t trig_evt;    // K::S: the PROCESS_EVENT key ordinal of a boundary event's trigger on trig_key
+  uint32_t inc;         // the incident info of a failed exclusive gateway (find_sequence_flow)
   bool pi_live;
   uint8_t pi_state;
   int pi_child;
@@ -586,8 +587,9 @@ __device__ __forceinline__ void join_set(Lane<K>& L, uint32_t s, uint32_t v) {
 }
 
 // ---- FEEL condition bytecode ------------------------------------------------------------------
-// Values: tag 0 NULL, 1 BOOL, 2 NUMBER (x 10^ZBHIP_DEC_SCALE).  Results that are not boolean
-// raise an incident in the reference (ExpressionProcessor.java:356-368) -> fallback.
+// Values: tag 0 NULL, 1 BOOL, 2 NUMBER (x 10^ZBHIP_DEC_SCALE), 3 STRING (never compared: an ordering
+// comparison of a string with a number is NULL in feel-scala 1.17, ConditionIncidentTest).  A result
+// that is not a boolean is an incident in the reference (ExpressionProcessor.java:356-368).
 // The operand stack is four registers, top first (the compiler bounds the depth to 4).
 template <class K>
 __device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32_t scope_key, uint32_t& t,
@@ -609,11 +611,13 @@ __device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32
     return true;
   }
   if (ty == ZBHIP_DOC_DEC) { t = 2; x = raw; return true; }
+  if (ty == ZBHIP_DOC_STR) { t = 3; return true; }
   return false;
 }
 
+// result: -1 outside the subset (fallback), else the tag of the value (1: boolean, in `out`)
 template <class K>
-__device__ __forceinline__ bool eval_condition(Lane<K>& L, uint32_t cond, uint32_t scope_key, bool& out) {
+__device__ __forceinline__ int eval_condition(Lane<K>& L, uint32_t cond, uint32_t scope_key, bool& out) {
   const uint32_t* pb = L.pb;
   uint32_t pc = pb[pb[3] + cond];
   const uint32_t* code = pb + pb[4];
@@ -629,45 +633,56 @@ __device__ __forceinline__ bool eval_condition(Lane<K>& L, uint32_t cond, uint32
       long long x = 0;
       if (op == ZBHIP_OP_PUSH_NUM) { t = 2; x = (long long)(((unsigned long long)in.w << 32) | in.z); }
       else if (op == ZBHIP_OP_PUSH_BOOL) { t = 1; x = in.y != 0; }
-      else if (op == ZBHIP_OP_PUSH_VAR) { if (!load_var(L, in.y, scope_key, t, x)) return false; }
-      if (sp >= 4) return false;
+      else if (op == ZBHIP_OP_PUSH_VAR) { if (!load_var(L, in.y, scope_key, t, x)) return -1; }
+      if (sp >= 4) return -1;
       t3 = t2; a3 = a2; t2 = t1; a2 = a1; t1 = t0; a1 = a0; t0 = t; a0 = x;
       ++sp;
       continue;
     }
     if (op == ZBHIP_OP_NOT) {
-      if (sp < 1 || t0 != 1) return false;
+      if (sp < 1 || t0 != 1) return -1;
       a0 = !a0;
       continue;
     }
-    if (sp < 2) return false;
+    if (sp < 2) return -1;
     // binary: a = second, b = top
     const uint32_t ta = t1, tb = t0;
     const long long a = a1, b = a0;
-    bool r;
+    uint32_t rt = 1;
+    bool r = false;
     if (op == ZBHIP_OP_AND || op == ZBHIP_OP_OR) {
-      if (ta != 1 || tb != 1) return false;
+      if (ta != 1 || tb != 1) return -1;
       r = op == ZBHIP_OP_AND ? (a && b) : (a || b);
     } else if (op == ZBHIP_OP_EQ || op == ZBHIP_OP_NE) {
       bool eq;
+      if (ta == 3 || tb == 3) return -1;
       if (ta == 0 || tb == 0) eq = ta == tb;
-      else if (ta != tb) return false;
+      else if (ta != tb) return -1;
       else eq = a == b;
       r = op == ZBHIP_OP_EQ ? eq : !eq;
+    } else if (ta == 0 || tb == 0 || (ta == 3 && tb == 2) || (ta == 2 && tb == 3)) {
+      rt = 0;  // null
     } else {
-      if (ta != 2 || tb != 2) return false;
+      if (ta != 2 || tb != 2) return -1;
       r = op == ZBHIP_OP_LT ? a < b : op == ZBHIP_OP_LE ? a <= b : op == ZBHIP_OP_GT ? a > b : a >= b;
     }
-    t0 = 1; a0 = r;
+    t0 = rt; a0 = r;
     t1 = t2; a1 = a2; t2 = t3; a2 = a3;
     --sp;
   }
-  if (sp != 1 || t0 != 1) return false;
-  out = a0 != 0;
-  return true;
+  if (sp != 1) return -1;
+  out = t0 == 1 && a0 != 0;
+  return (int)t0;
 }
 
-// ExclusiveGatewayProcessor.findSequenceFlowToTake (:86-126)
+// An exclusive gateway's incident (incident info in the element-table entry, bits 26..31): the
+// position of the flow whose condition was not a boolean in the gateway's outgoing list (0..14) or
+// 15 (none chosen, CONDITION_ERROR) | the ZBHIP_FEEL_* type of that result << 4
+constexpr uint16_t FLOW_INCIDENT = 0xFFFE;
+constexpr uint32_t INC_NONE_CHOSEN = 15;
+
+// ExclusiveGatewayProcessor.findSequenceFlowToTake (:86-126); a failure returns FLOW_INCIDENT with
+// the incident info in L.inc
 template <class K>
 __device__ __forceinline__ uint32_t find_sequence_flow(Lane<K>& L, uint4 gw, uint32_t gw_key) {
   uint32_t ob = gw.y & 0xFFFF, oc = gw.y >> 16;
@@ -679,12 +694,17 @@ __device__ __forceinline__ uint32_t find_sequence_flow(Lane<K>& L, uint4 gw, uin
     uint32_t cond = elem_of(L, f).z >> 16;
     if (cond == NONE || f == dflt) continue;  // outgoingWithCondition, default skipped
     bool ok;
-    if (!eval_condition(L, cond, gw_key, ok)) { set_fail(L, FB_FEEL); return NONE; }
+    const int rt = eval_condition(L, cond, gw_key, ok);
+    if (rt < 0 || (rt != 1 && i >= INC_NONE_CHOSEN)) { set_fail(L, FB_FEEL); return NONE; }
+    if (rt != 1) {  // typeCheck: EXTRACT_VALUE_ERROR
+      L.inc = i | ((rt == 0 ? ZBHIP_FEEL_NULL : rt == 2 ? ZBHIP_FEEL_NUMBER : ZBHIP_FEEL_STRING) << 4);
+      return FLOW_INCIDENT;
+    }
     if (ok) return f;
   }
   if (dflt != NONE) return dflt;
-  set_fail(L, FB_NO_CONDITION);
-  return NONE;
+  L.inc = INC_NONE_CHOSEN;  // NO_OUTGOING_FLOW_CHOSEN_ERROR (:121-125), CONDITION_ERROR
+  return FLOW_INCIDENT;
 }
 
 // ---- appliers ------------------------------------------------------------------------------
@@ -1403,6 +1423,17 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         if constexpr (!K::X) { set_fail(L, FB_UNSUPPORTED); return; }
         uint32_t flow = find_sequence_flow(L, w, key);
         if (L.fail) return;
+        if (flow == FLOW_INCIDENT) {
+          // BpmnIncidentBehavior.createIncident (behavior/BpmnIncidentBehavior.java:51-71): INCIDENT:CREATED
+          // (key = nextKey), IncidentCreatedApplier; the gateway stays ELEMENT_ACTIVATING (a persistent
+          // element instance: its job field holds the incident key, bits 26..31 the incident info)
+          const uint32_t ik = new_key(L);
+          emit(L, C_INCIDENT_CREATED, ik, key, elem, L.inc);
+          uint2 e = tget(L, t);
+          e.y = (ik & 0xFFFF) | (e.y & 0x00FF0000u) | (L.inc << 26);
+          tput(L, t, e);
+          return;
+        }
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
         emit(L, ZBHIP_PI_ELEMENT_COMPLETING, key, fsa, elem);
         transition_to_completed_child(L, t, elem, w, key);

@@ -109,6 +109,7 @@ struct SerElement {
   uint8_t type = 0, event = 0;
   std::string id;
   uint32_t duration_ms = 0;  // timer catch / boundary event (the device log path's TIMER dueDates)
+  std::string cond_text;     // sequence flow: its condition's FEEL text (incident messages)
   // ProcessInstanceRecord: [map, bpmnElementType .. processDefinitionKey, "processInstanceKey"] key
   // ["flowScopeKey"] key [bpmnEventType .. tenantId]
   Bytes pi_head, pi_tail;
@@ -195,6 +196,9 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
     S.event = E.element_type == ZBHIP_EL_PROCESS ? ZBHIP_EV_UNSPECIFIED : E.event_type;
     S.id = str(E.id);
     S.duration_ms = E.duration_ms;
+    if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW && E.condition != ZBHIP_NONE16 && csr->cond_text &&
+        E.condition < csr->n_conditions && csr->cond_text[E.condition])
+      S.cond_text = csr->cond_text[E.condition];
     // ProcessInstanceRecord (declaration order ProcessInstanceRecord.java:63-73)
     mp_map(S.pi_head, 11);
     key(S.pi_head, "bpmnElementType");
@@ -253,6 +257,33 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
   if (idx_out) *idx_out = (uint32_t)s->procs.size();
   s->procs.push_back(std::move(P));
   return ZBHIP_OK;
+}
+
+// The errorMessage of an exclusive gateway's incident (BpmnIncidentBehavior.createIncident with the
+// Failure of ExclusiveGatewayProcessor.findSequenceFlowToTake, :86-126): CONDITION_ERROR
+// NO_OUTGOING_FLOW_CHOSEN_ERROR (:121-125), or ExpressionProcessor.typeCheck's EXTRACT_VALUE_ERROR
+// (ExpressionProcessor.java:356-368) for the flow whose condition was not a boolean.
+static bool incident_message(const zbhip_serializer* s, int32_t proc, int32_t error_type, int64_t flow,
+                             uint32_t result, std::string& out) {
+  if (error_type == ZBHIP_ERR_CONDITION_ERROR) {
+    out = "Expected at least one condition to evaluate to true, or to have a default flow";
+    return true;
+  }
+  if (error_type != ZBHIP_ERR_EXTRACT_VALUE_ERROR || proc < 0 || (size_t)proc >= s->procs.size() || flow < 0 ||
+      (uint64_t)flow >= s->procs[proc].els.size() || result > ZBHIP_FEEL_STRING)
+    return false;
+  static const char* const kType[] = {"NULL", "NUMBER", "STRING"};
+  out = "Expected result of the expression '" + s->procs[proc].els[flow].cond_text + "' to be 'BOOLEAN', but was '" +
+        kType[result] + "'.";
+  return true;
+}
+
+int64_t zbhip_serializer_incident_message(zbhip_serializer* s, const zbhip_record* r, char* buf, size_t cap) {
+  if (!s || !r || (cap && !buf) || r->value_type != ZBHIP_VT_INCIDENT) return ZBHIP_EINVAL;
+  std::string m;
+  if (!incident_message(s, r->process_idx, r->partition, r->aux, r->reason_arg, m)) return ZBHIP_EINVAL;
+  if (cap) memcpy(buf, m.data(), std::min(cap, m.size()));
+  return (int64_t)m.size();
 }
 
 const char* zbhip_serializer_name(zbhip_serializer* s, uint32_t id) {
@@ -459,6 +490,24 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         key(value, "processDefinitionKey"); mp_int(value, P ? P->def_key : -1);
         key(value, "tenantId"); key(value, kTenant);
         break;
+      case ZBHIP_VT_INCIDENT: {
+        // IncidentRecord (protocol-impl/.../incident/IncidentRecord.java:36-47, declaration order)
+        std::string msg;
+        if (!E || !incident_message(s, r.process_idx, r.partition, r.aux, r.reason_arg, msg)) return ZBHIP_EINVAL;
+        mp_map(value, 10);
+        key(value, "errorType");
+        key(value, r.partition == ZBHIP_ERR_CONDITION_ERROR ? "CONDITION_ERROR" : "EXTRACT_VALUE_ERROR");
+        key(value, "errorMessage"); mp_str(value, msg);
+        key(value, "bpmnProcessId"); mp_str(value, P->bpmn_id);
+        key(value, "processDefinitionKey"); mp_int(value, P->def_key);
+        key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
+        key(value, "elementId"); mp_str(value, E->id);
+        key(value, "elementInstanceKey"); mp_int(value, r.scope_key);
+        key(value, "jobKey"); mp_int(value, -1);
+        key(value, "variableScopeKey"); mp_int(value, r.scope_key);
+        key(value, "tenantId"); key(value, kTenant);
+        break;
+      }
       case ZBHIP_VT_PROCESS_INSTANCE_BATCH:
         mp_map(value, 3);  // ProcessInstanceBatchRecord.java:38-40
         key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);
@@ -755,6 +804,35 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     key(v, "dueDate"); mp_int(v, ll(f["dueDate"]));
     key(v, "repetitions"); mp_int(v, ll(f["repetitions"]));
     key(v, "tenantId"); mp_str(v, f["tenantId"]);
+  } else if (cf == "INCIDENTS" && need(3)) {
+    ord = 34;  // DbIncidentState: DbLong incidentKey -> Incident{incidentRecord} (Incident.java:17-22)
+    auto f = fields_of(p[2]);
+    const int64_t def = ll(f["processDefinitionKey"]);
+    int32_t pi = -1;
+    for (size_t q = 0; q < s->procs.size(); ++q)
+      if (s->procs[q].def_key == def) { pi = (int32_t)q; break; }
+    std::string msg;
+    if (pi < 0 || !incident_message(s, pi, (int32_t)ll(f["errorType"]), ll(f["flow"]), (uint32_t)ll(f["result"]), msg))
+      return ZBHIP_EINVAL;
+    const SerProcess& P = s->procs[pi];
+    cf_prefix(k, ord); dbl(k, ll(p[1]));
+    mp_map(v, 1);
+    key(v, "incidentRecord");
+    mp_map(v, 10);  // IncidentRecord.java:36-47
+    key(v, "errorType"); key(v, ll(f["errorType"]) == ZBHIP_ERR_CONDITION_ERROR ? "CONDITION_ERROR" : "EXTRACT_VALUE_ERROR");
+    key(v, "errorMessage"); mp_str(v, msg);
+    key(v, "bpmnProcessId"); mp_str(v, P.bpmn_id);
+    key(v, "processDefinitionKey"); mp_int(v, def);
+    key(v, "processInstanceKey"); mp_int(v, ll(f["processInstanceKey"]));
+    key(v, "elementId"); mp_str(v, f["elementId"]);
+    key(v, "elementInstanceKey"); mp_int(v, ll(f["elementInstanceKey"]));
+    key(v, "jobKey"); mp_int(v, -1);
+    key(v, "variableScopeKey"); mp_int(v, ll(f["elementInstanceKey"]));
+    key(v, "tenantId"); key(v, kTenant);
+  } else if (cf == "INCIDENT_PROCESS_INSTANCES" && need(3)) {
+    ord = 35;  // DbForeignKey<DbLong> elementInstanceKey -> IncidentKey{key} (IncidentKey.java)
+    cf_prefix(k, ord); dbl(k, ll(p[1]));
+    mp_map(v, 1); key(v, "key"); mp_int(v, ll(p[2]));
   } else if (cf == "TIMER_DUE_DATES" && need(4)) {
     ord = 13;  // [dueDate, [elementInstanceKey, timerKey]] -> DbNil
     cf_prefix(k, ord); dbl(k, ll(p[1])); dbl(k, ll(p[2])); dbl(k, ll(p[3]));

@@ -2067,6 +2067,22 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.intent = ZBHIP_PIC_CREATED;
       r.record_type = ZBHIP_RT_EVENT;
       r.aux = doc;
+    } else if (c6 == C_INCIDENT_CREATED) {
+      // BpmnIncidentBehavior.createIncident: elementInstanceKey = variableScopeKey = the gateway's
+      // (scope_key); the ErrorType in partition, the failing flow in aux, its result type in reason_arg
+      const Proc* P = proc != NONE ? &h->procs[proc] : nullptr;
+      if (!P || elem >= P->els.size()) return ZBHIP_EDEVICE;
+      const zbhip_element& G = P->els[elem];
+      const uint32_t pos = fl & 15;
+      r.value_type = ZBHIP_VT_INCIDENT;
+      r.intent = ZBHIP_INCIDENT_CREATED;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.partition = pos == 15 ? ZBHIP_ERR_CONDITION_ERROR : ZBHIP_ERR_EXTRACT_VALUE_ERROR;
+      if (pos != 15) {
+        if (pos >= G.out_count || (size_t)G.out_begin + pos >= P->out.size()) return ZBHIP_EDEVICE;
+        r.aux = P->out[G.out_begin + pos];
+        r.reason_arg = (uint8_t)(fl >> 4);
+      }
     } else if (c6 == C_TIMER_CANCELED) {
       // CatchEventBehavior.unsubscribeFromTimerEvent: the stored timer's dueDate (cmd_due)
       r.value_type = ZBHIP_VT_TIMER;
@@ -2419,6 +2435,11 @@ int zbhip_submit_xparts_device(zbhip_handle* h, const zbhip_xpart_cmd* dev_xpart
   return zbhip_submit_device_ex(h, reinterpret_cast<const zbhip_command*>(h->d_cmds), n, nullptr, 0, dev_xparts, n);
 }
 
+int64_t zbhip_incident_message(zbhip_handle* h, const zbhip_record* r, char* out, size_t cap) {
+  if (!h || !h->ser) return ZBHIP_EINVAL;
+  return zbhip_serializer_incident_message(h->ser, r, out, cap);
+}
+
 int zbhip_string_partitions(zbhip_handle* h, const uint32_t* ids, size_t n, int32_t partition_count, int32_t* out) {
   if (!h || partition_count <= 0 || (n && (!ids || !out))) return ZBHIP_EINVAL;
   for (size_t i = 0; i < n; ++i) {
@@ -2509,7 +2530,9 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     const bool body = E.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY;  // childCount | loop counter << 8
     const Proc::Mi* im = P.mi_inner(elem);  // a multi-instance inner instance: its loop counter in the flags
     const bool jw = ZBHIP_IS_JOB_WORKER(E.element_type);
-    const long long jk = sub || body || (im && !jw) ? 0 : job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
+    // an exclusive gateway waits only with an incident: its job field is the incident key
+    const bool xgw = E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY;
+    const long long jk = sub || body || xgw || (im && !jw) ? 0 : job == JOB_ZERO ? 0 : job == JOB_MINUS1 ? -1 : h->key_of(inst, job);
     const long long fs = scope_key(E.flow_scope);
     const uint32_t child = sub || body ? job & 0xFF : 0u, loop = body ? (job >> 8) & 0xFF : im ? e.y >> 26 : 0u;
     snprintf(buf, sizeof buf,
@@ -2537,6 +2560,19 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     sink(ctx, buf);
     snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_CHILD_PARENT|%lld|%lld", k, fs);
     sink(ctx, buf);
+    if (xgw) {  // IncidentCreatedApplier -> DbIncidentState.createIncident (INCIDENTS, INCIDENT_PROCESS_INSTANCES)
+      const uint32_t info = e.y >> 26, pos = info & 15;
+      const long long ik = h->key_of(inst, job);
+      const int flow = pos == 15 || (size_t)E.out_begin + pos >= P.out.size() ? -1 : (int)P.out[E.out_begin + pos];
+      snprintf(buf, sizeof buf,
+               "INCIDENTS|%lld|errorType=%d,flow=%d,result=%u,processDefinitionKey=%lld,processInstanceKey=%lld,"
+               "elementId=%s,elementInstanceKey=%lld",
+               ik, pos == 15 ? ZBHIP_ERR_CONDITION_ERROR : ZBHIP_ERR_EXTRACT_VALUE_ERROR, flow, pos == 15 ? 0u : info >> 4,
+               (long long)P.def_key, pik, P.id(elem).c_str(), k);
+      sink(ctx, buf);
+      snprintf(buf, sizeof buf, "INCIDENT_PROCESS_INSTANCES|%lld|%lld", k, ik);
+      sink(ctx, buf);
+    }
     if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
         E.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
       // EventScopeInstance.java:25-35: a catch / boundary event's interrupting ids are its own id
@@ -3036,6 +3072,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       if (c->type == ZBHIP_EL_SUB_PROCESS && (c->child_count < 0 || c->child_count > 255 || c->asf < 0 || c->asf > 255))
         return ZBHIP_EUNSUPP;
       if (c->terminated != 0) return ZBHIP_EUNSUPP;
+      // an exclusive gateway waits only with an incident (INCIDENTS rows are not imported): CPU engine
+      if (c->type == ZBHIP_EL_EXCLUSIVE_GATEWAY) return ZBHIP_EUNSUPP;
       if (c->type == ZBHIP_EL_MULTI_INSTANCE_BODY &&  // childActivatedCount = loop, completed = loop - active
           (c->loop < 0 || c->loop > (int64_t)kMaxMiItems || c->asf != 0 || c->activated != c->loop ||
            c->child_count < 0 || c->completed != c->loop - c->child_count))

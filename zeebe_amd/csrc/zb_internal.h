@@ -91,7 +91,10 @@ enum : uint8_t {
   C_TIMER_TRIGGER = 53,   // (rejections of TIMER:TRIGGER)
   C_TIMER_TRIGGERED = 54,
   C_TIMER_CANCELED = 55,  // CatchEventBehavior.unsubscribeFromTimerEvent; dueDate in StepParams.cmd_due
-  C_TIMER_NEXT = 56,      // TIMER:CREATED of a cycle's next timer (rescheduleTimer): dueDate from the
+  C_TIMER_NEXT = 56,
+  C_INCIDENT_CREATED = 57,  // INCIDENT:CREATED of an exclusive gateway: key = incident, aux = the gateway's
+                            // element instance, elem = the gateway, flags = the incident info (kernels.hip
+                            // find_sequence_flow: flow position 0..14 / 15 none chosen | FEEL type << 4)      // TIMER:CREATED of a cycle's next timer (rescheduleTimer): dueDate from the
                           // TRIGGER command's, not the run's clock
   kRejectBit = 0x40,
 };

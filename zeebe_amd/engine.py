@@ -271,6 +271,18 @@ class Partition:
         self.L.zbhip_rejection_reason(self.h, C.byref(r), buf, 512)
         return buf.value.decode()
 
+    def incident_message(self, rec):
+        """errorMessage of a drained INCIDENT record (zbhip_incident_message)."""
+        r = abi.Record()
+        for f, _ in abi.Record._fields_:
+            if f != "pad":
+                setattr(r, f, int(rec[f]))
+        buf = C.create_string_buffer(1024)
+        n = self.L.zbhip_incident_message(self.h, C.byref(r), buf, 1024)
+        if n < 0 or n > 1024:
+            raise ValueError("zbhip_incident_message: %d" % n)
+        return buf.raw[:n].decode()
+
     def stats(self):
         s = abi.Stats()
         check(self.L.zbhip_get_stats(self.h, C.byref(s)))

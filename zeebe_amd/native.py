@@ -19,13 +19,13 @@ ERRORS = {-1: "ZBHIP_EINVAL", -2: "ZBHIP_ENOMEM", -3: "ZBHIP_EDEVICE", -4: "ZBHI
 SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", "zbhip_deploy", "zbhip_intern",
            "zbhip_string", "zbhip_name", "zbhip_submit", "zbhip_submit_device", "zbhip_run", "zbhip_set_clock", "zbhip_drain",
            "zbhip_pending_records", "zbhip_get_stats", "zbhip_export_state", "zbhip_fallback",
-           "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_build_info", "zbhip_command_status",
+           "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_incident_message", "zbhip_build_info", "zbhip_command_status",
            "zbhip_submit_ex", "zbhip_submit_device_ex", "zbhip_intern_string", "zbhip_intern_strings",
            "zbhip_string_value", "zbhip_subscription_partition", "zbhip_outbox", "zbhip_outbox_device",
            "zbhip_outbox_copy", "zbhip_submit_xparts_device", "zbhip_string_partitions",
            "zbhip_serializer_new", "zbhip_serializer_free", "zbhip_serializer_deploy", "zbhip_serializer_intern",
            "zbhip_serializer_intern_string", "zbhip_serializer_set_broker_version",
-           "zbhip_serializer_rejection_reason", "zbhip_handle_serializer", "zbhip_serialize_log",
+           "zbhip_serializer_rejection_reason", "zbhip_serializer_incident_message", "zbhip_handle_serializer", "zbhip_serialize_log",
            "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream",
            "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
            "zbhip_set_external_keys", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
@@ -81,6 +81,8 @@ def load():
     L.zbhip_fallback.argtypes = [vp, C.POINTER(u32), sz, C.POINTER(sz)]
     L.zbhip_resolve_key.argtypes = [vp, i64, C.POINTER(u32), C.POINTER(C.c_uint16)]
     L.zbhip_rejection_reason.argtypes = [vp, C.POINTER(abi.Record), C.c_char_p, sz]
+    L.zbhip_incident_message.argtypes = [vp, C.POINTER(abi.Record), C.c_char_p, sz]
+    L.zbhip_incident_message.restype = i64
     L.zbhip_command_status.argtypes = [vp, sz, C.POINTER(u32), C.POINTER(u32)]
     L.zbhip_submit_ex.argtypes = [vp, vp, sz, vp, sz, vp, sz]
     L.zbhip_submit_device_ex.argtypes = [vp, vp, sz, vp, sz, vp, sz]
