@@ -594,6 +594,19 @@ int64_t zbhip_serializer_incident_message(zbhip_serializer* s, const zbhip_recor
 zbhip_serializer* zbhip_handle_serializer(zbhip_handle* h);
 
 /* The window the records were drained from, and the log positions of its batches. */
+/* The TimerRecord of a TIMER:TRIGGER command as DueDateTimerChecker wrote it
+ * (engine/.../processing/timer/DueDateTimerChecker.java:118-125: the stored timer's keys, element,
+ * repetitions); a rejection of the command carries it (TypedRejectionWriter.appendRejection). */
+typedef struct zbhip_timer_value {
+  int64_t element_instance_key;
+  int64_t process_instance_key;
+  int64_t process_definition_key;
+  int32_t repetitions;
+  int32_t process_idx;           /* targetElementId = element element_idx of this process; -1 = "" */
+  int32_t element_idx;
+  int32_t pad;
+} zbhip_timer_value;
+
 typedef struct zbhip_log_window {
   const zbhip_command* cmds;       /* the submitted window (record.source_index - source_base) */
   size_t n_cmds;
@@ -606,6 +619,9 @@ typedef struct zbhip_log_window {
   int64_t timestamp;               /* the batches' timestamp (ms) */
   const int64_t* source_timestamps;/* timestamp of each window command (MESSAGE deadline =
                                       PUBLISH timestamp + timeToLive); NULL = timestamp */
+  const zbhip_timer_value* timer_values; /* per window command: a TIMER:TRIGGER's TimerRecord, written
+                                      for its rejection; NULL = the window's key and dueDate only (the
+                                      device form then leaves such windows to the host serialiser) */
 } zbhip_log_window;
 
 /* Serialises n drained records (in drain order) into out.  *used = bytes needed; ZBHIP_ENOMEM if

@@ -351,7 +351,7 @@ def _message_value(r, vt, tables, timestamp):
                                                            elementId=elem))
 
 
-def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
+def record_value(r, tables, docs_of_source, doc_entry, timestamp=0, timer_value=None):
     """msgpack record value of one drained record (fields of zbhip_record)."""
     vt, rt = int(r["value_type"]), int(r["record_type"])
     if vt in (VT_MESSAGE, VT_MS, VT_PMS):
@@ -390,6 +390,16 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
         return write_object(PROCESS_EVENT, dict(scopeKey=int(r["scope_key"]), targetElementId=el[2], variables=pe_vars,
                                                 processDefinitionKey=p["key"],
                                                 processInstanceKey=int(r["process_instance_key"])))
+    if vt == VT_TIMER and rt == RT_REJECTION and timer_value is not None:
+        # the TIMER:TRIGGER command's TimerRecord (DueDateTimerChecker.java:118-125), as the rejection
+        # writer copies it (TypedRejectionWriter.appendRejection)
+        tv = timer_value
+        tp = tables.processes[int(tv["process_idx"])] if int(tv["process_idx"]) >= 0 else None
+        return write_object(TIMER, dict(elementInstanceKey=int(tv["element_instance_key"]),
+                                        processInstanceKey=int(tv["process_instance_key"]), dueDate=int(r["aux"]),
+                                        targetElementId=tp["elements"][int(tv["element_idx"])][2] if tp else "",
+                                        repetitions=int(tv["repetitions"]),
+                                        processDefinitionKey=int(tv["process_definition_key"])))
     if vt == VT_TIMER:  # events: the timer's value (repetitions in `partition`); a rejected TIMER:TRIGGER:
         # the command's key and dueDate (the window's view of it)
         reps = 1 if rt == RT_REJECTION else int(r["partition"])
@@ -416,7 +426,7 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0):
 
 
 def serialize(records, tables, docs_of_source, doc_entry, reason_text, first_position, source_position, timestamp,
-              broker_version=(8, 4, 0), source_timestamp=None):
+              broker_version=(8, 4, 0), source_timestamp=None, timer_value_of=None):
     """The log bytes of the records' batches: records of one source command form one sequenced
     batch (sourcePosition = that command's position), positions consecutive from first_position."""
     out = bytearray()
@@ -427,7 +437,8 @@ def serialize(records, tables, docs_of_source, doc_entry, reason_text, first_pos
         md = record_metadata(rt, int(r["value_type"]), int(r["intent"]), rej, reason, broker_version)
         si = int(r["source_index"])
         value = record_value(r, tables, docs_of_source, doc_entry,
-                             source_timestamp(si) if source_timestamp else timestamp)
+                             source_timestamp(si) if source_timestamp else timestamp,
+                             timer_value_of(si) if timer_value_of else None)
         out += log_entry(int(r["key"]), md, value, first_position + i, source_position(int(r["source_index"])),
                          timestamp, rt == RT_COMMAND and not int(r["unprocessed"]))
     return bytes(out)

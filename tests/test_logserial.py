@@ -116,7 +116,7 @@ class Run:
         self.position = 1000
         self.total = 0
 
-    def window(self, cmds, docs=None):
+    def window(self, cmds, docs=None, timer_values=None):
         docs = docs if docs is not None else abi.make_docs(0)
         self.orc.clear_records()
         self.orc.submit(cmds, docs)
@@ -124,7 +124,8 @@ class Run:
         recs = with_reason_codes(self.orc.records(), self.orc)
         pos = self.position + 10 * np.arange(len(cmds), dtype=np.int64)
         first = int(pos[-1]) + 1 if len(cmds) else self.position
-        got = self.ser.serialize(recs, cmds, docs, self.source_base, self.doc_base, pos, first, 1700000000123)
+        got = self.ser.serialize(recs, cmds, docs, self.source_base, self.doc_base, pos, first, 1700000000123,
+                                 timer_values=timer_values)
         names, strings = self.orc.names(), self.orc.strings()
         tables = LS.Tables(self.orc.process_tables(), lambda i: names[i], lambda i: strings[i])
         sb, db = self.source_base, self.doc_base
@@ -134,9 +135,11 @@ class Run:
             return docs[int(c["doc_begin"]):int(c["doc_begin"]) + int(c["doc_count"])]
 
         want = LS.serialize(recs, tables, docs_of_source, lambda a: docs[a - db], self.orc.reason, first,
-                            lambda si: int(pos[si - sb]), 1700000000123)
+                            lambda si: int(pos[si - sb]), 1700000000123,
+                            timer_value_of=(lambda si: timer_values[si - sb]) if timer_values is not None else None)
         assert got == want
         check_entries(got, recs, first, pos, sb)
+        self.last_bytes = got
         self.source_base += len(cmds)
         self.doc_base += len(docs)
         self.position = first + len(recs)
@@ -338,3 +341,40 @@ def test_serializer_message_correlation(P):
     assert {abi.VT_MESSAGE, abi.VT_MESSAGE_SUBSCRIPTION, abi.VT_PROCESS_MESSAGE_SUBSCRIPTION} <= kinds
     assert ad.windows >= 2 * P
     assert {"PROCESS_SUBSCRIPTION_BY_KEY", "MESSAGE_STATS"} <= ad.state_cfs or P == 1
+
+
+def test_rejected_timer_trigger_carries_the_commands_timer_record():
+    # TriggerTimerProcessor rejects a TIMER:TRIGGER whose timer is gone (NOT_FOUND); the rejection
+    # writer copies the command's TimerRecord, which DueDateTimerChecker.java:118-125 filled with the
+    # stored timer's keys, element, repetitions and process (TypedRejectionWriter.appendRejection)
+    from test_oracle_timers import NOW, timer_process, trigger_commands
+    from zeebe_amd.logwriter import split_entries
+    run = Run([timer_process("PT1M")])
+    run.orc.set_clock(NOW)
+    run.window(create_commands(4, 0))
+    rows = [r.split("|") for r in run.orc.state() if r.startswith("TIMERS|")]
+    f = [dict(kv.split("=") for kv in p[3].split(",")) for p in rows]
+    piks = [int(x["processInstanceKey"]) for x in f]
+    insts = [sorted(piks).index(k) for k in piks]  # instance i's keys follow in log order
+    cmds = trigger_commands(insts, [int(p[2]) - k for p, k in zip(rows, piks)], [int(x["dueDate"]) for x in f])
+    tv = np.zeros(len(cmds), dtype=abi.TIMER_VALUE_DTYPE)
+    tv["element_instance_key"] = [int(x["elementInstanceKey"]) for x in f]
+    tv["process_instance_key"] = piks
+    tv["process_definition_key"] = [int(x["processDefinitionKey"]) for x in f]
+    tv["repetitions"] = [int(x["repetitions"]) for x in f]
+    tv["process_idx"] = 0
+    tv["element_idx"] = [next(e for e in range(20) if run.orc.element_id(0, e) == x["handlerNodeId"]) for x in f]
+    run.window(cmds, timer_values=tv)
+    recs = run.window(cmds, timer_values=tv)  # every timer already triggered: NOT_FOUND
+    assert len(recs) == 4 and (recs["record_type"] == abi.RT_REJECTION).all()
+    buf = run.last_bytes
+    for (off, framed), r in zip(split_entries(buf), recs):
+        e = buf[off + 12:off + framed]
+        mlen = struct.unpack_from("<HBBqqqqHH", e)[7]
+        val = msgpack.unpackb(e[40 + mlen:], raw=False)
+        x = f[int(r["source_index"]) - (run.source_base - len(cmds))]
+        assert val["elementInstanceKey"] == int(x["elementInstanceKey"])
+        assert val["processInstanceKey"] == int(x["processInstanceKey"])
+        assert val["targetElementId"] == x["handlerNodeId"] and val["repetitions"] == int(x["repetitions"])
+        assert val["processDefinitionKey"] == int(x["processDefinitionKey"])
+        assert val["dueDate"] == int(x["dueDate"])

@@ -126,7 +126,14 @@ class XpartCmd(C.Structure):
 class LogWindow(C.Structure):  # zbhip_log_window
     _fields_ = [("cmds", C.c_void_p), ("n_cmds", C.c_size_t), ("source_base", C.c_int64), ("docs", C.c_void_p),
                 ("n_docs", C.c_size_t), ("doc_base", C.c_int64), ("source_positions", C.c_void_p),
-                ("first_position", C.c_int64), ("timestamp", C.c_int64), ("source_timestamps", C.c_void_p)]
+                ("first_position", C.c_int64), ("timestamp", C.c_int64), ("source_timestamps", C.c_void_p),
+                ("timer_values", C.c_void_p)]
+
+
+# zbhip_timer_value: a TIMER:TRIGGER command's TimerRecord (DueDateTimerChecker.java:118-125)
+TIMER_VALUE_DTYPE = np.dtype([("element_instance_key", "<i8"), ("process_instance_key", "<i8"),
+                              ("process_definition_key", "<i8"), ("repetitions", "<i4"), ("process_idx", "<i4"),
+                              ("element_idx", "<i4"), ("pad", "<i4")])
 
 
 OPEN_TRUSTED_DEVICE_WINDOWS = 1

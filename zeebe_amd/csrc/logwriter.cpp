@@ -480,7 +480,22 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
         break;
       case ZBHIP_VT_TIMER:
         // TimerRecord.java:24-40 (CREATED / TRIGGERED: CatchEventBehavior.java:311-319; a rejected
-        // TIMER:TRIGGER: the command's value as far as the window holds it -- its key and dueDate)
+        // TIMER:TRIGGER: the command's value -- DueDateTimerChecker.java:118-125 from the window's
+        // timer_values, else as far as the window holds it: its key and dueDate)
+        if (r.record_type == ZBHIP_RT_REJECTION && w->timer_values) {
+          const zbhip_timer_value& tv = w->timer_values[ci];
+          const SerProcess* TP = tv.process_idx >= 0 && (size_t)tv.process_idx < s->procs.size() ? &s->procs[tv.process_idx] : nullptr;
+          const SerElement* TE = TP && tv.element_idx >= 0 && (size_t)tv.element_idx < TP->els.size() ? &TP->els[tv.element_idx] : nullptr;
+          mp_map(value, 7);
+          key(value, "elementInstanceKey"); mp_int(value, tv.element_instance_key);
+          key(value, "processInstanceKey"); mp_int(value, tv.process_instance_key);
+          key(value, "dueDate"); mp_int(value, r.aux);
+          key(value, "targetElementId"); mp_str(value, TE ? TE->id : std::string());
+          key(value, "repetitions"); mp_int(value, tv.repetitions);
+          key(value, "processDefinitionKey"); mp_int(value, tv.process_definition_key);
+          key(value, "tenantId"); key(value, kTenant);
+          break;
+        }
         mp_map(value, 7);
         key(value, "elementInstanceKey"); mp_int(value, r.scope_key);
         key(value, "processInstanceKey"); mp_int(value, r.process_instance_key);

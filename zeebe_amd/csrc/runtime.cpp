@@ -3548,6 +3548,11 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   if (!fill) h->ring_ok = false;
   h->ring_filled = h->windows_run;  // this window is accounted for, whether or not it is written here
   if (h->msg() || !h->cont_cmds.empty() || h->window_continues) h->ring_ok = false;
+  if (w->timer_values) {  // rejected TIMER:TRIGGERs carry the commands' TimerRecords: the host writes them
+    bool trig = h->h_cmds.size() < h->n_cmds;
+    for (size_t c = 0; c < h->n_cmds && !trig; ++c) trig = h->h_cmds[c].kind == ZBHIP_CMD_TIMER_TRIGGER;
+    if (trig) h->ring_ok = false;
+  }
   if (!h->ring_ok) return ZBHIP_EUNSUPP;
   const bool dbg = getenv("ZBHIP_DEBUG") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };

@@ -95,19 +95,23 @@ class LogSerializer:
         check(self.L.zbhip_serializer_set_broker_version(self.s, major, minor, patch))
 
     def serialize(self, records, cmds, docs=None, source_base=0, doc_base=0, source_positions=None,
-                  first_position=1, timestamp=0, source_timestamps=None):
+                  first_position=1, timestamp=0, source_timestamps=None, timer_values=None):
         """Log bytes of `records` (drain order) drained from the window (cmds, docs).
         source_positions[i] = log position of cmds[i] (default: 1 + i); source_timestamps[i] = its
-        timestamp (default: timestamp)."""
+        timestamp (default: timestamp); timer_values[i] = the TimerRecord of a TIMER:TRIGGER cmds[i]
+        (abi.TIMER_VALUE_DTYPE, written for its rejection)."""
         recs = np.ascontiguousarray(records, dtype=abi.RECORD_DTYPE)
         cmds = np.ascontiguousarray(cmds, dtype=abi.COMMAND_DTYPE)
         docs = np.ascontiguousarray(docs if docs is not None else abi.make_docs(0), dtype=abi.DOC_DTYPE)
         pos = np.ascontiguousarray(source_positions if source_positions is not None
                                    else np.arange(1, len(cmds) + 1), dtype=np.int64)
         ts = (np.ascontiguousarray(source_timestamps, dtype=np.int64) if source_timestamps is not None else None)
+        tv = (np.ascontiguousarray(timer_values, dtype=abi.TIMER_VALUE_DTYPE) if timer_values is not None else None)
+        if tv is not None and len(tv) != len(cmds):
+            raise ValueError("timer_values: one per window command")
         w = abi.LogWindow(cmds.ctypes.data, len(cmds), source_base, docs.ctypes.data if len(docs) else None, len(docs),
                           doc_base, pos.ctypes.data, first_position, timestamp,
-                          ts.ctypes.data if ts is not None else None)
+                          ts.ctypes.data if ts is not None else None, tv.ctypes.data if tv is not None else None)
         used = C.c_size_t()
         check(self.L.zbhip_serialize_log(self.s, recs.ctypes.data, len(recs), C.byref(w), None, 0, C.byref(used)),
               "zbhip_serialize_log")
