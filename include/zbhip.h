@@ -510,6 +510,13 @@ void* zbhip_stream(zbhip_handle* h);
 /* Copies bucketed outbox entries [first, first + count) (zbhip_outbox_device order) to dev_dst,
  * asynchronously on the handle's stream. */
 int zbhip_outbox_copy(zbhip_handle* h, void* dev_dst, size_t first, size_t count);
+/* The exchange of several partitions hosted by one process on one GPU, in one launch: target t's
+ * inbox dst[t] receives, for every source s in partition order, the count[s][t] entries of s's
+ * bucketed outbox (zbhip_outbox_device_async's pointer src[s]) bound for t -- the arrival order of
+ * DeviceExchange.  dev_counts: [P][P] uint32 in device memory (the sources' count rows); max_count
+ * bounds its entries (grid size); P <= 16; launched on `stream` (a hipStream_t, NULL = default). */
+int zbhip_exchange_gather(const zbhip_xpart_cmd* const* src, uint32_t P, const uint32_t* dev_counts,
+                          zbhip_xpart_cmd* const* dst, uint32_t max_count, void* stream);
 /* Receiving side of the exchange: submits the n received commands at dev_xparts (device memory,
  * arrival order) as the next window, building its commands on the device (subject = the PI
  * instance slot for PROCESS_MESSAGE_SUBSCRIPTION commands, the correlation slot otherwise).

@@ -3011,6 +3011,21 @@ __global__ __launch_bounds__(kBucketB) void k_bucket_scatter(BucketParams Q, con
   }
 }
 
+// zbhip_exchange_gather: one block row per (source, target) pair, a grid-stride copy of the pair's
+// 48-byte entries from the source's bucket for the target to its place in the target's inbox
+__global__ __launch_bounds__(256) void k_xgather(XGather A) {
+  const uint32_t s = blockIdx.y / A.P, t = blockIdx.y % A.P;
+  uint32_t so = 0, dof = 0;
+  for (uint32_t q = 0; q < A.P; ++q) {
+    if (q < t) so += A.counts[s * A.P + q];
+    if (q < s) dof += A.counts[q * A.P + t];
+  }
+  const uint32_t n = A.counts[s * A.P + t];
+  const uint4* src = reinterpret_cast<const uint4*>(A.src[s] + so);
+  uint4* dst = reinterpret_cast<uint4*>(A.dst[t] + dof);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < 3 * n; i += gridDim.x * 256) dst[i] = src[i];
+}
+
 // window of received cross-partition commands (exchange receiving side): one command per entry
 __global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -3195,6 +3210,13 @@ hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, 
 
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_xpart_window, dim3((n + 255) / 256), dim3(256), 0, s, xp, n, cmds);
+  return hipGetLastError();
+}
+
+hipError_t launch_xgather(const XGather& A, uint32_t max_count, hipStream_t s) {
+  if (A.P == 0 || max_count == 0) return hipSuccess;
+  const uint32_t gx = std::min<uint32_t>(1024, (3 * max_count + 255) / 256);
+  hipLaunchKernelGGL(k_xgather, dim3(gx, A.P * A.P), dim3(256), 0, s, A);
   return hipGetLastError();
 }
 

@@ -230,7 +230,32 @@ __device__ __forceinline__ bool key_of(const LogParams& L, uint32_t c, uint32_t 
   return true;
 }
 
-__device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const LogCmd& m, uint2 w, Rec& r) {
+// The same for the lane's own command m (in registers): its batch's keys need no memory, and the
+// older keys it names (the process instance, the element instances it continues) are looked up once
+// per command and kept -- every record of a batch repeats them, and re-reading them per record missed
+// L2 under the write stream (PMC: ~200 B fetched per written entry).
+struct KeyCache {
+  uint32_t o0 = NONE, o1 = NONE;
+  long long k0 = -1, k1 = -1;
+};
+__device__ __forceinline__ bool key_of_lane(const LogParams& L, const LogCmd& m, uint32_t ord, long long& key,
+                                            KeyCache& kc) {
+  if (ord == NONE) { key = -1; return true; }
+  if (ord >= m.first_ord && m.nkeys) {
+    key = L.pbits + (long long)(m.key0 + (uint16_t)(ord - m.first_ord));
+    return true;
+  }
+  if (ord == kc.o0) { key = kc.k0; return true; }
+  if (ord == kc.o1) { key = kc.k1; return true; }
+  if (!key_of(L, m.first_ord == 0 ? 0xFFFFFFFFu : m.prev, m.instance, ord, key)) return false;
+  kc.o1 = kc.o0;
+  kc.k1 = kc.k0;
+  kc.o0 = ord;
+  kc.k0 = key;
+  return true;
+}
+
+__device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const LogCmd& m, uint2 w, Rec& r, KeyCache& kc) {
   const uint32_t key_ord = w.x & 0xFFFF, aux_ord = w.x >> 16, elem = w.y & 0xFFFF;
   const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
   const bool rej = code & kRejectBit;
@@ -238,7 +263,8 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
   const uint32_t inst = m.instance;
   r.proc = inst < L.n_inst ? L.inst_proc[inst] : NONE;
   r.elem = elem;
-  if (!key_of(L, c, inst, key_ord, r.key) || !key_of(L, c, inst, aux_ord, r.scope) || !key_of(L, c, inst, 0, r.pik))
+  if (!key_of_lane(L, m, key_ord, r.key, kc) || !key_of_lane(L, m, aux_ord, r.scope, kc) ||
+      !key_of_lane(L, m, 0, r.pik, kc))
     return false;
   r.rej_type = ZBHIP_REJ_NONE;
   r.reason = r.reason_arg = 0;
@@ -577,10 +603,11 @@ __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
   if (c < L.n) {
     const LogCmd m = L.cmds[c];
     Count s;
+    KeyCache kc;
     for (uint32_t j = 0; j < m.nrec; ++j) {
       Rec r;
       uint4 d;
-      if (!decode(L, c, m, L.rows[m.rec_off + j], r)) {
+      if (!decode(L, c, m, L.rows[m.rec_off + j], r, kc)) {
         atomicOr(L.flag, 1u);
         break;
       }
@@ -622,95 +649,171 @@ __device__ __forceinline__ void patch8(unsigned long long& lo, unsigned long lon
   }
 }
 
-// a templated entry, handed from the lane that resolved its keys to the half wave that copies it
-struct TplEnt {
-  unsigned long long dst;
-  long long key, scope, pik, lpos, src;
-  uint32_t off, size, pa, sa;
+// pass 2: the templated entries, written as one byte stream per command.  A half wave (32 lanes)
+// takes a command at a time: lane l resolves record g*32 + l of group g (its template, keys, entry
+// start by a half-wave scan of the entry sizes) into the half wave's LDS slots, then the 32 lanes
+// write the group's bytes as consecutive 16-byte chunks -- every store instruction covers 1 KB of
+// whole lines (entries are 8-aligned, so each 8-byte half of a chunk belongs to one entry; the
+// halves outside the group, or in a composed entry, are left to their writer).  Writing each
+// command's ~4 KB contiguously instead of entry by entry from scattered lanes leaves one partial
+// line per command instead of one per entry.
+struct StreamEnt {
+  unsigned long long start;    // byte offset in the output
+  long long key, scope, pik, lpos;
+  uint32_t off, slow, pa, sa;  // template offset (16-aligned), composed entry, key patch positions
 };
 constexpr uint32_t kLogWriteB = 256;
-constexpr uint32_t kWaveEnts = 128;  // hand-over slots per wave (flushed once 64 are pending)
+constexpr uint32_t kHalf = 32;
 
-// one 16-byte chunk (o16) of a templated entry: template bytes + header fields + value keys
-__device__ __forceinline__ void tpl_chunk(const LogParams& L, uint8_t* out, const TplEnt& e, uint32_t o16,
-                                          unsigned long long ts, ulonglong2 t) {
-  unsigned long long lo = t.x, hi = t.y;
-  if (o16 == 16) { lo = (unsigned long long)e.lpos; hi = (unsigned long long)e.src; }
-  if (o16 == 32) { lo = (unsigned long long)e.key; hi = ts; }
-  if (e.pa) patch8(lo, hi, __builtin_bswap64((unsigned long long)e.pik), (int)e.pa - (int)o16);
-  if (e.sa) patch8(lo, hi, __builtin_bswap64((unsigned long long)e.scope), (int)e.sa - (int)o16);
-  uint8_t* const q = out + e.dst + o16;
-  if (o16 + 16 <= e.size) *reinterpret_cast<ulonglong2*>(q) = make_ulonglong2(lo, hi);
-  else *reinterpret_cast<unsigned long long*>(q) = lo;
+// x (8 bytes in memory order) placed at byte d of an 8-byte word (branch-free; |d| >= 8: unchanged)
+__device__ __forceinline__ unsigned long long patch_word(unsigned long long w, unsigned long long x, int d) {
+  const unsigned long long M = ~0ull;
+  const int sh = 8 * (d < 0 ? -d : d);
+  const unsigned long long keep = d < 0 ? ~(M >> sh) : ~(M << sh);
+  const unsigned long long put = d < 0 ? (x >> sh) : (x << sh);
+  return d <= -8 || d >= 8 ? w : (w & keep) | put;
 }
 
-// pass 2: the templated entries.  Each lane walks its command's records and resolves the keys of
-// the templated ones into the wave's hand-over slots; whenever 64 are pending the wave copies them,
-// two entries per store instruction (lanes 0-31 one, 32-63 the next, 16 B per lane), four in flight.
-__global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t table_words) {
+// the 8-byte word at byte rel (a multiple of 8) of a templated entry: template bytes (`tb`: the
+// templates, LDS-staged), the header's position / source position / key / timestamp, the
+// big-endian process instance and scope keys
+__device__ __forceinline__ unsigned long long tpl_word(const uint8_t* tb, const StreamEnt& e, uint32_t rel,
+                                                       long long src, unsigned long long ts) {
+  unsigned long long w = *reinterpret_cast<const unsigned long long*>(tb + e.off + rel);
+  w = rel == 16 ? (unsigned long long)e.lpos : rel == 24 ? (unsigned long long)src
+      : rel == 32 ? (unsigned long long)e.key : rel == 40 ? ts : w;
+  if (e.pa) w = patch_word(w, __builtin_bswap64((unsigned long long)e.pik), (int)e.pa - (int)rel);
+  if (e.sa) w = patch_word(w, __builtin_bswap64((unsigned long long)e.scope), (int)e.sa - (int)rel);
+  return w;
+}
+
+// Each half wave stages a group of its command's entries -- as many as fit kStage bytes -- in LDS
+// exactly as they go out (template bytes, then the header fields and keys patched in), then copies
+// the stage to the output in 16-byte chunks.  The copy loop issues no vector-memory load, so no
+// s_waitcnt vmcnt (on gfx950 it counts the stores too) holds its streaming stores back; the stores
+// drain once per group, when the next group's template loads are waited for.  Composed entries'
+// bytes are staged as garbage and written over by k_log_compose, which runs after this kernel.
+constexpr uint32_t kStage = 4096;  // bytes per half wave (+16 for the chunk alignment): 3 workgroups per CU
+constexpr uint32_t kStageAlloc = kStage + 16;
+
+__global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  TplEnt* const ents = reinterpret_cast<TplEnt*>(smem + ((table_words + 3) & ~3u));
-  if (table_words) stage_tables(L, smem);  // (0: they do not fit, read from HBM)
-  const uint32_t lane = threadIdx.x & 63;
-  TplEnt* const wents = ents + (threadIdx.x >> 6) * kWaveEnts;
-  const uint32_t c = blockIdx.x * kLogWriteB + threadIdx.x;
-  const bool live = c < L.n;
-  LogCmd m{};
-  if (live) m = L.cmds[c];
-  unsigned long long pos = live ? L.bytes[c] : 0ull;  // byte offset of the lane's next entry
-  const uint32_t nrec = live ? m.nrec : 0u;
-  uint32_t rounds = nrec;  // the wave's largest record count
-  for (int o = 32; o; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
+  const uint32_t lane = threadIdx.x & (kHalf - 1), hw = threadIdx.x / kHalf;
+  StreamEnt* const ents = reinterpret_cast<StreamEnt*>(smem) + hw * kHalf;
+  uint8_t* const stage = reinterpret_cast<uint8_t*>(smem) + (kLogWriteB / kHalf) * kHalf * sizeof(StreamEnt) +
+                         hw * kStageAlloc;
   uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
   const unsigned long long ts = (unsigned long long)L.timestamp;
-  const uint32_t half = lane >> 5, o16 = (lane & 31) * 16;
-  const unsigned long long below = (1ull << lane) - 1;
-  uint32_t cnt = 0;  // pending slots (wave-uniform)
-  for (uint32_t j = 0; j <= rounds; ++j) {
-    if (j < rounds) {
-      bool tpl = false;
-      TplEnt e;
-      if (j < nrec) {
+  const uint32_t c0 = blockIdx.x * kLogWriteB + hw * kHalf;
+  for (uint32_t ci = 0; ci < kHalf; ++ci) {
+    const uint32_t c = c0 + ci;  // (half-wave uniform)
+    if (c >= L.n) break;
+    const LogCmd m = L.cmds[c];
+    unsigned long long gbase = L.bytes[c];
+    KeyCache kc;
+    for (uint32_t g = 0; g < m.nrec;) {
+      const uint32_t j = g + lane;
+      StreamEnt e;
+      e.off = e.pa = e.sa = 0;
+      e.slow = 1;
+      e.key = e.scope = e.pik = e.lpos = 0;
+      uint32_t size = 0;
+      if (j < m.nrec) {
         const uint32_t info = L.rinfo[m.rec_off + j];
+        size = info & 0xFFFF;
         if (!(info & kSlow)) {
           const uint2 w = L.rows[m.rec_off + j];
-          const uint32_t inst = m.instance;
-          tpl = key_of(L, c, inst, w.x & 0xFFFF, e.key) && key_of(L, c, inst, w.x >> 16, e.scope) &&
-                key_of(L, c, inst, 0, e.pik);
           const uint4 d = L.tpl_desc[(info >> 16) - 1];
-          e.dst = pos;
-          e.lpos = L.first_position + (long long)(m.out_rec + j);
-          e.src = m.src_pos;
+          const bool ok = key_of_lane(L, m, w.x & 0xFFFF, e.key, kc) && key_of_lane(L, m, w.x >> 16, e.scope, kc) &&
+                          key_of_lane(L, m, 0, e.pik, kc);
+          e.slow = ok ? 0u : 1u;  // (k_log_sizes flagged a missing key already)
           e.off = d.x;
-          e.size = d.y & 0xFFFF;
           e.pa = d.y >> 16;
           e.sa = d.z;
         }
-        pos += info & 0xFFFF;
+        e.lpos = L.first_position + (long long)(m.out_rec + j);
       }
-      const unsigned long long mask = __ballot(tpl);
-      if (tpl) wents[cnt + (uint32_t)__popcll(mask & below)] = e;
-      cnt += (uint32_t)__popcll(mask);
-      if (cnt < 64 && j + 1 < rounds) continue;
+      // inclusive scan of the entry sizes over the half wave
+      unsigned long long incl = size;
+      for (uint32_t d = 1; d < kHalf; d <<= 1) {
+        const unsigned long long y = __shfl_up(incl, d, kHalf);
+        if (lane >= d) incl += y;
+      }
+      const uint32_t lead = (uint32_t)(gbase & 15);  // stage byte of gbase
+      // the entries of this group: the prefix that fits the stage (at least one)
+      const unsigned long long fits = __ballot(j < m.nrec && lead + incl <= kStage);
+      const uint32_t hmask = (uint32_t)(fits >> (threadIdx.x & 32));
+      uint32_t take = (uint32_t)__builtin_popcount(hmask);
+      const bool staged = take > 0;
+      if (!staged) take = 1;  // one entry larger than the stage: written from the templates directly
+      const unsigned long long gsize = __shfl(incl, take - 1, kHalf);
+      e.start = gbase + incl - size;
+      if (lane < take) ents[lane] = e;
+      const unsigned long long gend = gbase + gsize;
+      if (staged) {
+        if (lane < take && !e.slow) {  // the lane's entry into the stage
+          uint8_t* const dst = stage + lead + (uint32_t)(incl - size);
+          const uint8_t* const src = L.tpl + e.off;
+          const uint32_t n8 = size / 8;
+          uint32_t i = 0;
+          for (; i + 8 <= n8; i += 8) {  // four 16-byte loads in flight per round trip
+            uint4 t[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) t[k] = *reinterpret_cast<const uint4*>(src + 8 * i + 16 * k);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              reinterpret_cast<uint2*>(dst)[i + 2 * k] = make_uint2(t[k].x, t[k].y);
+              reinterpret_cast<uint2*>(dst)[i + 2 * k + 1] = make_uint2(t[k].z, t[k].w);
+            }
+          }
+          for (; i < n8; ++i) reinterpret_cast<uint2*>(dst)[i] = *reinterpret_cast<const uint2*>(src + 8 * i);
+          unsigned long long* const w = reinterpret_cast<unsigned long long*>(dst);
+          w[2] = (unsigned long long)e.lpos;  // LogEntryDescriptor: position, source position, key, timestamp
+          w[3] = (unsigned long long)m.src_pos;
+          w[4] = (unsigned long long)e.key;
+          w[5] = ts;
+          if (e.pa) {
+            const uint32_t q = e.pa / 8;
+            const unsigned long long x = __builtin_bswap64((unsigned long long)e.pik);
+            w[q] = patch_word(w[q], x, (int)e.pa - (int)(8 * q));
+            if (q + 1 < n8) w[q + 1] = patch_word(w[q + 1], x, (int)e.pa - (int)(8 * q + 8));
+          }
+          if (e.sa) {
+            const uint32_t q = e.sa / 8;
+            const unsigned long long x = __builtin_bswap64((unsigned long long)e.scope);
+            w[q] = patch_word(w[q], x, (int)e.sa - (int)(8 * q));
+            if (q + 1 < n8) w[q + 1] = patch_word(w[q + 1], x, (int)e.sa - (int)(8 * q + 8));
+          }
+        }
+        // (the half wave's LDS writes precede its reads: one wave's LDS operations complete in order)
+        __builtin_amdgcn_wave_barrier();
+        const unsigned long long o0 = gbase & ~15ull;
+        for (unsigned long long o = o0 + 16ull * lane; o < gend; o += 16ull * kHalf) {
+          const uint4 v = *reinterpret_cast<const uint4*>(stage + (o - o0));
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+          if (o >= gbase && o + 16 <= gend) {
+            u32x4 q;
+            q.x = v.x; q.y = v.y; q.z = v.z; q.w = v.w;
+            __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out + o));
+          } else {  // a chunk shared with the neighbouring group: only this group's half
+            u32x2 q;
+            if (o >= gbase) { q.x = v.x; q.y = v.y; __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o)); }
+            else { q.x = v.z; q.y = v.w; __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o + 8)); }
+          }
+        }
+      } else if (!ents[0].slow) {
+        // one oversized templated entry: 8-byte words straight from the template
+        __builtin_amdgcn_wave_barrier();
+        const StreamEnt x = ents[0];
+        for (unsigned long long a = gbase + 8ull * lane; a < gend; a += 8ull * kHalf)
+          __builtin_nontemporal_store(tpl_word(L.tpl, x, (uint32_t)(a - gbase), m.src_pos, ts),
+                                      reinterpret_cast<unsigned long long*>(out + a));
+      }
+      g += take;
+      gbase = gend;
+      __builtin_amdgcn_wave_barrier();  // the slots and the stage are rewritten by the next group
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t i = 0; i < cnt; i += 4) {
-      const uint32_t i0 = i + half, i1 = i + 2 + half;
-      const bool v0 = i0 < cnt, v1 = i1 < cnt;
-      TplEnt e0, e1;
-      if (v0) e0 = wents[i0];
-      if (v1) e1 = wents[i1];
-      const bool w0 = v0 && o16 < e0.size, w1 = v1 && o16 < e1.size;
-      ulonglong2 t0 = make_ulonglong2(0, 0), t1 = make_ulonglong2(0, 0);
-      if (w0) t0 = *reinterpret_cast<const ulonglong2*>(L.tpl + e0.off + o16);
-      if (w1) t1 = *reinterpret_cast<const ulonglong2*>(L.tpl + e1.off + o16);
-      if (w0) tpl_chunk(L, out, e0, o16, ts, t0);
-      if (w1) tpl_chunk(L, out, e1, o16, ts, t1);
-    }
-    cnt = 0;
-    __builtin_amdgcn_wave_barrier();  // the slots are rewritten next
   }
 }
 
@@ -722,11 +825,12 @@ __global__ __launch_bounds__(256) void k_log_compose(LogParams L) {
   if (c >= L.n) return;
   const LogCmd m = L.cmds[c];
   unsigned long long pos = L.bytes[c];
+  KeyCache kc;
   for (uint32_t j = 0; j < m.nrec; ++j) {
     const uint32_t info = L.rinfo[m.rec_off + j];
     if (info & kSlow) {
       Rec r;
-      if (!decode(L, c, m, L.rows[m.rec_off + j], r)) return;
+      if (!decode(L, c, m, L.rows[m.rec_off + j], r, kc)) return;
       Write w;
       w.start(L.out + (pos >> 3));
       entry(w, L, m, r, L.first_position + (long long)(m.out_rec + j));
@@ -897,11 +1001,10 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL(k_table_build, dim3(nb), dim3(kLogScanB), 0, s, L, a.hdr, a.wcmds, a.src_pos, a.key_base,
                          a.table_sums, a.table, a.inst_proc_w);
   } else if (a.phase == 1) {
-    // the tables (when they fit), then the waves' template hand-over slots
-    const uint32_t tw = (uint32_t)(lds / 4);
+    // k_log_write reads no serialiser table: LDS holds the half waves' entry slots and stages
     if (a.n)
       hipLaunchKernelGGL(k_log_write, dim3((a.n + kLogWriteB - 1) / kLogWriteB), dim3(kLogWriteB),
-                         (size_t)((tw + 3) & ~3u) * 4 + (kLogWriteB / 64) * kWaveEnts * sizeof(TplEnt), s, L, tw);
+                         (size_t)(kLogWriteB / kHalf) * (kHalf * sizeof(StreamEnt) + kStageAlloc), s, L, 0u);
     if (a.n && a.compose) hipLaunchKernelGGL(k_log_compose, dim3(g), dim3(256), lds, s, L);
   } else {
     if (a.n) hipLaunchKernelGGL(k_ring_create, dim3(g), dim3(256), 0, s, L);

@@ -52,6 +52,7 @@ hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, 
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t xcap,
                          uint32_t n, uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out,
                          hipStream_t s);
+hipError_t launch_xgather(const XGather& A, uint32_t max_count, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;
 constexpr size_t kBulkDrainMin = 1 << 16;  // records: below this the drain stays on the calling thread
 constexpr uint32_t kRegionPad = 0;  // regions for the extra workgroups of multi-round windows
@@ -2427,6 +2428,20 @@ int zbhip_outbox_copy(zbhip_handle* h, void* dev_dst, size_t first, size_t count
   return ZBHIP_OK;
 }
 
+int zbhip_exchange_gather(const zbhip_xpart_cmd* const* src, uint32_t P, const uint32_t* dev_counts,
+                          zbhip_xpart_cmd* const* dst, uint32_t max_count, void* stream) {
+  if (P > kMaxGatherParts || (P && (!src || !dst || !dev_counts))) return ZBHIP_EINVAL;
+  XGather A{};
+  A.P = P;
+  A.counts = dev_counts;
+  for (uint32_t q = 0; q < P; ++q) {
+    A.src[q] = src[q];
+    A.dst[q] = dst[q];
+  }
+  HIPCHK(launch_xgather(A, max_count, reinterpret_cast<hipStream_t>(stream)));
+  return ZBHIP_OK;
+}
+
 int zbhip_submit_xparts_device(zbhip_handle* h, const zbhip_xpart_cmd* dev_xparts, size_t n) {
   if (!h || (n && !dev_xparts)) return ZBHIP_EINVAL;
   if (!h->msg()) return ZBHIP_EUNSUPP;
@@ -3591,7 +3606,6 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     }
     if (idx.size() > h->log_idx_cap) {
       (void)hipFree(h->d_log_idx);
-  (void)hipFree(h->d_log_tpl);
       h->d_log_idx = nullptr;
       if (dalloc(&h->d_log_idx, idx.size() * 2) != hipSuccess) return ZBHIP_ENOMEM;
       h->log_idx_cap = idx.size() * 2;

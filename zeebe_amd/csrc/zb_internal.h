@@ -99,6 +99,15 @@ enum : uint8_t {
   kRejectBit = 0x40,
 };
 
+// zbhip_exchange_gather's launch arguments (kernels.hip k_xgather)
+constexpr uint32_t kMaxGatherParts = 16;
+struct XGather {
+  const zbhip_xpart_cmd* src[kMaxGatherParts];
+  zbhip_xpart_cmd* dst[kMaxGatherParts];
+  const uint32_t* counts;
+  uint32_t P;
+};
+
 // per-command header written by k_step: x = nrec | nkeys << 16, y = first_ord | status << 16 | fb << 24
 enum : uint8_t { ST_OK = 0, ST_FALLBACK = 1 };
 enum : uint8_t {

@@ -71,21 +71,21 @@ class LocalExchange:
             return self._step()
 
     def _step(self):
+        import ctypes as C
+
         import torch
+        from .native import check
         P = len(self.parts)
         mat = torch.zeros((P, P), dtype=torch.int32, device=self.inbox[0].device)
-        for s_, p in enumerate(self.parts):  # counts to the device, one host wait for all of them
-            p.outbox_device_async(mat[s_].data_ptr())
-        buckets = mat.cpu().numpy().astype(np.int64)
-        for t in range(P):
-            off = 0
-            for s_ in range(P):
-                c = int(buckets[s_, t])
-                if c:
-                    first = int(buckets[s_, :t].sum())
-                    self.parts[s_].outbox_copy(self.inbox[t].data_ptr() + off * XPART_BYTES, first, c)
-                    off += c
-            self.sizes[t] = off
+        src = [p.outbox_device_async(mat[s_].data_ptr()) for s_, p in enumerate(self.parts)]
+        buckets = mat.cpu().numpy().astype(np.int64)  # one host wait for all of them (the inbox sizes)
+        self.sizes = [int(buckets[:, t].sum()) for t in range(P)]
+        if buckets.sum():
+            # every (source, target) bucket into the targets' inboxes in one launch (zbhip_exchange_gather)
+            vp = C.c_void_p * P
+            L = self.parts[0].L
+            check(L.zbhip_exchange_gather(vp(*src), P, mat.data_ptr(), vp(*[b.data_ptr() for b in self.inbox]),
+                                          int(buckets.max()), L.zbhip_stream(self.parts[0].h)), "zbhip_exchange_gather")
         return list(self.sizes)
 
     def deliver(self, flags=0):

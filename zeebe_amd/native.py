@@ -22,7 +22,7 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_resolve_key", "zbhip_rejection_reason", "zbhip_incident_message", "zbhip_build_info", "zbhip_command_status",
            "zbhip_submit_ex", "zbhip_submit_device_ex", "zbhip_intern_string", "zbhip_intern_strings",
            "zbhip_string_value", "zbhip_subscription_partition", "zbhip_outbox", "zbhip_outbox_device",
-           "zbhip_outbox_copy", "zbhip_submit_xparts_device", "zbhip_string_partitions",
+           "zbhip_outbox_copy", "zbhip_exchange_gather", "zbhip_submit_xparts_device", "zbhip_string_partitions",
            "zbhip_serializer_new", "zbhip_serializer_free", "zbhip_serializer_deploy", "zbhip_serializer_intern",
            "zbhip_serializer_intern_string", "zbhip_serializer_set_broker_version",
            "zbhip_serializer_rejection_reason", "zbhip_serializer_incident_message", "zbhip_handle_serializer", "zbhip_serialize_log",
@@ -96,6 +96,7 @@ def load():
     L.zbhip_outbox.argtypes = [vp, vp, sz, C.POINTER(sz)]
     L.zbhip_outbox_device.argtypes = [vp, C.POINTER(vp), vp]
     L.zbhip_outbox_copy.argtypes = [vp, vp, sz, sz]
+    L.zbhip_exchange_gather.argtypes = [C.POINTER(vp), u32, vp, C.POINTER(vp), u32, vp]
     L.zbhip_outbox_device_async.argtypes = [vp, C.POINTER(vp), vp]
     L.zbhip_export_instances.argtypes = [vp, vp, sz, STATE_SINK, vp]
     L.zbhip_export_instances_db.argtypes = [vp, vp, sz, DB_SINK, vp]
