@@ -705,11 +705,30 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
   uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
   const unsigned long long ts = (unsigned long long)L.timestamp;
   const uint32_t c0 = blockIdx.x * kLogWriteB + hw * kHalf;
+  // the half wave's 32 command rows and byte offsets, loaded at once (lane l: command c0 + l) and
+  // handed to the whole half wave command by command: one coalesced load instead of a dependent
+  // HBM round trip per command
+  LogCmd mine{};
+  unsigned long long mine_bytes = 0;
+  if (c0 + lane < L.n) {
+    mine = L.cmds[c0 + lane];
+    mine_bytes = L.bytes[c0 + lane];
+  }
   for (uint32_t ci = 0; ci < kHalf; ++ci) {
     const uint32_t c = c0 + ci;  // (half-wave uniform)
     if (c >= L.n) break;
-    const LogCmd m = L.cmds[c];
-    unsigned long long gbase = L.bytes[c];
+    LogCmd m;
+    m.rec_off = __shfl(mine.rec_off, ci, kHalf);
+    m.out_rec = __shfl(mine.out_rec, ci, kHalf);
+    m.key0 = __shfl(mine.key0, ci, kHalf);
+    m.src_pos = __shfl(mine.src_pos, ci, kHalf);
+    m.instance = __shfl(mine.instance, ci, kHalf);
+    m.prev = __shfl(mine.prev, ci, kHalf);
+    m.first_ord = (uint16_t)__shfl((uint32_t)mine.first_ord, ci, kHalf);
+    m.nkeys = (uint16_t)__shfl((uint32_t)mine.nkeys, ci, kHalf);
+    m.nrec = (uint16_t)__shfl((uint32_t)mine.nrec, ci, kHalf);
+    m.doc_count = m.doc_begin = m.pad = 0;  // (templated entries carry no documents)
+    unsigned long long gbase = __shfl(mine_bytes, ci, kHalf);
     KeyCache kc;
     for (uint32_t g = 0; g < m.nrec;) {
       const uint32_t j = g + lane;
