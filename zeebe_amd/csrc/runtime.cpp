@@ -10,6 +10,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -109,10 +112,93 @@ unsigned host_threads() {
   return (unsigned)std::max(1, std::min(16, n));
 }
 
-// fn(t, T) for t in [0, T) on up to T threads; a thread that cannot be started runs its share on
-// the calling thread (no exception leaves the C ABI, no joinable thread is destroyed)
+// A process-wide pool of host worker threads, started once (thread creation cost ~0.3 ms per
+// 16-thread fork/join, several times per window on the log-byte path).  One job at a time: a call
+// that finds the pool busy (another handle's call on another thread) forks its own threads.
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool p;
+    return p;
+  }
+  // runs job(t, T) for t in [1, T) on the workers (T - 1 <= workers()); false when busy
+  bool run(unsigned T, const std::function<void(unsigned, unsigned)>& job, const std::function<void()>& own) {
+    std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
+    if (!busy.owns_lock() || T - 1 > workers_.size()) return false;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &job;
+      T_ = T;
+      remaining_ = T - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    own();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return remaining_ == 0; });
+    job_ = nullptr;
+    return true;
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  WorkerPool() {
+    const unsigned n = host_threads();
+    for (unsigned i = 1; i < n; ++i) {
+      try {
+        workers_.emplace_back([this, i] { loop(i); });
+      } catch (...) {
+        break;
+      }
+    }
+  }
+  void loop(unsigned idx) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned, unsigned)>* job;
+      unsigned T;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        job = job_;
+        T = T_;
+      }
+      if (idx < T) {
+        (*job)(idx, T);
+        std::lock_guard<std::mutex> g(m_);
+        if (--remaining_ == 0) done_.notify_one();
+      }
+    }
+  }
+  std::mutex busy_, m_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> workers_;
+  const std::function<void(unsigned, unsigned)>* job_ = nullptr;
+  unsigned T_ = 0, remaining_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// fn(t, T) for t in [0, T) on up to T threads (the pool's, else threads of its own); a thread that
+// cannot be started runs its share on the calling thread (no exception leaves the C ABI, no
+// joinable thread is destroyed)
 template <class F>
 void parallel_for(unsigned T, const F& fn) {
+  if (T <= 1) {
+    fn(0u, 1u);
+    return;
+  }
+  const std::function<void(unsigned, unsigned)> job = [&fn](unsigned t, unsigned TT) { fn(t, TT); };
+  if (WorkerPool::get().run(T, job, [&] { fn(0u, T); })) return;
   std::vector<std::thread> pool;
   pool.reserve(T);
   unsigned t = 1;
@@ -1096,6 +1182,24 @@ static int plan_rounds(zbhip_handle* h) {
     return h->plan_stamp;
   };
   uint32_t stamp = next_stamp();
+  if (!msg && h->n_cmds >= (1u << 16)) {
+    // the common window addresses every instance once: claim the subjects on the worker threads
+    // (an atomic stamp exchange each); a repeat falls through to the ordered pass below, with a
+    // fresh stamp
+    std::atomic<bool> repeat{false};
+    const size_t n = h->n_cmds;
+    parallel_for(host_threads(), [&](unsigned t, unsigned TT) {
+      for (size_t i = n * t / TT; i < n * (t + 1) / TT; ++i) {
+        auto& e = h->plan_last[h->h_cmds[i].instance];  // bounds: validate()
+        if (__atomic_exchange_n(&e.first, stamp, __ATOMIC_RELAXED) == stamp) {
+          repeat = true;
+          return;
+        }
+      }
+    });
+    if (!repeat) return ZBHIP_OK;  // one round: identity order
+    stamp = next_stamp();
+  }
   std::vector<uint32_t>& round_of = h->plan_round;
   if (round_of.size() < h->n_cmds) round_of.resize(h->n_cmds);
   uint32_t max_round = 0, epoch = 0;
@@ -1199,12 +1303,37 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   int rc = finalize(h);  // the previous window's keys are fixed before its commands are replaced
   if (rc) return rc;
   const auto t1 = now();
-  rc = validate(h, cmds, n, n_docs, xparts, n_xparts);
-  if (rc) return rc;
-  h->external = false;
-  h->h_cmds.assign(cmds, cmds + n);
-  bool continues = false;
-  for (const auto& c : h->h_cmds) continues |= c.kind == ZBHIP_CMD_CONTINUE;
+  // validation, then the host copy, on the worker threads by ranges (a refused window leaves the
+  // handle as it was); the first failing command's code wins, as in one pass
+  std::atomic<bool> continues_any{false};
+  {
+    const unsigned T = n >= (1u << 16) ? host_threads() : 1u;
+    std::vector<std::pair<size_t, int>> fail(T, {~(size_t)0, ZBHIP_OK});
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      const size_t lo = n * t / TT, hi = n * (t + 1) / TT;
+      for (size_t b = lo; b < hi; b += 4096) {
+        const size_t e = std::min(hi, b + 4096);
+        if (validate(h, cmds + b, e - b, n_docs, xparts, n_xparts) == ZBHIP_OK) continue;
+        for (size_t i = b; i < e; ++i)  // the block's first failing command
+          if (int ri = validate(h, cmds + i, 1, n_docs, xparts, n_xparts)) {
+            fail[t] = {i, ri};
+            return;
+          }
+      }
+    });
+    for (const auto& f : fail)
+      if (f.second) return f.second;  // ranges in log order: the first range's failure is the first
+    h->external = false;
+    h->h_cmds.resize(n);
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      const size_t lo = n * t / TT, hi = n * (t + 1) / TT;
+      if (hi > lo) memcpy(h->h_cmds.data() + lo, cmds + lo, (hi - lo) * sizeof(zbhip_command));
+      bool cont = false;
+      for (size_t i = lo; i < hi; ++i) cont |= cmds[i].kind == ZBHIP_CMD_CONTINUE;
+      if (cont) continues_any = true;
+    });
+  }
+  bool continues = continues_any.load();
   if (continues) {
     // duplicates of one id in a window are refused before anything is consumed
     std::unordered_map<uint64_t, int> seen;
