@@ -6,4 +6,4 @@ cd "$(dirname "$0")/../zeebe_amd/csrc"
 name=$1; shift
 make -s -j4 >/dev/null
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O3 -fPIC -Wall -Wno-unused-function "$@" -c kernels.hip -o build/kernels_$name.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libzbhip_$name.so build/kernels_$name.o build/runtime.o build/compiler.o build/logwriter.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libzbhip_$name.so build/kernels_$name.o build/logdev.o build/runtime.o build/compiler.o build/logwriter.o

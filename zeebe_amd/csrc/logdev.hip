@@ -699,9 +699,7 @@ constexpr uint32_t kStageAlloc = kStage + 16;
 __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t lane = threadIdx.x & (kHalf - 1), hw = threadIdx.x / kHalf;
-  StreamEnt* const ents = reinterpret_cast<StreamEnt*>(smem) + hw * kHalf;
-  uint8_t* const stage = reinterpret_cast<uint8_t*>(smem) + (kLogWriteB / kHalf) * kHalf * sizeof(StreamEnt) +
-                         hw * kStageAlloc;
+  uint8_t* const stage = reinterpret_cast<uint8_t*>(smem) + hw * kStageAlloc;
   uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
   const unsigned long long ts = (unsigned long long)L.timestamp;
   const uint32_t c0 = blockIdx.x * kLogWriteB + hw * kHalf;
@@ -767,7 +765,6 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
       if (!staged) take = 1;  // one entry larger than the stage: written from the templates directly
       const unsigned long long gsize = __shfl(incl, take - 1, kHalf);
       e.start = gbase + incl - size;
-      if (lane < take) ents[lane] = e;
       const unsigned long long gend = gbase + gsize;
       if (staged) {
         if (lane < take && !e.slow) {  // the lane's entry into the stage
@@ -821,13 +818,22 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
             else { q.x = v.z; q.y = v.w; __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o + 8)); }
           }
         }
-      } else if (!ents[0].slow) {
-        // one oversized templated entry: 8-byte words straight from the template
-        __builtin_amdgcn_wave_barrier();
-        const StreamEnt x = ents[0];
-        for (unsigned long long a = gbase + 8ull * lane; a < gend; a += 8ull * kHalf)
-          __builtin_nontemporal_store(tpl_word(L.tpl, x, (uint32_t)(a - gbase), m.src_pos, ts),
-                                      reinterpret_cast<unsigned long long*>(out + a));
+      } else {
+        // one oversized entry (lane 0's): 8-byte words straight from its template
+        StreamEnt x;
+        x.start = __shfl(e.start, 0, kHalf);
+        x.key = __shfl(e.key, 0, kHalf);
+        x.scope = __shfl(e.scope, 0, kHalf);
+        x.pik = __shfl(e.pik, 0, kHalf);
+        x.lpos = __shfl(e.lpos, 0, kHalf);
+        x.off = __shfl(e.off, 0, kHalf);
+        x.slow = __shfl(e.slow, 0, kHalf);
+        x.pa = __shfl(e.pa, 0, kHalf);
+        x.sa = __shfl(e.sa, 0, kHalf);
+        if (!x.slow)
+          for (unsigned long long a = gbase + 8ull * lane; a < gend; a += 8ull * kHalf)
+            __builtin_nontemporal_store(tpl_word(L.tpl, x, (uint32_t)(a - gbase), m.src_pos, ts),
+                                        reinterpret_cast<unsigned long long*>(out + a));
       }
       g += take;
       gbase = gend;
@@ -1023,7 +1029,7 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
     // k_log_write reads no serialiser table: LDS holds the half waves' entry slots and stages
     if (a.n)
       hipLaunchKernelGGL(k_log_write, dim3((a.n + kLogWriteB - 1) / kLogWriteB), dim3(kLogWriteB),
-                         (size_t)(kLogWriteB / kHalf) * (kHalf * sizeof(StreamEnt) + kStageAlloc), s, L, 0u);
+                         (size_t)(kLogWriteB / kHalf) * kStageAlloc, s, L, 0u);
     if (a.n && a.compose) hipLaunchKernelGGL(k_log_compose, dim3(g), dim3(256), lds, s, L);
   } else {
     if (a.n) hipLaunchKernelGGL(k_ring_create, dim3(g), dim3(256), 0, s, L);
