@@ -17,6 +17,7 @@ SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM
 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE
 FETCH_SIZE
 WRITE_SIZE
+TCC_HIT_sum TCC_MISS_sum
 GROUPS
 python3 scripts/pmc_traffic.py $O $O/k_log_write.json k_log_write && python3 scripts/pmc_traffic.py $O $O/k_log_sizes.json k_log_sizes
 echo "=== done"
