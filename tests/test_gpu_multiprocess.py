@@ -3,7 +3,7 @@ cuda:0), the subscription exchange through DeviceExchange.exchange_partition -- 
 buckets (zbhip_outbox_device_async), one count collective, one all-to-all of the 48-byte commands,
 the received window built on the device (zbhip_submit_xparts_device).  The ranks share one GPU, so
 the process group is gloo (host-staged collectives); with one GPU per rank the same code runs over
-RCCL (bench.py --config msg --gpus N).
+RCCL (bench.py --config msg --gpus N), exercised here at one rank over ``nccl``.
 
 Bar: every window's records (all parity fields, keys relabelled) and the final state of every
 partition equal the single-process oracle cluster driven by exchange.route()
@@ -31,7 +31,7 @@ def _keys(P):
     return ["k-%d-%d" % (p, i) for p in range(1, P + 1) for i in range(N)]
 
 
-def _rank_main(rank, P, port, out_dir):
+def _rank_main(rank, P, port, out_dir, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -39,8 +39,10 @@ def _rank_main(rank, P, port, out_dir):
 
     from zeebe_amd.engine import Partition
     from zeebe_amd.exchange import XPART_BYTES, DeviceExchange
-    dist.init_process_group("gloo", rank=rank, world_size=P)
     dev = torch.device("cuda", 0)
+    if backend == "nccl":  # RCCL: DeviceExchange's device branch (device counts, device all-to-all)
+        torch.cuda.set_device(dev)
+    dist.init_process_group(backend, rank=rank, world_size=P)
     stream = torch.cuda.Stream(device=dev).cuda_stream  # one stream shared by the partitions (exchange order)
     part = Partition(partition_id=rank + 1, partition_count=P, max_instances=N, max_commands=4 * N * P,
                      max_correlation_keys=N * P, max_records_per_batch=256, stream=stream)
@@ -100,9 +102,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("P", [2, 8])
-def test_gpu_ranks_exchange_matches_oracle_cluster(P, tmp_path):
-    mp.start_processes(_rank_main, args=(P, _free_port(), str(tmp_path)), nprocs=P, join=True, start_method="spawn")
+@pytest.mark.parametrize("P,backend", [(2, "gloo"), (8, "gloo"), (1, "nccl")])
+def test_gpu_ranks_exchange_matches_oracle_cluster(P, backend, tmp_path):
+    """(P = 1 over ``nccl``: the RCCL branch of DeviceExchange -- counts gathered and commands
+    exchanged as device tensors -- on the one GPU of the test box; the gloo cases share it.)"""
+    mp.start_processes(_rank_main, args=(P, _free_port(), str(tmp_path), backend), nprocs=P, join=True,
+                       start_method="spawn")
     ranks = [json.load(open(tmp_path / ("rank%d.json" % r))) for r in range(P)]
     cl = MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], OracleAdapter, XML)
     keys = _keys(P)
