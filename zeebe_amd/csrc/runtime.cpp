@@ -105,11 +105,40 @@ constexpr size_t kMaxMiItems = 63;
 
 // Host threads a bulk host pass may use: the CPUs this process may run on (affinity mask, which
 // honours taskset / cgroup cpusets), at most 16.
-unsigned host_threads() {
+// CPUs this process may keep busy: its affinity set, its cgroup's CPU quota (cpu.max, v2; cfs
+// quota / period, v1) -- a busy pool past the quota is throttled by the kernel for the rest of the
+// 100 ms period, which showed as 10-45 ms stalls of single windows -- at most 16, or
+// ZBHIP_HOST_THREADS.  One CPU of a quota is left to the calling thread and the runtime's own.
+static unsigned detect_host_threads() {
+  if (const char* e = getenv("ZBHIP_HOST_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return (unsigned)std::min(v, 64);
+  }
   cpu_set_t set;
   CPU_ZERO(&set);
   int n = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+  double quota = 0;
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) quota = atof(q) / (double)period;
+    fclose(f);
+  } else if (FILE* fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    long long q = -1, period = 0;
+    if (fscanf(fq, "%lld", &q) != 1) q = -1;
+    fclose(fq);
+    if (FILE* fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (fscanf(fp, "%lld", &period) != 1) period = 0;
+      fclose(fp);
+    }
+    if (q > 0 && period > 0) quota = (double)q / (double)period;
+  }
+  if (quota > 0) n = std::min(n, std::max(1, (int)quota - 1));
   return (unsigned)std::max(1, std::min(16, n));
+}
+unsigned host_threads() {
+  static const unsigned n = detect_host_threads();
+  return n;
 }
 
 // A process-wide pool of host worker threads, started once (thread creation cost ~0.3 ms per
@@ -262,12 +291,39 @@ struct KeyTable {
     auto it = std::upper_bound(s->begin(), s->end(), v, [](int64_t x, const BatchRef& b) { return x < b.base; });
     return it == s->begin() ? nullptr : &*(it - 1);
   }
+  // in 64 Ki-entry chunks over the host threads (whole segments per thread left one thread with two
+  // 10^6-entry segments: 36 ms stalls every ~11 windows), then each segment's kept runs closed up
   template <class Live>
   void compact(const Live& live) {
+    constexpr size_t kChunk = size_t(1) << 16;
+    std::vector<std::pair<uint32_t, size_t>> chunks;  // (segment, first entry)
+    std::vector<size_t> seg_chunk(seg.size() + 1, 0);
+    for (size_t i = 0; i < seg.size(); ++i) {
+      seg_chunk[i] = chunks.size();
+      for (size_t b = 0; b < seg[i].size(); b += kChunk) chunks.emplace_back((uint32_t)i, b);
+    }
+    seg_chunk[seg.size()] = chunks.size();
+    std::vector<size_t> kept(chunks.size(), 0);
     parallel_for(host_threads(), [&](unsigned t, unsigned T) {
-      for (size_t i = t; i < seg.size(); i += T)
-        seg[i].erase(std::remove_if(seg[i].begin(), seg[i].end(), [&](const BatchRef& b) { return !live(b); }),
-                     seg[i].end());
+      for (size_t k = t; k < chunks.size(); k += T) {
+        std::vector<BatchRef>& g = seg[chunks[k].first];
+        const size_t b = chunks[k].second, e = std::min(b + kChunk, g.size());
+        size_t o = b;
+        for (size_t x = b; x < e; ++x)
+          if (live(g[x])) g[o++] = g[x];
+        kept[k] = o - b;
+      }
+    });
+    parallel_for(host_threads(), [&](unsigned t, unsigned T) {
+      for (size_t i = t; i < seg.size(); i += T) {
+        std::vector<BatchRef>& g = seg[i];
+        size_t o = 0;
+        for (size_t k = seg_chunk[i]; k < seg_chunk[i + 1]; ++k) {
+          if (o != chunks[k].second && kept[k]) memmove(&g[o], &g[chunks[k].second], kept[k] * sizeof(BatchRef));
+          o += kept[k];
+        }
+        g.resize(o);
+      }
     });
     seg.erase(std::remove_if(seg.begin(), seg.end(), [](const std::vector<BatchRef>& g) { return g.empty(); }),
               seg.end());
@@ -438,6 +494,10 @@ struct zbhip_handle {
   unsigned long long* d_log_bytes = nullptr;  // [max_commands + 1 + scan blocks]
   long long* d_src_pos = nullptr;             // [max_commands] source positions (device-built command table)
   std::vector<uint16_t> inst_proc_stage;      // inst_proc as uploaded for that table
+  uint16_t* inst_proc_pin = nullptr;          // pinned staging of the device-table path's uploads
+  size_t inst_proc_pin_cap = 0;
+  long long* src_pos_pin = nullptr;
+  size_t src_pos_pin_cap = 0;
   unsigned long long* d_tbl_sums = nullptr;   // scan blocks of the device-built command table
   uint64_t* d_log_out = nullptr;
   size_t log_out_cap = 0;
@@ -707,6 +767,8 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_log_out);
   (void)hipFree(h->d_log_flag);
   (void)hipFree(h->d_log_rinfo);
+  if (h->inst_proc_pin) (void)hipHostFree(h->inst_proc_pin);
+  if (h->src_pos_pin) (void)hipHostFree(h->src_pos_pin);
   (void)hipFree(h->d_check_flag);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
   for (auto& e : h->ev)
@@ -3804,16 +3866,41 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   a.rinfo = h->d_log_rinfo;
   unsigned long long total = 0;
   uint32_t flag = 0;
+  auto tu = now(), tf = now();
   if (dev_table) {
     // the instances' processes before this window (the table kernel adds this window's CREATEs);
     // a copy, since finalize updates inst_proc while the upload may still read it
+    // (through pinned staging filled on the host threads: a pageable upload is copied by the driver
+    // through its own bounce buffers, synchronously and with stalls of tens of ms per window)
     if (h->inst_proc.size() >= N) {
-      h->inst_proc_stage.assign(h->inst_proc.begin(), h->inst_proc.begin() + N);
-      HIPCHK(hipMemcpyAsync(h->d_inst_proc, h->inst_proc_stage.data(), N * sizeof(uint16_t), hipMemcpyHostToDevice,
-                            h->stream));
+      if (h->inst_proc_pin_cap < N) {
+        if (h->inst_proc_pin) (void)hipHostFree(h->inst_proc_pin);
+        h->inst_proc_pin = nullptr;
+        h->inst_proc_pin_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&h->inst_proc_pin), N * sizeof(uint16_t), hipHostMallocDefault) != hipSuccess)
+          return ZBHIP_ENOMEM;
+        h->inst_proc_pin_cap = N;
+      }
+      memcpy(h->inst_proc_pin, h->inst_proc.data(), N * sizeof(uint16_t));
+      HIPCHK(hipMemcpyAsync(h->d_inst_proc, h->inst_proc_pin, N * sizeof(uint16_t), hipMemcpyHostToDevice, h->stream));
     }
-    if (w->source_positions)
-      HIPCHK(hipMemcpyAsync(h->d_src_pos, w->source_positions, n * sizeof(long long), hipMemcpyHostToDevice, h->stream));
+    if (w->source_positions) {
+      if (h->src_pos_pin_cap < n) {
+        if (h->src_pos_pin) (void)hipHostFree(h->src_pos_pin);
+        h->src_pos_pin = nullptr;
+        h->src_pos_pin_cap = 0;
+        const size_t cap = std::max<size_t>(n, h->cfg.max_commands);
+        if (hipHostMalloc(reinterpret_cast<void**>(&h->src_pos_pin), cap * sizeof(long long), hipHostMallocDefault) != hipSuccess)
+          return ZBHIP_ENOMEM;
+        h->src_pos_pin_cap = cap;
+      }
+      parallel_for(host_threads(), [&](unsigned t, unsigned TT) {
+        const size_t b = n * t / TT, e = n * (t + 1) / TT;
+        memcpy(h->src_pos_pin + b, w->source_positions + b, (e - b) * sizeof(long long));
+      });
+      HIPCHK(hipMemcpyAsync(h->d_src_pos, h->src_pos_pin, n * sizeof(long long), hipMemcpyHostToDevice, h->stream));
+    }
+    tu = now();
     HIPCHK(hipMemsetAsync(h->d_log_flag, 0, sizeof(uint32_t), h->stream));
     a.hdr = h->d_cmd_hdr;
     a.wcmds = reinterpret_cast<const zbhip_command*>(h->external ? h->ext_cmds : h->d_cmds);
@@ -3834,6 +3921,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
       return rc;
     }
     if (h->h_base[0] + 1 != (int64_t)key_base + 1 || h->key_counter < (int64_t)key_base) return ZBHIP_EDEVICE;
+    tf = now();
     HIPCHK(hipStreamSynchronize(h->stream));
   }
   const auto t2 = now();
@@ -3924,8 +4012,10 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   if (dbg) {
     const auto t4 = now();
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    fprintf(stderr, "[zbhip] serialize_log_device n=%zu (%s table): finalize %.2f ms, table %.2f ms, upload+sizes %.2f ms, "
-            "write+ring %.2f ms\n", n, dev_table ? "device" : "host", ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
+    fprintf(stderr, "[zbhip] serialize_log_device n=%zu (%s table): finalize %.2f ms, table %.2f ms (uploads %.2f, "
+            "key bookkeeping %.2f, wait %.2f), upload+sizes %.2f ms, write+ring %.2f ms\n", n,
+            dev_table ? "device" : "host", ms(t0, t1), ms(t1, t2), dev_table ? ms(t1, tu) : 0.0,
+            dev_table ? ms(tu, tf) : 0.0, dev_table ? ms(tf, t2) : 0.0, ms(t2, t3), ms(t3, t4));
   }
   return rc;
 }
