@@ -269,9 +269,21 @@ struct KeyTable {
   size_t count = 0;
   size_t size() const { return count; }
   // a new segment of n entries, filled by the caller (indexes 0 .. n-1, from any thread)
+  // emptied segments' buffers, reused by the next windows (freeing and re-faulting 24 MB per
+  // window cost milliseconds of page-table work on the bookkeeping's critical path)
+  std::vector<std::vector<BatchRef>> spare;
   BatchRef* append_segment(size_t n) {
     if (n == 0) return nullptr;
-    seg.emplace_back(n);
+    size_t best = spare.size();
+    for (size_t i = 0; i < spare.size(); ++i)
+      if (spare[i].capacity() >= n && (best == spare.size() || spare[i].capacity() < spare[best].capacity())) best = i;
+    if (best < spare.size()) {
+      seg.push_back(std::move(spare[best]));
+      spare.erase(spare.begin() + best);
+      seg.back().resize(n);
+    } else {
+      seg.emplace_back(n);
+    }
     count += n;
     return seg.back().data();
   }
@@ -325,8 +337,13 @@ struct KeyTable {
         g.resize(o);
       }
     });
-    seg.erase(std::remove_if(seg.begin(), seg.end(), [](const std::vector<BatchRef>& g) { return g.empty(); }),
-              seg.end());
+    std::vector<std::vector<BatchRef>> keep;
+    keep.reserve(seg.size());
+    for (auto& g : seg) {
+      if (!g.empty()) keep.push_back(std::move(g));
+      else if (spare.size() < 32) spare.push_back(std::move(g));
+    }
+    seg.swap(keep);
     count = 0;
     for (auto& g : seg) count += g.size();
   }
