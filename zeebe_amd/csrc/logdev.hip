@@ -71,6 +71,7 @@ struct LogParams {
   const uint4* tpl_desc;
   const uint32_t* tpl_idx;
   uint32_t* rinfo;              // [rows] per record: template id << 16 | entry bytes, or kSlow | bytes
+  unsigned long long out_cap;   // bytes at `out` (0: unchecked)
 };
 constexpr uint32_t kSlow = 1u << 31;
 
@@ -703,6 +704,7 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
   uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
   const unsigned long long ts = (unsigned long long)L.timestamp;
   const uint32_t c0 = blockIdx.x * kLogWriteB + hw * kHalf;
+  if (L.out_cap && L.bytes[L.n] > L.out_cap) return;  // (a speculative launch into a too small buffer)
   // the half wave's 32 command rows and byte offsets, loaded at once (lane l: command c0 + l) and
   // handed to the whole half wave command by command: one coalesced load instead of a dependent
   // HBM round trip per command
@@ -1009,7 +1011,7 @@ __global__ __launch_bounds__(256) void k_ring_add(LogParams L) {
 hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
   LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.arena_words, a.idx_words, a.docs, a.n_docs, a.inst_proc, a.ring,
               a.kpi, a.n_inst, a.pbits, a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]},
-              a.bytes, a.out, a.flag, a.now_ms, a.cmd_due, a.tpl, a.tpl_desc, a.tpl_idx, a.rinfo};
+              a.bytes, a.out, a.flag, a.now_ms, a.cmd_due, a.tpl, a.tpl_desc, a.tpl_idx, a.rinfo, a.out_cap};
   const uint32_t g = (a.n + 255) / 256;
   const size_t lds = a.arena_words + a.idx_words <= kLdsTableWords ? (size_t)(a.arena_words + a.idx_words) * 4 : 0;
   if (a.phase == 0) {  // sizes and byte offsets
@@ -1027,7 +1029,7 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
                          a.table_sums, a.table, a.inst_proc_w);
   } else if (a.phase == 1) {
     // k_log_write reads no serialiser table: LDS holds the half waves' entry slots and stages
-    if (a.n)
+    if (a.n && a.compose != 2)
       hipLaunchKernelGGL(k_log_write, dim3((a.n + kLogWriteB - 1) / kLogWriteB), dim3(kLogWriteB),
                          (size_t)(kLogWriteB / kHalf) * kStageAlloc, s, L, 0u);
     if (a.n && a.compose) hipLaunchKernelGGL(k_log_compose, dim3(g), dim3(256), lds, s, L);

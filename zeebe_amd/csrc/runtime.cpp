@@ -3884,6 +3884,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   unsigned long long total = 0;
   uint32_t flag = 0;
   auto tu = now(), tf = now();
+  bool spec = false;  // k_log_write launched before the total was known
   if (dev_table) {
     // the instances' processes before this window (the table kernel adds this window's CREATEs);
     // a copy, since finalize updates inst_proc while the upload may still read it
@@ -3932,6 +3933,17 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     HIPCHK(launch_log_device(a, h->stream));
     HIPCHK(hipMemcpyAsync(&total, h->d_log_bytes + n, sizeof total, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipMemcpyAsync(&flag, h->d_log_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
+    // the templated entries written right away, under the host bookkeeping below: the device table
+    // needs nothing from it (k_log_write returns at once when the window outgrew the buffer; a
+    // window the device cannot write is discarded after the size pass's flag is read)
+    if (h->log_out_cap) {
+      a.out = h->d_log_out;
+      a.out_cap = h->log_out_cap;
+      a.compose = 0;
+      a.phase = 1;
+      HIPCHK(launch_log_device(a, h->stream));
+      spec = true;
+    }
     // meanwhile on the host: the window's key relabelling bookkeeping (the same key bases)
     if (int rc = finalize(h)) {
       (void)hipStreamSynchronize(h->stream);
@@ -4008,6 +4020,15 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   if (flag & 1u) {
     rc = ZBHIP_EUNSUPP;  // a key the ring does not hold, or a value outside the device writer
   } else {
+    if (spec && total <= h->log_out_cap) {  // the bytes are written: composed entries only
+      if (flag & 2u) {
+        a.out = h->d_log_out;
+        a.out_cap = 0;
+        a.compose = 2;
+        a.phase = 1;
+        HIPCHK(launch_log_device(a, h->stream));
+      }
+    } else {
     if (total > h->log_out_cap) {
       (void)hipFree(h->d_log_out);
       h->d_log_out = nullptr;
@@ -4017,9 +4038,11 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
       h->log_out_cap = cap / 8 * 8;
     }
     a.out = h->d_log_out;
+    a.out_cap = 0;
     a.compose = (flag & 2u) ? 1 : 0;
     a.phase = 1;
     HIPCHK(launch_log_device(a, h->stream));
+    }
     *dev_bytes = h->d_log_out;
     *used = total;
   }

@@ -306,7 +306,10 @@ struct LogLaunch {
   const uint4* tpl_desc;       // per template: offset, size | pik offset + 1 << 16, scope offset + 1
   const uint32_t* tpl_idx;     // [0] n procs, [1 + p] base of process p's [element][kLogTplKinds] ids + 1
   uint32_t* rinfo;             // [rows] per record: its template or composed, and its entry bytes
-  int compose;                 // phase 1: entries without a template exist (the size pass's flag bit 1)
+  int compose;                 // phase 1: entries without a template exist (the size pass's flag bit 1);
+                               // 2: k_log_compose only (the write ran speculatively)
+  unsigned long long out_cap;  // phase 1: bytes at `out` (0: unchecked); k_log_write does nothing when the
+                               // window's total (bytes[n], from the scan) exceeds it
 };
 
 }  // namespace zb
