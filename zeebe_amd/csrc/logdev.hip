@@ -610,6 +610,7 @@ __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
       uint4 d;
       if (!decode(L, c, m, L.rows[m.rec_off + j], r, kc)) {
         atomicOr(L.flag, 1u);
+        for (; j < m.nrec; ++j) L.rinfo[m.rec_off + j] = kSlow;  // (no stale info behind a declined record)
         break;
       }
       const uint32_t id = tpl_of(L, m, r, d);
@@ -620,6 +621,7 @@ __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
         Count e;
         if (!entry(e, L, m, r, 0) || e.n >= 0x10000) {
           atomicOr(L.flag, 1u);
+          for (; j < m.nrec; ++j) L.rinfo[m.rec_off + j] = kSlow;
           break;
         }
         s.n += e.n;
@@ -704,7 +706,9 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
   uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
   const unsigned long long ts = (unsigned long long)L.timestamp;
   const uint32_t c0 = blockIdx.x * kLogWriteB + hw * kHalf;
-  if (L.out_cap && L.bytes[L.n] > L.out_cap) return;  // (a speculative launch into a too small buffer)
+  // a speculative launch (before the host read the size pass's results) writes nothing when the
+  // window outgrew the buffer or the size pass declined it (its entry sizes are then incomplete)
+  if (L.out_cap && ((*L.flag & 1u) || L.bytes[L.n] > L.out_cap)) return;
   // the half wave's 32 command rows and byte offsets, loaded at once (lane l: command c0 + l) and
   // handed to the whole half wave command by command: one coalesced load instead of a dependent
   // HBM round trip per command

@@ -144,6 +144,11 @@ unsigned host_threads() {
 // A process-wide pool of host worker threads, started once (thread creation cost ~0.3 ms per
 // 16-thread fork/join, several times per window on the log-byte path).  One job at a time: a call
 // that finds the pool busy (another handle's call on another thread) forks its own threads.
+// set on the pool's workers and on a caller's own share while a pool job runs: a parallel_for
+// nested inside a job runs serially instead of touching the pool (whose busy mutex that thread may
+// already own)
+static thread_local bool tl_in_pool_job = false;
+
 class WorkerPool {
  public:
   static WorkerPool& get() {
@@ -162,7 +167,9 @@ class WorkerPool {
       ++gen_;
     }
     cv_.notify_all();
+    tl_in_pool_job = true;
     own();
+    tl_in_pool_job = false;
     std::unique_lock<std::mutex> g(m_);
     done_.wait(g, [this] { return remaining_ == 0; });
     job_ = nullptr;
@@ -189,6 +196,7 @@ class WorkerPool {
     }
   }
   void loop(unsigned idx) {
+    tl_in_pool_job = true;
     uint64_t seen = 0;
     for (;;) {
       const std::function<void(unsigned, unsigned)>* job;
@@ -222,8 +230,8 @@ class WorkerPool {
 // joinable thread is destroyed)
 template <class F>
 void parallel_for(unsigned T, const F& fn) {
-  if (T <= 1) {
-    fn(0u, 1u);
+  if (T <= 1 || tl_in_pool_job) {
+    for (unsigned t = 0; t < std::max(T, 1u); ++t) fn(t, std::max(T, 1u));
     return;
   }
   const std::function<void(unsigned, unsigned)> job = [&fn](unsigned t, unsigned TT) { fn(t, TT); };
@@ -341,11 +349,26 @@ struct KeyTable {
     keep.reserve(seg.size());
     for (auto& g : seg) {
       if (!g.empty()) keep.push_back(std::move(g));
-      else if (spare.size() < 32) spare.push_back(std::move(g));
+      else spare.push_back(std::move(g));
     }
+    trim_spare();
     seg.swap(keep);
     count = 0;
     for (auto& g : seg) count += g.size();
+  }
+  // spare buffers are kept up to twice the largest live segment's capacity in total (a window or
+  // two), largest first: a table that shrank gives its memory back
+  void trim_spare() {
+    size_t live = 0;
+    for (auto& g : seg) live = std::max(live, g.capacity());
+    std::sort(spare.begin(), spare.end(),
+              [](const std::vector<BatchRef>& a, const std::vector<BatchRef>& b) { return a.capacity() > b.capacity(); });
+    size_t kept = 0, total = 0;
+    while (kept < spare.size() && kept < 4 && total + spare[kept].capacity() <= 2 * std::max<size_t>(live, 1u << 16)) {
+      total += spare[kept].capacity();
+      ++kept;
+    }
+    spare.resize(kept);
   }
   void sort_all() {  // (imports: one segment again)
     std::vector<BatchRef> all;

@@ -277,11 +277,15 @@ class Partition:
         for f, _ in abi.Record._fields_:
             if f != "pad":
                 setattr(r, f, int(rec[f]))
-        buf = C.create_string_buffer(1024)
-        n = self.L.zbhip_incident_message(self.h, C.byref(r), buf, 1024)
-        if n < 0 or n > 1024:
-            raise ValueError("zbhip_incident_message: %d" % n)
-        return buf.raw[:n].decode()
+        cap = 1024
+        while True:
+            buf = C.create_string_buffer(cap)
+            n = self.L.zbhip_incident_message(self.h, C.byref(r), buf, cap)
+            if n < 0:
+                raise ZbhipError(n, "zbhip_incident_message")
+            if n <= cap:
+                return buf.raw[:n].decode()
+            cap = n  # the full length: call again with room for it
 
     def stats(self):
         s = abi.Stats()
