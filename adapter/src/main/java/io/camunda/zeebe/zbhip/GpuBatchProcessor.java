@@ -17,7 +17,11 @@
  *    before each window zbhip_set_key_if_higher(DbKeyGenerator's key);
  *  - the fallback hand-off declares the engine's keys after its batch (a post-commit task);
  *  - JOB_BATCH:ACTIVATE of job types only device instances hold goes to zbhip_activate_jobs;
- *  - after recovery the instances of device processes move from RocksDB into HBM (onRecovered).
+ *  - after recovery the instances of device processes move from RocksDB into HBM (onRecovered);
+ *  - config 5 (correlationSlots > 0): MESSAGE:PUBLISH, MESSAGE_SUBSCRIPTION:CREATE/CORRELATE and
+ *    PROCESS_MESSAGE_SUBSCRIPTION:CREATE/CORRELATE run on the device (Messages), and the commands a
+ *    device batch sends to other partitions go to InterPartitionCommandSender in a post-commit task of
+ *    that batch (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition, :320-338).
  * The Python mirror zeebe_amd/adapter.py is this class line for line in behaviour; tests/test_gpu_psm.py
  * runs it inside a restatement of ProcessingStateMachine against the engine alone.
  *
@@ -54,6 +58,7 @@ import io.camunda.zeebe.protocol.record.intent.ProcessInstanceCreationIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessInstanceIntent;
 import io.camunda.zeebe.protocol.record.intent.TimerIntent;
 import io.camunda.zeebe.scheduler.clock.ActorClock;
+import io.camunda.zeebe.stream.api.InterPartitionCommandSender;
 import io.camunda.zeebe.stream.api.ProcessingResult;
 import io.camunda.zeebe.stream.api.ProcessingResultBuilder;
 import io.camunda.zeebe.stream.api.ReadonlyStreamProcessorContext;
@@ -127,7 +132,11 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   private final RawDb zeebeDb;
   private final int partitionCount;
   private final int device;
+  private final int correlationSlots; // config 5: correlation slots in HBM (0: messages stay with the engine)
+  private final Set<String> messageNames = new HashSet<>();
   private int partitionId;
+  private InterPartitionCommandSender sender;
+  private Messages messages;
 
   private final Arena arena = Arena.ofShared();
   private MemorySegment handle;
@@ -153,12 +162,24 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       final RawDb zeebeDb,
       final int partitionCount,
       final int device) {
+    this(engine, reader, deployments, zeebeDb, partitionCount, device, 0);
+  }
+
+  public GpuBatchProcessor(
+      final Engine engine,
+      final LogStreamReader reader,
+      final Deployments deployments,
+      final RawDb zeebeDb,
+      final int partitionCount,
+      final int device,
+      final int correlationSlots) {
     this.engine = engine;
     this.reader = reader;
     this.deployments = deployments;
     this.zeebeDb = zeebeDb;
     this.partitionCount = partitionCount;
     this.device = device;
+    this.correlationSlots = correlationSlots;
   }
 
   @Override
@@ -167,15 +188,16 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     // the platform's key generator is the DbKeyGenerator (StreamProcessor.java:368)
     keyGenerator = (DbKeyGenerator) ctx.getKeyGenerator();
     partitionId = ctx.getPartitionId();
+    sender = ctx.getPartitionCommandSender();
     final long partitionBits = (long) partitionId << 51;
     handle =
         ZbHip.open(
             arena, ctx.getPartitionId(), partitionCount, device, /* maxCommandsInBatch */ 100, INSTANCES, WINDOW,
-            keyGenerator.getCurrentKey() - partitionBits, /* correlation slots: config 5 only */ 0,
-            ZbHip.OPEN_DEFER_CONTINUATIONS);
+            keyGenerator.getCurrentKey() - partitionBits, correlationSlots, ZbHip.OPEN_DEFER_CONTINUATIONS);
     for (final var d : deployments.all()) {
       deploy(d);
     }
+    messages = new Messages(partitionId, correlationSlots, messageNames);
     window.init(arena);
     ctx.addLifecycleListeners(List.of(this));
   }
@@ -187,6 +209,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       engineJobTypes.addAll(JobTypes.of(d.xml()));
       return;
     }
+    messageNames.addAll(JobTypes.messageNames(d.xml()));
     byKey.put(d.definitionKey(), p);
     byIndex.add(p);
     final var prev = latestById.get(d.bpmnProcessId());
@@ -198,7 +221,8 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   @Override
   public boolean accepts(final ValueType valueType) {
     return valueType == ValueType.PROCESS_INSTANCE_CREATION || valueType == ValueType.JOB
-        || valueType == ValueType.TIMER || valueType == ValueType.JOB_BATCH || engine.accepts(valueType);
+        || valueType == ValueType.TIMER || valueType == ValueType.JOB_BATCH
+        || (correlationSlots > 0 && Messages.isMessageCommand(valueType)) || engine.accepts(valueType);
   }
 
   @Override
@@ -262,6 +286,9 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       return fallBack(i, record, out);
     }
     followUps = window.emit(i, record, out, this);
+    if (messages.enabled()) {
+      messages.send(handle, i, out, sender, this); // the batch's cross-partition commands, post-commit
+    }
     // DbKeyGenerator after this command: the device's keys so far (the engine's next command, a
     // fallback in this window or whatever follows the window, continues after them)
     keyGenerator.setKeyIfHigher(ZbHip.keyBefore(handle, i + 1));
@@ -307,6 +334,11 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
         || (vt == ValueType.PROCESS_INSTANCE_BATCH && record.getIntent() == ProcessInstanceBatchIntent.ACTIVATE)) {
       return next.hasNext() && next.next().matches(record);
     }
+    if (messages.enabled() && Messages.isMessageCommand(vt)) {
+      try (Arena a = Arena.ofConfined()) {
+        return messages.of(record, this, a) != null;
+      }
+    }
     return false;
   }
 
@@ -351,6 +383,8 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       } else if (vt == ValueType.TIMER) {
         final long ref = ZbHip.resolveKey(handle, event.getKey());
         window.addTimerTrigger(event.getPosition(), rec, ref, ((TimerRecord) rec.getValue()).getDueDate());
+      } else if (Messages.isMessageCommand(vt)) {
+        window.addMessageCommand(event.getPosition(), rec, messages.of(rec, this, window.arena()));
       } else {
         final Continuation c = next.next();
         claimed++;
@@ -393,6 +427,15 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
 
   long internString(final byte[] value) {
     return ZbHip.internString(handle, value);
+  }
+
+  /** zbhip_resolve_key: (slot << 16 | key ordinal) of a device key, or -1. */
+  long resolve(final long key) {
+    return key < 0 ? -1 : ZbHip.resolveKey(handle, key);
+  }
+
+  Messages messages() {
+    return messages;
   }
 
   private int takeSlot() {

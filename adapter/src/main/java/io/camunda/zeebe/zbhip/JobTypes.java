@@ -31,6 +31,19 @@ final class JobTypes {
     return out;
   }
 
+  // <message name="..."> (static names; the subset of the device's message catch events)
+  private static final Pattern MESSAGE = Pattern.compile("<(?:\\w+:)?message\\b[^>]*?\\sname=\"([^\"=][^\"]*)\"");
+
+  /** Static message names a BPMN XML declares (config 5: the PUBLISH commands the device takes). */
+  static Set<String> messageNames(final byte[] bpmnXml) {
+    final Set<String> out = new HashSet<>();
+    final Matcher m = MESSAGE.matcher(new String(bpmnXml, StandardCharsets.UTF_8));
+    while (m.find()) {
+      out.add(m.group(1));
+    }
+    return out;
+  }
+
   /** The job type of a JOBS column-family value (JobRecordValue, DbJobState.java:112-157). */
   static String typeOfJobsValue(final byte[] value) {
     final JobRecordValue v = new JobRecordValue();

@@ -24,6 +24,9 @@ import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
 import io.camunda.zeebe.protocol.impl.record.UnifiedRecordValue;
 import io.camunda.zeebe.protocol.impl.record.value.incident.IncidentRecord;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
+import io.camunda.zeebe.protocol.impl.record.value.message.MessageRecord;
+import io.camunda.zeebe.protocol.impl.record.value.message.MessageSubscriptionRecord;
+import io.camunda.zeebe.protocol.impl.record.value.message.ProcessMessageSubscriptionRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessEventRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceCreationRecord;
 import io.camunda.zeebe.protocol.impl.record.value.processinstance.ProcessInstanceBatchRecord;
@@ -35,6 +38,7 @@ import io.camunda.zeebe.protocol.record.RejectionType;
 import io.camunda.zeebe.protocol.record.ValueType;
 import io.camunda.zeebe.protocol.record.intent.Intent;
 import io.camunda.zeebe.protocol.record.intent.JobIntent;
+import io.camunda.zeebe.protocol.record.intent.MessageSubscriptionIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessEventIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessInstanceCreationIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessInstanceIntent;
@@ -66,6 +70,9 @@ final class Window {
   private MemorySegment handle;
   private MemorySegment cmds;
   private MemorySegment docs;
+  private MemorySegment xparts; // received cross-partition commands of the window (config 5)
+  private int nXparts;
+  private Arena arena;
   private MemorySegment recs;
   private long recCap;
   private int n;
@@ -81,8 +88,15 @@ final class Window {
   private final MsgPackReader msgpack = new MsgPackReader();
 
   void init(final Arena arena) {
+    this.arena = arena;
     cmds = arena.allocate(ZbHip.COMMAND.byteSize() * MAX, 16);
     docs = arena.allocate(ZbHip.DOC_ENTRY.byteSize() * MAX_DOCS, 16);
+    xparts = arena.allocate(ZbHip.XPART.byteSize() * MAX, 16);
+  }
+
+  /** Scratch for a read-ahead message command's xpart row (copied into the window by addMessageCommand). */
+  Arena arena() {
+    return arena;
   }
 
   void reset(final long firstPosition) {
@@ -90,6 +104,7 @@ final class Window {
     n = 0;
     addressed.clear();
     nDocs = 0;
+    nXparts = 0;
     entryValues.clear();
     Arrays.fill(documents, null);
   }
@@ -178,6 +193,19 @@ final class Window {
   void addContinuation(final long position, final TypedRecord command, final int slot, final long id) {
     put(position, command, slot, ZbHip.CMD_CONTINUE, 0, 0, (int) id, EMPTY);
     cmds.set(JAVA_INT, ZbHip.COMMAND.byteSize() * (n - 1) + 12, (int) (id >>> 32));
+  }
+
+  /**
+   * A message command (config 5, Messages.of): MESSAGE:PUBLISH -> ZBHIP_CMD_PUBLISH on its correlation
+   * slot; a subscription command -> its xpart row appended to the window's, doc_begin = its index.
+   */
+  void addMessageCommand(final long position, final TypedRecord command, final Messages.DeviceCommand c) {
+    int docBegin = 0;
+    if (c.xpart() != null) {
+      MemorySegment.copy(c.xpart(), 0, xparts, ZbHip.XPART.byteSize() * nXparts, ZbHip.XPART.byteSize());
+      docBegin = nXparts++;
+    }
+    put(position, command, c.instance(), c.kind(), 0, c.ref(), docBegin, EMPTY);
   }
 
   private static final DirectBuffer EMPTY = new UnsafeBuffer(new byte[0]);
@@ -270,7 +298,11 @@ final class Window {
    */
   void submitRun(final MemorySegment handle) {
     this.handle = handle;
-    ZbHip.submit(handle, cmds, n, docs, nDocs);
+    if (nXparts > 0) {
+      ZbHip.submitEx(handle, cmds, n, docs, nDocs, xparts, nXparts);
+    } else {
+      ZbHip.submit(handle, cmds, n, docs, nDocs);
+    }
     ZbHip.run(handle, 0);
   }
 
@@ -323,6 +355,8 @@ final class Window {
       } else if (valueType == ValueType.PROCESS_INSTANCE.value()
           && intent == ProcessInstanceIntent.ELEMENT_COMPLETED.value() && rec.get(JAVA_INT, 36) == 0) {
         p.instanceEnded(instances[i]); // the process element (index 0) completed
+      } else if (valueType == ValueType.MESSAGE_SUBSCRIPTION.value() && recordType == RecordType.EVENT.value()) {
+        p.messages().onSubscriptionEvent(meta.getIntent(), (MessageSubscriptionRecord) value, rec.get(JAVA_INT, 64));
       }
     }
     return admitted;
@@ -446,9 +480,41 @@ final class Window {
             .setVariables(documents[i]);
         return v.setTenantId(TENANT);
       }
-      default -> throw new IllegalStateException("value type outside configs 1-4: " + vt
-          + " (config 5 windows write their log bytes with zbhip_serialize_log)");
+      case MESSAGE, MESSAGE_SUBSCRIPTION, PROCESS_MESSAGE_SUBSCRIPTION -> {
+        return messageValue(r, vt, d, elem, scope, pik, p);
+      }
+      default -> throw new IllegalStateException("value type outside the device subset: " + vt);
     }
+  }
+
+  /**
+   * A message record: the drained zbhip_record carries every property (the log writer's fields,
+   * logwriter.cpp); message variables are empty in the subset, deadline = the PUBLISH command's
+   * timestamp + timeToLive 0 (MessagePublishProcessor.java:110).
+   */
+  private static UnifiedRecordValue messageValue(final MemorySegment r, final ValueType vt, final ZbHip.Deployed d,
+      final int elem, final long scope, final long pik, final GpuBatchProcessor p) {
+    final int nameId = r.get(JAVA_SHORT, 68) & 0xFFFF, bpmnId = r.get(JAVA_SHORT, 70) & 0xFFFF;
+    final int corrId = r.get(JAVA_INT, 64);
+    final DirectBuffer name = new UnsafeBuffer((nameId == 0xFFFF ? "" : p.name(nameId)).getBytes());
+    final DirectBuffer bpmn = new UnsafeBuffer((bpmnId == 0xFFFF ? "" : p.name(bpmnId)).getBytes());
+    final DirectBuffer corr = new UnsafeBuffer(corrId == Messages.NO_STRING ? new byte[0] : p.stringValue(corrId));
+    final boolean interrupting = r.get(JAVA_BYTE, 76) != 0;
+    final long messageKey = r.get(JAVA_LONG, 56);
+    if (vt == ValueType.MESSAGE) {
+      return new MessageRecord().setName(name).setCorrelationKey(corr).setTimeToLive(0).setDeadline(0)
+          .setTenantId(TENANT);
+    }
+    if (vt == ValueType.MESSAGE_SUBSCRIPTION) {
+      return new MessageSubscriptionRecord().setProcessInstanceKey(pik).setElementInstanceKey(scope)
+          .setMessageKey(messageKey).setMessageName(name).setCorrelationKey(corr).setInterrupting(interrupting)
+          .setBpmnProcessId(bpmn).setTenantId(TENANT);
+    }
+    return new ProcessMessageSubscriptionRecord().setSubscriptionPartitionId(r.get(JAVA_INT, 72))
+        .setProcessInstanceKey(pik).setElementInstanceKey(scope).setMessageKey(messageKey).setMessageName(name)
+        .setInterrupting(interrupting).setBpmnProcessId(bpmn).setCorrelationKey(corr)
+        .setElementId(new UnsafeBuffer((elem >= 0 && r.get(JAVA_INT, 32) >= 0 ? d.elementIds()[elem] : "").getBytes()))
+        .setTenantId(TENANT);
   }
 
   /** One msgpack value of a zbhip_doc_type (FeelToMessagePackTransformer's encoding of an item). */

@@ -165,6 +165,8 @@ public final class ZbHip {
   private static final MethodHandle PENDING = fn("zbhip_pending_records", FunctionDescriptor.of(JAVA_LONG, ADDRESS));
   private static final MethodHandle DRAIN = fn("zbhip_drain", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle OUTBOX = fn("zbhip_outbox", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
+  private static final MethodHandle OUTBOX_COMMAND =
+      fn("zbhip_outbox_command", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle STATS_FN = fn("zbhip_get_stats", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
   private static final MethodHandle STATUS =
       fn("zbhip_command_status", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
@@ -387,6 +389,24 @@ public final class ZbHip {
       final MemorySegment n = a.allocate(JAVA_LONG);
       check((int) call(OUTBOX, h, out, cap, n), "zbhip_outbox");
       return n.get(JAVA_LONG, 0);
+    }
+  }
+
+  /**
+   * zbhip_outbox_command: the cross-partition commands window command i sent (XPART rows, its batch's
+   * post-commit side effects in batch order); returns a segment of exactly those rows.
+   */
+  public static MemorySegment outboxCommand(final MemorySegment h, final long i, final Arena arena) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      MemorySegment out = arena.allocate(XPART.byteSize() * 4, 16);
+      int rc = (int) call(OUTBOX_COMMAND, h, i, out, 4L, n);
+      if (rc == ENOMEM) {
+        out = arena.allocate(XPART.byteSize() * n.get(JAVA_LONG, 0), 16);
+        rc = (int) call(OUTBOX_COMMAND, h, i, out, n.get(JAVA_LONG, 0), n);
+      }
+      check(rc, "zbhip_outbox_command");
+      return out.asSlice(0, XPART.byteSize() * n.get(JAVA_LONG, 0));
     }
   }
 

@@ -458,8 +458,8 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out);
  * '<text>' to be 'BOOLEAN', but was '<NULL|NUMBER|STRING>'." (ExpressionProcessor.java:356-368).
  * Writes at most cap bytes (no NUL) and returns the full length, or < 0. */
 int64_t zbhip_incident_message(zbhip_handle* h, const zbhip_record* r, char* out, size_t cap);
-/* The records of window command i only (plain windows; ZBHIP_EUNSUPP for message partitions): what a
- * host adapter emits when the platform reaches command i.  Keys of the commands after a fallback
+/* The records of window command i only: what a host adapter emits when the platform reaches
+ * command i (message partitions too: a message record is one zbhip_record, as in zbhip_drain).  Keys of the commands after a fallback
  * command are fixed once the CPU engine's keys for it are declared (zbhip_set_external_keys), so a
  * command after an undeclared fallback returns ZBHIP_ESTATE; zbhip_drain, by contrast, fixes the
  * whole window (undeclared fallbacks generated no keys).  cap too small: ZBHIP_ENOMEM with *n_out =
@@ -492,6 +492,11 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx);
 /* Cross-partition commands the last run sent (post-commit side effects of its batches, in log
  * order, keys relabelled); the host routes them to their target partitions (drain mode). */
 int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_out);
+/* The cross-partition commands window command i sent (its batch's post-commit side effects,
+ * SubscriptionCommandSender.java:320-338, in batch order; keys relabelled): what a host adapter hands
+ * to InterPartitionCommandSender.sendCommand (stream/api/InterPartitionCommandSender.java) once the
+ * platform committed command i's batch.  cap too small: ZBHIP_ENOMEM with *n_out = the entries. */
+int zbhip_outbox_command(zbhip_handle* h, size_t i, zbhip_xpart_cmd* out, size_t cap, size_t* n_out);
 /* Device form: after zbhip_run (any mode) the outbox bucketed by target partition, stable in log
  * order, with device-computed keys; counts[t] = entries for partition t + 1 (partition_count
  * entries).  The pointer stays valid until the next run.  This is what the RCCL all-to-all sends.

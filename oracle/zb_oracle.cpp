@@ -1128,12 +1128,36 @@ class Oracle {
     rec.pi.elem = r.element_idx;
     rec.pi.flowScopeKey = r.scope_key;
     rec.pi.piKey = r.process_instance_key;
+    const bool msg = (r.value_type == ZBHIP_VT_MESSAGE && r.intent == ZBHIP_MSG_PUBLISH) ||
+                     (r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION &&
+                      (r.intent == ZBHIP_MS_CREATE || r.intent == ZBHIP_MS_CORRELATE)) ||
+                     (r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION &&
+                      (r.intent == ZBHIP_PMS_CREATE || r.intent == ZBHIP_PMS_CORRELATE));
     const bool known = (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION && r.intent == ZBHIP_PIC_CREATE) ||
                        (r.value_type == ZBHIP_VT_JOB && r.intent == ZBHIP_JOB_COMPLETE) ||
                        (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT) ||
-                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && r.intent == ZBHIP_PIB_ACTIVATE);
+                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && r.intent == ZBHIP_PIB_ACTIVATE) || msg;
     if (!known) { last_error = "process_one: command outside the restated subset"; return ZBHIP_EUNSUPP; }
+    if (msg) {
+      // the command's record value as the log holds it (MessageRecord / MessageSubscriptionRecord /
+      // ProcessMessageSubscriptionRecord): the subject is the correlation slot `instance` for MESSAGE
+      // and MESSAGE_SUBSCRIPTION commands, the process instance slot for PROCESS_MESSAGE_SUBSCRIPTION
+      MsgVal m;
+      m.eik = r.scope_key;
+      m.pik = r.process_instance_key;
+      m.msg_key = r.message_key;
+      m.corr = r.correlation_key;
+      m.name = r.message_name;
+      m.bpmn = r.bpmn_process_id;
+      m.partition = r.partition;
+      m.interrupting = r.interrupting;
+      m.inst = instance;
+      rec.doc = Doc{0, 0};
+      rec.r.aux = -1;
+      fill_msg(rec, m);
+      rec.slot = r.value_type != ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION;
+    }
     if (r.value_type == ZBHIP_VT_PROCESS_INSTANCE || r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION)
       if (r.process_idx < 0 || r.process_idx >= (int)procs.size() ||
           (r.value_type == ZBHIP_VT_PROCESS_INSTANCE &&
@@ -1144,7 +1168,7 @@ class Oracle {
     std::vector<ORecord> batch;
     batch_ = &batch;
     cur_instance_ = instance;
-    cur_slot_ = false;
+    cur_slot_ = rec.slot;
     cur_source_ = source;
     try {
       process(rec);

@@ -21,8 +21,8 @@ import numpy as np
 
 from oracle.oracle import Oracle
 from zeebe_amd import abi
-from zeebe_amd.adapter import (JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED, VT_JOB_BATCH, RecordValues, doc_entries,
-                               typed_value)
+from zeebe_amd.adapter import (JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED, MESSAGE_VALUE_TYPES, VT_JOB_BATCH, XPART_COMMAND,
+                               RecordValues, doc_entries, typed_value, xpart_value)
 from zeebe_amd.engine import ProcessDefinition
 
 
@@ -165,10 +165,12 @@ class OracleEngine:
     also the partition's DbKeyGenerator (KeyGeneratorControls) and the RawDbWriter of a hand-off."""
 
     ACCEPTS = (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, abi.VT_PROCESS_INSTANCE, VT_JOB_BATCH,
-               abi.VT_PROCESS_INSTANCE_BATCH)
+               abi.VT_PROCESS_INSTANCE_BATCH) + MESSAGE_VALUE_TYPES
 
-    def __init__(self, partition_id=1, max_commands_in_batch=100, clock=0):
-        self.o = Oracle(partition_id=partition_id, max_commands_in_batch=max_commands_in_batch)
+    def __init__(self, partition_id=1, max_commands_in_batch=100, clock=0, partition_count=1, command_sender=None):
+        self.o = Oracle(partition_id=partition_id, partition_count=partition_count,
+                        max_commands_in_batch=max_commands_in_batch)
+        self.command_sender = command_sender  # InterPartitionCommandSender of config 5
         self.o.set_clock(clock)
         self.pbits = partition_id << 51
         self.slot_of = {}
@@ -248,6 +250,24 @@ class OracleEngine:
             r["scope_key"], r["process_instance_key"] = v["batchElementInstanceKey"], v["processInstanceKey"]
             r["partition"] = v["index"]
             slot = self.slot_of.setdefault(v["processInstanceKey"], 0xFFFFF0 - len(self.slot_of))
+        elif vt == abi.VT_MESSAGE:
+            r["message_name"] = self.o.intern(v["name"])
+            r["correlation_key"] = self.o.intern_string(v["correlationKey"])
+            slot = int(r["correlation_key"])
+            variables = ()
+        elif vt in MESSAGE_VALUE_TYPES:
+            r["scope_key"], r["process_instance_key"] = v["elementInstanceKey"], v["processInstanceKey"]
+            r["message_key"] = v["messageKey"]
+            r["message_name"] = self.o.intern(v["messageName"])
+            r["bpmn_process_id"] = self.o.intern(v["bpmnProcessId"]) if v["bpmnProcessId"] else 0xFFFF
+            r["correlation_key"] = self.o.intern_string(v["correlationKey"]) if v["correlationKey"] else abi.NO_STRING
+            r["interrupting"] = int(v["interrupting"])
+            r["partition"] = v.get("subscriptionPartitionId", 0)
+            variables = ()
+            if vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION:
+                slot = self.slot_of.setdefault(v["processInstanceKey"], 0xFFFFF0 - len(self.slot_of))
+            else:
+                slot = 0xFFFFFF  # (the correlation slot: only the oracle's key bookkeeping uses it)
         docs = doc_entries(variables, self.o.intern, self.o.intern_string)
         base = len(self.doc_values)
         self.doc_values.extend(val for _, val in variables)
@@ -264,6 +284,17 @@ class OracleEngine:
                 self.slot_of[int(x["scope_key"])] = slot
             out.append_record(int(x["key"]), rt, xvt, xit, int(x["rejection_type"]),
                               self.o.reason(k) if rt == abi.RT_REJECTION else "", value)
+        sends = self.o.outbox()  # SubscriptionCommandSender's side effects of this command
+        if len(sends):
+            strings = self.o.strings()
+            cmds = [(int(x["target_partition"]),) + XPART_COMMAND[int(x["kind"])] +
+                    (xpart_value(x, self.o.name, lambda i: strings[i].decode()),) for x in sends]
+
+            def task():
+                for target, svt, sit, value in cmds:
+                    self.command_sender.send_command(target, svt, sit, value)
+                return True
+            out.append_post_commit_task(task)
         return out.build()
 
     def _activate(self, record, out):
@@ -307,6 +338,13 @@ class Client:
         return Rec(abi.RT_COMMAND, abi.VT_TIMER, abi.TIMER_TRIGGER, created.key, dict(created.value))
 
     @staticmethod
+    def publish_message(name, correlation_key):
+        """MessageClient.publish with time-to-live 0 (MessageRecord.java:37-43)."""
+        return Rec(abi.RT_COMMAND, abi.VT_MESSAGE, abi.MSG_PUBLISH, -1,
+                   {"name": name, "correlationKey": correlation_key, "timeToLive": 0, "variables": (), "messageId": "",
+                    "deadline": -1, "tenantId": "<default>"})
+
+    @staticmethod
     def activate_jobs(job_type, worker="w", timeout=300000, max_jobs=10, timestamp=0):
         return Rec(abi.RT_COMMAND, VT_JOB_BATCH, JOB_BATCH_ACTIVATE, -1,
                    {"type": job_type, "worker": worker, "timeout": timeout, "maxJobsToActivate": max_jobs,
@@ -334,3 +372,28 @@ def open_timers(log):
             elif r.intent in (abi.TIMER_TRIGGERED, abi.TIMER_CANCELED):
                 alive.pop(r.key, None)
     return alive
+
+
+class InterPartitionCommandSender:
+    """TestInterPartitionCommandSender (engine/src/test/.../util/TestInterPartitionCommandSender.java:
+    23-59): a sent command is written to the receiving partition's log as a COMMAND with key -1
+    (LogAppendEntry.of(metadata, command))."""
+
+    def __init__(self, logs):
+        self.logs = logs  # partition id -> Log
+
+    def send_command(self, receiver_partition, value_type, intent, value, key=-1):
+        self.logs[receiver_partition].append([Rec(abi.RT_COMMAND, value_type, intent, key, value)])
+
+
+def run_cluster(processors):
+    """Every partition's processing loop, round robin, until no partition has an unprocessed command
+    (EngineRule.multiplePartition: one stream processor per partition)."""
+    while True:
+        busy = False
+        for sp in processors:
+            if sp.read < len(sp.log.entries):
+                sp.run()
+                busy = True
+        if not busy:
+            return

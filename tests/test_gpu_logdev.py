@@ -215,3 +215,28 @@ def test_window_past_two_gigabytes():
     buf = C.create_string_buffer(used)
     part.L.zbhip_log_device_copy(part.h, buf, used)
     assert buf.raw[used - len(host):used] == host
+
+
+def test_declined_window_past_earlier_windows_and_after_a_redeploy():
+    # a window the size pass declines (string variables: the host serialiser writes them) whose
+    # records reach far past every earlier window's per-record info: the speculative write pass must
+    # write nothing for it (its entry info is incomplete); the next windows -- also after another
+    # process was deployed -- are written on the device again
+    log = Log(bpmn.linear_process(2), 600, names=("s",))
+    log.window(create_commands(4))
+    log.window(create_commands(4, first_instance=4))
+    n = 400
+    c = create_commands(n, first_instance=8)
+    c["doc_count"] = 1
+    c["doc_begin"] = np.arange(n)
+    d = abi.make_docs(n)
+    d["name_id"] = log.names[0]
+    d["type"] = abi.DOC_STR
+    d["value"] = [log.part.intern_string("v%d" % i) for i in range(n)]
+    log.window(c, d, allow_host=True)
+    assert log.declined == 1
+    recs = log.window(create_commands(64, first_instance=420))
+    assert log.part.deploy(bpmn.linear_process(3, process_id="later")) == 1
+    log.window(create_commands(32, process_idx=1, first_instance=484))
+    log.window(job_completions(recs, log.part))
+    assert log.declined == 1

@@ -1,0 +1,102 @@
+"""Config 5 through the drop-in boundary inside the reference's processing loop, on three partitions.
+
+Every partition runs ProcessingStateMachine (tests/psm.py) over its own log; the reference cluster runs
+[engine] on each, the device cluster [GpuBatchProcessor (zeebe_amd/adapter.py), engine].  Commands a
+batch sends to another partition (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition,
+:320-338) are written to the receiver's log after the batch is committed, by the test form of
+InterPartitionCommandSender (TestInterPartitionCommandSender.java:23-59).  The bar: every partition's
+log -- every record, position, source position and processed flag -- and every partition's state equal
+the reference cluster's.
+
+Workload: MessageCorrelationMultiplePartitionsTest.java:36-40,57-175 -- correlation keys "item-2",
+"item-1", "item-0" whose subscription partitions are 1, 2, 3 (SubscriptionUtil), instances created on
+every partition with every key (remote and local subscriptions), then messages published on each
+key's partition until every instance is correlated (time-to-live 0: one subscription per publish)."""
+import pytest
+
+from psm import Client, InterPartitionCommandSender, Log, OracleEngine, StreamProcessor, run_cluster
+from zeebe_amd import abi, bpmn
+from zeebe_amd.adapter import GpuBatchProcessor
+
+pytestmark = pytest.mark.gpu
+
+P = 3
+KEY = 2251799813685249
+CORRELATION_KEYS = {1: "item-2", 2: "item-1", 3: "item-0"}  # MessageCorrelationMultiplePartitionsTest.java:36-40
+XML = bpmn.message_catch_process(message_name="message", correlation_key="key", catch_id="receive-message")
+
+
+class Cluster:
+    def __init__(self, device, limit=100, window=48):
+        self.logs = {p: Log() for p in range(1, P + 1)}
+        sender = InterPartitionCommandSender(self.logs)
+        self.engines, self.adapters, self.sps = {}, {}, []
+        for p in range(1, P + 1):
+            eng = OracleEngine(partition_id=p, partition_count=P, max_commands_in_batch=limit, command_sender=sender)
+            eng.deploy(XML, KEY, 1)
+            procs = [eng]
+            if device:
+                ad = GpuBatchProcessor(eng, self.logs[p].reader(), [(XML, KEY, 1)], zeebe_db=eng, key_generator=eng,
+                                       partition_id=p, partition_count=P, instances=256, window=window,
+                                       max_commands_in_batch=limit, correlation_keys=64, command_sender=sender)
+                ad.init()
+                self.adapters[p] = ad
+                procs = [ad, eng]
+            self.engines[p] = eng
+            self.sps.append(StreamProcessor(self.logs[p], procs, limit))
+
+    def state(self, p):
+        eng = self.engines[p]
+        if p not in self.adapters:
+            return eng.state()
+        part = self.adapters[p].part
+        dev = [r for r in part.state() if not r.startswith("KEY|")]
+        assert part.current_key() <= eng.current_key()  # one key generator per partition
+        return sorted(dev + eng.state())
+
+
+def phase(ref, gpu, writes):
+    for p, recs in writes:
+        Client(ref.logs[p], gpu.logs[p]).write(*recs)
+    run_cluster(ref.sps)
+    run_cluster(gpu.sps)
+    for p in range(1, P + 1):
+        want, got = ref.logs[p].canonical(), gpu.logs[p].canonical()
+        if got != want:
+            n = min(len(got), len(want))
+            bad = next((i for i in range(n) if got[i] != want[i]), n)
+            raise AssertionError("partition %d log entry %d of %d/%d:\n got  %s\n want %s" % (
+                p, bad, len(got), len(want), got[bad] if bad < len(got) else None, want[bad] if bad < len(want) else None))
+        assert gpu.state(p) == sorted(ref.state(p)), p
+
+
+def create_phase():
+    """30 instances, 10 per correlation key, every partition creating instances of every key (local
+    and remote subscriptions): instance i on partition 1 + i % 3, key of partition 1 + (i + i // 3) % 3."""
+    creates = {p: [] for p in range(1, P + 1)}
+    for i in range(30):
+        creates[1 + i % 3].append(Client.create("process", (("key", CORRELATION_KEYS[1 + (i + i // 3) % 3]),)))
+    return sorted(creates.items())
+
+
+def test_message_correlation_on_three_partitions_in_the_processing_loop():
+    ref, gpu = Cluster(device=False), Cluster(device=True)
+    phase(ref, gpu, create_phase())
+    # shouldOpenMessageSubscriptionsOnDifferentPartitions: MESSAGE_SUBSCRIPTION:CREATED of key k only on
+    # its subscription partition
+    for cl in (ref, gpu):
+        created = [(p, r.value["correlationKey"]) for p in range(1, P + 1) for r in cl.logs[p].entries
+                   if r.value_type == abi.VT_MESSAGE_SUBSCRIPTION and r.record_type == abi.RT_EVENT
+                   and r.intent == abi.MS_CREATED]
+        assert len(created) == 30 and set(created) == set(CORRELATION_KEYS.items())
+    # a message nobody waits for (published and expired), then one message per subscription
+    pubs = [(p, [Client.publish_message("message", "nobody")] +
+             [Client.publish_message("message", CORRELATION_KEYS[p]) for _ in range(10)]) for p in range(1, P + 1)]
+    phase(ref, gpu, pubs)
+    done = sum(1 for p in range(1, P + 1) for r in gpu.logs[p].entries
+               if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == 5
+               and r.value["bpmnElementType"] == "PROCESS")
+    assert done == 30
+    c = [gpu.adapters[p].counts for p in range(1, P + 1)]
+    assert all(x["fallbacks"] == 0 for x in c)
+    assert sum(x["device_commands"] for x in c) >= 30 + 3 * 11 + 2 * 30  # creates, publishes, received commands

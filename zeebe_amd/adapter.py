@@ -22,6 +22,12 @@ inside ``ProcessingStateMachine.batchProcessing`` / ``collectBatchProcessingStep
   (JobBatchActivateProcessor.java:60-143).
 * After recovery, instances of device processes move from the engine's state into HBM
   (``on_recovered`` -> ``zbhip_import_state``), as StreamProcessorLifecycleAware.onRecovered would.
+* Config 5 (``correlation_keys`` > 0): MESSAGE:PUBLISH (time-to-live <= 0, no message id, no
+  variables), MESSAGE_SUBSCRIPTION:CREATE / CORRELATE and PROCESS_MESSAGE_SUBSCRIPTION:CREATE /
+  CORRELATE go to the device.  The cross-partition commands a device batch sends
+  (``zbhip_outbox_command``) are handed to ``InterPartitionCommandSender.sendCommand`` in a post-commit
+  task of that batch, as SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition (:320-338)
+  does; received ones become device commands again (``xpart_of``).
 
 Record values are dicts keyed by the reference's property names (ProcessInstanceRecord.java:61-72,
 JobRecord, VariableRecord, ProcessEventRecord, TimerRecord, ProcessInstanceCreationRecord,
@@ -42,6 +48,48 @@ from .engine import Partition
 
 VT_JOB_BATCH = 1
 JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED = 0, 1
+MESSAGE_VALUE_TYPES = (abi.VT_MESSAGE, abi.VT_MESSAGE_SUBSCRIPTION, abi.VT_PROCESS_MESSAGE_SUBSCRIPTION)
+# zbhip_xpart_cmd kind <-> (value type, intent) of the command SubscriptionCommandSender sends
+XPART_COMMAND = {abi.CMD_MSG_SUB_CREATE: (abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_CREATE),
+                 abi.CMD_MSG_SUB_CORRELATE: (abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_CORRELATE),
+                 abi.CMD_PMS_CREATE: (abi.VT_PROCESS_MESSAGE_SUBSCRIPTION, abi.PMS_CREATE),
+                 abi.CMD_PMS_CORRELATE: (abi.VT_PROCESS_MESSAGE_SUBSCRIPTION, abi.PMS_CORRELATE)}
+XPART_KIND = {v: k for k, v in XPART_COMMAND.items()}
+KEY_BITS = 51  # Protocol.KEY_BITS
+
+
+def partition_of_key(key):
+    """Protocol.decodePartitionId (protocol/.../Protocol.java:102-104)."""
+    return key >> KEY_BITS
+
+
+def xpart_value(x, name, string_value):
+    """The record value of a sent cross-partition command (a zbhip_xpart_cmd row), exactly as the
+    SubscriptionCommandSender method that sends it sets it (SubscriptionCommandSender.java:54-218);
+    properties it does not set keep their declared defaults (MessageSubscriptionRecord.java:33-48,
+    ProcessMessageSubscriptionRecord.java:37-54: interrupting true, messageKey -1, strings empty)."""
+    kind = int(x["kind"])
+    nm = name(int(x["message_name"]))
+    bpmn = name(int(x["bpmn_process_id"])) if int(x["bpmn_process_id"]) != 0xFFFF else ""
+    corr = string_value(int(x["correlation_key"])) if int(x["correlation_key"]) != abi.NO_STRING else ""
+    pik, eik = int(x["process_instance_key"]), int(x["element_instance_key"])
+    if kind == abi.CMD_MSG_SUB_CREATE:  # openMessageSubscription (:54-76)
+        return {"processInstanceKey": pik, "elementInstanceKey": eik, "messageKey": -1, "messageName": nm,
+                "correlationKey": corr, "interrupting": bool(x["interrupting"]), "bpmnProcessId": bpmn,
+                "variables": (), "tenantId": TENANT}
+    if kind == abi.CMD_MSG_SUB_CORRELATE:  # correlateMessageSubscription (:200-218)
+        return {"processInstanceKey": pik, "elementInstanceKey": eik, "messageKey": -1, "messageName": nm,
+                "correlationKey": "", "interrupting": True, "bpmnProcessId": bpmn, "variables": (),
+                "tenantId": TENANT}
+    sender = int(x["source_partition"])
+    if kind == abi.CMD_PMS_CREATE:  # openProcessMessageSubscription (:116-134)
+        return {"subscriptionPartitionId": sender, "processInstanceKey": pik, "elementInstanceKey": eik,
+                "messageKey": -1, "messageName": nm, "variables": (), "interrupting": bool(x["interrupting"]),
+                "bpmnProcessId": "", "correlationKey": "", "elementId": "", "tenantId": TENANT}
+    # correlateProcessMessageSubscription (:136-159)
+    return {"subscriptionPartitionId": sender, "processInstanceKey": pik, "elementInstanceKey": eik,
+            "messageKey": int(x["message_key"]), "messageName": nm, "variables": (), "interrupting": True,
+            "bpmnProcessId": bpmn, "correlationKey": corr, "elementId": "", "tenantId": TENANT}
 PI_COMMAND_INTENTS = (8, 9, 10)  # ACTIVATE_ELEMENT, COMPLETE_ELEMENT, TERMINATE_ELEMENT
 TENANT = "<default>"  # TenantOwned.DEFAULT_TENANT_IDENTIFIER
 
@@ -124,6 +172,26 @@ class RecordValues:
             return {"bpmnProcessId": p.bpmn_process_id, "processDefinitionKey": p.definition_key,
                     "version": p.version, "processInstanceKey": scope, "variables": tuple(command_doc),
                     "tenantId": TENANT}
+        if vt in MESSAGE_VALUE_TYPES:
+            # the drained record carries every property of the reference value (logwriter.cpp: the
+            # same fields); message variables are empty in the subset, deadline = the PUBLISH
+            # command's timestamp + timeToLive 0 (MessagePublishProcessor.java:110)
+            nid, bid, cid = int(r["message_name"]), int(r["bpmn_process_id"]), int(r["correlation_key"])
+            nm = self.name(nid) if nid != 0xFFFF else ""
+            corr = self.string_value(cid) if cid != abi.NO_STRING else ""
+            if vt == abi.VT_MESSAGE:  # MessageRecord.java:37-43
+                return {"name": nm, "correlationKey": corr, "timeToLive": 0, "variables": (), "messageId": "",
+                        "deadline": 0, "tenantId": TENANT}
+            bpmn = self.name(bid) if bid != 0xFFFF else ""
+            common = {"processInstanceKey": pik, "elementInstanceKey": scope, "messageKey": int(r["message_key"]),
+                      "messageName": nm, "correlationKey": corr, "interrupting": bool(r["interrupting"]),
+                      "bpmnProcessId": bpmn, "variables": (), "tenantId": TENANT}
+            if vt == abi.VT_MESSAGE_SUBSCRIPTION:  # MessageSubscriptionRecord.java:40-48
+                return common
+            # ProcessMessageSubscriptionRecord.java:44-54
+            common.update({"subscriptionPartitionId": int(r["partition"]),
+                           "elementId": p.element_ids[elem] if elem >= 0 and int(r["process_idx"]) >= 0 else ""})
+            return common
         raise ValueError("value type outside the adapter's subset: %d" % vt)
 
     def job_batch(self, command, key, jobs, name, string_value):
@@ -155,6 +223,7 @@ class Window:
         self.doc_values = []  # the client value of each entry (VARIABLE records)
         self.positions = []
         self.instances = []
+        self.xparts = []     # received cross-partition commands (zbhip_xpart_cmd rows)
         self.doc_base = 0    # zbhip doc index of this window's first entry
 
     def reset(self, doc_base):
@@ -208,7 +277,7 @@ class GpuBatchProcessor:
 
     def __init__(self, engine, reader, deployments, zeebe_db, key_generator, partition_id=1, partition_count=1,
                  device=0, instances=1 << 16, window=None, max_commands_in_batch=100, max_records_per_batch=256,
-                 clock=None, engine_deployments=()):
+                 clock=None, engine_deployments=(), correlation_keys=0, command_sender=None):
         self.engine = engine
         self.reader = reader
         self.deployments = deployments
@@ -222,6 +291,14 @@ class GpuBatchProcessor:
         self.limit = max_commands_in_batch
         self.max_records = max_records_per_batch
         self.clock = clock or (lambda: 0)  # ActorClock.currentTimeMillis
+        # config 5: correlation slots in HBM (0: message commands stay with the engine) and the
+        # platform's InterPartitionCommandSender (RecordProcessorContext.getPartitionCommandSender)
+        self.correlation_keys = correlation_keys
+        self.command_sender = command_sender
+        self.message_names = set()     # message names of the device's catch events (PUBLISH subset)
+        self.subscriptions = {}        # (elementInstanceKey, messageName) -> correlation slot of an open
+                                       # MESSAGE_SUBSCRIPTION (MESSAGE_SUBSCRIPTION_BY_KEY): a CORRELATE's
+                                       # value carries no correlation key
         self.part = None
         self.by_key, self.latest_by_id, self.by_index = {}, {}, []
         self.engine_job_types = set()  # job types the engine's processes (or handed-off instances) hold
@@ -249,7 +326,7 @@ class GpuBatchProcessor:
         self.part = Partition(partition_id=self.partition_id, partition_count=self.partition_count,
                               device=self.device, max_instances=self.instances, max_commands=self.window_size,
                               max_records_per_batch=self.max_records, max_doc_entries=16 * self.window_size,
-                              max_commands_in_batch=self.limit,
+                              max_commands_in_batch=self.limit, max_correlation_keys=self.correlation_keys,
                               initial_key=self.key_generator.current_key() - pbits, defer_continuations=True)
         for xml, key, version in self.deployments:
             self.deploy(xml, key, version)
@@ -266,6 +343,8 @@ class GpuBatchProcessor:
             self.by_index.append(None)
             return None
         p = self.part.processes[idx]
+        from .bpmn import message_names_of
+        self.message_names.update(message_names_of(xml))
         self.by_key[key] = p
         self.by_index.append(p)
         prev = self.latest_by_id.get(p.bpmn_process_id)
@@ -275,7 +354,7 @@ class GpuBatchProcessor:
 
     def accepts(self, value_type):
         return value_type in (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, VT_JOB_BATCH) \
-            or self.engine.accepts(value_type)
+            or (self.correlation_keys > 0 and value_type in MESSAGE_VALUE_TYPES) or self.engine.accepts(value_type)
 
     def replay(self, record):
         # events only; the appliers write the engine's state.  Instances restored this way move
@@ -385,7 +464,83 @@ class GpuBatchProcessor:
                 (vt == abi.VT_PROCESS_INSTANCE_BATCH and it == abi.PIB_ACTIVATE):
             # a follow-up a device batch wrote unprocessed, read back in the order written
             return k < len(self.continuations) and self.continuations[k][2] == self._continuation_match(record)
+        if self.correlation_keys > 0 and vt in MESSAGE_VALUE_TYPES:
+            return self._message_command(record) is not None
         return False
+
+    # ---- config 5: message commands <-> device commands ------------------------------------------
+    def _message_command(self, record):
+        """A message command of the log as (zbhip_command row, zbhip_xpart_cmd row or None), or None
+        when the device does not take it: PUBLISH outside the subset (a time-to-live, a message id,
+        variables, a name no device catch event waits for), PROCESS_MESSAGE_SUBSCRIPTION commands of an
+        instance the device does not hold, MESSAGE_SUBSCRIPTION commands of a local instance the
+        device does not hold."""
+        v, vt, it = record.value, record.value_type, record.intent
+        if vt == abi.VT_MESSAGE:
+            if it != abi.MSG_PUBLISH or v.get("timeToLive", 0) > 0 or v.get("messageId") or v.get("variables") \
+                    or v.get("name") not in self.message_names or not isinstance(v.get("correlationKey"), str):
+                return None
+            corr = self.part.intern_string(v["correlationKey"])
+            if corr >= self.correlation_keys:
+                return None
+            return {"instance": corr, "kind": abi.CMD_PUBLISH, "ref": self.part.intern(v["name"])}, None
+        kind = XPART_KIND.get((vt, it))
+        if kind is None or v.get("variables"):
+            return None
+        pik, eik = v["processInstanceKey"], v["elementInstanceKey"]
+        x = abi.make_xparts(1)[0]
+        x["element_instance_key"], x["process_instance_key"] = eik, pik
+        x["message_key"] = v.get("messageKey", -1)
+        x["message_name"] = self.part.intern(v["messageName"])
+        x["bpmn_process_id"] = self.part.intern(v["bpmnProcessId"]) if v.get("bpmnProcessId") else 0xFFFF
+        x["correlation_key"] = self.part.intern_string(v["correlationKey"]) if v.get("correlationKey") else abi.NO_STRING
+        x["kind"] = kind
+        x["interrupting"] = int(bool(v.get("interrupting", True)))
+        x["target_partition"] = self.partition_id
+        if vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION:
+            # the PI partition's side: the subscribing element instance of a device instance
+            pi, el = self._resolve(pik), self._resolve(eik)
+            if pi is None or el is None or pi[0] != el[0]:
+                return None
+            x["instance"], x["element_ord"] = el
+            x["source_partition"] = v["subscriptionPartitionId"]
+            return {"instance": el[0], "kind": kind, "ref": 0}, x
+        # the message partition's side: the routing handle of the subscribing element instance --
+        # its slot and key ordinal when the instance lives here (a local correlation enters it in the
+        # same batch), else an id derived from the element instance key, unique per subscription like
+        # the reference's [elementInstanceKey, messageName] (the PI partition resolves the keys itself)
+        src = partition_of_key(pik)
+        if src == self.partition_id:
+            el = self._resolve(eik)
+            if el is None:
+                return None
+            x["instance"], x["element_ord"] = el
+        else:
+            n = eik - (partition_of_key(eik) << KEY_BITS)
+            x["instance"], x["element_ord"] = n & 0xFFFFFFFF, (n >> 32) & 0xFFFF
+        x["source_partition"] = src
+        if kind == abi.CMD_MSG_SUB_CORRELATE:
+            x["correlation_key"] = self.subscriptions.get((eik, v["messageName"]), 0)
+        if int(x["correlation_key"]) >= self.correlation_keys:
+            return None
+        return {"instance": int(x["correlation_key"]), "kind": kind, "ref": 0}, x
+
+    def _send(self, i, out):
+        """Window command i's cross-partition commands, sent once its batch is committed
+        (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition :320-338: a side effect)."""
+        sends = self.part.outbox_command(i)
+        if not len(sends):
+            return
+        if self.command_sender is None:
+            raise RuntimeError("a device batch sent cross-partition commands but no InterPartitionCommandSender is set")
+        cmds = [(int(x["target_partition"]),) + XPART_COMMAND[int(x["kind"])] +
+                (xpart_value(x, self.part.name, self.part.string_value),) for x in sends]
+
+        def task():
+            for target, vt, it, value in cmds:
+                self.command_sender.send_command(target, vt, it, value)
+            return True
+        out.append_post_commit_task(task)
 
     def _fill_window(self, first):
         """Reads consecutive hot-path commands from the log starting at `first` (GpuBatchProcessor
@@ -422,6 +577,12 @@ class GpuBatchProcessor:
                 inst, ordv = self._resolve(rec.key)
                 due = rec.value["dueDate"]
                 self.window.put(rec, inst, abi.CMD_TIMER_TRIGGER, ordv, doc_begin=due & 0xFFFFFFFF, pad=due >> 32)
+            elif vt in MESSAGE_VALUE_TYPES:
+                c, x = self._message_command(rec)
+                if x is not None:
+                    c["doc_begin"] = len(self.window.xparts)
+                    self.window.xparts.append(x)
+                self.window.put(rec, c["instance"], c["kind"], c["ref"], doc_begin=c.get("doc_begin", 0))
             else:
                 cid, slot, _ = self.continuations[claimed]
                 claimed += 1
@@ -433,7 +594,12 @@ class GpuBatchProcessor:
         self.part.set_clock(self.clock())
         cmds, docs = self.window.arrays()
         self.counts["windows"] += 1
-        self.part.submit(cmds, docs)
+        xparts = None
+        if self.window.xparts:
+            xparts = abi.make_xparts(len(self.window.xparts))
+            for j, x in enumerate(self.window.xparts):
+                xparts[j] = x
+        self.part.submit(cmds, docs, xparts)
         self.doc_total += len(docs)
         self.part.run()
         # the records are drained command by command as the platform reaches them
@@ -477,7 +643,15 @@ class GpuBatchProcessor:
                     admitted += 1
             elif vt == abi.VT_PROCESS_INSTANCE and it == 5 and value.get("bpmnElementType") == "PROCESS":
                 self.ended.add(win.instances[i])  # its slot is free once its continuations ran
+            elif vt == abi.VT_MESSAGE_SUBSCRIPTION and rt == abi.RT_EVENT:
+                sub = (value["elementInstanceKey"], value["messageName"])
+                if it == abi.MS_CREATED:
+                    self.subscriptions[sub] = int(r["correlation_key"])
+                elif it == abi.MS_CORRELATED:
+                    self.subscriptions.pop(sub, None)
         self.followups = admitted
+        if self.correlation_keys > 0:
+            self._send(i, out)
 
     # ---- keys ------------------------------------------------------------------------------------
     def _batch_done(self):

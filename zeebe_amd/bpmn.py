@@ -403,3 +403,11 @@ def job_types_of(xml):
     if isinstance(xml, bytes):
         xml = xml.decode()
     return set(m for m in re.findall(r'taskDefinition[^>]*?\stype="([^"=][^"]*)"', xml))
+
+
+def message_names_of(xml):
+    """Static message names (<message name="...">) a BPMN XML declares."""
+    import re
+    if isinstance(xml, bytes):
+        xml = xml.decode()
+    return set(re.findall(r'<(?:\w+:)?message\b[^>]*?\sname="([^"=][^"]*)"', xml))

@@ -359,11 +359,13 @@ __device__ __forceinline__ bool doc_ok(const zbhip_doc_entry& d) {
   return d.type == ZBHIP_DOC_NIL || d.type == ZBHIP_DOC_BOOL || d.type == ZBHIP_DOC_INT || d.type == ZBHIP_DOC_DEC;
 }
 
-// mp_bin of the command's document (DocumentValue: empty -> EMPTY_DOCUMENT; one entry -> a map)
+// mp_bin of the command's document (DocumentValue: empty -> EMPTY_DOCUMENT; one entry -> a map);
+// false for a document the device does not write (several entries, a string value)
 template <class S>
-__device__ __forceinline__ void src_doc_bin(S& s, const LogParams& L, const LogCmd& m) {
-  if (m.doc_count == 0) { s.bytes(L, run(L, G_EMPTY_BIN)); return; }
+__device__ __forceinline__ bool src_doc_bin(S& s, const LogParams& L, const LogCmd& m) {
+  if (m.doc_count == 0) { s.bytes(L, run(L, G_EMPTY_BIN)); return true; }
   const zbhip_doc_entry d = L.docs[m.doc_begin];
+  if (m.doc_count != 1 || !doc_ok(d)) return false;
   const uint2 nr = name_run(L, d.name_id);
   const uint32_t len = 1 + nr.y + doc_value_len(d);
   s.b(0xc4);  // < 256 bytes: a name and a scalar
@@ -371,6 +373,7 @@ __device__ __forceinline__ void src_doc_bin(S& s, const LogParams& L, const LogC
   s.b(0x81);
   s.bytes(L, nr);
   doc_value(s, d);
+  return true;
 }
 
 template <class S>
@@ -423,14 +426,14 @@ __device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m,
     case ZBHIP_VT_JOB:
       if (r.rt == ZBHIP_RT_REJECTION) {
         s.bytes(L, run(L, G_JREJ_HEAD));
-        src_doc_bin(s, L, m);
+        if (!src_doc_bin(s, L, m)) return false;
         s.bytes(L, run(L, G_JREJ_TAIL));
         return true;
       }
       if (!has_el || el_run(L, pb, r.elem, E_JOB_HEAD).y == 0) return false;
       s.bytes(L, el_run(L, pb, r.elem, E_JOB_HEAD));
-      if (r.intent == ZBHIP_JOB_COMPLETED) src_doc_bin(s, L, m);
-      else s.bytes(L, run(L, G_EMPTY_BIN));
+      if (r.intent != ZBHIP_JOB_COMPLETED) s.bytes(L, run(L, G_EMPTY_BIN));
+      else if (!src_doc_bin(s, L, m)) return false;
       s.bytes(L, el_run(L, pb, r.elem, E_JOB_MID));
       mp_int(s, r.pik);
       s.bytes(L, el_run(L, pb, r.elem, E_JOB_TAIL));
@@ -441,7 +444,7 @@ __device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m,
       // the batch's source document entry of that name (VariableRecord.java:35-41)
       if (!pb || m.doc_count != 1) return false;
       const zbhip_doc_entry d = L.docs[m.doc_begin];
-      if (d.name_id != r.elem) return false;
+      if (d.name_id != r.elem || !doc_ok(d)) return false;
       const uint2 nr = name_run(L, r.elem);
       s.bytes(L, run(L, G_VAR_A));
       s.bytes(L, nr);
@@ -468,7 +471,7 @@ __device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m,
       s.bytes(L, el_run(L, pb, r.elem, E_ID_STR));
       s.bytes(L, run(L, G_K_VARS));
       if (r.intent == ZBHIP_PE_TRIGGERED) s.bytes(L, run(L, G_EMPTY_BIN));  // processEventTriggered: reset record
-      else src_doc_bin(s, L, m);
+      else if (!src_doc_bin(s, L, m)) return false;
       s.bytes(L, run(L, G_K_DEF));
       mp_int(s, (long long)(((unsigned long long)L.idx[pb + 3] << 32) | L.idx[pb + 2]));
       s.bytes(L, run(L, G_K_PIK));
@@ -503,7 +506,7 @@ __device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m,
       s.bytes(L, run(L, G_K_VERSION));
       mp_int(s, (long long)(int32_t)L.idx[pb + 4]);
       s.bytes(L, run(L, G_K_VARS));
-      src_doc_bin(s, L, m);
+      if (!src_doc_bin(s, L, m)) return false;
       s.bytes(L, run(L, G_PIC_TAIL));
       s.bytes(L, run(L, G_TENANT));
       return true;

@@ -593,6 +593,7 @@ struct zbhip_handle {
   unsigned long long* d_key_blk = nullptr;
   bool bucketed = false;
   bool outbox_taken = false;  // zbhip_outbox_device already handed out the last run's outbox
+  uint64_t xout_host_run = ~0ull;  // windows_run of the outbox copy in h_xout (zbhip_outbox_command)
   bool published = false;                      // a publish ran: MESSAGE_STATS row exists
   std::vector<uint4> h_hdr2;
   std::vector<int64_t> h_base;                 // key counter before each command's first key
@@ -2362,6 +2363,64 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
   return ZBHIP_OK;
 }
 
+// Record drain_rec of window command c as a zbhip_record (ordinal ord), keys relabelled; advances
+// rec past the row(s) it used (a message record and its payload rows) and ord by one.
+static int expand_row(zbhip_handle* h, size_t c, size_t& rec, size_t& ord, zbhip_record& r) {
+  const uint2 hd = h->h_hdr[c];
+  const uint32_t nrec = hd.x & 0xFFFF;
+  const zbhip_command& cm = h->h_cmds[c];
+  // the instance the records refer to: the command's, or the one a message batch loaded
+  const uint32_t inst = h->msg() && slot_kind(cm.kind) ? h->h_hdr2[c].x : cm.instance;
+  const uint2* rows = h->h_out.data() + h->h_off[c];
+  const uint2 w = rows[rec];
+  const uint32_t elem = w.y & 0xFFFF;
+  const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
+  const bool rej = code & kRejectBit;
+  const uint32_t c6 = code & 0x3F;
+  const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
+  r = zbhip_record{};
+  r.source_index = h->source_base + (int64_t)c;
+  r.rejection_type = ZBHIP_REJ_NONE;
+  r.ordinal = (uint16_t)ord;
+  r.aux = -1;
+  r.message_key = -1;
+  r.correlation_key = ZBHIP_NO_STRING;
+  r.message_name = 0xFFFF;
+  r.bpmn_process_id = 0xFFFF;
+  if (h->msg() && elem != NONE && (elem & kPayloadBit)) {
+    // message record: 6 payload rows (kernels.hip emit_msg)
+    if (rec + kPayloadRows >= nrec) return ZBHIP_EDEVICE;
+    const uint2* pl = rows + rec + 1;
+    auto ll = [](uint2 v) { return (long long)(((unsigned long long)v.y << 32) | v.x); };
+    if (!message_code(c6, r)) return ZBHIP_EDEVICE;
+    const uint32_t el = elem & 0xFFF;
+    r.correlation_key = pl[0].x;
+    r.message_name = (uint16_t)(pl[0].y & 0xFFFF);
+    r.bpmn_process_id = (uint16_t)(pl[0].y >> 16);
+    r.key = h->resolve_ref(ll(pl[1]));
+    r.scope_key = h->resolve_ref(ll(pl[2]));
+    r.process_instance_key = h->resolve_ref(ll(pl[3]));
+    r.message_key = h->resolve_ref(ll(pl[4]));
+    r.partition = (int32_t)(pl[5].x & 0xFFFF);
+    r.interrupting = (uint8_t)(pl[5].x >> 16);
+    r.element_idx = el == kNoElem ? -1 : (int32_t)el;
+    r.process_idx = el == kNoElem || proc == NONE ? -1 : proc;
+    if (rej) {
+      r.record_type = ZBHIP_RT_REJECTION;
+      r.reason = fl & 0xF;
+      r.reason_arg = fl >> 4;
+      r.rejection_type = rejection_type_of(r.reason);
+    }
+    rec += 1 + kPayloadRows;
+    ++ord;
+    return ZBHIP_OK;
+  }
+  if (int rc = expand_plain(h, c, inst, w, ord, r)) return rc;
+  ++rec;
+  ++ord;
+  return ZBHIP_OK;
+}
+
 int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
   if (!h || (cap && !out)) return ZBHIP_EINVAL;
   if (n_out) *n_out = 0;
@@ -2406,61 +2465,9 @@ int zbhip_drain(zbhip_handle* h, zbhip_record* out, size_t cap, size_t* n_out) {
       h->drain_ord = 0;
       continue;
     }
-    const zbhip_command& cm = h->h_cmds[c];
-    // the instance the records refer to: the command's, or the one a message batch loaded
-    const uint32_t inst = h->msg() && slot_kind(cm.kind) ? h->h_hdr2[c].x : cm.instance;
-    const uint2* rows = h->h_out.data() + h->h_off[c];
-    const uint2 w = rows[h->drain_rec];
-    const uint32_t elem = w.y & 0xFFFF;
-    const uint32_t code = (w.y >> 16) & 0xFF, fl = w.y >> 24;
-    const bool rej = code & kRejectBit;
-    const uint32_t c6 = code & 0x3F;
-    const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
-    zbhip_record r{};
-    r.source_index = h->source_base + (int64_t)c;
-    r.rejection_type = ZBHIP_REJ_NONE;
-    r.ordinal = (uint16_t)h->drain_ord;
-    r.aux = -1;
-    r.message_key = -1;
-    r.correlation_key = ZBHIP_NO_STRING;
-    r.message_name = 0xFFFF;
-    r.bpmn_process_id = 0xFFFF;
-    if (h->msg() && elem != NONE && (elem & kPayloadBit)) {
-      // message record: 6 payload rows (kernels.hip emit_msg)
-      if (h->drain_rec + kPayloadRows >= nrec) return ZBHIP_EDEVICE;
-      const uint2* pl = rows + h->drain_rec + 1;
-      auto ll = [](uint2 v) { return (long long)(((unsigned long long)v.y << 32) | v.x); };
-      if (!message_code(c6, r)) return ZBHIP_EDEVICE;
-      const uint32_t el = elem & 0xFFF;
-      r.correlation_key = pl[0].x;
-      r.message_name = (uint16_t)(pl[0].y & 0xFFFF);
-      r.bpmn_process_id = (uint16_t)(pl[0].y >> 16);
-      r.key = h->resolve_ref(ll(pl[1]));
-      r.scope_key = h->resolve_ref(ll(pl[2]));
-      r.process_instance_key = h->resolve_ref(ll(pl[3]));
-      r.message_key = h->resolve_ref(ll(pl[4]));
-      r.partition = (int32_t)(pl[5].x & 0xFFFF);
-      r.interrupting = (uint8_t)(pl[5].x >> 16);
-      r.element_idx = el == kNoElem ? -1 : (int32_t)el;
-      r.process_idx = el == kNoElem || proc == NONE ? -1 : proc;
-      if (rej) {
-        r.record_type = ZBHIP_RT_REJECTION;
-        r.reason = fl & 0xF;
-        r.reason_arg = fl >> 4;
-        r.rejection_type = rejection_type_of(r.reason);
-      }
-      out[k++] = r;
-      h->drain_rec += 1 + kPayloadRows;
-      ++h->drain_ord;
-      continue;
-    }
-    {
-      const int rc = expand_plain(h, c, inst, w, h->drain_ord, r);
-      if (rc) return rc;
-    }
+    zbhip_record r;
+    if (int rc = expand_row(h, c, h->drain_rec, h->drain_ord, r)) return rc;
     out[k++] = r;
-    ++h->drain_rec;
-    ++h->drain_ord;
   }
   if (n_out) *n_out = k;
   return ZBHIP_OK;
@@ -2502,12 +2509,28 @@ int zbhip_drain_command(zbhip_handle* h, size_t i, zbhip_record* out, size_t cap
   if (!h || (cap && !out) || !n_out) return ZBHIP_EINVAL;
   *n_out = 0;
   if (!h->results) return ZBHIP_ESTATE;
-  if (h->msg()) return ZBHIP_EUNSUPP;
   if (i >= h->n_cmds) return ZBHIP_EINVAL;
   if (int rc = advance(h, i + 1, false)) return rc;
   if (h->fin_next <= i) return ZBHIP_ESTATE;
   if (int rc = ensure_out(h)) return rc;
   const uint32_t nrec = h->h_hdr[i].x & 0xFFFF;
+  if (h->msg()) {  // message records span payload rows: count them first
+    size_t need = 0;
+    const uint2* rows = h->h_out.data() + h->h_off[i];
+    for (uint32_t k = 0; k < nrec; ++need) {
+      const uint32_t elem = rows[k].y & 0xFFFF;
+      k += elem != NONE && (elem & kPayloadBit) ? 1 + kPayloadRows : 1;
+    }
+    if (cap < need) {
+      *n_out = need;
+      return ZBHIP_ENOMEM;
+    }
+    size_t rec = 0, ord = 0;
+    for (size_t k = 0; k < need; ++k)
+      if (int rc = expand_row(h, i, rec, ord, out[k])) return rc;
+    *n_out = need;
+    return ZBHIP_OK;
+  }
   if (cap < nrec) {
     *n_out = nrec;
     return ZBHIP_ENOMEM;
@@ -2604,6 +2627,38 @@ int zbhip_outbox(zbhip_handle* h, zbhip_xpart_cmd* out, size_t cap, size_t* n_ou
   }
   *n_out = k;
   return ZBHIP_OK;
+}
+
+// The sends of window command i (its batch's post-commit side effects, in batch order): what a host
+// adapter hands to InterPartitionCommandSender once the platform committed command i's batch.
+int zbhip_outbox_command(zbhip_handle* h, size_t i, zbhip_xpart_cmd* out, size_t cap, size_t* n_out) {
+  if (!h || !n_out || (cap && !out)) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (!h->results) return h->msg() ? ZBHIP_ESTATE : ZBHIP_OK;
+  if (!h->msg()) return ZBHIP_OK;
+  if (i >= h->n_cmds) return ZBHIP_EINVAL;
+  if (int rc = advance(h, i + 1, false)) return rc;
+  const size_t n = h->n_cmds;
+  if (h->xout_host_run != h->windows_run || h->h_xout.size() != n * kOut) {
+    h->h_xout.resize(n * kOut);
+    if (n) {
+      HIPCHK(hipMemcpy2DAsync(h->h_xout.data(), n * sizeof(zbhip_xpart_cmd), h->d_xout,
+                              (size_t)h->cfg.max_commands * sizeof(zbhip_xpart_cmd), n * sizeof(zbhip_xpart_cmd), kOut,
+                              hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+    }
+    h->xout_host_run = h->windows_run;
+  }
+  if (((h->h_hdr[i].y >> 16) & 0xFF) != ST_OK) return ZBHIP_OK;
+  size_t k = 0;
+  for (uint32_t j = 0; j < (h->h_hdr2[i].z & 0xF) && j < (uint32_t)kOut; ++j) {
+    const zbhip_xpart_cmd& x = h->h_xout[j * n + i];
+    if (x.kind == XK_PATCH) continue;
+    if (k < cap) out[k] = x;
+    ++k;
+  }
+  *n_out = k;
+  return k > cap ? ZBHIP_ENOMEM : ZBHIP_OK;
 }
 
 int zbhip_outbox_device(zbhip_handle* h, const zbhip_xpart_cmd** dev_out, uint32_t* counts) {

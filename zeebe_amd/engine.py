@@ -185,6 +185,16 @@ class Partition:
             check(self.L.zbhip_outbox(self.h, out.ctypes.data, n.value, C.byref(n)), "zbhip_outbox")
         return out
 
+    def outbox_command(self, i, cap=8):
+        """The cross-partition commands window command i sent (zbhip_outbox_command)."""
+        out = abi.make_xparts(cap)
+        n = C.c_size_t()
+        rc = self.L.zbhip_outbox_command(self.h, i, out.ctypes.data, cap, C.byref(n))
+        if rc == -2 and n.value > cap:
+            return self.outbox_command(i, n.value)
+        check(rc, "zbhip_outbox_command")
+        return out[: n.value]
+
     def outbox_copy(self, dev_dst, first, count):
         check(self.L.zbhip_outbox_copy(self.h, dev_dst, first, count), "zbhip_outbox_copy")
 

@@ -32,7 +32,7 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_import_state", "zbhip_activate_jobs", "zbhip_job_batch_rejection_reason",
            "zbhip_serialize_log_device", "zbhip_log_device_copy", "zbhip_continuations",
            "zbhip_pending_continuations", "zbhip_current_key", "zbhip_set_key_if_higher",
-           "zbhip_select_instances_db", "zbhip_drain_command"]
+           "zbhip_select_instances_db", "zbhip_drain_command", "zbhip_outbox_command"]
 
 
 class ZbhipError(RuntimeError):
@@ -107,6 +107,7 @@ def load():
     L.zbhip_current_key.argtypes = [vp, C.POINTER(i64)]
     L.zbhip_set_key_if_higher.argtypes = [vp, i64]
     L.zbhip_drain_command.argtypes = [vp, sz, vp, sz, C.POINTER(sz)]
+    L.zbhip_outbox_command.argtypes = [vp, sz, vp, sz, C.POINTER(sz)]
     L.zbhip_select_instances_db.argtypes = [vp, vp, sz, vp, sz, vp, sz, C.POINTER(sz)]
     L.zbhip_set_external_keys.argtypes = [vp, sz, u32]
     L.zbhip_serializer_decode_state_entry.argtypes = [vp, u32, C.c_char_p, sz, C.c_char_p, sz, INTERNER, vp,
