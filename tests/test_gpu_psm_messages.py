@@ -59,7 +59,10 @@ def phase(ref, gpu, writes):
     for p, recs in writes:
         Client(ref.logs[p], gpu.logs[p]).write(*recs)
     run_cluster(ref.sps)
-    run_cluster(gpu.sps)
+    try:
+        run_cluster(gpu.sps)
+    except Exception as e:
+        raise AssertionError("device fallbacks %s" % {p: a.fallback_reasons for p, a in gpu.adapters.items()}) from e
     for p in range(1, P + 1):
         want, got = ref.logs[p].canonical(), gpu.logs[p].canonical()
         if got != want:
@@ -70,12 +73,18 @@ def phase(ref, gpu, writes):
         assert gpu.state(p) == sorted(ref.state(p)), p
 
 
+# three subscribers per key (the device keeps 4 MESSAGE_SUBSCRIPTION rows per correlation key,
+# zb_internal.h kSubs): the test's keys plus seven more spread over the partitions
+KEYS = [CORRELATION_KEYS[1], CORRELATION_KEYS[2], CORRELATION_KEYS[3]] + ["order-%d" % j for j in range(7)]
+
+
 def create_phase():
-    """30 instances, 10 per correlation key, every partition creating instances of every key (local
-    and remote subscriptions): instance i on partition 1 + i % 3, key of partition 1 + (i + i // 3) % 3."""
+    """30 instances, 3 per correlation key, every partition creating instances of keys of every
+    partition (local and remote subscriptions): instance i on partition 1 + (i + i // 10) % 3 with key
+    KEYS[i % 10]."""
     creates = {p: [] for p in range(1, P + 1)}
     for i in range(30):
-        creates[1 + i % 3].append(Client.create("process", (("key", CORRELATION_KEYS[1 + (i + i // 3) % 3]),)))
+        creates[1 + (i + i // 10) % 3].append(Client.create("process", (("key", KEYS[i % 10]),)))
     return sorted(creates.items())
 
 
@@ -88,15 +97,19 @@ def test_message_correlation_on_three_partitions_in_the_processing_loop():
         created = [(p, r.value["correlationKey"]) for p in range(1, P + 1) for r in cl.logs[p].entries
                    if r.value_type == abi.VT_MESSAGE_SUBSCRIPTION and r.record_type == abi.RT_EVENT
                    and r.intent == abi.MS_CREATED]
-        assert len(created) == 30 and set(created) == set(CORRELATION_KEYS.items())
-    # a message nobody waits for (published and expired), then one message per subscription
-    pubs = [(p, [Client.publish_message("message", "nobody")] +
-             [Client.publish_message("message", CORRELATION_KEYS[p]) for _ in range(10)]) for p in range(1, P + 1)]
-    phase(ref, gpu, pubs)
+        assert len(created) == 30
+        assert {(p, k) for p, k in created if k.startswith("item")} == set(CORRELATION_KEYS.items())
+    # a message nobody waits for (published and expired), then one message per subscription, each on
+    # its key's subscription partition (SubscriptionUtil.getSubscriptionPartitionId)
+    from oracle.oracle import subscription_partition
+    pubs = {p: [Client.publish_message("message", "nobody")] for p in range(1, P + 1)}
+    for k in KEYS:
+        pubs[subscription_partition(k, P)] += [Client.publish_message("message", k) for _ in range(3)]
+    phase(ref, gpu, sorted(pubs.items()))
     done = sum(1 for p in range(1, P + 1) for r in gpu.logs[p].entries
                if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == 5
                and r.value["bpmnElementType"] == "PROCESS")
     assert done == 30
     c = [gpu.adapters[p].counts for p in range(1, P + 1)]
-    assert all(x["fallbacks"] == 0 for x in c)
+    assert all(x["fallbacks"] == 0 for x in c), [gpu.adapters[p].fallback_reasons for p in range(1, P + 1)]
     assert sum(x["device_commands"] for x in c) >= 30 + 3 * 11 + 2 * 30  # creates, publishes, received commands

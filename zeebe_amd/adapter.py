@@ -317,6 +317,7 @@ class GpuBatchProcessor:
         self.doc_total = 0             # document entries submitted so far (zbhip doc indices)
         self.values = None
         # what went where (tests read these)
+        self.fallback_reasons = []
         self.counts = {"windows": 0, "device_commands": 0, "continuations": 0, "fallbacks": 0, "activations": 0,
                        "engine_commands": 0, "followups_answered": 0}
 
@@ -415,9 +416,10 @@ class GpuBatchProcessor:
         if i < 0:
             self.engine_batch = True
             return self.engine.process(record, out)
-        st, _ = self.part.command_status(i)
+        st, why = self.part.command_status(i)
         if st != 0:
             self.counts["fallbacks"] += 1
+            self.fallback_reasons.append(why)
             return self._fall_back(i, record, out)
         self.counts["device_commands"] += 1
         self.counts["continuations"] += self.window.cmds[i]["kind"] == abi.CMD_CONTINUE
