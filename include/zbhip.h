@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 7  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+#define ZBHIP_ABI_VERSION 8  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
                                4: timer boundary events (start_event / flow_source / job_retries of job
                                   workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
                                   PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions;
@@ -50,7 +50,9 @@ extern "C" {
                                   records with inline values (ZBHIP_AUX_INLINE), six variables per
                                   activated job;
                                7: INCIDENT:CREATED records of exclusive gateways (ZBHIP_VT_INCIDENT,
-                                  zbhip_incident_message), zbhip_process_csr.cond_text */
+                                  zbhip_incident_message), zbhip_process_csr.cond_text;
+                               8: zbhip_outbox_command, zbhip_drain_command on message partitions,
+                                  zeebe:ioMapping (zbhip_process_csr.mappings) */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -231,6 +233,22 @@ typedef struct zbhip_insn {
   int64_t literal;
 } zbhip_insn;
 
+/* A zeebe:ioMapping entry of a job worker task or an embedded sub-process in the device subset
+ * (VariableMappingTransformer, deployment/model/transformer/VariableMappingTransformer.java:73-200;
+ * applied by BpmnVariableMappingBehavior.java:53-156): at most one input and one output mapping per
+ * element (several entries make a multi-entry document, iterated in agrona order: unpinned), a plain
+ * target name, a source that is a variable reference (`= x`) or a literal (`= 5`, `= true`, `= null`,
+ * `= "s"`, or a static string without '=').  Not on multi-instance inner activities. */
+#define ZBHIP_MAP_VARIABLE 0xFF
+typedef struct zbhip_mapping {
+  uint16_t element;      /* the element the mapping belongs to */
+  uint8_t output;        /* 0: input mapping (on activation), 1: output mapping (on completion) */
+  uint8_t source_type;   /* ZBHIP_MAP_VARIABLE, or the zbhip_doc_type of a literal (NIL, BOOL, INT, STR) */
+  uint16_t source;       /* a variable reference's name / a string literal's text: string index */
+  uint16_t target;       /* the target variable's name: string index */
+  int64_t literal;       /* BOOL / INT literal */
+} zbhip_mapping;
+
 typedef struct zbhip_process_csr {
   uint32_t n_elements;           /* elements[0] is the process */
   const zbhip_element* elements;
@@ -250,6 +268,8 @@ typedef struct zbhip_process_csr {
   uint16_t pad;
   const char* const* cond_text;  /* condition c's FEEL text after '=' (ParsedExpression.text: the incident
                                     message); "" for a multi-instance collection */
+  uint32_t n_mappings;           /* zeebe:ioMapping entries (ABI 8) */
+  const zbhip_mapping* mappings;
 } zbhip_process_csr;
 
 /* Host-side compiler: BPMN XML -> CSR (engine/.../deployment/model/transformation/BpmnTransformer.java:109-127).

@@ -350,6 +350,19 @@ struct OEl {
   std::vector<std::string> mi_item_text;
   std::string mi_input;
   int mi_input_id = -1, mi_loop_id = -1;
+  // zeebe:ioMapping (VariableMappingTransformer, deployment/model/transformer/VariableMappingTransformer.java:
+  // 73-200) in the subset: at most one input and one output mapping, a plain target name, a source that
+  // is a variable reference (`= x`), a literal (`= 5`, `= true`, `= null`, `= "s"`) or a static string
+  struct Mapping {
+    bool present = false;
+    bool var = false;         // the source is a variable reference
+    std::string source;       // the variable name, or the string literal's text
+    uint8_t type = 0;         // zbhip_doc_type of a literal
+    int64_t value = 0;
+    std::string target;
+    int source_id = -1, target_id = -1;  // name ids (deploy); a string literal: its value-dictionary id
+  };
+  Mapping in_map, out_map;
 };
 
 struct OProc {
@@ -476,6 +489,60 @@ static bool parse_multi_instance(const XNode& mil, OEl& body, std::string& err) 
   return true;
 }
 
+// zeebe:ioMapping of a job worker task or an embedded sub-process (the subset above); false + err
+// outside it.  A source without a leading '=' is a static string (StaticExpression:
+// VariableMappingTransformer.java:176-180 quotes it).  Several mappings of one kind produce a
+// multi-entry document, iterated in agrona Int2IntHashMap order (IndexedDocument.java:44-63):
+// parity unpinned, so they are outside the subset.
+static bool parse_mappings(const XNode* ext, OEl& e, std::string& err) {
+  const XNode* io = ext ? ext->child("ioMapping") : nullptr;
+  if (!io) return true;
+  auto trim = [](const std::string& t) {
+    const size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+    return a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+  };
+  auto ident = [](const std::string& v) {
+    bool ok = !v.empty() && (isalpha((unsigned char)v[0]) || v[0] == '_');
+    for (char ch : v) ok = ok && (isalnum((unsigned char)ch) || ch == '_');
+    return ok && v != "true" && v != "false" && v != "null";
+  };
+  for (auto& m : io->kids) {
+    if (m->name != "input" && m->name != "output") continue;
+    OEl::Mapping& M = m->name == "input" ? e.in_map : e.out_map;
+    if (M.present) { err = "more than one " + m->name + " mapping (document order unpinned)"; return false; }
+    M.present = true;
+    M.target = trim(m->attr("target"));
+    if (!ident(M.target)) { err = "io mapping target outside the subset: " + M.target; return false; }
+    const std::string src = m->attr("source");
+    if (src.empty() || src[0] != '=') {  // a static string
+      M.type = ZBHIP_DOC_STR;
+      M.source = src;
+      continue;
+    }
+    const std::string x = trim(src.substr(1));
+    if (ident(x)) { M.var = true; M.source = x; continue; }
+    if (x == "true" || x == "false") { M.type = ZBHIP_DOC_BOOL; M.value = x == "true"; continue; }
+    if (x == "null") { M.type = ZBHIP_DOC_NIL; continue; }
+    if (x.size() >= 2 && x.front() == '"' && x.back() == '"' && x.find('"', 1) == x.size() - 1 &&
+        x.find('\\') == std::string::npos) {
+      M.type = ZBHIP_DOC_STR;
+      M.source = x.substr(1, x.size() - 2);
+      continue;
+    }
+    size_t i = x[0] == '-' ? 1 : 0;
+    unsigned long long v = 0;
+    bool ok = i < x.size();
+    for (; ok && i < x.size(); ++i) {
+      ok = isdigit((unsigned char)x[i]) && v <= 922337203685477580ULL;
+      if (ok) v = v * 10 + (unsigned)(x[i] - '0');
+    }
+    if (!ok || v > 9223372036854775807ULL) { err = "io mapping source outside the subset: " + src; return false; }
+    M.type = ZBHIP_DOC_INT;
+    M.value = x[0] == '-' ? -(int64_t)v : (int64_t)v;
+  }
+  return true;
+}
+
 static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, std::string& err) {
   P.bpmn_id = proc.attr("id");
   P.els.clear();
@@ -533,10 +600,11 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
         return false;
       }
       e.retries = atoi(r.c_str());
-      if (ext && (ext->child("ioMapping") || ext->child("taskHeaders"))) {
-        err = "io mappings / task headers outside the supported subset";
+      if (ext && ext->child("taskHeaders")) {
+        err = "task headers outside the supported subset";
         return false;
       }
+      if (!parse_mappings(ext, e, err)) return false;
     } else if (n == "intermediateCatchEvent" && k->child("timerEventDefinition")) {
       // CatchEventTransformer.transformTimerEventDefinition: timeDuration (a static ISO-8601
       // duration, Interval.parse) only; timeDate / timeCycle / expressions outside the subset
@@ -632,8 +700,7 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
         err = "multi-instance outside the supported subset";
         return false;
       }
-      const XNode* ext = k->child("extensionElements");
-      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+      if (!parse_mappings(k->child("extensionElements"), e, err)) return false;
     } else if (n == "exclusiveGateway") {
       e.type = ZBHIP_EL_EXCLUSIVE_GATEWAY;
       xgws.push_back(k.get());
@@ -656,6 +723,11 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       // scope and sequence flows; the inner activity's flow scope is the body
       if (!ZBHIP_IS_JOB_WORKER(e.type) && e.type != ZBHIP_EL_TASK && e.type != ZBHIP_EL_MANUAL_TASK) {
         err = "multi-instance " + n + " outside the supported subset (job worker and undefined tasks)";
+        return false;
+      }
+      if (e.in_map.present || e.out_map.present) {
+        // an inner multi-instance activity maps in its own scope (getVariableScopeKey): outside the subset
+        err = "io mappings of a multi-instance activity outside the supported subset";
         return false;
       }
       OEl b;
@@ -981,6 +1053,15 @@ class Oracle {
       for (size_t j = 0; j < e.mi_items.size(); ++j)
         if (e.mi_items[j].first == ZBHIP_DOC_STR) e.mi_items[j].second = intern_string(e.mi_item_text[j]);
     }
+    // io mappings, in element order: the input's source variable and target, then the output's (the
+    // product's zbhip_deploy interns in this order); string literals into the value dictionary
+    for (auto& e : P.els)
+      for (OEl::Mapping* M : {&e.in_map, &e.out_map}) {
+        if (!M->present) continue;
+        if (M->var) M->source_id = intern(M->source);
+        else if (M->type == ZBHIP_DOC_STR) M->value = intern_string(M->source);
+        M->target_id = intern(M->target);
+      }
     procs.push_back(std::move(P));
     return (int)procs.size() - 1;
   }
@@ -2141,6 +2222,58 @@ class Oracle {
     vars_[{scopeKey, name}] = VarRow{key, type, value, UINT32_MAX};
   }
 
+  // ExpressionProcessor.evaluateVariableMappingExpression of a one-entry mapping context in `scope`
+  // (DbVariableState.getVariable walks the scope chain).  FeelToMessagePackTransformer writes a whole
+  // number as an integer (FeelToMessagePackTransformer.scala:35-39): a whole decimal becomes an INT.  A
+  // missing source variable is outside the subset (feel-scala 1.17's null for it is unpinned here).
+  void eval_mapping(const OEl::Mapping& M, int64_t scope, uint8_t& type, int64_t& value) {
+    if (!M.var) {
+      type = M.type;
+      value = M.value;
+      return;
+    }
+    const VarRow* vr = lookup_var(scope, M.source_id);
+    if (!vr) throw Unsupported{"io mapping source variable missing"};
+    if (vr->type != ZBHIP_DOC_NIL && vr->type != ZBHIP_DOC_BOOL && vr->type != ZBHIP_DOC_INT &&
+        vr->type != ZBHIP_DOC_DEC && vr->type != ZBHIP_DOC_STR)
+      throw Unsupported{"io mapping source outside the value subset"};
+    type = vr->type;
+    value = vr->value;
+    if (type == ZBHIP_DOC_DEC && value % 1000000 == 0) {
+      type = ZBHIP_DOC_INT;
+      value /= 1000000;
+    }
+  }
+
+  // BpmnVariableMappingBehavior.applyInputMappings (behavior/BpmnVariableMappingBehavior.java:53-77):
+  // the mapping evaluated in the element's scope, mergeLocalDocument into it
+  void apply_input_mappings(const OEl& el, int64_t key, const PiValue& v) {
+    if (!el.in_map.present) return;
+    uint8_t type;
+    int64_t value;
+    eval_mapping(el.in_map, key, type, value);
+    set_local_inline(key, v.proc, v.piKey, el.in_map.target_id, type, value);
+  }
+
+  // VariableBehavior.mergeDocument (VariableBehavior.java:105-150) of a one-entry document computed by
+  // the engine: updated in the first scope of the chain that holds it with another value, else set
+  // locally in the root scope
+  void merge_document_value(int64_t scopeKey, int proc, int64_t piKey, int name, uint8_t type, int64_t value) {
+    int64_t current = scopeKey;
+    for (;;) {
+      auto pit = child_parent_.find(current);
+      const int64_t parent = pit == child_parent_.end() ? -1 : pit->second;
+      if (parent <= 0) break;
+      auto vit = vars_.find({current, name});
+      if (vit != vars_.end() && !(vit->second.type == type && vit->second.value == value)) {
+        set_local_inline(current, proc, piKey, name, type, value);
+        return;
+      }
+      current = parent;
+    }
+    set_local_inline(current, proc, piKey, name, type, value);
+  }
+
   // ---------------------------------------------------------------------
   // BpmnStreamProcessor.processRecord (processing/bpmn/BpmnStreamProcessor.java:74-162)
   // ---------------------------------------------------------------------
@@ -2277,7 +2410,8 @@ class Oracle {
         break;
       }
       case ZBHIP_EL_SUB_PROCESS: {  // SubProcessProcessor.onActivate (processing/bpmn/container/SubProcessProcessor.java:49-66)
-        // applyInputMappings (none in the subset), transitionToActivated, activateChildInstance(none start)
+        // applyInputMappings, transitionToActivated, activateChildInstance(none start)
+        apply_input_mappings(el, key, v);
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         PiValue c = v;
         c.flowScopeKey = key;
@@ -2329,7 +2463,9 @@ class Oracle {
       case ZBHIP_EL_SEND_TASK:
       case ZBHIP_EL_SCRIPT_TASK:
       case ZBHIP_EL_BUSINESS_RULE_TASK: {
-        // eventSubscriptionBehavior.subscribeToEvents: the attached boundary event's timer first
+        // applyInputMappings, then eventSubscriptionBehavior.subscribeToEvents: the attached boundary
+        // event's timer, then the job
+        apply_input_mappings(el, key, v);
         if (el.boundary >= 0) {
           PiValue bv = v;
           bv.elem = el.boundary;
@@ -2488,7 +2624,17 @@ class Oracle {
       const EventTrigger* trig = nullptr;  // peekEventTrigger(elementInstanceKey)
       auto it = triggers_.lower_bound({key, INT64_MIN});
       if (it != triggers_.end() && it->first.first == key) trig = &it->second;
-      if (trig && trig->vars.count > 0) merge_document(key, v.proc, v.piKey, trig->vars);
+      if (el.out_map.present) {
+        // the event's variables become local, then the mapping is evaluated in the element's scope
+        // and merged into its flow scope (getVariableScopeKey; no multi-instance inner activities)
+        if (trig && trig->vars.count > 0) merge_local_document(key, v.proc, v.piKey, trig->vars);
+        uint8_t type;
+        int64_t value;
+        eval_mapping(el.out_map, key, type, value);
+        merge_document_value(v.flowScopeKey, v.proc, v.piKey, el.out_map.target_id, type, value);
+      } else if (trig && trig->vars.count > 0) {
+        merge_document(key, v.proc, v.piKey, trig->vars);
+      }
       // START_EVENT without trigger: local variables of the start event are empty.
     }
     if (unsubscribe) unsubscribe_timers(key);

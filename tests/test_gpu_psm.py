@@ -230,3 +230,23 @@ def test_multi_instance_in_the_processing_loop(limit):
     assert c["fallbacks"] == 0 and c["device_commands"] > 40
     assert (c["continuations"] > 0) == (limit == 3)
     assert not open_jobs(ref.log)
+
+
+def test_io_mappings_in_the_processing_loop():
+    # zeebe:ioMapping behind the adapter (KScopeIO): the mapped VARIABLE records' values inline in the
+    # log, task- and sub-process-scope variables in the state, job activations with the local variables
+    from test_gpu_io_mapping import _sub, _task_in_out
+    a = _task_in_out()
+    b = _sub([("input", "=x", "y"), ("output", "=y", "z")], "task").replace('id="process"', 'id="subproc"', 1)
+    deps = [(a, KEY_A, 1), (b, KEY_B, 1)]
+    ref, mixed = Ref(deps, 100), Mixed(deps, deps, 100)
+    phase(ref, mixed, [Client.create("process", (("x", k),)) for k in range(10)] +
+          [Client.create("subproc", (("x", 2.5 if k % 2 else k),)) for k in range(10)])
+    rng = np.random.default_rng(21)
+    for p in range(4):
+        recs = completions(ref, rng, lambda k: (("local", int(k) % 3),) if k % 2 else ())
+        if not recs:
+            break
+        phase(ref, mixed, recs + [Client.activate_jobs("t", max_jobs=3)])
+    c = mixed.adapter.counts
+    assert c["fallbacks"] == 0 and c["device_commands"] >= 30, c

@@ -30,6 +30,7 @@ class _Node:
         self.attached_to = None     # boundary event: the activity it is attached to
         self.cancel_activity = True  # boundary event: interrupting (BoundaryEvent default)
         self.multi = None    # activity: (isSequential, inputCollection, inputElement, extra attrs)
+        self.mappings = []   # zeebe:ioMapping entries: ("input" | "output", source, target)
 
 
 class ProcessBuilder:
@@ -165,6 +166,25 @@ class ProcessBuilder:
         self.current.multi = (bool(sequential), expr, input_element, extra)
         return self
 
+    # ZeebeVariablesMappingBuilder (bpmn-model/.../builder/ZeebeVariablesMappingBuilder.java): the
+    # *Expression forms prefix the source with "=" (asZeebeExpression); the plain forms keep a static
+    # source.  They apply to the current node (after subProcessDone(): the sub-process).
+    def _mapping(self, kind, source, target):
+        self.current.mappings.append((kind, source, target))
+        return self
+
+    def zeebeInputExpression(self, source, target):
+        return self._mapping("input", source if source.startswith("=") else "=" + source, target)
+
+    def zeebeOutputExpression(self, source, target):
+        return self._mapping("output", source if source.startswith("=") else "=" + source, target)
+
+    def zeebeInput(self, source, target):
+        return self._mapping("input", source, target)
+
+    def zeebeOutput(self, source, target):
+        return self._mapping("output", source, target)
+
     def cancelActivity(self, cancel):
         self.current.cancel_activity = bool(cancel)
         return self
@@ -256,9 +276,9 @@ class ProcessBuilder:
                                    % (ind, attrs, escape(c.condition)))
                 elif c.kind in ("serviceTask", "sendTask", "scriptTask", "businessRuleTask"):
                     retries = ' retries="%s"' % c.retries if c.retries is not None else ""
-                    out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>'
+                    out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>%s'
                                '</extensionElements>%s</%s>' % (ind, c.kind, quoteattr(c.id), quoteattr(c.job_type),
-                                                               retries, loop(c), c.kind))
+                                                               retries, io(c), loop(c), c.kind))
                 elif c.kind == "intermediateCatchEvent" and c.message:
                     catches.append(c)
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
@@ -282,13 +302,20 @@ class ProcessBuilder:
                 elif c.kind == "exclusiveGateway" and c.default:
                     out.append("%s<exclusiveGateway id=%s default=%s/>" % (ind, quoteattr(c.id), quoteattr(c.default.id)))
                 elif c.kind == "subProcess":
-                    out.append("%s<subProcess id=%s>" % (ind, quoteattr(c.id)))
+                    ext = "<extensionElements>%s</extensionElements>" % io(c) if c.mappings else ""
+                    out.append("%s<subProcess id=%s>%s" % (ind, quoteattr(c.id), ext))
                     render(c.children, ind + "  ")
                     out.append("%s</subProcess>" % ind)
                 elif c.multi:
                     out.append("%s<%s id=%s>%s</%s>" % (ind, c.kind, quoteattr(c.id), loop(c), c.kind))
                 else:
                     out.append("%s<%s id=%s/>" % (ind, c.kind, quoteattr(c.id)))
+
+        def io(c):
+            if not c.mappings:
+                return ""
+            return "<zeebe:ioMapping>%s</zeebe:ioMapping>" % "".join(
+                "<zeebe:%s source=%s target=%s/>" % (k, quoteattr(src), quoteattr(t)) for k, src, t in c.mappings)
 
         def loop(c):
             if not c.multi:

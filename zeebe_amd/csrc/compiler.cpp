@@ -317,6 +317,7 @@ struct Compiled {
   std::vector<std::string> cond_texts;
   std::vector<const char*> cond_ptrs;
   std::vector<zbhip_insn> code;
+  std::vector<zbhip_mapping> mappings;
   std::vector<std::string> strings;
   std::vector<const char*> string_ptrs;
   std::unordered_map<std::string, uint16_t> string_ids;
@@ -340,6 +341,8 @@ struct Compiled {
     csr.cond_begin = cond_begin.data();
     cond_ptrs.clear();
     for (auto& t : cond_texts) cond_ptrs.push_back(t.c_str());
+    csr.n_mappings = (uint32_t)mappings.size();
+    csr.mappings = mappings.data();
     csr.cond_text = cond_ptrs.data();
     csr.n_code = (uint32_t)code.size();
     csr.code = code.data();
@@ -474,6 +477,71 @@ static bool parse_loop(const Elem& mil, bool& seq, std::string& input, std::vect
   return true;
 }
 
+// zeebe:ioMapping (VariableMappingTransformer.java:73-200) in the device subset (zbhip.h
+// zbhip_mapping): one input and one output mapping at most, a plain target, a variable reference or a
+// literal source (a source without '=' is a static string: StaticExpression, quoted at :176-180).
+static int parse_mappings(const Elem* ext, uint16_t elem, Compiled& C, std::string& err) {
+  const Elem* io = ext ? ext->first("ioMapping") : nullptr;
+  if (!io) return ZBHIP_OK;
+  auto trim = [](const std::string& t) {
+    const size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+    return a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+  };
+  auto ident = [](const std::string& v) {
+    bool ok = !v.empty() && (isalpha((unsigned char)v[0]) || v[0] == '_');
+    for (char ch : v) ok = ok && (isalnum((unsigned char)ch) || ch == '_');
+    return ok && v != "true" && v != "false" && v != "null";
+  };
+  bool seen[2] = {false, false};
+  for (auto& m : io->children) {
+    if (m.tag != "input" && m.tag != "output") continue;
+    const int out = m.tag == "output";
+    if (seen[out]) { err = "more than one " + m.tag + " mapping outside the supported subset (document order unpinned)"; return ZBHIP_EUNSUPP; }
+    seen[out] = true;
+    const std::string* tp = m.get("target");
+    const std::string* sp = m.get("source");
+    const std::string target = tp ? trim(*tp) : "";
+    const std::string src = sp ? *sp : "";
+    if (!ident(target)) { err = "io mapping target outside the supported subset: " + target; return ZBHIP_EUNSUPP; }
+    zbhip_mapping M{};
+    M.element = elem;
+    M.output = (uint8_t)out;
+    M.target = C.str(target);
+    if (src.empty() || src[0] != '=') {
+      M.source_type = ZBHIP_DOC_STR;
+      M.source = C.str(src);
+    } else {
+      const std::string x = trim(src.substr(1));
+      if (ident(x)) {
+        M.source_type = ZBHIP_MAP_VARIABLE;
+        M.source = C.str(x);
+      } else if (x == "true" || x == "false") {
+        M.source_type = ZBHIP_DOC_BOOL;
+        M.literal = x == "true";
+      } else if (x == "null") {
+        M.source_type = ZBHIP_DOC_NIL;
+      } else if (x.size() >= 2 && x.front() == '"' && x.back() == '"' && x.find('"', 1) == x.size() - 1 &&
+                 x.find('\\') == std::string::npos) {
+        M.source_type = ZBHIP_DOC_STR;
+        M.source = C.str(x.substr(1, x.size() - 2));
+      } else {
+        size_t i = x.size() && x[0] == '-' ? 1 : 0;
+        unsigned long long v = 0;
+        bool ok = i < x.size();
+        for (; ok && i < x.size(); ++i) {
+          ok = isdigit((unsigned char)x[i]) && v <= 922337203685477580ULL;
+          if (ok) v = v * 10 + (unsigned)(x[i] - '0');
+        }
+        if (!ok || v > 9223372036854775807ULL) { err = "io mapping source outside the supported subset: " + src; return ZBHIP_EUNSUPP; }
+        M.source_type = ZBHIP_DOC_INT;
+        M.literal = x[0] == '-' ? -(int64_t)v : (int64_t)v;
+      }
+    }
+    C.mappings.push_back(M);
+  }
+  return ZBHIP_OK;
+}
+
 static zbhip_element blank(uint8_t type, uint16_t id) {
   zbhip_element e{};
   e.element_type = type;
@@ -601,8 +669,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           err = "multi-instance sub-process outside the supported subset";
           return ZBHIP_EUNSUPP;
         }
-        if (const Elem* ext = c.first("extensionElements"))
-          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        if (int rc = parse_mappings(c.first("extensionElements"), (uint16_t)C.elements.size(), C, err)) return rc;
       }
       if (type == ZBHIP_EL_BOUNDARY_EVENT) {
         // BoundaryEventTransformer: timer boundary events (a static timeDuration; interrupting or not)
@@ -698,10 +765,11 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           err = "job type/retries expressions outside the supported subset";
           return ZBHIP_EUNSUPP;
         }
-        if (ext->first("ioMapping") || ext->first("taskHeaders")) {
-          err = "io mappings / task headers outside the supported subset";
+        if (ext->first("taskHeaders")) {
+          err = "task headers outside the supported subset";
           return ZBHIP_EUNSUPP;
         }
+        if (int rc = parse_mappings(ext, (uint16_t)C.elements.size(), C, err)) return rc;
         e.job_type = C.str(*jt);
         e.job_retries = (uint16_t)atoi(retries.c_str());
       }
@@ -715,6 +783,10 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         // scope the body
         if (!ZBHIP_IS_JOB_WORKER(type) && type != ZBHIP_EL_TASK && type != ZBHIP_EL_MANUAL_TASK) {
           err = "multi-instance <" + c.tag + "> outside the supported subset (job worker and undefined tasks)";
+          return ZBHIP_EUNSUPP;
+        }
+        if (!C.mappings.empty() && C.mappings.back().element == C.elements.size()) {
+          err = "io mappings of a multi-instance activity outside the supported subset";
           return ZBHIP_EUNSUPP;
         }
         bool seq = false;

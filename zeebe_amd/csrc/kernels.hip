@@ -51,7 +51,7 @@ namespace zb {
 // its column, then writes it at its prefix) spilled and was ~2 % slower, and an owner map of stage
 // indices (one dependent LDS level fewer) ~4 % slower.)
 template <int B_, int T_, int Q_, int R_, bool M_ = false, bool J_ = true, bool X_ = true, int W_ = 0,
-          bool REG_ = false, bool S_ = false>
+          bool REG_ = false, bool S_ = false, bool IO_ = false>
 struct KCfg {
   static constexpr int B = B_, T = T_, Q = Q_, R = R_;
   static constexpr int W = W_;   // waves per SIMD the register allocation targets (0 = compiler default)
@@ -60,6 +60,7 @@ struct KCfg {
   static constexpr bool J = J_;  // parallel-gateway join counters
   static constexpr bool X = X_;  // exclusive gateways (FEEL condition evaluation)
   static constexpr bool S = S_;  // flow scopes below the process (embedded sub-processes)
+  static constexpr bool IO = IO_;  // io mappings: variables in the scopes of element instances (K::S only)
 };
 // One token per instance (exclusive gateways, no parallel gateways / multi-outgoing nodes: no join
 // counters).  Only R = 4 stage rows: rows j >= R go straight to the output region (one coalesced
@@ -108,6 +109,10 @@ using KMsg = KCfg<128, 12, 16, ZB_KMSG_R, true, true, true, ZB_KMSG_W>;  // mess
 #define ZB_KSCOPE_W ZB_KGENERIC_W
 #endif
 using KScope = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, ZB_KSCOPE_W, false, true>;
+// KScope plus zeebe:ioMapping (element-instance variable scopes, their lookups through the scope chain
+// and removal with the instance): a variant of its own so processes without mappings keep KScope's
+// register allocation
+using KScopeIO = KCfg<ZB_KGENERIC_B, 12, 16, ZB_KGENERIC_R, false, true, true, ZB_KSCOPE_W, false, true, true>;
 
 template <class K>
 struct Lane {
@@ -134,6 +139,7 @@ struct Lane {
   uint16_t trig_key;    // event trigger of a completed job (EVENT_TRIGGER row), NONE if none
   uint16_t trig_evt;    // K::S: the PROCESS_EVENT key ordinal of a boundary event's trigger on trig_key
   uint32_t inc;         // the incident info of a failed exclusive gateway (find_sequence_flow)
+  uint32_t n_map;       // K::S: io-mapped VARIABLE records of the batch so far (values in StepParams.map_val)
   bool pi_live;
   uint8_t pi_state;
   int pi_child;
@@ -552,26 +558,177 @@ __device__ __forceinline__ void set_local_variable(Lane<K>& L, uint32_t scope, c
   }
 }
 
-// VariableBehavior.mergeDocument (VariableBehavior.java:105-150) from an element scope whose
-// parent is the process instance (the only nesting in the supported subset).
+// The key ordinal of the instance of the i-th scope above an element in container c (K::S: the
+// instances of the enclosing sub-processes / multi-instance bodies; one per container element),
+// NONE past the process's children.  Scope chains are at most kMaxDepth deep on the device.
+constexpr int kMaxDepth = 8;
 template <class K>
-__device__ __forceinline__ void merge_document_from(Lane<K>& L, uint32_t scope_key, uint32_t begin, uint32_t count) {
+__device__ __forceinline__ uint32_t container_key(const Lane<K>& L, uint32_t& c) {
+  if constexpr (K::S) {
+    if (c == 0) return NONE;
+    const int t = scope_find(L, c);
+    c = scope_of<K>(elem_of(L, c));
+    return t < 0 ? NONE : tget(L, t).x >> 16;
+  } else {
+    return NONE;
+  }
+}
+
+// DbVariableState.getVariable (state/variable/DbVariableState.java:174-200): the scope `key`, then
+// the instances of the containers from c up, then the process instance
+template <class K>
+__device__ __forceinline__ int var_lookup(const Lane<K>& L, uint32_t key, uint32_t c, uint32_t name) {
+  int v = var_find(L, key, name);
+  if constexpr (!K::IO) return v >= 0 ? v : var_find(L, 0, name);
+  for (int d = 0; v < 0 && d < kMaxDepth; ++d) {
+    const uint32_t k = container_key(L, c);
+    if (k == NONE) break;
+    v = var_find(L, k, name);
+  }
+  return v >= 0 ? v : var_find(L, 0, name);
+}
+
+// VariableBehavior.mergeDocument (VariableBehavior.java:105-150) of the command's document from
+// the scope `scope_key` of an element in container c: updated in the first scope below the process
+// that holds the variable with another value, else set locally in the process instance's scope.
+template <class K>
+__device__ __forceinline__ void merge_document_from(Lane<K>& L, uint32_t scope_key, uint32_t c, uint32_t begin,
+                                                    uint32_t count) {
   if (count == 0) return;
   if (count > 1) { set_fail(L, FB_DOC); return; }
   const zbhip_doc_entry d = L.docs[begin];
   vm_drain();
-  if (scope_key != 0) {
-    int v = var_find(L, scope_key, d.name_id);
+  if constexpr (!K::IO) {  // (no variables in scopes between the element and the process)
+    if (scope_key != 0) {
+      int v = var_find(L, scope_key, d.name_id);
+      if (v >= 0) {
+        const uint32_t y = var_y(L, v);
+        if (!(((y >> 16) & 0xFF) == d.type && var_v(L, v) == d.value)) {
+          emit(L, C_VAR_UPDATED, y & 0xFFFF, scope_key, d.name_id);
+          var_put(L, v, var_x(L, v), (y & 0xFFFF) | ((uint32_t)d.type << 16), d.value);
+          return;
+        }
+      }
+    }
+    set_local_variable(L, 0, d);
+    return;
+  }
+  uint32_t k = scope_key;
+  for (int depth = 0; k != 0 && k != NONE && depth <= kMaxDepth; ++depth) {
+    int v = var_find(L, k, d.name_id);
     if (v >= 0) {
       const uint32_t y = var_y(L, v);
       if (!(((y >> 16) & 0xFF) == d.type && var_v(L, v) == d.value)) {
-        emit(L, C_VAR_UPDATED, y & 0xFFFF, scope_key, d.name_id);
+        emit(L, C_VAR_UPDATED, y & 0xFFFF, k, d.name_id);
         var_put(L, v, var_x(L, v), (y & 0xFFFF) | ((uint32_t)d.type << 16), d.value);
         return;  // consumed at this scope
       }
     }
+    k = container_key(L, c);
   }
   set_local_variable(L, 0, d);
+}
+
+// ---- io mappings (K::S; BpmnVariableMappingBehavior.java:53-156) ---------------------------------
+// mapping k (0 input, 1 output) of element e (runtime.cpp rebuild_program): x = type | target name
+// << 16 (type 0xFE: none; ZBHIP_MAP_VARIABLE: y = the source's name id), z/w = the literal
+constexpr uint32_t kIoNone = 0xFE;
+template <class K>
+__device__ __forceinline__ uint4 io_map(const Lane<K>& L, uint32_t e, int k) {
+  if constexpr (!K::IO) return make_uint4(kIoNone, 0, 0, 0);
+  if (!((L.pb[5] >> 17) & 1u)) return make_uint4(kIoNone, 0, 0, 0);
+  return reinterpret_cast<const uint4*>(L.pb + (L.pb[6] >> 16))[2 * e + k];
+}
+
+// ExpressionProcessor.evaluateVariableMappingExpression of a one-entry context in the scope `key` of
+// an element in container c: a literal, or a copy of the variable (a missing one: outside the
+// subset); FeelToMessagePackTransformer.scala:35-39 writes a whole number as an integer
+template <class K>
+__device__ __forceinline__ bool map_value(Lane<K>& L, uint4 m, uint32_t key, uint32_t c, uint32_t& type, long long& v) {
+  type = m.x & 0xFF;
+  v = (long long)(((unsigned long long)m.w << 32) | m.z);
+  if (type != ZBHIP_MAP_VARIABLE) return true;
+  const int i = var_lookup(L, key, c, m.y);
+  if (i < 0) { set_fail(L, FB_FEEL); return false; }
+  type = (var_y(L, i) >> 16) & 0xFF;
+  v = var_v(L, i);
+  if (type == ZBHIP_DOC_DEC && v % 1000000 == 0) {
+    type = ZBHIP_DOC_INT;
+    v /= 1000000;
+  }
+  return type <= ZBHIP_DOC_DEC || type == ZBHIP_DOC_STR;
+}
+
+// VariableBehavior.setLocalVariable of a value the engine computed: VARIABLE:CREATED (+key) or
+// UPDATED, the value into the batch's map_val slot (C_VAR_MAPPED)
+template <class K>
+__device__ __forceinline__ void set_local_mapped(Lane<K>& L, uint32_t scope, uint32_t name, uint32_t type, long long v) {
+  const StepParams& P = *L.sp;
+  int i = var_find(L, scope, name);
+  if (i >= 0 && ((var_y(L, i) >> 16) & 0xFF) == type && var_v(L, i) == v) return;
+  if (L.n_map >= (uint32_t)kMapVals || L.ci >= P.map_cap) { set_fail(L, FB_VARS); return; }
+  const bool updated = i >= 0;
+  uint32_t key;
+  if (!updated) {
+    if (L.nvars >= kVars) { set_fail(L, FB_VARS); return; }
+    key = new_key(L);
+    i = L.nvars++;
+  } else {
+    key = var_y(L, i) & 0xFFFF;
+  }
+  P.map_val[(size_t)L.n_map * P.map_cap + L.ci] = v;
+  emit(L, C_VAR_MAPPED, key, scope, name, type | ((updated ? 1u : 0u) << 3) | (L.n_map << 4));
+  ++L.n_map;
+  var_put(L, i, name | (scope << 16), key | (type << 16), v);
+}
+
+// applyInputMappings (:53-77): evaluated in the new element instance's scope, merged locally into it
+template <class K>
+__device__ __forceinline__ void apply_input_mapping(Lane<K>& L, uint32_t elem, uint32_t key) {
+  const uint4 m = io_map(L, elem, 0);
+  if ((m.x & 0xFF) == kIoNone) return;
+  uint32_t type;
+  long long v;
+  if (!map_value(L, m, key, scope_of<K>(elem_of(L, elem)), type, v)) { set_fail(L, FB_FEEL); return; }
+  set_local_mapped(L, key, m.x >> 16, type, v);
+}
+
+// the output mapping of applyOutputMappings (:86-131) after the event's variables were merged locally:
+// evaluated in the element's scope, then VariableBehavior.mergeDocument from its flow scope
+// (getVariableScopeKey, :157-165: no multi-instance inner activities)
+template <class K>
+__device__ __forceinline__ void apply_output_mapping(Lane<K>& L, uint4 m, uint32_t elem, uint32_t key) {
+  uint32_t c = scope_of<K>(elem_of(L, elem));
+  uint32_t type;
+  long long v;
+  if (!map_value(L, m, key, c, type, v)) { set_fail(L, FB_FEEL); return; }
+  const uint32_t name = m.x >> 16;
+  for (int depth = 0; depth < kMaxDepth; ++depth) {
+    const uint32_t k = container_key(L, c);
+    if (k == NONE) break;
+    const int i = var_find(L, k, name);
+    if (i >= 0 && !(((var_y(L, i) >> 16) & 0xFF) == type && var_v(L, i) == v)) {
+      set_local_mapped(L, k, name, type, v);
+      return;
+    }
+  }
+  set_local_mapped(L, 0, name, type, v);
+}
+
+// variableState.removeScope (DbElementInstanceState.removeInstance): the element instance's own
+// variables leave with it (registers closed up)
+template <class K>
+__device__ __forceinline__ void vars_drop_scope(Lane<K>& L, uint32_t key) {
+  int n = 0;
+  for (int i = 0; i < kVars; ++i) {
+    if (i >= L.nvars) break;
+    const uint32_t x = var_x(L, i), y = var_y(L, i);
+    const long long v = var_v(L, i);
+    if ((x >> 16) == key) continue;
+    if (n != i) var_put(L, n, x, y, v);
+    ++n;
+  }
+  L.nvars = n;
 }
 
 // ---- join counters (registers, 16 x u8) ----------------------------------------------------
@@ -592,11 +749,10 @@ __device__ __forceinline__ void join_set(Lane<K>& L, uint32_t s, uint32_t v) {
 // that is not a boolean is an incident in the reference (ExpressionProcessor.java:356-368).
 // The operand stack is four registers, top first (the compiler bounds the depth to 4).
 template <class K>
-__device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32_t scope_key, uint32_t& t,
+__device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32_t scope_key, uint32_t c, uint32_t& t,
                                          long long& x) {
-  // DbVariableState.getVariable: element scope first, then the process instance scope
-  int v = var_find(L, scope_key, name);
-  if (v < 0) v = var_find(L, 0, name);
+  // DbVariableState.getVariable: element scope first, then the enclosing scopes up to the process
+  const int v = var_lookup(L, scope_key, c, name);
   t = 0;
   x = 0;
   if (v < 0) return true;  // missing -> null
@@ -617,7 +773,7 @@ __device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32
 
 // result: -1 outside the subset (fallback), else the tag of the value (1: boolean, in `out`)
 template <class K>
-__device__ __forceinline__ int eval_condition(Lane<K>& L, uint32_t cond, uint32_t scope_key, bool& out) {
+__device__ __forceinline__ int eval_condition(Lane<K>& L, uint32_t cond, uint32_t scope_key, uint32_t c, bool& out) {
   const uint32_t* pb = L.pb;
   uint32_t pc = pb[pb[3] + cond];
   const uint32_t* code = pb + pb[4];
@@ -633,7 +789,7 @@ __device__ __forceinline__ int eval_condition(Lane<K>& L, uint32_t cond, uint32_
       long long x = 0;
       if (op == ZBHIP_OP_PUSH_NUM) { t = 2; x = (long long)(((unsigned long long)in.w << 32) | in.z); }
       else if (op == ZBHIP_OP_PUSH_BOOL) { t = 1; x = in.y != 0; }
-      else if (op == ZBHIP_OP_PUSH_VAR) { if (!load_var(L, in.y, scope_key, t, x)) return -1; }
+      else if (op == ZBHIP_OP_PUSH_VAR) { if (!load_var(L, in.y, scope_key, c, t, x)) return -1; }
       if (sp >= 4) return -1;
       t3 = t2; a3 = a2; t2 = t1; a2 = a1; t1 = t0; a1 = a0; t0 = t; a0 = x;
       ++sp;
@@ -694,7 +850,7 @@ __device__ __forceinline__ uint32_t find_sequence_flow(Lane<K>& L, uint4 gw, uin
     uint32_t cond = elem_of(L, f).z >> 16;
     if (cond == NONE || f == dflt) continue;  // outgoingWithCondition, default skipped
     bool ok;
-    const int rt = eval_condition(L, cond, gw_key, ok);
+    const int rt = eval_condition(L, cond, gw_key, scope_of<K>(gw), ok);
     if (rt < 0 || (rt != 1 && i >= INC_NONE_CHOSEN)) { set_fail(L, FB_FEEL); return NONE; }
     if (rt != 1) {  // typeCheck: EXTRACT_VALUE_ERROR
       L.inc = i | ((rt == 0 ? ZBHIP_FEEL_NULL : rt == 2 ? ZBHIP_FEEL_NUMBER : ZBHIP_FEEL_STRING) << 4);
@@ -764,6 +920,8 @@ __device__ __forceinline__ void apply_completed_child(Lane<K>& L, int t, uint32_
   if constexpr (K::S) {
     const uint4 w = elem_of(L, tget(L, t).x & 0xFFFF);
     tput(L, t, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+    if constexpr (K::IO)
+      if (L.nvars) vars_drop_scope(L, key);
     if (etype(w) == ZBHIP_EL_SUB_PROCESS) {  // its taken-flow counters go with it (removeInstance)
       const uint32_t m = w.z >> 16;
       for (uint32_t s = 0; s < (uint32_t)kMaxJoinSlots; ++s)
@@ -1396,8 +1554,13 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       case ZBHIP_EL_SCRIPT_TASK:
       case ZBHIP_EL_BUSINESS_RULE_TASK: {
         if constexpr (K::S) {
-          // eventSubscriptionBehavior.subscribeToEvents: the attached boundary event's timer
-          // (CatchEventBehavior.subscribeToTimerEvent) before the job; one timer per instance
+          // applyInputMappings, then eventSubscriptionBehavior.subscribeToEvents: the attached
+          // boundary event's timer (CatchEventBehavior.subscribeToTimerEvent) before the job; one
+          // timer per instance
+          if constexpr (K::IO) {
+            apply_input_mapping(L, elem, key);
+            if (L.fail) return;
+          }
           const uint32_t b = w.w & 0xFFFF;
           if (b != 0xFFFF) {
             if (!L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
@@ -1483,6 +1646,10 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         return;
       case ZBHIP_EL_SUB_PROCESS:  // SubProcessProcessor.onActivate (container/SubProcessProcessor.java:49-66)
         if constexpr (K::S) {
+          if constexpr (K::IO) {
+            apply_input_mapping(L, elem, key);  // applyInputMappings, then ACTIVATED
+            if (L.fail) return;
+          }
           emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
           tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
           // activateChildInstance: the none start event, key -1, flow scope = this instance
@@ -1562,8 +1729,24 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     set_fail(L, FB_UNSUPPORTED);
     return;
   }
-  // applyOutputMappings (BpmnVariableMappingBehavior.java:86-156): event-trigger variables
-  if (L.trig_key == cmd_key) {
+  // applyOutputMappings (BpmnVariableMappingBehavior.java:86-156): with an output mapping the event
+  // trigger's variables become local (mergeLocalDocument), then the mapping goes to the flow scope;
+  // without one the trigger's variables are merged from the element's scope
+  bool mapped = false;
+  if constexpr (K::IO) {
+    const uint4 om = io_map(L, elem, 1);
+    if ((om.x & 0xFF) != kIoNone) {
+      if (L.trig_key == cmd_key && L.doc_count) {
+        if (L.doc_count > 1) { set_fail(L, FB_DOC); return; }
+        vm_drain();
+        set_local_variable(L, cmd_key, L.docs[L.doc_begin]);
+      }
+      apply_output_mapping(L, om, elem, cmd_key);
+      if (L.fail) return;
+      mapped = true;
+    }
+  }
+  if (!mapped && L.trig_key == cmd_key) {
     if constexpr (K::S) {
       // an inner instance's own loop variables would be updated in its scope (mergeDocument): they
       // are not in the variable table (derived from the slot), so such a document falls back
@@ -1574,7 +1757,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         if (name == (bw.x >> 16) || name == (bw.w & 0xFFFF)) { set_fail(L, FB_DOC); return; }
       }
     }
-    merge_document_from(L, cmd_key, L.doc_begin, L.doc_count);
+    merge_document_from(L, cmd_key, c, L.doc_begin, L.doc_count);
   }
   if constexpr (K::S) {
     // JobWorkerTaskProcessor.onComplete (:63-75): unsubscribeFromEvents -- the boundary event's timer
@@ -1614,7 +1797,7 @@ template <class K>
 __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t ref, uint32_t doc_count) {
   if (L.fail || L.proc == NONE || doc_count != 0 || L.limit <= 4 || L.rec_cap < 16 || L.next_ord >= 0xFFE0)
     return false;
-  const uint32_t* seg = L.pb + L.pb[6];
+  const uint32_t* seg = L.pb + (L.pb[6] & 0xFFFF);
   if (kind == ZBHIP_CMD_JOB_COMPLETE) {
     if (!(L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED && L.nt == 1 && L.pi_child == 1 && L.pi_asf == 0))
       return false;
@@ -2054,6 +2237,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.nt = 0;
   L.trig_key = NONE;
   L.trig_evt = NONE;
+  L.n_map = 0;
   L.docs = P.docs;
   L.doc_begin = doc_begin;
   L.doc_count = doc_count;
@@ -3064,6 +3248,7 @@ struct ActivatedOut {
   uint4 a;             // x = slot word (elem | key ord << 16), y = hdr.x, z = hdr.y, w = 1 found
   uint2 meta[kVars];
   long long val[kVars];
+  uint2 slots[kSlots]; // the instance's element instances (the job's enclosing scopes: variables)
 };
 __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2* jobs, uint32_t n, ActivatedOut* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -3085,6 +3270,8 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
       o.meta[v] = st.var_meta[(size_t)v * st.n + inst];
       o.val[v] = st.var_val[(size_t)v * st.n + inst];
     }
+    for (uint32_t s = 0; s < (uint32_t)kSlots; ++s)
+      o.slots[s] = s < nslots ? st.slots[(size_t)s * st.n + inst] : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   }
   out[i] = o;
 }
@@ -3166,6 +3353,7 @@ uint32_t step_resident(int variant, uint32_t prog_words) {
   return variant == 3   ? resident_for<KLinear>(lds_bytes<KLinear>(prog_words))
          : variant == 2 ? resident_for<KMsg>(lds_bytes<KMsg>(prog_words))
          : variant == 4 ? resident_for<KScope>(lds_bytes<KScope>(prog_words))
+         : variant == 5 ? resident_for<KScopeIO>(lds_bytes<KScopeIO>(prog_words))
          : variant      ? resident_for<KGeneric>(lds_bytes<KGeneric>(prog_words))
                         : resident_for<KSimple>(lds_bytes<KSimple>(prog_words));
 }
@@ -3173,7 +3361,7 @@ uint32_t step_queue(int variant) {
   return variant == 3 ? KLinear::Q : variant == 2 ? KMsg::Q : variant ? KGeneric::Q : KSimple::Q;
 }
 
-// variants: 0 KSimple, 1 KGeneric, 2 KMsg, 3 KLinear, 4 KScope (KGeneric's B, T, Q, R)
+// variants: 0 KSimple, 1 KGeneric, 2 KMsg, 3 KLinear, 4 KScope, 5 KScopeIO (KGeneric's B, T, Q, R)
 static_assert(KScope::B == KGeneric::B && KScope::Q == KGeneric::Q && KScope::R == KGeneric::R, "KScope shapes");
 uint32_t step_block(int variant) {
   return variant == 3 ? KLinear::B : variant == 2 ? KMsg::B : variant ? KGeneric::B : KSimple::B;
@@ -3183,6 +3371,7 @@ size_t step_lds_bytes(int variant, uint32_t prog_words) {
   return variant == 3   ? lds_bytes<KLinear>(prog_words)
          : variant == 2 ? lds_bytes<KMsg>(prog_words)
          : variant == 4 ? lds_bytes<KScope>(prog_words)
+         : variant == 5 ? lds_bytes<KScopeIO>(prog_words)
          : variant      ? lds_bytes<KGeneric>(prog_words)
                         : lds_bytes<KSimple>(prog_words);
 }
@@ -3259,6 +3448,7 @@ hipError_t launch_step(int variant, const StepParams& P, hipStream_t s) {
     case 2: return launch_k<KMsg>(P, s);
     case 1: return launch_k<KGeneric>(P, s);
     case 4: return launch_k<KScope>(P, s);
+    case 5: return launch_k<KScopeIO>(P, s);
     default: return launch_k<KSimple>(P, s);
   }
 }

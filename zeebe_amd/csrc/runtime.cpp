@@ -9,6 +9,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -98,7 +99,18 @@ struct Proc {
     return m && m->inner == e ? m : nullptr;
   }
   const std::string& id(uint32_t e) const { return strings[els[e].id]; }
+  // zeebe:ioMapping per element ([0] input, [1] output; kernels.hip io_map): type kIoNone, ZBHIP_MAP_VARIABLE
+  // (src = the source variable's name id) or a literal's zbhip_doc_type (STR: value-dictionary id in lit)
+  struct Io {
+    uint8_t type = 0xFE;
+    uint16_t src = NONE, tgt = NONE;
+    int64_t lit = 0;
+  };
+  std::vector<std::array<Io, 2>> io;
+  bool has_io = false;
+  bool io_of(uint32_t e) const { return has_io && e < io.size() && (io[e][0].type != 0xFE || io[e][1].type != 0xFE); }
 };
+constexpr uint8_t kIoNone = 0xFE;
 // device limit of a multi-instance body: loop counters live in 6 bits of the inner instance's slot
 // (kernels.hip apply_activating_child), children in 8 bits of the body's
 constexpr size_t kMaxMiItems = 63;
@@ -582,6 +594,8 @@ struct zbhip_handle {
   size_t n_xparts = 0;
   uint4* d_cmd_hdr2 = nullptr;
   long long* d_cmd_due = nullptr;       // (KScope) dueDate of the timer each batch canceled
+  long long* d_map_val = nullptr;       // (KScope) io-mapped variable values per batch (StepParams.map_val)
+  std::vector<long long> h_map_val;
   bool debug = getenv("ZBHIP_DEBUG") != nullptr;  // per-call host timing lines on stderr
   std::vector<long long> h_cmd_due;
   zbhip_xpart_cmd* d_xout = nullptr;
@@ -599,6 +613,7 @@ struct zbhip_handle {
   std::vector<int64_t> h_base;                 // key counter before each command's first key
   std::vector<zbhip_xpart_cmd> h_xout;
   bool msg() const { return variant == 2; }
+  bool scope_variant() const { return variant == 4 || variant == 5; }  // KScope / KScopeIO
 
   zbhip_stats stats{};
   bool stats_dirty = false;
@@ -701,7 +716,8 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
        dalloc(&h->d_region_lanes, (size_t)h->regions_cap * 128) == hipSuccess &&
        dalloc(&h->d_region_off, h->regions_cap) == hipSuccess;
   // timer rows (KScope timer catch events): one per instance
-  ok = ok && dalloc(&h->st.tmr, N) == hipSuccess && dalloc(&h->d_cmd_due, cfg->max_commands) == hipSuccess;
+  ok = ok && dalloc(&h->st.tmr, N) == hipSuccess && dalloc(&h->d_cmd_due, cfg->max_commands) == hipSuccess &&
+       dalloc(&h->d_map_val, (size_t)kMapVals * cfg->max_commands) == hipSuccess;
   // message correlation state (config 5): PROCESS_SUBSCRIPTION rows per instance, correlation slots
   const size_t S = cfg->max_correlation_keys;
   h->st.n_slots = (uint32_t)S;
@@ -774,6 +790,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->st.pms);
   (void)hipFree(h->st.tmr);
   (void)hipFree(h->d_cmd_due);
+  (void)hipFree(h->d_map_val);
   (void)hipFree(h->st.pi_key);
   (void)hipFree(h->st.slot_hdr);
   (void)hipFree(h->st.sub_a);
@@ -950,7 +967,8 @@ static int rebuild_program(zbhip_handle* h) {
     const uint32_t n_cond = P.cond_begin.empty() ? 0 : (uint32_t)P.cond_begin.size() - 1;
     const uint32_t code_off = (cond_off + n_cond + 3) & ~3u;  // 16-byte aligned instructions (uint4 loads)
     const uint32_t seg_off = code_off + 4 * (uint32_t)P.code.size();
-    const uint32_t total = (seg_off + n_el + 3) & ~3u;
+    const uint32_t io_off = (seg_off + n_el + 3) & ~3u;  // io mappings: 8 words per element (kernels.hip io_map)
+    const uint32_t total = P.has_io ? io_off + 8 * n_el : io_off;
     prog.resize(base + total, 0);
     uint32_t* pb = prog.data() + base;
     pb[0] = n_el | ((uint32_t)P.none_start << 16);
@@ -958,8 +976,20 @@ static int rebuild_program(zbhip_handle* h) {
     pb[2] = out_off;
     pb[3] = cond_off;
     pb[4] = code_off;
-    pb[5] = P.bpmn_name | (P.has_timer ? 1u << 16 : 0u);  // name id of the bpmnProcessId (message records)
-    pb[6] = seg_off;
+    pb[5] = P.bpmn_name | (P.has_timer ? 1u << 16 : 0u) | (P.has_io ? 1u << 17 : 0u);  // bpmnProcessId name id
+    pb[6] = seg_off | (io_off << 16);
+    if (io_off >= 0x10000) return ZBHIP_ENOMEM;
+    if (P.has_io)
+      for (uint32_t e = 0; e < n_el; ++e)
+        for (int k = 0; k < 2; ++k) {
+          // w0 = type | target name << 16, w1 = source name id, w2/w3 = the literal (STR: its string id)
+          const Proc::Io& io = P.io[e][k];
+          uint32_t* m = pb + io_off + 8 * e + 4 * k;
+          m[0] = io.type | ((uint32_t)io.tgt << 16);
+          m[1] = io.src;
+          m[2] = (uint32_t)((uint64_t)io.lit & 0xFFFFFFFFu);
+          m[3] = (uint32_t)((uint64_t)io.lit >> 32);
+        }
     pb[7] = create_template_word(P);
     // straight-line segment words (kernels.hip fast_command): a start event or service task with
     // one unconditional outgoing flow into a service task or a none end event without outgoing flows
@@ -967,13 +997,13 @@ static int rebuild_program(zbhip_handle* h) {
       const zbhip_element& E = P.els[e];
       uint32_t sg = 0;
       if ((E.element_type == ZBHIP_EL_START_EVENT || ZBHIP_IS_JOB_WORKER(E.element_type)) && E.out_count == 1 &&
-          E.flow_scope == 0 && !(ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16)) {
+          E.flow_scope == 0 && !(ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) && !P.io_of(e)) {
         const uint32_t f = P.out[E.out_begin];
         const zbhip_element& F = P.els[f];
         const uint32_t n = F.flow_target;
         if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.condition == ZBHIP_NONE16 && n < n_el && f < 0xFFF && n < 0xFFF) {
           const zbhip_element& N = P.els[n];
-          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && N.start_event == ZBHIP_NONE16;
+          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && N.start_event == ZBHIP_NONE16 && !P.io_of(n);
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
           if (task || end)
             sg = (1u << 31) | (ZBHIP_IS_JOB_WORKER(E.element_type) ? 1u << 30 : 0u) | (end ? 1u << 24 : 0u) |
@@ -1188,11 +1218,56 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         it.second = sid;
       }
   }
+  // io mappings (zbhip_mapping): job worker tasks (not multi-instance inner activities) and embedded
+  // sub-processes, one input and one output each; names interned in element order, the input's source
+  // and target before the output's (the oracle's deploy order), string literals into the value
+  // dictionary
+  if (csr->n_mappings) {
+    if (!csr->mappings) return ZBHIP_EINVAL;
+    P.io.assign(P.els.size(), {});
+    for (uint32_t i = 0; i < csr->n_mappings; ++i) {
+      const zbhip_mapping& M = csr->mappings[i];
+      if (M.element >= P.els.size() || M.output > 1 || M.target >= P.strings.size()) return ZBHIP_EINVAL;
+      const zbhip_element& E = P.els[M.element];
+      if (!(ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_SUB_PROCESS) || P.mi_inner(M.element))
+        return ZBHIP_EUNSUPP;
+      Proc::Io& io = P.io[M.element][M.output];
+      if (io.type != kIoNone) return ZBHIP_EUNSUPP;  // one mapping of each kind
+      if (M.source_type == ZBHIP_MAP_VARIABLE || M.source_type == ZBHIP_DOC_STR) {
+        if (M.source >= P.strings.size()) return ZBHIP_EINVAL;
+      } else if (M.source_type != ZBHIP_DOC_NIL && M.source_type != ZBHIP_DOC_BOOL && M.source_type != ZBHIP_DOC_INT) {
+        return ZBHIP_EUNSUPP;
+      }
+      io.type = M.source_type;
+      io.src = M.source;
+      io.tgt = M.target;
+      io.lit = M.literal;
+    }
+    for (size_t e = 0; e < P.els.size(); ++e)
+      for (Proc::Io& io : P.io[e]) {
+        if (io.type == kIoNone) continue;
+        if (io.type == ZBHIP_MAP_VARIABLE) {
+          const int id = zbhip_intern(h, P.strings[io.src].c_str());
+          if (id < 0) return id;
+          io.src = (uint16_t)id;
+        } else if (io.type == ZBHIP_DOC_STR) {
+          const std::string& t = P.strings[io.src];
+          const int64_t sid = zbhip_intern_string(h, t.data(), t.size());
+          if (sid < 0) return (int)sid;
+          io.lit = sid;
+        }
+        const int tid = zbhip_intern(h, P.strings[io.tgt].c_str());
+        if (tid < 0) return tid;
+        io.tgt = (uint16_t)tid;
+        P.has_io = true;
+      }
+  }
   // kernel variant, the smallest that covers every deployed process (kernels.hip KCfg):
   //   3 KLinear  -- linear chains: every node <= 1 outgoing flow, no gateways (4 waves/SIMD)
   //   0 KSimple  -- one token per instance (no parallel gateway / multi-outgoing node but an XOR)
   //   1 KGeneric -- everything else in the subset
-  //   4 KScope   -- embedded sub-processes (flow scopes below the process)
+  //   4 KScope   -- embedded sub-processes (flow scopes below the process), timers
+  //   5 KScopeIO -- KScope plus zeebe:ioMapping (variables in element-instance scopes)
   //   2 KMsg     -- message catch events and subscription commands (config 5); a sub-process
   //                 deployed next to them falls back (KMsg has no flow scopes)
   int cls = 3;
@@ -1204,9 +1279,13 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       cls = 1;
     scopes |= e.element_type == ZBHIP_EL_SUB_PROCESS || e.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY;
   }
-  if (scopes || P.has_timer) cls = 4;  // timer catch events: KScope as well (the instance's timer row)
+  // timer catch events: KScope as well (the instance's timer row); io mappings: KScopeIO (variables
+  // in the scopes of element instances)
+  if (scopes || P.has_timer) cls = 4;
+  if (P.has_io) cls = 5;
   if (P.has_msg) cls = 2;
-  auto rank = [](int v) { return v == 3 ? 0 : v == 0 ? 1 : v == 1 ? 2 : v == 4 ? 3 : 4; };
+  auto rank = [](int v) { return v == 3 ? 0 : v == 0 ? 1 : v == 1 ? 2 : v == 4 ? 3 : v == 5 ? 4 : 5; };
+  if ((P.has_msg && (h->variant == 5 || P.has_io)) || (P.has_io && h->msg())) return ZBHIP_EUNSUPP;  // KMsg has no io
   const int old_variant = h->variant;
   if (h->procs.empty() || rank(cls) > rank(h->variant)) h->variant = cls;
   if (const char* fv = getenv("ZBHIP_FORCE_VARIANT")) {  // experiments: never below what the processes need
@@ -1843,8 +1922,10 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.stamp = h->window_stamp;
   P.now_ms = h->clock_ms;
   P.cmd_due = h->d_cmd_due;
+  P.map_val = h->d_map_val;
+  P.map_cap = h->cfg.max_commands;
   h->run_clock_ms = h->clock_ms;
-  P.tpl = (h->variant == 0 || h->variant == 1 || h->variant == 4) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
+  P.tpl = (h->variant == 0 || h->variant == 1 || h->scope_variant()) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
   if (h->msg()) {
     int rc = sync_strings(h);
     if (rc) return rc;
@@ -2066,9 +2147,16 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   // secondary headers: message partitions only (slot batches, outbox counts, payload rows)
   if (h->msg()) h->h_hdr2.assign(n, make_uint4(0, 0, 0, 0));
   else h->h_hdr2.clear();
-  if (n && h->variant == 4) {  // dueDates of canceled timers (TIMER:CANCELED values)
+  if (n && h->scope_variant()) {  // dueDates of canceled timers (TIMER:CANCELED values)
     h->h_cmd_due.resize(n);
     HIPCHK(hipMemcpyAsync(h->h_cmd_due.data(), h->d_cmd_due, n * sizeof(long long), hipMemcpyDeviceToHost, h->stream));
+  }
+  if (n && h->variant == 5) {  // io-mapped variable values (C_VAR_MAPPED records)
+    const size_t m = std::min<size_t>(n, h->cfg.max_commands);
+    h->h_map_val.resize((size_t)kMapVals * h->cfg.max_commands);
+    HIPCHK(hipMemcpy2DAsync(h->h_map_val.data(), h->cfg.max_commands * sizeof(long long), h->d_map_val,
+                            h->cfg.max_commands * sizeof(long long), m * sizeof(long long), kMapVals,
+                            hipMemcpyDeviceToHost, h->stream));
   }
   if (n && h->msg())
     HIPCHK(hipMemcpyAsync(h->h_hdr2.data(), h->d_cmd_hdr2, n * sizeof(uint4), hipMemcpyDeviceToHost, h->stream));
@@ -2276,6 +2364,18 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.aux = ZBHIP_AUX_INLINE;
       r.partition = c6 == C_MI_ITEM ? m->items[fl - 1].first : ZBHIP_DOC_INT;
       r.message_key = c6 == C_MI_ITEM ? m->items[fl - 1].second : (int64_t)fl;
+    } else if (c6 == C_VAR_MAPPED) {
+      // BpmnVariableMappingBehavior (behavior/BpmnVariableMappingBehavior.java:53-156): the value the
+      // mapping computed, inline (its zbhip_doc_type in flags bits 0..2, its map_val slot in bit 4)
+      const size_t slot = (fl >> 4) & 1;
+      const size_t at = slot * h->cfg.max_commands + c;
+      if (c >= h->cfg.max_commands || at >= h->h_map_val.size()) return ZBHIP_EDEVICE;
+      r.value_type = ZBHIP_VT_VARIABLE;
+      r.intent = (fl >> 3) & 1 ? ZBHIP_VAR_UPDATED : ZBHIP_VAR_CREATED;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.aux = ZBHIP_AUX_INLINE;
+      r.partition = (int32_t)(fl & 7);
+      r.message_key = h->h_map_val[at];
     } else if (c6 == C_PIB_ACTIVATE) {
       // PROCESS_INSTANCE_BATCH:ACTIVATE (activateChildInstancesInBatches): batchElementInstanceKey =
       // the body (scope_key), index = its collection's size
@@ -3390,7 +3490,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     std::map<int64_t, std::map<std::string, const ImpVar*>> loop_vars;
     for (const auto& v : vars)
       if (scope_of(v.scope)) {
-        if (subs.count(v.scope)) return ZBHIP_EUNSUPP;  // container-local variables: outside the subset
+        // container-local variables: written by a sub-process's input mapping (KScopeIO) only
+        if (subs.count(v.scope) && (!P.has_io || els[v.scope].type != ZBHIP_EL_SUB_PROCESS)) return ZBHIP_EUNSUPP;
         keys.push_back(v.key);
         if (v.scope != pe.key) {
           const ImpElement& se = els[v.scope];
@@ -3752,9 +3853,11 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     uint4 a;
     uint2 meta[kVars];
     long long val[kVars];
+    uint2 slots[kSlots];
     memcpy(&a, o, sizeof a);
     memcpy(meta, o + sizeof(uint4), sizeof meta);
     memcpy(val, o + sizeof(uint4) + sizeof meta, sizeof val);
+    memcpy(slots, o + sizeof(uint4) + sizeof meta + sizeof val, sizeof slots);
     const uint32_t inst = pick[i].second.first;
     if (!a.w) return ZBHIP_EDEVICE;  // the index and the device rows disagree
     const uint32_t proc = a.y & 0xFFFF, elem = a.x & 0xFFFF, eord = a.x >> 16;
@@ -3788,7 +3891,16 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
         j.variables[j.n_variables++] = d;
       }
     }
-    for (uint32_t scope : {eord, 0u}) {
+    // the element's scope, the instances of its enclosing containers (sub-processes with io-mapped
+    // variables), then the process instance's
+    std::vector<uint32_t> chain{eord};
+    if (proc < h->procs.size() && elem < h->procs[proc].els.size())
+      for (uint32_t c = h->procs[proc].els[elem].flow_scope, d = 0; c != 0 && c < h->procs[proc].els.size() && d < 16;
+           c = h->procs[proc].els[c].flow_scope, ++d)
+        for (const uint2& sl : slots)
+          if (sl.x != 0xFFFFFFFFu && (sl.x & 0xFFFF) == c) chain.push_back(sl.x >> 16);
+    chain.push_back(0u);
+    for (uint32_t scope : chain) {
       std::vector<uint32_t> local;
       for (uint32_t v = 0; v < nv; ++v)
         if ((meta[v].x >> 16) == scope) local.push_back(v);

@@ -92,6 +92,9 @@ enum : uint8_t {
   C_TIMER_TRIGGERED = 54,
   C_TIMER_CANCELED = 55,  // CatchEventBehavior.unsubscribeFromTimerEvent; dueDate in StepParams.cmd_due
   C_TIMER_NEXT = 56,
+  C_VAR_MAPPED = 58,       // VARIABLE:CREATED / UPDATED of an io mapping (BpmnVariableMappingBehavior): key =
+                           // the variable, aux = its scope, elem = its name, flags = zbhip_doc_type | updated
+                           // << 3 | value slot << 4 (the value in StepParams.map_val)
   C_INCIDENT_CREATED = 57,  // INCIDENT:CREATED of an exclusive gateway: key = incident, aux = the gateway's
                             // element instance, elem = the gateway, flags = the incident info (kernels.hip
                             // find_sequence_flow: flow position 0..14 / 15 none chosen | FEEL type << 4)      // TIMER:CREATED of a cycle's next timer (rescheduleTimer): dueDate from the
@@ -251,7 +254,11 @@ struct StepParams {
   uint32_t launch_seq;
   long long now_ms;           // zbhip_set_clock: ActorClock.currentTimeMillis() of this window
   long long* cmd_due;         // [n_cmds] (KScope) dueDate of the timer a batch canceled (at most one)
+  long long* map_val;         // [kMapVals][map_cap] (KScope) values of the variables a batch's io mappings
+                              // wrote: value j of window command c at j * map_cap + c (C_VAR_MAPPED)
+  uint32_t map_cap;
 };
+constexpr int kMapVals = 2;   // io-mapped VARIABLE records per batch (more: FB_VARS)
 
 // ---- log bytes on the device (logdev.hip) ----
 // entry templates of the device log writer (logwriter.cpp log_device_templates): PROCESS_INSTANCE
