@@ -413,6 +413,12 @@ final class Window {
         if (aux >= 0) {
           v.setVariables(documents[i]); // JOB:COMPLETED / COMPLETE rejection: the command's variables
         }
+        final long deadline = r.get(JAVA_LONG, 56); // message_key: an ACTIVATED job's deadline
+        if (deadline != -1) {
+          final int worker = r.get(JAVA_INT, 64); // correlation_key: its worker (value dictionary)
+          v.setDeadline(deadline)
+              .setWorker(new UnsafeBuffer(worker == Messages.NO_STRING ? new byte[0] : p.stringValue(worker)));
+        }
         return v.setTenantId(TENANT);
       }
       case VARIABLE -> {

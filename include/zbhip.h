@@ -453,9 +453,10 @@ typedef struct zbhip_record {
                                    message_key, its zbhip_doc_type in partition: multi-instance
                                    loopCounter / input element); JOB:COMPLETED: source doc; INCIDENT: the
                                    sequence flow whose condition was not a boolean (-1: none chosen); else -1 */
-  /* message value fields (MESSAGE / MESSAGE_SUBSCRIPTION / PROCESS_MESSAGE_SUBSCRIPTION) */
-  int64_t message_key;          /* messageKey, -1 unset */
-  uint32_t correlation_key;     /* string id, ZBHIP_NO_STRING = empty */
+  /* message value fields (MESSAGE / MESSAGE_SUBSCRIPTION / PROCESS_MESSAGE_SUBSCRIPTION); a JOB
+     record of an ACTIVATED job (JOB:COMPLETED / CANCELED write the stored job): its deadline and worker */
+  int64_t message_key;          /* messageKey / JOB: deadline; -1 unset */
+  uint32_t correlation_key;     /* string id (JOB: the worker), ZBHIP_NO_STRING = empty */
   uint16_t message_name;        /* name id, 0xFFFF = empty */
   uint16_t bpmn_process_id;     /* name id, 0xFFFF = empty */
   int32_t partition;            /* PMS: subscriptionPartitionId; TIMER events: repetitions (-1 infinite);
@@ -669,7 +670,9 @@ int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n,
  * older ones from a per-instance ring of the last 16 ordinals in HBM, which holds every key only if
  * every window of the handle comes through here.  ZBHIP_EUNSUPP (use the host serialiser for this
  * window and the later ones): message partitions, continuation batches, imported state, string
- * variables, a key older than the ring, or a window that skipped this call. */
+ * variables, a key older than the ring, or a window that skipped this call.  The bytes are written
+ * asynchronously in the order of the handle's stream (zbhip_stream): zbhip_log_device_copy and the
+ * handle's next run wait for them; a reader on another stream waits on that stream first. */
 int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_window* w, const void** dev_bytes, size_t* used);
 /* Copies n bytes of the last zbhip_serialize_log_device output into host memory. */
 int zbhip_log_device_copy(zbhip_handle* h, void* dst, size_t n);

@@ -374,6 +374,10 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0, timer_value=
                       elementInstanceKey=int(r["scope_key"]))
         if int(r["intent"]) == 2:  # COMPLETED: the stored job + the command's variables
             fields["variables"] = src_doc
+        if int(r["message_key"]) != -1:  # an ACTIVATED job (DbJobState.activate): its deadline and worker
+            fields["deadline"] = int(r["message_key"])
+            cid = int(r["correlation_key"])
+            fields["worker"] = tables.string_value(cid) if cid != NO_STRING else ""
         return write_object(JOB, fields)
     if vt == VT_VARIABLE:
         if int(r["aux"]) == AUX_INLINE:  # a value the engine computed (multi-instance loop variables)

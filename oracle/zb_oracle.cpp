@@ -1424,6 +1424,7 @@ class Oracle {
     if (max_jobs < 1) return 1;
     if (timeout < 1) return 2;
     if (type.empty()) return 3;
+    if (!worker.empty()) intern_string(worker);  // (the value dictionary: JOB records name it)
     batch_key = ((int64_t)partition_ << 51) + ++key_counter_;  // keyGenerator.nextKey, no instance's
     std::vector<int64_t> keys;
     for (auto it = activatable_.lower_bound({type, "<default>", INT64_MIN});
@@ -2122,6 +2123,7 @@ class Oracle {
     rec.r.process_instance_key = job.pi.piKey;
     rec.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
     rec.doc = cmd.doc;
+    job_activation_fields(rec, job);
     apply_job_completed(jobKey, job);
     // afterAccept
     auto sit = ei_.find(job.elementInstanceKey);
@@ -2145,6 +2147,14 @@ class Oracle {
         pi_command(job.elementInstanceKey, ZBHIP_PI_COMPLETE_ELEMENT, task.value);
       }
     }
+  }
+
+  // an ACTIVATED job's record carries the deadline and worker DbJobState.activate stored (the
+  // zbhip_record fields message_key / correlation_key of a JOB record)
+  void job_activation_fields(ORecord& rec, const JobRow& job) {
+    if (!job.activated) return;
+    rec.r.message_key = job.deadline;
+    rec.r.correlation_key = job.worker.empty() ? ZBHIP_NO_STRING : intern_string(job.worker);
   }
 
   // JobCreatedApplier (state/appliers/JobCreatedApplier.java:28-41) / DbJobState.create
@@ -2581,6 +2591,7 @@ class Oracle {
       rec.r.element_idx = job.pi.elem;
       rec.r.scope_key = job.elementInstanceKey;
       rec.r.process_instance_key = job.pi.piKey;
+      job_activation_fields(rec, job);
       apply_job_canceled(jobKey, job);
     }
     unsubscribe_timers(key);

@@ -226,6 +226,8 @@ def test_gpu_io_mapping_job_activation_variables():
 
 
 def test_gpu_io_mapping_restart():
+    from test_gpu_import import _same
+
     # export -> fresh handle -> import -> continue equals the uninterrupted partition and the oracle
     # (task- and sub-process-scope variables restored into their scopes)
     xml = _sub([("input", "=x", "y"), ("output", "=y", "z")], "task")
@@ -255,7 +257,7 @@ def test_gpu_io_mapping_restart():
     B.orc.clear_records()
     B.orc.submit(co)
     B.orc.run()
-    assert_same_records(got, B.orc.records(), fresh, B.orc)
+    _same(got, B.orc.records())  # (source_index / aux bases are each handle's own counters)
     assert fresh.state() == B.orc.state()
     assert [r for r in fresh.state() if not r.startswith("KEY|")] == []
 

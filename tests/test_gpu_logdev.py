@@ -240,3 +240,17 @@ def test_declined_window_past_earlier_windows_and_after_a_redeploy():
     log.window(create_commands(32, process_idx=1, first_instance=484))
     log.window(job_completions(recs, log.part))
     assert log.declined == 1
+
+
+def test_activated_job_completions_go_to_the_host_serialiser():
+    # JOB:COMPLETED of an ACTIVATED job carries the worker (a value-dictionary string): the device
+    # writer declines the window (ZBHIP_EUNSUPP) and the host serialiser writes it; windows without
+    # activated jobs before and after stay on the device
+    n = 64
+    log = Log(bpmn.linear_process(3, job_type="t"), n)
+    recs = log.window(create_commands(n))
+    log.part.activate_jobs("t", worker="w", timeout=1000, max_jobs=8, timestamp=10)
+    recs = log.window(job_completions(recs, log.part), allow_host=True)
+    assert log.declined == 1
+    log.window(job_completions(recs, log.part))  # (the declined window's keys went into the ring)
+    assert log.declined == 1

@@ -98,3 +98,25 @@ def test_gpu_log_bytes_xor_documents():
     cmds["doc_count"] = 1
     cmds["doc_begin"] = np.arange(150)
     pair.window(cmds, amount_docs(rng.integers(0, 200001, 150) * 10000, 0, decimal=True))
+
+
+def test_gpu_log_bytes_of_activated_jobs():
+    # JOB:COMPLETED of an ACTIVATED job is the stored job (JobCompleteProcessor.acceptCommand:
+    # jobState.getJob, DbJobState.activate stored the deadline and worker): the drained record carries
+    # them (message_key / correlation_key), both serialisers write them, and the device writer leaves
+    # such a window to the host serialiser (the worker is a value-dictionary string)
+    from zeebe_amd.native import ZbhipError
+    n = 40
+    pair = Pair(bpmn.linear_process(2, job_type="t"), n)
+    recs = pair.window(create_commands(n, 0))
+    g = pair.part.activate_jobs("t", worker="worker-A", timeout=60000, max_jobs=15, timestamp=500)
+    o = pair.orc.activate_jobs("t", worker="worker-A", timeout=60000, max_jobs=15, timestamp=500)
+    assert [int(k) for k in g[1]["key"]] == [int(k) for k in o[1]["key"]]
+    pair.part.activate_jobs("t", worker="", timeout=1000, max_jobs=5, timestamp=600)
+    pair.orc.activate_jobs("t", worker="", timeout=1000, max_jobs=5, timestamp=600)
+    jobs = [int(r["key"]) for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+    res = [pair.part.resolve_key(k) for k in jobs]
+    got = pair.window(complete_commands([r[0] for r in res], [r[1] for r in res]))
+    done = got[(got["value_type"] == abi.VT_JOB) & (got["intent"] == abi.JOB_COMPLETED)]
+    act = done[done["message_key"] != -1]
+    assert len(act) == 20 and set(act["message_key"].tolist()) == {60500, 1600}

@@ -378,3 +378,22 @@ def test_rejected_timer_trigger_carries_the_commands_timer_record():
         assert val["targetElementId"] == x["handlerNodeId"] and val["repetitions"] == int(x["repetitions"])
         assert val["processDefinitionKey"] == int(x["processDefinitionKey"])
         assert val["dueDate"] == int(x["dueDate"])
+
+
+def test_serializer_activated_job_completions():
+    """JOB:COMPLETED / JOB:CANCELED of an ACTIVATED job: the stored job, with the deadline and worker
+    JobBatchActivateProcessor stored (DbJobState.activate; JobCompleteProcessor.acceptCommand writes
+    jobState.getJob) -- in the drained record as message_key / correlation_key."""
+    run = Run([bpmn.linear_process(2, job_type="t")], strings=["w1"])
+    recs = run.window(create_commands(6, 0))
+    key, jobs, reason = run.orc.activate_jobs("t", worker="w1", timeout=1000, max_jobs=4, timestamp=50)
+    assert reason == 0 and len(jobs) == 4
+    km = _key_map(run.orc, 6)
+    keys = [int(r["key"]) for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+    recs = run.window(complete_commands([km[k][0] for k in keys], [km[k][1] for k in keys]))
+    done = recs[(recs["value_type"] == abi.VT_JOB) & (recs["intent"] == abi.JOB_COMPLETED)]
+    assert sorted(done["message_key"].tolist()) == [-1, -1, 1050, 1050, 1050, 1050]
+    values = [msgpack.unpackb(buf[40 + struct.unpack_from("<HBBqqqqHH", buf)[7]:], raw=False)
+              for buf in (run.last_bytes[o + 12:o + f] for o, f in split_entries(run.last_bytes))]
+    jobs_done = [v for v, r in zip(values, recs) if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_COMPLETED]
+    assert sorted((v["deadline"], v["worker"]) for v in jobs_done) == [(-1, "")] * 2 + [(1050, "w1")] * 4

@@ -151,6 +151,10 @@ class RecordValues:
                 v.update({"type": p.job_types[elem], "retries": p.retries[elem], "elementId": p.element_ids[elem],
                           "elementInstanceKey": scope, "processInstanceKey": pik, "bpmnProcessId": p.bpmn_process_id,
                           "processDefinitionVersion": p.version, "processDefinitionKey": p.definition_key})
+            if int(r["message_key"]) != -1:  # an ACTIVATED job: the deadline and worker it holds
+                cid = int(r["correlation_key"])
+                v.update({"deadline": int(r["message_key"]),
+                          "worker": self.string_value(cid) if cid != abi.NO_STRING else ""})
             return v
         if vt == abi.VT_VARIABLE:
             # ZBHIP_AUX_INLINE: a value the engine computed (multi-instance loop variables)

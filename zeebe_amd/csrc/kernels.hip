@@ -1410,7 +1410,8 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
   tbl_set_state(L, t, ZBHIP_PI_ELEMENT_TERMINATING);
   const uint2 e = tget(L, t);
   const uint32_t job = e.y & 0xFFFF;
-  if (((e.y >> 24) & 1u) && job != JOB_ZERO && job != JOB_MINUS1) emit(L, C_JOB_CANCELED, job, key, elem);
+  // (flag 1: the job was ACTIVATED -- its record carries the stored deadline and worker)
+  if (((e.y >> 24) & 1u) && job != JOB_ZERO && job != JOB_MINUS1) emit(L, C_JOB_CANCELED, job, key, elem, (e.y >> 25) & 1u);
   if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == key) cancel_timer(L);
   const uint32_t c = scope_of<K>(w);
   const uint32_t fst = c == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, c)).y >> 16) & 0xFF;
@@ -1810,7 +1811,7 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
     if ((sg & (SEG_VALID | SEG_FROM_TASK)) != (SEG_VALID | SEG_FROM_TASK)) return false;
     const uint32_t k = L.next_ord, n = (sg >> 12) & 0xFFF;
     // JobCompleteProcessor + EventTriggerBehavior.triggeringProcessEvent, then COMPLETE_ELEMENT(task)
-    put(L, 0, C_JOB_COMPLETED, ref, tk, te);
+    put(L, 0, C_JOB_COMPLETED | (((e.y >> 25) & 1u) << 8), ref, tk, te);  // (flag 1: an ACTIVATED job)
     put(L, 1, C_PE_TRIGGERING, k, tk, te);
     put(L, 2, ZBHIP_PI_COMPLETE_ELEMENT, tk, 0, te);
     put(L, 3, ZBHIP_PI_ELEMENT_COMPLETING, tk, 0, te);
@@ -2424,7 +2425,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     } else {
       uint2 e = tget(L, t);
       const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
-      emit(L, C_JOB_COMPLETED, ref, task_key, task_elem);
+      emit(L, C_JOB_COMPLETED, ref, task_key, task_elem, (e.y >> 25) & 1u);  // (flag 1: an ACTIVATED job)
       // the task's flow scope: the process instance, or (K::S) the sub-process instance around it
       bool fs_active = L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED;
       uint32_t fsk = 0;

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "zb_internal.h"
 
@@ -72,6 +73,8 @@ struct LogParams {
   const uint32_t* tpl_idx;
   uint32_t* rinfo;              // [rows] per record: template id << 16 | entry bytes, or kSlow | bytes
   unsigned long long out_cap;   // bytes at `out` (0: unchecked)
+  LogKeys* wkeys;               // [n] per command: the older keys its records name (k_log_sizes)
+  uint32_t tpl_lds;             // bytes of the templates + their descriptors (k_log_stream stages both)
 };
 constexpr uint32_t kSlow = 1u << 31;
 
@@ -276,6 +279,8 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
     r.rt = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
     r.skip = !rej && c6 >= 8 && !(fl & F_UNPROCESSED) ? 1 : 0;  // a follow-up command processed in its batch
   } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE || c6 == C_JOB_CANCELED) {
+    // an ACTIVATED job's record carries its worker (a value-dictionary string): the host serialiser
+    if (!rej && (fl & 1u) && (c6 == C_JOB_COMPLETED || c6 == C_JOB_CANCELED)) return false;
     r.vt = ZBHIP_VT_JOB;
     r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED
                : c6 == C_JOB_CANCELED ? ZBHIP_JOB_CANCELED : ZBHIP_JOB_COMPLETE;
@@ -607,7 +612,9 @@ __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
   if (c < L.n) {
     const LogCmd m = L.cmds[c];
     Count s;
-    KeyCache kc;
+    KeyCache kc, kp;
+    long long pik = -1;
+    if (!key_of_lane(L, m, 0, pik, kp)) pik = -1;
     for (uint32_t j = 0; j < m.nrec; ++j) {
       Rec r;
       uint4 d;
@@ -633,6 +640,15 @@ __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
       }
     }
     L.bytes[c] = s.n;
+    if (L.wkeys) {
+      LogKeys k;
+      k.pik = pik;
+      k.k0 = kc.k0;
+      k.k1 = kc.k1;
+      k.o0 = kc.o0;
+      k.o1 = kc.o1;
+      L.wkeys[c] = k;
+    }
   }
   const unsigned long long b = __ballot(slow);
   if (b && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(b)) atomicOr(L.flag, 2u);
@@ -851,6 +867,190 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
   }
 }
 
+// pass 2, streaming form (the templates and their descriptors fit LDS next to the waves' stages):
+// one wave per contiguous range of commands, taken in blocks of up to kStreamCmds commands /
+// kStreamRecs records.  A block's command rows and key sets go into the lanes' registers (lane k:
+// command k of the block, read out uniformly with v_readlane), its records' template info and rows
+// into the wave's LDS by direct global->LDS loads.  Those are the wave's only vector-memory loads, so
+// its only drain of outstanding stores is once per block: the ~128 KB of a block stream out without
+// a wait (k_log_write waited for its group's stores before every group's metadata loads).  Per record
+// the whole wave composes the entry into the stage: lane w copies template word w (LDS to LDS,
+// consecutive words: no bank conflicts), lanes 0-3 write the header's position / source position /
+// key / timestamp, lanes 0-15 the big-endian processInstanceKey / scope key bytes.  A full stage, a
+// composed entry (k_log_compose writes it) or the command's end flushes the stage in 16-byte chunks.
+constexpr uint32_t kStreamWaves = 8;
+constexpr uint32_t kStreamCmds = 32;
+constexpr uint32_t kStreamRecs = 256;
+constexpr uint32_t kStreamStage = 4096;
+constexpr uint32_t kStreamWaveLds = kStreamStage + kStreamRecs * 12;  // stage, rinfo, rows
+constexpr uint32_t kStreamLdsMax = 160 * 1024;
+
+typedef __attribute__((address_space(1))) void g_void;
+typedef __attribute__((address_space(3))) void l_void;
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ unsigned long long rl64(unsigned long long v, uint32_t k) {
+  return (unsigned long long)rl((uint32_t)v, k) | (unsigned long long)rl((uint32_t)(v >> 32), k) << 32;
+}
+
+// the stage's bytes [gs, ge) out (stage byte 0 = output byte sb = gs & ~15): whole 16-byte chunks, and
+// the 8-byte half of a chunk shared with the neighbouring group
+__device__ __forceinline__ void stream_flush(uint8_t* out, const uint8_t* stage, unsigned long long sb,
+                                             unsigned long long gs, unsigned long long ge, uint32_t lane) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_wave_barrier();
+  for (unsigned long long o = sb + 16ull * lane; o < ge; o += 1024ull) {
+    const uint4 v = *reinterpret_cast<const uint4*>(stage + (o - sb));
+    const bool h0 = o >= gs && o + 8 <= ge, h1 = o + 8 >= gs && o + 16 <= ge;
+    if (h0 && h1) {
+      u32x4 q;
+      q.x = v.x; q.y = v.y; q.z = v.z; q.w = v.w;
+      __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out + o));
+    } else if (h0) {
+      u32x2 q;
+      q.x = v.x; q.y = v.y;
+      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o));
+    } else if (h1) {
+      u32x2 q;
+      q.x = v.z; q.y = v.w;
+      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o + 8));
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint8_t* const lds = reinterpret_cast<uint8_t*>(smem);
+  if (L.out_cap && ((*L.flag & 1u) || L.bytes[L.n] > L.out_cap)) return;  // (as k_log_write)
+  const uint32_t T = (L.tpl_lds + 15u) & ~15u;
+  for (uint32_t i = threadIdx.x; i < T / 16; i += blockDim.x)
+    reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(L.tpl)[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint8_t* const stage = lds + T + wv * kStreamWaveLds;
+  uint32_t* const lri = reinterpret_cast<uint32_t*>(stage + kStreamStage);
+  uint32_t* const lrow = lri + kStreamRecs;  // two words per record
+  const uint4* const desc = reinterpret_cast<const uint4*>(lds + (reinterpret_cast<const uint8_t*>(L.tpl_desc) - L.tpl));
+  uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
+  const unsigned long long ts = (unsigned long long)L.timestamp;
+  const unsigned long long W = (unsigned long long)gridDim.x * kStreamWaves;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * kStreamWaves + wv);
+  const uint32_t ce = (uint32_t)((unsigned long long)L.n * (w + 1) / W);
+  uint32_t c = (uint32_t)((unsigned long long)L.n * w / W);
+  uint32_t j0 = 0;              // records of command c already written (a command longer than a block)
+  unsigned long long gpos = 0;  // and the byte position after them
+  while (c < ce) {
+    const uint32_t nb = ce - c < kStreamCmds ? ce - c : kStreamCmds;
+    LogCmd m{};
+    unsigned long long mb = 0;
+    LogKeys mk{};
+    if (lane < nb) {
+      m = L.cmds[c + lane];
+      mb = L.bytes[c + lane];
+      mk = L.wkeys[c + lane];
+    }
+    const uint32_t cnt = lane < nb ? (uint32_t)m.nrec - (lane == 0 ? j0 : 0u) : 0u;
+    uint32_t incl = cnt;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    uint32_t take = (uint32_t)__builtin_popcountll(__ballot(lane < nb && incl <= kStreamRecs));
+    uint32_t first = rl(cnt, 0);
+    const bool partial = take == 0;  // command c alone has more records than a block: its next kStreamRecs
+    if (partial) {
+      take = 1;
+      first = kStreamRecs;
+    }
+    // the block's record info and rows into the wave's LDS
+    uint32_t p = 0;
+    for (uint32_t k = 0; k < take; ++k) {
+      const uint32_t rk = rl((uint32_t)m.rec_off, k) + (k == 0 ? j0 : 0u);
+      const uint32_t nk = k == 0 ? first : rl(cnt, k);
+      for (uint32_t q = 0; q < nk; q += 64)
+        if (q + lane < nk)
+          __builtin_amdgcn_global_load_lds((g_void*)(L.rinfo + rk + q + lane), (l_void*)(lri + p + q), 4, 0, 0);
+      const uint32_t* const rw = reinterpret_cast<const uint32_t*>(L.rows) + 2ull * rk;
+      for (uint32_t q = 0; q < 2 * nk; q += 64)
+        if (q + lane < 2 * nk) __builtin_amdgcn_global_load_lds((g_void*)(rw + q + lane), (l_void*)(lrow + 2 * p + q), 4, 0, 0);
+      p += nk;
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loads above have landed in LDS
+    __builtin_amdgcn_wave_barrier();
+    p = 0;
+    for (uint32_t k = 0; k < take; ++k) {
+      const unsigned long long out_rec = rl64(m.out_rec, k), key0 = rl64(m.key0, k);
+      const long long src = (long long)rl64((unsigned long long)m.src_pos, k);
+      const uint32_t first_ord = rl(m.first_ord, k), nkeys = rl(m.nkeys, k);
+      const long long pik = (long long)rl64((unsigned long long)mk.pik, k);
+      const long long k0 = (long long)rl64((unsigned long long)mk.k0, k), k1 = (long long)rl64((unsigned long long)mk.k1, k);
+      const uint32_t o0 = rl(mk.o0, k), o1 = rl(mk.o1, k);
+      const uint32_t jb = k == 0 ? j0 : 0u;
+      const uint32_t nk = k == 0 ? first : rl(cnt, k);
+      auto wkey = [&](uint32_t ord) -> long long {
+        if (ord == NONE) return -1;
+        if (nkeys && ord >= first_ord) return L.pbits + (long long)(key0 + (uint16_t)(ord - first_ord));
+        if (ord == 0) return pik;
+        if (ord == o0) return k0;
+        if (ord == o1) return k1;
+        long long key = 0;  // (a third older ordinal: the key chain in memory)
+        key_of(L, first_ord == 0 ? 0xFFFFFFFFu : rl(m.prev, k), rl(m.instance, k), ord, key);
+        return key;
+      };
+      unsigned long long pos = k == 0 && j0 ? gpos : rl64(mb, k);
+      unsigned long long gs = pos, sb = pos & ~15ull;
+      for (uint32_t i = 0; i < nk; ++i) {
+        const uint32_t info = lri[p + i];
+        const uint32_t size = info & 0xFFFF;
+        if (info & kSlow) {  // composed by k_log_compose
+          stream_flush(out, stage, sb, gs, pos, lane);
+          pos += size;
+          gs = pos;
+          sb = pos & ~15ull;
+          continue;
+        }
+        if (pos + size - sb > kStreamStage) {
+          stream_flush(out, stage, sb, gs, pos, lane);
+          gs = pos;
+          sb = pos & ~15ull;
+        }
+        const uint32_t rx = lrow[2 * (p + i)];
+        const uint4 d = desc[(info >> 16) - 1];
+        const long long key = wkey(rx & 0xFFFF), scope = wkey(rx >> 16);
+        const long long lpos = L.first_position + (long long)(out_rec + jb + i);
+        const uint32_t so = (uint32_t)(pos - sb);
+        unsigned long long* const s64 = reinterpret_cast<unsigned long long*>(stage + so);
+        if (lane < size / 8) s64[lane] = reinterpret_cast<const unsigned long long*>(lds + d.x)[lane];
+        if (lane < 4)  // LogEntryDescriptor: position, source position, key, timestamp
+          s64[2 + lane] = lane == 0 ? (unsigned long long)lpos : lane == 1 ? (unsigned long long)src
+                          : lane == 2 ? (unsigned long long)key : ts;
+        if (lane < 16) {  // msgpack uint64 (big-endian) processInstanceKey / scope key
+          const bool sc = lane >= 8;
+          const uint32_t at = sc ? d.z : d.y >> 16;
+          const unsigned long long x = (unsigned long long)(sc ? scope : pik);
+          if (at) stage[so + at + (lane & 7)] = (uint8_t)(x >> (56 - 8 * (lane & 7)));
+        }
+        pos += size;
+      }
+      stream_flush(out, stage, sb, gs, pos, lane);
+      p += nk;
+      gpos = pos;
+    }
+    if (partial) {
+      j0 += first;
+      if (j0 >= rl(m.nrec, 0)) {
+        ++c;
+        j0 = 0;
+      }
+    } else {
+      c += take;
+      j0 = 0;
+    }
+  }
+}
+
 // pass 2b (flag bit 1 only): the entries without a template, composed by their command's lane
 __global__ __launch_bounds__(256) void k_log_compose(LogParams L) {
   extern __shared__ uint32_t tables[];
@@ -957,7 +1157,7 @@ __global__ __launch_bounds__(kLogScanB) void k_table_block_sums(const uint2* hdr
 __global__ __launch_bounds__(kLogScanB) void k_table_build(LogParams L, const uint2* hdr, const zbhip_command* cmds,
                                                           const long long* src_pos, unsigned long long key_base,
                                                           const unsigned long long* bs, LogCmd* out,
-                                                          uint16_t* inst_proc) {
+                                                          uint16_t* inst_proc, uint4* jrn) {
   const uint32_t i = blockIdx.x * kLogScanB + threadIdx.x;
   __shared__ unsigned long long ws[kLogScanB / 64];
   const uint2 h = i < L.n ? hdr[i] : make_uint2(0, 0);
@@ -990,6 +1190,12 @@ __global__ __launch_bounds__(kLogScanB) void k_table_build(LogParams L, const ui
   out[i] = m;
   // a CREATE starts its slot's instance (one command per instance in a one-round window)
   if (cm.kind == ZBHIP_CMD_CREATE && cm.instance < L.n_inst) inst_proc[cm.instance] = cm.ref;
+  // the window's key bookkeeping journal (runtime.cpp fold_journal): first key, its ordinal, the
+  // instance and whether the batch ended it, the key count and a CREATE's process
+  if (jrn)
+    jrn[i] = make_uint4((uint32_t)m.key0, ((uint32_t)(m.key0 >> 32) & 0xFFFFu) | (uint32_t)m.first_ord << 16,
+                        cm.instance | (h.y & HDR_ENDED), (uint32_t)m.nkeys |
+                        (uint32_t)(cm.kind == ZBHIP_CMD_CREATE ? cm.ref : 0xFFFFu) << 16);
 }
 
 // ring fill after the window: CREATEs reset their instance (a new generation), then every command
@@ -1018,7 +1224,8 @@ __global__ __launch_bounds__(256) void k_ring_add(LogParams L) {
 hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
   LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.arena_words, a.idx_words, a.docs, a.n_docs, a.inst_proc, a.ring,
               a.kpi, a.n_inst, a.pbits, a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]},
-              a.bytes, a.out, a.flag, a.now_ms, a.cmd_due, a.tpl, a.tpl_desc, a.tpl_idx, a.rinfo, a.out_cap};
+              a.bytes, a.out, a.flag, a.now_ms, a.cmd_due, a.tpl, a.tpl_desc, a.tpl_idx, a.rinfo, a.out_cap,
+              a.wkeys, a.tpl_lds};
   const uint32_t g = (a.n + 255) / 256;
   const size_t lds = a.arena_words + a.idx_words <= kLdsTableWords ? (size_t)(a.arena_words + a.idx_words) * 4 : 0;
   if (a.phase == 0) {  // sizes and byte offsets
@@ -1033,12 +1240,33 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
     hipLaunchKernelGGL(k_log_scan_sums, dim3(1), dim3(kLogScanB), 0, s, a.table_sums, nb, a.table_sums + nb);
     if (a.n)
       hipLaunchKernelGGL(k_table_build, dim3(nb), dim3(kLogScanB), 0, s, L, a.hdr, a.wcmds, a.src_pos, a.key_base,
-                         a.table_sums, a.table, a.inst_proc_w);
+                         a.table_sums, a.table, a.inst_proc_w, a.jrn);
   } else if (a.phase == 1) {
-    // k_log_write reads no serialiser table: LDS holds the half waves' entry slots and stages
-    if (a.n && a.compose != 2)
+    // k_log_stream when the templates fit LDS beside the waves' stages (k_log_write otherwise: it
+    // reads them from memory)
+    const size_t slds = (size_t)((a.tpl_lds + 15u) & ~15u) + (size_t)kStreamWaves * kStreamWaveLds;
+    static int cus = 0;
+    static bool stream_ok = true;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus <= 0)
+        cus = 256;
+      stream_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(k_log_stream), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kStreamLdsMax) == hipSuccess;
+      (void)hipGetLastError();
+    }
+    const bool stream = stream_ok && a.wkeys && a.tpl_lds && slds <= kStreamLdsMax && !getenv("ZBHIP_LOG_HALFWAVE");
+    if (a.n && a.compose != 2 && stream) {
+      const uint32_t per_cu = (uint32_t)(kStreamLdsMax / slds) < 4 ? (uint32_t)(kStreamLdsMax / slds) : 4u;
+      uint32_t grid = (uint32_t)cus * per_cu;
+      const uint32_t need = (a.n + kStreamWaves * 16 - 1) / (kStreamWaves * 16);  // >= 16 commands per wave
+      if (need < grid) grid = need;
+      hipLaunchKernelGGL(k_log_stream, dim3(grid), dim3(kStreamWaves * 64), slds, s, L);
+    } else if (a.n && a.compose != 2) {
       hipLaunchKernelGGL(k_log_write, dim3((a.n + kLogWriteB - 1) / kLogWriteB), dim3(kLogWriteB),
                          (size_t)(kLogWriteB / kHalf) * kStageAlloc, s, L, 0u);
+    }
     if (a.n && a.compose) hipLaunchKernelGGL(k_log_compose, dim3(g), dim3(256), lds, s, L);
   } else {
     if (a.n) hipLaunchKernelGGL(k_ring_create, dim3(g), dim3(256), 0, s, L);

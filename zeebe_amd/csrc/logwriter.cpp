@@ -116,6 +116,7 @@ struct SerElement {
   // JobRecord of a service task: [map .. customHeaders, "variables"] bin(doc) [errorMessage ..
   // processDefinitionKey, "processInstanceKey"] key ["elementId" .. "elementInstanceKey"] key [tenantId]
   Bytes job_head, job_mid, job_tail;
+  size_t job_rest = 0;  // job_head after its deadline and worker entries
 };
 struct SerProcess {
   std::string bpmn_id;
@@ -227,6 +228,7 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
       mp_int(S.job_head, -1);
       key(S.job_head, "worker");
       key(S.job_head, "");
+      S.job_rest = S.job_head.size();
       key(S.job_head, "retries");
       mp_int(S.job_head, (int32_t)E.job_retries);
       key(S.job_head, "retryBackoff");
@@ -433,7 +435,17 @@ extern "C" int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs
           key(value, "tenantId"); key(value, kTenant);
         } else {
           if (!E || E->job_head.empty()) return ZBHIP_EINVAL;
-          value += E->job_head;
+          if (r.message_key != -1) {  // an ACTIVATED job: the deadline and worker it was activated with
+            if (r.correlation_key != ZBHIP_NO_STRING && r.correlation_key >= s->strs.size()) return ZBHIP_EINVAL;
+            mp_map(value, 17);
+            key(value, "deadline");
+            mp_int(value, r.message_key);
+            key(value, "worker");
+            mp_str(value, r.correlation_key == ZBHIP_NO_STRING ? std::string() : s->strs[r.correlation_key]);
+            value.append(E->job_head, E->job_rest, std::string::npos);
+          } else {
+            value += E->job_head;
+          }
           mp_bin(value, r.intent == ZBHIP_JOB_COMPLETED ? src_doc : kEmptyDoc);
           value += E->job_mid;
           mp_int(value, r.process_instance_key);

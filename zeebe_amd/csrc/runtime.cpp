@@ -25,6 +25,9 @@
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
+#include <deque>
+#include <iterator>
+#include <new>
 #include <vector>
 
 #include "zb_internal.h"
@@ -281,6 +284,55 @@ struct BatchRef {
   BatchRef(int64_t b, uint32_t i, uint16_t f, uint16_t n, uint32_t g) : base(b), inst(i), first_ord(f), nkeys(n), gen(g) {}
 };
 
+// A std::vector-like buffer in pinned host memory: the window's commands are uploaded from it by
+// DMA, without the driver's synchronous staging of a pageable source.  (Trivially copyable T; grows
+// by reallocation, new elements zeroed as std::vector value-initialises them.)
+template <class T>
+struct PinnedVec {
+  T* p = nullptr;
+  size_t n = 0, cap = 0;
+  PinnedVec() = default;
+  PinnedVec(const PinnedVec&) = delete;
+  PinnedVec& operator=(const PinnedVec&) = delete;
+  ~PinnedVec() {
+    if (p) (void)hipHostFree(p);
+  }
+  void reserve(size_t c) {
+    if (c <= cap) return;
+    const size_t nc = std::max(c, cap * 2);
+    T* q = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&q), nc * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+    if (n) memcpy(q, p, n * sizeof(T));
+    if (p) (void)hipHostFree(p);
+    p = q;
+    cap = nc;
+  }
+  void resize(size_t m) {
+    reserve(m);
+    if (m > n) memset(static_cast<void*>(p + n), 0, (m - n) * sizeof(T));
+    n = m;
+  }
+  void clear() { n = 0; }
+  template <class It>
+  void insert(T* at, It first, It last) {  // (appending only)
+    const size_t k = (size_t)std::distance(first, last);
+    (void)at;
+    reserve(n + k);
+    std::copy(first, last, p + n);
+    n += k;
+  }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  T* begin() { return p; }
+  T* end() { return p + n; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+};
+
 // The resolve_key table: BatchRefs in key order, in segments (one per plain window, or appended
 // entries), so appending 10^6 entries never moves the older ones and a compaction runs segment by
 // segment on host threads.  Lookup: the segment by its first key, then within it.
@@ -485,7 +537,7 @@ struct zbhip_handle {
   bool external = false;
   const uint4* ext_cmds = nullptr;
   const zbhip_doc_entry* ext_docs = nullptr;
-  std::vector<zbhip_command> h_cmds;
+  PinnedVec<zbhip_command> h_cmds;  // (pinned: the upload source of host windows)
   std::vector<zbhip_doc_entry> h_docs;
   size_t n_cmds = 0, n_docs = 0;
   std::vector<uint32_t> round_begin;
@@ -498,6 +550,7 @@ struct zbhip_handle {
   std::vector<uint2> h_hdr;
   std::vector<uint2> h_out;
   std::vector<uint64_t> h_off;  // record offset of each command in h_out
+  bool off_ready = false;       // h_off is the last run's (compute_offsets)
   size_t out_total = 0;         // records of the last run (in d_rec; in h_out once out_host)
   bool out_host = false;
   size_t drain_cmd = 0, drain_rec = 0, drain_ord = 0;
@@ -531,6 +584,21 @@ struct zbhip_handle {
   std::vector<std::vector<std::pair<uint16_t, int64_t>>> hist;
   std::vector<uint16_t> inst_proc;
   KeyTable batches;
+  // Windows whose key bookkeeping stayed on the device (zbhip_serialize_log_device over a
+  // device-built command table): k_table_build journals each command's first key, ordinal, key
+  // count, instance, end and CREATE process in HBM (16 B per command), and the host tables above are
+  // brought up to date from the journal (fold_journal) only when a host consumer reads them -- a
+  // drain, resolve_key, an export, job activation, a host-built window -- or the journal is full.
+  struct JournalWindow {
+    uint32_t slot;
+    size_t n;
+    uint64_t window;  // windows_run of the window
+  };
+  uint4* d_jrn = nullptr;
+  uint32_t jrn_slots = 0;
+  uint32_t jrn_next = 0;
+  std::deque<JournalWindow> jrn_q;
+  std::vector<uint4> jrn_host;
 
   // ---- log bytes on the device (zbhip_serialize_log_device, logdev.hip) ----
   uint8_t* d_log_arena = nullptr;   // the serialiser's constant byte runs
@@ -555,6 +623,7 @@ struct zbhip_handle {
   size_t log_out_cap = 0;
   uint32_t* d_log_flag = nullptr;
   uint32_t* d_log_rinfo = nullptr;  // [rows] per record: template / composed, entry bytes
+  LogKeys* d_log_wkeys = nullptr;   // [max_commands] older keys per command (size pass -> write pass)
   std::vector<LogCmd> h_logcmd;
   std::vector<uint64_t> log_prev;   // per instance: window | last command of the window (prev chain)
   uint64_t windows_run = 0;         // zbhip_run calls
@@ -571,6 +640,7 @@ struct zbhip_handle {
     int64_t deadline;
     std::string worker;
     uint32_t inst;
+    uint32_t worker_id;  // the worker in the value dictionary (ZBHIP_NO_STRING: empty)
   };
   std::unordered_map<int64_t, Activation> activated;  // ACTIVATED jobs: deadline, worker
   std::vector<int64_t> completed_activated;           // completed in the last window (dropped next)
@@ -659,6 +729,7 @@ struct zbhip_handle {
   } while (0)
 
 static int finalize(zbhip_handle* h);
+static int settle(zbhip_handle* h);
 
 extern "C" {
 
@@ -825,6 +896,8 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_log_out);
   (void)hipFree(h->d_log_flag);
   (void)hipFree(h->d_log_rinfo);
+  (void)hipFree(h->d_log_wkeys);
+  (void)hipFree(h->d_jrn);
   if (h->inst_proc_pin) (void)hipHostFree(h->inst_proc_pin);
   if (h->src_pos_pin) (void)hipHostFree(h->src_pos_pin);
   (void)hipFree(h->d_check_flag);
@@ -1482,7 +1555,7 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   const bool dbg = h->debug;
   auto now = [] { return std::chrono::steady_clock::now(); };
   const auto t0 = now();
-  int rc = finalize(h);  // the previous window's keys are fixed before its commands are replaced
+  int rc = settle(h);  // the previous window's keys are fixed before its commands are replaced
   if (rc) return rc;
   const auto t1 = now();
   // validation, then the host copy, on the worker threads by ranges (a refused window leaves the
@@ -1556,12 +1629,13 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
     cmds = h->h_cmds.data();
   }
   h->window_continues = continues;
-  if (n) HIPCHK(hipMemcpyAsync(h->d_cmds, cmds, n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
+  if (n) HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
   if (n_docs)
     HIPCHK(hipMemcpyAsync(h->d_docs, docs, n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice, h->stream));
   if (!h->h_order.empty())
     HIPCHK(hipMemcpyAsync(h->d_order, h->h_order.data(), n * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  // (no wait: the pageable sources are staged by the driver before these calls return, and the pinned
+  // h_cmds is rewritten only by the next submit, after the run that waits for this upload)
   h->ran = false;
   h->results = false;
   if (dbg) {
@@ -1611,7 +1685,7 @@ int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_
                            size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts) {
   if (!h || (n && !dev_cmds)) return ZBHIP_EINVAL;
   if (n > h->rec_slots) return ZBHIP_ENOMEM;
-  if (int rc0 = finalize(h)) return rc0;
+  if (int rc0 = settle(h)) return rc0;
   bool replanned = false;
   const int rc = check_device_window(h, dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, &replanned);
   if (rc || replanned) return rc;
@@ -1646,8 +1720,49 @@ static hipEvent_t next_event(zbhip_handle* h) {
   return h->tev[h->tev_used++];
 }
 
+// record offset of every command of the last run in the gathered records: regions follow launch
+// order, lanes follow the launch order
+static int compute_offsets(zbhip_handle* h) {
+  if (h->off_ready) return ZBHIP_OK;
+  const uint32_t n = (uint32_t)h->n_cmds;
+  const uint64_t total = h->out_total;
+  h->h_off.resize(n + 1);
+  uint64_t off = 0;
+  if (h->launches.size() == 1 && h->launches[0].src == 0 && n >= (1u << 16)) {
+    // one launch in log order: a prefix sum of the record counts, by ranges on host threads
+    const unsigned T = host_threads();
+    std::vector<uint64_t> part(T + 1, 0);
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      uint64_t sum = 0;
+      for (size_t c = (size_t)n * t / TT; c < (size_t)n * (t + 1) / TT; ++c) sum += h->h_hdr[c].x & 0xFFFF;
+      part[t + 1] = sum;
+    });
+    for (unsigned t = 0; t < T; ++t) part[t + 1] += part[t];
+    parallel_for(T, [&](unsigned t, unsigned TT) {
+      uint64_t o = part[t];
+      for (size_t c = (size_t)n * t / TT; c < (size_t)n * (t + 1) / TT; ++c) {
+        h->h_off[c] = o;
+        o += h->h_hdr[c].x & 0xFFFF;
+      }
+    });
+    off = part[T];
+  } else {
+    for (const auto& l : h->launches)
+      for (uint32_t k = 0; k < l.count; ++k) {
+        const uint32_t c = l.src == 0 ? l.first + k : l.src == 1 ? h->h_order[l.first + k] : h->cont_order[l.first + k];
+        h->h_off[c] = off;
+        off += h->h_hdr[c].x & 0xFFFF;
+      }
+  }
+  h->h_off[n] = 0;
+  if (off != total) return ZBHIP_EDEVICE;
+  h->off_ready = true;
+  return ZBHIP_OK;
+}
+
 // the last run's records in host memory (ZBHIP_RUN_DEVICE_RECORDS left them in HBM)
 static int ensure_out(zbhip_handle* h) {
+  if (int rc = compute_offsets(h)) return rc;
   if (h->out_host) return ZBHIP_OK;
   h->h_out.resize(h->out_total);
   if (h->out_total)
@@ -1781,6 +1896,79 @@ static void advance_window_parallel(zbhip_handle* h) {
   h->fin_next = n;
 }
 
+// One journaled window into the host tables (the per-instance histories, processes and generations,
+// and a resolve-table segment), as advance_window_parallel books a one-round window: each command
+// is the only one of its instance, so ranges of commands go to host threads.  The current window's
+// key bases are set too.
+static void fold_journal(zbhip_handle* h, const uint4* e, size_t n, bool current) {
+  const unsigned T = host_threads();
+  const uint32_t N = h->cfg.max_instances;
+  auto range = [n](unsigned t, unsigned TT) { return std::make_pair(n * t / TT, n * (t + 1) / TT); };
+  auto has_entry = [N](const uint4& x) { return (x.w & 0xFFFF) != 0 && (x.z & 0x7FFFFFFFu) < N; };
+  std::vector<size_t> bbase(T + 1, 0);
+  parallel_for(T, [&](unsigned t, unsigned TT) {
+    size_t b = 0;
+    const auto [lo, hi] = range(t, TT);
+    for (size_t c = lo; c < hi; ++c) b += has_entry(e[c]);
+    bbase[t + 1] = b;
+  });
+  for (unsigned t = 0; t < T; ++t) bbase[t + 1] += bbase[t];
+  BatchRef* const tbl = h->batches.append_segment(bbase[T]);
+  if (current) h->h_base.resize(std::max(h->h_base.size(), n));
+  parallel_for(T, [&](unsigned t, unsigned TT) {
+    size_t nb = bbase[t], dead = 0;
+    const auto [lo, hi] = range(t, TT);
+    for (size_t c = lo; c < hi; ++c) {
+      const uint4 x = e[c];
+      const int64_t base = (int64_t)((uint64_t)x.x | (uint64_t)(x.y & 0xFFFF) << 32);
+      const uint16_t first = (uint16_t)(x.y >> 16), nkeys = (uint16_t)(x.w & 0xFFFF), proc = (uint16_t)(x.w >> 16);
+      const uint32_t inst = x.z & 0x7FFFFFFFu;
+      if (current) h->h_base[c] = base - 1;
+      if (inst >= N) continue;
+      if (proc != 0xFFFF) {  // a CREATE: a new instance in the slot, its own key history
+        h->hist[inst].clear();
+        h->inst_proc[inst] = proc;
+        ++h->inst_gen[inst];
+      }
+      if (nkeys) {
+        h->hist[inst].push_back({first, base});
+        tbl[nb++] = {base, inst, first, nkeys, h->inst_gen[inst]};
+      }
+      if (x.z >> 31) {  // the batch ended the instance: its keys no longer resolve
+        ++h->inst_gen[inst];
+        dead += h->hist[inst].size();
+      }
+    }
+    h->batches_dead.fetch_add(dead, std::memory_order_relaxed);
+  });
+  if (h->batches.size() >= 2 * h->batches_compacted + (1u << 20) && 3 * h->batches_dead.load() >= h->batches.size()) {
+    h->batches.compact([h](const BatchRef& b) { return b.gen == h->inst_gen[b.inst]; });
+    h->batches_compacted = h->batches.size();
+    h->batches_dead = 0;
+  }
+}
+
+// every journaled window into the host tables, oldest first (keep: windows left journaled)
+static int fold_journals(zbhip_handle* h, size_t keep = 0) {
+  if (h->jrn_q.size() <= keep) return ZBHIP_OK;
+  const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
+  if (h->hist.size() < subjects) {
+    h->hist.resize(subjects);
+    h->inst_gen.resize(subjects, 0);
+  }
+  if (h->inst_proc.size() < h->cfg.max_instances) h->inst_proc.resize(h->cfg.max_instances, NONE);
+  while (h->jrn_q.size() > keep) {
+    const zbhip_handle::JournalWindow j = h->jrn_q.front();
+    h->jrn_host.resize(j.n);
+    if (j.n)
+      HIPCHK(hipMemcpy(h->jrn_host.data(), h->d_jrn + (size_t)j.slot * h->cfg.max_commands, j.n * sizeof(uint4),
+                       hipMemcpyDeviceToHost));
+    fold_journal(h, h->jrn_host.data(), j.n, h->results && j.window == h->windows_run);
+    h->jrn_q.pop_front();
+  }
+  return ZBHIP_OK;
+}
+
 // Key relabelling bookkeeping of the last run, in log (source) order: each command's first key
 // (DbKeyGenerator order), the subjects' key histories and the resolve_key table.  It advances
 // lazily, command by command: up to `limit`, and never past a fallback command whose CPU-engine keys
@@ -1788,6 +1976,7 @@ static void advance_window_parallel(zbhip_handle* h) {
 // adapter can hand a fallback instance over (its earlier commands' keys are fixed) and declare the
 // keys the CPU engine generated before the keys of the window's later commands are fixed.
 static int advance(zbhip_handle* h, size_t limit, bool force) {
+  if (int rc = fold_journals(h)) return rc;
   if (!h->results || h->fin_next >= h->n_cmds) return ZBHIP_OK;
   if (h->fin_next == 0) {  // a new window: jobs completed in the previous one are gone
     for (int64_t k : h->completed_activated) h->activated.erase(k);
@@ -1872,6 +2061,13 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
 
 // the whole window (undeclared fallback commands generated no keys)
 static int finalize(zbhip_handle* h) { return advance(h, ~(size_t)0, true); }
+
+// before a new window replaces the last one's commands: its keys fixed -- booked here, or journaled
+// on the device (left there)
+static int settle(zbhip_handle* h) {
+  if (!h->results || h->fin_next >= h->n_cmds) return ZBHIP_OK;
+  return finalize(h);
+}
 
 int zbhip_set_clock(zbhip_handle* h, int64_t now_ms) {
   if (!h) return ZBHIP_EINVAL;
@@ -2176,37 +2372,11 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   }
   h->stats_dirty = true;
 
-  // record offset of every command: regions follow launch order, lanes follow the launch order
-  h->h_off.resize(n + 1);
-  uint64_t off = 0;
-  if (h->launches.size() == 1 && h->launches[0].src == 0 && n >= (1u << 16)) {
-    // one launch in log order: a prefix sum of the record counts, by ranges on host threads
-    const unsigned T = host_threads();
-    std::vector<uint64_t> part(T + 1, 0);
-    parallel_for(T, [&](unsigned t, unsigned TT) {
-      uint64_t sum = 0;
-      for (size_t c = (size_t)n * t / TT; c < (size_t)n * (t + 1) / TT; ++c) sum += h->h_hdr[c].x & 0xFFFF;
-      part[t + 1] = sum;
-    });
-    for (unsigned t = 0; t < T; ++t) part[t + 1] += part[t];
-    parallel_for(T, [&](unsigned t, unsigned TT) {
-      uint64_t o = part[t];
-      for (size_t c = (size_t)n * t / TT; c < (size_t)n * (t + 1) / TT; ++c) {
-        h->h_off[c] = o;
-        o += h->h_hdr[c].x & 0xFFFF;
-      }
-    });
-    off = part[T];
-  } else {
-    for (const auto& l : h->launches)
-      for (uint32_t k = 0; k < l.count; ++k) {
-        const uint32_t c = l.src == 0 ? l.first + k : l.src == 1 ? h->h_order[l.first + k] : h->cont_order[l.first + k];
-        h->h_off[c] = off;
-        off += h->h_hdr[c].x & 0xFFFF;
-      }
-  }
-  h->h_off[n] = 0;
-  if (off != total) return ZBHIP_EDEVICE;
+  // record offset of every command (the host needs them to read records; with the records left in
+  // HBM they are computed when a host reader first asks)
+  h->off_ready = false;
+  if (!(flags & ZBHIP_RUN_DEVICE_RECORDS))
+    if (int rc = compute_offsets(h)) return rc;
   if (h->debug) {
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     fprintf(stderr, "[zbhip] run n=%u: kernels + headers + gather %.2f ms, records copy + offsets %.2f ms\n", n,
@@ -2345,6 +2515,14 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
                  : c6 == C_JOB_CANCELED ? ZBHIP_JOB_CANCELED : ZBHIP_JOB_COMPLETE;
       r.record_type = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
       if (c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE) r.aux = doc;
+      if (!rej && (fl & 1u) && (c6 == C_JOB_COMPLETED || c6 == C_JOB_CANCELED)) {
+        // the stored job of an ACTIVATED job: its deadline and worker (DbJobState.activate)
+        auto it = h->activated.find(r.key);
+        if (it != h->activated.end()) {
+          r.message_key = it->second.deadline;
+          r.correlation_key = it->second.worker_id;
+        }
+      }
     } else if (c6 == C_VAR_CREATED || c6 == C_VAR_UPDATED) {
       r.value_type = ZBHIP_VT_VARIABLE;
       r.intent = c6 == C_VAR_CREATED ? ZBHIP_VAR_CREATED : ZBHIP_VAR_UPDATED;
@@ -3640,7 +3818,12 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   h->published |= stats_row;
   for (const Done& d : done)
     for (int64_t k : d.keys)
-      if (job_activated_state.count(k)) h->activated[k] = {job_act[k].first, job_act[k].second, d.slot};
+      if (job_activated_state.count(k)) {
+        const std::string& wk = job_act[k].second;
+        const int64_t wid = wk.empty() ? (int64_t)ZBHIP_NO_STRING : zbhip_intern_string(h, wk.data(), wk.size());
+        if (wid < 0) return (int)wid;
+        h->activated[k] = {job_act[k].first, wk, d.slot, (uint32_t)wid};
+      }
   h->job_index_on = false;  // rebuilt from the device rows at the next activation
   if (n_instances) *n_instances = (uint32_t)done.size();
   return ZBHIP_OK;
@@ -3804,6 +3987,10 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
   }
   if (!h->job_index_on)
     if (int rc = build_job_index(h)) return rc;
+  // the worker into the value dictionary: the activated jobs' records name it
+  const int64_t worker_wid = cmd->worker_len ? zbhip_intern_string(h, cmd->worker, cmd->worker_len) : (int64_t)ZBHIP_NO_STRING;
+  if (worker_wid < 0) return (int)worker_wid;
+  const uint32_t worker_id = (uint32_t)worker_wid;
   res->key = ((int64_t)h->cfg.partition_id << 51) + ++h->key_counter;  // keyGenerator.nextKey
   if (h->st.n_slots) {
     const unsigned long long kc = (unsigned long long)h->key_counter;
@@ -3919,7 +4106,7 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     }
     // JobBatchActivatedApplier -> DbJobState.activate: ACTIVATED, out of JOB_ACTIVATABLE, deadline
     h->job_index.erase({tit->second, j.key});
-    h->activated[j.key] = {j.deadline, worker, inst};
+    h->activated[j.key] = {j.deadline, worker, inst, worker_id};
   }
   return ZBHIP_OK;
 }
@@ -4040,7 +4227,8 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
         dalloc(&h->d_log_bytes, (size_t)h->cfg.max_commands + 1 + ((size_t)h->cfg.max_commands + 1023) / 1024 + 1) != hipSuccess ||
         dalloc(&h->d_log_flag, 1) != hipSuccess || dalloc(&h->d_src_pos, (size_t)h->cfg.max_commands) != hipSuccess ||
         dalloc(&h->d_tbl_sums, ((size_t)h->cfg.max_commands + 1023) / 1024 + 2) != hipSuccess ||
-        dalloc(&h->d_log_rinfo, ((size_t)h->cfg.max_commands + 64) * h->rec_cap) != hipSuccess)
+        dalloc(&h->d_log_rinfo, ((size_t)h->cfg.max_commands + 64) * h->rec_cap) != hipSuccess ||
+        dalloc(&h->d_log_wkeys, (size_t)h->cfg.max_commands) != hipSuccess)
       return ZBHIP_ENOMEM;
     HIPCHK(hipMemsetAsync(h->d_ring, 0, words * sizeof(unsigned long long), h->stream));
   }
@@ -4071,16 +4259,37 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   a.now_ms = h->run_clock_ms;
   a.cmd_due = h->d_cmd_due;
   a.rinfo = h->d_log_rinfo;
+  a.wkeys = h->d_log_wkeys;
+  a.tpl_lds = (uint32_t)h->log_tpl_idx_off;
   unsigned long long total = 0;
   uint32_t flag = 0;
   auto tu = now(), tf = now();
   bool spec = false;  // k_log_write launched before the total was known
+  // the window's key bookkeeping journaled on the device (fold_journal) instead of booked here
+  bool journal = dev_table && !h->job_index_on && !h->msg() && !getenv("ZBHIP_NO_JOURNAL");
+  uint32_t jslot = 0;
+  if (journal && !h->d_jrn) {
+    const char* e = getenv("ZBHIP_JOURNAL_WINDOWS");
+    const size_t per = (size_t)h->cfg.max_commands * sizeof(uint4);
+    size_t slots = e ? (size_t)atoi(e) : 64;
+    slots = std::min<size_t>(slots, std::max<size_t>(1, ((size_t)2 << 30) / std::max<size_t>(per, 1)));
+    if (slots && dalloc(&h->d_jrn, slots * h->cfg.max_commands) == hipSuccess) h->jrn_slots = (uint32_t)slots;
+  }
+  if (journal && !h->jrn_slots) journal = false;
+  if (journal) {
+    if (h->jrn_q.size() >= h->jrn_slots)  // full: the oldest window into the host tables
+      if (int rc = fold_journals(h, h->jrn_slots - 1)) return rc;
+    jslot = h->jrn_next;
+    h->jrn_next = (h->jrn_next + 1) % h->jrn_slots;
+  }
+  unsigned long long tbl_total = 0;  // the device table's scan total: records | keys << 32
   if (dev_table) {
-    // the instances' processes before this window (the table kernel adds this window's CREATEs);
-    // a copy, since finalize updates inst_proc while the upload may still read it
-    // (through pinned staging filled on the host threads: a pageable upload is copied by the driver
-    // through its own bounce buffers, synchronously and with stalls of tens of ms per window)
-    if (h->inst_proc.size() >= N) {
+    // the instances' processes before this window (the table kernel adds this window's CREATEs),
+    // from the host tables -- unless windows are journaled: then the device's copy is the current one
+    // (a copy, since finalize updates inst_proc while the upload may still read it, through pinned
+    // staging filled on the host threads: a pageable upload is copied by the driver through its own
+    // bounce buffers, synchronously and with stalls of tens of ms per window)
+    if (h->jrn_q.empty() && h->inst_proc.size() >= N) {
       if (h->inst_proc_pin_cap < N) {
         if (h->inst_proc_pin) (void)hipHostFree(h->inst_proc_pin);
         h->inst_proc_pin = nullptr;
@@ -4117,8 +4326,12 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
     a.table = h->d_logcmd;
     a.table_sums = h->d_tbl_sums;
     a.inst_proc_w = h->d_inst_proc;
+    a.jrn = journal ? h->d_jrn + (size_t)jslot * h->cfg.max_commands : nullptr;
     a.phase = 3;
     HIPCHK(launch_log_device(a, h->stream));
+    a.jrn = nullptr;
+    const size_t nb = (n + 1023) / 1024;  // (logdev.hip kLogScanB)
+    HIPCHK(hipMemcpyAsync(&tbl_total, h->d_tbl_sums + nb, sizeof tbl_total, hipMemcpyDeviceToHost, h->stream));
     a.phase = 0;
     HIPCHK(launch_log_device(a, h->stream));
     HIPCHK(hipMemcpyAsync(&total, h->d_log_bytes + n, sizeof total, hipMemcpyDeviceToHost, h->stream));
@@ -4134,19 +4347,29 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
       HIPCHK(launch_log_device(a, h->stream));
       spec = true;
     }
-    // meanwhile on the host: the window's key relabelling bookkeeping (the same key bases)
-    if (int rc = finalize(h)) {
-      (void)hipStreamSynchronize(h->stream);
-      return rc;
+    if (journal) {
+      tf = now();
+      HIPCHK(hipStreamSynchronize(h->stream));
+      h->key_counter = (int64_t)key_base + (int64_t)(tbl_total >> 32);
+      h->fin_next = n;
+      h->jrn_q.push_back({jslot, n, h->windows_run});
+    } else {
+      // meanwhile on the host: the window's key relabelling bookkeeping (the same key bases)
+      if (int rc = finalize(h)) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
+      }
+      if (h->h_base[0] + 1 != (int64_t)key_base + 1 || h->key_counter < (int64_t)key_base) return ZBHIP_EDEVICE;
+      tf = now();
+      HIPCHK(hipStreamSynchronize(h->stream));
+      if (h->key_counter != (int64_t)key_base + (int64_t)(tbl_total >> 32)) return ZBHIP_EDEVICE;
     }
-    if (h->h_base[0] + 1 != (int64_t)key_base + 1 || h->key_counter < (int64_t)key_base) return ZBHIP_EDEVICE;
-    tf = now();
-    HIPCHK(hipStreamSynchronize(h->stream));
   }
   const auto t2 = now();
   // the window's command table: rows, record positions, key bases, the prev chain per instance
   // (a window of one round has one command per instance: no chain, and it is filled on host threads)
   if (!dev_table) {
+  if (int rc = compute_offsets(h)) return rc;
   h->h_logcmd.resize(n);
   if (h->log_prev.size() < N) h->log_prev.assign(N, ~0ull);
   const uint64_t win = h->windows_run;
@@ -4238,8 +4461,10 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   }
   a.phase = 2;  // the window's keys into the ring, in any case
   HIPCHK(launch_log_device(a, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  // (no wait: the bytes are complete in the handle's stream order -- zbhip_log_device_copy and the
+  // next window's run wait for them, and the host meanwhile takes the next window)
   if (dbg) {
+    HIPCHK(hipStreamSynchronize(h->stream));
     const auto t4 = now();
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     fprintf(stderr, "[zbhip] serialize_log_device n=%zu (%s table): finalize %.2f ms, table %.2f ms (uploads %.2f, "

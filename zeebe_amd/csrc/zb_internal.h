@@ -278,6 +278,12 @@ struct LogCmd {
   uint32_t doc_begin;
   uint32_t pad;                // the command's pad (TIMER:TRIGGER: dueDate high word)
 };
+// the keys older than its own batch that a command's records name, found by the size pass for the
+// write pass: the process instance's (ordinal 0) and the last two others it looked up
+struct LogKeys {
+  long long pik, k0, k1;
+  uint32_t o0, o1;             // ordinals of k0 / k1 (NONE: empty)
+};
 struct LogLaunch {
   int phase;                   // 0 sizes + offsets, 1 write, 2 key ring, 3 command table
   const uint2* rows;
@@ -317,6 +323,9 @@ struct LogLaunch {
                                // 2: k_log_compose only (the write ran speculatively)
   unsigned long long out_cap;  // phase 1: bytes at `out` (0: unchecked); k_log_write does nothing when the
                                // window's total (bytes[n], from the scan) exceeds it
+  LogKeys* wkeys;              // [n] (phase 0 writes, phase 1 reads)
+  uint4* jrn;                  // phase 3: [n] the window's key bookkeeping journal (NULL: the host books it)
+  uint32_t tpl_lds;            // bytes of the templates and their descriptors (the `tpl` block up to tpl_idx)
 };
 
 }  // namespace zb

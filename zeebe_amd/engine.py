@@ -119,8 +119,9 @@ class Partition:
     def serialize_log_device(self, source_positions=None, first_position=1, timestamp=0, copy=True):
         """Log bytes of the last run's window written on the device (zbhip_serialize_log_device):
         the bytes `log_serializer().serialize(drain(), ...)` gives for the same window.  Returns the
-        bytes (copy=True) or (device pointer, size); raises ZbhipError(ZBHIP_EUNSUPP) when the window
-        needs the host serialiser."""
+        bytes (copy=True) or (device pointer, size) -- written in the handle's stream order
+        (zbhip_stream), so a reader on another stream waits on that one first; raises
+        ZbhipError(ZBHIP_EUNSUPP) when the window needs the host serialiser."""
         pos = np.ascontiguousarray(source_positions if source_positions is not None
                                    else np.arange(1, self._n_cmds + 1), dtype=np.int64)
         w = abi.LogWindow(None, self._n_cmds, 0, None, 0, 0, pos.ctypes.data, first_position, timestamp, None)
