@@ -414,6 +414,100 @@ static int64_t parse_duration_ms(std::string t) {
   return any ? ms : -1;
 }
 
+// The timer expressions of the subset, evaluated as ExpressionProcessor.evaluateIntervalExpression
+// (processing/common/ExpressionProcessor.java:142-175) does: a static text is a string; `=` starts a FEEL
+// expression whose constant value is a string ("..."), a day-time duration (duration("...") -- a
+// java.time.Duration, days of 24 h, turned into new Interval(duration)) or, for cycles, the string
+// FeelFunctionProvider.cycle (feel/.../FeelFunctionProvider.scala:23-47) builds, "R[n]/" + duration.
+// A string goes through Interval.parse (timeDuration) or RepeatingInterval.parse (timeCycle).
+struct TimerValue {
+  bool ok = false;
+  int64_t ms = -1;  // DURATION / the cycle's interval
+  int reps = 1;     // timeCycle: RepeatingInterval repetitions (-1 infinite)
+};
+static std::string strip(const std::string& t) {
+  size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+  return a == std::string::npos ? "" : t.substr(a, b - a + 1);
+}
+static int64_t parse_feel_daytime_ms(const std::string& t) {  // FEEL duration("P[nD][T[nH][nM][n[.f]S]]")
+  size_t d = t.find('D');
+  if (t.size() < 3 || t[0] != 'P' || t.find_first_of("YMW") < t.find('T')) return -1;
+  int64_t days = 0;
+  std::string rest = t;
+  if (d != std::string::npos && d < t.find('T')) {
+    const std::string n = t.substr(1, d - 1);
+    if (n.empty() || n.size() > 6 || n.find_first_not_of("0123456789") != std::string::npos) return -1;
+    days = atoll(n.c_str());
+    rest = "P" + t.substr(d + 1);
+    if (rest == "P") return days * 86400000LL;
+  }
+  const int64_t ms = parse_duration_ms(rest);
+  return ms < 0 ? -1 : ms + days * 86400000LL;
+}
+static bool feel_string(const std::string& e, std::string& v) {
+  if (e.size() < 2 || e.front() != '"' || e.back() != '"') return false;
+  v = e.substr(1, e.size() - 2);
+  return v.find('"') == std::string::npos && v.find('\\') == std::string::npos;
+}
+static bool feel_call(const std::string& e, const std::string& fn, std::vector<std::string>& args) {
+  if (e.compare(0, fn.size(), fn) != 0) return false;
+  const std::string r = strip(e.substr(fn.size()));
+  if (r.size() < 2 || r.front() != '(' || r.back() != ')') return false;
+  args.clear();
+  std::string cur;
+  int depth = 0;
+  for (char ch : r.substr(1, r.size() - 2)) {
+    if (ch == '(') ++depth;
+    if (ch == ')') --depth;
+    if (ch == ',' && depth == 0) { args.push_back(strip(cur)); cur.clear(); continue; }
+    cur += ch;
+  }
+  args.push_back(strip(cur));
+  return true;
+}
+static int repeating_reps(const std::string& n) {  // RepeatingInterval.parse: "R" [n] "/"
+  if (n.empty()) return -1;                         // INFINITE
+  if (n.size() > 3 || n.find_first_not_of("0123456789") != std::string::npos) return 0;
+  const int r = atoi(n.c_str());
+  return r >= 1 && r <= 254 ? r : 0;
+}
+static TimerValue timer_value(const std::string& text, bool cycle) {
+  TimerValue v;
+  std::string t = strip(text), str;
+  bool is_string = true;
+  if (!t.empty() && t[0] == '=') {
+    const std::string e = strip(t.substr(1));
+    std::vector<std::string> a;
+    if (feel_string(e, str)) {
+      t = str;
+    } else if (!cycle && feel_call(e, "duration", a) && a.size() == 1 && feel_string(a[0], str)) {
+      v.ms = parse_feel_daytime_ms(str);
+      is_string = false;
+    } else if (cycle && feel_call(e, "cycle", a) && (a.size() == 1 || a.size() == 2)) {
+      std::vector<std::string> d;
+      if (!feel_call(a.back(), "duration", d) || d.size() != 1 || !feel_string(d[0], str)) return v;
+      v.ms = parse_feel_daytime_ms(str);
+      v.reps = a.size() == 2 ? repeating_reps(a[0]) : -1;
+      v.ok = v.ms >= 0 && v.reps != 0;
+      return v;
+    } else {
+      return v;  // variables, other functions: outside the subset
+    }
+  }
+  if (is_string) {
+    if (cycle) {
+      const size_t slash = t.find('/');
+      if (t.size() < 3 || t[0] != 'R' || slash == std::string::npos || t.find('/', slash + 1) != std::string::npos) return v;
+      v.reps = repeating_reps(t.substr(1, slash - 1));
+      if (v.reps == 0) return v;
+      t = t.substr(slash + 1);
+    }
+    v.ms = parse_duration_ms(t);
+  }
+  v.ok = v.ms >= 0;
+  return v;
+}
+
 // MultiInstanceActivityTransformer.transformLoopCharacteristics
 // (deployment/model/transformer/MultiInstanceActivityTransformer.java:80-122) for the subset: the
 // inputCollection a static FEEL list literal (`= [10, 20, 30]`, `= ["a", "b"]`: integer, string,
@@ -615,7 +709,8 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
         err = "timer catch event outside the supported subset (timeDuration only)";
         return false;
       }
-      e.timer_ms = parse_duration_ms(td->text);
+      const TimerValue tv = timer_value(td->text, false);
+      e.timer_ms = tv.ok ? tv.ms : -1;
       if (e.timer_ms < 0 || e.timer_ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return false; }
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
@@ -634,26 +729,13 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
         err = "boundary event outside the supported subset (timer timeDuration, or timeCycle when non-interrupting)";
         return false;
       }
-      std::string dtext = td ? td->text : "";
-      if (tc) {  // RepeatingInterval.parse (bpmn-model/.../util/time/RepeatingInterval.java): "R[n]/interval"
-        std::string t = tc->text;
-        size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
-        t = a == std::string::npos ? "" : t.substr(a, b - a + 1);
-        const size_t slash = t.find('/');
-        bool ok = t.size() > 2 && t[0] == 'R' && slash != std::string::npos && t.find('/', slash + 1) == std::string::npos;
-        if (ok && slash == 1) {
-          e.reps = -1;  // RepeatingInterval.INFINITE
-        } else if (ok) {
-          const std::string n = t.substr(1, slash - 1);
-          ok = n.size() <= 3 && n.find_first_not_of("0123456789") == std::string::npos;
-          e.reps = ok ? atoi(n.c_str()) : 0;
-          ok = ok && e.reps >= 1 && e.reps <= 254;
-        }
-        if (!ok) { err = "timer cycle outside the supported subset: " + tc->text; return false; }
-        dtext = t.substr(slash + 1);
+      const TimerValue tv = timer_value(td ? td->text : tc->text, tc != nullptr);
+      e.reps = tc ? tv.reps : 1;
+      e.timer_ms = tv.ok ? tv.ms : -1;
+      if (e.timer_ms < 0 || e.timer_ms > 0xFFFFFFFFLL) {
+        err = "timer outside the supported subset: " + (td ? td->text : tc->text);
+        return false;
       }
-      e.timer_ms = parse_duration_ms(dtext);
-      if (e.timer_ms < 0 || e.timer_ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + dtext; return false; }
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_TIMER;

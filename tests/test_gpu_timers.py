@@ -94,7 +94,13 @@ def _timer_in_sub_process():
 
 SHAPES = {"timer": lambda: timer_process("PT10S"), "task_timer_task": _task_timer_task,
           "timer_in_branch": _timer_in_branch, "timer_in_sub_process": _timer_in_sub_process,
-          "zero": lambda: timer_process("PT0S")}
+          "zero": lambda: timer_process("PT0S"),
+          # constant FEEL expressions (BoundaryEventTest.java:48-69's forms)
+          "feel_duration": lambda: timer_process('=duration("PT0.1S")'),
+          "feel_cycle_boundary": lambda: (bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "type")
+                                          .boundaryEvent("event").cancelActivity(False)
+                                          .timerWithCycleExpression('cycle(3, duration("PT1S"))').endEvent()
+                                          .moveToActivity("task").endEvent().done())}
 
 
 @pytest.mark.parametrize("shape", sorted(SHAPES))

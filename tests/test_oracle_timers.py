@@ -122,10 +122,20 @@ def test_static_durations(text, ms):
     assert int(c.els[[c.id(i) for i in range(len(c.els))].index("timer")]["duration_ms"]) == ms
 
 
+# constant FEEL expressions (ExpressionProcessor.evaluateIntervalExpression): a day-time duration is a
+# java.time.Duration -- days of 24 h (new Interval(duration)), unlike the calendar days of the string
+# form; a string goes through Interval.parse.  BoundaryEventTest.java:54 uses duration("PT0.1S").
+@pytest.mark.parametrize("text,ms", [('=duration("PT0.1S")', 100), ('= duration( "PT2M" )', 120000),
+                                     ('=duration("P1D")', 86400000), ('=duration("P1DT1H")', 90000000),
+                                     ('="PT5S"', 5000)])
+def test_constant_feel_durations(text, ms):
+    test_static_durations(text, ms)
+
+
 # days are a Period (Interval.isCalendarBased): added in the broker's system zone, so a DST change
 # moves the due date -- refused rather than assuming a UTC zone
-@pytest.mark.parametrize("text", ["P1Y", "P1M", "P1W", "PT-1S", "= duration(\"PT1S\")", "PT", "R3/PT1S", "P60D", "P1DT2H",
-                                  "P2D"])
+@pytest.mark.parametrize("text", ["P1Y", "P1M", "P1W", "PT-1S", "PT", "R3/PT1S", "P60D", "P1DT2H", "P2D",
+                                  "=timeout", "=duration(d)", '=duration("P1M")', '="P1D"', '=date("2020-01-01")'])
 def test_durations_outside_the_subset_are_refused(text):
     with pytest.raises(ZbhipError):
         Compiled(timer_process(text))
@@ -183,3 +193,39 @@ def _ord(o, instance, key):
         if o.resolve(instance, i) == key:
             return i
     raise KeyError(key)
+
+
+def boundary_process(cycle=None, duration=None, interrupting=False):
+    b = (bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "type")
+         .boundaryEvent("event").cancelActivity(interrupting))
+    b = b.timerWithCycleExpression(cycle) if cycle else b.timerWithDurationExpression(duration)
+    return b.endEvent().moveToActivity("task").endEvent().done()
+
+
+# BoundaryEventTest.java:48-69's constant expressions: a duration("PT0.1S") interrupting timer and a
+# cycle(duration("PT1S")) non-interrupting one (FeelFunctionProvider.cycle -> "R/PT1S": infinite);
+# cycle(3, ...) -> "R3/..."
+@pytest.mark.parametrize("cycle,duration,interrupting,ms,reps", [
+    (None, 'duration("PT0.1S")', True, 100, 1),
+    ('cycle(duration("PT1S"))', None, False, 1000, -1),
+    ('cycle(3, duration("PT2S"))', None, False, 2000, 3),
+    ('"R2/PT3S"', None, False, 3000, 2),
+])
+def test_constant_feel_boundary_timers(cycle, duration, interrupting, ms, reps):
+    xml = boundary_process(cycle, duration, interrupting)
+    o = Oracle()
+    o.set_clock(NOW)
+    o.deploy(xml)
+    created = [r for r in _timer_records(_run(o, create_commands(1, 0))) if r["intent"] == abi.TIMER_CREATED]
+    assert len(created) == 1 and int(created[0]["aux"]) == NOW + ms and int(created[0]["partition"]) == reps
+    c = Compiled(xml)
+    e = c.els[[c.id(i) for i in range(len(c.els))].index("event")]
+    assert int(e["duration_ms"]) == ms and int(e["job_retries"]) >> 8 == (255 if reps == -1 else reps)
+
+
+@pytest.mark.parametrize("cycle", ['cycle(x)', 'cycle(0, duration("PT1S"))', 'cycle(duration(d))', '"PT1S"'])
+def test_feel_cycles_outside_the_subset(cycle):
+    with pytest.raises(ZbhipError):
+        Compiled(boundary_process(cycle))
+    with pytest.raises(OracleError):
+        Oracle().deploy(boundary_process(cycle))

@@ -202,6 +202,15 @@ class ProcessBuilder:
         self.current.timer = duration
         return self
 
+    def timerWithDurationExpression(self, expression):
+        """AbstractTimerEventDefinitionBuilder.timerWithDurationExpression: the FEEL expression as
+        `=expression` in <timeDuration>."""
+        return self.timerWithDuration("=" + expression)
+
+    def timerWithCycleExpression(self, expression):
+        """BoundaryEventBuilder.timerWithCycleExpression: `=expression` in <timeCycle>."""
+        return self.timerWithCycle("=" + expression)
+
     def exclusiveGateway(self, id_=None):
         self._add_node("exclusiveGateway", id_)
         return self

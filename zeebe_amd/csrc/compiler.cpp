@@ -355,7 +355,7 @@ struct Compiled {
 // "P[0D][T[nH][nM][n[.f]S]]": a Duration, so due = now + a fixed number of ms.  Days (a Period, which
 // Interval.toEpochMilli adds in the broker's system zone), years, months, weeks, negative parts and
 // `=` expressions: -1 (outside the subset).
-static int64_t duration_ms(const std::string& text) {
+static int64_t duration_ms(const std::string& text, bool days_exact = false) {
   size_t a = text.find_first_not_of(" \t\r\n"), b = text.find_last_not_of(" \t\r\n");
   if (a == std::string::npos) return -1;
   const std::string t = text.substr(a, b - a + 1);
@@ -389,13 +389,82 @@ static int64_t duration_ms(const std::string& text) {
     any = true;
     // days make the interval calendar-based (Interval.isCalendarBased): ZonedDateTime.plus in the
     // broker's system zone, so a DST change moves the due date by an hour -- outside the subset
-    if (!in_time && u == 'D' && !frac && whole == 0) continue;
+    // (days_exact: a FEEL day-time duration, java.time.Duration -- a day is 24 h)
+    if (!in_time && u == 'D' && !frac && (whole == 0 || days_exact)) ms += whole * 86400000LL;
     else if (in_time && u == 'H' && !frac) ms += whole * 3600000LL;
     else if (in_time && u == 'M' && !frac) ms += whole * 60000LL;
     else if (in_time && u == 'S') ms += whole * 1000LL + frac;
     else return -1;
   }
   return any ? ms : -1;
+}
+
+// A timer's timeDuration / timeCycle text -> (milliseconds, repetitions): the static forms, and the
+// constant FEEL expressions ExpressionProcessor.evaluateIntervalExpression (processing/common/
+// ExpressionProcessor.java:142-175) turns into the same Interval -- `=duration("d")` (a FEEL day-time
+// duration: new Interval(Duration), days of 24 h), `="d"` (a string: Interval.parse, as the static
+// form) -- and for a cycle the strings FeelFunctionProvider.cycle builds (feel/.../
+// FeelFunctionProvider.scala:23-47): `=cycle(duration("d"))` = "R/d", `=cycle(n, duration("d"))` =
+// "Rn/d".  reps: 1 for a duration, 255 for an infinite cycle.  Expressions naming variables, year-month
+// durations and calendar days stay outside the subset (-1).
+static std::string trim(const std::string& t) {
+  const size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
+  return a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+}
+// `name(args)` -> args, or false
+static bool call_args(const std::string& t, const char* name, std::string& args) {
+  const size_t n = strlen(name);
+  if (t.compare(0, n, name) != 0) return false;
+  const std::string r = trim(t.substr(n));
+  if (r.size() < 2 || r.front() != '(' || r.back() != ')') return false;
+  args = trim(r.substr(1, r.size() - 2));
+  return true;
+}
+static bool string_literal(const std::string& t, std::string& v) {
+  if (t.size() < 2 || t.front() != '"' || t.back() != '"') return false;
+  v = t.substr(1, t.size() - 2);
+  return v.find_first_of("\"\\") == std::string::npos;
+}
+static int64_t feel_interval_ms(const std::string& e) {  // a FEEL expression (after the `=`)
+  std::string a, v;
+  if (call_args(e, "duration", a) && string_literal(a, v)) return duration_ms(v, true);
+  if (string_literal(e, v)) return duration_ms(v);
+  return -1;
+}
+static int64_t parse_repetitions(const std::string& n) {  // RepeatingInterval.parse's "Rn"
+  if (n.empty()) return 255;
+  if (n.size() > 3 || n.find_first_not_of("0123456789") != std::string::npos) return -1;
+  const int r = atoi(n.c_str());
+  return r >= 1 && r <= 254 ? r : -1;
+}
+static int64_t timer_ms(const std::string& text, bool cycle, uint32_t& reps) {
+  const std::string t = trim(text);
+  reps = 1;
+  if (!cycle) return t.size() > 1 && t[0] == '=' ? feel_interval_ms(trim(t.substr(1))) : duration_ms(t);
+  std::string r = t;
+  if (t.size() > 1 && t[0] == '=') {
+    const std::string e = trim(t.substr(1));
+    std::string args, v;
+    if (string_literal(e, v)) {
+      r = v;
+    } else if (call_args(e, "cycle", args)) {
+      const size_t comma = args.find(',');
+      const std::string n = comma == std::string::npos ? std::string() : trim(args.substr(0, comma));
+      const int64_t rp = parse_repetitions(n);
+      if (rp < 0) return -1;
+      reps = (uint32_t)rp;
+      return feel_interval_ms(trim(comma == std::string::npos ? args : args.substr(comma + 1)));
+    } else {
+      return -1;
+    }
+  }
+  const size_t slash = r.find('/');
+  if (r.size() < 3 || r[0] != 'R' || slash == std::string::npos || r.find('/', slash + 1) != std::string::npos)
+    return -1;
+  const int64_t rp = parse_repetitions(r.substr(1, slash - 1));
+  if (rp < 0) return -1;
+  reps = (uint32_t)rp;
+  return duration_ms(r.substr(slash + 1));
 }
 
 // A multi-instance activity's loop characteristics (MultiInstanceActivityTransformer
@@ -681,33 +750,17 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         const Elem* tc = ted && !td ? ted->first("timeCycle") : nullptr;
         for (auto& d : c.children)
           if (&d != ted && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) td = tc = nullptr;
-        // a static timeCycle "R[n]/duration" (RepeatingInterval.parse) on a non-interrupting
-        // boundary event: repetitions n (1..254) or infinite (255); a duration: 1
+        // a timeCycle (RepeatingInterval.parse "R[n]/duration", or its constant FEEL form) on a
+        // non-interrupting boundary event: repetitions n (1..254) or infinite (255); a duration: 1
         uint32_t reps = 1;
-        std::string dtext = td ? td->text : "";
-        if (tc && !interrupting) {
-          std::string t = tc->text;
-          const size_t a = t.find_first_not_of(" \t\r\n"), b = t.find_last_not_of(" \t\r\n");
-          t = a == std::string::npos ? "" : t.substr(a, b - a + 1);
-          const size_t slash = t.find('/');
-          bool ok = t.size() > 2 && t[0] == 'R' && slash != std::string::npos && t.find('/', slash + 1) == std::string::npos;
-          if (ok && slash == 1) {
-            reps = 255;
-          } else if (ok) {
-            const std::string n = t.substr(1, slash - 1);
-            ok = n.size() <= 3 && n.find_first_not_of("0123456789") == std::string::npos;
-            reps = ok ? (uint32_t)atoi(n.c_str()) : 0;
-            ok = ok && reps >= 1 && reps <= 254;
-          }
-          if (!ok) { err = "timer cycle outside the supported subset: " + tc->text; return ZBHIP_EUNSUPP; }
-          dtext = t.substr(slash + 1);
-        } else if (!td) {
+        if (!td && !(tc && !interrupting)) {
           err = "boundary event outside the supported subset (timer timeDuration, or timeCycle when non-interrupting)";
           return ZBHIP_EUNSUPP;
         }
+        const std::string dtext = td ? td->text : tc->text;
+        const int64_t ms = timer_ms(dtext, !td, reps);
         e.job_retries = (uint16_t)((interrupting ? 1u : 0u) | (reps << 8));
-        const int64_t ms = duration_ms(dtext);
-        if (ms < 0 || ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + dtext; return ZBHIP_EUNSUPP; }
+        if (ms < 0 || ms > 0xFFFFFFFFLL) { err = "timer outside the supported subset: " + dtext; return ZBHIP_EUNSUPP; }
         if (const Elem* ext = c.first("extensionElements"))
           if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
         const std::string* at = c.get("attachedToRef");
@@ -724,7 +777,8 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           err = "timer catch event outside the supported subset (timeDuration only)";
           return ZBHIP_EUNSUPP;
         }
-        const int64_t ms = duration_ms(td->text);
+        uint32_t reps = 1;
+        const int64_t ms = timer_ms(td->text, false, reps);
         if (ms < 0 || ms > 0xFFFFFFFFLL) { err = "timer duration outside the supported subset: " + td->text; return ZBHIP_EUNSUPP; }
         if (const Elem* ext = c.first("extensionElements"))
           if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
