@@ -242,15 +242,21 @@ def test_declined_window_past_earlier_windows_and_after_a_redeploy():
     assert log.declined == 1
 
 
-def test_activated_job_completions_go_to_the_host_serialiser():
-    # JOB:COMPLETED of an ACTIVATED job carries the worker (a value-dictionary string): the device
-    # writer declines the window (ZBHIP_EUNSUPP) and the host serialiser writes it; windows without
-    # activated jobs before and after stay on the device
-    n = 64
+def test_activated_job_completions_on_the_device():
+    # JOB:COMPLETED / CANCELED of an ACTIVATED job carry the stored deadline and worker
+    # (DbJobState.activate): the device writer composes them from the batch's activation word and the
+    # value dictionary's bytes -- a plain, an empty and a 40-byte worker (msgpack str8 header)
+    n = 96
     log = Log(bpmn.linear_process(3, job_type="t"), n)
     recs = log.window(create_commands(n))
-    log.part.activate_jobs("t", worker="w", timeout=1000, max_jobs=8, timestamp=10)
-    recs = log.window(job_completions(recs, log.part), allow_host=True)
-    assert log.declined == 1
-    log.window(job_completions(recs, log.part))  # (the declined window's keys went into the ring)
-    assert log.declined == 1
+    log.part.activate_jobs("t", worker="w", timeout=1000, max_jobs=30, timestamp=10)
+    log.part.activate_jobs("t", worker="", timeout=2000, max_jobs=20, timestamp=20)
+    log.part.activate_jobs("t", worker="worker-" + "x" * 33, timeout=3000, max_jobs=20, timestamp=30)
+    recs = log.window(job_completions(recs, log.part))
+    done = recs[(recs["value_type"] == abi.VT_JOB) & (recs["intent"] == abi.JOB_COMPLETED)]
+    assert sorted(set(done["message_key"].tolist())) == [-1, 1010, 2020, 3030]
+    # the next tasks' jobs, activated again and completed; then the rest without activation
+    log.part.activate_jobs("t", worker="again", timeout=500, max_jobs=50, timestamp=40)
+    recs = log.window(job_completions(recs, log.part))
+    log.window(job_completions(recs, log.part))
+    assert log.declined == 0

@@ -201,3 +201,29 @@ def part_key(part, inst, ordv):
             if part.resolve_key(k) == (inst, ordv):
                 return k
     raise KeyError((inst, ordv))
+
+
+def test_gpu_activated_jobs_canceled_by_a_boundary_timer():
+    # an interrupting boundary timer fires on ACTIVATED jobs: JOB:CANCELED is the stored job (deadline
+    # and worker), in the records, the host serialiser's bytes and the device writer's bytes alike
+    from test_gpu_logdev import Log
+    xml = (bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "type")
+           .boundaryEvent("timer").cancelActivity(True).timerWithDuration("PT1M").endEvent("te")
+           .moveToActivity("task").endEvent().done())
+    pair = Pair(xml, 40)
+    log = Log(xml, 40)
+    for e in (pair.part, pair.orc, log.part):
+        e.set_clock(NOW)
+    pair.window(create_commands(40, 0))
+    log.window(create_commands(40, 0))
+    for e in (pair.part, pair.orc, log.part):
+        e.activate_jobs("type", worker="boundary-w", timeout=999, max_jobs=25, timestamp=5)
+    rows = [r.split("|") for r in pair.part.state() if r.startswith("TIMERS|")]
+    keys = [(int(p[2]), int(dict(kv.split("=") for kv in p[3].split(","))["dueDate"])) for p in rows]
+    res = [pair.part.resolve_key(k) for k, _ in keys]
+    c = trigger_commands([i for i, _ in res], [o for _, o in res], [d for _, d in keys])
+    got = pair.window(c)
+    canceled = got[(got["value_type"] == abi.VT_JOB) & (got["intent"] == abi.JOB_CANCELED)]
+    assert len(canceled) == 40 and (canceled["message_key"] == 1004).sum() == 25
+    log.window(c)
+    assert log.declined == 0

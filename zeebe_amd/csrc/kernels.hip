@@ -237,6 +237,11 @@ __device__ __forceinline__ void set_fail(Lane<K>& L, uint32_t why) {
   if (!L.fail) L.fail = why;
 }
 
+// an ACTIVATED job's record (JOB:COMPLETED / CANCELED: the stored job): its activation entry into the
+// batch's cmd_act word for the drain and the device log writer (none found: the writer declines)
+template <class K>
+__device__ __forceinline__ void note_activation(const Lane<K>& L, uint32_t job_ord, uint32_t inst);
+
 template <class K>
 __device__ __forceinline__ uint4 elem_of(const Lane<K>& L, uint32_t e) {
   return reinterpret_cast<const uint4*>(L.pb + 8)[e];
@@ -1411,7 +1416,10 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
   const uint2 e = tget(L, t);
   const uint32_t job = e.y & 0xFFFF;
   // (flag 1: the job was ACTIVATED -- its record carries the stored deadline and worker)
-  if (((e.y >> 24) & 1u) && job != JOB_ZERO && job != JOB_MINUS1) emit(L, C_JOB_CANCELED, job, key, elem, (e.y >> 25) & 1u);
+  if (((e.y >> 24) & 1u) && job != JOB_ZERO && job != JOB_MINUS1) {
+    emit(L, C_JOB_CANCELED, job, key, elem, (e.y >> 25) & 1u);
+    if ((e.y >> 25) & 1u) note_activation(L, job, L.inst);
+  }
   if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == key) cancel_timer(L);
   const uint32_t c = scope_of<K>(w);
   const uint32_t fst = c == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, c)).y >> 16) & 0xFF;
@@ -1768,6 +1776,18 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   take_outgoing(L, w);
 }
 
+template <class K>
+__device__ __forceinline__ void note_activation(const Lane<K>& L, uint32_t job_ord, uint32_t inst) {
+  const StepParams& P = *L.sp;
+  if (!P.cmd_act || !P.st.act || inst >= P.st.n) return;
+  uint4 f = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = 0; k < (uint32_t)kSlots; ++k) {
+    const uint4 a = P.st.act[(size_t)k * P.st.n + inst];
+    if ((a.x >> 31) && (a.x & 0xFFFF) == job_ord) f = a;
+  }
+  P.cmd_act[L.ci] = f;
+}
+
 // ---- straight-line segments of linear chains (K::REG) --------------------------------------
 // The arena's segment word of a start event or service task (runtime.cpp rebuild_program) says
 // that leaving it is deterministic: one unconditional outgoing flow `f` into a service task or a
@@ -1812,6 +1832,7 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
     const uint32_t k = L.next_ord, n = (sg >> 12) & 0xFFF;
     // JobCompleteProcessor + EventTriggerBehavior.triggeringProcessEvent, then COMPLETE_ELEMENT(task)
     put(L, 0, C_JOB_COMPLETED | (((e.y >> 25) & 1u) << 8), ref, tk, te);  // (flag 1: an ACTIVATED job)
+    if ((e.y >> 25) & 1u) note_activation(L, ref, L.inst);
     put(L, 1, C_PE_TRIGGERING, k, tk, te);
     put(L, 2, ZBHIP_PI_COMPLETE_ELEMENT, tk, 0, te);
     put(L, 3, ZBHIP_PI_ELEMENT_COMPLETING, tk, 0, te);
@@ -2254,6 +2275,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     L.tm_due = 0;
   }
   bool slot_kind = false;
+  L.inst = inst;  // (K::M: a slot lane loads its instance later)
   if constexpr (K::M) {
     L.prog = prog;
     L.inst = inst;
@@ -2426,6 +2448,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       uint2 e = tget(L, t);
       const uint32_t task_key = e.x >> 16, task_elem = e.x & 0xFFFF;
       emit(L, C_JOB_COMPLETED, ref, task_key, task_elem, (e.y >> 25) & 1u);  // (flag 1: an ACTIVATED job)
+      if ((e.y >> 25) & 1u) note_activation(L, ref, inst);
       // the task's flow scope: the process instance, or (K::S) the sub-process instance around it
       bool fs_active = L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED;
       uint32_t fsk = 0;
@@ -3251,7 +3274,8 @@ struct ActivatedOut {
   long long val[kVars];
   uint2 slots[kSlots]; // the instance's element instances (the job's enclosing scopes: variables)
 };
-__global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2* jobs, uint32_t n, ActivatedOut* out) {
+__global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2* jobs, uint32_t n, ActivatedOut* out,
+                                                      uint32_t worker, unsigned long long deadline) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint32_t inst = jobs[i].x, ord = jobs[i].y;
@@ -3259,13 +3283,34 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
   if (inst < st.n) {
     const uint4 h = st.hdr[inst];
     const uint32_t nslots = (h.y >> 8) & 0xFF, nvars = (h.y >> 16) & 0xFF;
+    bool marked = false;
     for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s) {
       uint2 e = st.slots[(size_t)s * st.n + inst];
       if ((e.y & 0xFFFF) == ord && ((e.y >> 24) & 3u) == 1u) {
         e.y |= 2u << 24;
         st.slots[(size_t)s * st.n + inst] = e;
         o.a = make_uint4(e.x, h.x, h.y, e.y);  // (e.y != 0: its state; a multi-instance loop counter)
+        marked = true;
       }
+    }
+    // the activation (DbJobState.activate stores the deadline and worker): an entry of the instance's
+    // activation table -- the one already naming this ordinal (a stale one of an earlier instance in
+    // the slot), or one whose job is gone
+    if (marked && st.act) {
+      int pick = -1;
+      for (uint32_t k = 0; k < (uint32_t)kSlots && pick < 0; ++k)
+        if ((st.act[(size_t)k * st.n + inst].x & 0xFFFF) == ord) pick = (int)k;
+      for (uint32_t k = 0; k < (uint32_t)kSlots && pick < 0; ++k) {
+        const uint4 a = st.act[(size_t)k * st.n + inst];
+        bool live = false;
+        for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s) {
+          const uint2 e = st.slots[(size_t)s * st.n + inst];
+          live |= (a.x >> 31) && (e.y & 0xFFFF) == (a.x & 0xFFFF) && ((e.y >> 24) & 3u) == 3u;
+        }
+        if (!live) pick = (int)k;
+      }
+      if (pick >= 0)
+        st.act[(size_t)pick * st.n + inst] = make_uint4(ord | (1u << 31), worker, (uint32_t)deadline, (uint32_t)(deadline >> 32));
     }
     for (uint32_t v = 0; v < nvars && v < (uint32_t)kVars; ++v) {
       o.meta[v] = st.var_meta[(size_t)v * st.n + inst];
@@ -3277,9 +3322,10 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
   out[i] = o;
 }
 
-hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, hipStream_t s) {
+hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, uint32_t worker,
+                                long long deadline, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_activate_jobs, dim3((n + 255) / 256), dim3(256), 0, s, st, jobs, n,
-                            static_cast<ActivatedOut*>(out));
+                            static_cast<ActivatedOut*>(out), worker, (unsigned long long)deadline);
   return hipGetLastError();
 }
 size_t activated_out_bytes() { return sizeof(ActivatedOut); }

@@ -41,11 +41,14 @@ enum LogRun : uint32_t {
   G_AUTH, G_TENANT, G_FLOWSCOPE, G_EMPTY_BIN, G_JREJ_HEAD, G_JREJ_TAIL, G_VAR_A, G_VAR_VALUE, G_VAR_SCOPE,
   G_K_PIK, G_K_DEF, G_K_BPMN, G_PE_A, G_PE_TARGET, G_K_VARS, G_PIC_A, G_K_VERSION, G_PIC_TAIL,
   G_RS_PGW_A, G_RS_PGW_B, G_RS_FSNF_A, G_RS_NF_B, G_RS_FSST_A, G_RS_Q, G_RS_EINF_A, G_RS_EIST_A, G_RS_JOB_A,
-  G_RS_JOB_B, G_RS_TNF_A, G_RS_TNF_B, G_RS_TNA_A, G_RS_TNA_B, G_TIMER_A, G_TIMER_DUE, G_TIMER_REPS, G_ST0,
+  G_RS_JOB_B, G_RS_TNF_A, G_RS_TNF_B, G_RS_TNA_A, G_RS_TNA_B, G_TIMER_A, G_TIMER_DUE, G_TIMER_REPS, G_JACT_A,
+  G_JACT_W, G_ST0,
   G_COUNT = G_ST0 + 16
 };
 // element runs (proc block word 6 + 16 e); E_DUR is the timer duration in ms (.x), not a byte run
-enum ElRun : uint32_t { E_PI_HEAD, E_PI_TAIL, E_JOB_HEAD, E_JOB_MID, E_JOB_TAIL, E_ID_STR, E_ID_RAW, E_DUR, E_COUNT };
+// (E_JOB_REST: E_JOB_HEAD after its deadline and worker entries -- an ACTIVATED job's head is composed)
+enum ElRun : uint32_t { E_PI_HEAD, E_PI_TAIL, E_JOB_HEAD, E_JOB_MID, E_JOB_TAIL, E_ID_STR, E_ID_RAW, E_JOB_REST, E_DUR,
+                        E_COUNT };
 
 struct LogParams {
   const uint2* rows;            // gathered compact rows (launch order)
@@ -75,6 +78,10 @@ struct LogParams {
   unsigned long long out_cap;   // bytes at `out` (0: unchecked)
   LogKeys* wkeys;               // [n] per command: the older keys its records name (k_log_sizes)
   uint32_t tpl_lds;             // bytes of the templates + their descriptors (k_log_stream stages both)
+  const uint4* cmd_act;         // [n] the ACTIVATED job a batch completed / canceled (StepParams.cmd_act)
+  const uint8_t* strs;          // the value dictionary's bytes (workers of activated jobs) ...
+  const unsigned long long* str_off;  // ... string i at [str_off[i], str_off[i + 1])
+  uint32_t n_strs;
 };
 constexpr uint32_t kSlow = 1u << 31;
 
@@ -101,6 +108,7 @@ struct Count {
   __device__ __forceinline__ void b(uint32_t) { ++n; }
   __device__ __forceinline__ void bytes(const LogParams&, uint2 r) { n += r.y; }
   __device__ __forceinline__ void zeros(uint32_t k) { n += k; }
+  __device__ __forceinline__ void raw(const uint8_t*, uint32_t k) { n += k; }
 };
 // appends up to four bytes at a time into a 128-bit accumulator, stored with one 16-byte store
 // when it fills (a lane writes its own command's bytes: every store is a separate transaction, so
@@ -150,6 +158,9 @@ struct Write {
   }
   __device__ __forceinline__ void zeros(uint32_t k) {
     for (uint32_t i = 0; i < k; i += 4) put(0, k - i < 4 ? k - i : 4);
+  }
+  __device__ __forceinline__ void raw(const uint8_t* p, uint32_t k) {  // (unaligned bytes)
+    for (uint32_t i = 0; i < k; ++i) put(p[i], 1);
   }
 };
 
@@ -207,6 +218,9 @@ struct Rec {
   int reps;                 // TIMER: repetitions (-1 infinite)
   uint32_t proc, elem;      // NONE when not applicable
   uint8_t rt, vt, intent, rej_type, reason, reason_arg, skip;
+  bool act;                 // JOB: an ACTIVATED job's record (deadline, worker below)
+  long long deadline;
+  uint32_t worker;
 };
 
 // key of ordinal `ord` of instance `inst` as seen by command c (see the header comment)
@@ -273,14 +287,25 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
   r.rej_type = ZBHIP_REJ_NONE;
   r.reason = r.reason_arg = 0;
   r.skip = 0;
+  r.act = false;
+  r.deadline = -1;
+  r.worker = ZBHIP_NO_STRING;
   if (c6 >= 1 && c6 <= 10) {
     r.vt = ZBHIP_VT_PROCESS_INSTANCE;
     r.intent = (uint8_t)c6;
     r.rt = rej ? ZBHIP_RT_REJECTION : (c6 >= 8 ? ZBHIP_RT_COMMAND : ZBHIP_RT_EVENT);
     r.skip = !rej && c6 >= 8 && !(fl & F_UNPROCESSED) ? 1 : 0;  // a follow-up command processed in its batch
   } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE || c6 == C_JOB_CANCELED) {
-    // an ACTIVATED job's record carries its worker (a value-dictionary string): the host serialiser
-    if (!rej && (fl & 1u) && (c6 == C_JOB_COMPLETED || c6 == C_JOB_CANCELED)) return false;
+    // an ACTIVATED job's record: the stored job's deadline and worker from the batch's activation
+    // word (missing, or naming another job: the host serialiser)
+    if (!rej && (fl & 1u) && (c6 == C_JOB_COMPLETED || c6 == C_JOB_CANCELED)) {
+      const uint4 a = L.cmd_act ? L.cmd_act[c] : make_uint4(0, 0, 0, 0);
+      if (!(a.x >> 31) || (a.x & 0xFFFF) != key_ord || (a.y != ZBHIP_NO_STRING && (a.y >= L.n_strs || !L.strs)))
+        return false;
+      r.act = true;
+      r.deadline = (long long)(((unsigned long long)a.w << 32) | a.z);
+      r.worker = a.y;
+    }
     r.vt = ZBHIP_VT_JOB;
     r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED
                : c6 == C_JOB_CANCELED ? ZBHIP_JOB_CANCELED : ZBHIP_JOB_COMPLETE;
@@ -436,7 +461,21 @@ __device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m,
         return true;
       }
       if (!has_el || el_run(L, pb, r.elem, E_JOB_HEAD).y == 0) return false;
-      s.bytes(L, el_run(L, pb, r.elem, E_JOB_HEAD));
+      if (r.act) {  // the stored job of an ACTIVATED job: its deadline and worker
+        s.bytes(L, run(L, G_JACT_A));
+        mp_int(s, r.deadline);
+        s.bytes(L, run(L, G_JACT_W));
+        const unsigned long long b = r.worker == ZBHIP_NO_STRING ? 0 : L.str_off[r.worker];
+        const uint32_t n = r.worker == ZBHIP_NO_STRING ? 0u : (uint32_t)(L.str_off[r.worker + 1] - b);
+        if (n < 32) s.b(0xa0 | n);  // MsgPackWriter.writeStringHeader (:214-240)
+        else if (n < 256) { s.b(0xd9); s.b(n); }
+        else if (n < 65536) { s.b(0xda); be(s, n, 2); }
+        else { s.b(0xdb); be(s, n, 4); }
+        if (n) s.raw(L.strs + b, n);
+        s.bytes(L, el_run(L, pb, r.elem, E_JOB_REST));
+      } else {
+        s.bytes(L, el_run(L, pb, r.elem, E_JOB_HEAD));
+      }
       if (r.intent != ZBHIP_JOB_COMPLETED) s.bytes(L, run(L, G_EMPTY_BIN));
       else if (!src_doc_bin(s, L, m)) return false;
       s.bytes(L, el_run(L, pb, r.elem, E_JOB_MID));
@@ -577,7 +616,7 @@ __device__ __forceinline__ void stage_tables(LogParams& L, uint32_t* lds) {
 // the keys the template can take (patched in its 9-byte msgpack form, or a process element's -1
 // flowScopeKey that is part of the template)
 __device__ __forceinline__ uint32_t tpl_of(const LogParams& L, const LogCmd& m, const Rec& r, uint4& d) {
-  if (r.rt == ZBHIP_RT_REJECTION || r.proc >= L.tpl_idx[0] || L.pbits < (1LL << 32)) return 0;
+  if (r.rt == ZBHIP_RT_REJECTION || r.act || r.proc >= L.tpl_idx[0] || L.pbits < (1LL << 32)) return 0;
   uint32_t k;
   switch (r.vt) {
     case ZBHIP_VT_PROCESS_INSTANCE: k = r.skip ? 10u + r.intent - 8u : r.intent - 1u; break;
@@ -1225,7 +1264,7 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
   LogParams L{a.rows, a.cmds, a.n, a.arena, a.idx, a.arena_words, a.idx_words, a.docs, a.n_docs, a.inst_proc, a.ring,
               a.kpi, a.n_inst, a.pbits, a.first_position, a.timestamp, {a.broker[0], a.broker[1], a.broker[2]},
               a.bytes, a.out, a.flag, a.now_ms, a.cmd_due, a.tpl, a.tpl_desc, a.tpl_idx, a.rinfo, a.out_cap,
-              a.wkeys, a.tpl_lds};
+              a.wkeys, a.tpl_lds, a.cmd_act, a.strs, a.str_off, a.n_strs};
   const uint32_t g = (a.n + 255) / 256;
   const size_t lds = a.arena_words + a.idx_words <= kLdsTableWords ? (size_t)(a.arena_words + a.idx_words) * 4 : 0;
   if (a.phase == 0) {  // sizes and byte offsets

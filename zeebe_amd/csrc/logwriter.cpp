@@ -1504,6 +1504,8 @@ int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, st
   b.clear(); mp_map(b, 7); key(b, "elementInstanceKey"); push(b);     // G_TIMER_A (TimerRecord.java:24-40)
   push(k({"dueDate"}));                                               // G_TIMER_DUE
   push(k({"repetitions"}));                                           // G_TIMER_REPS
+  b.clear(); mp_map(b, 17); key(b, "deadline"); push(b);              // G_JACT_A (an ACTIVATED job's head)
+  push(k({"worker"}));                                                // G_JACT_W
   for (int st = 0; st < 16; ++st) push(Bytes(state_text(st)));       // G_ST0 ..
   idx.push_back((uint32_t)s->names.size());
   for (const std::string& nm : s->names) {
@@ -1534,6 +1536,7 @@ int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, st
       mp_str(b, E.id);
       push(b);
       push(E.id);
+      push(E.job_head.empty() ? Bytes() : E.job_head.substr(E.job_rest));  // E_JOB_REST
       idx.push_back(E.duration_ms);  // E_DUR: not a byte run, the element's timer duration
       idx.push_back(0);
     }

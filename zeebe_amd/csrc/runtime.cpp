@@ -47,7 +47,8 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
                           unsigned long long* block_sum, unsigned long long* base, unsigned long long* counter,
                           zbhip_xpart_cmd* xout, uint32_t xcap, const DevState& st, long long pbits, hipStream_t s);
 hipError_t launch_xpart_window(const zbhip_xpart_cmd* xp, uint32_t n, uint4* cmds, hipStream_t s);
-hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, hipStream_t s);
+hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t n, void* out, uint32_t worker,
+                                long long deadline, hipStream_t s);
 hipError_t launch_log_device(const LogLaunch& a, hipStream_t s);
 int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, std::vector<uint32_t>& idx);
 int log_device_templates(zbhip_serializer* s, std::vector<uint8_t>& bytes, std::vector<uint32_t>& desc,
@@ -665,6 +666,10 @@ struct zbhip_handle {
   uint4* d_cmd_hdr2 = nullptr;
   long long* d_cmd_due = nullptr;       // (KScope) dueDate of the timer each batch canceled
   long long* d_map_val = nullptr;       // (KScope) io-mapped variable values per batch (StepParams.map_val)
+  uint4* d_cmd_act = nullptr;           // the ACTIVATED job each batch completed / canceled (StepParams.cmd_act)
+  uint8_t* d_strs = nullptr;            // the value dictionary on the device (the log writer's workers)
+  unsigned long long* d_str_off = nullptr;
+  size_t d_strs_n = 0, d_strs_cap = 0, d_str_off_cap = 0;
   std::vector<long long> h_map_val;
   bool debug = getenv("ZBHIP_DEBUG") != nullptr;  // per-call host timing lines on stderr
   std::vector<long long> h_cmd_due;
@@ -860,6 +865,10 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_stats);
   (void)hipFree(h->st.pms);
   (void)hipFree(h->st.tmr);
+  (void)hipFree(h->st.act);
+  (void)hipFree(h->d_cmd_act);
+  (void)hipFree(h->d_strs);
+  (void)hipFree(h->d_str_off);
   (void)hipFree(h->d_cmd_due);
   (void)hipFree(h->d_map_val);
   (void)hipFree(h->st.pi_key);
@@ -2120,6 +2129,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.cmd_due = h->d_cmd_due;
   P.map_val = h->d_map_val;
   P.map_cap = h->cfg.max_commands;
+  P.cmd_act = h->st.act ? h->d_cmd_act : nullptr;
   h->run_clock_ms = h->clock_ms;
   P.tpl = (h->variant == 0 || h->variant == 1 || h->scope_variant()) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
   if (h->msg()) {
@@ -3505,6 +3515,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   if (!h->relabel_ok) return ZBHIP_ESTATE;
   if (int rc = finalize(h)) return rc;
   h->ring_ok = false;  // imported keys are not in the device key ring: the host serialiser from now on
+  if (h->st.act)  // (activations of earlier instances in the slots no longer apply)
+    HIPCHK(hipMemset(h->st.act, 0, (size_t)kSlots * h->cfg.max_instances * sizeof(uint4)));
   std::map<int64_t, ImpElement> els;
   std::vector<ImpVar> vars;
   std::vector<std::tuple<int64_t, std::string, std::string, uint32_t>> taken;
@@ -4022,8 +4034,20 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     (void)hipFree(d_list);
     return ZBHIP_ENOMEM;
   }
-  hipError_t e = hipMemcpyAsync(d_list, list.data(), n * sizeof(uint2), hipMemcpyHostToDevice, h->stream);
-  if (e == hipSuccess) e = launch_activate_jobs(h->st, d_list, (uint32_t)n, d_out, h->stream);
+  // the device's activation table (the deadline and worker of ACTIVATED jobs, for their later records)
+  hipError_t e = hipSuccess;
+  if (!h->st.act) {
+    const size_t words = (size_t)kSlots * h->cfg.max_instances;
+    if (dalloc(&h->st.act, words) != hipSuccess || dalloc(&h->d_cmd_act, (size_t)h->cfg.max_commands) != hipSuccess) {
+      (void)hipFree(d_list);
+      (void)hipFree(d_out);
+      return ZBHIP_ENOMEM;
+    }
+    e = hipMemsetAsync(h->st.act, 0, words * sizeof(uint4), h->stream);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(d_list, list.data(), n * sizeof(uint2), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess)
+    e = launch_activate_jobs(h->st, d_list, (uint32_t)n, d_out, worker_id, cmd->timestamp + cmd->timeout, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(outb.data(), d_out, n * ob, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   (void)hipFree(d_list);
@@ -4261,6 +4285,36 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   a.rinfo = h->d_log_rinfo;
   a.wkeys = h->d_log_wkeys;
   a.tpl_lds = (uint32_t)h->log_tpl_idx_off;
+  if (h->st.act) {  // activated jobs' records name their workers: the dictionary's bytes on the device
+    if (h->d_strs_n != h->strs.size()) {
+      std::vector<unsigned long long> off(h->strs.size() + 1, 0);
+      for (size_t i = 0; i < h->strs.size(); ++i) off[i + 1] = off[i] + h->strs[i].size();
+      if (off.back() > h->d_strs_cap) {
+        (void)hipFree(h->d_strs);
+        h->d_strs = nullptr;
+        h->d_strs_cap = 0;
+        if (dalloc(&h->d_strs, (size_t)off.back() * 2 + 64) != hipSuccess) return ZBHIP_ENOMEM;
+        h->d_strs_cap = (size_t)off.back() * 2 + 64;
+      }
+      if (off.size() > h->d_str_off_cap) {
+        (void)hipFree(h->d_str_off);
+        h->d_str_off = nullptr;
+        h->d_str_off_cap = 0;
+        if (dalloc(&h->d_str_off, off.size() * 2) != hipSuccess) return ZBHIP_ENOMEM;
+        h->d_str_off_cap = off.size() * 2;
+      }
+      std::string bytes;
+      bytes.reserve((size_t)off.back());
+      for (const std::string& x : h->strs) bytes += x;
+      if (!bytes.empty()) HIPCHK(hipMemcpy(h->d_strs, bytes.data(), bytes.size(), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(h->d_str_off, off.data(), off.size() * sizeof(unsigned long long), hipMemcpyHostToDevice));
+      h->d_strs_n = h->strs.size();
+    }
+    a.cmd_act = h->d_cmd_act;
+    a.strs = h->d_strs;
+    a.str_off = h->d_str_off;
+    a.n_strs = (uint32_t)h->d_strs_n;
+  }
   unsigned long long total = 0;
   uint32_t flag = 0;
   auto tu = now(), tf = now();

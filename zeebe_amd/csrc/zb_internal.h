@@ -198,6 +198,9 @@ struct DevState {
                      //     timer key ordinal << 16, y = element-instance ordinal (the catch event's, or the
                      //     activity's a boundary event is attached to) | repetitions << 16 (255 infinite)
                      //     | live << 31, z/w = dueDate lo/hi
+  uint4* act;        // [kSlots][n] activations of the instance's jobs (zbhip_activate_jobs; NULL until the
+                     //     first): x = job key ordinal | valid << 31, y = worker (value-dictionary id),
+                     //     z/w = deadline lo/hi -- the stored job's fields its later records carry
 };
 
 // elements without behaviour: ACTIVATING, ACTIVATED, COMPLETE_ELEMENT, COMPLETING, COMPLETED, then
@@ -257,6 +260,8 @@ struct StepParams {
   long long* map_val;         // [kMapVals][map_cap] (KScope) values of the variables a batch's io mappings
                               // wrote: value j of window command c at j * map_cap + c (C_VAR_MAPPED)
   uint32_t map_cap;
+  uint4* cmd_act;             // [n_cmds] the ACTIVATED job a batch completed or canceled: its DevState.act
+                              // entry (x bit 31 clear: none found)
 };
 constexpr int kMapVals = 2;   // io-mapped VARIABLE records per batch (more: FB_VARS)
 
@@ -325,6 +330,10 @@ struct LogLaunch {
                                // window's total (bytes[n], from the scan) exceeds it
   LogKeys* wkeys;              // [n] (phase 0 writes, phase 1 reads)
   uint4* jrn;                  // phase 3: [n] the window's key bookkeeping journal (NULL: the host books it)
+  const uint4* cmd_act;        // [n] StepParams.cmd_act (NULL: no job was ever activated)
+  const uint8_t* strs;         // the value dictionary on the device (activated jobs' workers)
+  const unsigned long long* str_off;
+  uint32_t n_strs;
   uint32_t tpl_lds;            // bytes of the templates and their descriptors (the `tpl` block up to tpl_idx)
 };
 
