@@ -564,6 +564,7 @@ struct zbhip_handle {
   bool relabel_ok = true;
   size_t fin_next = 0;             // the last run's key bookkeeping is done for commands < fin_next (advance)
   std::vector<uint32_t> ext_keys;  // keys the CPU engine generated for the window's fallback commands
+  bool ext_ready = false;          // ext_keys / declared are the last run's (ensure_ext)
   std::vector<uint8_t> declared;   // ... declared by the adapter (zbhip_set_external_keys)
   // plan_rounds: (stamp, last round) per subject; window of the last command per instance slot
   std::vector<std::pair<uint32_t, uint32_t>> plan_last;
@@ -1809,6 +1810,26 @@ static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
   }
 }
 
+// the window's fallback key declarations, cleared on first use after a run (a window without fallback
+// commands never reads them)
+static void ensure_ext(zbhip_handle* h) {
+  if (h->ext_ready) return;
+  const size_t n = h->n_cmds;
+  h->ext_keys.resize(n);
+  h->declared.resize(n);
+  if (n >= (1u << 16)) {
+    parallel_for(host_threads(), [&](unsigned t, unsigned T) {
+      const size_t lo = n * t / T, hi = n * (t + 1) / T;
+      std::fill(h->ext_keys.begin() + lo, h->ext_keys.begin() + hi, 0);
+      std::fill(h->declared.begin() + lo, h->declared.begin() + hi, 0);
+    });
+  } else {
+    std::fill(h->ext_keys.begin(), h->ext_keys.end(), 0);
+    std::fill(h->declared.begin(), h->declared.end(), 0);
+  }
+  h->ext_ready = true;
+}
+
 // The whole bookkeeping of a plain window at once (no message subjects, no job index): key bases
 // in log order (a sequential prefix), then the per-instance histories, processes and generations on
 // host threads -- each thread owns the instances i % T == t and walks the window in log order, so
@@ -1987,6 +2008,7 @@ static int fold_journals(zbhip_handle* h, size_t keep = 0) {
 static int advance(zbhip_handle* h, size_t limit, bool force) {
   if (int rc = fold_journals(h)) return rc;
   if (!h->results || h->fin_next >= h->n_cmds) return ZBHIP_OK;
+  ensure_ext(h);
   if (h->fin_next == 0) {  // a new window: jobs completed in the previous one are gone
     for (int64_t k : h->completed_activated) h->activated.erase(k);
     h->completed_activated.clear();
@@ -2393,20 +2415,10 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
             ms(t0, t1), ms(t1, now()));
   }
 
-  // fallback key declarations start empty; key bases are written by advance() before any read
-  h->ext_keys.resize(n);
-  h->declared.resize(n);
+  // fallback key declarations start empty (cleared when first read: ensure_ext); key bases are
+  // written by advance() before any read
+  h->ext_ready = false;
   h->h_base.resize(n);
-  if (n >= (1u << 16)) {
-    parallel_for(host_threads(), [&](unsigned t, unsigned T) {
-      const size_t lo = (size_t)n * t / T, hi = (size_t)n * (t + 1) / T;
-      std::fill(h->ext_keys.begin() + lo, h->ext_keys.begin() + hi, 0);
-      std::fill(h->declared.begin() + lo, h->declared.begin() + hi, 0);
-    });
-  } else {
-    std::fill(h->ext_keys.begin(), h->ext_keys.end(), 0);
-    std::fill(h->declared.begin(), h->declared.end(), 0);
-  }
   h->fin_next = 0;
   h->results = true;
   }
@@ -3421,6 +3433,7 @@ int zbhip_key_before(zbhip_handle* h, size_t i, int64_t* key) {
     return ZBHIP_OK;
   }
   int64_t c = h->key_counter;  // after commands < fin_next
+  ensure_ext(h);
   for (size_t k = h->fin_next; k < i; ++k) {
     const uint2 hd = h->h_hdr[k];
     c += ((hd.y >> 16) & 0xFF) == ST_OK ? (int64_t)(hd.x >> 16) : (int64_t)h->ext_keys[k];
@@ -3436,6 +3449,7 @@ int zbhip_set_external_keys(zbhip_handle* h, size_t i, uint32_t nkeys) {
   if (i < h->fin_next) return ZBHIP_ESTATE;  // the keys after it are fixed already
   // config 5: the device key scan fixed this window's keys already (outbox, slot rows)
   if (h->msg() && nkeys) return ZBHIP_EUNSUPP;
+  ensure_ext(h);
   h->ext_keys[i] = nkeys;
   h->declared[i] = 1;
   return ZBHIP_OK;
