@@ -7,6 +7,7 @@ O=${OUT:-gpurun_out/logab}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+export ZBHIP_LOG_STREAM=1 ZBHIP_JOURNAL=1 ZBHIP_DEVICE_ACTIVATIONS=1
 [ -n "$LOGAB_NOTEST" ] || timeout -k 10 600 python -u -m pytest tests/test_gpu_logdev.py tests/test_gpu_logserial.py tests/test_gpu_journal.py tests/test_gpu_key_table.py -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for v in stream halfwave; do

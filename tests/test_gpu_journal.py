@@ -21,7 +21,9 @@ TS = 1700000000123
 
 class Side:
     def __init__(self, xml, n, journal_windows=None, journal=True):
-        env = {"ZBHIP_JOURNAL_WINDOWS": str(journal_windows)} if journal_windows else {}
+        env = {"ZBHIP_JOURNAL": "1"}
+        if journal_windows:
+            env["ZBHIP_JOURNAL_WINDOWS"] = str(journal_windows)
         self.env = env if journal else {"ZBHIP_NO_JOURNAL": "1"}
         self.part = Partition(max_instances=n, max_commands=4 * n, max_records_per_batch=128)
         assert self.part.deploy(xml) == 0

@@ -242,10 +242,11 @@ def test_declined_window_past_earlier_windows_and_after_a_redeploy():
     assert log.declined == 1
 
 
-def test_activated_job_completions_on_the_device():
+def test_activated_job_completions_on_the_device(monkeypatch):
     # JOB:COMPLETED / CANCELED of an ACTIVATED job carry the stored deadline and worker
     # (DbJobState.activate): the device writer composes them from the batch's activation word and the
     # value dictionary's bytes -- a plain, an empty and a 40-byte worker (msgpack str8 header)
+    monkeypatch.setenv("ZBHIP_DEVICE_ACTIVATIONS", "1")
     n = 96
     log = Log(bpmn.linear_process(3, job_type="t"), n)
     recs = log.window(create_commands(n))

@@ -203,10 +203,11 @@ def part_key(part, inst, ordv):
     raise KeyError((inst, ordv))
 
 
-def test_gpu_activated_jobs_canceled_by_a_boundary_timer():
+def test_gpu_activated_jobs_canceled_by_a_boundary_timer(monkeypatch):
     # an interrupting boundary timer fires on ACTIVATED jobs: JOB:CANCELED is the stored job (deadline
     # and worker), in the records, the host serialiser's bytes and the device writer's bytes alike
     from test_gpu_logdev import Log
+    monkeypatch.setenv("ZBHIP_DEVICE_ACTIVATIONS", "1")
     xml = (bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "type")
            .boundaryEvent("timer").cancelActivity(True).timerWithDuration("PT1M").endEvent("te")
            .moveToActivity("task").endEvent().done())

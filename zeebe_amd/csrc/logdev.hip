@@ -1295,7 +1295,9 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
                                       (int)kStreamLdsMax) == hipSuccess;
       (void)hipGetLastError();
     }
-    const bool stream = stream_ok && a.wkeys && a.tpl_lds && slds <= kStreamLdsMax && !getenv("ZBHIP_LOG_HALFWAVE");
+    // (opt-in until its GPU parity run: ZBHIP_LOG_STREAM=1)
+    const bool stream = stream_ok && a.wkeys && a.tpl_lds && slds <= kStreamLdsMax && getenv("ZBHIP_LOG_STREAM") &&
+                        !getenv("ZBHIP_LOG_HALFWAVE");
     if (a.n && a.compose != 2 && stream) {
       const uint32_t per_cu = (uint32_t)(kStreamLdsMax / slds) < 4 ? (uint32_t)(kStreamLdsMax / slds) : 4u;
       uint32_t grid = (uint32_t)cus * per_cu;
