@@ -963,15 +963,18 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* const lds = reinterpret_cast<uint8_t*>(smem);
   if (L.out_cap && ((*L.flag & 1u) || L.bytes[L.n] > L.out_cap)) return;  // (as k_log_write)
+  // LDS: the waves' record areas first (the direct global->LDS loads address LDS through M0: kept in
+  // the low 64 KB), then their stages, then the templates and descriptors
   const uint32_t T = (L.tpl_lds + 15u) & ~15u;
-  for (uint32_t i = threadIdx.x; i < T / 16; i += blockDim.x)
-    reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(L.tpl)[i];
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint8_t* const stage = lds + T + wv * kStreamWaveLds;
-  uint32_t* const lri = reinterpret_cast<uint32_t*>(stage + kStreamStage);
+  uint32_t* const lri = reinterpret_cast<uint32_t*>(lds + wv * (kStreamRecs * 12));
   uint32_t* const lrow = lri + kStreamRecs;  // two words per record
-  const uint4* const desc = reinterpret_cast<const uint4*>(lds + (reinterpret_cast<const uint8_t*>(L.tpl_desc) - L.tpl));
+  uint8_t* const stage = lds + kStreamWaves * (kStreamRecs * 12) + wv * kStreamStage;
+  uint8_t* const tpl = lds + kStreamWaves * kStreamWaveLds;
+  for (uint32_t i = threadIdx.x; i < T / 16; i += blockDim.x)
+    reinterpret_cast<uint4*>(tpl)[i] = reinterpret_cast<const uint4*>(L.tpl)[i];
+  __syncthreads();
+  const uint4* const desc = reinterpret_cast<const uint4*>(tpl + (reinterpret_cast<const uint8_t*>(L.tpl_desc) - L.tpl));
   uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
   const unsigned long long ts = (unsigned long long)L.timestamp;
   const unsigned long long W = (unsigned long long)gridDim.x * kStreamWaves;
@@ -1061,7 +1064,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
         const long long lpos = L.first_position + (long long)(out_rec + jb + i);
         const uint32_t so = (uint32_t)(pos - sb);
         unsigned long long* const s64 = reinterpret_cast<unsigned long long*>(stage + so);
-        if (lane < size / 8) s64[lane] = reinterpret_cast<const unsigned long long*>(lds + d.x)[lane];
+        if (lane < size / 8) s64[lane] = reinterpret_cast<const unsigned long long*>(tpl + d.x)[lane];
         if (lane < 4)  // LogEntryDescriptor: position, source position, key, timestamp
           s64[2 + lane] = lane == 0 ? (unsigned long long)lpos : lane == 1 ? (unsigned long long)src
                           : lane == 2 ? (unsigned long long)key : ts;
