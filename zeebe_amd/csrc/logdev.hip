@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 
 #include "zb_internal.h"
@@ -1301,6 +1302,12 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
     // (opt-in until its GPU parity run: ZBHIP_LOG_STREAM=1)
     const bool stream = stream_ok && a.wkeys && a.tpl_lds && slds <= kStreamLdsMax && getenv("ZBHIP_LOG_STREAM") &&
                         !getenv("ZBHIP_LOG_HALFWAVE");
+    static bool told = false;
+    if (!told && getenv("ZBHIP_DEBUG")) {
+      told = true;
+      fprintf(stderr, "[zbhip] log write pass: %s (templates + descriptors %u B, LDS %zu B, attribute %s)\n",
+              stream ? "k_log_stream" : "k_log_write", a.tpl_lds, slds, stream_ok ? "ok" : "refused");
+    }
     if (a.n && a.compose != 2 && stream) {
       const uint32_t per_cu = (uint32_t)(kStreamLdsMax / slds) < 4 ? (uint32_t)(kStreamLdsMax / slds) : 4u;
       uint32_t grid = (uint32_t)cus * per_cu;

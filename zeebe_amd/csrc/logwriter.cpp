@@ -1384,6 +1384,11 @@ int log_device_templates(zbhip_serializer* s, std::vector<uint8_t>& bytes, std::
         r.message_key = -1;
         r.correlation_key = ZBHIP_NO_STRING;
         r.message_name = r.bpmn_process_id = 0xFFFF;
+        // only the kinds an element of its type has on the path (a sequence flow is only taken; every
+        // other element never is; unprocessed commands -- past the batch limit -- are composed): the
+        // table then fits LDS next to the device writer's stages (logdev.hip k_log_stream)
+        const bool flow = s->procs[p].els[e].type == ZBHIP_EL_SEQUENCE_FLOW;
+        if (flow ? k != 0 : (k == 0 || (k >= 7 && k <= 9))) continue;
         if (k < 13) {  // PROCESS_INSTANCE: events 1..7, unprocessed commands 8..10, processed ones (10 + ...)
           const uint32_t intent = k < 10 ? k + 1 : k - 2;
           r.value_type = ZBHIP_VT_PROCESS_INSTANCE;

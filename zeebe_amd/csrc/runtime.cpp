@@ -565,6 +565,8 @@ struct zbhip_handle {
   size_t fin_next = 0;             // the last run's key bookkeeping is done for commands < fin_next (advance)
   std::vector<uint32_t> ext_keys;  // keys the CPU engine generated for the window's fallback commands
   bool ext_ready = false;          // ext_keys / declared are the last run's (ensure_ext)
+  unsigned long long fb_seen = 0;           // fallbacks counted in the statistics rows so far
+  unsigned long long window_fallbacks = 0;  // ... in the last run
   std::vector<uint8_t> declared;   // ... declared by the adapter (zbhip_set_external_keys)
   // plan_rounds: (stamp, last round) per subject; window of the last command per instance slot
   std::vector<std::pair<uint32_t, uint32_t>> plan_last;
@@ -1412,7 +1414,9 @@ static bool slot_kind(uint8_t k) {
 // rounds (the reference processes them in log order).  Message commands may touch an instance of
 // this partition and instance commands a correlation slot, so a change between the two classes
 // starts a new epoch: every later command goes to a round after all earlier ones.
-static int plan_rounds(zbhip_handle* h) {
+// dev_cmds: the window's commands already uploaded (a large plain window): its subjects are checked
+// for repeats on the device (k_subject_check) instead of claimed on the host threads
+static int plan_rounds(zbhip_handle* h, const zbhip_command* dev_cmds = nullptr) {
   h->round_begin.clear();
   h->h_order.clear();
   // a CREATE into an instance slot that an earlier command of the same window addressed is refused:
@@ -1447,7 +1451,20 @@ static int plan_rounds(zbhip_handle* h) {
     return h->plan_stamp;
   };
   uint32_t stamp = next_stamp();
-  if (!msg && h->n_cmds >= (1u << 16)) {
+  if (!msg && h->n_cmds >= (1u << 16) && dev_cmds) {
+    if (++h->check_stamp == 0) {
+      HIPCHK(hipMemsetAsync(h->d_seen, 0, ((size_t)h->cfg.max_instances + h->st.n_slots) * sizeof(uint32_t), h->stream));
+      h->check_stamp = 1;
+    }
+    uint32_t flag = 0;
+    HIPCHK(hipMemsetAsync(h->d_check_flag, 0, sizeof(uint32_t), h->stream));
+    HIPCHK(launch_subject_check(reinterpret_cast<const uint4*>(dev_cmds), (uint32_t)h->n_cmds, h->cfg.max_instances,
+                                h->st.n_slots, h->d_seen, h->check_stamp, h->d_check_flag, h->stream));
+    HIPCHK(hipMemcpyAsync(&flag, h->d_check_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (flag & 2) return ZBHIP_EINVAL;
+    if (!(flag & 1)) return ZBHIP_OK;  // one round: identity order
+  } else if (!msg && h->n_cmds >= (1u << 16)) {
     // the common window addresses every instance once: claim the subjects on the worker threads
     // (an atomic stamp exchange each); a repeat falls through to the ordered pass below, with a
     // fresh stamp
@@ -1614,7 +1631,10 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   h->n_cmds = n;
   h->n_docs = n_docs;
   const auto t2 = now();
-  rc = plan_rounds(h);
+  // a large plain window goes up before planning, and its subjects are checked there
+  const bool early = !continues && !h->msg() && n >= (1u << 16);
+  if (early) HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
+  rc = plan_rounds(h, early ? reinterpret_cast<const zbhip_command*>(h->d_cmds) : nullptr);
   if (rc) {
     h->n_cmds = h->n_docs = h->n_xparts = 0;
     return rc;
@@ -1639,7 +1659,8 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
     cmds = h->h_cmds.data();
   }
   h->window_continues = continues;
-  if (n) HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
+  if (n && !early)
+    HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
   if (n_docs)
     HIPCHK(hipMemcpyAsync(h->d_docs, docs, n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice, h->stream));
   if (!h->h_order.empty())
@@ -2392,7 +2413,17 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
                        P.region_stride, B, step_rows(h->variant), h->d_rec, h->d_stats + 64 * 8, h->stream));
   unsigned long long total = 0;
   HIPCHK(hipMemcpyAsync(&total, h->d_stats + 64 * 8, sizeof total, hipMemcpyDeviceToHost, h->stream));
+  // the statistics rows: this window's fallback count (whether every command ran on the device)
+  unsigned long long srows[64 * 8];
+  HIPCHK(hipMemcpyAsync(srows, h->d_stats, sizeof srows, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  {
+    unsigned long long fb = 0;
+    for (int r = 0; r < 64; ++r) fb += srows[r * 8 + 4];
+    if (!accumulate) h->fb_seen = 0;
+    h->window_fallbacks = fb - h->fb_seen;
+    h->fb_seen = fb;
+  }
   const auto t1 = now();
   h->out_total = total;
   h->out_host = false;
@@ -4204,14 +4235,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   // sizes the entries.  Otherwise the host builds the table after finalize.
   bool dev_table = n > 0 && h->round_begin.empty() && h->fin_next == 0 && h->launches.size() == 1 &&
                    h->launches[0].src == 0 && h->launches[0].count == n && !getenv("ZBHIP_HOST_LOG_TABLE");
-  if (dev_table) {
-    std::atomic<bool> all_ok{true};
-    parallel_for(host_threads(), [&](unsigned t, unsigned TT) {
-      for (size_t c = n * t / TT; c < n * (t + 1) / TT && all_ok.load(std::memory_order_relaxed); ++c)
-        if (((h->h_hdr[c].y >> 16) & 0xFF) != ST_OK) all_ok = false;
-    });
-    dev_table = all_ok;
-  }
+  if (dev_table) dev_table = h->window_fallbacks == 0;  // (every command of the window ran on the device)
   const unsigned long long key_base = (unsigned long long)h->key_counter;  // (fin_next == 0: the window's base)
   if (!dev_table)
     if (int rc = finalize(h)) return rc;
