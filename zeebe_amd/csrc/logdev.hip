@@ -933,13 +933,20 @@ __device__ __forceinline__ unsigned long long rl64(unsigned long long v, uint32_
   return (unsigned long long)rl((uint32_t)v, k) | (unsigned long long)rl((uint32_t)(v >> 32), k) << 32;
 }
 
+// orders one wave's LDS accesses across its lanes for the compiler (the hardware keeps a wave's LDS
+// operations in order)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // the stage's bytes [gs, ge) out (stage byte 0 = output byte sb = gs & ~15): whole 16-byte chunks, and
 // the 8-byte half of a chunk shared with the neighbouring group
 __device__ __forceinline__ void stream_flush(uint8_t* out, const uint8_t* stage, unsigned long long sb,
                                              unsigned long long gs, unsigned long long ge, uint32_t lane) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();  // (the stage's words, written by other lanes, before the chunk reads)
   for (unsigned long long o = sb + 16ull * lane; o < ge; o += 1024ull) {
     const uint4 v = *reinterpret_cast<const uint4*>(stage + (o - sb));
     const bool h0 = o >= gs && o + 8 <= ge, h1 = o + 8 >= gs && o + 16 <= ge;
@@ -957,7 +964,7 @@ __device__ __forceinline__ void stream_flush(uint8_t* out, const uint8_t* stage,
       __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o + 8));
     }
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();  // (the chunk reads before the next group's words)
 }
 
 __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
@@ -1021,7 +1028,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
       p += nk;
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loads above have landed in LDS
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     p = 0;
     for (uint32_t k = 0; k < take; ++k) {
       const unsigned long long out_rec = rl64(m.out_rec, k), key0 = rl64(m.key0, k);
@@ -1063,17 +1070,20 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
         const uint4 d = desc[(info >> 16) - 1];
         const long long key = wkey(rx & 0xFFFF), scope = wkey(rx >> 16);
         const long long lpos = L.first_position + (long long)(out_rec + jb + i);
+        // lane w's word of the entry, finished in registers (one store per lane: no lane writes a
+        // word another lane wrote): the template word, the LogEntryDescriptor's position / source
+        // position / key / timestamp, the big-endian processInstanceKey / scope key patched in
         const uint32_t so = (uint32_t)(pos - sb);
-        unsigned long long* const s64 = reinterpret_cast<unsigned long long*>(stage + so);
-        if (lane < size / 8) s64[lane] = reinterpret_cast<const unsigned long long*>(tpl + d.x)[lane];
-        if (lane < 4)  // LogEntryDescriptor: position, source position, key, timestamp
-          s64[2 + lane] = lane == 0 ? (unsigned long long)lpos : lane == 1 ? (unsigned long long)src
-                          : lane == 2 ? (unsigned long long)key : ts;
-        if (lane < 16) {  // msgpack uint64 (big-endian) processInstanceKey / scope key
-          const bool sc = lane >= 8;
-          const uint32_t at = sc ? d.z : d.y >> 16;
-          const unsigned long long x = (unsigned long long)(sc ? scope : pik);
-          if (at) stage[so + at + (lane & 7)] = (uint8_t)(x >> (56 - 8 * (lane & 7)));
+        if (lane < size / 8) {
+          StreamEnt e;
+          e.off = d.x;
+          e.pa = d.y >> 16;
+          e.sa = d.z;
+          e.key = key;
+          e.scope = scope;
+          e.pik = pik;
+          e.lpos = lpos;
+          reinterpret_cast<unsigned long long*>(stage + so)[lane] = tpl_word(tpl, e, 8 * lane, src, ts);
         }
         pos += size;
       }
