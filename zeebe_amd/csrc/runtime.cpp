@@ -332,6 +332,11 @@ struct PinnedVec {
   const T* end() const { return p + n; }
   T& operator[](size_t i) { return p[i]; }
   const T& operator[](size_t i) const { return p[i]; }
+  void swap(PinnedVec& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+  }
 };
 
 // The resolve_key table: BatchRefs in key order, in segments (one per plain window, or appended
@@ -539,6 +544,7 @@ struct zbhip_handle {
   const uint4* ext_cmds = nullptr;
   const zbhip_doc_entry* ext_docs = nullptr;
   PinnedVec<zbhip_command> h_cmds;  // (pinned: the upload source of host windows)
+  PinnedVec<zbhip_command> h_cmds_next;  // the next window's, validated and copied in one pass
   std::vector<zbhip_doc_entry> h_docs;
   size_t n_cmds = 0, n_docs = 0;
   std::vector<uint32_t> round_begin;
@@ -1589,31 +1595,34 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   // handle as it was); the first failing command's code wins, as in one pass
   std::atomic<bool> continues_any{false};
   {
+    // one pass over the caller's commands: each block validated, then copied (into the next
+    // window's pinned buffer, swapped in once the whole window validated: a refused window leaves the
+    // handle as it was)
     const unsigned T = n >= (1u << 16) ? host_threads() : 1u;
     std::vector<std::pair<size_t, int>> fail(T, {~(size_t)0, ZBHIP_OK});
+    h->h_cmds_next.resize(n);
+    zbhip_command* const dst = h->h_cmds_next.data();
     parallel_for(T, [&](unsigned t, unsigned TT) {
       const size_t lo = n * t / TT, hi = n * (t + 1) / TT;
+      bool cont = false;
       for (size_t b = lo; b < hi; b += 4096) {
         const size_t e = std::min(hi, b + 4096);
-        if (validate(h, cmds + b, e - b, n_docs, xparts, n_xparts) == ZBHIP_OK) continue;
-        for (size_t i = b; i < e; ++i)  // the block's first failing command
-          if (int ri = validate(h, cmds + i, 1, n_docs, xparts, n_xparts)) {
-            fail[t] = {i, ri};
-            return;
-          }
+        if (validate(h, cmds + b, e - b, n_docs, xparts, n_xparts) != ZBHIP_OK) {
+          for (size_t i = b; i < e; ++i)  // the block's first failing command
+            if (int ri = validate(h, cmds + i, 1, n_docs, xparts, n_xparts)) {
+              fail[t] = {i, ri};
+              return;
+            }
+        }
+        memcpy(dst + b, cmds + b, (e - b) * sizeof(zbhip_command));
+        for (size_t i = b; i < e; ++i) cont |= cmds[i].kind == ZBHIP_CMD_CONTINUE;
       }
+      if (cont) continues_any = true;
     });
     for (const auto& f : fail)
       if (f.second) return f.second;  // ranges in log order: the first range's failure is the first
     h->external = false;
-    h->h_cmds.resize(n);
-    parallel_for(T, [&](unsigned t, unsigned TT) {
-      const size_t lo = n * t / TT, hi = n * (t + 1) / TT;
-      if (hi > lo) memcpy(h->h_cmds.data() + lo, cmds + lo, (hi - lo) * sizeof(zbhip_command));
-      bool cont = false;
-      for (size_t i = lo; i < hi; ++i) cont |= cmds[i].kind == ZBHIP_CMD_CONTINUE;
-      if (cont) continues_any = true;
-    });
+    h->h_cmds.swap(h->h_cmds_next);
   }
   bool continues = continues_any.load();
   if (continues) {
