@@ -1468,8 +1468,10 @@ static int plan_rounds(zbhip_handle* h, const zbhip_command* dev_cmds = nullptr)
                                 h->st.n_slots, h->d_seen, h->check_stamp, h->d_check_flag, h->stream));
     HIPCHK(hipMemcpyAsync(&flag, h->d_check_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
-    if (flag & 2) return ZBHIP_EINVAL;
-    if (!(flag & 1)) return ZBHIP_OK;  // one round: identity order
+    // (flag 2: a kind the device check does not know -- validated on the host already: the ordered
+    // pass below decides)
+    if (!flag) return ZBHIP_OK;  // one round: identity order
+    stamp = next_stamp();
   } else if (!msg && h->n_cmds >= (1u << 16)) {
     // the common window addresses every instance once: claim the subjects on the worker threads
     // (an atomic stamp exchange each); a repeat falls through to the ordered pass below, with a
