@@ -374,3 +374,21 @@ def test_pass_through_element_parity(kind):
     drive(xml, 200)
     b = bpmn.createExecutableProcess("process").startEvent("start")
     drive(getattr(b, kind)("elem").done(), 50)  # the element ends the execution path
+
+
+def test_gpu_large_host_windows_with_repeated_subjects():
+    # windows of >= 2^16 host commands: subjects checked on the device (k_subject_check); a window
+    # addressing an instance twice is planned into rounds on the host -- both as the oracle
+    n = 70000
+    xml = bpmn.linear_process(2)
+    part, orc = Partition(max_instances=n, max_commands=n + 64, max_records_per_batch=64), Oracle()
+    assert part.deploy(xml) == orc.deploy(xml) == 0
+    recs = run_both(part, orc, create_commands(n))
+    jobs = [int(r["key"]) for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+    refs = [part.resolve_key(k) for k in jobs]
+    c = abi.make_commands(len(refs) + 3)
+    c["kind"] = abi.CMD_JOB_COMPLETE
+    for i, (inst, o) in enumerate(refs + refs[:3]):  # the first three instances again: rounds
+        c[i]["instance"], c[i]["ref"] = inst, o
+    run_both(part, orc, c)
+    assert part.state() == orc.state()
