@@ -234,3 +234,82 @@ def test_gpu_device_exchange_runs_the_protocol(P):
         assert s["transitions"] == c["transitions"] and s["completed_instances"] == c["completed_instances"]
     # records of every partition (device stats) = the oracle's
     assert sum(s["records"] for s in st) == sum(len(r) for _, _, r, _ in orc.log)
+
+
+def _exchange_protocol(P, n, drain):
+    """test_gpu_device_exchange_runs_the_protocol's device path with results: every window's drained
+    records and outbox, and the final states."""
+    import torch
+    from zeebe_amd.exchange import LocalExchange
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev).cuda_stream
+    parts = [Partition(partition_id=p, partition_count=P, max_instances=n, max_commands=4 * n,
+                       max_correlation_keys=n * P, max_records_per_batch=128, stream=stream) for p in range(1, P + 1)]
+    keys = ["k-%d-%d" % (p, i) for p in range(1, P + 1) for i in range(n)]
+    for part in parts:
+        part.deploy(XML)
+        ids = part.intern_strings(keys)
+    var_id, name_id = parts[0].intern("key"), parts[0].intern("msg")
+    owner = parts[0].string_partitions(ids, P)
+    out, bufs = [], []
+
+    def collect(tag):
+        for p, part in enumerate(parts, 1):
+            if part.L.zbhip_pending_records(part.h) or tag == "create":
+                out.append((tag, p, part.drain().copy(), part.outbox().copy()))
+
+    for p, part in enumerate(parts, 1):
+        c = create_commands(n)
+        c["doc_count"] = 1
+        c["doc_begin"] = np.arange(n)
+        d = string_docs(var_id, ids[(p - 1) * n:p * n])
+        tc = torch.from_numpy(c.view(np.uint8).copy()).to(dev)
+        td = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        bufs += [tc, td]
+        part.submit_device(tc.data_ptr(), n, td.data_ptr(), n)
+        part.run(0)
+        out.append(("create", p, part.drain().copy(), part.outbox().copy()))
+    ex = LocalExchange(parts, 4 * n, dev)
+    for phase in ("subscribe", "publish", "correlate"):
+        if phase == "publish":
+            for p, part in enumerate(parts, 1):
+                mine = ids[owner == p]
+                pub = abi.make_commands(len(mine))
+                pub["instance"] = mine
+                pub["kind"] = abi.CMD_PUBLISH
+                pub["ref"] = name_id
+                tp = torch.from_numpy(pub.view(np.uint8).copy()).to(dev)
+                bufs.append(tp)
+                part.submit_device(tp.data_ptr(), len(mine))
+                part.run(0)
+                out.append(("publish", p, part.drain().copy(), part.outbox().copy()))
+            continue
+        for r in range(4):
+            sizes = ex.step()
+            if sum(sizes) == 0:
+                break
+            for t, part in enumerate(parts):
+                if sizes[t]:
+                    part.submit_xparts_device(ex.inbox[t].data_ptr(), sizes[t])
+                    part.run(0)
+                    out.append((phase, t + 1, part.drain().copy(), part.outbox().copy()))
+    torch.cuda.synchronize()
+    return out, [part.state() for part in parts]
+
+
+def test_gpu_subject_sorted_device_windows(monkeypatch):
+    # a message partition's device window launched in subject order (ZBHIP_SUBJECT_SORT): the same
+    # records, outboxes and states as the window in arrival order
+    monkeypatch.delenv("ZBHIP_SUBJECT_SORT", raising=False)
+    base, base_state = _exchange_protocol(4, 512, True)
+    monkeypatch.setenv("ZBHIP_SUBJECT_SORT", "1")
+    got, got_state = _exchange_protocol(4, 512, True)
+    assert len(got) == len(base)
+    for (t1, p1, r1, o1), (t2, p2, r2, o2) in zip(got, base):
+        assert (t1, p1) == (t2, p2)
+        assert len(r1) == len(r2) and len(o1) == len(o2), (t1, p1)
+        for f in abi.PARITY_FIELDS:
+            assert np.array_equal(r1[f], r2[f]), (t1, p1, f)
+        for f in XPART_FIELDS:
+            assert np.array_equal(o1[f], o2[f]), (t1, p1, f)
+    assert got_state == base_state

@@ -28,6 +28,7 @@
 // k_scan_regions / k_gather (drain path only): exclusive scan of the per-chunk record totals and
 // an ordered copy of every chunk's records into one contiguous append buffer.
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -3262,6 +3263,37 @@ __global__ __launch_bounds__(256) void k_subject_check(const uint4* cmds, uint32
     }
   }
   if (f) atomicOr(flag, f);  // rare: a faulty window
+}
+
+// A device window's launch order by subject (instance slots, then correlation slots): the stable
+// radix sort keeps a subject's commands in log order, and a wave's lanes then read neighbouring
+// instance rows (an exchange inbox arrives as one run per sending partition, each spread over the
+// receiver's slots).  The records still come out per command (the drain and the key scan index
+// commands, not lanes).
+__global__ __launch_bounds__(256) void k_subject_keys(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t* keys,
+                                                      uint32_t* idx) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint4 c = cmds[i];
+  const uint32_t kind = c.y & 0xFF;
+  const bool sk = kind == ZBHIP_CMD_PUBLISH || kind == ZBHIP_CMD_MSG_SUB_CREATE || kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
+  keys[i] = (sk ? n_inst : 0u) + c.x;
+  idx[i] = i;
+}
+size_t subject_sort_temp_bytes(uint32_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32);
+  return bytes;
+}
+hipError_t launch_subject_sort(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_subjects, uint32_t* k0,
+                               uint32_t* k1, uint32_t* v0, uint32_t* order, void* temp, size_t temp_bytes,
+                               hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_subject_keys, dim3((n + 255) / 256), dim3(256), 0, s, cmds, n, n_inst, k0, v0);
+  int bits = 1;
+  while (bits < 32 && (1ull << bits) < n_subjects) ++bits;
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, order, (int)n, 0, bits, s);
 }
 
 // JOB_BATCH:ACTIVATE on the device (JobBatchActivatedApplier -> DbJobState.activate): the jobs the

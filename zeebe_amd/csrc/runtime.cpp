@@ -55,6 +55,10 @@ int log_device_templates(zbhip_serializer* s, std::vector<uint8_t>& bytes, std::
                          std::vector<uint32_t>& idx);
 void serializer_broker(const zbhip_serializer* s, int32_t out[3]);
 size_t activated_out_bytes();
+size_t subject_sort_temp_bytes(uint32_t n);
+hipError_t launch_subject_sort(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_subjects, uint32_t* k0,
+                               uint32_t* k1, uint32_t* v0, uint32_t* order, void* temp, size_t temp_bytes,
+                               hipStream_t s);
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
                                 uint32_t stamp, uint32_t* flag, hipStream_t s);
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t xcap,
@@ -492,6 +496,10 @@ struct zbhip_handle {
   uint4* d_cmds = nullptr;
   zbhip_doc_entry* d_docs = nullptr;
   uint32_t* d_order = nullptr;
+  bool order_on_device = false;  // h_order is d_order's (a device window sorted by subject): copied on use
+  uint32_t* d_sort = nullptr;    // [3][max_commands] subject keys in / out, indices in
+  void* d_sort_temp = nullptr;
+  size_t sort_temp_bytes = 0;
   uint2* d_rec = nullptr;
   uint2* d_cmd_hdr = nullptr;
   uint2* d_regions = nullptr;                // [regions][128 * rec_cap] per-workgroup record regions
@@ -865,6 +873,8 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_cmds);
   (void)hipFree(h->d_docs);
   (void)hipFree(h->d_order);
+  (void)hipFree(h->d_sort);
+  (void)hipFree(h->d_sort_temp);
   (void)hipFree(h->d_rec);
   (void)hipFree(h->d_cmd_hdr);
   (void)hipFree(h->d_regions);
@@ -1744,6 +1754,23 @@ int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_
   h->n_docs = n_docs;
   h->round_begin.clear();
   h->h_order.clear();
+  h->order_on_device = false;
+  // a message partition's window in subject order (one round: its subjects are distinct) -- opt-in
+  // until measured (ZBHIP_SUBJECT_SORT=1)
+  const char* sort_env = getenv("ZBHIP_SUBJECT_SORT");  // (its value: the smallest window sorted)
+  if (h->msg() && sort_env && n >= (size_t)std::max(1, atoi(sort_env))) {
+    const size_t cap = h->cfg.max_commands;
+    if (!h->d_sort) {
+      h->sort_temp_bytes = subject_sort_temp_bytes((uint32_t)cap);
+      if (dalloc(&h->d_sort, 3 * cap) != hipSuccess || hipMalloc(&h->d_sort_temp, h->sort_temp_bytes + 256) != hipSuccess)
+        return ZBHIP_ENOMEM;
+    }
+    HIPCHK(launch_subject_sort(reinterpret_cast<const uint4*>(dev_cmds), (uint32_t)n, h->cfg.max_instances,
+                               h->cfg.max_instances + h->st.n_slots, h->d_sort, h->d_sort + cap, h->d_sort + 2 * cap,
+                               h->d_order, h->d_sort_temp, h->sort_temp_bytes, h->stream));
+    h->round_begin = {0u, (uint32_t)n};
+    h->order_on_device = true;
+  }
   h->doc_base = h->next_doc_base;
   h->next_doc_base += (int64_t)n_docs;
   h->source_base = h->next_source;
@@ -1766,6 +1793,12 @@ static hipEvent_t next_event(zbhip_handle* h) {
 // order, lanes follow the launch order
 static int compute_offsets(zbhip_handle* h) {
   if (h->off_ready) return ZBHIP_OK;
+  if (h->order_on_device) {  // the launch order of a subject-sorted device window
+    h->h_order.resize(h->round_begin.empty() ? 0 : h->round_begin.back());
+    if (!h->h_order.empty())
+      HIPCHK(hipMemcpy(h->h_order.data(), h->d_order, h->h_order.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    h->order_on_device = false;
+  }
   const uint32_t n = (uint32_t)h->n_cmds;
   const uint64_t total = h->out_total;
   h->h_off.resize(n + 1);
