@@ -254,8 +254,10 @@ __device__ __forceinline__ bool key_of(const LogParams& L, uint32_t c, uint32_t 
 // per command and kept -- every record of a batch repeats them, and re-reading them per record missed
 // L2 under the write stream (PMC: ~200 B fetched per written entry).
 struct KeyCache {
-  uint32_t o0 = NONE, o1 = NONE;
-  long long k0 = -1, k1 = -1;
+  uint32_t o0 = NONE, o1 = NONE, o2 = NONE;
+  long long k0 = -1, k1 = -1, k2 = -1;
+  bool has_pi = false;  // the process instance's key (ordinal 0), kept apart: every record names it
+  long long kpi = -1;
 };
 __device__ __forceinline__ bool key_of_lane(const LogParams& L, const LogCmd& m, uint32_t ord, long long& key,
                                             KeyCache& kc) {
@@ -264,9 +266,18 @@ __device__ __forceinline__ bool key_of_lane(const LogParams& L, const LogCmd& m,
     key = L.pbits + (long long)(m.key0 + (uint16_t)(ord - m.first_ord));
     return true;
   }
+  if (ord == 0 && kc.has_pi) { key = kc.kpi; return true; }
   if (ord == kc.o0) { key = kc.k0; return true; }
   if (ord == kc.o1) { key = kc.k1; return true; }
+  if (ord == kc.o2) { key = kc.k2; return true; }
   if (!key_of(L, m.first_ord == 0 ? 0xFFFFFFFFu : m.prev, m.instance, ord, key)) return false;
+  if (ord == 0) {
+    kc.has_pi = true;
+    kc.kpi = key;
+    return true;
+  }
+  kc.o2 = kc.o1;
+  kc.k2 = kc.k1;
   kc.o1 = kc.o0;
   kc.k1 = kc.k0;
   kc.o0 = ord;
@@ -685,8 +696,10 @@ __global__ __launch_bounds__(256) void k_log_sizes(LogParams L) {
       k.pik = pik;
       k.k0 = kc.k0;
       k.k1 = kc.k1;
+      k.k2 = kc.k2;
       k.o0 = kc.o0;
       k.o1 = kc.o1;
+      k.o2 = kc.o2;
       L.wkeys[c] = k;
     }
   }
@@ -1036,7 +1049,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
       const uint32_t first_ord = rl(m.first_ord, k), nkeys = rl(m.nkeys, k);
       const long long pik = (long long)rl64((unsigned long long)mk.pik, k);
       const long long k0 = (long long)rl64((unsigned long long)mk.k0, k), k1 = (long long)rl64((unsigned long long)mk.k1, k);
-      const uint32_t o0 = rl(mk.o0, k), o1 = rl(mk.o1, k);
+      const long long k2 = (long long)rl64((unsigned long long)mk.k2, k);
+      const uint32_t o0 = rl(mk.o0, k), o1 = rl(mk.o1, k), o2 = rl(mk.o2, k);
       const uint32_t jb = k == 0 ? j0 : 0u;
       const uint32_t nk = k == 0 ? first : rl(cnt, k);
       auto wkey = [&](uint32_t ord) -> long long {
@@ -1045,7 +1059,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
         if (ord == 0) return pik;
         if (ord == o0) return k0;
         if (ord == o1) return k1;
-        long long key = 0;  // (a third older ordinal: the key chain in memory)
+        if (ord == o2) return k2;
+        long long key = 0;  // (a fourth older ordinal: the key chain in memory)
         key_of(L, first_ord == 0 ? 0xFFFFFFFFu : rl(m.prev, k), rl(m.instance, k), ord, key);
         return key;
       };

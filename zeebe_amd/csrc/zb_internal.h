@@ -284,10 +284,10 @@ struct LogCmd {
   uint32_t pad;                // the command's pad (TIMER:TRIGGER: dueDate high word)
 };
 // the keys older than its own batch that a command's records name, found by the size pass for the
-// write pass: the process instance's (ordinal 0) and the last two others it looked up
+// write pass: the process instance's (ordinal 0) and the last three others it looked up
 struct LogKeys {
-  long long pik, k0, k1;
-  uint32_t o0, o1;             // ordinals of k0 / k1 (NONE: empty)
+  long long pik, k0, k1, k2;
+  uint32_t o0, o1, o2, pad;    // ordinals of k0 / k1 / k2 (NONE: empty)
 };
 struct LogLaunch {
   int phase;                   // 0 sizes + offsets, 1 write, 2 key ring, 3 command table
