@@ -931,10 +931,13 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
 // consecutive words: no bank conflicts), lanes 0-3 write the header's position / source position /
 // key / timestamp, lanes 0-15 the big-endian processInstanceKey / scope key bytes.  A full stage, a
 // composed entry (k_log_compose writes it) or the command's end flushes the stage in 16-byte chunks.
-constexpr uint32_t kStreamWaves = 8;
+#ifndef ZB_STREAM_WAVES
+#define ZB_STREAM_WAVES 16  // 4 waves per SIMD (one 1024-thread workgroup per CU)
+#endif
+constexpr uint32_t kStreamWaves = ZB_STREAM_WAVES;
 constexpr uint32_t kStreamCmds = 32;
-constexpr uint32_t kStreamRecs = 256;
-constexpr uint32_t kStreamStage = 4096;
+constexpr uint32_t kStreamRecs = 128;
+constexpr uint32_t kStreamStage = 3072;
 constexpr uint32_t kStreamWaveLds = kStreamStage + kStreamRecs * 12;  // stage, rinfo, rows
 constexpr uint32_t kStreamLdsMax = 160 * 1024;
 
@@ -1066,41 +1069,55 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
       };
       unsigned long long pos = k == 0 && j0 ? gpos : rl64(mb, k);
       unsigned long long gs = pos, sb = pos & ~15ull;
-      for (uint32_t i = 0; i < nk; ++i) {
-        const uint32_t info = lri[p + i];
-        const uint32_t size = info & 0xFFFF;
-        if (info & kSlow) {  // composed by k_log_compose
-          stream_flush(out, stage, sb, gs, pos, lane);
-          pos += size;
-          gs = pos;
-          sb = pos & ~15ull;
-          continue;
+      for (uint32_t i0 = 0; i0 < nk; i0 += 64) {
+        // lane j resolves record i0 + j at once (its template, keys): one round of LDS reads for the
+        // whole group; the entries then take their fields from the lanes by v_readlane
+        const uint32_t ng = nk - i0 < 64 ? nk - i0 : 64u;
+        uint32_t v_info = 0, v_off = 0, v_pa = 0, v_sa = 0;
+        long long v_key = 0, v_scope = 0;
+        if (lane < ng) {
+          v_info = lri[p + i0 + lane];
+          if (!(v_info & kSlow)) {
+            const uint32_t rx = lrow[2 * (p + i0 + lane)];
+            const uint4 d = desc[(v_info >> 16) - 1];
+            v_off = d.x;
+            v_pa = d.y >> 16;
+            v_sa = d.z;
+            v_key = wkey(rx & 0xFFFF);
+            v_scope = wkey(rx >> 16);
+          }
         }
-        if (pos + size - sb > kStreamStage) {
-          stream_flush(out, stage, sb, gs, pos, lane);
-          gs = pos;
-          sb = pos & ~15ull;
-        }
-        const uint32_t rx = lrow[2 * (p + i)];
-        const uint4 d = desc[(info >> 16) - 1];
-        const long long key = wkey(rx & 0xFFFF), scope = wkey(rx >> 16);
-        const long long lpos = L.first_position + (long long)(out_rec + jb + i);
-        // lane w's word of the entry, finished in registers (one store per lane: no lane writes a
-        // word another lane wrote): the template word, the LogEntryDescriptor's position / source
-        // position / key / timestamp, the big-endian processInstanceKey / scope key patched in
-        const uint32_t so = (uint32_t)(pos - sb);
-        if (lane < size / 8) {
+        for (uint32_t i = 0; i < ng; ++i) {
+          const uint32_t info = rl(v_info, i);
+          const uint32_t size = info & 0xFFFF;
+          if (info & kSlow) {  // composed by k_log_compose
+            stream_flush(out, stage, sb, gs, pos, lane);
+            pos += size;
+            gs = pos;
+            sb = pos & ~15ull;
+            continue;
+          }
+          if (pos + size - sb > kStreamStage) {
+            stream_flush(out, stage, sb, gs, pos, lane);
+            gs = pos;
+            sb = pos & ~15ull;
+          }
+          // lane w's word of the entry, finished in registers (one store per lane: no lane writes a
+          // word another lane wrote): the template word, the LogEntryDescriptor's position / source
+          // position / key / timestamp, the big-endian processInstanceKey / scope key patched in
+          const uint32_t so = (uint32_t)(pos - sb);
           StreamEnt e;
-          e.off = d.x;
-          e.pa = d.y >> 16;
-          e.sa = d.z;
-          e.key = key;
-          e.scope = scope;
+          e.off = rl(v_off, i);
+          e.pa = rl(v_pa, i);
+          e.sa = rl(v_sa, i);
+          e.key = (long long)rl64((unsigned long long)v_key, i);
+          e.scope = (long long)rl64((unsigned long long)v_scope, i);
           e.pik = pik;
-          e.lpos = lpos;
-          reinterpret_cast<unsigned long long*>(stage + so)[lane] = tpl_word(tpl, e, 8 * lane, src, ts);
+          e.lpos = L.first_position + (long long)(out_rec + jb + i0 + i);
+          if (lane < size / 8)
+            reinterpret_cast<unsigned long long*>(stage + so)[lane] = tpl_word(tpl, e, 8 * lane, src, ts);
+          pos += size;
         }
-        pos += size;
       }
       stream_flush(out, stage, sb, gs, pos, lane);
       p += nk;
