@@ -1114,8 +1114,23 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
           e.scope = (long long)rl64((unsigned long long)v_scope, i);
           e.pik = pik;
           e.lpos = L.first_position + (long long)(out_rec + jb + i0 + i);
+#ifdef ZB_STREAM_TWOPHASE  // (A/B: the template copied as is, then the header words and key bytes over it)
+          unsigned long long* const s64 = reinterpret_cast<unsigned long long*>(stage + so);
+          if (lane < size / 8) s64[lane] = reinterpret_cast<const unsigned long long*>(tpl + e.off)[lane];
+          wave_lds_sync();
+          if (lane >= 2 && lane < 6)
+            s64[lane] = lane == 2 ? (unsigned long long)e.lpos : lane == 3 ? (unsigned long long)src
+                        : lane == 4 ? (unsigned long long)e.key : ts;
+          if (lane >= 8 && lane < 24) {
+            const bool sc = lane >= 16;
+            const uint32_t at = sc ? e.sa : e.pa;
+            const unsigned long long x = (unsigned long long)(sc ? e.scope : e.pik);
+            if (at) stage[so + at + (lane & 7)] = (uint8_t)(x >> (56 - 8 * (lane & 7)));
+          }
+#else
           if (lane < size / 8)
             reinterpret_cast<unsigned long long*>(stage + so)[lane] = tpl_word(tpl, e, 8 * lane, src, ts);
+#endif
           pos += size;
         }
       }
