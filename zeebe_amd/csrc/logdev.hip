@@ -1114,7 +1114,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
           e.scope = (long long)rl64((unsigned long long)v_scope, i);
           e.pik = pik;
           e.lpos = L.first_position + (long long)(out_rec + jb + i0 + i);
-#ifdef ZB_STREAM_TWOPHASE  // (A/B: the template copied as is, then the header words and key bytes over it)
+#ifndef ZB_STREAM_REGWORD  // the template copied as is, then the header words and key bytes over it (fewer
+                           // VALU than finishing each word in registers, the ZB_STREAM_REGWORD variant)
           unsigned long long* const s64 = reinterpret_cast<unsigned long long*>(stage + so);
           if (lane < size / 8) s64[lane] = reinterpret_cast<const unsigned long long*>(tpl + e.off)[lane];
           wave_lds_sync();
