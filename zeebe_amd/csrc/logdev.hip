@@ -958,26 +958,27 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // the stage's bytes [gs, ge) out (stage byte 0 = output byte sb = gs & ~15): whole 16-byte chunks, and
 // the 8-byte half of a chunk shared with the neighbouring group
-__device__ __forceinline__ void stream_flush(uint8_t* out, const uint8_t* stage, unsigned long long sb,
-                                             unsigned long long gs, unsigned long long ge, uint32_t lane) {
+__device__ __forceinline__ void stream_flush(uint8_t* obase, const uint8_t* stage, uint32_t sb, uint32_t gs,
+                                             uint32_t ge, uint32_t lane) {
+  // (offsets relative to obase, a 16-byte aligned output address: 32-bit arithmetic)
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   wave_lds_sync();  // (the stage's words, written by other lanes, before the chunk reads)
-  for (unsigned long long o = sb + 16ull * lane; o < ge; o += 1024ull) {
+  for (uint32_t o = sb + 16u * lane; o < ge; o += 1024u) {
     const uint4 v = *reinterpret_cast<const uint4*>(stage + (o - sb));
     const bool h0 = o >= gs && o + 8 <= ge, h1 = o + 8 >= gs && o + 16 <= ge;
     if (h0 && h1) {
       u32x4 q;
       q.x = v.x; q.y = v.y; q.z = v.z; q.w = v.w;
-      __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out + o));
+      __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(obase + o));
     } else if (h0) {
       u32x2 q;
       q.x = v.x; q.y = v.y;
-      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o));
+      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(obase + o));
     } else if (h1) {
       u32x2 q;
       q.x = v.z; q.y = v.w;
-      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(out + o + 8));
+      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(obase + o + 8));
     }
   }
   wave_lds_sync();  // (the chunk reads before the next group's words)
@@ -1067,8 +1068,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
         key_of(L, first_ord == 0 ? 0xFFFFFFFFu : rl(m.prev, k), rl(m.instance, k), ord, key);
         return key;
       };
-      unsigned long long pos = k == 0 && j0 ? gpos : rl64(mb, k);
-      unsigned long long gs = pos, sb = pos & ~15ull;
+      const unsigned long long pos0 = k == 0 && j0 ? gpos : rl64(mb, k);
+      uint8_t* const obase = out + (pos0 & ~15ull);
+      const long long lpos0 = L.first_position + (long long)(out_rec + jb);
+      uint32_t pos = (uint32_t)(pos0 & 15u);  // (relative to obase)
+      uint32_t gs = pos, sb = 0;
       for (uint32_t i0 = 0; i0 < nk; i0 += 64) {
         // lane j resolves record i0 + j at once (its template, keys): one round of LDS reads for the
         // whole group; the entries then take their fields from the lanes by v_readlane
@@ -1091,21 +1095,21 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
           const uint32_t info = rl(v_info, i);
           const uint32_t size = info & 0xFFFF;
           if (info & kSlow) {  // composed by k_log_compose
-            stream_flush(out, stage, sb, gs, pos, lane);
+            stream_flush(obase, stage, sb, gs, pos, lane);
             pos += size;
             gs = pos;
-            sb = pos & ~15ull;
+            sb = pos & ~15u;
             continue;
           }
           if (pos + size - sb > kStreamStage) {
-            stream_flush(out, stage, sb, gs, pos, lane);
+            stream_flush(obase, stage, sb, gs, pos, lane);
             gs = pos;
-            sb = pos & ~15ull;
+            sb = pos & ~15u;
           }
           // lane w's word of the entry, finished in registers (one store per lane: no lane writes a
           // word another lane wrote): the template word, the LogEntryDescriptor's position / source
           // position / key / timestamp, the big-endian processInstanceKey / scope key patched in
-          const uint32_t so = (uint32_t)(pos - sb);
+          const uint32_t so = pos - sb;
           StreamEnt e;
           e.off = rl(v_off, i);
           e.pa = rl(v_pa, i);
@@ -1113,7 +1117,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
           e.key = (long long)rl64((unsigned long long)v_key, i);
           e.scope = (long long)rl64((unsigned long long)v_scope, i);
           e.pik = pik;
-          e.lpos = L.first_position + (long long)(out_rec + jb + i0 + i);
+          e.lpos = lpos0 + (long long)(i0 + i);
 #ifndef ZB_STREAM_REGWORD  // the template copied as is, then the header words and key bytes over it (fewer
                            // VALU than finishing each word in registers, the ZB_STREAM_REGWORD variant)
           unsigned long long* const s64 = reinterpret_cast<unsigned long long*>(stage + so);
@@ -1135,9 +1139,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
           pos += size;
         }
       }
-      stream_flush(out, stage, sb, gs, pos, lane);
+      stream_flush(obase, stage, sb, gs, pos, lane);
       p += nk;
-      gpos = pos;
+      gpos = (pos0 & ~15ull) + pos;
     }
     if (partial) {
       j0 += first;
