@@ -4125,7 +4125,7 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
   }
   // the device's activation table (the deadline and worker of ACTIVATED jobs, for their later records)
   hipError_t e = hipSuccess;
-  if (!h->st.act && getenv("ZBHIP_DEVICE_ACTIVATIONS")) {  // (opt-in until its GPU parity run)
+  if (!h->st.act && !getenv("ZBHIP_NO_DEVICE_ACTIVATIONS")) {  // (off: activated jobs' windows go to the host serialiser)
     const size_t words = (size_t)kSlots * h->cfg.max_instances;
     if (dalloc(&h->st.act, words) != hipSuccess || dalloc(&h->d_cmd_act, (size_t)h->cfg.max_commands) != hipSuccess) {
       (void)hipFree(d_list);
@@ -4402,8 +4402,8 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
   auto tu = now(), tf = now();
   bool spec = false;  // k_log_write launched before the total was known
   // the window's key bookkeeping journaled on the device (fold_journal) instead of booked here
-  // (opt-in until its GPU parity run: ZBHIP_JOURNAL=1)
-  bool journal = dev_table && !h->job_index_on && !h->msg() && getenv("ZBHIP_JOURNAL") && !getenv("ZBHIP_NO_JOURNAL");
+  // (ZBHIP_NO_JOURNAL=1: booked on the host after every window, as before round 4)
+  bool journal = dev_table && !h->job_index_on && !h->msg() && !getenv("ZBHIP_NO_JOURNAL");
   uint32_t jslot = 0;
   if (journal && !h->d_jrn) {
     const char* e = getenv("ZBHIP_JOURNAL_WINDOWS");
