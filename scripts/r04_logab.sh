@@ -17,7 +17,7 @@ for v in stream halfwave; do
 done
 
 # the host side with two host threads (ZBHIP_DEBUG: per-call breakdown on stderr)
-unset ZBHIP_LOG_HALFWAVE
+unset ZBHIP_LOG_HALFWAVE ZBHIP_LOG_STREAM
 ZBHIP_HOST_THREADS=2 ZBHIP_DEBUG=1 timeout -k 10 300 python3 bench.py --host-io --steps 1 --warmup 0 --no-cpu-baseline > $O/t2.json 2> $O/t2.err || { tail -20 $O/t2.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/t2.json'))['host_io']['log_bytes'];print('threads=2 hbm', json.dumps(d['hbm']))"
 grep -m1 "log write pass" $O/t2.err; grep -E "submit n=1000000|serialize_log_device n=1000000|run n=1000000" $O/t2.err | tail -3 | cut -c1-220
