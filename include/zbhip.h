@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 8  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+#define ZBHIP_ABI_VERSION 9  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
                                4: timer boundary events (start_event / flow_source / job_retries of job
                                   workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
                                   PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions;
@@ -52,7 +52,9 @@ extern "C" {
                                7: INCIDENT:CREATED records of exclusive gateways (ZBHIP_VT_INCIDENT,
                                   zbhip_incident_message), zbhip_process_csr.cond_text;
                                8: zbhip_outbox_command, zbhip_drain_command on message partitions,
-                                  zeebe:ioMapping (zbhip_process_csr.mappings) */
+                                  zeebe:ioMapping (zbhip_process_csr.mappings);
+                               9: interrupting message boundary events, ZBHIP_CMD_MSG_SUB_DELETE /
+                                  ZBHIP_CMD_PMS_DELETE and the DELETING / DELETE / DELETED records */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -340,7 +342,13 @@ enum zbhip_command_kind {
    * ProcessingStateMachine.java:388-417) and the platform now reads back as a batch of its own, on a
    * handle opened with ZBHIP_OPEN_DEFER_CONTINUATIONS: instance = its instance slot,
    * doc_begin | pad << 32 = its continuation id (zbhip_continuations).  Host windows only. */
-  ZBHIP_CMD_CONTINUE = 9
+  ZBHIP_CMD_CONTINUE = 9,
+  /* Closing a subscription (CatchEventBehavior.unsubscribeFromMessageEvent, :407-432): the
+   * subscription partition's MessageSubscriptionDeleteProcessor.java:50-68 and the acknowledgement's
+   * ProcessMessageSubscriptionDeleteProcessor.java:39-56; subjects as for the other subscription
+   * commands (ABI 9) */
+  ZBHIP_CMD_MSG_SUB_DELETE = 10,
+  ZBHIP_CMD_PMS_DELETE = 11
 };
 
 /* STR values are string ids of the partition's value dictionary (zbhip_intern_string). */
@@ -382,7 +390,8 @@ typedef struct zbhip_xpart_cmd {
   uint16_t element_ord;      /* key ordinal of the subscribing element instance in that instance */
   uint16_t message_name;     /* name id */
   uint16_t bpmn_process_id;  /* name id */
-  uint8_t kind;              /* ZBHIP_CMD_MSG_SUB_CREATE .. ZBHIP_CMD_MSG_SUB_CORRELATE */
+  uint8_t kind;              /* ZBHIP_CMD_MSG_SUB_CREATE .. ZBHIP_CMD_MSG_SUB_CORRELATE,
+                                ZBHIP_CMD_MSG_SUB_DELETE, ZBHIP_CMD_PMS_DELETE */
   uint8_t interrupting;
   int16_t source_partition;
   int16_t target_partition;

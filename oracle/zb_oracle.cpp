@@ -715,6 +715,28 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_TIMER;
+    } else if (n == "boundaryEvent" && k->child("messageEventDefinition")) {
+      // an interrupting message boundary event (BoundaryEventTransformer, CatchEventTransformer
+      // .transformMessageEventDefinition): static name, `= variable` correlation key -- evaluated in the
+      // activity's flow scope (CatchEventBehavior.evaluateCorrelationKey, common/CatchEventBehavior.java:187-205)
+      e.type = ZBHIP_EL_BOUNDARY_EVENT;
+      e.interrupting = k->attr("cancelActivity") != "false";
+      if (k->child("timerEventDefinition") || k->child("errorEventDefinition") || k->child("signalEventDefinition") ||
+          k->child("escalationEventDefinition") || k->child("conditionalEventDefinition") || !e.interrupting) {
+        err = "message boundary event outside the supported subset (interrupting only)";
+        return false;
+      }
+      auto mi = msgs.find(k->child("messageEventDefinition")->attr("messageRef"));
+      if (mi == msgs.end() || mi->second.first.empty() || mi->second.second.empty()) {
+        err = "message outside the supported subset (static name, `= variable` correlation key)";
+        return false;
+      }
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+      e.event = ZBHIP_EV_MESSAGE;
+      e.msg_name = mi->second.first;
+      e.corr_var = mi->second.second;
+      boundaries.push_back({(int)P.els.size(), k->attr("attachedToRef")});
     } else if (n == "boundaryEvent") {
       // BoundaryEventTransformer (deployment/model/transformer/BoundaryEventTransformer.java):
       // timer boundary events (interrupting or not) with a static timeDuration on job worker tasks only
@@ -992,6 +1014,8 @@ static void xpart_kind(int kind, int& vt, int& intent) {
     case ZBHIP_CMD_MSG_SUB_CREATE: vt = ZBHIP_VT_MESSAGE_SUBSCRIPTION; intent = ZBHIP_MS_CREATE; return;
     case ZBHIP_CMD_MSG_SUB_CORRELATE: vt = ZBHIP_VT_MESSAGE_SUBSCRIPTION; intent = ZBHIP_MS_CORRELATE; return;
     case ZBHIP_CMD_PMS_CREATE: vt = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; intent = ZBHIP_PMS_CREATE; return;
+    case ZBHIP_CMD_MSG_SUB_DELETE: vt = ZBHIP_VT_MESSAGE_SUBSCRIPTION; intent = ZBHIP_MS_DELETE; return;
+    case ZBHIP_CMD_PMS_DELETE: vt = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; intent = ZBHIP_PMS_DELETE; return;
     default: vt = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; intent = ZBHIP_PMS_CORRELATE; return;
   }
 }
@@ -1000,7 +1024,9 @@ static void xpart_kind(int kind, int& vt, int& intent) {
 // openMessageSubscription: pik, eik, bpmnProcessId, messageKey -1, name, correlationKey, interrupting;
 // openProcessMessageSubscription: subscriptionPartitionId = sender, pik, eik, messageKey -1, name, interrupting;
 // correlateProcessMessageSubscription: subscriptionPartitionId = sender, pik, eik, bpmnProcessId, messageKey,
-//   name, variables, correlationKey;  correlateMessageSubscription: pik, eik, bpmnProcessId, messageKey -1, name.
+//   name, variables, correlationKey;  correlateMessageSubscription: pik, eik, bpmnProcessId, messageKey -1, name;
+// closeMessageSubscription: pik, eik, messageKey -1, name (:220-236); closeProcessMessageSubscription:
+//   subscriptionPartitionId = sender, pik, eik, messageKey -1, name (:267-283).
 // Properties not set keep their declared defaults: interrupting = true (MessageSubscriptionRecord.java:33,
 // ProcessMessageSubscriptionRecord.java:37), strings "", messageKey -1.
 static MsgVal command_value(int kind, const MsgVal& in, int sender) {
@@ -1017,6 +1043,10 @@ static MsgVal command_value(int kind, const MsgVal& in, int sender) {
       m.partition = sender; m.interrupting = in.interrupting; break;
     case ZBHIP_CMD_PMS_CORRELATE:  // interrupting keeps its default (true)
       m.partition = sender; m.bpmn = in.bpmn; m.msg_key = in.msg_key; m.corr = in.corr; m.interrupting = 1; break;
+    case ZBHIP_CMD_MSG_SUB_DELETE:
+      m.interrupting = 1; break;
+    case ZBHIP_CMD_PMS_DELETE:
+      m.partition = sender; m.interrupting = 1; break;
     default:  // MSG_SUB_CORRELATE; interrupting keeps its default (true)
       m.bpmn = in.bpmn; m.interrupting = 1; break;
   }
@@ -1120,7 +1150,7 @@ class Oracle {
     // events go into the same name dictionary (the product's zbhip_deploy interns in this order)
     bool has_msg = false;
     for (auto& e : P.els)
-      if (e.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && e.event == ZBHIP_EV_MESSAGE) {
+      if ((e.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || e.type == ZBHIP_EL_BOUNDARY_EVENT) && e.event == ZBHIP_EV_MESSAGE) {
         intern(e.msg_name);
         intern(e.corr_var);
         has_msg = true;
@@ -1195,7 +1225,8 @@ class Oracle {
         rec.m.name = c.ref;
         fill_msg(rec, rec.m);
         rec.slot = true;
-      } else if (c.kind >= ZBHIP_CMD_MSG_SUB_CREATE && c.kind <= ZBHIP_CMD_MSG_SUB_CORRELATE) {
+      } else if ((c.kind >= ZBHIP_CMD_MSG_SUB_CREATE && c.kind <= ZBHIP_CMD_MSG_SUB_CORRELATE) ||
+                 c.kind == ZBHIP_CMD_MSG_SUB_DELETE || c.kind == ZBHIP_CMD_PMS_DELETE) {
         const zbhip_xpart_cmd& x = xdocs[x_base + c.doc_begin];
         rec.doc = Doc{0, 0};
         rec.r.aux = -1;
@@ -1216,7 +1247,8 @@ class Oracle {
         rec.r.intent = (uint8_t)it;
         rec.m = command_value(c.kind, m, x.source_partition);
         fill_msg(rec, rec.m);
-        rec.slot = c.kind == ZBHIP_CMD_MSG_SUB_CREATE || c.kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
+        rec.slot = c.kind == ZBHIP_CMD_MSG_SUB_CREATE || c.kind == ZBHIP_CMD_MSG_SUB_CORRELATE ||
+                   c.kind == ZBHIP_CMD_MSG_SUB_DELETE;
       } else if (c.kind == ZBHIP_CMD_TIMER_TRIGGER) {
         rec.doc = Doc{0, 0};
         rec.r.aux = (int64_t)((uint64_t)c.doc_begin | ((uint64_t)c.pad << 32));  // the command's dueDate
@@ -1293,9 +1325,9 @@ class Oracle {
     rec.pi.piKey = r.process_instance_key;
     const bool msg = (r.value_type == ZBHIP_VT_MESSAGE && r.intent == ZBHIP_MSG_PUBLISH) ||
                      (r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION &&
-                      (r.intent == ZBHIP_MS_CREATE || r.intent == ZBHIP_MS_CORRELATE)) ||
+                      (r.intent == ZBHIP_MS_CREATE || r.intent == ZBHIP_MS_CORRELATE || r.intent == ZBHIP_MS_DELETE)) ||
                      (r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION &&
-                      (r.intent == ZBHIP_PMS_CREATE || r.intent == ZBHIP_PMS_CORRELATE));
+                      (r.intent == ZBHIP_PMS_CREATE || r.intent == ZBHIP_PMS_CORRELATE || r.intent == ZBHIP_PMS_DELETE));
     const bool known = (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION && r.intent == ZBHIP_PIC_CREATE) ||
                        (r.value_type == ZBHIP_VT_JOB && r.intent == ZBHIP_JOB_COMPLETE) ||
                        (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
@@ -1599,7 +1631,7 @@ class Oracle {
 
   // --- message state (ZbColumnFamilies PROCESS_SUBSCRIPTION_BY_KEY, MESSAGE_SUBSCRIPTION_BY_KEY,
   // MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY, MESSAGE_STATS) ---
-  struct PmsRow { int64_t key; bool opened; MsgVal rec; };
+  struct PmsRow { int64_t key; bool opened; MsgVal rec; bool closing = false; };
   struct MsgSub { int64_t key; bool correlating; MsgVal rec; };
   std::map<std::pair<int64_t, int>, PmsRow> pms_;                        // [eik, name]
   std::unordered_map<uint32_t, int> pms_inst_;                           // open subscriptions per instance slot
@@ -1774,6 +1806,10 @@ class Oracle {
       process_message_subscription_create(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_PMS_CORRELATE)
       process_message_subscription_correlate(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_MS_DELETE)
+      message_subscription_delete(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_PMS_DELETE)
+      process_message_subscription_delete(cmd);
     else
       throw Unsupported{"value type"};
   }
@@ -1934,11 +1970,13 @@ class Oracle {
     }
   }
 
-  void subscribe_to_message(const OEl& el, int64_t key, const PiValue& v) {
+  // `scope`: where the correlation key is evaluated -- the element itself, or for a boundary event
+  // the activity's flow scope (CatchEventBehavior.evaluateCorrelationKey, common/CatchEventBehavior.java:187-205)
+  void subscribe_to_message(const OEl& el, int64_t key, const PiValue& v, int64_t scope) {
     // evaluateCorrelationKey (:155-178) -> ExpressionProcessor.evaluateMessageCorrelationKeyExpression
     // (processing/common/ExpressionProcessor.java:309-337): STRING or NUMBER, else incident
     auto nit = name_ids.find(el.corr_var);
-    const VarRow* vr = nit == name_ids.end() ? nullptr : lookup_var(key, nit->second);
+    const VarRow* vr = nit == name_ids.end() ? nullptr : lookup_var(scope, nit->second);
     if (!vr || vr->type != ZBHIP_DOC_STR)
       throw Unsupported{"correlation key is not a string (incident, or a NUMBER outside the subset)"};
     MsgVal m;
@@ -1948,7 +1986,8 @@ class Oracle {
     m.pik = v.piKey;
     m.eik = key;
     m.partition = subscription_partition(str(m.corr), partition_count_);
-    m.interrupting = 1;  // intermediate catch events interrupt (ExecutableCatchEvent.java:36-38)
+    m.interrupting = 1;  // intermediate catch events interrupt (ExecutableCatchEvent.java:36-38); so do the
+                         // subset's boundary events (cancelActivity)
     m.proc = v.proc;
     m.elem = v.elem;
     m.inst = cur_instance_;
@@ -1995,7 +2034,48 @@ class Oracle {
     const std::string base = "Expected to create process message subscription with element key '" +
                              std::to_string(c.eik) + "' and message name '" + names.at(c.name) + "', but ";
     if (it == pms_.end()) reject(cmd, ZBHIP_REJ_NOT_FOUND, base + "no such subscription was found");
-    else reject(cmd, ZBHIP_REJ_INVALID_STATE, base + "it is already opened");
+    else reject(cmd, ZBHIP_REJ_INVALID_STATE, base + (it->second.closing ? "it is already closing" : "it is already opened"));
+  }
+
+  // CatchEventBehavior.unsubscribeFromMessageEvents / unsubscribeFromMessageEvent
+  // (processing/common/CatchEventBehavior.java:394-432): per process message subscription of the
+  // element instance, PROCESS_MESSAGE_SUBSCRIPTION:DELETING (its key and stored record;
+  // ProcessMessageSubscriptionDeletingApplier -> updateToClosingState) and MESSAGE_SUBSCRIPTION:DELETE
+  // to the subscription partition (SubscriptionCommandSender.closeMessageSubscription, :220-236)
+  void unsubscribe_messages(int64_t eik) {
+    for (auto it = pms_.lower_bound({eik, INT32_MIN}); it != pms_.end() && it->first.first == eik; ++it) {
+      PmsRow& row = it->second;
+      msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_DELETING, row.key, row.rec);
+      row.closing = true;
+      send_command(row.rec.partition, ZBHIP_CMD_MSG_SUB_DELETE, row.rec);
+    }
+  }
+
+  // MessageSubscriptionDeleteProcessor.processRecord (processing/message/MessageSubscriptionDeleteProcessor.java:50-68):
+  // MESSAGE_SUBSCRIPTION:DELETED (the stored subscription; MessageSubscriptionDeletedApplier removes it),
+  // then the acknowledgement PROCESS_MESSAGE_SUBSCRIPTION:DELETE (closeProcessMessageSubscription, :267-283)
+  void message_subscription_delete(ORecord& cmd) {
+    const MsgVal c = cmd.m;
+    auto it = msub_.find({c.eik, (int)c.name});
+    if (it == msub_.end()) throw Unsupported{"MESSAGE_SUBSCRIPTION:DELETE of no subscription (NOT_FOUND rejection)"};
+    const MsgSub sub = it->second;
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_DELETED, sub.key, sub.rec);
+    msub_by_corr_.erase({(int)sub.rec.name, sub.rec.corr, sub.rec.eik});
+    msub_.erase(it);
+    send_command(partition_of_key(c.pik), ZBHIP_CMD_PMS_DELETE, c);
+  }
+
+  // ProcessMessageSubscriptionDeleteProcessor.processRecord (processing/message/
+  // ProcessMessageSubscriptionDeleteProcessor.java:39-56): PROCESS_MESSAGE_SUBSCRIPTION:DELETED (the stored
+  // subscription; ProcessMessageSubscriptionDeletedApplier removes it)
+  void process_message_subscription_delete(ORecord& cmd) {
+    if (cmd.r.record_type == ZBHIP_RT_COMMAND && cur_slot_) enter_instance(cmd.m.inst);
+    const MsgVal c = cmd.m;
+    auto it = pms_.find({c.eik, (int)c.name});
+    if (it == pms_.end()) throw Unsupported{"PROCESS_MESSAGE_SUBSCRIPTION:DELETE of no subscription (NOT_FOUND rejection)"};
+    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_DELETED, it->second.key, it->second.rec);
+    --pms_inst_[it->second.rec.inst];
+    pms_.erase(it);
   }
 
   // MessagePublishProcessor.processRecord / handleNewMessage (processing/message/MessagePublishProcessor.java)
@@ -2038,6 +2118,7 @@ class Oracle {
     const MsgVal c = cmd.m;
     auto it = pms_.find({c.eik, (int)c.name});
     if (it == pms_.end()) throw Unsupported{"PMS correlate rejection (MESSAGE_SUBSCRIPTION:REJECT outside the subset)"};
+    if (it->second.closing) throw Unsupported{"PMS correlate of a closing subscription (MESSAGE_SUBSCRIPTION:REJECT)"};
     auto eit = ei_.find(c.eik);
     // EventHandle.canTriggerElement: active instance, event scope accepting, flow scope not interrupted
     if (eit == ei_.end() || eit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED || !event_scope_.count(c.eik))
@@ -2062,9 +2143,16 @@ class Oracle {
     pe.r.element_idx = inst.value.elem;
     pe.r.scope_key = c.eik;
     pe.r.process_instance_key = inst.value.piKey;
-    if (event_scope_.count(c.eik))  // ProcessEventTriggeringApplier: trigger with the message variables (none)
-      triggers_[{c.eik, eventKey}] = EventTrigger{inst.value.elem, inst.value.proc, Doc{0, 0}, inst.value.piKey};
-    pi_command(c.eik, ZBHIP_PI_COMPLETE_ELEMENT, inst.value);  // isElementActivated: intermediate catch
+    if (P(m.proc).els[m.elem].type == ZBHIP_EL_BOUNDARY_EVENT) {
+      // a boundary event of the activity: the trigger (ProcessEventTriggeringApplier, interrupting the
+      // event scope), then TERMINATE_ELEMENT of the activity -- its onTerminate activates the event
+      trigger_event(c.eik, eventKey, m.elem, m.proc, Doc{0, 0}, inst.value.piKey);
+      pi_command(c.eik, ZBHIP_PI_TERMINATE_ELEMENT, inst.value);
+    } else {
+      if (event_scope_.count(c.eik))  // ProcessEventTriggeringApplier: trigger with the message variables (none)
+        triggers_[{c.eik, eventKey}] = EventTrigger{inst.value.elem, inst.value.proc, Doc{0, 0}, inst.value.piKey};
+      pi_command(c.eik, ZBHIP_PI_COMPLETE_ELEMENT, inst.value);  // isElementActivated: intermediate catch
+    }
     // sendAcknowledgeCommand -> correlateMessageSubscription(record.subscriptionPartitionId, ...)
     MsgVal ack = c;
     ack.corr = it == pms_.end() ? c.corr : c.corr;
@@ -2556,12 +2644,14 @@ class Oracle {
       case ZBHIP_EL_SCRIPT_TASK:
       case ZBHIP_EL_BUSINESS_RULE_TASK: {
         // applyInputMappings, then eventSubscriptionBehavior.subscribeToEvents: the attached boundary
-        // event's timer, then the job
+        // event's message subscription or timer, then the job
         apply_input_mappings(el, key, v);
         if (el.boundary >= 0) {
           PiValue bv = v;
           bv.elem = el.boundary;
-          subscribe_to_timer(P(v.proc).els[el.boundary], key, bv);
+          const OEl& b = P(v.proc).els[el.boundary];
+          if (b.event == ZBHIP_EV_MESSAGE) subscribe_to_message(b, key, bv, v.flowScopeKey);
+          else subscribe_to_timer(b, key, bv);
         }
         // BpmnJobBehavior.createNewJob -> writeJobCreatedEvent (behavior/BpmnJobBehavior.java:113-119,194-218)
         JobRow job;
@@ -2596,7 +2686,7 @@ class Oracle {
         // IntermediateCatchEventProcessor.DefaultIntermediateCatchEventBehavior.onActivate
         // (processing/bpmn/event/IntermediateCatchEventProcessor.java): subscribeToEvents, then ACTIVATED
         if (el.event == ZBHIP_EV_TIMER) subscribe_to_timer(el, key, v);
-        else subscribe_to_message(el, key, v);
+        else subscribe_to_message(el, key, v, key);
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         break;
       case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (processing/bpmn/gateway/ParallelGatewayProcessor.java:34-50)
@@ -2676,7 +2766,8 @@ class Oracle {
       job_activation_fields(rec, job);
       apply_job_canceled(jobKey, job);
     }
-    unsubscribe_timers(key);
+    unsubscribe_timers(key);  // unsubscribeFromEvents: timers, then message subscriptions
+    unsubscribe_messages(key);
     // findEventTrigger (BpmnEventSubscriptionBehavior.java:63-70): the scope's first trigger, unless
     // it is the element's own
     auto tit = triggers_.lower_bound({key, INT64_MIN});
@@ -2730,7 +2821,10 @@ class Oracle {
       }
       // START_EVENT without trigger: local variables of the start event are empty.
     }
-    if (unsubscribe) unsubscribe_timers(key);
+    if (unsubscribe) {  // unsubscribeFromEvents (CatchEventBehavior.java:126-138): timers, then messages
+      unsubscribe_timers(key);
+      unsubscribe_messages(key);
+    }
     transition_to_completed(el, key, v);
     for (int f : el.out) take_sequence_flow(key, v, f);
   }
@@ -3141,7 +3235,7 @@ std::string Oracle::dump_state() const {
     snprintf(buf, sizeof buf,
              "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%d,processInstanceKey=%lld,"
              "bpmnProcessId=%s,messageKey=%lld,correlationKey=%s,elementId=%s,interrupting=%d",
-             (long long)k.first, nm(k.second), (long long)row.key, row.opened ? "OPENED" : "OPENING", m.partition,
+             (long long)k.first, nm(k.second), (long long)row.key, row.closing ? "CLOSING" : row.opened ? "OPENED" : "OPENING", m.partition,
              (long long)m.pik, nm(m.bpmn), (long long)m.msg_key, sv(m.corr), procs[m.proc].els[m.elem].id.c_str(),
              m.interrupting);
     rows.push_back(buf);
@@ -3395,7 +3489,8 @@ double zbo_bench_msg(const char* xml, int P, int n, uint64_t* transitions_out, u
         std::vector<zbhip_command> cs(inbox[t].size());
         for (size_t i = 0; i < inbox[t].size(); ++i) {
           const zbhip_xpart_cmd& x = inbox[t][i];
-          const bool pms = x.kind == ZBHIP_CMD_PMS_CREATE || x.kind == ZBHIP_CMD_PMS_CORRELATE;
+          const bool pms = x.kind == ZBHIP_CMD_PMS_CREATE || x.kind == ZBHIP_CMD_PMS_CORRELATE ||
+                           x.kind == ZBHIP_CMD_PMS_DELETE;
           cs[i] = zbhip_command{};
           cs[i].instance = pms ? x.instance : x.correlation_key;
           cs[i].kind = x.kind;

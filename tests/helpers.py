@@ -170,6 +170,14 @@ class MessageCluster:
             outboxes.append(self._run("create", p, cmds, string_docs(self.var_id, ids)))
         self.exchange("subscribe", outboxes)
 
+    def commands(self, phase, cmds_per_partition):
+        """One window per partition (None: none), then the exchange to quiescence."""
+        outboxes = []
+        for p in range(1, self.P + 1):
+            c = cmds_per_partition[p - 1]
+            outboxes.append(self._run(phase, p, c) if c is not None and len(c) else abi.make_xparts(0))
+        self.exchange(phase, outboxes)
+
     def publish(self, key_ids, key_partition):
         """key_partition[i] = message partition of key_ids[i] (SubscriptionUtil)."""
         outboxes = []

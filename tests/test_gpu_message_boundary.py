@@ -1,0 +1,106 @@
+"""Interrupting message boundary events on the gfx950 executor (KMsg) against the oracle cluster:
+the subscription opened with the job worker task, then the message first (PROCESS_MESSAGE_SUBSCRIPTION
+:CORRELATE terminates the task -- JOB:CANCELED -- and activates the boundary event) or the job first
+(the task's unsubscribeFromEvents: PROCESS_MESSAGE_SUBSCRIPTION:DELETING, MESSAGE_SUBSCRIPTION:DELETE /
+DELETED on the message partition, PROCESS_MESSAGE_SUBSCRIPTION:DELETE / DELETED back on the PI
+partition, also after the instance ended).  Bar as for config 5: every window's records (all parity
+fields), outbox entries and exported state bit-exact, at P = 1 and P = 3.  The oracle's lifecycles
+are pinned on MessageCatchElementTest / BoundaryEventTest (tests/test_oracle_message_boundary.py)."""
+import numpy as np
+import pytest
+
+from helpers import MessageCluster, OracleAdapter
+from oracle.oracle import Oracle, subscription_partition
+from test_gpu_messages import GpuAdapter, assert_same_logs, assert_same_state
+from test_oracle_message_boundary import job_completions, keys
+from zeebe_amd import abi, bpmn
+from zeebe_amd.engine import Partition
+
+pytestmark = pytest.mark.gpu
+
+XML = bpmn.message_boundary_process()
+
+
+def clusters(P, n_inst):
+    gpu = MessageCluster([Partition(partition_id=p, partition_count=P, max_instances=n_inst, max_commands=4 * n_inst,
+                                    max_correlation_keys=4 * n_inst * P, max_records_per_batch=256)
+                          for p in range(1, P + 1)], GpuAdapter, XML)
+    orc = MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], OracleAdapter, XML)
+    return gpu, orc
+
+
+def start(gpu, orc, P, n):
+    ks = keys(P, n)
+    for cl in (gpu, orc):
+        ids = cl.intern_keys(ks)
+        cl.create(n, [ids[(p - 1) * n:p * n] for p in range(1, P + 1)])
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)  # PROCESS_SUBSCRIPTION_BY_KEY OPENED, MESSAGE_SUBSCRIPTION rows, EVENT_SCOPE
+    return ks, ids
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_gpu_message_first(P):
+    n = 24
+    gpu, orc = clusters(P, n)
+    ks, ids = start(gpu, orc, P, n)
+    for cl in (gpu, orc):
+        cl.publish(ids, [subscription_partition(k, P) for k in ks])
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)
+    canceled = sum(int(np.sum((r["value_type"] == abi.VT_JOB) & (r["intent"] == abi.JOB_CANCELED))) for _, _, r, _ in gpu.log)
+    assert canceled == n * P
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_gpu_job_first(P):
+    n = 24
+    gpu, orc = clusters(P, n)
+    start(gpu, orc, P, n)
+    cmds = job_completions(orc, n)
+    for cl in (gpu, orc):
+        cl.commands("complete", cmds)
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)  # every subscription deleted on both sides
+    deleted = sum(int(np.sum((r["value_type"] == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION) & (r["intent"] == abi.PMS_DELETED)))
+                  for _, _, r, _ in gpu.log)
+    assert deleted == n * P
+
+
+def test_gpu_closing_subscription_state():
+    # P = 3, the PI partition's window alone: the subscriptions of the ended instances are CLOSING
+    # (exported from the device slot rows of instances that are gone), then the exchange deletes them
+    P, n = 3, 16
+    gpu, orc = clusters(P, n)
+    start(gpu, orc, P, n)
+    cmds = job_completions(orc, n)
+    outs = []
+    for cl in (gpu, orc):
+        outs.append(cl._run("complete", 1, cmds[0]))
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)
+    assert any("state=CLOSING" in r for r in gpu.parts[0].state())
+    for cl, ob in zip((gpu, orc), outs):
+        cl.exchange("close", [ob] + [abi.make_xparts(0) for _ in range(P - 1)])
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)
+    assert not any("state=CLOSING" in r for r in gpu.parts[0].state())
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_gpu_mixed_outcomes(P):
+    # half the instances get their message, the other half complete their job, in the same windows
+    n = 32
+    gpu, orc = clusters(P, n)
+    ks, ids = start(gpu, orc, P, n)
+    half = list(range(0, n, 2))
+    cmds = job_completions(orc, n, which=half)
+    for cl in (gpu, orc):
+        cl.commands("complete", cmds)
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)
+    rest = [(k, i) for k, i, j in zip(ks, ids, range(len(ks))) if (j % n) % 2 == 1]
+    for cl in (gpu, orc):
+        cl.publish([i for _, i in rest], [subscription_partition(k, P) for k, _ in rest])
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)

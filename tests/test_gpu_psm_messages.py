@@ -27,16 +27,16 @@ XML = bpmn.message_catch_process(message_name="message", correlation_key="key", 
 
 
 class Cluster:
-    def __init__(self, device, limit=100, window=48):
+    def __init__(self, device, limit=100, window=48, xml=XML):
         self.logs = {p: Log() for p in range(1, P + 1)}
         sender = InterPartitionCommandSender(self.logs)
         self.engines, self.adapters, self.sps = {}, {}, []
         for p in range(1, P + 1):
             eng = OracleEngine(partition_id=p, partition_count=P, max_commands_in_batch=limit, command_sender=sender)
-            eng.deploy(XML, KEY, 1)
+            eng.deploy(xml, KEY, 1)
             procs = [eng]
             if device:
-                ad = GpuBatchProcessor(eng, self.logs[p].reader(), [(XML, KEY, 1)], zeebe_db=eng, key_generator=eng,
+                ad = GpuBatchProcessor(eng, self.logs[p].reader(), [(xml, KEY, 1)], zeebe_db=eng, key_generator=eng,
                                        partition_id=p, partition_count=P, instances=256, window=window,
                                        max_commands_in_batch=limit, correlation_keys=64, command_sender=sender)
                 ad.init()
@@ -78,13 +78,13 @@ def phase(ref, gpu, writes):
 KEYS = [CORRELATION_KEYS[1], CORRELATION_KEYS[2], CORRELATION_KEYS[3]] + ["order-%d" % j for j in range(7)]
 
 
-def create_phase():
+def create_phase(process_id="process"):
     """30 instances, 3 per correlation key, every partition creating instances of keys of every
     partition (local and remote subscriptions): instance i on partition 1 + (i + i // 10) % 3 with key
     KEYS[i % 10]."""
     creates = {p: [] for p in range(1, P + 1)}
     for i in range(30):
-        creates[1 + (i + i // 10) % 3].append(Client.create("process", (("key", KEYS[i % 10]),)))
+        creates[1 + (i + i // 10) % 3].append(Client.create(process_id, (("key", KEYS[i % 10]),)))
     return sorted(creates.items())
 
 
@@ -113,3 +113,40 @@ def test_message_correlation_on_three_partitions_in_the_processing_loop():
     c = [gpu.adapters[p].counts for p in range(1, P + 1)]
     assert all(x["fallbacks"] == 0 for x in c), [gpu.adapters[p].fallback_reasons for p in range(1, P + 1)]
     assert sum(x["device_commands"] for x in c) >= 30 + 3 * 11 + 2 * 30  # creates, publishes, received commands
+
+
+BOUNDARY_XML = bpmn.message_boundary_process(message_name="message", correlation_key="key")
+
+
+def test_message_boundary_events_on_three_partitions_in_the_processing_loop():
+    """Interrupting message boundary events (MessageCatchElementTest's BOUNDARY_EVENT_PROCESS) in the
+    loop: the jobs of half the correlation keys' instances complete first -- their subscriptions close
+    through PROCESS_MESSAGE_SUBSCRIPTION:DELETING, MESSAGE_SUBSCRIPTION:DELETE / DELETED and
+    PROCESS_MESSAGE_SUBSCRIPTION:DELETE / DELETED across the partitions, some after the instance ended --
+    then messages for the other half's keys terminate their tasks (JOB:CANCELED) through the boundary
+    event."""
+    from psm import open_jobs
+    from oracle.oracle import subscription_partition
+    ref, gpu = Cluster(device=False, xml=BOUNDARY_XML), Cluster(device=True, xml=BOUNDARY_XML)
+    phase(ref, gpu, create_phase("boundaryEventProcess"))
+    job_first = set(KEYS[0::2])
+    jobs = {}
+    for p in range(1, P + 1):
+        keys_of = {r.value["processInstanceKey"]: str(r.value["value"]).strip('"') for r in ref.logs[p].entries
+                   if r.value_type == abi.VT_VARIABLE and r.record_type == abi.RT_EVENT and r.value["name"] == "key"}
+        jobs[p] = [Client.complete_job(k) for k, r in sorted(open_jobs(ref.logs[p]).items())
+                   if keys_of.get(r.value["processInstanceKey"]) in job_first]
+    phase(ref, gpu, sorted(jobs.items()))
+    for cl in (ref, gpu):
+        deleted = sum(1 for p in range(1, P + 1) for r in cl.logs[p].entries
+                      if r.value_type == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION and r.intent == abi.PMS_DELETED)
+        assert deleted == 15
+    pubs = {p: [] for p in range(1, P + 1)}
+    for k in KEYS[1::2]:
+        pubs[subscription_partition(k, P)] += [Client.publish_message("message", k) for _ in range(3)]
+    phase(ref, gpu, sorted(pubs.items()))
+    canceled = sum(1 for p in range(1, P + 1) for r in gpu.logs[p].entries
+                   if r.value_type == abi.VT_JOB and r.intent == abi.JOB_CANCELED)
+    assert canceled == 15
+    c = [gpu.adapters[p].counts for p in range(1, P + 1)]
+    assert all(x["fallbacks"] == 0 for x in c), [gpu.adapters[p].fallback_reasons for p in range(1, P + 1)]

@@ -54,7 +54,9 @@ PMS_INTENTS = {0: "CREATING", 1: "CREATE", 2: "CREATED", 3: "CORRELATE", 4: "COR
                6: "DELETE", 7: "DELETED"}
 MSG_PUBLISH, MSG_PUBLISHED, MSG_EXPIRED = 0, 1, 3
 MS_CREATE, MS_CREATED, MS_CORRELATE, MS_CORRELATED, MS_CORRELATING = 0, 1, 2, 3, 8
+MS_DELETE, MS_DELETED = 6, 7
 PMS_CREATING, PMS_CREATE, PMS_CREATED, PMS_CORRELATE, PMS_CORRELATED = 0, 1, 2, 3, 4
+PMS_DELETING, PMS_DELETE, PMS_DELETED = 5, 6, 7
 VALUE_TYPES = {0: "JOB", 5: "PROCESS_INSTANCE", 10: "MESSAGE", 11: "MESSAGE_SUBSCRIPTION",
                12: "PROCESS_MESSAGE_SUBSCRIPTION", 17: "VARIABLE", 19: "PROCESS_INSTANCE_CREATION",
                24: "PROCESS_EVENT", 15: "TIMER"}
@@ -84,7 +86,11 @@ CMD_PUBLISH = 3
 CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE = 4, 5, 6, 7
 CMD_TIMER_TRIGGER = 8  # ref = timer key ordinal, doc_begin | pad << 32 = the timer's dueDate
 CMD_CONTINUE = 9  # a deferred continuation read back from the log: doc_begin | pad << 32 = its id
-XPART_KINDS = (CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE)
+CMD_MSG_SUB_DELETE, CMD_PMS_DELETE = 10, 11  # closing a subscription and its acknowledgement
+XPART_KINDS = (CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SUB_CORRELATE, CMD_MSG_SUB_DELETE,
+               CMD_PMS_DELETE)
+SLOT_KINDS = (CMD_PUBLISH, CMD_MSG_SUB_CREATE, CMD_MSG_SUB_CORRELATE, CMD_MSG_SUB_DELETE)
+PMS_KINDS = (CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_PMS_DELETE)
 DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR = 0, 1, 2, 3, 4, 5
 NO_STRING = 0xFFFFFFFF
 DEC_SCALE = 6

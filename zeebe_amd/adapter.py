@@ -53,7 +53,9 @@ MESSAGE_VALUE_TYPES = (abi.VT_MESSAGE, abi.VT_MESSAGE_SUBSCRIPTION, abi.VT_PROCE
 XPART_COMMAND = {abi.CMD_MSG_SUB_CREATE: (abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_CREATE),
                  abi.CMD_MSG_SUB_CORRELATE: (abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_CORRELATE),
                  abi.CMD_PMS_CREATE: (abi.VT_PROCESS_MESSAGE_SUBSCRIPTION, abi.PMS_CREATE),
-                 abi.CMD_PMS_CORRELATE: (abi.VT_PROCESS_MESSAGE_SUBSCRIPTION, abi.PMS_CORRELATE)}
+                 abi.CMD_PMS_CORRELATE: (abi.VT_PROCESS_MESSAGE_SUBSCRIPTION, abi.PMS_CORRELATE),
+                 abi.CMD_MSG_SUB_DELETE: (abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_DELETE),
+                 abi.CMD_PMS_DELETE: (abi.VT_PROCESS_MESSAGE_SUBSCRIPTION, abi.PMS_DELETE)}
 XPART_KIND = {v: k for k, v in XPART_COMMAND.items()}
 KEY_BITS = 51  # Protocol.KEY_BITS
 
@@ -81,7 +83,15 @@ def xpart_value(x, name, string_value):
         return {"processInstanceKey": pik, "elementInstanceKey": eik, "messageKey": -1, "messageName": nm,
                 "correlationKey": "", "interrupting": True, "bpmnProcessId": bpmn, "variables": (),
                 "tenantId": TENANT}
+    if kind == abi.CMD_MSG_SUB_DELETE:  # closeMessageSubscription (:220-236)
+        return {"processInstanceKey": pik, "elementInstanceKey": eik, "messageKey": -1, "messageName": nm,
+                "correlationKey": "", "interrupting": True, "bpmnProcessId": "", "variables": (),
+                "tenantId": TENANT}
     sender = int(x["source_partition"])
+    if kind == abi.CMD_PMS_DELETE:  # closeProcessMessageSubscription (:267-283)
+        return {"subscriptionPartitionId": sender, "processInstanceKey": pik, "elementInstanceKey": eik,
+                "messageKey": -1, "messageName": nm, "variables": (), "interrupting": True,
+                "bpmnProcessId": "", "correlationKey": "", "elementId": "", "tenantId": TENANT}
     if kind == abi.CMD_PMS_CREATE:  # openProcessMessageSubscription (:116-134)
         return {"subscriptionPartitionId": sender, "processInstanceKey": pik, "elementInstanceKey": eik,
                 "messageKey": -1, "messageName": nm, "variables": (), "interrupting": bool(x["interrupting"]),
@@ -311,6 +321,9 @@ class GpuBatchProcessor:
             self.engine_job_types.update(job_types_of(xml))
         self.used_slots = set()
         self.ended = set()             # ended instances whose slot waits for their continuations
+        self.closing = set()           # instance slots with a closing process message subscription
+        self.pms_handles = {}          # (elementInstanceKey, messageName) -> (slot, ordinal) of a device
+                                       # subscription (its PROCESS_MESSAGE_SUBSCRIPTION:DELETE may come late)
         self.next_free = 0
         self.window = Window()
         self.handed_off = set()
@@ -504,8 +517,11 @@ class GpuBatchProcessor:
         x["interrupting"] = int(bool(v.get("interrupting", True)))
         x["target_partition"] = self.partition_id
         if vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION:
-            # the PI partition's side: the subscribing element instance of a device instance
+            # the PI partition's side: the subscribing element instance of a device instance (a closing
+            # subscription's DELETE may arrive after its instance ended: the handle kept at CREATING)
             pi, el = self._resolve(pik), self._resolve(eik)
+            if (pi is None or el is None) and kind == abi.CMD_PMS_DELETE:
+                pi = el = self.pms_handles.get((eik, v["messageName"]))
             if pi is None or el is None or pi[0] != el[0]:
                 return None
             x["instance"], x["element_ord"] = el
@@ -525,7 +541,8 @@ class GpuBatchProcessor:
             n = eik - (partition_of_key(eik) << KEY_BITS)
             x["instance"], x["element_ord"] = n & 0xFFFFFFFF, (n >> 32) & 0xFFFF
         x["source_partition"] = src
-        if kind == abi.CMD_MSG_SUB_CORRELATE:
+        if kind in (abi.CMD_MSG_SUB_CORRELATE, abi.CMD_MSG_SUB_DELETE):
+            # no correlation key in the value: the slot of the subscription it names
             x["correlation_key"] = self.subscriptions.get((eik, v["messageName"]), 0)
         if int(x["correlation_key"]) >= self.correlation_keys:
             return None
@@ -613,7 +630,7 @@ class GpuBatchProcessor:
 
     def _free_ended(self):
         for s in list(self.ended):
-            if self.part.pending_continuations(s) == 0:
+            if self.part.pending_continuations(s) == 0 and s not in self.closing:
                 self.ended.discard(s)
                 self.used_slots.discard(s)
 
@@ -653,8 +670,20 @@ class GpuBatchProcessor:
                 sub = (value["elementInstanceKey"], value["messageName"])
                 if it == abi.MS_CREATED:
                     self.subscriptions[sub] = int(r["correlation_key"])
-                elif it == abi.MS_CORRELATED:
+                elif it in (abi.MS_CORRELATED, abi.MS_DELETED):
                     self.subscriptions.pop(sub, None)
+            elif vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION and rt == abi.RT_EVENT:
+                # a closing subscription keeps its instance slot until PROCESS_MESSAGE_SUBSCRIPTION:DELETED
+                # (the device row outlives the instance: a CREATE into the slot would fall back)
+                sub = (value["elementInstanceKey"], value["messageName"])
+                if it == abi.PMS_CREATING:
+                    self.pms_handles[sub] = self._resolve(value["elementInstanceKey"])
+                elif it == abi.PMS_DELETING:
+                    self.closing.add(win.instances[i])
+                elif it in (abi.PMS_DELETED, abi.PMS_CORRELATED):
+                    self.pms_handles.pop(sub, None)
+                    if it == abi.PMS_DELETED:
+                        self.closing.discard(win.instances[i])
         self.followups = admitted
         if self.correlation_keys > 0:
             self._send(i, out)

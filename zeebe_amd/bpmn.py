@@ -306,6 +306,10 @@ class ProcessBuilder:
                     elif c.timer:
                         body = ('<timerEventDefinition id=%s><timeDuration>%s</timeDuration></timerEventDefinition>'
                                 % (quoteattr(c.id + "_ted"), escape(c.timer)))
+                    elif c.message:
+                        catches.append(c)
+                        body = '<messageEventDefinition id=%s messageRef=%s/>' % (quoteattr(c.id + "_med"),
+                                                                                quoteattr(c.message[0]))
                     out.append('%s<boundaryEvent id=%s attachedToRef=%s%s>%s</boundaryEvent>'
                                % (ind, quoteattr(c.id), quoteattr(c.attached_to), cancel, body))
                 elif c.kind == "exclusiveGateway" and c.default:
@@ -409,6 +413,15 @@ def message_catch_process(process_id="process", message_name="msg", correlation_
     (MessageCorrelationMultiplePartitionsTest.java:43-49 shape)."""
     return (createExecutableProcess(process_id).startEvent("start").intermediateCatchEvent(catch_id)
             .message(message_name, correlation_key).endEvent("end").done())
+
+
+def message_boundary_process(process_id="boundaryEventProcess", message_name="msg", correlation_key="key",
+                             task_id="task", job_type="type", flow_id="to-end2"):
+    """MessageCatchElementTest.BOUNDARY_EVENT_PROCESS (engine/src/test/.../message/MessageCatchElementTest.java:
+    71-80): start -> service task with an interrupting message boundary event (-> end2) -> end."""
+    b = createExecutableProcess(process_id).startEvent("start").serviceTask(task_id, job_type)
+    b.boundaryEvent("boundary").message(message_name, correlation_key).sequenceFlowId(flow_id).endEvent("end2")
+    return b.moveToActivity(task_id).endEvent("end").done()
 
 
 def multi_instance_process(items=(10, 20, 30), sequential=False, input_element="item", process_id="process",

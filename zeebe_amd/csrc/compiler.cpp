@@ -740,7 +740,32 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         }
         if (int rc = parse_mappings(c.first("extensionElements"), (uint16_t)C.elements.size(), C, err)) return rc;
       }
-      if (type == ZBHIP_EL_BOUNDARY_EVENT) {
+      if (type == ZBHIP_EL_BOUNDARY_EVENT && c.first("messageEventDefinition")) {
+        // BoundaryEventTransformer + CatchEventTransformer.transformMessageEventDefinition: an
+        // interrupting message boundary event on a job worker task (static name, `= variable`
+        // correlation key, evaluated in the task's flow scope); attached after the walk
+        const std::string* ca = c.get("cancelActivity");
+        const Elem* med = c.first("messageEventDefinition");
+        for (auto& d : c.children)
+          if (&d != med && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+            err = "event definition <" + d.tag + "> outside the supported subset";
+            return ZBHIP_EUNSUPP;
+          }
+        if (ca && *ca == "false") { err = "non-interrupting message boundary event outside the supported subset"; return ZBHIP_EUNSUPP; }
+        if (!med->get("messageRef")) { err = "boundary event without a message"; return ZBHIP_EUNSUPP; }
+        auto mi = messages.find(*med->get("messageRef"));
+        if (mi == messages.end()) { err = "unknown message " + *med->get("messageRef"); return ZBHIP_EPARSE; }
+        if (!mi->second.ok) { err = mi->second.why; return ZBHIP_EUNSUPP; }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        const std::string* at = c.get("attachedToRef");
+        if (!at) { err = "boundary event without attachedToRef"; return ZBHIP_EPARSE; }
+        e.event_type = ZBHIP_EV_MESSAGE;
+        e.message_name = C.str(mi->second.name);
+        e.correlation_var = C.str(mi->second.corr);
+        e.job_retries = 1;  // interrupting
+        boundaries.push_back({(uint16_t)C.elements.size(), *at});
+      } else if (type == ZBHIP_EL_BOUNDARY_EVENT) {
         // BoundaryEventTransformer: timer boundary events (a static timeDuration; interrupting or not)
         // on job worker tasks; attached after the walk
         const std::string* ca = c.get("cancelActivity");  // BoundaryEvent default: interrupting

@@ -161,7 +161,10 @@ struct Lane {
   // ---- message correlation (K::M only) ----
   uint32_t inst;            // instance whose rows are loaded (kNoInst: none, a slot lane before a
                             // local PROCESS_MESSAGE_SUBSCRIPTION command)
-  uint32_t pm_x, pm_y, pm_z;// PROCESS_SUBSCRIPTION row of the loaded instance
+  uint32_t pm_x, pm_y, pm_z;// PROCESS_SUBSCRIPTION row of the loaded instance: element | state << 12
+                            // (1 opening, 2 opened, 3 closing) | interrupting << 14 | partition << 16;
+                            // element-instance ordinal | key ordinal << 16; correlation key
+  uint32_t pm_w;            // its message name | bpmnProcessId << 16
   long long pik;            // real process-instance key of the loaded instance, or a reference
   bool slot_lane;           // primary subject is the correlation slot `slot`
   uint32_t slot;
@@ -426,7 +429,8 @@ __device__ __forceinline__ void follow_up(Lane<K>& L, uint32_t code, uint32_t ke
 
 // local subscription commands (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition,
 // :304-320: receiver == this partition -> follow-up command of the batch): bit 14 + kind
-enum : uint32_t { LQ_BIT = 1u << 14, LQ_MS_CREATE = 1, LQ_PMS_CREATE = 2, LQ_PMS_CORRELATE = 3, LQ_MS_CORRELATE = 4 };
+enum : uint32_t { LQ_BIT = 1u << 14, LQ_MS_CREATE = 1, LQ_PMS_CREATE = 2, LQ_PMS_CORRELATE = 3, LQ_MS_CORRELATE = 4,
+                  LQ_MS_DELETE = 5, LQ_PMS_DELETE = 6 };
 template <class K>
 __device__ __forceinline__ void push_local(Lane<K>& L, uint32_t kind) {
   // past the batch limit a local subscription command would need its pending context written to
@@ -910,7 +914,7 @@ __device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem
   }
   tbl_insert(L, elem, key, ZBHIP_PI_ELEMENT_ACTIVATING);
   ++L.pi_child;
-  if (type == ZBHIP_EL_START_EVENT) {
+  if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_BOUNDARY_EVENT) {  // not reached by a sequence flow
   } else if (type == ZBHIP_EL_PARALLEL_GATEWAY) {
     int n = (int)(w.x >> 16);
     L.pi_asf = L.pi_asf > n ? L.pi_asf - n : 0;  // decrementActiveSequenceFlows clamps at 0
@@ -1065,11 +1069,13 @@ __device__ __forceinline__ void send_xpart(Lane<K>& L, uint32_t kind, uint32_t t
 // CatchEventBehavior.java:111-125,155-178,248-283): correlation key `= var` (STRING), the
 // PROCESS_MESSAGE_SUBSCRIPTION:CREATING event (+key), then MESSAGE_SUBSCRIPTION:CREATE to the
 // subscription partition -- a follow-up command here, or an outbox entry for another partition.
+// A boundary event's correlation key is evaluated in the activity's flow scope (evaluateCorrelationKey,
+// CatchEventBehavior.java:187-205): `boundary` skips the element's own scope.
 template <class K>
-__device__ __forceinline__ void subscribe_message(Lane<K>& L, uint32_t elem, uint4 w, uint32_t key) {
+__device__ __forceinline__ void subscribe_message(Lane<K>& L, uint32_t elem, uint4 w, uint32_t key, bool boundary = false) {
   const StepParams& P = *L.sp;
   const uint32_t name = w.z & 0xFFFF, var = w.z >> 16;
-  int v = var_find(L, key, var);  // DbVariableState.getVariable: element scope, then the process
+  int v = boundary ? -1 : var_find(L, key, var);  // DbVariableState.getVariable: element scope, then the process
   if (v < 0) v = var_find(L, 0, var);
   // ExpressionProcessor.evaluateMessageCorrelationKeyExpression: STRING (NUMBER / null -> outside)
   if (v < 0 || ((var_y(L, v) >> 16) & 0xFF) != ZBHIP_DOC_STR || L.slot_lane) { set_fail(L, FB_MESSAGE); return; }
@@ -1082,6 +1088,7 @@ __device__ __forceinline__ void subscribe_message(Lane<K>& L, uint32_t elem, uin
   L.pm_x = elem | (1u << 12) | (1u << 14) | (part << 16);  // ProcessMessageSubscriptionCreatingApplier
   L.pm_y = key | (sub << 16);
   L.pm_z = corr;
+  L.pm_w = nb;
   emit_msg(L, C_PMS_CREATING, iref(L, sub), iref(L, key), iref(L, 0), -1, corr, nb, part, 1, elem);
   if ((int32_t)part == P.partition_id) {
     emit_msg(L, C_MS_CREATE, -1, iref(L, key), iref(L, 0), -1, corr, nb, 0, 1, kNoElem);
@@ -1162,16 +1169,15 @@ __device__ __forceinline__ void pms_create(Lane<K>& L, uint32_t eord, uint32_t n
                                            uint32_t part, uint32_t intr) {
   const uint32_t st = (L.pm_x >> 12) & 3;
   const uint32_t pm_elem = L.pm_x & 0xFFF;
-  const bool match = st != 0 && (L.pm_y & 0xFFFF) == eord && (elem_of(L, pm_elem).z & 0xFFFF) == name;
+  const bool match = st != 0 && (L.pm_y & 0xFFFF) == eord && (L.pm_w & 0xFFFF) == name;
   if (match && st == 1) {
-    const uint32_t nb = name | ((L.pb[5] & 0xFFFF) << 16);
-    emit_msg(L, C_PMS_CREATED, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, L.pm_z, nb, L.pm_x >> 16,
+    emit_msg(L, C_PMS_CREATED, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, L.pm_z, L.pm_w, L.pm_x >> 16,
              (L.pm_x >> 14) & 1, pm_elem);
     L.pm_x = (L.pm_x & ~(3u << 12)) | (2u << 12);  // ProcessMessageSubscriptionCreatedApplier: OPENED
     return;
   }
   emit_msg(L, kRejectBit | C_PMS_CREATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, name | 0xFFFF0000u, part, intr,
-           kNoElem, match ? (ZBHIP_REASON_PMS_CREATE_NOT_OPENING | (1u << 4)) : ZBHIP_REASON_PMS_CREATE_NOT_FOUND);
+           kNoElem, match ? (ZBHIP_REASON_PMS_CREATE_NOT_OPENING | ((st == 2 ? 1u : 0u) << 4)) : ZBHIP_REASON_PMS_CREATE_NOT_FOUND);
 }
 
 // ProcessMessageSubscriptionCorrelateProcessor.processRecord: CORRELATED, EventHandle.activateElement
@@ -1184,17 +1190,28 @@ __device__ __forceinline__ void pms_correlate(Lane<K>& L, uint32_t eord, uint32_
   const uint32_t st = (L.pm_x >> 12) & 3;
   const uint32_t elem = L.pm_x & 0xFFF;
   const uint32_t name = nb & 0xFFFF;
-  // no subscription / rejection -> MESSAGE_SUBSCRIPTION:REJECT (outside the subset)
-  if (st == 0 || (L.pm_y & 0xFFFF) != eord || (elem_of(L, elem).z & 0xFFFF) != name) { set_fail(L, FB_MESSAGE); return; }
+  // no subscription, or a closing one: a rejection and MESSAGE_SUBSCRIPTION:REJECT (outside the subset)
+  if (st == 0 || st == 3 || (L.pm_y & 0xFFFF) != eord || (L.pm_w & 0xFFFF) != name) { set_fail(L, FB_MESSAGE); return; }
   const int t = tbl_find(L, eord);  // canTriggerElement: the catch event is ACTIVATED with its event scope
   if (t < 0 || ((tget(L, t).y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED) { set_fail(L, FB_MESSAGE); return; }
   const uint32_t intr = (L.pm_x >> 14) & 1;
+  const bool boundary = etype(elem_of(L, elem)) == ZBHIP_EL_BOUNDARY_EVENT;
+  // an interrupting boundary event terminates its activity first (the command's context travels in
+  // the lane: past the batch limit it would be written unprocessed -- outside the device subset)
+  if (boundary && pending(L) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
   emit_msg(L, C_PMS_CORRELATED, iref(L, L.pm_y >> 16), eik_p, pik_p, msg_p, corr, nb, part, intr, elem);
-  L.pm_x = L.pm_y = L.pm_z = 0;  // ProcessMessageSubscriptionCorrelatedApplier: interrupting -> removed
+  L.pm_x = L.pm_y = L.pm_z = L.pm_w = 0;  // ProcessMessageSubscriptionCorrelatedApplier: interrupting -> removed
   const uint32_t pe = new_key(L);
   emit(L, C_PE_TRIGGERING, pe, eord, elem);
   L.trig_key = (uint16_t)eord;
-  follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, eord, 0, elem, true, true, eord);
+  if (boundary) {
+    // EventHandle.activateElement for a boundary event: TERMINATE_ELEMENT of the activity (its
+    // onTerminate activates the event with the trigger's PROCESS_EVENT key)
+    L.trig_evt = (uint16_t)pe;
+    follow_up(L, ZBHIP_PI_TERMINATE_ELEMENT, eord, 0, tget(L, t).x & 0xFFFF, false, true, eord, Q_TERM);
+  } else {
+    follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, eord, 0, elem, true, true, eord);
+  }
   // sendAcknowledgeCommand -> SubscriptionCommandSender.correlateMessageSubscription (sender partition)
   if ((int32_t)part == L.sp->partition_id) {
     emit_msg(L, C_MS_CORRELATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, nb, 0, 1, kNoElem);
@@ -1233,6 +1250,75 @@ __device__ __forceinline__ void ms_correlate(Lane<K>& L, uint32_t slot, uint32_t
   if (L.op_rm_mask && L.op_rm_slot != slot) { set_fail(L, FB_MESSAGE); return; }
   L.op_rm_mask |= 1u << r;
   L.op_rm_slot = slot;
+}
+
+// CatchEventBehavior.unsubscribeFromMessageEvent (processing/common/CatchEventBehavior.java:407-432):
+// PROCESS_MESSAGE_SUBSCRIPTION:DELETING with the stored subscription (ProcessMessageSubscriptionDeletingApplier
+// -> updateToClosingState), then MESSAGE_SUBSCRIPTION:DELETE to the subscription partition
+// (SubscriptionCommandSender.closeMessageSubscription, :220-236: pik, eik, messageKey -1, name)
+template <class K>
+__device__ __forceinline__ void unsubscribe_message(Lane<K>& L) {
+  const uint32_t eord = L.pm_y & 0xFFFF, part = L.pm_x >> 16, corr = L.pm_z, nb = L.pm_w;
+  emit_msg(L, C_PMS_DELETING, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, corr, nb, part,
+           (L.pm_x >> 14) & 1, L.pm_x & 0xFFF);
+  L.pm_x |= 3u << 12;
+  const uint32_t name_only = (nb & 0xFFFF) | 0xFFFF0000u;
+  if ((int32_t)part == L.sp->partition_id) {
+    emit_msg(L, C_MS_DELETE, -1, iref(L, eord), iref(L, 0), -1, ZBHIP_NO_STRING, name_only, 0, 1, kNoElem);
+    L.lq_slot = corr;
+    L.lq_name_bpmn = nb;
+    L.lq_eord = eord;
+    L.lq_eik = cref_inst(L, eord);
+    L.lq_pik = L.pik;
+    push_local(L, LQ_MS_DELETE);
+  } else {
+    send_xpart(L, ZBHIP_CMD_MSG_SUB_DELETE, part, cref_inst(L, eord), L.pik, -1, corr, L.inst, eord, name_only, 1);
+  }
+}
+
+// MessageSubscriptionDeleteProcessor.processRecord (processing/message/MessageSubscriptionDeleteProcessor.java:50-68):
+// MESSAGE_SUBSCRIPTION:DELETED with the stored subscription (MessageSubscriptionDeletedApplier removes the
+// row at commit), then the acknowledgement PROCESS_MESSAGE_SUBSCRIPTION:DELETE (closeProcessMessageSubscription,
+// SubscriptionCommandSender.java:267-283).  No such subscription (NOT_FOUND) is outside the subset.
+template <class K>
+__device__ __forceinline__ void ms_delete(Lane<K>& L, uint32_t slot, uint32_t pi_part, uint32_t inst, uint32_t eord,
+                                          uint32_t nb, long long eik_p, long long pik_p, long long eik, long long pik) {
+  const StepParams& P = *L.sp;
+  const int r = slot < P.st.n_slots ? find_row(L, slot, pi_part, inst, eord, nb & 0xFFFF) : -1;
+  if (r < 0 || r == kSubs) { set_fail(L, FB_MESSAGE); return; }
+  const size_t ri = sub_ri(r, slot);
+  const uint4 a = P.st.sub_a[ri];
+  const longlong2 b = P.st.sub_b[ri];
+  const longlong2 k = P.st.sub_k[ri];
+  const long long msg = (L.op_corr_mask >> r) & 1 ? L.op_corr_msg : k.y;
+  emit_msg(L, C_MS_DELETED, k.x, b.x, b.y, msg, slot, a.y, 0, (a.x >> 8) & 1, kNoElem);
+  if (L.op_rm_mask && L.op_rm_slot != slot) { set_fail(L, FB_MESSAGE); return; }
+  L.op_rm_mask |= 1u << r;
+  L.op_rm_slot = slot;
+  const uint32_t name_only = (nb & 0xFFFF) | 0xFFFF0000u;
+  if ((int32_t)pi_part == P.partition_id) {
+    emit_msg(L, C_PMS_DELETE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, name_only, (uint32_t)P.partition_id, 1, kNoElem);
+    L.lq_eord = eord;
+    L.lq_name_bpmn = nb;
+    L.lq_eik = eik;
+    L.lq_pik = pik;
+    L.lq_row = inst;
+    push_local(L, LQ_PMS_DELETE);
+  } else {
+    send_xpart(L, ZBHIP_CMD_PMS_DELETE, pi_part, eik, pik, -1, ZBHIP_NO_STRING, inst, eord, name_only, 1);
+  }
+}
+
+// ProcessMessageSubscriptionDeleteProcessor.processRecord (processing/message/
+// ProcessMessageSubscriptionDeleteProcessor.java:39-56): PROCESS_MESSAGE_SUBSCRIPTION:DELETED with the stored
+// subscription (ProcessMessageSubscriptionDeletedApplier removes it) -- also after the instance ended
+template <class K>
+__device__ __forceinline__ void pms_delete(Lane<K>& L, uint32_t eord, uint32_t name) {
+  const uint32_t st = (L.pm_x >> 12) & 3;
+  if (st == 0 || (L.pm_y & 0xFFFF) != eord || (L.pm_w & 0xFFFF) != name) { set_fail(L, FB_MESSAGE); return; }
+  emit_msg(L, C_PMS_DELETED, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, L.pm_z, L.pm_w, L.pm_x >> 16,
+           (L.pm_x >> 14) & 1, L.pm_x & 0xFFF);
+  L.pm_x = L.pm_y = L.pm_z = L.pm_w = 0;
 }
 
 // sort key of a subscription's element instance key for the visit order of
@@ -1421,7 +1507,13 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
     emit(L, C_JOB_CANCELED, job, key, elem, (e.y >> 25) & 1u);
     if ((e.y >> 25) & 1u) note_activation(L, job, L.inst);
   }
-  if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == key) cancel_timer(L);
+  if constexpr (K::S) {  // unsubscribeFromEvents: the timer, then message subscriptions
+    if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == key) cancel_timer(L);
+  }
+  if constexpr (K::M) {
+    if (((L.pm_x >> 12) & 3) != 0 && (L.pm_y & 0xFFFF) == key) unsubscribe_message(L);
+    if (L.fail) return;
+  }
   const uint32_t c = scope_of<K>(w);
   const uint32_t fst = c == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, c)).y >> 16) & 0xFF;
   const uint32_t target = w.w & 0xFFFF;  // the activity's boundary event
@@ -1479,6 +1571,12 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     }
     if (entry & Q_TERM) {
       if (complete) activate_batch(L, elem, w);  // PROCESS_INSTANCE_BATCH:ACTIVATE of a body
+      else terminate_pi(L, elem, w, cmd_key, fsa);
+      return;
+    }
+  } else if constexpr (K::M) {
+    if (entry & Q_TERM) {  // TERMINATE_ELEMENT of an activity whose message boundary event was triggered
+      if (complete) set_fail(L, FB_UNSUPPORTED);
       else terminate_pi(L, elem, w, cmd_key, fsa);
       return;
     }
@@ -1583,6 +1681,16 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
             emit(L, C_TIMER_CREATED, tk, key, b, reps);
           }
         }
+        if constexpr (K::M) {
+          // subscribeToEvents: the attached message boundary event's subscription before the job
+          const uint32_t b = w.w & 0xFFFF;
+          if (b != 0xFFFF) {
+            const uint4 bw = elem_of(L, b);
+            if (((bw.x >> 8) & 0xFF) != ZBHIP_EV_MESSAGE) { set_fail(L, FB_UNSUPPORTED); return; }
+            subscribe_message(L, b, bw, key, true);
+            if (L.fail) return;
+          }
+        }
         uint32_t job = new_key(L);     // BpmnJobBehavior.writeJobCreatedEvent (:194-218)
         emit(L, C_JOB_CREATED, job, key, elem);
         uint2 e = tget(L, t);   // JobCreatedApplier: element instance jobKey
@@ -1615,6 +1723,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       }
       case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT:  // IntermediateCatchEventProcessor.onActivate
         if constexpr (K::M) {
+          if (((w.x >> 8) & 0xFF) != ZBHIP_EV_MESSAGE) { set_fail(L, FB_UNSUPPORTED); return; }
           subscribe_message(L, elem, w, key);
           if (L.fail) return;
           emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
@@ -1723,7 +1832,9 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       // IntermediateCatchEventProcessor.onComplete -> unsubscribeFromEvents: a subscription still
       // open here would write PROCESS_MESSAGE_SUBSCRIPTION:DELETING (outside the subset)
       if (((L.pm_x >> 12) & 3) != 0 && (L.pm_y & 0xFFFF) == cmd_key) { set_fail(L, FB_MESSAGE); return; }
-    } else if (type != ZBHIP_EL_START_EVENT && !ZBHIP_IS_JOB_WORKER(type) && !pass_through(type)) {
+    } else if (type != ZBHIP_EL_START_EVENT && !ZBHIP_IS_JOB_WORKER(type) && !pass_through(type) &&
+               type != ZBHIP_EL_BOUNDARY_EVENT) {
+      // BoundaryEventProcessor.onComplete (event/BoundaryEventProcessor.java:47-56): no mappings
       set_fail(L, FB_UNSUPPORTED);
       return;
     }
@@ -1772,6 +1883,11 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   if constexpr (K::S) {
     // JobWorkerTaskProcessor.onComplete (:63-75): unsubscribeFromEvents -- the boundary event's timer
     if (ZBHIP_IS_JOB_WORKER(type) && (L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) cancel_timer(L);
+  }
+  if constexpr (K::M) {
+    // JobWorkerTaskProcessor.onComplete: unsubscribeFromEvents -- the boundary event's subscription
+    if (ZBHIP_IS_JOB_WORKER(type) && ((L.pm_x >> 12) & 3) != 0 && (L.pm_y & 0xFFFF) == cmd_key) unsubscribe_message(L);
+    if (L.fail) return;
   }
   transition_to_completed_child(L, t, elem, w, cmd_key);
   take_outgoing(L, w);
@@ -2089,6 +2205,7 @@ __device__ __forceinline__ void load_instance_mid(Lane<K>& L, uint32_t inst) {
   L.pm_x = pm.x;
   L.pm_y = pm.y;
   L.pm_z = pm.z;
+  L.pm_w = pm.w;
   L.pik = P.st.pi_key[inst];
   vm_drain();
 }
@@ -2119,6 +2236,13 @@ __device__ __forceinline__ void process_local(Lane<K>& L, uint32_t kind) {
     case LQ_MS_CORRELATE:
       ms_correlate(L, L.lq_slot, own, L.lq_row, L.lq_eord, L.lq_name_bpmn, L.lq_eik, L.lq_pik);
       return;
+    case LQ_MS_DELETE:  // from an activity of the loaded instance closing its subscription
+      ms_delete(L, L.lq_slot, own, L.inst, L.lq_eord, L.lq_name_bpmn, iref(L, L.lq_eord), iref(L, 0), L.lq_eik, L.lq_pik);
+      return;
+    case LQ_PMS_DELETE:  // the acknowledgement, back on the subscriber's instance (loaded: it sent the DELETE)
+      if (L.inst != L.lq_row) { set_fail(L, FB_MESSAGE); return; }
+      pms_delete(L, L.lq_eord, L.lq_name_bpmn & 0xFFFF);
+      return;
     default:
       set_fail(L, FB_UNSUPPORTED);
   }
@@ -2148,6 +2272,13 @@ __device__ __forceinline__ void message_command(Lane<K>& L, uint32_t kind, uint3
       if (L.proc == NONE) { set_fail(L, FB_MESSAGE); return; }
       pms_correlate(L, x.element_ord, nb, x.element_instance_key, x.process_instance_key, x.message_key,
                     x.correlation_key, src, x.element_instance_key, x.process_instance_key);
+      return;
+    case ZBHIP_CMD_MSG_SUB_DELETE:
+      ms_delete(L, subject, src, x.instance, x.element_ord, nb, x.element_instance_key, x.process_instance_key,
+                x.element_instance_key, x.process_instance_key);
+      return;
+    case ZBHIP_CMD_PMS_DELETE:
+      pms_delete(L, x.element_ord, x.message_name);
       return;
     default:
       set_fail(L, FB_UNSUPPORTED);
@@ -2280,7 +2411,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if constexpr (K::M) {
     L.prog = prog;
     L.inst = inst;
-    L.pm_x = L.pm_y = L.pm_z = 0;
+    L.pm_x = L.pm_y = L.pm_z = L.pm_w = 0;
     L.pik = -1;
     L.slot_lane = false;
     L.slot = 0;
@@ -2296,7 +2427,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     L.ins_eik = L.ins_pik = L.ins_key = -1;
     L.op_corr_mask = L.op_rm_mask = L.op_rm_slot = 0;
     L.op_corr_msg = -1;
-    slot_kind = kind == ZBHIP_CMD_PUBLISH || kind == ZBHIP_CMD_MSG_SUB_CREATE || kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
+    slot_kind = zb_slot_kind(kind);
   }
 
   const bool bad_cmd = (slot_kind ? inst >= P.st.n_slots : inst >= N) ||
@@ -2338,7 +2469,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     L.pi_live = false;
   } else if (kind == ZBHIP_CMD_CREATE) {
     // CreateProcessInstanceProcessor.createProcessInstance (:129-158)
-    if (L.proc != NONE) set_fail(L, FB_SLOT_IN_USE);
+    if (L.proc != NONE || ((h.y >> 25) & 1)) set_fail(L, FB_SLOT_IN_USE);
     else if (ref >= P.n_procs) set_fail(L, FB_BAD_PROCESS);
     L.proc = ref;
     L.next_ord = 0;
@@ -2372,11 +2503,12 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     if (!bad_cmd && !slot_kind) {
       if (kind == ZBHIP_CMD_CREATE) {
         L.pik = ref_cmd(ci, false, 0);
-      } else if (L.proc != NONE) {
+      } else if (L.proc != NONE || ((h.y >> 25) & 1)) {  // (an ended instance: its closing subscription)
         const uint4 pm = P.st.pms[inst];
         L.pm_x = pm.x;
         L.pm_y = pm.y;
         L.pm_z = pm.z;
+        L.pm_w = pm.w;
         L.pik = P.st.pi_key[inst];
         vm_drain();
       }
@@ -2558,8 +2690,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     P.st.join[(size_t)3 * N + winst] = live ? L.jw3 : 0u;
   }
   if constexpr (K::M) {
-    if (ok && winst != kNoInst) P.st.pms[winst] = make_uint4(L.pi_live ? L.pm_x : 0u, L.pi_live ? L.pm_y : 0u,
-                                                             L.pi_live ? L.pm_z : 0u, 0u);
+    // an ended instance keeps a closing subscription until its PROCESS_MESSAGE_SUBSCRIPTION:DELETE
+    const bool keep = L.pi_live || ((L.pm_x >> 12) & 3) == 3;
+    if (ok && winst != kNoInst) P.st.pms[winst] = keep ? make_uint4(L.pm_x, L.pm_y, L.pm_z, L.pm_w) : make_uint4(0, 0, 0, 0);
   }
   if constexpr (K::S) {
     if (ok && winst != kNoInst && L.has_tmr) {
@@ -2570,12 +2703,15 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   }
   if (ok && winst != kNoInst) {
     // a completed instance frees its slot (rows removed with the instance) but keeps next_ord,
-    // so late commands for the instance relabel consistently
+    // so late commands for the instance relabel consistently; bit 25: a closing subscription waits
+    // for its PROCESS_MESSAGE_SUBSCRIPTION:DELETE (the slot is not free for a CREATE yet)
     const bool live = L.pi_live;
+    bool pms_pending = false;
+    if constexpr (K::M) pms_pending = ((L.pm_x >> 12) & 3) == 3;
     P.st.hdr[winst] = live ? make_uint4(L.proc | ((uint32_t)L.next_ord << 16),
                                        L.pi_state | (ns << 8) | ((uint32_t)L.nvars << 16) | (1u << 24),
                                        (uint32_t)L.pi_child | ((uint32_t)L.pi_asf << 16), 0)
-                          : make_uint4(0xFFFFu | ((uint32_t)L.next_ord << 16), 0, 0, 0);
+                          : make_uint4(0xFFFFu | ((uint32_t)L.next_ord << 16), pms_pending ? (1u << 25) : 0u, 0, 0);
   }
   uint32_t nkeys = ok ? (uint16_t)(L.next_ord - L.first_ord) : 0u;
   uint32_t first = L.first_ord, npay = 0;
@@ -3240,7 +3376,7 @@ __global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp,
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const zbhip_xpart_cmd x = xp[i];
-  const bool pms = x.kind == ZBHIP_CMD_PMS_CREATE || x.kind == ZBHIP_CMD_PMS_CORRELATE;
+  const bool pms = zb_pms_kind(x.kind);
   cmds[i] = make_uint4(pms ? x.instance : x.correlation_key, x.kind, i, 0);  // zbhip_command layout
 }
 
@@ -3255,8 +3391,10 @@ __global__ __launch_bounds__(256) void k_subject_check(const uint4* cmds, uint32
   if (i < n) {
     const uint4 c = cmds[i];
     const uint32_t kind = c.y & 0xFF;
-    const bool sk = kind == ZBHIP_CMD_PUBLISH || kind == ZBHIP_CMD_MSG_SUB_CREATE || kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
-    if (kind < ZBHIP_CMD_CREATE || kind > ZBHIP_CMD_MSG_SUB_CORRELATE || (sk ? c.x >= n_slots : c.x >= n_inst)) {
+    const bool sk = zb_slot_kind(kind);
+    const bool known = (kind >= ZBHIP_CMD_CREATE && kind <= ZBHIP_CMD_MSG_SUB_CORRELATE) || kind == ZBHIP_CMD_MSG_SUB_DELETE ||
+                       kind == ZBHIP_CMD_PMS_DELETE;
+    if (!known || (sk ? c.x >= n_slots : c.x >= n_inst)) {
       f = 2;
     } else if (atomicExch(&seen[(sk ? n_inst : 0u) + c.x], stamp) == stamp) {
       f = 1;
@@ -3276,7 +3414,7 @@ __global__ __launch_bounds__(256) void k_subject_keys(const uint4* cmds, uint32_
   if (i >= n) return;
   const uint4 c = cmds[i];
   const uint32_t kind = c.y & 0xFF;
-  const bool sk = kind == ZBHIP_CMD_PUBLISH || kind == ZBHIP_CMD_MSG_SUB_CREATE || kind == ZBHIP_CMD_MSG_SUB_CORRELATE;
+  const bool sk = zb_slot_kind(kind);
   keys[i] = (sk ? n_inst : 0u) + c.x;
   idx[i] = i;
 }

@@ -1129,11 +1129,11 @@ static int rebuild_program(zbhip_handle* h) {
       if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW) w[2] = E.flow_target | ((uint32_t)E.condition << 16);
       else if (E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY) w[2] = E.default_flow | (0xFFFFu << 16);
       else if (ZBHIP_IS_JOB_WORKER(E.element_type)) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
-      else if ((E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && E.event_type == ZBHIP_EV_TIMER) ||
-               E.element_type == ZBHIP_EL_BOUNDARY_EVENT)
-        w[2] = E.duration_ms;
-      else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT)
+      else if ((E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT) &&
+               E.event_type == ZBHIP_EV_MESSAGE)
         w[2] = E.message_name | ((uint32_t)E.correlation_var << 16);  // name ids (zbhip_deploy)
+      else if (E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT)
+        w[2] = E.duration_ms;
       else if (E.element_type == ZBHIP_EL_SUB_PROCESS) w[2] = E.start_event | (join_mask[e] << 16);
       else w[2] = 0xFFFFFFFFu;
       // a job worker's join_slot half: its boundary event (zbhip_element.start_event), 0xFFFF if none
@@ -1231,10 +1231,12 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       return ZBHIP_EINVAL;
   }
   for (auto& e : P.els)
-    if ((e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && e.event_type == ZBHIP_EV_TIMER) ||
-        e.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
+    if ((e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || e.element_type == ZBHIP_EL_BOUNDARY_EVENT) &&
+        e.event_type == ZBHIP_EV_TIMER) {
       P.has_timer = true;
-    } else if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+    } else if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || e.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
+      // message catch events and message boundary events (KMsg)
+      if (e.event_type != ZBHIP_EV_MESSAGE) return ZBHIP_EINVAL;
       if (!h->st.n_slots) return ZBHIP_EUNSUPP;  // the handle was opened without message state
       if (e.message_name >= P.strings.size() || e.correlation_var >= P.strings.size()) return ZBHIP_EINVAL;
       P.has_msg = true;
@@ -1288,7 +1290,9 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   // oracle's order): the name dictionary is replicated across partitions by deploy order
   if (P.has_msg) {
     for (auto& e : P.els) {
-      if (e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || e.event_type != ZBHIP_EV_MESSAGE) continue;
+      if ((e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT && e.element_type != ZBHIP_EL_BOUNDARY_EVENT) ||
+          e.event_type != ZBHIP_EV_MESSAGE)
+        continue;
       int mn = zbhip_intern(h, P.strings[e.message_name].c_str());
       int cv = zbhip_intern(h, P.strings[e.correlation_var].c_str());
       if (mn < 0 || cv < 0) return ZBHIP_ENOMEM;
@@ -1421,9 +1425,7 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   return ZBHIP_OK;
 }
 
-static bool slot_kind(uint8_t k) {
-  return k == ZBHIP_CMD_PUBLISH || k == ZBHIP_CMD_MSG_SUB_CREATE || k == ZBHIP_CMD_MSG_SUB_CORRELATE;
-}
+static bool slot_kind(uint8_t k) { return zb_slot_kind(k); }
 
 // Splits the window into rounds so that each subject (instance slot; correlation slot for message
 // commands) appears at most once per launch; commands of one subject keep their log order across
@@ -1533,7 +1535,7 @@ static int validate(zbhip_handle* h, const zbhip_command* cmds, size_t n, size_t
                     const zbhip_xpart_cmd* xp, size_t n_xp) {
   for (size_t i = 0; i < n; ++i) {
     const zbhip_command& c = cmds[i];
-    if (slot_kind(c.kind) || c.kind == ZBHIP_CMD_PMS_CREATE || c.kind == ZBHIP_CMD_PMS_CORRELATE) {
+    if (slot_kind(c.kind) || zb_pms_kind(c.kind)) {
       if (!h->msg()) return ZBHIP_EUNSUPP;
       if (c.doc_count) return ZBHIP_EINVAL;
       if (slot_kind(c.kind) ? c.instance >= h->st.n_slots : c.instance >= h->cfg.max_instances) return ZBHIP_EINVAL;
@@ -2551,6 +2553,11 @@ static bool message_code(uint32_t c6, zbhip_record& r) {
     case C_MS_CORRELATING: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CORRELATING; r.record_type = ZBHIP_RT_EVENT; return true;
     case C_MS_CORRELATE: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CORRELATE; r.record_type = ZBHIP_RT_COMMAND; return true;
     case C_MS_CORRELATED: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_CORRELATED; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_PMS_DELETING: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_DELETING; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_PMS_DELETE: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_DELETE; r.record_type = ZBHIP_RT_COMMAND; return true;
+    case C_PMS_DELETED: r.value_type = ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_PMS_DELETED; r.record_type = ZBHIP_RT_EVENT; return true;
+    case C_MS_DELETE: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_DELETE; r.record_type = ZBHIP_RT_COMMAND; return true;
+    case C_MS_DELETED: r.value_type = ZBHIP_VT_MESSAGE_SUBSCRIPTION; r.intent = ZBHIP_MS_DELETED; r.record_type = ZBHIP_RT_EVENT; return true;
     case C_MSG_PUBLISHED: r.value_type = ZBHIP_VT_MESSAGE; r.intent = ZBHIP_MSG_PUBLISHED; r.record_type = ZBHIP_RT_EVENT; return true;
     case C_MSG_EXPIRED: r.value_type = ZBHIP_VT_MESSAGE; r.intent = ZBHIP_MSG_EXPIRED; r.record_type = ZBHIP_RT_EVENT; return true;
     default: return false;
@@ -3163,13 +3170,39 @@ struct InstRows {  // the SoA rows of one instance slot
 };
 }  // namespace
 
+// PROCESS_SUBSCRIPTION_BY_KEY [eik, name] (DbProcessMessageSubscriptionState) of an instance slot's
+// subscription row -- also after the instance ended, while a closing subscription waits for its
+// PROCESS_MESSAGE_SUBSCRIPTION:DELETE
+static void emit_pms(zbhip_handle* h, uint32_t inst, const InstRows& R, const Proc& P, long long pik,
+                     zbhip_state_sink sink, void* ctx) {
+  char buf[768];
+  if (R.has_pms && ((R.pms.x >> 12) & 3)) {  // PROCESS_SUBSCRIPTION_BY_KEY [eik, name] (DbProcessMessageSubscriptionState)
+    const uint4 m = R.pms;
+    const uint32_t el = m.x & 0xFFF;
+    const zbhip_element& E = P.els[el];
+    snprintf(buf, sizeof buf,
+             "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%u,processInstanceKey=%lld,"
+             "bpmnProcessId=%s,messageKey=-1,correlationKey=%s,elementId=%s,interrupting=%u",
+             h->key_of(inst, m.y & 0xFFFF), zbhip_name(h, E.message_name), h->key_of(inst, m.y >> 16),
+             ((m.x >> 12) & 3) == 1 ? "OPENING" : ((m.x >> 12) & 3) == 3 ? "CLOSING" : "OPENED", m.x >> 16, pik, zbhip_name(h, P.bpmn_name),
+             zbhip_string_value(h, m.z, nullptr), P.id(el).c_str(), (m.x >> 14) & 1);
+    sink(ctx, buf);
+  }
+}
+
 // the rows of one process instance (ELEMENT_INSTANCE_KEY ... NUMBER_OF_TAKEN_SEQUENCE_FLOWS,
 // PROCESS_SUBSCRIPTION_BY_KEY); nothing for a free slot
 static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbhip_state_sink sink, void* ctx) {
   char buf[768];
   const uint4 hd = R.hdr;
+  if (!((hd.y >> 24) & 1)) {  // an ended instance: only a subscription still closing (header bit 25)
+    const uint32_t ip = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
+    if (((hd.y >> 25) & 1) && ip != NONE && ip < h->procs.size())
+      emit_pms(h, inst, R, h->procs[ip], h->key_of(inst, 0), sink, ctx);
+    return;
+  }
   const uint32_t proc = hd.x & 0xFFFF;
-  if (proc == NONE || !((hd.y >> 24) & 1) || proc >= h->procs.size()) return;
+  if (proc == NONE || proc >= h->procs.size()) return;
   const Proc& P = h->procs[proc];
   const long long pik = h->key_of(inst, 0);
   const uint32_t nslots = (hd.y >> 8) & 0xFF, nvars = (hd.y >> 16) & 0xFF;
@@ -3303,18 +3336,7 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     snprintf(buf, sizeof buf, "TIMER_DUE_DATES|%lld|%lld|%lld", due, eik, tk);
     sink(ctx, buf);
   }
-  if (R.has_pms && ((R.pms.x >> 12) & 3)) {  // PROCESS_SUBSCRIPTION_BY_KEY [eik, name] (DbProcessMessageSubscriptionState)
-    const uint4 m = R.pms;
-    const uint32_t el = m.x & 0xFFF;
-    const zbhip_element& E = P.els[el];
-    snprintf(buf, sizeof buf,
-             "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%u,processInstanceKey=%lld,"
-             "bpmnProcessId=%s,messageKey=-1,correlationKey=%s,elementId=%s,interrupting=%u",
-             h->key_of(inst, m.y & 0xFFFF), zbhip_name(h, E.message_name), h->key_of(inst, m.y >> 16),
-             ((m.x >> 12) & 3) == 1 ? "OPENING" : "OPENED", m.x >> 16, pik, zbhip_name(h, P.bpmn_name),
-             zbhip_string_value(h, m.z, nullptr), P.id(el).c_str(), (m.x >> 14) & 1);
-    sink(ctx, buf);
-  }
+  emit_pms(h, inst, R, P, pik, sink, ctx);
   if (P.n_join_slots) {
     for (uint32_t f = 0; f < P.els.size(); ++f) {
       const zbhip_element& E = P.els[f];
@@ -3658,6 +3680,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       m.eik = to_ll(p[1]);
       m.name = p[2];
       m.key = to_ll(f["key"]);
+      // a closing subscription (its element instance may be gone) is outside the import subset
+      if (f["state"] == "CLOSING") return ZBHIP_EUNSUPP;
       m.state = f["state"] == "OPENING" ? 1u : 2u;
       m.part = (uint32_t)to_ll(f["subscriptionPartitionId"]);
       m.corr = f["correlationKey"];

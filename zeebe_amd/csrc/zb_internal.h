@@ -32,6 +32,15 @@ constexpr uint32_t TPL_OK = 1u << 31;        // program header word 7: bit 31 el
 // row r of correlation slot s in sub_a / sub_b / sub_k: slot-major, so a slot's kSubs rows share
 // one cache line per array (a lookup reads 3 lines, not 3 * kSubs)
 __host__ __device__ inline size_t sub_ri(uint32_t r, size_t slot) { return slot * kSubs + r; }
+// command kinds whose subject is a correlation slot (MESSAGE / MESSAGE_SUBSCRIPTION commands), and
+// the PROCESS_MESSAGE_SUBSCRIPTION commands (subject: an instance slot)
+__host__ __device__ inline bool zb_slot_kind(uint32_t k) {
+  return k == ZBHIP_CMD_PUBLISH || k == ZBHIP_CMD_MSG_SUB_CREATE || k == ZBHIP_CMD_MSG_SUB_CORRELATE ||
+         k == ZBHIP_CMD_MSG_SUB_DELETE;
+}
+__host__ __device__ inline bool zb_pms_kind(uint32_t k) {
+  return k == ZBHIP_CMD_PMS_CREATE || k == ZBHIP_CMD_PMS_CORRELATE || k == ZBHIP_CMD_PMS_DELETE;
+}
 constexpr int kOut = 6;            // outbox entries per command (sends + local-row key patches)
 constexpr uint8_t XK_PATCH = 0xFF; // outbox entry kind: patch the real keys of a locally inserted row
 constexpr uint32_t kNoElem = 0xFFF;       // element field of records without an element
@@ -79,11 +88,16 @@ enum : uint8_t {
   C_PMS_CREATED = 34,
   C_PMS_CORRELATE = 35,
   C_PMS_CORRELATED = 36,
+  C_PMS_DELETING = 37,    // CatchEventBehavior.unsubscribeFromMessageEvent (the stored subscription)
+  C_PMS_DELETE = 38,      // the acknowledgement command (closeProcessMessageSubscription)
+  C_PMS_DELETED = 39,
   C_MS_CREATE = 40,
   C_MS_CREATED = 41,
   C_MS_CORRELATING = 42,
   C_MS_CORRELATE = 43,
   C_MS_CORRELATED = 44,
+  C_MS_DELETE = 45,       // closeMessageSubscription (command)
+  C_MS_DELETED = 46,
   C_MSG_PUBLISHED = 49,
   C_MSG_EXPIRED = 50,
   C_TIMER_CREATED = 52,   // key = timer, aux = element instance, flags = repetitions (255 infinite)

@@ -29,7 +29,7 @@ def window_from_xparts(xp):
     kind = xp["kind"]
     cmds["kind"] = kind
     cmds["doc_begin"] = np.arange(len(xp), dtype=np.uint32)
-    pms = (kind == abi.CMD_PMS_CREATE) | (kind == abi.CMD_PMS_CORRELATE)
+    pms = np.isin(kind, abi.PMS_KINDS)
     cmds["instance"] = np.where(pms, xp["instance"], xp["correlation_key"])
     return cmds, xp
 
