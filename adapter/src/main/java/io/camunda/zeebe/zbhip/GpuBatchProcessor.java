@@ -409,7 +409,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   private void freeEndedSlots() {
     for (final Iterator<Integer> it = ended.iterator(); it.hasNext(); ) {
       final int slot = it.next();
-      if (ZbHip.pendingContinuations(handle, slot) == 0) {
+      if (ZbHip.pendingContinuations(handle, slot) == 0 && (messages == null || !messages.closing(slot))) {
         usedSlots.clear(slot);
         it.remove();
       }

@@ -62,6 +62,9 @@ final class Messages {
   // MESSAGE_SUBSCRIPTION_BY_KEY [elementInstanceKey, messageName] -> correlation slot of an open
   // subscription: a MESSAGE_SUBSCRIPTION:CORRELATE's value carries no correlation key
   private final Map<SubscriptionKey, Integer> subscriptions = new HashMap<>();
+  // (elementInstanceKey, messageName) -> routing handle (slot << 16 | ordinal) of a device subscription
+  private final Map<SubscriptionKey, Long> handles = new HashMap<>();
+  private final java.util.Set<Integer> closingSlots = new java.util.HashSet<>();
 
   private record SubscriptionKey(long elementInstanceKey, String messageName) {}
 
@@ -105,13 +108,19 @@ final class Messages {
       // the process instance partition's side: the subscribing element instance of a device instance
       final ProcessMessageSubscriptionRecord v = (ProcessMessageSubscriptionRecord) record.getValue();
       kind = record.getIntent() == ProcessMessageSubscriptionIntent.CREATE ? ZbHip.CMD_PMS_CREATE
-          : record.getIntent() == ProcessMessageSubscriptionIntent.CORRELATE ? ZbHip.CMD_PMS_CORRELATE : 0;
+          : record.getIntent() == ProcessMessageSubscriptionIntent.CORRELATE ? ZbHip.CMD_PMS_CORRELATE
+          : record.getIntent() == ProcessMessageSubscriptionIntent.DELETE ? ZbHip.CMD_PMS_DELETE : 0;
       if (kind == 0 || v.getVariablesBuffer().capacity() > 1) {
         return null;
       }
       pik = v.getProcessInstanceKey();
       eik = v.getElementInstanceKey();
-      final long pi = p.resolve(pik), el = p.resolve(eik);
+      long pi = p.resolve(pik), el = p.resolve(eik);
+      if ((pi < 0 || el < 0) && kind == ZbHip.CMD_PMS_DELETE) {
+        // a closing subscription's acknowledgement may arrive after its instance ended: the routing
+        // handle kept since PROCESS_MESSAGE_SUBSCRIPTION:CREATING
+        pi = el = handles.getOrDefault(new SubscriptionKey(eik, v.getMessageName()), -1L);
+      }
       if (pi < 0 || el < 0 || (pi >>> 16) != (el >>> 16)) {
         return null;
       }
@@ -124,7 +133,8 @@ final class Messages {
     // the message partition's side
     final MessageSubscriptionRecord v = (MessageSubscriptionRecord) record.getValue();
     kind = record.getIntent() == MessageSubscriptionIntent.CREATE ? ZbHip.CMD_MSG_SUB_CREATE
-        : record.getIntent() == MessageSubscriptionIntent.CORRELATE ? ZbHip.CMD_MSG_SUB_CORRELATE : 0;
+        : record.getIntent() == MessageSubscriptionIntent.CORRELATE ? ZbHip.CMD_MSG_SUB_CORRELATE
+        : record.getIntent() == MessageSubscriptionIntent.DELETE ? ZbHip.CMD_MSG_SUB_DELETE : 0;
     if (kind == 0 || v.getVariablesBuffer().capacity() > 1) {
       return null;
     }
@@ -149,7 +159,8 @@ final class Messages {
       ord = (int) ((n >>> 32) & 0xFFFF);
     }
     int corr = v.getCorrelationKey().isEmpty() ? NO_STRING : (int) p.internString(bytes(v.getCorrelationKeyBuffer()));
-    if (kind == ZbHip.CMD_MSG_SUB_CORRELATE) {
+    if (kind == ZbHip.CMD_MSG_SUB_CORRELATE || kind == ZbHip.CMD_MSG_SUB_DELETE) {
+      // no correlation key in the value: the slot of the subscription it names
       corr = subscriptions.getOrDefault(new SubscriptionKey(eik, v.getMessageName()), 0);
     }
     if (Integer.toUnsignedLong(corr) >= correlationSlots) {
@@ -183,9 +194,34 @@ final class Messages {
     final SubscriptionKey k = new SubscriptionKey(v.getElementInstanceKey(), v.getMessageName());
     if (intent == MessageSubscriptionIntent.CREATED) {
       subscriptions.put(k, correlationSlot);
-    } else if (intent == MessageSubscriptionIntent.CORRELATED) {
+    } else if (intent == MessageSubscriptionIntent.CORRELATED || intent == MessageSubscriptionIntent.DELETED) {
       subscriptions.remove(k);
     }
+  }
+
+  /**
+   * An emitted PROCESS_MESSAGE_SUBSCRIPTION event of instance slot `slot`: the routing handle of a device
+   * subscription is kept from CREATING until it is gone, and a slot with a closing subscription stays
+   * taken until its DELETED (the device row outlives the instance).
+   */
+  void onProcessSubscriptionEvent(final Intent intent, final ProcessMessageSubscriptionRecord v, final int slot,
+      final GpuBatchProcessor p) {
+    final SubscriptionKey k = new SubscriptionKey(v.getElementInstanceKey(), v.getMessageName());
+    if (intent == ProcessMessageSubscriptionIntent.CREATING) {
+      handles.put(k, p.resolve(v.getElementInstanceKey()));
+    } else if (intent == ProcessMessageSubscriptionIntent.DELETING) {
+      closingSlots.add(slot);
+    } else if (intent == ProcessMessageSubscriptionIntent.CORRELATED || intent == ProcessMessageSubscriptionIntent.DELETED) {
+      handles.remove(k);
+      if (intent == ProcessMessageSubscriptionIntent.DELETED) {
+        closingSlots.remove(slot);
+      }
+    }
+  }
+
+  /** Whether the instance slot waits for a closing subscription's PROCESS_MESSAGE_SUBSCRIPTION:DELETE. */
+  boolean closing(final int slot) {
+    return closingSlots.contains(slot);
   }
 
   /** Window command i's sends, handed to InterPartitionCommandSender once its batch is committed. */
@@ -213,8 +249,8 @@ final class Messages {
   }
 
   static ValueType valueType(final byte kind) {
-    return kind == ZbHip.CMD_MSG_SUB_CREATE || kind == ZbHip.CMD_MSG_SUB_CORRELATE ? ValueType.MESSAGE_SUBSCRIPTION
-        : ValueType.PROCESS_MESSAGE_SUBSCRIPTION;
+    return kind == ZbHip.CMD_MSG_SUB_CREATE || kind == ZbHip.CMD_MSG_SUB_CORRELATE || kind == ZbHip.CMD_MSG_SUB_DELETE
+        ? ValueType.MESSAGE_SUBSCRIPTION : ValueType.PROCESS_MESSAGE_SUBSCRIPTION;
   }
 
   static Intent intent(final byte kind) {
@@ -222,6 +258,8 @@ final class Messages {
       case ZbHip.CMD_MSG_SUB_CREATE -> MessageSubscriptionIntent.CREATE;
       case ZbHip.CMD_MSG_SUB_CORRELATE -> MessageSubscriptionIntent.CORRELATE;
       case ZbHip.CMD_PMS_CREATE -> ProcessMessageSubscriptionIntent.CREATE;
+      case ZbHip.CMD_MSG_SUB_DELETE -> MessageSubscriptionIntent.DELETE;
+      case ZbHip.CMD_PMS_DELETE -> ProcessMessageSubscriptionIntent.DELETE;
       default -> ProcessMessageSubscriptionIntent.CORRELATE;
     };
   }
@@ -247,6 +285,12 @@ final class Messages {
       case ZbHip.CMD_MSG_SUB_CORRELATE: // correlateMessageSubscription
         return new MessageSubscriptionRecord().setProcessInstanceKey(pik).setElementInstanceKey(eik)
             .setBpmnProcessId(bpmn).setMessageKey(-1).setMessageName(name).setTenantId(TENANT);
+      case ZbHip.CMD_MSG_SUB_DELETE: // closeMessageSubscription (:220-236)
+        return new MessageSubscriptionRecord().setProcessInstanceKey(pik).setElementInstanceKey(eik)
+            .setMessageKey(-1).setMessageName(name).setTenantId(TENANT);
+      case ZbHip.CMD_PMS_DELETE: // closeProcessMessageSubscription (:267-283)
+        return new ProcessMessageSubscriptionRecord().setSubscriptionPartitionId(sender).setProcessInstanceKey(pik)
+            .setElementInstanceKey(eik).setMessageKey(-1).setMessageName(name).setTenantId(TENANT);
       case ZbHip.CMD_PMS_CREATE: // openProcessMessageSubscription
         return new ProcessMessageSubscriptionRecord().setSubscriptionPartitionId(sender).setProcessInstanceKey(pik)
             .setElementInstanceKey(eik).setMessageKey(-1).setMessageName(name).setInterrupting(interrupting)

@@ -357,6 +357,8 @@ final class Window {
         p.instanceEnded(instances[i]); // the process element (index 0) completed
       } else if (valueType == ValueType.MESSAGE_SUBSCRIPTION.value() && recordType == RecordType.EVENT.value()) {
         p.messages().onSubscriptionEvent(meta.getIntent(), (MessageSubscriptionRecord) value, rec.get(JAVA_INT, 64));
+      } else if (valueType == ValueType.PROCESS_MESSAGE_SUBSCRIPTION.value() && recordType == RecordType.EVENT.value()) {
+        p.messages().onProcessSubscriptionEvent(meta.getIntent(), (ProcessMessageSubscriptionRecord) value, instances[i], p);
       }
     }
     return admitted;

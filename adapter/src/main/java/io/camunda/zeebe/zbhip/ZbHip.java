@@ -48,6 +48,8 @@ public final class ZbHip {
   public static final byte CMD_PMS_CREATE = 5;
   public static final byte CMD_PMS_CORRELATE = 6;
   public static final byte CMD_MSG_SUB_CORRELATE = 7;
+  public static final byte CMD_MSG_SUB_DELETE = 10; // closeMessageSubscription
+  public static final byte CMD_PMS_DELETE = 11; // closeProcessMessageSubscription (the acknowledgement)
 
   public static final int RUN_DEVICE_RECORDS = 8;
 

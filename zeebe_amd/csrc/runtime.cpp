@@ -1207,11 +1207,13 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         e.element_type != ZBHIP_EL_SUB_PROCESS && e.element_type != ZBHIP_EL_BOUNDARY_EVENT &&
         e.element_type != ZBHIP_EL_MULTI_INSTANCE_BODY && !pass_through(e.element_type))
       return ZBHIP_EUNSUPP;
-  // interrupting timer boundary events: one per job worker task, in the task's container
+  // timer boundary events and interrupting message boundary events: one per job worker task, in the
+  // task's container (message boundary events: the process's, KMsg has no flow scopes)
   for (size_t e = 0; e < P.els.size(); ++e) {
     const zbhip_element& E = P.els[e];
     if (E.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
-      if (E.event_type != ZBHIP_EV_TIMER || E.flow_source >= P.els.size()) return ZBHIP_EUNSUPP;
+      const bool msg = E.event_type == ZBHIP_EV_MESSAGE && (E.job_retries & 1) && E.flow_scope == 0;
+      if ((E.event_type != ZBHIP_EV_TIMER && !msg) || E.flow_source >= P.els.size()) return ZBHIP_EUNSUPP;
       const zbhip_element& A = P.els[E.flow_source];
       if (!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e || A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
     } else if (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) {
