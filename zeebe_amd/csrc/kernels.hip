@@ -914,7 +914,7 @@ __device__ __forceinline__ void apply_activating_child(Lane<K>& L, uint32_t elem
   }
   tbl_insert(L, elem, key, ZBHIP_PI_ELEMENT_ACTIVATING);
   ++L.pi_child;
-  if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_BOUNDARY_EVENT) {  // not reached by a sequence flow
+  if (type == ZBHIP_EL_START_EVENT || (K::M && type == ZBHIP_EL_BOUNDARY_EVENT)) {  // not reached by a sequence flow
   } else if (type == ZBHIP_EL_PARALLEL_GATEWAY) {
     int n = (int)(w.x >> 16);
     L.pi_asf = L.pi_asf > n ? L.pi_asf - n : 0;  // decrementActiveSequenceFlows clamps at 0
@@ -2248,6 +2248,10 @@ __device__ __forceinline__ void process_local(Lane<K>& L, uint32_t kind) {
   }
 }
 
+// an ended instance's header whose closing subscription waits for its PROCESS_MESSAGE_SUBSCRIPTION:DELETE
+// (k_step's commit; a never-used slot's header is all ones)
+__device__ __forceinline__ bool closing_pending(uint4 h) { return (h.x & 0xFFFF) == 0xFFFF && h.y == (1u << 25); }
+
 // the initial command of a batch that is a message / subscription command
 template <class K>
 __device__ __forceinline__ void message_command(Lane<K>& L, uint32_t kind, uint32_t subject, uint32_t ref, uint32_t xi) {
@@ -2469,7 +2473,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     L.pi_live = false;
   } else if (kind == ZBHIP_CMD_CREATE) {
     // CreateProcessInstanceProcessor.createProcessInstance (:129-158)
-    if (L.proc != NONE || ((h.y >> 25) & 1)) set_fail(L, FB_SLOT_IN_USE);
+    if (L.proc != NONE || (K::M && closing_pending(h))) set_fail(L, FB_SLOT_IN_USE);
     else if (ref >= P.n_procs) set_fail(L, FB_BAD_PROCESS);
     L.proc = ref;
     L.next_ord = 0;
@@ -2503,7 +2507,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     if (!bad_cmd && !slot_kind) {
       if (kind == ZBHIP_CMD_CREATE) {
         L.pik = ref_cmd(ci, false, 0);
-      } else if (L.proc != NONE || ((h.y >> 25) & 1)) {  // (an ended instance: its closing subscription)
+      } else if (L.proc != NONE || closing_pending(h)) {  // (an ended instance: its closing subscription)
         const uint4 pm = P.st.pms[inst];
         L.pm_x = pm.x;
         L.pm_y = pm.y;
