@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 closing evidence: the message boundary tests first (fail fast), the whole GPU suite, the
+# default bench line with a rocprofv3 kernel trace, and the config-5 P=8 bench line.
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=${OUT:-gpurun_out/final}
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 600 python -u -m pytest tests/test_gpu_message_boundary.py tests/test_gpu_psm_messages.py -x -v -m gpu \
+  --timeout 200 --timeout-method thread > $O/pytest_boundary.log 2>&1 || { grep -E "FAILED|Error" $O/pytest_boundary.log | head -20; tail -40 $O/pytest_boundary.log; exit 1; }
+tail -1 $O/pytest_boundary.log
+if [ -z "$NOSUITE" ]; then
+  timeout -k 10 1000 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error" $O/pytest_gpu.log | head -20; tail -30 $O/pytest_gpu.log; exit 1; }
+  tail -1 $O/pytest_gpu.log
+fi
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench.json'));print('bench', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+grep -h '"zb::k_step' $(find $O/prof -name '*kernel_stats.csv' | head -1) | cut -d, -f1-4
+timeout -k 10 300 python -u bench.py --config msg --virtual-partitions 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_msg8.json 2> $O/bench_msg8.err || { tail -20 $O/bench_msg8.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench_msg8.json'));print('msg8', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'], 'ms/step %.2f'%d['ms_per_step'])"
+echo "=== done"
