@@ -7,7 +7,7 @@ O=${OUT:-gpurun_out/final}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 600 python -u -m pytest tests/test_gpu_message_boundary.py tests/test_gpu_psm_messages.py -x -v -m gpu \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_message_boundary.py tests/test_gpu_psm_messages.py tests/test_gpu_boundary.py tests/test_gpu_timers.py -x -v -m gpu \
   --timeout 200 --timeout-method thread > $O/pytest_boundary.log 2>&1 || { grep -E "FAILED|Error" $O/pytest_boundary.log | head -20; tail -40 $O/pytest_boundary.log; exit 1; }
 tail -1 $O/pytest_boundary.log
 if [ -z "$NOSUITE" ]; then
@@ -20,4 +20,10 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 grep -h '"zb::k_step' $(find $O/prof -name '*kernel_stats.csv' | head -1) | cut -d, -f1-4
 timeout -k 10 300 python -u bench.py --config msg --virtual-partitions 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_msg8.json 2> $O/bench_msg8.err || { tail -20 $O/bench_msg8.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench_msg8.json'));print('msg8', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'], 'ms/step %.2f'%d['ms_per_step'])"
+for v in fast general; do
+  if [ $v = general ]; then export ZBHIP_NO_FAST_SCOPE=1; fi
+  timeout -k 10 300 python -u bench.py --config boundary10 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_boundary10_$v.json 2> $O/bench_boundary10_$v.err || { tail -20 $O/bench_boundary10_$v.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bench_boundary10_$v.json'));print('boundary10 $v', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+done
+unset ZBHIP_NO_FAST_SCOPE
 echo "=== done"

@@ -1915,6 +1915,9 @@ __device__ __forceinline__ void note_activation(const Lane<K>& L, uint32_t job_o
 // emits, written here with static stage rows and no FIFO, element table or guard dispatch.  Any
 // other state, a variable document, a tight batch limit or record capacity takes the general path.
 constexpr uint32_t SEG_VALID = 1u << 31, SEG_FROM_TASK = 1u << 30, SEG_TO_END = 1u << 24;
+// a segment whose task carries a timer boundary event (source: canceled on completion) or whose next
+// task does (target: created on activation) -- KScope's segments only (fast_scope_job)
+constexpr uint32_t SEG_SRC_TIMER = 1u << 25, SEG_DST_TIMER = 1u << 26;
 
 template <class K>
 __device__ __forceinline__ void put(Lane<K>& L, int j, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem) {
@@ -1945,7 +1948,7 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
       return false;
     const uint32_t te = e.x & 0xFFFF, tk = e.x >> 16;
     const uint32_t sg = seg[te];
-    if ((sg & (SEG_VALID | SEG_FROM_TASK)) != (SEG_VALID | SEG_FROM_TASK)) return false;
+    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_SRC_TIMER | SEG_DST_TIMER)) != (SEG_VALID | SEG_FROM_TASK)) return false;
     const uint32_t k = L.next_ord, n = (sg >> 12) & 0xFFF;
     // JobCompleteProcessor + EventTriggerBehavior.triggeringProcessEvent, then COMPLETE_ELEMENT(task)
     put(L, 0, C_JOB_COMPLETED | (((e.y >> 25) & 1u) << 8), ref, tk, te);  // (flag 1: an ACTIVATED job)
@@ -1985,7 +1988,7 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
     const uint32_t start = L.pb[0] >> 16;
     if (start == NONE) return false;
     const uint32_t sg = seg[start];
-    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END)) != SEG_VALID) return false;
+    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END | SEG_DST_TIMER)) != SEG_VALID) return false;
     const uint32_t n = (sg >> 12) & 0xFFF;
     put(L, 0, ZBHIP_PI_ACTIVATE_ELEMENT, 0, NONE, 0);
     put(L, 1, C_PIC_CREATED, 1, 0, 0);
@@ -2012,6 +2015,85 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
     return true;
   }
   return false;
+}
+
+// ---- straight-line JOB:COMPLETE batches of KScope ---------------------------------------------
+// The same segments for processes with timers (KScope: boundary10 and the like): a task at the
+// process level completing into the next task or a none end event, either task with a timer boundary
+// event.  From the canonical waiting state (the process ACTIVATED with that task as its only child,
+// the job unclaimed by a pending trigger, the instance's timer row the task's own or free) the batch
+// is the general path's exact sequence -- JOB:COMPLETED, PROCESS_EVENT:TRIGGERING, COMPLETE_ELEMENT,
+// COMPLETING, [TIMER:CANCELED], COMPLETED, SEQUENCE_FLOW_TAKEN, ACTIVATE_ELEMENT, ACTIVATING,
+// [TIMER:CREATED], JOB:CREATED, ACTIVATED (or the end event's and the process's completion) -- written
+// without the FIFO, guard dispatch or table search; the appliers' effects on the element table, the
+// process scope's counters and the timer row are set directly.  Anything else: the general path.
+template <class K>
+__device__ __forceinline__ bool fast_scope_job(Lane<K>& L, uint32_t ref, uint32_t doc_count) {
+  if (L.fail || L.proc == NONE || doc_count != 0 || L.limit <= 4 || L.rec_cap < 16 || L.next_ord >= 0xFFE0)
+    return false;
+  if (!(L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED && L.nt == 1 && L.pi_child == 1 && L.pi_asf == 0 &&
+        L.trig_key == NONE))
+    return false;
+  const uint2 e = tget(L, 0);
+  if (e.x == 0xFFFFFFFFu || (e.y & 0xFFFF) != ref || !((e.y >> 24) & 1u) || ((e.y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED)
+    return false;
+  const uint32_t te = e.x & 0xFFFF, tk = e.x >> 16;
+  const uint32_t sg = L.pb[(L.pb[6] & 0xFFFF) + te];
+  if ((sg & (SEG_VALID | SEG_FROM_TASK)) != (SEG_VALID | SEG_FROM_TASK)) return false;
+  const bool src_tmr = sg & SEG_SRC_TIMER, dst_tmr = sg & SEG_DST_TIMER;
+  const bool live_tmr = L.has_tmr && (L.tm_y >> 31);
+  if ((src_tmr || dst_tmr) && !L.has_tmr) return false;
+  if (src_tmr ? !(live_tmr && (L.tm_y & 0xFFFF) == tk) : live_tmr) return false;
+  const uint32_t n = (sg >> 12) & 0xFFF, f = sg & 0xFFF;
+  // JobCompleteProcessor: JOB:COMPLETED (the job row deleted), triggeringProcessEvent, COMPLETE_ELEMENT
+  emit(L, C_JOB_COMPLETED, ref, tk, te, (e.y >> 25) & 1u);  // (flag 1: an ACTIVATED job)
+  if ((e.y >> 25) & 1u) note_activation(L, ref, L.inst);
+  const uint32_t pe = new_key(L);
+  emit(L, C_PE_TRIGGERING, pe, tk, te);
+  emit(L, ZBHIP_PI_COMPLETE_ELEMENT, tk, 0, te);
+  // JobWorkerTaskProcessor.onComplete: COMPLETING, unsubscribeFromEvents (the boundary timer),
+  // COMPLETED (the instance and its trigger removed), the one outgoing flow
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, tk, 0, te);
+  if (src_tmr) cancel_timer(L);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, tk, 0, te);
+  const uint32_t sft = new_key(L);
+  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, f);
+  const uint32_t nk = new_key(L);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, nk, 0, n);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, nk, 0, n);
+  if (!(sg & SEG_TO_END)) {
+    // JobWorkerTaskProcessor.onActivate: the boundary event's timer, the job, ACTIVATED
+    if (dst_tmr) {
+      const uint32_t b = elem_of(L, n).w & 0xFFFF;
+      const uint4 bw = elem_of(L, b);
+      const uint32_t reps = (bw.w >> 8) & 0xFF;
+      const uint32_t tmk = new_key(L);
+      L.tm_x = b | (tmk << 16);
+      L.tm_y = nk | (reps << 16) | (1u << 31);
+      L.tm_due = L.sp->now_ms + (long long)bw.z;
+      emit(L, C_TIMER_CREATED, tmk, nk, b, reps);
+    }
+    const uint32_t job = new_key(L);
+    emit(L, C_JOB_CREATED, job, nk, n);
+    emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, nk, 0, n);
+    tput(L, 0, make_uint2(n | (nk << 16), (job & 0xFFFF) | ((uint32_t)ZBHIP_PI_ELEMENT_ACTIVATED << 16) | (1u << 24)));
+  } else {
+    // NoneEndEventBehavior, the end of the path -> ProcessProcessor.onComplete
+    emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, nk, 0, n);
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETING, nk, 0, n);
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETED, nk, 0, n);
+    emit(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0);
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETING, 0, NONE, 0);
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETED, 0, NONE, 0);
+    tput(L, 0, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+    L.pi_child = 0;
+    L.pi_live = false;
+    L.pi_state = ZBHIP_PI_ELEMENT_COMPLETING;
+    L.nvars = 0;
+    L.jw0 = L.jw1 = L.jw2 = L.jw3 = 0;
+    ++L.completed;
+  }
+  return !L.fail;
 }
 
 // ---- CREATE batch templates (non-register variants) -------------------------------------------
@@ -2545,6 +2627,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   // the FIFO; anything outside the canonical states takes the general path below
   bool fast = false;
   if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
+  if constexpr (K::S && !K::IO) {
+    if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_scope_job(L, ref, doc_count);
+  }
   int tpl_v = -1;
   uint32_t tpl_name = 0xFFFF;
   bool tpl_hit = false;

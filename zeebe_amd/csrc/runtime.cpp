@@ -1097,18 +1097,28 @@ static int rebuild_program(zbhip_handle* h) {
     for (uint32_t e = 0; e < n_el; ++e) {
       const zbhip_element& E = P.els[e];
       uint32_t sg = 0;
+      // (bits 25 / 26: the task / the next task carries a timer boundary event -- KScope's
+      // fast_scope_job; KLinear never holds such processes, its fast_command refuses the bits)
+      auto timer_boundary = [&](const zbhip_element& T) {
+        return T.start_event != ZBHIP_NONE16 && T.start_event < n_el &&
+               P.els[T.start_event].element_type == ZBHIP_EL_BOUNDARY_EVENT && P.els[T.start_event].event_type == ZBHIP_EV_TIMER;
+      };
+      const bool src_tmr = ZBHIP_IS_JOB_WORKER(E.element_type) && timer_boundary(E);
       if ((E.element_type == ZBHIP_EL_START_EVENT || ZBHIP_IS_JOB_WORKER(E.element_type)) && E.out_count == 1 &&
-          E.flow_scope == 0 && !(ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) && !P.io_of(e)) {
+          E.flow_scope == 0 && !(ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16 && !src_tmr) &&
+          !P.io_of(e) && !P.mi_inner(e)) {
         const uint32_t f = P.out[E.out_begin];
         const zbhip_element& F = P.els[f];
         const uint32_t n = F.flow_target;
         if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.condition == ZBHIP_NONE16 && n < n_el && f < 0xFFF && n < 0xFFF) {
           const zbhip_element& N = P.els[n];
-          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && N.start_event == ZBHIP_NONE16 && !P.io_of(n);
+          const bool dst_tmr = ZBHIP_IS_JOB_WORKER(N.element_type) && timer_boundary(N);
+          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && (N.start_event == ZBHIP_NONE16 || dst_tmr) &&
+                            !P.io_of(n) && !P.mi_inner(n);
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
           if (task || end)
             sg = (1u << 31) | (ZBHIP_IS_JOB_WORKER(E.element_type) ? 1u << 30 : 0u) | (end ? 1u << 24 : 0u) |
-                 (n << 12) | f;
+                 (src_tmr ? 1u << 25 : 0u) | (dst_tmr ? 1u << 26 : 0u) | (n << 12) | f;
         }
       }
       pb[seg_off + e] = sg;
@@ -2217,6 +2227,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
   P.stamp = h->window_stamp;
   P.now_ms = h->clock_ms;
+  P.no_fast_scope = getenv("ZBHIP_NO_FAST_SCOPE") ? 1u : 0u;
   P.cmd_due = h->d_cmd_due;
   P.map_val = h->d_map_val;
   P.map_cap = h->cfg.max_commands;

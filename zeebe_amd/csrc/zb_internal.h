@@ -269,6 +269,7 @@ struct StepParams {
   // number (a template recorded in the running launch is not used before the next one)
   uint2* tpl;
   uint32_t launch_seq;
+  uint32_t no_fast_scope;     // ZBHIP_NO_FAST_SCOPE: KScope's straight-line JOB:COMPLETE batches off (A/B)
   long long now_ms;           // zbhip_set_clock: ActorClock.currentTimeMillis() of this window
   long long* cmd_due;         // [n_cmds] (KScope) dueDate of the timer a batch canceled (at most one)
   long long* map_val;         // [kMapVals][map_cap] (KScope) values of the variables a batch's io mappings
