@@ -20,10 +20,13 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 grep -h '"zb::k_step' $(find $O/prof -name '*kernel_stats.csv' | head -1) | cut -d, -f1-4
 timeout -k 10 300 python -u bench.py --config msg --virtual-partitions 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_msg8.json 2> $O/bench_msg8.err || { tail -20 $O/bench_msg8.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench_msg8.json'));print('msg8', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'], 'ms/step %.2f'%d['ms_per_step'])"
-for v in fast general; do
+# boundary10 A/B: the straight-line KScope batches, the same build with them off, and the build before
+# them (zeebe_amd/libzbhip_prev.so, if present: KScope's register allocation without the new paths)
+for v in fast general prev; do
   if [ $v = general ]; then export ZBHIP_NO_FAST_SCOPE=1; fi
+  if [ $v = prev ]; then unset ZBHIP_NO_FAST_SCOPE; [ -f zeebe_amd/libzbhip_prev.so ] || continue; export ZBHIP_LIB=$PWD/zeebe_amd/libzbhip_prev.so; fi
   timeout -k 10 300 python -u bench.py --config boundary10 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_boundary10_$v.json 2> $O/bench_boundary10_$v.err || { tail -20 $O/bench_boundary10_$v.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/bench_boundary10_$v.json'));print('boundary10 $v', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
 done
-unset ZBHIP_NO_FAST_SCOPE
+unset ZBHIP_NO_FAST_SCOPE ZBHIP_LIB
 echo "=== done"

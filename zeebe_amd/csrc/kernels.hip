@@ -2096,6 +2096,60 @@ __device__ __forceinline__ bool fast_scope_job(Lane<K>& L, uint32_t ref, uint32_
   return !L.fail;
 }
 
+// A CREATE whose none start event leads into a task (with or without a timer boundary event):
+// CreateProcessInstanceProcessor, ProcessProcessor, StartEventProcessor and the task's activation in
+// the general path's order; no variables (a document takes the general path).
+template <class K>
+__device__ __forceinline__ bool fast_scope_create(Lane<K>& L, uint32_t doc_count) {
+  if (L.fail || L.proc == NONE || doc_count != 0 || L.limit <= 4 || L.rec_cap < 18 || L.pi_live || L.nt != 0)
+    return false;
+  const uint32_t start = L.pb[0] >> 16;
+  if (start == NONE) return false;
+  const uint32_t sg = L.pb[(L.pb[6] & 0xFFFF) + start];
+  if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END)) != SEG_VALID) return false;
+  const bool dst_tmr = sg & SEG_DST_TIMER;
+  if (dst_tmr && !L.has_tmr) return false;
+  const uint32_t n = (sg >> 12) & 0xFFF, f = sg & 0xFFF;
+  const uint32_t pi = new_key(L);  // 0
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0);
+  const uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
+  emit(L, C_PIC_CREATED, created, pi, 0);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, pi, NONE, 0);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, pi, NONE, 0);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, NONE, 0, start);  // activateChildInstance: key -1
+  const uint32_t sk = new_key(L);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, sk, 0, start);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, sk, 0, start);
+  emit(L, ZBHIP_PI_COMPLETE_ELEMENT, sk, 0, start);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, sk, 0, start);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, sk, 0, start);
+  const uint32_t sft = new_key(L);
+  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, f);
+  const uint32_t nk = new_key(L);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, nk, 0, n);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, nk, 0, n);
+  if (dst_tmr) {
+    const uint32_t b = elem_of(L, n).w & 0xFFFF;
+    const uint4 bw = elem_of(L, b);
+    const uint32_t reps = (bw.w >> 8) & 0xFF;
+    const uint32_t tmk = new_key(L);
+    L.tm_x = b | (tmk << 16);
+    L.tm_y = nk | (reps << 16) | (1u << 31);
+    L.tm_due = L.sp->now_ms + (long long)bw.z;
+    emit(L, C_TIMER_CREATED, tmk, nk, b, reps);
+  }
+  const uint32_t job = new_key(L);
+  emit(L, C_JOB_CREATED, job, nk, n);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, nk, 0, n);
+  L.nt = 1;
+  tput(L, 0, make_uint2(n | (nk << 16), (job & 0xFFFF) | ((uint32_t)ZBHIP_PI_ELEMENT_ACTIVATED << 16) | (1u << 24)));
+  L.pi_live = true;
+  L.pi_state = ZBHIP_PI_ELEMENT_ACTIVATED;
+  L.pi_child = 1;
+  L.pi_asf = 0;
+  return !L.fail;
+}
+
 // ---- CREATE batch templates (non-register variants) -------------------------------------------
 // A process whose CREATE batch never waits (runtime.cpp create_template_word: every element
 // reachable from the none start event is an event without wait state, a flow or a gateway; at most
@@ -2629,12 +2683,13 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
   if constexpr (K::S && !K::IO) {
     if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_scope_job(L, ref, doc_count);
+    else if (kind == ZBHIP_CMD_CREATE && !P.no_fast_scope) fast = fast_scope_create(L, doc_count);
   }
   int tpl_v = -1;
   uint32_t tpl_name = 0xFFFF;
   bool tpl_hit = false;
   if constexpr (!K::REG && !K::M) {
-    if (P.tpl && !L.fail && kind == ZBHIP_CMD_CREATE && L.proc != NONE) {
+    if (P.tpl && !fast && !L.fail && kind == ZBHIP_CMD_CREATE && L.proc != NONE) {
       tpl_v = tpl_create(L, doc_count, doc_begin, tpl_name, tpl_lds);
       if (tpl_v == kTplReplayed) {
         fast = true;
