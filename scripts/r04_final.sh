@@ -20,13 +20,17 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 grep -h '"zb::k_step' $(find $O/prof -name '*kernel_stats.csv' | head -1) | cut -d, -f1-4
 timeout -k 10 300 python -u bench.py --config msg --virtual-partitions 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_msg8.json 2> $O/bench_msg8.err || { tail -20 $O/bench_msg8.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench_msg8.json'));print('msg8', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'], 'ms/step %.2f'%d['ms_per_step'])"
-# boundary10 A/B: the straight-line KScope batches, the same build with them off, and the build before
-# them (zeebe_amd/libzbhip_prev.so, if present: KScope's register allocation without the new paths)
-for v in fast general prev; do
-  if [ $v = general ]; then export ZBHIP_NO_FAST_SCOPE=1; fi
-  if [ $v = prev ]; then unset ZBHIP_NO_FAST_SCOPE; [ -f zeebe_amd/libzbhip_prev.so ] || continue; export ZBHIP_LIB=$PWD/zeebe_amd/libzbhip_prev.so; fi
-  timeout -k 10 300 python -u bench.py --config boundary10 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_boundary10_$v.json 2> $O/bench_boundary10_$v.err || { tail -20 $O/bench_boundary10_$v.err; exit 1; }
-  python3 -c "import json;d=json.load(open('$O/bench_boundary10_$v.json'));print('boundary10 $v', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+# straight-line A/B (boundary10: KScope, forkjoin8_tasks: KGeneric's joins; forkjoin8: KGeneric's
+# register budget): the product, the same build with them off, and the build before them
+# (zeebe_amd/libzbhip_prev.so, if present)
+for cfg in boundary10 forkjoin8_tasks forkjoin8; do
+  for v in fast general prev; do
+    unset ZBHIP_NO_FAST_SCOPE ZBHIP_LIB
+    if [ $v = general ]; then [ $cfg = forkjoin8 ] && continue; export ZBHIP_NO_FAST_SCOPE=1; fi
+    if [ $v = prev ]; then [ -f zeebe_amd/libzbhip_prev.so ] || continue; export ZBHIP_LIB=$PWD/zeebe_amd/libzbhip_prev.so; fi
+    timeout -k 10 300 python -u bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_${cfg}_$v.json 2> $O/bench_${cfg}_$v.err || { tail -20 $O/bench_${cfg}_$v.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/bench_${cfg}_$v.json'));print('$cfg $v', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+  done
 done
 unset ZBHIP_NO_FAST_SCOPE ZBHIP_LIB
 echo "=== done"

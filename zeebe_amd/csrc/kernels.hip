@@ -1918,6 +1918,9 @@ constexpr uint32_t SEG_VALID = 1u << 31, SEG_FROM_TASK = 1u << 30, SEG_TO_END = 
 // a segment whose task carries a timer boundary event (source: canceled on completion) or whose next
 // task does (target: created on activation) -- KScope's segments only (fast_scope_job)
 constexpr uint32_t SEG_SRC_TIMER = 1u << 25, SEG_DST_TIMER = 1u << 26;
+// a task into a joining parallel gateway, and such a gateway's own word (its one flow onwards): the
+// joins of KGeneric (fast_join_job)
+constexpr uint32_t SEG_TO_JOIN = 1u << 27, SEG_FROM_GW = 1u << 28;
 
 template <class K>
 __device__ __forceinline__ void put(Lane<K>& L, int j, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem) {
@@ -1948,7 +1951,7 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
       return false;
     const uint32_t te = e.x & 0xFFFF, tk = e.x >> 16;
     const uint32_t sg = seg[te];
-    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_SRC_TIMER | SEG_DST_TIMER)) != (SEG_VALID | SEG_FROM_TASK)) return false;
+    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_SRC_TIMER | SEG_DST_TIMER | SEG_TO_JOIN)) != (SEG_VALID | SEG_FROM_TASK)) return false;
     const uint32_t k = L.next_ord, n = (sg >> 12) & 0xFFF;
     // JobCompleteProcessor + EventTriggerBehavior.triggeringProcessEvent, then COMPLETE_ELEMENT(task)
     put(L, 0, C_JOB_COMPLETED | (((e.y >> 25) & 1u) << 8), ref, tk, te);  // (flag 1: an ACTIVATED job)
@@ -2039,7 +2042,7 @@ __device__ __forceinline__ bool fast_scope_job(Lane<K>& L, uint32_t ref, uint32_
     return false;
   const uint32_t te = e.x & 0xFFFF, tk = e.x >> 16;
   const uint32_t sg = L.pb[(L.pb[6] & 0xFFFF) + te];
-  if ((sg & (SEG_VALID | SEG_FROM_TASK)) != (SEG_VALID | SEG_FROM_TASK)) return false;
+  if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_JOIN)) != (SEG_VALID | SEG_FROM_TASK)) return false;
   const bool src_tmr = sg & SEG_SRC_TIMER, dst_tmr = sg & SEG_DST_TIMER;
   const bool live_tmr = L.has_tmr && (L.tm_y >> 31);
   if ((src_tmr || dst_tmr) && !L.has_tmr) return false;
@@ -2087,6 +2090,103 @@ __device__ __forceinline__ bool fast_scope_job(Lane<K>& L, uint32_t ref, uint32_
     emit(L, ZBHIP_PI_ELEMENT_COMPLETED, 0, NONE, 0);
     tput(L, 0, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
     L.pi_child = 0;
+    L.pi_live = false;
+    L.pi_state = ZBHIP_PI_ELEMENT_COMPLETING;
+    L.nvars = 0;
+    L.jw0 = L.jw1 = L.jw2 = L.jw3 = 0;
+    ++L.completed;
+  }
+  return !L.fail;
+}
+
+// ---- straight-line JOB:COMPLETE batches into a join (KGeneric) -------------------------------
+// A branch task completing into a joining parallel gateway (fork/join with a task per branch): the
+// general path's records -- JOB:COMPLETED, PROCESS_EVENT:TRIGGERING, COMPLETE_ELEMENT, COMPLETING,
+// COMPLETED, SEQUENCE_FLOW_TAKEN (the join counter), ACTIVATE_ELEMENT of the gateway, then either its
+// rejection (ProcessInstanceStateTransitionGuard.canActivateParallelGateway: not all flows taken) or
+// its activation (the counters' Tetris decrement), completion and the one flow onwards into a task or a
+// none end event (the process completed when nothing else is active) -- with the appliers' effects set
+// directly: no FIFO, guard dispatch or element lookups beyond the segment words.
+template <class K>
+__device__ __forceinline__ bool fast_join_job(Lane<K>& L, uint32_t ref, uint32_t doc_count) {
+  if (L.fail || L.proc == NONE || doc_count != 0 || L.limit <= 6 || L.rec_cap < 24 || L.next_ord >= 0xFFE0 ||
+      !L.has_join)
+    return false;
+  if (!(L.pi_live && L.pi_state == ZBHIP_PI_ELEMENT_ACTIVATED && L.trig_key == NONE)) return false;
+  const int t = tbl_find_job(L, ref);
+  if (t < 0) return false;
+  const uint2 e = tget(L, t);
+  if (((e.y >> 16) & 0xFF) != ZBHIP_PI_ELEMENT_ACTIVATED) return false;
+  const uint32_t te = e.x & 0xFFFF, tk = e.x >> 16;
+  const uint32_t* seg = L.pb + (L.pb[6] & 0xFFFF);
+  const uint32_t sg = seg[te];
+  if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_JOIN)) != (SEG_VALID | SEG_FROM_TASK | SEG_TO_JOIN)) return false;
+  const uint32_t g = (sg >> 12) & 0xFFF, f = sg & 0xFFF;
+  const uint32_t sg2 = seg[g];
+  if ((sg2 & (SEG_VALID | SEG_FROM_GW)) != (SEG_VALID | SEG_FROM_GW)) return false;
+  // JobCompleteProcessor, triggeringProcessEvent, COMPLETE_ELEMENT of the task and its completion
+  emit(L, C_JOB_COMPLETED, ref, tk, te, (e.y >> 25) & 1u);  // (flag 1: an ACTIVATED job)
+  if ((e.y >> 25) & 1u) note_activation(L, ref, L.inst);
+  const uint32_t pe = new_key(L);
+  emit(L, C_PE_TRIGGERING, pe, tk, te);
+  emit(L, ZBHIP_PI_COMPLETE_ELEMENT, tk, 0, te);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, tk, 0, te);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, tk, 0, te);
+  tput(L, t, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+  --L.pi_child;
+  // takeSequenceFlow into the gateway: the taken-flow counter, then ACTIVATE_ELEMENT
+  const uint32_t sft = new_key(L);
+  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, f);
+  ++L.pi_asf;
+  const uint4 fw = elem_of(L, f);
+  const uint32_t js = fw.w & 0xFFFF, jc = join_get(L, js);
+  if (jc >= 255) set_fail(L, FB_JOIN);
+  join_set(L, js, jc + 1);
+  const uint32_t gk = new_key(L);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, gk, 0, g);
+  const uint4 gw = elem_of(L, g);
+  const uint32_t base = gw.w & 0xFFFF, nin = gw.x >> 16;
+  uint32_t taken = 0;
+  for (uint32_t s = base; s < base + nin; ++s) taken += join_get(L, s) > 0;
+  if (taken < nin) {  // canActivateParallelGateway: the command is rejected
+    emit(L, kRejectBit | ZBHIP_PI_ACTIVATE_ELEMENT, gk, 0, g, ZBHIP_REASON_PGW_NOT_ALL_TAKEN);
+    return !L.fail;
+  }
+  // ACTIVATING (cleanupSequenceFlowsTaken, the activation's counters), ACTIVATED, COMPLETING, COMPLETED
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, gk, 0, g);
+  for (uint32_t s = base; s < base + nin; ++s) {
+    const uint32_t c = join_get(L, s);
+    if (c > 0) join_set(L, s, c - 1);
+  }
+  L.pi_asf = L.pi_asf > (int)nin ? L.pi_asf - (int)nin : 0;
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, gk, 0, g);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, gk, 0, g);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, gk, 0, g);
+  // the gateway's one flow onwards
+  const uint32_t n = (sg2 >> 12) & 0xFFF, f2 = sg2 & 0xFFF;
+  const uint32_t sft2 = new_key(L);
+  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft2, 0, f2);
+  const uint32_t nk = new_key(L);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, nk, 0, n);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, nk, 0, n);  // (the flow's +1 and the activation's -1 cancel)
+  if (!(sg2 & SEG_TO_END)) {
+    const int tn = tbl_insert(L, n, nk, ZBHIP_PI_ELEMENT_ACTIVATING);
+    if (tn < 0) return false;
+    ++L.pi_child;
+    const uint32_t job = new_key(L);
+    emit(L, C_JOB_CREATED, job, nk, n);
+    tput(L, tn, make_uint2(n | (nk << 16), (job & 0xFFFF) | ((uint32_t)ZBHIP_PI_ELEMENT_ACTIVATED << 16) | (1u << 24)));
+    emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, nk, 0, n);
+    return !L.fail;
+  }
+  // NoneEndEventBehavior; the end of the path -> ProcessProcessor.onComplete once nothing is active
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, nk, 0, n);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, nk, 0, n);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, nk, 0, n);
+  if (L.pi_child + L.pi_asf == 0) {
+    emit(L, ZBHIP_PI_COMPLETE_ELEMENT, 0, NONE, 0);
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETING, 0, NONE, 0);
+    emit(L, ZBHIP_PI_ELEMENT_COMPLETED, 0, NONE, 0);
     L.pi_live = false;
     L.pi_state = ZBHIP_PI_ELEMENT_COMPLETING;
     L.nvars = 0;
@@ -2681,6 +2781,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   // the FIFO; anything outside the canonical states takes the general path below
   bool fast = false;
   if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
+  if constexpr (K::J && !K::S && !K::M && !K::REG) {
+    if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_join_job(L, ref, doc_count);
+  }
   if constexpr (K::S && !K::IO) {
     if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_scope_job(L, ref, doc_count);
     else if (kind == ZBHIP_CMD_CREATE && !P.no_fast_scope) fast = fast_scope_create(L, doc_count);

@@ -1116,9 +1116,25 @@ static int rebuild_program(zbhip_handle* h) {
           const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && (N.start_event == ZBHIP_NONE16 || dst_tmr) &&
                             !P.io_of(n) && !P.mi_inner(n);
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
-          if (task || end)
+          // bit 27: a task into a joining parallel gateway (KGeneric's fast_join_job)
+          const bool join = ZBHIP_IS_JOB_WORKER(E.element_type) && !src_tmr && N.element_type == ZBHIP_EL_PARALLEL_GATEWAY &&
+                            N.in_count >= 2 && N.out_count == 1 && N.flow_scope == 0;
+          if (task || end || join)
             sg = (1u << 31) | (ZBHIP_IS_JOB_WORKER(E.element_type) ? 1u << 30 : 0u) | (end ? 1u << 24 : 0u) |
-                 (src_tmr ? 1u << 25 : 0u) | (dst_tmr ? 1u << 26 : 0u) | (n << 12) | f;
+                 (src_tmr ? 1u << 25 : 0u) | (dst_tmr ? 1u << 26 : 0u) | (join ? 1u << 27 : 0u) | (n << 12) | f;
+        }
+      } else if (E.element_type == ZBHIP_EL_PARALLEL_GATEWAY && E.in_count >= 2 && E.out_count == 1 && E.flow_scope == 0) {
+        // bit 28: a joining gateway's one unconditional flow into a task (no boundary event) or a none
+        // end event (the continuation of fast_join_job)
+        const uint32_t f = P.out[E.out_begin];
+        const zbhip_element& F = P.els[f];
+        const uint32_t n = F.flow_target;
+        if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.condition == ZBHIP_NONE16 && n < n_el && f < 0xFFF && n < 0xFFF) {
+          const zbhip_element& N = P.els[n];
+          const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && N.start_event == ZBHIP_NONE16 && !P.io_of(n) &&
+                            !P.mi_inner(n);
+          const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
+          if (task || end) sg = (1u << 31) | (1u << 28) | (end ? 1u << 24 : 0u) | (n << 12) | f;
         }
       }
       pb[seg_off + e] = sg;
