@@ -7,7 +7,7 @@ O=${OUT:-gpurun_out/final}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 600 python -u -m pytest tests/test_gpu_message_boundary.py tests/test_gpu_psm_messages.py tests/test_gpu_boundary.py tests/test_gpu_timers.py -x -v -m gpu \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_message_boundary.py tests/test_gpu_psm_messages.py tests/test_gpu_boundary.py tests/test_gpu_timers.py tests/test_gpu_parity.py tests/test_gpu_random.py tests/test_gpu_batch_limit.py -x -v -m gpu \
   --timeout 200 --timeout-method thread > $O/pytest_boundary.log 2>&1 || { grep -E "FAILED|Error" $O/pytest_boundary.log | head -20; tail -40 $O/pytest_boundary.log; exit 1; }
 tail -1 $O/pytest_boundary.log
 if [ -z "$NOSUITE" ]; then
