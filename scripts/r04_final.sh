@@ -7,7 +7,7 @@ O=${OUT:-gpurun_out/final}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 600 python -u -m pytest tests/test_gpu_message_boundary.py tests/test_gpu_psm_messages.py tests/test_gpu_boundary.py tests/test_gpu_timers.py tests/test_gpu_parity.py tests/test_gpu_random.py tests/test_gpu_batch_limit.py -x -v -m gpu \
+ZBHIP_FAST_SCOPE=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_message_boundary.py tests/test_gpu_psm_messages.py tests/test_gpu_boundary.py tests/test_gpu_timers.py tests/test_gpu_parity.py tests/test_gpu_random.py tests/test_gpu_batch_limit.py -x -v -m gpu \
   --timeout 200 --timeout-method thread > $O/pytest_boundary.log 2>&1 || { grep -E "FAILED|Error" $O/pytest_boundary.log | head -20; tail -40 $O/pytest_boundary.log; exit 1; }
 tail -1 $O/pytest_boundary.log
 if [ -z "$NOSUITE" ]; then
@@ -25,12 +25,13 @@ python3 -c "import json;d=json.load(open('$O/bench_msg8.json'));print('msg8', '%
 # (zeebe_amd/libzbhip_prev.so, if present)
 for cfg in boundary10 forkjoin8_tasks forkjoin8; do
   for v in fast general prev; do
-    unset ZBHIP_NO_FAST_SCOPE ZBHIP_LIB
-    if [ $v = general ]; then [ $cfg = forkjoin8 ] && continue; export ZBHIP_NO_FAST_SCOPE=1; fi
+    unset ZBHIP_FAST_SCOPE ZBHIP_LIB
+    if [ $v = fast ]; then export ZBHIP_FAST_SCOPE=1; fi
+    if [ $v = general ]; then [ $cfg = forkjoin8 ] && continue; fi
     if [ $v = prev ]; then [ -f zeebe_amd/libzbhip_prev.so ] || continue; export ZBHIP_LIB=$PWD/zeebe_amd/libzbhip_prev.so; fi
     timeout -k 10 300 python -u bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_${cfg}_$v.json 2> $O/bench_${cfg}_$v.err || { tail -20 $O/bench_${cfg}_$v.err; exit 1; }
     python3 -c "import json;d=json.load(open('$O/bench_${cfg}_$v.json'));print('$cfg $v', '%.4e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
   done
 done
-unset ZBHIP_NO_FAST_SCOPE ZBHIP_LIB
+unset ZBHIP_FAST_SCOPE ZBHIP_LIB
 echo "=== done"
