@@ -2140,7 +2140,7 @@ class Oracle {
     int64_t eventKey = next_key();
     ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
     pe.r.process_idx = inst.value.proc;
-    pe.r.element_idx = inst.value.elem;
+    pe.r.element_idx = m.elem;  // ProcessEventRecord.targetElementId: the catch event (a boundary event's own id)
     pe.r.scope_key = c.eik;
     pe.r.process_instance_key = inst.value.piKey;
     if (P(m.proc).els[m.elem].type == ZBHIP_EL_BOUNDARY_EVENT) {

@@ -1174,6 +1174,9 @@ __device__ __forceinline__ void pms_create(Lane<K>& L, uint32_t eord, uint32_t n
     emit_msg(L, C_PMS_CREATED, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, L.pm_z, L.pm_w, L.pm_x >> 16,
              (L.pm_x >> 14) & 1, pm_elem);
     L.pm_x = (L.pm_x & ~(3u << 12)) | (2u << 12);  // ProcessMessageSubscriptionCreatedApplier: OPENED
+    // the acknowledgement of another partition carries the real element-instance key: kept for the
+    // MESSAGE_SUBSCRIPTION:DELETE of a later window (the instance's keys are references in this one)
+    if ((int32_t)part != L.sp->partition_id && L.inst < L.sp->st.n) L.sp->st.pms_eik[L.inst] = eik_p;
     return;
   }
   emit_msg(L, kRejectBit | C_PMS_CREATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, name | 0xFFFF0000u, part, intr,
@@ -1258,7 +1261,7 @@ __device__ __forceinline__ void ms_correlate(Lane<K>& L, uint32_t slot, uint32_t
 // (SubscriptionCommandSender.closeMessageSubscription, :220-236: pik, eik, messageKey -1, name)
 template <class K>
 __device__ __forceinline__ void unsubscribe_message(Lane<K>& L) {
-  const uint32_t eord = L.pm_y & 0xFFFF, part = L.pm_x >> 16, corr = L.pm_z, nb = L.pm_w;
+  const uint32_t eord = L.pm_y & 0xFFFF, part = L.pm_x >> 16, corr = L.pm_z, nb = L.pm_w, st0 = (L.pm_x >> 12) & 3;
   emit_msg(L, C_PMS_DELETING, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, corr, nb, part,
            (L.pm_x >> 14) & 1, L.pm_x & 0xFFF);
   L.pm_x |= 3u << 12;
@@ -1272,7 +1275,11 @@ __device__ __forceinline__ void unsubscribe_message(Lane<K>& L) {
     L.lq_pik = L.pik;
     push_local(L, LQ_MS_DELETE);
   } else {
-    send_xpart(L, ZBHIP_CMD_MSG_SUB_DELETE, part, cref_inst(L, eord), L.pik, -1, corr, L.inst, eord, name_only, 1);
+    // the real key the acknowledgement brought (an OPENING subscription -- the job completed before the
+    // acknowledgement arrived -- has none here: outside the subset)
+    const long long eik = L.inst < L.sp->st.n ? L.sp->st.pms_eik[L.inst] : -1;
+    if (eik < 0 || st0 != 2) { set_fail(L, FB_MESSAGE); return; }
+    send_xpart(L, ZBHIP_CMD_MSG_SUB_DELETE, part, eik, L.pik, -1, corr, L.inst, eord, name_only, 1);
   }
 }
 

@@ -816,6 +816,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   h->st.n_slots = (uint32_t)S;
   if (S) {
     ok = ok && dalloc(&h->st.pms, N) == hipSuccess && dalloc(&h->st.pi_key, N) == hipSuccess &&
+         dalloc(&h->st.pms_eik, N) == hipSuccess &&
          dalloc(&h->st.slot_hdr, S) == hipSuccess && dalloc(&h->st.sub_a, S * kSubs) == hipSuccess &&
          dalloc(&h->st.sub_b, S * kSubs) == hipSuccess && dalloc(&h->st.sub_k, S * kSubs) == hipSuccess;
   }
@@ -838,6 +839,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
     const unsigned long long kc = (unsigned long long)cfg->initial_key;
     if (hipMemsetAsync(h->st.pms, 0, N * sizeof(uint4), h->stream) != hipSuccess ||
         hipMemsetAsync(h->st.pi_key, 0xFF, N * sizeof(long long), h->stream) != hipSuccess ||
+        hipMemsetAsync(h->st.pms_eik, 0xFF, N * sizeof(long long), h->stream) != hipSuccess ||
         hipMemsetAsync(h->st.slot_hdr, 0, S * sizeof(uint2), h->stream) != hipSuccess ||
         hipMemsetAsync(h->st.sub_a, 0, S * kSubs * sizeof(uint4), h->stream) != hipSuccess ||
         hipMemcpyAsync(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice, h->stream) != hipSuccess) {
@@ -883,6 +885,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_region_off);
   (void)hipFree(h->d_stats);
   (void)hipFree(h->st.pms);
+  (void)hipFree(h->st.pms_eik);
   (void)hipFree(h->st.tmr);
   (void)hipFree(h->st.act);
   (void)hipFree(h->d_cmd_act);
@@ -3745,6 +3748,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   std::vector<long long> vv(N * kVars);
   std::vector<uint32_t> join(N * kJoinWords);
   std::vector<uint4> pmsrow(h->st.n_slots ? N : 0);
+  std::vector<long long> pmseik(h->st.n_slots ? N : 0, -1);
   std::vector<long long> pikrow(h->st.n_slots ? N : 0);
   std::vector<uint4> tmrrow(N);
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -3756,6 +3760,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   HIPCHK(hipMemcpy(tmrrow.data(), h->st.tmr, N * sizeof(uint4), hipMemcpyDeviceToHost));
   if (h->st.n_slots) {
     HIPCHK(hipMemcpy(pmsrow.data(), h->st.pms, N * sizeof(uint4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pmseik.data(), h->st.pms_eik, N * sizeof(long long), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(pikrow.data(), h->st.pi_key, N * sizeof(long long), hipMemcpyDeviceToHost));
   }
   const int64_t pbits = (int64_t)h->cfg.partition_id << 51;
@@ -3919,6 +3924,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     }
     if (h->st.n_slots) {
       pmsrow[inst] = make_uint4(0, 0, 0, 0);
+      pmseik[inst] = -1;
       pikrow[inst] = pe.key;
       if (sub) {
         const int el = elem_of_id(sub->elem_id);
@@ -3927,6 +3933,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
         if (corr < 0) return (int)corr;
         pmsrow[inst] = make_uint4((uint32_t)el | (sub->state << 12) | (sub->intr << 14) | (sub->part << 16),
                                   ord(sub->eik) | (ord(sub->key) << 16), (uint32_t)corr, 0);
+        // an opened subscription of another partition: its real element-instance key (the later DELETE's)
+        if (sub->state == 2 && (int32_t)sub->part != h->cfg.partition_id) pmseik[inst] = sub->eik;
       }
     } else if (sub) {
       return ZBHIP_EUNSUPP;
@@ -3951,6 +3959,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   HIPCHK(hipMemcpy(h->st.tmr, tmrrow.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
   if (h->st.n_slots) {
     HIPCHK(hipMemcpy(h->st.pms, pmsrow.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->st.pms_eik, pmseik.data(), N * sizeof(long long), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->st.pi_key, pikrow.data(), N * sizeof(long long), hipMemcpyHostToDevice));
   }
   // key histories and the resolve_key table: one entry per imported key

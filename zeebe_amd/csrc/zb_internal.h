@@ -200,6 +200,9 @@ struct DevState {
   uint4* pms;        // [n] PROCESS_SUBSCRIPTION row of the instance's waiting catch event:
                      //     x = elem | state << 12 (0 none, 1 opening, 2 opened) | interrupting << 14 | subpart << 16
                      //     y = eik ord | subscription key ord << 16; z = correlation key id; w = 0
+  long long* pms_eik; // [n] real element-instance key of the instance's subscription once its
+                      //     PROCESS_MESSAGE_SUBSCRIPTION:CREATE arrived from another partition (-1: none) --
+                      //     the MESSAGE_SUBSCRIPTION:DELETE a later window sends carries it
   long long* pi_key; // [n] real process-instance key (written by the device key scan)
   uint2* slot_hdr;   // [S] x = next key ordinal of the correlation slot; y = fence stamp (as hdr.w)
   uint4* sub_a;      // [kSubs][S] MESSAGE_SUBSCRIPTION rows: x = state (0 free, 1 open, 2 correlating)
