@@ -1279,7 +1279,9 @@ __device__ __forceinline__ void unsubscribe_message(Lane<K>& L) {
     // acknowledgement arrived -- has none here: outside the subset)
     const long long eik = L.inst < L.sp->st.n ? L.sp->st.pms_eik[L.inst] : -1;
     if (eik < 0 || st0 != 2) { set_fail(L, FB_MESSAGE); return; }
-    send_xpart(L, ZBHIP_CMD_MSG_SUB_DELETE, part, eik, L.pik, -1, corr, L.inst, eord, name_only, 1);
+    // (the entry carries the subscription's bpmnProcessId as the other sends do; the DELETE's record
+    // value leaves it empty -- the receiver builds it per kind)
+    send_xpart(L, ZBHIP_CMD_MSG_SUB_DELETE, part, eik, L.pik, -1, corr, L.inst, eord, nb, 1);
   }
 }
 
