@@ -3230,7 +3230,7 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
   const uint4 hd = R.hdr;
   if (!((hd.y >> 24) & 1)) {  // an ended instance: only a subscription still closing (header bit 25)
     const uint32_t ip = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
-    if (((hd.y >> 25) & 1) && ip != NONE && ip < h->procs.size())
+    if (hd.y == (1u << 25) && ip != NONE && ip < h->procs.size())
       emit_pms(h, inst, R, h->procs[ip], h->key_of(inst, 0), sink, ctx);
     return;
   }
@@ -3436,7 +3436,9 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   for (size_t i = 0; i < N; ++i) {
     R.hdr = hdr[i];
     const uint32_t proc = R.hdr.x & 0xFFFF;
-    if (proc == NONE || !((R.hdr.y >> 24) & 1)) continue;
+    // (an ended instance whose subscription is closing: header bit 25, its row only)
+    const bool closing = proc == NONE && R.hdr.y == (1u << 25) && S;
+    if (!closing && (proc == NONE || !((R.hdr.y >> 24) & 1))) continue;
     for (int k = 0; k < kSlots; ++k) R.slots[k] = slots[(size_t)k * N + i];
     for (int k = 0; k < kVars; ++k) {
       R.vm[k] = vm[(size_t)k * N + i];
