@@ -2790,7 +2790,6 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   // the FIFO; anything outside the canonical states takes the general path below
   bool fast = false;
   if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
-#ifdef ZB_FAST_SCOPE  // (the A/B build libzbhip_fast.so; its register allocation differs -- DESIGN §3)
   if constexpr (K::J && !K::S && !K::M && !K::REG) {
     if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_join_job(L, ref, doc_count);
   }
@@ -2798,7 +2797,6 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_scope_job(L, ref, doc_count);
     else if (kind == ZBHIP_CMD_CREATE && !P.no_fast_scope) fast = fast_scope_create(L, doc_count);
   }
-#endif
   int tpl_v = -1;
   uint32_t tpl_name = 0xFFFF;
   bool tpl_hit = false;

@@ -2246,8 +2246,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.max_cmds_in_batch = h->cfg.max_commands_in_batch;
   P.stamp = h->window_stamp;
   P.now_ms = h->clock_ms;
-  // the straight-line KScope / KGeneric batches are opt-in until measured on the GPU (ZBHIP_FAST_SCOPE=1)
-  P.no_fast_scope = getenv("ZBHIP_FAST_SCOPE") && !getenv("ZBHIP_NO_FAST_SCOPE") ? 0u : 1u;
+  // the straight-line KScope / KGeneric batches (ZBHIP_NO_FAST_SCOPE=1: the general path, for A/B)
+  P.no_fast_scope = getenv("ZBHIP_NO_FAST_SCOPE") ? 1u : 0u;
   P.cmd_due = h->d_cmd_due;
   P.map_val = h->d_map_val;
   P.map_cap = h->cfg.max_commands;
