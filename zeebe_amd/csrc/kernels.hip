@@ -1930,6 +1930,8 @@ constexpr uint32_t SEG_SRC_TIMER = 1u << 25, SEG_DST_TIMER = 1u << 26;
 // a task into a joining parallel gateway, and such a gateway's own word (its one flow onwards): the
 // joins of KGeneric (fast_join_job)
 constexpr uint32_t SEG_TO_JOIN = 1u << 27, SEG_FROM_GW = 1u << 28;
+// a none start event into a forking parallel gateway whose flows all lead into tasks (fast_fork_create)
+constexpr uint32_t SEG_TO_FORK = 1u << 29;
 
 template <class K>
 __device__ __forceinline__ void put(Lane<K>& L, int j, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem) {
@@ -2000,7 +2002,7 @@ __device__ __forceinline__ bool fast_command(Lane<K>& L, uint32_t kind, uint32_t
     const uint32_t start = L.pb[0] >> 16;
     if (start == NONE) return false;
     const uint32_t sg = seg[start];
-    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END | SEG_DST_TIMER)) != SEG_VALID) return false;
+    if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END | SEG_DST_TIMER | SEG_TO_FORK)) != SEG_VALID) return false;
     const uint32_t n = (sg >> 12) & 0xFFF;
     put(L, 0, ZBHIP_PI_ACTIVATE_ELEMENT, 0, NONE, 0);
     put(L, 1, C_PIC_CREATED, 1, 0, 0);
@@ -2205,6 +2207,70 @@ __device__ __forceinline__ bool fast_join_job(Lane<K>& L, uint32_t ref, uint32_t
   return !L.fail;
 }
 
+// A CREATE whose none start event leads into a forking parallel gateway with a task on every outgoing
+// flow (fork/join with a task per branch): the general path's records -- the process, the start event,
+// the gateway (its incoming flow's counter up and down again), SEQUENCE_FLOW_TAKEN + ACTIVATE_ELEMENT per
+// outgoing flow, then each task's ACTIVATING, JOB:CREATED, ACTIVATED in flow order -- no variables.
+template <class K>
+__device__ __forceinline__ bool fast_fork_create(Lane<K>& L, uint32_t doc_count) {
+  if (L.fail || L.proc == NONE || doc_count != 0 || L.limit <= 16 || L.pi_live || L.nt != 0 || !L.has_join)
+    return false;
+  const uint32_t start = L.pb[0] >> 16;
+  if (start == NONE) return false;
+  const uint32_t sg = L.pb[(L.pb[6] & 0xFFFF) + start];
+  if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_FORK)) != (SEG_VALID | SEG_TO_FORK)) return false;
+  const uint32_t g = (sg >> 12) & 0xFFF, f = sg & 0xFFF;
+  const uint4 gw = elem_of(L, g);
+  const uint32_t ob = gw.y & 0xFFFF, oc = gw.y >> 16;
+  if (oc > (uint32_t)K::T || oc > 8 || L.rec_cap < 16 + 5 * oc) return false;
+  const uint32_t pi = new_key(L);  // 0
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0);
+  const uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
+  emit(L, C_PIC_CREATED, created, pi, 0);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, pi, NONE, 0);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, pi, NONE, 0);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, NONE, 0, start);  // activateChildInstance: key -1
+  const uint32_t sk = new_key(L);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, sk, 0, start);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, sk, 0, start);
+  emit(L, ZBHIP_PI_COMPLETE_ELEMENT, sk, 0, start);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, sk, 0, start);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, sk, 0, start);
+  // the flow into the gateway counts on its join slot; the activation's Tetris decrement takes it off
+  const uint32_t sft = new_key(L);
+  emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, sft, 0, f);
+  const uint32_t gk = new_key(L);
+  emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, gk, 0, g);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, gk, 0, g);
+  emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, gk, 0, g);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETING, gk, 0, g);
+  emit(L, ZBHIP_PI_ELEMENT_COMPLETED, gk, 0, g);
+  uint32_t first = 0;
+  for (uint32_t i = 0; i < oc; ++i) {
+    const uint32_t fi = out_flow(L, ob + i);
+    const uint32_t ki = new_key(L);
+    emit(L, ZBHIP_PI_SEQUENCE_FLOW_TAKEN, ki, 0, fi);
+    const uint32_t kt = new_key(L);
+    if (i == 0) first = kt;
+    emit(L, ZBHIP_PI_ACTIVATE_ELEMENT, kt, 0, elem_of(L, fi).z & 0xFFFF);
+  }
+  for (uint32_t i = 0; i < oc; ++i) {
+    const uint32_t t = elem_of(L, out_flow(L, ob + i)).z & 0xFFFF;
+    const uint32_t kt = first + 2 * i;  // the task keys: every second key after the first flow's
+    emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, kt, 0, t);
+    const uint32_t job = new_key(L);
+    emit(L, C_JOB_CREATED, job, kt, t);
+    emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, kt, 0, t);
+    tput(L, (int)i, make_uint2(t | (kt << 16), (job & 0xFFFF) | ((uint32_t)ZBHIP_PI_ELEMENT_ACTIVATED << 16) | (1u << 24)));
+  }
+  L.nt = (int)oc;
+  L.pi_live = true;
+  L.pi_state = ZBHIP_PI_ELEMENT_ACTIVATED;
+  L.pi_child = (int)oc;
+  L.pi_asf = 0;
+  return !L.fail;
+}
+
 // A CREATE whose none start event leads into a task (with or without a timer boundary event):
 // CreateProcessInstanceProcessor, ProcessProcessor, StartEventProcessor and the task's activation in
 // the general path's order; no variables (a document takes the general path).
@@ -2215,7 +2281,7 @@ __device__ __forceinline__ bool fast_scope_create(Lane<K>& L, uint32_t doc_count
   const uint32_t start = L.pb[0] >> 16;
   if (start == NONE) return false;
   const uint32_t sg = L.pb[(L.pb[6] & 0xFFFF) + start];
-  if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END)) != SEG_VALID) return false;
+  if ((sg & (SEG_VALID | SEG_FROM_TASK | SEG_TO_END | SEG_TO_FORK)) != SEG_VALID) return false;
   const bool dst_tmr = sg & SEG_DST_TIMER;
   if (dst_tmr && !L.has_tmr) return false;
   const uint32_t n = (sg >> 12) & 0xFFF, f = sg & 0xFFF;
@@ -2792,6 +2858,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if constexpr (K::REG) fast = fast_command(L, kind, ref, doc_count);
   if constexpr (K::J && !K::S && !K::M && !K::REG) {
     if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_join_job(L, ref, doc_count);
+    else if (kind == ZBHIP_CMD_CREATE && !P.no_fast_scope) fast = fast_fork_create(L, doc_count);
   }
   if constexpr (K::S && !K::IO) {
     if (kind == ZBHIP_CMD_JOB_COMPLETE && !P.no_fast_scope) fast = fast_scope_job(L, ref, doc_count);

@@ -1119,6 +1119,18 @@ static int rebuild_program(zbhip_handle* h) {
           const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && (N.start_event == ZBHIP_NONE16 || dst_tmr) &&
                             !P.io_of(n) && !P.mi_inner(n);
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
+          // bit 29: a start event into a forking parallel gateway whose every outgoing flow is
+          // unconditional into a task without boundary event (KGeneric's fast_fork_create)
+          bool fork = E.element_type == ZBHIP_EL_START_EVENT && N.element_type == ZBHIP_EL_PARALLEL_GATEWAY &&
+                      N.in_count == 1 && N.out_count >= 2 && N.out_count <= 8 && N.flow_scope == 0;
+          for (uint32_t i = 0; fork && i < N.out_count; ++i) {
+            const zbhip_element& G = P.els[P.out[N.out_begin + i]];
+            const uint32_t t = G.flow_target;
+            fork = G.element_type == ZBHIP_EL_SEQUENCE_FLOW && G.condition == ZBHIP_NONE16 && t < n_el &&
+                   ZBHIP_IS_JOB_WORKER(P.els[t].element_type) && P.els[t].start_event == ZBHIP_NONE16 &&
+                   !P.io_of(t) && !P.mi_inner(t) && P.els[t].element_type != ZBHIP_EL_PARALLEL_GATEWAY;
+          }
+          if (fork) sg = (1u << 31) | (1u << 29) | (n << 12) | f;
           // bit 27: a task into a joining parallel gateway (KGeneric's fast_join_job)
           const bool join = ZBHIP_IS_JOB_WORKER(E.element_type) && !src_tmr && N.element_type == ZBHIP_EL_PARALLEL_GATEWAY &&
                             N.in_count >= 2 && N.out_count == 1 && N.flow_scope == 0;
