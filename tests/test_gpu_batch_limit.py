@@ -96,3 +96,25 @@ def test_fan_out_beyond_the_lds_ring(limit):
 @pytest.mark.parametrize("limit", [4, 100])
 def test_fork_join_with_tasks_batch_limit(limit):
     drive(bpmn.fork_join_process(6, tasks=True), limit)
+
+
+@pytest.mark.parametrize("limit", [16, 17, 100])
+def test_fork_join_8_tasks_straight_line_batches(limit):
+    # the bench's variant 4b: KGeneric's straight-line CREATE into the fork (limit > 16) and the branch
+    # completions into the join, against the general path's records (limit 16: CREATE on the FIFO)
+    drive(bpmn.fork_join_process(8, tasks=True), limit)
+
+
+def boundary_chain(n_tasks):
+    b = bpmn.createExecutableProcess("boundaryChain").startEvent("start")
+    for i in range(n_tasks):
+        b.serviceTask("task%d" % i, "t").boundaryEvent("late%d" % i).timerWithDuration("PT1H")
+        b.endEvent("lateEnd%d" % i).moveToActivity("task%d" % i)
+    return b.endEvent("end").done()
+
+
+@pytest.mark.parametrize("limit", [4, 5, 100])
+def test_timer_boundary_chain_straight_line_batches(limit):
+    # boundary10's shape: KScope's straight-line CREATE and completions (each cancels a timer and
+    # creates the next), and the general path at the tight limit
+    drive(boundary_chain(4), limit)
