@@ -1622,7 +1622,8 @@ class Oracle {
   std::map<int64_t, JobRow> jobs_;                              // JOBS (+ JOB_STATES = ACTIVATABLE)
   struct IncidentRow {  // IncidentRecord (protocol-impl/.../incident/IncidentRecord.java:20-48)
     PiValue pi;         // process, element, process instance key
-    int64_t eik = -1;   // elementInstanceKey = variableScopeKey
+    int64_t eik = -1;   // elementInstanceKey (= variableScopeKey unless variable_scope says otherwise)
+    int64_t variable_scope = -1;
     int error_type = 0, flow = -1, result = 0;  // the message: zbhip_incident_message
   };
   std::map<int64_t, IncidentRow> incidents_;                    // INCIDENTS
@@ -1972,13 +1973,28 @@ class Oracle {
 
   // `scope`: where the correlation key is evaluated -- the element itself, or for a boundary event
   // the activity's flow scope (CatchEventBehavior.evaluateCorrelationKey, common/CatchEventBehavior.java:187-205)
-  void subscribe_to_message(const OEl& el, int64_t key, const PiValue& v, int64_t scope) {
+  // Returns false after the EXTRACT_VALUE_ERROR incident of a correlation key that is neither a string
+  // nor a number (ExpressionProcessor.typeCheckCorrelationKey, :317-331; the failure's variableScopeKey
+  // is `scope`): the element is left ACTIVATING, its caller writes nothing more (incidentBehavior
+  // .createIncident(failure, context), JobWorkerTaskProcessor.onActivate :50-61).  `incident` is the
+  // element instance the incident is raised on (the task for a boundary event) and its value.
+  bool subscribe_to_message(const OEl& el, int64_t key, const PiValue& v, int64_t scope, int64_t incident_key,
+                            const PiValue& incident_v) {
     // evaluateCorrelationKey (:155-178) -> ExpressionProcessor.evaluateMessageCorrelationKeyExpression
     // (processing/common/ExpressionProcessor.java:309-337): STRING or NUMBER, else incident
     auto nit = name_ids.find(el.corr_var);
     const VarRow* vr = nit == name_ids.end() ? nullptr : lookup_var(scope, nit->second);
-    if (!vr || vr->type != ZBHIP_DOC_STR)
-      throw Unsupported{"correlation key is not a string (incident, or a NUMBER outside the subset)"};
+    if (!vr || vr->type == ZBHIP_DOC_NIL || vr->type == ZBHIP_DOC_BOOL) {
+      FlowFailure f;
+      f.error_type = ZBHIP_ERR_EXTRACT_VALUE_ERROR;
+      f.flow = kCorrelationKeyFailure;
+      f.result = vr && vr->type == ZBHIP_DOC_BOOL ? kFeelBoolean : ZBHIP_FEEL_NULL;
+      create_incident(f, incident_key, incident_v);
+      incidents_.rbegin()->second.variable_scope = scope;
+      batch_->back().r.message_key = scope;  // (the record's variableScopeKey; INCIDENT records only here)
+      return false;
+    }
+    if (vr->type != ZBHIP_DOC_STR) throw Unsupported{"correlation key is a NUMBER (outside the subset)"};
     MsgVal m;
     m.corr = (uint32_t)vr->value;
     m.name = (uint16_t)intern(el.msg_name);
@@ -1998,6 +2014,7 @@ class Oracle {
     pms_[{key, (int)m.name}] = PmsRow{subKey, false, m};  // ProcessMessageSubscriptionCreatingApplier
     ++pms_inst_[cur_instance_];
     send_command(m.partition, ZBHIP_CMD_MSG_SUB_CREATE, m);
+    return true;
   }
 
   // MessageSubscriptionCreateProcessor.processRecord (processing/message/MessageSubscriptionCreateProcessor.java:66-104)
@@ -2650,8 +2667,11 @@ class Oracle {
           PiValue bv = v;
           bv.elem = el.boundary;
           const OEl& b = P(v.proc).els[el.boundary];
-          if (b.event == ZBHIP_EV_MESSAGE) subscribe_to_message(b, key, bv, v.flowScopeKey);
-          else subscribe_to_timer(b, key, bv);
+          if (b.event == ZBHIP_EV_MESSAGE) {
+            if (!subscribe_to_message(b, key, bv, v.flowScopeKey, key, v)) break;  // incident on the task
+          } else {
+            subscribe_to_timer(b, key, bv);
+          }
         }
         // BpmnJobBehavior.createNewJob -> writeJobCreatedEvent (behavior/BpmnJobBehavior.java:113-119,194-218)
         JobRow job;
@@ -2686,7 +2706,7 @@ class Oracle {
         // IntermediateCatchEventProcessor.DefaultIntermediateCatchEventBehavior.onActivate
         // (processing/bpmn/event/IntermediateCatchEventProcessor.java): subscribeToEvents, then ACTIVATED
         if (el.event == ZBHIP_EV_TIMER) subscribe_to_timer(el, key, v);
-        else subscribe_to_message(el, key, v, key);
+        else if (!subscribe_to_message(el, key, v, key, key, v)) break;  // incident: stays ACTIVATING
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         break;
       case ZBHIP_EL_PARALLEL_GATEWAY:  // ParallelGatewayProcessor.onActivate (processing/bpmn/gateway/ParallelGatewayProcessor.java:34-50)
@@ -2876,6 +2896,9 @@ class Oracle {
   // A failure (Either.left) is returned as -2 with `fail`: the error type, the flow whose condition
   // did not evaluate to a boolean (-1: none chosen) and that result's type.
   struct FlowFailure { int error_type = 0, flow = -1, result = 0; };
+  // an incident's `flow` marking a message correlation key that is neither a string nor a number, and
+  // that key's BOOLEAN result type (beside ZBHIP_FEEL_NULL / NUMBER / STRING)
+  static constexpr int kCorrelationKeyFailure = -3, kFeelBoolean = 3;
   int find_sequence_flow_to_take(const OEl& el, int64_t gwKey, int proc, FlowFailure& fail) {
     const OProc& p = P(proc);
     if (el.out.empty()) return -1;  // implicit end of the flow scope

@@ -185,3 +185,32 @@ def test_non_interrupting_message_boundary_is_refused():
     o = Oracle()
     with pytest.raises(Exception):
         o.deploy(xml)
+
+
+def test_correlation_key_incident_on_the_task():
+    # BoundaryEventTest.shouldHaveScopeKeyIfBoundaryEvent (:352-391): a correlation key that is not a
+    # string or a number -> EXTRACT_VALUE_ERROR on the task (elementId task, elementInstanceKey = the
+    # task's ACTIVATING key, variableScopeKey = the process instance), no subscription, no job, the task
+    # left ACTIVATING.  (The gfx950 path falls back on such keys: no device counterpart.)
+    o = Oracle()
+    o.deploy(bpmn.message_boundary_process(correlation_key="orderId"))
+    name = o.intern("orderId")
+    from helpers import create_commands
+    c = create_commands(1)
+    c["doc_count"] = 1
+    d = abi.make_docs(1)
+    d["name_id"], d["type"], d["value"] = name, abi.DOC_BOOL, 1
+    o.submit(c, d)
+    o.run()
+    recs = o.records()
+    el = lambda r: o.element_id(int(r["process_idx"]), int(r["element_idx"]))  # noqa: E731
+    task = [r for r in recs if int(r["value_type"]) == abi.VT_PROCESS_INSTANCE and el(r) == "task"]
+    assert [int(r["intent"]) for r in task if int(r["record_type"]) == abi.RT_EVENT] == [2]  # ACTIVATING only
+    inc = [r for r in recs if int(r["value_type"]) == abi.VT_INCIDENT]
+    assert len(inc) == 1
+    r = inc[0]
+    assert int(r["partition"]) == 4  # ErrorType.EXTRACT_VALUE_ERROR
+    assert el(r) == "task" and int(r["scope_key"]) == int(task[-1]["key"])
+    pik = int(r["process_instance_key"])
+    assert int(r["message_key"]) == pik  # variableScopeKey: the task's flow scope
+    assert not any(int(x["value_type"]) in (abi.VT_JOB, abi.VT_PROCESS_MESSAGE_SUBSCRIPTION) for x in recs)
