@@ -7,7 +7,7 @@ O=${OUT:-gpurun_out/kab}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-for v in product w4 b64; do
+for v in ${VARIANTS:-product w4 b64}; do
   unset ZBHIP_LIB
   if [ $v != product ]; then [ -f zeebe_amd/libzbhip_$v.so ] || continue; export ZBHIP_LIB=$PWD/zeebe_amd/libzbhip_$v.so; fi
   for cfg in boundary10 forkjoin8_tasks forkjoin8; do
