@@ -390,6 +390,8 @@ def main():
     ap.add_argument("--config", default="linear10")
     ap.add_argument("--instances", type=int, default=0, help="override instances per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--untrusted-windows", action="store_true",
+                    help="check every device window's subjects on the device (k_subject_check) in the timed loop")
     ap.add_argument("--no-templates", action="store_true",
                     help="general path only: CREATE batch templates off (ZBHIP_NO_TEMPLATES)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -486,7 +488,9 @@ def run_rank(args):
     pstream = torch.cuda.Stream(device=torch.device("cuda", local_rank))
     part = Partition(partition_id=rank + 1, partition_count=world, device=local_rank, max_instances=n,
                      max_commands=n, max_records_per_batch=recs_per_batch, stream=pstream.cuda_stream,
-                     trusted_device_windows=True)  # one command per instance per window, by construction
+                     # one command per instance per window, by construction; --untrusted-windows runs the
+                     # device subject check (k_subject_check) on every window as an untrusted caller would
+                     trusted_device_windows=not args.untrusted_windows)
     part.deploy(xml)
     name = part.intern("amount") if with_amount else None
 
@@ -618,7 +622,7 @@ def run_rank(args):
                                               "event (timers created and canceled), 1M instances"}[args.config],
                    "instances_per_gpu": n, "windows_per_step": len(windows), "partitions": world,
                    "parallelism": "one partition per GPU (dp%d)" % world, "max_commands_in_batch": 100,
-                   "templates": not args.no_templates},
+                   "templates": not args.no_templates, "subject_check": bool(args.untrusted_windows)},
         "records_per_s": tot_recs / elapsed,
         # CREATE batches copied from a template the general path recorded (kernels.hip tpl_create)
         "template_batches_per_step": tpl_timed / max(1, args.steps),
