@@ -21,7 +21,11 @@
  *  - config 5 (correlationSlots > 0): MESSAGE:PUBLISH, MESSAGE_SUBSCRIPTION:CREATE/CORRELATE and
  *    PROCESS_MESSAGE_SUBSCRIPTION:CREATE/CORRELATE run on the device (Messages), and the commands a
  *    device batch sends to other partitions go to InterPartitionCommandSender in a post-commit task of
- *    that batch (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition, :320-338).
+ *    that batch (SubscriptionCommandSender.handleFollowUpCommandBasedOnPartition, :320-338);
+ *  - the engine's scheduled tasks read device-held state through DeviceScheduledState (timerState,
+ *    jobState, pending*State below, passed to the checkers EngineProcessors builds), device TIMER:CREATED
+ *    records schedule the DueDateTimerChecker as the engine's do (a side effect), and JOB:TIME_OUT of a
+ *    device job runs through zbhip_time_out_job (JobTimeOutProcessor.java:46-73).
  * The Python mirror zeebe_amd/adapter.py is this class line for line in behaviour; tests/test_gpu_psm.py
  * runs it inside a restatement of ProcessingStateMachine against the engine alone.
  *
@@ -154,6 +158,8 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   private final Set<Integer> handedOff = new HashSet<>();
   private final ArrayDeque<Continuation> continuations = new ArrayDeque<>();
   private int followUps; // follow-ups of the current device batch the platform feeds back
+  private boolean windowDone = true; // every command of the current window was emitted
+  private io.camunda.zeebe.engine.processing.timer.DueDateTimerChecker dueDateTimerChecker;
 
   public GpuBatchProcessor(
       final Engine engine,
@@ -264,6 +270,10 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       final JobBatchRecord batch = (JobBatchRecord) record.getValue();
       return engineJobTypes.contains(batch.getType()) ? engine.process(record, out) : activateJobs(record, batch, out);
     }
+    if (record.getValueType() == ValueType.JOB && record.getIntent() == JobIntent.TIME_OUT
+        && ZbHip.resolveKey(handle, record.getKey()) >= 0) {
+      return timeOutJob(record, out);
+    }
     int i = window.covers(record.getPosition()) ? window.indexOf(record.getPosition()) : -1;
     if (i < 0) {
       if (!isHotPath(record, continuations.iterator())) {
@@ -282,6 +292,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
         return engine.process(record, out); // the read-ahead stopped before it
       }
     }
+    windowDone = i == window.size() - 1;
     if (ZbHip.commandStatus(handle, i) != 0) {
       return fallBack(i, record, out);
     }
@@ -399,6 +410,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     // the window's clock: TIMER:CREATED dueDates (CatchEventBehavior.java:310, ActorClock)
     ZbHip.setClock(handle, ActorClock.currentTimeMillis());
     window.submitRun(handle);
+    windowDone = false;
   }
 
   /** A process instance completed (Window.emit): its slot is free once its continuations ran. */
@@ -502,6 +514,9 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       continuations.removeIf(c -> c.slot() == instance);
       usedSlots.clear(instance);
       ended.remove(instance);
+      if (messages != null && messages.enabled()) {
+        messages.handedOff(instance);
+      }
     }
   }
 
@@ -516,6 +531,85 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       return true;
     });
     return engine.process(record, out);
+  }
+
+  // ---- the engine's scheduled tasks over device-held state (DeviceScheduledState, INTEGRATION.md §8) ----
+
+  /** What EngineProcessors passes to DueDateTimerChecker instead of the engine's TimerInstanceState. */
+  public io.camunda.zeebe.engine.state.immutable.TimerInstanceState timerState(
+      final io.camunda.zeebe.engine.state.immutable.TimerInstanceState engineTimers) {
+    return new DeviceScheduledState.Timers(this, engineTimers);
+  }
+
+  /** ... to JobTimeoutTrigger instead of the engine's JobState. */
+  public io.camunda.zeebe.engine.state.immutable.JobState jobState(
+      final io.camunda.zeebe.engine.state.immutable.JobState engineJobs) {
+    return new DeviceScheduledState.Jobs(this, engineJobs);
+  }
+
+  /**
+   * ... to PendingProcessMessageSubscriptionChecker; {@code engineTransient} is the engine's
+   * TransientPendingSubscriptionState (the pending entries of handed-off instances move into it).
+   */
+  public io.camunda.zeebe.engine.state.immutable.PendingProcessMessageSubscriptionState pendingProcessSubscriptionState(
+      final io.camunda.zeebe.engine.state.immutable.PendingProcessMessageSubscriptionState engineState,
+      final io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState engineTransient) {
+    return new DeviceScheduledState.PendingProcessSubscriptions(this, engineState, engineTransient);
+  }
+
+  /** ... to MessageObserver (PendingMessageSubscriptionChecker). */
+  public io.camunda.zeebe.engine.state.immutable.PendingMessageSubscriptionState pendingMessageSubscriptionState(
+      final io.camunda.zeebe.engine.state.immutable.PendingMessageSubscriptionState engineState) {
+    return new DeviceScheduledState.PendingMessageSubscriptions(this, engineState);
+  }
+
+  /** The DueDateTimerChecker device TIMER:CREATED records schedule (CatchEventBehavior's side effect). */
+  public void setDueDateTimerChecker(final io.camunda.zeebe.engine.processing.timer.DueDateTimerChecker checker) {
+    dueDateTimerChecker = checker;
+  }
+
+  void timerCreated(final ProcessingResultBuilder out, final long dueDate) {
+    if (dueDateTimerChecker != null) {
+      out.appendPostCommitTask(() -> {
+        dueDateTimerChecker.scheduleTimer(dueDate);
+        return true;
+      });
+    }
+  }
+
+  /** The device state equals the log's: the current window's commands were all emitted. */
+  boolean scheduledReady() {
+    return windowDone;
+  }
+
+  MemorySegment handle() {
+    return handle;
+  }
+
+  /** The stored JobRecord of a zbhip_record JOB row (zbhip_timed_out_jobs / zbhip_time_out_job). */
+  JobRecord storedJob(final MemorySegment row) {
+    return (JobRecord) window.valueOf(row, this);
+  }
+
+  // ---- JOB:TIME_OUT of a device job (JobTimeOutProcessor.java:46-73) ------------------------------
+
+  private ProcessingResult timeOutJob(final TypedRecord record, final ProcessingResultBuilder out) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment r = a.allocate(ZbHip.RECORD);
+      ZbHip.timeOutJob(handle, record.getKey(), ActorClock.currentTimeMillis(), r);
+      final RecordMetadata meta = new RecordMetadata().valueType(ValueType.JOB);
+      if (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value()) {
+        meta.recordType(RecordType.COMMAND_REJECTION).intent(JobIntent.TIME_OUT)
+            .rejectionType(io.camunda.zeebe.protocol.record.RejectionType.NOT_FOUND)
+            .rejectionReason(rejectionReason(r));
+        out.appendRecord(record.getKey(), (JobRecord) record.getValue(), meta);
+      } else {
+        // JOB:TIMED_OUT with the stored job; publishWork -> notifyWorkAvailable (a side effect, no record)
+        meta.recordType(RecordType.EVENT).intent(JobIntent.TIMED_OUT);
+        out.appendRecord(record.getKey(), storedJob(r), meta);
+      }
+    }
+    return out.build();
   }
 
   // ---- job activation (JobBatchActivateProcessor.java:60-143) --------------------------------------

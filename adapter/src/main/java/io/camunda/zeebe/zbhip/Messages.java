@@ -65,8 +65,25 @@ final class Messages {
   // (elementInstanceKey, messageName) -> routing handle (slot << 16 | ordinal) of a device subscription
   private final Map<SubscriptionKey, Long> handles = new HashMap<>();
   private final java.util.Set<Integer> closingSlots = new java.util.HashSet<>();
+  // the transient pending states the appliers of the device's records keep in the reference
+  // (DbProcessMessageSubscriptionState.java:82-124,180-222, DbMessageSubscriptionState.java:157-222):
+  // OPENING / CLOSING process message subscriptions and CORRELATING message subscriptions, with the time
+  // they were last sent (insertion order kept: TransientPendingSubscriptionState.entriesBefore sorts by it)
+  final Map<SubscriptionKey, PendingProcessSubscription> pendingProcess = new java.util.LinkedHashMap<>();
+  final Map<SubscriptionKey, PendingSubscription> pendingMessage = new java.util.LinkedHashMap<>();
 
-  private record SubscriptionKey(long elementInstanceKey, String messageName) {}
+  record SubscriptionKey(long elementInstanceKey, String messageName) {}
+
+  static final class PendingProcessSubscription {
+    long sentTime;
+    final ProcessMessageSubscriptionRecord record = new ProcessMessageSubscriptionRecord();
+    boolean opening;
+  }
+
+  static final class PendingSubscription {
+    long sentTime;
+    final MessageSubscriptionRecord record = new MessageSubscriptionRecord();
+  }
 
   Messages(final int partitionId, final int correlationSlots, final Set<String> messageNames) {
     this.partitionId = partitionId;
@@ -196,6 +213,11 @@ final class Messages {
       subscriptions.put(k, correlationSlot);
     } else if (intent == MessageSubscriptionIntent.CORRELATED || intent == MessageSubscriptionIntent.DELETED) {
       subscriptions.remove(k);
+      pendingMessage.remove(k);
+    } else if (intent == MessageSubscriptionIntent.CORRELATING) {  // updateToCorrelatingState
+      final PendingSubscription ps = pendingMessage.computeIfAbsent(k, x -> new PendingSubscription());
+      ps.sentTime = io.camunda.zeebe.scheduler.clock.ActorClock.currentTimeMillis();
+      ps.record.wrap(v);
     }
   }
 
@@ -207,14 +229,46 @@ final class Messages {
   void onProcessSubscriptionEvent(final Intent intent, final ProcessMessageSubscriptionRecord v, final int slot,
       final GpuBatchProcessor p) {
     final SubscriptionKey k = new SubscriptionKey(v.getElementInstanceKey(), v.getMessageName());
+    if (intent == ProcessMessageSubscriptionIntent.CREATING || intent == ProcessMessageSubscriptionIntent.DELETING) {
+      // put (OPENING) / updateToClosingState: pending since now
+      final PendingProcessSubscription ps = pendingProcess.computeIfAbsent(k, x -> new PendingProcessSubscription());
+      ps.sentTime = io.camunda.zeebe.scheduler.clock.ActorClock.currentTimeMillis();
+      ps.record.wrap(v);
+      ps.opening = intent == ProcessMessageSubscriptionIntent.CREATING;
+    }
     if (intent == ProcessMessageSubscriptionIntent.CREATING) {
       handles.put(k, p.resolve(v.getElementInstanceKey()));
     } else if (intent == ProcessMessageSubscriptionIntent.DELETING) {
       closingSlots.add(slot);
+    } else if (intent == ProcessMessageSubscriptionIntent.CREATED) {
+      pendingProcess.remove(k);  // updateToOpenedState
     } else if (intent == ProcessMessageSubscriptionIntent.CORRELATED || intent == ProcessMessageSubscriptionIntent.DELETED) {
       handles.remove(k);
+      pendingProcess.remove(k);
       if (intent == ProcessMessageSubscriptionIntent.DELETED) {
         closingSlots.remove(slot);
+      }
+    }
+  }
+
+  // pending entries of handed-off instances, moved into the engine's transient state by
+  // DeviceScheduledState.PendingProcessSubscriptions (the hand-off writes RocksDB rows only)
+  final List<Map.Entry<SubscriptionKey, PendingProcessSubscription>> movedPending = new ArrayList<>();
+
+  /**
+   * Instance slot `slot` was handed off to the engine: its subscriptions are the engine's now -- no
+   * closing row holds the slot, no routing handle points into it, their pending entries move.
+   */
+  void handedOff(final int slot) {
+    closingSlots.remove(slot);
+    for (final var it = handles.entrySet().iterator(); it.hasNext(); ) {
+      final var e = it.next();
+      if (e.getValue() >= 0 && (int) (e.getValue() >>> 16) == slot) {
+        final PendingProcessSubscription ps = pendingProcess.remove(e.getKey());
+        if (ps != null) {
+          movedPending.add(Map.entry(e.getKey(), ps));
+        }
+        it.remove();
       }
     }
   }

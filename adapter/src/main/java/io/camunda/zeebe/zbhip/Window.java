@@ -43,6 +43,7 @@ import io.camunda.zeebe.protocol.record.intent.ProcessEventIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessInstanceCreationIntent;
 import io.camunda.zeebe.protocol.record.intent.ProcessInstanceIntent;
 import io.camunda.zeebe.protocol.record.intent.VariableIntent;
+import io.camunda.zeebe.protocol.record.intent.TimerIntent;
 import io.camunda.zeebe.protocol.record.value.BpmnElementType;
 import io.camunda.zeebe.protocol.record.value.BpmnEventType;
 import io.camunda.zeebe.protocol.record.value.ErrorType;
@@ -317,6 +318,7 @@ final class Window {
   int emit(final int i, final TypedRecord command, final ProcessingResultBuilder out, final GpuBatchProcessor p) {
     final long nr = ZbHip.drainCommand(handle, i, this::ofAtLeast);
     final RecordMetadata meta = new RecordMetadata();
+    commandTimestamp = command.getTimestamp(); // a MESSAGE record's deadline = timestamp + timeToLive
     int admitted = 0;
     for (long r = 0; r < nr; r++) {
       final MemorySegment rec = recs.asSlice(80L * r, 80);
@@ -355,6 +357,9 @@ final class Window {
       } else if (valueType == ValueType.PROCESS_INSTANCE.value()
           && intent == ProcessInstanceIntent.ELEMENT_COMPLETED.value() && rec.get(JAVA_INT, 36) == 0) {
         p.instanceEnded(instances[i]); // the process element (index 0) completed
+      } else if (valueType == ValueType.TIMER.value() && recordType == RecordType.EVENT.value()
+          && intent == TimerIntent.CREATED.value()) {
+        p.timerCreated(out, ((TimerRecord) value).getDueDate()); // DueDateTimerChecker.scheduleTimer, post-commit
       } else if (valueType == ValueType.MESSAGE_SUBSCRIPTION.value() && recordType == RecordType.EVENT.value()) {
         p.messages().onSubscriptionEvent(meta.getIntent(), (MessageSubscriptionRecord) value, rec.get(JAVA_INT, 64));
       } else if (valueType == ValueType.PROCESS_MESSAGE_SUBSCRIPTION.value() && recordType == RecordType.EVENT.value()) {
@@ -375,6 +380,13 @@ final class Window {
 
   private static Intent intent(final byte valueType, final byte intent) {
     return Intent.fromProtocolValue(ValueType.get((short) valueType), (short) intent);
+  }
+
+  private long commandTimestamp; // the timestamp of the command emit() expands
+
+  /** The record value of a zbhip_record row without a source document (the scheduled-task calls). */
+  UnifiedRecordValue valueOf(final MemorySegment r, final GpuBatchProcessor p) {
+    return value(r, -1, p);
   }
 
   private UnifiedRecordValue value(final MemorySegment r, final int i, final GpuBatchProcessor p) {
@@ -489,7 +501,7 @@ final class Window {
         return v.setTenantId(TENANT);
       }
       case MESSAGE, MESSAGE_SUBSCRIPTION, PROCESS_MESSAGE_SUBSCRIPTION -> {
-        return messageValue(r, vt, d, elem, scope, pik, p);
+        return messageValue(r, vt, d, elem, scope, pik, p, commandTimestamp);
       }
       default -> throw new IllegalStateException("value type outside the device subset: " + vt);
     }
@@ -501,7 +513,7 @@ final class Window {
    * timestamp + timeToLive 0 (MessagePublishProcessor.java:110).
    */
   private static UnifiedRecordValue messageValue(final MemorySegment r, final ValueType vt, final ZbHip.Deployed d,
-      final int elem, final long scope, final long pik, final GpuBatchProcessor p) {
+      final int elem, final long scope, final long pik, final GpuBatchProcessor p, final long timestamp) {
     final int nameId = r.get(JAVA_SHORT, 68) & 0xFFFF, bpmnId = r.get(JAVA_SHORT, 70) & 0xFFFF;
     final int corrId = r.get(JAVA_INT, 64);
     final DirectBuffer name = new UnsafeBuffer((nameId == 0xFFFF ? "" : p.name(nameId)).getBytes());
@@ -510,7 +522,7 @@ final class Window {
     final boolean interrupting = r.get(JAVA_BYTE, 76) != 0;
     final long messageKey = r.get(JAVA_LONG, 56);
     if (vt == ValueType.MESSAGE) {
-      return new MessageRecord().setName(name).setCorrelationKey(corr).setTimeToLive(0).setDeadline(0)
+      return new MessageRecord().setName(name).setCorrelationKey(corr).setTimeToLive(0).setDeadline(timestamp)
           .setTenantId(TENANT);
     }
     if (vt == ValueType.MESSAGE_SUBSCRIPTION) {

@@ -204,6 +204,12 @@ public final class ZbHip {
       fn("zbhip_import_state_db", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, JAVA_INT, ADDRESS));
   private static final MethodHandle STRING = fn("zbhip_string", FunctionDescriptor.of(ADDRESS, ADDRESS, JAVA_INT, JAVA_INT));
   private static final MethodHandle NAME = fn("zbhip_name", FunctionDescriptor.of(ADDRESS, ADDRESS, JAVA_INT));
+  private static final MethodHandle DUE_TIMERS =
+      fn("zbhip_due_timers", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
+  private static final MethodHandle TIMED_OUT_JOBS =
+      fn("zbhip_timed_out_jobs", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
+  private static final MethodHandle TIME_OUT_JOB =
+      fn("zbhip_time_out_job", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, JAVA_LONG, ADDRESS));
 
   /** The zbhip_db_sink upcall: (ctx, column family, key, key length, value, value length). */
   @FunctionalInterface
@@ -516,6 +522,36 @@ public final class ZbHip {
   public static void activateJobs(
       final MemorySegment h, final MemorySegment cmd, final MemorySegment jobs, final long cap, final MemorySegment result) {
     check((int) call(ACTIVATE_JOBS, h, cmd, jobs, cap, result), "zbhip_activate_jobs");
+  }
+
+  /**
+   * zbhip_due_timers: the TIMER:TRIGGER commands of device timers with dueDate <= now (RECORD rows in
+   * TIMER_DUE_DATES order) into {@code out}; returns their number, the first dueDate not returned in
+   * {@code nextDue[0]} (-1 none).
+   */
+  public static long dueTimers(final MemorySegment h, final long now, final MemorySegment out, final long cap,
+      final long[] nextDue) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      final MemorySegment next = a.allocate(JAVA_LONG);
+      check((int) call(DUE_TIMERS, h, now, out, cap, n, next), "zbhip_due_timers");
+      nextDue[0] = next.get(JAVA_LONG, 0);
+      return n.get(JAVA_LONG, 0);
+    }
+  }
+
+  /** zbhip_timed_out_jobs: the JOB:TIME_OUT commands of activated device jobs with deadline < now. */
+  public static long timedOutJobs(final MemorySegment h, final long now, final MemorySegment out, final long cap) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      check((int) call(TIMED_OUT_JOBS, h, now, out, cap, n), "zbhip_timed_out_jobs");
+      return n.get(JAVA_LONG, 0);
+    }
+  }
+
+  /** zbhip_time_out_job: JOB:TIMED_OUT or the NOT_FOUND rejection of a device job, one RECORD row. */
+  public static void timeOutJob(final MemorySegment h, final long jobKey, final long now, final MemorySegment out) {
+    check((int) call(TIME_OUT_JOB, h, jobKey, now, out), "zbhip_time_out_job");
   }
 
   /** Room for the records of one command: returns a buffer of at least n RECORD rows. */

@@ -105,7 +105,10 @@ enum zbhip_pi_intent {
 /* JobIntent CREATED=0 COMPLETE=1 COMPLETED=2 CANCELED=10 (JobIntent.java:19-45); VariableIntent
  * CREATED=0 UPDATED=1; ProcessEventIntent TRIGGERING=0 TRIGGERED=1; ProcessInstanceCreationIntent
  * CREATE=0 CREATED=1 */
-enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2, ZBHIP_JOB_CANCELED = 10 };
+enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2, ZBHIP_JOB_TIME_OUT = 3,
+       ZBHIP_JOB_TIMED_OUT = 4, ZBHIP_JOB_FAIL = 5, ZBHIP_JOB_FAILED = 6, ZBHIP_JOB_CANCELED = 10 };
+enum { ZBHIP_JOB_BATCH_ACTIVATE = 0, ZBHIP_JOB_BATCH_ACTIVATED = 1 };  /* JobBatchIntent */
+#define ZBHIP_VT_JOB_BATCH 1
 enum { ZBHIP_VAR_CREATED = 0, ZBHIP_VAR_UPDATED = 1 };
 enum { ZBHIP_PE_TRIGGERING = 0, ZBHIP_PE_TRIGGERED = 1 };
 enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
@@ -605,7 +608,9 @@ enum zbhip_reason {
   ZBHIP_REASON_PMS_CORR_NO_EVENT = 11,  /* ... NO_EVENT_OCCURRED_MESSAGE */
   ZBHIP_REASON_MS_CORR_NOT_FOUND = 12,  /* MessageSubscriptionCorrelateProcessor NO_SUBSCRIPTION_FOUND */
   ZBHIP_REASON_TIMER_NOT_FOUND = 13,    /* TriggerTimerProcessor NO_TIMER_FOUND_MESSAGE */
-  ZBHIP_REASON_TIMER_NOT_ACTIVE = 14    /* TriggerTimerProcessor NO_ACTIVE_TIMER_MESSAGE */
+  ZBHIP_REASON_TIMER_NOT_ACTIVE = 14,   /* TriggerTimerProcessor NO_ACTIVE_TIMER_MESSAGE */
+  ZBHIP_REASON_JOB_TIME_OUT = 15        /* JobTimeOutProcessor NOT_ACTIVATED_JOB_MESSAGE; reason_arg 0 "no such job
+                                           was found", 1 "it must be activated first", 2 "it has not timed out" */
 };
 /* Rejection reason text exactly as the reference writes it. */
 int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, size_t cap);
@@ -747,6 +752,29 @@ int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* cmd, zbhip_
                         zbhip_job_batch* result);
 /* The rejection reason of a refused JOB_BATCH:ACTIVATE, exactly as JobBatchActivateProcessor writes it. */
 int zbhip_job_batch_rejection_reason(const zbhip_job_activation* cmd, const zbhip_job_batch* result, char* buf, size_t cap);
+
+/* ---- the engine's scheduled tasks over device-held state ---------------------------------------
+ * The reference's checkers scan RocksDB, which does not hold what the device holds; a host adapter's
+ * checkers read these instead and write the same commands.  Call them between
+ * batches once the current window's commands were all emitted (zbhip_drain_command): the device state
+ * is then exactly the log's.  Records come back as zbhip_record rows, so the adapter builds the
+ * command values with the same code as drained records. */
+/* DueDateTimerChecker.TriggerTimersSideEffect (processing/timer/DueDateTimerChecker.java:86-129) ->
+ * DbTimerInstanceState.processTimersWithDueDateBefore (state/instance/DbTimerInstanceState.java:87-116):
+ * the TIMER:TRIGGER commands of the device timers with dueDate <= now, in TIMER_DUE_DATES order
+ * (dueDate, elementInstanceKey, timer key); at most cap, *next_due = the first dueDate not returned
+ * (-1: none) -- what DueDateChecker reschedules with.  A device scan (k_due_timers, 16 B per instance). */
+int zbhip_due_timers(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out, int64_t* next_due);
+/* JobTimeoutTrigger.DeactivateTimeOutJobs (processing/job/JobTimeoutTrigger.java:74-87) ->
+ * DbJobState.forEachTimedOutEntry (state/instance/DbJobState.java:286-298): the JOB:TIME_OUT commands
+ * (key = the job, value = the stored job) of ACTIVATED device jobs with deadline < now, in JOB_DEADLINES
+ * order (deadline, key). */
+int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out);
+/* JOB:TIME_OUT of a device job (JobTimeOutProcessor.processRecord, processing/job/JobTimeOutProcessor
+ * .java:46-73; `now` = ActorClock.currentTimeMillis()): *out = JOB:TIMED_OUT with the stored job
+ * (JobTimedOutApplier -> DbJobState.timeout: ACTIVATABLE again, deadline and worker kept), or the
+ * NOT_FOUND rejection (reason ZBHIP_REASON_JOB_TIME_OUT; the adapter writes the command's value). */
+int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out);
 
 /* ---- fallback hand-off (Engine.java:134 onProcessingError, ProcessingStateMachine.java:276-310) --
  * A command the device did not process (zbhip_command_status != 0) goes to the CPU engine, in log

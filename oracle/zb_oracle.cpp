@@ -1329,7 +1329,7 @@ class Oracle {
                      (r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION &&
                       (r.intent == ZBHIP_PMS_CREATE || r.intent == ZBHIP_PMS_CORRELATE || r.intent == ZBHIP_PMS_DELETE));
     const bool known = (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION && r.intent == ZBHIP_PIC_CREATE) ||
-                       (r.value_type == ZBHIP_VT_JOB && r.intent == ZBHIP_JOB_COMPLETE) ||
+                       (r.value_type == ZBHIP_VT_JOB && (r.intent == ZBHIP_JOB_COMPLETE || r.intent == ZBHIP_JOB_TIME_OUT)) ||
                        (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && r.intent == ZBHIP_PIB_ACTIVATE) || msg;
@@ -1789,6 +1789,8 @@ class Oracle {
   void process(ORecord& cmd) {
     if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION)
       create_process_instance(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_JOB && cmd.r.intent == ZBHIP_JOB_TIME_OUT)
+      time_out_job(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_JOB)
       complete_job(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_TIMER && cmd.r.intent == ZBHIP_TIMER_TRIGGER)
@@ -2336,10 +2338,38 @@ class Oracle {
     }
   }
 
-  // an ACTIVATED job's record carries the deadline and worker DbJobState.activate stored (the
-  // zbhip_record fields message_key / correlation_key of a JOB record)
+  // JobTimeOutProcessor.processRecord (processing/job/JobTimeOutProcessor.java:46-73): an ACTIVATED job
+  // whose deadline passed (deadline < ActorClock.currentTimeMillis()) -> JOB:TIMED_OUT with the stored
+  // job; JobTimedOutApplier -> DbJobState.timeout (:142-150): ACTIVATABLE again, the record (deadline,
+  // worker) kept, out of JOB_DEADLINES.  Else NOT_FOUND "Expected to time out activated job with key
+  // '%d', but %s".  (publishWork's notification / push is a side effect; no stream: no records.)
+  void time_out_job(ORecord& cmd) {
+    if (cmd.job_ord >= 0) cmd.r.key = resolve(cmd.instance, (uint32_t)cmd.job_ord);
+    const int64_t jobKey = cmd.r.key;
+    auto jit = jobs_.find(jobKey);
+    const char* why = jit == jobs_.end() ? "no such job was found"
+                      : !jit->second.activated ? "it must be activated first"
+                      : !(jit->second.deadline < now_ms) ? "it has not timed out" : nullptr;
+    if (why) {
+      reject(cmd, ZBHIP_REJ_NOT_FOUND,
+             "Expected to time out activated job with key '" + std::to_string(jobKey) + "', but " + why);
+      return;
+    }
+    JobRow& job = jit->second;
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_TIMED_OUT, jobKey);
+    rec.r.process_idx = job.pi.proc;
+    rec.r.element_idx = job.pi.elem;
+    rec.r.scope_key = job.elementInstanceKey;
+    rec.r.process_instance_key = job.pi.piKey;
+    job_activation_fields(rec, job);
+    job.activated = false;
+    activatable_.insert({job.type, "<default>", jobKey});
+  }
+
+  // the stored job's deadline and worker (DbJobState.activate wrote them; a timed-out job keeps
+  // them): the zbhip_record fields message_key / correlation_key of a JOB record
   void job_activation_fields(ORecord& rec, const JobRow& job) {
-    if (!job.activated) return;
+    if (job.deadline == -1 && job.worker.empty()) return;
     rec.r.message_key = job.deadline;
     rec.r.correlation_key = job.worker.empty() ? ZBHIP_NO_STRING : intern_string(job.worker);
   }

@@ -15,6 +15,11 @@ the RecordProcessor interface.
   one command) as a RecordProcessor, with the partition's key generator (DbKeyGenerator) and the
   RawDbWriter of a hand-off (import_rows).
 * :class:`Client` -- the EngineRule test clients writing commands to the log.
+* :class:`Clock` / :class:`ScheduleService` and the checkers -- ActorClock under test control
+  (EngineRule.increaseTime) and ProcessingScheduleServiceImpl: tasks run between batches, a task's
+  commands are written to the log as one batch; DueDateChecker / DueDateTimerChecker, JobTimeoutTrigger,
+  PendingProcessMessageSubscriptionChecker and MessageObserver's PendingMessageSubscriptionChecker
+  restated over a state view (the engine's, or the adapter's merged device + engine view).
 
 Only tests use this module (it loads the oracle)."""
 import numpy as np
@@ -160,6 +165,318 @@ def oracle_tables(o):
     return out
 
 
+class Clock:
+    """ActorClock (the controlled clock of EngineRule: increaseTime)."""
+
+    def __init__(self, now=0):
+        self.now = now
+
+    def __call__(self):
+        return self.now
+
+
+class TaskResultBuilder:
+    """stream-platform's TaskResultBuilder: appendCommandRecord(key, intent, value) of a scheduled task."""
+
+    def __init__(self):
+        self.records = []
+
+    def append_command_record(self, key, value_type, intent, value):
+        self.records.append(Rec(abi.RT_COMMAND, value_type, intent, key, value))
+        return True
+
+
+class ScheduleService:
+    """ProcessingScheduleServiceImpl (stream-platform/.../scheduling/ProcessingScheduleServiceImpl.java):
+    runDelayed / runAtFixedRate on the partition's actor; a task's result (its commands) is written to
+    the log as one batch without a source position.  run_due() runs the tasks due at the clock's time,
+    earliest first (same time: scheduling order)."""
+
+    def __init__(self, clock, log):
+        self.clock, self.log = clock, log
+        self.tasks = []
+        self.seq = 0
+
+    def run_delayed(self, delay, task):
+        self.seq += 1
+        self.tasks.append((self.clock.now + max(delay, 0), self.seq, task, None))
+
+    def run_at_fixed_rate(self, delay, runnable):
+        self.seq += 1
+        self.tasks.append((self.clock.now + delay, self.seq, runnable, delay))
+
+    def next_due(self):
+        return min((t[0], t[1]) for t in self.tasks) if self.tasks else None
+
+    def run_one(self):
+        """Runs the earliest due task; False when none is due."""
+        due = [t for t in self.tasks if t[0] <= self.clock.now]
+        if not due:
+            return False
+        t = min(due, key=lambda x: (x[0], x[1]))
+        self.tasks.remove(t)
+        _, _, task, rate = t
+        if rate is not None:  # a Runnable at fixed rate: no result, rescheduled
+            task()
+            self.seq += 1
+            self.tasks.append((self.clock.now + rate, self.seq, task, rate))
+            return True
+        builder = TaskResultBuilder()
+        task(builder)
+        self.log.append(builder.records)
+        return True
+
+
+class DueDateTimerChecker:
+    """DueDateTimerChecker + DueDateChecker (engine/.../processing/timer/DueDateTimerChecker.java:24-130,
+    processing/scheduled/DueDateChecker.java): one task for all timers, scheduled at the earliest known
+    dueDate (TIMER_RESOLUTION 100 ms floor); it writes TIMER:TRIGGER for every timer due (key = the
+    timer, the TimerInstance's TimerRecord) and reschedules itself at the first dueDate left."""
+    TIMER_RESOLUTION = 100
+
+    def __init__(self, timer_state, clock):
+        self.state, self.clock = timer_state, clock
+        self.service = None
+        self.running = False
+        self.next_due = -1
+
+    def on_recovered(self, service):
+        self.service = service
+        service.run_delayed(0, self._task)  # timers due after a restart
+
+    def _delay(self, due):
+        return max(due - self.clock.now, self.TIMER_RESOLUTION)
+
+    def schedule_timer(self, due):
+        if not self.running:
+            self.service.run_delayed(self._delay(due), self._task)
+            self.next_due, self.running = due, True
+        elif self.next_due - due > self.TIMER_RESOLUTION:
+            self.service.run_delayed(self._delay(due), self._task)
+            self.next_due = due
+
+    def _task(self, builder):
+        def visit(key, value):
+            return builder.append_command_record(key, abi.VT_TIMER, abi.TIMER_TRIGGER, dict(value))
+        self.next_due = self.state.process_timers_with_due_date_before(self.clock.now, visit)
+        if self.next_due > 0:
+            self.service.run_delayed(self._delay(self.next_due), self._task)
+            self.running = True
+        else:
+            self.running = False
+
+
+class JobTimeoutTrigger:
+    """JobTimeoutTrigger (engine/.../processing/job/JobTimeoutTrigger.java:21-88): every 30 s, JOB:TIME_OUT
+    for each job in JOB_DEADLINES with deadline < now (key = the job, value = the stored job)."""
+    INTERVAL = 30000
+
+    def __init__(self, job_state, clock):
+        self.state, self.clock = job_state, clock
+
+    def on_recovered(self, service):
+        self.service = service
+        service.run_delayed(self.INTERVAL, self._task)
+
+    def _task(self, builder):
+        self.state.for_each_timed_out_entry(
+            self.clock.now, lambda key, value: builder.append_command_record(key, abi.VT_JOB, abi.JOB_TIME_OUT, dict(value)))
+        self.service.run_delayed(self.INTERVAL, self._task)
+
+
+def open_message_subscription_value(r):
+    """SubscriptionCommandSender.sendDirectOpenMessageSubscription (:83-110) from the stored
+    ProcessMessageSubscriptionRecord."""
+    return {"processInstanceKey": r["processInstanceKey"], "elementInstanceKey": r["elementInstanceKey"],
+            "messageKey": -1, "messageName": r["messageName"], "correlationKey": r["correlationKey"],
+            "interrupting": r["interrupting"], "bpmnProcessId": r["bpmnProcessId"], "variables": (),
+            "tenantId": "<default>"}
+
+
+def close_message_subscription_value(r):
+    """SubscriptionCommandSender.sendDirectCloseMessageSubscription (:236-264)."""
+    return {"processInstanceKey": r["processInstanceKey"], "elementInstanceKey": r["elementInstanceKey"],
+            "messageKey": -1, "messageName": r["messageName"], "correlationKey": "", "interrupting": True,
+            "bpmnProcessId": "", "variables": (), "tenantId": "<default>"}
+
+
+def correlate_process_message_subscription_value(r, sender):
+    """SubscriptionCommandSender.sendDirectCorrelateProcessMessageSubscription (:160-198)."""
+    return {"subscriptionPartitionId": sender, "processInstanceKey": r["processInstanceKey"],
+            "elementInstanceKey": r["elementInstanceKey"], "messageKey": r["messageKey"],
+            "messageName": r["messageName"], "variables": tuple(r.get("variables", ())), "interrupting": True,
+            "bpmnProcessId": r["bpmnProcessId"], "correlationKey": r["correlationKey"], "elementId": "",
+            "tenantId": "<default>"}
+
+
+class PendingProcessMessageSubscriptionChecker:
+    """PendingProcessMessageSubscriptionChecker (engine/.../message/PendingProcessMessageSubscriptionChecker
+    .java:20-129): every 30 s, subscriptions still OPENING / CLOSING 10 s after they were last sent are
+    sent again directly (MESSAGE_SUBSCRIPTION:CREATE / DELETE to the subscription partition)."""
+    TIMEOUT, INTERVAL = 10000, 30000
+
+    def __init__(self, pending, clock, sender):
+        self.pending, self.clock, self.sender = pending, clock, sender
+
+    def on_recovered(self, service):
+        self.service = service
+        service.run_delayed(self.INTERVAL, self._task)
+
+    def _task(self, builder):
+        for _, sub, r, opening in self.pending.pending_process_message_subscriptions(self.clock.now - self.TIMEOUT):
+            if opening:
+                self.sender.send_command(r["subscriptionPartitionId"], abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_CREATE,
+                                         open_message_subscription_value(r))
+            else:
+                self.sender.send_command(r["subscriptionPartitionId"], abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_DELETE,
+                                         close_message_subscription_value(r))
+            self.pending.on_sent_pms(sub, self.clock.now)
+        self.service.run_delayed(self.INTERVAL, self._task)
+
+
+class PendingMessageSubscriptionChecker:
+    """MessageObserver's PendingMessageSubscriptionChecker (engine/.../message/MessageObserver.java:61-73,
+    PendingMessageSubscriptionChecker.java:15-57): at a fixed rate of 30 s, CORRELATING subscriptions
+    last sent 10 s ago or earlier are correlated again (PROCESS_MESSAGE_SUBSCRIPTION:CORRELATE to the
+    process instance's partition)."""
+    TIMEOUT, INTERVAL = 10000, 30000
+
+    def __init__(self, pending, clock, sender, partition_id):
+        self.pending, self.clock, self.sender, self.partition_id = pending, clock, sender, partition_id
+
+    def on_recovered(self, service):
+        service.run_at_fixed_rate(self.INTERVAL, self.run)
+
+    def run(self):
+        for _, sub, r in self.pending.pending_message_subscriptions(self.clock.now - self.TIMEOUT):
+            self.sender.send_command(r["processInstanceKey"] >> 51, abi.VT_PROCESS_MESSAGE_SUBSCRIPTION,
+                                     abi.PMS_CORRELATE, correlate_process_message_subscription_value(r, self.partition_id))
+            self.pending.on_sent_ms(sub, self.clock.now)
+
+
+def _row_fields(text):
+    out = {}
+    for kv in text.split(","):
+        k, _, v = kv.partition("=")
+        out[k] = v
+    return out
+
+
+class EngineTimerState:
+    """The engine's TimerInstanceState (its TIMERS / TIMER_DUE_DATES rows): due(now) -> [(dueDate,
+    elementInstanceKey, key, TimerRecord)], next_after(now); process_timers_with_due_date_before for the
+    engine-only loop."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def _timers(self):
+        out = []
+        for r in self.engine.state():
+            if r.startswith("TIMERS|"):
+                _, eik, key, f = r.split("|", 3)
+                f = _row_fields(f)
+                out.append((int(f["dueDate"]), int(eik), int(key),
+                            {"elementInstanceKey": int(eik), "processInstanceKey": int(f["processInstanceKey"]),
+                             "dueDate": int(f["dueDate"]), "repetitions": int(f["repetitions"]),
+                             "targetElementId": f["handlerNodeId"],
+                             "processDefinitionKey": int(f["processDefinitionKey"]), "tenantId": "<default>"}))
+        return sorted(out, key=lambda t: t[:3])
+
+    def due(self, now):
+        return [t for t in self._timers() if t[0] <= now]
+
+    def next_after(self, now):
+        later = [t[0] for t in self._timers() if t[0] > now]
+        return min(later) if later else -1
+
+    def process_timers_with_due_date_before(self, now, visitor):
+        for due, _, key, value in self._timers():
+            if due > now or not visitor(key, value):
+                return due
+        return -1
+
+
+class EngineJobState:
+    """The engine's JobState (JOBS / JOB_STATES / JOB_DEADLINES rows): timed_out(now) -> [(deadline, key,
+    JobRecord)]; for_each_timed_out_entry for the engine-only loop."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def timed_out(self, now):
+        rows = self.engine.state()
+        jobs = {}
+        for r in rows:
+            if r.startswith("JOBS|"):
+                _, key, f = r.split("|", 2)
+                jobs[int(key)] = _row_fields(f)
+        out = []
+        for r in rows:
+            if r.startswith("JOB_DEADLINES|"):
+                _, deadline, key = r.split("|")
+                deadline, key = int(deadline), int(key)
+                if deadline < now:
+                    f = jobs[key]
+                    out.append((deadline, key, {
+                        "tenantId": "<default>", "variables": (), "type": f["type"], "retries": int(f["retries"]),
+                        "elementId": f["elementId"], "elementInstanceKey": int(f["elementInstanceKey"]),
+                        "processInstanceKey": int(f["processInstanceKey"]), "bpmnProcessId": f["bpmnProcessId"],
+                        "processDefinitionVersion": int(f["processDefinitionVersion"]),
+                        "processDefinitionKey": int(f["processDefinitionKey"]), "deadline": int(f["deadline"]),
+                        "worker": f["worker"]}))
+        return sorted(out, key=lambda t: t[:2])
+
+    def for_each_timed_out_entry(self, now, callback):
+        for _, key, value in self.timed_out(now):
+            if not callback(key, value):
+                return
+
+
+class PendingStates:
+    """The engine's TransientPendingSubscriptionState pair, kept by its appliers (DbProcessMessage
+    SubscriptionState.java:82-124,180-222, DbMessageSubscriptionState.java:157-222): OPENING / CLOSING
+    process message subscriptions and CORRELATING message subscriptions with their last sent time."""
+
+    def __init__(self, clock):
+        self.clock = clock
+        self.pms, self.ms = {}, {}
+
+    def track(self, rt, vt, it, value):
+        if rt != abi.RT_EVENT:
+            return
+        if vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION:
+            sub = (value["elementInstanceKey"], value["messageName"])
+            if it in (abi.PMS_CREATING, abi.PMS_DELETING):
+                self.pms[sub] = [self.clock.now, dict(value), it == abi.PMS_CREATING]
+            elif it in (abi.PMS_CREATED, abi.PMS_DELETED, abi.PMS_CORRELATED):
+                self.pms.pop(sub, None)
+        elif vt == abi.VT_MESSAGE_SUBSCRIPTION:
+            sub = (value["elementInstanceKey"], value["messageName"])
+            if it == abi.MS_CORRELATING:
+                self.ms[sub] = [self.clock.now, dict(value)]
+            elif it in (abi.MS_CORRELATED, abi.MS_DELETED):
+                self.ms.pop(sub, None)
+
+    def pending_process_message_subscriptions(self, deadline):
+        return sorted(((t, sub, r, op) for sub, (t, r, op) in self.pms.items() if t < deadline), key=lambda x: x[0])
+
+    def add_pms(self, sub, sent, record, opening):
+        """TransientPendingSubscriptionState.add of a subscription whose row came in with a hand-off."""
+        self.pms[sub] = [sent, record, opening]
+
+    def pending_message_subscriptions(self, deadline):
+        return sorted(((t, sub, r) for sub, (t, r) in self.ms.items() if t < deadline), key=lambda x: x[0])
+
+    def on_sent_pms(self, sub, when):
+        if sub in self.pms:
+            self.pms[sub][0] = when
+
+    def on_sent_ms(self, sub, when):
+        if sub in self.ms:
+            self.ms[sub][0] = when
+
+
 class OracleEngine:
     """The reference engine as a RecordProcessor (Engine.java:71-131), one command per process call;
     also the partition's DbKeyGenerator (KeyGeneratorControls) and the RawDbWriter of a hand-off."""
@@ -171,7 +488,10 @@ class OracleEngine:
         self.o = Oracle(partition_id=partition_id, partition_count=partition_count,
                         max_commands_in_batch=max_commands_in_batch)
         self.command_sender = command_sender  # InterPartitionCommandSender of config 5
-        self.o.set_clock(clock)
+        self.clock = clock if isinstance(clock, Clock) else None  # a controlled ActorClock, or a fixed time
+        self.o.set_clock(clock.now if self.clock else clock)
+        self.due_date_checker = None  # DueDateTimerChecker.scheduleTimer (TIMER:CREATED side effects)
+        self.pending = PendingStates(self.clock or Clock(clock))
         self.pbits = partition_id << 51
         self.slot_of = {}
         self.next_slot = 0
@@ -272,6 +592,8 @@ class OracleEngine:
         base = len(self.doc_values)
         self.doc_values.extend(val for _, val in variables)
         self.o.clear_records()
+        if self.clock:
+            self.o.set_clock(self.clock.now)
         self.o.process_one(r, slot, docs, record.position or 0, len(out.entries))
         recs = self.o.records()
         for k, x in enumerate(recs):
@@ -279,11 +601,14 @@ class OracleEngine:
             if rt == abi.RT_REJECTION and k == 0 and xvt == vt and xit == it:
                 value = dict(v)  # TypedRejectionWriter: the command's value
             else:
-                value = self.values.value(x, variables, lambda aux: self.doc_values[aux])
+                value = self.values.value(x, variables, lambda aux: self.doc_values[aux], record.timestamp)
             if xvt == abi.VT_PROCESS_INSTANCE_CREATION:
                 self.slot_of[int(x["scope_key"])] = slot
             out.append_record(int(x["key"]), rt, xvt, xit, int(x["rejection_type"]),
                               self.o.reason(k) if rt == abi.RT_REJECTION else "", value)
+            self.pending.track(rt, xvt, xit, value)
+            if rt == abi.RT_EVENT and xvt == abi.VT_TIMER and xit == abi.TIMER_CREATED and self.due_date_checker:
+                out.append_post_commit_task(lambda d=value["dueDate"]: self.due_date_checker.schedule_timer(d) or True)
         sends = self.o.outbox()  # SubscriptionCommandSender's side effects of this command
         if len(sends):
             strings = self.o.strings()
@@ -319,7 +644,7 @@ class Client:
 
     def write(self, *recs):
         for log in self.logs:
-            log.append([Rec(r.record_type, r.value_type, r.intent, r.key, r.value) for r in recs])
+            log.append([Rec(r.record_type, r.value_type, r.intent, r.key, r.value, timestamp=r.timestamp) for r in recs])
 
     @staticmethod
     def create(bpmn_process_id, variables=(), key=-1):
@@ -333,16 +658,12 @@ class Client:
                                                                        "tenantId": "<default>"})
 
     @staticmethod
-    def trigger_timer(created):
-        """DueDateTimerChecker's TIMER:TRIGGER: the timer's TimerRecord (DueDateTimerChecker.java:118-125)."""
-        return Rec(abi.RT_COMMAND, abi.VT_TIMER, abi.TIMER_TRIGGER, created.key, dict(created.value))
-
-    @staticmethod
-    def publish_message(name, correlation_key):
-        """MessageClient.publish with time-to-live 0 (MessageRecord.java:37-43)."""
+    def publish_message(name, correlation_key, timestamp=0):
+        """MessageClient.publish with time-to-live 0 (MessageRecord.java:37-43); `timestamp` = the
+        command's record timestamp (the broker's clock when it was written)."""
         return Rec(abi.RT_COMMAND, abi.VT_MESSAGE, abi.MSG_PUBLISH, -1,
                    {"name": name, "correlationKey": correlation_key, "timeToLive": 0, "variables": (), "messageId": "",
-                    "deadline": -1, "tenantId": "<default>"})
+                    "deadline": -1, "tenantId": "<default>"}, timestamp=timestamp)
 
     @staticmethod
     def activate_jobs(job_type, worker="w", timeout=300000, max_jobs=10, timestamp=0):
@@ -359,17 +680,6 @@ def open_jobs(log):
             if r.intent == abi.JOB_CREATED:
                 alive[r.key] = r
             elif r.intent in (abi.JOB_COMPLETED, abi.JOB_CANCELED):
-                alive.pop(r.key, None)
-    return alive
-
-
-def open_timers(log):
-    alive = {}
-    for r in log.entries:
-        if r.value_type == abi.VT_TIMER and r.record_type == abi.RT_EVENT:
-            if r.intent == abi.TIMER_CREATED:
-                alive[r.key] = r
-            elif r.intent in (abi.TIMER_TRIGGERED, abi.TIMER_CANCELED):
                 alive.pop(r.key, None)
     return alive
 

@@ -15,8 +15,7 @@ engine's state (on_recovered -> zbhip_import_state)."""
 import numpy as np
 import pytest
 
-from psm import Client, Log, OracleEngine, StreamProcessor, open_jobs, open_timers
-from test_oracle_boundary import cycle_process, multiple_sequence_flows
+from psm import Client, Log, OracleEngine, StreamProcessor, open_jobs
 from test_oracle_timers import NOW
 from zeebe_amd import abi, bpmn
 from zeebe_amd.adapter import GpuBatchProcessor
@@ -144,31 +143,6 @@ def test_fallback_hand_off_in_the_processing_loop():
             recs.append(Client.complete_job(stale.key))
         phase(ref, mixed, recs + [Client.create("linear")])
     assert mixed.adapter.handed_off
-
-
-def test_boundary_timers_and_rejections_in_the_processing_loop():
-    # timer boundary events: some timers fire (TIMER:TRIGGER with the DueDateTimerChecker's full
-    # TimerRecord), some jobs complete first -- a trigger of a canceled timer is rejected NOT_FOUND and
-    # the rejection carries the command's TimerRecord (TypedRejectionWriter); a non-interrupting cycle
-    deps = [(multiple_sequence_flows("PT30S"), KEY_A, 1), (cycle_process("R3/PT10S"), KEY_B, 1)]
-    ref, mixed = Ref(deps, 100), Mixed(deps, deps, 100)
-    phase(ref, mixed, [Client.create("process", key=KEY_A if k % 2 else KEY_B) for k in range(24)])
-    rng = np.random.default_rng(9)
-    for _ in range(6):
-        timers = open_timers(ref.log)
-        jobs = open_jobs(ref.log)
-        if not timers and not jobs:
-            break
-        recs = []
-        for k in sorted(jobs):
-            if rng.integers(0, 2):
-                recs.append(Client.complete_job(k))
-        for k in sorted(timers):
-            recs.append(Client.trigger_timer(timers[k]))  # after a completion of its task: NOT_FOUND
-        rng.shuffle(recs)
-        phase(ref, mixed, recs)
-    rejected = [r for r in mixed.log.entries if r.record_type == abi.RT_REJECTION and r.value_type == abi.VT_TIMER]
-    assert rejected and all(r.value["elementInstanceKey"] > 0 and r.value["targetElementId"] for r in rejected)
 
 
 def test_restart_imports_device_instances():

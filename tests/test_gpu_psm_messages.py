@@ -102,10 +102,16 @@ def test_message_correlation_on_three_partitions_in_the_processing_loop():
     # a message nobody waits for (published and expired), then one message per subscription, each on
     # its key's subscription partition (SubscriptionUtil.getSubscriptionPartitionId)
     from oracle.oracle import subscription_partition
-    pubs = {p: [Client.publish_message("message", "nobody")] for p in range(1, P + 1)}
-    for k in KEYS:
-        pubs[subscription_partition(k, P)] += [Client.publish_message("message", k) for _ in range(3)]
+    # (the commands carry a broker timestamp: MESSAGE records' deadline = timestamp + timeToLive,
+    # MessagePublishProcessor.java:110)
+    pubs = {p: [Client.publish_message("message", "nobody", timestamp=1700000000000 + p)] for p in range(1, P + 1)}
+    for j, k in enumerate(KEYS):
+        pubs[subscription_partition(k, P)] += [Client.publish_message("message", k, timestamp=1700000000100 + 7 * j + n)
+                                               for n in range(3)]
     phase(ref, gpu, sorted(pubs.items()))
+    published = [r for p in range(1, P + 1) for r in gpu.logs[p].entries
+                 if r.value_type == abi.VT_MESSAGE and r.intent == abi.MSG_PUBLISHED]
+    assert len(published) == 33 and all(r.value["deadline"] >= 1700000000000 for r in published)
     done = sum(1 for p in range(1, P + 1) for r in gpu.logs[p].entries
                if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == 5
                and r.value["bpmnElementType"] == "PROCESS")

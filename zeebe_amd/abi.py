@@ -35,8 +35,10 @@ PI_INTENTS = {
 }
 PI_INTENT_IDS = {v: k for k, v in PI_INTENTS.items()}
 PI_SEQUENCE_FLOW_TAKEN, PI_ELEMENT_ACTIVATING, PI_ELEMENT_ACTIVATED = 1, 2, 3
-JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED", 10: "CANCELED"}
+JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED", 3: "TIME_OUT", 4: "TIMED_OUT", 5: "FAIL", 6: "FAILED",
+               10: "CANCELED"}
 JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED, JOB_CANCELED = 0, 1, 2, 10
+JOB_TIME_OUT, JOB_TIMED_OUT, JOB_FAIL, JOB_FAILED = 3, 4, 5, 6
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
 PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
 PIC_INTENTS = {0: "CREATE", 1: "CREATED"}

@@ -144,7 +144,8 @@ class RecordValues:
         self.name = name
         self.string_value = string_value  # value-dictionary id -> str (inline STR values)
 
-    def value(self, r, command_doc=(), entry_value=None):
+    def value(self, r, command_doc=(), entry_value=None, timestamp=0):
+        """`timestamp`: the source command's (a MESSAGE record's deadline = timestamp + timeToLive)."""
         vt = int(r["value_type"])
         p = self.procs[max(int(r["process_idx"]), 0)] if self.procs else None
         elem = int(r["element_idx"])
@@ -195,7 +196,7 @@ class RecordValues:
             corr = self.string_value(cid) if cid != abi.NO_STRING else ""
             if vt == abi.VT_MESSAGE:  # MessageRecord.java:37-43
                 return {"name": nm, "correlationKey": corr, "timeToLive": 0, "variables": (), "messageId": "",
-                        "deadline": 0, "tenantId": TENANT}
+                        "deadline": timestamp, "tenantId": TENANT}
             bpmn = self.name(bid) if bid != 0xFFFF else ""
             common = {"processInstanceKey": pik, "elementInstanceKey": scope, "messageKey": int(r["message_key"]),
                       "messageName": nm, "correlationKey": corr, "interrupting": bool(r["interrupting"]),
@@ -225,6 +226,76 @@ class RecordValues:
                         "tenantId": TENANT})
         v.update({"jobKeys": tuple(int(j["key"]) for j in jobs), "jobs": tuple(out), "truncated": False})
         return v
+
+
+class DeviceTimerInstanceState:
+    """The TimerInstanceState the platform's DueDateTimerChecker reads behind the adapter: the engine's
+    timers (RocksDB) and the device's (zbhip_due_timers), merged in TIMER_DUE_DATES order [dueDate,
+    [elementInstanceKey, timerKey]] -- DbTimerInstanceState.processTimersWithDueDateBefore (:87-116) over
+    both.  `engine` provides due(now) -> [(dueDate, elementInstanceKey, key, TimerRecord)] and
+    next_after(now) (the Java adapter wraps the engine's DbTimerInstanceState the same way)."""
+
+    def __init__(self, adapter, engine):
+        self.adapter, self.engine = adapter, engine
+
+    def process_timers_with_due_date_before(self, now, visitor):
+        if not self.adapter.scheduled_ready():
+            return now  # mid-window: look again after the timer resolution
+        dev, dev_next = self.adapter.due_timers(now)
+        both = sorted([(v["dueDate"], v["elementInstanceKey"], k, v) for k, v in dev] + list(self.engine.due(now)),
+                      key=lambda t: t[:3])
+        for due, _, key, value in both:
+            if not visitor(key, value):
+                return due
+        later = [d for d in (dev_next, self.engine.next_after(now)) if d >= 0]
+        return min(later) if later else -1
+
+
+class DeviceJobState:
+    """The JobState JobTimeoutTrigger reads behind the adapter: the engine's JOB_DEADLINES and the
+    device's activated jobs (zbhip_timed_out_jobs), merged in [deadline, jobKey] order --
+    DbJobState.forEachTimedOutEntry (:286-298) over both.  `engine` provides timed_out(now) ->
+    [(deadline, jobKey, JobRecord)]."""
+
+    def __init__(self, adapter, engine):
+        self.adapter, self.engine = adapter, engine
+
+    def for_each_timed_out_entry(self, now, callback):
+        dev = self.adapter.timed_out_jobs(now) if self.adapter.scheduled_ready() else []
+        for _, key, value in sorted(dev + list(self.engine.timed_out(now)), key=lambda t: t[:2]):
+            if not callback(key, value):
+                return
+
+
+class DevicePendingSubscriptionState:
+    """The pending-subscription states the platform's PendingProcessMessageSubscriptionChecker and
+    PendingMessageSubscriptionChecker (MessageObserver) read behind the adapter: the engine's transient
+    states and the device's (kept by the adapter from the device's records), visited by last sent time
+    (TransientPendingSubscriptionState.entriesBefore): the engine's entries, then the device's, each
+    group by last sent time (DeviceScheduledState.java: the engine's visitPending exposes no times).
+    `engine` provides the same four calls."""
+
+    def __init__(self, adapter, engine):
+        self.adapter, self.engine = adapter, engine
+
+    def pending_process_message_subscriptions(self, deadline):
+        for sub, entry in self.adapter.moved_pending:  # handed-off instances: the engine's now
+            self.engine.add_pms(sub, *entry)
+        self.adapter.moved_pending.clear()
+        dev = self.adapter.pending_process_message_subscriptions(deadline) if self.adapter.scheduled_ready() else []
+        return self.engine.pending_process_message_subscriptions(deadline) + dev
+
+    def pending_message_subscriptions(self, deadline):
+        dev = self.adapter.pending_message_subscriptions(deadline) if self.adapter.scheduled_ready() else []
+        return self.engine.pending_message_subscriptions(deadline) + dev
+
+    def on_sent_pms(self, sub, when):
+        self.adapter.on_sent_pms(sub, when)
+        self.engine.on_sent_pms(sub, when)
+
+    def on_sent_ms(self, sub, when):
+        self.adapter.on_sent_ms(sub, when)
+        self.engine.on_sent_ms(sub, when)
 
 
 class Window:
@@ -326,6 +397,11 @@ class GpuBatchProcessor:
                                        # subscription (its PROCESS_MESSAGE_SUBSCRIPTION:DELETE may come late)
         self.next_free = 0
         self.window = Window()
+        self._window_done = True       # every command of the current window was emitted
+        self.due_date_checker = None   # DueDateTimerChecker.scheduleTimer of the platform (side effects)
+        self.pending_pms = {}          # (elementInstanceKey, messageName) -> [sent time, record, opening]
+        self.pending_ms = {}           # (elementInstanceKey, messageName) -> [sent time, record]
+        self.moved_pending = []        # pending entries of handed-off instances, for the engine's state
         self.handed_off = set()
         self.followups = 0             # follow-ups of the current device batch the platform feeds back
         self.engine_batch = False      # the current batch's initial command went to the engine
@@ -336,7 +412,7 @@ class GpuBatchProcessor:
         # what went where (tests read these)
         self.fallback_reasons = []
         self.counts = {"windows": 0, "device_commands": 0, "continuations": 0, "fallbacks": 0, "activations": 0,
-                       "engine_commands": 0, "followups_answered": 0}
+                       "engine_commands": 0, "followups_answered": 0, "time_outs": 0}
 
     # ---- RecordProcessor ----------------------------------------------------------------------
     def init(self):
@@ -416,6 +492,8 @@ class GpuBatchProcessor:
         if record.value_type == VT_JOB_BATCH and record.intent == JOB_BATCH_ACTIVATE \
                 and record.value["type"] not in self.engine_job_types:
             return self._activate_jobs(record, out)
+        if record.value_type == abi.VT_JOB and record.intent == abi.JOB_TIME_OUT and self._resolve(record.key) is not None:
+            return self._time_out_job(record, out)
         i = self.window.index_of(record.position) if self.window.covers(record.position) else -1
         if i < 0:
             if not self._hot(record, 0):
@@ -433,6 +511,7 @@ class GpuBatchProcessor:
         if i < 0:
             self.engine_batch = True
             return self.engine.process(record, out)
+        self._window_done = i == self.window.size() - 1
         st, why = self.part.command_status(i)
         if st != 0:
             self.counts["fallbacks"] += 1
@@ -624,6 +703,7 @@ class GpuBatchProcessor:
                 xparts[j] = x
         self.part.submit(cmds, docs, xparts)
         self.doc_total += len(docs)
+        self._window_done = False
         self.part.run()
         # the records are drained command by command as the platform reaches them
         # (zbhip_drain_command): a fallback command's CPU-engine keys come before the later ones
@@ -655,9 +735,16 @@ class GpuBatchProcessor:
             if rt == abi.RT_REJECTION and int(r["ordinal"]) == 0 and vt == record.value_type and it == record.intent:
                 value = dict(record.value)
             else:
-                value = self.values.value(r, cmd_doc, lambda aux: win.doc_values[aux - win.doc_base])
+                value = self.values.value(r, cmd_doc, lambda aux: win.doc_values[aux - win.doc_base],
+                                          getattr(record, "timestamp", 0))
             reason = self.part.reason(r) if rt == abi.RT_REJECTION else ""
             out.append_record(int(r["key"]), rt, vt, it, int(r["rejection_type"]), reason, value)
+            if self.correlation_keys > 0:
+                self._track_pending(rt, vt, it, value)
+            if rt == abi.RT_EVENT and vt == abi.VT_TIMER and it == abi.TIMER_CREATED and self.due_date_checker:
+                due = value["dueDate"]
+                # CatchEventBehavior.subscribeToTimerEvent's side effect: timerChecker.scheduleTimer(dueDate)
+                out.append_post_commit_task(lambda d=due: self.due_date_checker.schedule_timer(d) or True)
             if rt == abi.RT_COMMAND:
                 if r["unprocessed"]:
                     # a continuation (its id in aux): expected back from the log in the order written
@@ -687,6 +774,68 @@ class GpuBatchProcessor:
         self.followups = admitted
         if self.correlation_keys > 0:
             self._send(i, out)
+
+    # ---- the engine's scheduled tasks over device-held state -------------------
+    def scheduled_ready(self):
+        """The device state equals the log's: every command of the current window was emitted (the
+        platform runs scheduled tasks between batches; mid-window the device is ahead of the log, so a
+        check waits for the window's end -- a later run of the checker, which the reference's actor
+        scheduling allows)."""
+        return self._window_done
+
+    def due_timers(self, now):
+        """TimerInstanceState.processTimersWithDueDateBefore over the device: [(timer key, TimerRecord)]
+        in TIMER_DUE_DATES order, and the first later dueDate (-1 none)."""
+        rows, nxt = self.part.due_timers(now)
+        return [(int(r["key"]), self.values.value(r)) for r in rows], nxt
+
+    def timed_out_jobs(self, now):
+        """JobState.forEachTimedOutEntry over the device's activated jobs: [(job key, JobRecord)] in
+        JOB_DEADLINES order (with the deadline: the merge key)."""
+        return [(int(r["message_key"]), int(r["key"]), self.values.value(r)) for r in self.part.timed_out_jobs(now)]
+
+    def _track_pending(self, rt, vt, it, value):
+        """The transient pending-subscription states the appliers of the device's records keep in the
+        reference (DbProcessMessageSubscriptionState.java:82-124,180-222, DbMessageSubscriptionState.java
+        :157-222, TransientPendingSubscriptionState): the PI side's OPENING / CLOSING subscriptions and the
+        message side's CORRELATING ones, with the time they were last sent."""
+        if rt != abi.RT_EVENT:
+            return
+        now = self.clock()
+        if vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION:
+            sub = (value["elementInstanceKey"], value["messageName"])
+            if it == abi.PMS_CREATING:  # put: OPENING
+                self.pending_pms[sub] = [now, dict(value), True]
+            elif it == abi.PMS_DELETING:
+                self.pending_pms[sub] = [now, dict(value), False]  # updateToClosingState
+            elif it in (abi.PMS_CREATED, abi.PMS_DELETED, abi.PMS_CORRELATED):
+                self.pending_pms.pop(sub, None)
+        elif vt == abi.VT_MESSAGE_SUBSCRIPTION:
+            sub = (value["elementInstanceKey"], value["messageName"])
+            if it == abi.MS_CORRELATING:  # updateToCorrelatingState
+                self.pending_ms[sub] = [now, dict(value)]
+            elif it in (abi.MS_CORRELATED, abi.MS_DELETED):
+                self.pending_ms.pop(sub, None)
+
+    def pending_process_message_subscriptions(self, deadline):
+        """PendingProcessMessageSubscriptionState.visitPending: the device's OPENING / CLOSING
+        subscriptions last sent before `deadline`, ordered by that time: [(time, sub, record, opening)]."""
+        due = sorted(((t, sub) for sub, (t, _, _) in self.pending_pms.items() if t < deadline), key=lambda x: x[0])
+        return [(t, sub, self.pending_pms[sub][1], self.pending_pms[sub][2]) for t, sub in due]
+
+    def pending_message_subscriptions(self, deadline):
+        """PendingMessageSubscriptionState.visitPending: the CORRELATING subscriptions of the device's
+        correlation slots last sent before `deadline`: [(time, sub, record)]."""
+        due = sorted(((t, sub) for sub, (t, _) in self.pending_ms.items() if t < deadline), key=lambda x: x[0])
+        return [(t, sub, self.pending_ms[sub][1]) for t, sub in due]
+
+    def on_sent_pms(self, sub, when):
+        if sub in self.pending_pms:
+            self.pending_pms[sub][0] = when
+
+    def on_sent_ms(self, sub, when):
+        if sub in self.pending_ms:
+            self.pending_ms[sub][0] = when
 
     # ---- keys ------------------------------------------------------------------------------------
     def _batch_done(self):
@@ -733,6 +882,25 @@ class GpuBatchProcessor:
             self.continuations = [c for c in self.continuations if c[1] != inst]
             self.used_slots.discard(inst)
             self.ended.discard(inst)
+            # its subscriptions are the engine's now: no closing row holds the slot, no routing handle
+            # points into it, and their pending entries move to the engine's transient state
+            self.closing.discard(inst)
+            for sub in [k for k, v in self.pms_handles.items() if v is not None and v[0] == inst]:
+                del self.pms_handles[sub]
+                if sub in self.pending_pms:
+                    self.moved_pending.append((sub, self.pending_pms.pop(sub)))
+
+    # ---- JOB:TIME_OUT of a device job (JobTimeOutProcessor.java:46-73) ------------------------------
+    def _time_out_job(self, record, out):
+        self.counts["time_outs"] += 1
+        r = self.part.time_out_job(record.key, self.clock())
+        if int(r["record_type"]) == abi.RT_REJECTION:
+            out.append_record(record.key, abi.RT_REJECTION, abi.VT_JOB, abi.JOB_TIME_OUT, int(r["rejection_type"]),
+                              self.part.reason(r), dict(record.value))
+            return out.build()
+        out.append_record(record.key, abi.RT_EVENT, abi.VT_JOB, abi.JOB_TIMED_OUT, abi.REJ_NONE, "", self.values.value(r))
+        # publishWork: no job stream -> jobStreamer.notifyWorkAvailable (a side effect, no record)
+        return out.build()
 
     # ---- job activation (JobBatchActivateProcessor.java:60-143) ------------------------------------
     def _activate_jobs(self, record, out):

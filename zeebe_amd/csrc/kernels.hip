@@ -570,8 +570,9 @@ __device__ __forceinline__ void set_local_variable(Lane<K>& L, uint32_t scope, c
 
 // The key ordinal of the instance of the i-th scope above an element in container c (K::S: the
 // instances of the enclosing sub-processes / multi-instance bodies; one per container element),
-// NONE past the process's children.  Scope chains are at most kMaxDepth deep on the device.
-constexpr int kMaxDepth = 8;
+// NONE past the process's children.  Scope chains are at most kMaxDepth deep on the device
+// (zbhip_deploy refuses io-mapped processes nested deeper).
+constexpr int kMaxDepth = kMaxScopeDepth;
 template <class K>
 __device__ __forceinline__ uint32_t container_key(const Lane<K>& L, uint32_t& c) {
   if constexpr (K::S) {
@@ -3771,7 +3772,9 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
                                                       uint32_t worker, unsigned long long deadline) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const uint32_t inst = jobs[i].x, ord = jobs[i].y;
+  // y bit 16: the host's state says ACTIVATABLE although the row holds a stored activation (a timed-out
+  // job, DbJobState.timeout keeps the deadline and worker): activate it again
+  const uint32_t inst = jobs[i].x, ord = jobs[i].y & 0xFFFF, again = (jobs[i].y >> 16) & 1u;
   ActivatedOut o = {};
   if (inst < st.n) {
     const uint4 h = st.hdr[inst];
@@ -3779,7 +3782,7 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
     bool marked = false;
     for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s) {
       uint2 e = st.slots[(size_t)s * st.n + inst];
-      if ((e.y & 0xFFFF) == ord && ((e.y >> 24) & 3u) == 1u) {
+      if ((e.y & 0xFFFF) == ord && (((e.y >> 24) & 3u) == 1u || (again && ((e.y >> 24) & 3u) == 3u))) {
         e.y |= 2u << 24;
         st.slots[(size_t)s * st.n + inst] = e;
         o.a = make_uint4(e.x, h.x, h.y, e.y);  // (e.y != 0: its state; a multi-instance loop counter)
@@ -3822,6 +3825,51 @@ hipError_t launch_activate_jobs(const DevState& st, const uint2* jobs, uint32_t 
   return hipGetLastError();
 }
 size_t activated_out_bytes() { return sizeof(ActivatedOut); }
+
+// The engine's due-date checker over the device's timers (zbhip_due_timers): DueDateTimerChecker ->
+// DbTimerInstanceState.processTimersWithDueDateBefore (:87-116) visits TIMER_DUE_DATES while dueDate <=
+// now and returns the first later dueDate.  One coalesced pass over the instances' timer rows (16 B
+// each): due rows are compacted into `out` (one atomic per wave: ballot + prefix count; the host sorts
+// them into (dueDate, elementInstanceKey, key) order), later dueDates reduce to one atomic min per wave.
+__global__ __launch_bounds__(256) void k_due_timers(const uint4* tmr, const uint4* hdr, uint32_t n, long long now,
+                                                   DueTimer* out, uint32_t* count, unsigned long long* next_due) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  bool due = false;
+  unsigned long long later = ~0ull;
+  uint4 t = make_uint4(0, 0, 0, 0);
+  uint32_t proc = 0;
+  if (i < n) {
+    t = tmr[i];
+    if (t.y >> 31) {
+      const uint4 hd = hdr[i];
+      if ((hd.y >> 24) & 1u) {  // a live instance's live timer
+        const long long d = (long long)(((unsigned long long)t.w << 32) | t.z);
+        due = d <= now;
+        if (!due) later = (unsigned long long)d;
+        proc = hd.x & 0xFFFF;
+      }
+    }
+  }
+  const uint64_t m = __ballot(due);
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == 0 && m) base = atomicAdd(count, (uint32_t)__popcll(m));
+  base = __shfl(base, 0);
+  if (due) out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = DueTimer{t, i, proc};
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long u = __shfl_xor(later, o);
+    later = u < later ? u : later;
+  }
+  if (lane == 0 && later != ~0ull) atomicMin(next_due, later);
+}
+
+hipError_t launch_due_timers(const DevState& st, long long now, DueTimer* out, uint32_t* count,
+                             unsigned long long* next_due, hipStream_t s) {
+  if (st.tmr && st.n)
+    hipLaunchKernelGGL(k_due_timers, dim3((st.n + 255) / 256), dim3(256), 0, s, st.tmr, st.hdr, st.n, now, out, count,
+                       next_due);
+  return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------------------------
 // launch wrappers (host)

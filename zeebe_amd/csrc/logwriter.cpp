@@ -332,6 +332,10 @@ int zbhip_serializer_rejection_reason(zbhip_serializer* s, const zbhip_record* r
     case ZBHIP_REASON_TIMER_NOT_ACTIVE:  // TriggerTimerProcessor.java:42-43
       return snprintf(buf, cap, "Expected to trigger a timer with key '%lld', but the timer is not active anymore",
                       (long long)r->key);
+    case ZBHIP_REASON_JOB_TIME_OUT:  // JobTimeOutProcessor.java:26-27,57-66
+      return snprintf(buf, cap, "Expected to time out activated job with key '%lld', but %s", (long long)r->key,
+                      r->reason_arg == 0 ? "no such job was found" : r->reason_arg == 1 ? "it must be activated first"
+                                                                       : "it has not timed out");
     default:
       if (cap) buf[0] = 0;
       return 0;

@@ -65,6 +65,8 @@ hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhi
                          uint32_t n, uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out,
                          hipStream_t s);
 hipError_t launch_xgather(const XGather& A, uint32_t max_count, hipStream_t s);
+hipError_t launch_due_timers(const DevState& st, long long now, DueTimer* out, uint32_t* count,
+                             unsigned long long* next_due, hipStream_t s);
 constexpr uint32_t kExtraRegions = 64;
 constexpr size_t kBulkDrainMin = 1 << 16;  // records: below this the drain stays on the calling thread
 constexpr uint32_t kRegionPad = 0;  // regions for the extra workgroups of multi-round windows
@@ -553,6 +555,8 @@ struct zbhip_handle {
   const zbhip_doc_entry* ext_docs = nullptr;
   PinnedVec<zbhip_command> h_cmds;  // (pinned: the upload source of host windows)
   PinnedVec<zbhip_command> h_cmds_next;  // the next window's, validated and copied in one pass
+  hipEvent_t upload_ev = nullptr;        // recorded after a submit's uploads (h_cmds, h_docs, h_xparts,
+                                         // h_order): the next submit waits on it before rewriting them
   std::vector<zbhip_doc_entry> h_docs;
   size_t n_cmds = 0, n_docs = 0;
   std::vector<uint32_t> round_begin;
@@ -654,13 +658,23 @@ struct zbhip_handle {
   bool job_index_on = false;
   std::map<std::pair<uint32_t, int64_t>, std::pair<uint32_t, uint16_t>> job_index;
   std::unordered_map<std::string, uint32_t> job_type_ids;
+  // A job whose stored JobRecord differs from the one JOB:CREATED wrote (slot flag bit 1 on the device):
+  // the deadline and worker DbJobState.activate stored, kept when the job timed out
+  // (DbJobState.timeout :142-150), and its JOB_STATES value.
+  enum : uint8_t { JS_ACTIVATED = 0, JS_ACTIVATABLE = 1, JS_GONE = 2 };  // (GONE: completed / canceled)
   struct Activation {
     int64_t deadline;
     std::string worker;
     uint32_t inst;
     uint32_t worker_id;  // the worker in the value dictionary (ZBHIP_NO_STRING: empty)
+    uint8_t state = JS_ACTIVATED;
+    int64_t eik = -1, pik = -1;  // the job's element instance and process instance
+    int32_t proc = -1, elem = -1;
   };
-  std::unordered_map<int64_t, Activation> activated;  // ACTIVATED jobs: deadline, worker
+  std::unordered_map<int64_t, Activation> activated;  // jobs with a stored activation: deadline, worker, state
+  DueTimer* d_due = nullptr;                          // zbhip_due_timers: [max_instances] due rows
+  uint32_t* d_due_count = nullptr;
+  unsigned long long* d_due_next = nullptr;
   std::vector<int64_t> completed_activated;           // completed in the last window (dropped next)
   uint32_t job_type(const std::string& t) {
     auto it = job_type_ids.find(t);
@@ -889,6 +903,9 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->st.tmr);
   (void)hipFree(h->st.act);
   (void)hipFree(h->d_cmd_act);
+  (void)hipFree(h->d_due);
+  (void)hipFree(h->d_due_count);
+  (void)hipFree(h->d_due_next);
   (void)hipFree(h->d_strs);
   (void)hipFree(h->d_str_off);
   (void)hipFree(h->d_cmd_due);
@@ -933,6 +950,7 @@ void zbhip_close(zbhip_handle* h) {
   if (h->src_pos_pin) (void)hipHostFree(h->src_pos_pin);
   (void)hipFree(h->d_check_flag);
   for (auto& e : h->tev) (void)hipEventDestroy(e);
+  if (h->upload_ev) (void)hipEventDestroy(h->upload_ev);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -1432,6 +1450,17 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   if (scopes || P.has_timer) cls = 4;
   if (P.has_io) cls = 5;
   if (P.has_msg) cls = 2;
+  if (P.has_io) {
+    // the device walks io-mapped scope chains at most kMaxScopeDepth containers up (kernels.hip
+    // var_lookup, merge_document_from, apply_output_mapping); a deeper nesting stays with the engine,
+    // whose DbVariableState walks the whole parent chain
+    for (uint32_t e = 0; e < P.els.size(); ++e) {
+      int depth = 0;
+      for (uint32_t c = P.els[e].flow_scope; c != 0 && c < P.els.size() && depth <= kMaxScopeDepth; c = P.els[c].flow_scope)
+        ++depth;
+      if (depth > kMaxScopeDepth) return ZBHIP_EUNSUPP;
+    }
+  }
   auto rank = [](int v) { return v == 3 ? 0 : v == 0 ? 1 : v == 1 ? 2 : v == 4 ? 3 : v == 5 ? 4 : 5; };
   if ((P.has_msg && (h->variant == 5 || P.has_io)) || (P.has_io && h->msg())) return ZBHIP_EUNSUPP;  // KMsg has no io
   const int old_variant = h->variant;
@@ -1645,6 +1674,9 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   const bool dbg = h->debug;
   auto now = [] { return std::chrono::steady_clock::now(); };
   const auto t0 = now();
+  // the previous submit's uploads read the handle's staging buffers: done before they are rewritten
+  // (a run in between has waited for them already; two submits in a row wait here)
+  if (h->upload_ev) HIPCHK(hipEventSynchronize(h->upload_ev));
   int rc = settle(h);  // the previous window's keys are fixed before its commands are replaced
   if (rc) return rc;
   const auto t1 = now();
@@ -1692,8 +1724,9 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   h->h_xparts.assign(xparts, xparts + n_xparts);
   h->n_xparts = n_xparts;
   h->ext_xparts = nullptr;
-  if (n_xparts)
-    HIPCHK(hipMemcpyAsync(h->d_xparts, xparts, n_xparts * sizeof(zbhip_xpart_cmd), hipMemcpyHostToDevice, h->stream));
+  if (n_xparts)  // (from the handle's copy: the caller's buffers are free once this returns)
+    HIPCHK(hipMemcpyAsync(h->d_xparts, h->h_xparts.data(), n_xparts * sizeof(zbhip_xpart_cmd), hipMemcpyHostToDevice,
+                          h->stream));
   h->n_cmds = n;
   h->n_docs = n_docs;
   const auto t2 = now();
@@ -1728,11 +1761,14 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   if (n && !early)
     HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
   if (n_docs)
-    HIPCHK(hipMemcpyAsync(h->d_docs, docs, n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d_docs, h->h_docs.data(), n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice,
+                          h->stream));
   if (!h->h_order.empty())
     HIPCHK(hipMemcpyAsync(h->d_order, h->h_order.data(), n * 4, hipMemcpyHostToDevice, h->stream));
-  // (no wait: the pageable sources are staged by the driver before these calls return, and the pinned
-  // h_cmds is rewritten only by the next submit, after the run that waits for this upload)
+  // no wait here: the uploads read only the handle's own buffers (h_cmds pinned, h_docs, h_xparts,
+  // h_order), which the next submit rewrites after waiting on this event
+  if (!h->upload_ev) HIPCHK(hipEventCreateWithFlags(&h->upload_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(h->upload_ev, h->stream));
   h->ran = false;
   h->results = false;
   if (dbg) {
@@ -1782,6 +1818,7 @@ int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_
                            size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts) {
   if (!h || (n && !dev_cmds)) return ZBHIP_EINVAL;
   if (n > h->rec_slots) return ZBHIP_ENOMEM;
+  if (h->upload_ev) HIPCHK(hipEventSynchronize(h->upload_ev));  // (h_order is rewritten by the planning)
   if (int rc0 = settle(h)) return rc0;
   bool replanned = false;
   const int rc = check_device_window(h, dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, &replanned);
@@ -1912,10 +1949,14 @@ static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
     const uint32_t tid = P.job_type_id[elem];
     const int64_t key = h->key_of(inst, w.x & 0xFFFF);
     if (code == C_JOB_CREATED) {
-      h->job_index[{tid, key}] = {inst, (uint16_t)(w.x & 0xFFFF)};
+      if (h->job_index_on) h->job_index[{tid, key}] = {inst, (uint16_t)(w.x & 0xFFFF)};
     } else {
-      h->job_index.erase({tid, key});
-      if (h->activated.count(key)) h->completed_activated.push_back(key);
+      if (h->job_index_on) h->job_index.erase({tid, key});
+      auto it = h->activated.find(key);
+      if (it != h->activated.end()) {  // gone (the drain still reads its deadline and worker)
+        it->second.state = zbhip_handle::JS_GONE;
+        h->completed_activated.push_back(key);
+      }
     }
   }
 }
@@ -2123,7 +2164,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
     for (int64_t k : h->completed_activated) h->activated.erase(k);
     h->completed_activated.clear();
   }
-  if (h->job_index_on)
+  if (h->job_index_on || !h->activated.empty())
     if (int rc = ensure_out(h)) return rc;
   const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
   if (h->hist.size() < subjects) {
@@ -2132,7 +2173,8 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
     h->inst_gen.resize(subjects, 0);
   }
   const size_t n = std::min(limit, h->n_cmds);
-  if (h->fin_next == 0 && n == h->n_cmds && !h->msg() && !h->job_index_on && n >= (1u << 16)) {
+  if (h->fin_next == 0 && n == h->n_cmds && !h->msg() && !h->job_index_on && h->activated.empty() &&
+      n >= (1u << 16)) {
     bool all_declared = true;  // the whole window can be done now (fallback keys declared, or forced)
     if (!force)
       for (size_t c = 0; c < n && all_declared; ++c)
@@ -2165,7 +2207,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
         h->hist[h2.x].push_back({(uint16_t)(h2.y & 0xFFFF), h->key_counter + 1 + nprim});
         h->batches.push_back({h->key_counter + 1 + nprim, h2.x, (uint16_t)(h2.y & 0xFFFF), (uint16_t)nsec, h->inst_gen[h2.x]});
       }
-      if (h->job_index_on && h2.x < h->cfg.max_instances) track_jobs(h, c, h2.x);
+      if ((h->job_index_on || !h->activated.empty()) && h2.x < h->cfg.max_instances) track_jobs(h, c, h2.x);
       if ((hd.y & HDR_ENDED) && h2.x < h->cfg.max_instances) {
         ++h->inst_gen[h2.x];
         h->batches_dead.fetch_add(h->hist[h2.x].size(), std::memory_order_relaxed);
@@ -2182,7 +2224,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
       h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
       h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[cm.instance]});
     }
-    if (h->job_index_on) track_jobs(h, c, cm.instance);
+    if (h->job_index_on || !h->activated.empty()) track_jobs(h, c, cm.instance);
     if (hd.y & HDR_ENDED) {  // completed: its job keys no longer resolve
       ++h->inst_gen[cm.instance];
       h->batches_dead.fetch_add(h->hist[cm.instance].size(), std::memory_order_relaxed);
@@ -3342,9 +3384,10 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     }
     if (job_row) {
       const char* type = P.strings[E.job_type].c_str();
-      const bool act = (e.y >> 25) & 1;  // ACTIVATED (zbhip_activate_jobs): deadline and worker on the host
-      const auto ait = act ? h->activated.find(jk) : h->activated.end();
+      const bool stored = (e.y >> 25) & 1;  // a stored activation (zbhip_activate_jobs): deadline, worker, state on the host
+      const auto ait = stored ? h->activated.find(jk) : h->activated.end();
       const long long deadline = ait != h->activated.end() ? (long long)ait->second.deadline : -1;
+      const bool act = ait != h->activated.end() && ait->second.state == zbhip_handle::JS_ACTIVATED;
       snprintf(buf, sizeof buf,
                "JOBS|%lld|type=%s,retries=%u,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
                "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
@@ -3681,6 +3724,12 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   std::set<int64_t> job_rows;
   std::map<int64_t, std::pair<int64_t, std::string>> job_act;  // ACTIVATED jobs: deadline, worker
   std::set<int64_t> job_activated_state;
+  struct JobMeta {
+    int64_t eik, pik;
+    std::string element_id;
+    int32_t elem;  // (set where the job's element instance is rebuilt)
+  };
+  std::map<int64_t, JobMeta> job_meta;
   std::vector<ImpPms> pms;
   std::vector<ImpTimer> timers;
   int64_t latest = -1;
@@ -3718,6 +3767,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       job_rows.insert(to_ll(p[1]));
       auto f = row_fields(p[2]);
       job_act[to_ll(p[1])] = {f.count("deadline") ? to_ll(f["deadline"]) : -1, f["worker"]};
+      job_meta[to_ll(p[1])] = {to_ll(f["elementInstanceKey"]), to_ll(f["processInstanceKey"]), f["elementId"], -1};
     } else if (cf == "JOB_STATES" && p.size() >= 3) {
       if (p[2] == "ACTIVATED") job_activated_state.insert(to_ll(p[1]));
       else if (p[2] != "ACTIVATABLE") return ZBHIP_EUNSUPP;  // failed / error-thrown jobs: outside the subset
@@ -3890,7 +3940,15 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       uint32_t job = sub_el ? (uint32_t)e.child_count | ((uint32_t)e.asf << 8)
                      : body ? (uint32_t)e.child_count | ((uint32_t)e.loop << 8)
                      : e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
-      uint32_t row = !sub_el && !body && e.job > 0 && job_rows.count(e.job) ? (job_activated_state.count(e.job) ? 3u : 1u) : 0u;
+      // (flag bit 1: a stored activation -- ACTIVATED, or timed out with its deadline and worker kept)
+      const auto ja = job_act.find(e.job);
+      const bool stored = job_activated_state.count(e.job) ||
+                          (ja != job_act.end() && (ja->second.first != -1 || !ja->second.second.empty()));
+      uint32_t row = !sub_el && !body && e.job > 0 && job_rows.count(e.job) ? (stored ? 3u : 1u) : 0u;
+      if (row) {
+        const auto jm = job_meta.find(e.job);
+        if (jm != job_meta.end()) jm->second.elem = el;
+      }
       if (const Proc::Mi* m = P.mi_inner((uint32_t)el)) {
         // the loop counter in the flags; its loop variables exactly what setLoopVariables wrote,
         // keyed right below the job's key (a job worker) or kept in the job field (an undefined task)
@@ -3996,11 +4054,20 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   h->published |= stats_row;
   for (const Done& d : done)
     for (int64_t k : d.keys)
-      if (job_activated_state.count(k)) {
+      if (job_act.count(k) && (job_activated_state.count(k) || job_act[k].first != -1 || !job_act[k].second.empty())) {
         const std::string& wk = job_act[k].second;
         const int64_t wid = wk.empty() ? (int64_t)ZBHIP_NO_STRING : zbhip_intern_string(h, wk.data(), wk.size());
         if (wid < 0) return (int)wid;
-        h->activated[k] = {job_act[k].first, wk, d.slot, (uint32_t)wid};
+        zbhip_handle::Activation& a = h->activated[k];
+        a = {job_act[k].first, wk, d.slot, (uint32_t)wid};
+        a.state = job_activated_state.count(k) ? zbhip_handle::JS_ACTIVATED : zbhip_handle::JS_ACTIVATABLE;
+        const auto jm = job_meta.find(k);
+        if (jm != job_meta.end()) {
+          a.eik = jm->second.eik;
+          a.pik = jm->second.pik;
+          a.proc = (int32_t)(hdr[d.slot].x & 0xFFFF);
+          a.elem = jm->second.elem;
+        }
       }
   h->job_index_on = false;  // rebuilt from the device rows at the next activation
   if (n_instances) *n_instances = (uint32_t)done.size();
@@ -4138,8 +4205,13 @@ static int build_job_index(zbhip_handle* h) {
     for (uint32_t s = 0; s < ns && s < (uint32_t)kSlots; ++s) {
       const uint2 e = slots[s * N + i];
       const uint32_t elem = e.x & 0xFFFF, job = e.y & 0xFFFF, fl = e.y >> 24;
-      if ((fl & 3u) != 1u || elem >= P.els.size()) continue;  // a job row, not activated
-      h->job_index[{P.job_type_id[elem], h->key_of((uint32_t)i, job)}] = {(uint32_t)i, (uint16_t)job};
+      if (!(fl & 1u) || elem >= P.els.size()) continue;  // a job row ...
+      const int64_t jk = h->key_of((uint32_t)i, job);
+      if (fl & 2u) {  // ... with a stored activation: activatable again once it timed out
+        const auto ait = h->activated.find(jk);
+        if (ait == h->activated.end() || ait->second.state != zbhip_handle::JS_ACTIVATABLE) continue;
+      }
+      h->job_index[{P.job_type_id[elem], jk}] = {(uint32_t)i, (uint16_t)job};
     }
   }
   h->job_index_on = true;
@@ -4191,7 +4263,10 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
   if (pick.empty()) return ZBHIP_OK;
   const size_t n = pick.size(), ob = activated_out_bytes();
   std::vector<uint2> list(n);
-  for (size_t i = 0; i < n; ++i) list[i] = make_uint2(pick[i].second.first, pick[i].second.second);
+  for (size_t i = 0; i < n; ++i) {  // (y bit 16: a timed-out job, its row keeps the stored activation)
+    const auto ait = h->activated.find(pick[i].first);
+    list[i] = make_uint2(pick[i].second.first, pick[i].second.second | (ait != h->activated.end() ? 1u << 16 : 0u));
+  }
   uint2* d_list = nullptr;
   void* d_out = nullptr;
   std::vector<uint8_t> outb(n * ob);
@@ -4296,7 +4371,12 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     }
     // JobBatchActivatedApplier -> DbJobState.activate: ACTIVATED, out of JOB_ACTIVATABLE, deadline
     h->job_index.erase({tit->second, j.key});
-    h->activated[j.key] = {j.deadline, worker, inst, worker_id};
+    zbhip_handle::Activation& act = h->activated[j.key];
+    act = {j.deadline, worker, inst, worker_id};
+    act.eik = j.element_instance_key;
+    act.pik = j.process_instance_key;
+    act.proc = j.process_idx;
+    act.elem = j.element_idx;
   }
   return ZBHIP_OK;
 }
@@ -4318,6 +4398,160 @@ extern "C" int zbhip_job_batch_rejection_reason(const zbhip_job_activation* cmd,
     case 3: snprintf(buf, cap, f, "type", "present", "blank"); break;
     default: buf[0] = 0;
   }
+  return ZBHIP_OK;
+}
+
+// ---- the engine's scheduled tasks over device-held state -------------------------------------------
+// The reference's scheduled checkers read RocksDB; the device's timers and activated jobs live in HBM
+// and in the handle.  These calls are what a host adapter's checkers read instead.
+
+// a TIMER:TRIGGER command of a due device timer, as WriteTriggerTimerCommandVisitor writes it
+// (DueDateTimerChecker.java:115-129): key = the timer, the TimerRecord of the TimerInstance
+static void timer_trigger_record(zbhip_handle* h, const DueTimer& d, zbhip_record& r) {
+  r = zbhip_record{};
+  r.record_type = ZBHIP_RT_COMMAND;
+  r.value_type = ZBHIP_VT_TIMER;
+  r.intent = ZBHIP_TIMER_TRIGGER;
+  r.rejection_type = ZBHIP_REJ_NONE;
+  r.key = h->key_of(d.inst, d.tmr.x >> 16);
+  r.scope_key = h->key_of(d.inst, d.tmr.y & 0xFFFF);
+  r.process_instance_key = h->key_of(d.inst, 0);
+  r.process_idx = (int32_t)d.proc;
+  r.element_idx = (int32_t)(d.tmr.x & 0xFFF);  // the handler node (catch / boundary event)
+  r.aux = (int64_t)(((unsigned long long)d.tmr.w << 32) | d.tmr.z);  // dueDate
+  const uint32_t reps = (d.tmr.y >> 16) & 0xFF;
+  r.partition = reps == 255 ? -1 : (int32_t)reps;
+  r.source_index = -1;
+  r.message_key = -1;
+  r.correlation_key = ZBHIP_NO_STRING;
+  r.message_name = r.bpmn_process_id = 0xFFFF;
+}
+
+extern "C" int zbhip_due_timers(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out, int64_t* next_due) {
+  if (!h || !n_out || (cap && !out)) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (next_due) *next_due = -1;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  const uint32_t N = h->cfg.max_instances;
+  if (!h->d_due) {
+    if (dalloc(&h->d_due, N) != hipSuccess || dalloc(&h->d_due_count, 1) != hipSuccess ||
+        dalloc(&h->d_due_next, 1) != hipSuccess)
+      return ZBHIP_ENOMEM;
+  }
+  const unsigned long long none = ~0ull;
+  HIPCHK(hipMemsetAsync(h->d_due_count, 0, sizeof(uint32_t), h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_due_next, &none, sizeof none, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(launch_due_timers(h->st, (long long)now, h->d_due, h->d_due_count, h->d_due_next, h->stream));
+  uint32_t count = 0;
+  unsigned long long later = none;
+  HIPCHK(hipMemcpyAsync(&count, h->d_due_count, sizeof count, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(&later, h->d_due_next, sizeof later, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  std::vector<DueTimer> due(count);
+  if (count) HIPCHK(hipMemcpy(due.data(), h->d_due, count * sizeof(DueTimer), hipMemcpyDeviceToHost));
+  // TIMER_DUE_DATES order: [dueDate, [elementInstanceKey, timerKey]] (DbTimerInstanceState :52-56)
+  std::vector<zbhip_record> recs(count);
+  for (uint32_t i = 0; i < count; ++i) timer_trigger_record(h, due[i], recs[i]);
+  std::sort(recs.begin(), recs.end(), [](const zbhip_record& a, const zbhip_record& b) {
+    return std::tie(a.aux, a.scope_key, a.key) < std::tie(b.aux, b.scope_key, b.key);
+  });
+  const size_t n = std::min<size_t>(cap, count);
+  for (size_t i = 0; i < n; ++i) out[i] = recs[i];
+  *n_out = n;
+  // processTimersWithDueDateBefore's result: the first dueDate it did not consume
+  if (next_due) *next_due = n < count ? recs[n].aux : later != none ? (int64_t)later : -1;
+  return ZBHIP_OK;
+}
+
+// a JOB record of a device job with a stored activation: the stored JobRecord (type, retries,
+// element and keys from the deployment and the handle, deadline and worker as DbJobState stored them)
+static void stored_job_record(const zbhip_handle::Activation& a, int64_t key, uint8_t rt, uint8_t intent,
+                              zbhip_record& r) {
+  r = zbhip_record{};
+  r.key = key;
+  r.record_type = rt;
+  r.value_type = ZBHIP_VT_JOB;
+  r.intent = intent;
+  r.rejection_type = ZBHIP_REJ_NONE;
+  r.scope_key = a.eik;
+  r.process_instance_key = a.pik;
+  r.process_idx = a.proc;
+  r.element_idx = a.elem;
+  r.source_index = -1;
+  r.aux = -1;
+  r.message_key = a.deadline;
+  r.correlation_key = a.worker_id;
+  r.message_name = r.bpmn_process_id = 0xFFFF;
+}
+
+extern "C" int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out) {
+  if (!h || !n_out || (cap && !out)) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  // DbJobState.forEachTimedOutEntry (:286-298): JOB_DEADLINES [deadline, jobKey] while deadline < now
+  std::vector<std::pair<int64_t, int64_t>> due;
+  for (const auto& [k, a] : h->activated)
+    if (a.state == zbhip_handle::JS_ACTIVATED && a.deadline < now) due.push_back({a.deadline, k});
+  std::sort(due.begin(), due.end());
+  const size_t n = std::min(cap, due.size());
+  for (size_t i = 0; i < n; ++i)
+    stored_job_record(h->activated.at(due[i].second), due[i].second, ZBHIP_RT_COMMAND, ZBHIP_JOB_TIME_OUT, out[i]);
+  *n_out = n;
+  return ZBHIP_OK;
+}
+
+extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out) {
+  if (!h || !out) return ZBHIP_EINVAL;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  // JobTimeOutProcessor.processRecord (:46-69): an ACTIVATED job past its deadline times out, anything
+  // else is rejected NOT_FOUND with the job's state
+  auto it = h->activated.find(job_key);
+  uint8_t why = 0;  // reason_arg: 0 no such job, 1 not activated, 2 not timed out
+  if (it != h->activated.end()) {
+    if (it->second.state == zbhip_handle::JS_ACTIVATED) {
+      if (it->second.deadline < now) {
+        zbhip_handle::Activation& a = it->second;
+        stored_job_record(a, job_key, ZBHIP_RT_EVENT, ZBHIP_JOB_TIMED_OUT, *out);
+        // JobTimedOutApplier -> DbJobState.timeout: ACTIVATABLE again, the record kept, no deadline row
+        a.state = zbhip_handle::JS_ACTIVATABLE;
+        uint32_t inst;
+        uint16_t ord;
+        if (h->job_index_on && a.proc >= 0 && (size_t)a.proc < h->procs.size() && a.elem >= 0 &&
+            (size_t)a.elem < h->procs[a.proc].els.size() && zbhip_resolve_key(h, job_key, &inst, &ord) == ZBHIP_OK)
+          h->job_index[{h->procs[a.proc].job_type_id[a.elem], job_key}] = {inst, ord};
+        return ZBHIP_OK;
+      }
+      why = 2;
+    } else {
+      why = it->second.state == zbhip_handle::JS_GONE ? 0 : 1;
+    }
+  } else {
+    // no stored activation: an ACTIVATABLE job of a live instance, or none at all
+    uint32_t inst;
+    uint16_t ord;
+    if (zbhip_resolve_key(h, job_key, &inst, &ord) == ZBHIP_OK && inst < h->cfg.max_instances) {
+      InstRows R{};
+      if (int rc = gather_instance(h, inst, R)) return rc;
+      const uint32_t nslots = (R.hdr.y >> 8) & 0xFF;
+      for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s)
+        if ((R.slots[s].y & 0xFFFF) == ord && ((R.slots[s].y >> 24) & 1u) && ((R.hdr.y >> 24) & 1u)) why = 1;
+    }
+  }
+  *out = zbhip_record{};
+  out->key = job_key;
+  out->record_type = ZBHIP_RT_REJECTION;
+  out->value_type = ZBHIP_VT_JOB;
+  out->intent = ZBHIP_JOB_TIME_OUT;
+  out->rejection_type = ZBHIP_REJ_NOT_FOUND;
+  out->reason = ZBHIP_REASON_JOB_TIME_OUT;
+  out->reason_arg = why;
+  out->scope_key = out->process_instance_key = out->aux = out->message_key = out->source_index = -1;
+  out->process_idx = out->element_idx = -1;
+  out->correlation_key = ZBHIP_NO_STRING;
+  out->message_name = out->bpmn_process_id = 0xFFFF;
   return ZBHIP_OK;
 }
 

@@ -16,6 +16,7 @@ constexpr uint32_t kMaxProgWords = 6144;  // program arena staged in LDS (24 KiB
 constexpr int kMaxElements = 4095;        // 12-bit element index in queue entries
 
 constexpr uint16_t NONE = 0xFFFF;
+constexpr int kMaxScopeDepth = 8;         // container scopes an io-mapped scope chain walk visits (KScopeIO)
 
 // ---- message correlation (config 5; kernel variant KMsg) ----
 constexpr int kSubs = 4;           // message-subscription rows per correlation slot (HBM)
@@ -218,6 +219,12 @@ struct DevState {
   uint4* act;        // [kSlots][n] activations of the instance's jobs (zbhip_activate_jobs; NULL until the
                      //     first): x = job key ordinal | valid << 31, y = worker (value-dictionary id),
                      //     z/w = deadline lo/hi -- the stored job's fields its later records carry
+};
+
+// a due timer found by k_due_timers (zbhip_due_timers): its DevState.tmr row, instance slot, process
+struct DueTimer {
+  uint4 tmr;
+  uint32_t inst, proc;
 };
 
 // elements without behaviour: ACTIVATING, ACTIVATED, COMPLETE_ELEMENT, COMPLETING, COMPLETED, then

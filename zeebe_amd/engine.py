@@ -411,6 +411,31 @@ class Partition:
         check(self.L.zbhip_command_status(self.h, i, C.byref(st), C.byref(rs)))
         return st.value, self.FALLBACK_REASONS.get(rs.value, rs.value)
 
+    # ---- the engine's scheduled tasks over device-held state ----
+    def due_timers(self, now, cap=1 << 16):
+        """DueDateTimerChecker over the device timers (zbhip_due_timers): (the TIMER:TRIGGER commands as
+        RECORD_DTYPE rows in TIMER_DUE_DATES order, the first dueDate not returned or -1)."""
+        out = np.zeros(max(cap, 1), dtype=abi.RECORD_DTYPE)
+        n, nxt = C.c_size_t(), C.c_int64()
+        check(self.L.zbhip_due_timers(self.h, int(now), out.ctypes.data, cap, C.byref(n), C.byref(nxt)),
+              "zbhip_due_timers")
+        return out[: n.value], nxt.value
+
+    def timed_out_jobs(self, now, cap=1 << 16):
+        """JobTimeoutTrigger over the device's activated jobs (zbhip_timed_out_jobs): the JOB:TIME_OUT
+        commands (RECORD_DTYPE rows, the stored job) in JOB_DEADLINES order."""
+        out = np.zeros(max(cap, 1), dtype=abi.RECORD_DTYPE)
+        n = C.c_size_t()
+        check(self.L.zbhip_timed_out_jobs(self.h, int(now), out.ctypes.data, cap, C.byref(n)), "zbhip_timed_out_jobs")
+        return out[: n.value]
+
+    def time_out_job(self, job_key, now):
+        """JOB:TIME_OUT of a device job (zbhip_time_out_job): JOB:TIMED_OUT or the rejection, one
+        RECORD_DTYPE row."""
+        out = np.zeros(1, dtype=abi.RECORD_DTYPE)
+        check(self.L.zbhip_time_out_job(self.h, int(job_key), int(now), out.ctypes.data), "zbhip_time_out_job")
+        return out[0]
+
     def resolve_key(self, key):
         inst, ordv = C.c_uint32(), C.c_uint16()
         check(self.L.zbhip_resolve_key(self.h, key, C.byref(inst), C.byref(ordv)), "unknown key %d" % key)

@@ -32,7 +32,8 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_import_state", "zbhip_activate_jobs", "zbhip_job_batch_rejection_reason",
            "zbhip_serialize_log_device", "zbhip_log_device_copy", "zbhip_continuations",
            "zbhip_pending_continuations", "zbhip_current_key", "zbhip_set_key_if_higher",
-           "zbhip_select_instances_db", "zbhip_drain_command", "zbhip_outbox_command"]
+           "zbhip_select_instances_db", "zbhip_drain_command", "zbhip_outbox_command", "zbhip_due_timers",
+           "zbhip_timed_out_jobs", "zbhip_time_out_job"]
 
 
 class ZbhipError(RuntimeError):
@@ -116,6 +117,9 @@ def load():
     L.zbhip_import_state.argtypes = [vp, C.c_char_p, sz, u32, C.POINTER(u32)]
     L.zbhip_activate_jobs.argtypes = [vp, C.POINTER(abi.JobActivation), vp, sz, C.POINTER(abi.JobBatch)]
     L.zbhip_job_batch_rejection_reason.argtypes = [C.POINTER(abi.JobActivation), C.POINTER(abi.JobBatch), C.c_char_p, sz]
+    L.zbhip_due_timers.argtypes = [vp, i64, vp, sz, C.POINTER(sz), C.POINTER(i64)]
+    L.zbhip_timed_out_jobs.argtypes = [vp, i64, vp, sz, C.POINTER(sz)]
+    L.zbhip_time_out_job.argtypes = [vp, i64, i64, vp]
     L.zbhip_stream.argtypes = [vp]
     L.zbhip_stream.restype = vp
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
