@@ -117,7 +117,7 @@ enum { ZBHIP_TIMER_CREATED = 0, ZBHIP_TIMER_TRIGGER = 1, ZBHIP_TIMER_TRIGGERED =
 /* IncidentIntent CREATED=0 RESOLVE=1 RESOLVED=2 (protocol/.../intent/IncidentIntent.java:19-22) */
 enum { ZBHIP_INCIDENT_CREATED = 0 };
 /* ErrorType ordinals (protocol/.../record/value/ErrorType.java) of the device's incidents */
-enum { ZBHIP_ERR_CONDITION_ERROR = 3, ZBHIP_ERR_EXTRACT_VALUE_ERROR = 4 };
+enum { ZBHIP_ERR_JOB_NO_RETRIES = 2, ZBHIP_ERR_CONDITION_ERROR = 3, ZBHIP_ERR_EXTRACT_VALUE_ERROR = 4 };
 /* the type of a condition's non-boolean result (ResultType names in the incident message) */
 enum { ZBHIP_FEEL_NULL = 0, ZBHIP_FEEL_NUMBER = 1, ZBHIP_FEEL_STRING = 2 };
 /* ProcessInstanceBatchIntent (protocol/.../intent/ProcessInstanceBatchIntent.java:18-20) */
@@ -609,8 +609,10 @@ enum zbhip_reason {
   ZBHIP_REASON_MS_CORR_NOT_FOUND = 12,  /* MessageSubscriptionCorrelateProcessor NO_SUBSCRIPTION_FOUND */
   ZBHIP_REASON_TIMER_NOT_FOUND = 13,    /* TriggerTimerProcessor NO_TIMER_FOUND_MESSAGE */
   ZBHIP_REASON_TIMER_NOT_ACTIVE = 14,   /* TriggerTimerProcessor NO_ACTIVE_TIMER_MESSAGE */
-  ZBHIP_REASON_JOB_TIME_OUT = 15        /* JobTimeOutProcessor NOT_ACTIVATED_JOB_MESSAGE; reason_arg 0 "no such job
+  ZBHIP_REASON_JOB_TIME_OUT = 15,       /* JobTimeOutProcessor NOT_ACTIVATED_JOB_MESSAGE; reason_arg 0 "no such job
                                            was found", 1 "it must be activated first", 2 "it has not timed out" */
+  ZBHIP_REASON_JOB_STATE = 16           /* JobCommandPreconditionChecker (:33-49) of the record's intent: reason_arg =
+                                           the JobState.State (2 FAILED: "it is in state 'FAILED'", 3 NOT_FOUND) */
 };
 /* Rejection reason text exactly as the reference writes it. */
 int zbhip_rejection_reason(zbhip_handle* h, const zbhip_record* rec, char* buf, size_t cap);
@@ -775,6 +777,28 @@ int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t
  * (JobTimedOutApplier -> DbJobState.timeout: ACTIVATABLE again, deadline and worker kept), or the
  * NOT_FOUND rejection (reason ZBHIP_REASON_JOB_TIME_OUT; the adapter writes the command's value). */
 int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out);
+/* JOB:FAIL of a device job (JobFailProcessor.processRecord / failJob, processing/job/JobFailProcessor.java
+ * :79-162; JobFailedApplier -> DbJobState.fail :191-203).  out[0] = JOB:FAILED (the stored job with the
+ * command's retries and errorMessage -- StringUtil.limitString at 10 000 -- JOB records: reason_arg bit 0 =
+ * partition holds the retries and message_name | bpmn_process_id << 16 the errorMessage's string id) or
+ * the rejection (NOT_FOUND / INVALID_STATE, reason ZBHIP_REASON_JOB_STATE); retries <= 0: out[1] =
+ * INCIDENT:CREATED (ErrorType JOB_NO_RETRIES in partition, aux = the job key, correlation_key = the
+ * errorMessage's id: the job's, or "No more retries left."; key = the next key) and the job is FAILED.
+ * ACTIVATABLE again with retries left; a later activation keeps the retries.  Returns ZBHIP_EUNSUPP for
+ * commands outside the subset (variables, a retry back-off): the adapter hands the instance to the
+ * engine.  cap >= 2. */
+typedef struct zbhip_job_fail {
+  int64_t job_key;
+  int64_t retry_backoff;
+  const char* error_message;
+  size_t error_message_len;
+  int32_t retries;
+  uint32_t n_variables;   /* entries of the command's variable document */
+} zbhip_job_fail;
+int zbhip_fail_job(zbhip_handle* h, const zbhip_job_fail* cmd, zbhip_record* out, size_t cap, size_t* n_out);
+/* The JobState.State of a device job with stored fields: 0 ACTIVATABLE, 1 ACTIVATED, 2 FAILED, 3 gone; -1 none
+ * stored (ACTIVATABLE if the key is a live job's).  The adapter rejects JOB:COMPLETE of a FAILED job itself. */
+int zbhip_job_state(zbhip_handle* h, int64_t job_key);
 
 /* ---- fallback hand-off (Engine.java:134 onProcessingError, ProcessingStateMachine.java:276-310) --
  * A command the device did not process (zbhip_command_status != 0) goes to the CPU engine, in log

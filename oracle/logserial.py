@@ -187,7 +187,7 @@ INCIDENT = [
     ("processDefinitionKey", "long", -1), ("processInstanceKey", "long", -1), ("elementId", "str", ""),
     ("elementInstanceKey", "long", -1), ("jobKey", "long", -1), ("variableScopeKey", "long", -1),
     ("tenantId", "str", "<default>")]
-ERROR_TYPE = {3: "CONDITION_ERROR", 4: "EXTRACT_VALUE_ERROR"}  # ErrorType.java ordinals
+ERROR_TYPE = {2: "JOB_NO_RETRIES", 3: "CONDITION_ERROR", 4: "EXTRACT_VALUE_ERROR"}  # ErrorType.java ordinals
 FEEL_RESULT = {0: "NULL", 1: "NUMBER", 2: "STRING"}
 
 

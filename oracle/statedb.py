@@ -44,7 +44,8 @@ CF = {"KEY": 1, "ELEMENT_INSTANCE_PARENT_CHILD": 6, "ELEMENT_INSTANCE_KEY": 7, "
       "ELEMENT_INSTANCE_CHILD_PARENT": 9, "VARIABLES": 10, "JOBS": 16, "JOB_STATES": 17, "EVENT_SCOPE": 37,
       "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY": 55, "JOB_ACTIVATABLE": 76, "MESSAGE_SUBSCRIPTION_BY_KEY": 27,
       "MESSAGE_STATS": 54, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY": 74, "PROCESS_SUBSCRIPTION_BY_KEY": 75,
-      "JOB_DEADLINES": 18, "TIMERS": 12, "TIMER_DUE_DATES": 13, "INCIDENTS": 34, "INCIDENT_PROCESS_INSTANCES": 35}
+      "JOB_DEADLINES": 18, "TIMERS": 12, "TIMER_DUE_DATES": 13, "INCIDENTS": 34, "INCIDENT_PROCESS_INSTANCES": 35,
+      "INCIDENT_JOBS": 36, "JOB_BACKOFF": 42}
 # TimerInstance.java:25-43 (declaration order)
 TIMER_INSTANCE = [
     ("handlerNodeId", "str", ""), ("processDefinitionKey", "long", 0), ("key", "long", 0),
@@ -149,8 +150,12 @@ def encode_rows(rows, processes, string_value):
             out.append((CF[name], prefix + dblong(int(parts[1])), val))
         elif name == "JOBS":
             key, f = int(parts[1]), fields(parts[2])
+            failed = {}
+            if "errorMessageHex" in f:  # a failed job's stored fields (JobFailProcessor.failJob)
+                failed = dict(errorMessage=bytes.fromhex(f["errorMessageHex"]).decode(),
+                              retryBackoff=int(f["retryBackoff"]), recurringTime=int(f["recurringTime"]))
             job = LS.write_object(LS.JOB, dict(
-                deadline=int(f.get("deadline", -1)), worker=f.get("worker", ""),
+                deadline=int(f.get("deadline", -1)), worker=f.get("worker", ""), **failed,
                 retries=int(f["retries"]), type=f["type"], bpmnProcessId=f["bpmnProcessId"],
                 processDefinitionVersion=int(f["processDefinitionVersion"]),
                 processDefinitionKey=int(f["processDefinitionKey"]), processInstanceKey=int(f["processInstanceKey"]),
@@ -194,16 +199,24 @@ def encode_rows(rows, processes, string_value):
             f = fields(parts[2])
             proc = by_def[int(f["processDefinitionKey"])]
             et, eik = int(f["errorType"]), int(f["elementInstanceKey"])
+            job = int(f.get("jobKey", -1))  # a job's incident (JOB_NO_RETRIES): its key and message
+            msg = bytes.fromhex(f["messageHex"]).decode() if job >= 0 else \
+                LS.incident_message(proc, et, int(f["flow"]), int(f["result"]))
             rec = LS.write_object(LS.INCIDENT, dict(
-                errorType=LS.ERROR_TYPE[et], errorMessage=LS.incident_message(proc, et, int(f["flow"]), int(f["result"])),
+                errorType=LS.ERROR_TYPE[et], errorMessage=msg,
                 bpmnProcessId=proc["bpmn_process_id"], processDefinitionKey=proc["key"],
                 processInstanceKey=int(f["processInstanceKey"]), elementId=f["elementId"], elementInstanceKey=eik,
-                variableScopeKey=eik))
+                jobKey=job, variableScopeKey=eik))
             out.append((CF[name], prefix + dblong(int(parts[1])), LS.write_object([("incidentRecord", "raw", None)],
                                                                                   {"incidentRecord": rec})))
         elif name == "INCIDENT_PROCESS_INSTANCES":  # DbForeignKey<DbLong> eik -> IncidentKey{key}
             out.append((CF[name], prefix + dblong(int(parts[1])),
                         LS.write_object([("key", "long", LS.NO_DEFAULT)], {"key": int(parts[2])})))
+        elif name == "INCIDENT_JOBS":  # DbForeignKey<DbLong> jobKey -> IncidentKey{key}
+            out.append((CF[name], prefix + dblong(int(parts[1])),
+                        LS.write_object([("key", "long", LS.NO_DEFAULT)], {"key": int(parts[2])})))
+        elif name == "JOB_BACKOFF":  # [recurringTime, jobKey] -> DbNil (DbJobState.java:103-108)
+            out.append((CF[name], prefix + dblong(int(parts[1])) + dblong(int(parts[2])), NIL))
         elif name == "TIMER_DUE_DATES":  # [dueDate, [elementInstanceKey, timerKey]] -> DbNil
             out.append((CF[name], prefix + dblong(int(parts[1])) + dblong(int(parts[2])) + dblong(int(parts[3])), NIL))
         elif name == "JOB_DEADLINES":  # DbJobState.java:100-102: [deadline, jobKey] -> DbNil

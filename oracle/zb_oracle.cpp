@@ -951,9 +951,28 @@ struct JobRow {  // JobRecord without variables (DbJobState.createJobRecord)
   std::string type;
   int retries = 3;
   bool activated = false;  // JOB_STATES ACTIVATED (DbJobState.activate :118-133)
+  bool failed = false;     // JOB_STATES FAILED (DbJobState.fail :191-203)
   int64_t deadline = -1;
   std::string worker;
+  // JobFailProcessor.failJob (:103-125) stored them: the record's retries / errorMessage /
+  // retryBackoff / recurringTime differ from JOB:CREATED's from then on
+  bool fail_fields = false;
+  std::string error_message;
+  int64_t retry_backoff = 0, recurring_time = -1;
 };
+
+// hex of a string in a state row (error messages may hold ',' and '|')
+static std::string hex_of(const std::string& v) {
+  static const char* d = "0123456789abcdef";
+  std::string o;
+  for (unsigned char c : v) { o += d[c >> 4]; o += d[c & 15]; }
+  return o;
+}
+static std::string unhex(const std::string& h) {
+  std::string o;
+  for (size_t i = 0; i + 1 < h.size(); i += 2) o += (char)std::stoi(h.substr(i, 2), nullptr, 16);
+  return o;
+}
 
 struct EventTrigger {  // state/instance/EventTrigger.java
   int elem = -1;
@@ -1329,7 +1348,8 @@ class Oracle {
                      (r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION &&
                       (r.intent == ZBHIP_PMS_CREATE || r.intent == ZBHIP_PMS_CORRELATE || r.intent == ZBHIP_PMS_DELETE));
     const bool known = (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION && r.intent == ZBHIP_PIC_CREATE) ||
-                       (r.value_type == ZBHIP_VT_JOB && (r.intent == ZBHIP_JOB_COMPLETE || r.intent == ZBHIP_JOB_TIME_OUT)) ||
+                       (r.value_type == ZBHIP_VT_JOB && (r.intent == ZBHIP_JOB_COMPLETE || r.intent == ZBHIP_JOB_TIME_OUT ||
+                                                          r.intent == ZBHIP_JOB_FAIL)) ||
                        (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && r.intent == ZBHIP_PIB_ACTIVATE) || msg;
@@ -1432,7 +1452,9 @@ class Oracle {
           const bool first = cf == "ELEMENT_INSTANCE_KEY";
           if ((first ? 0 : cf == "JOB_STATES" ? 2 : 1) != pass) continue;
           ++n;
-          if (cf == "KEY" || cf == "TIMER_DUE_DATES" || cf == "JOB_ACTIVATABLE" || cf == "JOB_DEADLINES") continue;
+          if (cf == "KEY" || cf == "TIMER_DUE_DATES" || cf == "JOB_ACTIVATABLE" || cf == "JOB_DEADLINES" ||
+              cf == "JOB_BACKOFF")
+            continue;
           if (first) {
             auto f = fields(r.at(2));
             ElementInstance ei;
@@ -1501,12 +1523,38 @@ class Oracle {
             j.retries = (int)L(f.at("retries"));
             j.deadline = L(f.at("deadline"));
             j.worker = f.at("worker");
+            if (f.count("errorMessageHex")) {  // a failed job's stored fields
+              j.fail_fields = true;
+              j.error_message = unhex(f.at("errorMessageHex"));
+              j.retry_backoff = L(f.at("retryBackoff"));
+              j.recurring_time = L(f.at("recurringTime"));
+            }
             jobs_[L(r.at(1))] = j;
           } else if (cf == "JOB_STATES") {
             const int64_t k = L(r.at(1));
             JobRow& j = jobs_.at(k);
             j.activated = r.at(2) == "ACTIVATED";
-            if (!j.activated) activatable_.insert({j.type, "<default>", k});
+            j.failed = r.at(2) == "FAILED";
+            if (!j.activated && !j.failed) activatable_.insert({j.type, "<default>", k});
+          } else if (cf == "INCIDENTS") {
+            auto f = fields(r.at(2));
+            IncidentRow in;
+            if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), in.pi.proc, in.pi.elem))
+              throw Unsupported{"incident element " + f.at("elementId")};
+            in.pi.piKey = L(f.at("processInstanceKey"));
+            in.eik = L(f.at("elementInstanceKey"));
+            in.error_type = (int)L(f.at("errorType"));
+            in.flow = (int)L(f.at("flow"));
+            in.result = (int)L(f.at("result"));
+            if (f.count("jobKey")) {
+              in.job_key = L(f.at("jobKey"));
+              in.message = unhex(f.at("messageHex"));
+            }
+            incidents_[L(r.at(1))] = in;
+          } else if (cf == "INCIDENT_PROCESS_INSTANCES") {
+            incident_pi_[L(r.at(1))] = L(r.at(2));
+          } else if (cf == "INCIDENT_JOBS") {
+            incident_jobs_[L(r.at(1))] = L(r.at(2));
           } else {
             throw Unsupported{"column family " + cf};
           }
@@ -1625,7 +1673,10 @@ class Oracle {
     int64_t eik = -1;   // elementInstanceKey (= variableScopeKey unless variable_scope says otherwise)
     int64_t variable_scope = -1;
     int error_type = 0, flow = -1, result = 0;  // the message: zbhip_incident_message
+    int64_t job_key = -1;       // a job's incident (JOB_NO_RETRIES): INCIDENT_JOBS, its errorMessage
+    std::string message;
   };
+  std::map<int64_t, int64_t> incident_jobs_;                    // INCIDENT_JOBS [jobKey -> incident]
   std::map<int64_t, IncidentRow> incidents_;                    // INCIDENTS
   std::map<int64_t, int64_t> incident_pi_;                      // INCIDENT_PROCESS_INSTANCES [eik -> incident]
   std::set<std::tuple<std::string, std::string, int64_t>> activatable_;  // JOB_ACTIVATABLE
@@ -1791,6 +1842,8 @@ class Oracle {
       create_process_instance(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_JOB && cmd.r.intent == ZBHIP_JOB_TIME_OUT)
       time_out_job(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_JOB && cmd.r.intent == ZBHIP_JOB_FAIL)
+      fail_job(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_JOB)
       complete_job(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_TIMER && cmd.r.intent == ZBHIP_TIMER_TRIGGER)
@@ -2303,6 +2356,11 @@ class Oracle {
              "Expected to complete job with key '" + std::to_string(jobKey) + "', but no such job was found");
       return;
     }
+    if (jit->second.failed) {  // DefaultJobCommandPreconditionGuard: ACTIVATABLE or ACTIVATED only
+      reject(cmd, ZBHIP_REJ_INVALID_STATE,
+             "Expected to complete job with key '" + std::to_string(jobKey) + "', but it is in state 'FAILED'");
+      return;
+    }
     JobRow job = jit->second;
     // accept(COMPLETED, job with command variables) -> event, JobCompletedApplier
     ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_COMPLETED, jobKey);
@@ -2348,6 +2406,7 @@ class Oracle {
     const int64_t jobKey = cmd.r.key;
     auto jit = jobs_.find(jobKey);
     const char* why = jit == jobs_.end() ? "no such job was found"
+                      : jit->second.failed ? "it is marked as failed and is not activated"
                       : !jit->second.activated ? "it must be activated first"
                       : !(jit->second.deadline < now_ms) ? "it has not timed out" : nullptr;
     if (why) {
@@ -2366,9 +2425,86 @@ class Oracle {
     activatable_.insert({job.type, "<default>", jobKey});
   }
 
+  // JobFailProcessor.processRecord / failJob (processing/job/JobFailProcessor.java:79-162): the job
+  // must be ACTIVATABLE or ACTIVATED (else NOT_FOUND / INVALID_STATE); JOB:FAILED with the stored job and
+  // the command's retries, errorMessage (limitString, 10000), retryBackoff and variables (recurringTime =
+  // timestamp + backoff when it retries later), the variables merged into the job's element instance
+  // (setFailedVariables), no retries left -> INCIDENT:CREATED (JOB_NO_RETRIES, "No more retries left."
+  // unless the job says otherwise; key = nextKey, jobKey, variableScopeKey = the element instance).
+  // JobFailedApplier -> DbJobState.fail (:191-203).  The command: retries in `partition`, retryBackoff in
+  // `message_key`, errorMessage's string id in `correlation_key`, its document in `aux`; timestamp = now.
+  void fail_job(ORecord& cmd) {
+    if (cmd.job_ord >= 0) cmd.r.key = resolve(cmd.instance, (uint32_t)cmd.job_ord);
+    const int64_t jobKey = cmd.r.key;
+    auto jit = jobs_.find(jobKey);
+    if (jit == jobs_.end()) {
+      reject(cmd, ZBHIP_REJ_NOT_FOUND, "Expected to fail job with key '" + std::to_string(jobKey) + "', but no such job was found");
+      return;
+    }
+    if (jit->second.failed) {
+      reject(cmd, ZBHIP_REJ_INVALID_STATE,
+             "Expected to fail job with key '" + std::to_string(jobKey) + "', but it is in state 'FAILED'");
+      return;
+    }
+    JobRow& job = jit->second;
+    const int retries = cmd.r.partition;
+    const int64_t backoff = cmd.r.message_key;
+    std::string msg = cmd.r.correlation_key < strs.size() ? strs[cmd.r.correlation_key] : std::string();
+    if (msg.size() > 10000) msg = msg.substr(0, 10000) + "...";  // StringUtil.limitString (ASCII)
+    job.retries = retries;
+    job.error_message = msg;
+    job.retry_backoff = backoff;
+    job.fail_fields = true;
+    if (retries > 0 && backoff > 0) job.recurring_time = now_ms + backoff;
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_FAILED, jobKey);
+    rec.r.process_idx = job.pi.proc;
+    rec.r.element_idx = job.pi.elem;
+    rec.r.scope_key = job.elementInstanceKey;
+    rec.r.process_instance_key = job.pi.piKey;
+    rec.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
+    rec.doc = cmd.doc;
+    job_activation_fields(rec, job);
+    // JobFailedApplier -> DbJobState.fail: updateJob(retries > 0: backoff ? FAILED : ACTIVATABLE; else FAILED)
+    job.activated = false;
+    job.failed = !(retries > 0 && backoff <= 0);
+    if (!job.failed) activatable_.insert({job.type, "<default>", jobKey});
+    else activatable_.erase({job.type, "<default>", jobKey});
+    // setFailedVariables: mergeLocalDocument into the job's element instance
+    merge_local_document(job.elementInstanceKey, job.pi.proc, job.pi.piKey, cmd.doc);
+    if (retries <= 0) {  // raiseIncident (:139-162)
+      const int64_t key = next_key();
+      ORecord& in = append(ZBHIP_RT_EVENT, ZBHIP_VT_INCIDENT, ZBHIP_INCIDENT_CREATED, key);
+      in.r.process_idx = job.pi.proc;
+      in.r.element_idx = job.pi.elem;
+      in.r.scope_key = job.elementInstanceKey;
+      in.r.process_instance_key = job.pi.piKey;
+      in.r.partition = ZBHIP_ERR_JOB_NO_RETRIES;
+      in.r.aux = jobKey;
+      const std::string text = msg.empty() ? "No more retries left." : msg;
+      in.r.correlation_key = intern_string(text);
+      IncidentRow row;
+      row.pi = job.pi;
+      row.eik = job.elementInstanceKey;
+      row.error_type = ZBHIP_ERR_JOB_NO_RETRIES;
+      row.job_key = jobKey;
+      row.message = text;
+      incidents_[key] = row;
+      incident_jobs_[jobKey] = key;
+    }
+  }
+
   // the stored job's deadline and worker (DbJobState.activate wrote them; a timed-out job keeps
-  // them): the zbhip_record fields message_key / correlation_key of a JOB record
+  // them): the zbhip_record fields message_key / correlation_key of a JOB record; a failed job's
+  // retries and errorMessage (reason_arg bit 0: partition = retries, message_name | bpmn_process_id
+  // << 16 = the errorMessage's string id)
   void job_activation_fields(ORecord& rec, const JobRow& job) {
+    if (job.fail_fields) {
+      rec.r.reason_arg = 1;
+      rec.r.partition = job.retries;
+      const uint32_t id = job.error_message.empty() ? ZBHIP_NO_STRING : intern_string(job.error_message);
+      rec.r.message_name = (uint16_t)(id & 0xFFFF);
+      rec.r.bpmn_process_id = (uint16_t)(id >> 16);
+    }
     if (job.deadline == -1 && job.worker.empty()) return;
     rec.r.message_key = job.deadline;
     rec.r.correlation_key = job.worker.empty() ? ZBHIP_NO_STRING : intern_string(job.worker);
@@ -3252,13 +3388,20 @@ std::string Oracle::dump_state() const {
     snprintf(buf, sizeof buf,
              "JOBS|%lld|type=%s,retries=%d,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
              "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
-             "deadline=%lld,worker=%s",
+             "deadline=%lld,worker=%s%s",
              (long long)k, j.type.c_str(), j.retries, p.els[j.pi.elem].id.c_str(), (long long)j.elementInstanceKey,
              (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version, (long long)j.deadline,
-             j.worker.c_str());
+             j.worker.c_str(),
+             j.fail_fields ? (",errorMessageHex=" + hex_of(j.error_message) + ",retryBackoff=" +
+                              std::to_string(j.retry_backoff) + ",recurringTime=" + std::to_string(j.recurring_time)).c_str()
+                           : "");
     rows.push_back(buf);
-    snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", (long long)k, j.activated ? "ACTIVATED" : "ACTIVATABLE");
+    snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", (long long)k, j.failed ? "FAILED" : j.activated ? "ACTIVATED" : "ACTIVATABLE");
     rows.push_back(buf);
+    if (j.failed && j.retries > 0 && j.retry_backoff > 0) {  // JOB_BACKOFF [recurringTime, jobKey] -> DbNil
+      snprintf(buf, sizeof buf, "JOB_BACKOFF|%lld|%lld", (long long)j.recurring_time, (long long)k);
+      rows.push_back(buf);
+    }
     if (j.activated) {  // JOB_DEADLINES [deadline, jobKey] -> DbNil
       snprintf(buf, sizeof buf, "JOB_DEADLINES|%lld|%lld", (long long)j.deadline, (long long)k);
       rows.push_back(buf);
@@ -3268,9 +3411,14 @@ std::string Oracle::dump_state() const {
     const OProc& p = procs[in.pi.proc];
     snprintf(buf, sizeof buf,
              "INCIDENTS|%lld|errorType=%d,flow=%d,result=%d,processDefinitionKey=%lld,processInstanceKey=%lld,"
-             "elementId=%s,elementInstanceKey=%lld",
+             "elementId=%s,elementInstanceKey=%lld%s",
              (long long)k, in.error_type, in.flow, in.result, (long long)p.def_key, (long long)in.pi.piKey,
-             p.els[in.pi.elem].id.c_str(), (long long)in.eik);
+             p.els[in.pi.elem].id.c_str(), (long long)in.eik,
+             in.job_key >= 0 ? (",jobKey=" + std::to_string(in.job_key) + ",messageHex=" + hex_of(in.message)).c_str() : "");
+    rows.push_back(buf);
+  }
+  for (auto& [j, k] : incident_jobs_) {  // INCIDENT_JOBS [jobKey] -> incident key (a job's incident)
+    snprintf(buf, sizeof buf, "INCIDENT_JOBS|%lld|%lld", (long long)j, (long long)k);
     rows.push_back(buf);
   }
   for (auto& [e, k] : incident_pi_) {

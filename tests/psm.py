@@ -558,6 +558,10 @@ class OracleEngine:
             self.next_slot += 1
         elif vt == abi.VT_TIMER:
             r["aux"] = v["dueDate"]
+        elif vt == abi.VT_JOB and it == abi.JOB_FAIL:  # zb_oracle.cpp fail_job's command fields
+            r["partition"] = v.get("retries", 0)
+            r["message_key"] = v.get("retryBackoff", 0)
+            r["correlation_key"] = self.o.intern_string(v["errorMessage"]) if v.get("errorMessage") else abi.NO_STRING
         elif vt == abi.VT_PROCESS_INSTANCE:
             p = self._proc_index(v)
             r["process_idx"] = p
@@ -656,6 +660,13 @@ class Client:
     def complete_job(key, variables=()):
         return Rec(abi.RT_COMMAND, abi.VT_JOB, abi.JOB_COMPLETE, key, {"variables": tuple(variables),
                                                                        "tenantId": "<default>"})
+
+    @staticmethod
+    def fail_job(key, retries, error_message="", variables=()):
+        """JobClient.fail (util/client/JobClient.java): JOB:FAIL with retries and an errorMessage."""
+        return Rec(abi.RT_COMMAND, abi.VT_JOB, abi.JOB_FAIL, key,
+                   {"retries": retries, "errorMessage": error_message, "retryBackoff": 0, "variables": tuple(variables),
+                    "tenantId": "<default>"})
 
     @staticmethod
     def publish_message(name, correlation_key, timestamp=0):

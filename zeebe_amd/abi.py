@@ -21,7 +21,8 @@ VT_TIMER = 15
 VT_PROCESS_INSTANCE_BATCH = 34
 VT_INCIDENT = 6
 INCIDENT_CREATED = 0
-ERR_CONDITION_ERROR, ERR_EXTRACT_VALUE_ERROR = 3, 4  # ErrorType ordinals
+ERR_JOB_NO_RETRIES, ERR_CONDITION_ERROR, ERR_EXTRACT_VALUE_ERROR = 2, 3, 4  # ErrorType ordinals
+ERROR_TYPES = {2: "JOB_NO_RETRIES", 3: "CONDITION_ERROR", 4: "EXTRACT_VALUE_ERROR"}
 FEEL_NULL, FEEL_NUMBER, FEEL_STRING = 0, 1, 2       # zbhip_record.reason_arg of an INCIDENT
 
 REJ_INVALID_ARGUMENT, REJ_NOT_FOUND, REJ_ALREADY_EXISTS, REJ_INVALID_STATE = 0, 1, 2, 3
@@ -223,3 +224,9 @@ def record_tuple(r, element_id=None, name=None):
             int(r["process_instance_key"]), int(r["process_idx"]), int(r["element_idx"]), int(r["aux"]),
             int(r["message_key"]), int(r["correlation_key"]), int(r["message_name"]), int(r["bpmn_process_id"]),
             int(r["partition"]), int(r["interrupting"]))
+
+
+class JobFail(C.Structure):
+    """zbhip_job_fail (JOB:FAIL of a device job)."""
+    _fields_ = [("job_key", C.c_int64), ("retry_backoff", C.c_int64), ("error_message", C.c_char_p),
+                ("error_message_len", C.c_size_t), ("retries", C.c_int32), ("n_variables", C.c_uint32)]

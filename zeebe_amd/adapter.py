@@ -139,10 +139,11 @@ class RecordValues:
     """zbhip_record rows -> the reference's record values (Window.value).  `procs` are the
     deployment's ProcessDefinitions (by process index), `name` the variable-name dictionary."""
 
-    def __init__(self, procs, name, string_value=None):
+    def __init__(self, procs, name, string_value=None, incident_message=None):
         self.procs = procs
         self.name = name
         self.string_value = string_value  # value-dictionary id -> str (inline STR values)
+        self.incident_message = incident_message  # a gateway incident's errorMessage (zbhip_incident_message)
 
     def value(self, r, command_doc=(), entry_value=None, timestamp=0):
         """`timestamp`: the source command's (a MESSAGE record's deadline = timestamp + timeToLive)."""
@@ -166,7 +167,21 @@ class RecordValues:
                 cid = int(r["correlation_key"])
                 v.update({"deadline": int(r["message_key"]),
                           "worker": self.string_value(cid) if cid != abi.NO_STRING else ""})
+            if int(r["record_type"]) == abi.RT_EVENT and int(r["reason_arg"]) & 1:
+                # a failed job's stored retries and errorMessage (JobFailProcessor.failJob)
+                eid = int(r["message_name"]) | int(r["bpmn_process_id"]) << 16
+                v.update({"retries": int(r["partition"]),
+                          "errorMessage": self.string_value(eid) if eid != abi.NO_STRING else ""})
             return v
+        if vt == abi.VT_INCIDENT:  # IncidentRecord.java:36-47
+            et = int(r["partition"])
+            job = et == abi.ERR_JOB_NO_RETRIES
+            msg = self.string_value(int(r["correlation_key"])) if job else \
+                (self.incident_message(r) if self.incident_message else "")
+            return {"errorType": abi.ERROR_TYPES.get(et, str(et)), "errorMessage": msg,
+                    "bpmnProcessId": p.bpmn_process_id, "processDefinitionKey": p.definition_key,
+                    "processInstanceKey": pik, "elementId": p.element_ids[elem], "elementInstanceKey": scope,
+                    "jobKey": aux if job else -1, "variableScopeKey": scope, "tenantId": TENANT}
         if vt == abi.VT_VARIABLE:
             # ZBHIP_AUX_INLINE: a value the engine computed (multi-instance loop variables)
             val = typed_value(int(r["partition"]), int(r["message_key"]), self.string_value) \
@@ -412,7 +427,7 @@ class GpuBatchProcessor:
         # what went where (tests read these)
         self.fallback_reasons = []
         self.counts = {"windows": 0, "device_commands": 0, "continuations": 0, "fallbacks": 0, "activations": 0,
-                       "engine_commands": 0, "followups_answered": 0, "time_outs": 0}
+                       "engine_commands": 0, "followups_answered": 0, "time_outs": 0, "job_failures": 0}
 
     # ---- RecordProcessor ----------------------------------------------------------------------
     def init(self):
@@ -424,7 +439,7 @@ class GpuBatchProcessor:
                               initial_key=self.key_generator.current_key() - pbits, defer_continuations=True)
         for xml, key, version in self.deployments:
             self.deploy(xml, key, version)
-        self.values = RecordValues(self.part.processes, self.part.name, self.part.string_value)
+        self.values = RecordValues(self.part.processes, self.part.name, self.part.string_value, self.part.incident_message)
 
     def deploy(self, xml, key, version):
         from .native import ZbhipError
@@ -494,6 +509,8 @@ class GpuBatchProcessor:
             return self._activate_jobs(record, out)
         if record.value_type == abi.VT_JOB and record.intent == abi.JOB_TIME_OUT and self._resolve(record.key) is not None:
             return self._time_out_job(record, out)
+        if record.value_type == abi.VT_JOB and record.intent == abi.JOB_FAIL and self._resolve(record.key) is not None:
+            return self._fail_job(record, out)
         i = self.window.index_of(record.position) if self.window.covers(record.position) else -1
         if i < 0:
             if not self._hot(record, 0):
@@ -889,6 +906,33 @@ class GpuBatchProcessor:
                 del self.pms_handles[sub]
                 if sub in self.pending_pms:
                     self.moved_pending.append((sub, self.pending_pms.pop(sub)))
+
+    # ---- JOB:FAIL of a device job (JobFailProcessor.java:79-162) -------------------------------------
+    def _fail_job(self, record, out):
+        v = record.value
+        self.part.set_key_if_higher(self.key_generator.current_key())
+        recs = self.part.fail_job(record.key, v.get("retries", 0), v.get("errorMessage", ""), v.get("retryBackoff", 0),
+                                  len(v.get("variables", ())))
+        if recs is None:  # outside the device subset (variables, a back-off): the engine's, with the instance
+            self._hand_off(self._resolve(record.key)[0])
+            self.key_generator.set_key_if_higher(self.part.current_key())
+            self.engine_batch = True
+            return self.engine.process(record, out)
+        self.counts["job_failures"] += 1
+        incident = False
+        for r in recs:
+            rt, vt, it = int(r["record_type"]), int(r["value_type"]), int(r["intent"])
+            if rt == abi.RT_REJECTION:
+                out.append_record(record.key, rt, vt, it, int(r["rejection_type"]), self.part.reason(r), dict(v))
+                continue
+            out.append_record(int(r["key"]), rt, vt, it, abi.REJ_NONE, "", self.values.value(r))
+            incident |= vt == abi.VT_INCIDENT
+        self.key_generator.set_key_if_higher(self.part.current_key())
+        if incident:
+            # the instance waits for the incident's resolution (JOB:UPDATE_RETRIES, INCIDENT:RESOLVE): the
+            # engine's, with the job's FAILED state and the incident rows
+            self._hand_off(self._resolve(record.key)[0])
+        return out.build()
 
     # ---- JOB:TIME_OUT of a device job (JobTimeOutProcessor.java:46-73) ------------------------------
     def _time_out_job(self, record, out):

@@ -332,10 +332,17 @@ int zbhip_serializer_rejection_reason(zbhip_serializer* s, const zbhip_record* r
     case ZBHIP_REASON_TIMER_NOT_ACTIVE:  // TriggerTimerProcessor.java:42-43
       return snprintf(buf, cap, "Expected to trigger a timer with key '%lld', but the timer is not active anymore",
                       (long long)r->key);
+    case ZBHIP_REASON_JOB_STATE: {  // JobCommandPreconditionChecker.java:19-49
+      const char* verb = r->intent == ZBHIP_JOB_FAIL ? "fail" : r->intent == ZBHIP_JOB_COMPLETE ? "complete" : "update";
+      if (r->reason_arg == 3)
+        return snprintf(buf, cap, "Expected to %s job with key '%lld', but no such job was found", verb, (long long)r->key);
+      return snprintf(buf, cap, "Expected to %s job with key '%lld', but it is in state '%s'", verb, (long long)r->key,
+                      r->reason_arg == 2 ? "FAILED" : r->reason_arg == 1 ? "ACTIVATED" : "ACTIVATABLE");
+    }
     case ZBHIP_REASON_JOB_TIME_OUT:  // JobTimeOutProcessor.java:26-27,57-66
       return snprintf(buf, cap, "Expected to time out activated job with key '%lld', but %s", (long long)r->key,
                       r->reason_arg == 0 ? "no such job was found" : r->reason_arg == 1 ? "it must be activated first"
-                                                                       : "it has not timed out");
+                      : r->reason_arg == 3 ? "it is marked as failed and is not activated" : "it has not timed out");
     default:
       if (cap) buf[0] = 0;
       return 0;
@@ -676,6 +683,12 @@ namespace {
 void dbl(Bytes& b, int64_t v) { be64(b, (uint64_t)v); }
 void dbs(Bytes& b, const std::string& s) { be32(b, (uint32_t)s.size()); b.append(s); }
 void cf_prefix(Bytes& b, uint32_t cf) { be64(b, cf); }
+// a string a state row holds in hex (error messages may contain ',' and '|')
+std::string unhex(const std::string& h) {
+  std::string o;
+  for (size_t i = 0; i + 1 < h.size(); i += 2) o += (char)std::stoi(h.substr(i, 2), nullptr, 16);
+  return o;
+}
 
 std::vector<std::string> split(const std::string& s, char sep) {
   std::vector<std::string> out;
@@ -805,15 +818,16 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     mp_map(v, 1);  // JobRecordValue.java:21 -> JobRecord stored without variables (DbJobState.create)
     key(v, "jobRecord");
     mp_map(v, 17);
+    const bool failed = f.count("errorMessageHex") != 0;  // a failed job's stored fields (JobFailProcessor)
     key(v, "deadline"); mp_int(v, f.count("deadline") ? ll(f["deadline"]) : -1);
     key(v, "worker"); mp_str(v, f["worker"]);
     key(v, "retries"); mp_int(v, ll(f["retries"]));
-    key(v, "retryBackoff"); mp_int(v, 0);
-    key(v, "recurringTime"); mp_int(v, -1);
+    key(v, "retryBackoff"); mp_int(v, failed ? ll(f["retryBackoff"]) : 0);
+    key(v, "recurringTime"); mp_int(v, failed ? ll(f["recurringTime"]) : -1);
     key(v, "type"); mp_str(v, f["type"]);
     key(v, "customHeaders"); v += kEmptyDoc;
     key(v, "variables"); mp_bin(v, kEmptyDoc);
-    key(v, "errorMessage"); key(v, "");
+    key(v, "errorMessage"); mp_str(v, failed ? unhex(f["errorMessageHex"]) : std::string());
     key(v, "errorCode"); key(v, "");
     key(v, "bpmnProcessId"); mp_str(v, f["bpmnProcessId"]);
     key(v, "processDefinitionVersion"); mp_int(v, ll(f["processDefinitionVersion"]));
@@ -843,23 +857,36 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     for (size_t q = 0; q < s->procs.size(); ++q)
       if (s->procs[q].def_key == def) { pi = (int32_t)q; break; }
     std::string msg;
-    if (pi < 0 || !incident_message(s, pi, (int32_t)ll(f["errorType"]), ll(f["flow"]), (uint32_t)ll(f["result"]), msg))
+    const bool job = f.count("jobKey") != 0;  // a job's incident (JOB_NO_RETRIES): its key and message
+    if (job) msg = unhex(f["messageHex"]);
+    if (pi < 0 ||
+        (!job && !incident_message(s, pi, (int32_t)ll(f["errorType"]), ll(f["flow"]), (uint32_t)ll(f["result"]), msg)))
       return ZBHIP_EINVAL;
     const SerProcess& P = s->procs[pi];
     cf_prefix(k, ord); dbl(k, ll(p[1]));
     mp_map(v, 1);
     key(v, "incidentRecord");
     mp_map(v, 10);  // IncidentRecord.java:36-47
-    key(v, "errorType"); key(v, ll(f["errorType"]) == ZBHIP_ERR_CONDITION_ERROR ? "CONDITION_ERROR" : "EXTRACT_VALUE_ERROR");
+    const int64_t et = ll(f["errorType"]);
+    key(v, "errorType");
+    key(v, et == ZBHIP_ERR_JOB_NO_RETRIES ? "JOB_NO_RETRIES" : et == ZBHIP_ERR_CONDITION_ERROR ? "CONDITION_ERROR" : "EXTRACT_VALUE_ERROR");
     key(v, "errorMessage"); mp_str(v, msg);
     key(v, "bpmnProcessId"); mp_str(v, P.bpmn_id);
     key(v, "processDefinitionKey"); mp_int(v, def);
     key(v, "processInstanceKey"); mp_int(v, ll(f["processInstanceKey"]));
     key(v, "elementId"); mp_str(v, f["elementId"]);
     key(v, "elementInstanceKey"); mp_int(v, ll(f["elementInstanceKey"]));
-    key(v, "jobKey"); mp_int(v, -1);
+    key(v, "jobKey"); mp_int(v, job ? ll(f["jobKey"]) : -1);
     key(v, "variableScopeKey"); mp_int(v, ll(f["elementInstanceKey"]));
     key(v, "tenantId"); key(v, kTenant);
+  } else if (cf == "INCIDENT_JOBS" && need(3)) {
+    ord = 36;  // DbForeignKey<DbLong> jobKey -> IncidentKey{key} (DbIncidentState.java:68-71)
+    cf_prefix(k, ord); dbl(k, ll(p[1]));
+    mp_map(v, 1); key(v, "key"); mp_int(v, ll(p[2]));
+  } else if (cf == "JOB_BACKOFF" && need(3)) {
+    ord = 42;  // [recurringTime, jobKey] -> DbNil (DbJobState.java:103-108)
+    cf_prefix(k, ord); dbl(k, ll(p[1])); dbl(k, ll(p[2]));
+    v.push_back((char)0xff);
   } else if (cf == "INCIDENT_PROCESS_INSTANCES" && need(3)) {
     ord = 35;  // DbForeignKey<DbLong> elementInstanceKey -> IncidentKey{key} (IncidentKey.java)
     cf_prefix(k, ord); dbl(k, ll(p[1]));

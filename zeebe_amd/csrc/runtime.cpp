@@ -76,6 +76,17 @@ using namespace zb;
 
 namespace {
 
+// hex of a string inside a state row (error messages may hold ',' and '|')
+std::string hex_of(const std::string& v) {
+  static const char* d = "0123456789abcdef";
+  std::string o;
+  for (unsigned char c : v) {
+    o += d[c >> 4];
+    o += d[c & 15];
+  }
+  return o;
+}
+
 struct Proc {
   std::vector<zbhip_element> els;
   std::vector<uint16_t> out;
@@ -661,7 +672,7 @@ struct zbhip_handle {
   // A job whose stored JobRecord differs from the one JOB:CREATED wrote (slot flag bit 1 on the device):
   // the deadline and worker DbJobState.activate stored, kept when the job timed out
   // (DbJobState.timeout :142-150), and its JOB_STATES value.
-  enum : uint8_t { JS_ACTIVATED = 0, JS_ACTIVATABLE = 1, JS_GONE = 2 };  // (GONE: completed / canceled)
+  enum : uint8_t { JS_ACTIVATED = 0, JS_ACTIVATABLE = 1, JS_GONE = 2, JS_FAILED = 3 };  // (GONE: completed / canceled)
   struct Activation {
     int64_t deadline;
     std::string worker;
@@ -670,6 +681,12 @@ struct zbhip_handle {
     uint8_t state = JS_ACTIVATED;
     int64_t eik = -1, pik = -1;  // the job's element instance and process instance
     int32_t proc = -1, elem = -1;
+    // JobFailProcessor.failJob stored them (zbhip_fail_job): retries and errorMessage from then on
+    bool fail_fields = false;
+    int32_t retries = 0;
+    uint32_t error_id = ZBHIP_NO_STRING;  // the errorMessage in the value dictionary
+    int64_t incident_key = -1;            // its JOB_NO_RETRIES incident (INCIDENTS, INCIDENT_JOBS)
+    uint32_t incident_msg_id = ZBHIP_NO_STRING;
   };
   std::unordered_map<int64_t, Activation> activated;  // jobs with a stored activation: deadline, worker, state
   DueTimer* d_due = nullptr;                          // zbhip_due_timers: [max_instances] due rows
@@ -2712,6 +2729,12 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
         if (it != h->activated.end()) {
           r.message_key = it->second.deadline;
           r.correlation_key = it->second.worker_id;
+          if (it->second.fail_fields) {  // a failed job's retries and errorMessage
+            r.reason_arg = 1;
+            r.partition = it->second.retries;
+            r.message_name = (uint16_t)(it->second.error_id & 0xFFFF);
+            r.bpmn_process_id = (uint16_t)(it->second.error_id >> 16);
+          }
         }
       }
     } else if (c6 == C_VAR_CREATED || c6 == C_VAR_UPDATED) {
@@ -3386,23 +3409,41 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       const char* type = P.strings[E.job_type].c_str();
       const bool stored = (e.y >> 25) & 1;  // a stored activation (zbhip_activate_jobs): deadline, worker, state on the host
       const auto ait = stored ? h->activated.find(jk) : h->activated.end();
-      const long long deadline = ait != h->activated.end() ? (long long)ait->second.deadline : -1;
-      const bool act = ait != h->activated.end() && ait->second.state == zbhip_handle::JS_ACTIVATED;
+      const zbhip_handle::Activation* A = ait != h->activated.end() ? &ait->second : nullptr;
+      const long long deadline = A ? (long long)A->deadline : -1;
+      const bool act = A && A->state == zbhip_handle::JS_ACTIVATED;
+      const bool failed = A && A->state == zbhip_handle::JS_FAILED;
+      std::string fail_suffix;  // a failed job's stored fields (errorMessage in hex: it may hold ',' or '|')
+      if (A && A->fail_fields)
+        fail_suffix = ",errorMessageHex=" + hex_of(A->error_id == ZBHIP_NO_STRING ? std::string() : h->strs[A->error_id]) +
+                      ",retryBackoff=0,recurringTime=-1";
       snprintf(buf, sizeof buf,
-               "JOBS|%lld|type=%s,retries=%u,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
+               "JOBS|%lld|type=%s,retries=%d,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
                "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
-               "deadline=%lld,worker=%s",
-               jk, type, E.job_retries, P.id(elem).c_str(), k, pik, P.strings[P.bpmn_id].c_str(), (long long)P.def_key,
-               P.version, deadline, ait != h->activated.end() ? ait->second.worker.c_str() : "");
+               "deadline=%lld,worker=%s%s",
+               jk, type, A && A->fail_fields ? A->retries : (int)E.job_retries, P.id(elem).c_str(), k, pik,
+               P.strings[P.bpmn_id].c_str(), (long long)P.def_key, P.version, deadline, A ? A->worker.c_str() : "",
+               fail_suffix.c_str());
       sink(ctx, buf);
-      snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", jk, act ? "ACTIVATED" : "ACTIVATABLE");
+      snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", jk, failed ? "FAILED" : act ? "ACTIVATED" : "ACTIVATABLE");
       sink(ctx, buf);
       if (act) {
         snprintf(buf, sizeof buf, "JOB_DEADLINES|%lld|%lld", deadline, jk);
-      } else {
+        sink(ctx, buf);
+      } else if (!failed) {
         snprintf(buf, sizeof buf, "JOB_ACTIVATABLE|%s|<default>|%lld", type, jk);
+        sink(ctx, buf);
       }
-      sink(ctx, buf);
+      if (A && A->incident_key >= 0) {  // its JOB_NO_RETRIES incident (DbIncidentState.createIncident)
+        snprintf(buf, sizeof buf,
+                 "INCIDENTS|%lld|errorType=%d,flow=-1,result=0,processDefinitionKey=%lld,processInstanceKey=%lld,"
+                 "elementId=%s,elementInstanceKey=%lld,jobKey=%lld,messageHex=%s",
+                 (long long)A->incident_key, (int)ZBHIP_ERR_JOB_NO_RETRIES, (long long)P.def_key, pik, P.id(elem).c_str(),
+                 k, jk, hex_of(A->incident_msg_id == ZBHIP_NO_STRING ? std::string() : h->strs[A->incident_msg_id]).c_str());
+        sink(ctx, buf);
+        snprintf(buf, sizeof buf, "INCIDENT_JOBS|%lld|%lld", jk, (long long)A->incident_key);
+        sink(ctx, buf);
+      }
     }
   }
   for (uint32_t v = 0; v < nvars; ++v) {
@@ -3728,6 +3769,9 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     int64_t eik, pik;
     std::string element_id;
     int32_t elem;  // (set where the job's element instance is rebuilt)
+    bool failed_fields;  // JobFailProcessor stored retries / errorMessage (hex in the row)
+    int32_t retries;
+    std::string error_hex;
   };
   std::map<int64_t, JobMeta> job_meta;
   std::vector<ImpPms> pms;
@@ -3767,7 +3811,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       job_rows.insert(to_ll(p[1]));
       auto f = row_fields(p[2]);
       job_act[to_ll(p[1])] = {f.count("deadline") ? to_ll(f["deadline"]) : -1, f["worker"]};
-      job_meta[to_ll(p[1])] = {to_ll(f["elementInstanceKey"]), to_ll(f["processInstanceKey"]), f["elementId"], -1};
+      job_meta[to_ll(p[1])] = {to_ll(f["elementInstanceKey"]), to_ll(f["processInstanceKey"]), f["elementId"], -1,
+                               f.count("errorMessageHex") != 0, (int32_t)to_ll(f["retries"]), f["errorMessageHex"]};
     } else if (cf == "JOB_STATES" && p.size() >= 3) {
       if (p[2] == "ACTIVATED") job_activated_state.insert(to_ll(p[1]));
       else if (p[2] != "ACTIVATABLE") return ZBHIP_EUNSUPP;  // failed / error-thrown jobs: outside the subset
@@ -3942,8 +3987,10 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
                      : e.job == 0 ? JOB_ZERO : e.job == -1 ? JOB_MINUS1 : ord(e.job);
       // (flag bit 1: a stored activation -- ACTIVATED, or timed out with its deadline and worker kept)
       const auto ja = job_act.find(e.job);
+      const auto jmf = job_meta.find(e.job);
       const bool stored = job_activated_state.count(e.job) ||
-                          (ja != job_act.end() && (ja->second.first != -1 || !ja->second.second.empty()));
+                          (ja != job_act.end() && (ja->second.first != -1 || !ja->second.second.empty())) ||
+                          (jmf != job_meta.end() && jmf->second.failed_fields);
       uint32_t row = !sub_el && !body && e.job > 0 && job_rows.count(e.job) ? (stored ? 3u : 1u) : 0u;
       if (row) {
         const auto jm = job_meta.find(e.job);
@@ -4054,7 +4101,8 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   h->published |= stats_row;
   for (const Done& d : done)
     for (int64_t k : d.keys)
-      if (job_act.count(k) && (job_activated_state.count(k) || job_act[k].first != -1 || !job_act[k].second.empty())) {
+      if (job_act.count(k) && (job_activated_state.count(k) || job_act[k].first != -1 || !job_act[k].second.empty() ||
+                               (job_meta.count(k) && job_meta[k].failed_fields))) {
         const std::string& wk = job_act[k].second;
         const int64_t wid = wk.empty() ? (int64_t)ZBHIP_NO_STRING : zbhip_intern_string(h, wk.data(), wk.size());
         if (wid < 0) return (int)wid;
@@ -4067,6 +4115,17 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
           a.pik = jm->second.pik;
           a.proc = (int32_t)(hdr[d.slot].x & 0xFFFF);
           a.elem = jm->second.elem;
+          if (jm->second.failed_fields) {  // a failed job with retries left (a FAILED one is refused above)
+            std::string msg;
+            const std::string& hx = jm->second.error_hex;
+            for (size_t q = 0; q + 1 < hx.size(); q += 2) msg += (char)std::stoi(hx.substr(q, 2), nullptr, 16);
+            const int64_t eid = msg.empty() ? (int64_t)ZBHIP_NO_STRING : zbhip_intern_string(h, msg.data(), msg.size());
+            if (eid < 0) return (int)eid;
+            a.fail_fields = true;
+            a.retries = jm->second.retries;
+            a.error_id = (uint32_t)eid;
+            h->ring_ok = false;
+          }
         }
       }
   h->job_index_on = false;  // rebuilt from the device rows at the next activation
@@ -4371,8 +4430,13 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     }
     // JobBatchActivatedApplier -> DbJobState.activate: ACTIVATED, out of JOB_ACTIVATABLE, deadline
     h->job_index.erase({tit->second, j.key});
-    zbhip_handle::Activation& act = h->activated[j.key];
-    act = {j.deadline, worker, inst, worker_id};
+    zbhip_handle::Activation& act = h->activated[j.key];  // (a failed job keeps its retries / errorMessage)
+    act.deadline = j.deadline;
+    act.worker = worker;
+    act.inst = inst;
+    act.worker_id = worker_id;
+    act.state = zbhip_handle::JS_ACTIVATED;
+    if (act.fail_fields) j.retries = act.retries;
     act.eik = j.element_instance_key;
     act.pik = j.process_instance_key;
     act.proc = j.process_idx;
@@ -4483,6 +4547,12 @@ static void stored_job_record(const zbhip_handle::Activation& a, int64_t key, ui
   r.message_key = a.deadline;
   r.correlation_key = a.worker_id;
   r.message_name = r.bpmn_process_id = 0xFFFF;
+  if (a.fail_fields) {  // a failed job's retries and errorMessage (zbhip_record, JOB records)
+    r.reason_arg = 1;
+    r.partition = a.retries;
+    r.message_name = (uint16_t)(a.error_id & 0xFFFF);
+    r.bpmn_process_id = (uint16_t)(a.error_id >> 16);
+  }
 }
 
 extern "C" int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out) {
@@ -4509,7 +4579,7 @@ extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now,
   // JobTimeOutProcessor.processRecord (:46-69): an ACTIVATED job past its deadline times out, anything
   // else is rejected NOT_FOUND with the job's state
   auto it = h->activated.find(job_key);
-  uint8_t why = 0;  // reason_arg: 0 no such job, 1 not activated, 2 not timed out
+  uint8_t why = 0;  // reason_arg: 0 no such job, 1 not activated, 2 not timed out, 3 failed
   if (it != h->activated.end()) {
     if (it->second.state == zbhip_handle::JS_ACTIVATED) {
       if (it->second.deadline < now) {
@@ -4526,7 +4596,7 @@ extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now,
       }
       why = 2;
     } else {
-      why = it->second.state == zbhip_handle::JS_GONE ? 0 : 1;
+      why = it->second.state == zbhip_handle::JS_GONE ? 0 : it->second.state == zbhip_handle::JS_FAILED ? 3 : 1;
     }
   } else {
     // no stored activation: an ACTIVATABLE job of a live instance, or none at all
@@ -4553,6 +4623,126 @@ extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now,
   out->correlation_key = ZBHIP_NO_STRING;
   out->message_name = out->bpmn_process_id = 0xFFFF;
   return ZBHIP_OK;
+}
+
+extern "C" int zbhip_fail_job(zbhip_handle* h, const zbhip_job_fail* cmd, zbhip_record* out, size_t cap, size_t* n_out) {
+  if (!h || !cmd || !n_out || (cap && !out) || (cmd->error_message_len && !cmd->error_message)) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (cap < 2) return ZBHIP_ENOMEM;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  const int64_t job_key = cmd->job_key;
+  auto reject = [&](uint8_t type, uint8_t state) {  // JobCommandPreconditionChecker.check (:33-49)
+    zbhip_record& r = out[0];
+    r = zbhip_record{};
+    r.key = job_key;
+    r.record_type = ZBHIP_RT_REJECTION;
+    r.value_type = ZBHIP_VT_JOB;
+    r.intent = ZBHIP_JOB_FAIL;
+    r.rejection_type = type;
+    r.reason = ZBHIP_REASON_JOB_STATE;
+    r.reason_arg = state;
+    r.scope_key = r.process_instance_key = r.aux = r.message_key = r.source_index = -1;
+    r.process_idx = r.element_idx = -1;
+    r.correlation_key = ZBHIP_NO_STRING;
+    r.message_name = r.bpmn_process_id = 0xFFFF;
+    *n_out = 1;
+    return ZBHIP_OK;
+  };
+  auto it = h->activated.find(job_key);
+  if (it != h->activated.end() && it->second.state == zbhip_handle::JS_GONE) return reject(ZBHIP_REJ_NOT_FOUND, 3);
+  if (it != h->activated.end() && it->second.state == zbhip_handle::JS_FAILED) return reject(ZBHIP_REJ_INVALID_STATE, 2);
+  // the job row on the device (ACTIVATABLE, or ACTIVATED with a stored activation)
+  uint32_t inst;
+  uint16_t ord;
+  if (zbhip_resolve_key(h, job_key, &inst, &ord) != ZBHIP_OK || inst >= h->cfg.max_instances)
+    return reject(ZBHIP_REJ_NOT_FOUND, 3);
+  InstRows R{};
+  if (int rc = gather_instance(h, inst, R)) return rc;
+  const uint32_t nslots = (R.hdr.y >> 8) & 0xFF, proc = R.hdr.x & 0xFFFF;
+  int slot = -1;
+  for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s)
+    if ((R.slots[s].y & 0xFFFF) == ord && ((R.slots[s].y >> 24) & 1u)) slot = (int)s;
+  if (slot < 0 || !((R.hdr.y >> 24) & 1u) || proc >= h->procs.size()) return reject(ZBHIP_REJ_NOT_FOUND, 3);
+  // the device subset: no variables (setFailedVariables), no retry back-off (JobBackoffChecker)
+  if (cmd->n_variables || (cmd->retries > 0 && cmd->retry_backoff > 0)) return ZBHIP_EUNSUPP;
+  std::string msg(cmd->error_message ? cmd->error_message : "", cmd->error_message_len);
+  if (msg.size() > 10000) msg = msg.substr(0, 10000) + "...";  // StringUtil.limitString (ASCII)
+  const int64_t eid = msg.empty() ? (int64_t)ZBHIP_NO_STRING : zbhip_intern_string(h, msg.data(), msg.size());
+  if (eid < 0) return (int)eid;
+  const uint32_t elem = R.slots[slot].x & 0xFFFF;
+  const Proc& P = h->procs[proc];
+  if (elem >= P.els.size()) return ZBHIP_EDEVICE;
+  const bool had = it != h->activated.end();
+  zbhip_handle::Activation& a = h->activated[job_key];
+  if (!had) {  // the first stored field of this job: the slot's flag bit 1 makes its later records read them
+    a.deadline = -1;
+    a.inst = inst;
+    a.worker_id = ZBHIP_NO_STRING;
+    a.eik = h->key_of(inst, R.slots[slot].x >> 16);
+    a.pik = h->key_of(inst, 0);
+    a.proc = (int32_t)proc;
+    a.elem = (int32_t)elem;
+    uint2 w = R.slots[slot];
+    w.y |= 2u << 24;
+    HIPCHK(hipMemcpy(h->st.slots + (size_t)slot * h->st.n + inst, &w, sizeof w, hipMemcpyHostToDevice));
+  }
+  a.fail_fields = true;
+  a.retries = cmd->retries;
+  a.error_id = (uint32_t)eid;
+  h->ring_ok = false;  // the device log writer does not write failed jobs' fields: the host serialiser does
+  // JOB:FAILED: the stored job with the command's retries / errorMessage (retryBackoff 0, no variables)
+  stored_job_record(a, job_key, ZBHIP_RT_EVENT, ZBHIP_JOB_FAILED, out[0]);
+  *n_out = 1;
+  // JobFailedApplier -> DbJobState.fail (:191-203): ACTIVATABLE again with retries left, else FAILED
+  const uint32_t tid = P.job_type_id[elem];
+  if (cmd->retries > 0) {
+    a.state = zbhip_handle::JS_ACTIVATABLE;
+    if (h->job_index_on) h->job_index[{tid, job_key}] = {inst, ord};
+    return ZBHIP_OK;
+  }
+  a.state = zbhip_handle::JS_FAILED;
+  if (h->job_index_on) h->job_index.erase({tid, job_key});
+  // raiseIncident (:139-162): INCIDENT:CREATED, key = keyGenerator.nextKey (no instance's ordinal)
+  const std::string text = msg.empty() ? std::string("No more retries left.") : msg;
+  const int64_t tid_msg = zbhip_intern_string(h, text.data(), text.size());
+  if (tid_msg < 0) return (int)tid_msg;
+  a.incident_key = ((int64_t)h->cfg.partition_id << 51) + ++h->key_counter;
+  a.incident_msg_id = (uint32_t)tid_msg;
+  if (h->st.n_slots) {
+    const unsigned long long kc = (unsigned long long)h->key_counter;
+    HIPCHK(hipMemcpy(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice));
+  }
+  zbhip_record& r = out[1];
+  r = zbhip_record{};
+  r.key = a.incident_key;
+  r.record_type = ZBHIP_RT_EVENT;
+  r.value_type = ZBHIP_VT_INCIDENT;
+  r.intent = ZBHIP_INCIDENT_CREATED;
+  r.rejection_type = ZBHIP_REJ_NONE;
+  r.scope_key = a.eik;
+  r.process_instance_key = a.pik;
+  r.process_idx = a.proc;
+  r.element_idx = a.elem;
+  r.partition = ZBHIP_ERR_JOB_NO_RETRIES;
+  r.aux = job_key;
+  r.correlation_key = a.incident_msg_id;
+  r.source_index = r.message_key = -1;
+  r.message_name = r.bpmn_process_id = 0xFFFF;
+  *n_out = 2;
+  return ZBHIP_OK;
+}
+
+extern "C" int zbhip_job_state(zbhip_handle* h, int64_t job_key) {
+  if (!h) return ZBHIP_EINVAL;
+  auto it = h->activated.find(job_key);
+  if (it == h->activated.end()) return -1;  // none stored: ACTIVATABLE if the key is a live job's
+  switch (it->second.state) {
+    case zbhip_handle::JS_ACTIVATED: return 1;
+    case zbhip_handle::JS_ACTIVATABLE: return 0;
+    case zbhip_handle::JS_FAILED: return 2;
+    default: return 3;
+  }
 }
 
 // ---- log bytes on the device (logdev.hip) ----------------------------------------------------------

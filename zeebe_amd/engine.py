@@ -436,6 +436,24 @@ class Partition:
         check(self.L.zbhip_time_out_job(self.h, int(job_key), int(now), out.ctypes.data), "zbhip_time_out_job")
         return out[0]
 
+    def fail_job(self, job_key, retries, error_message="", retry_backoff=0, n_variables=0):
+        """JOB:FAIL of a device job (zbhip_fail_job): the JOB:FAILED (+ INCIDENT:CREATED) or rejection
+        records, RECORD_DTYPE rows; None when the command is outside the device subset (the engine's)."""
+        m = error_message.encode()
+        cmd = abi.JobFail(job_key=int(job_key), retry_backoff=int(retry_backoff), error_message=m,
+                          error_message_len=len(m), retries=int(retries), n_variables=int(n_variables))
+        out = np.zeros(2, dtype=abi.RECORD_DTYPE)
+        n = C.c_size_t()
+        rc = self.L.zbhip_fail_job(self.h, C.byref(cmd), out.ctypes.data, 2, C.byref(n))
+        if rc == -5:
+            return None
+        check(rc, "zbhip_fail_job")
+        return out[: n.value]
+
+    def job_state(self, job_key):
+        """zbhip_job_state: 0 ACTIVATABLE, 1 ACTIVATED, 2 FAILED, 3 gone, -1 nothing stored."""
+        return self.L.zbhip_job_state(self.h, int(job_key))
+
     def resolve_key(self, key):
         inst, ordv = C.c_uint32(), C.c_uint16()
         check(self.L.zbhip_resolve_key(self.h, key, C.byref(inst), C.byref(ordv)), "unknown key %d" % key)
