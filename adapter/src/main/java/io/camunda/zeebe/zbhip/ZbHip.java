@@ -209,7 +209,15 @@ public final class ZbHip {
   private static final MethodHandle TIMED_OUT_JOBS =
       fn("zbhip_timed_out_jobs", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle TIME_OUT_JOB =
-      fn("zbhip_time_out_job", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, JAVA_LONG, ADDRESS));
+      fn("zbhip_time_out_job",
+          FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
+  private static final MethodHandle FAIL_JOB =
+      fn("zbhip_fail_job", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
+  private static final MethodHandle SET_JOB_STREAM =
+      fn("zbhip_set_job_stream",
+          FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, JAVA_LONG, JAVA_INT));
+  private static final MethodHandle JOB_STATE =
+      fn("zbhip_job_state", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG));
 
   /** The zbhip_db_sink upcall: (ctx, column family, key, key length, value, value length). */
   @FunctionalInterface
@@ -549,9 +557,77 @@ public final class ZbHip {
     }
   }
 
-  /** zbhip_time_out_job: JOB:TIMED_OUT or the NOT_FOUND rejection of a device job, one RECORD row. */
-  public static void timeOutJob(final MemorySegment h, final long jobKey, final long now, final MemorySegment out) {
-    check((int) call(TIME_OUT_JOB, h, jobKey, now, out), "zbhip_time_out_job");
+  /**
+   * zbhip_time_out_job: JOB:TIMED_OUT (then the push of a job stream's type, JOB_BATCH:ACTIVATED) or the
+   * rejection of a device job into {@code out} (room for 2 RECORD rows); returns the number of rows.
+   */
+  public static long timeOutJob(final MemorySegment h, final long jobKey, final long now, final MemorySegment out) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      check((int) call(TIME_OUT_JOB, h, jobKey, now, out, out.byteSize() / RECORD.byteSize(), n),
+          "zbhip_time_out_job");
+      return n.get(JAVA_LONG, 0);
+    }
+  }
+
+  /** zbhip_job_fail: the JOB:FAIL command's fields (JobRecord retries / retryBackoff / errorMessage). */
+  public static final StructLayout JOB_FAIL =
+      MemoryLayout.structLayout(
+          JAVA_LONG.withName("job_key"),
+          JAVA_LONG.withName("retry_backoff"),
+          JAVA_LONG.withName("timestamp"),
+          ADDRESS.withName("error_message"),
+          JAVA_LONG.withName("error_message_len"),
+          JAVA_INT.withName("retries"),
+          JAVA_INT.withName("n_variables"));
+
+  /**
+   * zbhip_fail_job (JobFailProcessor): JOB:FAILED (+ the push, or INCIDENT:CREATED JOB_NO_RETRIES) or the
+   * rejection into {@code out} (room for 2 rows); returns the number of rows, or -1 when the command is
+   * outside the device subset (variables, a back-off with retries left) and the engine must process it.
+   */
+  public static long failJob(final MemorySegment h, final long jobKey, final int retries, final long retryBackoff,
+      final byte[] errorMessage, final int nVariables, final long timestamp, final MemorySegment out) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment cmd = a.allocate(JOB_FAIL);
+      final MemorySegment msg = a.allocate(Math.max(1, errorMessage.length));
+      MemorySegment.copy(errorMessage, 0, msg, JAVA_BYTE, 0, errorMessage.length);
+      cmd.set(JAVA_LONG, 0, jobKey);
+      cmd.set(JAVA_LONG, 8, retryBackoff);
+      cmd.set(JAVA_LONG, 16, timestamp);
+      cmd.set(ADDRESS, 24, msg);
+      cmd.set(JAVA_LONG, 32, errorMessage.length);
+      cmd.set(JAVA_INT, 40, retries);
+      cmd.set(JAVA_INT, 44, nVariables);
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      final int rc = (int) call(FAIL_JOB, h, cmd, out, out.byteSize() / RECORD.byteSize(), n);
+      if (rc == EUNSUPP) {
+        return -1;
+      }
+      check(rc, "zbhip_fail_job");
+      return n.get(JAVA_LONG, 0);
+    }
+  }
+
+  /**
+   * zbhip_set_job_stream (JobStreamer.streamFor): jobs of {@code type} the device creates are activated for
+   * the stream's worker and timeout (JOB_BATCH:ACTIVATED after JOB:CREATED) while {@code on}.
+   */
+  public static void setJobStream(final MemorySegment h, final byte[] type, final byte[] worker, final long timeout,
+      final boolean on) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment t = a.allocate(Math.max(1, type.length));
+      final MemorySegment w = a.allocate(Math.max(1, worker.length));
+      MemorySegment.copy(type, 0, t, JAVA_BYTE, 0, type.length);
+      MemorySegment.copy(worker, 0, w, JAVA_BYTE, 0, worker.length);
+      check((int) call(SET_JOB_STREAM, h, t, (long) type.length, w, (long) worker.length, timeout, on ? 1 : 0),
+          "zbhip_set_job_stream");
+    }
+  }
+
+  /** zbhip_job_state: 0 ACTIVATABLE, 1 ACTIVATED, 2 FAILED, 3 gone, -1 not a device job. */
+  public static int jobState(final MemorySegment h, final long jobKey) {
+    return (int) call(JOB_STATE, h, jobKey);
   }
 
   /** Room for the records of one command: returns a buffer of at least n RECORD rows. */

@@ -752,6 +752,13 @@ typedef struct zbhip_job_batch {
 
 int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* cmd, zbhip_activated_job* jobs, size_t cap,
                         zbhip_job_batch* result);
+/* The push side effect of a job stream (BpmnJobActivationBehavior.java:83-97: JobVariablesCollector over
+ * the stream's fetchVariables, then JobStream.push of the ActivatedJob): for each of the n job keys (the
+ * aux of the JOB_BATCH:ACTIVATED records a run or zbhip_time_out_job / zbhip_fail_job wrote), its
+ * activation and variables document (`names`: the fetchVariables name ids, none = every variable) into
+ * out[i]; key -1 for a key that is no live device job.  Reads device state only. */
+int zbhip_job_variables(zbhip_handle* h, const int64_t* job_keys, size_t n, const uint32_t* names, size_t n_names,
+                        zbhip_activated_job* out);
 /* The rejection reason of a refused JOB_BATCH:ACTIVATE, exactly as JobBatchActivateProcessor writes it. */
 int zbhip_job_batch_rejection_reason(const zbhip_job_activation* cmd, const zbhip_job_batch* result, char* buf, size_t cap);
 
@@ -773,10 +780,20 @@ int zbhip_due_timers(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap
  * order (deadline, key). */
 int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out);
 /* JOB:TIME_OUT of a device job (JobTimeOutProcessor.processRecord, processing/job/JobTimeOutProcessor
- * .java:46-73; `now` = ActorClock.currentTimeMillis()): *out = JOB:TIMED_OUT with the stored job
- * (JobTimedOutApplier -> DbJobState.timeout: ACTIVATABLE again, deadline and worker kept), or the
- * NOT_FOUND rejection (reason ZBHIP_REASON_JOB_TIME_OUT; the adapter writes the command's value). */
-int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out);
+ * .java:46-73; `now` = ActorClock.currentTimeMillis()): out[0] = JOB:TIMED_OUT with the stored job
+ * (JobTimedOutApplier -> DbJobState.timeout: ACTIVATABLE again, deadline and worker kept) and, with a job
+ * stream of its type, out[1] = its push (publishWork); or the NOT_FOUND rejection (reason
+ * ZBHIP_REASON_JOB_TIME_OUT; the adapter writes the command's value).  cap >= 2. */
+int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out, size_t cap, size_t* n_out);
+/* A job stream for a job type (JobStreamer.streamFor: a gateway's StreamActivatedJobs with its worker and
+ * timeout; on = 0 removes it).  From the next run on, a job a device batch creates of that type is pushed
+ * as BpmnJobActivationBehavior.publishWork (processing/bpmn/behavior/BpmnJobActivationBehavior.java:61-100)
+ * does: JOB_BATCH:ACTIVATED (key = the next key) right after JOB:CREATED, the job ACTIVATED with deadline =
+ * the run's clock + timeout and the worker (drained record: value_type ZBHIP_VT_JOB_BATCH, aux = the job
+ * key, the job's fields as a JOB record's).  zbhip_time_out_job and zbhip_fail_job (retries left) push the
+ * same way.  Tasks with a stream run on the general path (no straight-line segment). */
+int zbhip_set_job_stream(zbhip_handle* h, const char* type, size_t type_len, const char* worker, size_t worker_len,
+                         int64_t timeout, int on);
 /* JOB:FAIL of a device job (JobFailProcessor.processRecord / failJob, processing/job/JobFailProcessor.java
  * :79-162; JobFailedApplier -> DbJobState.fail :191-203).  out[0] = JOB:FAILED (the stored job with the
  * command's retries and errorMessage -- StringUtil.limitString at 10 000 -- JOB records: reason_arg bit 0 =
@@ -790,6 +807,7 @@ int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_reco
 typedef struct zbhip_job_fail {
   int64_t job_key;
   int64_t retry_backoff;
+  int64_t timestamp;      /* the command's (ActorClock): a push's deadline */
   const char* error_message;
   size_t error_message_len;
   int32_t retries;

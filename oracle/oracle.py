@@ -59,6 +59,9 @@ def lib():
         L.zbo_activate_jobs.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int64, C.c_int, C.c_int64, C.c_char_p,
                                         C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
                                         C.POINTER(C.c_int64)]
+        L.zbo_set_job_stream.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int64, C.c_int]
+        L.zbo_job_variables.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_void_p]
+        L.zbo_set_job_stream.restype = None
         L.zbo_key_counter.restype = C.c_int64
         L.zbo_key_counter.argtypes = [C.c_void_p]
         L.zbo_set_key_counter.argtypes = [C.c_void_p, C.c_int64]
@@ -207,6 +210,20 @@ class Oracle:
         reason = self.L.zbo_activate_jobs(self.h, job_type.encode(), worker.encode(), timeout, max_jobs, timestamp, blob,
                                           len(variables), out.ctypes.data, len(out), C.byref(n), C.byref(key))
         return key.value, out[: n.value], reason
+
+    def set_job_stream(self, job_type, worker="", timeout=300000, on=True):
+        """A job stream of `job_type` (JobStreamer.streamFor): created jobs are pushed (publishWork)."""
+        self.L.zbo_set_job_stream(self.h, job_type.encode(), worker.encode(), int(timeout), 1 if on else 0)
+
+    def job_variables(self, job_keys, variables=()):
+        """The pushed jobs as stored now, with the stream's fetchVariables (zbo_job_variables)."""
+        import numpy as np
+        from zeebe_amd import abi
+        keys = np.asarray(job_keys, dtype=np.int64)
+        out = np.zeros(max(len(keys), 1), dtype=abi.ACTIVATED_JOB_DTYPE)
+        blob = b"".join(v.encode() + b"\0" for v in variables)
+        self.L.zbo_job_variables(self.h, keys.ctypes.data, len(keys), blob, len(variables), out.ctypes.data)
+        return out[: len(keys)]
 
     def key_counter(self):
         """DbKeyGenerator's current value (the counter, without the partition bits)."""

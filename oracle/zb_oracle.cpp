@@ -1594,11 +1594,6 @@ class Oracle {
          (int)keys.size() < max_jobs;
          ++it)
       keys.push_back(std::get<2>(*it));
-    auto name_less = [this](int a, int b) {  // DbString: 4-byte big-endian length, then the bytes
-      const std::string& x = names[a];
-      const std::string& y = names[b];
-      return x.size() != y.size() ? x.size() < y.size() : x < y;
-    };
     for (int64_t k : keys) {
       JobRow& j = jobs_.at(k);
       Activated a;
@@ -1609,25 +1604,7 @@ class Oracle {
       a.proc = j.pi.proc;
       a.elem = j.pi.elem;
       a.retries = j.retries;
-      // the element scope, then every scope above it (a multi-instance inner activity: its loop
-      // variables, the body, the process instance)
-      std::vector<int64_t> scopes{j.elementInstanceKey};
-      for (auto pit = child_parent_.find(j.elementInstanceKey); pit != child_parent_.end() && pit->second > 0;
-           pit = child_parent_.find(pit->second))
-        scopes.push_back(pit->second);
-      std::set<int> seen;
-      for (int64_t scope : scopes) {
-        std::vector<int> local;
-        for (auto& [sk, row] : vars_)
-          if (sk.first == scope) local.push_back(sk.second);
-        std::sort(local.begin(), local.end(), name_less);
-        for (int nid : local) {
-          if (seen.count(nid)) continue;
-          if (!requested.empty() && std::find(requested.begin(), requested.end(), names[nid]) == requested.end()) continue;
-          seen.insert(nid);
-          a.vars.push_back({nid, vars_.at({scope, nid})});
-        }
-      }
+      collect_variables(j, requested, a);
       j.activated = true;
       j.deadline = a.deadline;
       j.worker = worker;
@@ -1635,6 +1612,51 @@ class Oracle {
       out.push_back(std::move(a));
     }
     return 0;
+  }
+
+  // JobVariablesCollector.setJobVariables: the element scope, then every scope above it (a multi-instance
+  // inner activity: its loop variables, the body, the process instance); names in DbString key order
+  // (4-byte big-endian length, then the bytes), each once, `requested` only if any
+  void collect_variables(const JobRow& j, const std::vector<std::string>& requested, Activated& a) {
+    auto name_less = [this](int x_, int y_) {
+      const std::string& x = names[x_];
+      const std::string& y = names[y_];
+      return x.size() != y.size() ? x.size() < y.size() : x < y;
+    };
+    std::vector<int64_t> scopes{j.elementInstanceKey};
+    for (auto pit = child_parent_.find(j.elementInstanceKey); pit != child_parent_.end() && pit->second > 0;
+         pit = child_parent_.find(pit->second))
+      scopes.push_back(pit->second);
+    std::set<int> seen;
+    for (int64_t scope : scopes) {
+      std::vector<int> local;
+      for (auto& [sk, row] : vars_)
+        if (sk.first == scope) local.push_back(sk.second);
+      std::sort(local.begin(), local.end(), name_less);
+      for (int nid : local) {
+        if (seen.count(nid)) continue;
+        if (!requested.empty() && std::find(requested.begin(), requested.end(), names[nid]) == requested.end()) continue;
+        seen.insert(nid);
+        a.vars.push_back({nid, vars_.at({scope, nid})});
+      }
+    }
+  }
+  // the push side effect's ActivatedJob (BpmnJobActivationBehavior.publishWork :83-97): the job as stored
+  // now, with the stream's fetchVariables; false for no such job
+  bool job_variables(int64_t key, const std::vector<std::string>& requested, Activated& a) {
+    auto it = jobs_.find(key);
+    if (it == jobs_.end()) return false;
+    const JobRow& j = it->second;
+    a = Activated{};
+    a.key = key;
+    a.eik = j.elementInstanceKey;
+    a.pik = j.pi.piKey;
+    a.deadline = j.activated ? j.deadline : -1;
+    a.proc = j.pi.proc;
+    a.elem = j.pi.elem;
+    a.retries = j.retries;
+    collect_variables(j, requested, a);
+    return true;
   }
 
   // DbKeyGenerator's current value (the CPU engine of a fallback hand-off is set to the device's)
@@ -1666,6 +1688,7 @@ class Oracle {
   std::map<std::pair<int64_t, int64_t>, TimerRow> timers_;     // TIMERS [elementInstanceKey, timerKey]
  public:
   int64_t now_ms = 0;  // ActorClock.currentTimeMillis() of the window's processing (zbo_set_clock)
+  std::map<std::string, std::pair<std::string, int64_t>> streams;  // job streams: type -> (worker, timeout)
  private:
   std::map<int64_t, JobRow> jobs_;                              // JOBS (+ JOB_STATES = ACTIVATABLE)
   struct IncidentRow {  // IncidentRecord (protocol-impl/.../incident/IncidentRecord.java:20-48)
@@ -2423,6 +2446,7 @@ class Oracle {
     job_activation_fields(rec, job);
     job.activated = false;
     activatable_.insert({job.type, "<default>", jobKey});
+    publish_work(jobKey);
   }
 
   // JobFailProcessor.processRecord / failJob (processing/job/JobFailProcessor.java:79-162): the job
@@ -2471,6 +2495,7 @@ class Oracle {
     else activatable_.erase({job.type, "<default>", jobKey});
     // setFailedVariables: mergeLocalDocument into the job's element instance
     merge_local_document(job.elementInstanceKey, job.pi.proc, job.pi.piKey, cmd.doc);
+    if (retries > 0 && backoff <= 0) publish_work(jobKey);  // retryImmediately
     if (retries <= 0) {  // raiseIncident (:139-162)
       const int64_t key = next_key();
       ORecord& in = append(ZBHIP_RT_EVENT, ZBHIP_VT_INCIDENT, ZBHIP_INCIDENT_CREATED, key);
@@ -2491,6 +2516,31 @@ class Oracle {
       incidents_[key] = row;
       incident_jobs_[jobKey] = key;
     }
+  }
+
+  // BpmnJobActivationBehavior.publishWork (processing/bpmn/behavior/BpmnJobActivationBehavior.java:61-100):
+  // with a job stream for the job's type, JOB_BATCH:ACTIVATED (key = nextKey) of that one job -- deadline
+  // = now + the stream's timeout, its worker -- applied at once (JobBatchActivatedApplier ->
+  // DbJobState.activate); the push itself is a side effect.  No stream: a notification (no record).
+  // The record: aux = the job key, the job's fields as a JOB record's (scope_key = its element instance,
+  // message_key = the deadline, correlation_key = the worker's string id, a failed job's fields); the
+  // batch's timeout is the stream's.
+  void publish_work(int64_t jobKey) {
+    JobRow& job = jobs_.at(jobKey);
+    auto st = streams.find(job.type);
+    if (st == streams.end()) return;
+    const int64_t key = next_key();
+    job.activated = true;
+    job.deadline = now_ms + st->second.second;
+    job.worker = st->second.first;
+    activatable_.erase({job.type, "<default>", jobKey});
+    ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB_BATCH, ZBHIP_JOB_BATCH_ACTIVATED, key);
+    rec.r.process_idx = job.pi.proc;
+    rec.r.element_idx = job.pi.elem;
+    rec.r.scope_key = job.elementInstanceKey;
+    rec.r.process_instance_key = job.pi.piKey;
+    rec.r.aux = jobKey;
+    job_activation_fields(rec, job);  // the job as activated: deadline, worker (+ a failed job's fields)
   }
 
   // the stored job's deadline and worker (DbJobState.activate wrote them; a timed-out job keeps
@@ -2852,6 +2902,7 @@ class Oracle {
         rec.r.scope_key = key;
         rec.r.process_instance_key = v.piKey;
         apply_job_created(jobKey, job);
+        publish_work(jobKey);
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         break;
       }
@@ -3546,6 +3597,13 @@ int32_t zbo_java_hash(const char* b, size_t len) { return java_hash(std::string(
 int zbo_run(void* o) { return static_cast<Oracle*>(o)->run(); }
 int64_t zbo_key_counter(void* o) { return static_cast<Oracle*>(o)->key_counter(); }
 // names: requested variable names, NUL-separated (n of them)
+// a job stream for `type` (JobStreamer.streamFor: the gateway's StreamActivatedJobs), or none (on = 0)
+void zbo_set_job_stream(void* o, const char* type, const char* worker, int64_t timeout, int on) {
+  auto& e = *static_cast<Oracle*>(o);
+  if (on) e.streams[type] = {worker, timeout};
+  else e.streams.erase(type);
+}
+
 int zbo_activate_jobs(void* o, const char* type, const char* worker, int64_t timeout, int max_jobs, int64_t timestamp,
                       const char* names, size_t n_names, zbhip_activated_job* out, size_t cap, size_t* n_out,
                       int64_t* batch_key) {
@@ -3576,6 +3634,37 @@ int zbo_activate_jobs(void* o, const char* type, const char* worker, int64_t tim
     }
   }
   return reason;
+}
+// zbhip_job_variables' restatement: key -1 for a key that is no job
+int zbo_job_variables(void* o, const int64_t* keys, size_t n, const char* names, size_t n_names,
+                      zbhip_activated_job* out) {
+  auto* O = static_cast<Oracle*>(o);
+  std::vector<std::string> req;
+  for (size_t i = 0; i < n_names; ++i) {
+    req.emplace_back(names);
+    names += req.back().size() + 1;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    zbhip_activated_job& j = out[i];
+    memset(&j, 0, sizeof j);
+    j.key = -1;
+    Oracle::Activated a;
+    if (!O->job_variables(keys[i], req, a)) continue;
+    j.key = a.key;
+    j.element_instance_key = a.eik;
+    j.process_instance_key = a.pik;
+    j.deadline = a.deadline;
+    j.process_idx = a.proc;
+    j.element_idx = a.elem;
+    j.retries = (uint16_t)a.retries;
+    j.n_variables = (uint16_t)std::min<size_t>(a.vars.size(), 6);
+    for (size_t v = 0; v < a.vars.size() && v < 6; ++v) {
+      j.variables[v].name_id = (uint32_t)a.vars[v].first;
+      j.variables[v].type = a.vars[v].second.type;
+      j.variables[v].value = a.vars[v].second.value;
+    }
+  }
+  return 0;
 }
 void zbo_set_key_counter(void* o, int64_t v) { static_cast<Oracle*>(o)->set_key_counter(v); }
 

@@ -27,8 +27,19 @@ import numpy as np
 from oracle.oracle import Oracle
 from zeebe_amd import abi
 from zeebe_amd.adapter import (JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED, MESSAGE_VALUE_TYPES, VT_JOB_BATCH, XPART_COMMAND,
-                               RecordValues, doc_entries, typed_value, xpart_value)
+                               RecordValues, doc_entries, push_side_effects, typed_value, xpart_value)
 from zeebe_amd.engine import ProcessDefinition
+
+
+class RecordingJobStream:
+    """RecordingJobStreamer's stream (engine/src/test/.../util/RecordingJobStreamer.java): the pushed
+    ActivatedJobs, (jobKey, job record value) in push order."""
+
+    def __init__(self):
+        self.activated_jobs = []
+
+    def push(self, job_key, job):
+        self.activated_jobs.append((job_key, job))
 
 
 class Rec:
@@ -498,12 +509,27 @@ class OracleEngine:
         self.doc_values = []  # client value of every document entry the oracle holds (its doc indices)
         self.values = None
         self.tables = []
+        self.streams = {}  # job streams: type -> (worker, timeout)
+        self.stream_sinks = {}  # job type -> (fetchVariables, push)
 
     def deploy(self, xml, key, version=1):
         idx = self.o.deploy(xml, key, version)
         self.tables = oracle_tables(self.o)
-        self.values = RecordValues(self.tables, self.o.name, lambda i: self.o.string_value(i).decode())
+        self.values = RecordValues(self.tables, self.o.name, lambda i: self.o.string_value(i).decode(),
+                                   streams=self.streams)
         return idx
+
+    def set_job_stream(self, job_type, worker, timeout, on=True, fetch_variables=(), push=None):
+        """A job stream (JobStreamer.streamFor) of `job_type`: created jobs are pushed -- JOB_BATCH:ACTIVATED,
+        and after the commit push(jobKey, job) with its `fetch_variables`."""
+        self.o.set_job_stream(job_type, worker, timeout, on)
+        if on:
+            self.streams[job_type] = (worker, timeout)
+            if push is not None:
+                self.stream_sinks[job_type] = (tuple(fetch_variables), push)
+        else:
+            self.streams.pop(job_type, None)
+            self.stream_sinks.pop(job_type, None)
 
     def set_clock(self, now):
         self.o.set_clock(now)
@@ -600,6 +626,7 @@ class OracleEngine:
             self.o.set_clock(self.clock.now)
         self.o.process_one(r, slot, docs, record.position or 0, len(out.entries))
         recs = self.o.records()
+        pushes = []
         for k, x in enumerate(recs):
             rt, xvt, xit = int(x["record_type"]), int(x["value_type"]), int(x["intent"])
             if rt == abi.RT_REJECTION and k == 0 and xvt == vt and xit == it:
@@ -611,8 +638,14 @@ class OracleEngine:
             out.append_record(int(x["key"]), rt, xvt, xit, int(x["rejection_type"]),
                               self.o.reason(k) if rt == abi.RT_REJECTION else "", value)
             self.pending.track(rt, xvt, xit, value)
+            if rt == abi.RT_EVENT and xvt == VT_JOB_BATCH:
+                pushes.append((int(x["aux"]), value))
             if rt == abi.RT_EVENT and xvt == abi.VT_TIMER and xit == abi.TIMER_CREATED and self.due_date_checker:
                 out.append_post_commit_task(lambda d=value["dueDate"]: self.due_date_checker.schedule_timer(d) or True)
+        if pushes:
+            strings = self.o.strings()
+            push_side_effects(out, pushes, self.stream_sinks, self.o.job_variables, self.values, self.o.name,
+                              lambda i: strings[i].decode())
         sends = self.o.outbox()  # SubscriptionCommandSender's side effects of this command
         if len(sends):
             strings = self.o.strings()

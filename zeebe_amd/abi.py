@@ -9,6 +9,8 @@ import numpy as np
 
 # ---- protocol enums (protocol/src/main/resources/protocol.xml:23-72) ----
 RT_EVENT, RT_COMMAND, RT_REJECTION = 0, 1, 2
+VT_JOB_BATCH = 1
+JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED = 0, 1
 VT_JOB = 0
 VT_PROCESS_INSTANCE = 5
 VT_MESSAGE = 10
@@ -228,5 +230,5 @@ def record_tuple(r, element_id=None, name=None):
 
 class JobFail(C.Structure):
     """zbhip_job_fail (JOB:FAIL of a device job)."""
-    _fields_ = [("job_key", C.c_int64), ("retry_backoff", C.c_int64), ("error_message", C.c_char_p),
+    _fields_ = [("job_key", C.c_int64), ("retry_backoff", C.c_int64), ("timestamp", C.c_int64), ("error_message", C.c_char_p),
                 ("error_message_len", C.c_size_t), ("retries", C.c_int32), ("n_variables", C.c_uint32)]

@@ -46,8 +46,8 @@ Platform objects used (duck-typed like the Java interfaces):
 from . import abi
 from .engine import Partition
 
-VT_JOB_BATCH = 1
-JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED = 0, 1
+VT_JOB_BATCH = abi.VT_JOB_BATCH
+JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED = abi.JOB_BATCH_ACTIVATE, abi.JOB_BATCH_ACTIVATED
 MESSAGE_VALUE_TYPES = (abi.VT_MESSAGE, abi.VT_MESSAGE_SUBSCRIPTION, abi.VT_PROCESS_MESSAGE_SUBSCRIPTION)
 # zbhip_xpart_cmd kind <-> (value type, intent) of the command SubscriptionCommandSender sends
 XPART_COMMAND = {abi.CMD_MSG_SUB_CREATE: (abi.VT_MESSAGE_SUBSCRIPTION, abi.MS_CREATE),
@@ -135,15 +135,25 @@ def typed_value(t, v, string_value):
             else ("other", int(v)))
 
 
+def _as_job(r):
+    """A push's JOB_BATCH row read as the JOB record of its job (the same fields)."""
+    j = r.copy()
+    j["value_type"] = abi.VT_JOB
+    j["intent"] = abi.JOB_CREATED
+    j["aux"] = -1
+    return j
+
+
 class RecordValues:
     """zbhip_record rows -> the reference's record values (Window.value).  `procs` are the
     deployment's ProcessDefinitions (by process index), `name` the variable-name dictionary."""
 
-    def __init__(self, procs, name, string_value=None, incident_message=None):
+    def __init__(self, procs, name, string_value=None, incident_message=None, streams=None):
         self.procs = procs
         self.name = name
         self.string_value = string_value  # value-dictionary id -> str (inline STR values)
         self.incident_message = incident_message  # a gateway incident's errorMessage (zbhip_incident_message)
+        self.streams = streams if streams is not None else {}  # job streams: type -> (worker, timeout)
 
     def value(self, r, command_doc=(), entry_value=None, timestamp=0):
         """`timestamp`: the source command's (a MESSAGE record's deadline = timestamp + timeToLive)."""
@@ -173,6 +183,14 @@ class RecordValues:
                 v.update({"retries": int(r["partition"]),
                           "errorMessage": self.string_value(eid) if eid != abi.NO_STRING else ""})
             return v
+        if vt == VT_JOB_BATCH:
+            # a job stream's push (BpmnJobActivationBehavior.publishWork :61-100): a fresh JobBatchRecord
+            # (type, worker, timeout of the stream) with the one job, its variables left out
+            j = self.value(_as_job(r))
+            jt = j["type"]
+            return {"type": jt, "worker": j.get("worker", ""), "timeout": self.streams.get(jt, ("", -1))[1],
+                    "maxJobsToActivate": -1, "jobKeys": (aux,), "jobs": (j,), "variables": (), "truncated": False,
+                    "tenantIds": ()}
         if vt == abi.VT_INCIDENT:  # IncidentRecord.java:36-47
             et = int(r["partition"])
             job = et == abi.ERR_JOB_NO_RETRIES
@@ -241,6 +259,35 @@ class RecordValues:
                         "tenantId": TENANT})
         v.update({"jobKeys": tuple(int(j["key"]) for j in jobs), "jobs": tuple(out), "truncated": False})
         return v
+
+    def pushed_job(self, push_value, row, name, string_value):
+        """The ActivatedJob a job stream receives (BpmnJobActivationBehavior.publishWork :83-97): the
+        JOB_BATCH:ACTIVATED record's job with the variables JobVariablesCollector gathered (`row`: a
+        zbhip_job_variables / zbo_job_variables row)."""
+        j = dict(push_value["jobs"][0])
+        j["variables"] = tuple((name(int(x["name_id"])), typed_value(int(x["type"]), x["value"], string_value))
+                               for x in row["variables"][:int(row["n_variables"])])
+        return j
+
+
+def push_side_effects(out, pushes, sinks, gather, values, name, string_value):
+    """publishWork's side effect for the JOB_BATCH:ACTIVATED records of one command (`pushes`: (job key,
+    record value)): the jobs' variables collected now, the stream's push(jobKey, job) after the commit.
+    `sinks`: job type -> (fetchVariables, push); `gather(keys, fetch)` -> job-variable rows."""
+    by_type = {}
+    for key, value in pushes:
+        if value["type"] in sinks:
+            by_type.setdefault(value["type"], []).append((key, value))
+    for jt, items in by_type.items():
+        fetch, push = sinks[jt]
+        rows = gather([k for k, _ in items], fetch)
+        jobs = [(k, values.pushed_job(v, r, name, string_value)) for (k, v), r in zip(items, rows)]
+
+        def task(jobs=jobs, push=push):
+            for k, j in jobs:
+                push(k, j)
+            return True
+        out.append_post_commit_task(task)
 
 
 class DeviceTimerInstanceState:
@@ -424,6 +471,7 @@ class GpuBatchProcessor:
         self.continuations = []        # expected continuations, in log order: (id, slot, match key)
         self.doc_total = 0             # document entries submitted so far (zbhip doc indices)
         self.values = None
+        self.stream_sinks = {}  # job type -> (fetchVariables, push): the job streams' push side effects
         # what went where (tests read these)
         self.fallback_reasons = []
         self.counts = {"windows": 0, "device_commands": 0, "continuations": 0, "fallbacks": 0, "activations": 0,
@@ -747,6 +795,7 @@ class GpuBatchProcessor:
         cmd_doc = tuple(record.value.get("variables", ())) if isinstance(record.value, dict) else ()
         win = self.window
         admitted = 0
+        pushes = []
         for r in self.part.drain_command(i):
             rt, vt, it = int(r["record_type"]), int(r["value_type"]), int(r["intent"])
             if rt == abi.RT_REJECTION and int(r["ordinal"]) == 0 and vt == record.value_type and it == record.intent:
@@ -756,6 +805,8 @@ class GpuBatchProcessor:
                                           getattr(record, "timestamp", 0))
             reason = self.part.reason(r) if rt == abi.RT_REJECTION else ""
             out.append_record(int(r["key"]), rt, vt, it, int(r["rejection_type"]), reason, value)
+            if vt == VT_JOB_BATCH and rt == abi.RT_EVENT:
+                pushes.append((int(r["aux"]), value))
             if self.correlation_keys > 0:
                 self._track_pending(rt, vt, it, value)
             if rt == abi.RT_EVENT and vt == abi.VT_TIMER and it == abi.TIMER_CREATED and self.due_date_checker:
@@ -789,6 +840,8 @@ class GpuBatchProcessor:
                     if it == abi.PMS_DELETED:
                         self.closing.discard(win.instances[i])
         self.followups = admitted
+        if pushes:
+            self._push(out, pushes)
         if self.correlation_keys > 0:
             self._send(i, out)
 
@@ -912,7 +965,7 @@ class GpuBatchProcessor:
         v = record.value
         self.part.set_key_if_higher(self.key_generator.current_key())
         recs = self.part.fail_job(record.key, v.get("retries", 0), v.get("errorMessage", ""), v.get("retryBackoff", 0),
-                                  len(v.get("variables", ())))
+                                  len(v.get("variables", ())), timestamp=self.clock())
         if recs is None:  # outside the device subset (variables, a back-off): the engine's, with the instance
             self._hand_off(self._resolve(record.key)[0])
             self.key_generator.set_key_if_higher(self.part.current_key())
@@ -925,8 +978,11 @@ class GpuBatchProcessor:
             if rt == abi.RT_REJECTION:
                 out.append_record(record.key, rt, vt, it, int(r["rejection_type"]), self.part.reason(r), dict(v))
                 continue
-            out.append_record(int(r["key"]), rt, vt, it, abi.REJ_NONE, "", self.values.value(r))
+            value = self.values.value(r)
+            out.append_record(int(r["key"]), rt, vt, it, abi.REJ_NONE, "", value)
             incident |= vt == abi.VT_INCIDENT
+            if vt == VT_JOB_BATCH:
+                self._push(out, [(int(r["aux"]), value)])
         self.key_generator.set_key_if_higher(self.part.current_key())
         if incident:
             # the instance waits for the incident's resolution (JOB:UPDATE_RETRIES, INCIDENT:RESOLVE): the
@@ -937,14 +993,38 @@ class GpuBatchProcessor:
     # ---- JOB:TIME_OUT of a device job (JobTimeOutProcessor.java:46-73) ------------------------------
     def _time_out_job(self, record, out):
         self.counts["time_outs"] += 1
-        r = self.part.time_out_job(record.key, self.clock())
+        self.part.set_key_if_higher(self.key_generator.current_key())
+        recs = self.part.time_out_job(record.key, self.clock())
+        r = recs[0]
         if int(r["record_type"]) == abi.RT_REJECTION:
             out.append_record(record.key, abi.RT_REJECTION, abi.VT_JOB, abi.JOB_TIME_OUT, int(r["rejection_type"]),
                               self.part.reason(r), dict(record.value))
             return out.build()
         out.append_record(record.key, abi.RT_EVENT, abi.VT_JOB, abi.JOB_TIMED_OUT, abi.REJ_NONE, "", self.values.value(r))
-        # publishWork: no job stream -> jobStreamer.notifyWorkAvailable (a side effect, no record)
+        # publishWork: a job stream of the type -> the push (JOB_BATCH:ACTIVATED); none -> a notification
+        for p in recs[1:]:
+            value = self.values.value(p)
+            out.append_record(int(p["key"]), abi.RT_EVENT, VT_JOB_BATCH, JOB_BATCH_ACTIVATED, abi.REJ_NONE, "", value)
+            self._push(out, [(int(p["aux"]), value)])
+        self.key_generator.set_key_if_higher(self.part.current_key())
         return out.build()
+
+    def set_job_stream(self, job_type, worker, timeout, on=True, fetch_variables=(), push=None):
+        """A job stream opened / closed for `job_type` (JobStreamer: the gateway's StreamActivatedJobs): jobs
+        the device creates of that type are pushed from the next window on -- JOB_BATCH:ACTIVATED in the log,
+        and after the commit push(jobKey, job) with the job's `fetch_variables` (all when empty)."""
+        self.part.set_job_stream(job_type, worker, timeout, on)
+        if on:
+            self.values.streams[job_type] = (worker, timeout)
+            if push is not None:
+                self.stream_sinks[job_type] = (tuple(fetch_variables), push)
+        else:
+            self.values.streams.pop(job_type, None)
+            self.stream_sinks.pop(job_type, None)
+
+    def _push(self, out, pushes):
+        push_side_effects(out, pushes, self.stream_sinks, self.part.job_variables, self.values, self.part.name,
+                          self.part.string_value)
 
     # ---- job activation (JobBatchActivateProcessor.java:60-143) ------------------------------------
     def _activate_jobs(self, record, out):

@@ -1705,6 +1705,13 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         emit(L, C_JOB_CREATED, job, key, elem);
         uint2 e = tget(L, t);   // JobCreatedApplier: element instance jobKey
         e.y = (job & 0xFFFF) | (e.y & 0xFCFF0000u) | (1u << 24);  // (a multi-instance loop counter stays)
+        if ((w.z >> 16) != 0xFFFF) {
+          // BpmnJobActivationBehavior.publishWork (:61-100): a job stream of the type -- JOB_BATCH:ACTIVATED
+          // (key = nextKey) of this job, ACTIVATED from now on (its deadline and worker: the host's stream
+          // table; runtime.cpp track_jobs)
+          emit(L, C_JOB_PUSHED, new_key(L), job, elem);
+          e.y |= 2u << 24;
+        }
         tput(L, t, e);
         emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
         tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
@@ -3774,7 +3781,8 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
   if (i >= n) return;
   // y bit 16: the host's state says ACTIVATABLE although the row holds a stored activation (a timed-out
   // job, DbJobState.timeout keeps the deadline and worker): activate it again
-  const uint32_t inst = jobs[i].x, ord = jobs[i].y & 0xFFFF, again = (jobs[i].y >> 16) & 1u;
+  // y bit 17: peek (zbhip_job_variables: a pushed job's variables, nothing written)
+  const uint32_t inst = jobs[i].x, ord = jobs[i].y & 0xFFFF, again = (jobs[i].y >> 16) & 1u, peek = (jobs[i].y >> 17) & 1u;
   ActivatedOut o = {};
   if (inst < st.n) {
     const uint4 h = st.hdr[inst];
@@ -3782,11 +3790,14 @@ __global__ __launch_bounds__(256) void k_activate_jobs(DevState st, const uint2*
     bool marked = false;
     for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s) {
       uint2 e = st.slots[(size_t)s * st.n + inst];
-      if ((e.y & 0xFFFF) == ord && (((e.y >> 24) & 3u) == 1u || (again && ((e.y >> 24) & 3u) == 3u))) {
-        e.y |= 2u << 24;
-        st.slots[(size_t)s * st.n + inst] = e;
+      if ((e.y & 0xFFFF) != ord) continue;
+      if (peek ? ((e.y >> 24) & 1u) != 0u : (((e.y >> 24) & 3u) == 1u || (again && ((e.y >> 24) & 3u) == 3u))) {
+        if (!peek) {
+          e.y |= 2u << 24;
+          st.slots[(size_t)s * st.n + inst] = e;
+          marked = true;
+        }
         o.a = make_uint4(e.x, h.x, h.y, e.y);  // (e.y != 0: its state; a multi-instance loop counter)
-        marked = true;
       }
     }
     // the activation (DbJobState.activate stores the deadline and worker): an entry of the instance's

@@ -689,6 +689,15 @@ struct zbhip_handle {
     uint32_t incident_msg_id = ZBHIP_NO_STRING;
   };
   std::unordered_map<int64_t, Activation> activated;  // jobs with a stored activation: deadline, worker, state
+  // job streams (JobStreamer.streamFor: a gateway's StreamActivatedJobs), by job type id: the jobs a
+  // device batch creates of such a type are pushed (BpmnJobActivationBehavior.publishWork)
+  struct Stream {
+    std::string worker;
+    uint32_t worker_id;
+    int64_t timeout;
+  };
+  std::map<uint32_t, Stream> streams;
+  std::map<uint32_t, Stream> run_streams;  // the streams of the last run (its pushes' deadlines / workers)
   DueTimer* d_due = nullptr;                          // zbhip_due_timers: [max_instances] due rows
   uint32_t* d_due_count = nullptr;
   unsigned long long* d_due_next = nullptr;
@@ -1132,6 +1141,8 @@ static int rebuild_program(zbhip_handle* h) {
     pb[7] = create_template_word(P);
     // straight-line segment words (kernels.hip fast_command): a start event or service task with
     // one unconditional outgoing flow into a service task or a none end event without outgoing flows
+    // (a task whose jobs a job stream takes is entered on the general path: the push record)
+    auto streamed = [&](uint32_t t) { return ZBHIP_IS_JOB_WORKER(P.els[t].element_type) && h->streams.count(P.job_type_id[t]); };
     for (uint32_t e = 0; e < n_el; ++e) {
       const zbhip_element& E = P.els[e];
       uint32_t sg = 0;
@@ -1152,7 +1163,7 @@ static int rebuild_program(zbhip_handle* h) {
           const zbhip_element& N = P.els[n];
           const bool dst_tmr = ZBHIP_IS_JOB_WORKER(N.element_type) && timer_boundary(N);
           const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && (N.start_event == ZBHIP_NONE16 || dst_tmr) &&
-                            !P.io_of(n) && !P.mi_inner(n);
+                            !P.io_of(n) && !P.mi_inner(n) && !streamed(n);
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
           // bit 29: a start event into a forking parallel gateway whose every outgoing flow is
           // unconditional into a task without boundary event (KGeneric's fast_fork_create)
@@ -1163,7 +1174,7 @@ static int rebuild_program(zbhip_handle* h) {
             const uint32_t t = G.flow_target;
             fork = G.element_type == ZBHIP_EL_SEQUENCE_FLOW && G.condition == ZBHIP_NONE16 && t < n_el &&
                    ZBHIP_IS_JOB_WORKER(P.els[t].element_type) && P.els[t].start_event == ZBHIP_NONE16 &&
-                   !P.io_of(t) && !P.mi_inner(t) && P.els[t].element_type != ZBHIP_EL_PARALLEL_GATEWAY;
+                   !P.io_of(t) && !P.mi_inner(t) && P.els[t].element_type != ZBHIP_EL_PARALLEL_GATEWAY && !streamed(t);
           }
           if (fork) sg = (1u << 31) | (1u << 29) | (n << 12) | f;
           // bit 27: a task into a joining parallel gateway (KGeneric's fast_join_job)
@@ -1182,7 +1193,7 @@ static int rebuild_program(zbhip_handle* h) {
         if (F.element_type == ZBHIP_EL_SEQUENCE_FLOW && F.condition == ZBHIP_NONE16 && n < n_el && f < 0xFFF && n < 0xFFF) {
           const zbhip_element& N = P.els[n];
           const bool task = ZBHIP_IS_JOB_WORKER(N.element_type) && N.start_event == ZBHIP_NONE16 && !P.io_of(n) &&
-                            !P.mi_inner(n);
+                            !P.mi_inner(n) && !streamed(n);
           const bool end = N.element_type == ZBHIP_EL_END_EVENT && N.event_type == ZBHIP_EV_NONE && N.out_count == 0;
           if (task || end) sg = (1u << 31) | (1u << 28) | (end ? 1u << 24 : 0u) | (n << 12) | f;
         }
@@ -1204,7 +1215,8 @@ static int rebuild_program(zbhip_handle* h) {
       w[1] = E.out_begin | ((uint32_t)E.out_count << 16);
       if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW) w[2] = E.flow_target | ((uint32_t)E.condition << 16);
       else if (E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY) w[2] = E.default_flow | (0xFFFFu << 16);
-      else if (ZBHIP_IS_JOB_WORKER(E.element_type)) w[2] = E.job_type | ((uint32_t)E.job_retries << 16);
+      else if (ZBHIP_IS_JOB_WORKER(E.element_type))  // job type | 0 when a job stream takes its jobs (0xFFFF none)
+        w[2] = E.job_type | ((h->streams.count(P.job_type_id[e]) ? 0u : 0xFFFFu) << 16);
       else if ((E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT) &&
                E.event_type == ZBHIP_EV_MESSAGE)
         w[2] = E.message_name | ((uint32_t)E.correlation_var << 16);  // name ids (zbhip_deploy)
@@ -1953,6 +1965,7 @@ static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
   const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
   if (proc == NONE || proc >= h->procs.size()) return;
   const Proc& P = h->procs[proc];
+  uint32_t task_ord = NONE;
   for (uint32_t i = 0; i < nrec; ++i) {
     const uint2 w = rows[i];
     const uint32_t elem = w.y & 0xFFFF, code = (w.y >> 16) & 0x3F;
@@ -1960,11 +1973,30 @@ static void track_jobs(zbhip_handle* h, size_t c, uint32_t inst) {
       i += kPayloadRows;
       continue;
     }
-    if (((w.y >> 16) & kRejectBit) || (code != C_JOB_CREATED && code != C_JOB_COMPLETED && code != C_JOB_CANCELED) ||
+    if (((w.y >> 16) & kRejectBit) ||
+        (code != C_JOB_CREATED && code != C_JOB_COMPLETED && code != C_JOB_CANCELED && code != C_JOB_PUSHED) ||
         elem >= P.els.size())
       continue;
     const uint32_t tid = P.job_type_id[elem];
+    if (code == C_JOB_PUSHED) {  // publishWork: the job ACTIVATED with the stream's deadline and worker
+      const int64_t jk = h->key_of(inst, w.x >> 16);
+      const auto st = h->run_streams.find(tid);
+      if (h->job_index_on) h->job_index.erase({tid, jk});
+      if (st == h->run_streams.end()) continue;
+      zbhip_handle::Activation& a = h->activated[jk];
+      a.deadline = h->run_clock_ms + st->second.timeout;
+      a.worker = st->second.worker;
+      a.inst = inst;
+      a.worker_id = st->second.worker_id;
+      a.state = zbhip_handle::JS_ACTIVATED;
+      a.eik = h->key_of(inst, task_ord);
+      a.pik = h->key_of(inst, 0);
+      a.proc = (int32_t)proc;
+      a.elem = (int32_t)elem;
+      continue;
+    }
     const int64_t key = h->key_of(inst, w.x & 0xFFFF);
+    if (code == C_JOB_CREATED) task_ord = w.x >> 16;  // (its element instance: a push follows)
     if (code == C_JOB_CREATED) {
       if (h->job_index_on) h->job_index[{tid, key}] = {inst, (uint16_t)(w.x & 0xFFFF)};
     } else {
@@ -2181,7 +2213,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
     for (int64_t k : h->completed_activated) h->activated.erase(k);
     h->completed_activated.clear();
   }
-  if (h->job_index_on || !h->activated.empty())
+  if (h->job_index_on || !h->activated.empty() || !h->streams.empty())
     if (int rc = ensure_out(h)) return rc;
   const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
   if (h->hist.size() < subjects) {
@@ -2191,7 +2223,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
   }
   const size_t n = std::min(limit, h->n_cmds);
   if (h->fin_next == 0 && n == h->n_cmds && !h->msg() && !h->job_index_on && h->activated.empty() &&
-      n >= (1u << 16)) {
+      h->streams.empty() && n >= (1u << 16)) {
     bool all_declared = true;  // the whole window can be done now (fallback keys declared, or forced)
     if (!force)
       for (size_t c = 0; c < n && all_declared; ++c)
@@ -2224,7 +2256,8 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
         h->hist[h2.x].push_back({(uint16_t)(h2.y & 0xFFFF), h->key_counter + 1 + nprim});
         h->batches.push_back({h->key_counter + 1 + nprim, h2.x, (uint16_t)(h2.y & 0xFFFF), (uint16_t)nsec, h->inst_gen[h2.x]});
       }
-      if ((h->job_index_on || !h->activated.empty()) && h2.x < h->cfg.max_instances) track_jobs(h, c, h2.x);
+      if ((h->job_index_on || !h->activated.empty() || !h->streams.empty()) && h2.x < h->cfg.max_instances)
+        track_jobs(h, c, h2.x);
       if ((hd.y & HDR_ENDED) && h2.x < h->cfg.max_instances) {
         ++h->inst_gen[h2.x];
         h->batches_dead.fetch_add(h->hist[h2.x].size(), std::memory_order_relaxed);
@@ -2241,7 +2274,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
       h->hist[cm.instance].push_back({(uint16_t)first, h->key_counter + 1});
       h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[cm.instance]});
     }
-    if (h->job_index_on || !h->activated.empty()) track_jobs(h, c, cm.instance);
+    if (h->job_index_on || !h->activated.empty() || !h->streams.empty()) track_jobs(h, c, cm.instance);
     if (hd.y & HDR_ENDED) {  // completed: its job keys no longer resolve
       ++h->inst_gen[cm.instance];
       h->batches_dead.fetch_add(h->hist[cm.instance].size(), std::memory_order_relaxed);
@@ -2324,6 +2357,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.map_cap = h->cfg.max_commands;
   P.cmd_act = h->st.act ? h->d_cmd_act : nullptr;
   h->run_clock_ms = h->clock_ms;
+  if (!h->streams.empty() || !h->run_streams.empty()) h->run_streams = h->streams;  // (the pushes' deadlines / workers)
   P.tpl = (h->variant == 0 || h->variant == 1 || h->scope_variant()) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
   if (h->msg()) {
     int rc = sync_strings(h);
@@ -2681,6 +2715,9 @@ static uint8_t rejection_type_of(uint32_t reason) {
   }
 }
 
+static void stored_job_record(const zbhip_handle::Activation& a, int64_t key, uint8_t rt, uint8_t intent,
+                              zbhip_record& r);
+
 // One compact row of a plain (non-message) record -> zbhip_record: relabelled keys, record /
 // value type and intent from the row code, document references.  Read-only on the handle, so the
 // bulk drain runs it from several threads.
@@ -2717,6 +2754,21 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
         auto it = h->cont_ids.find(((uint64_t)c << 16) | ord);
         if (it != h->cont_ids.end()) r.aux = (int64_t)it->second;
       }
+    } else if (c6 == C_JOB_PUSHED) {
+      // JOB_BATCH:ACTIVATED of a job stream's push: aux = the job, the job's fields as a JOB record's
+      r.value_type = ZBHIP_VT_JOB_BATCH;
+      r.intent = ZBHIP_JOB_BATCH_ACTIVATED;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.aux = h->key_of(inst, aux_ord);
+      auto it = h->activated.find(r.aux);
+      if (it == h->activated.end()) return ZBHIP_EDEVICE;
+      const zbhip_record k = r;
+      stored_job_record(it->second, r.aux, ZBHIP_RT_EVENT, ZBHIP_JOB_BATCH_ACTIVATED, r);
+      r.key = k.key;
+      r.value_type = ZBHIP_VT_JOB_BATCH;
+      r.aux = k.aux;
+      r.source_index = k.source_index;
+      r.ordinal = k.ordinal;
     } else if (c6 == C_JOB_CREATED || c6 == C_JOB_COMPLETED || c6 == C_JOB_COMPLETE || c6 == C_JOB_CANCELED) {
       r.value_type = ZBHIP_VT_JOB;
       r.intent = c6 == C_JOB_CREATED ? ZBHIP_JOB_CREATED : c6 == C_JOB_COMPLETED ? ZBHIP_JOB_COMPLETED
@@ -4277,6 +4329,65 @@ static int build_job_index(zbhip_handle* h) {
   return ZBHIP_OK;
 }
 
+// JobVariablesCollector.setJobVariables (DbVariableState.getVariablesAsDocument :193-247) over one job's
+// gathered rows (k_activate_jobs' ActivatedOut): the element's scope, its enclosing containers', then the
+// process instance's; names in DbString key order (length, bytes), each once, `requested` only if any.
+static void collect_job_variables(zbhip_handle* h, const uint4& a, const uint2* meta, const long long* val,
+                                  const uint2* slots, const std::vector<uint32_t>& requested, zbhip_activated_job& j) {
+  auto name_less = [h](uint32_t x_, uint32_t y_) {
+    const std::string& x = h->names[x_];
+    const std::string& y = h->names[y_];
+    return x.size() != y.size() ? x.size() < y.size() : x < y;
+  };
+  const uint32_t proc = a.y & 0xFFFF, elem = a.x & 0xFFFF, eord = a.x >> 16;
+  // DbVariableState.visitVariables: the element's scope, then the process instance's
+  const uint32_t nv = std::min<uint32_t>((a.z >> 16) & 0xFF, (uint32_t)kVars);
+  std::vector<uint32_t> taken;
+  const Proc::Mi* m = proc < h->procs.size() ? h->procs[proc].mi_inner(elem) : nullptr;
+  const uint32_t loop = a.w >> 26;
+  if (m && loop >= 1 && loop <= m->items.size()) {
+    // a multi-instance inner instance's scope: its loop variables (setLoopVariables), then the
+    // body's (none), then the process instance's
+    std::vector<zbhip_doc_entry> local;
+    if (m->input_name != NONE)
+      local.push_back({m->input_name, m->items[loop - 1].first, {0, 0, 0}, m->items[loop - 1].second});
+    local.push_back({m->loop_name, (uint8_t)ZBHIP_DOC_INT, {0, 0, 0}, (int64_t)loop});
+    std::sort(local.begin(), local.end(),
+              [&](const zbhip_doc_entry& p, const zbhip_doc_entry& q) { return name_less(p.name_id, q.name_id); });
+    for (const zbhip_doc_entry& d : local) {
+      if (!requested.empty() && std::find(requested.begin(), requested.end(), d.name_id) == requested.end()) continue;
+      taken.push_back(d.name_id);
+      j.variables[j.n_variables++] = d;
+    }
+  }
+  // the element's scope, the instances of its enclosing containers (sub-processes with io-mapped
+  // variables), then the process instance's
+  std::vector<uint32_t> chain{eord};
+  if (proc < h->procs.size() && elem < h->procs[proc].els.size())
+    for (uint32_t c = h->procs[proc].els[elem].flow_scope, d = 0; c != 0 && c < h->procs[proc].els.size() && d < 16;
+         c = h->procs[proc].els[c].flow_scope, ++d)
+      for (uint32_t si = 0; si < (uint32_t)kSlots; ++si)
+        if (slots[si].x != 0xFFFFFFFFu && (slots[si].x & 0xFFFF) == c) chain.push_back(slots[si].x >> 16);
+  chain.push_back(0u);
+  for (uint32_t scope : chain) {
+    std::vector<uint32_t> local;
+    for (uint32_t v = 0; v < nv; ++v)
+      if ((meta[v].x >> 16) == scope) local.push_back(v);
+    std::sort(local.begin(), local.end(),
+              [&](uint32_t p, uint32_t q) { return name_less(meta[p].x & 0xFFFF, meta[q].x & 0xFFFF); });
+    for (uint32_t v : local) {
+      const uint32_t name = meta[v].x & 0xFFFF;
+      if (std::find(taken.begin(), taken.end(), name) != taken.end()) continue;
+      if (!requested.empty() && std::find(requested.begin(), requested.end(), name) == requested.end()) continue;
+      taken.push_back(name);
+      zbhip_doc_entry& d = j.variables[j.n_variables++];
+      d.name_id = name;
+      d.type = (uint8_t)((meta[v].y >> 16) & 0xFF);
+      d.value = val[v];
+    }
+  }
+}
+
 extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* cmd, zbhip_activated_job* jobs,
                                    size_t cap, zbhip_job_batch* res) {
   if (!h || !cmd || !res || (cap && !jobs) || (cmd->type_len && !cmd->type) || (cmd->worker_len && !cmd->worker) ||
@@ -4354,11 +4465,6 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
   (void)hipFree(d_out);
   if (e != hipSuccess) return ZBHIP_EDEVICE;
   std::vector<uint32_t> requested(cmd->variables, cmd->variables + cmd->n_variables);
-  auto name_less = [h](uint32_t a, uint32_t b) {  // DbString order: length, then bytes
-    const std::string& x = h->names[a];
-    const std::string& y = h->names[b];
-    return x.size() != y.size() ? x.size() < y.size() : x < y;
-  };
   for (size_t i = 0; i < n; ++i) {
     const uint8_t* o = outb.data() + i * ob;
     uint4 a;
@@ -4382,52 +4488,7 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     j.process_idx = (int32_t)proc;
     j.element_idx = (int32_t)elem;
     j.retries = proc < h->procs.size() && elem < h->procs[proc].els.size() ? h->procs[proc].els[elem].job_retries : 0;
-    // DbVariableState.visitVariables: the element's scope, then the process instance's
-    const uint32_t nv = std::min<uint32_t>((a.z >> 16) & 0xFF, (uint32_t)kVars);
-    std::vector<uint32_t> taken;
-    const Proc::Mi* m = proc < h->procs.size() ? h->procs[proc].mi_inner(elem) : nullptr;
-    const uint32_t loop = a.w >> 26;
-    if (m && loop >= 1 && loop <= m->items.size()) {
-      // a multi-instance inner instance's scope: its loop variables (setLoopVariables), then the
-      // body's (none), then the process instance's
-      std::vector<zbhip_doc_entry> local;
-      if (m->input_name != NONE)
-        local.push_back({m->input_name, m->items[loop - 1].first, {0, 0, 0}, m->items[loop - 1].second});
-      local.push_back({m->loop_name, (uint8_t)ZBHIP_DOC_INT, {0, 0, 0}, (int64_t)loop});
-      std::sort(local.begin(), local.end(),
-                [&](const zbhip_doc_entry& p, const zbhip_doc_entry& q) { return name_less(p.name_id, q.name_id); });
-      for (const zbhip_doc_entry& d : local) {
-        if (!requested.empty() && std::find(requested.begin(), requested.end(), d.name_id) == requested.end()) continue;
-        taken.push_back(d.name_id);
-        j.variables[j.n_variables++] = d;
-      }
-    }
-    // the element's scope, the instances of its enclosing containers (sub-processes with io-mapped
-    // variables), then the process instance's
-    std::vector<uint32_t> chain{eord};
-    if (proc < h->procs.size() && elem < h->procs[proc].els.size())
-      for (uint32_t c = h->procs[proc].els[elem].flow_scope, d = 0; c != 0 && c < h->procs[proc].els.size() && d < 16;
-           c = h->procs[proc].els[c].flow_scope, ++d)
-        for (const uint2& sl : slots)
-          if (sl.x != 0xFFFFFFFFu && (sl.x & 0xFFFF) == c) chain.push_back(sl.x >> 16);
-    chain.push_back(0u);
-    for (uint32_t scope : chain) {
-      std::vector<uint32_t> local;
-      for (uint32_t v = 0; v < nv; ++v)
-        if ((meta[v].x >> 16) == scope) local.push_back(v);
-      std::sort(local.begin(), local.end(),
-                [&](uint32_t p, uint32_t q) { return name_less(meta[p].x & 0xFFFF, meta[q].x & 0xFFFF); });
-      for (uint32_t v : local) {
-        const uint32_t name = meta[v].x & 0xFFFF;
-        if (std::find(taken.begin(), taken.end(), name) != taken.end()) continue;
-        if (!requested.empty() && std::find(requested.begin(), requested.end(), name) == requested.end()) continue;
-        taken.push_back(name);
-        zbhip_doc_entry& d = j.variables[j.n_variables++];
-        d.name_id = name;
-        d.type = (uint8_t)((meta[v].y >> 16) & 0xFF);
-        d.value = val[v];
-      }
-    }
+    collect_job_variables(h, a, meta, val, slots, requested, j);
     // JobBatchActivatedApplier -> DbJobState.activate: ACTIVATED, out of JOB_ACTIVATABLE, deadline
     h->job_index.erase({tit->second, j.key});
     zbhip_handle::Activation& act = h->activated[j.key];  // (a failed job keeps its retries / errorMessage)
@@ -4441,6 +4502,74 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     act.pik = j.process_instance_key;
     act.proc = j.process_idx;
     act.elem = j.element_idx;
+  }
+  return ZBHIP_OK;
+}
+
+// The push side effect's ActivatedJob (BpmnJobActivationBehavior.publishWork :83-97: JobVariablesCollector
+// over the stream's fetchVariables, then jobStream.push): the stored activation of each pushed job and its
+// variables, gathered in one k_activate_jobs launch in peek mode (nothing written).  A key that is not a
+// live device job comes back with key -1.
+extern "C" int zbhip_job_variables(zbhip_handle* h, const int64_t* job_keys, size_t n, const uint32_t* names,
+                                   size_t n_names, zbhip_activated_job* out) {
+  if (!h || (n && (!job_keys || !out)) || (n_names && !names)) return ZBHIP_EINVAL;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  if (!n) return ZBHIP_OK;
+  std::vector<uint2> list(n);
+  std::vector<uint8_t> live(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t inst = 0xFFFFFFFFu;
+    uint16_t ord = 0;
+    if (zbhip_resolve_key(h, job_keys[i], &inst, &ord) == ZBHIP_OK && inst < h->cfg.max_instances) live[i] = 1;
+    list[i] = make_uint2(live[i] ? inst : 0xFFFFFFFFu, (uint32_t)ord | 1u << 17);
+  }
+  const size_t ob = activated_out_bytes();
+  std::vector<uint8_t> outb(n * ob);
+  uint2* d_list = nullptr;
+  void* d_out = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&d_list), n * sizeof(uint2)) != hipSuccess) return ZBHIP_ENOMEM;
+  if (hipMalloc(&d_out, n * ob) != hipSuccess) {
+    (void)hipFree(d_list);
+    return ZBHIP_ENOMEM;
+  }
+  hipError_t e = hipMemcpyAsync(d_list, list.data(), n * sizeof(uint2), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = launch_activate_jobs(h->st, d_list, (uint32_t)n, d_out, 0, 0, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(outb.data(), d_out, n * ob, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d_list);
+  (void)hipFree(d_out);
+  if (e != hipSuccess) return ZBHIP_EDEVICE;
+  const std::vector<uint32_t> requested(names, names + n_names);
+  for (size_t i = 0; i < n; ++i) {
+    zbhip_activated_job& j = out[i];
+    j = zbhip_activated_job{};
+    j.key = -1;
+    const uint8_t* o = outb.data() + i * ob;
+    uint4 a;
+    uint2 meta[kVars];
+    long long val[kVars];
+    uint2 slots[kSlots];
+    memcpy(&a, o, sizeof a);
+    memcpy(meta, o + sizeof(uint4), sizeof meta);
+    memcpy(val, o + sizeof(uint4) + sizeof meta, sizeof val);
+    memcpy(slots, o + sizeof(uint4) + sizeof meta + sizeof val, sizeof slots);
+    if (!live[i] || !a.w) continue;
+    const uint32_t inst = list[i].x, proc = a.y & 0xFFFF, elem = a.x & 0xFFFF;
+    j.key = job_keys[i];
+    j.element_instance_key = h->key_of(inst, a.x >> 16);
+    j.process_instance_key = h->key_of(inst, 0);
+    j.instance = inst;
+    j.process_idx = (int32_t)proc;
+    j.element_idx = (int32_t)elem;
+    j.retries = proc < h->procs.size() && elem < h->procs[proc].els.size() ? h->procs[proc].els[elem].job_retries : 0;
+    j.deadline = -1;
+    const auto ait = h->activated.find(j.key);
+    if (ait != h->activated.end()) {
+      j.deadline = ait->second.deadline;
+      if (ait->second.fail_fields) j.retries = (uint16_t)ait->second.retries;
+    }
+    collect_job_variables(h, a, meta, val, slots, requested, j);
   }
   return ZBHIP_OK;
 }
@@ -4572,8 +4701,39 @@ extern "C" int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* 
   return ZBHIP_OK;
 }
 
-extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out) {
-  if (!h || !out) return ZBHIP_EINVAL;
+// BpmnJobActivationBehavior.publishWork of a job the host side made ACTIVATABLE (a time-out, a failure
+// with retries left): with a job stream for its type, JOB_BATCH:ACTIVATED (key = nextKey) of the job,
+// ACTIVATED again with the stream's deadline and worker.  Returns the records written (0 or 1).
+static size_t push_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out) {
+  auto it = h->activated.find(job_key);
+  if (it == h->activated.end() || it->second.proc < 0 || (size_t)it->second.proc >= h->procs.size()) return 0;
+  zbhip_handle::Activation& a = it->second;
+  const Proc& P = h->procs[a.proc];
+  if (a.elem < 0 || (size_t)a.elem >= P.els.size()) return 0;
+  const uint32_t tid = P.job_type_id[a.elem];
+  const auto st = h->streams.find(tid);
+  if (st == h->streams.end()) return 0;
+  a.deadline = now + st->second.timeout;
+  a.worker = st->second.worker;
+  a.worker_id = st->second.worker_id;
+  a.state = zbhip_handle::JS_ACTIVATED;
+  if (h->job_index_on) h->job_index.erase({tid, job_key});
+  const int64_t key = ((int64_t)h->cfg.partition_id << 51) + ++h->key_counter;
+  if (h->st.n_slots) {
+    const unsigned long long kc = (unsigned long long)h->key_counter;
+    if (hipMemcpy(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice) != hipSuccess) return 0;
+  }
+  stored_job_record(a, job_key, ZBHIP_RT_EVENT, ZBHIP_JOB_BATCH_ACTIVATED, *out);
+  out->key = key;
+  out->value_type = ZBHIP_VT_JOB_BATCH;
+  out->aux = job_key;
+  return 1;
+}
+
+extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now, zbhip_record* out, size_t cap,
+                                  size_t* n_out) {
+  if (!h || !out || !n_out || cap < 2) return ZBHIP_EINVAL;
+  *n_out = 1;
   if (!h->relabel_ok) return ZBHIP_ESTATE;
   if (int rc = finalize(h)) return rc;
   // JobTimeOutProcessor.processRecord (:46-69): an ACTIVATED job past its deadline times out, anything
@@ -4592,6 +4752,7 @@ extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now,
         if (h->job_index_on && a.proc >= 0 && (size_t)a.proc < h->procs.size() && a.elem >= 0 &&
             (size_t)a.elem < h->procs[a.proc].els.size() && zbhip_resolve_key(h, job_key, &inst, &ord) == ZBHIP_OK)
           h->job_index[{h->procs[a.proc].job_type_id[a.elem], job_key}] = {inst, ord};
+        *n_out += push_job(h, job_key, now, out + 1);  // publishWork (JobTimeOutProcessor.java:55)
         return ZBHIP_OK;
       }
       why = 2;
@@ -4699,6 +4860,7 @@ extern "C" int zbhip_fail_job(zbhip_handle* h, const zbhip_job_fail* cmd, zbhip_
   if (cmd->retries > 0) {
     a.state = zbhip_handle::JS_ACTIVATABLE;
     if (h->job_index_on) h->job_index[{tid, job_key}] = {inst, ord};
+    *n_out += push_job(h, job_key, cmd->timestamp, out + 1);  // retryImmediately: publishWork (:129-132)
     return ZBHIP_OK;
   }
   a.state = zbhip_handle::JS_FAILED;
@@ -4731,6 +4893,25 @@ extern "C" int zbhip_fail_job(zbhip_handle* h, const zbhip_job_fail* cmd, zbhip_
   r.message_name = r.bpmn_process_id = 0xFFFF;
   *n_out = 2;
   return ZBHIP_OK;
+}
+
+extern "C" int zbhip_set_job_stream(zbhip_handle* h, const char* type, size_t type_len, const char* worker,
+                                    size_t worker_len, int64_t timeout, int on) {
+  if (!h || !type || !type_len || (worker_len && !worker) || (on && timeout < 1)) return ZBHIP_EINVAL;
+  const uint32_t tid = h->job_type(std::string(type, type_len));
+  if (on) {
+    const std::string w(worker ? worker : "", worker_len);
+    const int64_t wid = w.empty() ? (int64_t)ZBHIP_NO_STRING : zbhip_intern_string(h, w.data(), w.size());
+    if (wid < 0) return (int)wid;
+    const auto old = h->streams.find(tid);
+    const bool same = old != h->streams.end();
+    h->streams[tid] = {w, (uint32_t)wid, timeout};
+    if (same) return ZBHIP_OK;  // (the program words only say whether a stream exists)
+  } else if (!h->streams.erase(tid)) {
+    return ZBHIP_OK;
+  }
+  h->ring_ok = false;  // the device log writer does not write pushes: the host serialiser does
+  return rebuild_program(h);
 }
 
 extern "C" int zbhip_job_state(zbhip_handle* h, int64_t job_key) {

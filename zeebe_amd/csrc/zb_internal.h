@@ -107,6 +107,8 @@ enum : uint8_t {
   C_TIMER_TRIGGERED = 54,
   C_TIMER_CANCELED = 55,  // CatchEventBehavior.unsubscribeFromTimerEvent; dueDate in StepParams.cmd_due
   C_TIMER_NEXT = 56,
+  C_JOB_PUSHED = 59,      // JOB_BATCH:ACTIVATED of a job stream's push (BpmnJobActivationBehavior.publishWork):
+                          // key = the batch, aux = the job, elem = the task
   C_VAR_MAPPED = 58,       // VARIABLE:CREATED / UPDATED of an io mapping (BpmnVariableMappingBehavior): key =
                            // the variable, aux = its scope, elem = its name, flags = zbhip_doc_type | updated
                            // << 3 | value slot << 4 (the value in StepParams.map_val)

@@ -370,6 +370,15 @@ class Partition:
         check(self.L.zbhip_activate_jobs(self.h, C.byref(cmd), out.ctypes.data, cap, C.byref(res)), "zbhip_activate_jobs")
         return res.key, out[: res.n_jobs], res.reason
 
+    def job_variables(self, job_keys, variables=()):
+        """The pushed jobs' ActivatedJob rows (zbhip_job_variables: activation + variables document)."""
+        keys = np.asarray(job_keys, dtype=np.int64)
+        names = np.asarray([self.intern(v) for v in variables], dtype=np.uint32)
+        out = np.zeros(max(len(keys), 1), dtype=abi.ACTIVATED_JOB_DTYPE)
+        check(self.L.zbhip_job_variables(self.h, keys.ctypes.data, len(keys), names.ctypes.data if len(names) else None,
+                                         len(names), out.ctypes.data), "zbhip_job_variables")
+        return out[: len(keys)]
+
     def key_before(self, i):
         k = C.c_int64()
         check(self.L.zbhip_key_before(self.h, i, C.byref(k)), "zbhip_key_before")
@@ -430,17 +439,25 @@ class Partition:
         return out[: n.value]
 
     def time_out_job(self, job_key, now):
-        """JOB:TIME_OUT of a device job (zbhip_time_out_job): JOB:TIMED_OUT or the rejection, one
-        RECORD_DTYPE row."""
-        out = np.zeros(1, dtype=abi.RECORD_DTYPE)
-        check(self.L.zbhip_time_out_job(self.h, int(job_key), int(now), out.ctypes.data), "zbhip_time_out_job")
-        return out[0]
+        """JOB:TIME_OUT of a device job (zbhip_time_out_job): JOB:TIMED_OUT (+ its push) or the rejection,
+        RECORD_DTYPE rows."""
+        out = np.zeros(2, dtype=abi.RECORD_DTYPE)
+        n = C.c_size_t()
+        check(self.L.zbhip_time_out_job(self.h, int(job_key), int(now), out.ctypes.data, 2, C.byref(n)),
+              "zbhip_time_out_job")
+        return out[: n.value]
 
-    def fail_job(self, job_key, retries, error_message="", retry_backoff=0, n_variables=0):
+    def set_job_stream(self, job_type, worker="", timeout=300000, on=True):
+        """zbhip_set_job_stream: a job stream of `job_type` (jobs of it are pushed when created)."""
+        t, w = job_type.encode(), worker.encode()
+        check(self.L.zbhip_set_job_stream(self.h, t, len(t), w, len(w), int(timeout), 1 if on else 0),
+              "zbhip_set_job_stream")
+
+    def fail_job(self, job_key, retries, error_message="", retry_backoff=0, n_variables=0, timestamp=0):
         """JOB:FAIL of a device job (zbhip_fail_job): the JOB:FAILED (+ INCIDENT:CREATED) or rejection
         records, RECORD_DTYPE rows; None when the command is outside the device subset (the engine's)."""
         m = error_message.encode()
-        cmd = abi.JobFail(job_key=int(job_key), retry_backoff=int(retry_backoff), error_message=m,
+        cmd = abi.JobFail(job_key=int(job_key), retry_backoff=int(retry_backoff), timestamp=int(timestamp), error_message=m,
                           error_message_len=len(m), retries=int(retries), n_variables=int(n_variables))
         out = np.zeros(2, dtype=abi.RECORD_DTYPE)
         n = C.c_size_t()

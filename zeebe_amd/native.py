@@ -33,7 +33,8 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_serialize_log_device", "zbhip_log_device_copy", "zbhip_continuations",
            "zbhip_pending_continuations", "zbhip_current_key", "zbhip_set_key_if_higher",
            "zbhip_select_instances_db", "zbhip_drain_command", "zbhip_outbox_command", "zbhip_due_timers",
-           "zbhip_timed_out_jobs", "zbhip_time_out_job", "zbhip_fail_job", "zbhip_job_state"]
+           "zbhip_timed_out_jobs", "zbhip_time_out_job", "zbhip_fail_job", "zbhip_job_state", "zbhip_set_job_stream",
+           "zbhip_job_variables"]
 
 
 class ZbhipError(RuntimeError):
@@ -119,9 +120,11 @@ def load():
     L.zbhip_job_batch_rejection_reason.argtypes = [C.POINTER(abi.JobActivation), C.POINTER(abi.JobBatch), C.c_char_p, sz]
     L.zbhip_due_timers.argtypes = [vp, i64, vp, sz, C.POINTER(sz), C.POINTER(i64)]
     L.zbhip_timed_out_jobs.argtypes = [vp, i64, vp, sz, C.POINTER(sz)]
-    L.zbhip_time_out_job.argtypes = [vp, i64, i64, vp]
+    L.zbhip_time_out_job.argtypes = [vp, i64, i64, vp, sz, C.POINTER(sz)]
+    L.zbhip_set_job_stream.argtypes = [vp, C.c_char_p, sz, C.c_char_p, sz, i64, C.c_int]
     L.zbhip_fail_job.argtypes = [vp, C.POINTER(abi.JobFail), vp, sz, C.POINTER(sz)]
     L.zbhip_job_state.argtypes = [vp, i64]
+    L.zbhip_job_variables.argtypes = [vp, vp, sz, vp, sz, vp]
     L.zbhip_stream.argtypes = [vp]
     L.zbhip_stream.restype = vp
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
