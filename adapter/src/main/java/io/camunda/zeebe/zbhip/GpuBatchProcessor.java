@@ -25,7 +25,10 @@
  *  - the engine's scheduled tasks read device-held state through DeviceScheduledState (timerState,
  *    jobState, pending*State below, passed to the checkers EngineProcessors builds), device TIMER:CREATED
  *    records schedule the DueDateTimerChecker as the engine's do (a side effect), and JOB:TIME_OUT of a
- *    device job runs through zbhip_time_out_job (JobTimeOutProcessor.java:46-73).
+ *    device job runs through zbhip_time_out_job (JobTimeOutProcessor.java:46-73), JOB:FAIL through
+ *    zbhip_fail_job (JobFailProcessor.java:79-162);
+ *  - job push (BpmnJobActivationBehavior.publishWork): the broker's JobStreamer mirrored per device job
+ *    type into zbhip_set_job_stream before each window (JobStreams), the stream's push a post-commit task.
  * The Python mirror zeebe_amd/adapter.py is this class line for line in behaviour; tests/test_gpu_psm.py
  * runs it inside a restatement of ProcessingStateMachine against the engine alone.
  *
@@ -160,6 +163,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   private int followUps; // follow-ups of the current device batch the platform feeds back
   private boolean windowDone = true; // every command of the current window was emitted
   private io.camunda.zeebe.engine.processing.timer.DueDateTimerChecker dueDateTimerChecker;
+  private JobStreams jobStreams = new JobStreams(null);
 
   public GpuBatchProcessor(
       final Engine engine,
@@ -273,6 +277,10 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     if (record.getValueType() == ValueType.JOB && record.getIntent() == JobIntent.TIME_OUT
         && ZbHip.resolveKey(handle, record.getKey()) >= 0) {
       return timeOutJob(record, out);
+    }
+    if (record.getValueType() == ValueType.JOB && record.getIntent() == JobIntent.FAIL
+        && ZbHip.resolveKey(handle, record.getKey()) >= 0) {
+      return failJob(record, out);
     }
     int i = window.covers(record.getPosition()) ? window.indexOf(record.getPosition()) : -1;
     if (i < 0) {
@@ -407,8 +415,10 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     }
     // keys the engine generated since the last window come first (setKeyIfHigher)
     ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
-    // the window's clock: TIMER:CREATED dueDates (CatchEventBehavior.java:310, ActorClock)
+    // the window's clock: TIMER:CREATED dueDates (CatchEventBehavior.java:310, ActorClock), pushed jobs'
+    // deadlines; the job streams open now (publishWork asks JobStreamer per job)
     ZbHip.setClock(handle, ActorClock.currentTimeMillis());
+    jobStreams.sync(handle, deviceJobTypes());
     window.submitRun(handle);
     windowDone = false;
   }
@@ -563,6 +573,11 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     return new DeviceScheduledState.PendingMessageSubscriptions(this, engineState);
   }
 
+  /** The broker's JobStreamer (the one EngineProcessors gets): device jobs of streamed types are pushed. */
+  public void setJobStreamer(final io.camunda.zeebe.engine.processing.streamprocessor.JobStreamer streamer) {
+    jobStreams = new JobStreams(streamer);
+  }
+
   /** The DueDateTimerChecker device TIMER:CREATED records schedule (CatchEventBehavior's side effect). */
   public void setDueDateTimerChecker(final io.camunda.zeebe.engine.processing.timer.DueDateTimerChecker checker) {
     dueDateTimerChecker = checker;
@@ -594,22 +609,102 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   // ---- JOB:TIME_OUT of a device job (JobTimeOutProcessor.java:46-73) ------------------------------
 
   private ProcessingResult timeOutJob(final TypedRecord record, final ProcessingResultBuilder out) {
+    jobStreams.sync(handle, deviceJobTypes());
+    ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
     try (Arena a = Arena.ofConfined()) {
-      final MemorySegment r = a.allocate(ZbHip.RECORD);
-      ZbHip.timeOutJob(handle, record.getKey(), ActorClock.currentTimeMillis(), r);
-      final RecordMetadata meta = new RecordMetadata().valueType(ValueType.JOB);
+      final MemorySegment r = a.allocate(ZbHip.RECORD.byteSize() * 2, 8);
+      final long n = ZbHip.timeOutJob(handle, record.getKey(), ActorClock.currentTimeMillis(), r);
       if (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value()) {
+        final RecordMetadata meta = new RecordMetadata().valueType(ValueType.JOB);
         meta.recordType(RecordType.COMMAND_REJECTION).intent(JobIntent.TIME_OUT)
             .rejectionType(io.camunda.zeebe.protocol.record.RejectionType.NOT_FOUND)
             .rejectionReason(rejectionReason(r));
         out.appendRecord(record.getKey(), (JobRecord) record.getValue(), meta);
-      } else {
-        // JOB:TIMED_OUT with the stored job; publishWork -> notifyWorkAvailable (a side effect, no record)
-        meta.recordType(RecordType.EVENT).intent(JobIntent.TIMED_OUT);
-        out.appendRecord(record.getKey(), storedJob(r), meta);
+        return out.build();
+      }
+      // JOB:TIMED_OUT with the stored job; publishWork: the push (JOB_BATCH:ACTIVATED) of a job stream's
+      // type, else notifyWorkAvailable (a side effect, no record)
+      appendDeviceRecords(r, n, out);
+    }
+    keyGenerator.setKeyIfHigher(ZbHip.currentKey(handle));
+    return out.build();
+  }
+
+  // ---- JOB:FAIL of a device job (JobFailProcessor.java:79-162) -------------------------------------
+
+  private ProcessingResult failJob(final TypedRecord record, final ProcessingResultBuilder out) {
+    final JobRecord v = (JobRecord) record.getValue();
+    jobStreams.sync(handle, deviceJobTypes());
+    ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
+    final int slot = (int) (ZbHip.resolveKey(handle, record.getKey()) >>> 16);
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment r = a.allocate(ZbHip.RECORD.byteSize() * 2, 8);
+      final byte[] message = new byte[v.getErrorMessageBuffer().capacity()];
+      v.getErrorMessageBuffer().getBytes(0, message);
+      final long n = ZbHip.failJob(handle, record.getKey(), v.getRetries(), v.getRetryBackoff(), message,
+          v.getVariablesBuffer().capacity() > 1 ? 1 : 0, ActorClock.currentTimeMillis(), r);
+      if (n < 0) {
+        // outside the device subset (variables, a retry back-off): the engine's, with the instance
+        handOff(slot);
+        keyGenerator.setKeyIfHigher(ZbHip.currentKey(handle));
+        return engine.process(record, out);
+      }
+      if (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value()) {
+        final RecordMetadata meta = new RecordMetadata().valueType(ValueType.JOB);
+        meta.recordType(RecordType.COMMAND_REJECTION).intent(JobIntent.FAIL)
+            .rejectionType(io.camunda.zeebe.protocol.record.RejectionType.get(
+                (short) (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 43) & 0xFF)))
+            .rejectionReason(rejectionReason(r));
+        out.appendRecord(record.getKey(), v, meta);
+        return out.build();
+      }
+      // JOB:FAILED, then the push (retries left) or INCIDENT:CREATED JOB_NO_RETRIES
+      final boolean incident = appendDeviceRecords(r, n, out);
+      keyGenerator.setKeyIfHigher(ZbHip.currentKey(handle));
+      if (incident) {
+        // the instance waits for the incident's resolution (JOB:UPDATE_RETRIES, INCIDENT:RESOLVE): the
+        // engine's, with the job's FAILED state and the incident rows
+        handOff(slot);
       }
     }
     return out.build();
+  }
+
+  /** Event rows of a host-side job call (TIMED_OUT / FAILED / JOB_BATCH push / INCIDENT); true if an incident. */
+  private boolean appendDeviceRecords(final MemorySegment rows, final long n, final ProcessingResultBuilder out) {
+    boolean incident = false;
+    for (long k = 0; k < n; k++) {
+      final MemorySegment r = rows.asSlice(ZbHip.RECORD.byteSize() * k, ZbHip.RECORD.byteSize());
+      final ValueType vt = ValueType.get((short) r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 41));
+      final byte intent = r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 42);
+      final RecordMetadata meta = new RecordMetadata().recordType(RecordType.EVENT).valueType(vt)
+          .intent(io.camunda.zeebe.protocol.record.intent.Intent.fromProtocolValue(vt, intent));
+      final var value = window.valueOf(r, this);
+      out.appendRecord(r.get(java.lang.foreign.ValueLayout.JAVA_LONG, 0), value, meta);
+      if (vt == ValueType.JOB_BATCH) {
+        jobStreams.push(out, handle, (JobBatchRecord) value, this);
+      }
+      incident |= vt == ValueType.INCIDENT;
+    }
+    return incident;
+  }
+
+  JobStreams jobStreams() {
+    return jobStreams;
+  }
+
+  /** The job types of device processes (the streams the device must know of). */
+  private Set<String> deviceJobTypes() {
+    final Set<String> types = new HashSet<>();
+    for (final ZbHip.Deployed d : byIndex) {
+      for (final String t : d.jobTypes()) {
+        if (t != null && !t.isEmpty()) {
+          types.add(t);
+        }
+      }
+    }
+    types.removeAll(engineJobTypes);
+    return types;
   }
 
   // ---- job activation (JobBatchActivateProcessor.java:60-143) --------------------------------------

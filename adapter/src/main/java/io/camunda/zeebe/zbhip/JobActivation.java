@@ -98,7 +98,7 @@ record JobActivation(MemorySegment command, MemorySegment jobs, long capacity, M
   }
 
   /** The job's collected variables (zbhip_doc_entry rows) as a msgpack document. */
-  private static UnsafeBuffer variables(final MemorySegment job, final GpuBatchProcessor p) {
+  static UnsafeBuffer variables(final MemorySegment job, final GpuBatchProcessor p) {
     final int n = job.get(JAVA_SHORT, 46) & 0xFFFF;
     final ExpandableArrayBuffer buf = new ExpandableArrayBuffer();
     final MsgPackWriter w = new MsgPackWriter().wrap(buf, 0);

@@ -23,6 +23,7 @@ import org.agrona.ExpandableArrayBuffer;
 import io.camunda.zeebe.protocol.impl.record.RecordMetadata;
 import io.camunda.zeebe.protocol.impl.record.UnifiedRecordValue;
 import io.camunda.zeebe.protocol.impl.record.value.incident.IncidentRecord;
+import io.camunda.zeebe.protocol.impl.record.value.job.JobBatchRecord;
 import io.camunda.zeebe.protocol.impl.record.value.job.JobRecord;
 import io.camunda.zeebe.protocol.impl.record.value.message.MessageRecord;
 import io.camunda.zeebe.protocol.impl.record.value.message.MessageSubscriptionRecord;
@@ -357,6 +358,8 @@ final class Window {
       } else if (valueType == ValueType.PROCESS_INSTANCE.value()
           && intent == ProcessInstanceIntent.ELEMENT_COMPLETED.value() && rec.get(JAVA_INT, 36) == 0) {
         p.instanceEnded(instances[i]); // the process element (index 0) completed
+      } else if (valueType == ValueType.JOB_BATCH.value() && recordType == RecordType.EVENT.value()) {
+        p.jobStreams().push(out, handle, (JobBatchRecord) value, p); // publishWork's push, post-commit
       } else if (valueType == ValueType.TIMER.value() && recordType == RecordType.EVENT.value()
           && intent == TimerIntent.CREATED.value()) {
         p.timerCreated(out, ((TimerRecord) value).getDueDate()); // DueDateTimerChecker.scheduleTimer, post-commit
@@ -433,7 +436,29 @@ final class Window {
           v.setDeadline(deadline)
               .setWorker(new UnsafeBuffer(worker == Messages.NO_STRING ? new byte[0] : p.stringValue(worker)));
         }
+        if (r.get(JAVA_BYTE, 40) == RecordType.EVENT.value() && (r.get(JAVA_BYTE, 47) & 1) != 0) {
+          // a failed job's stored retries and errorMessage (JobFailProcessor.failJob): reason_arg bit 0,
+          // retries in partition, the errorMessage's value-dictionary id in message_name | bpmn_process_id << 16
+          final int eid = (r.get(JAVA_SHORT, 68) & 0xFFFF) | (r.get(JAVA_SHORT, 70) & 0xFFFF) << 16;
+          v.setRetries(r.get(JAVA_INT, 72))
+              .setErrorMessage(eid == Messages.NO_STRING ? "" : new String(p.stringValue(eid), java.nio.charset.StandardCharsets.UTF_8));
+        }
         return v.setTenantId(TENANT);
+      }
+      case JOB_BATCH -> {
+        // a job stream's push (BpmnJobActivationBehavior.publishWork :61-100): the job (its row read as
+        // JOB:CREATED) in a fresh JobBatchRecord with the stream's type, worker and timeout
+        final MemorySegment asJob = Arena.ofAuto().allocate(ZbHip.RECORD);
+        asJob.copyFrom(r);
+        asJob.set(JAVA_BYTE, 41, (byte) ValueType.JOB.value());
+        asJob.set(JAVA_BYTE, 42, (byte) JobIntent.CREATED.value());
+        asJob.set(JAVA_LONG, 48, -1L);
+        final JobRecord job = (JobRecord) value(asJob, i, p);
+        final JobBatchRecord v = new JobBatchRecord();
+        v.setType(job.getTypeBuffer()).setWorker(job.getWorkerBuffer()).setTimeout(p.jobStreams().timeout(job.getType()));
+        v.jobKeys().add().setValue(aux);
+        v.jobs().add().wrapWithoutVariables(job);
+        return v;
       }
       case VARIABLE -> {
         final VariableRecord v = new VariableRecord();
@@ -476,8 +501,14 @@ final class Window {
         // BpmnIncidentBehavior.createIncident (:51-71) of an exclusive gateway: the ErrorType ordinal
         // in zbhip_record.partition, the message composed by the library (zbhip_incident_message)
         final IncidentRecord v = new IncidentRecord();
+        final boolean job = r.get(JAVA_INT, 72) == ErrorType.JOB_NO_RETRIES.ordinal();
+        if (job) { // JobFailProcessor.raiseIncident (:139-162): the job's key and message
+          final int mid = r.get(JAVA_INT, 64);
+          v.setJobKey(aux).setErrorMessage(new String(p.stringValue(mid), java.nio.charset.StandardCharsets.UTF_8));
+        } else {
+          v.setErrorMessage(p.incidentMessage(r));
+        }
         v.setErrorType(ErrorType.values()[r.get(JAVA_INT, 72)])
-            .setErrorMessage(p.incidentMessage(r))
             .setBpmnProcessId(new UnsafeBuffer(d.bpmnProcessId().getBytes()))
             .setProcessDefinitionKey(d.definitionKey())
             .setProcessInstanceKey(pik)

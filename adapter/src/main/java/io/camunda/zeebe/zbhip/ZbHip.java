@@ -216,6 +216,9 @@ public final class ZbHip {
   private static final MethodHandle SET_JOB_STREAM =
       fn("zbhip_set_job_stream",
           FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, JAVA_LONG, JAVA_INT));
+  private static final MethodHandle JOB_VARIABLES =
+      fn("zbhip_job_variables",
+          FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle JOB_STATE =
       fn("zbhip_job_state", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG));
 
@@ -623,6 +626,15 @@ public final class ZbHip {
       check((int) call(SET_JOB_STREAM, h, t, (long) type.length, w, (long) worker.length, timeout, on ? 1 : 0),
           "zbhip_set_job_stream");
     }
+  }
+
+  /**
+   * zbhip_job_variables: the pushed jobs' zbhip_activated_job rows (their activation and the variables of
+   * the stream's fetchVariables, {@code names}: name ids, none = all) into {@code out}.
+   */
+  public static void jobVariables(final MemorySegment h, final MemorySegment keys, final long n,
+      final MemorySegment names, final long nNames, final MemorySegment out) {
+    check((int) call(JOB_VARIABLES, h, keys, n, names, nNames, out), "zbhip_job_variables");
   }
 
   /** zbhip_job_state: 0 ACTIVATABLE, 1 ACTIVATED, 2 FAILED, 3 gone, -1 not a device job. */
