@@ -184,8 +184,40 @@ def test_device_window_with_duplicate_subjects_is_planned_like_a_host_window():
     for f in FIELDS:
         assert np.array_equal(got[f], want[f]), f
     assert dev_p.state() == host.state()
-    # a subject out of range refuses the device window
+    # a subject out of range refuses the device window (the speculative check reports it at the run)
     bad = complete_commands([99], [5])
     tb = torch.from_numpy(bad.view(np.uint8).copy()).to("cuda")
     with pytest.raises(ZbhipError):
         dev_p.submit_device(tb.data_ptr(), 1)
+        dev_p.run()
+
+
+def test_speculative_subject_check_replays_a_window_with_repeats():
+    """Untrusted device windows launch before their subject check is read back: k_step runs guarded by
+    the check's flag, and the next call that depends on the window reads it.  A window with a repeated
+    subject did nothing on the device; it is replanned on the host and run again before the next window
+    -- the statistics (transitions, records, completed instances) equal the host-planned run's."""
+    import torch
+    xml = bpmn.linear_process(3)
+    host, dev_p = Partition(max_instances=16, max_commands=32), Partition(max_instances=16, max_commands=32)
+    for p in (host, dev_p):
+        p.deploy(xml)
+        p.submit(create_commands(8))
+        p.run()
+        p.drain()
+    first = np.concatenate([complete_commands(np.arange(8), np.full(8, 5)), complete_commands(np.arange(4), np.full(4, 5))])
+    second = complete_commands(np.arange(8), np.full(8, 9))  # the next task's jobs
+    host.submit(first)
+    host.run(abi.RUN_NO_RESULTS)
+    host.submit(second)
+    host.run(abi.RUN_NO_RESULTS | abi.RUN_ACCUMULATE)
+    want = host.stats()
+    ts = [torch.from_numpy(c.view(np.uint8).copy()).to("cuda") for c in (first, second)]
+    dev_p.submit_device(ts[0].data_ptr(), len(first))
+    dev_p.run(abi.RUN_NO_RESULTS)
+    dev_p.submit_device(ts[1].data_ptr(), len(second))  # reads the first window's flag: replays it
+    dev_p.run(abi.RUN_NO_RESULTS | abi.RUN_ACCUMULATE)
+    got = dev_p.stats()  # reads the second window's flag (clean)
+    for k in ("transitions", "records", "completed_instances", "fallback"):
+        assert got[k] == want[k], k
+    assert want["completed_instances"] == 0 and want["transitions"] > 0

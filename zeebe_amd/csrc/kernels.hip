@@ -3126,6 +3126,9 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
 #ifdef ZB_STAMPS
   unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0};
 #endif
+  // a speculatively launched untrusted window whose subject check found a repeat: no lane touches
+  // state or output (uniform: the whole grid returns; the host replans and runs the window again)
+  if (P.guard && *P.guard) return;
   const uint32_t n_chunks = (P.n_launch + K::B - 1) / K::B;
   const uint32_t G = gridDim.x;
   const uint32_t lane = threadIdx.x & 63;

@@ -609,6 +609,23 @@ struct zbhip_handle {
   uint32_t* d_seen = nullptr;
   uint32_t* d_check_flag = nullptr;
   uint32_t check_stamp = 0;
+  // speculative subject check of an untrusted device window (no host read before its launch): the
+  // check's flag travels to pinned memory behind an event; k_step launches guarded by it, and the next
+  // host call that depends on the window (resolve_guard) reads the flag -- a repeat replans and reruns
+  struct GuardedWindow {
+    const zbhip_command* cmds;
+    size_t n;
+    const zbhip_doc_entry* docs;
+    size_t n_docs;
+    const zbhip_xpart_cmd* xparts;
+    size_t n_xparts;
+    int64_t doc_base, source_base;  // the handle's counters before the window (rolled back on a replay)
+    uint32_t run_flags;
+  } guard_win{};
+  bool guard_armed = false;    // submitted with a speculative check, not run yet
+  bool guard_pending = false;  // run guarded, flag not read yet
+  uint32_t* h_check_flag = nullptr;  // pinned
+  hipEvent_t check_ev = nullptr;
   // resolve_key: the generation of every subject (bumped when an instance is created or ends, so
   // keys of an earlier instance in a reused slot never resolve); stale entries are compacted away
   std::vector<uint32_t> inst_gen;
@@ -792,6 +809,7 @@ struct zbhip_handle {
 
 static int finalize(zbhip_handle* h);
 static int settle(zbhip_handle* h);
+static int resolve_guard(zbhip_handle* h);
 
 extern "C" {
 
@@ -906,6 +924,9 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
 
 void zbhip_close(zbhip_handle* h) {
   if (!h) return;
+  if (h->check_ev) (void)hipEventSynchronize(h->check_ev);
+  if (h->h_check_flag) (void)hipHostFree(h->h_check_flag);
+  if (h->check_ev) (void)hipEventDestroy(h->check_ev);
   (void)hipFree(h->st.hdr);
   (void)hipFree(h->st.slots);
   (void)hipFree(h->st.var_meta);
@@ -1533,9 +1554,9 @@ static bool slot_kind(uint8_t k) { return zb_slot_kind(k); }
 // rounds (the reference processes them in log order).  Message commands may touch an instance of
 // this partition and instance commands a correlation slot, so a change between the two classes
 // starts a new epoch: every later command goes to a round after all earlier ones.
-// dev_cmds: the window's commands already uploaded (a large plain window): its subjects are checked
-// for repeats on the device (k_subject_check) instead of claimed on the host threads
-static int plan_rounds(zbhip_handle* h, const zbhip_command* dev_cmds = nullptr) {
+// A large plain window's subjects are claimed on the host threads first (one atomic stamp exchange
+// each): the common window addresses every instance once and needs no ordered pass.
+static int plan_rounds(zbhip_handle* h) {
   h->round_begin.clear();
   h->h_order.clear();
   // a CREATE into an instance slot that an earlier command of the same window addressed is refused:
@@ -1570,22 +1591,7 @@ static int plan_rounds(zbhip_handle* h, const zbhip_command* dev_cmds = nullptr)
     return h->plan_stamp;
   };
   uint32_t stamp = next_stamp();
-  if (!msg && h->n_cmds >= (1u << 16) && dev_cmds) {
-    if (++h->check_stamp == 0) {
-      HIPCHK(hipMemsetAsync(h->d_seen, 0, ((size_t)h->cfg.max_instances + h->st.n_slots) * sizeof(uint32_t), h->stream));
-      h->check_stamp = 1;
-    }
-    uint32_t flag = 0;
-    HIPCHK(hipMemsetAsync(h->d_check_flag, 0, sizeof(uint32_t), h->stream));
-    HIPCHK(launch_subject_check(reinterpret_cast<const uint4*>(dev_cmds), (uint32_t)h->n_cmds, h->cfg.max_instances,
-                                h->st.n_slots, h->d_seen, h->check_stamp, h->d_check_flag, h->stream));
-    HIPCHK(hipMemcpyAsync(&flag, h->d_check_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    // (flag 2: a kind the device check does not know -- validated on the host already: the ordered
-    // pass below decides)
-    if (!flag) return ZBHIP_OK;  // one round: identity order
-    stamp = next_stamp();
-  } else if (!msg && h->n_cmds >= (1u << 16)) {
+  if (!msg && h->n_cmds >= (1u << 16)) {
     // the common window addresses every instance once: claim the subjects on the worker threads
     // (an atomic stamp exchange each); a repeat falls through to the ordered pass below, with a
     // fresh stamp
@@ -1705,6 +1711,7 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   const auto t0 = now();
   // the previous submit's uploads read the handle's staging buffers: done before they are rewritten
   // (a run in between has waited for them already; two submits in a row wait here)
+  if (int rc0 = resolve_guard(h)) return rc0;  // the last window's speculative check
   if (h->upload_ev) HIPCHK(hipEventSynchronize(h->upload_ev));
   int rc = settle(h);  // the previous window's keys are fixed before its commands are replaced
   if (rc) return rc;
@@ -1759,10 +1766,8 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
   h->n_cmds = n;
   h->n_docs = n_docs;
   const auto t2 = now();
-  // a large plain window goes up before planning, and its subjects are checked there
-  const bool early = !continues && !h->msg() && n >= (1u << 16);
-  if (early) HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
-  rc = plan_rounds(h, early ? reinterpret_cast<const zbhip_command*>(h->d_cmds) : nullptr);
+  // the host has the window: its subjects are claimed on the host threads (no device round trip)
+  rc = plan_rounds(h);
   if (rc) {
     h->n_cmds = h->n_docs = h->n_xparts = 0;
     return rc;
@@ -1787,8 +1792,7 @@ int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const 
     cmds = h->h_cmds.data();
   }
   h->window_continues = continues;
-  if (n && !early)
-    HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
+  if (n) HIPCHK(hipMemcpyAsync(h->d_cmds, h->h_cmds.data(), n * sizeof(zbhip_command), hipMemcpyHostToDevice, h->stream));
   if (n_docs)
     HIPCHK(hipMemcpyAsync(h->d_docs, h->h_docs.data(), n_docs * sizeof(zbhip_doc_entry), hipMemcpyHostToDevice,
                           h->stream));
@@ -1813,6 +1817,36 @@ int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n
   return zbhip_submit_device_ex(h, dev_cmds, n, dev_docs, n_docs, nullptr, 0);
 }
 
+static int replan_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
+                                size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts, bool* replanned);
+
+// The flag of a speculatively checked device window (check_device_window): read once, before anything
+// depends on the window.  Clean: nothing to do.  A repeated subject: the guarded launch did nothing; the
+// window is replanned on the host and run again with its run flags (before any later window).  A subject
+// out of range: the window is refused (nothing of it ran) and this call reports ZBHIP_EINVAL.
+static int resolve_guard(zbhip_handle* h) {
+  if (h->guard_armed) {  // submitted, never run: a new submit replaces it
+    h->guard_armed = false;
+    return ZBHIP_OK;
+  }
+  if (!h->guard_pending) return ZBHIP_OK;
+  h->guard_pending = false;
+  HIPCHK(hipEventSynchronize(h->check_ev));
+  const uint32_t flag = *h->h_check_flag;
+  if (!flag) return ZBHIP_OK;
+  const auto w = h->guard_win;
+  h->next_doc_base = w.doc_base;  // the window's log positions and documents are given again
+  h->next_source = w.source_base;
+  h->ran = false;
+  h->results = false;
+  h->n_cmds = 0;
+  if (flag & 2) return ZBHIP_EINVAL;
+  bool replanned = false;
+  if (int rc = replan_device_window(h, w.cmds, w.n, w.docs, w.n_docs, w.xparts, w.n_xparts, &replanned)) return rc;
+  const int rc = zbhip_run(h, w.run_flags);
+  return rc < 0 ? rc : ZBHIP_OK;
+}
+
 // A device window's subjects are checked on the device (k_subject_check): a window that addresses
 // one subject twice is copied to the host and planned into rounds like a host window (so it runs
 // in log order per subject); a subject out of range refuses the window.  Handles opened with
@@ -1825,14 +1859,35 @@ static int check_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, s
     HIPCHK(hipMemsetAsync(h->d_seen, 0, ((size_t)h->cfg.max_instances + h->st.n_slots) * sizeof(uint32_t), h->stream));
     h->check_stamp = 1;
   }
-  uint32_t flag = 0;
   HIPCHK(hipMemsetAsync(h->d_check_flag, 0, sizeof(uint32_t), h->stream));
   HIPCHK(launch_subject_check(reinterpret_cast<const uint4*>(dev_cmds), (uint32_t)n, h->cfg.max_instances, h->st.n_slots,
                               h->d_seen, h->check_stamp, h->d_check_flag, h->stream));
+  if (!h->msg() && !getenv("ZBHIP_SYNC_SUBJECT_CHECK")) {
+    // speculative: the flag follows into pinned memory behind an event, nobody waits now; the run
+    // launches its k_step guarded by the device flag (resolve_guard reads it later)
+    if (!h->h_check_flag) {
+      if (hipHostMalloc(reinterpret_cast<void**>(&h->h_check_flag), sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        return ZBHIP_ENOMEM;
+      *h->h_check_flag = 0;
+    }
+    if (!h->check_ev) HIPCHK(hipEventCreateWithFlags(&h->check_ev, hipEventDisableTiming));
+    HIPCHK(hipMemcpyAsync(h->h_check_flag, h->d_check_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipEventRecord(h->check_ev, h->stream));
+    h->guard_win = {dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, h->next_doc_base, h->next_source, 0};
+    h->guard_armed = true;
+    return ZBHIP_OK;
+  }
+  uint32_t flag = 0;
   HIPCHK(hipMemcpyAsync(&flag, h->d_check_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (flag & 2) return ZBHIP_EINVAL;
   if (!(flag & 1)) return ZBHIP_OK;
+  return replan_device_window(h, dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, replanned);
+}
+
+// the window copied to the host and submitted as a host window (planned into rounds in log order)
+static int replan_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
+                                size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts, bool* replanned) {
   std::vector<zbhip_command> c(n);
   std::vector<zbhip_doc_entry> d(n_docs);
   std::vector<zbhip_xpart_cmd> x(n_xparts);
@@ -1847,6 +1902,7 @@ int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_
                            size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts) {
   if (!h || (n && !dev_cmds)) return ZBHIP_EINVAL;
   if (n > h->rec_slots) return ZBHIP_ENOMEM;
+  if (int rc0 = resolve_guard(h)) return rc0;  // the last window's speculative check
   if (h->upload_ev) HIPCHK(hipEventSynchronize(h->upload_ev));  // (h_order is rewritten by the planning)
   if (int rc0 = settle(h)) return rc0;
   bool replanned = false;
@@ -2206,6 +2262,7 @@ static int fold_journals(zbhip_handle* h, size_t keep = 0) {
 // adapter can hand a fallback instance over (its earlier commands' keys are fixed) and declare the
 // keys the CPU engine generated before the keys of the window's later commands are fixed.
 static int advance(zbhip_handle* h, size_t limit, bool force) {
+  if (int rc = resolve_guard(h)) return rc;
   if (int rc = fold_journals(h)) return rc;
   if (!h->results || h->fin_next >= h->n_cmds) return ZBHIP_OK;
   ensure_ext(h);
@@ -2312,6 +2369,31 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   if (!h) return ZBHIP_EINVAL;
   if (h->ran) return ZBHIP_ESTATE;
   if (h->procs.empty()) return ZBHIP_ESTATE;
+  const uint32_t* guard = nullptr;
+  if (h->guard_armed) {
+    h->guard_armed = false;
+    if (flags & ZBHIP_RUN_NO_RESULTS) {
+      // speculative: k_step runs guarded by the check's flag; resolve_guard reads it later
+      guard = h->d_check_flag;
+      h->guard_win.run_flags = flags;
+      h->guard_pending = true;
+    } else {
+      // results are read back in this call anyway: decide now
+      HIPCHK(hipEventSynchronize(h->check_ev));
+      const uint32_t flag = *h->h_check_flag;
+      if (flag) {
+        const auto w = h->guard_win;
+        h->next_doc_base = w.doc_base;
+        h->next_source = w.source_base;
+        if (flag & 2) {
+          h->n_cmds = 0;
+          return ZBHIP_EINVAL;
+        }
+        bool replanned = false;
+        if (int rc = replan_device_window(h, w.cmds, w.n, w.docs, w.n_docs, w.xparts, w.n_xparts, &replanned)) return rc;
+      }
+    }
+  }
   if (h->ring_filled != h->windows_run) h->ring_ok = false;  // the previous window's keys are not in the ring
   ++h->windows_run;
   const bool timed = flags & ZBHIP_RUN_TIMED;
@@ -2356,6 +2438,7 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.map_val = h->d_map_val;
   P.map_cap = h->cfg.max_commands;
   P.cmd_act = h->st.act ? h->d_cmd_act : nullptr;
+  P.guard = guard;
   h->run_clock_ms = h->clock_ms;
   if (!h->streams.empty() || !h->run_streams.empty()) h->run_streams = h->streams;  // (the pushes' deadlines / workers)
   P.tpl = (h->variant == 0 || h->variant == 1 || h->scope_variant()) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
@@ -2650,6 +2733,7 @@ int64_t zbhip_pending_records(zbhip_handle* h) {
 int zbhip_get_stats(zbhip_handle* h, zbhip_stats* out) {
   if (getenv("ZBHIP_STAMPS")) dump_stamps();
   if (!h || !out) return ZBHIP_EINVAL;
+  if (int rc = resolve_guard(h)) return rc;
   if (h->stats_dirty) {
     unsigned long long rows[64 * 8];
     HIPCHK(hipMemcpyAsync(rows, h->d_stats, sizeof rows, hipMemcpyDeviceToHost, h->stream));

@@ -289,6 +289,8 @@ struct StepParams {
   uint32_t map_cap;
   uint4* cmd_act;             // [n_cmds] the ACTIVATED job a batch completed or canceled: its DevState.act
                               // entry (x bit 31 clear: none found)
+  const uint32_t* guard;      // an untrusted device window's subject-check flag (k_subject_check): nonzero
+                              // -> the launch does nothing (the host replans the window); null: no guard
 };
 constexpr int kMapVals = 2;   // io-mapped VARIABLE records per batch (more: FB_VARS)
 
