@@ -355,8 +355,10 @@ enum zbhip_command_kind {
 };
 
 /* STR values are string ids of the partition's value dictionary (zbhip_intern_string). */
+/* ZBHIP_DOC_LIST: a list of scalar items (a msgpack array), value = its id in the handle's list
+ * dictionary (zbhip_intern_list) -- a multi-instance inputCollection variable, an outputCollection */
 enum zbhip_doc_type { ZBHIP_DOC_NIL = 0, ZBHIP_DOC_BOOL = 1, ZBHIP_DOC_INT = 2, ZBHIP_DOC_DEC = 3,
-                      ZBHIP_DOC_OTHER = 4, ZBHIP_DOC_STR = 5 };
+                      ZBHIP_DOC_OTHER = 4, ZBHIP_DOC_STR = 5, ZBHIP_DOC_LIST = 6 };
 
 /* One entry of a variable document (a msgpack map entry on the reference side).
  * DEC values are value * 10^ZBHIP_DEC_SCALE (exact decimal). */

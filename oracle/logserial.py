@@ -238,14 +238,24 @@ EVENT_TYPE = {0: "UNSPECIFIED", 1: "CONDITIONAL", 2: "ERROR", 3: "ESCALATION", 4
               7: "SIGNAL", 8: "TERMINATE", 9: "TIMER"}
 
 # ---- documents (variables) -------------------------------------------------------------------------
-DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR = 0, 1, 2, 3, 4, 5
+DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR, DOC_LIST = 0, 1, 2, 3, 4, 5, 6
 
 
-def value_bytes(entry, string_value):
+def value_bytes(entry, string_value, list_items=None):
     """msgpack of one document value in the canonical encoding a client writes (compact ints,
-    float64 for decimals -- exact value v / 10^6 --, shortest str header)."""
+    float64 for decimals -- exact value v / 10^6 --, shortest str header); a list (`list_items(id)` ->
+    [(type, value)]): an array header and its items (MultiInstanceOutputCollectionBehavior.java:43-55,
+    writeArrayHeader + the items' own msgpack)."""
     w = MsgPackWriter()
     t, v = entry["type"], int(entry["value"])
+    if t == DOC_LIST:
+        if list_items is None:
+            raise ValueError("a list value without the list dictionary")
+        items = list_items(v)
+        w.array_header(len(items))
+        for it, iv in items:
+            w.b += value_bytes({"type": it, "value": iv}, string_value)
+        return bytes(w.b)
     if t == DOC_NIL:
         w.nil()
     elif t == DOC_BOOL:
@@ -261,14 +271,14 @@ def value_bytes(entry, string_value):
     return bytes(w.b)
 
 
-def document_bytes(entries, name, string_value):
+def document_bytes(entries, name, string_value, list_items=None):
     if len(entries) == 0:
         return EMPTY_DOCUMENT  # DocumentValue.wrap: empty / nil document -> EMPTY_DOCUMENT
     w = MsgPackWriter()
     w.map_header(len(entries))
     for e in entries:
         w.string(name(int(e["name_id"])))
-        w.b += value_bytes(e, string_value)
+        w.b += value_bytes(e, string_value, list_items)
     return bytes(w.b)
 
 
@@ -325,8 +335,9 @@ class Tables:
     {bpmn_process_id, version, key, elements: [(type, event_type, id, job_type, retries)]},
     name(id) for variable names, string_value(id) for STR values."""
 
-    def __init__(self, processes, name, string_value):
+    def __init__(self, processes, name, string_value, list_items=None):
         self.processes, self.name, self.string_value = processes, name, string_value
+        self.list_items = list_items  # list-dictionary id -> [(type, value)] (LIST values)
 
 
 def _message_value(r, vt, tables, timestamp):
@@ -358,7 +369,8 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0, timer_value=
         return _message_value(r, vt, tables, timestamp)
     p = tables.processes[int(r["process_idx"])] if int(r["process_idx"]) >= 0 else None
     el = p["elements"][int(r["element_idx"])] if p is not None and int(r["element_idx"]) >= 0 else None
-    src_doc = document_bytes(docs_of_source(int(r["source_index"])), tables.name, tables.string_value)
+    src_doc = document_bytes(docs_of_source(int(r["source_index"])), tables.name, tables.string_value,
+                             getattr(tables, "list_items", None))
     if vt == VT_PI:
         fields = dict(bpmnElementType=ELEMENT_TYPE[el[0]], elementId=el[2], bpmnProcessId=p["bpmn_process_id"],
                       version=p["version"], processDefinitionKey=p["key"],
@@ -385,7 +397,8 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0, timer_value=
         else:
             e = doc_entry(int(r["aux"]))
         return write_object(VARIABLE, dict(name=tables.name(int(r["element_idx"])),
-                                           value=value_bytes(e, tables.string_value), scopeKey=int(r["scope_key"]),
+                                           value=value_bytes(e, tables.string_value, getattr(tables, "list_items", None)),
+                                           scopeKey=int(r["scope_key"]),
                                            processInstanceKey=int(r["process_instance_key"]),
                                            processDefinitionKey=p["key"], bpmnProcessId=p["bpmn_process_id"]))
     if vt == VT_PE:

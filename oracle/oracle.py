@@ -89,6 +89,10 @@ def lib():
                                     C.c_size_t]
         L.zbo_intern_string.restype = C.c_int64
         L.zbo_intern_string.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        L.zbo_intern_list.restype = C.c_int64
+        L.zbo_intern_list.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.zbo_list_items.restype = C.c_size_t
+        L.zbo_list_items.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t]
         L.zbo_outbox.restype = C.c_size_t
         L.zbo_outbox.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.zbo_clear_outbox.argtypes = [C.c_void_p]
@@ -191,6 +195,18 @@ class Oracle:
     def intern_string(self, value):
         b = value.encode() if isinstance(value, str) else value
         return self.L.zbo_intern_string(self.h, b, len(b))
+
+    def intern_list(self, items):
+        """A list value [(zbhip_doc_type, value)] into the list dictionary: its id."""
+        d = abi_docs(items)
+        return self.L.zbo_intern_list(self.h, d.ctypes.data, len(items))
+
+    def list_items(self, list_id):
+        """The items [(zbhip_doc_type, value)] of list `list_id`."""
+        n = self.L.zbo_list_items(self.h, list_id, None, 0)
+        out = abi.make_docs(max(n, 1))
+        self.L.zbo_list_items(self.h, list_id, out.ctypes.data, n)
+        return [(int(x["type"]), int(x["value"])) for x in out[:n]]
 
     def outbox(self, clear=True):
         n = self.L.zbo_outbox(self.h, None, 0)
@@ -333,3 +349,12 @@ def bench_msg(xml, partitions, n_instances):
     if sec < 0:
         raise OracleError("bench deploy failed")
     return sec, t.value, c.value
+
+
+def abi_docs(items):
+    """[(zbhip_doc_type, value)] as zbhip_doc_entry rows (the list dictionary's item form; one spare row
+    for an empty list, so the buffer is never null)."""
+    d = abi.make_docs(max(len(items), 1))
+    for j, (t, v) in enumerate(items):
+        d[j]["type"], d[j]["value"] = t, v
+    return d

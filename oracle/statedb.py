@@ -130,9 +130,14 @@ def encode_rows(rows, processes, string_value):
             out.append((CF[name], prefix + dblong(int(parts[1])) + dblong(int(parts[2])), NIL))
         elif name == "VARIABLES":
             f = fields(parts[3])
-            entry = {"type": int(f["type"]), "value": int(f["value"])}
-            val = LS.write_object(VARIABLE_INSTANCE, {"key": int(f["key"]),
-                                                      "value": LS.value_bytes(entry, string_value)})
+            if int(f["type"]) == LS.DOC_LIST:  # a list: its items in the row ("type:value;...")
+                items = [tuple(int(x) for x in it.split(":")) for it in f["value"].split(";") if it]
+                entry = {"type": LS.DOC_LIST, "value": 0}
+                vb = LS.value_bytes(entry, string_value, lambda _: items)
+            else:
+                entry = {"type": int(f["type"]), "value": int(f["value"])}
+                vb = LS.value_bytes(entry, string_value)
+            val = LS.write_object(VARIABLE_INSTANCE, {"key": int(f["key"]), "value": vb})
             out.append((CF[name], prefix + dblong(int(parts[1])) + dbstr(parts[2]), val))
         elif name == "EVENT_SCOPE":
             f = fields(parts[2])

@@ -350,6 +350,12 @@ struct OEl {
   std::vector<std::string> mi_item_text;
   std::string mi_input;
   int mi_input_id = -1, mi_loop_id = -1;
+  // inputCollection `= name` (a list variable, evaluateArrayExpression), outputCollection with its
+  // outputElement `= name`, and a completionCondition (a FEEL boolean of the subset)
+  std::string mi_coll_name, mi_out_coll, mi_out_elem;
+  int mi_coll_id = -1, mi_out_coll_id = -1, mi_out_elem_id = -1;
+  std::unique_ptr<FExpr> mi_cond;
+  std::string mi_cond_text;
   // zeebe:ioMapping (VariableMappingTransformer, deployment/model/transformer/VariableMappingTransformer.java:
   // 73-200) in the subset: at most one input and one output mapping, a plain target name, a source that
   // is a variable reference (`= x`), a literal (`= 5`, `= true`, `= null`, `= "s"`) or a static string
@@ -508,29 +514,60 @@ static TimerValue timer_value(const std::string& text, bool cycle) {
   return v;
 }
 
+// `= name`: a FEEL variable reference (no path, no call) -> name, else ""
+static std::string feel_variable(const std::string& t) {
+  size_t i = t.find_first_not_of(" \t\r\n");
+  if (i == std::string::npos || t[i] != '=') return "";
+  ++i;
+  while (i < t.size() && isspace((unsigned char)t[i])) ++i;
+  const size_t s0 = i;
+  if (i >= t.size() || !(isalpha((unsigned char)t[i]) || t[i] == '_')) return "";
+  while (i < t.size() && (isalnum((unsigned char)t[i]) || t[i] == '_')) ++i;
+  const std::string v = t.substr(s0, i - s0);
+  while (i < t.size() && isspace((unsigned char)t[i])) ++i;
+  if (i != t.size() || v == "true" || v == "false" || v == "null" || v == "not") return "";
+  return v;
+}
+
 // MultiInstanceActivityTransformer.transformLoopCharacteristics
 // (deployment/model/transformer/MultiInstanceActivityTransformer.java:80-122) for the subset: the
 // inputCollection a static FEEL list literal (`= [10, 20, 30]`, `= ["a", "b"]`: integer, string,
-// boolean and null items -- FeelToMessagePackTransformer writes a whole number as a msgpack integer),
-// an optional inputElement; a completionCondition, outputCollection or outputElement is outside it.
+// boolean and null items -- FeelToMessagePackTransformer writes a whole number as a msgpack integer)
+// or a list variable (`= items`), an optional inputElement, an outputCollection with an outputElement
+// that names a variable (`= result`), and a completionCondition of the FEEL subset (`= x`, `= item = 20`,
+// comparisons over numberOfInstances / numberOfActiveInstances / numberOfCompletedInstances /
+// numberOfTerminatedInstances and variables).
 static bool parse_multi_instance(const XNode& mil, OEl& body, std::string& err) {
   body.mi_seq = mil.attr("isSequential") == "true";
   const XNode* cc = mil.child("completionCondition");
   if (cc && cc->text.find_first_not_of(" \t\r\n") != std::string::npos) {
-    err = "multi-instance completionCondition outside the supported subset";
-    return false;
+    const size_t a = cc->text.find_first_not_of(" \t\r\n");
+    if (cc->text[a] != '=') { err = "static (non-FEEL) completionCondition outside the subset"; return false; }
+    FeelParser fp(cc->text.substr(a + 1));
+    body.mi_cond = fp.parse_or();
+    fp.ws();
+    if (!fp.ok || fp.i != fp.s.size()) { err = "completionCondition outside the FEEL subset: " + cc->text; return false; }
+    const size_t b = cc->text.find_first_not_of(" \t\r\n", a + 1);
+    body.mi_cond_text = b == std::string::npos ? "" : cc->text.substr(b);
   }
   const XNode* ext = mil.child("extensionElements");
   const XNode* lc = ext ? ext->child("loopCharacteristics") : nullptr;
   if (!lc) { err = "multi-instance without zeebe:loopCharacteristics"; return false; }
-  if (!lc->attr("outputCollection").empty() || !lc->attr("outputElement").empty()) {
-    err = "multi-instance outputCollection / outputElement outside the supported subset";
-    return false;
+  const std::string oc = lc->attr("outputCollection"), oe = lc->attr("outputElement");
+  if (!oc.empty() || !oe.empty()) {
+    body.mi_out_elem = feel_variable(oe);
+    if (oc.empty() || body.mi_out_elem.empty()) {
+      err = "multi-instance outputCollection / outputElement outside the supported subset (a variable)";
+      return false;
+    }
+    body.mi_out_coll = oc;
   }
   body.mi_input = lc->attr("inputElement");
   std::string t = lc->attr("inputCollection");
+  body.mi_coll_name = feel_variable(t);
+  if (!body.mi_coll_name.empty()) return true;
   size_t i = t.find_first_not_of(" \t\r\n");
-  auto bad = [&err, &t]() { err = "multi-instance inputCollection outside the supported subset (a static list): " + t; return false; };
+  auto bad = [&err, &t]() { err = "multi-instance inputCollection outside the supported subset (a static list or a variable): " + t; return false; };
   if (i == std::string::npos || t[i] != '=') return bad();
   auto ws = [&]() { while (i < t.size() && isspace((unsigned char)t[i])) ++i; };
   ++i;
@@ -937,7 +974,7 @@ struct ElementInstance {  // state/instance/ElementInstance.java:23-54
   int state = 0;
   PiValue value;
   int activeSequenceFlows = 0;
-  int childActivated = 0, childCompleted = 0, loopCounter = 0;  // multi-instance (ElementInstance.java:25-33)
+  int childActivated = 0, childCompleted = 0, childTerminated = 0, loopCounter = 0;  // multi-instance (ElementInstance.java:25-33)
 };
 
 struct Doc {  // a variable document (msgpack map) as a list of entries
@@ -1119,6 +1156,40 @@ class Oracle {
     return id;
   }
 
+  // the list dictionary (ZBHIP_DOC_LIST values: a list of scalar items, each (zbhip_doc_type, value))
+  using Items = std::vector<std::pair<uint8_t, int64_t>>;
+  std::vector<Items> lists;
+  std::map<Items, int> list_ids;
+  int64_t intern_list(const Items& items) {
+    auto it = list_ids.find(items);
+    if (it != list_ids.end()) return it->second;
+    const int id = (int)lists.size();
+    lists.push_back(items);
+    list_ids.emplace(items, id);
+    return id;
+  }
+  static std::string list_text(const Items& items) {
+    std::string o;
+    for (size_t i = 0; i < items.size(); ++i) {
+      if (i) o += ';';
+      o += std::to_string((int)items[i].first) + ":" + std::to_string((long long)items[i].second);
+    }
+    return o;
+  }
+  static Items parse_list_text(const std::string& t) {
+    Items items;
+    size_t a = 0;
+    while (a < t.size()) {
+      size_t b = t.find(';', a);
+      if (b == std::string::npos) b = t.size();
+      const std::string it = t.substr(a, b - a);
+      const size_t c = it.find(':');
+      items.push_back({(uint8_t)std::stoi(it.substr(0, c)), (int64_t)std::stoll(it.substr(c + 1))});
+      a = b + 1;
+    }
+    return items;
+  }
+
   int intern(const std::string& n) {
     auto it = name_ids.find(n);
     if (it != name_ids.end()) return it->second;
@@ -1183,6 +1254,14 @@ class Oracle {
       e.mi_loop_id = intern("loopCounter");
       for (size_t j = 0; j < e.mi_items.size(); ++j)
         if (e.mi_items[j].first == ZBHIP_DOC_STR) e.mi_items[j].second = intern_string(e.mi_item_text[j]);
+      // then the collection variable, the outputCollection and outputElement names, the completion
+      // condition's variables
+      if (!e.mi_coll_name.empty()) e.mi_coll_id = intern(e.mi_coll_name);
+      if (!e.mi_out_coll.empty()) {
+        e.mi_out_coll_id = intern(e.mi_out_coll);
+        e.mi_out_elem_id = intern(e.mi_out_elem);
+      }
+      intern_vars(e.mi_cond.get());
     }
     // io mappings, in element order: the input's source variable and target, then the output's (the
     // product's zbhip_deploy interns in this order); string literals into the value dictionary
@@ -1352,7 +1431,8 @@ class Oracle {
                                                           r.intent == ZBHIP_JOB_FAIL)) ||
                        (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT) ||
-                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && r.intent == ZBHIP_PIB_ACTIVATE) || msg;
+                       (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH &&
+                        (r.intent == ZBHIP_PIB_ACTIVATE || r.intent == ZBHIP_PIB_TERMINATE)) || msg;
     if (!known) { last_error = "process_one: command outside the restated subset"; return ZBHIP_EUNSUPP; }
     if (msg) {
       // the command's record value as the log holds it (MessageRecord / MessageSubscriptionRecord /
@@ -1434,11 +1514,18 @@ class Oracle {
       return m;
     };
     auto L = [](const std::string& v) { return (int64_t)std::stoll(v); };
-    auto find_proc = [this](int64_t def_key, const std::string& elem_id, int& proc, int& elem) {
+    // (by id and, where given, element type -- -2: a job worker: a multi-instance body and its inner
+    // activity share the id)
+    auto find_proc = [this](int64_t def_key, const std::string& elem_id, int& proc, int& elem, int type = -1) {
       for (size_t p = 0; p < procs.size(); ++p) {
         if (procs[p].def_key != def_key) continue;
         for (size_t e = 0; e < procs[p].els.size(); ++e)
-          if (procs[p].els[e].id == elem_id) { proc = (int)p; elem = (int)e; return true; }
+          if (procs[p].els[e].id == elem_id &&
+              (type == -1 || procs[p].els[e].type == type || (type == -2 && ZBHIP_IS_JOB_WORKER(procs[p].els[e].type)))) {
+            proc = (int)p;
+            elem = (int)e;
+            return true;
+          }
       }
       return false;
     };
@@ -1467,10 +1554,11 @@ class Oracle {
             ei.childActivated = (int)L(f.at("childActivatedCount"));
             ei.childCompleted = (int)L(f.at("childCompletedCount"));
             ei.loopCounter = (int)L(f.at("multiInstanceLoopCounter"));
-            if (L(f.at("childTerminatedCount")) != 0) throw Unsupported{"terminated children"};
+            ei.childTerminated = (int)L(f.at("childTerminatedCount"));
             ei.value.flowScopeKey = L(f.at("flowScopeKey"));
             ei.value.piKey = L(f.at("processInstanceKey"));
-            if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), ei.value.proc, ei.value.elem))
+            if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), ei.value.proc, ei.value.elem,
+                           (int)L(f.at("bpmnElementType"))))
               throw Unsupported{"element " + f.at("elementId")};
             ei_[ei.key] = ei;
           } else if (cf == "ELEMENT_INSTANCE_PARENT_CHILD") {
@@ -1491,7 +1579,9 @@ class Oracle {
             pi_by_def_.insert({L(r.at(1)), L(r.at(2))});
           } else if (cf == "VARIABLES") {
             auto f = fields(r.at(3));
-            vars_[{L(r.at(1)), intern(r.at(2))}] = VarRow{L(f.at("key")), (uint8_t)L(f.at("type")), L(f.at("value")), 0};
+            const uint8_t type = (uint8_t)L(f.at("type"));
+            const int64_t value = type == ZBHIP_DOC_LIST ? intern_list(parse_list_text(f.at("value"))) : L(f.at("value"));
+            vars_[{L(r.at(1)), intern(r.at(2))}] = VarRow{L(f.at("key")), type, value, 0};
           } else if (cf == "EVENT_SCOPE") {
             auto f = fields(r.at(2));
             const int64_t k = L(r.at(1));
@@ -1513,7 +1603,7 @@ class Oracle {
           } else if (cf == "JOBS") {
             auto f = fields(r.at(2));
             JobRow j;
-            if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), j.pi.proc, j.pi.elem))
+            if (!find_proc(L(f.at("processDefinitionKey")), f.at("elementId"), j.pi.proc, j.pi.elem, -2))
               throw Unsupported{"job element " + f.at("elementId")};
             j.pi.piKey = L(f.at("processInstanceKey"));
             j.elementInstanceKey = L(f.at("elementInstanceKey"));
@@ -1873,6 +1963,8 @@ class Oracle {
       trigger_timer(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE)
       bpmn_process_record(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && cmd.r.intent == ZBHIP_PIB_TERMINATE)
+      terminate_batch(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH && cmd.r.intent == ZBHIP_PIB_ACTIVATE)
       activate_batch(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_MESSAGE && cmd.r.intent == ZBHIP_MSG_PUBLISH)
@@ -2601,12 +2693,82 @@ class Oracle {
 
   // MultiInstanceBodyProcessor.onChildActivating (:129-158) -> setLoopVariables (:270-305): the item at
   // loopCounter - 1 as the inputElement (if any), then loopCounter, local to the inner instance
+  // (the outputElement variable, nil-initialized unless it is the inputElement or loopCounter, between them)
   void on_child_activating(const OEl& body, int64_t key, const PiValue& v) {
     const int loop = ei_.at(key).loopCounter;
-    if (loop < 1 || loop > (int)body.mi_items.size()) throw Unsupported{"loop counter past the input collection (incident)"};
-    const auto& item = body.mi_items[loop - 1];
+    const Items items = input_collection(body, key);
+    if (loop < 1 || loop > (int)items.size()) throw Unsupported{"loop counter past the input collection (incident)"};
+    const auto& item = items[loop - 1];
     if (body.mi_input_id >= 0) set_local_inline(key, v.proc, v.piKey, body.mi_input_id, item.first, item.second);
+    if (body.mi_out_elem_id >= 0 && body.mi_out_elem != body.mi_input && body.mi_out_elem != "loopCounter")
+      set_local_inline(key, v.proc, v.piKey, body.mi_out_elem_id, ZBHIP_DOC_NIL, 0);
     set_local_inline(key, v.proc, v.piKey, body.mi_loop_id, ZBHIP_DOC_INT, loop);
+  }
+
+  // readInputCollectionVariable (MultiInstanceBodyProcessor.java:362-367 -> evaluateArrayExpression):
+  // the static list, or the list variable seen from `scope` (anything else is an EXTRACT_VALUE_ERROR
+  // incident: outside the subset)
+  Items input_collection(const OEl& b, int64_t scope) {
+    if (b.mi_coll_id < 0) return b.mi_items;
+    const VarRow* vr = lookup_var(scope, b.mi_coll_id);
+    if (!vr || vr->type != ZBHIP_DOC_LIST) throw Unsupported{"input collection is not a list (incident)"};
+    return lists.at((size_t)vr->value);
+  }
+
+  // MultiInstanceBodyProcessor.beforeExecutionPathCompleted (:160-191) of the inner instance `child`:
+  // updateOutputCollection (MultiInstanceOutputCollectionBehavior.java:57-141: the outputElement's value
+  // at loopCounter - 1 of the body's local collection, setLocalVariable), then the completion condition
+  // (satisfiesCompletionCondition :380-394, the numberOf* variables from the body first), then for a
+  // sequential body the input collection read again.  Returns whether the condition is satisfied.
+  bool mi_before_completed(const OEl& b, ElementInstance& body, int64_t child) {
+    if (b.mi_out_coll_id >= 0) {
+      const int loop = ei_.at(child).loopCounter;
+      const VarRow* ev = lookup_var(child, b.mi_out_elem_id);
+      if (!ev) throw Unsupported{"output element variable missing (null: unpinned)"};
+      if (ev->type == ZBHIP_DOC_LIST) throw Unsupported{"a list as output element"};
+      const uint8_t et = ev->type;
+      const int64_t evv = ev->value;
+      auto cit = vars_.find({body.key, b.mi_out_coll_id});
+      if (cit == vars_.end() || cit->second.type != ZBHIP_DOC_LIST) throw Unsupported{"output collection not a list (incident)"};
+      Items items = lists.at((size_t)cit->second.value);
+      if (loop < 1 || loop > (int)items.size()) throw Unsupported{"output collection too small (incident)"};
+      items[loop - 1] = {et, evv};
+      set_local_inline(body.key, body.value.proc, body.value.piKey, b.mi_out_coll_id, ZBHIP_DOC_LIST, intern_list(items));
+    }
+    bool sat = false;
+    if (b.mi_cond) {
+      cond_body_ = &body;
+      FVal r;
+      try {
+        r = eval(b.mi_cond.get(), child);
+      } catch (...) {
+        cond_body_ = nullptr;
+        throw;
+      }
+      cond_body_ = nullptr;
+      if (r.k != V_BOOL) throw Unsupported{"completion condition not a boolean (incident)"};
+      sat = r.b;
+    }
+    if (b.mi_seq) (void)input_collection(b, body.key);
+    return sat;
+  }
+  const ElementInstance* cond_body_ = nullptr;  // the body whose completion condition is evaluated
+
+  // TerminateProcessInstanceBatchProcessor.processRecord (processing/processinstance/
+  // TerminateProcessInstanceBatchProcessor.java:38-85): TERMINATE_ELEMENT of every child of the body
+  // that can terminate (ACTIVATING / ACTIVATED / COMPLETING), in ELEMENT_INSTANCE_PARENT_CHILD order
+  void terminate_batch(ORecord& cmd) {
+    const int64_t body = cmd.r.scope_key;
+    if (cmd.r.partition != -1) throw Unsupported{"a continued termination batch"};
+    std::vector<int64_t> kids;
+    for (auto it = parent_child_.lower_bound({body, INT64_MIN}); it != parent_child_.end() && it->first == body; ++it)
+      kids.push_back(it->second);
+    for (int64_t c : kids) {
+      const ElementInstance& ci = ei_.at(c);
+      if (ci.state == ZBHIP_PI_ELEMENT_ACTIVATING || ci.state == ZBHIP_PI_ELEMENT_ACTIVATED ||
+          ci.state == ZBHIP_PI_ELEMENT_COMPLETING)
+        pi_command(c, ZBHIP_PI_TERMINATE_ELEMENT, ci.value);
+    }
   }
 
   // VariableBehavior.setLocalVariable (VariableBehavior.java:191-200) of a value the engine computed
@@ -2838,8 +3000,12 @@ class Oracle {
         // ACTIVATED, then an empty collection completes the body, a sequential body activates its
         // first inner instance (activateChildInstanceWithKey, BpmnStateTransitionBehavior.java:292-307),
         // a parallel one writes PROCESS_INSTANCE_BATCH:ACTIVATE (activateChildInstancesInBatches :315-324)
+        const Items items = input_collection(el, key);
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
-        if (el.mi_items.empty()) {
+        if (el.mi_out_coll_id >= 0)  // initializeOutputCollection (:43-55): [nil] * size, local to the body
+          set_local_inline(key, v.proc, v.piKey, el.mi_out_coll_id, ZBHIP_DOC_LIST,
+                           intern_list(Items(items.size(), {(uint8_t)ZBHIP_DOC_NIL, 0})));
+        if (items.empty()) {
           pi_command(key, ZBHIP_PI_COMPLETE_ELEMENT, v);
           break;
         }
@@ -2855,7 +3021,7 @@ class Oracle {
           rec.r.element_idx = v.elem;
           rec.r.scope_key = key;  // batchElementInstanceKey
           rec.r.process_instance_key = v.piKey;
-          rec.r.partition = (int32_t)el.mi_items.size();  // index: the children to activate
+          rec.r.partition = (int32_t)items.size();  // index: the children to activate
           rec.pi = v;
         }
         break;
@@ -2966,8 +3132,17 @@ class Oracle {
         complete_and_take(el, key, v, false);
         break;
       case ZBHIP_EL_MULTI_INSTANCE_BODY:
-        // MultiInstanceBodyProcessor.onComplete (:100-114): unsubscribeFromEvents (none), no output
-        // collection to propagate, transitionToCompleted, takeOutgoingSequenceFlows
+        // MultiInstanceBodyProcessor.onComplete (:100-114): unsubscribeFromEvents (none), the output
+        // collection propagated (BpmnStateBehavior.propagateVariable :163-178: the variable seen from the
+        // body merged into its flow scope), transitionToCompleted, takeOutgoingSequenceFlows
+        if (el.mi_out_coll_id >= 0) {
+          const VarRow* vr = lookup_var(key, el.mi_out_coll_id);
+          if (vr) {
+            const uint8_t t = vr->type;
+            const int64_t val = vr->value;
+            merge_document_value(v.flowScopeKey, v.proc, v.piKey, el.mi_out_coll_id, t, val);
+          }
+        }
         complete_and_take(el, key, v, false);
         break;
       case ZBHIP_EL_INTERMEDIATE_CATCH_EVENT: {
@@ -3010,6 +3185,17 @@ class Oracle {
     auto tit = triggers_.lower_bound({key, INT64_MIN});
     const bool found = tit != triggers_.end() && tit->first.first == key && tit->second.elem != v.elem;
     auto fit = ei_.find(v.flowScopeKey);
+    if (!found && fit != ei_.end() && E(fit->second.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      // no event trigger: transitionToTerminated, onElementTerminated -> MultiInstanceBodyProcessor
+      // .onChildTerminated (:232-247): a body that is not terminating completes once no child is active
+      // (its completion condition was met)
+      pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
+      const ElementInstance& body = ei_.at(v.flowScopeKey);
+      if (body.state == ZBHIP_PI_ELEMENT_TERMINATING) throw Unsupported{"terminating multi-instance body"};
+      if ((int64_t)body.childCount + body.activeSequenceFlows == 0)
+        pi_command(body.key, ZBHIP_PI_COMPLETE_ELEMENT, body.value);
+      return;
+    }
     if (!found || fit == ei_.end() || fit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED)
       throw Unsupported{"termination without an event trigger (onElementTerminated)"};
     const int64_t eventKey = tit->first.second;
@@ -3069,17 +3255,39 @@ class Oracle {
   // BpmnStateTransitionBehavior.transitionToCompleted (:158-191) and afterExecutionPathCompleted (:404-417)
   void transition_to_completed(const OEl& el, int64_t key, const PiValue& v) {
     bool end_of_path = el.type != ZBHIP_EL_PROCESS && el.out.empty();
+    // beforeExecutionPathCompleted (BpmnStateTransitionBehavior.java:158-191): the container's check
+    // before the COMPLETED record (a multi-instance body: output collection, completion condition)
+    bool satisfies = false;
+    if (end_of_path) {
+      auto bit = ei_.find(v.flowScopeKey);
+      if (bit != ei_.end() && E(bit->second.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY)
+        satisfies = mi_before_completed(E(bit->second.value), bit->second, key);
+    }
     pi_event(key, ZBHIP_PI_ELEMENT_COMPLETED, v);
     if (end_of_path) {
       // ProcessProcessor.afterExecutionPathCompleted (:130-140) -> BpmnStateBehavior.canBeCompleted (behavior/BpmnStateBehavior.java:76-95)
       auto fit = ei_.find(v.flowScopeKey);
       if (fit != ei_.end() && E(fit->second.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
-        // MultiInstanceBodyProcessor.beforeExecutionPathCompleted (:160-191): no output collection, no
-        // completion condition (false); afterExecutionPathCompleted (:193-230): a sequential body
-        // creates its next inner instance while items are left, else completes once no child is active
+        // MultiInstanceBodyProcessor.afterExecutionPathCompleted (:193-230): a satisfied completion
+        // condition terminates the remaining children (terminateChildInstances, BpmnStateTransitionBehavior
+        // .java:348-363: PROCESS_INSTANCE_BATCH:TERMINATE) and completes the body once none is active (a
+        // sequential body at once); else a sequential body creates its next inner instance while items
+        // are left, and the body completes once no child is active
         const ElementInstance& body = fit->second;
         const OEl& b = E(body.value);
-        if (b.mi_seq && body.loopCounter < (int)b.mi_items.size()) {
+        if (satisfies) {
+          const bool none = body.childCount == 0;
+          if (!none) {
+            ORecord& rec = append(ZBHIP_RT_COMMAND, ZBHIP_VT_PROCESS_INSTANCE_BATCH, ZBHIP_PIB_TERMINATE, next_key());
+            rec.r.process_idx = body.value.proc;
+            rec.r.element_idx = body.value.elem;
+            rec.r.scope_key = body.key;  // batchElementInstanceKey
+            rec.r.process_instance_key = body.value.piKey;
+            rec.r.partition = -1;  // index: from the first child
+            rec.pi = body.value;
+          }
+          if (none || b.mi_seq) pi_command(body.key, ZBHIP_PI_COMPLETE_ELEMENT, body.value);
+        } else if (b.mi_seq && body.loopCounter < (int)input_collection(b, body.key).size()) {
           PiValue c = body.value;
           c.flowScopeKey = body.key;
           c.elem = b.inner;
@@ -3184,6 +3392,18 @@ class Oracle {
       case FExpr::BOOL: r.k = V_BOOL; r.b = e->b; return r;
       case FExpr::NUL: r.k = V_NULL; return r;
       case FExpr::VAR: {
+        if (cond_body_) {  // the completion condition's primary context (MultiInstanceBodyProcessor :396-460)
+          const ElementInstance& b = *cond_body_;
+          const std::string& n = e->var;
+          int64_t x = 0;
+          bool hit = true;
+          if (n == "numberOfInstances") x = b.childActivated;
+          else if (n == "numberOfActiveInstances") x = b.childCount - 1;
+          else if (n == "numberOfCompletedInstances") x = b.childCompleted + 1;
+          else if (n == "numberOfTerminatedInstances") x = b.childTerminated;
+          else hit = false;
+          if (hit) { r.k = V_NUM; r.n = (__int128)x * kScale18; return r; }
+        }
         auto it = name_ids.find(e->var);
         const VarRow* vr = it == name_ids.end() ? nullptr : lookup_var(scope, it->second);
         if (!vr || vr->type == ZBHIP_DOC_NIL) { r.k = V_NULL; return r; }
@@ -3329,9 +3549,9 @@ class Oracle {
         if (parent > 0) {
           ElementInstance& pe = ei_.at(parent);
           pe.childCount -= 1;
-          if (E(pe.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {  // manageMultiInstance (Completed :104-110)
-            if (intent == ZBHIP_PI_ELEMENT_TERMINATED) throw Unsupported{"terminated multi-instance child"};
-            pe.childCompleted += 1;
+          if (E(pe.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {  // manageMultiInstance (Completed :104-110,
+            if (intent == ZBHIP_PI_ELEMENT_TERMINATED) pe.childTerminated += 1;  // Terminated :53-58)
+            else pe.childCompleted += 1;
           }
         }
         break;
@@ -3359,11 +3579,11 @@ std::string Oracle::dump_state() const {
     const OEl& el = procs[e.value.proc].els[e.value.elem];
     snprintf(buf, sizeof buf,
              "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%d,childActivatedCount=%d,childCompletedCount=%d,"
-             "childTerminatedCount=0,jobKey=%lld,multiInstanceLoopCounter=%d,interruptingElementId=,"
+             "childTerminatedCount=%d,jobKey=%lld,multiInstanceLoopCounter=%d,interruptingElementId=,"
              "calledChildInstanceKey=-1,state=%d,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
              "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%d",
              (long long)k, (long long)e.parentKey, e.childCount, e.childActivated, e.childCompleted,
-             (long long)e.jobKey, e.loopCounter, e.state, el.id.c_str(), el.type,
+             e.childTerminated, (long long)e.jobKey, e.loopCounter, e.state, el.id.c_str(), el.type,
              el.event, (long long)e.value.flowScopeKey, (long long)e.value.piKey,
              (long long)procs[e.value.proc].def_key, e.activeSequenceFlows);
     rows.push_back(buf);
@@ -3392,6 +3612,12 @@ std::string Oracle::dump_state() const {
     rows.push_back(buf);
   }
   for (auto& [k, vr] : vars_) {
+    if (vr.type == ZBHIP_DOC_LIST) {  // a list: its items (type:value, ';'-separated)
+      snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%d,value=", (long long)k.first, names[k.second].c_str(),
+               (long long)vr.key, vr.type);
+      rows.push_back(std::string(buf) + list_text(lists.at((size_t)vr.value)));
+      continue;
+    }
     snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%d,value=%lld", (long long)k.first,
              names[k.second].c_str(), (long long)vr.key, vr.type, (long long)vr.value);
     rows.push_back(buf);
@@ -3582,6 +3808,23 @@ int zbo_submit_ex(void* o, const zbhip_command* cmds, size_t n, const zbhip_doc_
 }
 int64_t zbo_intern_string(void* o, const char* b, size_t len) {
   return static_cast<Oracle*>(o)->intern_string(std::string(b, len));
+}
+// the list dictionary (ZBHIP_DOC_LIST values): items as zbhip_doc_entry rows (type, value; name unused)
+int64_t zbo_intern_list(void* o, const zbhip_doc_entry* items, size_t n) {
+  Oracle::Items v;
+  for (size_t i = 0; i < n; ++i) v.push_back({items[i].type, items[i].value});
+  return static_cast<Oracle*>(o)->intern_list(v);
+}
+size_t zbo_list_items(void* o, int64_t id, zbhip_doc_entry* out, size_t cap) {
+  auto* O = static_cast<Oracle*>(o);
+  if (id < 0 || (size_t)id >= O->lists.size()) return 0;
+  const auto& v = O->lists[(size_t)id];
+  for (size_t i = 0; i < v.size() && i < cap; ++i) {
+    memset(&out[i], 0, sizeof out[i]);
+    out[i].type = v[i].first;
+    out[i].value = v[i].second;
+  }
+  return v.size();
 }
 size_t zbo_outbox(void* o, zbhip_xpart_cmd* out, size_t cap) {
   auto* O = static_cast<Oracle*>(o);

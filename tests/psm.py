@@ -516,6 +516,7 @@ class OracleEngine:
         idx = self.o.deploy(xml, key, version)
         self.tables = oracle_tables(self.o)
         self.values = RecordValues(self.tables, self.o.name, lambda i: self.o.string_value(i).decode(),
+                                   list_items=self.o.list_items,
                                    streams=self.streams)
         return idx
 
@@ -618,7 +619,7 @@ class OracleEngine:
                 slot = self.slot_of.setdefault(v["processInstanceKey"], 0xFFFFF0 - len(self.slot_of))
             else:
                 slot = 0xFFFFFF  # (the correlation slot: only the oracle's key bookkeeping uses it)
-        docs = doc_entries(variables, self.o.intern, self.o.intern_string)
+        docs = doc_entries(variables, self.o.intern, self.o.intern_string, self.o.intern_list)
         base = len(self.doc_values)
         self.doc_values.extend(val for _, val in variables)
         self.o.clear_records()

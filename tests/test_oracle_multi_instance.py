@@ -3,9 +3,9 @@ reference's MultiInstanceActivityTest (engine/src/test/java/io/camunda/zeebe/eng
 multiinstance/MultiInstanceActivityTest.java), both parameterisations (parallel, sequential).
 
 The reference test's process reads its inputCollection from a variable (`items`) and collects an
-output collection; the device subset takes a static list literal (`= [10, 20, 30]`: the same items)
-and no outputCollection, so the pins below are the lifecycle, job, loop-variable and skip assertions,
-which neither difference touches.  completeJobs (:1579-1613) activates one job at a time
+output collection: tests/test_oracle_mi_collections.py pins that form; the tests below drive the static
+list literal (`= [10, 20, 30]`: the same items) through the lifecycle, job, loop-variable and skip
+assertions.  completeJobs (:1579-1613) activates one job at a time
 (JOB_BATCH:ACTIVATE, maxJobsToActivate 1) and completes it with a `result` variable."""
 import numpy as np
 import pytest
@@ -220,21 +220,23 @@ def test_strings_and_limits():
 
 
 @pytest.mark.parametrize("bad", [
-    '= items', '= [1.5]', '= [x]', '= [1] + [2]', '= [1, 2', '= ["a\\\\b"]'])
+    '= items.nested', '= [1.5]', '= [x]', '= [1] + [2]', '= [1, 2', '= ["a\\\\b"]'])
 def test_refused_input_collections(bad):
     o = Oracle()
     with pytest.raises(OracleError, match="inputCollection"):
         o.deploy(bpmn.multi_instance_process(bad))
 
 
-def test_refused_output_collection_and_condition():
+@pytest.mark.parametrize("extra,match", [
+    (dict(outputCollection="results"), "outputCollection"),                           # no outputElement
+    (dict(outputCollection="results", outputElement="= result.nested"), "outputCollection"),  # a path
+    (dict(completionCondition="x"), "completionCondition"),                          # static text
+    (dict(completionCondition="= count(items) > 1"), "completionCondition")])        # a function call
+def test_refused_output_collection_and_condition(extra, match):
+    # (outputCollection / outputElement / completionCondition themselves: test_oracle_mi_collections.py)
     b = bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "t")
-    b.multiInstance("= [1]", "item", outputCollection="results", outputElement="= result")
-    with pytest.raises(OracleError, match="outputCollection"):
-        Oracle().deploy(b.endEvent().done())
-    b = bpmn.createExecutableProcess("process").startEvent().serviceTask("task", "t")
-    b.multiInstance("= [1]", "item", completionCondition="= x")
-    with pytest.raises(OracleError, match="completionCondition"):
+    b.multiInstance("= [1]", "item", **extra)
+    with pytest.raises(OracleError, match=match):
         Oracle().deploy(b.endEvent().done())
 
 

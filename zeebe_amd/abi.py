@@ -38,16 +38,18 @@ PI_INTENTS = {
 }
 PI_INTENT_IDS = {v: k for k, v in PI_INTENTS.items()}
 PI_SEQUENCE_FLOW_TAKEN, PI_ELEMENT_ACTIVATING, PI_ELEMENT_ACTIVATED = 1, 2, 3
+PI_ELEMENT_COMPLETING, PI_ELEMENT_COMPLETED, PI_ELEMENT_TERMINATED = 4, 5, 7
 JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED", 3: "TIME_OUT", 4: "TIMED_OUT", 5: "FAIL", 6: "FAILED",
                10: "CANCELED"}
 JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED, JOB_CANCELED = 0, 1, 2, 10
 JOB_TIME_OUT, JOB_TIMED_OUT, JOB_FAIL, JOB_FAILED = 3, 4, 5, 6
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}
+VAR_CREATED, VAR_UPDATED = 0, 1
 PE_INTENTS = {0: "TRIGGERING", 1: "TRIGGERED"}
 PIC_INTENTS = {0: "CREATE", 1: "CREATED"}
 TIMER_INTENTS = {0: "CREATED", 1: "TRIGGER", 2: "TRIGGERED", 3: "CANCEL", 4: "CANCELED"}
 PIB_INTENTS = {0: "TERMINATE", 1: "ACTIVATE"}
-PIB_ACTIVATE = 1
+PIB_TERMINATE, PIB_ACTIVATE = 0, 1
 AUX_INLINE = -2  # VARIABLE record with its value inline (message_key, doc type in partition)
 TIMER_CREATED, TIMER_TRIGGER, TIMER_TRIGGERED, TIMER_CANCELED = 0, 1, 2, 4
 PE_TRIGGERING, PE_TRIGGERED = 0, 1
@@ -96,7 +98,7 @@ XPART_KINDS = (CMD_MSG_SUB_CREATE, CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_MSG_SU
                CMD_PMS_DELETE)
 SLOT_KINDS = (CMD_PUBLISH, CMD_MSG_SUB_CREATE, CMD_MSG_SUB_CORRELATE, CMD_MSG_SUB_DELETE)
 PMS_KINDS = (CMD_PMS_CREATE, CMD_PMS_CORRELATE, CMD_PMS_DELETE)
-DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR = 0, 1, 2, 3, 4, 5
+DOC_NIL, DOC_BOOL, DOC_INT, DOC_DEC, DOC_OTHER, DOC_STR, DOC_LIST = 0, 1, 2, 3, 4, 5, 6
 NO_STRING = 0xFFFFFFFF
 DEC_SCALE = 6
 

@@ -104,32 +104,48 @@ PI_COMMAND_INTENTS = (8, 9, 10)  # ACTIVATE_ELEMENT, COMPLETE_ELEMENT, TERMINATE
 TENANT = "<default>"  # TenantOwned.DEFAULT_TENANT_IDENTIFIER
 
 
-def doc_entries(variables, intern_name, intern_string):
+def scalar_entry(v, intern_string):
+    """A scalar client value as (zbhip_doc_type, value), or None outside the subset (maps, nested
+    arrays, inexact decimals)."""
+    if v is None:
+        return abi.DOC_NIL, 0
+    if isinstance(v, bool):
+        return abi.DOC_BOOL, int(v)
+    if isinstance(v, int):
+        return abi.DOC_INT, v
+    if isinstance(v, float):
+        scaled = round(v * 10 ** abi.DEC_SCALE)
+        return (abi.DOC_DEC, scaled) if scaled / 10 ** abi.DEC_SCALE == v else None
+    if isinstance(v, str):
+        return abi.DOC_STR, intern_string(v)
+    return None
+
+
+def doc_entries(variables, intern_name, intern_string, intern_list=None):
     """A client's variable document [(name, value)] as zbhip_doc_entry rows, or None when a value is
-    outside the device subset (Window.decodeDocument: arrays, maps, inexact decimals)."""
+    outside the device subset (Window.decodeDocument: maps, nested arrays, inexact decimals; arrays
+    of scalars only where the side has a list dictionary, `intern_list`)."""
     d = abi.make_docs(len(variables))
     for j, (name, v) in enumerate(variables):
         d[j]["name_id"] = intern_name(name)
-        if v is None:
-            d[j]["type"] = abi.DOC_NIL
-        elif isinstance(v, bool):
-            d[j]["type"], d[j]["value"] = abi.DOC_BOOL, int(v)
-        elif isinstance(v, int):
-            d[j]["type"], d[j]["value"] = abi.DOC_INT, v
-        elif isinstance(v, float):
-            scaled = round(v * 10 ** abi.DEC_SCALE)
-            if scaled / 10 ** abi.DEC_SCALE != v:
+        if isinstance(v, (list, tuple)):
+            items = [scalar_entry(x, intern_string) for x in v]
+            if intern_list is None or any(x is None for x in items):
                 return None
-            d[j]["type"], d[j]["value"] = abi.DOC_DEC, scaled
-        elif isinstance(v, str):
-            d[j]["type"], d[j]["value"] = abi.DOC_STR, intern_string(v)
-        else:
+            d[j]["type"], d[j]["value"] = abi.DOC_LIST, intern_list(items)
+            continue
+        e = scalar_entry(v, intern_string)
+        if e is None:
             return None
+        d[j]["type"], d[j]["value"] = e
     return d
 
 
-def typed_value(t, v, string_value):
-    """A stored variable (zbhip_doc_type, value) as the client's value."""
+def typed_value(t, v, string_value, list_items=None):
+    """A stored variable (zbhip_doc_type, value) as the client's value (a list: a tuple of its items,
+    `list_items(id)` -> [(type, value)])."""
+    if t == abi.DOC_LIST and list_items is not None:
+        return tuple(typed_value(it, iv, string_value) for it, iv in list_items(int(v)))
     return (None if t == abi.DOC_NIL else bool(v) if t == abi.DOC_BOOL else int(v) if t == abi.DOC_INT
             else int(v) / 10 ** abi.DEC_SCALE if t == abi.DOC_DEC else string_value(int(v)) if t == abi.DOC_STR
             else ("other", int(v)))
@@ -148,10 +164,11 @@ class RecordValues:
     """zbhip_record rows -> the reference's record values (Window.value).  `procs` are the
     deployment's ProcessDefinitions (by process index), `name` the variable-name dictionary."""
 
-    def __init__(self, procs, name, string_value=None, incident_message=None, streams=None):
+    def __init__(self, procs, name, string_value=None, incident_message=None, streams=None, list_items=None):
         self.procs = procs
         self.name = name
         self.string_value = string_value  # value-dictionary id -> str (inline STR values)
+        self.list_items = list_items  # list-dictionary id -> [(type, value)] (inline LIST values)
         self.incident_message = incident_message  # a gateway incident's errorMessage (zbhip_incident_message)
         self.streams = streams if streams is not None else {}  # job streams: type -> (worker, timeout)
 
@@ -202,7 +219,7 @@ class RecordValues:
                     "jobKey": aux if job else -1, "variableScopeKey": scope, "tenantId": TENANT}
         if vt == abi.VT_VARIABLE:
             # ZBHIP_AUX_INLINE: a value the engine computed (multi-instance loop variables)
-            val = typed_value(int(r["partition"]), int(r["message_key"]), self.string_value) \
+            val = typed_value(int(r["partition"]), int(r["message_key"]), self.string_value, self.list_items) \
                 if aux == abi.AUX_INLINE else entry_value(aux)
             return {"name": self.name(elem), "value": val, "scopeKey": scope, "processInstanceKey": pik,
                     "processDefinitionKey": p.definition_key, "bpmnProcessId": p.bpmn_process_id, "tenantId": TENANT}
@@ -254,7 +271,8 @@ class RecordValues:
                         "elementInstanceKey": int(j["element_instance_key"]),
                         "processInstanceKey": int(j["process_instance_key"]), "bpmnProcessId": p.bpmn_process_id,
                         "processDefinitionKey": p.definition_key, "processDefinitionVersion": p.version,
-                        "variables": tuple((name(int(x["name_id"])), typed_value(int(x["type"]), x["value"], string_value))
+                        "variables": tuple((name(int(x["name_id"])),
+                                            typed_value(int(x["type"]), x["value"], string_value, self.list_items))
                                            for x in j["variables"][:int(j["n_variables"])]),
                         "tenantId": TENANT})
         v.update({"jobKeys": tuple(int(j["key"]) for j in jobs), "jobs": tuple(out), "truncated": False})
@@ -265,7 +283,8 @@ class RecordValues:
         JOB_BATCH:ACTIVATED record's job with the variables JobVariablesCollector gathered (`row`: a
         zbhip_job_variables / zbo_job_variables row)."""
         j = dict(push_value["jobs"][0])
-        j["variables"] = tuple((name(int(x["name_id"])), typed_value(int(x["type"]), x["value"], string_value))
+        j["variables"] = tuple((name(int(x["name_id"])),
+                                typed_value(int(x["type"]), x["value"], string_value, self.list_items))
                                for x in row["variables"][:int(row["n_variables"])])
         return j
 
