@@ -191,9 +191,11 @@ typedef struct zbhip_element {
                           * (attachedToRef, ExecutableActivity.attach); else ZBHIP_NONE16 */
   uint16_t flow_target;  /* sequence flow: target node; else ZBHIP_NONE16 */
   uint16_t condition;    /* sequence flow: condition index; ZBHIP_NONE16 = no condition;
-                          * multi-instance body: the index of its static inputCollection (ZBHIP_OP_ITEM
-                          * instructions, one per item, then ZBHIP_OP_END) */
-  uint16_t default_flow; /* exclusive gateway: default flow element; else ZBHIP_NONE16 */
+                          * multi-instance body: the index of its inputCollection (ZBHIP_OP_ITEM
+                          * instructions, one per item, or ZBHIP_OP_COLLECTION; then ZBHIP_OP_OUTPUT,
+                          * then ZBHIP_OP_END) */
+  uint16_t default_flow; /* exclusive gateway: default flow element; multi-instance body: the condition
+                          * index of its completionCondition; else ZBHIP_NONE16 */
   uint16_t job_type;     /* service task: string-table index of the job type */
   uint16_t job_retries;  /* service task: static retries; boundary event: bit 0 interrupting (cancelActivity),
                           * bits 8..15 the timer's repetitions (1 a duration, n of "Rn/", 255 "R/" infinite);
@@ -225,9 +227,16 @@ enum zbhip_op {
   ZBHIP_OP_LT = 5, ZBHIP_OP_LE = 6, ZBHIP_OP_GT = 7, ZBHIP_OP_GE = 8,
   ZBHIP_OP_EQ = 9, ZBHIP_OP_NE = 10,
   ZBHIP_OP_AND = 11, ZBHIP_OP_OR = 12, ZBHIP_OP_NOT = 13,
-  ZBHIP_OP_ITEM = 14       /* an inputCollection item: arg = its zbhip_doc_type -- INT, BOOL, NIL or STR;
-                            * literal = the value (STR: string-table index; zbhip_deploy interns it
-                            * into the value dictionary) */
+  /* an inputCollection item: arg = its zbhip_doc_type -- INT, BOOL, NIL or STR; literal = the value (STR:
+   * string-table index; zbhip_deploy interns it into the value dictionary) */
+  ZBHIP_OP_ITEM = 14,
+  /* a multi-instance body's inputCollection `= name`: arg = the list variable's string-table index (a
+   * ZBHIP_DOC_LIST value; anything else is an incident, outside the device subset) */
+  ZBHIP_OP_COLLECTION = 15,
+  /* its outputCollection: arg = the collection's string-table index, literal = the outputElement
+   * variable's (`= name`); a completionCondition is a condition of its own, its index in the body's
+   * default_flow */
+  ZBHIP_OP_OUTPUT = 16
 };
 #define ZBHIP_DEC_SCALE 6   /* fixed decimal scale of NUMBER values on the device */
 
@@ -428,6 +437,12 @@ int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_
  * the string, interning it if new, or an error.  The device holds each string's Java hashCode
  * (SubscriptionUtil.getSubscriptionHashCode, signed bytes) for subscription routing. */
 int64_t zbhip_intern_string(zbhip_handle* h, const char* bytes, size_t len);
+/* The list dictionary (ZBHIP_DOC_LIST values: arrays of scalar items -- a multi-instance inputCollection
+ * variable, an outputCollection): the id of the list `items` (type, value; name unused; STR values are
+ * value-dictionary ids), deduplicated; ZBHIP_EUNSUPP for nested lists.  zbhip_list_items: its items
+ * (*n_out = the count, at most cap written). */
+int64_t zbhip_intern_list(zbhip_handle* h, const zbhip_doc_entry* items, size_t n);
+int zbhip_list_items(zbhip_handle* h, int64_t id, zbhip_doc_entry* out, size_t cap, size_t* n_out);
 /* Bulk form: n strings, string i = bytes[offsets[i] .. offsets[i+1]); ids_out may be NULL. */
 int zbhip_intern_strings(zbhip_handle* h, const char* bytes, const uint64_t* offsets, size_t n, uint32_t* ids_out);
 const char* zbhip_string_value(zbhip_handle* h, uint32_t id, size_t* len);
@@ -637,6 +652,9 @@ void zbhip_serializer_free(zbhip_serializer* s);
 int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, uint32_t* process_idx_out);
 int zbhip_serializer_intern(zbhip_serializer* s, const char* name);
 int64_t zbhip_serializer_intern_string(zbhip_serializer* s, const char* bytes, size_t len);
+/* the list dictionary (ZBHIP_DOC_LIST values), in the handle's id order: items as zbhip_doc_entry rows
+ * (type, value; name unused) */
+int64_t zbhip_serializer_intern_list(zbhip_serializer* s, const zbhip_doc_entry* items, size_t n);
 /* RecordMetadata.brokerVersion written into every entry (default 8.4.0, the reference build). */
 int zbhip_serializer_set_broker_version(zbhip_serializer* s, int32_t major, int32_t minor, int32_t patch);
 int zbhip_serializer_rejection_reason(zbhip_serializer* s, const zbhip_record* rec, char* buf, size_t cap);
@@ -754,6 +772,12 @@ typedef struct zbhip_job_batch {
 
 int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* cmd, zbhip_activated_job* jobs, size_t cap,
                         zbhip_job_batch* result);
+/* The device's JOB_ACTIVATABLE keys of a job type in key order (DbJobState.forEachActivatableJobs,
+ * state/instance/DbJobState.java:231-252, over the device's jobs): at most cap into keys, *n_out the
+ * count.  A host whose engine holds jobs of the same type (handed-off instances) merges both lists and
+ * activates each side's share -- the engine's first (its nextKey is the batch key), then
+ * zbhip_activate_jobs with the device's, which takes the same key. */
+int zbhip_activatable_jobs(zbhip_handle* h, const char* type, size_t type_len, int64_t* keys, size_t cap, size_t* n_out);
 /* The push side effect of a job stream (BpmnJobActivationBehavior.java:83-97: JobVariablesCollector over
  * the stream's fetchVariables, then JobStream.push of the ActivatedJob): for each of the n job keys (the
  * aux of the JOB_BATCH:ACTIVATED records a run or zbhip_time_out_job / zbhip_fail_job wrote), its

@@ -1618,6 +1618,11 @@ class Oracle {
               j.error_message = unhex(f.at("errorMessageHex"));
               j.retry_backoff = L(f.at("retryBackoff"));
               j.recurring_time = L(f.at("recurringTime"));
+            } else if (j.retries != procs[j.pi.proc].els[j.pi.elem].retries) {
+              // a failure that left errorMessage, retryBackoff and recurringTime at their defaults (a state
+              // read back from zb-db rows, where they do not show): its retries alone
+              j.fail_fields = true;
+              j.recurring_time = -1;
             }
             jobs_[L(r.at(1))] = j;
           } else if (cf == "JOB_STATES") {

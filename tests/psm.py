@@ -436,6 +436,8 @@ class EngineJobState:
                         "processDefinitionVersion": int(f["processDefinitionVersion"]),
                         "processDefinitionKey": int(f["processDefinitionKey"]), "deadline": int(f["deadline"]),
                         "worker": f["worker"]}))
+                    if "errorMessageHex" in f:  # a failed job's stored errorMessage
+                        out[-1][2]["errorMessage"] = bytes.fromhex(f["errorMessageHex"]).decode()
         return sorted(out, key=lambda t: t[:2])
 
     def for_each_timed_out_entry(self, now, callback):
@@ -549,6 +551,11 @@ class OracleEngine:
 
     def state(self):
         return self.o.state()
+
+    def activatable_jobs(self, job_type):
+        """JobState.forEachActivatableJobs of `job_type`: the JOB_ACTIVATABLE [[type, jobKey], tenant] keys."""
+        return sorted(int(r.rsplit("|", 1)[1]) for r in self.o.state()
+                      if r.startswith("JOB_ACTIVATABLE|") and r.split("|")[1] == job_type)
 
     def accepts(self, vt):
         return vt in self.ACCEPTS

@@ -101,8 +101,12 @@ def check(ref, gpu):
         if got != want:
             n = min(len(got), len(want))
             bad = next((i for i in range(n) if got[i] != want[i]), n)
-            raise AssertionError("partition %d log entry %d of %d/%d:\n got  %s\n want %s" % (
-                p, bad, len(got), len(want), got[bad] if bad < len(got) else None, want[bad] if bad < len(want) else None))
+            ctx = "".join("\n  %d got  %s\n  %d want %s" % (i, got[i] if i < len(got) else None, i,
+                                                          want[i] if i < len(want) else None)
+                          for i in range(max(0, bad - 3), bad))
+            raise AssertionError("partition %d log entry %d of %d/%d:\n got  %s\n want %s\n before:%s" % (
+                p, bad, len(got), len(want), got[bad] if bad < len(got) else None, want[bad] if bad < len(want) else None,
+                ctx))
         assert b.state() == a.state(), p
 
 

@@ -43,6 +43,9 @@ Platform objects used (duck-typed like the Java interfaces):
   zeebe_db-- RawDbWriter: upsert(rows) of a hand-off (the zb-db rows of the instance)
   key_generator -- DbKeyGenerator: current_key(), set_key_if_higher(key)
 """
+import copy
+import types
+
 from . import abi
 from .engine import Partition
 
@@ -194,8 +197,9 @@ class RecordValues:
                 cid = int(r["correlation_key"])
                 v.update({"deadline": int(r["message_key"]),
                           "worker": self.string_value(cid) if cid != abi.NO_STRING else ""})
-            if int(r["record_type"]) == abi.RT_EVENT and int(r["reason_arg"]) & 1:
-                # a failed job's stored retries and errorMessage (JobFailProcessor.failJob)
+            if int(r["record_type"]) in (abi.RT_EVENT, abi.RT_COMMAND) and int(r["reason_arg"]) & 1:
+                # a failed job's stored retries and errorMessage (JobFailProcessor.failJob), in its events
+                # and in the TIME_OUT command JobTimeoutTrigger writes from the stored record
                 eid = int(r["message_name"]) | int(r["bpmn_process_id"]) << 16
                 v.update({"retries": int(r["partition"]),
                           "errorMessage": self.string_value(eid) if eid != abi.NO_STRING else ""})
@@ -431,6 +435,24 @@ class Window:
         return cmds, docs
 
 
+class _Scratch:
+    """A result builder for one side's share of a merged command (the records are combined afterwards)."""
+
+    def __init__(self):
+        self.entries, self.post_commit = [], []
+
+    def append_record(self, key, record_type, value_type, intent, rejection_type, rejection_reason, value):
+        self.entries.append(types.SimpleNamespace(key=key, record_type=record_type, value_type=value_type, intent=intent,
+                                                  rejection_type=rejection_type, rejection_reason=rejection_reason,
+                                                  value=value))
+
+    def append_post_commit_task(self, task):
+        self.post_commit.append(task)
+
+    def build(self):
+        return self
+
+
 class GpuBatchProcessor:
     """The adapter (GpuBatchProcessor.java).  `deployments`: [(bpmn xml, definition key, version)]
     in deployment order; processes the device compiler refuses stay with the engine, as do
@@ -468,6 +490,7 @@ class GpuBatchProcessor:
         self.part = None
         self.by_key, self.latest_by_id, self.by_index = {}, {}, []
         self.engine_job_types = set()  # job types the engine's processes (or handed-off instances) hold
+        self.device_job_types = set()  # job types of the device's processes
         from .bpmn import job_types_of
         for xml, _, _ in engine_deployments:
             self.engine_job_types.update(job_types_of(xml))
@@ -506,7 +529,8 @@ class GpuBatchProcessor:
                               initial_key=self.key_generator.current_key() - pbits, defer_continuations=True)
         for xml, key, version in self.deployments:
             self.deploy(xml, key, version)
-        self.values = RecordValues(self.part.processes, self.part.name, self.part.string_value, self.part.incident_message)
+        self.values = RecordValues(self.part.processes, self.part.name, self.part.string_value, self.part.incident_message,
+                                   list_items=self.part.list_items)
 
     def deploy(self, xml, key, version):
         from .native import ZbhipError
@@ -519,7 +543,8 @@ class GpuBatchProcessor:
             self.by_index.append(None)
             return None
         p = self.part.processes[idx]
-        from .bpmn import message_names_of
+        from .bpmn import job_types_of, message_names_of
+        self.device_job_types.update(job_types_of(xml))
         self.message_names.update(message_names_of(xml))
         self.by_key[key] = p
         self.by_index.append(p)
@@ -571,9 +596,11 @@ class GpuBatchProcessor:
         self._batch_done()
         self.followups = 0
         self.engine_batch = False
-        if record.value_type == VT_JOB_BATCH and record.intent == JOB_BATCH_ACTIVATE \
-                and record.value["type"] not in self.engine_job_types:
-            return self._activate_jobs(record, out)
+        if record.value_type == VT_JOB_BATCH and record.intent == JOB_BATCH_ACTIVATE:
+            if record.value["type"] not in self.engine_job_types:
+                return self._activate_jobs(record, out)
+            if record.value["type"] in self.device_job_types:
+                return self._activate_jobs_merged(record, out)
         if record.value_type == abi.VT_JOB and record.intent == abi.JOB_TIME_OUT and self._resolve(record.key) is not None:
             return self._time_out_job(record, out)
         if record.value_type == abi.VT_JOB and record.intent == abi.JOB_FAIL and self._resolve(record.key) is not None:
@@ -744,7 +771,7 @@ class GpuBatchProcessor:
             vt = rec.value_type
             if vt == abi.VT_PROCESS_INSTANCE_CREATION:
                 v = rec.value
-                docs = doc_entries(v.get("variables", ()), self.part.intern, self.part.intern_string)
+                docs = doc_entries(v.get("variables", ()), self.part.intern, self.part.intern_string, self.part.intern_list)
                 if docs is None:
                     break  # a document outside the subset: the engine takes this CREATE
                 slot = self._take_slot()
@@ -753,7 +780,8 @@ class GpuBatchProcessor:
                 self.window.put(rec, slot, abi.CMD_CREATE, self._create_target(v).idx, docs,
                                 [val for _, val in v.get("variables", ())])
             elif vt == abi.VT_JOB:
-                docs = doc_entries(rec.value.get("variables", ()), self.part.intern, self.part.intern_string)
+                docs = doc_entries(rec.value.get("variables", ()), self.part.intern, self.part.intern_string,
+                                   self.part.intern_list)
                 if docs is None:
                     break
                 inst, ordv = self._resolve(rec.key)
@@ -1046,6 +1074,49 @@ class GpuBatchProcessor:
                           self.part.string_value)
 
     # ---- job activation (JobBatchActivateProcessor.java:60-143) ------------------------------------
+    def _activate_jobs_merged(self, record, out):
+        """JOB_BATCH:ACTIVATE of a job type both the engine and the device hold jobs of (handed-off instances,
+        engine-only processes of a device type): JobBatchCollector.collectJobs (:67-123) walks
+        JOB_ACTIVATABLE [type, jobKey] in key order over both.  The first maxJobsToActivate keys of the two
+        lists (the engine's JobState.forEachActivatableJobs, zbhip_activatable_jobs) split into each side's
+        share; the engine activates its share first (its nextKey is the batch key), the device its own with
+        the same key (its key counter is one behind), and the one JOB_BATCH:ACTIVATED record lists both in
+        key order."""
+        v = record.value
+        mx = v["maxJobsToActivate"]
+        if mx < 1 or v["timeout"] < 1 or not v["type"]:
+            return self.engine.process(record, out)  # the rejection
+        self.part.set_key_if_higher(self.key_generator.current_key())
+        dev = self.part.activatable_jobs(v["type"], mx)
+        if not dev:
+            return self.engine.process(record, out)
+        eng = self.engine.activatable_jobs(v["type"])
+        picked = sorted(dev + eng[:mx])[:mx]
+        ndev = len(set(picked) & set(dev))
+        if ndev == len(picked):
+            return self._activate_jobs(record, out)
+        self.counts["activations"] += 1
+        share = _Scratch()
+        cmd = copy.copy(record)
+        cmd.value = dict(v, maxJobsToActivate=len(picked) - ndev)
+        self.engine.process(cmd, share)
+        ev = share.entries[-1]
+        key, jobs, _ = self.part.activate_jobs(v["type"], v["worker"], v["timeout"], ndev, v.get("timestamp", 0))
+        if key != ev.key:
+            raise RuntimeError("merged activation: batch keys %d / %d" % (ev.key, key))
+        value = dict(ev.value)
+        mine = self.values.job_batch(v, key, jobs, self.part.name, self.part.string_value)
+        both = sorted(zip(value["jobKeys"] + mine["jobKeys"], value["jobs"] + mine["jobs"]), key=lambda t: t[0])
+        value["jobKeys"] = tuple(k for k, _ in both) if isinstance(value["jobKeys"], tuple) else [k for k, _ in both]
+        value["jobs"] = tuple(j for _, j in both) if isinstance(value["jobs"], tuple) else [j for _, j in both]
+        value["maxJobsToActivate"] = mx
+        value["truncated"] = bool(value.get("truncated")) or bool(mine.get("truncated"))
+        self.key_generator.set_key_if_higher(key)
+        out.append_record(key, abi.RT_EVENT, VT_JOB_BATCH, JOB_BATCH_ACTIVATED, abi.REJ_NONE, "", value)
+        for task in share.post_commit:
+            out.append_post_commit_task(task)
+        return out.build()
+
     def _activate_jobs(self, record, out):
         v = record.value
         self.part.set_key_if_higher(self.key_generator.current_key())

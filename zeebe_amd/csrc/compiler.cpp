@@ -467,34 +467,68 @@ static int64_t timer_ms(const std::string& text, bool cycle, uint32_t& reps) {
   return duration_ms(r.substr(slash + 1));
 }
 
+// `= name`: a FEEL variable reference (no path, no call, no literal) -> name, else ""
+static std::string feel_variable(const std::string& t) {
+  size_t i = t.find_first_not_of(" \t\r\n");
+  if (i == std::string::npos || t[i] != '=') return "";
+  ++i;
+  while (i < t.size() && isspace((unsigned char)t[i])) ++i;
+  const size_t s0 = i;
+  if (i >= t.size() || !(isalpha((unsigned char)t[i]) || t[i] == '_')) return "";
+  while (i < t.size() && (isalnum((unsigned char)t[i]) || t[i] == '_')) ++i;
+  const std::string v = t.substr(s0, i - s0);
+  while (i < t.size() && isspace((unsigned char)t[i])) ++i;
+  if (i != t.size() || v == "true" || v == "false" || v == "null" || v == "not") return "";
+  return v;
+}
+
 // A multi-instance activity's loop characteristics (MultiInstanceActivityTransformer
 // .transformLoopCharacteristics, deployment/model/transformer/MultiInstanceActivityTransformer.java:
 // 80-122) in the subset: the inputCollection a static FEEL list literal of integer, string, boolean and
-// null items (FeelToMessagePackTransformer writes a whole number as a msgpack integer), an optional
-// inputElement; a completionCondition, outputCollection or outputElement is outside it.
+// null items (FeelToMessagePackTransformer writes a whole number as a msgpack integer) or a list
+// variable (`= items`: coll_var), an optional inputElement, an outputCollection with an outputElement
+// naming a variable (`= result`), and a completionCondition of the FEEL subset (its text after '=').
 struct MiItem { uint8_t type; int64_t value; std::string text; };
-static bool parse_loop(const Elem& mil, bool& seq, std::string& input, std::vector<MiItem>& items, std::string& err) {
+struct MiLoop {
+  bool seq = false;
+  std::string input, coll_var, out_coll, out_elem, cond;
+  std::vector<MiItem> items;
+};
+static bool parse_loop(const Elem& mil, MiLoop& L, std::string& err) {
   const std::string* sq = mil.get("isSequential");
-  seq = sq && *sq == "true";
-  if (const Elem* cc = mil.first("completionCondition"))
-    if (cc->text.find_first_not_of(" \t\r\n") != std::string::npos) {
-      err = "multi-instance completionCondition outside the supported subset";
-      return false;
+  L.seq = sq && *sq == "true";
+  bool& seq = L.seq;
+  (void)seq;
+  std::string& input = L.input;
+  std::vector<MiItem>& items = L.items;
+  if (const Elem* cc = mil.first("completionCondition")) {
+    const size_t a = cc->text.find_first_not_of(" \t\r\n");
+    if (a != std::string::npos) {
+      const size_t b = cc->text.find_last_not_of(" \t\r\n");
+      if (cc->text[a] != '=') { err = "static (non-FEEL) completionCondition outside the subset"; return false; }
+      L.cond = cc->text.substr(a + 1, b - a);
     }
+  }
   const Elem* ext = mil.first("extensionElements");
   const Elem* lc = ext ? ext->first("loopCharacteristics") : nullptr;
   if (!lc) { err = "multi-instance without zeebe:loopCharacteristics"; return false; }
   const std::string* oc = lc->get("outputCollection");
   const std::string* oe = lc->get("outputElement");
   if ((oc && !oc->empty()) || (oe && !oe->empty())) {
-    err = "multi-instance outputCollection / outputElement outside the supported subset";
-    return false;
+    L.out_elem = oe ? feel_variable(*oe) : "";
+    if (!oc || oc->empty() || L.out_elem.empty()) {
+      err = "multi-instance outputCollection / outputElement outside the supported subset (a variable)";
+      return false;
+    }
+    L.out_coll = *oc;
   }
   const std::string* ie = lc->get("inputElement");
   input = ie ? *ie : "";
   const std::string* ic = lc->get("inputCollection");
   const std::string t = ic ? *ic : "";
-  auto bad = [&]() { err = "multi-instance inputCollection outside the supported subset (a static list): " + t; return false; };
+  L.coll_var = feel_variable(t);
+  if (!L.coll_var.empty()) return true;
+  auto bad = [&]() { err = "multi-instance inputCollection outside the supported subset (a static list or a variable): " + t; return false; };
   size_t i = t.find_first_not_of(" \t\r\n");
   auto ws = [&]() { while (i < t.size() && isspace((unsigned char)t[i])) ++i; };
   if (i == std::string::npos || t[i] != '=') return bad();
@@ -677,7 +711,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
   std::vector<std::vector<uint16_t>> out_lists, in_lists;
   std::vector<const Elem*> xgws;
   std::vector<std::pair<uint16_t, std::string>> boundaries;  // (boundary event, attachedToRef)
-  std::vector<std::pair<uint16_t, std::vector<MiItem>>> collections;  // (multi-instance body, its items)
+  std::vector<std::pair<uint16_t, MiLoop>> collections;  // (multi-instance body, its loop characteristics)
 
   // Elements in document pre-order: an embedded sub-process, then its children, then its next
   // sibling (the oracle numbers them the same way).  Every sequence flow connects two nodes of one
@@ -868,19 +902,17 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           err = "io mappings of a multi-instance activity outside the supported subset";
           return ZBHIP_EUNSUPP;
         }
-        bool seq = false;
-        std::string input;
-        std::vector<MiItem> items;
-        if (!parse_loop(*mil, seq, input, items, err)) return ZBHIP_EUNSUPP;
+        MiLoop loop;
+        if (!parse_loop(*mil, loop, err)) return ZBHIP_EUNSUPP;
         zbhip_element b = blank(ZBHIP_EL_MULTI_INSTANCE_BODY, e.id);
         b.flow_scope = scope;
-        b.job_retries = seq ? 1 : 0;
-        b.message_name = input.empty() ? ZBHIP_NONE16 : C.str(input);
+        b.job_retries = loop.seq ? 1 : 0;
+        b.message_name = loop.input.empty() ? ZBHIP_NONE16 : C.str(loop.input);
         const uint16_t bi = (uint16_t)C.elements.size();
         b.start_event = (uint16_t)(bi + 1);
         index[*id] = bi;
         C.elements.push_back(b);
-        collections.push_back({bi, std::move(items)});
+        collections.push_back({bi, std::move(loop)});
         e.flow_scope = bi;
         C.elements.push_back(e);
         continue;
@@ -961,14 +993,30 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     out_lists[fe.flow_source].push_back(fi);
     in_lists[fe.flow_target].push_back(fi);
   }
-  // the bodies' inputCollections after the flows' conditions (condition indices of flows unchanged)
-  for (auto& [b, items] : collections) {
+  // the bodies' inputCollections after the flows' conditions (condition indices of flows unchanged):
+  // the static items (ZBHIP_OP_ITEM) or the collection variable (ZBHIP_OP_COLLECTION), then the
+  // outputCollection (ZBHIP_OP_OUTPUT); a completionCondition is a condition of its own, its index in
+  // the body's default_flow
+  for (auto& [b, loop] : collections) {
     C.elements[b].condition = (uint16_t)(C.cond_begin.size() - 1);
-    for (const MiItem& it : items) {
+    if (!loop.coll_var.empty()) {
+      zbhip_insn in{};
+      in.op = ZBHIP_OP_COLLECTION;
+      in.arg = C.str(loop.coll_var);
+      C.code.push_back(in);
+    }
+    for (const MiItem& it : loop.items) {
       zbhip_insn in{};
       in.op = ZBHIP_OP_ITEM;
       in.arg = it.type;
       in.literal = it.type == ZBHIP_DOC_STR ? (int64_t)C.str(it.text) : it.value;
+      C.code.push_back(in);
+    }
+    if (!loop.out_coll.empty()) {
+      zbhip_insn in{};
+      in.op = ZBHIP_OP_OUTPUT;
+      in.arg = C.str(loop.out_coll);
+      in.literal = C.str(loop.out_elem);
       C.code.push_back(in);
     }
     zbhip_insn end{};
@@ -976,6 +1024,13 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     C.code.push_back(end);
     C.cond_begin.push_back((uint32_t)C.code.size());
     C.cond_texts.emplace_back();
+    if (!loop.cond.empty()) {
+      FeelCompiler fc(loop.cond, C.code, name_of);
+      if (!fc.compile(err)) { err = "completionCondition: " + err; return ZBHIP_EUNSUPP; }
+      C.elements[b].default_flow = (uint16_t)(C.cond_begin.size() - 1);
+      C.cond_begin.push_back((uint32_t)C.code.size());
+      C.cond_texts.push_back(loop.cond);
+    }
   }
   // CSR of outgoing lists
   for (size_t e = 0; e < C.elements.size(); ++e) {

@@ -141,6 +141,11 @@ struct Lane {
   uint16_t trig_evt;    // K::S: the PROCESS_EVENT key ordinal of a boundary event's trigger on trig_key
   uint32_t inc;         // the incident info of a failed exclusive gateway (find_sequence_flow)
   uint32_t n_map;       // K::S: io-mapped VARIABLE records of the batch so far (values in StepParams.map_val)
+  // K::S: the value a job's document gave a multi-instance inner instance's local outputElement
+  // variable in this batch (mergeDocument updated it locally): set, zbhip_doc_type, value
+  uint8_t mo_set, mo_type;
+  uint16_t done_job;  // the job of the last JOB:COMPLETE (its key ordinal)
+  long long mo_val;
   bool pi_live;
   uint8_t pi_state;
   int pi_child;
@@ -419,9 +424,10 @@ __device__ __forceinline__ void overflow(Lane<K>& L, uint32_t entry) {
 // a follow-up command of the batch: its COMMAND record, then the FIFO (or the overflow list)
 template <class K>
 __device__ __forceinline__ void follow_up(Lane<K>& L, uint32_t code, uint32_t key, uint32_t aux, uint32_t elem,
-                                          bool complete, bool fs_pi, uint32_t qkey, uint32_t qflags = 0) {
+                                          bool complete, bool fs_pi, uint32_t qkey, uint32_t qflags = 0,
+                                          uint32_t rflags = 0) {
   const bool admit = pending(L) + L.processed + 1 < L.limit;
-  emit(L, code, key, aux, elem, admit ? 0u : F_UNPROCESSED);
+  emit(L, code, key, aux, elem, (admit ? 0u : F_UNPROCESSED) | rflags);
   const uint32_t entry = qentry(elem, complete, fs_pi, qkey) | qflags;
   if (admit) enqueue(L, entry);
   else overflow(L, entry);
@@ -609,6 +615,15 @@ __device__ __forceinline__ void merge_document_from(Lane<K>& L, uint32_t scope_k
   if (count > 1) { set_fail(L, FB_DOC); return; }
   const zbhip_doc_entry d = L.docs[begin];
   vm_drain();
+  if constexpr (K::IO) {
+    // a propagated multi-instance outputCollection: its items are the host's (the value comparison of
+    // setLocalVariable cannot be made here)
+    for (int i = 0; i < kVars; ++i)
+      if (i < L.nvars && (var_x(L, i) & 0xFFFF) == d.name_id && ((var_y(L, i) >> 16) & 0xFF) == kDocOutList) {
+        set_fail(L, FB_DOC);
+        return;
+      }
+  }
   if constexpr (!K::IO) {  // (no variables in scopes between the element and the process)
     if (scope_key != 0) {
       int v = var_find(L, scope_key, d.name_id);
@@ -649,6 +664,51 @@ __device__ __forceinline__ uint4 io_map(const Lane<K>& L, uint32_t e, int k) {
   if constexpr (!K::IO) return make_uint4(kIoNone, 0, 0, 0);
   if (!((L.pb[5] >> 17) & 1u)) return make_uint4(kIoNone, 0, 0, 0);
   return reinterpret_cast<const uint4*>(L.pb + (L.pb[6] >> 16))[2 * e + k];
+}
+
+// ---- multi-instance collections (K::IO: a body with a collection variable, output or condition) ----
+// a body's words in its io slots (runtime.cpp rebuild_program): [0] x = collection variable | output
+// collection << 16, y = outputElement | (completionCondition + 1) << 16, z / w = the numberOf* name ids;
+// [1] y = the static items' list id (0xFFFFFFFF: none)
+template <class K>
+__device__ __forceinline__ uint4 mi_ext(const Lane<K>& L, uint32_t body) {
+  if constexpr (!K::IO) return make_uint4(0xFFFFFFFFu, 0x0000FFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  if (!((L.pb[5] >> 17) & 1u)) return make_uint4(0xFFFFFFFFu, 0x0000FFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  return reinterpret_cast<const uint4*>(L.pb + (L.pb[6] >> 16))[2 * body];
+}
+
+// readInputCollectionVariable (MultiInstanceBodyProcessor.java:362-367): the item count and the list
+// (0xFFFFFFFF: the static items of a body without collection words), the variable seen from the scope
+// `key` in container c; a missing or non-list variable is an incident (outside the subset: fallback)
+template <class K>
+__device__ __forceinline__ bool mi_collection(Lane<K>& L, uint32_t body, uint4 bw, uint32_t key, uint32_t c, uint32_t& n,
+                                              uint32_t& list) {
+  const uint32_t coll = mi_ext(L, body).x & 0xFFFF;
+  list = 0xFFFFFFFFu;
+  if (coll == 0xFFFF) {
+    n = (bw.z >> 12) & 0xFF;
+    if constexpr (K::IO)
+      if ((L.pb[5] >> 17) & 1u) list = reinterpret_cast<const uint4*>(L.pb + (L.pb[6] >> 16))[2 * body + 1].y;
+    return true;
+  }
+  const int v = var_lookup(L, key, c, coll);
+  if (v < 0 || ((var_y(L, v) >> 16) & 0xFF) != ZBHIP_DOC_LIST) { set_fail(L, FB_FEEL); return false; }
+  const long long id = var_v(L, v);
+  const StepParams& P = *L.sp;
+  if (id < 0 || (unsigned long long)id >= P.n_lists) { set_fail(L, FB_FEEL); return false; }
+  n = P.list_hdr[id].y;
+  if (n > 63) { set_fail(L, FB_UNSUPPORTED); return false; }
+  list = (uint32_t)id;
+  return true;
+}
+
+// item i (0-based) of a list
+template <class K>
+__device__ __forceinline__ void list_item(const Lane<K>& L, uint32_t list, uint32_t i, uint32_t& type, long long& v) {
+  const StepParams& P = *L.sp;
+  const uint2 hd = P.list_hdr[list];
+  type = P.list_type[hd.x + i];
+  v = P.list_val[hd.x + i];
 }
 
 // ExpressionProcessor.evaluateVariableMappingExpression of a one-entry context in the scope `key` of
@@ -759,16 +819,37 @@ __device__ __forceinline__ void join_set(Lane<K>& L, uint32_t s, uint32_t v) {
 // comparison of a string with a number is NULL in feel-scala 1.17, ConditionIncidentTest).  A result
 // that is not a boolean is an incident in the reference (ExpressionProcessor.java:356-368).
 // The operand stack is four registers, top first (the compiler bounds the depth to 4).
+// The variables a multi-instance inner instance holds without a variable-table entry (its
+// inputElement, outputElement and loopCounter: setLoopVariables) and the body's numberOf* of a
+// completion condition (its primary context, MultiInstanceBodyProcessor.java:396-460): names (NONE:
+// none), zbhip_doc_types and values; looked up before the variable table
+struct MiVars {
+  uint32_t name[7];
+  uint32_t type[7];
+  long long val[7];
+};
+
 template <class K>
 __device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32_t scope_key, uint32_t c, uint32_t& t,
-                                         long long& x) {
+                                         long long& x, const MiVars* mv = nullptr) {
   // DbVariableState.getVariable: element scope first, then the enclosing scopes up to the process
-  const int v = var_lookup(L, scope_key, c, name);
+  uint32_t ty = 0;
+  long long raw = 0;
+  int hit = -1;
+  if (mv)
+    for (int i = 0; i < 7; ++i)
+      if (hit < 0 && mv->name[i] != NONE && mv->name[i] == name) hit = i;
   t = 0;
   x = 0;
-  if (v < 0) return true;  // missing -> null
-  const uint32_t ty = (var_y(L, v) >> 16) & 0xFF;
-  const long long raw = var_v(L, v);
+  if (hit >= 0) {
+    ty = mv->type[hit];
+    raw = mv->val[hit];
+  } else {
+    const int v = var_lookup(L, scope_key, c, name);
+    if (v < 0) return true;  // missing -> null
+    ty = (var_y(L, v) >> 16) & 0xFF;
+    raw = var_v(L, v);
+  }
   if (ty == ZBHIP_DOC_NIL) return true;
   if (ty == ZBHIP_DOC_BOOL) { t = 1; x = raw != 0; return true; }
   if (ty == ZBHIP_DOC_INT) {
@@ -784,7 +865,8 @@ __device__ __forceinline__ bool load_var(const Lane<K>& L, uint32_t name, uint32
 
 // result: -1 outside the subset (fallback), else the tag of the value (1: boolean, in `out`)
 template <class K>
-__device__ __forceinline__ int eval_condition(Lane<K>& L, uint32_t cond, uint32_t scope_key, uint32_t c, bool& out) {
+__device__ __forceinline__ int eval_condition(Lane<K>& L, uint32_t cond, uint32_t scope_key, uint32_t c, bool& out,
+                                              const MiVars* mv = nullptr) {
   const uint32_t* pb = L.pb;
   uint32_t pc = pb[pb[3] + cond];
   const uint32_t* code = pb + pb[4];
@@ -800,7 +882,7 @@ __device__ __forceinline__ int eval_condition(Lane<K>& L, uint32_t cond, uint32_
       long long x = 0;
       if (op == ZBHIP_OP_PUSH_NUM) { t = 2; x = (long long)(((unsigned long long)in.w << 32) | in.z); }
       else if (op == ZBHIP_OP_PUSH_BOOL) { t = 1; x = in.y != 0; }
-      else if (op == ZBHIP_OP_PUSH_VAR) { if (!load_var(L, in.y, scope_key, c, t, x)) return -1; }
+      else if (op == ZBHIP_OP_PUSH_VAR) { if (!load_var(L, in.y, scope_key, c, t, x, mv)) return -1; }
       if (sp >= 4) return -1;
       t3 = t2; a3 = a2; t2 = t1; a2 = a1; t1 = t0; a1 = a0; t0 = t; a0 = x;
       ++sp;
@@ -966,11 +1048,97 @@ __device__ __forceinline__ void take_sequence_flow(Lane<K>& L, uint32_t flow) {
   follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, fsk, target, false, true, k);
 }
 
+// MultiInstanceBodyProcessor.beforeExecutionPathCompleted (:160-191) of the inner instance `key` (table
+// entry t) of body c: updateOutputCollection (MultiInstanceOutputCollectionBehavior.java:57-141: the
+// outputElement's value at loopCounter - 1 -- C_MI_OUT, the host completes the array), then the
+// completion condition (satisfiesCompletionCondition :380-394), then for a sequential body the input
+// collection read again (its size in n).  Returns whether the condition is satisfied.
+template <class K>
+__device__ __forceinline__ bool mi_before_completed(Lane<K>& L, int t, uint32_t c, uint32_t key, uint32_t& n) {
+  const uint4 bw = elem_of(L, c), ext = mi_ext(L, c);
+  uint32_t list;
+  if (!mi_collection(L, c, bw, key, c, n, list)) return false;
+  const uint32_t loop = tget(L, t).y >> 26;
+  if (loop < 1 || loop > n) { set_fail(L, FB_UNSUPPORTED); return false; }
+  const uint32_t in = bw.x >> 16, ln = bw.w & 0xFFFF, oe = ext.y & 0xFFFF, oc = ext.x >> 16;
+  const uint32_t cond = ext.y >> 16;  // completionCondition + 1
+  if (oc == 0xFFFF && cond == 0) return false;
+  // the inner instance's own variables (not in the variable table)
+  MiVars mv;
+  for (int i = 0; i < 7; ++i) { mv.name[i] = NONE; mv.type[i] = 0; mv.val[i] = 0; }
+  if (in != 0xFFFF) {
+    if (list == 0xFFFFFFFFu) { set_fail(L, FB_UNSUPPORTED); return false; }
+    uint32_t ty;
+    long long v;
+    list_item(L, list, loop - 1, ty, v);
+    mv.name[0] = in;
+    mv.type[0] = ty;
+    mv.val[0] = v;
+  }
+  mv.name[1] = ln;
+  mv.type[1] = ZBHIP_DOC_INT;
+  mv.val[1] = loop;
+  if (oe != 0xFFFF && oe != in && oe != ln) {
+    mv.name[2] = oe;
+    mv.type[2] = L.mo_set ? L.mo_type : ZBHIP_DOC_NIL;
+    mv.val[2] = L.mo_set ? L.mo_val : 0;
+  }
+  if (oc != 0xFFFF) {
+    // the outputElement `= name` evaluated in the inner instance's scope
+    uint32_t ty = 0;
+    long long v = 0;
+    int hit = -1;
+    for (int i = 0; i < 3; ++i)
+      if (hit < 0 && mv.name[i] == oe) hit = i;
+    if (hit >= 0) {
+      ty = mv.type[hit];
+      v = mv.val[hit];
+    } else {
+      const int vi = var_lookup(L, key, c, oe);
+      if (vi < 0) { set_fail(L, FB_FEEL); return false; }  // null for a missing variable: unpinned
+      ty = (var_y(L, vi) >> 16) & 0xFF;
+      v = var_v(L, vi);
+    }
+    if (ty > ZBHIP_DOC_STR || ty == ZBHIP_DOC_OTHER) { set_fail(L, FB_UNSUPPORTED); return false; }
+    const StepParams& P = *L.sp;
+    if (L.n_map >= (uint32_t)kMapVals || L.ci >= P.map_cap) { set_fail(L, FB_VARS); return false; }
+    P.map_val[(size_t)L.n_map * P.map_cap + L.ci] = v;
+    emit(L, C_MI_OUT, loop - 1, scope_key(L, c), c, ty | (L.n_map << 4));
+    ++L.n_map;
+  }
+  if (cond == 0) return false;
+  // the body's numberOf* (the completing instance is still counted active, not yet completed)
+  const int tb = scope_find(L, c);
+  if (tb < 0) { set_fail(L, FB_UNSUPPORTED); return false; }
+  const uint2 be = tget(L, tb);
+  const uint32_t active = be.y & 0xFF, activated = (be.y >> 8) & 0xFF;
+  const long long nv[4] = {(long long)activated, (long long)active - 1, (long long)activated - (long long)active + 1, 0};
+  const uint32_t nn[4] = {ext.z & 0xFFFF, ext.z >> 16, ext.w & 0xFFFF, ext.w >> 16};
+  for (int k = 0; k < 4; ++k) {
+    mv.name[3 + k] = nn[k] == 0xFFFF ? NONE : nn[k];
+    mv.type[3 + k] = ZBHIP_DOC_INT;
+    mv.val[3 + k] = nv[k];
+  }
+  bool ok = false;
+  const int rt = eval_condition(L, cond - 1, key, c, ok, &mv);
+  if (rt != 1) { set_fail(L, FB_FEEL); return false; }  // not a boolean: an incident
+  return ok;
+}
+
 // transitionToCompleted (:158-191) + afterExecutionPathCompleted -> ProcessProcessor (:130-140)
 template <class K>
 __device__ __forceinline__ void transition_to_completed_child(Lane<K>& L, int t, uint32_t elem, uint4 w, uint32_t key) {
   const uint32_t c = scope_of<K>(w);
   const uint32_t fsk = K::S ? scope_key(L, c) : 0u;
+  // beforeExecutionPathCompleted (BpmnStateTransitionBehavior.java:171-178): a multi-instance body's
+  // checks before the COMPLETED record
+  bool satisfied = false;
+  uint32_t n_items = 0;
+  if constexpr (K::S)
+    if ((w.y >> 16) == 0 && c != 0 && etype(elem_of(L, c)) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      satisfied = mi_before_completed(L, t, c, key, n_items);
+      if (L.fail) return;
+    }
   emit(L, ZBHIP_PI_ELEMENT_COMPLETED, key, fsk, elem);
   apply_completed_child(L, t, key);
   if ((w.y >> 16) == 0) {  // end of the execution path
@@ -982,13 +1150,21 @@ __device__ __forceinline__ void transition_to_completed_child(Lane<K>& L, int t,
       const int ts = scope_find(L, c);
       const uint4 cw = elem_of(L, c);
       if (etype(cw) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
-        // MultiInstanceBodyProcessor.beforeExecutionPathCompleted (:160-191): no output collection, no
-        // completion condition; afterExecutionPathCompleted (:193-230): a sequential body activates its
-        // next inner instance while items are left, else the body completes once no child is active
+        // MultiInstanceBodyProcessor.afterExecutionPathCompleted (:193-230): a satisfied completion
+        // condition completes the body (terminateChildInstances of other active children --
+        // PROCESS_INSTANCE_BATCH:TERMINATE -- is outside the device subset); else a sequential body
+        // activates its next inner instance while items are left, and the body completes once no child
+        // is active
         if (ts < 0) { set_fail(L, FB_UNSUPPORTED); return; }
         const uint2 be = tget(L, ts);
         const uint32_t sk = be.x >> 16, loop = (be.y >> 8) & 0xFF;
-        if (((cw.z >> 20) & 1u) && loop < ((cw.z >> 12) & 0xFF)) {
+        if (satisfied) {
+          if ((be.y & 0xFF) != 0) { set_fail(L, FB_UNSUPPORTED); return; }
+          const uint32_t pc = scope_of<K>(cw);
+          follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, sk, scope_key(L, pc), c, true, pc == 0, sk);
+          return;
+        }
+        if (((cw.z >> 20) & 1u) && loop < n_items) {
           const uint32_t k = new_key(L);  // createInnerInstance -> activateChildInstanceWithKey
           follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, sk, cw.z & 0xFFF, false, false, k);
         } else if ((be.y & 0xFF) == 0) {
@@ -1546,7 +1722,9 @@ template <class K>
 __device__ __forceinline__ void activate_batch(Lane<K>& L, uint32_t body, uint4 w) {
   const int tb = scope_find(L, body);
   if (tb < 0) { set_fail(L, FB_UNSUPPORTED); return; }
-  const uint32_t bk = tget(L, tb).x >> 16, inner = w.z & 0xFFF, n = (w.z >> 12) & 0xFF;
+  const uint32_t bk = tget(L, tb).x >> 16, inner = w.z & 0xFFF;
+  uint32_t n, list;  // (ActivateProcessInstanceBatchProcessor: the record's index -- the collection's size)
+  if (!mi_collection(L, body, w, bk, scope_of<K>(w), n, list)) return;
   for (uint32_t i = 0; i < n && !L.fail; ++i) {
     const uint32_t k = new_key(L);
     follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, bk, inner, false, false, k);
@@ -1639,10 +1817,18 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         // setLoopVariables (:270-305): the item at loopCounter - 1 as the inputElement (if any), then
         // loopCounter, local to the inner instance (VARIABLE:CREATED, values from the program)
         const uint32_t loop = tget(L, t).y >> 26;
+        const uint4 ext = mi_ext(L, c);
+        uint32_t n, list;  // readInputCollectionVariable again: the item at loopCounter - 1
+        if (!mi_collection(L, c, bw, key, c, n, list)) return;
+        if (loop < 1 || loop > n) { set_fail(L, FB_FEEL); return; }  // (an EXTRACT_VALUE_ERROR incident)
         if ((bw.x >> 16) != 0xFFFFu) {
           const uint32_t ki = new_key(L);
-          emit(L, C_MI_ITEM, ki, key, c, loop);
+          if ((ext.x & 0xFFFF) == 0xFFFF) emit(L, C_MI_ITEM, ki, key, c, loop);
+          else emit(L, C_MI_LIST_ITEM, ki, list & 0xFFFF, list >> 16);
         }
+        // the outputElement variable nil-initialized locally, unless it is the inputElement or loopCounter
+        const uint32_t oe = ext.y & 0xFFFF;
+        if (oe != 0xFFFF && oe != (bw.x >> 16) && oe != (bw.w & 0xFFFF)) emit(L, C_MI_OUTEL, new_key(L), key, c);
         const uint32_t kl = new_key(L);
         emit(L, C_MI_LOOP, kl, key, c, loop);
         if (!ZBHIP_IS_JOB_WORKER(type)) {  // no job: the job field keeps the variables' key
@@ -1763,10 +1949,14 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         return;
       case ZBHIP_EL_MULTI_INSTANCE_BODY:  // MultiInstanceBodyProcessor.onActivate (:83-98) -> activate (:229-252)
         if constexpr (K::S) {
-          // the static inputCollection always evaluates; no event subscriptions on the body
+          // readInputCollectionVariable (a static collection always evaluates); no event subscriptions
+          // on the body
+          uint32_t n, list;
+          if (!mi_collection(L, elem, w, key, c, n, list)) return;
           emit(L, ZBHIP_PI_ELEMENT_ACTIVATED, key, fsa, elem);
           tbl_set_state(L, t, ZBHIP_PI_ELEMENT_ACTIVATED);
-          const uint32_t n = (w.z >> 12) & 0xFF;
+          if ((mi_ext(L, elem).x >> 16) != 0xFFFF)  // initializeOutputCollection (:43-55): [nil] * n, local
+            emit(L, C_MI_OUT, new_key(L), key, elem, 0x80u | n);
           if (n == 0) {  // an empty collection: completeElement
             follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, key, fsa, elem, true, true, key);
           } else if ((w.z >> 20) & 1u) {  // createInnerInstance -> activateChildInstanceWithKey (:292-307)
@@ -1774,7 +1964,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
             follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, k, key, w.z & 0xFFF, false, false, k);
           } else {  // activateChildInstancesInBatches (:315-324): PROCESS_INSTANCE_BATCH:ACTIVATE
             const uint32_t kb = new_key(L);
-            follow_up(L, C_PIB_ACTIVATE, kb, key, elem, true, false, kb, Q_TERM);
+            follow_up(L, C_PIB_ACTIVATE, kb, key, elem, true, false, kb, Q_TERM, n);  // (index: the size)
           }
         } else {
           set_fail(L, FB_UNSUPPORTED);
@@ -1890,16 +2080,52 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       // are not in the variable table (derived from the slot), so such a document falls back
       const uint4 bw = elem_of(L, c);
       if (c != 0 && L.doc_count == 1 && etype(bw) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
-        const uint32_t name = L.docs[L.doc_begin].name_id;
+        const zbhip_doc_entry d = L.docs[L.doc_begin];
+        const uint32_t name = d.name_id;
         vm_drain();
         if (name == (bw.x >> 16) || name == (bw.w & 0xFFFF)) { set_fail(L, FB_DOC); return; }
+        const uint4 ext = mi_ext(L, c);
+        const uint32_t oe = ext.y & 0xFFFF;
+        // the collections themselves: the body's output (held on the host) and the input variable (read
+        // again on every activation and completion) stay as they are on the device
+        if (name == (ext.x >> 16) || name == (ext.x & 0xFFFF)) { set_fail(L, FB_DOC); return; }
+        if (oe != 0xFFFF && name == oe) {
+          // the local outputElement variable (nil): updated in the inner instance's scope; its key is
+          // right below the loopCounter's (a job worker: two below the job's)
+          if (d.type == ZBHIP_DOC_LIST) { set_fail(L, FB_DOC); return; }
+          if (d.type != ZBHIP_DOC_NIL) {
+            // (a job worker's job field is -1 after JOB:COMPLETED: the completed job's key)
+            const uint32_t job = ZBHIP_IS_JOB_WORKER(type) ? L.done_job : tget(L, t).y & 0xFFFF;
+            emit(L, C_VAR_UPDATED, ZBHIP_IS_JOB_WORKER(type) ? job - 2 : job - 1, cmd_key, name);
+          }
+          L.mo_set = 1;
+          L.mo_type = d.type;
+          L.mo_val = d.type == ZBHIP_DOC_NIL ? 0 : d.value;
+          goto merged;
+        }
       }
     }
     merge_document_from(L, cmd_key, c, L.doc_begin, L.doc_count);
+  merged:;
   }
   if constexpr (K::S) {
     // JobWorkerTaskProcessor.onComplete (:63-75): unsubscribeFromEvents -- the boundary event's timer
     if (ZBHIP_IS_JOB_WORKER(type) && (L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) cancel_timer(L);
+  }
+  if constexpr (K::IO) {
+    // MultiInstanceBodyProcessor.onComplete (:100-114): propagateVariable of the outputCollection
+    // (BpmnStateBehavior.java:163-178 -> mergeDocument from the flow scope): created in the process
+    // instance's scope; a variable of that name above the body already (its array compared on the
+    // host only) is outside the subset
+    if (type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      const uint32_t oc = mi_ext(L, elem).x >> 16;
+      if (oc != 0xFFFF) {
+        if (var_lookup(L, cmd_key, c, oc) >= 0 || L.nvars >= kVars) { set_fail(L, FB_VARS); return; }
+        const uint32_t kv = new_key(L);
+        emit(L, C_MI_PROP, kv, cmd_key, elem);
+        var_put(L, L.nvars++, oc, kv | ((uint32_t)kDocOutList << 16), 0);
+      }
+    }
   }
   if constexpr (K::M) {
     // JobWorkerTaskProcessor.onComplete: unsubscribeFromEvents -- the boundary event's subscription
@@ -2715,6 +2941,9 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   L.trig_key = NONE;
   L.trig_evt = NONE;
   L.n_map = 0;
+  L.mo_set = 0;
+  L.mo_type = 0;
+  L.mo_val = 0;
   L.docs = P.docs;
   L.doc_begin = doc_begin;
   L.doc_count = doc_count;
@@ -2930,6 +3159,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
       }
       // JobCompletedApplier: job rows deleted; jobKey = -1 while the flow scope is active
       e.y &= ~(3u << 24);  // the job row (and its ACTIVATED state) is deleted
+      L.done_job = e.y & 0xFFFF;  // (an inner instance's loop variables: keys below the job's)
       if (fs_active) e.y = (e.y & 0xFFFF0000u) | JOB_MINUS1;
       tput(L, t, e);
       if (fs_active) {  // afterAccept
@@ -3717,9 +3947,12 @@ __global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp,
 // Subject check of a device-resident window (zbhip_submit_device*): every command claims its
 // subject (instance slot, or correlation slot for MESSAGE / MESSAGE_SUBSCRIPTION commands) with the
 // window's stamp; a second claim in the window flags a duplicate (bit 0), a subject out of range or
-// an unknown kind bit 1.  The host then plans the window into rounds (or refuses it).
+// an unknown kind bit 1.  The flags gather in w[0]; the last workgroup to finish (w[1] counts them)
+// moves them into the guard word w[2] (the window's k_step launch reads it) and writes the window's
+// completion marker stamp << 2 | flags into the host-mapped word `host` -- no copy, no reset launch:
+// the host reads the marker whenever it needs the verdict (runtime.cpp resolve_guard).
 __global__ __launch_bounds__(256) void k_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots,
-                                                       uint32_t* seen, uint32_t stamp, uint32_t* flag) {
+                                                       uint32_t* seen, uint32_t stamp, uint32_t* w, uint32_t* host) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   uint32_t f = 0;
   if (i < n) {
@@ -3734,7 +3967,19 @@ __global__ __launch_bounds__(256) void k_subject_check(const uint4* cmds, uint32
       f = 1;
     }
   }
-  if (f) atomicOr(flag, f);  // rare: a faulty window
+  if (f) atomicOr(&w[0], f);  // rare: a faulty window
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&w[1], 1u) == gridDim.x - 1) {  // the last workgroup: every flag is in w[0]
+      __threadfence();
+      const uint32_t all = atomicExch(&w[0], 0u);
+      atomicExch(&w[1], 0u);
+      atomicExch(&w[2], all);
+      __threadfence_system();
+      *reinterpret_cast<volatile uint32_t*>(host) = (stamp << 2) | all;
+    }
+  }
 }
 
 // A device window's launch order by subject (instance slots, then correlation slots): the stable
@@ -3993,9 +4238,9 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
 }
 
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
-                                uint32_t stamp, uint32_t* flag, hipStream_t s) {
+                                uint32_t stamp, uint32_t* w, uint32_t* host, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_subject_check, dim3((n + 255) / 256), dim3(256), 0, s, cmds, n, n_inst, n_slots, seen, stamp,
-                            flag);
+                            w, host);
   return hipGetLastError();
 }
 

@@ -133,6 +133,8 @@ struct zbhip_serializer {
   std::unordered_map<std::string, uint32_t> name_ids;
   std::vector<std::string> strs;
   std::unordered_map<std::string, uint32_t> str_ids;
+  // the list dictionary (ZBHIP_DOC_LIST values), mirrored from the handle's (zbhip_intern_list)
+  std::vector<std::vector<std::pair<uint8_t, int64_t>>> lists;
   int32_t broker[3] = {8, 4, 0};  // RecordMetadata.CURRENT_BROKER_VERSION of the reference build (8.4.0-SNAPSHOT)
   Bytes auth;                     // empty AuthInfo (format UNKNOWN, authData "")
 };
@@ -180,6 +182,14 @@ int64_t zbhip_serializer_intern_string(zbhip_serializer* s, const char* bytes, s
   s->strs.push_back(v);
   s->str_ids.emplace(std::move(v), id);
   return id;
+}
+
+int64_t zbhip_serializer_intern_list(zbhip_serializer* s, const zbhip_doc_entry* items, size_t n) {
+  if (!s || (n && !items)) return ZBHIP_EINVAL;
+  std::vector<std::pair<uint8_t, int64_t>> v;
+  for (size_t i = 0; i < n; ++i) v.push_back({items[i].type, items[i].value});
+  s->lists.push_back(std::move(v));
+  return (int64_t)s->lists.size() - 1;
 }
 
 int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, uint32_t* idx_out) {
@@ -371,8 +381,36 @@ bool doc_value(const zbhip_serializer* s, const zbhip_doc_entry& d, Bytes& b) {
       if ((uint64_t)d.value >= s->strs.size()) return false;
       mp_str(b, s->strs[(size_t)d.value]);
       return true;
+    case ZBHIP_DOC_LIST: {  // an array of its items (MultiInstanceOutputCollectionBehavior: header + items)
+      if ((uint64_t)d.value >= s->lists.size()) return false;
+      const auto& items = s->lists[(size_t)d.value];
+      mp_array(b, (uint32_t)items.size());
+      for (const auto& it : items) {
+        zbhip_doc_entry e{};
+        e.type = it.first;
+        e.value = it.second;
+        if (e.type == ZBHIP_DOC_LIST || !doc_value(s, e, b)) return false;
+      }
+      return true;
+    }
     default: return false;
   }
+}
+
+// a list value's items in a state row: "type:value;..." (the oracle's format, zb_oracle.cpp list_text)
+std::vector<std::pair<uint8_t, int64_t>> parse_list_text(const std::string& t) {
+  std::vector<std::pair<uint8_t, int64_t>> items;
+  size_t a = 0;
+  while (a < t.size()) {
+    size_t e = t.find(';', a);
+    if (e == std::string::npos) e = t.size();
+    const std::string it = t.substr(a, e - a);
+    const size_t c = it.find(':');
+    if (c != std::string::npos)
+      items.push_back({(uint8_t)strtol(it.substr(0, c).c_str(), nullptr, 10), (int64_t)strtoll(it.c_str() + c + 1, nullptr, 10)});
+    a = e + 1;
+  }
+  return items;
 }
 
 bool document(const zbhip_serializer* s, const zbhip_doc_entry* e, size_t n, Bytes& b) {
@@ -789,9 +827,20 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     auto f = fields_of(p[3]);
     zbhip_doc_entry d{};
     d.type = (uint8_t)ll(f["type"]);
-    d.value = ll(f["value"]);
     Bytes val;
-    if (!doc_value(s, d, val)) return ZBHIP_EUNSUPP;
+    if (d.type == ZBHIP_DOC_LIST) {  // the row holds the items
+      const auto items = parse_list_text(f["value"]);
+      mp_array(val, (uint32_t)items.size());
+      for (const auto& it : items) {
+        zbhip_doc_entry e{};
+        e.type = it.first;
+        e.value = it.second;
+        if (e.type == ZBHIP_DOC_LIST || !doc_value(s, e, val)) return ZBHIP_EUNSUPP;
+      }
+    } else {
+      d.value = ll(f["value"]);
+      if (!doc_value(s, d, val)) return ZBHIP_EUNSUPP;
+    }
     cf_prefix(k, ord); dbl(k, ll(p[1])); dbs(k, p[2]);
     mp_map(v, 2);  // VariableInstance.java:22
     key(v, "key"); mp_int(v, ll(f["key"]));
@@ -1208,8 +1257,39 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
           dv = id;
           break;
         }
-        default: return ZBHIP_EUNSUPP;  // documents / arrays: outside the device's variables
+        case MpNode::ARR: {  // a list of scalars: its items in the row (ZBHIP_DOC_LIST)
+          std::string items;
+          for (const auto& it : x.arr) {
+            long long iv = 0;
+            int ity;
+            if (it.k == MpNode::NIL) ity = ZBHIP_DOC_NIL;
+            else if (it.k == MpNode::BOOL) { ity = ZBHIP_DOC_BOOL; iv = it.i; }
+            else if (it.k == MpNode::INT) { ity = ZBHIP_DOC_INT; iv = it.i; }
+            else if (it.k == MpNode::FLOAT) {
+              ity = ZBHIP_DOC_DEC;
+              const double sc = it.f * 1e6;
+              if (!(sc > -9.2e18 && sc < 9.2e18)) return ZBHIP_EUNSUPP;
+              iv = llround(sc);
+              if ((double)iv / 1e6 != it.f) return ZBHIP_EUNSUPP;
+            } else if (it.k == MpNode::STR) {
+              if (!intern) return ZBHIP_EUNSUPP;
+              const int64_t id = intern(ictx, it.s.data(), it.s.size());
+              if (id < 0) return (int)id;
+              ity = ZBHIP_DOC_STR;
+              iv = id;
+            } else {
+              return ZBHIP_EUNSUPP;  // nested documents / arrays
+            }
+            items += (items.empty() ? "" : ";") + std::to_string(ity) + ":" + std::to_string(iv);
+          }
+          snprintf(b, sizeof b, "VARIABLES|%lld|%s|key=%lld,type=%d,value=", (long long)scope, name.c_str(),
+                   (long long)mi(v.get("key")), (int)ZBHIP_DOC_LIST);
+          out = std::string(b) + items;
+          break;
+        }
+        default: return ZBHIP_EUNSUPP;  // documents: outside the device's variables
       }
+      if (x.k == MpNode::ARR) break;
       snprintf(b, sizeof b, "VARIABLES|%lld|%s|key=%lld,type=%d,value=%lld", (long long)scope, name.c_str(),
                (long long)mi(v.get("key")), type, dv);
       out = b;
@@ -1245,6 +1325,19 @@ extern "C" int zbhip_serializer_decode_state_entry(zbhip_serializer* s, uint32_t
                (long long)mi(j->get("processDefinitionVersion")), ms(j->get("tenantId")).c_str(),
                (long long)mi(j->get("deadline")), ms(j->get("worker")).c_str());
       out = b;
+      // a failed job's stored fields (JobFailProcessor): errorMessage in hex, retryBackoff, recurringTime
+      // (a failure that left all three at their defaults reads back through its retries alone)
+      const std::string em = ms(j->get("errorMessage"));
+      const long long rb = mi(j->get("retryBackoff")), rt = j->get("recurringTime") ? mi(j->get("recurringTime")) : -1;
+      if (!em.empty() || rb != 0 || rt != -1) {
+        static const char* hx = "0123456789abcdef";
+        out += ",errorMessageHex=";
+        for (unsigned char c : em) {
+          out += hx[c >> 4];
+          out += hx[c & 15];
+        }
+        out += ",retryBackoff=" + std::to_string(rb) + ",recurringTime=" + std::to_string(rt);
+      }
       break;
     }
     case 17: {  // JOB_STATES

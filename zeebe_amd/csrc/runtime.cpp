@@ -60,7 +60,7 @@ hipError_t launch_subject_sort(const uint4* cmds, uint32_t n, uint32_t n_inst, u
                                uint32_t* k1, uint32_t* v0, uint32_t* order, void* temp, size_t temp_bytes,
                                hipStream_t s);
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
-                                uint32_t stamp, uint32_t* flag, hipStream_t s);
+                                uint32_t stamp, uint32_t* w, uint32_t* host, hipStream_t s);
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t xcap,
                          uint32_t n, uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out,
                          hipStream_t s);
@@ -110,6 +110,18 @@ struct Proc {
     bool seq;
     uint16_t input_name, loop_name;
     std::vector<std::pair<uint8_t, int64_t>> items;
+    // the inputCollection variable (ZBHIP_OP_COLLECTION; NONE: the static items), the outputCollection
+    // and outputElement names (ZBHIP_OP_OUTPUT), the completionCondition's condition index (-1 none),
+    // the name ids of numberOfInstances / ActiveInstances / CompletedInstances / TerminatedInstances
+    // (NONE: the condition does not read it)
+    uint16_t coll_name = NONE, out_coll = NONE, out_elem = NONE;
+    int32_t cond = -1;
+    uint32_t static_list = 0xFFFFFFFFu;  // the static items as a list (a body with collection words)
+    uint16_t n_names[4] = {NONE, NONE, NONE, NONE};
+    // the outputElement is a local nil-initialized variable of the inner instance (not the inputElement
+    // or loopCounter: setLoopVariables :283-300)
+    bool out_local() const { return out_elem != NONE && out_elem != input_name && out_elem != loop_name; }
+    bool ext() const { return coll_name != NONE || out_coll != NONE || cond >= 0; }
   };
   std::vector<Mi> mi;
   std::vector<int16_t> mi_of;  // per element: its body's index in `mi` (the body and its inner activity), -1
@@ -624,8 +636,9 @@ struct zbhip_handle {
   } guard_win{};
   bool guard_armed = false;    // submitted with a speculative check, not run yet
   bool guard_pending = false;  // run guarded, flag not read yet
-  uint32_t* h_check_flag = nullptr;  // pinned
-  hipEvent_t check_ev = nullptr;
+  uint32_t* h_check_flag = nullptr;  // host-mapped: the last check's completion marker (stamp << 2 | flags)
+  uint32_t* d_check_host = nullptr;  // its device address
+  uint32_t guard_stamp = 0;          // the stamp of the checked window
   // resolve_key: the generation of every subject (bumped when an instance is created or ends, so
   // keys of an earlier instance in a reused slot never resolve); stale entries are compacted away
   std::vector<uint32_t> inst_gen;
@@ -727,6 +740,37 @@ struct zbhip_handle {
     return id;
   }
 
+  // ---- the list dictionary (ZBHIP_DOC_LIST values: multi-instance inputCollection variables and
+  // outputCollections), deduplicated; its items on the device (d_list_*: uploaded before a run) ----
+  using Items = std::vector<std::pair<uint8_t, int64_t>>;
+  std::vector<Items> lists;
+  std::map<Items, uint32_t> list_ids;
+  std::vector<uint2> list_hdr;      // per list: first item, item count
+  std::vector<long long> list_val;  // the items' values, then their zbhip_doc_types
+  std::vector<uint8_t> list_type;
+  uint2* d_list_hdr = nullptr;
+  long long* d_list_val = nullptr;
+  uint8_t* d_list_type = nullptr;
+  size_t d_list_n = 0, d_list_items = 0, d_list_cap = 0, d_litem_cap = 0;
+  // multi-instance output collections (host-side: the device keeps no array): per body element
+  // instance the collection variable's key and items (track_mi, from the drained records); the list
+  // ids of propagated collections (variables of type kDocOutList on the device), by variable key;
+  // the inline values of the window's multi-instance records, by (command, ordinal)
+  struct MiOut {
+    int64_t var_key;
+    Items items;
+  };
+  std::unordered_map<int64_t, MiOut> mi_out;
+  std::unordered_map<int64_t, uint32_t> outlist_var;
+  struct MiRec {
+    int64_t key, scope;
+    int32_t name;
+    uint8_t intent, type;
+    int64_t value;
+  };
+  std::unordered_map<uint64_t, MiRec> mi_rec;
+  bool mi_ext = false;  // a deployed process has a multi-instance collection variable / output / condition
+
   // ---- message correlation (variant 2) ----
   std::vector<std::string> strs;               // value dictionary
   std::unordered_map<std::string, uint32_t> str_ids;
@@ -810,6 +854,8 @@ struct zbhip_handle {
 static int finalize(zbhip_handle* h);
 static int settle(zbhip_handle* h);
 static int resolve_guard(zbhip_handle* h);
+static int64_t intern_items(zbhip_handle* h, const zbhip_handle::Items& v);
+static int sync_lists(zbhip_handle* h);
 
 extern "C" {
 
@@ -882,7 +928,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
        dalloc(&h->d_xparts, cfg->max_commands) == hipSuccess &&
        dalloc(&h->d_key_counter, 1) == hipSuccess && dalloc(&h->d_key_base, cfg->max_commands) == hipSuccess &&
        dalloc(&h->d_key_blk, (cfg->max_commands + 1023) / 1024 + 1) == hipSuccess && dalloc(&h->d_xcount, 1024) == hipSuccess &&
-       dalloc(&h->d_seen, N + S) == hipSuccess && dalloc(&h->d_check_flag, 1) == hipSuccess &&
+       dalloc(&h->d_seen, N + S) == hipSuccess && dalloc(&h->d_check_flag, 4) == hipSuccess &&
        dalloc(&h->d_ovf, h->ovf_cap = std::max<uint32_t>(4096u, 4u * cfg->max_commands)) == hipSuccess &&
        dalloc(&h->d_ovf_count, 1) == hipSuccess &&
        dalloc(&h->d_cont, cfg->max_commands) == hipSuccess && dalloc(&h->d_cont_order, cfg->max_commands) == hipSuccess;
@@ -911,6 +957,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
       hipMemsetAsync(h->st.tmr, 0, N * sizeof(uint4), h->stream) != hipSuccess ||
       hipMemsetAsync(h->st.join, 0, N * kJoinWords * sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_seen, 0, (N + S) * sizeof(uint32_t), h->stream) != hipSuccess ||
+      hipMemsetAsync(h->d_check_flag, 0, 4 * sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_ovf_count, 0, sizeof(uint32_t), h->stream) != hipSuccess ||
       hipMemsetAsync(h->d_stats, 0, (64 * 8 + 8) * sizeof(unsigned long long), h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -924,9 +971,10 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
 
 void zbhip_close(zbhip_handle* h) {
   if (!h) return;
-  if (h->check_ev) (void)hipEventSynchronize(h->check_ev);
-  if (h->h_check_flag) (void)hipHostFree(h->h_check_flag);
-  if (h->check_ev) (void)hipEventDestroy(h->check_ev);
+  if (h->h_check_flag) {
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipHostFree(h->h_check_flag);
+  }
   (void)hipFree(h->st.hdr);
   (void)hipFree(h->st.slots);
   (void)hipFree(h->st.var_meta);
@@ -963,6 +1011,9 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->st.sub_b);
   (void)hipFree(h->st.sub_k);
   (void)hipFree(h->d_str_hash);
+  (void)hipFree(h->d_list_hdr);
+  (void)hipFree(h->d_list_val);
+  (void)hipFree(h->d_list_type);
   (void)hipFree(h->d_xparts);
   (void)hipFree(h->d_cmd_hdr2);
   (void)hipFree(h->d_xout);
@@ -1152,12 +1203,25 @@ static int rebuild_program(zbhip_handle* h) {
       for (uint32_t e = 0; e < n_el; ++e)
         for (int k = 0; k < 2; ++k) {
           // w0 = type | target name << 16, w1 = source name id, w2/w3 = the literal (STR: its string id)
-          const Proc::Io& io = P.io[e][k];
+          const Proc::Io io = e < P.io.size() ? P.io[e][k] : Proc::Io{};
           uint32_t* m = pb + io_off + 8 * e + 4 * k;
           m[0] = io.type | ((uint32_t)io.tgt << 16);
           m[1] = io.src;
           m[2] = (uint32_t)((uint64_t)io.lit & 0xFFFFFFFFu);
           m[3] = (uint32_t)((uint64_t)io.lit >> 32);
+          // a multi-instance body (never io-mapped) holds its collection words in its input slot
+          // (kernels.hip mi_ext): collection | outputCollection << 16, outputElement | (condition + 1) << 16,
+          // numberOfInstances | numberOfActiveInstances << 16, numberOfCompletedInstances |
+          // numberOfTerminatedInstances << 16
+          const Proc::Mi* mb = k == 0 && P.els[e].element_type == ZBHIP_EL_MULTI_INSTANCE_BODY ? P.mi_body(e) : nullptr;
+          if (mb) {
+            m[0] = mb->coll_name | ((uint32_t)mb->out_coll << 16);
+            m[1] = mb->out_elem | ((uint32_t)(mb->cond + 1) << 16);
+            m[2] = mb->n_names[0] | ((uint32_t)mb->n_names[1] << 16);
+            m[3] = mb->n_names[2] | ((uint32_t)mb->n_names[3] << 16);
+          } else if (k == 1 && P.els[e].element_type == ZBHIP_EL_MULTI_INSTANCE_BODY && P.mi_body(e)) {
+            m[1] = P.mi_body(e)->static_list;  // (no output mapping: m[0] stays kIoNone)
+          }
         }
     pb[7] = create_template_word(P);
     // straight-line segment words (kernels.hip fast_command): a start event or service task with
@@ -1375,13 +1439,29 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if (b1 <= b0 || b1 > P.code.size() || P.code[b1 - 1].op != ZBHIP_OP_END) return ZBHIP_EINVAL;
     for (uint32_t i = b0; i + 1 < b1; ++i) {
       const zbhip_insn& in = P.code[i];
-      if (in.op != ZBHIP_OP_ITEM) return ZBHIP_EINVAL;
+      if (in.op == ZBHIP_OP_COLLECTION) {  // (string-table indices until the names are interned below)
+        if (i != b0 || in.arg >= P.strings.size()) return ZBHIP_EINVAL;
+        m.coll_name = (uint16_t)in.arg;
+        continue;
+      }
+      if (in.op == ZBHIP_OP_OUTPUT) {
+        if (i + 2 != b1 || in.arg >= P.strings.size() || in.literal < 0 || (size_t)in.literal >= P.strings.size())
+          return ZBHIP_EINVAL;
+        m.out_coll = (uint16_t)in.arg;
+        m.out_elem = (uint16_t)in.literal;
+        continue;
+      }
+      if (in.op != ZBHIP_OP_ITEM || m.coll_name != NONE) return ZBHIP_EINVAL;
       if (in.arg != ZBHIP_DOC_INT && in.arg != ZBHIP_DOC_BOOL && in.arg != ZBHIP_DOC_NIL && in.arg != ZBHIP_DOC_STR)
         return ZBHIP_EUNSUPP;
       if (in.arg == ZBHIP_DOC_STR && (in.literal < 0 || (size_t)in.literal >= P.strings.size())) return ZBHIP_EINVAL;
       m.items.push_back({(uint8_t)in.arg, in.literal});
     }
     if (m.items.size() > kMaxMiItems) return ZBHIP_EUNSUPP;
+    if (E.default_flow != ZBHIP_NONE16) {  // the completionCondition
+      if ((size_t)E.default_flow + 1 >= P.cond_begin.size()) return ZBHIP_EINVAL;
+      m.cond = E.default_flow;
+    }
     if (E.message_name != ZBHIP_NONE16 && E.message_name >= P.strings.size()) return ZBHIP_EINVAL;
     P.mi_of[e] = P.mi_of[e + 1] = (int16_t)P.mi.size();
     P.mi.push_back(std::move(m));
@@ -1433,6 +1513,38 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         if (sid < 0) return (int)sid;
         it.second = sid;
       }
+    // then the collection variable, the outputCollection and outputElement names, the completion
+    // condition's variables (the oracle's deploy order); numberOf* are the condition's primary context
+    for (uint16_t* nm : {&m.coll_name, &m.out_coll, &m.out_elem})
+      if (*nm != NONE) {
+        const int id = zbhip_intern(h, P.strings[*nm].c_str());
+        if (id < 0) return id;
+        *nm = (uint16_t)id;
+      }
+    if (m.cond >= 0) {
+      static const char* kNumberOf[4] = {"numberOfInstances", "numberOfActiveInstances", "numberOfCompletedInstances",
+                                         "numberOfTerminatedInstances"};
+      for (uint32_t i = P.cond_begin[m.cond]; i < P.cond_begin[m.cond + 1]; ++i)
+        if (P.code[i].op == ZBHIP_OP_PUSH_VAR) {
+          if (P.code[i].arg >= P.strings.size()) return ZBHIP_EINVAL;
+          const std::string& vn = P.strings[P.code[i].arg];
+          const int id = zbhip_intern(h, vn.c_str());
+          if (id < 0) return id;
+          P.code[i].arg = (uint32_t)id;
+          for (int k = 0; k < 4; ++k)
+            if (vn == kNumberOf[k]) m.n_names[k] = (uint16_t)id;
+          // the outputCollection is not held on the device
+          if (id == m.out_coll) return ZBHIP_EUNSUPP;
+        }
+    }
+    if (m.ext()) {
+      P.has_io = true;  // the body's words in its io slot (rebuild_program): KScopeIO
+      if (m.coll_name == NONE) {  // the static items as a list: the device reads item values from it
+        const int64_t id = intern_items(h, m.items);
+        if (id < 0) return (int)id;
+        m.static_list = (uint32_t)id;
+      }
+    }
   }
   // io mappings (zbhip_mapping): job worker tasks (not multi-instance inner activities) and embedded
   // sub-processes, one input and one output each; names interned in element order, the input's source
@@ -1523,7 +1635,12 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   for (size_t e = 0; e < P.els.size(); ++e)
     if (ZBHIP_IS_JOB_WORKER(P.els[e].element_type) && P.els[e].job_type < P.strings.size())
       P.job_type_id[e] = h->job_type(P.strings[P.els[e].job_type]);
+  const bool mi_ext = std::any_of(P.mi.begin(), P.mi.end(), [](const Proc::Mi& m) { return m.ext(); });
   h->procs.push_back(std::move(P));
+  if (mi_ext) {
+    h->mi_ext = true;
+    h->ring_ok = false;  // list values: the host serialiser writes such windows
+  }
   {
     const uint64_t limit = (uint64_t)h->cfg.max_commands_in_batch;
     bool over = false;
@@ -1820,6 +1937,22 @@ int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n
 static int replan_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
                                 size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts, bool* replanned);
 
+// The subject check's verdict of the last checked window: its completion marker in host-mapped memory
+// (k_subject_check's last workgroup writes stamp << 2 | flags); a spin, bounded by the stream's own
+// completion (a device fault ends it)
+static int64_t read_check_marker(zbhip_handle* h) {
+  const volatile uint32_t* m = h->h_check_flag;
+  const uint32_t want = h->guard_stamp & 0x3FFFFFFFu;
+  for (uint32_t spin = 0; (*m >> 2) != want; ++spin) {
+    if (spin > (1u << 16)) {  // slow: let the runtime wait for the stream instead
+      HIPCHK(hipStreamSynchronize(h->stream));
+      if ((*m >> 2) != want) return ZBHIP_EDEVICE;
+      break;
+    }
+  }
+  return *m & 3u;
+}
+
 // The flag of a speculatively checked device window (check_device_window): read once, before anything
 // depends on the window.  Clean: nothing to do.  A repeated subject: the guarded launch did nothing; the
 // window is replanned on the host and run again with its run flags (before any later window).  A subject
@@ -1831,8 +1964,9 @@ static int resolve_guard(zbhip_handle* h) {
   }
   if (!h->guard_pending) return ZBHIP_OK;
   h->guard_pending = false;
-  HIPCHK(hipEventSynchronize(h->check_ev));
-  const uint32_t flag = *h->h_check_flag;
+  const int64_t fl = read_check_marker(h);
+  if (fl < 0) return (int)fl;
+  const uint32_t flag = (uint32_t)fl;
   if (!flag) return ZBHIP_OK;
   const auto w = h->guard_win;
   h->next_doc_base = w.doc_base;  // the window's log positions and documents are given again
@@ -1855,31 +1989,28 @@ static int check_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, s
                                size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts, bool* replanned) {
   *replanned = false;
   if ((h->cfg.flags & ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS) || n == 0) return ZBHIP_OK;
-  if (++h->check_stamp == 0) {
+  if (++h->check_stamp >= (1u << 30)) {  // (30-bit stamps: the completion marker's)
     HIPCHK(hipMemsetAsync(h->d_seen, 0, ((size_t)h->cfg.max_instances + h->st.n_slots) * sizeof(uint32_t), h->stream));
     h->check_stamp = 1;
   }
-  HIPCHK(hipMemsetAsync(h->d_check_flag, 0, sizeof(uint32_t), h->stream));
+  if (!h->h_check_flag) {  // the host-mapped completion marker (stamp << 2 | flags)
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->h_check_flag), sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
+      return ZBHIP_ENOMEM;
+    *h->h_check_flag = 0;
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->d_check_host), h->h_check_flag, 0));
+  }
   HIPCHK(launch_subject_check(reinterpret_cast<const uint4*>(dev_cmds), (uint32_t)n, h->cfg.max_instances, h->st.n_slots,
-                              h->d_seen, h->check_stamp, h->d_check_flag, h->stream));
+                              h->d_seen, h->check_stamp, h->d_check_flag, h->d_check_host, h->stream));
+  h->guard_win = {dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, h->next_doc_base, h->next_source, 0};
+  h->guard_stamp = h->check_stamp;
   if (!h->msg() && !getenv("ZBHIP_SYNC_SUBJECT_CHECK")) {
-    // speculative: the flag follows into pinned memory behind an event, nobody waits now; the run
-    // launches its k_step guarded by the device flag (resolve_guard reads it later)
-    if (!h->h_check_flag) {
-      if (hipHostMalloc(reinterpret_cast<void**>(&h->h_check_flag), sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
-        return ZBHIP_ENOMEM;
-      *h->h_check_flag = 0;
-    }
-    if (!h->check_ev) HIPCHK(hipEventCreateWithFlags(&h->check_ev, hipEventDisableTiming));
-    HIPCHK(hipMemcpyAsync(h->h_check_flag, h->d_check_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipEventRecord(h->check_ev, h->stream));
-    h->guard_win = {dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, h->next_doc_base, h->next_source, 0};
+    // speculative: nobody waits now; the run launches its k_step guarded by the device's verdict
+    // (resolve_guard reads the marker later)
     h->guard_armed = true;
     return ZBHIP_OK;
   }
-  uint32_t flag = 0;
-  HIPCHK(hipMemcpyAsync(&flag, h->d_check_flag, sizeof flag, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  int64_t flag = read_check_marker(h);
+  if (flag < 0) return (int)flag;
   if (flag & 2) return ZBHIP_EINVAL;
   if (!(flag & 1)) return ZBHIP_OK;
   return replan_device_window(h, dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, replanned);
@@ -2255,6 +2386,80 @@ static int fold_journals(zbhip_handle* h, size_t keep = 0) {
   return ZBHIP_OK;
 }
 
+// The multi-instance collection records of window command c (instance `inst`), in log order: the
+// values their expansion gives them (mi_rec: the device writes no list) and the host's copy of every
+// body's outputCollection (mi_out) and of the propagated ones (outlist_var) -- kernels.hip C_MI_*.
+static int track_mi(zbhip_handle* h, size_t c, uint32_t inst) {
+  auto mi_fail = [&](int site) {
+    if (getenv("ZBHIP_DEBUG_MI")) fprintf(stderr, "[track_mi] command %zu instance %u: site %d\n", c, inst, site);
+    return (int)ZBHIP_EDEVICE;
+  };
+  const uint32_t nrec = h->h_hdr[c].x & 0xFFFF;
+  const uint2* rows = h->h_out.data() + h->h_off[c];
+  const uint16_t proc = inst < h->inst_proc.size() ? h->inst_proc[inst] : NONE;
+  if (proc == NONE || proc >= h->procs.size()) return ZBHIP_OK;
+  const Proc& P = h->procs[proc];
+  for (uint32_t i = 0; i < nrec; ++i) {
+    const uint2 w = rows[i];
+    const uint32_t code = (w.y >> 16) & 0xFF, c6 = code & 0x3F, fl = w.y >> 24;
+    if (code & kRejectBit) continue;
+    const uint32_t key_ord = w.x & 0xFFFF, aux_ord = w.x >> 16, elem = w.y & 0xFFFF;
+    const uint64_t at = ((uint64_t)c << 16) | i;
+    if (c6 == C_MI_LIST_ITEM) {  // the C_MI_LOOP row that follows: the scope, the body, the loop counter
+      uint32_t j = i + 1;
+      while (j < nrec && ((rows[j].y >> 16) & 0x3F) != C_MI_LOOP) ++j;
+      if (j >= nrec) return mi_fail(1);
+      const uint32_t body = rows[j].y & 0xFFFF, loop = rows[j].y >> 24, list = aux_ord | (elem << 16);
+      const Proc::Mi* m = P.mi_body(body);
+      if (!m || list >= h->lists.size() || loop < 1 || loop > h->lists[list].size()) return mi_fail(2);
+      const auto& it = h->lists[list][loop - 1];
+      h->mi_rec[at] = {h->key_of(inst, key_ord), h->key_of(inst, rows[j].x >> 16), (int32_t)m->input_name,
+                       (uint8_t)ZBHIP_VAR_CREATED, it.first, it.second};
+    } else if (c6 == C_MI_OUTEL) {  // the outputElement variable, nil
+      const Proc::Mi* m = P.mi_body(elem);
+      if (!m) return mi_fail(3);
+      h->mi_rec[at] = {h->key_of(inst, key_ord), h->key_of(inst, aux_ord), (int32_t)m->out_elem,
+                       (uint8_t)ZBHIP_VAR_CREATED, (uint8_t)ZBHIP_DOC_NIL, 0};
+    } else if (c6 == C_MI_OUT) {
+      const Proc::Mi* m = P.mi_body(elem);
+      if (!m) return mi_fail(4);
+      const int64_t body_key = h->key_of(inst, aux_ord);
+      uint8_t intent = ZBHIP_VAR_CREATED;
+      if (fl & 0x80) {  // initializeOutputCollection: [nil] * n
+        auto& o = h->mi_out[body_key];
+        o.var_key = h->key_of(inst, key_ord);
+        o.items.assign(fl & 0x7F, {(uint8_t)ZBHIP_DOC_NIL, 0});
+      } else {  // updateOutputCollection: the item at index key_ord
+        auto f = h->mi_out.find(body_key);
+        const size_t slot = (fl >> 4) & 3, vat = slot * h->cfg.max_commands + c;
+        if (f == h->mi_out.end() || key_ord >= f->second.items.size() || c >= h->cfg.max_commands ||
+            vat >= h->h_map_val.size())
+          return mi_fail(5);
+        f->second.items[key_ord] = {(uint8_t)(fl & 7), (fl & 7) == ZBHIP_DOC_NIL ? 0 : (int64_t)h->h_map_val[vat]};
+        intent = ZBHIP_VAR_UPDATED;
+      }
+      const auto& o = h->mi_out[body_key];
+      const int64_t id = intern_items(h, o.items);
+      if (id < 0) return (int)id;
+      h->mi_rec[at] = {o.var_key, body_key, (int32_t)m->out_coll, intent, (uint8_t)ZBHIP_DOC_LIST, id};
+    } else if (c6 == C_MI_PROP) {  // propagateVariable: created in the process instance's scope
+      const Proc::Mi* m = P.mi_body(elem);
+      auto f = h->mi_out.find(h->key_of(inst, aux_ord));
+      if (!m || f == h->mi_out.end()) return mi_fail(6);
+      const int64_t id = intern_items(h, f->second.items);
+      if (id < 0) return (int)id;
+      const int64_t vk = h->key_of(inst, key_ord);
+      h->outlist_var[vk] = (uint32_t)id;
+      h->mi_rec[at] = {vk, h->key_of(inst, 0), (int32_t)m->out_coll, (uint8_t)ZBHIP_VAR_CREATED,
+                       (uint8_t)ZBHIP_DOC_LIST, id};
+    } else if ((c6 == ZBHIP_PI_ELEMENT_COMPLETED || c6 == ZBHIP_PI_ELEMENT_TERMINATED) && elem < P.els.size() &&
+               P.els[elem].element_type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      h->mi_out.erase(h->key_of(inst, key_ord));  // the body's variables leave with it
+    }
+  }
+  return ZBHIP_OK;
+}
+
 // Key relabelling bookkeeping of the last run, in log (source) order: each command's first key
 // (DbKeyGenerator order), the subjects' key histories and the resolve_key table.  It advances
 // lazily, command by command: up to `limit`, and never past a fallback command whose CPU-engine keys
@@ -2269,8 +2474,9 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
   if (h->fin_next == 0) {  // a new window: jobs completed in the previous one are gone
     for (int64_t k : h->completed_activated) h->activated.erase(k);
     h->completed_activated.clear();
+    h->mi_rec.clear();
   }
-  if (h->job_index_on || !h->activated.empty() || !h->streams.empty())
+  if (h->job_index_on || !h->activated.empty() || !h->streams.empty() || h->mi_ext)
     if (int rc = ensure_out(h)) return rc;
   const size_t subjects = (size_t)h->cfg.max_instances + h->st.n_slots;
   if (h->hist.size() < subjects) {
@@ -2280,7 +2486,7 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
   }
   const size_t n = std::min(limit, h->n_cmds);
   if (h->fin_next == 0 && n == h->n_cmds && !h->msg() && !h->job_index_on && h->activated.empty() &&
-      h->streams.empty() && n >= (1u << 16)) {
+      h->streams.empty() && !h->mi_ext && n >= (1u << 16)) {
     bool all_declared = true;  // the whole window can be done now (fallback keys declared, or forced)
     if (!force)
       for (size_t c = 0; c < n && all_declared; ++c)
@@ -2332,6 +2538,8 @@ static int advance(zbhip_handle* h, size_t limit, bool force) {
       h->batches.push_back({h->key_counter + 1, cm.instance, (uint16_t)first, (uint16_t)nkeys, h->inst_gen[cm.instance]});
     }
     if (h->job_index_on || !h->activated.empty() || !h->streams.empty()) track_jobs(h, c, cm.instance);
+    if (h->mi_ext)
+      if (int rc = track_mi(h, c, cm.instance)) return rc;
     if (hd.y & HDR_ENDED) {  // completed: its job keys no longer resolve
       ++h->inst_gen[cm.instance];
       h->batches_dead.fetch_add(h->hist[cm.instance].size(), std::memory_order_relaxed);
@@ -2374,13 +2582,14 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     h->guard_armed = false;
     if (flags & ZBHIP_RUN_NO_RESULTS) {
       // speculative: k_step runs guarded by the check's flag; resolve_guard reads it later
-      guard = h->d_check_flag;
+      guard = h->d_check_flag + 2;  // the guard word (k_subject_check's last workgroup writes it)
       h->guard_win.run_flags = flags;
       h->guard_pending = true;
     } else {
       // results are read back in this call anyway: decide now
-      HIPCHK(hipEventSynchronize(h->check_ev));
-      const uint32_t flag = *h->h_check_flag;
+      const int64_t fl = read_check_marker(h);
+      if (fl < 0) return (int)fl;
+      const uint32_t flag = (uint32_t)fl;
       if (flag) {
         const auto w = h->guard_win;
         h->next_doc_base = w.doc_base;
@@ -2439,6 +2648,12 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.map_cap = h->cfg.max_commands;
   P.cmd_act = h->st.act ? h->d_cmd_act : nullptr;
   P.guard = guard;
+  if (h->d_list_n != h->lists.size())
+    if (int rc = sync_lists(h)) return rc;
+  P.list_hdr = h->d_list_hdr;
+  P.list_val = h->d_list_val;
+  P.list_type = h->d_list_type;
+  P.n_lists = (uint32_t)h->d_list_n;
   h->run_clock_ms = h->clock_ms;
   if (!h->streams.empty() || !h->run_streams.empty()) h->run_streams = h->streams;  // (the pushes' deadlines / workers)
   P.tpl = (h->variant == 0 || h->variant == 1 || h->scope_variant()) && !getenv("ZBHIP_NO_TEMPLATES") ? h->d_tpl : nullptr;
@@ -2884,7 +3099,7 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       // MultiInstanceBodyProcessor.setLoopVariables: VARIABLE:CREATED in the inner instance's scope,
       // the value inline -- the body's item at loopCounter - 1, or loopCounter itself
       const Proc::Mi* m = proc != NONE ? h->procs[proc].mi_body(elem) : nullptr;
-      if (!m || fl < 1 || fl > m->items.size()) return ZBHIP_EDEVICE;
+      if (!m || fl < 1 || (c6 == C_MI_ITEM && fl > m->items.size())) return ZBHIP_EDEVICE;
       r.value_type = ZBHIP_VT_VARIABLE;
       r.intent = ZBHIP_VAR_CREATED;
       r.record_type = ZBHIP_RT_EVENT;
@@ -2892,6 +3107,23 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.aux = ZBHIP_AUX_INLINE;
       r.partition = c6 == C_MI_ITEM ? m->items[fl - 1].first : ZBHIP_DOC_INT;
       r.message_key = c6 == C_MI_ITEM ? m->items[fl - 1].second : (int64_t)fl;
+    } else if (c6 == C_MI_LIST_ITEM || c6 == C_MI_OUTEL || c6 == C_MI_OUT || c6 == C_MI_PROP) {
+      // multi-instance collection variables: their values from the log-order pass (track_mi)
+      auto it = h->mi_rec.find(((uint64_t)c << 16) | ord);
+      if (it == h->mi_rec.end()) {
+        if (getenv("ZBHIP_DEBUG_MI")) fprintf(stderr, "[expand] command %zu ordinal %u: no multi-instance record\n", c, ord);
+        return ZBHIP_EDEVICE;
+      }
+      const zbhip_handle::MiRec& m = it->second;
+      r.key = m.key;
+      r.scope_key = m.scope;
+      r.element_idx = m.name;
+      r.value_type = ZBHIP_VT_VARIABLE;
+      r.intent = m.intent;
+      r.record_type = ZBHIP_RT_EVENT;
+      r.aux = ZBHIP_AUX_INLINE;
+      r.partition = m.type;
+      r.message_key = m.value;
     } else if (c6 == C_VAR_MAPPED) {
       // BpmnVariableMappingBehavior (behavior/BpmnVariableMappingBehavior.java:53-156): the value the
       // mapping computed, inline (its zbhip_doc_type in flags bits 0..2, its map_val slot in bit 4)
@@ -2912,7 +3144,7 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.value_type = ZBHIP_VT_PROCESS_INSTANCE_BATCH;
       r.intent = ZBHIP_PIB_ACTIVATE;
       r.record_type = ZBHIP_RT_COMMAND;
-      r.partition = (int32_t)m->items.size();
+      r.partition = (int32_t)(fl & 0x3F);  // the collection's size (the row's flags)
       r.unprocessed = (fl & F_UNPROCESSED) ? 1 : 0;
       if (r.unprocessed && !h->cont_ids.empty()) {
         auto it = h->cont_ids.find(((uint64_t)c << 16) | ord);
@@ -3138,7 +3370,10 @@ int zbhip_drain_command(zbhip_handle* h, size_t i, zbhip_record* out, size_t cap
   *n_out = 0;
   if (!h->results) return ZBHIP_ESTATE;
   if (i >= h->n_cmds) return ZBHIP_EINVAL;
-  if (int rc = advance(h, i + 1, false)) return rc;
+  if (int rc = advance(h, i + 1, false)) {
+    if (getenv("ZBHIP_DEBUG_MI")) fprintf(stderr, "[drain_command] advance to %zu: %d\n", i + 1, rc);
+    return rc;
+  }
   if (h->fin_next <= i) return ZBHIP_ESTATE;
   if (int rc = ensure_out(h)) return rc;
   const uint32_t nrec = h->h_hdr[i].x & 0xFFFF;
@@ -3165,7 +3400,12 @@ int zbhip_drain_command(zbhip_handle* h, size_t i, zbhip_record* out, size_t cap
   }
   const uint2* rows = h->h_out.data() + h->h_off[i];
   for (uint32_t k = 0; k < nrec; ++k)
-    if (int rc = expand_plain(h, i, h->h_cmds[i].instance, rows[k], k, out[k])) return rc;
+    if (int rc = expand_plain(h, i, h->h_cmds[i].instance, rows[k], k, out[k])) {
+      if (getenv("ZBHIP_DEBUG_MI"))
+        fprintf(stderr, "[drain_command] command %zu row %u code %u flags %u elem %u: %d\n", i, k, (rows[k].y >> 16) & 0xFF,
+                rows[k].y >> 24, rows[k].y & 0xFFFF, rc);
+      return rc;
+    }
   *n_out = nrec;
   return ZBHIP_OK;
 }
@@ -3198,6 +3438,86 @@ int64_t zbhip_intern_string(zbhip_handle* h, const char* bytes, size_t len) {
   h->strs.push_back(std::move(v));
   h->str_ids.emplace(h->strs.back(), id);
   return id;
+}
+
+static int64_t intern_items(zbhip_handle* h, const zbhip_handle::Items& v) {
+  auto it = h->list_ids.find(v);
+  if (it != h->list_ids.end()) return it->second;
+  if (h->lists.size() >= 0x7FFFFFF0u) return ZBHIP_ENOMEM;
+  const uint32_t id = (uint32_t)h->lists.size();
+  h->list_hdr.push_back(make_uint2((uint32_t)h->list_val.size(), (uint32_t)v.size()));
+  std::vector<zbhip_doc_entry> rows(v.size());
+  for (size_t i = 0; i < v.size(); ++i) {
+    h->list_val.push_back(v[i].second);
+    h->list_type.push_back(v[i].first);
+    rows[i] = zbhip_doc_entry{};
+    rows[i].type = v[i].first;
+    rows[i].value = v[i].second;
+  }
+  if (h->ser) zbhip_serializer_intern_list(h->ser, rows.data(), rows.size());
+  h->lists.push_back(v);
+  h->list_ids.emplace(v, id);
+  return id;
+}
+
+extern "C" int64_t zbhip_intern_list(zbhip_handle* h, const zbhip_doc_entry* items, size_t n) {
+  if (!h || (n && !items)) return ZBHIP_EINVAL;
+  zbhip_handle::Items v;
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t t = items[i].type;
+    if (t != ZBHIP_DOC_NIL && t != ZBHIP_DOC_BOOL && t != ZBHIP_DOC_INT && t != ZBHIP_DOC_DEC && t != ZBHIP_DOC_STR)
+      return ZBHIP_EUNSUPP;  // nested lists / documents
+    if (t == ZBHIP_DOC_STR && (items[i].value < 0 || (size_t)items[i].value >= h->strs.size())) return ZBHIP_EINVAL;
+    v.push_back({t, t == ZBHIP_DOC_NIL ? 0 : items[i].value});
+  }
+  return intern_items(h, v);
+}
+
+extern "C" int zbhip_list_items(zbhip_handle* h, int64_t id, zbhip_doc_entry* out, size_t cap, size_t* n_out) {
+  if (!h || !n_out || (cap && !out)) return ZBHIP_EINVAL;
+  if (id < 0 || (size_t)id >= h->lists.size()) return ZBHIP_EINVAL;
+  const auto& v = h->lists[(size_t)id];
+  *n_out = v.size();
+  for (size_t i = 0; i < v.size() && i < cap; ++i) {
+    out[i] = zbhip_doc_entry{};
+    out[i].type = v[i].first;
+    out[i].value = v[i].second;
+  }
+  return ZBHIP_OK;
+}
+
+// uploads the lists interned since the last run (their headers and items)
+static int sync_lists(zbhip_handle* h) {
+  if (h->d_list_n == h->lists.size()) return ZBHIP_OK;
+  if (h->lists.size() > h->d_list_cap || h->list_val.size() > h->d_litem_cap) {
+    const size_t lc = std::max<size_t>(1024, h->lists.size() * 2), ic = std::max<size_t>(4096, h->list_val.size() * 2);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    (void)hipFree(h->d_list_hdr);
+    (void)hipFree(h->d_list_val);
+    (void)hipFree(h->d_list_type);
+    h->d_list_hdr = nullptr;
+    h->d_list_val = nullptr;
+    h->d_list_type = nullptr;
+    if (dalloc(&h->d_list_hdr, lc) != hipSuccess || dalloc(&h->d_list_val, ic) != hipSuccess ||
+        dalloc(&h->d_list_type, ic) != hipSuccess)
+      return ZBHIP_ENOMEM;
+    h->d_list_cap = lc;
+    h->d_litem_cap = ic;
+    h->d_list_n = h->d_list_items = 0;
+  }
+  HIPCHK(hipMemcpyAsync(h->d_list_hdr + h->d_list_n, h->list_hdr.data() + h->d_list_n,
+                        (h->lists.size() - h->d_list_n) * sizeof(uint2), hipMemcpyHostToDevice, h->stream));
+  const size_t ni = h->list_val.size() - h->d_list_items;
+  if (ni) {
+    HIPCHK(hipMemcpyAsync(h->d_list_val + h->d_list_items, h->list_val.data() + h->d_list_items, ni * sizeof(long long),
+                          hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d_list_type + h->d_list_items, h->list_type.data() + h->d_list_items, ni,
+                          hipMemcpyHostToDevice, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));  // (the host vectors may grow before the next run)
+  h->d_list_n = h->lists.size();
+  h->d_list_items = h->list_val.size();
+  return ZBHIP_OK;
 }
 
 int zbhip_intern_strings(zbhip_handle* h, const char* bytes, const uint64_t* offsets, size_t n, uint32_t* ids_out) {
@@ -3436,6 +3756,38 @@ static void emit_pms(zbhip_handle* h, uint32_t inst, const InstRows& R, const Pr
   }
 }
 
+// a list's items in a state row: "type:value;..." (the oracle's format, zb_oracle.cpp list_text)
+static std::string list_text(const zbhip_handle::Items& items) {
+  std::string o;
+  for (size_t i = 0; i < items.size(); ++i) {
+    if (i) o += ';';
+    o += std::to_string((int)items[i].first) + ":" + std::to_string((long long)items[i].second);
+  }
+  return o;
+}
+
+// a multi-instance body's collection as the instance holds it: the static items, or the list variable
+// (seen from the body: its containers' scopes, then the process instance's; nullptr: none)
+static const zbhip_handle::Items* mi_items_of(const zbhip_handle* h, const Proc& P, const Proc::Mi& m, const InstRows& R,
+                                              uint32_t inst) {
+  (void)inst;
+  if (m.coll_name == NONE) return &m.items;
+  const uint32_t nslots = (R.hdr.y >> 8) & 0xFF, nvars = (R.hdr.y >> 16) & 0xFF;
+  std::vector<uint32_t> chain;  // the scope ordinals from the body's container up, then the process (0)
+  for (uint32_t c = P.els[m.body].flow_scope, d = 0; c != 0 && c < P.els.size() && d < 16; c = P.els[c].flow_scope, ++d)
+    for (uint32_t s = 0; s < nslots && s < (uint32_t)kSlots; ++s)
+      if ((R.slots[s].x & 0xFFFF) == c) chain.push_back(R.slots[s].x >> 16);
+  chain.push_back(0);
+  for (uint32_t sc : chain)
+    for (uint32_t v = 0; v < nvars && v < (uint32_t)kVars; ++v)
+      if ((R.vm[v].x & 0xFFFF) == m.coll_name && (R.vm[v].x >> 16) == sc) {
+        if (((R.vm[v].y >> 16) & 0xFF) != ZBHIP_DOC_LIST || R.vv[v] < 0 || (size_t)R.vv[v] >= h->lists.size())
+          return nullptr;
+        return &h->lists[(size_t)R.vv[v]];
+      }
+  return nullptr;
+}
+
 // the rows of one process instance (ELEMENT_INSTANCE_KEY ... NUMBER_OF_TAKEN_SEQUENCE_FLOWS,
 // PROCESS_SUBSCRIPTION_BY_KEY); nothing for a free slot
 static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbhip_state_sink sink, void* ctx) {
@@ -3498,18 +3850,36 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
              k, fs, child, body ? loop : 0u, body ? loop - child : 0u, jk, loop, state, P.id(elem).c_str(),
              E.element_type, E.event_type, fs, pik, (long long)P.def_key, sub ? (job >> 8) & 0xFF : 0u);
     sink(ctx, buf);
-    if (im && loop >= 1 && loop <= im->items.size() && (jw ? job_row : job != JOB_ZERO)) {
+    const zbhip_handle::Items* coll = im ? mi_items_of(h, P, *im, R, inst) : nullptr;
+    if (im && coll && loop >= 1 && loop <= coll->size() && (jw ? job_row : job != JOB_ZERO)) {
       // the inner instance's loop variables (setLoopVariables): keys right before its job's (a job
-      // worker) or the loopCounter key in its job field (an undefined task), values from the program
+      // worker) or the loopCounter key in its job field (an undefined task) -- the inputElement, the
+      // local outputElement (nil: a job's document updates it only in the batch that completes the
+      // instance), the loopCounter -- values from the collection
       const uint32_t kl = jw ? job - 1 : job;
+      const uint32_t ko = im->out_local() ? 1u : 0u;
       if (im->input_name != NONE) {
         snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%lld", k, h->names[im->input_name].c_str(),
-                 h->key_of(inst, kl - 1), (unsigned)im->items[loop - 1].first, (long long)im->items[loop - 1].second);
+                 h->key_of(inst, kl - 1 - ko), (unsigned)(*coll)[loop - 1].first, (long long)(*coll)[loop - 1].second);
+        sink(ctx, buf);
+      }
+      if (ko) {
+        snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=0", k, h->names[im->out_elem].c_str(),
+                 h->key_of(inst, kl - 1), (unsigned)ZBHIP_DOC_NIL);
         sink(ctx, buf);
       }
       snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%u", k, h->names[im->loop_name].c_str(),
                h->key_of(inst, kl), (unsigned)ZBHIP_DOC_INT, loop);
       sink(ctx, buf);
+    }
+    if (body && P.mi_body(elem) && P.mi_body(elem)->out_coll != NONE) {
+      // the body's local outputCollection (initializeOutputCollection / updateOutputCollection): the host's
+      const auto o = h->mi_out.find(k);
+      if (o != h->mi_out.end()) {
+        snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=", k,
+                 h->names[P.mi_body(elem)->out_coll].c_str(), (long long)o->second.var_key, (unsigned)ZBHIP_DOC_LIST);
+        sink(ctx, (std::string(buf) + list_text(o->second.items)).c_str());
+      }
     }
     snprintf(buf, sizeof buf, "ELEMENT_INSTANCE_PARENT_CHILD|%lld|%lld", fs, k);
     sink(ctx, buf);
@@ -3584,9 +3954,19 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
   }
   for (uint32_t v = 0; v < nvars; ++v) {
     const uint2 m = R.vm[v];
-    const uint32_t scope = m.x >> 16;
+    const uint32_t scope = m.x >> 16, type = (m.y >> 16) & 0xFF;
+    const long long vk = h->key_of(inst, m.y & 0xFFFF);
+    if (type == ZBHIP_DOC_LIST || type == kDocOutList) {  // a list: its items in the row
+      const auto ov = type == kDocOutList ? h->outlist_var.find(vk) : h->outlist_var.end();
+      const long long id = type == kDocOutList ? (ov == h->outlist_var.end() ? -1 : (long long)ov->second) : R.vv[v];
+      if (id < 0 || (size_t)id >= h->lists.size()) continue;
+      snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=", h->key_of(inst, scope),
+               h->names[m.x & 0xFFFF].c_str(), vk, (unsigned)ZBHIP_DOC_LIST);
+      sink(ctx, (std::string(buf) + list_text(h->lists[(size_t)id])).c_str());
+      continue;
+    }
     snprintf(buf, sizeof buf, "VARIABLES|%lld|%s|key=%lld,type=%u,value=%lld", h->key_of(inst, scope),
-             h->names[m.x & 0xFFFF].c_str(), h->key_of(inst, m.y & 0xFFFF), (m.y >> 16) & 0xFF, R.vv[v]);
+             h->names[m.x & 0xFFFF].c_str(), vk, type, R.vv[v]);
     sink(ctx, buf);
   }
   if (R.tmr.y >> 31) {  // TIMERS [eik, timerKey] -> TimerInstance, TIMER_DUE_DATES [dueDate, eik, timerKey] (DbTimerInstanceState)
@@ -3940,7 +4320,20 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       els[e.key] = e;
     } else if (cf == "VARIABLES" && p.size() >= 4) {
       auto f = row_fields(p[3]);
-      vars.push_back({to_ll(p[1]), to_ll(f["key"]), to_ll(f["value"]), p[2], (uint32_t)to_ll(f["type"])});
+      const uint32_t type = (uint32_t)to_ll(f["type"]);
+      int64_t value = to_ll(f["value"]);
+      if (type == ZBHIP_DOC_LIST) {  // a list: its items in the row
+        zbhip_handle::Items items;
+        for (const std::string& it : split_row(f["value"], ';')) {
+          if (it.empty()) continue;
+          const size_t c = it.find(':');
+          if (c == std::string::npos) return ZBHIP_EINVAL;
+          items.push_back({(uint8_t)to_ll(it.substr(0, c)), to_ll(it.substr(c + 1))});
+        }
+        value = intern_items(h, items);
+        if (value < 0) return (int)value;
+      }
+      vars.push_back({to_ll(p[1]), to_ll(f["key"]), value, p[2], type});
     } else if (cf == "NUMBER_OF_TAKEN_SEQUENCE_FLOWS" && p.size() >= 5) {
       taken.emplace_back(to_ll(p[1]), p[2], p[3], (uint32_t)to_ll(p[4]));
     } else if (cf == "JOBS" && p.size() >= 3) {
@@ -4069,10 +4462,21 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     std::vector<const ImpVar*> ivars;
     auto scope_of = [&](int64_t s) { return s == pe.key || std::any_of(children.begin(), children.end(), [&](const ImpElement* c) { return c->key == s; }); };
     // a multi-instance inner instance's own variables: its loop variables, derived from its slot on
-    // the device (checked against the program below); their keys take ordinals like any other
+    // the device (checked against the program below); their keys take ordinals like any other.  A
+    // body's local outputCollection is the host's (mi_out)
     std::map<int64_t, std::map<std::string, const ImpVar*>> loop_vars;
+    std::vector<std::pair<int64_t, const ImpVar*>> out_colls;
     for (const auto& v : vars)
       if (scope_of(v.scope)) {
+        if (subs.count(v.scope) && els[v.scope].type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+          const int be = elem_of_id(els[v.scope].id, ZBHIP_EL_MULTI_INSTANCE_BODY);
+          const Proc::Mi* bm = be < 0 ? nullptr : P.mi_body((uint32_t)be);
+          if (!bm || bm->out_coll == NONE || h->names[bm->out_coll] != v.name || v.type != ZBHIP_DOC_LIST)
+            return ZBHIP_EUNSUPP;
+          keys.push_back(v.key);
+          out_colls.push_back({v.scope, &v});
+          continue;
+        }
         // container-local variables: written by a sub-process's input mapping (KScopeIO) only
         if (subs.count(v.scope) && (!P.has_io || els[v.scope].type != ZBHIP_EL_SUB_PROCESS)) return ZBHIP_EUNSUPP;
         keys.push_back(v.key);
@@ -4124,6 +4528,10 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       // (flag bit 1: a stored activation -- ACTIVATED, or timed out with its deadline and worker kept)
       const auto ja = job_act.find(e.job);
       const auto jmf = job_meta.find(e.job);
+      // a failure that left errorMessage, retryBackoff and recurringTime at their defaults shows in its
+      // retries alone
+      if (jmf != job_meta.end() && !sub_el && !body && jmf->second.retries != (int32_t)P.els[el].job_retries)
+        jmf->second.failed_fields = true;
       const bool stored = job_activated_state.count(e.job) ||
                           (ja != job_act.end() && (ja->second.first != -1 || !ja->second.second.empty())) ||
                           (jmf != job_meta.end() && jmf->second.failed_fields);
@@ -4134,18 +4542,33 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       }
       if (const Proc::Mi* m = P.mi_inner((uint32_t)el)) {
         // the loop counter in the flags; its loop variables exactly what setLoopVariables wrote,
-        // keyed right below the job's key (a job worker) or kept in the job field (an undefined task)
-        if (e.loop < 1 || e.loop > (int64_t)m->items.size()) return ZBHIP_EUNSUPP;
+        // keyed right below the job's key (a job worker) or kept in the job field (an undefined task);
+        // the items: the static ones or the imported collection variable's (the process instance's)
+        const zbhip_handle::Items* coll = &m->items;
+        if (m->coll_name != NONE) {
+          coll = nullptr;
+          for (const auto& v : vars)
+            if (v.scope == pe.key && v.name == h->names[m->coll_name] && v.type == ZBHIP_DOC_LIST)
+              coll = &h->lists[(size_t)v.value];
+          if (!coll) return ZBHIP_EUNSUPP;
+        }
+        if (e.loop < 1 || e.loop > (int64_t)coll->size()) return ZBHIP_EUNSUPP;
+        const uint32_t ko = m->out_local() ? 1u : 0u;
         const auto lv = loop_vars.find(e.key);
-        if (lv == loop_vars.end() || lv->second.size() != (m->input_name != NONE ? 2u : 1u)) return ZBHIP_EUNSUPP;
+        if (lv == loop_vars.end() || lv->second.size() != (m->input_name != NONE ? 2u : 1u) + ko) return ZBHIP_EUNSUPP;
         const auto li = lv->second.find(h->names[m->loop_name]);
         if (li == lv->second.end() || li->second->type != ZBHIP_DOC_INT || li->second->value != e.loop) return ZBHIP_EUNSUPP;
         const uint32_t kl = ord(li->second->key);
+        if (ko) {  // the local outputElement: nil until the batch that completes the instance
+          const auto oi = lv->second.find(h->names[m->out_elem]);
+          if (oi == lv->second.end() || oi->second->type != ZBHIP_DOC_NIL || ord(oi->second->key) + 1 != kl)
+            return ZBHIP_EUNSUPP;
+        }
         if (m->input_name != NONE) {
           const auto ii = lv->second.find(h->names[m->input_name]);
-          const auto& item = m->items[(size_t)e.loop - 1];
+          const auto& item = (*coll)[(size_t)e.loop - 1];
           if (ii == lv->second.end() || ii->second->type != item.first || ii->second->value != item.second ||
-              ord(ii->second->key) + 1 != kl)
+              ord(ii->second->key) + 1 + ko != kl)
             return ZBHIP_EUNSUPP;
         }
         if (ZBHIP_IS_JOB_WORKER(e.type) ? !(row & 1) || job != kl + 1 : e.job != 0) return ZBHIP_EUNSUPP;
@@ -4204,6 +4627,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     hdr[inst] = make_uint4((uint32_t)proc | ((uint32_t)keys.size() << 16),
                            pe.state | ((uint32_t)children.size() << 8) | ((uint32_t)ivars.size() << 16) | (1u << 24),
                            (uint32_t)pe.child_count | ((uint32_t)pe.asf << 16), 0);
+    for (const auto& [body_key, v] : out_colls) h->mi_out[body_key] = {v->key, h->lists[(size_t)v->value]};
     done.push_back({inst, std::move(keys)});
   }
   HIPCHK(hipMemcpy(h->st.hdr, hdr.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
@@ -4429,20 +4853,45 @@ static void collect_job_variables(zbhip_handle* h, const uint4& a, const uint2* 
   std::vector<uint32_t> taken;
   const Proc::Mi* m = proc < h->procs.size() ? h->procs[proc].mi_inner(elem) : nullptr;
   const uint32_t loop = a.w >> 26;
-  if (m && loop >= 1 && loop <= m->items.size()) {
-    // a multi-instance inner instance's scope: its loop variables (setLoopVariables), then the
-    // body's (none), then the process instance's
+  // the collection the inner instance's item comes from: the static items or the list variable's
+  const zbhip_handle::Items* coll = m ? &m->items : nullptr;
+  if (m && m->coll_name != NONE) {
+    coll = nullptr;
+    for (uint32_t v = 0; v < nv; ++v)
+      if ((meta[v].x & 0xFFFF) == m->coll_name && ((meta[v].y >> 16) & 0xFF) == ZBHIP_DOC_LIST && val[v] >= 0 &&
+          (size_t)val[v] < h->lists.size())
+        coll = &h->lists[(size_t)val[v]];
+  }
+  if (m && coll && loop >= 1 && loop <= coll->size()) {
+    // a multi-instance inner instance's scope: its loop variables (setLoopVariables: the inputElement,
+    // the local outputElement -- nil --, the loopCounter), then the body's (its outputCollection),
+    // then the process instance's
     std::vector<zbhip_doc_entry> local;
     if (m->input_name != NONE)
-      local.push_back({m->input_name, m->items[loop - 1].first, {0, 0, 0}, m->items[loop - 1].second});
+      local.push_back({m->input_name, (*coll)[loop - 1].first, {0, 0, 0}, (*coll)[loop - 1].second});
+    if (m->out_local()) local.push_back({m->out_elem, (uint8_t)ZBHIP_DOC_NIL, {0, 0, 0}, 0});
     local.push_back({m->loop_name, (uint8_t)ZBHIP_DOC_INT, {0, 0, 0}, (int64_t)loop});
     std::sort(local.begin(), local.end(),
               [&](const zbhip_doc_entry& p, const zbhip_doc_entry& q) { return name_less(p.name_id, q.name_id); });
     for (const zbhip_doc_entry& d : local) {
       if (!requested.empty() && std::find(requested.begin(), requested.end(), d.name_id) == requested.end()) continue;
+      if (j.n_variables >= 6) break;
       taken.push_back(d.name_id);
       j.variables[j.n_variables++] = d;
     }
+    // the body's local outputCollection (the host's copy)
+    if (m->out_coll != NONE && j.n_variables < 6 &&
+        (requested.empty() || std::find(requested.begin(), requested.end(), m->out_coll) != requested.end()))
+      for (uint32_t s = 0; s < (uint32_t)kSlots; ++s)
+        if (slots[s].x != 0xFFFFFFFFu && (slots[s].x & 0xFFFF) == m->body) {
+          const auto o = h->mi_out.find(h->key_of(j.instance, slots[s].x >> 16));
+          if (o == h->mi_out.end()) break;
+          const int64_t id = intern_items(h, o->second.items);
+          if (id < 0) break;
+          taken.push_back(m->out_coll);
+          j.variables[j.n_variables++] = {m->out_coll, (uint8_t)ZBHIP_DOC_LIST, {0, 0, 0}, id};
+          break;
+        }
   }
   // the element's scope, the instances of its enclosing containers (sub-processes with io-mapped
   // variables), then the process instance's
@@ -4463,11 +4912,17 @@ static void collect_job_variables(zbhip_handle* h, const uint4& a, const uint2* 
       const uint32_t name = meta[v].x & 0xFFFF;
       if (std::find(taken.begin(), taken.end(), name) != taken.end()) continue;
       if (!requested.empty() && std::find(requested.begin(), requested.end(), name) == requested.end()) continue;
+      if (j.n_variables >= 6) break;
       taken.push_back(name);
       zbhip_doc_entry& d = j.variables[j.n_variables++];
       d.name_id = name;
       d.type = (uint8_t)((meta[v].y >> 16) & 0xFF);
       d.value = val[v];
+      if (d.type == kDocOutList) {  // a propagated outputCollection: the host's list
+        const auto ov = h->outlist_var.find(h->key_of(j.instance, meta[v].y & 0xFFFF));
+        d.type = ZBHIP_DOC_LIST;
+        d.value = ov == h->outlist_var.end() ? 0 : ov->second;
+      }
     }
   }
 }
@@ -4587,6 +5042,25 @@ extern "C" int zbhip_activate_jobs(zbhip_handle* h, const zbhip_job_activation* 
     act.proc = j.process_idx;
     act.elem = j.element_idx;
   }
+  return ZBHIP_OK;
+}
+
+// JOB_ACTIVATABLE of one type over the device's jobs, in key order (the host's job index)
+extern "C" int zbhip_activatable_jobs(zbhip_handle* h, const char* type, size_t type_len, int64_t* keys, size_t cap,
+                                      size_t* n_out) {
+  if (!h || !n_out || (type_len && !type) || (cap && !keys)) return ZBHIP_EINVAL;
+  *n_out = 0;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  if (!h->job_index_on)
+    if (int rc = build_job_index(h)) return rc;
+  const auto tit = h->job_type_ids.find(std::string(type ? type : "", type_len));
+  if (tit == h->job_type_ids.end()) return ZBHIP_OK;
+  size_t n = 0;
+  for (auto it = h->job_index.lower_bound({tit->second, INT64_MIN});
+       it != h->job_index.end() && it->first.first == tit->second && n < cap; ++it)
+    keys[n++] = it->first.second;
+  *n_out = n;
   return ZBHIP_OK;
 }
 

@@ -80,7 +80,8 @@ enum : uint8_t {
   C_MI_ITEM = 22,         // VARIABLE:CREATED of a multi-instance inner instance's inputElement / its
   C_MI_LOOP = 23,         // loopCounter (MultiInstanceBodyProcessor.setLoopVariables): key = the variable,
                           // aux = the inner instance, elem = the body, flags = the loop counter
-  C_PIB_ACTIVATE = 26,    // PROCESS_INSTANCE_BATCH:ACTIVATE (command): aux = the body, elem = the body
+  C_PIB_ACTIVATE = 26,    // PROCESS_INSTANCE_BATCH:ACTIVATE (command): aux = the body, elem = the body,
+                          // flags = the collection's size (the record's index) | F_UNPROCESSED
   C_PE_TRIGGERING = 24,
   C_PE_TRIGGERED = 25,    // EventTriggerBehavior.processEventTriggered
   C_PIC_CREATED = 28,
@@ -109,6 +110,18 @@ enum : uint8_t {
   C_TIMER_NEXT = 56,
   C_JOB_PUSHED = 59,      // JOB_BATCH:ACTIVATED of a job stream's push (BpmnJobActivationBehavior.publishWork):
                           // key = the batch, aux = the job, elem = the task
+  // multi-instance collections (MultiInstanceBodyProcessor / MultiInstanceOutputCollectionBehavior); the
+  // host completes their values from the drained rows in log order (runtime.cpp track_mi)
+  C_MI_LIST_ITEM = 60,    // VARIABLE:CREATED of the inputElement from a list variable: key = the variable,
+                          // aux / elem = the list id's low / high half (scope, body and loop counter: the
+                          // C_MI_LOOP row that follows)
+  C_MI_OUTEL = 61,        // VARIABLE:CREATED nil of the outputElement variable (setLoopVariables): key = the
+                          // variable, aux = the inner instance, elem = the body
+  C_MI_OUT = 62,          // the body's outputCollection: aux = the body instance, elem = the body; flags bit 7
+                          // set: CREATED [nil] * (flags & 0x7F), key = the variable; else UPDATED at index
+                          // key of the item (zbhip_doc_type flags & 7, value in map_val slot flags >> 4 & 3)
+  C_MI_PROP = 63,         // propagateVariable of the outputCollection: VARIABLE:CREATED in the process scope,
+                          // key = the variable, aux = the body instance, elem = the body
   C_VAR_MAPPED = 58,       // VARIABLE:CREATED / UPDATED of an io mapping (BpmnVariableMappingBehavior): key =
                            // the variable, aux = its scope, elem = its name, flags = zbhip_doc_type | updated
                            // << 3 | value slot << 4 (the value in StepParams.map_val)
@@ -291,8 +304,17 @@ struct StepParams {
                               // entry (x bit 31 clear: none found)
   const uint32_t* guard;      // an untrusted device window's subject-check flag (k_subject_check): nonzero
                               // -> the launch does nothing (the host replans the window); null: no guard
+  // the list dictionary (ZBHIP_DOC_LIST values): per list its first item and count, the items' values
+  // and zbhip_doc_types
+  const uint2* list_hdr;
+  const long long* list_val;
+  const uint8_t* list_type;
+  uint32_t n_lists;
 };
 constexpr int kMapVals = 2;   // io-mapped VARIABLE records per batch (more: FB_VARS)
+// a variable holding a propagated multi-instance outputCollection: its items on the host
+// (zbhip_handle::outlist_var, by the variable's key); never a document entry's type
+constexpr uint8_t kDocOutList = 7;
 
 // ---- log bytes on the device (logdev.hip) ----
 // entry templates of the device log writer (logwriter.cpp log_device_templates): PROCESS_INSTANCE

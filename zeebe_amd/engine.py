@@ -370,6 +370,29 @@ class Partition:
         check(self.L.zbhip_activate_jobs(self.h, C.byref(cmd), out.ctypes.data, cap, C.byref(res)), "zbhip_activate_jobs")
         return res.key, out[: res.n_jobs], res.reason
 
+    def activatable_jobs(self, job_type, cap=1 << 16):
+        """The device's JOB_ACTIVATABLE keys of `job_type` in key order (zbhip_activatable_jobs)."""
+        t = job_type.encode()
+        keys = np.zeros(max(cap, 1), dtype=np.int64)
+        n = C.c_size_t()
+        check(self.L.zbhip_activatable_jobs(self.h, t, len(t), keys.ctypes.data, cap, C.byref(n)), "zbhip_activatable_jobs")
+        return [int(k) for k in keys[: n.value]]
+
+    def intern_list(self, items):
+        """A list value [(zbhip_doc_type, value)] into the list dictionary (zbhip_intern_list): its id."""
+        d = abi.make_docs(max(len(items), 1))
+        for j, (t, v) in enumerate(items):
+            d[j]["type"], d[j]["value"] = t, v
+        return check(self.L.zbhip_intern_list(self.h, d.ctypes.data, len(items)), "zbhip_intern_list")
+
+    def list_items(self, list_id):
+        """The items [(zbhip_doc_type, value)] of list `list_id` (zbhip_list_items)."""
+        n = C.c_size_t()
+        check(self.L.zbhip_list_items(self.h, int(list_id), None, 0, C.byref(n)), "zbhip_list_items")
+        out = abi.make_docs(max(n.value, 1))
+        check(self.L.zbhip_list_items(self.h, int(list_id), out.ctypes.data, n.value, C.byref(n)), "zbhip_list_items")
+        return [(int(x["type"]), int(x["value"])) for x in out[: n.value]]
+
     def job_variables(self, job_keys, variables=()):
         """The pushed jobs' ActivatedJob rows (zbhip_job_variables: activation + variables document)."""
         keys = np.asarray(job_keys, dtype=np.int64)

@@ -29,12 +29,12 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream",
            "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
            "zbhip_set_external_keys", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
-           "zbhip_import_state", "zbhip_activate_jobs", "zbhip_job_batch_rejection_reason",
+           "zbhip_import_state", "zbhip_activate_jobs", "zbhip_activatable_jobs", "zbhip_job_batch_rejection_reason",
            "zbhip_serialize_log_device", "zbhip_log_device_copy", "zbhip_continuations",
            "zbhip_pending_continuations", "zbhip_current_key", "zbhip_set_key_if_higher",
            "zbhip_select_instances_db", "zbhip_drain_command", "zbhip_outbox_command", "zbhip_due_timers",
            "zbhip_timed_out_jobs", "zbhip_time_out_job", "zbhip_fail_job", "zbhip_job_state", "zbhip_set_job_stream",
-           "zbhip_job_variables"]
+           "zbhip_job_variables", "zbhip_intern_list", "zbhip_list_items", "zbhip_serializer_intern_list"]
 
 
 class ZbhipError(RuntimeError):
@@ -117,6 +117,7 @@ def load():
     L.zbhip_import_state_db.argtypes = [vp, C.c_char_p, sz, u32, C.POINTER(u32)]
     L.zbhip_import_state.argtypes = [vp, C.c_char_p, sz, u32, C.POINTER(u32)]
     L.zbhip_activate_jobs.argtypes = [vp, C.POINTER(abi.JobActivation), vp, sz, C.POINTER(abi.JobBatch)]
+    L.zbhip_activatable_jobs.argtypes = [vp, C.c_char_p, sz, vp, sz, C.POINTER(sz)]
     L.zbhip_job_batch_rejection_reason.argtypes = [C.POINTER(abi.JobActivation), C.POINTER(abi.JobBatch), C.c_char_p, sz]
     L.zbhip_due_timers.argtypes = [vp, i64, vp, sz, C.POINTER(sz), C.POINTER(i64)]
     L.zbhip_timed_out_jobs.argtypes = [vp, i64, vp, sz, C.POINTER(sz)]
@@ -125,6 +126,9 @@ def load():
     L.zbhip_fail_job.argtypes = [vp, C.POINTER(abi.JobFail), vp, sz, C.POINTER(sz)]
     L.zbhip_job_state.argtypes = [vp, i64]
     L.zbhip_job_variables.argtypes = [vp, vp, sz, vp, sz, vp]
+    L.zbhip_intern_list.restype = i64
+    L.zbhip_intern_list.argtypes = [vp, vp, sz]
+    L.zbhip_list_items.argtypes = [vp, i64, vp, sz, C.POINTER(sz)]
     L.zbhip_stream.argtypes = [vp]
     L.zbhip_stream.restype = vp
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
