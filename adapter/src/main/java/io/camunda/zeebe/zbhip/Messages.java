@@ -212,7 +212,10 @@ final class Messages {
     if (intent == MessageSubscriptionIntent.CREATED) {
       subscriptions.put(k, correlationSlot);
     } else if (intent == MessageSubscriptionIntent.CORRELATED || intent == MessageSubscriptionIntent.DELETED) {
-      subscriptions.remove(k);
+      // (a non-interrupting subscription stays open after its correlation: updateToCorrelatedState)
+      if (intent == MessageSubscriptionIntent.DELETED || v.isInterrupting()) {
+        subscriptions.remove(k);
+      }
       pendingMessage.remove(k);
     } else if (intent == MessageSubscriptionIntent.CORRELATING) {  // updateToCorrelatingState
       final PendingSubscription ps = pendingMessage.computeIfAbsent(k, x -> new PendingSubscription());
@@ -243,7 +246,10 @@ final class Messages {
     } else if (intent == ProcessMessageSubscriptionIntent.CREATED) {
       pendingProcess.remove(k);  // updateToOpenedState
     } else if (intent == ProcessMessageSubscriptionIntent.CORRELATED || intent == ProcessMessageSubscriptionIntent.DELETED) {
-      handles.remove(k);
+      // (a non-interrupting subscription stays open after its correlation: updateToOpenedState)
+      if (intent == ProcessMessageSubscriptionIntent.DELETED || v.isInterrupting()) {
+        handles.remove(k);
+      }
       pendingProcess.remove(k);
       if (intent == ProcessMessageSubscriptionIntent.DELETED) {
         closingSlots.remove(slot);

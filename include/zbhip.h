@@ -421,12 +421,16 @@ int zbhip_submit(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbh
 /* Same, with the window's received cross-partition commands (referenced by doc_begin). */
 int zbhip_submit_ex(zbhip_handle* h, const zbhip_command* cmds, size_t n, const zbhip_doc_entry* docs,
                     size_t n_docs, const zbhip_xpart_cmd* xparts, size_t n_xparts);
-/* Same, from device-resident arrays already in HBM (no copy; must stay valid until run returns).
- * The window's subjects are checked on the device (one small kernel and a host wait): a window that
- * addresses a subject (instance slot / correlation slot) more than once is copied to the host and
- * planned into rounds like a host window; a subject out of range returns ZBHIP_EINVAL.  Handles
- * opened with ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS skip the check: the caller then guarantees one
- * command per subject (the benchmark's windows, by construction). */
+/* Same, from device-resident arrays already in HBM (no copy; they must stay valid until the next
+ * submit, or until zbhip_run returns for a run that reads results back).  The window's subjects are
+ * checked on the device (k_subject_check): a window that addresses a subject (instance slot /
+ * correlation slot) more than once is copied to the host and planned into rounds like a host window;
+ * a subject out of range refuses the window (ZBHIP_EINVAL).  On a partition without messages the check
+ * is speculative -- no host wait: a ZBHIP_RUN_NO_RESULTS run launches k_step guarded by the device's
+ * verdict, and the next submit (or advance / stats call) reads it and replays a refused window before
+ * anything else, reporting ZBHIP_EINVAL there for a subject out of range.  Handles opened with
+ * ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS skip the check: the caller then guarantees one command per
+ * subject (the benchmark's windows, by construction). */
 int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,
                         const zbhip_doc_entry* dev_docs, size_t n_docs);
 int zbhip_submit_device_ex(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n,

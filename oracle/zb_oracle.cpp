@@ -753,14 +753,14 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_TIMER;
     } else if (n == "boundaryEvent" && k->child("messageEventDefinition")) {
-      // an interrupting message boundary event (BoundaryEventTransformer, CatchEventTransformer
+      // a message boundary event, interrupting or not (BoundaryEventTransformer, CatchEventTransformer
       // .transformMessageEventDefinition): static name, `= variable` correlation key -- evaluated in the
       // activity's flow scope (CatchEventBehavior.evaluateCorrelationKey, common/CatchEventBehavior.java:187-205)
       e.type = ZBHIP_EL_BOUNDARY_EVENT;
       e.interrupting = k->attr("cancelActivity") != "false";
       if (k->child("timerEventDefinition") || k->child("errorEventDefinition") || k->child("signalEventDefinition") ||
-          k->child("escalationEventDefinition") || k->child("conditionalEventDefinition") || !e.interrupting) {
-        err = "message boundary event outside the supported subset (interrupting only)";
+          k->child("escalationEventDefinition") || k->child("conditionalEventDefinition")) {
+        err = "message boundary event outside the supported subset";
         return false;
       }
       auto mi = msgs.find(k->child("messageEventDefinition")->attr("messageRef"));
@@ -2177,8 +2177,9 @@ class Oracle {
     m.pik = v.piKey;
     m.eik = key;
     m.partition = subscription_partition(str(m.corr), partition_count_);
-    m.interrupting = 1;  // intermediate catch events interrupt (ExecutableCatchEvent.java:36-38); so do the
-                         // subset's boundary events (cancelActivity)
+    // intermediate catch events interrupt (ExecutableCatchEvent.java:36-38); a boundary event as its
+    // cancelActivity says (ExecutableBoundaryEvent.interrupting)
+    m.interrupting = el.type == ZBHIP_EL_BOUNDARY_EVENT ? (el.interrupting ? 1 : 0) : 1;
     m.proc = v.proc;
     m.elem = v.elem;
     m.inst = cur_instance_;
@@ -2239,7 +2240,11 @@ class Oracle {
       PmsRow& row = it->second;
       msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_DELETING, row.key, row.rec);
       row.closing = true;
-      send_command(row.rec.partition, ZBHIP_CMD_MSG_SUB_DELETE, row.rec);
+      // closeMessageSubscription (SubscriptionCommandSender.java:220-236): a fresh record -- its
+      // interrupting flag keeps the default (true)
+      MsgVal del = row.rec;
+      del.interrupting = 1;
+      send_command(row.rec.partition, ZBHIP_CMD_MSG_SUB_DELETE, del);
     }
   }
 
@@ -2322,11 +2327,17 @@ class Oracle {
     const int64_t subKey = it->second.key;
     const bool interrupting = it->second.rec.interrupting;
     msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION, ZBHIP_PMS_CORRELATED, subKey, m);
-    if (interrupting) {  // ProcessMessageSubscriptionCorrelatedApplier
+    if (interrupting) {  // ProcessMessageSubscriptionCorrelatedApplier (:27-37): removed ...
       --pms_inst_[it->second.rec.inst];
       pms_.erase(it);
+    } else {  // ... or, non-interrupting, updateToOpenedState(record): the stored record is the CORRELATED one
+      MsgVal& row = it->second.rec;
+      const MsgVal keep = row;
+      row = m;
+      row.inst = keep.inst;
+      row.eord = keep.eord;
+      it->second.opened = true;
     }
-    else throw Unsupported{"non-interrupting subscription"};
     // EventHandle.activateElement (processing/common/EventHandle.java:109-150)
     const ElementInstance inst = eit->second;
     int64_t eventKey = next_key();
@@ -2337,9 +2348,13 @@ class Oracle {
     pe.r.process_instance_key = inst.value.piKey;
     if (P(m.proc).els[m.elem].type == ZBHIP_EL_BOUNDARY_EVENT) {
       // a boundary event of the activity: the trigger (ProcessEventTriggeringApplier, interrupting the
-      // event scope), then TERMINATE_ELEMENT of the activity -- its onTerminate activates the event
+      // event scope), then TERMINATE_ELEMENT of the activity -- its onTerminate activates the event; a
+      // non-interrupting one is activated right away (EventTriggerBehavior.activateTriggeredEvent)
       trigger_event(c.eik, eventKey, m.elem, m.proc, Doc{0, 0}, inst.value.piKey);
-      pi_command(c.eik, ZBHIP_PI_TERMINATE_ELEMENT, inst.value);
+      if (interrupting)
+        pi_command(c.eik, ZBHIP_PI_TERMINATE_ELEMENT, inst.value);
+      else
+        activate_triggered_event(eventKey, m.elem, c.eik, inst.value.flowScopeKey, inst.value);
     } else {
       if (event_scope_.count(c.eik))  // ProcessEventTriggeringApplier: trigger with the message variables (none)
         triggers_[{c.eik, eventKey}] = EventTrigger{inst.value.elem, inst.value.proc, Doc{0, 0}, inst.value.piKey};
@@ -2363,8 +2378,13 @@ class Oracle {
     }
     const MsgSub sub = it->second;
     msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_CORRELATED, sub.key, sub.rec);
-    if (!sub.rec.interrupting) throw Unsupported{"non-interrupting message subscription"};
-    msub_by_corr_.erase({(int)sub.rec.name, sub.rec.corr, sub.rec.eik});  // MessageSubscriptionCorrelatedApplier
+    // MessageSubscriptionCorrelatedApplier (:26-37): removed, or (non-interrupting) open again for the
+    // next message -- updateToCorrelatedState: not correlating, the last message key kept
+    if (!sub.rec.interrupting) {
+      it->second.correlating = false;
+      return;
+    }
+    msub_by_corr_.erase({(int)sub.rec.name, sub.rec.corr, sub.rec.eik});
     msub_.erase(it);
   }
 

@@ -8,7 +8,10 @@ join counters, a default flow on every exclusive split so no incident is raised)
 blocks -> end), never inside a parallel branch (one active instance per sub-process element).
 With ``boundaries`` a task outside parallel branches may carry a timer boundary event whose path
 ends in an end event or (interrupting ones) merges back after the task (one timer per instance at a
-time)."""
+time).  With ``multi_instance`` a task outside parallel branches may be a multi-instance activity over
+a static list (MultiInstanceActivityTest's shapes): parallel or sequential, the inputElement `x`, an
+outputCollection (its own name) of `= x` or `= loopCounter`, and -- sequential ones -- a
+completionCondition."""
 from xml.sax.saxutils import escape, quoteattr
 
 BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
@@ -17,8 +20,9 @@ ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
 
 class _Gen:
     def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True, sub_processes=False,
-                 task_kinds=False, boundaries=False):
+                 task_kinds=False, boundaries=False, multi_instance=False):
         self.rng = rng
+        self.multi_instance = multi_instance
         self.boundaries = boundaries
         self.task_kinds = task_kinds
         self.sub_processes = sub_processes
@@ -103,6 +107,16 @@ class _Gen:
                 kind = ("serviceTask", "sendTask", "scriptTask", "businessRuleTask")[int(r.integers(0, 4))]
             t = self.node(kind, job_type="job%d" % int(r.integers(0, 3)))
             self.flow(cur, t)
+            if self.multi_instance and width == 1 and int(r.integers(0, 2)):
+                seq = bool(int(r.integers(0, 2)))
+                items = [int(v) for v in r.integers(1, 5, int(r.integers(1, 4)))]
+                loop = {"seq": seq, "coll": "= [%s]" % ", ".join(map(str, items))}
+                if int(r.integers(0, 2)):
+                    loop["out"] = ("= x", "= loopCounter")[int(r.integers(0, 2))]
+                if seq and int(r.integers(0, 2)):
+                    loop["cond"] = ("= x >= 3", "= numberOfCompletedInstances >= 2", "= loopCounter = 2")[int(r.integers(0, 3))]
+                self.nodes[-1][2]["loop"] = loop
+                return t
             if self.boundaries and width == 1 and int(r.integers(0, 2)):
                 # an interrupting timer boundary event: its own end, or back through an XOR merge
                 cancel = bool(int(r.integers(0, 3)))
@@ -154,11 +168,11 @@ class _Gen:
 
 
 def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False,
-                   tasks=True, sub_processes=False, task_kinds=False, boundaries=False):
+                   tasks=True, sub_processes=False, task_kinds=False, boundaries=False, multi_instance=False):
     """tasks=False: no wait states (the CREATE batch runs the instance to its end); task_kinds: job
     worker tasks among service / send / script / business-rule tasks."""
     g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes, task_kinds,
-             boundaries)
+             boundaries, multi_instance)
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")
@@ -171,8 +185,18 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
             if extra["scope"] != scope:
                 continue
             if kind in ("serviceTask", "sendTask", "scriptTask", "businessRuleTask"):
+                loop = extra.get("loop")
+                lc = ""
+                if loop:
+                    lc = ('<multiInstanceLoopCharacteristics isSequential="%s"><extensionElements>'
+                          '<zeebe:loopCharacteristics inputCollection=%s inputElement="x"%s/></extensionElements>%s'
+                          '</multiInstanceLoopCharacteristics>'
+                          % ("true" if loop["seq"] else "false", quoteattr(loop["coll"]),
+                             ' outputCollection=%s outputElement=%s' % (quoteattr("out_" + nid), quoteattr(loop["out"]))
+                             if "out" in loop else "",
+                             "<completionCondition>%s</completionCondition>" % escape(loop["cond"]) if "cond" in loop else ""))
                 out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s/>'
-                           '</extensionElements></%s>' % (ind, kind, quoteattr(nid), quoteattr(extra["job_type"]), kind))
+                           '</extensionElements>%s</%s>' % (ind, kind, quoteattr(nid), quoteattr(extra["job_type"]), lc, kind))
             elif kind == "exclusiveGateway" and nid in g.defaults:
                 out.append('%s<exclusiveGateway id=%s default=%s/>' % (ind, quoteattr(nid), quoteattr(g.defaults[nid])))
             elif kind == "intermediateCatchEvent":

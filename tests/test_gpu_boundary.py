@@ -121,6 +121,19 @@ def test_gpu_random_processes_with_boundary_events(seed):
     assert [r for r in part.state() if not r.startswith("KEY|")] == []
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_random_processes_with_multi_instance_activities(seed):
+    # the same with multi-instance tasks among them (static collections, parallel or sequential, an
+    # outputCollection, sequential completion conditions): each round completes inner instances' jobs
+    from helpers import amount_docs
+    from random_bpmn import random_process
+    rng = np.random.default_rng(7000 + seed)
+    xml = random_process(rng, sub_processes=True, task_kinds=True, boundaries=True, multi_instance=True)
+    part, orc = drive_timers(xml, 96, seed=seed, phases=80, max_records=256,
+                             docs_fn=lambda n: amount_docs(rng.integers(0, 1000, n), 0))
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []
+
+
 @pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch", "non_interrupting_escalation",
                                    "cycle_r3"])
 def test_gpu_boundary_log_and_db_bytes(shape):

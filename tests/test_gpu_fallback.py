@@ -194,30 +194,34 @@ def test_device_window_with_duplicate_subjects_is_planned_like_a_host_window():
 
 def test_speculative_subject_check_replays_a_window_with_repeats():
     """Untrusted device windows launch before their subject check is read back: k_step runs guarded by
-    the check's flag, and the next call that depends on the window reads it.  A window with a repeated
-    subject did nothing on the device; it is replanned on the host and run again before the next window
-    -- the statistics (transitions, records, completed instances) equal the host-planned run's."""
+    the check's verdict (the guard word of the window's stamp), and the next call that depends on the
+    window reads it.  A window with a repeated subject did nothing on the device; it is replanned on the
+    host and run again before the next window -- the statistics (transitions, records, completed
+    instances) equal the host-planned run's."""
     import torch
     xml = bpmn.linear_process(3)
-    host, dev_p = Partition(max_instances=16, max_commands=32), Partition(max_instances=16, max_commands=32)
+    host = Partition(max_instances=16, max_commands=32)
+    dev_p = Partition(max_instances=16, max_commands=32)
     for p in (host, dev_p):
         p.deploy(xml)
         p.submit(create_commands(8))
         p.run()
         p.drain()
-    first = np.concatenate([complete_commands(np.arange(8), np.full(8, 5)), complete_commands(np.arange(4), np.full(4, 5))])
-    second = complete_commands(np.arange(8), np.full(8, 9))  # the next task's jobs
-    host.submit(first)
-    host.run(abi.RUN_NO_RESULTS)
-    host.submit(second)
-    host.run(abi.RUN_NO_RESULTS | abi.RUN_ACCUMULATE)
+    # faulty (a repeat), clean, faulty, clean: the jobs of tasks 1, 2, 3
+    windows = [np.concatenate([complete_commands(np.arange(8), np.full(8, 5)), complete_commands(np.arange(4), np.full(4, 5))]),
+               complete_commands(np.arange(8), np.full(8, 9)),
+               np.concatenate([complete_commands(np.arange(4), np.full(4, 13)), complete_commands(np.arange(2), np.full(2, 13))]),
+               complete_commands(np.arange(4, 8), np.full(4, 13))]
+    for k, w in enumerate(windows):
+        host.submit(w)
+        host.run(abi.RUN_NO_RESULTS | (abi.RUN_ACCUMULATE if k else 0))
     want = host.stats()
-    ts = [torch.from_numpy(c.view(np.uint8).copy()).to("cuda") for c in (first, second)]
-    dev_p.submit_device(ts[0].data_ptr(), len(first))
-    dev_p.run(abi.RUN_NO_RESULTS)
-    dev_p.submit_device(ts[1].data_ptr(), len(second))  # reads the first window's flag: replays it
-    dev_p.run(abi.RUN_NO_RESULTS | abi.RUN_ACCUMULATE)
-    got = dev_p.stats()  # reads the second window's flag (clean)
+    ts = [torch.from_numpy(c.view(np.uint8).copy()).to("cuda") for c in windows]
+    torch.cuda.synchronize()
+    for k, t in enumerate(ts):
+        dev_p.submit_device(t.data_ptr(), len(windows[k]))  # reads the last window's verdict: replays it
+        dev_p.run(abi.RUN_NO_RESULTS | (abi.RUN_ACCUMULATE if k else 0))
+    got = dev_p.stats()  # reads the last window's verdict (clean)
     for k in ("transitions", "records", "completed_instances", "fallback"):
         assert got[k] == want[k], k
-    assert want["completed_instances"] == 0 and want["transitions"] > 0
+    assert want["completed_instances"] == 8 and want["transitions"] > 0

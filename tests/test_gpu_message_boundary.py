@@ -1,11 +1,14 @@
-"""Interrupting message boundary events on the gfx950 executor (KMsg) against the oracle cluster:
+"""Message boundary events on the gfx950 executor (KMsg) against the oracle cluster -- interrupting:
 the subscription opened with the job worker task, then the message first (PROCESS_MESSAGE_SUBSCRIPTION
 :CORRELATE terminates the task -- JOB:CANCELED -- and activates the boundary event) or the job first
 (the task's unsubscribeFromEvents: PROCESS_MESSAGE_SUBSCRIPTION:DELETING, MESSAGE_SUBSCRIPTION:DELETE /
 DELETED on the message partition, PROCESS_MESSAGE_SUBSCRIPTION:DELETE / DELETED back on the PI
 partition, also after the instance ended).  Bar as for config 5: every window's records (all parity
 fields), outbox entries and exported state bit-exact, at P = 1 and P = 3.  The oracle's lifecycles
-are pinned on MessageCatchElementTest / BoundaryEventTest (tests/test_oracle_message_boundary.py)."""
+are pinned on MessageCatchElementTest / BoundaryEventTest (tests/test_oracle_message_boundary.py).
+Non-interrupting ones (NON_INT_BOUNDARY_EVENT_PROCESS): every message activates the boundary event while
+the task stays, both subscriptions stay open with the last message key in their records, and the
+job's completion closes them."""
 import numpy as np
 import pytest
 
@@ -21,11 +24,14 @@ pytestmark = pytest.mark.gpu
 XML = bpmn.message_boundary_process()
 
 
-def clusters(P, n_inst):
+NON_INT = bpmn.message_boundary_process("nonIntBoundaryEventProcess", interrupting=False)
+
+
+def clusters(P, n_inst, xml=XML):
     gpu = MessageCluster([Partition(partition_id=p, partition_count=P, max_instances=n_inst, max_commands=4 * n_inst,
                                     max_correlation_keys=4 * n_inst * P, max_records_per_batch=256)
-                          for p in range(1, P + 1)], GpuAdapter, XML)
-    orc = MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], OracleAdapter, XML)
+                          for p in range(1, P + 1)], GpuAdapter, xml)
+    orc = MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], OracleAdapter, xml)
     return gpu, orc
 
 
@@ -104,3 +110,27 @@ def test_gpu_mixed_outcomes(P):
         cl.publish([i for _, i in rest], [subscription_partition(k, P) for k, _ in rest])
     assert_same_logs(gpu, orc)
     assert_same_state(gpu, orc)
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_gpu_non_interrupting_boundary(P):
+    # two messages per instance (the boundary event activated twice, the task kept), then the jobs;
+    # the state between the steps carries the open subscriptions with their last message key
+    n = 24
+    gpu, orc = clusters(P, n, NON_INT)
+    ks, ids = start(gpu, orc, P, n)
+    for _ in range(2):
+        for cl in (gpu, orc):
+            cl.publish(ids, [subscription_partition(k, P) for k in ks])
+        assert_same_logs(gpu, orc)
+        assert_same_state(gpu, orc)
+    assert any("messageKey=-1" not in r for r in gpu.parts[0].state() if r.startswith("PROCESS_SUBSCRIPTION_BY_KEY"))
+    cmds = job_completions(orc, n)
+    for cl in (gpu, orc):
+        cl.commands("complete", cmds)
+    assert_same_logs(gpu, orc)
+    assert_same_state(gpu, orc)
+    done = sum(int(np.sum((r["value_type"] == abi.VT_PROCESS_INSTANCE) & (r["intent"] == abi.PI_ELEMENT_COMPLETED)
+                          & (r["element_idx"] == 0))) for _, _, r, _ in gpu.log)
+    assert done == n * P
+    assert not [r for p in gpu.parts for r in p.state() if not r.startswith(("KEY|", "MESSAGE_STATS"))]

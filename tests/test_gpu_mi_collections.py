@@ -115,3 +115,35 @@ def test_random_collections():
         rng.shuffle(live)
         write(ref, gpu, *[Client.complete_job(k, (("result", int(rng.integers(0, 50))),)) for k in live[:3]])
     check(ref, gpu)
+
+
+def test_output_collections_of_one_name_in_sequence():
+    """Two multi-instance activities one after the other collecting into the same outputCollection:
+    the second body's propagateVariable finds the first's array in the process instance's scope and
+    updates it (VARIABLE:UPDATED -- mergeDocument, VariableBehavior.java:105-150) when the arrays differ
+    (lengths 3 and 2 here); direct parity with the oracle, no fallback."""
+    from test_gpu_parity import run_both
+    from helpers import complete_commands, create_commands
+    from oracle.oracle import Oracle
+    from zeebe_amd.engine import Partition
+    b = bpmn.createExecutableProcess("process").startEvent("s")
+    b.serviceTask("a", "a").multiInstance("= [1, 2, 3]", "x", True, outputCollection="out", outputElement="= x")
+    b.serviceTask("b", "b").multiInstance("= [7, 8]", "x", False, outputCollection="out", outputElement="= loopCounter")
+    xml = b.endEvent("e").done()
+    n = 8
+    part, orc = Partition(max_instances=n, max_commands=n, max_records_per_batch=128), Oracle()
+    assert part.deploy(xml) == orc.deploy(xml) == 0
+    run_both(part, orc, create_commands(n, 0))
+    for _ in range(6):
+        keys = sorted(int(r.split("|")[1]) for r in part.state() if r.startswith("JOBS|"))
+        if not keys:
+            break
+        by = {}
+        for k in keys:
+            inst, ordv = part.resolve_key(k)
+            by.setdefault(inst, ordv)
+        insts = sorted(by)
+        run_both(part, orc, complete_commands(insts, [by[i] for i in insts]))
+        assert part.state() == orc.state()
+    assert part.stats()["fallback"] == 0
+    assert [r for r in part.state() if not r.startswith("KEY|")] == []

@@ -15,12 +15,30 @@ pytestmark = pytest.mark.gpu
 FIELDS = abi.PARITY_FIELDS
 
 
+def _first_difference(got, want):
+    """The first record index where the two logs differ (by all parity fields), with both sides' rows."""
+    n = min(len(got), len(want))
+    i = next((i for i in range(n) if any(got[f][i] != want[f][i] for f in FIELDS)), n)
+    rows = lambda a: [tuple(int(a[f][j]) for f in ("value_type", "intent", "record_type", "element_idx", "key"))  # noqa: E731
+                      for j in range(max(0, i - 2), min(len(a), i + 3))]
+    return "first difference at %d: got %s want %s" % (i, rows(got), rows(want))
+
+
 def assert_same_records(got, want, part=None, orc=None):
-    assert len(got) == len(want), (len(got), len(want))
+    assert len(got) == len(want), (len(got), len(want), _first_difference(got, want))
+    # list values (ZBHIP_DOC_LIST) are ids into each side's own list dictionary: compared by their items
+    lists = (got["value_type"] == abi.VT_VARIABLE) & (got["partition"] == abi.DOC_LIST) & (got["aux"] == abi.AUX_INLINE)
+    if part is not None and lists.any():
+        for i in np.nonzero(lists)[0]:
+            assert want["partition"][i] == abi.DOC_LIST, i
+            assert part.list_items(int(got["message_key"][i])) == orc.list_items(int(want["message_key"][i])), i
+        got, want = got.copy(), want.copy()
+        got["message_key"][lists] = want["message_key"][lists] = 0
     for f in FIELDS:
         if not np.array_equal(got[f], want[f]):
             bad = np.nonzero(got[f] != want[f])[0][:5]
-            raise AssertionError("field %s differs at %s: got %s want %s" % (f, bad, got[f][bad], want[f][bad]))
+            rows = "".join("\n  %d got  %s\n  %d want %s" % (i, got[i], i, want[i]) for i in bad[:2])
+            raise AssertionError("field %s differs at %s: got %s want %s%s" % (f, bad, got[f][bad], want[f][bad], rows))
     if part is not None:
         for i in np.nonzero(got["record_type"] == abi.RT_REJECTION)[0]:
             assert part.reason(got[i]) == orc.reason(int(i))

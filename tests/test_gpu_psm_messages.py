@@ -156,3 +156,30 @@ def test_message_boundary_events_on_three_partitions_in_the_processing_loop():
     assert canceled == 15
     c = [gpu.adapters[p].counts for p in range(1, P + 1)]
     assert all(x["fallbacks"] == 0 for x in c), [gpu.adapters[p].fallback_reasons for p in range(1, P + 1)]
+
+
+NON_INT_XML = bpmn.message_boundary_process("nonIntBoundaryEventProcess", message_name="message", correlation_key="key",
+                                            interrupting=False)
+
+
+def test_non_interrupting_message_boundary_events_in_the_processing_loop():
+    """Non-interrupting message boundary events (NON_INT_BOUNDARY_EVENT_PROCESS) on three partitions:
+    each key gets three messages -- every one activates the boundary event again while the task stays
+    (both subscriptions open, their records holding the last message key) -- then every job completes
+    and closes its subscription; logs and state equal the engine-only cluster's at every phase."""
+    from psm import open_jobs
+    from oracle.oracle import subscription_partition
+    ref, gpu = Cluster(device=False, xml=NON_INT_XML), Cluster(device=True, xml=NON_INT_XML)
+    phase(ref, gpu, create_phase("nonIntBoundaryEventProcess"))
+    pubs = {p: [] for p in range(1, P + 1)}
+    for k in KEYS:
+        pubs[subscription_partition(k, P)] += [Client.publish_message("message", k) for _ in range(3)]
+    phase(ref, gpu, sorted(pubs.items()))
+    jobs = {p: [Client.complete_job(k) for k in sorted(open_jobs(ref.logs[p]))] for p in range(1, P + 1)}
+    phase(ref, gpu, sorted(jobs.items()))
+    boundary = [sum(1 for p in range(1, P + 1) for r in cl.logs[p].entries
+                    if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_COMPLETED
+                    and r.value["elementId"] == "boundary") for cl in (ref, gpu)]
+    assert boundary[0] == boundary[1] > len(KEYS)  # (a message meeting a CORRELATING subscription skips it)
+    c = [gpu.adapters[p].counts for p in range(1, P + 1)]
+    assert all(x["fallbacks"] == 0 for x in c), [gpu.adapters[p].fallback_reasons for p in range(1, P + 1)]

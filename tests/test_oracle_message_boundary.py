@@ -23,8 +23,8 @@ XML = bpmn.message_boundary_process()
 N = 6
 
 
-def cluster(P):
-    return MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], OracleAdapter, XML)
+def cluster(P, xml=XML):
+    return MessageCluster([Oracle(partition_id=p, partition_count=P) for p in range(1, P + 1)], OracleAdapter, xml)
 
 
 def keys(P, n=N):
@@ -180,11 +180,49 @@ def test_correlation_key_from_the_flow_scope():
     assert cl.parts[0].element_id(int(rec["process_idx"]), int(rec["element_idx"])) == "boundary"
 
 
-def test_non_interrupting_message_boundary_is_refused():
-    xml = bpmn.message_boundary_process().replace('attachedToRef="task"', 'attachedToRef="task" cancelActivity="false"')
-    o = Oracle()
-    with pytest.raises(Exception):
-        o.deploy(xml)
+NON_INT = bpmn.message_boundary_process("nonIntBoundaryEventProcess", interrupting=False)
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_non_interrupting_boundary_correlates_every_message(P):
+    # MessageCatchElementTest "non int boundary event" (NON_INT_BOUNDARY_EVENT_PROCESS :81-91): the
+    # message activates the boundary event ("event" ELEMENT_COMPLETED, its flow taken) and the task stays
+    # ACTIVATED; ProcessMessageSubscriptionCorrelatedApplier / MessageSubscriptionCorrelatedApplier keep
+    # both subscriptions (OPENED with the CORRELATED record; not correlating, the message key kept), so a
+    # second message correlates again (BoundaryEventTest.shouldTriggerMultipleNonInterruptingBoundaryEvents
+    # :394-470); the job's completion then closes them (DELETING .. DELETED, the last message key in the
+    # values) and the instance completes through the task's own end event
+    cl = cluster(P, NON_INT)
+    ks, ids = start(cl, P)
+    parts = [subscription_partition(k, P) for k in ks]
+    cl.publish(ids, parts)
+    cl.publish(ids, parts)
+    for part in cl.parts:
+        rows = [r for r in part.state() if r.startswith(("PROCESS_SUBSCRIPTION_BY_KEY", "MESSAGE_SUBSCRIPTION_BY_KEY"))]
+        for r in rows:
+            assert "messageKey=-1" not in r
+            assert "state=OPENED" in r or "correlating=0" in r, r
+    assert sum(len([r for r in part.state() if r.startswith("PROCESS_SUBSCRIPTION_BY_KEY")]) for part in cl.parts) == N * P
+    cl.commands("complete", job_completions(cl))
+    recs = all_records(cl)
+    piks = sorted({t[7] for t in recs if t[3] == abi.VT_PROCESS_INSTANCE and t[4] == 5 and t[8] == "nonIntBoundaryEventProcess"})
+    assert len(piks) == N * P
+    for pik in piks:
+        mine = of_instance(recs, pik)
+        pi = [(t[4], t[8]) for t in mine if t[3] == abi.VT_PROCESS_INSTANCE and t[2] == abi.RT_EVENT]
+        assert pi.count((5, "boundary")) == 2 and pi.count((5, "end2")) == 2 and pi.count((5, "end")) == 1
+        assert (7, "task") not in pi and pi.count((5, "task")) == 1
+        pev = [(t[4], t[5], t[9]) for t in mine if t[3] == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION and t[2] == abi.RT_EVENT]
+        assert [it for it, _, _ in pev] == [abi.PMS_CREATING, abi.PMS_CREATED, abi.PMS_CORRELATED, abi.PMS_CORRELATED,
+                                            abi.PMS_DELETING, abi.PMS_DELETED]
+        assert len({k for _, k, _ in pev}) == 1 and not int(pev[2][2]["interrupting"])
+        # the stored record after the second correlation: its message key
+        assert int(pev[4][2]["message_key"]) == int(pev[3][2]["message_key"]) != int(pev[2][2]["message_key"])
+        ms = [t[4] for t in mine if t[3] == abi.VT_MESSAGE_SUBSCRIPTION and t[2] == abi.RT_EVENT]
+        assert ms == [abi.MS_CREATED, abi.MS_CORRELATING, abi.MS_CORRELATED, abi.MS_CORRELATING, abi.MS_CORRELATED,
+                      abi.MS_DELETED]
+    for part in cl.parts:
+        assert [r for r in part.state() if not r.startswith(("KEY|", "MESSAGE_STATS"))] == []
 
 
 def test_correlation_key_incident_on_the_task():

@@ -872,7 +872,8 @@ class GpuBatchProcessor:
                 sub = (value["elementInstanceKey"], value["messageName"])
                 if it == abi.MS_CREATED:
                     self.subscriptions[sub] = int(r["correlation_key"])
-                elif it in (abi.MS_CORRELATED, abi.MS_DELETED):
+                elif it == abi.MS_DELETED or (it == abi.MS_CORRELATED and value.get("interrupting", True)):
+                    # (a non-interrupting subscription stays open after its correlation)
                     self.subscriptions.pop(sub, None)
             elif vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION and rt == abi.RT_EVENT:
                 # a closing subscription keeps its instance slot until PROCESS_MESSAGE_SUBSCRIPTION:DELETED
@@ -882,7 +883,8 @@ class GpuBatchProcessor:
                     self.pms_handles[sub] = self._resolve(value["elementInstanceKey"])
                 elif it == abi.PMS_DELETING:
                     self.closing.add(win.instances[i])
-                elif it in (abi.PMS_DELETED, abi.PMS_CORRELATED):
+                elif it == abi.PMS_DELETED or (it == abi.PMS_CORRELATED and value.get("interrupting", True)):
+                    # (a non-interrupting subscription stays open after its correlation)
                     self.pms_handles.pop(sub, None)
                     if it == abi.PMS_DELETED:
                         self.closing.discard(win.instances[i])

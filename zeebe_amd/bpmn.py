@@ -416,11 +416,15 @@ def message_catch_process(process_id="process", message_name="msg", correlation_
 
 
 def message_boundary_process(process_id="boundaryEventProcess", message_name="msg", correlation_key="key",
-                             task_id="task", job_type="type", flow_id="to-end2"):
+                             task_id="task", job_type="type", flow_id="to-end2", interrupting=True):
     """MessageCatchElementTest.BOUNDARY_EVENT_PROCESS (engine/src/test/.../message/MessageCatchElementTest.java:
-    71-80): start -> service task with an interrupting message boundary event (-> end2) -> end."""
+    71-80): start -> service task with an interrupting message boundary event (-> end2) -> end;
+    interrupting=False: NON_INT_BOUNDARY_EVENT_PROCESS (:81-91, cancelActivity(false))."""
     b = createExecutableProcess(process_id).startEvent("start").serviceTask(task_id, job_type)
-    b.boundaryEvent("boundary").message(message_name, correlation_key).sequenceFlowId(flow_id).endEvent("end2")
+    b.boundaryEvent("boundary")
+    if not interrupting:
+        b.cancelActivity(False)
+    b.message(message_name, correlation_key).sequenceFlowId(flow_id).endEvent("end2")
     return b.moveToActivity(task_id).endEvent("end").done()
 
 

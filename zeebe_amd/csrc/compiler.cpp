@@ -775,8 +775,8 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         if (int rc = parse_mappings(c.first("extensionElements"), (uint16_t)C.elements.size(), C, err)) return rc;
       }
       if (type == ZBHIP_EL_BOUNDARY_EVENT && c.first("messageEventDefinition")) {
-        // BoundaryEventTransformer + CatchEventTransformer.transformMessageEventDefinition: an
-        // interrupting message boundary event on a job worker task (static name, `= variable`
+        // BoundaryEventTransformer + CatchEventTransformer.transformMessageEventDefinition: a message
+        // boundary event on a job worker task, interrupting or not (static name, `= variable`
         // correlation key, evaluated in the task's flow scope); attached after the walk
         const std::string* ca = c.get("cancelActivity");
         const Elem* med = c.first("messageEventDefinition");
@@ -785,7 +785,6 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
             err = "event definition <" + d.tag + "> outside the supported subset";
             return ZBHIP_EUNSUPP;
           }
-        if (ca && *ca == "false") { err = "non-interrupting message boundary event outside the supported subset"; return ZBHIP_EUNSUPP; }
         if (!med->get("messageRef")) { err = "boundary event without a message"; return ZBHIP_EUNSUPP; }
         auto mi = messages.find(*med->get("messageRef"));
         if (mi == messages.end()) { err = "unknown message " + *med->get("messageRef"); return ZBHIP_EPARSE; }
@@ -797,7 +796,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         e.event_type = ZBHIP_EV_MESSAGE;
         e.message_name = C.str(mi->second.name);
         e.correlation_var = C.str(mi->second.corr);
-        e.job_retries = 1;  // interrupting
+        e.job_retries = ca && *ca == "false" ? 0 : 1;  // cancelActivity (BoundaryEvent default: interrupting)
         boundaries.push_back({(uint16_t)C.elements.size(), *at});
       } else if (type == ZBHIP_EL_BOUNDARY_EVENT) {
         // BoundaryEventTransformer: timer boundary events (a static timeDuration; interrupting or not)

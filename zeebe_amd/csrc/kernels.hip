@@ -170,6 +170,8 @@ struct Lane {
                             // (1 opening, 2 opened, 3 closing) | interrupting << 14 | partition << 16;
                             // element-instance ordinal | key ordinal << 16; correlation key
   uint32_t pm_w;            // its message name | bpmnProcessId << 16
+  long long pm_msg;         // the message key the (non-interrupting) subscription's record holds: its
+                            // last correlation's (updateToOpenedState), -1 before one (DevState.pms_msg)
   long long pik;            // real process-instance key of the loaded instance, or a reference
   bool slot_lane;           // primary subject is the correlation slot `slot`
   uint32_t slot;
@@ -183,6 +185,7 @@ struct Lane {
   long long lq_msg;         // its message key (reference)
   uint32_t lq_name_bpmn;    // message name | bpmnProcessId << 16 of the pending command
   uint32_t lq_corr;         // correlation key of the pending command
+  uint32_t lq_intr;         // interrupting flag of the pending command's subscription
   long long lq_eik, lq_pik; // element / process instance keys of the pending command (references)
   uint32_t lq_eord;         // routing handle ordinal of the pending command
   // deferred correlation-slot row operations, applied at commit
@@ -191,6 +194,7 @@ struct Lane {
   uint4 ins_a;
   long long ins_eik, ins_pik;
   uint32_t op_corr_mask, op_rm_mask, op_rm_slot;
+  uint32_t op_open_mask, op_open_slot;  // non-interrupting rows correlated: open again (state 1)
   long long op_corr_msg, ins_key;
   const StepParams* sp;
   const uint32_t* prog;     // LDS program arena (mid-batch instance loads)
@@ -1262,22 +1266,26 @@ __device__ __forceinline__ void subscribe_message(Lane<K>& L, uint32_t elem, uin
   const uint32_t part = subscription_partition((int32_t)P.str_hash[corr], P.partition_count);
   const uint32_t nb = name | ((L.pb[5] & 0xFFFF) << 16);
   const uint32_t sub = new_key(L);
-  L.pm_x = elem | (1u << 12) | (1u << 14) | (part << 16);  // ProcessMessageSubscriptionCreatingApplier
+  // ExecutableCatchEvent.isInterrupting: a catch event always, a boundary event as cancelActivity says
+  const uint32_t intr = boundary ? (w.w & 1u) : 1u;
+  L.pm_x = elem | (1u << 12) | (intr << 14) | (part << 16);  // ProcessMessageSubscriptionCreatingApplier
   L.pm_y = key | (sub << 16);
   L.pm_z = corr;
   L.pm_w = nb;
-  emit_msg(L, C_PMS_CREATING, iref(L, sub), iref(L, key), iref(L, 0), -1, corr, nb, part, 1, elem);
+  L.pm_msg = -1;
+  emit_msg(L, C_PMS_CREATING, iref(L, sub), iref(L, key), iref(L, 0), -1, corr, nb, part, intr, elem);
   if ((int32_t)part == P.partition_id) {
-    emit_msg(L, C_MS_CREATE, -1, iref(L, key), iref(L, 0), -1, corr, nb, 0, 1, kNoElem);
+    emit_msg(L, C_MS_CREATE, -1, iref(L, key), iref(L, 0), -1, corr, nb, 0, intr, kNoElem);
     L.lq_slot = corr;
     L.lq_corr = corr;
+    L.lq_intr = intr;
     L.lq_name_bpmn = nb;
     L.lq_eord = key;
     L.lq_eik = cref_inst(L, key);
     L.lq_pik = L.pik;
     push_local(L, LQ_MS_CREATE);
   } else {
-    send_xpart(L, ZBHIP_CMD_MSG_SUB_CREATE, part, cref_inst(L, key), L.pik, -1, corr, L.inst, key, nb, 1);
+    send_xpart(L, ZBHIP_CMD_MSG_SUB_CREATE, part, cref_inst(L, key), L.pik, -1, corr, L.inst, key, nb, intr);
   }
 }
 
@@ -1332,6 +1340,7 @@ __device__ __forceinline__ void ms_create(Lane<K>& L, uint32_t slot, uint32_t co
     L.lq_eik = eik;
     L.lq_pik = pik;
     L.lq_row = inst;  // the instance to load in a slot lane
+    L.lq_intr = intr;
     push_local(L, LQ_PMS_CREATE);
   } else {
     send_xpart(L, ZBHIP_CMD_PMS_CREATE, pi_part, eik, pik, -1, corr, inst, eord, nb, intr);
@@ -1378,13 +1387,21 @@ __device__ __forceinline__ void pms_correlate(Lane<K>& L, uint32_t eord, uint32_
   const bool boundary = etype(elem_of(L, elem)) == ZBHIP_EL_BOUNDARY_EVENT;
   // an interrupting boundary event terminates its activity first (the command's context travels in
   // the lane: past the batch limit it would be written unprocessed -- outside the device subset)
-  if (boundary && pending(L) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
+  if (boundary && intr && pending(L) + L.processed + 1 >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
   emit_msg(L, C_PMS_CORRELATED, iref(L, L.pm_y >> 16), eik_p, pik_p, msg_p, corr, nb, part, intr, elem);
-  L.pm_x = L.pm_y = L.pm_z = L.pm_w = 0;  // ProcessMessageSubscriptionCorrelatedApplier: interrupting -> removed
+  // ProcessMessageSubscriptionCorrelatedApplier (:27-37): interrupting -> removed; otherwise
+  // updateToOpenedState(record): open, the record the CORRELATED one (its message key)
+  if (intr) L.pm_x = L.pm_y = L.pm_z = L.pm_w = 0;
+  else L.pm_msg = msg_p;
   const uint32_t pe = new_key(L);
   emit(L, C_PE_TRIGGERING, pe, eord, elem);
   L.trig_key = (uint16_t)eord;
-  if (boundary) {
+  if (boundary && !intr) {
+    // a non-interrupting boundary event: EventHandle.activateElement -> activateTriggeredEvent in this
+    // batch; the activity stays active (its EVENT_TRIGGER row is deleted by TRIGGERED)
+    L.trig_key = NONE;
+    activate_triggered_event(L, pe, eord, elem, scope_key(L, 0));
+  } else if (boundary) {
     // EventHandle.activateElement for a boundary event: TERMINATE_ELEMENT of the activity (its
     // onTerminate activates the event with the trigger's PROCESS_EVENT key)
     L.trig_evt = (uint16_t)pe;
@@ -1424,8 +1441,17 @@ __device__ __forceinline__ void ms_correlate(Lane<K>& L, uint32_t slot, uint32_t
   const longlong2 b = P.st.sub_b[ri];
   const longlong2 k = P.st.sub_k[ri];
   const long long msg = (L.op_corr_mask >> r) & 1 ? L.op_corr_msg : k.y;
-  if (!((a.x >> 8) & 1)) { set_fail(L, FB_MESSAGE); return; }  // non-interrupting: correlateNextMessage
-  emit_msg(L, C_MS_CORRELATED, k.x, b.x, b.y, msg, slot, a.y, 0, 1, kNoElem);
+  const uint32_t intr = (a.x >> 8) & 1;
+  emit_msg(L, C_MS_CORRELATED, k.x, b.x, b.y, msg, slot, a.y, 0, intr, kNoElem);
+  if (!intr) {
+    // MessageSubscriptionCorrelatedApplier (:26-37), non-interrupting: updateToCorrelatedState -- open
+    // again, the message key kept (at commit); correlateNextMessage finds no buffered message (the
+    // subset's messages live for their PUBLISH batch only)
+    if (L.op_open_mask && L.op_open_slot != slot) { set_fail(L, FB_MESSAGE); return; }
+    L.op_open_mask |= 1u << r;
+    L.op_open_slot = slot;
+    return;
+  }
   // MessageSubscriptionCorrelatedApplier: interrupting -> removed (at commit)
   if (L.op_rm_mask && L.op_rm_slot != slot) { set_fail(L, FB_MESSAGE); return; }
   L.op_rm_mask |= 1u << r;
@@ -1439,7 +1465,7 @@ __device__ __forceinline__ void ms_correlate(Lane<K>& L, uint32_t slot, uint32_t
 template <class K>
 __device__ __forceinline__ void unsubscribe_message(Lane<K>& L) {
   const uint32_t eord = L.pm_y & 0xFFFF, part = L.pm_x >> 16, corr = L.pm_z, nb = L.pm_w, st0 = (L.pm_x >> 12) & 3;
-  emit_msg(L, C_PMS_DELETING, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, corr, nb, part,
+  emit_msg(L, C_PMS_DELETING, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), L.pm_msg, corr, nb, part,
            (L.pm_x >> 14) & 1, L.pm_x & 0xFFF);
   L.pm_x |= 3u << 12;
   const uint32_t name_only = (nb & 0xFFFF) | 0xFFFF0000u;
@@ -1502,9 +1528,10 @@ template <class K>
 __device__ __forceinline__ void pms_delete(Lane<K>& L, uint32_t eord, uint32_t name) {
   const uint32_t st = (L.pm_x >> 12) & 3;
   if (st == 0 || (L.pm_y & 0xFFFF) != eord || (L.pm_w & 0xFFFF) != name) { set_fail(L, FB_MESSAGE); return; }
-  emit_msg(L, C_PMS_DELETED, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), -1, L.pm_z, L.pm_w, L.pm_x >> 16,
+  emit_msg(L, C_PMS_DELETED, iref(L, L.pm_y >> 16), iref(L, eord), iref(L, 0), L.pm_msg, L.pm_z, L.pm_w, L.pm_x >> 16,
            (L.pm_x >> 14) & 1, L.pm_x & 0xFFF);
   L.pm_x = L.pm_y = L.pm_z = L.pm_w = 0;
+  L.pm_msg = -1;
 }
 
 // sort key of a subscription's element instance key for the visit order of
@@ -2115,15 +2142,30 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   if constexpr (K::IO) {
     // MultiInstanceBodyProcessor.onComplete (:100-114): propagateVariable of the outputCollection
     // (BpmnStateBehavior.java:163-178 -> mergeDocument from the flow scope): created in the process
-    // instance's scope; a variable of that name above the body already (its array compared on the
-    // host only) is outside the subset
+    // instance's scope, or UPDATED where it exists -- unless equal (VariableBehavior.java:134).  The
+    // device holds an output array's length (the variable's value), not its items: an existing array
+    // of another length or a scalar differs; one of the same length, a list variable, or a variable
+    // of a sub-process scope is outside the subset
     if (type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
       const uint32_t oc = mi_ext(L, elem).x >> 16;
       if (oc != 0xFFFF) {
-        if (var_lookup(L, cmd_key, c, oc) >= 0 || L.nvars >= kVars) { set_fail(L, FB_VARS); return; }
-        const uint32_t kv = new_key(L);
-        emit(L, C_MI_PROP, kv, cmd_key, elem);
-        var_put(L, L.nvars++, oc, kv | ((uint32_t)kDocOutList << 16), 0);
+        uint32_t n, list;
+        if (!mi_collection(L, elem, w, cmd_key, c, n, list)) return;
+        const int vi = var_lookup(L, cmd_key, c, oc);
+        if (vi >= 0) {
+          const uint32_t vy = var_y(L, vi), vt = (vy >> 16) & 0xFF;
+          if ((var_x(L, vi) >> 16) != 0 || vt == ZBHIP_DOC_LIST || (vt == kDocOutList && var_v(L, vi) == (long long)n)) {
+            set_fail(L, FB_VARS);
+            return;
+          }
+          emit(L, C_MI_PROP, vy & 0xFFFF, cmd_key, elem, 1u);  // (flags 1: UPDATED)
+          var_put(L, vi, var_x(L, vi), (vy & 0xFFFF) | ((uint32_t)kDocOutList << 16), (long long)n);
+        } else {
+          if (L.nvars >= kVars) { set_fail(L, FB_VARS); return; }
+          const uint32_t kv = new_key(L);
+          emit(L, C_MI_PROP, kv, cmd_key, elem);
+          var_put(L, L.nvars++, oc, kv | ((uint32_t)kDocOutList << 16), (long long)n);
+        }
       }
     }
   }
@@ -2751,6 +2793,7 @@ __device__ __forceinline__ void load_instance_mid(Lane<K>& L, uint32_t inst) {
   L.pm_y = pm.y;
   L.pm_z = pm.z;
   L.pm_w = pm.w;
+  L.pm_msg = P.st.pms_msg[inst];
   L.pik = P.st.pi_key[inst];
   vm_drain();
 }
@@ -2761,7 +2804,7 @@ __device__ __forceinline__ void process_local(Lane<K>& L, uint32_t kind) {
   const uint32_t own = (uint32_t)L.sp->partition_id;
   switch (kind) {
     case LQ_MS_CREATE:  // from a catch event of the loaded instance
-      ms_create(L, L.lq_slot, L.lq_corr, L.lq_name_bpmn, 1, own, L.inst, L.lq_eord, L.lq_eik, L.lq_pik,
+      ms_create(L, L.lq_slot, L.lq_corr, L.lq_name_bpmn, L.lq_intr, own, L.inst, L.lq_eord, L.lq_eik, L.lq_pik,
                 iref(L, L.lq_eord), iref(L, 0));
       return;
     case LQ_PMS_CREATE: {  // acknowledgement of a subscription this partition opened
@@ -2770,7 +2813,7 @@ __device__ __forceinline__ void process_local(Lane<K>& L, uint32_t kind) {
       if (L.fail) return;
       const long long eik_p = was_loaded && !L.slot_lane ? iref(L, L.lq_eord) : L.lq_eik;
       const long long pik_p = was_loaded && !L.slot_lane ? iref(L, 0) : L.lq_pik;
-      pms_create(L, L.lq_eord, L.lq_name_bpmn & 0xFFFF, eik_p, pik_p, own, 1);
+      pms_create(L, L.lq_eord, L.lq_name_bpmn & 0xFFFF, eik_p, pik_p, own, L.lq_intr);
       return;
     }
     case LQ_PMS_CORRELATE:  // a message published on this partition for one of its instances
@@ -2873,6 +2916,13 @@ __device__ __forceinline__ void commit_slot_rows(Lane<K>& L) {
     patch_slot = L.slot;
     patch_what |= 2u;  // the correlating message key
   }
+  if (L.op_open_mask) {  // non-interrupting rows correlated (after their CORRELATING of this batch, if any)
+    for (int r = 0; r < kSubs; ++r)
+      if ((L.op_open_mask >> r) & 1) {
+        const size_t ri = sub_ri(r, L.op_open_slot);
+        P.st.sub_a[ri].x = (P.st.sub_a[ri].x & ~0xFFu) | 1u;
+      }
+  }
   if (L.op_rm_mask) {
     for (int r = 0; r < kSubs; ++r)
       if ((L.op_rm_mask >> r) & 1) P.st.sub_a[sub_ri(r, L.op_rm_slot)] = make_uint4(0, 0, 0, 0);
@@ -2964,6 +3014,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     L.prog = prog;
     L.inst = inst;
     L.pm_x = L.pm_y = L.pm_z = L.pm_w = 0;
+    L.pm_msg = -1;
     L.pik = -1;
     L.slot_lane = false;
     L.slot = 0;
@@ -2978,6 +3029,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     L.ins_a = make_uint4(0, 0, 0, 0);
     L.ins_eik = L.ins_pik = L.ins_key = -1;
     L.op_corr_mask = L.op_rm_mask = L.op_rm_slot = 0;
+    L.op_open_mask = L.op_open_slot = 0;
     L.op_corr_msg = -1;
     slot_kind = zb_slot_kind(kind);
   }
@@ -3061,6 +3113,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
         L.pm_y = pm.y;
         L.pm_z = pm.z;
         L.pm_w = pm.w;
+        L.pm_msg = P.st.pms_msg[inst];
         L.pik = P.st.pi_key[inst];
         vm_drain();
       }
@@ -3253,7 +3306,10 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
   if constexpr (K::M) {
     // an ended instance keeps a closing subscription until its PROCESS_MESSAGE_SUBSCRIPTION:DELETE
     const bool keep = L.pi_live || ((L.pm_x >> 12) & 3) == 3;
-    if (ok && winst != kNoInst) P.st.pms[winst] = keep ? make_uint4(L.pm_x, L.pm_y, L.pm_z, L.pm_w) : make_uint4(0, 0, 0, 0);
+    if (ok && winst != kNoInst) {
+      P.st.pms[winst] = keep ? make_uint4(L.pm_x, L.pm_y, L.pm_z, L.pm_w) : make_uint4(0, 0, 0, 0);
+      P.st.pms_msg[winst] = keep && ((L.pm_x >> 12) & 3) ? L.pm_msg : -1;
+    }
   }
   if constexpr (K::S) {
     if (ok && winst != kNoInst && L.has_tmr) {
@@ -3358,7 +3414,17 @@ __global__ __launch_bounds__(K::B) __attribute__((amdgpu_waves_per_eu(K::W ? K::
 #endif
   // a speculatively launched untrusted window whose subject check found a repeat: no lane touches
   // state or output (uniform: the whole grid returns; the host replans and runs the window again)
-  if (P.guard && *P.guard) return;
+  if (P.guard) {
+    // an untrusted device window's subject check (k_subject_check): its verdict to the host (once per
+    // launch), and a faulty window does nothing (the host replans it)
+    const uint32_t g = *reinterpret_cast<const volatile uint32_t*>(P.guard);
+    const uint32_t f = (g >> 2) == P.guard_stamp ? g & 3u : 0u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      *reinterpret_cast<volatile uint32_t*>(P.guard_host) = (P.guard_stamp << 2) | f;
+      __threadfence_system();
+    }
+    if (f) return;
+  }
   const uint32_t n_chunks = (P.n_launch + K::B - 1) / K::B;
   const uint32_t G = gridDim.x;
   const uint32_t lane = threadIdx.x & 63;
@@ -3944,42 +4010,45 @@ __global__ __launch_bounds__(256) void k_xpart_window(const zbhip_xpart_cmd* xp,
   cmds[i] = make_uint4(pms ? x.instance : x.correlation_key, x.kind, i, 0);  // zbhip_command layout
 }
 
+constexpr uint32_t kCheckPerThread = 1;
+
 // Subject check of a device-resident window (zbhip_submit_device*): every command claims its
 // subject (instance slot, or correlation slot for MESSAGE / MESSAGE_SUBSCRIPTION commands) with the
 // window's stamp; a second claim in the window flags a duplicate (bit 0), a subject out of range or
-// an unknown kind bit 1.  The flags gather in w[0]; the last workgroup to finish (w[1] counts them)
-// moves them into the guard word w[2] (the window's k_step launch reads it) and writes the window's
-// completion marker stamp << 2 | flags into the host-mapped word `host` -- no copy, no reset launch:
-// the host reads the marker whenever it needs the verdict (runtime.cpp resolve_guard).
+// an unknown kind bit 1.  A flagged lane raises the window's guard word gw to stamp << 2 | flags
+// (atomicMax: stamps grow, so the word needs no reset between windows, and clean windows write nothing;
+// the host alternates two words by stamp parity).  The
+// window's k_step reads the verdict (StepParams.guard) and publishes it to the host; a caller that
+// needs it before any k_step runs launches k_check_publish.
 __global__ __launch_bounds__(256) void k_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots,
-                                                       uint32_t* seen, uint32_t stamp, uint32_t* w, uint32_t* host) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+                                                       uint32_t* seen, uint32_t stamp, uint32_t* gw) {
+  // kCheckPerThread commands a thread, strided by the grid (coalesced loads and claims)
+  const uint32_t stride = gridDim.x * 256;
   uint32_t f = 0;
-  if (i < n) {
+#pragma unroll
+  for (uint32_t k = 0; k < kCheckPerThread; ++k) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x + k * stride;
+    if (i >= n) break;
     const uint4 c = cmds[i];
     const uint32_t kind = c.y & 0xFF;
     const bool sk = zb_slot_kind(kind);
-    const bool known = (kind >= ZBHIP_CMD_CREATE && kind <= ZBHIP_CMD_MSG_SUB_CORRELATE) || kind == ZBHIP_CMD_MSG_SUB_DELETE ||
-                       kind == ZBHIP_CMD_PMS_DELETE;
+    const bool known = (kind >= ZBHIP_CMD_CREATE && kind <= ZBHIP_CMD_MSG_SUB_CORRELATE) ||
+                       kind == ZBHIP_CMD_MSG_SUB_DELETE || kind == ZBHIP_CMD_PMS_DELETE;
     if (!known || (sk ? c.x >= n_slots : c.x >= n_inst)) {
-      f = 2;
+      f |= 2;
     } else if (atomicExch(&seen[(sk ? n_inst : 0u) + c.x], stamp) == stamp) {
-      f = 1;
+      f |= 1;
     }
   }
-  if (f) atomicOr(&w[0], f);  // rare: a faulty window
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(&w[1], 1u) == gridDim.x - 1) {  // the last workgroup: every flag is in w[0]
-      __threadfence();
-      const uint32_t all = atomicExch(&w[0], 0u);
-      atomicExch(&w[1], 0u);
-      atomicExch(&w[2], all);
-      __threadfence_system();
-      *reinterpret_cast<volatile uint32_t*>(host) = (stamp << 2) | all;
-    }
-  }
+  if (f) atomicMax(gw, (stamp << 2) | f);  // rare: a faulty window
+}
+
+// The verdict of the window checked with `stamp` into host-mapped memory (stamp << 2 | flags)
+__global__ void k_check_publish(const uint32_t* gw, uint32_t stamp, uint32_t* host) {
+  if (threadIdx.x != 0) return;
+  const uint32_t g = *reinterpret_cast<const volatile uint32_t*>(gw);
+  *reinterpret_cast<volatile uint32_t*>(host) = (stamp << 2) | ((g >> 2) == stamp ? g & 3u : 0u);
+  __threadfence_system();
 }
 
 // A device window's launch order by subject (instance slots, then correlation slots): the stable
@@ -4238,9 +4307,15 @@ hipError_t launch_keyscan(const uint2* cmd_hdr, const uint4* cmd_hdr2, const uin
 }
 
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
-                                uint32_t stamp, uint32_t* w, uint32_t* host, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_subject_check, dim3((n + 255) / 256), dim3(256), 0, s, cmds, n, n_inst, n_slots, seen, stamp,
-                            w, host);
+                                uint32_t stamp, uint32_t* gw, hipStream_t s) {
+  const uint32_t per_block = 256 * kCheckPerThread;
+  if (n) hipLaunchKernelGGL(k_subject_check, dim3((n + per_block - 1) / per_block), dim3(256), 0, s, cmds, n, n_inst, n_slots,
+                            seen, stamp, gw);
+  return hipGetLastError();
+}
+
+hipError_t launch_check_publish(const uint32_t* gw, uint32_t stamp, uint32_t* host, hipStream_t s) {
+  hipLaunchKernelGGL(k_check_publish, dim3(1), dim3(64), 0, s, gw, stamp, host);
   return hipGetLastError();
 }
 

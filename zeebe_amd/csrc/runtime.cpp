@@ -60,7 +60,8 @@ hipError_t launch_subject_sort(const uint4* cmds, uint32_t n, uint32_t n_inst, u
                                uint32_t* k1, uint32_t* v0, uint32_t* order, void* temp, size_t temp_bytes,
                                hipStream_t s);
 hipError_t launch_subject_check(const uint4* cmds, uint32_t n, uint32_t n_inst, uint32_t n_slots, uint32_t* seen,
-                                uint32_t stamp, uint32_t* w, uint32_t* host, hipStream_t s);
+                                uint32_t stamp, uint32_t* w, hipStream_t s);
+hipError_t launch_check_publish(const uint32_t* w, uint32_t stamp, uint32_t* host, hipStream_t s);
 hipError_t launch_bucket(const uint2* cmd_hdr, const uint4* cmd_hdr2, const zbhip_xpart_cmd* xout, uint32_t xcap,
                          uint32_t n, uint32_t parts, uint32_t* blk_cnt, uint32_t* counts, zbhip_xpart_cmd* out,
                          hipStream_t s);
@@ -920,7 +921,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
   h->st.n_slots = (uint32_t)S;
   if (S) {
     ok = ok && dalloc(&h->st.pms, N) == hipSuccess && dalloc(&h->st.pi_key, N) == hipSuccess &&
-         dalloc(&h->st.pms_eik, N) == hipSuccess &&
+         dalloc(&h->st.pms_eik, N) == hipSuccess && dalloc(&h->st.pms_msg, N) == hipSuccess &&
          dalloc(&h->st.slot_hdr, S) == hipSuccess && dalloc(&h->st.sub_a, S * kSubs) == hipSuccess &&
          dalloc(&h->st.sub_b, S * kSubs) == hipSuccess && dalloc(&h->st.sub_k, S * kSubs) == hipSuccess;
   }
@@ -944,6 +945,7 @@ int zbhip_open(const zbhip_config* cfg, zbhip_handle** out) {
     if (hipMemsetAsync(h->st.pms, 0, N * sizeof(uint4), h->stream) != hipSuccess ||
         hipMemsetAsync(h->st.pi_key, 0xFF, N * sizeof(long long), h->stream) != hipSuccess ||
         hipMemsetAsync(h->st.pms_eik, 0xFF, N * sizeof(long long), h->stream) != hipSuccess ||
+        hipMemsetAsync(h->st.pms_msg, 0xFF, N * sizeof(long long), h->stream) != hipSuccess ||
         hipMemsetAsync(h->st.slot_hdr, 0, S * sizeof(uint2), h->stream) != hipSuccess ||
         hipMemsetAsync(h->st.sub_a, 0, S * kSubs * sizeof(uint4), h->stream) != hipSuccess ||
         hipMemcpyAsync(h->d_key_counter, &kc, sizeof kc, hipMemcpyHostToDevice, h->stream) != hipSuccess) {
@@ -995,6 +997,7 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_stats);
   (void)hipFree(h->st.pms);
   (void)hipFree(h->st.pms_eik);
+  (void)hipFree(h->st.pms_msg);
   (void)hipFree(h->st.tmr);
   (void)hipFree(h->st.act);
   (void)hipFree(h->d_cmd_act);
@@ -1380,12 +1383,12 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         e.element_type != ZBHIP_EL_SUB_PROCESS && e.element_type != ZBHIP_EL_BOUNDARY_EVENT &&
         e.element_type != ZBHIP_EL_MULTI_INSTANCE_BODY && !pass_through(e.element_type))
       return ZBHIP_EUNSUPP;
-  // timer boundary events and interrupting message boundary events: one per job worker task, in the
-  // task's container (message boundary events: the process's, KMsg has no flow scopes)
+  // timer and message boundary events: one per job worker task, in the task's container (message
+  // boundary events: the process's, KMsg has no flow scopes)
   for (size_t e = 0; e < P.els.size(); ++e) {
     const zbhip_element& E = P.els[e];
     if (E.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
-      const bool msg = E.event_type == ZBHIP_EV_MESSAGE && (E.job_retries & 1) && E.flow_scope == 0;
+      const bool msg = E.event_type == ZBHIP_EV_MESSAGE && E.flow_scope == 0;
       if ((E.event_type != ZBHIP_EV_TIMER && !msg) || E.flow_source >= P.els.size()) return ZBHIP_EUNSUPP;
       const zbhip_element& A = P.els[E.flow_source];
       if (!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e || A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
@@ -1937,9 +1940,9 @@ int zbhip_submit_device(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n
 static int replan_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, size_t n, const zbhip_doc_entry* dev_docs,
                                 size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts, bool* replanned);
 
-// The subject check's verdict of the last checked window: its completion marker in host-mapped memory
-// (k_subject_check's last workgroup writes stamp << 2 | flags); a spin, bounded by the stream's own
-// completion (a device fault ends it)
+// The subject check's verdict of the last checked window: its marker in host-mapped memory (stamp << 2
+// | flags: the window's guarded k_step, or k_check_publish, writes it); a spin, bounded by the stream's
+// own completion (a device fault ends it)
 static int64_t read_check_marker(zbhip_handle* h) {
   const volatile uint32_t* m = h->h_check_flag;
   const uint32_t want = h->guard_stamp & 0x3FFFFFFFu;
@@ -1989,8 +1992,11 @@ static int check_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, s
                                size_t n_docs, const zbhip_xpart_cmd* dev_xparts, size_t n_xparts, bool* replanned) {
   *replanned = false;
   if ((h->cfg.flags & ZBHIP_OPEN_TRUSTED_DEVICE_WINDOWS) || n == 0) return ZBHIP_OK;
-  if (++h->check_stamp >= (1u << 30)) {  // (30-bit stamps: the completion marker's)
-    HIPCHK(hipMemsetAsync(h->d_seen, 0, ((size_t)h->cfg.max_instances + h->st.n_slots) * sizeof(uint32_t), h->stream));
+  // (on the handle's stream: in order after whatever produced the window)
+  hipStream_t cs = h->stream;
+  if (++h->check_stamp >= (1u << 30)) {  // (30-bit stamps: the guard word's and the marker's)
+    HIPCHK(hipMemsetAsync(h->d_seen, 0, ((size_t)h->cfg.max_instances + h->st.n_slots) * sizeof(uint32_t), cs));
+    HIPCHK(hipMemsetAsync(h->d_check_flag, 0, 4 * sizeof(uint32_t), cs));
     h->check_stamp = 1;
   }
   if (!h->h_check_flag) {  // the host-mapped completion marker (stamp << 2 | flags)
@@ -2000,7 +2006,7 @@ static int check_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, s
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->d_check_host), h->h_check_flag, 0));
   }
   HIPCHK(launch_subject_check(reinterpret_cast<const uint4*>(dev_cmds), (uint32_t)n, h->cfg.max_instances, h->st.n_slots,
-                              h->d_seen, h->check_stamp, h->d_check_flag, h->d_check_host, h->stream));
+                              h->d_seen, h->check_stamp, h->d_check_flag + 2, cs));
   h->guard_win = {dev_cmds, n, dev_docs, n_docs, dev_xparts, n_xparts, h->next_doc_base, h->next_source, 0};
   h->guard_stamp = h->check_stamp;
   if (!h->msg() && !getenv("ZBHIP_SYNC_SUBJECT_CHECK")) {
@@ -2009,6 +2015,7 @@ static int check_device_window(zbhip_handle* h, const zbhip_command* dev_cmds, s
     h->guard_armed = true;
     return ZBHIP_OK;
   }
+  HIPCHK(launch_check_publish(h->d_check_flag + 2, h->check_stamp, h->d_check_host, cs));
   int64_t flag = read_check_marker(h);
   if (flag < 0) return (int)flag;
   if (flag & 2) return ZBHIP_EINVAL;
@@ -2442,7 +2449,8 @@ static int track_mi(zbhip_handle* h, size_t c, uint32_t inst) {
       const int64_t id = intern_items(h, o.items);
       if (id < 0) return (int)id;
       h->mi_rec[at] = {o.var_key, body_key, (int32_t)m->out_coll, intent, (uint8_t)ZBHIP_DOC_LIST, id};
-    } else if (c6 == C_MI_PROP) {  // propagateVariable: created in the process instance's scope
+    } else if (c6 == C_MI_PROP) {  // propagateVariable: created in the process instance's scope, or
+      // (flags 1) the variable there updated
       const Proc::Mi* m = P.mi_body(elem);
       auto f = h->mi_out.find(h->key_of(inst, aux_ord));
       if (!m || f == h->mi_out.end()) return mi_fail(6);
@@ -2450,8 +2458,8 @@ static int track_mi(zbhip_handle* h, size_t c, uint32_t inst) {
       if (id < 0) return (int)id;
       const int64_t vk = h->key_of(inst, key_ord);
       h->outlist_var[vk] = (uint32_t)id;
-      h->mi_rec[at] = {vk, h->key_of(inst, 0), (int32_t)m->out_coll, (uint8_t)ZBHIP_VAR_CREATED,
-                       (uint8_t)ZBHIP_DOC_LIST, id};
+      h->mi_rec[at] = {vk, h->key_of(inst, 0), (int32_t)m->out_coll,
+                       (uint8_t)(fl & 1 ? ZBHIP_VAR_UPDATED : ZBHIP_VAR_CREATED), (uint8_t)ZBHIP_DOC_LIST, id};
     } else if ((c6 == ZBHIP_PI_ELEMENT_COMPLETED || c6 == ZBHIP_PI_ELEMENT_TERMINATED) && elem < P.els.size() &&
                P.els[elem].element_type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
       h->mi_out.erase(h->key_of(inst, key_ord));  // the body's variables leave with it
@@ -2582,11 +2590,12 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
     h->guard_armed = false;
     if (flags & ZBHIP_RUN_NO_RESULTS) {
       // speculative: k_step runs guarded by the check's flag; resolve_guard reads it later
-      guard = h->d_check_flag + 2;  // the guard word (k_subject_check's last workgroup writes it)
+      guard = h->d_check_flag + 2;  // the guard word (k_subject_check's faulty lanes raise it)
       h->guard_win.run_flags = flags;
       h->guard_pending = true;
     } else {
       // results are read back in this call anyway: decide now
+      HIPCHK(launch_check_publish(h->d_check_flag + 2, h->guard_stamp, h->d_check_host, h->stream));
       const int64_t fl = read_check_marker(h);
       if (fl < 0) return (int)fl;
       const uint32_t flag = (uint32_t)fl;
@@ -2648,6 +2657,8 @@ int zbhip_run(zbhip_handle* h, uint32_t flags) {
   P.map_cap = h->cfg.max_commands;
   P.cmd_act = h->st.act ? h->d_cmd_act : nullptr;
   P.guard = guard;
+  P.guard_stamp = h->guard_stamp & 0x3FFFFFFFu;
+  P.guard_host = h->d_check_host;
   if (h->d_list_n != h->lists.size())
     if (int rc = sync_lists(h)) return rc;
   P.list_hdr = h->d_list_hdr;
@@ -3731,6 +3742,7 @@ struct InstRows {  // the SoA rows of one instance slot
   long long vv[kVars];
   uint32_t join[kJoinWords];
   uint4 pms;
+  long long pms_msg = -1;  // DevState.pms_msg
   bool has_pms;
   uint4 tmr;  // the instance's timer row (DevState.tmr)
 };
@@ -3748,10 +3760,10 @@ static void emit_pms(zbhip_handle* h, uint32_t inst, const InstRows& R, const Pr
     const zbhip_element& E = P.els[el];
     snprintf(buf, sizeof buf,
              "PROCESS_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,state=%s,subscriptionPartitionId=%u,processInstanceKey=%lld,"
-             "bpmnProcessId=%s,messageKey=-1,correlationKey=%s,elementId=%s,interrupting=%u",
+             "bpmnProcessId=%s,messageKey=%lld,correlationKey=%s,elementId=%s,interrupting=%u",
              h->key_of(inst, m.y & 0xFFFF), zbhip_name(h, E.message_name), h->key_of(inst, m.y >> 16),
              ((m.x >> 12) & 3) == 1 ? "OPENING" : ((m.x >> 12) & 3) == 3 ? "CLOSING" : "OPENED", m.x >> 16, pik, zbhip_name(h, P.bpmn_name),
-             zbhip_string_value(h, m.z, nullptr), P.id(el).c_str(), (m.x >> 14) & 1);
+             h->resolve_ref(R.pms_msg), zbhip_string_value(h, m.z, nullptr), P.id(el).c_str(), (m.x >> 14) & 1);
     sink(ctx, buf);
   }
 }
@@ -4010,7 +4022,10 @@ static int gather_instance(zbhip_handle* h, uint32_t i, InstRows& R) {
   for (int w = 0; w < kJoinWords; ++w)
     HIPCHK(hipMemcpy(&R.join[w], h->st.join + w * N + i, sizeof(uint32_t), hipMemcpyDeviceToHost));
   R.has_pms = h->st.n_slots != 0;
-  if (R.has_pms) HIPCHK(hipMemcpy(&R.pms, h->st.pms + i, sizeof(uint4), hipMemcpyDeviceToHost));
+  if (R.has_pms) {
+    HIPCHK(hipMemcpy(&R.pms, h->st.pms + i, sizeof(uint4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&R.pms_msg, h->st.pms_msg + i, sizeof(long long), hipMemcpyDeviceToHost));
+  }
   HIPCHK(hipMemcpy(&R.tmr, h->st.tmr + i, sizeof(uint4), hipMemcpyDeviceToHost));
   return ZBHIP_OK;
 }
@@ -4029,8 +4044,10 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   std::vector<uint4> pms(S ? N : 0), sub_a(S * kSubs);
   std::vector<longlong2> sub_b(S * kSubs), sub_k(S * kSubs);
   HIPCHK(hipStreamSynchronize(h->stream));
+  std::vector<long long> pms_msg(S ? N : 0, -1);
   if (S) {
     HIPCHK(hipMemcpy(pms.data(), h->st.pms, N * sizeof(uint4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pms_msg.data(), h->st.pms_msg, N * sizeof(long long), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(sub_a.data(), h->st.sub_a, S * kSubs * sizeof(uint4), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(sub_b.data(), h->st.sub_b, S * kSubs * sizeof(longlong2), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(sub_k.data(), h->st.sub_k, S * kSubs * sizeof(longlong2), hipMemcpyDeviceToHost));
@@ -4058,7 +4075,10 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
     }
     for (int k = 0; k < kJoinWords; ++k) R.join[k] = join[(size_t)k * N + i];
     R.has_pms = S != 0;
-    if (S) R.pms = pms[i];
+    if (S) {
+      R.pms = pms[i];
+      R.pms_msg = pms_msg[i];
+    }
     R.tmr = tmr[i];
     emit_instance(h, (uint32_t)i, R, sink, ctx);
   }
@@ -4260,6 +4280,7 @@ struct ImpPms {
   int64_t eik = 0, key = 0;
   std::string name, corr, elem_id;
   uint32_t state = 0, part = 0, intr = 0;
+  int64_t msg = -1;  // messageKey of the stored record (a non-interrupting subscription's last correlation)
 };
 int64_t string_interner(void* ctx, const char* b, size_t n) {
   return zbhip_intern_string(static_cast<zbhip_handle*>(ctx), b, n);
@@ -4358,6 +4379,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
       m.corr = f["correlationKey"];
       m.elem_id = f["elementId"];
       m.intr = (uint32_t)to_ll(f["interrupting"]);
+      m.msg = f.count("messageKey") ? to_ll(f["messageKey"]) : -1;
       pms.push_back(m);
     } else if (cf == "TIMERS" && p.size() >= 4) {
       auto f = row_fields(p[3]);
@@ -4387,6 +4409,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   std::vector<uint32_t> join(N * kJoinWords);
   std::vector<uint4> pmsrow(h->st.n_slots ? N : 0);
   std::vector<long long> pmseik(h->st.n_slots ? N : 0, -1);
+  std::vector<long long> pmsmsg(h->st.n_slots ? N : 0, -1);
   std::vector<long long> pikrow(h->st.n_slots ? N : 0);
   std::vector<uint4> tmrrow(N);
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -4399,6 +4422,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   if (h->st.n_slots) {
     HIPCHK(hipMemcpy(pmsrow.data(), h->st.pms, N * sizeof(uint4), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(pmseik.data(), h->st.pms_eik, N * sizeof(long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pmsmsg.data(), h->st.pms_msg, N * sizeof(long long), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(pikrow.data(), h->st.pi_key, N * sizeof(long long), hipMemcpyDeviceToHost));
   }
   const int64_t pbits = (int64_t)h->cfg.partition_id << 51;
@@ -4603,14 +4627,19 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
     if (h->st.n_slots) {
       pmsrow[inst] = make_uint4(0, 0, 0, 0);
       pmseik[inst] = -1;
+      pmsmsg[inst] = -1;
       pikrow[inst] = pe.key;
       if (sub) {
         const int el = elem_of_id(sub->elem_id);
         if (el < 0) return ZBHIP_EINVAL;
         const int64_t corr = zbhip_intern_string(h, sub->corr.data(), sub->corr.size());
         if (corr < 0) return (int)corr;
+        const int name = zbhip_intern(h, sub->name.c_str());
+        if (name < 0) return name;
         pmsrow[inst] = make_uint4((uint32_t)el | (sub->state << 12) | (sub->intr << 14) | (sub->part << 16),
-                                  ord(sub->eik) | (ord(sub->key) << 16), (uint32_t)corr, 0);
+                                  ord(sub->eik) | (ord(sub->key) << 16), (uint32_t)corr,
+                                  (uint32_t)name | ((uint32_t)P.bpmn_name << 16));
+        pmsmsg[inst] = sub->msg;
         // an opened subscription of another partition: its real element-instance key (the later DELETE's)
         if (sub->state == 2 && (int32_t)sub->part != h->cfg.partition_id) pmseik[inst] = sub->eik;
       }
@@ -4639,6 +4668,7 @@ extern "C" int zbhip_import_state(zbhip_handle* h, const char* text, size_t len,
   if (h->st.n_slots) {
     HIPCHK(hipMemcpy(h->st.pms, pmsrow.data(), N * sizeof(uint4), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->st.pms_eik, pmseik.data(), N * sizeof(long long), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->st.pms_msg, pmsmsg.data(), N * sizeof(long long), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->st.pi_key, pikrow.data(), N * sizeof(long long), hipMemcpyHostToDevice));
   }
   // key histories and the resolve_key table: one entry per imported key

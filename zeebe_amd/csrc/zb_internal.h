@@ -219,6 +219,8 @@ struct DevState {
   long long* pms_eik; // [n] real element-instance key of the instance's subscription once its
                       //     PROCESS_MESSAGE_SUBSCRIPTION:CREATE arrived from another partition (-1: none) --
                       //     the MESSAGE_SUBSCRIPTION:DELETE a later window sends carries it
+  long long* pms_msg; // [n] the message key of the subscription's record: its last correlation's for a
+                      //     non-interrupting one (updateToOpenedState), -1 before (a key reference or real key)
   long long* pi_key; // [n] real process-instance key (written by the device key scan)
   uint2* slot_hdr;   // [S] x = next key ordinal of the correlation slot; y = fence stamp (as hdr.w)
   uint4* sub_a;      // [kSubs][S] MESSAGE_SUBSCRIPTION rows: x = state (0 free, 1 open, 2 correlating)
@@ -302,8 +304,11 @@ struct StepParams {
   uint32_t map_cap;
   uint4* cmd_act;             // [n_cmds] the ACTIVATED job a batch completed or canceled: its DevState.act
                               // entry (x bit 31 clear: none found)
-  const uint32_t* guard;      // an untrusted device window's subject-check flag (k_subject_check): nonzero
-                              // -> the launch does nothing (the host replans the window); null: no guard
+  const uint32_t* guard;      // an untrusted device window's subject-check word (k_subject_check): stamp << 2 |
+                              // flags; flags of this window's stamp -> the launch does nothing (the host
+                              // replans the window); null: no guard
+  uint32_t guard_stamp;       // the window's check stamp
+  uint32_t* guard_host;       // host-mapped: the verdict, stamp << 2 | flags (block 0 writes it)
   // the list dictionary (ZBHIP_DOC_LIST values): per list its first item and count, the items' values
   // and zbhip_doc_types
   const uint2* list_hdr;
