@@ -195,7 +195,8 @@ typedef struct zbhip_element {
                           * instructions, one per item, or ZBHIP_OP_COLLECTION; then ZBHIP_OP_OUTPUT,
                           * then ZBHIP_OP_END) */
   uint16_t default_flow; /* exclusive gateway: default flow element; multi-instance body: the condition
-                          * index of its completionCondition; else ZBHIP_NONE16 */
+                          * index of its completionCondition; sub-process: its (timer) boundary event;
+                          * else ZBHIP_NONE16 */
   uint16_t job_type;     /* service task: string-table index of the job type */
   uint16_t job_retries;  /* service task: static retries; boundary event: bit 0 interrupting (cancelActivity),
                           * bits 8..15 the timer's repetitions (1 a duration, n of "Rn/", 255 "R/" infinite);

@@ -903,8 +903,11 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
     auto it = idx.find(ref);
     if (it == idx.end()) { err = "boundary event attached to an unknown element"; return false; }
     OEl& a = P.els[it->second];
-    if (!ZBHIP_IS_JOB_WORKER(a.type) || a.scope != P.els[b].scope) {
-      err = "boundary event on an element outside the supported subset (job worker tasks only)";
+    // job worker tasks; embedded sub-processes with a timer boundary event (subscribed when their start
+    // event completes, StartEventProcessor.onComplete :52-67)
+    const bool sub_ok = a.type == ZBHIP_EL_SUB_PROCESS && P.els[b].event == ZBHIP_EV_TIMER;
+    if ((!ZBHIP_IS_JOB_WORKER(a.type) && !sub_ok) || a.scope != P.els[b].scope) {
+      err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return false;
     }
     if (a.boundary >= 0) { err = "more than one boundary event on an activity outside the supported subset"; return false; }
@@ -3133,12 +3136,13 @@ class Oracle {
       case ZBHIP_EL_PROCESS:  // ProcessProcessor.onComplete (:63-76): never end of path
         pi_event(key, ZBHIP_PI_ELEMENT_COMPLETED, v);
         break;
-      case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onComplete (:52-67)
-        complete_and_take(el, key, v, true);
+      case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onComplete (:52-67): applyOutputMappings,
+        // subscribeToEvents of the flow scope (a sub-process's boundary timer), transitionToCompleted
+        complete_and_take(el, key, v, true, false, /*subscribe_scope=*/true);
         break;
       case ZBHIP_EL_SUB_PROCESS:  // SubProcessProcessor.onComplete (:68-82): applyOutputMappings,
-        // unsubscribeFromEvents (no subscriptions in the subset), transitionToCompleted, take flows
-        complete_and_take(el, key, v, true);
+        // unsubscribeFromEvents (its boundary timer: TIMER:CANCELED), transitionToCompleted, take flows
+        complete_and_take(el, key, v, true, /*unsubscribe=*/true);
         break;
       case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onComplete (:63-75)
       case ZBHIP_EL_SEND_TASK:
@@ -3188,8 +3192,39 @@ class Oracle {
   }
 
   // JobWorkerTaskProcessor.onTerminate (processing/bpmn/task/JobWorkerTaskProcessor.java:77-104)
+  // the processors' onTerminate (processing/bpmn/**: JobWorkerTaskProcessor :77-104, IntermediateCatch
+  // EventProcessor, SubProcessProcessor :84-95): job workers cancel their job, catch events and
+  // containers unsubscribe; a container terminates its children first (terminateChildInstances,
+  // BpmnStateTransitionBehavior.java:348-363: PROCESS_INSTANCE_BATCH:TERMINATE) and finishes in
+  // onChildTerminated once none is active
   void on_terminate(const OEl& el, int64_t key, const PiValue& v) {
-    if (!ZBHIP_IS_JOB_WORKER(el.type)) throw Unsupported{"terminate of a non job worker element"};
+    if (el.type == ZBHIP_EL_SUB_PROCESS) {
+      unsubscribe_timers(key);  // unsubscribeFromEvents
+      unsubscribe_messages(key);
+      const ElementInstance& sub = ei_.at(key);
+      if (sub.childCount == 0) {
+        container_child_terminated(key);
+      } else {
+        ORecord& rec = append(ZBHIP_RT_COMMAND, ZBHIP_VT_PROCESS_INSTANCE_BATCH, ZBHIP_PIB_TERMINATE, next_key());
+        rec.r.process_idx = v.proc;
+        rec.r.element_idx = v.elem;
+        rec.r.scope_key = key;  // batchElementInstanceKey
+        rec.r.process_instance_key = v.piKey;
+        rec.r.partition = -1;   // index: from the first child
+        rec.pi = v;
+      }
+      return;
+    }
+    if (el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {
+      // IntermediateCatchEventProcessor.onTerminate: unsubscribeFromEvents, resolveIncidents (none),
+      // transitionToTerminated, onElementTerminated
+      unsubscribe_timers(key);
+      unsubscribe_messages(key);
+      pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
+      child_terminated(v);
+      return;
+    }
+    if (!ZBHIP_IS_JOB_WORKER(el.type)) throw Unsupported{"terminate of an element outside the subset"};
     // jobBehavior.cancelJob (behavior/BpmnJobBehavior.java:251-274): JOB:CANCELED with the stored job
     const int64_t jobKey = ei_.at(key).jobKey;
     auto jit = jobKey > 0 ? jobs_.find(jobKey) : jobs_.end();
@@ -3206,27 +3241,69 @@ class Oracle {
     unsubscribe_timers(key);  // unsubscribeFromEvents: timers, then message subscriptions
     unsubscribe_messages(key);
     // findEventTrigger (BpmnEventSubscriptionBehavior.java:63-70): the scope's first trigger, unless
-    // it is the element's own
+    // it is the element's own -- taken only while the flow scope is active and not interrupted
     auto tit = triggers_.lower_bound({key, INT64_MIN});
     const bool found = tit != triggers_.end() && tit->first.first == key && tit->second.elem != v.elem;
     auto fit = ei_.find(v.flowScopeKey);
-    if (!found && fit != ei_.end() && E(fit->second.value).type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
-      // no event trigger: transitionToTerminated, onElementTerminated -> MultiInstanceBodyProcessor
-      // .onChildTerminated (:232-247): a body that is not terminating completes once no child is active
-      // (its completion condition was met)
-      pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
-      const ElementInstance& body = ei_.at(v.flowScopeKey);
+    const bool fs_active = v.flowScopeKey == v.piKey ? fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED
+                                                      : fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED;
+    if (found && fs_active && !es_interrupted_.count(v.flowScopeKey)) {
+      const int64_t eventKey = tit->first.second;
+      const int target = tit->second.elem;
+      pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);  // transitionToTerminated
+      activate_triggered_event(eventKey, target, key, v.flowScopeKey, v);
+      return;
+    }
+    // no event trigger: transitionToTerminated, onElementTerminated
+    pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
+    child_terminated(v);
+  }
+
+  // BpmnStateTransitionBehavior.onElementTerminated (:419-441): the flow scope's onChildTerminated --
+  // a multi-instance body (MultiInstanceBodyProcessor.onChildTerminated :232-247: one that is not
+  // terminating completes once no child is active: its completion condition was met), a sub-process
+  // (SubProcessProcessor.onChildTerminated :108-160)
+  void child_terminated(const PiValue& child) {
+    auto fit = ei_.find(child.flowScopeKey);
+    if (fit == ei_.end()) throw Unsupported{"terminated child without its flow scope"};
+    const OEl& fe = E(fit->second.value);
+    if (fe.type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      const ElementInstance& body = fit->second;
       if (body.state == ZBHIP_PI_ELEMENT_TERMINATING) throw Unsupported{"terminating multi-instance body"};
       if ((int64_t)body.childCount + body.activeSequenceFlows == 0)
         pi_command(body.key, ZBHIP_PI_COMPLETE_ELEMENT, body.value);
       return;
     }
-    if (!found || fit == ei_.end() || fit->second.state != ZBHIP_PI_ELEMENT_ACTIVATED)
-      throw Unsupported{"termination without an event trigger (onElementTerminated)"};
-    const int64_t eventKey = tit->first.second;
-    const int target = tit->second.elem;
-    pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);  // transitionToTerminated
-    activate_triggered_event(eventKey, target, key, v.flowScopeKey, v);
+    if (fe.type == ZBHIP_EL_SUB_PROCESS) {
+      // canBeTerminated(child): no active child of the sub-process is left
+      if (fit->second.childCount == 0) container_child_terminated(fit->first);
+      return;
+    }
+    throw Unsupported{"terminated child of the process (cancel)"};
+  }
+
+  // SubProcessProcessor.onChildTerminated (:108-160) with no active child left: its boundary event's
+  // trigger (the flow scope active and not interrupted) -> transitionToTerminated and
+  // activateTriggeredEvent; else, terminated by its own flow scope -> transitionToTerminated and
+  // onElementTerminated
+  void container_child_terminated(int64_t key) {
+    const ElementInstance sub = ei_.at(key);
+    const PiValue v = sub.value;
+    auto tit = triggers_.lower_bound({key, INT64_MIN});
+    const bool found = tit != triggers_.end() && tit->first.first == key;
+    auto fit = ei_.find(v.flowScopeKey);
+    const bool fs_active = fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED;
+    if (found && fs_active && !es_interrupted_.count(v.flowScopeKey)) {
+      const int64_t eventKey = tit->first.second;
+      const int target = tit->second.elem;
+      pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
+      activate_triggered_event(eventKey, target, key, v.flowScopeKey, v);
+      return;
+    }
+    if (sub.state == ZBHIP_PI_ELEMENT_TERMINATING) {
+      pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
+      child_terminated(v);
+    }
   }
 
   // EventTriggerBehavior.activateTriggeredEvent (processing/common/EventTriggerBehavior.java:191-244):
@@ -3251,7 +3328,8 @@ class Oracle {
 
   // applyOutputMappings (behavior/BpmnVariableMappingBehavior.java:86-156) ->
   // transitionToCompleted -> takeOutgoingSequenceFlows (BpmnStateTransitionBehavior.java:365-369)
-  void complete_and_take(const OEl& el, int64_t key, const PiValue& v, bool output_mappings, bool unsubscribe = false) {
+  void complete_and_take(const OEl& el, int64_t key, const PiValue& v, bool output_mappings, bool unsubscribe = false,
+                         bool subscribe_scope = false) {
     if (output_mappings) {
       const EventTrigger* trig = nullptr;  // peekEventTrigger(elementInstanceKey)
       auto it = triggers_.lower_bound({key, INT64_MIN});
@@ -3272,6 +3350,17 @@ class Oracle {
     if (unsubscribe) {  // unsubscribeFromEvents (CatchEventBehavior.java:126-138): timers, then messages
       unsubscribe_timers(key);
       unsubscribe_messages(key);
+    }
+    if (subscribe_scope) {  // a start event: subscribeToEvents(flowScope) -- the sub-process's boundary timer
+      auto fit = ei_.find(v.flowScopeKey);
+      if (fit != ei_.end()) {
+        const OEl& fe = E(fit->second.value);
+        if (fe.type == ZBHIP_EL_SUB_PROCESS && fe.boundary >= 0) {
+          PiValue bv = fit->second.value;
+          bv.elem = fe.boundary;
+          subscribe_to_timer(P(bv.proc).els[fe.boundary], fit->first, bv);
+        }
+      }
     }
     transition_to_completed(el, key, v);
     for (int f : el.out) take_sequence_flow(key, v, f);
@@ -3493,8 +3582,9 @@ class Oracle {
     switch (intent) {
       case ZBHIP_PI_ELEMENT_ACTIVATING: {  // ProcessInstanceElementActivatingApplier.applyState (:48-77)
         // createEventScope (:255-289): job worker elements get an event scope
+        // (a sub-process only with events: its boundary event)
         if (ZBHIP_IS_JOB_WORKER(el.type) || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
-            el.type == ZBHIP_EL_BOUNDARY_EVENT)
+            el.type == ZBHIP_EL_BOUNDARY_EVENT || (el.type == ZBHIP_EL_SUB_PROCESS && el.boundary >= 0))
           event_scope_.insert(key);
         // cleanupSequenceFlowsTaken (:79-98): Tetris decrement of (flowScope, gateway)
         if (el.type == ZBHIP_EL_PARALLEL_GATEWAY) {

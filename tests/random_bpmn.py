@@ -8,7 +8,7 @@ join counters, a default flow on every exclusive split so no incident is raised)
 blocks -> end), never inside a parallel branch (one active instance per sub-process element).
 With ``boundaries`` a task outside parallel branches may carry a timer boundary event whose path
 ends in an end event or (interrupting ones) merges back after the task (one timer per instance at a
-time).  With ``multi_instance`` a task outside parallel branches may be a multi-instance activity over
+time; a sub-process may carry one too, with none inside it).  With ``multi_instance`` a task outside parallel branches may be a multi-instance activity over
 a static list (MultiInstanceActivityTest's shapes): parallel or sequential, the inputElement `x`, an
 outputCollection (its own name) of `= x` or `= loopCounter`, and -- sequential ones -- a
 completionCondition."""
@@ -91,11 +91,25 @@ class _Gen:
             sp = self.node("subProcess")
             self.flow(cur, sp)
             outer, self.scope = self.scope, sp
+            # a timer boundary event on the sub-process (then none inside it: one timer per instance)
+            timed = self.boundaries and int(r.integers(0, 3)) == 0
+            inner_b, self.boundaries = self.boundaries, self.boundaries and not timed
             st = self.node("startEvent")
             end = self.sequence(st, depth + 1, width)
             en = self.node("endEvent")
             self.flow(end, en)
             self.scope = outer
+            self.boundaries = inner_b
+            if timed:
+                cancel = bool(int(r.integers(0, 3)))
+                b = self.node("boundaryEvent", attached=sp, duration="PT%dS" % int(r.integers(1, 120)), cancel=cancel)
+                if not cancel or int(r.integers(0, 2)):
+                    self.flow(b, self.node("endEvent"))
+                    return sp
+                merge = self.node("exclusiveGateway")
+                self.flow(sp, merge)
+                self.flow(b, merge)
+                return merge
             return sp
         if c == "pass":  # elements without behaviour: undefined / manual task, none throw event
             t = self.node(("task", "manualTask", "intermediateThrowEvent")[int(r.integers(0, 3))])

@@ -9,7 +9,7 @@ import pytest
 
 from test_gpu_logserial import Pair
 from test_gpu_timers import _open_work, drive_timers, part_key
-from test_oracle_boundary import cycle_process, multiple_sequence_flows, non_interrupting_process
+from test_oracle_boundary import cycle_process, multiple_sequence_flows, non_interrupting_process, sub_process_boundary
 from test_oracle_timers import NOW
 from zeebe_amd import abi, bpmn
 from zeebe_amd.engine import Partition
@@ -57,7 +57,30 @@ def _non_interrupting_escalation():
     return b.serviceTask("b", "b").endEvent("e").done()
 
 
+def _sub_process_parallel(interrupting=True):
+    # a timer boundary event on a sub-process whose fork keeps two tasks active: PROCESS_INSTANCE_BATCH
+    # :TERMINATE terminates both (key order), then the sub-process, then the boundary event
+    b = bpmn.createExecutableProcess("process").startEvent("s").subProcess("sub").startEvent("ss").parallelGateway("fork")
+    b.serviceTask("x", "x").parallelGateway("join").moveToNode("fork").serviceTask("y", "y").connectTo("join")
+    b.endEvent("se").subProcessDone().boundaryEvent("late").cancelActivity(interrupting).timerWithDuration("PT20S")
+    b.serviceTask("late_task", "late").endEvent("le")
+    return b.moveToActivity("sub").serviceTask("after", "after").endEvent("e").done()
+
+
+def _nested_sub_processes():
+    # the boundary event on the outer sub-process: its termination reaches the inner one's task
+    b = bpmn.createExecutableProcess("process").startEvent("s").subProcess("outer").startEvent("os")
+    b.serviceTask("a", "a").subProcess("inner").startEvent("is").serviceTask("b", "b").endEvent("ie").subProcessDone()
+    b.endEvent("oe").subProcessDone().boundaryEvent("late").timerWithDuration("PT15S").endEvent("le")
+    return b.moveToActivity("outer").endEvent("e").done()
+
+
 SHAPES = {"multiple_sequence_flows": lambda: multiple_sequence_flows("PT30S"), "linear": _linear_with_boundary,
+          "sub_process": lambda: sub_process_boundary(True, "PT10S"),
+          "sub_process_non_interrupting": lambda: sub_process_boundary(False, "PT10S"),
+          "sub_process_parallel": _sub_process_parallel,
+          "sub_process_parallel_non_interrupting": lambda: _sub_process_parallel(False),
+          "nested_sub_processes": _nested_sub_processes,
           "non_interrupting": lambda: non_interrupting_process("PT30S"),
           "non_interrupting_escalation": _non_interrupting_escalation,
           "cycle_infinite": lambda: cycle_process("R/PT30S"), "cycle_r3": lambda: cycle_process("R3/PT10S"),
@@ -135,7 +158,7 @@ def test_gpu_random_processes_with_multi_instance_activities(seed):
 
 
 @pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch", "non_interrupting_escalation",
-                                   "cycle_r3"])
+                                   "cycle_r3", "sub_process", "sub_process_parallel", "nested_sub_processes"])
 def test_gpu_boundary_log_and_db_bytes(shape):
     pair = Pair(SHAPES[shape](), 100)
     for e in (pair.part, pair.orc):
@@ -151,7 +174,8 @@ def test_gpu_boundary_log_and_db_bytes(shape):
         pair.window(c)
 
 
-@pytest.mark.parametrize("shape", ["linear", "in_sub_process", "non_interrupting_escalation", "cycle_infinite"])
+@pytest.mark.parametrize("shape", ["linear", "in_sub_process", "non_interrupting_escalation", "cycle_infinite",
+                                   "sub_process", "sub_process_parallel_non_interrupting"])
 def test_gpu_boundary_restart_equivalence(shape):
     xml = SHAPES[shape]()
     n = 48

@@ -338,3 +338,27 @@ def test_pending_subscription_checkers_resend_lost_commands(lose):
     assert done == 30
     c = [p.adapter.counts for p in gpu.parts]
     assert all(x["fallbacks"] == 0 for x in c), [p.adapter.fallback_reasons for p in gpu.parts]
+
+
+def test_sub_process_boundary_timers_in_the_processing_loop():
+    """Timer boundary events on embedded sub-processes behind the adapter: the DueDateTimerChecker's
+    TIMER:TRIGGER terminates a sub-process (PROCESS_INSTANCE_BATCH:TERMINATE of its children, their jobs
+    canceled) before its boundary event, or -- non-interrupting -- runs the boundary path beside it;
+    jobs completed first cancel the timers.  Logs and state equal the engine-only loop's."""
+    from test_oracle_boundary import sub_process_boundary
+    from test_gpu_boundary import _sub_process_parallel
+    deps = [(sub_process_boundary(True, "PT10S"), KEY_A, 1), (_sub_process_parallel(False), KEY_B, 1)]
+    ref, gpu = single(deps, deps)
+    rng = np.random.default_rng(5)
+    write(ref, gpu, *([Client.create("process", key=KEY_A) for _ in range(6)] +
+                      [Client.create("process", key=KEY_B) for _ in range(6)]))
+    for t in range(6):
+        jobs = sorted(open_jobs(ref.parts[0].log))
+        done = [Client.complete_job(k) for k in jobs if rng.integers(0, 3) == 0]
+        if done:
+            write(ref, gpu, *done)
+        step(ref, gpu, 7000)
+    check(ref, gpu)
+    log = gpu.parts[0].log
+    assert any(r.value_type == abi.VT_PROCESS_INSTANCE_BATCH for r in log.entries)
+    assert gpu.parts[0].adapter.counts["fallbacks"] == 0, gpu.parts[0].adapter.fallback_reasons

@@ -369,3 +369,60 @@ def _ord(o, instance, key):
         if o.resolve(instance, i) == key:
             return i
     raise KeyError(key)
+
+
+def sub_process_boundary(interrupting=True, duration="PT1S"):
+    """BoundaryEventTest.shouldTerminateSubProcessBeforeTriggeringBoundaryEvent (:218-273): a timer
+    boundary event on an embedded sub-process holding a service task."""
+    b = bpmn.createExecutableProcess("process").startEvent().subProcess("sub").startEvent("subStart")
+    b.serviceTask("task", "type").endEvent("subEnd").subProcessDone()
+    b.boundaryEvent("timer").cancelActivity(interrupting).timerWithDuration(duration).endEvent("endTimer")
+    return b.moveToActivity("sub").endEvent("end").done()
+
+
+def test_terminate_sub_process_before_triggering_boundary_event():
+    # the golden tail of BoundaryEventTest.shouldTerminateSubProcessBeforeTriggeringBoundaryEvent: the
+    # timer (subscribed when the sub-process's start event completes) terminates the sub-process --
+    # PROCESS_INSTANCE_BATCH:TERMINATE of its children, the task's job canceled -- then the boundary event
+    o, recs = _started(sub_process_boundary())
+    created = [r for r in recs if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CREATED]
+    assert len(created) == 1 and _eid(o, created[0]) == "timer"
+    out = _trigger_all(o, recs)
+    want = [("TIMER", "TRIGGERED", "timer"), ("PROCESS_EVENT", "TRIGGERING", "timer"),
+            ("PROCESS_INSTANCE", "TERMINATE_ELEMENT", "sub"), ("PROCESS_INSTANCE", "ELEMENT_TERMINATING", "sub"),
+            ("PROCESS_INSTANCE_BATCH", "TERMINATE", "sub"), ("PROCESS_INSTANCE", "TERMINATE_ELEMENT", "task"),
+            ("PROCESS_INSTANCE", "ELEMENT_TERMINATING", "task"), ("JOB", "CANCELED", "task"),
+            ("PROCESS_INSTANCE", "ELEMENT_TERMINATED", "task"), ("PROCESS_INSTANCE", "ELEMENT_TERMINATED", "sub"),
+            ("PROCESS_EVENT", "TRIGGERED", "timer"), ("PROCESS_INSTANCE", "ELEMENT_ACTIVATING", "timer"),
+            ("PROCESS_INSTANCE", "ELEMENT_ACTIVATED", "timer"), ("PROCESS_INSTANCE", "COMPLETE_ELEMENT", "timer"),
+            ("PROCESS_INSTANCE", "ELEMENT_COMPLETING", "timer"), ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "timer")]
+    got = [_tuple(o, r) for r in out]
+    end = got.index(("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "timer")) + 1
+    assert got[end - len(want):end] == want
+    assert got[-1] == ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "process")
+    assert [r for r in o.state() if not r.startswith("KEY|")] == []
+
+
+def test_sub_process_boundary_timer_cancelled_on_completion():
+    # SubProcessProcessor.onComplete: unsubscribeFromEvents -- the job completes, the sub-process
+    # completes and its boundary timer is canceled (TIMER:CANCELED before ELEMENT_COMPLETED of sub)
+    o, recs = _started(sub_process_boundary())
+    out = _complete_jobs(o, recs)
+    got = [_tuple(o, r) for r in out]
+    i = got.index(("TIMER", "CANCELED", "timer"))
+    assert got[i - 1] == ("PROCESS_INSTANCE", "ELEMENT_COMPLETING", "sub")
+    assert got[i + 1] == ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "sub")
+    assert got[-1] == ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "process")
+    assert [r for r in o.state() if not r.startswith("KEY|")] == []
+
+
+def test_non_interrupting_sub_process_boundary_keeps_the_sub_process():
+    o, recs = _started(sub_process_boundary(False))
+    out = _trigger_all(o, recs)
+    got = [_tuple(o, r) for r in out]
+    assert ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "endTimer") in got
+    assert not any(t[1] in ("TERMINATE_ELEMENT", "ELEMENT_TERMINATING") for t in got)
+    st = o.state()
+    assert any("elementId=task" in r for r in st if r.startswith("ELEMENT_INSTANCE_KEY"))
+    out = _complete_jobs(o, recs)
+    assert _tuple(o, out[-1]) == ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "process")

@@ -66,7 +66,7 @@ PMS_CREATING, PMS_CREATE, PMS_CREATED, PMS_CORRELATE, PMS_CORRELATED = 0, 1, 2, 
 PMS_DELETING, PMS_DELETE, PMS_DELETED = 5, 6, 7
 VALUE_TYPES = {0: "JOB", 5: "PROCESS_INSTANCE", 10: "MESSAGE", 11: "MESSAGE_SUBSCRIPTION",
                12: "PROCESS_MESSAGE_SUBSCRIPTION", 17: "VARIABLE", 19: "PROCESS_INSTANCE_CREATION",
-               24: "PROCESS_EVENT", 15: "TIMER"}
+               24: "PROCESS_EVENT", 15: "TIMER", 34: "PROCESS_INSTANCE_BATCH"}
 RECORD_TYPES = {0: "EVENT", 1: "COMMAND", 2: "COMMAND_REJECTION"}
 REJECTION_TYPES = {0: "INVALID_ARGUMENT", 1: "NOT_FOUND", 2: "ALREADY_EXISTS", 3: "INVALID_STATE",
                    4: "PROCESSING_ERROR", 255: "NULL_VAL"}

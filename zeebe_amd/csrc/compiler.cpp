@@ -935,12 +935,16 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     auto it = index.find(ref);
     if (it == index.end()) { err = "boundary event attached to an unknown element " + ref; return ZBHIP_EPARSE; }
     zbhip_element& A = C.elements[it->second];
-    if (!ZBHIP_IS_JOB_WORKER(A.element_type) || A.flow_scope != C.elements[b].flow_scope) {
-      err = "boundary event on an element outside the supported subset (job worker tasks only)";
+    // job worker tasks; embedded sub-processes with a timer boundary event (the sub-process keeps it
+    // in default_flow: its start_event is its none start event)
+    const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS && C.elements[b].event_type == ZBHIP_EV_TIMER;
+    if ((!ZBHIP_IS_JOB_WORKER(A.element_type) && !on_sub) || A.flow_scope != C.elements[b].flow_scope) {
+      err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return ZBHIP_EUNSUPP;
     }
-    if (A.start_event != ZBHIP_NONE16) { err = "more than one boundary event on an activity outside the supported subset"; return ZBHIP_EUNSUPP; }
-    A.start_event = b;
+    uint16_t& slot = on_sub ? A.default_flow : A.start_event;
+    if (slot != ZBHIP_NONE16) { err = "more than one boundary event on an activity outside the supported subset"; return ZBHIP_EUNSUPP; }
+    slot = b;
     C.elements[b].flow_source = it->second;
   }
   for (size_t e = 1; e < C.elements.size(); ++e)

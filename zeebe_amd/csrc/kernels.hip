@@ -363,9 +363,10 @@ __device__ __forceinline__ void qput(Lane<K>& L, int i, uint32_t v) {
   }
 }
 
-// queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | (K::M local command) << 14 |
-// terminate (K::S TERMINATE_ELEMENT) << 15 | key << 16
+// queue entry: elem (12) | complete (1) << 12 | fs_is_pi (1) << 13 | (K::M local command; K::S with
+// Q_TERM: PROCESS_INSTANCE_BATCH:TERMINATE) << 14 | terminate (K::S TERMINATE_ELEMENT) << 15 | key << 16
 constexpr uint32_t Q_TERM = 1u << 15;
+constexpr uint32_t Q_PIBT = 1u << 14;
 __device__ __forceinline__ uint32_t qentry(uint32_t elem, bool complete, bool fs_pi, uint32_t key) {
   return elem | (complete ? 1u << 12 : 0u) | (fs_pi ? 1u << 13 : 0u) | (key << 16);
 }
@@ -1694,31 +1695,99 @@ __device__ __forceinline__ void cancel_timer(Lane<K>& L) {
   L.tm_due = 0;
 }
 
-// TERMINATE_ELEMENT of a job worker task whose interrupting boundary event was triggered:
-// ProcessInstanceStateTransitionGuard (:60-64), transitionToTerminating, then
-// JobWorkerTaskProcessor.onTerminate (task/JobWorkerTaskProcessor.java:77-104): cancelJob
-// (JOB:CANCELED, BpmnJobBehavior.java:251-274), unsubscribeFromEvents, findEventTrigger ->
-// transitionToTerminated (ProcessInstanceElementTerminatedApplier: the instance removed like a
-// completed one) and EventTriggerBehavior.activateTriggeredEvent (EventTriggerBehavior.java:191-244):
-// PROCESS_EVENT:TRIGGERED, the boundary event ACTIVATING + ACTIVATED (+key, flow scope = the
-// activity's), COMPLETE_ELEMENT
+// BpmnStateTransitionBehavior.onElementTerminated (:419-441) of a child of container c: the
+// container's onChildTerminated.  A sub-process (SubProcessProcessor.onChildTerminated :108-160) with no
+// active child left: with its boundary event's trigger (the flow scope active) transitionToTerminated
+// and activateTriggeredEvent; terminated by its own flow scope, transitionToTerminated and the same one
+// level up.  Children of the process (a cancel) or of a multi-instance body: outside the subset.
+template <class K>
+__device__ __forceinline__ void child_terminated(Lane<K>& L, uint32_t c) {
+  if constexpr (K::S) {
+    for (int d = 0; d < kMaxDepth; ++d) {
+      if (c == 0) { set_fail(L, FB_UNSUPPORTED); return; }
+      const uint4 cw = elem_of(L, c);
+      if (etype(cw) != ZBHIP_EL_SUB_PROCESS) { set_fail(L, FB_UNSUPPORTED); return; }
+      const int tc = scope_find(L, c);
+      if (tc < 0) { set_fail(L, FB_UNSUPPORTED); return; }
+      const uint2 ce = tget(L, tc);
+      if ((ce.y & 0xFF) != 0) return;  // canBeTerminated: a child is still active
+      const uint32_t ckey = ce.x >> 16, cst = (ce.y >> 16) & 0xFF;
+      const uint32_t pc = scope_of<K>(cw);
+      const uint32_t pfsa = scope_key(L, pc);
+      const uint32_t pst = pc == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, pc)).y >> 16) & 0xFF;
+      const uint32_t target = cw.w & 0xFFFF;  // the sub-process's boundary event
+      if (L.trig_key == ckey && L.trig_evt != NONE && pst == ZBHIP_PI_ELEMENT_ACTIVATED && target != 0xFFFF) {
+        const uint32_t pe = L.trig_evt;
+        emit(L, ZBHIP_PI_ELEMENT_TERMINATED, ckey, pfsa, c);
+        apply_completed_child(L, tc, ckey);
+        L.trig_evt = NONE;
+        activate_triggered_event(L, pe, ckey, target, pfsa);
+        return;
+      }
+      if (cst != ZBHIP_PI_ELEMENT_TERMINATING) return;
+      emit(L, ZBHIP_PI_ELEMENT_TERMINATED, ckey, pfsa, c);
+      apply_completed_child(L, tc, ckey);
+      c = pc;
+    }
+    set_fail(L, FB_UNSUPPORTED);
+  } else {
+    (void)c;
+    set_fail(L, FB_UNSUPPORTED);
+  }
+}
+
+// TERMINATE_ELEMENT (ProcessInstanceStateTransitionGuard :60-64, transitionToTerminating), then the
+// processor's onTerminate:
+// - a job worker task (JobWorkerTaskProcessor.onTerminate, task/JobWorkerTaskProcessor.java:77-104):
+//   cancelJob (JOB:CANCELED, BpmnJobBehavior.java:251-274), unsubscribeFromEvents, then findEventTrigger
+//   while its flow scope is active: transitionToTerminated (the instance removed like a completed one)
+//   and EventTriggerBehavior.activateTriggeredEvent (EventTriggerBehavior.java:191-244: PROCESS_EVENT
+//   :TRIGGERED, the boundary event ACTIVATING + ACTIVATED (+key, the activity's flow scope),
+//   COMPLETE_ELEMENT); without one (terminated by its flow scope) transitionToTerminated and
+//   onElementTerminated;
+// - an intermediate catch event: unsubscribeFromEvents, transitionToTerminated, onElementTerminated;
+// - a sub-process (SubProcessProcessor.onTerminate :84-95): unsubscribeFromEvents (its boundary
+//   timer), terminateChildInstances (BpmnStateTransitionBehavior.java:348-363): with children
+//   PROCESS_INSTANCE_BATCH:TERMINATE (+key), else onChildTerminated at once
 template <class K>
 __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w, uint32_t key, uint32_t fsa) {
   const int t = tbl_find(L, key);
   const uint32_t st = t < 0 ? 0u : (tget(L, t).y >> 16) & 0xFF;
-  if (t < 0 || !ZBHIP_IS_JOB_WORKER(etype(w)) ||
+  const uint32_t type = etype(w);
+  const bool ok_type = ZBHIP_IS_JOB_WORKER(type) || (K::S && (type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT));
+  if (t < 0 || !ok_type ||
       (st != ZBHIP_PI_ELEMENT_ACTIVATING && st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING)) {
     set_fail(L, FB_UNSUPPORTED);
     return;
   }
+  const uint32_t c = scope_of<K>(w);
+  if constexpr (K::S) {
+    if (type == ZBHIP_EL_SUB_PROCESS) {
+      const uint32_t nch = tget(L, t).y & 0xFF;  // childCount
+      // the termination's commands stay in this batch (the trigger's context travels in the lane)
+      if (pending(L) + L.processed + 2 + nch >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
+      emit(L, ZBHIP_PI_ELEMENT_TERMINATING, key, fsa, elem);
+      tbl_set_state(L, t, ZBHIP_PI_ELEMENT_TERMINATING);
+      if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == key) cancel_timer(L);
+      if (nch == 0) {
+        child_terminated(L, elem);  // onChildTerminated(element, terminating, null)
+      } else {
+        const uint32_t kb = new_key(L);
+        follow_up(L, C_PIB_TERMINATE, kb, key, elem, false, false, key, Q_TERM | Q_PIBT);
+      }
+      return;
+    }
+  }
   emit(L, ZBHIP_PI_ELEMENT_TERMINATING, key, fsa, elem);
   tbl_set_state(L, t, ZBHIP_PI_ELEMENT_TERMINATING);
   const uint2 e = tget(L, t);
-  const uint32_t job = e.y & 0xFFFF;
-  // (flag 1: the job was ACTIVATED -- its record carries the stored deadline and worker)
-  if (((e.y >> 24) & 1u) && job != JOB_ZERO && job != JOB_MINUS1) {
-    emit(L, C_JOB_CANCELED, job, key, elem, (e.y >> 25) & 1u);
-    if ((e.y >> 25) & 1u) note_activation(L, job, L.inst);
+  if (ZBHIP_IS_JOB_WORKER(type)) {
+    const uint32_t job = e.y & 0xFFFF;
+    // (flag 1: the job was ACTIVATED -- its record carries the stored deadline and worker)
+    if (((e.y >> 24) & 1u) && job != JOB_ZERO && job != JOB_MINUS1) {
+      emit(L, C_JOB_CANCELED, job, key, elem, (e.y >> 25) & 1u);
+      if ((e.y >> 25) & 1u) note_activation(L, job, L.inst);
+    }
   }
   if constexpr (K::S) {  // unsubscribeFromEvents: the timer, then message subscriptions
     if ((L.tm_y >> 31) && (L.tm_y & 0xFFFF) == key) cancel_timer(L);
@@ -1727,18 +1796,53 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
     if (((L.pm_x >> 12) & 3) != 0 && (L.pm_y & 0xFFFF) == key) unsubscribe_message(L);
     if (L.fail) return;
   }
-  const uint32_t c = scope_of<K>(w);
   const uint32_t fst = c == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, c)).y >> 16) & 0xFF;
-  const uint32_t target = w.w & 0xFFFF;  // the activity's boundary event
-  if (L.trig_key != key || L.trig_evt == NONE || fst != ZBHIP_PI_ELEMENT_ACTIVATED || target == 0xFFFF) {
-    set_fail(L, FB_UNSUPPORTED);  // a termination without an event trigger (onElementTerminated)
+  const uint32_t target = ZBHIP_IS_JOB_WORKER(type) ? w.w & 0xFFFF : 0xFFFFu;  // the activity's boundary event
+  if (L.trig_key == key && L.trig_evt != NONE && fst == ZBHIP_PI_ELEMENT_ACTIVATED && target != 0xFFFF) {
+    const uint32_t pe = L.trig_evt;
+    emit(L, ZBHIP_PI_ELEMENT_TERMINATED, key, fsa, elem);
+    apply_completed_child(L, t, key);  // removeInstance; the event scope with its trigger
+    L.trig_evt = NONE;
+    activate_triggered_event(L, pe, key, target, fsa);
     return;
   }
-  const uint32_t pe = L.trig_evt;
+  // terminated by its flow scope: transitionToTerminated, onElementTerminated
   emit(L, ZBHIP_PI_ELEMENT_TERMINATED, key, fsa, elem);
-  apply_completed_child(L, t, key);  // removeInstance; the event scope with its trigger
-  L.trig_evt = NONE;
-  activate_triggered_event(L, pe, key, target, fsa);
+  apply_completed_child(L, t, key);
+  child_terminated(L, c);
+}
+
+// TerminateProcessInstanceBatchProcessor (processing/processinstance/TerminateProcessInstanceBatchProcessor
+// .java:38-85): TERMINATE_ELEMENT of every child of the container that can terminate (ACTIVATING /
+// ACTIVATED / COMPLETING), in ELEMENT_INSTANCE_PARENT_CHILD (child key) order
+template <class K>
+__device__ __forceinline__ void terminate_batch(Lane<K>& L, uint32_t container, uint32_t ckey) {
+  if constexpr (K::S) {
+    static_assert(K::T <= 32, "one mask bit per table entry");
+    uint32_t done = 0;
+    for (int it = 0; it < K::T && !L.fail; ++it) {
+      int best = -1;
+      uint32_t bk = 0xFFFFFFFFu;
+      for (int t = 0; t < L.nt; ++t) {
+        if ((done >> t) & 1u) continue;
+        const uint2 e = tget(L, t);
+        if (e.x == 0xFFFFFFFFu) continue;
+        const uint32_t el = e.x & 0xFFFF, k = e.x >> 16, st = (e.y >> 16) & 0xFF;
+        if (scope_of<K>(elem_of(L, el)) != container || (st != ZBHIP_PI_ELEMENT_ACTIVATING &&
+            st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING))
+          continue;
+        if (k < bk) { bk = k; best = t; }
+      }
+      if (best < 0) return;
+      done |= 1u << best;
+      const uint32_t el = tget(L, best).x & 0xFFFF;
+      follow_up(L, ZBHIP_PI_TERMINATE_ELEMENT, bk, ckey, el, false, false, bk, Q_TERM);
+    }
+  } else {
+    (void)container;
+    (void)ckey;
+    set_fail(L, FB_UNSUPPORTED);
+  }
 }
 
 // ActivateProcessInstanceBatchProcessor.processRecord (processing/processinstance/
@@ -1785,7 +1889,8 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       raux = fsa;
     }
     if (entry & Q_TERM) {
-      if (complete) activate_batch(L, elem, w);  // PROCESS_INSTANCE_BATCH:ACTIVATE of a body
+      if (entry & Q_PIBT) terminate_batch(L, elem, cmd_key);  // PROCESS_INSTANCE_BATCH:TERMINATE of a container
+      else if (complete) activate_batch(L, elem, w);         // PROCESS_INSTANCE_BATCH:ACTIVATE of a body
       else terminate_pi(L, elem, w, cmd_key, fsa);
       return;
     }
@@ -2136,8 +2241,27 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
   merged:;
   }
   if constexpr (K::S) {
-    // JobWorkerTaskProcessor.onComplete (:63-75): unsubscribeFromEvents -- the boundary event's timer
-    if (ZBHIP_IS_JOB_WORKER(type) && (L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key) cancel_timer(L);
+    // JobWorkerTaskProcessor.onComplete (:63-75), SubProcessProcessor.onComplete (:68-82):
+    // unsubscribeFromEvents -- the boundary event's timer
+    if ((ZBHIP_IS_JOB_WORKER(type) || type == ZBHIP_EL_SUB_PROCESS) && (L.tm_y >> 31) && (L.tm_y & 0xFFFF) == cmd_key)
+      cancel_timer(L);
+    // StartEventProcessor.onComplete (:52-67): subscribeToEvents of the flow scope -- a sub-process's
+    // timer boundary event (CatchEventBehavior.subscribeToTimerEvent: dueDate = now + duration)
+    if (type == ZBHIP_EL_START_EVENT && c != 0) {
+      const uint4 cw = elem_of(L, c);
+      const uint32_t b = cw.w & 0xFFFF;
+      if (etype(cw) == ZBHIP_EL_SUB_PROCESS && b != 0xFFFF) {
+        if (!L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
+        const uint32_t ck = scope_key(L, c);
+        const uint4 bw = elem_of(L, b);
+        const uint32_t reps = (bw.w >> 8) & 0xFF;  // 1 a duration, a cycle's count, 255 infinite
+        const uint32_t tk = new_key(L);
+        L.tm_x = b | (tk << 16);
+        L.tm_y = ck | (reps << 16) | (1u << 31);
+        L.tm_due = L.sp->now_ms + (long long)bw.z;
+        emit(L, C_TIMER_CREATED, tk, ck, b, reps);
+      }
+    }
   }
   if constexpr (K::IO) {
     // MultiInstanceBodyProcessor.onComplete (:100-114): propagateVariable of the outputCollection

@@ -1312,9 +1312,11 @@ static int rebuild_program(zbhip_handle* h) {
         w[2] = E.duration_ms;
       else if (E.element_type == ZBHIP_EL_SUB_PROCESS) w[2] = E.start_event | (join_mask[e] << 16);
       else w[2] = 0xFFFFFFFFu;
-      // a job worker's join_slot half: its boundary event (zbhip_element.start_event), 0xFFFF if none
-      // a boundary event's: 1 if interrupting (zbhip_element.job_retries)
+      // a job worker's join_slot half: its boundary event (zbhip_element.start_event), 0xFFFF if none;
+      // a sub-process's: its boundary event (zbhip_element.default_flow); a boundary event's: 1 if
+      // interrupting (zbhip_element.job_retries)
       const uint32_t low = ZBHIP_IS_JOB_WORKER(E.element_type) ? E.start_event
+                           : E.element_type == ZBHIP_EL_SUB_PROCESS ? E.default_flow
                            : E.element_type == ZBHIP_EL_BOUNDARY_EVENT ? E.job_retries : E.join_slot;
       w[3] = low | ((uint32_t)E.flow_scope << 16);
       if (const Proc::Mi* m = E.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY ? P.mi_body(e) : nullptr) {
@@ -1391,7 +1393,10 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       const bool msg = E.event_type == ZBHIP_EV_MESSAGE && E.flow_scope == 0;
       if ((E.event_type != ZBHIP_EV_TIMER && !msg) || E.flow_source >= P.els.size()) return ZBHIP_EUNSUPP;
       const zbhip_element& A = P.els[E.flow_source];
-      if (!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e || A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
+      // (a timer boundary event on an embedded sub-process: zbhip_element.default_flow of the sub-process)
+      const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS && E.event_type == ZBHIP_EV_TIMER && A.default_flow == e;
+      if ((!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e) && !on_sub) return ZBHIP_EINVAL;
+      if (A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
     } else if (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) {
       if (E.start_event >= P.els.size() || P.els[E.start_event].element_type != ZBHIP_EL_BOUNDARY_EVENT) return ZBHIP_EINVAL;
     }
@@ -3161,6 +3166,15 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
         auto it = h->cont_ids.find(((uint64_t)c << 16) | ord);
         if (it != h->cont_ids.end()) r.aux = (int64_t)it->second;
       }
+    } else if (c6 == C_PIB_TERMINATE) {
+      // PROCESS_INSTANCE_BATCH:TERMINATE (terminateChildInstances): batchElementInstanceKey = the
+      // container (scope_key), index -1
+      r.value_type = ZBHIP_VT_PROCESS_INSTANCE_BATCH;
+      r.intent = ZBHIP_PIB_TERMINATE;
+      r.record_type = ZBHIP_RT_COMMAND;
+      r.partition = -1;
+      r.unprocessed = (fl & F_UNPROCESSED) ? 1 : 0;
+      if (r.unprocessed) return ZBHIP_EDEVICE;  // (the kernel keeps terminations in their batch)
     } else if (c6 == C_PE_TRIGGERING || c6 == C_PE_TRIGGERED) {
       r.value_type = ZBHIP_VT_PROCESS_EVENT;
       r.intent = c6 == C_PE_TRIGGERING ? ZBHIP_PE_TRIGGERING : ZBHIP_PE_TRIGGERED;
@@ -3910,15 +3924,19 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       snprintf(buf, sizeof buf, "INCIDENT_PROCESS_INSTANCES|%lld|%lld", k, ik);
       sink(ctx, buf);
     }
+    const bool sub_bnd = E.element_type == ZBHIP_EL_SUB_PROCESS && E.default_flow != ZBHIP_NONE16 &&
+                         E.default_flow < P.els.size();
     if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
-        E.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
+        E.element_type == ZBHIP_EL_BOUNDARY_EVENT || sub_bnd) {
       // EventScopeInstance.java:25-35: a catch / boundary event's interrupting ids are its own id
-      // (ExecutableCatchEventElement.java:124-132), a job worker's those of its interrupting
-      // boundary event, which is also its boundaryElementIds (ExecutableActivity.java:28-38)
+      // (ExecutableCatchEventElement.java:124-132), a job worker's (a sub-process's: an event scope
+      // only with events) those of its interrupting boundary event, which is also its
+      // boundaryElementIds (ExecutableActivity.java:28-38)
       const bool own = E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT;
-      const bool bnd = ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16;
-      const std::string ids = own ? P.id(elem) : bnd ? P.id(E.start_event) : std::string();
-      const bool intr = own || (bnd && (P.els[E.start_event].job_retries & 1));  // cancelActivity boundary events only
+      const uint16_t be = sub_bnd ? E.default_flow : E.start_event;
+      const bool bnd = (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) || sub_bnd;
+      const std::string ids = own ? P.id(elem) : bnd ? P.id(be) : std::string();
+      const bool intr = own || (bnd && (P.els[be].job_retries & 1));  // cancelActivity boundary events only
       snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=%s", k,
                intr ? ids.c_str() : "", bnd ? ids.c_str() : "");
       sink(ctx, buf);

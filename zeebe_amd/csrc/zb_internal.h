@@ -82,6 +82,8 @@ enum : uint8_t {
                           // aux = the inner instance, elem = the body, flags = the loop counter
   C_PIB_ACTIVATE = 26,    // PROCESS_INSTANCE_BATCH:ACTIVATE (command): aux = the body, elem = the body,
                           // flags = the collection's size (the record's index) | F_UNPROCESSED
+  C_PIB_TERMINATE = 27,   // PROCESS_INSTANCE_BATCH:TERMINATE (terminateChildInstances, command): aux = the
+                          // container instance, elem = the container (index -1: from the first child)
   C_PE_TRIGGERING = 24,
   C_PE_TRIGGERED = 25,    // EventTriggerBehavior.processEventTriggered
   C_PIC_CREATED = 28,
