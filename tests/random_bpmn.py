@@ -10,8 +10,7 @@ With ``boundaries`` a task outside parallel branches may carry a timer boundary 
 ends in an end event or (interrupting ones) merges back after the task (one timer per instance at a
 time; a sub-process may carry one too, with none inside it).  With ``multi_instance`` a task outside parallel branches may be a multi-instance activity over
 a static list (MultiInstanceActivityTest's shapes): parallel or sequential, the inputElement `x`, an
-outputCollection (its own name) of `= x` or `= loopCounter`, and -- sequential ones -- a
-completionCondition."""
+outputCollection (its own name) of `= x` or `= loopCounter`, and a completionCondition."""
 from xml.sax.saxutils import escape, quoteattr
 
 BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
@@ -127,7 +126,7 @@ class _Gen:
                 loop = {"seq": seq, "coll": "= [%s]" % ", ".join(map(str, items))}
                 if int(r.integers(0, 2)):
                     loop["out"] = ("= x", "= loopCounter")[int(r.integers(0, 2))]
-                if seq and int(r.integers(0, 2)):
+                if int(r.integers(0, 2)):
                     loop["cond"] = ("= x >= 3", "= numberOfCompletedInstances >= 2", "= loopCounter = 2")[int(r.integers(0, 3))]
                 self.nodes[-1][2]["loop"] = loop
                 return t

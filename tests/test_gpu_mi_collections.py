@@ -6,9 +6,10 @@ with the inner instance's own variables and the body's numberOf* as its primary 
 
 The workloads of tests/test_oracle_mi_collections.py (pinned there on MultiInstanceActivityTest.java)
 run through the loop over the engine alone and over [adapter, engine] at batch limits 3 and 100: every
-log (record, key, value -- lists as tuples --, position) and every state row equal.  What the device
-leaves to the engine (a satisfied condition with other inner instances active: PROCESS_INSTANCE_BATCH
-:TERMINATE; a batch past the limit) goes there with the instance, through the hand-off's state rows."""
+log (record, key, value -- lists as tuples --, position) and every state row equal.  A satisfied
+condition with other inner instances active terminates them on the device (PROCESS_INSTANCE_BATCH
+:TERMINATE); a batch past the limit goes to the engine with the instance, through the hand-off's
+state rows."""
 import numpy as np
 import pytest
 
@@ -75,9 +76,9 @@ def test_completion_conditions(mode, seq, cond, jobs):
     write(ref, gpu, *[Client.complete_job(k, (("result", 1),)) for k in live])
     check(ref, gpu)
     ad = gpu.parts[0].adapter
-    # the parallel form of a satisfied condition with other inner instances active goes to the engine
-    if not seq and cond != "= false":
-        assert ad.counts["fallbacks"] > 0
+    # the parallel form of a satisfied condition terminates the other inner instances on the device
+    # (PROCESS_INSTANCE_BATCH:TERMINATE)
+    assert ad.counts["fallbacks"] == 0, ad.fallback_reasons
 
 
 def test_restart_keeps_the_collections():

@@ -1156,16 +1156,23 @@ __device__ __forceinline__ void transition_to_completed_child(Lane<K>& L, int t,
       const uint4 cw = elem_of(L, c);
       if (etype(cw) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
         // MultiInstanceBodyProcessor.afterExecutionPathCompleted (:193-230): a satisfied completion
-        // condition completes the body (terminateChildInstances of other active children --
-        // PROCESS_INSTANCE_BATCH:TERMINATE -- is outside the device subset); else a sequential body
-        // activates its next inner instance while items are left, and the body completes once no child
-        // is active
+        // condition terminates the other active children (terminateChildInstances,
+        // BpmnStateTransitionBehavior.java:348-363: PROCESS_INSTANCE_BATCH:TERMINATE) and completes the
+        // body at once when none is (else onChildTerminated does, child_terminated); otherwise a
+        // sequential body activates its next inner instance while items are left, and the body
+        // completes once no child is active
         if (ts < 0) { set_fail(L, FB_UNSUPPORTED); return; }
         const uint2 be = tget(L, ts);
         const uint32_t sk = be.x >> 16, loop = (be.y >> 8) & 0xFF;
         if (satisfied) {
-          if ((be.y & 0xFF) != 0) { set_fail(L, FB_UNSUPPORTED); return; }
-          const uint32_t pc = scope_of<K>(cw);
+          const uint32_t pc = scope_of<K>(cw), nch = be.y & 0xFF;
+          if (nch != 0) {
+            // (the terminations and the body's completion stay in this batch: their context is the lane's)
+            if (pending(L) + L.processed + 3 + nch >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
+            const uint32_t kb = new_key(L);
+            follow_up(L, C_PIB_TERMINATE, kb, sk, c, false, false, sk, Q_TERM | Q_PIBT);
+            return;
+          }
           follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, sk, scope_key(L, pc), c, true, pc == 0, sk);
           return;
         }
@@ -1706,14 +1713,22 @@ __device__ __forceinline__ void child_terminated(Lane<K>& L, uint32_t c) {
     for (int d = 0; d < kMaxDepth; ++d) {
       if (c == 0) { set_fail(L, FB_UNSUPPORTED); return; }
       const uint4 cw = elem_of(L, c);
-      if (etype(cw) != ZBHIP_EL_SUB_PROCESS) { set_fail(L, FB_UNSUPPORTED); return; }
+      const uint32_t ct = etype(cw);
+      if (ct != ZBHIP_EL_SUB_PROCESS && ct != ZBHIP_EL_MULTI_INSTANCE_BODY) { set_fail(L, FB_UNSUPPORTED); return; }
       const int tc = scope_find(L, c);
       if (tc < 0) { set_fail(L, FB_UNSUPPORTED); return; }
       const uint2 ce = tget(L, tc);
-      if ((ce.y & 0xFF) != 0) return;  // canBeTerminated: a child is still active
       const uint32_t ckey = ce.x >> 16, cst = (ce.y >> 16) & 0xFF;
       const uint32_t pc = scope_of<K>(cw);
       const uint32_t pfsa = scope_key(L, pc);
+      if (ct == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+        // MultiInstanceBodyProcessor.onChildTerminated (:232-247): a body that is not terminating (its
+        // completion condition was met) completes once no child is active
+        if (cst == ZBHIP_PI_ELEMENT_TERMINATING) { set_fail(L, FB_UNSUPPORTED); return; }
+        if ((ce.y & 0xFF) == 0) follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, ckey, pfsa, c, true, pc == 0, ckey);
+        return;
+      }
+      if ((ce.y & 0xFF) != 0) return;  // canBeTerminated: a child is still active
       const uint32_t pst = pc == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, pc)).y >> 16) & 0xFF;
       const uint32_t target = cw.w & 0xFFFF;  // the sub-process's boundary event
       if (L.trig_key == ckey && L.trig_evt != NONE && pst == ZBHIP_PI_ELEMENT_ACTIVATED && target != 0xFFFF) {
