@@ -920,26 +920,21 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
   }
 }
 
-// pass 2, streaming form (the templates and their descriptors fit LDS next to the waves' stages):
-// one wave per contiguous range of commands, taken in blocks of up to kStreamCmds commands /
-// kStreamRecs records.  A block's command rows and key sets go into the lanes' registers (lane k:
-// command k of the block, read out uniformly with v_readlane), its records' template info and rows
-// into the wave's LDS by direct global->LDS loads.  Those are the wave's only vector-memory loads, so
-// its only drain of outstanding stores is once per block: the ~128 KB of a block stream out without
-// a wait (k_log_write waited for its group's stores before every group's metadata loads).  Per record
-// the whole wave composes the entry into the stage: lane w copies template word w (LDS to LDS,
-// consecutive words: no bank conflicts), lanes 0-3 write the header's position / source position /
-// key / timestamp, lanes 0-15 the big-endian processInstanceKey / scope key bytes.  A full stage, a
-// composed entry (k_log_compose writes it) or the command's end flushes the stage in 16-byte chunks.
-#ifndef ZB_STREAM_WAVES
-#define ZB_STREAM_WAVES 16  // 4 waves per SIMD (one 1024-thread workgroup per CU)
-#endif
-constexpr uint32_t kStreamWaves = ZB_STREAM_WAVES;
-constexpr uint32_t kStreamCmds = 32;
-constexpr uint32_t kStreamRecs = 128;
-constexpr uint32_t kStreamStage = 3072;
-constexpr uint32_t kStreamWaveLds = kStreamStage + kStreamRecs * 12;  // stage, rinfo, rows
-constexpr uint32_t kStreamLdsMax = 160 * 1024;
+// pass 2, block form (the templates and their descriptors fit LDS beside the waves' areas): one
+// wave per contiguous range of commands, taken in blocks of up to kBlkCmds commands / kBlkRecs
+// records.  A block's command rows and key sets go into the lanes' registers (lane k: command k of
+// the block, read out uniformly with v_readlane), its records' template info and rows into the
+// wave's LDS by direct global->LDS loads.  Those are the wave's only vector-memory loads, so it waits
+// for its outstanding stores once per block (~100 KB), not once per group as k_log_write does (on
+// gfx950 s_waitcnt vmcnt counts stores too: k_log_write's waves spent 62 % of their cycles there).
+// Within a command, lane j composes entry j of a group of 64 into the wave's LDS stage as k_log_write
+// does (one lane per entry: a wave instruction copies 64 entries' words, ~10x fewer instructions per
+// byte than composing entry by entry with the whole wave, k_log_stream in round 4), the prefix of the
+// group that fits the stage at a time, and the wave streams the stage out in 16-byte non-temporal
+// chunks, 1 KB of whole lines per store instruction.
+constexpr uint32_t kBlkCmds = 32;
+constexpr uint32_t kBlkRecs = 192;
+constexpr uint32_t kBlkLdsMax = 160 * 1024;
 
 typedef __attribute__((address_space(1))) void g_void;
 typedef __attribute__((address_space(3))) void l_void;
@@ -948,43 +943,31 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t k) { return __builti
 __device__ __forceinline__ unsigned long long rl64(unsigned long long v, uint32_t k) {
   return (unsigned long long)rl((uint32_t)v, k) | (unsigned long long)rl((uint32_t)(v >> 32), k) << 32;
 }
-
 // orders one wave's LDS accesses across its lanes for the compiler (the hardware keeps a wave's LDS
 // operations in order)
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
-
-// the stage's bytes [gs, ge) out (stage byte 0 = output byte sb = gs & ~15): whole 16-byte chunks, and
-// the 8-byte half of a chunk shared with the neighbouring group
-__device__ __forceinline__ void stream_flush(uint8_t* obase, const uint8_t* stage, uint32_t sb, uint32_t gs,
-                                             uint32_t ge, uint32_t lane) {
-  // (offsets relative to obase, a 16-byte aligned output address: 32-bit arithmetic)
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  wave_lds_sync();  // (the stage's words, written by other lanes, before the chunk reads)
-  for (uint32_t o = sb + 16u * lane; o < ge; o += 1024u) {
-    const uint4 v = *reinterpret_cast<const uint4*>(stage + (o - sb));
-    const bool h0 = o >= gs && o + 8 <= ge, h1 = o + 8 >= gs && o + 16 <= ge;
-    if (h0 && h1) {
-      u32x4 q;
-      q.x = v.x; q.y = v.y; q.z = v.z; q.w = v.w;
-      __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(obase + o));
-    } else if (h0) {
-      u32x2 q;
-      q.x = v.x; q.y = v.y;
-      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(obase + o));
-    } else if (h1) {
-      u32x2 q;
-      q.x = v.z; q.y = v.w;
-      __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(obase + o + 8));
-    }
-  }
-  wave_lds_sync();  // (the chunk reads before the next group's words)
+// inclusive scan over the wave by DPP (row shifts within rows of 16, then the row broadcasts): VALU
+// only, where __shfl_up is an LDS permute and its round trip per step
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
 }
+template <uint32_t NW, uint32_t ST>
+struct BlkShape {
+  static constexpr uint32_t kWaveLds = kBlkRecs * 8 + ST + 16;  // rinfo, rows (their first words), stage
+  static constexpr uint32_t kLds = NW * kWaveLds;
+};
 
-__global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
+template <uint32_t NW, uint32_t ST>
+__global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* const lds = reinterpret_cast<uint8_t*>(smem);
   if (L.out_cap && ((*L.flag & 1u) || L.bytes[L.n] > L.out_cap)) return;  // (as k_log_write)
@@ -992,24 +975,26 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
   // the low 64 KB), then their stages, then the templates and descriptors
   const uint32_t T = (L.tpl_lds + 15u) & ~15u;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* const lri = reinterpret_cast<uint32_t*>(lds + wv * (kStreamRecs * 12));
-  uint32_t* const lrow = lri + kStreamRecs;  // two words per record
-  uint8_t* const stage = lds + kStreamWaves * (kStreamRecs * 12) + wv * kStreamStage;
-  uint8_t* const tpl = lds + kStreamWaves * kStreamWaveLds;
+  uint32_t* const lri = reinterpret_cast<uint32_t*>(lds + wv * (kBlkRecs * 8));
+  uint32_t* const lrow = lri + kBlkRecs;  // the first word of each record's row (its key ordinals)
+  uint8_t* const stage = lds + NW * (kBlkRecs * 8) + wv * (ST + 16);
+  uint8_t* const tpl = lds + BlkShape<NW, ST>::kLds;
   for (uint32_t i = threadIdx.x; i < T / 16; i += blockDim.x)
     reinterpret_cast<uint4*>(tpl)[i] = reinterpret_cast<const uint4*>(L.tpl)[i];
   __syncthreads();
   const uint4* const desc = reinterpret_cast<const uint4*>(tpl + (reinterpret_cast<const uint8_t*>(L.tpl_desc) - L.tpl));
   uint8_t* const out = reinterpret_cast<uint8_t*>(L.out);
   const unsigned long long ts = (unsigned long long)L.timestamp;
-  const unsigned long long W = (unsigned long long)gridDim.x * kStreamWaves;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * kStreamWaves + wv);
+  const unsigned long long W = (unsigned long long)gridDim.x * NW;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + wv);
   const uint32_t ce = (uint32_t)((unsigned long long)L.n * (w + 1) / W);
   uint32_t c = (uint32_t)((unsigned long long)L.n * w / W);
   uint32_t j0 = 0;              // records of command c already written (a command longer than a block)
   unsigned long long gpos = 0;  // and the byte position after them
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   while (c < ce) {
-    const uint32_t nb = ce - c < kStreamCmds ? ce - c : kStreamCmds;
+    const uint32_t nb = ce - c < kBlkCmds ? ce - c : kBlkCmds;
     LogCmd m{};
     unsigned long long mb = 0;
     LogKeys mk{};
@@ -1019,17 +1004,13 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
       mk = L.wkeys[c + lane];
     }
     const uint32_t cnt = lane < nb ? (uint32_t)m.nrec - (lane == 0 ? j0 : 0u) : 0u;
-    uint32_t incl = cnt;
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
-    }
-    uint32_t take = (uint32_t)__builtin_popcountll(__ballot(lane < nb && incl <= kStreamRecs));
+    const uint32_t incl = wave_scan(cnt);
+    uint32_t take = (uint32_t)__builtin_popcountll(__ballot(lane < nb && incl <= kBlkRecs));
     uint32_t first = rl(cnt, 0);
-    const bool partial = take == 0;  // command c alone has more records than a block: its next kStreamRecs
+    const bool partial = take == 0;  // command c alone has more records than a block: its next kBlkRecs
     if (partial) {
       take = 1;
-      first = kStreamRecs;
+      first = kBlkRecs;
     }
     // the block's record info and rows into the wave's LDS
     uint32_t p = 0;
@@ -1040,8 +1021,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
         if (q + lane < nk)
           __builtin_amdgcn_global_load_lds((g_void*)(L.rinfo + rk + q + lane), (l_void*)(lri + p + q), 4, 0, 0);
       const uint32_t* const rw = reinterpret_cast<const uint32_t*>(L.rows) + 2ull * rk;
-      for (uint32_t q = 0; q < 2 * nk; q += 64)
-        if (q + lane < 2 * nk) __builtin_amdgcn_global_load_lds((g_void*)(rw + q + lane), (l_void*)(lrow + 2 * p + q), 4, 0, 0);
+      for (uint32_t q = 0; q < nk; q += 64)
+        if (q + lane < nk) __builtin_amdgcn_global_load_lds((g_void*)(rw + 2 * (q + lane)), (l_void*)(lrow + p + q), 4, 0, 0);
       p += nk;
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loads above have landed in LDS
@@ -1049,7 +1030,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
     p = 0;
     for (uint32_t k = 0; k < take; ++k) {
       const unsigned long long out_rec = rl64(m.out_rec, k), key0 = rl64(m.key0, k);
-      const long long src = (long long)rl64((unsigned long long)m.src_pos, k);
+      const unsigned long long src = rl64((unsigned long long)m.src_pos, k);
       const uint32_t first_ord = rl(m.first_ord, k), nkeys = rl(m.nkeys, k);
       const long long pik = (long long)rl64((unsigned long long)mk.pik, k);
       const long long k0 = (long long)rl64((unsigned long long)mk.k0, k), k1 = (long long)rl64((unsigned long long)mk.k1, k);
@@ -1068,80 +1049,140 @@ __global__ __launch_bounds__(kStreamWaves * 64) void k_log_stream(LogParams L) {
         key_of(L, first_ord == 0 ? 0xFFFFFFFFu : rl(m.prev, k), rl(m.instance, k), ord, key);
         return key;
       };
-      const unsigned long long pos0 = k == 0 && j0 ? gpos : rl64(mb, k);
-      uint8_t* const obase = out + (pos0 & ~15ull);
+      unsigned long long pos = k == 0 && j0 ? gpos : rl64(mb, k);  // output byte of the next entry
       const long long lpos0 = L.first_position + (long long)(out_rec + jb);
-      uint32_t pos = (uint32_t)(pos0 & 15u);  // (relative to obase)
-      uint32_t gs = pos, sb = 0;
       for (uint32_t i0 = 0; i0 < nk; i0 += 64) {
-        // lane j resolves record i0 + j at once (its template, keys): one round of LDS reads for the
-        // whole group; the entries then take their fields from the lanes by v_readlane
         const uint32_t ng = nk - i0 < 64 ? nk - i0 : 64u;
-        uint32_t v_info = 0, v_off = 0, v_pa = 0, v_sa = 0;
-        long long v_key = 0, v_scope = 0;
+        // lane j: entry i0 + j (its template, keys, size)
+        uint32_t size = 0, off = 0, pa = 0, sa = 0;
+        bool slow = true;
+        long long key = 0, scope = 0;
         if (lane < ng) {
-          v_info = lri[p + i0 + lane];
-          if (!(v_info & kSlow)) {
-            const uint32_t rx = lrow[2 * (p + i0 + lane)];
-            const uint4 d = desc[(v_info >> 16) - 1];
-            v_off = d.x;
-            v_pa = d.y >> 16;
-            v_sa = d.z;
-            v_key = wkey(rx & 0xFFFF);
-            v_scope = wkey(rx >> 16);
+          const uint32_t info = lri[p + i0 + lane];
+          size = info & 0xFFFF;
+          if (!(info & kSlow)) {
+            const uint32_t rx = lrow[p + i0 + lane];
+            const uint4 d = desc[(info >> 16) - 1];
+            off = d.x;
+            pa = d.y >> 16;
+            sa = d.z;
+            key = wkey(rx & 0xFFFF);
+            scope = wkey(rx >> 16);
+            slow = false;
           }
         }
-        for (uint32_t i = 0; i < ng; ++i) {
-          const uint32_t info = rl(v_info, i);
-          const uint32_t size = info & 0xFFFF;
-          if (info & kSlow) {  // composed by k_log_compose
-            stream_flush(obase, stage, sb, gs, pos, lane);
-            pos += size;
-            gs = pos;
-            sb = pos & ~15u;
+        const uint32_t end = wave_scan(size);  // entry j ends at byte `end` of the group
+        const unsigned long long lpos = (unsigned long long)(lpos0 + (long long)(i0 + lane));
+        const unsigned long long pik_be = __builtin_bswap64((unsigned long long)pik);
+        const unsigned long long scope_be = __builtin_bswap64((unsigned long long)scope);
+        uint32_t g = 0;     // entries of the group written
+        uint32_t gb = 0;    // and their bytes
+        while (g < ng) {
+          const uint32_t lead = (uint32_t)(pos & 15);  // stage byte of pos
+          // the entries that fit the stage from entry g on (at least one)
+          const unsigned long long fits = __ballot(lane >= g && lane < ng && lead + (end - gb) <= ST);
+          const uint32_t t = (uint32_t)__builtin_popcountll(fits);
+          if (!t) {
+            // entry g alone is larger than the stage: its words straight from the template
+            const uint32_t sz = rl(size, g), o = rl(off, g), a = rl(pa, g), b = rl(sa, g);
+            if (!(rl((uint32_t)slow, g))) {
+              const unsigned long long kk = rl64((unsigned long long)key, g), sb = rl64(scope_be, g), lp = rl64(lpos, g);
+              for (uint32_t x = 8 * lane; x < sz; x += 512) {
+                unsigned long long v = *reinterpret_cast<const unsigned long long*>(tpl + o + x);
+                v = x == 16 ? lp : x == 24 ? src : x == 32 ? kk : x == 40 ? ts : v;
+                if (a) v = patch_word(v, pik_be, (int)a - (int)x);
+                if (b) v = patch_word(v, sb, (int)b - (int)x);
+                __builtin_nontemporal_store(v, reinterpret_cast<unsigned long long*>(out + pos + x));
+              }
+            }
+            pos += sz;
+            gb += sz;
+            ++g;
             continue;
           }
-          if (pos + size - sb > kStreamStage) {
-            stream_flush(obase, stage, sb, gs, pos, lane);
-            gs = pos;
-            sb = pos & ~15u;
+          const uint32_t ge = rl(end, g + t - 1) - gb;  // the staged entries' bytes
+          const bool mine = lane >= g && lane < g + t;
+          // the template words into the stage, word-parallel (lane x: stage word cb + x, consecutive
+          // words: no bank conflicts): its entry is the last one starting at or before it
+          const uint32_t sw = (lead + end - size - gb) >> 3;  // the lane's entry's first stage word
+          const uint32_t ew = (lead + ge) >> 3;
+          const uint32_t oo = slow ? 0u : off;
+          for (uint32_t cb = lead >> 3; cb < ew; cb += 128) {  // (two words per lane in flight)
+            const uint32_t x0 = cb + lane, x1 = x0 + 64;
+            uint32_t r0 = (uint32_t)__builtin_popcountll(__ballot(mine && sw <= cb)) + g - 1u, r1 = r0;
+            unsigned long long S = __ballot(mine && sw > cb && sw < cb + 128);
+            while (S) {
+              const uint32_t j = (uint32_t)__builtin_ctzll(S);
+              S &= S - 1;
+              const uint32_t v = rl(sw, j);
+              r0 += x0 >= v ? 1u : 0u;
+              r1 += x1 >= v ? 1u : 0u;
+            }
+            const uint32_t o0 = __shfl(oo, (int)r0), s0 = __shfl(sw, (int)r0);
+            const uint32_t o1 = __shfl(oo, (int)r1), s1 = __shfl(sw, (int)r1);
+            // (a composed entry's words read template 0's bytes: garbage k_log_compose writes over)
+            const unsigned long long t0 = *reinterpret_cast<const unsigned long long*>(tpl + o0 + 8 * (x0 - s0));
+            const unsigned long long t1 = *reinterpret_cast<const unsigned long long*>(tpl + o1 + 8 * (x1 - s1));
+            if (x0 < ew) reinterpret_cast<unsigned long long*>(stage)[x0] = t0;
+            if (x1 < ew) reinterpret_cast<unsigned long long*>(stage)[x1] = t1;
           }
-          // lane w's word of the entry, finished in registers (one store per lane: no lane writes a
-          // word another lane wrote): the template word, the LogEntryDescriptor's position / source
-          // position / key / timestamp, the big-endian processInstanceKey / scope key patched in
-          const uint32_t so = pos - sb;
-          StreamEnt e;
-          e.off = rl(v_off, i);
-          e.pa = rl(v_pa, i);
-          e.sa = rl(v_sa, i);
-          e.key = (long long)rl64((unsigned long long)v_key, i);
-          e.scope = (long long)rl64((unsigned long long)v_scope, i);
-          e.pik = pik;
-          e.lpos = lpos0 + (long long)(i0 + i);
-#ifndef ZB_STREAM_REGWORD  // the template copied as is, then the header words and key bytes over it (fewer
-                           // VALU than finishing each word in registers, the ZB_STREAM_REGWORD variant)
-          unsigned long long* const s64 = reinterpret_cast<unsigned long long*>(stage + so);
-          if (lane < size / 8) s64[lane] = reinterpret_cast<const unsigned long long*>(tpl + e.off)[lane];
           wave_lds_sync();
-          if (lane >= 2 && lane < 6)
-            s64[lane] = lane == 2 ? (unsigned long long)e.lpos : lane == 3 ? (unsigned long long)src
-                        : lane == 4 ? (unsigned long long)e.key : ts;
-          if (lane >= 8 && lane < 24) {
-            const bool sc = lane >= 16;
-            const uint32_t at = sc ? e.sa : e.pa;
-            const unsigned long long x = (unsigned long long)(sc ? e.scope : e.pik);
-            if (at) stage[so + at + (lane & 7)] = (uint8_t)(x >> (56 - 8 * (lane & 7)));
+          if (mine && !slow) {
+            // the lane's entry: header fields and keys over the template words
+            unsigned long long* const d64 = reinterpret_cast<unsigned long long*>(stage) + sw;
+            const uint32_t n8 = size / 8;
+            d64[2] = lpos;  // LogEntryDescriptor: position, source position, key, timestamp
+            d64[3] = src;
+            d64[4] = (unsigned long long)key;
+            d64[5] = ts;
+            if (pa) {
+              const uint32_t q = pa / 8;
+              d64[q] = patch_word(d64[q], pik_be, (int)pa - (int)(8 * q));
+              if (q + 1 < n8) d64[q + 1] = patch_word(d64[q + 1], pik_be, (int)pa - (int)(8 * q + 8));
+            }
+            if (sa) {
+              const uint32_t q = sa / 8;
+              d64[q] = patch_word(d64[q], scope_be, (int)sa - (int)(8 * q));
+              if (q + 1 < n8) d64[q + 1] = patch_word(d64[q + 1], scope_be, (int)sa - (int)(8 * q + 8));
+            }
           }
-#else
-          if (lane < size / 8)
-            reinterpret_cast<unsigned long long*>(stage + so)[lane] = tpl_word(tpl, e, 8 * lane, src, ts);
-#endif
-          pos += size;
+          wave_lds_sync();
+          // the stage out: 16-byte chunks of whole lines, the 8-byte half of a chunk shared with the
+          // neighbouring group alone
+          uint8_t* const ob = out + (pos & ~15ull);
+          const uint32_t e = lead + ge;
+          auto put = [&](uint32_t o, uint4 v) {
+            const bool h0 = o >= lead, h1 = o + 16 <= e;
+            if (h0 && h1) {
+              u32x4 q;
+              q.x = v.x; q.y = v.y; q.z = v.z; q.w = v.w;
+              __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(ob + o));
+            } else if (h0) {
+              u32x2 q;
+              q.x = v.x; q.y = v.y;
+              __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(ob + o));
+            } else {
+              u32x2 q;
+              q.x = v.z; q.y = v.w;
+              __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(ob + o + 8));
+            }
+          };
+          for (uint32_t o = 16u * lane; o < e; o += 2048u) {  // (two chunks per lane in flight)
+            const uint4 v0 = *reinterpret_cast<const uint4*>(stage + o);
+            const bool k1 = o + 1024 < e;
+            uint4 v1{};
+            if (k1) v1 = *reinterpret_cast<const uint4*>(stage + o + 1024);
+            put(o, v0);
+            if (k1) put(o + 1024, v1);
+          }
+          wave_lds_sync();
+          pos += ge;
+          gb += ge;
+          g += t;
         }
       }
-      stream_flush(obase, stage, sb, gs, pos, lane);
       p += nk;
-      gpos = (pos0 & ~15ull) + pos;
+      gpos = pos;
     }
     if (partial) {
       j0 += first;
@@ -1347,35 +1388,39 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL(k_table_build, dim3(nb), dim3(kLogScanB), 0, s, L, a.hdr, a.wcmds, a.src_pos, a.key_base,
                          a.table_sums, a.table, a.inst_proc_w, a.jrn);
   } else if (a.phase == 1) {
-    // k_log_stream when the templates fit LDS beside the waves' stages (k_log_write otherwise: it
-    // reads them from memory)
-    const size_t slds = (size_t)((a.tpl_lds + 15u) & ~15u) + (size_t)kStreamWaves * kStreamWaveLds;
+    // k_log_blocks when the templates fit LDS beside the waves' areas (k_log_write otherwise: it reads
+    // them from memory; ZBHIP_LOG_HALFWAVE=1 forces it).  Two shapes: 8 waves with 8 KB stages, or 16
+    // waves with 3 KB stages (ZBHIP_LOG_BLOCKS=16)
     static int cus = 0;
-    static bool stream_ok = true;
+    static bool attr8 = false, attr16 = false;
     if (!cus) {
       int dev = 0;
       if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
           cus <= 0)
         cus = 256;
-      stream_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(k_log_stream), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)kStreamLdsMax) == hipSuccess;
+      attr8 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_log_blocks<8, 8192>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kBlkLdsMax) == hipSuccess;
+      attr16 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_log_blocks<16, 4096>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kBlkLdsMax) == hipSuccess;
       (void)hipGetLastError();
     }
-    // (opt-in until its GPU parity run: ZBHIP_LOG_STREAM=1)
-    const bool stream = stream_ok && a.wkeys && a.tpl_lds && slds <= kStreamLdsMax && getenv("ZBHIP_LOG_STREAM") &&
-                        !getenv("ZBHIP_LOG_HALFWAVE");
+    const bool w16 = getenv("ZBHIP_LOG_BLOCKS") && atoi(getenv("ZBHIP_LOG_BLOCKS")) == 16;
+    const size_t T = (size_t)((a.tpl_lds + 15u) & ~15u);
+    const size_t blds = T + (w16 ? BlkShape<16, 4096>::kLds : BlkShape<8, 8192>::kLds);
+    const bool blocks = (w16 ? attr16 : attr8) && a.wkeys && a.tpl_lds && blds <= kBlkLdsMax && !getenv("ZBHIP_LOG_HALFWAVE");
     static bool told = false;
     if (!told && getenv("ZBHIP_DEBUG")) {
       told = true;
-      fprintf(stderr, "[zbhip] log write pass: %s (templates + descriptors %u B, LDS %zu B, attribute %s)\n",
-              stream ? "k_log_stream" : "k_log_write", a.tpl_lds, slds, stream_ok ? "ok" : "refused");
+      fprintf(stderr, "[zbhip] log write pass: %s (templates + descriptors %u B, LDS %zu B)\n",
+              blocks ? (w16 ? "k_log_blocks<16>" : "k_log_blocks<8>") : "k_log_write", a.tpl_lds, blds);
     }
-    if (a.n && a.compose != 2 && stream) {
-      const uint32_t per_cu = (uint32_t)(kStreamLdsMax / slds) < 4 ? (uint32_t)(kStreamLdsMax / slds) : 4u;
-      uint32_t grid = (uint32_t)cus * per_cu;
-      const uint32_t need = (a.n + kStreamWaves * 16 - 1) / (kStreamWaves * 16);  // >= 16 commands per wave
+    if (a.n && a.compose != 2 && blocks) {
+      const uint32_t nw = w16 ? 16u : 8u;
+      uint32_t grid = (uint32_t)cus * (kBlkLdsMax / blds >= 2 ? 2u : 1u);
+      const uint32_t need = (a.n + nw * 16 - 1) / (nw * 16);  // >= 16 commands per wave
       if (need < grid) grid = need;
-      hipLaunchKernelGGL(k_log_stream, dim3(grid), dim3(kStreamWaves * 64), slds, s, L);
+      if (w16) hipLaunchKernelGGL((k_log_blocks<16, 4096>), dim3(grid), dim3(16 * 64), blds, s, L);
+      else hipLaunchKernelGGL((k_log_blocks<8, 8192>), dim3(grid), dim3(8 * 64), blds, s, L);
     } else if (a.n && a.compose != 2) {
       hipLaunchKernelGGL(k_log_write, dim3((a.n + kLogWriteB - 1) / kLogWriteB), dim3(kLogWriteB),
                          (size_t)(kLogWriteB / kHalf) * kStageAlloc, s, L, 0u);
