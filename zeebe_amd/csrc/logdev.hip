@@ -921,17 +921,20 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
 }
 
 // pass 2, block form (the templates and their descriptors fit LDS beside the waves' areas): one
-// wave per contiguous range of commands, taken in blocks of up to kBlkCmds commands / kBlkRecs
-// records.  A block's command rows and key sets go into the lanes' registers (lane k: command k of
-// the block, read out uniformly with v_readlane), its records' template info and rows into the
+// wave per contiguous range of commands -- one contiguous byte range of the output -- taken in
+// blocks of up to kBlkCmds commands / kBlkRecs records.  A block's command rows and key sets go into
+// the lanes' registers (lane k: command k), its records' template info and key ordinals into the
 // wave's LDS by direct global->LDS loads.  Those are the wave's only vector-memory loads, so it waits
-// for its outstanding stores once per block (~100 KB), not once per group as k_log_write does (on
-// gfx950 s_waitcnt vmcnt counts stores too: k_log_write's waves spent 62 % of their cycles there).
-// Within a command, lane j composes entry j of a group of 64 into the wave's LDS stage as k_log_write
-// does (one lane per entry: a wave instruction copies 64 entries' words, ~10x fewer instructions per
-// byte than composing entry by entry with the whole wave, k_log_stream in round 4), the prefix of the
-// group that fits the stage at a time, and the wave streams the stage out in 16-byte non-temporal
-// chunks, 1 KB of whole lines per store instruction.
+// for its outstanding stores once per block, not once per group as k_log_write does (on gfx950
+// s_waitcnt vmcnt counts stores too: k_log_write's waves spent 62 % of their cycles there).  The
+// block's entries form one stream: lane j of a group of 64 takes entry e0 + j, its command's fields
+// by permutes from the command lanes, and resolves its template and keys; the prefix of the group
+// that fits the wave's stage is then composed in three steps -- the template words, word-parallel
+// (lane x: stage word x, its entry found from one ballot of the entry starts; consecutive words, no
+// bank conflicts), the header fields and big-endian keys, one lane per entry, and the stage out in
+// 16-byte non-temporal chunks, 1 KB of whole lines per store instruction.  Scans are DPP (no LDS
+// round trip).  (Round 4's k_log_stream composed entry by entry with the whole wave: ~100
+// wave-instructions per entry; round 5's word-only form, no stage, ~150 per 512 bytes: both slower.)
 constexpr uint32_t kBlkCmds = 32;
 constexpr uint32_t kBlkRecs = 192;
 constexpr uint32_t kBlkLdsMax = 160 * 1024;
@@ -987,12 +990,12 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
   const unsigned long long ts = (unsigned long long)L.timestamp;
   const unsigned long long W = (unsigned long long)gridDim.x * NW;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + wv);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   const uint32_t ce = (uint32_t)((unsigned long long)L.n * (w + 1) / W);
   uint32_t c = (uint32_t)((unsigned long long)L.n * w / W);
   uint32_t j0 = 0;              // records of command c already written (a command longer than a block)
   unsigned long long gpos = 0;  // and the byte position after them
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   while (c < ce) {
     const uint32_t nb = ce - c < kBlkCmds ? ce - c : kBlkCmds;
     LogCmd m{};
@@ -1027,17 +1030,31 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loads above have landed in LDS
     wave_lds_sync();
-    p = 0;
-    for (uint32_t k = 0; k < take; ++k) {
-      const unsigned long long out_rec = rl64(m.out_rec, k), key0 = rl64(m.key0, k);
-      const unsigned long long src = rl64((unsigned long long)m.src_pos, k);
-      const uint32_t first_ord = rl(m.first_ord, k), nkeys = rl(m.nkeys, k);
-      const long long pik = (long long)rl64((unsigned long long)mk.pik, k);
-      const long long k0 = (long long)rl64((unsigned long long)mk.k0, k), k1 = (long long)rl64((unsigned long long)mk.k1, k);
-      const long long k2 = (long long)rl64((unsigned long long)mk.k2, k);
-      const uint32_t o0 = rl(mk.o0, k), o1 = rl(mk.o1, k), o2 = rl(mk.o2, k);
-      const uint32_t jb = k == 0 ? j0 : 0u;
-      const uint32_t nk = k == 0 ? first : rl(cnt, k);
+    // the block's entries as one stream (the commands' bytes follow each other): lane j of a group
+    // takes entry e0 + j, its command's fields by permutes from the command lanes
+    const uint32_t P = partial ? first : rl(incl, take - 1);
+    const uint32_t ks = incl - cnt;  // (command lane k: its first entry in the block)
+    unsigned long long pos = j0 ? gpos : rl64(mb, 0);  // output byte of the next entry
+    for (uint32_t e0 = 0; e0 < P; e0 += 64) {
+      const uint32_t ng = P - e0 < 64 ? P - e0 : 64u;
+      const uint32_t e = e0 + lane;
+      // the entry's command: the last one starting at or before it
+      uint32_t kk = (uint32_t)__builtin_popcountll(__ballot(lane < take && ks <= e0)) - 1u;
+      unsigned long long S = __ballot(lane < take && ks > e0 && ks < e0 + 64);
+      while (S) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(S);
+        S &= S - 1;
+        kk += e >= rl(ks, j) ? 1u : 0u;
+      }
+      const int ki = (int)kk;
+      const unsigned long long out_rec = __shfl(m.out_rec, ki), key0 = __shfl(m.key0, ki);
+      const unsigned long long src = (unsigned long long)__shfl(m.src_pos, ki);
+      const uint32_t fo_nk = __shfl((uint32_t)m.first_ord | (uint32_t)m.nkeys << 16, ki);
+      const uint32_t first_ord = fo_nk & 0xFFFF, nkeys = fo_nk >> 16;
+      const long long pik = __shfl(mk.pik, ki), k0 = __shfl(mk.k0, ki), k1 = __shfl(mk.k1, ki), k2 = __shfl(mk.k2, ki);
+      const uint32_t o0 = __shfl(mk.o0, ki), o1 = __shfl(mk.o1, ki), o2 = __shfl(mk.o2, ki);
+      const uint32_t prev = __shfl(m.prev, ki), inst = __shfl(m.instance, ki);
+      const uint32_t ie = e - __shfl(ks, ki) + (kk == 0 ? j0 : 0u);  // the entry's index in its command
       auto wkey = [&](uint32_t ord) -> long long {
         if (ord == NONE) return -1;
         if (nkeys && ord >= first_ord) return L.pbits + (long long)(key0 + (uint16_t)(ord - first_ord));
@@ -1046,22 +1063,19 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
         if (ord == o1) return k1;
         if (ord == o2) return k2;
         long long key = 0;  // (a fourth older ordinal: the key chain in memory)
-        key_of(L, first_ord == 0 ? 0xFFFFFFFFu : rl(m.prev, k), rl(m.instance, k), ord, key);
+        key_of(L, first_ord == 0 ? 0xFFFFFFFFu : prev, inst, ord, key);
         return key;
       };
-      unsigned long long pos = k == 0 && j0 ? gpos : rl64(mb, k);  // output byte of the next entry
-      const long long lpos0 = L.first_position + (long long)(out_rec + jb);
-      for (uint32_t i0 = 0; i0 < nk; i0 += 64) {
-        const uint32_t ng = nk - i0 < 64 ? nk - i0 : 64u;
-        // lane j: entry i0 + j (its template, keys, size)
+      {
+        // lane j: entry e0 + j (its template, keys, size)
         uint32_t size = 0, off = 0, pa = 0, sa = 0;
         bool slow = true;
         long long key = 0, scope = 0;
         if (lane < ng) {
-          const uint32_t info = lri[p + i0 + lane];
+          const uint32_t info = lri[e];
           size = info & 0xFFFF;
           if (!(info & kSlow)) {
-            const uint32_t rx = lrow[p + i0 + lane];
+            const uint32_t rx = lrow[e];
             const uint4 d = desc[(info >> 16) - 1];
             off = d.x;
             pa = d.y >> 16;
@@ -1072,7 +1086,7 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
           }
         }
         const uint32_t end = wave_scan(size);  // entry j ends at byte `end` of the group
-        const unsigned long long lpos = (unsigned long long)(lpos0 + (long long)(i0 + lane));
+        const unsigned long long lpos = (unsigned long long)(L.first_position + (long long)(out_rec + ie));
         const unsigned long long pik_be = __builtin_bswap64((unsigned long long)pik);
         const unsigned long long scope_be = __builtin_bswap64((unsigned long long)scope);
         uint32_t g = 0;     // entries of the group written
@@ -1086,11 +1100,12 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
             // entry g alone is larger than the stage: its words straight from the template
             const uint32_t sz = rl(size, g), o = rl(off, g), a = rl(pa, g), b = rl(sa, g);
             if (!(rl((uint32_t)slow, g))) {
-              const unsigned long long kk = rl64((unsigned long long)key, g), sb = rl64(scope_be, g), lp = rl64(lpos, g);
+              const unsigned long long kg = rl64((unsigned long long)key, g), sb = rl64(scope_be, g), lp = rl64(lpos, g);
+              const unsigned long long sg = rl64(src, g), pb = rl64(pik_be, g);
               for (uint32_t x = 8 * lane; x < sz; x += 512) {
                 unsigned long long v = *reinterpret_cast<const unsigned long long*>(tpl + o + x);
-                v = x == 16 ? lp : x == 24 ? src : x == 32 ? kk : x == 40 ? ts : v;
-                if (a) v = patch_word(v, pik_be, (int)a - (int)x);
+                v = x == 16 ? lp : x == 24 ? sg : x == 32 ? kg : x == 40 ? ts : v;
+                if (a) v = patch_word(v, pb, (int)a - (int)x);
                 if (b) v = patch_word(v, sb, (int)b - (int)x);
                 __builtin_nontemporal_store(v, reinterpret_cast<unsigned long long*>(out + pos + x));
               }
@@ -1106,7 +1121,7 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
           // words: no bank conflicts): its entry is the last one starting at or before it
           const uint32_t sw = (lead + end - size - gb) >> 3;  // the lane's entry's first stage word
           const uint32_t ew = (lead + ge) >> 3;
-          const uint32_t oo = slow ? 0u : off;
+          const uint32_t dl = (slow ? 0u : off) - 8 * sw;  // (mod 2^32)
           for (uint32_t cb = lead >> 3; cb < ew; cb += 128) {  // (two words per lane in flight)
             const uint32_t x0 = cb + lane, x1 = x0 + 64;
             uint32_t r0 = (uint32_t)__builtin_popcountll(__ballot(mine && sw <= cb)) + g - 1u, r1 = r0;
@@ -1118,13 +1133,14 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
               r0 += x0 >= v ? 1u : 0u;
               r1 += x1 >= v ? 1u : 0u;
             }
-            const uint32_t o0 = __shfl(oo, (int)r0), s0 = __shfl(sw, (int)r0);
-            const uint32_t o1 = __shfl(oo, (int)r1), s1 = __shfl(sw, (int)r1);
-            // (a composed entry's words read template 0's bytes: garbage k_log_compose writes over)
-            const unsigned long long t0 = *reinterpret_cast<const unsigned long long*>(tpl + o0 + 8 * (x0 - s0));
-            const unsigned long long t1 = *reinterpret_cast<const unsigned long long*>(tpl + o1 + 8 * (x1 - s1));
-            if (x0 < ew) reinterpret_cast<unsigned long long*>(stage)[x0] = t0;
-            if (x1 < ew) reinterpret_cast<unsigned long long*>(stage)[x1] = t1;
+            // (one permute per word: the entry's template byte minus its stage byte)
+            const uint32_t d0 = __shfl(dl, (int)r0), d1 = __shfl(dl, (int)r1);
+            // (a composed entry's words read template 0's bytes: garbage k_log_compose writes over;
+            // words past the group go to the stage's spare last word: no branches)
+            const unsigned long long t0 = *reinterpret_cast<const unsigned long long*>(tpl + d0 + 8 * x0);
+            const unsigned long long t1 = *reinterpret_cast<const unsigned long long*>(tpl + d1 + 8 * x1);
+            *reinterpret_cast<unsigned long long*>(stage + (x0 < ew ? 8 * x0 : ST + 8)) = t0;
+            *reinterpret_cast<unsigned long long*>(stage + (x1 < ew ? 8 * x1 : ST + 8)) = t1;
           }
           wave_lds_sync();
           if (mine && !slow) {
@@ -1135,15 +1151,18 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
             d64[3] = src;
             d64[4] = (unsigned long long)key;
             d64[5] = ts;
+            // (each key's two words read together, then written: one round trip per key)
             if (pa) {
-              const uint32_t q = pa / 8;
-              d64[q] = patch_word(d64[q], pik_be, (int)pa - (int)(8 * q));
-              if (q + 1 < n8) d64[q + 1] = patch_word(d64[q + 1], pik_be, (int)pa - (int)(8 * q + 8));
+              const uint32_t q = pa / 8, q1 = q + 1 < n8 ? q + 1 : q;
+              const unsigned long long a0 = d64[q], a1 = d64[q1];
+              d64[q1] = patch_word(a1, pik_be, (int)pa - (int)(8 * q1));
+              d64[q] = patch_word(a0, pik_be, (int)pa - (int)(8 * q));
             }
             if (sa) {
-              const uint32_t q = sa / 8;
-              d64[q] = patch_word(d64[q], scope_be, (int)sa - (int)(8 * q));
-              if (q + 1 < n8) d64[q + 1] = patch_word(d64[q + 1], scope_be, (int)sa - (int)(8 * q + 8));
+              const uint32_t q = sa / 8, q1 = q + 1 < n8 ? q + 1 : q;
+              const unsigned long long a0 = d64[q], a1 = d64[q1];
+              d64[q1] = patch_word(a1, scope_be, (int)sa - (int)(8 * q1));
+              d64[q] = patch_word(a0, scope_be, (int)sa - (int)(8 * q));
             }
           }
           wave_lds_sync();
@@ -1168,12 +1187,11 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
             }
           };
           for (uint32_t o = 16u * lane; o < e; o += 2048u) {  // (two chunks per lane in flight)
+            // (both reads before the stores; a read past the stage reads a neighbour's bytes, unused)
             const uint4 v0 = *reinterpret_cast<const uint4*>(stage + o);
-            const bool k1 = o + 1024 < e;
-            uint4 v1{};
-            if (k1) v1 = *reinterpret_cast<const uint4*>(stage + o + 1024);
+            const uint4 v1 = *reinterpret_cast<const uint4*>(stage + o + 1024);
             put(o, v0);
-            if (k1) put(o + 1024, v1);
+            if (o + 1024 < e) put(o + 1024, v1);
           }
           wave_lds_sync();
           pos += ge;
@@ -1181,9 +1199,8 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
           g += t;
         }
       }
-      p += nk;
-      gpos = pos;
     }
+    gpos = pos;
     if (partial) {
       j0 += first;
       if (j0 >= rl(m.nrec, 0)) {
@@ -1392,7 +1409,7 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
     // them from memory; ZBHIP_LOG_HALFWAVE=1 forces it).  Two shapes: 8 waves with 8 KB stages, or 16
     // waves with 3 KB stages (ZBHIP_LOG_BLOCKS=16)
     static int cus = 0;
-    static bool attr8 = false, attr16 = false;
+    static bool attr8 = false, attr12 = false, attr16 = false;
     if (!cus) {
       int dev = 0;
       if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -1400,26 +1417,30 @@ hipError_t launch_log_device(const LogLaunch& a, hipStream_t s) {
         cus = 256;
       attr8 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_log_blocks<8, 8192>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)kBlkLdsMax) == hipSuccess;
+      attr12 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_log_blocks<12, 6144>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kBlkLdsMax) == hipSuccess;
       attr16 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_log_blocks<16, 4096>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kBlkLdsMax) == hipSuccess;
       (void)hipGetLastError();
     }
-    const bool w16 = getenv("ZBHIP_LOG_BLOCKS") && atoi(getenv("ZBHIP_LOG_BLOCKS")) == 16;
+    const int want = getenv("ZBHIP_LOG_BLOCKS") ? atoi(getenv("ZBHIP_LOG_BLOCKS")) : 16;
+    const uint32_t nw = want == 8 ? 8u : want == 12 ? 12u : 16u;
     const size_t T = (size_t)((a.tpl_lds + 15u) & ~15u);
-    const size_t blds = T + (w16 ? BlkShape<16, 4096>::kLds : BlkShape<8, 8192>::kLds);
-    const bool blocks = (w16 ? attr16 : attr8) && a.wkeys && a.tpl_lds && blds <= kBlkLdsMax && !getenv("ZBHIP_LOG_HALFWAVE");
+    const size_t blds = T + (nw == 8 ? BlkShape<8, 8192>::kLds : nw == 12 ? BlkShape<12, 6144>::kLds : BlkShape<16, 4096>::kLds);
+    const bool attr = nw == 8 ? attr8 : nw == 12 ? attr12 : attr16;
+    const bool blocks = attr && a.wkeys && a.tpl_lds && blds <= kBlkLdsMax && !getenv("ZBHIP_LOG_HALFWAVE");
     static bool told = false;
     if (!told && getenv("ZBHIP_DEBUG")) {
       told = true;
-      fprintf(stderr, "[zbhip] log write pass: %s (templates + descriptors %u B, LDS %zu B)\n",
-              blocks ? (w16 ? "k_log_blocks<16>" : "k_log_blocks<8>") : "k_log_write", a.tpl_lds, blds);
+      fprintf(stderr, "[zbhip] log write pass: %s, %u waves (templates + descriptors %u B, LDS %zu B)\n",
+              blocks ? "k_log_blocks" : "k_log_write", nw, a.tpl_lds, blds);
     }
     if (a.n && a.compose != 2 && blocks) {
-      const uint32_t nw = w16 ? 16u : 8u;
       uint32_t grid = (uint32_t)cus * (kBlkLdsMax / blds >= 2 ? 2u : 1u);
       const uint32_t need = (a.n + nw * 16 - 1) / (nw * 16);  // >= 16 commands per wave
       if (need < grid) grid = need;
-      if (w16) hipLaunchKernelGGL((k_log_blocks<16, 4096>), dim3(grid), dim3(16 * 64), blds, s, L);
+      if (nw == 16) hipLaunchKernelGGL((k_log_blocks<16, 4096>), dim3(grid), dim3(16 * 64), blds, s, L);
+      else if (nw == 12) hipLaunchKernelGGL((k_log_blocks<12, 6144>), dim3(grid), dim3(12 * 64), blds, s, L);
       else hipLaunchKernelGGL((k_log_blocks<8, 8192>), dim3(grid), dim3(8 * 64), blds, s, L);
     } else if (a.n && a.compose != 2) {
       hipLaunchKernelGGL(k_log_write, dim3((a.n + kLogWriteB - 1) / kLogWriteB), dim3(kLogWriteB),
