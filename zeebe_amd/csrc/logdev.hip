@@ -935,6 +935,13 @@ __global__ __launch_bounds__(kLogWriteB) void k_log_write(LogParams L, uint32_t)
 // 16-byte non-temporal chunks, 1 KB of whole lines per store instruction.  Scans are DPP (no LDS
 // round trip).  (Round 4's k_log_stream composed entry by entry with the whole wave: ~100
 // wave-instructions per entry; round 5's word-only form, no stage, ~150 per 512 bytes: both slower.)
+// default-policy stores: measured 1.07 ms per window against 1.24 ms with non-temporal stores
+// (scripts/ab_logstores.sh; ZB_LOG_NT_STORES builds the other)
+#ifdef ZB_LOG_NT_STORES
+#define ZB_LOG_STORE(v, p) __builtin_nontemporal_store(v, p)
+#else
+#define ZB_LOG_STORE(v, p) (*(p) = (v))
+#endif
 constexpr uint32_t kBlkCmds = 32;
 constexpr uint32_t kBlkRecs = 192;
 constexpr uint32_t kBlkLdsMax = 160 * 1024;
@@ -1175,15 +1182,15 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
             if (h0 && h1) {
               u32x4 q;
               q.x = v.x; q.y = v.y; q.z = v.z; q.w = v.w;
-              __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(ob + o));
+              ZB_LOG_STORE(q, reinterpret_cast<u32x4*>(ob + o));
             } else if (h0) {
               u32x2 q;
               q.x = v.x; q.y = v.y;
-              __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(ob + o));
+              ZB_LOG_STORE(q, reinterpret_cast<u32x2*>(ob + o));
             } else {
               u32x2 q;
               q.x = v.z; q.y = v.w;
-              __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(ob + o + 8));
+              ZB_LOG_STORE(q, reinterpret_cast<u32x2*>(ob + o + 8));
             }
           };
           for (uint32_t o = 16u * lane; o < e; o += 2048u) {  // (two chunks per lane in flight)
