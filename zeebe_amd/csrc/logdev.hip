@@ -1003,6 +1003,16 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
   uint32_t c = (uint32_t)((unsigned long long)L.n * w / W);
   uint32_t j0 = 0;              // records of command c already written (a command longer than a block)
   unsigned long long gpos = 0;  // and the byte position after them
+  bool carry = false;           // the stage's first word holds the 8 bytes before gpos, not yet written
+  auto flush_carry = [&](unsigned long long at) {  // (the carried word is the 8 bytes before `at`)
+    if (carry && lane == 0) {
+      u32x2 q;
+      const uint2 v = *reinterpret_cast<const uint2*>(stage);
+      q.x = v.x; q.y = v.y;
+      ZB_LOG_STORE(q, reinterpret_cast<u32x2*>(out + at - 8));
+    }
+    carry = false;
+  };
   while (c < ce) {
     const uint32_t nb = ce - c < kBlkCmds ? ce - c : kBlkCmds;
     LogCmd m{};
@@ -1104,6 +1114,7 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
           const unsigned long long fits = __ballot(lane >= g && lane < ng && lead + (end - gb) <= ST);
           const uint32_t t = (uint32_t)__builtin_popcountll(fits);
           if (!t) {
+            flush_carry(pos);
             // entry g alone is larger than the stage: its words straight from the template
             const uint32_t sz = rl(size, g), o = rl(off, g), a = rl(pa, g), b = rl(sa, g);
             if (!(rl((uint32_t)slow, g))) {
@@ -1177,16 +1188,15 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
           // neighbouring group alone
           uint8_t* const ob = out + (pos & ~15ull);
           const uint32_t e = lead + ge;
+          // (a trailing half chunk is not written: its 8 bytes move to the stage's first word and go
+          // out with the next group's first chunk -- `carry` -- so every store is a whole chunk but
+          // the upper half at the start of the wave's range and the last word at its end)
           auto put = [&](uint32_t o, uint4 v) {
-            const bool h0 = o >= lead, h1 = o + 16 <= e;
-            if (h0 && h1) {
+            if (o + 16 > e) return;  // (the trailing half: carried)
+            if (o >= lead || carry) {
               u32x4 q;
               q.x = v.x; q.y = v.y; q.z = v.z; q.w = v.w;
               ZB_LOG_STORE(q, reinterpret_cast<u32x4*>(ob + o));
-            } else if (h0) {
-              u32x2 q;
-              q.x = v.x; q.y = v.y;
-              ZB_LOG_STORE(q, reinterpret_cast<u32x2*>(ob + o));
             } else {
               u32x2 q;
               q.x = v.z; q.y = v.w;
@@ -1200,6 +1210,9 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
             put(o, v0);
             if (o + 1024 < e) put(o + 1024, v1);
           }
+          carry = (e & 15) != 0;
+          if (carry && lane == 0)
+            *reinterpret_cast<unsigned long long*>(stage) = *reinterpret_cast<const unsigned long long*>(stage + e - 8);
           wave_lds_sync();
           pos += ge;
           gb += ge;
@@ -1219,6 +1232,7 @@ __global__ __launch_bounds__(NW * 64) void k_log_blocks(LogParams L) {
       j0 = 0;
     }
   }
+  flush_carry(gpos);
 }
 
 // pass 2b (flag bit 1 only): the entries without a template, composed by their command's lane
