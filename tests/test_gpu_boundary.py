@@ -130,7 +130,10 @@ def test_gpu_boundary_both_outcomes():
     assert part.stats()["fallback"] == 0
 
 
-@pytest.mark.parametrize("seed", range(8))
+# (141, 312: a batch cancels the task's stored timer, then creates and cancels a sub-process's
+# boundary timer of its own -- two TIMER:CANCELED with different dueDates in one batch; found by
+# scripts/fuzz_random.py)
+@pytest.mark.parametrize("seed", list(range(8)) + [141, 312])
 def test_gpu_random_processes_with_boundary_events(seed):
     # tests/random_bpmn.py: random structured processes (sub-processes, job worker kinds) whose
     # tasks outside parallel branches may carry a timer boundary event; each round completes a job
@@ -144,7 +147,7 @@ def test_gpu_random_processes_with_boundary_events(seed):
     assert [r for r in part.state() if not r.startswith("KEY|")] == []
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", list(range(8)) + [228, 271])
 def test_gpu_random_processes_with_multi_instance_activities(seed):
     # the same with multi-instance tasks among them (static collections, parallel or sequential, an
     # outputCollection, sequential completion conditions): each round completes inner instances' jobs

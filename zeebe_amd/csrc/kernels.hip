@@ -1692,12 +1692,14 @@ __device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord, long lo
 }
 
 // CatchEventBehavior.unsubscribeFromTimerEvent (processing/common/CatchEventBehavior.java:380-392):
-// TIMER:CANCELED with the timer's key and stored value (its dueDate goes to the command's cmd_due
-// entry: at most one timer is canceled per batch); TimerCancelledApplier removes the row
+// TIMER:CANCELED with the timer's key and stored value; TimerCancelledApplier removes the row.  The
+// dueDate of a timer stored before the batch goes to the command's cmd_due entry (one timer row per
+// instance: at most one such cancel per batch); a timer the batch created itself is due at the clock
+// plus its duration, which the host and the log writer derive from the key (one of the batch's own)
 template <class K>
 __device__ __forceinline__ void cancel_timer(Lane<K>& L) {
   emit(L, C_TIMER_CANCELED, L.tm_x >> 16, L.tm_y & 0xFFFF, L.tm_x & 0xFFF, (L.tm_y >> 16) & 0xFF);
-  L.sp->cmd_due[L.ci] = L.tm_due;
+  if ((L.tm_x >> 16) < L.first_ord) L.sp->cmd_due[L.ci] = L.tm_due;
   L.tm_x = L.tm_y = 0;
   L.tm_due = 0;
 }

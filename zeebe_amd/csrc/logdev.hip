@@ -341,12 +341,15 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
     r.rt = rej ? ZBHIP_RT_REJECTION : ZBHIP_RT_EVENT;
     const long long cmd = (long long)(((unsigned long long)m.pad << 32) | m.doc_begin);
     long long dur = 0;
-    if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT) {
+    // (a timer created in this batch and canceled in it: the clock plus its duration, as CREATED --
+    // cmd_due holds only the dueDate of a timer stored before the batch)
+    const bool fresh = c6 == C_TIMER_CANCELED && m.nkeys && key_ord >= m.first_ord && key_ord < (uint32_t)m.first_ord + m.nkeys;
+    if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT || fresh) {
       const uint32_t pb = r.proc != NONE ? proc_block(L, r.proc) : 0u;
       if (!pb || elem >= L.idx[pb + 5]) return false;
       dur = (long long)el_run(L, pb, elem, E_DUR).x;
     }
-    r.due = c6 == C_TIMER_CREATED ? L.now_ms + dur : c6 == C_TIMER_NEXT ? next_cycle_due(cmd, dur, L.now_ms)
+    r.due = c6 == C_TIMER_CREATED || fresh ? L.now_ms + dur : c6 == C_TIMER_NEXT ? next_cycle_due(cmd, dur, L.now_ms)
             : c6 == C_TIMER_CANCELED ? L.cmd_due[c] : cmd;
     r.reps = rej ? 1 : fl == 255 ? -1 : (int)fl;
   } else if (c6 == C_PIC_CREATED) {

@@ -3207,6 +3207,13 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
       r.intent = ZBHIP_TIMER_CANCELED;
       r.record_type = ZBHIP_RT_EVENT;
       r.aux = c < h->h_cmd_due.size() ? h->h_cmd_due[c] : -1;
+      if (c < h->h_hdr.size()) {
+        // a timer created in this batch and canceled in it: the clock plus its duration (as its
+        // CREATED); cmd_due holds only the dueDate of a timer stored before the batch
+        const uint32_t first = h->h_hdr[c].y & 0xFFFF, nkeys = h->h_hdr[c].x >> 16;
+        const zbhip_element* E = proc != NONE && elem < h->procs[proc].els.size() ? &h->procs[proc].els[elem] : nullptr;
+        if (E && nkeys && key_ord >= first && key_ord < first + nkeys) r.aux = h->run_clock_ms + (int64_t)E->duration_ms;
+      }
       r.partition = fl == 255 ? -1 : (int32_t)fl;  // TimerRecord.repetitions
     } else if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT || c6 == C_TIMER_TRIGGERED || c6 == C_TIMER_TRIGGER) {
       // TimerRecord: elementInstanceKey (scope_key), dueDate in aux -- CREATED: the run's clock plus
