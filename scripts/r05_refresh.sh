@@ -11,7 +11,7 @@ echo "default bench $(( $(date +%s) - T0 )) s" > gpurun_out/r05/times.txt
 T0=$(date +%s)
 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-io > gpurun_out/r05/bench_hostio.json 2> gpurun_out/r05/bench_hostio.err
 echo "host-io bench $(( $(date +%s) - T0 )) s" >> gpurun_out/r05/times.txt
-for cfg in one_task xor forkjoin8 forkjoin8_tasks boundary10 linear10; do
+for cfg in ${CFGS:-one_task xor forkjoin8 forkjoin8_tasks boundary10 linear10}; do
   timeout -k 10 300 python -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/r05/bench_$cfg.json 2>> gpurun_out/r05/errs.txt
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05/prof_$cfg -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline > /dev/null 2>> gpurun_out/r05/errs.txt
 done
