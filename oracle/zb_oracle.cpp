@@ -3198,6 +3198,24 @@ class Oracle {
   // BpmnStateTransitionBehavior.java:348-363: PROCESS_INSTANCE_BATCH:TERMINATE) and finishes in
   // onChildTerminated once none is active
   void on_terminate(const OEl& el, int64_t key, const PiValue& v) {
+    if (el.type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      // MultiInstanceBodyProcessor.onTerminate (:116-125): unsubscribeFromEvents, terminateChildInstances,
+      // terminate at once when no inner instance is active
+      unsubscribe_timers(key);
+      unsubscribe_messages(key);
+      if (ei_.at(key).childCount == 0) {
+        mi_terminate(key);
+      } else {
+        ORecord& rec = append(ZBHIP_RT_COMMAND, ZBHIP_VT_PROCESS_INSTANCE_BATCH, ZBHIP_PIB_TERMINATE, next_key());
+        rec.r.process_idx = v.proc;
+        rec.r.element_idx = v.elem;
+        rec.r.scope_key = key;  // batchElementInstanceKey
+        rec.r.process_instance_key = v.piKey;
+        rec.r.partition = -1;
+        rec.pi = v;
+      }
+      return;
+    }
     if (el.type == ZBHIP_EL_SUB_PROCESS) {
       unsubscribe_timers(key);  // unsubscribeFromEvents
       unsubscribe_messages(key);
@@ -3269,7 +3287,11 @@ class Oracle {
     const OEl& fe = E(fit->second.value);
     if (fe.type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
       const ElementInstance& body = fit->second;
-      if (body.state == ZBHIP_PI_ELEMENT_TERMINATING) throw Unsupported{"terminating multi-instance body"};
+      if (body.state == ZBHIP_PI_ELEMENT_TERMINATING) {
+        // (:244-246) canBeTerminated: no inner instance is active
+        if (body.childCount == 0) mi_terminate(body.key);
+        return;
+      }
       if ((int64_t)body.childCount + body.activeSequenceFlows == 0)
         pi_command(body.key, ZBHIP_PI_COMPLETE_ELEMENT, body.value);
       return;
@@ -3279,7 +3301,27 @@ class Oracle {
       if (fit->second.childCount == 0) container_child_terminated(fit->first);
       return;
     }
+    // ProcessProcessor.onChildTerminated (:143-180): an active process with an active child left (the
+    // boundary event a terminated multi-instance body's trigger activated) does nothing
+    if (fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED && fit->second.childCount > 0) return;
     throw Unsupported{"terminated child of the process (cancel)"};
+  }
+
+  // MultiInstanceBodyProcessor.terminate (:282-315): resolveIncidents (none), then with the body's
+  // boundary event trigger (its flow scope active and not interrupted) transitionToTerminated,
+  // activateTriggeredEvent and onElementTerminated; otherwise transitionToTerminated and
+  // onElementTerminated
+  void mi_terminate(int64_t key) {
+    const ElementInstance body = ei_.at(key);
+    const PiValue v = body.value;
+    auto tit = triggers_.lower_bound({key, INT64_MIN});
+    const bool found = tit != triggers_.end() && tit->first.first == key;
+    auto fit = ei_.find(v.flowScopeKey);
+    const bool fs_active = fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED;
+    pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
+    if (found && fs_active && !es_interrupted_.count(v.flowScopeKey))
+      activate_triggered_event(tit->first.second, tit->second.elem, key, v.flowScopeKey, v);
+    child_terminated(v);
   }
 
   // SubProcessProcessor.onChildTerminated (:108-160) with no active child left: its boundary event's

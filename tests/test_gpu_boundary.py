@@ -75,7 +75,20 @@ def _nested_sub_processes():
     return b.moveToActivity("outer").endEvent("e").done()
 
 
+def _sub_process_multi_instance():
+    # a multi-instance task inside a sub-process whose boundary timer terminates it: the body's inner
+    # instances through PROCESS_INSTANCE_BATCH:TERMINATE, then the body, then the sub-process
+    # (MultiInstanceBodyProcessor.onTerminate / onChildTerminated / terminate)
+    b = bpmn.createExecutableProcess("process").startEvent("start").subProcess("sub").startEvent("ss")
+    b.serviceTask("task", "task")
+    b.multiInstance("= [1, 2, 3]", "item", False)
+    b.endEvent("se").subProcessDone().boundaryEvent("late").timerWithDuration("PT2S")
+    b.sequenceFlowId("to-canceled").endEvent("canceled")
+    return b.moveToActivity("sub").endEvent("end").done()
+
+
 SHAPES = {"multiple_sequence_flows": lambda: multiple_sequence_flows("PT30S"), "linear": _linear_with_boundary,
+          "sub_process_multi_instance": _sub_process_multi_instance,
           "sub_process": lambda: sub_process_boundary(True, "PT10S"),
           "sub_process_non_interrupting": lambda: sub_process_boundary(False, "PT10S"),
           "sub_process_parallel": _sub_process_parallel,
@@ -147,7 +160,8 @@ def test_gpu_random_processes_with_boundary_events(seed):
     assert [r for r in part.state() if not r.startswith("KEY|")] == []
 
 
-@pytest.mark.parametrize("seed", list(range(8)) + [228, 271])
+# (140, 151: multi-instance bodies terminated with their sub-process; 228, 271: see above)
+@pytest.mark.parametrize("seed", list(range(8)) + [140, 151, 228, 271])
 def test_gpu_random_processes_with_multi_instance_activities(seed):
     # the same with multi-instance tasks among them (static collections, parallel or sequential, an
     # outputCollection, sequential completion conditions): each round completes inner instances' jobs

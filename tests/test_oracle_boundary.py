@@ -426,3 +426,38 @@ def test_non_interrupting_sub_process_boundary_keeps_the_sub_process():
     assert any("elementId=task" in r for r in st if r.startswith("ELEMENT_INSTANCE_KEY"))
     out = _complete_jobs(o, recs)
     assert _tuple(o, out[-1]) == ("PROCESS_INSTANCE", "ELEMENT_COMPLETED", "process")
+
+
+def test_multi_instance_body_terminated_with_its_sub_process():
+    # MultiInstanceActivityTest.shouldTerminateInstancesOnTerminatingBody (:584-620)'s subsequence --
+    # body TERMINATING, the open inner instance TERMINATING / TERMINATED, body TERMINATED -- with the
+    # body terminated by its flow scope: a sub-process around the multi-instance task whose timer
+    # boundary event fires after all but one inner job completed (MultiInstanceBodyProcessor.onTerminate
+    # :116-125, onChildTerminated :240-253, terminate :282-315; SubProcessProcessor.onChildTerminated)
+    b = bpmn.createExecutableProcess("process").startEvent("start").subProcess("sub").startEvent("ss")
+    b.serviceTask("task", "task")
+    b.multiInstance("= [1, 2, 3]", "item", False)
+    b.endEvent("se").subProcessDone().boundaryEvent("late").timerWithDuration("PT10S")
+    b.sequenceFlowId("to-canceled").endEvent("canceled")
+    xml = b.moveToActivity("sub").endEvent("end").done()
+    o, recs = _started(xml)
+    jobs = [r for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CREATED]
+    assert len(jobs) == 3
+    c = abi.make_commands(2)
+    c["kind"] = abi.CMD_JOB_COMPLETE
+    c["ref"] = [int(r["key"]) - BASE - 1 for r in jobs[:2]]
+    _run(o, c)
+    rows = [x for x in o.state() if x.startswith("TIMERS|")]
+    assert len(rows) == 1  # the sub-process's boundary timer
+    due = int(dict(kv.split("=") for kv in rows[0].split("|")[3].split(","))["dueDate"])
+    tkey = int(rows[0].split("|")[2])
+    recs = _run(o, trigger_commands([0], [tkey - BASE - 1], [due]))
+    seq = [(abi.intent_name(int(r["value_type"]), int(r["intent"])), _eid(o, r)) for r in recs
+           if r["value_type"] == abi.VT_PROCESS_INSTANCE]
+    want = [("ELEMENT_TERMINATING", "sub"), ("ELEMENT_TERMINATING", "task"), ("ELEMENT_TERMINATING", "task"),
+            ("ELEMENT_TERMINATED", "task"), ("ELEMENT_TERMINATED", "task"), ("ELEMENT_TERMINATED", "sub"),
+            ("SEQUENCE_FLOW_TAKEN", "to-canceled"), ("ELEMENT_COMPLETED", "canceled"), ("ELEMENT_COMPLETED", "process")]
+    it = iter(seq)
+    assert all(any(x == w for x in it) for w in want), seq  # containsSubsequence
+    assert sum(1 for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CANCELED) == 1
+    assert [x for x in o.state() if not x.startswith("KEY|")] == []

@@ -1726,9 +1726,19 @@ __device__ __forceinline__ void child_terminated(Lane<K>& L, uint32_t c) {
       if (ct == ZBHIP_EL_MULTI_INSTANCE_BODY) {
         // MultiInstanceBodyProcessor.onChildTerminated (:232-247): a body that is not terminating (its
         // completion condition was met) completes once no child is active
-        if (cst == ZBHIP_PI_ELEMENT_TERMINATING) { set_fail(L, FB_UNSUPPORTED); return; }
-        if ((ce.y & 0xFF) == 0) follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, ckey, pfsa, c, true, pc == 0, ckey);
-        return;
+        if (cst != ZBHIP_PI_ELEMENT_TERMINATING) {
+          if ((ce.y & 0xFF) == 0) follow_up(L, ZBHIP_PI_COMPLETE_ELEMENT, ckey, pfsa, c, true, pc == 0, ckey);
+          return;
+        }
+        // a terminating body (:244-247, terminate :282-315) once no inner instance is active:
+        // transitionToTerminated and onElementTerminated; with its own boundary event's trigger
+        // (activateTriggeredEvent in between) outside the subset
+        if ((ce.y & 0xFF) != 0) return;
+        if (L.trig_key == ckey && L.trig_evt != NONE) { set_fail(L, FB_UNSUPPORTED); return; }
+        emit(L, ZBHIP_PI_ELEMENT_TERMINATED, ckey, pfsa, c);
+        apply_completed_child(L, tc, ckey);
+        c = pc;
+        continue;
       }
       if ((ce.y & 0xFF) != 0) return;  // canBeTerminated: a child is still active
       const uint32_t pst = pc == 0 ? (L.pi_live ? (uint32_t)L.pi_state : 0u) : (tget(L, scope_find(L, pc)).y >> 16) & 0xFF;
@@ -1771,7 +1781,8 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
   const int t = tbl_find(L, key);
   const uint32_t st = t < 0 ? 0u : (tget(L, t).y >> 16) & 0xFF;
   const uint32_t type = etype(w);
-  const bool ok_type = ZBHIP_IS_JOB_WORKER(type) || (K::S && (type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT));
+  const bool ok_type = ZBHIP_IS_JOB_WORKER(type) || (K::S && (type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
+                                                              type == ZBHIP_EL_MULTI_INSTANCE_BODY));
   if (t < 0 || !ok_type ||
       (st != ZBHIP_PI_ELEMENT_ACTIVATING && st != ZBHIP_PI_ELEMENT_ACTIVATED && st != ZBHIP_PI_ELEMENT_COMPLETING)) {
     set_fail(L, FB_UNSUPPORTED);
@@ -1779,7 +1790,8 @@ __device__ __forceinline__ void terminate_pi(Lane<K>& L, uint32_t elem, uint4 w,
   }
   const uint32_t c = scope_of<K>(w);
   if constexpr (K::S) {
-    if (type == ZBHIP_EL_SUB_PROCESS) {
+    if (type == ZBHIP_EL_SUB_PROCESS || type == ZBHIP_EL_MULTI_INSTANCE_BODY) {
+      // (a multi-instance body the same way: MultiInstanceBodyProcessor.onTerminate :116-125)
       const uint32_t nch = tget(L, t).y & 0xFF;  // childCount
       // the termination's commands stay in this batch (the trigger's context travels in the lane)
       if (pending(L) + L.processed + 2 + nch >= L.limit) { set_fail(L, FB_BATCH_LIMIT); return; }
