@@ -5,7 +5,8 @@ the CPU oracle window by window (each round completes an open job or fires an op
 instance, at random).  Every window the device took in full must equal the oracle bit-exact
 (records and state); a window in which the device declined commands (a fallback: the adapter hands
 those instances to the engine) ends that run as "declined".  Usage:
-python scripts/fuzz_random.py FIRST LAST [budget_s]; exit 1 on any parity failure."""
+python scripts/fuzz_random.py FIRST LAST [budget_s]; exit 1 on any parity failure.  FUZZ_MAX_RECORDS sets
+the device's records per batch (default 256; smaller values exercise the continuation batches)."""
 import collections
 import os
 import sys
@@ -37,7 +38,7 @@ def run(flavour, seed, n=96, phases=80):
     base, kw = FLAVOURS[flavour]
     rng = np.random.default_rng(base + seed)
     xml = random_process(rng, **kw)
-    part = Partition(max_instances=n, max_commands=n, max_records_per_batch=256)
+    part = Partition(max_instances=n, max_commands=n, max_records_per_batch=int(os.environ.get("FUZZ_MAX_RECORDS", 256)))
     orc = Oracle()
     assert part.deploy(xml) == orc.deploy(xml) == 0
     clock = NOW
