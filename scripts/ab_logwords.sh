@@ -12,7 +12,7 @@ ZBHIP_LOG_BLOCKS=16 timeout -k 10 400 python -u -m pytest tests/test_gpu_logdev.
 for b in ${BLOCKS:-16}; do
   ZBHIP_DEBUG=1 ZBHIP_LOG_BLOCKS=$b timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_b$b -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-io > $O/b$b.json 2>> $O/err.txt
 done
-ZBHIP_LOG_HALFWAVE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_half -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-io > $O/half.json 2>> $O/err.txt
+#ZBHIP_LOG_HALFWAVE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_half -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-io > $O/half.json 2>> $O/err.txt
 i=0
 while read -r group; do
   [ -z "$group" ] && continue
