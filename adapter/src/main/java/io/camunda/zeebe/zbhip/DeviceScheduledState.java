@@ -83,17 +83,27 @@ final class DeviceScheduledState {
         return true;
       });
       final long[] deviceNext = {-1};
+      TimerInstance last = null;
       try (Arena a = Arena.ofConfined()) {
         final MemorySegment out = a.allocate(ZbHip.RECORD.byteSize() * CAP, 16);
         final long n = ZbHip.dueTimers(gpu.handle(), timestamp, out, CAP, deviceNext);
         for (long r = 0; r < n; r++) {
-          due.add(timerInstance(out.asSlice(80L * r, 80)));
+          last = timerInstance(out.asSlice(ZbHip.RECORD.byteSize() * r, ZbHip.RECORD.byteSize()));
+          due.add(last);
         }
       }
       // TIMER_DUE_DATES order: [dueDate, [elementInstanceKey, timerKey]]
-      due.sort(Comparator.comparingLong(TimerInstance::getDueDate)
-          .thenComparingLong(TimerInstance::getElementInstanceKey).thenComparingLong(TimerInstance::getKey));
+      final Comparator<TimerInstance> order = Comparator.comparingLong(TimerInstance::getDueDate)
+          .thenComparingLong(TimerInstance::getElementInstanceKey).thenComparingLong(TimerInstance::getKey);
+      due.sort(order);
+      // a truncated device scan (due rows left out): the first row left out may precede engine timers
+      // ordered after the last row returned, so the visit stops there and the checker runs again at the
+      // date returned (processTimersWithDueDateBefore stops at any timer its visitor refuses, :87-116)
+      final TimerInstance bound = last != null && deviceNext[0] >= 0 && deviceNext[0] <= timestamp ? last : null;
       for (final TimerInstance t : due) {
+        if (bound != null && order.compare(t, bound) > 0) {
+          return Math.min(t.getDueDate(), deviceNext[0]);
+        }
         if (!consumer.visit(t)) {
           return t.getDueDate();
         }
@@ -104,14 +114,14 @@ final class DeviceScheduledState {
 
     /** A TIMER:TRIGGER row of zbhip_due_timers as the TimerInstance the visitor writes it from. */
     private TimerInstance timerInstance(final MemorySegment r) {
-      final ZbHip.Deployed d = gpu.process(r.get(JAVA_INT, 32));
+      final ZbHip.Deployed d = gpu.process(r.get(JAVA_INT, ZbHip.Rec.PROCESS_IDX));
       final TimerInstance t = new TimerInstance();
-      t.setKey(r.get(JAVA_LONG, 0));
-      t.setElementInstanceKey(r.get(JAVA_LONG, 8));
-      t.setProcessInstanceKey(r.get(JAVA_LONG, 16));
-      t.setDueDate(r.get(JAVA_LONG, 48));
-      t.setHandlerNodeId(new UnsafeBuffer(d.elementIds()[r.get(JAVA_INT, 36)].getBytes()));
-      t.setRepetitions(r.get(JAVA_INT, 68));
+      t.setKey(r.get(JAVA_LONG, ZbHip.Rec.KEY));
+      t.setElementInstanceKey(r.get(JAVA_LONG, ZbHip.Rec.SCOPE_KEY));
+      t.setProcessInstanceKey(r.get(JAVA_LONG, ZbHip.Rec.PROCESS_INSTANCE_KEY));
+      t.setDueDate(r.get(JAVA_LONG, ZbHip.Rec.AUX));
+      t.setHandlerNodeId(new UnsafeBuffer(d.elementIds()[r.get(JAVA_INT, ZbHip.Rec.ELEMENT_IDX)].getBytes()));
+      t.setRepetitions(r.get(JAVA_INT, ZbHip.Rec.PARTITION)); // zbhip_due_timers: repetitions in partition
       t.setProcessDefinitionKey(d.definitionKey());
       t.setTenantId(TimerRecord.DEFAULT_TENANT_ID);
       return t;
@@ -149,18 +159,27 @@ final class DeviceScheduledState {
         due.add(new Due(copy.getDeadline(), key, copy));
         return true;
       });
+      Due last = null;
+      final long[] deviceNext = {-1};
       if (gpu.scheduledReady()) {
         try (Arena a = Arena.ofConfined()) {
           final MemorySegment out = a.allocate(ZbHip.RECORD.byteSize() * CAP, 16);
-          final long n = ZbHip.timedOutJobs(gpu.handle(), upperBound, out, CAP);
+          final long n = ZbHip.timedOutJobs(gpu.handle(), upperBound, out, CAP, deviceNext);
           for (long r = 0; r < n; r++) {
-            final MemorySegment row = out.asSlice(80L * r, 80);
-            due.add(new Due(row.get(JAVA_LONG, 56), row.get(JAVA_LONG, 0), gpu.storedJob(row)));
+            final MemorySegment row = out.asSlice(ZbHip.RECORD.byteSize() * r, ZbHip.RECORD.byteSize());
+            last = new Due(row.get(JAVA_LONG, ZbHip.Rec.MESSAGE_KEY), row.get(JAVA_LONG, ZbHip.Rec.KEY), gpu.storedJob(row));
+            due.add(last);
           }
         }
       }
-      due.sort(Comparator.comparingLong(Due::deadline).thenComparingLong(Due::key)); // [deadline, jobKey]
+      final Comparator<Due> order = Comparator.comparingLong(Due::deadline).thenComparingLong(Due::key);
+      due.sort(order); // [deadline, jobKey]
+      // a truncated device list: engine entries past its last row wait for the trigger's next run
+      final Due bound = last != null && deviceNext[0] >= 0 ? last : null;
       for (final Due d : due) {
+        if (bound != null && order.compare(d, bound) > 0) {
+          return;
+        }
         if (!callback.test(d.key(), d.job())) {
           return;
         }

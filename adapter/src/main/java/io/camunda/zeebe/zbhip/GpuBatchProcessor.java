@@ -373,6 +373,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     final RecordMetadata meta = new RecordMetadata();
     final Iterator<Continuation> next = continuations.iterator();
     int claimed = 0;
+    jobStreams.sync(handle, deviceJobTypes()); // the streams open now (pushFenced reads them)
     while (reader.hasNext() && window.size() < WINDOW) {
       final LoggedEvent event = reader.next();
       event.readMetadata(meta);
@@ -385,6 +386,9 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
         break; // the engine's: the window ends before it (log order is kept)
       }
       final ValueType vt = meta.getValueType();
+      if (pushFenced(rec, vt, claimed)) {
+        break; // the next window takes it
+      }
       if (vt == ValueType.PROCESS_INSTANCE_CREATION) {
         final ProcessInstanceCreationRecord create = (ProcessInstanceCreationRecord) rec.getValue();
         final int slot = takeSlot();
@@ -416,11 +420,36 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     // keys the engine generated since the last window come first (setKeyIfHigher)
     ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
     // the window's clock: TIMER:CREATED dueDates (CatchEventBehavior.java:310, ActorClock), pushed jobs'
-    // deadlines; the job streams open now (publishWork asks JobStreamer per job)
+    // deadlines (the job streams were synced before the read-ahead: publishWork asks JobStreamer per job)
     ZbHip.setClock(handle, ActorClock.currentTimeMillis());
-    jobStreams.sync(handle, deviceJobTypes());
     window.submitRun(handle);
     windowDone = false;
+  }
+
+  /**
+   * A job stream's push gathers the job's variables when the push record is appended (JobStreams.push:
+   * zbhip_job_variables), after the whole window ran; the reference gathers them in publishWork, at
+   * JOB:CREATED (BpmnJobActivationBehavior.java:83).  While a stream pushes, a window holds at most one
+   * command per process instance, so no later command of the window changes what a push reads or ends
+   * its job (adapter.py _push_fenced).
+   */
+  private boolean pushFenced(final TypedRecord rec, final ValueType vt, final int claimed) {
+    if (!jobStreams.pushing()) {
+      return false;
+    }
+    final int instance;
+    if (vt == ValueType.JOB || vt == ValueType.TIMER) {
+      instance = (int) (ZbHip.resolveKey(handle, rec.getKey()) >>> 16);
+    } else if (vt == ValueType.PROCESS_INSTANCE || vt == ValueType.PROCESS_INSTANCE_BATCH) {
+      instance = continuations.stream().skip(claimed).findFirst().orElseThrow().slot();
+    } else if (vt == ValueType.PROCESS_MESSAGE_SUBSCRIPTION) {
+      try (Arena a = Arena.ofConfined()) {
+        instance = messages.of(rec, this, a).instance();
+      }
+    } else {
+      return false;
+    }
+    return window.addresses(instance);
   }
 
   /** A process instance completed (Window.emit): its slot is free once its continuations ran. */
@@ -614,7 +643,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     try (Arena a = Arena.ofConfined()) {
       final MemorySegment r = a.allocate(ZbHip.RECORD.byteSize() * 2, 8);
       final long n = ZbHip.timeOutJob(handle, record.getKey(), ActorClock.currentTimeMillis(), r);
-      if (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value()) {
+      if (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, ZbHip.Rec.RECORD_TYPE) == RecordType.COMMAND_REJECTION.value()) {
         final RecordMetadata meta = new RecordMetadata().valueType(ValueType.JOB);
         meta.recordType(RecordType.COMMAND_REJECTION).intent(JobIntent.TIME_OUT)
             .rejectionType(io.camunda.zeebe.protocol.record.RejectionType.NOT_FOUND)
@@ -649,11 +678,11 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
         keyGenerator.setKeyIfHigher(ZbHip.currentKey(handle));
         return engine.process(record, out);
       }
-      if (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value()) {
+      if (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, ZbHip.Rec.RECORD_TYPE) == RecordType.COMMAND_REJECTION.value()) {
         final RecordMetadata meta = new RecordMetadata().valueType(ValueType.JOB);
         meta.recordType(RecordType.COMMAND_REJECTION).intent(JobIntent.FAIL)
             .rejectionType(io.camunda.zeebe.protocol.record.RejectionType.get(
-                (short) (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 43) & 0xFF)))
+                (short) (r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, ZbHip.Rec.REJECTION_TYPE) & 0xFF)))
             .rejectionReason(rejectionReason(r));
         out.appendRecord(record.getKey(), v, meta);
         return out.build();
@@ -670,21 +699,33 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     return out.build();
   }
 
-  /** Event rows of a host-side job call (TIMED_OUT / FAILED / JOB_BATCH push / INCIDENT); true if an incident. */
+  /**
+   * Event rows of a host-side job call (TIMED_OUT / FAILED / JOB_BATCH push / INCIDENT); true if an incident.
+   * A job made activatable again (TIMED_OUT, FAILED with retries left) went through publishWork: pushed, or
+   * without a stream notifyJobAvailable (BpmnJobActivationBehavior.java:97-111).
+   */
   private boolean appendDeviceRecords(final MemorySegment rows, final long n, final ProcessingResultBuilder out) {
-    boolean incident = false;
+    boolean incident = false, pushed = false;
+    JobRecord activatable = null;
     for (long k = 0; k < n; k++) {
       final MemorySegment r = rows.asSlice(ZbHip.RECORD.byteSize() * k, ZbHip.RECORD.byteSize());
-      final ValueType vt = ValueType.get((short) r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 41));
-      final byte intent = r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, 42);
+      final ValueType vt = ValueType.get((short) r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, ZbHip.Rec.VALUE_TYPE));
+      final byte intent = r.get(java.lang.foreign.ValueLayout.JAVA_BYTE, ZbHip.Rec.INTENT);
       final RecordMetadata meta = new RecordMetadata().recordType(RecordType.EVENT).valueType(vt)
           .intent(io.camunda.zeebe.protocol.record.intent.Intent.fromProtocolValue(vt, intent));
       final var value = window.valueOf(r, this);
-      out.appendRecord(r.get(java.lang.foreign.ValueLayout.JAVA_LONG, 0), value, meta);
+      out.appendRecord(r.get(java.lang.foreign.ValueLayout.JAVA_LONG, ZbHip.Rec.KEY), value, meta);
       if (vt == ValueType.JOB_BATCH) {
         jobStreams.push(out, handle, (JobBatchRecord) value, this);
+        pushed = true;
+      } else if (vt == ValueType.JOB && (intent == JobIntent.TIMED_OUT.value()
+          || (intent == JobIntent.FAILED.value() && ((JobRecord) value).getRetries() > 0))) {
+        activatable = (JobRecord) value;
       }
       incident |= vt == ValueType.INCIDENT;
+    }
+    if (activatable != null && !pushed) {
+      jobStreams.notifyAvailable(out, activatable.getType());
     }
     return incident;
   }

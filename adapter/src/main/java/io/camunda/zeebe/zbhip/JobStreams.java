@@ -58,6 +58,22 @@ final class JobStreams {
     }
   }
 
+  /**
+   * publishWork without a stream for the job's type: notifyJobAvailable's side effect, post-commit
+   * (BpmnJobActivationBehavior.java:97-111) -- long-polling workers of that type are woken.
+   */
+  void notifyAvailable(final ProcessingResultBuilder out, final String type) {
+    out.appendPostCommitTask(() -> {
+      streamer.notifyWorkAvailable(type);
+      return true;
+    });
+  }
+
+  /** Whether a device job type has a stream now (the device pushes its jobs). */
+  boolean pushing() {
+    return !onDevice.isEmpty();
+  }
+
   /** The stream's timeout of a push record's JobBatchRecord (createJobBatchRecord :122-131). */
   long timeout(final String type) {
     final JobStream s = onDevice.get(type);

@@ -321,14 +321,15 @@ final class Window {
     final RecordMetadata meta = new RecordMetadata();
     commandTimestamp = command.getTimestamp(); // a MESSAGE record's deadline = timestamp + timeToLive
     int admitted = 0;
+    final java.util.LinkedHashMap<Long, String> created = new java.util.LinkedHashMap<>(); // jobs not pushed (yet)
     for (long r = 0; r < nr; r++) {
       final MemorySegment rec = recs.asSlice(80L * r, 80);
-      final long key = rec.get(JAVA_LONG, 0);
-      final byte recordType = rec.get(JAVA_BYTE, 40);
-      final byte valueType = rec.get(JAVA_BYTE, 41);
-      final byte intent = rec.get(JAVA_BYTE, 42);
-      final int rejection = rec.get(JAVA_BYTE, 43) & 0xFF;
-      final int ordinal = rec.get(JAVA_SHORT, 44) & 0xFFFF;
+      final long key = rec.get(JAVA_LONG, ZbHip.Rec.KEY);
+      final byte recordType = rec.get(JAVA_BYTE, ZbHip.Rec.RECORD_TYPE);
+      final byte valueType = rec.get(JAVA_BYTE, ZbHip.Rec.VALUE_TYPE);
+      final byte intent = rec.get(JAVA_BYTE, ZbHip.Rec.INTENT);
+      final int rejection = rec.get(JAVA_BYTE, ZbHip.Rec.REJECTION_TYPE) & 0xFF;
+      final int ordinal = rec.get(JAVA_SHORT, ZbHip.Rec.ORDINAL) & 0xFFFF;
       meta.reset()
           .recordType(RecordType.values()[recordType])
           .valueType(ValueType.get((short) valueType))
@@ -341,33 +342,41 @@ final class Window {
       final UnifiedRecordValue value = ofCommand ? (UnifiedRecordValue) command.getValue() : value(rec, i, p);
       out.appendRecord(key, value, meta);
       if (recordType == RecordType.COMMAND.value()) {
-        if (rec.get(JAVA_BYTE, 77) != 0) { // zbhip_record.unprocessed: a continuation, its id in aux
+        if (rec.get(JAVA_BYTE, ZbHip.Rec.UNPROCESSED) != 0) { // zbhip_record.unprocessed: a continuation, its id in aux
           if (value instanceof final ProcessInstanceRecord v) {
             p.expectContinuation(new GpuBatchProcessor.Continuation(
-                rec.get(JAVA_LONG, 48), instances[i], key, valueType, intent, v.getElementId(), v.getFlowScopeKey(),
+                rec.get(JAVA_LONG, ZbHip.Rec.AUX), instances[i], key, valueType, intent, v.getElementId(), v.getFlowScopeKey(),
                 -1, v.getProcessInstanceKey()));
           } else {
             final ProcessInstanceBatchRecord v = (ProcessInstanceBatchRecord) value;
             p.expectContinuation(new GpuBatchProcessor.Continuation(
-                rec.get(JAVA_LONG, 48), instances[i], key, valueType, intent, null, -1,
+                rec.get(JAVA_LONG, ZbHip.Rec.AUX), instances[i], key, valueType, intent, null, -1,
                 v.getBatchElementInstanceKey(), v.getProcessInstanceKey()));
           }
         } else {
           admitted++;
         }
       } else if (valueType == ValueType.PROCESS_INSTANCE.value()
-          && intent == ProcessInstanceIntent.ELEMENT_COMPLETED.value() && rec.get(JAVA_INT, 36) == 0) {
+          && intent == ProcessInstanceIntent.ELEMENT_COMPLETED.value() && rec.get(JAVA_INT, ZbHip.Rec.ELEMENT_IDX) == 0) {
         p.instanceEnded(instances[i]); // the process element (index 0) completed
+      } else if (valueType == ValueType.JOB.value() && recordType == RecordType.EVENT.value()
+          && intent == JobIntent.CREATED.value()) {
+        created.put(key, ((JobRecord) value).getType());
       } else if (valueType == ValueType.JOB_BATCH.value() && recordType == RecordType.EVENT.value()) {
         p.jobStreams().push(out, handle, (JobBatchRecord) value, p); // publishWork's push, post-commit
+        created.remove(((JobBatchRecord) value).jobKeys().iterator().next().getValue());
       } else if (valueType == ValueType.TIMER.value() && recordType == RecordType.EVENT.value()
           && intent == TimerIntent.CREATED.value()) {
         p.timerCreated(out, ((TimerRecord) value).getDueDate()); // DueDateTimerChecker.scheduleTimer, post-commit
       } else if (valueType == ValueType.MESSAGE_SUBSCRIPTION.value() && recordType == RecordType.EVENT.value()) {
-        p.messages().onSubscriptionEvent(meta.getIntent(), (MessageSubscriptionRecord) value, rec.get(JAVA_INT, 64));
+        p.messages().onSubscriptionEvent(meta.getIntent(), (MessageSubscriptionRecord) value, rec.get(JAVA_INT, ZbHip.Rec.CORRELATION_KEY));
       } else if (valueType == ValueType.PROCESS_MESSAGE_SUBSCRIPTION.value() && recordType == RecordType.EVENT.value()) {
         p.messages().onProcessSubscriptionEvent(meta.getIntent(), (ProcessMessageSubscriptionRecord) value, instances[i], p);
       }
+    }
+    // publishWork of a created job no stream took: notifyJobAvailable (BpmnJobActivationBehavior.java:97-111)
+    for (final String type : created.values()) {
+      p.jobStreams().notifyAvailable(out, type);
     }
     return admitted;
   }
@@ -393,12 +402,12 @@ final class Window {
   }
 
   private UnifiedRecordValue value(final MemorySegment r, final int i, final GpuBatchProcessor p) {
-    final ZbHip.Deployed d = p.process(r.get(JAVA_INT, 32) < 0 ? 0 : r.get(JAVA_INT, 32));
-    final int elem = r.get(JAVA_INT, 36);
-    final long scope = r.get(JAVA_LONG, 8);
-    final long pik = r.get(JAVA_LONG, 16);
-    final long aux = r.get(JAVA_LONG, 48);
-    final ValueType vt = ValueType.get((short) r.get(JAVA_BYTE, 41));
+    final ZbHip.Deployed d = p.process(r.get(JAVA_INT, ZbHip.Rec.PROCESS_IDX) < 0 ? 0 : r.get(JAVA_INT, ZbHip.Rec.PROCESS_IDX));
+    final int elem = r.get(JAVA_INT, ZbHip.Rec.ELEMENT_IDX);
+    final long scope = r.get(JAVA_LONG, ZbHip.Rec.SCOPE_KEY);
+    final long pik = r.get(JAVA_LONG, ZbHip.Rec.PROCESS_INSTANCE_KEY);
+    final long aux = r.get(JAVA_LONG, ZbHip.Rec.AUX);
+    final ValueType vt = ValueType.get((short) r.get(JAVA_BYTE, ZbHip.Rec.VALUE_TYPE));
     switch (vt) {
       case PROCESS_INSTANCE -> {
         final ProcessInstanceRecord v = new ProcessInstanceRecord();
@@ -430,17 +439,17 @@ final class Window {
         if (aux >= 0) {
           v.setVariables(documents[i]); // JOB:COMPLETED / COMPLETE rejection: the command's variables
         }
-        final long deadline = r.get(JAVA_LONG, 56); // message_key: an ACTIVATED job's deadline
+        final long deadline = r.get(JAVA_LONG, ZbHip.Rec.MESSAGE_KEY); // message_key: an ACTIVATED job's deadline
         if (deadline != -1) {
-          final int worker = r.get(JAVA_INT, 64); // correlation_key: its worker (value dictionary)
+          final int worker = r.get(JAVA_INT, ZbHip.Rec.CORRELATION_KEY); // correlation_key: its worker (value dictionary)
           v.setDeadline(deadline)
               .setWorker(new UnsafeBuffer(worker == Messages.NO_STRING ? new byte[0] : p.stringValue(worker)));
         }
-        if (r.get(JAVA_BYTE, 40) == RecordType.EVENT.value() && (r.get(JAVA_BYTE, 47) & 1) != 0) {
+        if (r.get(JAVA_BYTE, ZbHip.Rec.RECORD_TYPE) == RecordType.EVENT.value() && (r.get(JAVA_BYTE, ZbHip.Rec.REASON_ARG) & 1) != 0) {
           // a failed job's stored retries and errorMessage (JobFailProcessor.failJob): reason_arg bit 0,
           // retries in partition, the errorMessage's value-dictionary id in message_name | bpmn_process_id << 16
-          final int eid = (r.get(JAVA_SHORT, 68) & 0xFFFF) | (r.get(JAVA_SHORT, 70) & 0xFFFF) << 16;
-          v.setRetries(r.get(JAVA_INT, 72))
+          final int eid = (r.get(JAVA_SHORT, ZbHip.Rec.MESSAGE_NAME) & 0xFFFF) | (r.get(JAVA_SHORT, ZbHip.Rec.BPMN_PROCESS_ID) & 0xFFFF) << 16;
+          v.setRetries(r.get(JAVA_INT, ZbHip.Rec.PARTITION))
               .setErrorMessage(eid == Messages.NO_STRING ? "" : new String(p.stringValue(eid), java.nio.charset.StandardCharsets.UTF_8));
         }
         return v.setTenantId(TENANT);
@@ -465,7 +474,7 @@ final class Window {
         // aux == ZBHIP_AUX_INLINE: a value the engine computed (a multi-instance loop variable), its
         // zbhip_doc_type in zbhip_record.partition and the value in message_key
         v.setName(new UnsafeBuffer(p.name(elem).getBytes()))
-            .setValue(aux == -2 ? inline(r.get(JAVA_INT, 72), r.get(JAVA_LONG, 56), p) : entryValues.get((int) aux))
+            .setValue(aux == -2 ? inline(r.get(JAVA_INT, ZbHip.Rec.PARTITION), r.get(JAVA_LONG, ZbHip.Rec.MESSAGE_KEY), p) : entryValues.get((int) aux))
             .setScopeKey(scope)
             .setProcessInstanceKey(pik)
             .setProcessDefinitionKey(d.definitionKey())
@@ -476,7 +485,7 @@ final class Window {
         final ProcessEventRecord v = new ProcessEventRecord();
         v.setScopeKey(scope)
             .setTargetElementIdBuffer(new UnsafeBuffer(d.elementIds()[elem].getBytes()));
-        if (r.get(JAVA_BYTE, 42) == ProcessEventIntent.TRIGGERING.value()) {
+        if (r.get(JAVA_BYTE, ZbHip.Rec.INTENT) == ProcessEventIntent.TRIGGERING.value()) {
           v.setVariablesBuffer(documents[i]); // TRIGGERED: processEventTriggered resets the record
         }
         v
@@ -492,7 +501,7 @@ final class Window {
             .setProcessInstanceKey(pik)
             .setDueDate(aux)
             // zbhip_record.partition: the TimerRecord's repetitions (-1 infinite); a rejection: 1
-            .setRepetitions(r.get(JAVA_BYTE, 40) == RecordType.COMMAND_REJECTION.value() ? 1 : r.get(JAVA_INT, 72))
+            .setRepetitions(r.get(JAVA_BYTE, ZbHip.Rec.RECORD_TYPE) == RecordType.COMMAND_REJECTION.value() ? 1 : r.get(JAVA_INT, ZbHip.Rec.PARTITION))
             .setTargetElementId(new UnsafeBuffer(elem >= 0 ? d.elementIds()[elem].getBytes() : new byte[0]))
             .setProcessDefinitionKey(elem >= 0 ? d.definitionKey() : -1);
         return v.setTenantId(TENANT);
@@ -501,14 +510,14 @@ final class Window {
         // BpmnIncidentBehavior.createIncident (:51-71) of an exclusive gateway: the ErrorType ordinal
         // in zbhip_record.partition, the message composed by the library (zbhip_incident_message)
         final IncidentRecord v = new IncidentRecord();
-        final boolean job = r.get(JAVA_INT, 72) == ErrorType.JOB_NO_RETRIES.ordinal();
+        final boolean job = r.get(JAVA_INT, ZbHip.Rec.PARTITION) == ErrorType.JOB_NO_RETRIES.ordinal();
         if (job) { // JobFailProcessor.raiseIncident (:139-162): the job's key and message
-          final int mid = r.get(JAVA_INT, 64);
+          final int mid = r.get(JAVA_INT, ZbHip.Rec.CORRELATION_KEY);
           v.setJobKey(aux).setErrorMessage(new String(p.stringValue(mid), java.nio.charset.StandardCharsets.UTF_8));
         } else {
           v.setErrorMessage(p.incidentMessage(r));
         }
-        v.setErrorType(ErrorType.values()[r.get(JAVA_INT, 72)])
+        v.setErrorType(ErrorType.values()[r.get(JAVA_INT, ZbHip.Rec.PARTITION)])
             .setBpmnProcessId(new UnsafeBuffer(d.bpmnProcessId().getBytes()))
             .setProcessDefinitionKey(d.definitionKey())
             .setProcessInstanceKey(pik)
@@ -520,7 +529,7 @@ final class Window {
       case PROCESS_INSTANCE_BATCH -> {
         // a multi-instance body's activateChildInstancesInBatches (index in zbhip_record.partition)
         final ProcessInstanceBatchRecord v = new ProcessInstanceBatchRecord();
-        return v.setProcessInstanceKey(pik).setBatchElementInstanceKey(scope).setIndex(r.get(JAVA_INT, 72));
+        return v.setProcessInstanceKey(pik).setBatchElementInstanceKey(scope).setIndex(r.get(JAVA_INT, ZbHip.Rec.PARTITION));
       }
       case PROCESS_INSTANCE_CREATION -> {
         final ProcessInstanceCreationRecord v = new ProcessInstanceCreationRecord();
@@ -545,13 +554,13 @@ final class Window {
    */
   private static UnifiedRecordValue messageValue(final MemorySegment r, final ValueType vt, final ZbHip.Deployed d,
       final int elem, final long scope, final long pik, final GpuBatchProcessor p, final long timestamp) {
-    final int nameId = r.get(JAVA_SHORT, 68) & 0xFFFF, bpmnId = r.get(JAVA_SHORT, 70) & 0xFFFF;
-    final int corrId = r.get(JAVA_INT, 64);
+    final int nameId = r.get(JAVA_SHORT, ZbHip.Rec.MESSAGE_NAME) & 0xFFFF, bpmnId = r.get(JAVA_SHORT, ZbHip.Rec.BPMN_PROCESS_ID) & 0xFFFF;
+    final int corrId = r.get(JAVA_INT, ZbHip.Rec.CORRELATION_KEY);
     final DirectBuffer name = new UnsafeBuffer((nameId == 0xFFFF ? "" : p.name(nameId)).getBytes());
     final DirectBuffer bpmn = new UnsafeBuffer((bpmnId == 0xFFFF ? "" : p.name(bpmnId)).getBytes());
     final DirectBuffer corr = new UnsafeBuffer(corrId == Messages.NO_STRING ? new byte[0] : p.stringValue(corrId));
-    final boolean interrupting = r.get(JAVA_BYTE, 76) != 0;
-    final long messageKey = r.get(JAVA_LONG, 56);
+    final boolean interrupting = r.get(JAVA_BYTE, ZbHip.Rec.INTERRUPTING) != 0;
+    final long messageKey = r.get(JAVA_LONG, ZbHip.Rec.MESSAGE_KEY);
     if (vt == ValueType.MESSAGE) {
       return new MessageRecord().setName(name).setCorrelationKey(corr).setTimeToLive(0).setDeadline(timestamp)
           .setTenantId(TENANT);
@@ -561,10 +570,10 @@ final class Window {
           .setMessageKey(messageKey).setMessageName(name).setCorrelationKey(corr).setInterrupting(interrupting)
           .setBpmnProcessId(bpmn).setTenantId(TENANT);
     }
-    return new ProcessMessageSubscriptionRecord().setSubscriptionPartitionId(r.get(JAVA_INT, 72))
+    return new ProcessMessageSubscriptionRecord().setSubscriptionPartitionId(r.get(JAVA_INT, ZbHip.Rec.PARTITION))
         .setProcessInstanceKey(pik).setElementInstanceKey(scope).setMessageKey(messageKey).setMessageName(name)
         .setInterrupting(interrupting).setBpmnProcessId(bpmn).setCorrelationKey(corr)
-        .setElementId(new UnsafeBuffer((elem >= 0 && r.get(JAVA_INT, 32) >= 0 ? d.elementIds()[elem] : "").getBytes()))
+        .setElementId(new UnsafeBuffer((elem >= 0 && r.get(JAVA_INT, ZbHip.Rec.PROCESS_IDX) >= 0 ? d.elementIds()[elem] : "").getBytes()))
         .setTenantId(TENANT);
   }
 

@@ -110,6 +110,35 @@ public final class ZbHip {
           JAVA_BYTE.withName("unprocessed"),
           MemoryLayout.paddingLayout(2)); // 80 bytes
 
+  /** Byte offsets of zbhip_record fields, taken from RECORD (one source for every reader of a row). */
+  public static final class Rec {
+    private static long off(final String f) {
+      return RECORD.byteOffset(MemoryLayout.PathElement.groupElement(f));
+    }
+
+    public static final long KEY = off("key");
+    public static final long SCOPE_KEY = off("scope_key");
+    public static final long PROCESS_INSTANCE_KEY = off("process_instance_key");
+    public static final long PROCESS_IDX = off("process_idx");
+    public static final long ELEMENT_IDX = off("element_idx");
+    public static final long RECORD_TYPE = off("record_type");
+    public static final long VALUE_TYPE = off("value_type");
+    public static final long INTENT = off("intent");
+    public static final long REJECTION_TYPE = off("rejection_type");
+    public static final long ORDINAL = off("ordinal");
+    public static final long REASON_ARG = off("reason_arg");
+    public static final long AUX = off("aux");
+    public static final long MESSAGE_KEY = off("message_key");
+    public static final long CORRELATION_KEY = off("correlation_key");
+    public static final long MESSAGE_NAME = off("message_name");
+    public static final long BPMN_PROCESS_ID = off("bpmn_process_id");
+    public static final long PARTITION = off("partition");
+    public static final long INTERRUPTING = off("interrupting");
+    public static final long UNPROCESSED = off("unprocessed");
+
+    private Rec() {}
+  }
+
   public static final StructLayout XPART =
       MemoryLayout.structLayout(
           JAVA_LONG.withName("element_instance_key"),
@@ -207,7 +236,7 @@ public final class ZbHip {
   private static final MethodHandle DUE_TIMERS =
       fn("zbhip_due_timers", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle TIMED_OUT_JOBS =
-      fn("zbhip_timed_out_jobs", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
+      fn("zbhip_timed_out_jobs", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle TIME_OUT_JOB =
       fn("zbhip_time_out_job",
           FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
@@ -551,11 +580,17 @@ public final class ZbHip {
     }
   }
 
-  /** zbhip_timed_out_jobs: the JOB:TIME_OUT commands of activated device jobs with deadline < now. */
-  public static long timedOutJobs(final MemorySegment h, final long now, final MemorySegment out, final long cap) {
+  /**
+   * zbhip_timed_out_jobs: the JOB:TIME_OUT commands of activated device jobs with deadline < now;
+   * {@code nextDeadline[0]} = the deadline of the first one left out (-1: none).
+   */
+  public static long timedOutJobs(final MemorySegment h, final long now, final MemorySegment out, final long cap,
+      final long[] nextDeadline) {
     try (Arena a = Arena.ofConfined()) {
       final MemorySegment n = a.allocate(JAVA_LONG);
-      check((int) call(TIMED_OUT_JOBS, h, now, out, cap, n), "zbhip_timed_out_jobs");
+      final MemorySegment next = a.allocate(JAVA_LONG);
+      check((int) call(TIMED_OUT_JOBS, h, now, out, cap, n, next), "zbhip_timed_out_jobs");
+      nextDeadline[0] = next.get(JAVA_LONG, 0);
       return n.get(JAVA_LONG, 0);
     }
   }

@@ -79,7 +79,8 @@ enum zbhip_value_type {
   ZBHIP_VT_PROCESS_INSTANCE_CREATION = 19,
   ZBHIP_VT_PROCESS_EVENT = 24,
   ZBHIP_VT_TIMER = 15,
-  ZBHIP_VT_PROCESS_INSTANCE_BATCH = 34
+  ZBHIP_VT_PROCESS_INSTANCE_BATCH = 34,
+  ZBHIP_VT_JOB_BATCH = 14  /* JOB_BATCH (protocol.xml:31): a job stream's push */
 };
 enum zbhip_rejection_type {
   ZBHIP_REJ_INVALID_ARGUMENT = 0,
@@ -108,7 +109,6 @@ enum zbhip_pi_intent {
 enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2, ZBHIP_JOB_TIME_OUT = 3,
        ZBHIP_JOB_TIMED_OUT = 4, ZBHIP_JOB_FAIL = 5, ZBHIP_JOB_FAILED = 6, ZBHIP_JOB_CANCELED = 10 };
 enum { ZBHIP_JOB_BATCH_ACTIVATE = 0, ZBHIP_JOB_BATCH_ACTIVATED = 1 };  /* JobBatchIntent */
-#define ZBHIP_VT_JOB_BATCH 1
 enum { ZBHIP_VAR_CREATED = 0, ZBHIP_VAR_UPDATED = 1 };
 enum { ZBHIP_PE_TRIGGERING = 0, ZBHIP_PE_TRIGGERED = 1 };
 enum { ZBHIP_PIC_CREATE = 0, ZBHIP_PIC_CREATED = 1 };
@@ -803,13 +803,19 @@ int zbhip_job_batch_rejection_reason(const zbhip_job_activation* cmd, const zbhi
  * DbTimerInstanceState.processTimersWithDueDateBefore (state/instance/DbTimerInstanceState.java:87-116):
  * the TIMER:TRIGGER commands of the device timers with dueDate <= now, in TIMER_DUE_DATES order
  * (dueDate, elementInstanceKey, timer key); at most cap, *next_due = the first dueDate not returned
- * (-1: none) -- what DueDateChecker reschedules with.  A device scan (k_due_timers, 16 B per instance). */
+ * (-1: none) -- what DueDateChecker reschedules with.  A device scan (k_due_timers, 16 B per instance).
+ * Truncated (n == cap and *next_due <= now: due rows were left out), a merge with the engine's
+ * TIMER_DUE_DATES visits the engine's timers only up to the last row returned and stops there
+ * (processTimersWithDueDateBefore may stop at any timer; the checker runs again at the returned date). */
 int zbhip_due_timers(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out, int64_t* next_due);
 /* JobTimeoutTrigger.DeactivateTimeOutJobs (processing/job/JobTimeoutTrigger.java:74-87) ->
  * DbJobState.forEachTimedOutEntry (state/instance/DbJobState.java:286-298): the JOB:TIME_OUT commands
  * (key = the job, value = the stored job) of ACTIVATED device jobs with deadline < now, in JOB_DEADLINES
- * order (deadline, key). */
-int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out);
+ * order (deadline, key); at most cap, *next_deadline = the deadline of the first timed-out job not returned
+ * (-1: none were left out; NULL allowed).  A merge with the engine's JOB_DEADLINES then visits the
+ * engine's entries only up to the last row returned (the rest come with the trigger's next run). */
+int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out,
+                         int64_t* next_deadline);
 /* JOB:TIME_OUT of a device job (JobTimeOutProcessor.processRecord, processing/job/JobTimeOutProcessor
  * .java:46-73; `now` = ActorClock.currentTimeMillis()): out[0] = JOB:TIMED_OUT with the stored job
  * (JobTimedOutApplier -> DbJobState.timeout: ACTIVATABLE again, deadline and worker kept) and, with a job

@@ -96,6 +96,8 @@ def lib():
         L.zbo_outbox.restype = C.c_size_t
         L.zbo_outbox.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.zbo_clear_outbox.argtypes = [C.c_void_p]
+        L.zbo_take_notified.restype = C.c_size_t
+        L.zbo_take_notified.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
         L.zbo_subscription_partition.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
         L.zbo_java_hash.restype = C.c_int32
         L.zbo_java_hash.argtypes = [C.c_char_p, C.c_size_t]
@@ -207,6 +209,14 @@ class Oracle:
         out = abi.make_docs(max(n, 1))
         self.L.zbo_list_items(self.h, list_id, out.ctypes.data, n)
         return [(int(x["type"]), int(x["value"])) for x in out[:n]]
+
+    def take_notified(self):
+        """The job types publishWork notified (JobStreamer.notifyWorkAvailable, no stream) since the last
+        call, in order."""
+        n = self.L.zbo_take_notified(self.h, None, 0)
+        buf = C.create_string_buffer(max(n, 1))
+        self.L.zbo_take_notified(self.h, buf, n)
+        return buf.raw[:n].decode().split("\n")[:-1] if n else []
 
     def outbox(self, clear=True):
         n = self.L.zbo_outbox(self.h, None, 0)

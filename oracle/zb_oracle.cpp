@@ -1126,6 +1126,22 @@ static int subscription_partition(const std::string& b, int partition_count) {
   return (r < 0 ? -r : r) + 1;
 }
 
+// StringUtil.limitString(message, maxLength) (util/.../StringUtil.java:50-56) on the UTF-8 bytes of a Java
+// String: the length counts UTF-16 code units (a character beyond the BMP is two); a cut inside a
+// surrogate pair keeps the lone high surrogate, which String.getBytes(UTF_8) writes as '?'
+static std::string limit_java_string(const std::string& s, size_t max_units) {
+  size_t units = 0, i = 0;
+  while (i < s.size()) {
+    const unsigned char c = (unsigned char)s[i];
+    const size_t len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : 4;
+    const size_t u = len == 4 ? 2 : 1;
+    if (units + u > max_units) return s.substr(0, i) + (units < max_units ? "?" : "") + "...";
+    units += u;
+    i += len;
+  }
+  return s;
+}
+
 struct Unsupported {
   std::string what;
 };
@@ -1143,6 +1159,8 @@ class Oracle {
   std::vector<zbhip_doc_entry> docs;  // all submitted document entries (global index)
   std::vector<zbhip_xpart_cmd> xdocs;  // all received cross-partition commands (global index)
   std::vector<zbhip_xpart_cmd> outbox;  // sent cross-partition commands (post-commit side effects)
+  std::vector<std::string> notified;    // job types of publishWork's notifyJobAvailable side effects
+  bool track_notified = false;          // (kept only when a caller takes them: zbo_take_notified)
   std::string last_error;
 
   // value dictionary (zbhip_intern_string)
@@ -2594,7 +2612,7 @@ class Oracle {
     const int retries = cmd.r.partition;
     const int64_t backoff = cmd.r.message_key;
     std::string msg = cmd.r.correlation_key < strs.size() ? strs[cmd.r.correlation_key] : std::string();
-    if (msg.size() > 10000) msg = msg.substr(0, 10000) + "...";  // StringUtil.limitString (ASCII)
+    msg = limit_java_string(msg, 10000);
     job.retries = retries;
     job.error_message = msg;
     job.retry_backoff = backoff;
@@ -2648,7 +2666,10 @@ class Oracle {
   void publish_work(int64_t jobKey) {
     JobRow& job = jobs_.at(jobKey);
     auto st = streams.find(job.type);
-    if (st == streams.end()) return;
+    if (st == streams.end()) {  // notifyJobAvailable (:103-111): JobStreamer.notifyWorkAvailable(type)
+      if (track_notified) notified.push_back(job.type);
+      return;
+    }
     const int64_t key = next_key();
     job.activated = true;
     job.deadline = now_ms + st->second.second;
@@ -3990,6 +4011,18 @@ size_t zbo_outbox(void* o, zbhip_xpart_cmd* out, size_t cap) {
   return O->outbox.size();
 }
 void zbo_clear_outbox(void* o) { static_cast<Oracle*>(o)->outbox.clear(); }
+// the job types notified since the last call (notifyWorkAvailable side effects), '\n'-separated; cleared
+size_t zbo_take_notified(void* o, char* buf, size_t cap) {
+  auto* O = static_cast<Oracle*>(o);
+  O->track_notified = true;
+  std::string s;
+  for (const auto& t : O->notified) s += t + "\n";
+  if (buf && cap >= s.size()) {
+    std::memcpy(buf, s.data(), s.size());
+    O->notified.clear();
+  }
+  return s.size();
+}
 int zbo_subscription_partition(const char* b, size_t len, int partition_count) {
   return subscription_partition(std::string(b, len), partition_count);
 }

@@ -42,6 +42,18 @@ class RecordingJobStream:
         self.activated_jobs.append((job_key, job))
 
 
+class RecordingJobStreamer:
+    """RecordingJobStreamer's notifications (engine/src/test/.../util/RecordingJobStreamer.java:22-32):
+    notifyWorkAvailable(jobType) counted per type -- publishWork's side effect for a job made activatable
+    with no stream for its type (BpmnJobActivationBehavior.java:97-111)."""
+
+    def __init__(self):
+        self.notifications = {}
+
+    def notify_work_available(self, job_type):
+        self.notifications[job_type] = self.notifications.get(job_type, 0) + 1
+
+
 class Rec:
     """A logged record (LoggedEvent + TypedRecord); position None = UnwrittenRecord."""
     __slots__ = ("position", "source_position", "record_type", "value_type", "intent", "key", "rejection_type",
@@ -513,6 +525,8 @@ class OracleEngine:
         self.tables = []
         self.streams = {}  # job streams: type -> (worker, timeout)
         self.stream_sinks = {}  # job type -> (fetchVariables, push)
+        self.job_streamer = None  # JobStreamer.notifyWorkAvailable of publishWork without a stream
+        self.o.take_notified()  # (the oracle keeps its notifications from now on)
 
     def deploy(self, xml, key, version=1):
         idx = self.o.deploy(xml, key, version)
@@ -654,6 +668,10 @@ class OracleEngine:
             strings = self.o.strings()
             push_side_effects(out, pushes, self.stream_sinks, self.o.job_variables, self.values, self.o.name,
                               lambda i: strings[i].decode())
+        notified = self.o.take_notified()
+        if notified and self.job_streamer is not None:
+            out.append_post_commit_task(lambda types=notified: [self.job_streamer.notify_work_available(t)
+                                                                for t in types] and True)
         sends = self.o.outbox()  # SubscriptionCommandSender's side effects of this command
         if len(sends):
             strings = self.o.strings()

@@ -86,3 +86,20 @@ def test_java_adapter_binds_exported_symbols():
     # the struct sizes the binding documents
     assert C.sizeof(abi.Command) == 16 and C.sizeof(abi.DocEntry) == 16
     assert C.sizeof(abi.Record) == 80 and C.sizeof(abi.XpartCmd) == 48
+
+
+# ValueType of protocol/src/main/resources/protocol.xml:23-53 (transcribed): the Java adapter compares
+# drained rows against ValueType.value(), so the header, the Python mirror and the oracle must use the
+# protocol's numbers (a push row with JOB_BATCH = 1 would fall into the adapter's default branch)
+PROTOCOL_VALUE_TYPES = {"JOB": 0, "PROCESS_INSTANCE": 5, "INCIDENT": 6, "MESSAGE": 10, "MESSAGE_SUBSCRIPTION": 11,
+                        "PROCESS_MESSAGE_SUBSCRIPTION": 12, "JOB_BATCH": 14, "TIMER": 15, "VARIABLE": 17,
+                        "PROCESS_INSTANCE_CREATION": 19, "PROCESS_EVENT": 24, "PROCESS_INSTANCE_BATCH": 34}
+
+
+def test_value_types_equal_protocol_values():
+    src = open(os.path.join(ROOT, "include", "zbhip.h")).read()
+    header = {m.group(1): int(m.group(2)) for m in re.finditer(r"ZBHIP_VT_([A-Z_]+)\s*=\s*(\d+)", src)}
+    assert header == PROTOCOL_VALUE_TYPES
+    for name, value in PROTOCOL_VALUE_TYPES.items():
+        assert getattr(abi, "VT_" + name) == value, name
+    assert "#define ZBHIP_VT_" not in src

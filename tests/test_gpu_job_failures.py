@@ -24,6 +24,8 @@ def test_job_failures_in_the_processing_loop():
     b = bpmn.linear_process(2, process_id="engineOnly", job_type="engine-task")
     deps = [(a, KEY_A, 1), (b, KEY_B, 1)]
     ref, gpu = single(deps, deps[:1])
+    from test_gpu_job_push import notified_equal, notifiers
+    notifiers(ref, gpu)  # failures with retries left (and time-outs) notify the job type again
     write(ref, gpu, *([Client.create("linear") for _ in range(12)] + [Client.create("engineOnly") for _ in range(2)]))
     clock = ref.clock
     write(ref, gpu, Client.activate_jobs("benchmark-task", worker="w1", timeout=60000, max_jobs=6, timestamp=clock.now))
@@ -31,16 +33,20 @@ def test_job_failures_in_the_processing_loop():
     # retries left (activated / never activated), none left (incidents), outside the subset, rejections
     write(ref, gpu, Client.fail_job(jobs[0], 2, "boom, with|separators"), Client.fail_job(jobs[1], 0),
           Client.fail_job(jobs[7], 1), Client.fail_job(jobs[8], 0, "custom message"),
-          Client.fail_job(jobs[9], 3, "", variables=(("reason", 7),)), Client.fail_job(123, 3))
+          Client.fail_job(jobs[9], 3, "", variables=(("reason", 7),)), Client.fail_job(123, 3),
+          # StringUtil.limitString counts UTF-16 code units: the cut falls inside a surrogate pair
+          Client.fail_job(jobs[3], 1, "a" + "\U0001D11E" * 5000))
     write(ref, gpu, Client.fail_job(jobs[1], 3), Client.complete_job(jobs[8]))
     log = gpu.parts[0].log
     incidents = [r for r in log.entries if r.value_type == abi.VT_INCIDENT]
     assert len(incidents) == 2 and {r.value["errorMessage"] for r in incidents} == {"No more retries left.",
                                                                                       "custom message"}
+    assert any(r.value.get("errorMessage", "").endswith("?...") for r in log.entries
+               if r.value_type == abi.VT_JOB and r.intent == abi.JOB_FAILED)
     rej = [r for r in log.entries if r.record_type == abi.RT_REJECTION and r.value_type == abi.VT_JOB]
     assert len(rej) == 3
     ad = gpu.parts[0].adapter
-    assert ad.counts["job_failures"] == 4 and len(ad.handed_off) == 3  # two incidents + the variables' failure
+    assert ad.counts["job_failures"] == 5 and len(ad.handed_off) == 3  # two incidents + the variables' failure
     # the failed jobs with retries left are activated again (their retries), completed or timed out
     write(ref, gpu, Client.activate_jobs("benchmark-task", worker="w2", timeout=10000, max_jobs=20, timestamp=clock.now))
     batch = [r for r in log.entries if r.value_type == VT_JOB_BATCH and r.intent == JOB_BATCH_ACTIVATED]
@@ -65,3 +71,4 @@ def test_job_failures_in_the_processing_loop():
     completed = [r for r in log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_COMPLETED]
     assert any(r.value.get("retries") == 2 and r.value.get("errorMessage") for r in completed)
     check(ref, gpu)
+    notified_equal(ref, gpu)

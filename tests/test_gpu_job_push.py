@@ -33,6 +33,22 @@ def pushed_equal(ref, gpu):
     assert gpu.job_stream.activated_jobs == ref.job_stream.activated_jobs
 
 
+def notifiers(ref, gpu):
+    """RecordingJobStreamer per side: the engine's and the adapter's notifyWorkAvailable side effects."""
+    from psm import RecordingJobStreamer
+    out = []
+    for side, procs in ((ref, [ref.parts[0].engine]), (gpu, [gpu.parts[0].adapter, gpu.parts[0].engine])):
+        side.streamer = RecordingJobStreamer()
+        for p in procs:
+            p.job_streamer = side.streamer
+        out.append(side.streamer)
+    return out
+
+
+def notified_equal(ref, gpu):
+    assert gpu.streamer.notifications == ref.streamer.notifications
+
+
 def pushes(log):
     return [r for r in log.entries if r.value_type == VT_JOB_BATCH and r.intent == JOB_BATCH_ACTIVATED
             and r.value["maxJobsToActivate"] == -1]
@@ -43,7 +59,10 @@ def test_job_push_in_the_processing_loop():
     b = bpmn.linear_process(2, process_id="engineOnly", job_type="engine-task")
     deps = [(a, KEY_A, 1), (b, KEY_B, 1)]
     ref, gpu = single(deps, deps[:1])
+    notifiers(ref, gpu)  # publishWork without a stream: JobStreamer.notifyWorkAvailable
     write(ref, gpu, *[Client.create("linear") for _ in range(4)])  # polled jobs, no stream yet
+    notified_equal(ref, gpu)
+    assert gpu.streamer.notifications == {"benchmark-task": 4}
     streams(ref, gpu, "benchmark-task", "pusher", 20000)
     streams(ref, gpu, "engine-task", "pusher", 20000, fetch=("n",))
     write(ref, gpu, *([Client.create("linear", (("n", i),) if i % 3 else ()) for i in range(12)] +
@@ -85,6 +104,8 @@ def test_job_push_in_the_processing_loop():
         write(ref, gpu, *[Client.complete_job(k) for k in live])
     check(ref, gpu)
     pushed_equal(ref, gpu)
+    notified_equal(ref, gpu)  # creations, time-outs and failures with retries after the stream closed
+    assert gpu.streamer.notifications["benchmark-task"] > 4
 
 
 def test_push_survives_a_restart():
@@ -100,3 +121,34 @@ def test_push_survives_a_restart():
     fresh.import_state_db(part.state_db())
     assert fresh.state() == part.state()
     assert any("|ACTIVATED" in r for r in part.state() if r.startswith("JOB_STATES|"))
+
+
+def test_push_reads_the_variables_at_its_creation():
+    """publishWork collects the pushed job's variables when JOB:CREATED is written (BpmnJobActivationBehavior
+    .java:83): a later command of the same instance -- here a parallel branch's completion with a document,
+    read in the same log window -- must not leak into the pushed job.  The adapter keeps such commands out
+    of the pushing window (adapter.py _push_fenced)."""
+    xml = (bpmn.createExecutableProcess("fork").startEvent("start").parallelGateway("fork")
+           .serviceTask("a", "a").serviceTask("p", "pushed").sequenceFlowId("j1").parallelGateway("join")
+           .moveToNode("fork").serviceTask("b", "b").sequenceFlowId("j2").connectTo("join")
+           .moveToNode("join").endEvent("end").done())
+    ref, gpu = single([(xml, KEY_A, 1)], [(xml, KEY_A, 1)])
+    streams(ref, gpu, "pushed", "pusher", 20000)
+    write(ref, gpu, *[Client.create("fork", (("n", i),)) for i in range(6)])
+    jobs = open_jobs(ref.parts[0].log)
+    by_type = {}
+    for k, r in sorted(jobs.items()):
+        by_type.setdefault(r.value["type"], []).append((r.value["processInstanceKey"], k))
+    a, b = dict(by_type["a"]), dict(by_type["b"])
+    # one window: task a's completion (task p's job created and pushed), then b's with a document
+    recs = []
+    for pik in sorted(a):
+        recs += [Client.complete_job(a[pik]), Client.complete_job(b[pik], (("n", 1000 + pik % 7),))]
+    write(ref, gpu, *recs)
+    pushed_equal(ref, gpu)
+    assert len(gpu.job_stream.activated_jobs) == 6
+    assert all(dict(j["variables"])["n"] < 1000 for _, j in gpu.job_stream.activated_jobs)
+    assert gpu.parts[0].adapter.counts["windows"] >= 6
+    live = sorted(open_jobs(ref.parts[0].log))
+    write(ref, gpu, *[Client.complete_job(k) for k in live])
+    check(ref, gpu)

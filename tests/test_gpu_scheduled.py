@@ -362,3 +362,42 @@ def test_sub_process_boundary_timers_in_the_processing_loop():
     log = gpu.parts[0].log
     assert any(r.value_type == abi.VT_PROCESS_INSTANCE_BATCH for r in log.entries)
     assert gpu.parts[0].adapter.counts["fallbacks"] == 0, gpu.parts[0].adapter.fallback_reasons
+
+
+def test_truncated_device_scans_keep_the_checkers_order():
+    """zbhip_due_timers / zbhip_timed_out_jobs return at most a cap of rows; a truncated device list may
+    leave out a row ordered before engine entries past its last returned row, so the merged views stop
+    there (DeviceTimerInstanceState / DeviceJobState) and the checkers' next runs take the rest.  With the
+    cap forced to 4, the TIMER:TRIGGER and JOB:TIME_OUT commands reach the log in the engine-only loop's
+    order (TIMER_DUE_DATES [dueDate, elementInstanceKey, timerKey], JOB_DEADLINES [deadline, jobKey]),
+    over several checker runs instead of one, and every instance ends in the same state."""
+    deps = [(timer_process("PT10S", pid="catch"), KEY_A, 1), (timer_process("PT10S", pid="engineTimer"), KEY_D, 1),
+            (bpmn.linear_process(1), KEY_B, 1), (bpmn.linear_process(1, process_id="engineOnly", job_type="engine-task"),
+                                                 KEY_C, 1)]
+    ref, gpu = single(deps, deps[:1] + deps[2:3])
+    gpu.parts[0].adapter.scheduled_cap = 4
+    # timers with one dueDate, device and engine instances interleaved in key order
+    write(ref, gpu, *[Client.create("catch" if k % 3 else "engineTimer") for k in range(18)])
+    write(ref, gpu, *[Client.create("linear" if k % 3 else "engineOnly") for k in range(15)])
+    clock = ref.clock
+    write(ref, gpu, Client.activate_jobs("benchmark-task", worker="w", timeout=5000, max_jobs=20, timestamp=clock.now),
+          Client.activate_jobs("engine-task", worker="e", timeout=5000, max_jobs=20, timestamp=clock.now))
+    for cl in (ref, gpu):
+        cl.increase_time(15000)
+        for _ in range(12):  # the checkers' later runs (100 ms / 30 s apart)
+            cl.increase_time(30000)
+
+    def order(cl, vt, it):
+        return [r.key for r in checker_commands(cl.parts[0].log, vt, it)]
+    triggers = order(gpu, abi.VT_TIMER, abi.TIMER_TRIGGER)
+    assert len(triggers) == 18 and triggers == order(ref, abi.VT_TIMER, abi.TIMER_TRIGGER)
+    time_outs = order(gpu, abi.VT_JOB, abi.JOB_TIME_OUT)
+    assert len(time_outs) == 15 and time_outs == order(ref, abi.VT_JOB, abi.JOB_TIME_OUT)
+    # the truncated scans spread them over several checker runs (batches without a source position)
+    runs = {r.position - i for i, r in enumerate(checker_commands(gpu.parts[0].log, abi.VT_TIMER, abi.TIMER_TRIGGER))}
+    assert len(runs) > 1
+    for cl in (ref, gpu):
+        live = sorted(open_jobs(cl.parts[0].log))
+        Client(cl.parts[0].log).write(*[Client.complete_job(k) for k in live])
+        cl.settle()
+    assert gpu.parts[0].state() == ref.parts[0].state()

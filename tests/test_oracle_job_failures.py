@@ -116,3 +116,18 @@ def test_state_rows_survive_the_zb_db_encoding():
     fresh.deploy(bpmn.linear_process(1, process_id="process", job_type="test"), KEY, 1)
     fresh.upsert([r for r in rows if not r.startswith("KEY|")])
     assert [r for r in fresh.state() if not r.startswith("KEY|")] == [r for r in rows if not r.startswith("KEY|")]
+
+
+def test_error_message_limited_in_utf16_code_units():
+    # JobFailProcessor.java:42 / failJob: StringUtil.limitString(errorMessage, 10000) (util/.../StringUtil
+    # .java:50-56) counts Java chars -- UTF-16 code units, not UTF-8 bytes: a two-byte character is one
+    # unit, a character beyond the BMP two; a cut between a surrogate pair leaves a lone high surrogate,
+    # which the UTF-8 encoding of the record writes as '?'
+    cases = [("é" * 10001, "é" * 10000 + "..."), ("é" * 10000, "é" * 10000),
+             ("\U0001D11E" * 5001, "\U0001D11E" * 5000 + "..."), ("a" + "\U0001D11E" * 5000, "a" + "\U0001D11E" * 4999 + "?...")]
+    log, eng, sp = loop()
+    run(log, sp, *[Client.create("process") for _ in cases])
+    jobs = sorted(open_jobs(log))
+    for job_key, (msg, want) in zip(jobs, cases):
+        failed = job_events(run(log, sp, Client.fail_job(job_key, 1, msg)), abi.JOB_FAILED)[0]
+        assert failed.value["errorMessage"] == want

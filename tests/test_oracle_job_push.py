@@ -114,3 +114,54 @@ def test_no_push_once_the_stream_is_gone():
     eng.set_job_stream("pushed", "test", TIMEOUT, on=False)
     entries = run(log, sp, Client.create("process"))
     assert order(entries) == [(abi.VT_JOB, abi.JOB_CREATED)]
+
+
+# ---- notifyWorkAvailable: ActivatableJobsNotificationTests.java (engine/src/test/.../processing/job/) -------
+def notifying_loop(clock=None, job_type="task"):
+    from psm import RecordingJobStreamer
+    log = Log()
+    eng = OracleEngine(clock=clock or 0)
+    eng.deploy(bpmn.linear_process(1, process_id="process", job_type=job_type), KEY, 1)
+    eng.job_streamer = RecordingJobStreamer()
+    return log, eng, StreamProcessor(log, [eng])
+
+
+def test_notify_when_job_created():
+    # shouldNotifyWhenJobCreated (:67-74): three jobs, three notifications of the type
+    log, eng, sp = notifying_loop()
+    run(log, sp, *[Client.create("process") for _ in range(3)])
+    assert eng.job_streamer.notifications == {"task": 3}
+
+
+def test_notify_when_jobs_available_again_and_after_time_out():
+    # shouldNotifyWhenJobsAvailableAgain (:76-87): create, activate, create -> 2;
+    # shouldNotifyWhenJobsAvailableAfterTimeOut (:101-113): the time-out makes it activatable -> 2
+    clock = Clock(0)
+    log, eng, sp = notifying_loop(clock)
+    run(log, sp, Client.create("process"))
+    job_key = run(log, sp, Client.activate_jobs("task", timeout=10))[-1].value["jobKeys"][0]
+    run(log, sp, Client.create("process"))
+    assert eng.job_streamer.notifications == {"task": 2}
+    clock.now += 100
+    run(log, sp, _time_out(job_key))
+    assert eng.job_streamer.notifications == {"task": 3}
+
+
+def test_notify_when_jobs_fail_with_retries_available():
+    # shouldNotifyWhenJobsFailWithRetryAvailable (:129-141): FAIL with retries -> 2; none left: no notification
+    log, eng, sp = notifying_loop()
+    run(log, sp, Client.create("process"), Client.create("process"))
+    a, b = [r.key for r in log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_CREATED]
+    run(log, sp, Client.fail_job(a, 10))
+    assert eng.job_streamer.notifications == {"task": 3}
+    run(log, sp, Client.fail_job(b, 0))
+    assert eng.job_streamer.notifications == {"task": 3}
+
+
+def test_notify_per_job_type_and_not_with_a_stream():
+    # shouldNotifyForMultipleJobTypes (:164-175); a type with a stream is pushed instead (publishWork)
+    log, eng, sp = notifying_loop(job_type="first")
+    eng.deploy(bpmn.linear_process(1, process_id="second", job_type="second"), KEY + 1, 1)
+    eng.set_job_stream("second", "w", TIMEOUT)
+    run(log, sp, Client.create("process"), Client.create("second"))
+    assert eng.job_streamer.notifications == {"first": 1}

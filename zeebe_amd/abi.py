@@ -9,7 +9,7 @@ import numpy as np
 
 # ---- protocol enums (protocol/src/main/resources/protocol.xml:23-72) ----
 RT_EVENT, RT_COMMAND, RT_REJECTION = 0, 1, 2
-VT_JOB_BATCH = 1
+VT_JOB_BATCH = 14  # ValueType.JOB_BATCH (protocol.xml:31)
 JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED = 0, 1
 VT_JOB = 0
 VT_PROCESS_INSTANCE = 5

@@ -327,9 +327,15 @@ class DeviceTimerInstanceState:
         if not self.adapter.scheduled_ready():
             return now  # mid-window: look again after the timer resolution
         dev, dev_next = self.adapter.due_timers(now)
-        both = sorted([(v["dueDate"], v["elementInstanceKey"], k, v) for k, v in dev] + list(self.engine.due(now)),
-                      key=lambda t: t[:3])
-        for due, _, key, value in both:
+        dev_rows = [(v["dueDate"], v["elementInstanceKey"], k, v) for k, v in dev]
+        both = sorted(dev_rows + list(self.engine.due(now)), key=lambda t: t[:3])
+        # a truncated device scan (due rows left out): the first row left out may precede engine timers
+        # ordered after the last row returned, so the merge stops there; the checker runs again at the
+        # date returned (processTimersWithDueDateBefore stops at any timer its visitor refuses, :87-116)
+        bound = dev_rows[-1][:3] if dev_rows and 0 <= dev_next <= now else None
+        for due, eik, key, value in both:
+            if bound is not None and (due, eik, key) > bound:
+                return min(due, dev_next)
             if not visitor(key, value):
                 return due
         later = [d for d in (dev_next, self.engine.next_after(now)) if d >= 0]
@@ -346,8 +352,12 @@ class DeviceJobState:
         self.adapter, self.engine = adapter, engine
 
     def for_each_timed_out_entry(self, now, callback):
-        dev = self.adapter.timed_out_jobs(now) if self.adapter.scheduled_ready() else []
-        for _, key, value in sorted(dev + list(self.engine.timed_out(now)), key=lambda t: t[:2]):
+        dev, dev_next = self.adapter.timed_out_jobs(now, with_next=True) if self.adapter.scheduled_ready() else ([], -1)
+        # a truncated device list: engine entries past its last row wait for the trigger's next run
+        bound = dev[-1][:2] if dev and dev_next >= 0 else None
+        for deadline, key, value in sorted(dev + list(self.engine.timed_out(now)), key=lambda t: t[:2]):
+            if bound is not None and (deadline, key) > bound:
+                return
             if not callback(key, value):
                 return
 
@@ -503,6 +513,7 @@ class GpuBatchProcessor:
         self.window = Window()
         self._window_done = True       # every command of the current window was emitted
         self.due_date_checker = None   # DueDateTimerChecker.scheduleTimer of the platform (side effects)
+        self.scheduled_cap = 1 << 16   # rows per device scan of the scheduled tasks (the rest: the next run)
         self.pending_pms = {}          # (elementInstanceKey, messageName) -> [sent time, record, opening]
         self.pending_ms = {}           # (elementInstanceKey, messageName) -> [sent time, record]
         self.moved_pending = []        # pending entries of handed-off instances, for the engine's state
@@ -514,6 +525,7 @@ class GpuBatchProcessor:
         self.doc_total = 0             # document entries submitted so far (zbhip doc indices)
         self.values = None
         self.stream_sinks = {}  # job type -> (fetchVariables, push): the job streams' push side effects
+        self.job_streamer = None  # JobStreamer: notifyWorkAvailable(type) of publishWork without a stream
         # what went where (tests read these)
         self.fallback_reasons = []
         self.counts = {"windows": 0, "device_commands": 0, "continuations": 0, "fallbacks": 0, "activations": 0,
@@ -768,6 +780,8 @@ class GpuBatchProcessor:
                 continue  # events and processed follow-ups of earlier batches between the commands
             if not self._hot(rec, claimed):
                 break  # the engine's: the window ends before it (log order is kept)
+            if self._push_fenced(rec, claimed):
+                break  # the next window takes it (see _push_fenced)
             vt = rec.value_type
             if vt == abi.VT_PROCESS_INSTANCE_CREATION:
                 v = rec.value
@@ -820,6 +834,26 @@ class GpuBatchProcessor:
         # the records are drained command by command as the platform reaches them
         # (zbhip_drain_command): a fallback command's CPU-engine keys come before the later ones
 
+    def _push_fenced(self, rec, claimed):
+        """A job stream's push gathers the job's variables when the push record is emitted
+        (zbhip_job_variables), after the whole window ran; the reference gathers them in publishWork, at
+        JOB:CREATED (BpmnJobActivationBehavior.java:83).  While a stream pushes, a window therefore holds
+        at most one command per process instance: no later command of the window changes the variables a
+        push reads, or ends its job.  (CREATEs take fresh slots; message-partition commands address
+        correlation slots, not instances.)"""
+        if not self.stream_sinks:
+            return False
+        vt = rec.value_type
+        if vt in (abi.VT_JOB, abi.VT_TIMER):
+            inst = self._resolve(rec.key)[0]
+        elif vt in (abi.VT_PROCESS_INSTANCE, abi.VT_PROCESS_INSTANCE_BATCH):
+            inst = self.continuations[claimed][1]
+        elif vt == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION:
+            inst = self._message_command(rec)[0]["instance"]
+        else:
+            return False
+        return inst in self.window.instances
+
     def _free_ended(self):
         for s in list(self.ended):
             if self.part.pending_continuations(s) == 0 and s not in self.closing:
@@ -843,6 +877,7 @@ class GpuBatchProcessor:
         win = self.window
         admitted = 0
         pushes = []
+        created = {}  # jobs created in the batch -> type (publishWork: pushed, or notified)
         for r in self.part.drain_command(i):
             rt, vt, it = int(r["record_type"]), int(r["value_type"]), int(r["intent"])
             if rt == abi.RT_REJECTION and int(r["ordinal"]) == 0 and vt == record.value_type and it == record.intent:
@@ -854,6 +889,9 @@ class GpuBatchProcessor:
             out.append_record(int(r["key"]), rt, vt, it, int(r["rejection_type"]), reason, value)
             if vt == VT_JOB_BATCH and rt == abi.RT_EVENT:
                 pushes.append((int(r["aux"]), value))
+                created.pop(int(r["aux"]), None)
+            elif vt == abi.VT_JOB and rt == abi.RT_EVENT and it == abi.JOB_CREATED:
+                created[int(r["key"])] = value["type"]
             if self.correlation_keys > 0:
                 self._track_pending(rt, vt, it, value)
             if rt == abi.RT_EVENT and vt == abi.VT_TIMER and it == abi.TIMER_CREATED and self.due_date_checker:
@@ -891,6 +929,7 @@ class GpuBatchProcessor:
         self.followups = admitted
         if pushes:
             self._push(out, pushes)
+        self._notify(out, created.values())
         if self.correlation_keys > 0:
             self._send(i, out)
 
@@ -904,14 +943,16 @@ class GpuBatchProcessor:
 
     def due_timers(self, now):
         """TimerInstanceState.processTimersWithDueDateBefore over the device: [(timer key, TimerRecord)]
-        in TIMER_DUE_DATES order, and the first later dueDate (-1 none)."""
-        rows, nxt = self.part.due_timers(now)
+        in TIMER_DUE_DATES order (at most `scheduled_cap`), and the first dueDate not returned (-1 none)."""
+        rows, nxt = self.part.due_timers(now, cap=self.scheduled_cap)
         return [(int(r["key"]), self.values.value(r)) for r in rows], nxt
 
-    def timed_out_jobs(self, now):
-        """JobState.forEachTimedOutEntry over the device's activated jobs: [(job key, JobRecord)] in
-        JOB_DEADLINES order (with the deadline: the merge key)."""
-        return [(int(r["message_key"]), int(r["key"]), self.values.value(r)) for r in self.part.timed_out_jobs(now)]
+    def timed_out_jobs(self, now, with_next=False):
+        """JobState.forEachTimedOutEntry over the device's activated jobs: [(deadline, job key, JobRecord)] in
+        JOB_DEADLINES order (at most `scheduled_cap`; with_next: and the deadline of the first one left out)."""
+        rows, nxt = self.part.timed_out_jobs(now, cap=self.scheduled_cap, with_next=True)
+        out = [(int(r["message_key"]), int(r["key"]), self.values.value(r)) for r in rows]
+        return (out, nxt) if with_next else out
 
     def _track_pending(self, rt, vt, it, value):
         """The transient pending-subscription states the appliers of the device's records keep in the
@@ -1032,6 +1073,8 @@ class GpuBatchProcessor:
             incident |= vt == abi.VT_INCIDENT
             if vt == VT_JOB_BATCH:
                 self._push(out, [(int(r["aux"]), value)])
+            elif vt == abi.VT_JOB and it == abi.JOB_FAILED and value["retries"] > 0 and len(recs) == 1:
+                self._notify(out, [value["type"]])  # retryImmediately -> publishWork, no stream
         self.key_generator.set_key_if_higher(self.part.current_key())
         if incident:
             # the instance waits for the incident's resolution (JOB:UPDATE_RETRIES, INCIDENT:RESOLVE): the
@@ -1049,8 +1092,11 @@ class GpuBatchProcessor:
             out.append_record(record.key, abi.RT_REJECTION, abi.VT_JOB, abi.JOB_TIME_OUT, int(r["rejection_type"]),
                               self.part.reason(r), dict(record.value))
             return out.build()
-        out.append_record(record.key, abi.RT_EVENT, abi.VT_JOB, abi.JOB_TIMED_OUT, abi.REJ_NONE, "", self.values.value(r))
+        value = self.values.value(r)
+        out.append_record(record.key, abi.RT_EVENT, abi.VT_JOB, abi.JOB_TIMED_OUT, abi.REJ_NONE, "", value)
         # publishWork: a job stream of the type -> the push (JOB_BATCH:ACTIVATED); none -> a notification
+        if len(recs) == 1:
+            self._notify(out, [value["type"]])
         for p in recs[1:]:
             value = self.values.value(p)
             out.append_record(int(p["key"]), abi.RT_EVENT, VT_JOB_BATCH, JOB_BATCH_ACTIVATED, abi.REJ_NONE, "", value)
@@ -1070,6 +1116,13 @@ class GpuBatchProcessor:
         else:
             self.values.streams.pop(job_type, None)
             self.stream_sinks.pop(job_type, None)
+
+    def _notify(self, out, types):
+        """publishWork without a stream: notifyJobAvailable's side effect (BpmnJobActivationBehavior.java
+        :97-111), JobStreamer.notifyWorkAvailable(type) after the commit -- long-polling workers wake up."""
+        types = list(types)
+        if types and self.job_streamer is not None:
+            out.append_post_commit_task(lambda: [self.job_streamer.notify_work_available(t) for t in types] and True)
 
     def _push(self, out, pushes):
         push_side_effects(out, pushes, self.stream_sinks, self.part.job_variables, self.values, self.part.name,

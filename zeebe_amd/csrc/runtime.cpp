@@ -5297,9 +5297,11 @@ static void stored_job_record(const zbhip_handle::Activation& a, int64_t key, ui
   }
 }
 
-extern "C" int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out) {
+extern "C" int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* out, size_t cap, size_t* n_out,
+                                    int64_t* next_deadline) {
   if (!h || !n_out || (cap && !out)) return ZBHIP_EINVAL;
   *n_out = 0;
+  if (next_deadline) *next_deadline = -1;
   if (!h->relabel_ok) return ZBHIP_ESTATE;
   if (int rc = finalize(h)) return rc;
   // DbJobState.forEachTimedOutEntry (:286-298): JOB_DEADLINES [deadline, jobKey] while deadline < now
@@ -5311,6 +5313,8 @@ extern "C" int zbhip_timed_out_jobs(zbhip_handle* h, int64_t now, zbhip_record* 
   for (size_t i = 0; i < n; ++i)
     stored_job_record(h->activated.at(due[i].second), due[i].second, ZBHIP_RT_COMMAND, ZBHIP_JOB_TIME_OUT, out[i]);
   *n_out = n;
+  // the first timed-out deadline not returned (a merge with the engine's JOB_DEADLINES stops before it)
+  if (next_deadline && n < due.size()) *next_deadline = due[n].first;
   return ZBHIP_OK;
 }
 
@@ -5399,6 +5403,22 @@ extern "C" int zbhip_time_out_job(zbhip_handle* h, int64_t job_key, int64_t now,
   return ZBHIP_OK;
 }
 
+// StringUtil.limitString(message, maxLength) (util/.../StringUtil.java:50-56) on the UTF-8 bytes of a Java
+// String: the length counts UTF-16 code units (a character beyond the BMP is two); a cut inside a
+// surrogate pair keeps the lone high surrogate, which String.getBytes(UTF_8) writes as '?'
+static std::string limit_java_string(const std::string& s, size_t max_units) {
+  size_t units = 0, i = 0;
+  while (i < s.size()) {
+    const unsigned char c = (unsigned char)s[i];
+    const size_t len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : 4;
+    const size_t u = len == 4 ? 2 : 1;
+    if (units + u > max_units) return s.substr(0, i) + (units < max_units ? "?" : "") + "...";
+    units += u;
+    i += len;
+  }
+  return s;
+}
+
 extern "C" int zbhip_fail_job(zbhip_handle* h, const zbhip_job_fail* cmd, zbhip_record* out, size_t cap, size_t* n_out) {
   if (!h || !cmd || !n_out || (cap && !out) || (cmd->error_message_len && !cmd->error_message)) return ZBHIP_EINVAL;
   *n_out = 0;
@@ -5441,7 +5461,7 @@ extern "C" int zbhip_fail_job(zbhip_handle* h, const zbhip_job_fail* cmd, zbhip_
   // the device subset: no variables (setFailedVariables), no retry back-off (JobBackoffChecker)
   if (cmd->n_variables || (cmd->retries > 0 && cmd->retry_backoff > 0)) return ZBHIP_EUNSUPP;
   std::string msg(cmd->error_message ? cmd->error_message : "", cmd->error_message_len);
-  if (msg.size() > 10000) msg = msg.substr(0, 10000) + "...";  // StringUtil.limitString (ASCII)
+  msg = limit_java_string(msg, 10000);
   const int64_t eid = msg.empty() ? (int64_t)ZBHIP_NO_STRING : zbhip_intern_string(h, msg.data(), msg.size());
   if (eid < 0) return (int)eid;
   const uint32_t elem = R.slots[slot].x & 0xFFFF;

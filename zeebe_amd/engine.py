@@ -453,13 +453,15 @@ class Partition:
               "zbhip_due_timers")
         return out[: n.value], nxt.value
 
-    def timed_out_jobs(self, now, cap=1 << 16):
+    def timed_out_jobs(self, now, cap=1 << 16, with_next=False):
         """JobTimeoutTrigger over the device's activated jobs (zbhip_timed_out_jobs): the JOB:TIME_OUT
-        commands (RECORD_DTYPE rows, the stored job) in JOB_DEADLINES order."""
+        commands (RECORD_DTYPE rows, the stored job) in JOB_DEADLINES order (with_next: and the deadline of
+        the first timed-out job not returned, -1 none)."""
         out = np.zeros(max(cap, 1), dtype=abi.RECORD_DTYPE)
-        n = C.c_size_t()
-        check(self.L.zbhip_timed_out_jobs(self.h, int(now), out.ctypes.data, cap, C.byref(n)), "zbhip_timed_out_jobs")
-        return out[: n.value]
+        n, nxt = C.c_size_t(), C.c_int64()
+        check(self.L.zbhip_timed_out_jobs(self.h, int(now), out.ctypes.data, cap, C.byref(n), C.byref(nxt)),
+              "zbhip_timed_out_jobs")
+        return (out[: n.value], nxt.value) if with_next else out[: n.value]
 
     def time_out_job(self, job_key, now):
         """JOB:TIME_OUT of a device job (zbhip_time_out_job): JOB:TIMED_OUT (+ its push) or the rejection,

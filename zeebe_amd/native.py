@@ -120,7 +120,7 @@ def load():
     L.zbhip_activatable_jobs.argtypes = [vp, C.c_char_p, sz, vp, sz, C.POINTER(sz)]
     L.zbhip_job_batch_rejection_reason.argtypes = [C.POINTER(abi.JobActivation), C.POINTER(abi.JobBatch), C.c_char_p, sz]
     L.zbhip_due_timers.argtypes = [vp, i64, vp, sz, C.POINTER(sz), C.POINTER(i64)]
-    L.zbhip_timed_out_jobs.argtypes = [vp, i64, vp, sz, C.POINTER(sz)]
+    L.zbhip_timed_out_jobs.argtypes = [vp, i64, vp, sz, C.POINTER(sz), C.POINTER(i64)]
     L.zbhip_time_out_job.argtypes = [vp, i64, i64, vp, sz, C.POINTER(sz)]
     L.zbhip_set_job_stream.argtypes = [vp, C.c_char_p, sz, C.c_char_p, sz, i64, C.c_int]
     L.zbhip_fail_job.argtypes = [vp, C.POINTER(abi.JobFail), vp, sz, C.POINTER(sz)]
