@@ -75,8 +75,11 @@ import io.camunda.zeebe.stream.api.StreamProcessorLifecycleAware;
 import io.camunda.zeebe.stream.api.records.TypedRecord;
 import io.camunda.zeebe.stream.impl.records.UnwrittenRecord;
 import io.camunda.zeebe.stream.impl.state.DbKeyGenerator;
+import io.camunda.zeebe.protocol.record.value.TenantOwned;
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
+import java.nio.charset.StandardCharsets;
+import org.agrona.concurrent.UnsafeBuffer;
 import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.BitSet;
@@ -164,6 +167,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   private boolean windowDone = true; // every command of the current window was emitted
   private io.camunda.zeebe.engine.processing.timer.DueDateTimerChecker dueDateTimerChecker;
   private JobStreams jobStreams = new JobStreams(null);
+  private io.camunda.zeebe.engine.state.immutable.JobState engineJobState; // the engine's (jobState(...))
 
   public GpuBatchProcessor(
       final Engine engine,
@@ -272,7 +276,11 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     followUps = 0;
     if (record.getValueType() == ValueType.JOB_BATCH && record.getIntent() == JobBatchIntent.ACTIVATE) {
       final JobBatchRecord batch = (JobBatchRecord) record.getValue();
-      return engineJobTypes.contains(batch.getType()) ? engine.process(record, out) : activateJobs(record, batch, out);
+      if (!engineJobTypes.contains(batch.getType())) {
+        return activateJobs(record, batch, out);
+      }
+      return deviceProcessJobTypes().contains(batch.getType()) ? activateJobsMerged(record, batch, out)
+          : engine.process(record, out);
     }
     if (record.getValueType() == ValueType.JOB && record.getIntent() == JobIntent.TIME_OUT
         && ZbHip.resolveKey(handle, record.getKey()) >= 0) {
@@ -580,9 +588,13 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     return new DeviceScheduledState.Timers(this, engineTimers);
   }
 
-  /** ... to JobTimeoutTrigger instead of the engine's JobState. */
+  /**
+   * ... to JobTimeoutTrigger instead of the engine's JobState (kept: merged activations read the engine's
+   * JOB_ACTIVATABLE through it).
+   */
   public io.camunda.zeebe.engine.state.immutable.JobState jobState(
       final io.camunda.zeebe.engine.state.immutable.JobState engineJobs) {
+    engineJobState = engineJobs;
     return new DeviceScheduledState.Jobs(this, engineJobs);
   }
 
@@ -736,6 +748,13 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
 
   /** The job types of device processes (the streams the device must know of). */
   private Set<String> deviceJobTypes() {
+    final Set<String> types = deviceProcessJobTypes();
+    types.removeAll(engineJobTypes);
+    return types;
+  }
+
+  /** Every job type a device process declares (some may be held by the engine too). */
+  private Set<String> deviceProcessJobTypes() {
     final Set<String> types = new HashSet<>();
     for (final ZbHip.Deployed d : byIndex) {
       for (final String t : d.jobTypes()) {
@@ -744,7 +763,6 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
         }
       }
     }
-    types.removeAll(engineJobTypes);
     return types;
   }
 
@@ -760,6 +778,167 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       keyGenerator.setKeyIfHigher(activation.key());
     }
     return out.build();
+  }
+
+  /**
+   * JOB_BATCH:ACTIVATE of a job type both the engine and the device hold jobs of (handed-off instances,
+   * engine-only processes of a device type): JobBatchCollector.collectJobs (:67-123) walks JOB_ACTIVATABLE
+   * [type, jobKey] in key order over both.  The first maxJobsToActivate keys of the two lists (the engine's
+   * JobState.forEachActivatableJobs, zbhip_activatable_jobs) split into each side's share; the engine
+   * activates its share first (its nextKey is the batch key: the engine's record and response are caught
+   * in a scratch builder), the device its own with the same key (its key counter is one behind), and the
+   * one JOB_BATCH:ACTIVATED record -- and the engine's response -- list both in key order
+   * (adapter.py _activate_jobs_merged).
+   */
+  private ProcessingResult activateJobsMerged(
+      final TypedRecord record, final JobBatchRecord batch, final ProcessingResultBuilder out) {
+    final int max = batch.getMaxJobsToActivate();
+    if (max < 1 || batch.getTimeout() < 1 || batch.getType().isEmpty() || engineJobState == null) {
+      return engine.process(record, out); // the rejection (or no view of the engine's jobs)
+    }
+    ZbHip.setKeyIfHigher(handle, keyGenerator.getCurrentKey());
+    final long[] device = ZbHip.activatableJobs(handle, batch.getType().getBytes(StandardCharsets.UTF_8), max);
+    if (device.length == 0) {
+      return engine.process(record, out);
+    }
+    final List<Long> picked = new ArrayList<>();
+    engineJobState.forEachActivatableJobs(batch.getTypeBuffer(), List.of(TenantOwned.DEFAULT_TENANT_IDENTIFIER),
+        (key, job) -> {
+          picked.add(key);
+          return picked.size() < max;
+        });
+    for (final long k : device) {
+      picked.add(k);
+    }
+    picked.sort(Long::compare);
+    final Set<Long> mine = new HashSet<>();
+    for (final long k : device) {
+      mine.add(k);
+    }
+    final List<Long> first = picked.subList(0, Math.min(max, picked.size()));
+    final int onDevice = (int) first.stream().filter(mine::contains).count();
+    if (onDevice == first.size()) {
+      return activateJobs(record, batch, out);
+    }
+    // the command as written (the engine's processor adds its jobs to the command's value)
+    final UnsafeBuffer asWritten = new UnsafeBuffer(new byte[batch.getLength()]);
+    batch.write(asWritten, 0);
+    final ScratchResult share = new ScratchResult();
+    batch.setMaxJobsToActivate(first.size() - onDevice);
+    engine.process(record, share);
+    final JobBatchRecord engineBatch = (JobBatchRecord) share.value;
+    final java.util.TreeMap<Long, JobRecord> jobs = new java.util.TreeMap<>();
+    final Iterator<JobRecord> engineJobs = engineBatch.jobs().iterator();
+    for (final var k : engineBatch.jobKeys()) {
+      final JobRecord copy = new JobRecord();
+      copy.wrap(engineJobs.next());
+      jobs.put(k.getValue(), copy);
+    }
+    final boolean engineTruncated = engineBatch.getTruncated();
+    // the device's share, with the batch key the engine generated
+    final JobBatchRecord deviceCmd = new JobBatchRecord();
+    deviceCmd.wrap(asWritten);
+    deviceCmd.setMaxJobsToActivate(onDevice);
+    final JobActivation activation = JobActivation.of(arena, deviceCmd, record.getTimestamp(), this);
+    ZbHip.activateJobs(handle, activation.command(), activation.jobs(), activation.capacity(), activation.result());
+    if (activation.key() != share.key) {
+      throw new IllegalStateException("merged activation: batch keys " + share.key + " / " + activation.key());
+    }
+    jobs.putAll(activation.activated(this));
+    final JobBatchRecord merged = new JobBatchRecord();
+    merged.wrap(asWritten);
+    for (final var e : jobs.entrySet()) {
+      merged.jobKeys().add().setValue(e.getKey());
+      merged.jobs().add().wrap(e.getValue());
+    }
+    merged.setTruncated(engineTruncated || activation.truncated());
+    keyGenerator.setKeyIfHigher(share.key);
+    out.appendRecord(share.key, merged, share.metadata);
+    if (share.response != null) {
+      share.response.replay(out, merged);
+    }
+    for (final var task : share.postCommit) {
+      out.appendPostCommitTask(task);
+    }
+    return out.build();
+  }
+
+  /** The engine's share of a merged activation: its one record, response and side effects, held back. */
+  private static final class ScratchResult implements ProcessingResultBuilder, ProcessingResult {
+    long key = -1;
+    io.camunda.zeebe.protocol.record.RecordValue value;
+    final RecordMetadata metadata = new RecordMetadata();
+    Response response;
+    final List<io.camunda.zeebe.stream.api.PostCommitTask> postCommit = new ArrayList<>();
+
+    record Response(RecordType type, long key, io.camunda.zeebe.protocol.record.intent.Intent intent,
+        ValueType valueType, io.camunda.zeebe.protocol.record.RejectionType rejectionType, String reason,
+        long requestId, int requestStreamId) {
+      void replay(final ProcessingResultBuilder out, final io.camunda.zeebe.msgpack.UnpackedObject value) {
+        out.withResponse(type, key, intent, value, valueType, rejectionType, reason, requestId, requestStreamId);
+      }
+    }
+
+    @Override
+    public io.camunda.zeebe.util.Either<RuntimeException, ProcessingResultBuilder> appendRecordReturnEither(
+        final long key, final io.camunda.zeebe.protocol.record.RecordValue value, final RecordMetadata metadata) {
+      this.key = key;
+      this.value = value;
+      this.metadata.wrap(metadata);
+      return io.camunda.zeebe.util.Either.right(this);
+    }
+
+    @Override
+    public ProcessingResultBuilder withResponse(final RecordType type, final long key,
+        final io.camunda.zeebe.protocol.record.intent.Intent intent, final io.camunda.zeebe.msgpack.UnpackedObject value,
+        final ValueType valueType, final io.camunda.zeebe.protocol.record.RejectionType rejectionType,
+        final String rejectionReason, final long requestId, final int requestStreamId) {
+      response = new Response(type, key, intent, valueType, rejectionType, rejectionReason, requestId, requestStreamId);
+      return this;
+    }
+
+    @Override
+    public ProcessingResultBuilder appendPostCommitTask(final io.camunda.zeebe.stream.api.PostCommitTask task) {
+      postCommit.add(task);
+      return this;
+    }
+
+    @Override
+    public ProcessingResultBuilder resetPostCommitTasks() {
+      postCommit.clear();
+      return this;
+    }
+
+    @Override
+    public ProcessingResult build() {
+      return this;
+    }
+
+    @Override
+    public boolean canWriteEventOfLength(final int eventLength) {
+      return true;
+    }
+
+    // ProcessingResult (ProcessingResult.java:17-51): never handed to the platform
+    @Override
+    public io.camunda.zeebe.stream.api.records.ImmutableRecordBatch getRecordBatch() {
+      throw new UnsupportedOperationException();
+    }
+
+    @Override
+    public java.util.Optional<io.camunda.zeebe.stream.api.ProcessingResponse> getProcessingResponse() {
+      throw new UnsupportedOperationException();
+    }
+
+    @Override
+    public boolean executePostCommitTasks() {
+      throw new UnsupportedOperationException();
+    }
+
+    @Override
+    public boolean isEmpty() {
+      return key < 0;
+    }
   }
 
   public void close() {

@@ -72,13 +72,28 @@ record JobActivation(MemorySegment command, MemorySegment jobs, long capacity, M
       out.appendRecord(command.getKey(), batch, meta);
       return;
     }
+    for (final var e : activated(p).entrySet()) {
+      batch.jobKeys().add().setValue(e.getKey());
+      batch.jobs().add().wrap(e.getValue());
+    }
+    batch.setTruncated(truncated());
+    meta.recordType(RecordType.EVENT).intent(JobBatchIntent.ACTIVATED);
+    out.appendRecord(key(), batch, meta);
+  }
+
+  boolean truncated() {
+    return result.get(JAVA_BYTE, 14) != 0;
+  }
+
+  /** The activated device jobs in key order: job key -> JobRecord (JobBatchCollector's jobs). */
+  java.util.LinkedHashMap<Long, JobRecord> activated(final GpuBatchProcessor p) {
+    final java.util.LinkedHashMap<Long, JobRecord> out = new java.util.LinkedHashMap<>();
     final int n = result.get(JAVA_INT, 8);
     for (int i = 0; i < n; i++) {
       final MemorySegment j = jobs.asSlice((long) JOB_BYTES * i, JOB_BYTES);
       final ZbHip.Deployed d = p.process(j.get(JAVA_INT, 36));
       final int elem = j.get(JAVA_INT, 40);
-      batch.jobKeys().add().setValue(j.get(JAVA_LONG, 0));
-      final JobRecord job = batch.jobs().add();
+      final JobRecord job = new JobRecord();
       job.setType(batch.getType())
           .setWorker(batch.getWorker())
           .setDeadline(j.get(JAVA_LONG, 24))
@@ -91,10 +106,9 @@ record JobActivation(MemorySegment command, MemorySegment jobs, long capacity, M
           .setProcessDefinitionVersion(d.version())
           .setVariables(variables(j, p))
           .setTenantId("<default>");
+      out.put(j.get(JAVA_LONG, 0), job);
     }
-    batch.setTruncated(result.get(JAVA_BYTE, 14) != 0);
-    meta.recordType(RecordType.EVENT).intent(JobBatchIntent.ACTIVATED);
-    out.appendRecord(key(), batch, meta);
+    return out;
   }
 
   /** The job's collected variables (zbhip_doc_entry rows) as a msgpack document. */

@@ -250,6 +250,8 @@ public final class ZbHip {
           FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle JOB_STATE =
       fn("zbhip_job_state", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG));
+  private static final MethodHandle ACTIVATABLE_JOBS =
+      fn("zbhip_activatable_jobs", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
 
   /** The zbhip_db_sink upcall: (ctx, column family, key, key length, value, value length). */
   @FunctionalInterface
@@ -562,6 +564,21 @@ public final class ZbHip {
   public static void activateJobs(
       final MemorySegment h, final MemorySegment cmd, final MemorySegment jobs, final long cap, final MemorySegment result) {
     check((int) call(ACTIVATE_JOBS, h, cmd, jobs, cap, result), "zbhip_activate_jobs");
+  }
+
+  /** zbhip_activatable_jobs: the first {@code cap} JOB_ACTIVATABLE keys of a job type on the device, key order. */
+  public static long[] activatableJobs(final MemorySegment h, final byte[] type, final int cap) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment keys = a.allocate(JAVA_LONG.byteSize() * Math.max(cap, 1), 8);
+      final MemorySegment n = a.allocate(JAVA_LONG);
+      check((int) call(ACTIVATABLE_JOBS, h, a.allocateArray(JAVA_BYTE, type), (long) type.length, keys, (long) cap, n),
+          "zbhip_activatable_jobs");
+      final long[] out = new long[(int) n.get(JAVA_LONG, 0)];
+      for (int i = 0; i < out.length; i++) {
+        out[i] = keys.getAtIndex(JAVA_LONG, i);
+      }
+      return out;
+    }
   }
 
   /**
