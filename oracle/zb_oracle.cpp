@@ -3843,14 +3843,14 @@ std::string Oracle::dump_state() const {
     snprintf(buf, sizeof buf,
              "JOBS|%lld|type=%s,retries=%d,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
              "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
-             "deadline=%lld,worker=%s%s",
+             "deadline=%lld,worker=",
              (long long)k, j.type.c_str(), j.retries, p.els[j.pi.elem].id.c_str(), (long long)j.elementInstanceKey,
-             (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version, (long long)j.deadline,
-             j.worker.c_str(),
-             j.fail_fields ? (",errorMessageHex=" + hex_of(j.error_message) + ",retryBackoff=" +
-                              std::to_string(j.retry_backoff) + ",recurringTime=" + std::to_string(j.recurring_time)).c_str()
-                           : "");
-    rows.push_back(buf);
+             (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version, (long long)j.deadline);
+    // (worker and errorMessage appended unbounded: a message holds up to 10 000 characters)
+    rows.push_back(std::string(buf) + j.worker +
+                   (j.fail_fields ? ",errorMessageHex=" + hex_of(j.error_message) + ",retryBackoff=" +
+                                        std::to_string(j.retry_backoff) + ",recurringTime=" + std::to_string(j.recurring_time)
+                                  : std::string()));
     snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", (long long)k, j.failed ? "FAILED" : j.activated ? "ACTIVATED" : "ACTIVATABLE");
     rows.push_back(buf);
     if (j.failed && j.retries > 0 && j.retry_backoff > 0) {  // JOB_BACKOFF [recurringTime, jobKey] -> DbNil
@@ -3866,11 +3866,11 @@ std::string Oracle::dump_state() const {
     const OProc& p = procs[in.pi.proc];
     snprintf(buf, sizeof buf,
              "INCIDENTS|%lld|errorType=%d,flow=%d,result=%d,processDefinitionKey=%lld,processInstanceKey=%lld,"
-             "elementId=%s,elementInstanceKey=%lld%s",
+             "elementId=%s,elementInstanceKey=%lld",
              (long long)k, in.error_type, in.flow, in.result, (long long)p.def_key, (long long)in.pi.piKey,
-             p.els[in.pi.elem].id.c_str(), (long long)in.eik,
-             in.job_key >= 0 ? (",jobKey=" + std::to_string(in.job_key) + ",messageHex=" + hex_of(in.message)).c_str() : "");
-    rows.push_back(buf);
+             p.els[in.pi.elem].id.c_str(), (long long)in.eik);
+    rows.push_back(std::string(buf) +
+                   (in.job_key >= 0 ? ",jobKey=" + std::to_string(in.job_key) + ",messageHex=" + hex_of(in.message) : ""));
   }
   for (auto& [j, k] : incident_jobs_) {  // INCIDENT_JOBS [jobKey] -> incident key (a job's incident)
     snprintf(buf, sizeof buf, "INCIDENT_JOBS|%lld|%lld", (long long)j, (long long)k);

@@ -128,13 +128,13 @@ def test_push_reads_the_variables_at_its_creation():
     .java:83): a later command of the same instance -- here a parallel branch's completion with a document,
     read in the same log window -- must not leak into the pushed job.  The adapter keeps such commands out
     of the pushing window (adapter.py _push_fenced)."""
-    xml = (bpmn.createExecutableProcess("fork").startEvent("start").parallelGateway("fork")
+    xml = (bpmn.createExecutableProcess("forked").startEvent("start").parallelGateway("fork")
            .serviceTask("a", "a").serviceTask("p", "pushed").sequenceFlowId("j1").parallelGateway("join")
            .moveToNode("fork").serviceTask("b", "b").sequenceFlowId("j2").connectTo("join")
            .moveToNode("join").endEvent("end").done())
     ref, gpu = single([(xml, KEY_A, 1)], [(xml, KEY_A, 1)])
     streams(ref, gpu, "pushed", "pusher", 20000)
-    write(ref, gpu, *[Client.create("fork", (("n", i),)) for i in range(6)])
+    write(ref, gpu, *[Client.create("forked", (("n", i),)) for i in range(6)])
     jobs = open_jobs(ref.parts[0].log)
     by_type = {}
     for k, r in sorted(jobs.items()):

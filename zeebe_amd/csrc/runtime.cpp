@@ -3963,11 +3963,12 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       snprintf(buf, sizeof buf,
                "JOBS|%lld|type=%s,retries=%d,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
                "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
-               "deadline=%lld,worker=%s%s",
+               "deadline=%lld,worker=",
                jk, type, A && A->fail_fields ? A->retries : (int)E.job_retries, P.id(elem).c_str(), k, pik,
-               P.strings[P.bpmn_id].c_str(), (long long)P.def_key, P.version, deadline, A ? A->worker.c_str() : "",
-               fail_suffix.c_str());
-      sink(ctx, buf);
+               P.strings[P.bpmn_id].c_str(), (long long)P.def_key, P.version, deadline);
+      // (worker and errorMessage appended unbounded: a message holds up to 10 000 characters)
+      const std::string row = std::string(buf) + (A ? A->worker : std::string()) + fail_suffix;
+      sink(ctx, row.c_str());
       snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", jk, failed ? "FAILED" : act ? "ACTIVATED" : "ACTIVATABLE");
       sink(ctx, buf);
       if (act) {
@@ -3980,10 +3981,12 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       if (A && A->incident_key >= 0) {  // its JOB_NO_RETRIES incident (DbIncidentState.createIncident)
         snprintf(buf, sizeof buf,
                  "INCIDENTS|%lld|errorType=%d,flow=-1,result=0,processDefinitionKey=%lld,processInstanceKey=%lld,"
-                 "elementId=%s,elementInstanceKey=%lld,jobKey=%lld,messageHex=%s",
+                 "elementId=%s,elementInstanceKey=%lld,jobKey=%lld,messageHex=",
                  (long long)A->incident_key, (int)ZBHIP_ERR_JOB_NO_RETRIES, (long long)P.def_key, pik, P.id(elem).c_str(),
-                 k, jk, hex_of(A->incident_msg_id == ZBHIP_NO_STRING ? std::string() : h->strs[A->incident_msg_id]).c_str());
-        sink(ctx, buf);
+                 k, jk);
+        const std::string row =
+            std::string(buf) + hex_of(A->incident_msg_id == ZBHIP_NO_STRING ? std::string() : h->strs[A->incident_msg_id]);
+        sink(ctx, row.c_str());
         snprintf(buf, sizeof buf, "INCIDENT_JOBS|%lld|%lld", jk, (long long)A->incident_key);
         sink(ctx, buf);
       }
@@ -4760,8 +4763,13 @@ extern "C" int zbhip_import_state_db(zbhip_handle* h, const uint8_t* entries, si
     memcpy(hd, entries + off, 12);
     off += 12;
     if (len - off < (size_t)hd[1] + hd[2]) return ZBHIP_EINVAL;
-    const int n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
-                                                      string_interner, h, row.data(), row.size());
+    int n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
+                                                string_interner, h, row.data(), row.size());
+    while (n == ZBHIP_ENOMEM && row.size() < ((size_t)1 << 26)) {  // a long value (an errorMessage: 10 000 chars)
+      row.resize(row.size() * 8);
+      n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
+                                              string_interner, h, row.data(), row.size());
+    }
     if (n < 0) return n;
     if (n > 0) {
       rows.append(row.data(), (size_t)n);
@@ -4789,8 +4797,13 @@ extern "C" int zbhip_select_instances_db(zbhip_handle* h, const uint8_t* entries
     memcpy(hd, entries + off, 12);
     off += 12;
     if (len - off < (size_t)hd[1] + hd[2]) return ZBHIP_EINVAL;
-    const int n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
-                                                      string_interner, h, row.data(), row.size());
+    int n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
+                                                string_interner, h, row.data(), row.size());
+    while (n == ZBHIP_ENOMEM && row.size() < ((size_t)1 << 26)) {  // a long value (an errorMessage: 10 000 chars)
+      row.resize(row.size() * 8);
+      n = zbhip_serializer_decode_state_entry(h->ser, hd[0], entries + off, hd[1], entries + off + hd[1], hd[2],
+                                              string_interner, h, row.data(), row.size());
+    }
     if (n < 0) return n;
     rows.emplace_back(row.data(), (size_t)n);
     off += (size_t)hd[1] + hd[2];

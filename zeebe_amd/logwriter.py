@@ -82,11 +82,16 @@ class LogSerializer:
 
         from .native import INTERNER
         cb = INTERNER((lambda ctx, b, n: intern(C.string_at(b, n))) if intern else (lambda ctx, b, n: -5))
-        buf = C.create_string_buffer(8192)
+        cap = 8192
+        buf = C.create_string_buffer(cap)
         rows = []
         for cf, k, v in entries:
-            n = check(self.L.zbhip_serializer_decode_state_entry(self.s, cf, k, len(k), v, len(v), cb, None, buf, 8192),
-                      "decode_state_entry")
+            n = self.L.zbhip_serializer_decode_state_entry(self.s, cf, k, len(k), v, len(v), cb, None, buf, cap)
+            while n == -2 and cap < 1 << 26:  # ZBHIP_ENOMEM: a long value (an errorMessage of 10 000 chars)
+                cap *= 8
+                buf = C.create_string_buffer(cap)
+                n = self.L.zbhip_serializer_decode_state_entry(self.s, cf, k, len(k), v, len(v), cb, None, buf, cap)
+            n = check(n, "decode_state_entry")
             if n:
                 rows.append(buf.value.decode())
         return sorted(rows)
