@@ -283,14 +283,24 @@ final class DeviceScheduledState {
   static final class PendingMessageSubscriptions implements PendingMessageSubscriptionState {
     private final GpuBatchProcessor gpu;
     private final PendingMessageSubscriptionState engine;
+    private final TransientPendingSubscriptionState engineTransient;
 
-    PendingMessageSubscriptions(final GpuBatchProcessor gpu, final PendingMessageSubscriptionState engine) {
+    PendingMessageSubscriptions(final GpuBatchProcessor gpu, final PendingMessageSubscriptionState engine,
+        final TransientPendingSubscriptionState engineTransient) {
       this.gpu = gpu;
       this.engine = engine;
+      this.engineTransient = engineTransient;
     }
 
     @Override
     public void visitPending(final long deadline, final MessageSubscriptionVisitor visitor) {
+      // subscriptions moved with their correlation key (Messages.toEngine): pending in the engine's state now
+      for (final var e : gpu.messages().movedPendingMessage) {
+        engineTransient.add(new TransientPendingSubscriptionState.PendingSubscription(
+            e.getKey().elementInstanceKey(), e.getKey().messageName(), e.getValue().record.getTenantId()),
+            e.getValue().sentTime);
+      }
+      gpu.messages().movedPendingMessage.clear();
       engine.visitPending(deadline, visitor);
       if (!gpu.scheduledReady()) {
         return;

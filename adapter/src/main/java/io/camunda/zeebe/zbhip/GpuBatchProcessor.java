@@ -293,6 +293,12 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     int i = window.covers(record.getPosition()) ? window.indexOf(record.getPosition()) : -1;
     if (i < 0) {
       if (!isHotPath(record, continuations.iterator())) {
+        if (messages.enabled() && record.getValueType() == ValueType.MESSAGE
+            && record.getIntent() == io.camunda.zeebe.protocol.record.intent.MessageIntent.PUBLISH) {
+          // a publish the engine processes: its correlation key's message state goes there first
+          messages.toEngine(((io.camunda.zeebe.protocol.impl.record.value.message.MessageRecord) record.getValue())
+              .getCorrelationKey(), this, zeebeDb::upsert);
+        }
         // a command the device does not run for an instance it holds (INCIDENT:RESOLVE of a gateway's
         // incident, PROCESS_INSTANCE:CANCEL, ...): the instance moves to RocksDB first
         final int held = heldInstance(record);
@@ -569,7 +575,12 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
 
   private ProcessingResult fallBack(final int i, final TypedRecord record, final ProcessingResultBuilder out) {
     final int instance = window.instanceOf(i);
-    handOff(instance);
+    if (Messages.isMessageCommand(record.getValueType()) && record.getValueType() != ValueType.PROCESS_MESSAGE_SUBSCRIPTION) {
+      // a message-partition command the device declined: its correlation key's state moves to the engine
+      messages.toEngine(new String(stringValue(instance), StandardCharsets.UTF_8), this, zeebeDb::upsert);
+    } else {
+      handOff(instance);
+    }
     final long before = ZbHip.keyBefore(handle, i);
     keyGenerator.setKeyIfHigher(before);
     // the keys the engine's batch generates (follow-ups included) are declared after it
@@ -608,10 +619,15 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     return new DeviceScheduledState.PendingProcessSubscriptions(this, engineState, engineTransient);
   }
 
-  /** ... to MessageObserver (PendingMessageSubscriptionChecker). */
+  /**
+   * ... to MessageObserver (PendingMessageSubscriptionChecker); {@code engineTransient} is the message
+   * side's TransientPendingSubscriptionState (CORRELATING entries of subscriptions moved with their
+   * correlation key go into it).
+   */
   public io.camunda.zeebe.engine.state.immutable.PendingMessageSubscriptionState pendingMessageSubscriptionState(
-      final io.camunda.zeebe.engine.state.immutable.PendingMessageSubscriptionState engineState) {
-    return new DeviceScheduledState.PendingMessageSubscriptions(this, engineState);
+      final io.camunda.zeebe.engine.state.immutable.PendingMessageSubscriptionState engineState,
+      final io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState engineTransient) {
+    return new DeviceScheduledState.PendingMessageSubscriptions(this, engineState, engineTransient);
   }
 
   /** The broker's JobStreamer (the one EngineProcessors gets): device jobs of streamed types are pushed. */

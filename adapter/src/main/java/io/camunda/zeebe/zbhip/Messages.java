@@ -4,9 +4,14 @@
  * zeebe_amd/adapter.py (GpuBatchProcessor._message_command, xpart_value); tests/test_gpu_psm_messages.py
  * runs it on three partitions inside a restatement of ProcessingStateMachine against the engine alone.
  *
- *  - MESSAGE:PUBLISH (MessagePublishProcessor) with time-to-live <= 0, no message id and no variables,
+ *  - MESSAGE:PUBLISH (MessagePublishProcessor) with time-to-live 0, no message id and no variables,
  *    of a message name a device catch event waits for -> ZBHIP_CMD_PUBLISH on the correlation slot
  *    (the value-dictionary id of the correlation key);
+ *  - one owner per correlation key: a publish the engine processes (outside that subset) first moves its
+ *    key's subscriptions from the device into RocksDB (toEngine: zbhip_export_correlation_slots_db +
+ *    zbhip_evict_correlation_slots), and every later message command of the key is the engine's -- it
+ *    buffers messages with a time-to-live, correlates them when a subscription opens and expires them
+ *    (MessagePublishProcessor.java:83-185, MessageCorrelator.java:41-96, MessageTimeToLiveChecker);
  *  - MESSAGE_SUBSCRIPTION:CREATE / CORRELATE (the message partition's side) and
  *    PROCESS_MESSAGE_SUBSCRIPTION:CREATE / CORRELATE (the process instance partition's side) ->
  *    zbhip_xpart_cmd rows of the window (ZBHIP_CMD_MSG_SUB_* / ZBHIP_CMD_PMS_*).
@@ -62,6 +67,10 @@ final class Messages {
   // MESSAGE_SUBSCRIPTION_BY_KEY [elementInstanceKey, messageName] -> correlation slot of an open
   // subscription: a MESSAGE_SUBSCRIPTION:CORRELATE's value carries no correlation key
   private final Map<SubscriptionKey, Integer> subscriptions = new HashMap<>();
+  // correlation keys whose message state the engine holds (toEngine)
+  private final Set<String> engineOwned = new java.util.HashSet<>();
+  // CORRELATING entries of subscriptions moved with their key, for the engine's transient state
+  final List<Map.Entry<SubscriptionKey, PendingSubscription>> movedPendingMessage = new ArrayList<>();
   // (elementInstanceKey, messageName) -> routing handle (slot << 16 | ordinal) of a device subscription
   private final Map<SubscriptionKey, Long> handles = new HashMap<>();
   private final java.util.Set<Integer> closingSlots = new java.util.HashSet<>();
@@ -108,8 +117,9 @@ final class Messages {
   DeviceCommand of(final TypedRecord record, final GpuBatchProcessor p, final Arena arena) {
     if (record.getValueType() == ValueType.MESSAGE) {
       final MessageRecord v = (MessageRecord) record.getValue();
-      if (record.getIntent() != MessageIntent.PUBLISH || v.getTimeToLive() > 0 || !v.getMessageId().isEmpty()
-          || v.getVariablesBuffer().capacity() > 1 || !messageNames.contains(v.getName())) {
+      if (record.getIntent() != MessageIntent.PUBLISH || v.getTimeToLive() != 0 || !v.getMessageId().isEmpty()
+          || v.getVariablesBuffer().capacity() > 1 || !messageNames.contains(v.getName())
+          || engineOwned.contains(v.getCorrelationKey())) {
         return null;
       }
       final long corr = p.internString(v.getCorrelationKey().getBytes(StandardCharsets.UTF_8));
@@ -157,6 +167,12 @@ final class Messages {
     }
     pik = v.getProcessInstanceKey();
     eik = v.getElementInstanceKey();
+    // a key the engine owns: a CREATE by its key, a CORRELATE / DELETE (no key in the value) when the
+    // device holds no such subscription
+    final SubscriptionKey sk = new SubscriptionKey(eik, v.getMessageName());
+    if (kind == ZbHip.CMD_MSG_SUB_CREATE ? engineOwned.contains(v.getCorrelationKey()) : !subscriptions.containsKey(sk)) {
+      return null;
+    }
     // the routing handle of the subscribing element instance: its slot and key ordinal when the
     // instance lives here (a local correlation enters it in the same batch), else an id derived from
     // the element instance key -- unique per subscription like the reference's
@@ -178,10 +194,13 @@ final class Messages {
     int corr = v.getCorrelationKey().isEmpty() ? NO_STRING : (int) p.internString(bytes(v.getCorrelationKeyBuffer()));
     if (kind == ZbHip.CMD_MSG_SUB_CORRELATE || kind == ZbHip.CMD_MSG_SUB_DELETE) {
       // no correlation key in the value: the slot of the subscription it names
-      corr = subscriptions.getOrDefault(new SubscriptionKey(eik, v.getMessageName()), 0);
+      corr = subscriptions.get(sk);
     }
     if (Integer.toUnsignedLong(corr) >= correlationSlots) {
       return null;
+    }
+    if (kind == ZbHip.CMD_MSG_SUB_CREATE) {
+      subscriptions.putIfAbsent(sk, corr); // a DELETE read into the same window finds the slot
     }
     fill(x, pik, eik, v.getMessageKey(), p.internName(v.getMessageName()),
         v.getBpmnProcessId().isEmpty() ? 0xFFFF : p.internName(v.getBpmnProcessId()), corr, kind,
@@ -273,6 +292,33 @@ final class Messages {
         final PendingProcessSubscription ps = pendingProcess.remove(e.getKey());
         if (ps != null) {
           movedPending.add(Map.entry(e.getKey(), ps));
+        }
+        it.remove();
+      }
+    }
+  }
+
+  /**
+   * One owner per correlation key: before the engine processes a publish of {@code correlationKey} (or a
+   * message command of it the device declined), the key's subscriptions move from its correlation slot
+   * into RocksDB and off the device, their CORRELATING entries into the engine's transient state, and
+   * the key's later message commands go to the engine (adapter.py _message_state_to_engine).
+   */
+  void toEngine(final String correlationKey, final GpuBatchProcessor p, final ZbHip.DbSink rocksDb) {
+    if (!engineOwned.add(correlationKey)) {
+      return;
+    }
+    final long slot = p.internString(correlationKey.getBytes(StandardCharsets.UTF_8));
+    if (slot < 0 || slot >= correlationSlots) {
+      return;
+    }
+    ZbHip.correlationSlotToEngine(p.handle(), (int) slot, rocksDb);
+    for (final var it = subscriptions.entrySet().iterator(); it.hasNext(); ) {
+      final var e = it.next();
+      if (e.getValue() == slot) {
+        final PendingSubscription ps = pendingMessage.remove(e.getKey());
+        if (ps != null) {
+          movedPendingMessage.add(Map.entry(e.getKey(), ps));
         }
         it.remove();
       }

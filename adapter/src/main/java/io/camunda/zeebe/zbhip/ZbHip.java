@@ -210,6 +210,10 @@ public final class ZbHip {
   private static final MethodHandle EXPORT_INSTANCES_DB =
       fn("zbhip_export_instances_db", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle EVICT = fn("zbhip_evict_instances", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG));
+  private static final MethodHandle EXPORT_SLOTS_DB =
+      fn("zbhip_export_correlation_slots_db", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
+  private static final MethodHandle EVICT_SLOTS =
+      fn("zbhip_evict_correlation_slots", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG));
   private static final MethodHandle KEY_BEFORE = fn("zbhip_key_before", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle CONTINUATIONS =
       fn("zbhip_continuations", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
@@ -517,6 +521,19 @@ public final class ZbHip {
       final MemorySegment stub = sinkStub(a, sink);
       check((int) call(EXPORT_INSTANCES_DB, h, ids, 1L, stub, MemorySegment.NULL), "zbhip_export_instances_db");
       check((int) call(EVICT, h, ids, 1L), "zbhip_evict_instances");
+    }
+  }
+
+  /**
+   * A correlation key's message state moves to the engine (one owner per key): the slot's
+   * MESSAGE_SUBSCRIPTION zb-db entries into {@code sink} (RocksDB), then the rows leave the device.
+   */
+  public static void correlationSlotToEngine(final MemorySegment h, final int slot, final DbSink sink) {
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment ids = a.allocateArray(JAVA_INT, slot);
+      final MemorySegment stub = sinkStub(a, sink);
+      check((int) call(EXPORT_SLOTS_DB, h, ids, 1L, stub, MemorySegment.NULL), "zbhip_export_correlation_slots_db");
+      check((int) call(EVICT_SLOTS, h, ids, 1L), "zbhip_evict_correlation_slots");
     }
   }
 

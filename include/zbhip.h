@@ -334,7 +334,7 @@ const char* zbhip_name(zbhip_handle* h, uint32_t name_id);
 enum zbhip_command_kind {
   ZBHIP_CMD_CREATE = 1,        /* PROCESS_INSTANCE_CREATION:CREATE (CreateProcessInstanceProcessor.java:129-158) */
   ZBHIP_CMD_JOB_COMPLETE = 2,  /* JOB:COMPLETE (JobCompleteProcessor.java:47-92) */
-  /* MESSAGE:PUBLISH with timeToLive <= 0, no messageId and no variables (MessagePublishProcessor.java
+  /* MESSAGE:PUBLISH with timeToLive 0, no messageId and no variables (MessagePublishProcessor.java
    * handleNewMessage): instance = correlation-key string id (the correlation slot of this message
    * partition), ref = message-name id (zbhip_intern).  Other publishes belong to the CPU engine. */
   ZBHIP_CMD_PUBLISH = 3,
@@ -872,6 +872,20 @@ int zbhip_export_instances_db(zbhip_handle* h, const uint32_t* instances, size_t
 int zbhip_evict_instances(zbhip_handle* h, const uint32_t* instances, size_t n);
 int zbhip_key_before(zbhip_handle* h, size_t i, int64_t* key);
 int zbhip_set_external_keys(zbhip_handle* h, size_t i, uint32_t nkeys);
+
+/* ---- one owner of a correlation key's message state (config 5, the message partition) ----------
+ * The reference correlates a publish to every open subscription of [name, correlationKey] and buffers a
+ * message with a time-to-live for subscriptions opened later (MessagePublishProcessor.java:83-124,
+ * MessageSubscriptionCreateProcessor.java:83-104 -> MessageCorrelator.correlateNextMessage).  The device
+ * keeps subscriptions only; a publish outside its subset (a time-to-live, a message id, variables, a
+ * name the device's catch events do not wait for) is the engine's, and so from then on is the whole
+ * correlation key: before the engine processes that publish the adapter moves the key's correlation
+ * slot to the engine -- zbhip_export_correlation_slots(_db) (its MESSAGE_SUBSCRIPTION_BY_KEY /
+ * _BY_NAME_AND_CORRELATION_KEY rows, into RocksDB) + zbhip_evict_correlation_slots (the rows freed) --
+ * and routes every later message command of that key to the engine. */
+int zbhip_export_correlation_slots(zbhip_handle* h, const uint32_t* slots, size_t n, zbhip_state_sink sink, void* ctx);
+int zbhip_export_correlation_slots_db(zbhip_handle* h, const uint32_t* slots, size_t n, zbhip_db_sink sink, void* ctx);
+int zbhip_evict_correlation_slots(zbhip_handle* h, const uint32_t* slots, size_t n);
 
 /* ---- zb-db bytes back into HBM (restart / hand-back; the reference's
  * replay-equivalence property, ReplayStateRandomizedPropertyTest.java:74-140) ----------------------

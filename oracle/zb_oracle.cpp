@@ -1040,6 +1040,9 @@ struct MsgVal {
   int proc = -1, elem = -1;  // PMS records that carry the elementId
   uint32_t inst = 0;
   uint16_t eord = 0;
+  // MESSAGE:PUBLISH (MessageRecord.java:37-43): timeToLive, messageId (string id), the command's timestamp
+  int64_t ttl = 0, timestamp = 0;
+  uint32_t message_id = ZBHIP_NO_STRING;
 };
 
 // A command or event in flight (TypedRecord)
@@ -1442,7 +1445,7 @@ class Oracle {
     rec.pi.elem = r.element_idx;
     rec.pi.flowScopeKey = r.scope_key;
     rec.pi.piKey = r.process_instance_key;
-    const bool msg = (r.value_type == ZBHIP_VT_MESSAGE && r.intent == ZBHIP_MSG_PUBLISH) ||
+    const bool msg = (r.value_type == ZBHIP_VT_MESSAGE && (r.intent == ZBHIP_MSG_PUBLISH || r.intent == ZBHIP_MSG_EXPIRE)) ||
                      (r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION &&
                       (r.intent == ZBHIP_MS_CREATE || r.intent == ZBHIP_MS_CORRELATE || r.intent == ZBHIP_MS_DELETE)) ||
                      (r.value_type == ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION &&
@@ -1469,6 +1472,14 @@ class Oracle {
       m.partition = r.partition;
       m.interrupting = r.interrupting;
       m.inst = instance;
+      if (r.value_type == ZBHIP_VT_MESSAGE) {
+        // a PUBLISH carries timeToLive in aux, the command's timestamp in scope_key and the messageId's
+        // string id in process_instance_key (-1: none); an EXPIRE its message key as the key
+        m.ttl = r.aux;
+        m.timestamp = r.scope_key;
+        m.message_id = r.process_instance_key < 0 ? ZBHIP_NO_STRING : (uint32_t)r.process_instance_key;
+        m.eik = m.pik = -1;
+      }
       rec.doc = Doc{0, 0};
       rec.r.aux = -1;
       fill_msg(rec, m);
@@ -1671,6 +1682,22 @@ class Oracle {
             incident_pi_[L(r.at(1))] = L(r.at(2));
           } else if (cf == "INCIDENT_JOBS") {
             incident_jobs_[L(r.at(1))] = L(r.at(2));
+          } else if (cf == "MESSAGE_SUBSCRIPTION_BY_KEY") {
+            // a message partition's subscriptions moved from the device (its correlation key's message
+            // state goes to the engine): [elementInstanceKey, messageName] -> MessageSubscription
+            auto f = fields(r.at(3));
+            MsgVal m;
+            m.eik = L(r.at(1));
+            m.name = (uint16_t)intern(r.at(2));
+            m.pik = L(f.at("processInstanceKey"));
+            m.bpmn = (uint16_t)intern(f.at("bpmnProcessId"));
+            m.msg_key = L(f.at("messageKey"));
+            m.corr = (uint32_t)intern_string(f.at("correlationKey"));
+            m.interrupting = (uint8_t)L(f.at("interrupting"));
+            msub_[{m.eik, (int)m.name}] = MsgSub{L(f.at("key")), f.at("correlating") == "1", m};
+            msub_by_corr_.insert({(int)m.name, m.corr, m.eik});
+          } else if (cf == "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY") {
+            continue;  // (the index of the BY_KEY rows)
           } else {
             throw Unsupported{"column family " + cf};
           }
@@ -1829,6 +1856,16 @@ class Oracle {
   std::map<std::pair<int64_t, int>, MsgSub> msub_;                       // [eik, name]
   std::set<std::tuple<int, uint32_t, int64_t>> msub_by_corr_;           // [name, corr, eik]
   bool msg_stats_ = false;                                               // messagesDeadlineCount row
+  // buffered messages (DbMessageState.java:133-213): MESSAGE_KEY, MESSAGES [[tenant, name, correlationKey],
+  // key], MESSAGE_DEADLINES [deadline, key], MESSAGE_IDS [[tenant, name, correlationKey], messageId],
+  // MESSAGE_CORRELATED [key, bpmnProcessId] and the messagesDeadlineCount of MESSAGE_STATS
+  struct StoredMessage { uint16_t name; uint32_t corr; int64_t ttl, deadline; uint32_t message_id; };
+  std::map<int64_t, StoredMessage> messages_;
+  std::set<std::tuple<int, uint32_t, int64_t>> msg_by_corr_;
+  std::set<std::pair<int64_t, int64_t>> msg_deadlines_;
+  std::set<std::tuple<int, uint32_t, uint32_t>> msg_ids_;
+  std::set<std::pair<int64_t, int>> msg_correlated_;
+  int64_t msg_deadline_count_ = 0;
 
   // --- batch context ---
   std::vector<ORecord>* batch_ = nullptr;
@@ -1995,6 +2032,8 @@ class Oracle {
       activate_batch(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_MESSAGE && cmd.r.intent == ZBHIP_MSG_PUBLISH)
       publish_message(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_MESSAGE && cmd.r.intent == ZBHIP_MSG_EXPIRE)
+      expire_message(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_MS_CREATE)
       message_subscription_create(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_MESSAGE_SUBSCRIPTION && cmd.r.intent == ZBHIP_MS_CORRELATE)
@@ -2230,8 +2269,23 @@ class Oracle {
     msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_CREATED, k, c);
     msub_[{c.eik, (int)c.name}] = MsgSub{k, false, c};  // MessageSubscriptionCreatedApplier
     msub_by_corr_.insert({(int)c.name, c.corr, c.eik});
-    // MessageCorrelator.correlateNextMessage: a message outlives its PUBLISH batch only with a
-    // positive time-to-live, which the subset excludes -> nothing buffered to correlate
+    // MessageCorrelator.correlateNextMessage (processing/message/MessageCorrelator.java:41-96): the first
+    // buffered message of [tenant, name, correlationKey] (key order) whose deadline is after now and that
+    // no instance of this process got yet -> MESSAGE_SUBSCRIPTION:CORRELATING (the subscription key, the
+    // command's record with the message key) and PROCESS_MESSAGE_SUBSCRIPTION:CORRELATE instead of the
+    // acknowledgement
+    for (auto it = msg_by_corr_.lower_bound({(int)c.name, c.corr, INT64_MIN});
+         it != msg_by_corr_.end() && std::get<0>(*it) == (int)c.name && std::get<1>(*it) == c.corr; ++it) {
+      const int64_t mk = std::get<2>(*it);
+      if (!(messages_.at(mk).deadline > now_ms) || msg_correlated_.count({mk, (int)c.bpmn})) continue;
+      MsgSub& sub = msub_.at({c.eik, (int)c.name});
+      sub.rec.msg_key = mk;
+      msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_CORRELATING, k, sub.rec);
+      sub.correlating = true;  // MessageSubscriptionCorrelatingApplier: updateToCorrelatingState,
+      msg_correlated_.insert({mk, (int)c.bpmn});  // putMessageCorrelation
+      send_command(partition_of_key(c.pik), ZBHIP_CMD_PMS_CORRELATE, sub.rec);
+      return;
+    }
     send_command(partition_of_key(c.pik), ZBHIP_CMD_PMS_CREATE, ack);
   }
 
@@ -2296,15 +2350,64 @@ class Oracle {
     pms_.erase(it);
   }
 
-  // MessagePublishProcessor.processRecord / handleNewMessage (processing/message/MessagePublishProcessor.java)
-  void publish_message(ORecord& cmd) {
-    const MsgVal c = cmd.m;  // name, correlationKey (no messageId, TTL 0, no variables)
-    int64_t msgKey = next_key();
+  // the MESSAGE record of a message (MessageRecord.java:37-43): name, correlationKey, timeToLive, messageId,
+  // deadline -- zbhip_record.reason_arg bit 1 marks them set: aux = timeToLive, scope_key = deadline,
+  // partition = the messageId's string id (-1 none); without it (TTL 0, no id: the records the device
+  // writes too) a reader takes TTL 0 / deadline = the command's timestamp
+  void message_record(int intent, int64_t key, const StoredMessage& sm) {
     MsgVal mv;
-    mv.name = c.name;
-    mv.corr = c.corr;
-    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE, ZBHIP_MSG_PUBLISHED, msgKey, mv);
-    msg_stats_ = true;  // MessagePublishedApplier -> DbMessageState.put: messagesDeadlineCount upsert
+    mv.name = sm.name;
+    mv.corr = sm.corr;
+    ORecord& r = msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE, intent, key, mv);
+    if (sm.ttl == 0 && sm.message_id == ZBHIP_NO_STRING) return;  // (the device's form: TTL 0, no id)
+    r.r.reason_arg = 2;
+    r.r.aux = sm.ttl;
+    r.r.scope_key = sm.deadline;
+    r.r.partition = sm.message_id == ZBHIP_NO_STRING ? -1 : (int32_t)sm.message_id;
+  }
+
+  // MessagePublishedApplier -> DbMessageState.put (:225-249)
+  void put_message(int64_t key, const StoredMessage& sm) {
+    messages_[key] = sm;
+    msg_by_corr_.insert({(int)sm.name, sm.corr, key});
+    msg_deadlines_.insert({sm.deadline, key});
+    ++msg_deadline_count_;
+    msg_stats_ = true;
+    if (sm.message_id != ZBHIP_NO_STRING) msg_ids_.insert({(int)sm.name, sm.corr, sm.message_id});
+  }
+
+  // MessageExpiredApplier -> DbMessageState.remove (:313-349): the message, its index rows and its
+  // MESSAGE_CORRELATED rows (a key no longer stored: nothing)
+  void remove_message(int64_t key) {
+    auto it = messages_.find(key);
+    if (it == messages_.end()) return;
+    const StoredMessage sm = it->second;
+    messages_.erase(it);
+    msg_by_corr_.erase({(int)sm.name, sm.corr, key});
+    if (sm.message_id != ZBHIP_NO_STRING) msg_ids_.erase({(int)sm.name, sm.corr, sm.message_id});
+    msg_deadlines_.erase({sm.deadline, key});
+    --msg_deadline_count_;
+    for (auto c = msg_correlated_.lower_bound({key, INT32_MIN}); c != msg_correlated_.end() && c->first == key;)
+      c = msg_correlated_.erase(c);
+  }
+
+  // MessagePublishProcessor.processRecord / handleNewMessage (processing/message/MessagePublishProcessor.java
+  // :83-124): a messageId already buffered for [name, correlationKey] -> ALREADY_EXISTS; else PUBLISHED
+  // (deadline = the command's timestamp + timeToLive), correlateToSubscriptions, the correlate commands,
+  // and with timeToLive <= 0 EXPIRED in the same batch.  (No message start events: their processes are
+  // outside the oracle's deployments.)
+  void publish_message(ORecord& cmd) {
+    const MsgVal c = cmd.m;  // name, correlationKey, timeToLive, messageId (no variables)
+    if (c.message_id != ZBHIP_NO_STRING && msg_ids_.count({(int)c.name, c.corr, c.message_id})) {
+      reject(cmd, ZBHIP_REJ_ALREADY_EXISTS,
+             "Expected to publish a new message with id '" + str(c.message_id) +
+                 "', but a message with that id was already published");
+      return;
+    }
+    int64_t msgKey = next_key();
+    const StoredMessage sm{c.name, c.corr, c.ttl, c.timestamp + c.ttl, c.message_id};
+    message_record(ZBHIP_MSG_PUBLISHED, msgKey, sm);
+    put_message(msgKey, sm);
     // correlateToSubscriptions: visit [tenant, name, correlationKey, *] in element-instance-key order
     std::vector<MsgVal> correlating;
     std::set<int> bpmn_seen;
@@ -2314,7 +2417,8 @@ class Oracle {
       if (sub.correlating || bpmn_seen.count(sub.rec.bpmn)) continue;
       sub.rec.msg_key = msgKey;
       msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_SUBSCRIPTION, ZBHIP_MS_CORRELATING, sub.key, sub.rec);
-      sub.correlating = true;  // MessageSubscriptionCorrelatingApplier (+ transient message correlation)
+      sub.correlating = true;  // MessageSubscriptionCorrelatingApplier
+      msg_correlated_.insert({msgKey, (int)sub.rec.bpmn});
       bpmn_seen.insert(sub.rec.bpmn);
       correlating.push_back(sub.rec);
     }
@@ -2325,9 +2429,19 @@ class Oracle {
       m.corr = c.corr;
       send_command(partition_of_key(m.pik), ZBHIP_CMD_PMS_CORRELATE, m);
     }
-    // timeToLive <= 0: EXPIRED in the same batch; MessageExpiredApplier removes the message and its
-    // MESSAGE_CORRELATED rows (DbMessageState.remove :314-349)
-    msg_record(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE, ZBHIP_MSG_EXPIRED, msgKey, mv);
+    if (c.ttl <= 0) {  // EXPIRED in the same batch: MessageExpiredApplier removes it and its correlations
+      message_record(ZBHIP_MSG_EXPIRED, msgKey, sm);
+      remove_message(msgKey);
+    }
+  }
+
+  // MESSAGE_BATCH:EXPIRE of the MessageTimeToLiveChecker, one message key at a time (MessageBatchExpire
+  // Processor.java:33-52): MESSAGE:EXPIRED with an empty MessageRecord (name "", correlationKey "",
+  // timeToLive -1, deadline -1), then MessageExpiredApplier.  tests/psm.py feeds the batch's keys.
+  void expire_message(ORecord& cmd) {
+    const StoredMessage empty{0xFFFF, ZBHIP_NO_STRING, -1, -1, ZBHIP_NO_STRING};
+    message_record(ZBHIP_MSG_EXPIRED, cmd.r.key, empty);
+    remove_message(cmd.r.key);
   }
 
   // ProcessMessageSubscriptionCorrelateProcessor.processRecord
@@ -3910,7 +4024,17 @@ std::string Oracle::dump_state() const {
              (long long)e);
     rows.push_back(buf);
   }
-  if (msg_stats_) rows.push_back("MESSAGE_STATS|messagesDeadlineCount|0");
+  for (auto& [k, m] : messages_) {
+    rows.push_back("MESSAGE_KEY|" + std::to_string(k) + "|name=" + nm(m.name) + ",correlationKey=" + sv(m.corr) +
+                   ",timeToLive=" + std::to_string(m.ttl) + ",deadline=" + std::to_string(m.deadline) +
+                   ",messageId=" + (m.message_id == ZBHIP_NO_STRING ? std::string() : sv(m.message_id)));
+    rows.push_back("MESSAGES|<default>|" + std::string(nm(m.name)) + "|" + sv(m.corr) + "|" + std::to_string(k));
+    if (m.message_id != ZBHIP_NO_STRING)
+      rows.push_back("MESSAGE_IDS|<default>|" + std::string(nm(m.name)) + "|" + sv(m.corr) + "|" + sv(m.message_id));
+  }
+  for (auto& [d, k] : msg_deadlines_) rows.push_back("MESSAGE_DEADLINES|" + std::to_string(d) + "|" + std::to_string(k));
+  for (auto& [k, b] : msg_correlated_) rows.push_back("MESSAGE_CORRELATED|" + std::to_string(k) + "|" + nm(b));
+  if (msg_stats_) rows.push_back("MESSAGE_STATS|messagesDeadlineCount|" + std::to_string(msg_deadline_count_));
   std::sort(rows.begin(), rows.end());
   std::string s;
   for (auto& r : rows) { s += r; s += '\n'; }

@@ -307,6 +307,50 @@ class JobTimeoutTrigger:
         self.service.run_delayed(self.INTERVAL, self._task)
 
 
+class EngineMessageState:
+    """The engine's MessageState for the MessageTimeToLiveChecker (its MESSAGE_DEADLINES rows):
+    DbMessageState.visitMessagesWithDeadlineBeforeTimestamp (:408-434), [deadline, messageKey] order."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def deadlines(self):
+        out = []
+        for r in self.engine.state():
+            if r.startswith("MESSAGE_DEADLINES|"):
+                _, d, k = r.split("|")
+                out.append((int(d), int(k)))
+        return sorted(out)
+
+    def visit_messages_with_deadline_before(self, timestamp, visitor):
+        for deadline, key in self.deadlines():
+            if deadline > timestamp or not visitor(deadline, key):
+                return
+
+
+class MessageTimeToLiveChecker:
+    """MessageTimeToLiveChecker (engine/.../processing/message/MessageTimeToLiveChecker.java:35-124),
+    scheduled by MessageObserver.onRecovered (:47-66) after messagesTtlCheckerInterval (EngineConfiguration:
+    1 min; batch limit Integer.MAX_VALUE): one MESSAGE_BATCH:EXPIRE with the keys of every message whose
+    deadline <= now, then again after the interval."""
+    INTERVAL = 60000
+
+    def __init__(self, message_state, clock):
+        self.state, self.clock = message_state, clock
+
+    def on_recovered(self, service):
+        self.service = service
+        service.run_delayed(self.INTERVAL, self._task)
+
+    def _task(self, builder):
+        keys = []
+        self.state.visit_messages_with_deadline_before(self.clock.now, lambda d, k: keys.append(k) or True)
+        if keys:
+            builder.append_command_record(-1, abi.VT_MESSAGE_BATCH, abi.MESSAGE_BATCH_EXPIRE,
+                                          {"messageKeys": tuple(keys)})
+        self.service.run_delayed(self.INTERVAL, self._task)
+
+
 def open_message_subscription_value(r):
     """SubscriptionCommandSender.sendDirectOpenMessageSubscription (:83-110) from the stored
     ProcessMessageSubscriptionRecord."""
@@ -493,6 +537,11 @@ class PendingStates:
     def pending_message_subscriptions(self, deadline):
         return sorted(((t, sub, r) for sub, (t, r) in self.ms.items() if t < deadline), key=lambda x: x[0])
 
+    def add_ms(self, sub, sent, record):
+        """TransientPendingSubscriptionState.add of a CORRELATING subscription whose row came in with a
+        correlation key's move to the engine."""
+        self.ms[sub] = [sent, record]
+
     def on_sent_pms(self, sub, when):
         if sub in self.pms:
             self.pms[sub][0] = when
@@ -507,7 +556,7 @@ class OracleEngine:
     also the partition's DbKeyGenerator (KeyGeneratorControls) and the RawDbWriter of a hand-off."""
 
     ACCEPTS = (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, abi.VT_PROCESS_INSTANCE, VT_JOB_BATCH,
-               abi.VT_PROCESS_INSTANCE_BATCH) + MESSAGE_VALUE_TYPES
+               abi.VT_PROCESS_INSTANCE_BATCH, abi.VT_MESSAGE_BATCH) + MESSAGE_VALUE_TYPES
 
     def __init__(self, partition_id=1, max_commands_in_batch=100, clock=0, partition_count=1, command_sender=None):
         self.o = Oracle(partition_id=partition_id, partition_count=partition_count,
@@ -521,12 +570,13 @@ class OracleEngine:
         self.slot_of = {}
         self.next_slot = 0
         self.doc_values = []  # client value of every document entry the oracle holds (its doc indices)
-        self.values = None
         self.tables = []
         self.streams = {}  # job streams: type -> (worker, timeout)
         self.stream_sinks = {}  # job type -> (fetchVariables, push)
         self.job_streamer = None  # JobStreamer.notifyWorkAvailable of publishWork without a stream
         self.o.take_notified()  # (the oracle keeps its notifications from now on)
+        self.values = RecordValues([], self.o.name, lambda i: self.o.string_value(i).decode(),
+                                   list_items=self.o.list_items, streams=self.streams)
 
     def deploy(self, xml, key, version=1):
         idx = self.o.deploy(xml, key, version)
@@ -592,6 +642,8 @@ class OracleEngine:
         vt, it, v = record.value_type, record.intent, record.value
         if vt == VT_JOB_BATCH:
             return self._activate(record, out)
+        if vt == abi.VT_MESSAGE_BATCH:
+            return self._expire(record, out)
         r = np.zeros(1, dtype=abi.RECORD_DTYPE)[0]
         r["record_type"], r["value_type"], r["intent"], r["key"] = abi.RT_COMMAND, vt, it, record.key
         r["process_idx"] = r["element_idx"] = -1
@@ -625,6 +677,11 @@ class OracleEngine:
         elif vt == abi.VT_MESSAGE:
             r["message_name"] = self.o.intern(v["name"])
             r["correlation_key"] = self.o.intern_string(v["correlationKey"])
+            # (zb_oracle.cpp process_one: timeToLive in aux, the command's timestamp in scope_key, the
+            # messageId's string id in process_instance_key)
+            r["aux"] = v.get("timeToLive", 0)
+            r["scope_key"] = record.timestamp
+            r["process_instance_key"] = self.o.intern_string(v["messageId"]) if v.get("messageId") else -1
             slot = int(r["correlation_key"])
             variables = ()
         elif vt in MESSAGE_VALUE_TYPES:
@@ -685,6 +742,23 @@ class OracleEngine:
             out.append_post_commit_task(task)
         return out.build()
 
+    def _expire(self, record, out):
+        """MESSAGE_BATCH:EXPIRE (MessageBatchExpireProcessor.java:33-52): MESSAGE:EXPIRED per message key, in
+        the batch's order (the oracle's MESSAGE:EXPIRE of one key each)."""
+        for mk in record.value["messageKeys"]:
+            r = np.zeros(1, dtype=abi.RECORD_DTYPE)[0]
+            r["record_type"], r["value_type"], r["intent"], r["key"] = abi.RT_COMMAND, abi.VT_MESSAGE, abi.MSG_EXPIRE, mk
+            r["process_idx"] = r["element_idx"] = -1
+            r["scope_key"] = r["process_instance_key"] = r["aux"] = r["message_key"] = -1
+            r["correlation_key"], r["message_name"], r["bpmn_process_id"] = abi.NO_STRING, 0xFFFF, 0xFFFF
+            r["rejection_type"] = abi.REJ_NONE
+            self.o.clear_records()
+            self.o.process_one(r, 0xFFFFFF, abi.make_docs(0), record.position or 0, len(out.entries))
+            for x in self.o.records():
+                out.append_record(int(x["key"]), int(x["record_type"]), int(x["value_type"]), int(x["intent"]),
+                                  abi.REJ_NONE, "", self.values.value(x))
+        return out.build()
+
     def _activate(self, record, out):
         v = record.value
         key, jobs, reason = self.o.activate_jobs(v["type"], v["worker"], v["timeout"], v["maxJobsToActivate"],
@@ -728,12 +802,12 @@ class Client:
                     "tenantId": "<default>"})
 
     @staticmethod
-    def publish_message(name, correlation_key, timestamp=0):
-        """MessageClient.publish with time-to-live 0 (MessageRecord.java:37-43); `timestamp` = the
-        command's record timestamp (the broker's clock when it was written)."""
+    def publish_message(name, correlation_key, timestamp=0, time_to_live=0, message_id=""):
+        """MessageClient.publish (MessageRecord.java:37-43): time-to-live 0 unless given, an optional message
+        id; `timestamp` = the command's record timestamp (the broker's clock when it was written)."""
         return Rec(abi.RT_COMMAND, abi.VT_MESSAGE, abi.MSG_PUBLISH, -1,
-                   {"name": name, "correlationKey": correlation_key, "timeToLive": 0, "variables": (), "messageId": "",
-                    "deadline": -1, "tenantId": "<default>"}, timestamp=timestamp)
+                   {"name": name, "correlationKey": correlation_key, "timeToLive": time_to_live, "variables": (),
+                    "messageId": message_id, "deadline": -1, "tenantId": "<default>"}, timestamp=timestamp)
 
     @staticmethod
     def activate_jobs(job_type, worker="w", timeout=300000, max_jobs=10, timestamp=0):

@@ -16,8 +16,9 @@ loop over the engine alone (tests/psm.py: the oracle engine, its own state views
 import numpy as np
 import pytest
 
-from psm import (Client, Clock, DueDateTimerChecker, EngineJobState, EngineTimerState, InterPartitionCommandSender,
-                 JobTimeoutTrigger, Log, OracleEngine, PendingMessageSubscriptionChecker,
+from psm import (Client, Clock, DueDateTimerChecker, EngineJobState, EngineMessageState, EngineTimerState,
+                 InterPartitionCommandSender, JobTimeoutTrigger, Log, MessageTimeToLiveChecker, OracleEngine,
+                 PendingMessageSubscriptionChecker,
                  PendingProcessMessageSubscriptionChecker, Rec, ScheduleService, StreamProcessor, open_jobs, run_cluster)
 from test_oracle_boundary import cycle_process, multiple_sequence_flows
 from test_oracle_timers import NOW, timer_process
@@ -65,6 +66,9 @@ class PartitionLoop:
         # StreamProcessorLifecycleAware.onRecovered, in registration order
         self.timer_checker.on_recovered(self.service)
         JobTimeoutTrigger(jobs, clock).on_recovered(self.service)
+        # MessageObserver.onRecovered (:47-66): the TTL checker over the engine's MESSAGE_DEADLINES (the
+        # device buffers no messages: a key with a buffered message is the engine's)
+        MessageTimeToLiveChecker(EngineMessageState(self.engine), clock).on_recovered(self.service)
         if sender is not None:
             PendingProcessMessageSubscriptionChecker(pending, clock, sender).on_recovered(self.service)
             PendingMessageSubscriptionChecker(pending, clock, sender, partition_id).on_recovered(self.service)
@@ -75,7 +79,13 @@ class PartitionLoop:
             return sorted(eng)
         part = self.adapter.part
         assert part.current_key() <= self.engine.current_key()  # one key generator
-        return sorted([r for r in part.state() if not r.startswith("KEY|")] + eng)
+        rows = [r for r in part.state() if not r.startswith("KEY|")] + eng
+        # MESSAGE_STATS: one messagesDeadlineCount row, the buffered messages of both (the device's are 0)
+        stats = [r for r in rows if r.startswith("MESSAGE_STATS|")]
+        if len(stats) > 1:
+            rows = [r for r in rows if not r.startswith("MESSAGE_STATS|")] + \
+                ["MESSAGE_STATS|messagesDeadlineCount|%d" % sum(int(r.rsplit("|", 1)[1]) for r in stats)]
+        return sorted(rows)
 
 
 class Cluster:

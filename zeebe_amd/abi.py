@@ -59,7 +59,8 @@ MS_INTENTS = {0: "CREATE", 1: "CREATED", 2: "CORRELATE", 3: "CORRELATED", 4: "RE
               6: "DELETE", 7: "DELETED", 8: "CORRELATING"}
 PMS_INTENTS = {0: "CREATING", 1: "CREATE", 2: "CREATED", 3: "CORRELATE", 4: "CORRELATED", 5: "DELETING",
                6: "DELETE", 7: "DELETED"}
-MSG_PUBLISH, MSG_PUBLISHED, MSG_EXPIRED = 0, 1, 3
+MSG_PUBLISH, MSG_PUBLISHED, MSG_EXPIRE, MSG_EXPIRED = 0, 1, 2, 3
+VT_MESSAGE_BATCH, MESSAGE_BATCH_EXPIRE = 35, 0  # ValueType.MESSAGE_BATCH (protocol.xml:52), MessageBatchIntent
 MS_CREATE, MS_CREATED, MS_CORRELATE, MS_CORRELATED, MS_CORRELATING = 0, 1, 2, 3, 8
 MS_DELETE, MS_DELETED = 6, 7
 PMS_CREATING, PMS_CREATE, PMS_CREATED, PMS_CORRELATE, PMS_CORRELATED = 0, 1, 2, 3, 4

@@ -22,7 +22,7 @@ inside ``ProcessingStateMachine.batchProcessing`` / ``collectBatchProcessingStep
   (JobBatchActivateProcessor.java:60-143).
 * After recovery, instances of device processes move from the engine's state into HBM
   (``on_recovered`` -> ``zbhip_import_state``), as StreamProcessorLifecycleAware.onRecovered would.
-* Config 5 (``correlation_keys`` > 0): MESSAGE:PUBLISH (time-to-live <= 0, no message id, no
+* Config 5 (``correlation_keys`` > 0): MESSAGE:PUBLISH (time-to-live 0, no message id, no
   variables), MESSAGE_SUBSCRIPTION:CREATE / CORRELATE and PROCESS_MESSAGE_SUBSCRIPTION:CREATE /
   CORRELATE go to the device.  The cross-partition commands a device batch sends
   (``zbhip_outbox_command``) are handed to ``InterPartitionCommandSender.sendCommand`` in a post-commit
@@ -249,6 +249,11 @@ class RecordValues:
             nm = self.name(nid) if nid != 0xFFFF else ""
             corr = self.string_value(cid) if cid != abi.NO_STRING else ""
             if vt == abi.VT_MESSAGE:  # MessageRecord.java:37-43
+                if int(r["reason_arg"]) & 2:  # the fields set (a buffered message, an EXPIRED of the TTL checker)
+                    mid = int(r["partition"])
+                    return {"name": nm, "correlationKey": corr, "timeToLive": aux, "variables": (),
+                            "messageId": self.string_value(mid) if mid >= 0 else "", "deadline": scope,
+                            "tenantId": TENANT}
                 return {"name": nm, "correlationKey": corr, "timeToLive": 0, "variables": (), "messageId": "",
                         "deadline": timestamp, "tenantId": TENANT}
             bpmn = self.name(bid) if bid != 0xFFFF else ""
@@ -381,6 +386,9 @@ class DevicePendingSubscriptionState:
         return self.engine.pending_process_message_subscriptions(deadline) + dev
 
     def pending_message_subscriptions(self, deadline):
+        for sub, entry in self.adapter.moved_pending_ms:  # subscriptions moved with their key: the engine's now
+            self.engine.add_ms(sub, *entry)
+        self.adapter.moved_pending_ms.clear()
         dev = self.adapter.pending_message_subscriptions(deadline) if self.adapter.scheduled_ready() else []
         return self.engine.pending_message_subscriptions(deadline) + dev
 
@@ -497,6 +505,9 @@ class GpuBatchProcessor:
         self.subscriptions = {}        # (elementInstanceKey, messageName) -> correlation slot of an open
                                        # MESSAGE_SUBSCRIPTION (MESSAGE_SUBSCRIPTION_BY_KEY): a CORRELATE's
                                        # value carries no correlation key
+        self.engine_owned = set()      # correlation keys whose message state the engine holds (one owner
+                                       # per key: _message_state_to_engine)
+        self.moved_pending_ms = []     # CORRELATING entries of subscriptions moved with their key
         self.part = None
         self.by_key, self.latest_by_id, self.by_index = {}, {}, []
         self.engine_job_types = set()  # job types the engine's processes (or handed-off instances) hold
@@ -529,7 +540,8 @@ class GpuBatchProcessor:
         # what went where (tests read these)
         self.fallback_reasons = []
         self.counts = {"windows": 0, "device_commands": 0, "continuations": 0, "fallbacks": 0, "activations": 0,
-                       "engine_commands": 0, "followups_answered": 0, "time_outs": 0, "job_failures": 0}
+                       "engine_commands": 0, "followups_answered": 0, "time_outs": 0, "job_failures": 0,
+                       "keys_to_engine": 0}
 
     # ---- RecordProcessor ----------------------------------------------------------------------
     def init(self):
@@ -620,6 +632,10 @@ class GpuBatchProcessor:
         i = self.window.index_of(record.position) if self.window.covers(record.position) else -1
         if i < 0:
             if not self._hot(record, 0):
+                if self.correlation_keys > 0 and record.value_type == abi.VT_MESSAGE and \
+                        record.intent == abi.MSG_PUBLISH:
+                    # a publish the engine processes: its correlation key's message state goes there first
+                    self._message_state_to_engine(record.value.get("correlationKey"))
                 # a command the device does not run for an instance it holds (INCIDENT:RESOLVE of a
                 # gateway's incident, PROCESS_INSTANCE:CANCEL, ...): the instance moves to the engine first
                 held = self._held_instance(record)
@@ -698,8 +714,9 @@ class GpuBatchProcessor:
         device does not hold."""
         v, vt, it = record.value, record.value_type, record.intent
         if vt == abi.VT_MESSAGE:
-            if it != abi.MSG_PUBLISH or v.get("timeToLive", 0) > 0 or v.get("messageId") or v.get("variables") \
-                    or v.get("name") not in self.message_names or not isinstance(v.get("correlationKey"), str):
+            if it != abi.MSG_PUBLISH or v.get("timeToLive", 0) != 0 or v.get("messageId") or v.get("variables") \
+                    or v.get("name") not in self.message_names or not isinstance(v.get("correlationKey"), str) \
+                    or v["correlationKey"] in self.engine_owned:
                 return None
             corr = self.part.intern_string(v["correlationKey"])
             if corr >= self.correlation_keys:
@@ -709,6 +726,14 @@ class GpuBatchProcessor:
         if kind is None or v.get("variables"):
             return None
         pik, eik = v["processInstanceKey"], v["elementInstanceKey"]
+        # the message partition's commands of a correlation key the engine owns stay with the engine: a
+        # CREATE by its key, a CORRELATE / DELETE (no key in the value) when the device holds no such
+        # subscription
+        if kind == abi.CMD_MSG_SUB_CREATE and v.get("correlationKey") in self.engine_owned:
+            return None
+        if kind in (abi.CMD_MSG_SUB_CORRELATE, abi.CMD_MSG_SUB_DELETE) and \
+                (eik, v["messageName"]) not in self.subscriptions:
+            return None
         x = abi.make_xparts(1)[0]
         x["element_instance_key"], x["process_instance_key"] = eik, pik
         x["message_key"] = v.get("messageKey", -1)
@@ -745,7 +770,7 @@ class GpuBatchProcessor:
         x["source_partition"] = src
         if kind in (abi.CMD_MSG_SUB_CORRELATE, abi.CMD_MSG_SUB_DELETE):
             # no correlation key in the value: the slot of the subscription it names
-            x["correlation_key"] = self.subscriptions.get((eik, v["messageName"]), 0)
+            x["correlation_key"] = self.subscriptions[(eik, v["messageName"])]
         if int(x["correlation_key"]) >= self.correlation_keys:
             return None
         return {"instance": int(x["correlation_key"]), "kind": kind, "ref": 0}, x
@@ -810,6 +835,10 @@ class GpuBatchProcessor:
                 if x is not None:
                     c["doc_begin"] = len(self.window.xparts)
                     self.window.xparts.append(x)
+                    if c["kind"] == abi.CMD_MSG_SUB_CREATE:
+                        # a DELETE read into the same window finds the slot (its CREATED is emitted later)
+                        self.subscriptions.setdefault((rec.value["elementInstanceKey"], rec.value["messageName"]),
+                                                      c["instance"])
                 self.window.put(rec, c["instance"], c["kind"], c["ref"], doc_begin=c.get("doc_begin", 0))
             else:
                 cid, slot, _ = self.continuations[claimed]
@@ -1017,9 +1046,37 @@ class GpuBatchProcessor:
                     return ref[0]
         return None
 
+    def _message_state_to_engine(self, correlation_key):
+        """One owner per correlation key (include/zbhip.h).  The reference correlates a
+        publish to every open subscription of [name, correlationKey] (MessagePublishProcessor.java:127-185)
+        and buffers a message with a time-to-live for later subscriptions (MessageCorrelator.java:41-96);
+        the device holds subscriptions only.  Before the engine processes a publish of a key, the key's
+        subscriptions move from its correlation slot into the engine's state (zb-db rows through the
+        platform's transaction, then evicted) with their pending CORRELATING entries, and every later
+        message command of the key goes to the engine."""
+        if not isinstance(correlation_key, str) or correlation_key in self.engine_owned:
+            return
+        self.engine_owned.add(correlation_key)
+        slot = self.part.intern_string(correlation_key)
+        if slot >= self.correlation_keys:
+            return  # (never a device slot)
+        rows = self.part.export_correlation_slots([slot])
+        if rows:
+            self.zeebe_db.upsert(rows)
+            self.part.evict_correlation_slots([slot])
+        for sub in [k for k, s in self.subscriptions.items() if s == slot]:
+            del self.subscriptions[sub]
+            if sub in self.pending_ms:
+                self.moved_pending_ms.append((sub, self.pending_ms.pop(sub)))
+        self.counts["keys_to_engine"] += 1
+
     def _fall_back(self, i, record, out):
         inst = self.window.instances[i]
-        self._hand_off(inst)
+        if self.window.cmds[i]["kind"] in abi.SLOT_KINDS:
+            # a message-partition command the device declined: its correlation key's state moves to the engine
+            self._message_state_to_engine(self.part.string_value(inst))
+        else:
+            self._hand_off(inst)
         before = self.part.key_before(i)
         self.key_generator.set_key_if_higher(before)
         self.engine_batch = True

@@ -4058,6 +4058,28 @@ static int gather_instance(zbhip_handle* h, uint32_t i, InstRows& R) {
   return ZBHIP_OK;
 }
 
+// MESSAGE_SUBSCRIPTION_BY_KEY / _BY_NAME_AND_CORRELATION_KEY rows of one correlation slot's kSubs rows
+static void emit_slot_rows(zbhip_handle* h, uint32_t slot, const uint4* sa, const longlong2* sb, const longlong2* sk,
+                           zbhip_state_sink sink, void* ctx) {
+  char buf[768];
+  for (int r = 0; r < kSubs; ++r) {
+    const uint4 a = sa[r];
+    const uint32_t st = a.x & 0xFF;
+    if (st != 1 && st != 2) continue;
+    const char* name = zbhip_name(h, a.y & 0xFFFF);
+    const char* corr = zbhip_string_value(h, slot, nullptr);
+    snprintf(buf, sizeof buf,
+             "MESSAGE_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,correlating=%d,processInstanceKey=%lld,bpmnProcessId=%s,"
+             "messageKey=%lld,correlationKey=%s,interrupting=%u",
+             (long long)sb[r].x, name, (long long)sk[r].x, st == 2 ? 1 : 0, (long long)sb[r].y,
+             zbhip_name(h, a.y >> 16), (long long)sk[r].y, corr, (a.x >> 8) & 1);
+    sink(ctx, buf);
+    snprintf(buf, sizeof buf, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY|<default>|%s|%s|%lld", name, corr,
+             (long long)sb[r].x);
+    sink(ctx, buf);
+  }
+}
+
 int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   if (!h || !sink) return ZBHIP_EINVAL;
   if (!h->relabel_ok) return ZBHIP_ESTATE;
@@ -4113,24 +4135,52 @@ int zbhip_export_state(zbhip_handle* h, zbhip_state_sink sink, void* ctx) {
   // MESSAGE_SUBSCRIPTION_BY_KEY [eik, name] and MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY
   // [tenant, name, correlationKey, eik] of this (message) partition (DbMessageSubscriptionState)
   for (size_t slot = 0; slot < S; ++slot)
-    for (int r = 0; r < kSubs; ++r) {
-      const size_t ri = sub_ri(r, slot);
-      const uint4 a = sub_a[ri];
-      const uint32_t st = a.x & 0xFF;
-      if (st != 1 && st != 2) continue;
-      const char* name = zbhip_name(h, a.y & 0xFFFF);
-      const char* corr = zbhip_string_value(h, (uint32_t)slot, nullptr);
-      snprintf(buf, sizeof buf,
-               "MESSAGE_SUBSCRIPTION_BY_KEY|%lld|%s|key=%lld,correlating=%d,processInstanceKey=%lld,bpmnProcessId=%s,"
-               "messageKey=%lld,correlationKey=%s,interrupting=%u",
-               (long long)sub_b[ri].x, name, (long long)sub_k[ri].x, st == 2 ? 1 : 0, (long long)sub_b[ri].y,
-               zbhip_name(h, a.y >> 16), (long long)sub_k[ri].y, corr, (a.x >> 8) & 1);
-      sink(ctx, buf);
-      snprintf(buf, sizeof buf, "MESSAGE_SUBSCRIPTION_BY_NAME_AND_CORRELATION_KEY|<default>|%s|%s|%lld", name, corr,
-               (long long)sub_b[ri].x);
-      sink(ctx, buf);
-    }
+    emit_slot_rows(h, (uint32_t)slot, &sub_a[sub_ri(0, slot)], &sub_b[sub_ri(0, slot)], &sub_k[sub_ri(0, slot)], sink, ctx);
   if (h->published) sink(ctx, "MESSAGE_STATS|messagesDeadlineCount|0");
+  return ZBHIP_OK;
+}
+
+// The message state of correlation slots (one owner per correlation key): the slots'
+// MESSAGE_SUBSCRIPTION rows as zbhip_export_state writes them, for the engine's state.
+int zbhip_export_correlation_slots(zbhip_handle* h, const uint32_t* slots, size_t n, zbhip_state_sink sink, void* ctx) {
+  if (!h || !sink || (n && !slots)) return ZBHIP_EINVAL;
+  if (!h->relabel_ok) return ZBHIP_ESTATE;
+  if (int rc = finalize(h)) return rc;
+  const size_t S = h->st.n_slots;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (size_t i = 0; i < n; ++i) {
+    if (slots[i] >= S) return ZBHIP_EINVAL;
+    uint4 a[kSubs];
+    longlong2 b[kSubs], k[kSubs];
+    const size_t r0 = sub_ri(0, slots[i]);
+    HIPCHK(hipMemcpy(a, h->st.sub_a + r0, sizeof a, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(b, h->st.sub_b + r0, sizeof b, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(k, h->st.sub_k + r0, sizeof k, hipMemcpyDeviceToHost));
+    emit_slot_rows(h, slots[i], a, b, k, sink, ctx);
+  }
+  return ZBHIP_OK;
+}
+
+int zbhip_export_correlation_slots_db(zbhip_handle* h, const uint32_t* slots, size_t n, zbhip_db_sink sink, void* ctx) {
+  if (!h || !sink) return ZBHIP_EINVAL;
+  DbExport e{h->ser, sink, ctx, ZBHIP_OK};
+  const int rc = zbhip_export_correlation_slots(h, slots, n, db_row, &e);
+  return rc ? rc : e.rc;
+}
+
+// The slots' MESSAGE_SUBSCRIPTION rows leave the device (after zbhip_export_correlation_slots put them into
+// the engine's state): zeroed rows are free rows.
+int zbhip_evict_correlation_slots(zbhip_handle* h, const uint32_t* slots, size_t n) {
+  if (!h || (n && !slots)) return ZBHIP_EINVAL;
+  const size_t S = h->st.n_slots;
+  for (size_t i = 0; i < n; ++i) {
+    if (slots[i] >= S) return ZBHIP_EINVAL;
+    const size_t r0 = sub_ri(0, slots[i]);
+    HIPCHK(hipMemsetAsync(h->st.sub_a + r0, 0, kSubs * sizeof(uint4), h->stream));
+    HIPCHK(hipMemsetAsync(h->st.sub_b + r0, 0, kSubs * sizeof(longlong2), h->stream));
+    HIPCHK(hipMemsetAsync(h->st.sub_k + r0, 0, kSubs * sizeof(longlong2), h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
   return ZBHIP_OK;
 }
 

@@ -324,6 +324,28 @@ class Partition:
         check(self.L.zbhip_export_instances_db(self.h, ids.ctypes.data, len(ids), cb, None), "zbhip_export_instances_db")
         return sorted(out)
 
+    # ---- one owner per correlation key (config 5, include/zbhip.h) ----
+    def export_correlation_slots(self, slots):
+        """The correlation slots' MESSAGE_SUBSCRIPTION rows (text, the export_state format)."""
+        rows = []
+        cb = STATE_SINK(lambda ctx, row: rows.append(row.decode()))
+        ids = np.ascontiguousarray(slots, dtype=np.uint32)
+        check(self.L.zbhip_export_correlation_slots(self.h, ids.ctypes.data, len(ids), cb, None),
+              "zbhip_export_correlation_slots")
+        return sorted(rows)
+
+    def export_correlation_slots_db(self, slots):
+        from .logwriter import _db_collector
+        out, cb = _db_collector()
+        ids = np.ascontiguousarray(slots, dtype=np.uint32)
+        check(self.L.zbhip_export_correlation_slots_db(self.h, ids.ctypes.data, len(ids), cb, None),
+              "zbhip_export_correlation_slots_db")
+        return sorted(out)
+
+    def evict_correlation_slots(self, slots):
+        ids = np.ascontiguousarray(slots, dtype=np.uint32)
+        check(self.L.zbhip_evict_correlation_slots(self.h, ids.ctypes.data, len(ids)), "zbhip_evict_correlation_slots")
+
     def evict_instances(self, instances):
         ids = np.ascontiguousarray(instances, dtype=np.uint32)
         check(self.L.zbhip_evict_instances(self.h, ids.ctypes.data, len(ids)), "zbhip_evict_instances")
