@@ -717,6 +717,15 @@ int zbhip_serialize_log(zbhip_serializer* s, const zbhip_record* recs, size_t n,
 int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_window* w, const void** dev_bytes, size_t* used);
 /* Copies n bytes of the last zbhip_serialize_log_device output into host memory. */
 int zbhip_log_device_copy(zbhip_handle* h, void* dst, size_t n);
+/* The log bytes into host memory without a wait (LogStorage.append's input on the host): the n bytes of the
+ * last zbhip_serialize_log_device output are copied on a copy stream of the handle, after the write, into a
+ * pinned buffer the handle owns; *host_bytes is where they land.  From the first call on the handle keeps two
+ * device output buffers and two pinned ones used in turn, so window k's bytes cross PCIe while window k+1 is
+ * submitted, run and serialised (the write of window k+2 waits for copy k).  The bytes are complete once
+ * zbhip_log_copy_wait(h, *host_bytes) returns and stay valid until the second next zbhip_log_copy_async
+ * (NULL waits for every pending copy). */
+int zbhip_log_copy_async(zbhip_handle* h, size_t n, const void** host_bytes);
+int zbhip_log_copy_wait(zbhip_handle* h, const void* host_bytes);
 
 /* ---- zb-db byte encoding of the state ---------------------------------------
  * The partition state as RocksDB entries: key = 8-byte big-endian ZbColumnFamilies ordinal +

@@ -261,3 +261,32 @@ def test_activated_job_completions_on_the_device(monkeypatch):
     recs = log.window(job_completions(recs, log.part))
     log.window(job_completions(recs, log.part))
     assert log.declined == 0
+
+
+def test_log_bytes_copied_asynchronously_into_pinned_buffers():
+    # zbhip_log_copy_async: window k's bytes cross PCIe into one of the handle's two pinned buffers while
+    # window k+1 is submitted, run and serialised into the other device buffer; once waited for they equal
+    # the host serialiser's bytes of window k (and stay valid until the second next copy)
+    n = 300
+    part = Partition(max_instances=n, max_commands=16 * n, max_records_per_batch=128)
+    part.deploy(bpmn.linear_process(4))
+    ser = part.log_serializer()
+    cmds, source_base, position, pending, landings = create_commands(n), 0, 100, None, []
+    for _ in range(5):
+        part.submit(cmds)
+        part.run(abi.RUN_DEVICE_RECORDS)
+        pos = position + 2 * np.arange(len(cmds), dtype=np.int64)
+        first = int(pos[-1]) + 1
+        _, used = part.serialize_log_device(pos, first, TS, copy=False)
+        landing = part.log_copy_async(used)
+        landings.append(landing)
+        recs = part.drain()
+        want = ser.serialize(recs, cmds, abi.make_docs(0), source_base, 0, pos, first, TS)
+        if pending is not None:
+            assert part.log_copy_wait(pending[0], pending[1]) == pending[2]
+        pending = (landing, used, want)
+        source_base += len(cmds)
+        position = first + len(recs)
+        cmds = job_completions(recs, part)
+    assert part.log_copy_wait(pending[0], pending[1]) == pending[2]
+    assert len(set(landings)) == 2 and landings[0] == landings[2] != landings[1]

@@ -1,0 +1,111 @@
+"""One owner per correlation key at the drop-in boundary (include/zbhip.h
+zbhip_export_correlation_slots / zbhip_evict_correlation_slots), on three partitions in the reference's
+processing loop with its scheduled tasks (tests/test_gpu_scheduled.py: DueDateTimerChecker, the pending-
+subscription checkers, MessageObserver's MessageTimeToLiveChecker).
+
+The device holds message subscriptions, never messages.  A publish with a time-to-live, a message id or a
+name no device catch event waits for is the engine's, and with it its correlation key: the key's
+subscriptions move from the device's correlation slot into the engine's state before the engine processes
+the publish (MessagePublishProcessor.java:83-185 correlates a publish to every open subscription of the key),
+and every later MESSAGE_SUBSCRIPTION command of the key is the engine's (MessageSubscriptionCreateProcessor
+.java:83-104 -> MessageCorrelator.correlateNextMessage correlates a buffered message when a subscription
+opens).  The workload mixes: messages with a time-to-live published before the subscriptions open and after,
+a duplicate message id, time-to-live 0 publishes the device takes, an engine-only process subscribing to the
+same message name on the same keys, and the TTL checker expiring what nobody took.  The bar: every
+partition's log and state equal the engine-only cluster's."""
+import pytest
+
+from psm import Client, Clock, InterPartitionCommandSender, Log
+from test_gpu_scheduled import KEY_A, KEY_B, Cluster, PartitionLoop, check
+from test_oracle_timers import NOW
+from zeebe_amd import abi, bpmn
+
+pytestmark = pytest.mark.gpu
+
+P = 3
+HOUR = 3600000
+DEVICE_XML = bpmn.message_catch_process(message_name="message", correlation_key="key", catch_id="receive-message")
+# an engine-only process (not deployed on the device) waiting for the same message name
+ENGINE_XML = (bpmn.createExecutableProcess("engineCatch").startEvent("start").serviceTask("task", "engine-task")
+              .intermediateCatchEvent("catch").message("message", "key").endEvent("end").done())
+KEYS = ["item-2", "item-1", "item-0"] + ["order-%d" % j for j in range(7)]
+
+
+def clusters():
+    def make(device):
+        clock = Clock(NOW)
+        logs = {p: Log() for p in range(1, P + 1)}
+        sender = InterPartitionCommandSender(logs)
+        deps = [(DEVICE_XML, KEY_A, 1), (ENGINE_XML, KEY_B, 1)]
+        parts = [PartitionLoop(clock, deps, deps[:1] if device else None, partition_id=p, partition_count=P,
+                               sender=sender, log=logs[p], correlation_keys=64) for p in range(1, P + 1)]
+        cl = Cluster(parts, clock)
+        cl.settle()
+        return cl
+    return make(False), make(True)
+
+
+def write(ref, gpu, per_partition):
+    for p, recs in sorted(per_partition.items()):
+        for cl in (ref, gpu):
+            Client(cl.parts[p - 1].log).write(*recs)
+    ref.settle()
+    gpu.settle()
+    check(ref, gpu)
+
+
+def publishes(cl, pairs):
+    from oracle.oracle import subscription_partition
+    out = {p: [] for p in range(1, P + 1)}
+    for k, kw in pairs:
+        out[subscription_partition(k, P)].append(Client.publish_message("message", k, timestamp=cl.clock.now, **kw))
+    return out
+
+
+def test_message_state_has_one_owner_per_correlation_key():
+    ref, gpu = clusters()
+    # 1. messages with a time-to-live before any subscription (buffered by the engine: those keys are the
+    # engine's from the start), one with a message id published twice (ALREADY_EXISTS)
+    early = [("order-0", dict(time_to_live=HOUR)), ("order-1", dict(time_to_live=HOUR, message_id="m-1")),
+             ("order-1", dict(time_to_live=HOUR, message_id="m-1")), ("order-2", dict(time_to_live=5000))]
+    write(ref, gpu, publishes(ref, early))
+    # 2. instances of the device process on every partition with every key, and of the engine-only process
+    # on some keys: their subscriptions open -- on the device for keys it owns, on the engine for the others
+    # (correlating the buffered messages: MESSAGE_SUBSCRIPTION:CORRELATING right after CREATED)
+    creates = {p: [] for p in range(1, P + 1)}
+    for i in range(30):
+        creates[1 + (i + i // 10) % 3].append(Client.create("process", (("key", KEYS[i % 10]),)))
+    for i, k in enumerate(KEYS[:6]):
+        creates[1 + i % 3].append(Client.create("engineCatch", (("key", k),)))
+    write(ref, gpu, creates)
+    # 3. time-to-live 0 publishes the device takes (its keys), then messages with a time-to-live and a message id
+    # on keys whose subscriptions the device holds: their state moves to the engine first
+    late = [(k, {}) for k in KEYS[3:]] + [("item-2", dict(time_to_live=HOUR)), ("item-1", dict(message_id="late-id")),
+                                          ("order-5", dict(time_to_live=HOUR)), ("order-6", {})]
+    write(ref, gpu, publishes(ref, late))
+    moved = sum(a.adapter.counts["keys_to_engine"] for a in gpu.parts)
+    assert moved >= 3
+    # 4. the engine-only instances' jobs complete: their catch events subscribe now (buffered messages
+    # correlate at once), more publishes, then the TTL checker expires what nobody took
+    for cl in (ref, gpu):
+        jobs = [r.key for p in cl.parts for r in p.log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_CREATED]
+        for p in cl.parts:
+            mine = [k for k in jobs if k >> 51 == p.engine.pbits >> 51]
+            Client(p.log).write(*[Client.complete_job(k) for k in mine])
+        cl.settle()
+    check(ref, gpu)
+    write(ref, gpu, publishes(ref, [(k, dict(time_to_live=HOUR)) for k in KEYS] + [(k, {}) for k in KEYS] * 2))
+    for _ in range(3):
+        for cl in (ref, gpu):
+            cl.increase_time(HOUR)
+        check(ref, gpu)
+    logs = [r for p in gpu.parts for r in p.log.entries]
+    assert [r for r in logs if r.value_type == abi.VT_MESSAGE_BATCH]  # the TTL checker expired buffered messages
+    assert [r for r in logs if r.record_type == abi.RT_REJECTION and r.rejection_type == abi.REJ_ALREADY_EXISTS]
+    assert [r for r in logs if r.value_type == abi.VT_MESSAGE_SUBSCRIPTION and r.intent == abi.MS_CORRELATING]
+    done = sum(1 for r in logs if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_COMPLETED
+               and r.value["bpmnElementType"] == "PROCESS")
+    assert done == 36
+    c = [p.adapter.counts for p in gpu.parts]
+    assert sum(x["device_commands"] for x in c) > 60, c
+    assert all(x["fallbacks"] == 0 for x in c), [p.adapter.fallback_reasons for p in gpu.parts]

@@ -685,6 +685,20 @@ struct zbhip_handle {
   unsigned long long* d_tbl_sums = nullptr;   // scan blocks of the device-built command table
   uint64_t* d_log_out = nullptr;
   size_t log_out_cap = 0;
+  // zbhip_log_copy_async: two device output buffers used in turn (window k's bytes stay put while they
+  // cross PCIe and window k+1 is written into the other one) and two pinned host buffers, the copies on a
+  // stream of their own ordered after the write by events
+  struct LogBuf {
+    uint64_t* dev = nullptr;
+    size_t dev_cap = 0;
+    char* host = nullptr;
+    size_t host_cap = 0;
+    hipEvent_t written = nullptr, copied = nullptr;
+    bool pending = false;  // a copy out of this buffer was queued and not yet waited for
+  } log_bufs[2];
+  int log_cur = 0;
+  bool log_double = false;
+  hipStream_t copy_stream = nullptr;
   uint32_t* d_log_flag = nullptr;
   uint32_t* d_log_rinfo = nullptr;  // [rows] per record: template / composed, entry bytes
   LogKeys* d_log_wkeys = nullptr;   // [max_commands] older keys per command (size pass -> write pass)
@@ -854,6 +868,7 @@ struct zbhip_handle {
 
 static int finalize(zbhip_handle* h);
 static int settle(zbhip_handle* h);
+static int log_next_buffer(zbhip_handle* h);
 static int resolve_guard(zbhip_handle* h);
 static int64_t intern_items(zbhip_handle* h, const zbhip_handle::Items& v);
 static int sync_lists(zbhip_handle* h);
@@ -1042,6 +1057,15 @@ void zbhip_close(zbhip_handle* h) {
   (void)hipFree(h->d_log_bytes);
   (void)hipFree(h->d_src_pos);
   (void)hipFree(h->d_tbl_sums);
+  if (h->log_double) (void)hipFree(h->log_bufs[h->log_cur ^ 1].dev);  // (the current one is d_log_out)
+  for (int b = 0; b < 2; ++b) {
+    auto& L = h->log_bufs[b];
+    if (L.pending && L.copied) (void)hipEventSynchronize(L.copied);
+    if (L.host) (void)hipHostFree(L.host);
+    if (L.written) (void)hipEventDestroy(L.written);
+    if (L.copied) (void)hipEventDestroy(L.copied);
+  }
+  if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   (void)hipFree(h->d_log_out);
   (void)hipFree(h->d_log_flag);
   (void)hipFree(h->d_log_rinfo);
@@ -5833,6 +5857,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
       HIPCHK(hipMemcpyAsync(h->d_src_pos, h->src_pos_pin, n * sizeof(long long), hipMemcpyHostToDevice, h->stream));
     }
     tu = now();
+    if (int rc = log_next_buffer(h)) return rc;
     HIPCHK(hipMemsetAsync(h->d_log_flag, 0, sizeof(uint32_t), h->stream));
     a.hdr = h->d_cmd_hdr;
     a.wcmds = reinterpret_cast<const zbhip_command*>(h->external ? h->ext_cmds : h->d_cmds);
@@ -5933,6 +5958,7 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
       }
     }
   }
+  if (int rc = log_next_buffer(h)) return rc;
   if (n) HIPCHK(hipMemcpyAsync(h->d_logcmd, h->h_logcmd.data(), n * sizeof(LogCmd), hipMemcpyHostToDevice, h->stream));
   if (h->inst_proc.size() >= N)
     HIPCHK(hipMemcpyAsync(h->d_inst_proc, h->inst_proc.data(), N * sizeof(uint16_t), hipMemcpyHostToDevice, h->stream));
@@ -5988,6 +6014,64 @@ extern "C" int zbhip_serialize_log_device(zbhip_handle* h, const zbhip_log_windo
             dev_table ? ms(tu, tf) : 0.0, dev_table ? ms(tf, t2) : 0.0, ms(t2, t3), ms(t3, t4));
   }
   return rc;
+}
+
+// Double-buffered log output (zbhip_log_copy_async): the window about to be written takes the other device
+// buffer; the stream waits for the copy still reading it (two windows back).
+static int log_next_buffer(zbhip_handle* h) {
+  if (!h->log_double) return ZBHIP_OK;
+  zbhip_handle::LogBuf& cur = h->log_bufs[h->log_cur];
+  cur.dev = h->d_log_out;
+  cur.dev_cap = h->log_out_cap;
+  h->log_cur ^= 1;
+  zbhip_handle::LogBuf& nxt = h->log_bufs[h->log_cur];
+  if (nxt.pending) HIPCHK(hipStreamWaitEvent(h->stream, nxt.copied, 0));
+  h->d_log_out = nxt.dev;
+  h->log_out_cap = nxt.dev_cap;
+  return ZBHIP_OK;
+}
+
+extern "C" int zbhip_log_copy_async(zbhip_handle* h, size_t n, const void** host_bytes) {
+  if (!h || !host_bytes) return ZBHIP_EINVAL;
+  *host_bytes = nullptr;
+  if (n > h->log_out_cap || (n && !h->d_log_out)) return ZBHIP_EINVAL;
+  if (!h->copy_stream) {
+    HIPCHK(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+    for (auto& L : h->log_bufs) {
+      HIPCHK(hipEventCreateWithFlags(&L.written, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&L.copied, hipEventDisableTiming));
+    }
+  }
+  zbhip_handle::LogBuf& L = h->log_bufs[h->log_cur];
+  if (L.host_cap < n) {  // (grown before its first use, or after its last copy was waited for)
+    if (L.pending) HIPCHK(hipEventSynchronize(L.copied));
+    L.pending = false;
+    if (L.host) (void)hipHostFree(L.host);
+    L.host = nullptr;
+    L.host_cap = 0;
+    const size_t cap = n + n / 8 + (1 << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&L.host), cap, hipHostMallocDefault) != hipSuccess) return ZBHIP_ENOMEM;
+    L.host_cap = cap;
+  }
+  HIPCHK(hipEventRecord(L.written, h->stream));
+  HIPCHK(hipStreamWaitEvent(h->copy_stream, L.written, 0));
+  if (n) HIPCHK(hipMemcpyAsync(L.host, h->d_log_out, n, hipMemcpyDeviceToHost, h->copy_stream));
+  HIPCHK(hipEventRecord(L.copied, h->copy_stream));
+  L.pending = true;
+  h->log_double = true;
+  *host_bytes = L.host;
+  return ZBHIP_OK;
+}
+
+extern "C" int zbhip_log_copy_wait(zbhip_handle* h, const void* host_bytes) {
+  if (!h) return ZBHIP_EINVAL;
+  for (auto& L : h->log_bufs)
+    if (host_bytes == nullptr || L.host == host_bytes) {
+      if (L.pending) HIPCHK(hipEventSynchronize(L.copied));
+      L.pending = false;
+      if (host_bytes) return ZBHIP_OK;
+    }
+  return host_bytes ? ZBHIP_EINVAL : ZBHIP_OK;
 }
 
 extern "C" int zbhip_log_device_copy(zbhip_handle* h, void* dst, size_t n) {

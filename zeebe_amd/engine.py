@@ -134,6 +134,18 @@ class Partition:
         check(self.L.zbhip_log_device_copy(self.h, out, used.value), "zbhip_log_device_copy")
         return out.raw[:used.value]
 
+    def log_copy_async(self, used):
+        """zbhip_log_copy_async: the last serialised window's `used` bytes on their way into the handle's
+        pinned buffer; returns the host address (complete after log_copy_wait(address))."""
+        ptr = C.c_void_p()
+        check(self.L.zbhip_log_copy_async(self.h, used, C.byref(ptr)), "zbhip_log_copy_async")
+        return ptr.value
+
+    def log_copy_wait(self, address=None, used=None):
+        """zbhip_log_copy_wait; with `used`, returns the bytes at `address`."""
+        check(self.L.zbhip_log_copy_wait(self.h, address), "zbhip_log_copy_wait")
+        return C.string_at(address, used) if used is not None else None
+
     def log_serializer(self):
         """The partition's log serialiser (follows its deployments and dictionaries)."""
         from .logwriter import LogSerializer

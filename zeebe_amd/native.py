@@ -29,7 +29,7 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_export_state_db", "zbhip_serializer_encode_state_row", "zbhip_outbox_device_async", "zbhip_stream",
            "zbhip_export_instances", "zbhip_export_instances_db", "zbhip_evict_instances", "zbhip_key_before",
            "zbhip_set_external_keys", "zbhip_export_correlation_slots", "zbhip_export_correlation_slots_db",
-           "zbhip_evict_correlation_slots", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
+           "zbhip_evict_correlation_slots", "zbhip_log_copy_async", "zbhip_log_copy_wait", "zbhip_serializer_decode_state_entry", "zbhip_import_state_db",
            "zbhip_import_state", "zbhip_activate_jobs", "zbhip_activatable_jobs", "zbhip_job_batch_rejection_reason",
            "zbhip_serialize_log_device", "zbhip_log_device_copy", "zbhip_continuations",
            "zbhip_pending_continuations", "zbhip_current_key", "zbhip_set_key_if_higher",
@@ -106,6 +106,8 @@ def load():
     L.zbhip_export_correlation_slots.argtypes = [vp, vp, sz, STATE_SINK, vp]
     L.zbhip_export_correlation_slots_db.argtypes = [vp, vp, sz, DB_SINK, vp]
     L.zbhip_evict_correlation_slots.argtypes = [vp, vp, sz]
+    L.zbhip_log_copy_async.argtypes = [vp, sz, C.POINTER(vp)]
+    L.zbhip_log_copy_wait.argtypes = [vp, vp]
     L.zbhip_evict_instances.argtypes = [vp, vp, sz]
     L.zbhip_key_before.argtypes = [vp, sz, C.POINTER(i64)]
     L.zbhip_continuations.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
