@@ -168,6 +168,10 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   private io.camunda.zeebe.engine.processing.timer.DueDateTimerChecker dueDateTimerChecker;
   private JobStreams jobStreams = new JobStreams(null);
   private io.camunda.zeebe.engine.state.immutable.JobState engineJobState; // the engine's (jobState(...))
+  // the engine's transient pending-subscription states: entries of subscriptions that move to the engine go
+  // there at once (its appliers clear them when its batches close the subscriptions)
+  io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState engineProcessTransient;
+  io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState engineMessageTransient;
 
   public GpuBatchProcessor(
       final Engine engine,
@@ -427,6 +431,12 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
         claimed++;
         window.addContinuation(event.getPosition(), rec, c.slot(), c.id());
       }
+      if (messages.enabled() && messages.ownsKeys() && !Messages.isSlotCommand(vt, rec)) {
+        // a correlation key of this partition is the engine's: a process-instance command may subscribe to
+        // it locally and fall back with engine keys, which a message window takes only after its last device
+        // key (zbhip_set_external_keys) -- such a command ends its window
+        break;
+      }
     }
     for (int k = 0; k < claimed; k++) {
       continuations.removeFirst();
@@ -554,6 +564,15 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     return ref < 0 ? -1 : (int) (ref >>> 16);
   }
 
+  /** Hands the device instance of process instance key {@code pik} to the engine (if the device holds it). */
+  void handOffInstanceOf(final long pik) {
+    final long ref = ZbHip.resolveKey(handle, pik);
+    if (ref >= 0) {
+      handOff((int) (ref >>> 16));
+      keyGenerator.setKeyIfHigher(ZbHip.currentKey(handle));
+    }
+  }
+
   private void handOff(final int instance) {
     if (handedOff.add(instance)) {
       // the instance's zb-db entries into RocksDB (the platform's transaction), then off the device
@@ -568,7 +587,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
       usedSlots.clear(instance);
       ended.remove(instance);
       if (messages != null && messages.enabled()) {
-        messages.handedOff(instance);
+        messages.handedOff(instance, engineProcessTransient);
       }
     }
   }
@@ -616,6 +635,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   public io.camunda.zeebe.engine.state.immutable.PendingProcessMessageSubscriptionState pendingProcessSubscriptionState(
       final io.camunda.zeebe.engine.state.immutable.PendingProcessMessageSubscriptionState engineState,
       final io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState engineTransient) {
+    engineProcessTransient = engineTransient;
     return new DeviceScheduledState.PendingProcessSubscriptions(this, engineState, engineTransient);
   }
 
@@ -627,6 +647,7 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   public io.camunda.zeebe.engine.state.immutable.PendingMessageSubscriptionState pendingMessageSubscriptionState(
       final io.camunda.zeebe.engine.state.immutable.PendingMessageSubscriptionState engineState,
       final io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState engineTransient) {
+    engineMessageTransient = engineTransient;
     return new DeviceScheduledState.PendingMessageSubscriptions(this, engineState, engineTransient);
   }
 

@@ -104,6 +104,16 @@ final class Messages {
     return correlationSlots > 0;
   }
 
+  /** Whether the engine owns a correlation key of this partition (toEngine ran). */
+  boolean ownsKeys() {
+    return !engineOwned.isEmpty();
+  }
+
+  /** A message-partition command (its subject a correlation slot, not an instance). */
+  static boolean isSlotCommand(final ValueType vt, final TypedRecord record) {
+    return vt == ValueType.MESSAGE || vt == ValueType.MESSAGE_SUBSCRIPTION;
+  }
+
   static boolean isMessageCommand(final ValueType vt) {
     return vt == ValueType.MESSAGE || vt == ValueType.MESSAGE_SUBSCRIPTION
         || vt == ValueType.PROCESS_MESSAGE_SUBSCRIPTION;
@@ -285,12 +295,19 @@ final class Messages {
    * closing row holds the slot, no routing handle points into it, their pending entries move.
    */
   void handedOff(final int slot) {
+    handedOff(slot, null);
+  }
+
+  void handedOff(final int slot, final io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState engine) {
     closingSlots.remove(slot);
     for (final var it = handles.entrySet().iterator(); it.hasNext(); ) {
       final var e = it.next();
       if (e.getValue() >= 0 && (int) (e.getValue() >>> 16) == slot) {
         final PendingProcessSubscription ps = pendingProcess.remove(e.getKey());
-        if (ps != null) {
+        if (ps != null && engine != null) {  // the engine's transient state now
+          engine.add(new io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState.PendingSubscription(
+              e.getKey().elementInstanceKey(), e.getKey().messageName(), ps.record.getTenantId()), ps.sentTime);
+        } else if (ps != null) {
           movedPending.add(Map.entry(e.getKey(), ps));
         }
         it.remove();
@@ -312,12 +329,32 @@ final class Messages {
     if (slot < 0 || slot >= correlationSlots) {
       return;
     }
+    // subscribers on this partition: the engine's correlations reach them as follow-ups of its own batches,
+    // so their instances go with the key (a later local subscription to the key falls back the same way)
+    final List<Long> local = new ArrayList<>();
+    for (final String row : ZbHip.exportCorrelationSlotRows(p.handle(), (int) slot)) {
+      if (row.startsWith("MESSAGE_SUBSCRIPTION_BY_KEY|")) {
+        final long pik = Long.parseLong(row.split("processInstanceKey=", 2)[1].split(",", 2)[0]);
+        if (Protocol.decodePartitionId(pik) == partitionId) {
+          local.add(pik);
+        }
+      }
+    }
     ZbHip.correlationSlotToEngine(p.handle(), (int) slot, rocksDb);
+    if (p.scheduledReady()) {
+      for (final long pik : local) {
+        p.handOffInstanceOf(pik);
+      }
+    }
     for (final var it = subscriptions.entrySet().iterator(); it.hasNext(); ) {
       final var e = it.next();
       if (e.getValue() == slot) {
         final PendingSubscription ps = pendingMessage.remove(e.getKey());
-        if (ps != null) {
+        if (ps != null && p.engineMessageTransient != null) {  // the engine's transient state now
+          p.engineMessageTransient.add(new io.camunda.zeebe.engine.state.message.TransientPendingSubscriptionState
+              .PendingSubscription(e.getKey().elementInstanceKey(), e.getKey().messageName(), ps.record.getTenantId()),
+              ps.sentTime);
+        } else if (ps != null) {
           movedPendingMessage.add(Map.entry(e.getKey(), ps));
         }
         it.remove();

@@ -210,6 +210,8 @@ public final class ZbHip {
   private static final MethodHandle EXPORT_INSTANCES_DB =
       fn("zbhip_export_instances_db", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle EVICT = fn("zbhip_evict_instances", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG));
+  private static final MethodHandle EXPORT_SLOTS =
+      fn("zbhip_export_correlation_slots", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle EXPORT_SLOTS_DB =
       fn("zbhip_export_correlation_slots_db", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, ADDRESS));
   private static final MethodHandle EVICT_SLOTS =
@@ -537,6 +539,17 @@ public final class ZbHip {
     }
   }
 
+  /** zbhip_export_correlation_slots of one slot: its MESSAGE_SUBSCRIPTION rows as text (the state export format). */
+  public static java.util.List<String> exportCorrelationSlotRows(final MemorySegment h, final int slot) {
+    final java.util.List<String> rows = new java.util.ArrayList<>();
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment ids = a.allocateArray(JAVA_INT, slot);
+      final MemorySegment stub = stateSinkStub(a, rows::add);
+      check((int) call(EXPORT_SLOTS, h, ids, 1L, stub, MemorySegment.NULL), "zbhip_export_correlation_slots");
+    }
+    return rows;
+  }
+
   /** DbKeyGenerator's value before window command i (the keys of everything before it are fixed). */
   public static long keyBefore(final MemorySegment h, final long i) {
     try (Arena a = Arena.ofConfined()) {
@@ -794,6 +807,29 @@ public final class ZbHip {
     } catch (final ReflectiveOperationException e) {
       throw new IllegalStateException(e);
     }
+  }
+
+  /** The zbhip_state_sink upcall: (ctx, NUL-terminated row). */
+  private static final FunctionDescriptor STATE_SINK = FunctionDescriptor.ofVoid(ADDRESS, ADDRESS);
+
+  private static MemorySegment stateSinkStub(final Arena a, final java.util.function.Consumer<String> rows) {
+    try {
+      final MethodHandle target =
+          MethodHandles.lookup()
+              .findStatic(ZbHip.class, "stateSinkTrampoline",
+                  MethodType.methodType(void.class, java.util.function.Consumer.class, MemorySegment.class,
+                      MemorySegment.class))
+              .bindTo(rows);
+      return LINKER.upcallStub(target, STATE_SINK, a);
+    } catch (final ReflectiveOperationException e) {
+      throw new IllegalStateException(e);
+    }
+  }
+
+  @SuppressWarnings({"unused", "unchecked"})
+  private static void stateSinkTrampoline(
+      final java.util.function.Consumer<String> rows, final MemorySegment ctx, final MemorySegment row) {
+    rows.accept(row.reinterpret(Long.MAX_VALUE).getUtf8String(0));
   }
 
   @SuppressWarnings("unused")

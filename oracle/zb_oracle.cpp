@@ -1682,6 +1682,26 @@ class Oracle {
             incident_pi_[L(r.at(1))] = L(r.at(2));
           } else if (cf == "INCIDENT_JOBS") {
             incident_jobs_[L(r.at(1))] = L(r.at(2));
+          } else if (cf == "PROCESS_SUBSCRIPTION_BY_KEY") {
+            // a handed-off instance's process message subscription [elementInstanceKey, messageName]
+            auto f = fields(r.at(3));
+            MsgVal m;
+            m.eik = L(r.at(1));
+            m.name = (uint16_t)intern(r.at(2));
+            m.pik = L(f.at("processInstanceKey"));
+            m.partition = (int32_t)L(f.at("subscriptionPartitionId"));
+            m.bpmn = (uint16_t)intern(f.at("bpmnProcessId"));
+            m.msg_key = L(f.at("messageKey"));
+            m.corr = (uint32_t)intern_string(f.at("correlationKey"));
+            m.interrupting = (uint8_t)L(f.at("interrupting"));
+            const ElementInstance& owner = ei_.at(m.eik);
+            if (!find_proc(procs[owner.value.proc].def_key, f.at("elementId"), m.proc, m.elem))
+              throw Unsupported{"subscription element " + f.at("elementId")};
+            m.inst = 0xFFFFFFFFu;  // (no instance slot of this engine's: routing handles are the device's)
+            PmsRow row{L(f.at("key")), f.at("state") == "OPENED", m};
+            row.closing = f.at("state") == "CLOSING";
+            pms_[{m.eik, (int)m.name}] = row;
+            ++pms_inst_[m.inst];
           } else if (cf == "MESSAGE_SUBSCRIPTION_BY_KEY") {
             // a message partition's subscriptions moved from the device (its correlation key's message
             // state goes to the engine): [elementInstanceKey, messageName] -> MessageSubscription

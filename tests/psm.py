@@ -610,8 +610,24 @@ class OracleEngine:
             self.o.set_key_counter(key - self.pbits)
 
     # RawDbWriter
-    def upsert(self, rows):
+    def upsert(self, rows, string_value=None):
+        """The rows of a hand-off into the engine's state.  The text rows name STRING variable values (and
+        list items) by the writer's value-dictionary ids; with `string_value` (the writer's id -> bytes)
+        they are re-interned into this engine's dictionary (zb-db bytes carry the strings themselves)."""
+        if string_value is not None:
+            rows = [self._reintern(r, string_value) if r.startswith("VARIABLES|") else r for r in rows]
         self.o.import_rows(rows)
+
+    def _reintern(self, row, string_value):
+        head, _, f = row.rpartition("|")
+        fields = dict(kv.split("=", 1) for kv in f.split(","))
+        mine = lambda i: str(self.o.intern_string(string_value(int(i))))  # noqa: E731
+        if fields["type"] == str(abi.DOC_STR):
+            fields["value"] = mine(fields["value"])
+        elif fields["type"] == str(abi.DOC_LIST) and fields["value"]:
+            fields["value"] = ";".join(t + ":" + (mine(v) if t == str(abi.DOC_STR) else v)
+                                       for t, v in (it.split(":", 1) for it in fields["value"].split(";")))
+        return head + "|" + ",".join("%s=%s" % kv for kv in fields.items())
 
     def state(self):
         return self.o.state()
@@ -838,6 +854,26 @@ class InterPartitionCommandSender:
 
     def send_command(self, receiver_partition, value_type, intent, value, key=-1):
         self.logs[receiver_partition].append([Rec(abi.RT_COMMAND, value_type, intent, key, value)])
+
+
+def canon_strings(rows, string_value):
+    """State rows with STRING variable values (and string list items) spelled out instead of value-
+    dictionary ids: each engine and each device interns strings in the order it meets them, so ids differ
+    between a cluster and its reference while the strings are the same.  `string_value`: id -> str."""
+    out = []
+    for r in rows:
+        if r.startswith("VARIABLES|"):
+            head, _, f = r.rpartition("|")
+            fields = dict(kv.split("=", 1) for kv in f.split(","))
+            sv = lambda i: "'" + string_value(int(i)) + "'"  # noqa: E731
+            if fields["type"] == str(abi.DOC_STR):
+                fields["value"] = sv(fields["value"])
+            elif fields["type"] == str(abi.DOC_LIST) and fields["value"]:
+                fields["value"] = ";".join(t + ":" + (sv(v) if t == str(abi.DOC_STR) else v)
+                                           for t, v in (it.split(":", 1) for it in fields["value"].split(";")))
+            r = head + "|" + ",".join("%s=%s" % kv for kv in fields.items())
+        out.append(r)
+    return out
 
 
 def run_cluster(processors):

@@ -108,4 +108,8 @@ def test_message_state_has_one_owner_per_correlation_key():
     assert done == 36
     c = [p.adapter.counts for p in gpu.parts]
     assert sum(x["device_commands"] for x in c) > 60, c
-    assert all(x["fallbacks"] == 0 for x in c), [p.adapter.fallback_reasons for p in gpu.parts]
+    # the only fallbacks: device instances subscribing on their own partition to a key the engine owns there
+    # (the engine's correlation reaches them as follow-ups of its batches: they go to the engine, FB_MESSAGE)
+    assert all(set(p.adapter.fallback_reasons) <= {"message"} for p in gpu.parts), \
+        [p.adapter.fallback_reasons for p in gpu.parts]
+    assert sum(x["fallbacks"] for x in c) <= 6

@@ -16,7 +16,7 @@ loop over the engine alone (tests/psm.py: the oracle engine, its own state views
 import numpy as np
 import pytest
 
-from psm import (Client, Clock, DueDateTimerChecker, EngineJobState, EngineMessageState, EngineTimerState,
+from psm import (Client, Clock, DueDateTimerChecker, canon_strings, EngineJobState, EngineMessageState, EngineTimerState,
                  InterPartitionCommandSender, JobTimeoutTrigger, Log, MessageTimeToLiveChecker, OracleEngine,
                  PendingMessageSubscriptionChecker,
                  PendingProcessMessageSubscriptionChecker, Rec, ScheduleService, StreamProcessor, open_jobs, run_cluster)
@@ -74,12 +74,13 @@ class PartitionLoop:
             PendingMessageSubscriptionChecker(pending, clock, sender, partition_id).on_recovered(self.service)
 
     def state(self):
-        eng = self.engine.state()
+        # (string variables spelled out: the engine's and the device's dictionaries intern in their own order)
+        eng = canon_strings(self.engine.state(), lambda i: self.engine.o.string_value(i).decode())
         if self.adapter is None:
             return sorted(eng)
         part = self.adapter.part
         assert part.current_key() <= self.engine.current_key()  # one key generator
-        rows = [r for r in part.state() if not r.startswith("KEY|")] + eng
+        rows = canon_strings([r for r in part.state() if not r.startswith("KEY|")], part.string_value) + eng
         # MESSAGE_STATS: one messagesDeadlineCount row, the buffered messages of both (the device's are 0)
         stats = [r for r in rows if r.startswith("MESSAGE_STATS|")]
         if len(stats) > 1:

@@ -377,6 +377,7 @@ class DevicePendingSubscriptionState:
 
     def __init__(self, adapter, engine):
         self.adapter, self.engine = adapter, engine
+        adapter.engine_pending = engine  # entries moved to the engine go there at once
 
     def pending_process_message_subscriptions(self, deadline):
         for sub, entry in self.adapter.moved_pending:  # handed-off instances: the engine's now
@@ -508,6 +509,7 @@ class GpuBatchProcessor:
         self.engine_owned = set()      # correlation keys whose message state the engine holds (one owner
                                        # per key: _message_state_to_engine)
         self.moved_pending_ms = []     # CORRELATING entries of subscriptions moved with their key
+        self.engine_pending = None     # the engine's transient pending states (DevicePendingSubscriptionState)
         self.part = None
         self.by_key, self.latest_by_id, self.by_index = {}, {}, []
         self.engine_job_types = set()  # job types the engine's processes (or handed-off instances) hold
@@ -844,6 +846,11 @@ class GpuBatchProcessor:
                 cid, slot, _ = self.continuations[claimed]
                 claimed += 1
                 self.window.put(rec, slot, abi.CMD_CONTINUE, 0, doc_begin=cid & 0xFFFFFFFF, pad=cid >> 32)
+            if self.engine_owned and self.window.cmds[-1]["kind"] not in abi.SLOT_KINDS:
+                # a correlation key of this partition is the engine's: a process-instance command may subscribe
+                # to it locally and fall back with engine keys, which a message window takes only after its
+                # last device key (zbhip_set_external_keys) -- such a command ends its window
+                break
         del self.continuations[:claimed]
         # keys the engine generated since the last window come first (setKeyIfHigher)
         self.part.set_key_if_higher(self.key_generator.current_key())
@@ -1062,12 +1069,26 @@ class GpuBatchProcessor:
             return  # (never a device slot)
         rows = self.part.export_correlation_slots([slot])
         if rows:
-            self.zeebe_db.upsert(rows)
-            self.part.evict_correlation_slots([slot])
+            self.zeebe_db.upsert(rows, self.part.string_value)
+        self.part.evict_correlation_slots([slot])  # (and the device declines the key's commands from now on)
         for sub in [k for k, s in self.subscriptions.items() if s == slot]:
             del self.subscriptions[sub]
             if sub in self.pending_ms:
-                self.moved_pending_ms.append((sub, self.pending_ms.pop(sub)))
+                if self.engine_pending is not None:  # the engine's transient state now (its appliers clear it)
+                    self.engine_pending.add_ms(sub, *self.pending_ms.pop(sub))
+                else:
+                    self.moved_pending_ms.append((sub, self.pending_ms.pop(sub)))
+        # subscribers on this partition: the engine's correlations reach them as follow-ups of its own
+        # batches (SubscriptionCommandSender: the own partition is a follow-up command), so their instances
+        # go with the key (a later local subscription to the key falls back and goes the same way)
+        if self._window_done:
+            for r in rows:
+                if r.startswith("MESSAGE_SUBSCRIPTION_BY_KEY|"):
+                    pik = int(r.split("processInstanceKey=", 1)[1].split(",", 1)[0])
+                    held = self._resolve(pik) if partition_of_key(pik) == self.partition_id else None
+                    if held is not None:
+                        self._hand_off(held[0])
+                        self.key_generator.set_key_if_higher(self.part.current_key())
         self.counts["keys_to_engine"] += 1
 
     def _fall_back(self, i, record, out):
@@ -1094,7 +1115,7 @@ class GpuBatchProcessor:
             # its jobs are the engine's now: activations of their types go there too
             self.engine_job_types.update(r.split("|")[2].split(",")[0][len("type="):] for r in rows
                                          if r.startswith("JOBS|"))
-            self.zeebe_db.upsert(rows)
+            self.zeebe_db.upsert(rows, self.part.string_value)
             self.part.evict_instances([inst])
             self.continuations = [c for c in self.continuations if c[1] != inst]
             self.used_slots.discard(inst)
@@ -1105,7 +1126,10 @@ class GpuBatchProcessor:
             for sub in [k for k, v in self.pms_handles.items() if v is not None and v[0] == inst]:
                 del self.pms_handles[sub]
                 if sub in self.pending_pms:
-                    self.moved_pending.append((sub, self.pending_pms.pop(sub)))
+                    if self.engine_pending is not None:
+                        self.engine_pending.add_pms(sub, *self.pending_pms.pop(sub))
+                    else:
+                        self.moved_pending.append((sub, self.pending_pms.pop(sub)))
 
     # ---- JOB:FAIL of a device job (JobFailProcessor.java:79-162) -------------------------------------
     def _fail_job(self, record, out):

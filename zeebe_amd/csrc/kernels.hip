@@ -1297,6 +1297,12 @@ __device__ __forceinline__ void subscribe_message(Lane<K>& L, uint32_t elem, uin
   }
 }
 
+// a correlation key whose message state the engine holds (zbhip_evict_correlation_slots: slot_hdr.x bit 31):
+// every message command of it -- a local follow-up of an instance's batch too -- is the engine's
+__device__ __forceinline__ bool engine_owned(const StepParams& P, uint32_t slot) {
+  return (P.st.slot_hdr[slot].x >> 31) != 0;
+}
+
 // a row of correlation slot `slot`: state != free, same subscriber (PI partition, instance, ord), same name
 template <class K>
 __device__ __forceinline__ int find_row(const Lane<K>& L, uint32_t slot, uint32_t pi_part, uint32_t inst, uint32_t eord,
@@ -1321,7 +1327,7 @@ __device__ __forceinline__ void ms_create(Lane<K>& L, uint32_t slot, uint32_t co
                                           uint32_t pi_part, uint32_t inst, uint32_t eord, long long eik,
                                           long long pik, long long eik_p, long long pik_p) {
   const StepParams& P = *L.sp;
-  if (slot >= P.st.n_slots) { set_fail(L, FB_MESSAGE); return; }
+  if (slot >= P.st.n_slots || engine_owned(P, slot)) { set_fail(L, FB_MESSAGE); return; }
   const bool dup = find_row(L, slot, pi_part, inst, eord, nb & 0xFFFF) >= 0;
   uint32_t key = NONE;
   if (!dup) {
@@ -1437,6 +1443,7 @@ template <class K>
 __device__ __forceinline__ void ms_correlate(Lane<K>& L, uint32_t slot, uint32_t pi_part, uint32_t inst, uint32_t eord,
                                              uint32_t nb, long long eik_p, long long pik_p) {
   const StepParams& P = *L.sp;
+  if (slot < P.st.n_slots && engine_owned(P, slot)) { set_fail(L, FB_MESSAGE); return; }
   const int r = slot < P.st.n_slots ? find_row(L, slot, pi_part, inst, eord, nb & 0xFFFF) : -1;
   if (r < 0) {
     emit_msg(L, kRejectBit | C_MS_CORRELATE, -1, eik_p, pik_p, -1, ZBHIP_NO_STRING, nb, 0, 1, kNoElem,
@@ -1504,7 +1511,7 @@ template <class K>
 __device__ __forceinline__ void ms_delete(Lane<K>& L, uint32_t slot, uint32_t pi_part, uint32_t inst, uint32_t eord,
                                           uint32_t nb, long long eik_p, long long pik_p, long long eik, long long pik) {
   const StepParams& P = *L.sp;
-  const int r = slot < P.st.n_slots ? find_row(L, slot, pi_part, inst, eord, nb & 0xFFFF) : -1;
+  const int r = slot < P.st.n_slots && !engine_owned(P, slot) ? find_row(L, slot, pi_part, inst, eord, nb & 0xFFFF) : -1;
   if (r < 0 || r == kSubs) { set_fail(L, FB_MESSAGE); return; }
   const size_t ri = sub_ri(r, slot);
   const uint4 a = P.st.sub_a[ri];
@@ -1558,7 +1565,7 @@ __device__ __forceinline__ unsigned long long eik_order(long long eik, uint32_t 
 template <class K>
 __device__ __forceinline__ void publish_message(Lane<K>& L, uint32_t slot, uint32_t name) {
   const StepParams& P = *L.sp;
-  if (slot >= P.st.n_slots) { set_fail(L, FB_MESSAGE); return; }
+  if (slot >= P.st.n_slots || engine_owned(P, slot)) { set_fail(L, FB_MESSAGE); return; }
   const uint32_t msg = new_slot_key(L);
   const uint32_t nb_msg = name | 0xFFFF0000u;
   emit_msg(L, C_MSG_PUBLISHED, sref(L, msg), -1, -1, -1, slot, nb_msg, 0, 0, kNoElem);

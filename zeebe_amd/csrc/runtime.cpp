@@ -4203,6 +4203,13 @@ int zbhip_evict_correlation_slots(zbhip_handle* h, const uint32_t* slots, size_t
     HIPCHK(hipMemsetAsync(h->st.sub_a + r0, 0, kSubs * sizeof(uint4), h->stream));
     HIPCHK(hipMemsetAsync(h->st.sub_b + r0, 0, kSubs * sizeof(longlong2), h->stream));
     HIPCHK(hipMemsetAsync(h->st.sub_k + r0, 0, kSubs * sizeof(longlong2), h->stream));
+    // slot_hdr.x bit 31: the engine owns the key -- the device declines its commands (local follow-ups
+    // of an instance's batch included: FB_MESSAGE), so the adapter hands such an instance to the engine
+    uint2 sh;
+    HIPCHK(hipMemcpyAsync(&sh, h->st.slot_hdr + slots[i], sizeof sh, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    sh.x |= 1u << 31;
+    HIPCHK(hipMemcpyAsync(h->st.slot_hdr + slots[i], &sh, sizeof sh, hipMemcpyHostToDevice, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
   return ZBHIP_OK;
@@ -4313,8 +4320,15 @@ int zbhip_set_external_keys(zbhip_handle* h, size_t i, uint32_t nkeys) {
   if (!h->results) return ZBHIP_ESTATE;
   if (i >= h->n_cmds || ((h->h_hdr[i].y >> 16) & 0xFF) == ST_OK) return ZBHIP_EINVAL;
   if (i < h->fin_next) return ZBHIP_ESTATE;  // the keys after it are fixed already
-  // config 5: the device key scan fixed this window's keys already (outbox, slot rows)
-  if (h->msg() && nkeys) return ZBHIP_EUNSUPP;
+  // config 5: the device key scan fixed this window's keys already (outbox, slot rows): the engine's keys
+  // can only come after the window's last device key -- no later command of the window generated one (the
+  // adapter runs a process-instance command last in its window when a fallback may take engine keys); the
+  // next window starts after them (zbhip_set_key_if_higher)
+  if (h->msg() && nkeys) {
+    for (size_t j = i + 1; j < h->n_cmds; ++j)
+      if (((h->h_hdr[j].y >> 16) & 0xFF) == ST_OK && (h->h_hdr[j].x >> 16) != 0) return ZBHIP_EUNSUPP;
+    return ZBHIP_OK;
+  }
   ensure_ext(h);
   h->ext_keys[i] = nkeys;
   h->declared[i] = 1;
