@@ -6050,7 +6050,12 @@ extern "C" int zbhip_log_copy_async(zbhip_handle* h, size_t n, const void** host
   *host_bytes = nullptr;
   if (n > h->log_out_cap || (n && !h->d_log_out)) return ZBHIP_EINVAL;
   if (!h->copy_stream) {
-    HIPCHK(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+    // a high-priority stream: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues round robin, and a copy
+    // stream sharing the compute stream's queue would run its blit behind the next window's kernels (measured:
+    // no overlap at all); priority streams come from a queue pool of their own
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&h->copy_stream, hipStreamNonBlocking, hi));
     for (auto& L : h->log_bufs) {
       HIPCHK(hipEventCreateWithFlags(&L.written, hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&L.copied, hipEventDisableTiming));
