@@ -144,6 +144,8 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
   private final int device;
   private final int correlationSlots; // config 5: correlation slots in HBM (0: messages stay with the engine)
   private final Set<String> messageNames = new HashSet<>();
+  // names of every deployed process's message start events: their publishes (and keys) are the engine's
+  private final Set<String> startMessageNames = new HashSet<>();
   private int partitionId;
   private InterPartitionCommandSender sender;
   private Messages messages;
@@ -215,13 +217,14 @@ public final class GpuBatchProcessor implements RecordProcessor, StreamProcessor
     for (final var d : deployments.all()) {
       deploy(d);
     }
-    messages = new Messages(partitionId, correlationSlots, messageNames);
+    messages = new Messages(partitionId, correlationSlots, messageNames, startMessageNames);
     window.init(arena);
     ctx.addLifecycleListeners(List.of(this));
   }
 
   private void deploy(final Deployments.DeployedResource d) {
     final ZbHip.Deployed p = ZbHip.deploy(handle, d.xml(), d.definitionKey(), d.version());
+    startMessageNames.addAll(JobTypes.messageStartNames(d.xml()));
     if (p == null) {
       // outside the device subset: its instances (and their job types) stay on the CPU engine
       engineJobTypes.addAll(JobTypes.of(d.xml()));

@@ -44,6 +44,37 @@ final class JobTypes {
     return out;
   }
 
+  // <startEvent ...><messageEventDefinition ... messageRef="..."> and <message id="..." name="...">
+  private static final Pattern START_REF = Pattern.compile(
+      "<(?:\\w+:)?startEvent\\b[^>]*>\\s*<(?:\\w+:)?messageEventDefinition\\b[^>]*?\\smessageRef=\"([^\"]*)\"");
+  private static final Pattern MESSAGE_ID_NAME =
+      Pattern.compile("<(?:\\w+:)?message\\b([^>]*)>");
+  private static final Pattern ATTR_ID = Pattern.compile("\\sid=\"([^\"]*)\"");
+  private static final Pattern ATTR_NAME = Pattern.compile("\\sname=\"([^\"]*)\"");
+
+  /**
+   * Message names of the message start events a BPMN XML declares: a publish of such a name starts
+   * instances (MessagePublishProcessor.correlateToMessageStartEvents, :157-180), so it is the engine's.
+   */
+  static Set<String> messageStartNames(final byte[] bpmnXml) {
+    final String xml = new String(bpmnXml, StandardCharsets.UTF_8);
+    final Set<String> refs = new HashSet<>();
+    final Matcher r = START_REF.matcher(xml);
+    while (r.find()) {
+      refs.add(r.group(1));
+    }
+    final Set<String> out = new HashSet<>();
+    final Matcher m = MESSAGE_ID_NAME.matcher(xml);
+    while (m.find()) {
+      final Matcher id = ATTR_ID.matcher(m.group(1));
+      final Matcher name = ATTR_NAME.matcher(m.group(1));
+      if (id.find() && name.find() && refs.contains(id.group(1))) {
+        out.add(name.group(1));
+      }
+    }
+    return out;
+  }
+
   /** The job type of a JOBS column-family value (JobRecordValue, DbJobState.java:112-157). */
   static String typeOfJobsValue(final byte[] value) {
     final JobRecordValue v = new JobRecordValue();

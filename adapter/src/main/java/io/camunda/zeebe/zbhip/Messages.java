@@ -64,6 +64,9 @@ final class Messages {
   private final int partitionId;
   private final int correlationSlots;
   private final Set<String> messageNames;
+  // message start event names of every deployment: a publish of such a name starts instances
+  // (MessagePublishProcessor.correlateToMessageStartEvents, :157-180), so it is the engine's
+  private final Set<String> startMessageNames;
   // MESSAGE_SUBSCRIPTION_BY_KEY [elementInstanceKey, messageName] -> correlation slot of an open
   // subscription: a MESSAGE_SUBSCRIPTION:CORRELATE's value carries no correlation key
   private final Map<SubscriptionKey, Integer> subscriptions = new HashMap<>();
@@ -94,10 +97,15 @@ final class Messages {
     final MessageSubscriptionRecord record = new MessageSubscriptionRecord();
   }
 
-  Messages(final int partitionId, final int correlationSlots, final Set<String> messageNames) {
+  Messages(
+      final int partitionId,
+      final int correlationSlots,
+      final Set<String> messageNames,
+      final Set<String> startMessageNames) {
     this.partitionId = partitionId;
     this.correlationSlots = correlationSlots;
     this.messageNames = messageNames;
+    this.startMessageNames = startMessageNames;
   }
 
   boolean enabled() {
@@ -121,7 +129,7 @@ final class Messages {
 
   /**
    * The device form of a message command, or null when the engine keeps it: a PUBLISH outside the
-   * subset, PROCESS_MESSAGE_SUBSCRIPTION commands of an instance the device does not hold,
+   * subset (or of a message start event's name), PROCESS_MESSAGE_SUBSCRIPTION commands of an instance the device does not hold,
    * MESSAGE_SUBSCRIPTION commands of a local instance the device does not hold.
    */
   DeviceCommand of(final TypedRecord record, final GpuBatchProcessor p, final Arena arena) {
@@ -129,7 +137,7 @@ final class Messages {
       final MessageRecord v = (MessageRecord) record.getValue();
       if (record.getIntent() != MessageIntent.PUBLISH || v.getTimeToLive() != 0 || !v.getMessageId().isEmpty()
           || v.getVariablesBuffer().capacity() > 1 || !messageNames.contains(v.getName())
-          || engineOwned.contains(v.getCorrelationKey())) {
+          || startMessageNames.contains(v.getName()) || engineOwned.contains(v.getCorrelationKey())) {
         return null;
       }
       final long corr = p.internString(v.getCorrelationKey().getBytes(StandardCharsets.UTF_8));

@@ -75,6 +75,7 @@ enum zbhip_value_type {
   ZBHIP_VT_MESSAGE = 10,
   ZBHIP_VT_MESSAGE_SUBSCRIPTION = 11,
   ZBHIP_VT_PROCESS_MESSAGE_SUBSCRIPTION = 12,
+  ZBHIP_VT_MESSAGE_START_EVENT_SUBSCRIPTION = 16,  /* engine-only: message start events stay with the CPU engine */
   ZBHIP_VT_VARIABLE = 17,
   ZBHIP_VT_PROCESS_INSTANCE_CREATION = 19,
   ZBHIP_VT_PROCESS_EVENT = 24,
@@ -131,6 +132,8 @@ enum { ZBHIP_MS_CREATE = 0, ZBHIP_MS_CREATED = 1, ZBHIP_MS_CORRELATE = 2, ZBHIP_
        ZBHIP_MS_CORRELATING = 8 };
 enum { ZBHIP_PMS_CREATING = 0, ZBHIP_PMS_CREATE = 1, ZBHIP_PMS_CREATED = 2, ZBHIP_PMS_CORRELATE = 3,
        ZBHIP_PMS_CORRELATED = 4, ZBHIP_PMS_DELETING = 5, ZBHIP_PMS_DELETE = 6, ZBHIP_PMS_DELETED = 7 };
+/* MessageStartEventSubscriptionIntent (protocol/.../intent/MessageStartEventSubscriptionIntent.java:19-21) */
+enum { ZBHIP_MSES_CREATED = 0, ZBHIP_MSES_CORRELATED = 1, ZBHIP_MSES_DELETED = 2 };
 
 /* BpmnElementType / BpmnEventType ordinals (protocol/.../value/BpmnElementType.java:24-58,
  * BpmnEventType.java:24-35) */

@@ -377,6 +377,8 @@ struct OProc {
   int version = 1;
   std::vector<OEl> els;  // [0] = process
   int none_start = -1;
+  std::vector<int> msg_starts;  // message start events of the process (ExecutableProcess.getStartEvents)
+  int bpmn_name = -1;           // the bpmnProcessId in the name dictionary (message start events)
 };
 
 // BpmnTransformer.transformDefinitions (deployment/model/transformation/BpmnTransformer.java:109-127)
@@ -696,13 +698,27 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
     if (n == "startEvent") {
       e.type = ZBHIP_EL_START_EVENT;
       // StartEventTransformer.java:40 — event type from the event definition
-      if (k->child("messageEventDefinition") || k->child("timerEventDefinition") ||
+      const XNode* med = k->child("messageEventDefinition");
+      if ((med && scope != 0) || k->child("timerEventDefinition") ||
           k->child("signalEventDefinition") || k->child("errorEventDefinition") ||
           k->child("escalationEventDefinition") || k->child("conditionalEventDefinition")) {
         err = "start event with event definition outside the supported subset";
         return false;
       }
       e.event = ZBHIP_EV_NONE;
+      if (med) {
+        // a message start event of the process (CatchEventTransformer.transformMessageEventDefinition:
+        // a static message name, no correlation key), opened as a MessageStartEventSubscription at deploy
+        auto mi = msgs.find(med->attr("messageRef"));
+        if (mi == msgs.end() || mi->second.first.empty()) {
+          err = "message start event outside the supported subset (static name)";
+          return false;
+        }
+        const XNode* ext = k->child("extensionElements");
+        if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+        e.event = ZBHIP_EV_MESSAGE;
+        e.msg_name = mi->second.first;
+      }
     } else if (n == "endEvent") {
       e.type = ZBHIP_EL_END_EVENT;
       if (k->child("terminateEventDefinition") || k->child("errorEventDefinition") ||
@@ -893,6 +909,8 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       if (P.els[self].start < 0) { err = "sub-process without a none start event"; return false; }
     } else if (type == ZBHIP_EL_START_EVENT && event == ZBHIP_EV_NONE) {
       P.els[scope].start = self;
+    } else if (type == ZBHIP_EL_START_EVENT) {
+      P.msg_starts.push_back(self);
     }
   }
   return true;
@@ -1296,8 +1314,34 @@ class Oracle {
         else if (M->type == ZBHIP_DOC_STR) M->value = intern_string(M->source);
         M->target_id = intern(M->target);
       }
+    std::set<std::string> start_names;
+    for (int s : P.msg_starts) {
+      if (!start_names.insert(P.els[s].msg_name).second) {
+        last_error = "two message start events with one message name";
+        return ZBHIP_EUNSUPP;
+      }
+      intern(P.els[s].msg_name);
+    }
+    if (!P.msg_starts.empty()) P.bpmn_name = intern(P.bpmn_id);
     procs.push_back(std::move(P));
+    open_start_event_subscriptions((int)procs.size() - 1);
     return (int)procs.size() - 1;
+  }
+
+  // StartEventSubscriptionManager.tryReOpenStartEventSubscription (processing/deployment/
+  // StartEventSubscriptionManager.java:46-140) for a deployed process that is the latest version of its
+  // bpmnProcessId: the previous versions' message start event subscriptions closed, its own opened
+  // (MessageStartEventSubscriptionCreatedApplier / DeletedApplier: DbMessageStartEventSubscriptionState
+  // .put / remove).  Deployment runs outside the processing loop here, so no CREATED / DELETED records
+  // are written, and a subscription's key stands at its process definition key.
+  void open_start_event_subscriptions(int proc) {
+    const OProc& p = procs[proc];
+    for (size_t i = 0; i < procs.size(); ++i)
+      if ((int)i != proc && procs[i].bpmn_id == p.bpmn_id && procs[i].version > p.version) return;
+    for (auto it = msg_start_subs_.begin(); it != msg_start_subs_.end();)
+      it = procs[it->second.proc].bpmn_id == p.bpmn_id ? msg_start_subs_.erase(it) : std::next(it);
+    for (int s : p.msg_starts)
+      msg_start_subs_[{intern(p.els[s].msg_name), p.def_key}] = MsgStartSub{proc, s, p.def_key};
   }
 
   void intern_vars(const FExpr* e) {
@@ -1886,6 +1930,14 @@ class Oracle {
   std::set<std::tuple<int, uint32_t, uint32_t>> msg_ids_;
   std::set<std::pair<int64_t, int>> msg_correlated_;
   int64_t msg_deadline_count_ = 0;
+  // message start events (DbMessageStartEventSubscriptionState: MESSAGE_START_EVENT_SUBSCRIPTION_BY_NAME_AND_KEY
+  // [[tenant, messageName], processDefinitionKey]) and the process-correlation-key locks of DbMessageState
+  // (MESSAGE_PROCESSES_ACTIVE_BY_CORRELATION_KEY [[bpmnProcessId, correlationKey]],
+  // MESSAGE_PROCESS_INSTANCE_CORRELATION_KEYS [processInstanceKey -> correlationKey])
+  struct MsgStartSub { int proc; int elem; int64_t key; };
+  std::map<std::pair<int, int64_t>, MsgStartSub> msg_start_subs_;
+  std::set<std::pair<int, uint32_t>> active_by_corr_;
+  std::map<int64_t, uint32_t> pi_corr_keys_;
 
   // --- batch context ---
   std::vector<ORecord>* batch_ = nullptr;
@@ -2442,6 +2494,18 @@ class Oracle {
       bpmn_seen.insert(sub.rec.bpmn);
       correlating.push_back(sub.rec);
     }
+    // correlateToMessageStartEvents (:157-180): the start event subscriptions of the name in process
+    // definition key order; one instance per process, and per correlation key while an instance the key
+    // created is active (an empty correlation key creates one every time)
+    const bool no_key = c.corr == ZBHIP_NO_STRING || str(c.corr).empty();
+    for (auto it = msg_start_subs_.lower_bound({(int)c.name, INT64_MIN});
+         it != msg_start_subs_.end() && it->first.first == (int)c.name; ++it) {
+      const MsgStartSub s = it->second;
+      const int bpmn = P(s.proc).bpmn_name;
+      if (bpmn_seen.count(bpmn) || (!no_key && active_by_corr_.count({bpmn, c.corr}))) continue;
+      bpmn_seen.insert(bpmn);
+      trigger_message_start_event(s, msgKey, c.name, c.corr);
+    }
     // sendCorrelateCommand: correlateProcessMessageSubscription with the message's name and key
     for (MsgVal m : correlating) {
       m.msg_key = msgKey;
@@ -2462,6 +2526,79 @@ class Oracle {
     const StoredMessage empty{0xFFFF, ZBHIP_NO_STRING, -1, -1, ZBHIP_NO_STRING};
     message_record(ZBHIP_MSG_EXPIRED, cmd.r.key, empty);
     remove_message(cmd.r.key);
+  }
+
+  // EventHandle.triggerMessageStartEvent (processing/common/EventHandle.java:176-235): a new process
+  // instance key; MESSAGE_START_EVENT_SUBSCRIPTION:CORRELATED (MessageStartEventSubscriptionCorrelatedApplier
+  // .java:27-39: putMessageCorrelation, and with a correlation key the lock [bpmnProcessId, correlationKey]
+  // and the instance's correlation key); PROCESS_EVENT:TRIGGERING of the start event in the process
+  // definition's event scope (ProcessEventTriggeringApplier -> triggerStartEvent); then
+  // PROCESS_INSTANCE:ACTIVATE_ELEMENT of the process (activateProcessInstanceForStartEvent)
+  void trigger_message_start_event(const MsgStartSub& s, int64_t msgKey, uint16_t name, uint32_t corr) {
+    const OProc& p = P(s.proc);
+    const int64_t piKey = next_key();
+    ORecord& r = append(ZBHIP_RT_EVENT, ZBHIP_VT_MESSAGE_START_EVENT_SUBSCRIPTION, ZBHIP_MSES_CORRELATED, s.key);
+    r.r.process_idx = s.proc;
+    r.r.element_idx = s.elem;
+    r.r.process_instance_key = piKey;
+    r.r.message_key = msgKey;
+    r.r.correlation_key = corr;
+    r.r.message_name = name;
+    r.r.bpmn_process_id = (uint16_t)p.bpmn_name;
+    msg_correlated_.insert({msgKey, p.bpmn_name});
+    if (corr != ZBHIP_NO_STRING && !str(corr).empty()) {
+      active_by_corr_.insert({p.bpmn_name, corr});
+      pi_corr_keys_[piKey] = corr;
+    }
+    const int64_t eventKey = next_key();
+    ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
+    pe.r.process_idx = s.proc;
+    pe.r.element_idx = s.elem;
+    pe.r.scope_key = p.def_key;
+    pe.r.process_instance_key = piKey;
+    triggers_[{p.def_key, eventKey}] = EventTrigger{s.elem, s.proc, Doc{0, 0}, piKey};
+    PiValue v;
+    v.proc = s.proc;
+    v.elem = 0;
+    v.flowScopeKey = -1;
+    v.piKey = piKey;
+    pi_command(piKey, ZBHIP_PI_ACTIVATE_ELEMENT, v);
+  }
+
+  // ProcessProcessor's post-transition action of a process with message start events (ProcessProcessor
+  // .java:196-206) -> BpmnBufferedMessageStartEventBehavior.correlateMessage (:56-120): after an instance a
+  // message created with a correlation key ended (its lock released by the applier), the first buffered
+  // message of that key for the latest version's start events -- by message key over the subscriptions,
+  // visited in message-name order -- that is not expired and not yet correlated to the process starts the
+  // next instance
+  void correlate_buffered_start_message(int proc, uint32_t corr) {
+    int latest = proc;
+    for (size_t i = 0; i < procs.size(); ++i)
+      if (procs[i].bpmn_id == P(proc).bpmn_id && procs[i].version > P(latest).version) latest = (int)i;
+    const OProc& p = P(latest);
+    std::vector<std::pair<std::string, MsgStartSub>> subs;  // [processDefinitionKey, [tenant, messageName]] order
+    for (auto& [k, s] : msg_start_subs_)
+      if (s.proc == latest) subs.push_back({names.at(k.first), s});
+    std::sort(subs.begin(), subs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    int64_t best = INT64_MAX;
+    const MsgStartSub* chosen = nullptr;
+    uint16_t chosen_name = 0;
+    for (auto& [nm, s] : subs) {
+      const int name = (int)name_ids.at(nm);
+      for (auto it = msg_by_corr_.lower_bound({name, corr, INT64_MIN});
+           it != msg_by_corr_.end() && std::get<0>(*it) == name && std::get<1>(*it) == corr; ++it) {
+        const int64_t mk = std::get<2>(*it);
+        if (messages_.at(mk).deadline > now_ms && !msg_correlated_.count({mk, p.bpmn_name})) {
+          if (mk < best) {
+            best = mk;
+            chosen = &s;
+            chosen_name = (uint16_t)name;
+          }
+          break;
+        }
+      }
+    }
+    if (chosen) trigger_message_start_event(*chosen, best, chosen_name, corr);
   }
 
   // ProcessMessageSubscriptionCorrelateProcessor.processRecord
@@ -3161,6 +3298,17 @@ class Oracle {
       case ZBHIP_EL_PROCESS: {  // ProcessProcessor.onActivate (processing/bpmn/container/ProcessProcessor.java:55-61,119-128)
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         const OProc& p = P(v.proc);
+        if (!p.msg_starts.empty()) {
+          // activateStartEvent (:98-114): the process definition's first event trigger, if it is this
+          // instance's, activates its start event (BpmnEventSubscriptionBehavior.activateTriggeredStartEvent)
+          auto tit = triggers_.lower_bound({p.def_key, INT64_MIN});
+          if (tit != triggers_.end() && tit->first.first == p.def_key &&
+              (tit->second.piKey == v.piKey || tit->second.piKey == -1)) {
+            activate_triggered_event(tit->first.second, tit->second.elem, p.def_key, key, v);
+            break;
+          }
+        }
+        if (p.none_start < 0) throw Unsupported{"process without a none start event activated without a trigger"};
         PiValue c = v;  // activateChildInstance (BpmnStateTransitionBehavior.java:279-290)
         c.flowScopeKey = key;
         c.elem = p.none_start;
@@ -3288,9 +3436,16 @@ class Oracle {
 
   void on_complete(const OEl& el, int64_t key, const PiValue& v) {
     switch (el.type) {
-      case ZBHIP_EL_PROCESS:  // ProcessProcessor.onComplete (:63-76): never end of path
+      case ZBHIP_EL_PROCESS: {  // ProcessProcessor.onComplete (:63-76): never end of path
+        // getPostTransitionAction (:186-206): the correlation key read before the transition (the
+        // applier releases the lock), the next buffered message correlated after it
+        auto cit = P(v.proc).msg_starts.empty() ? pi_corr_keys_.end() : pi_corr_keys_.find(v.piKey);
+        const bool by_message = cit != pi_corr_keys_.end();
+        const uint32_t corr = by_message ? cit->second : ZBHIP_NO_STRING;
         pi_event(key, ZBHIP_PI_ELEMENT_COMPLETED, v);
+        if (by_message) correlate_buffered_start_message(v.proc, corr);
         break;
+      }
       case ZBHIP_EL_START_EVENT:  // StartEventProcessor.onComplete (:52-67): applyOutputMappings,
         // subscribeToEvents of the flow scope (a sub-process's boundary timer), transitionToCompleted
         complete_and_take(el, key, v, true, false, /*subscribe_scope=*/true);
@@ -3858,6 +4013,14 @@ class Oracle {
         for (auto tit = taken_.lower_bound({key, INT32_MIN, INT32_MIN}); tit != taken_.end() && std::get<0>(tit->first) == key;)
           tit = taken_.erase(tit);
         if (el.type == ZBHIP_EL_PROCESS) pi_by_def_.erase({P(v.proc).def_key, key});
+        if (el.type == ZBHIP_EL_PROCESS && !P(v.proc).msg_starts.empty()) {
+          // BufferedStartMessageEventStateApplier.removeMessageLock (:36-66)
+          auto cit = pi_corr_keys_.find(v.piKey);
+          if (cit != pi_corr_keys_.end()) {
+            active_by_corr_.erase({P(v.proc).bpmn_name, cit->second});
+            pi_corr_keys_.erase(cit);
+          }
+        }
         if (parent > 0) {
           ElementInstance& pe = ei_.at(parent);
           pe.childCount -= 1;
@@ -4054,6 +4217,18 @@ std::string Oracle::dump_state() const {
   }
   for (auto& [d, k] : msg_deadlines_) rows.push_back("MESSAGE_DEADLINES|" + std::to_string(d) + "|" + std::to_string(k));
   for (auto& [k, b] : msg_correlated_) rows.push_back("MESSAGE_CORRELATED|" + std::to_string(k) + "|" + nm(b));
+  for (auto& [k, s] : msg_start_subs_) {  // DbMessageStartEventSubscriptionState's two column families
+    const OProc& p = procs[s.proc];
+    rows.push_back("MESSAGE_START_EVENT_SUBSCRIPTION_BY_NAME_AND_KEY|<default>|" + std::string(nm(k.first)) + "|" +
+                   std::to_string(k.second) + "|key=" + std::to_string(s.key) + ",bpmnProcessId=" + p.bpmn_id +
+                   ",startEventId=" + p.els[s.elem].id);
+    rows.push_back("MESSAGE_START_EVENT_SUBSCRIPTION_BY_KEY_AND_NAME|" + std::to_string(k.second) + "|<default>|" +
+                   nm(k.first));
+  }
+  for (auto& [b, c] : active_by_corr_)
+    rows.push_back("MESSAGE_PROCESSES_ACTIVE_BY_CORRELATION_KEY|" + std::string(nm(b)) + "|" + sv(c));
+  for (auto& [pk, c] : pi_corr_keys_)
+    rows.push_back("MESSAGE_PROCESS_INSTANCE_CORRELATION_KEYS|" + std::to_string(pk) + "|" + sv(c));
   if (msg_stats_) rows.push_back("MESSAGE_STATS|messagesDeadlineCount|" + std::to_string(msg_deadline_count_));
   std::sort(rows.begin(), rows.end());
   std::string s;

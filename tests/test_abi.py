@@ -92,7 +92,8 @@ def test_java_adapter_binds_exported_symbols():
 # drained rows against ValueType.value(), so the header, the Python mirror and the oracle must use the
 # protocol's numbers (a push row with JOB_BATCH = 1 would fall into the adapter's default branch)
 PROTOCOL_VALUE_TYPES = {"JOB": 0, "PROCESS_INSTANCE": 5, "INCIDENT": 6, "MESSAGE": 10, "MESSAGE_SUBSCRIPTION": 11,
-                        "PROCESS_MESSAGE_SUBSCRIPTION": 12, "JOB_BATCH": 14, "TIMER": 15, "VARIABLE": 17,
+                        "PROCESS_MESSAGE_SUBSCRIPTION": 12, "JOB_BATCH": 14, "TIMER": 15,
+                        "MESSAGE_START_EVENT_SUBSCRIPTION": 16, "VARIABLE": 17,
                         "PROCESS_INSTANCE_CREATION": 19, "PROCESS_EVENT": 24, "PROCESS_INSTANCE_BATCH": 34}
 
 

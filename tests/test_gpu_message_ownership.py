@@ -16,7 +16,7 @@ partition's log and state equal the engine-only cluster's."""
 import pytest
 
 from psm import Client, Clock, InterPartitionCommandSender, Log
-from test_gpu_scheduled import KEY_A, KEY_B, Cluster, PartitionLoop, check
+from test_gpu_scheduled import KEY_A, KEY_B, KEY_C, Cluster, PartitionLoop, check
 from test_oracle_timers import NOW
 from zeebe_amd import abi, bpmn
 
@@ -31,12 +31,17 @@ ENGINE_XML = (bpmn.createExecutableProcess("engineCatch").startEvent("start").se
 KEYS = ["item-2", "item-1", "item-0"] + ["order-%d" % j for j in range(7)]
 
 
-def clusters():
+# an engine-only process started by the same message name (MessagePublishProcessor.correlateToMessageStartEvents)
+STARTER_XML = (bpmn.createExecutableProcess("starter").startEvent("start").message("message")
+               .serviceTask("task", "starter-task").endEvent("end").done())
+
+
+def clusters(extra=()):
     def make(device):
         clock = Clock(NOW)
         logs = {p: Log() for p in range(1, P + 1)}
         sender = InterPartitionCommandSender(logs)
-        deps = [(DEVICE_XML, KEY_A, 1), (ENGINE_XML, KEY_B, 1)]
+        deps = [(DEVICE_XML, KEY_A, 1), (ENGINE_XML, KEY_B, 1)] + list(extra)
         parts = [PartitionLoop(clock, deps, deps[:1] if device else None, partition_id=p, partition_count=P,
                                sender=sender, log=logs[p], correlation_keys=64) for p in range(1, P + 1)]
         cl = Cluster(parts, clock)
@@ -113,3 +118,51 @@ def test_message_state_has_one_owner_per_correlation_key():
     assert all(set(p.adapter.fallback_reasons) <= {"message"} for p in gpu.parts), \
         [p.adapter.fallback_reasons for p in gpu.parts]
     assert sum(x["fallbacks"] for x in c) <= 6
+
+
+def complete_jobs(ref, gpu, job_type):
+    for cl in (ref, gpu):
+        for p in cl.parts:
+            done = {r.key for r in p.log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_COMPLETED}
+            open_ = [r.key for r in p.log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_CREATED
+                     and r.value["type"] == job_type and r.key not in done]
+            Client(p.log).write(*[Client.complete_job(k) for k in open_])
+        cl.settle()
+    check(ref, gpu)
+
+
+def test_message_start_event_takes_the_name_to_the_engine():
+    """A message start event of the name the device's catch events wait for: every publish of the name is the
+    engine's (it starts instances, MessagePublishProcessor.java:157-180), so each key's subscriptions move
+    from the device before its first publish; the engine correlates the publish to them and starts the
+    starter process, one instance per correlation key while it runs (the lock), the buffered messages starting
+    the next ones when the instances complete (BpmnBufferedMessageStartEventBehavior)."""
+    ref, gpu = clusters([(STARTER_XML, KEY_C, 1)])
+    creates = {p: [] for p in range(1, P + 1)}
+    for i in range(24):
+        creates[1 + (i + i // 10) % 3].append(Client.create("process", (("key", KEYS[i % 10]),)))
+    write(ref, gpu, creates)
+    assert sum(x["device_commands"] for x in (p.adapter.counts for p in gpu.parts)) > 0
+    # time-to-live 0 on every key (the device would take these without the start event), then messages with a
+    # time-to-live on some keys while their starter instances run (buffered: the lock), one with an id
+    write(ref, gpu, publishes(ref, [(k, {}) for k in KEYS]))
+    assert sum(a.adapter.counts["keys_to_engine"] for a in gpu.parts) >= 6
+    write(ref, gpu, publishes(ref, [(k, dict(time_to_live=HOUR)) for k in KEYS[:6]] +
+                              [("order-3", dict(time_to_live=HOUR, message_id="s-1"))] +
+                              [(k, {}) for k in KEYS[6:]]))
+    # the starter tasks complete: the buffered messages start the next instances (and correlate to the
+    # device process's later subscriptions); more instances subscribe on engine-owned keys
+    complete_jobs(ref, gpu, "starter-task")
+    write(ref, gpu, {1: [Client.create("process", (("key", k),)) for k in KEYS[:5]]})
+    complete_jobs(ref, gpu, "starter-task")
+    for _ in range(2):
+        for cl in (ref, gpu):
+            cl.increase_time(HOUR)
+        check(ref, gpu)
+    logs = [r for p in gpu.parts for r in p.log.entries]
+    started = [r for r in logs if r.value_type == abi.VT_MESSAGE_START_EVENT_SUBSCRIPTION and r.intent == abi.MSES_CORRELATED]
+    assert len(started) >= 15
+    assert [r for r in logs if r.value_type == abi.VT_MESSAGE_SUBSCRIPTION and r.intent == abi.MS_CORRELATING]
+    assert [r for r in logs if r.value_type == abi.VT_PROCESS_MESSAGE_SUBSCRIPTION and r.intent == abi.PMS_CORRELATED]
+    assert all(set(p.adapter.fallback_reasons) <= {"message"} for p in gpu.parts), \
+        [p.adapter.fallback_reasons for p in gpu.parts]

@@ -16,6 +16,7 @@ VT_PROCESS_INSTANCE = 5
 VT_MESSAGE = 10
 VT_MESSAGE_SUBSCRIPTION = 11
 VT_PROCESS_MESSAGE_SUBSCRIPTION = 12
+VT_MESSAGE_START_EVENT_SUBSCRIPTION = 16  # engine-only (message start events stay with the CPU engine)
 VT_VARIABLE = 17
 VT_PROCESS_INSTANCE_CREATION = 19
 VT_PROCESS_EVENT = 24
@@ -65,9 +66,12 @@ MS_CREATE, MS_CREATED, MS_CORRELATE, MS_CORRELATED, MS_CORRELATING = 0, 1, 2, 3,
 MS_DELETE, MS_DELETED = 6, 7
 PMS_CREATING, PMS_CREATE, PMS_CREATED, PMS_CORRELATE, PMS_CORRELATED = 0, 1, 2, 3, 4
 PMS_DELETING, PMS_DELETE, PMS_DELETED = 5, 6, 7
+MSES_INTENTS = {0: "CREATED", 1: "CORRELATED", 2: "DELETED"}  # MessageStartEventSubscriptionIntent
+MSES_CREATED, MSES_CORRELATED, MSES_DELETED = 0, 1, 2
 VALUE_TYPES = {0: "JOB", 5: "PROCESS_INSTANCE", 10: "MESSAGE", 11: "MESSAGE_SUBSCRIPTION",
                12: "PROCESS_MESSAGE_SUBSCRIPTION", 17: "VARIABLE", 19: "PROCESS_INSTANCE_CREATION",
-               24: "PROCESS_EVENT", 15: "TIMER", 34: "PROCESS_INSTANCE_BATCH"}
+               24: "PROCESS_EVENT", 15: "TIMER", 34: "PROCESS_INSTANCE_BATCH",
+               16: "MESSAGE_START_EVENT_SUBSCRIPTION"}
 RECORD_TYPES = {0: "EVENT", 1: "COMMAND", 2: "COMMAND_REJECTION"}
 REJECTION_TYPES = {0: "INVALID_ARGUMENT", 1: "NOT_FOUND", 2: "ALREADY_EXISTS", 3: "INVALID_STATE",
                    4: "PROCESSING_ERROR", 255: "NULL_VAL"}
@@ -84,7 +88,8 @@ def intent_name(value_type, intent):
     table = {VT_PROCESS_INSTANCE: PI_INTENTS, VT_JOB: JOB_INTENTS, VT_VARIABLE: VAR_INTENTS,
              VT_PROCESS_EVENT: PE_INTENTS, VT_PROCESS_INSTANCE_CREATION: PIC_INTENTS, VT_MESSAGE: MSG_INTENTS,
              VT_MESSAGE_SUBSCRIPTION: MS_INTENTS, VT_PROCESS_MESSAGE_SUBSCRIPTION: PMS_INTENTS,
-             VT_TIMER: TIMER_INTENTS, VT_PROCESS_INSTANCE_BATCH: PIB_INTENTS}.get(value_type, {})
+             VT_TIMER: TIMER_INTENTS, VT_PROCESS_INSTANCE_BATCH: PIB_INTENTS,
+             VT_MESSAGE_START_EVENT_SUBSCRIPTION: MSES_INTENTS}.get(value_type, {})
     return table.get(intent, str(intent))
 
 

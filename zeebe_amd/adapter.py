@@ -241,6 +241,15 @@ class RecordValues:
             return {"bpmnProcessId": p.bpmn_process_id, "processDefinitionKey": p.definition_key,
                     "version": p.version, "processInstanceKey": scope, "variables": tuple(command_doc),
                     "tenantId": TENANT}
+        if vt == abi.VT_MESSAGE_START_EVENT_SUBSCRIPTION:
+            # MessageStartEventSubscriptionRecord.java:26-48 (the engine's records: message start events are
+            # outside the device subset)
+            nid, cid = int(r["message_name"]), int(r["correlation_key"])
+            return {"processDefinitionKey": p.definition_key, "messageName": self.name(nid) if nid != 0xFFFF else "",
+                    "startEventId": p.element_ids[elem], "bpmnProcessId": p.bpmn_process_id,
+                    "processInstanceKey": pik, "messageKey": int(r["message_key"]),
+                    "correlationKey": self.string_value(cid) if cid != abi.NO_STRING else "", "variables": (),
+                    "tenantId": TENANT}
         if vt in MESSAGE_VALUE_TYPES:
             # the drained record carries every property of the reference value (logwriter.cpp: the
             # same fields); message variables are empty in the subset, deadline = the PUBLISH
@@ -503,6 +512,9 @@ class GpuBatchProcessor:
         self.correlation_keys = correlation_keys
         self.command_sender = command_sender
         self.message_names = set()     # message names of the device's catch events (PUBLISH subset)
+        # message names of any deployed process's message start events: a publish of such a name is the
+        # engine's (MessagePublishProcessor.correlateToMessageStartEvents, :157-180), and so its key
+        self.start_message_names = set()
         self.subscriptions = {}        # (elementInstanceKey, messageName) -> correlation slot of an open
                                        # MESSAGE_SUBSCRIPTION (MESSAGE_SUBSCRIPTION_BY_KEY): a CORRELATE's
                                        # value carries no correlation key
@@ -517,6 +529,7 @@ class GpuBatchProcessor:
         from .bpmn import job_types_of
         for xml, _, _ in engine_deployments:
             self.engine_job_types.update(job_types_of(xml))
+            self.on_engine_deployment(xml)
         self.used_slots = set()
         self.ended = set()             # ended instances whose slot waits for their continuations
         self.closing = set()           # instance slots with a closing process message subscription
@@ -566,18 +579,26 @@ class GpuBatchProcessor:
             # outside the device subset: its instances (and job types) run on the CPU engine
             from .bpmn import job_types_of
             self.engine_job_types.update(job_types_of(xml))
+            self.on_engine_deployment(xml)
             self.by_index.append(None)
             return None
         p = self.part.processes[idx]
-        from .bpmn import job_types_of, message_names_of
+        from .bpmn import job_types_of, message_names_of, message_start_names_of
         self.device_job_types.update(job_types_of(xml))
         self.message_names.update(message_names_of(xml))
+        self.start_message_names.update(message_start_names_of(xml))
         self.by_key[key] = p
         self.by_index.append(p)
         prev = self.latest_by_id.get(p.bpmn_process_id)
         if prev is None or prev.version < version:
             self.latest_by_id[p.bpmn_process_id] = p
         return p
+
+    def on_engine_deployment(self, xml):
+        """A process the engine holds (the device refused it, or the host deployed it there): its message
+        start events' names go to the engine from now on."""
+        from .bpmn import message_start_names_of
+        self.start_message_names.update(message_start_names_of(xml))
 
     def accepts(self, value_type):
         return value_type in (abi.VT_PROCESS_INSTANCE_CREATION, abi.VT_JOB, abi.VT_TIMER, VT_JOB_BATCH) \
@@ -711,14 +732,15 @@ class GpuBatchProcessor:
     def _message_command(self, record):
         """A message command of the log as (zbhip_command row, zbhip_xpart_cmd row or None), or None
         when the device does not take it: PUBLISH outside the subset (a time-to-live, a message id,
-        variables, a name no device catch event waits for), PROCESS_MESSAGE_SUBSCRIPTION commands of an
+        variables, a name no device catch event waits for, a name of a message start event: the engine
+        starts those instances), PROCESS_MESSAGE_SUBSCRIPTION commands of an
         instance the device does not hold, MESSAGE_SUBSCRIPTION commands of a local instance the
         device does not hold."""
         v, vt, it = record.value, record.value_type, record.intent
         if vt == abi.VT_MESSAGE:
             if it != abi.MSG_PUBLISH or v.get("timeToLive", 0) != 0 or v.get("messageId") or v.get("variables") \
-                    or v.get("name") not in self.message_names or not isinstance(v.get("correlationKey"), str) \
-                    or v["correlationKey"] in self.engine_owned:
+                    or v.get("name") not in self.message_names or v.get("name") in self.start_message_names \
+                    or not isinstance(v.get("correlationKey"), str) or v["correlationKey"] in self.engine_owned:
                 return None
             corr = self.part.intern_string(v["correlationKey"])
             if corr >= self.correlation_keys:

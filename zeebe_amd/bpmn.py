@@ -117,10 +117,12 @@ class ProcessBuilder:
         self._add_node("intermediateCatchEvent", id_)
         return self
 
-    def message(self, name, correlation_key):
+    def message(self, name, correlation_key=None):
         """IntermediateCatchEventBuilder.message(m -> m.name(name).zeebeCorrelationKeyExpression(key)):
-        a <message> with a zeebe:subscription under the definitions (ZeebeExpression: "=" prefix)."""
-        expr = correlation_key if correlation_key.startswith("=") else "=" + correlation_key
+        a <message> with a zeebe:subscription under the definitions (ZeebeExpression: "=" prefix);
+        StartEventBuilder.message(name): a message start event, no correlation key."""
+        expr = None if correlation_key is None else \
+            correlation_key if correlation_key.startswith("=") else "=" + correlation_key
         self.current.message = ("Message_%s" % self.current.id, name, expr)
         return self
 
@@ -293,6 +295,10 @@ class ProcessBuilder:
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
                                '</intermediateCatchEvent>' % (ind, quoteattr(c.id), quoteattr(c.id + "_med"),
                                                               quoteattr(c.message[0])))
+                elif c.kind == "startEvent" and c.message:
+                    catches.append(c)
+                    out.append('%s<startEvent id=%s><messageEventDefinition id=%s messageRef=%s/></startEvent>'
+                               % (ind, quoteattr(c.id), quoteattr(c.id + "_med"), quoteattr(c.message[0])))
                 elif c.kind == "intermediateCatchEvent" and c.timer:
                     out.append('%s<intermediateCatchEvent id=%s><timerEventDefinition id=%s><timeDuration>%s'
                                '</timeDuration></timerEventDefinition></intermediateCatchEvent>'
@@ -349,6 +355,9 @@ class ProcessBuilder:
         render(self.root, "    ")
         out.append("  </process>")
         for c in catches:
+            if c.message[2] is None:
+                out.append('  <message id=%s name=%s/>' % tuple(quoteattr(x) for x in c.message[:2]))
+                continue
             out.append('  <message id=%s name=%s><extensionElements><zeebe:subscription correlationKey=%s/>'
                        '</extensionElements></message>' % tuple(quoteattr(x) for x in c.message))
         out.append("</definitions>")
@@ -456,6 +465,19 @@ def job_types_of(xml):
     if isinstance(xml, bytes):
         xml = xml.decode()
     return set(m for m in re.findall(r'taskDefinition[^>]*?\stype="([^"=][^"]*)"', xml))
+
+
+def message_start_names_of(xml):
+    """Message names of the message start events a BPMN XML declares (startEvent > messageEventDefinition
+    messageRef -> <message name>)."""
+    import re
+    if isinstance(xml, bytes):
+        xml = xml.decode()
+    refs = set(re.findall(r'<(?:\w+:)?startEvent\b[^>]*>\s*<(?:\w+:)?messageEventDefinition\b[^>]*?\smessageRef="([^"]*)"',
+                          xml))
+    names = dict(re.findall(r'<(?:\w+:)?message\b[^>]*?\sid="([^"]*)"[^>]*?\sname="([^"]*)"', xml))
+    names.update((i, n) for n, i in re.findall(r'<(?:\w+:)?message\b[^>]*?\sname="([^"]*)"[^>]*?\sid="([^"]*)"', xml))
+    return {names[r] for r in refs if r in names}
 
 
 def message_names_of(xml):
