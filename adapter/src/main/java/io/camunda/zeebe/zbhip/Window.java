@@ -435,6 +435,10 @@ final class Window {
               .setBpmnProcessId(d.bpmnProcessId())
               .setProcessDefinitionVersion(d.version())
               .setProcessDefinitionKey(d.definitionKey());
+          if (d.customHeaders()[elem] != null) {
+            // BpmnJobBehavior.encodeHeaders: the task headers' msgpack map (the compiler's HashMap order)
+            v.setCustomHeaders(new UnsafeBuffer(d.customHeaders()[elem]));
+          }
         }
         if (aux >= 0) {
           v.setVariables(documents[i]); // JOB:COMPLETED / COMPLETE rejection: the command's variables

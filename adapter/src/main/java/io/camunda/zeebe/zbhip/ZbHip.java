@@ -331,7 +331,8 @@ public final class ZbHip {
       byte[] elementTypes,
       byte[] eventTypes,
       String[] jobTypes,
-      int[] retries) {}
+      int[] retries,
+      byte[][] customHeaders) {} // zeebe:taskHeaders per element (zbhip_process_csr.header_bytes), null: none
 
   /**
    * zbhip_compile_bpmn + zbhip_deploy: the deployment, or null when the process uses a construct
@@ -348,7 +349,7 @@ public final class ZbHip {
         return null;
       }
       check(rc, "zbhip_compile_bpmn: " + err.getUtf8String(0));
-      final MemorySegment c = csrOut.get(ADDRESS, 0).reinterpret(104);
+      final MemorySegment c = csrOut.get(ADDRESS, 0).reinterpret(144);
       try {
         final MemorySegment idx = a.allocate(JAVA_INT);
         final int d = (int) call(DEPLOY, h, c, idx);
@@ -379,7 +380,21 @@ public final class ZbHip {
           ids[e] = strings[els.get(JAVA_SHORT, o + 22) & 0xFFFF];
         }
         final String bpmnId = strings[c.get(JAVA_SHORT, 100) & 0xFFFF];
-        return new Deployed(idx.get(JAVA_INT, 0), bpmnId, definitionKey, version, ids, types, events, jobTypes, retries);
+        // header_begin (offset 128: n + 1 offsets) and header_bytes (136), ABI 10
+        final byte[][] headers = new byte[n][];
+        final MemorySegment hb = c.get(ADDRESS, 128);
+        if (hb.address() != 0) {
+          final MemorySegment begin = hb.reinterpret(4L * (n + 1));
+          final MemorySegment bytes = c.get(ADDRESS, 136).reinterpret(begin.getAtIndex(JAVA_INT, n));
+          for (int e = 0; e < n; e++) {
+            final int b = begin.getAtIndex(JAVA_INT, e), end = begin.getAtIndex(JAVA_INT, e + 1);
+            if (end > b) {
+              headers[e] = bytes.asSlice(b, end - b).toArray(JAVA_BYTE);
+            }
+          }
+        }
+        return new Deployed(
+            idx.get(JAVA_INT, 0), bpmnId, definitionKey, version, ids, types, events, jobTypes, retries, headers);
       } finally {
         call(FREE_CSR, c);
       }

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 9  /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+#define ZBHIP_ABI_VERSION 10 /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
                                4: timer boundary events (start_event / flow_source / job_retries of job
                                   workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
                                   PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions;
@@ -54,7 +54,9 @@ extern "C" {
                                8: zbhip_outbox_command, zbhip_drain_command on message partitions,
                                   zeebe:ioMapping (zbhip_process_csr.mappings);
                                9: interrupting message boundary events, ZBHIP_CMD_MSG_SUB_DELETE /
-                                  ZBHIP_CMD_PMS_DELETE and the DELETING / DELETE / DELETED records */
+                                  ZBHIP_CMD_PMS_DELETE and the DELETING / DELETE / DELETED records;
+                              10: static zeebe:taskHeaders (zbhip_process_csr.header_begin /
+                                  header_bytes) */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -288,6 +290,12 @@ typedef struct zbhip_process_csr {
                                     message); "" for a multi-instance collection */
   uint32_t n_mappings;           /* zeebe:ioMapping entries (ABI 8) */
   const zbhip_mapping* mappings;
+  /* zeebe:taskHeaders (ABI 10): job worker element e's customHeaders -- the msgpack map
+   * BpmnJobBehavior.encodeHeaders (BpmnJobBehavior.java:219-248,365-399) writes, its entries in the
+   * iteration order of the Java HashMap it builds -- at header_bytes[header_begin[e] ..
+   * header_begin[e + 1]); an empty range is JobRecord.NO_HEADERS (an empty map).  NULL: no headers. */
+  const uint32_t* header_begin;  /* n_elements + 1 offsets */
+  const uint8_t* header_bytes;
 } zbhip_process_csr;
 
 /* Host-side compiler: BPMN XML -> CSR (engine/.../deployment/model/transformation/BpmnTransformer.java:109-127).

@@ -384,6 +384,9 @@ def record_value(r, tables, docs_of_source, doc_entry, timestamp=0, timer_value=
                       processDefinitionVersion=p["version"], processDefinitionKey=p["key"],
                       processInstanceKey=int(r["process_instance_key"]), elementId=el[2],
                       elementInstanceKey=int(r["scope_key"]))
+        hs = p.get("headers")
+        if hs and hs[int(r["element_idx"])]:  # zeebe:taskHeaders (BpmnJobBehavior.encodeHeaders)
+            fields["customHeaders"] = hs[int(r["element_idx"])]
         if int(r["intent"]) == 2:  # COMPLETED: the stored job + the command's variables
             fields["variables"] = src_doc
         if int(r["message_key"]) != -1:  # an ACTIVATED job (DbJobState.activate): its deadline and worker

@@ -40,6 +40,8 @@ def lib():
         L.zbo_name.restype = C.c_char_p
         L.zbo_element_job_type.restype = C.c_char_p
         L.zbo_element_job_type.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.zbo_element_headers.restype = C.c_int
+        L.zbo_element_headers.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_int]
         L.zbo_element_cond_text.restype = C.c_char_p
         L.zbo_element_cond_text.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.zbo_process_info.restype = C.c_char_p
@@ -169,6 +171,13 @@ class Oracle:
     def names(self):
         return [self.name(i) for i in range(self.L.zbo_n_names(self.h))]
 
+    def element_headers(self, p, e):
+        """The customHeaders msgpack map of element e's jobs (b"": NO_HEADERS)."""
+        n = self.L.zbo_element_headers(self.h, p, e, None, 0)
+        buf = C.create_string_buffer(max(n, 1))
+        self.L.zbo_element_headers(self.h, p, e, buf, n)
+        return buf.raw[:n]
+
     def process_tables(self):
         """Deployment tables for oracle/logserial.py: per process bpmn_process_id, version, key and
         elements (type, event_type, id, job_type, retries)."""
@@ -184,7 +193,7 @@ class Oracle:
                             self.L.zbo_element_job_type(self.h, p, e).decode(), r.value))
             conds = [self.L.zbo_element_cond_text(self.h, p, e).decode() for e in range(len(els))]
             out.append({"bpmn_process_id": bid, "version": ver.value, "key": key.value, "elements": els,
-                        "cond_text": conds})
+                        "cond_text": conds, "headers": [self.element_headers(p, e) for e in range(len(els))]})
         return out
 
     def submit(self, cmds, docs=None, xparts=None):

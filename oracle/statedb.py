@@ -159,8 +159,15 @@ def encode_rows(rows, processes, string_value):
             if "errorMessageHex" in f:  # a failed job's stored fields (JobFailProcessor.failJob)
                 failed = dict(errorMessage=bytes.fromhex(f["errorMessageHex"]).decode(),
                               retryBackoff=int(f["retryBackoff"]), recurringTime=int(f["recurringTime"]))
+            # the stored job's customHeaders: its element's task headers (BpmnJobBehavior.encodeHeaders)
+            proc = by_def.get(int(f["processDefinitionKey"]))
+            hdr = {}
+            if proc is not None and proc.get("headers"):
+                for e, el in enumerate(proc["elements"]):
+                    if el[2] == f["elementId"] and proc["headers"][e]:
+                        hdr = {"customHeaders": proc["headers"][e]}
             job = LS.write_object(LS.JOB, dict(
-                deadline=int(f.get("deadline", -1)), worker=f.get("worker", ""), **failed,
+                deadline=int(f.get("deadline", -1)), worker=f.get("worker", ""), **failed, **hdr,
                 retries=int(f["retries"]), type=f["type"], bpmnProcessId=f["bpmnProcessId"],
                 processDefinitionVersion=int(f["processDefinitionVersion"]),
                 processDefinitionKey=int(f["processDefinitionKey"]), processInstanceKey=int(f["processInstanceKey"]),

@@ -18,6 +18,7 @@
 // ============================================================================
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -369,6 +370,9 @@ struct OEl {
     int source_id = -1, target_id = -1;  // name ids (deploy); a string literal: its value-dictionary id
   };
   Mapping in_map, out_map;
+  // zeebe:taskHeaders of a job worker (document order) and the customHeaders its jobs carry
+  std::vector<std::pair<std::string, std::string>> headers;
+  std::string header_bytes;
 };
 
 struct OProc {
@@ -747,9 +751,18 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
         return false;
       }
       e.retries = atoi(r.c_str());
-      if (ext && ext->child("taskHeaders")) {
-        err = "task headers outside the supported subset";
-        return false;
+      if (const XNode* th = ext ? ext->child("taskHeaders") : nullptr) {
+        // TaskHeadersTransformer (deployment/model/transformer/zeebe/TaskHeadersTransformer.java:24-58):
+        // the headers with a non-empty key and value, in document order (Collectors.toMap: a duplicate
+        // key fails the deployment)
+        for (auto& h : th->kids) {
+          if (h->name != "header") continue;
+          const std::string hk = h->attr("key"), hv = h->attr("value");
+          if (hk.empty() || hv.empty()) continue;
+          for (auto& x : e.headers)
+            if (x.first == hk) { err = "duplicate task header key"; return false; }
+          e.headers.push_back({hk, hv});
+        }
       }
       if (!parse_mappings(ext, e, err)) return false;
     } else if (n == "intermediateCatchEvent" && k->child("timerEventDefinition")) {
@@ -1018,6 +1031,103 @@ struct JobRow {  // JobRecord without variables (DbJobState.createJobRecord)
   std::string error_message;
   int64_t retry_backoff = 0, recurring_time = -1;
 };
+
+// java.lang.String.hashCode over the UTF-16 code units of UTF-8 text
+static int32_t jstring_hash(const std::string& s) {
+  uint32_t h = 0;
+  size_t i = 0;
+  while (i < s.size()) {
+    const unsigned char c = (unsigned char)s[i];
+    const int n = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+    uint32_t cp = n == 1 ? c : n == 2 ? (c & 0x1Fu) : n == 3 ? (c & 0x0Fu) : (c & 0x07u);
+    for (int k = 1; k < n; ++k) cp = (cp << 6) | (i + k < s.size() ? ((unsigned char)s[i + k] & 0x3Fu) : 0u);
+    i += (size_t)n;
+    if (cp > 0xFFFF) {
+      h = 31u * h + (0xD800u + ((cp - 0x10000u) >> 10));
+      h = 31u * h + (0xDC00u + ((cp - 0x10000u) & 0x3FFu));
+    } else {
+      h = 31u * h + cp;
+    }
+  }
+  return (int32_t)h;
+}
+
+// java.util.HashMap<String, String> (JDK 21) as far as its iteration order goes: a power-of-two table of
+// insertion-ordered chains, hash (h ^ h >>> 16) & (n - 1), resize at size > 3/4 capacity (chains split in
+// order), first table 16 -- or, pre-sized by HashMap(Map) (putMapEntries), tableSizeFor(ceil(s / 0.75)).
+// A chain reaching TREEIFY_THRESHOLD would turn into a tree (or resize early): outside the restatement.
+struct JHashMap {
+  std::vector<std::vector<std::pair<std::string, std::string>>> tab;
+  size_t size = 0, threshold = 0;
+  static uint32_t spread(const std::string& k) {
+    const uint32_t h = (uint32_t)jstring_hash(k);
+    return h ^ (h >> 16);
+  }
+  void resize() {
+    const size_t cap = tab.empty() ? (threshold ? threshold : 16) : tab.size() * 2;
+    std::vector<std::vector<std::pair<std::string, std::string>>> t(cap);
+    for (auto& b : tab)
+      for (auto& e : b) t[spread(e.first) & (cap - 1)].push_back(e);
+    tab.swap(t);
+    threshold = cap / 4 * 3;
+  }
+  void presize(size_t s) {  // HashMap(Map m) -> putMapEntries (table == null)
+    if (!s) return;
+    const size_t t = (size_t)std::ceil((double)s / 0.75);
+    size_t c = 1;
+    while (c < t) c <<= 1;
+    threshold = c;
+  }
+  bool put(const std::string& k, const std::string& v) {
+    if (tab.empty()) resize();
+    auto& b = tab[spread(k) & (tab.size() - 1)];
+    for (auto& e : b)
+      if (e.first == k) { e.second = v; return true; }
+    if (b.size() >= 8) return false;
+    b.push_back({k, v});
+    if (++size > threshold) resize();
+    return true;
+  }
+  std::vector<std::pair<std::string, std::string>> entries() const {
+    std::vector<std::pair<std::string, std::string>> o;
+    for (auto& b : tab) o.insert(o.end(), b.begin(), b.end());
+    return o;
+  }
+};
+
+// msgpack (MsgPackWriter.writeMapHeader / writeString): fix / 8 / 16 / 32-bit forms, big-endian lengths
+static void mp_len(std::string& o, uint32_t n, uint8_t fix, uint32_t fix_max, uint8_t b8, uint8_t b16, uint8_t b32) {
+  if (n <= fix_max) { o += (char)(fix | n); return; }
+  if (b8 && n <= 0xFF) { o += (char)b8; o += (char)n; return; }
+  if (n <= 0xFFFF) { o += (char)b16; o += (char)(n >> 8); o += (char)n; return; }
+  o += (char)b32;
+  for (int k = 3; k >= 0; --k) o += (char)(n >> (8 * k));
+}
+
+// BpmnJobBehavior.writeJobCreatedEvent -> encodeHeaders (processing/bpmn/behavior/BpmnJobBehavior.java:194-248):
+// the transformer's map (Collectors.toMap over the document-ordered headers), copied with new HashMap<>(m),
+// then HeaderEncoder.encode (:365-399) collects the valid entries into a third HashMap (Collectors.toMap)
+// and writes its entries in iteration order; no headers: JobRecord.NO_HEADERS (an empty map)
+static bool encode_headers(const std::vector<std::pair<std::string, std::string>>& hs, std::string& out) {
+  out.clear();
+  if (hs.empty()) return true;
+  JHashMap h1, h2, h3;
+  for (auto& [k, v] : hs)
+    if (!h1.put(k, v)) return false;
+  h2.presize(h1.size);
+  for (auto& [k, v] : h1.entries())
+    if (!h2.put(k, v)) return false;
+  for (auto& [k, v] : h2.entries())
+    if (!k.empty() && !v.empty() && !h3.put(k, v)) return false;
+  mp_len(out, (uint32_t)h3.size, 0x80, 15, 0, 0xDE, 0xDF);
+  for (auto& [k, v] : h3.entries()) {
+    mp_len(out, (uint32_t)k.size(), 0xA0, 31, 0xD9, 0xDA, 0xDB);
+    out += k;
+    mp_len(out, (uint32_t)v.size(), 0xA0, 31, 0xD9, 0xDA, 0xDB);
+    out += v;
+  }
+  return true;
+}
 
 // hex of a string in a state row (error messages may hold ',' and '|')
 static std::string hex_of(const std::string& v) {
@@ -1313,6 +1423,11 @@ class Oracle {
         if (M->var) M->source_id = intern(M->source);
         else if (M->type == ZBHIP_DOC_STR) M->value = intern_string(M->source);
         M->target_id = intern(M->target);
+      }
+    for (auto& e : P.els)
+      if (!encode_headers(e.headers, e.header_bytes)) {
+        last_error = "task headers a HashMap would treeify";
+        return ZBHIP_EUNSUPP;
       }
     std::set<std::string> start_names;
     for (int s : P.msg_starts) {
@@ -4278,6 +4393,12 @@ const char* zbo_element_cond_text(void* o, int proc, int elem) {
 
 const char* zbo_element_job_type(void* o, int proc, int elem) {
   return static_cast<Oracle*>(o)->procs.at(proc).els.at(elem).job_type.c_str();
+}
+// the customHeaders msgpack map of a job worker's jobs (empty: NO_HEADERS); returns its length
+int zbo_element_headers(void* o, int proc, int elem, char* buf, int cap) {
+  const std::string& h = static_cast<Oracle*>(o)->procs.at(proc).els.at(elem).header_bytes;
+  if (buf && cap > 0) memcpy(buf, h.data(), std::min<size_t>((size_t)cap, h.size()));
+  return (int)h.size();
 }
 const char* zbo_process_info(void* o, int proc, int64_t* def_key, int* version) {
   const OProc& P = static_cast<Oracle*>(o)->procs.at(proc);

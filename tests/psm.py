@@ -28,7 +28,7 @@ from oracle.oracle import Oracle
 from zeebe_amd import abi
 from zeebe_amd.adapter import (JOB_BATCH_ACTIVATE, JOB_BATCH_ACTIVATED, MESSAGE_VALUE_TYPES, VT_JOB_BATCH, XPART_COMMAND,
                                RecordValues, doc_entries, push_side_effects, typed_value, xpart_value)
-from zeebe_amd.engine import ProcessDefinition
+from zeebe_amd.engine import ProcessDefinition, msgpack_string_map
 
 
 class RecordingJobStream:
@@ -184,7 +184,8 @@ def oracle_tables(o):
         els = t["elements"]
         out.append(ProcessDefinition(i, t["bpmn_process_id"], [e[2] for e in els], [abi.ELEMENT_TYPES[e[0]] for e in els],
                                      [e[3] or None for e in els], [abi.EVENT_TYPES[e[1]] for e in els],
-                                     [e[4] for e in els], t["version"], t["key"]))
+                                     [e[4] for e in els], t["version"], t["key"],
+                                     [msgpack_string_map(h) if h else () for h in t["headers"]]))
     return out
 
 

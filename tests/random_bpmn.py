@@ -208,8 +208,16 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
                              ' outputCollection=%s outputElement=%s' % (quoteattr("out_" + nid), quoteattr(loop["out"]))
                              if "out" in loop else "",
                              "<completionCondition>%s</completionCondition>" % escape(loop["cond"]) if "cond" in loop else ""))
-                out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s/>'
-                           '</extensionElements>%s</%s>' % (ind, kind, quoteattr(nid), quoteattr(extra["job_type"]), lc, kind))
+                # with task kinds, every other task has static task headers (derived from its id, no draw from
+                # the generator: the campaigns' processes keep their shapes)
+                th = ""
+                if g.task_kinds and sum(map(ord, nid)) % 2:
+                    th = "<zeebe:taskHeaders>%s</zeebe:taskHeaders>" % "".join(
+                        "<zeebe:header key=%s value=%s/>" % (quoteattr(k), quoteattr(v))
+                        for k, v in (("workerVersion", "42"), (nid, "h-" + nid), ("Aa", "1"), ("BB", "2")))
+                out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s/>%s'
+                           '</extensionElements>%s</%s>' % (ind, kind, quoteattr(nid), quoteattr(extra["job_type"]), th,
+                                                            lc, kind))
             elif kind == "exclusiveGateway" and nid in g.defaults:
                 out.append('%s<exclusiveGateway id=%s default=%s/>' % (ind, quoteattr(nid), quoteattr(g.defaults[nid])))
             elif kind == "intermediateCatchEvent":

@@ -193,6 +193,8 @@ class RecordValues:
                 v.update({"type": p.job_types[elem], "retries": p.retries[elem], "elementId": p.element_ids[elem],
                           "elementInstanceKey": scope, "processInstanceKey": pik, "bpmnProcessId": p.bpmn_process_id,
                           "processDefinitionVersion": p.version, "processDefinitionKey": p.definition_key})
+                if p.custom_headers[elem]:  # zeebe:taskHeaders (BpmnJobBehavior.encodeHeaders)
+                    v["customHeaders"] = p.custom_headers[elem]
             if int(r["message_key"]) != -1:  # an ACTIVATED job: the deadline and worker it holds
                 cid = int(r["correlation_key"])
                 v.update({"deadline": int(r["message_key"]),
@@ -285,6 +287,7 @@ class RecordValues:
             p = self.procs[int(j["process_idx"])]
             e = int(j["element_idx"])
             out.append({"type": command["type"], "worker": command["worker"], "deadline": int(j["deadline"]),
+                        **({"customHeaders": p.custom_headers[e]} if p.custom_headers[e] else {}),
                         "retries": int(j["retries"]), "elementId": p.element_ids[e],
                         "elementInstanceKey": int(j["element_instance_key"]),
                         "processInstanceKey": int(j["process_instance_key"]), "bpmnProcessId": p.bpmn_process_id,

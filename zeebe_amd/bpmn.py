@@ -101,6 +101,11 @@ class ProcessBuilder:
         self.current.job_type = t
         return self
 
+    def zeebeTaskHeader(self, key, value):
+        """AbstractJobWorkerTaskBuilder.zeebeTaskHeader: a <zeebe:header> in the task's <zeebe:taskHeaders>."""
+        self.current.headers = getattr(self.current, "headers", []) + [(key, value)]
+        return self
+
     def task(self, id_=None):
         self._add_node("task", id_)
         return self
@@ -287,9 +292,12 @@ class ProcessBuilder:
                                    % (ind, attrs, escape(c.condition)))
                 elif c.kind in ("serviceTask", "sendTask", "scriptTask", "businessRuleTask"):
                     retries = ' retries="%s"' % c.retries if c.retries is not None else ""
-                    out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>%s'
+                    hs = getattr(c, "headers", [])
+                    th = "<zeebe:taskHeaders>%s</zeebe:taskHeaders>" % "".join(
+                        "<zeebe:header key=%s value=%s/>" % (quoteattr(k), quoteattr(v)) for k, v in hs) if hs else ""
+                    out.append('%s<%s id=%s><extensionElements><zeebe:taskDefinition type=%s%s/>%s%s'
                                '</extensionElements>%s</%s>' % (ind, c.kind, quoteattr(c.id), quoteattr(c.job_type),
-                                                               retries, io(c), loop(c), c.kind))
+                                                               retries, th, io(c), loop(c), c.kind))
                 elif c.kind == "intermediateCatchEvent" and c.message:
                     catches.append(c)
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'

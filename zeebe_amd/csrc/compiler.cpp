@@ -14,6 +14,7 @@
 // FEEL conditions (`=`-prefixed, FeelExpressionLanguage.parseExpression) are lowered to the
 // postfix bytecode of include/zbhip.h; anything outside the typed comparison subset is rejected
 // at deploy time (ZBHIP_EUNSUPP) rather than evaluated differently on the device.
+#include <algorithm>
 #include <cctype>
 #include <cstddef>
 #include <cstdio>
@@ -318,6 +319,9 @@ struct Compiled {
   std::vector<const char*> cond_ptrs;
   std::vector<zbhip_insn> code;
   std::vector<zbhip_mapping> mappings;
+  std::vector<std::string> headers;  // per element: its customHeaders msgpack map ("" = NO_HEADERS)
+  std::vector<uint32_t> header_begin;
+  std::vector<uint8_t> header_bytes;
   std::vector<std::string> strings;
   std::vector<const char*> string_ptrs;
   std::unordered_map<std::string, uint16_t> string_ids;
@@ -348,8 +352,101 @@ struct Compiled {
     csr.code = code.data();
     csr.n_strings = (uint32_t)strings.size();
     csr.strings = string_ptrs.data();
+    header_begin.clear();
+    header_bytes.clear();
+    headers.resize(elements.size());
+    bool any = false;
+    for (auto& h : headers) any |= !h.empty();
+    if (any) {
+      for (auto& h : headers) {
+        header_begin.push_back((uint32_t)header_bytes.size());
+        header_bytes.insert(header_bytes.end(), h.begin(), h.end());
+      }
+      header_begin.push_back((uint32_t)header_bytes.size());
+    }
+    csr.header_begin = any ? header_begin.data() : nullptr;
+    csr.header_bytes = any ? header_bytes.data() : nullptr;
   }
 };
+
+// String.hashCode (java.lang.String): s[0]*31^(n-1) + ... over the UTF-16 code units of the UTF-8 text
+static int32_t java_string_hash(const std::string& s) {
+  uint32_t h = 0;
+  auto unit = [&h](uint32_t u) { h = 31u * h + u; };
+  for (size_t i = 0; i < s.size();) {
+    const unsigned char c = (unsigned char)s[i];
+    uint32_t cp;
+    int n;
+    if (c < 0x80) { cp = c; n = 1; }
+    else if ((c >> 5) == 6) { cp = c & 0x1F; n = 2; }
+    else if ((c >> 4) == 14) { cp = c & 0x0F; n = 3; }
+    else { cp = c & 0x07; n = 4; }
+    for (int k = 1; k < n && i + k < s.size(); ++k) cp = (cp << 6) | ((unsigned char)s[i + k] & 0x3F);
+    i += n;
+    if (cp >= 0x10000) {  // a surrogate pair
+      cp -= 0x10000;
+      unit(0xD800 + (cp >> 10));
+      unit(0xDC00 + (cp & 0x3FF));
+    } else {
+      unit(cp);
+    }
+  }
+  return (int32_t)h;
+}
+
+// MsgPackWriter.writeString / writeMapHeader (msgpack-core/.../MsgPackWriter.java): fixstr / str8 / str16 /
+// str32, fixmap / map16 / map32, big-endian lengths
+static void mp_header(std::string& o, uint32_t n, uint8_t fix, uint32_t fix_max, uint8_t b8, uint8_t b16, uint8_t b32) {
+  if (n <= fix_max) { o += (char)(fix | n); return; }
+  if (b8 && n <= 0xFF) { o += (char)b8; o += (char)n; return; }
+  if (n <= 0xFFFF) { o += (char)b16; o += (char)(n >> 8); o += (char)n; return; }
+  o += (char)b32;
+  for (int k = 3; k >= 0; --k) o += (char)(n >> (8 * k));
+}
+
+// zeebe:taskHeaders -> the customHeaders of the job worker's jobs.  TaskHeadersTransformer (deployment/
+// model/transformer/zeebe/TaskHeadersTransformer.java:24-58) keeps the headers with a non-empty key and value
+// (Collectors.toMap: a duplicate key fails the deployment -- refused here); BpmnJobBehavior.encodeHeaders
+// copies them into a HashMap (:219-248) and HeaderEncoder.encode (:365-399) collects them into another,
+// whose iteration order is written.  A java.util.HashMap iterates its buckets in index order and a bucket's
+// entries in insertion order (a resize splits a bucket keeping it), the bucket being (h ^ h >>> 16) &
+// (capacity - 1): the two default-constructed maps grow alike (16, doubled past 3/4 load), the pre-sized copy
+// (JDK 21 HashMap(Map): tableSizeFor(ceil(size / 0.75))) has a capacity dividing theirs, so every map keeps
+// ties in document order and the entries come out in document order stably sorted by the final bucket.  A
+// bucket of 9 entries would turn into a tree (or force an extra resize): outside the subset.
+static int encode_task_headers(const Elem& th, std::string& out, std::string& err) {
+  std::vector<std::pair<std::string, std::string>> hs;
+  for (auto& h : th.children) {
+    if (h.tag != "header") continue;
+    const std::string* k = h.get("key");
+    const std::string* v = h.get("value");
+    if (!k || !v || k->empty() || v->empty()) continue;  // isValidHeader
+    for (auto& e : hs)
+      if (e.first == *k) { err = "duplicate task header key '" + *k + "'"; return ZBHIP_EPARSE; }
+    hs.push_back({*k, *v});
+  }
+  out.clear();
+  if (hs.empty()) return ZBHIP_OK;  // no valid header: NO_HEADERS
+  uint32_t cap = 16;
+  while (hs.size() > cap / 4 * 3) cap *= 2;
+  std::vector<std::pair<uint32_t, size_t>> order;
+  uint32_t in16[16] = {};
+  for (size_t i = 0; i < hs.size(); ++i) {
+    const uint32_t h = (uint32_t)java_string_hash(hs[i].first);
+    const uint32_t spread = h ^ (h >> 16);
+    order.push_back({spread & (cap - 1), i});
+    if (++in16[spread & 15] > 8) { err = "task headers that a HashMap would treeify"; return ZBHIP_EUNSUPP; }
+  }
+  std::stable_sort(order.begin(), order.end(), [](auto& a, auto& b) { return a.first < b.first; });
+  mp_header(out, (uint32_t)hs.size(), 0x80, 15, 0, 0xDE, 0xDF);
+  for (auto& [b, i] : order) {
+    for (const std::string* t : {&hs[i].first, &hs[i].second}) {
+      mp_header(out, (uint32_t)t->size(), 0xA0, 31, 0xD9, 0xDA, 0xDB);
+      out += *t;
+    }
+  }
+  return ZBHIP_OK;
+}
 
 // Interval.parse (bpmn-model/.../util/time/Interval.java) of a static duration
 // "P[0D][T[nH][nM][n[.f]S]]": a Duration, so due = now + a fixed number of ms.  Days (a Period, which
@@ -877,9 +974,9 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
           err = "job type/retries expressions outside the supported subset";
           return ZBHIP_EUNSUPP;
         }
-        if (ext->first("taskHeaders")) {
-          err = "task headers outside the supported subset";
-          return ZBHIP_EUNSUPP;
+        if (const Elem* th = ext->first("taskHeaders")) {
+          C.headers.resize(C.elements.size() + 1);
+          if (int rc = encode_task_headers(*th, C.headers[C.elements.size()], err)) return rc;
         }
         if (int rc = parse_mappings(ext, (uint16_t)C.elements.size(), C, err)) return rc;
         e.job_type = C.str(*jt);
@@ -909,6 +1006,11 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         b.message_name = loop.input.empty() ? ZBHIP_NONE16 : C.str(loop.input);
         const uint16_t bi = (uint16_t)C.elements.size();
         b.start_event = (uint16_t)(bi + 1);
+        if (C.headers.size() > bi) {  // the task headers belong to the inner activity, after the body
+          std::string h = std::move(C.headers[bi]);
+          C.headers.resize(bi + 2);
+          C.headers[bi + 1] = std::move(h);
+        }
         index[*id] = bi;
         C.elements.push_back(b);
         collections.push_back({bi, std::move(loop)});

@@ -117,6 +117,7 @@ struct SerElement {
   // processDefinitionKey, "processInstanceKey"] key ["elementId" .. "elementInstanceKey"] key [tenantId]
   Bytes job_head, job_mid, job_tail;
   size_t job_rest = 0;  // job_head after its deadline and worker entries
+  Bytes headers;        // customHeaders: the task headers' msgpack map (zbhip_process_csr.header_bytes)
 };
 struct SerProcess {
   std::string bpmn_id;
@@ -248,7 +249,11 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
       key(S.job_head, "type");
       mp_str(S.job_head, str(E.job_type));
       key(S.job_head, "customHeaders");
-      S.job_head += kEmptyDoc;  // no task headers: NO_HEADERS (BpmnJobBehavior.java:365-367)
+      // BpmnJobBehavior.encodeHeaders (:219-248,365-399): the compiled task headers, or NO_HEADERS
+      if (csr->header_begin && csr->header_begin[e + 1] > csr->header_begin[e])
+        S.headers.assign(reinterpret_cast<const char*>(csr->header_bytes) + csr->header_begin[e],
+                         csr->header_begin[e + 1] - csr->header_begin[e]);
+      S.job_head += S.headers.empty() ? kEmptyDoc : S.headers;
       key(S.job_head, "variables");
       key(S.job_mid, "errorMessage");
       key(S.job_mid, "");
@@ -269,6 +274,15 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
   if (idx_out) *idx_out = (uint32_t)s->procs.size();
   s->procs.push_back(std::move(P));
   return ZBHIP_OK;
+}
+
+// the stored customHeaders of a job of element `id` (its process by definition key): the element's task headers
+static const Bytes& job_headers(const zbhip_serializer* s, int64_t def_key, const std::string& id) {
+  for (const SerProcess& P : s->procs)
+    if (P.def_key == def_key)
+      for (const SerElement& E : P.els)
+        if (E.id == id && ZBHIP_IS_JOB_WORKER(E.type)) return E.headers.empty() ? kEmptyDoc : E.headers;
+  return kEmptyDoc;
 }
 
 // The errorMessage of an exclusive gateway's incident (BpmnIncidentBehavior.createIncident with the
@@ -874,7 +888,7 @@ extern "C" int zbhip_serializer_encode_state_row(zbhip_serializer* s, const char
     key(v, "retryBackoff"); mp_int(v, failed ? ll(f["retryBackoff"]) : 0);
     key(v, "recurringTime"); mp_int(v, failed ? ll(f["recurringTime"]) : -1);
     key(v, "type"); mp_str(v, f["type"]);
-    key(v, "customHeaders"); v += kEmptyDoc;
+    key(v, "customHeaders"); v += job_headers(s, ll(f["processDefinitionKey"]), f["elementId"]);
     key(v, "variables"); mp_bin(v, kEmptyDoc);
     key(v, "errorMessage"); mp_str(v, failed ? unhex(f["errorMessageHex"]) : std::string());
     key(v, "errorCode"); key(v, "");

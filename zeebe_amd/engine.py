@@ -21,7 +21,7 @@ from .native import STATE_SINK, ZbhipError, check, load
 
 class ProcessDefinition:
     def __init__(self, idx, bpmn_process_id, element_ids, element_types, job_types, event_types=None, retries=None,
-                 version=1, definition_key=-1):
+                 version=1, definition_key=-1, custom_headers=None):
         self.idx = idx
         self.bpmn_process_id = bpmn_process_id
         self.element_ids = element_ids
@@ -31,13 +31,38 @@ class ProcessDefinition:
         self.retries = retries               # job retries of job worker elements
         self.version = version
         self.definition_key = definition_key
+        # zeebe:taskHeaders per element: (key, value) pairs in the order BpmnJobBehavior writes them
+        self.custom_headers = custom_headers or [()] * len(element_ids)
 
 
-class _Csr(C.Structure):  # prefix of zbhip_process_csr needed to read the element table
+class _Csr(C.Structure):  # zbhip_process_csr (include/zbhip.h, ABI 10)
     _fields_ = [("n_elements", C.c_uint32), ("elements", C.c_void_p), ("n_out", C.c_uint32),
                 ("out_flow", C.c_void_p), ("n_conditions", C.c_uint32), ("cond_begin", C.c_void_p),
                 ("n_code", C.c_uint32), ("code", C.c_void_p), ("n_strings", C.c_uint32),
-                ("strings", C.POINTER(C.c_char_p))]
+                ("strings", C.POINTER(C.c_char_p)), ("none_start", C.c_uint16), ("n_join_slots", C.c_uint16),
+                ("process_definition_key", C.c_int64), ("version", C.c_int32), ("bpmn_process_id", C.c_uint16),
+                ("pad", C.c_uint16), ("cond_text", C.c_void_p), ("n_mappings", C.c_uint32), ("mappings", C.c_void_p),
+                ("header_begin", C.POINTER(C.c_uint32)), ("header_bytes", C.c_void_p)]
+
+
+def msgpack_string_map(b):
+    """The (key, value) pairs of a msgpack map of strings (a job's customHeaders), in stored order."""
+    def ln(i, fix, fixmask):
+        t = b[i]
+        if t & ~fixmask == fix:
+            return t & fixmask, i + 1
+        w = {0xD9: 1, 0xDA: 2, 0xDB: 4, 0xDE: 2, 0xDF: 4}[t]
+        return int.from_bytes(b[i + 1:i + 1 + w], "big"), i + 1 + w
+    n, i = ln(0, 0x80, 0x0F)
+    out = []
+    for _ in range(n):
+        kv = []
+        for _ in range(2):
+            m, i = ln(i, 0xA0, 0x1F)
+            kv.append(b[i:i + m].decode())
+            i += m
+        out.append(tuple(kv))
+    return tuple(out)
 
 
 ELEMENT_DTYPE = np.dtype([("element_type", "u1"), ("event_type", "u1"), ("out_begin", "<u2"), ("out_count", "<u2"),
@@ -93,6 +118,12 @@ class Partition:
             c = C.cast(csr, C.POINTER(_Csr)).contents
             els = np.frombuffer(C.string_at(c.elements, c.n_elements * ELEMENT_DTYPE.itemsize), dtype=ELEMENT_DTYPE)
             strings = [c.strings[i].decode() for i in range(c.n_strings)]
+            headers = [()] * c.n_elements
+            if c.header_begin:
+                hb = [c.header_begin[i] for i in range(c.n_elements + 1)]
+                raw = C.string_at(c.header_bytes, hb[-1])
+                headers = [msgpack_string_map(raw[hb[e]:hb[e + 1]]) if hb[e + 1] > hb[e] else ()
+                           for e in range(c.n_elements)]
             idx = C.c_uint32()
             check(self.L.zbhip_deploy(self.h, csr, C.byref(idx)), "zbhip_deploy")
         finally:
@@ -102,7 +133,7 @@ class Partition:
                                [strings[j] if j != 0xFFFF else None for j in els["job_type"]],
                                [abi.EVENT_TYPES[t] for t in els["event_type"]],
                                [int(r) if j != 0xFFFF else None for r, j in zip(els["job_retries"], els["job_type"])],
-                               version, process_definition_key)
+                               version, process_definition_key, headers)
         self.processes.append(pd)
         return idx.value
 
