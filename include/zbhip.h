@@ -110,7 +110,8 @@ enum zbhip_pi_intent {
  * CREATED=0 UPDATED=1; ProcessEventIntent TRIGGERING=0 TRIGGERED=1; ProcessInstanceCreationIntent
  * CREATE=0 CREATED=1 */
 enum { ZBHIP_JOB_CREATED = 0, ZBHIP_JOB_COMPLETE = 1, ZBHIP_JOB_COMPLETED = 2, ZBHIP_JOB_TIME_OUT = 3,
-       ZBHIP_JOB_TIMED_OUT = 4, ZBHIP_JOB_FAIL = 5, ZBHIP_JOB_FAILED = 6, ZBHIP_JOB_CANCELED = 10 };
+       ZBHIP_JOB_TIMED_OUT = 4, ZBHIP_JOB_FAIL = 5, ZBHIP_JOB_FAILED = 6, ZBHIP_JOB_CANCELED = 10,
+       ZBHIP_JOB_THROW_ERROR = 11, ZBHIP_JOB_ERROR_THROWN = 12 };
 enum { ZBHIP_JOB_BATCH_ACTIVATE = 0, ZBHIP_JOB_BATCH_ACTIVATED = 1 };  /* JobBatchIntent */
 enum { ZBHIP_VAR_CREATED = 0, ZBHIP_VAR_UPDATED = 1 };
 enum { ZBHIP_PE_TRIGGERING = 0, ZBHIP_PE_TRIGGERED = 1 };
@@ -120,7 +121,8 @@ enum { ZBHIP_TIMER_CREATED = 0, ZBHIP_TIMER_TRIGGER = 1, ZBHIP_TIMER_TRIGGERED =
 /* IncidentIntent CREATED=0 RESOLVE=1 RESOLVED=2 (protocol/.../intent/IncidentIntent.java:19-22) */
 enum { ZBHIP_INCIDENT_CREATED = 0 };
 /* ErrorType ordinals (protocol/.../record/value/ErrorType.java) of the device's incidents */
-enum { ZBHIP_ERR_JOB_NO_RETRIES = 2, ZBHIP_ERR_CONDITION_ERROR = 3, ZBHIP_ERR_EXTRACT_VALUE_ERROR = 4 };
+enum { ZBHIP_ERR_JOB_NO_RETRIES = 2, ZBHIP_ERR_CONDITION_ERROR = 3, ZBHIP_ERR_EXTRACT_VALUE_ERROR = 4,
+       ZBHIP_ERR_UNHANDLED_ERROR_EVENT = 6 };
 /* the type of a condition's non-boolean result (ResultType names in the incident message) */
 enum { ZBHIP_FEEL_NULL = 0, ZBHIP_FEEL_NUMBER = 1, ZBHIP_FEEL_STRING = 2 };
 /* ProcessInstanceBatchIntent (protocol/.../intent/ProcessInstanceBatchIntent.java:18-20) */

@@ -370,6 +370,8 @@ struct OEl {
     int source_id = -1, target_id = -1;  // name ids (deploy); a string literal: its value-dictionary id
   };
   Mapping in_map, out_map;
+  // an error boundary event: the errorCode of its <error> ("" = a catch-all errorEventDefinition)
+  std::string error_code;
   // zeebe:taskHeaders of a job worker (document order) and the customHeaders its jobs carry
   std::vector<std::pair<std::string, std::string>> headers;
   std::string header_bytes;
@@ -680,7 +682,10 @@ static bool parse_mappings(const XNode* ext, OEl& e, std::string& err) {
   return true;
 }
 
-static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, std::string& err) {
+using ErrorDefs = std::unordered_map<std::string, std::string>;  // <error> id -> errorCode
+
+static bool build_process(const XNode& proc, const MessageDefs& msgs, const ErrorDefs& errors, OProc& P,
+                          std::string& err) {
   P.bpmn_id = proc.attr("id");
   P.els.clear();
   OEl pe;
@@ -781,6 +786,31 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, OProc& P, 
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_TIMER;
+    } else if (n == "boundaryEvent" && k->child("errorEventDefinition")) {
+      // an error boundary event (BoundaryEventTransformer, ErrorTransformer): interrupting; the errorCode of
+      // its <error> (a static code; no errorRef: a catch-all, errorCode "") -- looked up when a job throws
+      // an error (CatchEventAnalyzer.findErrorCatchEvent)
+      e.type = ZBHIP_EL_BOUNDARY_EVENT;
+      e.interrupting = true;
+      const XNode* ed = k->child("errorEventDefinition");
+      if (k->attr("cancelActivity") == "false" || k->child("timerEventDefinition") || k->child("messageEventDefinition") ||
+          k->child("signalEventDefinition") || k->child("escalationEventDefinition")) {
+        err = "error boundary event outside the supported subset";
+        return false;
+      }
+      const std::string ref = ed->attr("errorRef");
+      if (!ref.empty()) {
+        auto it = errors.find(ref);
+        if (it == errors.end() || (!it->second.empty() && it->second[0] == '=')) {
+          err = "error outside the supported subset (a static errorCode)";
+          return false;
+        }
+        e.error_code = it->second;
+      }
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+      e.event = ZBHIP_EV_ERROR;
+      boundaries.push_back({(int)P.els.size(), k->attr("attachedToRef")});
     } else if (n == "boundaryEvent" && k->child("messageEventDefinition")) {
       // a message boundary event, interrupting or not (BoundaryEventTransformer, CatchEventTransformer
       // .transformMessageEventDefinition): static name, `= variable` correlation key -- evaluated in the
@@ -1030,6 +1060,10 @@ struct JobRow {  // JobRecord without variables (DbJobState.createJobRecord)
   bool fail_fields = false;
   std::string error_message;
   int64_t retry_backoff = 0, recurring_time = -1;
+  // JobThrowErrorProcessor with no catch event (DbJobState.throwError): ERROR_THROWN, the stored record's
+  // errorCode, and its elementId the NO_CATCH_EVENT_FOUND marker
+  bool error_thrown = false, no_catch = false;
+  std::string error_code;
 };
 
 // java.lang.String.hashCode over the UTF-16 code units of UTF-8 text
@@ -1382,8 +1416,11 @@ class Oracle {
       if (!nm.empty() && nm[0] == '=') nm.clear();
       msgs[k->attr("id")] = {nm, var};
     }
+    ErrorDefs errors;  // <error> elements of the definitions (ErrorTransformer: errorCode)
+    for (auto& k : root->kids)
+      if (k->name == "error") errors[k->attr("id")] = k->attr("errorCode");
     OProc P;
-    if (!build_process(*proc, msgs, P, last_error)) return ZBHIP_EUNSUPP;
+    if (!build_process(*proc, msgs, errors, P, last_error)) return ZBHIP_EUNSUPP;
     P.def_key = def_key;
     P.version = version;
     // intern condition variable names now so ids match the product's deploy order
@@ -1611,7 +1648,7 @@ class Oracle {
                       (r.intent == ZBHIP_PMS_CREATE || r.intent == ZBHIP_PMS_CORRELATE || r.intent == ZBHIP_PMS_DELETE));
     const bool known = (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_CREATION && r.intent == ZBHIP_PIC_CREATE) ||
                        (r.value_type == ZBHIP_VT_JOB && (r.intent == ZBHIP_JOB_COMPLETE || r.intent == ZBHIP_JOB_TIME_OUT ||
-                                                          r.intent == ZBHIP_JOB_FAIL)) ||
+                                                          r.intent == ZBHIP_JOB_FAIL || r.intent == ZBHIP_JOB_THROW_ERROR)) ||
                        (r.value_type == ZBHIP_VT_TIMER && r.intent == ZBHIP_TIMER_TRIGGER) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE && r.intent >= ZBHIP_PI_ACTIVATE_ELEMENT) ||
                        (r.value_type == ZBHIP_VT_PROCESS_INSTANCE_BATCH &&
@@ -2020,6 +2057,7 @@ class Oracle {
     int error_type = 0, flow = -1, result = 0;  // the message: zbhip_incident_message
     int64_t job_key = -1;       // a job's incident (JOB_NO_RETRIES): INCIDENT_JOBS, its errorMessage
     std::string message;
+    bool no_catch = false;      // UNHANDLED_ERROR_EVENT: elementId NO_CATCH_EVENT_FOUND (the job's record)
   };
   std::map<int64_t, int64_t> incident_jobs_;                    // INCIDENT_JOBS [jobKey -> incident]
   std::map<int64_t, IncidentRow> incidents_;                    // INCIDENTS
@@ -2207,6 +2245,8 @@ class Oracle {
       time_out_job(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_JOB && cmd.r.intent == ZBHIP_JOB_FAIL)
       fail_job(cmd);
+    else if (cmd.r.value_type == ZBHIP_VT_JOB && cmd.r.intent == ZBHIP_JOB_THROW_ERROR)
+      throw_error(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_JOB)
       complete_job(cmd);
     else if (cmd.r.value_type == ZBHIP_VT_TIMER && cmd.r.intent == ZBHIP_TIMER_TRIGGER)
@@ -3042,6 +3082,138 @@ class Oracle {
     }
   }
 
+  // JobThrowErrorProcessor (processing/job/JobThrowErrorProcessor.java:84-176) with CatchEventAnalyzer
+  // .findErrorCatchEvent (processing/common/CatchEventAnalyzer.java:55-160): the job must be ACTIVATABLE or
+  // ACTIVATED (JobCommandPreconditionChecker: NOT_FOUND / INVALID_STATE); the job takes the command's errorCode,
+  // errorMessage (limitString, 10 000) and variables; the catch event is looked up from the job's element
+  // instance up through its flow scopes, per scope the element's error events code-specific before a catch-all
+  // (the codes seen are the "available" ones).  Caught: JOB:ERROR_THROWN (JobErrorThrownApplier: throwError,
+  // then the task's job reference removed and the job deleted), then BpmnEventPublicationBehavior
+  // .throwErrorEvent -> EventHandle.activateElement: PROCESS_EVENT:TRIGGERING (the command's variables) and,
+  // an error boundary event interrupting, TERMINATE_ELEMENT of the task.  Not caught: the job's elementId
+  // becomes NO_CATCH_EVENT_FOUND, JOB:ERROR_THROWN (the job stays, ERROR_THROWN) and INCIDENT:CREATED
+  // (UNHANDLED_ERROR_EVENT, the analyzer's message; elementId the marker, jobKey, variableScopeKey = the
+  // element instance).  The command: errorCode's string id in `partition`, errorMessage's in
+  // `correlation_key`, its document in `aux`.
+  void throw_error(ORecord& cmd) {
+    if (cmd.job_ord >= 0) cmd.r.key = resolve(cmd.instance, (uint32_t)cmd.job_ord);
+    const int64_t jobKey = cmd.r.key;
+    auto jit = jobs_.find(jobKey);
+    const std::string pre = "Expected to throw an error for job with key '" + std::to_string(jobKey) + "', but ";
+    if (jit == jobs_.end()) { reject(cmd, ZBHIP_REJ_NOT_FOUND, pre + "no such job was found"); return; }
+    if (jit->second.failed || jit->second.error_thrown) {
+      reject(cmd, ZBHIP_REJ_INVALID_STATE,
+             pre + "it is in state '" + (jit->second.error_thrown ? "ERROR_THROWN" : "FAILED") + "'");
+      return;
+    }
+    JobRow& job = jit->second;
+    const std::string code = cmd.r.partition >= 0 && (uint32_t)cmd.r.partition < strs.size() ? strs[cmd.r.partition] : "";
+    const std::string msg =
+        limit_java_string(cmd.r.correlation_key < strs.size() ? strs[cmd.r.correlation_key] : std::string(), 10000);
+    // findErrorCatchEvent: from the job's element instance through its active, not interrupted flow scopes
+    std::vector<std::string> avail;
+    int catch_elem = -1;
+    int64_t scope = job.elementInstanceKey;
+    for (auto it = ei_.find(scope); it != ei_.end() && catch_elem < 0;) {
+      const ElementInstance& inst = it->second;
+      if (!(inst.state == ZBHIP_PI_ELEMENT_ACTIVATING || inst.state == ZBHIP_PI_ELEMENT_ACTIVATED) ||
+          es_interrupted_.count(inst.key))
+        break;
+      const OEl& el = E(inst.value);
+      if (el.boundary >= 0 && P(inst.value.proc).els[el.boundary].event == ZBHIP_EV_ERROR) {
+        const std::string& bc = P(inst.value.proc).els[el.boundary].error_code;
+        avail.push_back(bc);
+        if (bc.empty() || bc == code) {
+          catch_elem = el.boundary;
+          scope = inst.key;
+          break;
+        }
+      }
+      it = ei_.find(inst.parentKey);
+    }
+    auto put = [&](const char* elem_marker) {  // JOB:ERROR_THROWN with the stored job + the command's fields
+      ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_ERROR_THROWN, jobKey);
+      rec.r.process_idx = job.pi.proc;
+      rec.r.element_idx = job.pi.elem;
+      rec.r.scope_key = job.elementInstanceKey;
+      rec.r.process_instance_key = job.pi.piKey;
+      rec.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
+      rec.doc = cmd.doc;
+      JobRow shown = job;
+      shown.fail_fields = true;  // (the errorMessage travels as a failed job's does)
+      shown.error_message = msg;
+      job_activation_fields(rec, shown);
+      // errorCode's string id: reason_arg bit 2, in interrupting | pad[0] << 8 | pad[1] << 16
+      const uint32_t cid = intern_string(code);
+      rec.r.reason_arg |= 4 | (elem_marker ? 8 : 0);  // (bit 3: elementId NO_CATCH_EVENT_FOUND)
+      rec.r.interrupting = (uint8_t)cid;
+      rec.r.pad[0] = (uint8_t)(cid >> 8);
+      rec.r.pad[1] = (uint8_t)(cid >> 16);
+    };
+    if (catch_elem < 0) {
+      job.no_catch = true;
+      put("NO_CATCH_EVENT_FOUND");
+      // DbJobState.throwError: the record (errorCode, errorMessage, the marker) stored, ERROR_THROWN, not
+      // activatable, out of JOB_DEADLINES
+      job.error_thrown = true;
+      job.error_code = code;
+      job.error_message = msg;
+      job.fail_fields = true;
+      job.activated = false;
+      activatable_.erase({job.type, "<default>", jobKey});
+      std::string text = "Expected to throw an error event with the code '" + code + "'" +
+                         (msg.empty() ? std::string() : " with message '" + msg + "'") + ", but it was not caught.";
+      if (avail.empty()) {
+        text += " No error events are available in the scope.";
+      } else {
+        text += " Available error events are [";
+        for (size_t i = 0; i < avail.size(); ++i) text += (i ? ", " : "") + avail[i];
+        text += "]";
+      }
+      const int64_t key = next_key();
+      ORecord& in = append(ZBHIP_RT_EVENT, ZBHIP_VT_INCIDENT, ZBHIP_INCIDENT_CREATED, key);
+      in.r.process_idx = job.pi.proc;
+      in.r.element_idx = job.pi.elem;
+      in.r.reason_arg = 8;  // elementId NO_CATCH_EVENT_FOUND
+      in.r.scope_key = job.elementInstanceKey;
+      in.r.process_instance_key = job.pi.piKey;
+      in.r.partition = ZBHIP_ERR_UNHANDLED_ERROR_EVENT;
+      in.r.aux = jobKey;
+      in.r.correlation_key = intern_string(text);
+      IncidentRow row;
+      row.pi = job.pi;
+      row.eik = job.elementInstanceKey;
+      row.error_type = ZBHIP_ERR_UNHANDLED_ERROR_EVENT;
+      row.job_key = jobKey;
+      row.message = text;
+      row.no_catch = true;
+      incidents_[key] = row;
+      incident_jobs_[jobKey] = key;
+      return;
+    }
+    // (the task not active / its event scope not accepting: rejections naming ElementInstance.toString --
+    // outside the restatement)
+    if (!can_trigger(scope, catch_elem, job.pi.proc)) throw Unsupported{"THROW_ERROR into a scope not accepting events"};
+    put(nullptr);
+    // JobErrorThrownApplier: the task's job reference removed, the job deleted
+    const JobRow gone = job;
+    ei_.at(job.elementInstanceKey).jobKey = -1;
+    activatable_.erase({gone.type, "<default>", jobKey});
+    jobs_.erase(jit);
+    // throwErrorEvent -> EventHandle.activateElement (common/EventHandle.java:104-150)
+    const ElementInstance task = ei_.at(scope);
+    const int64_t eventKey = next_key();
+    ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
+    pe.r.process_idx = task.value.proc;
+    pe.r.element_idx = catch_elem;
+    pe.r.scope_key = scope;
+    pe.r.process_instance_key = task.value.piKey;
+    pe.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
+    pe.doc = cmd.doc;
+    trigger_event(scope, eventKey, catch_elem, task.value.proc, cmd.doc, task.value.piKey);
+    pi_command(scope, ZBHIP_PI_TERMINATE_ELEMENT, task.value);
+  }
+
   // BpmnJobActivationBehavior.publishWork (processing/bpmn/behavior/BpmnJobActivationBehavior.java:61-100):
   // with a job stream for the job's type, JOB_BATCH:ACTIVATED (key = nextKey) of that one job -- deadline
   // = now + the stream's timeout, its worker -- applied at once (JobBatchActivatedApplier ->
@@ -3497,9 +3669,9 @@ class Oracle {
           const OEl& b = P(v.proc).els[el.boundary];
           if (b.event == ZBHIP_EV_MESSAGE) {
             if (!subscribe_to_message(b, key, bv, v.flowScopeKey, key, v)) break;  // incident on the task
-          } else {
+          } else if (b.event == ZBHIP_EV_TIMER) {
             subscribe_to_timer(b, key, bv);
-          }
+          }  // (an error boundary event subscribes to nothing: JOB:THROW_ERROR looks it up)
         }
         // BpmnJobBehavior.createNewJob -> writeJobCreatedEvent (behavior/BpmnJobBehavior.java:113-119,194-218)
         JobRow job;
@@ -3693,8 +3865,9 @@ class Oracle {
     if (found && fs_active && !es_interrupted_.count(v.flowScopeKey)) {
       const int64_t eventKey = tit->first.second;
       const int target = tit->second.elem;
+      const Doc vars = tit->second.vars;  // (the event trigger read before the scope's removal)
       pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);  // transitionToTerminated
-      activate_triggered_event(eventKey, target, key, v.flowScopeKey, v);
+      activate_triggered_event(eventKey, target, key, v.flowScopeKey, v, &vars);
       return;
     }
     // no event trigger: transitionToTerminated, onElementTerminated
@@ -3776,13 +3949,16 @@ class Oracle {
   // EventTriggerBehavior.activateTriggeredEvent (processing/common/EventTriggerBehavior.java:191-244):
   // PROCESS_EVENT:TRIGGERED (the trigger's key), ACTIVATING + ACTIVATED of the triggered event
   // (+key, flow scope = the given one), COMPLETE_ELEMENT
-  void activate_triggered_event(int64_t eventKey, int target, int64_t scope, int64_t flowScopeKey, const PiValue& v) {
+  void activate_triggered_event(int64_t eventKey, int target, int64_t scope, int64_t flowScopeKey, const PiValue& v,
+                                const Doc* trigger_vars = nullptr) {
     ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERED, eventKey);
     pe.r.process_idx = v.proc;
     pe.r.element_idx = target;
     pe.r.scope_key = scope;
     pe.r.process_instance_key = v.piKey;
     pe.r.aux = -1;
+    auto tr = triggers_.find({scope, eventKey});
+    const Doc vars = trigger_vars ? *trigger_vars : tr != triggers_.end() ? tr->second.vars : Doc{0, 0};
     triggers_.erase({scope, eventKey});  // ProcessEventTriggeredApplier: deleteTrigger (if it exists)
     PiValue bv = v;
     bv.elem = target;
@@ -3790,6 +3966,8 @@ class Oracle {
     const int64_t bk = next_key();
     pi_event(bk, ZBHIP_PI_ELEMENT_ACTIVATING, bv);
     pi_event(bk, ZBHIP_PI_ELEMENT_ACTIVATED, bv);
+    // the event's variables become local variables of the event instance (for its output mappings)
+    if (vars.count > 0) merge_local_document(bk, v.proc, v.piKey, vars);
     pi_command(bk, ZBHIP_PI_COMPLETE_ELEMENT, bv);
   }
 
@@ -4256,14 +4434,17 @@ std::string Oracle::dump_state() const {
              "JOBS|%lld|type=%s,retries=%d,elementId=%s,elementInstanceKey=%lld,processInstanceKey=%lld,"
              "bpmnProcessId=%s,processDefinitionKey=%lld,processDefinitionVersion=%d,tenantId=<default>,"
              "deadline=%lld,worker=",
-             (long long)k, j.type.c_str(), j.retries, p.els[j.pi.elem].id.c_str(), (long long)j.elementInstanceKey,
-             (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version, (long long)j.deadline);
+             (long long)k, j.type.c_str(), j.retries, j.no_catch ? "NO_CATCH_EVENT_FOUND" : p.els[j.pi.elem].id.c_str(),
+             (long long)j.elementInstanceKey, (long long)j.pi.piKey, p.bpmn_id.c_str(), (long long)p.def_key, p.version,
+             (long long)j.deadline);
     // (worker and errorMessage appended unbounded: a message holds up to 10 000 characters)
     rows.push_back(std::string(buf) + j.worker +
                    (j.fail_fields ? ",errorMessageHex=" + hex_of(j.error_message) + ",retryBackoff=" +
                                         std::to_string(j.retry_backoff) + ",recurringTime=" + std::to_string(j.recurring_time)
-                                  : std::string()));
-    snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", (long long)k, j.failed ? "FAILED" : j.activated ? "ACTIVATED" : "ACTIVATABLE");
+                                  : std::string()) +
+                   (j.error_thrown ? ",errorCodeHex=" + hex_of(j.error_code) : std::string()));
+    snprintf(buf, sizeof buf, "JOB_STATES|%lld|%s", (long long)k,
+             j.error_thrown ? "ERROR_THROWN" : j.failed ? "FAILED" : j.activated ? "ACTIVATED" : "ACTIVATABLE");
     rows.push_back(buf);
     if (j.failed && j.retries > 0 && j.retry_backoff > 0) {  // JOB_BACKOFF [recurringTime, jobKey] -> DbNil
       snprintf(buf, sizeof buf, "JOB_BACKOFF|%lld|%lld", (long long)j.recurring_time, (long long)k);
@@ -4280,7 +4461,7 @@ std::string Oracle::dump_state() const {
              "INCIDENTS|%lld|errorType=%d,flow=%d,result=%d,processDefinitionKey=%lld,processInstanceKey=%lld,"
              "elementId=%s,elementInstanceKey=%lld",
              (long long)k, in.error_type, in.flow, in.result, (long long)p.def_key, (long long)in.pi.piKey,
-             p.els[in.pi.elem].id.c_str(), (long long)in.eik);
+             in.no_catch ? "NO_CATCH_EVENT_FOUND" : p.els[in.pi.elem].id.c_str(), (long long)in.eik);
     rows.push_back(std::string(buf) +
                    (in.job_key >= 0 ? ",jobKey=" + std::to_string(in.job_key) + ",messageHex=" + hex_of(in.message) : ""));
   }

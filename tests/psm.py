@@ -675,6 +675,9 @@ class OracleEngine:
             self.next_slot += 1
         elif vt == abi.VT_TIMER:
             r["aux"] = v["dueDate"]
+        elif vt == abi.VT_JOB and it == abi.JOB_THROW_ERROR:  # zb_oracle.cpp throw_error's command fields
+            r["partition"] = self.o.intern_string(v.get("errorCode", ""))
+            r["correlation_key"] = self.o.intern_string(v["errorMessage"]) if v.get("errorMessage") else abi.NO_STRING
         elif vt == abi.VT_JOB and it == abi.JOB_FAIL:  # zb_oracle.cpp fail_job's command fields
             r["partition"] = v.get("retries", 0)
             r["message_key"] = v.get("retryBackoff", 0)
@@ -816,6 +819,13 @@ class Client:
         """JobClient.fail (util/client/JobClient.java): JOB:FAIL with retries and an errorMessage."""
         return Rec(abi.RT_COMMAND, abi.VT_JOB, abi.JOB_FAIL, key,
                    {"retries": retries, "errorMessage": error_message, "retryBackoff": 0, "variables": tuple(variables),
+                    "tenantId": "<default>"})
+
+    @staticmethod
+    def throw_error(key, error_code, error_message="", variables=()):
+        """JobClient.withErrorCode(..).throwError (util/client/JobClient.java): JOB:THROW_ERROR."""
+        return Rec(abi.RT_COMMAND, abi.VT_JOB, abi.JOB_THROW_ERROR, key,
+                   {"errorCode": error_code, "errorMessage": error_message, "variables": tuple(variables),
                     "tenantId": "<default>"})
 
     @staticmethod

@@ -1,0 +1,59 @@
+"""Error boundary events in the reference's processing loop.  A process whose job worker tasks carry error
+boundary events runs on the device (the boundary subscribes to nothing); a JOB:THROW_ERROR of a device job
+moves the instance to the engine first (the adapter's held-instance hand-off: its zb-db rows -- the task's
+event scope with the boundary event among its interrupting and boundary ids -- into the engine's state),
+whose JobThrowErrorProcessor then catches it at the boundary event or raises UNHANDLED_ERROR_EVENT
+(oracle pinned by tests/test_oracle_error_events.py).  The same workload through the loop over the engine
+alone and through [adapter, engine]: every log and state equal, at batch limits 3 and 100."""
+import pytest
+
+from psm import Client, open_jobs
+from test_gpu_scheduled import KEY_A, KEY_B, check, single, write
+from zeebe_amd import abi, bpmn
+
+pytestmark = pytest.mark.gpu
+
+
+def processes():
+    a = (bpmn.createExecutableProcess("errors").startEvent("start").serviceTask("task", "work")
+         .boundaryEvent("on-error").error("E1").serviceTask("recover", "recover").endEvent("end-error")
+         .moveToActivity("task").serviceTask("next", "work-2").endEvent("end").done())
+    b = (bpmn.createExecutableProcess("catchAll").startEvent("s").serviceTask("t", "work")
+         .boundaryEvent("any").error().endEvent("e2").moveToActivity("t").endEvent("e1").done())
+    return a, b
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_error_boundary_events_in_the_processing_loop(limit):
+    a, b = processes()
+    deps = [(a, KEY_A, 1), (b, KEY_B, 1)]
+    ref, gpu = single(deps, deps, limit=limit)
+    write(ref, gpu, *([Client.create("errors") for _ in range(10)] + [Client.create("catchAll") for _ in range(4)]))
+    assert gpu.parts[0].adapter.counts["device_commands"] >= 14
+    jobs = sorted(k for k, r in open_jobs(ref.parts[0].log).items() if r.value["type"] == "work")
+    # caught (code-specific / catch-all), with variables, uncaught (incident), rejections, completions
+    write(ref, gpu, Client.throw_error(jobs[0], "E1"), Client.throw_error(jobs[1], "E1", "with message"),
+          Client.throw_error(jobs[2], "E1", "", variables=(("reason", "bad"),)),
+          Client.throw_error(jobs[3], "other", "not caught"), Client.throw_error(jobs[10], "anything"),
+          Client.throw_error(123, "E1"), Client.complete_job(jobs[4]))
+    write(ref, gpu, Client.throw_error(jobs[3], "E1"), Client.complete_job(jobs[5]), Client.throw_error(jobs[4], "E1"))
+    # the recovering and the remaining tasks complete
+    for _ in range(3):
+        live = sorted(k for k, r in open_jobs(ref.parts[0].log).items() if r.value["type"] != "work" or k in jobs[6:10])
+        if not live:
+            break
+        write(ref, gpu, *[Client.complete_job(k) for k in live])
+    check(ref, gpu)
+    log = gpu.parts[0].log.entries
+    thrown = [r for r in log if r.value_type == abi.VT_JOB and r.intent == abi.JOB_ERROR_THROWN]
+    assert len(thrown) == 5
+    assert any(r.value["elementId"] == "NO_CATCH_EVENT_FOUND" for r in thrown)
+    assert [r for r in log if r.value_type == abi.VT_INCIDENT and r.value["errorType"] == "UNHANDLED_ERROR_EVENT"]
+    assert [r for r in log if r.value_type == abi.VT_VARIABLE and r.value["name"] == "reason"]
+    done = sum(1 for r in log if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_COMPLETED
+               and r.value["bpmnElementType"] == "PROCESS")
+    assert done == 10  # (the incident instance waits; three catchAll tasks stay open)
+    ad = gpu.parts[0].adapter
+    # one hand-off per thrown error (a throw for a completed job still resolving to its running instance moves
+    # that instance too: the engine rejects it, NOT_FOUND), no declines
+    assert 5 <= len(ad.handed_off) <= 6 and not ad.fallback_reasons

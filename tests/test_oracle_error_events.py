@@ -1,0 +1,138 @@
+"""The oracle's error boundary events and JOB:THROW_ERROR (zb_oracle.cpp throw_error; JobThrowErrorProcessor
+.java:84-176, CatchEventAnalyzer.java:55-160, JobErrorThrownApplier, BpmnEventPublicationBehavior
+.throwErrorEvent -> EventHandle.activateElement, EventTriggerBehavior.activateTriggeredEvent) pinned on the
+reference's ErrorEventTest, ErrorEventIncidentTest and JobThrowErrorTest (engine/src/test/.../processing/
+{bpmn/error,incident,job}), run through the restated processing loop (tests/psm.py, one partition over the
+oracle engine).  One boundary event per activity: the cases with two error boundary events on one task
+(shouldCatchErrorEventsByErrorCode, ...WithSpecificErrorCode) are outside the subset."""
+from psm import Client
+from test_gpu_scheduled import KEY_A
+from test_oracle_message_ttl import cluster, of, write
+from zeebe_amd import abi, bpmn
+
+JOB_TYPE, ERROR_CODE = "test", "ERROR"
+
+
+def process(code=ERROR_CODE, boundary=True):
+    # ErrorEventTest.process(...) with serviceTask.boundaryEvent("error", b -> b.error(code)).endEvent()
+    b = bpmn.createExecutableProcess("wf").startEvent("start").serviceTask("task", JOB_TYPE)
+    if boundary:
+        b.boundaryEvent("error").error(code).endEvent("end-error").moveToActivity("task")
+    return b.endEvent("end").done()
+
+
+def started(cl, xml):
+    e = write(cl, Client.create("wf"))
+    job = of(e, abi.VT_JOB, abi.JOB_CREATED)[0]
+    pik = job.value["processInstanceKey"]
+    return job, pik
+
+
+def pi_of(cl, pik):
+    return [(r.value["bpmnElementType"], abi.PI_INTENTS[r.intent]) for r in cl.parts[0].log.entries
+            if r.value_type == abi.VT_PROCESS_INSTANCE and r.value["processInstanceKey"] == pik]
+
+
+def subsequence(got, want):
+    it = iter(got)
+    return all(w in it for w in want)
+
+
+def test_error_boundary_event_is_triggered():
+    # ErrorEventTest.shouldTriggerEvent (:60-97) and shouldNotCancelJob (:429-448)
+    cl = cluster((process(), KEY_A, 1))
+    job, pik = started(cl, None)
+    e = write(cl, Client.throw_error(job.key, ERROR_CODE))
+    thrown = of(e, abi.VT_JOB, abi.JOB_ERROR_THROWN)
+    assert len(thrown) == 1 and thrown[0].key == job.key
+    assert thrown[0].value["errorCode"] == ERROR_CODE and thrown[0].value["elementId"] == "task"
+    assert subsequence(pi_of(cl, pik), [
+        ("SERVICE_TASK", "ELEMENT_TERMINATING"), ("SERVICE_TASK", "ELEMENT_TERMINATED"),
+        ("BOUNDARY_EVENT", "ELEMENT_ACTIVATING"), ("BOUNDARY_EVENT", "ELEMENT_ACTIVATED"),
+        ("BOUNDARY_EVENT", "COMPLETE_ELEMENT"), ("BOUNDARY_EVENT", "ELEMENT_COMPLETING"),
+        ("BOUNDARY_EVENT", "ELEMENT_COMPLETED"), ("SEQUENCE_FLOW", "SEQUENCE_FLOW_TAKEN"),
+        ("END_EVENT", "ELEMENT_ACTIVATING"), ("END_EVENT", "ELEMENT_ACTIVATED"), ("END_EVENT", "ELEMENT_COMPLETING"),
+        ("END_EVENT", "ELEMENT_COMPLETED"), ("PROCESS", "COMPLETE_ELEMENT"), ("PROCESS", "ELEMENT_COMPLETING"),
+        ("PROCESS", "ELEMENT_COMPLETED")])
+    jobs = [abi.JOB_INTENTS[r.intent] for r in cl.parts[0].log.entries if r.value_type == abi.VT_JOB]
+    assert jobs == ["CREATED", "THROW_ERROR", "ERROR_THROWN"]
+    # the boundary event was triggered through the task's event scope: TRIGGERING then TRIGGERED
+    pe = [r for r in e if r.value_type == abi.VT_PROCESS_EVENT]
+    assert [r.intent for r in pe] == [abi.PE_TRIGGERING, abi.PE_TRIGGERED] and pe[0].value["targetElementId"] == "error"
+    assert not [r for r in cl.parts[0].state() if r.startswith(("JOBS|", "JOB_STATES|"))]
+
+
+def test_numeric_and_catch_all_error_codes():
+    # shouldCatchErrorEventsByNumericErrorCode (:148-191); ...OnBoundaryEventWithoutErrorRef (:194-224);
+    # ...WithoutErrorCode (:227-254)
+    for code, thrown in (("404", "404"), ("", "error"), (None, "error")):
+        xml = process(code) if code is not None else process("").replace(' errorRef="Error_error"', "")
+        cl = cluster((xml, KEY_A, 1))
+        job, pik = started(cl, None)
+        write(cl, Client.throw_error(job.key, thrown))
+        assert ("BOUNDARY_EVENT", "ELEMENT_COMPLETED") in pi_of(cl, pik)
+        assert pi_of(cl, pik)[-1] == ("PROCESS", "ELEMENT_COMPLETED")
+
+
+def test_uncaught_error_creates_an_incident():
+    # ErrorEventIncidentTest.shouldCreateIncidentWhenThrownErrorIsUncaught (:92-123) and
+    # shouldCreateIncidentWithDefaultErrorMessage (:125-156); JobThrowErrorTest (:397-445) without a boundary
+    cl = cluster((process("error"), KEY_A, 1))
+    job, pik = started(cl, None)
+    e = write(cl, Client.throw_error(job.key, "other-error", "error thrown"))
+    thrown = of(e, abi.VT_JOB, abi.JOB_ERROR_THROWN)[0]
+    assert thrown.value["elementId"] == "NO_CATCH_EVENT_FOUND" and thrown.value["errorMessage"] == "error thrown"
+    inc = of(e, abi.VT_INCIDENT, abi.INCIDENT_CREATED)[0].value
+    assert inc["errorType"] == "UNHANDLED_ERROR_EVENT"
+    assert inc["errorMessage"] == ("Expected to throw an error event with the code 'other-error' with message 'error thrown', "
+                                   "but it was not caught. Available error events are [error]")
+    assert (inc["elementId"], inc["elementInstanceKey"], inc["variableScopeKey"], inc["jobKey"], inc["processInstanceKey"]) == \
+        (thrown.value["elementId"], thrown.value["elementInstanceKey"], thrown.value["elementInstanceKey"], thrown.key, pik)
+    # the job stays, ERROR_THROWN: a second throw is rejected (JobThrowErrorTest.shouldRejectIfErrorIsThrown :100-114)
+    e = write(cl, Client.throw_error(job.key, "error"))
+    rej = [r for r in e if r.record_type == abi.RT_REJECTION]
+    assert rej and rej[0].rejection_type == abi.REJ_INVALID_STATE and "it is in state 'ERROR_THROWN'" in rej[0].rejection_reason
+    state = cl.parts[0].state()
+    assert "JOB_STATES|%d|ERROR_THROWN" % job.key in state
+    cl = cluster((process(boundary=False), KEY_A, 1))
+    job, _ = started(cl, None)
+    e = write(cl, Client.throw_error(job.key, "other-error"))
+    assert of(e, abi.VT_INCIDENT, abi.INCIDENT_CREATED)[0].value["errorMessage"] == \
+        "Expected to throw an error event with the code 'other-error', but it was not caught. No error events are available in the scope."
+
+
+def test_rejections_and_truncation():
+    # JobThrowErrorTest.shouldRejectIfJobNotFound (:70-81), shouldRejectIfJobIsFailed (:83-98),
+    # shouldTruncateErrorMessage (:396-419)
+    cl = cluster((process(), KEY_A, 1))
+    e = write(cl, Client.throw_error(123, "error"))
+    assert e[-1].record_type == abi.RT_REJECTION and e[-1].rejection_type == abi.REJ_NOT_FOUND
+    assert e[-1].rejection_reason == "Expected to throw an error for job with key '123', but no such job was found"
+    job, _ = started(cl, None)
+    write(cl, Client.fail_job(job.key, 0))
+    e = write(cl, Client.throw_error(job.key, "error"))
+    assert e[-1].rejection_type == abi.REJ_INVALID_STATE and "it is in state 'FAILED'" in e[-1].rejection_reason
+    # shouldTruncateErrorMessage (:395-419) / shouldNotTruncateErrorMessage (:421-445): limitString to 10 000
+    # characters and "...", no error code
+    for n, want in ((10001, "*" * 10000 + "..."), (10000, "*" * 10000)):
+        cl = cluster((process(boundary=False), KEY_A, 1))
+        job, _ = started(cl, None)
+        e = write(cl, Client.throw_error(job.key, "", "*" * n))
+        assert of(e, abi.VT_JOB, abi.JOB_ERROR_THROWN)[0].value["errorMessage"] == want
+        assert of(e, abi.VT_INCIDENT, abi.INCIDENT_CREATED)[0].value["errorMessage"] == (
+            "Expected to throw an error event with the code '' with message '" + want +
+            "', but it was not caught. No error events are available in the scope.")
+
+
+def test_error_variables_are_local_to_the_catch_event():
+    # JobThrowErrorTest.shouldThrowErrorWithVariables (:116-167): one VARIABLE:CREATED, at the error catch event
+    cl = cluster((process(), KEY_A, 1))
+    job, pik = started(cl, None)
+    e = write(cl, Client.throw_error(job.key, ERROR_CODE, "error-message", variables=[("foo", "bar")]))
+    thrown = of(e, abi.VT_JOB, abi.JOB_ERROR_THROWN)[0]
+    assert dict(thrown.value["variables"]) == {"foo": "bar"} and thrown.value["errorMessage"] == "error-message"
+    boundary = [r for r in e if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_ACTIVATING
+                and r.value["elementId"] == "error"][0]
+    var = [r for r in e if r.value_type == abi.VT_VARIABLE]
+    assert [(r.value["name"], r.value["value"], r.value["scopeKey"], r.intent) for r in var] == \
+        [("foo", "bar", boundary.key, abi.VAR_CREATED)]

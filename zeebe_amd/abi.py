@@ -25,7 +25,8 @@ VT_PROCESS_INSTANCE_BATCH = 34
 VT_INCIDENT = 6
 INCIDENT_CREATED = 0
 ERR_JOB_NO_RETRIES, ERR_CONDITION_ERROR, ERR_EXTRACT_VALUE_ERROR = 2, 3, 4  # ErrorType ordinals
-ERROR_TYPES = {2: "JOB_NO_RETRIES", 3: "CONDITION_ERROR", 4: "EXTRACT_VALUE_ERROR"}
+ERR_UNHANDLED_ERROR_EVENT = 6
+ERROR_TYPES = {2: "JOB_NO_RETRIES", 3: "CONDITION_ERROR", 4: "EXTRACT_VALUE_ERROR", 6: "UNHANDLED_ERROR_EVENT"}
 FEEL_NULL, FEEL_NUMBER, FEEL_STRING = 0, 1, 2       # zbhip_record.reason_arg of an INCIDENT
 
 REJ_INVALID_ARGUMENT, REJ_NOT_FOUND, REJ_ALREADY_EXISTS, REJ_INVALID_STATE = 0, 1, 2, 3
@@ -41,7 +42,8 @@ PI_INTENT_IDS = {v: k for k, v in PI_INTENTS.items()}
 PI_SEQUENCE_FLOW_TAKEN, PI_ELEMENT_ACTIVATING, PI_ELEMENT_ACTIVATED = 1, 2, 3
 PI_ELEMENT_COMPLETING, PI_ELEMENT_COMPLETED, PI_ELEMENT_TERMINATED = 4, 5, 7
 JOB_INTENTS = {0: "CREATED", 1: "COMPLETE", 2: "COMPLETED", 3: "TIME_OUT", 4: "TIMED_OUT", 5: "FAIL", 6: "FAILED",
-               10: "CANCELED"}
+               10: "CANCELED", 11: "THROW_ERROR", 12: "ERROR_THROWN"}
+JOB_THROW_ERROR, JOB_ERROR_THROWN = 11, 12
 JOB_CREATED, JOB_COMPLETE, JOB_COMPLETED, JOB_CANCELED = 0, 1, 2, 10
 JOB_TIME_OUT, JOB_TIMED_OUT, JOB_FAIL, JOB_FAILED = 3, 4, 5, 6
 VAR_INTENTS = {0: "CREATED", 1: "UPDATED"}

@@ -205,6 +205,13 @@ class RecordValues:
                 eid = int(r["message_name"]) | int(r["bpmn_process_id"]) << 16
                 v.update({"retries": int(r["partition"]),
                           "errorMessage": self.string_value(eid) if eid != abi.NO_STRING else ""})
+            if int(r["record_type"]) == abi.RT_EVENT and int(r["reason_arg"]) & 4:
+                # JOB:ERROR_THROWN (JobThrowErrorProcessor): the errorCode (bit 2) and, no catch event, the
+                # NO_CATCH_EVENT_FOUND elementId (bit 3)
+                cid = int(r["interrupting"]) | int(r["pad"][0]) << 8 | int(r["pad"][1]) << 16
+                v["errorCode"] = self.string_value(cid)
+                if int(r["reason_arg"]) & 8:
+                    v["elementId"] = "NO_CATCH_EVENT_FOUND"
             return v
         if vt == VT_JOB_BATCH:
             # a job stream's push (BpmnJobActivationBehavior.publishWork :61-100): a fresh JobBatchRecord
@@ -216,13 +223,15 @@ class RecordValues:
                     "tenantIds": ()}
         if vt == abi.VT_INCIDENT:  # IncidentRecord.java:36-47
             et = int(r["partition"])
-            job = et == abi.ERR_JOB_NO_RETRIES
+            job = et in (abi.ERR_JOB_NO_RETRIES, abi.ERR_UNHANDLED_ERROR_EVENT)
             msg = self.string_value(int(r["correlation_key"])) if job else \
                 (self.incident_message(r) if self.incident_message else "")
+            no_catch = et == abi.ERR_UNHANDLED_ERROR_EVENT and int(r["reason_arg"]) & 8
             return {"errorType": abi.ERROR_TYPES.get(et, str(et)), "errorMessage": msg,
                     "bpmnProcessId": p.bpmn_process_id, "processDefinitionKey": p.definition_key,
-                    "processInstanceKey": pik, "elementId": p.element_ids[elem], "elementInstanceKey": scope,
-                    "jobKey": aux if job else -1, "variableScopeKey": scope, "tenantId": TENANT}
+                    "processInstanceKey": pik, "elementId": "NO_CATCH_EVENT_FOUND" if no_catch else p.element_ids[elem],
+                    "elementInstanceKey": scope, "jobKey": aux if job else -1, "variableScopeKey": scope,
+                    "tenantId": TENANT}
         if vt == abi.VT_VARIABLE:
             # ZBHIP_AUX_INLINE: a value the engine computed (multi-instance loop variables)
             val = typed_value(int(r["partition"]), int(r["message_key"]), self.string_value, self.list_items) \

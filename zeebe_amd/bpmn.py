@@ -164,6 +164,12 @@ class ProcessBuilder:
         self._pending_flow = None
         return self
 
+    def error(self, error_code=None):
+        """BoundaryEventBuilder.error(code): an <errorEventDefinition> referring to an <error errorCode>;
+        no code: a catch-all errorEventDefinition without errorRef."""
+        self.current.error = error_code if error_code is not None else ""
+        return self
+
     def multiInstance(self, input_collection, input_element=None, sequential=False, **extra):
         """AbstractActivityBuilder.multiInstance(b -> b.zeebeInputCollectionExpression(..)
         .zeebeInputElement(..).sequential()/.parallel()): a <multiInstanceLoopCharacteristics> with a
@@ -280,6 +286,7 @@ class ProcessBuilder:
                % (BPMN_NS, ZEEBE_NS, BPMN_NS),
                '  <process id=%s isExecutable="true">' % quoteattr(self.process_id)]
         catches = []
+        errors = []
 
         def render(children, ind):
             for c in children:
@@ -324,6 +331,11 @@ class ProcessBuilder:
                         catches.append(c)
                         body = '<messageEventDefinition id=%s messageRef=%s/>' % (quoteattr(c.id + "_med"),
                                                                                 quoteattr(c.message[0]))
+                    elif getattr(c, "error", None) is not None:
+                        ref = ' errorRef=%s' % quoteattr("Error_" + c.id) if c.error else ""
+                        if c.error:
+                            errors.append(c)
+                        body = '<errorEventDefinition id=%s%s/>' % (quoteattr(c.id + "_eed"), ref)
                     out.append('%s<boundaryEvent id=%s attachedToRef=%s%s>%s</boundaryEvent>'
                                % (ind, quoteattr(c.id), quoteattr(c.attached_to), cancel, body))
                 elif c.kind == "exclusiveGateway" and c.default:
@@ -368,6 +380,8 @@ class ProcessBuilder:
                 continue
             out.append('  <message id=%s name=%s><extensionElements><zeebe:subscription correlationKey=%s/>'
                        '</extensionElements></message>' % tuple(quoteattr(x) for x in c.message))
+        for c in errors:
+            out.append('  <error id=%s errorCode=%s/>' % (quoteattr("Error_" + c.id), quoteattr(c.error)))
         out.append("</definitions>")
         return "\n".join(out) + "\n"
 

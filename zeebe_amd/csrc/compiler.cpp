@@ -800,6 +800,10 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     }
     messages[*c.get("id")] = m;
   }
+  // <error> elements of the definitions (ErrorTransformer): static error codes
+  std::unordered_map<std::string, std::string> errors;
+  for (auto& c : root.children)
+    if (c.tag == "error" && c.get("id")) errors[*c.get("id")] = c.get("errorCode") ? *c.get("errorCode") : "";
   C.csr.bpmn_process_id = C.str(pid);
   C.elements.push_back(blank(ZBHIP_EL_PROCESS, C.csr.bpmn_process_id));
   C.elements[0].flow_scope = 0;
@@ -871,7 +875,35 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         }
         if (int rc = parse_mappings(c.first("extensionElements"), (uint16_t)C.elements.size(), C, err)) return rc;
       }
-      if (type == ZBHIP_EL_BOUNDARY_EVENT && c.first("messageEventDefinition")) {
+      if (type == ZBHIP_EL_BOUNDARY_EVENT && c.first("errorEventDefinition")) {
+        // an error boundary event on a job worker task (BoundaryEventTransformer, ErrorTransformer):
+        // interrupting, a static errorCode ("" -- no errorRef, or an <error> without a code -- catches every
+        // code); nothing to subscribe: JOB:THROW_ERROR finds it (CatchEventAnalyzer), and the adapter hands
+        // the instance to the engine for that command
+        const Elem* eed = c.first("errorEventDefinition");
+        for (auto& d : c.children)
+          if (&d != eed && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+            err = "event definition <" + d.tag + "> outside the supported subset";
+            return ZBHIP_EUNSUPP;
+          }
+        const std::string* ca = c.get("cancelActivity");
+        if (ca && *ca == "false") { err = "a non-interrupting error boundary event"; return ZBHIP_EPARSE; }
+        std::string code;
+        if (const std::string* ref = eed->get("errorRef")) {
+          auto ei = errors.find(*ref);
+          if (ei == errors.end()) { err = "unknown error " + *ref; return ZBHIP_EPARSE; }
+          code = ei->second;
+          if (!code.empty() && code[0] == '=') { err = "error code expressions outside the supported subset"; return ZBHIP_EUNSUPP; }
+        }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        const std::string* at = c.get("attachedToRef");
+        if (!at) { err = "boundary event without attachedToRef"; return ZBHIP_EPARSE; }
+        e.event_type = ZBHIP_EV_ERROR;
+        e.message_name = C.str(code);
+        e.job_retries = 1;  // interrupting
+        boundaries.push_back({(uint16_t)C.elements.size(), *at});
+      } else if (type == ZBHIP_EL_BOUNDARY_EVENT && c.first("messageEventDefinition")) {
         // BoundaryEventTransformer + CatchEventTransformer.transformMessageEventDefinition: a message
         // boundary event on a job worker task, interrupting or not (static name, `= variable`
         // correlation key, evaluated in the task's flow scope); attached after the walk

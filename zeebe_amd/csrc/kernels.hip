@@ -2034,7 +2034,8 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
             if (L.fail) return;
           }
           const uint32_t b = w.w & 0xFFFF;
-          if (b != 0xFFFF) {
+          // (an error boundary event subscribes to nothing: JOB:THROW_ERROR looks it up)
+          if (b != 0xFFFF && ((elem_of(L, b).x >> 8) & 0xFF) != ZBHIP_EV_ERROR) {
             if (!L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
             const uint4 bw = elem_of(L, b);
             const uint32_t reps = (bw.w >> 8) & 0xFF;  // 1 a duration, a cycle's count, 255 infinite
@@ -2048,7 +2049,7 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
         if constexpr (K::M) {
           // subscribeToEvents: the attached message boundary event's subscription before the job
           const uint32_t b = w.w & 0xFFFF;
-          if (b != 0xFFFF) {
+          if (b != 0xFFFF && ((elem_of(L, b).x >> 8) & 0xFF) != ZBHIP_EV_ERROR) {
             const uint4 bw = elem_of(L, b);
             if (((bw.x >> 8) & 0xFF) != ZBHIP_EV_MESSAGE) { set_fail(L, FB_UNSUPPORTED); return; }
             subscribe_message(L, b, bw, key, true);

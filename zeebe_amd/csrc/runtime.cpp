@@ -1415,7 +1415,9 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     const zbhip_element& E = P.els[e];
     if (E.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
       const bool msg = E.event_type == ZBHIP_EV_MESSAGE && E.flow_scope == 0;
-      if ((E.event_type != ZBHIP_EV_TIMER && !msg) || E.flow_source >= P.els.size()) return ZBHIP_EUNSUPP;
+      // (an error boundary event: nothing on the device -- JOB:THROW_ERROR hands the instance off)
+      if ((E.event_type != ZBHIP_EV_TIMER && E.event_type != ZBHIP_EV_ERROR && !msg) || E.flow_source >= P.els.size())
+        return ZBHIP_EUNSUPP;
       const zbhip_element& A = P.els[E.flow_source];
       // (a timer boundary event on an embedded sub-process: zbhip_element.default_flow of the sub-process)
       const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS && E.event_type == ZBHIP_EV_TIMER && A.default_flow == e;
@@ -1441,6 +1443,8 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
     if ((e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || e.element_type == ZBHIP_EL_BOUNDARY_EVENT) &&
         e.event_type == ZBHIP_EV_TIMER) {
       P.has_timer = true;
+    } else if (e.element_type == ZBHIP_EL_BOUNDARY_EVENT && e.event_type == ZBHIP_EV_ERROR) {
+      // error boundary events: no device state (the instance moves to the engine for JOB:THROW_ERROR)
     } else if (e.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || e.element_type == ZBHIP_EL_BOUNDARY_EVENT) {
       // message catch events and message boundary events (KMsg)
       if (e.event_type != ZBHIP_EV_MESSAGE) return ZBHIP_EINVAL;
