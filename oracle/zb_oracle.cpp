@@ -965,8 +965,10 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
     if (it == idx.end()) { err = "boundary event attached to an unknown element"; return false; }
     OEl& a = P.els[it->second];
     // job worker tasks; embedded sub-processes with a timer boundary event (subscribed when their start
-    // event completes, StartEventProcessor.onComplete :52-67)
-    const bool sub_ok = a.type == ZBHIP_EL_SUB_PROCESS && P.els[b].event == ZBHIP_EV_TIMER;
+    // event completes, StartEventProcessor.onComplete :52-67) or an error boundary event (found by
+    // CatchEventAnalyzer's walk through the flow scopes of a job's task)
+    const bool sub_ok = a.type == ZBHIP_EL_SUB_PROCESS &&
+                        (P.els[b].event == ZBHIP_EV_TIMER || P.els[b].event == ZBHIP_EV_ERROR);
     if ((!ZBHIP_IS_JOB_WORKER(a.type) && !sub_ok) || a.scope != P.els[b].scope) {
       err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return false;
@@ -4000,7 +4002,8 @@ class Oracle {
       auto fit = ei_.find(v.flowScopeKey);
       if (fit != ei_.end()) {
         const OEl& fe = E(fit->second.value);
-        if (fe.type == ZBHIP_EL_SUB_PROCESS && fe.boundary >= 0) {
+        if (fe.type == ZBHIP_EL_SUB_PROCESS && fe.boundary >= 0 &&
+            P(fit->second.value.proc).els[fe.boundary].event == ZBHIP_EV_TIMER) {
           PiValue bv = fit->second.value;
           bv.elem = fe.boundary;
           subscribe_to_timer(P(bv.proc).els[fe.boundary], fit->first, bv);

@@ -57,3 +57,27 @@ def test_error_boundary_events_in_the_processing_loop(limit):
     # one hand-off per thrown error (a throw for a completed job still resolving to its running instance moves
     # that instance too: the engine rejects it, NOT_FOUND), no declines
     assert 5 <= len(ad.handed_off) <= 6 and not ad.fallback_reasons
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_error_boundary_events_on_sub_processes_in_the_processing_loop(limit):
+    # ErrorEventIncidentTest.BOUNDARY_EVENT_SUBPROCESS: caught inside, at the sub-process, or nowhere; the
+    # hand-off carries the sub-process's event scope (its boundary event among its interrupting ids)
+    from test_oracle_error_events import sub_process_boundaries
+    deps = [(sub_process_boundaries(), KEY_A, 1)]
+    ref, gpu = single(deps, deps, limit=limit)
+    write(ref, gpu, *[Client.create("wf") for _ in range(6)])
+    assert gpu.parts[0].adapter.counts["device_commands"] >= 6
+    jobs = sorted(open_jobs(ref.parts[0].log))
+    write(ref, gpu, Client.throw_error(jobs[0], "error_in_subprocess"), Client.throw_error(jobs[1], "error"),
+          Client.throw_error(jobs[2], "error", "", variables=(("why", "x"),)), Client.throw_error(jobs[3], "nope"),
+          Client.complete_job(jobs[4]))
+    write(ref, gpu, *[Client.complete_job(k) for k in sorted(open_jobs(ref.parts[0].log))])
+    check(ref, gpu)
+    log = gpu.parts[0].log.entries
+    done = [r.value["elementId"] for r in log if r.value_type == abi.VT_PROCESS_INSTANCE
+            and r.intent == abi.PI_ELEMENT_COMPLETED]
+    assert done.count("wf") == 5 and done.count("end_boundary") == 2 and done.count("end_boundary_in_subprocess") == 1
+    assert [r for r in log if r.value_type == abi.VT_VARIABLE and r.value["name"] == "why"]
+    ad = gpu.parts[0].adapter
+    assert len(ad.handed_off) == 4 and not ad.fallback_reasons

@@ -3,7 +3,7 @@
 .throwErrorEvent -> EventHandle.activateElement, EventTriggerBehavior.activateTriggeredEvent) pinned on the
 reference's ErrorEventTest, ErrorEventIncidentTest and JobThrowErrorTest (engine/src/test/.../processing/
 {bpmn/error,incident,job}), run through the restated processing loop (tests/psm.py, one partition over the
-oracle engine).  One boundary event per activity: the cases with two error boundary events on one task
+oracle engine).  One boundary event per activity (job worker tasks and embedded sub-processes): the cases with two error boundary events on one task
 (shouldCatchErrorEventsByErrorCode, ...WithSpecificErrorCode) are outside the subset."""
 from psm import Client
 from test_gpu_scheduled import KEY_A
@@ -136,3 +136,48 @@ def test_error_variables_are_local_to_the_catch_event():
     var = [r for r in e if r.value_type == abi.VT_VARIABLE]
     assert [(r.value["name"], r.value["value"], r.value["scopeKey"], r.intent) for r in var] == \
         [("foo", "bar", boundary.key, abi.VAR_CREATED)]
+
+
+def sub_process_boundaries():
+    # ErrorEventIncidentTest.BOUNDARY_EVENT_SUBPROCESS (:69-89)
+    b = bpmn.createExecutableProcess("wf").startEvent("start").subProcess("subprocess").startEvent("start_subprocess")
+    b.serviceTask("task_in_subprocess", JOB_TYPE).boundaryEvent("error_in_subprocess").error("error_in_subprocess")
+    b.endEvent("end_boundary_in_subprocess").moveToActivity("task_in_subprocess").endEvent("end_subprocess")
+    b.subProcessDone().boundaryEvent("error").error("error").endEvent("end_boundary").moveToActivity("subprocess")
+    return b.endEvent("end").done()
+
+
+def test_error_boundary_event_on_a_sub_process():
+    # ErrorEventIncidentTest.shouldCreateIncidentIfErrorIsThrownFromSubprocessWithoutCatchEvent... (:379-409):
+    # the walk through the flow scopes lists every error event it passes
+    cl = cluster((sub_process_boundaries(), KEY_A, 1))
+    job, pik = started(cl, None)
+    e = write(cl, Client.throw_error(job.key, "unknown_error_code", "error message"))
+    assert of(e, abi.VT_INCIDENT, abi.INCIDENT_CREATED)[0].value["errorMessage"] == (
+        "Expected to throw an error event with the code 'unknown_error_code' with message 'error message', but it "
+        "was not caught. Available error events are [error_in_subprocess, error]")
+    # caught at the sub-process's boundary event: the sub-process terminates (its task first), then the
+    # boundary event activates in the process scope (as ErrorEventTest.shouldCatchErrorOutsideMultiInstance
+    # Subprocess :570-616, without the body)
+    cl = cluster((sub_process_boundaries(), KEY_A, 1))
+    job, pik = started(cl, None)
+    e = write(cl, Client.throw_error(job.key, "error"))
+    assert of(e, abi.VT_JOB, abi.JOB_ERROR_THROWN)[0].value["elementId"] == "task_in_subprocess"
+    assert subsequence(pi_of(cl, pik), [
+        ("SUB_PROCESS", "ELEMENT_TERMINATING"), ("SERVICE_TASK", "ELEMENT_TERMINATING"),
+        ("SERVICE_TASK", "ELEMENT_TERMINATED"), ("SUB_PROCESS", "ELEMENT_TERMINATED"),
+        ("BOUNDARY_EVENT", "ELEMENT_ACTIVATING"), ("BOUNDARY_EVENT", "ELEMENT_COMPLETED"),
+        ("END_EVENT", "ELEMENT_COMPLETED"), ("PROCESS", "ELEMENT_COMPLETED")])
+    ids = [r.value["elementId"] for r in cl.parts[0].log.entries if r.value_type == abi.VT_PROCESS_INSTANCE
+           and r.intent == abi.PI_ELEMENT_COMPLETED]
+    assert ids[-3:] == ["error", "end_boundary", "wf"]
+    pe = [r for r in e if r.value_type == abi.VT_PROCESS_EVENT]
+    assert [r.intent for r in pe] == [abi.PE_TRIGGERING, abi.PE_TRIGGERED] and pe[0].value["targetElementId"] == "error"
+    # caught inside: the sub-process continues
+    cl = cluster((sub_process_boundaries(), KEY_A, 1))
+    job, pik = started(cl, None)
+    write(cl, Client.throw_error(job.key, "error_in_subprocess"))
+    ids = [r.value["elementId"] for r in cl.parts[0].log.entries if r.value_type == abi.VT_PROCESS_INSTANCE
+           and r.intent == abi.PI_ELEMENT_COMPLETED]
+    assert ids[-5:] == ["error_in_subprocess", "end_boundary_in_subprocess", "subprocess", "end", "wf"]
+    assert not [r for r in cl.parts[0].state() if r.startswith(("JOBS|", "EVENT_SCOPE|"))]

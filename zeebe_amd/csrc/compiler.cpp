@@ -1069,9 +1069,10 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     auto it = index.find(ref);
     if (it == index.end()) { err = "boundary event attached to an unknown element " + ref; return ZBHIP_EPARSE; }
     zbhip_element& A = C.elements[it->second];
-    // job worker tasks; embedded sub-processes with a timer boundary event (the sub-process keeps it
-    // in default_flow: its start_event is its none start event)
-    const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS && C.elements[b].event_type == ZBHIP_EV_TIMER;
+    // job worker tasks; embedded sub-processes with a timer or an error boundary event (the sub-process
+    // keeps it in default_flow: its start_event is its none start event)
+    const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS && (C.elements[b].event_type == ZBHIP_EV_TIMER ||
+                                                                   C.elements[b].event_type == ZBHIP_EV_ERROR);
     if ((!ZBHIP_IS_JOB_WORKER(A.element_type) && !on_sub) || A.flow_scope != C.elements[b].flow_scope) {
       err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return ZBHIP_EUNSUPP;

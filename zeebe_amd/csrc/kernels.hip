@@ -2287,7 +2287,8 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     if (type == ZBHIP_EL_START_EVENT && c != 0) {
       const uint4 cw = elem_of(L, c);
       const uint32_t b = cw.w & 0xFFFF;
-      if (etype(cw) == ZBHIP_EL_SUB_PROCESS && b != 0xFFFF) {
+      // (an error boundary event subscribes to nothing)
+      if (etype(cw) == ZBHIP_EL_SUB_PROCESS && b != 0xFFFF && ((elem_of(L, b).x >> 8) & 0xFF) != ZBHIP_EV_ERROR) {
         if (!L.has_tmr || (L.tm_y >> 31)) { set_fail(L, FB_UNSUPPORTED); return; }
         const uint32_t ck = scope_key(L, c);
         const uint4 bw = elem_of(L, b);

@@ -1419,8 +1419,10 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       if ((E.event_type != ZBHIP_EV_TIMER && E.event_type != ZBHIP_EV_ERROR && !msg) || E.flow_source >= P.els.size())
         return ZBHIP_EUNSUPP;
       const zbhip_element& A = P.els[E.flow_source];
-      // (a timer boundary event on an embedded sub-process: zbhip_element.default_flow of the sub-process)
-      const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS && E.event_type == ZBHIP_EV_TIMER && A.default_flow == e;
+      // (a timer or error boundary event on an embedded sub-process: zbhip_element.default_flow of the
+      // sub-process)
+      const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS &&
+                          (E.event_type == ZBHIP_EV_TIMER || E.event_type == ZBHIP_EV_ERROR) && A.default_flow == e;
       if ((!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e) && !on_sub) return ZBHIP_EINVAL;
       if (A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
     } else if (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) {
