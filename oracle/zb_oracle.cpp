@@ -2945,9 +2945,10 @@ class Oracle {
              "Expected to complete job with key '" + std::to_string(jobKey) + "', but no such job was found");
       return;
     }
-    if (jit->second.failed) {  // DefaultJobCommandPreconditionGuard: ACTIVATABLE or ACTIVATED only
-      reject(cmd, ZBHIP_REJ_INVALID_STATE,
-             "Expected to complete job with key '" + std::to_string(jobKey) + "', but it is in state 'FAILED'");
+    if (jit->second.failed || jit->second.error_thrown) {  // DefaultJobCommandPreconditionGuard: ACTIVATABLE or ACTIVATED only
+      reject(cmd, ZBHIP_REJ_INVALID_STATE, "Expected to complete job with key '" + std::to_string(jobKey) +
+                                               "', but it is in state '" +
+                                               (jit->second.error_thrown ? "ERROR_THROWN" : "FAILED") + "'");
       return;
     }
     JobRow job = jit->second;
@@ -2996,6 +2997,7 @@ class Oracle {
     auto jit = jobs_.find(jobKey);
     const char* why = jit == jobs_.end() ? "no such job was found"
                       : jit->second.failed ? "it is marked as failed and is not activated"
+                      : jit->second.error_thrown ? "it has thrown an error and is not activated"
                       : !jit->second.activated ? "it must be activated first"
                       : !(jit->second.deadline < now_ms) ? "it has not timed out" : nullptr;
     if (why) {
@@ -3031,9 +3033,10 @@ class Oracle {
       reject(cmd, ZBHIP_REJ_NOT_FOUND, "Expected to fail job with key '" + std::to_string(jobKey) + "', but no such job was found");
       return;
     }
-    if (jit->second.failed) {
-      reject(cmd, ZBHIP_REJ_INVALID_STATE,
-             "Expected to fail job with key '" + std::to_string(jobKey) + "', but it is in state 'FAILED'");
+    if (jit->second.failed || jit->second.error_thrown) {
+      reject(cmd, ZBHIP_REJ_INVALID_STATE, "Expected to fail job with key '" + std::to_string(jobKey) +
+                                               "', but it is in state '" +
+                                               (jit->second.error_thrown ? "ERROR_THROWN" : "FAILED") + "'");
       return;
     }
     JobRow& job = jit->second;

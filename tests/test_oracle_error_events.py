@@ -94,6 +94,13 @@ def test_uncaught_error_creates_an_incident():
     assert rej and rej[0].rejection_type == abi.REJ_INVALID_STATE and "it is in state 'ERROR_THROWN'" in rej[0].rejection_reason
     state = cl.parts[0].state()
     assert "JOB_STATES|%d|ERROR_THROWN" % job.key in state
+    # FailJobTest.shouldRejectFailIfErrorThrown (:265-280); completion the same (DefaultJobCommand
+    # PreconditionGuard: ACTIVATABLE or ACTIVATED)
+    for cmd, verb in ((Client.fail_job(job.key, 3), "fail"), (Client.complete_job(job.key), "complete")):
+        rej = [r for r in write(cl, cmd) if r.record_type == abi.RT_REJECTION]
+        assert rej[0].rejection_type == abi.REJ_INVALID_STATE and rej[0].rejection_reason == (
+            "Expected to %s job with key '%d', but it is in state 'ERROR_THROWN'" % (verb, job.key))
+    assert cl.parts[0].state() == state
     cl = cluster((process(boundary=False), KEY_A, 1))
     job, _ = started(cl, None)
     e = write(cl, Client.throw_error(job.key, "other-error"))
