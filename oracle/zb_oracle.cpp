@@ -3921,9 +3921,13 @@ class Oracle {
     const bool found = tit != triggers_.end() && tit->first.first == key;
     auto fit = ei_.find(v.flowScopeKey);
     const bool fs_active = fit != ei_.end() && fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED;
+    // (the trigger read before the TERMINATED applier removes the event scope)
+    const Doc vars = found ? tit->second.vars : Doc();
+    const int64_t eventKey = found ? tit->first.second : -1;
+    const int target = found ? tit->second.elem : -1;
     pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
     if (found && fs_active && !es_interrupted_.count(v.flowScopeKey))
-      activate_triggered_event(tit->first.second, tit->second.elem, key, v.flowScopeKey, v);
+      activate_triggered_event(eventKey, target, key, v.flowScopeKey, v, &vars);
     child_terminated(v);
   }
 
@@ -3941,8 +3945,9 @@ class Oracle {
     if (found && fs_active && !es_interrupted_.count(v.flowScopeKey)) {
       const int64_t eventKey = tit->first.second;
       const int target = tit->second.elem;
+      const Doc vars = tit->second.vars;  // (an error's variables: local to the boundary event)
       pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
-      activate_triggered_event(eventKey, target, key, v.flowScopeKey, v);
+      activate_triggered_event(eventKey, target, key, v.flowScopeKey, v, &vars);
       return;
     }
     if (sub.state == ZBHIP_PI_ELEMENT_TERMINATING) {

@@ -168,8 +168,12 @@ def test_error_boundary_event_on_a_sub_process():
     # Subprocess :570-616, without the body)
     cl = cluster((sub_process_boundaries(), KEY_A, 1))
     job, pik = started(cl, None)
-    e = write(cl, Client.throw_error(job.key, "error"))
+    e = write(cl, Client.throw_error(job.key, "error", variables=[("foo", "bar")]))
     assert of(e, abi.VT_JOB, abi.JOB_ERROR_THROWN)[0].value["elementId"] == "task_in_subprocess"
+    boundary = [r for r in e if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_ACTIVATING
+                and r.value["elementId"] == "error"][0]
+    assert [(r.value["name"], r.value["scopeKey"]) for r in e if r.value_type == abi.VT_VARIABLE] == \
+        [("foo", boundary.key)]
     assert subsequence(pi_of(cl, pik), [
         ("SUB_PROCESS", "ELEMENT_TERMINATING"), ("SERVICE_TASK", "ELEMENT_TERMINATING"),
         ("SERVICE_TASK", "ELEMENT_TERMINATED"), ("SUB_PROCESS", "ELEMENT_TERMINATED"),
