@@ -10,7 +10,10 @@ With ``boundaries`` a task outside parallel branches may carry a timer boundary 
 ends in an end event or (interrupting ones) merges back after the task (one timer per instance at a
 time; a sub-process may carry one too, with none inside it).  With ``multi_instance`` a task outside parallel branches may be a multi-instance activity over
 a static list (MultiInstanceActivityTest's shapes): parallel or sequential, the inputElement `x`, an
-outputCollection (its own name) of `= x` or `= loopCounter`, and a completionCondition."""
+outputCollection (its own name) of `= x` or `= loopCounter`, and a completionCondition.  With ``errors`` a
+task outside parallel branches may carry an error boundary event (code E1 or E2, or a catch-all) and a
+sub-process without a timer boundary event one of its own; its path ends in an end event or (always
+interrupting) merges back after the activity."""
 from xml.sax.saxutils import escape, quoteattr
 
 BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
@@ -19,8 +22,10 @@ ZEEBE_NS = "http://camunda.org/schema/zeebe/1.0"
 
 class _Gen:
     def __init__(self, rng, max_depth, max_blocks, messages, pass_through=False, tasks=True, sub_processes=False,
-                 task_kinds=False, boundaries=False, multi_instance=False):
+                 task_kinds=False, boundaries=False, multi_instance=False, errors=False):
         self.rng = rng
+        self.errors = errors
+        self.error_codes = set()
         self.multi_instance = multi_instance
         self.boundaries = boundaries
         self.task_kinds = task_kinds
@@ -66,6 +71,20 @@ class _Gen:
             return "= amount >= %d and amount < %d" % (a, b)
         return "= amount = %d or amount > %d" % (a, int(r.integers(500, 1000)))
 
+    def error_boundary(self, activity):
+        r = self.rng
+        code = ("E1", "E2", "")[int(r.integers(0, 3))]
+        if code:
+            self.error_codes.add(code)
+        b = self.node("boundaryEvent", attached=activity, error=code, cancel=True)
+        if int(r.integers(0, 2)):
+            self.flow(b, self.node("endEvent"))
+            return activity
+        merge = self.node("exclusiveGateway")
+        self.flow(activity, merge)
+        self.flow(b, merge)
+        return merge
+
     def sequence(self, cur, depth, width):
         for _ in range(int(self.rng.integers(0, self.max_blocks + 1))):
             cur = self.block(cur, depth, width)
@@ -99,6 +118,8 @@ class _Gen:
             self.flow(end, en)
             self.scope = outer
             self.boundaries = inner_b
+            if not timed and self.errors and int(r.integers(0, 3)) == 0:
+                return self.error_boundary(sp)
             if timed:
                 cancel = bool(int(r.integers(0, 3)))
                 b = self.node("boundaryEvent", attached=sp, duration="PT%dS" % int(r.integers(1, 120)), cancel=cancel)
@@ -145,6 +166,8 @@ class _Gen:
                 self.flow(t, merge)
                 self.flow(b, merge)
                 return merge
+            if self.errors and width == 1 and int(r.integers(0, 2)):
+                return self.error_boundary(t)
             return t
         if c == "catch":
             self.catches += 1
@@ -181,11 +204,12 @@ class _Gen:
 
 
 def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False,
-                   tasks=True, sub_processes=False, task_kinds=False, boundaries=False, multi_instance=False):
+                   tasks=True, sub_processes=False, task_kinds=False, boundaries=False, multi_instance=False,
+                   errors=False):
     """tasks=False: no wait states (the CREATE batch runs the instance to its end); task_kinds: job
     worker tasks among service / send / script / business-rule tasks."""
     g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes, task_kinds,
-             boundaries, multi_instance)
+             boundaries, multi_instance, errors)
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")
@@ -223,6 +247,10 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
             elif kind == "intermediateCatchEvent":
                 out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition messageRef="msg_def"/>'
                            '</intermediateCatchEvent>' % (ind, quoteattr(nid)))
+            elif kind == "boundaryEvent" and "error" in extra:
+                ref = ' errorRef="err_%s"' % extra["error"] if extra["error"] else ""
+                out.append('%s<boundaryEvent id=%s attachedToRef=%s><errorEventDefinition%s/></boundaryEvent>'
+                           % (ind, quoteattr(nid), quoteattr(extra["attached"]), ref))
             elif kind == "boundaryEvent":
                 tag = "timeCycle" if extra["duration"].startswith("R") else "timeDuration"
                 out.append('%s<boundaryEvent id=%s attachedToRef=%s%s><timerEventDefinition><%s>%s'
@@ -250,5 +278,7 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
     if messages:
         out.append('  <message id="msg_def" name="msg"><extensionElements>'
                    '<zeebe:subscription correlationKey="= key"/></extensionElements></message>')
+    for code in sorted(g.error_codes):
+        out.append('  <error id="err_%s" errorCode="%s"/>' % (code, code))
     out.append("</definitions>")
     return "\n".join(out) + "\n"

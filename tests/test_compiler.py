@@ -125,3 +125,18 @@ def test_throw_event_with_definition_is_rejected(definition):
         Compiled(xml)
     with pytest.raises(Exception):
         Oracle().deploy(xml)
+
+
+def test_random_processes_with_error_boundary_events_compile_like_the_oracle():
+    # random_bpmn's error boundary events on tasks and sub-processes: both sides accept them, with the
+    # same element indexing
+    from random_bpmn import random_process
+    n_errors = 0
+    for seed in range(40):
+        xml = random_process(np.random.default_rng(9000 + seed), sub_processes=True, task_kinds=True, errors=True)
+        n_errors += xml.count("errorEventDefinition")
+        c = Compiled(xml)
+        o = Oracle()
+        assert o.deploy(xml) == 0
+        assert [c.id(i) for i in range(len(c.els))] == [o.element_id(0, i) for i in range(len(c.els))]
+    assert n_errors >= 20

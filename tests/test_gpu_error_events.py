@@ -81,3 +81,48 @@ def test_error_boundary_events_on_sub_processes_in_the_processing_loop(limit):
     assert [r for r in log if r.value_type == abi.VT_VARIABLE and r.value["name"] == "why"]
     ad = gpu.parts[0].adapter
     assert len(ad.handed_off) == 4 and not ad.fallback_reasons
+
+
+def random_error_campaign(seed, ref, emit, xml, rounds=30, n=24):
+    """tests/random_bpmn.py processes with error boundary events (tasks, sub-processes; codes E1 / E2 or
+    catch-all): every round each open job is completed, left, or gets an error thrown with E1, E2 or E3
+    (caught by its code, by a catch-all, or nowhere: an incident) -- half of the jobs of tasks with an error
+    boundary event, one in twelve of the others."""
+    import re
+    import numpy as np
+    from psm import Client as C
+    guarded = set(re.findall(r'attachedToRef="([^"]+)"><errorEventDefinition', xml))
+    rng = np.random.default_rng(seed)
+    emit(*[C.create("random", variables=(("amount", int(a)),)) for a in rng.integers(0, 1000, n)])
+    thrown = 0
+    for _ in range(rounds):
+        log = ref.parts[0].log
+        dead = {r.key for r in log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_ERROR_THROWN}
+        jobs = sorted((k, r.value["elementId"]) for k, r in open_jobs(log).items() if k not in dead)
+        if not jobs:
+            break
+        cmds = []
+        for k, elem in jobs:
+            m = int(rng.integers(0, 12))
+            if m == 0:
+                continue
+            if m <= (6 if elem in guarded else 1):
+                thrown += 1
+                cmds.append(C.throw_error(k, ("E1", "E1", "E2", "E2", "E3")[int(rng.integers(0, 5))]))
+            else:
+                cmds.append(C.complete_job(k))
+        emit(*cmds)
+    return thrown
+
+
+# (seeds whose processes hold three or more error boundary events; 3, 4, 9, 29: on sub-processes too)
+@pytest.mark.parametrize("seed", [0, 3, 4, 7, 9, 19, 29, 36])
+def test_random_processes_with_error_boundary_events(seed):
+    import numpy as np
+    from random_bpmn import random_process
+    xml = random_process(np.random.default_rng(9000 + seed), sub_processes=True, task_kinds=True, errors=True)
+    deps = [(xml, KEY_A, 1)]
+    ref, gpu = single(deps, deps, limit=100)
+    random_error_campaign(seed, ref, lambda *r: write(ref, gpu, *r), xml)
+    check(ref, gpu)
+    assert not gpu.parts[0].adapter.fallback_reasons

@@ -192,3 +192,21 @@ def test_error_boundary_event_on_a_sub_process():
            and r.intent == abi.PI_ELEMENT_COMPLETED]
     assert ids[-5:] == ["error_in_subprocess", "end_boundary_in_subprocess", "subprocess", "end", "wf"]
     assert not [r for r in cl.parts[0].state() if r.startswith(("JOBS|", "EVENT_SCOPE|"))]
+
+
+def test_random_processes_with_error_boundary_events_on_the_engine():
+    # the GPU campaign's workloads (tests/test_gpu_error_events.py) through the engine alone: the oracle takes
+    # every throw (caught, or an incident) and every completion without refusing
+    import numpy as np
+    from random_bpmn import random_process
+    from test_gpu_error_events import random_error_campaign
+    caught = incidents = 0
+    for seed in (3, 19):
+        xml = random_process(np.random.default_rng(9000 + seed), sub_processes=True, task_kinds=True, errors=True)
+        cl = cluster((xml, KEY_A, 1))
+        random_error_campaign(seed, cl, lambda *r: write(cl, *r), xml)
+        log = cl.parts[0].log.entries
+        caught += sum(1 for r in log if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_COMPLETED
+                      and r.value["bpmnElementType"] == "BOUNDARY_EVENT")
+        incidents += sum(1 for r in log if r.value_type == abi.VT_INCIDENT)
+    assert caught >= 10 and incidents >= 10
