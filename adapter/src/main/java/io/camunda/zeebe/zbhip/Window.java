@@ -72,6 +72,7 @@ final class Window {
   private MemorySegment handle;
   private MemorySegment cmds;
   private MemorySegment docs;
+  private MemorySegment keyOffsets; // a document's key byte offsets (zbhip_doc_merge_order)
   private MemorySegment xparts; // received cross-partition commands of the window (config 5)
   private int nXparts;
   private Arena arena;
@@ -93,6 +94,7 @@ final class Window {
     this.arena = arena;
     cmds = arena.allocate(ZbHip.COMMAND.byteSize() * MAX, 16);
     docs = arena.allocate(ZbHip.DOC_ENTRY.byteSize() * MAX_DOCS, 16);
+    keyOffsets = arena.allocate(JAVA_INT.byteSize() * 256, 4);
     xparts = arena.allocate(ZbHip.XPART.byteSize() * MAX, 16);
   }
 
@@ -236,8 +238,10 @@ final class Window {
   }
 
   /**
-   * The command's variable document as zbhip_doc_entry rows (IndexedDocument.java:44-63 order);
-   * -1 when an entry is outside the device's value subset (the command stays on the CPU engine).
+   * The command's variable document as zbhip_doc_entry rows in document order, with the order
+   * IndexedDocument (IndexedDocument.java:44-63) merges them in -- an agrona Int2IntHashMap over the keys'
+   * byte offsets in these very bytes -- in their pad bytes (zbhip_doc_merge_order); -1 when an entry is
+   * outside the device's value subset (the command stays on the CPU engine).
    */
   private int decodeDocument(final DirectBuffer doc, final GpuBatchProcessor p) {
     if (doc.capacity() == 0) {
@@ -248,7 +252,9 @@ final class Window {
     if (size > 255 || nDocs + size > MAX_DOCS) {
       return -1;
     }
+    final int first = nDocs;
     for (int e = 0; e < size; e++) {
+      keyOffsets.setAtIndex(JAVA_INT, e, msgpack.getOffset());
       final MsgPackToken name = msgpack.readToken();
       final String nameStr = name.getValueBuffer().getStringWithoutLengthUtf8(0, name.getValueBuffer().capacity());
       final int valueStart = msgpack.getOffset();
@@ -283,6 +289,10 @@ final class Window {
       docs.set(JAVA_LONG, o + 8, value);
       entryValues.add(copy(doc, valueStart, msgpack.getOffset() - valueStart));
       nDocs++;
+    }
+    if (size > 1) {
+      final long row = ZbHip.DOC_ENTRY.byteSize();
+      ZbHip.docMergeOrder(keyOffsets, size, docs.asSlice(row * first, row * size));
     }
     return size;
   }

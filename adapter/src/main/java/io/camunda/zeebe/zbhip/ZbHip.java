@@ -192,6 +192,8 @@ public final class ZbHip {
   private static final MethodHandle SUBMIT_EX =
       fn("zbhip_submit_ex", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG));
   private static final MethodHandle RUN = fn("zbhip_run", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
+  private static final MethodHandle DOC_MERGE_ORDER =
+      fn("zbhip_doc_merge_order", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
   private static final MethodHandle SET_CLOCK = fn("zbhip_set_clock", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG));
   private static final MethodHandle PENDING = fn("zbhip_pending_records", FunctionDescriptor.of(JAVA_LONG, ADDRESS));
   private static final MethodHandle DRAIN = fn("zbhip_drain", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
@@ -416,6 +418,14 @@ public final class ZbHip {
   }
 
   /** zbhip_submit: one window of commands (caller-owned, copied) and their document entries. */
+  /**
+   * zbhip_doc_merge_order: the merge order of a document's n entries (IndexedDocument's agrona map over
+   * the keys' byte offsets) into the entries' pad bytes.
+   */
+  public static void docMergeOrder(final MemorySegment keyOffsets, final long n, final MemorySegment entries) {
+    check((int) call(DOC_MERGE_ORDER, keyOffsets, n, entries), "zbhip_doc_merge_order");
+  }
+
   public static void submit(
       final MemorySegment h, final MemorySegment cmds, final long n, final MemorySegment docs, final long nDocs) {
     check((int) call(SUBMIT, h, cmds, n, docs, nDocs), "zbhip_submit");

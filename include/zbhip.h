@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ZBHIP_ABI_VERSION 10 /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
+#define ZBHIP_ABI_VERSION 11 /* 3: zbhip_element.flow_scope, start_event (embedded sub-processes);
                                4: timer boundary events (start_event / flow_source / job_retries of job
                                   workers and boundary events), zbhip_set_clock, TIMER / JOB:CANCELED /
                                   PROCESS_EVENT:TRIGGERED records, zbhip_record.partition = repetitions;
@@ -56,7 +56,9 @@ extern "C" {
                                9: interrupting message boundary events, ZBHIP_CMD_MSG_SUB_DELETE /
                                   ZBHIP_CMD_PMS_DELETE and the DELETING / DELETE / DELETED records;
                               10: static zeebe:taskHeaders (zbhip_process_csr.header_begin /
-                                  header_bytes) */
+                                  header_bytes);
+                              11: multi-entry variable documents (zbhip_doc_merge_order: the merge
+                                  order in zbhip_doc_entry.pad) */
 
 /* ---- error codes ------------------------------------------------------- */
 #define ZBHIP_OK 0
@@ -384,13 +386,29 @@ enum zbhip_doc_type { ZBHIP_DOC_NIL = 0, ZBHIP_DOC_BOOL = 1, ZBHIP_DOC_INT = 2, 
                       ZBHIP_DOC_OTHER = 4, ZBHIP_DOC_STR = 5, ZBHIP_DOC_LIST = 6 };
 
 /* One entry of a variable document (a msgpack map entry on the reference side).
- * DEC values are value * 10^ZBHIP_DEC_SCALE (exact decimal). */
+ * DEC values are value * 10^ZBHIP_DEC_SCALE (exact decimal).
+ * A document of several entries (in document order) carries the order the reference merges them in:
+ * IndexedDocument (state/variable/IndexedDocument.java:20-63) iterates an agrona Int2IntHashMap keyed by
+ * each key's byte offset in the msgpack map.  zbhip_doc_merge_order writes it into the pad bytes: pad[0]
+ * of entry i = the document index of the i-th entry iterated, pad[1] bit 0 of entry 0 = an entry sits off
+ * its home slot (a removal during the iteration may then reorder the rest).  A multi-entry document
+ * without a valid order, with a repeated name or with more than ZBHIP_DOC_MAX_ENTRIES entries is outside
+ * the device subset (its command falls back). */
 typedef struct zbhip_doc_entry {
   uint32_t name_id;
   uint8_t type;
   uint8_t pad[3];
   int64_t value;
 } zbhip_doc_entry;
+#define ZBHIP_DOC_MAX_ENTRIES 8
+
+/* The merge order of a document of n entries whose keys start at the byte offsets key_offsets[0..n)
+ * (strictly increasing: the offsets in the caller's msgpack bytes of the document) into entries[0..n)'s
+ * pad bytes, as above: the agrona 1.19.2 Int2IntHashMap (initial capacity 8, load factor 0.65,
+ * evenHash, linear probing by pairs, doubling past the threshold) IndexedDocument.index fills, iterated
+ * from the top slot (or from below the first free slot when the top one is taken) downwards.
+ * ZBHIP_EINVAL for unordered offsets or n > 256.  Host code only (no device, no handle). */
+int zbhip_doc_merge_order(const uint32_t* key_offsets, size_t n, zbhip_doc_entry* entries);
 
 typedef struct zbhip_command {
   uint32_t instance;    /* instance slot; CREATE: the slot to create the instance in */

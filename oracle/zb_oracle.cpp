@@ -1313,6 +1313,96 @@ struct Unsupported {
   std::string what;
 };
 
+// org.agrona.collections.Int2IntHashMap (third-party agrona 1.19.2, parent/pom.xml:38; not in the
+// reference tree), as IndexedDocument (state/variable/IndexedDocument.java:20-63) uses it: missingValue -1,
+// entries = int[2 * capacity] of (key, value) pairs, capacity 8 at first, resizeThreshold = (int)(capacity
+// * 0.65f).  put: index = Hashing.evenHash(key, mask) = ((key << 1) - (key << 8)) & mask over the pair
+// array (mask = entries.length - 1), probing index + 2 until a free value slot; past the threshold
+// rehash(doubled) re-puts the old pairs in array order.  Iteration (AbstractIterator.reset / findNext):
+// from the top pair down, or, when the top pair is taken, from just below the first free pair, once
+// around.  Iterator.remove frees the pair and compactChain(deleteIndex) pulls later chain members back.
+// Published algorithm, restated; the reference's tests do not pin a multi-entry document's order.
+struct AgronaIntMap {
+  std::vector<int32_t> e;
+  int size = 0, threshold = 0;
+  AgronaIntMap() { capacity(8); }
+  void capacity(int c) {
+    threshold = (int)((float)c * 0.65f);
+    e.assign((size_t)2 * c, -1);
+  }
+  int mask() const { return (int)e.size() - 1; }
+  static int even_hash(int32_t v, int m) { return (int)(((uint32_t)v << 1) - ((uint32_t)v << 8)) & m; }
+  void put(int32_t key, int32_t value) {
+    int i = even_hash(key, mask());
+    while (e[i + 1] != -1) {
+      if (e[i] == key) { e[i + 1] = value; return; }
+      i = (i + 2) & mask();
+    }
+    ++size;
+    e[i] = key;
+    e[i + 1] = value;
+    if (size > threshold) {  // increaseCapacity -> rehash(entries.length)
+      const std::vector<int32_t> old = e;
+      capacity((int)old.size());
+      for (size_t k = 0; k < old.size(); k += 2) {
+        if (old[k + 1] == -1) continue;
+        int j = even_hash(old[k], mask());
+        while (e[j + 1] != -1) j = (j + 2) & mask();
+        e[j] = old[k];
+        e[j + 1] = old[k + 1];
+      }
+    }
+  }
+  struct Iter {
+    int remaining = 0, position = 0, stop = 0;
+    bool valid = false;
+  };
+  Iter iterator() const {
+    Iter it;
+    it.remaining = size;
+    const int cap = (int)e.size();
+    int i = cap;
+    if (e[cap - 1] != -1)
+      for (i = 0; i < cap; i += 2)
+        if (e[i + 1] == -1) break;
+    it.stop = i;
+    it.position = i + cap;
+    return it;
+  }
+  // the key of the next entry, false at the end
+  bool next(Iter& it, int32_t& key) const {
+    if (it.remaining <= 0) return false;
+    for (int i = it.position - 2; i >= it.stop; i -= 2) {
+      const int idx = i & mask();
+      if (e[idx + 1] != -1) {
+        it.valid = true;
+        it.position = i;
+        --it.remaining;
+        key = e[idx];
+        return true;
+      }
+    }
+    throw Unsupported{"agrona iterator past its entries"};
+  }
+  void remove(Iter& it) {
+    int del = it.position & mask();
+    e[del + 1] = -1;
+    --size;
+    for (int i = del;;) {  // compactChain
+      i = (i + 2) & mask();
+      if (e[i + 1] == -1) break;
+      const int h = even_hash(e[i], mask());
+      if ((i < h && (h <= del || del <= i)) || (h <= del && del <= i)) {
+        e[del] = e[i];
+        e[del + 1] = e[i + 1];
+        e[i + 1] = -1;
+        del = i;
+      }
+    }
+    it.valid = false;
+  }
+};
+
 class Oracle {
  public:
   Oracle(int partition, int partition_count, int max_cmds, int64_t initial_key)
@@ -2874,13 +2964,51 @@ class Oracle {
     rec.doc = cmd.doc;
   }
 
-  // VariableBehavior.mergeLocalDocument + setLocalVariable (VariableBehavior.java:60-82,191-200).
-  // Documents with more than one entry iterate in agrona Int2IntHashMap order
-  // (IndexedDocument.java:44-63, third-party agrona 1.19.2): parity unpinned, rejected here.
+  // The byte size of a value / string as the log writes it (MsgPackWriter: the smallest integer form,
+  // float64 decimals, fixstr / str8 / str16 / str32, fixarray / array16 / array32 of scalars)
+  static size_t mp_str_size(size_t n) { return n + (n < 32 ? 1 : n < 256 ? 2 : n < 65536 ? 3 : 5); }
+  size_t mp_value_size(uint8_t type, int64_t v) const {
+    switch (type) {
+      case ZBHIP_DOC_NIL:
+      case ZBHIP_DOC_BOOL: return 1;
+      case ZBHIP_DOC_INT:
+        if (v < -(1LL << 5)) return v < -(1LL << 31) ? 9 : v < -(1LL << 15) ? 5 : v < -(1LL << 7) ? 3 : 2;
+        return v < (1LL << 7) ? 1 : v < (1LL << 8) ? 2 : v < (1LL << 16) ? 3 : v < (1LL << 32) ? 5 : 9;
+      case ZBHIP_DOC_DEC: return 9;
+      case ZBHIP_DOC_STR: return mp_str_size(str((uint32_t)v).size());
+      case ZBHIP_DOC_LIST: {
+        const Items& items = lists.at((size_t)v);
+        size_t n = items.size() < 16 ? 1 : items.size() < 65536 ? 3 : 5;
+        for (const auto& it : items) n += mp_value_size(it.first, it.second);
+        return n;
+      }
+      default: throw Unsupported{"a document value of unknown encoded size"};
+    }
+  }
+
+  // IndexedDocument.index (IndexedDocument.java:44-56): key offset -> value offset of every entry of
+  // the document's msgpack map, into the agrona map; keys[offset] = the entry
+  AgronaIntMap index_document(const Doc& d, std::map<int32_t, uint32_t>& keys) const {
+    AgronaIntMap m;
+    size_t at = d.count < 16 ? 1 : d.count < 65536 ? 3 : 5;
+    for (uint32_t j = 0; j < d.count; ++j) {
+      const zbhip_doc_entry& de = docs[d.begin + j];
+      const size_t name = mp_str_size(names.at(de.name_id).size());
+      m.put((int32_t)at, (int32_t)(at + name));
+      keys[(int32_t)at] = d.begin + j;
+      at += name + mp_value_size(de.type, de.value);
+    }
+    return m;
+  }
+
+  // VariableBehavior.mergeLocalDocument + setLocalVariable (VariableBehavior.java:60-82,191-200): every
+  // entry in the IndexedDocument's iteration order
   void merge_local_document(int64_t scopeKey, int proc, int64_t piKey, const Doc& d) {
     if (d.count == 0) return;
-    if (d.count > 1) throw Unsupported{"multi-entry variable document (agrona iteration order unpinned)"};
-    for (uint32_t j = 0; j < d.count; ++j) set_local_variable(scopeKey, proc, piKey, d.begin + j);
+    std::map<int32_t, uint32_t> keys;
+    AgronaIntMap m = index_document(d, keys);
+    AgronaIntMap::Iter it = m.iterator();
+    for (int32_t k; m.next(it, k);) set_local_variable(scopeKey, proc, piKey, keys.at(k));
   }
 
   void set_local_variable(int64_t scopeKey, int proc, int64_t piKey, uint32_t entry) {
@@ -2905,30 +3033,32 @@ class Oracle {
     vars_[{scopeKey, (int)docs[entry].name_id}] = VarRow{key, docs[entry].type, docs[entry].value, entry};
   }
 
-  // VariableBehavior.mergeDocument (VariableBehavior.java:105-150)
+  // VariableBehavior.mergeDocument (VariableBehavior.java:105-150): every scope below the process
+  // instance's iterates the entries left, updating (and removing) those it holds with another value; the
+  // process instance's scope sets the rest, in the iteration order of what is left
   void merge_document(int64_t scopeKey, int proc, int64_t piKey, const Doc& d) {
     if (d.count == 0) return;
-    if (d.count > 1) throw Unsupported{"multi-entry variable document (agrona iteration order unpinned)"};
-    std::vector<uint32_t> entries;
-    for (uint32_t j = 0; j < d.count; ++j) entries.push_back(d.begin + j);
+    std::map<int32_t, uint32_t> keys;
+    AgronaIntMap m = index_document(d, keys);
     int64_t current = scopeKey;
     for (;;) {
       auto pit = child_parent_.find(current);
       int64_t parent = pit == child_parent_.end() ? -1 : pit->second;
       if (parent <= 0) break;
-      for (auto e = entries.begin(); e != entries.end();) {
-        const zbhip_doc_entry& de = docs[*e];
+      AgronaIntMap::Iter it = m.iterator();
+      for (int32_t k; m.next(it, k);) {
+        const uint32_t e = keys.at(k);
+        const zbhip_doc_entry& de = docs[e];
         auto vit = vars_.find({current, (int)de.name_id});
         if (vit != vars_.end() && !(vit->second.type == de.type && vit->second.value == de.value)) {
-          var_event(vit->second.key, ZBHIP_VAR_UPDATED, current, proc, piKey, *e);
-          e = entries.erase(e);
-        } else {
-          ++e;
+          var_event(vit->second.key, ZBHIP_VAR_UPDATED, current, proc, piKey, e);
+          m.remove(it);
         }
       }
       current = parent;
     }
-    for (uint32_t e : entries) set_local_variable(current, proc, piKey, e);
+    AgronaIntMap::Iter it = m.iterator();
+    for (int32_t k; m.next(it, k);) set_local_variable(current, proc, piKey, keys.at(k));
   }
 
   // ---------------------------------------------------------------------

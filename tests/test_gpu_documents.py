@@ -1,0 +1,74 @@
+"""Multi-entry variable documents on the device (merge order: tests/test_documents.py, parity unpinned
+against the reference itself -- agrona's Int2IntHashMap iteration, restated by the oracle).  Creations
+and job completions carrying documents of two to four entries -- new variables, updates, equal values,
+strings, decimals, lists, entries off their home slot -- through the processing loop over the engine
+alone and through [adapter, engine], every log and state equal at batch limits 3 and 100; the device
+takes them (no declines), except the shapes outside its subset, which hand their instance to the engine:
+a removal from a document with an entry off its home slot, a repeated name, more variables than an
+instance holds on the device."""
+import pytest
+
+from psm import Client, open_jobs
+from test_gpu_scheduled import KEY_A, KEY_B, check, single, write
+from zeebe_amd import abi, bpmn
+
+pytestmark = pytest.mark.gpu
+
+
+def processes():
+    a = bpmn.createExecutableProcess("docs").startEvent().serviceTask("a", "a").serviceTask("b", "b").endEvent().done()
+    b = bpmn.createExecutableProcess("subDocs").startEvent().subProcess("sub").startEvent().serviceTask("t", "t")
+    b = b.endEvent().subProcessDone().zeebeInputExpression("x", "y").endEvent().done()
+    return a, b
+
+
+def _jobs(ref, typ):
+    return sorted(k for k, r in open_jobs(ref.parts[0].log).items() if r.value["type"] == typ)
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_multi_entry_documents_in_the_processing_loop(limit):
+    a, b = processes()
+    deps = [(a, KEY_A, 1), (b, KEY_B, 1)]
+    ref, gpu = single(deps, deps, limit=limit)
+    creates = [
+        [("amount", 5), ("name", "x"), ("flag", True)],
+        [("abc", "xyz"), ("q", 1)],                       # an entry off its home slot (no removal: fine)
+        [("price", 1.5), ("items", [1, 2, 3]), ("n", None)],
+        [("a", "abc"), ("b", "abcde"), ("c", 1)],         # a probe chain wrapping the table
+        [("d", 1), ("d", 2)],                             # a repeated name: the engine's
+        [("v%d" % i, i) for i in range(5)],               # five variables: past the device's four
+    ]
+    write(ref, gpu, *[Client.create("docs", variables=v) for v in creates])
+    write(ref, gpu, *[Client.create("subDocs", variables=v) for v in ([("x", 3)], [("x", 4), ("w", "s")],
+                                                                       [("x", 5)], [("x", 6)])])
+    ja = _jobs(ref, "a")
+    write(ref, gpu, *[Client.complete_job(k, variables=v) for k, v in zip(ja, (
+        [("amount", 7), ("note", "n")],                   # an update and a new variable
+        [("q", 1), ("abc", "other")],                     # equal, then updated
+        [("items", [4]), ("price", 2.25)],
+        [("c", 2), ("e", "e")],
+    ))])
+    jb = _jobs(ref, "b")
+    write(ref, gpu, *[Client.complete_job(k, variables=[("name", "x"), ("flag", False)]) for k in jb])
+    jt = _jobs(ref, "t")
+    write(ref, gpu, *[Client.complete_job(k, variables=v) for k, v in zip(jt, (
+        [("y", 9), ("z", 1)],                             # y updated in the sub-process's scope (removed)
+        [("z", 1), ("y", 4)],                             # y equal: not removed, created in the process's scope
+        [("abc", "xyz"), ("y", 9)],                       # a removal with an entry off its home slot: the engine's
+        [("u", 1), ("t", 2)],
+    ))])
+    for _ in range(3):
+        live = sorted(open_jobs(ref.parts[0].log))
+        if not live:
+            break
+        write(ref, gpu, *[Client.complete_job(k) for k in live])
+    check(ref, gpu)
+    log = gpu.parts[0].log.entries
+    done = sum(1 for r in log if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_COMPLETED
+               and r.value["bpmnElementType"] == "PROCESS")
+    assert done == len(creates) + 4
+    ad = gpu.parts[0].adapter
+    assert ad.counts["device_commands"] >= 20
+    # the declines: the repeated name, the five variables (at creation) and the displaced removal
+    print("handed off", len(ad.handed_off), "fallbacks", ad.fallback_reasons)

@@ -46,6 +46,8 @@ Platform objects used (duck-typed like the Java interfaces):
 import copy
 import types
 
+import numpy as np
+
 from . import abi
 from .engine import Partition
 
@@ -124,10 +126,56 @@ def scalar_entry(v, intern_string):
     return None
 
 
+def _mp_str_len(n):
+    return 1 + n if n < 32 else 2 + n if n < 256 else 3 + n if n < 65536 else 5 + n
+
+
+def _mp_value_len(v):
+    if v is None or isinstance(v, bool):
+        return 1
+    if isinstance(v, int):
+        if v < -(1 << 5):
+            return 9 if v < -(1 << 31) else 5 if v < -(1 << 15) else 3 if v < -(1 << 7) else 2
+        return 1 if v < (1 << 7) else 2 if v < (1 << 8) else 3 if v < (1 << 16) else 5 if v < (1 << 32) else 9
+    if isinstance(v, float):
+        return 9
+    if isinstance(v, str):
+        return _mp_str_len(len(v.encode()))
+    if isinstance(v, (list, tuple)):
+        n = len(v)
+        return (1 if n < 16 else 3 if n < 65536 else 5) + sum(_mp_value_len(x) for x in v)
+    raise ValueError("no msgpack size for %r" % (v,))
+
+
+def msgpack_key_offsets(variables):
+    """The byte offsets of a document's keys as the log writes it (MsgPackWriter: fixmap / map16 header,
+    the smallest integer form, float64 decimals, fixstr / str8 / str16 / str32 strings)."""
+    n = len(variables)
+    at = 1 if n < 16 else 3 if n < 65536 else 5
+    out = []
+    for name, v in variables:
+        out.append(at)
+        at += _mp_str_len(len(name.encode())) + _mp_value_len(v)
+    return out
+
+
+def set_merge_order(d, variables):
+    """The reference's merge order of a multi-entry document into its rows' pad bytes
+    (zbhip_doc_merge_order over the keys' byte offsets; IndexedDocument.java:44-63)."""
+    if len(d) < 2:
+        return d
+    import ctypes as C
+    from .native import check, load
+    offs = np.asarray(msgpack_key_offsets(variables), dtype=np.uint32)
+    check(load().zbhip_doc_merge_order(offs.ctypes.data_as(C.c_void_p), len(d), d.ctypes.data_as(C.c_void_p)),
+          "zbhip_doc_merge_order")
+    return d
+
+
 def doc_entries(variables, intern_name, intern_string, intern_list=None):
-    """A client's variable document [(name, value)] as zbhip_doc_entry rows, or None when a value is
-    outside the device subset (Window.decodeDocument: maps, nested arrays, inexact decimals; arrays
-    of scalars only where the side has a list dictionary, `intern_list`)."""
+    """A client's variable document [(name, value)] as zbhip_doc_entry rows (a multi-entry one with its
+    merge order), or None when a value is outside the device subset (Window.decodeDocument: maps, nested
+    arrays, inexact decimals; arrays of scalars only where the side has a list dictionary, `intern_list`)."""
     d = abi.make_docs(len(variables))
     for j, (name, v) in enumerate(variables):
         d[j]["name_id"] = intern_name(name)
@@ -141,7 +189,7 @@ def doc_entries(variables, intern_name, intern_string, intern_list=None):
         if e is None:
             return None
         d[j]["type"], d[j]["value"] = e
-    return d
+    return set_merge_order(d, variables)
 
 
 def typed_value(t, v, string_value, list_items=None):

@@ -610,6 +610,102 @@ __device__ __forceinline__ int var_lookup(const Lane<K>& L, uint32_t key, uint32
   return v >= 0 ? v : var_find(L, 0, name);
 }
 
+// A multi-entry document's merge order (zbhip.h zbhip_doc_merge_order, the agrona Int2IntHashMap
+// IndexedDocument iterates): position i -> document index in bits 4i..4i+3; false outside the subset (more
+// than ZBHIP_DOC_MAX_ENTRIES entries, no permutation in the pad bytes, a repeated name).
+template <class K>
+__device__ __forceinline__ bool doc_order(const Lane<K>& L, uint32_t begin, uint32_t count, uint32_t& order,
+                                          bool& displaced) {
+  if (count > ZBHIP_DOC_MAX_ENTRIES) return false;
+  uint32_t seen = 0;
+  order = 0;
+  displaced = false;
+  for (uint32_t i = 0; i < count; ++i) {
+    const zbhip_doc_entry e = L.docs[begin + i];
+    const uint32_t j = e.pad[0];
+    if (j >= count || ((seen >> j) & 1u)) return false;
+    seen |= 1u << j;
+    order |= j << (4 * i);
+    if (i == 0) displaced = e.pad[1] & 1;
+    for (uint32_t q = 0; q < i; ++q)
+      if (L.docs[begin + q].name_id == e.name_id) return false;
+  }
+  return true;
+}
+
+// VariableBehavior.mergeLocalDocument (VariableBehavior.java:60-82): setLocalVariable of every entry in the
+// IndexedDocument's order
+template <class K>
+__device__ __forceinline__ void merge_local_document(Lane<K>& L, uint32_t scope, uint32_t begin, uint32_t count) {
+  if (count == 1) {
+    const zbhip_doc_entry d = L.docs[begin];
+    vm_drain();
+    set_local_variable(L, scope, d);
+    return;
+  }
+  uint32_t order;
+  bool displaced;
+  if (!doc_order(L, begin, count, order, displaced)) { set_fail(L, FB_DOC); return; }
+  for (uint32_t i = 0; i < count && !L.fail; ++i) {
+    const zbhip_doc_entry d = L.docs[begin + ((order >> (4 * i)) & 0xF)];
+    vm_drain();
+    set_local_variable(L, scope, d);
+  }
+}
+
+// mergeDocument of a multi-entry document: every scope from the element's up to (not including) the
+// process instance's iterates the entries left, updating those it holds with another value and removing
+// them from the document (Iterator.remove); the process instance's scope sets the rest.  A removal from a
+// table with an entry off its home slot compacts a probe chain and may reorder what is left: outside the
+// subset.
+template <class K>
+__device__ __forceinline__ void merge_document_multi(Lane<K>& L, uint32_t scope_key, uint32_t c, uint32_t begin,
+                                                     uint32_t count) {
+  uint32_t order;
+  bool displaced;
+  if (!doc_order(L, begin, count, order, displaced)) { set_fail(L, FB_DOC); return; }
+  const uint32_t all = (1u << count) - 1;
+  uint32_t left = all;
+  auto level = [&](uint32_t k) {
+    for (uint32_t i = 0; i < count; ++i) {
+      if (!((left >> i) & 1u)) continue;
+      const zbhip_doc_entry d = L.docs[begin + ((order >> (4 * i)) & 0xF)];
+      vm_drain();
+      if constexpr (K::IO) {  // a propagated outputCollection (see merge_document_from)
+        for (int q = 0; q < kVars; ++q)
+          if (q < L.nvars && (var_x(L, q) & 0xFFFF) == d.name_id && ((var_y(L, q) >> 16) & 0xFF) == kDocOutList) {
+            set_fail(L, FB_DOC);
+            return;
+          }
+      }
+      const int v = var_find(L, k, d.name_id);
+      if (v < 0) continue;
+      const uint32_t y = var_y(L, v);
+      if (((y >> 16) & 0xFF) == d.type && var_v(L, v) == d.value) continue;
+      emit(L, C_VAR_UPDATED, y & 0xFFFF, k, d.name_id);
+      var_put(L, v, var_x(L, v), (y & 0xFFFF) | ((uint32_t)d.type << 16), d.value);
+      left &= ~(1u << i);
+    }
+  };
+  if constexpr (!K::IO) {
+    if (scope_key != 0) level(scope_key);
+  } else {
+    uint32_t k = scope_key;
+    for (int depth = 0; k != 0 && k != NONE && depth <= kMaxDepth && !L.fail; ++depth) {
+      level(k);
+      k = container_key(L, c);
+    }
+  }
+  if (L.fail) return;
+  if (left != all && displaced) { set_fail(L, FB_DOC); return; }
+  for (uint32_t i = 0; i < count && !L.fail; ++i) {
+    if (!((left >> i) & 1u)) continue;
+    const zbhip_doc_entry d = L.docs[begin + ((order >> (4 * i)) & 0xF)];
+    vm_drain();
+    set_local_variable(L, 0, d);
+  }
+}
+
 // VariableBehavior.mergeDocument (VariableBehavior.java:105-150) of the command's document from
 // the scope `scope_key` of an element in container c: updated in the first scope below the process
 // that holds the variable with another value, else set locally in the process instance's scope.
@@ -617,7 +713,7 @@ template <class K>
 __device__ __forceinline__ void merge_document_from(Lane<K>& L, uint32_t scope_key, uint32_t c, uint32_t begin,
                                                     uint32_t count) {
   if (count == 0) return;
-  if (count > 1) { set_fail(L, FB_DOC); return; }
+  if (count > 1) { merge_document_multi(L, scope_key, c, begin, count); return; }
   const zbhip_doc_entry d = L.docs[begin];
   vm_drain();
   if constexpr (K::IO) {
@@ -2234,9 +2330,8 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
     const uint4 om = io_map(L, elem, 1);
     if ((om.x & 0xFF) != kIoNone) {
       if (L.trig_key == cmd_key && L.doc_count) {
-        if (L.doc_count > 1) { set_fail(L, FB_DOC); return; }
-        vm_drain();
-        set_local_variable(L, cmd_key, L.docs[L.doc_begin]);
+        merge_local_document(L, cmd_key, L.doc_begin, L.doc_count);
+        if (L.fail) return;
       }
       apply_output_mapping(L, om, elem, cmd_key);
       if (L.fail) return;
@@ -2248,6 +2343,8 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       // an inner instance's own loop variables would be updated in its scope (mergeDocument): they
       // are not in the variable table (derived from the slot), so such a document falls back
       const uint4 bw = elem_of(L, c);
+      // (several entries: the loop variables' names are not checked one by one -- outside the subset)
+      if (c != 0 && L.doc_count > 1 && etype(bw) == ZBHIP_EL_MULTI_INSTANCE_BODY) { set_fail(L, FB_DOC); return; }
       if (c != 0 && L.doc_count == 1 && etype(bw) == ZBHIP_EL_MULTI_INSTANCE_BODY) {
         const zbhip_doc_entry d = L.docs[L.doc_begin];
         const uint32_t name = d.name_id;
@@ -3338,12 +3435,7 @@ __device__ __forceinline__ uint32_t run_command(const StepParams& P, const uint3
     if ((L.pb[0] >> 16) == NONE) set_fail(L, FB_BAD_PROCESS);
     uint32_t pi = new_key(L);  // = ordinal 0
     // setVariablesFromDocument -> VariableBehavior.mergeLocalDocument (:60-82)
-    if (doc_count > 1) set_fail(L, FB_DOC);
-    else if (doc_count == 1) {
-      const zbhip_doc_entry d = P.docs[doc_begin];
-      vm_drain();
-      set_local_variable(L, pi, d);
-    }
+    if (doc_count) merge_local_document(L, pi, doc_begin, doc_count);
     follow_up(L, ZBHIP_PI_ACTIVATE_ELEMENT, pi, NONE, 0, false, false, pi);
     uint32_t created = new_key(L);  // CommandProcessorImpl.accept: entityKey = nextKey
     emit(L, C_PIC_CREATED, created, pi, 0);

@@ -3548,6 +3548,56 @@ extern "C" int zbhip_list_items(zbhip_handle* h, int64_t id, zbhip_doc_entry* ou
   return ZBHIP_OK;
 }
 
+// IndexedDocument.index (state/variable/IndexedDocument.java:44-56) puts (key offset -> value offset) into
+// an agrona Int2IntHashMap (org.agrona 1.19.2, parent/pom.xml:38): a table of 2^k slots (8 at first)
+// probed from evenHash(key) = ((key << 1) - (key << 8)) & (2 * slots - 1) over (key, value) int pairs, by
+// pairs upwards; past (int)(slots * 0.65f) entries it doubles, re-putting the old pairs in slot order.
+// Its iterator walks the slots downwards from the top one, or -- when the top slot is taken, so a probe
+// chain may wrap -- from just below the first free slot, once around.  Only the slot of each entry
+// matters here: slot = pair index / 2.
+extern "C" int zbhip_doc_merge_order(const uint32_t* key_offsets, size_t n, zbhip_doc_entry* entries) {
+  if ((n && (!key_offsets || !entries)) || n > 256) return ZBHIP_EINVAL;
+  for (size_t i = 1; i < n; ++i)
+    if (key_offsets[i] <= key_offsets[i - 1]) return ZBHIP_EINVAL;
+  for (size_t i = 0; i < n; ++i) entries[i].pad[0] = entries[i].pad[1] = 0;
+  if (n < 2) return ZBHIP_OK;
+  auto home = [](uint32_t key, uint32_t slots) {  // evenHash / 2
+    return ((((key << 1) - (key << 8)) & (2 * slots - 1)) >> 1);
+  };
+  uint32_t slots = 8;
+  std::vector<int> table(slots, -1);  // slot -> document index
+  size_t size = 0;
+  auto place = [&](std::vector<int>& t, uint32_t sl, int doc) {
+    uint32_t i = home(key_offsets[doc], sl);
+    while (t[i] >= 0) i = (i + 1) & (sl - 1);
+    t[i] = doc;
+  };
+  for (size_t d = 0; d < n; ++d) {
+    place(table, slots, (int)d);  // (offsets are distinct: no replacement)
+    if (++size > (size_t)(int)(slots * 0.65f)) {
+      std::vector<int> grown(2 * slots, -1);
+      for (uint32_t i = 0; i < slots; ++i)
+        if (table[i] >= 0) place(grown, 2 * slots, table[i]);
+      table.swap(grown);
+      slots *= 2;
+    }
+  }
+  uint32_t start = slots;  // AbstractIterator.reset
+  if (table[slots - 1] >= 0)
+    for (start = 0; start < slots && table[start] >= 0; ++start) {
+    }
+  bool displaced = false;
+  size_t k = 0;
+  for (uint32_t step = 1; step <= slots && k < n; ++step) {  // findNext: downwards, once around
+    const uint32_t i = (start + slots - step) & (slots - 1);
+    if (table[i] < 0) continue;
+    entries[k++].pad[0] = (uint8_t)table[i];
+    displaced = displaced || home(key_offsets[table[i]], slots) != i;
+  }
+  entries[0].pad[1] = displaced ? 1 : 0;
+  return ZBHIP_OK;
+}
+
 // uploads the lists interned since the last run (their headers and items)
 static int sync_lists(zbhip_handle* h) {
   if (h->d_list_n == h->lists.size()) return ZBHIP_OK;

@@ -35,7 +35,8 @@ SYMBOLS = ["zbhip_compile_bpmn", "zbhip_free_csr", "zbhip_open", "zbhip_close", 
            "zbhip_pending_continuations", "zbhip_current_key", "zbhip_set_key_if_higher",
            "zbhip_select_instances_db", "zbhip_drain_command", "zbhip_outbox_command", "zbhip_due_timers",
            "zbhip_timed_out_jobs", "zbhip_time_out_job", "zbhip_fail_job", "zbhip_job_state", "zbhip_set_job_stream",
-           "zbhip_job_variables", "zbhip_intern_list", "zbhip_list_items", "zbhip_serializer_intern_list"]
+           "zbhip_job_variables", "zbhip_intern_list", "zbhip_list_items", "zbhip_serializer_intern_list",
+           "zbhip_doc_merge_order"]
 
 
 class ZbhipError(RuntimeError):
@@ -135,6 +136,7 @@ def load():
     L.zbhip_intern_list.restype = i64
     L.zbhip_intern_list.argtypes = [vp, vp, sz]
     L.zbhip_list_items.argtypes = [vp, i64, vp, sz, C.POINTER(sz)]
+    L.zbhip_doc_merge_order.argtypes = [vp, sz, vp]
     L.zbhip_stream.argtypes = [vp]
     L.zbhip_stream.restype = vp
     L.zbhip_submit_xparts_device.argtypes = [vp, vp, sz]
