@@ -72,3 +72,43 @@ def test_multi_entry_documents_in_the_processing_loop(limit):
     assert ad.counts["device_commands"] >= 20
     # the declines: the repeated name, the five variables (at creation) and the displaced removal
     print("handed off", len(ad.handed_off), "fallbacks", ad.fallback_reasons)
+
+
+def random_document_campaign(seed, ref, emit, n=24, rounds=30):
+    """Each round completes every open job with a random document of zero to three entries over the names
+    amount / p / q / r (ints, strings, booleans, decimals; amount stays an integer for the conditions)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+
+    def value(name):
+        k = int(rng.integers(0, 4))
+        if name == "amount" or k == 0:
+            return int(rng.integers(0, 1000))
+        return ("s%d" % int(rng.integers(0, 5)), bool(int(rng.integers(0, 2))), int(rng.integers(0, 8)) / 4)[k - 1]
+
+    emit(*[Client.create("random", variables=[("amount", int(a)), ("p", value("p"))]) for a in rng.integers(0, 1000, n)])
+    for _ in range(rounds):
+        jobs = sorted(open_jobs(ref.parts[0].log))
+        if not jobs:
+            break
+        cmds = []
+        for k in jobs:
+            names = [x for x in ("amount", "p", "q", "r") if int(rng.integers(0, 3)) == 0]
+            rng.shuffle(names)
+            cmds.append(Client.complete_job(k, variables=[(x, value(x)) for x in names]))
+        emit(*cmds)
+
+
+# (seeds whose processes wait in job worker tasks: 1, 3, 4, 9, 15, 18 update the most variables)
+@pytest.mark.parametrize("seed", [1, 3, 4, 9, 15, 18])
+def test_random_processes_with_multi_entry_documents(seed):
+    import numpy as np
+    from random_bpmn import random_process
+    xml = random_process(np.random.default_rng(9500 + seed), sub_processes=True, task_kinds=True)
+    deps = [(xml, KEY_A, 1)]
+    ref, gpu = single(deps, deps, limit=100)
+    random_document_campaign(seed, ref, lambda *r: write(ref, gpu, *r))
+    check(ref, gpu)
+    ad = gpu.parts[0].adapter
+    assert ad.counts["device_commands"] >= 24
+    print("handed off", len(ad.handed_off), "fallbacks", ad.fallback_reasons)
