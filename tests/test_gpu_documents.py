@@ -112,3 +112,65 @@ def test_random_processes_with_multi_entry_documents(seed):
     ad = gpu.parts[0].adapter
     assert ad.counts["device_commands"] >= 24
     print("handed off", len(ad.handed_off), "fallbacks", ad.fallback_reasons)
+
+
+def _doc_window(rng, names, n, width):
+    """n documents of `width` scalar entries (ints, booleans, decimals, nil) over `names`, their merge order
+    set: the docs array and each command's (doc_begin, doc_count)."""
+    import numpy as np
+    from zeebe_amd.adapter import set_merge_order
+    rows, spans = [], []
+    for _ in range(n):
+        pick = list(rng.choice(len(names), size=width, replace=False))
+        variables = []
+        for j in pick:
+            k = int(rng.integers(0, 4))
+            variables.append((names[j][0], (int(rng.integers(-100000, 100000)), bool(k & 1), int(rng.integers(0, 99)) / 4,
+                                             None)[k]))
+        d = abi.make_docs(width)
+        for e, (nm, v) in enumerate(variables):
+            d[e]["name_id"] = dict(names)[nm]
+            if v is None:
+                d[e]["type"] = abi.DOC_NIL
+            elif isinstance(v, bool):
+                d[e]["type"], d[e]["value"] = abi.DOC_BOOL, int(v)
+            elif isinstance(v, float):
+                d[e]["type"], d[e]["value"] = abi.DOC_DEC, round(v * 10 ** abi.DEC_SCALE)
+            else:
+                d[e]["type"], d[e]["value"] = abi.DOC_INT, v
+        spans.append((sum(len(r) for r in rows), width))
+        rows.append(set_merge_order(d, variables))
+    return np.concatenate(rows), spans
+
+
+@pytest.mark.parametrize("width", [2, 3, 4])
+def test_multi_entry_documents_log_bytes(width):
+    # creations and two rounds of job completions with multi-entry documents: the device's records and state
+    # equal the oracle's, its log bytes equal the host serialiser's, which equal the Python restatement's
+    # (tests/test_gpu_logserial.Pair), and the device log writer takes the windows (no host fallback)
+    import numpy as np
+    from helpers import create_commands
+    from test_gpu_logdev import Log, job_completions
+    from test_gpu_logserial import Pair
+    xml = bpmn.createExecutableProcess("docs").startEvent().serviceTask("a", "a").serviceTask("b", "b").endEvent().done()
+    words = ("amount", "p", "q", "r_long_variable_name")
+    n = 64
+    pair, log = Pair(xml, n, names=words), Log(xml, n, names=words)
+    names = [(w, pair.part.intern(w)) for w in words]
+    assert names == [(w, log.part.intern(w)) for w in words]
+    rng = np.random.default_rng(width)
+    cmds = create_commands(n)
+    docs, spans = _doc_window(rng, names, n, width)
+    cmds["doc_begin"], cmds["doc_count"] = [s[0] for s in spans], [s[1] for s in spans]
+    pair.window(cmds, docs)
+    recs = log.window(cmds, docs)
+    assert log.part.state() == pair.orc.state()
+    for _ in range(2):
+        c = job_completions(recs, log.part)
+        docs, spans = _doc_window(rng, names, len(c), width)
+        c["doc_begin"], c["doc_count"] = [s[0] for s in spans], [s[1] for s in spans]
+        pair.window(c, docs)
+        recs = log.window(c, docs)
+        assert log.part.state() == pair.orc.state()
+    assert log.declined == 0 and log.part.stats()["fallback"] == 0
+    assert [r for r in log.part.state() if not r.startswith("KEY|")] == []

@@ -404,20 +404,32 @@ __device__ __forceinline__ bool doc_ok(const zbhip_doc_entry& d) {
   return d.type == ZBHIP_DOC_NIL || d.type == ZBHIP_DOC_BOOL || d.type == ZBHIP_DOC_INT || d.type == ZBHIP_DOC_DEC;
 }
 
-// mp_bin of the command's document (DocumentValue: empty -> EMPTY_DOCUMENT; one entry -> a map);
-// false for a document the device does not write (several entries, a string value)
+// mp_bin of the command's document (DocumentValue: empty -> EMPTY_DOCUMENT; else its map, entries in
+// document order); false for a document the device does not write (a string or list value, more than
+// ZBHIP_DOC_MAX_ENTRIES entries)
 template <class S>
 __device__ __forceinline__ bool src_doc_bin(S& s, const LogParams& L, const LogCmd& m) {
   if (m.doc_count == 0) { s.bytes(L, run(L, G_EMPTY_BIN)); return true; }
-  const zbhip_doc_entry d = L.docs[m.doc_begin];
-  if (m.doc_count != 1 || !doc_ok(d)) return false;
-  const uint2 nr = name_run(L, d.name_id);
-  const uint32_t len = 1 + nr.y + doc_value_len(d);
-  s.b(0xc4);  // < 256 bytes: a name and a scalar
-  s.b(len);
-  s.b(0x81);
-  s.bytes(L, nr);
-  doc_value(s, d);
+  if (m.doc_count > ZBHIP_DOC_MAX_ENTRIES) return false;
+  uint32_t len = 1;  // fixmap header
+  for (uint32_t i = 0; i < m.doc_count; ++i) {
+    const zbhip_doc_entry d = L.docs[m.doc_begin + i];
+    if (!doc_ok(d)) return false;
+    len += name_run(L, d.name_id).y + doc_value_len(d);
+  }
+  if (len < 256) {  // MsgPackWriter.writeBinaryHeader: bin8 / bin16
+    s.b(0xc4);
+    s.b(len);
+  } else {
+    s.b(0xc5);
+    be(s, len, 2);
+  }
+  s.b(0x80 | m.doc_count);
+  for (uint32_t i = 0; i < m.doc_count; ++i) {
+    const zbhip_doc_entry d = L.docs[m.doc_begin + i];
+    s.bytes(L, name_run(L, d.name_id));
+    doc_value(s, d);
+  }
   return true;
 }
 
@@ -500,9 +512,11 @@ __device__ __forceinline__ bool value(S& s, const LogParams& L, const LogCmd& m,
       s.bytes(L, run(L, G_TENANT));
       return true;
     case ZBHIP_VT_VARIABLE: {
-      // the batch's source document entry of that name (VariableRecord.java:35-41)
-      if (!pb || m.doc_count != 1) return false;
-      const zbhip_doc_entry d = L.docs[m.doc_begin];
+      // the batch's source document entry of that name (VariableRecord.java:35-41; names are distinct)
+      if (!pb || m.doc_count == 0 || m.doc_count > ZBHIP_DOC_MAX_ENTRIES) return false;
+      uint32_t at = 0;
+      while (at + 1 < m.doc_count && L.docs[m.doc_begin + at].name_id != r.elem) ++at;
+      const zbhip_doc_entry d = L.docs[m.doc_begin + at];
       if (d.name_id != r.elem || !doc_ok(d)) return false;
       const uint2 nr = name_run(L, r.elem);
       s.bytes(L, run(L, G_VAR_A));
