@@ -338,7 +338,8 @@ struct OEl {
   int scope = 0;                   // flow scope element (ExecutableFlowElement.getFlowScope): 0 = process
   int start = -1;                  // process / sub-process: getNoneStartEvent
   int attached = -1;               // boundary event: the activity it is attached to (attachedToRef)
-  int boundary = -1;               // activity: its (one) boundary event (ExecutableActivity.attach)
+  int boundary = -1;               // activity: its timer / message boundary event, else its first error one
+  std::vector<int> boundaries;     // every boundary event, in attach order (ExecutableActivity.attach)
   bool interrupting = true;        // boundary event: cancelActivity (ExecutableBoundaryEvent.interrupting)
   int reps = 1;                    // timer: repetitions (RepeatingInterval; 1 a duration, -1 infinite)
   // multi-instance body (ExecutableMultiInstanceBody / ExecutableLoopCharacteristics): its inner
@@ -973,8 +974,17 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
       err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return false;
     }
-    if (a.boundary >= 0) { err = "more than one boundary event on an activity outside the supported subset"; return false; }
-    a.boundary = b;
+    // several error boundary events beside at most one timer / message boundary event
+    if (a.boundary >= 0) {
+      if (P.els[a.boundary].event != ZBHIP_EV_ERROR && P.els[b].event != ZBHIP_EV_ERROR) {
+        err = "more than one timer / message boundary event on an activity outside the supported subset";
+        return false;
+      }
+      if (P.els[b].event != ZBHIP_EV_ERROR) a.boundary = b;
+    } else {
+      a.boundary = b;
+    }
+    a.boundaries.push_back(b);
     P.els[b].attached = it->second;
   }
   // gateway default flows (ExclusiveGatewayTransformer.transformDefaultFlow)
@@ -2500,11 +2510,12 @@ class Oracle {
     auto sit = ei_.find(scope);
     if (sit != ei_.end()) {
       const OEl& owner = procs[sit->second.value.proc].els[sit->second.value.elem];
+      const bool attached = std::find(owner.boundaries.begin(), owner.boundaries.end(), elem) != owner.boundaries.end();
       const bool interrupting = owner.id == procs[proc].els[elem].id ? owner.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
                                                                            owner.type == ZBHIP_EL_BOUNDARY_EVENT
-                                                                     : owner.boundary == elem && procs[proc].els[elem].interrupting;
+                                                                     : attached && procs[proc].els[elem].interrupting;
       if (interrupting) es_interrupted_.insert(scope);
-      if (interrupting && owner.boundary == elem) es_closed_.insert(scope);
+      if (interrupting && attached) es_closed_.insert(scope);
     }
     triggers_[{scope, eventKey}] = EventTrigger{elem, proc, vars, piKey};
   }
@@ -3255,15 +3266,30 @@ class Oracle {
           es_interrupted_.count(inst.key))
         break;
       const OEl& el = E(inst.value);
-      if (el.boundary >= 0 && P(inst.value.proc).els[el.boundary].event == ZBHIP_EV_ERROR) {
-        const std::string& bc = P(inst.value.proc).els[el.boundary].error_code;
+      // findErrorCatchEventInScope: the element's error catch events ordered by errorCode, descending
+      // (ERROR_CODE_COMPARATOR: DirectBuffer.compareTo -- signed bytes, then length -- reversed; a
+      // stable sort), each visited code joining the available ones until the first match
+      std::vector<int> errs;
+      for (int b : el.boundaries)
+        if (P(inst.value.proc).els[b].event == ZBHIP_EV_ERROR) errs.push_back(b);
+      auto signed_less = [](const std::string& x, const std::string& y) {
+        for (size_t i = 0; i < x.size() && i < y.size(); ++i)
+          if ((int8_t)x[i] != (int8_t)y[i]) return (int8_t)x[i] < (int8_t)y[i];
+        return x.size() < y.size();
+      };
+      std::stable_sort(errs.begin(), errs.end(), [&](int x, int y) {
+        return signed_less(P(inst.value.proc).els[y].error_code, P(inst.value.proc).els[x].error_code);
+      });
+      for (int b : errs) {
+        const std::string& bc = P(inst.value.proc).els[b].error_code;
         avail.push_back(bc);
         if (bc.empty() || bc == code) {
-          catch_elem = el.boundary;
+          catch_elem = b;
           scope = inst.key;
           break;
         }
       }
+      if (catch_elem >= 0) break;
       it = ei_.find(inst.parentKey);
     }
     auto put = [&](const char* elem_marker) {  // JOB:ERROR_THROWN with the stored job + the command's fields
@@ -4542,8 +4568,10 @@ std::string Oracle::dump_state() const {
     std::string intr, bnd;
     if (el && (el->type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || el->type == ZBHIP_EL_BOUNDARY_EVENT)) intr = el->id;
     if (el && el->boundary >= 0) {  // interruptingIds only for cancelActivity boundary events
-      bnd = op->els[el->boundary].id;
-      if (op->els[el->boundary].interrupting) intr = bnd;
+      for (int b : el->boundaries) {
+        bnd += (bnd.empty() ? "" : ";") + op->els[b].id;
+        if (op->els[b].interrupting) intr += (intr.empty() ? "" : ";") + op->els[b].id;
+      }
     }
     snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=%d,interrupted=%d,interrupting=%s,boundaryElementIds=%s",
              (long long)k, es_closed_.count(k) ? 0 : 1, es_interrupted_.count(k) ? 1 : 0, intr.c_str(), bnd.c_str());

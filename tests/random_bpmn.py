@@ -12,8 +12,8 @@ time; a sub-process may carry one too, with none inside it).  With ``multi_insta
 a static list (MultiInstanceActivityTest's shapes): parallel or sequential, the inputElement `x`, an
 outputCollection (its own name) of `= x` or `= loopCounter`, and a completionCondition.  With ``errors`` a
 task outside parallel branches may carry an error boundary event (code E1 or E2, or a catch-all) and a
-sub-process without a timer boundary event one of its own; its path ends in an end event or (always
-interrupting) merges back after the activity."""
+sub-process without a timer boundary event one of its own (sometimes a second one with the other code);
+its path ends in an end event or (always interrupting) merges back after the activity."""
 from xml.sax.saxutils import escape, quoteattr
 
 BPMN_NS = "http://www.omg.org/spec/BPMN/20100524/MODEL"
@@ -77,6 +77,10 @@ class _Gen:
         if code:
             self.error_codes.add(code)
         b = self.node("boundaryEvent", attached=activity, error=code, cancel=True)
+        if int(r.integers(0, 3)) == 0:  # a second error boundary event with another code, to its own end
+            other = "E2" if code == "E1" else "E1"
+            self.error_codes.add(other)
+            self.flow(self.node("boundaryEvent", attached=activity, error=other, cancel=True), self.node("endEvent"))
         if int(r.integers(0, 2)):
             self.flow(b, self.node("endEvent"))
             return activity

@@ -126,3 +126,26 @@ def test_random_processes_with_error_boundary_events(seed):
     random_error_campaign(seed, ref, lambda *r: write(ref, gpu, *r), xml)
     check(ref, gpu)
     assert not gpu.parts[0].adapter.fallback_reasons
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_several_boundary_events_on_one_task_in_the_processing_loop(limit):
+    # two error boundary events (a catch-all and a code-specific one) and a timer boundary event on one task:
+    # the timer stays the device's (TIMER:CREATED with the task), the event scope lists all three; thrown
+    # errors go to the code-specific or the catch-all boundary event, canceling the timer; some timers fire
+    from test_oracle_error_events import two_boundaries
+    deps = [(two_boundaries(("catch-all", None), ("code-specific", "E"), timer="PT10S"), KEY_A, 1)]
+    ref, gpu = single(deps, deps, limit=limit)
+    write(ref, gpu, *[Client.create("wf") for _ in range(8)])
+    jobs = sorted(open_jobs(ref.parts[0].log))
+    write(ref, gpu, Client.throw_error(jobs[0], "E"), Client.throw_error(jobs[1], "other"),
+          Client.complete_job(jobs[2]))
+    from test_gpu_scheduled import step
+    step(ref, gpu, 11000)
+    check(ref, gpu)
+    log = gpu.parts[0].log.entries
+    caught = [r.value["elementId"] for r in log if r.value_type == abi.VT_PROCESS_INSTANCE
+              and r.intent == abi.PI_ELEMENT_COMPLETED and r.value["bpmnElementType"] == "BOUNDARY_EVENT"]
+    assert sorted(caught) == ["catch-all", "code-specific"] + ["timer"] * 5
+    ad = gpu.parts[0].adapter
+    assert len(ad.handed_off) == 2 and not ad.fallback_reasons

@@ -210,3 +210,67 @@ def test_random_processes_with_error_boundary_events_on_the_engine():
                       and r.value["bpmnElementType"] == "BOUNDARY_EVENT")
         incidents += sum(1 for r in log if r.value_type == abi.VT_INCIDENT)
     assert caught >= 10 and incidents >= 10
+
+
+def two_boundaries(first=("error-1", "error-1"), second=("error-2", "error-2"), timer=None):
+    # ErrorEventTest.process(serviceTask -> two boundaryEvent(..).error(..).endEvent()); with `timer` a
+    # timer boundary event (the activity's one timer) besides them
+    b = bpmn.createExecutableProcess("wf").startEvent("start").serviceTask("task", JOB_TYPE)
+    for bid, code in (first, second):
+        b.boundaryEvent(bid).error(code).endEvent("end-" + bid).moveToActivity("task")
+    if timer:
+        b.boundaryEvent("timer").timerWithDuration(timer).endEvent("end-timer").moveToActivity("task")
+    return b.endEvent("end").done()
+
+
+def boundary_path(cl, pik):
+    return [r.value["elementId"] for r in cl.parts[0].log.entries if r.value_type == abi.VT_PROCESS_INSTANCE
+            and r.value["processInstanceKey"] == pik and r.value["bpmnElementType"] == "BOUNDARY_EVENT"]
+
+
+def test_two_error_boundary_events_by_error_code():
+    # ErrorEventTest.shouldCatchErrorEventsByErrorCode (:99-146): each code its own boundary event
+    cl = cluster((two_boundaries(), KEY_A, 1))
+    j1, p1 = started(cl, None)
+    j2, p2 = started(cl, None)
+    write(cl, Client.throw_error(j1.key, "error-1"), Client.throw_error(j2.key, "error-2"))
+    assert set(boundary_path(cl, p1)) == {"error-1"} and set(boundary_path(cl, p2)) == {"error-2"}
+    assert pi_of(cl, p1)[-1] == pi_of(cl, p2)[-1] == ("PROCESS", "ELEMENT_COMPLETED")
+
+
+def test_code_specific_error_boundary_event_wins():
+    # ErrorEventTest.shouldCatchErrorEventsOnBoundaryEventWithSpecificErrorCode (:256-287): the catch-all is
+    # attached first, the code-specific one catches (ERROR_CODE_COMPARATOR orders codes descending)
+    cl = cluster((two_boundaries(("catch-all", None), ("code-specific", ERROR_CODE)), KEY_A, 1))
+    job, pik = started(cl, None)
+    write(cl, Client.throw_error(job.key, ERROR_CODE))
+    assert set(boundary_path(cl, pik)) == {"code-specific"}
+    # another code: the catch-all
+    job, pik = started(cl, None)
+    write(cl, Client.throw_error(job.key, "other"))
+    assert set(boundary_path(cl, pik)) == {"catch-all"}
+
+
+def test_available_error_codes_in_comparator_order():
+    # findErrorCatchEventInScope visits the codes in ERROR_CODE_COMPARATOR order (reversed byte order) and
+    # lists each visited one; the event scope holds every boundary event in attach order
+    cl = cluster((two_boundaries(("b1", "A-1"), ("b2", "B-2")), KEY_A, 1))
+    job, pik = started(cl, None)
+    state = [r for r in cl.parts[0].state() if r.startswith("EVENT_SCOPE|")]
+    assert any("interrupting=b1;b2,boundaryElementIds=b1;b2" in r for r in state)
+    e = write(cl, Client.throw_error(job.key, "C-3"))
+    assert of(e, abi.VT_INCIDENT, abi.INCIDENT_CREATED)[0].value["errorMessage"] == (
+        "Expected to throw an error event with the code 'C-3', but it was not caught. "
+        "Available error events are [B-2, A-1]")
+
+
+def test_error_boundary_events_beside_a_timer_boundary_event():
+    # a timer and two error boundary events on one task: the timer fires, or an error is caught (the timer
+    # canceled with the task's termination)
+    cl = cluster((two_boundaries(timer="PT10S"), KEY_A, 1))
+    job, pik = started(cl, None)
+    assert [r for r in cl.parts[0].state() if r.startswith("TIMERS|")]
+    e = write(cl, Client.throw_error(job.key, "error-2"))
+    assert of(e, abi.VT_TIMER, abi.TIMER_CANCELED)
+    assert set(boundary_path(cl, pik)) == {"error-2"}
+    assert not [r for r in cl.parts[0].state() if r.startswith(("TIMERS|", "JOBS|", "EVENT_SCOPE|"))]

@@ -1077,9 +1077,19 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return ZBHIP_EUNSUPP;
     }
+    // the slot holds the activity's timer / message boundary event, else its first error one; further
+    // error boundary events need no device state (the runtime finds them by flow_source)
     uint16_t& slot = on_sub ? A.default_flow : A.start_event;
-    if (slot != ZBHIP_NONE16) { err = "more than one boundary event on an activity outside the supported subset"; return ZBHIP_EUNSUPP; }
-    slot = b;
+    const bool err_b = C.elements[b].event_type == ZBHIP_EV_ERROR;
+    if (slot != ZBHIP_NONE16) {
+      if (!err_b && C.elements[slot].event_type != ZBHIP_EV_ERROR) {
+        err = "more than one timer / message boundary event on an activity outside the supported subset";
+        return ZBHIP_EUNSUPP;
+      }
+      if (!err_b) slot = b;
+    } else {
+      slot = b;
+    }
     C.elements[b].flow_source = it->second;
   }
   for (size_t e = 1; e < C.elements.size(); ++e)

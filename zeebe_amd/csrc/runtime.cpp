@@ -1423,7 +1423,11 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
       // sub-process)
       const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS &&
                           (E.event_type == ZBHIP_EV_TIMER || E.event_type == ZBHIP_EV_ERROR) && A.default_flow == e;
-      if ((!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e) && !on_sub) return ZBHIP_EINVAL;
+      // (further error boundary events of an activity: outside its slot, found by flow_source)
+      const uint16_t slot = A.element_type == ZBHIP_EL_SUB_PROCESS ? A.default_flow : A.start_event;
+      const bool extra_error = E.event_type == ZBHIP_EV_ERROR && slot != ZBHIP_NONE16 && slot < P.els.size() &&
+                               (ZBHIP_IS_JOB_WORKER(A.element_type) || A.element_type == ZBHIP_EL_SUB_PROCESS);
+      if ((!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e) && !on_sub && !extra_error) return ZBHIP_EINVAL;
       if (A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
     } else if (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) {
       if (E.start_event >= P.els.size() || P.els[E.start_event].element_type != ZBHIP_EL_BOUNDARY_EVENT) return ZBHIP_EINVAL;
@@ -4020,12 +4024,17 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       // only with events) those of its interrupting boundary event, which is also its
       // boundaryElementIds (ExecutableActivity.java:28-38)
       const bool own = E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT;
-      const uint16_t be = sub_bnd ? E.default_flow : E.start_event;
       const bool bnd = (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) || sub_bnd;
-      const std::string ids = own ? P.id(elem) : bnd ? P.id(be) : std::string();
-      const bool intr = own || (bnd && (P.els[be].job_retries & 1));  // cancelActivity boundary events only
+      // an activity's boundary events in attach order (element order), the cancelActivity ones interrupting
+      std::string ids = own ? P.id(elem) : std::string(), intr_ids = own ? ids : std::string();
+      if (bnd)
+        for (size_t b = 0; b < P.els.size(); ++b)
+          if (P.els[b].element_type == ZBHIP_EL_BOUNDARY_EVENT && P.els[b].flow_source == elem) {
+            ids += (ids.empty() ? "" : ";") + P.id((uint32_t)b);
+            if (P.els[b].job_retries & 1) intr_ids += (intr_ids.empty() ? "" : ";") + P.id((uint32_t)b);
+          }
       snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=%s", k,
-               intr ? ids.c_str() : "", bnd ? ids.c_str() : "");
+               intr_ids.c_str(), bnd ? ids.c_str() : "");
       sink(ctx, buf);
     }
     if (job_row) {
