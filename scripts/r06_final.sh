@@ -9,7 +9,7 @@ O=gpurun_out/r06/final
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_default -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > /dev/null 2>> $O/errs.txt
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_default -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io > /dev/null 2>> $O/errs.txt
 for cfg in linear10 forkjoin8_tasks; do
   i=0
   for group in FETCH_SIZE WRITE_SIZE; do
