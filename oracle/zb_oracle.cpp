@@ -340,6 +340,7 @@ struct OEl {
   int attached = -1;               // boundary event: the activity it is attached to (attachedToRef)
   int boundary = -1;               // activity: its timer / message boundary event, else its first error one
   std::vector<int> boundaries;     // every boundary event, in attach order (ExecutableActivity.attach)
+  std::vector<int> esps;           // a container's event sub-processes, in attach order (SubProcessTransformer)
   bool interrupting = true;        // boundary event: cancelActivity (ExecutableBoundaryEvent.interrupting)
   int reps = 1;                    // timer: repetitions (RepeatingInterval; 1 a duration, -1 infinite)
   // multi-instance body (ExecutableMultiInstanceBody / ExecutableLoopCharacteristics): its inner
@@ -705,7 +706,28 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
     OEl e;
     e.id = k->attr("id");
     e.scope = scope;
-    if (n == "startEvent") {
+    if (n == "startEvent" && k->child("errorEventDefinition") && P.els[scope].type == ZBHIP_EL_EVENT_SUB_PROCESS) {
+      // the error start event of an event sub-process (CatchEventTransformer.java:166: ERROR; its errorCode
+      // as an error boundary event's; interrupting -- isInterrupting, default true -- as an error start
+      // event must be)
+      e.type = ZBHIP_EL_START_EVENT;
+      e.event = ZBHIP_EV_ERROR;
+      e.interrupting = k->attr("isInterrupting") != "false";
+      if (!e.interrupting || k->child("messageEventDefinition") || k->child("timerEventDefinition") ||
+          k->child("signalEventDefinition")) {
+        err = "error start event outside the supported subset";
+        return false;
+      }
+      const std::string ref = k->child("errorEventDefinition")->attr("errorRef");
+      if (!ref.empty()) {
+        auto it = errors.find(ref);
+        if (it == errors.end()) { err = "error start event with an unknown errorRef"; return false; }
+        if (!it->second.empty() && it->second[0] == '=') { err = "error code expression outside the supported subset"; return false; }
+        e.error_code = it->second;
+      }
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
+    } else if (n == "startEvent") {
       e.type = ZBHIP_EL_START_EVENT;
       // StartEventTransformer.java:40 — event type from the event definition
       const XNode* med = k->child("messageEventDefinition");
@@ -893,10 +915,20 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
       const XNode* ext = k->child("extensionElements");
       if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
       e.event = ZBHIP_EV_NONE;
+    } else if (n == "subProcess" && k->attr("triggeredByEvent") == "true") {
+      // an event sub-process (SubProcessTransformer.transformEventSubprocess :36-60): EVENT_SUB_PROCESS,
+      // attached to its container -- the process or an embedded sub-process; one error start event
+      e.type = ZBHIP_EL_EVENT_SUB_PROCESS;
+      const XNode* ext = k->child("extensionElements");
+      if ((ext && ext->child("ioMapping")) || k->child("multiInstanceLoopCharacteristics") ||
+          k->child("standardLoopCharacteristics") ||
+          (P.els[scope].type != ZBHIP_EL_PROCESS && P.els[scope].type != ZBHIP_EL_SUB_PROCESS)) {
+        err = "event sub-process outside the supported subset";
+        return false;
+      }
     } else if (n == "subProcess") {
-      // embedded sub-process only (SubProcessProcessor): no event sub-process, no loop, no mappings
+      // embedded sub-process (SubProcessProcessor): no loop
       e.type = ZBHIP_EL_SUB_PROCESS;
-      if (k->attr("triggeredByEvent") == "true") { err = "event sub-process outside the supported subset"; return false; }
       if (k->child("multiInstanceLoopCharacteristics") || k->child("standardLoopCharacteristics")) {
         err = "multi-instance outside the supported subset";
         return false;
@@ -951,6 +983,16 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
     if (type == ZBHIP_EL_SUB_PROCESS) {
       if (!walk(*k, self)) return false;
       if (P.els[self].start < 0) { err = "sub-process without a none start event"; return false; }
+    } else if (type == ZBHIP_EL_EVENT_SUB_PROCESS) {
+      if (!walk(*k, self)) return false;
+      if (P.els[self].start < 0) { err = "event sub-process without an error start event"; return false; }
+      P.els[scope].esps.push_back(self);  // ExecutableActivity.attach(eventSubprocess)
+    } else if (type == ZBHIP_EL_START_EVENT && P.els[scope].type == ZBHIP_EL_EVENT_SUB_PROCESS) {
+      if (event != ZBHIP_EV_ERROR || P.els[scope].start >= 0) {
+        err = "event sub-process start event outside the supported subset";
+        return false;
+      }
+      P.els[scope].start = self;
     } else if (type == ZBHIP_EL_START_EVENT && event == ZBHIP_EV_NONE) {
       P.els[scope].start = self;
     } else if (type == ZBHIP_EL_START_EVENT) {
@@ -1051,6 +1093,7 @@ struct ElementInstance {  // state/instance/ElementInstance.java:23-54
   PiValue value;
   int activeSequenceFlows = 0;
   int childActivated = 0, childCompleted = 0, childTerminated = 0, loopCounter = 0;  // multi-instance (ElementInstance.java:25-33)
+  int interrupting_elem = -1;  // interruptingElementId: the interrupting event sub-process (EventSubProcessInterruptionMarker)
 };
 
 struct Doc {  // a variable document (msgpack map) as a list of entries
@@ -2511,11 +2554,16 @@ class Oracle {
     if (sit != ei_.end()) {
       const OEl& owner = procs[sit->second.value.proc].els[sit->second.value.elem];
       const bool attached = std::find(owner.boundaries.begin(), owner.boundaries.end(), elem) != owner.boundaries.end();
-      const bool interrupting = owner.id == procs[proc].els[elem].id ? owner.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
-                                                                           owner.type == ZBHIP_EL_BOUNDARY_EVENT
-                                                                     : attached && procs[proc].els[elem].interrupting;
+      const OEl& te = procs[proc].els[elem];
+      const bool esp_start = te.type == ZBHIP_EL_START_EVENT && te.scope > 0 &&
+                             std::find(owner.esps.begin(), owner.esps.end(), te.scope) != owner.esps.end();
+      const bool interrupting = owner.id == te.id ? owner.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
+                                                        owner.type == ZBHIP_EL_BOUNDARY_EVENT
+                                                  : (attached || esp_start) && te.interrupting;
       if (interrupting) es_interrupted_.insert(scope);
       if (interrupting && attached) es_closed_.insert(scope);
+      // EventSubProcessInterruptionMarker.markInstanceIfInterrupted (:36-63)
+      if (esp_start && te.interrupting) sit->second.interrupting_elem = te.scope;
     }
     triggers_[{scope, eventKey}] = EventTrigger{elem, proc, vars, piKey};
   }
@@ -3269,7 +3317,12 @@ class Oracle {
       // findErrorCatchEventInScope: the element's error catch events ordered by errorCode, descending
       // (ERROR_CODE_COMPARATOR: DirectBuffer.compareTo -- signed bytes, then length -- reversed; a
       // stable sort), each visited code joining the available ones until the first match
+      // (getEvents: the event sub-processes' start events -- each attached at index 0, so the last one
+      // first -- then the boundary events)
       std::vector<int> errs;
+      for (auto e = el.esps.rbegin(); e != el.esps.rend(); ++e)
+        if (P(inst.value.proc).els[P(inst.value.proc).els[*e].start].event == ZBHIP_EV_ERROR)
+          errs.push_back(P(inst.value.proc).els[*e].start);
       for (int b : el.boundaries)
         if (P(inst.value.proc).els[b].event == ZBHIP_EV_ERROR) errs.push_back(b);
       auto signed_less = [](const std::string& x, const std::string& y) {
@@ -3372,7 +3425,55 @@ class Oracle {
     pe.r.aux = cmd.doc.count ? (int64_t)cmd.doc.begin : -1;
     pe.doc = cmd.doc;
     trigger_event(scope, eventKey, catch_elem, task.value.proc, cmd.doc, task.value.piKey);
+    if (P(task.value.proc).els[catch_elem].type == ZBHIP_EL_START_EVENT) {
+      trigger_event_sub_process(catch_elem, scope);  // an event sub-process's start event
+      return;
+    }
     pi_command(scope, ZBHIP_PI_TERMINATE_ELEMENT, task.value);
+  }
+
+  // EventTriggerBehavior.triggerEventSubProcess (common/EventTriggerBehavior.java:74-118): discarded when
+  // the flow scope is interrupted by another event sub-process or holds no trigger; an interrupting one
+  // terminates the flow scope's children (a TERMINATE_ELEMENT each, key order, those that can terminate)
+  // and activates the event sub-process once none is active -- at once when there was none, else from
+  // the flow scope's onChildTerminated
+  void trigger_event_sub_process(int start, int64_t scope) {
+    ElementInstance& fs = ei_.at(scope);
+    const OEl& st = P(fs.value.proc).els[start];
+    if (fs.interrupting_elem >= 0 && fs.interrupting_elem != st.scope) return;
+    auto tit = triggers_.lower_bound({scope, INT64_MIN});
+    if (tit == triggers_.end() || tit->first.first != scope) return;
+    if (st.interrupting) {
+      std::vector<int64_t> children;  // unsubscribeEventSubprocesses: error start events hold none
+      for (auto it = parent_child_.lower_bound({scope, INT64_MIN}); it != parent_child_.end() && it->first == scope; ++it)
+        children.push_back(it->second);
+      for (int64_t c : children) {
+        const ElementInstance& ci = ei_.at(c);
+        if (ci.state == ZBHIP_PI_ELEMENT_ACTIVATING || ci.state == ZBHIP_PI_ELEMENT_ACTIVATED ||
+            ci.state == ZBHIP_PI_ELEMENT_COMPLETING)
+          pi_command(c, ZBHIP_PI_TERMINATE_ELEMENT, ci.value);
+      }
+      if (ei_.at(scope).childCount != 0) return;
+    }
+    activate_event_sub_process(scope);
+  }
+
+  // BpmnEventSubscriptionBehavior.activateTriggeredEvent -> EventTriggerBehavior.activateTriggeredEvent
+  // (:191-244) for an event sub-process's start event: activateEventSubProcess (:258-264) --
+  // ACTIVATE_ELEMENT of the event sub-process as a new command (key -1; the start event's trigger stays
+  // for its output mappings: no PROCESS_EVENT:TRIGGERED)
+  void activate_event_sub_process(int64_t scope) {
+    auto tit = triggers_.lower_bound({scope, INT64_MIN});
+    if (tit == triggers_.end() || tit->first.first != scope) return;
+    PiValue c = ei_.at(scope).value;
+    c.elem = P(c.proc).els[tit->second.elem].scope;
+    c.flowScopeKey = scope;
+    pi_command(-1, ZBHIP_PI_ACTIVATE_ELEMENT, c);
+  }
+
+  // BpmnStateBehavior.isInterrupted (:205-212): no active child, interrupted by an event sub-process, active
+  bool esp_interrupted(const ElementInstance& fs) const {
+    return fs.childCount == 0 && fs.interrupting_elem >= 0 && fs.state == ZBHIP_PI_ELEMENT_ACTIVATED;
   }
 
   // BpmnJobActivationBehavior.publishWork (processing/bpmn/behavior/BpmnJobActivationBehavior.java:61-100):
@@ -3676,7 +3777,14 @@ class Oracle {
           state_name(it->second.state) + "'.";
       return false;
     }
-    return true;  // never interrupted in the supported subset
+    // hasNonInterruptedFlowScope (:160-174): only the interrupting event sub-process itself
+    const int ie = it->second.interrupting_elem;
+    if (ie >= 0 && ie != cmd.pi.elem) {
+      v = "Expected flow scope instance to be not interrupted but was interrupted by an event with id '" +
+          P(cmd.pi.proc).els[ie].id + "'.";
+      return false;
+    }
+    return true;
   }
 
   bool check_state_transition(const ORecord& cmd, std::string& v) {
@@ -3763,6 +3871,7 @@ class Oracle {
         pi_command(-1, ZBHIP_PI_ACTIVATE_ELEMENT, c);
         break;
       }
+      case ZBHIP_EL_EVENT_SUB_PROCESS:  // EventSubProcessProcessor.onActivate (container/EventSubProcessProcessor.java:41-54)
       case ZBHIP_EL_SUB_PROCESS: {  // SubProcessProcessor.onActivate (processing/bpmn/container/SubProcessProcessor.java:49-66)
         // applyInputMappings, transitionToActivated, activateChildInstance(none start)
         apply_input_mappings(el, key, v);
@@ -3902,6 +4011,10 @@ class Oracle {
         // unsubscribeFromEvents (its boundary timer: TIMER:CANCELED), transitionToCompleted, take flows
         complete_and_take(el, key, v, true, /*unsubscribe=*/true);
         break;
+      case ZBHIP_EL_EVENT_SUB_PROCESS:  // EventSubProcessProcessor.onComplete (:58-66): applyOutputMappings,
+        // transitionToCompleted (no outgoing flows: the flow scope's afterExecutionPathCompleted)
+        complete_and_take(el, key, v, true);
+        break;
       case ZBHIP_EL_SERVICE_TASK:  // JobWorkerTaskProcessor.onComplete (:63-75)
       case ZBHIP_EL_SEND_TASK:
       case ZBHIP_EL_SCRIPT_TASK:
@@ -3974,7 +4087,8 @@ class Oracle {
       }
       return;
     }
-    if (el.type == ZBHIP_EL_SUB_PROCESS) {
+    if (el.type == ZBHIP_EL_SUB_PROCESS || el.type == ZBHIP_EL_EVENT_SUB_PROCESS) {
+      // (EventSubProcessProcessor.onTerminate :68-77: terminateChildInstances, no subscriptions)
       unsubscribe_timers(key);  // unsubscribeFromEvents
       unsubscribe_messages(key);
       const ElementInstance& sub = ei_.at(key);
@@ -4055,13 +4169,18 @@ class Oracle {
         pi_command(body.key, ZBHIP_PI_COMPLETE_ELEMENT, body.value);
       return;
     }
-    if (fe.type == ZBHIP_EL_SUB_PROCESS) {
+    if (fe.type == ZBHIP_EL_SUB_PROCESS || fe.type == ZBHIP_EL_EVENT_SUB_PROCESS) {
       // canBeTerminated(child): no active child of the sub-process is left
       if (fit->second.childCount == 0) container_child_terminated(fit->first);
       return;
     }
-    // ProcessProcessor.onChildTerminated (:143-180): an active process with an active child left (the
-    // boundary event a terminated multi-instance body's trigger activated) does nothing
+    // ProcessProcessor.onChildTerminated (:143-180): interrupted by an event sub-process, its trigger
+    // activates it; an active process with an active child left (the boundary event a terminated
+    // multi-instance body's trigger activated) does nothing
+    if (esp_interrupted(fit->second)) {
+      activate_event_sub_process(fit->first);
+      return;
+    }
     if (fit->second.state == ZBHIP_PI_ELEMENT_ACTIVATED && fit->second.childCount > 0) return;
     throw Unsupported{"terminated child of the process (cancel)"};
   }
@@ -4094,6 +4213,10 @@ class Oracle {
   void container_child_terminated(int64_t key) {
     const ElementInstance sub = ei_.at(key);
     const PiValue v = sub.value;
+    if (esp_interrupted(sub)) {  // an interrupting event sub-process was triggered (SubProcessProcessor :114-125)
+      activate_event_sub_process(key);
+      return;
+    }
     auto tit = triggers_.lower_bound({key, INT64_MIN});
     const bool found = tit != triggers_.end() && tit->first.first == key;
     auto fit = ei_.find(v.flowScopeKey);
@@ -4396,7 +4519,8 @@ class Oracle {
         // createEventScope (:255-289): job worker elements get an event scope
         // (a sub-process only with events: its boundary event)
         if (ZBHIP_IS_JOB_WORKER(el.type) || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
-            el.type == ZBHIP_EL_BOUNDARY_EVENT || (el.type == ZBHIP_EL_SUB_PROCESS && el.boundary >= 0))
+            el.type == ZBHIP_EL_BOUNDARY_EVENT || (el.type == ZBHIP_EL_SUB_PROCESS && el.boundary >= 0) ||
+            ((el.type == ZBHIP_EL_PROCESS || el.type == ZBHIP_EL_SUB_PROCESS) && !el.esps.empty()))
           event_scope_.insert(key);
         // cleanupSequenceFlowsTaken (:79-98): Tetris decrement of (flowScope, gateway)
         if (el.type == ZBHIP_EL_PARALLEL_GATEWAY) {
@@ -4438,8 +4562,22 @@ class Oracle {
           case ZBHIP_EL_PARALLEL_GATEWAY:
             for (size_t i = 0; i < el.in.size(); ++i) dec();
             break;
+          case ZBHIP_EL_EVENT_SUB_PROCESS:  // decrementEventSubProcessSequenceFlow (:206-218): interrupting -> reset
+            if (P(v.proc).els[el.start].interrupting) fs.activeSequenceFlows = 0;
+            break;
           default:
             dec();
+        }
+        if (el.type == ZBHIP_EL_START_EVENT && E(fs.value).type == ZBHIP_EL_EVENT_SUB_PROCESS) {
+          // moveVariablesToNewEventScope (:102-116): the event sub-process's flow scope's (first) event
+          // trigger moves to the start event's instance, whose output mappings read its variables
+          auto tit = triggers_.lower_bound({fs.parentKey, INT64_MIN});
+          if (tit != triggers_.end() && tit->first.first == fs.parentKey) {
+            EventTrigger t = tit->second;
+            const int64_t eventKey = tit->first.second;
+            triggers_.erase(tit);
+            triggers_[{key, eventKey}] = t;
+          }
         }
         break;
       }
@@ -4514,11 +4652,12 @@ std::string Oracle::dump_state() const {
     const OEl& el = procs[e.value.proc].els[e.value.elem];
     snprintf(buf, sizeof buf,
              "ELEMENT_INSTANCE_KEY|%lld|parentKey=%lld,childCount=%d,childActivatedCount=%d,childCompletedCount=%d,"
-             "childTerminatedCount=%d,jobKey=%lld,multiInstanceLoopCounter=%d,interruptingElementId=,"
+             "childTerminatedCount=%d,jobKey=%lld,multiInstanceLoopCounter=%d,interruptingElementId=%s,"
              "calledChildInstanceKey=-1,state=%d,elementId=%s,bpmnElementType=%d,bpmnEventType=%d,flowScopeKey=%lld,"
              "processInstanceKey=%lld,processDefinitionKey=%lld,activeSequenceFlows=%d",
              (long long)k, (long long)e.parentKey, e.childCount, e.childActivated, e.childCompleted,
-             e.childTerminated, (long long)e.jobKey, e.loopCounter, e.state, el.id.c_str(), el.type,
+             e.childTerminated, (long long)e.jobKey, e.loopCounter,
+             e.interrupting_elem >= 0 ? procs[e.value.proc].els[e.interrupting_elem].id.c_str() : "", e.state, el.id.c_str(), el.type,
              el.event, (long long)e.value.flowScopeKey, (long long)e.value.piKey,
              (long long)procs[e.value.proc].def_key, e.activeSequenceFlows);
     rows.push_back(buf);
@@ -4567,10 +4706,15 @@ std::string Oracle::dump_state() const {
     const OEl* el = op ? &op->els[eit->second.value.elem] : nullptr;
     std::string intr, bnd;
     if (el && (el->type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || el->type == ZBHIP_EL_BOUNDARY_EVENT)) intr = el->id;
-    if (el && el->boundary >= 0) {  // interruptingIds only for cancelActivity boundary events
+    if (el && (el->boundary >= 0 || !el->esps.empty())) {  // interruptingIds only for cancelActivity boundary events
       for (int b : el->boundaries) {
         bnd += (bnd.empty() ? "" : ";") + op->els[b].id;
         if (op->els[b].interrupting) intr += (intr.empty() ? "" : ";") + op->els[b].id;
+      }
+      // then the interrupting event sub-processes' start events (attached in a later transformation step)
+      for (int esp : el->esps) {
+        const OEl& st = op->els[op->els[esp].start];
+        if (st.interrupting) intr += (intr.empty() ? "" : ";") + st.id;
       }
     }
     snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=%d,interrupted=%d,interrupting=%s,boundaryElementIds=%s",

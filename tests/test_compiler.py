@@ -140,3 +140,22 @@ def test_random_processes_with_error_boundary_events_compile_like_the_oracle():
         assert o.deploy(xml) == 0
         assert [c.id(i) for i in range(len(c.els))] == [o.element_id(0, i) for i in range(len(c.els))]
     assert n_errors >= 20
+
+
+def test_event_sub_processes_compile_like_the_oracle():
+    # error-start event sub-processes in the process and in an embedded sub-process: the same element
+    # indexing on both sides, the start event's error code in message_name, interrupting in job_retries
+    from test_oracle_event_subprocess import esp_process
+    b = bpmn.createExecutableProcess("wf").startEvent().subProcess("sub")
+    b.eventSubProcess("inner-esp").startEvent("inner-start").error("E").serviceTask("fix", "fix").endEvent("ie")
+    b.eventSubProcessDone().startEvent("s2").serviceTask("task", "test").endEvent("e2").subProcessDone()
+    nested = b.endEvent("end").done()
+    for xml in (esp_process(("esp", "esp-start", "E1"), ("esp2", "esp2-start", None)), nested):
+        c = Compiled(xml)
+        o = Oracle()
+        assert o.deploy(xml) == 0
+        assert [c.id(i) for i in range(len(c.els))] == [o.element_id(0, i) for i in range(len(c.els))]
+        # (ZBHIP_EL_START_EVENT = 4, ZBHIP_EV_ERROR = 2 -- zbhip.h)
+        starts = [i for i in range(len(c.els)) if int(c.els[i]["element_type"]) == 4
+                  and int(c.els[i]["event_type"]) == 2]
+        assert starts and all(int(c.els[i]["job_retries"]) & 1 for i in starts)

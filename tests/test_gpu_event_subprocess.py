@@ -1,0 +1,65 @@
+"""Error-start event sub-processes in the reference's processing loop.  A process (or an embedded
+sub-process) with event sub-processes whose start events catch errors runs on the device -- they subscribe
+to nothing; the instance's (the sub-process's) event scope lists their start events among its interrupting
+ids, as the state export writes it -- and a JOB:THROW_ERROR of a device job moves the instance to the engine
+(the adapter's held-instance hand-off), which terminates the flow scope's children and runs the event
+sub-process (oracle pinned by tests/test_oracle_event_subprocess.py).  The same workload through the loop
+over the engine alone and through [adapter, engine]: every log and state equal, at batch limits 3 and 100."""
+import pytest
+
+from psm import Client, open_jobs
+from test_gpu_scheduled import KEY_A, KEY_B, KEY_C, check, single, write
+from zeebe_amd import abi, bpmn
+
+pytestmark = pytest.mark.gpu
+
+
+def processes():
+    # the process's event sub-processes (code-specific with a recovery task, catch-all) and two branches
+    a = bpmn.createExecutableProcess("esp")
+    a.eventSubProcess("on-e1").startEvent("e1-start").error("E1").serviceTask("recover", "recover").endEvent("e1-end")
+    a.eventSubProcessDone().eventSubProcess("on-any").startEvent("any-start").error().endEvent("any-end")
+    a.eventSubProcessDone().startEvent("start").parallelGateway("fork").serviceTask("work", "work")
+    a = a.parallelGateway("join").moveToNode("fork").serviceTask("other", "other").connectTo("join").endEvent("end").done()
+    # an event sub-process inside an embedded sub-process, beside the sub-process's own error boundary
+    b = bpmn.createExecutableProcess("nested").startEvent("s").subProcess("sub")
+    b.eventSubProcess("inner").startEvent("inner-start").error("E2").endEvent("inner-end").eventSubProcessDone()
+    b.startEvent("sub-start").serviceTask("work", "work").endEvent("sub-end").subProcessDone()
+    b = b.boundaryEvent("outer").error("E2").endEvent("outer-end").moveToActivity("sub").endEvent("end").done()
+    # the task's own boundary event first, then the process's event sub-process
+    c = bpmn.createExecutableProcess("both").eventSubProcess("proc-esp").startEvent("ps").error("E3").endEvent("pe")
+    c.eventSubProcessDone().startEvent("s").serviceTask("work", "work").boundaryEvent("b").error("E1").endEvent("be")
+    c = c.moveToActivity("work").endEvent("end").done()
+    return a, b, c
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_error_event_sub_processes_in_the_processing_loop(limit):
+    a, b, c = processes()
+    deps = [(a, KEY_A, 1), (b, KEY_B, 1), (c, KEY_C, 1)]
+    ref, gpu = single(deps, deps, limit=limit)
+    write(ref, gpu, *([Client.create("esp") for _ in range(6)] + [Client.create("nested") for _ in range(3)] +
+                      [Client.create("both") for _ in range(3)]))
+    ad = gpu.parts[0].adapter
+    assert ad.counts["device_commands"] >= 12
+    jobs = sorted((k, r.value["elementId"], r.value["processInstanceKey"]) for k, r in open_jobs(ref.parts[0].log).items())
+    work = [k for k, e, _ in jobs if e == "work"]
+    other = [k for k, e, _ in jobs if e == "other"]
+    write(ref, gpu, Client.throw_error(work[0], "E1", "", variables=(("why", "x"),)), Client.throw_error(work[1], "Z"),
+          Client.throw_error(other[2], "E1"), Client.complete_job(work[3]), Client.complete_job(other[3]),
+          Client.throw_error(work[6], "E2"), Client.throw_error(work[7], "nope"), Client.throw_error(work[9], "E1"),
+          Client.throw_error(work[10], "E3"), Client.complete_job(work[11]))
+    for _ in range(3):
+        dead = {r.key for r in ref.parts[0].log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_ERROR_THROWN}
+        live = sorted(k for k in open_jobs(ref.parts[0].log) if k not in dead)
+        if not live:
+            break
+        write(ref, gpu, *[Client.complete_job(k) for k in live])
+    check(ref, gpu)
+    log = gpu.parts[0].log.entries
+    done = [r.value["elementId"] for r in log if r.value_type == abi.VT_PROCESS_INSTANCE
+            and r.intent == abi.PI_ELEMENT_COMPLETED]
+    assert done.count("on-e1") == 2 and done.count("on-any") == 1 and done.count("inner") == 1
+    assert done.count("b") == 1 and done.count("proc-esp") == 1
+    assert [r for r in log if r.value_type == abi.VT_VARIABLE and r.value["name"] == "why"]
+    assert not ad.fallback_reasons

@@ -149,6 +149,27 @@ class ProcessBuilder:
         self._pending_flow = None
         return self
 
+    def eventSubProcess(self, id_=None):
+        """AbstractFlowNodeBuilder / ProcessBuilder.eventSubProcess(id, e -> ...): a subProcess with
+        triggeredByEvent="true" in the current container, not connected; its children follow (its start
+        event: startEvent(..).error(code)); ``eventSubProcessDone()`` returns to where the builder was."""
+        id_ = id_ or self._gen_id("eventSubProcess")
+        n = _Node("subProcess", id_, triggeredByEvent="true")
+        n.children = []
+        self.children.append(n)
+        self.nodes[id_] = n
+        self._container_of[id_] = self.children
+        self._stack.append((self.children, self.current))
+        self.children = n.children
+        self.current = None
+        self._pending_flow = None
+        return self
+
+    def eventSubProcessDone(self):
+        self.children, self.current = self._stack.pop()
+        self._pending_flow = None
+        return self
+
     def boundaryEvent(self, id_=None):
         """AbstractActivityBuilder.boundaryEvent(id): a boundaryEvent sibling of the current activity
         appended to its container (no connecting flow), attachedToRef = the activity; the builder
@@ -165,8 +186,8 @@ class ProcessBuilder:
         return self
 
     def error(self, error_code=None):
-        """BoundaryEventBuilder.error(code): an <errorEventDefinition> referring to an <error errorCode>;
-        no code: a catch-all errorEventDefinition without errorRef."""
+        """BoundaryEventBuilder / StartEventBuilder.error(code): an <errorEventDefinition> referring to an
+        <error errorCode>; no code: a catch-all errorEventDefinition without errorRef."""
         self.current.error = error_code if error_code is not None else ""
         return self
 
@@ -310,6 +331,12 @@ class ProcessBuilder:
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
                                '</intermediateCatchEvent>' % (ind, quoteattr(c.id), quoteattr(c.id + "_med"),
                                                               quoteattr(c.message[0])))
+                elif c.kind == "startEvent" and getattr(c, "error", None) is not None:
+                    ref = ' errorRef=%s' % quoteattr("Error_" + c.id) if c.error else ""
+                    if c.error:
+                        errors.append(c)
+                    out.append('%s<startEvent id=%s><errorEventDefinition id=%s%s/></startEvent>'
+                               % (ind, quoteattr(c.id), quoteattr(c.id + "_eed"), ref))
                 elif c.kind == "startEvent" and c.message:
                     catches.append(c)
                     out.append('%s<startEvent id=%s><messageEventDefinition id=%s messageRef=%s/></startEvent>'
@@ -342,7 +369,8 @@ class ProcessBuilder:
                     out.append("%s<exclusiveGateway id=%s default=%s/>" % (ind, quoteattr(c.id), quoteattr(c.default.id)))
                 elif c.kind == "subProcess":
                     ext = "<extensionElements>%s</extensionElements>" % io(c) if c.mappings else ""
-                    out.append("%s<subProcess id=%s>%s" % (ind, quoteattr(c.id), ext))
+                    trig = ' triggeredByEvent="true"' if c.attrs.get("triggeredByEvent") else ""
+                    out.append("%s<subProcess id=%s%s>%s" % (ind, quoteattr(c.id), trig, ext))
                     render(c.children, ind + "  ")
                     out.append("%s</subProcess>" % ind)
                 elif c.multi:

@@ -833,7 +833,10 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       else if (c.tag == "intermediateThrowEvent") type = ZBHIP_EL_INTERMEDIATE_THROW_EVENT;
       else if (c.tag == "task") type = ZBHIP_EL_TASK;
       else if (c.tag == "manualTask") type = ZBHIP_EL_MANUAL_TASK;
-      else if (c.tag == "subProcess") type = ZBHIP_EL_SUB_PROCESS;
+      else if (c.tag == "subProcess") {
+        const std::string* tbe = c.get("triggeredByEvent");
+        type = tbe && *tbe == "true" ? ZBHIP_EL_EVENT_SUB_PROCESS : ZBHIP_EL_SUB_PROCESS;
+      }
       else if (c.tag == "boundaryEvent") type = ZBHIP_EL_BOUNDARY_EVENT;
       else if (c.tag == "extensionElements" || c.tag == "documentation" || c.tag == "textAnnotation" ||
                c.tag == "association" || c.tag == "incoming" || c.tag == "outgoing")
@@ -844,13 +847,51 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       if (C.elements.size() >= 0xFF0) { err = "too many elements"; return ZBHIP_EUNSUPP; }
       zbhip_element e = blank(type, C.str(*id));
       e.flow_scope = scope;
-      if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_END_EVENT) {
+      const bool esp_start = type == ZBHIP_EL_START_EVENT && C.elements[scope].element_type == ZBHIP_EL_EVENT_SUB_PROCESS;
+      if (esp_start) {
+        // the error start event of an event sub-process (CatchEventTransformer.java:166): a static
+        // errorCode ("" catches every code) in message_name, interrupting (isInterrupting, default true)
+        // in job_retries bit 0; the device never activates it -- a JOB:THROW_ERROR hands the instance off
+        const Elem* eed = c.first("errorEventDefinition");
+        for (auto& d : c.children)
+          if (&d != eed && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+            err = "event definition <" + d.tag + "> of an event sub-process outside the supported subset";
+            return ZBHIP_EUNSUPP;
+          }
+        const std::string* ii = c.get("isInterrupting");
+        if (!eed || (ii && *ii == "false")) {
+          err = "event sub-process start event outside the supported subset (interrupting error start events)";
+          return ZBHIP_EUNSUPP;
+        }
+        std::string code;
+        if (const std::string* ref = eed->get("errorRef")) {
+          auto ei = errors.find(*ref);
+          if (ei == errors.end()) { err = "unknown error " + *ref; return ZBHIP_EPARSE; }
+          code = ei->second;
+          if (!code.empty() && code[0] == '=') { err = "error code expressions outside the supported subset"; return ZBHIP_EUNSUPP; }
+        }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        e.event_type = ZBHIP_EV_ERROR;
+        e.message_name = C.str(code);
+        e.job_retries = 1;
+      } else if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_END_EVENT) {
         for (auto& d : c.children)
           if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
             err = "event definition <" + d.tag + "> outside the supported subset";
             return ZBHIP_EUNSUPP;
           }
         e.event_type = ZBHIP_EV_NONE;
+      }
+      if (type == ZBHIP_EL_EVENT_SUB_PROCESS) {
+        // an event sub-process (SubProcessTransformer.transformEventSubprocess :36-60), attached to the
+        // process or an embedded sub-process; its start event is its start_event
+        if (c.first("multiInstanceLoopCharacteristics") || c.first("standardLoopCharacteristics") ||
+            (c.first("extensionElements") && c.first("extensionElements")->first("ioMapping")) ||
+            (scope != 0 && C.elements[scope].element_type != ZBHIP_EL_SUB_PROCESS)) {
+          err = "event sub-process outside the supported subset";
+          return ZBHIP_EUNSUPP;
+        }
       }
       if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT || type == ZBHIP_EL_TASK || type == ZBHIP_EL_MANUAL_TASK) {
         // activities / events without behaviour (UndefinedTaskProcessor, ManualTaskProcessor,
@@ -865,10 +906,7 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         if (type == ZBHIP_EL_INTERMEDIATE_THROW_EVENT) e.event_type = ZBHIP_EV_NONE;
       }
       if (type == ZBHIP_EL_SUB_PROCESS) {
-        // embedded sub-process (SubProcessTransformer / SubProcessProcessor): no event
-        // sub-process, no multi-instance, no io mappings
-        const std::string* tbe = c.get("triggeredByEvent");
-        if (tbe && *tbe == "true") { err = "event sub-process outside the supported subset"; return ZBHIP_EUNSUPP; }
+        // embedded sub-process (SubProcessTransformer / SubProcessProcessor): no multi-instance
         if (c.first("multiInstanceLoopCharacteristics") || c.first("standardLoopCharacteristics")) {
           err = "multi-instance sub-process outside the supported subset";
           return ZBHIP_EUNSUPP;
@@ -1055,6 +1093,13 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
       C.elements.push_back(e);
       if (type == ZBHIP_EL_SUB_PROCESS) {
         if (int rc = container(c, self)) return rc;
+      } else if (type == ZBHIP_EL_EVENT_SUB_PROCESS) {
+        if (int rc = container(c, self)) return rc;
+        const uint16_t st = C.elements[self].start_event;
+        if (st == ZBHIP_NONE16 || C.elements[st].event_type != ZBHIP_EV_ERROR) {
+          err = "event sub-process without an error start event";
+          return ZBHIP_EUNSUPP;
+        }
       } else if (type == ZBHIP_EL_START_EVENT) {
         // getNoneStartEvent of the container (the last none start event in document order)
         C.elements[scope].start_event = self;

@@ -1407,8 +1407,29 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
         e.element_type != ZBHIP_EL_EXCLUSIVE_GATEWAY && e.element_type != ZBHIP_EL_PARALLEL_GATEWAY &&
         e.element_type != ZBHIP_EL_SEQUENCE_FLOW && e.element_type != ZBHIP_EL_INTERMEDIATE_CATCH_EVENT &&
         e.element_type != ZBHIP_EL_SUB_PROCESS && e.element_type != ZBHIP_EL_BOUNDARY_EVENT &&
-        e.element_type != ZBHIP_EL_MULTI_INSTANCE_BODY && !pass_through(e.element_type))
+        e.element_type != ZBHIP_EL_MULTI_INSTANCE_BODY && e.element_type != ZBHIP_EL_EVENT_SUB_PROCESS &&
+        !pass_through(e.element_type))
       return ZBHIP_EUNSUPP;
+  // event sub-processes (error start events only): never entered on the device -- a JOB:THROW_ERROR hands
+  // the instance to the engine, which activates them -- so their contents are held to elements that need
+  // no deploy-time device state (no catch or boundary events, no nested containers); an error start event
+  // lives only there
+  for (size_t e = 1; e < P.els.size(); ++e) {
+    const zbhip_element& E = P.els[e];
+    if (E.flow_scope >= P.els.size()) return ZBHIP_EINVAL;
+    if (E.element_type == ZBHIP_EL_START_EVENT && E.event_type != ZBHIP_EV_NONE &&
+        (E.event_type != ZBHIP_EV_ERROR || P.els[E.flow_scope].element_type != ZBHIP_EL_EVENT_SUB_PROCESS))
+      return ZBHIP_EINVAL;
+    bool inside = false;
+    for (uint32_t c = E.flow_scope, d = 0; c != 0 && c < P.els.size() && d < 64; c = P.els[c].flow_scope, ++d)
+      inside |= P.els[c].element_type == ZBHIP_EL_EVENT_SUB_PROCESS;
+    if (!inside) continue;
+    const bool ok = E.element_type == ZBHIP_EL_START_EVENT || E.element_type == ZBHIP_EL_END_EVENT ||
+                    (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event == ZBHIP_NONE16) ||
+                    E.element_type == ZBHIP_EL_EXCLUSIVE_GATEWAY || E.element_type == ZBHIP_EL_PARALLEL_GATEWAY ||
+                    E.element_type == ZBHIP_EL_SEQUENCE_FLOW || pass_through(E.element_type);
+    if (!ok) return ZBHIP_EUNSUPP;
+  }
   // timer and message boundary events: one per job worker task, in the task's container (message
   // boundary events: the process's, KMsg has no flow scopes)
   for (size_t e = 0; e < P.els.size(); ++e) {
@@ -1436,7 +1457,13 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
   for (size_t e = 0; e < P.els.size(); ++e) {  // containers: a sub-process element, before its children
     const zbhip_element& E = P.els[e];
     if (e > 0 && (E.flow_scope >= e || (E.flow_scope && P.els[E.flow_scope].element_type != ZBHIP_EL_SUB_PROCESS &&
-                                        P.els[E.flow_scope].element_type != ZBHIP_EL_MULTI_INSTANCE_BODY)))
+                                        P.els[E.flow_scope].element_type != ZBHIP_EL_MULTI_INSTANCE_BODY &&
+                                        P.els[E.flow_scope].element_type != ZBHIP_EL_EVENT_SUB_PROCESS)))
+      return ZBHIP_EINVAL;
+    if (E.element_type == ZBHIP_EL_EVENT_SUB_PROCESS &&
+        (E.start_event >= P.els.size() || P.els[E.start_event].flow_scope != e ||
+         P.els[E.start_event].event_type != ZBHIP_EV_ERROR ||
+         (E.flow_scope != 0 && P.els[E.flow_scope].element_type != ZBHIP_EL_SUB_PROCESS)))
       return ZBHIP_EINVAL;
     if (E.flow_scope && P.els[E.flow_scope].element_type == ZBHIP_EL_MULTI_INSTANCE_BODY &&
         P.els[E.flow_scope].start_event != e)
@@ -3935,6 +3962,27 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
   sink(ctx, buf);
   snprintf(buf, sizeof buf, "PROCESS_INSTANCE_KEY_BY_DEFINITION_KEY|%lld|%lld", (long long)P.def_key, pik);
   sink(ctx, buf);
+  // the start events of the event sub-processes attached to container c (SubProcessTransformer: after
+  // the boundary events), the interrupting ones (job_retries bit 0)
+  auto esp_ids = [&](uint32_t c, std::string& intr, bool& any) {
+    for (size_t x = 0; x < P.els.size(); ++x)
+      if (P.els[x].element_type == ZBHIP_EL_EVENT_SUB_PROCESS && P.els[x].flow_scope == c &&
+          P.els[x].start_event < P.els.size()) {
+        any = true;
+        if (P.els[P.els[x].start_event].job_retries & 1)
+          intr += (intr.empty() ? "" : ";") + P.id(P.els[x].start_event);
+      }
+  };
+  {  // the process instance's event scope: only with event sub-processes (createEventScope: hasEvents)
+    std::string intr;
+    bool any = false;
+    esp_ids(0, intr, any);
+    if (any) {
+      snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=", pik,
+               intr.c_str());
+      sink(ctx, buf);
+    }
+  }
   // the key of the instance of container c (an element's flow scope): the process instance, or the
   // slot of the sub-process element c (one active instance per sub-process element)
   auto scope_key = [&](uint32_t c) -> long long {
@@ -4015,10 +4063,13 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
       snprintf(buf, sizeof buf, "INCIDENT_PROCESS_INSTANCES|%lld|%lld", k, ik);
       sink(ctx, buf);
     }
+    std::string esp_intr;
+    bool has_esp = false;
+    if (E.element_type == ZBHIP_EL_SUB_PROCESS) esp_ids(elem, esp_intr, has_esp);
     const bool sub_bnd = E.element_type == ZBHIP_EL_SUB_PROCESS && E.default_flow != ZBHIP_NONE16 &&
                          E.default_flow < P.els.size();
     if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
-        E.element_type == ZBHIP_EL_BOUNDARY_EVENT || sub_bnd) {
+        E.element_type == ZBHIP_EL_BOUNDARY_EVENT || sub_bnd || has_esp) {
       // EventScopeInstance.java:25-35: a catch / boundary event's interrupting ids are its own id
       // (ExecutableCatchEventElement.java:124-132), a job worker's (a sub-process's: an event scope
       // only with events) those of its interrupting boundary event, which is also its
@@ -4033,6 +4084,7 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
             ids += (ids.empty() ? "" : ";") + P.id((uint32_t)b);
             if (P.els[b].job_retries & 1) intr_ids += (intr_ids.empty() ? "" : ";") + P.id((uint32_t)b);
           }
+      if (!esp_intr.empty()) intr_ids += (intr_ids.empty() ? "" : ";") + esp_intr;
       snprintf(buf, sizeof buf, "EVENT_SCOPE|%lld|accepting=1,interrupted=0,interrupting=%s,boundaryElementIds=%s", k,
                intr_ids.c_str(), bnd ? ids.c_str() : "");
       sink(ctx, buf);
