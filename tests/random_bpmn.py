@@ -209,11 +209,21 @@ class _Gen:
 
 def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages=False, pass_through=False,
                    tasks=True, sub_processes=False, task_kinds=False, boundaries=False, multi_instance=False,
-                   errors=False):
+                   errors=False, event_sub_processes=False):
     """tasks=False: no wait states (the CREATE batch runs the instance to its end); task_kinds: job
     worker tasks among service / send / script / business-rule tasks."""
     g = _Gen(rng, max_depth, max_blocks, messages, pass_through or not tasks, tasks, sub_processes, task_kinds,
              boundaries, multi_instance, errors)
+    # event_sub_processes: one or two error-start event sub-processes of the process (E1 / E2 / catch-all), each
+    # a recovery task or none before its end event (drawn first: the rest of the process keeps its draws
+    # relative to each other)
+    esps = []
+    if event_sub_processes:
+        for i in range(int(rng.integers(1, 3))):
+            code = ("E1", "E2", "")[int(rng.integers(0, 3))]
+            if code:
+                g.error_codes.add(code)
+            esps.append(("esp_%d" % i, code, bool(int(rng.integers(0, 2)))))
     start = g.node("startEvent")
     cur = g.sequence(start, 0, 1)
     end = g.node("endEvent")
@@ -277,6 +287,19 @@ def random_process(rng, process_id="random", max_depth=2, max_blocks=3, messages
                 out.append("%s<sequenceFlow %s><conditionExpression>%s</conditionExpression></sequenceFlow>"
                            % (ind, attrs, escape(cond)))
 
+    for eid, code, task in esps:
+        ref = ' errorRef="err_%s"' % code if code else ""
+        out.append('    <subProcess id="%s" triggeredByEvent="true">' % eid)
+        out.append('      <startEvent id="%s_start"><errorEventDefinition%s/></startEvent>' % (eid, ref))
+        out.append('      <endEvent id="%s_end"/>' % eid)
+        if task:
+            out.append('      <serviceTask id="%s_task"><extensionElements><zeebe:taskDefinition type="recover"/>'
+                       '</extensionElements></serviceTask>' % eid)
+            out.append('      <sequenceFlow id="%s_f1" sourceRef="%s_start" targetRef="%s_task"/>' % (eid, eid, eid))
+            out.append('      <sequenceFlow id="%s_f2" sourceRef="%s_task" targetRef="%s_end"/>' % (eid, eid, eid))
+        else:
+            out.append('      <sequenceFlow id="%s_f1" sourceRef="%s_start" targetRef="%s_end"/>' % (eid, eid, eid))
+        out.append('    </subProcess>')
     render(None, "    ")
     out.append("  </process>")
     if messages:

@@ -63,3 +63,19 @@ def test_error_event_sub_processes_in_the_processing_loop(limit):
     assert done.count("b") == 1 and done.count("proc-esp") == 1
     assert [r for r in log if r.value_type == abi.VT_VARIABLE and r.value["name"] == "why"]
     assert not ad.fallback_reasons
+
+
+# (random processes with error boundary events and one or two error-start event sub-processes; seeds whose
+# campaigns run event sub-processes the most)
+@pytest.mark.parametrize("seed", [1, 5, 10, 13, 16, 35, 37])
+def test_random_processes_with_event_sub_processes(seed):
+    import numpy as np
+    from random_bpmn import random_process
+    from test_gpu_error_events import random_error_campaign
+    xml = random_process(np.random.default_rng(9000 + seed), sub_processes=True, task_kinds=True, errors=True,
+                         event_sub_processes=True)
+    deps = [(xml, KEY_A, 1)]
+    ref, gpu = single(deps, deps, limit=100)
+    random_error_campaign(seed, ref, lambda *r: write(ref, gpu, *r), xml)
+    check(ref, gpu)
+    assert gpu.parts[0].adapter.counts["device_commands"] >= 24 and not gpu.parts[0].adapter.fallback_reasons
