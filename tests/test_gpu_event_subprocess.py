@@ -42,13 +42,18 @@ def test_error_event_sub_processes_in_the_processing_loop(limit):
                       [Client.create("both") for _ in range(3)]))
     ad = gpu.parts[0].adapter
     assert ad.counts["device_commands"] >= 12
-    jobs = sorted((k, r.value["elementId"], r.value["processInstanceKey"]) for k, r in open_jobs(ref.parts[0].log).items())
-    work = [k for k, e, _ in jobs if e == "work"]
-    other = [k for k, e, _ in jobs if e == "other"]
-    write(ref, gpu, Client.throw_error(work[0], "E1", "", variables=(("why", "x"),)), Client.throw_error(work[1], "Z"),
-          Client.throw_error(other[2], "E1"), Client.complete_job(work[3]), Client.complete_job(other[3]),
-          Client.throw_error(work[6], "E2"), Client.throw_error(work[7], "nope"), Client.throw_error(work[9], "E1"),
-          Client.throw_error(work[10], "E3"), Client.complete_job(work[11]))
+    # the jobs by instance (instance keys follow the CREATE order at every batch limit)
+    by = {}
+    for k, r in open_jobs(ref.parts[0].log).items():
+        by.setdefault(r.value["processInstanceKey"], {})[r.value["elementId"]] = k
+    inst = [by[p] for p in sorted(by)]
+    esp, nested, both = inst[:6], inst[6:9], inst[9:]
+    write(ref, gpu, Client.throw_error(esp[0]["work"], "E1", "", variables=(("why", "x"),)),
+          Client.throw_error(esp[1]["work"], "Z"), Client.throw_error(esp[2]["other"], "E1"),
+          Client.complete_job(esp[3]["work"]), Client.complete_job(esp[3]["other"]),
+          Client.throw_error(nested[0]["work"], "E2"), Client.throw_error(nested[1]["work"], "nope"),
+          Client.throw_error(both[0]["work"], "E1"), Client.throw_error(both[1]["work"], "E3"),
+          Client.complete_job(both[2]["work"]))
     for _ in range(3):
         dead = {r.key for r in ref.parts[0].log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_ERROR_THROWN}
         live = sorted(k for k in open_jobs(ref.parts[0].log) if k not in dead)
