@@ -751,6 +751,20 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
         e.event = ZBHIP_EV_MESSAGE;
         e.msg_name = mi->second.first;
       }
+    } else if (n == "endEvent" && k->child("errorEventDefinition")) {
+      // an error end event (EndEventTransformer.java:70-83: ERROR): a static errorCode (ErrorTransformer)
+      e.type = ZBHIP_EL_END_EVENT;
+      e.event = ZBHIP_EV_ERROR;
+      const std::string ref = k->child("errorEventDefinition")->attr("errorRef");
+      auto it = errors.find(ref);
+      if (ref.empty() || it == errors.end() || it->second.empty() || it->second[0] == '=' ||
+          k->child("messageEventDefinition") || k->child("terminateEventDefinition")) {
+        err = "error end event outside the supported subset (a static errorCode)";
+        return false;
+      }
+      e.error_code = it->second;
+      const XNode* ext = k->child("extensionElements");
+      if (ext && ext->child("ioMapping")) { err = "io mappings outside the supported subset"; return false; }
     } else if (n == "endEvent") {
       e.type = ZBHIP_EL_END_EVENT;
       if (k->child("terminateEventDefinition") || k->child("errorEventDefinition") ||
@@ -3308,43 +3322,7 @@ class Oracle {
     std::vector<std::string> avail;
     int catch_elem = -1;
     int64_t scope = job.elementInstanceKey;
-    for (auto it = ei_.find(scope); it != ei_.end() && catch_elem < 0;) {
-      const ElementInstance& inst = it->second;
-      if (!(inst.state == ZBHIP_PI_ELEMENT_ACTIVATING || inst.state == ZBHIP_PI_ELEMENT_ACTIVATED) ||
-          es_interrupted_.count(inst.key))
-        break;
-      const OEl& el = E(inst.value);
-      // findErrorCatchEventInScope: the element's error catch events ordered by errorCode, descending
-      // (ERROR_CODE_COMPARATOR: DirectBuffer.compareTo -- signed bytes, then length -- reversed; a
-      // stable sort), each visited code joining the available ones until the first match
-      // (getEvents: the event sub-processes' start events -- each attached at index 0, so the last one
-      // first -- then the boundary events)
-      std::vector<int> errs;
-      for (auto e = el.esps.rbegin(); e != el.esps.rend(); ++e)
-        if (P(inst.value.proc).els[P(inst.value.proc).els[*e].start].event == ZBHIP_EV_ERROR)
-          errs.push_back(P(inst.value.proc).els[*e].start);
-      for (int b : el.boundaries)
-        if (P(inst.value.proc).els[b].event == ZBHIP_EV_ERROR) errs.push_back(b);
-      auto signed_less = [](const std::string& x, const std::string& y) {
-        for (size_t i = 0; i < x.size() && i < y.size(); ++i)
-          if ((int8_t)x[i] != (int8_t)y[i]) return (int8_t)x[i] < (int8_t)y[i];
-        return x.size() < y.size();
-      };
-      std::stable_sort(errs.begin(), errs.end(), [&](int x, int y) {
-        return signed_less(P(inst.value.proc).els[y].error_code, P(inst.value.proc).els[x].error_code);
-      });
-      for (int b : errs) {
-        const std::string& bc = P(inst.value.proc).els[b].error_code;
-        avail.push_back(bc);
-        if (bc.empty() || bc == code) {
-          catch_elem = b;
-          scope = inst.key;
-          break;
-        }
-      }
-      if (catch_elem >= 0) break;
-      it = ei_.find(inst.parentKey);
-    }
+    find_error_catch_event(code, scope, avail, catch_elem);
     auto put = [&](const char* elem_marker) {  // JOB:ERROR_THROWN with the stored job + the command's fields
       ORecord& rec = append(ZBHIP_RT_EVENT, ZBHIP_VT_JOB, ZBHIP_JOB_ERROR_THROWN, jobKey);
       rec.r.process_idx = job.pi.proc;
@@ -3430,6 +3408,107 @@ class Oracle {
       return;
     }
     pi_command(scope, ZBHIP_PI_TERMINATE_ELEMENT, task.value);
+  }
+
+  // CatchEventAnalyzer.findErrorCatchEvent (:55-160): from the instance `scope` through its active flow
+  // scopes not interrupted by an event sub-process (ElementInstance.isInterrupted); every error code visited
+  // joins `avail`; on a match `catch_elem` is the catch event and `scope` the instance it belongs to
+  void find_error_catch_event(const std::string& code, int64_t& scope, std::vector<std::string>& avail,
+                              int& catch_elem) {
+    catch_elem = -1;
+    for (auto it = ei_.find(scope); it != ei_.end() && catch_elem < 0;) {
+      const ElementInstance& inst = it->second;
+      if (!(inst.state == ZBHIP_PI_ELEMENT_ACTIVATING || inst.state == ZBHIP_PI_ELEMENT_ACTIVATED) ||
+          inst.interrupting_elem >= 0)
+        break;
+
+      const OEl& el = E(inst.value);
+      // findErrorCatchEventInScope: the element's error catch events ordered by errorCode, descending
+      // (ERROR_CODE_COMPARATOR: DirectBuffer.compareTo -- signed bytes, then length -- reversed; a
+      // stable sort), each visited code joining the available ones until the first match
+      // (getEvents: the event sub-processes' start events -- each attached at index 0, so the last one
+      // first -- then the boundary events)
+      std::vector<int> errs;
+      for (auto e = el.esps.rbegin(); e != el.esps.rend(); ++e)
+        if (P(inst.value.proc).els[P(inst.value.proc).els[*e].start].event == ZBHIP_EV_ERROR)
+          errs.push_back(P(inst.value.proc).els[*e].start);
+      for (int b : el.boundaries)
+        if (P(inst.value.proc).els[b].event == ZBHIP_EV_ERROR) errs.push_back(b);
+      auto signed_less = [](const std::string& x, const std::string& y) {
+        for (size_t i = 0; i < x.size() && i < y.size(); ++i)
+          if ((int8_t)x[i] != (int8_t)y[i]) return (int8_t)x[i] < (int8_t)y[i];
+        return x.size() < y.size();
+      };
+      std::stable_sort(errs.begin(), errs.end(), [&](int x, int y) {
+        return signed_less(P(inst.value.proc).els[y].error_code, P(inst.value.proc).els[x].error_code);
+      });
+      for (int b : errs) {
+        const std::string& bc = P(inst.value.proc).els[b].error_code;
+        avail.push_back(bc);
+        if (bc.empty() || bc == code) {
+          catch_elem = b;
+          scope = inst.key;
+          break;
+        }
+      }
+      if (catch_elem >= 0) break;
+      it = ei_.find(inst.parentKey);
+    }
+  }
+
+  // EndEventProcessor.ErrorEndEventBehavior.onActivate (:143-158): the catch event from the end event's
+  // flow scope up (BpmnEventPublicationBehavior.findErrorCatchEvent) -> ACTIVATED, then throwErrorEvent
+  // (canTriggerElement -> EventHandle.activateElement without variables: PROCESS_EVENT:TRIGGERING, then the
+  // event sub-process's trigger or TERMINATE_ELEMENT of the boundary event's activity); none -> an
+  // UNHANDLED_ERROR_EVENT incident on the end event (ACTIVATING), its message without an error message
+  void throw_error_end_event(const OEl& el, int64_t key, const PiValue& v) {
+    std::vector<std::string> avail;
+    int catch_elem = -1;
+    int64_t scope = v.flowScopeKey;
+    find_error_catch_event(el.error_code, scope, avail, catch_elem);
+    if (catch_elem < 0) {
+      std::string text = "Expected to throw an error event with the code '" + el.error_code + "', but it was not caught.";
+      if (avail.empty()) {
+        text += " No error events are available in the scope.";
+      } else {
+        text += " Available error events are [";
+        for (size_t i = 0; i < avail.size(); ++i) text += (i ? ", " : "") + avail[i];
+        text += "]";
+      }
+      const int64_t ik = next_key();
+      ORecord& in = append(ZBHIP_RT_EVENT, ZBHIP_VT_INCIDENT, ZBHIP_INCIDENT_CREATED, ik);
+      in.r.process_idx = v.proc;
+      in.r.element_idx = v.elem;
+      in.r.scope_key = key;
+      in.r.process_instance_key = v.piKey;
+      in.r.partition = ZBHIP_ERR_UNHANDLED_ERROR_EVENT;
+      in.r.aux = -1;  // jobKey
+      in.r.correlation_key = intern_string(text);
+      IncidentRow row;
+      row.pi = v;
+      row.eik = key;
+      row.error_type = ZBHIP_ERR_UNHANDLED_ERROR_EVENT;
+      row.message = text;
+      incidents_[ik] = row;
+      incident_pi_[key] = ik;
+      return;
+    }
+    pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
+    if (!can_trigger(scope, catch_elem, v.proc)) return;
+    const ElementInstance target = ei_.at(scope);
+    const int64_t eventKey = next_key();
+    ORecord& pe = append(ZBHIP_RT_EVENT, ZBHIP_VT_PROCESS_EVENT, ZBHIP_PE_TRIGGERING, eventKey);
+    pe.r.process_idx = target.value.proc;
+    pe.r.element_idx = catch_elem;
+    pe.r.scope_key = scope;
+    pe.r.process_instance_key = target.value.piKey;
+    pe.r.aux = -1;
+    trigger_event(scope, eventKey, catch_elem, target.value.proc, Doc{}, target.value.piKey);
+    if (P(target.value.proc).els[catch_elem].type == ZBHIP_EL_START_EVENT) {
+      trigger_event_sub_process(catch_elem, scope);
+      return;
+    }
+    pi_command(scope, ZBHIP_PI_TERMINATE_ELEMENT, target.value);
   }
 
   // EventTriggerBehavior.triggerEventSubProcess (common/EventTriggerBehavior.java:74-118): discarded when
@@ -3922,6 +4001,10 @@ class Oracle {
         pi_command(key, ZBHIP_PI_COMPLETE_ELEMENT, v);
         break;
       case ZBHIP_EL_END_EVENT:  // EndEventProcessor.NoneEndEventBehavior.onActivate (processing/bpmn/event/EndEventProcessor.java:110-134)
+        if (el.event == ZBHIP_EV_ERROR) {
+          throw_error_end_event(el, key, v);
+          break;
+        }
         pi_event(key, ZBHIP_PI_ELEMENT_ACTIVATED, v);
         pi_event(key, ZBHIP_PI_ELEMENT_COMPLETING, v);
         complete_and_take(el, key, v, /*output_mappings=*/true);
@@ -4103,6 +4186,15 @@ class Oracle {
         rec.r.partition = -1;   // index: from the first child
         rec.pi = v;
       }
+      return;
+    }
+    if (el.type == ZBHIP_EL_END_EVENT) {
+      // EndEventProcessor.onTerminate (:92-101): an error end event that threw (ACTIVATED) -- resolveIncidents
+      // (none: an uncaught one stays ACTIVATING with its incident, outside this restatement),
+      // transitionToTerminated, onElementTerminated
+      if (incident_pi_.count(key)) throw Unsupported{"terminating an end event with an incident"};
+      pi_event(key, ZBHIP_PI_ELEMENT_TERMINATED, v);
+      child_terminated(v);
       return;
     }
     if (el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT) {

@@ -84,3 +84,43 @@ def test_random_processes_with_event_sub_processes(seed):
     random_error_campaign(seed, ref, lambda *r: write(ref, gpu, *r), xml)
     check(ref, gpu)
     assert gpu.parts[0].adapter.counts["device_commands"] >= 24 and not gpu.parts[0].adapter.fallback_reasons
+
+
+def end_event_processes():
+    # an error end event inside a sub-process caught by the sub-process's boundary event; one caught by the
+    # process's event sub-process; an uncaught one (an incident on the end event)
+    a = bpmn.createExecutableProcess("endBoundary").startEvent().subProcess("sub").startEvent("ss")
+    a.serviceTask("work", "work").endEvent("throw").error("E").subProcessDone()
+    a = a.boundaryEvent("caught").error("E").endEvent("caught-end").moveToActivity("sub").endEvent("end").done()
+    b = bpmn.createExecutableProcess("endEsp")
+    b.eventSubProcess("esp").startEvent("esp-start").error("E").serviceTask("recover", "recover").endEvent("esp-end")
+    b = b.eventSubProcessDone().startEvent("s").serviceTask("work", "work").endEvent("throw").error("E").done()
+    c = bpmn.createExecutableProcess("endUncaught").startEvent().serviceTask("work", "work").endEvent("throw").error("X").done()
+    return a, b, c
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_error_end_events_in_the_processing_loop(limit):
+    # the job completion that reaches an error end event hands the instance to the engine (the device
+    # declines the command before any record), which throws the error: caught by a boundary event, by an
+    # event sub-process, or an UNHANDLED_ERROR_EVENT incident on the end event
+    a, b, c = end_event_processes()
+    deps = [(a, KEY_A, 1), (b, KEY_B, 1), (c, KEY_C, 1)]
+    ref, gpu = single(deps, deps, limit=limit)
+    write(ref, gpu, *([Client.create("endBoundary") for _ in range(3)] + [Client.create("endEsp") for _ in range(3)] +
+                      [Client.create("endUncaught") for _ in range(2)]))
+    ad = gpu.parts[0].adapter
+    assert ad.counts["device_commands"] >= 8
+    for _ in range(3):
+        live = sorted(open_jobs(ref.parts[0].log))
+        if not live:
+            break
+        write(ref, gpu, *[Client.complete_job(k) for k in live])
+    check(ref, gpu)
+    log = gpu.parts[0].log.entries
+    done = [r.value["elementId"] for r in log if r.value_type == abi.VT_PROCESS_INSTANCE
+            and r.intent == abi.PI_ELEMENT_COMPLETED]
+    assert done.count("caught") == 3 and done.count("esp") == 3
+    inc = [r for r in log if r.value_type == abi.VT_INCIDENT and r.intent == abi.INCIDENT_CREATED]
+    assert len(inc) == 2 and all(r.value["elementId"] == "throw" for r in inc)
+    assert ad.fallback_reasons and set(ad.fallback_reasons) == {"unsupported"}

@@ -142,3 +142,72 @@ def test_parallel_branches_are_terminated():
     write(cl, Client.complete_job(rec[0].key))
     assert pi_of(cl, pik)[-1] == ("PROCESS", "ELEMENT_COMPLETED")
     assert [r for r in cl.parts[0].state() if not r.startswith("KEY|")] == []
+
+
+def test_error_end_event_caught_by_a_sub_process_boundary_event():
+    # ErrorEventTest.shouldThrowErrorOnEndEvent (:618-656)
+    b = bpmn.createExecutableProcess("wf").startEvent().subProcess("subProcess").startEvent()
+    b.endEvent("throw-error").error(ERROR_CODE).subProcessDone()
+    xml = b.boundaryEvent("catch-error").error(ERROR_CODE).endEvent("end-error").moveToActivity("subProcess").endEvent("end").done()
+    cl = cluster((xml, KEY_A, 1))
+    e = write(cl, Client.create("wf"))
+    pik = e[-1].value["processInstanceKey"] if e[-1].value_type == abi.VT_PROCESS_INSTANCE else \
+        of(e, abi.VT_PROCESS_INSTANCE, abi.PI_ELEMENT_ACTIVATED)[0].value["processInstanceKey"]
+    events = [(t, i) for t, i in pi_of(cl, pik) if not i.endswith("_ELEMENT") and i != "SEQUENCE_FLOW_TAKEN"]
+    assert subsequence(events, [
+        ("END_EVENT", "ELEMENT_ACTIVATED"), ("SUB_PROCESS", "ELEMENT_TERMINATING"), ("END_EVENT", "ELEMENT_TERMINATING"),
+        ("END_EVENT", "ELEMENT_TERMINATED"), ("SUB_PROCESS", "ELEMENT_TERMINATED"), ("BOUNDARY_EVENT", "ELEMENT_ACTIVATING"),
+        ("BOUNDARY_EVENT", "ELEMENT_COMPLETED"), ("PROCESS", "ELEMENT_COMPLETED")])
+
+
+def test_uncaught_error_end_event_raises_an_incident():
+    # ErrorEventIncidentTest.shouldCreateIncidentOnErrorEndEvent (:264-297): on the end event itself
+    xml = bpmn.createExecutableProcess("wf").startEvent().endEvent("error").error("error").done()
+    cl = cluster((xml, KEY_A, 1))
+    e = write(cl, Client.create("wf"))
+    inc = of(e, abi.VT_INCIDENT, abi.INCIDENT_CREATED)[0].value
+    # (the reference takes the first END_EVENT record, the ACTIVATE_ELEMENT command: the same key)
+    end = [r for r in e if r.value_type == abi.VT_PROCESS_INSTANCE and r.value["bpmnElementType"] == "END_EVENT"
+           and r.record_type == abi.RT_EVENT][-1]
+    assert inc["errorType"] == "UNHANDLED_ERROR_EVENT" and inc["errorMessage"] == (
+        "Expected to throw an error event with the code 'error', but it was not caught. "
+        "No error events are available in the scope.")
+    assert (inc["elementId"], inc["elementInstanceKey"], inc["variableScopeKey"], inc["jobKey"]) == \
+        ("error", end.key, end.key, -1)
+    assert abi.PI_INTENTS[end.intent] == "ELEMENT_ACTIVATING"
+
+
+def test_error_inside_a_triggered_event_sub_process_is_not_caught_by_its_container():
+    # ErrorEventIncidentTest.shouldCreateIncidentIfErrorIsThrownFromInterruptingEventSubprocess (:190-228): the
+    # interrupted process is not searched
+    b = bpmn.createExecutableProcess("wf")
+    b.eventSubProcess("error").startEvent("error-start").error(ERROR_CODE).serviceTask("task-in-subprocess", JOB_TYPE)
+    b.endEvent("esp-end").eventSubProcessDone()
+    xml = b.startEvent("start").serviceTask("task", JOB_TYPE).endEvent("end").done()
+    cl = cluster((xml, KEY_A, 1))
+    job, pik = started(cl, None)
+    e = write(cl, Client.throw_error(job.key, ERROR_CODE))
+    inner = of(e, abi.VT_JOB, abi.JOB_CREATED)[0]
+    assert inner.value["elementId"] == "task-in-subprocess"
+    e = write(cl, Client.throw_error(inner.key, ERROR_CODE))
+    inc = of(e, abi.VT_INCIDENT, abi.INCIDENT_CREATED)[0].value
+    assert inc["errorType"] == "UNHANDLED_ERROR_EVENT" and inc["elementId"] == "NO_CATCH_EVENT_FOUND"
+    assert inc["errorMessage"] == ("Expected to throw an error event with the code '%s', but it was not caught. "
+                                   "No error events are available in the scope." % ERROR_CODE)
+
+
+def test_error_end_event_caught_by_an_event_sub_process():
+    # an error end event inside a sub-process, caught by the process's event sub-process: the process's
+    # children terminate (the sub-process with its end event), then the event sub-process runs
+    b = bpmn.createExecutableProcess("wf")
+    b.eventSubProcess("esp").startEvent("esp-start").error("E").endEvent("esp-end").eventSubProcessDone()
+    b.startEvent("start").subProcess("sub").startEvent("ss").endEvent("throw").error("E").subProcessDone()
+    xml = b.endEvent("end").done()
+    cl = cluster((xml, KEY_A, 1))
+    write(cl, Client.create("wf"))
+    ids = [(r.value["elementId"], abi.PI_INTENTS[r.intent]) for r in cl.parts[0].log.entries
+           if r.value_type == abi.VT_PROCESS_INSTANCE]
+    assert subsequence(ids, [("throw", "ELEMENT_ACTIVATED"), ("sub", "ELEMENT_TERMINATING"), ("throw", "ELEMENT_TERMINATED"),
+                             ("sub", "ELEMENT_TERMINATED"), ("esp", "ELEMENT_ACTIVATING"), ("esp-end", "ELEMENT_COMPLETED"),
+                             ("esp", "ELEMENT_COMPLETED"), ("wf", "ELEMENT_COMPLETED")])
+    assert [r for r in cl.parts[0].state() if not r.startswith("KEY|")] == []

@@ -331,6 +331,10 @@ class ProcessBuilder:
                     out.append('%s<intermediateCatchEvent id=%s><messageEventDefinition id=%s messageRef=%s/>'
                                '</intermediateCatchEvent>' % (ind, quoteattr(c.id), quoteattr(c.id + "_med"),
                                                               quoteattr(c.message[0])))
+                elif c.kind == "endEvent" and getattr(c, "error", None) is not None:
+                    errors.append(c)  # EndEventBuilder.error(code): an error end event (a code is required)
+                    out.append('%s<endEvent id=%s><errorEventDefinition id=%s errorRef=%s/></endEvent>'
+                               % (ind, quoteattr(c.id), quoteattr(c.id + "_eed"), quoteattr("Error_" + c.id)))
                 elif c.kind == "startEvent" and getattr(c, "error", None) is not None:
                     ref = ' errorRef=%s' % quoteattr("Error_" + c.id) if c.error else ""
                     if c.error:

@@ -875,6 +875,25 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         e.event_type = ZBHIP_EV_ERROR;
         e.message_name = C.str(code);
         e.job_retries = 1;
+      } else if (type == ZBHIP_EL_END_EVENT && c.first("errorEventDefinition")) {
+        // an error end event (EndEventTransformer.java:70-83): a static errorCode in message_name; the
+        // device never activates it (the command reaching it hands the instance to the engine)
+        const Elem* eed = c.first("errorEventDefinition");
+        for (auto& d : c.children)
+          if (&d != eed && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {
+            err = "event definition <" + d.tag + "> outside the supported subset";
+            return ZBHIP_EUNSUPP;
+          }
+        const std::string* ref = eed->get("errorRef");
+        auto ei = ref ? errors.find(*ref) : errors.end();
+        if (ei == errors.end() || ei->second.empty() || ei->second[0] == '=') {
+          err = "error end event outside the supported subset (a static errorCode)";
+          return ZBHIP_EUNSUPP;
+        }
+        if (const Elem* ext = c.first("extensionElements"))
+          if (ext->first("ioMapping")) { err = "io mappings outside the supported subset"; return ZBHIP_EUNSUPP; }
+        e.event_type = ZBHIP_EV_ERROR;
+        e.message_name = C.str(ei->second);
       } else if (type == ZBHIP_EL_START_EVENT || type == ZBHIP_EL_END_EVENT) {
         for (auto& d : c.children)
           if (d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) {

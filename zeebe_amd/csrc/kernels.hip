@@ -2069,6 +2069,9 @@ __device__ __forceinline__ void process_pi(Lane<K>& L, uint32_t entry) {
       return;
     }
     if (cmd_key != NONE && tbl_find(L, cmd_key) >= 0) { set_fail(L, FB_UNSUPPORTED); return; }
+    // an error end event (EndEventProcessor.ErrorEndEventBehavior): its error is thrown by the engine -- the
+    // command that reaches it hands the instance off
+    if (type == ZBHIP_EL_END_EVENT && ((w.x >> 8) & 0xFF) == ZBHIP_EV_ERROR) { set_fail(L, FB_UNSUPPORTED); return; }
     const uint32_t key = cmd_key == NONE ? new_key(L) : cmd_key;
     emit(L, ZBHIP_PI_ELEMENT_ACTIVATING, key, fsa, elem);
     apply_activating_child(L, elem, w, key);
