@@ -1026,7 +1026,10 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
     // CatchEventAnalyzer's walk through the flow scopes of a job's task)
     const bool sub_ok = a.type == ZBHIP_EL_SUB_PROCESS &&
                         (P.els[b].event == ZBHIP_EV_TIMER || P.els[b].event == ZBHIP_EV_ERROR);
-    if ((!ZBHIP_IS_JOB_WORKER(a.type) && !sub_ok) || a.scope != P.els[b].scope) {
+    // (an error boundary event of a multi-instance activity attaches to its body, MultiInstanceActivity
+    // Transformer: the body takes the activity's id)
+    const bool body_ok = a.type == ZBHIP_EL_MULTI_INSTANCE_BODY && P.els[b].event == ZBHIP_EV_ERROR;
+    if ((!ZBHIP_IS_JOB_WORKER(a.type) && !sub_ok && !body_ok) || a.scope != P.els[b].scope) {
       err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return false;
     }
@@ -4611,7 +4614,8 @@ class Oracle {
         // createEventScope (:255-289): job worker elements get an event scope
         // (a sub-process only with events: its boundary event)
         if (ZBHIP_IS_JOB_WORKER(el.type) || el.type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
-            el.type == ZBHIP_EL_BOUNDARY_EVENT || (el.type == ZBHIP_EL_SUB_PROCESS && el.boundary >= 0) ||
+            el.type == ZBHIP_EL_BOUNDARY_EVENT ||
+            ((el.type == ZBHIP_EL_SUB_PROCESS || el.type == ZBHIP_EL_MULTI_INSTANCE_BODY) && el.boundary >= 0) ||
             ((el.type == ZBHIP_EL_PROCESS || el.type == ZBHIP_EL_SUB_PROCESS) && !el.esps.empty()))
           event_scope_.insert(key);
         // cleanupSequenceFlowsTaken (:79-98): Tetris decrement of (flowScope, gateway)

@@ -149,3 +149,36 @@ def test_several_boundary_events_on_one_task_in_the_processing_loop(limit):
     assert sorted(caught) == ["catch-all", "code-specific"] + ["timer"] * 5
     ad = gpu.parts[0].adapter
     assert len(ad.handed_off) == 2 and not ad.fallback_reasons
+
+
+@pytest.mark.parametrize("limit", [3, 100])
+def test_error_boundary_events_on_multi_instance_activities_in_the_processing_loop(limit):
+    # an error boundary event of a multi-instance task attaches to its body (ErrorCatchEventTest "boundary event
+    # on multi-instance service task"): parallel and sequential bodies; a throw terminates the body with its
+    # other inner instances (their jobs canceled) and activates the boundary event
+    par = (bpmn.createExecutableProcess("par").startEvent().serviceTask("task", "work").multiInstance("= [1, 2, 3]", "x")
+           .boundaryEvent("caught").error("E").endEvent("ce").moveToActivity("task").endEvent("end").done())
+    seq = (bpmn.createExecutableProcess("seq").startEvent().serviceTask("task", "work").multiInstance("= [1, 2]", "x", True)
+           .boundaryEvent("caught").error().endEvent("ce").moveToActivity("task").endEvent("end").done())
+    deps = [(par, KEY_A, 1), (seq, KEY_B, 1)]
+    ref, gpu = single(deps, deps, limit=limit)
+    write(ref, gpu, *([Client.create("par") for _ in range(4)] + [Client.create("seq") for _ in range(4)]))
+    by = {}
+    for k, r in open_jobs(ref.parts[0].log).items():
+        by.setdefault(r.value["processInstanceKey"], []).append(k)
+    inst = [sorted(by[p]) for p in sorted(by)]
+    write(ref, gpu, Client.throw_error(inst[0][1], "E", "", variables=(("why", "x"),)), Client.throw_error(inst[1][0], "Z"),
+          Client.complete_job(inst[2][0]), Client.throw_error(inst[4][0], "any"), Client.complete_job(inst[5][0]))
+    for _ in range(4):
+        dead = {r.key for r in ref.parts[0].log.entries if r.value_type == abi.VT_JOB and r.intent == abi.JOB_ERROR_THROWN}
+        live = sorted(k for k in open_jobs(ref.parts[0].log) if k not in dead)
+        if not live:
+            break
+        write(ref, gpu, *[Client.complete_job(k) for k in live])
+    check(ref, gpu)
+    log = gpu.parts[0].log.entries
+    done = [r.value["elementId"] for r in log if r.value_type == abi.VT_PROCESS_INSTANCE
+            and r.intent == abi.PI_ELEMENT_COMPLETED]
+    assert done.count("caught") == 2
+    assert [r for r in log if r.value_type == abi.VT_JOB and r.intent == abi.JOB_CANCELED]
+    assert not gpu.parts[0].adapter.fallback_reasons

@@ -274,3 +274,25 @@ def test_error_boundary_events_beside_a_timer_boundary_event():
     assert of(e, abi.VT_TIMER, abi.TIMER_CANCELED)
     assert set(boundary_path(cl, pik)) == {"error-2"}
     assert not [r for r in cl.parts[0].state() if r.startswith(("TIMERS|", "JOBS|", "EVENT_SCOPE|"))]
+
+
+def test_error_boundary_event_on_a_multi_instance_task():
+    # ErrorCatchEventTest["boundary event on multi-instance service task"] (:103-116): the boundary event
+    # attaches to the body; shouldTriggerEvent's subsequence (:191-218) and shouldThrowErrorWithVariables
+    # (:220-273: the variable local to the boundary event)
+    b = bpmn.createExecutableProcess("wf").startEvent().serviceTask("task", JOB_TYPE).multiInstance("= [1]")
+    xml = b.boundaryEvent("error-boundary-event").error(ERROR_CODE).endEvent("be").moveToActivity("task").endEvent("end").done()
+    cl = cluster((xml, KEY_A, 1))
+    job, pik = started(cl, None)
+    body = [r for r in cl.parts[0].state() if r.startswith("EVENT_SCOPE|") and "error-boundary-event" in r]
+    assert len(body) == 1
+    e = write(cl, Client.throw_error(job.key, ERROR_CODE, variables=[("foo", "bar")]))
+    ids = [(r.value["elementId"], abi.PI_INTENTS[r.intent]) for r in cl.parts[0].log.entries
+           if r.value_type == abi.VT_PROCESS_INSTANCE and r.value["processInstanceKey"] == pik]
+    assert subsequence(ids, [("task", "ELEMENT_TERMINATING"), ("task", "ELEMENT_TERMINATED"),
+                             ("error-boundary-event", "ELEMENT_ACTIVATING"), ("error-boundary-event", "ELEMENT_COMPLETED"),
+                             ("wf", "ELEMENT_COMPLETED")])
+    bk = [r.key for r in e if r.value_type == abi.VT_PROCESS_INSTANCE and r.intent == abi.PI_ELEMENT_ACTIVATING
+          and r.value["elementId"] == "error-boundary-event"][0]
+    assert [(r.value["name"], r.value["scopeKey"]) for r in e if r.value_type == abi.VT_VARIABLE] == [("foo", bk)]
+    assert [r for r in cl.parts[0].state() if not r.startswith("KEY|")] == []

@@ -1137,6 +1137,13 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
     // keeps it in default_flow: its start_event is its none start event)
     const bool on_sub = A.element_type == ZBHIP_EL_SUB_PROCESS && (C.elements[b].event_type == ZBHIP_EV_TIMER ||
                                                                    C.elements[b].event_type == ZBHIP_EV_ERROR);
+    // (an error boundary event of a multi-instance activity: attached to its body, which keeps no slot for
+    // it -- the runtime finds it by flow_source)
+    if (A.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY && C.elements[b].event_type == ZBHIP_EV_ERROR &&
+        A.flow_scope == C.elements[b].flow_scope) {
+      C.elements[b].flow_source = it->second;
+      continue;
+    }
     if ((!ZBHIP_IS_JOB_WORKER(A.element_type) && !on_sub) || A.flow_scope != C.elements[b].flow_scope) {
       err = "boundary event on an element outside the supported subset (job worker tasks, timers on sub-processes)";
       return ZBHIP_EUNSUPP;

@@ -1446,8 +1446,10 @@ int zbhip_deploy(zbhip_handle* h, const zbhip_process_csr* csr, uint32_t* idx_ou
                           (E.event_type == ZBHIP_EV_TIMER || E.event_type == ZBHIP_EV_ERROR) && A.default_flow == e;
       // (further error boundary events of an activity: outside its slot, found by flow_source)
       const uint16_t slot = A.element_type == ZBHIP_EL_SUB_PROCESS ? A.default_flow : A.start_event;
-      const bool extra_error = E.event_type == ZBHIP_EV_ERROR && slot != ZBHIP_NONE16 && slot < P.els.size() &&
-                               (ZBHIP_IS_JOB_WORKER(A.element_type) || A.element_type == ZBHIP_EL_SUB_PROCESS);
+      const bool extra_error = E.event_type == ZBHIP_EV_ERROR &&
+                               ((slot != ZBHIP_NONE16 && slot < P.els.size() &&
+                                 (ZBHIP_IS_JOB_WORKER(A.element_type) || A.element_type == ZBHIP_EL_SUB_PROCESS)) ||
+                                A.element_type == ZBHIP_EL_MULTI_INSTANCE_BODY);  // (a body: no slot)
       if ((!ZBHIP_IS_JOB_WORKER(A.element_type) || A.start_event != e) && !on_sub && !extra_error) return ZBHIP_EINVAL;
       if (A.flow_scope != E.flow_scope) return ZBHIP_EINVAL;
     } else if (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) {
@@ -4066,16 +4068,20 @@ static void emit_instance(zbhip_handle* h, uint32_t inst, const InstRows& R, zbh
     std::string esp_intr;
     bool has_esp = false;
     if (E.element_type == ZBHIP_EL_SUB_PROCESS) esp_ids(elem, esp_intr, has_esp);
+    bool body_bnd = false;  // a multi-instance body with (error) boundary events: an event scope
+    if (body)
+      for (size_t b = 0; b < P.els.size() && !body_bnd; ++b)
+        body_bnd = P.els[b].element_type == ZBHIP_EL_BOUNDARY_EVENT && P.els[b].flow_source == elem;
     const bool sub_bnd = E.element_type == ZBHIP_EL_SUB_PROCESS && E.default_flow != ZBHIP_NONE16 &&
                          E.default_flow < P.els.size();
     if (ZBHIP_IS_JOB_WORKER(E.element_type) || E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT ||
-        E.element_type == ZBHIP_EL_BOUNDARY_EVENT || sub_bnd || has_esp) {
+        E.element_type == ZBHIP_EL_BOUNDARY_EVENT || sub_bnd || has_esp || body_bnd) {
       // EventScopeInstance.java:25-35: a catch / boundary event's interrupting ids are its own id
       // (ExecutableCatchEventElement.java:124-132), a job worker's (a sub-process's: an event scope
       // only with events) those of its interrupting boundary event, which is also its
       // boundaryElementIds (ExecutableActivity.java:28-38)
       const bool own = E.element_type == ZBHIP_EL_INTERMEDIATE_CATCH_EVENT || E.element_type == ZBHIP_EL_BOUNDARY_EVENT;
-      const bool bnd = (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) || sub_bnd;
+      const bool bnd = (ZBHIP_IS_JOB_WORKER(E.element_type) && E.start_event != ZBHIP_NONE16) || sub_bnd || body_bnd;
       // an activity's boundary events in attach order (element order), the cancelActivity ones interrupting
       std::string ids = own ? P.id(elem) : std::string(), intr_ids = own ? ids : std::string();
       if (bnd)
