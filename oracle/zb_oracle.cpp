@@ -877,11 +877,11 @@ static bool build_process(const XNode& proc, const MessageDefs& msgs, const Erro
       e.interrupting = k->attr("cancelActivity") != "false";
       const XNode* ted = k->child("timerEventDefinition");
       const XNode* td = ted ? ted->child("timeDuration") : nullptr;
-      const XNode* tc = ted && !td && !e.interrupting ? ted->child("timeCycle") : nullptr;
+      const XNode* tc = ted && !td ? ted->child("timeCycle") : nullptr;
       if ((!td && !tc) || k->child("messageEventDefinition") || k->child("errorEventDefinition") ||
           k->child("signalEventDefinition") || k->child("escalationEventDefinition") ||
           k->child("compensateEventDefinition") || k->child("conditionalEventDefinition")) {
-        err = "boundary event outside the supported subset (timer timeDuration, or timeCycle when non-interrupting)";
+        err = "boundary event outside the supported subset (timer timeDuration or timeCycle)";
         return false;
       }
       const TimerValue tv = timer_value(td ? td->text : tc->text, tc != nullptr);

@@ -87,7 +87,23 @@ def _sub_process_multi_instance():
     return b.moveToActivity("sub").endEvent("end").done()
 
 
+def _interrupting_cycle(sub=False):
+    # an interrupting boundary event with a timeCycle (TriggerTimerProcessor.shouldReschedule does not look at
+    # the activity: the next timer is created after the TERMINATE_ELEMENT command and canceled with the
+    # activity); on a task or on a sub-process
+    b = bpmn.createExecutableProcess("process").startEvent("s")
+    if sub:
+        b.subProcess("sub").startEvent("ss").serviceTask("a", "a").endEvent("se").subProcessDone()
+        act = "sub"
+    else:
+        b.serviceTask("a", "a")
+        act = "a"
+    b.boundaryEvent("late").timerWithCycle("R3/PT20S").serviceTask("c", "c").endEvent("ce").moveToActivity(act)
+    return b.endEvent("e").done()
+
+
 SHAPES = {"multiple_sequence_flows": lambda: multiple_sequence_flows("PT30S"), "linear": _linear_with_boundary,
+          "interrupting_cycle": _interrupting_cycle, "interrupting_cycle_sub": lambda: _interrupting_cycle(True),
           "sub_process_multi_instance": _sub_process_multi_instance,
           "sub_process": lambda: sub_process_boundary(True, "PT10S"),
           "sub_process_non_interrupting": lambda: sub_process_boundary(False, "PT10S"),
@@ -175,7 +191,8 @@ def test_gpu_random_processes_with_multi_instance_activities(seed):
 
 
 @pytest.mark.parametrize("shape", ["multiple_sequence_flows", "in_sub_process", "then_catch", "non_interrupting_escalation",
-                                   "cycle_r3", "sub_process", "sub_process_parallel", "nested_sub_processes"])
+                                   "cycle_r3", "sub_process", "sub_process_parallel", "nested_sub_processes",
+                                   "interrupting_cycle", "interrupting_cycle_sub"])
 def test_gpu_boundary_log_and_db_bytes(shape):
     pair = Pair(SHAPES[shape](), 100)
     for e in (pair.part, pair.orc):

@@ -461,3 +461,24 @@ def test_multi_instance_body_terminated_with_its_sub_process():
     assert all(any(x == w for x in it) for w in want), seq  # containsSubsequence
     assert sum(1 for r in recs if r["value_type"] == abi.VT_JOB and r["intent"] == abi.JOB_CANCELED) == 1
     assert [x for x in o.state() if not x.startswith("KEY|")] == []
+
+
+def test_interrupting_cycle_reschedules_then_cancels():
+    # TriggerTimerProcessor.processRecord (:80-114) + shouldReschedule (:128-130): an interrupting boundary
+    # timer with a cycle writes TIMER:TRIGGERED, PROCESS_EVENT:TRIGGERING, the activity's TERMINATE_ELEMENT
+    # and the cycle's next TIMER:CREATED (one repetition fewer, due from the trigger's dueDate); the
+    # termination then cancels that timer (JOB:CANCELED, TIMER:CANCELED) before the boundary event runs
+    from zeebe_amd import bpmn as B
+    b = B.createExecutableProcess("process").startEvent("s").serviceTask("a", "a").boundaryEvent("late")
+    xml = b.timerWithCycle("R3/PT20S").endEvent("ce").moveToActivity("a").endEvent("e").done()
+    o, recs = _started(xml)
+    timers = [r for r in recs if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CREATED]
+    assert len(timers) == 1 and int(timers[0]["partition"]) == 3
+    got = _trigger_all(o, recs)
+    seq = [(int(r["value_type"]), int(r["intent"])) for r in got]
+    created = [i for i, r in enumerate(got) if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CREATED]
+    canceled = [i for i, r in enumerate(got) if r["value_type"] == abi.VT_TIMER and r["intent"] == abi.TIMER_CANCELED]
+    assert len(created) == 1 and len(canceled) == 1 and created[0] < canceled[0]
+    assert int(got[created[0]]["partition"]) == 2 and got[created[0]]["key"] == got[canceled[0]]["key"]
+    assert int(got[canceled[0]]["aux"]) == int(got[created[0]]["aux"])  # the same dueDate
+    assert (abi.VT_JOB, abi.JOB_CANCELED) in seq

@@ -994,11 +994,11 @@ static int compile(const char* xml, size_t len, int64_t def_key, int32_t version
         const Elem* tc = ted && !td ? ted->first("timeCycle") : nullptr;
         for (auto& d : c.children)
           if (&d != ted && d.tag.size() > 15 && d.tag.compare(d.tag.size() - 15, 15, "EventDefinition") == 0) td = tc = nullptr;
-        // a timeCycle (RepeatingInterval.parse "R[n]/duration", or its constant FEEL form) on a
-        // non-interrupting boundary event: repetitions n (1..254) or infinite (255); a duration: 1
+        // a timeCycle (RepeatingInterval.parse "R[n]/duration", or its constant FEEL form): repetitions n
+        // (1..254) or infinite (255); a duration: 1
         uint32_t reps = 1;
-        if (!td && !(tc && !interrupting)) {
-          err = "boundary event outside the supported subset (timer timeDuration, or timeCycle when non-interrupting)";
+        if (!td && !tc) {
+          err = "boundary event outside the supported subset (timer timeDuration or timeCycle)";
           return ZBHIP_EUNSUPP;
         }
         const std::string dtext = td ? td->text : tc->text;

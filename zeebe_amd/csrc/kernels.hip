@@ -1788,6 +1788,16 @@ __device__ __forceinline__ void trigger_timer(Lane<K>& L, uint32_t tord, long lo
     const uint32_t task = tget(L, t).x & 0xFFFF;
     const uint32_t c = scope_of<K>(elem_of(L, task));
     follow_up(L, ZBHIP_PI_TERMINATE_ELEMENT, eord, scope_key(L, c), task, false, c == 0, eord, Q_TERM);
+    // a cycle reschedules here too (shouldReschedule does not look at the activity): TIMER:CREATED after the
+    // TERMINATE_ELEMENT command; the activity's termination cancels that timer again
+    if (reps == 255 || reps > 1) {
+      const uint32_t nr = reps == 255 ? 255u : reps - 1;
+      const uint32_t tk = new_key(L);
+      L.tm_x = elem | (tk << 16);
+      L.tm_y = eord | (nr << 16) | (1u << 31);
+      L.tm_due = next_cycle_due(cmd_due, (long long)bw.z, L.sp->now_ms);
+      emit(L, C_TIMER_NEXT, tk, eord, elem, nr);
+    }
     return;
   }
   const uint32_t c = scope_of<K>(elem_of(L, elem));

@@ -344,12 +344,17 @@ __device__ __forceinline__ bool decode(const LogParams& L, uint32_t c, const Log
     // (a timer created in this batch and canceled in it: the clock plus its duration, as CREATED --
     // cmd_due holds only the dueDate of a timer stored before the batch)
     const bool fresh = c6 == C_TIMER_CANCELED && m.nkeys && key_ord >= m.first_ord && key_ord < (uint32_t)m.first_ord + m.nkeys;
+    bool next = c6 == C_TIMER_NEXT;
     if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT || fresh) {
       const uint32_t pb = r.proc != NONE ? proc_block(L, r.proc) : 0u;
       if (!pb || elem >= L.idx[pb + 5]) return false;
-      dur = (long long)el_run(L, pb, elem, E_DUR).x;
+      const uint2 d = el_run(L, pb, elem, E_DUR);
+      dur = (long long)d.x;
+      // (a fresh cancel of an interrupting boundary cycle's next timer: only a TIMER:TRIGGER batch -- a
+      // nonzero command dueDate -- reschedules one; due as its CREATED)
+      if (fresh && d.y && cmd != 0) next = true;
     }
-    r.due = c6 == C_TIMER_CREATED || fresh ? L.now_ms + dur : c6 == C_TIMER_NEXT ? next_cycle_due(cmd, dur, L.now_ms)
+    r.due = next ? next_cycle_due(cmd, dur, L.now_ms) : c6 == C_TIMER_CREATED || fresh ? L.now_ms + dur
             : c6 == C_TIMER_CANCELED ? L.cmd_due[c] : cmd;
     r.reps = rej ? 1 : fl == 255 ? -1 : (int)fl;
   } else if (c6 == C_PIC_CREATED) {

@@ -109,6 +109,7 @@ struct SerElement {
   uint8_t type = 0, event = 0;
   std::string id;
   uint32_t duration_ms = 0;  // timer catch / boundary event (the device log path's TIMER dueDates)
+  uint32_t interrupting_cycle = 0;  // an interrupting boundary event's timeCycle (its next timer, E_DUR .y)
   std::string cond_text;     // sequence flow: its condition's FEEL text (incident messages)
   // ProcessInstanceRecord: [map, bpmnElementType .. processDefinitionKey, "processInstanceKey"] key
   // ["flowScopeKey"] key [bpmnEventType .. tenantId]
@@ -208,6 +209,8 @@ int zbhip_serializer_deploy(zbhip_serializer* s, const zbhip_process_csr* csr, u
     S.event = E.element_type == ZBHIP_EL_PROCESS ? ZBHIP_EV_UNSPECIFIED : E.event_type;
     S.id = str(E.id);
     S.duration_ms = E.duration_ms;
+    S.interrupting_cycle = E.element_type == ZBHIP_EL_BOUNDARY_EVENT && E.event_type == ZBHIP_EV_TIMER &&
+                           (E.job_retries & 1) && (E.job_retries >> 8) != 1;
     if (E.element_type == ZBHIP_EL_SEQUENCE_FLOW && E.condition != ZBHIP_NONE16 && csr->cond_text &&
         E.condition < csr->n_conditions && csr->cond_text[E.condition])
       S.cond_text = csr->cond_text[E.condition];
@@ -1681,7 +1684,7 @@ int log_device_tables(const zbhip_serializer* s, std::vector<uint8_t>& arena, st
       push(E.id);
       push(E.job_head.empty() ? Bytes() : E.job_head.substr(E.job_rest));  // E_JOB_REST
       idx.push_back(E.duration_ms);  // E_DUR: not a byte run, the element's timer duration
-      idx.push_back(0);
+      idx.push_back(E.interrupting_cycle);  // (and whether it is an interrupting boundary event's cycle)
     }
   }
   while (arena.size() % 4) arena.push_back(0);

@@ -3275,7 +3275,15 @@ static int expand_plain(const zbhip_handle* h, size_t c, uint32_t inst, uint2 w,
         // CREATED); cmd_due holds only the dueDate of a timer stored before the batch
         const uint32_t first = h->h_hdr[c].y & 0xFFFF, nkeys = h->h_hdr[c].x >> 16;
         const zbhip_element* E = proc != NONE && elem < h->procs[proc].els.size() ? &h->procs[proc].els[elem] : nullptr;
-        if (E && nkeys && key_ord >= first && key_ord < first + nkeys) r.aux = h->run_clock_ms + (int64_t)E->duration_ms;
+        if (E && nkeys && key_ord >= first && key_ord < first + nkeys) {
+          // (an interrupting boundary event's cycle: the next timer TIMER:TRIGGER rescheduled before the
+          // activity's termination canceled it -- due from the command's dueDate, as its CREATED)
+          const bool next = cm.kind == ZBHIP_CMD_TIMER_TRIGGER && E->element_type == ZBHIP_EL_BOUNDARY_EVENT &&
+                            (E->job_retries & 1) && (E->job_retries >> 8) != 1;
+          const int64_t cmd_due = (int64_t)((uint64_t)cm.doc_begin | ((uint64_t)cm.pad << 32));
+          r.aux = next ? next_cycle_due(cmd_due, (int64_t)E->duration_ms, h->run_clock_ms)
+                       : h->run_clock_ms + (int64_t)E->duration_ms;
+        }
       }
       r.partition = fl == 255 ? -1 : (int32_t)fl;  // TimerRecord.repetitions
     } else if (c6 == C_TIMER_CREATED || c6 == C_TIMER_NEXT || c6 == C_TIMER_TRIGGERED || c6 == C_TIMER_TRIGGER) {
