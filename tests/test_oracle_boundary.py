@@ -249,7 +249,7 @@ def test_boundary_model_subset():
         ids = [c.id(i) for i in range(len(c.els))]
         assert int(c.els[ids.index("b")]["job_retries"]) == reps << 8, cycle
         Oracle().deploy(_boundary_model(' cancelActivity="false"', _cycle(cycle)))
-    for xml in (_boundary_model("", _cycle("R/PT1S")), _boundary_model(' cancelActivity="false"', _cycle("R0/PT1S")),
+    for xml in (_boundary_model(' cancelActivity="false"', _cycle("R0/PT1S")),
                 _boundary_model(' cancelActivity="false"', _cycle("R255/PT1S")),
                 _boundary_model(' cancelActivity="false"', _cycle("R/2024-01-01T00:00:00Z/PT1S"))):
         with pytest.raises(ZbhipError):
