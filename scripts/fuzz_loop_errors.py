@@ -2,8 +2,9 @@
 with error boundary events and, in the second flavour, error-start event sub-processes, driven through
 the platform's processing loop twice -- the engine alone and [adapter, engine] -- by
 tests/test_gpu_error_events.py's campaign (complete, leave or throw E1 / E2 / E3 per open job each
-round).  A seed passes when every record and the state agree after every write.  Batch limits alternate
-between 100 and 3 by seed.  Usage: python scripts/fuzz_loop_errors.py FIRST LAST"""
+round); with --documents, processes without error events whose jobs complete with documents of zero to
+three entries (tests/test_gpu_documents.py's campaign: the multi-entry merge order).  A seed passes when every record and the state agree after every write.  Batch limits alternate
+between 100 and 3 by seed.  Usage: python scripts/fuzz_loop_errors.py FIRST LAST [--documents]"""
 import os
 import sys
 import time
@@ -14,6 +15,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 
 import numpy as np  # noqa: E402
 from random_bpmn import random_process  # noqa: E402
+from test_gpu_documents import random_document_campaign  # noqa: E402
 from test_gpu_error_events import random_error_campaign  # noqa: E402
 from test_gpu_scheduled import KEY_A, single, write  # noqa: E402
 
@@ -28,16 +30,26 @@ def run(seed, esp):
     return thrown, ad.counts["device_commands"], sorted(set(ad.fallback_reasons))
 
 
+def run_documents(seed):
+    xml = random_process(np.random.default_rng(9500 + seed), sub_processes=True, task_kinds=True)
+    deps = [(xml, KEY_A, 1)]
+    ref, gpu = single(deps, deps, limit=3 if seed % 2 else 100)
+    random_document_campaign(seed, ref, lambda *r: write(ref, gpu, *r))
+    ad = gpu.parts[0].adapter
+    return 0, ad.counts["device_commands"], sorted(set(ad.fallback_reasons))
+
+
 def main():
     first, last = int(sys.argv[1]), int(sys.argv[2])
+    docs = "--documents" in sys.argv[3:]
     t0 = time.time()
     passed = failed = thrown = dev = 0
     declined = {}
     for seed in range(first, last):
-        for esp in (False, True):
-            tag = "%d/%s" % (seed, "esp" if esp else "boundary")
+        for esp in ((None,) if docs else (False, True)):
+            tag = "%d/%s" % (seed, "documents" if docs else "esp" if esp else "boundary")
             try:
-                t, d, reasons = run(seed, esp)
+                t, d, reasons = run_documents(seed) if docs else run(seed, esp)
             except Exception:  # a parity difference (check's AssertionError) or a crash
                 failed += 1
                 print("FAIL", tag, traceback.format_exc().splitlines()[-1][:400], flush=True)
