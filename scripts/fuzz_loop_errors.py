@@ -55,6 +55,8 @@ def main():
                 print("FAIL", tag, traceback.format_exc().splitlines()[-1][:400], flush=True)
                 continue
             passed += 1
+            if reasons:
+                print("FALLBACK", tag, reasons, flush=True)
             thrown += t
             dev += d
             for r in reasons:
