@@ -5,7 +5,7 @@
 # gpurun_out/r06/final; scripts/pmc_traffic.py summarises the PMC passes afterwards (on the CPU side).
 set -e
 cd "$(dirname "$0")/.."
-O=gpurun_out/r06/final
+O=${OUT:-gpurun_out/r06/final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err
